@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): encoded FPS + p50 end-to-end latency of a
+1080p60 H.264 desktop session per MI355X; concurrent sessions/node.
+
+One process per GPU (torchrun / torch.distributed over RCCL for N > 1).  Each rank runs
+one 1920x1080 session of the flagship pipeline on its GPU:
+
+    HIP synthetic desktop render (animated noise + gears + scrolling text + moving window,
+    frame-id/timestamp barcode) -> BT.709 NV12 (HIP) -> H.264 encode (HIP: ME, transform,
+    quant, recon, CAVLC, bit packing) -> Annex-B access unit in host memory
+
+A "step" is one encoded frame.  Frames are encoded back-to-back (unpaced) to measure the
+encoder's capacity; E2E latency is render-start -> access unit available on the host, per
+frame.  `value` is the whole-job aggregate encoded FPS (sum over GPUs, total frames /
+slowest rank's time).  Weak scaling: per-GPU work is fixed as N grows.
+
+The reference publishes no numbers, so vs_baseline is null; the reference's
+operating point (60 encoded FPS per session, one session per GPU) is reported as
+`vs_operating_point` = value / (60 * N).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--fps", type=int, default=60)
+    ap.add_argument("--bitrate-kbps", type=int, default=8000)
+    ap.add_argument("--search-range", type=int, default=16)
+    ap.add_argument("--subpel", type=int, default=1)
+    ap.add_argument("--json-out", type=str, default="")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(local_rank)
+
+    import mxdesk
+
+    N = mxdesk.native()
+    N.set_device(local_rank)
+    cfg = N.SessionConfig()
+    cfg.width, cfg.height, cfg.fps = args.width, args.height, args.fps
+    cfg.enc.bitrate_kbps = args.bitrate_kbps
+    cfg.enc.search_range = args.search_range
+    cfg.enc.subpel = args.subpel
+    sess = N.Session(cfg)
+
+    for _ in range(args.warmup):
+        sess.step(False)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    lat_ms, sizes, qps, gpu_ms = [], [], [], []
+    for _ in range(args.steps):
+        r = sess.step(False)
+        lat_ms.append((r.t_encoded_us - r.t_capture_us) / 1000.0)
+        sizes.append(len(r.au))
+        qps.append(r.qp)
+        gpu_ms.append(r.gpu_ms)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed_max = float(t.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, lat_ms)
+        all_lat = [x for g in gathered for x in g]
+        gsz = [None] * world
+        dist.all_gather_object(gsz, sizes)
+        all_sizes = [x for g in gsz for x in g]
+    else:
+        elapsed_max, all_lat, all_sizes = elapsed, lat_ms, sizes
+
+    total_frames = args.steps * world
+    fps_total = total_frames / elapsed_max
+    p50 = statistics.median(all_lat)
+    p95 = sorted(all_lat)[int(0.95 * (len(all_lat) - 1))]
+    per_gpu = fps_total / world
+    kbps = statistics.mean(all_sizes) * 8 * args.fps / 1000.0
+    if rank == 0:
+        out = {
+            "metric": "encoded FPS (1080p H.264 desktop session, aggregate over GPUs) + p50 E2E latency",
+            "value": round(fps_total, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1000.0, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "vs_operating_point": round(fps_total / (60.0 * world), 3),
+            "p50_e2e_latency_ms": round(p50, 3),
+            "p95_e2e_latency_ms": round(p95, 3),
+            "encoded_fps_per_gpu": round(per_gpu, 2),
+            "sessions_per_node_at_60fps": int(fps_total // 60),
+            "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
+            "mean_bitrate_kbps_at_60fps": round(kbps, 1),
+            "mean_qp": round(statistics.mean(qps), 2),
+            "dtype": "uint8 video (8-bit 4:2:0), H.264 Constrained Baseline",
+            "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",
+            "config": {
+                "model": f"{args.width}x{args.height}@{args.fps} H.264 desktop session (mxh264enc, CBR "
+                         f"{args.bitrate_kbps} kbps, ME +/-{args.search_range} qpel={args.subpel})",
+                "global_batch": world,
+                "seq_len": args.width * args.height,
+                "parallelism": f"session-per-gpu x{world}",
+            },
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            Path(args.json_out).write_text(line + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,368 @@
+// pybind11 bindings: mxdesk._native
+// Device buffers are passed as integer pointers (e.g. torch.Tensor.data_ptr()) and HIP
+// streams as integers (torch.cuda.current_stream().cuda_stream), so the kernels compose
+// with PyTorch-ROCm tensors and torch.distributed (RCCL) without copies.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../codec/h264_core.h"
+#include "../codec/h264_encoder.h"
+#include "../common/hip_check.h"
+#include "../kernels/pixel.h"
+#include "../runtime/session.h"
+
+namespace py = pybind11;
+using namespace mx;
+
+namespace {
+
+template <class T>
+T* as_ptr(uintptr_t p) {
+    return reinterpret_cast<T*>(p);
+}
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::bytes to_bytes(const std::vector<uint8_t>& v) {
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+}
+
+// --- bit helpers exposed for unit tests
+struct PyBits {
+    std::vector<uint32_t> words;
+    h264::BitWriter w;
+    PyBits() : words(4096) { w.init(words.data()); }
+    py::tuple finish() {
+        const uint32_t bits = w.bits;
+        w.flush();
+        std::vector<uint8_t> out;
+        for (uint32_t i = 0; i < (bits + 7) / 8; ++i) out.push_back((uint8_t)(words[i / 4] >> (24 - 8 * (i % 4))));
+        return py::make_tuple(to_bytes(out), bits);
+    }
+};
+
+py::tuple cavlc_block_py(const std::vector<int>& coef, int nc) {
+    PyBits b;
+    int c[16] = {0};
+    const int n = (int)coef.size();
+    if (n != 4 && n != 15 && n != 16) throw std::invalid_argument("block must have 4, 15 or 16 coefficients");
+    for (int i = 0; i < n; ++i) c[i] = coef[i];
+    h264::cavlc_block(b.w, c, n, nc);
+    return b.finish();
+}
+
+py::array_t<int> fdct_py(py::array_t<int, py::array::c_style | py::array::forcecast> x) {
+    if (x.size() != 16) throw std::invalid_argument("need 16 values");
+    py::array_t<int> y(16);
+    h264::fdct4x4(x.data(), y.mutable_data());
+    return y;
+}
+py::array_t<int> idct_py(py::array_t<int, py::array::c_style | py::array::forcecast> x) {
+    if (x.size() != 16) throw std::invalid_argument("need 16 values");
+    py::array_t<int> y(16);
+    h264::idct4x4(x.data(), y.mutable_data());
+    return y;
+}
+
+py::array_t<uint8_t> copy_plane(const uint8_t* dev, int pitch, int w, int h) {
+    py::array_t<uint8_t> out({h, w});
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy2D(out.mutable_data(), w, dev, pitch, w, h, hipMemcpyDeviceToHost));
+    return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+    m.doc() = "mxdesk native runtime: HIP kernels (gfx950), H.264 encoder, session pipeline";
+
+    m.def("device_count", []() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+        return n;
+    });
+    m.def("set_device", [](int d) { HIP_CHECK(hipSetDevice(d)); });
+    m.def("device_name", [](int d) {
+        hipDeviceProp_t p;
+        HIP_CHECK(hipGetDeviceProperties(&p, d));
+        return std::string(p.gcnArchName) + " / " + p.name;
+    });
+    m.def("synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
+
+    // ---------------------------------------------------------------- codec helpers
+    py::module h = m.def_submodule("h264", "H.264 building blocks (for tests)");
+    h.def("cavlc_block", &cavlc_block_py, py::arg("coef"), py::arg("nc"));
+    h.def("fdct4x4", &fdct_py);
+    h.def("idct4x4", &idct_py);
+    h.def("ue", [](uint32_t k) {
+        PyBits b;
+        h264::put_ue(b.w, k);
+        return b.finish();
+    });
+    h.def("se", [](int v) {
+        PyBits b;
+        h264::put_se(b.w, v);
+        return b.finish();
+    });
+    h.def("luma_qpel", [](py::array_t<uint8_t, py::array::c_style> plane, int x4, int y4) {
+        if (plane.ndim() != 2) throw std::invalid_argument("2-D plane");
+        const int H = (int)plane.shape(0), W = (int)plane.shape(1);
+        return h264::luma_qpel(plane.data(), W, W, H, x4, y4);
+    });
+    h.def("level_for", &h264::pick_level);
+
+    py::class_<h264::EncoderConfig>(m, "EncoderConfig")
+        .def(py::init<>())
+        .def_readwrite("width", &h264::EncoderConfig::width)
+        .def_readwrite("height", &h264::EncoderConfig::height)
+        .def_readwrite("fps", &h264::EncoderConfig::fps)
+        .def_readwrite("bitrate_kbps", &h264::EncoderConfig::bitrate_kbps)
+        .def_readwrite("qp", &h264::EncoderConfig::qp)
+        .def_readwrite("qp_min", &h264::EncoderConfig::qp_min)
+        .def_readwrite("qp_max", &h264::EncoderConfig::qp_max)
+        .def_readwrite("keyint", &h264::EncoderConfig::keyint)
+        .def_readwrite("search_range", &h264::EncoderConfig::search_range)
+        .def_readwrite("subpel", &h264::EncoderConfig::subpel)
+        .def_readwrite("chroma_qp_offset", &h264::EncoderConfig::chroma_qp_offset);
+
+    py::class_<h264::FrameStats>(m, "FrameStats")
+        .def_readonly("frame_index", &h264::FrameStats::frame_index)
+        .def_readonly("idr", &h264::FrameStats::idr)
+        .def_readonly("qp", &h264::FrameStats::qp)
+        .def_readonly("bytes", &h264::FrameStats::bytes)
+        .def_readonly("skipped_mbs", &h264::FrameStats::skipped_mbs)
+        .def_readonly("encode_ms", &h264::FrameStats::encode_ms);
+
+    py::class_<h264::CpuH264Encoder>(m, "CpuH264Encoder")
+        .def(py::init<const h264::EncoderConfig&>())
+        .def(
+            "encode",
+            [](h264::CpuH264Encoder& e, py::array_t<uint8_t, py::array::c_style> y,
+               py::array_t<uint8_t, py::array::c_style> uv, bool force_idr) {
+                if (y.ndim() != 2 || uv.ndim() != 2 || y.shape(1) != uv.shape(1))
+                    throw std::invalid_argument("y (H,P) and uv (H/2,P) planes with equal pitch");
+                const int pitch = (int)y.shape(1);
+                const int cw = e.coded_pitch();
+                const auto& cfg = e.common().config();
+                const int ch = e.common().mb_h() * 16;
+                std::vector<uint8_t> py_, puv;
+                const uint8_t* yy = y.data();
+                const uint8_t* uu = uv.data();
+                int p = pitch;
+                if (y.shape(0) < ch || pitch < cw) {
+                    h264::pad_nv12(yy, uu, cfg.width, cfg.height, pitch, cw, ch, py_, puv);
+                    yy = py_.data();
+                    uu = puv.data();
+                    p = cw;
+                }
+                const auto& au = e.encode(yy, uu, p, force_idr);
+                return to_bytes(au);
+            },
+            py::arg("y"), py::arg("uv"), py::arg("force_idr") = false)
+        .def("recon",
+             [](h264::CpuH264Encoder& e) {
+                 const int cw = e.coded_pitch(), ch = e.common().mb_h() * 16;
+                 py::array_t<uint8_t> y({ch, cw}), uv({ch / 2, cw});
+                 std::memcpy(y.mutable_data(), e.recon_y().data(), (size_t)cw * ch);
+                 std::memcpy(uv.mutable_data(), e.recon_uv().data(), (size_t)cw * ch / 2);
+                 return py::make_tuple(y, uv);
+             })
+        .def("request_idr", [](h264::CpuH264Encoder& e) { e.common().request_idr(); })
+        .def("set_bitrate", [](h264::CpuH264Encoder& e, int k) { e.common().set_bitrate(k); })
+        .def_property_readonly("stats", &h264::CpuH264Encoder::last_stats);
+
+    py::class_<h264::GpuH264Encoder>(m, "GpuH264Encoder")
+        .def(py::init([](const h264::EncoderConfig& c, uintptr_t stream) {
+                 return new h264::GpuH264Encoder(c, as_stream(stream));
+             }),
+             py::arg("config"), py::arg("stream") = 0)
+        .def_property_readonly("pitch", &h264::GpuH264Encoder::pitch)
+        .def_property_readonly("coded_height", [](h264::GpuH264Encoder& e) { return e.geometry().coded_h; })
+        .def(
+            "encode",
+            [](h264::GpuH264Encoder& e, uintptr_t y, uintptr_t uv, bool force_idr) {
+                {
+                    py::gil_scoped_release rel;
+                    e.submit(as_ptr<const uint8_t>(y), as_ptr<const uint8_t>(uv), force_idr);
+                }
+                std::vector<uint8_t> au;
+                {
+                    py::gil_scoped_release rel;
+                    au = e.collect();
+                }
+                return to_bytes(au);
+            },
+            py::arg("y_ptr"), py::arg("uv_ptr"), py::arg("force_idr") = false)
+        .def("submit", [](h264::GpuH264Encoder& e, uintptr_t y, uintptr_t uv,
+                          bool force_idr) { e.submit(as_ptr<const uint8_t>(y), as_ptr<const uint8_t>(uv), force_idr); })
+        .def("collect",
+             [](h264::GpuH264Encoder& e) {
+                 std::vector<uint8_t> au;
+                 {
+                     py::gil_scoped_release rel;
+                     au = e.collect();
+                 }
+                 return to_bytes(au);
+             })
+        .def("recon",
+             [](h264::GpuH264Encoder& e) {
+                 const auto& g = e.geometry();
+                 return py::make_tuple(copy_plane(e.recon_y(), g.pitch, g.coded_w, g.coded_h),
+                                       copy_plane(e.recon_uv(), g.pitch, g.coded_w, g.coded_h / 2));
+             })
+        .def("request_idr", [](h264::GpuH264Encoder& e) { e.common().request_idr(); })
+        .def("set_bitrate", [](h264::GpuH264Encoder& e, int k) { e.common().set_bitrate(k); })
+        .def_property_readonly("stats", &h264::GpuH264Encoder::last_stats);
+
+    // ---------------------------------------------------------------- pixel kernels
+    m.def(
+        "synth",
+        [](uintptr_t out, int w, int h, int pitch, uint32_t frame_id, uint32_t ts, float t, int noise, int ox, int oy,
+           int wall_w, int wall_h, int cx, int cy, uintptr_t stream) {
+            pix::SynthParams p{w, h, pitch, frame_id, ts, t, ox, oy, wall_w > 0 ? wall_w : w, wall_h > 0 ? wall_h : h,
+                               noise, cx, cy};
+            pix::launch_synth(as_ptr<uint8_t>(out), p, as_stream(stream));
+            HIP_CHECK(hipGetLastError());
+        },
+        py::arg("out_ptr"), py::arg("width"), py::arg("height"), py::arg("pitch"), py::arg("frame_id") = 0,
+        py::arg("timestamp_us") = 0, py::arg("t") = 0.f, py::arg("noise") = 1, py::arg("origin_x") = 0,
+        py::arg("origin_y") = 0, py::arg("wall_w") = 0, py::arg("wall_h") = 0, py::arg("cursor_x") = -1,
+        py::arg("cursor_y") = -1, py::arg("stream") = 0);
+    m.def(
+        "bgrx_to_nv12",
+        [](uintptr_t in, int in_pitch, int w, int h, uintptr_t y, uintptr_t uv, int out_pitch, int cw, int ch,
+           uintptr_t stream) {
+            if ((w & 1) || (h & 1) || (cw & 3) || (ch & 1) || cw < w || ch < h || out_pitch < cw || (out_pitch & 3) ||
+                (in_pitch & 15))
+                throw std::invalid_argument("bgrx_to_nv12: bad geometry");
+            pix::launch_bgrx_to_nv12(as_ptr<const uint8_t>(in), in_pitch, w, h, as_ptr<uint8_t>(y), as_ptr<uint8_t>(uv),
+                                     out_pitch, cw, ch, as_stream(stream));
+            HIP_CHECK(hipGetLastError());
+        },
+        py::arg("in_ptr"), py::arg("in_pitch"), py::arg("width"), py::arg("height"), py::arg("y_ptr"),
+        py::arg("uv_ptr"), py::arg("out_pitch"), py::arg("coded_w"), py::arg("coded_h"), py::arg("stream") = 0);
+    m.def(
+        "scale_to_nv12",
+        [](uintptr_t in, int in_pitch, int in_w, int in_h, int out_w, int out_h, uintptr_t x0, uintptr_t wx, int taps_x,
+           uintptr_t y0, uintptr_t wy, int taps_y, uintptr_t y, uintptr_t uv, int out_pitch, int cw, int ch,
+           uintptr_t stream) {
+            if ((out_w & 1) || (out_h & 1) || cw < out_w || ch < out_h || (cw & 1) || (ch & 1))
+                throw std::invalid_argument("scale_to_nv12: bad geometry");
+            pix::LanczosTables t{out_w,
+                                 out_h,
+                                 taps_x,
+                                 taps_y,
+                                 as_ptr<const int>(x0),
+                                 as_ptr<const float>(wx),
+                                 as_ptr<const int>(y0),
+                                 as_ptr<const float>(wy)};
+            pix::launch_scale_to_nv12(as_ptr<const uint8_t>(in), in_pitch, in_w, in_h, t, as_ptr<uint8_t>(y),
+                                      as_ptr<uint8_t>(uv), out_pitch, cw, ch, as_stream(stream));
+            HIP_CHECK(hipGetLastError());
+        },
+        py::arg("in_ptr"), py::arg("in_pitch"), py::arg("in_w"), py::arg("in_h"), py::arg("out_w"), py::arg("out_h"),
+        py::arg("x0_ptr"), py::arg("wx_ptr"), py::arg("taps_x"), py::arg("y0_ptr"), py::arg("wy_ptr"),
+        py::arg("taps_y"), py::arg("y_ptr"), py::arg("uv_ptr"), py::arg("out_pitch"), py::arg("coded_w"),
+        py::arg("coded_h"), py::arg("stream") = 0);
+    m.def(
+        "composite",
+        [](uintptr_t tile, int tile_pitch, int tw, int th, uintptr_t dst, int dst_pitch, int dx, int dy,
+           uintptr_t stream) {
+            pix::launch_composite(as_ptr<const uint8_t>(tile), tile_pitch, tw, th, as_ptr<uint8_t>(dst), dst_pitch, dx,
+                                  dy, as_stream(stream));
+            HIP_CHECK(hipGetLastError());
+        },
+        py::arg("tile_ptr"), py::arg("tile_pitch"), py::arg("tile_w"), py::arg("tile_h"), py::arg("dst_ptr"),
+        py::arg("dst_pitch"), py::arg("dx"), py::arg("dy"), py::arg("stream") = 0);
+    m.def("lanczos_table", [](int in_size, int out_size) {
+        std::vector<int> s;
+        std::vector<float> w;
+        int taps;
+        make_lanczos_table(in_size, out_size, s, w, taps);
+        py::array_t<int32_t> sa((py::ssize_t)s.size());
+        std::memcpy(sa.mutable_data(), s.data(), s.size() * 4);
+        py::array_t<float> wa({(py::ssize_t)out_size, (py::ssize_t)taps});
+        std::memcpy(wa.mutable_data(), w.data(), w.size() * 4);
+        return py::make_tuple(sa, wa, taps);
+    });
+    m.attr("BARCODE_CELL") = pix::kBarCell;
+    m.attr("BARCODE_X") = pix::kBarX;
+    m.attr("BARCODE_Y") = pix::kBarY;
+
+    // ---------------------------------------------------------------- session
+    py::class_<SessionConfig>(m, "SessionConfig")
+        .def(py::init<>())
+        .def_readwrite("width", &SessionConfig::width)
+        .def_readwrite("height", &SessionConfig::height)
+        .def_readwrite("out_width", &SessionConfig::out_width)
+        .def_readwrite("out_height", &SessionConfig::out_height)
+        .def_readwrite("fps", &SessionConfig::fps)
+        .def_readwrite("noise", &SessionConfig::noise)
+        .def_readwrite("pool_slots", &SessionConfig::pool_slots)
+        .def_readwrite("enc", &SessionConfig::enc);
+
+    py::class_<FrameResult>(m, "FrameResult")
+        .def_readonly("frame_id", &FrameResult::frame_id)
+        .def_readonly("t_capture_us", &FrameResult::t_capture_us)
+        .def_readonly("t_encoded_us", &FrameResult::t_encoded_us)
+        .def_readonly("gpu_ms", &FrameResult::gpu_ms)
+        .def_readonly("idr", &FrameResult::idr)
+        .def_readonly("qp", &FrameResult::qp)
+        .def_property_readonly("au", [](const FrameResult& r) { return to_bytes(r.au); });
+
+    py::class_<Session>(m, "Session")
+        .def(py::init<const SessionConfig&>())
+        .def(
+            "step",
+            [](Session& s, bool force_idr) {
+                py::gil_scoped_release rel;
+                return s.step(force_idr);
+            },
+            py::arg("force_idr") = false)
+        .def(
+            "submit",
+            [](Session& s, bool force_idr) {
+                py::gil_scoped_release rel;
+                s.submit_synthetic(force_idr);
+            },
+            py::arg("force_idr") = false)
+        .def(
+            "submit_bgrx",
+            [](Session& s, py::array_t<uint8_t, py::array::c_style> img, bool force_idr) {
+                if (img.ndim() != 3 || img.shape(2) != 4) throw std::invalid_argument("expect HxWx4 BGRx");
+                if (img.shape(0) != s.config().height || img.shape(1) != s.config().width)
+                    throw std::invalid_argument("frame size != session desktop size");
+                const uint8_t* p = img.data();
+                const int pitch = (int)img.shape(1) * 4;
+                py::gil_scoped_release rel;
+                s.submit_bgrx(p, pitch, force_idr);
+            },
+            py::arg("frame"), py::arg("force_idr") = false)
+        .def("collect",
+             [](Session& s) {
+                 py::gil_scoped_release rel;
+                 return s.collect();
+             })
+        .def("set_cursor", &Session::set_cursor)
+        .def("request_idr", &Session::request_idr)
+        .def("set_bitrate", &Session::set_bitrate)
+        .def_property_readonly("stream", [](Session& s) { return reinterpret_cast<uintptr_t>(s.stream()); })
+        .def_property_readonly("nv12_y_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_y()); })
+        .def_property_readonly("nv12_uv_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_uv()); })
+        .def_property_readonly("nv12_pitch", &Session::nv12_pitch)
+        .def("nv12",
+             [](Session& s) {
+                 const auto& g = s.encoder().geometry();
+                 return py::make_tuple(copy_plane(s.nv12_y(), g.pitch, g.coded_w, g.coded_h),
+                                       copy_plane(s.nv12_uv(), g.pitch, g.coded_w, g.coded_h / 2));
+             })
+        .def("recon",
+             [](Session& s) {
+                 const auto& g = s.encoder().geometry();
+                 return py::make_tuple(copy_plane(s.encoder().recon_y(), g.pitch, g.coded_w, g.coded_h),
+                                       copy_plane(s.encoder().recon_uv(), g.pitch, g.coded_w, g.coded_h / 2));
+             })
+        .def_property_readonly("stats", [](Session& s) { return s.encoder().last_stats(); });
+}

@@ -1,0 +1,399 @@
+// CPU H.264 encoder: the same decisions and arithmetic as the HIP kernels, serial.
+// Serves the no-GPU plumbing configuration (BASELINE.json config 1, the reference's
+// `x264enc` fallback, README.md:21) and is the bit-exact oracle for the GPU encoder.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+#include "h264_encoder.h"
+#include "h264_mb.h"
+
+namespace mx {
+namespace h264 {
+
+void pad_nv12(const uint8_t* y, const uint8_t* uv, int w, int h, int pitch, int coded_w, int coded_h,
+              std::vector<uint8_t>& oy, std::vector<uint8_t>& ouv) {
+    oy.resize((size_t)coded_w * coded_h);
+    ouv.resize((size_t)coded_w * coded_h / 2);
+    for (int r = 0; r < coded_h; ++r) {
+        const uint8_t* s = y + (size_t)std::min(r, h - 1) * pitch;
+        uint8_t* d = oy.data() + (size_t)r * coded_w;
+        std::memcpy(d, s, w);
+        for (int c = w; c < coded_w; ++c) d[c] = s[w - 1];
+    }
+    for (int r = 0; r < coded_h / 2; ++r) {
+        const uint8_t* s = uv + (size_t)std::min(r, h / 2 - 1) * pitch;
+        uint8_t* d = ouv.data() + (size_t)r * coded_w;
+        std::memcpy(d, s, w);
+        for (int c = w; c < coded_w; c += 2) {
+            d[c] = s[w - 2];
+            d[c + 1] = s[w - 1];
+        }
+    }
+}
+
+CpuH264Encoder::CpuH264Encoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
+    cw_ = common_.mb_w() * 16;
+    ch_ = common_.mb_h() * 16;
+    for (int i = 0; i < 2; ++i) {
+        rec_y_[i].assign((size_t)cw_ * ch_, 16);
+        rec_uv_[i].assign((size_t)cw_ * ch_ / 2, 128);
+    }
+    mb_.resize((size_t)common_.mb_w() * common_.mb_h());
+    coef_.resize(mb_.size() * kCoefStride);
+}
+
+static Geometry geom_of(const EncoderCommon& c, int cw, int ch) {
+    Geometry g;
+    g.width = c.config().width;
+    g.height = c.config().height;
+    g.mb_w = c.mb_w();
+    g.mb_h = c.mb_h();
+    g.coded_w = cw;
+    g.coded_h = ch;
+    g.pitch = cw;
+    return g;
+}
+
+void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pitch) {
+    const Geometry g = geom_of(common_, cw_, ch_);
+    const uint8_t* ref_y = rec_y_[cur_ ^ 1].data();
+    const uint8_t* ref_uv = rec_uv_[cur_ ^ 1].data();
+    uint8_t* rec_y = rec_y_[cur_].data();
+    uint8_t* rec_uv = rec_uv_[cur_].data();
+    const int qp = common_.cur_qp();
+    const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+    const int lambda = lambda_sad(qp);
+    const int R = std::clamp(cfg_.search_range, 1, 32);
+    const int side = 2 * R + 1;
+    for (int mby = 0; mby < g.mb_h; ++mby)
+        for (int mbx = 0; mbx < g.mb_w; ++mbx) {
+            const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
+            MbInfo& m = mb_[mbi];
+            std::memset(&m, 0, sizeof m);
+            // ---- integer full search (identical order / tie-break to k_me_full)
+            unsigned long long best = ~0ull;
+            for (int c = 0; c < side * side; ++c) {
+                const int dy = c / side - R, dx = c % side - R;
+                uint32_t sad = 0;
+                for (int r = 0; r < 16; ++r)
+                    for (int k = 0; k < 16; ++k)
+                        sad += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
+                                        ref_px(ref_y, cw_, cw_, ch_, x0 + dx + k, y0 + dy + r));
+                const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
+                const uint32_t dist = (uint32_t)(std::abs(dx) + std::abs(dy));
+                const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
+                best = std::min(best, key);
+            }
+            const int cb = (int)(best & 0xffff);
+            int mvx = 4 * ((cb % side) - R), mvy = 4 * ((cb / side) - R);
+            if (cfg_.subpel) {
+                auto sad_at = [&](int vx, int vy) {
+                    uint32_t s = 0;
+                    for (int r = 0; r < 16; ++r)
+                        for (int k = 0; k < 16; ++k)
+                            s += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
+                                          luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + vx, (y0 + r) * 4 + vy));
+                    return s;
+                };
+                uint32_t cur_cost = me_cost(sad_at(mvx, mvy), lambda, mvx, mvy);
+                for (int step = 2; step >= 1; step >>= 1) {
+                    int bdx = 0, bdy = 0;
+                    uint32_t bcost = cur_cost;
+                    for (int k = 0; k < 8; ++k) {
+                        int ddx, ddy;
+                        subpel_offset(k, &ddx, &ddy);
+                        const int cx = mvx + ddx * step, cy = mvy + ddy * step;
+                        const uint32_t cost = me_cost(sad_at(cx, cy), lambda, cx, cy);
+                        if (cost < bcost) {
+                            bcost = cost;
+                            bdx = ddx * step;
+                            bdy = ddy * step;
+                        }
+                    }
+                    mvx += bdx;
+                    mvy += bdy;
+                    cur_cost = bcost;
+                }
+            }
+            m.mvx = (int16_t)mvx;
+            m.mvy = (int16_t)mvy;
+            m.type = kMbP16x16;
+            // ---- prediction + residual
+            int pred[384], res[384];
+            for (int r = 0; r < 16; ++r)
+                for (int k = 0; k < 16; ++k) {
+                    const int p = luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
+                    pred[r * 16 + k] = p;
+                    res[r * 16 + k] = sy[(y0 + r) * pitch + x0 + k] - p;
+                }
+            for (int comp = 0; comp < 2; ++comp)
+                for (int r = 0; r < 8; ++r)
+                    for (int k = 0; k < 8; ++k) {
+                        const int xc = x0 / 2 + k, yc = y0 / 2 + r;
+                        const int p = chroma_pred8(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc * 8 + mvx, yc * 8 + mvy);
+                        pred[256 + comp * 64 + r * 8 + k] = p;
+                        res[256 + comp * 64 + r * 8 + k] = suv[yc * pitch + 2 * xc + comp] - p;
+                    }
+            int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
+            int cbp = 0;
+            for (int b = 0; b < 16; ++b) {
+                const int bx = kBlkX[b], by = kBlkY[b];
+                int x[16], zs[16], rr[16];
+                for (int i = 0; i < 4; ++i)
+                    for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[(by * 4 + i) * 16 + bx * 4 + j];
+                const int nz = luma_block_inter(x, qp, zs, rr);
+                for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
+                m.nz_luma[by * 4 + bx] = (uint8_t)nz;
+                if (nz) cbp |= 1 << (b >> 2);
+                for (int i = 0; i < 4; ++i)
+                    for (int j = 0; j < 4; ++j)
+                        rec_y[(y0 + by * 4 + i) * cw_ + x0 + bx * 4 + j] =
+                            (uint8_t)clip255(pred[(by * 4 + i) * 16 + bx * 4 + j] + rr[i * 4 + j]);
+            }
+            bool any_ac = false, any_dc = false;
+            for (int comp = 0; comp < 2; ++comp) {
+                int z[4][16], dcin[4];
+                for (int cbk = 0; cbk < 4; ++cbk) {
+                    const int bx = cbk & 1, by = cbk >> 1;
+                    int x[16], y[16];
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
+                    fdct4x4(x, y);
+                    dcin[cbk] = y[0];
+                    const int nz = quant4x4(y, z[cbk], qpc, false, 1);
+                    for (int k = 1; k < 16; ++k)
+                        mc[kCoefChromaAc + (comp * 4 + cbk) * 16 + k] = (int16_t)z[cbk][kZigzag4x4[k]];
+                    (comp ? m.nz_cr : m.nz_cb)[cbk] = (uint8_t)nz;
+                    any_ac |= nz > 0;
+                }
+                int zd[4], dq[4];
+                any_dc |= quant_dc_chroma(dcin, zd, qpc, false) > 0;
+                for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zd[i];
+                dequant_dc_chroma(zd, dq, qpc);
+                for (int cbk = 0; cbk < 4; ++cbk) {
+                    const int bx = cbk & 1, by = cbk >> 1;
+                    int d[16], rr[16];
+                    dequant4x4(z[cbk], d, qpc, 1);
+                    d[0] = dq[cbk];
+                    idct4x4(d, rr);
+                    const int xc = x0 / 2 + bx * 4, yc = y0 / 2 + by * 4;
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = 0; j < 4; ++j)
+                            rec_uv[(yc + i) * cw_ + 2 * (xc + j) + comp] = (uint8_t)clip255(
+                                pred[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j] + rr[i * 4 + j]);
+                }
+            }
+            cbp |= (any_ac ? 2 : (any_dc ? 1 : 0)) << 4;
+            m.cbp = (uint8_t)cbp;
+        }
+}
+
+void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
+    const Geometry g = geom_of(common_, cw_, ch_);
+    uint8_t* rec_y = rec_y_[cur_].data();
+    uint8_t* rec_uv = rec_uv_[cur_].data();
+    const int qp = common_.cur_qp();
+    const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+    for (int mby = 0; mby < g.mb_h; ++mby) {
+        uint8_t left[32] = {0};
+        for (int mbx = 0; mbx < g.mb_w; ++mbx) {
+            const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
+            const bool have_left = mbx > 0;
+            MbInfo& m = mb_[mbi];
+            std::memset(&m, 0, sizeof m);
+            int dcl = 128;
+            if (have_left) {
+                int s = 0;
+                for (int i = 0; i < 16; ++i) s += left[i];
+                dcl = (s + 8) >> 4;
+            }
+            int sad_dc = 0, sad_h = 0;
+            for (int r = 0; r < 16; ++r)
+                for (int k = 0; k < 16; ++k) {
+                    const int sv = sy[(y0 + r) * pitch + x0 + k];
+                    sad_dc += std::abs(sv - dcl);
+                    sad_h += have_left ? std::abs(sv - left[r]) : 0;
+                }
+            const int lmode = (have_left && sad_h < sad_dc) ? 1 : 2;
+            int pred[384], res[384];
+            for (int r = 0; r < 16; ++r)
+                for (int k = 0; k < 16; ++k) {
+                    const int p = lmode == 1 ? left[r] : dcl;
+                    pred[r * 16 + k] = p;
+                    res[r * 16 + k] = sy[(y0 + r) * pitch + x0 + k] - p;
+                }
+            int pdc[2][2] = {{128, 128}, {128, 128}};  // [comp][upper/lower 4 rows]
+            if (have_left)
+                for (int comp = 0; comp < 2; ++comp)
+                    for (int h = 0; h < 2; ++h)
+                        pdc[comp][h] = (left[16 + comp * 8 + h * 4] + left[16 + comp * 8 + h * 4 + 1] +
+                                        left[16 + comp * 8 + h * 4 + 2] + left[16 + comp * 8 + h * 4 + 3] + 2) >> 2;
+            int sdc = 0, sh = 0;
+            for (int comp = 0; comp < 2; ++comp)
+                for (int r = 0; r < 8; ++r)
+                    for (int k = 0; k < 8; ++k) {
+                        const int s = suv[(y0 / 2 + r) * pitch + 2 * (x0 / 2 + k) + comp];
+                        sdc += std::abs(s - pdc[comp][r >> 2]);
+                        sh += have_left ? std::abs(s - left[16 + comp * 8 + r]) : 0;
+                    }
+            const int cmode = (have_left && sh < sdc) ? 1 : 0;
+            for (int comp = 0; comp < 2; ++comp)
+                for (int r = 0; r < 8; ++r)
+                    for (int k = 0; k < 8; ++k) {
+                        const int s = suv[(y0 / 2 + r) * pitch + 2 * (x0 / 2 + k) + comp];
+                        const int p = cmode == 1 ? left[16 + comp * 8 + r] : pdc[comp][r >> 2];
+                        pred[256 + comp * 64 + r * 8 + k] = p;
+                        res[256 + comp * 64 + r * 8 + k] = s - p;
+                    }
+            int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
+            int z[16][16], ldc[16];
+            bool luma_ac = false;
+            int nzl[16];
+            for (int b = 0; b < 16; ++b) {
+                const int bx = kBlkX[b], by = kBlkY[b];
+                int x[16], y[16];
+                for (int i = 0; i < 4; ++i)
+                    for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[(by * 4 + i) * 16 + bx * 4 + j];
+                fdct4x4(x, y);
+                ldc[by * 4 + bx] = y[0];
+                nzl[b] = quant4x4(y, z[b], qp, true, 1);
+                luma_ac |= nzl[b] > 0;
+                for (int k = 1; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)z[b][kZigzag4x4[k]];
+                mc[kCoefLuma + b * 16] = 0;
+            }
+            int zd[16], dq[16];
+            quant_dc_luma(ldc, zd, qp);
+            for (int k = 0; k < 16; ++k) mc[kCoefLumaDc + k] = (int16_t)zd[kZigzag4x4[k]];
+            dequant_dc_luma(zd, dq, qp);
+            for (int b = 0; b < 16; ++b) {
+                const int bx = kBlkX[b], by = kBlkY[b];
+                int d[16], rr[16];
+                if (luma_ac)
+                    dequant4x4(z[b], d, qp, 1);
+                else
+                    for (int i = 1; i < 16; ++i) d[i] = 0;
+                d[0] = dq[by * 4 + bx];
+                idct4x4(d, rr);
+                for (int i = 0; i < 4; ++i)
+                    for (int j = 0; j < 4; ++j) {
+                        const int v = clip255(pred[(by * 4 + i) * 16 + bx * 4 + j] + rr[i * 4 + j]);
+                        rec_y[(y0 + by * 4 + i) * cw_ + x0 + bx * 4 + j] = (uint8_t)v;
+                    }
+                m.nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nzl[b] : 0);
+            }
+            bool any_ac = false, any_dc = false;
+            for (int comp = 0; comp < 2; ++comp) {
+                int zc[4][16], dcin[4];
+                for (int cbk = 0; cbk < 4; ++cbk) {
+                    const int bx = cbk & 1, by = cbk >> 1;
+                    int x[16], y[16];
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
+                    fdct4x4(x, y);
+                    dcin[cbk] = y[0];
+                    const int nz = quant4x4(y, zc[cbk], qpc, true, 1);
+                    for (int k = 1; k < 16; ++k)
+                        mc[kCoefChromaAc + (comp * 4 + cbk) * 16 + k] = (int16_t)zc[cbk][kZigzag4x4[k]];
+                    (comp ? m.nz_cr : m.nz_cb)[cbk] = (uint8_t)nz;
+                    any_ac |= nz > 0;
+                }
+                int zdc[4], dqc[4];
+                any_dc |= quant_dc_chroma(dcin, zdc, qpc, true) > 0;
+                for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zdc[i];
+                dequant_dc_chroma(zdc, dqc, qpc);
+                for (int cbk = 0; cbk < 4; ++cbk) {
+                    const int bx = cbk & 1, by = cbk >> 1;
+                    int d[16], rr[16];
+                    dequant4x4(zc[cbk], d, qpc, 1);
+                    d[0] = dqc[cbk];
+                    idct4x4(d, rr);
+                    const int xc = x0 / 2 + bx * 4, yc = y0 / 2 + by * 4;
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = 0; j < 4; ++j)
+                            rec_uv[(yc + i) * cw_ + 2 * (xc + j) + comp] = (uint8_t)clip255(
+                                pred[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j] + rr[i * 4 + j]);
+                }
+            }
+            // left column for the next MB
+            for (int i = 0; i < 16; ++i) left[i] = rec_y[(y0 + i) * cw_ + x0 + 15];
+            for (int comp = 0; comp < 2; ++comp)
+                for (int i = 0; i < 8; ++i) left[16 + comp * 8 + i] = rec_uv[(y0 / 2 + i) * cw_ + 2 * (x0 / 2 + 7) + comp];
+            const int ccbp = any_ac ? 2 : (any_dc ? 1 : 0);
+            m.type = kMbI16x16;
+            m.cbp = (uint8_t)((luma_ac ? 15 : 0) | (ccbp << 4));
+            m.i16_mode = (uint8_t)lmode;
+            m.chroma_mode = (uint8_t)cmode;
+        }
+    }
+}
+
+void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& soff, std::vector<uint32_t>& slen) {
+    const Geometry g = geom_of(common_, cw_, ch_);
+    const bool idr = common_.cur_idr();
+    const int slice_rows = idr ? 1 : g.mb_h;
+    const int per_slice = slice_rows * g.mb_w;
+    const int nmb = g.mb_w * g.mb_h;
+    std::vector<uint32_t> words((size_t)nmb * kSlotWords / 4 + 4096);
+    for (int first = 0; first < nmb; first += per_slice) {
+        const int last = std::min(first + per_slice, nmb);
+        BitWriter w;
+        w.init(words.data());
+        write_slice_header(w, make_slice_params(first, idr, common_.cur_frame_num(), common_.log2_max_frame_num(),
+                                                common_.cur_idr_pic_id(), common_.cur_qp() - common_.pic_init_qp(), 1));
+        int run = 0;
+        for (int mbi = first; mbi < last; ++mbi) {
+            const Avail av = mb_avail(g, mbi % g.mb_w, mbi / g.mb_w, slice_rows);
+            int mvdx, mvdy;
+            const bool skip = decide_skip(g, mb_.data(), mbi, av, &mvdx, &mvdy);
+            mb_[mbi].skip = skip;
+            if (skip) {
+                ++run;
+                continue;
+            }
+            if (!idr) {
+                put_ue(w, (uint32_t)run);
+                run = 0;
+            }
+            const int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
+            for (int role = 0; role < kNumRoles; ++role)
+                code_role(w, role, g, idr, mb_.data(), mb_[mbi], mc, mbi, av, mvdx, mvdy);
+        }
+        if (!idr && run > 0) put_ue(w, (uint32_t)run);
+        w.put(1, 1);
+        w.flush();
+        soff.push_back((uint32_t)payload.size());
+        const uint32_t nbytes = (w.bits + 7) / 8;
+        for (uint32_t i = 0; i < nbytes; ++i) payload.push_back((uint8_t)(words[i / 4] >> (24 - 8 * (i % 4))));
+        slen.push_back(nbytes);
+    }
+}
+
+const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
+    common_.begin_frame(force_idr || !have_ref_);
+    cur_ ^= 1;
+    if (common_.cur_idr())
+        encode_intra(y, uv, pitch);
+    else
+        encode_inter(y, uv, pitch);
+    std::vector<uint8_t> payload;
+    std::vector<uint32_t> soff, slen;
+    entropy(payload, soff, slen);
+    au_.clear();
+    if (common_.cur_idr()) common_.write_parameter_sets(au_);
+    int skipped = 0;
+    for (const MbInfo& m : mb_) skipped += m.skip;
+    for (size_t s = 0; s < soff.size(); ++s) common_.write_slice_nal(au_, payload.data() + soff[s], slen[s]);
+    stats_.frame_index = common_.frames();
+    stats_.idr = common_.cur_idr();
+    stats_.qp = common_.cur_qp();
+    stats_.bytes = (int)au_.size();
+    stats_.skipped_mbs = skipped;
+    common_.end_frame((int)au_.size());
+    have_ref_ = true;
+    return au_;
+}
+
+}  // namespace h264
+}  // namespace mx

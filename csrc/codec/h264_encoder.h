@@ -1,0 +1,164 @@
+// Host-side H.264 encoder API: GpuH264Encoder (HIP kernels, the production path) and
+// CpuH264Encoder (same bitstream subset, serial C++ over the same core functions; used
+// for the no-GPU "plumbing" configuration of BASELINE.json and as a bit-exact oracle
+// for the GPU kernels in tests).
+//
+// Reference parity: WEBRTC_ENCODER selects nvh264enc (NVENC) or x264enc (CPU) in the
+// reference (Dockerfile:210, README.md:21); here "mxh264enc" (GPU) / "cpuh264enc" (CPU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "h264_core.h"
+#include "h264_gpu.h"
+
+namespace mx {
+namespace h264 {
+
+struct EncoderConfig {
+    int width = 1920;
+    int height = 1080;
+    int fps = 60;
+    int bitrate_kbps = 8000;  // 0 = constant QP
+    int qp = 28;              // initial / constant QP
+    int qp_min = 18;
+    int qp_max = 46;
+    int keyint = 0;           // IDR period in frames, 0 = only on demand (infinite GOP)
+    int search_range = 16;    // integer-pel full search radius (<= 32)
+    int subpel = 1;           // quarter-pel refinement
+    int chroma_qp_offset = 0;
+};
+
+struct FrameStats {
+    int64_t frame_index = 0;
+    int idr = 0;
+    int qp = 0;
+    int bytes = 0;
+    int skipped_mbs = 0;
+    double encode_ms = 0;
+};
+
+// Annex-B / rate-control logic shared by both encoders.
+class EncoderCommon {
+   public:
+    explicit EncoderCommon(const EncoderConfig& c);
+    const EncoderConfig& config() const { return cfg_; }
+    int mb_w() const { return mb_w_; }
+    int mb_h() const { return mb_h_; }
+    // Decide frame type/params for the next frame.
+    void begin_frame(bool force_idr);
+    bool cur_idr() const { return cur_idr_; }
+    int cur_qp() const { return cur_qp_; }
+    int cur_frame_num() const { return frame_num_; }
+    int cur_idr_pic_id() const { return idr_pic_id_; }
+    int log2_max_frame_num() const { return 8; }
+    int pic_init_qp() const { return 26; }
+    // Append SPS/PPS NAL units (Annex-B) to out.
+    void write_parameter_sets(std::vector<uint8_t>& out) const;
+    // Append one slice NAL (start code + header byte + emulation-prevented payload).
+    void write_slice_nal(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n) const;
+    // Update rate control after a frame of `bytes` bytes.
+    void end_frame(int bytes);
+    void request_idr() { idr_requested_ = true; }
+    void set_bitrate(int kbps) { cfg_.bitrate_kbps = kbps; }
+    int64_t frames() const { return frame_index_; }
+
+   private:
+    EncoderConfig cfg_;
+    int mb_w_, mb_h_;
+    bool cur_idr_ = true;
+    bool idr_requested_ = true;
+    int cur_qp_;
+    int frame_num_ = 0;
+    int idr_pic_id_ = -1;
+    int64_t frame_index_ = 0;
+    int64_t since_idr_ = 0;
+    double rc_qp_;        // continuous QP state
+    double vbv_fill_ = 0;  // bits above the target rate accumulated so far
+};
+
+void emulation_prevent(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n);
+
+class GpuH264Encoder {
+   public:
+    GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream);
+    ~GpuH264Encoder();
+    GpuH264Encoder(const GpuH264Encoder&) = delete;
+    GpuH264Encoder& operator=(const GpuH264Encoder&) = delete;
+
+    const Geometry& geometry() const { return geom_; }
+    int pitch() const { return geom_.pitch; }
+    hipStream_t stream() const { return stream_; }
+
+    // Enqueue the encode of an NV12 frame already in device memory (pitch = pitch()).
+    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false);
+    // Wait for the submitted frame and return its Annex-B access unit.
+    const std::vector<uint8_t>& collect();
+    const FrameStats& last_stats() const { return stats_; }
+    EncoderCommon& common() { return common_; }
+    // Reconstructed frame of the last encoded picture (device pointers).
+    const uint8_t* recon_y() const { return rec_y_[cur_]; }
+    const uint8_t* recon_uv() const { return rec_uv_[cur_]; }
+    // Enqueue everything after the frame-state upload; exposed for graph capture.
+    void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
+    uint8_t* host_out() const { return host_out_; }
+
+   private:
+    EncoderConfig cfg_;
+    EncoderCommon common_;
+    hipStream_t stream_;
+    Geometry geom_;
+    DeviceBuffers buf_{};
+    FrameState* fs_host_ = nullptr;  // pinned
+    uint8_t* host_out_ = nullptr;    // pinned, mapped: OutHeader | slice tables | payload
+    size_t host_out_bytes_ = 0;
+    uint8_t* rec_y_[2] = {nullptr, nullptr};
+    uint8_t* rec_uv_[2] = {nullptr, nullptr};
+    int cur_ = 0;  // index of the frame being reconstructed
+    bool have_ref_ = false;
+    hipEvent_t done_ = nullptr;
+    hipEvent_t start_ = nullptr;
+    std::vector<uint8_t> au_;
+    FrameStats stats_;
+    bool pending_ = false;
+};
+
+class CpuH264Encoder {
+   public:
+    explicit CpuH264Encoder(const EncoderConfig& cfg);
+    // Encode an NV12 frame (host memory, luma pitch == uv pitch == `pitch`, at least the
+    // coded size mb_w*16 x mb_h*16 readable; use pad_nv12() for display-sized frames).
+    const std::vector<uint8_t>& encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr = false);
+    const FrameStats& last_stats() const { return stats_; }
+    EncoderCommon& common() { return common_; }
+    const std::vector<uint8_t>& recon_y() const { return rec_y_[cur_]; }
+    const std::vector<uint8_t>& recon_uv() const { return rec_uv_[cur_]; }
+    int coded_pitch() const { return cw_; }
+
+   private:
+    void encode_intra(const uint8_t* y, const uint8_t* uv, int pitch);
+    void encode_inter(const uint8_t* y, const uint8_t* uv, int pitch);
+    void entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& slice_off, std::vector<uint32_t>& slice_len);
+
+    EncoderConfig cfg_;
+    EncoderCommon common_;
+    int cw_, ch_;
+    std::vector<uint8_t> rec_y_[2], rec_uv_[2];
+    int cur_ = 0;
+    bool have_ref_ = false;
+    std::vector<MbInfo> mb_;
+    std::vector<int16_t> coef_;
+    std::vector<uint8_t> au_;
+    FrameStats stats_;
+};
+
+// Pad a display-sized NV12 frame to the coded size by edge replication (what the CSC
+// kernel does on the GPU side).  Returns pitch = coded width.
+void pad_nv12(const uint8_t* y, const uint8_t* uv, int w, int h, int pitch, int coded_w, int coded_h,
+              std::vector<uint8_t>& oy, std::vector<uint8_t>& ouv);
+
+}  // namespace h264
+}  // namespace mx

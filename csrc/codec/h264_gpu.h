@@ -1,0 +1,102 @@
+// Device data layout and host API of the HIP H.264 encoder.
+//
+// Per-frame kernel chain (all on one HIP stream, graph-capturable):
+//   P frame: k_me_full -> k_inter_encode -> k_cavlc -> k_scan -> k_pack -> k_copy_out
+//   I frame: k_intra_rows                 -> k_cavlc -> k_scan -> k_pack -> k_copy_out
+// Only the slice payloads (RBSP, byte aligned) leave the GPU; the host adds start
+// codes, NAL headers and emulation-prevention bytes (h264_encoder.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mx {
+namespace h264 {
+
+constexpr int kSlotWords = 640;   // per-MB CAVLC bit slot (2560 B >= worst case)
+constexpr int kCoefStride = 416;  // int16 coefficients per MB
+constexpr int kCoefLuma = 0;      // [16 blkIdx][16 scan]
+constexpr int kCoefLumaDc = 256;  // [16 scan]
+constexpr int kCoefChromaDc = 272;  // [2][4]
+constexpr int kCoefChromaAc = 280;  // [2][4 blk][16 scan], index 0 unused
+
+enum MbType : uint8_t { kMbP16x16 = 0, kMbI16x16 = 1 };
+
+struct MbInfo {
+    int16_t mvx, mvy;  // quarter-pel
+    uint8_t type;      // MbType
+    uint8_t cbp;       // bits 0..3 luma 8x8, bits 4..5 chroma (0/1/2)
+    uint8_t i16_mode;  // Intra16x16 prediction mode
+    uint8_t chroma_mode;
+    uint8_t nz_luma[16];  // TotalCoeff per 4x4 block, raster (by*4+bx)
+    uint8_t nz_cb[4];     // chroma AC TotalCoeff, raster 2x2
+    uint8_t nz_cr[4];
+    uint8_t skip;  // set by k_cavlc
+    uint8_t pad[3];
+};
+static_assert(sizeof(MbInfo) == 36, "MbInfo layout");
+
+// Per-frame state, written by the host into pinned memory and copied to the device at
+// the start of every frame (one memcpy node), so a captured graph replays correctly.
+struct FrameState {
+    const uint8_t* ref_y;
+    const uint8_t* ref_uv;
+    uint8_t* rec_y;
+    uint8_t* rec_uv;
+    int32_t idr;
+    int32_t frame_num;
+    int32_t idr_pic_id;
+    int32_t qp;
+    int32_t slice_rows;  // MB rows per slice
+    int32_t num_slices;
+    int32_t search_range;  // integer-pel full-search radius
+    int32_t subpel;        // 1 = quarter-pel refinement
+    int32_t deblock_off;   // disable_deblocking_filter_idc
+    int32_t pic_init_qp;
+    int32_t chroma_qp_offset;
+    int32_t log2_max_frame_num;
+    int32_t pad[2];
+};
+
+// Header written at the start of the device output / host output buffer.
+struct OutHeader {
+    uint32_t total_bytes;  // payload bytes (all slices, byte aligned)
+    uint32_t num_slices;
+    uint32_t overflow;     // nonzero if any MB exceeded its slot
+    uint32_t pad;
+};
+constexpr int kMaxSlices = 1024;
+// host buffer: OutHeader | uint32 slice_off[kMaxSlices] | uint32 slice_len[kMaxSlices] | payload
+constexpr size_t kOutPayloadOffset = sizeof(OutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
+
+struct Geometry {
+    int width, height;  // display size
+    int mb_w, mb_h;
+    int pitch;          // luma pitch (bytes); UV plane has the same pitch
+    int coded_w, coded_h;  // mb_w*16, mb_h*16
+};
+
+// Device buffers owned by the GPU encoder.
+struct DeviceBuffers {
+    FrameState* fs;         // device copy of the frame state
+    MbInfo* mb;             // [nmb]
+    int16_t* coef;          // [nmb * kCoefStride]
+    uint32_t* slot;         // [nmb * kSlotWords]
+    uint32_t* slot_bits;    // [nmb]
+    uint32_t* unit_off;     // [nmb] absolute bit offset of the MB unit (incl. skip run prefix)
+    int32_t* skip_run;      // [nmb] skip run preceding a coded MB, -1 for skipped MBs
+    uint32_t* slice_info;   // [4 * kMaxSlices]: hdr_bits, byte_off, bytes, trailing_run
+    uint32_t* out;          // device payload words (bswapped), OutHeader-sized prefix excluded
+    size_t out_words;
+    OutHeader* out_hdr;     // device header
+};
+
+// Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.
+void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream);
+void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                  hipStream_t stream);
+void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                  hipStream_t stream);
+void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
+
+}  // namespace h264
+}  // namespace mx

@@ -1,0 +1,175 @@
+// Macroblock-level syntax helpers shared by the HIP kernels and the CPU encoder:
+// neighbour availability, nC prediction, motion-vector prediction / P_Skip decision and
+// the per-"role" CAVLC coding of one macroblock (role 0 = header, 1 = Intra16x16 DC,
+// 2..17 = luma 4x4 blocks in blkIdx order, 18/19 = chroma DC, 20..27 = chroma AC).
+// Coding roles in ascending order reproduces macroblock_layer() syntax order.
+#pragma once
+#include "h264_core.h"
+#include "h264_gpu.h"
+
+namespace mx {
+namespace h264 {
+
+constexpr int kNumRoles = 28;
+
+struct Avail {
+    bool left, top, topright, topleft;
+};
+
+MXHD Avail mb_avail(const Geometry& g, int mbx, int mby, int slice_rows) {
+    Avail a;
+    const bool top_same_slice = mby > 0 && (mby / slice_rows) == ((mby - 1) / slice_rows);
+    a.left = mbx > 0;
+    a.top = top_same_slice;
+    a.topright = top_same_slice && mbx < g.mb_w - 1;
+    a.topleft = top_same_slice && mbx > 0;
+    return a;
+}
+
+MXHD int combine_nc(bool ha, int na, bool hb, int nb) {
+    if (ha && hb) return (na + nb + 1) >> 1;
+    if (ha) return na;
+    if (hb) return nb;
+    return 0;
+}
+
+MXHD MvNb mv_nb(const MbInfo* mbs, int idx, bool avail) {
+    MvNb n;
+    n.avail = avail;
+    n.ref = -1;
+    n.mv = Mv{0, 0};
+    if (!avail) return n;
+    const MbInfo& m = mbs[idx];
+    if (m.type != kMbI16x16) {
+        n.ref = 0;
+        n.mv = Mv{m.mvx, m.mvy};
+    }
+    return n;
+}
+
+// P_Skip decision + mvd for macroblock mbi (type P16x16).  Returns true for P_Skip.
+MXHD bool decide_skip(const Geometry& g, const MbInfo* mbs, int mbi, const Avail& av, int* mvdx, int* mvdy) {
+    const MbInfo& m = mbs[mbi];
+    *mvdx = 0;
+    *mvdy = 0;
+    if (m.type != kMbP16x16) return false;
+    const MvNb a = mv_nb(mbs, mbi - 1, av.left);
+    const MvNb b = mv_nb(mbs, mbi - g.mb_w, av.top);
+    MvNb c = mv_nb(mbs, mbi - g.mb_w + 1, av.topright);
+    if (!av.topright) c = mv_nb(mbs, mbi - g.mb_w - 1, av.topleft);
+    const Mv pskip = predict_mv_skip(a, b, c);
+    const Mv p = predict_mv16x16(a, b, c);
+    *mvdx = m.mvx - p.x;
+    *mvdy = m.mvy - p.y;
+    return m.cbp == 0 && m.mvx == pskip.x && m.mvy == pskip.y;
+}
+
+template <class W>
+MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mbs, const MbInfo& m,
+                    const int16_t* mc, int mbi, const Avail& av, int mvdx, int mvdy) {
+    const bool intra = m.type == kMbI16x16;
+    const int cbp = m.cbp;
+    const int cbp_l = cbp & 15, cbp_c = cbp >> 4;
+    const MbInfo* ml = av.left ? &mbs[mbi - 1] : nullptr;
+    const MbInfo* mt = av.top ? &mbs[mbi - g.mb_w] : nullptr;
+    if (role == 0) {
+        if (intra) {
+            const int mbtype = 1 + m.i16_mode + 4 * cbp_c + (cbp_l ? 12 : 0);
+            put_ue(w, (uint32_t)(idr ? mbtype : 5 + mbtype));
+            put_ue(w, m.chroma_mode);
+            put_se(w, 0);  // mb_qp_delta
+        } else {
+            put_ue(w, 0);  // P_L0_16x16
+            put_se(w, mvdx);
+            put_se(w, mvdy);
+            put_ue(w, (uint32_t)cbp_to_codenum(cbp, false));
+            if (cbp) put_se(w, 0);
+        }
+        return;
+    }
+    int c[16];
+    if (role == 1) {
+        if (!intra) return;
+        const int nc = combine_nc(av.left, ml ? ml->nz_luma[3] : 0, av.top, mt ? mt->nz_luma[12] : 0);
+        for (int k = 0; k < 16; ++k) c[k] = mc[kCoefLumaDc + k];
+        cavlc_block(w, c, 16, nc);
+        return;
+    }
+    if (role <= 17) {
+        const int b = role - 2;
+        if (!(cbp_l & (1 << (b >> 2)))) return;
+        const int bx = kBlkX[b], by = kBlkY[b];
+        const bool ha = bx > 0 || av.left, hb = by > 0 || av.top;
+        const int na = bx > 0 ? m.nz_luma[by * 4 + bx - 1] : (ml ? ml->nz_luma[by * 4 + 3] : 0);
+        const int nb = by > 0 ? m.nz_luma[(by - 1) * 4 + bx] : (mt ? mt->nz_luma[12 + bx] : 0);
+        const int nc = combine_nc(ha, na, hb, nb);
+        if (intra) {
+            for (int k = 0; k < 15; ++k) c[k] = mc[kCoefLuma + b * 16 + 1 + k];
+            cavlc_block(w, c, 15, nc);
+        } else {
+            for (int k = 0; k < 16; ++k) c[k] = mc[kCoefLuma + b * 16 + k];
+            cavlc_block(w, c, 16, nc);
+        }
+        return;
+    }
+    if (role <= 19) {
+        if (!cbp_c) return;
+        const int comp = role - 18;
+        for (int k = 0; k < 4; ++k) c[k] = mc[kCoefChromaDc + comp * 4 + k];
+        cavlc_block(w, c, 4, -1);
+        return;
+    }
+    if (role < kNumRoles) {
+        if (cbp_c != 2) return;
+        const int comp = (role - 20) >> 2, cb = (role - 20) & 3, bx = cb & 1, by = cb >> 1;
+        const uint8_t* own = comp ? m.nz_cr : m.nz_cb;
+        const uint8_t* lft = ml ? (comp ? ml->nz_cr : ml->nz_cb) : nullptr;
+        const uint8_t* top = mt ? (comp ? mt->nz_cr : mt->nz_cb) : nullptr;
+        const bool ha = bx > 0 || av.left, hb = by > 0 || av.top;
+        const int na = bx > 0 ? own[by * 2] : (lft ? lft[by * 2 + 1] : 0);
+        const int nb = by > 0 ? own[bx] : (top ? top[2 + bx] : 0);
+        const int nc = combine_nc(ha, na, hb, nb);
+        for (int k = 0; k < 15; ++k) c[k] = mc[kCoefChromaAc + (comp * 4 + cb) * 16 + 1 + k];
+        cavlc_block(w, c, 15, nc);
+    }
+}
+
+MXHD SliceParams make_slice_params(int first_mb, int idr, int frame_num, int log2_max_frame_num, int idr_pic_id,
+                                   int qp_delta, int deblock_off) {
+    SliceParams sp;
+    sp.first_mb = first_mb;
+    sp.idr = idr;
+    sp.frame_num = frame_num;
+    sp.log2_max_frame_num = log2_max_frame_num;
+    sp.idr_pic_id = idr_pic_id;
+    sp.qp_delta = qp_delta;
+    sp.disable_deblock = deblock_off;
+    return sp;
+}
+
+// ---- per-block transform pipelines (same arithmetic on both encoders)
+
+// Inter luma block: residual (raster) -> levels (scan order) + reconstructed residual.
+MXHD int luma_block_inter(const int* res, int qp, int* zscan, int* rres) {
+    int y[16], z[16], d[16];
+    fdct4x4(res, y);
+    const int nz = quant4x4(y, z, qp, false, 0);
+    for (int k = 0; k < 16; ++k) zscan[k] = z[kZigzag4x4[k]];
+    dequant4x4(z, d, qp, 0);
+    idct4x4(d, rres);
+    return nz;
+}
+
+// ME cost shared by both encoders.
+MXHD uint32_t me_cost(uint32_t sad, int lambda, int mvx, int mvy) {
+    return sad + (uint32_t)(lambda * (mvd_bits(mvx) + mvd_bits(mvy)));
+}
+
+// Sub-pel refinement neighbour k (0..7) offsets.
+MXHD void subpel_offset(int k, int* dx, int* dy) {
+    *dx = (k < 3) ? (k - 1) : (k == 3 ? -1 : (k == 4 ? 1 : (k - 6)));
+    *dy = (k < 3) ? -1 : ((k == 3 || k == 4) ? 0 : 1);
+}
+
+}  // namespace h264
+}  // namespace mx

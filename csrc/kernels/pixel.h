@@ -1,0 +1,52 @@
+// Pixel kernels (SURVEY.md C40 synthetic desktop, C42 CSC/scale, K7 composite).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mx {
+namespace pix {
+
+// Parameters of the synthetic desktop frame (animated noise + gears + scrolling text +
+// moving window + frame-id/timestamp barcode).
+struct SynthParams {
+    int width, height;      // frame size
+    int pitch;              // bytes per BGRx row
+    uint32_t frame_id;      // encoded in the barcode
+    uint32_t timestamp_us;  // encoded in the barcode (capture clock, low 32 bits)
+    float t;                // animation time in seconds
+    int origin_x, origin_y; // offset of this frame inside a larger wall (tile rendering)
+    int wall_w, wall_h;     // full desktop size (== width/height for a single session)
+    int noise;              // 1 = animated-noise panel on
+    int cursor_x, cursor_y; // remote cursor position (-1 = hidden)
+};
+
+// Barcode geometry: 64 bits (frame_id, timestamp_us), 8x8-pixel cells, two rows of 32
+// cells, drawn at the top-left of the desktop with a one-cell quiet zone.
+constexpr int kBarCell = 8;
+constexpr int kBarX = 8, kBarY = 8;
+
+void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream);
+
+// BGRx -> NV12 (BT.709 limited range), padding the output to (coded_w, coded_h) by edge
+// replication.  Output Y plane pitch = UV plane pitch = out_pitch.
+void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_t* y, uint8_t* uv, int out_pitch,
+                         int coded_w, int coded_h, hipStream_t stream);
+
+// Fused separable Lanczos-3 resample (in_w x in_h -> out_w x out_h) + BT.709 CSC into
+// NV12, LDS-tiled.  `weights` from make_lanczos_tables (device memory).
+struct LanczosTables {
+    int out_w, out_h, taps_x, taps_y;
+    const int* x0;      // [out_w] first input column
+    const float* wx;    // [out_w * taps_x]
+    const int* y0;      // [out_h]
+    const float* wy;    // [out_h * taps_y]
+};
+void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
+                          uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream);
+
+// Copy a BGRx tile into a larger BGRx frame at (dx, dy) (tiled-wall composite).
+void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,
+                      hipStream_t stream);
+
+}  // namespace pix
+}  // namespace mx

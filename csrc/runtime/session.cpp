@@ -1,0 +1,191 @@
+#include "session.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "../common/hip_check.h"
+
+namespace mx {
+
+// ------------------------------------------------------------------ FramePool
+FramePool::FramePool(int width, int height, int slots) : w_(width), h_(height) {
+    if (slots < 1) throw std::invalid_argument("FramePool needs >= 1 slot");
+    pitch_ = ((width * 4) + 255) & ~255;
+    buf_.resize(slots, nullptr);
+    gen_.assign(slots, 0);
+    for (auto& b : buf_) HIP_CHECK(hipMalloc(&b, (size_t)pitch_ * height));
+}
+
+FramePool::~FramePool() {
+    for (auto b : buf_) hipFree(b);
+}
+
+int FramePool::acquire() {
+    const int s = next_;
+    next_ = (next_ + 1) % (int)buf_.size();
+    gen_[s] = ++counter_;
+    return s;
+}
+
+// ------------------------------------------------------------------ Lanczos tables
+static double lanczos3(double x) {
+    x = std::fabs(x);
+    if (x < 1e-9) return 1.0;
+    if (x >= 3.0) return 0.0;
+    const double px = M_PI * x;
+    return 3.0 * std::sin(px) * std::sin(px / 3.0) / (px * px);
+}
+
+void make_lanczos_table(int in_size, int out_size, std::vector<int>& start, std::vector<float>& weights, int& taps) {
+    const double s = (double)in_size / out_size;
+    const double f = std::max(1.0, s);
+    const double support = 3.0 * f;
+    taps = (int)std::ceil(2.0 * support) + 1;
+    start.resize(out_size);
+    weights.assign((size_t)out_size * taps, 0.f);
+    for (int o = 0; o < out_size; ++o) {
+        const double center = (o + 0.5) * s - 0.5;
+        const int x0 = (int)std::floor(center - support) + 1;
+        start[o] = x0;
+        double sum = 0;
+        std::vector<double> w(taps);
+        for (int k = 0; k < taps; ++k) {
+            w[k] = lanczos3((x0 + k - center) / f);
+            sum += w[k];
+        }
+        for (int k = 0; k < taps; ++k) weights[(size_t)o * taps + k] = (float)(w[k] / sum);
+    }
+}
+
+// ------------------------------------------------------------------ Session
+int64_t Session::now_us() {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
+    if (cfg_.out_width <= 0) cfg_.out_width = cfg_.width;
+    if (cfg_.out_height <= 0) cfg_.out_height = cfg_.height;
+    cfg_.enc.width = cfg_.out_width;
+    cfg_.enc.height = cfg_.out_height;
+    cfg_.enc.fps = cfg_.fps;
+    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    pool_ = std::make_unique<FramePool>(cfg_.width, cfg_.height, cfg_.pool_slots);
+    enc_ = std::make_unique<h264::GpuH264Encoder>(cfg_.enc, stream_);
+    const h264::Geometry& g = enc_->geometry();
+    HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
+    HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));
+    HIP_CHECK(hipHostMalloc(&staging_, (size_t)pool_->pitch() * cfg_.height, hipHostMallocDefault));
+    scale_ = cfg_.out_width != cfg_.width || cfg_.out_height != cfg_.height;
+    if (scale_) {
+        std::vector<int> sx, sy;
+        std::vector<float> wx, wy;
+        int tx, ty;
+        make_lanczos_table(cfg_.width, cfg_.out_width, sx, wx, tx);
+        make_lanczos_table(cfg_.height, cfg_.out_height, sy, wy, ty);
+        const size_t bytes = (sx.size() + sy.size()) * 4 + (wx.size() + wy.size()) * 4;
+        HIP_CHECK(hipMalloc(&lt_mem_, bytes));
+        char* p = static_cast<char*>(lt_mem_);
+        lt_.out_w = cfg_.out_width;
+        lt_.out_h = cfg_.out_height;
+        lt_.taps_x = tx;
+        lt_.taps_y = ty;
+        lt_.x0 = reinterpret_cast<const int*>(p);
+        HIP_CHECK(hipMemcpy(p, sx.data(), sx.size() * 4, hipMemcpyHostToDevice));
+        p += sx.size() * 4;
+        lt_.y0 = reinterpret_cast<const int*>(p);
+        HIP_CHECK(hipMemcpy(p, sy.data(), sy.size() * 4, hipMemcpyHostToDevice));
+        p += sy.size() * 4;
+        lt_.wx = reinterpret_cast<const float*>(p);
+        HIP_CHECK(hipMemcpy(p, wx.data(), wx.size() * 4, hipMemcpyHostToDevice));
+        p += wx.size() * 4;
+        lt_.wy = reinterpret_cast<const float*>(p);
+        HIP_CHECK(hipMemcpy(p, wy.data(), wy.size() * 4, hipMemcpyHostToDevice));
+    }
+    HIP_CHECK(hipEventCreate(&ev_start_));
+    t0_us_ = now_us();
+}
+
+Session::~Session() {
+    if (stream_) hipStreamSynchronize(stream_);
+    enc_.reset();
+    pool_.reset();
+    hipFree(nv12_y_);
+    hipFree(nv12_uv_);
+    hipHostFree(staging_);
+    if (lt_mem_) hipFree(lt_mem_);
+    hipEventDestroy(ev_start_);
+    hipStreamDestroy(stream_);
+}
+
+void Session::convert_and_encode(int slot, bool force_idr) {
+    const h264::Geometry& g = enc_->geometry();
+    if (scale_) {
+        pix::launch_scale_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, lt_, nv12_y_, nv12_uv_,
+                                  g.pitch, g.coded_w, g.coded_h, stream_);
+    } else {
+        pix::launch_bgrx_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, nv12_y_, nv12_uv_,
+                                 g.pitch, g.coded_w, g.coded_h, stream_);
+    }
+    HIP_CHECK(hipGetLastError());
+    enc_->submit(nv12_y_, nv12_uv_, force_idr);
+    pending_ = true;
+}
+
+void Session::submit_synthetic(bool force_idr) {
+    if (pending_) throw std::logic_error("Session: collect() before the next submit");
+    const int slot = pool_->acquire();
+    t_capture_ = now_us();
+    pix::SynthParams p;
+    p.width = cfg_.width;
+    p.height = cfg_.height;
+    p.pitch = pool_->pitch();
+    p.frame_id = frame_id_;
+    p.timestamp_us = (uint32_t)(t_capture_ - t0_us_);
+    p.t = (float)frame_id_ / (float)std::max(1, cfg_.fps);
+    p.origin_x = 0;
+    p.origin_y = 0;
+    p.wall_w = cfg_.width;
+    p.wall_h = cfg_.height;
+    p.noise = cfg_.noise;
+    p.cursor_x = cursor_x_;
+    p.cursor_y = cursor_y_;
+    HIP_CHECK(hipEventRecord(ev_start_, stream_));
+    pix::launch_synth(pool_->data(slot), p, stream_);
+    HIP_CHECK(hipGetLastError());
+    convert_and_encode(slot, force_idr);
+}
+
+void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
+    if (pending_) throw std::logic_error("Session: collect() before the next submit");
+    const int slot = pool_->acquire();
+    t_capture_ = now_us();
+    const int row = cfg_.width * 4;
+    for (int r = 0; r < cfg_.height; ++r)
+        std::memcpy(staging_ + (size_t)r * pool_->pitch(), host_bgrx + (size_t)r * host_pitch, row);
+    HIP_CHECK(hipEventRecord(ev_start_, stream_));
+    HIP_CHECK(hipMemcpyAsync(pool_->data(slot), staging_, (size_t)pool_->pitch() * cfg_.height,
+                             hipMemcpyHostToDevice, stream_));
+    convert_and_encode(slot, force_idr);
+}
+
+FrameResult Session::collect() {
+    if (!pending_) throw std::logic_error("Session: nothing submitted");
+    pending_ = false;
+    FrameResult r;
+    const std::vector<uint8_t>& au = enc_->collect();
+    r.t_encoded_us = now_us();
+    r.au = au;
+    r.frame_id = frame_id_++;
+    r.t_capture_us = t_capture_ - t0_us_;
+    r.t_encoded_us -= t0_us_;
+    const h264::FrameStats& st = enc_->last_stats();
+    r.idr = st.idr;
+    r.qp = st.qp;
+    r.gpu_ms = st.encode_ms;
+    return r;
+}
+
+}  // namespace mx

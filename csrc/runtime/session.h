@@ -1,0 +1,126 @@
+// Per-GPU streaming session: frame source -> colour conversion (+ scale) -> H.264 encode,
+// driven on HIP streams (SURVEY.md C41 frame pool, C44 pipeline scheduler).
+//
+// Replaces the reference's GStreamer pipeline `ximagesrc ! cudaupload ! cudaconvert !
+// nvh264enc` (selkies, launched from selkies-gstreamer-entrypoint.sh:44-47): the desktop
+// framebuffer lives in HBM (synthetic source) or is uploaded from pinned host memory
+// (X11 SHM capture), and only the encoded bitstream crosses PCIe.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "../codec/h264_encoder.h"
+#include "../kernels/pixel.h"
+
+namespace mx {
+
+// HBM ring of BGRx frames with generation counters (use-after-recycle detection).
+class FramePool {
+   public:
+    FramePool(int width, int height, int slots);
+    ~FramePool();
+    FramePool(const FramePool&) = delete;
+    FramePool& operator=(const FramePool&) = delete;
+    int width() const { return w_; }
+    int height() const { return h_; }
+    int pitch() const { return pitch_; }
+    int slots() const { return (int)buf_.size(); }
+    // Acquire the next slot for writing; returns its index and bumps its generation.
+    int acquire();
+    uint8_t* data(int slot) const { return buf_[slot]; }
+    uint64_t generation(int slot) const { return gen_[slot]; }
+    // True if `slot` still holds generation `gen` (not recycled).
+    bool valid(int slot, uint64_t gen) const { return gen_[slot] == gen; }
+
+   private:
+    int w_, h_, pitch_;
+    std::vector<uint8_t*> buf_;
+    std::vector<uint64_t> gen_;
+    int next_ = 0;
+    uint64_t counter_ = 0;
+};
+
+struct SessionConfig {
+    int width = 1920;       // desktop (capture) size
+    int height = 1080;
+    int out_width = 0;      // encode size; 0 = same as desktop (no scaling)
+    int out_height = 0;
+    int fps = 60;
+    int noise = 1;          // synthetic animated-noise panel
+    int pool_slots = 3;
+    h264::EncoderConfig enc;  // width/height overwritten from out size
+};
+
+struct FrameResult {
+    uint32_t frame_id = 0;
+    int64_t t_capture_us = 0;  // host clock when the frame was rendered/captured
+    int64_t t_encoded_us = 0;  // host clock when the access unit was available
+    double gpu_ms = 0;         // device time render->bitstream (events)
+    int idr = 0;
+    int qp = 0;
+    std::vector<uint8_t> au;
+};
+
+class Session {
+   public:
+    explicit Session(const SessionConfig& cfg);
+    ~Session();
+    Session(const Session&) = delete;
+    Session& operator=(const Session&) = delete;
+
+    // Synthetic desktop frame -> encode.  `submit` enqueues, `collect` waits.
+    void submit_synthetic(bool force_idr = false);
+    // Externally captured BGRx frame (host memory, e.g. X11 SHM) -> upload -> encode.
+    void submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr = false);
+    FrameResult collect();
+    FrameResult step(bool force_idr = false) {
+        submit_synthetic(force_idr);
+        return collect();
+    }
+
+    void set_cursor(int x, int y) {
+        cursor_x_ = x;
+        cursor_y_ = y;
+    }
+    void request_idr() { enc_->common().request_idr(); }
+    void set_bitrate(int kbps) { enc_->common().set_bitrate(kbps); }
+    const SessionConfig& config() const { return cfg_; }
+    hipStream_t stream() const { return stream_; }
+    h264::GpuH264Encoder& encoder() { return *enc_; }
+    FramePool& pool() { return *pool_; }
+    // Device pointers of the NV12 frame fed to the encoder (tests / wall composite).
+    const uint8_t* nv12_y() const { return nv12_y_; }
+    const uint8_t* nv12_uv() const { return nv12_uv_; }
+    int nv12_pitch() const { return enc_->pitch(); }
+    static int64_t now_us();
+
+   private:
+    void convert_and_encode(int slot, bool force_idr);
+
+    SessionConfig cfg_;
+    hipStream_t stream_ = nullptr;
+    std::unique_ptr<FramePool> pool_;
+    std::unique_ptr<h264::GpuH264Encoder> enc_;
+    uint8_t* nv12_y_ = nullptr;
+    uint8_t* nv12_uv_ = nullptr;
+    uint8_t* staging_ = nullptr;  // pinned upload buffer
+    // Lanczos tables (device) when out size != desktop size
+    bool scale_ = false;
+    pix::LanczosTables lt_{};
+    void* lt_mem_ = nullptr;
+    hipEvent_t ev_start_ = nullptr;
+    uint32_t frame_id_ = 0;
+    int64_t t0_us_ = 0;
+    int64_t t_capture_ = 0;
+    int cursor_x_ = -1, cursor_y_ = -1;
+    bool pending_ = false;
+};
+
+// Host-side Lanczos-3 table generation (shared with the Python reference in tests).
+void make_lanczos_table(int in_size, int out_size, std::vector<int>& start, std::vector<float>& weights, int& taps);
+
+}  // namespace mx

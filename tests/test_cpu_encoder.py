@@ -1,0 +1,83 @@
+"""CPU H.264 encoder (the no-GPU plumbing encoder and the GPU oracle) -> independent
+decoder: the decoded pictures must equal the encoder's reconstruction bit-exactly."""
+import numpy as np
+import pytest
+
+from mxdesk.codec.h264_decoder import Decoder, psnr
+
+
+def synthetic_nv12(w, h, t, seed=0):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    y = 128 + 60 * np.sin((xx + 3 * t) / 7.0) + 40 * np.cos((yy + 2 * t) / 5.0)
+    y = y.astype(np.uint8)
+    y[h // 4: h // 2, 8 + 2 * t: 24 + 2 * t] = 230
+    y[h // 2:, : w // 3] = rng.integers(0, 255, (h - h // 2, w // 3)).astype(np.uint8)  # noise patch
+    uv = np.empty((h // 2, w), np.uint8)
+    uv[:, 0::2] = (128 + 30 * np.sin(xx[::2, ::2] / 9.0 + t)).astype(np.uint8)
+    uv[:, 1::2] = (128 + 30 * np.cos(yy[::2, ::2] / 7.0)).astype(np.uint8)
+    return y, uv
+
+
+def encode_decode(native, w, h, frames, **kw):
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height = w, h
+    cfg.bitrate_kbps = kw.get("bitrate_kbps", 0)
+    cfg.qp = kw.get("qp", 28)
+    cfg.search_range = kw.get("search_range", 8)
+    cfg.subpel = kw.get("subpel", 1)
+    cfg.keyint = kw.get("keyint", 0)
+    enc = native.CpuH264Encoder(cfg)
+    stream, recon, src, sizes = b"", [], [], []
+    for t in range(frames):
+        y, uv = synthetic_nv12(w, h, t)
+        au = enc.encode(y, uv, False)
+        sizes.append(len(au))
+        stream += au
+        recon.append(tuple(p.copy() for p in enc.recon()))
+        src.append(y)
+    dec = Decoder()
+    out = dec.decode(stream)
+    return dec, out, recon, src, sizes, enc
+
+
+@pytest.mark.parametrize("w,h,subpel", [(64, 48, 1), (96, 64, 0), (100, 60, 1), (48, 32, 1)])
+def test_roundtrip_bit_exact(native, w, h, subpel):
+    dec, out, recon, src, sizes, _ = encode_decode(native, w, h, 4, subpel=subpel)
+    assert len(out) == 4
+    for (y, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
+        assert np.array_equal(y, ry)
+        assert np.array_equal(u, ruv[:, 0::2])
+        assert np.array_equal(v, ruv[:, 1::2])
+    for (y, _, _), s in zip(out, src):
+        assert y.shape == (h, w)
+        assert psnr(y, s) > 30
+
+
+def test_static_content_skips(native):
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height, cfg.bitrate_kbps, cfg.qp, cfg.subpel = 64, 48, 0, 30, 0
+    enc = native.CpuH264Encoder(cfg)
+    y, uv = synthetic_nv12(64, 48, 0)
+    big = len(enc.encode(y, uv, False))
+    small = len(enc.encode(y, uv, False))
+    assert enc.stats.skipped_mbs >= 6
+    assert small < big / 4
+
+
+def test_forced_idr_and_keyint(native):
+    dec, out, recon, src, sizes, enc = encode_decode(native, 64, 48, 5, keyint=2)
+    assert dec.stats["i16"] == 12 * 3  # IDR at frames 0, 2, 4
+
+
+def test_rate_control_moves_qp(native):
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps, cfg.bitrate_kbps, cfg.qp = 96, 64, 30, 20, 20
+    cfg.qp_min, cfg.qp_max = 10, 51
+    enc = native.CpuH264Encoder(cfg)
+    qps = []
+    for t in range(12):
+        y, uv = synthetic_nv12(96, 64, t)
+        enc.encode(y, uv, False)
+        qps.append(enc.stats.qp)
+    assert qps[-1] > qps[1]
