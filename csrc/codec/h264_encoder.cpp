@@ -128,6 +128,9 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMemsetAsync(rec_y_[i], 16, ysz, stream_));
         HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
     }
+    hp_pitch_ = (geom_.coded_w + 2 * kHpelPad + 255) & ~255;
+    const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
+    for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     HIP_CHECK(hipMalloc(&buf_.fs, sizeof(FrameState)));
     HIP_CHECK(hipMalloc(&buf_.mb, sizeof(MbInfo) * nmb));
     HIP_CHECK(hipMemsetAsync(buf_.mb, 0, sizeof(MbInfo) * nmb, stream_));
@@ -136,14 +139,13 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     HIP_CHECK(hipMalloc(&buf_.slot_bits, sizeof(uint32_t) * nmb));
     HIP_CHECK(hipMalloc(&buf_.unit_off, sizeof(uint32_t) * nmb));
     HIP_CHECK(hipMalloc(&buf_.skip_run, sizeof(int32_t) * nmb));
-    HIP_CHECK(hipMalloc(&buf_.slice_info, sizeof(uint32_t) * 4 * kMaxSlices));
-    HIP_CHECK(hipMemsetAsync(buf_.slice_info, 0, sizeof(uint32_t) * 4 * kMaxSlices, stream_));
-    // payload capacity: 768 B per MB (intra at low QP stays far below), 16-B rounded
-    buf_.out_words = ((size_t)nmb * 768 + 15) / 16 * 4;
-    HIP_CHECK(hipMalloc(&buf_.out, buf_.out_words * 4));
+    HIP_CHECK(hipMalloc(&buf_.slice_info, sizeof(uint32_t) * kSliceInfo * kMaxSlices));
+    HIP_CHECK(hipMemsetAsync(buf_.slice_info, 0, sizeof(uint32_t) * kSliceInfo * kMaxSlices, stream_));
+    // payload capacity: 768 B per MB (intra at low QP stays far below)
+    buf_.out_bytes = (size_t)nmb * 768;
     HIP_CHECK(hipMalloc(&buf_.out_hdr, sizeof(OutHeader)));
     HIP_CHECK(hipHostMalloc(&fs_host_, sizeof(FrameState), hipHostMallocDefault));
-    host_out_bytes_ = kOutPayloadOffset + buf_.out_words * 4;
+    host_out_bytes_ = kOutPayloadOffset + buf_.out_bytes + 16;
     HIP_CHECK(hipHostMalloc(&host_out_, host_out_bytes_, hipHostMallocMapped));
     std::memset(host_out_, 0, kOutPayloadOffset);
     HIP_CHECK(hipEventCreate(&done_));
@@ -157,6 +159,7 @@ GpuH264Encoder::~GpuH264Encoder() {
         hipFree(rec_y_[i]);
         hipFree(rec_uv_[i]);
     }
+    for (int i = 0; i < 4; ++i) hipFree(hp_[i]);
     hipFree(buf_.fs);
     hipFree(buf_.mb);
     hipFree(buf_.coef);
@@ -165,7 +168,6 @@ GpuH264Encoder::~GpuH264Encoder() {
     hipFree(buf_.unit_off);
     hipFree(buf_.skip_run);
     hipFree(buf_.slice_info);
-    hipFree(buf_.out);
     hipFree(buf_.out_hdr);
     hipHostFree(fs_host_);
     hipHostFree(host_out_);
@@ -177,6 +179,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     if (idr) {
         launch_intra(geom_, buf_, src_y, src_uv, stream_);
     } else {
+        launch_hpel(geom_, fs_host_->ref_y, hp_, hp_pitch_, stream_);
         launch_me(geom_, buf_, src_y, stream_);
         launch_inter(geom_, buf_, src_y, src_uv, stream_);
     }
@@ -207,6 +210,12 @@ void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
     f.pic_init_qp = common_.pic_init_qp();
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
     f.log2_max_frame_num = common_.log2_max_frame_num();
+    const size_t org = (size_t)kHpelPad * hp_pitch_ + kHpelPad;
+    f.hp_pitch = hp_pitch_;
+    f.hp_f = hp_[0] + org;
+    f.hp_h = hp_[1] + org;
+    f.hp_v = hp_[2] + org;
+    f.hp_j = hp_[3] + org;
     HIP_CHECK(hipEventRecord(start_, stream_));
     HIP_CHECK(hipMemcpyAsync(buf_.fs, fs_host_, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
     enqueue_kernels(idr, src_y, src_uv);

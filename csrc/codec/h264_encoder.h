@@ -115,6 +115,8 @@ class GpuH264Encoder {
     FrameState* fs_host_ = nullptr;  // pinned
     uint8_t* host_out_ = nullptr;    // pinned, mapped: OutHeader | slice tables | payload
     size_t host_out_bytes_ = 0;
+    uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};  // padded F/H/V/J reference planes
+    int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     int cur_ = 0;  // index of the frame being reconstructed

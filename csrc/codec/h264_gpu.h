@@ -1,8 +1,9 @@
 // Device data layout and host API of the HIP H.264 encoder.
 //
 // Per-frame kernel chain (all on one HIP stream, graph-capturable):
-//   P frame: k_me_full -> k_inter_encode -> k_cavlc -> k_scan -> k_pack -> k_copy_out
-//   I frame: k_intra_rows                 -> k_cavlc -> k_scan -> k_pack -> k_copy_out
+//   P frame: k_me_full -> k_inter_encode -> k_cavlc -> k_scan -> k_pack
+//   I frame: k_intra_rows                 -> k_cavlc -> k_scan -> k_pack
+// k_pack writes the payload straight into pinned host memory (zero-copy).
 // Only the slice payloads (RBSP, byte aligned) leave the GPU; the host adds start
 // codes, NAL headers and emulation-prevention bytes (h264_encoder.cpp).
 #pragma once
@@ -54,8 +55,15 @@ struct FrameState {
     int32_t pic_init_qp;
     int32_t chroma_qp_offset;
     int32_t log2_max_frame_num;
-    int32_t pad[2];
+    int32_t hp_pitch;  // pitch of the padded half-pel planes
+    int32_t pad;
+    // padded reference planes (origin at picture (0,0), valid for x,y in [-kHpelPad, size+kHpelPad))
+    const uint8_t* hp_f;  // full-sample (edge-replicated)
+    const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
+    const uint8_t* hp_v;  // vertical half sample h at (x, y+1/2)
+    const uint8_t* hp_j;  // centre half sample j at (x+1/2, y+1/2)
 };
+constexpr int kHpelPad = 48;
 
 // Header written at the start of the device output / host output buffer.
 struct OutHeader {
@@ -65,6 +73,9 @@ struct OutHeader {
     uint32_t pad;
 };
 constexpr int kMaxSlices = 1024;
+// slice_info fields: 0 header bits, 1 byte offset, 2 bytes, 3 trailing skip run,
+// 4 data-end bit (trailer start), 5 unit-bit prefix at the slice's first MB
+constexpr int kSliceInfo = 8;
 // host buffer: OutHeader | uint32 slice_off[kMaxSlices] | uint32 slice_len[kMaxSlices] | payload
 constexpr size_t kOutPayloadOffset = sizeof(OutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
 
@@ -84,9 +95,8 @@ struct DeviceBuffers {
     uint32_t* slot_bits;    // [nmb]
     uint32_t* unit_off;     // [nmb] absolute bit offset of the MB unit (incl. skip run prefix)
     int32_t* skip_run;      // [nmb] skip run preceding a coded MB, -1 for skipped MBs
-    uint32_t* slice_info;   // [4 * kMaxSlices]: hdr_bits, byte_off, bytes, trailing_run
-    uint32_t* out;          // device payload words (bswapped), OutHeader-sized prefix excluded
-    size_t out_words;
+    uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
+    size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
 };
 
@@ -96,6 +106,9 @@ void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
                   hipStream_t stream);
 void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream);
+// Build the padded F/H/V/J planes of `ref` (luma) into `planes` (4 planes, each
+// hp_pitch x (coded_h + 2*kHpelPad), origin offset applied by the caller via FrameState).
+void launch_hpel(const Geometry& g, const uint8_t* ref_y, uint8_t* const planes[4], int hp_pitch, hipStream_t stream);
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
 
 }  // namespace h264

@@ -14,8 +14,8 @@
 //                   median mv prediction, cbp), lanes 1..27 code one residual block each;
 //                   a wave prefix-sum places every lane's bits in an LDS slot.
 //  * k_scan         one workgroup: skip runs, per-MB and per-slice bit offsets.
-//  * k_pack         one wave per MB / slice: OR the slot bits into the payload.
-//  * k_copy_out     payload -> pinned host memory (zero-copy), exactly total_bytes.
+//  * k_pack         one thread per output word gathers the overlapping header / MB /
+//                   trailer bits and stores the word straight into pinned host memory.
 #include <hip/hip_runtime.h>
 
 #include "h264_core.h"
@@ -81,6 +81,77 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
+// ------------------------------------------------------------------ half-pel planes
+struct Planes {
+    const uint8_t *f, *h, *v, *j;
+    int pitch;
+};
+__device__ __forceinline__ Planes planes_of(const FrameState* fs) {
+    return Planes{fs->hp_f, fs->hp_h, fs->hp_v, fs->hp_j, fs->hp_pitch};
+}
+// Quarter-sample luma value from the precomputed planes (Table 8-12); identical to
+// luma_qpel() on the clamped reference.
+__device__ __forceinline__ int qpel_planes(const Planes& P, int x4, int y4) {
+    const int xi = x4 >> 2, yi = y4 >> 2, xf = x4 & 3, yf = y4 & 3;
+    const int o = yi * P.pitch + xi;
+    const int G = P.f[o];
+    if ((xf | yf) == 0) return G;
+    if (yf == 0) {
+        const int b = P.h[o];
+        if (xf == 2) return b;
+        return ((xf == 1 ? G : (int)P.f[o + 1]) + b + 1) >> 1;
+    }
+    if (xf == 0) {
+        const int hh = P.v[o];
+        if (yf == 2) return hh;
+        return ((yf == 1 ? G : (int)P.f[o + P.pitch]) + hh + 1) >> 1;
+    }
+    if (xf == 2 && yf == 2) return P.j[o];
+    if (xf == 2) return ((yf == 1 ? (int)P.h[o] : (int)P.h[o + P.pitch]) + P.j[o] + 1) >> 1;
+    if (yf == 2) return ((xf == 1 ? (int)P.v[o] : (int)P.v[o + 1]) + P.j[o] + 1) >> 1;
+    const int bb = (yf == 1) ? P.h[o] : P.h[o + P.pitch];
+    const int hh = (xf == 1) ? P.v[o] : P.v[o + 1];
+    return (bb + hh + 1) >> 1;
+}
+
+// LDS-tiled F/H/V/J plane builder: a 64x16 output tile needs a (64+5)x(16+5) clamped
+// sample footprint; the 6-tap horizontal intermediates b1 are kept in LDS as int16 and
+// reused for both H and the centre sample J.
+constexpr int kHpTW = 64, kHpTH = 16;
+__global__ __launch_bounds__(256) void k_hpel(Geometry g, const uint8_t* __restrict__ ref, uint8_t* __restrict__ pf,
+                                              uint8_t* __restrict__ ph, uint8_t* __restrict__ pv,
+                                              uint8_t* __restrict__ pj, int hp_pitch) {
+    __shared__ uint8_t smp[kHpTH + 5][kHpTW + 8];
+    __shared__ int16_t b1[kHpTH + 5][kHpTW];
+    const int px0 = blockIdx.x * kHpTW, py0 = blockIdx.y * kHpTH;  // padded-plane coordinates
+    const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
+    const int tid = threadIdx.x;
+    // samples for rows py0-2 .. py0+kHpTH+2, cols px0-2 .. px0+kHpTW+2 (picture coords = padded - pad)
+    for (int i = tid; i < (kHpTH + 5) * (kHpTW + 5); i += 256) {
+        const int r = i / (kHpTW + 5), c = i - r * (kHpTW + 5);
+        smp[r][c] = (uint8_t)ref_px(ref, g.pitch, g.coded_w, g.coded_h, px0 + c - 2 - kHpelPad, py0 + r - 2 - kHpelPad);
+    }
+    __syncthreads();
+    for (int i = tid; i < (kHpTH + 5) * kHpTW; i += 256) {
+        const int r = i / kHpTW, c = i - r * kHpTW;
+        b1[r][c] = (int16_t)tap6(smp[r][c], smp[r][c + 1], smp[r][c + 2], smp[r][c + 3], smp[r][c + 4], smp[r][c + 5]);
+    }
+    __syncthreads();
+    for (int i = tid; i < kHpTH * kHpTW; i += 256) {
+        const int r = i / kHpTW, c = i - r * kHpTW;
+        const int x = px0 + c, y = py0 + r;
+        if (x >= W || y >= H) continue;
+        const int rr = r + 2, cc = c + 2;
+        const size_t o = (size_t)y * hp_pitch + x;
+        pf[o] = smp[rr][cc];
+        ph[o] = (uint8_t)clip255((b1[rr][c] + 16) >> 5);
+        const int v1 = tap6(smp[rr - 2][cc], smp[rr - 1][cc], smp[rr][cc], smp[rr + 1][cc], smp[rr + 2][cc], smp[rr + 3][cc]);
+        pv[o] = (uint8_t)clip255((v1 + 16) >> 5);
+        const int j1 = tap6(b1[rr - 2][c], b1[rr - 1][c], b1[rr][c], b1[rr + 1][c], b1[rr + 2][c], b1[rr + 3][c]);
+        pj[o] = (uint8_t)clip255((j1 + 512) >> 10);
+    }
+}
+
 // ------------------------------------------------------------------ motion estimation
 constexpr int kMaxRange = 32;
 constexpr int kWinStride = 16 + 2 * kMaxRange + 8;  // bytes per LDS window row (dword padded)
@@ -99,14 +170,17 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     int R = fs->search_range;
     R = R > kMaxRange ? kMaxRange : (R < 1 ? 1 : R);
     const int W = 16 + 2 * R;
-    const uint8_t* ref = fs->ref_y;
+    const Planes P = planes_of(fs);
     const int qp = fs->qp;
     const int lambda = lambda_sad(qp);
 
-    uint8_t* win = reinterpret_cast<uint8_t*>(win32);
-    for (int i = tid; i < W * kWinStride; i += 256) {
-        const int wy = i / kWinStride, wx = i - wy * kWinStride;
-        win[i] = (wx < W) ? (uint8_t)ref_px(ref, g.pitch, g.coded_w, g.coded_h, x0 - R + wx, y0 - R + wy) : 0;
+    // search window from the padded full-sample plane (R + 1 <= kHpelPad: no clamping)
+    for (int i = tid; i < W * (kWinStride / 4); i += 256) {
+        const int wy = i / (kWinStride / 4), wx4 = (i - wy * (kWinStride / 4)) * 4;
+        const uint8_t* src = P.f + (y0 - R + wy) * P.pitch + (x0 - R + wx4);
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)(wx4 + k < W ? src[k] : 0) << (8 * k);
+        win32[i] = v;
     }
     if (tid < 64) {
         const int r = tid >> 2, c = (tid & 3) * 4;
@@ -151,7 +225,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         const int s = src_y[(y0 + py) * g.pitch + x0 + px];
         uint32_t cur_cost;
         {
-            const int p = luma_qpel(ref, g.pitch, g.coded_w, g.coded_h, (x0 + px) * 4 + mvx, (y0 + py) * 4 + mvy);
+            const int p = qpel_planes(P, (x0 + px) * 4 + mvx, (y0 + py) * 4 + mvy);
             int d = abs(s - p);
             d = wave_sum(d);
             __syncthreads();
@@ -166,7 +240,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
                 int ddx, ddy;
                 subpel_offset(k, &ddx, &ddy);
                 const int cx = mvx + ddx * step, cy = mvy + ddy * step;
-                const int p = luma_qpel(ref, g.pitch, g.coded_w, g.coded_h, (x0 + px) * 4 + cx, (y0 + py) * 4 + cy);
+                const int p = qpel_planes(P, (x0 + px) * 4 + cx, (y0 + py) * 4 + cy);
                 int d = wave_sum(abs(s - p));
                 __syncthreads();
                 if ((tid & 63) == 0) sub_cost[tid >> 6] = d;
@@ -207,7 +281,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     const int x0 = mbx * 16, y0 = mby * 16;
     const int qp = fs->qp;
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
-    const uint8_t* ref_y = fs->ref_y;
+    const Planes P = planes_of(fs);
     const uint8_t* ref_uv = fs->ref_uv;
     const int cw = g.coded_w / 2, ch = g.coded_h / 2;
     int mvx = 0, mvy = 0;
@@ -217,7 +291,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         const int r = lane >> 2, c0 = (lane & 3) * 4;
         const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
         for (int k = 0; k < 4; ++k) {
-            const int p = luma_qpel(ref_y, g.pitch, g.coded_w, g.coded_h, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
+            const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
             pred[wave][r * 16 + c0 + k] = (uint8_t)p;
             res[wave][r * 16 + c0 + k] = (int16_t)((int)((sw >> (8 * k)) & 0xff) - p);
         }
@@ -519,229 +593,307 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     for (uint32_t i = lane; i < nwords && i < (uint32_t)kSlotWords; i += 64)
         slot[(size_t)mbi * kSlotWords + i] = lds_slot[wave][i];
     if (lane == 0) {
-        slot_bits[mbi] = total <= kSlotWords * 32u ? total : 0xffffffffu;
+        slot_bits[mbi] = skip ? 0u : (total <= kSlotWords * 32u ? total : 0xffffffffu);
         mbs[mbi].skip = skip ? 1 : 0;
     }
 }
 
 // ------------------------------------------------------------------ scan
 constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 8;
+constexpr int kScanTile = kScanThreads * kScanPer;
 
 __device__ __forceinline__ SliceParams slice_params(const FrameState* fs, int s, int mb_w) {
     return make_slice_params(s * fs->slice_rows * mb_w, fs->idr, fs->frame_num, fs->log2_max_frame_num,
                              fs->idr_pic_id, fs->qp - fs->pic_init_qp, fs->deblock_off);
 }
 
+// Block-wide exclusive scans over 1024 threads (16 waves): wave shuffles + one LDS pass.
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t x = lane < kScanThreads / 64 ? wsum[lane] : 0;
+        uint32_t xi = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(xi, o, 64);
+            if (lane >= o) xi += t;
+        }
+        if (lane < kScanThreads / 64) wsum[lane] = xi - x;
+        if (lane == kScanThreads / 64 - 1) wsum[kScanThreads / 64] = xi;
+    }
+    __syncthreads();
+    const uint32_t r = wsum[w] + incl - v;
+    *total = wsum[kScanThreads / 64];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ int block_excl_max(int v, int* wmax, int init) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl = max(incl, t);
+    }
+    int excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = init;
+    if (lane == 63) wmax[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        int x = lane < kScanThreads / 64 ? wmax[lane] : init;
+        int xi = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(xi, o, 64);
+            if (lane >= o) xi = max(xi, t);
+        }
+        int xe = __shfl_up(xi, 1, 64);
+        if (lane == 0) xe = init;
+        if (lane < kScanThreads / 64) wmax[lane] = xe;
+    }
+    __syncthreads();
+    const int r = max(wmax[w], excl);
+    __syncthreads();
+    return r;
+}
+
+// slot_bits[i]: 0 = P_Skip, 0xffffffff = slot overflow, else coded MB bits (>= 1).
+// Outputs: unit_off[i] absolute bit offset of MB i's unit (skip-run prefix + MB bits),
+// skip_run[i] (-1 for skipped MBs), slice_info[kSliceInfo * s + ...].
 __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameState* __restrict__ fs,
-                                                       const MbInfo* __restrict__ mbs,
                                                        const uint32_t* __restrict__ slot_bits,
                                                        uint32_t* __restrict__ unit_off, int32_t* __restrict__ skip_run,
-                                                       uint32_t* __restrict__ slice_info, uint32_t* __restrict__ out,
-                                                       size_t out_words, OutHeader* __restrict__ hdr) {
-    __shared__ int s_i[kScanThreads];
-    __shared__ uint32_t s_u[kScanThreads];
+                                                       uint32_t* __restrict__ slice_info, size_t out_bytes,
+                                                       OutHeader* __restrict__ hdr) {
+    __shared__ uint32_t sb[kScanTile];
+    __shared__ uint32_t wsum[kScanThreads / 64 + 1];
+    __shared__ int wmax[kScanThreads / 64];
     __shared__ uint32_t s_overflow;
     const int t = threadIdx.x;
     const int nmb = g.mb_w * g.mb_h;
-    const int rows = fs->slice_rows;
+    const int per_slice = fs->slice_rows * g.mb_w;
     const int ns = fs->num_slices;
-    const int per_slice = rows * g.mb_w;
-    const int C = (nmb + kScanThreads - 1) / kScanThreads;
-    const int lo = t * C, hi = min(lo + C, nmb);
+    const bool idr = fs->idr != 0;
     if (t == 0) s_overflow = 0;
-
-    // 1. last coded (non-skipped) MB per chunk -> exclusive max scan
-    int last = -1;
-    for (int i = lo; i < hi; ++i)
-        if (!mbs[i].skip) last = i;
-    s_i[t] = last;
-    __syncthreads();
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        int v = t >= o ? s_i[t - o] : -1;
+    int carry_last = -1;      // last coded MB index before the current tile
+    uint32_t carry_bits = 0;  // unit bits before the current tile
+    for (int base = 0; base < nmb; base += kScanTile) {
+        const int n = min(kScanTile, nmb - base);
+        for (int j = t; j < n; j += kScanThreads) sb[j] = slot_bits[base + j];
         __syncthreads();
-        s_i[t] = max(s_i[t], v);
-        __syncthreads();
-    }
-    int carry = t > 0 ? s_i[t - 1] : -1;
-    __syncthreads();
-    // 2. skip runs and unit bit lengths; local sums
-    uint32_t local = 0;
-    for (int i = lo; i < hi; ++i) {
-        const int s = i / per_slice;
-        const int first = s * per_slice;
-        const int prev = max(carry, first - 1);
-        const bool coded = !mbs[i].skip;
-        uint32_t ub = 0;
-        if (coded) {
-            const int run = i - prev - 1;
-            skip_run[i] = run;
-            uint32_t sb = slot_bits[i];
-            if (sb == 0xffffffffu) {
-                s_overflow = 1;
-                sb = 0;
+        const int j0 = t * kScanPer;
+        int last = -1;
+        for (int k = 0; k < kScanPer; ++k)
+            if (j0 + k < n && sb[j0 + k] != 0) last = base + j0 + k;
+        int prev = block_excl_max(last, wmax, -1);
+        prev = max(prev, carry_last);
+        uint32_t local = 0;
+        uint32_t ub[kScanPer];
+        for (int k = 0; k < kScanPer; ++k) {
+            ub[k] = 0;
+            const int j = j0 + k;
+            if (j >= n) continue;
+            const int i = base + j;
+            const int s = i / per_slice, first = s * per_slice;
+            const int slast = min(first + per_slice, nmb) - 1;
+            const int pv = max(prev, first - 1);
+            uint32_t b = sb[j];
+            if (b != 0) {
+                if (b == 0xffffffffu) {
+                    s_overflow = 1;
+                    b = 1;
+                }
+                const int run = i - pv - 1;
+                skip_run[i] = run;
+                ub[k] = (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b;
+                prev = i;
+            } else {
+                skip_run[i] = -1;
             }
-            ub = (fs->idr ? 0 : ue_len((uint32_t)run)) + sb;
-            carry = i;
-        } else {
-            skip_run[i] = -1;
+            if (i == slast) slice_info[kSliceInfo * s + 3] = (b != 0) ? 0u : (uint32_t)(i - pv);
+            local += ub[k];
         }
-        const int slast = min(first + per_slice, nmb) - 1;
-        if (i == slast) slice_info[4 * s + 3] = coded ? 0u : (uint32_t)(i - prev);
-        unit_off[i] = ub;  // temporarily: unit bits
-        local += ub;
-    }
-    s_u[t] = local;
-    __syncthreads();
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        uint32_t v = t >= o ? s_u[t - o] : 0;
+        uint32_t tile_total;
+        const uint32_t ex = block_excl_sum(local, wsum, &tile_total);
+        uint32_t run_sum = carry_bits + ex;
+        for (int k = 0; k < kScanPer; ++k) {
+            if (j0 + k < n) sb[j0 + k] = run_sum;  // E[i]: exclusive prefix of unit bits
+            run_sum += ub[k];
+        }
         __syncthreads();
-        s_u[t] += v;
+        for (int j = t; j < n; j += kScanThreads) unit_off[base + j] = sb[j];
+        // carry: the last thread's running `prev` is the last coded MB up to the tile end
+        if (t == kScanThreads - 1) wmax[0] = prev;
+        __syncthreads();
+        carry_last = wmax[0];
+        carry_bits += tile_total;
         __syncthreads();
     }
-    uint32_t run_sum = t > 0 ? s_u[t - 1] : 0;
-    for (int i = lo; i < hi; ++i) {  // unit_off <- exclusive global prefix (E[i])
-        const uint32_t ub = unit_off[i];
-        unit_off[i] = run_sum;
-        run_sum += ub;
-    }
-    const uint32_t grand_total = s_u[kScanThreads - 1];
+    const uint32_t grand_total = carry_bits;
     __syncthreads();
-    // 3. per slice sizes (one thread per slice; ns <= kMaxSlices <= kScanThreads)
-    uint32_t sbytes = 0;
-    uint32_t ebase = 0, hbits = 0;
+    // per slice sizes (one thread per slice; ns <= kMaxSlices <= kScanThreads)
+    uint32_t sbytes = 0, ebase = 0, eend = 0, hbits = 0, trail = 0;
     if (t < ns) {
         const int first = t * per_slice;
         const int slast = min(first + per_slice, nmb) - 1;
         ebase = unit_off[first];
-        const uint32_t eend = (slast + 1 < nmb) ? unit_off[slast + 1] : grand_total;
+        eend = (slast + 1 < nmb) ? unit_off[slast + 1] : grand_total;
         BitCounter bc;
         bc.init(nullptr);
         write_slice_header(bc, slice_params(fs, t, g.mb_w));
         hbits = bc.bits;
-        const uint32_t trail = fs->idr ? 0u : slice_info[4 * t + 3];
+        trail = idr ? 0u : slice_info[kSliceInfo * t + 3];
         const uint32_t bits = hbits + (eend - ebase) + (trail ? ue_len(trail) : 0) + 1;
         sbytes = (bits + 7) >> 3;
     }
-    __syncthreads();
-    s_u[t] = sbytes;
-    __syncthreads();
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        uint32_t v = t >= o ? s_u[t - o] : 0;
-        __syncthreads();
-        s_u[t] += v;
-        __syncthreads();
-    }
-    const uint32_t total_bytes = s_u[kScanThreads - 1];
+    uint32_t total_bytes;
+    const uint32_t soff = block_excl_sum(sbytes, wsum, &total_bytes);
     if (t < ns) {
-        slice_info[4 * t + 0] = hbits;
-        slice_info[4 * t + 1] = s_u[t] - sbytes;  // byte offset
-        slice_info[4 * t + 2] = sbytes;
-        s_i[t] = (int)ebase;
+        slice_info[kSliceInfo * t + 0] = hbits;
+        slice_info[kSliceInfo * t + 1] = soff;
+        slice_info[kSliceInfo * t + 2] = sbytes;
+        slice_info[kSliceInfo * t + 4] = soff * 8 + hbits + (eend - ebase);  // data end (trailer start)
+        slice_info[kSliceInfo * t + 5] = ebase;
     }
     __syncthreads();
-    // 4. absolute unit offsets
-    for (int i = lo; i < hi; ++i) {
+    for (int i = t; i < nmb; i += kScanThreads) {
         const int s = i / per_slice;
-        unit_off[i] = slice_info[4 * s + 1] * 8 + slice_info[4 * s + 0] + (unit_off[i] - (uint32_t)s_i[s]);
+        unit_off[i] = slice_info[kSliceInfo * s + 1] * 8 + slice_info[kSliceInfo * s + 0] +
+                      (unit_off[i] - slice_info[kSliceInfo * s + 5]);
     }
-    // 5. zero the payload words that k_pack will OR into
-    const size_t nwords = ((size_t)total_bytes + 3) / 4;
-    const bool over = nwords > out_words;
-    for (size_t i = t; i < nwords && i < out_words; i += kScanThreads) out[i] = 0;
-    __syncthreads();
     if (t == 0) {
+        const bool over = total_bytes > out_bytes;
         hdr->total_bytes = over ? 0 : total_bytes;
         hdr->num_slices = ns;
         hdr->overflow = s_overflow | (over ? 2u : 0u);
     }
 }
 
-// ------------------------------------------------------------------ pack
+// ------------------------------------------------------------------ pack (gather)
+// n bits (1..32) starting at bit b of an MB slot.
+__device__ __forceinline__ uint32_t slot_get(const uint32_t* slot, uint32_t b, int n) {
+    const uint32_t wi = b >> 5, sh = b & 31;
+    const uint64_t hi = ((uint64_t)slot[wi] << 32) | (wi + 1 < (uint32_t)kSlotWords ? slot[wi + 1] : 0u);
+    return (uint32_t)((hi << sh) >> (64 - n));
+}
+
+__device__ __forceinline__ uint32_t mask_bits(int n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1); }
+
+// OR the overlap of segment [s0, s0+len) with output word [W0, W0+32) into acc; getbits
+// returns `n` segment-relative bits starting at `a`.
+template <class F>
+__device__ __forceinline__ void overlap(uint32_t& acc, uint32_t W0, uint32_t s0, uint32_t len, F getbits) {
+    const uint32_t lo = max(W0, s0), hi = min(W0 + 32, s0 + len);
+    if (lo >= hi) return;
+    const int n = (int)(hi - lo);
+    const uint32_t bits = getbits(lo - s0, n) & mask_bits(n);
+    acc |= bits << (W0 + 32 - hi);
+}
+
+// One thread per output word; assembles the word from the slice header, the MB units and
+// the slice trailer that overlap it, and stores it (big-endian) straight into pinned
+// host memory.  No atomics and no zero-fill pass.
 __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __restrict__ fs,
-                                              const MbInfo* __restrict__ mbs, const uint32_t* __restrict__ slot,
+                                              const uint32_t* __restrict__ slot,
                                               const uint32_t* __restrict__ slot_bits,
                                               const uint32_t* __restrict__ unit_off,
                                               const int32_t* __restrict__ skip_run,
-                                              const uint32_t* __restrict__ slice_info, uint32_t* __restrict__ out,
-                                              const OutHeader* __restrict__ hdr) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nmb = g.mb_w * g.mb_h;
-    const int u = blockIdx.x * 4 + wave;
-    if (hdr->overflow) return;
-    if (u < nmb) {
-        const int run = skip_run[u];
-        if (run < 0) return;
-        uint32_t pos = unit_off[u];
-        if (!fs->idr) {
-            if (lane == 0) {
-                OrWriter<true> w;
-                w.init(out, pos);
-                put_ue(w, (uint32_t)run);
-                w.flush();
-            }
-            pos += ue_len((uint32_t)run);
-        }
-        const uint32_t nb = slot_bits[u];
-        const uint32_t nw = (nb + 31) >> 5;
-        const uint32_t* src = slot + (size_t)u * kSlotWords;
-        for (uint32_t i = lane; i < nw; i += 64) {
-            const uint32_t v = src[i];
-            const int n = (i == nw - 1) ? (int)(nb - 32 * i) : 32;
-            OrWriter<true> w;
-            w.init(out, pos + 32 * i);
-            w.emit(v, n);
-        }
-        return;
-    }
-    const int s = u - nmb;
-    if (s >= fs->num_slices || lane != 0) return;
-    const uint32_t hbits = slice_info[4 * s + 0];
-    const uint32_t byte_off = slice_info[4 * s + 1];
-    const uint32_t bytes = slice_info[4 * s + 2];
-    OrWriter<true> w;
-    w.init(out, byte_off * 8);
-    write_slice_header(w, slice_params(fs, s, g.mb_w));
-    w.flush();
-    // trailer: optional trailing mb_skip_run, then rbsp_stop_one_bit at the end of data
-    const int per_slice = fs->slice_rows * g.mb_w;
-    const int first = s * per_slice, slast = min(first + per_slice, nmb) - 1;
-    // find end of data: the last coded MB's unit end, or header end if none
-    const uint32_t trail = fs->idr ? 0u : slice_info[4 * s + 3];
-    uint32_t data_end = byte_off * 8 + hbits;
-    for (int i = slast; i >= first; --i) {
-        if (skip_run[i] >= 0) {
-            data_end = unit_off[i] + (fs->idr ? 0 : ue_len((uint32_t)skip_run[i])) + slot_bits[i];
-            break;
-        }
-    }
-    OrWriter<true> t2;
-    t2.init(out, data_end);
-    if (trail) put_ue(t2, trail);
-    t2.put(1, 1);
-    t2.flush();
-    (void)bytes;
-}
-
-// ------------------------------------------------------------------ copy to host
-__global__ __launch_bounds__(256) void k_copy_out(const uint32_t* __restrict__ out, const OutHeader* __restrict__ hdr,
-                                                  const uint32_t* __restrict__ slice_info, uint8_t* __restrict__ host) {
-    const uint32_t total = hdr->total_bytes;
-    const uint32_t ns = hdr->num_slices;
-    const size_t gid = blockIdx.x * 256 + threadIdx.x;
+                                              const uint32_t* __restrict__ slice_info,
+                                              const OutHeader* __restrict__ hdr, uint8_t* __restrict__ host) {
+    const OutHeader h = *hdr;
+    const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * 256;
-    if (gid == 0) *reinterpret_cast<OutHeader*>(host) = *hdr;
+    if (gid == 0) *reinterpret_cast<OutHeader*>(host) = h;
     uint32_t* hs = reinterpret_cast<uint32_t*>(host + sizeof(OutHeader));
-    for (size_t s = gid; s < ns; s += stride) {
-        hs[s] = slice_info[4 * s + 1];
-        hs[kMaxSlices + s] = slice_info[4 * s + 2];
+    for (size_t s = gid; s < h.num_slices; s += stride) {
+        hs[s] = slice_info[kSliceInfo * s + 1];
+        hs[kMaxSlices + s] = slice_info[kSliceInfo * s + 2];
     }
-    const size_t n16 = ((size_t)total + 15) / 16;
-    const uint4* src = reinterpret_cast<const uint4*>(out);
-    uint4* dst = reinterpret_cast<uint4*>(host + kOutPayloadOffset);
-    for (size_t i = gid; i < n16; i += stride) dst[i] = src[i];
+    if (h.overflow) return;
+    const int nmb = g.mb_w * g.mb_h;
+    const int per_slice = fs->slice_rows * g.mb_w;
+    const bool idr = fs->idr != 0;
+    const int ns = (int)h.num_slices;
+    const uint32_t nwords = (h.total_bytes + 3) / 4;
+    uint32_t* out = reinterpret_cast<uint32_t*>(host + kOutPayloadOffset);
+    for (size_t w = gid; w < nwords; w += stride) {
+        const uint32_t W0 = (uint32_t)w * 32;
+        // last slice starting at or before W0
+        int lo = 0, hi = ns - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (slice_info[kSliceInfo * mid + 1] * 8 <= W0) lo = mid; else hi = mid - 1;
+        }
+        uint32_t acc = 0;
+        for (int s = lo; s < ns; ++s) {
+            const uint32_t sbit = slice_info[kSliceInfo * s + 1] * 8;
+            if (sbit >= W0 + 32) break;
+            const uint32_t hbits = slice_info[kSliceInfo * s + 0];
+            const uint32_t dend = slice_info[kSliceInfo * s + 4];
+            const uint32_t trail = idr ? 0u : slice_info[kSliceInfo * s + 3];
+            // header
+            if (sbit < W0 + 32 && sbit + hbits > W0) {
+                uint32_t hw[4] = {0, 0, 0, 0};
+                BitWriter bw;
+                bw.init(hw);
+                write_slice_header(bw, slice_params(fs, s, g.mb_w));
+                bw.flush();
+                overlap(acc, W0, sbit, hbits, [&](uint32_t a, int n) { return slot_get(hw, a, n); });
+            }
+            // macroblock units overlapping the word
+            const int first = s * per_slice, slast = min(first + per_slice, nmb) - 1;
+            if (dend > W0 && sbit + hbits < W0 + 32) {
+                int a = first, b = slast;
+                while (a < b) {  // last MB with unit_off <= W0
+                    const int mid = (a + b + 1) >> 1;
+                    if (unit_off[mid] <= W0) a = mid; else b = mid - 1;
+                }
+                for (int i = a; i <= slast; ++i) {
+                    const uint32_t off = unit_off[i];
+                    if (off >= W0 + 32) break;
+                    const int run = skip_run[i];
+                    if (run < 0) continue;
+                    const int plen = idr ? 0 : ue_len((uint32_t)run);
+                    const uint32_t pv = (uint32_t)run + 1;
+                    const uint32_t sb = slot_bits[i];
+                    const uint32_t* sp = slot + (size_t)i * kSlotWords;
+                    overlap(acc, W0, off, plen + sb, [&](uint32_t x, int n) {
+                        uint32_t r = 0;
+                        int rem = n;
+                        if ((int)x < plen) {
+                            const int k = min(rem, plen - (int)x);
+                            r = (pv >> (plen - (int)x - k)) & mask_bits(k);
+                            rem -= k;
+                            x += k;
+                        }
+                        if (rem > 0) r = (rem == 32 ? 0u : (r << rem)) | slot_get(sp, x - plen, rem);
+                        return r;
+                    });
+                }
+            }
+            // trailer: [ue(trailing skip run)] + rbsp_stop_one_bit; zero padding follows
+            const int tl = trail ? ue_len(trail) : 0;
+            const uint32_t tv = trail ? (((trail + 1) << 1) | 1u) : 1u;
+            overlap(acc, W0, dend, tl + 1, [&](uint32_t x, int n) { return tv >> (tl + 1 - (int)x - n); });
+        }
+        out[w] = bswap32(acc);
+    }
 }
 
 }  // namespace
+
+void launch_hpel(const Geometry& g, const uint8_t* ref_y, uint8_t* const planes[4], int hp_pitch, hipStream_t stream) {
+    const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
+    dim3 grid((W + kHpTW - 1) / kHpTW, (H + kHpTH - 1) / kHpTH);
+    hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, ref_y, planes[0], planes[1], planes[2], planes[3],
+                       hp_pitch);
+}
 
 void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream) {
     const int nmb = g.mb_w * g.mb_h;
@@ -764,12 +916,10 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
     const int nmb = g.mb_w * g.mb_h;
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, b.mb, b.coef, b.slot,
                        b.slot_bits);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.mb, b.slot_bits, b.unit_off,
-                       b.skip_run, b.slice_info, b.out, b.out_words, b.out_hdr);
-    const int units = nmb + g.mb_h;  // MBs + at most mb_h slices
-    hipLaunchKernelGGL(k_pack, dim3((units + 3) / 4), dim3(256), 0, stream, g, b.fs, b.mb, b.slot, b.slot_bits,
-                       b.unit_off, b.skip_run, b.slice_info, b.out, b.out_hdr);
-    hipLaunchKernelGGL(k_copy_out, dim3(128), dim3(256), 0, stream, b.out, b.out_hdr, b.slice_info, host_out);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.unit_off, b.skip_run,
+                       b.slice_info, b.out_bytes, b.out_hdr);
+    hipLaunchKernelGGL(k_pack, dim3(64), dim3(256), 0, stream, g, b.fs, b.slot, b.slot_bits, b.unit_off, b.skip_run,
+                       b.slice_info, b.out_hdr, host_out);
 }
 
 }  // namespace h264

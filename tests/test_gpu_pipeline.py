@@ -47,7 +47,7 @@ def _lanczos_ref(img, xs, wx, ys, wy):
     f = img[..., :3].astype(np.float64)
     tx, ty = wx.shape[1], wy.shape[1]
     cols = np.clip(xs[:, None] + np.arange(tx)[None, :], 0, w - 1)
-    hz = np.einsum("hok,ok->hoc", f[:, cols.reshape(-1)].reshape(h, len(xs), tx, 3), wx)  # noqa
+    hz = np.einsum("hokc,ok->hoc", f[:, cols.reshape(-1)].reshape(h, len(xs), tx, 3), wx)  # noqa
     rows = np.clip(ys[:, None] + np.arange(ty)[None, :], 0, h - 1)
     out = np.einsum("okxc,ok->oxc", hz[rows.reshape(-1)].reshape(len(ys), ty, hz.shape[1], 3), wy)
     return np.clip(np.rint(out), 0, 255)
