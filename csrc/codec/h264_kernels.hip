@@ -796,9 +796,10 @@ __device__ __forceinline__ void overlap(uint32_t& acc, uint32_t W0, uint32_t s0,
     acc |= bits << (W0 + 32 - hi);
 }
 
-// One thread per output word; assembles the word from the slice header, the MB units and
-// the slice trailer that overlap it, and stores it (big-endian) straight into pinned
-// host memory.  No atomics and no zero-fill pass.
+// One thread per 16 output bytes: one binary search locates the first overlapping MB
+// unit, then each of the 4 words is assembled from the slice header / MB units / slice
+// trailer bits overlapping it and the 16 bytes are stored (big-endian) straight into
+// pinned host memory with one 16-byte store.  No atomics and no zero-fill pass.
 __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __restrict__ fs,
                                               const uint32_t* __restrict__ slot,
                                               const uint32_t* __restrict__ slot_bits,
@@ -820,69 +821,78 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
     const int per_slice = fs->slice_rows * g.mb_w;
     const bool idr = fs->idr != 0;
     const int ns = (int)h.num_slices;
-    const uint32_t nwords = (h.total_bytes + 3) / 4;
-    uint32_t* out = reinterpret_cast<uint32_t*>(host + kOutPayloadOffset);
-    for (size_t w = gid; w < nwords; w += stride) {
-        const uint32_t W0 = (uint32_t)w * 32;
-        // last slice starting at or before W0
+    const uint32_t nquads = (h.total_bytes + 15) / 16;  // each thread emits 16 bytes
+    uint4* out = reinterpret_cast<uint4*>(host + kOutPayloadOffset);
+    for (size_t q = gid; q < nquads; q += stride) {
+        uint32_t res[4];
+        const uint32_t Q0 = (uint32_t)q * 128;
+        // last slice starting at or before Q0, and last MB unit starting at or before Q0
         int lo = 0, hi = ns - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (slice_info[kSliceInfo * mid + 1] * 8 <= W0) lo = mid; else hi = mid - 1;
+            if (slice_info[kSliceInfo * mid + 1] * 8 <= Q0) lo = mid; else hi = mid - 1;
         }
-        uint32_t acc = 0;
-        for (int s = lo; s < ns; ++s) {
-            const uint32_t sbit = slice_info[kSliceInfo * s + 1] * 8;
-            if (sbit >= W0 + 32) break;
-            const uint32_t hbits = slice_info[kSliceInfo * s + 0];
-            const uint32_t dend = slice_info[kSliceInfo * s + 4];
-            const uint32_t trail = idr ? 0u : slice_info[kSliceInfo * s + 3];
-            // header
-            if (sbit < W0 + 32 && sbit + hbits > W0) {
-                uint32_t hw[4] = {0, 0, 0, 0};
-                BitWriter bw;
-                bw.init(hw);
-                write_slice_header(bw, slice_params(fs, s, g.mb_w));
-                bw.flush();
-                overlap(acc, W0, sbit, hbits, [&](uint32_t a, int n) { return slot_get(hw, a, n); });
+        int first_mb;
+        {
+            const int first = lo * per_slice, slast = min(first + per_slice, nmb) - 1;
+            int a = first, b = slast;
+            while (a < b) {
+                const int mid = (a + b + 1) >> 1;
+                if (unit_off[mid] <= Q0) a = mid; else b = mid - 1;
             }
-            // macroblock units overlapping the word
-            const int first = s * per_slice, slast = min(first + per_slice, nmb) - 1;
-            if (dend > W0 && sbit + hbits < W0 + 32) {
-                int a = first, b = slast;
-                while (a < b) {  // last MB with unit_off <= W0
-                    const int mid = (a + b + 1) >> 1;
-                    if (unit_off[mid] <= W0) a = mid; else b = mid - 1;
-                }
-                for (int i = a; i <= slast; ++i) {
-                    const uint32_t off = unit_off[i];
-                    if (off >= W0 + 32) break;
-                    const int run = skip_run[i];
-                    if (run < 0) continue;
-                    const int plen = idr ? 0 : ue_len((uint32_t)run);
-                    const uint32_t pv = (uint32_t)run + 1;
-                    const uint32_t sb = slot_bits[i];
-                    const uint32_t* sp = slot + (size_t)i * kSlotWords;
-                    overlap(acc, W0, off, plen + sb, [&](uint32_t x, int n) {
-                        uint32_t r = 0;
-                        int rem = n;
-                        if ((int)x < plen) {
-                            const int k = min(rem, plen - (int)x);
-                            r = (pv >> (plen - (int)x - k)) & mask_bits(k);
-                            rem -= k;
-                            x += k;
-                        }
-                        if (rem > 0) r = (rem == 32 ? 0u : (r << rem)) | slot_get(sp, x - plen, rem);
-                        return r;
-                    });
-                }
-            }
-            // trailer: [ue(trailing skip run)] + rbsp_stop_one_bit; zero padding follows
-            const int tl = trail ? ue_len(trail) : 0;
-            const uint32_t tv = trail ? (((trail + 1) << 1) | 1u) : 1u;
-            overlap(acc, W0, dend, tl + 1, [&](uint32_t x, int n) { return tv >> (tl + 1 - (int)x - n); });
+            first_mb = a;
         }
-        out[w] = bswap32(acc);
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t W0 = Q0 + 32 * k;
+            uint32_t acc = 0;
+            for (int s = lo; s < ns; ++s) {
+                const uint32_t sbit = slice_info[kSliceInfo * s + 1] * 8;
+                if (sbit >= W0 + 32) break;
+                const uint32_t hbits = slice_info[kSliceInfo * s + 0];
+                const uint32_t dend = slice_info[kSliceInfo * s + 4];
+                if (sbit + slice_info[kSliceInfo * s + 2] * 8 <= W0) continue;  // slice ends before the word
+                const uint32_t trail = idr ? 0u : slice_info[kSliceInfo * s + 3];
+                if (sbit + hbits > W0) {
+                    uint32_t hw[4] = {0, 0, 0, 0};
+                    BitWriter bw;
+                    bw.init(hw);
+                    write_slice_header(bw, slice_params(fs, s, g.mb_w));
+                    bw.flush();
+                    overlap(acc, W0, sbit, hbits, [&](uint32_t x, int n) { return slot_get(hw, x, n); });
+                }
+                const int first = s * per_slice, slast = min(first + per_slice, nmb) - 1;
+                if (dend > W0 && sbit + hbits < W0 + 32) {
+                    for (int i = max(first, s == lo ? first_mb : first); i <= slast; ++i) {
+                        const uint32_t off = unit_off[i];
+                        if (off >= W0 + 32) break;
+                        const int run = skip_run[i];
+                        if (run < 0) continue;
+                        const int plen = idr ? 0 : ue_len((uint32_t)run);
+                        const uint32_t sb = slot_bits[i];
+                        if (off + plen + sb <= W0) continue;
+                        const uint32_t pv = (uint32_t)run + 1;
+                        const uint32_t* sp = slot + (size_t)i * kSlotWords;
+                        overlap(acc, W0, off, plen + sb, [&](uint32_t x, int n) {
+                            uint32_t r = 0;
+                            int rem = n;
+                            if ((int)x < plen) {
+                                const int kk = min(rem, plen - (int)x);
+                                r = (pv >> (plen - (int)x - kk)) & mask_bits(kk);
+                                rem -= kk;
+                                x += kk;
+                            }
+                            if (rem > 0) r = (rem == 32 ? 0u : (r << rem)) | slot_get(sp, x - plen, rem);
+                            return r;
+                        });
+                    }
+                }
+                const int tl = trail ? ue_len(trail) : 0;
+                const uint32_t tv = trail ? (((trail + 1) << 1) | 1u) : 1u;
+                overlap(acc, W0, dend, tl + 1, [&](uint32_t x, int n) { return tv >> (tl + 1 - (int)x - n); });
+            }
+            res[k] = bswap32(acc);
+        }
+        out[q] = make_uint4(res[0], res[1], res[2], res[3]);
     }
 }
 

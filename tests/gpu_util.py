@@ -7,13 +7,17 @@ def to_dev(arr: np.ndarray) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(arr)).to("cuda")
 
 
-def pitched(arr: np.ndarray, pitch: int, rows: int) -> torch.Tensor:
-    """Copy a (h, w) uint8 plane into a zero-padded (rows, pitch) device tensor."""
+def pitched(arr: np.ndarray, pitch: int, rows: int, uv: bool = False) -> torch.Tensor:
+    """Copy a (h, w) uint8 plane into a (rows, pitch) device tensor, replicating the last
+    column (last U/V pair for an interleaved chroma plane) and row like the CSC kernel."""
     out = np.zeros((rows, pitch), np.uint8)
     out[: arr.shape[0], : arr.shape[1]] = arr
-    # replicate edges like the CSC kernel does
     if arr.shape[1] < pitch:
-        out[: arr.shape[0], arr.shape[1]:] = arr[:, -1:]
+        if uv:
+            reps = (pitch - arr.shape[1]) // 2
+            out[: arr.shape[0], arr.shape[1]: arr.shape[1] + 2 * reps] = np.tile(arr[:, -2:], (1, reps))
+        else:
+            out[: arr.shape[0], arr.shape[1]:] = arr[:, -1:]
     if arr.shape[0] < rows:
         out[arr.shape[0]:] = out[arr.shape[0] - 1]
     return to_dev(out)

@@ -120,7 +120,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     for t in range(frames):
         y, uv = synthetic_nv12(w, h, t)
         dy = pitched(y, genc.pitch, ch)
-        duv = pitched(uv, genc.pitch, ch // 2)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
