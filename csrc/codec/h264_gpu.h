@@ -74,7 +74,8 @@ struct OutHeader {
 };
 constexpr int kMaxSlices = 1024;
 // slice_info fields: 0 header bits, 1 byte offset, 2 bytes, 3 trailing skip run,
-// 4 data-end bit (trailer start), 5 unit-bit prefix at the slice's first MB
+// 4 data-end bit (trailer start), 5 unit-bit prefix at the slice's first MB,
+// 6 / 7 first / end rank of the slice's coded MBs in coded_list
 constexpr int kSliceInfo = 8;
 // host buffer: OutHeader | uint32 slice_off[kMaxSlices] | uint32 slice_len[kMaxSlices] | payload
 constexpr size_t kOutPayloadOffset = sizeof(OutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
@@ -95,6 +96,7 @@ struct DeviceBuffers {
     uint32_t* slot_bits;    // [nmb]
     uint32_t* unit_off;     // [nmb] absolute bit offset of the MB unit (incl. skip run prefix)
     int32_t* skip_run;      // [nmb] skip run preceding a coded MB, -1 for skipped MBs
+    uint32_t* coded_list;   // [nmb] indices of coded (non-skipped) MBs, in order
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header

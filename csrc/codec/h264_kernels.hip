@@ -669,6 +669,7 @@ __device__ __forceinline__ int block_excl_max(int v, int* wmax, int init) {
 __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ slot_bits,
                                                        uint32_t* __restrict__ unit_off, int32_t* __restrict__ skip_run,
+                                                       uint32_t* __restrict__ coded_list,
                                                        uint32_t* __restrict__ slice_info, size_t out_bytes,
                                                        OutHeader* __restrict__ hdr) {
     __shared__ uint32_t sb[kScanTile];
@@ -683,14 +684,21 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     if (t == 0) s_overflow = 0;
     int carry_last = -1;      // last coded MB index before the current tile
     uint32_t carry_bits = 0;  // unit bits before the current tile
+    uint32_t carry_rank = 0;  // coded MBs before the current tile
     for (int base = 0; base < nmb; base += kScanTile) {
         const int n = min(kScanTile, nmb - base);
         for (int j = t; j < n; j += kScanThreads) sb[j] = slot_bits[base + j];
         __syncthreads();
         const int j0 = t * kScanPer;
         int last = -1;
+        uint32_t ncoded = 0;
         for (int k = 0; k < kScanPer; ++k)
-            if (j0 + k < n && sb[j0 + k] != 0) last = base + j0 + k;
+            if (j0 + k < n && sb[j0 + k] != 0) {
+                last = base + j0 + k;
+                ++ncoded;
+            }
+        uint32_t tile_coded;
+        uint32_t rank = carry_rank + block_excl_sum(ncoded, wsum, &tile_coded);
         int prev = block_excl_max(last, wmax, -1);
         prev = max(prev, carry_last);
         uint32_t local = 0;
@@ -704,7 +712,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
             const int slast = min(first + per_slice, nmb) - 1;
             const int pv = max(prev, first - 1);
             uint32_t b = sb[j];
+            if (i == first) slice_info[kSliceInfo * s + 6] = rank;  // coded MBs before the slice
             if (b != 0) {
+                coded_list[rank++] = (uint32_t)i;
                 if (b == 0xffffffffu) {
                     s_overflow = 1;
                     b = 1;
@@ -733,9 +743,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         __syncthreads();
         carry_last = wmax[0];
         carry_bits += tile_total;
+        carry_rank += tile_coded;
         __syncthreads();
     }
     const uint32_t grand_total = carry_bits;
+    __syncthreads();
+    if (t < ns) slice_info[kSliceInfo * t + 7] = (t + 1 < ns ? slice_info[kSliceInfo * (t + 1) + 6] : carry_rank);
     __syncthreads();
     // per slice sizes (one thread per slice; ns <= kMaxSlices <= kScanThreads)
     uint32_t sbytes = 0, ebase = 0, eend = 0, hbits = 0, trail = 0;
@@ -805,6 +818,7 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
                                               const uint32_t* __restrict__ slot_bits,
                                               const uint32_t* __restrict__ unit_off,
                                               const int32_t* __restrict__ skip_run,
+                                              const uint32_t* __restrict__ coded_list,
                                               const uint32_t* __restrict__ slice_info,
                                               const OutHeader* __restrict__ hdr, uint8_t* __restrict__ host) {
     const OutHeader h = *hdr;
@@ -832,15 +846,18 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
             const int mid = (lo + hi + 1) >> 1;
             if (slice_info[kSliceInfo * mid + 1] * 8 <= Q0) lo = mid; else hi = mid - 1;
         }
-        int first_mb;
+        int first_rank;  // last coded unit of slice `lo` starting at or before Q0
         {
-            const int first = lo * per_slice, slast = min(first + per_slice, nmb) - 1;
-            int a = first, b = slast;
-            while (a < b) {
-                const int mid = (a + b + 1) >> 1;
-                if (unit_off[mid] <= Q0) a = mid; else b = mid - 1;
+            int a = (int)slice_info[kSliceInfo * lo + 6], b = (int)slice_info[kSliceInfo * lo + 7] - 1;
+            if (b < a) {
+                first_rank = a;
+            } else {
+                while (a < b) {
+                    const int mid = (a + b + 1) >> 1;
+                    if (unit_off[coded_list[mid]] <= Q0) a = mid; else b = mid - 1;
+                }
+                first_rank = a;
             }
-            first_mb = a;
         }
         for (int k = 0; k < 4; ++k) {
             const uint32_t W0 = Q0 + 32 * k;
@@ -860,29 +877,29 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
                     bw.flush();
                     overlap(acc, W0, sbit, hbits, [&](uint32_t x, int n) { return slot_get(hw, x, n); });
                 }
-                const int first = s * per_slice, slast = min(first + per_slice, nmb) - 1;
                 if (dend > W0 && sbit + hbits < W0 + 32) {
-                    for (int i = max(first, s == lo ? first_mb : first); i <= slast; ++i) {
+                    const int rend = (int)slice_info[kSliceInfo * s + 7];
+                    for (int r = (s == lo ? first_rank : (int)slice_info[kSliceInfo * s + 6]); r < rend; ++r) {
+                        const int i = (int)coded_list[r];
                         const uint32_t off = unit_off[i];
                         if (off >= W0 + 32) break;
                         const int run = skip_run[i];
-                        if (run < 0) continue;
                         const int plen = idr ? 0 : ue_len((uint32_t)run);
                         const uint32_t sb = slot_bits[i];
                         if (off + plen + sb <= W0) continue;
                         const uint32_t pv = (uint32_t)run + 1;
                         const uint32_t* sp = slot + (size_t)i * kSlotWords;
                         overlap(acc, W0, off, plen + sb, [&](uint32_t x, int n) {
-                            uint32_t r = 0;
+                            uint32_t r2 = 0;
                             int rem = n;
                             if ((int)x < plen) {
                                 const int kk = min(rem, plen - (int)x);
-                                r = (pv >> (plen - (int)x - kk)) & mask_bits(kk);
+                                r2 = (pv >> (plen - (int)x - kk)) & mask_bits(kk);
                                 rem -= kk;
                                 x += kk;
                             }
-                            if (rem > 0) r = (rem == 32 ? 0u : (r << rem)) | slot_get(sp, x - plen, rem);
-                            return r;
+                            if (rem > 0) r2 = (rem == 32 ? 0u : (r2 << rem)) | slot_get(sp, x - plen, rem);
+                            return r2;
                         });
                     }
                 }
@@ -927,9 +944,9 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, b.mb, b.coef, b.slot,
                        b.slot_bits);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.unit_off, b.skip_run,
-                       b.slice_info, b.out_bytes, b.out_hdr);
+                       b.coded_list, b.slice_info, b.out_bytes, b.out_hdr);
     hipLaunchKernelGGL(k_pack, dim3(64), dim3(256), 0, stream, g, b.fs, b.slot, b.slot_bits, b.unit_off, b.skip_run,
-                       b.slice_info, b.out_hdr, host_out);
+                       b.coded_list, b.slice_info, b.out_hdr, host_out);
 }
 
 }  // namespace h264
