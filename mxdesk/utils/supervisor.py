@@ -235,9 +235,9 @@ def load_ini(path: str | os.PathLike, env: Mapping[str, str] | None = None) -> t
     """Parse a supervisord-style config.  Returns (programs, [supervisord] section)."""
     env = os.environ if env is None else env
     defaults = {f"ENV_{k}": v.replace("%", "%%") for k, v in env.items()}
-    cp = configparser.ConfigParser(defaults=defaults, interpolation=configparser.BasicInterpolation(),
-                                   strict=False)
-    cp.optionxform = str  # keep case of keys... and ENV_ names
+    cp = configparser.ConfigParser(interpolation=configparser.BasicInterpolation(), strict=False)
+    cp.optionxform = str  # keep the case of %(ENV_X)s names
+    cp.read_dict({"DEFAULT": defaults})
     text = Path(path).read_text()
     cp.read_string(text)
     progs = []
