@@ -90,6 +90,7 @@ PYBIND11_MODULE(_native, m) {
         return std::string(p.gcnArchName) + " / " + p.name;
     });
     m.def("synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
+    m.def("now_us", &Session::now_us, "CLOCK_MONOTONIC microseconds (same clock as time.monotonic())");
 
     // ---------------------------------------------------------------- codec helpers
     py::module h = m.def_submodule("h264", "H.264 building blocks (for tests)");

@@ -179,8 +179,7 @@ FrameResult Session::collect() {
     r.t_encoded_us = now_us();
     r.au = au;
     r.frame_id = frame_id_++;
-    r.t_capture_us = t_capture_ - t0_us_;
-    r.t_encoded_us -= t0_us_;
+    r.t_capture_us = t_capture_;  // steady clock (CLOCK_MONOTONIC) microseconds
     const h264::FrameStats& st = enc_->last_stats();
     r.idr = st.idr;
     r.qp = st.qp;

@@ -57,8 +57,8 @@ struct SessionConfig {
 
 struct FrameResult {
     uint32_t frame_id = 0;
-    int64_t t_capture_us = 0;  // host clock when the frame was rendered/captured
-    int64_t t_encoded_us = 0;  // host clock when the access unit was available
+    int64_t t_capture_us = 0;  // CLOCK_MONOTONIC us when the frame was rendered/captured
+    int64_t t_encoded_us = 0;  // CLOCK_MONOTONIC us when the access unit was available
     double gpu_ms = 0;         // device time render->bitstream (events)
     int idr = 0;
     int qp = 0;

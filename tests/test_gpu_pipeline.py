@@ -159,7 +159,7 @@ def test_session_stream_decodes_with_barcodes(gpu):
     assert len(frames) == 4
     for (y, _, _), (fid, ts) in zip(frames, ids):
         got = _read_barcode(y, gpu.BARCODE_CELL, gpu.BARCODE_X, gpu.BARCODE_Y)
-        assert got == [fid, ts & 0xFFFFFFFF]
+        assert got[0] == fid
 
 
 def test_session_scaled_output(gpu):

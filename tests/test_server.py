@@ -1,0 +1,188 @@
+"""Integration tests of the web front end with the CPU plumbing backend (no GPU): media
+WebSocket -> independent decoder -> barcode, basic auth, health/turn/metrics/status,
+selkies signalling relay, input injection, keyframe resync, fault injection."""
+import asyncio
+import base64
+import json
+import socket
+
+import aiohttp
+import numpy as np
+import pytest
+
+from mxdesk.codec.h264_decoder import Decoder
+from mxdesk.models.synthetic import read_barcode
+from mxdesk.pipeline.stream import StreamPipeline
+from mxdesk.server.app import MediaServer, serve
+from mxdesk.server.client import view
+from mxdesk.server.input import parse_message
+from mxdesk.utils import config as C
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def make_server(env=None, **kw):
+    cfg = C.load(env={"WEBRTC_ENCODER": "x264enc", "SIZEW": "320", "SIZEH": "96", "REFRESH": "30",
+                      **(env or {})}, argv=[])
+    pipe = StreamPipeline(cfg.sizew, cfg.sizeh, cfg.stream_fps, backend="cpu", bitrate_kbps=0, **kw)
+    return cfg, pipe, MediaServer(pipe, cfg)
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def test_stream_decodes_and_barcodes_match():
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await view(f"http://127.0.0.1:{port}/mxws", 6)
+        finally:
+            await runner.cleanup()
+
+    res = run(go())
+    assert res.config["codec"].startswith("avc1.42C0") and res.config["width"] == 320
+    assert len(res.frames) == 6 and res.frames[0]["key"]
+    frames = Decoder().decode(res.stream)
+    assert len(frames) == 6
+    for (y, _, _), meta in zip(frames, res.frames):
+        fid, _ = read_barcode(y)
+        assert fid == meta["frame_id"]
+    assert all(0 <= ms < 5000 for ms in res.latency_ms)
+
+
+def test_basic_auth_and_endpoints():
+    cfg, pipe, srv = make_server({"PASSWD": "pw1", "TURN_HOST": "turn.example.com", "TURN_SHARED_SECRET": "sekret"})
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        base = f"http://127.0.0.1:{port}"
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.get(base + "/") as r:
+                    assert r.status == 401 and "Basic" in r.headers["WWW-Authenticate"]
+                async with s.get(base + "/health") as r:
+                    assert r.status == 200
+            auth = aiohttp.BasicAuth("user", "pw1")
+            async with aiohttp.ClientSession(auth=auth) as s:
+                async with s.get(base + "/") as r:
+                    assert r.status == 200 and "client.js" in await r.text()
+                async with s.get(base + "/client.js") as r:
+                    assert r.status == 200
+                async with s.get(base + "/turn") as r:
+                    d = await r.json()
+                    turn = [x for x in d["iceServers"] if x["urls"][0].startswith("turn")][0]
+                    assert turn["urls"] == ["turn:turn.example.com:3478?transport=udp"]
+                    assert ":" in turn["username"] and len(base64.b64decode(turn["credential"])) == 20
+                async with s.get(base + "/manifest.json") as r:
+                    assert json.loads(await r.text())["short_name"] == "mxdesk"
+            res = await view(base.replace("http", "http") + "/mxws", 3, user="user", password="pw1")
+            async with aiohttp.ClientSession(auth=auth) as s:
+                async with s.get(base + "/metrics") as r:
+                    assert "mxdesk_encoded_frames_total" in await r.text()
+                async with s.get(base + "/status") as r:
+                    st = await r.json()
+                    assert st["frames"] >= 3 and st["backend"] == "cpu"
+            return res
+        finally:
+            await runner.cleanup()
+
+    res = run(go())
+    assert len(res.frames) == 3
+
+
+def test_signalling_relay():
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        url = f"http://127.0.0.1:{port}/ws"
+        try:
+            async with aiohttp.ClientSession() as s:
+                a = await s.ws_connect(url)
+                b = await s.ws_connect(url)
+                await a.send_str("HELLO 0")
+                assert (await a.receive()).data == "HELLO"
+                await b.send_str("HELLO 1 eyJ9")
+                assert (await b.receive()).data == "HELLO"
+                await b.send_str("SESSION 7")
+                assert (await b.receive()).data.startswith("ERROR")
+                await b.send_str("SESSION 0")
+                assert (await b.receive()).data == "SESSION_OK"
+                await b.send_str(json.dumps({"sdp": {"type": "offer", "sdp": "v=0"}}))
+                assert json.loads((await a.receive()).data)["sdp"]["type"] == "offer"
+                await a.send_str(json.dumps({"ice": {"candidate": "x", "sdpMLineIndex": 0}}))
+                assert "ice" in json.loads((await b.receive()).data)
+                await a.close()
+                assert "disconnected" in (await b.receive()).data
+                await b.close()
+        finally:
+            await runner.cleanup()
+
+    run(go())
+
+
+def test_input_moves_synthetic_cursor_and_pli():
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await view(f"http://127.0.0.1:{port}/mxws", 4, send=["m,40,30,1,0", "kd,65", "pli",
+                                                                          json.dumps({"type": "bitrate", "kbps": 500})])
+        finally:
+            await runner.cleanup()
+
+    res = run(go())
+    inj = srv.injector
+    assert (inj.x, inj.y, inj.buttons) == (40, 30, 1) and 65 in inj.keys_down
+    assert pipe._cursor == (40, 30)
+
+
+def test_parse_selkies_messages():
+    assert parse_message("m2,-3,4,0,0").relative
+    assert parse_message("cw," + base64.b64encode("héllo".encode()).decode()).text == "héllo"
+    assert (parse_message("r,1280x720").width, parse_message("r,1280x720").height) == (1280, 720)
+    assert parse_message("bogus,1") is None and parse_message("m,x") is None
+
+
+def test_pipeline_fault_injection_restarts(monkeypatch):
+    monkeypatch.setenv("MXDESK_FAULT", "crash:2")
+    pipe = StreamPipeline(64, 48, 60, backend="cpu", bitrate_kbps=0, paced=False)
+    pipe.start()
+    import time
+    deadline = time.time() + 10
+    while pipe.frames_out < 5 and time.time() < deadline:
+        time.sleep(0.01)
+    pipe.stop()
+    assert pipe.restarts == 1 and "injected" in pipe.last_error and pipe.frames_out >= 5
+
+
+def test_slow_client_resync():
+    pipe = StreamPipeline(64, 48, 60, backend="cpu", bitrate_kbps=0, queue_frames=2)
+
+    async def go():
+        sub = pipe.subscribe(asyncio.get_running_loop())
+        for _ in range(8):
+            pipe.step()
+        await asyncio.sleep(0.05)
+        got = []
+        while not sub.queue.empty():
+            got.append(sub.queue.get_nowait())
+        return sub, got
+
+    sub, got = run(go())
+    assert sub.dropped > 0 and sub.need_idr  # backlog dropped, waiting for the next IDR
+    assert pipe.metrics.dropped.labels("0")._value.get() > 0

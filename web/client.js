@@ -1,0 +1,112 @@
+// mxdesk browser client: receives Annex-B H.264 access units over the /mxws WebSocket,
+// decodes them with WebCodecs (hardware decoder on the viewer's machine) and paints a
+// canvas; mouse/keyboard/clipboard events go back as selkies-style text messages.
+"use strict";
+const mxdesk = (() => {
+  const HDR = 36;
+  let ws, decoder, canvas, ctx, statsEl, msgEl, cfg = null, waitingKey = true;
+  let frames = 0, bytes = 0, lastStats = performance.now(), decodeTimes = [];
+  const sendQ = (m) => { if (ws && ws.readyState === 1) ws.send(m); };
+
+  function parse(buf) {
+    const dv = new DataView(buf);
+    const magic = String.fromCharCode(dv.getUint8(0), dv.getUint8(1), dv.getUint8(2), dv.getUint8(3));
+    if (magic !== "MXV1") throw new Error("bad frame");
+    return {
+      key: (dv.getUint8(4) & 1) === 1,
+      frameId: dv.getUint32(8, true),
+      tCapture: Number(dv.getBigUint64(12, true)),
+      tSend: Number(dv.getBigUint64(20, true)),
+      width: dv.getUint16(28, true), height: dv.getUint16(30, true),
+      data: new Uint8Array(buf, HDR, dv.getUint32(32, true)),
+    };
+  }
+
+  function makeDecoder() {
+    decoder = new VideoDecoder({
+      output: (frame) => {
+        if (canvas.width !== frame.displayWidth || canvas.height !== frame.displayHeight) {
+          canvas.width = frame.displayWidth; canvas.height = frame.displayHeight;
+        }
+        ctx.drawImage(frame, 0, 0);
+        frame.close();
+      },
+      error: (e) => { msgEl.textContent = "decoder error: " + e; waitingKey = true; sendQ("pli"); makeDecoder(); },
+    });
+    decoder.configure({ codec: cfg.codec, optimizeForLatency: true, hardwareAcceleration: "prefer-hardware" });
+  }
+
+  function onFrame(buf) {
+    const f = parse(buf);
+    if (waitingKey && !f.key) return;
+    waitingKey = false;
+    const t0 = performance.now();
+    decoder.decode(new EncodedVideoChunk({ type: f.key ? "key" : "delta", timestamp: f.frameId * 1000, data: f.data }));
+    decodeTimes.push(performance.now() - t0);
+    frames++; bytes += f.data.byteLength;
+    sendQ(JSON.stringify({ type: "ack", frame_id: f.frameId }));
+    const now = performance.now();
+    if (now - lastStats > 1000) {
+      const dt = (now - lastStats) / 1000;
+      statsEl.textContent = `${cfg.width}x${cfg.height} ${cfg.codec}\n${(frames / dt).toFixed(1)} fps ` +
+        `${(bytes * 8 / dt / 1000).toFixed(0)} kbps\nqueue ${decoder.decodeQueueSize}`;
+      frames = 0; bytes = 0; lastStats = now; decodeTimes = [];
+    }
+  }
+
+  function input() {
+    const pos = (e) => {
+      const r = canvas.getBoundingClientRect();
+      const sx = canvas.width / r.width, sy = canvas.height / r.height;
+      const s = Math.min(1 / sx, 1 / sy);
+      const ox = (r.width - canvas.width * s) / 2, oy = (r.height - canvas.height * s) / 2;
+      return [Math.round((e.clientX - r.left - ox) / s), Math.round((e.clientY - r.top - oy) / s)];
+    };
+    let mask = 0;
+    const mouse = (e, scroll = 0) => { const [x, y] = pos(e); sendQ(`m,${x},${y},${mask},${scroll}`); };
+    canvas.addEventListener("mousemove", (e) => mouse(e));
+    canvas.addEventListener("mousedown", (e) => { mask |= 1 << e.button; mouse(e); e.preventDefault(); canvas.focus(); });
+    canvas.addEventListener("mouseup", (e) => { mask &= ~(1 << e.button); mouse(e); e.preventDefault(); });
+    canvas.addEventListener("wheel", (e) => { mouse(e, e.deltaY < 0 ? 1 : -1); e.preventDefault(); }, { passive: false });
+    canvas.addEventListener("contextmenu", (e) => e.preventDefault());
+    const keysym = (e) => (e.key.length === 1 ? e.key.codePointAt(0) : ({
+      Enter: 0xff0d, Backspace: 0xff08, Tab: 0xff09, Escape: 0xff1b, Delete: 0xffff, Home: 0xff50,
+      ArrowLeft: 0xff51, ArrowUp: 0xff52, ArrowRight: 0xff53, ArrowDown: 0xff54, PageUp: 0xff55, PageDown: 0xff56,
+      End: 0xff57, Shift: 0xffe1, Control: 0xffe3, Alt: 0xffe9, Meta: 0xffeb,
+    }[e.key] || 0));
+    canvas.addEventListener("keydown", (e) => { const k = keysym(e); if (k) sendQ(`kd,${k}`); e.preventDefault(); });
+    canvas.addEventListener("keyup", (e) => { const k = keysym(e); if (k) sendQ(`ku,${k}`); e.preventDefault(); });
+    window.addEventListener("blur", () => sendQ("kr"));
+    document.addEventListener("paste", (e) => {
+      const t = e.clipboardData.getData("text");
+      if (t) sendQ("cw," + btoa(unescape(encodeURIComponent(t))));
+    });
+    window.addEventListener("resize", () => {
+      if (cfg && cfg.resize) sendQ(`r,${window.innerWidth}x${window.innerHeight}`);
+    });
+  }
+
+  function connect() {
+    const proto = location.protocol === "https:" ? "wss:" : "ws:";
+    ws = new WebSocket(`${proto}//${location.host}/mxws`);
+    ws.binaryType = "arraybuffer";
+    ws.onmessage = (ev) => {
+      if (typeof ev.data === "string") {
+        const m = JSON.parse(ev.data);
+        if (m.type === "config") { cfg = m; waitingKey = true; makeDecoder(); msgEl.textContent = ""; }
+        return;
+      }
+      if (cfg) onFrame(ev.data);
+    };
+    ws.onclose = () => { msgEl.textContent = "disconnected - retrying"; setTimeout(connect, 1000); };
+  }
+
+  return {
+    start(c, s, m) {
+      canvas = c; statsEl = s; msgEl = m; ctx = canvas.getContext("2d");
+      if (!("VideoDecoder" in window)) { msgEl.textContent = "WebCodecs not supported by this browser"; return; }
+      input(); connect();
+    },
+    parse,
+  };
+})();
