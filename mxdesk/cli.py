@@ -49,12 +49,14 @@ def _x_available(display: str) -> bool:
 
 
 def _gpu_index(cfg: C.Config) -> int:
+    """HIP ordinal of the selected GPU: HIP enumerates only the visible devices, in PCI
+    order, so the ordinal is the position inside the visible list."""
     from .utils import devices as D
 
     gpus = D.visible_gpus(D.enumerate_gpus())
     if not gpus:
         return 0
-    return D.select_gpu(gpus, cfg.gpu).index
+    return gpus.index(D.select_gpu(gpus, cfg.gpu))
 
 
 def cmd_serve(cfg: C.Config, args) -> None:
