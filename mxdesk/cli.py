@@ -68,8 +68,10 @@ def cmd_serve(cfg: C.Config, args) -> None:
     if cfg.novnc_enable:
         from .server.rfb import RfbServer
 
-        rfb = RfbServer(pipe, cfg.effective_basic_auth_password, cfg.novnc_viewpass)
-    srv = MediaServer(pipe, cfg, rfb=rfb)
+        rfb = RfbServer(pipe, cfg.effective_basic_auth_password, cfg.novnc_viewpass, fps=min(cfg.stream_fps, 30))
+    # NOVNC_ENABLE=true: the RFB front end replaces WebRTC (supervisord.conf:36 puts selkies
+    # to sleep), so the H.264 pipeline is not started.
+    srv = MediaServer(pipe, cfg, rfb=rfb, start_pipeline=not cfg.novnc_enable)
     print(f"mxdesk: serving {cfg.sizew}x{cfg.sizeh}@{cfg.stream_fps} ({cfg.encoder_backend}) on "
           f"{cfg.addr}:{cfg.port}", flush=True)
     run_forever(srv, cfg.addr, cfg.port, ssl_context(cfg))

@@ -49,13 +49,14 @@ def render_manifest(app_name: str = "mxdesk", short: str = "mxdesk", start_url: 
 
 class MediaServer:
     def __init__(self, pipeline: StreamPipeline, cfg: Any = None, injector: Any = None,
-                 web_root: Path | None = None, rfb: Any = None):
+                 web_root: Path | None = None, rfb: Any = None, start_pipeline: bool = True):
         self.pipeline = pipeline
         self.cfg = cfg
         self.injector = injector or SyntheticInjector(pipeline, pipeline.out_w, pipeline.out_h)
         self.web_root = Path(web_root) if web_root else WEB_ROOT
         self.signalling = SignallingRelay()
         self.rfb = rfb
+        self.start_pipeline = start_pipeline
         self.clients: set[web.WebSocketResponse] = set()
         self.resize_enabled = bool(getattr(cfg, "enable_resize", False))
 
@@ -86,7 +87,8 @@ class MediaServer:
         return app
 
     async def _on_startup(self, app):
-        self.pipeline.start()
+        if self.start_pipeline:
+            self.pipeline.start()
 
     async def _on_cleanup(self, app):
         self.pipeline.stop()
@@ -113,7 +115,7 @@ class MediaServer:
         return web.Response(text=render_manifest(), content_type="application/manifest+json")
 
     async def health(self, request: web.Request) -> web.Response:
-        ok = self.pipeline.healthy() or self.pipeline.frames_out == 0
+        ok = not self.start_pipeline or self.pipeline.healthy() or self.pipeline.frames_out == 0
         return web.Response(status=200 if ok else 503, text="OK" if ok else "STALLED")
 
     async def turn(self, request: web.Request) -> web.Response:
