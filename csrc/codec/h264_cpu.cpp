@@ -65,16 +65,21 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
     const int qp = common_.cur_qp();
     const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
     const int lambda = lambda_sad(qp);
-    const int R = std::clamp(cfg_.search_range, 1, 32);
+    const int R = me_range(cfg_.search_range);
     const int side = 2 * R + 1;
     for (int mby = 0; mby < g.mb_h; ++mby)
         for (int mbx = 0; mbx < g.mb_w; ++mbx) {
             const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
             MbInfo& m = mb_[mbi];
             std::memset(&m, 0, sizeof m);
-            // ---- integer full search (identical order / tie-break to k_me_full)
+            // ---- static-block early exit, then integer full search (same rules as k_me_full)
+            uint32_t sad0 = 0;
+            for (int r = 0; r < 16; ++r)
+                for (int k = 0; k < 16; ++k)
+                    sad0 += std::abs((int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + k, y0 + r));
+            const bool is_static = sad0 <= kStaticSad;
             unsigned long long best = ~0ull;
-            for (int c = 0; c < side * side; ++c) {
+            for (int c = 0; c < (is_static ? 0 : side * side); ++c) {
                 const int dy = c / side - R, dx = c % side - R;
                 uint32_t sad = 0;
                 for (int r = 0; r < 16; ++r)
@@ -87,8 +92,8 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                 best = std::min(best, key);
             }
             const int cb = (int)(best & 0xffff);
-            int mvx = 4 * ((cb % side) - R), mvy = 4 * ((cb / side) - R);
-            if (cfg_.subpel) {
+            int mvx = is_static ? 0 : 4 * ((cb % side) - R), mvy = is_static ? 0 : 4 * ((cb / side) - R);
+            if (cfg_.subpel && !is_static) {
                 auto sad_at = [&](int vx, int vy) {
                     uint32_t s = 0;
                     for (int r = 0; r < 16; ++r)
@@ -97,7 +102,7 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                                           luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + vx, (y0 + r) * 4 + vy));
                     return s;
                 };
-                uint32_t cur_cost = me_cost(sad_at(mvx, mvy), lambda, mvx, mvy);
+                uint32_t cur_cost = (uint32_t)(best >> 32);
                 for (int step = 2; step >= 1; step >>= 1) {
                     int bdx = 0, bdy = 0;
                     uint32_t bcost = cur_cost;

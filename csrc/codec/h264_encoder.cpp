@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../common/hip_check.h"
+#include "h264_mb.h"
 
 namespace mx {
 namespace h264 {
@@ -206,7 +207,7 @@ void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
     f.qp = common_.cur_qp();
     f.slice_rows = idr ? 1 : geom_.mb_h;
     f.num_slices = idr ? geom_.mb_h : 1;
-    f.search_range = std::clamp(cfg_.search_range, 1, 32);
+    f.search_range = me_range(cfg_.search_range);
     f.subpel = cfg_.subpel;
     f.deblock_off = 1;
     f.pic_init_qp = common_.pic_init_qp();

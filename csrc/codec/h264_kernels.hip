@@ -154,6 +154,7 @@ __global__ __launch_bounds__(256) void k_hpel(Geometry g, const uint8_t* __restr
 
 // ------------------------------------------------------------------ motion estimation
 constexpr int kMaxRange = 32;
+static_assert(kMaxRange + 2 <= kHpelPad, "search window must stay inside the padded planes");
 constexpr int kWinStride = 16 + 2 * kMaxRange + 8;  // bytes per LDS window row (dword padded)
 
 __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* __restrict__ fs,
@@ -161,32 +162,49 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     __shared__ uint32_t win32[(16 + 2 * kMaxRange) * kWinStride / 4];
     __shared__ uint32_t srcw[64];
     __shared__ unsigned long long red[4];
-    __shared__ int sub_cost[9];
+    __shared__ uint32_t cand_cost[8];
+    __shared__ uint32_t s_sad0[4];
 
     const int mbi = blockIdx.x;
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
     const int x0 = mbx * 16, y0 = mby * 16;
-    const int tid = threadIdx.x;
-    int R = fs->search_range;
-    R = R > kMaxRange ? kMaxRange : (R < 1 ? 1 : R);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int R = me_range(fs->search_range);
     const int W = 16 + 2 * R;
     const Planes P = planes_of(fs);
-    const int qp = fs->qp;
-    const int lambda = lambda_sad(qp);
+    const int lambda = lambda_sad(fs->qp);
 
-    // search window from the padded full-sample plane (R + 1 <= kHpelPad: no clamping)
-    for (int i = tid; i < W * (kWinStride / 4); i += 256) {
-        const int wy = i / (kWinStride / 4), wx4 = (i - wy * (kWinStride / 4)) * 4;
-        const uint8_t* src = P.f + (y0 - R + wy) * P.pitch + (x0 - R + wx4);
-        uint32_t v = 0;
-        for (int k = 0; k < 4; ++k) v |= (uint32_t)(wx4 + k < W ? src[k] : 0) << (8 * k);
-        win32[i] = v;
+    // search window from the padded full-sample plane with dword loads (x0 - R is a
+    // multiple of 4 and R + 2 <= kHpelPad: no clamping, no byte gathers)
+    constexpr int kWs4 = kWinStride / 4;
+    for (int i = tid; i < W * kWs4; i += 256) {
+        const int wy = i / kWs4, wx4 = (i - wy * kWs4) * 4;
+        win32[i] = (wx4 < W) ? *reinterpret_cast<const uint32_t*>(P.f + (y0 - R + wy) * P.pitch + (x0 - R + wx4)) : 0u;
     }
     if (tid < 64) {
         const int r = tid >> 2, c = (tid & 3) * 4;
         srcw[tid] = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c);
     }
     __syncthreads();
+
+    // static-block early exit: SAD of the zero vector (same rule as the CPU encoder)
+    {
+        const int r = tid >> 4, c4 = (tid & 15) >> 2, k = tid & 3;  // tid<256 covers 16 rows x 16 px
+        const uint32_t sw = srcw[r * 4 + c4];
+        const uint8_t* win = reinterpret_cast<const uint8_t*>(win32);
+        int d = abs((int)((sw >> (8 * k)) & 0xff) - (int)win[(R + r) * kWinStride + R + c4 * 4 + k]);
+        d = wave_sum(d);
+        if (lane == 0) s_sad0[tid >> 6] = d;
+        __syncthreads();
+        const uint32_t sad0 = s_sad0[0] + s_sad0[1] + s_sad0[2] + s_sad0[3];
+        if (sad0 <= kStaticSad) {
+            if (tid == 0) {
+                mbs[mbi].mvx = 0;
+                mbs[mbi].mvy = 0;
+            }
+            return;  // uniform across the workgroup
+        }
+    }
 
     const int side = 2 * R + 1, ncand = side * side;
     unsigned long long best = ~0ull;
@@ -212,7 +230,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         unsigned long long other = __shfl_xor(best, o, 64);
         best = other < best ? other : best;
     }
-    if ((tid & 63) == 0) red[tid >> 6] = best;
+    if (lane == 0) red[tid >> 6] = best;
     __syncthreads();
     unsigned long long b = red[0];
     for (int i = 1; i < 4; ++i) b = red[i] < b ? red[i] : b;
@@ -220,36 +238,35 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     int mvx = 4 * ((cbest % side) - R), mvy = 4 * ((cbest / side) - R);
 
     if (fs->subpel) {
-        // two refinement rounds: half-pel (step 2) then quarter-pel (step 1), 8 neighbours each.
-        const int px = tid & 15, py = tid >> 4;
-        const int s = src_y[(y0 + py) * g.pitch + x0 + px];
-        uint32_t cur_cost;
-        {
-            const int p = qpel_planes(P, (x0 + px) * 4 + mvx, (y0 + py) * 4 + mvy);
-            int d = abs(s - p);
-            d = wave_sum(d);
-            __syncthreads();
-            if ((tid & 63) == 0) sub_cost[tid >> 6] = d;
-            __syncthreads();
-            cur_cost = me_cost(sub_cost[0] + sub_cost[1] + sub_cost[2] + sub_cost[3], lambda, mvx, mvy);
-        }
+        // half-pel then quarter-pel: the 8 neighbours of a step are scored at once, one per
+        // 32-lane half-wave group; each lane sums 8 pixels, a 5-step xor shuffle reduces the
+        // group, then one barrier publishes the 8 costs.
+        uint32_t cur_cost = (uint32_t)(b >> 32);
+        const int k = tid >> 5, sub = tid & 31;
+        const int py = sub >> 1, px0 = (sub & 1) * 8;
+        const uint8_t* srow = src_y + (y0 + py) * g.pitch + x0 + px0;
         for (int step = 2; step >= 1; step >>= 1) {
+            int ddx, ddy;
+            subpel_offset(k, &ddx, &ddy);
+            const int cx = mvx + ddx * step, cy = mvy + ddy * step;
+            int d = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                d += abs((int)srow[j] - qpel_planes(P, (x0 + px0 + j) * 4 + cx, (y0 + py) * 4 + cy));
+            for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+            __syncthreads();  // previous step's readers are done with cand_cost
+            if (sub == 0) cand_cost[k] = me_cost((uint32_t)d, lambda, cx, cy);
+            __syncthreads();
             int bdx = 0, bdy = 0;
             uint32_t bcost = cur_cost;
-            for (int k = 0; k < 8; ++k) {
-                int ddx, ddy;
-                subpel_offset(k, &ddx, &ddy);
-                const int cx = mvx + ddx * step, cy = mvy + ddy * step;
-                const int p = qpel_planes(P, (x0 + px) * 4 + cx, (y0 + py) * 4 + cy);
-                int d = wave_sum(abs(s - p));
-                __syncthreads();
-                if ((tid & 63) == 0) sub_cost[tid >> 6] = d;
-                __syncthreads();
-                const uint32_t cost = me_cost(sub_cost[0] + sub_cost[1] + sub_cost[2] + sub_cost[3], lambda, cx, cy);
-                if (cost < bcost) {
-                    bcost = cost;
-                    bdx = ddx * step;
-                    bdy = ddy * step;
+            for (int kk = 0; kk < 8; ++kk) {
+                const uint32_t cc = cand_cost[kk];
+                if (cc < bcost) {
+                    int ex, ey;
+                    subpel_offset(kk, &ex, &ey);
+                    bcost = cc;
+                    bdx = ex * step;
+                    bdy = ey * step;
                 }
             }
             mvx += bdx;

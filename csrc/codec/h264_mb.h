@@ -165,6 +165,16 @@ MXHD uint32_t me_cost(uint32_t sad, int lambda, int mvx, int mvy) {
     return sad + (uint32_t)(lambda * (mvd_bits(mvx) + mvd_bits(mvy)));
 }
 
+// Integer search radius actually used: clamped to [4, 32] and rounded up to a multiple of
+// 4 so the search window starts on a dword boundary.
+MXHD int me_range(int r) {
+    r = r < 4 ? 4 : (r > 32 ? 32 : r);
+    return (r + 3) & ~3;
+}
+// Static-block early exit: a zero vector with SAD <= kStaticSad ends the search (both
+// encoders apply the same rule, so their decisions stay bit-identical).
+constexpr uint32_t kStaticSad = 128;
+
 // Sub-pel refinement neighbour k (0..7) offsets.
 MXHD void subpel_offset(int k, int* dx, int* dy) {
     *dx = (k < 3) ? (k - 1) : (k == 3 ? -1 : (k == 4 ? 1 : (k - 6)));

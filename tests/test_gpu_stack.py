@@ -51,9 +51,9 @@ def test_gpu_pipeline_through_server(gpu):
 def test_gpu_framegrab_matches_synth(gpu):
     from mxdesk.server.framegrab import FrameGrabber
 
-    fg = FrameGrabber(256, 144, 60, backend="gpu")
+    fg = FrameGrabber(320, 192, 60, backend="gpu")
     a = fg.grab()
-    assert a.shape == (144, 256, 4) and a[..., 3].min() == 255
+    assert a.shape == (192, 320, 4) and a[..., 3].min() == 255
     fid, _ = read_barcode(((47 * a[..., 2].astype(int) + 157 * a[..., 1] + 16 * a[..., 0] + 128) >> 8) + 16)
     assert fid == 0
 
