@@ -17,6 +17,8 @@
 namespace py = pybind11;
 using namespace mx;
 
+void register_net(py::module& m);  // net_bindings.cpp
+
 namespace {
 
 template <class T>
@@ -90,6 +92,7 @@ PYBIND11_MODULE(_native, m) {
         return std::string(p.gcnArchName) + " / " + p.name;
     });
     m.def("synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
+    register_net(m);
     m.def("now_us", &Session::now_us, "CLOCK_MONOTONIC microseconds (same clock as time.monotonic())");
 
     // ---------------------------------------------------------------- codec helpers

@@ -117,8 +117,9 @@ class TileExchange:
                    if r != self.root]
         else:
             ops = [dist.P2POp(dist.isend, tile, self.root)]
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+        if ops:  # world size 1: nothing to exchange
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
         return self.tiles if self.rank == self.root else None
 
 
