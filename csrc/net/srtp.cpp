@@ -122,12 +122,24 @@ std::string SrtpSession::protect_rtp(const std::string& rtp) {
     uint8_t* b = (uint8_t*)&out[0];
     const uint16_t seq = be16(b + 2);
     const uint32_t ssrc = be32(b + 8);
-    if (have_seq_ && seq < last_seq_ && (uint16_t)(last_seq_ - seq) > 0x8000) ++roc_;  // wrapped
-    if (!have_seq_ || (int16_t)(seq - last_seq_) > 0) last_seq_ = seq;
-    have_seq_ = true;
-    const uint64_t index = ((uint64_t)roc_ << 16) | seq;
+    // Sender-side index: advance ROC on forward wrap; a retransmission of a packet sent
+    // before the last wrap keeps its original (previous) ROC.
+    uint32_t v = roc_;
+    if (!have_seq_) {
+        last_seq_ = seq;
+        have_seq_ = true;
+    } else {
+        const int16_t d = (int16_t)(uint16_t)(seq - last_seq_);
+        if (d > 0) {
+            if (seq < last_seq_) v = ++roc_;
+            last_seq_ = seq;
+        } else if (d < 0 && seq > last_seq_) {
+            v = roc_ - 1;
+        }
+    }
+    const uint64_t index = ((uint64_t)v << 16) | seq;
     xor_keystream(k_e_, k_s_, ssrc, index, b + hl, out.size() - hl);
-    const uint8_t roc_be[4] = {(uint8_t)(roc_ >> 24), (uint8_t)(roc_ >> 16), (uint8_t)(roc_ >> 8), (uint8_t)roc_};
+    const uint8_t roc_be[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
     uint8_t tag[10];
     hmac80(k_a_, (const uint8_t*)out.data(), out.size(), roc_be, 4, tag);
     out.append((const char*)tag, 10);

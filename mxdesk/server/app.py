@@ -59,6 +59,10 @@ class MediaServer:
         self.start_pipeline = start_pipeline
         self.clients: set[web.WebSocketResponse] = set()
         self.resize_enabled = bool(getattr(cfg, "enable_resize", False))
+        from .webrtc import WhepEndpoint
+
+        self.whep = WhepEndpoint(pipeline, host=getattr(cfg, "webrtc_host", None) or None,
+                                 udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0))
 
     # ------------------------------------------------------------------ app
     def make_app(self) -> web.Application:
@@ -77,6 +81,7 @@ class MediaServer:
         app.router.add_get("/manifest.json", self.manifest)
         app.router.add_get("/ws", self.signalling.handler)
         app.router.add_get("/mxws", self.media_ws)
+        self.whep.routes(app)
         if self.rfb is not None:
             app.router.add_get("/websockify", self.rfb.ws_handler)
         if self.web_root.is_dir():
@@ -91,6 +96,7 @@ class MediaServer:
             self.pipeline.start()
 
     async def _on_cleanup(self, app):
+        self.whep.close_all()
         self.pipeline.stop()
         for ws in list(self.clients):
             await ws.close()
@@ -142,9 +148,11 @@ class MediaServer:
             "type": "config", "codec": h264_codec_string(p.out_w, p.out_h, p.fps), "width": p.out_w,
             "height": p.out_h, "fps": p.fps, "resize": self.resize_enabled,
         }))
-        sub = p.subscribe(asyncio.get_running_loop())
+        # ?media=0: control/input channel only (the WebRTC client receives video over SRTP)
+        media = request.query.get("media", "1") != "0"
+        sub = p.subscribe(asyncio.get_running_loop()) if media else None
         self.clients.add(ws)
-        sender = asyncio.create_task(self._send_loop(ws, sub))
+        sender = asyncio.create_task(self._send_loop(ws, sub)) if media else None
         try:
             async for msg in ws:
                 if msg.type == WSMsgType.TEXT:
@@ -152,8 +160,9 @@ class MediaServer:
                 elif msg.type == WSMsgType.ERROR:
                     break
         finally:
-            sender.cancel()
-            p.unsubscribe(sub)
+            if sender is not None:
+                sender.cancel()
+                p.unsubscribe(sub)
             self.clients.discard(ws)
         return ws
 

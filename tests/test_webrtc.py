@@ -1,0 +1,182 @@
+"""WebRTC transport: STUN (RFC 5769 vectors), SRTP (RFC 3711 B.2/B.3 vectors + roundtrip),
+DTLS-SRTP handshake, RFC 6184 packetizer <-> depacketizer, RTCP builders, SDP answer, and a
+full WHEP loopback (ICE-lite -> DTLS -> SRTP -> H.264 depacketize -> independent decoder ->
+barcode) with NACK retransmission and PLI -> IDR."""
+import asyncio
+import os
+import struct
+
+import pytest
+
+from mxdesk.codec.h264_decoder import Decoder
+from mxdesk.models.synthetic import read_barcode
+from mxdesk.server import rtp as R
+from mxdesk.server import stun as S
+from mxdesk.server.webrtc import build_answer, parse_sdp, pick_h264
+from mxdesk.server.whep_client import make_offer, whep_view
+
+from .test_server import free_port, make_server
+
+# RFC 5769 §2.1 sample request (password "VOkJxbRl1RmTxUk/WvJxBt")
+RFC5769_REQ = bytes.fromhex(
+    "000100582112a442b7e7a701bc34d686fa87dfae802200105354554e2074657374"
+    "20636c69656e7400240004" "6e0001ff80290008932ff9b151263b36000600096576746a3a6836765920202000080014"
+    "9aeaa70cbfd8cb56781ef2b5b2d3f249c1b571a280280004e57a3bcf")
+
+
+def test_stun_rfc5769_request_vector():
+    m = S.StunMessage.decode(RFC5769_REQ)
+    assert m.type == S.BINDING_REQUEST
+    assert m.get(S.A_USERNAME) == b"evtj:h6vY"
+    assert m.check_integrity(b"VOkJxbRl1RmTxUk/WvJxBt")
+    assert not m.check_integrity(b"wrong")
+    bad = bytearray(RFC5769_REQ)
+    bad[30] ^= 1
+    assert not S.StunMessage.decode(bytes(bad)).check_integrity(b"VOkJxbRl1RmTxUk/WvJxBt")
+
+
+def test_stun_roundtrip_and_xor_address():
+    tid = os.urandom(12)
+    for host, port in [("192.0.2.1", 32853), ("2001:db8:1234:5678:11:2233:4455:6677", 32853)]:
+        v = S.xor_address(host, port, tid)
+        assert S.parse_xor_address(v, tid) == (host, port)
+    m = S.StunMessage(S.BINDING_SUCCESS, tid, [(S.A_XOR_MAPPED_ADDRESS, S.xor_address("10.1.2.3", 5000, tid))])
+    raw = m.encode(b"key")
+    d = S.StunMessage.decode(raw)
+    assert S.is_stun(raw) and d.tid == tid and d.check_integrity(b"key")
+    assert S.parse_xor_address(d.get(S.A_XOR_MAPPED_ADDRESS), tid) == ("10.1.2.3", 5000)
+    # RFC 5769 §2.2 response XOR-MAPPED-ADDRESS (192.0.2.1:32853)
+    tid2 = bytes.fromhex("b7e7a701bc34d686fa87dfae")
+    assert S.parse_xor_address(bytes.fromhex("0001a147e112a643"), tid2) == ("192.0.2.1", 32853)
+
+
+def test_srtp_rfc3711_vectors(native):
+    net = native.net
+    ks = net.SrtpSession.aes_cm_keystream(bytes.fromhex("2B7E151628AED2A6ABF7158809CF4F3C"),
+                                          bytes.fromhex("F0F1F2F3F4F5F6F7F8F9FAFBFCFD0000"), 48)
+    assert ks.hex() == ("e03ead0935c95e80e166b16dd92b4eb4d23513162b02d0f72a43a2fe4a5f97ab"
+                        "41e95b3bb0a2e8dd477901e4fca894c0")
+    s = net.SrtpSession(bytes.fromhex("E1F97A0D3E018BE0D64FA32C06DE4139"), bytes.fromhex("0EC675AD498AFEEBB6960B3AABE6"))
+    assert s.rtp_key.hex() == "c61e7a93744f39ee10734afe3ff7a087"
+    assert s.rtp_salt.hex() == "30cbbc08863d8c85d49db34a9ae1"
+    assert s.rtp_auth.hex()[:40] == "cebe321f6ff7716b6fd4ab49af256a156d38baa4"
+
+
+def test_srtp_roundtrip_tamper_and_wrap(native):
+    net = native.net
+    k, salt = os.urandom(16), os.urandom(14)
+    tx, rx = net.SrtpSession(k, salt), net.SrtpSession(k, salt)
+    seqs = list(range(65530, 65536)) + list(range(0, 6))
+    sent = []
+    for i, seq in enumerate(seqs):
+        pkt = struct.pack("!BBHII", 0x80, 96, seq, 1000 * i, 0x1234) + os.urandom(50)
+        p = tx.protect_rtp(pkt)
+        sent.append((pkt, p))
+        assert len(p) == len(pkt) + 10 and p[12:62] != pkt[12:]
+        assert rx.unprotect_rtp(p) == pkt
+    # retransmission of a pre-wrap packet after the wrap keeps its ROC
+    pkt0, p0 = sent[2]
+    assert tx.protect_rtp(pkt0) == p0
+    assert rx.unprotect_rtp(p0) == pkt0
+    bad = bytearray(sent[-1][1])
+    bad[20] ^= 0x40
+    assert rx.unprotect_rtp(bytes(bad)) == b""
+    rtcp = R.build_pli(1, 2)
+    c = tx.protect_rtcp(rtcp)
+    assert rx.unprotect_rtcp(c) == rtcp and len(c) == len(rtcp) + 14
+
+
+def test_dtls_srtp_handshake(native):
+    net = native.net
+    srv, cli = net.DtlsEndpoint(True), net.DtlsEndpoint(False)
+    assert srv.fingerprint.startswith("sha-256 ") and len(srv.fingerprint) == 8 + 32 * 3 - 1  # one identity per process
+    to_srv = cli.start()
+    for _ in range(20):
+        to_cli = [d for x in to_srv for d in srv.feed(x)]
+        to_srv = [d for x in to_cli for d in cli.feed(x)]
+        if srv.handshake_done and cli.handshake_done:
+            break
+    assert srv.handshake_done and cli.handshake_done, (srv.error, cli.error)
+    assert srv.peer_fingerprint == cli.fingerprint and cli.peer_fingerprint == srv.fingerprint
+    assert srv.srtp_profile == cli.srtp_profile == "SRTP_AES128_CM_SHA1_80"
+    km = srv.export_srtp_keys()
+    assert len(km) == 60 and km == cli.export_srtp_keys()
+
+
+def _annexb(nals):
+    return b"".join(b"\x00\x00\x00\x01" + n for n in nals)
+
+
+def test_packetizer_depacketizer_roundtrip(native):
+    net = native.net
+    sps, pps = b"\x67\x42\xc0\x2a" + os.urandom(8), b"\x68\xce\x3c\x80"
+    big = b"\x65" + os.urandom(5000)
+    small = b"\x41" + os.urandom(100)
+    au = _annexb([sps, pps, big, small])
+    assert [bytes(x) for x in net.split_annexb(au)] == [sps, pps, big, small]
+    pk = net.RtpH264Packetizer(0xABCD, 102, 1150, 65534)
+    pkts = pk.packetize(au, 12345)
+    assert all(len(p) <= 12 + 1150 for p in pkts)
+    hs = [R.rtp_header(p) for p in pkts]
+    assert [h["marker"] for h in hs] == [False] * (len(pkts) - 1) + [True]
+    assert hs[0]["payload"][0] & 0x1F == 24  # STAP-A with SPS+PPS
+    assert any(h["payload"][0] & 0x1F == 28 for h in hs)  # FU-A
+    assert [h["seq"] for h in hs][:3] == [65534, 65535, 0] and all(h["ts"] == 12345 for h in hs)
+    d = R.H264Depacketizer()
+    outs = [d.push(p) for p in pkts]
+    assert outs[-1] == au and all(o is None for o in outs[:-1]) and d.lost == 0
+    assert pk.packets == len(pkts)
+
+
+def test_rtcp_builders_parse():
+    nack = R.build_nack(1, 2, [100, 101, 105, 116, 117, 200])
+    (p,) = R.parse_rtcp(nack)
+    assert p["pt"] == 205 and p["fmt"] == 1 and sorted(p["nack"]) == [100, 101, 105, 116, 117, 200]
+    parsed = R.parse_rtcp(R.build_sr(7, 9000, 10, 1000) + R.build_pli(1, 7))
+    assert [(x["pt"], x["fmt"]) for x in parsed] == [(200, 0), (202, 1), (206, 1)]
+    assert parsed[0]["ssrc"] == 7
+
+
+def test_sdp_answer():
+    offer = make_offer("abcd", "p" * 24, "sha-256 AA:BB", h264_pt=102)
+    assert pick_h264(parse_sdp(offer).media[0]) == "102"
+    a = build_answer(offer, "uf", "pw" * 12, "sha-256 CC:DD", "127.0.0.1", 5000, 42)
+    assert a.pt == 102 and a.mid == "0" and a.remote_ufrag == "abcd" and a.remote_fingerprint == "sha-256 AA:BB"
+    sdp = parse_sdp(a.sdp)
+    assert "a=ice-lite" in sdp.session and "a=group:BUNDLE 0" in sdp.session
+    v, au = sdp.media
+    assert v.kind == "video" and v.port == 5000 and v.fmts == ["102"] and v.attr("setup") == "passive"
+    assert "packetization-mode=1" in v.attr("fmtp") and v.attr("sendonly") == ""
+    assert au.kind == "audio" and au.port == 0
+    with pytest.raises(ValueError):
+        build_answer(offer.replace("H264", "H265"), "uf", "pw", "fp", "127.0.0.1", 5000, 42)
+
+
+def test_whep_loopback_decodes_with_nack_and_pli(native, monkeypatch):
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+    from mxdesk.server.app import serve
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            res = await whep_view(f"http://127.0.0.1:{port}/whep", 12, drop_seq_every=7, pli_after=5)
+            peers = dict(srv.whep.peers)
+            return res, peers
+        finally:
+            await runner.cleanup()
+
+    res, peers = asyncio.run(go())
+    assert len(res.aus) == 12 and res.lost > 0 and res.rtx == res.lost
+    frames = Decoder().decode(res.stream)
+    assert len(frames) == 12
+    ids = [read_barcode(y)[0] for y, _, _ in frames]
+    assert all(b == a + 1 for a, b in zip(ids, ids[1:]))
+    # 90 kHz timestamps follow the capture clock (30 fps -> ~3000 ticks)
+    dts = [(b - a) & 0xFFFFFFFF for a, b in zip(res.rtp_ts, res.rtp_ts[1:])]
+    assert all(1000 < d < 9000 for d in dts)
+    # the PLI after frame 5 produced a second IDR (NAL type 5) within the next frames
+    idr = [i for i, au in enumerate(res.aus) if any((n[0] & 0x1F) == 5 for n in native.net.split_annexb(au))]
+    assert idr[0] == 0 and any(i >= 5 for i in idr[1:])
+    assert not peers  # DELETE /whep/<id> removed the session

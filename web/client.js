@@ -1,6 +1,8 @@
 // mxdesk browser client: receives Annex-B H.264 access units over the /mxws WebSocket,
 // decodes them with WebCodecs (hardware decoder on the viewer's machine) and paints a
 // canvas; mouse/keyboard/clipboard events go back as selkies-style text messages.
+// `?transport=webrtc` instead plays the stream through RTCPeerConnection (WHEP offer/answer
+// against POST /whep; SRTP video into a <video> element) and keeps /mxws?media=0 for input.
 "use strict";
 const mxdesk = (() => {
   const HDR = 36;
@@ -86,9 +88,34 @@ const mxdesk = (() => {
     });
   }
 
-  function connect() {
+  async function whep(video) {
+    const pc = new RTCPeerConnection({ iceServers: [] });
+    pc.addTransceiver("video", { direction: "recvonly" });
+    pc.ontrack = (ev) => { video.srcObject = ev.streams[0] || new MediaStream([ev.track]); video.play().catch(() => {}); };
+    pc.onconnectionstatechange = () => {
+      msgEl.textContent = pc.connectionState === "connected" ? "" : "webrtc: " + pc.connectionState;
+      if (pc.connectionState === "failed") { pc.close(); setTimeout(() => whep(video), 1000); }
+    };
+    await pc.setLocalDescription(await pc.createOffer());
+    const r = await fetch("whep", { method: "POST", headers: { "Content-Type": "application/sdp" }, body: pc.localDescription.sdp });
+    if (r.status !== 201) { msgEl.textContent = "WHEP failed: " + r.status; return; }
+    const loc = r.headers.get("Location");
+    window.addEventListener("beforeunload", () => { fetch(loc, { method: "DELETE", keepalive: true }); });
+    await pc.setRemoteDescription({ type: "answer", sdp: await r.text() });
+    setInterval(async () => {
+      const st = await pc.getStats();
+      st.forEach((x) => {
+        if (x.type === "inbound-rtp" && x.kind === "video") {
+          statsEl.textContent = `webrtc ${x.frameWidth}x${x.frameHeight}\n${(x.framesPerSecond || 0).toFixed(1)} fps ` +
+            `lost ${x.packetsLost} nack ${x.nackCount} pli ${x.pliCount}`;
+        }
+      });
+    }, 1000);
+  }
+
+  function connect(media = true) {
     const proto = location.protocol === "https:" ? "wss:" : "ws:";
-    ws = new WebSocket(`${proto}//${location.host}/mxws`);
+    ws = new WebSocket(`${proto}//${location.host}/mxws${media ? "" : "?media=0"}`);
     ws.binaryType = "arraybuffer";
     ws.onmessage = (ev) => {
       if (typeof ev.data === "string") {
@@ -98,13 +125,21 @@ const mxdesk = (() => {
       }
       if (cfg) onFrame(ev.data);
     };
-    ws.onclose = () => { msgEl.textContent = "disconnected - retrying"; setTimeout(connect, 1000); };
+    ws.onclose = () => { msgEl.textContent = "disconnected - retrying"; setTimeout(() => connect(media), 1000); };
   }
 
   return {
-    start(c, s, m) {
-      canvas = c; statsEl = s; msgEl = m; ctx = canvas.getContext("2d");
-      if (!("VideoDecoder" in window)) { msgEl.textContent = "WebCodecs not supported by this browser"; return; }
+    start(c, s, m, video) {
+      canvas = c; statsEl = s; msgEl = m;
+      if (new URLSearchParams(location.search).get("transport") === "webrtc" || !("VideoDecoder" in window)) {
+        // video element on top; input events still come from the canvas-sized overlay
+        video.style.display = "block"; canvas.style.position = "fixed"; canvas.style.inset = "0";
+        canvas.width = 1920; canvas.height = 1080; canvas.style.opacity = "0";
+        video.addEventListener("resize", () => { canvas.width = video.videoWidth; canvas.height = video.videoHeight; });
+        input(); connect(false); whep(video);
+        return;
+      }
+      ctx = canvas.getContext("2d");
       input(); connect();
     },
     parse,
