@@ -48,6 +48,33 @@ def test_gpu_pipeline_through_server(gpu):
     assert res.p50_ms < 50
 
 
+def test_gpu_pipeline_over_webrtc(gpu, monkeypatch):
+    """GPU encoder -> WHEP/DTLS-SRTP -> depacketize -> independent decoder, with NACK + PLI."""
+    from mxdesk.pipeline.stream import StreamPipeline
+    from mxdesk.server.app import MediaServer, serve
+    from mxdesk.server.whep_client import whep_view
+    from mxdesk.utils import config as C
+
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg = C.load(env={"ENABLE_BASIC_AUTH": "false", "SIZEW": "320", "SIZEH": "192"}, argv=[])
+    pipe = StreamPipeline(320, 192, 60, backend="gpu", bitrate_kbps=0)
+    srv = MediaServer(pipe, cfg)
+
+    async def go():
+        port = _free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await whep_view(f"http://127.0.0.1:{port}/whep", 16, drop_seq_every=5, pli_after=6)
+        finally:
+            await runner.cleanup()
+
+    res = asyncio.run(go())
+    frames = Decoder().decode(res.stream)
+    assert len(frames) == 16 and res.rtx == res.lost
+    ids = [read_barcode(y)[0] for y, _, _ in frames]
+    assert all(b == a + 1 for a, b in zip(ids, ids[1:]))
+
+
 def test_gpu_framegrab_matches_synth(gpu):
     from mxdesk.server.framegrab import FrameGrabber
 
