@@ -43,6 +43,7 @@ def main() -> None:
     ap.add_argument("--bitrate-kbps", type=int, default=8000)
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
+    ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
 
@@ -70,6 +71,7 @@ def main() -> None:
     cfg.enc.bitrate_kbps = args.bitrate_kbps
     cfg.enc.search_range = args.search_range
     cfg.enc.subpel = args.subpel
+    cfg.noise = args.noise
     sess = N.Session(cfg)
 
     for _ in range(args.warmup):
@@ -83,12 +85,13 @@ def main() -> None:
 
     barrier()
     t0 = time.perf_counter()
-    lat_ms, sizes, qps, gpu_ms = [], [], [], []
+    lat_ms, sizes, qps, gpu_ms, psnrs = [], [], [], [], []
     for _ in range(args.steps):
         r = sess.step(False)
         lat_ms.append((r.t_encoded_us - r.t_capture_us) / 1000.0)
         sizes.append(len(r.au))
         qps.append(r.qp)
+        psnrs.append(r.psnr_y)
         gpu_ms.append(r.gpu_ms)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -132,6 +135,7 @@ def main() -> None:
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),
             "mean_qp": round(statistics.mean(qps), 2),
+            "mean_psnr_y_db": round(statistics.mean(psnrs), 2),
             "dtype": "uint8 video (8-bit 4:2:0), H.264 Constrained Baseline",
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",
             "config": {

@@ -137,7 +137,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("qp", &h264::FrameStats::qp)
         .def_readonly("bytes", &h264::FrameStats::bytes)
         .def_readonly("skipped_mbs", &h264::FrameStats::skipped_mbs)
-        .def_readonly("encode_ms", &h264::FrameStats::encode_ms);
+        .def_readonly("encode_ms", &h264::FrameStats::encode_ms)
+        .def_property_readonly("sse", [](const h264::FrameStats& s) { return py::make_tuple(s.sse[0], s.sse[1], s.sse[2]); });
 
     py::class_<h264::CpuH264Encoder>(m, "CpuH264Encoder")
         .def(py::init<const h264::EncoderConfig&>())
@@ -314,6 +315,9 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("gpu_ms", &FrameResult::gpu_ms)
         .def_readonly("idr", &FrameResult::idr)
         .def_readonly("qp", &FrameResult::qp)
+        .def_readonly("psnr_y", &FrameResult::psnr_y)
+        .def_readonly("psnr_u", &FrameResult::psnr_u)
+        .def_readonly("psnr_v", &FrameResult::psnr_v)
         .def_property_readonly("au", [](const FrameResult& r) { return to_bytes(r.au); });
 
     py::class_<Session>(m, "Session")

@@ -39,6 +39,7 @@ struct FrameStats {
     int bytes = 0;
     int skipped_mbs = 0;
     double encode_ms = 0;
+    uint64_t sse[3] = {0, 0, 0};  // source vs reconstruction (Y, U, V), display area
 };
 
 // Annex-B / rate-control logic shared by both encoders.

@@ -62,6 +62,9 @@ struct FrameState {
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
     const uint8_t* hp_v;  // vertical half sample h at (x, y+1/2)
     const uint8_t* hp_j;  // centre half sample j at (x+1/2, y+1/2)
+    // per-frame distortion accumulators (Y, U, V) over the display area; k_scan moves
+    // them into OutHeader and clears them for the next frame
+    unsigned long long* sse;
 };
 constexpr int kHpelPad = 48;
 
@@ -71,7 +74,10 @@ struct OutHeader {
     uint32_t num_slices;
     uint32_t overflow;     // nonzero if any MB exceeded its slot
     uint32_t pad;
+    uint64_t sse[3];       // source vs reconstruction squared error (Y, U, V)
+    uint64_t pad2;
 };
+static_assert(sizeof(OutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
 // slice_info fields: 0 header bits, 1 byte offset, 2 bytes, 3 trailing skip run,
 // 4 data-end bit (trailer start), 5 unit-bit prefix at the slice's first MB,
@@ -100,6 +106,7 @@ struct DeviceBuffers {
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
+    unsigned long long* sse;  // [3] distortion accumulators
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.

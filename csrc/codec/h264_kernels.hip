@@ -325,6 +325,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
 
     int z[16];
     int nz = 0;
+    int sse_y = 0, sse_c = 0;
     int16_t* mc = coef + (size_t)(valid ? mbi : 0) * kCoefStride;
     if (valid && lane < 16) {
         const int b = lane, bx = kBlkX[b], by = kBlkY[b];
@@ -335,10 +336,15 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         nz = luma_block_inter(x, qp, zs, r);
         for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
         mbs[mbi].nz_luma[by * 4 + bx] = (uint8_t)nz;
+        const bool vis_x = x0 + bx * 4 < g.width;
         for (int i = 0; i < 4; ++i) {
             uint32_t packed = 0;
+            const bool vis = vis_x && (y0 + by * 4 + i) < g.height;
             for (int j = 0; j < 4; ++j) {
-                const int v = clip255(pred[wave][(by * 4 + i) * 16 + bx * 4 + j] + r[i * 4 + j]);
+                const int pv = pred[wave][(by * 4 + i) * 16 + bx * 4 + j];
+                const int v = clip255(pv + r[i * 4 + j]);
+                const int e = pv + x[i * 4 + j] - v;
+                sse_y += vis ? e * e : 0;
                 packed |= (uint32_t)v << (8 * j);
             }
             *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + by * 4 + i) * g.pitch + x0 + bx * 4) = packed;
@@ -375,9 +381,23 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         const int xc = x0 / 2 + bx * 4, yc = y0 / 2 + by * 4;
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) {
-                const int v = clip255(pred[wave][256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j] + r[i * 4 + j]);
+                const int o = 256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j;
+                const int v = clip255(pred[wave][o] + r[i * 4 + j]);
+                const int e = pred[wave][o] + res[wave][o] - v;
+                sse_c += (2 * (xc + j) < g.width && 2 * (yc + i) < g.height) ? e * e : 0;
                 fs->rec_uv[(yc + i) * g.pitch + 2 * (xc + j) + comp] = (uint8_t)v;
             }
+    }
+    {
+        // Y on lanes 0..15, U on 16..19, V on 20..23
+        const int sy = wave_sum(sse_y);
+        const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
+        const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
+        if (valid && lane == 0) {
+            atomicAdd(&fs->sse[0], (unsigned long long)sy);
+            atomicAdd(&fs->sse[1], (unsigned long long)su);
+            atomicAdd(&fs->sse[2], (unsigned long long)sv);
+        }
     }
     const unsigned long long luma_mask = __ballot(valid && lane < 16 && nz > 0);
     const unsigned long long chroma_mask = __ballot(valid && lane >= 16 && lane < 24 && nz > 0);
@@ -414,6 +434,7 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     const int y0 = mby * 16;
 
+    unsigned long long sse_row[3] = {0, 0, 0};
     for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16;
         const bool have_left = mbx > 0;
@@ -513,6 +534,7 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
         const unsigned long long luma_mask = __ballot(lane < 16 && nz > 0);
         const unsigned long long chroma_mask = __ballot(lane >= 16 && lane < 24 && nz > 0);
         const bool luma_ac = luma_mask != 0;
+        int sse_y = 0, sse_c = 0;
         // ---- reconstruction
         if (lane < 16) {
             const int b = lane, bx = kBlkX[b], by = kBlkY[b];
@@ -526,8 +548,12 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
             idct4x4(d, rr);
             for (int i = 0; i < 4; ++i) {
                 uint32_t packed = 0;
+                const bool vis = x0 + bx * 4 < g.width && (y0 + by * 4 + i) < g.height;
                 for (int j = 0; j < 4; ++j) {
-                    const int v = clip255(pred[(by * 4 + i) * 16 + bx * 4 + j] + rr[i * 4 + j]);
+                    const int o = (by * 4 + i) * 16 + bx * 4 + j;
+                    const int v = clip255(pred[o] + rr[i * 4 + j]);
+                    const int e = pred[o] + res[o] - v;
+                    sse_y += vis ? e * e : 0;
                     packed |= (uint32_t)v << (8 * j);
                     if (bx == 3 && j == 3) left[by * 4 + i] = (uint8_t)v;
                 }
@@ -543,12 +569,18 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
             const int xcb = x0 / 2 + bx * 4, ycb = y0 / 2 + by * 4;
             for (int i = 0; i < 4; ++i)
                 for (int j = 0; j < 4; ++j) {
-                    const int v = clip255(pred[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j] + rr[i * 4 + j]);
+                    const int o = 256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j;
+                    const int v = clip255(pred[o] + rr[i * 4 + j]);
+                    const int e = pred[o] + res[o] - v;
+                    sse_c += (2 * (xcb + j) < g.width && 2 * (ycb + i) < g.height) ? e * e : 0;
                     fs->rec_uv[(ycb + i) * g.pitch + 2 * (xcb + j) + comp] = (uint8_t)v;
                     if (bx == 1 && j == 3) left[16 + comp * 8 + by * 4 + i] = (uint8_t)v;
                 }
             (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
         }
+        sse_row[0] += wave_sum(sse_y);
+        sse_row[1] += wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
+        sse_row[2] += wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
         if (lane == 0) {
             const int ccbp = (chroma_mask != 0) ? 2 : ((cdc_nz[0] | cdc_nz[1]) ? 1 : 0);
             MbInfo& m = mbs[mbi];
@@ -562,6 +594,8 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
         __syncthreads();
         (void)modes;
     }
+    if (lane == 0)
+        for (int c = 0; c < 3; ++c) atomicAdd(&fs->sse[c], sse_row[c]);
 }
 
 // ------------------------------------------------------------------ CAVLC
@@ -802,6 +836,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         hdr->total_bytes = over ? 0 : total_bytes;
         hdr->num_slices = ns;
         hdr->overflow = s_overflow | (over ? 2u : 0u);
+        for (int c = 0; c < 3; ++c) {
+            hdr->sse[c] = fs->sse[c];
+            fs->sse[c] = 0;
+        }
     }
 }
 

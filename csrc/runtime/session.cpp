@@ -184,6 +184,11 @@ FrameResult Session::collect() {
     r.idr = st.idr;
     r.qp = st.qp;
     r.gpu_ms = st.encode_ms;
+    const double ny = (double)enc_->common().config().width * enc_->common().config().height, nc = ny / 4;
+    auto psnr = [](uint64_t sse, double n) { return sse == 0 ? 99.0 : std::min(99.0, 10.0 * std::log10(65025.0 * n / (double)sse)); };
+    r.psnr_y = psnr(st.sse[0], ny);
+    r.psnr_u = psnr(st.sse[1], nc);
+    r.psnr_v = psnr(st.sse[2], nc);
     return r;
 }
 

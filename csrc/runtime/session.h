@@ -62,6 +62,7 @@ struct FrameResult {
     double gpu_ms = 0;         // device time render->bitstream (events)
     int idr = 0;
     int qp = 0;
+    double psnr_y = 0, psnr_u = 0, psnr_v = 0;  // encoder reconstruction vs source (dB, cap 99)
     std::vector<uint8_t> au;
 };
 

@@ -171,3 +171,31 @@ def test_session_scaled_output(gpu):
     stream = b"".join(s.step(False).au for _ in range(2))
     frames = Decoder().decode(stream)
     assert frames[0][0].shape == (192, 320)
+
+
+def test_session_reports_psnr_of_reconstruction(gpu):
+    """Encoder-side SSE (k_inter_encode / k_intra_rows -> k_scan) equals the PSNR of the
+    independently decoded picture against the source, over the display area only."""
+    cfg = gpu.SessionConfig()
+    cfg.width, cfg.height, cfg.fps = 200, 120, 60  # coded 208x128: padding must be excluded
+    cfg.enc.bitrate_kbps = 0
+    cfg.enc.qp = 30
+    s = gpu.Session(cfg)
+    stream, res, srcs = b"", [], []
+    for _ in range(3):
+        r = s.step(False)
+        stream += r.au
+        res.append(r)
+        y, uv = s.nv12()
+        srcs.append((y[:120, :200].astype(np.float64), uv[:60, :200].astype(np.float64)))
+    frames = Decoder().decode(stream)
+
+    def psnr(a, b):
+        mse = np.mean((a - b) ** 2)
+        return 99.0 if mse == 0 else min(99.0, 10 * np.log10(255.0 ** 2 / mse))
+
+    for (dy, du, dv), (sy, suv), r in zip(frames, srcs, res):
+        assert abs(psnr(dy.astype(np.float64), sy) - r.psnr_y) < 1e-6
+        assert abs(psnr(du.astype(np.float64), suv[:, 0::2]) - r.psnr_u) < 1e-6
+        assert abs(psnr(dv.astype(np.float64), suv[:, 1::2]) - r.psnr_v) < 1e-6
+        assert 25 < r.psnr_y < 99
