@@ -62,9 +62,9 @@ struct FrameState {
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
     const uint8_t* hp_v;  // vertical half sample h at (x, y+1/2)
     const uint8_t* hp_j;  // centre half sample j at (x+1/2, y+1/2)
-    // per-frame distortion accumulators (Y, U, V) over the display area; k_scan moves
-    // them into OutHeader and clears them for the next frame
-    unsigned long long* sse;
+    // per-MB distortion (Y, U, V) over the display area, [nmb * 3]; written by the
+    // inter/intra kernels, reduced by k_scan into OutHeader (no contended atomics)
+    uint32_t* sse_mb;
 };
 constexpr int kHpelPad = 48;
 
@@ -106,7 +106,7 @@ struct DeviceBuffers {
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
-    unsigned long long* sse;  // [3] distortion accumulators
+    uint32_t* sse_mb;         // [nmb * 3] per-MB distortion
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.

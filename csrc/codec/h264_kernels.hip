@@ -394,9 +394,9 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
         const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
         if (valid && lane == 0) {
-            atomicAdd(&fs->sse[0], (unsigned long long)sy);
-            atomicAdd(&fs->sse[1], (unsigned long long)su);
-            atomicAdd(&fs->sse[2], (unsigned long long)sv);
+            fs->sse_mb[3 * mbi + 0] = (uint32_t)sy;
+            fs->sse_mb[3 * mbi + 1] = (uint32_t)su;
+            fs->sse_mb[3 * mbi + 2] = (uint32_t)sv;
         }
     }
     const unsigned long long luma_mask = __ballot(valid && lane < 16 && nz > 0);
@@ -434,7 +434,6 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     const int y0 = mby * 16;
 
-    unsigned long long sse_row[3] = {0, 0, 0};
     for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16;
         const bool have_left = mbx > 0;
@@ -578,9 +577,16 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
                 }
             (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
         }
-        sse_row[0] += wave_sum(sse_y);
-        sse_row[1] += wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
-        sse_row[2] += wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
+        {
+            const int sy = wave_sum(sse_y);
+            const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
+            const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
+            if (lane == 0) {
+                fs->sse_mb[3 * mbi + 0] = (uint32_t)sy;
+                fs->sse_mb[3 * mbi + 1] = (uint32_t)su;
+                fs->sse_mb[3 * mbi + 2] = (uint32_t)sv;
+            }
+        }
         if (lane == 0) {
             const int ccbp = (chroma_mask != 0) ? 2 : ((cdc_nz[0] | cdc_nz[1]) ? 1 : 0);
             MbInfo& m = mbs[mbi];
@@ -594,8 +600,6 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
         __syncthreads();
         (void)modes;
     }
-    if (lane == 0)
-        for (int c = 0; c < 3; ++c) atomicAdd(&fs->sse[c], sse_row[c]);
 }
 
 // ------------------------------------------------------------------ CAVLC
@@ -836,9 +840,23 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         hdr->total_bytes = over ? 0 : total_bytes;
         hdr->num_slices = ns;
         hdr->overflow = s_overflow | (over ? 2u : 0u);
+    }
+    // distortion: block-wide reduction of the per-MB partials
+    {
+        unsigned long long acc[3] = {0, 0, 0};
+        for (int i = t; i < nmb; i += kScanThreads)
+            for (int c = 0; c < 3; ++c) acc[c] += fs->sse_mb[3 * i + c];
+        __shared__ unsigned long long red[3][kScanThreads / 64];
         for (int c = 0; c < 3; ++c) {
-            hdr->sse[c] = fs->sse[c];
-            fs->sse[c] = 0;
+            unsigned long long v = acc[c];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if ((t & 63) == 0) red[c][t >> 6] = v;
+        }
+        __syncthreads();
+        if (t < 3) {
+            unsigned long long v = 0;
+            for (int w = 0; w < kScanThreads / 64; ++w) v += red[t][w];
+            hdr->sse[t] = v;
         }
     }
 }

@@ -91,9 +91,9 @@ def lanczos_tables(in_w: int, in_h: int, out_w: int, out_h: int, device):
     key = (in_w, in_h, out_w, out_h, str(device))
     if key not in _tables:
         N = native()
-        sx, wx = N.lanczos_table(in_w, out_w)
-        sy, wy = N.lanczos_table(in_h, out_h)
-        _tables[key] = tuple(torch.from_numpy(a).to(device) for a in (sx, wx, sy, wy)) + (wx.shape[1], wy.shape[1])
+        sx, wx, tx = N.lanczos_table(in_w, out_w)
+        sy, wy, ty = N.lanczos_table(in_h, out_h)
+        _tables[key] = tuple(torch.from_numpy(a).to(device) for a in (sx, wx, sy, wy)) + (tx, ty)
     return _tables[key]
 
 
