@@ -146,7 +146,8 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     // payload capacity: 768 B per MB (intra at low QP stays far below)
     buf_.out_bytes = (size_t)nmb * 768;
     HIP_CHECK(hipMalloc(&buf_.out_hdr, sizeof(OutHeader)));
-    HIP_CHECK(hipMalloc(&buf_.sse_mb, 3 * sizeof(uint32_t) * nmb));
+    if ((nmb + 3) / 4 > kSsePartStride) throw std::invalid_argument("frame too large for the distortion partials");
+    HIP_CHECK(hipMalloc(&buf_.sse_part, 3 * sizeof(unsigned long long) * kSsePartStride));
     HIP_CHECK(hipHostMalloc(&fs_host_, sizeof(FrameState), hipHostMallocDefault));
     host_out_bytes_ = kOutPayloadOffset + buf_.out_bytes + 16;
     HIP_CHECK(hipHostMalloc(&host_out_, host_out_bytes_, hipHostMallocMapped));
@@ -173,7 +174,7 @@ GpuH264Encoder::~GpuH264Encoder() {
     hipFree(buf_.coded_list);
     hipFree(buf_.slice_info);
     hipFree(buf_.out_hdr);
-    hipFree(buf_.sse_mb);
+    hipFree(buf_.sse_part);
     hipHostFree(fs_host_);
     hipHostFree(host_out_);
     hipEventDestroy(done_);
@@ -221,7 +222,7 @@ void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
     f.hp_h = hp_[1] + org;
     f.hp_v = hp_[2] + org;
     f.hp_j = hp_[3] + org;
-    f.sse_mb = buf_.sse_mb;
+    f.sse_part = buf_.sse_part;
     HIP_CHECK(hipEventRecord(start_, stream_));
     HIP_CHECK(hipMemcpyAsync(buf_.fs, fs_host_, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
     enqueue_kernels(idr, src_y, src_uv);

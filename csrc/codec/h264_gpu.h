@@ -62,11 +62,12 @@ struct FrameState {
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
     const uint8_t* hp_v;  // vertical half sample h at (x, y+1/2)
     const uint8_t* hp_j;  // centre half sample j at (x+1/2, y+1/2)
-    // per-MB distortion (Y, U, V) over the display area, [nmb * 3]; written by the
-    // inter/intra kernels, reduced by k_scan into OutHeader (no contended atomics)
-    uint32_t* sse_mb;
+    // distortion partials (Y, U, V) over the display area, [3][kSsePartStride]: one per
+    // inter workgroup / intra MB row, reduced by k_scan into OutHeader (no atomics)
+    unsigned long long* sse_part;
 };
 constexpr int kHpelPad = 48;
+constexpr int kSsePartStride = 65536;  // >= ceil(nmb / 4): 8K is 129600 MBs -> 32400 partials
 
 // Header written at the start of the device output / host output buffer.
 struct OutHeader {
@@ -106,7 +107,7 @@ struct DeviceBuffers {
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
-    uint32_t* sse_mb;         // [nmb * 3] per-MB distortion
+    unsigned long long* sse_part;       // [3 * kSsePartStride] distortion partials
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.

@@ -393,10 +393,17 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         const int sy = wave_sum(sse_y);
         const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
         const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
-        if (valid && lane == 0) {
-            fs->sse_mb[3 * mbi + 0] = (uint32_t)sy;
-            fs->sse_mb[3 * mbi + 1] = (uint32_t)su;
-            fs->sse_mb[3 * mbi + 2] = (uint32_t)sv;
+        __shared__ uint32_t part[3][4];
+        if (lane == 0) {
+            part[0][wave] = valid ? (uint32_t)sy : 0u;
+            part[1][wave] = valid ? (uint32_t)su : 0u;
+            part[2][wave] = valid ? (uint32_t)sv : 0u;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            const int c = threadIdx.x;
+            fs->sse_part[c * kSsePartStride + blockIdx.x] =
+                (unsigned long long)part[c][0] + part[c][1] + part[c][2] + part[c][3];
         }
     }
     const unsigned long long luma_mask = __ballot(valid && lane < 16 && nz > 0);
@@ -434,6 +441,7 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     const int y0 = mby * 16;
 
+    unsigned long long row_sse[3] = {0, 0, 0};
     for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16;
         const bool have_left = mbx > 0;
@@ -577,16 +585,9 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
                 }
             (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
         }
-        {
-            const int sy = wave_sum(sse_y);
-            const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
-            const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
-            if (lane == 0) {
-                fs->sse_mb[3 * mbi + 0] = (uint32_t)sy;
-                fs->sse_mb[3 * mbi + 1] = (uint32_t)su;
-                fs->sse_mb[3 * mbi + 2] = (uint32_t)sv;
-            }
-        }
+        row_sse[0] += (unsigned)wave_sum(sse_y);
+        row_sse[1] += (unsigned)wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
+        row_sse[2] += (unsigned)wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
         if (lane == 0) {
             const int ccbp = (chroma_mask != 0) ? 2 : ((cdc_nz[0] | cdc_nz[1]) ? 1 : 0);
             MbInfo& m = mbs[mbi];
@@ -600,6 +601,7 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
         __syncthreads();
         (void)modes;
     }
+    if (lane < 3) fs->sse_part[lane * kSsePartStride + mby] = row_sse[lane];
 }
 
 // ------------------------------------------------------------------ CAVLC
@@ -843,9 +845,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     }
     // distortion: block-wide reduction of the per-MB partials
     {
+        // partials: one per inter workgroup (4 MBs) or per intra MB row
+        const int nparts = idr ? g.mb_h : (nmb + 3) / 4;
         unsigned long long acc[3] = {0, 0, 0};
-        for (int i = t; i < nmb; i += kScanThreads)
-            for (int c = 0; c < 3; ++c) acc[c] += fs->sse_mb[3 * i + c];
+        for (int i = t; i < nparts; i += kScanThreads)
+            for (int c = 0; c < 3; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
         __shared__ unsigned long long red[3][kScanThreads / 64];
         for (int c = 0; c < 3; ++c) {
             unsigned long long v = acc[c];
