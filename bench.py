@@ -44,6 +44,8 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
+    ap.add_argument("--sessions-per-gpu", type=int, default=1,
+                    help="concurrent sessions per GPU (density): each has its own HIP stream and one frame in flight")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
 
@@ -72,10 +74,24 @@ def main() -> None:
     cfg.enc.search_range = args.search_range
     cfg.enc.subpel = args.subpel
     cfg.noise = args.noise
-    sess = N.Session(cfg)
+    K = max(1, args.sessions_per_gpu)
+    sessions = [N.Session(cfg) for _ in range(K)]
 
-    for _ in range(args.warmup):
-        sess.step(False)
+    def run(n_frames: int, record: bool):
+        """n_frames per session; K sessions interleaved, one frame in flight each."""
+        out = []
+        for s in sessions:
+            s.submit(False)
+        for i in range(n_frames):
+            for s in sessions:
+                r = s.collect()
+                if i + 1 < n_frames:
+                    s.submit(False)
+                if record:
+                    out.append(r)
+        return out
+
+    run(args.warmup, False)
 
     def barrier():
         torch.cuda.synchronize()
@@ -86,15 +102,18 @@ def main() -> None:
     barrier()
     t0 = time.perf_counter()
     lat_ms, sizes, qps, gpu_ms, psnrs = [], [], [], [], []
-    for _ in range(args.steps):
-        r = sess.step(False)
+    if K == 1:
+        results = [sessions[0].step(False) for _ in range(args.steps)]
+    else:
+        results = run(args.steps, True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    for r in results:
         lat_ms.append((r.t_encoded_us - r.t_capture_us) / 1000.0)
         sizes.append(len(r.au))
         qps.append(r.qp)
         psnrs.append(r.psnr_y)
         gpu_ms.append(r.gpu_ms)
-    barrier()
-    elapsed = time.perf_counter() - t0
 
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
@@ -109,7 +128,7 @@ def main() -> None:
     else:
         elapsed_max, all_lat, all_sizes = elapsed, lat_ms, sizes
 
-    total_frames = args.steps * world
+    total_frames = args.steps * world * K
     fps_total = total_frames / elapsed_max
     p50 = statistics.median(all_lat)
     p95 = sorted(all_lat)[int(0.95 * (len(all_lat) - 1))]
@@ -131,6 +150,7 @@ def main() -> None:
             "p50_e2e_latency_ms": round(p50, 3),
             "p95_e2e_latency_ms": round(p95, 3),
             "encoded_fps_per_gpu": round(per_gpu, 2),
+            "sessions_per_gpu": K,
             "sessions_per_node_at_60fps": int(fps_total // 60),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),
@@ -141,9 +161,9 @@ def main() -> None:
             "config": {
                 "model": f"{args.width}x{args.height}@{args.fps} H.264 desktop session (mxh264enc, CBR "
                          f"{args.bitrate_kbps} kbps, ME +/-{args.search_range} qpel={args.subpel})",
-                "global_batch": world,
+                "global_batch": world * K,
                 "seq_len": args.width * args.height,
-                "parallelism": f"session-per-gpu x{world}",
+                "parallelism": f"session-per-gpu x{world}" + (f", {K} sessions/GPU" if K > 1 else ""),
             },
         }
         line = json.dumps(out)
