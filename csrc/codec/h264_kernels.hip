@@ -585,9 +585,9 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
                 }
             (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
         }
-        row_sse[0] += (unsigned)wave_sum(sse_y);
-        row_sse[1] += (unsigned)wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
-        row_sse[2] += (unsigned)wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
+        // per-lane running sums; reduced across the wave once per row
+        row_sse[0] += (unsigned)sse_y;
+        row_sse[(lane >= 20) ? 2 : 1] += (unsigned)sse_c;
         if (lane == 0) {
             const int ccbp = (chroma_mask != 0) ? 2 : ((cdc_nz[0] | cdc_nz[1]) ? 1 : 0);
             MbInfo& m = mbs[mbi];
@@ -601,7 +601,13 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
         __syncthreads();
         (void)modes;
     }
-    if (lane < 3) fs->sse_part[lane * kSsePartStride + mby] = row_sse[lane];
+    unsigned long long tot[3];
+    for (int c = 0; c < 3; ++c) {
+        unsigned long long v = row_sse[c];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        tot[c] = v;
+    }
+    if (lane < 3) fs->sse_part[lane * kSsePartStride + mby] = tot[lane];
 }
 
 // ------------------------------------------------------------------ CAVLC
