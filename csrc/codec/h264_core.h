@@ -187,7 +187,7 @@ MXHD int quant4x4(const int* y, int* z, int qp, bool intra, int start) {
 // when `start` = 1 (it comes from the separate DC path).
 MXHD void dequant4x4(const int* z, int* d, int qp, int start) {
     const int qm = qp % 6, qs = qp / 6;
-    for (int i = start; i < 16; ++i) d[i] = (z[i] * kDequantV[qm][kPosClass[i]]) << qs;
+    for (int i = start; i < 16; ++i) d[i] = z[i] * kDequantV[qm][kPosClass[i]] * (1 << qs);  // multiply: << of negatives is UB
 }
 
 // Intra16x16 luma DC: forward Hadamard of the 16 DCs, /2 with rounding, quantise.
@@ -217,7 +217,7 @@ MXHD void dequant_dc_luma(const int* z, int* dcY, int qp) {
     const int qs = qp / 6;
     for (int i = 0; i < 16; ++i) {
         if (qp >= 36)
-            dcY[i] = (f[i] * ls) << (qs - 6);
+            dcY[i] = f[i] * ls * (1 << (qs - 6));
         else
             dcY[i] = (f[i] * ls + (1 << (5 - qs))) >> (6 - qs);
     }
@@ -247,7 +247,7 @@ MXHD void dequant_dc_chroma(const int* z, int* dcC, int qpc) {
     int a2 = z[2] + z[3], a3 = z[2] - z[3];
     int f[4] = {a0 + a2, a1 + a3, a0 - a2, a1 - a3};
     const int ls = 16 * kDequantV[qpc % 6][0];
-    for (int i = 0; i < 4; ++i) dcC[i] = ((f[i] * ls) << (qpc / 6)) >> 5;
+    for (int i = 0; i < 4; ++i) dcC[i] = (f[i] * ls * (1 << (qpc / 6))) >> 5;
 }
 
 MXHD int chroma_qp(int qp, int offset) {

@@ -21,6 +21,7 @@ void aes_ecb_blocks(EVP_CIPHER_CTX* ctx, const uint8_t* key, const uint8_t* in, 
 
 // AES-CM keystream of n bytes for a 128-bit initial counter block (low 16 bits count).
 void keystream(EVP_CIPHER_CTX* ctx, const uint8_t* key, const uint8_t iv[16], uint8_t* out, size_t n) {
+    if (n == 0) return;
     const size_t nb = (n + 15) / 16;
     std::vector<uint8_t> ctr(nb * 16), ks(nb * 16);
     for (size_t b = 0; b < nb; ++b) {
@@ -90,6 +91,7 @@ std::string SrtpSession::aes_cm_keystream(const std::string& key, const std::str
 
 void SrtpSession::xor_keystream(const uint8_t* key, const uint8_t* salt, uint32_t ssrc, uint64_t index,
                                 uint8_t* data, size_t n) const {
+    if (n == 0) return;
     // IV = (salt * 2^16) XOR (SSRC * 2^64) XOR (index * 2^16)
     uint8_t iv[16] = {0};
     std::memcpy(iv, salt, 14);

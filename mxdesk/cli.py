@@ -1,6 +1,7 @@
 """mxdesk command line (``python -m mxdesk <command>``).
 
 Commands
+  desktop    X server + desktop session, blocks while X runs (reference entrypoint.sh)
   serve      one streaming session on :8080 (the reference's selkies-gstreamer entrypoint,
              selkies-gstreamer-entrypoint.sh:44-47, or noVNC when NOVNC_ENABLE=true)
   launch     one session per visible GPU on ports 8080+i
@@ -121,6 +122,10 @@ def main(argv: list[str] | None = None) -> None:
                                                cfg.video_port, busid, "dummy", cfg.display)), end="")
     elif cmd == "serve":
         cmd_serve(cfg, args)
+    elif cmd == "desktop":
+        from .display.desktop import run_display_session
+
+        sys.exit(run_display_session(cfg))
     elif cmd == "launch":
         from .parallel.launcher import launch_sessions
 

@@ -1,0 +1,119 @@
+// Host-side ASan/UBSan driver for the native code that parses or produces untrusted /
+// variable-length data: CPU H.264 encoder (same MB core as the HIP
+// kernels), SRTP/SRTCP, DTLS-SRTP handshake, RTP H.264 packetizer, Annex-B splitter.
+// Built by tools/sanitize.sh with -fsanitize on the host side only; no GPU is touched.
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../csrc/codec/h264_encoder.h"
+#include "../csrc/net/dtls.h"
+#include "../csrc/net/rtp_h264.h"
+#include "../csrc/net/srtp.h"
+
+using namespace mx;
+
+static int fails = 0;
+#define CHECK(c)                                                  \
+    do {                                                          \
+        if (!(c)) {                                               \
+            std::fprintf(stderr, "CHECK failed: %s (%s:%d)\n", #c, __FILE__, __LINE__); \
+            ++fails;                                              \
+        }                                                         \
+    } while (0)
+
+static void encoder_pass(std::mt19937& rng) {
+    const int sizes[][2] = {{176, 144}, {100, 60}, {64, 48}};
+    for (auto& s : sizes) {
+        for (int subpel = 0; subpel < 2; ++subpel) {
+            h264::EncoderConfig c;
+            c.width = s[0];
+            c.height = s[1];
+            c.bitrate_kbps = 0;
+            c.qp = 10 + (int)(rng() % 36);
+            c.subpel = subpel;
+            c.search_range = 8;
+            h264::CpuH264Encoder enc(c);
+            const int cw = enc.coded_pitch(), ch = (s[1] + 15) / 16 * 16;
+            std::vector<uint8_t> y((size_t)cw * ch), uv((size_t)cw * ch / 2);
+            for (int f = 0; f < 4; ++f) {
+                for (int r = 0; r < ch; ++r)
+                    for (int x = 0; x < cw; ++x)
+                        y[(size_t)r * cw + x] = (uint8_t)((x * 3 + r * 2 + f * 5) ^ ((f & 1) ? (rng() & 31) : 0));
+                for (auto& v : uv) v = (uint8_t)(128 + (int)(rng() % 32) - 16);
+                const auto& au = enc.encode(y.data(), uv.data(), cw, f == 0);
+                CHECK(au.size() > 4);
+                CHECK(au[0] == 0 && au[1] == 0);
+            }
+        }
+    }
+}
+
+static std::string rnd(std::mt19937& rng, size_t n) {
+    std::string s(n, '\0');
+    for (auto& ch : s) ch = (char)(rng() & 0xff);
+    return s;
+}
+
+static void srtp_pass(std::mt19937& rng) {
+    const std::string k = rnd(rng, 16), salt = rnd(rng, 14);
+    net::SrtpSession tx(k, salt), rx(k, salt);
+    for (int i = 0; i < 300; ++i) {
+        std::string pkt = rnd(rng, 12 + rng() % 1200);
+        pkt[0] = (char)0x80;
+        pkt[2] = (char)(i >> 8);
+        pkt[3] = (char)i;
+        const std::string p = tx.protect_rtp(pkt);
+        CHECK(rx.unprotect_rtp(p) == pkt);
+        std::string bad = p;
+        bad[bad.size() / 2] ^= 1;
+        CHECK(rx.unprotect_rtp(bad).empty());
+        CHECK(rx.unprotect_rtp(p.substr(0, rng() % 22)).empty());
+    }
+    for (int i = 0; i < 50; ++i) {
+        std::string r = rnd(rng, 8 + rng() % 100);
+        r[0] = (char)0x81;
+        r[1] = (char)206;
+        CHECK(rx.unprotect_rtcp(tx.protect_rtcp(r)) == r);
+    }
+}
+
+static void rtp_pass(std::mt19937& rng) {
+    for (int i = 0; i < 200; ++i) {
+        std::string au = rnd(rng, rng() % 6000);
+        if (i % 2) au = std::string("\x00\x00\x00\x01\x67", 5) + au + std::string("\x00\x00\x01\x65", 4) + au;
+        net::RtpH264Packetizer pk((uint32_t)rng(), 96, 64 + rng() % 1200, (uint16_t)rng());
+        for (const auto& p : pk.packetize(au, (uint32_t)rng())) CHECK(p.size() >= 12);
+        (void)net::split_annexb(au);
+    }
+}
+
+static void dtls_pass() {
+    net::DtlsEndpoint srv(true), cli(false);
+    auto to_srv = cli.start();
+    for (int round = 0; round < 20 && !(srv.handshake_done() && cli.handshake_done()); ++round) {
+        std::vector<std::string> to_cli;
+        for (const auto& d : to_srv)
+            for (auto& o : srv.feed(d)) to_cli.push_back(o);
+        to_srv.clear();
+        for (const auto& d : to_cli)
+            for (auto& o : cli.feed(d)) to_srv.push_back(o);
+    }
+    CHECK(srv.handshake_done() && cli.handshake_done());
+    CHECK(srv.export_srtp_keys() == cli.export_srtp_keys());
+    net::DtlsEndpoint junk(true);
+    std::mt19937 rng(7);
+    for (int i = 0; i < 50; ++i) (void)junk.feed(rnd(rng, 1 + rng() % 300));
+}
+
+int main() {
+    std::mt19937 rng(12345);
+    encoder_pass(rng);
+    srtp_pass(rng);
+    rtp_pass(rng);
+    dtls_pass();
+    std::printf("sanitize: %s (%d failures)\n", fails ? "FAIL" : "ok", fails);
+    return fails ? 1 : 0;
+}
