@@ -11,6 +11,7 @@
 #include "../codec/h264_core.h"
 #include "../codec/h264_encoder.h"
 #include "../common/hip_check.h"
+#include "../common/trace.h"
 #include "../kernels/pixel.h"
 #include "../runtime/session.h"
 
@@ -222,6 +223,10 @@ PYBIND11_MODULE(_native, m) {
         .def_property_readonly("stats", &h264::GpuH264Encoder::last_stats);
 
     // ---------------------------------------------------------------- pixel kernels
+    // roctx ranges from Python (packetize / send stages of the streaming pipeline)
+    m.def("trace_push", [](const std::string& name) { roctxRangePushA(name.c_str()); });
+    m.def("trace_pop", []() { roctxRangePop(); });
+    m.def("trace_mark", [](const std::string& name) { roctxMarkA(name.c_str()); });
     m.def(
         "synth",
         [](uintptr_t out, int w, int h, int pitch, uint32_t frame_id, uint32_t ts, float t, int noise, int ox, int oy,

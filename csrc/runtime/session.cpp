@@ -6,6 +6,7 @@
 #include <stdexcept>
 
 #include "../common/hip_check.h"
+#include "../common/trace.h"
 
 namespace mx {
 
@@ -121,6 +122,7 @@ Session::~Session() {
 }
 
 void Session::convert_and_encode(int slot, bool force_idr) {
+    TraceRange tr("mxdesk.convert+encode.enqueue");
     const h264::Geometry& g = enc_->geometry();
     if (scale_) {
         pix::launch_scale_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, lt_, nv12_y_, nv12_uv_,
@@ -136,6 +138,7 @@ void Session::convert_and_encode(int slot, bool force_idr) {
 
 void Session::submit_synthetic(bool force_idr) {
     if (pending_) throw std::logic_error("Session: collect() before the next submit");
+    TraceRange tr("mxdesk.submit_synthetic");
     const int slot = pool_->acquire();
     t_capture_ = now_us();
     pix::SynthParams p;
@@ -160,6 +163,7 @@ void Session::submit_synthetic(bool force_idr) {
 
 void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
     if (pending_) throw std::logic_error("Session: collect() before the next submit");
+    TraceRange tr("mxdesk.submit_bgrx(upload)");
     const int slot = pool_->acquire();
     t_capture_ = now_us();
     const int row = cfg_.width * 4;
@@ -175,6 +179,7 @@ FrameResult Session::collect() {
     if (!pending_) throw std::logic_error("Session: nothing submitted");
     pending_ = false;
     FrameResult r;
+    TraceRange tr("mxdesk.collect(wait+annexb)");
     const std::vector<uint8_t>& au = enc_->collect();
     r.t_encoded_us = now_us();
     r.au = au;

@@ -100,7 +100,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     newest = max(o.stat().st_mtime for o in objs)
     if force or not TARGET.exists() or TARGET.stat().st_mtime < newest:
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(TARGET),
-               "-ldrm_amdgpu", "-ldrm", "-lssl", "-lcrypto", "-lz"]
+               "-ldrm_amdgpu", "-ldrm", "-lssl", "-lcrypto", "-lz", "-lrocprofiler-sdk-roctx"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {shlex.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -26,6 +26,7 @@ import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
 
+from ..utils.tracing import trace
 from . import rtp as R
 from . import stun as S
 
@@ -297,13 +298,14 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             if self.ts0 is None:
                 self.ts0 = fr.t_capture_us
             ts = ((fr.t_capture_us - self.ts0) * 9 // 100) & 0xFFFFFFFF  # 90 kHz
-            for raw in self.pkt.packetize(fr.au, ts):
-                seq = struct.unpack_from("!H", raw, 2)[0]
-                self.history[seq] = raw
-                if len(self.history) > self.HISTORY:
-                    self.history.popitem(last=False)
-                self.transport.sendto(self.srtp_tx.protect_rtp(raw), self.remote)
-                self.stats["rtp_out"] += 1
+            with trace("mxdesk.webrtc.packetize+srtp+send"):
+                for raw in self.pkt.packetize(fr.au, ts):
+                    seq = struct.unpack_from("!H", raw, 2)[0]
+                    self.history[seq] = raw
+                    if len(self.history) > self.HISTORY:
+                        self.history.popitem(last=False)
+                    self.transport.sendto(self.srtp_tx.protect_rtp(raw), self.remote)
+                    self.stats["rtp_out"] += 1
             self.last_ts = ts
 
     async def _timers(self) -> None:
