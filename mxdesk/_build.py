@@ -104,7 +104,23 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {shlex.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    build_interposer(force)
     return TARGET
+
+
+INTERPOSER_SRC = CSRC / "interposer" / "js_interposer.c"
+INTERPOSER = ROOT / "mxdesk" / "libmxjs_interposer.so"
+
+
+def build_interposer(force: bool = False) -> Path:
+    """Host-only LD_PRELOAD library (plain C, no HIP): the joystick interposer (C60)."""
+    if force or not INTERPOSER.exists() or INTERPOSER.stat().st_mtime < INTERPOSER_SRC.stat().st_mtime:
+        cc = os.environ.get("CC", "gcc")
+        cmd = [cc, "-O2", "-fPIC", "-shared", "-Wall", "-o", str(INTERPOSER), str(INTERPOSER_SRC), "-ldl", "-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"interposer build failed: {shlex.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return INTERPOSER
 
 
 def main() -> None:

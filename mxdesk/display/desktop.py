@@ -74,6 +74,23 @@ def preflight(runtime_dir: str | None = None) -> str:
     return rd
 
 
+def joystick_placeholders(dev_input: str = "/dev/input", n: int = 4) -> list[str]:
+    """Create empty /dev/input/js0..3 so apps that scan the directory find joysticks; the
+    interposer redirects the actual open() (reference selkies-gstreamer-entrypoint.sh:15).
+    Best effort: needs write access to /dev/input (root or a 1777 dir)."""
+    made = []
+    try:
+        Path(dev_input).mkdir(parents=True, exist_ok=True)
+        for i in range(n):
+            p = Path(dev_input) / f"js{i}"
+            if not p.exists():
+                p.touch()
+                made.append(str(p))
+    except OSError as e:
+        log.info("joystick placeholders not created (%s)", e)
+    return made
+
+
 def desktop_command(env: dict | None = None) -> list[str]:
     env = os.environ if env is None else env
     cmd = env.get("MXDESK_DESKTOP_CMD")
@@ -92,6 +109,7 @@ def run_display_session(cfg, conf_dir: str = "/tmp/mxdesk-x") -> int:
     from ..utils import devices as D
 
     preflight()
+    joystick_placeholders()
     removed = clean_stale_locks(cfg.display)
     if removed:
         log.info("removed stale X files: %s", removed)

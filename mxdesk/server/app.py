@@ -59,7 +59,10 @@ class MediaServer:
         self.start_pipeline = start_pipeline
         self.clients: set[web.WebSocketResponse] = set()
         self.resize_enabled = bool(getattr(cfg, "enable_resize", False))
+        from .gamepad import GamepadServer
         from .webrtc import WhepEndpoint
+
+        self.gamepad = GamepadServer(getattr(cfg, "js_dir", None)) if bool(getattr(cfg, "enable_gamepad", True)) else None
 
         self.whep = WhepEndpoint(pipeline, host=getattr(cfg, "webrtc_host", None) or None,
                                  udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0))
@@ -92,11 +95,19 @@ class MediaServer:
         return app
 
     async def _on_startup(self, app):
+        if self.gamepad is not None:
+            try:
+                await self.gamepad.start()
+            except OSError as e:  # e.g. read-only /tmp: gamepads are optional
+                log.warning("gamepad sockets unavailable: %s", e)
+                self.gamepad = None
         if self.start_pipeline:
             self.pipeline.start()
 
     async def _on_cleanup(self, app):
         self.whep.close_all()
+        if self.gamepad is not None:
+            await self.gamepad.stop()
         self.pipeline.stop()
         for ws in list(self.clients):
             await ws.close()
@@ -190,6 +201,9 @@ class MediaServer:
             lat = ev.extra.get("latency_ms")
             if lat is not None:
                 p.metrics.on_client_latency(float(lat))
+        elif ev.kind == "gamepad":
+            if self.gamepad is not None:
+                self.gamepad.apply(ev)
         elif ev.kind == "resize":
             if self.resize_enabled:
                 log.info("client resize request %dx%d (applied on next session restart)", ev.width, ev.height)

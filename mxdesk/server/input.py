@@ -2,8 +2,8 @@
 
 Accepts both mxdesk JSON messages (``{"type": "mouse", ...}``) and the selkies data-channel
 text protocol [UP] (``m,x,y,mask,scroll`` / ``m2,dx,dy,mask,scroll`` / ``kd,keysym`` /
-``ku,keysym`` / ``kr`` / ``cw,<base64>`` / ``r,WxH`` / ``vb,kbps`` / ``_f,fps``) and turns
-them into injector calls.
+``ku,keysym`` / ``kr`` / ``cw,<base64>`` / ``r,WxH`` / ``vb,kbps`` / ``_f,fps`` /
+``js,c|d|b|a,...`` gamepads) and turns them into injector / gamepad-server calls.
 
 Injectors:
   * ``SyntheticInjector`` drives the synthetic desktop (remote cursor position; keys and
@@ -88,6 +88,19 @@ def parse_message(msg: str) -> InputEvent | None:
             return InputEvent("fps", value=float(parts[1]))
         if op == "pli":
             return InputEvent("pli")
+        if op == "js":
+            sub, idx = parts[1], int(parts[2])
+            if sub == "c":
+                name = base64.b64decode(parts[3]).decode("utf-8", "replace") if len(parts) > 3 else ""
+                return InputEvent("gamepad", extra={"op": "c", "idx": idx, "name": name,
+                                                    "axes": int(parts[4]) if len(parts) > 4 else 4,
+                                                    "buttons": int(parts[5]) if len(parts) > 5 else 17})
+            if sub == "d":
+                return InputEvent("gamepad", extra={"op": "d", "idx": idx})
+            if sub in ("b", "a"):
+                return InputEvent("gamepad", extra={"op": sub, "idx": idx, "num": int(parts[3]),
+                                                    "value": float(parts[4])})
+            return None
     except (IndexError, ValueError) as e:
         log.debug("bad input message %r: %s", msg, e)
         return None

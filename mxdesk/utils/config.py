@@ -133,6 +133,9 @@ SCHEMA: list[Var] = [
     Var("noise", ["MXDESK_NOISE"], True, bool, "synthetic desktop: animated-noise panel"),
     Var("wall", ["MXDESK_WALL"], "", str, "tiled wall layout, e.g. '2x2' (one tile per GPU)"),
     Var("sessions", ["MXDESK_SESSIONS"], 0, int, "sessions to launch (0 = one per visible GPU)"),
+    Var("enable_gamepad", ["MXDESK_GAMEPAD", "SELKIES_ENABLE_GAMEPAD"], True, bool,
+        "browser gamepads -> /dev/input/jsN via the LD_PRELOAD interposer", ref="Dockerfile:473-476"),
+    Var("js_dir", ["MXDESK_JS_DIR"], "/tmp", str, "directory of the joystick interposer sockets"),
     Var("webrtc_host", ["MXDESK_WEBRTC_HOST"], "", str, "address advertised in the WebRTC host candidate"),
     Var("webrtc_udp_port", ["MXDESK_WEBRTC_UDP_PORT"], 0, int, "UDP port for WebRTC media (0 = ephemeral)"),
     Var("log_dir", ["MXDESK_LOG_DIR"], "/tmp", str, "log directory", ref="supervisord.conf:9"),

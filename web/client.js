@@ -86,6 +86,28 @@ const mxdesk = (() => {
     window.addEventListener("resize", () => {
       if (cfg && cfg.resize) sendQ(`r,${window.innerWidth}x${window.innerHeight}`);
     });
+    gamepads();
+  }
+
+  // Gamepad API -> selkies-style js,* messages -> /dev/input/jsN in the desktop (interposer)
+  function gamepads() {
+    const last = {};
+    window.addEventListener("gamepadconnected", (e) => {
+      const g = e.gamepad;
+      sendQ(`js,c,${g.index},${btoa(unescape(encodeURIComponent(g.id)))},${g.axes.length},${g.buttons.length}`);
+      last[g.index] = { b: g.buttons.map(() => 0), a: g.axes.map(() => 0) };
+    });
+    window.addEventListener("gamepaddisconnected", (e) => { sendQ(`js,d,${e.gamepad.index}`); delete last[e.gamepad.index]; });
+    const poll = () => {
+      for (const g of navigator.getGamepads ? navigator.getGamepads() : []) {
+        if (!g || !last[g.index]) continue;
+        const s = last[g.index];
+        g.buttons.forEach((b, i) => { if (b.value !== s.b[i]) { s.b[i] = b.value; sendQ(`js,b,${g.index},${i},${b.value}`); } });
+        g.axes.forEach((v, i) => { const q = Math.round(v * 100) / 100; if (q !== s.a[i]) { s.a[i] = q; sendQ(`js,a,${g.index},${i},${q}`); } });
+      }
+      requestAnimationFrame(poll);
+    };
+    requestAnimationFrame(poll);
   }
 
   async function whep(video) {
