@@ -64,7 +64,17 @@ class MediaServer:
 
         self.gamepad = GamepadServer(getattr(cfg, "js_dir", None)) if bool(getattr(cfg, "enable_gamepad", True)) else None
 
-        self.whep = WhepEndpoint(pipeline, host=getattr(cfg, "webrtc_host", None) or None,
+        self.audio = None
+        if bool(getattr(cfg, "enable_audio", False)):
+            from ..audio import AudioPipeline, make_source
+
+            try:
+                src = make_source(getattr(cfg, "audio_source", "auto"))
+            except (OSError, ValueError) as e:
+                log.warning("audio disabled: %s", e)
+                src = None
+            self.audio = AudioPipeline(src) if src is not None else None
+        self.whep = WhepEndpoint(pipeline, audio=self.audio, host=getattr(cfg, "webrtc_host", None) or None,
                                  udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0))
 
     # ------------------------------------------------------------------ app
@@ -103,9 +113,13 @@ class MediaServer:
                 self.gamepad = None
         if self.start_pipeline:
             self.pipeline.start()
+        if self.audio is not None:
+            self.audio.start()
 
     async def _on_cleanup(self, app):
         self.whep.close_all()
+        if self.audio is not None:
+            self.audio.stop()
         if self.gamepad is not None:
             await self.gamepad.stop()
         self.pipeline.stop()
@@ -155,15 +169,21 @@ class MediaServer:
         ws = web.WebSocketResponse(heartbeat=10, max_msg_size=64 * 1024 * 1024)
         await ws.prepare(request)
         p = self.pipeline
+        # ?media=0: control/input channel only (the WebRTC client receives media over SRTP)
+        media = request.query.get("media", "1") != "0"
+        want_audio = media and self.audio is not None and request.query.get("audio", "1") != "0"
+        from ..audio.pipeline import CHANNELS, RATE
+
         await ws.send_str(json.dumps({
             "type": "config", "codec": h264_codec_string(p.out_w, p.out_h, p.fps), "width": p.out_w,
             "height": p.out_h, "fps": p.fps, "resize": self.resize_enabled,
+            "audio": {"codec": "pcm_s16le", "rate": RATE, "channels": CHANNELS} if want_audio else None,
         }))
-        # ?media=0: control/input channel only (the WebRTC client receives video over SRTP)
-        media = request.query.get("media", "1") != "0"
         sub = p.subscribe(asyncio.get_running_loop()) if media else None
         self.clients.add(ws)
         sender = asyncio.create_task(self._send_loop(ws, sub)) if media else None
+        asub = self.audio.subscribe(asyncio.get_running_loop()) if want_audio else None
+        asender = asyncio.create_task(self._audio_loop(ws, asub)) if want_audio else None
         try:
             async for msg in ws:
                 if msg.type == WSMsgType.TEXT:
@@ -174,6 +194,9 @@ class MediaServer:
             if sender is not None:
                 sender.cancel()
                 p.unsubscribe(sub)
+            if asender is not None:
+                asender.cancel()
+                self.audio.unsubscribe(asub)
             self.clients.discard(ws)
         return ws
 
@@ -184,6 +207,16 @@ class MediaServer:
             fr = await sub.queue.get()
             try:
                 await ws.send_bytes(frame_header(fr, native().now_us()) + fr.au)
+            except (ConnectionResetError, RuntimeError):
+                return
+
+    async def _audio_loop(self, ws: web.WebSocketResponse, sub) -> None:
+        from ..audio.pipeline import audio_message
+
+        while not ws.closed:
+            ch = await sub.queue.get()
+            try:
+                await ws.send_bytes(audio_message(ch))
             except (ConnectionResetError, RuntimeError):
                 return
 

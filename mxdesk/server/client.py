@@ -16,6 +16,7 @@ from dataclasses import dataclass, field
 
 import aiohttp
 
+from ..audio.pipeline import parse_audio_message
 from ..pipeline.stream import parse_frame
 
 
@@ -25,6 +26,7 @@ class ViewerResult:
     frames: list[dict] = field(default_factory=list)
     latency_ms: list[float] = field(default_factory=list)
     stream: bytes = b""
+    audio: list[dict] = field(default_factory=list)  # parsed MXA1 chunks (PCM)
 
     @property
     def p50_ms(self) -> float:
@@ -50,6 +52,9 @@ async def view(url: str, nframes: int, user: str | None = None, password: str | 
                         res.config = d
                 elif msg.type == aiohttp.WSMsgType.BINARY:
                     t_recv = time.monotonic() * 1e6
+                    if msg.data[:4] == b"MXA1":
+                        res.audio.append(parse_audio_message(msg.data))
+                        continue
                     fr = parse_frame(msg.data)
                     lat = (t_recv - fr["t_capture_us"]) / 1000.0
                     res.latency_ms.append(lat)

@@ -114,50 +114,59 @@ class Answer:
     remote_ufrag: str
     remote_pwd: str
     remote_fingerprint: str
+    audio_pt: int | None = None  # PCMU (0) when the offer has an audio section and audio is on
+    audio_mid: str | None = None
+
+
+def _has_pcmu(md: MediaDesc) -> bool:
+    return "0" in md.fmts or any(re.search(r"\sPCMU/8000", r, re.I) for r in md.attrs_named("rtpmap"))
 
 
 def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
-                 level_idc: int = 0x2A) -> Answer:
+                 level_idc: int = 0x2A, audio_ssrc: int | None = None) -> Answer:
+    """Answer one H.264 video section (and, with ``audio_ssrc``, one PCMU audio section);
+    everything else is rejected with port 0.  All accepted sections are BUNDLEd onto the
+    single ICE-lite host candidate."""
     offer = parse_sdp(offer_text)
     lines = ["v=0", f"o=mxdesk {secrets.randbelow(1 << 62)} 2 IN IP4 {host}", "s=mxdesk", "t=0 0", "a=ice-lite",
              "a=msid-semantic: WMS mxdesk"]
     out_media: list[str] = []
     chosen = None
+    audio = None  # (pt, mid)
+    bundle: list[str] = []
+    transport = [f"c=IN IP4 {host}", f"a=candidate:1 1 udp 2130706431 {host} {port} typ host", "a=end-of-candidates",
+                 f"a=ice-ufrag:{ice_ufrag}", f"a=ice-pwd:{ice_pwd}", f"a=fingerprint:{fingerprint}", "a=setup:passive"]
     for md in offer.media:
-        mid = md.attr("mid") or str(len(out_media))
+        mid = md.attr("mid") or str(len(bundle) + len(out_media))
         pt = pick_h264(md) if (md.kind == "video" and chosen is None) else None
         ufrag = md.attr("ice-ufrag") or offer.attr("ice-ufrag")
         pwd = md.attr("ice-pwd") or offer.attr("ice-pwd")
         fp = md.attr("fingerprint") or offer.attr("fingerprint")
-        if pt is None:  # reject (audio, data channels, second video)
-            out_media += [f"m={md.kind} 0 {md.proto} {md.fmts[0] if md.fmts else '0'}", "c=IN IP4 0.0.0.0",
-                          f"a=mid:{mid}", "a=inactive"]
+        if pt is not None:
+            chosen = Answer("", int(pt), mid, ufrag or "", pwd or "", fp or "")
+            bundle.append(mid)
+            out_media += [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport,
+                          f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtcp-rsize",
+                          f"a=rtpmap:{pt} H264/90000", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
+                          f"a=rtcp-fb:{pt} ccm fir",
+                          f"a=fmtp:{pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}",
+                          f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
             continue
-        chosen = Answer("", int(pt), mid, ufrag or "", pwd or "", fp or "")
-        out_media += [
-            f"m=video {port} UDP/TLS/RTP/SAVPF {pt}",
-            f"c=IN IP4 {host}",
-            f"a=candidate:1 1 udp 2130706431 {host} {port} typ host",
-            "a=end-of-candidates",
-            f"a=ice-ufrag:{ice_ufrag}",
-            f"a=ice-pwd:{ice_pwd}",
-            f"a=fingerprint:{fingerprint}",
-            "a=setup:passive",
-            f"a=mid:{mid}",
-            "a=sendonly",
-            "a=rtcp-mux",
-            "a=rtcp-rsize",
-            f"a=rtpmap:{pt} H264/90000",
-            f"a=rtcp-fb:{pt} nack",
-            f"a=rtcp-fb:{pt} nack pli",
-            f"a=rtcp-fb:{pt} ccm fir",
-            f"a=fmtp:{pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}",
-            f"a=ssrc:{ssrc} cname:mxdesk",
-            f"a=ssrc:{ssrc} msid:mxdesk video0",
-        ]
+        if md.kind == "audio" and audio is None and audio_ssrc is not None and _has_pcmu(md):
+            audio = (0, mid)
+            bundle.append(mid)
+            out_media += [f"m=audio {port} UDP/TLS/RTP/SAVPF 0", *transport,
+                          f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtpmap:0 PCMU/8000",
+                          f"a=ssrc:{audio_ssrc} cname:mxdesk", f"a=ssrc:{audio_ssrc} msid:mxdesk audio0"]
+            continue
+        # reject (data channels, second video, audio when disabled)
+        out_media += [f"m={md.kind} 0 {md.proto} {md.fmts[0] if md.fmts else '0'}", "c=IN IP4 0.0.0.0",
+                      f"a=mid:{mid}", "a=inactive"]
     if chosen is None:
         raise ValueError("offer has no H.264 (packetization-mode=1, baseline-compatible) video section")
-    lines.insert(4, f"a=group:BUNDLE {chosen.mid}")
+    if audio is not None:
+        chosen.audio_pt, chosen.audio_mid = audio
+    lines.insert(4, "a=group:BUNDLE " + " ".join(bundle))
     chosen.sdp = "\r\n".join(lines + out_media) + "\r\n"
     return chosen
 
@@ -180,9 +189,14 @@ def local_ip() -> str:
 class WebRtcPeer(asyncio.DatagramProtocol):
     HISTORY = 1024
 
-    def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A):
+    def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
+                 audio=None):
         N = _native()
         self.pipeline = pipeline
+        self.audio = audio
+        self.audio_ssrc = (secrets.randbits(32) | 1) if audio is not None else None
+        self.srtp_tx_audio = None
+        self.asub = None
         self.id = secrets.token_hex(8)
         self.ufrag = secrets.token_hex(4)
         self.pwd = secrets.token_hex(16)
@@ -211,7 +225,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.transport, _ = await loop.create_datagram_endpoint(lambda: self, local_addr=(self.host, self.bind_port))
         port = self.transport.get_extra_info("sockname")[1]
         self.answer = build_answer(self.offer_sdp, self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port,
-                                   self.ssrc, self.level_idc)
+                                   self.ssrc, self.level_idc, self.audio_ssrc)
         self.pkt = _native().net.RtpH264Packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
         self.tasks.append(asyncio.create_task(self._timers()))
         return self.answer.sdp
@@ -269,6 +283,11 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         log.info("WebRTC peer %s: DTLS-SRTP up (%s)", self.id, self.dtls.srtp_profile)
         self.sub = self.pipeline.subscribe(asyncio.get_running_loop())
         self.tasks.append(asyncio.create_task(self._send_loop()))
+        if self.answer.audio_pt is not None and self.audio is not None:
+            # separate SRTP context per SSRC (own rollover counter / SRTCP index), same keys
+            self.srtp_tx_audio = N.net.SrtpSession(sk, ss)
+            self.asub = self.audio.subscribe(asyncio.get_running_loop())
+            self.tasks.append(asyncio.create_task(self._audio_loop()))
 
     def _on_rtcp(self, data: bytes) -> None:
         if self.srtp_rx is None:
@@ -308,6 +327,32 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                     self.stats["rtp_out"] += 1
             self.last_ts = ts
 
+    async def _audio_loop(self) -> None:
+        """48 kHz stereo chunks -> 8 kHz mono (native FIR decimator) -> 20 ms PCMU packets."""
+        import numpy as np
+
+        A = _native().audio
+        dec = A.Decimator(6, 2)
+        pending = np.zeros(0, np.int16)
+        seq = secrets.randbits(16)
+        ts = secrets.randbits(32)
+        first = True
+        self.audio_packets = 0
+        while not self.closed.is_set():
+            ch = await self.asub.queue.get()
+            pending = np.concatenate([pending, dec.process(ch.pcm)])
+            while len(pending) >= 160 and self.remote is not None:
+                frame, pending = pending[:160], pending[160:]
+                hdr = struct.pack("!BBHII", 0x80, (0x80 if first else 0) | self.answer.audio_pt, seq, ts,
+                                  self.audio_ssrc)
+                self.transport.sendto(self.srtp_tx_audio.protect_rtp(hdr + A.encode_ulaw(frame)), self.remote)
+                first = False
+                seq = (seq + 1) & 0xFFFF
+                ts = (ts + 160) & 0xFFFFFFFF
+                self.audio_packets += 1
+                self.audio_octets = getattr(self, "audio_octets", 0) + 160
+                self.audio_ts = ts
+
     async def _timers(self) -> None:
         last_sr = 0.0
         while not self.closed.is_set():
@@ -318,6 +363,9 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             if self.srtp_tx is not None and self.remote is not None and now - last_sr > 1.0:
                 sr = R.build_sr(self.ssrc, getattr(self, "last_ts", 0), self.pkt.packets, self.pkt.octets)
                 self.transport.sendto(self.srtp_tx.protect_rtcp(sr), self.remote)
+                if self.srtp_tx_audio is not None and getattr(self, "audio_packets", 0):
+                    asr = R.build_sr(self.audio_ssrc, self.audio_ts, self.audio_packets, self.audio_octets)
+                    self.transport.sendto(self.srtp_tx_audio.protect_rtcp(asr), self.remote)
                 last_sr = now
             if now - self.last_consent > 30.0:  # consent freshness (RFC 7675)
                 log.info("WebRTC peer %s: consent expired", self.id)
@@ -329,6 +377,8 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.closed.set()
         if self.sub is not None:
             self.pipeline.unsubscribe(self.sub)
+        if self.asub is not None:
+            self.audio.unsubscribe(self.asub)
         for t in self.tasks:
             t.cancel()
         if self.transport is not None:
@@ -338,8 +388,9 @@ class WebRtcPeer(asyncio.DatagramProtocol):
 class WhepEndpoint:
     """``POST /whep`` (application/sdp offer) -> 201 answer; ``DELETE /whep/{id}``."""
 
-    def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A):
+    def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A, audio=None):
         self.pipeline = pipeline
+        self.audio = audio
         self.host = host
         self.udp_port = udp_port
         self.level_idc = level_idc
@@ -353,7 +404,7 @@ class WhepEndpoint:
         from aiohttp import web
 
         offer = await request.text()
-        peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc)
+        peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc, audio=self.audio)
         try:
             answer = await peer.start()
         except ValueError as e:

@@ -27,9 +27,9 @@ def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_
              "a=msid-semantic: WMS"]
     media = []
     if with_audio:
-        media += ["m=audio 9 UDP/TLS/RTP/SAVPF 111", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}", f"a=ice-pwd:{pwd}",
-                  f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:1", "a=recvonly", "a=rtcp-mux",
-                  "a=rtpmap:111 opus/48000/2"]
+        media += ["m=audio 9 UDP/TLS/RTP/SAVPF 111 0", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
+                  f"a=ice-pwd:{pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:1", "a=recvonly",
+                  "a=rtcp-mux", "a=rtpmap:111 opus/48000/2", "a=rtpmap:0 PCMU/8000"]
     media = ["m=video 9 UDP/TLS/RTP/SAVPF 96 %d 108" % h264_pt, "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
              f"a=ice-pwd:{pwd}", "a=ice-options:trickle", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:0",
              "a=recvonly", "a=rtcp-mux", "a=rtcp-rsize", "a=rtpmap:96 VP8/90000",
@@ -50,6 +50,8 @@ class WhepResult:
     answer: str = ""
     connect_ms: float = 0.0
     stream: bytes = b""
+    audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
+    audio_seqs: list[int] = field(default_factory=list)
 
 
 class _Client(asyncio.DatagramProtocol):
@@ -126,7 +128,13 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
         if dtls.peer_fingerprint.lower() != r_fp.lower():
             raise RuntimeError("server fingerprint mismatch")
         km = dtls.export_srtp_keys()
-        rx = N.net.SrtpSession(km[16:32], km[46:60])  # server -> client
+        rx_ctx: dict[int, object] = {}  # one SRTP receive context per SSRC (own rollover counter)
+
+        def rx_for(pkt: bytes):
+            ssrc = struct.unpack_from("!I", pkt, 4 if 192 <= pkt[1] <= 223 else 8)[0]
+            if ssrc not in rx_ctx:
+                rx_ctx[ssrc] = N.net.SrtpSession(km[16:32], km[46:60])  # server -> client
+            return rx_ctx[ssrc]
         tx = N.net.SrtpSession(km[0:16], km[32:46])   # client -> server (RTCP)
         res.connect_ms = (time.monotonic() - t0) * 1000
         my_ssrc = secrets.randbits(32)
@@ -142,15 +150,19 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
             if not 128 <= d[0] <= 191:
                 continue
             if 192 <= d[1] <= 223:
-                p = rx.unprotect_rtcp(d)
+                p = rx_for(d).unprotect_rtcp(d)
                 if p and any(x["pt"] == 200 for x in R.parse_rtcp(p)):
                     res.srs += 1
                 continue
-            p = rx.unprotect_rtp(d)
+            p = rx_for(d).unprotect_rtp(d)
             if not p:
                 raise RuntimeError("SRTP authentication failed")
-            res.packets += 1
             h = R.rtp_header(p)
+            if h["pt"] == 0:  # PCMU audio
+                res.audio_payloads.append(h["payload"])
+                res.audio_seqs.append(h["seq"])
+                continue
+            res.packets += 1
             media_ssrc = h["ssrc"]
             seq = h["seq"]
             if next_seq is None:

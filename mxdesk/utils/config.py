@@ -116,7 +116,8 @@ SCHEMA: list[Var] = [
     Var("video_bitrate", ["SELKIES_VIDEO_BITRATE", "WEBRTC_VIDEO_BITRATE"], 8000, int, "video bitrate (kbps)"),
     Var("keyframe_distance", ["SELKIES_KEYFRAME_DISTANCE"], -1.0, float, "seconds between IDRs (-1 = on demand)"),
     Var("congestion_control", ["SELKIES_CONGESTION_CONTROL"], False, bool, "adapt bitrate to the client"),
-    Var("enable_audio", ["SELKIES_ENABLE_AUDIO"], True, bool, "audio (not available: no PulseAudio/Opus yet)"),
+    Var("enable_audio", ["SELKIES_ENABLE_AUDIO"], True, bool, "desktop audio (PCM over WebSocket, PCMU over WebRTC)"),
+    Var("audio_source", ["MXDESK_AUDIO_SOURCE"], "auto", str, "audio capture: auto | pulse | synthetic | fifo:PATH | none"),
     Var("audio_bitrate", ["SELKIES_AUDIO_BITRATE"], 128000, int, "audio bitrate (bps)"),
     Var("enable_clipboard", ["SELKIES_ENABLE_CLIPBOARD"], True, bool, "clipboard sync"),
     Var("enable_cursors", ["SELKIES_ENABLE_CURSORS"], True, bool, "remote cursor forwarding"),

@@ -56,7 +56,36 @@ const mxdesk = (() => {
     }
   }
 
+  // ---- desktop audio over the WebSocket: "MXA1" chunks of s16le PCM, scheduled on an
+  // AudioContext with a ~60 ms jitter buffer (browsers need a user gesture to start audio)
+  let actx = null, playAt = 0;
+  const unlockAudio = () => {
+    if (!actx && window.AudioContext) actx = new AudioContext({ sampleRate: 48000, latencyHint: "interactive" });
+    if (actx && actx.state === "suspended") actx.resume();
+  };
+  function onAudio(buf) {
+    if (!actx || actx.state !== "running") return;
+    const dv = new DataView(buf);
+    const ch = dv.getUint8(5), rate = dv.getUint16(6, true) * 100, n = dv.getUint32(20, true);
+    const pcm = new Int16Array(buf, 24, n / 2);
+    const frames = pcm.length / ch;
+    const ab = actx.createBuffer(ch, frames, rate);
+    for (let c = 0; c < ch; c++) {
+      const d = ab.getChannelData(c);
+      for (let i = 0; i < frames; i++) d[i] = pcm[i * ch + c] / 32768;
+    }
+    const src = actx.createBufferSource();
+    src.buffer = ab;
+    src.connect(actx.destination);
+    const now = actx.currentTime;
+    if (playAt < now + 0.02 || playAt > now + 0.25) playAt = now + 0.06;
+    src.start(playAt);
+    playAt += frames / rate;
+  }
+
   function input() {
+    canvas.addEventListener("mousedown", unlockAudio);
+    window.addEventListener("keydown", unlockAudio);
     const pos = (e) => {
       const r = canvas.getBoundingClientRect();
       const sx = canvas.width / r.width, sy = canvas.height / r.height;
@@ -113,7 +142,18 @@ const mxdesk = (() => {
   async function whep(video) {
     const pc = new RTCPeerConnection({ iceServers: [] });
     pc.addTransceiver("video", { direction: "recvonly" });
-    pc.ontrack = (ev) => { video.srcObject = ev.streams[0] || new MediaStream([ev.track]); video.play().catch(() => {}); };
+    pc.addTransceiver("audio", { direction: "recvonly" });
+    const audioEl = new Audio();
+    pc.ontrack = (ev) => {
+      if (ev.track.kind === "audio") {
+        audioEl.srcObject = new MediaStream([ev.track]);
+        const go = () => audioEl.play().catch(() => {});
+        go(); window.addEventListener("mousedown", go, { once: true });
+        return;
+      }
+      video.srcObject = new MediaStream([ev.track]);
+      video.play().catch(() => {});
+    };
     pc.onconnectionstatechange = () => {
       msgEl.textContent = pc.connectionState === "connected" ? "" : "webrtc: " + pc.connectionState;
       if (pc.connectionState === "failed") { pc.close(); setTimeout(() => whep(video), 1000); }
@@ -145,6 +185,7 @@ const mxdesk = (() => {
         if (m.type === "config") { cfg = m; waitingKey = true; makeDecoder(); msgEl.textContent = ""; }
         return;
       }
+      if (new Uint8Array(ev.data, 0, 4).every((b, i) => b === "MXA1".charCodeAt(i))) { onAudio(ev.data); return; }
       if (cfg) onFrame(ev.data);
     };
     ws.onclose = () => { msgEl.textContent = "disconnected - retrying"; setTimeout(() => connect(media), 1000); };
