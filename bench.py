@@ -44,6 +44,7 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
+    ap.add_argument("--graph", type=int, default=1, help="replay the per-frame chain as a hipGraph")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
                     help="concurrent sessions per GPU (density): each has its own HIP stream and one frame in flight")
     ap.add_argument("--json-out", type=str, default="")
@@ -74,6 +75,7 @@ def main() -> None:
     cfg.enc.search_range = args.search_range
     cfg.enc.subpel = args.subpel
     cfg.noise = args.noise
+    cfg.use_graph = args.graph
     K = max(1, args.sessions_per_gpu)
     sessions = [N.Session(cfg) for _ in range(K)]
 
@@ -151,6 +153,7 @@ def main() -> None:
             "p95_e2e_latency_ms": round(p95, 3),
             "encoded_fps_per_gpu": round(per_gpu, 2),
             "sessions_per_gpu": K,
+            "hip_graph": bool(args.graph),
             "sessions_per_node_at_60fps": int(fps_total // 60),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),

@@ -313,6 +313,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("fps", &SessionConfig::fps)
         .def_readwrite("noise", &SessionConfig::noise)
         .def_readwrite("pool_slots", &SessionConfig::pool_slots)
+        .def_readwrite("use_graph", &SessionConfig::use_graph)
+        .def_readwrite("fake_clock", &SessionConfig::fake_clock)
         .def_readwrite("enc", &SessionConfig::enc);
 
     py::class_<FrameResult>(m, "FrameResult")
@@ -367,6 +369,7 @@ PYBIND11_MODULE(_native, m) {
         .def_property_readonly("nv12_y_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_y()); })
         .def_property_readonly("nv12_uv_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_uv()); })
         .def_property_readonly("nv12_pitch", &Session::nv12_pitch)
+        .def_property_readonly("graphs_built", &Session::graphs_built)
         .def("nv12",
              [](Session& s) {
                  const auto& g = s.encoder().geometry();

@@ -185,7 +185,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     if (idr) {
         launch_intra(geom_, buf_, src_y, src_uv, stream_);
     } else {
-        launch_hpel(geom_, fs_host_->ref_y, hp_, hp_pitch_, stream_);
+        launch_hpel(geom_, buf_, hp_, hp_pitch_, stream_);
         launch_me(geom_, buf_, src_y, stream_);
         launch_inter(geom_, buf_, src_y, src_uv, stream_);
     }
@@ -193,7 +193,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     HIP_CHECK(hipGetLastError());
 }
 
-void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
+bool GpuH264Encoder::prepare(bool force_idr) {
     if (pending_) throw std::logic_error("GpuH264Encoder: collect() the previous frame first");
     common_.begin_frame(force_idr || !have_ref_);
     const bool idr = common_.cur_idr();
@@ -223,11 +223,28 @@ void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
     f.hp_v = hp_[2] + org;
     f.hp_j = hp_[3] + org;
     f.sse_part = buf_.sse_part;
-    HIP_CHECK(hipEventRecord(start_, stream_));
+    return idr;
+}
+
+void GpuH264Encoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    // everything here depends only on fixed buffers + the device frame state, so the same
+    // sequence can be captured once into a hipGraph and replayed every frame
     HIP_CHECK(hipMemcpyAsync(buf_.fs, fs_host_, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
     enqueue_kernels(idr, src_y, src_uv);
+}
+
+void GpuH264Encoder::record_start() { HIP_CHECK(hipEventRecord(start_, stream_)); }
+
+void GpuH264Encoder::record_done() {
     HIP_CHECK(hipEventRecord(done_, stream_));
     pending_ = true;
+}
+
+void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
+    const bool idr = prepare(force_idr);
+    record_start();
+    enqueue_body(idr, src_y, src_uv);
+    record_done();
 }
 
 const std::vector<uint8_t>& GpuH264Encoder::collect() {

@@ -95,7 +95,16 @@ class GpuH264Encoder {
     hipStream_t stream() const { return stream_; }
 
     // Enqueue the encode of an NV12 frame already in device memory (pitch = pitch()).
+    // Equivalent to prepare() + record_start() + enqueue_body() + record_done().
     void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false);
+    // Split form for hipGraph replay: host-side frame decisions (rate control, reference
+    // swap) into the pinned frame state; returns whether this is an IDR frame.
+    bool prepare(bool force_idr);
+    // Frame-state upload + kernels (stream-capturable; identical every frame of a type).
+    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
+    void record_start();
+    void record_done();
+    hipEvent_t done_event() const { return done_; }
     // Wait for the submitted frame and return its Annex-B access unit.
     const std::vector<uint8_t>& collect();
     const FrameStats& last_stats() const { return stats_; }

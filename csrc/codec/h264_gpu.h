@@ -116,9 +116,10 @@ void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
                   hipStream_t stream);
 void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream);
-// Build the padded F/H/V/J planes of `ref` (luma) into `planes` (4 planes, each
-// hp_pitch x (coded_h + 2*kHpelPad), origin offset applied by the caller via FrameState).
-void launch_hpel(const Geometry& g, const uint8_t* ref_y, uint8_t* const planes[4], int hp_pitch, hipStream_t stream);
+// Build the padded F/H/V/J planes of the reference luma (b.fs->ref_y) into `planes` (4 planes,
+// each hp_pitch x (coded_h + 2*kHpelPad), origin offset applied by the caller via FrameState).
+void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
+                 hipStream_t stream);
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
 
 }  // namespace h264

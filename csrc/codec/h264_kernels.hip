@@ -118,11 +118,12 @@ __device__ __forceinline__ int qpel_planes(const Planes& P, int x4, int y4) {
 // sample footprint; the 6-tap horizontal intermediates b1 are kept in LDS as int16 and
 // reused for both H and the centre sample J.
 constexpr int kHpTW = 64, kHpTH = 16;
-__global__ __launch_bounds__(256) void k_hpel(Geometry g, const uint8_t* __restrict__ ref, uint8_t* __restrict__ pf,
+__global__ __launch_bounds__(256) void k_hpel(Geometry g, const FrameState* __restrict__ fs, uint8_t* __restrict__ pf,
                                               uint8_t* __restrict__ ph, uint8_t* __restrict__ pv,
                                               uint8_t* __restrict__ pj, int hp_pitch) {
     __shared__ uint8_t smp[kHpTH + 5][kHpTW + 8];
     __shared__ int16_t b1[kHpTH + 5][kHpTW];
+    const uint8_t* __restrict__ ref = fs->ref_y;  // via the frame state: graph-replay safe
     const int px0 = blockIdx.x * kHpTW, py0 = blockIdx.y * kHpTH;  // padded-plane coordinates
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     const int tid = threadIdx.x;
@@ -998,10 +999,11 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
 
 }  // namespace
 
-void launch_hpel(const Geometry& g, const uint8_t* ref_y, uint8_t* const planes[4], int hp_pitch, hipStream_t stream) {
+void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
+                 hipStream_t stream) {
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     dim3 grid((W + kHpTW - 1) / kHpTW, (H + kHpTH - 1) / kHpTH);
-    hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, ref_y, planes[0], planes[1], planes[2], planes[3],
+    hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, b.fs, planes[0], planes[1], planes[2], planes[3],
                        hp_pitch);
 }
 

@@ -26,6 +26,8 @@ constexpr int kBarCell = 8;
 constexpr int kBarX = 8, kBarY = 8;
 
 void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream);
+// Same, reading the parameters from device memory (hipGraph replay; width/height fix the grid).
+void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int height, hipStream_t stream);
 
 // BGRx -> NV12 (BT.709 limited range), padding the output to (coded_w, coded_h) by edge
 // replication.  Output Y plane pitch = UV plane pitch = out_pitch.

@@ -177,7 +177,7 @@ __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
     return bgrx((int)(20 + 40 * fy + 20 * band), (int)(40 + 60 * fy + 10 * band), (int)(90 + 110 * (1.f - fy * 0.5f)));
 }
 
-__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, SynthParams p) {
+__device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const SynthParams& p) {
     const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (y >= p.height || x4 >= p.width) return;
@@ -190,6 +190,15 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, SynthP
     } else {
         for (int k = 0; k < 4 && x4 + k < p.width; ++k) row[x4 + k] = v[k];
     }
+}
+
+__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, SynthParams p) { synth_body(out, p); }
+
+// Graph-replay variant: per-frame parameters come from device memory (uploaded by a memcpy
+// node of the same graph), so the captured kernel node never changes.
+__global__ __launch_bounds__(256) void k_synth_dev(uint8_t* __restrict__ out, const SynthParams* __restrict__ pp) {
+    const SynthParams p = *pp;
+    synth_body(out, p);
 }
 
 // BT.709 limited-range integer coefficients (x256); each row sums to 220 / 0 / 0.
@@ -349,6 +358,12 @@ void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream) {
     dim3 block(64, 4);
     dim3 grid((p.width / 4 + 63) / 64 + 1, (p.height + 3) / 4);
     hipLaunchKernelGGL(k_synth, grid, block, 0, stream, bgrx, p);
+}
+
+void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int height, hipStream_t stream) {
+    dim3 block(64, 4);
+    dim3 grid((width / 4 + 63) / 64 + 1, (height + 3) / 4);
+    hipLaunchKernelGGL(k_synth_dev, grid, block, 0, stream, bgrx, d_params);
 }
 
 void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_t* y, uint8_t* uv, int out_pitch,

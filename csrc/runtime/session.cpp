@@ -106,11 +106,18 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         HIP_CHECK(hipMemcpy(p, wy.data(), wy.size() * 4, hipMemcpyHostToDevice));
     }
     HIP_CHECK(hipEventCreate(&ev_start_));
+    HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams), hipHostMallocDefault));
+    HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams)));
+    graphs_.assign((size_t)cfg_.pool_slots * 2, nullptr);
     t0_us_ = now_us();
 }
 
 Session::~Session() {
     if (stream_) hipStreamSynchronize(stream_);
+    for (auto g : graphs_)
+        if (g) hipGraphExecDestroy(g);
+    hipHostFree(synth_host_);
+    hipFree(synth_dev_);
     enc_.reset();
     pool_.reset();
     hipFree(nv12_y_);
@@ -121,8 +128,7 @@ Session::~Session() {
     hipStreamDestroy(stream_);
 }
 
-void Session::convert_and_encode(int slot, bool force_idr) {
-    TraceRange tr("mxdesk.convert+encode.enqueue");
+void Session::convert(int slot) {
     const h264::Geometry& g = enc_->geometry();
     if (scale_) {
         pix::launch_scale_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, lt_, nv12_y_, nv12_uv_,
@@ -132,21 +138,23 @@ void Session::convert_and_encode(int slot, bool force_idr) {
                                  g.pitch, g.coded_w, g.coded_h, stream_);
     }
     HIP_CHECK(hipGetLastError());
+}
+
+void Session::convert_and_encode(int slot, bool force_idr) {
+    TraceRange tr("mxdesk.convert+encode.enqueue");
+    convert(slot);
     enc_->submit(nv12_y_, nv12_uv_, force_idr);
     pending_ = true;
 }
 
-void Session::submit_synthetic(bool force_idr) {
-    if (pending_) throw std::logic_error("Session: collect() before the next submit");
-    TraceRange tr("mxdesk.submit_synthetic");
-    const int slot = pool_->acquire();
-    t_capture_ = now_us();
+pix::SynthParams Session::synth_params() {
     pix::SynthParams p;
     p.width = cfg_.width;
     p.height = cfg_.height;
     p.pitch = pool_->pitch();
     p.frame_id = frame_id_;
-    p.timestamp_us = (uint32_t)(t_capture_ - t0_us_);
+    p.timestamp_us = cfg_.fake_clock ? (uint32_t)((int64_t)frame_id_ * 1000000 / std::max(1, cfg_.fps))
+                                     : (uint32_t)(t_capture_ - t0_us_);
     p.t = (float)frame_id_ / (float)std::max(1, cfg_.fps);
     p.origin_x = 0;
     p.origin_y = 0;
@@ -155,10 +163,54 @@ void Session::submit_synthetic(bool force_idr) {
     p.noise = cfg_.noise;
     p.cursor_x = cursor_x_;
     p.cursor_y = cursor_y_;
+    return p;
+}
+
+hipGraphExec_t Session::capture_frame_graph(int slot, bool idr) {
+    TraceRange tr("mxdesk.graph.capture");
+    hipGraph_t graph = nullptr;
+    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    try {
+        HIP_CHECK(hipMemcpyAsync(synth_dev_, synth_host_, sizeof(pix::SynthParams), hipMemcpyHostToDevice, stream_));
+        pix::launch_synth_dev(pool_->data(slot), synth_dev_, cfg_.width, cfg_.height, stream_);
+        HIP_CHECK(hipGetLastError());
+        convert(slot);
+        enc_->enqueue_body(idr, nv12_y_, nv12_uv_);
+    } catch (...) {
+        hipStreamEndCapture(stream_, &graph);  // leave capture mode before propagating
+        if (graph) hipGraphDestroy(graph);
+        throw;
+    }
+    HIP_CHECK(hipStreamEndCapture(stream_, &graph));
+    hipGraphExec_t exec = nullptr;
+    HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(graph));
+    ++graphs_built_;
+    return exec;
+}
+
+void Session::submit_synthetic(bool force_idr) {
+    if (pending_) throw std::logic_error("Session: collect() before the next submit");
+    TraceRange tr("mxdesk.submit_synthetic");
+    const int slot = pool_->acquire();
+    t_capture_ = now_us();
+    const pix::SynthParams p = synth_params();
+    if (!cfg_.use_graph) {
+        HIP_CHECK(hipEventRecord(ev_start_, stream_));
+        pix::launch_synth(pool_->data(slot), p, stream_);
+        HIP_CHECK(hipGetLastError());
+        convert_and_encode(slot, force_idr);
+        return;
+    }
+    *synth_host_ = p;  // read by the graph's memcpy node (previous frame already collected)
+    const bool idr = enc_->prepare(force_idr);
     HIP_CHECK(hipEventRecord(ev_start_, stream_));
-    pix::launch_synth(pool_->data(slot), p, stream_);
-    HIP_CHECK(hipGetLastError());
-    convert_and_encode(slot, force_idr);
+    enc_->record_start();
+    hipGraphExec_t& exec = graphs_[(size_t)slot * 2 + (idr ? 1 : 0)];
+    if (!exec) exec = capture_frame_graph(slot, idr);
+    HIP_CHECK(hipGraphLaunch(exec, stream_));
+    enc_->record_done();
+    pending_ = true;
 }
 
 void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
@@ -188,7 +240,9 @@ FrameResult Session::collect() {
     const h264::FrameStats& st = enc_->last_stats();
     r.idr = st.idr;
     r.qp = st.qp;
-    r.gpu_ms = st.encode_ms;
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev_start_, enc_->done_event());
+    r.gpu_ms = ms;  // render/upload start -> bitstream written
     const double ny = (double)enc_->common().config().width * enc_->common().config().height, nc = ny / 4;
     auto psnr = [](uint64_t sse, double n) { return sse == 0 ? 99.0 : std::min(99.0, 10.0 * std::log10(65025.0 * n / (double)sse)); };
     r.psnr_y = psnr(st.sse[0], ny);

@@ -52,6 +52,8 @@ struct SessionConfig {
     int fps = 60;
     int noise = 1;          // synthetic animated-noise panel
     int pool_slots = 3;
+    int use_graph = 1;      // replay the per-frame chain (synth -> CSC -> encoder) as a hipGraph
+    int fake_clock = 0;     // barcode timestamp = frame_id * 1e6 / fps (deterministic streams for tests)
     h264::EncoderConfig enc;  // width/height overwritten from out size
 };
 
@@ -99,8 +101,13 @@ class Session {
     int nv12_pitch() const { return enc_->pitch(); }
     static int64_t now_us();
 
+    int graphs_built() const { return graphs_built_; }
+
    private:
+    void convert(int slot);
     void convert_and_encode(int slot, bool force_idr);
+    pix::SynthParams synth_params();
+    hipGraphExec_t capture_frame_graph(int slot, bool idr);
 
     SessionConfig cfg_;
     hipStream_t stream_ = nullptr;
@@ -114,6 +121,12 @@ class Session {
     pix::LanczosTables lt_{};
     void* lt_mem_ = nullptr;
     hipEvent_t ev_start_ = nullptr;
+    // hipGraph replay: pinned + device synth parameters, one executable graph per
+    // (pool slot, frame type) -- the only things that change the captured node arguments
+    pix::SynthParams* synth_host_ = nullptr;
+    pix::SynthParams* synth_dev_ = nullptr;
+    std::vector<hipGraphExec_t> graphs_;
+    int graphs_built_ = 0;
     uint32_t frame_id_ = 0;
     int64_t t0_us_ = 0;
     int64_t t_capture_ = 0;
