@@ -141,6 +141,7 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     HIP_CHECK(hipMalloc(&buf_.unit_off, sizeof(uint32_t) * nmb));
     HIP_CHECK(hipMalloc(&buf_.skip_run, sizeof(int32_t) * nmb));
     HIP_CHECK(hipMalloc(&buf_.coded_list, sizeof(uint32_t) * nmb));
+    HIP_CHECK(hipMalloc(&buf_.coded_info, sizeof(uint4) * nmb));
     HIP_CHECK(hipMalloc(&buf_.slice_info, sizeof(uint32_t) * kSliceInfo * kMaxSlices));
     HIP_CHECK(hipMemsetAsync(buf_.slice_info, 0, sizeof(uint32_t) * kSliceInfo * kMaxSlices, stream_));
     // payload capacity: 768 B per MB (intra at low QP stays far below)
@@ -172,6 +173,7 @@ GpuH264Encoder::~GpuH264Encoder() {
     hipFree(buf_.unit_off);
     hipFree(buf_.skip_run);
     hipFree(buf_.coded_list);
+    hipFree(buf_.coded_info);
     hipFree(buf_.slice_info);
     hipFree(buf_.out_hdr);
     hipFree(buf_.sse_part);

@@ -734,6 +734,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
                                                        const uint32_t* __restrict__ slot_bits,
                                                        uint32_t* __restrict__ unit_off, int32_t* __restrict__ skip_run,
                                                        uint32_t* __restrict__ coded_list,
+                                                       uint4* __restrict__ coded_info,
                                                        uint32_t* __restrict__ slice_info, size_t out_bytes,
                                                        OutHeader* __restrict__ hdr) {
     __shared__ uint32_t sb[kScanTile];
@@ -839,6 +840,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         slice_info[kSliceInfo * t + 5] = ebase;
     }
     __syncthreads();
+    // dense per-rank unit records for k_pack: one 16-byte load per unit instead of the
+    // coded_list -> unit_off / skip_run / slot_bits chains
+    for (uint32_t r = t; r < carry_rank; r += kScanThreads) {
+        const int i = (int)coded_list[r];
+        const int s = i / per_slice;
+        const uint32_t off = slice_info[kSliceInfo * s + 1] * 8 + slice_info[kSliceInfo * s + 0] +
+                             (unit_off[i] - slice_info[kSliceInfo * s + 5]);
+        const int run = skip_run[i];
+        uint32_t b = slot_bits[i];
+        if (b == 0xffffffffu) b = 1;
+        coded_info[r] = make_uint4(off, (uint32_t)i, (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b, (uint32_t)run);
+    }
+    __syncthreads();
     for (int i = t; i < nmb; i += kScanThreads) {
         const int s = i / per_slice;
         unit_off[i] = slice_info[kSliceInfo * s + 1] * 8 + slice_info[kSliceInfo * s + 0] +
@@ -893,16 +907,15 @@ __device__ __forceinline__ void overlap(uint32_t& acc, uint32_t W0, uint32_t s0,
     acc |= bits << (W0 + 32 - hi);
 }
 
-// One thread per 16 output bytes: one binary search locates the first overlapping MB
-// unit, then each of the 4 words is assembled from the slice header / MB units / slice
-// trailer bits overlapping it and the 16 bytes are stored (big-endian) straight into
-// pinned host memory with one 16-byte store.  No atomics and no zero-fill pass.
+// One thread per 32-bit output word, four lanes per 16-byte quad: each lane locates its
+// word's first overlapping slice / MB unit (4-ary search over the dense per-rank unit
+// records written by k_scan), assembles the word from the slice header / MB units / slice
+// trailer bits that overlap it, and lane 0 of the quad gathers the four words with lane
+// shuffles and writes them with one 16-byte store straight into pinned host memory.
+// No atomics, no zero-fill pass, short dependent-load chains (latency-bound kernel).
 __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __restrict__ fs,
                                               const uint32_t* __restrict__ slot,
-                                              const uint32_t* __restrict__ slot_bits,
-                                              const uint32_t* __restrict__ unit_off,
-                                              const int32_t* __restrict__ skip_run,
-                                              const uint32_t* __restrict__ coded_list,
+                                              const uint4* __restrict__ coded_info,
                                               const uint32_t* __restrict__ slice_info,
                                               const OutHeader* __restrict__ hdr, uint8_t* __restrict__ host) {
     const OutHeader h = *hdr;
@@ -915,37 +928,23 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
         hs[kMaxSlices + s] = slice_info[kSliceInfo * s + 2];
     }
     if (h.overflow) return;
-    const int nmb = g.mb_w * g.mb_h;
-    const int per_slice = fs->slice_rows * g.mb_w;
     const bool idr = fs->idr != 0;
     const int ns = (int)h.num_slices;
-    const uint32_t nquads = (h.total_bytes + 15) / 16;  // each thread emits 16 bytes
+    const uint32_t nquads = (h.total_bytes + 15) / 16;
     uint4* out = reinterpret_cast<uint4*>(host + kOutPayloadOffset);
-    for (size_t q = gid; q < nquads; q += stride) {
-        uint32_t res[4];
-        const uint32_t Q0 = (uint32_t)q * 128;
-        // last slice starting at or before Q0, and last MB unit starting at or before Q0
-        int lo = 0, hi = ns - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (slice_info[kSliceInfo * mid + 1] * 8 <= Q0) lo = mid; else hi = mid - 1;
-        }
-        int first_rank;  // last coded unit of slice `lo` starting at or before Q0
-        {
-            int a = (int)slice_info[kSliceInfo * lo + 6], b = (int)slice_info[kSliceInfo * lo + 7] - 1;
-            if (b < a) {
-                first_rank = a;
-            } else {
-                while (a < b) {
-                    const int mid = (a + b + 1) >> 1;
-                    if (unit_off[coded_list[mid]] <= Q0) a = mid; else b = mid - 1;
-                }
-                first_rank = a;
+    const int sub = threadIdx.x & 3;  // word within the quad
+    // all four lanes of a quad iterate together (uniform trip count for the shuffles)
+    for (size_t qbase = gid >> 2; qbase < ((nquads + 63) / 64) * 64; qbase += stride >> 2) {
+        const bool active = qbase < nquads;
+        uint32_t acc = 0;
+        if (active) {
+            const uint32_t W0 = (uint32_t)qbase * 128 + 32 * sub;
+            // last slice starting at or before W0
+            int lo = 0, hi = ns - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (slice_info[kSliceInfo * mid + 1] * 8 <= W0) lo = mid; else hi = mid - 1;
             }
-        }
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t W0 = Q0 + 32 * k;
-            uint32_t acc = 0;
             for (int s = lo; s < ns; ++s) {
                 const uint32_t sbit = slice_info[kSliceInfo * s + 1] * 8;
                 if (sbit >= W0 + 32) break;
@@ -962,18 +961,31 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
                     overlap(acc, W0, sbit, hbits, [&](uint32_t x, int n) { return slot_get(hw, x, n); });
                 }
                 if (dend > W0 && sbit + hbits < W0 + 32) {
+                    // last coded unit of the slice starting at or before W0 (4-ary search:
+                    // three independent loads per step)
+                    int a = (int)slice_info[kSliceInfo * s + 6];
                     const int rend = (int)slice_info[kSliceInfo * s + 7];
-                    for (int r = (s == lo ? first_rank : (int)slice_info[kSliceInfo * s + 6]); r < rend; ++r) {
-                        const int i = (int)coded_list[r];
-                        const uint32_t off = unit_off[i];
+                    int b = rend - 1;
+                    while (b - a > 2) {
+                        const int step = (b - a + 3) >> 2;
+                        const int m1 = a + step, m2 = min(a + 2 * step, b), m3 = min(a + 3 * step, b);
+                        const uint32_t o1 = coded_info[m1].x, o2 = coded_info[m2].x, o3 = coded_info[m3].x;
+                        if (o3 <= W0) a = m3;
+                        else if (o2 <= W0) { a = m2; b = m3 - 1; }
+                        else if (o1 <= W0) { a = m1; b = m2 - 1; }
+                        else b = m1 - 1;
+                    }
+                    while (a < b && coded_info[a + 1].x <= W0) ++a;
+                    for (int r = a; r < rend; ++r) {
+                        const uint4 ci = coded_info[r];
+                        const uint32_t off = ci.x;
                         if (off >= W0 + 32) break;
-                        const int run = skip_run[i];
+                        if (off + ci.z <= W0) continue;
+                        const int run = (int)ci.w;
                         const int plen = idr ? 0 : ue_len((uint32_t)run);
-                        const uint32_t sb = slot_bits[i];
-                        if (off + plen + sb <= W0) continue;
                         const uint32_t pv = (uint32_t)run + 1;
-                        const uint32_t* sp = slot + (size_t)i * kSlotWords;
-                        overlap(acc, W0, off, plen + sb, [&](uint32_t x, int n) {
+                        const uint32_t* sp = slot + (size_t)ci.y * kSlotWords;
+                        overlap(acc, W0, off, ci.z, [&](uint32_t x, int n) {
                             uint32_t r2 = 0;
                             int rem = n;
                             if ((int)x < plen) {
@@ -991,9 +1003,11 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
                 const uint32_t tv = trail ? (((trail + 1) << 1) | 1u) : 1u;
                 overlap(acc, W0, dend, tl + 1, [&](uint32_t x, int n) { return tv >> (tl + 1 - (int)x - n); });
             }
-            res[k] = bswap32(acc);
         }
-        out[q] = make_uint4(res[0], res[1], res[2], res[3]);
+        const uint32_t w = bswap32(acc);
+        const int lane = threadIdx.x & 63, q0 = lane & ~3;
+        const uint32_t w0 = __shfl(w, q0), w1 = __shfl(w, q0 + 1), w2 = __shfl(w, q0 + 2), w3 = __shfl(w, q0 + 3);
+        if (active && sub == 0) out[qbase] = make_uint4(w0, w1, w2, w3);
     }
 }
 
@@ -1029,9 +1043,9 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, b.mb, b.coef, b.slot,
                        b.slot_bits);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.unit_off, b.skip_run,
-                       b.coded_list, b.slice_info, b.out_bytes, b.out_hdr);
-    hipLaunchKernelGGL(k_pack, dim3(64), dim3(256), 0, stream, g, b.fs, b.slot, b.slot_bits, b.unit_off, b.skip_run,
-                       b.coded_list, b.slice_info, b.out_hdr, host_out);
+                       b.coded_list, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr);
+    hipLaunchKernelGGL(k_pack, dim3(256), dim3(256), 0, stream, g, b.fs, b.slot, b.coded_info, b.slice_info,
+                       b.out_hdr, host_out);
 }
 
 }  // namespace h264
