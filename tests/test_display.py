@@ -1,0 +1,56 @@
+"""Display bring-up helpers: Xwrapper patch, Xorg command line,
+X-socket readiness probe, X11 capture failure mode without a server, session-per-GPU programs."""
+import os
+import threading
+import time
+from pathlib import Path
+
+import pytest
+
+from mxdesk.display import xorg as X
+from mxdesk.parallel.launcher import session_programs
+
+
+def test_patch_xwrapper():
+    out = X.patch_xwrapper("# Xwrapper.config\nallowed_users=console\n")
+    assert "allowed_users=anybody" in out and "needs_root_rights=yes" in out
+    assert X.patch_xwrapper("allowed_users=anybody\nneeds_root_rights=no\n").count("needs_root_rights") == 1
+
+
+def test_xorg_command_extensions_and_randr_off():
+    s = X.DisplaySettings(video_port="DFP", dpi=120, display=":3")
+    cmd = X.xorg_command(s, "/tmp/x.conf")
+    assert cmd[:6] == ["Xorg", "vt7", "-noreset", "-novtswitch", "-sharevts", "-dpi"] and cmd[-1] == ":3"
+    assert ["+extension", "MIT-SHM"] == cmd[cmd.index("MIT-SHM") - 1:cmd.index("MIT-SHM") + 1]
+    assert "RANDR" in cmd and "-config" in cmd
+    assert "RANDR" not in X.xorg_command(X.DisplaySettings(video_port="none"))  # README.md:226,234
+
+
+def test_wait_for_x_sees_socket():
+    disp = ":%d" % (900 + os.getpid() % 90)
+    path = Path(X.x_socket(disp))
+    path.parent.mkdir(parents=True, exist_ok=True)
+    path.unlink(missing_ok=True)
+    try:
+        assert not X.wait_for_x(disp, timeout=0.2, poll=0.05)
+        threading.Timer(0.2, path.touch).start()
+        t0 = time.monotonic()
+        assert X.wait_for_x(disp, timeout=5, poll=0.05)
+        assert time.monotonic() - t0 < 4
+    finally:
+        path.unlink(missing_ok=True)
+
+
+def test_x11_capture_without_server_fails_cleanly():
+    from mxdesk.models.x11 import X11Capture
+
+    with pytest.raises(OSError, match="cannot open X display"):
+        X11Capture(":987")
+
+
+def test_session_programs_pin_one_gpu_each():
+    progs = session_programs(4, base_port=9000, sessions_per_gpu=2)
+    assert len(progs) == 8
+    assert [p.environment["HIP_VISIBLE_DEVICES"] for p in progs] == ["0", "0", "1", "1", "2", "2", "3", "3"]
+    assert [p.environment["SELKIES_PORT"] for p in progs] == [str(9000 + i) for i in range(8)]
+    assert all(p.ready.kind == "tcp" and p.command[1:4] == ["-m", "mxdesk", "serve"] for p in progs)
