@@ -20,6 +20,7 @@ using namespace mx;
 
 void register_net(py::module& m);    // net_bindings.cpp
 void register_audio(py::module& m);  // audio_bindings.cpp
+void register_rfb(py::module& m);    // rfb_bindings.cpp
 
 namespace {
 
@@ -96,6 +97,7 @@ PYBIND11_MODULE(_native, m) {
     m.def("synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
     register_net(m);
     register_audio(m);
+    register_rfb(m);
     m.def("now_us", &Session::now_us, "CLOCK_MONOTONIC microseconds (same clock as time.monotonic())");
 
     // ---------------------------------------------------------------- codec helpers

@@ -6,7 +6,8 @@
 * Security: VNC authentication (DES challenge, RFC 6143 §7.2.2) with the full-access
   password and an optional view-only password (input is ignored for view-only clients);
   ``None`` when no password is configured.
-* Encodings: ZRLE (per-connection zlib stream; solid / raw 64x64 tiles), Raw, and the
+* Encodings: ZRLE (native C++ encoder, csrc/rfb/zrle.cpp: solid / packed-palette / RLE /
+  palette-RLE / raw 64x64 tiles over a per-connection zlib stream), Raw, and the
   DesktopSize pseudo-encoding.  Updates carry only the 64x64 tiles that changed since the
   last frame sent to that client (incremental updates), merged into row spans.
 * Pixel formats: 32 bpp true colour with any byte permutation of R/G/B (noVNC asks for
@@ -21,11 +22,12 @@ import logging
 import os
 import struct
 import time
-import zlib
 from typing import Any, Callable
 
 import numpy as np
 from aiohttp import WSMsgType, web
+
+from .. import native
 
 from .des import vnc_response
 from .input import InputEvent
@@ -100,7 +102,7 @@ class RfbConnection:
         self.encodings: list[int] = [ENC_RAW]
         self.perm = None  # byte permutation from BGRX to the client format
         self.last: np.ndarray | None = None
-        self.z = zlib.compressobj(6)
+        self.zrle = native().rfb.ZrleEncoder(6)  # one zlib stream per connection (RFC 6143 §7.7.6)
         self.pending: tuple[int, int, int, int, int] | None = None
         self.w, self.h = server.width, server.height
 
@@ -209,11 +211,7 @@ class RfbConnection:
         if not incremental or self.last is None or self.last.shape != frame.shape:
             return [(0, 0, w, h)]
         th, tw = (h + TILE - 1) // TILE, (w + TILE - 1) // TILE
-        ph, pw = th * TILE - h, tw * TILE - w
-        diff = np.any(frame != self.last, axis=2)
-        if ph or pw:
-            diff = np.pad(diff, ((0, ph), (0, pw)))
-        tiles = diff.reshape(th, TILE, tw, TILE).any(axis=(1, 3))
+        tiles = native().rfb.tile_diff(np.ascontiguousarray(frame), np.ascontiguousarray(self.last), TILE)
         rects = []
         for ty in range(th):
             tx = 0
@@ -234,21 +232,13 @@ class RfbConnection:
     def _encode_update(self, frame: np.ndarray, rects: list[tuple[int, int, int, int]]) -> bytes:
         zrle = ENC_ZRLE in self.encodings
         out = [struct.pack(">BxH", 0, len(rects))]
+        frame = np.ascontiguousarray(frame)
+        perm = list(self.perm[:3]) if self.perm is not None else [0, 1, 2]
         for x, y, w, h in rects:
-            px = self._pixels(frame[y:y + h, x:x + w])
-            if zrle:
-                raw = bytearray()
-                for ty in range(0, h, TILE):
-                    for tx in range(0, w, TILE):
-                        t = px[ty:ty + TILE, tx:tx + TILE, :3]
-                        first = t[0, 0]
-                        if np.all(t == first):
-                            raw += b"\x01" + first.tobytes()
-                        else:
-                            raw += b"\x00" + np.ascontiguousarray(t).tobytes()
-                data = self.z.compress(bytes(raw)) + self.z.flush(zlib.Z_SYNC_FLUSH)
-                out.append(struct.pack(">HHHHi", x, y, w, h, ENC_ZRLE) + struct.pack(">I", len(data)) + data)
+            if zrle:  # native ZRLE: all tile subencodings, persistent zlib stream
+                out.append(struct.pack(">HHHHi", x, y, w, h, ENC_ZRLE) + self.zrle.encode(frame, x, y, w, h, perm))
             else:
+                px = self._pixels(frame[y:y + h, x:x + w])
                 out.append(struct.pack(">HHHHi", x, y, w, h, ENC_RAW) + np.ascontiguousarray(px).tobytes())
         return b"".join(out)
 

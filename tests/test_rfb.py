@@ -66,6 +66,66 @@ async def _client(reader, writer, password, pixfmt_rgbx=True, encodings=(16, 0))
     return w, h, name
 
 
+def _cpixels(raw, off, n):
+    return np.frombuffer(raw[off:off + 3 * n], np.uint8).reshape(n, 3), off + 3 * n
+
+
+def _run(raw, off):
+    n = 1
+    while raw[off] == 255:
+        n += 255
+        off += 1
+    return n + raw[off], off + 1
+
+
+def zrle_tile(raw, off, tw, th):
+    """Independent ZRLE tile decoder (RFC 6143 §7.7.6), 3-byte CPIXELs -> (th, tw, 3)."""
+    sub = raw[off]
+    off += 1
+    n = tw * th
+    if sub == 0:
+        px, off = _cpixels(raw, off, n)
+    elif sub == 1:
+        c, off = _cpixels(raw, off, 1)
+        px = np.repeat(c, n, axis=0)
+    elif 2 <= sub <= 16:
+        pal, off = _cpixels(raw, off, sub)
+        bits = 1 if sub == 2 else 2 if sub <= 4 else 4
+        rowb = (tw * bits + 7) // 8
+        idx = []
+        for r in range(th):
+            row = raw[off:off + rowb]
+            off += rowb
+            v = int.from_bytes(row, "big")
+            tot = rowb * 8
+            idx += [(v >> (tot - bits * (c + 1))) & ((1 << bits) - 1) for c in range(tw)]
+        px = pal[np.array(idx)]
+    elif sub == 128:
+        out = []
+        while len(out) < n:
+            c, off = _cpixels(raw, off, 1)
+            ln, off = _run(raw, off)
+            out += [c[0]] * ln
+        assert len(out) == n
+        px = np.array(out)
+    elif sub >= 130:
+        pal, off = _cpixels(raw, off, sub - 128)
+        out = []
+        while len(out) < n:
+            b = raw[off]
+            off += 1
+            if b & 128:
+                ln, off = _run(raw, off)
+                out += [pal[b & 127]] * ln
+            else:
+                out.append(pal[b])
+        assert len(out) == n
+        px = np.array(out)
+    else:
+        raise AssertionError(f"bad subencoding {sub}")
+    return px.reshape(th, tw, 3), off
+
+
 async def _read_update(reader, w, h, fb, zd):
     t = (await reader.readexactly(1))[0]
     assert t == 0
@@ -82,19 +142,60 @@ async def _read_update(reader, w, h, fb, zd):
             for ty in range(y, y + rh, 64):
                 for tx in range(x, x + rw, 64):
                     tw, th = min(64, x + rw - tx), min(64, y + rh - ty)
-                    sub = raw[off]
-                    off += 1
-                    if sub == 1:
-                        fb[ty:ty + th, tx:tx + tw] = np.frombuffer(raw[off:off + 3], np.uint8)
-                        off += 3
-                    else:
-                        assert sub == 0
-                        fb[ty:ty + th, tx:tx + tw] = np.frombuffer(raw[off:off + tw * th * 3], np.uint8).reshape(th, tw, 3)
-                        off += tw * th * 3
+                    fb[ty:ty + th, tx:tx + tw], off = zrle_tile(raw, off, tw, th)
+            assert off == len(raw)
         else:
             assert enc == 0
             fb[y:y + rh, x:x + rw] = np.frombuffer(await reader.readexactly(rw * rh * 4), np.uint8).reshape(rh, rw, 4)[..., :3]
     return rects
+
+
+def _tiles_frame(rng):
+    """Frame whose 64x64 tiles exercise every ZRLE subencoding."""
+    f = np.zeros((130, 330, 4), np.uint8)
+    f[:64, 0:64, :3] = (1, 2, 3)                                        # solid
+    f[:64, 64:128, :3] = rng.choice([0, 255], (64, 64, 1))              # 2 colours, noisy -> packed
+    f[:64, 128:192, :3] = np.array([[9, 9, 9], [200, 1, 1], [1, 200, 1], [5, 6, 7], [90, 90, 9]])[
+        rng.integers(0, 5, (64, 64))]                                   # 5 colours -> packed 4 bit
+    f[:64, 192:256, :3] = np.repeat(np.arange(64, dtype=np.uint8)[:, None, None] * 3, 64, axis=1)  # 64 colours, long runs
+    f[:64, 256:320, :3] = rng.integers(0, 256, (64, 64, 3))             # raw
+    f[64:, :, :3] = np.where((np.arange(330) // 17 % 2)[None, :, None] == 0, 40, 220)  # 2 colours in runs
+    f[64:, 300:330, :3] = 77
+    return f
+
+
+@pytest.mark.parametrize("perm", [[0, 1, 2], [2, 1, 0]])
+def test_native_zrle_all_subencodings_roundtrip(native, perm):
+    import zlib
+
+    rng = np.random.default_rng(5)
+    frame = _tiles_frame(rng)
+    enc = native.rfb.ZrleEncoder(6)
+    zd = zlib.decompressobj()
+    for rect in [(0, 0, 330, 130), (64, 0, 200, 64), (3, 70, 61, 60)]:
+        x, y, w, h = rect
+        body = enc.encode(frame, x, y, w, h, perm)
+        ln = struct.unpack(">I", body[:4])[0]
+        assert ln == len(body) - 4
+        raw = zd.decompress(body[4:])
+        off, got = 0, np.zeros((h, w, 3), np.uint8)
+        for ty in range(0, h, 64):
+            for tx in range(0, w, 64):
+                tw, th = min(64, w - tx), min(64, h - ty)
+                got[ty:ty + th, tx:tx + tw], off = zrle_tile(raw, off, tw, th)
+        assert off == len(raw)
+        assert np.array_equal(got, frame[y:y + h, x:x + w][..., perm])
+    st = enc.stats
+    assert st[1] and st[0] and st[128] + sum(st[130:]) > 0 and sum(st[2:17]) > 0
+
+
+def test_native_tile_diff(native):
+    a = np.zeros((130, 200, 4), np.uint8)
+    b = a.copy()
+    b[129, 199, 1] = 1
+    b[0, 64, 0] = 1
+    fl = native.rfb.tile_diff(b, a, 64)
+    assert fl.shape == (3, 4) and fl.sum() == 2 and fl[2, 3] == 1 and fl[0, 1] == 1
 
 
 @pytest.mark.parametrize("encodings", [(16, 0), (0,)])
