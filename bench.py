@@ -44,7 +44,8 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
-    ap.add_argument("--graph", type=int, default=1, help="replay the per-frame chain as a hipGraph")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
                     help="concurrent sessions per GPU (density): each has its own HIP stream and one frame in flight")
     ap.add_argument("--json-out", type=str, default="")

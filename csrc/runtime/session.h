@@ -52,7 +52,8 @@ struct SessionConfig {
     int fps = 60;
     int noise = 1;          // synthetic animated-noise panel
     int pool_slots = 3;
-    int use_graph = 1;      // replay the per-frame chain (synth -> CSC -> encoder) as a hipGraph
+    int use_graph = 0;      // replay the per-frame chain as a hipGraph (measured slower than eager
+                            // launches on ROCm 7.2 for this chain: profiles/r01_graph)
     int fake_clock = 0;     // barcode timestamp = frame_id * 1e6 / fps (deterministic streams for tests)
     h264::EncoderConfig enc;  // width/height overwritten from out size
 };

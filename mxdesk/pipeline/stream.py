@@ -95,6 +95,7 @@ class StreamPipeline:
         self.queue_frames = queue_frames
         self.stall_s = stall_s
         self.paced = paced
+        self.bitrate_kbps = bitrate_kbps  # configured CBR target (congestion control upper bound)
         self._enc_args = dict(bitrate_kbps=bitrate_kbps, keyint=keyint, search_range=search_range, subpel=subpel,
                               noise=noise)
         self._subs: list[_Subscriber] = []
@@ -192,6 +193,11 @@ class StreamPipeline:
     def set_bitrate(self, kbps: int) -> None:
         self._pending_bitrate = int(max(100, min(kbps, 200_000)))
 
+    def set_fps(self, fps: float) -> None:
+        """Client frame-rate request (selkies ``_f,fps``): changes the pacing only; the
+        stream's VUI timing stays at the session rate."""
+        self.pace_fps = float(max(1.0, min(float(fps), 240.0)))
+
     def set_cursor(self, x: int, y: int) -> None:
         self._cursor = (int(x), int(y))
 
@@ -238,7 +244,6 @@ class StreamPipeline:
         return fr
 
     def _run(self) -> None:
-        period = 1.0 / self.fps
         next_t = time.monotonic()
         while not self._stop.is_set():
             try:
@@ -255,7 +260,7 @@ class StreamPipeline:
                 self.request_idr()
                 self._stop.wait(min(2.0, 0.1 * self.restarts))  # back off on repeated failures
             if self.paced:
-                next_t += period
+                next_t += 1.0 / (getattr(self, "pace_fps", None) or self.fps)
                 delay = next_t - time.monotonic()
                 if delay > 0:
                     self._stop.wait(delay)

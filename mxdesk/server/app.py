@@ -74,7 +74,8 @@ class MediaServer:
                 log.warning("audio disabled: %s", e)
                 src = None
             self.audio = AudioPipeline(src) if src is not None else None
-        self.whep = WhepEndpoint(pipeline, audio=self.audio, host=getattr(cfg, "webrtc_host", None) or None,
+        self.whep = WhepEndpoint(pipeline, audio=self.audio,
+                                 congestion_control=bool(getattr(cfg, "congestion_control", False)), host=getattr(cfg, "webrtc_host", None) or None,
                                  udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0))
 
     # ------------------------------------------------------------------ app
@@ -234,6 +235,8 @@ class MediaServer:
             lat = ev.extra.get("latency_ms")
             if lat is not None:
                 p.metrics.on_client_latency(float(lat))
+        elif ev.kind == "fps":
+            p.set_fps(ev.value)
         elif ev.kind == "gamepad":
             if self.gamepad is not None:
                 self.gamepad.apply(ev)

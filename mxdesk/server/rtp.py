@@ -1,5 +1,6 @@
 """RTP/RTCP helpers in Python: H.264 depacketizer (RFC 6184) for test peers and RTCP
-packet builders/parsers (RFC 3550 SR/SDES, RFC 4585 generic NACK + PLI, RFC 5104 FIR)."""
+packet builders/parsers (RFC 3550 SR/RR/SDES, RFC 4585 generic NACK + PLI, RFC 5104 FIR,
+REMB receiver bandwidth estimates)."""
 from __future__ import annotations
 
 import struct
@@ -80,6 +81,20 @@ def build_pli(sender_ssrc: int, media_ssrc: int) -> bytes:
     return struct.pack("!BBHII", 0x81, 206, 2, sender_ssrc, media_ssrc)
 
 
+def build_rr(sender_ssrc: int, media_ssrc: int, fraction_lost: float, cum_lost: int = 0, ext_seq: int = 0) -> bytes:
+    lost = (int(max(0.0, min(fraction_lost, 255 / 256)) * 256) << 24) | (cum_lost & 0xFFFFFF)
+    return struct.pack("!BBHI", 0x81, 201, 7, sender_ssrc) + struct.pack("!IIIIII", media_ssrc, lost, ext_seq, 0, 0, 0)
+
+
+def build_remb(sender_ssrc: int, media_ssrc: int, bps: int) -> bytes:
+    exp = 0
+    while bps >> exp > 0x3FFFF:
+        exp += 1
+    mant = bps >> exp
+    fci = b"REMB" + struct.pack("!BBBBI", 1, (exp << 2) | (mant >> 16), (mant >> 8) & 0xFF, mant & 0xFF, media_ssrc)
+    return struct.pack("!BBHII", 0x8F, 206, 2 + len(fci) // 4, sender_ssrc, 0) + fci
+
+
 def build_nack(sender_ssrc: int, media_ssrc: int, seqs: list[int]) -> bytes:
     fci = b""
     seqs = sorted(set(s & 0xFFFF for s in seqs))
@@ -114,8 +129,23 @@ def parse_rtcp(buf: bytes) -> list[dict]:
                     seqs.append(pid)
                     seqs += [(pid + i + 1) & 0xFFFF for i in range(16) if blp & (1 << i)]
                 d["nack"] = seqs
-        elif pt == 200 and len(body) >= 24:
+            if pt == 206 and fmt == 15 and len(body) >= 16 and body[8:12] == b"REMB":
+                # draft-alvestrand-rmcat-remb: receiver estimated maximum bitrate
+                n, b1, b2, b3 = struct.unpack_from("!BBBB", body, 12)
+                exp, mant = b1 >> 2, ((b1 & 3) << 16) | (b2 << 8) | b3
+                d["remb_bps"] = mant << exp
+        elif pt in (200, 201) and len(body) >= 4:
             d["ssrc"] = struct.unpack_from("!I", body)[0]
+            blocks = []
+            k = 24 if pt == 200 else 4
+            for _ in range(fmt):  # report blocks (fmt = reception report count)
+                if k + 24 > len(body):
+                    break
+                ssrc, lost_word, hseq, jitter, lsr, dlsr = struct.unpack_from("!IIIIII", body, k)
+                blocks.append({"ssrc": ssrc, "fraction_lost": (lost_word >> 24) / 256.0,
+                               "cum_lost": lost_word & 0xFFFFFF, "jitter": jitter, "lsr": lsr, "dlsr": dlsr})
+                k += 24
+            d["reports"] = blocks
         out.append(d)
         off = end
     return out

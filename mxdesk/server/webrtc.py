@@ -148,7 +148,7 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
             out_media += [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport,
                           f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtcp-rsize",
                           f"a=rtpmap:{pt} H264/90000", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
-                          f"a=rtcp-fb:{pt} ccm fir",
+                          f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb",
                           f"a=fmtp:{pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}",
                           f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
             continue
@@ -185,12 +185,45 @@ def local_ip() -> str:
         return "127.0.0.1"
 
 
+# ------------------------------------------------------------------ congestion control
+class CongestionController:
+    """``SELKIES_CONGESTION_CONTROL``: steer the encoder's CBR target from the receiver's
+    feedback -- REMB estimates (upper bound) and RTCP receiver-report loss (multiplicative
+    decrease above 10 % loss, +8 % additive-style probe below 2 %), never above the configured
+    bitrate."""
+
+    def __init__(self, pipeline, enabled: bool, min_kbps: int = 500):
+        self.pipeline = pipeline
+        self.enabled = enabled
+        self.max_kbps = int(getattr(pipeline, "bitrate_kbps", 0) or 8000)
+        self.kbps = self.max_kbps
+        self.min_kbps = min_kbps
+        self.remb_kbps: int | None = None
+
+    def _apply(self, kbps: float) -> None:
+        cap = min(self.max_kbps, self.remb_kbps or self.max_kbps)
+        new = int(max(self.min_kbps, min(cap, kbps)))
+        if self.enabled and abs(new - self.kbps) >= max(50, self.kbps // 50):
+            self.pipeline.set_bitrate(new)
+        self.kbps = new
+
+    def on_remb(self, bps: int) -> None:
+        self.remb_kbps = max(self.min_kbps, int(bps * 0.95) // 1000)
+        self._apply(self.kbps)
+
+    def on_loss(self, fraction: float) -> None:
+        if fraction > 0.10:
+            self._apply(self.kbps * (1.0 - 0.5 * fraction))
+        elif fraction < 0.02:
+            self._apply(self.kbps * 1.08)
+
+
 # ------------------------------------------------------------------ peer
 class WebRtcPeer(asyncio.DatagramProtocol):
     HISTORY = 1024
 
     def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
-                 audio=None):
+                 audio=None, congestion_control: bool = False):
         N = _native()
         self.pipeline = pipeline
         self.audio = audio
@@ -219,6 +252,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.stats = {"stun": 0, "dtls_in": 0, "rtp_out": 0, "rtcp_in": 0, "pli": 0, "nack": 0, "rtx": 0}
         self.last_consent = time.monotonic()
         self.ts0: int | None = None
+        self.cc = CongestionController(pipeline, enabled=congestion_control)
 
     async def start(self) -> str:
         loop = asyncio.get_running_loop()
@@ -300,6 +334,12 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             if p["pt"] == 206 and p["fmt"] in (1, 4):  # PLI / FIR
                 self.stats["pli"] += 1
                 self.pipeline.request_idr()
+            elif "remb_bps" in p:
+                self.cc.on_remb(p["remb_bps"])
+            elif p["pt"] in (200, 201) and p.get("reports"):
+                for rb in p["reports"]:
+                    if rb["ssrc"] == self.ssrc:
+                        self.cc.on_loss(rb["fraction_lost"])
             elif p["pt"] == 205 and p["fmt"] == 1:
                 self.stats["nack"] += 1
                 for seq in p.get("nack", []):
@@ -388,9 +428,11 @@ class WebRtcPeer(asyncio.DatagramProtocol):
 class WhepEndpoint:
     """``POST /whep`` (application/sdp offer) -> 201 answer; ``DELETE /whep/{id}``."""
 
-    def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A, audio=None):
+    def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A, audio=None,
+                 congestion_control: bool = False):
         self.pipeline = pipeline
         self.audio = audio
+        self.congestion_control = congestion_control
         self.host = host
         self.udp_port = udp_port
         self.level_idc = level_idc
@@ -404,7 +446,8 @@ class WhepEndpoint:
         from aiohttp import web
 
         offer = await request.text()
-        peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc, audio=self.audio)
+        peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc, audio=self.audio,
+                          congestion_control=self.congestion_control)
         try:
             answer = await peer.start()
         except ValueError as e:

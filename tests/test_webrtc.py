@@ -180,3 +180,40 @@ def test_whep_loopback_decodes_with_nack_and_pli(native, monkeypatch):
     idr = [i for i, au in enumerate(res.aus) if any((n[0] & 0x1F) == 5 for n in native.net.split_annexb(au))]
     assert idr[0] == 0 and any(i >= 5 for i in idr[1:])
     assert not peers  # DELETE /whep/<id> removed the session
+
+
+def test_rtcp_rr_and_remb_roundtrip():
+    rr = R.build_rr(11, 22, 0.25, cum_lost=7, ext_seq=1000)
+    (p,) = R.parse_rtcp(rr)
+    assert p["pt"] == 201 and p["reports"][0]["ssrc"] == 22 and abs(p["reports"][0]["fraction_lost"] - 0.25) < 1e-9
+    assert p["reports"][0]["cum_lost"] == 7
+    (q,) = R.parse_rtcp(R.build_remb(11, 22, 3_500_000))
+    assert q["pt"] == 206 and q["fmt"] == 15 and abs(q["remb_bps"] - 3_500_000) < 3_500_000 / 2 ** 17
+
+
+def test_congestion_controller():
+    from mxdesk.server.webrtc import CongestionController
+
+    class P:
+        bitrate_kbps = 8000
+        calls = []
+
+        def set_bitrate(self, k):
+            self.calls.append(k)
+
+    p = P()
+    cc = CongestionController(p, enabled=True)
+    cc.on_loss(0.30)  # heavy loss: multiplicative decrease
+    assert p.calls[-1] == int(8000 * 0.85)
+    cc.on_remb(2_000_000)  # receiver estimate caps the target
+    assert p.calls[-1] == 1900
+    for _ in range(30):
+        cc.on_loss(0.0)  # probing never exceeds the REMB cap / configured max
+    assert p.calls[-1] == 1900
+    cc.on_remb(50_000_000)
+    for _ in range(40):
+        cc.on_loss(0.0)
+    assert p.calls[-1] == 8000
+    off = CongestionController(P(), enabled=False)
+    off.on_loss(0.5)
+    assert off.pipeline.calls == p.calls  # disabled: no set_bitrate calls added
