@@ -50,10 +50,10 @@ struct PyBits {
 
 py::tuple cavlc_block_py(const std::vector<int>& coef, int nc) {
     PyBits b;
-    int c[16] = {0};
+    int16_t c[16] = {0};
     const int n = (int)coef.size();
     if (n != 4 && n != 15 && n != 16) throw std::invalid_argument("block must have 4, 15 or 16 coefficients");
-    for (int i = 0; i < n; ++i) c[i] = coef[i];
+    for (int i = 0; i < n; ++i) c[i] = (int16_t)coef[i];
     h264::cavlc_block(b.w, c, n, nc);
     return b.finish();
 }

@@ -268,21 +268,21 @@ MXHD int nc_table(int nC) {
 // Code one residual block with CAVLC (9.2).  `coef` holds maxNum levels in scan order.
 // Returns TotalCoeff.
 template <class W>
-MXHD int cavlc_block(W& w, const int* coef, int maxNum, int nC) {
-    int lev[16];
-    int run[16];
-    int total = 0, last = -1;
-    // gather non-zeros from highest frequency down; run[k] = zeros preceding lev[k]
-    int zeros_pending = 0;
+MXHD int cavlc_block(W& w, const int16_t* coef, int maxNum, int nC) {
+    // Streaming form (no per-block level/run arrays: on the GPU those would be dynamically
+    // indexed private arrays, i.e. scratch memory).  Three passes over coef[], highest
+    // frequency first.
+    int total = 0, last = -1, t1 = 0;
+    bool t1_open = true;
     for (int i = maxNum - 1; i >= 0; --i) {
-        int c = coef[i];
+        const int c = coef[i];
         if (c != 0) {
             if (last < 0) last = i;
-            if (total > 0) run[total - 1] = zeros_pending;
-            lev[total++] = c;
-            zeros_pending = 0;
-        } else if (last >= 0) {
-            ++zeros_pending;
+            if (t1_open) {
+                if ((c == 1 || c == -1) && t1 < 3) ++t1;
+                else t1_open = false;
+            }
+            ++total;
         }
     }
     const int tab = nc_table(nC);
@@ -290,17 +290,21 @@ MXHD int cavlc_block(W& w, const int* coef, int maxNum, int nC) {
         w.put(kCoeffToken0[tab].code, kCoeffToken0[tab].len);
         return 0;
     }
-    run[total - 1] = zeros_pending;  // zeros below the lowest-frequency coefficient
-    int t1 = 0;
-    while (t1 < total && t1 < 3 && (lev[t1] == 1 || lev[t1] == -1)) ++t1;
     const Vlc ct = kCoeffToken[tab][total - 1][t1];
     w.put(ct.code, ct.len);
-    for (int i = 0; i < t1; ++i) w.put(lev[i] < 0 ? 1u : 0u, 1);
+    // trailing-one signs, then levels
     int sl = (total > 10 && t1 < 3) ? 1 : 0;
-    for (int i = t1; i < total; ++i) {
-        int l = lev[i];
+    int k = 0;
+    for (int i = last; i >= 0; --i) {
+        const int l = coef[i];
+        if (l == 0) continue;
+        if (k < t1) {
+            w.put(l < 0 ? 1u : 0u, 1);
+            ++k;
+            continue;
+        }
         int code = l > 0 ? 2 * l - 2 : -2 * l - 1;
-        if (i == t1 && t1 < 3) code -= 2;
+        if (k == t1 && t1 < 3) code -= 2;
         if (sl == 0) {
             if (code < 14) {
                 w.put(1, code + 1);
@@ -321,20 +325,28 @@ MXHD int cavlc_block(W& w, const int* coef, int maxNum, int nC) {
             }
         }
         if (sl == 0) sl = 1;
-        int a = l < 0 ? -l : l;
+        const int a = l < 0 ? -l : l;
         if (a > (3 << (sl - 1)) && sl < 6) ++sl;
+        ++k;
     }
     const int total_zeros = last + 1 - total;
     if (total < maxNum) {
         const Vlc tz = (maxNum == 4) ? kTotalZerosDc[total - 1][total_zeros] : kTotalZeros[total - 1][total_zeros];
         w.put(tz.code, tz.len);
     }
+    // run_before: zeros directly below each non-zero (highest first), except the lowest one
     int zl = total_zeros;
-    for (int i = 0; i < total - 1 && zl > 0; ++i) {
-        const int rb = run[i];
+    int i = last;
+    for (int seen = 0; seen < total - 1 && zl > 0; ++seen) {
+        int j = i - 1, rb = 0;
+        while (coef[j] == 0) {
+            ++rb;
+            --j;
+        }
         const Vlc v = kRunBefore[(zl > 7 ? 7 : zl) - 1][rb];
         w.put(v.code, v.len);
         zl -= rb;
+        i = j;
     }
     return total;
 }

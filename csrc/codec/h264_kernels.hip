@@ -39,14 +39,14 @@ struct OrWriter {
     int nacc;
     uint32_t bits;
 
-    __device__ void init(uint32_t* d, uint32_t bitpos) {
+    __device__ __forceinline__ void init(uint32_t* d, uint32_t bitpos) {
         dst = d;
         pos = bitpos;
         acc = 0;
         nacc = 0;
         bits = 0;
     }
-    __device__ void emit(uint32_t w, int n) {  // w: n valid bits left-aligned
+    __device__ __forceinline__ void emit(uint32_t w, int n) {  // w: n valid bits left-aligned
         const uint32_t wi = pos >> 5, sh = pos & 31;
         uint32_t a = w >> sh;
         if (a) atomicOr(dst + wi, kSwap ? bswap32(a) : a);
@@ -56,7 +56,7 @@ struct OrWriter {
         }
         pos += n;
     }
-    __device__ void put(uint32_t v, int n) {
+    __device__ __forceinline__ void put(uint32_t v, int n) {
         if (n <= 0) return;
         uint64_t m = (n == 32) ? 0xffffffffull : ((1ull << n) - 1);
         acc = (acc << n) | (v & m);
@@ -67,7 +67,7 @@ struct OrWriter {
             nacc -= 32;
         }
     }
-    __device__ void flush() {
+    __device__ __forceinline__ void flush() {
         if (nacc > 0) {
             emit((uint32_t)(acc << (32 - nacc)), nacc);
             nacc = 0;
@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     if (mbi >= nmb) return;  // whole wave exits together; no workgroup barrier below
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
     const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
-    const MbInfo m = mbs[mbi];
+    const MbInfo& m = mbs[mbi];  // by reference: a private copy with dynamically indexed nz arrays spills to scratch
     const int16_t* mc = coef + (size_t)mbi * kCoefStride;
 
     // motion vector prediction + P_Skip decision (every lane computes the same values)

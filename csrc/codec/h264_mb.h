@@ -87,12 +87,10 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mb
         }
         return;
     }
-    int c[16];
     if (role == 1) {
         if (!intra) return;
         const int nc = combine_nc(av.left, ml ? ml->nz_luma[3] : 0, av.top, mt ? mt->nz_luma[12] : 0);
-        for (int k = 0; k < 16; ++k) c[k] = mc[kCoefLumaDc + k];
-        cavlc_block(w, c, 16, nc);
+        cavlc_block(w, mc + kCoefLumaDc, 16, nc);
         return;
     }
     if (role <= 17) {
@@ -104,19 +102,16 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mb
         const int nb = by > 0 ? m.nz_luma[(by - 1) * 4 + bx] : (mt ? mt->nz_luma[12 + bx] : 0);
         const int nc = combine_nc(ha, na, hb, nb);
         if (intra) {
-            for (int k = 0; k < 15; ++k) c[k] = mc[kCoefLuma + b * 16 + 1 + k];
-            cavlc_block(w, c, 15, nc);
+            cavlc_block(w, mc + kCoefLuma + b * 16 + 1, 15, nc);  // AC only (DC in the Intra16x16 DC block)
         } else {
-            for (int k = 0; k < 16; ++k) c[k] = mc[kCoefLuma + b * 16 + k];
-            cavlc_block(w, c, 16, nc);
+            cavlc_block(w, mc + kCoefLuma + b * 16, 16, nc);
         }
         return;
     }
     if (role <= 19) {
         if (!cbp_c) return;
         const int comp = role - 18;
-        for (int k = 0; k < 4; ++k) c[k] = mc[kCoefChromaDc + comp * 4 + k];
-        cavlc_block(w, c, 4, -1);
+        cavlc_block(w, mc + kCoefChromaDc + comp * 4, 4, -1);
         return;
     }
     if (role < kNumRoles) {
@@ -129,8 +124,7 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mb
         const int na = bx > 0 ? own[by * 2] : (lft ? lft[by * 2 + 1] : 0);
         const int nb = by > 0 ? own[bx] : (top ? top[2 + bx] : 0);
         const int nc = combine_nc(ha, na, hb, nb);
-        for (int k = 0; k < 15; ++k) c[k] = mc[kCoefChromaAc + (comp * 4 + cb) * 16 + 1 + k];
-        cavlc_block(w, c, 15, nc);
+        cavlc_block(w, mc + kCoefChromaAc + (comp * 4 + cb) * 16 + 1, 15, nc);
     }
 }
 
