@@ -40,6 +40,8 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--fps", type=int, default=60)
+    ap.add_argument("--out-width", type=int, default=0, help="encode width (0 = desktop width; else fused Lanczos-3 + CSC)")
+    ap.add_argument("--out-height", type=int, default=0)
     ap.add_argument("--bitrate-kbps", type=int, default=8000)
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
@@ -72,6 +74,7 @@ def main() -> None:
     N.set_device(local_rank)
     cfg = N.SessionConfig()
     cfg.width, cfg.height, cfg.fps = args.width, args.height, args.fps
+    cfg.out_width, cfg.out_height = args.out_width, args.out_height
     cfg.enc.bitrate_kbps = args.bitrate_kbps
     cfg.enc.search_range = args.search_range
     cfg.enc.subpel = args.subpel
@@ -163,7 +166,9 @@ def main() -> None:
             "dtype": "uint8 video (8-bit 4:2:0), H.264 Constrained Baseline",
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",
             "config": {
-                "model": f"{args.width}x{args.height}@{args.fps} H.264 desktop session (mxh264enc, CBR "
+                "model": f"{args.width}x{args.height}@{args.fps} H.264 desktop session"
+                         + (f" scaled to {args.out_width}x{args.out_height}" if args.out_width else "")
+                         + " (mxh264enc, CBR "
                          f"{args.bitrate_kbps} kbps, ME +/-{args.search_range} qpel={args.subpel})",
                 "global_batch": world * K,
                 "seq_len": args.width * args.height,
