@@ -123,7 +123,7 @@ def _has_pcmu(md: MediaDesc) -> bool:
 
 
 def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
-                 level_idc: int = 0x2A, audio_ssrc: int | None = None) -> Answer:
+                 level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None) -> Answer:
     """Answer one H.264 video section (and, with ``audio_ssrc``, one PCMU audio section);
     everything else is rejected with port 0.  All accepted sections are BUNDLEd onto the
     single ICE-lite host candidate."""
@@ -134,7 +134,9 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
     chosen = None
     audio = None  # (pt, mid)
     bundle: list[str] = []
-    transport = [f"c=IN IP4 {host}", f"a=candidate:1 1 udp 2130706431 {host} {port} typ host", "a=end-of-candidates",
+    hosts = [host] + [h for h in (extra_hosts or []) if h != host]
+    cands = [f"a=candidate:{k + 1} 1 udp {2130706431 - k} {h} {port} typ host" for k, h in enumerate(hosts)]
+    transport = [f"c=IN IP4 {host}", *cands, "a=end-of-candidates",
                  f"a=ice-ufrag:{ice_ufrag}", f"a=ice-pwd:{ice_pwd}", f"a=fingerprint:{fingerprint}", "a=setup:passive"]
     for md in offer.media:
         mid = md.attr("mid") or str(len(bundle) + len(out_media))
@@ -169,6 +171,18 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
     lines.insert(4, "a=group:BUNDLE " + " ".join(bundle))
     chosen.sdp = "\r\n".join(lines + out_media) + "\r\n"
     return chosen
+
+
+def local_ips() -> list[str]:
+    """Non-loopback IPv4 addresses of this host (one ICE host candidate each)."""
+    try:
+        import psutil
+
+        out = [a.address for addrs in psutil.net_if_addrs().values() for a in addrs
+               if a.family == socket.AF_INET and not a.address.startswith("127.")]
+        return sorted(set(out))
+    except Exception:
+        return []
 
 
 def local_ip() -> str:
@@ -235,7 +249,11 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.pwd = secrets.token_hex(16)
         self.dtls = N.net.DtlsEndpoint(True)
         self.ssrc = secrets.randbits(32) | 1
-        self.host = host or local_ip()
+        explicit = host or os.environ.get("MXDESK_WEBRTC_HOST")
+        self.host = explicit or local_ip()
+        # no explicit host: listen on all interfaces and offer every address as a candidate
+        self.bind_host = self.host if explicit else "0.0.0.0"
+        self.extra_hosts = [] if explicit else local_ips()
         self.bind_port = port
         self.level_idc = level_idc
         self.offer_sdp = offer_sdp
@@ -256,10 +274,11 @@ class WebRtcPeer(asyncio.DatagramProtocol):
 
     async def start(self) -> str:
         loop = asyncio.get_running_loop()
-        self.transport, _ = await loop.create_datagram_endpoint(lambda: self, local_addr=(self.host, self.bind_port))
+        self.transport, _ = await loop.create_datagram_endpoint(lambda: self,
+                                                                local_addr=(self.bind_host, self.bind_port))
         port = self.transport.get_extra_info("sockname")[1]
         self.answer = build_answer(self.offer_sdp, self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port,
-                                   self.ssrc, self.level_idc, self.audio_ssrc)
+                                   self.ssrc, self.level_idc, self.audio_ssrc, self.extra_hosts)
         self.pkt = _native().net.RtpH264Packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
         self.tasks.append(asyncio.create_task(self._timers()))
         return self.answer.sdp

@@ -217,3 +217,11 @@ def test_congestion_controller():
     off = CongestionController(P(), enabled=False)
     off.on_loss(0.5)
     assert off.pipeline.calls == p.calls  # disabled: no set_bitrate calls added
+
+
+def test_answer_lists_every_host_candidate():
+    offer = make_offer("abcd", "p" * 24, "sha-256 AA:BB")
+    a = build_answer(offer, "uf", "pw" * 12, "sha-256 CC:DD", "10.0.0.5", 5000, 42, extra_hosts=["10.0.0.5", "192.168.1.9"])
+    v = parse_sdp(a.sdp).media[0]
+    cands = v.attrs_named("candidate")
+    assert [c.split()[4] for c in cands] == ["10.0.0.5", "192.168.1.9"] and all(c.split()[5] == "5000" for c in cands)

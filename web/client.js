@@ -140,7 +140,10 @@ const mxdesk = (() => {
   }
 
   async function whep(video) {
-    const pc = new RTCPeerConnection({ iceServers: [] });
+    // RTC configuration (STUN/TURN with time-limited credentials) from the server's /turn
+    let iceServers = [];
+    try { iceServers = (await (await fetch("turn")).json()).iceServers || []; } catch (e) { /* no TURN */ }
+    const pc = new RTCPeerConnection({ iceServers });
     pc.addTransceiver("video", { direction: "recvonly" });
     pc.addTransceiver("audio", { direction: "recvonly" });
     const audioEl = new Audio();
