@@ -456,6 +456,7 @@ class WhepEndpoint:
         self.udp_port = udp_port
         self.level_idc = level_idc
         self.peers: dict[str, WebRtcPeer] = {}
+        self.last_peer: WebRtcPeer | None = None
 
     def routes(self, app) -> None:
         app.router.add_post("/whep", self.post)
@@ -473,6 +474,7 @@ class WhepEndpoint:
             peer.close()
             raise web.HTTPBadRequest(text=str(e))
         self.peers[peer.id] = peer
+        self.last_peer = peer
         return web.Response(status=201, text=answer, content_type="application/sdp",
                             headers={"Location": f"/whep/{peer.id}"})
 

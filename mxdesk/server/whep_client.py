@@ -50,6 +50,7 @@ class WhepResult:
     answer: str = ""
     connect_ms: float = 0.0
     stream: bytes = b""
+    arrival_us: list[int] = field(default_factory=list)  # CLOCK_MONOTONIC us when each AU completed
     audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
     audio_seqs: list[int] = field(default_factory=list)
 
@@ -184,6 +185,7 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                 if au is not None:
                     res.aus.append(au)
                     res.rtp_ts.append(R.rtp_header(pk)["ts"])
+                    res.arrival_us.append(time.monotonic_ns() // 1000)
                     if pli_after and len(res.aus) == pli_after and not sent_pli:
                         tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
                         sent_pli = True
