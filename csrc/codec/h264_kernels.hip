@@ -153,6 +153,32 @@ __global__ __launch_bounds__(256) void k_hpel(Geometry g, const FrameState* __re
     }
 }
 
+// Quarter-sample luma value from an LDS-staged 18x18 footprint of the four planes
+// (sp[0] F, sp[1] H, sp[2] V, sp[3] J; local origin one sample up-left of the integer
+// match); exactly qpel_planes() on the same samples.
+constexpr int kSpW = 20;
+__device__ __forceinline__ int qpel_lds(const uint8_t (*sp)[18][kSpW], int x4, int y4) {
+    const int xi = x4 >> 2, yi = y4 >> 2, xf = x4 & 3, yf = y4 & 3;
+    const int G = sp[0][yi][xi];
+    if ((xf | yf) == 0) return G;
+    if (yf == 0) {
+        const int b = sp[1][yi][xi];
+        if (xf == 2) return b;
+        return ((xf == 1 ? G : (int)sp[0][yi][xi + 1]) + b + 1) >> 1;
+    }
+    if (xf == 0) {
+        const int hh = sp[2][yi][xi];
+        if (yf == 2) return hh;
+        return ((yf == 1 ? G : (int)sp[0][yi + 1][xi]) + hh + 1) >> 1;
+    }
+    if (xf == 2 && yf == 2) return sp[3][yi][xi];
+    if (xf == 2) return ((yf == 1 ? (int)sp[1][yi][xi] : (int)sp[1][yi + 1][xi]) + sp[3][yi][xi] + 1) >> 1;
+    if (yf == 2) return ((xf == 1 ? (int)sp[2][yi][xi] : (int)sp[2][yi][xi + 1]) + sp[3][yi][xi] + 1) >> 1;
+    const int bb = (yf == 1) ? sp[1][yi][xi] : sp[1][yi + 1][xi];
+    const int hh = (xf == 1) ? sp[2][yi][xi] : sp[2][yi][xi + 1];
+    return (bb + hh + 1) >> 1;
+}
+
 // ------------------------------------------------------------------ motion estimation
 constexpr int kMaxRange = 32;
 static_assert(kMaxRange + 2 <= kHpelPad, "search window must stay inside the padded planes");
@@ -239,21 +265,34 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     int mvx = 4 * ((cbest % side) - R), mvy = 4 * ((cbest / side) - R);
 
     if (fs->subpel) {
-        // half-pel then quarter-pel: the 8 neighbours of a step are scored at once, one per
-        // 32-lane half-wave group; each lane sums 8 pixels, a 5-step xor shuffle reduces the
-        // group, then one barrier publishes the 8 costs.
+        // half-pel then quarter-pel around the integer match.  Every candidate of both steps
+        // lies in one 18x18 footprint of the F/H/V/J planes (the integer match +-1 sample),
+        // staged into LDS once with independent byte loads; the 8 neighbours of a step are
+        // scored at once, one per 32-lane half-wave group (8 pixels per lane, source from
+        // srcw), a 5-step xor shuffle reduces each group, one barrier publishes the costs.
+        __shared__ uint8_t sp[4][18][kSpW];
+        const int ix = x0 + (mvx >> 2) - 1, iy = y0 + (mvy >> 2) - 1;
+        for (int i = tid; i < 4 * 18 * 18; i += 256) {
+            const int pl = i / 324, rem = i - pl * 324, r = rem / 18, c = rem - r * 18;
+            const uint8_t* base = pl == 0 ? P.f : pl == 1 ? P.h : pl == 2 ? P.v : P.j;
+            sp[pl][r][c] = base[(iy + r) * P.pitch + ix + c];
+        }
+        __syncthreads();
         uint32_t cur_cost = (uint32_t)(b >> 32);
         const int k = tid >> 5, sub = tid & 31;
         const int py = sub >> 1, px0 = (sub & 1) * 8;
-        const uint8_t* srow = src_y + (y0 + py) * g.pitch + x0 + px0;
+        const uint32_t s0 = srcw[py * 4 + (px0 >> 2)], s1 = srcw[py * 4 + (px0 >> 2) + 1];
+        const int base_x4 = px0 * 4 + 4 - mvx, base_y4 = py * 4 + 4 - mvy;  // local qpel coords = base + candidate mv
         for (int step = 2; step >= 1; step >>= 1) {
             int ddx, ddy;
             subpel_offset(k, &ddx, &ddy);
             const int cx = mvx + ddx * step, cy = mvy + ddy * step;
             int d = 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                d += abs((int)srow[j] - qpel_planes(P, (x0 + px0 + j) * 4 + cx, (y0 + py) * 4 + cy));
+            for (int j = 0; j < 8; ++j) {
+                const int sv = (int)(((j < 4 ? s0 : s1) >> (8 * (j & 3))) & 0xff);
+                d += abs(sv - qpel_lds(sp, base_x4 + 4 * j + cx, base_y4 + cy));
+            }
             for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
             __syncthreads();  // previous step's readers are done with cand_cost
             if (sub == 0) cand_cost[k] = me_cost((uint32_t)d, lambda, cx, cy);
