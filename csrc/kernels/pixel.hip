@@ -259,7 +259,7 @@ constexpr int kTileW = 64, kTileH = 16;
 __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict__ in, int in_pitch, int in_w,
                                                        int in_h, LanczosTables t, uint8_t* __restrict__ yp,
                                                        uint8_t* __restrict__ uvp, int out_pitch, int coded_w,
-                                                       int coded_h, int max_nc) {
+                                                       int coded_h, int max_nc, int max_nr) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int ox0 = blockIdx.x * kTileW, oy0 = blockIdx.y * kTileH;
     const int tid = threadIdx.x;
@@ -268,25 +268,40 @@ __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict
     const int xlo = t.x0[oxf], xhi = t.x0[oxl] + t.taps_x - 1;
     const int ylo = t.y0[oyf], yhi = t.y0[oyl] + t.taps_y - 1;
     const int nc = xhi - xlo + 1, nr = yhi - ylo + 1;
-    // LDS: input footprint [nr][max_nc] BGRx, then horizontal result [nr][kTileW] x RGB float
+    const int tx = t.taps_x, ty = t.taps_y;
+    // LDS: input footprint [nr][max_nc] BGRx | horizontal result [nr][kTileW] x RGB float |
+    //      this tile's filter weights [kTileW][tx] + [kTileH][ty] and first-tap offsets
     uint32_t* lin = reinterpret_cast<uint32_t*>(smem);
-    float* hr = reinterpret_cast<float*>(smem + (((size_t)nr * max_nc * 4 + 15) & ~(size_t)15));
-    float* hg = hr + nr * kTileW;
-    float* hb = hg + nr * kTileW;
+    float* hr = reinterpret_cast<float*>(smem + (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15));
+    float* hg = hr + max_nr * kTileW;
+    float* hb = hg + max_nr * kTileW;
+    float* wxs = hb + max_nr * kTileW;
+    float* wys = wxs + kTileW * tx;
+    int* bx = reinterpret_cast<int*>(wys + kTileH * ty);
+    int* by = bx + kTileW;
     for (int i = tid; i < nr * nc; i += 256) {
         const int r = i / nc, c = i - r * nc;
         const int sy = min(max(ylo + r, 0), in_h - 1), sx = min(max(xlo + c, 0), in_w - 1);
         lin[r * max_nc + c] = *reinterpret_cast<const uint32_t*>(in + (size_t)sy * in_pitch + sx * 4);
     }
+    for (int i = tid; i < kTileW * tx; i += 256) {
+        const int c = i / tx, k = i - c * tx;
+        wxs[i] = t.wx[(size_t)min(ox0 + c, t.out_w - 1) * tx + k];
+    }
+    for (int i = tid; i < kTileH * ty; i += 256) {
+        const int r = i / ty, k = i - r * ty;
+        wys[i] = t.wy[(size_t)min(oy0 + r, t.out_h - 1) * ty + k];
+    }
+    if (tid < kTileW) bx[tid] = t.x0[min(ox0 + tid, t.out_w - 1)] - xlo;
+    if (tid < kTileH) by[tid] = t.y0[min(oy0 + tid, t.out_h - 1)] - ylo;
     __syncthreads();
     for (int i = tid; i < nr * kTileW; i += 256) {
         const int r = i / kTileW, c = i - r * kTileW;
-        const int ox = min(ox0 + c, t.out_w - 1);
-        const int base = t.x0[ox] - xlo;
-        const float* w = t.wx + (size_t)ox * t.taps_x;
+        const uint32_t* src = lin + r * max_nc + bx[c];
+        const float* w = wxs + c * tx;
         float R = 0.f, G = 0.f, B = 0.f;
-        for (int k = 0; k < t.taps_x; ++k) {
-            const uint32_t v = lin[r * max_nc + base + k];
+        for (int k = 0; k < tx; ++k) {
+            const uint32_t v = src[k];
             const float wk = w[k];
             B += wk * (float)(v & 0xff);
             G += wk * (float)((v >> 8) & 0xff);
@@ -301,18 +316,18 @@ __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict
     int Rq[2][2], Gq[2][2], Bq[2][2];
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
-        const int oy = min(oy0 + ly + dy, t.out_h - 1);
-        const int base = t.y0[oy] - ylo;
-        const float* w = t.wy + (size_t)oy * t.taps_y;
+        const int base = by[ly + dy];
+        const float* w = wys + (ly + dy) * ty;
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
             const int c = lx + dx;
             float R = 0.f, G = 0.f, B = 0.f;
-            for (int k = 0; k < t.taps_y; ++k) {
+            for (int k = 0; k < ty; ++k) {
                 const float wk = w[k];
-                R += wk * hr[(base + k) * kTileW + c];
-                G += wk * hg[(base + k) * kTileW + c];
-                B += wk * hb[(base + k) * kTileW + c];
+                const int o = (base + k) * kTileW + c;
+                R += wk * hr[o];
+                G += wk * hg[o];
+                B += wk * hb[o];
             }
             Rq[dy][dx] = min(max((int)lrintf(R), 0), 255);
             Gq[dy][dx] = min(max((int)lrintf(G), 0), 255);
@@ -380,7 +395,8 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     const float sx = (float)in_w / t.out_w, sy = (float)in_h / t.out_h;
     const int max_nc = (int)ceilf(sx * kTileW) + t.taps_x + 2;
     const int max_nr = (int)ceilf(sy * kTileH) + t.taps_y + 2;
-    const size_t lds = (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15) + (size_t)max_nr * kTileW * 12;
+    const size_t lds = (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15) + (size_t)max_nr * kTileW * 12 +
+                       (size_t)(kTileW * t.taps_x + kTileH * t.taps_y) * 4 + (kTileW + kTileH) * 4;
     if (lds > 160 * 1024) throw std::runtime_error("scale_to_nv12: scale factor too large for one LDS tile");
     if (lds > 64 * 1024) {
         static bool raised = false;
@@ -392,7 +408,7 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     }
     dim3 grid((coded_w + kTileW - 1) / kTileW, (coded_h + kTileH - 1) / kTileH);
     hipLaunchKernelGGL(k_scale_to_nv12, grid, dim3(256), lds, stream, bgrx, in_pitch, in_w, in_h, t, y, uv, out_pitch,
-                       coded_w, coded_h, max_nc);
+                       coded_w, coded_h, max_nc, max_nr);
 }
 
 void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,
