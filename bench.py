@@ -46,6 +46,8 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
+    ap.add_argument("--depth", type=int, default=1,
+                    help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1)")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
@@ -80,19 +82,25 @@ def main() -> None:
     cfg.enc.subpel = args.subpel
     cfg.noise = args.noise
     cfg.use_graph = args.graph
+    cfg.enc.pipeline_depth = args.depth
     K = max(1, args.sessions_per_gpu)
     sessions = [N.Session(cfg) for _ in range(K)]
 
     def run(n_frames: int, record: bool):
-        """n_frames per session; K sessions interleaved, one frame in flight each."""
+        """n_frames per session; K sessions interleaved, up to `depth` frames in flight each."""
         out = []
-        for s in sessions:
-            s.submit(False)
-        for i in range(n_frames):
-            for s in sessions:
+        depth = max(1, args.depth)
+        sent = [0] * K
+        for k, s in enumerate(sessions):
+            while sent[k] < min(depth, n_frames):
+                s.submit(False)
+                sent[k] += 1
+        for _ in range(n_frames):
+            for k, s in enumerate(sessions):
                 r = s.collect()
-                if i + 1 < n_frames:
+                if sent[k] < n_frames:
                     s.submit(False)
+                    sent[k] += 1
                 if record:
                     out.append(r)
         return out
@@ -108,7 +116,7 @@ def main() -> None:
     barrier()
     t0 = time.perf_counter()
     lat_ms, sizes, qps, gpu_ms, psnrs = [], [], [], [], []
-    if K == 1:
+    if K == 1 and args.depth == 1:
         results = [sessions[0].step(False) for _ in range(args.steps)]
     else:
         results = run(args.steps, True)
@@ -158,6 +166,7 @@ def main() -> None:
             "encoded_fps_per_gpu": round(per_gpu, 2),
             "sessions_per_gpu": K,
             "hip_graph": bool(args.graph),
+            "pipeline_depth": args.depth,
             "sessions_per_node_at_60fps": int(fps_total // 60),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),

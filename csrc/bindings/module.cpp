@@ -134,7 +134,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("keyint", &h264::EncoderConfig::keyint)
         .def_readwrite("search_range", &h264::EncoderConfig::search_range)
         .def_readwrite("subpel", &h264::EncoderConfig::subpel)
-        .def_readwrite("chroma_qp_offset", &h264::EncoderConfig::chroma_qp_offset);
+        .def_readwrite("chroma_qp_offset", &h264::EncoderConfig::chroma_qp_offset)
+        .def_readwrite("pipeline_depth", &h264::EncoderConfig::pipeline_depth);
 
     py::class_<h264::FrameStats>(m, "FrameStats")
         .def_readonly("frame_index", &h264::FrameStats::frame_index)
@@ -372,6 +373,8 @@ PYBIND11_MODULE(_native, m) {
         .def_property_readonly("nv12_uv_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_uv()); })
         .def_property_readonly("nv12_pitch", &Session::nv12_pitch)
         .def_property_readonly("graphs_built", &Session::graphs_built)
+        .def_property_readonly("in_flight", &Session::in_flight)
+        .def_property_readonly("depth", &Session::depth)
         .def("nv12",
              [](Session& s) {
                  const auto& g = s.encoder().geometry();

@@ -389,13 +389,14 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     if (common_.cur_idr()) common_.write_parameter_sets(au_);
     int skipped = 0;
     for (const MbInfo& m : mb_) skipped += m.skip;
-    for (size_t s = 0; s < soff.size(); ++s) common_.write_slice_nal(au_, payload.data() + soff[s], slen[s]);
+    for (size_t s = 0; s < soff.size(); ++s)
+        common_.write_slice_nal(au_, payload.data() + soff[s], slen[s], common_.cur_idr());
     stats_.frame_index = common_.frames();
     stats_.idr = common_.cur_idr();
     stats_.qp = common_.cur_qp();
     stats_.bytes = (int)au_.size();
     stats_.skipped_mbs = skipped;
-    common_.end_frame((int)au_.size());
+    common_.end_frame((int)au_.size(), common_.cur_idr());
     have_ref_ = true;
     return au_;
 }

@@ -25,32 +25,34 @@ EncoderCommon::EncoderCommon(const EncoderConfig& c) : cfg_(c) {
 }
 
 void EncoderCommon::begin_frame(bool force_idr) {
-    const bool idr = idr_requested_ || force_idr || frame_index_ == 0 ||
-                     (cfg_.keyint > 0 && since_idr_ >= cfg_.keyint);
+    // frame counters advance here (not in end_frame) so that a second frame can be begun
+    // before the first one is finished (pipelined GPU encode)
+    const bool idr = idr_requested_ || force_idr || begun_ == 0 || (cfg_.keyint > 0 && since_idr_ >= cfg_.keyint);
     cur_idr_ = idr;
     idr_requested_ = false;
+    ++begun_;
     if (idr) {
         frame_num_ = 0;
         idr_pic_id_ = (idr_pic_id_ + 1) & 0xffff;
-        since_idr_ = 0;
+        since_idr_ = 1;
     } else {
         frame_num_ = (frame_num_ + 1) % (1 << log2_max_frame_num());
+        ++since_idr_;
     }
     int q = (int)std::lround(rc_qp_);
     if (cfg_.bitrate_kbps > 0) q = std::clamp(q, cfg_.qp_min, cfg_.qp_max);
     cur_qp_ = std::clamp(q, 0, 51);
 }
 
-void EncoderCommon::end_frame(int bytes) {
+void EncoderCommon::end_frame(int bytes, bool idr) {
     ++frame_index_;
-    ++since_idr_;
     if (cfg_.bitrate_kbps <= 0) return;
     const double target = cfg_.bitrate_kbps * 1000.0 / std::max(1, cfg_.fps);
     const double bits = bytes * 8.0;
     vbv_fill_ = std::max(0.0, vbv_fill_ + bits - target);
     // cap the virtual buffer at ~0.5 s so a burst cannot pin the QP forever
     vbv_fill_ = std::min(vbv_fill_, target * std::max(1, cfg_.fps) * 0.5);
-    if (cur_idr_) return;  // I frames are expected to be large; steer on P frames
+    if (idr) return;  // I frames are expected to be large; steer on P frames
     const double ratio = (bits + 0.25 * vbv_fill_ + 1.0) / target;
     const double step = std::clamp(6.0 * std::log2(ratio) * 0.25, -1.0, 1.5);
     rc_qp_ = std::clamp(rc_qp_ + step, (double)cfg_.qp_min, (double)cfg_.qp_max);
@@ -103,16 +105,58 @@ void EncoderCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
     emulation_prevent(out, rbsp.data(), rbsp.size());
 }
 
-void EncoderCommon::write_slice_nal(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n) const {
+void EncoderCommon::write_slice_nal(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n, bool idr) const {
     static const uint8_t sc[4] = {0, 0, 0, 1};
     out.insert(out.end(), sc, sc + 4);
-    out.push_back(cur_idr_ ? 0x65 : 0x41);  // IDR slice (ref_idc 3) / non-IDR slice (ref_idc 2)
+    out.push_back(idr ? 0x65 : 0x41);  // IDR slice (ref_idc 3) / non-IDR slice (ref_idc 2)
     emulation_prevent(out, rbsp, n);
 }
 
 // ------------------------------------------------------------------ GpuH264Encoder
+void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
+    const int nmb = geom_.mb_w * geom_.mb_h;
+    DeviceBuffers& b = sl.buf;
+    HIP_CHECK(hipMalloc(&b.fs, sizeof(FrameState)));
+    HIP_CHECK(hipMalloc(&b.mb, sizeof(MbInfo) * nmb));
+    HIP_CHECK(hipMemsetAsync(b.mb, 0, sizeof(MbInfo) * nmb, stream_));
+    HIP_CHECK(hipMalloc(&b.coef, sizeof(int16_t) * kCoefStride * nmb));
+    HIP_CHECK(hipMalloc(&b.slot, sizeof(uint32_t) * kSlotWords * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.slot_bits, sizeof(uint32_t) * nmb));
+    HIP_CHECK(hipMalloc(&b.unit_off, sizeof(uint32_t) * nmb));
+    HIP_CHECK(hipMalloc(&b.skip_run, sizeof(int32_t) * nmb));
+    HIP_CHECK(hipMalloc(&b.coded_list, sizeof(uint32_t) * nmb));
+    HIP_CHECK(hipMalloc(&b.coded_info, sizeof(uint4) * nmb));
+    HIP_CHECK(hipMalloc(&b.slice_info, sizeof(uint32_t) * kSliceInfo * kMaxSlices));
+    HIP_CHECK(hipMemsetAsync(b.slice_info, 0, sizeof(uint32_t) * kSliceInfo * kMaxSlices, stream_));
+    // payload capacity: 768 B per MB (intra at low QP stays far below)
+    b.out_bytes = (size_t)nmb * 768;
+    HIP_CHECK(hipMalloc(&b.out_hdr, sizeof(OutHeader)));
+    HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * kSsePartStride));
+    HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
+    std::memset(sl.host_out, 0, kOutPayloadOffset);
+    HIP_CHECK(hipEventCreate(&sl.start));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreate(&sl.done));
+}
+
+void GpuH264Encoder::free_slot(FrameSlot& sl) {
+    DeviceBuffers& b = sl.buf;
+    for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.unit_off,
+                    (void*)b.skip_run, (void*)b.coded_list, (void*)b.coded_info, (void*)b.slice_info,
+                    (void*)b.out_hdr, (void*)b.sse_part})
+        if (p) (void)hipFree(p);
+    if (sl.fs_host) (void)hipHostFree(sl.fs_host);
+    if (sl.host_out) (void)hipHostFree(sl.host_out);
+    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.done})
+        if (e) (void)hipEventDestroy(e);
+}
+
 GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     : cfg_(cfg), common_(cfg), stream_(stream) {
+    if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
+        throw std::invalid_argument("pipeline_depth must be 1 or 2");
+    depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;
     geom_.height = cfg.height;
     geom_.mb_w = common_.mb_w();
@@ -122,6 +166,7 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     geom_.pitch = (geom_.coded_w + 255) & ~255;
     if (geom_.mb_h > kMaxSlices) throw std::invalid_argument("picture too tall");
     const int nmb = geom_.mb_w * geom_.mb_h;
+    if ((nmb + 3) / 4 > kSsePartStride) throw std::invalid_argument("frame too large for the distortion partials");
     const size_t ysz = (size_t)geom_.pitch * geom_.coded_h, uvsz = ysz / 2;
     for (int i = 0; i < 2; ++i) {
         HIP_CHECK(hipMalloc(&rec_y_[i], ysz));
@@ -132,76 +177,59 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     hp_pitch_ = (geom_.coded_w + 2 * kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
-    HIP_CHECK(hipMalloc(&buf_.fs, sizeof(FrameState)));
-    HIP_CHECK(hipMalloc(&buf_.mb, sizeof(MbInfo) * nmb));
-    HIP_CHECK(hipMemsetAsync(buf_.mb, 0, sizeof(MbInfo) * nmb, stream_));
-    HIP_CHECK(hipMalloc(&buf_.coef, sizeof(int16_t) * kCoefStride * nmb));
-    HIP_CHECK(hipMalloc(&buf_.slot, sizeof(uint32_t) * kSlotWords * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&buf_.slot_bits, sizeof(uint32_t) * nmb));
-    HIP_CHECK(hipMalloc(&buf_.unit_off, sizeof(uint32_t) * nmb));
-    HIP_CHECK(hipMalloc(&buf_.skip_run, sizeof(int32_t) * nmb));
-    HIP_CHECK(hipMalloc(&buf_.coded_list, sizeof(uint32_t) * nmb));
-    HIP_CHECK(hipMalloc(&buf_.coded_info, sizeof(uint4) * nmb));
-    HIP_CHECK(hipMalloc(&buf_.slice_info, sizeof(uint32_t) * kSliceInfo * kMaxSlices));
-    HIP_CHECK(hipMemsetAsync(buf_.slice_info, 0, sizeof(uint32_t) * kSliceInfo * kMaxSlices, stream_));
-    // payload capacity: 768 B per MB (intra at low QP stays far below)
-    buf_.out_bytes = (size_t)nmb * 768;
-    HIP_CHECK(hipMalloc(&buf_.out_hdr, sizeof(OutHeader)));
-    if ((nmb + 3) / 4 > kSsePartStride) throw std::invalid_argument("frame too large for the distortion partials");
-    HIP_CHECK(hipMalloc(&buf_.sse_part, 3 * sizeof(unsigned long long) * kSsePartStride));
-    HIP_CHECK(hipHostMalloc(&fs_host_, sizeof(FrameState), hipHostMallocDefault));
-    host_out_bytes_ = kOutPayloadOffset + buf_.out_bytes + 16;
-    HIP_CHECK(hipHostMalloc(&host_out_, host_out_bytes_, hipHostMallocMapped));
-    std::memset(host_out_, 0, kOutPayloadOffset);
-    HIP_CHECK(hipEventCreate(&done_));
-    HIP_CHECK(hipEventCreate(&start_));
+    for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
+    if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 GpuH264Encoder::~GpuH264Encoder() {
-    hipStreamSynchronize(stream_);
-    for (int i = 0; i < 2; ++i) {
-        hipFree(rec_y_[i]);
-        hipFree(rec_uv_[i]);
+    (void)hipStreamSynchronize(stream_);
+    if (stream_e_) {
+        (void)hipStreamSynchronize(stream_e_);
+        (void)hipStreamDestroy(stream_e_);
     }
-    for (int i = 0; i < 4; ++i) hipFree(hp_[i]);
-    hipFree(buf_.fs);
-    hipFree(buf_.mb);
-    hipFree(buf_.coef);
-    hipFree(buf_.slot);
-    hipFree(buf_.slot_bits);
-    hipFree(buf_.unit_off);
-    hipFree(buf_.skip_run);
-    hipFree(buf_.coded_list);
-    hipFree(buf_.coded_info);
-    hipFree(buf_.slice_info);
-    hipFree(buf_.out_hdr);
-    hipFree(buf_.sse_part);
-    hipHostFree(fs_host_);
-    hipHostFree(host_out_);
-    hipEventDestroy(done_);
-    hipEventDestroy(start_);
+    for (int i = 0; i < 2; ++i) {
+        (void)hipFree(rec_y_[i]);
+        (void)hipFree(rec_uv_[i]);
+    }
+    for (int i = 0; i < 4; ++i) (void)hipFree(hp_[i]);
+    for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
 }
 
 void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    FrameSlot& sl = slots_[prep_slot_];
     if (idr) {
-        launch_intra(geom_, buf_, src_y, src_uv, stream_);
+        launch_intra(geom_, sl.buf, src_y, src_uv, stream_);
     } else {
-        launch_hpel(geom_, buf_, hp_, hp_pitch_, stream_);
-        launch_me(geom_, buf_, src_y, stream_);
-        launch_inter(geom_, buf_, src_y, src_uv, stream_);
+        launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_);
+        launch_me(geom_, sl.buf, src_y, stream_);
+        launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
-    launch_entropy(geom_, buf_, host_out_, stream_);
+    hipStream_t es = stream_;
+    if (stream_e_) {  // entropy of this frame overlaps the analysis of the next one
+        HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
+        HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+        es = stream_e_;
+    }
+    launch_entropy(geom_, sl.buf, sl.host_out, es);
     HIP_CHECK(hipGetLastError());
 }
 
 bool GpuH264Encoder::prepare(bool force_idr) {
-    if (pending_) throw std::logic_error("GpuH264Encoder: collect() the previous frame first");
+    if ((int)inflight_.size() >= depth_)
+        throw std::logic_error("GpuH264Encoder: collect() a frame first (pipeline full)");
+    const int s = (depth_ == 1) ? 0 : next_slot_;
+    next_slot_ = (next_slot_ + 1) % depth_;
+    prep_slot_ = s;
+    FrameSlot& sl = slots_[s];
     common_.begin_frame(force_idr || !have_ref_);
+    have_ref_ = true;  // this frame becomes the reference of the next one
     const bool idr = common_.cur_idr();
+    sl.idr = idr;
+    sl.qp = common_.cur_qp();
     const int ref = cur_;
     cur_ ^= 1;
-    FrameState& f = *fs_host_;
+    FrameState& f = *sl.fs_host;
     f.ref_y = rec_y_[ref];
     f.ref_uv = rec_uv_[ref];
     f.rec_y = rec_y_[cur_];
@@ -224,22 +252,24 @@ bool GpuH264Encoder::prepare(bool force_idr) {
     f.hp_h = hp_[1] + org;
     f.hp_v = hp_[2] + org;
     f.hp_j = hp_[3] + org;
-    f.sse_part = buf_.sse_part;
+    f.sse_part = sl.buf.sse_part;
     return idr;
 }
 
 void GpuH264Encoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
-    // everything here depends only on fixed buffers + the device frame state, so the same
-    // sequence can be captured once into a hipGraph and replayed every frame
-    HIP_CHECK(hipMemcpyAsync(buf_.fs, fs_host_, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
+    // frame-state upload + kernels: depends only on fixed buffers and the device frame state
+    // (with depth 1 the same slot every frame, so it can be captured into a hipGraph)
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
     enqueue_kernels(idr, src_y, src_uv);
 }
 
-void GpuH264Encoder::record_start() { HIP_CHECK(hipEventRecord(start_, stream_)); }
+void GpuH264Encoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
 
 void GpuH264Encoder::record_done() {
-    HIP_CHECK(hipEventRecord(done_, stream_));
-    pending_ = true;
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipEventRecord(sl.done, stream_e_ ? stream_e_ : stream_));
+    inflight_.push_back(prep_slot_);
 }
 
 void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
@@ -250,32 +280,34 @@ void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
 }
 
 const std::vector<uint8_t>& GpuH264Encoder::collect() {
-    if (!pending_) throw std::logic_error("GpuH264Encoder: nothing submitted");
-    HIP_CHECK(hipEventSynchronize(done_));
-    pending_ = false;
+    if (inflight_.empty()) throw std::logic_error("GpuH264Encoder: nothing submitted");
+    const int s = inflight_.front();
+    inflight_.pop_front();
+    FrameSlot& sl = slots_[s];
+    HIP_CHECK(hipEventSynchronize(sl.done));
+    last_done_ = sl.done;
     float ms = 0;
-    hipEventElapsedTime(&ms, start_, done_);
-    const OutHeader hdr = *reinterpret_cast<const OutHeader*>(host_out_);
+    (void)hipEventElapsedTime(&ms, sl.start, sl.done);
+    const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);
     if (hdr.overflow) {
-        common_.end_frame(0);
+        common_.end_frame(0, sl.idr);
         have_ref_ = false;  // reference is incomplete: next frame must be IDR
         throw std::runtime_error("h264 gpu encoder: output overflow (flags " + std::to_string(hdr.overflow) + ")");
     }
-    const uint32_t* soff = reinterpret_cast<const uint32_t*>(host_out_ + sizeof(OutHeader));
+    const uint32_t* soff = reinterpret_cast<const uint32_t*>(sl.host_out + sizeof(OutHeader));
     const uint32_t* slen = soff + kMaxSlices;
-    const uint8_t* payload = host_out_ + kOutPayloadOffset;
+    const uint8_t* payload = sl.host_out + kOutPayloadOffset;
     au_.clear();
     au_.reserve(hdr.total_bytes + hdr.total_bytes / 64 + 256);
-    if (common_.cur_idr()) common_.write_parameter_sets(au_);
-    for (uint32_t s = 0; s < hdr.num_slices; ++s) common_.write_slice_nal(au_, payload + soff[s], slen[s]);
+    if (sl.idr) common_.write_parameter_sets(au_);
+    for (uint32_t k = 0; k < hdr.num_slices; ++k) common_.write_slice_nal(au_, payload + soff[k], slen[k], sl.idr);
     stats_.frame_index = common_.frames();
-    stats_.idr = common_.cur_idr();
-    stats_.qp = common_.cur_qp();
+    stats_.idr = sl.idr;
+    stats_.qp = sl.qp;
     stats_.bytes = (int)au_.size();
     stats_.encode_ms = ms;
     for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
-    common_.end_frame((int)au_.size());
-    have_ref_ = true;
+    common_.end_frame((int)au_.size(), sl.idr);
     return au_;
 }
 

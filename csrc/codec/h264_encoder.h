@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,8 @@ struct EncoderConfig {
     int search_range = 16;    // integer-pel full search radius (<= 32)
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
+    int pipeline_depth = 1;   // GPU frames in flight: 2 overlaps frame n's entropy coding with
+                              // frame n+1's analysis on a second HIP stream (rate control lags a frame)
 };
 
 struct FrameStats {
@@ -60,9 +63,9 @@ class EncoderCommon {
     // Append SPS/PPS NAL units (Annex-B) to out.
     void write_parameter_sets(std::vector<uint8_t>& out) const;
     // Append one slice NAL (start code + header byte + emulation-prevented payload).
-    void write_slice_nal(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n) const;
-    // Update rate control after a frame of `bytes` bytes.
-    void end_frame(int bytes);
+    void write_slice_nal(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n, bool idr) const;
+    // Update rate control after a frame of `bytes` bytes (frames end in begin order).
+    void end_frame(int bytes, bool idr);
     void request_idr() { idr_requested_ = true; }
     void set_bitrate(int kbps) { cfg_.bitrate_kbps = kbps; }
     int64_t frames() const { return frame_index_; }
@@ -75,8 +78,9 @@ class EncoderCommon {
     int cur_qp_;
     int frame_num_ = 0;
     int idr_pic_id_ = -1;
-    int64_t frame_index_ = 0;
-    int64_t since_idr_ = 0;
+    int64_t frame_index_ = 0;  // frames ended
+    int64_t begun_ = 0;        // frames begun
+    int64_t since_idr_ = 0;    // frames begun since (and including) the last IDR
     double rc_qp_;        // continuous QP state
     double vbv_fill_ = 0;  // bits above the target rate accumulated so far
 };
@@ -85,6 +89,7 @@ void emulation_prevent(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n)
 
 class GpuH264Encoder {
    public:
+    static constexpr int kMaxInFlight = 2;
     GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream);
     ~GpuH264Encoder();
     GpuH264Encoder(const GpuH264Encoder&) = delete;
@@ -93,49 +98,63 @@ class GpuH264Encoder {
     const Geometry& geometry() const { return geom_; }
     int pitch() const { return geom_.pitch; }
     hipStream_t stream() const { return stream_; }
+    int depth() const { return depth_; }
+    int in_flight() const { return (int)inflight_.size(); }
 
     // Enqueue the encode of an NV12 frame already in device memory (pitch = pitch()).
-    // Equivalent to prepare() + record_start() + enqueue_body() + record_done().
+    // Equivalent to prepare() + record_start() + enqueue_body() + record_done().  With
+    // pipeline_depth 2 a second frame may be submitted before the first is collected:
+    // analysis (hpel/ME/inter or intra) runs on `stream`, entropy coding (CAVLC/scan/pack) on
+    // an internal stream, so frame n's entropy coding overlaps frame n+1's analysis.
     void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false);
-    // Split form for hipGraph replay: host-side frame decisions (rate control, reference
-    // swap) into the pinned frame state; returns whether this is an IDR frame.
+    // Wait for the oldest submitted frame and return its Annex-B access unit.
+    const std::vector<uint8_t>& collect();
+    const FrameStats& last_stats() const { return stats_; }
+    EncoderCommon& common() { return common_; }
+    // Reconstructed frame of the last prepared picture (device pointers).
+    const uint8_t* recon_y() const { return rec_y_[cur_]; }
+    const uint8_t* recon_uv() const { return rec_uv_[cur_]; }
+    // Split form for hipGraph replay (depth 1): host-side frame decisions (rate control,
+    // reference swap) into the pinned frame state; returns whether this is an IDR frame.
     bool prepare(bool force_idr);
     // Frame-state upload + kernels (stream-capturable; identical every frame of a type).
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
     void record_start();
     void record_done();
-    hipEvent_t done_event() const { return done_; }
-    // Wait for the submitted frame and return its Annex-B access unit.
-    const std::vector<uint8_t>& collect();
-    const FrameStats& last_stats() const { return stats_; }
-    EncoderCommon& common() { return common_; }
-    // Reconstructed frame of the last encoded picture (device pointers).
-    const uint8_t* recon_y() const { return rec_y_[cur_]; }
-    const uint8_t* recon_uv() const { return rec_uv_[cur_]; }
-    // Enqueue everything after the frame-state upload; exposed for graph capture.
+    // Completion event of the last collected frame.
+    hipEvent_t done_event() const { return last_done_; }
     void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
-    uint8_t* host_out() const { return host_out_; }
 
    private:
+    struct FrameSlot {  // per-frame-in-flight state
+        DeviceBuffers buf{};
+        FrameState* fs_host = nullptr;  // pinned
+        uint8_t* host_out = nullptr;    // pinned, mapped: OutHeader | slice tables | payload
+        hipEvent_t start = nullptr, analysis_done = nullptr, done = nullptr;
+        bool idr = false;
+        int qp = 0;
+    };
+    void alloc_slot(FrameSlot& sl);
+    void free_slot(FrameSlot& sl);
+
     EncoderConfig cfg_;
     EncoderCommon common_;
     hipStream_t stream_;
+    hipStream_t stream_e_ = nullptr;  // entropy stream (depth 2)
+    int depth_ = 1;
     Geometry geom_;
-    DeviceBuffers buf_{};
-    FrameState* fs_host_ = nullptr;  // pinned
-    uint8_t* host_out_ = nullptr;    // pinned, mapped: OutHeader | slice tables | payload
-    size_t host_out_bytes_ = 0;
+    FrameSlot slots_[kMaxInFlight];
+    int next_slot_ = 0, prep_slot_ = 0;
+    std::deque<int> inflight_;
+    hipEvent_t last_done_ = nullptr;
     uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};  // padded F/H/V/J reference planes
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
-    hipEvent_t done_ = nullptr;
-    hipEvent_t start_ = nullptr;
     std::vector<uint8_t> au_;
     FrameStats stats_;
-    bool pending_ = false;
 };
 
 class CpuH264Encoder {

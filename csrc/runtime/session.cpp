@@ -78,7 +78,11 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     const h264::Geometry& g = enc_->geometry();
     HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
     HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));
-    HIP_CHECK(hipHostMalloc(&staging_, (size_t)pool_->pitch() * cfg_.height, hipHostMallocDefault));
+    depth_ = enc_->depth();
+    if (depth_ > 1 && cfg_.use_graph) throw std::invalid_argument("hipGraph replay needs pipeline_depth 1");
+    if (depth_ >= cfg_.pool_slots) throw std::invalid_argument("pool_slots must exceed pipeline_depth");
+    for (int k = 0; k < depth_; ++k)
+        HIP_CHECK(hipHostMalloc(&staging_[k], (size_t)pool_->pitch() * cfg_.height, hipHostMallocDefault));
     scale_ = cfg_.out_width != cfg_.width || cfg_.out_height != cfg_.height;
     if (scale_) {
         std::vector<int> sx, sy;
@@ -105,7 +109,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         lt_.wy = reinterpret_cast<const float*>(p);
         HIP_CHECK(hipMemcpy(p, wy.data(), wy.size() * 4, hipMemcpyHostToDevice));
     }
-    HIP_CHECK(hipEventCreate(&ev_start_));
+    for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
     HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams), hipHostMallocDefault));
     HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams)));
     graphs_.assign((size_t)cfg_.pool_slots * 2, nullptr);
@@ -122,9 +126,10 @@ Session::~Session() {
     pool_.reset();
     hipFree(nv12_y_);
     hipFree(nv12_uv_);
-    hipHostFree(staging_);
+    for (int k = 0; k < 2; ++k)
+        if (staging_[k]) (void)hipHostFree(staging_[k]);
     if (lt_mem_) hipFree(lt_mem_);
-    hipEventDestroy(ev_start_);
+    for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
     hipStreamDestroy(stream_);
 }
 
@@ -144,7 +149,15 @@ void Session::convert_and_encode(int slot, bool force_idr) {
     TraceRange tr("mxdesk.convert+encode.enqueue");
     convert(slot);
     enc_->submit(nv12_y_, nv12_uv_, force_idr);
-    pending_ = true;
+}
+
+int Session::begin_frame() {
+    if ((int)inflight_.size() >= depth_) throw std::logic_error("Session: collect() before the next submit");
+    const int k = next_k_;
+    next_k_ = (next_k_ + 1) % depth_;
+    inflight_.push_back(Inflight{frame_id_, now_us(), k});
+    t_capture_ = inflight_.back().t_capture;
+    return k;
 }
 
 pix::SynthParams Session::synth_params() {
@@ -190,13 +203,13 @@ hipGraphExec_t Session::capture_frame_graph(int slot, bool idr) {
 }
 
 void Session::submit_synthetic(bool force_idr) {
-    if (pending_) throw std::logic_error("Session: collect() before the next submit");
     TraceRange tr("mxdesk.submit_synthetic");
+    const int k = begin_frame();
     const int slot = pool_->acquire();
-    t_capture_ = now_us();
     const pix::SynthParams p = synth_params();
+    ++frame_id_;
     if (!cfg_.use_graph) {
-        HIP_CHECK(hipEventRecord(ev_start_, stream_));
+        HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
         pix::launch_synth(pool_->data(slot), p, stream_);
         HIP_CHECK(hipGetLastError());
         convert_and_encode(slot, force_idr);
@@ -204,44 +217,44 @@ void Session::submit_synthetic(bool force_idr) {
     }
     *synth_host_ = p;  // read by the graph's memcpy node (previous frame already collected)
     const bool idr = enc_->prepare(force_idr);
-    HIP_CHECK(hipEventRecord(ev_start_, stream_));
+    HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
     enc_->record_start();
     hipGraphExec_t& exec = graphs_[(size_t)slot * 2 + (idr ? 1 : 0)];
     if (!exec) exec = capture_frame_graph(slot, idr);
     HIP_CHECK(hipGraphLaunch(exec, stream_));
     enc_->record_done();
-    pending_ = true;
 }
 
 void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
-    if (pending_) throw std::logic_error("Session: collect() before the next submit");
     TraceRange tr("mxdesk.submit_bgrx(upload)");
+    const int k = begin_frame();
+    ++frame_id_;
     const int slot = pool_->acquire();
-    t_capture_ = now_us();
     const int row = cfg_.width * 4;
     for (int r = 0; r < cfg_.height; ++r)
-        std::memcpy(staging_ + (size_t)r * pool_->pitch(), host_bgrx + (size_t)r * host_pitch, row);
-    HIP_CHECK(hipEventRecord(ev_start_, stream_));
-    HIP_CHECK(hipMemcpyAsync(pool_->data(slot), staging_, (size_t)pool_->pitch() * cfg_.height,
+        std::memcpy(staging_[k] + (size_t)r * pool_->pitch(), host_bgrx + (size_t)r * host_pitch, row);
+    HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+    HIP_CHECK(hipMemcpyAsync(pool_->data(slot), staging_[k], (size_t)pool_->pitch() * cfg_.height,
                              hipMemcpyHostToDevice, stream_));
     convert_and_encode(slot, force_idr);
 }
 
 FrameResult Session::collect() {
-    if (!pending_) throw std::logic_error("Session: nothing submitted");
-    pending_ = false;
+    if (inflight_.empty()) throw std::logic_error("Session: nothing submitted");
+    const Inflight fl = inflight_.front();
+    inflight_.pop_front();
     FrameResult r;
     TraceRange tr("mxdesk.collect(wait+annexb)");
     const std::vector<uint8_t>& au = enc_->collect();
     r.t_encoded_us = now_us();
     r.au = au;
-    r.frame_id = frame_id_++;
-    r.t_capture_us = t_capture_;  // steady clock (CLOCK_MONOTONIC) microseconds
+    r.frame_id = fl.frame_id;
+    r.t_capture_us = fl.t_capture;  // steady clock (CLOCK_MONOTONIC) microseconds
     const h264::FrameStats& st = enc_->last_stats();
     r.idr = st.idr;
     r.qp = st.qp;
     float ms = 0;
-    hipEventElapsedTime(&ms, ev_start_, enc_->done_event());
+    hipEventElapsedTime(&ms, ev_start_[fl.k], enc_->done_event());
     r.gpu_ms = ms;  // render/upload start -> bitstream written
     const double ny = (double)enc_->common().config().width * enc_->common().config().height, nc = ny / 4;
     auto psnr = [](uint64_t sse, double n) { return sse == 0 ? 99.0 : std::min(99.0, 10.0 * std::log10(65025.0 * n / (double)sse)); };

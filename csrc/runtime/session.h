@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <deque>
 #include <cstdint>
 #include <memory>
 #include <vector>
@@ -78,6 +79,8 @@ class Session {
 
     // Synthetic desktop frame -> encode.  `submit` enqueues, `collect` waits.
     void submit_synthetic(bool force_idr = false);
+    int in_flight() const { return (int)inflight_.size(); }
+    int depth() const { return depth_; }
     // Externally captured BGRx frame (host memory, e.g. X11 SHM) -> upload -> encode.
     void submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr = false);
     FrameResult collect();
@@ -116,23 +119,32 @@ class Session {
     std::unique_ptr<h264::GpuH264Encoder> enc_;
     uint8_t* nv12_y_ = nullptr;
     uint8_t* nv12_uv_ = nullptr;
-    uint8_t* staging_ = nullptr;  // pinned upload buffer
+    uint8_t* staging_[2] = {nullptr, nullptr};  // pinned upload buffers (one per frame in flight)
     // Lanczos tables (device) when out size != desktop size
     bool scale_ = false;
     pix::LanczosTables lt_{};
     void* lt_mem_ = nullptr;
-    hipEvent_t ev_start_ = nullptr;
+    // frames in flight (pipeline depth 1 or 2): per-frame start event / staging buffer
+    struct Inflight {
+        uint32_t frame_id;
+        int64_t t_capture;
+        int k;  // index into ev_start_ / staging_
+    };
+    std::deque<Inflight> inflight_;
+    hipEvent_t ev_start_[2] = {nullptr, nullptr};
+    int next_k_ = 0;
+    int depth_ = 1;
     // hipGraph replay: pinned + device synth parameters, one executable graph per
     // (pool slot, frame type) -- the only things that change the captured node arguments
     pix::SynthParams* synth_host_ = nullptr;
     pix::SynthParams* synth_dev_ = nullptr;
     std::vector<hipGraphExec_t> graphs_;
     int graphs_built_ = 0;
-    uint32_t frame_id_ = 0;
+    uint32_t frame_id_ = 0;  // id of the next submitted frame
     int64_t t0_us_ = 0;
     int64_t t_capture_ = 0;
     int cursor_x_ = -1, cursor_y_ = -1;
-    bool pending_ = false;
+    int begin_frame();  // reserve an in-flight entry, returns its k
 };
 
 // Host-side Lanczos-3 table generation (shared with the Python reference in tests).

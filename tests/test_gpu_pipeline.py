@@ -220,3 +220,39 @@ def test_graph_replay_matches_stream_launches(gpu):
     for i, (a, b) in enumerate(zip(eager, graph)):
         assert a == b, f"frame {i} differs"
     assert len(Decoder().decode(b"".join(graph))) == 9
+
+
+def test_pipelined_depth2_matches_depth1(gpu):
+    """Two frames in flight (entropy of frame n on a second stream, overlapping analysis of
+    n+1): constant-QP output is bit-identical to depth 1; with CBR the stream still decodes and
+    frame ids / capture times come back in submission order."""
+    def run(depth, kbps, n=8):
+        cfg = gpu.SessionConfig()
+        cfg.width, cfg.height, cfg.fps = 320, 192, 60
+        cfg.enc.bitrate_kbps = kbps
+        cfg.enc.pipeline_depth = depth
+        cfg.fake_clock = 1
+        s = gpu.Session(cfg)
+        out = []
+        s.submit(False)
+        for i in range(n):
+            if i + 1 < n:
+                if depth == 2:
+                    s.submit(i + 1 == 5)  # forced IDR mid-stream
+                    out.append(s.collect())
+                else:
+                    out.append(s.collect())
+                    s.submit(i + 1 == 5)
+            else:
+                out.append(s.collect())
+        assert s.in_flight == 0
+        return out
+
+    a, b = run(1, 0), run(2, 0)
+    assert [r.au for r in a] == [r.au for r in b]
+    assert [r.frame_id for r in b] == list(range(8)) and [r.idr for r in b][5] == 1
+    c = run(2, 600)
+    frames = Decoder().decode(b"".join(r.au for r in c))
+    ids = [_read_barcode(y, gpu.BARCODE_CELL, gpu.BARCODE_X, gpu.BARCODE_Y)[0] for y, _, _ in frames]
+    assert ids == list(range(8))
+    assert all(r2.t_capture_us >= r1.t_capture_us for r1, r2 in zip(c, c[1:]))
