@@ -665,14 +665,38 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
 }
 
 // ------------------------------------------------------------------ CAVLC
+__device__ __forceinline__ uint32_t mask_bits(int n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1); }
+
+// OR the overlap of segment [s0, s0+len) with output word [W0, W0+32) into acc; getbits
+// returns `n` segment-relative bits starting at `a`.
+template <class F>
+__device__ __forceinline__ void overlap(uint32_t& acc, uint32_t W0, uint32_t s0, uint32_t len, F getbits) {
+    const uint32_t lo = max(W0, s0), hi = min(W0 + 32, s0 + len);
+    if (lo >= hi) return;
+    const int n = (int)(hi - lo);
+    const uint32_t bits = getbits(lo - s0, n) & mask_bits(n);
+    acc |= bits << (W0 + 32 - hi);
+}
+
+// One wave per MB, one CAVLC "role" per lane.  Single coding pass: each role writes its bits
+// MSB-first into a private LDS buffer; a wave prefix sum of the bit counts places the roles;
+// then each lane assembles whole output words of the MB slot from the (at most a few) role
+// buffers overlapping them and stores them straight to the global slot.
+constexpr int kRoleWords = 24;  // worst-case CAVLC 4x4 block ~630 bits
+__device__ __forceinline__ uint32_t role_get(const uint32_t* buf, uint32_t b, int n) {
+    const uint32_t wi = b >> 5, sh = b & 31;
+    const uint64_t hi = ((uint64_t)buf[wi] << 32) | (wi + 1 < (uint32_t)kRoleWords ? buf[wi + 1] : 0u);
+    return (uint32_t)((hi << sh) >> (64 - n));
+}
+
 __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __restrict__ fs, MbInfo* __restrict__ mbs,
                                                const int16_t* __restrict__ coef, uint32_t* __restrict__ slot,
                                                uint32_t* __restrict__ slot_bits) {
-    __shared__ uint32_t lds_slot[4][kSlotWords];
+    __shared__ uint32_t rbuf[4][kNumRoles][kRoleWords];
+    __shared__ uint32_t roff[4][kNumRoles + 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nmb = g.mb_w * g.mb_h;
     const int mbi = blockIdx.x * 4 + wave;
-    for (int i = lane; i < kSlotWords; i += 64) lds_slot[wave][i] = 0;
     if (mbi >= nmb) return;  // whole wave exits together; no workgroup barrier below
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
     const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
@@ -684,33 +708,45 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     const bool skip = decide_skip(g, mbs, mbi, av, &mvdx, &mvdy);
     uint32_t bits = 0;
     if (!skip && lane < kNumRoles) {
-        BitCounter bc;
-        bc.init(nullptr);
-        code_role(bc, lane, g, fs->idr, mbs, m, mc, mbi, av, mvdx, mvdy);
-        bits = bc.bits;
+        BitWriter w;
+        w.init(rbuf[wave][lane]);
+        code_role(w, lane, g, fs->idr, mbs, m, mc, mbi, av, mvdx, mvdy);
+        w.flush();
+        bits = w.bits;
     }
-    // exclusive prefix sum of bits over lanes
+    // exclusive prefix sum of bits over lanes -> role offsets in the MB slot
     uint32_t incl = bits;
     for (int o = 1; o < 64; o <<= 1) {
         uint32_t v = __shfl_up(incl, o, 64);
         if (lane >= o) incl += v;
     }
     const uint32_t total = __shfl(incl, 63, 64);
-    const uint32_t off = incl - bits;
-    __builtin_amdgcn_wave_barrier();
-    if (!skip && lane < kNumRoles && bits > 0 && total <= kSlotWords * 32u) {
-        OrWriter<false> w;
-        w.init(lds_slot[wave], off);
-        code_role(w, lane, g, fs->idr, mbs, m, mc, mbi, av, mvdx, mvdy);
-        w.flush();
-    }
+    if (lane < kNumRoles) roff[wave][lane] = incl - bits;
+    if (lane == kNumRoles) roff[wave][kNumRoles] = total;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const uint32_t nwords = (total + 31) >> 5;
-    for (uint32_t i = lane; i < nwords && i < (uint32_t)kSlotWords; i += 64)
-        slot[(size_t)mbi * kSlotWords + i] = lds_slot[wave][i];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool fits = total <= kSlotWords * 32u;
+    if (!skip && fits) {
+        const uint32_t nwords = (total + 31) >> 5;
+        uint32_t* dst = slot + (size_t)mbi * kSlotWords;
+        for (uint32_t wi = lane; wi < nwords; wi += 64) {
+            const uint32_t W0 = wi * 32;
+            // first role ending after W0 (roles are contiguous and in lane order)
+            int r = 0;
+            while (r < kNumRoles - 1 && roff[wave][r + 1] <= W0) ++r;
+            uint32_t acc = 0;
+            for (; r < kNumRoles; ++r) {
+                const uint32_t o = roff[wave][r], len = roff[wave][r + 1] - o;
+                if (o >= W0 + 32) break;
+                if (len == 0) continue;
+                overlap(acc, W0, o, len, [&](uint32_t x, int n) { return role_get(rbuf[wave][r], x, n); });
+            }
+            dst[wi] = acc;
+        }
+    }
     if (lane == 0) {
-        slot_bits[mbi] = skip ? 0u : (total <= kSlotWords * 32u ? total : 0xffffffffu);
+        slot_bits[mbi] = skip ? 0u : (fits ? total : 0xffffffffu);
         mbs[mbi].skip = skip ? 1 : 0;
     }
 }
@@ -947,18 +983,7 @@ __device__ __forceinline__ uint32_t slot_get(const uint32_t* slot, uint32_t b, i
     return (uint32_t)((hi << sh) >> (64 - n));
 }
 
-__device__ __forceinline__ uint32_t mask_bits(int n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1); }
 
-// OR the overlap of segment [s0, s0+len) with output word [W0, W0+32) into acc; getbits
-// returns `n` segment-relative bits starting at `a`.
-template <class F>
-__device__ __forceinline__ void overlap(uint32_t& acc, uint32_t W0, uint32_t s0, uint32_t len, F getbits) {
-    const uint32_t lo = max(W0, s0), hi = min(W0 + 32, s0 + len);
-    if (lo >= hi) return;
-    const int n = (int)(hi - lo);
-    const uint32_t bits = getbits(lo - s0, n) & mask_bits(n);
-    acc |= bits << (W0 + 32 - hi);
-}
 
 // One thread per 32-bit output word, four lanes per 16-byte quad: each lane locates its
 // word's first overlapping slice / MB unit (4-ary search over the dense per-rank unit
