@@ -817,7 +817,8 @@ __device__ __forceinline__ int block_excl_max(int v, int* wmax, int init) {
 }
 
 // slot_bits[i]: 0 = P_Skip, 0xffffffff = slot overflow, else coded MB bits (>= 1).
-// Outputs: unit_off[i] absolute bit offset of MB i's unit (skip-run prefix + MB bits),
+// Outputs: unit_off[i] bit offset of MB i's unit (skip-run prefix + MB bits) within the
+// concatenated slice data (k_pack reads the absolute offsets from coded_info),
 // skip_run[i] (-1 for skipped MBs), slice_info[kSliceInfo * s + ...].
 __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ slot_bits,
@@ -940,12 +941,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         uint32_t b = slot_bits[i];
         if (b == 0xffffffffu) b = 1;
         coded_info[r] = make_uint4(off, (uint32_t)i, (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b, (uint32_t)run);
-    }
-    __syncthreads();
-    for (int i = t; i < nmb; i += kScanThreads) {
-        const int s = i / per_slice;
-        unit_off[i] = slice_info[kSliceInfo * s + 1] * 8 + slice_info[kSliceInfo * s + 0] +
-                      (unit_off[i] - slice_info[kSliceInfo * s + 5]);
     }
     if (t == 0) {
         const bool over = total_bytes > out_bytes;
