@@ -102,6 +102,20 @@ PYBIND11_MODULE(_native, m) {
 
     // ---------------------------------------------------------------- codec helpers
     py::module h = m.def_submodule("h264", "H.264 building blocks (for tests)");
+    h.def("hpel_planes", [](py::array_t<uint8_t, py::array::c_style> ref, int coded_w) {
+        if (ref.ndim() != 2 || coded_w % 16 || ref.shape(0) % 16 || ref.shape(1) < coded_w)
+            throw std::invalid_argument("ref must be (coded_h, pitch) with 16-aligned coded size");
+        int hp = 0;
+        auto planes = h264::hpel_planes_for_test(ref.data(), coded_w, (int)ref.shape(0), (int)ref.shape(1), &hp);
+        const int rows = (int)ref.shape(0) + 2 * h264::kHpelPad;
+        py::list out;
+        for (auto& p : planes) {
+            py::array_t<uint8_t> a({rows, hp});
+            std::memcpy(a.mutable_data(), p.data(), p.size());
+            out.append(a);
+        }
+        return out;
+    });
     h.def("cavlc_block", &cavlc_block_py, py::arg("coef"), py::arg("nc"));
     h.def("fdct4x4", &fdct_py);
     h.def("idct4x4", &idct_py);

@@ -112,6 +112,46 @@ void EncoderCommon::write_slice_nal(std::vector<uint8_t>& out, const uint8_t* rb
     emulation_prevent(out, rbsp, n);
 }
 
+// ------------------------------------------------------------------ test hook: half-sample planes
+std::vector<std::vector<uint8_t>> hpel_planes_for_test(const uint8_t* ref, int coded_w, int coded_h, int pitch,
+                                                       int* hp_pitch_out) {
+    Geometry g{};
+    g.width = coded_w;
+    g.height = coded_h;
+    g.mb_w = coded_w / 16;
+    g.mb_h = coded_h / 16;
+    g.coded_w = coded_w;
+    g.coded_h = coded_h;
+    g.pitch = pitch;
+    const int hp_pitch = (coded_w + 2 * kHpelPad + 255) & ~255;
+    const size_t hp_bytes = (size_t)hp_pitch * (coded_h + 2 * kHpelPad);
+    uint8_t* dref = nullptr;
+    uint8_t* planes[4];
+    FrameState fs{};
+    DeviceBuffers b{};
+    HIP_CHECK(hipMalloc(&dref, (size_t)pitch * coded_h));
+    HIP_CHECK(hipMemcpy(dref, ref, (size_t)pitch * coded_h, hipMemcpyHostToDevice));
+    for (auto& p : planes) {
+        HIP_CHECK(hipMalloc(&p, hp_bytes));
+        HIP_CHECK(hipMemset(p, 0, hp_bytes));
+    }
+    fs.ref_y = dref;
+    HIP_CHECK(hipMalloc(&b.fs, sizeof(FrameState)));
+    HIP_CHECK(hipMemcpy(b.fs, &fs, sizeof(FrameState), hipMemcpyHostToDevice));
+    launch_hpel(g, b, planes, hp_pitch, nullptr);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
+    std::vector<std::vector<uint8_t>> out(4, std::vector<uint8_t>(hp_bytes));
+    for (int i = 0; i < 4; ++i) {
+        HIP_CHECK(hipMemcpy(out[i].data(), planes[i], hp_bytes, hipMemcpyDeviceToHost));
+        (void)hipFree(planes[i]);
+    }
+    (void)hipFree(dref);
+    (void)hipFree(b.fs);
+    *hp_pitch_out = hp_pitch;
+    return out;
+}
+
 // ------------------------------------------------------------------ GpuH264Encoder
 void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     const int nmb = geom_.mb_w * geom_.mb_h;

@@ -86,6 +86,10 @@ class EncoderCommon {
 };
 
 void emulation_prevent(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n);
+// Test hook: run k_hpel on a host reference picture; returns the padded F/H/V/J planes
+// (origin at (kHpelPad, kHpelPad), pitch in *hp_pitch).
+std::vector<std::vector<uint8_t>> hpel_planes_for_test(const uint8_t* ref, int coded_w, int coded_h, int pitch,
+                                                       int* hp_pitch);
 
 class GpuH264Encoder {
    public:

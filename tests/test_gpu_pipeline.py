@@ -256,3 +256,36 @@ def test_pipelined_depth2_matches_depth1(gpu):
     ids = [_read_barcode(y, gpu.BARCODE_CELL, gpu.BARCODE_X, gpu.BARCODE_Y)[0] for y, _, _ in frames]
     assert ids == list(range(8))
     assert all(r2.t_capture_us >= r1.t_capture_us for r1, r2 in zip(c, c[1:]))
+
+
+def _hpel_reference(ref, pad=48):
+    """numpy 6-tap half-sample planes of a clamped reference (8.4.2.2.1), padded by `pad`."""
+    h, w = ref.shape
+    ys = np.clip(np.arange(-pad - 2, h + pad + 3), 0, h - 1)
+    xs = np.clip(np.arange(-pad - 2, w + pad + 3), 0, w - 1)
+    e = ref[np.ix_(ys, xs)].astype(np.int64)  # extended by pad+2 / pad+3
+    H, W = h + 2 * pad, w + 2 * pad
+    t = lambda a, b, c, d, e_, f: a - 5 * b + 20 * c + 20 * d - 5 * e_ + f
+    F = e[2:2 + H, 2:2 + W]
+    b1 = t(*(e[:, k:k + W] for k in range(6)))  # rows of e, horizontal taps -> (H+5, W)
+    Hh = np.clip((b1[2:2 + H] + 16) >> 5, 0, 255)
+    v1 = t(*(e[k:k + H, 2:2 + W] for k in range(6)))
+    V = np.clip((v1 + 16) >> 5, 0, 255)
+    j1 = t(*(b1[k:k + H] for k in range(6)))
+    J = np.clip((j1 + 512) >> 10, 0, 255)
+    return [p.astype(np.uint8) for p in (F, Hh, V, J)]
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (160, 96), (112, 64)])
+def test_hpel_planes_match_reference(gpu, w, h):
+    rng = np.random.default_rng(w + h)
+    ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    pitch = (w + 255) // 256 * 256
+    buf = np.zeros((h, pitch), np.uint8)
+    buf[:, :w] = ref
+    planes = gpu.h264.hpel_planes(buf, w)
+    want = _hpel_reference(ref)
+    for name, got, exp in zip("FHVJ", planes, want):
+        g = got[: exp.shape[0], : exp.shape[1]]
+        bad = np.argwhere(g != exp)
+        assert bad.size == 0, f"plane {name}: {len(bad)} mismatches, first at {bad[:3].tolist()}"

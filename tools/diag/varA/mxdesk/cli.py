@@ -1,0 +1,143 @@
+"""mxdesk command line (``python -m mxdesk <command>``).
+
+Commands
+  desktop    X server + desktop session, blocks while X runs (reference entrypoint.sh)
+  serve      one streaming session on :8080 (the reference's selkies-gstreamer entrypoint,
+             selkies-gstreamer-entrypoint.sh:44-47, or noVNC when NOVNC_ENABLE=true)
+  launch     one session per visible GPU on ports 8080+i
+  wall       tiled video wall: one tile per GPU, RCCL all-gather, single stream (C58)
+  supervise  run a supervisord-style config (C56)
+  config     print the resolved configuration (secrets redacted)
+  devices    list AMD GPUs (sysfs/KFD) and the selected one
+  cvt        print a CVT / CVT-RB modeline (``cvt [-r] W H [R]``)
+  xorg-conf  print the generated xorg.conf for the current config
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+
+from .utils import config as C
+
+
+def _setup_logging(cfg: C.Config) -> None:
+    logging.basicConfig(level=getattr(logging, cfg.log_level_name, logging.WARNING),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+
+
+def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0"):
+    from .pipeline.stream import StreamPipeline
+
+    backend = "gpu" if cfg.encoder_backend == "mxh264enc" else "cpu"
+    capture = None
+    if cfg.source == "x11" or (cfg.source == "auto" and _x_available(cfg.display)):
+        from .models.x11 import X11Capture
+
+        capture = X11Capture(cfg.display, cfg.sizew, cfg.sizeh)
+    return StreamPipeline(cfg.sizew, cfg.sizeh, cfg.stream_fps, backend=backend, device=device,
+                          bitrate_kbps=cfg.video_bitrate, keyint=cfg.keyint_frames, search_range=cfg.search_range,
+                          subpel=cfg.subpel, noise=cfg.noise, out_width=cfg.out_width, out_height=cfg.out_height,
+                          session_name=session_name, capture=capture)
+
+
+def _x_available(display: str) -> bool:
+    from .display.xorg import x_socket
+
+    return os.path.exists(x_socket(display))
+
+
+def _gpu_index(cfg: C.Config) -> int:
+    """HIP ordinal of the selected GPU: HIP enumerates only the visible devices, in PCI
+    order, so the ordinal is the position inside the visible list."""
+    from .utils import devices as D
+
+    gpus = D.visible_gpus(D.enumerate_gpus())
+    if not gpus:
+        return 0
+    return gpus.index(D.select_gpu(gpus, cfg.gpu))
+
+
+def cmd_serve(cfg: C.Config, args) -> None:
+    from .server.app import MediaServer, run_forever, ssl_context
+
+    device = 0 if cfg.encoder_backend != "mxh264enc" else _gpu_index(cfg)
+    pipe = build_pipeline(cfg, device)
+    rfb = None
+    if cfg.novnc_enable:
+        from .server.rfb import RfbServer
+
+        rfb = RfbServer(pipe, cfg.effective_basic_auth_password, cfg.novnc_viewpass, fps=min(cfg.stream_fps, 30))
+    # NOVNC_ENABLE=true: the RFB front end replaces WebRTC (supervisord.conf:36 puts selkies
+    # to sleep), so the H.264 pipeline is not started.
+    srv = MediaServer(pipe, cfg, rfb=rfb, start_pipeline=not cfg.novnc_enable)
+    print(f"mxdesk: serving {cfg.sizew}x{cfg.sizeh}@{cfg.stream_fps} ({cfg.encoder_backend}) on "
+          f"{cfg.addr}:{cfg.port}", flush=True)
+    run_forever(srv, cfg.addr, cfg.port, ssl_context(cfg))
+
+
+def main(argv: list[str] | None = None) -> None:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] in ("-h", "--help"):
+        print(__doc__)
+        return
+    cmd, rest = argv[0], argv[1:]
+    if cmd == "cvt":
+        from .display.cvt import main as cvt_main
+
+        cvt_main(rest)
+        return
+    if cmd == "supervise":
+        from .utils.supervisor import main as sup_main
+
+        sup_main(rest)
+        return
+    ap = argparse.ArgumentParser(prog=f"mxdesk {cmd}")
+    C.add_cli_flags(ap)
+    if cmd == "launch":
+        ap.add_argument("--base-port", type=int, default=None)
+    if cmd == "wall":
+        ap.add_argument("--layout", default=None)
+    args, _ = ap.parse_known_args(rest)
+    cfg = C.load(cli=args)
+    _setup_logging(cfg)
+    if cmd == "config":
+        print(cfg.dump())
+    elif cmd == "devices":
+        from dataclasses import asdict
+
+        from .utils import devices as D
+
+        gpus = D.visible_gpus(D.enumerate_gpus())
+        print(json.dumps([asdict(g) | {"xorg_busid": g.xorg_busid} for g in gpus], indent=1))
+    elif cmd == "xorg-conf":
+        from .display.xorg import DisplaySettings, render_xorg_conf
+        from .utils import devices as D
+
+        gpus = D.visible_gpus(D.enumerate_gpus())
+        busid = D.select_gpu(gpus, cfg.gpu).xorg_busid if gpus else ""
+        print(render_xorg_conf(DisplaySettings(cfg.sizew, cfg.sizeh, cfg.refresh, cfg.cdepth, cfg.dpi,
+                                               cfg.video_port, busid, "dummy", cfg.display)), end="")
+    elif cmd == "serve":
+        cmd_serve(cfg, args)
+    elif cmd == "desktop":
+        from .display.desktop import run_display_session
+
+        sys.exit(run_display_session(cfg))
+    elif cmd == "launch":
+        from .parallel.launcher import launch_sessions
+
+        launch_sessions(cfg, base_port=args.base_port or cfg.port)
+    elif cmd == "wall":
+        from .parallel.wall import wall_main
+
+        wall_main(cfg, layout=args.layout or cfg.wall or "2x2")
+    else:
+        print(f"unknown command {cmd}\n{__doc__}")
+        sys.exit(2)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,47 @@
+"""Session-per-GPU launcher (SURVEY.md C57, §2.6 "DP" analogue).
+
+The reference runs exactly one desktop per container/GPU and scales out with more pods
+(xgl.yml:10, README.md:180-182).  Here one node serves N independent sessions, one per
+visible MI355X: session i is pinned to GPU i with ``HIP_VISIBLE_DEVICES`` and listens on
+``base_port + i``.  Children are run by the mxdesk supervisor (autorestart with backoff,
+process-group kill, readiness = the HTTP port accepting connections).
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Any
+
+from ..utils.supervisor import Program, Ready, Supervisor
+
+
+def session_programs(n_gpus: int, base_port: int = 8080, extra_args: list[str] | None = None,
+                     sessions_per_gpu: int = 1, python: str = sys.executable) -> list[Program]:
+    progs = []
+    k = 0
+    for gpu in range(n_gpus):
+        for s in range(sessions_per_gpu):
+            port = base_port + k
+            env = {"HIP_VISIBLE_DEVICES": str(gpu), "MXDESK_GPU": "0", "SELKIES_PORT": str(port),
+                   "MXDESK_SESSION": str(k)}
+            progs.append(Program(name=f"session{k}-gpu{gpu}", command=[python, "-m", "mxdesk", "serve",
+                                                                       "--port", str(port), *(extra_args or [])],
+                                 priority=10 + k, environment=env, ready=Ready("tcp", f"127.0.0.1:{port}", 120.0),
+                                 wait_ready=False, startsecs=2.0, startretries=5))
+            k += 1
+    return progs
+
+
+def launch_sessions(cfg: Any, base_port: int = 8080, n_gpus: int | None = None, sessions_per_gpu: int = 1) -> None:
+    from ..utils import devices as D
+
+    if n_gpus is None:
+        n_gpus = len(D.visible_gpus(D.enumerate_gpus())) or 1
+    progs = session_programs(n_gpus, base_port, sessions_per_gpu=sessions_per_gpu)
+    print(f"mxdesk launch: {len(progs)} session(s) on {n_gpus} GPU(s), ports {base_port}..{base_port + len(progs) - 1}",
+          flush=True)
+    Supervisor(progs, log_dir=getattr(cfg, "log_dir", "/tmp")).run()
+
+
+if __name__ == "__main__":
+    os.environ.setdefault("PYTHONUNBUFFERED", "1")

@@ -1,0 +1,268 @@
+"""Tiled video wall: N GPUs render one tile each, tiles are exchanged over RCCL/xGMI and the
+composite is encoded as a single stream (BASELINE.json config 5
+"2x2 tiled 8K60 wall: 4-GPU render, RCCL all-gather composite over xGMI").
+
+Per frame, on every rank (one process per GPU, ``torch.distributed`` backend ``nccl`` =
+RCCL on ROCm; ``gloo`` for CPU tests):
+  1. rank 0 broadcasts a small control tensor (frame id, force-IDR, stop) -> lockstep;
+  2. each rank renders its tile of the wall (HIP synthetic desktop with a tile origin) and
+     converts it to NV12 on its own GPU (HIP CSC), so only 1.5 B/pixel cross xGMI;
+  3. the tiles reach the encode rank either by a ring ``all_gather_into_tensor``
+     (``exchange="allgather"``) or by a direct gather -- one batched send/recv per peer, so
+     the encode rank pulls the three tiles over three xGMI links at once
+     (``exchange="gather"``; xGMI is point-to-point, a ring is per-link bound);
+  4. the encode rank composites the NV12 tiles into the wall frame and H.264-encodes it.
+If process-group initialisation fails the launcher falls back to per-GPU sessions
+(SURVEY.md §5.3).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from dataclasses import dataclass
+from typing import Any
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+from ..pipeline.stream import EncodedFrame, StreamPipeline
+
+log = logging.getLogger("mxdesk.wall")
+
+
+def parse_layout(layout: str) -> tuple[int, int]:
+    c, r = layout.lower().split("x")
+    return int(c), int(r)
+
+
+@dataclass
+class WallGeometry:
+    cols: int
+    rows: int
+    tile_w: int
+    tile_h: int
+
+    @property
+    def width(self) -> int:
+        return self.cols * self.tile_w
+
+    @property
+    def height(self) -> int:
+        return self.rows * self.tile_h
+
+    @property
+    def tile_bytes(self) -> int:
+        return self.tile_w * self.tile_h * 3 // 2
+
+    def origin(self, rank: int) -> tuple[int, int]:
+        return (rank % self.cols) * self.tile_w, (rank // self.cols) * self.tile_h
+
+
+class TileRenderer:
+    """Renders + converts one tile to packed NV12 (Y rows then interleaved UV rows)."""
+
+    def __init__(self, geo: WallGeometry, rank: int, device: torch.device, noise: bool = True):
+        self.geo, self.rank, self.device = geo, rank, device
+        self.ox, self.oy = geo.origin(rank)
+        tw, th = geo.tile_w, geo.tile_h
+        self.out = torch.empty(geo.tile_bytes, dtype=torch.uint8, device=device)
+        if device.type == "cuda":
+            from .. import native
+
+            self.N = native()
+            self.pitch = ((tw * 4) + 255) // 256 * 256
+            self.bgrx = torch.empty((th, self.pitch), dtype=torch.uint8, device=device)
+        else:
+            self.N = None
+            self.desk = CpuSyntheticDesktop(geo.width, geo.height, noise)
+
+    def render(self, frame_id: int, t: float, ts_us: int) -> torch.Tensor:
+        g = self.geo
+        if self.N is not None:
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            self.N.synth(self.bgrx.data_ptr(), g.tile_w, g.tile_h, self.pitch, frame_id, ts_us & 0xFFFFFFFF, t, 1,
+                         self.ox, self.oy, g.width, g.height, -1, -1, st)
+            y_ptr = self.out.data_ptr()
+            uv_ptr = y_ptr + g.tile_w * g.tile_h
+            self.N.bgrx_to_nv12(self.bgrx.data_ptr(), self.pitch, g.tile_w, g.tile_h, y_ptr, uv_ptr, g.tile_w,
+                                g.tile_w, g.tile_h, st)
+            return self.out
+        full = self.desk.render(frame_id, t, ts_us)
+        tile = np.ascontiguousarray(full[self.oy:self.oy + g.tile_h, self.ox:self.ox + g.tile_w])
+        y, uv = bgrx_to_nv12(tile)
+        self.out.copy_(torch.from_numpy(np.concatenate([y.reshape(-1), uv.reshape(-1)])))
+        return self.out
+
+
+class TileExchange:
+    def __init__(self, geo: WallGeometry, rank: int, world: int, device: torch.device, mode: str = "gather",
+                 root: int = 0):
+        if world != geo.cols * geo.rows:
+            raise ValueError(f"wall {geo.cols}x{geo.rows} needs {geo.cols * geo.rows} ranks, got {world}")
+        self.geo, self.rank, self.world, self.mode, self.root = geo, rank, world, mode, root
+        self.tiles = torch.empty(world * geo.tile_bytes, dtype=torch.uint8, device=device) \
+            if (rank == root or mode == "allgather") else None
+
+    def exchange(self, tile: torch.Tensor) -> torch.Tensor | None:
+        if self.mode == "allgather":
+            dist.all_gather_into_tensor(self.tiles, tile)
+            return self.tiles if self.rank == self.root else None
+        tb = self.geo.tile_bytes
+        if self.rank == self.root:
+            self.tiles[self.root * tb:(self.root + 1) * tb].copy_(tile)
+            ops = [dist.P2POp(dist.irecv, self.tiles[r * tb:(r + 1) * tb], r) for r in range(self.world)
+                   if r != self.root]
+        else:
+            ops = [dist.P2POp(dist.isend, tile, self.root)]
+        if ops:  # world size 1: nothing to exchange
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return self.tiles if self.rank == self.root else None
+
+
+def composite_nv12(tiles: torch.Tensor, geo: WallGeometry, y: torch.Tensor, uv: torch.Tensor) -> None:
+    """Place packed NV12 tiles into the wall planes y (H, P) and uv (H/2, P)."""
+    tb, tw, th = geo.tile_bytes, geo.tile_w, geo.tile_h
+    for r in range(geo.cols * geo.rows):
+        ox, oy = geo.origin(r)
+        t = tiles[r * tb:(r + 1) * tb]
+        y[oy:oy + th, ox:ox + tw].copy_(t[: tw * th].view(th, tw))
+        uv[oy // 2:oy // 2 + th // 2, ox:ox + tw].copy_(t[tw * th:].view(th // 2, tw))
+
+
+class WallPipeline(StreamPipeline):
+    """Rank-0 pipeline: lockstep tile render on every rank, exchange, composite, encode."""
+
+    def __init__(self, geo: WallGeometry, fps: int, rank: int, world: int, device: torch.device,
+                 exchange: str = "gather", bitrate_kbps: int = 20000, **kw):
+        self.geo, self.rank, self.world, self.dev = geo, rank, world, device
+        self.renderer = TileRenderer(geo, rank, device)
+        self.xchg = TileExchange(geo, rank, world, device, exchange)
+        self.ctrl = torch.zeros(4, dtype=torch.int64, device=device)
+        self._t0 = time.monotonic()
+        self._fid = 0
+        super().__init__(geo.width, geo.height, fps, backend="gpu" if device.type == "cuda" else "cpu",
+                         device=device.index or 0, bitrate_kbps=bitrate_kbps, **kw)
+
+    def _make_session(self) -> None:
+        from .. import native
+
+        N = native()
+        cw, ch = (self.geo.width + 15) // 16 * 16, (self.geo.height + 15) // 16 * 16
+        ec = N.EncoderConfig()
+        ec.width, ec.height, ec.fps = self.geo.width, self.geo.height, self.fps
+        ec.bitrate_kbps = self._enc_args["bitrate_kbps"]
+        ec.search_range = self._enc_args["search_range"]
+        ec.subpel = 1 if self._enc_args["subpel"] else 0
+        if self.dev.type == "cuda":
+            self.enc = N.GpuH264Encoder(ec, torch.cuda.current_stream(self.dev).cuda_stream)
+            pitch = self.enc.pitch
+        else:
+            ec.search_range = min(ec.search_range, 4)
+            ec.subpel = 0
+            self.enc = N.CpuH264Encoder(ec)
+            pitch = cw
+        self.wy = torch.zeros((ch, pitch), dtype=torch.uint8, device=self.dev)
+        self.wuv = torch.zeros((ch // 2, pitch), dtype=torch.uint8, device=self.dev)
+        self._sess = None
+        self._cpu = self.enc if self.dev.type != "cuda" else None
+
+    def set_bitrate(self, kbps: int) -> None:
+        self.enc.set_bitrate(int(kbps))
+
+    def lockstep_frame(self, force_idr: bool, stop: bool = False) -> torch.Tensor | None:
+        from .. import native
+
+        t_cap = native().now_us()
+        self.ctrl[0], self.ctrl[1], self.ctrl[2], self.ctrl[3] = self._fid, int(force_idr), int(stop), t_cap
+        dist.broadcast(self.ctrl, 0)
+        if stop:
+            return None
+        tile = self.renderer.render(self._fid, self._fid / self.fps, t_cap)
+        tiles = self.xchg.exchange(tile)
+        if tiles is not None:
+            composite_nv12(tiles, self.geo, self.wy, self.wuv)
+        return tiles
+
+    def _produce(self, force_idr: bool) -> EncodedFrame:
+        from .. import native
+
+        t_cap = native().now_us()
+        self.lockstep_frame(force_idr)
+        fid = self._fid
+        self._fid += 1
+        if self.dev.type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
+            au = self.enc.encode(self.wy.data_ptr(), self.wuv.data_ptr(), force_idr)
+        else:
+            au = self.enc.encode(self.wy.cpu().numpy()[: self.geo.height], self.wuv.cpu().numpy()[: self.geo.height // 2],
+                                 force_idr)
+        st = self.enc.stats
+        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, self.geo.width, self.geo.height)
+
+    def stop(self) -> None:
+        super().stop()
+        try:
+            self.lockstep_frame(False, stop=True)
+        except Exception:
+            pass
+
+
+def follower_loop(geo: WallGeometry, rank: int, world: int, device: torch.device, exchange: str = "gather",
+                  fps: int = 60) -> int:
+    """Ranks != 0: render + send tiles in lockstep until rank 0 broadcasts stop."""
+    renderer = TileRenderer(geo, rank, device)
+    xchg = TileExchange(geo, rank, world, device, exchange)
+    ctrl = torch.zeros(4, dtype=torch.int64, device=device)
+    n = 0
+    while True:
+        dist.broadcast(ctrl, 0)
+        fid, _, stop, t_cap = (int(x) for x in ctrl.tolist())
+        if stop:
+            return n
+        xchg.exchange(renderer.render(fid, fid / fps, t_cap))
+        n += 1
+
+
+def init_distributed(backend: str | None = None) -> tuple[int, int, torch.device]:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        dist.init_process_group(backend or ("nccl" if use_gpu else "gloo"),
+                                **({"device_id": device} if use_gpu else {}))
+    return rank, world, device
+
+
+def wall_main(cfg: Any, layout: str = "2x2") -> None:
+    cols, rows = parse_layout(layout)
+    try:
+        rank, world, device = init_distributed()
+    except Exception as e:  # degrade to per-GPU sessions
+        log.error("wall: process group init failed (%s); falling back to per-GPU sessions", e)
+        from .launcher import launch_sessions
+
+        launch_sessions(cfg)
+        return
+    geo = WallGeometry(cols, rows, cfg.sizew, cfg.sizeh)
+    exchange = os.environ.get("MXDESK_WALL_EXCHANGE", "gather")
+    if rank != 0:
+        follower_loop(geo, rank, world, device, exchange, cfg.stream_fps)
+        dist.destroy_process_group()
+        return
+    from ..server.app import MediaServer, run_forever, ssl_context
+
+    pipe = WallPipeline(geo, cfg.stream_fps, rank, world, device, exchange, bitrate_kbps=cfg.video_bitrate * 4)
+    print(f"mxdesk wall {cols}x{rows}: {geo.width}x{geo.height} on {world} ranks, serving :{cfg.port}", flush=True)
+    try:
+        run_forever(MediaServer(pipe, cfg), cfg.addr, cfg.port, ssl_context(cfg))
+    finally:
+        pipe.stop()
+        dist.destroy_process_group()

@@ -1,0 +1,310 @@
+"""Streaming pipeline: paced frame production + fan-out to viewers.
+
+A ``StreamPipeline`` owns one encoder session (GPU: the native HIP session; CPU: numpy
+desktop + CPU H.264 encoder for the plumbing configuration), produces frames at the stream
+rate on a dedicated thread and pushes each encoded access unit to every subscriber queue
+(asyncio-safe).  Policies:
+  * a new viewer or a PLI/keyframe request forces an IDR on the next frame;
+  * a viewer whose queue overflows is resynchronised: its backlog is dropped and it waits
+    for the next IDR (counted in ``mxdesk_dropped_frames``);
+  * a watchdog restarts the encoder session if no frame was produced for ``stall_s``;
+  * ``MXDESK_FAULT`` (tests only) injects failures: ``drop:N`` drops every Nth frame,
+    ``stall:S`` stalls the producer once for S seconds, ``crash:N`` raises at frame N.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import threading
+import time
+from dataclasses import dataclass
+from typing import Any, Callable
+
+import numpy as np
+
+from ..models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+from ..utils.metrics import SessionMetrics
+
+log = logging.getLogger("mxdesk.pipeline")
+
+
+@dataclass
+class EncodedFrame:
+    frame_id: int
+    t_capture_us: int   # CLOCK_MONOTONIC us
+    t_encoded_us: int
+    idr: bool
+    qp: int
+    au: bytes
+    width: int
+    height: int
+    gpu_ms: float = 0.0
+
+
+def h264_codec_string(width: int, height: int, fps: int) -> str:
+    """WebCodecs/RFC 6381 codec id of our Constrained Baseline stream (avc1.42C0LL)."""
+    from .. import native
+
+    mbs = ((width + 15) // 16) * ((height + 15) // 16)
+    level = native().h264.level_for(mbs, fps)
+    return f"avc1.42C0{level:02X}"
+
+
+class _Subscriber:
+    def __init__(self, loop: asyncio.AbstractEventLoop, maxsize: int):
+        self.loop = loop
+        self.queue: asyncio.Queue = asyncio.Queue(maxsize=maxsize)
+        self.need_idr = True
+        self.dropped = 0
+
+    def offer(self, fr: EncodedFrame, on_drop: Callable[[int], None]) -> None:
+        def put():
+            if self.need_idr and not fr.idr:
+                return
+            if self.queue.full():
+                n = self.queue.qsize()
+                while not self.queue.empty():
+                    self.queue.get_nowait()
+                self.dropped += n
+                on_drop(n)
+                self.need_idr = True
+                return
+            self.need_idr = False
+            self.queue.put_nowait(fr)
+
+        try:
+            self.loop.call_soon_threadsafe(put)
+        except RuntimeError:
+            pass  # loop closed
+
+
+class StreamPipeline:
+    def __init__(self, width: int, height: int, fps: int, *, backend: str = "gpu", device: int = 0,
+                 bitrate_kbps: int = 8000, keyint: int = 0, search_range: int = 16, subpel: bool = True,
+                 noise: bool = True, out_width: int = 0, out_height: int = 0, session_name: str = "0",
+                 capture: Any = None, metrics: SessionMetrics | None = None, queue_frames: int = 8,
+                 stall_s: float = 2.0, paced: bool = True):
+        self.width, self.height, self.fps = width, height, fps
+        self.out_w = out_width or width
+        self.out_h = out_height or height
+        self.backend = backend
+        self.device = device
+        self.capture = capture
+        self.metrics = metrics or SessionMetrics(session_name)
+        self.queue_frames = queue_frames
+        self.stall_s = stall_s
+        self.paced = paced
+        self.bitrate_kbps = bitrate_kbps  # configured CBR target (congestion control upper bound)
+        self._enc_args = dict(bitrate_kbps=bitrate_kbps, keyint=keyint, search_range=search_range, subpel=subpel,
+                              noise=noise)
+        self._subs: list[_Subscriber] = []
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._thread: threading.Thread | None = None
+        self._force_idr = True
+        self._pending_bitrate: int | None = None
+        self._cursor = (-1, -1)
+        self.frames_out = 0
+        self.last_frame_t = 0.0
+        self.restarts = 0
+        self.last_error: str | None = None
+        self._fault = self._parse_fault(os.environ.get("MXDESK_FAULT", ""))
+        self._make_session()
+
+    # ------------------------------------------------------------------ session backends
+    @staticmethod
+    def _parse_fault(spec: str) -> dict[str, float]:
+        out = {}
+        for part in spec.split(","):
+            if ":" in part:
+                k, v = part.split(":", 1)
+                out[k.strip()] = float(v)
+        return out
+
+    def _make_session(self) -> None:
+        a = self._enc_args
+        if self.backend == "gpu":
+            from .. import native
+
+            N = native()
+            N.set_device(self.device)
+            cfg = N.SessionConfig()
+            cfg.width, cfg.height, cfg.fps = self.width, self.height, self.fps
+            cfg.out_width, cfg.out_height = self.out_w, self.out_h
+            cfg.noise = 1 if a["noise"] else 0
+            cfg.enc.bitrate_kbps = a["bitrate_kbps"]
+            cfg.enc.keyint = a["keyint"]
+            cfg.enc.search_range = a["search_range"]
+            cfg.enc.subpel = 1 if a["subpel"] else 0
+            self._sess = N.Session(cfg)
+            self._cpu = None
+        elif self.backend == "cpu":
+            from .. import native
+
+            N = native()
+            if (self.out_w, self.out_h) != (self.width, self.height):
+                raise ValueError("the CPU plumbing backend does not scale")
+            ec = N.EncoderConfig()
+            ec.width, ec.height, ec.fps = self.width, self.height, self.fps
+            ec.bitrate_kbps = a["bitrate_kbps"]
+            ec.keyint = a["keyint"]
+            ec.search_range = min(a["search_range"], 4)  # keep the serial encoder real-time
+            ec.subpel = 0
+            self._cpu = N.CpuH264Encoder(ec)
+            self._desk = CpuSyntheticDesktop(self.width, self.height, a["noise"])
+            self._sess = None
+            self._cpu_frame = 0
+        else:
+            raise ValueError(f"unknown backend {self.backend}")
+
+    def _produce(self, force_idr: bool) -> EncodedFrame:
+        from .. import native
+
+        if self._pending_bitrate is not None:
+            (self._sess or self._cpu).set_bitrate(self._pending_bitrate)
+            self._pending_bitrate = None
+        if self._sess is not None:
+            s = self._sess
+            s.set_cursor(*self._cursor)
+            if self.capture is not None:
+                img = self.capture.grab()
+                s.submit_bgrx(img, force_idr)
+                r = s.collect()
+            else:
+                r = s.step(force_idr)
+            return EncodedFrame(r.frame_id, r.t_capture_us, r.t_encoded_us, bool(r.idr), r.qp, r.au, self.out_w,
+                                self.out_h, r.gpu_ms)
+        t_cap = native().now_us()
+        fid = self._cpu_frame
+        self._cpu_frame += 1
+        self._desk.cursor = self._cursor
+        img = self.capture.grab() if self.capture is not None else self._desk.render(fid, fid / self.fps,
+                                                                                     t_cap & 0xFFFFFFFF)
+        y, uv = bgrx_to_nv12(img)
+        au = self._cpu.encode(y, uv, force_idr)
+        st = self._cpu.stats
+        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, self.width, self.height)
+
+    # ------------------------------------------------------------------ control
+    def request_idr(self) -> None:
+        self._force_idr = True
+
+    def set_bitrate(self, kbps: int) -> None:
+        self._pending_bitrate = int(max(100, min(kbps, 200_000)))
+
+    def set_fps(self, fps: float) -> None:
+        """Client frame-rate request (selkies ``_f,fps``): changes the pacing only; the
+        stream's VUI timing stays at the session rate."""
+        self.pace_fps = float(max(1.0, min(float(fps), 240.0)))
+
+    def set_cursor(self, x: int, y: int) -> None:
+        self._cursor = (int(x), int(y))
+
+    def subscribe(self, loop: asyncio.AbstractEventLoop | None = None) -> _Subscriber:
+        sub = _Subscriber(loop or asyncio.get_event_loop(), self.queue_frames)
+        with self._lock:
+            self._subs.append(sub)
+            self.metrics.set_clients(len(self._subs))
+        self.request_idr()
+        return sub
+
+    def unsubscribe(self, sub: _Subscriber) -> None:
+        with self._lock:
+            if sub in self._subs:
+                self._subs.remove(sub)
+            self.metrics.set_clients(len(self._subs))
+
+    @property
+    def subscribers(self) -> int:
+        with self._lock:
+            return len(self._subs)
+
+    # ------------------------------------------------------------------ loop
+    def step(self) -> EncodedFrame:
+        """Produce one frame synchronously (no pacing); publishes to subscribers."""
+        force = self._force_idr
+        self._force_idr = False
+        n = self.frames_out
+        if "crash" in self._fault and n == int(self._fault["crash"]):
+            raise RuntimeError("injected encoder crash")
+        if "stall" in self._fault and n == 3:
+            time.sleep(self._fault.pop("stall"))
+        fr = self._produce(force)
+        self.frames_out += 1
+        self.last_frame_t = time.monotonic()
+        self.metrics.on_frame(len(fr.au), (fr.t_encoded_us - fr.t_capture_us) / 1000.0, fr.gpu_ms, fr.qp, fr.idr)
+        if "drop" in self._fault and self.frames_out % int(self._fault["drop"]) == 0:
+            self.metrics.on_drop()
+            return fr
+        with self._lock:
+            subs = list(self._subs)
+        for s in subs:
+            s.offer(fr, self.metrics.on_drop)
+        return fr
+
+    def _run(self) -> None:
+        next_t = time.monotonic()
+        while not self._stop.is_set():
+            try:
+                self.step()
+            except Exception as e:  # encoder failure -> restart the session, force IDR
+                self.last_error = repr(e)
+                log.exception("frame production failed; restarting session")
+                self.restarts += 1
+                self._fault.pop("crash", None)
+                try:
+                    self._make_session()
+                except Exception:
+                    log.exception("session restart failed")
+                self.request_idr()
+                self._stop.wait(min(2.0, 0.1 * self.restarts))  # back off on repeated failures
+            if self.paced:
+                next_t += 1.0 / (getattr(self, "pace_fps", None) or self.fps)
+                delay = next_t - time.monotonic()
+                if delay > 0:
+                    self._stop.wait(delay)
+                else:
+                    next_t = time.monotonic()  # fell behind: do not burst
+
+    def start(self) -> None:
+        if self._thread is None:
+            self._stop.clear()
+            self._thread = threading.Thread(target=self._run, name="mxdesk-pipeline", daemon=True)
+            self._thread.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+            self._thread = None
+
+    def healthy(self) -> bool:
+        return self._thread is not None and (time.monotonic() - self.last_frame_t) < self.stall_s
+
+    def status(self) -> dict:
+        return {"backend": self.backend, "device": self.device, "width": self.out_w, "height": self.out_h,
+                "fps": self.fps, "frames": self.frames_out, "clients": self.subscribers, "restarts": self.restarts,
+                "last_error": self.last_error, **self.metrics.summary()}
+
+
+def frame_header(fr: EncodedFrame, t_send_us: int) -> bytes:
+    """Binary media header of the WebSocket transport (36 bytes, little endian)."""
+    import struct
+
+    return struct.pack("<4sBBHIQQHHI", b"MXV1", 1 if fr.idr else 0, 1, 0, fr.frame_id & 0xFFFFFFFF,
+                       fr.t_capture_us, t_send_us, fr.width, fr.height, len(fr.au))
+
+
+def parse_frame(msg: bytes) -> dict:
+    import struct
+
+    magic, flags, codec, _, fid, tcap, tsend, w, h, n = struct.unpack_from("<4sBBHIQQHHI", msg)
+    if magic != b"MXV1":
+        raise ValueError("bad media frame")
+    return {"key": bool(flags & 1), "codec": codec, "frame_id": fid, "t_capture_us": tcap, "t_send_us": tsend,
+            "width": w, "height": h, "au": msg[36:36 + n]}
+
+
+def nv12_planes_equal(a: tuple[np.ndarray, np.ndarray], b: tuple[np.ndarray, np.ndarray]) -> bool:
+    return all(np.array_equal(x, y) for x, y in zip(a, b))

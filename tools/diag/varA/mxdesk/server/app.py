@@ -1,0 +1,283 @@
+"""HTTP(S) + WebSocket front end on :8080.
+
+Replaces the selkies-gstreamer web/signalling server started by
+selkies-gstreamer-entrypoint.sh:44-47 (``--addr=0.0.0.0 --port=8080``) and, when
+``NOVNC_ENABLE=true``, the noVNC/websockify front end (entrypoint.sh:121-125):
+
+  GET  /                 web client (WebCodecs H.264 player + input capture), PWA manifest
+  GET  /health           liveness/readiness (200 when frames flow)
+  GET  /turn             RTCConfiguration JSON (STUN/TURN; HMAC or legacy credentials)
+  GET  /metrics          Prometheus exposition
+  GET  /status           JSON session status (fps, bitrate, QP, latency quantiles)
+  WS   /ws               selkies-compatible signalling relay
+  WS   /mxws             media transport: binary Annex-B access units + JSON control/input
+  WS   /websockify       RFB (noVNC) over WebSocket when NOVNC_ENABLE=true
+
+Basic auth (ENABLE_BASIC_AUTH, user ``user``, password BASIC_AUTH_PASSWORD or PASSWD) and
+HTTPS (ENABLE_HTTPS_WEB + HTTPS_WEB_CERT/KEY) follow the reference contract.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import ssl
+import time
+from pathlib import Path
+from typing import Any
+
+from aiohttp import WSMsgType, web
+
+from ..pipeline.stream import StreamPipeline, frame_header, h264_codec_string
+from . import turn
+from .auth import basic_auth_middleware
+from .input import SyntheticInjector, parse_message
+from .signalling import SignallingRelay
+
+log = logging.getLogger("mxdesk.server")
+WEB_ROOT = Path(__file__).resolve().parent.parent.parent / "web"
+
+
+def render_manifest(app_name: str = "mxdesk", short: str = "mxdesk", start_url: str = "/index.html") -> str:
+    """PWA manifest (reference templating: selkies-gstreamer-entrypoint.sh:27-38)."""
+    return json.dumps({
+        "name": app_name, "short_name": short, "start_url": start_url, "display": "fullscreen",
+        "background_color": "#000000", "theme_color": "#000000",
+        "icons": [{"src": "icon.svg", "sizes": "any", "type": "image/svg+xml"}],
+    }, indent=1)
+
+
+class MediaServer:
+    def __init__(self, pipeline: StreamPipeline, cfg: Any = None, injector: Any = None,
+                 web_root: Path | None = None, rfb: Any = None, start_pipeline: bool = True):
+        self.pipeline = pipeline
+        self.cfg = cfg
+        self.injector = injector or SyntheticInjector(pipeline, pipeline.out_w, pipeline.out_h)
+        self.web_root = Path(web_root) if web_root else WEB_ROOT
+        self.signalling = SignallingRelay()
+        self.rfb = rfb
+        self.start_pipeline = start_pipeline
+        self.clients: set[web.WebSocketResponse] = set()
+        self.resize_enabled = bool(getattr(cfg, "enable_resize", False))
+        from .gamepad import GamepadServer
+        from .webrtc import WhepEndpoint
+
+        self.gamepad = GamepadServer(getattr(cfg, "js_dir", None)) if bool(getattr(cfg, "enable_gamepad", True)) else None
+
+        self.audio = None
+        if bool(getattr(cfg, "enable_audio", False)):
+            from ..audio import AudioPipeline, make_source
+
+            try:
+                src = make_source(getattr(cfg, "audio_source", "auto"))
+            except (OSError, ValueError) as e:
+                log.warning("audio disabled: %s", e)
+                src = None
+            self.audio = AudioPipeline(src) if src is not None else None
+        self.whep = WhepEndpoint(pipeline, audio=self.audio,
+                                 congestion_control=bool(getattr(cfg, "congestion_control", False)), host=getattr(cfg, "webrtc_host", None) or None,
+                                 udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0))
+
+    # ------------------------------------------------------------------ app
+    def make_app(self) -> web.Application:
+        mws = []
+        if self.cfg is not None and getattr(self.cfg, "enable_basic_auth", False):
+            mws.append(basic_auth_middleware(getattr(self.cfg, "basic_auth_user", "user"),
+                                             self.cfg.effective_basic_auth_password))
+        app = web.Application(middlewares=mws)
+        app.router.add_get("/", self.index)
+        app.router.add_get("/index.html", self.index)
+        app.router.add_get("/health", self.health)
+        app.router.add_get("/turn", self.turn)
+        app.router.add_get("/turn/", self.turn)
+        app.router.add_get("/metrics", self.metrics)
+        app.router.add_get("/status", self.status)
+        app.router.add_get("/manifest.json", self.manifest)
+        app.router.add_get("/ws", self.signalling.handler)
+        app.router.add_get("/mxws", self.media_ws)
+        self.whep.routes(app)
+        if self.rfb is not None:
+            app.router.add_get("/websockify", self.rfb.ws_handler)
+        if self.web_root.is_dir():
+            app.router.add_static("/static/", self.web_root, show_index=False)
+            app.router.add_get("/{name:[A-Za-z0-9_.-]+\\.(?:js|css|svg|json|html)}", self.static_file)
+        app.on_startup.append(self._on_startup)
+        app.on_cleanup.append(self._on_cleanup)
+        return app
+
+    async def _on_startup(self, app):
+        if self.gamepad is not None:
+            try:
+                await self.gamepad.start()
+            except OSError as e:  # e.g. read-only /tmp: gamepads are optional
+                log.warning("gamepad sockets unavailable: %s", e)
+                self.gamepad = None
+        if self.start_pipeline:
+            self.pipeline.start()
+        if self.audio is not None:
+            self.audio.start()
+
+    async def _on_cleanup(self, app):
+        self.whep.close_all()
+        if self.audio is not None:
+            self.audio.stop()
+        if self.gamepad is not None:
+            await self.gamepad.stop()
+        self.pipeline.stop()
+        for ws in list(self.clients):
+            await ws.close()
+
+    # ------------------------------------------------------------------ http handlers
+    async def index(self, request: web.Request) -> web.StreamResponse:
+        f = self.web_root / "index.html"
+        if f.exists():
+            return web.FileResponse(f)
+        return web.Response(text="<html><body>mxdesk</body></html>", content_type="text/html")
+
+    async def static_file(self, request: web.Request) -> web.StreamResponse:
+        name = request.match_info["name"]
+        if name == "manifest.json":
+            return await self.manifest(request)
+        f = (self.web_root / name).resolve()
+        if self.web_root.resolve() not in f.parents or not f.is_file():
+            raise web.HTTPNotFound()
+        return web.FileResponse(f)
+
+    async def manifest(self, request: web.Request) -> web.Response:
+        return web.Response(text=render_manifest(), content_type="application/manifest+json")
+
+    async def health(self, request: web.Request) -> web.Response:
+        ok = not self.start_pipeline or self.pipeline.healthy() or self.pipeline.frames_out == 0
+        return web.Response(status=200 if ok else 503, text="OK" if ok else "STALLED")
+
+    async def turn(self, request: web.Request) -> web.Response:
+        cfg = self.cfg
+        if cfg is not None and getattr(cfg, "turn_rest_uri", None):
+            data = await turn.fetch_rest_credentials(cfg.turn_rest_uri, protocol=cfg.turn_protocol,
+                                                     tls=cfg.turn_tls)
+        else:
+            data = turn.rtc_config(cfg) if cfg is not None else {"iceServers": []}
+        return web.json_response(data)
+
+    async def metrics(self, request: web.Request) -> web.Response:
+        return web.Response(body=self.pipeline.metrics.exposition(), content_type="text/plain")
+
+    async def status(self, request: web.Request) -> web.Response:
+        return web.json_response(self.pipeline.status())
+
+    # ------------------------------------------------------------------ media websocket
+    async def media_ws(self, request: web.Request) -> web.WebSocketResponse:
+        ws = web.WebSocketResponse(heartbeat=10, max_msg_size=64 * 1024 * 1024)
+        await ws.prepare(request)
+        p = self.pipeline
+        # ?media=0: control/input channel only (the WebRTC client receives media over SRTP)
+        media = request.query.get("media", "1") != "0"
+        want_audio = media and self.audio is not None and request.query.get("audio", "1") != "0"
+        from ..audio.pipeline import CHANNELS, RATE
+
+        await ws.send_str(json.dumps({
+            "type": "config", "codec": h264_codec_string(p.out_w, p.out_h, p.fps), "width": p.out_w,
+            "height": p.out_h, "fps": p.fps, "resize": self.resize_enabled,
+            "audio": {"codec": "pcm_s16le", "rate": RATE, "channels": CHANNELS} if want_audio else None,
+        }))
+        sub = p.subscribe(asyncio.get_running_loop()) if media else None
+        self.clients.add(ws)
+        sender = asyncio.create_task(self._send_loop(ws, sub)) if media else None
+        asub = self.audio.subscribe(asyncio.get_running_loop()) if want_audio else None
+        asender = asyncio.create_task(self._audio_loop(ws, asub)) if want_audio else None
+        try:
+            async for msg in ws:
+                if msg.type == WSMsgType.TEXT:
+                    self._on_client_message(msg.data)
+                elif msg.type == WSMsgType.ERROR:
+                    break
+        finally:
+            if sender is not None:
+                sender.cancel()
+                p.unsubscribe(sub)
+            if asender is not None:
+                asender.cancel()
+                self.audio.unsubscribe(asub)
+            self.clients.discard(ws)
+        return ws
+
+    async def _send_loop(self, ws: web.WebSocketResponse, sub) -> None:
+        from .. import native
+
+        while not ws.closed:
+            fr = await sub.queue.get()
+            try:
+                await ws.send_bytes(frame_header(fr, native().now_us()) + fr.au)
+            except (ConnectionResetError, RuntimeError):
+                return
+
+    async def _audio_loop(self, ws: web.WebSocketResponse, sub) -> None:
+        from ..audio.pipeline import audio_message
+
+        while not ws.closed:
+            ch = await sub.queue.get()
+            try:
+                await ws.send_bytes(audio_message(ch))
+            except (ConnectionResetError, RuntimeError):
+                return
+
+    def _on_client_message(self, text: str) -> None:
+        ev = parse_message(text)
+        if ev is None:
+            return
+        p = self.pipeline
+        if ev.kind == "pli":
+            p.request_idr()
+        elif ev.kind == "bitrate":
+            p.set_bitrate(int(ev.value))
+        elif ev.kind == "ack":
+            # client-measured latency (same-clock clients) or RTT-based estimate
+            lat = ev.extra.get("latency_ms")
+            if lat is not None:
+                p.metrics.on_client_latency(float(lat))
+        elif ev.kind == "fps":
+            p.set_fps(ev.value)
+        elif ev.kind == "gamepad":
+            if self.gamepad is not None:
+                self.gamepad.apply(ev)
+        elif ev.kind == "resize":
+            if self.resize_enabled:
+                log.info("client resize request %dx%d (applied on next session restart)", ev.width, ev.height)
+        else:
+            self.injector.apply(ev)
+
+
+def ssl_context(cfg: Any) -> ssl.SSLContext | None:
+    if not getattr(cfg, "enable_https", False):
+        return None
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(cfg.https_cert, cfg.https_key)
+    return ctx
+
+
+async def serve(server: MediaServer, host: str, port: int, ssl_ctx: ssl.SSLContext | None = None) -> web.AppRunner:
+    runner = web.AppRunner(server.make_app())
+    await runner.setup()
+    site = web.TCPSite(runner, host, port, ssl_context=ssl_ctx)
+    await site.start()
+    log.info("serving on %s://%s:%d", "https" if ssl_ctx else "http", host, port)
+    return runner
+
+
+def run_forever(server: MediaServer, host: str, port: int, ssl_ctx: ssl.SSLContext | None = None) -> None:
+    async def main():
+        runner = await serve(server, host, port, ssl_ctx)
+        try:
+            while True:
+                await asyncio.sleep(3600)
+        finally:
+            await runner.cleanup()
+
+    try:
+        asyncio.run(main())
+    except KeyboardInterrupt:
+        pass
+
+
+def now_ms() -> float:
+    return time.monotonic() * 1000.0

@@ -1,0 +1,493 @@
+"""WebRTC media transport (replaces GStreamer webrtcbin + libnice + libsrtp
+of the reference's selkies pipeline, Dockerfile:439-444).
+
+* Signalling: WHEP-style HTTP offer/answer (``POST /whep`` with the browser's SDP offer ->
+  201 + SDP answer, ``DELETE /whep/<id>``); the selkies WebSocket relay (``/ws``) stays
+  available for selkies-style clients.
+* ICE-lite (RFC 8445 §2.5): one host candidate; connectivity checks answered with
+  MESSAGE-INTEGRITY/FINGERPRINT-protected Binding responses; the browser (full agent,
+  controlling) nominates.  TURN relays work because the browser allocates the relay.
+* DTLS-SRTP (RFC 5764): native OpenSSL endpoint (server role, ``a=setup:passive``), peer
+  certificate checked against the offer's ``a=fingerprint``; AES_CM_128_HMAC_SHA1_80 keys.
+* Media: native RFC 6184 packetizer (STAP-A / FU-A), native SRTP, 90 kHz timestamps from
+  the capture clock; RTCP PLI/FIR -> IDR, generic NACK -> retransmission from a packet
+  history, periodic SR + SDES.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import re
+import secrets
+import socket
+import struct
+import time
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+from ..utils.tracing import trace
+from . import rtp as R
+from . import stun as S
+
+log = logging.getLogger("mxdesk.webrtc")
+
+
+def _native():
+    from .. import native
+
+    return native()
+
+
+# ------------------------------------------------------------------ SDP
+@dataclass
+class MediaDesc:
+    kind: str
+    port: int
+    proto: str
+    fmts: list[str]
+    attrs: list[str] = field(default_factory=list)
+
+    def attr(self, name: str) -> str | None:
+        for a in self.attrs:
+            if a == name or a.startswith(name + ":"):
+                return a[len(name) + 1:] if ":" in a else ""
+        return None
+
+    def attrs_named(self, name: str) -> list[str]:
+        return [a[len(name) + 1:] for a in self.attrs if a.startswith(name + ":")]
+
+
+@dataclass
+class Sdp:
+    session: list[str]
+    media: list[MediaDesc]
+
+    def attr(self, name: str) -> str | None:
+        for line in self.session:
+            if line.startswith("a=" + name + ":"):
+                return line[len(name) + 3:]
+        return None
+
+
+def parse_sdp(text: str) -> Sdp:
+    session: list[str] = []
+    media: list[MediaDesc] = []
+    for line in text.replace("\r\n", "\n").split("\n"):
+        line = line.strip()
+        if not line:
+            continue
+        if line.startswith("m="):
+            kind, port, proto, *fmts = line[2:].split()
+            media.append(MediaDesc(kind, int(port), proto, fmts))
+        elif media:
+            if line.startswith("a="):
+                media[-1].attrs.append(line[2:])
+        else:
+            session.append(line)
+    return Sdp(session, media)
+
+
+def pick_h264(md: MediaDesc) -> str | None:
+    """Payload type of a packetization-mode=1 H.264 codec the browser accepts for our
+    Constrained Baseline stream (profile-level-id 42xxxx, preferring 42e0xx)."""
+    h264 = [r.split()[0] for r in md.attrs_named("rtpmap") if re.search(r"\sH264/90000", r, re.I)]
+    best = None
+    for pt in h264:
+        fmtp = next((f[len(pt) + 1:] for f in md.attrs_named("fmtp") if f.split()[0] == pt), "")
+        params = dict(kv.split("=", 1) for kv in fmtp.split(";") if "=" in kv)
+        if params.get("packetization-mode", "0") != "1":
+            continue
+        pli = params.get("profile-level-id", "42e01f").lower()
+        if pli.startswith("42"):
+            if pli.startswith("42e0"):
+                return pt
+            best = best or pt
+    return best
+
+
+@dataclass
+class Answer:
+    sdp: str
+    pt: int
+    mid: str
+    remote_ufrag: str
+    remote_pwd: str
+    remote_fingerprint: str
+    audio_pt: int | None = None  # PCMU (0) when the offer has an audio section and audio is on
+    audio_mid: str | None = None
+
+
+def _has_pcmu(md: MediaDesc) -> bool:
+    return "0" in md.fmts or any(re.search(r"\sPCMU/8000", r, re.I) for r in md.attrs_named("rtpmap"))
+
+
+def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
+                 level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None) -> Answer:
+    """Answer one H.264 video section (and, with ``audio_ssrc``, one PCMU audio section);
+    everything else is rejected with port 0.  All accepted sections are BUNDLEd onto the
+    single ICE-lite host candidate."""
+    offer = parse_sdp(offer_text)
+    lines = ["v=0", f"o=mxdesk {secrets.randbelow(1 << 62)} 2 IN IP4 {host}", "s=mxdesk", "t=0 0", "a=ice-lite",
+             "a=msid-semantic: WMS mxdesk"]
+    out_media: list[str] = []
+    chosen = None
+    audio = None  # (pt, mid)
+    bundle: list[str] = []
+    hosts = [host] + [h for h in (extra_hosts or []) if h != host]
+    cands = [f"a=candidate:{k + 1} 1 udp {2130706431 - k} {h} {port} typ host" for k, h in enumerate(hosts)]
+    transport = [f"c=IN IP4 {host}", *cands, "a=end-of-candidates",
+                 f"a=ice-ufrag:{ice_ufrag}", f"a=ice-pwd:{ice_pwd}", f"a=fingerprint:{fingerprint}", "a=setup:passive"]
+    for md in offer.media:
+        mid = md.attr("mid") or str(len(bundle) + len(out_media))
+        pt = pick_h264(md) if (md.kind == "video" and chosen is None) else None
+        ufrag = md.attr("ice-ufrag") or offer.attr("ice-ufrag")
+        pwd = md.attr("ice-pwd") or offer.attr("ice-pwd")
+        fp = md.attr("fingerprint") or offer.attr("fingerprint")
+        if pt is not None:
+            chosen = Answer("", int(pt), mid, ufrag or "", pwd or "", fp or "")
+            bundle.append(mid)
+            out_media += [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport,
+                          f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtcp-rsize",
+                          f"a=rtpmap:{pt} H264/90000", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
+                          f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb",
+                          f"a=fmtp:{pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}",
+                          f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
+            continue
+        if md.kind == "audio" and audio is None and audio_ssrc is not None and _has_pcmu(md):
+            audio = (0, mid)
+            bundle.append(mid)
+            out_media += [f"m=audio {port} UDP/TLS/RTP/SAVPF 0", *transport,
+                          f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtpmap:0 PCMU/8000",
+                          f"a=ssrc:{audio_ssrc} cname:mxdesk", f"a=ssrc:{audio_ssrc} msid:mxdesk audio0"]
+            continue
+        # reject (data channels, second video, audio when disabled)
+        out_media += [f"m={md.kind} 0 {md.proto} {md.fmts[0] if md.fmts else '0'}", "c=IN IP4 0.0.0.0",
+                      f"a=mid:{mid}", "a=inactive"]
+    if chosen is None:
+        raise ValueError("offer has no H.264 (packetization-mode=1, baseline-compatible) video section")
+    if audio is not None:
+        chosen.audio_pt, chosen.audio_mid = audio
+    lines.insert(4, "a=group:BUNDLE " + " ".join(bundle))
+    chosen.sdp = "\r\n".join(lines + out_media) + "\r\n"
+    return chosen
+
+
+def local_ips() -> list[str]:
+    """Non-loopback IPv4 addresses of this host (one ICE host candidate each)."""
+    try:
+        import psutil
+
+        out = [a.address for addrs in psutil.net_if_addrs().values() for a in addrs
+               if a.family == socket.AF_INET and not a.address.startswith("127.")]
+        return sorted(set(out))
+    except Exception:
+        return []
+
+
+def local_ip() -> str:
+    env = os.environ.get("MXDESK_WEBRTC_HOST")
+    if env:
+        return env
+    try:
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        s.connect(("10.255.255.255", 1))
+        ip = s.getsockname()[0]
+        s.close()
+        return ip
+    except OSError:
+        return "127.0.0.1"
+
+
+# ------------------------------------------------------------------ congestion control
+class CongestionController:
+    """``SELKIES_CONGESTION_CONTROL``: steer the encoder's CBR target from the receiver's
+    feedback -- REMB estimates (upper bound) and RTCP receiver-report loss (multiplicative
+    decrease above 10 % loss, +8 % additive-style probe below 2 %), never above the configured
+    bitrate."""
+
+    def __init__(self, pipeline, enabled: bool, min_kbps: int = 500):
+        self.pipeline = pipeline
+        self.enabled = enabled
+        self.max_kbps = int(getattr(pipeline, "bitrate_kbps", 0) or 8000)
+        self.kbps = self.max_kbps
+        self.min_kbps = min_kbps
+        self.remb_kbps: int | None = None
+
+    def _apply(self, kbps: float) -> None:
+        cap = min(self.max_kbps, self.remb_kbps or self.max_kbps)
+        new = int(max(self.min_kbps, min(cap, kbps)))
+        if self.enabled and abs(new - self.kbps) >= max(50, self.kbps // 50):
+            self.pipeline.set_bitrate(new)
+        self.kbps = new
+
+    def on_remb(self, bps: int) -> None:
+        self.remb_kbps = max(self.min_kbps, int(bps * 0.95) // 1000)
+        self._apply(self.kbps)
+
+    def on_loss(self, fraction: float) -> None:
+        if fraction > 0.10:
+            self._apply(self.kbps * (1.0 - 0.5 * fraction))
+        elif fraction < 0.02:
+            self._apply(self.kbps * 1.08)
+
+
+# ------------------------------------------------------------------ peer
+class WebRtcPeer(asyncio.DatagramProtocol):
+    HISTORY = 1024
+
+    def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
+                 audio=None, congestion_control: bool = False):
+        N = _native()
+        self.pipeline = pipeline
+        self.audio = audio
+        self.audio_ssrc = (secrets.randbits(32) | 1) if audio is not None else None
+        self.srtp_tx_audio = None
+        self.asub = None
+        self.id = secrets.token_hex(8)
+        self.ufrag = secrets.token_hex(4)
+        self.pwd = secrets.token_hex(16)
+        self.dtls = N.net.DtlsEndpoint(True)
+        self.ssrc = secrets.randbits(32) | 1
+        explicit = host or os.environ.get("MXDESK_WEBRTC_HOST")
+        self.host = explicit or local_ip()
+        # no explicit host: listen on all interfaces and offer every address as a candidate
+        self.bind_host = self.host if explicit else "0.0.0.0"
+        self.extra_hosts = [] if explicit else local_ips()
+        self.bind_port = port
+        self.level_idc = level_idc
+        self.offer_sdp = offer_sdp
+        self.transport: asyncio.DatagramTransport | None = None
+        self.remote: tuple[str, int] | None = None
+        self.srtp_tx = None
+        self.srtp_rx = None
+        self.pkt = None
+        self.history: OrderedDict[int, bytes] = OrderedDict()
+        self.answer: Answer | None = None
+        self.sub = None
+        self.tasks: list[asyncio.Task] = []
+        self.closed = asyncio.Event()
+        self.stats = {"stun": 0, "dtls_in": 0, "rtp_out": 0, "rtcp_in": 0, "pli": 0, "nack": 0, "rtx": 0}
+        self.last_consent = time.monotonic()
+        self.ts0: int | None = None
+        self.cc = CongestionController(pipeline, enabled=congestion_control)
+
+    async def start(self) -> str:
+        loop = asyncio.get_running_loop()
+        self.transport, _ = await loop.create_datagram_endpoint(lambda: self,
+                                                                local_addr=(self.bind_host, self.bind_port))
+        port = self.transport.get_extra_info("sockname")[1]
+        self.answer = build_answer(self.offer_sdp, self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port,
+                                   self.ssrc, self.level_idc, self.audio_ssrc, self.extra_hosts)
+        self.pkt = _native().net.RtpH264Packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
+        self.tasks.append(asyncio.create_task(self._timers()))
+        return self.answer.sdp
+
+    # ------------------------------------------------------------------ datagrams
+    def datagram_received(self, data: bytes, addr) -> None:
+        if not data:
+            return
+        b = data[0]
+        try:
+            if b < 4 and S.is_stun(data):
+                self._on_stun(data, addr)
+            elif 20 <= b <= 63:
+                self.stats["dtls_in"] += 1
+                self._send_all(self.dtls.feed(data), addr)
+                if self.dtls.handshake_done and self.srtp_tx is None:
+                    self._on_dtls_done()
+            elif 128 <= b <= 191 and len(data) > 1 and 192 <= data[1] <= 223:
+                self._on_rtcp(data)
+        except Exception:
+            log.exception("bad datagram from %s", addr)
+
+    def _send_all(self, dgrams, addr) -> None:
+        for d in dgrams:
+            self.transport.sendto(d, addr)
+
+    def _on_stun(self, data: bytes, addr) -> None:
+        m = S.StunMessage.decode(data)
+        if m.type != S.BINDING_REQUEST:
+            return
+        user = (m.get(S.A_USERNAME) or b"").decode(errors="replace")
+        if not user.startswith(self.ufrag + ":") or not m.check_integrity(self.pwd.encode()):
+            err = S.StunMessage(S.BINDING_ERROR, m.tid, [(S.A_ERROR_CODE, struct.pack("!HBB", 0, 4, 1) + b"Unauthorized")])
+            self.transport.sendto(err.encode(), addr)
+            return
+        self.stats["stun"] += 1
+        self.last_consent = time.monotonic()
+        resp = S.StunMessage(S.BINDING_SUCCESS, m.tid, [(S.A_XOR_MAPPED_ADDRESS, S.xor_address(addr[0], addr[1], m.tid))])
+        self.transport.sendto(resp.encode(self.pwd.encode()), addr)
+        if self.remote is None or m.get(S.A_USE_CANDIDATE) is not None:
+            self.remote = addr
+
+    def _on_dtls_done(self) -> None:
+        N = _native()
+        fp = self.dtls.peer_fingerprint
+        want = (self.answer.remote_fingerprint or "").strip()
+        if want and fp.lower() != want.lower():
+            log.error("DTLS fingerprint mismatch: %s != %s", fp, want)
+            self.close()
+            return
+        km = self.dtls.export_srtp_keys()
+        ck, sk, cs, ss = km[:16], km[16:32], km[32:46], km[46:60]
+        self.srtp_tx = N.net.SrtpSession(sk, ss)
+        self.srtp_rx = N.net.SrtpSession(ck, cs)
+        log.info("WebRTC peer %s: DTLS-SRTP up (%s)", self.id, self.dtls.srtp_profile)
+        self.sub = self.pipeline.subscribe(asyncio.get_running_loop())
+        self.tasks.append(asyncio.create_task(self._send_loop()))
+        if self.answer.audio_pt is not None and self.audio is not None:
+            # separate SRTP context per SSRC (own rollover counter / SRTCP index), same keys
+            self.srtp_tx_audio = N.net.SrtpSession(sk, ss)
+            self.asub = self.audio.subscribe(asyncio.get_running_loop())
+            self.tasks.append(asyncio.create_task(self._audio_loop()))
+
+    def _on_rtcp(self, data: bytes) -> None:
+        if self.srtp_rx is None:
+            return
+        pkt = self.srtp_rx.unprotect_rtcp(data)
+        if not pkt:
+            return
+        self.stats["rtcp_in"] += 1
+        for p in R.parse_rtcp(pkt):
+            if p["pt"] == 206 and p["fmt"] in (1, 4):  # PLI / FIR
+                self.stats["pli"] += 1
+                self.pipeline.request_idr()
+            elif "remb_bps" in p:
+                self.cc.on_remb(p["remb_bps"])
+            elif p["pt"] in (200, 201) and p.get("reports"):
+                for rb in p["reports"]:
+                    if rb["ssrc"] == self.ssrc:
+                        self.cc.on_loss(rb["fraction_lost"])
+            elif p["pt"] == 205 and p["fmt"] == 1:
+                self.stats["nack"] += 1
+                for seq in p.get("nack", []):
+                    raw = self.history.get(seq)
+                    if raw is not None and self.remote is not None:
+                        self.transport.sendto(self.srtp_tx.protect_rtp(raw), self.remote)
+                        self.stats["rtx"] += 1
+
+    # ------------------------------------------------------------------ media
+    async def _send_loop(self) -> None:
+        while not self.closed.is_set():
+            fr = await self.sub.queue.get()
+            if self.remote is None:
+                continue
+            if self.ts0 is None:
+                self.ts0 = fr.t_capture_us
+            ts = ((fr.t_capture_us - self.ts0) * 9 // 100) & 0xFFFFFFFF  # 90 kHz
+            with trace("mxdesk.webrtc.packetize+srtp+send"):
+                for raw in self.pkt.packetize(fr.au, ts):
+                    seq = struct.unpack_from("!H", raw, 2)[0]
+                    self.history[seq] = raw
+                    if len(self.history) > self.HISTORY:
+                        self.history.popitem(last=False)
+                    self.transport.sendto(self.srtp_tx.protect_rtp(raw), self.remote)
+                    self.stats["rtp_out"] += 1
+            self.last_ts = ts
+
+    async def _audio_loop(self) -> None:
+        """48 kHz stereo chunks -> 8 kHz mono (native FIR decimator) -> 20 ms PCMU packets."""
+        import numpy as np
+
+        A = _native().audio
+        dec = A.Decimator(6, 2)
+        pending = np.zeros(0, np.int16)
+        seq = secrets.randbits(16)
+        ts = secrets.randbits(32)
+        first = True
+        self.audio_packets = 0
+        while not self.closed.is_set():
+            ch = await self.asub.queue.get()
+            pending = np.concatenate([pending, dec.process(ch.pcm)])
+            while len(pending) >= 160 and self.remote is not None:
+                frame, pending = pending[:160], pending[160:]
+                hdr = struct.pack("!BBHII", 0x80, (0x80 if first else 0) | self.answer.audio_pt, seq, ts,
+                                  self.audio_ssrc)
+                self.transport.sendto(self.srtp_tx_audio.protect_rtp(hdr + A.encode_ulaw(frame)), self.remote)
+                first = False
+                seq = (seq + 1) & 0xFFFF
+                ts = (ts + 160) & 0xFFFFFFFF
+                self.audio_packets += 1
+                self.audio_octets = getattr(self, "audio_octets", 0) + 160
+                self.audio_ts = ts
+
+    async def _timers(self) -> None:
+        last_sr = 0.0
+        while not self.closed.is_set():
+            await asyncio.sleep(0.05)
+            if self.remote is not None and not self.dtls.handshake_done:
+                self._send_all(self.dtls.tick(), self.remote)
+            now = time.monotonic()
+            if self.srtp_tx is not None and self.remote is not None and now - last_sr > 1.0:
+                sr = R.build_sr(self.ssrc, getattr(self, "last_ts", 0), self.pkt.packets, self.pkt.octets)
+                self.transport.sendto(self.srtp_tx.protect_rtcp(sr), self.remote)
+                if self.srtp_tx_audio is not None and getattr(self, "audio_packets", 0):
+                    asr = R.build_sr(self.audio_ssrc, self.audio_ts, self.audio_packets, self.audio_octets)
+                    self.transport.sendto(self.srtp_tx_audio.protect_rtcp(asr), self.remote)
+                last_sr = now
+            if now - self.last_consent > 30.0:  # consent freshness (RFC 7675)
+                log.info("WebRTC peer %s: consent expired", self.id)
+                self.close()
+
+    def close(self) -> None:
+        if self.closed.is_set():
+            return
+        self.closed.set()
+        if self.sub is not None:
+            self.pipeline.unsubscribe(self.sub)
+        if self.asub is not None:
+            self.audio.unsubscribe(self.asub)
+        for t in self.tasks:
+            t.cancel()
+        if self.transport is not None:
+            self.transport.close()
+
+
+class WhepEndpoint:
+    """``POST /whep`` (application/sdp offer) -> 201 answer; ``DELETE /whep/{id}``."""
+
+    def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A, audio=None,
+                 congestion_control: bool = False):
+        self.pipeline = pipeline
+        self.audio = audio
+        self.congestion_control = congestion_control
+        self.host = host
+        self.udp_port = udp_port
+        self.level_idc = level_idc
+        self.peers: dict[str, WebRtcPeer] = {}
+        self.last_peer: WebRtcPeer | None = None
+
+    def routes(self, app) -> None:
+        app.router.add_post("/whep", self.post)
+        app.router.add_delete("/whep/{pid}", self.delete)
+
+    async def post(self, request):
+        from aiohttp import web
+
+        offer = await request.text()
+        peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc, audio=self.audio,
+                          congestion_control=self.congestion_control)
+        try:
+            answer = await peer.start()
+        except ValueError as e:
+            peer.close()
+            raise web.HTTPBadRequest(text=str(e))
+        self.peers[peer.id] = peer
+        self.last_peer = peer
+        return web.Response(status=201, text=answer, content_type="application/sdp",
+                            headers={"Location": f"/whep/{peer.id}"})
+
+    async def delete(self, request):
+        from aiohttp import web
+
+        peer = self.peers.pop(request.match_info["pid"], None)
+        if peer is None:
+            raise web.HTTPNotFound()
+        peer.close()
+        return web.Response(status=200)
+
+    def close_all(self) -> None:
+        for p in list(self.peers.values()):
+            p.close()
+        self.peers.clear()

@@ -1,0 +1,224 @@
+"""Headless WHEP/WebRTC viewer: plays the browser's role against ``POST /whep`` (full ICE
+agent in the controlling role, DTLS client, SRTP receiver, RTCP PLI/NACK sender).  Used by the
+loopback tests and as a CLI smoke-check of a running server (``python -m mxdesk.server.whep_client``).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import secrets
+import struct
+import time
+from dataclasses import dataclass, field
+
+from . import rtp as R
+from . import stun as S
+from .webrtc import parse_sdp
+
+
+def _native():
+    from .. import native
+
+    return native()
+
+
+def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_audio: bool = True) -> str:
+    lines = ["v=0", "o=- 4611731400430051336 2 IN IP4 127.0.0.1", "s=-", "t=0 0", "a=group:BUNDLE 0 1",
+             "a=msid-semantic: WMS"]
+    media = []
+    if with_audio:
+        media += ["m=audio 9 UDP/TLS/RTP/SAVPF 111 0", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
+                  f"a=ice-pwd:{pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:1", "a=recvonly",
+                  "a=rtcp-mux", "a=rtpmap:111 opus/48000/2", "a=rtpmap:0 PCMU/8000"]
+    media = ["m=video 9 UDP/TLS/RTP/SAVPF 96 %d 108" % h264_pt, "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
+             f"a=ice-pwd:{pwd}", "a=ice-options:trickle", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:0",
+             "a=recvonly", "a=rtcp-mux", "a=rtcp-rsize", "a=rtpmap:96 VP8/90000",
+             f"a=rtpmap:{h264_pt} H264/90000", f"a=rtcp-fb:{h264_pt} nack", f"a=rtcp-fb:{h264_pt} nack pli",
+             f"a=fmtp:{h264_pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e01f",
+             "a=rtpmap:108 H264/90000", "a=fmtp:108 packetization-mode=0;profile-level-id=42e01f"] + media
+    return "\r\n".join(lines + media) + "\r\n"
+
+
+@dataclass
+class WhepResult:
+    aus: list[bytes] = field(default_factory=list)
+    rtp_ts: list[int] = field(default_factory=list)
+    packets: int = 0
+    lost: int = 0
+    rtx: int = 0
+    srs: int = 0
+    answer: str = ""
+    connect_ms: float = 0.0
+    stream: bytes = b""
+    arrival_us: list[int] = field(default_factory=list)  # CLOCK_MONOTONIC us when each AU completed
+    audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
+    audio_seqs: list[int] = field(default_factory=list)
+
+
+class _Client(asyncio.DatagramProtocol):
+    def __init__(self):
+        self.q: asyncio.Queue = asyncio.Queue()
+
+    def connection_made(self, transport):
+        self.transport = transport
+
+    def datagram_received(self, data, addr):
+        self.q.put_nowait(data)
+
+
+async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
+                    timeout: float = 30.0) -> WhepResult:
+    """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
+
+    ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
+    ``pli_after``: send a PLI after that many frames (the server must answer with an IDR).
+    """
+    import aiohttp
+
+    N = _native()
+    dtls = N.net.DtlsEndpoint(False)
+    ufrag, pwd = secrets.token_hex(4), secrets.token_hex(12)
+    offer = make_offer(ufrag, pwd, dtls.fingerprint)
+    res = WhepResult()
+    t0 = time.monotonic()
+    async with aiohttp.ClientSession(auth=auth) as s:
+        async with s.post(url, data=offer, headers={"Content-Type": "application/sdp"}) as r:
+            if r.status != 201:
+                raise RuntimeError(f"WHEP POST failed: {r.status} {await r.text()}")
+            res.answer = await r.text()
+            location = r.headers["Location"]
+    ans = parse_sdp(res.answer)
+    vid = next(m for m in ans.media if m.kind == "video" and m.port)
+    cand = vid.attr("candidate").split()
+    host, port = cand[4], int(cand[5])
+    r_ufrag, r_pwd = vid.attr("ice-ufrag"), vid.attr("ice-pwd")
+    r_fp = vid.attr("fingerprint")
+    loop = asyncio.get_running_loop()
+    tr, cl = await loop.create_datagram_endpoint(_Client, remote_addr=(host, port))
+    deadline = time.monotonic() + timeout
+    try:
+        # ICE connectivity check (controlling, nominating)
+        req = S.StunMessage(S.BINDING_REQUEST, None, [
+            (S.A_USERNAME, f"{r_ufrag}:{ufrag}".encode()), (S.A_PRIORITY, struct.pack("!I", 1853824767)),
+            (S.A_ICE_CONTROLLING, os.urandom(8)), (S.A_USE_CANDIDATE, b"")])
+        tr.sendto(req.encode(r_pwd.encode()))
+        while True:
+            d = await asyncio.wait_for(cl.q.get(), max(0.1, deadline - time.monotonic()))
+            if S.is_stun(d):
+                m = S.StunMessage.decode(d)
+                if m.type == S.BINDING_SUCCESS and m.tid == req.tid:
+                    if not m.check_integrity(r_pwd.encode()):
+                        raise RuntimeError("bad MESSAGE-INTEGRITY in binding response")
+                    break
+        for dg in dtls.start():
+            tr.sendto(dg)
+        while not dtls.handshake_done:
+            try:
+                d = await asyncio.wait_for(cl.q.get(), 0.1)
+            except asyncio.TimeoutError:
+                for dg in dtls.tick():
+                    tr.sendto(dg)
+                if time.monotonic() > deadline:
+                    raise RuntimeError("DTLS handshake timed out")
+                continue
+            if 20 <= d[0] <= 63:
+                for dg in dtls.feed(d):
+                    tr.sendto(dg)
+            if dtls.failed:
+                raise RuntimeError("DTLS failed: " + dtls.error)
+        if dtls.peer_fingerprint.lower() != r_fp.lower():
+            raise RuntimeError("server fingerprint mismatch")
+        km = dtls.export_srtp_keys()
+        rx_ctx: dict[int, object] = {}  # one SRTP receive context per SSRC (own rollover counter)
+
+        def rx_for(pkt: bytes):
+            ssrc = struct.unpack_from("!I", pkt, 4 if 192 <= pkt[1] <= 223 else 8)[0]
+            if ssrc not in rx_ctx:
+                rx_ctx[ssrc] = N.net.SrtpSession(km[16:32], km[46:60])  # server -> client
+            return rx_ctx[ssrc]
+        tx = N.net.SrtpSession(km[0:16], km[32:46])   # client -> server (RTCP)
+        res.connect_ms = (time.monotonic() - t0) * 1000
+        my_ssrc = secrets.randbits(32)
+        depk = R.H264Depacketizer()
+        pending: dict[int, bytes] = {}
+        next_seq = None
+        n_pkts = 0
+        sent_pli = False
+        nacked: set[int] = set()
+        media_ssrc = 0
+        while len(res.aus) < n_frames:
+            d = await asyncio.wait_for(cl.q.get(), max(0.1, deadline - time.monotonic()))
+            if not 128 <= d[0] <= 191:
+                continue
+            if 192 <= d[1] <= 223:
+                p = rx_for(d).unprotect_rtcp(d)
+                if p and any(x["pt"] == 200 for x in R.parse_rtcp(p)):
+                    res.srs += 1
+                continue
+            p = rx_for(d).unprotect_rtp(d)
+            if not p:
+                raise RuntimeError("SRTP authentication failed")
+            h = R.rtp_header(p)
+            if h["pt"] == 0:  # PCMU audio
+                res.audio_payloads.append(h["payload"])
+                res.audio_seqs.append(h["seq"])
+                continue
+            res.packets += 1
+            media_ssrc = h["ssrc"]
+            seq = h["seq"]
+            if next_seq is None:
+                next_seq = seq
+            if seq in pending or ((seq - next_seq) & 0xFFFF) > 0x8000:
+                continue  # duplicate / already delivered
+            n_pkts += 1
+            if drop_seq_every and n_pkts % drop_seq_every == 0 and seq not in nacked:
+                res.lost += 1
+                nacked.add(seq)
+                tr.sendto(tx.protect_rtcp(R.build_nack(my_ssrc, media_ssrc, [seq])))
+                continue
+            if seq in nacked:
+                res.rtx += 1
+            pending[seq] = p
+            while next_seq in pending:  # in-order delivery to the depacketizer
+                pk = pending.pop(next_seq)
+                au = depk.push(pk)
+                if au is not None:
+                    res.aus.append(au)
+                    res.rtp_ts.append(R.rtp_header(pk)["ts"])
+                    res.arrival_us.append(time.monotonic_ns() // 1000)
+                    if pli_after and len(res.aus) == pli_after and not sent_pli:
+                        tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
+                        sent_pli = True
+                next_seq = (next_seq + 1) & 0xFFFF
+        res.stream = b"".join(res.aus)
+    finally:
+        tr.close()
+        try:
+            async with aiohttp.ClientSession(auth=auth) as s:
+                base = url.rsplit("/whep", 1)[0]
+                async with s.delete(base + location):
+                    pass
+        except Exception:
+            pass
+    return res
+
+
+def main(argv=None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(description="headless WHEP viewer")
+    ap.add_argument("url")
+    ap.add_argument("--frames", type=int, default=120)
+    ap.add_argument("--user")
+    ap.add_argument("--password")
+    a = ap.parse_args(argv)
+    import aiohttp
+
+    auth = aiohttp.BasicAuth(a.user, a.password) if a.user else None
+    r = asyncio.run(whep_view(a.url, a.frames, auth))
+    print(f"frames={len(r.aus)} packets={r.packets} bytes={len(r.stream)} connect_ms={r.connect_ms:.1f}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
