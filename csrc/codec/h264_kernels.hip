@@ -138,32 +138,18 @@ __global__ __launch_bounds__(256) void k_hpel(Geometry g, const FrameState* __re
         b1[r][c] = (int16_t)tap6(smp[r][c], smp[r][c + 1], smp[r][c + 2], smp[r][c + 3], smp[r][c + 4], smp[r][c + 5]);
     }
     __syncthreads();
-    // 4 adjacent outputs per thread -> one dword store per plane (W is a multiple of 16 and
-    // px0 of 64, so a quad is either fully inside or fully outside the padded plane)
-    static_assert(kHpTH * kHpTW / 4 == 256, "one quad per thread");
-    {
-        const int r = tid / (kHpTW / 4), c0 = (tid % (kHpTW / 4)) * 4;
-        const int x = px0 + c0, y = py0 + r;
-        if (x < W && y < H) {
-            const int rr = r + 2;
-            uint32_t wf = 0, wh = 0, wv = 0, wj = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int c = c0 + k, cc = c + 2;
-                wf |= (uint32_t)smp[rr][cc] << (8 * k);
-                wh |= (uint32_t)clip255((b1[rr][c] + 16) >> 5) << (8 * k);
-                const int v1 =
-                    tap6(smp[rr - 2][cc], smp[rr - 1][cc], smp[rr][cc], smp[rr + 1][cc], smp[rr + 2][cc], smp[rr + 3][cc]);
-                wv |= (uint32_t)clip255((v1 + 16) >> 5) << (8 * k);
-                const int j1 = tap6(b1[rr - 2][c], b1[rr - 1][c], b1[rr][c], b1[rr + 1][c], b1[rr + 2][c], b1[rr + 3][c]);
-                wj |= (uint32_t)clip255((j1 + 512) >> 10) << (8 * k);
-            }
-            const size_t o = (size_t)y * hp_pitch + x;
-            *reinterpret_cast<uint32_t*>(pf + o) = wf;
-            *reinterpret_cast<uint32_t*>(ph + o) = wh;
-            *reinterpret_cast<uint32_t*>(pv + o) = wv;
-            *reinterpret_cast<uint32_t*>(pj + o) = wj;
-        }
+    for (int i = tid; i < kHpTH * kHpTW; i += 256) {
+        const int r = i / kHpTW, c = i - r * kHpTW;
+        const int x = px0 + c, y = py0 + r;
+        if (x >= W || y >= H) continue;
+        const int rr = r + 2, cc = c + 2;
+        const size_t o = (size_t)y * hp_pitch + x;
+        pf[o] = smp[rr][cc];
+        ph[o] = (uint8_t)clip255((b1[rr][c] + 16) >> 5);
+        const int v1 = tap6(smp[rr - 2][cc], smp[rr - 1][cc], smp[rr][cc], smp[rr + 1][cc], smp[rr + 2][cc], smp[rr + 3][cc]);
+        pv[o] = (uint8_t)clip255((v1 + 16) >> 5);
+        const int j1 = tap6(b1[rr - 2][c], b1[rr - 1][c], b1[rr][c], b1[rr + 1][c], b1[rr + 2][c], b1[rr + 3][c]);
+        pj[o] = (uint8_t)clip255((j1 + 512) >> 10);
     }
 }
 
