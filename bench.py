@@ -10,8 +10,10 @@ one 1920x1080 session of the flagship pipeline on its GPU:
     quant, recon, CAVLC, bit packing) -> Annex-B access unit in host memory
 
 A "step" is one encoded frame.  Frames are encoded back-to-back (unpaced) to measure the
-encoder's capacity; E2E latency is render-start -> access unit available on the host, per
-frame.  `value` is the whole-job aggregate encoded FPS (sum over GPUs, total frames /
+encoder's capacity, with two frames in flight per session by default (frame n's entropy
+coding overlaps frame n+1's analysis on a second HIP stream, as hardware encoders pipeline);
+E2E latency is render-start -> access unit available on the host, per frame, measured in the
+same run (so it includes the pipelining queueing).  `value` is the whole-job aggregate encoded FPS (sum over GPUs, total frames /
 slowest rank's time).  Weak scaling: per-GPU work is fixed as N grows.
 
 The reference publishes no numbers, so vs_baseline is null; the reference's
@@ -46,8 +48,9 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
-    ap.add_argument("--depth", type=int, default=1,
-                    help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1)")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1; "
+                         "1: strictly one frame at a time, lowest back-to-back latency)")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
