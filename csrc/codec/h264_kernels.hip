@@ -233,25 +233,43 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         }
     }
 
-    const int side = 2 * R + 1, ncand = side * side;
+    // Each thread scores four horizontally adjacent candidates per step: their 16x16 blocks
+    // share one dword-aligned 20-byte row span of the window, so every row costs 5 LDS reads
+    // (instead of 5 per candidate), 12 v_alignbyte and 16 v_sad_u8.
+    const int side = 2 * R + 1, gw = (side + 3) >> 2, ngroups = side * gw;
     unsigned long long best = ~0ull;
-    for (int c = tid; c < ncand; c += 256) {
-        const int dy = c / side - R, dx = c - (c / side) * side - R;
-        uint32_t sad = 0;
-#pragma unroll 4
+    for (int q = tid; q < ngroups; q += 256) {
+        const int dyr = q / gw, g = q - dyr * gw;
+        uint32_t sad[4] = {0, 0, 0, 0};
+#pragma unroll 2
         for (int r = 0; r < 16; ++r) {
-            const int base = (dy + R + r) * kWinStride + (dx + R);
-            const int a = base >> 2, sh = base & 3;
+            const int a = (dyr + r) * kWs4 + g;
             const uint32_t w0 = win32[a], w1 = win32[a + 1], w2 = win32[a + 2], w3 = win32[a + 3], w4 = win32[a + 4];
-            sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, sh), srcw[r * 4 + 0], sad);
-            sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w2, w1, sh), srcw[r * 4 + 1], sad);
-            sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w3, w2, sh), srcw[r * 4 + 2], sad);
-            sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w4, w3, sh), srcw[r * 4 + 3], sad);
+            const uint32_t s0 = srcw[r * 4 + 0], s1 = srcw[r * 4 + 1], s2 = srcw[r * 4 + 2], s3 = srcw[r * 4 + 3];
+            sad[0] = __builtin_amdgcn_sad_u8(w0, s0, sad[0]);
+            sad[0] = __builtin_amdgcn_sad_u8(w1, s1, sad[0]);
+            sad[0] = __builtin_amdgcn_sad_u8(w2, s2, sad[0]);
+            sad[0] = __builtin_amdgcn_sad_u8(w3, s3, sad[0]);
+#pragma unroll
+            for (int sh = 1; sh < 4; ++sh) {
+                uint32_t t = sad[sh];
+                t = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, sh), s0, t);
+                t = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w2, w1, sh), s1, t);
+                t = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w3, w2, sh), s2, t);
+                t = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w4, w3, sh), s3, t);
+                sad[sh] = t;
+            }
         }
-        const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
-        const uint32_t dist = (uint32_t)(abs(dx) + abs(dy));
-        const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
-        best = key < best ? key : best;
+#pragma unroll
+        for (int sh = 0; sh < 4; ++sh) {
+            const int dxr = 4 * g + sh;
+            if (dxr >= side) break;
+            const int dx = dxr - R, dy = dyr - R, c = dyr * side + dxr;
+            const uint32_t cost = me_cost(sad[sh], lambda, 4 * dx, 4 * dy);
+            const uint32_t dist = (uint32_t)(abs(dx) + abs(dy));
+            const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
+            best = key < best ? key : best;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         unsigned long long other = __shfl_xor(best, o, 64);
