@@ -201,25 +201,13 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     const Planes P = planes_of(fs);
     const int lambda = lambda_sad(fs->qp);
 
-    // search window from the padded full-sample plane with dword loads (x0 - R is a
-    // multiple of 4 and R + 2 <= kHpelPad: no clamping, no byte gathers)
+    // static-block early exit first: SAD of the zero vector from one source and one reference
+    // pixel per thread (same rule as the CPU encoder), so the ~70 % static MBs of a desktop
+    // never load the search window
     constexpr int kWs4 = kWinStride / 4;
-    for (int i = tid; i < W * kWs4; i += 256) {
-        const int wy = i / kWs4, wx4 = (i - wy * kWs4) * 4;
-        win32[i] = (wx4 < W) ? *reinterpret_cast<const uint32_t*>(P.f + (y0 - R + wy) * P.pitch + (x0 - R + wx4)) : 0u;
-    }
-    if (tid < 64) {
-        const int r = tid >> 2, c = (tid & 3) * 4;
-        srcw[tid] = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c);
-    }
-    __syncthreads();
-
-    // static-block early exit: SAD of the zero vector (same rule as the CPU encoder)
     {
-        const int r = tid >> 4, c4 = (tid & 15) >> 2, k = tid & 3;  // tid<256 covers 16 rows x 16 px
-        const uint32_t sw = srcw[r * 4 + c4];
-        const uint8_t* win = reinterpret_cast<const uint8_t*>(win32);
-        int d = abs((int)((sw >> (8 * k)) & 0xff) - (int)win[(R + r) * kWinStride + R + c4 * 4 + k]);
+        const int r = tid >> 4, c = tid & 15;  // 256 threads = 16 rows x 16 px
+        int d = abs((int)src_y[(y0 + r) * g.pitch + x0 + c] - (int)P.f[(y0 + r) * P.pitch + x0 + c]);
         d = wave_sum(d);
         if (lane == 0) s_sad0[tid >> 6] = d;
         __syncthreads();
@@ -232,6 +220,17 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             return;  // uniform across the workgroup
         }
     }
+    // search window from the padded full-sample plane with dword loads (x0 - R is a
+    // multiple of 4 and R + 2 <= kHpelPad: no clamping, no byte gathers)
+    for (int i = tid; i < W * kWs4; i += 256) {
+        const int wy = i / kWs4, wx4 = (i - wy * kWs4) * 4;
+        win32[i] = (wx4 < W) ? *reinterpret_cast<const uint32_t*>(P.f + (y0 - R + wy) * P.pitch + (x0 - R + wx4)) : 0u;
+    }
+    if (tid < 64) {
+        const int r = tid >> 2, c = (tid & 3) * 4;
+        srcw[tid] = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c);
+    }
+    __syncthreads();
 
     // Each thread scores four horizontally adjacent candidates per step: their 16x16 blocks
     // share one dword-aligned 20-byte row span of the window, so every row costs 5 LDS reads
