@@ -62,9 +62,8 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
     const uint8_t* ref_uv = rec_uv_[cur_ ^ 1].data();
     uint8_t* rec_y = rec_y_[cur_].data();
     uint8_t* rec_uv = rec_uv_[cur_].data();
-    const int qp = common_.cur_qp();
-    const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
-    const int lambda = lambda_sad(qp);
+    const int frame_qp = common_.cur_qp();
+    const int lambda = lambda_sad(frame_qp);
     const int R = me_range(cfg_.search_range);
     const int side = 2 * R + 1;
     for (int mby = 0; mby < g.mb_h; ++mby)
@@ -127,12 +126,17 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             m.type = kMbP16x16;
             // ---- prediction + residual
             int pred[384], res[384];
+            uint32_t lsad = 0;
             for (int r = 0; r < 16; ++r)
                 for (int k = 0; k < 16; ++k) {
                     const int p = luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
                     pred[r * 16 + k] = p;
                     res[r * 16 + k] = sy[(y0 + r) * pitch + x0 + k] - p;
+                    lsad += (uint32_t)std::abs(res[r * 16 + k]);
                 }
+            const int qp = aq_mb_qp(frame_qp, lsad, cfg_.aq);
+            const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+            m.qp = (uint8_t)qp;
             for (int comp = 0; comp < 2; ++comp)
                 for (int r = 0; r < 8; ++r)
                     for (int k = 0; k < 8; ++k) {
@@ -208,6 +212,7 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
             const bool have_left = mbx > 0;
             MbInfo& m = mb_[mbi];
             std::memset(&m, 0, sizeof m);
+            m.qp = (uint8_t)qp;
             int dcl = 128;
             if (have_left) {
                 int s = 0;
@@ -348,6 +353,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         write_slice_header(w, make_slice_params(first, idr, common_.cur_frame_num(), common_.log2_max_frame_num(),
                                                 common_.cur_idr_pic_id(), common_.cur_qp() - common_.pic_init_qp(), 1));
         int run = 0;
+        int qp_pred = common_.cur_qp();  // mb_qp_delta predictor: QP of the last MB that carried one
         for (int mbi = first; mbi < last; ++mbi) {
             const Avail av = mb_avail(g, mbi % g.mb_w, mbi / g.mb_w, slice_rows);
             int mvdx, mvdy;
@@ -362,8 +368,13 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
                 run = 0;
             }
             const int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
+            int dqp = 0;
+            if (!idr && mb_[mbi].cbp != 0) {
+                dqp = qp_delta(mb_[mbi].qp, qp_pred);
+                qp_pred = mb_[mbi].qp;
+            }
             for (int role = 0; role < kNumRoles; ++role)
-                code_role(w, role, g, idr, mb_.data(), mb_[mbi], mc, mbi, av, mvdx, mvdy);
+                code_role(w, role, g, idr, mb_.data(), mb_[mbi], mc, mbi, av, mvdx, mvdy, dqp);
         }
         if (!idr && run > 0) put_ue(w, (uint32_t)run);
         w.put(1, 1);

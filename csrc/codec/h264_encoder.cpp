@@ -288,6 +288,7 @@ bool GpuH264Encoder::prepare(bool force_idr) {
     f.log2_max_frame_num = common_.log2_max_frame_num();
     const size_t org = (size_t)kHpelPad * hp_pitch_ + kHpelPad;
     f.hp_pitch = hp_pitch_;
+    f.aq = cfg_.aq;
     f.hp_f = hp_[0] + org;
     f.hp_h = hp_[1] + org;
     f.hp_v = hp_[2] + org;

@@ -31,6 +31,7 @@ struct EncoderConfig {
     int search_range = 16;    // integer-pel full search radius (<= 32)
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
+    int aq = 1;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta)
     int pipeline_depth = 1;   // GPU frames in flight: 2 overlaps frame n's entropy coding with
                               // frame n+1's analysis on a second HIP stream (rate control lags a frame)
 };

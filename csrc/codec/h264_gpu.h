@@ -32,7 +32,8 @@ struct MbInfo {
     uint8_t nz_cb[4];     // chroma AC TotalCoeff, raster 2x2
     uint8_t nz_cr[4];
     uint8_t skip;  // set by k_cavlc
-    uint8_t pad[3];
+    uint8_t qp;    // macroblock QP (frame QP + adaptive-quantisation offset)
+    uint8_t pad[2];
 };
 static_assert(sizeof(MbInfo) == 36, "MbInfo layout");
 
@@ -56,7 +57,7 @@ struct FrameState {
     int32_t chroma_qp_offset;
     int32_t log2_max_frame_num;
     int32_t hp_pitch;  // pitch of the padded half-pel planes
-    int32_t pad;
+    int32_t aq;        // adaptive quantisation on/off (P frames)
     // padded reference planes (origin at picture (0,0), valid for x,y in [-kHpelPad, size+kHpelPad))
     const uint8_t* hp_f;  // full-sample (edge-replicated)
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)

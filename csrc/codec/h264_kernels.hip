@@ -353,12 +353,11 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     const bool valid = mbi < nmb;
     const int mbx = valid ? mbi % g.mb_w : 0, mby = valid ? mbi / g.mb_w : 0;
     const int x0 = mbx * 16, y0 = mby * 16;
-    const int qp = fs->qp;
-    const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     const Planes P = planes_of(fs);
     const uint8_t* ref_uv = fs->ref_uv;
     const int cw = g.coded_w / 2, ch = g.coded_h / 2;
     int mvx = 0, mvy = 0;
+    int lsad = 0;  // this lane's share of sum |luma residual| (adaptive quantisation)
     if (valid) {
         mvx = mbs[mbi].mvx;
         mvy = mbs[mbi].mvy;
@@ -366,8 +365,10 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
         for (int k = 0; k < 4; ++k) {
             const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
+            const int d = (int)((sw >> (8 * k)) & 0xff) - p;
             pred[wave][r * 16 + c0 + k] = (uint8_t)p;
-            res[wave][r * 16 + c0 + k] = (int16_t)((int)((sw >> (8 * k)) & 0xff) - p);
+            res[wave][r * 16 + c0 + k] = (int16_t)d;
+            lsad += d < 0 ? -d : d;
         }
         const int cr_ = lane >> 3, cc = lane & 7;
         const int xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
@@ -379,6 +380,8 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         }
     }
     __syncthreads();
+    const int qp = aq_mb_qp(fs->qp, (uint32_t)wave_sum(lsad), fs->aq);  // wave-uniform
+    const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
 
     int z[16];
     int nz = 0;
@@ -474,6 +477,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         MbInfo& m = mbs[mbi];
         m.type = kMbP16x16;
         m.cbp = (uint8_t)cbp;
+        m.qp = (uint8_t)qp;
         m.i16_mode = 0;
         m.chroma_mode = 0;
     }
@@ -649,6 +653,7 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
             const int ccbp = (chroma_mask != 0) ? 2 : ((cdc_nz[0] | cdc_nz[1]) ? 1 : 0);
             MbInfo& m = mbs[mbi];
             m.type = kMbI16x16;
+            m.qp = (uint8_t)qp;
             m.cbp = (uint8_t)((luma_ac ? 15 : 0) | (ccbp << 4));
             m.i16_mode = (uint8_t)lmode;
             m.chroma_mode = (uint8_t)cmode;
@@ -709,11 +714,28 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     // motion vector prediction + P_Skip decision (every lane computes the same values)
     int mvdx = 0, mvdy = 0;
     const bool skip = decide_skip(g, mbs, mbi, av, &mvdx, &mvdy);
+    // mb_qp_delta: QP predictor = QP of the previous MB in the slice that carried one (a P
+    // macroblock with residual); skipped / residual-free MBs inherit it.  Wave-parallel
+    // backward search, 64 MBs per step.  I slices: every MB is at the slice QP.
+    int dqp = 0;
+    if (!skip && !fs->idr && m.cbp != 0) {
+        const int per_slice = fs->slice_rows * g.mb_w, first = (mbi / per_slice) * per_slice;
+        int pred = fs->qp;
+        for (int j0 = mbi - 1; j0 >= first; j0 -= 64) {
+            const int j = j0 - lane;
+            const unsigned long long bal = __ballot(j >= first && mbs[j].cbp != 0);
+            if (bal) {
+                pred = mbs[j0 - (__ffsll((long long)bal) - 1)].qp;
+                break;
+            }
+        }
+        dqp = qp_delta(m.qp, pred);
+    }
     uint32_t bits = 0;
     if (!skip && lane < kNumRoles) {
         BitWriter w;
         w.init(rbuf[wave][lane]);
-        code_role(w, lane, g, fs->idr, mbs, m, mc, mbi, av, mvdx, mvdy);
+        code_role(w, lane, g, fs->idr, mbs, m, mc, mbi, av, mvdx, mvdy, dqp);
         w.flush();
         bits = w.bits;
     }

@@ -66,7 +66,7 @@ MXHD bool decide_skip(const Geometry& g, const MbInfo* mbs, int mbi, const Avail
 
 template <class W>
 MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mbs, const MbInfo& m,
-                    const int16_t* mc, int mbi, const Avail& av, int mvdx, int mvdy) {
+                    const int16_t* mc, int mbi, const Avail& av, int mvdx, int mvdy, int dqp = 0) {
     const bool intra = m.type == kMbI16x16;
     const int cbp = m.cbp;
     const int cbp_l = cbp & 15, cbp_c = cbp >> 4;
@@ -83,7 +83,7 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mb
             put_se(w, mvdx);
             put_se(w, mvdy);
             put_ue(w, (uint32_t)cbp_to_codenum(cbp, false));
-            if (cbp) put_se(w, 0);
+            if (cbp) put_se(w, dqp);  // mb_qp_delta (adaptive quantisation)
         }
         return;
     }
@@ -127,6 +127,21 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mb
         cavlc_block(w, mc + kCoefChromaAc + (comp * 4 + cb) * 16 + 1, 15, nc);
     }
 }
+
+// Adaptive quantisation (residual-energy based, P macroblocks): a block whose motion-
+// compensated luma residual stays noise-like (mean |residual| above 32 / 48 per pixel) is
+// quantised 6 / 12 QP coarser -- refining incompressible content costs far more bits than
+// it returns -- and the rate controller hands those bits to the rest of the picture (text,
+// UI edges).  sad = sum |src - pred| over the 16x16 luma block.
+MXHD int aq_mb_qp(int frame_qp, uint32_t sad, int aq) {
+    if (!aq) return frame_qp;
+    const int off = sad > 256u * 48 ? 12 : (sad > 256u * 32 ? 6 : 0);
+    const int q = frame_qp + off;
+    return q > 51 ? 51 : q;
+}
+
+// mb_qp_delta value for QP `qp` after predictor `pred` (both 0..51), in -26..25.
+MXHD int qp_delta(int qp, int pred) { return ((qp - pred + 26 + 52) % 52) - 26; }
 
 MXHD SliceParams make_slice_params(int first_mb, int idr, int frame_num, int log2_max_frame_num, int idr_pic_id,
                                    int qp_delta, int deblock_off) {

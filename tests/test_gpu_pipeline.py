@@ -118,7 +118,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     gs, cs, grec = b"", b"", []
     ch = genc.coded_height
     for t in range(frames):
-        y, uv = synthetic_nv12(w, h, t)
+        y, uv = synthetic_nv12(w, h, t, seed=t if kw.get("fresh_noise") else 0)
         dy = pitched(y, genc.pitch, ch)
         duv = pitched(uv, genc.pitch, ch // 2, uv=True)
         torch.cuda.synchronize()
@@ -131,9 +131,11 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     return gs, grec
 
 
-@pytest.mark.parametrize("w,h,subpel,sr", [(64, 48, 1, 8), (160, 96, 0, 16), (100, 60, 1, 16), (320, 192, 1, 32)])
-def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr):
-    stream, grec = _gpu_cpu_encode(gpu, w, h, 4, subpel=subpel, search_range=sr)
+@pytest.mark.parametrize("w,h,subpel,sr,fresh", [(64, 48, 1, 8, 0), (160, 96, 0, 16, 0), (100, 60, 1, 16, 0),
+                                                 (320, 192, 1, 32, 0), (96, 64, 1, 8, 1)])
+def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr, fresh):
+    # fresh=1: new noise every frame -> adaptive quantisation (mb_qp_delta != 0) is exercised
+    stream, grec = _gpu_cpu_encode(gpu, w, h, 4, subpel=subpel, search_range=sr, fresh_noise=fresh, qp=24)
     dec = Decoder()
     dec.decode(stream)
     for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
