@@ -55,6 +55,9 @@ def main() -> None:
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
                     help="concurrent sessions per GPU (density): each has its own HIP stream and one frame in flight")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse the "
+                         "multi-rank plumbing with several ranks on one GPU)")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
 
@@ -64,19 +67,26 @@ def main() -> None:
 
     import torch
 
+    # one rank per GPU; the modulo only matters when rehearsing several ranks on fewer GPUs
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local_rank % ndev
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(dev_index)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.backend)
     else:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(dev_index)
+    coll_dev = "cuda" if (dist is None or args.backend == "nccl") else "cpu"
 
     import mxdesk
 
     N = mxdesk.native()
-    N.set_device(local_rank)
+    N.set_device(dev_index)
     cfg = N.SessionConfig()
     cfg.width, cfg.height, cfg.fps = args.width, args.height, args.fps
     cfg.out_width, cfg.out_height = args.out_width, args.out_height
@@ -133,7 +143,7 @@ def main() -> None:
         gpu_ms.append(r.gpu_ms)
 
     if dist is not None:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed_max = float(t.item())
         gathered = [None] * world
