@@ -10,6 +10,7 @@
 
 #include "../codec/h264_core.h"
 #include "../codec/h264_encoder.h"
+#include "../codec/hevc_encoder.h"
 #include "../common/hip_check.h"
 #include "../common/trace.h"
 #include "../kernels/pixel.h"
@@ -198,6 +199,57 @@ PYBIND11_MODULE(_native, m) {
         .def("request_idr", [](h264::CpuH264Encoder& e) { e.common().request_idr(); })
         .def("set_bitrate", [](h264::CpuH264Encoder& e, int k) { e.common().set_bitrate(k); })
         .def_property_readonly("stats", &h264::CpuH264Encoder::last_stats);
+
+    py::class_<hevc::CpuHevcEncoder>(m, "CpuHevcEncoder")
+        .def(py::init<const h264::EncoderConfig&>())
+        .def(
+            "encode",
+            [](hevc::CpuHevcEncoder& e, py::array_t<uint8_t, py::array::c_style> y,
+               py::array_t<uint8_t, py::array::c_style> uv, bool force_idr) {
+                if (y.ndim() != 2 || uv.ndim() != 2 || y.shape(1) != uv.shape(1))
+                    throw std::invalid_argument("y (H,P) and uv (H/2,P) planes with equal pitch");
+                const int pitch = (int)y.shape(1);
+                const int cw = e.coded_pitch();
+                const auto& cfg = e.common().config();
+                const int ch = e.common().ctb_h() * hevc::kCtb;
+                std::vector<uint8_t> py_, puv;
+                const uint8_t* yy = y.data();
+                const uint8_t* uu = uv.data();
+                int p = pitch;
+                if (y.shape(0) < ch || pitch < cw) {
+                    h264::pad_nv12(yy, uu, cfg.width, cfg.height, pitch, cw, ch, py_, puv);
+                    yy = py_.data();
+                    uu = puv.data();
+                    p = cw;
+                }
+                std::vector<uint8_t> au;
+                {
+                    py::gil_scoped_release rel;
+                    au = e.encode(yy, uu, p, force_idr);
+                }
+                return to_bytes(au);
+            },
+            py::arg("y"), py::arg("uv"), py::arg("force_idr") = false)
+        .def("recon",
+             [](hevc::CpuHevcEncoder& e) {
+                 const int cw = e.coded_pitch(), ch = e.common().ctb_h() * hevc::kCtb;
+                 py::array_t<uint8_t> y({ch, cw}), uv({ch / 2, cw});
+                 std::memcpy(y.mutable_data(), e.recon_y().data(), (size_t)cw * ch);
+                 std::memcpy(uv.mutable_data(), e.recon_uv().data(), (size_t)cw * ch / 2);
+                 return py::make_tuple(y, uv);
+             })
+        .def("cu_types",
+             [](hevc::CpuHevcEncoder& e) {
+                 std::vector<int> t;
+                 for (const auto& c : e.cus()) t.push_back(c.type);
+                 return t;
+             })
+        .def_property_readonly("slice_rows", [](hevc::CpuHevcEncoder& e) { return e.common().slice_rows(); })
+        .def_property_readonly("level_idc", [](hevc::CpuHevcEncoder& e) { return e.common().level_idc(); })
+        .def("request_idr", [](hevc::CpuHevcEncoder& e) { e.common().rc().request_idr(); })
+        .def("set_bitrate", [](hevc::CpuHevcEncoder& e, int k) { e.common().rc().set_bitrate(k); })
+        .def_property_readonly("stats", &hevc::CpuHevcEncoder::last_stats);
+    m.def("hevc_level", &hevc::pick_level, py::arg("width"), py::arg("height"), py::arg("fps"));
 
     py::class_<h264::GpuH264Encoder>(m, "GpuH264Encoder")
         .def(py::init([](const h264::EncoderConfig& c, uintptr_t stream) {

@@ -33,6 +33,68 @@ void pad_nv12(const uint8_t* y, const uint8_t* uv, int w, int h, int pitch, int 
     }
 }
 
+// Integer full search + quarter-pel refinement of the 16x16 block at (x0, y0): the same
+// rules as k_me_full (static-block exit, cost = SAD + lambda * mv bits, tie -> shorter vector
+// then lower candidate index).  Shared by the CPU H.264 and HEVC encoders.
+void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, int ch_, int x0, int y0,
+                   int frame_qp, int search_range, int subpel, int* out_mvx, int* out_mvy) {
+    const int lambda = lambda_sad(frame_qp);
+    const int R = me_range(search_range);
+    const int side = 2 * R + 1;
+    // ---- static-block early exit, then integer full search (same rules as k_me_full)
+    uint32_t sad0 = 0;
+    for (int r = 0; r < 16; ++r)
+        for (int k = 0; k < 16; ++k)
+            sad0 += std::abs((int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + k, y0 + r));
+    const bool is_static = sad0 <= kStaticSad;
+    unsigned long long best = ~0ull;
+    for (int c = 0; c < (is_static ? 0 : side * side); ++c) {
+        const int dy = c / side - R, dx = c % side - R;
+        uint32_t sad = 0;
+        for (int r = 0; r < 16; ++r)
+            for (int k = 0; k < 16; ++k)
+                sad += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
+                                ref_px(ref_y, cw_, cw_, ch_, x0 + dx + k, y0 + dy + r));
+        const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
+        const uint32_t dist = (uint32_t)(std::abs(dx) + std::abs(dy));
+        const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
+        best = std::min(best, key);
+    }
+    const int cb = (int)(best & 0xffff);
+    int mvx = is_static ? 0 : 4 * ((cb % side) - R), mvy = is_static ? 0 : 4 * ((cb / side) - R);
+    if (subpel && !is_static) {
+        auto sad_at = [&](int vx, int vy) {
+            uint32_t s = 0;
+            for (int r = 0; r < 16; ++r)
+                for (int k = 0; k < 16; ++k)
+                    s += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
+                                  luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + vx, (y0 + r) * 4 + vy));
+            return s;
+        };
+        uint32_t cur_cost = (uint32_t)(best >> 32);
+        for (int step = 2; step >= 1; step >>= 1) {
+            int bdx = 0, bdy = 0;
+            uint32_t bcost = cur_cost;
+            for (int k = 0; k < 8; ++k) {
+                int ddx, ddy;
+                subpel_offset(k, &ddx, &ddy);
+                const int cx = mvx + ddx * step, cy = mvy + ddy * step;
+                const uint32_t cost = me_cost(sad_at(cx, cy), lambda, cx, cy);
+                if (cost < bcost) {
+                    bcost = cost;
+                    bdx = ddx * step;
+                    bdy = ddy * step;
+                }
+            }
+            mvx += bdx;
+            mvy += bdy;
+            cur_cost = bcost;
+        }
+    }
+    *out_mvx = mvx;
+    *out_mvy = mvy;
+}
+
 CpuH264Encoder::CpuH264Encoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
     cw_ = common_.mb_w() * 16;
     ch_ = common_.mb_h() * 16;
@@ -63,64 +125,13 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
     uint8_t* rec_y = rec_y_[cur_].data();
     uint8_t* rec_uv = rec_uv_[cur_].data();
     const int frame_qp = common_.cur_qp();
-    const int lambda = lambda_sad(frame_qp);
-    const int R = me_range(cfg_.search_range);
-    const int side = 2 * R + 1;
     for (int mby = 0; mby < g.mb_h; ++mby)
         for (int mbx = 0; mbx < g.mb_w; ++mbx) {
             const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
             MbInfo& m = mb_[mbi];
             std::memset(&m, 0, sizeof m);
-            // ---- static-block early exit, then integer full search (same rules as k_me_full)
-            uint32_t sad0 = 0;
-            for (int r = 0; r < 16; ++r)
-                for (int k = 0; k < 16; ++k)
-                    sad0 += std::abs((int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + k, y0 + r));
-            const bool is_static = sad0 <= kStaticSad;
-            unsigned long long best = ~0ull;
-            for (int c = 0; c < (is_static ? 0 : side * side); ++c) {
-                const int dy = c / side - R, dx = c % side - R;
-                uint32_t sad = 0;
-                for (int r = 0; r < 16; ++r)
-                    for (int k = 0; k < 16; ++k)
-                        sad += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
-                                        ref_px(ref_y, cw_, cw_, ch_, x0 + dx + k, y0 + dy + r));
-                const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
-                const uint32_t dist = (uint32_t)(std::abs(dx) + std::abs(dy));
-                const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
-                best = std::min(best, key);
-            }
-            const int cb = (int)(best & 0xffff);
-            int mvx = is_static ? 0 : 4 * ((cb % side) - R), mvy = is_static ? 0 : 4 * ((cb / side) - R);
-            if (cfg_.subpel && !is_static) {
-                auto sad_at = [&](int vx, int vy) {
-                    uint32_t s = 0;
-                    for (int r = 0; r < 16; ++r)
-                        for (int k = 0; k < 16; ++k)
-                            s += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
-                                          luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + vx, (y0 + r) * 4 + vy));
-                    return s;
-                };
-                uint32_t cur_cost = (uint32_t)(best >> 32);
-                for (int step = 2; step >= 1; step >>= 1) {
-                    int bdx = 0, bdy = 0;
-                    uint32_t bcost = cur_cost;
-                    for (int k = 0; k < 8; ++k) {
-                        int ddx, ddy;
-                        subpel_offset(k, &ddx, &ddy);
-                        const int cx = mvx + ddx * step, cy = mvy + ddy * step;
-                        const uint32_t cost = me_cost(sad_at(cx, cy), lambda, cx, cy);
-                        if (cost < bcost) {
-                            bcost = cost;
-                            bdx = ddx * step;
-                            bdy = ddy * step;
-                        }
-                    }
-                    mvx += bdx;
-                    mvy += bdy;
-                    cur_cost = bcost;
-                }
-            }
+            int mvx = 0, mvy = 0;
+            me_search_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &mvx, &mvy);
             m.mvx = (int16_t)mvx;
             m.mvy = (int16_t)mvy;
             m.type = kMbP16x16;

@@ -191,6 +191,11 @@ class CpuH264Encoder {
     FrameStats stats_;
 };
 
+// CPU motion search of one 16x16 block (same rules as the GPU k_me_full); shared by the
+// CPU H.264 and HEVC encoders.
+void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw, int ch, int x0, int y0, int qp,
+                   int search_range, int subpel, int* mvx, int* mvy);
+
 // Pad a display-sized NV12 frame to the coded size by edge replication (what the CSC
 // kernel does on the GPU side).  Returns pitch = coded width.
 void pad_nv12(const uint8_t* y, const uint8_t* uv, int w, int h, int pitch, int coded_w, int coded_h,

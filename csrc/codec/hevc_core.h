@@ -1,0 +1,1017 @@
+// HEVC (ISO/IEC 23008-2, Main profile) building blocks shared by the HIP encoder kernels
+// (hevc_kernels.hip) and the CPU encoder (hevc_cpu.cpp): CABAC engine and context
+// tables, residual / CU syntax, the integer core transform, (de)quantisation, intra
+// prediction (all 35 modes) and the 8-tap / 4-tap inter interpolation.  Every function is
+// __host__ __device__, so the GPU kernels and the CPU oracle share one definition of
+// every bit and every sample.
+//
+// Coding subset (fixed by the SPS/PPS that hevc_encoder.cpp writes):
+//   CTB = CU = 16x16 (no split_cu_flag), PU 2Nx2N, TU 16x16 luma / 8x8 chroma
+//   (max_transform_hierarchy_depth 0), I slices of intra CUs, P slices of skip / merge /
+//   AMVP CUs with one reference picture, MaxNumMergeCand 1, no TMVP, no SAO, no
+//   deblocking, no sign hiding, cu_qp_delta per CU (adaptive quantisation), one slice per
+//   CTU row so every slice is entropy coded by its own GPU wave.
+//
+// Replaces NVENC HEVC behind the reference's GStreamer stack (nvh264enc default encoder,
+// reference Dockerfile:210 / README.md:21; BASELINE.json config "4K60 HEVC").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef MXHD
+#define MXHD __host__ __device__ __forceinline__
+#endif
+
+namespace mx {
+namespace hevc {
+
+constexpr int kCtb = 16;  // CTB = CU size
+constexpr int kCoefPerCu = 384;  // 256 luma + 64 Cb + 64 Cr, each TU in scan order
+
+// ---------------------------------------------------------------- scans (6.5.3)
+// 4x4 up-right diagonal scan: position n -> (x, y); also used for the 4x4 sub-block
+// grid of a 16x16 TU.  kDiag4Inv maps raster (y*4+x) -> n.
+constexpr uint8_t kDiag4X[16] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+constexpr uint8_t kDiag4Y[16] = {0, 1, 0, 2, 1, 0, 3, 2, 1, 0, 3, 2, 1, 3, 2, 3};
+constexpr uint8_t kDiag4Inv[16] = {0, 2, 5, 9, 1, 4, 8, 12, 3, 7, 11, 14, 6, 10, 13, 15};
+// 2x2 diagonal scan (sub-block grid of an 8x8 TU)
+constexpr uint8_t kDiag2X[4] = {0, 0, 1, 1};
+constexpr uint8_t kDiag2Y[4] = {0, 1, 0, 1};
+constexpr uint8_t kDiag2Inv[4] = {0, 2, 1, 3};
+
+// scan index (sub-block * 16 + position) of raster coordinate (x, y) in an NxN TU
+MXHD int scan_index(int log2n, int x, int y) {
+    const int sb = log2n == 4 ? kDiag4Inv[(y >> 2) * 4 + (x >> 2)] : (log2n == 3 ? kDiag2Inv[(y >> 2) * 2 + (x >> 2)] : 0);
+    return sb * 16 + kDiag4Inv[(y & 3) * 4 + (x & 3)];
+}
+MXHD void scan_pos(int log2n, int idx, int* x, int* y) {
+    const int sb = idx >> 4, n = idx & 15;
+    const int sx = log2n == 4 ? kDiag4X[sb] : (log2n == 3 ? kDiag2X[sb] : 0);
+    const int sy = log2n == 4 ? kDiag4Y[sb] : (log2n == 3 ? kDiag2Y[sb] : 0);
+    *x = sx * 4 + kDiag4X[n];
+    *y = sy * 4 + kDiag4Y[n];
+}
+
+// ---------------------------------------------------------------- core transform (8.6.4.2)
+// 32-point matrix coefficients by angle index m (cos(pi*m/64) scaled); every N-point
+// matrix row k is row k*32/N of the 32-point matrix.
+constexpr uint8_t kCos32[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                                61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+MXHD int dct_coef32(int k, int n) {
+    if (k == 0) return 64;
+    int m = (k * (2 * n + 1)) & 127;
+    if (m > 64) m = 128 - m;
+    return m > 32 ? -(int)kCos32[64 - m] : (int)kCos32[m];
+}
+// N-point matrix entry (row = frequency k, column = sample n)
+MXHD int dct_coef(int log2n, int k, int n) { return dct_coef32(k << (5 - log2n), n); }
+
+// Forward 2-D transform (encoder side; HM-style shifts: log2N+bitDepth-9, then log2N+6).
+// res: raster NxN residual, out: raster NxN coefficients [v][u].
+MXHD void fwd_transform(int log2n, const int* res, int* out) {
+    const int N = 1 << log2n;
+    const int s1 = log2n - 1, s2 = log2n + 6;  // bitDepth 8
+    int tmp[16 * 16];
+    for (int y = 0; y < N; ++y)
+        for (int k = 0; k < N; ++k) {
+            int s = 0;
+            for (int n = 0; n < N; ++n) s += dct_coef(log2n, k, n) * res[y * N + n];
+            tmp[y * N + k] = (s + (1 << (s1 - 1))) >> s1;
+        }
+    for (int k2 = 0; k2 < N; ++k2)
+        for (int k = 0; k < N; ++k) {
+            int s = 0;
+            for (int y = 0; y < N; ++y) s += dct_coef(log2n, k2, y) * tmp[y * N + k];
+            out[k2 * N + k] = (s + (1 << (s2 - 1))) >> s2;
+        }
+}
+
+MXHD int clip16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+
+// Inverse 2-D transform (normative): columns, clip to 16 bit after (e + 64) >> 7, rows,
+// (g + 2048) >> 12.  d: raster coefficients [v][u], r: raster residual.
+MXHD void inv_transform(int log2n, const int* d, int* r) {
+    const int N = 1 << log2n;
+    int g[16 * 16];
+    for (int x = 0; x < N; ++x)
+        for (int y = 0; y < N; ++y) {
+            int s = 0;
+            for (int k = 0; k < N; ++k) s += dct_coef(log2n, k, y) * d[k * N + x];
+            g[y * N + x] = clip16((s + 64) >> 7);
+        }
+    for (int y = 0; y < N; ++y)
+        for (int x = 0; x < N; ++x) {
+            int s = 0;
+            for (int k = 0; k < N; ++k) s += dct_coef(log2n, k, x) * g[y * N + k];
+            r[y * N + x] = (s + 2048) >> 12;
+        }
+}
+
+// ---------------------------------------------------------------- quantisation (8.6.2/8.6.3)
+constexpr uint16_t kQuantScale[6] = {26214, 23302, 20560, 18396, 16384, 14564};
+constexpr uint8_t kLevelScale[6] = {40, 45, 51, 57, 64, 72};
+
+MXHD int quant_coef(int c, int qp, int log2n, bool intra) {
+    const int qbits = 14 + qp / 6 + (15 - 8 - log2n);
+    const int64_t add = (int64_t)(intra ? 171 : 85) << (qbits - 9);
+    const int a = c < 0 ? -c : c;
+    int l = (int)(((int64_t)a * kQuantScale[qp % 6] + add) >> qbits);
+    l = l > 32767 ? 32767 : l;
+    return c < 0 ? -l : l;
+}
+MXHD int dequant_coef(int level, int qp, int log2n) {
+    const int bd = log2n + 3;  // BitDepth + log2(nTbS) - 5
+    const int64_t v = (((int64_t)level * 16 * kLevelScale[qp % 6]) << (qp / 6)) + (1 << (bd - 1));
+    const int64_t s = v >> bd;
+    return s < -32768 ? -32768 : (s > 32767 ? 32767 : (int)s);
+}
+// Table 8-10 (ChromaArrayType 1)
+MXHD int chroma_qp(int qp_y, int offset) {
+    int q = qp_y + offset;
+    q = q < 0 ? 0 : (q > 57 ? 57 : q);
+    constexpr uint8_t tab[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+    if (q < 30) return q;
+    if (q > 43) return q - 6;
+    return tab[q - 30];
+}
+MXHD int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// ---------------------------------------------------------------- intra prediction (8.4.4.2)
+// Reference samples: left[k] = p[-1][k-1], top[k] = p[k-1][-1] for k = 0..2N (index 0 is the
+// shared corner p[-1][-1]).
+constexpr int8_t kIntraAngle[35] = {0,  0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2,
+                                    -5, -9,  -13, -17, -21, -26, -32, -26, -21, -17, -13, -9,
+                                    -5, -2,  0,   2,   5,   9,   13,  17,  21,  26,  32};
+MXHD int inv_angle(int angle) {
+    // 8192 / angle rounded, for the negative angles of modes 11..25
+    switch (angle) {
+        case -2: return -4096;
+        case -5: return -1638;
+        case -9: return -910;
+        case -13: return -630;
+        case -17: return -482;
+        case -21: return -390;
+        case -26: return -315;
+        default: return -256;  // -32
+    }
+}
+
+// Substitution process (8.4.4.2.2) for the availability pattern of a block whose left
+// column (N samples) may be present and whose corner / top / top-right / below-left are
+// absent or present as whole units.  lpx: left column (N), bpx: below-left (N), tpx: top
+// (N), trx: top-right (N), corner: p[-1][-1].
+MXHD void intra_refs(int N, bool a_left, bool a_bl, bool a_top, bool a_tr, bool a_corner, const uint8_t* lpx,
+                     const uint8_t* bpx, const uint8_t* tpx, const uint8_t* trx, int corner, int* left, int* top) {
+    // linear order of the spec's search: p[-1][2N-1] .. p[-1][-1], p[0][-1] .. p[2N-1][-1]
+    // -> q[0 .. 4N]
+    int q[4 * 32 + 1];
+    bool av[4 * 32 + 1];
+    for (int k = 0; k < N; ++k) {
+        q[k] = a_bl ? bpx[N - 1 - k] : 0;  // p[-1][2N-1-k]
+        av[k] = a_bl;
+        q[N + k] = a_left ? lpx[N - 1 - k] : 0;  // p[-1][N-1-k]
+        av[N + k] = a_left;
+        q[2 * N + 1 + k] = a_top ? tpx[k] : 0;
+        av[2 * N + 1 + k] = a_top;
+        q[3 * N + 1 + k] = a_tr ? trx[k] : 0;
+        av[3 * N + 1 + k] = a_tr;
+    }
+    q[2 * N] = corner;
+    av[2 * N] = a_corner;
+    const int total = 4 * N + 1;
+    bool any = false;
+    for (int i = 0; i < total; ++i) any |= av[i];
+    if (!any) {
+        for (int i = 0; i < total; ++i) q[i] = 128;
+    } else {
+        if (!av[0]) {
+            for (int i = 1; i < total; ++i)
+                if (av[i]) {
+                    q[0] = q[i];
+                    break;
+                }
+        }
+        for (int i = 1; i < total; ++i)
+            if (!av[i]) q[i] = q[i - 1];
+    }
+    // back to the left/top arrays
+    for (int k = 0; k < 2 * N; ++k) left[1 + k] = q[2 * N - 1 - k];
+    left[0] = q[2 * N];
+    top[0] = q[2 * N];
+    for (int k = 0; k < 2 * N; ++k) top[1 + k] = q[2 * N + 1 + k];
+}
+
+// Prediction of an NxN block (N = 4..32, 8-bit).  cidx 0 = luma (reference filtering,
+// DC / angular edge filters apply), 1/2 = chroma.  pred: raster NxN.
+MXHD void intra_predict(int mode, int log2n, int cidx, const int* left_in, const int* top_in, int* pred) {
+    const int N = 1 << log2n;
+    int left[65], top[65];
+    for (int k = 0; k <= 2 * N; ++k) {
+        left[k] = left_in[k];
+        top[k] = top_in[k];
+    }
+    // 8.4.4.2.3 filtering (luma only for 4:2:0; strong smoothing disabled)
+    if (cidx == 0 && mode != 1 && N != 4) {
+        const int d1 = mode > 26 ? mode - 26 : 26 - mode, d2 = mode > 10 ? mode - 10 : 10 - mode;
+        const int mind = d1 < d2 ? d1 : d2;
+        const int thres = N == 8 ? 7 : (N == 16 ? 1 : 0);
+        if (mind > thres) {
+            int fl[65], ft[65];
+            fl[0] = ft[0] = (left[1] + 2 * left[0] + top[1] + 2) >> 2;
+            for (int k = 1; k < 2 * N; ++k) {
+                fl[k] = (left[k + 1] + 2 * left[k] + left[k - 1] + 2) >> 2;
+                ft[k] = (top[k + 1] + 2 * top[k] + top[k - 1] + 2) >> 2;
+            }
+            fl[2 * N] = left[2 * N];
+            ft[2 * N] = top[2 * N];
+            for (int k = 0; k <= 2 * N; ++k) {
+                left[k] = fl[k];
+                top[k] = ft[k];
+            }
+        }
+    }
+    if (mode == 0) {  // planar
+        for (int y = 0; y < N; ++y)
+            for (int x = 0; x < N; ++x)
+                pred[y * N + x] = ((N - 1 - x) * left[1 + y] + (x + 1) * top[1 + N] + (N - 1 - y) * top[1 + x] +
+                                   (y + 1) * left[1 + N] + N) >>
+                                  (log2n + 1);
+        return;
+    }
+    if (mode == 1) {  // DC
+        int s = N;
+        for (int k = 1; k <= N; ++k) s += left[k] + top[k];
+        const int dc = s >> (log2n + 1);
+        for (int i = 0; i < N * N; ++i) pred[i] = dc;
+        if (cidx == 0 && N < 32) {
+            pred[0] = (left[1] + 2 * dc + top[1] + 2) >> 2;
+            for (int x = 1; x < N; ++x) pred[x] = (top[1 + x] + 3 * dc + 2) >> 2;
+            for (int y = 1; y < N; ++y) pred[y * N] = (left[1 + y] + 3 * dc + 2) >> 2;
+        }
+        return;
+    }
+    const int angle = kIntraAngle[mode];
+    int refbuf[3 * 32 + 1];
+    int* ref = refbuf + N;  // ref[-N .. 2N]
+    const bool vert = mode >= 18;
+    const int* mainr = vert ? top : left;  // p along the main direction, index k = ref[k]
+    const int* side = vert ? left : top;
+    for (int x = 0; x <= N; ++x) ref[x] = mainr[x];
+    if (angle < 0) {
+        const int lo = (N * angle) >> 5;
+        if (lo < -1) {
+            const int ia = inv_angle(angle);
+            for (int x = lo; x <= -1; ++x) ref[x] = side[(x * ia + 128) >> 8];
+        }
+    } else {
+        for (int x = N + 1; x <= 2 * N; ++x) ref[x] = mainr[x];
+    }
+    for (int y = 0; y < N; ++y)
+        for (int x = 0; x < N; ++x) {
+            const int a = vert ? y : x, b = vert ? x : y;  // a: distance along prediction, b: across
+            const int idx = ((a + 1) * angle) >> 5, fact = ((a + 1) * angle) & 31;
+            const int v = fact ? ((32 - fact) * ref[b + idx + 1] + fact * ref[b + idx + 2] + 16) >> 5 : ref[b + idx + 1];
+            pred[y * N + x] = v;
+        }
+    if (cidx == 0 && N < 32) {
+        if (mode == 26)
+            for (int y = 0; y < N; ++y) pred[y * N] = clip255(top[1] + ((left[1 + y] - left[0]) >> 1));
+        else if (mode == 10)
+            for (int x = 0; x < N; ++x) pred[x] = clip255(left[1] + ((top[1 + x] - top[0]) >> 1));
+    }
+}
+
+// Most probable modes (8.4.2); cand_b is always DC here because the CU above lies in
+// another CTB, but the function is general.
+MXHD void mpm_list(int cand_a, int cand_b, int* l) {
+    if (cand_a == cand_b) {
+        if (cand_a < 2) {
+            l[0] = 0;
+            l[1] = 1;
+            l[2] = 26;
+        } else {
+            l[0] = cand_a;
+            l[1] = 2 + ((cand_a + 29) % 32);
+            l[2] = 2 + ((cand_a - 2 + 1) % 32);
+        }
+    } else {
+        l[0] = cand_a;
+        l[1] = cand_b;
+        if (cand_a != 0 && cand_b != 0)
+            l[2] = 0;
+        else if (cand_a != 1 && cand_b != 1)
+            l[2] = 1;
+        else
+            l[2] = 26;
+    }
+}
+
+// ---------------------------------------------------------------- inter interpolation (8.5.3.3.3)
+constexpr int8_t kLumaTap[4][8] = {
+    {0, 0, 0, 64, 0, 0, 0, 0}, {-1, 4, -10, 58, 17, -5, 1, 0}, {-1, 4, -11, 40, 40, -11, 4, -1}, {0, 1, -5, 17, 58, -10, 4, -1}};
+constexpr int8_t kChromaTap[8][4] = {{0, 64, 0, 0},     {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
+                                     {-4, 36, 36, -4},  {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
+
+MXHD int ref_at(const uint8_t* p, int pitch, int w, int h, int x, int y, int step = 1) {
+    x = x < 0 ? 0 : (x >= w ? w - 1 : x);
+    y = y < 0 ? 0 : (y >= h ? h - 1 : y);
+    return p[y * pitch + x * step];
+}
+
+// Uni-predicted luma sample at integer position (x, y) displaced by the quarter-pel
+// vector (mvx, mvy); reference plane w x h with edge clamping.
+MXHD int luma_mc(const uint8_t* ref, int pitch, int w, int h, int x, int y, int mvx, int mvy) {
+    const int xi = x + (mvx >> 2), yi = y + (mvy >> 2), fx = mvx & 3, fy = mvy & 3;
+    int v;
+    if (!fx && !fy) {
+        v = ref_at(ref, pitch, w, h, xi, yi) << 6;
+    } else if (!fy) {
+        v = 0;
+        for (int i = 0; i < 8; ++i) v += kLumaTap[fx][i] * ref_at(ref, pitch, w, h, xi + i - 3, yi);
+    } else if (!fx) {
+        v = 0;
+        for (int i = 0; i < 8; ++i) v += kLumaTap[fy][i] * ref_at(ref, pitch, w, h, xi, yi + i - 3);
+    } else {
+        int s = 0;
+        for (int n = 0; n < 8; ++n) {
+            int t = 0;
+            for (int i = 0; i < 8; ++i) t += kLumaTap[fx][i] * ref_at(ref, pitch, w, h, xi + i - 3, yi + n - 3);
+            s += kLumaTap[fy][n] * t;
+        }
+        v = s >> 6;
+    }
+    return clip255((v + 32) >> 6);
+}
+
+// Chroma sample (interleaved NV12 plane, comp 0 = Cb, 1 = Cr) at chroma position (x, y),
+// luma quarter-pel vector = chroma eighth-pel vector for 4:2:0.
+MXHD int chroma_mc(const uint8_t* uv, int pitch, int cw, int ch, int comp, int x, int y, int mvx, int mvy) {
+    const int xi = x + (mvx >> 3), yi = y + (mvy >> 3), fx = mvx & 7, fy = mvy & 7;
+    const uint8_t* p = uv + comp;
+    int v;
+    if (!fx && !fy) {
+        v = ref_at(p, pitch, cw, ch, xi, yi, 2) << 6;
+    } else if (!fy) {
+        v = 0;
+        for (int i = 0; i < 4; ++i) v += kChromaTap[fx][i] * ref_at(p, pitch, cw, ch, xi + i - 1, yi, 2);
+    } else if (!fx) {
+        v = 0;
+        for (int i = 0; i < 4; ++i) v += kChromaTap[fy][i] * ref_at(p, pitch, cw, ch, xi, yi + i - 1, 2);
+    } else {
+        int s = 0;
+        for (int n = 0; n < 4; ++n) {
+            int t = 0;
+            for (int i = 0; i < 4; ++i) t += kChromaTap[fx][i] * ref_at(p, pitch, cw, ch, xi + i - 1, yi + n - 1, 2);
+            s += kChromaTap[fy][n] * t;
+        }
+        v = s >> 6;
+    }
+    return clip255((v + 32) >> 6);
+}
+
+// ---------------------------------------------------------------- CABAC (9.3)
+constexpr uint8_t kLps[64][4] = {
+    {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205}, {116, 142, 169, 195},
+    {111, 135, 160, 185}, {105, 128, 152, 175}, {100, 122, 144, 166}, {95, 116, 137, 158},  {90, 110, 130, 150},
+    {85, 104, 123, 142},  {81, 99, 117, 135},   {77, 94, 111, 128},   {73, 89, 105, 122},   {69, 85, 100, 116},
+    {66, 80, 95, 110},    {62, 76, 90, 104},    {59, 72, 86, 99},     {56, 69, 81, 94},     {53, 65, 77, 89},
+    {51, 62, 73, 85},     {48, 59, 69, 80},     {46, 56, 66, 76},     {43, 53, 63, 72},     {41, 50, 59, 69},
+    {39, 48, 56, 65},     {37, 45, 54, 62},     {35, 43, 51, 59},     {33, 41, 48, 56},     {32, 39, 46, 53},
+    {30, 37, 43, 50},     {29, 35, 41, 48},     {27, 33, 39, 45},     {26, 31, 37, 43},     {24, 30, 35, 41},
+    {23, 28, 33, 39},     {22, 27, 32, 37},     {21, 26, 30, 35},     {20, 24, 29, 33},     {19, 23, 27, 31},
+    {18, 22, 26, 30},     {17, 21, 25, 28},     {16, 20, 23, 27},     {15, 19, 22, 25},     {14, 18, 21, 24},
+    {14, 17, 20, 23},     {13, 16, 19, 22},     {12, 15, 18, 21},     {12, 14, 17, 20},     {11, 14, 16, 19},
+    {11, 13, 15, 18},     {10, 12, 15, 17},     {10, 12, 14, 16},     {9, 11, 13, 15},      {9, 11, 12, 14},
+    {8, 10, 12, 14},      {8, 9, 11, 13},       {7, 9, 11, 12},       {7, 9, 10, 12},       {7, 8, 10, 11},
+    {6, 8, 9, 11},        {6, 7, 9, 10},        {6, 7, 8, 9},         {2, 2, 2, 2}};
+constexpr uint8_t kNextLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12,
+                                  13, 13, 15, 15, 16, 16, 18, 18, 19, 19, 21, 21, 22, 22, 23, 24,
+                                  24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
+                                  33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
+
+// Context index layout (this encoder's numbering; the decoder uses the same initValues)
+enum Ctx : int {
+    C_SKIP = 0,            // 3
+    C_MERGE_FLAG = 3,      // 1
+    C_MERGE_IDX = 4,       // 1
+    C_PRED_MODE = 5,       // 1
+    C_PART_MODE = 6,       // 4
+    C_PREV_INTRA = 10,     // 1
+    C_CHROMA_PRED = 11,    // 1
+    C_RQT_ROOT = 12,       // 1
+    C_MVP = 13,            // 1
+    C_MVD_G0 = 14,         // 1
+    C_MVD_G1 = 15,         // 1
+    C_CBF_LUMA = 16,       // 2
+    C_CBF_CHROMA = 18,     // 4
+    C_QP_DELTA = 22,       // 2
+    C_LAST_X = 24,         // 18
+    C_LAST_Y = 42,         // 18
+    C_CSBF = 60,           // 4
+    C_SIG = 64,            // 42
+    C_GT1 = 106,           // 24
+    C_GT2 = 130,           // 6
+    C_SPLIT_TRANSFORM = 136,  // 3
+    C_SPLIT_CU = 139,      // 3
+    C_NUM = 142
+};
+
+// initValue per initType (0: I, 1: P without cabac_init_flag, 2: B), Tables 9-5..9-37
+constexpr uint8_t kCtxInit[3][C_NUM] = {
+    {// I
+     154, 154, 154,                          // skip (unused)
+     154, 154, 154,                          // merge flag / idx, pred mode (unused)
+     184, 154, 154, 154,                     // part_mode
+     184, 63, 154, 154, 154, 154,            // prev_intra, chroma_pred, rqt_root, mvp, mvd g0/g1 (unused)
+     111, 141,                               // cbf_luma
+     94, 138, 182, 154,                      // cbf_cb/cr
+     154, 154,                               // cu_qp_delta_abs
+     110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
+     110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
+     91, 171, 134, 141,
+     111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141, 179, 153, 125,
+     107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153, 136, 139, 111, 136, 139, 111,
+     140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182, 140, 227,
+     122, 197,
+     138, 153, 136, 167, 152, 152,
+     153, 138, 138,
+     139, 141, 157},
+    {// P (initType 1)
+     197, 185, 201,
+     110, 122, 149,
+     154, 139, 154, 154,
+     154, 152, 79, 168, 140, 198,
+     153, 111,
+     149, 107, 167, 154,
+     154, 154,
+     125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,
+     125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,
+     121, 140, 61, 154,
+     155, 154, 139, 153, 139, 123, 123, 63, 153, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153, 154,
+     166, 183, 140, 136, 153, 154, 170, 153, 123, 123, 107, 121, 107, 121, 167, 151, 183, 140, 151, 183, 140,
+     154, 196, 196, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 137, 169, 194, 166, 167, 154, 167,
+     137, 182,
+     107, 167, 91, 122, 107, 167,
+     124, 138, 94,
+     107, 139, 126},
+    {// B (initType 2)
+     197, 185, 201,
+     154, 137, 134,
+     154, 139, 154, 154,
+     183, 152, 79, 168, 169, 198,
+     153, 111,
+     149, 92, 167, 154,
+     154, 154,
+     125, 110, 124, 110, 95, 94, 125, 111, 111, 79, 125, 126, 111, 111, 79, 108, 123, 93,
+     125, 110, 124, 110, 95, 94, 125, 111, 111, 79, 125, 126, 111, 111, 79, 108, 123, 93,
+     121, 140, 61, 154,
+     170, 154, 139, 153, 139, 123, 123, 63, 124, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153, 154,
+     166, 183, 140, 136, 153, 154, 170, 153, 138, 138, 122, 121, 122, 121, 167, 151, 183, 140, 151, 183, 140,
+     154, 196, 167, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 122, 169, 208, 166, 167, 154, 152,
+     167, 182,
+     107, 167, 91, 107, 107, 167,
+     224, 167, 122,
+     107, 139, 126}};
+
+// Context state byte: (pStateIdx << 1) | valMps (9.3.2.2)
+MXHD uint8_t ctx_init_state(int init_value, int qp) {
+    const int slope = (init_value >> 4) * 5 - 45;
+    const int offset = ((init_value & 15) << 3) - 16;
+    qp = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
+    int pre = ((slope * qp) >> 4) + offset;
+    pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
+    return pre <= 63 ? (uint8_t)((63 - pre) << 1) : (uint8_t)(((pre - 64) << 1) | 1);
+}
+MXHD void ctx_init_all(uint8_t* ctx, int init_type, int qp) {
+    for (int i = 0; i < C_NUM; ++i) ctx[i] = ctx_init_state(kCtxInit[init_type][i], qp);
+}
+
+// Arithmetic encoder (HM-style: 32-bit low register, byte output with carry resolution).
+struct CabacEnc {
+    uint32_t low, range;
+    int bits_left, buffered, num_buffered;
+    uint8_t* out;
+    uint32_t pos, cap, overflow;
+
+    MXHD void start(uint8_t* o, uint32_t c) {
+        low = 0;
+        range = 510;
+        bits_left = 23;
+        buffered = 0xff;
+        num_buffered = 0;
+        out = o;
+        pos = 0;
+        cap = c;
+        overflow = 0;
+    }
+    MXHD void put_byte(uint32_t b) {
+        if (pos < cap)
+            out[pos] = (uint8_t)b;
+        else
+            overflow = 1;
+        ++pos;
+    }
+    MXHD void write_out() {
+        const uint32_t lead = low >> (24 - bits_left);
+        bits_left += 8;
+        low &= 0xffffffffu >> bits_left;
+        if (lead == 0xff) {
+            ++num_buffered;
+        } else if (num_buffered > 0) {
+            const uint32_t carry = lead >> 8;
+            put_byte(buffered + carry);
+            buffered = (int)(lead & 0xff);
+            const uint32_t fill = (0xff + carry) & 0xff;
+            while (num_buffered > 1) {
+                put_byte(fill);
+                --num_buffered;
+            }
+        } else {
+            num_buffered = 1;
+            buffered = (int)lead;
+        }
+    }
+    MXHD void test_write_out() {
+        if (bits_left < 12) write_out();
+    }
+    MXHD void bin(uint8_t& st, int b) {
+        uint32_t s = st >> 1, mps = st & 1;
+        const uint32_t lps = kLps[s][(range >> 6) & 3];
+        range -= lps;
+        if ((uint32_t)b != mps) {
+            const int nb = __builtin_clz(lps) - 23;
+            low = (low + range) << nb;
+            range = lps << nb;
+            if (s == 0) mps ^= 1;
+            s = kNextLps[s];
+            bits_left -= nb;
+            st = (uint8_t)((s << 1) | mps);
+            test_write_out();
+        } else {
+            s = s < 62 ? s + 1 : s;
+            st = (uint8_t)((s << 1) | mps);
+            if (range >= 256) return;
+            low <<= 1;
+            range <<= 1;
+            --bits_left;
+            test_write_out();
+        }
+    }
+    MXHD void bypass(int b) {
+        low <<= 1;
+        if (b) low += range;
+        --bits_left;
+        test_write_out();
+    }
+    MXHD void bypass_bits(uint32_t v, int n) {  // MSB first
+        for (int i = n - 1; i >= 0; --i) bypass((v >> i) & 1);
+    }
+    MXHD void terminate(int b) {
+        range -= 2;
+        if (b) {
+            low += range;
+            low <<= 7;
+            range = 2 << 7;
+            bits_left -= 7;
+        } else if (range >= 256) {
+            return;
+        } else {
+            low <<= 1;
+            range <<= 1;
+            --bits_left;
+        }
+        test_write_out();
+    }
+    // Flush after the final terminate(1) and append rbsp_slice_segment_trailing_bits.
+    MXHD void finish_slice() {
+        if (low >> (32 - bits_left)) {
+            put_byte(buffered + 1);
+            while (num_buffered > 1) {
+                put_byte(0x00);
+                --num_buffered;
+            }
+            low -= 1u << (32 - bits_left);
+        } else {
+            if (num_buffered > 0) put_byte(buffered);
+            while (num_buffered > 1) {
+                put_byte(0xff);
+                --num_buffered;
+            }
+        }
+        // remaining (24 - bits_left) bits of low >> 8, then the stop bit, then zero alignment
+        int n = 24 - bits_left;
+        uint32_t v = (low >> 8) & ((1u << n) - 1);
+        v = (v << 1) | 1;
+        ++n;
+        const int pad = (8 - (n & 7)) & 7;
+        v <<= pad;
+        n += pad;
+        for (int i = n - 8; i >= 0; i -= 8) put_byte((v >> i) & 0xff);
+    }
+    // k-th order Exp-Golomb, bypass coded (9.3.3.3)
+    MXHD void egk(uint32_t v, int k) {
+        while (v >= (1u << k)) {
+            bypass(1);
+            v -= 1u << k;
+            ++k;
+        }
+        bypass(0);
+        bypass_bits(v, k);
+    }
+};
+
+// ---------------------------------------------------------------- CU description
+enum CuType : uint8_t { kCuSkip = 0, kCuMerge = 1, kCuAmvp = 2, kCuIntra = 3 };
+
+struct CuInfo {
+    uint8_t type;        // CuType
+    uint8_t intra_mode;  // luma intra mode (chroma uses mode 4 = DM)
+    uint8_t qp;          // QP the residual was quantised with
+    uint8_t cbf;         // bit0 Y, bit1 Cb, bit2 Cr
+    int16_t mvx, mvy;    // final quarter-pel motion vector
+    int16_t mvdx, mvdy;  // AMVP motion vector difference
+    uint8_t mvp_idx;
+    uint8_t last[3];     // last significant scan index per TU (Y 0..255, Cb/Cr 0..63)
+    uint16_t csbf_y;     // coded sub-block mask (bit = sub-block scan index)
+    uint8_t csbf_c[2];
+};
+static_assert(sizeof(CuInfo) == 20, "CuInfo layout");
+
+// Per-TU summary (cbf, last position, coded sub-blocks) of coefficients in scan order.
+MXHD bool tu_summary(const int16_t* c, int n, uint8_t* last, uint32_t* csbf) {
+    int l = -1;
+    uint32_t m = 0;
+    for (int i = 0; i < n; ++i)
+        if (c[i]) {
+            l = i;
+            m |= 1u << (i >> 4);
+        }
+    *last = (uint8_t)(l < 0 ? 0 : l);
+    *csbf = m;
+    return l >= 0;
+}
+
+// ---------------------------------------------------------------- residual_coding (7.3.8.11)
+constexpr uint8_t kLastGroup[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                    8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+constexpr uint8_t kLastMin[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
+constexpr uint8_t kSig4x4Ctx[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+
+MXHD void code_last_prefix(CabacEnc& e, uint8_t* ctx, int base, int pos, int log2n, int cidx) {
+    const int off = cidx ? 15 : 3 * (log2n - 2) + ((log2n - 1) >> 2);
+    const int shift = cidx ? log2n - 2 : (log2n + 1) >> 2;
+    const int prefix = kLastGroup[pos];
+    const int cmax = (log2n << 1) - 1;
+    for (int b = 0; b < prefix; ++b) e.bin(ctx[base + off + (b >> shift)], 1);
+    if (prefix < cmax) e.bin(ctx[base + off + (prefix >> shift)], 0);
+}
+MXHD void code_last_suffix(CabacEnc& e, int pos) {
+    const int prefix = kLastGroup[pos];
+    if (prefix > 3) e.bypass_bits((uint32_t)(pos - kLastMin[prefix]), (prefix >> 1) - 1);
+}
+
+// coeff_abs_level_remaining (9.3.3.11)
+MXHD void code_remaining(CabacEnc& e, uint32_t v, int rice) {
+    if (v < (4u << rice)) {
+        const uint32_t pre = v >> rice;
+        for (uint32_t i = 0; i < pre; ++i) e.bypass(1);
+        e.bypass(0);
+        e.bypass_bits(v & ((1u << rice) - 1), rice);
+    } else {
+        for (int i = 0; i < 4; ++i) e.bypass(1);
+        e.egk(v - (4u << rice), rice + 1);
+    }
+}
+
+// One TU (coefficients in scan order, see scan_index) of size 2^log2n (8 or 16; scanIdx 0).
+MXHD void code_residual(CabacEnc& e, uint8_t* ctx, const int16_t* c, int log2n, int cidx, int last_idx,
+                        uint32_t csbf_mask) {
+    int lx, ly;
+    scan_pos(log2n, last_idx, &lx, &ly);
+    code_last_prefix(e, ctx, C_LAST_X, lx, log2n, cidx);
+    code_last_prefix(e, ctx, C_LAST_Y, ly, log2n, cidx);
+    code_last_suffix(e, lx);
+    code_last_suffix(e, ly);
+    const int last_sb = last_idx >> 4, last_n = last_idx & 15;
+    const int sbw = 1 << (log2n - 2);  // sub-blocks per row
+    // coded_sub_block_flag per raster sub-block: coded / inferred (DC and last sub-block)
+    uint32_t csbf_r = 0;
+    for (int i = 0; i <= last_sb; ++i) {
+        const int sx = log2n == 4 ? kDiag4X[i] : kDiag2X[i], sy = log2n == 4 ? kDiag4Y[i] : kDiag2Y[i];
+        if (i == 0 || i == last_sb || ((csbf_mask >> i) & 1)) csbf_r |= 1u << (sy * sbw + sx);
+    }
+    int g1ctx_prev = -1;  // greater1Ctx state carried from the previous sub-block with levels (-1: none yet)
+    for (int i = last_sb; i >= 0; --i) {
+        const int sx = log2n == 4 ? kDiag4X[i] : kDiag2X[i], sy = log2n == 4 ? kDiag4Y[i] : kDiag2Y[i];
+        const bool right = sx + 1 < sbw && ((csbf_r >> (sy * sbw + sx + 1)) & 1);
+        const bool below = sy + 1 < sbw && ((csbf_r >> ((sy + 1) * sbw + sx)) & 1);
+        const int16_t* sb = c + i * 16;
+        bool infer_dc = false;
+        if (i < last_sb && i > 0) {
+            const int coded = (csbf_mask >> i) & 1;
+            e.bin(ctx[C_CSBF + (cidx ? 2 : 0) + ((right || below) ? 1 : 0)], coded);
+            if (!coded) continue;
+            infer_dc = true;
+        }
+        // significance
+        const int prev_csbf = (right ? 1 : 0) | (below ? 2 : 0);
+        const int nstart = (i == last_sb) ? last_n - 1 : 15;
+        for (int n = nstart; n >= 0; --n) {
+            if (n == 0 && infer_dc) break;
+            const int sig = sb[n] != 0;
+            const int xp = kDiag4X[n], yp = kDiag4Y[n];
+            int sc;
+            if (i == 0 && n == 0) {
+                sc = 0;
+            } else {
+                if (prev_csbf == 0)
+                    sc = (xp + yp == 0) ? 2 : (xp + yp < 3 ? 1 : 0);
+                else if (prev_csbf == 1)
+                    sc = yp == 0 ? 2 : (yp == 1 ? 1 : 0);
+                else if (prev_csbf == 2)
+                    sc = xp == 0 ? 2 : (xp == 1 ? 1 : 0);
+                else
+                    sc = 2;
+                if (cidx == 0) {
+                    if (i > 0) sc += 3;
+                    sc += log2n == 3 ? 9 : 21;
+                } else {
+                    sc += log2n == 3 ? 9 : 12;
+                }
+            }
+            e.bin(ctx[C_SIG + (cidx ? 27 : 0) + sc], sig);
+            if (sig) infer_dc = false;
+        }
+        // levels: nonzero coefficients from n = 15 down to 0
+        int absv[16], neg[16], nsig = 0;
+        for (int n = 15; n >= 0; --n)
+            if (sb[n]) {
+                absv[nsig] = sb[n] < 0 ? -sb[n] : sb[n];
+                neg[nsig] = sb[n] < 0;
+                ++nsig;
+            }
+        if (!nsig) continue;
+        int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+        if (g1ctx_prev == 0) ++ctx_set;
+        int g1ctx = 1;
+        int g2_idx = -1;
+        const int ng1 = nsig < 8 ? nsig : 8;
+        for (int k = 0; k < ng1; ++k) {
+            const int g1 = absv[k] > 1;
+            e.bin(ctx[C_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + (g1ctx < 3 ? g1ctx : 3)], g1);
+            if (g1) {
+                g1ctx = 0;
+                if (g2_idx < 0) g2_idx = k;
+            } else if (g1ctx > 0) {
+                ++g1ctx;
+            }
+        }
+        g1ctx_prev = g1ctx;
+        if (g2_idx >= 0) e.bin(ctx[C_GT2 + (cidx ? 4 : 0) + ctx_set], absv[g2_idx] > 2);
+        for (int k = 0; k < nsig; ++k) e.bypass(neg[k]);
+        int rice = 0;
+        for (int k = 0; k < nsig; ++k) {
+            int base, thr;
+            if (k < 8) {
+                base = 1 + (absv[k] > 1 ? 1 : 0) + (k == g2_idx && absv[k] > 2 ? 1 : 0);
+                thr = (k == g2_idx) ? 3 : 2;
+            } else {
+                base = 1;
+                thr = 1;
+            }
+            if (base == thr) {
+                code_remaining(e, (uint32_t)(absv[k] - base), rice);
+                if (absv[k] > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- CU syntax (7.3.8.5)
+MXHD void code_mvd(CabacEnc& e, uint8_t* ctx, int dx, int dy) {
+    const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
+    e.bin(ctx[C_MVD_G0], ax > 0);
+    e.bin(ctx[C_MVD_G0], ay > 0);
+    if (ax > 0) e.bin(ctx[C_MVD_G1], ax > 1);
+    if (ay > 0) e.bin(ctx[C_MVD_G1], ay > 1);
+    if (ax > 0) {
+        if (ax > 1) e.egk((uint32_t)(ax - 2), 1);
+        e.bypass(dx < 0);
+    }
+    if (ay > 0) {
+        if (ay > 1) e.egk((uint32_t)(ay - 2), 1);
+        e.bypass(dy < 0);
+    }
+}
+
+MXHD int qp_delta_wrap(int qp, int pred) { return ((qp - pred + 26 + 52) % 52) - 26; }
+
+// One CTU (= one CU).  left / above: neighbouring CUs in the same slice or null.
+// qp_prev: QP predictor (QpY of the previous CU in decoding order, slice QP at start).
+MXHD void code_cu(CabacEnc& e, uint8_t* ctx, bool islice, const CuInfo& c, const int16_t* coef, const CuInfo* left,
+                  const CuInfo* above, int& qp_prev, bool end_of_slice) {
+    if (!islice) {
+        const int inc = (left && left->type == kCuSkip ? 1 : 0) + (above && above->type == kCuSkip ? 1 : 0);
+        e.bin(ctx[C_SKIP + inc], c.type == kCuSkip);
+    }
+    if (c.type != kCuSkip) {
+        const bool intra = c.type == kCuIntra;
+        if (!islice) e.bin(ctx[C_PRED_MODE], intra);
+        e.bin(ctx[C_PART_MODE], 1);  // PART_2Nx2N
+        if (intra) {
+            const int cand_a = (left && left->type == kCuIntra) ? left->intra_mode : 1;
+            int l[3];
+            mpm_list(cand_a, 1, l);
+            const int m = c.intra_mode;
+            const int hit = (m == l[0]) ? 0 : (m == l[1] ? 1 : (m == l[2] ? 2 : -1));
+            e.bin(ctx[C_PREV_INTRA], hit >= 0);
+            if (hit >= 0) {
+                e.bypass(hit > 0);
+                if (hit > 0) e.bypass(hit > 1);
+            } else {
+                int rem = m;
+                for (int k = 0; k < 3; ++k) rem -= (l[k] < m) ? 1 : 0;
+                e.bypass_bits((uint32_t)rem, 5);
+            }
+            e.bin(ctx[C_CHROMA_PRED], 0);  // intra_chroma_pred_mode 4 (DM)
+        } else {
+            const bool merge = c.type == kCuMerge;
+            e.bin(ctx[C_MERGE_FLAG], merge);
+            if (!merge) {
+                code_mvd(e, ctx, c.mvdx, c.mvdy);
+                e.bin(ctx[C_MVP], c.mvp_idx);
+            }
+        }
+        bool root = true;
+        if (c.type == kCuAmvp) {
+            root = c.cbf != 0;
+            e.bin(ctx[C_RQT_ROOT], root);
+        }
+        if (root) {
+            const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
+            e.bin(ctx[C_CBF_CHROMA + 0], cb);
+            e.bin(ctx[C_CBF_CHROMA + 0], cr);
+            if (intra || cb || cr) e.bin(ctx[C_CBF_LUMA + 1], cy);
+            if (c.cbf) {
+                const int d = qp_delta_wrap(c.qp, qp_prev);
+                const int a = d < 0 ? -d : d;
+                const int pre = a < 5 ? a : 5;
+                for (int k = 0; k < pre; ++k) e.bin(ctx[C_QP_DELTA + (k ? 1 : 0)], 1);
+                if (pre < 5) e.bin(ctx[C_QP_DELTA + (pre ? 1 : 0)], 0);
+                if (a >= 5) e.egk((uint32_t)(a - 5), 0);
+                if (a) e.bypass(d < 0);
+                qp_prev = c.qp;
+                if (cy) code_residual(e, ctx, coef, 4, 0, c.last[0], c.csbf_y);
+                if (cb) code_residual(e, ctx, coef + 256, 3, 1, c.last[1], c.csbf_c[0]);
+                if (cr) code_residual(e, ctx, coef + 320, 3, 2, c.last[2], c.csbf_c[1]);
+            }
+        }
+    }
+    e.terminate(end_of_slice ? 1 : 0);
+}
+
+// Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row).
+// Returns the number of payload bytes (> cap means overflow).
+MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
+                         int first, int count, int ctb_w, uint8_t* ctx) {
+    ctx_init_all(ctx, islice ? 0 : 1, slice_qp);
+    CabacEnc e;
+    e.start(out, cap);
+    int qp_prev = slice_qp;
+    for (int k = 0; k < count; ++k) {
+        const int i = first + k;
+        const int x = i % ctb_w;
+        const CuInfo* left = (x > 0 && k > 0) ? &cus[i - 1] : nullptr;
+        const CuInfo* above = (k >= ctb_w) ? &cus[i - ctb_w] : nullptr;
+        code_cu(e, ctx, islice, cus[i], coef + (size_t)i * kCoefPerCu, left, above, qp_prev, k == count - 1);
+    }
+    e.finish_slice();
+    return e.pos;
+}
+
+// ---------------------------------------------------------------- encoder decisions
+// Intra candidates tried by the encoder, in tie-break order (any of the 35 modes decodes).
+constexpr int kNumIntraCands = 4;
+constexpr uint8_t kIntraCands[kNumIntraCands] = {1, 0, 26, 10};  // DC, planar, vertical, horizontal
+// Approximate luma mode signalling cost in bins given the left neighbour's MPM candidate.
+MXHD int intra_mode_bits(int mode, int cand_a) {
+    int l[3];
+    mpm_list(cand_a, 1, l);
+    if (mode == l[0]) return 2;
+    if (mode == l[1] || mode == l[2]) return 3;
+    return 6;
+}
+
+// Residual (raster NxN) -> quantised levels in scan order + reconstructed residual (raster).
+// Returns the number of nonzero levels.
+MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* levels, int* rres) {
+    const int N = 1 << log2n;
+    int c[256], d[256];
+    fwd_transform(log2n, res, c);
+    int nz = 0;
+    for (int v = 0; v < N; ++v)
+        for (int u = 0; u < N; ++u) {
+            const int l = quant_coef(c[v * N + u], qp, log2n, intra);
+            levels[scan_index(log2n, u, v)] = (int16_t)l;
+            nz += l != 0;
+            d[v * N + u] = dequant_coef(l, qp, log2n);
+        }
+    if (nz)
+        inv_transform(log2n, d, rres);
+    else
+        for (int i = 0; i < N * N; ++i) rres[i] = 0;
+    return nz;
+}
+
+// Spatial neighbour motion of a 16x16 PU (every CU of a P slice is inter, so "available"
+// means inside the picture, inside the slice and already coded).  A0 (below-left) is
+// never available: it lies in the next CTU row.
+struct MvCand {
+    bool avail;
+    int x, y;
+};
+
+// Merge candidate 0 (8.5.3.2.2-8.5.3.2.4 with MaxNumMergeCand 1, no TMVP): the first
+// available of A1, B1, B0, B2, else the zero candidate.
+MXHD MvCand merge_cand(MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
+    if (a1.avail) return a1;
+    if (b1.avail) return b1;
+    if (b0.avail) return b0;
+    if (b2.avail) return b2;
+    return MvCand{true, 0, 0};
+}
+
+// AMVP list (8.5.3.2.6/7, one reference picture so no scaling): A = A1; B = first of
+// B0, B1, B2; without A the B vector moves into A; duplicates removed; zero padding.
+MXHD void amvp_list(MvCand a1, MvCand b1, MvCand b0, MvCand b2, int* lx, int* ly) {
+    const MvCand b = b0.avail ? b0 : (b1.avail ? b1 : b2);
+    lx[1] = ly[1] = 0;
+    if (a1.avail) {
+        lx[0] = a1.x;
+        ly[0] = a1.y;
+        if (b.avail && (b.x != a1.x || b.y != a1.y)) {
+            lx[1] = b.x;
+            ly[1] = b.y;
+        }
+    } else if (b.avail) {
+        lx[0] = b.x;
+        ly[0] = b.y;
+    } else {
+        lx[0] = ly[0] = 0;
+    }
+}
+
+MXHD int mvd_cost_bits(int d) {
+    const int a = d < 0 ? -d : d;
+    if (a == 0) return 1;
+    if (a == 1) return 3;
+    int k = 1, v = a - 2, bits = 3;
+    while (v >= (1 << k)) {
+        v -= 1 << k;
+        ++k;
+        ++bits;
+    }
+    return bits + 1 + k;
+}
+
+// Fill type / mvp / mvd of an inter CU (c.mvx/mvy/cbf set) from its neighbours' motion.
+MXHD void decide_inter(CuInfo& c, MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
+    const MvCand m = merge_cand(a1, b1, b0, b2);
+    c.mvp_idx = 0;
+    c.mvdx = c.mvdy = 0;
+    if (c.mvx == m.x && c.mvy == m.y) {
+        c.type = c.cbf ? kCuMerge : kCuSkip;
+        return;
+    }
+    c.type = kCuAmvp;
+    int lx[2], ly[2];
+    amvp_list(a1, b1, b0, b2, lx, ly);
+    const int c0 = mvd_cost_bits(c.mvx - lx[0]) + mvd_cost_bits(c.mvy - ly[0]);
+    const int c1 = mvd_cost_bits(c.mvx - lx[1]) + mvd_cost_bits(c.mvy - ly[1]);
+    const int idx = c1 < c0 ? 1 : 0;
+    c.mvp_idx = (uint8_t)idx;
+    c.mvdx = (int16_t)(c.mvx - lx[idx]);
+    c.mvdy = (int16_t)(c.mvy - ly[idx]);
+}
+
+// Neighbour candidates of CU (x, y) in a picture of ctb_w CTUs whose slices are
+// slice_rows CTU rows tall; mv: per-CU quarter-pel motion, (x, y) at mv[i*stride], mv[i*stride+1].
+MXHD void inter_neighbours(const int16_t* mv, int stride, int x, int y, int ctb_w, int slice_rows, MvCand* a1,
+                           MvCand* b1, MvCand* b0, MvCand* b2) {
+    const bool up = (y % slice_rows) != 0;  // row above is in the same slice
+    auto at = [&](bool ok, int cx, int cy) {
+        MvCand c{ok, 0, 0};
+        if (ok) {
+            c.x = mv[(size_t)(cy * ctb_w + cx) * stride];
+            c.y = mv[(size_t)(cy * ctb_w + cx) * stride + 1];
+        }
+        return c;
+    };
+    *a1 = at(x > 0, x - 1, y);
+    *b1 = at(up, x, y - 1);
+    *b0 = at(up && x + 1 < ctb_w, x + 1, y - 1);
+    *b2 = at(up && x > 0, x - 1, y - 1);
+}
+
+}  // namespace hevc
+}  // namespace mx

@@ -1,0 +1,478 @@
+// HEVC host side: parameter sets / slice headers / Annex-B assembly (shared with the GPU
+// encoder) and the serial CPU encoder, which makes exactly the decisions of the HIP
+// kernels (hevc_kernels.hip) through the shared hevc_core.h functions.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "h264_mb.h"
+#include "hevc_encoder.h"
+
+namespace mx {
+namespace hevc {
+
+// ------------------------------------------------------------------ bit writer (headers)
+namespace {
+struct Bits {
+    std::vector<uint8_t> b;
+    uint32_t acc = 0;
+    int n = 0;
+    void put(uint32_t v, int k) {
+        for (int i = k - 1; i >= 0; --i) {
+            acc = (acc << 1) | ((v >> i) & 1);
+            if (++n == 8) {
+                b.push_back((uint8_t)acc);
+                acc = 0;
+                n = 0;
+            }
+        }
+    }
+    void ue(uint32_t v) {
+        const uint64_t x = (uint64_t)v + 1;
+        int len = 0;
+        while ((x >> len) > 1) ++len;
+        put(0, len);
+        put((uint32_t)x, len + 1);
+    }
+    void se(int v) { ue(v > 0 ? (uint32_t)(2 * v - 1) : (uint32_t)(-2 * v)); }
+    void trailing() {  // rbsp_trailing_bits / byte_alignment: 1 then zeros
+        put(1, 1);
+        while (n) put(0, 1);
+    }
+};
+
+void profile_tier_level(Bits& w, int level_idc) {
+    w.put(0, 2);   // general_profile_space
+    w.put(0, 1);   // general_tier_flag (Main tier)
+    w.put(1, 5);   // general_profile_idc = Main
+    w.put(0x60000000u, 32);  // compatibility flags 1 (Main) and 2 (Main 10)
+    w.put(1, 1);   // progressive_source
+    w.put(0, 1);   // interlaced_source
+    w.put(0, 1);   // non_packed_constraint
+    w.put(1, 1);   // frame_only_constraint
+    w.put(0, 32);  // 43 reserved zero bits + general_inbld_flag
+    w.put(0, 12);
+    w.put((uint32_t)level_idc, 8);
+}
+
+void nal(std::vector<uint8_t>& out, int type, const std::vector<uint8_t>& rbsp) {
+    static const uint8_t sc[4] = {0, 0, 0, 1};
+    out.insert(out.end(), sc, sc + 4);
+    out.push_back((uint8_t)(type << 1));  // forbidden 0, nal_unit_type, nuh_layer_id high bit 0
+    out.push_back(1);                      // nuh_layer_id low bits 0, nuh_temporal_id_plus1 = 1
+    h264::emulation_prevent(out, rbsp.data(), rbsp.size());
+}
+}  // namespace
+
+// Table A.6 (Main tier): general_level_idc, MaxLumaPs, MaxLumaSr, MaxSliceSegmentsPerPicture
+struct LevelLimits {
+    int idc;
+    int64_t ps, sr;
+    int slices;
+};
+static const LevelLimits kLevels[] = {
+    {30, 36864, 552960, 16},           {60, 122880, 3686400, 16},          {63, 245760, 7372800, 20},
+    {90, 552960, 16588800, 30},        {93, 983040, 33177600, 40},         {120, 2228224, 66846720, 75},
+    {123, 2228224, 133693440, 75},     {150, 8912896, 267386880, 200},     {153, 8912896, 534773760, 200},
+    {156, 8912896, 1069547520, 200},   {180, 35651584, 1069547520, 600},   {183, 35651584, 2139095040, 600},
+    {186, 35651584, 4278190080LL, 600}};
+
+int pick_level(int width, int height, int fps) {
+    const int64_t ps = (int64_t)width * height, sr = ps * std::max(1, fps);
+    for (const auto& l : kLevels) {
+        const double maxdim = std::sqrt((double)l.ps * 8);
+        if (ps <= l.ps && sr <= l.sr && width <= maxdim && height <= maxdim) return l.idc;
+    }
+    return 186;
+}
+
+int max_slices_for_level(int level_idc) {
+    for (const auto& l : kLevels)
+        if (l.idc == level_idc) return l.slices;
+    return 600;
+}
+
+HevcCommon::HevcCommon(const EncoderConfig& c) : rc_(c) {
+    level_ = pick_level(c.width, c.height, c.fps);
+    const int maxs = max_slices_for_level(level_);
+    slice_rows_ = 1;
+    while ((ctb_h() + slice_rows_ - 1) / slice_rows_ > maxs) ++slice_rows_;
+    if (num_slices() > kMaxSlices) throw std::invalid_argument("hevc: too many slices");
+}
+
+void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
+    const EncoderConfig& c = config();
+    const int cw = ctb_w() * kCtb, ch = ctb_h() * kCtb;
+    {  // VPS
+        Bits w;
+        w.put(0, 4);       // vps_video_parameter_set_id
+        w.put(1, 1);       // vps_base_layer_internal_flag
+        w.put(1, 1);       // vps_base_layer_available_flag
+        w.put(0, 6);       // vps_max_layers_minus1
+        w.put(0, 3);       // vps_max_sub_layers_minus1
+        w.put(1, 1);       // vps_temporal_id_nesting_flag
+        w.put(0xffff, 16);
+        profile_tier_level(w, level_);
+        w.put(1, 1);  // vps_sub_layer_ordering_info_present_flag
+        w.ue(1);      // vps_max_dec_pic_buffering_minus1
+        w.ue(0);      // vps_max_num_reorder_pics
+        w.ue(0);      // vps_max_latency_increase_plus1
+        w.put(0, 6);  // vps_max_layer_id
+        w.ue(0);      // vps_num_layer_sets_minus1
+        w.put(0, 1);  // vps_timing_info_present_flag
+        w.put(0, 1);  // vps_extension_flag
+        w.trailing();
+        nal(out, 32, w.b);
+    }
+    {  // SPS
+        Bits w;
+        w.put(0, 4);  // sps_video_parameter_set_id
+        w.put(0, 3);  // sps_max_sub_layers_minus1
+        w.put(1, 1);  // sps_temporal_id_nesting_flag
+        profile_tier_level(w, level_);
+        w.ue(0);  // sps_seq_parameter_set_id
+        w.ue(1);  // chroma_format_idc 4:2:0
+        w.ue((uint32_t)cw);
+        w.ue((uint32_t)ch);
+        const bool crop = cw != c.width || ch != c.height;
+        w.put(crop, 1);
+        if (crop) {
+            w.ue(0);
+            w.ue((uint32_t)(cw - c.width) / 2);
+            w.ue(0);
+            w.ue((uint32_t)(ch - c.height) / 2);
+        }
+        w.ue(0);  // bit_depth_luma_minus8
+        w.ue(0);  // bit_depth_chroma_minus8
+        w.ue(4);  // log2_max_pic_order_cnt_lsb_minus4 (8-bit POC LSB)
+        w.put(1, 1);  // sps_sub_layer_ordering_info_present_flag
+        w.ue(1);
+        w.ue(0);
+        w.ue(0);
+        w.ue(1);  // log2_min_luma_coding_block_size_minus3 (16)
+        w.ue(0);  // log2_diff_max_min_luma_coding_block_size (CTB 16)
+        w.ue(0);  // log2_min_luma_transform_block_size_minus2 (4)
+        w.ue(2);  // log2_diff_max_min_luma_transform_block_size (16)
+        w.ue(0);  // max_transform_hierarchy_depth_inter
+        w.ue(0);  // max_transform_hierarchy_depth_intra
+        w.put(0, 1);  // scaling_list_enabled_flag
+        w.put(0, 1);  // amp_enabled_flag
+        w.put(0, 1);  // sample_adaptive_offset_enabled_flag
+        w.put(0, 1);  // pcm_enabled_flag
+        w.ue(1);      // num_short_term_ref_pic_sets
+        w.ue(1);      // st_ref_pic_set(0): num_negative_pics
+        w.ue(0);      //   num_positive_pics
+        w.ue(0);      //   delta_poc_s0_minus1
+        w.put(1, 1);  //   used_by_curr_pic_s0_flag
+        w.put(0, 1);  // long_term_ref_pics_present_flag
+        w.put(0, 1);  // sps_temporal_mvp_enabled_flag
+        w.put(0, 1);  // strong_intra_smoothing_enabled_flag
+        w.put(1, 1);  // vui_parameters_present_flag
+        w.put(0, 1);  //   aspect_ratio_info_present_flag
+        w.put(0, 1);  //   overscan_info_present_flag
+        w.put(1, 1);  //   video_signal_type_present_flag
+        w.put(5, 3);  //     video_format (unspecified)
+        w.put(0, 1);  //     video_full_range_flag (limited range, as the CSC produces)
+        w.put(1, 1);  //     colour_description_present_flag
+        w.put(1, 8);  //     colour_primaries BT.709
+        w.put(1, 8);  //     transfer_characteristics BT.709
+        w.put(1, 8);  //     matrix_coeffs BT.709
+        w.put(0, 1);  //   chroma_loc_info_present_flag
+        w.put(0, 1);  //   neutral_chroma_indication_flag
+        w.put(0, 1);  //   field_seq_flag
+        w.put(0, 1);  //   frame_field_info_present_flag
+        w.put(0, 1);  //   default_display_window_flag
+        w.put(1, 1);  //   vui_timing_info_present_flag
+        w.put(1, 32);  //     vui_num_units_in_tick
+        w.put((uint32_t)std::max(1, c.fps), 32);  // vui_time_scale
+        w.put(0, 1);  //     vui_poc_proportional_to_timing_flag
+        w.put(0, 1);  //     vui_hrd_parameters_present_flag
+        w.put(0, 1);  //   bitstream_restriction_flag
+        w.put(0, 1);  // sps_extension_present_flag
+        w.trailing();
+        nal(out, 33, w.b);
+    }
+    {  // PPS
+        Bits w;
+        w.ue(0);      // pps_pic_parameter_set_id
+        w.ue(0);      // pps_seq_parameter_set_id
+        w.put(0, 1);  // dependent_slice_segments_enabled_flag
+        w.put(0, 1);  // output_flag_present_flag
+        w.put(0, 3);  // num_extra_slice_header_bits
+        w.put(0, 1);  // sign_data_hiding_enabled_flag
+        w.put(0, 1);  // cabac_init_present_flag
+        w.ue(0);      // num_ref_idx_l0_default_active_minus1
+        w.ue(0);      // num_ref_idx_l1_default_active_minus1
+        w.se(0);      // init_qp_minus26
+        w.put(0, 1);  // constrained_intra_pred_flag
+        w.put(0, 1);  // transform_skip_enabled_flag
+        w.put(1, 1);  // cu_qp_delta_enabled_flag
+        w.ue(0);      //   diff_cu_qp_delta_depth (one QP per 16x16 CU)
+        w.se(c.chroma_qp_offset);  // pps_cb_qp_offset
+        w.se(c.chroma_qp_offset);  // pps_cr_qp_offset
+        w.put(0, 1);  // pps_slice_chroma_qp_offsets_present_flag
+        w.put(0, 1);  // weighted_pred_flag
+        w.put(0, 1);  // weighted_bipred_flag
+        w.put(0, 1);  // transquant_bypass_enabled_flag
+        w.put(0, 1);  // tiles_enabled_flag
+        w.put(0, 1);  // entropy_coding_sync_enabled_flag
+        w.put(0, 1);  // pps_loop_filter_across_slices_enabled_flag
+        w.put(1, 1);  // deblocking_filter_control_present_flag
+        w.put(0, 1);  //   deblocking_filter_override_enabled_flag
+        w.put(1, 1);  //   pps_deblocking_filter_disabled_flag
+        w.put(0, 1);  // pps_scaling_list_data_present_flag
+        w.put(0, 1);  // lists_modification_present_flag
+        w.ue(0);      // log2_parallel_merge_level_minus2
+        w.put(0, 1);  // slice_segment_header_extension_present_flag
+        w.put(0, 1);  // pps_extension_present_flag
+        w.trailing();
+        nal(out, 34, w.b);
+    }
+}
+
+void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int slice, bool idr, int poc, int qp,
+                                 const uint8_t* data, size_t n) const {
+    const int ctbs = ctb_w() * ctb_h();
+    const int addr = slice * slice_rows_ * ctb_w();
+    Bits w;
+    w.put(addr == 0, 1);  // first_slice_segment_in_pic_flag
+    if (idr) w.put(0, 1);  // no_output_of_prior_pics_flag
+    w.ue(0);               // slice_pic_parameter_set_id
+    if (addr != 0) {
+        int bits = 0;
+        while ((1 << bits) < ctbs) ++bits;
+        w.put((uint32_t)addr, bits);  // slice_segment_address
+    }
+    w.ue(idr ? 2 : 1);  // slice_type I / P
+    if (!idr) {
+        w.put((uint32_t)(poc & 255), 8);  // slice_pic_order_cnt_lsb
+        w.put(1, 1);                      // short_term_ref_pic_set_sps_flag
+    }
+    if (!idr) {
+        w.put(0, 1);  // num_ref_idx_active_override_flag
+        w.ue(4);      // five_minus_max_num_merge_cand -> MaxNumMergeCand 1
+    }
+    w.se(qp - 26);  // slice_qp_delta
+    w.trailing();   // byte_alignment()
+    std::vector<uint8_t> rbsp = std::move(w.b);
+    rbsp.insert(rbsp.end(), data, data + n);
+    nal(out, idr ? 19 : 1, rbsp);  // IDR_W_RADL / TRAIL_R
+}
+
+// ------------------------------------------------------------------ CPU encoder
+CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
+    cw_ = common_.ctb_w() * kCtb;
+    ch_ = common_.ctb_h() * kCtb;
+    for (int i = 0; i < 2; ++i) {
+        rec_y_[i].assign((size_t)cw_ * ch_, 16);
+        rec_uv_[i].assign((size_t)cw_ * ch_ / 2, 128);
+    }
+    const size_t n = (size_t)common_.ctb_w() * common_.ctb_h();
+    cu_.resize(n);
+    mv_.resize(2 * n);
+    coef_.resize(n * kCoefPerCu);
+}
+
+namespace {
+// Finish a CU's residual bookkeeping: cbf / last / coded sub-block masks.
+void summarise(CuInfo& c, const int16_t* coef) {
+    uint32_t m;
+    c.cbf = 0;
+    if (tu_summary(coef, 256, &c.last[0], &m)) c.cbf |= 1;
+    c.csbf_y = (uint16_t)m;
+    if (tu_summary(coef + 256, 64, &c.last[1], &m)) c.cbf |= 2;
+    c.csbf_c[0] = (uint8_t)m;
+    if (tu_summary(coef + 320, 64, &c.last[2], &m)) c.cbf |= 4;
+    c.csbf_c[1] = (uint8_t)m;
+}
+}  // namespace
+
+void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
+    uint8_t* ry = rec_y_[cur_].data();
+    uint8_t* ruv = rec_uv_[cur_].data();
+    const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
+    const int qp = common_.rc().cur_qp();
+    const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+    const int lambda = h264::lambda_sad(qp);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const int i = y * W + x, x0 = x * 16, y0 = y * 16;
+            CuInfo& c = cu_[i];
+            std::memset(&c, 0, sizeof c);
+            const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < W, ac = at && x > 0;
+            uint8_t lp[16], tp[16], tr[16];
+            for (int k = 0; k < 16; ++k) {
+                lp[k] = al ? ry[(y0 + k) * cw_ + x0 - 1] : 0;
+                tp[k] = at ? ry[(y0 - 1) * cw_ + x0 + k] : 0;
+                tr[k] = atr ? ry[(y0 - 1) * cw_ + x0 + 16 + k] : 0;
+            }
+            const int corner = ac ? ry[(y0 - 1) * cw_ + x0 - 1] : 0;
+            int L[33], T[33];
+            intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
+            const int cand_a = al ? cu_[i - 1].intra_mode : 1;
+            int best = -1, best_cost = 0;
+            int pred[256];
+            for (int k = 0; k < kNumIntraCands; ++k) {
+                const int m = kIntraCands[k];
+                intra_predict(m, 4, 0, L, T, pred);
+                int sad = 0;
+                for (int r = 0; r < 16; ++r)
+                    for (int q = 0; q < 16; ++q) sad += std::abs((int)sy[(y0 + r) * pitch + x0 + q] - pred[r * 16 + q]);
+                const int cost = sad + lambda * intra_mode_bits(m, cand_a);
+                if (best < 0 || cost < best_cost) {
+                    best = m;
+                    best_cost = cost;
+                }
+            }
+            c.type = kCuIntra;
+            c.intra_mode = (uint8_t)best;
+            c.qp = (uint8_t)qp;
+            int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
+            intra_predict(best, 4, 0, L, T, pred);
+            int res[256], rr[256];
+            for (int r = 0; r < 16; ++r)
+                for (int q = 0; q < 16; ++q) res[r * 16 + q] = sy[(y0 + r) * pitch + x0 + q] - pred[r * 16 + q];
+            tu_encode(4, res, qp, true, co, rr);
+            for (int r = 0; r < 16; ++r)
+                for (int q = 0; q < 16; ++q) ry[(y0 + r) * cw_ + x0 + q] = (uint8_t)clip255(pred[r * 16 + q] + rr[r * 16 + q]);
+            for (int comp = 0; comp < 2; ++comp) {
+                const int xc = x0 / 2, yc = y0 / 2;
+                uint8_t lc[8], tc[8], trc[8];
+                for (int k = 0; k < 8; ++k) {
+                    lc[k] = al ? ruv[(yc + k) * cw_ + 2 * (xc - 1) + comp] : 0;
+                    tc[k] = at ? ruv[(yc - 1) * cw_ + 2 * (xc + k) + comp] : 0;
+                    trc[k] = atr ? ruv[(yc - 1) * cw_ + 2 * (xc + 8 + k) + comp] : 0;
+                }
+                const int cc = ac ? ruv[(yc - 1) * cw_ + 2 * (xc - 1) + comp] : 0;
+                int Lc[17], Tc[17], pc[64], rc[64], rrc[64];
+                intra_refs(8, al, false, at, atr, ac, lc, lc, tc, trc, cc, Lc, Tc);
+                intra_predict(best, 3, 1 + comp, Lc, Tc, pc);
+                for (int r = 0; r < 8; ++r)
+                    for (int q = 0; q < 8; ++q) rc[r * 8 + q] = suv[(yc + r) * pitch + 2 * (xc + q) + comp] - pc[r * 8 + q];
+                tu_encode(3, rc, qpc, true, co + 256 + 64 * comp, rrc);
+                for (int r = 0; r < 8; ++r)
+                    for (int q = 0; q < 8; ++q)
+                        ruv[(yc + r) * cw_ + 2 * (xc + q) + comp] = (uint8_t)clip255(pc[r * 8 + q] + rrc[r * 8 + q]);
+            }
+            summarise(c, co);
+            mv_[2 * i] = mv_[2 * i + 1] = 0;
+        }
+}
+
+void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pitch) {
+    const uint8_t* ref_y = rec_y_[cur_ ^ 1].data();
+    const uint8_t* ref_uv = rec_uv_[cur_ ^ 1].data();
+    uint8_t* ry = rec_y_[cur_].data();
+    uint8_t* ruv = rec_uv_[cur_].data();
+    const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
+    const int fqp = common_.rc().cur_qp();
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const int i = y * W + x;
+            int mvx = 0, mvy = 0;
+            h264::me_search_cpu(sy, pitch, ref_y, cw_, ch_, x * 16, y * 16, fqp, cfg_.search_range, cfg_.subpel, &mvx,
+                                &mvy);
+            mv_[2 * i] = (int16_t)mvx;
+            mv_[2 * i + 1] = (int16_t)mvy;
+        }
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const int i = y * W + x, x0 = x * 16, y0 = y * 16;
+            CuInfo& c = cu_[i];
+            std::memset(&c, 0, sizeof c);
+            c.mvx = mv_[2 * i];
+            c.mvy = mv_[2 * i + 1];
+            int pred[256], res[256], rr[256];
+            uint32_t lsad = 0;
+            for (int r = 0; r < 16; ++r)
+                for (int q = 0; q < 16; ++q) {
+                    const int p = luma_mc(ref_y, cw_, cw_, ch_, x0 + q, y0 + r, c.mvx, c.mvy);
+                    pred[r * 16 + q] = p;
+                    res[r * 16 + q] = sy[(y0 + r) * pitch + x0 + q] - p;
+                    lsad += (uint32_t)std::abs(res[r * 16 + q]);
+                }
+            const int qp = h264::aq_mb_qp(fqp, lsad, cfg_.aq);
+            const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+            c.qp = (uint8_t)qp;
+            int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
+            tu_encode(4, res, qp, false, co, rr);
+            for (int r = 0; r < 16; ++r)
+                for (int q = 0; q < 16; ++q) ry[(y0 + r) * cw_ + x0 + q] = (uint8_t)clip255(pred[r * 16 + q] + rr[r * 16 + q]);
+            for (int comp = 0; comp < 2; ++comp) {
+                int pc[64], rc[64], rrc[64];
+                const int xc = x0 / 2, yc = y0 / 2;
+                for (int r = 0; r < 8; ++r)
+                    for (int q = 0; q < 8; ++q) {
+                        const int p = chroma_mc(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc + q, yc + r, c.mvx, c.mvy);
+                        pc[r * 8 + q] = p;
+                        rc[r * 8 + q] = suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
+                    }
+                tu_encode(3, rc, qpc, false, co + 256 + 64 * comp, rrc);
+                for (int r = 0; r < 8; ++r)
+                    for (int q = 0; q < 8; ++q)
+                        ruv[(yc + r) * cw_ + 2 * (xc + q) + comp] = (uint8_t)clip255(pc[r * 8 + q] + rrc[r * 8 + q]);
+            }
+            summarise(c, co);
+        }
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            MvCand a1, b1, b0, b2;
+            inter_neighbours(mv_.data(), 2, x, y, W, sr, &a1, &b1, &b0, &b2);
+            decide_inter(cu_[y * W + x], a1, b1, b0, b2);
+        }
+}
+
+const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
+    h264::EncoderCommon& rc = common_.rc();
+    rc.begin_frame(force_idr || !have_ref_);
+    const bool idr = rc.cur_idr();
+    const int qp = rc.cur_qp();
+    if (have_ref_) cur_ ^= 1;
+    have_ref_ = true;
+    if (idr)
+        analyse_intra(y, uv, pitch);
+    else
+        analyse_inter(y, uv, pitch);
+    au_.clear();
+    if (idr) common_.write_parameter_sets(au_);
+    const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
+    std::vector<uint8_t> buf;
+    uint8_t ctx[C_NUM];
+    for (int s = 0; s < common_.num_slices(); ++s) {
+        const int first = s * sr * W, count = std::min(sr, H - s * sr) * W;
+        const uint32_t cap = (uint32_t)count * 1024 + 1024;
+        buf.resize(cap);
+        const uint32_t n = code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count, W, ctx);
+        if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
+        common_.write_slice_nal(au_, s, idr, idr ? 0 : common_.poc(), qp, buf.data(), n);
+    }
+    // distortion over the display area
+    const EncoderConfig& c = common_.config();
+    uint64_t sse[3] = {0, 0, 0};
+    const uint8_t* ry = rec_y_[cur_].data();
+    const uint8_t* ruv = rec_uv_[cur_].data();
+    for (int r = 0; r < c.height; ++r)
+        for (int q = 0; q < c.width; ++q) {
+            const int d = (int)y[r * pitch + q] - ry[r * cw_ + q];
+            sse[0] += (uint64_t)(d * d);
+        }
+    for (int r = 0; r < c.height / 2; ++r)
+        for (int q = 0; q < c.width / 2; ++q)
+            for (int comp = 0; comp < 2; ++comp) {
+                const int d = (int)uv[r * pitch + 2 * q + comp] - ruv[r * cw_ + 2 * q + comp];
+                sse[1 + comp] += (uint64_t)(d * d);
+            }
+    stats_.frame_index = rc.frames();
+    stats_.idr = idr;
+    stats_.qp = qp;
+    stats_.bytes = (int)au_.size();
+    stats_.skipped_mbs = 0;
+    for (const auto& cu : cu_) stats_.skipped_mbs += cu.type == kCuSkip;
+    for (int k = 0; k < 3; ++k) stats_.sse[k] = sse[k];
+    rc.end_frame((int)au_.size(), idr);
+    return au_;
+}
+
+}  // namespace hevc
+}  // namespace mx

@@ -1,0 +1,197 @@
+// Host-side HEVC encoder API: GpuHevcEncoder (HIP kernels, production path) and
+// CpuHevcEncoder (same decisions and syntax, serial C++ over the shared hevc_core.h
+// functions; bit-exact oracle of the GPU encoder in tests).
+//
+// Reference parity: the reference's WEBRTC_ENCODER selects a GStreamer encoder element
+// (reference Dockerfile:210, README.md:21); the HEVC configuration of BASELINE.json ("4K60
+// HEVC, HIP CSC+scale path") runs through these classes ("mxh265enc").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <deque>
+#include <vector>
+
+#include "h264_encoder.h"
+#include "hevc_core.h"
+
+namespace mx {
+namespace hevc {
+
+using h264::EncoderConfig;
+using h264::FrameStats;
+using h264::Geometry;
+
+// Level (A.4) for a picture size / frame rate, as general_level_idc (30 x level).
+int pick_level(int width, int height, int fps);
+int max_slices_for_level(int level_idc);
+
+// Parameter sets, slice headers and Annex-B assembly shared by both encoders.  Rate
+// control and IDR scheduling come from h264::EncoderCommon (codec independent).
+class HevcCommon {
+   public:
+    explicit HevcCommon(const EncoderConfig& c);
+    h264::EncoderCommon& rc() { return rc_; }
+    const h264::EncoderCommon& rc() const { return rc_; }
+    const EncoderConfig& config() const { return rc_.config(); }
+    int ctb_w() const { return rc_.mb_w(); }
+    int ctb_h() const { return rc_.mb_h(); }
+    int slice_rows() const { return slice_rows_; }
+    int num_slices() const { return (ctb_h() + slice_rows_ - 1) / slice_rows_; }
+    int level_idc() const { return level_; }
+    // POC LSB (8 bits) of the current frame = frames since the last IDR.
+    int poc() const { return rc_.cur_frame_num(); }
+    void write_parameter_sets(std::vector<uint8_t>& out) const;
+    // One slice segment NAL: start code, NAL header, header + payload with emulation prevention.
+    void write_slice_nal(std::vector<uint8_t>& out, int slice, bool idr, int poc, int qp, const uint8_t* data,
+                         size_t n) const;
+
+   private:
+    h264::EncoderCommon rc_;
+    int slice_rows_ = 1;
+    int level_ = 0;
+};
+
+class CpuHevcEncoder {
+   public:
+    explicit CpuHevcEncoder(const EncoderConfig& cfg);
+    // NV12 frame in host memory (pitch shared by both planes, at least the coded size readable;
+    // h264::pad_nv12 pads display-sized frames).
+    const std::vector<uint8_t>& encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr = false);
+    const FrameStats& last_stats() const { return stats_; }
+    HevcCommon& common() { return common_; }
+    const std::vector<uint8_t>& recon_y() const { return rec_y_[cur_]; }
+    const std::vector<uint8_t>& recon_uv() const { return rec_uv_[cur_]; }
+    int coded_pitch() const { return cw_; }
+    const std::vector<CuInfo>& cus() const { return cu_; }
+
+   private:
+    void analyse_intra(const uint8_t* y, const uint8_t* uv, int pitch);
+    void analyse_inter(const uint8_t* y, const uint8_t* uv, int pitch);
+
+    EncoderConfig cfg_;
+    HevcCommon common_;
+    int cw_, ch_;
+    std::vector<uint8_t> rec_y_[2], rec_uv_[2];
+    int cur_ = 0;
+    bool have_ref_ = false;
+    std::vector<CuInfo> cu_;
+    std::vector<int16_t> mv_;  // per CU (x, y)
+    std::vector<int16_t> coef_;
+    std::vector<uint8_t> au_;
+    FrameStats stats_;
+};
+
+// ---------------------------------------------------------------- GPU encoder
+// Per-frame kernel chain (hevc_kernels.hip):
+//   P: k_hpel -> k_me_full (shared with H.264) -> k_hevc_inter -> k_hevc_decide
+//   I: k_hevc_intra (one workgroup per slice, wavefront over its CTU rows)
+//   then k_hevc_cabac (one wave per slice) -> k_hevc_pack (zero-copy into pinned memory)
+struct HevcFrameState {
+    const uint8_t* ref_y;
+    const uint8_t* ref_uv;
+    uint8_t* rec_y;
+    uint8_t* rec_uv;
+    const uint8_t* hp_f;  // padded full-sample reference luma (origin at picture (0,0))
+    int32_t hp_pitch;
+    int32_t idr;
+    int32_t qp;
+    int32_t slice_rows;
+    int32_t num_slices;
+    int32_t aq;
+    int32_t chroma_qp_offset;
+    int32_t pad;
+    unsigned long long* sse_part;  // [3][kSsePartStride] per-workgroup distortion partials
+};
+
+struct HevcOutHeader {
+    uint32_t total_bytes;
+    uint32_t num_slices;
+    uint32_t overflow;
+    uint32_t pad;
+    uint64_t sse[3];
+    uint64_t pad2;
+};
+static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
+constexpr int kMaxSlices = 1024;
+constexpr size_t kOutPayloadOffset = sizeof(HevcOutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
+
+struct HevcDeviceBuffers {
+    HevcFrameState* fs;
+    h264::DeviceBuffers me;  // H.264 ME state (frame state + MbInfo with the motion vectors)
+    CuInfo* cu;
+    int16_t* coef;
+    uint8_t* slice_data;     // [num_slices * slice_cap]
+    uint32_t* slice_len;     // [num_slices]
+    uint32_t slice_cap;
+    size_t out_bytes;
+    unsigned long long* sse_part;
+};
+
+void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                       hipStream_t s);
+void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
+                       const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
+void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int num_slices, uint8_t* host_out,
+                         hipStream_t s);
+
+class GpuHevcEncoder {
+   public:
+    static constexpr int kMaxInFlight = 2;
+    GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream);
+    ~GpuHevcEncoder();
+    GpuHevcEncoder(const GpuHevcEncoder&) = delete;
+    GpuHevcEncoder& operator=(const GpuHevcEncoder&) = delete;
+
+    const Geometry& geometry() const { return geom_; }
+    int pitch() const { return geom_.pitch; }
+    int depth() const { return depth_; }
+    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false);
+    const std::vector<uint8_t>& collect();
+    const FrameStats& last_stats() const { return stats_; }
+    HevcCommon& common() { return common_; }
+    const uint8_t* recon_y() const { return rec_y_[cur_]; }
+    const uint8_t* recon_uv() const { return rec_uv_[cur_]; }
+    hipEvent_t done_event() const { return last_done_; }
+    // split form (same as GpuH264Encoder) for the session's graph path
+    bool prepare(bool force_idr);
+    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
+    void record_start();
+    void record_done();
+
+   private:
+    struct FrameSlot {
+        HevcDeviceBuffers buf{};
+        HevcFrameState* fs_host = nullptr;     // pinned
+        h264::FrameState* me_fs_host = nullptr;  // pinned
+        uint8_t* host_out = nullptr;           // pinned, mapped
+        hipEvent_t start = nullptr, analysis_done = nullptr, done = nullptr;
+        bool idr = false;
+        int qp = 0;
+        int poc = 0;
+    };
+    void alloc_slot(FrameSlot& sl);
+    void free_slot(FrameSlot& sl);
+
+    EncoderConfig cfg_;
+    HevcCommon common_;
+    hipStream_t stream_;
+    hipStream_t stream_e_ = nullptr;
+    int depth_ = 1;
+    Geometry geom_;
+    FrameSlot slots_[kMaxInFlight];
+    int next_slot_ = 0, prep_slot_ = 0;
+    std::deque<int> inflight_;
+    hipEvent_t last_done_ = nullptr;
+    uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};
+    int hp_pitch_ = 0;
+    uint8_t* rec_y_[2] = {nullptr, nullptr};
+    uint8_t* rec_uv_[2] = {nullptr, nullptr};
+    int cur_ = 0;
+    bool have_ref_ = false;
+    std::vector<uint8_t> au_;
+    FrameStats stats_;
+};
+
+}  // namespace hevc
+}  // namespace mx
