@@ -249,6 +249,46 @@ PYBIND11_MODULE(_native, m) {
         .def("request_idr", [](hevc::CpuHevcEncoder& e) { e.common().rc().request_idr(); })
         .def("set_bitrate", [](hevc::CpuHevcEncoder& e, int k) { e.common().rc().set_bitrate(k); })
         .def_property_readonly("stats", &hevc::CpuHevcEncoder::last_stats);
+    py::class_<hevc::GpuHevcEncoder>(m, "GpuHevcEncoder")
+        .def(py::init([](const h264::EncoderConfig& c, uintptr_t stream) {
+                 return new hevc::GpuHevcEncoder(c, as_stream(stream));
+             }),
+             py::arg("config"), py::arg("stream") = 0)
+        .def_property_readonly("pitch", &hevc::GpuHevcEncoder::pitch)
+        .def_property_readonly("coded_height", [](hevc::GpuHevcEncoder& e) { return e.geometry().coded_h; })
+        .def_property_readonly("slice_rows", [](hevc::GpuHevcEncoder& e) { return e.common().slice_rows(); })
+        .def(
+            "encode",
+            [](hevc::GpuHevcEncoder& e, uintptr_t y, uintptr_t uv, bool force_idr) {
+                std::vector<uint8_t> au;
+                {
+                    py::gil_scoped_release rel;
+                    e.submit(as_ptr<const uint8_t>(y), as_ptr<const uint8_t>(uv), force_idr);
+                    au = e.collect();
+                }
+                return to_bytes(au);
+            },
+            py::arg("y_ptr"), py::arg("uv_ptr"), py::arg("force_idr") = false)
+        .def("submit", [](hevc::GpuHevcEncoder& e, uintptr_t y, uintptr_t uv,
+                          bool force_idr) { e.submit(as_ptr<const uint8_t>(y), as_ptr<const uint8_t>(uv), force_idr); })
+        .def("collect",
+             [](hevc::GpuHevcEncoder& e) {
+                 std::vector<uint8_t> au;
+                 {
+                     py::gil_scoped_release rel;
+                     au = e.collect();
+                 }
+                 return to_bytes(au);
+             })
+        .def("recon",
+             [](hevc::GpuHevcEncoder& e) {
+                 const auto& g = e.geometry();
+                 return py::make_tuple(copy_plane(e.recon_y(), g.pitch, g.coded_w, g.coded_h),
+                                       copy_plane(e.recon_uv(), g.pitch, g.coded_w, g.coded_h / 2));
+             })
+        .def("request_idr", [](hevc::GpuHevcEncoder& e) { e.common().rc().request_idr(); })
+        .def("set_bitrate", [](hevc::GpuHevcEncoder& e, int k) { e.common().rc().set_bitrate(k); })
+        .def_property_readonly("stats", &hevc::GpuHevcEncoder::last_stats);
     m.def("hevc_level", &hevc::pick_level, py::arg("width"), py::arg("height"), py::arg("fps"));
 
     py::class_<h264::GpuH264Encoder>(m, "GpuH264Encoder")
@@ -385,6 +425,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("pool_slots", &SessionConfig::pool_slots)
         .def_readwrite("use_graph", &SessionConfig::use_graph)
         .def_readwrite("fake_clock", &SessionConfig::fake_clock)
+        .def_readwrite("codec", &SessionConfig::codec)
         .def_readwrite("enc", &SessionConfig::enc);
 
     py::class_<FrameResult>(m, "FrameResult")
@@ -442,6 +483,7 @@ PYBIND11_MODULE(_native, m) {
         .def_property_readonly("graphs_built", &Session::graphs_built)
         .def_property_readonly("in_flight", &Session::in_flight)
         .def_property_readonly("depth", &Session::depth)
+        .def_property_readonly("codec", [](Session& s) { return std::string(s.encoder().codec()); })
         .def("nv12",
              [](Session& s) {
                  const auto& g = s.encoder().geometry();

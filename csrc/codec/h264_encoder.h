@@ -15,6 +15,7 @@
 
 #include "h264_core.h"
 #include "h264_gpu.h"
+#include "video_encoder.h"
 
 namespace mx {
 namespace h264 {
@@ -92,18 +93,20 @@ void emulation_prevent(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n)
 std::vector<std::vector<uint8_t>> hpel_planes_for_test(const uint8_t* ref, int coded_w, int coded_h, int pitch,
                                                        int* hp_pitch);
 
-class GpuH264Encoder {
+class GpuH264Encoder final : public VideoEncoder {
    public:
+    const char* codec() const override { return "h264"; }
+    EncoderCommon& rc() override { return common_; }
     static constexpr int kMaxInFlight = 2;
     GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream);
     ~GpuH264Encoder();
     GpuH264Encoder(const GpuH264Encoder&) = delete;
     GpuH264Encoder& operator=(const GpuH264Encoder&) = delete;
 
-    const Geometry& geometry() const { return geom_; }
-    int pitch() const { return geom_.pitch; }
+    const Geometry& geometry() const override { return geom_; }
+    int pitch() const override { return geom_.pitch; }
     hipStream_t stream() const { return stream_; }
-    int depth() const { return depth_; }
+    int depth() const override { return depth_; }
     int in_flight() const { return (int)inflight_.size(); }
 
     // Enqueue the encode of an NV12 frame already in device memory (pitch = pitch()).
@@ -111,23 +114,23 @@ class GpuH264Encoder {
     // pipeline_depth 2 a second frame may be submitted before the first is collected:
     // analysis (hpel/ME/inter or intra) runs on `stream`, entropy coding (CAVLC/scan/pack) on
     // an internal stream, so frame n's entropy coding overlaps frame n+1's analysis.
-    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false);
+    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false) override;
     // Wait for the oldest submitted frame and return its Annex-B access unit.
-    const std::vector<uint8_t>& collect();
-    const FrameStats& last_stats() const { return stats_; }
+    const std::vector<uint8_t>& collect() override;
+    const FrameStats& last_stats() const override { return stats_; }
     EncoderCommon& common() { return common_; }
     // Reconstructed frame of the last prepared picture (device pointers).
-    const uint8_t* recon_y() const { return rec_y_[cur_]; }
-    const uint8_t* recon_uv() const { return rec_uv_[cur_]; }
+    const uint8_t* recon_y() const override { return rec_y_[cur_]; }
+    const uint8_t* recon_uv() const override { return rec_uv_[cur_]; }
     // Split form for hipGraph replay (depth 1): host-side frame decisions (rate control,
     // reference swap) into the pinned frame state; returns whether this is an IDR frame.
-    bool prepare(bool force_idr);
+    bool prepare(bool force_idr) override;
     // Frame-state upload + kernels (stream-capturable; identical every frame of a type).
-    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
-    void record_start();
-    void record_done();
+    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
+    void record_start() override;
+    void record_done() override;
     // Completion event of the last collected frame.
-    hipEvent_t done_event() const { return last_done_; }
+    hipEvent_t done_event() const override { return last_done_; }
     void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
 
    private:

@@ -162,43 +162,32 @@ MXHD int inv_angle(int angle) {
 // (N), trx: top-right (N), corner: p[-1][-1].
 MXHD void intra_refs(int N, bool a_left, bool a_bl, bool a_top, bool a_tr, bool a_corner, const uint8_t* lpx,
                      const uint8_t* bpx, const uint8_t* tpx, const uint8_t* trx, int corner, int* left, int* top) {
-    // linear order of the spec's search: p[-1][2N-1] .. p[-1][-1], p[0][-1] .. p[2N-1][-1]
-    // -> q[0 .. 4N]
-    int q[4 * 32 + 1];
-    bool av[4 * 32 + 1];
+    // The spec's search order p[-1][2N-1] .. p[-1][-1], p[0][-1] .. p[2N-1][-1] is the linear
+    // index i = 0 .. 4N; i < 2N lives in left[2N - i], i == 2N is the corner, i > 2N in top[i - 2N].
+    const int n2 = 2 * N, total = 4 * N + 1;
+    auto avail = [&](int i) { return i < N ? a_bl : (i < n2 ? a_left : (i == n2 ? a_corner : (i <= 3 * N ? a_top : a_tr))); };
+    auto ref = [&](int i) -> int& { return i < n2 ? left[n2 - i] : (i == n2 ? left[0] : top[i - n2]); };
     for (int k = 0; k < N; ++k) {
-        q[k] = a_bl ? bpx[N - 1 - k] : 0;  // p[-1][2N-1-k]
-        av[k] = a_bl;
-        q[N + k] = a_left ? lpx[N - 1 - k] : 0;  // p[-1][N-1-k]
-        av[N + k] = a_left;
-        q[2 * N + 1 + k] = a_top ? tpx[k] : 0;
-        av[2 * N + 1 + k] = a_top;
-        q[3 * N + 1 + k] = a_tr ? trx[k] : 0;
-        av[3 * N + 1 + k] = a_tr;
+        left[1 + k] = a_left ? lpx[k] : 0;
+        left[1 + N + k] = a_bl ? bpx[k] : 0;
+        top[1 + k] = a_top ? tpx[k] : 0;
+        top[1 + N + k] = a_tr ? trx[k] : 0;
     }
-    q[2 * N] = corner;
-    av[2 * N] = a_corner;
-    const int total = 4 * N + 1;
-    bool any = false;
-    for (int i = 0; i < total; ++i) any |= av[i];
-    if (!any) {
-        for (int i = 0; i < total; ++i) q[i] = 128;
+    left[0] = a_corner ? corner : 0;
+    if (!(a_left || a_bl || a_top || a_tr || a_corner)) {
+        for (int i = 0; i < total; ++i) ref(i) = 128;
     } else {
-        if (!av[0]) {
+        if (!avail(0)) {
             for (int i = 1; i < total; ++i)
-                if (av[i]) {
-                    q[0] = q[i];
+                if (avail(i)) {
+                    ref(0) = ref(i);
                     break;
                 }
         }
         for (int i = 1; i < total; ++i)
-            if (!av[i]) q[i] = q[i - 1];
+            if (!avail(i)) ref(i) = ref(i - 1);
     }
-    // back to the left/top arrays
-    for (int k = 0; k < 2 * N; ++k) left[1 + k] = q[2 * N - 1 - k];
-    left[0] = q[2 * N];
-    top[0] = q[2 * N];
-    for (int k = 0; k < 2 * N; ++k) top[1 + k] = q[2 * N + 1 + k];
+    top[0] = left[0];
 }
 
 // Prediction of an NxN block (N = 4..32, 8-bit).  cidx 0 = luma (reference filtering,
@@ -742,47 +731,52 @@ MXHD void code_residual(CabacEnc& e, uint8_t* ctx, const int16_t* c, int log2n, 
             e.bin(ctx[C_SIG + (cidx ? 27 : 0) + sc], sig);
             if (sig) infer_dc = false;
         }
-        // levels: nonzero coefficients from n = 15 down to 0
-        int absv[16], neg[16], nsig = 0;
-        for (int n = 15; n >= 0; --n)
-            if (sb[n]) {
-                absv[nsig] = sb[n] < 0 ? -sb[n] : sb[n];
-                neg[nsig] = sb[n] < 0;
-                ++nsig;
-            }
+        // levels of the nonzero coefficients, n = 15 down to 0 (greater1 flags for the first 8)
+        int nsig = 0;
+        for (int n = 15; n >= 0; --n) nsig += sb[n] != 0;
         if (!nsig) continue;
         int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
         if (g1ctx_prev == 0) ++ctx_set;
-        int g1ctx = 1;
-        int g2_idx = -1;
-        const int ng1 = nsig < 8 ? nsig : 8;
-        for (int k = 0; k < ng1; ++k) {
-            const int g1 = absv[k] > 1;
+        int g1ctx = 1, g2_pos = -1, k = 0;
+        for (int n = 15; n >= 0 && k < 8; --n) {
+            const int v = sb[n];
+            if (!v) continue;
+            const int g1 = (v > 1 || v < -1) ? 1 : 0;
             e.bin(ctx[C_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + (g1ctx < 3 ? g1ctx : 3)], g1);
             if (g1) {
                 g1ctx = 0;
-                if (g2_idx < 0) g2_idx = k;
+                if (g2_pos < 0) g2_pos = n;
             } else if (g1ctx > 0) {
                 ++g1ctx;
             }
+            ++k;
         }
         g1ctx_prev = g1ctx;
-        if (g2_idx >= 0) e.bin(ctx[C_GT2 + (cidx ? 4 : 0) + ctx_set], absv[g2_idx] > 2);
-        for (int k = 0; k < nsig; ++k) e.bypass(neg[k]);
+        if (g2_pos >= 0) {
+            const int a = sb[g2_pos] < 0 ? -sb[g2_pos] : sb[g2_pos];
+            e.bin(ctx[C_GT2 + (cidx ? 4 : 0) + ctx_set], a > 2);
+        }
+        for (int n = 15; n >= 0; --n)
+            if (sb[n]) e.bypass(sb[n] < 0);
         int rice = 0;
-        for (int k = 0; k < nsig; ++k) {
+        k = 0;
+        for (int n = 15; n >= 0; --n) {
+            const int v = sb[n];
+            if (!v) continue;
+            const int a = v < 0 ? -v : v;
             int base, thr;
             if (k < 8) {
-                base = 1 + (absv[k] > 1 ? 1 : 0) + (k == g2_idx && absv[k] > 2 ? 1 : 0);
-                thr = (k == g2_idx) ? 3 : 2;
+                base = 1 + (a > 1 ? 1 : 0) + (n == g2_pos && a > 2 ? 1 : 0);
+                thr = (n == g2_pos) ? 3 : 2;
             } else {
                 base = 1;
                 thr = 1;
             }
             if (base == thr) {
-                code_remaining(e, (uint32_t)(absv[k] - base), rice);
-                if (absv[k] > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
+                code_remaining(e, (uint32_t)(a - base), rice);
+                if (a > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
             }
+            ++k;
         }
     }
 }

@@ -1,0 +1,215 @@
+// Host driver of the HIP HEVC encoder (kernel chain in hevc_kernels.hip).  Mirrors the
+// H.264 driver: per-frame slots (pinned frame state, zero-copy output), optional second
+// HIP stream for entropy coding so frame n's CABAC overlaps frame n+1's analysis.
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../common/hip_check.h"
+#include "h264_mb.h"
+#include "hevc_encoder.h"
+
+namespace mx {
+namespace hevc {
+
+void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
+    const int ncu = geom_.mb_w * geom_.mb_h;
+    const int ns = common_.num_slices();
+    HevcDeviceBuffers& b = sl.buf;
+    HIP_CHECK(hipMalloc(&b.fs, sizeof(HevcFrameState)));
+    HIP_CHECK(hipMalloc(&b.me.fs, sizeof(h264::FrameState)));
+    HIP_CHECK(hipMalloc(&b.me.mb, sizeof(h264::MbInfo) * ncu));
+    HIP_CHECK(hipMemsetAsync(b.me.mb, 0, sizeof(h264::MbInfo) * ncu, stream_));
+    HIP_CHECK(hipMalloc(&b.cu, sizeof(CuInfo) * ncu));
+    HIP_CHECK(hipMalloc(&b.coef, sizeof(int16_t) * kCoefPerCu * (size_t)ncu));
+    // per-slice CABAC output slot: 1 KiB per CTU (dense intra at QP 0 stays below)
+    b.slice_cap = (uint32_t)(((size_t)common_.slice_rows() * geom_.mb_w * 1024 + 15) & ~(size_t)15);
+    HIP_CHECK(hipMalloc(&b.slice_data, (size_t)b.slice_cap * ns));
+    HIP_CHECK(hipMalloc(&b.slice_len, sizeof(uint32_t) * ns));
+    HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
+    b.out_bytes = (size_t)ncu * 768;
+    HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc(&sl.me_fs_host, sizeof(h264::FrameState), hipHostMallocDefault));
+    std::memset(sl.me_fs_host, 0, sizeof(h264::FrameState));
+    HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
+    std::memset(sl.host_out, 0, kOutPayloadOffset);
+    HIP_CHECK(hipEventCreate(&sl.start));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreate(&sl.done));
+}
+
+void GpuHevcEncoder::free_slot(FrameSlot& sl) {
+    HevcDeviceBuffers& b = sl.buf;
+    for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
+                    (void*)b.slice_len, (void*)b.sse_part})
+        if (p) (void)hipFree(p);
+    if (sl.fs_host) (void)hipHostFree(sl.fs_host);
+    if (sl.me_fs_host) (void)hipHostFree(sl.me_fs_host);
+    if (sl.host_out) (void)hipHostFree(sl.host_out);
+    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.done})
+        if (e) (void)hipEventDestroy(e);
+}
+
+GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
+    : cfg_(cfg), common_(cfg), stream_(stream) {
+    if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
+        throw std::invalid_argument("pipeline_depth must be 1 or 2");
+    if (common_.slice_rows() > kMaxSliceRows) throw std::invalid_argument("hevc: too many CTU rows per slice");
+    depth_ = cfg.pipeline_depth;
+    geom_.width = cfg.width;
+    geom_.height = cfg.height;
+    geom_.mb_w = common_.ctb_w();
+    geom_.mb_h = common_.ctb_h();
+    geom_.coded_w = geom_.mb_w * kCtb;
+    geom_.coded_h = geom_.mb_h * kCtb;
+    geom_.pitch = (geom_.coded_w + 255) & ~255;
+    const int ncu = geom_.mb_w * geom_.mb_h;
+    if ((ncu + 3) / 4 > h264::kSsePartStride) throw std::invalid_argument("frame too large for the distortion partials");
+    const size_t ysz = (size_t)geom_.pitch * geom_.coded_h, uvsz = ysz / 2;
+    for (int i = 0; i < 2; ++i) {
+        HIP_CHECK(hipMalloc(&rec_y_[i], ysz));
+        HIP_CHECK(hipMalloc(&rec_uv_[i], uvsz));
+        HIP_CHECK(hipMemsetAsync(rec_y_[i], 16, ysz, stream_));
+        HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
+    }
+    hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
+    const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
+    for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
+    for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
+    if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+GpuHevcEncoder::~GpuHevcEncoder() {
+    (void)hipStreamSynchronize(stream_);
+    if (stream_e_) {
+        (void)hipStreamSynchronize(stream_e_);
+        (void)hipStreamDestroy(stream_e_);
+    }
+    for (int i = 0; i < 2; ++i) {
+        (void)hipFree(rec_y_[i]);
+        (void)hipFree(rec_uv_[i]);
+    }
+    for (int i = 0; i < 4; ++i) (void)hipFree(hp_[i]);
+    for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
+}
+
+bool GpuHevcEncoder::prepare(bool force_idr) {
+    if ((int)inflight_.size() >= depth_) throw std::logic_error("GpuHevcEncoder: collect() a frame first (pipeline full)");
+    const int s = (depth_ == 1) ? 0 : next_slot_;
+    next_slot_ = (next_slot_ + 1) % depth_;
+    prep_slot_ = s;
+    FrameSlot& sl = slots_[s];
+    h264::EncoderCommon& rc = common_.rc();
+    rc.begin_frame(force_idr || !have_ref_);
+    have_ref_ = true;
+    const bool idr = rc.cur_idr();
+    sl.idr = idr;
+    sl.qp = rc.cur_qp();
+    sl.poc = idr ? 0 : common_.poc();
+    const int ref = cur_;
+    cur_ ^= 1;
+    const size_t org = (size_t)h264::kHpelPad * hp_pitch_ + h264::kHpelPad;
+    HevcFrameState& f = *sl.fs_host;
+    f.ref_y = rec_y_[ref];
+    f.ref_uv = rec_uv_[ref];
+    f.rec_y = rec_y_[cur_];
+    f.rec_uv = rec_uv_[cur_];
+    f.hp_f = hp_[0] + org;
+    f.hp_pitch = hp_pitch_;
+    f.idr = idr ? 1 : 0;
+    f.qp = sl.qp;
+    f.slice_rows = common_.slice_rows();
+    f.num_slices = common_.num_slices();
+    f.aq = cfg_.aq;
+    f.chroma_qp_offset = cfg_.chroma_qp_offset;
+    f.n_sse_parts = idr ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
+    f.sse_part = sl.buf.sse_part;
+    h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
+    m.ref_y = rec_y_[ref];
+    m.ref_uv = rec_uv_[ref];
+    m.qp = sl.qp;
+    m.search_range = h264::me_range(cfg_.search_range);
+    m.subpel = cfg_.subpel;
+    m.hp_pitch = hp_pitch_;
+    m.hp_f = hp_[0] + org;
+    m.hp_h = hp_[1] + org;
+    m.hp_v = hp_[2] + org;
+    m.hp_j = hp_[3] + org;
+    m.sse_part = sl.buf.sse_part;
+    return idr;
+}
+
+void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(HevcFrameState), hipMemcpyHostToDevice, stream_));
+    if (idr) {
+        launch_hevc_intra(geom_, sl.buf, common_.slice_rows(), common_.num_slices(), src_y, src_uv, stream_);
+    } else {
+        HIP_CHECK(hipMemcpyAsync(sl.buf.me.fs, sl.me_fs_host, sizeof(h264::FrameState), hipMemcpyHostToDevice, stream_));
+        h264::launch_hpel(geom_, sl.buf.me, hp_, hp_pitch_, stream_);
+        h264::launch_me(geom_, sl.buf.me, src_y, stream_);
+        launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
+    }
+    hipStream_t es = stream_;
+    if (stream_e_) {
+        HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
+        HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+        es = stream_e_;
+    }
+    launch_hevc_entropy(geom_, sl.buf, common_.num_slices(), sl.host_out, es);
+    HIP_CHECK(hipGetLastError());
+}
+
+void GpuHevcEncoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
+
+void GpuHevcEncoder::record_done() {
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipEventRecord(sl.done, stream_e_ ? stream_e_ : stream_));
+    inflight_.push_back(prep_slot_);
+}
+
+void GpuHevcEncoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
+    const bool idr = prepare(force_idr);
+    record_start();
+    enqueue_body(idr, src_y, src_uv);
+    record_done();
+}
+
+const std::vector<uint8_t>& GpuHevcEncoder::collect() {
+    if (inflight_.empty()) throw std::logic_error("GpuHevcEncoder: nothing submitted");
+    const int s = inflight_.front();
+    inflight_.pop_front();
+    FrameSlot& sl = slots_[s];
+    HIP_CHECK(hipEventSynchronize(sl.done));
+    last_done_ = sl.done;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, sl.start, sl.done);
+    const HevcOutHeader hdr = *reinterpret_cast<const HevcOutHeader*>(sl.host_out);
+    h264::EncoderCommon& rc = common_.rc();
+    if (hdr.overflow) {
+        rc.end_frame(0, sl.idr);
+        have_ref_ = false;  // reference incomplete: the next frame must be IDR
+        throw std::runtime_error("hevc gpu encoder: output overflow");
+    }
+    const uint32_t* soff = reinterpret_cast<const uint32_t*>(sl.host_out + sizeof(HevcOutHeader));
+    const uint32_t* slen = soff + kMaxSlices;
+    const uint8_t* payload = sl.host_out + kOutPayloadOffset;
+    au_.clear();
+    au_.reserve(hdr.total_bytes + hdr.total_bytes / 64 + 64 * hdr.num_slices + 256);
+    if (sl.idr) common_.write_parameter_sets(au_);
+    for (uint32_t k = 0; k < hdr.num_slices; ++k)
+        common_.write_slice_nal(au_, (int)k, sl.idr, sl.poc, sl.qp, payload + soff[k], slen[k]);
+    stats_.frame_index = rc.frames();
+    stats_.idr = sl.idr;
+    stats_.qp = sl.qp;
+    stats_.bytes = (int)au_.size();
+    stats_.encode_ms = ms;
+    for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
+    rc.end_frame((int)au_.size(), sl.idr);
+    return au_;
+}
+
+}  // namespace hevc
+}  // namespace mx

@@ -100,7 +100,7 @@ struct HevcFrameState {
     int32_t num_slices;
     int32_t aq;
     int32_t chroma_qp_offset;
-    int32_t pad;
+    int32_t n_sse_parts;  // distortion partials written this frame (P: one per 4 CUs, I: one per CTU row)
     unsigned long long* sse_part;  // [3][kSsePartStride] per-workgroup distortion partials
 };
 
@@ -114,6 +114,7 @@ struct HevcOutHeader {
 };
 static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
+constexpr int kMaxSliceRows = 4;  // CTU rows per slice the intra wavefront kernel supports
 constexpr size_t kOutPayloadOffset = sizeof(HevcOutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
 
 struct HevcDeviceBuffers {
@@ -135,29 +136,31 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int num_slices, uint8_t* host_out,
                          hipStream_t s);
 
-class GpuHevcEncoder {
+class GpuHevcEncoder final : public VideoEncoder {
    public:
+    const char* codec() const override { return "hevc"; }
+    h264::EncoderCommon& rc() override { return common_.rc(); }
     static constexpr int kMaxInFlight = 2;
     GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream);
     ~GpuHevcEncoder();
     GpuHevcEncoder(const GpuHevcEncoder&) = delete;
     GpuHevcEncoder& operator=(const GpuHevcEncoder&) = delete;
 
-    const Geometry& geometry() const { return geom_; }
-    int pitch() const { return geom_.pitch; }
-    int depth() const { return depth_; }
-    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false);
-    const std::vector<uint8_t>& collect();
-    const FrameStats& last_stats() const { return stats_; }
+    const Geometry& geometry() const override { return geom_; }
+    int pitch() const override { return geom_.pitch; }
+    int depth() const override { return depth_; }
+    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false) override;
+    const std::vector<uint8_t>& collect() override;
+    const FrameStats& last_stats() const override { return stats_; }
     HevcCommon& common() { return common_; }
-    const uint8_t* recon_y() const { return rec_y_[cur_]; }
-    const uint8_t* recon_uv() const { return rec_uv_[cur_]; }
-    hipEvent_t done_event() const { return last_done_; }
+    const uint8_t* recon_y() const override { return rec_y_[cur_]; }
+    const uint8_t* recon_uv() const override { return rec_uv_[cur_]; }
+    hipEvent_t done_event() const override { return last_done_; }
     // split form (same as GpuH264Encoder) for the session's graph path
-    bool prepare(bool force_idr);
-    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
-    void record_start();
-    void record_done();
+    bool prepare(bool force_idr) override;
+    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
+    void record_start() override;
+    void record_done() override;
 
    private:
     struct FrameSlot {

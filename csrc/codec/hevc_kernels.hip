@@ -1,0 +1,622 @@
+// HIP/CDNA4 kernels of the HEVC encoder (BASELINE.json "4K60 HEVC").
+//
+// Decomposition (gfx950: 256 CUs, wave64):
+//  * k_hevc_inter  one wave per 16x16 CU (4 per workgroup) after the shared H.264 motion
+//                  search (k_hpel + k_me_full): 8-tap luma / 4-tap chroma motion
+//                  compensation, the 16x16 / 8x8 core transforms as LDS-staged
+//                  matrix products (4 luma + 2 chroma outputs per lane per stage),
+//                  quantisation, normative inverse transform and reconstruction, coded
+//                  sub-block / last-position summaries by wave reductions, and the
+//                  skip / merge / AMVP decision from the neighbours' motion.
+//  * k_hevc_intra  one workgroup per slice, one wave per CTU row; the rows of a slice run
+//                  as a wavefront (row r two CTUs behind row r-1) with the left column
+//                  and the bottom rows of the row above exchanged through LDS.
+//  * k_hevc_cabac  one wave per slice; lane 0 runs the shared CABAC slice coder
+//                  (hevc_core.h code_slice) with its 142 context states in LDS.
+//  * k_hevc_pack   one workgroup per slice copies the slice bytes (16-byte stores) into
+//                  pinned host memory at 16-byte aligned offsets; workgroup 0 writes the
+//                  header (lengths, overflow, distortion totals).
+#include <hip/hip_runtime.h>
+
+#include "h264_core.h"
+#include "h264_gpu.h"
+#include "h264_mb.h"
+#include "hevc_core.h"
+#include "hevc_encoder.h"
+
+namespace mx {
+namespace hevc {
+
+namespace {
+
+__device__ __forceinline__ int wsum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int wmax(int v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const int t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wor(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Transform matrices in LDS (filled once per workgroup).
+struct Mats {
+    int16_t t16[256];
+    int16_t t8[64];
+};
+__device__ __forceinline__ void fill_mats(Mats& m) {
+    for (int i = threadIdx.x; i < 256 + 64; i += blockDim.x) {
+        if (i < 256)
+            m.t16[i] = (int16_t)dct_coef(4, i >> 4, i & 15);
+        else
+            m.t8[i - 256] = (int16_t)dct_coef(3, (i - 256) >> 3, (i - 256) & 7);
+    }
+}
+
+// Per-wave TU scratch: residual / prediction / two int32 stage buffers for 256 luma +
+// 2 x 64 chroma samples.
+struct TuBuf {
+    int16_t res[384];
+    uint8_t pred[384];
+    int32_t a[384];
+    int32_t b[384];
+};
+
+// One wave transforms, quantises and reconstructs its CU's three TUs.  Lane mapping per
+// stage: luma outputs lane*4 .. lane*4+3, chroma outputs (lane&31)*2 .. +1 of component
+// lane>>5.  __syncthreads() separate the stages, so every wave of the workgroup calls this
+// the same number of times (idle waves with valid == false).
+struct TuResult {
+    int last[3];
+    uint32_t csbf[3];
+    int nz[3];
+    int sse[3];
+};
+
+__device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool intra, bool valid,
+                                             int16_t* coef, uint8_t* rec_y, int pitch_y, uint8_t* rec_uv, int x0,
+                                             int y0, int disp_w, int disp_h) {
+    const int lane = threadIdx.x & 63;
+    const int comp = lane >> 5, cl = lane & 31;
+    // ---- forward stage 1 (rows): a[y][k] = sum_n T[k][n] res[y][n]
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = lane * 4 + j, y = idx >> 4, k = idx & 15;
+            int s = 0;
+#pragma unroll
+            for (int n = 0; n < 16; ++n) s += M.t16[k * 16 + n] * t.res[y * 16 + n];
+            t.a[idx] = (s + 4) >> 3;
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = cl * 2 + j, y = idx >> 3, k = idx & 7;
+            const int16_t* r = t.res + 256 + comp * 64;
+            int s = 0;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) s += M.t8[k * 8 + n] * r[y * 8 + n];
+            t.a[256 + comp * 64 + idx] = (s + 2) >> 2;
+        }
+    }
+    __syncthreads();
+    TuResult out;
+    int lastl = -1, lastc = -1, nzl = 0, nzc = 0;
+    uint32_t csl = 0, csc = 0;
+    // ---- forward stage 2 (columns) + quantisation + dequantisation into b
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = lane * 4 + j, k2 = idx >> 4, k = idx & 15;
+            int s = 0;
+#pragma unroll
+            for (int y = 0; y < 16; ++y) s += M.t16[k2 * 16 + y] * t.a[y * 16 + k];
+            const int c = (s + 512) >> 10;
+            const int l = quant_coef(c, qp, 4, intra);
+            const int si = scan_index(4, k, k2);
+            coef[si] = (int16_t)l;
+            t.b[idx] = dequant_coef(l, qp, 4);
+            if (l) {
+                ++nzl;
+                lastl = si > lastl ? si : lastl;
+                csl |= 1u << (si >> 4);
+            }
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = cl * 2 + j, k2 = idx >> 3, k = idx & 7;
+            const int32_t* a = t.a + 256 + comp * 64;
+            int s = 0;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) s += M.t8[k2 * 8 + y] * a[y * 8 + k];
+            const int c = (s + 256) >> 9;
+            const int l = quant_coef(c, qpc, 3, intra);
+            const int si = scan_index(3, k, k2);
+            coef[256 + comp * 64 + si] = (int16_t)l;
+            t.b[256 + comp * 64 + idx] = dequant_coef(l, qpc, 3);
+            if (l) {
+                ++nzc;
+                lastc = si > lastc ? si : lastc;
+                csc |= 1u << (si >> 4);
+            }
+        }
+    }
+    out.nz[0] = wsum(nzl);
+    out.last[0] = wmax(lastl);
+    out.csbf[0] = wor(csl);
+    {
+        const int n_cb = wsum(comp == 0 ? nzc : 0), n_cr = wsum(comp == 1 ? nzc : 0);
+        out.nz[1] = n_cb;
+        out.nz[2] = n_cr;
+        out.last[1] = wmax(comp == 0 ? lastc : -1);
+        out.last[2] = wmax(comp == 1 ? lastc : -1);
+        out.csbf[1] = wor(comp == 0 ? csc : 0u);
+        out.csbf[2] = wor(comp == 1 ? csc : 0u);
+    }
+    __syncthreads();
+    // ---- inverse stage 1 (columns): a[y][x] = clip16((sum_k T[k][y] b[k][x] + 64) >> 7)
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = lane * 4 + j, y = idx >> 4, x = idx & 15;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) s += M.t16[k * 16 + y] * t.b[k * 16 + x];
+            t.a[idx] = clip16((s + 64) >> 7);
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = cl * 2 + j, y = idx >> 3, x = idx & 7;
+            const int32_t* b = t.b + 256 + comp * 64;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + y] * b[k * 8 + x];
+            t.a[256 + comp * 64 + idx] = clip16((s + 64) >> 7);
+        }
+    }
+    __syncthreads();
+    // ---- inverse stage 2 (rows) + reconstruction
+    int sy = 0, sc = 0;
+    if (valid) {
+        const int y = lane >> 2, xb = (lane & 3) * 4;
+        uint32_t packed = 0;
+        for (int j = 0; j < 4; ++j) {
+            const int x = xb + j;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) s += M.t16[k * 16 + x] * t.a[y * 16 + k];
+            const int r = out.nz[0] ? (s + 2048) >> 12 : 0;
+            const int p = t.pred[y * 16 + x];
+            const int v = clip255(p + r);
+            const int e = p + t.res[y * 16 + x] - v;
+            sy += (x0 + x < disp_w && y0 + y < disp_h) ? e * e : 0;
+            packed |= (uint32_t)v << (8 * j);
+            t.pred[y * 16 + x] = (uint8_t)v;  // reconstruction stays readable in LDS
+        }
+        *reinterpret_cast<uint32_t*>(rec_y + (size_t)(y0 + y) * pitch_y + x0 + xb) = packed;
+        const int nzcomp = comp ? out.nz[2] : out.nz[1];
+        for (int j = 0; j < 2; ++j) {
+            const int idx = cl * 2 + j, yy = idx >> 3, x = idx & 7;
+            const int32_t* a = t.a + 256 + comp * 64;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + x] * a[yy * 8 + k];
+            const int r = nzcomp ? (s + 2048) >> 12 : 0;
+            const int o = 256 + comp * 64 + idx;
+            const int p = t.pred[o];
+            const int v = clip255(p + r);
+            const int e = p + t.res[o] - v;
+            t.pred[o] = (uint8_t)v;
+            const int xc = x0 / 2 + x, yc = y0 / 2 + yy;
+            sc += (2 * xc < disp_w && 2 * yc < disp_h) ? e * e : 0;
+            rec_uv[(size_t)yc * pitch_y + 2 * xc + comp] = (uint8_t)v;
+        }
+    }
+    out.sse[0] = wsum(sy);
+    out.sse[1] = wsum(comp == 0 ? sc : 0);
+    out.sse[2] = wsum(comp == 1 ? sc : 0);
+    return out;
+}
+
+__device__ __forceinline__ void fill_cu(CuInfo& c, const TuResult& r) {
+    c.cbf = (uint8_t)((r.nz[0] ? 1 : 0) | (r.nz[1] ? 2 : 0) | (r.nz[2] ? 4 : 0));
+    c.last[0] = (uint8_t)(r.last[0] < 0 ? 0 : r.last[0]);
+    c.last[1] = (uint8_t)(r.last[1] < 0 ? 0 : r.last[1]);
+    c.last[2] = (uint8_t)(r.last[2] < 0 ? 0 : r.last[2]);
+    c.csbf_y = (uint16_t)r.csbf[0];
+    c.csbf_c[0] = (uint8_t)r.csbf[1];
+    c.csbf_c[1] = (uint8_t)r.csbf[2];
+}
+
+// ------------------------------------------------------------------ inter
+__global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                     const h264::MbInfo* __restrict__ mbs,
+                                                     const uint8_t* __restrict__ src_y,
+                                                     const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
+                                                     int16_t* __restrict__ coef) {
+    __shared__ Mats M;
+    __shared__ TuBuf tb[4];
+    __shared__ unsigned long long part[3][4];
+    fill_mats(M);
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ncu = g.mb_w * g.mb_h;
+    const int i = blockIdx.x * 4 + wave;
+    const bool valid = i < ncu;
+    const int x = valid ? i % g.mb_w : 0, y = valid ? i / g.mb_w : 0;
+    const int x0 = x * 16, y0 = y * 16;
+    TuBuf& t = tb[wave];
+    int mvx = 0, mvy = 0, lsad = 0;
+    if (valid) {
+        mvx = mbs[i].mvx;
+        mvy = mbs[i].mvy;
+        // luma: 4 samples per lane from the edge-padded reference (|mv| stays inside the pad)
+        const int r = lane >> 2, cb = (lane & 3) * 4;
+        const uint8_t* F = fs->hp_f;
+        const int P = fs->hp_pitch;
+        const int fx = mvx & 3, fy = mvy & 3;
+        const int xi = x0 + cb + (mvx >> 2), yi = y0 + r + (mvy >> 2);
+        for (int j = 0; j < 4; ++j) {
+            int v;
+            if (!fx && !fy) {
+                v = F[yi * P + xi + j] << 6;
+            } else if (!fy) {
+                v = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v += kLumaTap[fx][k] * F[yi * P + xi + j + k - 3];
+            } else if (!fx) {
+                v = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v += kLumaTap[fy][k] * F[(yi + k - 3) * P + xi + j];
+            } else {
+                int s = 0;
+#pragma unroll
+                for (int n = 0; n < 8; ++n) {
+                    int h = 0;
+                    const uint8_t* row = F + (yi + n - 3) * P + xi + j - 3;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) h += kLumaTap[fx][k] * row[k];
+                    s += kLumaTap[fy][n] * h;
+                }
+                v = s >> 6;
+            }
+            const int p = clip255((v + 32) >> 6);
+            const int d = (int)src_y[(size_t)(y0 + r) * g.pitch + x0 + cb + j] - p;
+            t.pred[r * 16 + cb + j] = (uint8_t)p;
+            t.res[r * 16 + cb + j] = (int16_t)d;
+            lsad += d < 0 ? -d : d;
+        }
+        // chroma: one sample per lane and component
+        const int rc = lane >> 3, cc = lane & 7;
+        const int xc = x0 / 2 + cc, yc = y0 / 2 + rc;
+        for (int comp = 0; comp < 2; ++comp) {
+            const int p = chroma_mc(fs->ref_uv, g.pitch, g.coded_w / 2, g.coded_h / 2, comp, xc, yc, mvx, mvy);
+            const int s = src_uv[(size_t)yc * g.pitch + 2 * xc + comp];
+            t.pred[256 + comp * 64 + rc * 8 + cc] = (uint8_t)p;
+            t.res[256 + comp * 64 + rc * 8 + cc] = (int16_t)(s - p);
+        }
+    }
+    const int qp = h264::aq_mb_qp(fs->qp, (uint32_t)wsum(lsad), fs->aq);  // wave-uniform
+    const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
+    __syncthreads();
+    int16_t* co = coef + (size_t)(valid ? i : 0) * kCoefPerCu;
+    const TuResult r = code_tus(t, M, qp, qpc, false, valid, co, fs->rec_y, g.pitch, fs->rec_uv, x0, y0, g.width,
+                                g.height);
+    if (lane == 0) {
+        part[0][wave] = valid ? (unsigned long long)r.sse[0] : 0ull;
+        part[1][wave] = valid ? (unsigned long long)r.sse[1] : 0ull;
+        part[2][wave] = valid ? (unsigned long long)r.sse[2] : 0ull;
+    }
+    if (valid && lane == 0) {
+        CuInfo c;
+        c.type = kCuAmvp;
+        c.intra_mode = 1;
+        c.qp = (uint8_t)qp;
+        c.mvx = (int16_t)mvx;
+        c.mvy = (int16_t)mvy;
+        c.mvdx = c.mvdy = 0;
+        c.mvp_idx = 0;
+        fill_cu(c, r);
+        MvCand a1, b1, b0, b2;
+        constexpr int kStride = sizeof(h264::MbInfo) / sizeof(int16_t);
+        inter_neighbours(&mbs[0].mvx, kStride, x, y, g.mb_w, fs->slice_rows, &a1, &b1, &b0, &b2);
+        decide_inter(c, a1, b1, b0, b2);
+        cus[i] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int c = threadIdx.x;
+        fs->sse_part[c * h264::kSsePartStride + blockIdx.x] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
+    }
+}
+
+// ------------------------------------------------------------------ intra
+// Per-wave reference state of the CU being predicted.
+struct IntraRefs {
+    uint8_t lpx[16], tpx[16], trx[16];
+    uint8_t lc[2][8], tc[2][8], trc[2][8];
+    int corner, corner_c[2];
+    int L[33], T[33], LF[33], TF[33];  // luma refs (unfiltered / planar-filtered)
+    int Lc[2][17], Tc[2][17];
+    int dc, dcc[2];
+};
+
+// Sample (x, y) of the prediction for one of the candidate modes (planar, DC, 26, 10);
+// equals intra_predict() for those modes.
+__device__ __forceinline__ int pred_sample(int mode, int log2n, bool luma, const int* L, const int* T, const int* LF,
+                                           const int* TF, int dc, int x, int y) {
+    const int N = 1 << log2n;
+    if (mode == 0)
+        return ((N - 1 - x) * LF[1 + y] + (x + 1) * TF[1 + N] + (N - 1 - y) * TF[1 + x] + (y + 1) * LF[1 + N] + N) >>
+               (log2n + 1);
+    if (mode == 1) {
+        if (luma && N < 32) {
+            if (x == 0 && y == 0) return (L[1] + 2 * dc + T[1] + 2) >> 2;
+            if (y == 0) return (T[1 + x] + 3 * dc + 2) >> 2;
+            if (x == 0) return (L[1 + y] + 3 * dc + 2) >> 2;
+        }
+        return dc;
+    }
+    if (mode == 26) return (luma && x == 0) ? clip255(T[1] + ((L[1 + y] - L[0]) >> 1)) : T[1 + x];
+    return (luma && y == 0) ? clip255(L[1] + ((T[1 + x] - T[0]) >> 1)) : L[1 + y];  // mode 10
+}
+
+__global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                      const uint8_t* __restrict__ src_y,
+                                                      const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
+                                                      int16_t* __restrict__ coef) {
+    // dynamic LDS: per row of the slice, the bottom luma row and bottom chroma (NV12) row
+    extern __shared__ uint8_t bottom[];
+    __shared__ Mats M;
+    __shared__ TuBuf tb[kMaxSliceRows];
+    __shared__ IntraRefs rf[kMaxSliceRows];
+    __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
+    __shared__ int cost[kMaxSliceRows][4];
+    __shared__ int prev_mode[kMaxSliceRows];
+    fill_mats(M);
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sr = fs->slice_rows;
+    const int y = blockIdx.x * sr + wave;  // CTU row of this wave
+    const bool row_ok = wave < sr && y < g.mb_h;
+    const int qp = fs->qp;
+    const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
+    const int lambda = h264::lambda_sad(qp);
+    const int cw = g.coded_w;
+    uint8_t* bot_y = bottom + (size_t)wave * 2 * cw;
+    uint8_t* bot_c = bot_y + cw;
+    const uint8_t* up_y = bottom + (size_t)(wave - 1) * 2 * cw;  // row above (same slice), valid if wave > 0
+    const uint8_t* up_c = up_y + cw;
+    TuBuf& t = tb[wave];
+    IntraRefs& R = rf[wave];
+    unsigned long long acc[3] = {0, 0, 0};
+    const int steps = g.mb_w + 2 * (sr - 1);
+    for (int step = 0; step < steps; ++step) {
+        const int x = step - 2 * wave;
+        const bool valid = row_ok && x >= 0 && x < g.mb_w;
+        const int x0 = x * 16, y0 = y * 16;
+        const bool al = x > 0, at = wave > 0, atr = at && x + 1 < g.mb_w, ac = at && x > 0;
+        // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
+        if (valid) {
+            if (lane < 16) {
+                R.lpx[lane] = al ? leftc[wave][lane] : 0;
+                R.tpx[lane] = at ? up_y[x0 + lane] : 0;
+                R.trx[lane] = atr ? up_y[x0 + 16 + lane] : 0;
+            } else if (lane < 32) {
+                const int k = lane - 16, comp = k >> 3, q = k & 7;
+                R.lc[comp][q] = al ? leftc[wave][16 + comp * 8 + q] : 0;
+                R.tc[comp][q] = at ? up_c[x0 + 2 * q + comp] : 0;
+                R.trc[comp][q] = atr ? up_c[x0 + 16 + 2 * q + comp] : 0;
+            } else if (lane == 32) {
+                R.corner = ac ? up_y[x0 - 1] : 0;
+                R.corner_c[0] = ac ? up_c[x0 - 2] : 0;
+                R.corner_c[1] = ac ? up_c[x0 - 1] : 0;
+            }
+        }
+        __syncthreads();
+        // ---- reference substitution + planar filter (lane 0 luma, lanes 1/2 chroma)
+        if (valid && lane < 3) {
+            if (lane == 0) {
+                intra_refs(16, al, false, at, atr, ac, R.lpx, R.lpx, R.tpx, R.trx, R.corner, R.L, R.T);
+                R.LF[0] = R.TF[0] = (R.L[1] + 2 * R.L[0] + R.T[1] + 2) >> 2;
+                for (int k = 1; k < 32; ++k) {
+                    R.LF[k] = (R.L[k + 1] + 2 * R.L[k] + R.L[k - 1] + 2) >> 2;
+                    R.TF[k] = (R.T[k + 1] + 2 * R.T[k] + R.T[k - 1] + 2) >> 2;
+                }
+                R.LF[32] = R.L[32];
+                R.TF[32] = R.T[32];
+                int s = 16;
+                for (int k = 1; k <= 16; ++k) s += R.L[k] + R.T[k];
+                R.dc = s >> 5;
+            } else {
+                const int comp = lane - 1;
+                intra_refs(8, al, false, at, atr, ac, R.lc[comp], R.lc[comp], R.tc[comp], R.trc[comp],
+                           R.corner_c[comp], R.Lc[comp], R.Tc[comp]);
+                int s = 8;
+                for (int k = 1; k <= 8; ++k) s += R.Lc[comp][k] + R.Tc[comp][k];
+                R.dcc[comp] = s >> 4;
+            }
+        }
+        __syncthreads();
+        // ---- mode decision: SAD of each candidate, 4 samples per lane
+        int mode = 1;
+        if (valid) {
+            const int cand_a = al ? prev_mode[wave] : 1;
+            const int r = lane >> 2, cb = (lane & 3) * 4;
+            for (int m = 0; m < kNumIntraCands; ++m) {
+                const int md = kIntraCands[m];
+                int sad = 0;
+                for (int j = 0; j < 4; ++j) {
+                    const int p = pred_sample(md, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
+                    const int d = (int)src_y[(size_t)(y0 + r) * g.pitch + x0 + cb + j] - p;
+                    sad += d < 0 ? -d : d;
+                }
+                sad = wsum(sad);
+                if (lane == 0) cost[wave][m] = sad + lambda * intra_mode_bits(md, cand_a);
+            }
+        }
+        __syncthreads();
+        if (valid) {
+            int bm = 0;
+            for (int m = 1; m < kNumIntraCands; ++m)
+                if (cost[wave][m] < cost[wave][bm]) bm = m;
+            mode = kIntraCands[bm];
+            const int r = lane >> 2, cb = (lane & 3) * 4;
+            for (int j = 0; j < 4; ++j) {
+                const int p = pred_sample(mode, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
+                t.pred[r * 16 + cb + j] = (uint8_t)p;
+                t.res[r * 16 + cb + j] = (int16_t)((int)src_y[(size_t)(y0 + r) * g.pitch + x0 + cb + j] - p);
+            }
+            const int rc = lane >> 3, cc = lane & 7;
+            for (int comp = 0; comp < 2; ++comp) {
+                const int p = pred_sample(mode, 3, false, R.Lc[comp], R.Tc[comp], R.Lc[comp], R.Tc[comp], R.dcc[comp],
+                                          cc, rc);
+                t.pred[256 + comp * 64 + rc * 8 + cc] = (uint8_t)p;
+                t.res[256 + comp * 64 + rc * 8 + cc] =
+                    (int16_t)((int)src_uv[(size_t)(y0 / 2 + rc) * g.pitch + x0 + 2 * cc + comp] - p);
+            }
+        }
+        __syncthreads();
+        const int i = valid ? y * g.mb_w + x : 0;
+        const TuResult res = code_tus(t, M, qp, qpc, true, valid, coef + (size_t)i * kCoefPerCu, fs->rec_y, g.pitch,
+                                      fs->rec_uv, x0, y0, g.width, g.height);
+        if (valid) {
+            acc[0] += (unsigned)res.sse[0];
+            acc[1] += (unsigned)res.sse[1];
+            acc[2] += (unsigned)res.sse[2];
+            if (lane == 0) {
+                CuInfo c;
+                c.type = kCuIntra;
+                c.intra_mode = (uint8_t)mode;
+                c.qp = (uint8_t)qp;
+                c.mvx = c.mvy = c.mvdx = c.mvdy = 0;
+                c.mvp_idx = 0;
+                fill_cu(c, res);
+                cus[i] = c;
+                prev_mode[wave] = mode;
+            }
+        }
+        __syncthreads();
+        if (valid) {
+            // reconstruction edges (kept in t.pred by code_tus): right column -> left
+            // neighbour of this wave's next CU, bottom rows -> the wave of the row below
+            if (lane < 16) {
+                leftc[wave][lane] = t.pred[lane * 16 + 15];
+                bot_y[x0 + lane] = t.pred[15 * 16 + lane];
+                bot_c[x0 + lane] = t.pred[256 + (lane & 1) * 64 + 7 * 8 + (lane >> 1)];
+            } else if (lane < 32) {
+                const int k = lane - 16, comp = k >> 3, q = k & 7;
+                leftc[wave][16 + comp * 8 + q] = t.pred[256 + comp * 64 + q * 8 + 7];
+            }
+        }
+        __syncthreads();
+    }
+    if (row_ok && lane < 3)  // wave sums (identical in every lane)
+        fs->sse_part[lane * h264::kSsePartStride + y] = lane == 0 ? acc[0] : (lane == 1 ? acc[1] : acc[2]);
+}
+
+// ------------------------------------------------------------------ CABAC
+__global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                    const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
+                                                    uint8_t* __restrict__ slice_data, uint32_t slice_cap,
+                                                    uint32_t* __restrict__ slice_len) {
+    __shared__ uint8_t ctx[C_NUM];
+    const int s = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    const int sr = fs->slice_rows;
+    const int rows = min(sr, g.mb_h - s * sr);
+    const int first = s * sr * g.mb_w, count = rows * g.mb_w;
+    const uint32_t n = code_slice(slice_data + (size_t)s * slice_cap, slice_cap, fs->idr != 0, fs->qp, cus, coef, first,
+                                  count, g.mb_w, ctx);
+    slice_len[s] = n;
+}
+
+// ------------------------------------------------------------------ pack
+__global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restrict__ fs, int num_slices,
+                                                    const uint8_t* __restrict__ slice_data,
+                                                    uint32_t slice_cap, const uint32_t* __restrict__ slice_len,
+                                                    uint8_t* __restrict__ host_out, size_t out_bytes) {
+    __shared__ uint32_t red[256];
+    __shared__ unsigned long long red64[3][256];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    // offset of this slice: sum of the 16-byte rounded lengths before it
+    uint32_t part = 0;
+    for (int k = tid; k < s; k += 256) part += (min(slice_len[k], slice_cap) + 15) & ~15u;
+    red[tid] = part;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    const uint32_t off = red[0];
+    const uint32_t len = slice_len[s];
+    const bool fits = len <= slice_cap && (size_t)off + ((len + 15) & ~15u) <= out_bytes;
+    if (fits) {
+        const uint4* src = reinterpret_cast<const uint4*>(slice_data + (size_t)s * slice_cap);
+        uint4* dst = reinterpret_cast<uint4*>(host_out + kOutPayloadOffset + off);
+        for (uint32_t k = tid; k < (len + 15) / 16; k += 256) dst[k] = src[k];
+    }
+    if (tid == 0) {
+        uint32_t* offs = reinterpret_cast<uint32_t*>(host_out + sizeof(HevcOutHeader));
+        offs[s] = off;
+        offs[kMaxSlices + s] = len;
+    }
+    if (s != 0) return;
+    // header: totals, overflow, distortion
+    uint32_t tot = 0, ovf = 0;
+    for (int k = tid; k < num_slices; k += 256) {
+        tot += (min(slice_len[k], slice_cap) + 15) & ~15u;
+        ovf |= slice_len[k] > slice_cap ? 1u : 0u;
+    }
+    unsigned long long e[3] = {0, 0, 0};
+    const int num_sse_parts = fs->n_sse_parts;
+    for (int k = tid; k < num_sse_parts; k += 256)
+        for (int c = 0; c < 3; ++c) e[c] += fs->sse_part[c * h264::kSsePartStride + k];
+    __syncthreads();
+    red[tid] = tot | (ovf << 31);
+    for (int c = 0; c < 3; ++c) red64[c][tid] = e[c];
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t T = 0, O = 0;
+        unsigned long long E[3] = {0, 0, 0};
+        for (int k = 0; k < 256; ++k) {
+            T += red[k] & 0x7fffffffu;
+            O |= red[k] >> 31;
+            for (int c = 0; c < 3; ++c) E[c] += red64[c][k];
+        }
+        HevcOutHeader h;
+        h.total_bytes = T;
+        h.num_slices = (uint32_t)num_slices;
+        h.overflow = (O || T > out_bytes) ? 1u : 0u;
+        h.pad = 0;
+        for (int c = 0; c < 3; ++c) h.sse[c] = E[c];
+        h.pad2 = 0;
+        *reinterpret_cast<HevcOutHeader*>(host_out) = h;
+    }
+}
+
+}  // namespace
+
+void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                       hipStream_t s) {
+    const int ncu = g.mb_w * g.mb_h;
+    hipLaunchKernelGGL(k_hevc_inter, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, b.me.mb, src_y, src_uv, b.cu,
+                       b.coef);
+}
+
+void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
+                       const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
+    const size_t lds = (size_t)slice_rows * 2 * g.coded_w;
+    hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows), lds, s, g, b.fs, src_y, src_uv, b.cu,
+                       b.coef);
+}
+
+void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int num_slices, uint8_t* host_out,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_hevc_cabac, dim3(num_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
+                       b.slice_cap, b.slice_len);
+    hipLaunchKernelGGL(k_hevc_pack, dim3(num_slices), dim3(256), 0, s, b.fs, num_slices, b.slice_data,
+                       b.slice_cap, b.slice_len, host_out, b.out_bytes);
+}
+
+}  // namespace hevc
+}  // namespace mx

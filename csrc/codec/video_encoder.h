@@ -1,0 +1,39 @@
+// Codec-independent interface of the GPU encoders the streaming Session drives
+// (GpuH264Encoder, GpuHevcEncoder).  Selected by SessionConfig::codec, the equivalent of
+// the reference's WEBRTC_ENCODER element choice (reference Dockerfile:210).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "h264_gpu.h"
+
+namespace mx {
+namespace h264 {
+class EncoderCommon;
+struct FrameStats;
+}  // namespace h264
+
+class VideoEncoder {
+   public:
+    virtual ~VideoEncoder() = default;
+    virtual const char* codec() const = 0;  // "h264" / "hevc"
+    virtual const h264::Geometry& geometry() const = 0;
+    virtual int pitch() const = 0;
+    virtual int depth() const = 0;
+    virtual void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) = 0;
+    virtual const std::vector<uint8_t>& collect() = 0;
+    virtual const h264::FrameStats& last_stats() const = 0;
+    virtual h264::EncoderCommon& rc() = 0;  // rate control / IDR requests
+    virtual const uint8_t* recon_y() const = 0;
+    virtual const uint8_t* recon_uv() const = 0;
+    virtual hipEvent_t done_event() const = 0;
+    // split form for hipGraph capture (pipeline depth 1)
+    virtual bool prepare(bool force_idr) = 0;
+    virtual void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) = 0;
+    virtual void record_start() = 0;
+    virtual void record_done() = 0;
+};
+
+}  // namespace mx

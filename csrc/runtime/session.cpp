@@ -7,6 +7,7 @@
 
 #include "../common/hip_check.h"
 #include "../common/trace.h"
+#include "../codec/hevc_encoder.h"
 
 namespace mx {
 
@@ -74,7 +75,12 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     cfg_.enc.fps = cfg_.fps;
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     pool_ = std::make_unique<FramePool>(cfg_.width, cfg_.height, cfg_.pool_slots);
-    enc_ = std::make_unique<h264::GpuH264Encoder>(cfg_.enc, stream_);
+    if (cfg_.codec == "h264" || cfg_.codec == "avc")
+        enc_ = std::make_unique<h264::GpuH264Encoder>(cfg_.enc, stream_);
+    else if (cfg_.codec == "hevc" || cfg_.codec == "h265")
+        enc_ = std::make_unique<hevc::GpuHevcEncoder>(cfg_.enc, stream_);
+    else
+        throw std::invalid_argument("Session: unknown codec '" + cfg_.codec + "' (h264 | hevc)");
     const h264::Geometry& g = enc_->geometry();
     HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
     HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));
@@ -256,7 +262,7 @@ FrameResult Session::collect() {
     float ms = 0;
     hipEventElapsedTime(&ms, ev_start_[fl.k], enc_->done_event());
     r.gpu_ms = ms;  // render/upload start -> bitstream written
-    const double ny = (double)enc_->common().config().width * enc_->common().config().height, nc = ny / 4;
+    const double ny = (double)enc_->rc().config().width * enc_->rc().config().height, nc = ny / 4;
     auto psnr = [](uint64_t sse, double n) { return sse == 0 ? 99.0 : std::min(99.0, 10.0 * std::log10(65025.0 * n / (double)sse)); };
     r.psnr_y = psnr(st.sse[0], ny);
     r.psnr_u = psnr(st.sse[1], nc);

@@ -15,6 +15,8 @@
 #include <vector>
 
 #include "../codec/h264_encoder.h"
+#include "../codec/video_encoder.h"
+#include <string>
 #include "../kernels/pixel.h"
 
 namespace mx {
@@ -56,6 +58,7 @@ struct SessionConfig {
     int use_graph = 0;      // replay the per-frame chain as a hipGraph (measured slower than eager
                             // launches on ROCm 7.2 for this chain: profiles/r01_graph)
     int fake_clock = 0;     // barcode timestamp = frame_id * 1e6 / fps (deterministic streams for tests)
+    std::string codec = "h264";  // "h264" (mxh264enc) or "hevc" / "h265" (mxh265enc)
     h264::EncoderConfig enc;  // width/height overwritten from out size
 };
 
@@ -93,11 +96,11 @@ class Session {
         cursor_x_ = x;
         cursor_y_ = y;
     }
-    void request_idr() { enc_->common().request_idr(); }
-    void set_bitrate(int kbps) { enc_->common().set_bitrate(kbps); }
+    void request_idr() { enc_->rc().request_idr(); }
+    void set_bitrate(int kbps) { enc_->rc().set_bitrate(kbps); }
     const SessionConfig& config() const { return cfg_; }
     hipStream_t stream() const { return stream_; }
-    h264::GpuH264Encoder& encoder() { return *enc_; }
+    VideoEncoder& encoder() { return *enc_; }
     FramePool& pool() { return *pool_; }
     // Device pointers of the NV12 frame fed to the encoder (tests / wall composite).
     const uint8_t* nv12_y() const { return nv12_y_; }
@@ -116,7 +119,7 @@ class Session {
     SessionConfig cfg_;
     hipStream_t stream_ = nullptr;
     std::unique_ptr<FramePool> pool_;
-    std::unique_ptr<h264::GpuH264Encoder> enc_;
+    std::unique_ptr<VideoEncoder> enc_;
     uint8_t* nv12_y_ = nullptr;
     uint8_t* nv12_uv_ = nullptr;
     uint8_t* staging_[2] = {nullptr, nullptr};  // pinned upload buffers (one per frame in flight)

@@ -22,7 +22,17 @@ __version__ = "0.1.0"
 
 
 def native():
-    """Import the compiled extension (mxdesk/_native*.so); raises if it is missing."""
+    """Import the compiled extension (mxdesk/_native*.so); raises if it is missing.
+
+    PyTorch-ROCm bundles its own libamdhip64 with the same SONAME as /opt/rocm's.  Whichever
+    is loaded first serves the whole process, and torch's HIP initialisation fails when it
+    finds the system runtime already bound ("No HIP GPUs are available"), so torch (when
+    installed) is imported before the extension.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     from . import _native  # noqa: F401
 
     return _native

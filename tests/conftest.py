@@ -16,9 +16,9 @@ def pytest_configure(config):
 
 def _native_or_none():
     try:
-        from mxdesk import _native
+        from mxdesk import native
 
-        return _native
+        return native()  # imports torch first (shared HIP runtime, see mxdesk.native)
     except ImportError:
         return None
 

@@ -1,0 +1,191 @@
+"""HEVC encoder tests.
+
+CPU tier: the C++ CPU HEVC encoder (same decisions as the HIP kernels) is decoded by the
+independent pure-Python decoder (mxdesk/codec/hevc_decoder.py) and the decoded pictures
+must equal the encoder's reconstruction exactly.  No HEVC reference decoder exists in
+this image (no ffmpeg / libde265), so conformance to other decoders is "parity
+unpinned"; the tables are additionally checked against their closed-form definitions.
+
+GPU tier: the HIP encoder's bitstream must be bit-identical to the CPU encoder's, and its
+reconstruction must equal the decoded pictures.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from mxdesk.codec import hevc_decoder as hd
+from mxdesk.codec.hevc_decoder import Decoder, psnr
+
+from .test_cpu_encoder import synthetic_nv12
+
+
+def _cfg(native, w, h, fps=60, qp=28, bitrate=0, aq=1, sr=8):
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps = w, h, fps
+    cfg.bitrate_kbps = bitrate
+    cfg.qp = qp
+    cfg.aq = aq
+    cfg.search_range = sr
+    return cfg
+
+
+def _cpu_roundtrip(native, w, h, frames, fps=60, qp=28, bitrate=0, fresh=False, idr_at=()):
+    enc = native.CpuHevcEncoder(_cfg(native, w, h, fps, qp, bitrate))
+    stream, recon, src, sizes = b"", [], [], []
+    for t in range(frames):
+        y, uv = synthetic_nv12(w, h, t, seed=t if fresh else 0)
+        au = enc.encode(y, uv, t in idr_at)
+        stream += au
+        sizes.append(len(au))
+        recon.append(tuple(p.copy() for p in enc.recon()))
+        src.append(y)
+    dec = Decoder()
+    frames_out = dec.decode(stream)
+    assert len(dec.frames_coded) == frames
+    for i, ((y, u, v), (ry, ruv)) in enumerate(zip(dec.frames_coded, recon)):
+        assert np.array_equal(y, ry), f"frame {i}: luma differs"
+        assert np.array_equal(u, ruv[:, 0::2]), f"frame {i}: Cb differs"
+        assert np.array_equal(v, ruv[:, 1::2]), f"frame {i}: Cr differs"
+    return frames_out, src, sizes, dec, enc
+
+
+@pytest.mark.parametrize("w,h,qp", [(64, 48, 28), (128, 96, 4), (128, 96, 51), (100, 60, 30), (320, 192, 22)])
+def test_cpu_hevc_decodes_to_reconstruction(native, w, h, qp):
+    out, src, sizes, dec, _ = _cpu_roundtrip(native, w, h, 3, qp=qp, fresh=True)
+    assert out[0][0].shape == (h, w)  # conformance window crops the coded size
+    if qp <= 30:
+        assert psnr(out[0][0], src[0]) > 30
+    assert dec.stats["intra"] == ((w + 15) // 16) * ((h + 15) // 16)
+
+
+def test_cpu_hevc_static_frames_are_skipped(native):
+    enc = native.CpuHevcEncoder(_cfg(native, 128, 64, qp=22))
+    yy, xx = np.mgrid[0:64, 0:128]
+    y = (40 + xx + yy).astype(np.uint8)
+    uv = np.full((32, 128), 128, np.uint8)
+    stream = enc.encode(y, uv, False)
+    p = enc.encode(y, uv, False)
+    stream += p
+    assert set(enc.cu_types()) == {0}  # every CU skipped
+    assert len(p) < 120  # 4 slice headers + one bin per CU
+    Decoder().decode(stream)
+
+
+def test_cpu_hevc_rate_control_and_idr(native):
+    out, _, sizes, dec, enc = _cpu_roundtrip(native, 160, 96, 6, bitrate=300, idr_at=(3,))
+    assert dec.stats["intra"] == 2 * 60  # two IDR pictures of 10 x 6 CUs
+    assert enc.stats.idr == 0
+
+
+def test_cpu_hevc_two_row_slices(native):
+    # 352x288 @ 30 fps is level 2 (16 slice segments) -> 18 CTU rows need 2-row slices, which
+    # exercises above-neighbour intra references, merge/AMVP B candidates and skip contexts
+    _, _, _, dec, enc = _cpu_roundtrip(native, 352, 288, 2, fps=30, qp=30)
+    assert enc.slice_rows == 2
+    assert dec.stats["slices"] == 2 * 9
+
+
+def test_hevc_level_selection(native):
+    assert native.hevc_level(1920, 1080, 60) == 123  # 4.1
+    assert native.hevc_level(3840, 2160, 60) == 153  # 5.1
+    assert native.hevc_level(7680, 4320, 60) == 183  # 6.1
+    assert native.hevc_level(1280, 720, 30) == 93  # 3.1
+
+
+def test_decoder_tables_match_closed_forms():
+    # CABAC rangeTabLps follows p_s = 0.5 * alpha^s, alpha = (0.01875 / 0.5)^(1/63), scaled by
+    # the quantised range midpoints (rows 0-2 of column 0 are clipped to 128)
+    alpha = (0.01875 / 0.5) ** (1 / 63)
+    for s, row in enumerate(hd._RANGE_LPS[:63]):
+        for q, v in enumerate(row):
+            est = 0.5 * alpha ** s * (288 + 64 * q)
+            if not (s < 3 and q == 0):
+                assert abs(v - est) <= 3.5, (s, q, v, est)
+    # transIdxLps follows p' = alpha * p + (1 - alpha)
+    for s in range(1, 63):
+        p = 0.5 * alpha ** s
+        target = math.log((alpha * p + 1 - alpha) / 0.5) / math.log(alpha)
+        assert abs(hd._TRANS_LPS[s] - target) <= 1.0, (s, hd._TRANS_LPS[s], target)
+    # core transform: rows nearly orthogonal with norm 64^2 * N
+    for n in (4, 8, 16, 32):
+        t = hd._tmat(n).astype(np.float64)
+        g = t @ t.T
+        assert np.allclose(np.diag(g), 64 * 64 * n, rtol=0.01)
+        off = g - np.diag(np.diag(g))
+        assert np.abs(off).max() < 0.01 * 64 * 64 * n
+
+
+def test_decoder_rejects_truncated_stream(native):
+    enc = native.CpuHevcEncoder(_cfg(native, 64, 48))
+    y, uv = synthetic_nv12(64, 48, 0)
+    au = enc.encode(y, uv, False)
+    with pytest.raises(Exception):
+        Decoder().decode(au[:-3])
+
+
+# ---------------------------------------------------------------------------- GPU tier
+def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8):
+    import torch
+
+    from .gpu_util import pitched
+
+    cfg = _cfg(gpu, w, h, fps, qp, sr=sr)
+    stream = torch.cuda.current_stream().cuda_stream
+    genc = gpu.GpuHevcEncoder(cfg, stream)
+    cenc = gpu.CpuHevcEncoder(cfg)
+    ch = genc.coded_height
+    gs, grec = b"", []
+    for t in range(frames):
+        y, uv = synthetic_nv12(w, h, t, seed=t if fresh else 0)
+        dy = pitched(y, genc.pitch, ch)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
+        torch.cuda.synchronize()
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        assert gau == cau, f"frame {t}: GPU HEVC bitstream differs from the CPU encoder ({len(gau)} vs {len(cau)})"
+        gs += gau
+        grec.append(genc.recon())
+        cs = cenc.stats
+        assert tuple(genc.stats.sse) == tuple(cs.sse)
+    dec = Decoder()
+    dec.decode(gs)
+    for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
+        assert np.array_equal(yy, ry)
+        assert np.array_equal(u, ruv[:, 0::2])
+        assert np.array_equal(v, ruv[:, 1::2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,fps,qp", [(64, 48, 60, 26), (100, 60, 60, 30), (320, 192, 60, 22), (352, 288, 30, 30),
+                                        (128, 96, 60, 4)])
+def test_gpu_hevc_bit_exact_vs_cpu(gpu, w, h, fps, qp):
+    _gpu_vs_cpu(gpu, w, h, 3, fps=fps, qp=qp)
+
+
+@pytest.mark.gpu
+def test_gpu_session_hevc_stream(gpu):
+    from .test_gpu_pipeline import _read_barcode
+
+    cfg = gpu.SessionConfig()
+    cfg.width, cfg.height, cfg.fps = 320, 192, 60
+    cfg.codec = "hevc"
+    cfg.enc.bitrate_kbps = 0
+    cfg.enc.qp = 24
+    s = gpu.Session(cfg)
+    assert s.codec == "hevc"
+    stream, ids = b"", []
+    for _ in range(4):
+        r = s.step(False)
+        stream += r.au
+        ids.append(r.frame_id)
+        assert r.psnr_y > 30
+    s.request_idr()
+    r = s.step(False)
+    assert r.idr == 1
+    stream += r.au
+    ids.append(r.frame_id)
+    frames = Decoder().decode(stream)
+    assert len(frames) == 5
+    for (y, _, _), fid in zip(frames, ids):
+        assert _read_barcode(y, gpu.BARCODE_CELL, gpu.BARCODE_X, gpu.BARCODE_Y)[0] == fid
