@@ -40,16 +40,22 @@ constexpr uint8_t kDiag2Y[4] = {0, 1, 0, 1};
 constexpr uint8_t kDiag2Inv[4] = {0, 2, 1, 3};
 
 // scan index (sub-block * 16 + position) of raster coordinate (x, y) in an NxN TU
+// nibble-packed copies (ALU lookups for the wave-uniform CABAC kernel)
+constexpr uint64_t kDiag4XP = 0x3323213210210100ull;  // kDiag4X[n] = nibble n
+constexpr uint64_t kDiag4YP = 0x3231230123012010ull;
+MXHD int diag4x(int n) { return (int)((kDiag4XP >> (4 * n)) & 15); }
+MXHD int diag4y(int n) { return (int)((kDiag4YP >> (4 * n)) & 15); }
+
 MXHD int scan_index(int log2n, int x, int y) {
     const int sb = log2n == 4 ? kDiag4Inv[(y >> 2) * 4 + (x >> 2)] : (log2n == 3 ? kDiag2Inv[(y >> 2) * 2 + (x >> 2)] : 0);
     return sb * 16 + kDiag4Inv[(y & 3) * 4 + (x & 3)];
 }
 MXHD void scan_pos(int log2n, int idx, int* x, int* y) {
     const int sb = idx >> 4, n = idx & 15;
-    const int sx = log2n == 4 ? kDiag4X[sb] : (log2n == 3 ? kDiag2X[sb] : 0);
-    const int sy = log2n == 4 ? kDiag4Y[sb] : (log2n == 3 ? kDiag2Y[sb] : 0);
-    *x = sx * 4 + kDiag4X[n];
-    *y = sy * 4 + kDiag4Y[n];
+    const int sx = log2n == 4 ? diag4x(sb) : (log2n == 3 ? (sb >> 1) : 0);
+    const int sy = log2n == 4 ? diag4y(sb) : (log2n == 3 ? (sb & 1) : 0);
+    *x = sx * 4 + diag4x(n);
+    *y = sy * 4 + diag4y(n);
 }
 
 // ---------------------------------------------------------------- core transform (8.6.4.2)
@@ -475,6 +481,28 @@ MXHD void ctx_init_all(uint8_t* ctx, int init_type, int qp) {
     for (int i = 0; i < C_NUM; ++i) ctx[i] = ctx_init_state(kCtxInit[init_type][i], qp);
 }
 
+// Context states in a byte array (host encoder; any memory on the device).
+// A context store also provides the state-transition tables (rangeTabLps, transIdxLps).
+struct ArrCtx {
+    uint8_t* p;
+    MXHD uint32_t get(int i) const { return p[i]; }
+    MXHD void set(int i, uint32_t v) { p[i] = (uint8_t)v; }
+    MXHD uint32_t lps(uint32_t s, uint32_t q) const { return kLps[s][q]; }
+    MXHD uint32_t next_lps(uint32_t s) const { return kNextLps[s]; }
+};
+
+// Wave-uniform value hint: on the device the CABAC kernel runs one slice per wave with every
+// lane holding the same coder state; readfirstlane keeps that state in SGPRs (the compiler
+// cannot prove uniformity through the coder's data-dependent branches).
+MXHD uint32_t uni(uint32_t v) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+#else
+    return v;
+#endif
+}
+MXHD int uni(int v) { return (int)uni((uint32_t)v); }
+
 // Arithmetic encoder (HM-style: 32-bit low register, byte output with carry resolution).
 struct CabacEnc {
     uint32_t low, range;
@@ -498,12 +526,14 @@ struct CabacEnc {
             out[pos] = (uint8_t)b;
         else
             overflow = 1;
-        ++pos;
+        pos = uni(pos + 1);
     }
     MXHD void write_out() {
-        const uint32_t lead = low >> (24 - bits_left);
+        const uint32_t lead = uni(low >> (24 - bits_left));
         bits_left += 8;
         low &= 0xffffffffu >> bits_left;
+        num_buffered = uni(num_buffered);
+        buffered = uni(buffered);
         if (lead == 0xff) {
             ++num_buffered;
         } else if (num_buffered > 0) {
@@ -521,24 +551,31 @@ struct CabacEnc {
         }
     }
     MXHD void test_write_out() {
+        low = uni(low);
+        range = uni(range);
+        bits_left = uni(bits_left);
         if (bits_left < 12) write_out();
     }
-    MXHD void bin(uint8_t& st, int b) {
+    // Context-coded bin; Ctx stores the 142 state bytes ((pStateIdx << 1) | valMps).
+    template <class Ctx>
+    MXHD void bin(Ctx& cx, int idx, int b) {
+        const uint32_t st = cx.get(idx);
         uint32_t s = st >> 1, mps = st & 1;
-        const uint32_t lps = kLps[s][(range >> 6) & 3];
+        const uint32_t lps = cx.lps(s, (range >> 6) & 3);
         range -= lps;
         if ((uint32_t)b != mps) {
             const int nb = __builtin_clz(lps) - 23;
             low = (low + range) << nb;
             range = lps << nb;
             if (s == 0) mps ^= 1;
-            s = kNextLps[s];
+            s = cx.next_lps(s);
             bits_left -= nb;
-            st = (uint8_t)((s << 1) | mps);
+            cx.set(idx, (s << 1) | mps);
             test_write_out();
         } else {
             s = s < 62 ? s + 1 : s;
-            st = (uint8_t)((s << 1) | mps);
+            cx.set(idx, (s << 1) | mps);
+            range = uni(range);
             if (range >= 256) return;
             low <<= 1;
             range <<= 1;
@@ -552,8 +589,20 @@ struct CabacEnc {
         --bits_left;
         test_write_out();
     }
-    MXHD void bypass_bits(uint32_t v, int n) {  // MSB first
-        for (int i = n - 1; i >= 0; --i) bypass((v >> i) & 1);
+    // n bypass bins at once (MSB first): low = (low << n) + range * v, in chunks of 8 so the
+    // 32-bit register never overflows (HM encodeBinsEP)
+    MXHD void bypass_bits(uint32_t v, int n) {
+        while (n > 8) {
+            n -= 8;
+            low = (low << 8) + range * ((v >> n) & 0xffu);
+            bits_left -= 8;
+            test_write_out();
+        }
+        if (n > 0) {
+            low = (low << n) + range * (v & ((1u << n) - 1));
+            bits_left -= n;
+            test_write_out();
+        }
     }
     MXHD void terminate(int b) {
         range -= 2;
@@ -597,15 +646,16 @@ struct CabacEnc {
         n += pad;
         for (int i = n - 8; i >= 0; i -= 8) put_byte((v >> i) & 0xff);
     }
-    // k-th order Exp-Golomb, bypass coded (9.3.3.3)
+    // k-th order Exp-Golomb, bypass coded (9.3.3.3): m ones, a zero, then k + m suffix bits
     MXHD void egk(uint32_t v, int k) {
+        int m = 0;
         while (v >= (1u << k)) {
-            bypass(1);
             v -= 1u << k;
             ++k;
+            ++m;
         }
-        bypass(0);
-        bypass_bits(v, k);
+        bypass_bits((1u << m) - 1, m);
+        bypass_bits(v, k + 1);  // leading zero + k bits
     }
 };
 
@@ -641,39 +691,62 @@ MXHD bool tu_summary(const int16_t* c, int n, uint8_t* last, uint32_t* csbf) {
 }
 
 // ---------------------------------------------------------------- residual_coding (7.3.8.11)
-constexpr uint8_t kLastGroup[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
-                                    8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
-constexpr uint8_t kLastMin[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
-constexpr uint8_t kSig4x4Ctx[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+// last_sig_coeff prefix group of a position and the smallest position of a group
+MXHD int last_group(int pos) {
+    if (pos < 4) return pos;
+    const int l = 31 - __builtin_clz((uint32_t)pos);
+    return 2 * l + ((pos >> (l - 1)) & 1);
+}
+MXHD int last_min(int g) { return g < 4 ? g : (1 << ((g >> 1) - 1)) * (2 + (g & 1)); }
 
-MXHD void code_last_prefix(CabacEnc& e, uint8_t* ctx, int base, int pos, int log2n, int cidx) {
+template <class Ctx>
+MXHD void code_last_prefix(CabacEnc& e, Ctx& ctx, int base, int pos, int log2n, int cidx) {
     const int off = cidx ? 15 : 3 * (log2n - 2) + ((log2n - 1) >> 2);
     const int shift = cidx ? log2n - 2 : (log2n + 1) >> 2;
-    const int prefix = kLastGroup[pos];
+    const int prefix = last_group(pos);
     const int cmax = (log2n << 1) - 1;
-    for (int b = 0; b < prefix; ++b) e.bin(ctx[base + off + (b >> shift)], 1);
-    if (prefix < cmax) e.bin(ctx[base + off + (prefix >> shift)], 0);
+    for (int b = 0; b < prefix; ++b) e.bin(ctx, base + off + (b >> shift), 1);
+    if (prefix < cmax) e.bin(ctx, base + off + (prefix >> shift), 0);
 }
 MXHD void code_last_suffix(CabacEnc& e, int pos) {
-    const int prefix = kLastGroup[pos];
-    if (prefix > 3) e.bypass_bits((uint32_t)(pos - kLastMin[prefix]), (prefix >> 1) - 1);
+    const int prefix = last_group(pos);
+    if (prefix > 3) e.bypass_bits((uint32_t)(pos - last_min(prefix)), (prefix >> 1) - 1);
 }
 
 // coeff_abs_level_remaining (9.3.3.11)
 MXHD void code_remaining(CabacEnc& e, uint32_t v, int rice) {
     if (v < (4u << rice)) {
-        const uint32_t pre = v >> rice;
-        for (uint32_t i = 0; i < pre; ++i) e.bypass(1);
-        e.bypass(0);
-        e.bypass_bits(v & ((1u << rice) - 1), rice);
+        const uint32_t pre = v >> rice;  // pre ones, a zero, rice LSBs
+        e.bypass_bits((((1u << pre) - 1) << (rice + 1)) | (v & ((1u << rice) - 1)), (int)pre + 1 + rice);
     } else {
-        for (int i = 0; i < 4; ++i) e.bypass(1);
+        e.bypass_bits(15, 4);
         e.egk(v - (4u << rice), rice + 1);
     }
 }
 
-// One TU (coefficients in scan order, see scan_index) of size 2^log2n (8 or 16; scanIdx 0).
-MXHD void code_residual(CabacEnc& e, uint8_t* ctx, const int16_t* c, int log2n, int cidx, int last_idx,
+// Coefficient access for the residual coder.  A CU's 24 coded sub-blocks are numbered
+// luma 0..15, Cb 16..19, Cr 20..23 (each TU in scan order); sig(sb) / neg(sb) are 16-bit masks
+// (bit n = scan position n) and absval(sb * 16 + n) the level magnitude.
+struct CoefArray {  // host / generic: the CU's 384 int16 levels
+    const int16_t* c;
+    MXHD uint32_t sig(int sb) const {
+        uint32_t m = 0;
+        for (int n = 0; n < 16; ++n) m |= (c[sb * 16 + n] != 0 ? 1u : 0u) << n;
+        return m;
+    }
+    MXHD uint32_t neg(int sb) const {
+        uint32_t m = 0;
+        for (int n = 0; n < 16; ++n) m |= (c[sb * 16 + n] < 0 ? 1u : 0u) << n;
+        return m;
+    }
+    MXHD int absval(int i) const { return c[i] < 0 ? -c[i] : c[i]; }
+};
+
+MXHD int msb16(uint32_t m) { return 31 - __builtin_clz(m); }  // m != 0
+
+// One TU of size 2^log2n (8 or 16; scanIdx 0) whose sub-blocks start at CU sub-block sb0.
+template <class Ctx, class Cf>
+MXHD void code_residual(CabacEnc& e, Ctx& ctx, const Cf& cf, int sb0, int log2n, int cidx, int last_idx,
                         uint32_t csbf_mask) {
     int lx, ly;
     scan_pos(log2n, last_idx, &lx, &ly);
@@ -686,29 +759,29 @@ MXHD void code_residual(CabacEnc& e, uint8_t* ctx, const int16_t* c, int log2n, 
     // coded_sub_block_flag per raster sub-block: coded / inferred (DC and last sub-block)
     uint32_t csbf_r = 0;
     for (int i = 0; i <= last_sb; ++i) {
-        const int sx = log2n == 4 ? kDiag4X[i] : kDiag2X[i], sy = log2n == 4 ? kDiag4Y[i] : kDiag2Y[i];
+        const int sx = log2n == 4 ? diag4x(i) : (i >> 1), sy = log2n == 4 ? diag4y(i) : (i & 1);
         if (i == 0 || i == last_sb || ((csbf_mask >> i) & 1)) csbf_r |= 1u << (sy * sbw + sx);
     }
-    int g1ctx_prev = -1;  // greater1Ctx state carried from the previous sub-block with levels (-1: none yet)
+    int g1ctx_prev = -1;  // greater1Ctx carried from the previous sub-block with levels (-1: none yet)
     for (int i = last_sb; i >= 0; --i) {
-        const int sx = log2n == 4 ? kDiag4X[i] : kDiag2X[i], sy = log2n == 4 ? kDiag4Y[i] : kDiag2Y[i];
+        const int sx = log2n == 4 ? diag4x(i) : (i >> 1), sy = log2n == 4 ? diag4y(i) : (i & 1);
         const bool right = sx + 1 < sbw && ((csbf_r >> (sy * sbw + sx + 1)) & 1);
         const bool below = sy + 1 < sbw && ((csbf_r >> ((sy + 1) * sbw + sx)) & 1);
-        const int16_t* sb = c + i * 16;
         bool infer_dc = false;
         if (i < last_sb && i > 0) {
             const int coded = (csbf_mask >> i) & 1;
-            e.bin(ctx[C_CSBF + (cidx ? 2 : 0) + ((right || below) ? 1 : 0)], coded);
+            e.bin(ctx, C_CSBF + (cidx ? 2 : 0) + ((right || below) ? 1 : 0), coded);
             if (!coded) continue;
             infer_dc = true;
         }
+        const uint32_t sig = cf.sig(sb0 + i);
         // significance
         const int prev_csbf = (right ? 1 : 0) | (below ? 2 : 0);
         const int nstart = (i == last_sb) ? last_n - 1 : 15;
         for (int n = nstart; n >= 0; --n) {
             if (n == 0 && infer_dc) break;
-            const int sig = sb[n] != 0;
-            const int xp = kDiag4X[n], yp = kDiag4Y[n];
+            const int bit = (sig >> n) & 1;
+            const int xp = diag4x(n), yp = diag4y(n);
             int sc;
             if (i == 0 && n == 0) {
                 sc = 0;
@@ -728,42 +801,47 @@ MXHD void code_residual(CabacEnc& e, uint8_t* ctx, const int16_t* c, int log2n, 
                     sc += log2n == 3 ? 9 : 12;
                 }
             }
-            e.bin(ctx[C_SIG + (cidx ? 27 : 0) + sc], sig);
-            if (sig) infer_dc = false;
+            e.bin(ctx, C_SIG + (cidx ? 27 : 0) + sc, bit);
+            if (bit) infer_dc = false;
         }
+        if (!sig) continue;
         // levels of the nonzero coefficients, n = 15 down to 0 (greater1 flags for the first 8)
-        int nsig = 0;
-        for (int n = 15; n >= 0; --n) nsig += sb[n] != 0;
-        if (!nsig) continue;
+        const int base_i = (sb0 + i) * 16;
         int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
         if (g1ctx_prev == 0) ++ctx_set;
         int g1ctx = 1, g2_pos = -1, k = 0;
-        for (int n = 15; n >= 0 && k < 8; --n) {
-            const int v = sb[n];
-            if (!v) continue;
-            const int g1 = (v > 1 || v < -1) ? 1 : 0;
-            e.bin(ctx[C_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + (g1ctx < 3 ? g1ctx : 3)], g1);
+        for (uint32_t m = sig; m && k < 8; ++k) {
+            const int n = msb16(m);
+            m &= ~(1u << n);
+            const int g1 = cf.absval(base_i + n) > 1 ? 1 : 0;
+            e.bin(ctx, C_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + (g1ctx < 3 ? g1ctx : 3), g1);
             if (g1) {
                 g1ctx = 0;
                 if (g2_pos < 0) g2_pos = n;
             } else if (g1ctx > 0) {
                 ++g1ctx;
             }
-            ++k;
         }
         g1ctx_prev = g1ctx;
-        if (g2_pos >= 0) {
-            const int a = sb[g2_pos] < 0 ? -sb[g2_pos] : sb[g2_pos];
-            e.bin(ctx[C_GT2 + (cidx ? 4 : 0) + ctx_set], a > 2);
+        if (g2_pos >= 0) e.bin(ctx, C_GT2 + (cidx ? 4 : 0) + ctx_set, cf.absval(base_i + g2_pos) > 2);
+        {  // sign bits of the nonzero levels, n = 15 down to 0, as one bypass run
+            const uint32_t neg = cf.neg(sb0 + i);
+            uint32_t bits = 0;
+            int nb = 0;
+            for (uint32_t m = sig; m; ++nb) {
+                const int n = msb16(m);
+                m &= ~(1u << n);
+                bits = (bits << 1) | ((neg >> n) & 1);
+            }
+            e.bypass_bits(bits, nb);
         }
-        for (int n = 15; n >= 0; --n)
-            if (sb[n]) e.bypass(sb[n] < 0);
         int rice = 0;
         k = 0;
-        for (int n = 15; n >= 0; --n) {
-            const int v = sb[n];
-            if (!v) continue;
-            const int a = v < 0 ? -v : v;
+        for (uint32_t m = sig; m; ++k) {
+            const int n = msb16(m);
+            m &= ~(1u << n);
+            if (k < 8 && n != g2_pos && g2_pos < 0) continue;  // all levels 1: nothing left to code
+            const int a = cf.absval(base_i + n);
             int base, thr;
             if (k < 8) {
                 base = 1 + (a > 1 ? 1 : 0) + (n == g2_pos && a > 2 ? 1 : 0);
@@ -776,18 +854,18 @@ MXHD void code_residual(CabacEnc& e, uint8_t* ctx, const int16_t* c, int log2n, 
                 code_remaining(e, (uint32_t)(a - base), rice);
                 if (a > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
             }
-            ++k;
         }
     }
 }
 
 // ---------------------------------------------------------------- CU syntax (7.3.8.5)
-MXHD void code_mvd(CabacEnc& e, uint8_t* ctx, int dx, int dy) {
+template <class Ctx>
+MXHD void code_mvd(CabacEnc& e, Ctx& ctx, int dx, int dy) {
     const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
-    e.bin(ctx[C_MVD_G0], ax > 0);
-    e.bin(ctx[C_MVD_G0], ay > 0);
-    if (ax > 0) e.bin(ctx[C_MVD_G1], ax > 1);
-    if (ay > 0) e.bin(ctx[C_MVD_G1], ay > 1);
+    e.bin(ctx, C_MVD_G0, ax > 0);
+    e.bin(ctx, C_MVD_G0, ay > 0);
+    if (ax > 0) e.bin(ctx, C_MVD_G1, ax > 1);
+    if (ay > 0) e.bin(ctx, C_MVD_G1, ay > 1);
     if (ax > 0) {
         if (ax > 1) e.egk((uint32_t)(ax - 2), 1);
         e.bypass(dx < 0);
@@ -802,23 +880,32 @@ MXHD int qp_delta_wrap(int qp, int pred) { return ((qp - pred + 26 + 52) % 52) -
 
 // One CTU (= one CU).  left / above: neighbouring CUs in the same slice or null.
 // qp_prev: QP predictor (QpY of the previous CU in decoding order, slice QP at start).
-MXHD void code_cu(CabacEnc& e, uint8_t* ctx, bool islice, const CuInfo& c, const int16_t* coef, const CuInfo* left,
-                  const CuInfo* above, int& qp_prev, bool end_of_slice) {
+// Neighbour facts the CU syntax needs (type -1: not available in the slice).
+struct CuNb {
+    int left_type, left_mode, above_type;
+};
+MXHD CuNb cu_nb(const CuInfo* left, const CuInfo* above) {
+    return CuNb{left ? (int)left->type : -1, left ? (int)left->intra_mode : 1, above ? (int)above->type : -1};
+}
+
+template <class Ctx, class Cf>
+MXHD void code_cu(CabacEnc& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf& cf, CuNb nb, int& qp_prev,
+                  bool end_of_slice) {
     if (!islice) {
-        const int inc = (left && left->type == kCuSkip ? 1 : 0) + (above && above->type == kCuSkip ? 1 : 0);
-        e.bin(ctx[C_SKIP + inc], c.type == kCuSkip);
+        const int inc = (nb.left_type == kCuSkip ? 1 : 0) + (nb.above_type == kCuSkip ? 1 : 0);
+        e.bin(ctx, C_SKIP + inc, c.type == kCuSkip);
     }
     if (c.type != kCuSkip) {
         const bool intra = c.type == kCuIntra;
-        if (!islice) e.bin(ctx[C_PRED_MODE], intra);
-        e.bin(ctx[C_PART_MODE], 1);  // PART_2Nx2N
+        if (!islice) e.bin(ctx, C_PRED_MODE, intra);
+        e.bin(ctx, C_PART_MODE, 1);  // PART_2Nx2N
         if (intra) {
-            const int cand_a = (left && left->type == kCuIntra) ? left->intra_mode : 1;
+            const int cand_a = nb.left_type == kCuIntra ? nb.left_mode : 1;
             int l[3];
             mpm_list(cand_a, 1, l);
             const int m = c.intra_mode;
             const int hit = (m == l[0]) ? 0 : (m == l[1] ? 1 : (m == l[2] ? 2 : -1));
-            e.bin(ctx[C_PREV_INTRA], hit >= 0);
+            e.bin(ctx, C_PREV_INTRA, hit >= 0);
             if (hit >= 0) {
                 e.bypass(hit > 0);
                 if (hit > 0) e.bypass(hit > 1);
@@ -827,37 +914,42 @@ MXHD void code_cu(CabacEnc& e, uint8_t* ctx, bool islice, const CuInfo& c, const
                 for (int k = 0; k < 3; ++k) rem -= (l[k] < m) ? 1 : 0;
                 e.bypass_bits((uint32_t)rem, 5);
             }
-            e.bin(ctx[C_CHROMA_PRED], 0);  // intra_chroma_pred_mode 4 (DM)
+            e.bin(ctx, C_CHROMA_PRED, 0);  // intra_chroma_pred_mode 4 (DM)
         } else {
             const bool merge = c.type == kCuMerge;
-            e.bin(ctx[C_MERGE_FLAG], merge);
+            e.bin(ctx, C_MERGE_FLAG, merge);
             if (!merge) {
                 code_mvd(e, ctx, c.mvdx, c.mvdy);
-                e.bin(ctx[C_MVP], c.mvp_idx);
+                e.bin(ctx, C_MVP, c.mvp_idx);
             }
         }
         bool root = true;
         if (c.type == kCuAmvp) {
             root = c.cbf != 0;
-            e.bin(ctx[C_RQT_ROOT], root);
+            e.bin(ctx, C_RQT_ROOT, root);
         }
         if (root) {
             const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
-            e.bin(ctx[C_CBF_CHROMA + 0], cb);
-            e.bin(ctx[C_CBF_CHROMA + 0], cr);
-            if (intra || cb || cr) e.bin(ctx[C_CBF_LUMA + 1], cy);
+            e.bin(ctx, C_CBF_CHROMA + 0, cb);
+            e.bin(ctx, C_CBF_CHROMA + 0, cr);
+            if (intra || cb || cr) e.bin(ctx, C_CBF_LUMA + 1, cy);
             if (c.cbf) {
                 const int d = qp_delta_wrap(c.qp, qp_prev);
                 const int a = d < 0 ? -d : d;
                 const int pre = a < 5 ? a : 5;
-                for (int k = 0; k < pre; ++k) e.bin(ctx[C_QP_DELTA + (k ? 1 : 0)], 1);
-                if (pre < 5) e.bin(ctx[C_QP_DELTA + (pre ? 1 : 0)], 0);
+                for (int k = 0; k < pre; ++k) e.bin(ctx, C_QP_DELTA + (k ? 1 : 0), 1);
+                if (pre < 5) e.bin(ctx, C_QP_DELTA + (pre ? 1 : 0), 0);
                 if (a >= 5) e.egk((uint32_t)(a - 5), 0);
                 if (a) e.bypass(d < 0);
                 qp_prev = c.qp;
-                if (cy) code_residual(e, ctx, coef, 4, 0, c.last[0], c.csbf_y);
-                if (cb) code_residual(e, ctx, coef + 256, 3, 1, c.last[1], c.csbf_c[0]);
-                if (cr) code_residual(e, ctx, coef + 320, 3, 2, c.last[2], c.csbf_c[1]);
+                // one call site for the three TUs keeps the (inlined) device code small
+#pragma unroll 1
+                for (int t = 0; t < 3; ++t) {
+                    if (!((c.cbf >> t) & 1)) continue;
+                    const int last = t == 0 ? c.last[0] : (t == 1 ? c.last[1] : c.last[2]);
+                    const uint32_t csbf = t == 0 ? c.csbf_y : (t == 1 ? c.csbf_c[0] : c.csbf_c[1]);
+                    code_residual(e, ctx, cf, t == 0 ? 0 : (t == 1 ? 16 : 20), t == 0 ? 4 : 3, t, last, csbf);
+                }
             }
         }
     }
@@ -867,8 +959,9 @@ MXHD void code_cu(CabacEnc& e, uint8_t* ctx, bool islice, const CuInfo& c, const
 // Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row).
 // Returns the number of payload bytes (> cap means overflow).
 MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
-                         int first, int count, int ctb_w, uint8_t* ctx) {
-    ctx_init_all(ctx, islice ? 0 : 1, slice_qp);
+                         int first, int count, int ctb_w, uint8_t* ctx_mem) {
+    ctx_init_all(ctx_mem, islice ? 0 : 1, slice_qp);
+    ArrCtx ctx{ctx_mem};
     CabacEnc e;
     e.start(out, cap);
     int qp_prev = slice_qp;
@@ -877,7 +970,8 @@ MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, 
         const int x = i % ctb_w;
         const CuInfo* left = (x > 0 && k > 0) ? &cus[i - 1] : nullptr;
         const CuInfo* above = (k >= ctb_w) ? &cus[i - ctb_w] : nullptr;
-        code_cu(e, ctx, islice, cus[i], coef + (size_t)i * kCoefPerCu, left, above, qp_prev, k == count - 1);
+        const CoefArray cf{coef + (size_t)i * kCoefPerCu};
+        code_cu(e, ctx, islice, cus[i], cf, cu_nb(left, above), qp_prev, k == count - 1);
     }
     e.finish_slice();
     return e.pos;
@@ -898,15 +992,50 @@ MXHD int intra_mode_bits(int mode, int cand_a) {
 
 // Residual (raster NxN) -> quantised levels in scan order + reconstructed residual (raster).
 // Returns the number of nonzero levels.
+// Inter TU decimation: a TU whose only levels are a few +-1s is zeroed (it costs many
+// significance bins and bits for a fraction of a dB; HM/x264 drop such blocks by RD or
+// decimation scores).  Same rule in the CPU and GPU encoders.
+// Trailing-level trim (inter): the last significant level is dropped while it is +-1 and
+// more than kTrimGap zero positions separate it from the previous one (each costs a
+// significance bin), at most kTrimIters times per TU.
+constexpr int kTrimGap = 8;
+constexpr int kTrimIters = 4;
+
+MXHD bool tu_decimate(int log2n, bool intra, int nz, int max_abs) {
+    return !intra && nz > 0 && max_abs == 1 && nz <= (log2n == 4 ? 4 : 2);
+}
+
 MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* levels, int* rres) {
     const int N = 1 << log2n;
     int c[256], d[256];
     fwd_transform(log2n, res, c);
-    int nz = 0;
+    int nz = 0, mx = 0;
     for (int v = 0; v < N; ++v)
         for (int u = 0; u < N; ++u) {
             const int l = quant_coef(c[v * N + u], qp, log2n, intra);
-            levels[scan_index(log2n, u, v)] = (int16_t)l;
+            c[v * N + u] = l;
+            nz += l != 0;
+            mx = (l < 0 ? -l : l) > mx ? (l < 0 ? -l : l) : mx;
+        }
+    const bool drop = tu_decimate(log2n, intra, nz, mx);
+    for (int v = 0; v < N; ++v)
+        for (int u = 0; u < N; ++u) levels[scan_index(log2n, u, v)] = (int16_t)(drop ? 0 : c[v * N + u]);
+    if (!intra) {  // trailing isolated +-1 levels (same rule as the GPU kernel)
+        for (int it = 0; it < kTrimIters; ++it) {
+            int last = -1, prev = -1;
+            for (int i = 0; i < N * N; ++i)
+                if (levels[i]) {
+                    prev = last;
+                    last = i;
+                }
+            if (last < 0 || (levels[last] != 1 && levels[last] != -1) || last - prev <= kTrimGap) break;
+            levels[last] = 0;
+        }
+    }
+    nz = 0;
+    for (int v = 0; v < N; ++v)
+        for (int u = 0; u < N; ++u) {
+            const int l = levels[scan_index(log2n, u, v)];
             nz += l != 0;
             d[v * N + u] = dequant_coef(l, qp, log2n);
         }

@@ -106,15 +106,90 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     TuResult out;
     int lastl = -1, lastc = -1, nzl = 0, nzc = 0;
     uint32_t csl = 0, csc = 0;
-    // ---- forward stage 2 (columns) + quantisation + dequantisation into b
+    // ---- forward stage 2 (columns) + quantisation (levels kept in registers)
+    int ll[4] = {0, 0, 0, 0}, lc[2] = {0, 0};
+    int mxl = 0, mxc = 0;
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = lane * 4 + j, k2 = idx >> 4, k = idx & 15;
             int s = 0;
 #pragma unroll
             for (int y = 0; y < 16; ++y) s += M.t16[k2 * 16 + y] * t.a[y * 16 + k];
-            const int c = (s + 512) >> 10;
-            const int l = quant_coef(c, qp, 4, intra);
+            ll[j] = quant_coef((s + 512) >> 10, qp, 4, intra);
+            nzl += ll[j] != 0;
+            mxl = max(mxl, abs(ll[j]));
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = cl * 2 + j, k2 = idx >> 3, k = idx & 7;
+            const int32_t* a = t.a + 256 + comp * 64;
+            int s = 0;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) s += M.t8[k2 * 8 + y] * a[y * 8 + k];
+            lc[j] = quant_coef((s + 256) >> 9, qpc, 3, intra);
+            nzc += lc[j] != 0;
+            mxc = max(mxc, abs(lc[j]));
+        }
+    }
+    // decimation (wave-uniform decisions per TU), then levels / dequantised values / summaries
+    const bool drop_y = tu_decimate(4, intra, wsum(nzl), wmax(mxl));
+    const bool drop_cb = tu_decimate(3, intra, wsum(comp == 0 ? nzc : 0), wmax(comp == 0 ? mxc : 0));
+    const bool drop_cr = tu_decimate(3, intra, wsum(comp == 1 ? nzc : 0), wmax(comp == 1 ? mxc : 0));
+    const bool drop_c = comp ? drop_cr : drop_cb;
+    if (drop_y)
+        for (int j = 0; j < 4; ++j) ll[j] = 0;
+    if (drop_c)
+        for (int j = 0; j < 2; ++j) lc[j] = 0;
+    if (!intra) {
+        // trailing isolated +-1 trim (tu_encode rule), one TU after the other; the lane owning
+        // the last level clears it
+        for (int it = 0; it < kTrimIters; ++it) {
+            int last = -1;
+            for (int j = 0; j < 4; ++j)
+                if (ll[j]) last = max(last, scan_index(4, (lane * 4 + j) & 15, (lane * 4 + j) >> 4));
+            last = wmax(last);
+            if (last < 0) break;
+            int prev = -1, lv = 0;
+            for (int j = 0; j < 4; ++j) {
+                const int si = scan_index(4, (lane * 4 + j) & 15, (lane * 4 + j) >> 4);
+                if (ll[j] && si < last) prev = max(prev, si);
+                if (si == last) lv = abs(ll[j]);
+            }
+            prev = wmax(prev);
+            lv = wmax(lv);
+            if (lv != 1 || last - prev <= kTrimGap) break;
+            for (int j = 0; j < 4; ++j)
+                if (scan_index(4, (lane * 4 + j) & 15, (lane * 4 + j) >> 4) == last) ll[j] = 0;
+        }
+        for (int cc = 0; cc < 2; ++cc) {
+            for (int it = 0; it < kTrimIters; ++it) {
+                int last = -1;
+                for (int j = 0; j < 2; ++j) {
+                    const int idx = cl * 2 + j;
+                    if (comp == cc && lc[j]) last = max(last, scan_index(3, idx & 7, idx >> 3));
+                }
+                last = wmax(last);
+                if (last < 0) break;
+                int prev = -1, lv = 0;
+                for (int j = 0; j < 2; ++j) {
+                    const int idx = cl * 2 + j, si = scan_index(3, idx & 7, idx >> 3);
+                    if (comp == cc && lc[j] && si < last) prev = max(prev, si);
+                    if (comp == cc && si == last) lv = abs(lc[j]);
+                }
+                prev = wmax(prev);
+                lv = wmax(lv);
+                if (lv != 1 || last - prev <= kTrimGap) break;
+                for (int j = 0; j < 2; ++j) {
+                    const int idx = cl * 2 + j;
+                    if (comp == cc && scan_index(3, idx & 7, idx >> 3) == last) lc[j] = 0;
+                }
+            }
+        }
+    }
+    nzl = nzc = 0;
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = lane * 4 + j, k2 = idx >> 4, k = idx & 15;
+            const int l = ll[j];
             const int si = scan_index(4, k, k2);
             coef[si] = (int16_t)l;
             t.b[idx] = dequant_coef(l, qp, 4);
@@ -126,12 +201,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = cl * 2 + j, k2 = idx >> 3, k = idx & 7;
-            const int32_t* a = t.a + 256 + comp * 64;
-            int s = 0;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) s += M.t8[k2 * 8 + y] * a[y * 8 + k];
-            const int c = (s + 256) >> 9;
-            const int l = quant_coef(c, qpc, 3, intra);
+            const int l = lc[j];
             const int si = scan_index(3, k, k2);
             coef[256 + comp * 64 + si] = (int16_t)l;
             t.b[256 + comp * 64 + idx] = dequant_coef(l, qpc, 3);
@@ -515,19 +585,127 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
 }
 
 // ------------------------------------------------------------------ CABAC
+// The whole wave runs the slice coder in lockstep on identical (wave-uniform) values, so
+// the arithmetic-coder state lives in SGPRs and every table lookup is a register read:
+//  * context states: lane l of r0/r1/r2 holds state 64*j + l, read with v_readlane and
+//    written with v_writelane (no memory round trip per bin);
+//  * rangeTabLps / transIdxLps: lane s holds row s (4 packed bytes / next state);
+//  * coefficients of the CU being coded: lane l holds levels l, 64+l, ..., 320+l; their
+//    significance / sign masks come from six ballots, magnitudes from v_readlane.
+struct LaneCtx {
+    uint32_t r0, r1, r2;
+    uint32_t lps_row, next;
+    int lane;
+    __device__ __forceinline__ uint32_t get(int i) const {
+        const uint32_t v = i < 64 ? r0 : (i < 128 ? r1 : r2);
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, i & 63);
+    }
+    __device__ __forceinline__ void set(int i, uint32_t v) {
+        const bool me = lane == (i & 63);  // v_cndmask: only the owning lane takes the new state
+        if (i < 64)
+            r0 = me ? v : r0;
+        else if (i < 128)
+            r1 = me ? v : r1;
+        else
+            r2 = me ? v : r2;
+    }
+    __device__ __forceinline__ uint32_t lps(uint32_t s, uint32_t q) const {
+        return ((uint32_t)__builtin_amdgcn_readlane((int)lps_row, (int)s) >> (8 * q)) & 0xff;
+    }
+    __device__ __forceinline__ uint32_t next_lps(uint32_t s) const {
+        return (uint32_t)__builtin_amdgcn_readlane((int)next, (int)s);
+    }
+};
+
+__device__ __forceinline__ uint64_t sel6(const uint64_t* v, int k) {
+    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : k == 3 ? v[3] : k == 4 ? v[4] : v[5];
+}
+__device__ __forceinline__ int sel6i(const int* v, int k) {
+    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : k == 3 ? v[3] : k == 4 ? v[4] : v[5];
+}
+
+struct WaveCoef {
+    uint64_t sigm[6], negm[6];  // wave-uniform ballots
+    int a[6];                   // this lane's magnitudes
+    __device__ __forceinline__ uint32_t sig(int sb) const { return (uint32_t)(sel6(sigm, sb >> 2) >> ((sb & 3) * 16)) & 0xffffu; }
+    __device__ __forceinline__ uint32_t neg(int sb) const { return (uint32_t)(sel6(negm, sb >> 2) >> ((sb & 3) * 16)) & 0xffffu; }
+    __device__ __forceinline__ int absval(int i) const { return __builtin_amdgcn_readlane(sel6i(a, i >> 6), i & 63); }
+};
+
+__device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
+    // 5 dwords (CuInfo is 20 bytes, 4-byte aligned in the array) -> scalar loads
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(cus) + (size_t)i * 5;
+    uint32_t w[5];
+    for (int k = 0; k < 5; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[k]);
+    CuInfo c;
+    __builtin_memcpy(&c, w, sizeof c);
+    return c;
+}
+
 __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameState* __restrict__ fs,
                                                     const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
                                                     uint8_t* __restrict__ slice_data, uint32_t slice_cap,
                                                     uint32_t* __restrict__ slice_len) {
-    __shared__ uint8_t ctx[C_NUM];
-    const int s = blockIdx.x;
-    if (threadIdx.x != 0) return;
+    const int s = blockIdx.x, lane = threadIdx.x;
     const int sr = fs->slice_rows;
     const int rows = min(sr, g.mb_h - s * sr);
     const int first = s * sr * g.mb_w, count = rows * g.mb_w;
-    const uint32_t n = code_slice(slice_data + (size_t)s * slice_cap, slice_cap, fs->idr != 0, fs->qp, cus, coef, first,
-                                  count, g.mb_w, ctx);
-    slice_len[s] = n;
+    const bool islice = fs->idr != 0;
+    const int qp = fs->qp;
+    LaneCtx ctx;
+    {
+        const int t = islice ? 0 : 1;
+        ctx.r0 = ctx_init_state(kCtxInit[t][lane], qp);
+        ctx.r1 = ctx_init_state(kCtxInit[t][64 + lane], qp);
+        ctx.r2 = 128 + lane < C_NUM ? ctx_init_state(kCtxInit[t][128 + lane], qp) : 0u;
+        ctx.lps_row = (uint32_t)kLps[lane][0] | ((uint32_t)kLps[lane][1] << 8) | ((uint32_t)kLps[lane][2] << 16) |
+                      ((uint32_t)kLps[lane][3] << 24);
+        ctx.next = kNextLps[lane];
+        ctx.lane = lane;
+    }
+    CabacEnc e;
+    e.start(slice_data + (size_t)s * slice_cap, slice_cap);
+    int qp_prev = qp;
+    int prev_type = -1, prev_mode = 1;
+    // software pipeline: the next CU's descriptor words and levels are loaded (vector loads
+    // in flight) while the current CU is coded
+    const uint32_t* cuw = reinterpret_cast<const uint32_t*>(cus);
+    uint32_t raw[5];
+    int vn[6];
+    for (int q = 0; q < 5; ++q) raw[q] = cuw[(size_t)first * 5 + q];
+    for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)first * kCoefPerCu + q * 64 + lane];
+    for (int k = 0; k < count; ++k) {
+        const int i = first + k;
+        const int x = i % g.mb_w;
+        CuInfo c;
+        {
+            uint32_t w[5];
+            for (int q = 0; q < 5; ++q) w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)raw[q]);
+            __builtin_memcpy(&c, w, sizeof c);
+        }
+        int v[6];
+        for (int q = 0; q < 6; ++q) v[q] = vn[q];
+        if (k + 1 < count) {
+            for (int q = 0; q < 5; ++q) raw[q] = cuw[(size_t)(i + 1) * 5 + q];
+            for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)(i + 1) * kCoefPerCu + q * 64 + lane];
+        }
+        WaveCoef cf;
+        for (int q = 0; q < 6; ++q) {
+            const bool use = c.type != kCuSkip && c.cbf;
+            cf.sigm[q] = use ? __ballot(v[q] != 0) : 0ull;
+            cf.negm[q] = use ? __ballot(v[q] < 0) : 0ull;
+            cf.a[q] = v[q] < 0 ? -v[q] : v[q];
+        }
+        CuNb nb;
+        nb.left_type = (x > 0 && k > 0) ? prev_type : -1;
+        nb.left_mode = prev_mode;
+        nb.above_type = k >= g.mb_w ? (int)load_cu(cus, i - g.mb_w).type : -1;
+        code_cu(e, ctx, islice, c, cf, nb, qp_prev, k == count - 1);
+        prev_type = c.type;
+        prev_mode = c.intra_mode;
+    }
+    e.finish_slice();
+    if (lane == 0) slice_len[s] = e.pos;
 }
 
 // ------------------------------------------------------------------ pack
