@@ -45,6 +45,8 @@ def main() -> None:
     ap.add_argument("--out-width", type=int, default=0, help="encode width (0 = desktop width; else fused Lanczos-3 + CSC)")
     ap.add_argument("--out-height", type=int, default=0)
     ap.add_argument("--bitrate-kbps", type=int, default=8000)
+    ap.add_argument("--codec", default="h264", choices=["h264", "hevc"],
+                    help="h264 (headline, mxh264enc) or hevc (mxh265enc, BASELINE config '4K60 HEVC')")
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
@@ -96,6 +98,7 @@ def main() -> None:
     cfg.noise = args.noise
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth
+    cfg.codec = args.codec
     K = max(1, args.sessions_per_gpu)
     sessions = [N.Session(cfg) for _ in range(K)]
 
@@ -163,7 +166,9 @@ def main() -> None:
     kbps = statistics.mean(all_sizes) * 8 * args.fps / 1000.0
     if rank == 0:
         out = {
-            "metric": "encoded FPS (1080p H.264 desktop session, aggregate over GPUs) + p50 E2E latency",
+            "metric": "encoded FPS (1080p H.264 desktop session, aggregate over GPUs) + p50 E2E latency"
+                      if args.codec == "h264" else
+                      "encoded FPS (HEVC desktop session, aggregate over GPUs) + p50 E2E latency",
             "value": round(fps_total, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -185,12 +190,14 @@ def main() -> None:
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),
             "mean_qp": round(statistics.mean(qps), 2),
             "mean_psnr_y_db": round(statistics.mean(psnrs), 2),
-            "dtype": "uint8 video (8-bit 4:2:0), H.264 Constrained Baseline",
+            "dtype": "uint8 video (8-bit 4:2:0), " + ("H.264 Constrained Baseline" if args.codec == "h264"
+                                                       else "HEVC Main profile"),
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",
             "config": {
-                "model": f"{args.width}x{args.height}@{args.fps} H.264 desktop session"
+                "model": f"{args.width}x{args.height}@{args.fps} {'H.264' if args.codec == 'h264' else 'HEVC'}"
+                         " desktop session"
                          + (f" scaled to {args.out_width}x{args.out_height}" if args.out_width else "")
-                         + " (mxh264enc, CBR "
+                         + f" ({'mxh264enc' if args.codec == 'h264' else 'mxh265enc'}, CBR "
                          f"{args.bitrate_kbps} kbps, ME +/-{args.search_range} qpel={args.subpel})",
                 "global_batch": world * K,
                 "seq_len": args.width * args.height,

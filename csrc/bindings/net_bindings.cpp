@@ -4,6 +4,7 @@
 
 #include "../net/dtls.h"
 #include "../net/rtp_h264.h"
+#include "../net/rtp_h265.h"
 #include "../net/srtp.h"
 
 namespace py = pybind11;
@@ -54,5 +55,13 @@ void register_net(py::module& m) {
         .def_property_readonly("ssrc", &RtpH264Packetizer::ssrc)
         .def_property_readonly("packets", &RtpH264Packetizer::packets)
         .def_property_readonly("octets", &RtpH264Packetizer::octets);
+    py::class_<RtpH265Packetizer>(n, "RtpH265Packetizer")
+        .def(py::init<uint32_t, uint8_t, size_t, uint16_t>(), py::arg("ssrc"), py::arg("payload_type"),
+             py::arg("max_payload") = 1150, py::arg("first_seq") = 0)
+        .def("packetize", [](RtpH265Packetizer& p, py::bytes au, uint32_t ts) { return BV(p.packetize(au, ts)); })
+        .def_property_readonly("next_seq", &RtpH265Packetizer::next_seq)
+        .def_property_readonly("ssrc", &RtpH265Packetizer::ssrc)
+        .def_property_readonly("packets", &RtpH265Packetizer::packets)
+        .def_property_readonly("octets", &RtpH265Packetizer::octets);
     n.def("split_annexb", [](py::bytes au) { return BV(split_annexb(au)); });
 }

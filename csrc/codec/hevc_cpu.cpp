@@ -49,7 +49,7 @@ void profile_tier_level(Bits& w, int level_idc) {
     w.put(0x60000000u, 32);  // compatibility flags 1 (Main) and 2 (Main 10)
     w.put(1, 1);   // progressive_source
     w.put(0, 1);   // interlaced_source
-    w.put(0, 1);   // non_packed_constraint
+    w.put(1, 1);   // non_packed_constraint (no frame-packing SEI): codec string hvc1.1.6.Lxx.B0
     w.put(1, 1);   // frame_only_constraint
     w.put(0, 32);  // 43 reserved zero bits + general_inbld_flag
     w.put(0, 12);

@@ -31,7 +31,7 @@ def _setup_logging(cfg: C.Config) -> None:
 def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0"):
     from .pipeline.stream import StreamPipeline
 
-    backend = "gpu" if cfg.encoder_backend == "mxh264enc" else "cpu"
+    backend = "gpu" if cfg.gpu_encoder else "cpu"
     capture = None
     if cfg.source == "x11" or (cfg.source == "auto" and _x_available(cfg.display)):
         from .models.x11 import X11Capture
@@ -40,7 +40,7 @@ def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0"):
     return StreamPipeline(cfg.sizew, cfg.sizeh, cfg.stream_fps, backend=backend, device=device,
                           bitrate_kbps=cfg.video_bitrate, keyint=cfg.keyint_frames, search_range=cfg.search_range,
                           subpel=cfg.subpel, noise=cfg.noise, out_width=cfg.out_width, out_height=cfg.out_height,
-                          session_name=session_name, capture=capture)
+                          session_name=session_name, capture=capture, codec=cfg.codec)
 
 
 def _x_available(display: str) -> bool:
@@ -63,7 +63,7 @@ def _gpu_index(cfg: C.Config) -> int:
 def cmd_serve(cfg: C.Config, args) -> None:
     from .server.app import MediaServer, run_forever, ssl_context
 
-    device = 0 if cfg.encoder_backend != "mxh264enc" else _gpu_index(cfg)
+    device = _gpu_index(cfg) if cfg.gpu_encoder else 0
     pipe = build_pipeline(cfg, device)
     rfb = None
     if cfg.novnc_enable:

@@ -40,6 +40,18 @@ class EncodedFrame:
     width: int
     height: int
     gpu_ms: float = 0.0
+    codec_id: int = 1  # media header codec byte: 1 = H.264, 2 = HEVC
+
+
+def hevc_codec_string(width: int, height: int, fps: int) -> str:
+    """WebCodecs/RFC 6381 codec id of our Main-profile HEVC stream (hvc1.1.6.L<level>.B0)."""
+    from .. import native
+
+    return f"hvc1.1.6.L{native().hevc_level(width, height, fps)}.B0"
+
+
+def codec_string(codec: str, width: int, height: int, fps: int) -> str:
+    return hevc_codec_string(width, height, fps) if codec == "hevc" else h264_codec_string(width, height, fps)
 
 
 def h264_codec_string(width: int, height: int, fps: int) -> str:
@@ -84,7 +96,11 @@ class StreamPipeline:
                  bitrate_kbps: int = 8000, keyint: int = 0, search_range: int = 16, subpel: bool = True,
                  noise: bool = True, out_width: int = 0, out_height: int = 0, session_name: str = "0",
                  capture: Any = None, metrics: SessionMetrics | None = None, queue_frames: int = 8,
-                 stall_s: float = 2.0, paced: bool = True):
+                 stall_s: float = 2.0, paced: bool = True, codec: str = "h264"):
+        if codec not in ("h264", "hevc"):
+            raise ValueError(f"unknown codec {codec!r} (h264 | hevc)")
+        self.codec = codec
+        self.codec_id = 2 if codec == "hevc" else 1
         self.width, self.height, self.fps = width, height, fps
         self.out_w = out_width or width
         self.out_h = out_height or height
@@ -137,6 +153,7 @@ class StreamPipeline:
             cfg.enc.keyint = a["keyint"]
             cfg.enc.search_range = a["search_range"]
             cfg.enc.subpel = 1 if a["subpel"] else 0
+            cfg.codec = self.codec
             self._sess = N.Session(cfg)
             self._cpu = None
         elif self.backend == "cpu":
@@ -151,7 +168,7 @@ class StreamPipeline:
             ec.keyint = a["keyint"]
             ec.search_range = min(a["search_range"], 4)  # keep the serial encoder real-time
             ec.subpel = 0
-            self._cpu = N.CpuH264Encoder(ec)
+            self._cpu = N.CpuHevcEncoder(ec) if self.codec == "hevc" else N.CpuH264Encoder(ec)
             self._desk = CpuSyntheticDesktop(self.width, self.height, a["noise"])
             self._sess = None
             self._cpu_frame = 0
@@ -174,7 +191,7 @@ class StreamPipeline:
             else:
                 r = s.step(force_idr)
             return EncodedFrame(r.frame_id, r.t_capture_us, r.t_encoded_us, bool(r.idr), r.qp, r.au, self.out_w,
-                                self.out_h, r.gpu_ms)
+                                self.out_h, r.gpu_ms, self.codec_id)
         t_cap = native().now_us()
         fid = self._cpu_frame
         self._cpu_frame += 1
@@ -184,7 +201,8 @@ class StreamPipeline:
         y, uv = bgrx_to_nv12(img)
         au = self._cpu.encode(y, uv, force_idr)
         st = self._cpu.stats
-        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, self.width, self.height)
+        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, self.width, self.height,
+                            codec_id=self.codec_id)
 
     # ------------------------------------------------------------------ control
     def request_idr(self) -> None:
@@ -292,7 +310,7 @@ def frame_header(fr: EncodedFrame, t_send_us: int) -> bytes:
     """Binary media header of the WebSocket transport (36 bytes, little endian)."""
     import struct
 
-    return struct.pack("<4sBBHIQQHHI", b"MXV1", 1 if fr.idr else 0, 1, 0, fr.frame_id & 0xFFFFFFFF,
+    return struct.pack("<4sBBHIQQHHI", b"MXV1", 1 if fr.idr else 0, fr.codec_id, 0, fr.frame_id & 0xFFFFFFFF,
                        fr.t_capture_us, t_send_us, fr.width, fr.height, len(fr.au))
 
 

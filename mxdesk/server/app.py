@@ -28,7 +28,7 @@ from typing import Any
 
 from aiohttp import WSMsgType, web
 
-from ..pipeline.stream import StreamPipeline, frame_header, h264_codec_string
+from ..pipeline.stream import StreamPipeline, codec_string, frame_header
 from . import turn
 from .auth import basic_auth_middleware
 from .input import SyntheticInjector, parse_message
@@ -176,7 +176,7 @@ class MediaServer:
         from ..audio.pipeline import CHANNELS, RATE
 
         await ws.send_str(json.dumps({
-            "type": "config", "codec": h264_codec_string(p.out_w, p.out_h, p.fps), "width": p.out_w,
+            "type": "config", "codec": codec_string(getattr(p, "codec", "h264"), p.out_w, p.out_h, p.fps), "width": p.out_w,
             "height": p.out_h, "fps": p.fps, "resize": self.resize_enabled,
             "audio": {"codec": "pcm_s16le", "rate": RATE, "channels": CHANNELS} if want_audio else None,
         }))

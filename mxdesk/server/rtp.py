@@ -60,6 +60,46 @@ class H264Depacketizer:
         return None
 
 
+class H265Depacketizer:
+    """Reassembles Annex-B access units from RFC 7798 packets (single NAL, AP, FU; no DONL)."""
+
+    def __init__(self):
+        self.nals: list[bytes] = []
+        self.fu: bytearray | None = None
+        self.last_seq: int | None = None
+        self.lost = 0
+
+    def push(self, pkt: bytes) -> bytes | None:
+        h = rtp_header(pkt)
+        if self.last_seq is not None and ((h["seq"] - self.last_seq) & 0xFFFF) != 1:
+            self.lost += 1
+        self.last_seq = h["seq"]
+        p = h["payload"]
+        t = (p[0] >> 1) & 0x3F
+        if t < 48:
+            self.nals.append(p)
+        elif t == 48:  # aggregation packet
+            off = 2
+            while off + 2 <= len(p):
+                n = struct.unpack_from("!H", p, off)[0]
+                self.nals.append(p[off + 2: off + 2 + n])
+                off += 2 + n
+        elif t == 49:  # fragmentation unit
+            fu = p[2]
+            if fu & 0x80:
+                self.fu = bytearray([(p[0] & 0x81) | ((fu & 0x3F) << 1), p[1]])
+            if self.fu is not None:
+                self.fu += p[3:]
+                if fu & 0x40:
+                    self.nals.append(bytes(self.fu))
+                    self.fu = None
+        if h["marker"]:
+            au = b"".join(b"\x00\x00\x00\x01" + n for n in self.nals)
+            self.nals = []
+            return au
+        return None
+
+
 def ntp_now() -> tuple[int, int]:
     t = time.time() + NTP_EPOCH_OFFSET
     sec = int(t)

@@ -106,6 +106,17 @@ def pick_h264(md: MediaDesc) -> str | None:
     return best
 
 
+def pick_h265(md: MediaDesc) -> str | None:
+    """Payload type of an H.265 (RFC 7798) codec whose profile is Main (profile-id 1 or
+    absent) for our Main-profile HEVC stream."""
+    for pt in [r.split()[0] for r in md.attrs_named("rtpmap") if re.search(r"\sH265/90000", r, re.I)]:
+        fmtp = next((f[len(pt) + 1:] for f in md.attrs_named("fmtp") if f.split()[0] == pt), "")
+        params = dict(kv.strip().split("=", 1) for kv in fmtp.split(";") if "=" in kv)
+        if params.get("profile-id", "1") == "1" and params.get("tx-mode", "SRST").upper() == "SRST":
+            return pt
+    return None
+
+
 @dataclass
 class Answer:
     sdp: str
@@ -123,10 +134,18 @@ def _has_pcmu(md: MediaDesc) -> bool:
 
 
 def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
-                 level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None) -> Answer:
-    """Answer one H.264 video section (and, with ``audio_ssrc``, one PCMU audio section);
-    everything else is rejected with port 0.  All accepted sections are BUNDLEd onto the
-    single ICE-lite host candidate."""
+                 level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None,
+                 codec: str = "h264") -> Answer:
+    """Answer one video section in the stream's codec (H.264 packetization-mode 1, or H.265
+    with ``codec="hevc"``; ``level_idc`` is then general_level_idc) and, with ``audio_ssrc``,
+    one PCMU audio section; everything else is rejected with port 0.  All accepted sections
+    are BUNDLEd onto the single ICE-lite host candidate."""
+    pick = pick_h265 if codec == "hevc" else pick_h264
+    if codec == "hevc":
+        rtpmap, fmtp = "H265/90000", f"profile-id=1;tier-flag=0;level-id={level_idc};tx-mode=SRST"
+    else:
+        rtpmap = "H264/90000"
+        fmtp = f"level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}"
     offer = parse_sdp(offer_text)
     lines = ["v=0", f"o=mxdesk {secrets.randbelow(1 << 62)} 2 IN IP4 {host}", "s=mxdesk", "t=0 0", "a=ice-lite",
              "a=msid-semantic: WMS mxdesk"]
@@ -140,7 +159,7 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
                  f"a=ice-ufrag:{ice_ufrag}", f"a=ice-pwd:{ice_pwd}", f"a=fingerprint:{fingerprint}", "a=setup:passive"]
     for md in offer.media:
         mid = md.attr("mid") or str(len(bundle) + len(out_media))
-        pt = pick_h264(md) if (md.kind == "video" and chosen is None) else None
+        pt = pick(md) if (md.kind == "video" and chosen is None) else None
         ufrag = md.attr("ice-ufrag") or offer.attr("ice-ufrag")
         pwd = md.attr("ice-pwd") or offer.attr("ice-pwd")
         fp = md.attr("fingerprint") or offer.attr("fingerprint")
@@ -149,9 +168,8 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
             bundle.append(mid)
             out_media += [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport,
                           f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtcp-rsize",
-                          f"a=rtpmap:{pt} H264/90000", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
-                          f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb",
-                          f"a=fmtp:{pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}",
+                          f"a=rtpmap:{pt} {rtpmap}", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
+                          f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb", f"a=fmtp:{pt} {fmtp}",
                           f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
             continue
         if md.kind == "audio" and audio is None and audio_ssrc is not None and _has_pcmu(md):
@@ -165,7 +183,8 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
         out_media += [f"m={md.kind} 0 {md.proto} {md.fmts[0] if md.fmts else '0'}", "c=IN IP4 0.0.0.0",
                       f"a=mid:{mid}", "a=inactive"]
     if chosen is None:
-        raise ValueError("offer has no H.264 (packetization-mode=1, baseline-compatible) video section")
+        raise ValueError("offer has no H.265 (Main profile) video section" if codec == "hevc" else
+                         "offer has no H.264 (packetization-mode=1, baseline-compatible) video section")
     if audio is not None:
         chosen.audio_pt, chosen.audio_mid = audio
     lines.insert(4, "a=group:BUNDLE " + " ".join(bundle))
@@ -277,9 +296,15 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.transport, _ = await loop.create_datagram_endpoint(lambda: self,
                                                                 local_addr=(self.bind_host, self.bind_port))
         port = self.transport.get_extra_info("sockname")[1]
+        codec = getattr(self.pipeline, "codec", "h264")
+        level = self.level_idc
+        if codec == "hevc":
+            p = self.pipeline
+            level = _native().hevc_level(p.out_w, p.out_h, p.fps)
         self.answer = build_answer(self.offer_sdp, self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port,
-                                   self.ssrc, self.level_idc, self.audio_ssrc, self.extra_hosts)
-        self.pkt = _native().net.RtpH264Packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
+                                   self.ssrc, level, self.audio_ssrc, self.extra_hosts, codec=codec)
+        packetizer = _native().net.RtpH265Packetizer if codec == "hevc" else _native().net.RtpH264Packetizer
+        self.pkt = packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
         self.tasks.append(asyncio.create_task(self._timers()))
         return self.answer.sdp
 

@@ -22,7 +22,8 @@ def _native():
     return native()
 
 
-def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_audio: bool = True) -> str:
+def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_audio: bool = True,
+               h265_pt: int = 104) -> str:
     lines = ["v=0", "o=- 4611731400430051336 2 IN IP4 127.0.0.1", "s=-", "t=0 0", "a=group:BUNDLE 0 1",
              "a=msid-semantic: WMS"]
     media = []
@@ -30,12 +31,14 @@ def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_
         media += ["m=audio 9 UDP/TLS/RTP/SAVPF 111 0", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
                   f"a=ice-pwd:{pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:1", "a=recvonly",
                   "a=rtcp-mux", "a=rtpmap:111 opus/48000/2", "a=rtpmap:0 PCMU/8000"]
-    media = ["m=video 9 UDP/TLS/RTP/SAVPF 96 %d 108" % h264_pt, "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
+    media = ["m=video 9 UDP/TLS/RTP/SAVPF 96 %d 108 %d" % (h264_pt, h265_pt), "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
              f"a=ice-pwd:{pwd}", "a=ice-options:trickle", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:0",
              "a=recvonly", "a=rtcp-mux", "a=rtcp-rsize", "a=rtpmap:96 VP8/90000",
              f"a=rtpmap:{h264_pt} H264/90000", f"a=rtcp-fb:{h264_pt} nack", f"a=rtcp-fb:{h264_pt} nack pli",
              f"a=fmtp:{h264_pt} level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e01f",
-             "a=rtpmap:108 H264/90000", "a=fmtp:108 packetization-mode=0;profile-level-id=42e01f"] + media
+             "a=rtpmap:108 H264/90000", "a=fmtp:108 packetization-mode=0;profile-level-id=42e01f",
+             f"a=rtpmap:{h265_pt} H265/90000", f"a=rtcp-fb:{h265_pt} nack", f"a=rtcp-fb:{h265_pt} nack pli",
+             f"a=fmtp:{h265_pt} profile-id=1;tier-flag=0;level-id=186;tx-mode=SRST"] + media
     return "\r\n".join(lines + media) + "\r\n"
 
 
@@ -139,7 +142,8 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
         tx = N.net.SrtpSession(km[0:16], km[32:46])   # client -> server (RTCP)
         res.connect_ms = (time.monotonic() - t0) * 1000
         my_ssrc = secrets.randbits(32)
-        depk = R.H264Depacketizer()
+        hevc = " H265/90000" in res.answer
+        depk = R.H265Depacketizer() if hevc else R.H264Depacketizer()
         pending: dict[int, bytes] = {}
         next_seq = None
         n_pkts = 0

@@ -35,7 +35,7 @@ def parse_bool(v: Any, default: bool = False) -> bool:
 
 
 # Encoder names accepted by WEBRTC_ENCODER.  The reference's nvh264enc (NVENC) and the
-# VA-API names map to the HIP encoder; x264enc (CPU) maps to the CPU encoder.
+# VA-API names map to the HIP encoders; x264enc / x265enc (CPU) map to the CPU encoders.
 ENCODER_ALIASES = {
     "nvh264enc": "mxh264enc",
     "vah264enc": "mxh264enc",
@@ -44,8 +44,15 @@ ENCODER_ALIASES = {
     "x264enc": "cpuh264enc",
     "openh264enc": "cpuh264enc",
     "cpuh264enc": "cpuh264enc",
+    "nvh265enc": "mxh265enc",
+    "vah265enc": "mxh265enc",
+    "vaapih265enc": "mxh265enc",
+    "mxh265enc": "mxh265enc",
+    "x265enc": "cpuh265enc",
+    "cpuh265enc": "cpuh265enc",
 }
-UNSUPPORTED_ENCODERS = {"vp8enc", "vp9enc", "nvh265enc", "vah265enc", "x265enc", "av1enc"}
+GPU_ENCODERS = {"mxh264enc", "mxh265enc"}
+UNSUPPORTED_ENCODERS = {"vp8enc", "vp9enc", "av1enc"}
 
 
 @dataclass
@@ -177,10 +184,20 @@ class Config:
     def encoder_backend(self) -> str:
         name = str(self.values["encoder"]).strip().lower()
         if name in UNSUPPORTED_ENCODERS:
-            raise ValueError(f"WEBRTC_ENCODER={name} is not implemented yet (H.264 only: mxh264enc / cpuh264enc)")
+            raise ValueError(f"WEBRTC_ENCODER={name} is not implemented yet (H.264 / HEVC: mxh264enc, "
+                             "mxh265enc, x264enc, x265enc)")
         if name not in ENCODER_ALIASES:
             raise ValueError(f"unknown WEBRTC_ENCODER={name}")
         return ENCODER_ALIASES[name]
+
+    @property
+    def codec(self) -> str:
+        """Bitstream format of the selected encoder: "h264" or "hevc"."""
+        return "hevc" if "265" in self.encoder_backend else "h264"
+
+    @property
+    def gpu_encoder(self) -> bool:
+        return self.encoder_backend in GPU_ENCODERS
 
     @property
     def stream_fps(self) -> int:

@@ -30,6 +30,8 @@ def free_port():
 def make_server(env=None, **kw):
     cfg = C.load(env={"WEBRTC_ENCODER": "x264enc", "SIZEW": "320", "SIZEH": "96", "REFRESH": "30",
                       **(env or {})}, argv=[])
+    if kw.get("codec", "h264") is None:
+        kw["codec"] = cfg.codec
     pipe = StreamPipeline(cfg.sizew, cfg.sizeh, cfg.stream_fps, backend="cpu", bitrate_kbps=0, **kw)
     return cfg, pipe, MediaServer(pipe, cfg)
 
@@ -186,3 +188,26 @@ def test_slow_client_resync():
     sub, got = run(go())
     assert sub.dropped > 0 and sub.need_idr  # backlog dropped, waiting for the next IDR
     assert pipe.metrics.dropped.labels("0")._value.get() > 0
+
+
+def test_hevc_stream_over_websocket():
+    from mxdesk.codec.hevc_decoder import Decoder as HevcDecoder
+
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "WEBRTC_ENCODER": "x265enc"}, codec=None)
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await view(f"http://127.0.0.1:{port}/mxws", 4)
+        finally:
+            await runner.cleanup()
+
+    assert cfg.codec == "hevc" and pipe.codec == "hevc"
+    res = run(go())
+    assert res.config["codec"].startswith("hvc1.1.6.L") and res.config["codec"].endswith(".B0")
+    assert all(f["codec"] == 2 for f in res.frames)
+    frames = HevcDecoder().decode(res.stream)
+    assert len(frames) == 4
+    for (y, _, _), meta in zip(frames, res.frames):
+        assert read_barcode(y)[0] == meta["frame_id"]
