@@ -1117,23 +1117,48 @@ MXHD void decide_inter(CuInfo& c, MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
     c.mvdy = (int16_t)(c.mvy - ly[idx]);
 }
 
-// Neighbour candidates of CU (x, y) in a picture of ctb_w CTUs whose slices are
-// slice_rows CTU rows tall; mv: per-CU quarter-pel motion, (x, y) at mv[i*stride], mv[i*stride+1].
-MXHD void inter_neighbours(const int16_t* mv, int stride, int x, int y, int ctb_w, int slice_rows, MvCand* a1,
+// Neighbour candidates of CU i = (x, y) in a picture of ctb_w CTUs whose slice starts at CU
+// `first` (slices are raster runs, so an earlier CU j is in the same slice iff j >= first);
+// mv: per-CU quarter-pel motion, (x, y) at mv[i*stride], mv[i*stride+1].
+MXHD void inter_neighbours(const int16_t* mv, int stride, int x, int y, int ctb_w, int first, MvCand* a1,
                            MvCand* b1, MvCand* b0, MvCand* b2) {
-    const bool up = (y % slice_rows) != 0;  // row above is in the same slice
-    auto at = [&](bool ok, int cx, int cy) {
+    const int i = y * ctb_w + x;
+    auto at = [&](bool ok, int j) {
         MvCand c{ok, 0, 0};
         if (ok) {
-            c.x = mv[(size_t)(cy * ctb_w + cx) * stride];
-            c.y = mv[(size_t)(cy * ctb_w + cx) * stride + 1];
+            c.x = mv[(size_t)j * stride];
+            c.y = mv[(size_t)j * stride + 1];
         }
         return c;
     };
-    *a1 = at(x > 0, x - 1, y);
-    *b1 = at(up, x, y - 1);
-    *b0 = at(up && x + 1 < ctb_w, x + 1, y - 1);
-    *b2 = at(up && x > 0, x - 1, y - 1);
+    *a1 = at(x > 0 && i - 1 >= first, i - 1);
+    *b1 = at(i - ctb_w >= first, i - ctb_w);
+    *b0 = at(x + 1 < ctb_w && i - ctb_w + 1 >= first, i - ctb_w + 1);
+    *b2 = at(x > 0 && i - ctb_w - 1 >= first, i - ctb_w - 1);
+}
+
+// ---------------------------------------------------------------- adaptive slice layout (P)
+// Entropy-coding cost estimate of a CU in CABAC work units: significance bins up to the
+// last position of every coded TU plus a few bins per coded sub-block, on top of the CU
+// header.  Used only to balance slices; identical on the CPU and the GPU.
+MXHD uint32_t cu_cost(const CuInfo& c) {
+    uint32_t k = 4;
+    if (c.cbf & 1) k += c.last[0] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_y);
+    if (c.cbf & 2) k += c.last[1] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_c[0]);
+    if (c.cbf & 4) k += c.last[2] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_c[1]);
+    return k;
+}
+constexpr uint32_t kCostPerSlice = 4096;  // below this much work per slice, fewer slices
+// Number of slices for a P picture of total cost T, bounded by the level's slice limit.
+MXHD int plan_num_slices(uint64_t total, int max_slices) {
+    const uint64_t s = total / kCostPerSlice;
+    return s < 1 ? 1 : (s > (uint64_t)max_slices ? max_slices : (int)s);
+}
+// Slice of a CU whose exclusive cost prefix is `pre`: floor(pre * S / T) -- non-decreasing in
+// raster order, so every slice is a raster run and equal-cost runs share the work evenly.
+MXHD int plan_slice_of(uint64_t pre, uint64_t total, int S) {
+    const uint64_t id = pre * (uint64_t)S / total;
+    return id >= (uint64_t)S ? S - 1 : (int)id;
 }
 
 }  // namespace hevc

@@ -99,6 +99,29 @@ HevcCommon::HevcCommon(const EncoderConfig& c) : rc_(c) {
     slice_rows_ = 1;
     while ((ctb_h() + slice_rows_ - 1) / slice_rows_ > maxs) ++slice_rows_;
     if (num_slices() > kMaxSlices) throw std::invalid_argument("hevc: too many slices");
+    max_slices_ = std::min({maxs, kMaxSlices, ctb_w() * ctb_h()});
+}
+
+std::vector<int> HevcCommon::row_slices() const {
+    std::vector<int> f;
+    for (int s = 0; s < num_slices(); ++s) f.push_back(s * slice_rows_ * ctb_w());
+    return f;
+}
+
+std::vector<int> HevcCommon::plan_p_slices(const std::vector<CuInfo>& cus) const {
+    uint64_t total = 0;
+    for (const auto& c : cus) total += cu_cost(c);
+    const int S = plan_num_slices(total, max_slices_);
+    std::vector<int> f;
+    uint64_t pre = 0;
+    int prev = -1;
+    for (size_t i = 0; i < cus.size(); ++i) {
+        const int id = plan_slice_of(pre, total, S);
+        if (id != prev) f.push_back((int)i);
+        prev = id;
+        pre += cu_cost(cus[i]);
+    }
+    return f;
 }
 
 void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
@@ -231,10 +254,9 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
     }
 }
 
-void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int slice, bool idr, int poc, int qp,
+void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp,
                                  const uint8_t* data, size_t n) const {
     const int ctbs = ctb_w() * ctb_h();
-    const int addr = slice * slice_rows_ * ctb_w();
     Bits w;
     w.put(addr == 0, 1);  // first_slice_segment_in_pic_flag
     if (idr) w.put(0, 1);  // no_output_of_prior_pics_flag
@@ -415,12 +437,16 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
             }
             summarise(c, co);
         }
-    for (int y = 0; y < H; ++y)
-        for (int x = 0; x < W; ++x) {
-            MvCand a1, b1, b0, b2;
-            inter_neighbours(mv_.data(), 2, x, y, W, sr, &a1, &b1, &b0, &b2);
-            decide_inter(cu_[y * W + x], a1, b1, b0, b2);
-        }
+    // cost-balanced slices, then the merge / AMVP decisions against each slice's neighbours
+    slices_ = common_.plan_p_slices(cu_);
+    int s = 0;
+    for (int i = 0; i < W * H; ++i) {
+        while (s + 1 < (int)slices_.size() && slices_[s + 1] <= i) ++s;
+        MvCand a1, b1, b0, b2;
+        inter_neighbours(mv_.data(), 2, i % W, i / W, W, slices_[s], &a1, &b1, &b0, &b2);
+        decide_inter(cu_[i], a1, b1, b0, b2);
+    }
+    (void)sr;
 }
 
 const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
@@ -430,22 +456,24 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     const int qp = rc.cur_qp();
     if (have_ref_) cur_ ^= 1;
     have_ref_ = true;
-    if (idr)
+    if (idr) {
         analyse_intra(y, uv, pitch);
-    else
+        slices_ = common_.row_slices();
+    } else {
         analyse_inter(y, uv, pitch);
+    }
     au_.clear();
     if (idr) common_.write_parameter_sets(au_);
-    const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
+    const int W = common_.ctb_w(), H = common_.ctb_h();
     std::vector<uint8_t> buf;
     uint8_t ctx[C_NUM];
-    for (int s = 0; s < common_.num_slices(); ++s) {
-        const int first = s * sr * W, count = std::min(sr, H - s * sr) * W;
+    for (size_t s = 0; s < slices_.size(); ++s) {
+        const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
         const uint32_t cap = (uint32_t)count * 1024 + 1024;
         buf.resize(cap);
         const uint32_t n = code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count, W, ctx);
         if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
-        common_.write_slice_nal(au_, s, idr, idr ? 0 : common_.poc(), qp, buf.data(), n);
+        common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n);
     }
     // distortion over the display area
     const EncoderConfig& c = common_.config();

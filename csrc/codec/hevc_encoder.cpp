@@ -15,7 +15,7 @@ namespace hevc {
 
 void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     const int ncu = geom_.mb_w * geom_.mb_h;
-    const int ns = common_.num_slices();
+    const int ns = common_.max_slices();
     HevcDeviceBuffers& b = sl.buf;
     HIP_CHECK(hipMalloc(&b.fs, sizeof(HevcFrameState)));
     HIP_CHECK(hipMalloc(&b.me.fs, sizeof(h264::FrameState)));
@@ -23,10 +23,15 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMemsetAsync(b.me.mb, 0, sizeof(h264::MbInfo) * ncu, stream_));
     HIP_CHECK(hipMalloc(&b.cu, sizeof(CuInfo) * ncu));
     HIP_CHECK(hipMalloc(&b.coef, sizeof(int16_t) * kCoefPerCu * (size_t)ncu));
-    // per-slice CABAC output slot: 1 KiB per CTU (dense intra at QP 0 stays below)
-    b.slice_cap = (uint32_t)(((size_t)common_.slice_rows() * geom_.mb_w * 1024 + 15) & ~(size_t)15);
+    // per-slice CABAC output slot: room for 1 KiB per CTU of an even share of the picture plus
+    // one CTU row (slices are cost-balanced, so a slice of many cheap CTUs stays small)
+    const size_t ctus_per_slot = (size_t)(ncu + ns - 1) / ns + (size_t)common_.slice_rows() * geom_.mb_w;
+    b.slice_cap = (uint32_t)((ctus_per_slot * 1024 + 15) & ~(size_t)15);
     HIP_CHECK(hipMalloc(&b.slice_data, (size_t)b.slice_cap * ns));
     HIP_CHECK(hipMalloc(&b.slice_len, sizeof(uint32_t) * ns));
+    HIP_CHECK(hipMalloc(&b.slice_first, sizeof(int) * ns));
+    HIP_CHECK(hipMalloc(&b.slice_of_cu, sizeof(int) * ncu));
+    HIP_CHECK(hipMalloc(&b.nslices, sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
@@ -42,7 +47,8 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
 void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
-                    (void*)b.slice_len, (void*)b.sse_part})
+                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices,
+                    (void*)b.sse_part})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.me_fs_host) (void)hipHostFree(sl.me_fs_host);
@@ -158,7 +164,7 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
         HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
         es = stream_e_;
     }
-    launch_hevc_entropy(geom_, sl.buf, common_.num_slices(), sl.host_out, es);
+    launch_hevc_entropy(geom_, sl.buf, idr, common_.max_slices(), sl.host_out, es);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -195,12 +201,13 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     }
     const uint32_t* soff = reinterpret_cast<const uint32_t*>(sl.host_out + sizeof(HevcOutHeader));
     const uint32_t* slen = soff + kMaxSlices;
+    const uint32_t* saddr = soff + 2 * kMaxSlices;
     const uint8_t* payload = sl.host_out + kOutPayloadOffset;
     au_.clear();
     au_.reserve(hdr.total_bytes + hdr.total_bytes / 64 + 64 * hdr.num_slices + 256);
     if (sl.idr) common_.write_parameter_sets(au_);
     for (uint32_t k = 0; k < hdr.num_slices; ++k)
-        common_.write_slice_nal(au_, (int)k, sl.idr, sl.poc, sl.qp, payload + soff[k], slen[k]);
+        common_.write_slice_nal(au_, (int)saddr[k], sl.idr, sl.poc, sl.qp, payload + soff[k], slen[k]);
     stats_.frame_index = rc.frames();
     stats_.idr = sl.idr;
     stats_.qp = sl.qp;

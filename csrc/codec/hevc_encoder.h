@@ -39,17 +39,24 @@ class HevcCommon {
     int slice_rows() const { return slice_rows_; }
     int num_slices() const { return (ctb_h() + slice_rows_ - 1) / slice_rows_; }
     int level_idc() const { return level_; }
+    int max_slices() const { return max_slices_; }  // level limit (MaxSliceSegmentsPerPicture), capped
     // POC LSB (8 bits) of the current frame = frames since the last IDR.
     int poc() const { return rc_.cur_frame_num(); }
     void write_parameter_sets(std::vector<uint8_t>& out) const;
-    // One slice segment NAL: start code, NAL header, header + payload with emulation prevention.
-    void write_slice_nal(std::vector<uint8_t>& out, int slice, bool idr, int poc, int qp, const uint8_t* data,
+    // One slice segment NAL (slice starting at CTU `addr`): start code, NAL header, header +
+    // payload with emulation prevention.
+    void write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp, const uint8_t* data,
                          size_t n) const;
+    // Slice layout: I pictures one slice per slice_rows() CTU rows (the intra wavefront needs a
+    // fixed layout), P pictures cost-balanced raster runs (plan_p_slices).  Returns first CTUs.
+    std::vector<int> row_slices() const;
+    std::vector<int> plan_p_slices(const std::vector<CuInfo>& cus) const;
 
    private:
     h264::EncoderCommon rc_;
     int slice_rows_ = 1;
     int level_ = 0;
+    int max_slices_ = 1;
 };
 
 class CpuHevcEncoder {
@@ -77,6 +84,7 @@ class CpuHevcEncoder {
     bool have_ref_ = false;
     std::vector<CuInfo> cu_;
     std::vector<int16_t> mv_;  // per CU (x, y)
+    std::vector<int> slices_;  // first CTU of every slice of the current picture
     std::vector<int16_t> coef_;
     std::vector<uint8_t> au_;
     FrameStats stats_;
@@ -84,9 +92,10 @@ class CpuHevcEncoder {
 
 // ---------------------------------------------------------------- GPU encoder
 // Per-frame kernel chain (hevc_kernels.hip):
-//   P: k_hpel -> k_me_full (shared with H.264) -> k_hevc_inter -> k_hevc_decide
+//   P: k_hpel -> k_me_full (shared with H.264) -> k_hevc_inter
 //   I: k_hevc_intra (one workgroup per slice, wavefront over its CTU rows)
-//   then k_hevc_cabac (one wave per slice) -> k_hevc_pack (zero-copy into pinned memory)
+//   then k_hevc_layout (slices: rows for I, cost-balanced runs for P) -> k_hevc_decide (P:
+//   skip/merge/AMVP per slice) -> k_hevc_cabac (one wave per slice) -> k_hevc_pack
 struct HevcFrameState {
     const uint8_t* ref_y;
     const uint8_t* ref_uv;
@@ -115,16 +124,20 @@ struct HevcOutHeader {
 static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
 constexpr int kMaxSliceRows = 4;  // CTU rows per slice the intra wavefront kernel supports
-constexpr size_t kOutPayloadOffset = sizeof(HevcOutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
+// host buffer: header | slice payload offset[kMaxSlices] | length[] | first CTU[] | payloads
+constexpr size_t kOutPayloadOffset = sizeof(HevcOutHeader) + 3 * kMaxSlices * sizeof(uint32_t);
 
 struct HevcDeviceBuffers {
     HevcFrameState* fs;
     h264::DeviceBuffers me;  // H.264 ME state (frame state + MbInfo with the motion vectors)
     CuInfo* cu;
     int16_t* coef;
-    uint8_t* slice_data;     // [num_slices * slice_cap]
-    uint32_t* slice_len;     // [num_slices]
+    uint8_t* slice_data;     // [max_slices * slice_cap]
+    uint32_t* slice_len;     // [max_slices]
     uint32_t slice_cap;
+    int* slice_first;        // [max_slices] first CTU of every slice (k_hevc_layout)
+    int* slice_of_cu;        // [ncu]
+    uint32_t* nslices;       // slice count of the frame
     size_t out_bytes;
     unsigned long long* sse_part;
 };
@@ -133,7 +146,7 @@ void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint
                        hipStream_t s);
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
-void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int num_slices, uint8_t* host_out,
+void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, uint8_t* host_out,
                          hipStream_t s);
 
 class GpuHevcEncoder final : public VideoEncoder {

@@ -386,11 +386,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         c.mvdx = c.mvdy = 0;
         c.mvp_idx = 0;
         fill_cu(c, r);
-        MvCand a1, b1, b0, b2;
-        constexpr int kStride = sizeof(h264::MbInfo) / sizeof(int16_t);
-        inter_neighbours(&mbs[0].mvx, kStride, x, y, g.mb_w, fs->slice_rows, &a1, &b1, &b0, &b2);
-        decide_inter(c, a1, b1, b0, b2);
-        cus[i] = c;
+        cus[i] = c;  // skip / merge / AMVP are decided by k_hevc_decide once the slices are laid out
     }
     __syncthreads();
     if (threadIdx.x < 3) {
@@ -584,6 +580,85 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         fs->sse_part[lane * h264::kSsePartStride + y] = lane == 0 ? acc[0] : (lane == 1 ? acc[1] : acc[2]);
 }
 
+// ------------------------------------------------------------------ slice layout
+// One 1024-thread workgroup.  I pictures: fixed slices of slice_rows CTU rows.  P pictures:
+// cost-balanced raster runs (hevc_core.h plan_*): block prefix sum of cu_cost, slice id of
+// every CU from its exclusive prefix, starts compacted by a second scan.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+    const int t = threadIdx.x, n = blockDim.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < n; o <<= 1) {
+        const uint32_t add = t >= o ? sh[t - o] : 0u;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    const uint32_t incl = sh[t];
+    *total = sh[n - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
+                                                       const CuInfo* __restrict__ cus, int ncu, int ctb_w,
+                                                       int max_slices, int* __restrict__ slice_first,
+                                                       int* __restrict__ slice_of_cu, uint32_t* __restrict__ nslices) {
+    __shared__ uint32_t sh[1024];
+    const int tid = threadIdx.x;
+    if (fs->idr) {
+        const int sr = fs->slice_rows, S = fs->num_slices;
+        for (int k = tid; k < S; k += blockDim.x) slice_first[k] = k * sr * ctb_w;
+        for (int i = tid; i < ncu; i += blockDim.x) slice_of_cu[i] = (i / ctb_w) / sr;
+        if (tid == 0) *nslices = (uint32_t)S;
+        return;
+    }
+    const int chunk = (ncu + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int i0 = min(ncu, tid * chunk), i1 = min(ncu, i0 + chunk);
+    uint32_t local = 0;
+    for (int i = i0; i < i1; ++i) local += cu_cost(cus[i]);
+    uint32_t total;
+    const uint32_t pre0 = block_excl_scan(local, sh, &total);
+    const int S = plan_num_slices(total, max_slices);
+    // starts in this chunk
+    int prev = i0 > 0 ? plan_slice_of(pre0 - cu_cost(cus[i0 - 1]), total, S) : -1;
+    uint32_t pre = pre0, nst = 0;
+    for (int i = i0; i < i1; ++i) {
+        const int id = plan_slice_of(pre, total, S);
+        nst += id != prev;
+        prev = id;
+        pre += cu_cost(cus[i]);
+    }
+    uint32_t nstarts;
+    const uint32_t base = block_excl_scan(nst, sh, &nstarts);
+    prev = i0 > 0 ? plan_slice_of(pre0 - cu_cost(cus[i0 - 1]), total, S) : -1;
+    pre = pre0;
+    int rank = (int)base - 1;
+    for (int i = i0; i < i1; ++i) {
+        const int id = plan_slice_of(pre, total, S);
+        if (id != prev) slice_first[++rank] = i;
+        slice_of_cu[i] = rank;
+        prev = id;
+        pre += cu_cost(cus[i]);
+    }
+    if (tid == 0) *nslices = nstarts;
+}
+
+// Skip / merge / AMVP of every CU of a P picture against its slice's neighbours.
+__global__ __launch_bounds__(256) void k_hevc_decide(Geometry g, const h264::MbInfo* __restrict__ mbs,
+                                                      const int* __restrict__ slice_first,
+                                                      const int* __restrict__ slice_of_cu, CuInfo* __restrict__ cus) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.mb_w * g.mb_h) return;
+    constexpr int kStride = sizeof(h264::MbInfo) / sizeof(int16_t);
+    MvCand a1, b1, b0, b2;
+    inter_neighbours(&mbs[0].mvx, kStride, i % g.mb_w, i / g.mb_w, g.mb_w, slice_first[slice_of_cu[i]], &a1, &b1, &b0,
+                     &b2);
+    CuInfo c = cus[i];
+    decide_inter(c, a1, b1, b0, b2);
+    cus[i] = c;
+}
+
 // ------------------------------------------------------------------ CABAC
 // The whole wave runs the slice coder in lockstep on identical (wave-uniform) values, so
 // the arithmetic-coder state lives in SGPRs and every table lookup is a register read:
@@ -645,11 +720,14 @@ __device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
 __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameState* __restrict__ fs,
                                                     const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
                                                     uint8_t* __restrict__ slice_data, uint32_t slice_cap,
-                                                    uint32_t* __restrict__ slice_len) {
+                                                    uint32_t* __restrict__ slice_len,
+                                                    const int* __restrict__ slice_first,
+                                                    const uint32_t* __restrict__ nslices) {
     const int s = blockIdx.x, lane = threadIdx.x;
-    const int sr = fs->slice_rows;
-    const int rows = min(sr, g.mb_h - s * sr);
-    const int first = s * sr * g.mb_w, count = rows * g.mb_w;
+    const int ns = (int)*nslices;
+    if (s >= ns) return;
+    const int first = slice_first[s];
+    const int count = (s + 1 < ns ? slice_first[s + 1] : g.mb_w * g.mb_h) - first;
     const bool islice = fs->idr != 0;
     const int qp = fs->qp;
     LaneCtx ctx;
@@ -709,13 +787,17 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
 }
 
 // ------------------------------------------------------------------ pack
-__global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restrict__ fs, int num_slices,
+__global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restrict__ fs,
+                                                    const uint32_t* __restrict__ nslices,
+                                                    const int* __restrict__ slice_first,
                                                     const uint8_t* __restrict__ slice_data,
                                                     uint32_t slice_cap, const uint32_t* __restrict__ slice_len,
                                                     uint8_t* __restrict__ host_out, size_t out_bytes) {
     __shared__ uint32_t red[256];
     __shared__ unsigned long long red64[3][256];
     const int s = blockIdx.x, tid = threadIdx.x;
+    const int num_slices = (int)*nslices;
+    if (s >= num_slices) return;
     // offset of this slice: sum of the 16-byte rounded lengths before it
     uint32_t part = 0;
     for (int k = tid; k < s; k += 256) part += (min(slice_len[k], slice_cap) + 15) & ~15u;
@@ -737,6 +819,7 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
         uint32_t* offs = reinterpret_cast<uint32_t*>(host_out + sizeof(HevcOutHeader));
         offs[s] = off;
         offs[kMaxSlices + s] = len;
+        offs[2 * kMaxSlices + s] = (uint32_t)slice_first[s];
     }
     if (s != 0) return;
     // header: totals, overflow, distortion
@@ -788,11 +871,17 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
                        b.coef);
 }
 
-void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int num_slices, uint8_t* host_out,
+void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, uint8_t* host_out,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_hevc_cabac, dim3(num_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
-                       b.slice_cap, b.slice_len);
-    hipLaunchKernelGGL(k_hevc_pack, dim3(num_slices), dim3(256), 0, s, b.fs, num_slices, b.slice_data,
+    const int ncu = g.mb_w * g.mb_h;
+    hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cu, ncu, g.mb_w, max_slices, b.slice_first,
+                       b.slice_of_cu, b.nslices);
+    if (!idr)
+        hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
+                           b.slice_of_cu, b.cu);
+    hipLaunchKernelGGL(k_hevc_cabac, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
+                       b.slice_cap, b.slice_len, b.slice_first, b.nslices);
+    hipLaunchKernelGGL(k_hevc_pack, dim3(max_slices), dim3(256), 0, s, b.fs, b.nslices, b.slice_first, b.slice_data,
                        b.slice_cap, b.slice_len, host_out, b.out_bytes);
 }
 

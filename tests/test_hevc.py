@@ -83,7 +83,40 @@ def test_cpu_hevc_two_row_slices(native):
     # exercises above-neighbour intra references, merge/AMVP B candidates and skip contexts
     _, _, _, dec, enc = _cpu_roundtrip(native, 352, 288, 2, fps=30, qp=30)
     assert enc.slice_rows == 2
-    assert dec.stats["slices"] == 2 * 9
+    assert dec.stats["slices"] > 9  # 9 two-row slices in the IDR picture, cost-balanced ones in P
+
+
+def test_cpu_hevc_cost_balanced_p_slices(native):
+    """P pictures are split into raster runs of equal estimated CABAC work (not CTU rows): a
+    picture whose bottom half is noise gets most slice boundaries in the noisy half, slices
+    start mid-row, and the stream still decodes to the reconstruction."""
+    from mxdesk.codec import hevc_decoder as hd
+
+    w, h = 320, 192
+    enc = native.CpuHevcEncoder(_cfg(native, w, h, qp=22, aq=0))
+    rng = np.random.default_rng(5)
+    stream, recon = b"", []
+    for t in range(3):
+        y = np.full((h, w), 90, np.uint8)
+        y[h // 2:] = rng.integers(0, 255, (h - h // 2, w))
+        uv = np.full((h // 2, w), 128, np.uint8)
+        stream += enc.encode(y, uv, False)
+        recon.append(enc.recon())
+    addrs = []
+    for nal in hd.split_nal_units(stream):
+        if (nal[0] >> 1) & 63 == 1:  # TRAIL_R slice: first_slice flag + address
+            r = hd.BitReader(hd.unescape(nal), 16)
+            first = r.u(1)
+            r.ue()
+            addrs.append(0 if first else r.u((12 * 20 - 1).bit_length()))
+    ctb_w = w // 16
+    p_addrs = addrs[: len(addrs) // 2]
+    assert len(p_addrs) > 3 and any(a % ctb_w for a in p_addrs)  # mid-row slice starts
+    assert sum(a >= (h // 32) * ctb_w for a in p_addrs) > len(p_addrs) // 2  # mostly in the noisy half
+    dec = Decoder()
+    dec.decode(stream)
+    for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
+        assert np.array_equal(yy, ry) and np.array_equal(u, ruv[:, 0::2])
 
 
 def test_hevc_level_selection(native):
