@@ -127,7 +127,7 @@ MXHD int quant_coef(int c, int qp, int log2n, bool intra) {
 }
 MXHD int dequant_coef(int level, int qp, int log2n) {
     const int bd = log2n + 3;  // BitDepth + log2(nTbS) - 5
-    const int64_t v = (((int64_t)level * 16 * kLevelScale[qp % 6]) << (qp / 6)) + (1 << (bd - 1));
+    const int64_t v = (int64_t)level * 16 * kLevelScale[qp % 6] * ((int64_t)1 << (qp / 6)) + (1 << (bd - 1));
     const int64_t s = v >> bd;
     return s < -32768 ? -32768 : (s > 32767 ? 32767 : (int)s);
 }

@@ -9,8 +9,10 @@
 #include <vector>
 
 #include "../csrc/codec/h264_encoder.h"
+#include "../csrc/codec/hevc_encoder.h"
 #include "../csrc/net/dtls.h"
 #include "../csrc/net/rtp_h264.h"
+#include "../csrc/net/rtp_h265.h"
 #include "../csrc/net/srtp.h"
 
 using namespace mx;
@@ -51,6 +53,31 @@ static void encoder_pass(std::mt19937& rng) {
     }
 }
 
+static void hevc_pass(std::mt19937& rng) {
+    const int sizes[][3] = {{176, 144, 60}, {100, 60, 60}, {352, 288, 30}};  // 352x288@30: two-row slices
+    for (auto& s : sizes) {
+        h264::EncoderConfig c;
+        c.width = s[0];
+        c.height = s[1];
+        c.fps = s[2];
+        c.bitrate_kbps = 0;
+        c.qp = 4 + (int)(rng() % 46);
+        c.search_range = 8;
+        hevc::CpuHevcEncoder enc(c);
+        const int cw = enc.coded_pitch(), ch = (s[1] + 15) / 16 * 16;
+        std::vector<uint8_t> y((size_t)cw * ch), uv((size_t)cw * ch / 2);
+        for (int f = 0; f < 4; ++f) {
+            for (int r = 0; r < ch; ++r)
+                for (int x = 0; x < cw; ++x)
+                    y[(size_t)r * cw + x] = (uint8_t)((x * 3 + r * 2 + f * 5) ^ ((r > ch / 2) ? (rng() & 255) : 0));
+            for (auto& v : uv) v = (uint8_t)(128 + (int)(rng() % 32) - 16);
+            const auto& au = enc.encode(y.data(), uv.data(), cw, f == 0);
+            CHECK(au.size() > 6);
+            CHECK(au[0] == 0 && au[1] == 0 && au[2] == 0 && au[3] == 1);
+        }
+    }
+}
+
 static std::string rnd(std::mt19937& rng, size_t n) {
     std::string s(n, '\0');
     for (auto& ch : s) ch = (char)(rng() & 0xff);
@@ -86,6 +113,8 @@ static void rtp_pass(std::mt19937& rng) {
         if (i % 2) au = std::string("\x00\x00\x00\x01\x67", 5) + au + std::string("\x00\x00\x01\x65", 4) + au;
         net::RtpH264Packetizer pk((uint32_t)rng(), 96, 64 + rng() % 1200, (uint16_t)rng());
         for (const auto& p : pk.packetize(au, (uint32_t)rng())) CHECK(p.size() >= 12);
+        net::RtpH265Packetizer pk5((uint32_t)rng(), 97, 64 + rng() % 1200, (uint16_t)rng());
+        for (const auto& p : pk5.packetize(au, (uint32_t)rng())) CHECK(p.size() >= 12);
         (void)net::split_annexb(au);
     }
 }
@@ -111,6 +140,7 @@ static void dtls_pass() {
 int main() {
     std::mt19937 rng(12345);
     encoder_pass(rng);
+    hevc_pass(rng);
     srtp_pass(rng);
     rtp_pass(rng);
     dtls_pass();
