@@ -1137,6 +1137,120 @@ MXHD void inter_neighbours(const int16_t* mv, int stride, int x, int y, int ctb_
     *b2 = at(x > 0 && i - ctb_w - 1 >= first, i - ctb_w - 1);
 }
 
+// ---------------------------------------------------------------- deblocking (8.7.2)
+// With CTB = CU = PU = TU = 16x16 the only transform / prediction edges on the 8x8 grid are
+// the CU edges, and every 4-sample segment of a CU edge shares one boundary strength.
+constexpr uint8_t kDbBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                                 8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                                 34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+constexpr uint8_t kDbTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,  1,  1,  1,  1,  1,  1,  1, 1,
+                               2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+// bS of the edge between CU p and CU q (8.7.2.4): 2 intra, 1 coded luma residual on either
+// side or a motion difference of >= 1 integer sample (one reference picture), else 0.
+MXHD int db_bs(const CuInfo& p, const CuInfo& q) {
+    if (p.type == kCuIntra || q.type == kCuIntra) return 2;
+    if ((p.cbf & 1) || (q.cbf & 1)) return 1;
+    const int dx = p.mvx - q.mvx, dy = p.mvy - q.mvy;
+    return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
+}
+
+// One 4-line luma edge segment.  q0 points at the first q sample of line 0, `step` crosses
+// the edge (p_i = q0[-(i+1)*step], q_i = q0[i*step]) and `line` advances along it.
+MXHD void db_luma_seg(uint8_t* q0, int step, int line, int bs, int qp_p, int qp_q) {
+    if (bs == 0) return;
+    const int qpl = (qp_p + qp_q + 1) >> 1;
+    const int beta = kDbBeta[qpl < 0 ? 0 : (qpl > 51 ? 51 : qpl)];
+    int qt = qpl + 2 * (bs - 1);
+    qt = qt < 0 ? 0 : (qt > 53 ? 53 : qt);
+    const int tc = kDbTc[qt];
+    auto P = [&](int k, int i) { return (int)q0[k * line - (i + 1) * step]; };
+    auto Q = [&](int k, int i) { return (int)q0[k * line + i * step]; };
+    const int dp0 = abs(P(0, 2) - 2 * P(0, 1) + P(0, 0)), dp3 = abs(P(3, 2) - 2 * P(3, 1) + P(3, 0));
+    const int dq0 = abs(Q(0, 2) - 2 * Q(0, 1) + Q(0, 0)), dq3 = abs(Q(3, 2) - 2 * Q(3, 1) + Q(3, 0));
+    const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3;
+    if (dpq0 + dpq3 >= beta) return;
+    auto strong = [&](int k, int dpq) {
+        return 2 * dpq < (beta >> 2) && abs(P(k, 3) - P(k, 0)) + abs(Q(k, 0) - Q(k, 3)) < (beta >> 3) &&
+               abs(P(k, 0) - Q(k, 0)) < ((5 * tc + 1) >> 1);
+    };
+    const bool de2 = strong(0, dpq0) && strong(3, dpq3);
+    const bool dep = dp < ((beta + (beta >> 1)) >> 3), deq = dq < ((beta + (beta >> 1)) >> 3);
+    for (int k = 0; k < 4; ++k) {
+        uint8_t* s = q0 + k * line;
+        const int p0 = P(k, 0), p1 = P(k, 1), p2 = P(k, 2), p3 = P(k, 3);
+        const int q0v = Q(k, 0), q1 = Q(k, 1), q2 = Q(k, 2), q3 = Q(k, 3);
+        auto cl = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+        if (de2) {
+            s[-1 * step] = (uint8_t)cl((p2 + 2 * p1 + 2 * p0 + 2 * q0v + q1 + 4) >> 3, p0 - 2 * tc, p0 + 2 * tc);
+            s[-2 * step] = (uint8_t)cl((p2 + p1 + p0 + q0v + 2) >> 2, p1 - 2 * tc, p1 + 2 * tc);
+            s[-3 * step] = (uint8_t)cl((2 * p3 + 3 * p2 + p1 + p0 + q0v + 4) >> 3, p2 - 2 * tc, p2 + 2 * tc);
+            s[0] = (uint8_t)cl((p1 + 2 * p0 + 2 * q0v + 2 * q1 + q2 + 4) >> 3, q0v - 2 * tc, q0v + 2 * tc);
+            s[step] = (uint8_t)cl((p0 + q0v + q1 + q2 + 2) >> 2, q1 - 2 * tc, q1 + 2 * tc);
+            s[2 * step] = (uint8_t)cl((p0 + q0v + q1 + 3 * q2 + 2 * q3 + 4) >> 3, q2 - 2 * tc, q2 + 2 * tc);
+        } else {
+            int d = (9 * (q0v - p0) - 3 * (q1 - p1) + 8) >> 4;
+            if (abs(d) >= tc * 10) continue;
+            d = cl(d, -tc, tc);
+            s[-1 * step] = (uint8_t)clip255(p0 + d);
+            s[0] = (uint8_t)clip255(q0v - d);
+            if (dep) s[-2 * step] = (uint8_t)clip255(p1 + cl((((p2 + p0 + 1) >> 1) - p1 + d) >> 1, -(tc >> 1), tc >> 1));
+            if (deq) s[step] = (uint8_t)clip255(q1 + cl((((q2 + q0v + 1) >> 1) - q1 - d) >> 1, -(tc >> 1), tc >> 1));
+        }
+    }
+}
+
+// Chroma edge lines (bS == 2 only, 8.7.2.5.5); cb_qp_offset = pps_cb/cr_qp_offset.
+MXHD void db_chroma_lines(uint8_t* q0, int step, int line, int nlines, int qp_p, int qp_q, int c_qp_offset) {
+    const int qpc = chroma_qp(((qp_p + qp_q + 1) >> 1), c_qp_offset);
+    int qt = qpc + 2;  // 2 * (bS - 1) with bS = 2
+    qt = qt > 53 ? 53 : qt;
+    const int tc = kDbTc[qt];
+    for (int k = 0; k < nlines; ++k) {
+        uint8_t* s = q0 + k * line;
+        const int p0 = s[-step], p1 = s[-2 * step], q0v = s[0], q1 = s[step];
+        int d = ((((q0v - p0) * 4) + p1 - q1 + 4) >> 3);
+        d = d < -tc ? -tc : (d > tc ? tc : d);
+        s[-step] = (uint8_t)clip255(p0 + d);
+        s[0] = (uint8_t)clip255(q0v - d);
+    }
+}
+
+// QpY of every CU (8.6.1): the coded QP where residual was sent, else the prediction = the
+// previous CU's QpY in the slice (slice QP at its start).
+MXHD void slice_qpy(const CuInfo* cus, int first, int count, int slice_qp, uint8_t* qpy) {
+    int prev = slice_qp;
+    for (int k = 0; k < count; ++k) {
+        const CuInfo& c = cus[first + k];
+        if (c.type != kCuSkip && c.cbf) prev = c.qp;
+        qpy[first + k] = (uint8_t)prev;
+    }
+}
+
+// Deblock the vertical (dir 0) or horizontal (dir 1) CU edge between CU i and its left /
+// upper neighbour: rows [r0, r0 + 4) of luma and the matching 2 chroma lines (NV12).
+MXHD void db_edge_seg(uint8_t* ry, uint8_t* ruv, int pitch, int ctb_w, const CuInfo* cus, const uint8_t* qpy, int i,
+                      int dir, int seg, int c_qp_offset) {
+    const int x = i % ctb_w, y = i / ctb_w;
+    const int j = dir == 0 ? i - 1 : i - ctb_w;
+    const int bs = db_bs(cus[j], cus[i]);
+    if (!bs) return;
+    const int qp_p = qpy[j], qp_q = qpy[i];
+    if (dir == 0) {
+        db_luma_seg(ry + (size_t)(y * 16 + seg * 4) * pitch + x * 16, 1, pitch, bs, qp_p, qp_q);
+        if (bs == 2)
+            for (int c = 0; c < 2; ++c)
+                db_chroma_lines(ruv + (size_t)(y * 8 + seg * 2) * pitch + x * 16 + c, 2, pitch, 2, qp_p, qp_q,
+                                c_qp_offset);
+    } else {
+        db_luma_seg(ry + (size_t)(y * 16) * pitch + x * 16 + seg * 4, pitch, 1, bs, qp_p, qp_q);
+        if (bs == 2)
+            for (int c = 0; c < 2; ++c)
+                db_chroma_lines(ruv + (size_t)(y * 8) * pitch + x * 16 + seg * 4 + c, pitch, 2, 2, qp_p, qp_q,
+                                c_qp_offset);
+    }
+}
+
 // ---------------------------------------------------------------- adaptive slice layout (P)
 // Entropy-coding cost estimate of a CU in CABAC work units: significance bins up to the
 // last position of every coded TU plus a few bins per coded sub-block, on top of the CU

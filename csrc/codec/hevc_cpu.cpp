@@ -240,10 +240,15 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.put(0, 1);  // transquant_bypass_enabled_flag
         w.put(0, 1);  // tiles_enabled_flag
         w.put(0, 1);  // entropy_coding_sync_enabled_flag
-        w.put(0, 1);  // pps_loop_filter_across_slices_enabled_flag
-        w.put(1, 1);  // deblocking_filter_control_present_flag
-        w.put(0, 1);  //   deblocking_filter_override_enabled_flag
-        w.put(1, 1);  //   pps_deblocking_filter_disabled_flag
+        const bool db = c.deblock != 0;
+        w.put(db, 1);  // pps_loop_filter_across_slices_enabled_flag (CU edges on slice borders too)
+        w.put(1, 1);   // deblocking_filter_control_present_flag
+        w.put(0, 1);   //   deblocking_filter_override_enabled_flag
+        w.put(!db, 1);  //   pps_deblocking_filter_disabled_flag
+        if (db) {
+            w.se(0);  //   pps_beta_offset_div2
+            w.se(0);  //   pps_tc_offset_div2
+        }
         w.put(0, 1);  // pps_scaling_list_data_present_flag
         w.put(0, 1);  // lists_modification_present_flag
         w.ue(0);      // log2_parallel_merge_level_minus2
@@ -276,6 +281,7 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
         w.ue(4);      // five_minus_max_num_merge_cand -> MaxNumMergeCand 1
     }
     w.se(qp - 26);  // slice_qp_delta
+    if (config().deblock) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
     w.trailing();   // byte_alignment()
     std::vector<uint8_t> rbsp = std::move(w.b);
     rbsp.insert(rbsp.end(), data, data + n);
@@ -462,9 +468,23 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     } else {
         analyse_inter(y, uv, pitch);
     }
+    const int W = common_.ctb_w(), H = common_.ctb_h();
+    if (cfg_.deblock) {  // in-loop deblocking: all vertical CU edges, then all horizontal ones
+        std::vector<uint8_t> qpy((size_t)W * H);
+        for (size_t s = 0; s < slices_.size(); ++s) {
+            const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
+            slice_qpy(cu_.data(), first, count, qp, qpy.data());
+        }
+        for (int dir = 0; dir < 2; ++dir)
+            for (int i = 0; i < W * H; ++i) {
+                if (dir == 0 ? (i % W) == 0 : (i / W) == 0) continue;
+                for (int seg = 0; seg < 4; ++seg)
+                    db_edge_seg(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir, seg,
+                                cfg_.chroma_qp_offset);
+            }
+    }
     au_.clear();
     if (idr) common_.write_parameter_sets(au_);
-    const int W = common_.ctb_w(), H = common_.ctb_h();
     std::vector<uint8_t> buf;
     uint8_t ctx[C_NUM];
     for (size_t s = 0; s < slices_.size(); ++s) {

@@ -32,6 +32,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.slice_first, sizeof(int) * ns));
     HIP_CHECK(hipMalloc(&b.slice_of_cu, sizeof(int) * ncu));
     HIP_CHECK(hipMalloc(&b.nslices, sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&b.qpy, ncu));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
@@ -47,7 +48,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
 void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
-                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices,
+                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy,
                     (void*)b.sse_part})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
@@ -130,7 +131,8 @@ bool GpuHevcEncoder::prepare(bool force_idr) {
     f.num_slices = common_.num_slices();
     f.aq = cfg_.aq;
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
-    f.n_sse_parts = idr ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
+    // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
+    f.n_sse_parts = (idr || cfg_.deblock) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
     f.sse_part = sl.buf.sse_part;
     h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
     m.ref_y = rec_y_[ref];
@@ -158,13 +160,14 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
         h264::launch_me(geom_, sl.buf.me, src_y, stream_);
         launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
+    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.deblock != 0, src_y, src_uv, stream_);
     hipStream_t es = stream_;
     if (stream_e_) {
         HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
         HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
         es = stream_e_;
     }
-    launch_hevc_entropy(geom_, sl.buf, idr, common_.max_slices(), sl.host_out, es);
+    launch_hevc_entropy(geom_, sl.buf, common_.max_slices(), sl.host_out, es);
     HIP_CHECK(hipGetLastError());
 }
 

@@ -138,6 +138,7 @@ struct HevcDeviceBuffers {
     int* slice_first;        // [max_slices] first CTU of every slice (k_hevc_layout)
     int* slice_of_cu;        // [ncu]
     uint32_t* nslices;       // slice count of the frame
+    uint8_t* qpy;            // [ncu] QpY per CU (deblocking)
     size_t out_bytes;
     unsigned long long* sse_part;
 };
@@ -146,7 +147,11 @@ void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint
                        hipStream_t s);
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
-void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, uint8_t* host_out,
+// Slice layout, per-slice decisions and (with deblock) the in-loop filter + final distortion:
+// runs on the analysis stream because the deblocked picture is the next frame's reference.
+void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
+                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
+void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s);
 
 class GpuHevcEncoder final : public VideoEncoder {

@@ -6,13 +6,17 @@
 //                  compensation, the 16x16 / 8x8 core transforms as LDS-staged
 //                  matrix products (4 luma + 2 chroma outputs per lane per stage),
 //                  quantisation, normative inverse transform and reconstruction, coded
-//                  sub-block / last-position summaries by wave reductions, and the
-//                  skip / merge / AMVP decision from the neighbours' motion.
+//                  sub-block / last-position summaries by wave reductions.
 //  * k_hevc_intra  one workgroup per slice, one wave per CTU row; the rows of a slice run
 //                  as a wavefront (row r two CTUs behind row r-1) with the left column
 //                  and the bottom rows of the row above exchanged through LDS.
-//  * k_hevc_cabac  one wave per slice; lane 0 runs the shared CABAC slice coder
-//                  (hevc_core.h code_slice) with its 142 context states in LDS.
+//  * k_hevc_cabac  one wave per slice running the shared CABAC CU coder (hevc_core.h
+//                  code_cu) in lockstep on wave-uniform state (see the section comment).
+//  * k_hevc_layout / k_hevc_decide  slice layout (rows for I, cost-balanced raster runs for
+//                  P) and the per-slice skip / merge / AMVP decisions.
+//  * k_hevc_qpy + k_hevc_deblock + k_hevc_sse  in-loop deblocking (QP chain per slice, one
+//                  thread per 4-sample CU-edge segment, vertical then horizontal pass) and the
+//                  distortion of the final picture.
 //  * k_hevc_pack   one workgroup per slice copies the slice bytes (16-byte stores) into
 //                  pinned host memory at 16-byte aligned offsets; workgroup 0 writes the
 //                  header (lengths, overflow, distortion totals).
@@ -786,6 +790,73 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
     if (lane == 0) slice_len[s] = e.pos;
 }
 
+// ------------------------------------------------------------------ deblocking
+// QpY of every CU: one lane per slice walks its raster run (the QP prediction chain).
+__global__ __launch_bounds__(64) void k_hevc_qpy(const HevcFrameState* __restrict__ fs, const CuInfo* __restrict__ cus,
+                                                  int ncu, const int* __restrict__ slice_first,
+                                                  const uint32_t* __restrict__ nslices, uint8_t* __restrict__ qpy) {
+    const int s = blockIdx.x * 64 + threadIdx.x;
+    const int ns = (int)*nslices;
+    if (s >= ns) return;
+    const int first = slice_first[s], count = (s + 1 < ns ? slice_first[s + 1] : ncu) - first;
+    slice_qpy(cus, first, count, fs->qp, qpy);
+}
+
+// One thread per 4-sample segment of a CU's left (dir 0) or top (dir 1) edge.  Vertical
+// edges are 16 samples apart and a filter reads p3..q3 / writes p2..q2, so all segments of a
+// direction are independent; the horizontal pass runs as a second launch on its output.
+__global__ __launch_bounds__(256) void k_hevc_deblock(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                      const CuInfo* __restrict__ cus, const uint8_t* __restrict__ qpy,
+                                                      int dir) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int ncu = g.mb_w * g.mb_h;
+    if (t >= ncu * 4) return;
+    const int i = t >> 2, seg = t & 3;
+    if (dir == 0 ? (i % g.mb_w) == 0 : (i / g.mb_w) == 0) return;
+    db_edge_seg(fs->rec_y, fs->rec_uv, g.pitch, g.mb_w, cus, qpy, i, dir, seg, fs->chroma_qp_offset);
+}
+
+// Distortion of the final (deblocked) picture over the display area: one workgroup per CTU
+// row, partial sums per row for k_hevc_pack.
+__global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                   const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv) {
+    __shared__ unsigned long long red[3][4];
+    const int r = blockIdx.x, tid = threadIdx.x;
+    unsigned long long e[3] = {0, 0, 0};
+    const int rows = min(16, g.height - r * 16);
+    for (int k = tid; k < rows * g.width; k += 256) {
+        const int yy = r * 16 + k / g.width, x = k % g.width;
+        const int d = (int)src_y[(size_t)yy * g.pitch + x] - (int)fs->rec_y[(size_t)yy * g.pitch + x];
+        e[0] += (unsigned)(d * d);
+    }
+    const int crows = min(8, g.height / 2 - r * 8), cw = g.width;  // NV12: Cb / Cr interleaved
+    for (int k = tid; k < crows * cw; k += 256) {
+        const int yy = r * 8 + k / cw, x = k % cw;
+        const int d = (int)src_uv[(size_t)yy * g.pitch + x] - (int)fs->rec_uv[(size_t)yy * g.pitch + x];
+        if (x & 1)
+            e[2] += (unsigned)(d * d);
+        else
+            e[1] += (unsigned)(d * d);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        e[0] += __shfl_xor(e[0], o, 64);
+        e[1] += __shfl_xor(e[1], o, 64);
+        e[2] += __shfl_xor(e[2], o, 64);
+    }
+    if ((tid & 63) == 0) {
+        red[0][tid >> 6] = e[0];
+        red[1][tid >> 6] = e[1];
+        red[2][tid >> 6] = e[2];
+    }
+    __syncthreads();
+    if (tid < 3) {
+        const unsigned long long v = tid == 0 ? red[0][0] + red[0][1] + red[0][2] + red[0][3]
+                                     : tid == 1 ? red[1][0] + red[1][1] + red[1][2] + red[1][3]
+                                                : red[2][0] + red[2][1] + red[2][2] + red[2][3];
+        fs->sse_part[tid * h264::kSsePartStride + r] = v;
+    }
+}
+
 // ------------------------------------------------------------------ pack
 __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restrict__ fs,
                                                     const uint32_t* __restrict__ nslices,
@@ -871,14 +942,25 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
                        b.coef);
 }
 
-void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, uint8_t* host_out,
-                         hipStream_t s) {
+void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
+                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
     hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cu, ncu, g.mb_w, max_slices, b.slice_first,
                        b.slice_of_cu, b.nslices);
     if (!idr)
         hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
                            b.slice_of_cu, b.cu);
+    if (deblock) {
+        hipLaunchKernelGGL(k_hevc_qpy, dim3((max_slices + 63) / 64), dim3(64), 0, s, b.fs, b.cu, ncu, b.slice_first,
+                           b.nslices, b.qpy);
+        for (int dir = 0; dir < 2; ++dir)
+            hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
+        hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
+    }
+}
+
+void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
+                         hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_cabac, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
                        b.slice_cap, b.slice_len, b.slice_first, b.nslices);
     hipLaunchKernelGGL(k_hevc_pack, dim3(max_slices), dim3(256), 0, s, b.fs, b.nslices, b.slice_first, b.slice_data,

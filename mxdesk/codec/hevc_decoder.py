@@ -98,6 +98,9 @@ _LUMA_FILTER = [[0, 0, 0, 64, 0, 0, 0, 0], [-1, 4, -10, 58, 17, -5, 1, 0], [-1, 
 _CHROMA_FILTER = [[0, 64, 0, 0], [-2, 58, 10, -2], [-4, 54, 16, -2], [-6, 46, 28, -4], [-4, 36, 36, -4],
                   [-4, 28, 46, -6], [-2, 16, 54, -4], [-2, 10, 58, -2]]
 _LEVEL_SCALE = [40, 45, 51, 57, 64, 72]
+# deblocking beta' (Table 8-12, Q = 0..51) and tC' (Q = 0..53)
+_DB_BETA = [0] * 16 + [6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18] + list(range(20, 66, 2))
+_DB_TC = [0] * 18 + [1] * 9 + [2] * 4 + [3] * 4 + [4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24]
 _QPC_TABLE = {30: 29, 31: 30, 32: 31, 33: 32, 34: 33, 35: 33, 36: 34, 37: 34, 38: 35, 39: 35, 40: 36, 41: 36,
               42: 37, 43: 37}
 
@@ -254,6 +257,8 @@ class PPS:
     loop_filter_across_slices: int = 0
     deblocking_override_enabled: int = 0
     deblocking_disabled: int = 0
+    beta_offset_div2: int = 0
+    tc_offset_div2: int = 0
     lists_modification_present: int = 0
     log2_parallel_merge_level: int = 2
 
@@ -391,8 +396,8 @@ def parse_pps(rbsp: bytes) -> PPS:
         p.deblocking_override_enabled = r.u(1)
         p.deblocking_disabled = r.u(1)
         if not p.deblocking_disabled:
-            r.se()
-            r.se()
+            p.beta_offset_div2 = r.se()
+            p.tc_offset_div2 = r.se()
     if r.u(1):
         raise NotImplementedError("PPS scaling lists")
     p.lists_modification_present = r.u(1)
@@ -571,6 +576,8 @@ class Decoder:
             return
         s = self.sps
         p = self.cur
+        if any(not sp["db_disabled"] for sp in self.slice_params.values()):
+            self._deblock()
         self.frames_coded.append((p.y.copy(), p.u.copy(), p.v.copy()))
         l, r, t, b = s.conf
         h, w = p.y.shape
@@ -578,6 +585,97 @@ class Decoder:
                             p.u[t:h // 2 - b, l:w // 2 - r].copy(), p.v[t:h // 2 - b, l:w // 2 - r].copy()))
         self.ref = p
         self.cur = None
+
+    # ---------------------------------------------------------------- deblocking (8.7.2)
+    def _deblock(self) -> None:
+        for vertical in (True, False):  # all vertical edges of the picture first, then horizontal
+            self._deblock_dir(vertical)
+
+    def _deblock_dir(self, vertical: bool) -> None:
+        y, u, v = self.cur.y, self.cur.u, self.cur.v
+        H, W = y.shape
+        emap = self.edge_v if vertical else self.edge_h
+        for e in range(8, W if vertical else H, 8):  # 8x8 luma grid, picture borders excluded
+            for t in range(0, H if vertical else W, 4):  # 4-sample segments along the edge
+                xq, yq = (e, t) if vertical else (t, e)
+                xp, yp = (e - 1, t) if vertical else (t, e - 1)
+                if not emap[yq >> 2, xq >> 2]:
+                    continue
+                sq, sp_ = self.slice_map[yq >> 2, xq >> 2], self.slice_map[yp >> 2, xp >> 2]
+                prm = self.slice_params[int(sq)]
+                if prm["db_disabled"] or (sq != sp_ and not prm["lf_across"]):
+                    continue
+                bq, bp = (yq >> 2, xq >> 2), (yp >> 2, xp >> 2)
+                if self.pred_intra[bq] or self.pred_intra[bp]:
+                    bs = 2
+                elif self.cbf_map[bq] or self.cbf_map[bp]:
+                    bs = 1
+                else:
+                    mq, mp = self.mv_map[bq], self.mv_map[bp]
+                    bs = 1 if abs(int(mq[0]) - int(mp[0])) >= 4 or abs(int(mq[1]) - int(mp[1])) >= 4 else 0
+                if bs == 0:
+                    continue
+                qpl = (int(self.qp_map[bq]) + int(self.qp_map[bp]) + 1) >> 1
+                self._db_luma(y, vertical, e, t, bs, qpl, prm)
+                if bs == 2 and e % 16 == 0:  # chroma: 8-sample chroma grid, intra edges only
+                    for plane, off in ((u, self.pps.cb_qp_offset), (v, self.pps.cr_qp_offset)):
+                        qpi = qpl + off
+                        qpc = qpi if qpi < 30 else (qpi - 6 if qpi > 43 else _QPC_TABLE[qpi])
+                        tc = _DB_TC[min(max(qpc + 2 + prm["tc_offset"], 0), 53)]
+                        for k in range(2):
+                            if vertical:
+                                row, c = plane[t // 2 + k], e // 2
+                                p0, p1, q0, q1 = int(row[c - 1]), int(row[c - 2]), int(row[c]), int(row[c + 1])
+                            else:
+                                col, c = plane[:, t // 2 + k], e // 2
+                                p0, p1, q0, q1 = int(col[c - 1]), int(col[c - 2]), int(col[c]), int(col[c + 1])
+                            d = min(max((((q0 - p0) * 4) + p1 - q1 + 4) >> 3, -tc), tc)
+                            (row if vertical else col)[c - 1] = min(max(p0 + d, 0), 255)
+                            (row if vertical else col)[c] = min(max(q0 - d, 0), 255)
+
+    @staticmethod
+    def _db_luma(y, vertical: bool, e: int, t: int, bs: int, qpl: int, prm: dict) -> None:
+        beta = _DB_BETA[min(max(qpl + prm["beta_offset"], 0), 51)]
+        tc = _DB_TC[min(max(qpl + 2 * (bs - 1) + prm["tc_offset"], 0), 53)]
+        lines = [y[t + k, e - 4: e + 4] if vertical else y[e - 4: e + 4, t + k] for k in range(4)]
+        vals = [[int(x) for x in ln] for ln in lines]  # p3 p2 p1 p0 q0 q1 q2 q3
+        def dp(k):
+            return abs(vals[k][1] - 2 * vals[k][2] + vals[k][3])
+        def dq(k):
+            return abs(vals[k][6] - 2 * vals[k][5] + vals[k][4])
+        dpq0, dpq3 = dp(0) + dq(0), dp(3) + dq(3)
+        if dpq0 + dpq3 >= beta:
+            return
+        def strong(k, dpq):
+            a = vals[k]
+            return (2 * dpq < (beta >> 2) and abs(a[0] - a[3]) + abs(a[4] - a[7]) < (beta >> 3)
+                    and abs(a[3] - a[4]) < ((5 * tc + 1) >> 1))
+        de2 = strong(0, dpq0) and strong(3, dpq3)
+        dep = dp(0) + dp(3) < ((beta + (beta >> 1)) >> 3)
+        deq = dq(0) + dq(3) < ((beta + (beta >> 1)) >> 3)
+        def c3(lo, hi, x):
+            return min(max(x, lo), hi)
+        for k in range(4):
+            p3, p2, p1, p0, q0, q1, q2, q3 = vals[k]
+            out = lines[k]
+            if de2:
+                out[3] = c3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3)
+                out[2] = c3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2)
+                out[1] = c3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3)
+                out[4] = c3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3)
+                out[5] = c3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2)
+                out[6] = c3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3)
+            else:
+                d = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4
+                if abs(d) >= tc * 10:
+                    continue
+                d = c3(-tc, tc, d)
+                out[3] = c3(0, 255, p0 + d)
+                out[4] = c3(0, 255, q0 - d)
+                if dep:
+                    out[2] = c3(0, 255, p1 + c3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + d) >> 1))
+                if deq:
+                    out[5] = c3(0, 255, q1 + c3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - d) >> 1))
 
     # ---------------------------------------------------------------- slice
     def _slice(self, typ: int, rbsp: bytes) -> None:
@@ -635,6 +733,10 @@ class Decoder:
             self.mv_map = np.zeros(n4 + (2,), np.int32)
             self.intra_mode_map = np.full(n4, 1, np.int32)
             self.qp_map = np.zeros(n4, np.int32)
+            self.cbf_map = np.zeros(n4, bool)    # luma TU with nonzero levels covering the 4x4 block
+            self.edge_v = np.zeros(n4, bool)     # transform/prediction edge on the left of the 4x4 block
+            self.edge_h = np.zeros(n4, bool)     # ... on the top
+            self.slice_params = {}
             self.prev_poc_tid0 = poc
         elif self.cur is None:
             raise ValueError("slice of a picture whose first slice is missing")
@@ -666,8 +768,12 @@ class Decoder:
             r.se()
         if p.deblocking_override_enabled and r.u(1):
             raise NotImplementedError("deblocking override")
-        if not p.deblocking_disabled:
-            raise NotImplementedError("deblocking filter")
+        db_disabled = p.deblocking_disabled
+        lf_across = p.loop_filter_across_slices
+        if p.loop_filter_across_slices and not db_disabled:  # (no SAO)
+            lf_across = r.u(1)
+        self.slice_params[addr] = {"db_disabled": db_disabled, "lf_across": lf_across,
+                                   "beta_offset": 2 * p.beta_offset_div2, "tc_offset": 2 * p.tc_offset_div2}
         r.byte_alignment()
         self.stats["slices"] += 1
         self.slice_type = slice_type
@@ -746,6 +852,9 @@ class Decoder:
                 inc += 1
             skip = cab.decision("cu_skip_flag", inc)
         b4 = (slice(y0 >> 2, (y0 + size) >> 2), slice(x0 >> 2, (x0 + size) >> 2))
+        self.edge_v[b4[0], x0 >> 2] = True  # prediction-unit (= CU) edges
+        self.edge_h[y0 >> 2, b4[1]] = True
+        self.cbf_map[b4] = False
         if skip:
             self.stats["skip"] += 1
             mv = self._prediction_unit(cab, x0, y0, size, size, merge_flag=1)
@@ -1002,6 +1111,10 @@ class Decoder:
             raise NotImplementedError("4x4 intra luma (DST)")
         # luma
         res = self._residual(cab, log2, 0, mode if intra else None) if cbf_luma else None
+        tb4 = (slice(y0 >> 2, (y0 + n) >> 2), slice(x0 >> 2, (x0 + n) >> 2))
+        self.cbf_map[tb4] = bool(cbf_luma)
+        self.edge_v[tb4[0], x0 >> 2] = True
+        self.edge_h[y0 >> 2, tb4[1]] = True
         if intra:
             self._intra_predict(x0, y0, log2, 0, mode)
         self._add_residual(self.cur.y, x0, y0, n, res, self.qp_y, log2)

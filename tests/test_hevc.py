@@ -222,3 +222,25 @@ def test_gpu_session_hevc_stream(gpu):
     assert len(frames) == 5
     for (y, _, _), fid in zip(frames, ids):
         assert _read_barcode(y, gpu.BARCODE_CELL, gpu.BARCODE_X, gpu.BARCODE_Y)[0] == fid
+
+
+def test_cpu_hevc_deblocking(native):
+    """In-loop deblocking (8.7.2): the filtered reconstruction is what the decoder outputs,
+    it differs from the unfiltered one at a coarse QP, and it is closer to the source."""
+    out = {}
+    for db in (0, 1):
+        cfg = _cfg(native, 160, 96, qp=40)
+        cfg.deblock = db
+        enc = native.CpuHevcEncoder(cfg)
+        stream, recon, err = b"", [], 0.0
+        for t in range(3):
+            y, uv = synthetic_nv12(160, 96, t)
+            stream += enc.encode(y, uv, False)
+            recon.append(enc.recon()[0].copy())
+            err += float(((recon[-1][:96, :160].astype(np.int64) - y) ** 2).sum())
+        dec = Decoder()
+        dec.decode(stream)
+        assert all(np.array_equal(a[0], b) for a, b in zip(dec.frames_coded, recon))
+        out[db] = (recon, err)
+    assert not np.array_equal(out[0][0][0], out[1][0][0])
+    assert out[1][1] < out[0][1]
