@@ -33,6 +33,8 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.slice_of_cu, sizeof(int) * ncu));
     HIP_CHECK(hipMalloc(&b.nslices, sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&b.qpy, ncu));
+    HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * ncu));
+    HIP_CHECK(hipMalloc(&b.qpc, ncu));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
@@ -48,7 +50,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
 void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
-                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy,
+                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
                     (void*)b.sse_part})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);

@@ -139,6 +139,8 @@ struct HevcDeviceBuffers {
     int* slice_of_cu;        // [ncu]
     uint32_t* nslices;       // slice count of the frame
     uint8_t* qpy;            // [ncu] QpY per CU (deblocking)
+    uint32_t* cost;          // [ncu] CABAC cost estimate (slice layout)
+    uint8_t* qpc;            // [ncu] QP of CUs that code a residual, else 255 (QP chain)
     size_t out_bytes;
     unsigned long long* sse_part;
 };

@@ -306,7 +306,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
                                                      const h264::MbInfo* __restrict__ mbs,
                                                      const uint8_t* __restrict__ src_y,
                                                      const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
-                                                     int16_t* __restrict__ coef) {
+                                                     int16_t* __restrict__ coef, uint32_t* __restrict__ cost,
+                                                     uint8_t* __restrict__ qp_coded) {
     __shared__ Mats M;
     __shared__ TuBuf tb[4];
     __shared__ unsigned long long part[3][4];
@@ -391,6 +392,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         c.mvp_idx = 0;
         fill_cu(c, r);
         cus[i] = c;  // skip / merge / AMVP are decided by k_hevc_decide once the slices are laid out
+        cost[i] = cu_cost(c);
+        qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
     }
     __syncthreads();
     if (threadIdx.x < 3) {
@@ -433,14 +436,15 @@ __device__ __forceinline__ int pred_sample(int mode, int log2n, bool luma, const
 __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, const HevcFrameState* __restrict__ fs,
                                                       const uint8_t* __restrict__ src_y,
                                                       const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
-                                                      int16_t* __restrict__ coef) {
+                                                      int16_t* __restrict__ coef, uint32_t* __restrict__ cost,
+                                                      uint8_t* __restrict__ qp_coded) {
     // dynamic LDS: per row of the slice, the bottom luma row and bottom chroma (NV12) row
     extern __shared__ uint8_t bottom[];
     __shared__ Mats M;
     __shared__ TuBuf tb[kMaxSliceRows];
     __shared__ IntraRefs rf[kMaxSliceRows];
     __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
-    __shared__ int cost[kMaxSliceRows][4];
+    __shared__ int mode_cost[kMaxSliceRows][4];
     __shared__ int prev_mode[kMaxSliceRows];
     fill_mats(M);
     __syncthreads();
@@ -521,14 +525,14 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                     sad += d < 0 ? -d : d;
                 }
                 sad = wsum(sad);
-                if (lane == 0) cost[wave][m] = sad + lambda * intra_mode_bits(md, cand_a);
+                if (lane == 0) mode_cost[wave][m] = sad + lambda * intra_mode_bits(md, cand_a);
             }
         }
         __syncthreads();
         if (valid) {
             int bm = 0;
             for (int m = 1; m < kNumIntraCands; ++m)
-                if (cost[wave][m] < cost[wave][bm]) bm = m;
+                if (mode_cost[wave][m] < mode_cost[wave][bm]) bm = m;
             mode = kIntraCands[bm];
             const int r = lane >> 2, cb = (lane & 3) * 4;
             for (int j = 0; j < 4; ++j) {
@@ -562,6 +566,8 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 c.mvp_idx = 0;
                 fill_cu(c, res);
                 cus[i] = c;
+                cost[i] = cu_cost(c);
+                qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
                 prev_mode[wave] = mode;
             }
         }
@@ -605,7 +611,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
 }
 
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
-                                                       const CuInfo* __restrict__ cus, int ncu, int ctb_w,
+                                                       const uint32_t* __restrict__ cost, int ncu, int ctb_w,
                                                        int max_slices, int* __restrict__ slice_first,
                                                        int* __restrict__ slice_of_cu, uint32_t* __restrict__ nslices) {
     __shared__ uint32_t sh[1024];
@@ -620,22 +626,22 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     const int chunk = (ncu + (int)blockDim.x - 1) / (int)blockDim.x;
     const int i0 = min(ncu, tid * chunk), i1 = min(ncu, i0 + chunk);
     uint32_t local = 0;
-    for (int i = i0; i < i1; ++i) local += cu_cost(cus[i]);
+    for (int i = i0; i < i1; ++i) local += cost[i];
     uint32_t total;
     const uint32_t pre0 = block_excl_scan(local, sh, &total);
     const int S = plan_num_slices(total, max_slices);
     // starts in this chunk
-    int prev = i0 > 0 ? plan_slice_of(pre0 - cu_cost(cus[i0 - 1]), total, S) : -1;
+    int prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
     uint32_t pre = pre0, nst = 0;
     for (int i = i0; i < i1; ++i) {
         const int id = plan_slice_of(pre, total, S);
         nst += id != prev;
         prev = id;
-        pre += cu_cost(cus[i]);
+        pre += cost[i];
     }
     uint32_t nstarts;
     const uint32_t base = block_excl_scan(nst, sh, &nstarts);
-    prev = i0 > 0 ? plan_slice_of(pre0 - cu_cost(cus[i0 - 1]), total, S) : -1;
+    prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
     pre = pre0;
     int rank = (int)base - 1;
     for (int i = i0; i < i1; ++i) {
@@ -643,7 +649,7 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
         if (id != prev) slice_first[++rank] = i;
         slice_of_cu[i] = rank;
         prev = id;
-        pre += cu_cost(cus[i]);
+        pre += cost[i];
     }
     if (tid == 0) *nslices = nstarts;
 }
@@ -791,15 +797,37 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
 }
 
 // ------------------------------------------------------------------ deblocking
-// QpY of every CU: one lane per slice walks its raster run (the QP prediction chain).
-__global__ __launch_bounds__(64) void k_hevc_qpy(const HevcFrameState* __restrict__ fs, const CuInfo* __restrict__ cus,
-                                                  int ncu, const int* __restrict__ slice_first,
-                                                  const uint32_t* __restrict__ nslices, uint8_t* __restrict__ qpy) {
-    const int s = blockIdx.x * 64 + threadIdx.x;
+// QpY of every CU (hevc_core.h slice_qpy): the QP of the last CU at or before it in its slice
+// that coded a residual, else the slice QP.  One workgroup per slice; qpc holds (QP or 255) per
+// CU from the analysis kernels; a block max-scan of (index << 8 | QP) over 256-CU chunks with
+// the previous chunk's maximum carried in.
+__global__ __launch_bounds__(256) void k_hevc_qpy(const HevcFrameState* __restrict__ fs,
+                                                   const uint8_t* __restrict__ qpc, int ncu,
+                                                   const int* __restrict__ slice_first,
+                                                   const uint32_t* __restrict__ nslices, uint8_t* __restrict__ qpy) {
+    __shared__ int wmaxv[4];
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ns = (int)*nslices;
     if (s >= ns) return;
-    const int first = slice_first[s], count = (s + 1 < ns ? slice_first[s + 1] : ncu) - first;
-    slice_qpy(cus, first, count, fs->qp, qpy);
+    const int first = slice_first[s], end = s + 1 < ns ? slice_first[s + 1] : ncu;
+    int carry = -1;
+    for (int base = first; base < end; base += 256) {
+        const int i = base + tid;
+        const int q = i < end ? qpc[i] : 255;
+        int key = q != 255 ? ((i << 8) | q) : -1;
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive max-scan within the wave
+            const int t = __shfl_up(key, o, 64);
+            if (lane >= o) key = max(key, t);
+        }
+        if (lane == 63) wmaxv[wave] = key;
+        __syncthreads();
+        for (int w = 0; w < wave; ++w) key = max(key, wmaxv[w]);
+        key = max(key, carry);
+        if (i < end) qpy[i] = (uint8_t)(key >= 0 ? (key & 255) : fs->qp);
+        const int chunk_max = max(max(wmaxv[0], wmaxv[1]), max(wmaxv[2], wmaxv[3]));
+        carry = max(carry, chunk_max);
+        __syncthreads();
+    }
 }
 
 // One thread per 4-sample segment of a CU's left (dir 0) or top (dir 1) edge.  Vertical
@@ -823,21 +851,24 @@ __global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameSta
     __shared__ unsigned long long red[3][4];
     const int r = blockIdx.x, tid = threadIdx.x;
     unsigned long long e[3] = {0, 0, 0};
-    const int rows = min(16, g.height - r * 16);
-    for (int k = tid; k < rows * g.width; k += 256) {
-        const int yy = r * 16 + k / g.width, x = k % g.width;
-        const int d = (int)src_y[(size_t)yy * g.pitch + x] - (int)fs->rec_y[(size_t)yy * g.pitch + x];
-        e[0] += (unsigned)(d * d);
-    }
-    const int crows = min(8, g.height / 2 - r * 8), cw = g.width;  // NV12: Cb / Cr interleaved
-    for (int k = tid; k < crows * cw; k += 256) {
-        const int yy = r * 8 + k / cw, x = k % cw;
-        const int d = (int)src_uv[(size_t)yy * g.pitch + x] - (int)fs->rec_uv[(size_t)yy * g.pitch + x];
-        if (x & 1)
-            e[2] += (unsigned)(d * d);
-        else
-            e[1] += (unsigned)(d * d);
-    }
+    const int quads = (g.width + 3) >> 2;  // dword columns (pitch is 256-aligned)
+    auto acc = [&](const uint8_t* a, const uint8_t* b, int row, int q, bool chroma) {
+        const uint32_t va = *reinterpret_cast<const uint32_t*>(a + (size_t)row * g.pitch + 4 * q);
+        const uint32_t vb = *reinterpret_cast<const uint32_t*>(b + (size_t)row * g.pitch + 4 * q);
+        for (int j = 0; j < 4; ++j) {
+            if (4 * q + j >= g.width) break;
+            const int d = (int)((va >> (8 * j)) & 255) - (int)((vb >> (8 * j)) & 255);
+            if (!chroma)
+                e[0] += (unsigned)(d * d);
+            else if (j & 1)
+                e[2] += (unsigned)(d * d);
+            else
+                e[1] += (unsigned)(d * d);
+        }
+    };
+    const int rows = min(16, g.height - r * 16), crows = min(8, g.height / 2 - r * 8);
+    for (int k = tid; k < rows * quads; k += 256) acc(src_y, fs->rec_y, r * 16 + k / quads, k % quads, false);
+    for (int k = tid; k < crows * quads; k += 256) acc(src_uv, fs->rec_uv, r * 8 + k / quads, k % quads, true);
     for (int o = 32; o > 0; o >>= 1) {
         e[0] += __shfl_xor(e[0], o, 64);
         e[1] += __shfl_xor(e[1], o, 64);
@@ -932,27 +963,27 @@ void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint
                        hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
     hipLaunchKernelGGL(k_hevc_inter, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, b.me.mb, src_y, src_uv, b.cu,
-                       b.coef);
+                       b.coef, b.cost, b.qpc);
 }
 
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const size_t lds = (size_t)slice_rows * 2 * g.coded_w;
     hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows), lds, s, g, b.fs, src_y, src_uv, b.cu,
-                       b.coef);
+                       b.coef, b.cost, b.qpc);
 }
 
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
                         const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cu, ncu, g.mb_w, max_slices, b.slice_first,
+    hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, b.slice_first,
                        b.slice_of_cu, b.nslices);
     if (!idr)
         hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
                            b.slice_of_cu, b.cu);
     if (deblock) {
-        hipLaunchKernelGGL(k_hevc_qpy, dim3((max_slices + 63) / 64), dim3(64), 0, s, b.fs, b.cu, ncu, b.slice_first,
-                           b.nslices, b.qpy);
+        hipLaunchKernelGGL(k_hevc_qpy, dim3(max_slices), dim3(256), 0, s, b.fs, b.qpc, ncu, b.slice_first, b.nslices,
+                           b.qpy);
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
         hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
