@@ -5,6 +5,7 @@
 #include "../net/dtls.h"
 #include "../net/rtp_h264.h"
 #include "../net/rtp_h265.h"
+#include "../net/sctp.h"
 #include "../net/srtp.h"
 
 namespace py = pybind11;
@@ -46,7 +47,90 @@ void register_net(py::module& m) {
         .def_property_readonly("error", &DtlsEndpoint::error)
         .def_property_readonly("peer_fingerprint", &DtlsEndpoint::peer_fingerprint)
         .def_property_readonly("srtp_profile", &DtlsEndpoint::srtp_profile)
-        .def("export_srtp_keys", [](DtlsEndpoint& d) { return B(d.export_srtp_keys()); });
+        .def("export_srtp_keys", [](DtlsEndpoint& d) { return B(d.export_srtp_keys()); })
+        .def("write", [](DtlsEndpoint& d, py::bytes b) { return BV(d.write(b)); })
+        .def("take_app_data", [](DtlsEndpoint& d) { return BV(d.take_app_data()); });
+    n.def("crc32c", [](py::bytes b) {
+        std::string s = b;
+        return crc32c(s.data(), s.size());
+    });
+    py::class_<SctpStats>(n, "SctpStats")
+        .def_readonly("packets_in", &SctpStats::packets_in)
+        .def_readonly("packets_out", &SctpStats::packets_out)
+        .def_readonly("data_in", &SctpStats::data_in)
+        .def_readonly("data_out", &SctpStats::data_out)
+        .def_readonly("retransmits", &SctpStats::retransmits)
+        .def_readonly("fast_retransmits", &SctpStats::fast_retransmits)
+        .def_readonly("t3_expiries", &SctpStats::t3_expiries)
+        .def_readonly("abandoned", &SctpStats::abandoned)
+        .def_readonly("forward_tsn_out", &SctpStats::forward_tsn_out)
+        .def_readonly("forward_tsn_in", &SctpStats::forward_tsn_in)
+        .def_readonly("sacks_in", &SctpStats::sacks_in)
+        .def_readonly("sacks_out", &SctpStats::sacks_out)
+        .def_readonly("dup_tsns", &SctpStats::dup_tsns)
+        .def_readonly("bad_checksum", &SctpStats::bad_checksum)
+        .def_readonly("bad_tag", &SctpStats::bad_tag)
+        .def_readonly("messages_in", &SctpStats::messages_in)
+        .def_readonly("messages_out", &SctpStats::messages_out);
+    py::class_<SctpAssociation>(n, "SctpAssociation")
+        .def(py::init<uint16_t, uint16_t, size_t>(), py::arg("local_port") = 5000, py::arg("remote_port") = 5000,
+             py::arg("max_message") = 256 * 1024)
+        .def("connect", [](SctpAssociation& a) { return BV(a.connect()); })
+        .def("feed", [](SctpAssociation& a, py::bytes p) { return BV(a.feed(p)); })
+        .def("send", [](SctpAssociation& a, uint16_t stream, uint32_t ppid, py::bytes d, bool unordered,
+                        int max_rtx, int lifetime) { return BV(a.send(stream, ppid, d, unordered, max_rtx, lifetime)); },
+             py::arg("stream"), py::arg("ppid"), py::arg("data"), py::arg("unordered") = false,
+             py::arg("max_retransmits") = -1, py::arg("lifetime_ms") = -1)
+        .def("tick", [](SctpAssociation& a) { return BV(a.tick()); })
+        .def("reset_streams", [](SctpAssociation& a, const std::vector<uint16_t>& s) { return BV(a.reset_streams(s)); })
+        .def("shutdown", [](SctpAssociation& a) { return BV(a.shutdown()); })
+        .def("abort", [](SctpAssociation& a, const std::string& why) { return BV(a.abort(why)); })
+        .def("take_messages", [](SctpAssociation& a) {
+            py::list out;
+            for (auto& m : a.take_messages())
+                out.append(py::make_tuple(m.stream, m.ppid, m.unordered, py::bytes(m.data)));
+            return out;
+        })
+        .def("take_reset_streams", &SctpAssociation::take_reset_streams)
+        .def_property_readonly("state", [](const SctpAssociation& a) { return (int)a.state(); })
+        .def_property_readonly("established", &SctpAssociation::established)
+        .def_property_readonly("stats", &SctpAssociation::stats, py::return_value_policy::copy)
+        .def_property_readonly("buffered_amount", &SctpAssociation::buffered_amount)
+        .def_property_readonly("rto_ms", &SctpAssociation::rto_ms)
+        .def_property_readonly("cwnd", &SctpAssociation::cwnd)
+        .def_property_readonly("peer_rwnd", &SctpAssociation::peer_rwnd)
+        .def_property_readonly("peer_supports_forward_tsn", &SctpAssociation::peer_supports_forward_tsn)
+        .def_property_readonly("error", &SctpAssociation::error)
+        .def("set_clock", &SctpAssociation::set_clock);
+    py::class_<DataChannelEndpoint>(n, "DataChannelEndpoint")
+        .def(py::init<bool, uint16_t, uint16_t, size_t>(), py::arg("dtls_server"), py::arg("local_port") = 5000,
+             py::arg("remote_port") = 5000, py::arg("max_message") = 256 * 1024)
+        .def("connect", [](DataChannelEndpoint& e) { return BV(e.connect()); })
+        .def("feed", [](DataChannelEndpoint& e, py::bytes p) { return BV(e.feed(p)); })
+        .def("tick", [](DataChannelEndpoint& e) { return BV(e.tick()); })
+        .def("open", [](DataChannelEndpoint& e, const std::string& label, const std::string& protocol, bool ordered,
+                        int max_rtx, int lifetime) {
+                 auto r = e.open(label, protocol, ordered, max_rtx, lifetime);
+                 return py::make_tuple(r.first, BV(r.second));
+             },
+             py::arg("label"), py::arg("protocol") = "", py::arg("ordered") = true, py::arg("max_retransmits") = -1,
+             py::arg("max_lifetime_ms") = -1)
+        .def("send", [](DataChannelEndpoint& e, uint16_t id, py::bytes d, bool binary) { return BV(e.send(id, d, binary)); },
+             py::arg("id"), py::arg("data"), py::arg("binary") = false)
+        .def("close", [](DataChannelEndpoint& e, uint16_t id) { return BV(e.close(id)); })
+        .def("take_events", [](DataChannelEndpoint& e) {
+            py::list out;
+            for (auto& ev : e.take_events())
+                out.append(py::make_tuple(ev.kind, ev.id, ev.label, ev.protocol, ev.binary, py::bytes(ev.data)));
+            return out;
+        })
+        .def("is_open", &DataChannelEndpoint::is_open)
+        .def("label", &DataChannelEndpoint::label)
+        .def("channels", &DataChannelEndpoint::channels)
+        .def_property_readonly("established", [](DataChannelEndpoint& e) { return e.sctp().established(); })
+        .def_property_readonly("stats", [](DataChannelEndpoint& e) { return e.sctp().stats(); })
+        .def_property_readonly("buffered_amount", [](DataChannelEndpoint& e) { return e.sctp().buffered_amount(); })
+        .def("set_clock", [](DataChannelEndpoint& e, int64_t ms) { e.sctp().set_clock(ms); });
     py::class_<RtpH264Packetizer>(n, "RtpH264Packetizer")
         .def(py::init<uint32_t, uint8_t, size_t, uint16_t>(), py::arg("ssrc"), py::arg("payload_type"),
              py::arg("max_payload") = 1150, py::arg("first_seq") = 0)

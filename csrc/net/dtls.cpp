@@ -143,10 +143,13 @@ void DtlsEndpoint::step() {
                 err_ = b;
             }
         }
-    } else {
-        char tmp[2048];
-        while (SSL_read(ssl, tmp, sizeof tmp) > 0) {
-        }  // no application data expected (no SCTP); drains alerts
+    }
+    if (done_) {
+        // application data (SCTP packets) that arrived with or after the final flight;
+        // SSL_read also processes alerts and renegotiation records
+        char tmp[16384];
+        int n;
+        while ((n = SSL_read(ssl, tmp, sizeof tmp)) > 0) app_in_.emplace_back(tmp, (size_t)n);
     }
 }
 
@@ -164,6 +167,18 @@ std::vector<std::string> DtlsEndpoint::feed(const std::string& d) {
 std::vector<std::string> DtlsEndpoint::tick() {
     if (!done_ && DTLSv1_handle_timeout((SSL*)ssl_) > 0) return drain();
     return {};
+}
+
+std::vector<std::string> DtlsEndpoint::write(const std::string& data) {
+    if (!done_ || failed_ || data.empty()) return {};
+    if (SSL_write((SSL*)ssl_, data.data(), (int)data.size()) <= 0) return {};
+    return drain();
+}
+
+std::vector<std::string> DtlsEndpoint::take_app_data() {
+    std::vector<std::string> v;
+    v.swap(app_in_);
+    return v;
 }
 
 std::string DtlsEndpoint::peer_fingerprint() const {

@@ -33,6 +33,11 @@ class DtlsEndpoint {
     std::string srtp_profile() const;
     // 60 bytes: client key | server key | client salt | server salt
     std::string export_srtp_keys() const;
+    // Application data (SCTP for WebRTC data channels, RFC 8261): encrypt one message into
+    // DTLS record(s) and return the datagrams to send; empty before the handshake is done.
+    std::vector<std::string> write(const std::string& data);
+    // Decrypted application-data records received by feed(), in arrival order.
+    std::vector<std::string> take_app_data();
 
    private:
     std::vector<std::string> drain();
@@ -47,6 +52,7 @@ class DtlsEndpoint {
     bool done_ = false;
     bool failed_ = false;
     std::string err_;
+    std::vector<std::string> app_in_;
 };
 
 // Certificate/key shared by all endpoints of the process.

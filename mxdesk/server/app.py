@@ -76,7 +76,8 @@ class MediaServer:
             self.audio = AudioPipeline(src) if src is not None else None
         self.whep = WhepEndpoint(pipeline, audio=self.audio,
                                  congestion_control=bool(getattr(cfg, "congestion_control", False)), host=getattr(cfg, "webrtc_host", None) or None,
-                                 udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0))
+                                 udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0),
+                                 on_input=self._on_client_message)
 
     # ------------------------------------------------------------------ app
     def make_app(self) -> web.Application:

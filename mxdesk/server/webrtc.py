@@ -12,6 +12,11 @@ of the reference's selkies pipeline, Dockerfile:439-444).
 * Media: native RFC 6184 packetizer (STAP-A / FU-A), native SRTP, 90 kHz timestamps from
   the capture clock; RTCP PLI/FIR -> IDR, generic NACK -> retransmission from a packet
   history, periodic SR + SDES.
+* Data channels (RFC 8831/8832 over SCTP over DTLS, RFC 8261): native SCTP association
+  (``csrc/net/sctp.cpp``) on the same DTLS session; the browser opens the channel (selkies
+  names it ``input``) and its text messages go through the same input parser as the
+  WebSocket control channel (keyboard / mouse / clipboard / gamepad / bitrate); the server
+  answers with ``{"type": "stats", ...}`` once a second.
 """
 from __future__ import annotations
 
@@ -127,6 +132,8 @@ class Answer:
     remote_fingerprint: str
     audio_pt: int | None = None  # PCMU (0) when the offer has an audio section and audio is on
     audio_mid: str | None = None
+    dc_mid: str | None = None        # accepted m=application (SCTP data channels)
+    remote_sctp_port: int = 5000
 
 
 def _has_pcmu(md: MediaDesc) -> bool:
@@ -135,11 +142,12 @@ def _has_pcmu(md: MediaDesc) -> bool:
 
 def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
                  level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None,
-                 codec: str = "h264") -> Answer:
+                 codec: str = "h264", datachannel: bool = True, max_message: int = 262144) -> Answer:
     """Answer one video section in the stream's codec (H.264 packetization-mode 1, or H.265
     with ``codec="hevc"``; ``level_idc`` is then general_level_idc) and, with ``audio_ssrc``,
-    one PCMU audio section; everything else is rejected with port 0.  All accepted sections
-    are BUNDLEd onto the single ICE-lite host candidate."""
+    one PCMU audio section, and with ``datachannel`` one ``UDP/DTLS/SCTP webrtc-datachannel``
+    section (RFC 8841); everything else is rejected with port 0.  All accepted sections are
+    BUNDLEd onto the single ICE-lite host candidate."""
     pick = pick_h265 if codec == "hevc" else pick_h264
     if codec == "hevc":
         rtpmap, fmtp = "H265/90000", f"profile-id=1;tier-flag=0;level-id={level_idc};tx-mode=SRST"
@@ -152,6 +160,7 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
     out_media: list[str] = []
     chosen = None
     audio = None  # (pt, mid)
+    dc = None     # (mid, remote sctp-port)
     bundle: list[str] = []
     hosts = [host] + [h for h in (extra_hosts or []) if h != host]
     cands = [f"a=candidate:{k + 1} 1 udp {2130706431 - k} {h} {port} typ host" for k, h in enumerate(hosts)]
@@ -179,7 +188,14 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
                           f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtpmap:0 PCMU/8000",
                           f"a=ssrc:{audio_ssrc} cname:mxdesk", f"a=ssrc:{audio_ssrc} msid:mxdesk audio0"]
             continue
-        # reject (data channels, second video, audio when disabled)
+        if md.kind == "application" and dc is None and datachannel and md.proto.upper().endswith("DTLS/SCTP") \
+                and "webrtc-datachannel" in md.fmts:
+            dc = (mid, int(md.attr("sctp-port") or 5000))
+            bundle.append(mid)
+            out_media += [f"m=application {port} UDP/DTLS/SCTP webrtc-datachannel", *transport,
+                          f"a=mid:{mid}", "a=sctp-port:5000", f"a=max-message-size:{max_message}"]
+            continue
+        # reject (legacy SCTP syntax, second video, audio when disabled)
         out_media += [f"m={md.kind} 0 {md.proto} {md.fmts[0] if md.fmts else '0'}", "c=IN IP4 0.0.0.0",
                       f"a=mid:{mid}", "a=inactive"]
     if chosen is None:
@@ -187,6 +203,8 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
                          "offer has no H.264 (packetization-mode=1, baseline-compatible) video section")
     if audio is not None:
         chosen.audio_pt, chosen.audio_mid = audio
+    if dc is not None:
+        chosen.dc_mid, chosen.remote_sctp_port = dc
     lines.insert(4, "a=group:BUNDLE " + " ".join(bundle))
     chosen.sdp = "\r\n".join(lines + out_media) + "\r\n"
     return chosen
@@ -256,8 +274,11 @@ class WebRtcPeer(asyncio.DatagramProtocol):
     HISTORY = 1024
 
     def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
-                 audio=None, congestion_control: bool = False):
+                 audio=None, congestion_control: bool = False, on_input=None):
         N = _native()
+        self.on_input = on_input  # callback(str) for data-channel text messages
+        self.dc = None            # DataChannelEndpoint once DTLS is up and the offer had m=application
+        self.dc_channels: dict[int, str] = {}
         self.pipeline = pipeline
         self.audio = audio
         self.audio_ssrc = (secrets.randbits(32) | 1) if audio is not None else None
@@ -286,7 +307,8 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.sub = None
         self.tasks: list[asyncio.Task] = []
         self.closed = asyncio.Event()
-        self.stats = {"stun": 0, "dtls_in": 0, "rtp_out": 0, "rtcp_in": 0, "pli": 0, "nack": 0, "rtx": 0}
+        self.stats = {"stun": 0, "dtls_in": 0, "rtp_out": 0, "rtcp_in": 0, "pli": 0, "nack": 0, "rtx": 0,
+                      "dc_in": 0, "dc_out": 0}
         self.last_consent = time.monotonic()
         self.ts0: int | None = None
         self.cc = CongestionController(pipeline, enabled=congestion_control)
@@ -321,6 +343,8 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                 self._send_all(self.dtls.feed(data), addr)
                 if self.dtls.handshake_done and self.srtp_tx is None:
                     self._on_dtls_done()
+                for pkt in self.dtls.take_app_data():
+                    self._on_sctp(pkt, addr)
             elif 128 <= b <= 191 and len(data) > 1 and 192 <= data[1] <= 223:
                 self._on_rtcp(data)
         except Exception:
@@ -366,6 +390,57 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             self.srtp_tx_audio = N.net.SrtpSession(sk, ss)
             self.asub = self.audio.subscribe(asyncio.get_running_loop())
             self.tasks.append(asyncio.create_task(self._audio_loop()))
+
+    # ------------------------------------------------------------------ data channels
+    def _sctp_out(self, packets, addr=None) -> None:
+        addr = addr or self.remote
+        if addr is None:
+            return
+        for p in packets:
+            self._send_all(self.dtls.write(p), addr)
+
+    def _on_sctp(self, pkt: bytes, addr) -> None:
+        if self.dc is None:
+            if self.answer is None or self.answer.dc_mid is None:
+                return
+            # we are the DTLS server: odd stream ids for channels we open; the browser opens
+            self.dc = _native().net.DataChannelEndpoint(True, 5000, self.answer.remote_sctp_port)
+        self._sctp_out(self.dc.feed(pkt), addr)
+        self._dc_events()
+
+    def _dc_events(self) -> None:
+        for kind, cid, label, _proto, binary, data in self.dc.take_events():
+            if kind == 0:
+                self.dc_channels[cid] = label
+                log.info("WebRTC peer %s: data channel %d '%s' open", self.id, cid, label)
+            elif kind == 1:
+                self.stats["dc_in"] += 1
+                if self.on_input is not None and not binary:
+                    try:
+                        self.on_input(data.decode("utf-8", "replace"))
+                    except Exception:
+                        log.exception("data-channel message %r", data[:64])
+            elif kind == 2:
+                self.dc_channels.pop(cid, None)
+
+    def dc_send(self, text: str, label: str | None = None) -> bool:
+        """Send one text message on the first open channel (or the one named ``label``)."""
+        if self.dc is None:
+            return False
+        for cid, lab in self.dc_channels.items():
+            if (label is None or lab == label) and self.dc.is_open(cid):
+                self._sctp_out(self.dc.send(cid, text.encode(), False))
+                self.stats["dc_out"] += 1
+                return True
+        return False
+
+    def _dc_stats(self) -> str:
+        import json
+
+        m = getattr(self.pipeline, "metrics", None)
+        snap = m.summary() if m is not None and hasattr(m, "summary") else {}
+        return json.dumps({"type": "stats", "rtp_out": self.stats["rtp_out"], "rtx": self.stats["rtx"],
+                           "kbps": self.cc.kbps, **{k: v for k, v in snap.items() if isinstance(v, (int, float))}})
 
     def _on_rtcp(self, data: bytes) -> None:
         if self.srtp_rx is None:
@@ -444,6 +519,12 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             if self.remote is not None and not self.dtls.handshake_done:
                 self._send_all(self.dtls.tick(), self.remote)
             now = time.monotonic()
+            if self.dc is not None:
+                self._sctp_out(self.dc.tick())
+                self._dc_events()
+                if now - getattr(self, "_last_dc_stats", 0.0) > 1.0 and self.dc_channels:
+                    self.dc_send(self._dc_stats())
+                    self._last_dc_stats = now
             if self.srtp_tx is not None and self.remote is not None and now - last_sr > 1.0:
                 sr = R.build_sr(self.ssrc, getattr(self, "last_ts", 0), self.pkt.packets, self.pkt.octets)
                 self.transport.sendto(self.srtp_tx.protect_rtcp(sr), self.remote)
@@ -473,8 +554,9 @@ class WhepEndpoint:
     """``POST /whep`` (application/sdp offer) -> 201 answer; ``DELETE /whep/{id}``."""
 
     def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A, audio=None,
-                 congestion_control: bool = False):
+                 congestion_control: bool = False, on_input=None):
         self.pipeline = pipeline
+        self.on_input = on_input
         self.audio = audio
         self.congestion_control = congestion_control
         self.host = host
@@ -492,7 +574,7 @@ class WhepEndpoint:
 
         offer = await request.text()
         peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc, audio=self.audio,
-                          congestion_control=self.congestion_control)
+                          congestion_control=self.congestion_control, on_input=self.on_input)
         try:
             answer = await peer.start()
         except ValueError as e:

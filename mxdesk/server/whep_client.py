@@ -23,10 +23,15 @@ def _native():
 
 
 def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_audio: bool = True,
-               h265_pt: int = 104) -> str:
-    lines = ["v=0", "o=- 4611731400430051336 2 IN IP4 127.0.0.1", "s=-", "t=0 0", "a=group:BUNDLE 0 1",
+               h265_pt: int = 104, with_datachannel: bool = False) -> str:
+    mids = "0 1" + (" 2" if with_datachannel else "")
+    lines = ["v=0", "o=- 4611731400430051336 2 IN IP4 127.0.0.1", "s=-", "t=0 0", f"a=group:BUNDLE {mids}",
              "a=msid-semantic: WMS"]
     media = []
+    if with_datachannel:  # the section browsers put in the offer after createDataChannel()
+        media += ["m=application 9 UDP/DTLS/SCTP webrtc-datachannel", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
+                  f"a=ice-pwd:{pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:2",
+                  "a=sctp-port:5000", "a=max-message-size:262144"]
     if with_audio:
         media += ["m=audio 9 UDP/TLS/RTP/SAVPF 111 0", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
                   f"a=ice-pwd:{pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:1", "a=recvonly",
@@ -56,6 +61,8 @@ class WhepResult:
     arrival_us: list[int] = field(default_factory=list)  # CLOCK_MONOTONIC us when each AU completed
     audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
     audio_seqs: list[int] = field(default_factory=list)
+    dc_received: list[str] = field(default_factory=list)  # server -> client data-channel messages
+    dc_sent: int = 0
 
 
 class _Client(asyncio.DatagramProtocol):
@@ -70,18 +77,22 @@ class _Client(asyncio.DatagramProtocol):
 
 
 async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
-                    timeout: float = 30.0) -> WhepResult:
+                    timeout: float = 30.0, dc_messages: list[str] | None = None,
+                    dc_wait_stats: bool = False) -> WhepResult:
     """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
 
     ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
     ``pli_after``: send a PLI after that many frames (the server must answer with an IDR).
+    ``dc_messages``: offer a data channel, open ``input`` on it (SCTP client side, even
+    stream id) and send these text messages; the call returns once all are acknowledged
+    (and, with ``dc_wait_stats``, a server stats message has arrived).
     """
     import aiohttp
 
     N = _native()
     dtls = N.net.DtlsEndpoint(False)
     ufrag, pwd = secrets.token_hex(4), secrets.token_hex(12)
-    offer = make_offer(ufrag, pwd, dtls.fingerprint)
+    offer = make_offer(ufrag, pwd, dtls.fingerprint, with_datachannel=dc_messages is not None)
     res = WhepResult()
     t0 = time.monotonic()
     async with aiohttp.ClientSession(auth=auth) as s:
@@ -141,6 +152,44 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
             return rx_ctx[ssrc]
         tx = N.net.SrtpSession(km[0:16], km[32:46])   # client -> server (RTCP)
         res.connect_ms = (time.monotonic() - t0) * 1000
+        dc = None
+        dc_id = -1
+        app = next((m for m in ans.media if m.kind == "application" and m.port), None)
+
+        def sctp_out(packets) -> None:
+            for p in packets:
+                for dg in dtls.write(p):
+                    tr.sendto(dg)
+        if dc_messages is not None:
+            if app is None:
+                raise RuntimeError("answer rejected the data channel")
+            dc = N.net.DataChannelEndpoint(False, 5000, int(app.attr("sctp-port") or 5000))
+            out = dc.connect()
+            dc_id, more = dc.open("input")
+            for msg in dc_messages:
+                more += dc.send(dc_id, msg.encode(), False)
+            res.dc_sent = len(dc_messages)
+            sctp_out(out + more)
+
+        def on_dtls(d: bytes) -> None:
+            sctp_out_raw = dtls.feed(d)
+            for dg in sctp_out_raw:
+                tr.sendto(dg)
+            for p in dtls.take_app_data():
+                if dc is not None:
+                    sctp_out(dc.feed(p))
+            if dc is not None:
+                for kind, _cid, _label, _proto, _binary, data in dc.take_events():
+                    if kind == 1:
+                        res.dc_received.append(data.decode("utf-8", "replace"))
+
+        def dc_pending() -> bool:
+            if dc is None:
+                return False
+            if dc.buffered_amount or not dc.is_open(dc_id):
+                return True
+            return dc_wait_stats and not any('"stats"' in m for m in res.dc_received)
+        last_tick = time.monotonic()
         my_ssrc = secrets.randbits(32)
         hevc = " H265/90000" in res.answer
         depk = R.H265Depacketizer() if hevc else R.H264Depacketizer()
@@ -150,8 +199,22 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
         sent_pli = False
         nacked: set[int] = set()
         media_ssrc = 0
-        while len(res.aus) < n_frames:
-            d = await asyncio.wait_for(cl.q.get(), max(0.1, deadline - time.monotonic()))
+        while len(res.aus) < n_frames or dc_pending():
+            if dc is not None and time.monotonic() - last_tick > 0.05:
+                sctp_out(dc.tick())
+                last_tick = time.monotonic()
+            try:
+                d = await asyncio.wait_for(cl.q.get(), 0.05 if dc is not None else
+                                           max(0.1, deadline - time.monotonic()))
+            except asyncio.TimeoutError:
+                if time.monotonic() > deadline:
+                    raise
+                continue
+            if time.monotonic() > deadline:
+                raise asyncio.TimeoutError()
+            if 20 <= d[0] <= 63:
+                on_dtls(d)
+                continue
             if not 128 <= d[0] <= 191:
                 continue
             if 192 <= d[1] <= 223:

@@ -2,13 +2,17 @@
 // decodes them with WebCodecs (hardware decoder on the viewer's machine) and paints a
 // canvas; mouse/keyboard/clipboard events go back as selkies-style text messages.
 // `?transport=webrtc` instead plays the stream through RTCPeerConnection (WHEP offer/answer
-// against POST /whep; SRTP video into a <video> element) and keeps /mxws?media=0 for input.
+// against POST /whep; SRTP video into a <video> element); input then travels on an SCTP data
+// channel named "input" (selkies' channel), with /mxws?media=0 as the fallback until it opens.
 "use strict";
 const mxdesk = (() => {
   const HDR = 36;
-  let ws, decoder, canvas, ctx, statsEl, msgEl, cfg = null, waitingKey = true;
+  let ws, dc = null, decoder, canvas, ctx, statsEl, msgEl, cfg = null, waitingKey = true;
   let frames = 0, bytes = 0, lastStats = performance.now(), decodeTimes = [];
-  const sendQ = (m) => { if (ws && ws.readyState === 1) ws.send(m); };
+  const sendQ = (m) => {
+    if (dc && dc.readyState === "open") dc.send(m);
+    else if (ws && ws.readyState === 1) ws.send(m);
+  };
 
   function parse(buf) {
     const dv = new DataView(buf);
@@ -146,6 +150,17 @@ const mxdesk = (() => {
     const pc = new RTCPeerConnection({ iceServers });
     pc.addTransceiver("video", { direction: "recvonly" });
     pc.addTransceiver("audio", { direction: "recvonly" });
+    const ch = pc.createDataChannel("input", { ordered: true });
+    ch.onopen = () => { dc = ch; };
+    ch.onclose = () => { if (dc === ch) dc = null; };
+    ch.onmessage = (ev) => {
+      try {
+        const m = JSON.parse(ev.data);
+        if (m.type === "stats") serverStats = `\nserver ${(m.encoded_fps_1s || 0).toFixed(1)} fps ` +
+          `${Math.round(m.bitrate_kbps_1s || 0)} kbps qp ${m.qp || 0} rtx ${m.rtx}`;
+      } catch (e) { /* not JSON */ }
+    };
+    let serverStats = "";
     const audioEl = new Audio();
     pc.ontrack = (ev) => {
       if (ev.track.kind === "audio") {
@@ -172,7 +187,7 @@ const mxdesk = (() => {
       st.forEach((x) => {
         if (x.type === "inbound-rtp" && x.kind === "video") {
           statsEl.textContent = `webrtc ${x.frameWidth}x${x.frameHeight}\n${(x.framesPerSecond || 0).toFixed(1)} fps ` +
-            `lost ${x.packetsLost} nack ${x.nackCount} pli ${x.pliCount}`;
+            `lost ${x.packetsLost} nack ${x.nackCount} pli ${x.pliCount}` + (dc ? " dc" : "") + serverStats;
         }
       });
     }, 1000);
