@@ -33,6 +33,25 @@ class XImage(ctypes.Structure):  # leading fields of Xlib's XImage (x86_64 layou
                 ("depth", ctypes.c_int), ("bytes_per_line", ctypes.c_int), ("bits_per_pixel", ctypes.c_int)]
 
 
+class XFixesCursorImage(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_short), ("y", ctypes.c_short), ("width", ctypes.c_ushort),
+                ("height", ctypes.c_ushort), ("xhot", ctypes.c_ushort), ("yhot", ctypes.c_ushort),
+                ("cursor_serial", ctypes.c_ulong), ("pixels", ctypes.POINTER(ctypes.c_ulong)),
+                ("atom", ctypes.c_ulong), ("name", ctypes.c_char_p)]
+
+
+def argb_longs_to_rgba(pixels: np.ndarray, width: int, height: int) -> np.ndarray:
+    """XFixes cursor pixels (one premultiplied 0xAARRGGBB per ``unsigned long``) -> straight
+    RGBA (H, W, 4) uint8, the layout a PNG cursor image needs."""
+    p = np.asarray(pixels, np.uint64)[: width * height].astype(np.uint32).reshape(height, width)
+    a = (p >> 24) & 0xFF
+    rgb = np.stack([(p >> 16) & 0xFF, (p >> 8) & 0xFF, p & 0xFF], axis=-1).astype(np.uint32)
+    nz = a > 0
+    # un-premultiply (X cursors are premultiplied ARGB)
+    rgb[nz] = np.minimum(255, (rgb[nz] * 255 + a[nz, None] // 2) // a[nz, None])
+    return np.concatenate([rgb, a[..., None]], axis=-1).astype(np.uint8)
+
+
 class X11Capture:
     def __init__(self, display: str = ":0", width: int | None = None, height: int | None = None):
         self.x11 = ctypes.CDLL(ctypes.util.find_library("X11") or "libX11.so.6")
@@ -52,6 +71,7 @@ class X11Capture:
         x.XGetImage.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int, ctypes.c_int, ctypes.c_uint,
                                 ctypes.c_uint, ctypes.c_ulong, ctypes.c_int]
         x.XDestroyImage = getattr(x, "XDestroyImage", None)
+        self.display_name = display
         self.dpy = x.XOpenDisplay(display.encode())
         if not self.dpy:
             raise OSError(f"cannot open X display {display}")
@@ -100,6 +120,55 @@ class X11Capture:
         self.shm = (info, img, size)
         self.view = np.ctypeslib.as_array(ctypes.cast(info.shmaddr, ctypes.POINTER(ctypes.c_uint8)), shape=(size,))
         self.pitch = img.contents.bytes_per_line
+
+    def _release_shm(self) -> None:
+        if self.shm is not None:
+            info, img, _ = self.shm
+            self.xext.XShmDetach.argtypes = [ctypes.c_void_p, ctypes.POINTER(XShmSegmentInfo)]
+            self.xext.XShmDetach(self.dpy, ctypes.byref(info))
+            self.x11.XSync.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            self.x11.XSync(self.dpy, 0)
+            self.libc.shmdt.argtypes = [ctypes.c_void_p]
+            self.libc.shmdt(info.shmaddr)
+            self.shm = None
+
+    def resize(self, width: int, height: int) -> None:
+        """Re-create the capture image after the screen changed size (RandR resize)."""
+        self._release_shm()
+        self.w, self.h = int(width), int(height)
+        try:
+            self._init_shm(self.x11.XDefaultScreen(self.dpy))
+        except OSError:
+            self.shm = None
+
+    def cursor_image(self):
+        """Current cursor as ``(serial, xhot, yhot, rgba)`` via XFixesGetCursorImage, or None
+        when XFixes is unavailable (selkies' remote-cursor feature)."""
+        if not hasattr(self, "_xfixes"):
+            try:
+                xf = ctypes.CDLL(ctypes.util.find_library("Xfixes") or "libXfixes.so.3")
+                xf.XFixesGetCursorImage.restype = ctypes.POINTER(XFixesCursorImage)
+                xf.XFixesGetCursorImage.argtypes = [ctypes.c_void_p]
+                self.x11.XFree.argtypes = [ctypes.c_void_p]
+                self._xfixes = xf
+            except OSError:
+                self._xfixes = None
+        if self._xfixes is None:
+            return None
+        if not hasattr(self, "_cursor_dpy"):
+            # own connection: Xlib is not thread-safe and grab() runs on the pipeline thread
+            self._cursor_dpy = self.x11.XOpenDisplay(self.display_name.encode())
+        if not self._cursor_dpy:
+            return None
+        ci = self._xfixes.XFixesGetCursorImage(self._cursor_dpy)
+        if not ci:
+            return None
+        c = ci.contents
+        n = c.width * c.height
+        px = np.ctypeslib.as_array(c.pixels, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
+        out = (int(c.cursor_serial), int(c.xhot), int(c.yhot), argb_longs_to_rgba(px, c.width, c.height))
+        self.x11.XFree(ci)
+        return out
 
     def grab(self) -> np.ndarray:
         """One frame as an (H, W, 4) uint8 BGRx array."""

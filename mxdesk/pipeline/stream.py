@@ -121,6 +121,8 @@ class StreamPipeline:
         self._force_idr = True
         self._pending_bitrate: int | None = None
         self._cursor = (-1, -1)
+        self._pending_resize: tuple[int, int] | None = None
+        self.resizes = 0
         self.frames_out = 0
         self.last_frame_t = 0.0
         self.restarts = 0
@@ -216,6 +218,29 @@ class StreamPipeline:
         stream's VUI timing stays at the session rate."""
         self.pace_fps = float(max(1.0, min(float(fps), 240.0)))
 
+    def resize(self, width: int, height: int) -> tuple[int, int]:
+        """Client-driven resize (``WEBRTC_ENABLE_RESIZE``): the next frame is produced by a new
+        session at the (sanitised) size, starting with an IDR; returns that size.  The
+        desktop and the encoded stream both take the new size (the X screen is resized by
+        the caller through RandR)."""
+        from ..display.randr import clamp_size
+
+        w, h = clamp_size(width, height)
+        self._pending_resize = (w, h)
+        return w, h
+
+    def _apply_resize(self, w: int, h: int) -> None:
+        if (w, h) == (self.width, self.height) and (self.out_w, self.out_h) == (w, h):
+            return
+        if self.capture is not None and hasattr(self.capture, "resize"):
+            self.capture.resize(w, h)
+        self.width, self.height = w, h
+        self.out_w, self.out_h = w, h
+        self._make_session()
+        self._force_idr = True
+        self.resizes += 1
+        log.info("session resized to %dx%d", w, h)
+
     def set_cursor(self, x: int, y: int) -> None:
         self._cursor = (int(x), int(y))
 
@@ -241,6 +266,9 @@ class StreamPipeline:
     # ------------------------------------------------------------------ loop
     def step(self) -> EncodedFrame:
         """Produce one frame synchronously (no pacing); publishes to subscribers."""
+        pending, self._pending_resize = self._pending_resize, None
+        if pending is not None:
+            self._apply_resize(*pending)
         force = self._force_idr
         self._force_idr = False
         n = self.frames_out
@@ -303,7 +331,7 @@ class StreamPipeline:
     def status(self) -> dict:
         return {"backend": self.backend, "device": self.device, "width": self.out_w, "height": self.out_h,
                 "fps": self.fps, "frames": self.frames_out, "clients": self.subscribers, "restarts": self.restarts,
-                "last_error": self.last_error, **self.metrics.summary()}
+                "last_error": self.last_error, "resizes": self.resizes, **self.metrics.summary()}
 
 
 def frame_header(fr: EncodedFrame, t_send_us: int) -> bytes:

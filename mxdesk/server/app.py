@@ -15,6 +15,12 @@ selkies-gstreamer-entrypoint.sh:44-47 (``--addr=0.0.0.0 --port=8080``) and, when
 
 Basic auth (ENABLE_BASIC_AUTH, user ``user``, password BASIC_AUTH_PASSWORD or PASSWD) and
 HTTPS (ENABLE_HTTPS_WEB + HTTPS_WEB_CERT/KEY) follow the reference contract.
+
+Remote -> client state (``desktop_sync``): clipboard changes (SELKIES_ENABLE_CLIPBOARD) and
+cursor images (SELKIES_ENABLE_CURSORS, X capture only) are pushed to every /mxws client and
+every WebRTC data channel.  With WEBRTC_ENABLE_RESIZE a client ``r,WxH`` / ``{"type":
+"resize"}`` message resizes the X screen (RandR) and restarts the session at that size; the
+WebSocket clients get a new ``config`` message before the first frame of the new size.
 """
 from __future__ import annotations
 
@@ -59,6 +65,15 @@ class MediaServer:
         self.start_pipeline = start_pipeline
         self.clients: set[web.WebSocketResponse] = set()
         self.resize_enabled = bool(getattr(cfg, "enable_resize", False))
+        from .desktop_sync import ClipboardSync, CursorSync
+
+        x_display = getattr(cfg, "display", None) if pipeline.capture is not None else None
+        self.x_display = x_display
+        self.clipboard = ClipboardSync(self.injector, x_display) if bool(getattr(cfg, "enable_clipboard", True)) \
+            else None
+        self.cursors = CursorSync(pipeline.capture) if (pipeline.capture is not None and
+                                                         bool(getattr(cfg, "enable_cursors", True))) else None
+        self._sync_task: asyncio.Task | None = None
         from .gamepad import GamepadServer
         from .webrtc import WhepEndpoint
 
@@ -117,8 +132,12 @@ class MediaServer:
             self.pipeline.start()
         if self.audio is not None:
             self.audio.start()
+        if self.clipboard is not None or self.cursors is not None:
+            self._sync_task = asyncio.create_task(self._sync_loop())
 
     async def _on_cleanup(self, app):
+        if self._sync_task is not None:
+            self._sync_task.cancel()
         self.whep.close_all()
         if self.audio is not None:
             self.audio.stop()
@@ -181,6 +200,8 @@ class MediaServer:
             "height": p.out_h, "fps": p.fps, "resize": self.resize_enabled,
             "audio": {"codec": "pcm_s16le", "rate": RATE, "channels": CHANNELS} if want_audio else None,
         }))
+        if self.cursors is not None and self.cursors.last_message:
+            await ws.send_str(self.cursors.last_message)
         sub = p.subscribe(asyncio.get_running_loop()) if media else None
         self.clients.add(ws)
         sender = asyncio.create_task(self._send_loop(ws, sub)) if media else None
@@ -202,12 +223,22 @@ class MediaServer:
             self.clients.discard(ws)
         return ws
 
+    def _config_message(self, width: int, height: int) -> str:
+        p = self.pipeline
+        return json.dumps({"type": "config", "codec": codec_string(getattr(p, "codec", "h264"), width, height, p.fps),
+                           "width": width, "height": height, "fps": p.fps, "resize": self.resize_enabled,
+                           "audio": None, "reconfigure": True})
+
     async def _send_loop(self, ws: web.WebSocketResponse, sub) -> None:
         from .. import native
 
+        dims = (self.pipeline.out_w, self.pipeline.out_h)
         while not ws.closed:
             fr = await sub.queue.get()
             try:
+                if (fr.width, fr.height) != dims:  # resized session: new decoder config first
+                    dims = (fr.width, fr.height)
+                    await ws.send_str(self._config_message(*dims))
                 await ws.send_bytes(frame_header(fr, native().now_us()) + fr.au)
             except (ConnectionResetError, RuntimeError):
                 return
@@ -243,9 +274,71 @@ class MediaServer:
                 self.gamepad.apply(ev)
         elif ev.kind == "resize":
             if self.resize_enabled:
-                log.info("client resize request %dx%d (applied on next session restart)", ev.width, ev.height)
+                self.request_resize(ev.width, ev.height)
+            else:
+                log.info("client resize %dx%d ignored (WEBRTC_ENABLE_RESIZE=false)", ev.width, ev.height)
         else:
             self.injector.apply(ev)
+            if ev.kind == "clipboard" and self.clipboard is not None:
+                self.clipboard.write(ev.text)
+
+    # ------------------------------------------------------------------ resize / sync
+    def request_resize(self, width: int, height: int) -> None:
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            loop = None
+        if loop is not None:  # RandR runs subprocesses: keep them off the event loop
+            loop.run_in_executor(None, self._resize_blocking, width, height)
+        else:
+            self._resize_blocking(width, height)
+
+    def _resize_blocking(self, width: int, height: int) -> None:
+        from ..display.randr import clamp_size, resize_display
+
+        w, h = clamp_size(width, height)
+        if (w, h) == (self.pipeline.out_w, self.pipeline.out_h):
+            return
+        if self.x_display:
+            try:
+                resize_display(self.x_display, w, h, float(getattr(self.cfg, "refresh", 60) or 60))
+            except Exception as e:
+                log.warning("RandR resize to %dx%d failed: %s", w, h, e)
+                return
+        self.pipeline.resize(w, h)
+        if hasattr(self.injector, "w"):
+            self.injector.w, self.injector.h = w, h
+        log.info("client resize -> %dx%d", w, h)
+
+    def broadcast(self, text: str) -> None:
+        """One control message to every /mxws client and every WebRTC data channel."""
+        for ws in list(self.clients):
+            if not ws.closed:
+                asyncio.ensure_future(ws.send_str(text))
+        for peer in list(self.whep.peers.values()):
+            peer.dc_send(text)
+
+    async def _sync_loop(self, period: float = 0.1, clipboard_every: int = 10) -> None:
+        loop = asyncio.get_running_loop()
+        n = 0
+        while True:
+            try:
+                if self.cursors is not None:
+                    msg = await loop.run_in_executor(None, self.cursors.poll)
+                    if msg:
+                        self.broadcast(msg)
+                if self.clipboard is not None and n % clipboard_every == 0:
+                    text = await loop.run_in_executor(None, self.clipboard.poll)
+                    if text is not None:
+                        from .desktop_sync import clipboard_message
+
+                        self.broadcast(clipboard_message(text))
+            except asyncio.CancelledError:
+                raise
+            except Exception:
+                log.exception("desktop sync")
+            n += 1
+            await asyncio.sleep(period)
 
 
 def ssl_context(cfg: Any) -> ssl.SSLContext | None:

@@ -75,6 +75,44 @@ def test_gpu_pipeline_over_webrtc(gpu, monkeypatch):
     assert all(b == a + 1 for a, b in zip(ids, ids[1:]))
 
 
+def test_gpu_live_resize_and_webrtc_datachannel_input(gpu, monkeypatch):
+    """Client-driven resize on the HIP session (new Session at the new size, IDR first, the
+    independent decoder sees the new dimensions) and input over the SCTP data channel."""
+    from mxdesk.pipeline.stream import StreamPipeline
+    from mxdesk.server.app import MediaServer, serve
+    from mxdesk.server.whep_client import whep_view
+    from mxdesk.utils import config as C
+
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg = C.load(env={"ENABLE_BASIC_AUTH": "false", "SIZEW": "320", "SIZEH": "192",
+                      "WEBRTC_ENABLE_RESIZE": "true"}, argv=[])
+    pipe = StreamPipeline(320, 192, 60, backend="gpu", bitrate_kbps=0, paced=False)
+    a = pipe.step()
+    assert (a.width, a.height) == (320, 192)
+    assert pipe.resize(647, 360) == (640, 360)
+    frs = [pipe.step() for _ in range(4)]
+    assert all((f.width, f.height) == (640, 360) for f in frs) and frs[0].idr
+    dec = Decoder().decode(b"".join(f.au for f in frs))
+    assert len(dec) == 4 and dec[0][0].shape == (360, 640)
+    ids = [read_barcode(y)[0] for y, _, _ in dec]
+    assert all(b == x + 1 for x, b in zip(ids, ids[1:]))
+
+    pipe2 = StreamPipeline(320, 192, 60, backend="gpu", bitrate_kbps=0)
+    srv = MediaServer(pipe2, cfg)
+
+    async def go():
+        port = _free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await whep_view(f"http://127.0.0.1:{port}/whep", 6, dc_messages=["m,10,20,0,0", "kd,97"])
+        finally:
+            await runner.cleanup()
+
+    res = asyncio.run(go())
+    assert len(Decoder().decode(res.stream)) == 6
+    assert (srv.injector.x, srv.injector.y) == (10, 20) and srv.injector.keys_down == {97}
+
+
 def test_gpu_framegrab_matches_synth(gpu):
     from mxdesk.server.framegrab import FrameGrabber
 

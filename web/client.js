@@ -28,6 +28,24 @@ const mxdesk = (() => {
     };
   }
 
+  // remote -> client state pushed by the server (selkies message shapes)
+  function onControl(m) {
+    if (m.type === "clipboard" && m.data) {
+      const text = decodeURIComponent(escape(atob(m.data.content)));
+      if (navigator.clipboard && navigator.clipboard.writeText) navigator.clipboard.writeText(text).catch(() => {});
+    } else if (m.type === "cursor" && m.data) {
+      const h = m.data.hotspot || { x: 0, y: 0 };
+      canvas.style.cursor = `url(data:image/png;base64,${m.data.curdata}) ${h.x} ${h.y}, auto`;
+    }
+  }
+
+  let resizeTimer = null;
+  function requestResize() {
+    if (!cfg || !cfg.resize) return;
+    clearTimeout(resizeTimer);
+    resizeTimer = setTimeout(() => sendQ(`r,${window.innerWidth}x${window.innerHeight}`), 300);
+  }
+
   function makeDecoder() {
     decoder = new VideoDecoder({
       output: (frame) => {
@@ -116,9 +134,7 @@ const mxdesk = (() => {
       const t = e.clipboardData.getData("text");
       if (t) sendQ("cw," + btoa(unescape(encodeURIComponent(t))));
     });
-    window.addEventListener("resize", () => {
-      if (cfg && cfg.resize) sendQ(`r,${window.innerWidth}x${window.innerHeight}`);
-    });
+    window.addEventListener("resize", requestResize);
     gamepads();
   }
 
@@ -156,7 +172,8 @@ const mxdesk = (() => {
     ch.onmessage = (ev) => {
       try {
         const m = JSON.parse(ev.data);
-        if (m.type === "stats") serverStats = `\nserver ${(m.encoded_fps_1s || 0).toFixed(1)} fps ` +
+        if (m.type !== "stats") { onControl(m); return; }
+        serverStats = `\nserver ${(m.encoded_fps_1s || 0).toFixed(1)} fps ` +
           `${Math.round(m.bitrate_kbps_1s || 0)} kbps qp ${m.qp || 0} rtx ${m.rtx}`;
       } catch (e) { /* not JSON */ }
     };
@@ -200,7 +217,11 @@ const mxdesk = (() => {
     ws.onmessage = (ev) => {
       if (typeof ev.data === "string") {
         const m = JSON.parse(ev.data);
-        if (m.type === "config") { cfg = m; waitingKey = true; makeDecoder(); msgEl.textContent = ""; }
+        if (m.type === "config") {
+          const first = !cfg;
+          cfg = m; waitingKey = true; if (ctx) makeDecoder(); msgEl.textContent = "";
+          if (first) requestResize();  // follow the browser window from the start (WEBRTC_ENABLE_RESIZE)
+        } else onControl(m);
         return;
       }
       if (new Uint8Array(ev.data, 0, 4).every((b, i) => b === "MXA1".charCodeAt(i))) { onAudio(ev.data); return; }
