@@ -4,7 +4,8 @@ Replaces the selkies-gstreamer web/signalling server started by
 selkies-gstreamer-entrypoint.sh:44-47 (``--addr=0.0.0.0 --port=8080``) and, when
 ``NOVNC_ENABLE=true``, the noVNC/websockify front end (entrypoint.sh:121-125):
 
-  GET  /                 web client (WebCodecs H.264 player + input capture), PWA manifest
+  GET  /                 web client (WebCodecs H.264 player + input capture), PWA manifest;
+                         with NOVNC_ENABLE=true the VNC viewer (web/vnc.html + vnc.js)
   GET  /health           liveness/readiness (200 when frames flow)
   GET  /turn             RTCConfiguration JSON (STUN/TURN; HMAC or legacy credentials)
   GET  /metrics          Prometheus exposition
@@ -149,7 +150,9 @@ class MediaServer:
 
     # ------------------------------------------------------------------ http handlers
     async def index(self, request: web.Request) -> web.StreamResponse:
-        f = self.web_root / "index.html"
+        # NOVNC_ENABLE=true: the VNC viewer (RFB over /websockify) is the front page, as noVNC's
+        # vnc.html is in the reference (entrypoint.sh:124)
+        f = self.web_root / ("vnc.html" if self.rfb is not None else "index.html")
         if f.exists():
             return web.FileResponse(f)
         return web.Response(text="<html><body>mxdesk</body></html>", content_type="text/html")
