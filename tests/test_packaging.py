@@ -84,3 +84,16 @@ def test_desktop_command_override():
 def test_host_sanitizers_clean():
     r = subprocess.run(["bash", str(ROOT / "tools/sanitize.sh")], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "sanitize: ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_dockerfile_optional_app_bundle_and_wine():
+    text = (ROOT / "docker/Dockerfile").read_text()
+    for arg in ("ARG APPS=core", "ARG WINE=false", "ARG WINE_BRANCH=staging"):
+        assert arg in text
+    assert "winehq-${WINE_BRANCH}" in text and "winetricks" in text and "lutris" in text
+    assert "firefox" in text and "libreoffice" in text and "kscreenlockerrc" in text
+    import yaml
+
+    ci = yaml.safe_load((ROOT / ".github/workflows/ci.yml").read_text())
+    tags = [m["tag"] for m in ci["jobs"]["image"]["strategy"]["matrix"]["include"]]
+    assert "kde-full" in tags
