@@ -76,7 +76,7 @@ class MediaServer:
                                                          bool(getattr(cfg, "enable_cursors", True))) else None
         self._sync_task: asyncio.Task | None = None
         from .gamepad import GamepadServer
-        from .webrtc import WhepEndpoint
+        from .webrtc import WhepEndpoint, turn_relay_settings
 
         self.gamepad = GamepadServer(getattr(cfg, "js_dir", None)) if bool(getattr(cfg, "enable_gamepad", True)) else None
 
@@ -93,7 +93,7 @@ class MediaServer:
         self.whep = WhepEndpoint(pipeline, audio=self.audio,
                                  congestion_control=bool(getattr(cfg, "congestion_control", False)), host=getattr(cfg, "webrtc_host", None) or None,
                                  udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0),
-                                 on_input=self._on_client_message)
+                                 on_input=self._on_client_message, turn=turn_relay_settings(cfg))
 
     # ------------------------------------------------------------------ app
     def make_app(self) -> web.Application:

@@ -142,7 +142,8 @@ def _has_pcmu(md: MediaDesc) -> bool:
 
 def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
                  level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None,
-                 codec: str = "h264", datachannel: bool = True, max_message: int = 262144) -> Answer:
+                 codec: str = "h264", datachannel: bool = True, max_message: int = 262144,
+                 relay_candidates: list[str] | None = None) -> Answer:
     """Answer one video section in the stream's codec (H.264 packetization-mode 1, or H.265
     with ``codec="hevc"``; ``level_idc`` is then general_level_idc) and, with ``audio_ssrc``,
     one PCMU audio section, and with ``datachannel`` one ``UDP/DTLS/SCTP webrtc-datachannel``
@@ -164,6 +165,7 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
     bundle: list[str] = []
     hosts = [host] + [h for h in (extra_hosts or []) if h != host]
     cands = [f"a=candidate:{k + 1} 1 udp {2130706431 - k} {h} {port} typ host" for k, h in enumerate(hosts)]
+    cands += list(relay_candidates or [])
     transport = [f"c=IN IP4 {host}", *cands, "a=end-of-candidates",
                  f"a=ice-ufrag:{ice_ufrag}", f"a=ice-pwd:{ice_pwd}", f"a=fingerprint:{fingerprint}", "a=setup:passive"]
     for md in offer.media:
@@ -269,13 +271,36 @@ class CongestionController:
             self._apply(self.kbps * 1.08)
 
 
+class RelayAddr(tuple):
+    """A browser address reached through our TURN allocation (sends go via the relay)."""
+
+
+def turn_relay_settings(cfg) -> dict | None:
+    """Server-side TURN relay settings from the TURN_* config (shared-secret HMAC or legacy
+    credentials), or None when no TURN server is configured / MXDESK_TURN_RELAY=false."""
+    if cfg is None or not getattr(cfg, "turn_host", None) or not getattr(cfg, "turn_relay", True):
+        return None
+    from .turn import hmac_credentials
+
+    if getattr(cfg, "turn_shared_secret", None):
+        user, pw = hmac_credentials(cfg.turn_shared_secret, "mxdesk-server")
+    elif getattr(cfg, "turn_username", None) and getattr(cfg, "turn_password", None):
+        user, pw = cfg.turn_username, cfg.turn_password
+    else:
+        return None
+    return {"host": cfg.turn_host, "port": int(cfg.turn_port or 3478), "username": user, "password": pw,
+            "protocol": (cfg.turn_protocol or "udp").lower(), "tls": bool(cfg.turn_tls)}
+
+
 # ------------------------------------------------------------------ peer
 class WebRtcPeer(asyncio.DatagramProtocol):
     HISTORY = 1024
 
     def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
-                 audio=None, congestion_control: bool = False, on_input=None):
+                 audio=None, congestion_control: bool = False, on_input=None, turn: dict | None = None):
         N = _native()
+        self.turn = turn          # server-side relay settings (host, port, username, password, protocol, tls)
+        self.relay = None         # TurnClient once allocated
         self.on_input = on_input  # callback(str) for data-channel text messages
         self.dc = None            # DataChannelEndpoint once DTLS is up and the offer had m=application
         self.dc_channels: dict[int, str] = {}
@@ -323,12 +348,36 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         if codec == "hevc":
             p = self.pipeline
             level = _native().hevc_level(p.out_w, p.out_h, p.fps)
+        relay_cands = []
+        if self.turn:
+            relay_cands = await self._allocate_relay()
         self.answer = build_answer(self.offer_sdp, self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port,
-                                   self.ssrc, level, self.audio_ssrc, self.extra_hosts, codec=codec)
+                                   self.ssrc, level, self.audio_ssrc, self.extra_hosts, codec=codec,
+                                   relay_candidates=relay_cands)
         packetizer = _native().net.RtpH265Packetizer if codec == "hevc" else _native().net.RtpH264Packetizer
         self.pkt = packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
         self.tasks.append(asyncio.create_task(self._timers()))
         return self.answer.sdp
+
+    async def _allocate_relay(self) -> list[str]:
+        """TURN allocation + permissions for the offer's candidates -> relay candidate lines."""
+        from .turn_client import TurnClient, TurnError, offer_candidate_ips
+
+        t = self.turn
+        self.relay = TurnClient(t["host"], t["port"], t["username"], t["password"], t.get("protocol", "udp"),
+                                bool(t.get("tls", False)), on_data=self._on_relay_data)
+        try:
+            rip, rport = await asyncio.wait_for(self.relay.allocate(), float(t.get("timeout", 5.0)))
+            ips = offer_candidate_ips(self.offer_sdp)
+            if ips:
+                await self.relay.create_permission(ips)
+        except (TurnError, OSError, asyncio.TimeoutError) as e:
+            log.warning("TURN relay unavailable (%s); answering with host candidates only", e)
+            self.relay.close()
+            self.relay = None
+            return []
+        mip, mport = self.relay.mapped or (rip, rport)
+        return [f"a=candidate:9 1 udp 16777215 {rip} {rport} typ relay raddr {mip} rport {mport}"]
 
     # ------------------------------------------------------------------ datagrams
     def datagram_received(self, data: bytes, addr) -> None:
@@ -352,7 +401,17 @@ class WebRtcPeer(asyncio.DatagramProtocol):
 
     def _send_all(self, dgrams, addr) -> None:
         for d in dgrams:
-            self.transport.sendto(d, addr)
+            self._sendto(d, addr)
+
+    def _sendto(self, data: bytes, addr) -> None:
+        if isinstance(addr, RelayAddr):
+            if self.relay is not None:
+                self.relay.send(data, tuple(addr))
+        elif self.transport is not None:
+            self.transport.sendto(data, addr)
+
+    def _on_relay_data(self, payload: bytes, peer) -> None:
+        self.datagram_received(payload, RelayAddr(peer))
 
     def _on_stun(self, data: bytes, addr) -> None:
         m = S.StunMessage.decode(data)
@@ -361,13 +420,16 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         user = (m.get(S.A_USERNAME) or b"").decode(errors="replace")
         if not user.startswith(self.ufrag + ":") or not m.check_integrity(self.pwd.encode()):
             err = S.StunMessage(S.BINDING_ERROR, m.tid, [(S.A_ERROR_CODE, struct.pack("!HBB", 0, 4, 1) + b"Unauthorized")])
-            self.transport.sendto(err.encode(), addr)
+            self._sendto(err.encode(), addr)
             return
         self.stats["stun"] += 1
         self.last_consent = time.monotonic()
         resp = S.StunMessage(S.BINDING_SUCCESS, m.tid, [(S.A_XOR_MAPPED_ADDRESS, S.xor_address(addr[0], addr[1], m.tid))])
-        self.transport.sendto(resp.encode(self.pwd.encode()), addr)
+        self._sendto(resp.encode(self.pwd.encode()), addr)
         if self.remote is None or m.get(S.A_USE_CANDIDATE) is not None:
+            if isinstance(addr, RelayAddr) and addr != self.remote and self.relay is not None:
+                # nominated through our relay: bind a channel (4-byte framing per packet)
+                self.tasks.append(asyncio.ensure_future(self._bind_channel(tuple(addr))))
             self.remote = addr
 
     def _on_dtls_done(self) -> None:
@@ -390,6 +452,26 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             self.srtp_tx_audio = N.net.SrtpSession(sk, ss)
             self.asub = self.audio.subscribe(asyncio.get_running_loop())
             self.tasks.append(asyncio.create_task(self._audio_loop()))
+
+    async def _bind_channel(self, peer) -> None:
+        from .turn_client import TurnError
+
+        try:
+            await self.relay.channel_bind(peer)
+        except (TurnError, OSError) as e:
+            log.warning("TURN ChannelBind failed (Send indications stay in use): %s", e)
+
+    async def add_remote_candidates(self, sdp_fragment: str) -> int:
+        """Trickled browser candidates (WHEP PATCH): TURN permissions for their addresses."""
+        from .turn_client import TurnError, offer_candidate_ips
+
+        ips = offer_candidate_ips(sdp_fragment)
+        if ips and self.relay is not None:
+            try:
+                await self.relay.create_permission(ips)
+            except (TurnError, OSError) as e:
+                log.warning("TURN CreatePermission failed: %s", e)
+        return len(ips)
 
     # ------------------------------------------------------------------ data channels
     def _sctp_out(self, packets, addr=None) -> None:
@@ -464,7 +546,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                 for seq in p.get("nack", []):
                     raw = self.history.get(seq)
                     if raw is not None and self.remote is not None:
-                        self.transport.sendto(self.srtp_tx.protect_rtp(raw), self.remote)
+                        self._sendto(self.srtp_tx.protect_rtp(raw), self.remote)
                         self.stats["rtx"] += 1
 
     # ------------------------------------------------------------------ media
@@ -482,7 +564,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                     self.history[seq] = raw
                     if len(self.history) > self.HISTORY:
                         self.history.popitem(last=False)
-                    self.transport.sendto(self.srtp_tx.protect_rtp(raw), self.remote)
+                    self._sendto(self.srtp_tx.protect_rtp(raw), self.remote)
                     self.stats["rtp_out"] += 1
             self.last_ts = ts
 
@@ -504,7 +586,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                 frame, pending = pending[:160], pending[160:]
                 hdr = struct.pack("!BBHII", 0x80, (0x80 if first else 0) | self.answer.audio_pt, seq, ts,
                                   self.audio_ssrc)
-                self.transport.sendto(self.srtp_tx_audio.protect_rtp(hdr + A.encode_ulaw(frame)), self.remote)
+                self._sendto(self.srtp_tx_audio.protect_rtp(hdr + A.encode_ulaw(frame)), self.remote)
                 first = False
                 seq = (seq + 1) & 0xFFFF
                 ts = (ts + 160) & 0xFFFFFFFF
@@ -527,10 +609,10 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                     self._last_dc_stats = now
             if self.srtp_tx is not None and self.remote is not None and now - last_sr > 1.0:
                 sr = R.build_sr(self.ssrc, getattr(self, "last_ts", 0), self.pkt.packets, self.pkt.octets)
-                self.transport.sendto(self.srtp_tx.protect_rtcp(sr), self.remote)
+                self._sendto(self.srtp_tx.protect_rtcp(sr), self.remote)
                 if self.srtp_tx_audio is not None and getattr(self, "audio_packets", 0):
                     asr = R.build_sr(self.audio_ssrc, self.audio_ts, self.audio_packets, self.audio_octets)
-                    self.transport.sendto(self.srtp_tx_audio.protect_rtcp(asr), self.remote)
+                    self._sendto(self.srtp_tx_audio.protect_rtcp(asr), self.remote)
                 last_sr = now
             if now - self.last_consent > 30.0:  # consent freshness (RFC 7675)
                 log.info("WebRTC peer %s: consent expired", self.id)
@@ -548,15 +630,21 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             t.cancel()
         if self.transport is not None:
             self.transport.close()
+        if self.relay is not None:
+            try:
+                asyncio.get_running_loop().create_task(self.relay.aclose())
+            except RuntimeError:
+                self.relay.close()
 
 
 class WhepEndpoint:
     """``POST /whep`` (application/sdp offer) -> 201 answer; ``DELETE /whep/{id}``."""
 
     def __init__(self, pipeline, host: str | None = None, udp_port: int = 0, level_idc: int = 0x2A, audio=None,
-                 congestion_control: bool = False, on_input=None):
+                 congestion_control: bool = False, on_input=None, turn: dict | None = None):
         self.pipeline = pipeline
         self.on_input = on_input
+        self.turn = turn
         self.audio = audio
         self.congestion_control = congestion_control
         self.host = host
@@ -568,13 +656,14 @@ class WhepEndpoint:
     def routes(self, app) -> None:
         app.router.add_post("/whep", self.post)
         app.router.add_delete("/whep/{pid}", self.delete)
+        app.router.add_patch("/whep/{pid}", self.patch)
 
     async def post(self, request):
         from aiohttp import web
 
         offer = await request.text()
         peer = WebRtcPeer(self.pipeline, offer, self.host, self.udp_port, self.level_idc, audio=self.audio,
-                          congestion_control=self.congestion_control, on_input=self.on_input)
+                          congestion_control=self.congestion_control, on_input=self.on_input, turn=self.turn)
         try:
             answer = await peer.start()
         except ValueError as e:
@@ -584,6 +673,17 @@ class WhepEndpoint:
         self.last_peer = peer
         return web.Response(status=201, text=answer, content_type="application/sdp",
                             headers={"Location": f"/whep/{peer.id}"})
+
+    async def patch(self, request):
+        """Trickle ICE (RFC 9725 §4.3): ``application/trickle-ice-sdpfrag`` with the browser's
+        late candidates; they become TURN permissions on our relay."""
+        from aiohttp import web
+
+        peer = self.peers.get(request.match_info["pid"])
+        if peer is None:
+            raise web.HTTPNotFound()
+        await peer.add_remote_candidates(await request.text())
+        return web.Response(status=204)
 
     async def delete(self, request):
         from aiohttp import web

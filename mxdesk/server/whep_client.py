@@ -23,7 +23,7 @@ def _native():
 
 
 def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_audio: bool = True,
-               h265_pt: int = 104, with_datachannel: bool = False) -> str:
+               h265_pt: int = 104, with_datachannel: bool = False, candidate_ip: str | None = None) -> str:
     mids = "0 1" + (" 2" if with_datachannel else "")
     lines = ["v=0", "o=- 4611731400430051336 2 IN IP4 127.0.0.1", "s=-", "t=0 0", f"a=group:BUNDLE {mids}",
              "a=msid-semantic: WMS"]
@@ -36,7 +36,9 @@ def make_offer(ufrag: str, pwd: str, fingerprint: str, h264_pt: int = 102, with_
         media += ["m=audio 9 UDP/TLS/RTP/SAVPF 111 0", "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
                   f"a=ice-pwd:{pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:1", "a=recvonly",
                   "a=rtcp-mux", "a=rtpmap:111 opus/48000/2", "a=rtpmap:0 PCMU/8000"]
-    media = ["m=video 9 UDP/TLS/RTP/SAVPF 96 %d 108 %d" % (h264_pt, h265_pt), "c=IN IP4 0.0.0.0", f"a=ice-ufrag:{ufrag}",
+    cand = [f"a=candidate:1 1 udp 2122260223 {candidate_ip} 9 typ host"] if candidate_ip else []
+    media = ["m=video 9 UDP/TLS/RTP/SAVPF 96 %d 108 %d" % (h264_pt, h265_pt), "c=IN IP4 0.0.0.0", *cand,
+             f"a=ice-ufrag:{ufrag}",
              f"a=ice-pwd:{pwd}", "a=ice-options:trickle", f"a=fingerprint:{fingerprint}", "a=setup:actpass", "a=mid:0",
              "a=recvonly", "a=rtcp-mux", "a=rtcp-rsize", "a=rtpmap:96 VP8/90000",
              f"a=rtpmap:{h264_pt} H264/90000", f"a=rtcp-fb:{h264_pt} nack", f"a=rtcp-fb:{h264_pt} nack pli",
@@ -78,7 +80,7 @@ class _Client(asyncio.DatagramProtocol):
 
 async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
                     timeout: float = 30.0, dc_messages: list[str] | None = None,
-                    dc_wait_stats: bool = False) -> WhepResult:
+                    dc_wait_stats: bool = False, via_relay: bool = False) -> WhepResult:
     """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
 
     ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
@@ -86,13 +88,16 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     ``dc_messages``: offer a data channel, open ``input`` on it (SCTP client side, even
     stream id) and send these text messages; the call returns once all are acknowledged
     (and, with ``dc_wait_stats``, a server stats message has arrived).
+    ``via_relay``: connect to the server's TURN relay candidate instead of its host candidate
+    (the offer then carries a host candidate so the server can create the TURN permission).
     """
     import aiohttp
 
     N = _native()
     dtls = N.net.DtlsEndpoint(False)
     ufrag, pwd = secrets.token_hex(4), secrets.token_hex(12)
-    offer = make_offer(ufrag, pwd, dtls.fingerprint, with_datachannel=dc_messages is not None)
+    offer = make_offer(ufrag, pwd, dtls.fingerprint, with_datachannel=dc_messages is not None,
+                       candidate_ip="127.0.0.1" if via_relay else None)
     res = WhepResult()
     t0 = time.monotonic()
     async with aiohttp.ClientSession(auth=auth) as s:
@@ -103,7 +108,11 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
             location = r.headers["Location"]
     ans = parse_sdp(res.answer)
     vid = next(m for m in ans.media if m.kind == "video" and m.port)
-    cand = vid.attr("candidate").split()
+    cands = [c.split() for c in vid.attrs_named("candidate")]
+    want = "relay" if via_relay else "host"
+    cand = next((c for c in cands if c[7] == want), None)
+    if cand is None:
+        raise RuntimeError(f"answer has no {want} candidate")
     host, port = cand[4], int(cand[5])
     r_ufrag, r_pwd = vid.attr("ice-ufrag"), vid.attr("ice-pwd")
     r_fp = vid.attr("fingerprint")

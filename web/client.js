@@ -194,9 +194,26 @@ const mxdesk = (() => {
       if (pc.connectionState === "failed") { pc.close(); setTimeout(() => whep(video), 1000); }
     };
     await pc.setLocalDescription(await pc.createOffer());
+    // non-trickle WHEP: wait (<= 2 s) for candidates so the offer carries them -- the server
+    // turns them into TURN permissions on its relay; late candidates go out as PATCHes
+    await new Promise((resolve) => {
+      if (pc.iceGatheringState === "complete") return resolve();
+      const t = setTimeout(resolve, 2000);
+      pc.addEventListener("icegatheringstatechange", () => {
+        if (pc.iceGatheringState === "complete") { clearTimeout(t); resolve(); }
+      });
+    });
+    let whepLocation = null;
+    pc.onicecandidate = (ev) => {
+      if (ev.candidate && ev.candidate.candidate && whepLocation) {
+        fetch(whepLocation, { method: "PATCH", headers: { "Content-Type": "application/trickle-ice-sdpfrag" },
+                              body: `a=${ev.candidate.candidate}\r\n` }).catch(() => {});
+      }
+    };
     const r = await fetch("whep", { method: "POST", headers: { "Content-Type": "application/sdp" }, body: pc.localDescription.sdp });
     if (r.status !== 201) { msgEl.textContent = "WHEP failed: " + r.status; return; }
     const loc = r.headers.get("Location");
+    whepLocation = loc;
     window.addEventListener("beforeunload", () => { fetch(loc, { method: "DELETE", keepalive: true }); });
     await pc.setRemoteDescription({ type: "answer", sdp: await r.text() });
     setInterval(async () => {
