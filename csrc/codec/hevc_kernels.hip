@@ -25,6 +25,7 @@
 #include "h264_core.h"
 #include "h264_gpu.h"
 #include "h264_mb.h"
+#include "../common/xcd.h"
 #include "hevc_core.h"
 #include "hevc_encoder.h"
 
@@ -315,7 +316,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ncu = g.mb_w * g.mb_h;
-    const int i = blockIdx.x * 4 + wave;
+    const int bid = (g.mb_w % 4) ? (int)blockIdx.x : xcd_interleave(blockIdx.x, gridDim.x, g.mb_w / 4);  // CU rows over XCDs
+    const int i = bid * 4 + wave;
     const bool valid = i < ncu;
     const int x = valid ? i % g.mb_w : 0, y = valid ? i / g.mb_w : 0;
     const int x0 = x * 16, y0 = y * 16;
@@ -398,7 +400,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     __syncthreads();
     if (threadIdx.x < 3) {
         const int c = threadIdx.x;
-        fs->sse_part[c * h264::kSsePartStride + blockIdx.x] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
+        fs->sse_part[c * h264::kSsePartStride + bid] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
     }
 }
 
