@@ -21,7 +21,6 @@
 #include "h264_core.h"
 #include "h264_gpu.h"
 #include "h264_mb.h"
-#include "../common/xcd.h"
 
 namespace mx {
 namespace h264 {
@@ -125,9 +124,7 @@ __global__ __launch_bounds__(256) void k_hpel(Geometry g, const FrameState* __re
     __shared__ uint8_t smp[kHpTH + 5][kHpTW + 8];
     __shared__ int16_t b1[kHpTH + 5][kHpTW];
     const uint8_t* __restrict__ ref = fs->ref_y;  // via the frame state: graph-replay safe
-    // tile rows round-robin over XCDs: horizontal halos of neighbouring tiles share L2 lines
-    const int tile = xcd_interleave(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, gridDim.x);
-    const int px0 = (tile % gridDim.x) * kHpTW, py0 = (tile / gridDim.x) * kHpTH;  // padded-plane coordinates
+    const int px0 = blockIdx.x * kHpTW, py0 = blockIdx.y * kHpTH;  // padded-plane coordinates
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     const int tid = threadIdx.x;
     // samples for rows py0-2 .. py0+kHpTH+2, cols px0-2 .. px0+kHpTW+2 (picture coords = padded - pad)
@@ -195,7 +192,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     __shared__ uint32_t cand_cost[8];
     __shared__ uint32_t s_sad0[4];
 
-    const int mbi = xcd_interleave(blockIdx.x, gridDim.x, g.mb_w);  // MB rows round-robin over XCDs
+    const int mbi = blockIdx.x;  // default dispatch order (XCD mappings measured: profiles/r01_xcd)
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
     const int x0 = mbx * 16, y0 = mby * 16;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -352,7 +349,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nmb = g.mb_w * g.mb_h;
-    const int bid = (g.mb_w % 4) ? (int)blockIdx.x : xcd_interleave(blockIdx.x, gridDim.x, g.mb_w / 4);  // rows over XCDs
+    const int bid = blockIdx.x;
     const int mbi = bid * 4 + wave;
     const bool valid = mbi < nmb;
     const int mbx = valid ? mbi % g.mb_w : 0, mby = valid ? mbi / g.mb_w : 0;

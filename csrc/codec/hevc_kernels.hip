@@ -25,7 +25,6 @@
 #include "h264_core.h"
 #include "h264_gpu.h"
 #include "h264_mb.h"
-#include "../common/xcd.h"
 #include "hevc_core.h"
 #include "hevc_encoder.h"
 
@@ -316,7 +315,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ncu = g.mb_w * g.mb_h;
-    const int bid = (g.mb_w % 4) ? (int)blockIdx.x : xcd_interleave(blockIdx.x, gridDim.x, g.mb_w / 4);  // CU rows over XCDs
+    const int bid = blockIdx.x;
     const int i = bid * 4 + wave;
     const bool valid = i < ncu;
     const int x = valid ? i % g.mb_w : 0, y = valid ? i / g.mb_w : 0;
