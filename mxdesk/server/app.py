@@ -70,7 +70,10 @@ class MediaServer:
 
         x_display = getattr(cfg, "display", None) if pipeline.capture is not None else None
         self.x_display = x_display
-        self.clipboard = ClipboardSync(self.injector, x_display) if bool(getattr(cfg, "enable_clipboard", True)) \
+        from ..utils.config import clipboard_directions
+
+        self.clipboard_in, self.clipboard_out = clipboard_directions(getattr(cfg, "enable_clipboard", "true"))
+        self.clipboard = ClipboardSync(self.injector, x_display) if (self.clipboard_in or self.clipboard_out) \
             else None
         self.cursors = CursorSync(pipeline.capture) if (pipeline.capture is not None and
                                                          bool(getattr(cfg, "enable_cursors", True))) else None
@@ -280,10 +283,13 @@ class MediaServer:
                 self.request_resize(ev.width, ev.height)
             else:
                 log.info("client resize %dx%d ignored (WEBRTC_ENABLE_RESIZE=false)", ev.width, ev.height)
+        elif ev.kind == "clipboard":
+            if self.clipboard_in:
+                self.injector.apply(ev)
+                if self.clipboard is not None:
+                    self.clipboard.write(ev.text)
         else:
             self.injector.apply(ev)
-            if ev.kind == "clipboard" and self.clipboard is not None:
-                self.clipboard.write(ev.text)
 
     # ------------------------------------------------------------------ resize / sync
     def request_resize(self, width: int, height: int) -> None:
@@ -330,7 +336,7 @@ class MediaServer:
                     msg = await loop.run_in_executor(None, self.cursors.poll)
                     if msg:
                         self.broadcast(msg)
-                if self.clipboard is not None and n % clipboard_every == 0:
+                if self.clipboard is not None and self.clipboard_out and n % clipboard_every == 0:
                     text = await loop.run_in_executor(None, self.clipboard.poll)
                     if text is not None:
                         from .desktop_sync import clipboard_message

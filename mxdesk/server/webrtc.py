@@ -16,7 +16,9 @@ of the reference's selkies pipeline, Dockerfile:439-444).
   (``csrc/net/sctp.cpp``) on the same DTLS session; the browser opens the channel (selkies
   names it ``input``) and its text messages go through the same input parser as the
   WebSocket control channel (keyboard / mouse / clipboard / gamepad / bitrate); the server
-  answers with ``{"type": "stats", ...}`` once a second.
+  answers with ``{"type": "stats", ...}`` once a second.  A browser-opened ``audio`` channel
+  (unordered, no retransmissions) receives 48 kHz stereo PCM chunks -- full-band audio
+  without Opus, which the image lacks; PCMU over RTP remains for plain WHEP players.
 """
 from __future__ import annotations
 
@@ -495,6 +497,8 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             if kind == 0:
                 self.dc_channels[cid] = label
                 log.info("WebRTC peer %s: data channel %d '%s' open", self.id, cid, label)
+                if label == "audio" and self.audio is not None:
+                    self.tasks.append(asyncio.ensure_future(self._dc_audio_loop(cid)))
             elif kind == 1:
                 self.stats["dc_in"] += 1
                 if self.on_input is not None and not binary:
@@ -504,6 +508,24 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                         log.exception("data-channel message %r", data[:64])
             elif kind == 2:
                 self.dc_channels.pop(cid, None)
+
+    async def _dc_audio_loop(self, cid: int) -> None:
+        """48 kHz stereo PCM (``MXA1`` chunks, 10 ms) on a browser-opened ``audio`` channel --
+        full-band audio for WebRTC viewers without an Opus encoder; the browser opens it
+        unordered with maxRetransmits 0, so late chunks are dropped, never waited for."""
+        from ..audio.pipeline import audio_message
+
+        sub = self.audio.subscribe(asyncio.get_running_loop())
+        try:
+            while not self.closed.is_set() and cid in self.dc_channels:
+                ch = await sub.queue.get()
+                if self.dc.buffered_amount > 256 * 1024:  # congested: real-time audio is dropped, not queued
+                    self.stats["dc_audio_drop"] = self.stats.get("dc_audio_drop", 0) + 1
+                    continue
+                self._sctp_out(self.dc.send(cid, audio_message(ch), True))
+                self.stats["dc_audio"] = self.stats.get("dc_audio", 0) + 1
+        finally:
+            self.audio.unsubscribe(sub)
 
     def dc_send(self, text: str, label: str | None = None) -> bool:
         """Send one text message on the first open channel (or the one named ``label``)."""

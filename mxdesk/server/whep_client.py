@@ -64,6 +64,7 @@ class WhepResult:
     audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
     audio_seqs: list[int] = field(default_factory=list)
     dc_received: list[str] = field(default_factory=list)  # server -> client data-channel messages
+    dc_audio: list[bytes] = field(default_factory=list)   # MXA1 chunks from the "audio" channel
     dc_sent: int = 0
 
 
@@ -80,7 +81,7 @@ class _Client(asyncio.DatagramProtocol):
 
 async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
                     timeout: float = 30.0, dc_messages: list[str] | None = None,
-                    dc_wait_stats: bool = False, via_relay: bool = False) -> WhepResult:
+                    dc_wait_stats: bool = False, via_relay: bool = False, dc_audio_chunks: int = 0) -> WhepResult:
     """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
 
     ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
@@ -88,6 +89,8 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     ``dc_messages``: offer a data channel, open ``input`` on it (SCTP client side, even
     stream id) and send these text messages; the call returns once all are acknowledged
     (and, with ``dc_wait_stats``, a server stats message has arrived).
+    ``dc_audio_chunks``: also open an unordered, no-retransmit ``audio`` channel and wait for
+    that many PCM chunks on it.
     ``via_relay``: connect to the server's TURN relay candidate instead of its host candidate
     (the offer then carries a host candidate so the server can create the TURN permission).
     """
@@ -175,6 +178,9 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
             dc = N.net.DataChannelEndpoint(False, 5000, int(app.attr("sctp-port") or 5000))
             out = dc.connect()
             dc_id, more = dc.open("input")
+            if dc_audio_chunks:
+                _aid, amore = dc.open("audio", "", False, 0)
+                more += amore
             for msg in dc_messages:
                 more += dc.send(dc_id, msg.encode(), False)
             res.dc_sent = len(dc_messages)
@@ -188,14 +194,16 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                 if dc is not None:
                     sctp_out(dc.feed(p))
             if dc is not None:
-                for kind, _cid, _label, _proto, _binary, data in dc.take_events():
-                    if kind == 1:
+                for kind, _cid, _label, _proto, binary, data in dc.take_events():
+                    if kind == 1 and binary:
+                        res.dc_audio.append(data)
+                    elif kind == 1:
                         res.dc_received.append(data.decode("utf-8", "replace"))
 
         def dc_pending() -> bool:
             if dc is None:
                 return False
-            if dc.buffered_amount or not dc.is_open(dc_id):
+            if dc.buffered_amount or not dc.is_open(dc_id) or len(res.dc_audio) < dc_audio_chunks:
                 return True
             return dc_wait_stats and not any('"stats"' in m for m in res.dc_received)
         last_tick = time.monotonic()

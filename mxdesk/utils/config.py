@@ -126,7 +126,8 @@ SCHEMA: list[Var] = [
     Var("enable_audio", ["SELKIES_ENABLE_AUDIO"], True, bool, "desktop audio (PCM over WebSocket, PCMU over WebRTC)"),
     Var("audio_source", ["MXDESK_AUDIO_SOURCE"], "auto", str, "audio capture: auto | pulse | synthetic | fifo:PATH | none"),
     Var("audio_bitrate", ["SELKIES_AUDIO_BITRATE"], 128000, int, "audio bitrate (bps)"),
-    Var("enable_clipboard", ["SELKIES_ENABLE_CLIPBOARD"], True, bool, "clipboard sync"),
+    Var("enable_clipboard", ["SELKIES_ENABLE_CLIPBOARD"], "true", str,
+        "clipboard sync: true | false | in (browser -> desktop only) | out (desktop -> browser only)"),
     Var("enable_cursors", ["SELKIES_ENABLE_CURSORS"], True, bool, "remote cursor forwarding"),
     Var("enable_metrics_http", ["SELKIES_ENABLE_METRICS_HTTP"], False, bool, "Prometheus /metrics on its own port"),
     Var("metrics_http_port", ["SELKIES_METRICS_HTTP_PORT"], 8000, int, "metrics port"),
@@ -279,3 +280,14 @@ def load(env: Mapping[str, str] | None = None, argv: Sequence[str] | None = None
 
 def schema_table() -> list[dict[str, Any]]:
     return [dataclasses.asdict(v) | {"kind": v.kind.__name__} for v in SCHEMA]
+
+
+def clipboard_directions(value: Any) -> tuple[bool, bool]:
+    """(browser -> desktop, desktop -> browser) for SELKIES_ENABLE_CLIPBOARD's selkies values."""
+    v = str(value if value is not None else "true").strip().lower()
+    if v == "in":
+        return True, False
+    if v == "out":
+        return False, True
+    on = parse_bool(v, True)
+    return on, on

@@ -260,3 +260,30 @@ def test_whep_loopback_input_over_datachannel(native, monkeypatch):
     assert (inj.x, inj.y) == (105, 47) and inj.keys_down == {66} and inj.clipboard == "héllo"
     assert any('"stats"' in m for m in res.dc_received)
     assert list(chans.values()) == ["input"]
+
+
+def test_whep_audio_over_datachannel(native, monkeypatch):
+    """48 kHz stereo PCM chunks on a browser-opened unordered / no-retransmit channel."""
+    from mxdesk.audio.pipeline import CHANNELS, RATE, parse_audio_message
+
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "MXDESK_AUDIO_SOURCE": "synthetic"})
+    from mxdesk.server.app import serve
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            res = await whep_view(f"http://127.0.0.1:{port}/whep", 2, dc_messages=[], dc_audio_chunks=20)
+            return res, dict(srv.whep.last_peer.stats)
+        finally:
+            await runner.cleanup()
+
+    res, stats = asyncio.run(go())
+    msgs = [parse_audio_message(m) for m in res.dc_audio]
+    assert len(msgs) >= 20 and stats["dc_audio"] >= 20
+    assert all(m["rate"] == RATE and m["channels"] == CHANNELS and len(m["pcm"]) == RATE // 100 * CHANNELS
+               for m in msgs)
+    seqs = [m["seq"] for m in msgs]
+    assert len(set(seqs)) == len(seqs)  # unordered channel: no duplicates (no retransmissions)
+    assert max(abs(int(x)) for m in msgs for x in m["pcm"]) > 1000  # the synthetic tone, not silence

@@ -187,3 +187,17 @@ def test_remote_clipboard_pushed_to_websocket_clients():
     # the client's own paste is not echoed back
     srv._on_client_message('{"type": "clipboard", "text": "pasted"}')
     assert srv.clipboard.poll() is None and srv.injector.clipboard == "pasted"
+
+
+def test_clipboard_direction_modes():
+    from mxdesk.utils.config import clipboard_directions
+
+    assert clipboard_directions("true") == (True, True) and clipboard_directions("False") == (False, False)
+    assert clipboard_directions("in") == (True, False) and clipboard_directions("OUT") == (False, True)
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "SELKIES_ENABLE_CLIPBOARD": "out"})
+    srv._on_client_message('{"type": "clipboard", "text": "blocked"}')
+    assert srv.injector.clipboard == "" and srv.clipboard is not None and srv.clipboard_out
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "SELKIES_ENABLE_CLIPBOARD": "false"})
+    assert srv.clipboard is None
+    srv._on_client_message('{"type": "clipboard", "text": "blocked"}')
+    assert srv.injector.clipboard == ""

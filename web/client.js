@@ -165,7 +165,11 @@ const mxdesk = (() => {
     try { iceServers = (await (await fetch("turn")).json()).iceServers || []; } catch (e) { /* no TURN */ }
     const pc = new RTCPeerConnection({ iceServers });
     pc.addTransceiver("video", { direction: "recvonly" });
-    pc.addTransceiver("audio", { direction: "recvonly" });
+    // audio: 48 kHz PCM on an unordered, no-retransmit data channel (played through WebAudio
+    // like the WebSocket transport) instead of the 8 kHz PCMU RTP track
+    const ach = pc.createDataChannel("audio", { ordered: false, maxRetransmits: 0 });
+    ach.binaryType = "arraybuffer";
+    ach.onmessage = (ev) => onAudio(ev.data);
     const ch = pc.createDataChannel("input", { ordered: true });
     ch.onopen = () => { dc = ch; };
     ch.onclose = () => { if (dc === ch) dc = null; };
