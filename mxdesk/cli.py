@@ -23,9 +23,27 @@ import sys
 from .utils import config as C
 
 
+class JsonFormatter(logging.Formatter):
+    """One JSON object per line (``MXDESK_LOG_FORMAT=json``; SURVEY.md §5.5 structured logs)."""
+
+    def format(self, record: logging.LogRecord) -> str:
+        import json
+
+        d = {"ts": round(record.created, 6), "level": record.levelname, "logger": record.name,
+             "msg": record.getMessage(), "pid": record.process}
+        if record.exc_info:
+            d["exc"] = self.formatException(record.exc_info)
+        return json.dumps(d, ensure_ascii=False)
+
+
 def _setup_logging(cfg: C.Config) -> None:
-    logging.basicConfig(level=getattr(logging, cfg.log_level_name, logging.WARNING),
-                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    level = getattr(logging, cfg.log_level_name, logging.WARNING)
+    if str(getattr(cfg, "log_format", "text")).lower() == "json":
+        h = logging.StreamHandler()
+        h.setFormatter(JsonFormatter())
+        logging.basicConfig(level=level, handlers=[h])
+    else:
+        logging.basicConfig(level=level, format="%(asctime)s %(name)s %(levelname)s %(message)s")
 
 
 def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0"):

@@ -186,7 +186,25 @@ class MediaServer:
         return web.json_response(data)
 
     async def metrics(self, request: web.Request) -> web.Response:
+        self._refresh_gpu_telemetry()
         return web.Response(body=self.pipeline.metrics.exposition(), content_type="text/plain")
+
+    def _refresh_gpu_telemetry(self) -> None:
+        """GPU busy %, VRAM, power, temperature of the session's GPU (amdgpu sysfs)."""
+        if getattr(self.pipeline, "backend", "cpu") != "gpu":
+            return
+        try:
+            from ..utils import devices as D
+
+            if not hasattr(self, "_gpu_bdf"):
+                vis = D.visible_gpus(D.enumerate_gpus())
+                dev = int(getattr(self.pipeline, "device", 0))
+                self._gpu_bdf = vis[dev].pci_bdf if dev < len(vis) else None
+            if self._gpu_bdf:
+                self.pipeline.metrics.set_gpu_telemetry(self._gpu_bdf, D.gpu_telemetry(self._gpu_bdf))
+        except (OSError, ValueError, IndexError) as e:
+            log.debug("GPU telemetry unavailable: %s", e)
+            self._gpu_bdf = None
 
     async def status(self, request: web.Request) -> web.Response:
         return web.json_response(self.pipeline.status())

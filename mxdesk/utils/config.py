@@ -150,6 +150,7 @@ SCHEMA: list[Var] = [
     Var("turn_relay", ["MXDESK_TURN_RELAY"], True, bool,
         "allocate a server-side TURN relay candidate when TURN_HOST + credentials are set"),
     Var("log_dir", ["MXDESK_LOG_DIR"], "/tmp", str, "log directory", ref="supervisord.conf:9"),
+    Var("log_format", ["MXDESK_LOG_FORMAT"], "text", str, "log line format: text | json"),
 ]
 _BY_ATTR = {v.attr: v for v in SCHEMA}
 

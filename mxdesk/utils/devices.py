@@ -192,3 +192,37 @@ def hip_device_index(dev: GpuDevice, all_gpus: Sequence[GpuDevice]) -> int:
         if g.pci_bdf == dev.pci_bdf:
             return i
     raise KeyError(dev.pci_bdf)
+
+
+def gpu_telemetry(pci_bdf: str, sysfs_root: str | os.PathLike = "/sys") -> dict[str, float]:
+    """amdgpu sysfs telemetry of one GPU (what ``amd-smi metric`` reports, read without the
+    tool): busy %, VRAM used/total, power (W) and edge/junction temperature (deg C).  Missing
+    files are simply absent from the result (e.g. inside containers without hwmon)."""
+    dev = Path(sysfs_root) / "bus/pci/devices" / pci_bdf
+    out: dict[str, float] = {}
+
+    def num(path: Path) -> float | None:
+        v = _read(path)
+        try:
+            return float(v)
+        except ValueError:
+            return None
+
+    for key, name, scale in (("busy_percent", "gpu_busy_percent", 1.0), ("vram_used_bytes", "mem_info_vram_used", 1.0),
+                             ("vram_total_bytes", "mem_info_vram_total", 1.0)):
+        v = num(dev / name)
+        if v is not None:
+            out[key] = v * scale
+    hw = dev / "hwmon"
+    if hw.is_dir():
+        for h in sorted(hw.iterdir()):
+            for key, names, scale in (("power_watts", ("power1_average", "power1_input"), 1e-6),
+                                      ("temperature_c", ("temp2_input", "temp1_input"), 1e-3)):
+                if key in out:
+                    continue
+                for n in names:  # temp2 is the junction (hotspot) sensor on amdgpu, temp1 the edge
+                    v = num(h / n)
+                    if v is not None:
+                        out[key] = v * scale
+                        break
+    return out

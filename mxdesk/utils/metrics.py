@@ -59,6 +59,9 @@ class SessionMetrics:
                              registry=self.registry)
         self.fps = Gauge("mxdesk_encoded_fps", "Encoded frames per second (1 s window)", lab, registry=self.registry)
         self.clients = Gauge("mxdesk_clients", "Connected viewers", lab, registry=self.registry)
+        self.gpu = Gauge("mxdesk_gpu", "GPU telemetry from amdgpu sysfs (busy_percent, vram_used_bytes, "
+                         "vram_total_bytes, power_watts, temperature_c)", ["session", "gpu", "metric"],
+                         registry=self.registry)
         self.roll_encode = Rolling()
         self.roll_e2e = Rolling()
         self._win = collections.deque()
@@ -104,6 +107,10 @@ class SessionMetrics:
             "e2e_ms_p50": self.roll_e2e.quantile(0.5),
             "e2e_ms_p95": self.roll_e2e.quantile(0.95),
         }
+
+    def set_gpu_telemetry(self, gpu: str, values: dict) -> None:
+        for k, v in values.items():
+            self.gpu.labels(self.session, gpu, k).set(float(v))
 
     def exposition(self) -> bytes:
         return generate_latest(self.registry)

@@ -216,3 +216,37 @@ def test_load_reference_supervisord_conf(tmp_path):
         assert all(x.autorestart == "true" for x in progs) and progs[0].stopsignal == signal.SIGINT
         assert "false" in " ".join(progs[2].command)
         assert sup["logfile"] == "/tmp/supervisord.log"
+
+
+def test_gpu_telemetry_from_fake_sysfs(tmp_path):
+    from mxdesk.utils.devices import gpu_telemetry
+    from mxdesk.utils.metrics import SessionMetrics
+
+    dev = tmp_path / "bus/pci/devices/0000:05:00.0"
+    (dev / "hwmon/hwmon3").mkdir(parents=True)
+    (dev / "gpu_busy_percent").write_text("37\n")
+    (dev / "mem_info_vram_used").write_text("1073741824\n")
+    (dev / "mem_info_vram_total").write_text("309237645312\n")
+    (dev / "hwmon/hwmon3/power1_average").write_text("512000000\n")
+    (dev / "hwmon/hwmon3/temp1_input").write_text("45000\n")
+    (dev / "hwmon/hwmon3/temp2_input").write_text("61000\n")
+    t = gpu_telemetry("0000:05:00.0", tmp_path)
+    assert t == {"busy_percent": 37.0, "vram_used_bytes": 1073741824.0, "vram_total_bytes": 309237645312.0,
+                 "power_watts": 512.0, "temperature_c": 61.0}
+    assert gpu_telemetry("0000:99:00.0", tmp_path) == {}
+    m = SessionMetrics("s0")
+    m.set_gpu_telemetry("0000:05:00.0", t)
+    text = m.exposition().decode()
+    assert 'mxdesk_gpu{gpu="0000:05:00.0",metric="power_watts",session="s0"} 512.0' in text
+
+
+def test_json_log_format():
+    import json
+    import logging
+
+    from mxdesk.cli import JsonFormatter
+
+    rec = logging.LogRecord("mxdesk.test", logging.WARNING, __file__, 1, "hello %s", ("wörld",), None)
+    d = json.loads(JsonFormatter().format(rec))
+    assert d["msg"] == "hello wörld" and d["level"] == "WARNING" and d["logger"] == "mxdesk.test"
+    assert C.load(env={"MXDESK_LOG_FORMAT": "json"}, argv=[]).log_format == "json"

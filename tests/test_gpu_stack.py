@@ -139,3 +139,14 @@ def test_gpu_wall_single_rank_rccl(gpu):
             assert len(frames) == 3 and read_barcode(frames[2][0])[0] == 2
     finally:
         dist.destroy_process_group()
+
+
+def test_gpu_telemetry_sysfs(gpu):
+    """amdgpu sysfs telemetry of the visible GPU feeds the mxdesk_gpu gauges of /metrics."""
+    from mxdesk.utils import devices as D
+
+    vis = D.visible_gpus(D.enumerate_gpus())
+    assert vis, "no AMD render node found in sysfs"
+    t = D.gpu_telemetry(vis[0].pci_bdf)
+    print("telemetry", vis[0].pci_bdf, t)
+    assert "vram_total_bytes" in t or "busy_percent" in t
