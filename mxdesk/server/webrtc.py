@@ -345,6 +345,12 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.transport, _ = await loop.create_datagram_endpoint(lambda: self,
                                                                 local_addr=(self.bind_host, self.bind_port))
         port = self.transport.get_extra_info("sockname")[1]
+        try:  # an IDR is a burst of hundreds of packets: room in the kernel queue instead of drops
+            sock = self.transport.get_extra_info("socket")
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+            sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 20)
+        except OSError:
+            pass
         codec = getattr(self.pipeline, "codec", "h264")
         level = self.level_idc
         if codec == "hevc":

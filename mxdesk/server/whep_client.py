@@ -7,6 +7,7 @@ from __future__ import annotations
 import asyncio
 import os
 import secrets
+import socket
 import struct
 import time
 from dataclasses import dataclass, field
@@ -63,6 +64,10 @@ class WhepResult:
     arrival_us: list[int] = field(default_factory=list)  # CLOCK_MONOTONIC us when each AU completed
     audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
     audio_seqs: list[int] = field(default_factory=list)
+    nacked: int = 0        # RTP packets NACKed after a real (not test-injected) loss
+    recovered: int = 0     # of those, retransmissions that arrived
+    gave_up: int = 0       # holes not repaired in time -> PLI, resync at the next IDR
+    dropped_aus: int = 0   # access units discarded while waiting for that IDR
     dc_received: list[str] = field(default_factory=list)  # server -> client data-channel messages
     dc_audio: list[bytes] = field(default_factory=list)   # MXA1 chunks from the "audio" channel
     dc_sent: int = 0
@@ -81,7 +86,8 @@ class _Client(asyncio.DatagramProtocol):
 
 async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
                     timeout: float = 30.0, dc_messages: list[str] | None = None,
-                    dc_wait_stats: bool = False, via_relay: bool = False, dc_audio_chunks: int = 0) -> WhepResult:
+                    dc_wait_stats: bool = False, via_relay: bool = False, dc_audio_chunks: int = 0,
+                    simulate_loss: float = 0.0) -> WhepResult:
     """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
 
     ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
@@ -91,6 +97,8 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     (and, with ``dc_wait_stats``, a server stats message has arrived).
     ``dc_audio_chunks``: also open an unordered, no-retransmit ``audio`` channel and wait for
     that many PCM chunks on it.
+    ``simulate_loss``: silently drop that fraction of received video packets (seeded), so only
+    the client's automatic NACK / PLI repair brings them back.
     ``via_relay``: connect to the server's TURN relay candidate instead of its host candidate
     (the offer then carries a host candidate so the server can create the TURN permission).
     """
@@ -121,6 +129,10 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     r_fp = vid.attr("fingerprint")
     loop = asyncio.get_running_loop()
     tr, cl = await loop.create_datagram_endpoint(_Client, remote_addr=(host, port))
+    try:  # a 1080p IDR is hundreds of packets in one burst; the default buffer can overflow
+        tr.get_extra_info("socket").setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    except OSError:
+        pass
     deadline = time.monotonic() + timeout
     try:
         # ICE connectivity check (controlling, nominating)
@@ -215,17 +227,81 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
         n_pkts = 0
         sent_pli = False
         nacked: set[int] = set()
+        auto_nacked: set[int] = set()
+        import random
+
+        loss_rng = random.Random(1234)
         media_ssrc = 0
+        gap_since = None       # when the oldest hole in `pending` appeared
+        await_idr = False      # after giving up on a hole: drop AUs until the next IDR
+
+        def dist(a: int, b: int) -> int:
+            return (a - b) & 0xFFFF
+
+        def is_idr(au: bytes) -> bool:
+            for n in N.net.split_annexb(au):
+                t = (n[0] >> 1) & 0x3F if hevc else n[0] & 0x1F
+                if (16 <= t <= 21) if hevc else t == 5:
+                    return True
+            return False
+
+        def deliver() -> None:
+            nonlocal next_seq, await_idr, sent_pli
+            while next_seq in pending:  # in-order delivery to the depacketizer
+                pk = pending.pop(next_seq)
+                au = depk.push(pk)
+                next_seq = (next_seq + 1) & 0xFFFF
+                if au is None:
+                    continue
+                if await_idr and not is_idr(au):
+                    res.dropped_aus += 1
+                    continue
+                await_idr = False
+                res.aus.append(au)
+                res.rtp_ts.append(R.rtp_header(pk)["ts"])
+                res.arrival_us.append(time.monotonic_ns() // 1000)
+                if pli_after and len(res.aus) == pli_after and not sent_pli:
+                    tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
+                    sent_pli = True
+
+        def repair() -> None:
+            """Generic NACK for every hole below the newest packet (once), as browsers do; a
+            hole still open after 300 ms is abandoned: PLI, resync at the next IDR."""
+            nonlocal gap_since, next_seq, await_idr, depk
+            if not pending:
+                gap_since = None
+                return
+            now = time.monotonic()
+            if gap_since is None:
+                gap_since = now
+            if now - gap_since > 0.3:
+                res.gave_up += 1
+                tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
+                next_seq = min(pending, key=lambda q: dist(q, next_seq))
+                depk = R.H265Depacketizer() if hevc else R.H264Depacketizer()
+                await_idr = True
+                gap_since = None
+                deliver()
+                return
+            hi = max(pending, key=lambda q: dist(q, next_seq))
+            new = [q for q in ((next_seq + k) & 0xFFFF for k in range(dist(hi, next_seq)))
+                   if q not in pending and q not in nacked and q not in auto_nacked]
+            for i in range(0, len(new), 64):
+                tr.sendto(tx.protect_rtcp(R.build_nack(my_ssrc, media_ssrc, new[i:i + 64])))
+            auto_nacked.update(new)
+            res.nacked += len(new)
+
         while len(res.aus) < n_frames or dc_pending():
             if dc is not None and time.monotonic() - last_tick > 0.05:
                 sctp_out(dc.tick())
                 last_tick = time.monotonic()
             try:
-                d = await asyncio.wait_for(cl.q.get(), 0.05 if dc is not None else
-                                           max(0.1, deadline - time.monotonic()))
+                d = await asyncio.wait_for(cl.q.get(), 0.05)
             except asyncio.TimeoutError:
                 if time.monotonic() > deadline:
                     raise
+                if next_seq is not None:
+                    repair()
                 continue
             if time.monotonic() > deadline:
                 raise asyncio.TimeoutError()
@@ -255,6 +331,8 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
             if seq in pending or ((seq - next_seq) & 0xFFFF) > 0x8000:
                 continue  # duplicate / already delivered
             n_pkts += 1
+            if simulate_loss and loss_rng.random() < simulate_loss and seq not in auto_nacked:
+                continue  # lost on the "network": no test-mode NACK, the repair logic must notice
             if drop_seq_every and n_pkts % drop_seq_every == 0 and seq not in nacked:
                 res.lost += 1
                 nacked.add(seq)
@@ -262,18 +340,11 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                 continue
             if seq in nacked:
                 res.rtx += 1
+            if seq in auto_nacked:
+                res.recovered += 1
             pending[seq] = p
-            while next_seq in pending:  # in-order delivery to the depacketizer
-                pk = pending.pop(next_seq)
-                au = depk.push(pk)
-                if au is not None:
-                    res.aus.append(au)
-                    res.rtp_ts.append(R.rtp_header(pk)["ts"])
-                    res.arrival_us.append(time.monotonic_ns() // 1000)
-                    if pli_after and len(res.aus) == pli_after and not sent_pli:
-                        tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
-                        sent_pli = True
-                next_seq = (next_seq + 1) & 0xFFFF
+            deliver()
+            repair()
         res.stream = b"".join(res.aus)
     finally:
         tr.close()

@@ -281,3 +281,25 @@ def test_whep_loopback_hevc(native, monkeypatch):
     assert len(frames) == 6
     ids = [read_barcode(y)[0] for y, _, _ in frames]
     assert all(b == a + 1 for a, b in zip(ids, ids[1:]))
+
+
+def test_whep_client_repairs_real_loss_with_nack(native, monkeypatch):
+    """10 % of video packets silently lost: the viewer NACKs every hole (as browsers do) and
+    the server retransmits from its history; the decoded sequence stays contiguous."""
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+    from mxdesk.server.app import serve
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await whep_view(f"http://127.0.0.1:{port}/whep", 15, simulate_loss=0.1)
+        finally:
+            await runner.cleanup()
+
+    res = asyncio.run(go())
+    assert res.nacked > 0 and res.recovered == res.nacked and res.gave_up == 0
+    frames = Decoder().decode(res.stream)
+    ids = [read_barcode(y)[0] for y, _, _ in frames]
+    assert len(ids) == 15 and all(b == a + 1 for a, b in zip(ids, ids[1:]))
