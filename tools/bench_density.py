@@ -51,6 +51,8 @@ def child(a) -> None:
                           session_name=str(a.index))
     srv = MediaServer(pipe, cfg)
 
+    loss: dict = {}
+
     async def go():
         port = free_port()
         runner = await serve(srv, "127.0.0.1", port)
@@ -61,6 +63,7 @@ def child(a) -> None:
                 r = await whep_view(f"http://127.0.0.1:{port}/whep", a.frames, timeout=a.frames / a.fps + 60)
                 lat = [(t - tc) / 1000.0 for t, tc in zip(r.arrival_us, _capture_times(r))]
                 n = len(r.aus)
+                loss.update(nacked=r.nacked, recovered=r.recovered, gave_up=r.gave_up)
                 if n > 1:  # frame rate over the received stream (excludes ICE/DTLS setup)
                     return n, (r.arrival_us[-1] - r.arrival_us[0]) / 1e6 * n / (n - 1), lat
             else:
@@ -82,7 +85,7 @@ def child(a) -> None:
     steady = lat[a.fps:] if len(lat) > 2 * a.fps else lat
     print(json.dumps({"index": a.index, "frames": n, "fps": n / elapsed,
                       "p50_ms": statistics.median(steady), "p95_ms": sorted(steady)[int(0.95 * (len(steady) - 1))],
-                      "gpu_ms_p50": pipe.metrics.summary().get("encode_ms_p50")}), flush=True)
+                      "gpu_ms_p50": pipe.metrics.summary().get("encode_ms_p50"), **loss}), flush=True)
 
 
 def parent(a) -> None:
