@@ -121,6 +121,8 @@ def main(argv: list[str] | None = None) -> None:
     args, _ = ap.parse_known_args(rest)
     cfg = C.load(cli=args)
     _setup_logging(cfg)
+    if cfg.encoder_fallback:
+        logging.getLogger("mxdesk").warning(cfg.encoder_fallback)
     if cmd == "config":
         print(cfg.dump())
     elif cmd == "devices":

@@ -207,7 +207,11 @@ class MediaServer:
             self._gpu_bdf = None
 
     async def status(self, request: web.Request) -> web.Response:
-        return web.json_response(self.pipeline.status())
+        st = self.pipeline.status()
+        fb = getattr(self.cfg, "encoder_fallback", None) if self.cfg is not None else None
+        if fb:
+            st["encoder_fallback"] = fb
+        return web.json_response(st)
 
     # ------------------------------------------------------------------ media websocket
     async def media_ws(self, request: web.Request) -> web.WebSocketResponse:

@@ -52,7 +52,10 @@ ENCODER_ALIASES = {
     "cpuh265enc": "cpuh265enc",
 }
 GPU_ENCODERS = {"mxh264enc", "mxh265enc"}
-UNSUPPORTED_ENCODERS = {"vp8enc", "vp9enc", "av1enc"}
+# selkies encoders without an mxdesk implementation: the session falls back to the GPU H.264
+# encoder (every WebRTC browser decodes H.264) with a startup warning instead of failing
+FALLBACK_ENCODERS = {"vp8enc": "mxh264enc", "vp9enc": "mxh264enc", "av1enc": "mxh264enc",
+                     "vaapivp8enc": "mxh264enc", "vaapivp9enc": "mxh264enc", "vaapiav1enc": "mxh264enc"}
 
 
 @dataclass
@@ -187,12 +190,20 @@ class Config:
     @property
     def encoder_backend(self) -> str:
         name = str(self.values["encoder"]).strip().lower()
-        if name in UNSUPPORTED_ENCODERS:
-            raise ValueError(f"WEBRTC_ENCODER={name} is not implemented yet (H.264 / HEVC: mxh264enc, "
-                             "mxh265enc, x264enc, x265enc)")
+        if name in FALLBACK_ENCODERS:
+            return FALLBACK_ENCODERS[name]
         if name not in ENCODER_ALIASES:
             raise ValueError(f"unknown WEBRTC_ENCODER={name}")
         return ENCODER_ALIASES[name]
+
+    @property
+    def encoder_fallback(self) -> str | None:
+        """Why the requested WEBRTC_ENCODER is not the one running, or None."""
+        name = str(self.values["encoder"]).strip().lower()
+        if name in FALLBACK_ENCODERS:
+            return (f"WEBRTC_ENCODER={name} is not implemented; streaming H.264 with "
+                    f"{FALLBACK_ENCODERS[name]} instead (all WebRTC browsers decode it)")
+        return None
 
     @property
     def codec(self) -> str:

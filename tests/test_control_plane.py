@@ -42,7 +42,7 @@ def test_env_and_cli_override_and_bool_case():
     assert red["BASIC_AUTH_PASSWORD"] == "******" and red["PASSWD"] == "******"
 
 
-@pytest.mark.parametrize("env", [{"SIZEW": "1281"}, {"CDEPTH": "17"}, {"WEBRTC_ENCODER": "vp9enc"},
+@pytest.mark.parametrize("env", [{"SIZEW": "1281"}, {"CDEPTH": "17"}, {"WEBRTC_ENCODER": "bogusenc"},
                                  {"TURN_PROTOCOL": "sctp"}, {"NOVNC_ENABLE": "maybe"}])
 def test_invalid_config_rejected(env):
     with pytest.raises(ValueError):
@@ -250,3 +250,12 @@ def test_json_log_format():
     d = json.loads(JsonFormatter().format(rec))
     assert d["msg"] == "hello wörld" and d["level"] == "WARNING" and d["logger"] == "mxdesk.test"
     assert C.load(env={"MXDESK_LOG_FORMAT": "json"}, argv=[]).log_format == "json"
+
+
+def test_unimplemented_selkies_encoders_fall_back_to_h264():
+    cfg = C.load(env={"WEBRTC_ENCODER": "vp8enc"}, argv=[])
+    assert cfg.encoder_backend == "mxh264enc" and cfg.codec == "h264" and cfg.gpu_encoder
+    assert "vp8enc" in cfg.encoder_fallback
+    assert C.load(env={"WEBRTC_ENCODER": "nvh264enc"}, argv=[]).encoder_fallback is None
+    with pytest.raises(ValueError):
+        C.load(env={"WEBRTC_ENCODER": "bogusenc"}, argv=[]).encoder_backend
