@@ -78,6 +78,11 @@ class MediaServer:
         self.cursors = CursorSync(pipeline.capture) if (pipeline.capture is not None and
                                                          bool(getattr(cfg, "enable_cursors", True))) else None
         self._sync_task: asyncio.Task | None = None
+        self.stats_log = None
+        if bool(getattr(cfg, "enable_webrtc_statistics", False)):
+            from ..utils.metrics import ClientStatsLog
+
+            self.stats_log = ClientStatsLog(getattr(cfg, "webrtc_statistics_dir", "/tmp") or "/tmp")
         from .gamepad import GamepadServer
         from .webrtc import WhepEndpoint, turn_relay_settings
 
@@ -297,6 +302,9 @@ class MediaServer:
                 p.metrics.on_client_latency(float(lat))
         elif ev.kind == "fps":
             p.set_fps(ev.value)
+        elif ev.kind == "stats":
+            if self.stats_log is not None:
+                self.stats_log.write(ev.extra)
         elif ev.kind == "gamepad":
             if self.gamepad is not None:
                 self.gamepad.apply(ev)

@@ -40,7 +40,7 @@ async def view(url: str, nframes: int, user: str | None = None, password: str | 
         headers["Authorization"] = "Basic " + base64.b64encode(f"{user}:{password}".encode()).decode()
     res = ViewerResult()
     async with aiohttp.ClientSession(headers=headers) as s:
-        async with s.ws_connect(url, max_msg_size=64 * 1024 * 1024, timeout=timeout) as ws:
+        async with s.ws_connect(url, max_msg_size=64 * 1024 * 1024, timeout=aiohttp.ClientWSTimeout(ws_close=timeout)) as ws:
             deadline = time.monotonic() + timeout
             for m in send or []:
                 await ws.send_str(m)

@@ -111,7 +111,7 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                        candidate_ip="127.0.0.1" if via_relay else None)
     res = WhepResult()
     t0 = time.monotonic()
-    async with aiohttp.ClientSession(auth=auth) as s:
+    async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
         async with s.post(url, data=offer, headers={"Content-Type": "application/sdp"}) as r:
             if r.status != 201:
                 raise RuntimeError(f"WHEP POST failed: {r.status} {await r.text()}")
@@ -349,7 +349,7 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     finally:
         tr.close()
         try:
-            async with aiohttp.ClientSession(auth=auth) as s:
+            async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
                 base = url.rsplit("/whep", 1)[0]
                 async with s.delete(base + location):
                     pass

@@ -133,6 +133,9 @@ SCHEMA: list[Var] = [
         "clipboard sync: true | false | in (browser -> desktop only) | out (desktop -> browser only)"),
     Var("enable_cursors", ["SELKIES_ENABLE_CURSORS"], True, bool, "remote cursor forwarding"),
     Var("enable_metrics_http", ["SELKIES_ENABLE_METRICS_HTTP"], False, bool, "Prometheus /metrics on its own port"),
+    Var("enable_webrtc_statistics", ["SELKIES_ENABLE_WEBRTC_STATISTICS"], False, bool,
+        "append client-reported WebRTC statistics to CSV files"),
+    Var("webrtc_statistics_dir", ["SELKIES_WEBRTC_STATISTICS_DIR"], "/tmp", str, "directory of those CSV files"),
     Var("metrics_http_port", ["SELKIES_METRICS_HTTP_PORT"], 8000, int, "metrics port"),
     Var("web_root", ["SELKIES_WEB_ROOT"], "", str, "static web client directory ('' = bundled)"),
     # ---- mxdesk options

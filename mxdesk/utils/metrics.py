@@ -114,3 +114,31 @@ class SessionMetrics:
 
     def exposition(self) -> bytes:
         return generate_latest(self.registry)
+
+
+class ClientStatsLog:
+    """``SELKIES_ENABLE_WEBRTC_STATISTICS``: client-reported statistics (``{"type": "stats",
+    ...}`` on the data channel or the control WebSocket) appended to
+    ``<dir>/mxdesk-webrtc-stats-<pid>.csv``; the header row is the first report's keys,
+    later reports are written in that column order (missing values left empty)."""
+
+    FIELDS_MAX = 64
+
+    def __init__(self, directory: str):
+        import os
+
+        os.makedirs(directory, exist_ok=True)
+        self.path = os.path.join(directory, f"mxdesk-webrtc-stats-{os.getpid()}.csv")
+        self.cols: list[str] | None = None
+        self._lock = threading.Lock()
+
+    def write(self, report: dict) -> None:
+        import csv
+
+        row = {k: v for k, v in report.items() if k != "type" and isinstance(v, (int, float, str, bool))}
+        with self._lock, open(self.path, "a", newline="") as f:
+            w = csv.writer(f)
+            if self.cols is None:
+                self.cols = ["server_time"] + sorted(row)[: self.FIELDS_MAX]
+                w.writerow(self.cols)
+            w.writerow([round(time.time(), 3)] + [row.get(c, "") for c in self.cols[1:]])

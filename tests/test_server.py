@@ -76,7 +76,7 @@ def test_basic_auth_and_endpoints():
                 async with s.get(base + "/health") as r:
                     assert r.status == 200
             auth = aiohttp.BasicAuth("user", "pw1")
-            async with aiohttp.ClientSession(auth=auth) as s:
+            async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
                 async with s.get(base + "/") as r:
                     assert r.status == 200 and "client.js" in await r.text()
                 async with s.get(base + "/client.js") as r:
@@ -89,7 +89,7 @@ def test_basic_auth_and_endpoints():
                 async with s.get(base + "/manifest.json") as r:
                     assert json.loads(await r.text())["short_name"] == "mxdesk"
             res = await view(base.replace("http", "http") + "/mxws", 3, user="user", password="pw1")
-            async with aiohttp.ClientSession(auth=auth) as s:
+            async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
                 async with s.get(base + "/metrics") as r:
                     assert "mxdesk_encoded_frames_total" in await r.text()
                 async with s.get(base + "/status") as r:
@@ -211,3 +211,17 @@ def test_hevc_stream_over_websocket():
     assert len(frames) == 4
     for (y, _, _), meta in zip(frames, res.frames):
         assert read_barcode(y)[0] == meta["frame_id"]
+
+
+def test_webrtc_statistics_csv(tmp_path):
+    import csv
+
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "SELKIES_ENABLE_WEBRTC_STATISTICS": "true",
+                                  "SELKIES_WEBRTC_STATISTICS_DIR": str(tmp_path)})
+    srv._on_client_message('{"type": "stats", "fps": 59.9, "packets_lost": 2, "nested": {"x": 1}}')
+    srv._on_client_message('{"type": "stats", "fps": 60.0, "jitter": 0.001}')
+    rows = list(csv.reader(open(srv.stats_log.path)))
+    assert rows[0] == ["server_time", "fps", "packets_lost"]
+    assert rows[1][1:] == ["59.9", "2"] and rows[2][1:] == ["60.0", ""]
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+    assert srv.stats_log is None

@@ -224,6 +224,10 @@ const mxdesk = (() => {
       const st = await pc.getStats();
       st.forEach((x) => {
         if (x.type === "inbound-rtp" && x.kind === "video") {
+          // client statistics for the server's CSV log (SELKIES_ENABLE_WEBRTC_STATISTICS)
+          sendQ(JSON.stringify({ type: "stats", fps: x.framesPerSecond || 0, frames_decoded: x.framesDecoded,
+            packets_lost: x.packetsLost, jitter: x.jitter, nack: x.nackCount, pli: x.pliCount,
+            bytes: x.bytesReceived, decode_s: x.totalDecodeTime, width: x.frameWidth, height: x.frameHeight }));
           statsEl.textContent = `webrtc ${x.frameWidth}x${x.frameHeight}\n${(x.framesPerSecond || 0).toFixed(1)} fps ` +
             `lost ${x.packetsLost} nack ${x.nackCount} pli ${x.pliCount}` + (dc ? " dc" : "") + serverStats;
         }
