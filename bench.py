@@ -47,6 +47,8 @@ def main() -> None:
     ap.add_argument("--bitrate-kbps", type=int, default=8000)
     ap.add_argument("--codec", default="h264", choices=["h264", "hevc"],
                     help="h264 (headline, mxh264enc) or hevc (mxh265enc, BASELINE config '4K60 HEVC')")
+    ap.add_argument("--tu-split", type=int, default=None,
+                    help="HEVC: let inter CUs split their transform tree into 8x8 / 4x4 TUs (default: encoder default)")
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
@@ -95,6 +97,8 @@ def main() -> None:
     cfg.enc.bitrate_kbps = args.bitrate_kbps
     cfg.enc.search_range = args.search_range
     cfg.enc.subpel = args.subpel
+    if args.tu_split is not None:
+        cfg.enc.tu_split = args.tu_split
     cfg.noise = args.noise
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth

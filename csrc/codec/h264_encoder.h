@@ -34,6 +34,7 @@ struct EncoderConfig {
     int chroma_qp_offset = 0;
     int aq = 1;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta)
     int deblock = 1;          // HEVC in-loop deblocking filter (the H.264 encoder always disables it)
+    int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
     int pipeline_depth = 1;   // GPU frames in flight: 2 overlaps frame n's entropy coding with
                               // frame n+1's analysis on a second HIP stream (rate control lags a frame)
 };

@@ -6,8 +6,10 @@
 // every bit and every sample.
 //
 // Coding subset (fixed by the SPS/PPS that hevc_encoder.cpp writes):
-//   CTB = CU = 16x16 (no split_cu_flag), PU 2Nx2N, TU 16x16 luma / 8x8 chroma
-//   (max_transform_hierarchy_depth 0), I slices of intra CUs, P slices of skip / merge /
+//   CTB = CU = 16x16 (no split_cu_flag), PU 2Nx2N, TU 16x16 luma / 8x8 chroma; with
+//   EncoderConfig.tu_split an inter CU may instead split its transform tree once (four 8x8
+//   luma TUs, eight 4x4 chroma TUs: max_transform_hierarchy_depth_inter 1), chosen per CU by
+//   SSE + lambda * estimated bits, I slices of intra CUs, P slices of skip / merge /
 //   AMVP CUs with one reference picture, MaxNumMergeCand 1, no TMVP, no SAO, no
 //   deblocking, no sign hiding, cu_qp_delta per CU (adaptive quantisation), one slice per
 //   CTU row so every slice is entropy coded by its own GPU wave.
@@ -673,8 +675,15 @@ struct CuInfo {
     uint8_t last[3];     // last significant scan index per TU (Y 0..255, Cb/Cr 0..63)
     uint16_t csbf_y;     // coded sub-block mask (bit = sub-block scan index)
     uint8_t csbf_c[2];
+    // transform tree of inter CUs: 0 = not coded (SPS depth 0), 1 = one 16x16 TU, 2 = split into
+    // four 8x8 luma TUs (sub-blocks 4k..4k+3) and 4x4 chroma TUs (Cb sub-block 16+k, Cr 20+k)
+    uint8_t tu_split;
+    uint8_t cbf_y4;  // split: bit k = luma TU k coded
+    uint8_t cbf_c4;  // split: bit k = Cb TU k, bit 4+k = Cr TU k coded
+    uint8_t pad;
 };
-static_assert(sizeof(CuInfo) == 20, "CuInfo layout");
+static_assert(sizeof(CuInfo) == 24, "CuInfo layout");
+constexpr int kCuWords = (int)(sizeof(CuInfo) / 4);
 
 // Per-TU summary (cbf, last position, coded sub-blocks) of coefficients in scan order.
 MXHD bool tu_summary(const int16_t* c, int n, uint8_t* last, uint32_t* csbf) {
@@ -688,6 +697,50 @@ MXHD bool tu_summary(const int16_t* c, int n, uint8_t* last, uint32_t* csbf) {
     *last = (uint8_t)(l < 0 ? 0 : l);
     *csbf = m;
     return l >= 0;
+}
+
+// CU summary from its levels (cbf bits, per-TU last positions and coded sub-blocks).  For a
+// split transform tree the per-TU cbf go to cbf_y4 / cbf_c4, and last[] / csbf_* hold sums
+// and unions that only feed the entropy-cost estimate (code_cu recomputes per-TU values).
+MXHD void cu_summarise(CuInfo& c, const int16_t* co) {
+    uint32_t m;
+    c.cbf = 0;
+    c.cbf_y4 = c.cbf_c4 = 0;
+    if (c.tu_split != 2) {
+        if (tu_summary(co, 256, &c.last[0], &m)) c.cbf |= 1;
+        c.csbf_y = (uint16_t)m;
+        if (tu_summary(co + 256, 64, &c.last[1], &m)) c.cbf |= 2;
+        c.csbf_c[0] = (uint8_t)m;
+        if (tu_summary(co + 320, 64, &c.last[2], &m)) c.cbf |= 4;
+        c.csbf_c[1] = (uint8_t)m;
+        return;
+    }
+    uint32_t lsum = 0, csy = 0;
+    for (int k = 0; k < 4; ++k) {
+        uint8_t l;
+        if (tu_summary(co + 64 * k, 64, &l, &m)) {
+            c.cbf_y4 |= (uint8_t)(1u << k);
+            lsum += l + 1u;
+            csy |= m << (4 * k);
+        }
+    }
+    c.cbf |= c.cbf_y4 ? 1 : 0;
+    c.last[0] = (uint8_t)(lsum ? (lsum > 256 ? 255 : lsum - 1) : 0);
+    c.csbf_y = (uint16_t)csy;
+    for (int comp = 0; comp < 2; ++comp) {
+        uint32_t csum = 0, cm = 0;
+        for (int k = 0; k < 4; ++k) {
+            uint8_t l;
+            if (tu_summary(co + 256 + 64 * comp + 16 * k, 16, &l, &m)) {
+                c.cbf_c4 |= (uint8_t)(1u << (4 * comp + k));
+                csum += l + 1u;
+                cm |= 1u << k;
+            }
+        }
+        if (cm) c.cbf |= (uint8_t)(2 << comp);
+        c.last[1 + comp] = (uint8_t)(csum ? csum - 1 : 0);
+        c.csbf_c[comp] = (uint8_t)cm;
+    }
 }
 
 // ---------------------------------------------------------------- residual_coding (7.3.8.11)
@@ -744,7 +797,27 @@ struct CoefArray {  // host / generic: the CU's 384 int16 levels
 
 MXHD int msb16(uint32_t m) { return 31 - __builtin_clz(m); }  // m != 0
 
-// One TU of size 2^log2n (8 or 16; scanIdx 0) whose sub-blocks start at CU sub-block sb0.
+// sigCtx of a 4x4 TU position (raster y*4+x), 9.3.4.2.5
+constexpr uint8_t kCtxIdxMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+
+// last significant scan index and coded-sub-block mask of a TU of `nsb` sub-blocks (1 or 4)
+// starting at CU sub-block sb0, from the coefficient accessor's significance masks
+template <class Cf>
+MXHD int tu_last(const Cf& cf, int sb0, int nsb, uint32_t* csbf) {
+    int last = -1;
+    uint32_t m = 0;
+    for (int i = 0; i < nsb; ++i) {
+        const uint32_t sg = cf.sig(sb0 + i);
+        if (sg) {
+            m |= 1u << i;
+            last = i * 16 + msb16(sg);
+        }
+    }
+    *csbf = m;
+    return last;
+}
+
+// One TU of size 2^log2n (4, 8 or 16; scanIdx 0) whose sub-blocks start at CU sub-block sb0.
 template <class Ctx, class Cf>
 MXHD void code_residual(CabacEnc& e, Ctx& ctx, const Cf& cf, int sb0, int log2n, int cidx, int last_idx,
                         uint32_t csbf_mask) {
@@ -783,7 +856,9 @@ MXHD void code_residual(CabacEnc& e, Ctx& ctx, const Cf& cf, int sb0, int log2n,
             const int bit = (sig >> n) & 1;
             const int xp = diag4x(n), yp = diag4y(n);
             int sc;
-            if (i == 0 && n == 0) {
+            if (log2n == 2) {
+                sc = kCtxIdxMap4x4[(yp << 2) + xp];
+            } else if (i == 0 && n == 0) {
                 sc = 0;
             } else {
                 if (prev_csbf == 0)
@@ -878,6 +953,17 @@ MXHD void code_mvd(CabacEnc& e, Ctx& ctx, int dx, int dy) {
 
 MXHD int qp_delta_wrap(int qp, int pred) { return ((qp - pred + 26 + 52) % 52) - 26; }
 
+// cu_qp_delta_abs (TU prefix of 5 context bins + EG0 suffix) and its sign
+template <class Ctx>
+MXHD void code_qp_delta(CabacEnc& e, Ctx& ctx, int d) {
+    const int a = d < 0 ? -d : d;
+    const int pre = a < 5 ? a : 5;
+    for (int k = 0; k < pre; ++k) e.bin(ctx, C_QP_DELTA + (k ? 1 : 0), 1);
+    if (pre < 5) e.bin(ctx, C_QP_DELTA + (pre ? 1 : 0), 0);
+    if (a >= 5) e.egk((uint32_t)(a - 5), 0);
+    if (a) e.bypass(d < 0);
+}
+
 // One CTU (= one CU).  left / above: neighbouring CUs in the same slice or null.
 // qp_prev: QP predictor (QpY of the previous CU in decoding order, slice QP at start).
 // Neighbour facts the CU syntax needs (type -1: not available in the slice).
@@ -928,19 +1014,41 @@ MXHD void code_cu(CabacEnc& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf&
             root = c.cbf != 0;
             e.bin(ctx, C_RQT_ROOT, root);
         }
-        if (root) {
+        if (root && !intra && c.tu_split) e.bin(ctx, C_SPLIT_TRANSFORM + 1, c.tu_split == 2);  // 5 - log2(16)
+        if (root && !intra && c.tu_split == 2) {
+            // transform_tree depth 1: per 8x8 child cbf_cb / cbf_cr (if the parent's is set),
+            // cbf_luma, then its transform_unit; cu_qp_delta with the first coded TU
+            const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1;
+            e.bin(ctx, C_CBF_CHROMA + 0, cb);
+            e.bin(ctx, C_CBF_CHROMA + 0, cr);
+            bool qp_done = false;
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const int yk = (c.cbf_y4 >> k) & 1, cbk = (c.cbf_c4 >> k) & 1, crk = (c.cbf_c4 >> (4 + k)) & 1;
+                if (cb) e.bin(ctx, C_CBF_CHROMA + 1, cbk);
+                if (cr) e.bin(ctx, C_CBF_CHROMA + 1, crk);
+                e.bin(ctx, C_CBF_LUMA + 0, yk);
+                if ((yk | cbk | crk) && !qp_done) {
+                    code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
+                    qp_prev = c.qp;
+                    qp_done = true;
+                }
+#pragma unroll 1
+                for (int t = 0; t < 3; ++t) {
+                    if (!((t == 0 ? yk : (t == 1 ? cbk : crk)))) continue;
+                    const int sb0 = t == 0 ? 4 * k : (t == 1 ? 16 + k : 20 + k);
+                    uint32_t csbf;
+                    const int last = tu_last(cf, sb0, t == 0 ? 4 : 1, &csbf);
+                    code_residual(e, ctx, cf, sb0, t == 0 ? 3 : 2, t, last, csbf);
+                }
+            }
+        } else if (root) {
             const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
             e.bin(ctx, C_CBF_CHROMA + 0, cb);
             e.bin(ctx, C_CBF_CHROMA + 0, cr);
             if (intra || cb || cr) e.bin(ctx, C_CBF_LUMA + 1, cy);
             if (c.cbf) {
-                const int d = qp_delta_wrap(c.qp, qp_prev);
-                const int a = d < 0 ? -d : d;
-                const int pre = a < 5 ? a : 5;
-                for (int k = 0; k < pre; ++k) e.bin(ctx, C_QP_DELTA + (k ? 1 : 0), 1);
-                if (pre < 5) e.bin(ctx, C_QP_DELTA + (pre ? 1 : 0), 0);
-                if (a >= 5) e.egk((uint32_t)(a - 5), 0);
-                if (a) e.bypass(d < 0);
+                code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
                 qp_prev = c.qp;
                 // one call site for the three TUs keeps the (inlined) device code small
 #pragma unroll 1
@@ -1005,10 +1113,49 @@ MXHD bool tu_decimate(int log2n, bool intra, int nz, int max_abs) {
     return !intra && nz > 0 && max_abs == 1 && nz <= (log2n == 4 ? 4 : 2);
 }
 
-MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* levels, int* rres) {
-    const int N = 1 << log2n;
-    int c[256], d[256];
-    fwd_transform(log2n, res, c);
+// Fixed-size forward / inverse transforms (same arithmetic as fwd_transform / inv_transform,
+// arrays sized for the TU so per-lane GPU callers keep them out of scratch).
+template <int L>
+MXHD void fwd_transform_t(const int* res, int* out) {
+    constexpr int N = 1 << L, s1 = L - 1, s2 = L + 6;
+    int tmp[N * N];
+    for (int y = 0; y < N; ++y)
+        for (int k = 0; k < N; ++k) {
+            int s = 0;
+            for (int n = 0; n < N; ++n) s += dct_coef(L, k, n) * res[y * N + n];
+            tmp[y * N + k] = (s + (1 << (s1 - 1))) >> s1;
+        }
+    for (int k2 = 0; k2 < N; ++k2)
+        for (int k = 0; k < N; ++k) {
+            int s = 0;
+            for (int y = 0; y < N; ++y) s += dct_coef(L, k2, y) * tmp[y * N + k];
+            out[k2 * N + k] = (s + (1 << (s2 - 1))) >> s2;
+        }
+}
+template <int L>
+MXHD void inv_transform_t(const int* d, int* r) {
+    constexpr int N = 1 << L;
+    int g[N * N];
+    for (int x = 0; x < N; ++x)
+        for (int y = 0; y < N; ++y) {
+            int s = 0;
+            for (int k = 0; k < N; ++k) s += dct_coef(L, k, y) * d[k * N + x];
+            g[y * N + x] = clip16((s + 64) >> 7);
+        }
+    for (int y = 0; y < N; ++y)
+        for (int x = 0; x < N; ++x) {
+            int s = 0;
+            for (int k = 0; k < N; ++k) s += dct_coef(L, k, x) * g[y * N + k];
+            r[y * N + x] = (s + 2048) >> 12;
+        }
+}
+
+template <int L>
+MXHD int tu_encode_t(const int* res, int qp, bool intra, int16_t* levels, int* rres) {
+    constexpr int N = 1 << L;
+    const int log2n = L;
+    int c[N * N], d[N * N];
+    fwd_transform_t<L>(res, c);
     int nz = 0, mx = 0;
     for (int v = 0; v < N; ++v)
         for (int u = 0; u < N; ++u) {
@@ -1040,10 +1187,75 @@ MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* level
             d[v * N + u] = dequant_coef(l, qp, log2n);
         }
     if (nz)
-        inv_transform(log2n, d, rres);
+        inv_transform_t<L>(d, rres);
     else
         for (int i = 0; i < N * N; ++i) rres[i] = 0;
     return nz;
+}
+
+MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* levels, int* rres) {
+    if (log2n == 2) return tu_encode_t<2>(res, qp, intra, levels, rres);
+    if (log2n == 3) return tu_encode_t<3>(res, qp, intra, levels, rres);
+    return tu_encode_t<4>(res, qp, intra, levels, rres);
+}
+
+// lambda for SSE decisions, HM's 0.57 * 2^((QP-12)/3), in 1/16 units (integer: CPU == GPU)
+constexpr uint32_t kLambdaSse16[52] = {1,    1,    1,    1,    1,    2,     2,     3,     4,     5,     6,
+                                       7,    9,    11,   14,   18,   23,    29,    36,    46,    58,    73,
+                                       92,   116,  146,  184,  232,  292,   368,   463,   584,   735,   927,
+                                       1167, 1471, 1853, 2335, 2942, 3706,  4669,  5883,  7412,  9339,  11766,
+                                       14825, 18678, 23533, 29649, 37356, 47065, 59298, 74711};
+// Rough CABAC bits of one TU's levels: ~3.5 bins per significant level plus the magnitude
+// (Golomb-Rice growth), ~4 bits of last position / cbf overhead per coded TU.
+MXHD uint32_t tu_bits_est(const int16_t* lv, int n) {
+    uint32_t b = 0;
+    bool any = false;
+    for (int k = 0; k < n; ++k) {
+        const int a = lv[k] < 0 ? -lv[k] : lv[k];
+        if (!a) continue;
+        any = true;
+        b += 4 + 2 * (31 - __builtin_clz((uint32_t)a));
+    }
+    return any ? b + 4 : 1;
+}
+// Split wins when its SSE + lambda * bits is lower (costs in 1/16 units).
+MXHD bool choose_split(uint64_t sse16, uint32_t bits16, uint64_t sse8, uint32_t bits8, int qp) {
+    const uint64_t l = kLambdaSse16[qp < 0 ? 0 : (qp > 51 ? 51 : qp)];
+    return sse8 * 16 + l * bits8 < sse16 * 16 + l * bits16;
+}
+
+// The split transform tree of an inter CU: luma TU k is the 8x8 block (k & 1, k >> 1) of the
+// 16x16 residual, chroma TU k the 4x4 block (k & 1, k >> 1) of each 8x8 chroma residual; levels
+// go to the CU's sub-blocks 4k.. (luma), 16 + k (Cb), 20 + k (Cr), i.e. co + 64k,
+// co + 256 + 16k, co + 320 + 16k, each TU in scan order.  rr / rrc: reconstructed residuals.
+MXHD void split_encode(const int* res, const int (*rc)[64], int qp, int qpc, int16_t* co, int* rr, int (*rrc)[64]) {
+    int blk[64], rb[64];
+    for (int k = 0; k < 4; ++k) {
+        const int bx = (k & 1) * 8, by = (k >> 1) * 8;
+        for (int r = 0; r < 8; ++r)
+            for (int q = 0; q < 8; ++q) blk[r * 8 + q] = res[(by + r) * 16 + bx + q];
+        tu_encode(3, blk, qp, false, co + 64 * k, rb);
+        for (int r = 0; r < 8; ++r)
+            for (int q = 0; q < 8; ++q) rr[(by + r) * 16 + bx + q] = rb[r * 8 + q];
+    }
+    for (int comp = 0; comp < 2; ++comp)
+        for (int k = 0; k < 4; ++k) {
+            const int bx = (k & 1) * 4, by = (k >> 1) * 4;
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q) blk[r * 4 + q] = rc[comp][(by + r) * 8 + bx + q];
+            tu_encode(2, blk, qpc, false, co + 256 + 64 * comp + 16 * k, rb);
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q) rrc[comp][(by + r) * 8 + bx + q] = rb[r * 4 + q];
+        }
+}
+
+// Estimated level bits of a CU's transform tree (unsplit: 16x16 + 2 x 8x8; split: 4 x 8x8 + 8 x 4x4).
+MXHD uint32_t cu_bits_est(const int16_t* co, bool split) {
+    if (!split) return tu_bits_est(co, 256) + tu_bits_est(co + 256, 64) + tu_bits_est(co + 320, 64);
+    uint32_t b = 0;
+    for (int k = 0; k < 4; ++k) b += tu_bits_est(co + 64 * k, 64);
+    for (int k = 0; k < 8; ++k) b += tu_bits_est(co + 256 + 16 * k, 16);
+    return b;
 }
 
 // Spatial neighbour motion of a 16x16 PU (every CU of a P slice is inter, so "available"
@@ -1146,11 +1358,18 @@ constexpr uint8_t kDbBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0, 
 constexpr uint8_t kDbTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,  1,  1,  1,  1,  1,  1,  1, 1,
                                2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
 
-// bS of the edge between CU p and CU q (8.7.2.4): 2 intra, 1 coded luma residual on either
-// side or a motion difference of >= 1 integer sample (one reference picture), else 0.
-MXHD int db_bs(const CuInfo& p, const CuInfo& q) {
+// Luma cbf of the TU of CU c that holds its 4x4 block (bx, by), 0..3 each.
+MXHD bool tu_cbf_at(const CuInfo& c, int bx, int by) {
+    if (c.tu_split == 2) return (c.cbf_y4 >> ((by >> 1) * 2 + (bx >> 1))) & 1;
+    return c.cbf & 1;
+}
+
+// bS of an edge segment between 4x4 block (pbx, pby) of CU p and (qbx, qby) of CU q
+// (8.7.2.4): 2 intra, 1 coded luma residual in the TU on either side or a motion difference
+// of >= 1 integer sample (one reference picture), else 0.
+MXHD int db_bs(const CuInfo& p, int pbx, int pby, const CuInfo& q, int qbx, int qby) {
     if (p.type == kCuIntra || q.type == kCuIntra) return 2;
-    if ((p.cbf & 1) || (q.cbf & 1)) return 1;
+    if (tu_cbf_at(p, pbx, pby) || tu_cbf_at(q, qbx, qby)) return 1;
     const int dx = p.mvx - q.mvx, dy = p.mvy - q.mvy;
     return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
 }
@@ -1233,7 +1452,7 @@ MXHD void db_edge_seg(uint8_t* ry, uint8_t* ruv, int pitch, int ctb_w, const CuI
                       int dir, int seg, int c_qp_offset) {
     const int x = i % ctb_w, y = i / ctb_w;
     const int j = dir == 0 ? i - 1 : i - ctb_w;
-    const int bs = db_bs(cus[j], cus[i]);
+    const int bs = dir == 0 ? db_bs(cus[j], 3, seg, cus[i], 0, seg) : db_bs(cus[j], seg, 3, cus[i], seg, 0);
     if (!bs) return;
     const int qp_p = qpy[j], qp_q = qpy[i];
     if (dir == 0) {
@@ -1251,6 +1470,24 @@ MXHD void db_edge_seg(uint8_t* ry, uint8_t* ruv, int pitch, int ctb_w, const CuI
     }
 }
 
+// The internal 8x8 TU edge (vertical dir 0 at x = 8, horizontal dir 1 at y = 8) of a CU
+// whose transform tree is split: one PU, so bS is 1 exactly when a TU beside the segment has
+// coded luma; luma only (chroma edges lie on the 16-sample grid).
+MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, const uint8_t* qpy, int i, int dir,
+                          int seg) {
+    const CuInfo& c = cus[i];
+    if (c.tu_split != 2) return;
+    const bool coded = dir == 0 ? (tu_cbf_at(c, 1, seg) || tu_cbf_at(c, 2, seg)) : (tu_cbf_at(c, seg, 1) ||
+                                                                                      tu_cbf_at(c, seg, 2));
+    if (!coded) return;
+    const int x = i % ctb_w, y = i / ctb_w;
+    if (dir == 0)
+        db_luma_seg(ry + (size_t)(y * 16 + seg * 4) * pitch + x * 16 + 8, 1, pitch, 1, qpy[i], qpy[i]);
+    else
+        db_luma_seg(ry + (size_t)(y * 16 + 8) * pitch + x * 16 + seg * 4, pitch, 1, 1, qpy[i], qpy[i]);
+}
+
+// ---------------------------------------------------------------- inter transform-tree decision
 // ---------------------------------------------------------------- adaptive slice layout (P)
 // Entropy-coding cost estimate of a CU in CABAC work units: significance bins up to the
 // last position of every coded TU plus a few bins per coded sub-block, on top of the CU

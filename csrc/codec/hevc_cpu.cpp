@@ -177,7 +177,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.ue(0);  // log2_diff_max_min_luma_coding_block_size (CTB 16)
         w.ue(0);  // log2_min_luma_transform_block_size_minus2 (4)
         w.ue(2);  // log2_diff_max_min_luma_transform_block_size (16)
-        w.ue(0);  // max_transform_hierarchy_depth_inter
+        w.ue(c.tu_split ? 1 : 0);  // max_transform_hierarchy_depth_inter
         w.ue(0);  // max_transform_hierarchy_depth_intra
         w.put(0, 1);  // scaling_list_enabled_flag
         w.put(0, 1);  // amp_enabled_flag
@@ -304,16 +304,7 @@ CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cf
 
 namespace {
 // Finish a CU's residual bookkeeping: cbf / last / coded sub-block masks.
-void summarise(CuInfo& c, const int16_t* coef) {
-    uint32_t m;
-    c.cbf = 0;
-    if (tu_summary(coef, 256, &c.last[0], &m)) c.cbf |= 1;
-    c.csbf_y = (uint16_t)m;
-    if (tu_summary(coef + 256, 64, &c.last[1], &m)) c.cbf |= 2;
-    c.csbf_c[0] = (uint8_t)m;
-    if (tu_summary(coef + 320, 64, &c.last[2], &m)) c.cbf |= 4;
-    c.csbf_c[1] = (uint8_t)m;
-}
+void summarise(CuInfo& c, const int16_t* coef) { cu_summarise(c, coef); }
 }  // namespace
 
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
@@ -424,23 +415,54 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
             const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
             c.qp = (uint8_t)qp;
             int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
-            tu_encode(4, res, qp, false, co, rr);
-            for (int r = 0; r < 16; ++r)
-                for (int q = 0; q < 16; ++q) ry[(y0 + r) * cw_ + x0 + q] = (uint8_t)clip255(pred[r * 16 + q] + rr[r * 16 + q]);
-            for (int comp = 0; comp < 2; ++comp) {
-                int pc[64], rc[64], rrc[64];
-                const int xc = x0 / 2, yc = y0 / 2;
+            int pc[2][64], rc[2][64];
+            const int xc = x0 / 2, yc = y0 / 2;
+            for (int comp = 0; comp < 2; ++comp)
                 for (int r = 0; r < 8; ++r)
                     for (int q = 0; q < 8; ++q) {
                         const int p = chroma_mc(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc + q, yc + r, c.mvx, c.mvy);
-                        pc[r * 8 + q] = p;
-                        rc[r * 8 + q] = suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
+                        pc[comp][r * 8 + q] = p;
+                        rc[comp][r * 8 + q] = suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
                     }
-                tu_encode(3, rc, qpc, false, co + 256 + 64 * comp, rrc);
+            // option 1: one 16x16 luma TU, 8x8 chroma TUs
+            int rrc[2][64];
+            tu_encode(4, res, qp, false, co, rr);
+            for (int comp = 0; comp < 2; ++comp) tu_encode(3, rc[comp], qpc, false, co + 256 + 64 * comp, rrc[comp]);
+            c.tu_split = cfg_.tu_split ? 1 : 0;
+            if (cfg_.tu_split) {
+                // option 2: four 8x8 luma TUs, eight 4x4 chroma TUs; keep the cheaper by SSE + lambda * bits
+                int16_t co2[kCoefPerCu];
+                int rr2[256], rrc2[2][64];
+                split_encode(res, rc, qp, qpc, co2, rr2, rrc2);
+                uint64_t sse1 = 0, sse2 = 0;
+                for (int k = 0; k < 256; ++k) {
+                    const int s0 = pred[k] + res[k];
+                    const int e1 = s0 - clip255(pred[k] + rr[k]), e2 = s0 - clip255(pred[k] + rr2[k]);
+                    sse1 += (uint64_t)(e1 * e1);
+                    sse2 += (uint64_t)(e2 * e2);
+                }
+                for (int comp = 0; comp < 2; ++comp)
+                    for (int k = 0; k < 64; ++k) {
+                        const int s0 = pc[comp][k] + rc[comp][k];
+                        const int e1 = s0 - clip255(pc[comp][k] + rrc[comp][k]);
+                        const int e2 = s0 - clip255(pc[comp][k] + rrc2[comp][k]);
+                        sse1 += (uint64_t)(e1 * e1);
+                        sse2 += (uint64_t)(e2 * e2);
+                    }
+                if (choose_split(sse1, cu_bits_est(co, false), sse2, cu_bits_est(co2, true), qp)) {
+                    c.tu_split = 2;
+                    std::memcpy(co, co2, sizeof co2);
+                    std::memcpy(rr, rr2, sizeof rr2);
+                    std::memcpy(rrc, rrc2, sizeof rrc2);
+                }
+            }
+            for (int r = 0; r < 16; ++r)
+                for (int q = 0; q < 16; ++q) ry[(y0 + r) * cw_ + x0 + q] = (uint8_t)clip255(pred[r * 16 + q] + rr[r * 16 + q]);
+            for (int comp = 0; comp < 2; ++comp)
                 for (int r = 0; r < 8; ++r)
                     for (int q = 0; q < 8; ++q)
-                        ruv[(yc + r) * cw_ + 2 * (xc + q) + comp] = (uint8_t)clip255(pc[r * 8 + q] + rrc[r * 8 + q]);
-            }
+                        ruv[(yc + r) * cw_ + 2 * (xc + q) + comp] =
+                            (uint8_t)clip255(pc[comp][r * 8 + q] + rrc[comp][r * 8 + q]);
             summarise(c, co);
         }
     // cost-balanced slices, then the merge / AMVP decisions against each slice's neighbours
@@ -476,12 +498,13 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
             slice_qpy(cu_.data(), first, count, qp, qpy.data());
         }
         for (int dir = 0; dir < 2; ++dir)
-            for (int i = 0; i < W * H; ++i) {
-                if (dir == 0 ? (i % W) == 0 : (i / W) == 0) continue;
-                for (int seg = 0; seg < 4; ++seg)
-                    db_edge_seg(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir, seg,
-                                cfg_.chroma_qp_offset);
-            }
+            for (int i = 0; i < W * H; ++i)
+                for (int seg = 0; seg < 4; ++seg) {
+                    if (dir == 0 ? (i % W) != 0 : (i / W) != 0)
+                        db_edge_seg(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir,
+                                    seg, cfg_.chroma_qp_offset);
+                    db_internal_seg(rec_y_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir, seg);
+                }
     }
     au_.clear();
     if (idr) common_.write_parameter_sets(au_);

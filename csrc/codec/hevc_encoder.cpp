@@ -132,6 +132,7 @@ bool GpuHevcEncoder::prepare(bool force_idr) {
     f.slice_rows = common_.slice_rows();
     f.num_slices = common_.num_slices();
     f.aq = cfg_.aq;
+    f.tu_split = cfg_.tu_split ? 1 : 0;
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
     // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
     f.n_sse_parts = (idr || cfg_.deblock) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;

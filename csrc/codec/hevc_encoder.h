@@ -110,6 +110,7 @@ struct HevcFrameState {
     int32_t aq;
     int32_t chroma_qp_offset;
     int32_t n_sse_parts;  // distortion partials written this frame (P: one per 4 CUs, I: one per CTU row)
+    int32_t tu_split;     // inter CUs may split their transform tree (EncoderConfig.tu_split)
     unsigned long long* sse_part;  // [3][kSsePartStride] per-workgroup distortion partials
 };
 

@@ -80,7 +80,9 @@ struct TuResult {
     int last[3];
     uint32_t csbf[3];
     int nz[3];
-    int sse[3];
+    int sse[3];     // over the display area (PSNR)
+    int sse_full;   // over the whole CU (transform-tree decision, as the CPU encoder)
+    uint32_t bits;  // cu_bits_est of the levels (unsplit tree)
 };
 
 __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool intra, bool valid,
@@ -190,10 +192,12 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         }
     }
     nzl = nzc = 0;
+    int lbits = 0, cbits = 0;  // tu_bits_est terms of this lane's levels
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = lane * 4 + j, k2 = idx >> 4, k = idx & 15;
             const int l = ll[j];
+            if (l) lbits += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
             const int si = scan_index(4, k, k2);
             coef[si] = (int16_t)l;
             t.b[idx] = dequant_coef(l, qp, 4);
@@ -206,6 +210,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         for (int j = 0; j < 2; ++j) {
             const int idx = cl * 2 + j, k2 = idx >> 3, k = idx & 7;
             const int l = lc[j];
+            if (l) cbits += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
             const int si = scan_index(3, k, k2);
             coef[256 + comp * 64 + si] = (int16_t)l;
             t.b[256 + comp * 64 + idx] = dequant_coef(l, qpc, 3);
@@ -228,6 +233,10 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         out.csbf[1] = wor(comp == 0 ? csc : 0u);
         out.csbf[2] = wor(comp == 1 ? csc : 0u);
     }
+    {
+        const int bl = wsum(lbits), bcb = wsum(comp == 0 ? cbits : 0), bcr = wsum(comp == 1 ? cbits : 0);
+        out.bits = (uint32_t)((out.nz[0] ? bl + 4 : 1) + (out.nz[1] ? bcb + 4 : 1) + (out.nz[2] ? bcr + 4 : 1));
+    }
     __syncthreads();
     // ---- inverse stage 1 (columns): a[y][x] = clip16((sum_k T[k][y] b[k][x] + 64) >> 7)
     if (valid) {
@@ -249,7 +258,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     }
     __syncthreads();
     // ---- inverse stage 2 (rows) + reconstruction
-    int sy = 0, sc = 0;
+    int sy = 0, sc = 0, sf = 0;
     if (valid) {
         const int y = lane >> 2, xb = (lane & 3) * 4;
         uint32_t packed = 0;
@@ -263,6 +272,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             const int v = clip255(p + r);
             const int e = p + t.res[y * 16 + x] - v;
             sy += (x0 + x < disp_w && y0 + y < disp_h) ? e * e : 0;
+            sf += e * e;
             packed |= (uint32_t)v << (8 * j);
             t.pred[y * 16 + x] = (uint8_t)v;  // reconstruction stays readable in LDS
         }
@@ -282,16 +292,21 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             t.pred[o] = (uint8_t)v;
             const int xc = x0 / 2 + x, yc = y0 / 2 + yy;
             sc += (2 * xc < disp_w && 2 * yc < disp_h) ? e * e : 0;
+            sf += e * e;
             rec_uv[(size_t)yc * pitch_y + 2 * xc + comp] = (uint8_t)v;
         }
     }
     out.sse[0] = wsum(sy);
     out.sse[1] = wsum(comp == 0 ? sc : 0);
     out.sse[2] = wsum(comp == 1 ? sc : 0);
+    out.sse_full = wsum(sf);
     return out;
 }
 
 __device__ __forceinline__ void fill_cu(CuInfo& c, const TuResult& r) {
+    c.tu_split = 0;
+    c.cbf_y4 = c.cbf_c4 = 0;
+    c.pad = 0;
     c.cbf = (uint8_t)((r.nz[0] ? 1 : 0) | (r.nz[1] ? 2 : 0) | (r.nz[2] ? 4 : 0));
     c.last[0] = (uint8_t)(r.last[0] < 0 ? 0 : r.last[0]);
     c.last[1] = (uint8_t)(r.last[1] < 0 ? 0 : r.last[1]);
@@ -311,6 +326,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     __shared__ Mats M;
     __shared__ TuBuf tb[4];
     __shared__ unsigned long long part[3][4];
+    __shared__ int16_t lv2[4][kCoefPerCu];  // split transform tree: levels and reconstruction
+    __shared__ uint8_t rec2[4][384];
     fill_mats(M);
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -375,12 +392,67 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     __syncthreads();
     int16_t* co = coef + (size_t)(valid ? i : 0) * kCoefPerCu;
+    // option 2, the split transform tree (split_encode of the CPU encoder, one TU per lane):
+    // lanes 0..3 the 8x8 luma TUs, lanes 4..11 the 4x4 Cb / Cr TUs
+    const bool try_split = fs->tu_split != 0;
+    int s2f = 0, s2d = 0, b2 = 0;
+    if (try_split && valid && lane < 12) {
+        int blk[64], rb[64];
+        if (lane < 4) {
+            const int k = lane, bx = (k & 1) * 8, by = (k >> 1) * 8;
+            for (int rr = 0; rr < 8; ++rr)
+                for (int q = 0; q < 8; ++q) blk[rr * 8 + q] = t.res[(by + rr) * 16 + bx + q];
+            int16_t* lv = &lv2[wave][64 * k];
+            tu_encode_t<3>(blk, qp, false, lv, rb);
+            b2 = (int)tu_bits_est(lv, 64);
+            for (int rr = 0; rr < 8; ++rr)
+                for (int q = 0; q < 8; ++q) {
+                    const int o = (by + rr) * 16 + bx + q, p = t.pred[o];
+                    const int v = clip255(p + rb[rr * 8 + q]), e = p + t.res[o] - v;
+                    s2f += e * e;
+                    s2d += (x0 + bx + q < g.width && y0 + by + rr < g.height) ? e * e : 0;
+                    rec2[wave][o] = (uint8_t)v;
+                }
+        } else {
+            const int comp = (lane - 4) >> 2, k = (lane - 4) & 3, bx = (k & 1) * 4, by = (k >> 1) * 4;
+            for (int rr = 0; rr < 4; ++rr)
+                for (int q = 0; q < 4; ++q) blk[rr * 4 + q] = t.res[256 + comp * 64 + (by + rr) * 8 + bx + q];
+            int16_t* lv = &lv2[wave][256 + 64 * comp + 16 * k];
+            tu_encode_t<2>(blk, qpc, false, lv, rb);
+            b2 = (int)tu_bits_est(lv, 16);
+            for (int rr = 0; rr < 4; ++rr)
+                for (int q = 0; q < 4; ++q) {
+                    const int o = 256 + comp * 64 + (by + rr) * 8 + bx + q, p = t.pred[o];
+                    const int v = clip255(p + rb[rr * 4 + q]), e = p + t.res[o] - v;
+                    s2f += e * e;
+                    s2d += (2 * (x0 / 2 + bx + q) < g.width && 2 * (y0 / 2 + by + rr) < g.height) ? e * e : 0;
+                    rec2[wave][o] = (uint8_t)v;
+                }
+        }
+    }
+    const int sse2 = wsum(s2f), bits2 = wsum(b2);
+    const int sse2y = wsum(lane < 4 ? s2d : 0), sse2u = wsum(lane >= 4 && lane < 8 ? s2d : 0),
+              sse2v = wsum(lane >= 8 && lane < 12 ? s2d : 0);
+    // option 1, one 16x16 luma TU (writes its levels and reconstruction)
     const TuResult r = code_tus(t, M, qp, qpc, false, valid, co, fs->rec_y, g.pitch, fs->rec_uv, x0, y0, g.width,
                                 g.height);
+    const bool split = try_split && valid &&
+                       choose_split((uint64_t)r.sse_full, r.bits, (uint64_t)sse2, (uint32_t)bits2, qp);  // wave-uniform
+    if (split) {  // the split tree wins: overwrite option 1's levels and reconstruction
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int k = lane; k < kCoefPerCu; k += 64) co[k] = lv2[wave][k];
+        const int yy = lane >> 2, xb = (lane & 3) * 4;
+        uint32_t packed = 0;
+        for (int j = 0; j < 4; ++j) packed |= (uint32_t)rec2[wave][yy * 16 + xb + j] << (8 * j);
+        *reinterpret_cast<uint32_t*>(fs->rec_y + (size_t)(y0 + yy) * g.pitch + x0 + xb) = packed;
+        const int rc = lane >> 3, cc = lane & 7;
+        for (int comp = 0; comp < 2; ++comp)
+            fs->rec_uv[(size_t)(y0 / 2 + rc) * g.pitch + 2 * (x0 / 2 + cc) + comp] = rec2[wave][256 + comp * 64 + rc * 8 + cc];
+    }
     if (lane == 0) {
-        part[0][wave] = valid ? (unsigned long long)r.sse[0] : 0ull;
-        part[1][wave] = valid ? (unsigned long long)r.sse[1] : 0ull;
-        part[2][wave] = valid ? (unsigned long long)r.sse[2] : 0ull;
+        part[0][wave] = valid ? (unsigned long long)(split ? sse2y : r.sse[0]) : 0ull;
+        part[1][wave] = valid ? (unsigned long long)(split ? sse2u : r.sse[1]) : 0ull;
+        part[2][wave] = valid ? (unsigned long long)(split ? sse2v : r.sse[2]) : 0ull;
     }
     if (valid && lane == 0) {
         CuInfo c;
@@ -392,6 +464,10 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         c.mvdx = c.mvdy = 0;
         c.mvp_idx = 0;
         fill_cu(c, r);
+        if (try_split) {
+            c.tu_split = split ? 2 : 1;
+            if (split) cu_summarise(c, lv2[wave]);
+        }
         cus[i] = c;  // skip / merge / AMVP are decided by k_hevc_decide once the slices are laid out
         cost[i] = cu_cost(c);
         qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
@@ -719,10 +795,10 @@ struct WaveCoef {
 };
 
 __device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
-    // 5 dwords (CuInfo is 20 bytes, 4-byte aligned in the array) -> scalar loads
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(cus) + (size_t)i * 5;
-    uint32_t w[5];
-    for (int k = 0; k < 5; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[k]);
+    // kCuWords dwords (CuInfo is 24 bytes, 4-byte aligned in the array) -> wave-uniform values
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(cus) + (size_t)i * kCuWords;
+    uint32_t w[kCuWords];
+    for (int k = 0; k < kCuWords; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[k]);
     CuInfo c;
     __builtin_memcpy(&c, w, sizeof c);
     return c;
@@ -759,23 +835,23 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
     // software pipeline: the next CU's descriptor words and levels are loaded (vector loads
     // in flight) while the current CU is coded
     const uint32_t* cuw = reinterpret_cast<const uint32_t*>(cus);
-    uint32_t raw[5];
+    uint32_t raw[kCuWords];
     int vn[6];
-    for (int q = 0; q < 5; ++q) raw[q] = cuw[(size_t)first * 5 + q];
+    for (int q = 0; q < kCuWords; ++q) raw[q] = cuw[(size_t)first * kCuWords + q];
     for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)first * kCoefPerCu + q * 64 + lane];
     for (int k = 0; k < count; ++k) {
         const int i = first + k;
         const int x = i % g.mb_w;
         CuInfo c;
         {
-            uint32_t w[5];
-            for (int q = 0; q < 5; ++q) w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)raw[q]);
+            uint32_t w[kCuWords];
+            for (int q = 0; q < kCuWords; ++q) w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)raw[q]);
             __builtin_memcpy(&c, w, sizeof c);
         }
         int v[6];
         for (int q = 0; q < 6; ++q) v[q] = vn[q];
         if (k + 1 < count) {
-            for (int q = 0; q < 5; ++q) raw[q] = cuw[(size_t)(i + 1) * 5 + q];
+            for (int q = 0; q < kCuWords; ++q) raw[q] = cuw[(size_t)(i + 1) * kCuWords + q];
             for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)(i + 1) * kCoefPerCu + q * 64 + lane];
         }
         WaveCoef cf;
@@ -841,8 +917,10 @@ __global__ __launch_bounds__(256) void k_hevc_deblock(Geometry g, const HevcFram
     const int ncu = g.mb_w * g.mb_h;
     if (t >= ncu * 4) return;
     const int i = t >> 2, seg = t & 3;
-    if (dir == 0 ? (i % g.mb_w) == 0 : (i / g.mb_w) == 0) return;
-    db_edge_seg(fs->rec_y, fs->rec_uv, g.pitch, g.mb_w, cus, qpy, i, dir, seg, fs->chroma_qp_offset);
+    if (dir == 0 ? (i % g.mb_w) != 0 : (i / g.mb_w) != 0)
+        db_edge_seg(fs->rec_y, fs->rec_uv, g.pitch, g.mb_w, cus, qpy, i, dir, seg, fs->chroma_qp_offset);
+    // internal 8x8 TU edge of a split CU: 8 samples from the CU edge, disjoint from its filtering
+    db_internal_seg(fs->rec_y, g.pitch, g.mb_w, cus, qpy, i, dir, seg);
 }
 
 // Distortion of the final (deblocked) picture over the display area: one workgroup per CTU

@@ -1083,6 +1083,7 @@ class Decoder:
         else:
             cbf_cb, cbf_cr = parent_cbf
         if split:
+            self.stats["tu_split"] = self.stats.get("tu_split", 0) + 1
             h = 1 << (log2 - 1)
             for k, (dx, dy) in enumerate(((0, 0), (h, 0), (0, h), (h, h))):
                 self._transform_tree(cab, x0 + dx, y0 + dy, x0, y0, log2 - 1, depth + 1, k, max_depth, intra,

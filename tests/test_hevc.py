@@ -20,8 +20,9 @@ from mxdesk.codec.hevc_decoder import Decoder, psnr
 from .test_cpu_encoder import synthetic_nv12
 
 
-def _cfg(native, w, h, fps=60, qp=28, bitrate=0, aq=1, sr=8):
+def _cfg(native, w, h, fps=60, qp=28, bitrate=0, aq=1, sr=8, tu_split=0):
     cfg = native.EncoderConfig()
+    cfg.tu_split = tu_split
     cfg.width, cfg.height, cfg.fps = w, h, fps
     cfg.bitrate_kbps = bitrate
     cfg.qp = qp
@@ -30,8 +31,8 @@ def _cfg(native, w, h, fps=60, qp=28, bitrate=0, aq=1, sr=8):
     return cfg
 
 
-def _cpu_roundtrip(native, w, h, frames, fps=60, qp=28, bitrate=0, fresh=False, idr_at=()):
-    enc = native.CpuHevcEncoder(_cfg(native, w, h, fps, qp, bitrate))
+def _cpu_roundtrip(native, w, h, frames, fps=60, qp=28, bitrate=0, fresh=False, idr_at=(), tu_split=0):
+    enc = native.CpuHevcEncoder(_cfg(native, w, h, fps, qp, bitrate, tu_split=tu_split))
     stream, recon, src, sizes = b"", [], [], []
     for t in range(frames):
         y, uv = synthetic_nv12(w, h, t, seed=t if fresh else 0)
@@ -158,12 +159,12 @@ def test_decoder_rejects_truncated_stream(native):
 
 
 # ---------------------------------------------------------------------------- GPU tier
-def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8):
+def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0):
     import torch
 
     from .gpu_util import pitched
 
-    cfg = _cfg(gpu, w, h, fps, qp, sr=sr)
+    cfg = _cfg(gpu, w, h, fps, qp, sr=sr, tu_split=tu_split)
     stream = torch.cuda.current_stream().cuda_stream
     genc = gpu.GpuHevcEncoder(cfg, stream)
     cenc = gpu.CpuHevcEncoder(cfg)
@@ -183,6 +184,8 @@ def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8):
         assert tuple(genc.stats.sse) == tuple(cs.sse)
     dec = Decoder()
     dec.decode(gs)
+    if tu_split:
+        assert dec.stats.get("tu_split", 0) > 0, "no CU chose the split transform tree"
     for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
         assert np.array_equal(yy, ry)
         assert np.array_equal(u, ruv[:, 0::2])
@@ -194,6 +197,14 @@ def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8):
                                         (128, 96, 60, 4)])
 def test_gpu_hevc_bit_exact_vs_cpu(gpu, w, h, fps, qp):
     _gpu_vs_cpu(gpu, w, h, 3, fps=fps, qp=qp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,qp", [(160, 96, 30), (320, 192, 24), (100, 60, 38)])
+def test_gpu_hevc_tu_split_bit_exact_vs_cpu(gpu, w, h, qp):
+    """Split transform trees (8x8 luma / 4x4 chroma TUs), chosen per CU by the same rule on
+    both sides: GPU bitstream == CPU bitstream, decoded == reconstruction (deblocking on)."""
+    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=1)
 
 
 @pytest.mark.gpu
@@ -244,3 +255,32 @@ def test_cpu_hevc_deblocking(native):
         out[db] = (recon, err)
     assert not np.array_equal(out[0][0][0], out[1][0][0])
     assert out[1][1] < out[0][1]
+
+
+@pytest.mark.parametrize("w,h,qp", [(64, 48, 28), (160, 96, 30), (100, 60, 40), (320, 192, 22)])
+def test_cpu_hevc_tu_split_decodes_to_reconstruction(native, w, h, qp):
+    """Inter transform trees split into 8x8 luma / 4x4 chroma TUs where SSE + lambda * bits
+    prefers it; the independent decoder (with deblocking of the internal TU edges) must
+    reproduce the reconstruction exactly and must actually see split trees."""
+    out, src, sizes, dec, _ = _cpu_roundtrip(native, w, h, 4, qp=qp, fresh=True, tu_split=1)
+    assert dec.stats.get("tu_split", 0) > 0
+
+
+def test_cpu_hevc_tu_split_saves_bits_on_desktop_content(native):
+    """On the synthetic desktop the split tree codes P pictures in fewer bytes at a higher
+    PSNR than 16x16-only TUs (profiles/r01_rd)."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    res = {}
+    for split in (0, 1):
+        enc = native.CpuHevcEncoder(_cfg(native, 320, 192, qp=32, tu_split=split))
+        desk = CpuSyntheticDesktop(320, 192, False)
+        nbytes, err = 0, 0.0
+        for f in range(6):
+            y, uv = bgrx_to_nv12(desk.render(f, f / 60, 0))
+            au = enc.encode(y, uv, False)
+            if f:
+                nbytes += len(au)
+                err += float(((enc.recon()[0][:192, :320].astype(np.int64) - y) ** 2).sum())
+        res[split] = (nbytes, err)
+    assert res[1][0] < res[0][0] and res[1][1] <= res[0][1] * 1.02
