@@ -37,6 +37,17 @@ __device__ __forceinline__ int wsum(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// reductions inside aligned groups of G lanes (G = 8 or 16): every lane gets its group's value
+template <int G>
+__device__ __forceinline__ int gsum(int v) {
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int G>
+__device__ __forceinline__ int gmax(int v) {
+    for (int o = G / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
 __device__ __forceinline__ int wmax(int v) {
     for (int o = 32; o > 0; o >>= 1) {
         const int t = __shfl_xor(v, o, 64);
@@ -53,13 +64,16 @@ __device__ __forceinline__ uint32_t wor(uint32_t v) {
 struct Mats {
     int16_t t16[256];
     int16_t t8[64];
+    int16_t t4[16];
 };
 __device__ __forceinline__ void fill_mats(Mats& m) {
-    for (int i = threadIdx.x; i < 256 + 64; i += blockDim.x) {
+    for (int i = threadIdx.x; i < 256 + 64 + 16; i += blockDim.x) {
         if (i < 256)
             m.t16[i] = (int16_t)dct_coef(4, i >> 4, i & 15);
-        else
+        else if (i < 320)
             m.t8[i - 256] = (int16_t)dct_coef(3, (i - 256) >> 3, (i - 256) & 7);
+        else
+            m.t4[i - 320] = (int16_t)dct_coef(2, (i - 320) >> 2, (i - 320) & 3);
     }
 }
 
@@ -303,6 +317,203 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     return out;
 }
 
+// The split transform tree of an inter CU (split_encode / tu_encode_t of the CPU encoder,
+// same integer stages), computed by the whole wave: luma TU k = lanes 16k..16k+15 with 4
+// coefficients each, chroma TU (comp, k) = lanes 8(4comp+k).. with 2 each; decimation and
+// the trailing trim per TU through segmented shuffle reductions.  Levels go to lv (CU
+// layout), the reconstruction to rec (TuBuf layout); t.a / t.b are the stage buffers.
+// Called by every wave of the workgroup (barriers inside).
+struct SplitResult {
+    int sse_full;
+    int sse[3];
+    uint32_t bits;
+};
+__device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool valid, int16_t* lv,
+                                                uint8_t* rec, int x0, int y0, int disp_w, int disp_h) {
+    const int lane = threadIdx.x & 63;
+    const int tk = lane >> 4, lbx = (tk & 1) * 8, lby = (tk >> 1) * 8, lbase = 64 * tk;  // luma TU of the lane
+    const int ct = lane >> 3, comp = ct >> 2, ck = ct & 3;                                 // chroma TU of the lane
+    const int cbx = (ck & 1) * 4, cby = (ck >> 1) * 4, cbase = 256 + 64 * comp + 16 * ck;
+    // ---- forward stage 1 (rows)
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = (lane & 15) * 4 + j, y = idx >> 3, k = idx & 7;
+            int s = 0;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) s += M.t8[k * 8 + n] * t.res[(lby + y) * 16 + lbx + n];
+            t.a[lbase + idx] = (s + 2) >> 2;
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = (lane & 7) * 2 + j, y = idx >> 2, k = idx & 3;
+            int s = 0;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) s += M.t4[k * 4 + n] * t.res[256 + comp * 64 + (cby + y) * 8 + cbx + n];
+            t.a[cbase + idx] = (s + 1) >> 1;
+        }
+    }
+    __syncthreads();
+    // ---- forward stage 2 (columns) + quantisation
+    int ll[4] = {0, 0, 0, 0}, lc[2] = {0, 0};
+    int sil[4], sic[2];
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = (lane & 15) * 4 + j, k2 = idx >> 3, k = idx & 7;
+            int s = 0;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) s += M.t8[k2 * 8 + y] * t.a[lbase + y * 8 + k];
+            ll[j] = quant_coef((s + 256) >> 9, qp, 3, false);
+            sil[j] = scan_index(3, k, k2);
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = (lane & 7) * 2 + j, k2 = idx >> 2, k = idx & 3;
+            int s = 0;
+#pragma unroll
+            for (int y = 0; y < 4; ++y) s += M.t4[k2 * 4 + y] * t.a[cbase + y * 4 + k];
+            lc[j] = quant_coef((s + 128) >> 8, qpc, 2, false);
+            sic[j] = scan_index(2, k, k2);
+        }
+    } else {
+        for (int j = 0; j < 4; ++j) sil[j] = 0;
+        for (int j = 0; j < 2; ++j) sic[j] = 0;
+    }
+    // ---- decimation per TU
+    {
+        int nz = 0, mx = 0;
+        for (int j = 0; j < 4; ++j) {
+            nz += ll[j] != 0;
+            mx = max(mx, abs(ll[j]));
+        }
+        if (tu_decimate(3, false, gsum<16>(nz), gmax<16>(mx)))
+            for (int j = 0; j < 4; ++j) ll[j] = 0;
+        nz = mx = 0;
+        for (int j = 0; j < 2; ++j) {
+            nz += lc[j] != 0;
+            mx = max(mx, abs(lc[j]));
+        }
+        if (tu_decimate(2, false, gsum<8>(nz), gmax<8>(mx)))
+            for (int j = 0; j < 2; ++j) lc[j] = 0;
+    }
+    // ---- trailing isolated +-1 trim per TU (tu_encode_t rule; a stopped TU stays stopped)
+    {
+        bool on_l = true, on_c = true;
+        for (int it = 0; it < kTrimIters; ++it) {
+            int last = -1;
+            for (int j = 0; j < 4; ++j)
+                if (ll[j]) last = max(last, sil[j]);
+            last = gmax<16>(last);
+            int prev = -1, lvv = 0;
+            for (int j = 0; j < 4; ++j) {
+                if (ll[j] && sil[j] < last) prev = max(prev, sil[j]);
+                if (ll[j] && sil[j] == last) lvv = abs(ll[j]);
+            }
+            prev = gmax<16>(prev);
+            lvv = gmax<16>(lvv);
+            if (last < 0 || lvv != 1 || last - prev <= kTrimGap) on_l = false;
+            if (on_l)
+                for (int j = 0; j < 4; ++j)
+                    if (sil[j] == last) ll[j] = 0;
+            int lastc = -1;
+            for (int j = 0; j < 2; ++j)
+                if (lc[j]) lastc = max(lastc, sic[j]);
+            lastc = gmax<8>(lastc);
+            int prevc = -1, lvc = 0;
+            for (int j = 0; j < 2; ++j) {
+                if (lc[j] && sic[j] < lastc) prevc = max(prevc, sic[j]);
+                if (lc[j] && sic[j] == lastc) lvc = abs(lc[j]);
+            }
+            prevc = gmax<8>(prevc);
+            lvc = gmax<8>(lvc);
+            if (lastc < 0 || lvc != 1 || lastc - prevc <= kTrimGap) on_c = false;
+            if (on_c)
+                for (int j = 0; j < 2; ++j)
+                    if (sic[j] == lastc) lc[j] = 0;
+        }
+    }
+    // ---- levels, dequantised values, per-TU counts and bit estimates
+    int nzl = 0, nzc = 0, bl = 0, bc = 0;
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = (lane & 15) * 4 + j, k2 = idx >> 3, k = idx & 7;
+            const int l = ll[j];
+            lv[lbase + sil[j]] = (int16_t)l;
+            t.b[lbase + k2 * 8 + k] = dequant_coef(l, qp, 3);
+            if (l) {
+                ++nzl;
+                bl += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
+            }
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = (lane & 7) * 2 + j, k2 = idx >> 2, k = idx & 3;
+            const int l = lc[j];
+            lv[cbase + sic[j]] = (int16_t)l;
+            t.b[cbase + k2 * 4 + k] = dequant_coef(l, qpc, 2);
+            if (l) {
+                ++nzc;
+                bc += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
+            }
+        }
+    }
+    nzl = gsum<16>(nzl);
+    nzc = gsum<8>(nzc);
+    bl = gsum<16>(bl);
+    bc = gsum<8>(bc);
+    SplitResult out;
+    out.bits = (uint32_t)wsum(((lane & 15) == 0 ? (nzl ? bl + 4 : 1) : 0) + ((lane & 7) == 0 ? (nzc ? bc + 4 : 1) : 0));
+    __syncthreads();
+    // ---- inverse stage 1 (columns)
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = (lane & 15) * 4 + j, y = idx >> 3, x = idx & 7;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + y] * t.b[lbase + k * 8 + x];
+            t.a[lbase + idx] = clip16((s + 64) >> 7);
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = (lane & 7) * 2 + j, y = idx >> 2, x = idx & 3;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s += M.t4[k * 4 + y] * t.b[cbase + k * 4 + x];
+            t.a[cbase + idx] = clip16((s + 64) >> 7);
+        }
+    }
+    __syncthreads();
+    // ---- inverse stage 2 (rows) + reconstruction
+    int sf = 0, sy = 0, sc = 0;
+    if (valid) {
+        for (int j = 0; j < 4; ++j) {
+            const int idx = (lane & 15) * 4 + j, y = idx >> 3, x = idx & 7;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + x] * t.a[lbase + y * 8 + k];
+            const int r = nzl ? (s + 2048) >> 12 : 0;
+            const int o = (lby + y) * 16 + lbx + x, p = t.pred[o];
+            const int v = clip255(p + r), e = p + t.res[o] - v;
+            sf += e * e;
+            sy += (x0 + lbx + x < disp_w && y0 + lby + y < disp_h) ? e * e : 0;
+            rec[o] = (uint8_t)v;
+        }
+        for (int j = 0; j < 2; ++j) {
+            const int idx = (lane & 7) * 2 + j, y = idx >> 2, x = idx & 3;
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s += M.t4[k * 4 + x] * t.a[cbase + y * 4 + k];
+            const int r = nzc ? (s + 2048) >> 12 : 0;
+            const int o = 256 + comp * 64 + (cby + y) * 8 + cbx + x, p = t.pred[o];
+            const int v = clip255(p + r), e = p + t.res[o] - v;
+            sf += e * e;
+            sc += (2 * (x0 / 2 + cbx + x) < disp_w && 2 * (y0 / 2 + cby + y) < disp_h) ? e * e : 0;
+            rec[o] = (uint8_t)v;
+        }
+    }
+    out.sse_full = wsum(sf);
+    out.sse[0] = wsum(sy);
+    out.sse[1] = wsum(comp == 0 ? sc : 0);
+    out.sse[2] = wsum(comp == 1 ? sc : 0);
+    __syncthreads();
+    return out;
+}
+
 __device__ __forceinline__ void fill_cu(CuInfo& c, const TuResult& r) {
     c.tu_split = 0;
     c.cbf_y4 = c.cbf_c4 = 0;
@@ -392,47 +603,13 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     __syncthreads();
     int16_t* co = coef + (size_t)(valid ? i : 0) * kCoefPerCu;
-    // option 2, the split transform tree (split_encode of the CPU encoder, one TU per lane):
-    // lanes 0..3 the 8x8 luma TUs, lanes 4..11 the 4x4 Cb / Cr TUs
-    const bool try_split = fs->tu_split != 0;
-    int s2f = 0, s2d = 0, b2 = 0;
-    if (try_split && valid && lane < 12) {
-        int blk[64], rb[64];
-        if (lane < 4) {
-            const int k = lane, bx = (k & 1) * 8, by = (k >> 1) * 8;
-            for (int rr = 0; rr < 8; ++rr)
-                for (int q = 0; q < 8; ++q) blk[rr * 8 + q] = t.res[(by + rr) * 16 + bx + q];
-            int16_t* lv = &lv2[wave][64 * k];
-            tu_encode_t<3>(blk, qp, false, lv, rb);
-            b2 = (int)tu_bits_est(lv, 64);
-            for (int rr = 0; rr < 8; ++rr)
-                for (int q = 0; q < 8; ++q) {
-                    const int o = (by + rr) * 16 + bx + q, p = t.pred[o];
-                    const int v = clip255(p + rb[rr * 8 + q]), e = p + t.res[o] - v;
-                    s2f += e * e;
-                    s2d += (x0 + bx + q < g.width && y0 + by + rr < g.height) ? e * e : 0;
-                    rec2[wave][o] = (uint8_t)v;
-                }
-        } else {
-            const int comp = (lane - 4) >> 2, k = (lane - 4) & 3, bx = (k & 1) * 4, by = (k >> 1) * 4;
-            for (int rr = 0; rr < 4; ++rr)
-                for (int q = 0; q < 4; ++q) blk[rr * 4 + q] = t.res[256 + comp * 64 + (by + rr) * 8 + bx + q];
-            int16_t* lv = &lv2[wave][256 + 64 * comp + 16 * k];
-            tu_encode_t<2>(blk, qpc, false, lv, rb);
-            b2 = (int)tu_bits_est(lv, 16);
-            for (int rr = 0; rr < 4; ++rr)
-                for (int q = 0; q < 4; ++q) {
-                    const int o = 256 + comp * 64 + (by + rr) * 8 + bx + q, p = t.pred[o];
-                    const int v = clip255(p + rb[rr * 4 + q]), e = p + t.res[o] - v;
-                    s2f += e * e;
-                    s2d += (2 * (x0 / 2 + bx + q) < g.width && 2 * (y0 / 2 + by + rr) < g.height) ? e * e : 0;
-                    rec2[wave][o] = (uint8_t)v;
-                }
-        }
-    }
-    const int sse2 = wsum(s2f), bits2 = wsum(b2);
-    const int sse2y = wsum(lane < 4 ? s2d : 0), sse2u = wsum(lane >= 4 && lane < 8 ? s2d : 0),
-              sse2v = wsum(lane >= 8 && lane < 12 ? s2d : 0);
+    // option 2, the split transform tree (split_encode of the CPU encoder), whole wave
+    const bool try_split = fs->tu_split != 0;  // uniform over the grid: barriers inside are safe
+    SplitResult r2 = {0, {0, 0, 0}, 0};
+    if (try_split)
+        r2 = split_tus(t, M, qp, qpc, valid, lv2[wave], rec2[wave], x0, y0, g.width, g.height);
+    const int sse2 = r2.sse_full, bits2 = (int)r2.bits;
+    const int sse2y = r2.sse[0], sse2u = r2.sse[1], sse2v = r2.sse[2];
     // option 1, one 16x16 luma TU (writes its levels and reconstruction)
     const TuResult r = code_tus(t, M, qp, qpc, false, valid, co, fs->rec_y, g.pitch, fs->rec_uv, x0, y0, g.width,
                                 g.height);
