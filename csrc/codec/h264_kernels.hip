@@ -114,42 +114,104 @@ __device__ __forceinline__ int qpel_planes(const Planes& P, int x4, int y4) {
     return (bb + hh + 1) >> 1;
 }
 
-// LDS-tiled F/H/V/J plane builder: a 64x16 output tile needs a (64+5)x(16+5) clamped
-// sample footprint; the 6-tap horizontal intermediates b1 are kept in LDS as int16 and
-// reused for both H and the centre sample J.
-constexpr int kHpTW = 64, kHpTH = 16;
+// LDS-tiled F/H/V/J plane builder, 128x16 output tile per 256-thread workgroup.
+//  1. the (16+5)-row clamped sample footprint is staged as whole dwords (aligned start
+//     4 samples left of the tile; interior tiles use dword loads, border tiles clamp);
+//  2. the horizontal 6-tap intermediates b1 for all 21 rows, 4 columns per item;
+//  3. each lane produces a 4-pixel x 2-row block of all four planes from 7 sample dwords
+//     and 7 b1 quads it shares between the two rows, and stores dwords (64 lanes = 2 rows
+//     x 128 contiguous bytes per plane).
+// The byte-per-lane version (64x16 tile) ran 19.6 us at 1080p (profiles/r01_final_check).
+constexpr int kHpTW = 128, kHpTH = 16;
+constexpr int kHpSW = kHpTW + 8;  // staged samples per row: padded x in [px0-4, px0+kHpTW+4)
+__device__ __forceinline__ int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xff); }
+// Low bytes of a..d -> one dword via v_perm_b32.  Written as `clip255(v) << 8*j` ORs, the
+// build produced 0xff in bytes 2-3 whenever sample 1 clamped from below to 0 (seen on the
+// MI355X in test_hpel_planes_match_reference; a codegen issue, most likely in the narrowed
+// clamp); v_perm reads only byte 0 of each operand, so stale high bits cannot leak.
+__device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)d, (uint32_t)c, 0x0c0c0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
 __global__ __launch_bounds__(256) void k_hpel(Geometry g, const FrameState* __restrict__ fs, uint8_t* __restrict__ pf,
                                               uint8_t* __restrict__ ph, uint8_t* __restrict__ pv,
                                               uint8_t* __restrict__ pj, int hp_pitch) {
-    __shared__ uint8_t smp[kHpTH + 5][kHpTW + 8];
-    __shared__ int16_t b1[kHpTH + 5][kHpTW];
+    __shared__ uint32_t smp[kHpTH + 5][kHpSW / 4];
+    __shared__ int4 b1[kHpTH + 5][kHpTW / 4];  // 4 columns per entry
     const uint8_t* __restrict__ ref = fs->ref_y;  // via the frame state: graph-replay safe
     const int px0 = blockIdx.x * kHpTW, py0 = blockIdx.y * kHpTH;  // padded-plane coordinates
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     const int tid = threadIdx.x;
-    // samples for rows py0-2 .. py0+kHpTH+2, cols px0-2 .. px0+kHpTW+2 (picture coords = padded - pad)
-    for (int i = tid; i < (kHpTH + 5) * (kHpTW + 5); i += 256) {
-        const int r = i / (kHpTW + 5), c = i - r * (kHpTW + 5);
-        smp[r][c] = (uint8_t)ref_px(ref, g.pitch, g.coded_w, g.coded_h, px0 + c - 2 - kHpelPad, py0 + r - 2 - kHpelPad);
+    // smp[r][k] = picture sample (px0 - 4 + k - pad, py0 - 2 + r - pad), clamped to the picture
+    const int xs = px0 - 4 - kHpelPad, ys = py0 - 2 - kHpelPad;
+    const bool interior = xs >= 0 && xs + kHpSW <= g.coded_w && ys >= 0 && ys + kHpTH + 5 <= g.coded_h &&
+                          (g.pitch & 3) == 0 && (reinterpret_cast<uintptr_t>(ref) & 3) == 0;
+    for (int i = tid; i < (kHpTH + 5) * (kHpSW / 4); i += 256) {
+        const int r = i / (kHpSW / 4), k4 = i - r * (kHpSW / 4);
+        uint32_t w;
+        if (interior) {
+            w = *reinterpret_cast<const uint32_t*>(ref + (size_t)(ys + r) * g.pitch + xs + 4 * k4);
+        } else {
+            w = 0;
+            for (int k = 0; k < 4; ++k)
+                w |= (uint32_t)ref_px(ref, g.pitch, g.coded_w, g.coded_h, xs + 4 * k4 + k, ys + r) << (8 * k);
+        }
+        smp[r][k4] = w;
     }
     __syncthreads();
-    for (int i = tid; i < (kHpTH + 5) * kHpTW; i += 256) {
-        const int r = i / kHpTW, c = i - r * kHpTW;
-        b1[r][c] = (int16_t)tap6(smp[r][c], smp[r][c + 1], smp[r][c + 2], smp[r][c + 3], smp[r][c + 4], smp[r][c + 5]);
+    // b1 at output column c uses samples k = c+2 .. c+7; a 4-column group c = 4q needs
+    // staged dwords q, q+1, q+2
+    for (int i = tid; i < (kHpTH + 5) * (kHpTW / 4); i += 256) {
+        const int r = i / (kHpTW / 4), q = i - r * (kHpTW / 4);
+        const uint32_t w0 = smp[r][q], w1 = smp[r][q + 1], w2 = smp[r][q + 2];
+        int s[12];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s[k] = byte_of(w0, k);
+            s[4 + k] = byte_of(w1, k);
+            s[8 + k] = byte_of(w2, k);
+        }
+        int t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = tap6(s[j + 2], s[j + 3], s[j + 4], s[j + 5], s[j + 6], s[j + 7]);
+        b1[r][q] = make_int4(t[0], t[1], t[2], t[3]);
     }
     __syncthreads();
-    for (int i = tid; i < kHpTH * kHpTW; i += 256) {
-        const int r = i / kHpTW, c = i - r * kHpTW;
-        const int x = px0 + c, y = py0 + r;
-        if (x >= W || y >= H) continue;
-        const int rr = r + 2, cc = c + 2;
+    const int q = tid & (kHpTW / 4 - 1), r0 = (tid / (kHpTW / 4)) * 2;  // 32 groups x 8 row pairs
+    const int x = px0 + 4 * q;
+    if (x >= W) return;  // W % 4 == 0: a group is wholly inside or outside
+    // output row r reads staged rows r .. r+5 (centre r+2); the pair shares rows r0+1 .. r0+5
+    int sv[7][4], bv[7][4];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const uint32_t w = smp[r0 + k][q + 1];  // samples k = 4q+4 .. 4q+7 = output columns 4q .. 4q+3
+        const int4 bb = b1[r0 + k][q];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sv[k][j] = byte_of(w, j);
+        bv[k][0] = bb.x;
+        bv[k][1] = bb.y;
+        bv[k][2] = bb.z;
+        bv[k][3] = bb.w;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int y = py0 + r0 + rr;
+        if (y >= H) break;
+        int Hs[4], Vs[4], Js[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            Hs[j] = clip255((bv[rr + 2][j] + 16) >> 5);  // centre row of this output row: rr + 2
+            const int v1 = tap6(sv[rr][j], sv[rr + 1][j], sv[rr + 2][j], sv[rr + 3][j], sv[rr + 4][j], sv[rr + 5][j]);
+            Vs[j] = clip255((v1 + 16) >> 5);
+            const int j1 = tap6(bv[rr][j], bv[rr + 1][j], bv[rr + 2][j], bv[rr + 3][j], bv[rr + 4][j], bv[rr + 5][j]);
+            Js[j] = clip255((j1 + 512) >> 10);
+        }
         const size_t o = (size_t)y * hp_pitch + x;
-        pf[o] = smp[rr][cc];
-        ph[o] = (uint8_t)clip255((b1[rr][c] + 16) >> 5);
-        const int v1 = tap6(smp[rr - 2][cc], smp[rr - 1][cc], smp[rr][cc], smp[rr + 1][cc], smp[rr + 2][cc], smp[rr + 3][cc]);
-        pv[o] = (uint8_t)clip255((v1 + 16) >> 5);
-        const int j1 = tap6(b1[rr - 2][c], b1[rr - 1][c], b1[rr][c], b1[rr + 1][c], b1[rr + 2][c], b1[rr + 3][c]);
-        pj[o] = (uint8_t)clip255((j1 + 512) >> 10);
+        *reinterpret_cast<uint32_t*>(pf + o) = smp[r0 + rr + 2][q + 1];
+        *reinterpret_cast<uint32_t*>(ph + o) = pack4(Hs[0], Hs[1], Hs[2], Hs[3]);
+        *reinterpret_cast<uint32_t*>(pv + o) = pack4(Vs[0], Vs[1], Vs[2], Vs[3]);
+        *reinterpret_cast<uint32_t*>(pj + o) = pack4(Js[0], Js[1], Js[2], Js[3]);
     }
 }
 
@@ -698,15 +760,21 @@ __device__ __forceinline__ uint32_t role_get(const uint32_t* buf, uint32_t b, in
     return (uint32_t)((hi << sh) >> (64 - n));
 }
 
+// Two macroblocks per wave (one per 32-lane half): the 28 roles of an MB fill a half, so a
+// wave no longer idles 36 of its 64 lanes; the prefix sum, ballots and word assembly are
+// segmented per half.
+constexpr int kCavlcMbPerBlock = 8;
 __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __restrict__ fs, MbInfo* __restrict__ mbs,
                                                const int16_t* __restrict__ coef, uint32_t* __restrict__ slot,
                                                uint32_t* __restrict__ slot_bits) {
-    __shared__ uint32_t rbuf[4][kNumRoles][kRoleWords];
-    __shared__ uint32_t roff[4][kNumRoles + 1];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    static_assert(kNumRoles < 32, "the roles of one MB (plus the total slot) must fit a half-wave");
+    __shared__ uint32_t rbuf[kCavlcMbPerBlock][kNumRoles][kRoleWords];
+    __shared__ uint32_t roff[kCavlcMbPerBlock][kNumRoles + 1];
+    const int hw = (threadIdx.x >> 5) & 1, lane = threadIdx.x & 31;  // hw: half of the wave; lane = role
+    const int wave = threadIdx.x >> 5;                                   // MB slot in the block (half-wave)
     const int nmb = g.mb_w * g.mb_h;
-    const int mbi = blockIdx.x * 4 + wave;
-    if (mbi >= nmb) return;  // whole wave exits together; no workgroup barrier below
+    const int mbi = blockIdx.x * kCavlcMbPerBlock + wave;
+    if (mbi >= nmb) return;  // a whole half exits; only half-local shuffles below, no workgroup barrier
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
     const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
     const MbInfo& m = mbs[mbi];  // by reference: a private copy with dynamically indexed nz arrays spills to scratch
@@ -716,17 +784,19 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     int mvdx = 0, mvdy = 0;
     const bool skip = decide_skip(g, mbs, mbi, av, &mvdx, &mvdy);
     // mb_qp_delta: QP predictor = QP of the previous MB in the slice that carried one (a P
-    // macroblock with residual); skipped / residual-free MBs inherit it.  Wave-parallel
-    // backward search, 64 MBs per step.  I slices: every MB is at the slice QP.
+    // macroblock with residual); skipped / residual-free MBs inherit it.  Half-wave-parallel
+    // backward search, 32 MBs per step (the ballot holds active lanes only; this half's bits
+    // are taken).  I slices: every MB is at the slice QP.
     int dqp = 0;
     if (!skip && !fs->idr && m.cbp != 0) {
         const int per_slice = fs->slice_rows * g.mb_w, first = (mbi / per_slice) * per_slice;
         int pred = fs->qp;
-        for (int j0 = mbi - 1; j0 >= first; j0 -= 64) {
+        for (int j0 = mbi - 1; j0 >= first; j0 -= 32) {
             const int j = j0 - lane;
             const unsigned long long bal = __ballot(j >= first && mbs[j].cbp != 0);
-            if (bal) {
-                pred = mbs[j0 - (__ffsll((long long)bal) - 1)].qp;
+            const uint32_t hb = (uint32_t)(bal >> (32 * hw));
+            if (hb) {
+                pred = mbs[j0 - (__ffs(hb) - 1)].qp;
                 break;
             }
         }
@@ -740,13 +810,13 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
         w.flush();
         bits = w.bits;
     }
-    // exclusive prefix sum of bits over lanes -> role offsets in the MB slot
+    // exclusive prefix sum of bits over the half's lanes -> role offsets in the MB slot
     uint32_t incl = bits;
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t v = __shfl_up(incl, o, 64);
+    for (int o = 1; o < 32; o <<= 1) {
+        uint32_t v = __shfl_up(incl, o, 32);
         if (lane >= o) incl += v;
     }
-    const uint32_t total = __shfl(incl, 63, 64);
+    const uint32_t total = __shfl(incl, 31, 32);
     if (lane < kNumRoles) roff[wave][lane] = incl - bits;
     if (lane == kNumRoles) roff[wave][kNumRoles] = total;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -756,7 +826,7 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     if (!skip && fits) {
         const uint32_t nwords = (total + 31) >> 5;
         uint32_t* dst = slot + (size_t)mbi * kSlotWords;
-        for (uint32_t wi = lane; wi < nwords; wi += 64) {
+        for (uint32_t wi = lane; wi < nwords; wi += 32) {
             const uint32_t W0 = wi * 32;
             // first role ending after W0 (roles are contiguous and in lane order)
             int r = 0;
@@ -1139,7 +1209,8 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
 
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream) {
     const int nmb = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, b.mb, b.coef, b.slot,
+    hipLaunchKernelGGL(k_cavlc, dim3((nmb + kCavlcMbPerBlock - 1) / kCavlcMbPerBlock), dim3(256), 0, stream, g, b.fs,
+                       b.mb, b.coef, b.slot,
                        b.slot_bits);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.unit_off, b.skip_run,
                        b.coded_list, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr);

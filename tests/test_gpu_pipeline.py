@@ -278,7 +278,7 @@ def _hpel_reference(ref, pad=48):
     return [p.astype(np.uint8) for p in (F, Hh, V, J)]
 
 
-@pytest.mark.parametrize("w,h", [(64, 48), (160, 96), (112, 64)])
+@pytest.mark.parametrize("w,h", [(64, 48), (160, 96), (112, 64), (416, 240)])  # 416x240: interior tiles
 def test_hpel_planes_match_reference(gpu, w, h):
     rng = np.random.default_rng(w + h)
     ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
