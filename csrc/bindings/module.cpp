@@ -428,6 +428,10 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("use_graph", &SessionConfig::use_graph)
         .def_readwrite("fake_clock", &SessionConfig::fake_clock)
         .def_readwrite("codec", &SessionConfig::codec)
+        .def_readwrite("mask_x0", &SessionConfig::mask_x0)
+        .def_readwrite("mask_y0", &SessionConfig::mask_y0)
+        .def_readwrite("mask_x1", &SessionConfig::mask_x1)
+        .def_readwrite("mask_y1", &SessionConfig::mask_y1)
         .def_readwrite("enc", &SessionConfig::enc);
 
     py::class_<FrameResult>(m, "FrameResult")
@@ -440,6 +444,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("psnr_y", &FrameResult::psnr_y)
         .def_readonly("psnr_u", &FrameResult::psnr_u)
         .def_readonly("psnr_v", &FrameResult::psnr_v)
+        .def_readonly("psnr_y_masked", &FrameResult::psnr_y_masked)
         .def_property_readonly("au", [](const FrameResult& r) { return to_bytes(r.au); });
 
     py::class_<Session>(m, "Session")

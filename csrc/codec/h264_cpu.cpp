@@ -124,7 +124,7 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
     const uint8_t* ref_uv = rec_uv_[cur_ ^ 1].data();
     uint8_t* rec_y = rec_y_[cur_].data();
     uint8_t* rec_uv = rec_uv_[cur_].data();
-    const int frame_qp = common_.cur_qp();
+    const int frame_qp = frame_qp_();
     for (int mby = 0; mby < g.mb_h; ++mby)
         for (int mbx = 0; mbx < g.mb_w; ++mbx) {
             const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
@@ -214,7 +214,7 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
     const Geometry g = geom_of(common_, cw_, ch_);
     uint8_t* rec_y = rec_y_[cur_].data();
     uint8_t* rec_uv = rec_uv_[cur_].data();
-    const int qp = common_.cur_qp();
+    const int qp = frame_qp_();
     const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
     for (int mby = 0; mby < g.mb_h; ++mby) {
         uint8_t left[32] = {0};
@@ -362,9 +362,9 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         BitWriter w;
         w.init(words.data());
         write_slice_header(w, make_slice_params(first, idr, common_.cur_frame_num(), common_.log2_max_frame_num(),
-                                                common_.cur_idr_pic_id(), common_.cur_qp() - common_.pic_init_qp(), 1));
+                                                common_.cur_idr_pic_id(), frame_qp_() - common_.pic_init_qp(), 1));
         int run = 0;
-        int qp_pred = common_.cur_qp();  // mb_qp_delta predictor: QP of the last MB that carried one
+        int qp_pred = frame_qp_();  // mb_qp_delta predictor: QP of the last MB that carried one
         for (int mbi = first; mbi < last; ++mbi) {
             const Avail av = mb_avail(g, mbi % g.mb_w, mbi / g.mb_w, slice_rows);
             int mvdx, mvdy;
@@ -398,6 +398,15 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
 }
 
 const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
+    while (common_.wants_probe()) {  // size the first IDR (rate control), as the GPU encoder does
+        qp_override_ = common_.probe_qp();
+        encode_intra(y, uv, pitch);
+        std::vector<uint8_t> payload;
+        std::vector<uint32_t> soff, slen;
+        entropy(payload, soff, slen);
+        common_.add_probe(qp_override_, (int)(payload.size() + soff.size() * 6 + 32));
+        qp_override_ = -1;
+    }
     common_.begin_frame(force_idr || !have_ref_);
     cur_ ^= 1;
     if (common_.cur_idr())

@@ -21,7 +21,34 @@ EncoderCommon::EncoderCommon(const EncoderConfig& c) : cfg_(c) {
     mb_w_ = (c.width + 15) / 16;
     mb_h_ = (c.height + 15) / 16;
     cur_qp_ = std::clamp(c.qp, 0, 51);
-    rc_qp_ = cur_qp_;
+}
+
+double EncoderCommon::frame_budget_bits() const {
+    return cfg_.bitrate_kbps * 1000.0 / std::max(1, cfg_.fps);
+}
+
+int EncoderCommon::qp_for(double x, double bits) const {
+    // bits = x / qstep(qp)  =>  qp = 6 * log2(x / (0.625 * bits))
+    const double q = 6.0 * std::log2(std::max(1e-9, x) / (0.625 * std::max(1.0, bits)));
+    return (int)std::lround(std::clamp(q, 0.0, 51.0));
+}
+
+int EncoderCommon::probe_qp() const {
+    if (probes_ == 0) {
+        // prior: ~1 bit per luma sample at QP 30 for desktop content, scaled to the IDR budget
+        const double px = (double)cfg_.width * cfg_.height;
+        return std::clamp(qp_for(px * qstep(30), kIdrBudget * frame_budget_bits()), cfg_.qp_min, cfg_.qp_max);
+    }
+    return std::clamp(qp_for(x_i_, kIdrBudget * frame_budget_bits()), cfg_.qp_min, cfg_.qp_max);
+}
+
+void EncoderCommon::add_probe(int qp, int bytes) {
+    probe_q_[probes_ < kMaxProbes ? probes_ : kMaxProbes - 1] = qp;
+    ++probes_;
+    x_i_ = std::max(8.0, bytes * 8.0) * qstep(qp);
+    // a second probe only if the first one was far from the budget
+    const int next = probe_qp();
+    if (probes_ >= kMaxProbes || std::abs(next - qp) <= 2) probe_done_ = true;
 }
 
 void EncoderCommon::begin_frame(bool force_idr) {
@@ -31,6 +58,7 @@ void EncoderCommon::begin_frame(bool force_idr) {
     cur_idr_ = idr;
     idr_requested_ = false;
     ++begun_;
+    probe_done_ = true;  // probing only ever precedes the first frame
     if (idr) {
         frame_num_ = 0;
         idr_pic_id_ = (idr_pic_id_ + 1) & 0xffff;
@@ -39,23 +67,61 @@ void EncoderCommon::begin_frame(bool force_idr) {
         frame_num_ = (frame_num_ + 1) % (1 << log2_max_frame_num());
         ++since_idr_;
     }
-    int q = (int)std::lround(rc_qp_);
-    if (cfg_.bitrate_kbps > 0) q = std::clamp(q, cfg_.qp_min, cfg_.qp_max);
-    cur_qp_ = std::clamp(q, 0, 51);
+    if (cfg_.bitrate_kbps <= 0) {
+        cur_qp_ = std::clamp(cfg_.qp, 0, 51);
+        return;
+    }
+    const double T = frame_budget_bits();
+    // buffer state including the frames still in flight, charged at their budgets
+    double vbv = vbv_;
+    for (const Pending& p : pending_) vbv += p.budget - T;
+    double budget;
+    int q;
+    if (idr) {
+        budget = kIdrBudget * T;
+        const double x = x_i_ > 0 ? x_i_ : (double)cfg_.width * cfg_.height * qstep(30);
+        q = qp_for(x, budget);
+    } else {
+        // linear drain of the buffer excess over the recovery window that follows an IDR
+        // (the whole excess is paid back kDrainFrames after it), then a gentle correction
+        const int64_t k = since_idr_ - 1;  // P frames since the IDR, this one included
+        const double div = k <= kDrainFrames ? (double)(kDrainFrames - k + 1) : 3.0;
+        budget = std::clamp(T - vbv / div, 0.25 * T, 2.0 * T);
+        if (x_p_ > 0) {
+            q = qp_for(x_p_, budget);
+            if (last_p_qp_ >= 0) q = std::clamp(q, last_p_qp_ - 6, last_p_qp_ + 6);
+        } else if (x_i_ > 0) {
+            // no P picture finished yet: assume a P picture costs half an I picture at equal QP
+            // (pessimistic for desktops -- undershooting for a frame or two is cheaper than a
+            // latency spike; the model has real P data two frames later)
+            q = qp_for(0.5 * x_i_, budget);
+        } else {
+            q = (last_i_qp_ >= 0 ? last_i_qp_ : cfg_.qp) + 2;
+        }
+    }
+    cur_qp_ = std::clamp(std::clamp(q, cfg_.qp_min, cfg_.qp_max), 0, 51);
+    pending_.push_back(Pending{budget, cur_qp_, idr});
+    if (idr)
+        last_i_qp_ = cur_qp_;
+    else
+        last_p_qp_ = cur_qp_;
 }
 
 void EncoderCommon::end_frame(int bytes, bool idr) {
     ++frame_index_;
+    if (pending_.empty()) return;  // constant QP (nothing tracked)
+    const Pending p = pending_.front();
+    pending_.pop_front();
     if (cfg_.bitrate_kbps <= 0) return;
-    const double target = cfg_.bitrate_kbps * 1000.0 / std::max(1, cfg_.fps);
+    const double T = frame_budget_bits();
     const double bits = bytes * 8.0;
-    vbv_fill_ = std::max(0.0, vbv_fill_ + bits - target);
-    // cap the virtual buffer at ~0.5 s so a burst cannot pin the QP forever
-    vbv_fill_ = std::min(vbv_fill_, target * std::max(1, cfg_.fps) * 0.5);
-    if (idr) return;  // I frames are expected to be large; steer on P frames
-    const double ratio = (bits + 0.25 * vbv_fill_ + 1.0) / target;
-    const double step = std::clamp(6.0 * std::log2(ratio) * 0.25, -1.0, 1.5);
-    rc_qp_ = std::clamp(rc_qp_ + step, (double)cfg_.qp_min, (double)cfg_.qp_max);
+    vbv_ = std::max(-2.0 * T, vbv_ + bits - T);
+    const double x = std::max(8.0, bits) * qstep(p.qp);
+    if (idr || p.idr) {
+        x_i_ = x;
+    } else {
+        x_p_ = x_p_ > 0 ? 0.3 * x_p_ + 0.7 * x : x;
+    }
 }
 
 static void words_to_bytes(const uint32_t* w, uint32_t bits, std::vector<uint8_t>& out) {
@@ -255,29 +321,16 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     HIP_CHECK(hipGetLastError());
 }
 
-bool GpuH264Encoder::prepare(bool force_idr) {
-    if ((int)inflight_.size() >= depth_)
-        throw std::logic_error("GpuH264Encoder: collect() a frame first (pipeline full)");
-    const int s = (depth_ == 1) ? 0 : next_slot_;
-    next_slot_ = (next_slot_ + 1) % depth_;
-    prep_slot_ = s;
-    FrameSlot& sl = slots_[s];
-    common_.begin_frame(force_idr || !have_ref_);
-    have_ref_ = true;  // this frame becomes the reference of the next one
-    const bool idr = common_.cur_idr();
-    sl.idr = idr;
-    sl.qp = common_.cur_qp();
-    const int ref = cur_;
-    cur_ ^= 1;
+void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur) {
     FrameState& f = *sl.fs_host;
     f.ref_y = rec_y_[ref];
     f.ref_uv = rec_uv_[ref];
-    f.rec_y = rec_y_[cur_];
-    f.rec_uv = rec_uv_[cur_];
+    f.rec_y = rec_y_[cur];
+    f.rec_uv = rec_uv_[cur];
     f.idr = idr ? 1 : 0;
     f.frame_num = common_.cur_frame_num();
     f.idr_pic_id = common_.cur_idr_pic_id();
-    f.qp = common_.cur_qp();
+    f.qp = qp;
     f.slice_rows = idr ? 1 : geom_.mb_h;
     f.num_slices = idr ? geom_.mb_h : 1;
     f.search_range = me_range(cfg_.search_range);
@@ -294,6 +347,41 @@ bool GpuH264Encoder::prepare(bool force_idr) {
     f.hp_v = hp_[2] + org;
     f.hp_j = hp_[3] + org;
     f.sse_part = sl.buf.sse_part;
+}
+
+int GpuH264Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp) {
+    // synchronous IDR encode of the first picture at `qp` (rate-control probe); touches no
+    // stream state: the real first frame overwrites the reconstruction
+    if (!inflight_.empty()) throw std::logic_error("GpuH264Encoder: probe with frames in flight");
+    prep_slot_ = 0;
+    FrameSlot& sl = slots_[0];
+    fill_state(sl, true, qp, cur_ ^ 1, cur_);
+    sl.fs_host->frame_num = 0;
+    sl.fs_host->idr_pic_id = 0;
+    HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
+    enqueue_kernels(true, src_y, src_uv);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
+    const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);
+    // + start code, NAL header and a rough emulation-prevention allowance per slice
+    return hdr.overflow ? (int)sl.buf.out_bytes : (int)(hdr.total_bytes + hdr.num_slices * 6 + 32);
+}
+
+bool GpuH264Encoder::prepare(bool force_idr) {
+    if ((int)inflight_.size() >= depth_)
+        throw std::logic_error("GpuH264Encoder: collect() a frame first (pipeline full)");
+    const int s = (depth_ == 1) ? 0 : next_slot_;
+    next_slot_ = (next_slot_ + 1) % depth_;
+    prep_slot_ = s;
+    FrameSlot& sl = slots_[s];
+    common_.begin_frame(force_idr || !have_ref_);
+    have_ref_ = true;  // this frame becomes the reference of the next one
+    const bool idr = common_.cur_idr();
+    sl.idr = idr;
+    sl.qp = common_.cur_qp();
+    const int ref = cur_;
+    cur_ ^= 1;
+    fill_state(sl, idr, sl.qp, ref, cur_);
     return idr;
 }
 
@@ -314,6 +402,10 @@ void GpuH264Encoder::record_done() {
 }
 
 void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
+    while (common_.wants_probe()) {
+        const int q = common_.probe_qp();
+        common_.add_probe(q, probe_bytes(src_y, src_uv, q));
+    }
     const bool idr = prepare(force_idr);
     record_start();
     enqueue_body(idr, src_y, src_uv);

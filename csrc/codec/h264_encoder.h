@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
 #include <deque>
 #include <string>
 #include <vector>
@@ -50,6 +51,17 @@ struct FrameStats {
 };
 
 // Annex-B / rate-control logic shared by both encoders.
+//
+// Rate control (CBR, bitrate_kbps > 0) is a per-frame bit-budget controller with a virtual
+// buffer (VBV) model, replacing the reference's NVENC low-latency CBR (`nvh264enc`,
+// reference Dockerfile:210):
+//  * rate model per picture type t in {I, P}: bits = X_t / qstep(QP), qstep = 0.625*2^(QP/6);
+//    X_t is re-estimated from every finished frame (P: exponential average, I: latest IDR);
+//  * the very first IDR is sized by a synchronous probe encode (wants_probe()/add_probe()),
+//    so the stream starts on budget instead of converging for a second;
+//  * every IDR gets its own budget (idr_budget x the per-frame budget) and IS charged to the
+//    buffer; the excess is drained over the next kDrainFrames P frames (bounded recovery);
+//  * frames in flight (pipelined encode) are charged at their budget until they finish.
 class EncoderCommon {
    public:
     explicit EncoderCommon(const EncoderConfig& c);
@@ -74,7 +86,20 @@ class EncoderCommon {
     void set_bitrate(int kbps) { cfg_.bitrate_kbps = kbps; }
     int64_t frames() const { return frame_index_; }
 
+    // ---- rate-control internals (exposed for the encoders and tests)
+    static double qstep(double qp) { return 0.625 * std::exp2(qp / 6.0); }
+    double frame_budget_bits() const;  // bitrate / fps
+    // True while the first IDR of a CBR stream still wants a probe encode.
+    bool wants_probe() const { return cfg_.bitrate_kbps > 0 && begun_ == 0 && probes_ < kMaxProbes && !probe_done_; }
+    int probe_qp() const;                 // QP to probe next
+    void add_probe(int qp, int bytes);    // result of a probe encode of the first picture
+    double vbv_excess_bits() const { return vbv_; }
+    static constexpr int kDrainFrames = 6;
+    static constexpr double kIdrBudget = 3.0;  // IDR budget in frames
+    static constexpr int kMaxProbes = 2;
+
    private:
+    int qp_for(double x, double bits) const;
     EncoderConfig cfg_;
     int mb_w_, mb_h_;
     bool cur_idr_ = true;
@@ -85,8 +110,19 @@ class EncoderCommon {
     int64_t frame_index_ = 0;  // frames ended
     int64_t begun_ = 0;        // frames begun
     int64_t since_idr_ = 0;    // frames begun since (and including) the last IDR
-    double rc_qp_;        // continuous QP state
-    double vbv_fill_ = 0;  // bits above the target rate accumulated so far
+    // rate model / buffer
+    double x_i_ = 0, x_p_ = 0;  // complexity (bits * qstep) of I / P pictures; 0 = unknown
+    int last_i_qp_ = -1, last_p_qp_ = -1;
+    double vbv_ = 0;  // bits sent above the CBR line so far (>= -1 frame budget)
+    struct Pending {
+        double budget;
+        int qp;
+        bool idr;
+    };
+    std::deque<Pending> pending_;  // begun, not yet ended (pipelined frames)
+    int probes_ = 0;
+    bool probe_done_ = false;
+    int probe_q_[kMaxProbes] = {0, 0};
 };
 
 void emulation_prevent(std::vector<uint8_t>& out, const uint8_t* rbsp, size_t n);
@@ -146,6 +182,8 @@ class GpuH264Encoder final : public VideoEncoder {
     };
     void alloc_slot(FrameSlot& sl);
     void free_slot(FrameSlot& sl);
+    void fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur);
+    int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
 
     EncoderConfig cfg_;
     EncoderCommon common_;
@@ -183,6 +221,8 @@ class CpuH264Encoder {
     void encode_intra(const uint8_t* y, const uint8_t* uv, int pitch);
     void encode_inter(const uint8_t* y, const uint8_t* uv, int pitch);
     void entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& slice_off, std::vector<uint32_t>& slice_len);
+    int frame_qp_() const { return qp_override_ >= 0 ? qp_override_ : common_.cur_qp(); }
+    int qp_override_ = -1;  // rate-control probe of the first picture
 
     EncoderConfig cfg_;
     EncoderCommon common_;

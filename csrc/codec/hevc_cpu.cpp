@@ -311,7 +311,7 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
     uint8_t* ry = rec_y_[cur_].data();
     uint8_t* ruv = rec_uv_[cur_].data();
     const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
-    const int qp = common_.rc().cur_qp();
+    const int qp = frame_qp_();
     const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
     const int lambda = h264::lambda_sad(qp);
     for (int y = 0; y < H; ++y)
@@ -385,7 +385,7 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
     uint8_t* ry = rec_y_[cur_].data();
     uint8_t* ruv = rec_uv_[cur_].data();
     const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
-    const int fqp = common_.rc().cur_qp();
+    const int fqp = frame_qp_();
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             const int i = y * W + x;
@@ -479,6 +479,23 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
 
 const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
     h264::EncoderCommon& rc = common_.rc();
+    while (rc.wants_probe()) {  // size the first IDR (rate control), as the GPU encoder does
+        qp_override_ = rc.probe_qp();
+        analyse_intra(y, uv, pitch);
+        const std::vector<int> rows = common_.row_slices();
+        const int W = common_.ctb_w(), H = common_.ctb_h();
+        std::vector<uint8_t> buf;
+        uint8_t ctx[C_NUM];
+        size_t total = 0;
+        for (size_t s = 0; s < rows.size(); ++s) {
+            const int first = rows[s], count = (s + 1 < rows.size() ? rows[s + 1] : W * H) - first;
+            const uint32_t cap = (uint32_t)count * 1024 + 1024;
+            buf.resize(cap);
+            total += code_slice(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(), first, count, W, ctx) + 12;
+        }
+        rc.add_probe(qp_override_, (int)total + 64);
+        qp_override_ = -1;
+    }
     rc.begin_frame(force_idr || !have_ref_);
     const bool idr = rc.cur_idr();
     const int qp = rc.cur_qp();

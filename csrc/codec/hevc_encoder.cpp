@@ -104,6 +104,53 @@ GpuHevcEncoder::~GpuHevcEncoder() {
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
 }
 
+void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur) {
+    const size_t org = (size_t)h264::kHpelPad * hp_pitch_ + h264::kHpelPad;
+    HevcFrameState& f = *sl.fs_host;
+    f.ref_y = rec_y_[ref];
+    f.ref_uv = rec_uv_[ref];
+    f.rec_y = rec_y_[cur];
+    f.rec_uv = rec_uv_[cur];
+    f.hp_f = hp_[0] + org;
+    f.hp_pitch = hp_pitch_;
+    f.idr = idr ? 1 : 0;
+    f.qp = qp;
+    f.slice_rows = common_.slice_rows();
+    f.num_slices = common_.num_slices();
+    f.aq = cfg_.aq;
+    f.tu_split = cfg_.tu_split ? 1 : 0;
+    f.chroma_qp_offset = cfg_.chroma_qp_offset;
+    // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
+    f.n_sse_parts = (idr || cfg_.deblock) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
+    f.sse_part = sl.buf.sse_part;
+    h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
+    m.ref_y = rec_y_[ref];
+    m.ref_uv = rec_uv_[ref];
+    m.qp = qp;
+    m.search_range = h264::me_range(cfg_.search_range);
+    m.subpel = cfg_.subpel;
+    m.hp_pitch = hp_pitch_;
+    m.hp_f = hp_[0] + org;
+    m.hp_h = hp_[1] + org;
+    m.hp_v = hp_[2] + org;
+    m.hp_j = hp_[3] + org;
+    m.sse_part = sl.buf.sse_part;
+}
+
+int GpuHevcEncoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp) {
+    // synchronous IDR encode of the first picture at `qp` (rate-control probe, see
+    // h264::EncoderCommon); the real first frame overwrites the reconstruction
+    if (!inflight_.empty()) throw std::logic_error("GpuHevcEncoder: probe with frames in flight");
+    prep_slot_ = 0;
+    FrameSlot& sl = slots_[0];
+    fill_state(sl, true, qp, cur_ ^ 1, cur_);
+    enqueue_body(true, src_y, src_uv);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
+    const HevcOutHeader hdr = *reinterpret_cast<const HevcOutHeader*>(sl.host_out);
+    return hdr.overflow ? (int)sl.buf.out_bytes : (int)(hdr.total_bytes + hdr.num_slices * 12 + 64);
+}
+
 bool GpuHevcEncoder::prepare(bool force_idr) {
     if ((int)inflight_.size() >= depth_) throw std::logic_error("GpuHevcEncoder: collect() a frame first (pipeline full)");
     const int s = (depth_ == 1) ? 0 : next_slot_;
@@ -119,36 +166,7 @@ bool GpuHevcEncoder::prepare(bool force_idr) {
     sl.poc = idr ? 0 : common_.poc();
     const int ref = cur_;
     cur_ ^= 1;
-    const size_t org = (size_t)h264::kHpelPad * hp_pitch_ + h264::kHpelPad;
-    HevcFrameState& f = *sl.fs_host;
-    f.ref_y = rec_y_[ref];
-    f.ref_uv = rec_uv_[ref];
-    f.rec_y = rec_y_[cur_];
-    f.rec_uv = rec_uv_[cur_];
-    f.hp_f = hp_[0] + org;
-    f.hp_pitch = hp_pitch_;
-    f.idr = idr ? 1 : 0;
-    f.qp = sl.qp;
-    f.slice_rows = common_.slice_rows();
-    f.num_slices = common_.num_slices();
-    f.aq = cfg_.aq;
-    f.tu_split = cfg_.tu_split ? 1 : 0;
-    f.chroma_qp_offset = cfg_.chroma_qp_offset;
-    // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
-    f.n_sse_parts = (idr || cfg_.deblock) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
-    f.sse_part = sl.buf.sse_part;
-    h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
-    m.ref_y = rec_y_[ref];
-    m.ref_uv = rec_uv_[ref];
-    m.qp = sl.qp;
-    m.search_range = h264::me_range(cfg_.search_range);
-    m.subpel = cfg_.subpel;
-    m.hp_pitch = hp_pitch_;
-    m.hp_f = hp_[0] + org;
-    m.hp_h = hp_[1] + org;
-    m.hp_v = hp_[2] + org;
-    m.hp_j = hp_[3] + org;
-    m.sse_part = sl.buf.sse_part;
+    fill_state(sl, idr, sl.qp, ref, cur_);
     return idr;
 }
 
@@ -183,6 +201,11 @@ void GpuHevcEncoder::record_done() {
 }
 
 void GpuHevcEncoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
+    h264::EncoderCommon& rc = common_.rc();
+    while (rc.wants_probe()) {
+        const int q = rc.probe_qp();
+        rc.add_probe(q, probe_bytes(src_y, src_uv, q));
+    }
     const bool idr = prepare(force_idr);
     record_start();
     enqueue_body(idr, src_y, src_uv);

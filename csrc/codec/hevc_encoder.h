@@ -75,6 +75,8 @@ class CpuHevcEncoder {
    private:
     void analyse_intra(const uint8_t* y, const uint8_t* uv, int pitch);
     void analyse_inter(const uint8_t* y, const uint8_t* uv, int pitch);
+    int frame_qp_() { return qp_override_ >= 0 ? qp_override_ : common_.rc().cur_qp(); }
+    int qp_override_ = -1;  // rate-control probe of the first picture
 
     EncoderConfig cfg_;
     HevcCommon common_;
@@ -196,6 +198,8 @@ class GpuHevcEncoder final : public VideoEncoder {
     };
     void alloc_slot(FrameSlot& sl);
     void free_slot(FrameSlot& sl);
+    void fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur);
+    int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
 
     EncoderConfig cfg_;
     HevcCommon common_;

@@ -46,6 +46,11 @@ struct LanczosTables {
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
                           uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream);
 
+// Luma squared error between two planes over [0,w) x [0,h) excluding the rectangle
+// [mx0,mx1) x [my0,my1), atomically added to *acc (quality report with a panel masked out).
+void launch_sse_masked(const uint8_t* a, const uint8_t* b, int pitch, int w, int h, int mx0, int my0, int mx1,
+                       int my1, unsigned long long* acc, hipStream_t stream);
+
 // Copy a BGRx tile into a larger BGRx frame at (dx, dy) (tiled-wall composite).
 void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,
                       hipStream_t stream);

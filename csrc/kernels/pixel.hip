@@ -367,7 +367,43 @@ __global__ __launch_bounds__(256) void k_composite(const uint8_t* __restrict__ t
     }
 }
 
+// One 256-thread workgroup per 8 rows; every thread owns 4-pixel dword columns (16-byte
+// loads where aligned), one atomic per workgroup.
+__global__ __launch_bounds__(256) void k_sse_masked(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                    int pitch, int w, int h, int mx0, int my0, int mx1, int my1,
+                                                    unsigned long long* __restrict__ acc) {
+    const int y0 = blockIdx.x * 8;
+    unsigned long long s = 0;
+    const int ngroups = (w + 3) / 4;
+    for (int i = threadIdx.x; i < 8 * ngroups; i += 256) {
+        const int r = i / ngroups, x = (i - r * ngroups) * 4, y = y0 + r;
+        if (y >= h) break;
+        const uint32_t va = *reinterpret_cast<const uint32_t*>(a + (size_t)y * pitch + x);
+        const uint32_t vb = *reinterpret_cast<const uint32_t*>(b + (size_t)y * pitch + x);
+        const bool in_y = y >= my0 && y < my1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int xx = x + k;
+            const int d = (int)((va >> (8 * k)) & 0xff) - (int)((vb >> (8 * k)) & 0xff);
+            const bool masked = in_y && xx >= mx0 && xx < mx1;
+            s += (xx < w && !masked) ? (unsigned)(d * d) : 0u;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ unsigned long long part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(acc, part[0] + part[1] + part[2] + part[3]);
+}
+
 }  // namespace
+
+void launch_sse_masked(const uint8_t* a, const uint8_t* b, int pitch, int w, int h, int mx0, int my0, int mx1,
+                       int my1, unsigned long long* acc, hipStream_t stream) {
+    if ((pitch & 3) != 0) throw std::invalid_argument("sse_masked: pitch must be a multiple of 4");
+    hipLaunchKernelGGL(k_sse_masked, dim3((h + 7) / 8), dim3(256), 0, stream, a, b, pitch, w, h, mx0, my0, mx1, my1,
+                       acc);
+}
 
 void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream) {
     dim3 block(64, 4);

@@ -116,6 +116,11 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         HIP_CHECK(hipMemcpy(p, wy.data(), wy.size() * 4, hipMemcpyHostToDevice));
     }
     for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
+    if (masked()) {
+        HIP_CHECK(hipMalloc(&mask_dev_, 2 * sizeof(unsigned long long)));
+        HIP_CHECK(hipHostMalloc(&mask_host_, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_mask_[k], hipEventDisableTiming));
+    }
     HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams), hipHostMallocDefault));
     HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams)));
     graphs_.assign((size_t)cfg_.pool_slots * 2, nullptr);
@@ -136,6 +141,10 @@ Session::~Session() {
         if (staging_[k]) (void)hipHostFree(staging_[k]);
     if (lt_mem_) hipFree(lt_mem_);
     for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
+    if (mask_dev_) (void)hipFree(mask_dev_);
+    if (mask_host_) (void)hipHostFree(mask_host_);
+    for (int k = 0; k < 2; ++k)
+        if (ev_mask_[k]) (void)hipEventDestroy(ev_mask_[k]);
     hipStreamDestroy(stream_);
 }
 
@@ -155,6 +164,19 @@ void Session::convert_and_encode(int slot, bool force_idr) {
     TraceRange tr("mxdesk.convert+encode.enqueue");
     convert(slot);
     enc_->submit(nv12_y_, nv12_uv_, force_idr);
+    enqueue_mask_sse(inflight_.back().k);
+}
+
+void Session::enqueue_mask_sse(int k) {
+    // after the analysis kernels on stream_ (reconstruction final, source not yet overwritten
+    // by the next frame's conversion, which is later on the same stream)
+    if (!masked()) return;
+    const h264::EncoderConfig& e = enc_->rc().config();
+    HIP_CHECK(hipMemsetAsync(mask_dev_ + k, 0, sizeof(unsigned long long), stream_));
+    pix::launch_sse_masked(nv12_y_, enc_->recon_y(), enc_->pitch(), e.width, e.height, cfg_.mask_x0, cfg_.mask_y0,
+                           cfg_.mask_x1, cfg_.mask_y1, mask_dev_ + k, stream_);
+    HIP_CHECK(hipMemcpyAsync(mask_host_ + k, mask_dev_ + k, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipEventRecord(ev_mask_[k], stream_));
 }
 
 int Session::begin_frame() {
@@ -214,7 +236,8 @@ void Session::submit_synthetic(bool force_idr) {
     const int slot = pool_->acquire();
     const pix::SynthParams p = synth_params();
     ++frame_id_;
-    if (!cfg_.use_graph) {
+    // the first CBR frame runs eagerly: its rate-control probe encodes synchronously
+    if (!cfg_.use_graph || enc_->rc().wants_probe()) {
         HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
         pix::launch_synth(pool_->data(slot), p, stream_);
         HIP_CHECK(hipGetLastError());
@@ -229,6 +252,7 @@ void Session::submit_synthetic(bool force_idr) {
     if (!exec) exec = capture_frame_graph(slot, idr);
     HIP_CHECK(hipGraphLaunch(exec, stream_));
     enc_->record_done();
+    enqueue_mask_sse(k);
 }
 
 void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
@@ -267,6 +291,12 @@ FrameResult Session::collect() {
     r.psnr_y = psnr(st.sse[0], ny);
     r.psnr_u = psnr(st.sse[1], nc);
     r.psnr_v = psnr(st.sse[2], nc);
+    if (masked()) {
+        HIP_CHECK(hipEventSynchronize(ev_mask_[fl.k]));
+        const double mw = std::max(0, std::min(cfg_.mask_x1, enc_->rc().config().width) - std::max(0, cfg_.mask_x0));
+        const double mh = std::max(0, std::min(cfg_.mask_y1, enc_->rc().config().height) - std::max(0, cfg_.mask_y0));
+        r.psnr_y_masked = psnr(mask_host_[fl.k], ny - mw * mh);
+    }
     return r;
 }
 

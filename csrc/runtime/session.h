@@ -59,6 +59,9 @@ struct SessionConfig {
                             // launches on ROCm 7.2 for this chain: profiles/r01_graph)
     int fake_clock = 0;     // barcode timestamp = frame_id * 1e6 / fps (deterministic streams for tests)
     std::string codec = "h264";  // "h264" (mxh264enc) or "hevc" / "h265" (mxh265enc)
+    // optional quality report: luma PSNR with a rectangle (encoded-picture coordinates) left
+    // out, e.g. the incompressible noise panel of the synthetic desktop; mask_x1 <= mask_x0 = off
+    int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;
     h264::EncoderConfig enc;  // width/height overwritten from out size
 };
 
@@ -70,6 +73,7 @@ struct FrameResult {
     int idr = 0;
     int qp = 0;
     double psnr_y = 0, psnr_u = 0, psnr_v = 0;  // encoder reconstruction vs source (dB, cap 99)
+    double psnr_y_masked = 0;                   // luma PSNR outside SessionConfig::mask_* (0 = off)
     std::vector<uint8_t> au;
 };
 
@@ -135,6 +139,12 @@ class Session {
     };
     std::deque<Inflight> inflight_;
     hipEvent_t ev_start_[2] = {nullptr, nullptr};
+    // masked-PSNR accumulators (device) + their host copies, one per frame in flight
+    unsigned long long* mask_dev_ = nullptr;
+    unsigned long long* mask_host_ = nullptr;
+    hipEvent_t ev_mask_[2] = {nullptr, nullptr};
+    bool masked() const { return cfg_.mask_x1 > cfg_.mask_x0 && cfg_.mask_y1 > cfg_.mask_y0; }
+    void enqueue_mask_sse(int k);
     int next_k_ = 0;
     int depth_ = 1;
     // hipGraph replay: pinned + device synth parameters, one executable graph per

@@ -78,19 +78,40 @@ def _gpu_index(cfg: C.Config) -> int:
     return gpus.index(D.select_gpu(gpus, cfg.gpu))
 
 
+def make_injector(cfg: C.Config, pipe):
+    """Input sink for a pipeline: XTest into the X server the pipeline captures (the reference
+    injects through XTest/xdotool, Dockerfile:428-430); the synthetic desktop's cursor only when
+    there is no X capture, or when libXtst / the display cannot be opened."""
+    if getattr(pipe, "capture", None) is None:
+        return None  # MediaServer / RfbServer build their SyntheticInjector
+    from .server.input import XTestInjector
+
+    try:
+        return XTestInjector(cfg.display)
+    except OSError as e:
+        logging.getLogger("mxdesk").warning("XTest injection unavailable (%s): input drives the synthetic cursor", e)
+        return None
+
+
+def _clipboard_in(cfg: C.Config) -> bool:
+    return C.clipboard_directions(getattr(cfg, "enable_clipboard", "true"))[0]
+
+
 def cmd_serve(cfg: C.Config, args) -> None:
     from .server.app import MediaServer, run_forever, ssl_context
 
     device = _gpu_index(cfg) if cfg.gpu_encoder else 0
     pipe = build_pipeline(cfg, device)
+    injector = make_injector(cfg, pipe)
     rfb = None
     if cfg.novnc_enable:
         from .server.rfb import RfbServer
 
-        rfb = RfbServer(pipe, cfg.effective_basic_auth_password, cfg.novnc_viewpass, fps=min(cfg.stream_fps, 30))
+        rfb = RfbServer(pipe, cfg.effective_basic_auth_password, cfg.novnc_viewpass, fps=min(cfg.stream_fps, 30),
+                        injector=injector, clipboard_in=_clipboard_in(cfg))
     # NOVNC_ENABLE=true: the RFB front end replaces WebRTC (supervisord.conf:36 puts selkies
     # to sleep), so the H.264 pipeline is not started.
-    srv = MediaServer(pipe, cfg, rfb=rfb, start_pipeline=not cfg.novnc_enable)
+    srv = MediaServer(pipe, cfg, injector=injector, rfb=rfb, start_pipeline=not cfg.novnc_enable)
     print(f"mxdesk: serving {cfg.sizew}x{cfg.sizeh}@{cfg.stream_fps} ({cfg.encoder_backend}) on "
           f"{cfg.addr}:{cfg.port}", flush=True)
     run_forever(srv, cfg.addr, cfg.port, ssl_context(cfg))

@@ -38,6 +38,9 @@ ENC_RAW, ENC_COPYRECT, ENC_ZRLE, ENC_DESKTOPSIZE = 0, 1, 16, -223
 TILE = 64
 
 
+# ClientCutText cap (RFC 6143 7.5.6 has a u32 length; 1 MiB is ample for a clipboard)
+MAX_CUT_TEXT = 1 << 20
+
 class FrameCache:
     """Latest desktop frame (H, W, 4 BGRx), rendered at most `fps` times per second and
     shared by all RFB connections."""
@@ -180,8 +183,10 @@ class RfbConnection:
                         self.srv.inject(InputEvent("mouse", x, y, mask & 7, scroll))
                 elif t == 6:  # ClientCutText
                     _, n = struct.unpack(">3sI", await self.s.read(7))
+                    if n > MAX_CUT_TEXT:  # attacker-chosen u32: never buffer it
+                        raise ConnectionError(f"ClientCutText of {n} bytes exceeds {MAX_CUT_TEXT}")
                     text = (await self.s.read(n)).decode("latin-1")
-                    if not self.view_only:
+                    if not self.view_only and self.srv.clipboard_in:
                         self.srv.inject(InputEvent("clipboard", text=text))
                 else:
                     raise ConnectionError(f"unknown client message {t}")
@@ -246,7 +251,7 @@ class RfbConnection:
 class RfbServer:
     def __init__(self, grab: Any, password: str | None, view_password: str | None = None,
                  width: int | None = None, height: int | None = None, fps: float = 30.0, name: str = "mxdesk",
-                 injector: Any = None):
+                 injector: Any = None, clipboard_in: bool = True):
         """``grab`` is a callable returning an (H, W, 4) BGRx frame, or a StreamPipeline (its
         desktop is then rendered/captured through ``FrameGrabber``)."""
         if not callable(grab):
@@ -264,6 +269,7 @@ class RfbServer:
         self.width, self.height = width, height
         self.name = name
         self.injector = injector
+        self.clipboard_in = clipboard_in
         self.connections = 0
 
     def inject(self, ev: InputEvent) -> None:

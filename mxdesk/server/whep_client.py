@@ -257,6 +257,8 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                     res.dropped_aus += 1
                     continue
                 await_idr = False
+                if len(res.aus) >= n_frames:  # one burst can complete several AUs: keep exactly n
+                    continue
                 res.aus.append(au)
                 res.rtp_ts.append(R.rtp_header(pk)["ts"])
                 res.arrival_us.append(time.monotonic_ns() // 1000)

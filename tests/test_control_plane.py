@@ -259,3 +259,35 @@ def test_unimplemented_selkies_encoders_fall_back_to_h264():
     assert C.load(env={"WEBRTC_ENCODER": "nvh264enc"}, argv=[]).encoder_fallback is None
     with pytest.raises(ValueError):
         C.load(env={"WEBRTC_ENCODER": "bogusenc"}, argv=[]).encoder_backend
+
+
+def test_serve_wires_xtest_injector_for_x11_capture(monkeypatch):
+    """with an X11 capture the WebRTC/VNC input must reach X through XTest, not the
+    synthetic cursor; without a capture (synthetic desktop) no XTest is attempted."""
+    import types
+
+    from mxdesk import cli
+    from mxdesk.server import input as I
+    from mxdesk.utils import config as C
+
+    made = []
+
+    class FakeXTest:
+        def __init__(self, display):
+            made.append(display)
+
+        def apply(self, ev):
+            pass
+
+    monkeypatch.setattr(I, "XTestInjector", FakeXTest)
+    cfg = C.load(env={"DISPLAY": ":7"})
+    inj = cli.make_injector(cfg, types.SimpleNamespace(capture=object()))
+    assert isinstance(inj, FakeXTest) and made == [cfg.display]
+    assert cli.make_injector(cfg, types.SimpleNamespace(capture=None)) is None
+
+    class Broken:
+        def __init__(self, display):
+            raise OSError("no libXtst")
+
+    monkeypatch.setattr(I, "XTestInjector", Broken)
+    assert cli.make_injector(cfg, types.SimpleNamespace(capture=object())) is None

@@ -80,7 +80,9 @@ def test_rate_control_moves_qp(native):
         y, uv = synthetic_nv12(96, 64, t)
         enc.encode(y, uv, False)
         qps.append(enc.stats.qp)
-    assert qps[-1] > qps[1]
+    # a starved budget (20 kbps) drives the QP up immediately (probe-sized first IDR, bit-budget
+    # model), not one step per frame
+    assert min(qps[:3]) >= 40 and qps[-1] >= 40, qps
 
 
 def test_adaptive_quantisation_roundtrip_and_saves_bits(native):

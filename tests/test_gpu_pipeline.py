@@ -132,7 +132,8 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
 
 
 @pytest.mark.parametrize("w,h,subpel,sr,fresh", [(64, 48, 1, 8, 0), (160, 96, 0, 16, 0), (100, 60, 1, 16, 0),
-                                                 (320, 192, 1, 32, 0), (96, 64, 1, 8, 1)])
+                                                 (320, 192, 1, 32, 0), (96, 64, 1, 8, 1),
+                                                 (80, 48, 1, 8, 1), (48, 48, 0, 8, 1), (576, 64, 1, 8, 1)])
 def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr, fresh):
     # fresh=1: new noise every frame -> adaptive quantisation (mb_qp_delta != 0) is exercised
     stream, grec = _gpu_cpu_encode(gpu, w, h, 4, subpel=subpel, search_range=sr, fresh_noise=fresh, qp=24)

@@ -1,0 +1,71 @@
+"""CBR rate control (h264::EncoderCommon, shared by the H.264 and HEVC encoders): the stream
+must sit on its budget from the first frames on and recover within a bounded number of frames
+after a forced IDR (a WebRTC viewer join or PLI), instead of converging over a second.
+
+Reference operating point: nvh264enc low-latency CBR (reference Dockerfile:210, README.md:21)."""
+import numpy as np
+import pytest
+
+from tests.test_cpu_encoder import synthetic_nv12
+
+
+def _run(native, enc_cls, w, h, fps, kbps, frames, idr_at=(), **kw):
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps, cfg.bitrate_kbps = w, h, fps, kbps
+    cfg.search_range = kw.get("search_range", 8)
+    cfg.qp_min = 10  # small test pictures: keep the controller off the QP floor
+    enc = enc_cls(cfg)
+    bits, qps = [], []
+    for t in range(frames):
+        y, uv = synthetic_nv12(w, h, t, seed=t)  # fresh noise every frame: P frames cost bits
+        au = enc.encode(y, uv, t in idr_at)
+        bits.append(len(au) * 8)
+        qps.append(enc.stats.qp)
+    return np.array(bits, float), np.array(qps), cfg
+
+
+@pytest.mark.parametrize("kbps", [200, 500])
+def test_cbr_holds_budget_from_the_start(native, kbps):
+    fps, frames = 30, 30
+    bits, qps, _ = _run(native, native.CpuH264Encoder, 160, 96, fps, kbps, frames)
+    T = kbps * 1000.0 / fps
+    # the first IDR is sized by the probe encode to its budget (3 frames), not 10x over
+    assert 1.5 * T < bits[0] < 5.0 * T, (bits[0] / T)
+    # the driver's window: skip 5 warm-up frames, then 20+ frames within +-10 % of the target
+    window = bits[5:]
+    assert abs(window.mean() / T - 1.0) < 0.10, window.mean() / T
+    # and the QP is already settled: the late mean within 2 of the early window's
+    assert abs(qps[5:15].mean() - qps[20:].mean()) <= 2.0, qps
+
+
+def test_cbr_recovers_after_forced_idr(native):
+    fps, kbps = 30, 600
+    bits, qps, _ = _run(native, native.CpuH264Encoder, 160, 96, fps, kbps, 50, idr_at=(30,))
+    T = kbps * 1000.0 / fps
+    # the IDR is budgeted (charged to the buffer, bounded), the next 10 frames pay it back and
+    # the ten after are back on the line at the pre-IDR QP
+    assert bits[30] < 5.0 * T
+    pre = bits[20:30].mean()
+    post = bits[40:50].mean()
+    assert abs(pre / T - 1) < 0.15 and abs(post / T - 1) < 0.15, (pre / T, post / T)
+    assert abs(qps[40:50].mean() - qps[20:30].mean()) <= 2.0, qps
+    # overall: the IDR excess has been drained (whole-window average on target)
+    assert abs(bits[5:].mean() / T - 1) < 0.12
+
+
+def test_cbr_hevc_shares_the_controller(native):
+    fps, kbps = 30, 600
+    bits, qps, _ = _run(native, native.CpuHevcEncoder, 160, 96, fps, kbps, 25)
+    T = kbps * 1000.0 / fps
+    assert bits[0] < 5.0 * T
+    assert abs(bits[5:].mean() / T - 1.0) < 0.12, bits[5:].mean() / T
+
+
+def test_constant_qp_mode_untouched(native):
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height, cfg.bitrate_kbps, cfg.qp = 64, 48, 0, 31
+    enc = native.CpuH264Encoder(cfg)
+    for t in range(3):
+        y, uv = synthetic_nv12(64, 48, t)
+        enc.encode(y, uv, False)
+        assert enc.stats.qp == 31

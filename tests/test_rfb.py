@@ -276,3 +276,38 @@ def test_rfb_over_websocket():
             await runner.cleanup()
 
     asyncio.run(go())
+
+
+def test_rfb_cut_text_capped_and_view_only_ignored():
+    """ClientCutText carries an attacker-chosen u32 length -- an oversized one closes
+    the connection without buffering; view-only sessions never set the clipboard."""
+    import time
+
+    frames = Frames()
+    inj = Inj()
+    srv = RfbServer(frames, "pw", "view", 130, 70, fps=1000, injector=inj)
+
+    async def go():
+        server = await srv.serve_tcp("127.0.0.1", 0)
+        port = server.sockets[0].getsockname()[1]
+        try:
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            await _client(r, w, "pw")
+            w.write(struct.pack(">B3sI", 6, b"\0\0\0", 5) + b"hello")
+            w.write(struct.pack(">B3sI", 6, b"\0\0\0", 0xFFFFFFF0))  # 4 GiB announced
+            await w.drain()
+            t0 = time.monotonic()
+            assert await asyncio.wait_for(r.read(), 5) is not None  # server closes: EOF
+            assert time.monotonic() - t0 < 5
+            w.close()
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            await _client(r, w, "view")
+            w.write(struct.pack(">B3sI", 6, b"\0\0\0", 3) + b"abc")
+            await w.drain()
+            await asyncio.sleep(0.1)
+            w.close()
+        finally:
+            server.close()
+
+    asyncio.run(go())
+    assert [(e.kind, e.text) for e in inj.events] == [("clipboard", "hello")]
