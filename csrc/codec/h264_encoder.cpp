@@ -27,9 +27,10 @@ double EncoderCommon::frame_budget_bits() const {
     return cfg_.bitrate_kbps * 1000.0 / std::max(1, cfg_.fps);
 }
 
-int EncoderCommon::qp_for(double x, double bits) const {
-    // bits = x / qstep(qp)  =>  qp = 6 * log2(x / (0.625 * bits))
-    const double q = 6.0 * std::log2(std::max(1e-9, x) / (0.625 * std::max(1.0, bits)));
+int EncoderCommon::qp_for(double x, double bits, double alpha) const {
+    // bits = x / qstep(qp)^alpha  =>  qp = 6 * log2((x / bits)^(1/alpha) / 0.625)
+    const double r = std::max(1e-9, x) / std::max(1.0, bits);
+    const double q = 6.0 * std::log2(std::pow(r, 1.0 / alpha) / 0.625);
     return (int)std::lround(std::clamp(q, 0.0, 51.0));
 }
 
@@ -37,9 +38,9 @@ int EncoderCommon::probe_qp() const {
     if (probes_ == 0) {
         // prior: ~1 bit per luma sample at QP 30 for desktop content, scaled to the IDR budget
         const double px = (double)cfg_.width * cfg_.height;
-        return std::clamp(qp_for(px * qstep(30), kIdrBudget * frame_budget_bits()), cfg_.qp_min, cfg_.qp_max);
+        return std::clamp(qp_for(px * qstep(30), kIdrBudget * frame_budget_bits(), 1.0), cfg_.qp_min, cfg_.qp_max);
     }
-    return std::clamp(qp_for(x_i_, kIdrBudget * frame_budget_bits()), cfg_.qp_min, cfg_.qp_max);
+    return std::clamp(qp_for(x_i_, kIdrBudget * frame_budget_bits(), 1.0), cfg_.qp_min, cfg_.qp_max);
 }
 
 void EncoderCommon::add_probe(int qp, int bytes) {
@@ -80,7 +81,7 @@ void EncoderCommon::begin_frame(bool force_idr) {
     if (idr) {
         budget = kIdrBudget * T;
         const double x = x_i_ > 0 ? x_i_ : (double)cfg_.width * cfg_.height * qstep(30);
-        q = qp_for(x, budget);
+        q = qp_for(x, budget, 1.0);
     } else {
         // linear drain of the buffer excess over the recovery window that follows an IDR
         // (the whole excess is paid back kDrainFrames after it), then a gentle correction
@@ -88,13 +89,13 @@ void EncoderCommon::begin_frame(bool force_idr) {
         const double div = k <= kDrainFrames ? (double)(kDrainFrames - k + 1) : 3.0;
         budget = std::clamp(T - vbv / div, 0.25 * T, 2.0 * T);
         if (x_p_ > 0) {
-            q = qp_for(x_p_, budget);
-            if (last_p_qp_ >= 0) q = std::clamp(q, last_p_qp_ - 6, last_p_qp_ + 6);
+            q = qp_for(x_p_, budget, alpha_p_);
+            if (last_p_qp_ >= 0) q = std::clamp(q, last_p_qp_ - kMaxStep, last_p_qp_ + kMaxStep);
         } else if (x_i_ > 0) {
             // no P picture finished yet: assume a P picture costs half an I picture at equal QP
             // (pessimistic for desktops -- undershooting for a frame or two is cheaper than a
             // latency spike; the model has real P data two frames later)
-            q = qp_for(0.5 * x_i_, budget);
+            q = qp_for(0.5 * x_i_, budget, 1.0);
         } else {
             q = (last_i_qp_ >= 0 ? last_i_qp_ : cfg_.qp) + 2;
         }
@@ -116,12 +117,20 @@ void EncoderCommon::end_frame(int bytes, bool idr) {
     const double T = frame_budget_bits();
     const double bits = bytes * 8.0;
     vbv_ = std::max(-2.0 * T, vbv_ + bits - T);
-    const double x = std::max(8.0, bits) * qstep(p.qp);
+    const double b = std::max(8.0, bits);
     if (idr || p.idr) {
-        x_i_ = x;
-    } else {
-        x_p_ = x_p_ > 0 ? 0.3 * x_p_ + 0.7 * x : x;
+        x_i_ = b * qstep(p.qp);
+        return;
     }
+    // local slope of the rate-QP curve from consecutive P pictures at different QPs (desktop
+    // content is far from bits ~ 1/qstep: adaptive quantisation saturates noise-like areas)
+    if (prev_p_bits_ > 0 && prev_p_qp_ != p.qp) {
+        const double a = std::log(prev_p_bits_ / b) / std::log(qstep(p.qp) / qstep(prev_p_qp_));
+        alpha_p_ = 0.5 * alpha_p_ + 0.5 * std::clamp(a, 0.6, 3.0);
+    }
+    prev_p_bits_ = b;
+    prev_p_qp_ = p.qp;
+    x_p_ = b * std::pow(qstep(p.qp), alpha_p_);
 }
 
 static void words_to_bytes(const uint32_t* w, uint32_t bits, std::vector<uint8_t>& out) {

@@ -55,8 +55,9 @@ struct FrameStats {
 // Rate control (CBR, bitrate_kbps > 0) is a per-frame bit-budget controller with a virtual
 // buffer (VBV) model, replacing the reference's NVENC low-latency CBR (`nvh264enc`,
 // reference Dockerfile:210):
-//  * rate model per picture type t in {I, P}: bits = X_t / qstep(QP), qstep = 0.625*2^(QP/6);
-//    X_t is re-estimated from every finished frame (P: exponential average, I: latest IDR);
+//  * rate model per picture type t in {I, P}: bits = X_t / qstep(QP)^a, qstep = 0.625*2^(QP/6);
+//    X_t is re-estimated from every finished frame, the P slope `a` from consecutive P frames
+//    at different QPs (tuned offline on measured rate-QP curves: tools/rc_trace.py);
 //  * the very first IDR is sized by a synchronous probe encode (wants_probe()/add_probe()),
 //    so the stream starts on budget instead of converging for a second;
 //  * every IDR gets its own budget (idr_budget x the per-frame budget) and IS charged to the
@@ -97,9 +98,10 @@ class EncoderCommon {
     static constexpr int kDrainFrames = 6;
     static constexpr double kIdrBudget = 3.0;  // IDR budget in frames
     static constexpr int kMaxProbes = 2;
+    static constexpr int kMaxStep = 3;  // max P-picture QP change per frame (damps the pipelined loop)
 
    private:
-    int qp_for(double x, double bits) const;
+    int qp_for(double x, double bits, double alpha) const;
     EncoderConfig cfg_;
     int mb_w_, mb_h_;
     bool cur_idr_ = true;
@@ -111,7 +113,10 @@ class EncoderCommon {
     int64_t begun_ = 0;        // frames begun
     int64_t since_idr_ = 0;    // frames begun since (and including) the last IDR
     // rate model / buffer
-    double x_i_ = 0, x_p_ = 0;  // complexity (bits * qstep) of I / P pictures; 0 = unknown
+    double x_i_ = 0, x_p_ = 0;  // complexity (bits * qstep^alpha) of I / P pictures; 0 = unknown
+    double alpha_p_ = 1.0;      // P rate-QP slope, re-estimated from consecutive P pictures
+    double prev_p_bits_ = 0;
+    int prev_p_qp_ = -1;
     int last_i_qp_ = -1, last_p_qp_ = -1;
     double vbv_ = 0;  // bits sent above the CBR line so far (>= -1 frame budget)
     struct Pending {

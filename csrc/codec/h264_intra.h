@@ -1,0 +1,366 @@
+// H.264 intra prediction (Intra4x4 9 modes, Intra16x16 4 modes, chroma 4 modes), the
+// open-loop intra mode decision, Intra4x4 mode prediction, and the in-loop deblocking
+// filter (8.7) -- shared, __host__ __device__, by the HIP kernels (h264_kernels.hip) and the
+// CPU encoder (h264_cpu.cpp), so both make identical decisions and reconstructions.
+//
+// Replaces NVENC's intra toolset and loop filter behind `nvh264enc` (reference
+// Dockerfile:210, README.md:21).  Formulas follow ITU-T H.264 8.3.1.2, 8.3.3, 8.3.4, 8.7.
+#pragma once
+#include "h264_core.h"
+
+namespace mx {
+namespace h264 {
+
+// ---------------------------------------------------------------- Intra4x4 (8.3.1.2)
+enum I4Mode : int {
+    kI4V = 0, kI4H = 1, kI4DC = 2, kI4DDL = 3, kI4DDR = 4, kI4VR = 5, kI4HD = 6, kI4VL = 7, kI4HU = 8
+};
+
+// Neighbour samples of a 4x4 block: t[0..7] = p[0..7,-1] (p[4..7,-1] already replaced by
+// p[3,-1] when the top-right block is unavailable but the top is), l[0..3] = p[-1,0..3],
+// tl = p[-1,-1].
+struct Nb4 {
+    int t[8];
+    int l[4];
+    int tl;
+    bool top, left, topleft;
+};
+
+MXHD bool i4_mode_ok(int mode, const Nb4& n) {
+    switch (mode) {
+        case kI4V: case kI4DDL: case kI4VL: return n.top;
+        case kI4H: case kI4HU: return n.left;
+        case kI4DC: return true;
+        default: return n.top && n.left && n.topleft;  // DDR, VR, HD
+    }
+}
+
+// p[x, y] of 8.3.1.2 for x == -1 or y == -1
+MXHD int i4_p(const Nb4& n, int x, int y) {
+    if (y < 0) return x < 0 ? n.tl : n.t[x];
+    return n.l[y];
+}
+
+// Prediction sample (x, y) of mode `mode` (mode must be available).
+MXHD int pred4x4_px(int mode, const Nb4& n, int x, int y) {
+    switch (mode) {
+        case kI4V: return n.t[x];
+        case kI4H: return n.l[y];
+        case kI4DC: {
+            const int st = n.t[0] + n.t[1] + n.t[2] + n.t[3], sl = n.l[0] + n.l[1] + n.l[2] + n.l[3];
+            if (n.top && n.left) return (st + sl + 4) >> 3;
+            if (n.left) return (sl + 2) >> 2;
+            if (n.top) return (st + 2) >> 2;
+            return 128;
+        }
+        case kI4DDL:
+            if (x == 3 && y == 3) return (n.t[6] + 3 * n.t[7] + 2) >> 2;
+            return (n.t[x + y] + 2 * n.t[x + y + 1] + n.t[x + y + 2] + 2) >> 2;
+        case kI4DDR:
+            if (x > y) return (i4_p(n, x - y - 2, -1) + 2 * i4_p(n, x - y - 1, -1) + i4_p(n, x - y, -1) + 2) >> 2;
+            if (x < y) return (i4_p(n, -1, y - x - 2) + 2 * i4_p(n, -1, y - x - 1) + i4_p(n, -1, y - x) + 2) >> 2;
+            return (n.t[0] + 2 * n.tl + n.l[0] + 2) >> 2;
+        case kI4VR: {
+            const int z = 2 * x - y;
+            if (z >= 0 && (z & 1) == 0) return (i4_p(n, x - (y >> 1) - 1, -1) + i4_p(n, x - (y >> 1), -1) + 1) >> 1;
+            if (z > 0)
+                return (i4_p(n, x - (y >> 1) - 2, -1) + 2 * i4_p(n, x - (y >> 1) - 1, -1) + i4_p(n, x - (y >> 1), -1) +
+                        2) >> 2;
+            if (z == -1) return (n.l[0] + 2 * n.tl + n.t[0] + 2) >> 2;
+            return (i4_p(n, -1, y - 1) + 2 * i4_p(n, -1, y - 2) + i4_p(n, -1, y - 3) + 2) >> 2;
+        }
+        case kI4HD: {
+            const int z = 2 * y - x;
+            if (z >= 0 && (z & 1) == 0) return (i4_p(n, -1, y - (x >> 1) - 1) + i4_p(n, -1, y - (x >> 1)) + 1) >> 1;
+            if (z > 0)
+                return (i4_p(n, -1, y - (x >> 1) - 2) + 2 * i4_p(n, -1, y - (x >> 1) - 1) + i4_p(n, -1, y - (x >> 1)) +
+                        2) >> 2;
+            if (z == -1) return (n.l[0] + 2 * n.tl + n.t[0] + 2) >> 2;
+            return (i4_p(n, x - 1, -1) + 2 * i4_p(n, x - 2, -1) + i4_p(n, x - 3, -1) + 2) >> 2;
+        }
+        case kI4VL:
+            if ((y & 1) == 0) return (n.t[x + (y >> 1)] + n.t[x + (y >> 1) + 1] + 1) >> 1;
+            return (n.t[x + (y >> 1)] + 2 * n.t[x + (y >> 1) + 1] + n.t[x + (y >> 1) + 2] + 2) >> 2;
+        default: {  // kI4HU
+            const int z = x + 2 * y;
+            if (z < 5 && (z & 1) == 0) return (n.l[y + (x >> 1)] + n.l[y + (x >> 1) + 1] + 1) >> 1;
+            if (z < 5) return (n.l[y + (x >> 1)] + 2 * n.l[y + (x >> 1) + 1] + n.l[y + (x >> 1) + 2] + 2) >> 2;
+            if (z == 5) return (n.l[2] + 3 * n.l[3] + 2) >> 2;
+            return n.l[3];
+        }
+    }
+}
+
+// Availability of the top-right 4x4 neighbour of luma block (bx, by) inside a macroblock
+// (decoding order, 6.4.11.4): blocks whose top-right lies later in decoding order, or in
+// the macroblock to the right, have none; the top row uses the macroblock above-right.
+MXHD bool i4_topright_inside(int bx, int by) {
+    // true if the top-right block is inside this MB (or above-right MB for by == 0) and
+    // already decoded
+    if (by == 0) return true;  // depends on the above / above-right MB (checked by caller)
+    if (bx == 3) return false;
+    // blkIdx order: the top-right of (1,1) is (2,0) = blk 4, after blk 3; likewise (1,3) / (3,*)
+    if (bx == 1 && (by == 1 || by == 3)) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------- Intra16x16 / chroma
+// Neighbours of a 16x16 luma block (t/l 16 samples) or an 8x8 chroma block (t/l 8).
+struct NbMb {
+    int t[16];
+    int l[16];
+    int tl;
+    bool top, left, topleft;
+};
+
+enum I16Mode : int { kI16V = 0, kI16H = 1, kI16DC = 2, kI16Plane = 3 };
+enum ChromaMode : int { kCDC = 0, kCH = 1, kCV = 2, kCPlane = 3 };
+
+MXHD bool i16_mode_ok(int mode, const NbMb& n) {
+    if (mode == kI16V) return n.top;
+    if (mode == kI16H) return n.left;
+    if (mode == kI16DC) return true;
+    return n.top && n.left && n.topleft;
+}
+MXHD bool chroma_mode_ok(int mode, const NbMb& n) {
+    if (mode == kCV) return n.top;
+    if (mode == kCH) return n.left;
+    if (mode == kCDC) return true;
+    return n.top && n.left && n.topleft;
+}
+
+struct PredMb {  // precomputed DC / plane parameters of one 16x16 (luma) or 8x8 (chroma) block
+    int mode;
+    int dc[4];     // luma: dc[0]; chroma: per 4x4 block (raster)
+    int a, b, c;   // plane
+};
+
+MXHD PredMb prep_i16(int mode, const NbMb& n) {
+    PredMb p{};
+    p.mode = mode;
+    if (mode == kI16DC) {
+        int st = 0, sl = 0;
+        for (int i = 0; i < 16; ++i) {
+            st += n.t[i];
+            sl += n.l[i];
+        }
+        p.dc[0] = (n.top && n.left) ? (st + sl + 16) >> 5 : n.left ? (sl + 8) >> 4 : n.top ? (st + 8) >> 4 : 128;
+    } else if (mode == kI16Plane) {
+        int H = 0, V = 0;
+        for (int k = 0; k < 8; ++k) {
+            H += (k + 1) * (n.t[8 + k] - (k == 7 ? n.tl : n.t[6 - k]));
+            V += (k + 1) * (n.l[8 + k] - (k == 7 ? n.tl : n.l[6 - k]));
+        }
+        p.a = 16 * (n.l[15] + n.t[15]);
+        p.b = (5 * H + 32) >> 6;
+        p.c = (5 * V + 32) >> 6;
+    }
+    return p;
+}
+MXHD int pred16_px(const PredMb& p, const NbMb& n, int x, int y) {
+    switch (p.mode) {
+        case kI16V: return n.t[x];
+        case kI16H: return n.l[y];
+        case kI16DC: return p.dc[0];
+        default: return clip255((p.a + p.b * (x - 7) + p.c * (y - 7) + 16) >> 5);
+    }
+}
+
+MXHD PredMb prep_chroma(int mode, const NbMb& n) {
+    PredMb p{};
+    p.mode = mode;
+    if (mode == kCDC) {
+        for (int blk = 0; blk < 4; ++blk) {
+            const int xo = (blk & 1) * 4, yo = (blk >> 1) * 4;
+            const int st = n.t[xo] + n.t[xo + 1] + n.t[xo + 2] + n.t[xo + 3];
+            const int sl = n.l[yo] + n.l[yo + 1] + n.l[yo + 2] + n.l[yo + 3];
+            int v;
+            if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) {
+                v = (n.top && n.left) ? (st + sl + 4) >> 3 : n.left ? (sl + 2) >> 2 : n.top ? (st + 2) >> 2 : 128;
+            } else if (xo > 0) {  // yo == 0: top row prefers the top samples
+                v = n.top ? (st + 2) >> 2 : n.left ? (sl + 2) >> 2 : 128;
+            } else {  // xo == 0, yo > 0: left column prefers the left samples
+                v = n.left ? (sl + 2) >> 2 : n.top ? (st + 2) >> 2 : 128;
+            }
+            p.dc[blk] = v;
+        }
+    } else if (mode == kCPlane) {
+        int H = 0, V = 0;
+        for (int k = 0; k < 4; ++k) {
+            H += (k + 1) * (n.t[4 + k] - (k == 3 ? n.tl : n.t[2 - k]));
+            V += (k + 1) * (n.l[4 + k] - (k == 3 ? n.tl : n.l[2 - k]));
+        }
+        p.a = 16 * (n.l[7] + n.t[7]);
+        p.b = (34 * H + 32) >> 6;
+        p.c = (34 * V + 32) >> 6;
+    }
+    return p;
+}
+MXHD int predc_px(const PredMb& p, const NbMb& n, int x, int y) {
+    switch (p.mode) {
+        case kCDC: return p.dc[(y >> 2) * 2 + (x >> 2)];
+        case kCH: return n.l[y];
+        case kCV: return n.t[x];
+        default: return clip255((p.a + p.b * (x - 3) + p.c * (y - 3) + 16) >> 5);
+    }
+}
+
+// ---------------------------------------------------------------- SATD / decision
+// Sum of absolute 4x4 Hadamard coefficients of a residual block, halved (SATD).
+MXHD uint32_t satd4x4(const int* d) {
+    int h[16];
+    hadamard4x4(d, h);
+    uint32_t s = 0;
+    for (int i = 0; i < 16; ++i) s += (uint32_t)(h[i] < 0 ? -h[i] : h[i]);
+    return (s + 1) >> 1;
+}
+
+constexpr uint32_t kCostInf = 0x3fffffffu;
+
+// Per-macroblock open-loop intra costs (SATD against predictions built from SOURCE
+// neighbours, so every macroblock is analysed independently and in parallel):
+struct IntraCosts {
+    uint32_t c4[16][9];  // [blkIdx][I4 mode], kCostInf when unavailable
+    uint32_t c16[4];     // [I16 mode]
+    uint32_t cc[4];      // [chroma mode] (Cb + Cr)
+};
+
+struct IntraDecision {
+    int type;        // kMbI16x16 / kMbI4x4
+    int i16_mode;
+    int chroma_mode;
+    uint8_t i4[16];  // modes, raster (by * 4 + bx)
+    uint32_t cost;   // luma + chroma, lambda-weighted
+};
+
+// Estimated predicted-mode flag cost inside the MB: internal neighbours use the modes just
+// chosen; neighbours in other macroblocks are unknown during the parallel analysis and are
+// taken as DC (the actual coding uses the true predictor).
+MXHD IntraDecision decide_intra(const IntraCosts& c, int qp) {
+    const uint32_t lam = (uint32_t)lambda_sad(qp);
+    IntraDecision d{};
+    int m4[16];  // raster
+    uint32_t cost4 = 6 * lam;  // I_NxN signalling overhead vs I16x16 (16 mode fields + cbp)
+    for (int b = 0; b < 16; ++b) {
+        const int bx = kBlkX[b], by = kBlkY[b];
+        const int ma = bx > 0 ? m4[by * 4 + bx - 1] : kI4DC;
+        const int mb = by > 0 ? m4[(by - 1) * 4 + bx] : kI4DC;
+        const int pm = ma < mb ? ma : mb;
+        uint32_t best = kCostInf;
+        int bm = kI4DC;
+        for (int m = 0; m < 9; ++m) {
+            if (c.c4[b][m] >= kCostInf) continue;
+            const uint32_t v = c.c4[b][m] + lam * (m == pm ? 1u : 4u);
+            if (v < best) {
+                best = v;
+                bm = m;
+            }
+        }
+        m4[by * 4 + bx] = bm;
+        cost4 += best;
+    }
+    uint32_t cost16 = kCostInf;
+    int b16 = kI16DC;
+    for (int m = 0; m < 4; ++m) {
+        if (c.c16[m] >= kCostInf) continue;
+        const uint32_t v = c.c16[m] + lam * 2u;
+        if (v < cost16) {
+            cost16 = v;
+            b16 = m;
+        }
+    }
+    uint32_t costc = kCostInf;
+    int bc = kCDC;
+    for (int m = 0; m < 4; ++m) {
+        if (c.cc[m] >= kCostInf) continue;
+        const uint32_t v = c.cc[m] + lam * (uint32_t)ue_len((uint32_t)m);
+        if (v < costc) {
+            costc = v;
+            bc = m;
+        }
+    }
+    d.type = cost4 < cost16 ? 2 /* kMbI4x4 */ : 1 /* kMbI16x16 */;
+    d.i16_mode = b16;
+    d.chroma_mode = bc;
+    for (int i = 0; i < 16; ++i) d.i4[i] = (uint8_t)m4[i];
+    d.cost = (cost4 < cost16 ? cost4 : cost16) + costc;
+    return d;
+}
+
+// predIntra4x4PredMode (8.3.1.1) given the neighbour modes (-1 = "use DC": neighbour MB
+// unavailable -> dcPredModePredictedFlag, or not coded in Intra4x4).
+MXHD int i4_pred_mode(int mode_a, int mode_b, bool a_avail, bool b_avail) {
+    if (!a_avail || !b_avail) return kI4DC;
+    const int a = mode_a < 0 ? kI4DC : mode_a, b = mode_b < 0 ? kI4DC : mode_b;
+    return a < b ? a : b;
+}
+
+// ---------------------------------------------------------------- deblocking (8.7)
+constexpr uint8_t kAlpha[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   0,   0,   4,   4,
+                                5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20,  22,  25,  28,  32,  36,  40,  45,
+                                50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+constexpr uint8_t kBeta[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  0,  0,  2,  2,  2,  3,  3,  3,  3,  4,  4, 4,
+                               6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+constexpr uint8_t kTc0[52][3] = {
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
+    {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
+    {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4},
+    {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
+    {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+MXHD int iabs(int v) { return v < 0 ? -v : v; }
+MXHD int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Filter one line of luma samples across an edge: s[0..3] = p3..p0... stored as
+// p[k] = p_k (p[0] nearest the edge) and q[k] = q_k.  indexA = clip(qPav) (offsets 0).
+MXHD void db_luma_line(int* p, int* q, int bS, int indexA) {
+    const int alpha = kAlpha[indexA], beta = kBeta[indexA];
+    const int p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3], q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+    const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
+    if (bS < 4) {
+        const int tc0 = kTc0[indexA][bS - 1];
+        const int tc = tc0 + (ap < beta ? 1 : 0) + (aq < beta ? 1 : 0);
+        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + (p1 - q1) + 4) >> 3));
+        p[0] = clip255(p0 + delta);
+        q[0] = clip255(q0 - delta);
+        if (ap < beta) p[1] = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1);
+        if (aq < beta) q[1] = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1);
+        return;
+    }
+    const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
+    if (ap < beta && strong) {
+        p[0] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+        p[1] = (p2 + p1 + p0 + q0 + 2) >> 2;
+        p[2] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+    } else {
+        p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
+    }
+    if (aq < beta && strong) {
+        q[0] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+        q[1] = (p0 + q0 + q1 + q2 + 2) >> 2;
+        q[2] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+    } else {
+        q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
+    }
+}
+
+// Chroma line (chromaStyleFilteringFlag): p[0..1], q[0..1].
+MXHD void db_chroma_line(int* p, int* q, int bS, int indexA) {
+    const int alpha = kAlpha[indexA], beta = kBeta[indexA];
+    const int p0 = p[0], p1 = p[1], q0 = q[0], q1 = q[1];
+    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+    if (bS < 4) {
+        const int tc = kTc0[indexA][bS - 1] + 1;
+        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + (p1 - q1) + 4) >> 3));
+        p[0] = clip255(p0 + delta);
+        q[0] = clip255(q0 - delta);
+        return;
+    }
+    p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
+    q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
+}
+
+}  // namespace h264
+}  // namespace mx
