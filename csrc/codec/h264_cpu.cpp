@@ -46,7 +46,7 @@ void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, 
     for (int r = 0; r < 16; ++r)
         for (int k = 0; k < 16; ++k)
             sad0 += std::abs((int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + k, y0 + r));
-    const bool is_static = sad0 <= kStaticSad;
+    const bool is_static = sad0 <= static_sad(frame_qp);
     unsigned long long best = ~0ull;
     for (int c = 0; c < (is_static ? 0 : side * side); ++c) {
         const int dy = c / side - R, dx = c % side - R;

@@ -90,7 +90,6 @@ void EncoderCommon::begin_frame(bool force_idr) {
         budget = std::clamp(T - vbv / div, 0.25 * T, 2.0 * T);
         if (x_p_ > 0) {
             q = qp_for(x_p_, budget, alpha_p_);
-            if (last_p_qp_ >= 0) q = std::clamp(q, last_p_qp_ - kMaxStep, last_p_qp_ + kMaxStep);
         } else if (x_i_ > 0) {
             // no P picture finished yet: assume a P picture costs half an I picture at equal QP
             // (pessimistic for desktops -- undershooting for a frame or two is cheaper than a
@@ -99,13 +98,21 @@ void EncoderCommon::begin_frame(bool force_idr) {
         } else {
             q = (last_i_qp_ >= 0 ? last_i_qp_ : cfg_.qp) + 2;
         }
+        // asymmetric step limits: lowering the QP below the reference's makes the picture
+        // refine the whole reference (a P at QP-3 after a coarse IDR cost 2.6 budgets on the
+        // 1080p desktop: profiles/r02_rc), so QP falls by at most kMaxDown per frame; rising is
+        // cheap and protects the buffer.  Right after an IDR the ramp starts from the IDR's QP.
+        if (last_was_idr_)
+            q = std::max(q, last_p_qp_ - kMaxDown);
+        else if (last_p_qp_ >= 0)
+            q = std::clamp(q, last_p_qp_ - kMaxDown, last_p_qp_ + kMaxStep);
     }
     cur_qp_ = std::clamp(std::clamp(q, cfg_.qp_min, cfg_.qp_max), 0, 51);
-    pending_.push_back(Pending{budget, cur_qp_, idr});
-    if (idr)
-        last_i_qp_ = cur_qp_;
-    else
-        last_p_qp_ = cur_qp_;
+    pending_.push_back(Pending{budget, cur_qp_, idr, since_idr_});
+    last_p_qp_ = cur_qp_;  // an IDR anchors the next P: its QP ramps down from the IDR's by
+                           // kMaxStep per frame instead of refining the whole picture at once
+    if (idr) last_i_qp_ = cur_qp_;
+    last_was_idr_ = idr;
 }
 
 void EncoderCommon::end_frame(int bytes, bool idr) {
@@ -124,7 +131,9 @@ void EncoderCommon::end_frame(int bytes, bool idr) {
     }
     // local slope of the rate-QP curve from consecutive P pictures at different QPs (desktop
     // content is far from bits ~ 1/qstep: adaptive quantisation saturates noise-like areas)
-    if (prev_p_bits_ > 0 && prev_p_qp_ != p.qp) {
+    // (not across the refinement frames right after an IDR: their cost reflects the IDR's
+    // quality, not the content's rate-QP slope)
+    if (prev_p_bits_ > 0 && prev_p_qp_ != p.qp && p.since_idr > kDrainFrames / 2) {
         const double a = std::log(prev_p_bits_ / b) / std::log(qstep(p.qp) / qstep(prev_p_qp_));
         alpha_p_ = 0.5 * alpha_p_ + 0.5 * std::clamp(a, 0.6, 3.0);
     }
@@ -311,12 +320,13 @@ GpuH264Encoder::~GpuH264Encoder() {
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
 }
 
-void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
     FrameSlot& sl = slots_[prep_slot_];
+    const FrameState* pub = publish ? sl.fs_host : nullptr;
     if (idr) {
-        launch_intra(geom_, sl.buf, src_y, src_uv, stream_);
+        launch_intra(geom_, sl.buf, src_y, src_uv, stream_, pub);
     } else {
-        launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_);
+        launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
         launch_me(geom_, sl.buf, src_y, stream_);
         launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
@@ -367,8 +377,7 @@ int GpuH264Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     fill_state(sl, true, qp, cur_ ^ 1, cur_);
     sl.fs_host->frame_num = 0;
     sl.fs_host->idr_pic_id = 0;
-    HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
-    enqueue_kernels(true, src_y, src_uv);
+    enqueue_kernels(true, src_y, src_uv, true);
     HIP_CHECK(hipStreamSynchronize(stream_));
     if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
     const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);
@@ -395,11 +404,11 @@ bool GpuH264Encoder::prepare(bool force_idr) {
 }
 
 void GpuH264Encoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
-    // frame-state upload + kernels: depends only on fixed buffers and the device frame state
-    // (with depth 1 the same slot every frame, so it can be captured into a hipGraph)
+    // hipGraph form: frame-state upload node + kernels that read the device copy (depends
+    // only on fixed buffers, so with depth 1 the same graph replays every frame of a type)
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
-    enqueue_kernels(idr, src_y, src_uv);
+    enqueue_kernels(idr, src_y, src_uv, false);
 }
 
 void GpuH264Encoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
@@ -417,7 +426,7 @@ void GpuH264Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
     }
     const bool idr = prepare(force_idr);
     record_start();
-    enqueue_body(idr, src_y, src_uv);
+    enqueue_kernels(idr, src_y, src_uv, true);  // eager: the state travels as kernel arguments
     record_done();
 }
 

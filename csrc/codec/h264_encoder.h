@@ -95,10 +95,11 @@ class EncoderCommon {
     int probe_qp() const;                 // QP to probe next
     void add_probe(int qp, int bytes);    // result of a probe encode of the first picture
     double vbv_excess_bits() const { return vbv_; }
-    static constexpr int kDrainFrames = 6;
+    static constexpr int kDrainFrames = 8;
     static constexpr double kIdrBudget = 3.0;  // IDR budget in frames
     static constexpr int kMaxProbes = 2;
-    static constexpr int kMaxStep = 3;  // max P-picture QP change per frame (damps the pipelined loop)
+    static constexpr int kMaxStep = 3;  // max P-picture QP rise per frame (damps the pipelined loop)
+    static constexpr int kMaxDown = 2;  // max P-picture QP fall per frame (bounds refinement spikes)
 
    private:
     int qp_for(double x, double bits, double alpha) const;
@@ -117,12 +118,14 @@ class EncoderCommon {
     double alpha_p_ = 1.0;      // P rate-QP slope, re-estimated from consecutive P pictures
     double prev_p_bits_ = 0;
     int prev_p_qp_ = -1;
-    int last_i_qp_ = -1, last_p_qp_ = -1;
+    int last_i_qp_ = -1, last_p_qp_ = -1;  // last_p_qp_: QP of the last begun picture (IDR included)
+    bool last_was_idr_ = false;
     double vbv_ = 0;  // bits sent above the CBR line so far (>= -1 frame budget)
     struct Pending {
         double budget;
         int qp;
         bool idr;
+        int64_t since_idr;  // frames since the IDR (1 = the IDR itself)
     };
     std::deque<Pending> pending_;  // begun, not yet ended (pipelined frames)
     int probes_ = 0;
@@ -174,7 +177,9 @@ class GpuH264Encoder final : public VideoEncoder {
     void record_done() override;
     // Completion event of the last collected frame.
     hipEvent_t done_event() const override { return last_done_; }
-    void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv);
+    // publish: the first kernel takes the frame state by value and stores it (eager launches);
+    // otherwise the kernels read the device copy uploaded by enqueue_body's memcpy node.
+    void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish);
 
    private:
     struct FrameSlot {  // per-frame-in-flight state

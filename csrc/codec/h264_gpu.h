@@ -116,12 +116,15 @@ struct DeviceBuffers {
 void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream);
 void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream);
+// The first kernel of a frame (launch_intra for I, launch_hpel for P) publishes the frame
+// state: with `publish` non-null it takes the state by value and stores it to b.fs for the
+// later kernels (no copy node); with nullptr it reads b.fs (filled by a memcpy node, hipGraph).
 void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                  hipStream_t stream);
+                  hipStream_t stream, const FrameState* publish = nullptr);
 // Build the padded F/H/V/J planes of the reference luma (b.fs->ref_y) into `planes` (4 planes,
 // each hp_pitch x (coded_h + 2*kHpelPad), origin offset applied by the caller via FrameState).
 void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
-                 hipStream_t stream);
+                 hipStream_t stream, const FrameState* publish = nullptr);
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
 
 }  // namespace h264

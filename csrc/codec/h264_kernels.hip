@@ -134,12 +134,30 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
     const uint32_t hi = __builtin_amdgcn_perm((uint32_t)d, (uint32_t)c, 0x0c0c0400u);
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
-__global__ __launch_bounds__(256) void k_hpel(Geometry g, const FrameState* __restrict__ fs, uint8_t* __restrict__ pf,
+// Frame-state publication: the first kernel of a frame receives the state by value (kernel
+// arguments, no extra dispatch) and stores it for the later kernels, replacing a per-frame
+// 4.4 us host->device copy node (profiles/r02_b).  Under hipGraph capture the state still
+// comes from a captured memcpy node (the captured argument would be stale), so `publish` = 0
+// and the kernel reads the device copy.
+struct StateArg {
+    FrameState v;
+    FrameState* dst;
+    int publish;
+};
+__device__ __forceinline__ void publish_state(const StateArg& a) {
+    static_assert(sizeof(FrameState) % 4 == 0, "FrameState is copied as dwords");
+    if (a.publish && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < sizeof(FrameState) / 4)
+        reinterpret_cast<uint32_t*>(a.dst)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&a.v)[threadIdx.x];
+}
+__device__ __forceinline__ const FrameState& state_of(const StateArg& a) { return a.publish ? a.v : *a.dst; }
+
+__global__ __launch_bounds__(256) void k_hpel(Geometry g, StateArg sa, uint8_t* __restrict__ pf,
                                               uint8_t* __restrict__ ph, uint8_t* __restrict__ pv,
                                               uint8_t* __restrict__ pj, int hp_pitch) {
     __shared__ uint32_t smp[kHpTH + 5][kHpSW / 4];
     __shared__ int4 b1[kHpTH + 5][kHpTW / 4];  // 4 columns per entry
-    const uint8_t* __restrict__ ref = fs->ref_y;  // via the frame state: graph-replay safe
+    publish_state(sa);
+    const uint8_t* __restrict__ ref = state_of(sa).ref_y;
     const int px0 = blockIdx.x * kHpTW, py0 = blockIdx.y * kHpTH;  // padded-plane coordinates
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     const int tid = threadIdx.x;
@@ -274,7 +292,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         if (lane == 0) s_sad0[tid >> 6] = d;
         __syncthreads();
         const uint32_t sad0 = s_sad0[0] + s_sad0[1] + s_sad0[2] + s_sad0[3];
-        if (sad0 <= kStaticSad) {
+        if (sad0 <= static_sad(fs->qp)) {
             if (tid == 0) {
                 mbs[mbi].mvx = 0;
                 mbs[mbi].mvy = 0;
@@ -548,7 +566,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
 
 // ------------------------------------------------------------------ intra (I slices)
 // One wave per MB row; every row is its own slice, so the only neighbour is the left MB.
-__global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState* __restrict__ fs,
+__global__ __launch_bounds__(64) void k_intra_rows(Geometry g, StateArg sa,
                                                     const uint8_t* __restrict__ src_y,
                                                     const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
                                                     int16_t* __restrict__ coef) {
@@ -560,6 +578,8 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, const FrameState*
     __shared__ int cdc_nz[2];
     __shared__ int modes[2];
 
+    publish_state(sa);
+    const FrameState* fs = &state_of(sa);
     const int mby = blockIdx.x, lane = threadIdx.x;
     const int qp = fs->qp;
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
@@ -1183,10 +1203,14 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
 }  // namespace
 
 void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
-                 hipStream_t stream) {
+                 hipStream_t stream, const FrameState* publish) {
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     dim3 grid((W + kHpTW - 1) / kHpTW, (H + kHpTH - 1) / kHpTH);
-    hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, b.fs, planes[0], planes[1], planes[2], planes[3],
+    StateArg sa{};
+    if (publish) sa.v = *publish;
+    sa.dst = b.fs;
+    sa.publish = publish ? 1 : 0;
+    hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, sa, planes[0], planes[1], planes[2], planes[3],
                        hp_pitch);
 }
 
@@ -1203,8 +1227,12 @@ void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
 }
 
 void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                  hipStream_t stream) {
-    hipLaunchKernelGGL(k_intra_rows, dim3(g.mb_h), dim3(64), 0, stream, g, b.fs, src_y, src_uv, b.mb, b.coef);
+                  hipStream_t stream, const FrameState* publish) {
+    StateArg sa{};
+    if (publish) sa.v = *publish;
+    sa.dst = b.fs;
+    sa.publish = publish ? 1 : 0;
+    hipLaunchKernelGGL(k_intra_rows, dim3(g.mb_h), dim3(64), 0, stream, g, sa, src_y, src_uv, b.mb, b.coef);
 }
 
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream) {

@@ -180,9 +180,18 @@ MXHD int me_range(int r) {
     r = r < 4 ? 4 : (r > 32 ? 32 : r);
     return (r + 3) & ~3;
 }
-// Static-block early exit: a zero vector with SAD <= kStaticSad ends the search (both
-// encoders apply the same rule, so their decisions stay bit-identical).
+// Static-block early exit: a zero vector with SAD <= static_sad(qp) ends the search (both
+// encoders apply the same rule, so their decisions stay bit-identical).  The reference is the
+// lossy reconstruction, so an unchanged desktop region differs from it by the coding noise of
+// the previous picture; a fixed threshold (128 = 0.5 per pixel) sent nearly every static MB of
+// a QP-36 desktop through the full search (profiles/r02_c: ~1100 VALU per wave in k_me_full).
+// A flat 16x16 residual of r per sample quantises to zero while r < ~qstep/4.7 (inter dead
+// zone, 4x4 DC); 64 * lambda_sad(qp) ~ 256 * qstep / 12 stays well inside that.
 constexpr uint32_t kStaticSad = 128;
+MXHD uint32_t static_sad(int qp) {
+    const uint32_t t = 64u * (uint32_t)lambda_sad(qp);
+    return t > kStaticSad ? t : kStaticSad;
+}
 
 // Sub-pel refinement neighbour k (0..7) offsets.
 MXHD void subpel_offset(int k, int* dx, int* dy) {

@@ -47,9 +47,13 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
                           uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream);
 
 // Luma squared error between two planes over [0,w) x [0,h) excluding the rectangle
-// [mx0,mx1) x [my0,my1), atomically added to *acc (quality report with a panel masked out).
+// [mx0,mx1) x [my0,my1) (quality report with a panel masked out), in one dispatch: `part`
+// holds sse_masked_blocks(w, h) partials, `counter` is a zero-initialised device uint that the
+// kernel leaves at zero, and the total is stored to `host_out` (mapped pinned memory).
+int sse_masked_blocks(int w, int h);
 void launch_sse_masked(const uint8_t* a, const uint8_t* b, int pitch, int w, int h, int mx0, int my0, int mx1,
-                       int my1, unsigned long long* acc, hipStream_t stream);
+                       int my1, unsigned long long* part, unsigned int* counter, unsigned long long* host_out,
+                       hipStream_t stream);
 
 // Copy a BGRx tile into a larger BGRx frame at (dx, dy) (tiled-wall composite).
 void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,

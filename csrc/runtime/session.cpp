@@ -117,8 +117,13 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     }
     for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
     if (masked()) {
-        HIP_CHECK(hipMalloc(&mask_dev_, 2 * sizeof(unsigned long long)));
-        HIP_CHECK(hipHostMalloc(&mask_host_, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        const h264::Geometry& eg = enc_->geometry();
+        const int nb = pix::sse_masked_blocks(eg.width, eg.height);
+        HIP_CHECK(hipMalloc(&mask_dev_, 2 * (size_t)nb * sizeof(unsigned long long)));
+        HIP_CHECK(hipMalloc(&mask_counter_, 2 * sizeof(unsigned int)));
+        HIP_CHECK(hipMemset(mask_counter_, 0, 2 * sizeof(unsigned int)));
+        mask_stride_ = nb;
+        HIP_CHECK(hipHostMalloc(&mask_host_, 2 * sizeof(unsigned long long), hipHostMallocMapped));
         for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_mask_[k], hipEventDisableTiming));
     }
     HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams), hipHostMallocDefault));
@@ -142,6 +147,7 @@ Session::~Session() {
     if (lt_mem_) hipFree(lt_mem_);
     for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
     if (mask_dev_) (void)hipFree(mask_dev_);
+    if (mask_counter_) (void)hipFree(mask_counter_);
     if (mask_host_) (void)hipHostFree(mask_host_);
     for (int k = 0; k < 2; ++k)
         if (ev_mask_[k]) (void)hipEventDestroy(ev_mask_[k]);
@@ -172,10 +178,9 @@ void Session::enqueue_mask_sse(int k) {
     // by the next frame's conversion, which is later on the same stream)
     if (!masked()) return;
     const h264::EncoderConfig& e = enc_->rc().config();
-    HIP_CHECK(hipMemsetAsync(mask_dev_ + k, 0, sizeof(unsigned long long), stream_));
     pix::launch_sse_masked(nv12_y_, enc_->recon_y(), enc_->pitch(), e.width, e.height, cfg_.mask_x0, cfg_.mask_y0,
-                           cfg_.mask_x1, cfg_.mask_y1, mask_dev_ + k, stream_);
-    HIP_CHECK(hipMemcpyAsync(mask_host_ + k, mask_dev_ + k, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream_));
+                           cfg_.mask_x1, cfg_.mask_y1, mask_dev_ + (size_t)k * mask_stride_, mask_counter_ + k,
+                           mask_host_ + k, stream_);  // mapped: the kernel stores the total to the host
     HIP_CHECK(hipEventRecord(ev_mask_[k], stream_));
 }
 

@@ -141,7 +141,9 @@ class Session {
     hipEvent_t ev_start_[2] = {nullptr, nullptr};
     // masked-PSNR accumulators (device) + their host copies, one per frame in flight
     unsigned long long* mask_dev_ = nullptr;
-    unsigned long long* mask_host_ = nullptr;
+    unsigned long long* mask_host_ = nullptr;  // mapped pinned, one word per frame in flight
+    unsigned int* mask_counter_ = nullptr;     // single-pass reduction counters (device)
+    int mask_stride_ = 0;
     hipEvent_t ev_mask_[2] = {nullptr, nullptr};
     bool masked() const { return cfg_.mask_x1 > cfg_.mask_x0 && cfg_.mask_y1 > cfg_.mask_y0; }
     void enqueue_mask_sse(int k);
