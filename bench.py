@@ -52,6 +52,8 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
+    ap.add_argument("--intra-in-p", type=int, default=None,
+                    help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
     ap.add_argument("--depth", type=int, default=2,
                     help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1; "
                          "1: strictly one frame at a time, lowest back-to-back latency)")
@@ -99,6 +101,8 @@ def main() -> None:
     cfg.enc.subpel = args.subpel
     if args.tu_split is not None:
         cfg.enc.tu_split = args.tu_split
+    if args.intra_in_p is not None:
+        cfg.enc.intra_in_p = args.intra_in_p
     cfg.noise = args.noise
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth

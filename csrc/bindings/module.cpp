@@ -152,6 +152,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("chroma_qp_offset", &h264::EncoderConfig::chroma_qp_offset)
         .def_readwrite("pipeline_depth", &h264::EncoderConfig::pipeline_depth)
         .def_readwrite("aq", &h264::EncoderConfig::aq)
+        .def_readwrite("intra_in_p", &h264::EncoderConfig::intra_in_p)
         .def_readwrite("deblock", &h264::EncoderConfig::deblock)
         .def_readwrite("tu_split", &h264::EncoderConfig::tu_split);
 

@@ -118,6 +118,160 @@ static Geometry geom_of(const EncoderCommon& c, int cw, int ch) {
     return g;
 }
 
+// Open-loop intra analysis of one macroblock (source neighbours): the same costs and decision
+// as k_intra_analyze.
+static IntraDecision analyze_intra_mb(const Geometry& g, const uint8_t* sy, const uint8_t* suv, int pitch, int mbx,
+                                      int mby, int slice_rows, int qp) {
+    const Avail av = mb_avail(g, mbx, mby, slice_rows);
+    const int x0 = mbx * 16, y0 = mby * 16;
+    IntraCosts c;
+    for (int b = 0; b < 16; ++b)
+        for (int m = 0; m < 9; ++m) c.c4[b][m] = i4_cost(sy, pitch, x0, y0, b, m, av.left, av.top, av.topright, av.topleft);
+    const NbMb nl = nbmb_from_plane(sy, pitch, x0, y0, 16, 1, 0, av.left, av.top, av.topleft);
+    for (int m = 0; m < 4; ++m) {
+        if (!i16_mode_ok(m, nl)) {
+            c.c16[m] = kCostInf;
+            continue;
+        }
+        const PredMb p = prep_i16(m, nl);
+        uint32_t t = 0;
+        for (int rb = 0; rb < 16; ++rb) t += i16_block_cost(sy, pitch, x0, y0, rb, p, nl);
+        c.c16[m] = t;
+    }
+    for (int m = 0; m < 4; ++m) {
+        uint32_t t = 0;
+        for (int comp = 0; comp < 2; ++comp) {
+            const NbMb nc = nbmb_from_plane(suv, pitch, x0 / 2, y0 / 2, 8, 2, comp, av.left, av.top, av.topleft);
+            if (!chroma_mode_ok(m, nc)) {
+                t = kCostInf;
+                break;
+            }
+            const PredMb p = prep_chroma(m, nc);
+            for (int cb = 0; cb < 4; ++cb) t += chroma_block_cost(suv, pitch, x0 / 2, y0 / 2, comp, cb, p, nc);
+        }
+        c.cc[m] = t;
+    }
+    return decide_intra(c, qp);
+}
+
+static void set_intra(MbInfo& m, const IntraDecision& d, int qp) {
+    m.type = (uint8_t)d.type;
+    m.i16_mode = (uint8_t)d.i16_mode;
+    m.chroma_mode = (uint8_t)d.chroma_mode;
+    for (int rb = 0; rb < 16; ++rb) i4_set(m.i4, rb, d.i4[rb]);
+    m.qp = (uint8_t)qp;
+    m.mvx = 0;
+    m.mvy = 0;
+}
+
+// Closed-loop coding of one intra macroblock (modes already decided): prediction from the
+// reconstruction, transform, quantisation, reconstruction; the same arithmetic as k_intra_wave.
+static void code_intra_mb(const Geometry& g, const uint8_t* sy, const uint8_t* suv, int pitch, uint8_t* rec_y,
+                          uint8_t* rec_uv, int cw, int mbx, int mby, int slice_rows, int qp, int chroma_qp_offset,
+                          MbInfo& m, int16_t* mc) {
+    const Avail av = mb_avail(g, mbx, mby, slice_rows);
+    const int x0 = mbx * 16, y0 = mby * 16;
+    const int qpc = chroma_qp(qp, chroma_qp_offset);
+    int cbp_l = 0;
+    if (m.type == kMbI4x4) {
+        for (int b = 0; b < 16; ++b) {
+            const int bx = kBlkX[b], by = kBlkY[b];
+            const Nb4 n = nb4_from_plane(rec_y, cw, x0, y0, bx, by, av.left, av.top, av.topright, av.topleft);
+            const int mode = i4_get(m.i4, by * 4 + bx);
+            int pred[16], x[16], y[16], z[16], d[16], r[16];
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) {
+                    pred[i * 4 + j] = pred4x4_px(mode, n, j, i);
+                    x[i * 4 + j] = sy[(y0 + 4 * by + i) * pitch + x0 + 4 * bx + j] - pred[i * 4 + j];
+                }
+            fdct4x4(x, y);
+            const int nz = quant4x4(y, z, qp, true, 0);
+            for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)z[kZigzag4x4[k]];
+            dequant4x4(z, d, qp, 0);
+            idct4x4(d, r);
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    rec_y[(y0 + 4 * by + i) * cw + x0 + 4 * bx + j] = (uint8_t)clip255(pred[i * 4 + j] + r[i * 4 + j]);
+            m.nz_luma[by * 4 + bx] = (uint8_t)nz;
+            if (nz) cbp_l |= 1 << (b >> 2);
+        }
+    } else {  // Intra16x16
+        const NbMb n = nbmb_from_plane(rec_y, cw, x0, y0, 16, 1, 0, av.left, av.top, av.topleft);
+        const PredMb p = prep_i16(m.i16_mode, n);
+        int z[16][16], ldc[16], nzl[16];
+        bool luma_ac = false;
+        for (int b = 0; b < 16; ++b) {
+            const int bx = kBlkX[b], by = kBlkY[b];
+            int x[16], y[16];
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    x[i * 4 + j] = sy[(y0 + 4 * by + i) * pitch + x0 + 4 * bx + j] - pred16_px(p, n, 4 * bx + j, 4 * by + i);
+            fdct4x4(x, y);
+            ldc[by * 4 + bx] = y[0];
+            nzl[b] = quant4x4(y, z[b], qp, true, 1);
+            luma_ac |= nzl[b] > 0;
+            for (int k = 1; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)z[b][kZigzag4x4[k]];
+            mc[kCoefLuma + b * 16] = 0;
+        }
+        int zd[16], dq[16];
+        quant_dc_luma(ldc, zd, qp);
+        for (int k = 0; k < 16; ++k) mc[kCoefLumaDc + k] = (int16_t)zd[kZigzag4x4[k]];
+        dequant_dc_luma(zd, dq, qp);
+        for (int b = 0; b < 16; ++b) {
+            const int bx = kBlkX[b], by = kBlkY[b];
+            int d[16], rr[16];
+            if (luma_ac)
+                dequant4x4(z[b], d, qp, 1);
+            else
+                for (int i = 1; i < 16; ++i) d[i] = 0;
+            d[0] = dq[by * 4 + bx];
+            idct4x4(d, rr);
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    rec_y[(y0 + 4 * by + i) * cw + x0 + 4 * bx + j] =
+                        (uint8_t)clip255(pred16_px(p, n, 4 * bx + j, 4 * by + i) + rr[i * 4 + j]);
+            m.nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nzl[b] : 0);
+        }
+        cbp_l = luma_ac ? 15 : 0;
+    }
+    bool any_ac = false, any_dc = false;
+    for (int comp = 0; comp < 2; ++comp) {
+        const NbMb n = nbmb_from_plane(rec_uv, cw, x0 / 2, y0 / 2, 8, 2, comp, av.left, av.top, av.topleft);
+        const PredMb p = prep_chroma(m.chroma_mode, n);
+        int zc[4][16], dcin[4];
+        for (int cbk = 0; cbk < 4; ++cbk) {
+            const int bx = cbk & 1, by = cbk >> 1;
+            int x[16], y[16];
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    x[i * 4 + j] = suv[(y0 / 2 + 4 * by + i) * pitch + 2 * (x0 / 2 + 4 * bx + j) + comp] -
+                                   predc_px(p, n, 4 * bx + j, 4 * by + i);
+            fdct4x4(x, y);
+            dcin[cbk] = y[0];
+            const int nz = quant4x4(y, zc[cbk], qpc, true, 1);
+            for (int k = 1; k < 16; ++k) mc[kCoefChromaAc + (comp * 4 + cbk) * 16 + k] = (int16_t)zc[cbk][kZigzag4x4[k]];
+            (comp ? m.nz_cr : m.nz_cb)[cbk] = (uint8_t)nz;
+            any_ac |= nz > 0;
+        }
+        int zdc[4], dqc[4];
+        any_dc |= quant_dc_chroma(dcin, zdc, qpc, true) > 0;
+        for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zdc[i];
+        dequant_dc_chroma(zdc, dqc, qpc);
+        for (int cbk = 0; cbk < 4; ++cbk) {
+            const int bx = cbk & 1, by = cbk >> 1;
+            int d[16], rr[16];
+            dequant4x4(zc[cbk], d, qpc, 1);
+            d[0] = dqc[cbk];
+            idct4x4(d, rr);
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j)
+                    rec_uv[(y0 / 2 + 4 * by + i) * cw + 2 * (x0 / 2 + 4 * bx + j) + comp] =
+                        (uint8_t)clip255(predc_px(p, n, 4 * bx + j, 4 * by + i) + rr[i * 4 + j]);
+        }
+    }
+    m.cbp = (uint8_t)(cbp_l | ((any_ac ? 2 : (any_dc ? 1 : 0)) << 4));
+}
+
 void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pitch) {
     const Geometry g = geom_of(common_, cw_, ch_);
     const uint8_t* ref_y = rec_y_[cur_ ^ 1].data();
@@ -158,11 +312,13 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                     }
             int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
             int cbp = 0;
+            uint32_t satd = 0;
             for (int b = 0; b < 16; ++b) {
                 const int bx = kBlkX[b], by = kBlkY[b];
                 int x[16], zs[16], rr[16];
                 for (int i = 0; i < 4; ++i)
                     for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[(by * 4 + i) * 16 + bx * 4 + j];
+                satd += satd4x4(x);
                 const int nz = luma_block_inter(x, qp, zs, rr);
                 for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
                 m.nz_luma[by * 4 + bx] = (uint8_t)nz;
@@ -207,7 +363,26 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             }
             cbp |= (any_ac ? 2 : (any_dc ? 1 : 0)) << 4;
             m.cbp = (uint8_t)cbp;
+            m.cost = inter_cost(satd, frame_qp, mvx, mvy);
         }
+    // intra macroblocks in the P slice: open-loop decision against the inter cost, local-maximum
+    // selection (independent intra MBs), then their coding from the final inter reconstruction
+    // (the same selection and arithmetic as k_intra_analyze + k_intra_p)
+    if (!cfg_.intra_in_p) return;
+    const int nmb = g.mb_w * g.mb_h;
+    std::vector<int32_t> gain(nmb, 0);
+    std::vector<IntraDecision> dec(nmb);
+    for (int mbi = 0; mbi < nmb; ++mbi) {
+        if (!intra_candidate(mb_[mbi].cost)) continue;
+        dec[mbi] = analyze_intra_mb(g, sy, suv, pitch, mbi % g.mb_w, mbi / g.mb_w, g.mb_h, frame_qp);
+        gain[mbi] = intra_gain(dec[mbi].cost_luma, mb_[mbi].cost, frame_qp);
+    }
+    for (int mbi = 0; mbi < nmb; ++mbi)
+        if (intra_selected(gain.data(), g.mb_w, g.mb_h, mbi % g.mb_w, mbi / g.mb_w)) set_intra(mb_[mbi], dec[mbi], frame_qp);
+    for (int mbi = 0; mbi < nmb; ++mbi)
+        if (is_intra(mb_[mbi]))
+            code_intra_mb(g, sy, suv, pitch, rec_y, rec_uv, cw_, mbi % g.mb_w, mbi / g.mb_w, g.mb_h, mb_[mbi].qp,
+                          cfg_.chroma_qp_offset, mb_[mbi], coef_.data() + (size_t)mbi * kCoefStride);
 }
 
 void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
@@ -215,145 +390,21 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
     uint8_t* rec_y = rec_y_[cur_].data();
     uint8_t* rec_uv = rec_uv_[cur_].data();
     const int qp = frame_qp_();
-    const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
-    for (int mby = 0; mby < g.mb_h; ++mby) {
-        uint8_t left[32] = {0};
-        for (int mbx = 0; mbx < g.mb_w; ++mbx) {
-            const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
-            const bool have_left = mbx > 0;
-            MbInfo& m = mb_[mbi];
-            std::memset(&m, 0, sizeof m);
-            m.qp = (uint8_t)qp;
-            int dcl = 128;
-            if (have_left) {
-                int s = 0;
-                for (int i = 0; i < 16; ++i) s += left[i];
-                dcl = (s + 8) >> 4;
-            }
-            int sad_dc = 0, sad_h = 0;
-            for (int r = 0; r < 16; ++r)
-                for (int k = 0; k < 16; ++k) {
-                    const int sv = sy[(y0 + r) * pitch + x0 + k];
-                    sad_dc += std::abs(sv - dcl);
-                    sad_h += have_left ? std::abs(sv - left[r]) : 0;
-                }
-            const int lmode = (have_left && sad_h < sad_dc) ? 1 : 2;
-            int pred[384], res[384];
-            for (int r = 0; r < 16; ++r)
-                for (int k = 0; k < 16; ++k) {
-                    const int p = lmode == 1 ? left[r] : dcl;
-                    pred[r * 16 + k] = p;
-                    res[r * 16 + k] = sy[(y0 + r) * pitch + x0 + k] - p;
-                }
-            int pdc[2][2] = {{128, 128}, {128, 128}};  // [comp][upper/lower 4 rows]
-            if (have_left)
-                for (int comp = 0; comp < 2; ++comp)
-                    for (int h = 0; h < 2; ++h)
-                        pdc[comp][h] = (left[16 + comp * 8 + h * 4] + left[16 + comp * 8 + h * 4 + 1] +
-                                        left[16 + comp * 8 + h * 4 + 2] + left[16 + comp * 8 + h * 4 + 3] + 2) >> 2;
-            int sdc = 0, sh = 0;
-            for (int comp = 0; comp < 2; ++comp)
-                for (int r = 0; r < 8; ++r)
-                    for (int k = 0; k < 8; ++k) {
-                        const int s = suv[(y0 / 2 + r) * pitch + 2 * (x0 / 2 + k) + comp];
-                        sdc += std::abs(s - pdc[comp][r >> 2]);
-                        sh += have_left ? std::abs(s - left[16 + comp * 8 + r]) : 0;
-                    }
-            const int cmode = (have_left && sh < sdc) ? 1 : 0;
-            for (int comp = 0; comp < 2; ++comp)
-                for (int r = 0; r < 8; ++r)
-                    for (int k = 0; k < 8; ++k) {
-                        const int s = suv[(y0 / 2 + r) * pitch + 2 * (x0 / 2 + k) + comp];
-                        const int p = cmode == 1 ? left[16 + comp * 8 + r] : pdc[comp][r >> 2];
-                        pred[256 + comp * 64 + r * 8 + k] = p;
-                        res[256 + comp * 64 + r * 8 + k] = s - p;
-                    }
-            int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
-            int z[16][16], ldc[16];
-            bool luma_ac = false;
-            int nzl[16];
-            for (int b = 0; b < 16; ++b) {
-                const int bx = kBlkX[b], by = kBlkY[b];
-                int x[16], y[16];
-                for (int i = 0; i < 4; ++i)
-                    for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[(by * 4 + i) * 16 + bx * 4 + j];
-                fdct4x4(x, y);
-                ldc[by * 4 + bx] = y[0];
-                nzl[b] = quant4x4(y, z[b], qp, true, 1);
-                luma_ac |= nzl[b] > 0;
-                for (int k = 1; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)z[b][kZigzag4x4[k]];
-                mc[kCoefLuma + b * 16] = 0;
-            }
-            int zd[16], dq[16];
-            quant_dc_luma(ldc, zd, qp);
-            for (int k = 0; k < 16; ++k) mc[kCoefLumaDc + k] = (int16_t)zd[kZigzag4x4[k]];
-            dequant_dc_luma(zd, dq, qp);
-            for (int b = 0; b < 16; ++b) {
-                const int bx = kBlkX[b], by = kBlkY[b];
-                int d[16], rr[16];
-                if (luma_ac)
-                    dequant4x4(z[b], d, qp, 1);
-                else
-                    for (int i = 1; i < 16; ++i) d[i] = 0;
-                d[0] = dq[by * 4 + bx];
-                idct4x4(d, rr);
-                for (int i = 0; i < 4; ++i)
-                    for (int j = 0; j < 4; ++j) {
-                        const int v = clip255(pred[(by * 4 + i) * 16 + bx * 4 + j] + rr[i * 4 + j]);
-                        rec_y[(y0 + by * 4 + i) * cw_ + x0 + bx * 4 + j] = (uint8_t)v;
-                    }
-                m.nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nzl[b] : 0);
-            }
-            bool any_ac = false, any_dc = false;
-            for (int comp = 0; comp < 2; ++comp) {
-                int zc[4][16], dcin[4];
-                for (int cbk = 0; cbk < 4; ++cbk) {
-                    const int bx = cbk & 1, by = cbk >> 1;
-                    int x[16], y[16];
-                    for (int i = 0; i < 4; ++i)
-                        for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
-                    fdct4x4(x, y);
-                    dcin[cbk] = y[0];
-                    const int nz = quant4x4(y, zc[cbk], qpc, true, 1);
-                    for (int k = 1; k < 16; ++k)
-                        mc[kCoefChromaAc + (comp * 4 + cbk) * 16 + k] = (int16_t)zc[cbk][kZigzag4x4[k]];
-                    (comp ? m.nz_cr : m.nz_cb)[cbk] = (uint8_t)nz;
-                    any_ac |= nz > 0;
-                }
-                int zdc[4], dqc[4];
-                any_dc |= quant_dc_chroma(dcin, zdc, qpc, true) > 0;
-                for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zdc[i];
-                dequant_dc_chroma(zdc, dqc, qpc);
-                for (int cbk = 0; cbk < 4; ++cbk) {
-                    const int bx = cbk & 1, by = cbk >> 1;
-                    int d[16], rr[16];
-                    dequant4x4(zc[cbk], d, qpc, 1);
-                    d[0] = dqc[cbk];
-                    idct4x4(d, rr);
-                    const int xc = x0 / 2 + bx * 4, yc = y0 / 2 + by * 4;
-                    for (int i = 0; i < 4; ++i)
-                        for (int j = 0; j < 4; ++j)
-                            rec_uv[(yc + i) * cw_ + 2 * (xc + j) + comp] = (uint8_t)clip255(
-                                pred[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j] + rr[i * 4 + j]);
-                }
-            }
-            // left column for the next MB
-            for (int i = 0; i < 16; ++i) left[i] = rec_y[(y0 + i) * cw_ + x0 + 15];
-            for (int comp = 0; comp < 2; ++comp)
-                for (int i = 0; i < 8; ++i) left[16 + comp * 8 + i] = rec_uv[(y0 / 2 + i) * cw_ + 2 * (x0 / 2 + 7) + comp];
-            const int ccbp = any_ac ? 2 : (any_dc ? 1 : 0);
-            m.type = kMbI16x16;
-            m.cbp = (uint8_t)((luma_ac ? 15 : 0) | (ccbp << 4));
-            m.i16_mode = (uint8_t)lmode;
-            m.chroma_mode = (uint8_t)cmode;
-        }
+    const int rows = idr_slice_rows(g.mb_h);
+    for (int mbi = 0; mbi < g.mb_w * g.mb_h; ++mbi) {
+        MbInfo& m = mb_[mbi];
+        std::memset(&m, 0, sizeof m);
+        set_intra(m, analyze_intra_mb(g, sy, suv, pitch, mbi % g.mb_w, mbi / g.mb_w, rows, qp), qp);
     }
+    for (int mbi = 0; mbi < g.mb_w * g.mb_h; ++mbi)
+        code_intra_mb(g, sy, suv, pitch, rec_y, rec_uv, cw_, mbi % g.mb_w, mbi / g.mb_w, rows, qp, cfg_.chroma_qp_offset,
+                      mb_[mbi], coef_.data() + (size_t)mbi * kCoefStride);
 }
 
 void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& soff, std::vector<uint32_t>& slen) {
     const Geometry g = geom_of(common_, cw_, ch_);
     const bool idr = common_.cur_idr();
-    const int slice_rows = idr ? 1 : g.mb_h;
+    const int slice_rows = idr ? idr_slice_rows(g.mb_h) : g.mb_h;
     const int per_slice = slice_rows * g.mb_w;
     const int nmb = g.mb_w * g.mb_h;
     std::vector<uint32_t> words((size_t)nmb * kSlotWords / 4 + 4096);
@@ -380,7 +431,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
             }
             const int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
             int dqp = 0;
-            if (!idr && mb_[mbi].cbp != 0) {
+            if (!idr && carries_dqp(mb_[mbi])) {
                 dqp = qp_delta(mb_[mbi].qp, qp_pred);
                 qp_pred = mb_[mbi].qp;
             }

@@ -256,6 +256,12 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     b.out_bytes = (size_t)nmb * 768;
     HIP_CHECK(hipMalloc(&b.out_hdr, sizeof(OutHeader)));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * kSsePartStride));
+    HIP_CHECK(hipMalloc(&b.wave_prog, sizeof(int) * 4));
+    HIP_CHECK(hipMalloc(&b.mb_sse, sizeof(uint32_t) * 3 * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.intra_gain, sizeof(int32_t) * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.intra_cand, sizeof(int) * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.wave_line, sizeof(uint64_t) * (size_t)geom_.mb_h * geom_.coded_w / 2));
+    HIP_CHECK(hipMemsetAsync(b.wave_line, 0, sizeof(uint64_t) * (size_t)geom_.mb_h * geom_.coded_w / 2, stream_));
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
     std::memset(sl.host_out, 0, kOutPayloadOffset);
@@ -268,7 +274,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     DeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.unit_off,
                     (void*)b.skip_run, (void*)b.coded_list, (void*)b.coded_info, (void*)b.slice_info,
-                    (void*)b.out_hdr, (void*)b.sse_part})
+                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.wave_line, (void*)b.intra_gain, (void*)b.intra_cand})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);
@@ -289,8 +295,10 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     geom_.coded_h = geom_.mb_h * 16;
     geom_.pitch = (geom_.coded_w + 255) & ~255;
     if (geom_.mb_h > kMaxSlices) throw std::invalid_argument("picture too tall");
+    if (geom_.mb_w > 512) throw std::invalid_argument("picture too wide (k_intra_wave stages <= 512 MBs per row)");
     const int nmb = geom_.mb_w * geom_.mb_h;
-    if ((nmb + 3) / 4 > kSsePartStride) throw std::invalid_argument("frame too large for the distortion partials");
+    if ((nmb + 3) / 4 + geom_.mb_h > kSsePartStride)
+        throw std::invalid_argument("frame too large for the distortion partials");
     const size_t ysz = (size_t)geom_.pitch * geom_.coded_h, uvsz = ysz / 2;
     for (int i = 0; i < 2; ++i) {
         HIP_CHECK(hipMalloc(&rec_y_[i], ysz));
@@ -329,6 +337,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
         launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
         launch_me(geom_, sl.buf, src_y, stream_);
         launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
+        if (cfg_.intra_in_p) launch_intra_in_p(geom_, sl.buf, src_y, src_uv, stream_);
     }
     hipStream_t es = stream_;
     if (stream_e_) {  // entropy of this frame overlaps the analysis of the next one
@@ -350,8 +359,8 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.frame_num = common_.cur_frame_num();
     f.idr_pic_id = common_.cur_idr_pic_id();
     f.qp = qp;
-    f.slice_rows = idr ? 1 : geom_.mb_h;
-    f.num_slices = idr ? geom_.mb_h : 1;
+    f.slice_rows = idr ? idr_slice_rows(geom_.mb_h) : geom_.mb_h;
+    f.num_slices = (geom_.mb_h + f.slice_rows - 1) / f.slice_rows;
     f.search_range = me_range(cfg_.search_range);
     f.subpel = cfg_.subpel;
     f.deblock_off = 1;
@@ -361,6 +370,8 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     const size_t org = (size_t)kHpelPad * hp_pitch_ + kHpelPad;
     f.hp_pitch = hp_pitch_;
     f.aq = cfg_.aq;
+    f.intra_in_p = cfg_.intra_in_p;
+    f.frame_tag = (int32_t)++frame_tag_;  // tags start at 1: the zeroed line buffer never matches
     f.hp_f = hp_[0] + org;
     f.hp_h = hp_[1] + org;
     f.hp_v = hp_[2] + org;

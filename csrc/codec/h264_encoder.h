@@ -35,6 +35,8 @@ struct EncoderConfig {
     int chroma_qp_offset = 0;
     int aq = 1;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta)
     int deblock = 1;          // HEVC in-loop deblocking filter (the H.264 encoder always disables it)
+    int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
+                              // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
     int pipeline_depth = 1;   // GPU frames in flight: 2 overlaps frame n's entropy coding with
                               // frame n+1's analysis on a second HIP stream (rate control lags a frame)
@@ -211,6 +213,7 @@ class GpuH264Encoder final : public VideoEncoder {
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
+    uint32_t frame_tag_ = 0;
     std::vector<uint8_t> au_;
     FrameStats stats_;
 };

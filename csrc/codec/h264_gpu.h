@@ -1,14 +1,20 @@
 // Device data layout and host API of the HIP H.264 encoder.
 //
 // Per-frame kernel chain (all on one HIP stream, graph-capturable):
-//   P frame: k_me_full -> k_inter_encode -> k_cavlc -> k_scan -> k_pack
-//   I frame: k_intra_rows                 -> k_cavlc -> k_scan -> k_pack
+//   P frame: k_hpel -> k_me_full -> k_inter_encode -> k_intra_analyze -> k_intra_wave
+//            -> k_cavlc -> k_scan -> k_pack
+//   I frame: k_intra_analyze -> k_intra_wave -> k_cavlc -> k_scan -> k_pack
+// k_intra_analyze decides every macroblock's intra modes open-loop (SATD against predictions
+// from source neighbours, fully parallel); k_intra_wave reconstructs the intra macroblocks
+// closed-loop in a diagonal wavefront (one luma and one chroma wave per MB row).
 // k_pack writes the payload straight into pinned host memory (zero-copy).
 // Only the slice payloads (RBSP, byte aligned) leave the GPU; the host adds start
 // codes, NAL headers and emulation-prevention bytes (h264_encoder.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#define MXHD_GPU __host__ __device__ __forceinline__
 
 namespace mx {
 namespace h264 {
@@ -20,7 +26,7 @@ constexpr int kCoefLumaDc = 256;  // [16 scan]
 constexpr int kCoefChromaDc = 272;  // [2][4]
 constexpr int kCoefChromaAc = 280;  // [2][4 blk][16 scan], index 0 unused
 
-enum MbType : uint8_t { kMbP16x16 = 0, kMbI16x16 = 1 };
+enum MbType : uint8_t { kMbP16x16 = 0, kMbI16x16 = 1, kMbI4x4 = 2 };
 
 struct MbInfo {
     int16_t mvx, mvy;  // quarter-pel
@@ -33,9 +39,16 @@ struct MbInfo {
     uint8_t nz_cr[4];
     uint8_t skip;  // set by k_cavlc
     uint8_t qp;    // macroblock QP (frame QP + adaptive-quantisation offset)
-    uint8_t pad[2];
+    uint8_t cbp_c; // chroma cbp of an intra MB, written by the chroma wave of k_intra_wave / k_intra_p
+    uint8_t itype; // P pictures: the intra type k_intra_analyze decided (applied if k_intra_p selects the MB)
+    uint8_t i4[8];     // Intra4x4 prediction modes, two per byte, raster block order
+    uint32_t cost;     // P pictures: inter luma SATD cost (+ mv rate), for the intra decision
 };
-static_assert(sizeof(MbInfo) == 36, "MbInfo layout");
+static_assert(sizeof(MbInfo) == 48, "MbInfo layout");
+
+MXHD_GPU bool is_intra(const MbInfo& m) { return m.type != kMbP16x16; }
+// mb_qp_delta present: Intra16x16 always, other macroblocks when they carry residual.
+MXHD_GPU bool carries_dqp(const MbInfo& m) { return m.type == kMbI16x16 || m.cbp != 0; }
 
 // Per-frame state, written by the host into pinned memory and copied to the device at
 // the start of every frame (one memcpy node), so a captured graph replays correctly.
@@ -58,6 +71,8 @@ struct FrameState {
     int32_t log2_max_frame_num;
     int32_t hp_pitch;  // pitch of the padded half-pel planes
     int32_t aq;        // adaptive quantisation on/off (P frames)
+    int32_t intra_in_p;  // P frames: k_intra_analyze / k_intra_wave run (distortion deltas included)
+    int32_t frame_tag;   // nonzero, new every frame: validity tag of k_intra_wave's line buffer words
     // padded reference planes (origin at picture (0,0), valid for x,y in [-kHpelPad, size+kHpelPad))
     const uint8_t* hp_f;  // full-sample (edge-replicated)
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
@@ -110,6 +125,11 @@ struct DeviceBuffers {
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
     unsigned long long* sse_part;       // [3 * kSsePartStride] distortion partials
+    int* wave_prog;         // [0] k_intra_wave row ticket, [1] intra candidate count
+    uint64_t* wave_line;    // [mb_h * coded_w / 2] k_intra_wave: tagged bottom sample lines of intra MBs
+    int32_t* intra_gain;    // [nmb] P frames: gain of switching each MB to intra (0 = stays inter)
+    int* intra_cand;        // [nmb] P frames: MBs with a positive gain (count in wave_prog[1])
+    uint32_t* mb_sse;       // [3 * nmb] P frames: per-MB inter distortion (replaced for intra MBs)
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.
@@ -126,6 +146,10 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
 void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
                  hipStream_t stream, const FrameState* publish = nullptr);
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
+// P pictures, after launch_inter: open-loop intra analysis of every MB (intra vs inter) and the
+// closed-loop reconstruction of the MBs that switched to intra.
+void launch_intra_in_p(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                       hipStream_t stream);
 
 }  // namespace h264
 }  // namespace mx

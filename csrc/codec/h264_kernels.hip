@@ -8,8 +8,10 @@
 //  * k_inter_encode one wave per macroblock (4 per workgroup): motion compensation
 //                   (6-tap qpel / bilinear chroma), 4x4 integer transform, quantisation,
 //                   reconstruction into the reference frame.  Fully parallel over MBs.
-//  * k_intra_rows   one wave per MB row (slice per row): Intra16x16 H/DC with a serial
-//                   left-to-right dependency held in LDS.
+//  * k_intra_analyze one wave per MB: open-loop Intra4x4 / Intra16x16 / chroma mode costs
+//                   (SATD vs source-neighbour predictions) and the intra / inter decision.
+//  * k_intra_wave   one workgroup per MB row (luma wave + chroma wave): closed-loop coding
+//                   of the intra MBs in a diagonal wavefront with per-row progress flags.
 //  * k_cavlc        one wave per macroblock: lane 0 codes the MB header (P_Skip decision,
 //                   median mv prediction, cbp), lanes 1..27 code one residual block each;
 //                   a wave prefix-sum places every lane's bits in an LDS slot.
@@ -17,6 +19,8 @@
 //  * k_pack         one thread per output word gathers the overlapping header / MB /
 //                   trailer bits and stores the word straight into pinned host memory.
 #include <hip/hip_runtime.h>
+
+#include <cstddef>
 
 #include "h264_core.h"
 #include "h264_gpu.h"
@@ -421,7 +425,8 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
 __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameState* __restrict__ fs,
                                                        const uint8_t* __restrict__ src_y,
                                                        const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
-                                                       int16_t* __restrict__ coef) {
+                                                       int16_t* __restrict__ coef, uint32_t* __restrict__ mb_sse,
+                                                       int* __restrict__ wave_prog) {
     __shared__ uint8_t pred[4][384];
     __shared__ int16_t res[4][384];
     __shared__ int cdc[4][8];
@@ -431,6 +436,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     const int nmb = g.mb_w * g.mb_h;
     const int bid = blockIdx.x;
     const int mbi = bid * 4 + wave;
+    if (bid == 0 && threadIdx.x == 0) wave_prog[1] = 0;  // k_intra_analyze's candidate list (next kernel)
     const bool valid = mbi < nmb;
     const int mbx = valid ? mbi % g.mb_w : 0, mby = valid ? mbi / g.mb_w : 0;
     const int x0 = mbx * 16, y0 = mby * 16;
@@ -467,12 +473,14 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     int z[16];
     int nz = 0;
     int sse_y = 0, sse_c = 0;
+    uint32_t satd = 0;
     int16_t* mc = coef + (size_t)(valid ? mbi : 0) * kCoefStride;
     if (valid && lane < 16) {
         const int b = lane, bx = kBlkX[b], by = kBlkY[b];
         int x[16];
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[wave][(by * 4 + i) * 16 + bx * 4 + j];
+        satd = satd4x4(x);
         int zs[16], r[16];
         nz = luma_block_inter(x, qp, zs, r);
         for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
@@ -529,11 +537,14 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
                 fs->rec_uv[(yc + i) * g.pitch + 2 * (xc + j) + comp] = (uint8_t)v;
             }
     }
+    const uint32_t satd_mb = (uint32_t)wave_sum((int)satd);
     {
         // Y on lanes 0..15, U on 16..19, V on 20..23
         const int sy = wave_sum(sse_y);
         const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
         const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
+        if (valid && fs->intra_in_p && lane < 3)  // per-MB copy: replaced if the MB switches to intra
+            mb_sse[lane * nmb + mbi] = (uint32_t)(lane == 0 ? sy : (lane == 1 ? su : sv));
         __shared__ uint32_t part[3][4];
         if (lane == 0) {
             part[0][wave] = valid ? (uint32_t)sy : 0u;
@@ -561,134 +572,322 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         m.qp = (uint8_t)qp;
         m.i16_mode = 0;
         m.chroma_mode = 0;
+        m.cost = inter_cost(satd_mb, fs->qp, mvx, mvy);
     }
 }
 
-// ------------------------------------------------------------------ intra (I slices)
-// One wave per MB row; every row is its own slice, so the only neighbour is the left MB.
-__global__ __launch_bounds__(64) void k_intra_rows(Geometry g, StateArg sa,
-                                                    const uint8_t* __restrict__ src_y,
-                                                    const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
-                                                    int16_t* __restrict__ coef) {
-    __shared__ uint8_t left[32];  // 16 luma, 8 cb, 8 cr: right column of the previous MB
-    __shared__ uint8_t pred[384];
-    __shared__ int16_t res[384];
-    __shared__ int ldc[16];
-    __shared__ int cdc[8];
-    __shared__ int cdc_nz[2];
-    __shared__ int modes[2];
+// ------------------------------------------------------------------ intra analysis
+// raster block index -> blkIdx
+__constant__ uint8_t kRasterToBlk[16] = {0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15};
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
+// One wave per macroblock, fully parallel: SATD of the 9 Intra4x4 modes of the 16 blocks
+// (144 block/mode pairs over 64 lanes), of the 4 Intra16x16 modes (one 4x4 block per lane)
+// and of the 4 chroma modes, all predicted from SOURCE neighbours (open loop), then the
+// shared decide_intra() on lane 0.  IDR: every MB takes its decision; P: only MBs whose
+// intra cost beats the inter cost k_inter_encode left in MbInfo::cost.  Block 0 also resets
+// k_intra_wave's progress counters and row ticket.
+constexpr int kLT = 24;  // luma LDS tile pitch: x -1 .. 19 at columns 0 .. 20 (rows y -1 .. 15)
+constexpr int kCT = 10;  // chroma LDS tile pitch (per plane): x -1 .. 7 at columns 0 .. 8
+constexpr int kCTI = 20; // interleaved chroma LDS tile pitch: (x -1 .. 8) x 2 planes
+
+__global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, const uint8_t* __restrict__ src_y,
+                                                       const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
+                                                       int* __restrict__ wave_prog, int32_t* __restrict__ gain,
+                                                       int* __restrict__ cand) {
+    __shared__ IntraCosts costs[4];
+    __shared__ uint8_t ltile[4][17][kLT];   // source luma: MB + one-sample border + top-right
+    __shared__ uint8_t ctile[4][9][kCTI];   // source chroma (interleaved): MB + one-sample border
     publish_state(sa);
     const FrameState* fs = &state_of(sa);
-    const int mby = blockIdx.x, lane = threadIdx.x;
-    const int qp = fs->qp;
-    const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
-    const int y0 = mby * 16;
-
-    unsigned long long row_sse[3] = {0, 0, 0};
-    for (int mbx = 0; mbx < g.mb_w; ++mbx) {
-        const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16;
-        const bool have_left = mbx > 0;
-        // ---- mode decision (SAD) and prediction
-        const int r = lane >> 2, c0 = (lane & 3) * 4;
-        const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
-        int dcl = 128;
-        if (have_left) {
-            int s = 0;
-            for (int i = 0; i < 16; ++i) s += left[i];
-            dcl = (s + 8) >> 4;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) wave_prog[0] = 0;  // k_intra_wave's row ticket
+        if (!fs->idr)  // k_intra_p's per-row distortion deltas (atomically accumulated)
+            for (int i = threadIdx.x; i < 3 * g.mb_h; i += 256)
+                fs->sse_part[(i / g.mb_h) * kSsePartStride + (g.mb_w * g.mb_h + 3) / 4 + i % g.mb_h] = 0;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mbi = blockIdx.x * 4 + wave;
+    if (mbi >= g.mb_w * g.mb_h) return;  // whole wave; no workgroup barriers below
+    if (!fs->idr && !intra_candidate(mbs[mbi].cost)) {  // well-predicted: stays inter
+        if (lane == 0) gain[mbi] = 0;
+        return;
+    }
+    const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
+    const int x0 = mbx * 16, y0 = mby * 16;
+    const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
+    // stage the source footprint (samples outside the picture are never read: availability)
+    for (int i = lane; i < 17 * 21; i += 64) {
+        const int r = i / 21, cx = i - r * 21, x = x0 - 1 + cx, y = y0 - 1 + r;
+        ltile[wave][r][cx] = (x >= 0 && y >= 0 && x < g.coded_w) ? src_y[y * g.pitch + x] : 0;
+    }
+    for (int i = lane; i < 9 * 18; i += 64) {
+        const int r = i / 18, bx = i - r * 18, x = x0 - 2 + bx, y = y0 / 2 - 1 + r;
+        ctile[wave][r][bx] = (x >= 0 && y >= 0) ? src_uv[y * g.pitch + x] : 0;
+    }
+    wave_sync_lds();
+    const uint8_t* sy = &ltile[wave][1][1];
+    const uint8_t* suv = &ctile[wave][1][2];
+    IntraCosts& c = costs[wave];
+    // lane = (4x4 block, row): every mode is evaluated by the whole wave at once (a per-lane
+    // mode would diverge the prediction switch 9 ways), SATD as row Hadamards in registers plus
+    // a column butterfly over the block's 4 lanes; the same integers as satd4x4().
+    const int rb = lane >> 2, r = lane & 3, bx = rb & 3, by = rb >> 2;
+    auto satd_quad = [&](int d0, int d1, int d2, int d3) -> uint32_t {
+        int t[4] = {d0 + d1 + d2 + d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3, d0 - d1 + d2 - d3};
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int v = t[j];
+            int o = __shfl_xor(v, 1, 64);
+            v = (r & 1) ? o - v : v + o;
+            o = __shfl_xor(v, 2, 64);
+            v = (r & 2) ? o - v : v + o;
+            sum += (uint32_t)(v < 0 ? -v : v);
         }
-        int sad_dc = 0, sad_h = 0;
-        for (int k = 0; k < 4; ++k) {
-            const int sv = (sw >> (8 * k)) & 0xff;
-            sad_dc += abs(sv - dcl);
-            sad_h += have_left ? abs(sv - left[r]) : 0;
+        sum += __shfl_xor(sum, 1, 64);
+        sum += __shfl_xor(sum, 2, 64);
+        return (sum + 1) >> 1;  // satd of the block, in all 4 lanes
+    };
+    {
+        const Nb4 n = nb4_from_plane(sy, kLT, 0, 0, bx, by, av.left, av.top, av.topright, av.topleft);
+        int sv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sv[j] = sy[(4 * by + r) * kLT + 4 * bx + j];
+        for (int m = 0; m < 9; ++m) {
+            const bool ok = i4_mode_ok(m, n);
+            int d[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[j] = ok ? sv[j] - pred4x4_px(m, n, j, r) : 0;
+            const uint32_t t = satd_quad(d[0], d[1], d[2], d[3]);
+            if (r == 0) c.c4[kRasterToBlk[rb]][m] = ok ? t : kCostInf;
         }
-        sad_dc = wave_sum(sad_dc);
-        sad_h = wave_sum(sad_h);
-        const int lmode = (have_left && sad_h < sad_dc) ? 1 : 2;  // 1 = horizontal, 2 = DC
-        for (int k = 0; k < 4; ++k) {
-            const int sv = (sw >> (8 * k)) & 0xff;
-            const int p = (lmode == 1) ? left[r] : dcl;
-            pred[r * 16 + c0 + k] = (uint8_t)p;
-            res[r * 16 + c0 + k] = (int16_t)(sv - p);
-        }
-        // chroma: DC (0) or horizontal (1); with no top neighbour DC uses the left column
-        const int cr_ = lane >> 3, cc = lane & 7;
-        const int xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
-        int sdc = 0, sh = 0;
-        int pdc[2];
-        for (int comp = 0; comp < 2; ++comp) {
-            int d = 128;
-            if (have_left) {
-                const int rb = (cr_ >> 2) * 4;
-                d = (left[16 + comp * 8 + rb] + left[16 + comp * 8 + rb + 1] + left[16 + comp * 8 + rb + 2] +
-                     left[16 + comp * 8 + rb + 3] + 2) >> 2;
+    }
+    {  // Intra16x16: 4 modes, all 16 blocks at once, summed over the wave
+        const NbMb n = nbmb_from_plane(sy, kLT, 0, 0, 16, 1, 0, av.left, av.top, av.topleft);
+        for (int m = 0; m < 4; ++m) {
+            const bool ok = i16_mode_ok(m, n);  // wave-uniform
+            uint32_t t = 0;
+            if (ok) {
+                const PredMb p = prep_i16(m, n);
+                int d[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    d[j] = (int)sy[(4 * by + r) * kLT + 4 * bx + j] - pred16_px(p, n, 4 * bx + j, 4 * by + r);
+                t = satd_quad(d[0], d[1], d[2], d[3]);
+                t = r == 0 ? t : 0u;
+                for (int o = 4; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
             }
-            pdc[comp] = d;
-            const int s = src_uv[yc * g.pitch + 2 * xc + comp];
-            sdc += abs(s - d);
-            sh += have_left ? abs(s - left[16 + comp * 8 + cr_]) : 0;
+            if (lane == 0) c.c16[m] = ok ? t : kCostInf;
         }
-        sdc = wave_sum(sdc);
-        sh = wave_sum(sh);
-        const int cmode = (have_left && sh < sdc) ? 1 : 0;
-        for (int comp = 0; comp < 2; ++comp) {
-            const int s = src_uv[yc * g.pitch + 2 * xc + comp];
-            const int p = cmode == 1 ? left[16 + comp * 8 + cr_] : pdc[comp];
-            pred[256 + comp * 64 + cr_ * 8 + cc] = (uint8_t)p;
-            res[256 + comp * 64 + cr_ * 8 + cc] = (int16_t)(s - p);
+    }
+    {  // chroma: 4 modes; lanes 0..31 = (component, 4x4 block, row), lanes 32..63 idle
+        const int comp = (lane >> 4) & 1, cb = (lane >> 2) & 3, cbx = cb & 1, cby = cb >> 1;
+        const NbMb n = nbmb_from_plane(suv, kCTI, 0, 0, 8, 2, comp, av.left, av.top, av.topleft);
+        for (int m = 0; m < 4; ++m) {
+            const bool ok = chroma_mode_ok(m, n);  // wave-uniform (same availability for both planes)
+            uint32_t t = 0;
+            if (ok) {
+                const PredMb p = prep_chroma(m, n);
+                int d[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    d[j] = lane < 32 ? (int)suv[(4 * cby + r) * kCTI + 2 * (4 * cbx + j) + comp] -
+                                           predc_px(p, n, 4 * cbx + j, 4 * cby + r)
+                                     : 0;
+                t = satd_quad(d[0], d[1], d[2], d[3]);
+                t = (r == 0 && lane < 32) ? t : 0u;
+                for (int o = 4; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+            }
+            if (lane == 0) c.cc[m] = ok ? t : kCostInf;
         }
-        __syncthreads();
-        // ---- transform + quant
-        int z[16];
-        int nz = 0;
-        int16_t* mc = coef + (size_t)mbi * kCoefStride;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        const IntraDecision d = decide_intra(c, fs->qp);
+        MbInfo& m = mbs[mbi];
+        const int32_t gn = fs->idr ? 1 : intra_gain(d.cost_luma, m.cost, fs->qp);
+        if (!fs->idr) {
+            gain[mbi] = gn;
+            if (gn > 0) cand[atomicAdd(&wave_prog[1], 1)] = mbi;  // k_intra_p's work list
+        }
+        if (gn > 0) {  // IDR: the decision; P: a pending decision, applied by k_intra_p if selected
+            const int qp = fs->qp;
+            if (fs->idr)
+                m.type = (uint8_t)d.type;
+            else
+                m.itype = (uint8_t)d.type;
+            m.i16_mode = (uint8_t)d.i16_mode;
+            m.chroma_mode = (uint8_t)d.chroma_mode;
+            uint8_t md[8];
+            for (int rb = 0; rb < 16; rb += 2) md[rb >> 1] = (uint8_t)(d.i4[rb] | (d.i4[rb + 1] << 4));
+            for (int k = 0; k < 8; ++k) m.i4[k] = md[k];
+            if (fs->idr) {
+                m.qp = (uint8_t)qp;
+                m.mvx = 0;
+                m.mvy = 0;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ intra reconstruction
+// Closed-loop coding of the intra macroblocks in a diagonal wavefront.  One workgroup per MB
+// row (row order taken from a ticket counter, so a row only ever waits on rows that are
+// already running); wave 0 codes luma, wave 1 chroma -- the two planes' intra predictions
+// are independent, so they run as two wavefronts.  A macroblock waits until the row above
+// (same slice) has finished the macroblock above-right (per-plane progress counters,
+// agent-scope release / acquire).  Neighbour samples are staged in LDS tiles with a one-
+// sample border; the prediction helpers read them through the same plane-accessors as the
+// CPU encoder, so decisions and reconstructions are bit-identical.
+//  * Intra4x4: the 16 blocks in 10 dependency steps (block (bx,by) at step bx + 2*by, up to
+//    two blocks per step), one pixel per lane; the 4x4 transforms run as row / column
+//    butterflies over lane shuffles within each 16-lane block group.
+//  * Intra16x16 and chroma: one 4x4 block per lane, DC transforms on one lane.
+// In P pictures the waves skip inter macroblocks (final since k_inter_encode) and replace the
+// inter distortion of the switched macroblocks by a per-row delta partial.
+
+
+// Cross-workgroup hand-off between MB rows.  The 8 XCDs' L2 caches are not coherent with each
+// other, so an agent-scope release / acquire fence writes back / invalidates the whole L2 --
+// ~20 us per macroblock when the first version fenced every MB (profiles/r02_l), and a
+// progress counter behind a store-completion wait still cost a memory round trip per MB on
+// the critical path (profiles/r02_n).  Instead the data carries its own flag: every dword of
+// an intra MB's bottom sample line is stored as one 64-bit agent-coherent (L2-bypassing)
+// atomic {frame tag, 4 samples}; a reader polls exactly the words it needs until they carry
+// this frame's tag.  No fences, no counters, and the writer never waits.
+__device__ __forceinline__ uint64_t load_line(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_line(uint64_t* p, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(p, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 4x4 forward / inverse core transform of one block held one coefficient per lane (lane
+// r*4 + c of a 16-lane group); the same integer butterflies as fdct4x4 / idct4x4.
+__device__ __forceinline__ int fdct_lane(int x, int base, int r, int c) {
+    const int x0 = __shfl(x, base + r * 4 + 0, 64), x1 = __shfl(x, base + r * 4 + 1, 64);
+    const int x2 = __shfl(x, base + r * 4 + 2, 64), x3 = __shfl(x, base + r * 4 + 3, 64);
+    const int s03 = x0 + x3, d03 = x0 - x3, s12 = x1 + x2, d12 = x1 - x2;
+    const int t = c == 0 ? s03 + s12 : c == 1 ? 2 * d03 + d12 : c == 2 ? s03 - s12 : d03 - 2 * d12;
+    const int t0 = __shfl(t, base + 0 * 4 + c, 64), t1 = __shfl(t, base + 1 * 4 + c, 64);
+    const int t2 = __shfl(t, base + 2 * 4 + c, 64), t3 = __shfl(t, base + 3 * 4 + c, 64);
+    const int u03 = t0 + t3, e03 = t0 - t3, u12 = t1 + t2, e12 = t1 - t2;
+    return r == 0 ? u03 + u12 : r == 1 ? 2 * e03 + e12 : r == 2 ? u03 - u12 : e03 - 2 * e12;
+}
+__device__ __forceinline__ int idct_lane(int d, int base, int r, int c) {
+    const int d0 = __shfl(d, base + r * 4 + 0, 64), d1 = __shfl(d, base + r * 4 + 1, 64);
+    const int d2 = __shfl(d, base + r * 4 + 2, 64), d3 = __shfl(d, base + r * 4 + 3, 64);
+    const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+    const int f = c == 0 ? e0 + e3 : c == 1 ? e1 + e2 : c == 2 ? e1 - e2 : e0 - e3;
+    const int f0 = __shfl(f, base + 0 * 4 + c, 64), f1 = __shfl(f, base + 1 * 4 + c, 64);
+    const int f2 = __shfl(f, base + 2 * 4 + c, 64), f3 = __shfl(f, base + 3 * 4 + c, 64);
+    const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
+    const int v = r == 0 ? g0 + g3 : r == 1 ? g1 + g2 : r == 2 ? g1 - g2 : g0 - g3;
+    return (v + 32) >> 6;
+}
+
+// Intra4x4 schedule: blocks (raster index by*4+bx) of each of the 10 dependency steps.
+__constant__ int8_t kI4Step[10][2] = {{0, -1}, {1, -1}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {14, -1}, {15, -1}};
+
+// Per-MB fields the reconstruction needs, read once (prefetched a macroblock ahead).
+struct MbFields {
+    int type, qp, i16_mode, chroma_mode;
+    uint32_t i4lo, i4hi;  // Intra4x4 modes, nibbles in raster block order
+    __device__ int i4(int rb) const { return (int)(((rb < 8 ? i4lo : i4hi) >> (4 * (rb & 7))) & 15u); }
+};
+__device__ __forceinline__ MbFields load_fields(const MbInfo* m) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(m);  // MbInfo: 48 B, dword aligned
+    const uint32_t d1 = w[1], d8 = w[8], d9 = w[9], d10 = w[10];
+    MbFields f;
+    f.type = (int)(d1 & 0xff);
+    f.i16_mode = (int)((d1 >> 16) & 0xff);
+    f.chroma_mode = (int)(d1 >> 24);
+    f.qp = (int)((d8 >> 8) & 0xff);
+    f.i4lo = d9;
+    f.i4hi = d10;
+    return f;
+}
+static_assert(offsetof(MbInfo, type) == 4 && offsetof(MbInfo, i16_mode) == 6 && offsetof(MbInfo, chroma_mode) == 7 &&
+                  offsetof(MbInfo, qp) == 33 && offsetof(MbInfo, i4) == 36,
+              "load_fields() layout");
+
+// ls: the macroblock's source luma in LDS (16 x 16, pitch 16).
+__device__ void intra_luma_mb(const Geometry& g, const MbFields& f, const uint8_t* ls, MbInfo& m,
+                              int16_t* __restrict__ mc, int mbx, int mby, const Avail& av, uint8_t (*lt)[kLT],
+                              int* ldc, int lane, uint32_t& sse) {
+    const int x0 = mbx * 16, y0 = mby * 16;
+    const int qp = f.qp;
+    const uint8_t* tile = &lt[1][1];
+    int cbp_l = 0;
+    if (f.type == kMbI4x4) {
+        const int grp = lane >> 4, base = grp << 4, r = (lane >> 2) & 3, c = lane & 3, i = r * 4 + c;
+        const int qm = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
+        for (int t = 0; t < 10; ++t) {
+            const int rb = lane < 32 ? kI4Step[t][grp] : -1;
+            int nzb = 0;
+            if (rb >= 0) {
+                const int bx = rb & 3, by = rb >> 2;
+                const Nb4 n = nb4_from_plane(tile, kLT, 0, 0, bx, by, av.left, av.top, av.topright, av.topleft);
+                const int pred = pred4x4_px(f.i4(rb), n, c, r);
+                const int xs = x0 + 4 * bx + c, ys = y0 + 4 * by + r;
+                const int sv = ls[(4 * by + r) * 16 + 4 * bx + c];
+                const int res = sv - pred;
+                const int y = fdct_lane(res, base, r, c);
+                const int a = y < 0 ? -y : y;
+                int q = (int)(((int64_t)a * kQuantMF[qm][kPosClass[i]] + fq) >> qbits);
+                q = q > kMaxLevel ? kMaxLevel : q;
+                const int z = y < 0 ? -q : q;
+                const unsigned long long bal = __ballot(z != 0);
+                nzb = __popcll((bal >> base) & 0xffffull);
+                mc[kCoefLuma + kRasterToBlk[rb] * 16 + kZigzagInv4x4[i]] = (int16_t)z;
+                const int d = z * kDequantV[qm][kPosClass[i]] * (1 << (qp / 6));
+                const int rec = clip255(pred + idct_lane(d, base, r, c));
+                lt[1 + 4 * by + r][1 + 4 * bx + c] = (uint8_t)rec;
+                const int e = sv - rec;
+                sse += (xs < g.width && ys < g.height) ? (uint32_t)(e * e) : 0u;
+                if (i == 0) {
+                    m.nz_luma[rb] = (uint8_t)nzb;
+                }
+            }
+            const unsigned long long any = __ballot(rb >= 0 && i == 0 && nzb > 0);
+            for (int gq = 0; gq < 2; ++gq)
+                if ((any >> (16 * gq)) & 1ull) cbp_l |= 1 << (kRasterToBlk[kI4Step[t][gq]] >> 2);
+            wave_sync_lds();
+        }
+    } else {  // Intra16x16: lane b (blkIdx) < 16 codes one 4x4 block
+        const NbMb n = nbmb_from_plane(tile, kLT, 0, 0, 16, 1, 0, av.left, av.top, av.topleft);
+        const PredMb p = prep_i16(f.i16_mode, n);
+        int z[16], nz = 0;
+        const int b = lane, bx = kBlkX[b & 15], by = kBlkY[b & 15];
         if (lane < 16) {
-            const int b = lane, bx = kBlkX[b], by = kBlkY[b];
             int x[16], y[16];
             for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[(by * 4 + i) * 16 + bx * 4 + j];
+                for (int j = 0; j < 4; ++j)
+                    x[i * 4 + j] = (int)ls[(4 * by + i) * 16 + 4 * bx + j] - pred16_px(p, n, 4 * bx + j, 4 * by + i);
             fdct4x4(x, y);
             ldc[by * 4 + bx] = y[0];
             nz = quant4x4(y, z, qp, true, 1);
             for (int k = 1; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)z[kZigzag4x4[k]];
             mc[kCoefLuma + b * 16] = 0;
-        } else if (lane < 24) {
-            const int comp = (lane - 16) >> 2, cb = (lane - 16) & 3, bx = cb & 1, by = cb >> 1;
-            int x[16], y[16];
-            for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
-            fdct4x4(x, y);
-            cdc[comp * 4 + cb] = y[0];
-            nz = quant4x4(y, z, qpc, true, 1);
-            for (int k = 1; k < 16; ++k) mc[kCoefChromaAc + (comp * 4 + cb) * 16 + k] = (int16_t)z[kZigzag4x4[k]];
         }
-        __syncthreads();
+        wave_sync_lds();
         if (lane == 0) {
             int zd[16], dq[16];
             quant_dc_luma(ldc, zd, qp);
             for (int k = 0; k < 16; ++k) mc[kCoefLumaDc + k] = (int16_t)zd[kZigzag4x4[k]];
             dequant_dc_luma(zd, dq, qp);
             for (int k = 0; k < 16; ++k) ldc[k] = dq[k];
-        } else if (lane == 16 || lane == 20) {
-            const int comp = (lane - 16) >> 2;
-            int in[4], zd[4], dq[4];
-            for (int i = 0; i < 4; ++i) in[i] = cdc[comp * 4 + i];
-            const int n = quant_dc_chroma(in, zd, qpc, true);
-            for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zd[i];
-            dequant_dc_chroma(zd, dq, qpc);
-            for (int i = 0; i < 4; ++i) cdc[comp * 4 + i] = dq[i];
-            cdc_nz[comp] = n;
         }
-        __syncthreads();
-        const unsigned long long luma_mask = __ballot(lane < 16 && nz > 0);
-        const unsigned long long chroma_mask = __ballot(lane >= 16 && lane < 24 && nz > 0);
-        const bool luma_ac = luma_mask != 0;
-        int sse_y = 0, sse_c = 0;
-        // ---- reconstruction
+        wave_sync_lds();
+        const bool luma_ac = __ballot(lane < 16 && nz > 0) != 0;
         if (lane < 16) {
-            const int b = lane, bx = kBlkX[b], by = kBlkY[b];
             int d[16], rr[16];
             if (luma_ac) {
                 dequant4x4(z, d, qp, 1);
@@ -697,62 +896,351 @@ __global__ __launch_bounds__(64) void k_intra_rows(Geometry g, StateArg sa,
             }
             d[0] = ldc[by * 4 + bx];
             idct4x4(d, rr);
-            for (int i = 0; i < 4; ++i) {
-                uint32_t packed = 0;
-                const bool vis = x0 + bx * 4 < g.width && (y0 + by * 4 + i) < g.height;
-                for (int j = 0; j < 4; ++j) {
-                    const int o = (by * 4 + i) * 16 + bx * 4 + j;
-                    const int v = clip255(pred[o] + rr[i * 4 + j]);
-                    const int e = pred[o] + res[o] - v;
-                    sse_y += vis ? e * e : 0;
-                    packed |= (uint32_t)v << (8 * j);
-                    if (bx == 3 && j == 3) left[by * 4 + i] = (uint8_t)v;
-                }
-                *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + by * 4 + i) * g.pitch + x0 + bx * 4) = packed;
-            }
-            mbs[mbi].nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nz : 0);
-        } else if (lane < 24) {
-            const int comp = (lane - 16) >> 2, cb = (lane - 16) & 3, bx = cb & 1, by = cb >> 1;
-            int d[16], rr[16];
-            dequant4x4(z, d, qpc, 1);
-            d[0] = cdc[comp * 4 + cb];
-            idct4x4(d, rr);
-            const int xcb = x0 / 2 + bx * 4, ycb = y0 / 2 + by * 4;
             for (int i = 0; i < 4; ++i)
                 for (int j = 0; j < 4; ++j) {
-                    const int o = 256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j;
-                    const int v = clip255(pred[o] + rr[i * 4 + j]);
-                    const int e = pred[o] + res[o] - v;
-                    sse_c += (2 * (xcb + j) < g.width && 2 * (ycb + i) < g.height) ? e * e : 0;
-                    fs->rec_uv[(ycb + i) * g.pitch + 2 * (xcb + j) + comp] = (uint8_t)v;
-                    if (bx == 1 && j == 3) left[16 + comp * 8 + by * 4 + i] = (uint8_t)v;
+                    const int xs = x0 + 4 * bx + j, ys = y0 + 4 * by + i;
+                    const int rec = clip255(pred16_px(p, n, 4 * bx + j, 4 * by + i) + rr[i * 4 + j]);
+                    const int e = (int)ls[(4 * by + i) * 16 + 4 * bx + j] - rec;
+                    sse += (xs < g.width && ys < g.height) ? (uint32_t)(e * e) : 0u;
+                    lt[1 + 4 * by + i][1 + 4 * bx + j] = (uint8_t)rec;
                 }
-            (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
+            m.nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nz : 0);
         }
-        // per-lane running sums; reduced across the wave once per row
-        row_sse[0] += (unsigned)sse_y;
-        row_sse[(lane >= 20) ? 2 : 1] += (unsigned)sse_c;
-        if (lane == 0) {
-            const int ccbp = (chroma_mask != 0) ? 2 : ((cdc_nz[0] | cdc_nz[1]) ? 1 : 0);
-            MbInfo& m = mbs[mbi];
-            m.type = kMbI16x16;
-            m.qp = (uint8_t)qp;
-            m.cbp = (uint8_t)((luma_ac ? 15 : 0) | (ccbp << 4));
-            m.i16_mode = (uint8_t)lmode;
-            m.chroma_mode = (uint8_t)cmode;
-            m.mvx = 0;
-            m.mvy = 0;
+        cbp_l = luma_ac ? 15 : 0;
+        wave_sync_lds();
+    }
+    if (lane == 0) m.cbp = (uint8_t)cbp_l;  // chroma bits merged at the end of the row
+}
+
+// cs: the macroblock's source chroma in LDS (8 rows x 16 interleaved bytes).
+__device__ void intra_chroma_mb(const Geometry& g, const FrameState* fs, const MbFields& f, const uint8_t* cs,
+                                MbInfo& m, int16_t* __restrict__ mc, int mbx, int mby, const Avail& av,
+                                uint8_t (*ct)[9][kCT], int* cdc, int lane, uint32_t& sse_u, uint32_t& sse_v) {
+    const int xc0 = mbx * 8, yc0 = mby * 8;
+    const int qpc = chroma_qp(f.qp, fs->chroma_qp_offset);
+    const int comp = lane >> 2, cb = lane & 3, bx = cb & 1, by = cb >> 1;
+    int z[16], nz = 0;
+    NbMb n;
+    PredMb p;
+    if (lane < 8) {
+        n = nbmb_from_plane(&ct[comp][1][1], kCT, 0, 0, 8, 1, 0, av.left, av.top, av.topleft);
+        p = prep_chroma(f.chroma_mode, n);
+        int x[16], y[16];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j)
+                x[i * 4 + j] = (int)cs[(4 * by + i) * 16 + 2 * (4 * bx + j) + comp] - predc_px(p, n, 4 * bx + j, 4 * by + i);
+        fdct4x4(x, y);
+        cdc[comp * 4 + cb] = y[0];
+        nz = quant4x4(y, z, qpc, true, 1);
+        for (int k = 1; k < 16; ++k) mc[kCoefChromaAc + (comp * 4 + cb) * 16 + k] = (int16_t)z[kZigzag4x4[k]];
+        (comp ? m.nz_cr : m.nz_cb)[cb] = (uint8_t)nz;
+    }
+    wave_sync_lds();
+    int ndc = 0;
+    if (lane == 0 || lane == 4) {
+        int in[4], zd[4], dq[4];
+        for (int i = 0; i < 4; ++i) in[i] = cdc[comp * 4 + i];
+        ndc = quant_dc_chroma(in, zd, qpc, true);
+        for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zd[i];
+        dequant_dc_chroma(zd, dq, qpc);
+        for (int i = 0; i < 4; ++i) cdc[comp * 4 + i] = dq[i];
+    }
+    wave_sync_lds();
+    const bool any_ac = __ballot(lane < 8 && nz > 0) != 0, any_dc = __ballot(ndc > 0) != 0;
+    if (lane < 8) {
+        int d[16], rr[16];
+        dequant4x4(z, d, qpc, 1);
+        d[0] = cdc[comp * 4 + cb];
+        idct4x4(d, rr);
+        uint32_t s = 0;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                const int xc = xc0 + 4 * bx + j, yc = yc0 + 4 * by + i;
+                const int rec = clip255(predc_px(p, n, 4 * bx + j, 4 * by + i) + rr[i * 4 + j]);
+                const int e = (int)cs[(4 * by + i) * 16 + 2 * (4 * bx + j) + comp] - rec;
+                s += (2 * xc < g.width && 2 * yc < g.height) ? (uint32_t)(e * e) : 0u;
+                ct[comp][1 + 4 * by + i][1 + 4 * bx + j] = (uint8_t)rec;
+            }
+        if (comp)
+            sse_v += s;
+        else
+            sse_u += s;
+    }
+    if (lane == 0) m.cbp_c = (uint8_t)(any_ac ? 2 : (any_dc ? 1 : 0));
+    wave_sync_lds();
+}
+
+constexpr int kMaxMbW = 512;  // 8192 samples
+
+// Top neighbour byte at position x of the row above's bottom line (luma samples, or interleaved
+// chroma bytes), owned by macroblock x >> 4: intra MBs of this picture publish it through the
+// tagged line buffer (polled until written), inter MBs are final in the picture since
+// k_inter_encode.  Every lane of the wave calls this (inactive lanes with need = false).
+__device__ __forceinline__ uint8_t top_sample(bool need, bool owner_intra, const uint8_t* __restrict__ pic_row,
+                                              const uint64_t* __restrict__ line, int x, uint32_t tag) {
+    uint64_t v = 0;
+    bool pending = need && owner_intra;
+    while (true) {
+        if (pending) {
+            v = load_line(line + (x >> 2));
+            pending = (uint32_t)(v >> 32) != tag;
         }
-        __syncthreads();
-        (void)modes;
+        if (__ballot(pending) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
     }
-    unsigned long long tot[3];
-    for (int c = 0; c < 3; ++c) {
-        unsigned long long v = row_sse[c];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        tot[c] = v;
+    if (!need) return 0;
+    return owner_intra ? (uint8_t)(v >> (8 * (x & 3))) : pic_row[x];
+}
+
+__global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState* __restrict__ fs,
+                                                    const uint8_t* __restrict__ src_y,
+                                                    const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
+                                                    int16_t* __restrict__ coef, int* __restrict__ wave_prog,
+                                                    uint64_t* __restrict__ wave_line,
+                                                    const uint32_t* __restrict__ mb_sse) {
+    __shared__ uint8_t lt[17][kLT];      // luma tile: row 0 = top neighbours, column 0 = left neighbours
+    __shared__ uint8_t ct[2][9][kCT];    // chroma tiles (Cb, Cr)
+    __shared__ uint32_t ls[64];          // source luma of the current MB (16 x 16)
+    __shared__ uint32_t cs[32];          // source chroma of the current MB (8 rows x 16 interleaved bytes)
+    __shared__ int ldc[16], cdc[8];
+    __shared__ int s_row;
+    __shared__ unsigned long long s_sse[3];
+    __shared__ uint8_t rintra[2][kMaxMbW];  // intra flags of this row's / the row above's macroblocks
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // rows are taken in dispatch order (ticket): a row only ever waits on rows already running
+    if (threadIdx.x == 0) s_row = atomicAdd(&wave_prog[0], 1);
+    const bool idr = fs->idr != 0;
+    const uint32_t tag = (uint32_t)fs->frame_tag;
+    __syncthreads();
+    const int mby = s_row;
+    for (int x = threadIdx.x; x < g.mb_w; x += 128) {
+        rintra[0][x] = (uint8_t)(idr || is_intra(mbs[mby * g.mb_w + x]));
+        rintra[1][x] = (uint8_t)(mby > 0 && (idr || is_intra(mbs[(mby - 1) * g.mb_w + x])));
     }
-    if (lane < 3) fs->sse_part[lane * kSsePartStride + mby] = tot[lane];
+    __syncthreads();
+    // bottom-line buffers: per MB row, coded_w / 4 luma words then coded_w / 4 chroma words
+    const int line_words = g.coded_w / 2;
+    uint64_t* my_line = wave_line + (size_t)mby * line_words + (wave ? g.coded_w / 4 : 0);
+    const uint64_t* up_line = wave_line + (size_t)(mby > 0 ? mby - 1 : 0) * line_words + (wave ? g.coded_w / 4 : 0);
+    int last_coded = -2;  // the left neighbour's reconstruction is in the tile when last_coded == mbx - 1
+    uint32_t sse_a = 0, sse_b = 0;  // luma wave: Y; chroma wave: U, V
+    uint32_t old_a = 0, old_b = 0, old_c = 0;  // P pictures: inter distortion of the replaced MBs
+    // software pipeline: the source samples and fields of the next intra MB are loaded while the
+    // current one is coded (one dword of source per lane)
+    auto next_intra = [&](int from) {
+        int x = from;
+        while (x < g.mb_w && !rintra[0][x]) ++x;
+        return x;
+    };
+    auto fetch_src = [&](int mbx) -> uint32_t {
+        if (mbx >= g.mb_w) return 0u;
+        if (wave == 0) {
+            const int r = lane >> 2, c4 = (lane & 3) * 4;
+            return *reinterpret_cast<const uint32_t*>(src_y + (size_t)(mby * 16 + r) * g.pitch + mbx * 16 + c4);
+        }
+        if (lane >= 32) return 0u;
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        return *reinterpret_cast<const uint32_t*>(src_uv + (size_t)(mby * 8 + r) * g.pitch + mbx * 16 + c4);
+    };
+    int nxt = next_intra(0);
+    uint32_t nsrc = fetch_src(nxt);
+    MbFields nf = load_fields(&mbs[mby * g.mb_w + (nxt < g.mb_w ? nxt : 0)]);
+    for (int mbx = nxt; mbx < g.mb_w; mbx = nxt) {
+        const int mbi = mby * g.mb_w + mbx;
+        MbInfo& m = mbs[mbi];
+        const bool left_in_tile = last_coded == mbx - 1;
+        const MbFields f = nf;
+        if (wave == 0) ls[lane] = nsrc;
+        else if (lane < 32) cs[lane] = nsrc;
+        const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
+        int16_t* mc = coef + (size_t)mbi * kCoefStride;
+        if (wave == 0) {
+            const int x0 = mbx * 16, y0 = mby * 16;
+            // left column: keep the previous MB's right column from the tile, or load it
+            const uint8_t keep = (lane < 16 && left_in_tile) ? lt[1 + lane][16] : 0;
+            const uint8_t lft = (lane < 16 && !left_in_tile && av.left) ? fs->rec_y[(y0 + lane) * g.pitch + x0 - 1] : 0;
+            const int x = x0 - 1 + lane;
+            const bool need = lane < 21 && (lane == 0 ? av.topleft : (lane <= 16 ? av.top : av.topright));
+            const uint8_t top = top_sample(need, need && rintra[1][x >> 4],
+                                           fs->rec_y + (size_t)(y0 > 0 ? y0 - 1 : 0) * g.pitch, up_line, x, tag);
+            nxt = next_intra(mbx + 1);  // prefetch the next intra MB behind this one's neighbour loads
+            nsrc = fetch_src(nxt);
+            nf = load_fields(&mbs[mby * g.mb_w + (nxt < g.mb_w ? nxt : mbx)]);
+            wave_sync_lds();
+            if (lane < 16) lt[1 + lane][0] = left_in_tile ? keep : lft;
+            if (lane < 21) lt[0][lane] = top;
+            wave_sync_lds();
+            intra_luma_mb(g, f, reinterpret_cast<const uint8_t*>(ls), m, mc, mbx, mby, av, lt, ldc, lane, sse_a);
+            {  // tile -> reconstruction: 16 rows x 16 bytes, one dword per lane; bottom line -> buffer
+                const int r = lane >> 2, c4 = (lane & 3) * 4;
+                const uint32_t v = (uint32_t)lt[1 + r][1 + c4] | ((uint32_t)lt[1 + r][2 + c4] << 8) |
+                                   ((uint32_t)lt[1 + r][3 + c4] << 16) | ((uint32_t)lt[1 + r][4 + c4] << 24);
+                *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + r) * g.pitch + x0 + c4) = v;
+                if (r == 15) store_line(my_line + (x0 + c4) / 4, tag, v);
+            }
+            if (!idr && lane == 0) old_a += mb_sse[mbi];
+        } else {
+            const int xc0 = mbx * 8, yc0 = mby * 8;
+            uint8_t keep = 0, lft = 0;
+            if (lane < 16) {
+                const int comp = lane >> 3, r = lane & 7;
+                keep = left_in_tile ? ct[comp][1 + r][8] : 0;
+                lft = (!left_in_tile && av.left) ? fs->rec_uv[(yc0 + r) * g.pitch + 2 * (xc0 - 1) + comp] : 0;
+            }
+            // top: lanes 16..33 -> (comp, cx 0..8 = x -1..7), byte 2*(xc0-1+cx)+comp of the line
+            const int k = lane - 16, comp_t = k >= 9 ? 1 : 0, cx = k - 9 * comp_t;
+            const int x = 2 * (xc0 - 1 + cx) + comp_t;
+            const bool need = lane >= 16 && lane < 34 && (cx == 0 ? av.topleft : av.top);
+            const uint8_t top = top_sample(need, need && rintra[1][x >> 4],
+                                           fs->rec_uv + (size_t)(yc0 > 0 ? yc0 - 1 : 0) * g.pitch, up_line, x, tag);
+            nxt = next_intra(mbx + 1);
+            nsrc = fetch_src(nxt);
+            nf = load_fields(&mbs[mby * g.mb_w + (nxt < g.mb_w ? nxt : mbx)]);
+            wave_sync_lds();
+            if (lane < 16) {
+                ct[lane >> 3][1 + (lane & 7)][0] = left_in_tile ? keep : lft;
+            } else if (lane < 34) {
+                ct[comp_t][0][cx] = top;
+            }
+            wave_sync_lds();
+            intra_chroma_mb(g, fs, f, reinterpret_cast<const uint8_t*>(cs), m, mc, mbx, mby, av, ct, cdc, lane, sse_a,
+                            sse_b);
+            if (lane < 32) {  // 8 rows x 16 interleaved bytes, one dword (2 samples x 2 planes) per lane
+                const int r = lane >> 2, c2 = (lane & 3) * 2;
+                const uint32_t v = (uint32_t)ct[0][1 + r][1 + c2] | ((uint32_t)ct[1][1 + r][1 + c2] << 8) |
+                                   ((uint32_t)ct[0][1 + r][2 + c2] << 16) | ((uint32_t)ct[1][1 + r][2 + c2] << 24);
+                *reinterpret_cast<uint32_t*>(fs->rec_uv + (yc0 + r) * g.pitch + 2 * (xc0 + c2)) = v;
+                if (r == 7) store_line(my_line + (2 * (xc0 + c2)) / 4, tag, v);
+            }
+            if (!idr && lane == 0) {
+                old_b += mb_sse[g.mb_w * g.mb_h + mbi];
+                old_c += mb_sse[2 * g.mb_w * g.mb_h + mbi];
+            }
+        }
+        last_coded = mbx;
+    }
+    // distortion of the row: absolute (IDR: one partial per row) or, in P pictures, the delta
+    // of the switched macroblocks against their inter distortion (modulo-2^64 sums)
+    unsigned long long a = sse_a, b = sse_b;
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    if (lane == 0) {
+        if (wave == 0) {
+            s_sse[0] = a - old_a;
+        } else {
+            s_sse[1] = a - old_b;
+            s_sse[2] = b - old_c;
+        }
+    }
+    __syncthreads();
+    for (int mbx = threadIdx.x; mbx < g.mb_w; mbx += 128) {
+        MbInfo& m = mbs[mby * g.mb_w + mbx];
+        if (idr || is_intra(m)) m.cbp = (uint8_t)((m.cbp & 15) | (m.cbp_c << 4));
+    }
+    if (threadIdx.x < 3) {
+        const int slot = idr ? mby : (g.mb_w * g.mb_h + 3) / 4 + mby;
+        fs->sse_part[threadIdx.x * kSsePartStride + slot] = s_sse[threadIdx.x];
+    }
+}
+
+// Intra macroblocks of P pictures (independent by construction, see intra_selected()): one
+// workgroup per macroblock, luma on wave 0 and chroma on wave 1, neighbours straight from the
+// final inter reconstruction, coded by the same routines as k_intra_wave.  The distortion
+// delta against the MB's inter distortion goes into its row's partial (atomic, few MBs).
+__device__ void intra_p_mb(const Geometry& g, const FrameState* __restrict__ fs, const uint8_t* __restrict__ src_y,
+                           const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs, int16_t* __restrict__ coef,
+                           const int32_t* __restrict__ gain, const uint32_t* __restrict__ mb_sse, int mbi) {
+    __shared__ uint8_t lt[17][kLT];
+    __shared__ uint8_t ct[2][9][kCT];
+    __shared__ uint32_t ls[64];
+    __shared__ uint32_t cs[32];
+    __shared__ int ldc[16], cdc[8];
+    const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
+    if (!intra_selected(gain, g.mb_w, g.mb_h, mbx, mby)) return;  // uniform over the workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    MbInfo& m = mbs[mbi];
+    MbFields f = load_fields(&m);
+    f.type = m.itype;
+    f.qp = fs->qp;
+    const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
+    int16_t* mc = coef + (size_t)mbi * kCoefStride;
+    uint32_t s0 = 0, s1 = 0;
+    __syncthreads();  // every wave has read the MB fields before they are overwritten
+    if (threadIdx.x == 0) {
+        m.type = (uint8_t)f.type;
+        m.qp = (uint8_t)f.qp;
+        m.mvx = 0;
+        m.mvy = 0;
+    }
+    if (wave == 0) {
+        const int x0 = mbx * 16, y0 = mby * 16;
+        {
+            const int r = lane >> 2, c4 = (lane & 3) * 4;
+            ls[lane] = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * g.pitch + x0 + c4);
+        }
+        if (lane < 16) lt[1 + lane][0] = av.left ? fs->rec_y[(y0 + lane) * g.pitch + x0 - 1] : 0;
+        if (lane < 21) {
+            const bool ok = lane == 0 ? av.topleft : (lane <= 16 ? av.top : av.topright);
+            lt[0][lane] = ok ? fs->rec_y[(y0 - 1) * g.pitch + x0 - 1 + lane] : 0;
+        }
+        wave_sync_lds();
+        intra_luma_mb(g, f, reinterpret_cast<const uint8_t*>(ls), m, mc, mbx, mby, av, lt, ldc, lane, s0);
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        const uint32_t v = (uint32_t)lt[1 + r][1 + c4] | ((uint32_t)lt[1 + r][2 + c4] << 8) |
+                           ((uint32_t)lt[1 + r][3 + c4] << 16) | ((uint32_t)lt[1 + r][4 + c4] << 24);
+        *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + r) * g.pitch + x0 + c4) = v;
+    } else {
+        const int xc0 = mbx * 8, yc0 = mby * 8;
+        if (lane < 32) {
+            const int r = lane >> 2, c4 = (lane & 3) * 4;
+            cs[lane] = *reinterpret_cast<const uint32_t*>(src_uv + (size_t)(yc0 + r) * g.pitch + mbx * 16 + c4);
+        }
+        if (lane < 16) {
+            const int comp = lane >> 3, r = lane & 7;
+            ct[comp][1 + r][0] = av.left ? fs->rec_uv[(yc0 + r) * g.pitch + 2 * (xc0 - 1) + comp] : 0;
+        } else if (lane < 34) {
+            const int k = lane - 16, comp = k / 9, cx = k - comp * 9;
+            const bool ok = cx == 0 ? av.topleft : av.top;
+            ct[comp][0][cx] = ok ? fs->rec_uv[(yc0 - 1) * g.pitch + 2 * (xc0 - 1 + cx) + comp] : 0;
+        }
+        wave_sync_lds();
+        intra_chroma_mb(g, fs, f, reinterpret_cast<const uint8_t*>(cs), m, mc, mbx, mby, av, ct, cdc, lane, s0, s1);
+        if (lane < 32) {
+            const int r = lane >> 2, c2 = (lane & 3) * 2;
+            const uint32_t v = (uint32_t)ct[0][1 + r][1 + c2] | ((uint32_t)ct[1][1 + r][1 + c2] << 8) |
+                               ((uint32_t)ct[0][1 + r][2 + c2] << 16) | ((uint32_t)ct[1][1 + r][2 + c2] << 24);
+            *reinterpret_cast<uint32_t*>(fs->rec_uv + (yc0 + r) * g.pitch + 2 * (xc0 + c2)) = v;
+        }
+    }
+    unsigned long long a = s0, b = s1;
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    __syncthreads();  // both waves done: merge the chroma cbp
+    const int nmb = g.mb_w * g.mb_h;
+    const int slot = (nmb + 3) / 4 + mby;
+    if (lane == 0) {
+        if (wave == 0) {
+            m.cbp = (uint8_t)((m.cbp & 15) | (m.cbp_c << 4));
+            atomicAdd(&fs->sse_part[slot], a - mb_sse[mbi]);
+        } else {
+            atomicAdd(&fs->sse_part[kSsePartStride + slot], a - mb_sse[nmb + mbi]);
+            atomicAdd(&fs->sse_part[2 * kSsePartStride + slot], b - mb_sse[2 * nmb + mbi]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(128) void k_intra_p(Geometry g, const FrameState* __restrict__ fs,
+                                                 const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
+                                                 MbInfo* __restrict__ mbs, int16_t* __restrict__ coef,
+                                                 const int32_t* __restrict__ gain, const uint32_t* __restrict__ mb_sse,
+                                                 const int* __restrict__ wave_prog, const int* __restrict__ cand) {
+    // the candidates (positive gain) listed by k_intra_analyze; a fixed grid walks the list
+    const int ncand = wave_prog[1];
+    for (int k = blockIdx.x; k < ncand; k += gridDim.x) intra_p_mb(g, fs, src_y, src_uv, mbs, coef, gain, mb_sse, cand[k]);
 }
 
 // ------------------------------------------------------------------ CAVLC
@@ -808,12 +1296,12 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     // backward search, 32 MBs per step (the ballot holds active lanes only; this half's bits
     // are taken).  I slices: every MB is at the slice QP.
     int dqp = 0;
-    if (!skip && !fs->idr && m.cbp != 0) {
+    if (!skip && !fs->idr && carries_dqp(m)) {
         const int per_slice = fs->slice_rows * g.mb_w, first = (mbi / per_slice) * per_slice;
         int pred = fs->qp;
         for (int j0 = mbi - 1; j0 >= first; j0 -= 32) {
             const int j = j0 - lane;
-            const unsigned long long bal = __ballot(j >= first && mbs[j].cbp != 0);
+            const unsigned long long bal = __ballot(j >= first && carries_dqp(mbs[j]));
             const uint32_t hb = (uint32_t)(bal >> (32 * hw));
             if (hb) {
                 pred = mbs[j0 - (__ffs(hb) - 1)].qp;
@@ -1066,8 +1554,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     }
     // distortion: block-wide reduction of the per-MB partials
     {
-        // partials: one per inter workgroup (4 MBs) or per intra MB row
-        const int nparts = idr ? g.mb_h : (nmb + 3) / 4;
+        // partials: one per intra MB row (IDR) or per inter workgroup (4 MBs) + the per-row
+        // intra deltas of k_intra_wave (P pictures with intra macroblocks)
+        const int nparts = idr ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
         unsigned long long acc[3] = {0, 0, 0};
         for (int i = t; i < nparts; i += kScanThreads)
             for (int c = 0; c < 3; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
@@ -1223,16 +1712,33 @@ void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
                   hipStream_t stream) {
     const int nmb = g.mb_w * g.mb_h;
     hipLaunchKernelGGL(k_inter_encode, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, src_y, src_uv, b.mb,
-                       b.coef);
+                       b.coef, b.mb_sse, b.wave_prog);
 }
 
-void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                  hipStream_t stream, const FrameState* publish) {
+static void launch_analyze(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                           hipStream_t stream, const FrameState* publish) {
+    const int nmb = g.mb_w * g.mb_h;
     StateArg sa{};
     if (publish) sa.v = *publish;
     sa.dst = b.fs;
     sa.publish = publish ? 1 : 0;
-    hipLaunchKernelGGL(k_intra_rows, dim3(g.mb_h), dim3(64), 0, stream, g, sa, src_y, src_uv, b.mb, b.coef);
+    hipLaunchKernelGGL(k_intra_analyze, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, sa, src_y, src_uv, b.mb,
+                       b.wave_prog, b.intra_gain, b.intra_cand);
+}
+
+void launch_intra_in_p(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                       hipStream_t stream) {
+    launch_analyze(g, b, src_y, src_uv, stream, nullptr);
+    // a fixed grid over k_intra_analyze's candidate list (a few percent of the MBs)
+    hipLaunchKernelGGL(k_intra_p, dim3(256), dim3(128), 0, stream, g, b.fs, src_y, src_uv, b.mb, b.coef,
+                       b.intra_gain, b.mb_sse, b.wave_prog, b.intra_cand);
+}
+
+void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                  hipStream_t stream, const FrameState* publish) {
+    launch_analyze(g, b, src_y, src_uv, stream, publish);
+    hipLaunchKernelGGL(k_intra_wave, dim3(g.mb_h), dim3(128), 0, stream, g, b.fs, src_y, src_uv, b.mb, b.coef,
+                       b.wave_prog, b.wave_line, b.mb_sse);
 }
 
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream) {

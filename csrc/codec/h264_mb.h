@@ -6,6 +6,7 @@
 #pragma once
 #include "h264_core.h"
 #include "h264_gpu.h"
+#include "h264_intra.h"
 
 namespace mx {
 namespace h264 {
@@ -40,7 +41,7 @@ MXHD MvNb mv_nb(const MbInfo* mbs, int idx, bool avail) {
     n.mv = Mv{0, 0};
     if (!avail) return n;
     const MbInfo& m = mbs[idx];
-    if (m.type != kMbI16x16) {
+    if (m.type == kMbP16x16) {
         n.ref = 0;
         n.mv = Mv{m.mvx, m.mvy};
     }
@@ -67,7 +68,7 @@ MXHD bool decide_skip(const Geometry& g, const MbInfo* mbs, int mbi, const Avail
 template <class W>
 MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mbs, const MbInfo& m,
                     const int16_t* mc, int mbi, const Avail& av, int mvdx, int mvdy, int dqp = 0) {
-    const bool intra = m.type == kMbI16x16;
+    const bool intra = m.type == kMbI16x16;  // Intra16x16: DC / AC split of the luma residual
     const int cbp = m.cbp;
     const int cbp_l = cbp & 15, cbp_c = cbp >> 4;
     const MbInfo* ml = av.left ? &mbs[mbi - 1] : nullptr;
@@ -77,7 +78,31 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mb
             const int mbtype = 1 + m.i16_mode + 4 * cbp_c + (cbp_l ? 12 : 0);
             put_ue(w, (uint32_t)(idr ? mbtype : 5 + mbtype));
             put_ue(w, m.chroma_mode);
-            put_se(w, 0);  // mb_qp_delta
+            put_se(w, dqp);  // mb_qp_delta (0 in I slices: every MB at the slice QP)
+        } else if (m.type == kMbI4x4) {
+            put_ue(w, idr ? 0u : 5u);  // I_NxN
+            // prev_intra4x4_pred_mode_flag / rem_intra4x4_pred_mode, blkIdx order (8.3.1.1:
+            // a neighbour MB that is not Intra4x4 counts as DC, an unavailable one forces DC)
+            for (int b = 0; b < 16; ++b) {
+                const int bx = kBlkX[b], by = kBlkY[b];
+                const bool ha = bx > 0 || av.left, hb = by > 0 || av.top;
+                int ma = -1, mb = -1;
+                if (bx > 0) ma = i4_get(m.i4, by * 4 + bx - 1);
+                else if (ml && ml->type == kMbI4x4) ma = i4_get(ml->i4, by * 4 + 3);
+                if (by > 0) mb = i4_get(m.i4, (by - 1) * 4 + bx);
+                else if (mt && mt->type == kMbI4x4) mb = i4_get(mt->i4, 12 + bx);
+                const int pm = i4_pred_mode(ma, mb, ha, hb);
+                const int mode = i4_get(m.i4, by * 4 + bx);
+                if (mode == pm) {
+                    w.put(1, 1);
+                } else {
+                    w.put(0, 1);
+                    w.put((uint32_t)(mode < pm ? mode : mode - 1), 3);
+                }
+            }
+            put_ue(w, m.chroma_mode);
+            put_ue(w, (uint32_t)cbp_to_codenum(cbp, true));
+            if (cbp) put_se(w, dqp);
         } else {
             put_ue(w, 0);  // P_L0_16x16
             put_se(w, mvdx);
@@ -138,6 +163,20 @@ MXHD int aq_mb_qp(int frame_qp, uint32_t sad, int aq) {
     const int off = sad > 256u * 48 ? 12 : (sad > 256u * 32 ? 6 : 0);
     const int q = frame_qp + off;
     return q > 51 ? 51 : q;
+}
+
+// Inter cost of a P16x16 macroblock for the intra decision: luma SATD of the motion-
+// compensated residual + mv rate at the frame lambda.
+MXHD uint32_t inter_cost(uint32_t satd, int frame_qp, int mvx, int mvy) {
+    return satd + (uint32_t)(lambda_sad(frame_qp) * (mvd_bits(mvx) + mvd_bits(mvy)));
+}
+
+// Rows per slice of an IDR picture: intra macroblocks are reconstructed in a diagonal
+// wavefront per slice, so the critical path is mb_w + 2 * (rows - 1) macroblocks; ~16-row
+// slices keep it near mb_w at every size (one slice = 254 MB steps at 1080p, 5 slices = 146).
+MXHD int idr_slice_rows(int mb_h) {
+    const int ns = (mb_h + 15) / 16;
+    return (mb_h + ns - 1) / ns;
 }
 
 // mb_qp_delta value for QP `qp` after predictor `pred` (both 0..51), in -26..25.

@@ -405,6 +405,8 @@ class Decoder:
         self.ref = None  # (Y, U, V) int32 planes of the reference (coded size)
         self.frames: list[tuple[np.ndarray, np.ndarray, np.ndarray]] = []
         self.frames_coded: list[tuple[np.ndarray, np.ndarray, np.ndarray]] = []
+        # tests: decode a subset of a picture's slices (the missing macroblocks stay zero)
+        self.allow_partial = False
         self.cur = None
         self.mbs: list[MbState] = []
         self.slice_count = 0
@@ -452,7 +454,7 @@ class Decoder:
         if self.cur is None:
             return
         s = self.sps
-        if self.decoded_mbs != s.mb_w * s.mb_h:
+        if self.decoded_mbs != s.mb_w * s.mb_h and not self.allow_partial:
             raise DecodeError(f"incomplete picture: {self.decoded_mbs}/{s.mb_w * s.mb_h} MBs")
         y, u, v = (p.astype(np.uint8) for p in self.cur)
         self.frames_coded.append((y, u, v))
@@ -833,7 +835,7 @@ class Decoder:
                         o[y, x] = (T8[6] + 3 * T8[7] + 2) >> 2
                     else:
                         o[y, x] = (T8[x + y] + 2 * T8[x + y + 1] + T8[x + y + 2] + 2) >> 2
-        else:
+        elif mode in (4, 5, 6):
             if not (top and left and tl):
                 raise DecodeError(f"I4 mode {mode} needs top/left/top-left")
 
@@ -873,7 +875,9 @@ class Decoder:
                             v = (P(x - 1, -1) + 2 * P(x - 2, -1) + P(x - 3, -1) + 2) >> 2
                     o[y, x] = v
             return o
-        if mode == 7:  # vertical left
+        elif mode == 7:  # vertical left
+            if not top:
+                raise DecodeError("I4 VL without top")
             for y in range(4):
                 for x in range(4):
                     i = x + (y >> 1)

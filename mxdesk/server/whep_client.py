@@ -71,6 +71,7 @@ class WhepResult:
     dc_received: list[str] = field(default_factory=list)  # server -> client data-channel messages
     dc_audio: list[bytes] = field(default_factory=list)   # MXA1 chunks from the "audio" channel
     dc_sent: int = 0
+    dc_labels: list[str] = field(default_factory=list)  # server-opened channels (selkies "input")
 
 
 class _Client(asyncio.DatagramProtocol):
@@ -117,7 +118,32 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                 raise RuntimeError(f"WHEP POST failed: {r.status} {await r.text()}")
             res.answer = await r.text()
             location = r.headers["Location"]
-    ans = parse_sdp(res.answer)
+    try:
+        await media_session(res, res.answer, dtls, ufrag, N, n_frames, t0, timeout=timeout,
+                            drop_seq_every=drop_seq_every, pli_after=pli_after, dc_messages=dc_messages,
+                            dc_wait_stats=dc_wait_stats, via_relay=via_relay, dc_audio_chunks=dc_audio_chunks,
+                            simulate_loss=simulate_loss)
+    finally:
+        try:
+            async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
+                base = url.rsplit("/whep", 1)[0]
+                async with s.delete(base + location):
+                    pass
+        except Exception:
+            pass
+    return res
+
+
+async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n_frames: int, t0: float,
+                        timeout: float = 30.0, drop_seq_every: int = 0, pli_after: int = 0,
+                        dc_messages: list[str] | None = None, dc_wait_stats: bool = False, via_relay: bool = False,
+                        dc_audio_chunks: int = 0, simulate_loss: float = 0.0,
+                        server_channel: str | None = None) -> None:
+    """The browser side of an established negotiation (remote SDP = the server's answer for
+    WHEP, its offer for the selkies protocol): ICE check, DTLS client, SRTP receive with NACK /
+    PLI repair, data channels.  ``server_channel``: the server opens that channel (selkies
+    ``input``); ``dc_messages`` are sent on it once it is open instead of on one we open."""
+    ans = parse_sdp(remote_sdp)
     vid = next(m for m in ans.media if m.kind == "video" and m.port)
     cands = [c.split() for c in vid.attrs_named("candidate")]
     want = "relay" if via_relay else "host"
@@ -186,19 +212,22 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                     tr.sendto(dg)
         if dc_messages is not None:
             if app is None:
-                raise RuntimeError("answer rejected the data channel")
+                raise RuntimeError("remote SDP has no data channel section")
             dc = N.net.DataChannelEndpoint(False, 5000, int(app.attr("sctp-port") or 5000))
             out = dc.connect()
-            dc_id, more = dc.open("input")
-            if dc_audio_chunks:
-                _aid, amore = dc.open("audio", "", False, 0)
-                more += amore
-            for msg in dc_messages:
-                more += dc.send(dc_id, msg.encode(), False)
-            res.dc_sent = len(dc_messages)
+            more = []
+            if server_channel is None:
+                dc_id, more = dc.open("input")
+                if dc_audio_chunks:
+                    _aid, amore = dc.open("audio", "", False, 0)
+                    more += amore
+                for msg in dc_messages:
+                    more += dc.send(dc_id, msg.encode(), False)
+                res.dc_sent = len(dc_messages)
             sctp_out(out + more)
 
         def on_dtls(d: bytes) -> None:
+            nonlocal dc_id
             sctp_out_raw = dtls.feed(d)
             for dg in sctp_out_raw:
                 tr.sendto(dg)
@@ -206,8 +235,16 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                 if dc is not None:
                     sctp_out(dc.feed(p))
             if dc is not None:
-                for kind, _cid, _label, _proto, binary, data in dc.take_events():
-                    if kind == 1 and binary:
+                for kind, cid, label, _proto, binary, data in dc.take_events():
+                    if kind == 0 and server_channel is not None and label == server_channel and dc_id < 0:
+                        dc_id = cid
+                        more = []
+                        for msg in dc_messages:
+                            more += dc.send(cid, msg.encode(), False)
+                        res.dc_sent = len(dc_messages)
+                        res.dc_labels.append(label)
+                        sctp_out(more)
+                    elif kind == 1 and binary:
                         res.dc_audio.append(data)
                     elif kind == 1:
                         res.dc_received.append(data.decode("utf-8", "replace"))
@@ -350,16 +387,6 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
         res.stream = b"".join(res.aus)
     finally:
         tr.close()
-        try:
-            async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
-                base = url.rsplit("/whep", 1)[0]
-                async with s.delete(base + location):
-                    pass
-        except Exception:
-            pass
-    return res
-
-
 def main(argv=None) -> int:
     import argparse
 

@@ -27,6 +27,7 @@ def encode_decode(native, w, h, frames, **kw):
     cfg.search_range = kw.get("search_range", 8)
     cfg.subpel = kw.get("subpel", 1)
     cfg.keyint = kw.get("keyint", 0)
+    cfg.intra_in_p = kw.get("intra_in_p", 1)
     enc = native.CpuH264Encoder(cfg)
     stream, recon, src, sizes = b"", [], [], []
     for t in range(frames):
@@ -66,8 +67,35 @@ def test_static_content_skips(native):
 
 
 def test_forced_idr_and_keyint(native):
-    dec, out, recon, src, sizes, enc = encode_decode(native, 64, 48, 5, keyint=2)
-    assert dec.stats["i16"] == 12 * 3  # IDR at frames 0, 2, 4
+    dec, out, recon, src, sizes, enc = encode_decode(native, 64, 48, 5, keyint=2, intra_in_p=0)
+    assert dec.stats["i16"] + dec.stats["i4"] == 12 * 3  # IDR at frames 0, 2, 4
+
+
+def test_intra4x4_and_intra_in_p_round_trip(native):
+    """Intra4x4 IDR macroblocks and intra macroblocks inside P slices (a new high-contrast patch
+    every frame that inter prediction cannot follow) decode to the reconstruction."""
+    w, h = 96, 64
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height, cfg.bitrate_kbps, cfg.qp = w, h, 0, 26
+    cfg.intra_in_p = 1
+    enc = native.CpuH264Encoder(cfg)
+    rng = np.random.default_rng(7)
+    stream, recon = b"", []
+    for t in range(4):
+        y, uv = synthetic_nv12(w, h, t)
+        # text-like glyph patch at a fresh position: sharp edges, no temporal match
+        gy, gx = 4 + 8 * t, 40 + 10 * t
+        glyph = (rng.integers(0, 2, (16, 16)) * 200 + 20).astype(np.uint8)
+        y[gy:gy + 16, gx:gx + 16] = glyph
+        stream += enc.encode(y, uv, False)
+        recon.append(enc.recon()[0].copy())
+    dec = Decoder()
+    dec.decode(stream)
+    assert dec.stats["i4"] > 0, dec.stats
+    p_intra = dec.stats["i4"] + dec.stats["i16"] - 24  # minus the 24 IDR macroblocks
+    assert p_intra > 0, dec.stats
+    for i, (yd, _, _) in enumerate(dec.frames_coded):
+        assert np.array_equal(yd, recon[i]), i
 
 
 def test_rate_control_moves_qp(native):

@@ -113,6 +113,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     cfg.qp = kw.get("qp", 28)
     cfg.search_range = kw.get("search_range", 8)
     cfg.subpel = kw.get("subpel", 1)
+    cfg.intra_in_p = kw.get("intra_in_p", 1)
     genc = gpu.GpuH264Encoder(cfg, _stream())
     cenc = gpu.CpuH264Encoder(cfg)
     gs, cs, grec = b"", b"", []
