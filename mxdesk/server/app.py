@@ -10,7 +10,7 @@ selkies-gstreamer-entrypoint.sh:44-47 (``--addr=0.0.0.0 --port=8080``) and, when
   GET  /turn             RTCConfiguration JSON (STUN/TURN; HMAC or legacy credentials)
   GET  /metrics          Prometheus exposition
   GET  /status           JSON session status (fps, bitrate, QP, latency quantiles)
-  WS   /ws               selkies-compatible signalling relay
+  WS   /ws               selkies signalling: streaming peer (offers to each client) + relay
   WS   /mxws             media transport: binary Annex-B access units + JSON control/input
   WS   /websockify       RFB (noVNC) over WebSocket when NOVNC_ENABLE=true
 
@@ -102,6 +102,17 @@ class MediaServer:
                                  congestion_control=bool(getattr(cfg, "congestion_control", False)), host=getattr(cfg, "webrtc_host", None) or None,
                                  udp_port=int(getattr(cfg, "webrtc_udp_port", 0) or 0),
                                  on_input=self._on_client_message, turn=turn_relay_settings(cfg))
+        self.selkies = None
+        if bool(getattr(cfg, "selkies_peer", True)):
+            from .selkies_peer import SelkiesServerPeer
+            from .webrtc import WebRtcPeer
+
+            w = self.whep
+            self.selkies = SelkiesServerPeer(self.signalling, lambda: WebRtcPeer(
+                pipeline, None, w.host, w.udp_port, w.level_idc, audio=w.audio,
+                congestion_control=w.congestion_control, on_input=w.on_input, turn=w.turn,
+                server_channels=("input",)))
+            self.signalling.attach_server(self.selkies)
 
     # ------------------------------------------------------------------ app
     def make_app(self) -> web.Application:
@@ -119,6 +130,7 @@ class MediaServer:
         app.router.add_get("/status", self.status)
         app.router.add_get("/manifest.json", self.manifest)
         app.router.add_get("/ws", self.signalling.handler)
+        app.router.add_get("/webrtc/signalling/", self.signalling.handler)  # selkies >= 1.5 web app path
         app.router.add_get("/mxws", self.media_ws)
         self.whep.routes(app)
         if self.rfb is not None:
@@ -148,6 +160,8 @@ class MediaServer:
         if self._sync_task is not None:
             self._sync_task.cancel()
         self.whep.close_all()
+        if self.selkies is not None:
+            self.selkies.close_all()
         if self.audio is not None:
             self.audio.stop()
         if self.gamepad is not None:

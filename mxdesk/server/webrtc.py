@@ -214,6 +214,74 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
     return chosen
 
 
+def build_offer(ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port: int, ssrc: int,
+                level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None,
+                codec: str = "h264", datachannel: bool = True, max_message: int = 262144,
+                relay_candidates: list[str] | None = None, video_pt: int = 96) -> str:
+    """Server-side OFFER for the selkies signalling protocol, where the streaming peer offers
+    (upstream webrtcbin): one sendonly video section in the stream's codec, optionally one
+    PCMU audio section and one SCTP data-channel section, all BUNDLEd on the ICE-lite host
+    candidate(s), DTLS ``actpass`` (browsers answer ``active``: we stay the DTLS server)."""
+    if codec == "hevc":
+        rtpmap, fmtp = "H265/90000", f"profile-id=1;tier-flag=0;level-id={level_idc};tx-mode=SRST"
+    else:
+        rtpmap = "H264/90000"
+        fmtp = f"level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}"
+    hosts = [host] + [h for h in (extra_hosts or []) if h != host]
+    cands = [f"a=candidate:{k + 1} 1 udp {2130706431 - k} {h} {port} typ host" for k, h in enumerate(hosts)]
+    cands += list(relay_candidates or [])
+    transport = [f"c=IN IP4 {host}", *cands, "a=end-of-candidates",
+                 f"a=ice-ufrag:{ice_ufrag}", f"a=ice-pwd:{ice_pwd}", f"a=fingerprint:{fingerprint}", "a=setup:actpass"]
+    pt = video_pt
+    mids = ["0"]
+    media = [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport, "a=mid:0", "a=sendonly", "a=rtcp-mux",
+             "a=rtcp-rsize", f"a=rtpmap:{pt} {rtpmap}", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
+             f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb", f"a=fmtp:{pt} {fmtp}",
+             f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
+    if audio_ssrc is not None:
+        mids.append(str(len(mids)))
+        media += [f"m=audio {port} UDP/TLS/RTP/SAVPF 0", *transport, f"a=mid:{mids[-1]}", "a=sendonly", "a=rtcp-mux",
+                  "a=rtpmap:0 PCMU/8000", f"a=ssrc:{audio_ssrc} cname:mxdesk", f"a=ssrc:{audio_ssrc} msid:mxdesk audio0"]
+    if datachannel:
+        mids.append(str(len(mids)))
+        media += [f"m=application {port} UDP/DTLS/SCTP webrtc-datachannel", *transport, f"a=mid:{mids[-1]}",
+                  "a=sctp-port:5000", f"a=max-message-size:{max_message}"]
+    lines = ["v=0", f"o=mxdesk {secrets.randbelow(1 << 62)} 2 IN IP4 {host}", "s=mxdesk", "t=0 0", "a=ice-lite",
+             "a=group:BUNDLE " + " ".join(mids), "a=msid-semantic: WMS mxdesk"]
+    return "\r\n".join(lines + media) + "\r\n"
+
+
+def parse_answer(answer_text: str, video_pt: int) -> tuple[Answer, str]:
+    """The browser's ANSWER to build_offer(): negotiated sections, its ICE / DTLS parameters and
+    its DTLS role (``a=setup``)."""
+    ans = parse_sdp(answer_text)
+    chosen = None
+    audio = dc = None
+    setup = ans.attr("setup") or ""
+    for md in ans.media:
+        if md.port == 0:
+            continue
+        mid = md.attr("mid") or ""
+        setup = md.attr("setup") or setup
+        if md.kind == "video" and chosen is None:
+            if str(video_pt) not in md.fmts:
+                raise ValueError("answer does not accept the offered video format")
+            chosen = Answer(answer_text, video_pt, mid, md.attr("ice-ufrag") or ans.attr("ice-ufrag") or "",
+                            md.attr("ice-pwd") or ans.attr("ice-pwd") or "",
+                            md.attr("fingerprint") or ans.attr("fingerprint") or "")
+        elif md.kind == "audio" and audio is None and "0" in md.fmts:
+            audio = (0, mid)
+        elif md.kind == "application" and dc is None:
+            dc = (mid, int(md.attr("sctp-port") or 5000))
+    if chosen is None:
+        raise ValueError("answer rejected the video section")
+    if audio is not None:
+        chosen.audio_pt, chosen.audio_mid = audio
+    if dc is not None:
+        chosen.dc_mid, chosen.remote_sctp_port = dc
+    return chosen, setup.strip()
+
+
 def local_ips() -> list[str]:
     """Non-loopback IPv4 addresses of this host (one ICE host candidate each)."""
     try:
@@ -298,9 +366,15 @@ def turn_relay_settings(cfg) -> dict | None:
 class WebRtcPeer(asyncio.DatagramProtocol):
     HISTORY = 1024
 
-    def __init__(self, pipeline, offer_sdp: str, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
-                 audio=None, congestion_control: bool = False, on_input=None, turn: dict | None = None):
+    def __init__(self, pipeline, offer_sdp: str | None, host: str | None = None, port: int = 0, level_idc: int = 0x2A,
+                 audio=None, congestion_control: bool = False, on_input=None, turn: dict | None = None,
+                 server_channels: tuple[str, ...] = ()):
+        """``offer_sdp``: the browser's offer (WHEP, we answer); None for the selkies protocol,
+        where we offer (start_offer / accept_answer).  ``server_channels``: data channels we open
+        once SCTP is up (selkies opens ``input`` from the server side)."""
         N = _native()
+        self.server_channels = tuple(server_channels)
+        self.video_pt = 96
         self.turn = turn          # server-side relay settings (host, port, username, password, protocol, tls)
         self.relay = None         # TurnClient once allocated
         self.on_input = on_input  # callback(str) for data-channel text messages
@@ -340,7 +414,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.ts0: int | None = None
         self.cc = CongestionController(pipeline, enabled=congestion_control)
 
-    async def start(self) -> str:
+    async def _bind(self) -> int:
         loop = asyncio.get_running_loop()
         self.transport, _ = await loop.create_datagram_endpoint(lambda: self,
                                                                 local_addr=(self.bind_host, self.bind_port))
@@ -351,21 +425,56 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 20)
         except OSError:
             pass
+        return port
+
+    def _codec_level(self) -> tuple[str, int]:
         codec = getattr(self.pipeline, "codec", "h264")
         level = self.level_idc
         if codec == "hevc":
             p = self.pipeline
             level = _native().hevc_level(p.out_w, p.out_h, p.fps)
+        return codec, level
+
+    def _media_ready(self, codec: str) -> None:
+        packetizer = _native().net.RtpH265Packetizer if codec == "hevc" else _native().net.RtpH264Packetizer
+        self.pkt = packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
+        self.tasks.append(asyncio.create_task(self._timers()))
+
+    async def start(self) -> str:
+        """WHEP: answer the browser's offer."""
+        port = await self._bind()
+        codec, level = self._codec_level()
         relay_cands = []
         if self.turn:
             relay_cands = await self._allocate_relay()
         self.answer = build_answer(self.offer_sdp, self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port,
                                    self.ssrc, level, self.audio_ssrc, self.extra_hosts, codec=codec,
                                    relay_candidates=relay_cands)
-        packetizer = _native().net.RtpH265Packetizer if codec == "hevc" else _native().net.RtpH264Packetizer
-        self.pkt = packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
-        self.tasks.append(asyncio.create_task(self._timers()))
+        self._media_ready(codec)
         return self.answer.sdp
+
+    async def start_offer(self) -> str:
+        """selkies protocol: our offer (the answer comes back through accept_answer)."""
+        port = await self._bind()
+        codec, level = self._codec_level()
+        relay_cands = []
+        if self.turn:
+            relay_cands = await self._allocate_relay()
+        self.local_offer = build_offer(self.ufrag, self.pwd, self.dtls.fingerprint, self.host, port, self.ssrc, level,
+                                       self.audio_ssrc, self.extra_hosts, codec=codec, relay_candidates=relay_cands,
+                                       video_pt=self.video_pt)
+        self._codec = codec
+        return self.local_offer
+
+    async def accept_answer(self, answer_sdp: str) -> None:
+        answer, setup = parse_answer(answer_sdp, self.video_pt)
+        if setup == "passive":  # our certificate / fingerprint is the DTLS server's
+            raise ValueError("answer asks us to be the DTLS client (a=setup:passive); answer with active")
+        self.answer = answer
+        self.offer_sdp = answer_sdp  # remote description (TURN permissions for its candidates)
+        self._media_ready(self._codec)
+        if self.relay is not None:
+            await self.add_remote_candidates(answer_sdp)
 
     async def _allocate_relay(self) -> list[str]:
         """TURN allocation + permissions for the offer's candidates -> relay candidate lines."""
@@ -376,7 +485,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                                 bool(t.get("tls", False)), on_data=self._on_relay_data)
         try:
             rip, rport = await asyncio.wait_for(self.relay.allocate(), float(t.get("timeout", 5.0)))
-            ips = offer_candidate_ips(self.offer_sdp)
+            ips = offer_candidate_ips(self.offer_sdp) if self.offer_sdp else []
             if ips:
                 await self.relay.create_permission(ips)
         except (TurnError, OSError, asyncio.TimeoutError) as e:
@@ -495,6 +604,10 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                 return
             # we are the DTLS server: odd stream ids for channels we open; the browser opens
             self.dc = _native().net.DataChannelEndpoint(True, 5000, self.answer.remote_sctp_port)
+            for label in self.server_channels:  # queued until the association is up
+                cid, out = self.dc.open(label)
+                self.dc_channels[cid] = label
+                self._sctp_out(out, addr)
         self._sctp_out(self.dc.feed(pkt), addr)
         self._dc_events()
 

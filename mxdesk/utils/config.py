@@ -153,6 +153,8 @@ SCHEMA: list[Var] = [
     Var("js_dir", ["MXDESK_JS_DIR"], "/tmp", str, "directory of the joystick interposer sockets"),
     Var("webrtc_host", ["MXDESK_WEBRTC_HOST"], "", str, "address advertised in the WebRTC host candidate"),
     Var("webrtc_udp_port", ["MXDESK_WEBRTC_UDP_PORT"], 0, int, "UDP port for WebRTC media (0 = ephemeral)"),
+    Var("selkies_peer", ["MXDESK_SELKIES_PEER"], True, bool,
+        "the streaming peer on /ws offers a stream to every registering selkies client"),
     Var("turn_relay", ["MXDESK_TURN_RELAY"], True, bool,
         "allocate a server-side TURN relay candidate when TURN_HOST + credentials are set"),
     Var("log_dir", ["MXDESK_LOG_DIR"], "/tmp", str, "log directory", ref="supervisord.conf:9"),

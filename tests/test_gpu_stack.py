@@ -75,6 +75,34 @@ def test_gpu_pipeline_over_webrtc(gpu, monkeypatch):
     assert all(b == a + 1 for a, b in zip(ids, ids[1:]))
 
 
+def test_gpu_pipeline_over_selkies_signalling(gpu, monkeypatch):
+    """GPU encoder -> selkies streaming peer on /ws (server offer, client answer) -> DTLS-SRTP
+    -> independent decoder; input messages on the server-opened ``input`` channel."""
+    from mxdesk.pipeline.stream import StreamPipeline
+    from mxdesk.server.app import MediaServer, serve
+    from mxdesk.server.selkies_client import selkies_view
+    from mxdesk.utils import config as C
+
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg = C.load(env={"ENABLE_BASIC_AUTH": "false", "SIZEW": "320", "SIZEH": "192"}, argv=[])
+    pipe = StreamPipeline(320, 192, 60, backend="gpu", bitrate_kbps=0)
+    srv = MediaServer(pipe, cfg)
+
+    async def go():
+        port = _free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await selkies_view(f"ws://127.0.0.1:{port}/ws", 12, dc_messages=["m,10,20,0,0"])
+        finally:
+            await runner.cleanup()
+
+    res = asyncio.run(go())
+    frames = Decoder().decode(res.stream)
+    assert len(frames) == 12 and res.dc_labels == ["input"]
+    ids = [read_barcode(y)[0] for y, _, _ in frames]
+    assert all(b == a + 1 for a, b in zip(ids, ids[1:]))
+
+
 def test_gpu_live_resize_and_webrtc_datachannel_input(gpu, monkeypatch):
     """Client-driven resize on the HIP session (new Session at the new size, IDR first, the
     independent decoder sees the new dimensions) and input over the SCTP data channel."""

@@ -104,7 +104,8 @@ def test_basic_auth_and_endpoints():
 
 
 def test_signalling_relay():
-    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+    # browser <-> browser relaying (the in-process streaming peer off: it would take uid 0)
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "MXDESK_SELKIES_PEER": "false"})
 
     async def go():
         port = free_port()
