@@ -153,6 +153,10 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("pipeline_depth", &h264::EncoderConfig::pipeline_depth)
         .def_readwrite("aq", &h264::EncoderConfig::aq)
         .def_readwrite("intra_in_p", &h264::EncoderConfig::intra_in_p)
+        .def_readwrite("mask_x0", &h264::EncoderConfig::mask_x0)
+        .def_readwrite("mask_y0", &h264::EncoderConfig::mask_y0)
+        .def_readwrite("mask_x1", &h264::EncoderConfig::mask_x1)
+        .def_readwrite("mask_y1", &h264::EncoderConfig::mask_y1)
         .def_readwrite("deblock", &h264::EncoderConfig::deblock)
         .def_readwrite("tu_split", &h264::EncoderConfig::tu_split);
 
@@ -163,7 +167,9 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("bytes", &h264::FrameStats::bytes)
         .def_readonly("skipped_mbs", &h264::FrameStats::skipped_mbs)
         .def_readonly("encode_ms", &h264::FrameStats::encode_ms)
-        .def_property_readonly("sse", [](const h264::FrameStats& s) { return py::make_tuple(s.sse[0], s.sse[1], s.sse[2]); });
+        .def_property_readonly("sse", [](const h264::FrameStats& s) { return py::make_tuple(s.sse[0], s.sse[1], s.sse[2]); })
+        .def_readonly("sse_masked", &h264::FrameStats::sse_masked)
+        .def_readonly("masked_pixels", &h264::FrameStats::masked_pixels);
 
     py::class_<h264::CpuH264Encoder>(m, "CpuH264Encoder")
         .def(py::init<const h264::EncoderConfig&>())
@@ -345,16 +351,24 @@ PYBIND11_MODULE(_native, m) {
     m.def(
         "synth",
         [](uintptr_t out, int w, int h, int pitch, uint32_t frame_id, uint32_t ts, float t, int noise, int ox, int oy,
-           int wall_w, int wall_h, int cx, int cy, uintptr_t stream) {
+           int wall_w, int wall_h, int cx, int cy, uintptr_t stream, uintptr_t static_bg) {
             pix::SynthParams p{w, h, pitch, frame_id, ts, t, ox, oy, wall_w > 0 ? wall_w : w, wall_h > 0 ? wall_h : h,
                                noise, cx, cy};
-            pix::launch_synth(as_ptr<uint8_t>(out), p, as_stream(stream));
+            pix::launch_synth(as_ptr<uint8_t>(out), p, as_stream(stream), as_ptr<const uint8_t>(static_bg));
             HIP_CHECK(hipGetLastError());
         },
         py::arg("out_ptr"), py::arg("width"), py::arg("height"), py::arg("pitch"), py::arg("frame_id") = 0,
         py::arg("timestamp_us") = 0, py::arg("t") = 0.f, py::arg("noise") = 1, py::arg("origin_x") = 0,
         py::arg("origin_y") = 0, py::arg("wall_w") = 0, py::arg("wall_h") = 0, py::arg("cursor_x") = -1,
-        py::arg("cursor_y") = -1, py::arg("stream") = 0);
+        py::arg("cursor_y") = -1, py::arg("stream") = 0, py::arg("static_bg") = 0);
+    m.def(
+        "synth_static",
+        [](uintptr_t out, int w, int h, int pitch, uintptr_t stream) {
+            pix::SynthParams p{w, h, pitch, 0, 0, 0.f, 0, 0, w, h, 1, -1, -1};
+            pix::launch_synth_static(as_ptr<uint8_t>(out), p, as_stream(stream));
+            HIP_CHECK(hipGetLastError());
+        },
+        py::arg("out_ptr"), py::arg("width"), py::arg("height"), py::arg("pitch"), py::arg("stream") = 0);
     m.def(
         "bgrx_to_nv12",
         [](uintptr_t in, int in_pitch, int w, int h, uintptr_t y, uintptr_t uv, int out_pitch, int cw, int ch,

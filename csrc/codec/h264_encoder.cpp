@@ -255,7 +255,7 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     // payload capacity: 768 B per MB (intra at low QP stays far below)
     b.out_bytes = (size_t)nmb * 768;
     HIP_CHECK(hipMalloc(&b.out_hdr, sizeof(OutHeader)));
-    HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * kSsePartStride));
+    HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * kSsePartStride));
     HIP_CHECK(hipMalloc(&b.wave_prog, sizeof(int) * 4));
     HIP_CHECK(hipMalloc(&b.mb_sse, sizeof(uint32_t) * 3 * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.intra_gain, sizeof(int32_t) * (size_t)nmb));
@@ -306,6 +306,17 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMemsetAsync(rec_y_[i], 16, ysz, stream_));
         HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
     }
+    if (cfg.mask_x1 > cfg.mask_x0 && cfg.mask_y1 > cfg.mask_y0) {
+        mask_mb_[0] = std::max(0, cfg.mask_x0) / 16;
+        mask_mb_[1] = std::max(0, cfg.mask_y0) / 16;
+        mask_mb_[2] = std::min(geom_.mb_w, (cfg.mask_x1 + 15) / 16);
+        mask_mb_[3] = std::min(geom_.mb_h, (cfg.mask_y1 + 15) / 16);
+    }
+    masked_pixels_ = (int64_t)cfg.width * cfg.height;
+    for (int my = mask_mb_[1]; my < mask_mb_[3]; ++my)
+        for (int mx = mask_mb_[0]; mx < mask_mb_[2]; ++mx)
+            masked_pixels_ -= (int64_t)std::max(0, std::min(16, cfg.width - 16 * mx)) *
+                              std::max(0, std::min(16, cfg.height - 16 * my));
     hp_pitch_ = (geom_.coded_w + 2 * kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
@@ -372,6 +383,10 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.aq = cfg_.aq;
     f.intra_in_p = cfg_.intra_in_p;
     f.frame_tag = (int32_t)++frame_tag_;  // tags start at 1: the zeroed line buffer never matches
+    f.mask_mx0 = mask_mb_[0];
+    f.mask_my0 = mask_mb_[1];
+    f.mask_mx1 = mask_mb_[2];
+    f.mask_my1 = mask_mb_[3];
     f.hp_f = hp_[0] + org;
     f.hp_h = hp_[1] + org;
     f.hp_v = hp_[2] + org;
@@ -469,6 +484,8 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     stats_.bytes = (int)au_.size();
     stats_.encode_ms = ms;
     for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
+    stats_.sse_masked = hdr.sse_masked;
+    stats_.masked_pixels = masked_pixels_;
     common_.end_frame((int)au_.size(), sl.idr);
     return au_;
 }

@@ -38,6 +38,9 @@ struct EncoderConfig {
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
+    // quality report: luma distortion outside the macroblocks touching this pixel rectangle
+    // (FrameStats::sse_masked; mask_x1 <= mask_x0 = no mask)
+    int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;
     int pipeline_depth = 1;   // GPU frames in flight: 2 overlaps frame n's entropy coding with
                               // frame n+1's analysis on a second HIP stream (rate control lags a frame)
 };
@@ -50,6 +53,8 @@ struct FrameStats {
     int skipped_mbs = 0;
     double encode_ms = 0;
     uint64_t sse[3] = {0, 0, 0};  // source vs reconstruction (Y, U, V), display area
+    uint64_t sse_masked = 0;      // Y outside the mask macroblocks (EncoderConfig::mask_*)
+    int64_t masked_pixels = 0;    // display luma samples outside them (the PSNR denominator)
 };
 
 // Annex-B / rate-control logic shared by both encoders.
@@ -214,6 +219,8 @@ class GpuH264Encoder final : public VideoEncoder {
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
     uint32_t frame_tag_ = 0;
+    int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
+    int64_t masked_pixels_ = 0;
     std::vector<uint8_t> au_;
     FrameStats stats_;
 };

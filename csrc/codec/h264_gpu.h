@@ -47,6 +47,11 @@ struct MbInfo {
 static_assert(sizeof(MbInfo) == 48, "MbInfo layout");
 
 MXHD_GPU bool is_intra(const MbInfo& m) { return m.type != kMbP16x16; }
+// Whether macroblock (mbx, mby) is outside the quality-report mask of the frame state.
+template <class FS>
+MXHD_GPU bool mb_unmasked(const FS* fs, int mbx, int mby) {
+    return !(mbx >= fs->mask_mx0 && mbx < fs->mask_mx1 && mby >= fs->mask_my0 && mby < fs->mask_my1);
+}
 // mb_qp_delta present: Intra16x16 always, other macroblocks when they carry residual.
 MXHD_GPU bool carries_dqp(const MbInfo& m) { return m.type == kMbI16x16 || m.cbp != 0; }
 
@@ -73,12 +78,15 @@ struct FrameState {
     int32_t aq;        // adaptive quantisation on/off (P frames)
     int32_t intra_in_p;  // P frames: k_intra_analyze / k_intra_wave run (distortion deltas included)
     int32_t frame_tag;   // nonzero, new every frame: validity tag of k_intra_wave's line buffer words
+    // quality report: MBs in [mask_mx0, mask_mx1) x [mask_my0, mask_my1) are left out of the 4th
+    // distortion channel (e.g. the synthetic desktop's noise panel); empty rect = no mask
+    int32_t mask_mx0, mask_my0, mask_mx1, mask_my1;
     // padded reference planes (origin at picture (0,0), valid for x,y in [-kHpelPad, size+kHpelPad))
     const uint8_t* hp_f;  // full-sample (edge-replicated)
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
     const uint8_t* hp_v;  // vertical half sample h at (x, y+1/2)
     const uint8_t* hp_j;  // centre half sample j at (x+1/2, y+1/2)
-    // distortion partials (Y, U, V) over the display area, [3][kSsePartStride]: one per
+    // distortion partials (Y, U, V, Y outside the mask MBs) over the display area, [4][kSsePartStride]: one per
     // inter workgroup / intra MB row, reduced by k_scan into OutHeader (no atomics)
     unsigned long long* sse_part;
 };
@@ -92,7 +100,7 @@ struct OutHeader {
     uint32_t overflow;     // nonzero if any MB exceeded its slot
     uint32_t pad;
     uint64_t sse[3];       // source vs reconstruction squared error (Y, U, V)
-    uint64_t pad2;
+    uint64_t sse_masked;   // Y outside the mask macroblocks (FrameState::mask_*)
 };
 static_assert(sizeof(OutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
@@ -124,7 +132,7 @@ struct DeviceBuffers {
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
-    unsigned long long* sse_part;       // [3 * kSsePartStride] distortion partials
+    unsigned long long* sse_part;       // [4 * kSsePartStride] distortion partials
     int* wave_prog;         // [0] k_intra_wave row ticket, [1] intra candidate count
     uint64_t* wave_line;    // [mb_h * coded_w / 2] k_intra_wave: tagged bottom sample lines of intra MBs
     int32_t* intra_gain;    // [nmb] P frames: gain of switching each MB to intra (0 = stays inter)

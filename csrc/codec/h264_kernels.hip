@@ -545,14 +545,15 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
         if (valid && fs->intra_in_p && lane < 3)  // per-MB copy: replaced if the MB switches to intra
             mb_sse[lane * nmb + mbi] = (uint32_t)(lane == 0 ? sy : (lane == 1 ? su : sv));
-        __shared__ uint32_t part[3][4];
+        __shared__ uint32_t part[4][4];
         if (lane == 0) {
             part[0][wave] = valid ? (uint32_t)sy : 0u;
             part[1][wave] = valid ? (uint32_t)su : 0u;
             part[2][wave] = valid ? (uint32_t)sv : 0u;
+            part[3][wave] = (valid && mb_unmasked(fs, mbx, mby)) ? (uint32_t)sy : 0u;
         }
         __syncthreads();
-        if (threadIdx.x < 3) {
+        if (threadIdx.x < 4) {
             const int c = threadIdx.x;
             fs->sse_part[c * kSsePartStride + bid] =
                 (unsigned long long)part[c][0] + part[c][1] + part[c][2] + part[c][3];
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) wave_prog[0] = 0;  // k_intra_wave's row ticket
         if (!fs->idr)  // k_intra_p's per-row distortion deltas (atomically accumulated)
-            for (int i = threadIdx.x; i < 3 * g.mb_h; i += 256)
+            for (int i = threadIdx.x; i < 4 * g.mb_h; i += 256)
                 fs->sse_part[(i / g.mb_h) * kSsePartStride + (g.mb_w * g.mb_h + 3) / 4 + i % g.mb_h] = 0;
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1004,7 +1005,7 @@ __global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState
     __shared__ uint32_t cs[32];          // source chroma of the current MB (8 rows x 16 interleaved bytes)
     __shared__ int ldc[16], cdc[8];
     __shared__ int s_row;
-    __shared__ unsigned long long s_sse[3];
+    __shared__ unsigned long long s_sse[4];
     __shared__ uint8_t rintra[2][kMaxMbW];  // intra flags of this row's / the row above's macroblocks
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // rows are taken in dispatch order (ticket): a row only ever waits on rows already running
@@ -1024,7 +1025,8 @@ __global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState
     const uint64_t* up_line = wave_line + (size_t)(mby > 0 ? mby - 1 : 0) * line_words + (wave ? g.coded_w / 4 : 0);
     int last_coded = -2;  // the left neighbour's reconstruction is in the tile when last_coded == mbx - 1
     uint32_t sse_a = 0, sse_b = 0;  // luma wave: Y; chroma wave: U, V
-    uint32_t old_a = 0, old_b = 0, old_c = 0;  // P pictures: inter distortion of the replaced MBs
+    uint32_t sse_m = 0;             // luma wave: Y of the MBs outside the quality-report mask
+    uint32_t old_a = 0, old_b = 0, old_c = 0, old_m = 0;  // P pictures: inter distortion of the replaced MBs
     // software pipeline: the source samples and fields of the next intra MB are loaded while the
     // current one is coded (one dword of source per lane)
     auto next_intra = [&](int from) {
@@ -1070,7 +1072,12 @@ __global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState
             if (lane < 16) lt[1 + lane][0] = left_in_tile ? keep : lft;
             if (lane < 21) lt[0][lane] = top;
             wave_sync_lds();
-            intra_luma_mb(g, f, reinterpret_cast<const uint8_t*>(ls), m, mc, mbx, mby, av, lt, ldc, lane, sse_a);
+            uint32_t sse_mb = 0;
+            intra_luma_mb(g, f, reinterpret_cast<const uint8_t*>(ls), m, mc, mbx, mby, av, lt, ldc, lane, sse_mb);
+            sse_a += sse_mb;
+            const bool unmasked = mb_unmasked(fs, mbx, mby);
+            if (unmasked) sse_m += sse_mb;
+            if (!idr && unmasked && lane == 0) old_m += mb_sse[mbi];
             {  // tile -> reconstruction: 16 rows x 16 bytes, one dword per lane; bottom line -> buffer
                 const int r = lane >> 2, c4 = (lane & 3) * 4;
                 const uint32_t v = (uint32_t)lt[1 + r][1 + c4] | ((uint32_t)lt[1 + r][2 + c4] << 8) |
@@ -1121,14 +1128,16 @@ __global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState
     }
     // distortion of the row: absolute (IDR: one partial per row) or, in P pictures, the delta
     // of the switched macroblocks against their inter distortion (modulo-2^64 sums)
-    unsigned long long a = sse_a, b = sse_b;
+    unsigned long long a = sse_a, b = sse_b, mm = sse_m;
     for (int o = 32; o > 0; o >>= 1) {
         a += __shfl_xor(a, o, 64);
         b += __shfl_xor(b, o, 64);
+        mm += __shfl_xor(mm, o, 64);
     }
     if (lane == 0) {
         if (wave == 0) {
             s_sse[0] = a - old_a;
+            s_sse[3] = mm - old_m;
         } else {
             s_sse[1] = a - old_b;
             s_sse[2] = b - old_c;
@@ -1139,7 +1148,7 @@ __global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState
         MbInfo& m = mbs[mby * g.mb_w + mbx];
         if (idr || is_intra(m)) m.cbp = (uint8_t)((m.cbp & 15) | (m.cbp_c << 4));
     }
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 4) {
         const int slot = idr ? mby : (g.mb_w * g.mb_h + 3) / 4 + mby;
         fs->sse_part[threadIdx.x * kSsePartStride + slot] = s_sse[threadIdx.x];
     }
@@ -1226,6 +1235,7 @@ __device__ void intra_p_mb(const Geometry& g, const FrameState* __restrict__ fs,
         if (wave == 0) {
             m.cbp = (uint8_t)((m.cbp & 15) | (m.cbp_c << 4));
             atomicAdd(&fs->sse_part[slot], a - mb_sse[mbi]);
+            if (mb_unmasked(fs, mbx, mby)) atomicAdd(&fs->sse_part[3 * kSsePartStride + slot], a - mb_sse[mbi]);
         } else {
             atomicAdd(&fs->sse_part[kSsePartStride + slot], a - mb_sse[nmb + mbi]);
             atomicAdd(&fs->sse_part[2 * kSsePartStride + slot], b - mb_sse[2 * nmb + mbi]);
@@ -1557,20 +1567,23 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         // partials: one per intra MB row (IDR) or per inter workgroup (4 MBs) + the per-row
         // intra deltas of k_intra_wave (P pictures with intra macroblocks)
         const int nparts = idr ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
-        unsigned long long acc[3] = {0, 0, 0};
+        unsigned long long acc[4] = {0, 0, 0, 0};
         for (int i = t; i < nparts; i += kScanThreads)
-            for (int c = 0; c < 3; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
-        __shared__ unsigned long long red[3][kScanThreads / 64];
-        for (int c = 0; c < 3; ++c) {
+            for (int c = 0; c < 4; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
+        __shared__ unsigned long long red[4][kScanThreads / 64];
+        for (int c = 0; c < 4; ++c) {
             unsigned long long v = acc[c];
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
             if ((t & 63) == 0) red[c][t >> 6] = v;
         }
         __syncthreads();
-        if (t < 3) {
+        if (t < 4) {
             unsigned long long v = 0;
             for (int w = 0; w < kScanThreads / 64; ++w) v += red[t][w];
-            hdr->sse[t] = v;
+            if (t < 3)
+                hdr->sse[t] = v;
+            else
+                hdr->sse_masked = v;
         }
     }
 }

@@ -25,9 +25,13 @@ struct SynthParams {
 constexpr int kBarCell = 8;
 constexpr int kBarX = 8, kBarY = 8;
 
-void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream);
+// static_bg: the static-layer cache rendered by launch_synth_static for the same size /
+// pitch / origin (pixels outside the animated elements are copied from it), or nullptr.
+void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream, const uint8_t* static_bg = nullptr);
+void launch_synth_static(uint8_t* bgrx, const SynthParams& p, hipStream_t stream);
 // Same, reading the parameters from device memory (hipGraph replay; width/height fix the grid).
-void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int height, hipStream_t stream);
+void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int height, hipStream_t stream,
+                      const uint8_t* static_bg = nullptr);
 
 // BGRx -> NV12 (BT.709 limited range), padding the output to (coded_w, coded_h) by edge
 // replication.  Output Y plane pitch = UV plane pitch = out_pitch.

@@ -66,6 +66,43 @@ __device__ __forceinline__ bool gear_hit(float gx, float gy, float inner, float 
     return true;
 }
 
+__device__ __attribute__((noinline)) uint32_t static_px(int gx, int gy, const SynthParams& p);
+
+// Axis-aligned bounds of everything animated (barcode, cursor, moving window, gears,
+// terminal, noise panel); outside them desktop_px() == static_px().
+struct DynBoxes {
+    int x0[6], y0[6], x1[6], y1[6];
+};
+__device__ __forceinline__ DynBoxes dyn_boxes(const SynthParams& p) {
+    const int W = p.wall_w, H = p.wall_h;
+    DynBoxes b;
+    b.x0[0] = kBarX - kBarCell; b.y0[0] = kBarY - kBarCell;
+    b.x1[0] = kBarX + 33 * kBarCell; b.y1[0] = kBarY + 3 * kBarCell;
+    b.x0[1] = p.cursor_x >= 0 ? p.cursor_x : 0; b.y0[1] = p.cursor_y;
+    b.x1[1] = p.cursor_x >= 0 ? p.cursor_x + 12 : 0; b.y1[1] = p.cursor_y + 19;
+    const int mw = W / 8 > 48 ? W / 8 : 48, mh = H / 8 > 32 ? H / 8 : 32;
+    b.x0[2] = (int)(W * 0.5f + W * 0.18f * sinf(p.t * 0.7f)) - mw / 2;
+    b.y0[2] = (int)(H * 0.62f + H * 0.12f * sinf(p.t * 1.1f)) - mh / 2;
+    b.x1[2] = b.x0[2] + mw; b.y1[2] = b.y0[2] + mh;
+    b.x0[3] = (int)(W * 0.55f); b.y0[3] = (int)(H * 0.10f);
+    b.x1[3] = b.x0[3] + (int)(W * 0.38f); b.y1[3] = b.y0[3] + (int)(H * 0.50f);
+    b.x0[4] = (int)(W * 0.04f); b.y0[4] = (int)(H * 0.10f);
+    b.x1[4] = b.x0[4] + (int)(W * 0.42f); b.y1[4] = b.y0[4] + (int)(H * 0.38f);
+    b.x0[5] = (int)(W * 0.04f); b.y0[5] = (int)(H * 0.55f);
+    b.x1[5] = p.noise ? b.x0[5] + (int)(W * 0.16f) : b.x0[5]; b.y1[5] = b.y0[5] + (int)(H * 0.22f);
+    return b;
+}
+// Whether any of pixels [gx, gx+n) of row gy lies in an animated element's bounds.
+// (2-pixel margin: the moving window's float position may round differently here than in
+// desktop_px() under FMA contraction; margin pixels are rendered exactly, not copied)
+__device__ __forceinline__ bool in_dyn(const DynBoxes& b, int gx, int n, int gy) {
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        hit |= b.x1[k] > b.x0[k] && gy >= b.y0[k] - 2 && gy < b.y1[k] + 2 && gx + n > b.x0[k] - 2 && gx < b.x1[k] + 2;
+    return hit;
+}
+
 __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
     const int W = p.wall_w, H = p.wall_h;
     // ---- barcode (frame id + timestamp), always on top
@@ -148,6 +185,16 @@ __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
             return bgrx(v, (h >> 8) & 0xff, v);
         }
     }
+    return static_px(gx, gy, p);
+}
+
+// The parts of the desktop that never change (document window, taskbar, wallpaper): rendered
+// once per session into a cache that the per-frame kernel copies wherever no animated element
+// covers the pixel (the per-pixel wallpaper sinf was most of k_synth's 17 us at 1080p).
+// noinline: one instance for both callers (k_synth_static and desktop_px), so the float
+// wallpaper math cannot round differently under per-site FMA contraction.
+__device__ __attribute__((noinline)) uint32_t static_px(int gx, int gy, const SynthParams& p) {
+    const int W = p.wall_w, H = p.wall_h;
     // ---- static text window (document)
     {
         const int x0 = (int)(W * 0.25f), y0 = (int)(H * 0.52f);
@@ -177,13 +224,21 @@ __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
     return bgrx((int)(20 + 40 * fy + 20 * band), (int)(40 + 60 * fy + 10 * band), (int)(90 + 110 * (1.f - fy * 0.5f)));
 }
 
-__device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const SynthParams& p) {
+// bg: the session's static-layer cache (same size / pitch / origin), or nullptr.
+__device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const SynthParams& p,
+                                           const uint8_t* __restrict__ bg) {
     const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (y >= p.height || x4 >= p.width) return;
     uint32_t v[4];
+    const int gx = p.origin_x + x4, gy = p.origin_y + y;
+    if (bg != nullptr && x4 + 4 <= p.width && !in_dyn(dyn_boxes(p), gx, 4, gy)) {
+        const uint4 c = *reinterpret_cast<const uint4*>(bg + (size_t)y * p.pitch + 4 * x4);
+        v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = (x4 + k < p.width) ? desktop_px(p.origin_x + x4 + k, p.origin_y + y, p) : 0u;
+        for (int k = 0; k < 4; ++k) v[k] = (x4 + k < p.width) ? desktop_px(gx + k, gy, p) : 0u;
+    }
     uint32_t* row = reinterpret_cast<uint32_t*>(out + (size_t)y * p.pitch);
     if (x4 + 4 <= p.width) {
         *reinterpret_cast<uint4*>(row + x4) = make_uint4(v[0], v[1], v[2], v[3]);
@@ -192,13 +247,22 @@ __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const Synt
     }
 }
 
-__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, SynthParams p) { synth_body(out, p); }
+__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, SynthParams p, const uint8_t* __restrict__ bg) {
+    synth_body(out, p, bg);
+}
+
+__global__ __launch_bounds__(256) void k_synth_static(uint8_t* __restrict__ out, SynthParams p) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= p.width || y >= p.height) return;
+    reinterpret_cast<uint32_t*>(out + (size_t)y * p.pitch)[x] = static_px(p.origin_x + x, p.origin_y + y, p);
+}
 
 // Graph-replay variant: per-frame parameters come from device memory (uploaded by a memcpy
 // node of the same graph), so the captured kernel node never changes.
-__global__ __launch_bounds__(256) void k_synth_dev(uint8_t* __restrict__ out, const SynthParams* __restrict__ pp) {
+__global__ __launch_bounds__(256) void k_synth_dev(uint8_t* __restrict__ out, const SynthParams* __restrict__ pp,
+                                                   const uint8_t* __restrict__ bg) {
     const SynthParams p = *pp;
-    synth_body(out, p);
+    synth_body(out, p, bg);
 }
 
 // BT.709 limited-range integer coefficients (x256); each row sums to 220 / 0 / 0.
@@ -443,16 +507,25 @@ void launch_sse_masked(const uint8_t* a, const uint8_t* b, int pitch, int w, int
                        mx0, my0, mx1, my1, part, counter, host_out);
 }
 
-void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream) {
+void launch_synth(uint8_t* bgrx, const SynthParams& p, hipStream_t stream, const uint8_t* static_bg) {
+    if (static_bg != nullptr && ((p.pitch & 15) || (reinterpret_cast<uintptr_t>(static_bg) & 15)))
+        throw std::invalid_argument("synth: the static-layer cache needs a 16-byte aligned pitch");
     dim3 block(64, 4);
     dim3 grid((p.width / 4 + 63) / 64 + 1, (p.height + 3) / 4);
-    hipLaunchKernelGGL(k_synth, grid, block, 0, stream, bgrx, p);
+    hipLaunchKernelGGL(k_synth, grid, block, 0, stream, bgrx, p, static_bg);
 }
 
-void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int height, hipStream_t stream) {
+void launch_synth_static(uint8_t* bgrx, const SynthParams& p, hipStream_t stream) {
+    dim3 block(64, 4);
+    dim3 grid((p.width + 63) / 64, (p.height + 3) / 4);
+    hipLaunchKernelGGL(k_synth_static, grid, block, 0, stream, bgrx, p);
+}
+
+void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int height, hipStream_t stream,
+                      const uint8_t* static_bg) {
     dim3 block(64, 4);
     dim3 grid((width / 4 + 63) / 64 + 1, (height + 3) / 4);
-    hipLaunchKernelGGL(k_synth_dev, grid, block, 0, stream, bgrx, d_params);
+    hipLaunchKernelGGL(k_synth_dev, grid, block, 0, stream, bgrx, d_params, static_bg);
 }
 
 void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_t* y, uint8_t* uv, int out_pitch,

@@ -73,6 +73,12 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     cfg_.enc.width = cfg_.out_width;
     cfg_.enc.height = cfg_.out_height;
     cfg_.enc.fps = cfg_.fps;
+    // the H.264 encoder reports the masked distortion itself (a 4th channel of its per-MB
+    // partials, MB-aligned mask); other codecs use the separate k_sse_masked pass
+    cfg_.enc.mask_x0 = cfg_.mask_x0;
+    cfg_.enc.mask_y0 = cfg_.mask_y0;
+    cfg_.enc.mask_x1 = cfg_.mask_x1;
+    cfg_.enc.mask_y1 = cfg_.mask_y1;
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     pool_ = std::make_unique<FramePool>(cfg_.width, cfg_.height, cfg_.pool_slots);
     if (cfg_.codec == "h264" || cfg_.codec == "avc")
@@ -116,7 +122,8 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         HIP_CHECK(hipMemcpy(p, wy.data(), wy.size() * 4, hipMemcpyHostToDevice));
     }
     for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
-    if (masked()) {
+    mask_in_encoder_ = std::string(enc_->codec()) == "h264";
+    if (masked() && !mask_in_encoder_) {
         const h264::Geometry& eg = enc_->geometry();
         const int nb = pix::sse_masked_blocks(eg.width, eg.height);
         HIP_CHECK(hipMalloc(&mask_dev_, 2 * (size_t)nb * sizeof(unsigned long long)));
@@ -127,6 +134,11 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_mask_[k], hipEventDisableTiming));
     }
     HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams), hipHostMallocDefault));
+    // static layer of the synthetic desktop, rendered once (k_synth copies it outside the
+    // animated elements)
+    HIP_CHECK(hipMalloc(&synth_bg_, (size_t)pool_->pitch() * cfg_.height));
+    pix::launch_synth_static(synth_bg_, synth_params(), stream_);
+    HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams)));
     graphs_.assign((size_t)cfg_.pool_slots * 2, nullptr);
     t0_us_ = now_us();
@@ -137,6 +149,7 @@ Session::~Session() {
     for (auto g : graphs_)
         if (g) hipGraphExecDestroy(g);
     hipHostFree(synth_host_);
+    if (synth_bg_) hipFree(synth_bg_);
     hipFree(synth_dev_);
     enc_.reset();
     pool_.reset();
@@ -176,7 +189,7 @@ void Session::convert_and_encode(int slot, bool force_idr) {
 void Session::enqueue_mask_sse(int k) {
     // after the analysis kernels on stream_ (reconstruction final, source not yet overwritten
     // by the next frame's conversion, which is later on the same stream)
-    if (!masked()) return;
+    if (!masked() || mask_in_encoder_) return;
     const h264::EncoderConfig& e = enc_->rc().config();
     pix::launch_sse_masked(nv12_y_, enc_->recon_y(), enc_->pitch(), e.width, e.height, cfg_.mask_x0, cfg_.mask_y0,
                            cfg_.mask_x1, cfg_.mask_y1, mask_dev_ + (size_t)k * mask_stride_, mask_counter_ + k,
@@ -218,7 +231,7 @@ hipGraphExec_t Session::capture_frame_graph(int slot, bool idr) {
     HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
     try {
         HIP_CHECK(hipMemcpyAsync(synth_dev_, synth_host_, sizeof(pix::SynthParams), hipMemcpyHostToDevice, stream_));
-        pix::launch_synth_dev(pool_->data(slot), synth_dev_, cfg_.width, cfg_.height, stream_);
+        pix::launch_synth_dev(pool_->data(slot), synth_dev_, cfg_.width, cfg_.height, stream_, synth_bg_);
         HIP_CHECK(hipGetLastError());
         convert(slot);
         enc_->enqueue_body(idr, nv12_y_, nv12_uv_);
@@ -244,7 +257,7 @@ void Session::submit_synthetic(bool force_idr) {
     // the first CBR frame runs eagerly: its rate-control probe encodes synchronously
     if (!cfg_.use_graph || enc_->rc().wants_probe()) {
         HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
-        pix::launch_synth(pool_->data(slot), p, stream_);
+        pix::launch_synth(pool_->data(slot), p, stream_, synth_bg_);
         HIP_CHECK(hipGetLastError());
         convert_and_encode(slot, force_idr);
         return;
@@ -296,7 +309,9 @@ FrameResult Session::collect() {
     r.psnr_y = psnr(st.sse[0], ny);
     r.psnr_u = psnr(st.sse[1], nc);
     r.psnr_v = psnr(st.sse[2], nc);
-    if (masked()) {
+    if (masked() && mask_in_encoder_) {
+        r.psnr_y_masked = psnr(st.sse_masked, (double)std::max<int64_t>(1, st.masked_pixels));
+    } else if (masked()) {
         HIP_CHECK(hipEventSynchronize(ev_mask_[fl.k]));
         const double mw = std::max(0, std::min(cfg_.mask_x1, enc_->rc().config().width) - std::max(0, cfg_.mask_x0));
         const double mh = std::max(0, std::min(cfg_.mask_y1, enc_->rc().config().height) - std::max(0, cfg_.mask_y0));

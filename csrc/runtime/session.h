@@ -146,6 +146,7 @@ class Session {
     int mask_stride_ = 0;
     hipEvent_t ev_mask_[2] = {nullptr, nullptr};
     bool masked() const { return cfg_.mask_x1 > cfg_.mask_x0 && cfg_.mask_y1 > cfg_.mask_y0; }
+    bool mask_in_encoder_ = false;  // H.264: the encoder reports the masked distortion itself
     void enqueue_mask_sse(int k);
     int next_k_ = 0;
     int depth_ = 1;
@@ -153,6 +154,7 @@ class Session {
     // (pool slot, frame type) -- the only things that change the captured node arguments
     pix::SynthParams* synth_host_ = nullptr;
     pix::SynthParams* synth_dev_ = nullptr;
+    uint8_t* synth_bg_ = nullptr;  // static layer of the synthetic desktop (rendered once)
     std::vector<hipGraphExec_t> graphs_;
     int graphs_built_ = 0;
     uint32_t frame_id_ = 0;  // id of the next submitted frame

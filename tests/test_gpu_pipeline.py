@@ -177,6 +177,33 @@ def test_session_scaled_output(gpu):
     assert frames[0][0].shape == (192, 320)
 
 
+@pytest.mark.parametrize("intra_in_p", [0, 1])
+def test_session_masked_psnr_from_encoder(gpu, intra_in_p):
+    """The H.264 encoder's 4th distortion channel (luma outside the macroblocks touching the
+    mask rectangle) equals the PSNR of the decoded picture over those samples (IDR wavefront,
+    inter and intra-in-P paths)."""
+    cfg = gpu.SessionConfig()
+    cfg.width, cfg.height, cfg.fps = 200, 120, 60
+    cfg.enc.bitrate_kbps = 0
+    cfg.enc.qp = 30
+    cfg.enc.intra_in_p = intra_in_p
+    cfg.mask_x0, cfg.mask_y0, cfg.mask_x1, cfg.mask_y1 = 20, 40, 90, 75  # -> MBs x 1..5, y 2..4
+    s = gpu.Session(cfg)
+    stream, res, srcs = b"", [], []
+    for _ in range(4):
+        r = s.step(False)
+        stream += r.au
+        res.append(r)
+        srcs.append(s.nv12()[0][:120, :200].astype(np.float64))
+    frames = Decoder().decode(stream)
+    keep = np.ones((120, 200), bool)
+    keep[32:80, 16:96] = False
+    for (dy, _, _), sy, r in zip(frames, srcs, res):
+        mse = np.mean(((dy.astype(np.float64) - sy) ** 2)[keep])
+        want = 99.0 if mse == 0 else min(99.0, 10 * np.log10(255.0 ** 2 / mse))
+        assert abs(want - r.psnr_y_masked) < 1e-6, (want, r.psnr_y_masked)
+
+
 def test_session_reports_psnr_of_reconstruction(gpu):
     """Encoder-side SSE (k_inter_encode / k_intra_rows -> k_scan) equals the PSNR of the
     independently decoded picture against the source, over the display area only."""
@@ -293,3 +320,20 @@ def test_hpel_planes_match_reference(gpu, w, h):
         g = got[: exp.shape[0], : exp.shape[1]]
         bad = np.argwhere(g != exp)
         assert bad.size == 0, f"plane {name}: {len(bad)} mismatches, first at {bad[:3].tolist()}"
+
+
+def test_synth_static_cache_matches_full_render(gpu):
+    """k_synth with the static-layer cache == the full per-pixel render, at several animation
+    times (moving window, cursor) and sizes."""
+    for w, h in [(512, 288), (1920, 1080)]:
+        pitch = w * 4
+        bg = torch.zeros((h, pitch), dtype=torch.uint8, device="cuda")
+        gpu.synth_static(bg.data_ptr(), w, h, pitch, _stream())
+        for t in (0.0, 0.37, 1.9, 7.25):
+            a = torch.zeros((h, pitch), dtype=torch.uint8, device="cuda")
+            b = torch.zeros((h, pitch), dtype=torch.uint8, device="cuda")
+            gpu.synth(a.data_ptr(), w, h, pitch, frame_id=5, timestamp_us=7, t=t, stream=_stream())
+            gpu.synth(b.data_ptr(), w, h, pitch, frame_id=5, timestamp_us=7, t=t, stream=_stream(),
+                      static_bg=bg.data_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(a, b), (w, h, t)
