@@ -34,6 +34,59 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 
+def density_probe(N, cfg, fps: int, ks=(8, 16, 32, 48, 64, 96, 128), seconds: float = 1.0) -> dict:
+    """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1), every
+    1/fps slot each submits one frame and collects it; K is sustained if no slot overran
+    (all K frames of every slot encoded before the next slot starts) over `seconds`.  K grows
+    until a slot is missed; the whole serving path per session (render, CSC, encode, bitstream
+    to host) runs, but a single host thread drives all sessions."""
+    import time as _t
+
+    period = 1.0 / fps
+    out = {"fps": fps, "seconds": seconds, "tried": {}}
+    best = 0
+    for K in ks:
+        sess = []
+        try:
+            for _ in range(K):
+                c = N.SessionConfig()
+                for a in ("width", "height", "fps", "noise", "codec", "out_width", "out_height"):
+                    setattr(c, a, getattr(cfg, a))
+                c.enc.bitrate_kbps = cfg.enc.bitrate_kbps
+                c.enc.pipeline_depth = 1
+                sess.append(N.Session(c))
+            for s in sess:  # warm-up: first IDR + rate-control probe
+                s.step(False)
+            n = max(1, int(seconds * fps))
+            late, lat = 0, []
+            t0 = _t.perf_counter()
+            for f in range(n):
+                tick = t0 + f * period
+                d = tick - _t.perf_counter()
+                if d > 0:
+                    _t.sleep(d)
+                for s in sess:
+                    s.submit(False)
+                for s in sess:
+                    r = s.collect()
+                    lat.append((r.t_encoded_us - r.t_capture_us) / 1000.0)
+                if _t.perf_counter() > tick + period:
+                    late += 1
+            lat.sort()
+            out["tried"][K] = {"late_slots": late, "p50_ms": round(lat[len(lat) // 2], 3),
+                               "p99_ms": round(lat[int(0.99 * (len(lat) - 1))], 3)}
+        except RuntimeError as e:  # out of device memory etc.: the previous K stands
+            out["tried"][K] = {"error": str(e)[:120]}
+            break
+        finally:
+            del sess
+        if late:
+            break
+        best = K
+    out["sustained"] = best
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,6 +114,9 @@ def main() -> None:
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
                     help="concurrent sessions per GPU (density): each has its own HIP stream and one frame in flight")
+    ap.add_argument("--density-probe", type=int, default=1,
+                    help="after the timed run, measure how many paced 1080p60 sessions this GPU sustains in this "
+                         "process (doubling K until a 60 fps slot is missed); reported, never part of `value`")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse the "
                          "multi-rank plumbing with several ranks on one GPU)")
@@ -160,6 +216,8 @@ def main() -> None:
         psnrs_m.append(r.psnr_y_masked if args.noise else r.psnr_y)
         gpu_ms.append(r.gpu_ms)
 
+    density = density_probe(N, cfg, args.fps) if args.density_probe else None
+
     if dist is not None:
         t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -206,6 +264,10 @@ def main() -> None:
             "mean_qp": round(statistics.mean(qps), 2),
             "mean_psnr_y_db": round(statistics.mean(psnrs), 2),
             "mean_psnr_y_db_noise_masked": round(statistics.mean(psnrs_m), 2),
+            # measured, not extrapolated: K paced sessions (one HIP stream each, depth 1) on this
+            # GPU from one host thread, every frame of every session encoded within its 1/fps slot
+            "sessions_per_gpu_at_60fps_measured": density["sustained"] if density else None,
+            "density_probe": density,
             "dtype": "uint8 video (8-bit 4:2:0), " + ("H.264 Constrained Baseline" if args.codec == "h264"
                                                        else "HEVC Main profile"),
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",

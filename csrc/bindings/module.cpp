@@ -362,6 +362,16 @@ PYBIND11_MODULE(_native, m) {
         py::arg("origin_y") = 0, py::arg("wall_w") = 0, py::arg("wall_h") = 0, py::arg("cursor_x") = -1,
         py::arg("cursor_y") = -1, py::arg("stream") = 0, py::arg("static_bg") = 0);
     m.def(
+        "composite_nv12",
+        [](uintptr_t tiles, int tw, int th, int cols, int rows, uintptr_t y, uintptr_t uv, int pitch,
+           uintptr_t stream) {
+            pix::launch_composite_nv12(as_ptr<const uint8_t>(tiles), tw, th, cols, rows, as_ptr<uint8_t>(y),
+                                       as_ptr<uint8_t>(uv), pitch, as_stream(stream));
+            HIP_CHECK(hipGetLastError());
+        },
+        py::arg("tiles_ptr"), py::arg("tile_w"), py::arg("tile_h"), py::arg("cols"), py::arg("rows"), py::arg("y_ptr"),
+        py::arg("uv_ptr"), py::arg("pitch"), py::arg("stream") = 0);
+    m.def(
         "synth_static",
         [](uintptr_t out, int w, int h, int pitch, uintptr_t stream) {
             pix::SynthParams p{w, h, pitch, 0, 0, 0.f, 0, 0, w, h, 1, -1, -1};

@@ -62,10 +62,8 @@ struct BitCounter {
     MXHD void flush() {}
 };
 
-MXHD int ilog2_u32(uint32_t v) {  // floor(log2(v)), v > 0
-    int r = 0;
-    while (v >>= 1) ++r;
-    return r;
+MXHD int ilog2_u32(uint32_t v) {  // floor(log2(v)), v > 0 (one v_ffbh on the GPU, not a shift loop)
+    return 31 - __builtin_clz(v);
 }
 
 MXHD int ue_len(uint32_t k) { return 2 * ilog2_u32(k + 1) + 1; }

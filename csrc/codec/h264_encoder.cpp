@@ -254,6 +254,7 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMemsetAsync(b.slice_info, 0, sizeof(uint32_t) * kSliceInfo * kMaxSlices, stream_));
     // payload capacity: 768 B per MB (intra at low QP stays far below)
     b.out_bytes = (size_t)nmb * 768;
+    HIP_CHECK(hipMalloc(&b.quad_unit, sizeof(uint32_t) * (b.out_bytes / 16 + 1)));
     HIP_CHECK(hipMalloc(&b.out_hdr, sizeof(OutHeader)));
     HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * kSsePartStride));
     HIP_CHECK(hipMalloc(&b.wave_prog, sizeof(int) * 4));
@@ -274,7 +275,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     DeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.unit_off,
                     (void*)b.skip_run, (void*)b.coded_list, (void*)b.coded_info, (void*)b.slice_info,
-                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.wave_line, (void*)b.intra_gain, (void*)b.intra_cand})
+                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.wave_line, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);

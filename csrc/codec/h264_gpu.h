@@ -129,6 +129,7 @@ struct DeviceBuffers {
     int32_t* skip_run;      // [nmb] skip run preceding a coded MB, -1 for skipped MBs
     uint32_t* coded_list;   // [nmb] indices of coded (non-skipped) MBs, in order
     uint4* coded_info;      // [nmb] per coded rank: {absolute bit offset, MB index, unit bits, skip run}
+    uint32_t* quad_unit;    // [out_bytes / 16] per 128-bit output quad: rank of the unit holding its first bit
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header

@@ -1440,8 +1440,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
                                                        uint32_t* __restrict__ coded_list,
                                                        uint4* __restrict__ coded_info,
                                                        uint32_t* __restrict__ slice_info, size_t out_bytes,
-                                                       OutHeader* __restrict__ hdr) {
+                                                       OutHeader* __restrict__ hdr, uint32_t* __restrict__ quad_unit) {
     __shared__ uint32_t sb[kScanTile];
+    __shared__ uint32_t s_base[kMaxSlices];
     __shared__ uint32_t wsum[kScanThreads / 64 + 1];
     __shared__ int wmax[kScanThreads / 64];
     __shared__ uint32_t s_overflow;
@@ -1454,6 +1455,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     int carry_last = -1;      // last coded MB index before the current tile
     uint32_t carry_bits = 0;  // unit bits before the current tile
     uint32_t carry_rank = 0;  // coded MBs before the current tile
+    // single-tile pictures (<= 8192 MBs, 1080p) keep each thread's MB records in registers for
+    // the final coded_info pass (no dependent global reloads)
+    uint32_t ubk[kScanPer];
+    int runk[kScanPer];
+    uint32_t rank0 = 0;
     for (int base = 0; base < nmb; base += kScanTile) {
         const int n = min(kScanTile, nmb - base);
         for (int j = t; j < n; j += kScanThreads) sb[j] = slot_bits[base + j];
@@ -1468,16 +1474,20 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
             }
         uint32_t tile_coded;
         uint32_t rank = carry_rank + block_excl_sum(ncoded, wsum, &tile_coded);
+        rank0 = rank;
         int prev = block_excl_max(last, wmax, -1);
         prev = max(prev, carry_last);
         uint32_t local = 0;
         uint32_t ub[kScanPer];
+        int s = (base + j0) / per_slice;  // slice of the thread's first MB; advanced, not divided, per MB
         for (int k = 0; k < kScanPer; ++k) {
             ub[k] = 0;
+            runk[k] = -1;
             const int j = j0 + k;
             if (j >= n) continue;
             const int i = base + j;
-            const int s = i / per_slice, first = s * per_slice;
+            if (i >= (s + 1) * per_slice) ++s;
+            const int first = s * per_slice;
             const int slast = min(first + per_slice, nmb) - 1;
             const int pv = max(prev, first - 1);
             uint32_t b = sb[j];
@@ -1490,6 +1500,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
                 }
                 const int run = i - pv - 1;
                 skip_run[i] = run;
+                runk[k] = run;
                 ub[k] = (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b;
                 prev = i;
             } else {
@@ -1497,6 +1508,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
             }
             if (i == slast) slice_info[kSliceInfo * s + 3] = (b != 0) ? 0u : (uint32_t)(i - pv);
             local += ub[k];
+            ubk[k] = ub[k];
         }
         uint32_t tile_total;
         const uint32_t ex = block_excl_sum(local, wsum, &tile_total);
@@ -1545,16 +1557,45 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     }
     __syncthreads();
     // dense per-rank unit records for k_pack: one 16-byte load per unit instead of the
-    // coded_list -> unit_off / skip_run / slot_bits chains
-    for (uint32_t r = t; r < carry_rank; r += kScanThreads) {
-        const int i = (int)coded_list[r];
-        const int s = i / per_slice;
-        const uint32_t off = slice_info[kSliceInfo * s + 1] * 8 + slice_info[kSliceInfo * s + 0] +
-                             (unit_off[i] - slice_info[kSliceInfo * s + 5]);
-        const int run = skip_run[i];
-        uint32_t b = slot_bits[i];
-        if (b == 0xffffffffu) b = 1;
-        coded_info[r] = make_uint4(off, (uint32_t)i, (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b, (uint32_t)run);
+    // coded_list -> unit_off / skip_run / slot_bits chains; and the quad -> unit table: for
+    // every 128-bit output quad, the rank of the unit (or the slice's first / end rank for
+    // header / trailer bits) holding the quad's first bit, so k_pack needs no search
+    if (t < ns) s_base[t] = soff * 8 + hbits - ebase;  // output bit of the slice's unit offset 0
+    __syncthreads();
+    const uint32_t nquads_max = (uint32_t)((out_bytes + 15) / 16);
+    auto mark_quads = [&](uint32_t a, uint32_t len, uint32_t r) {  // quads starting in [a, a + len)
+        if (len == 0) return;
+        const uint32_t qe = min((a + len - 1) >> 7, nquads_max - 1);
+        for (uint32_t q = (a + 127) >> 7; q <= qe; ++q) quad_unit[q] = r;
+    };
+    if (nmb <= kScanTile) {
+        uint32_t r = rank0;
+        const int j0 = t * kScanPer;
+        for (int k = 0; k < kScanPer; ++k) {
+            const int j = j0 + k;
+            if (j >= nmb || ubk[k] == 0) continue;
+            const uint32_t off = s_base[j / per_slice] + sb[j];
+            coded_info[r] = make_uint4(off, (uint32_t)j, ubk[k], (uint32_t)runk[k]);
+            mark_quads(off, ubk[k], r);
+            ++r;
+        }
+    } else {
+        for (uint32_t r = t; r < carry_rank; r += kScanThreads) {
+            const int i = (int)coded_list[r];
+            const int s = i / per_slice;
+            const uint32_t off = s_base[s] + unit_off[i];
+            const int run = skip_run[i];
+            uint32_t b = slot_bits[i];
+            if (b == 0xffffffffu) b = 1;
+            const uint32_t len = (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b;
+            coded_info[r] = make_uint4(off, (uint32_t)i, len, (uint32_t)run);
+            mark_quads(off, len, r);
+        }
+    }
+    if (t < ns && total_bytes <= out_bytes) {  // header and trailer quads of the slice
+        mark_quads(soff * 8, hbits, slice_info[kSliceInfo * t + 6]);
+        const uint32_t dend = soff * 8 + hbits + (eend - ebase);
+        mark_quads(dend, soff * 8 + sbytes * 8 - dend, slice_info[kSliceInfo * t + 7]);
     }
     if (t == 0) {
         const bool over = total_bytes > out_bytes;
@@ -1608,7 +1649,8 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
                                               const uint32_t* __restrict__ slot,
                                               const uint4* __restrict__ coded_info,
                                               const uint32_t* __restrict__ slice_info,
-                                              const OutHeader* __restrict__ hdr, uint8_t* __restrict__ host) {
+                                              const OutHeader* __restrict__ hdr, uint8_t* __restrict__ host,
+                                              const uint32_t* __restrict__ quad_unit) {
     const OutHeader h = *hdr;
     const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * 256;
@@ -1630,6 +1672,7 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
         uint32_t acc = 0;
         if (active) {
             const uint32_t W0 = (uint32_t)qbase * 128 + 32 * sub;
+            const int qa = (int)quad_unit[qbase];  // unit holding the quad's first bit (k_scan)
             // last slice starting at or before W0
             int lo = 0, hi = ns - 1;
             while (lo < hi) {
@@ -1652,20 +1695,11 @@ __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __re
                     overlap(acc, W0, sbit, hbits, [&](uint32_t x, int n) { return slot_get(hw, x, n); });
                 }
                 if (dend > W0 && sbit + hbits < W0 + 32) {
-                    // last coded unit of the slice starting at or before W0 (4-ary search:
-                    // three independent loads per step)
-                    int a = (int)slice_info[kSliceInfo * s + 6];
+                    // last coded unit of the slice starting at or before W0: from the quad's
+                    // first unit, forward over the (at most a few) units inside the quad
+                    int a = max((int)slice_info[kSliceInfo * s + 6], qa);
                     const int rend = (int)slice_info[kSliceInfo * s + 7];
-                    int b = rend - 1;
-                    while (b - a > 2) {
-                        const int step = (b - a + 3) >> 2;
-                        const int m1 = a + step, m2 = min(a + 2 * step, b), m3 = min(a + 3 * step, b);
-                        const uint32_t o1 = coded_info[m1].x, o2 = coded_info[m2].x, o3 = coded_info[m3].x;
-                        if (o3 <= W0) a = m3;
-                        else if (o2 <= W0) { a = m2; b = m3 - 1; }
-                        else if (o1 <= W0) { a = m1; b = m2 - 1; }
-                        else b = m1 - 1;
-                    }
+                    const int b = rend - 1;
                     while (a < b && coded_info[a + 1].x <= W0) ++a;
                     for (int r = a; r < rend; ++r) {
                         const uint4 ci = coded_info[r];
@@ -1760,9 +1794,9 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
                        b.mb, b.coef, b.slot,
                        b.slot_bits);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.unit_off, b.skip_run,
-                       b.coded_list, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr);
+                       b.coded_list, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr, b.quad_unit);
     hipLaunchKernelGGL(k_pack, dim3(256), dim3(256), 0, stream, g, b.fs, b.slot, b.coded_info, b.slice_info,
-                       b.out_hdr, host_out);
+                       b.out_hdr, host_out, b.quad_unit);
 }
 
 }  // namespace h264

@@ -59,6 +59,11 @@ void launch_sse_masked(const uint8_t* a, const uint8_t* b, int pitch, int w, int
                        int my1, unsigned long long* part, unsigned int* counter, unsigned long long* host_out,
                        hipStream_t stream);
 
+// Place cols x rows packed NV12 tiles (rank order, each tw x th: Y rows then UV rows, pitch tw)
+// into the wall's NV12 planes (pitch `pitch`) in one launch (tiled-wall composite, K7).
+void launch_composite_nv12(const uint8_t* tiles, int tw, int th, int cols, int rows, uint8_t* y, uint8_t* uv,
+                           int pitch, hipStream_t stream);
+
 // Copy a BGRx tile into a larger BGRx frame at (dx, dy) (tiled-wall composite).
 void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,
                       hipStream_t stream);

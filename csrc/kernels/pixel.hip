@@ -431,6 +431,25 @@ __global__ __launch_bounds__(256) void k_composite(const uint8_t* __restrict__ t
     }
 }
 
+// Tiled-wall composite of packed NV12 tiles (Y rows then interleaved UV rows, tile_w pitch,
+// tiles in rank order) into the wall's Y / UV planes: one launch for every tile and both
+// planes (blockIdx.z = tile, blockIdx.y = tile row incl. the UV rows), 16-byte copies.
+__global__ __launch_bounds__(256) void k_composite_nv12(const uint8_t* __restrict__ tiles, int tw, int th, int cols,
+                                                        uint8_t* __restrict__ y, uint8_t* __restrict__ uv, int pitch) {
+    const int tile = blockIdx.z, row = blockIdx.y;
+    const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (x >= tw) return;
+    const int ox = (tile % cols) * tw, oy = (tile / cols) * th;
+    const uint8_t* src = tiles + (size_t)tile * tw * th * 3 / 2 + (size_t)row * tw + x;
+    uint8_t* dst = row < th ? y + (size_t)(oy + row) * pitch + ox + x
+                            : uv + (size_t)(oy / 2 + row - th) * pitch + ox + x;
+    if (x + 16 <= tw && ((tw | pitch) & 15) == 0) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    } else {
+        for (int k = 0; k < 16 && x + k < tw; ++k) dst[k] = src[k];
+    }
+}
+
 // One 256-thread workgroup per 8 rows; every thread owns 4-pixel dword columns (16-byte
 // loads where aligned), one atomic per workgroup.
 // Single-pass masked luma SSE: 16-byte loads, one partial per workgroup, the last workgroup
@@ -562,6 +581,13 @@ void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8
                       hipStream_t stream) {
     dim3 grid((tw / 4 + 255) / 256 + 1, th);
     hipLaunchKernelGGL(k_composite, grid, dim3(256), 0, stream, tile, tile_pitch, tw, th, dst, dst_pitch, dx, dy);
+}
+
+void launch_composite_nv12(const uint8_t* tiles, int tw, int th, int cols, int rows, uint8_t* y, uint8_t* uv,
+                           int pitch, hipStream_t stream) {
+    if ((tw & 1) || (th & 1) || pitch < cols * tw) throw std::invalid_argument("composite_nv12: bad tile geometry");
+    dim3 grid((tw / 16 + 255) / 256 + 1, th + th / 2, cols * rows);
+    hipLaunchKernelGGL(k_composite_nv12, grid, dim3(256), 0, stream, tiles, tw, th, cols, y, uv, pitch);
 }
 
 }  // namespace pix

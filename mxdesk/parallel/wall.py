@@ -4,14 +4,21 @@ composite is encoded as a single stream (BASELINE.j
 
 Per frame, on every rank (one process per GPU, ``torch.distributed`` backend ``nccl`` =
 RCCL on ROCm; ``gloo`` for CPU tests):
-  1. rank 0 broadcasts a small control tensor (frame id, force-IDR, stop) -> lockstep;
+  1. rank 0 broadcasts a small control tensor (frame id, stop, capture time) -> lockstep;
   2. each rank renders its tile of the wall (HIP synthetic desktop with a tile origin) and
      converts it to NV12 on its own GPU (HIP CSC), so only 1.5 B/pixel cross xGMI;
   3. the tiles reach the encode rank either by a ring ``all_gather_into_tensor``
      (``exchange="allgather"``) or by a direct gather -- one batched send/recv per peer, so
      the encode rank pulls the three tiles over three xGMI links at once
      (``exchange="gather"``; xGMI is point-to-point, a ring is per-link bound);
-  4. the encode rank composites the NV12 tiles into the wall frame and H.264-encodes it.
+  4. the encode rank composites the NV12 tiles into the wall frame with one HIP launch
+     (k_composite_nv12) and encodes it -- HEVC by default above 4K (an 8K H.264 stream needs
+     level 6.x, which browser decoders rarely take; HEVC 8K is level 6.1).
+Pipelining on the encode rank: frame n+1's lockstep render + tile exchange is posted (RCCL
+runs it on its own stream, the followers render meanwhile) BEFORE frame n is encoded, so
+exchange(n+1) overlaps encode(n); the control tensor goes up with one host->device copy.
+``MXDESK_WALL_MODE=tiles`` skips the composite: every rank serves its own tile as an
+independent stream (port + rank) for clients that cannot decode the full wall's level.
 If process-group initialisation fails the launcher falls back to per-GPU sessions
 (SURVEY.md §5.3).
 """
@@ -106,10 +113,10 @@ class TileExchange:
         self.tiles = torch.empty(world * geo.tile_bytes, dtype=torch.uint8, device=device) \
             if (rank == root or mode == "allgather") else None
 
-    def exchange(self, tile: torch.Tensor) -> torch.Tensor | None:
+    def post(self, tile: torch.Tensor) -> list:
+        """Start the exchange of this rank's tile; returns the requests to wait for."""
         if self.mode == "allgather":
-            dist.all_gather_into_tensor(self.tiles, tile)
-            return self.tiles if self.rank == self.root else None
+            return [dist.all_gather_into_tensor(self.tiles, tile, async_op=True)]
         tb = self.geo.tile_bytes
         if self.rank == self.root:
             self.tiles[self.root * tb:(self.root + 1) * tb].copy_(tile)
@@ -117,15 +124,27 @@ class TileExchange:
                    if r != self.root]
         else:
             ops = [dist.P2POp(dist.isend, tile, self.root)]
-        if ops:  # world size 1: nothing to exchange
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        return dist.batch_isend_irecv(ops) if ops else []  # world size 1: nothing to exchange
+
+    def wait(self, reqs: list) -> torch.Tensor | None:
+        for req in reqs:
+            req.wait()
         return self.tiles if self.rank == self.root else None
+
+    def exchange(self, tile: torch.Tensor) -> torch.Tensor | None:
+        return self.wait(self.post(tile))
 
 
 def composite_nv12(tiles: torch.Tensor, geo: WallGeometry, y: torch.Tensor, uv: torch.Tensor) -> None:
-    """Place packed NV12 tiles into the wall planes y (H, P) and uv (H/2, P)."""
+    """Place packed NV12 tiles into the wall planes y (H, P) and uv (H/2, P): one HIP launch on
+    the GPU (k_composite_nv12), tensor copies on the CPU."""
     tb, tw, th = geo.tile_bytes, geo.tile_w, geo.tile_h
+    if tiles.device.type == "cuda":
+        from .. import native
+
+        native().composite_nv12(tiles.data_ptr(), tw, th, geo.cols, geo.rows, y.data_ptr(), uv.data_ptr(),
+                                y.stride(0), torch.cuda.current_stream(tiles.device).cuda_stream)
+        return
     for r in range(geo.cols * geo.rows):
         ox, oy = geo.origin(r)
         t = tiles[r * tb:(r + 1) * tb]
@@ -137,15 +156,19 @@ class WallPipeline(StreamPipeline):
     """Rank-0 pipeline: lockstep tile render on every rank, exchange, composite, encode."""
 
     def __init__(self, geo: WallGeometry, fps: int, rank: int, world: int, device: torch.device,
-                 exchange: str = "gather", bitrate_kbps: int = 20000, **kw):
+                 exchange: str = "gather", bitrate_kbps: int = 20000, codec: str | None = None, **kw):
         self.geo, self.rank, self.world, self.dev = geo, rank, world, device
         self.renderer = TileRenderer(geo, rank, device)
         self.xchg = TileExchange(geo, rank, world, device, exchange)
         self.ctrl = torch.zeros(4, dtype=torch.int64, device=device)
+        self._ctrl_host = torch.zeros(4, dtype=torch.int64).pin_memory() if device.type == "cuda" else self.ctrl
         self._t0 = time.monotonic()
         self._fid = 0
+        self._pending = None  # (frame id, capture us, exchange requests) of the posted frame
+        # above 4K the wall goes out as HEVC (level 6.1 at 8K; H.264 would need level 6.x)
+        wall_codec = codec or ("hevc" if geo.width > 4096 else "h264")
         super().__init__(geo.width, geo.height, fps, backend="gpu" if device.type == "cuda" else "cpu",
-                         device=device.index or 0, bitrate_kbps=bitrate_kbps, **kw)
+                         device=device.index or 0, bitrate_kbps=bitrate_kbps, codec=wall_codec, **kw)
 
     def _make_session(self) -> None:
         from .. import native
@@ -157,13 +180,15 @@ class WallPipeline(StreamPipeline):
         ec.bitrate_kbps = self._enc_args["bitrate_kbps"]
         ec.search_range = self._enc_args["search_range"]
         ec.subpel = 1 if self._enc_args["subpel"] else 0
+        hevc = self.codec == "hevc"
         if self.dev.type == "cuda":
-            self.enc = N.GpuH264Encoder(ec, torch.cuda.current_stream(self.dev).cuda_stream)
+            cls = N.GpuHevcEncoder if hevc else N.GpuH264Encoder
+            self.enc = cls(ec, torch.cuda.current_stream(self.dev).cuda_stream)
             pitch = self.enc.pitch
         else:
             ec.search_range = min(ec.search_range, 4)
             ec.subpel = 0
-            self.enc = N.CpuH264Encoder(ec)
+            self.enc = (N.CpuHevcEncoder if hevc else N.CpuH264Encoder)(ec)
             pitch = cw
         self.wy = torch.zeros((ch, pitch), dtype=torch.uint8, device=self.dev)
         self.wuv = torch.zeros((ch // 2, pitch), dtype=torch.uint8, device=self.dev)
@@ -173,35 +198,64 @@ class WallPipeline(StreamPipeline):
     def set_bitrate(self, kbps: int) -> None:
         self.enc.set_bitrate(int(kbps))
 
-    def lockstep_frame(self, force_idr: bool, stop: bool = False) -> torch.Tensor | None:
+    def _broadcast_ctrl(self, fid: int, stop: bool, t_cap: int) -> None:
+        h = self._ctrl_host
+        h[0], h[1], h[2], h[3] = fid, 0, int(stop), t_cap
+        if h is not self.ctrl:
+            self.ctrl.copy_(h, non_blocking=True)  # one host->device copy, not four element writes
+        dist.broadcast(self.ctrl, 0)
+
+    def post_frame(self) -> tuple[int, int, list]:
+        """Lockstep step of the next frame: control broadcast, own tile render, exchange posted."""
         from .. import native
 
         t_cap = native().now_us()
-        self.ctrl[0], self.ctrl[1], self.ctrl[2], self.ctrl[3] = self._fid, int(force_idr), int(stop), t_cap
-        dist.broadcast(self.ctrl, 0)
+        fid = self._fid
+        self._fid += 1
+        self._broadcast_ctrl(fid, False, t_cap)
+        tile = self.renderer.render(fid, fid / self.fps, t_cap)
+        return fid, t_cap, self.xchg.post(tile)
+
+    def lockstep_frame(self, force_idr: bool = False, stop: bool = False) -> torch.Tensor | None:
+        """One unpipelined lockstep frame (tests / stop): returns the tiles on the encode rank."""
         if stop:
+            self._drain()
+            from .. import native
+
+            self._broadcast_ctrl(self._fid, True, native().now_us())
             return None
-        tile = self.renderer.render(self._fid, self._fid / self.fps, t_cap)
-        tiles = self.xchg.exchange(tile)
+        self._drain()
+        _, _, reqs = self.post_frame()
+        tiles = self.xchg.wait(reqs)
         if tiles is not None:
             composite_nv12(tiles, self.geo, self.wy, self.wuv)
         return tiles
 
+    def _drain(self) -> None:
+        if self._pending is not None:
+            self.xchg.wait(self._pending[2])
+            self._pending = None
+
     def _produce(self, force_idr: bool) -> EncodedFrame:
         from .. import native
 
-        t_cap = native().now_us()
-        self.lockstep_frame(force_idr)
-        fid = self._fid
-        self._fid += 1
+        if self._pending is None:
+            self._pending = self.post_frame()
+        fid, t_cap, reqs = self._pending
+        tiles = self.xchg.wait(reqs)
+        composite_nv12(tiles, self.geo, self.wy, self.wuv)
+        # frame fid+1's render + exchange run (followers, RCCL stream) while frame fid encodes;
+        # the receive is ordered after the composite above on the device (RCCL waits on the
+        # current stream), so one tile buffer suffices
+        self._pending = self.post_frame()
         if self.dev.type == "cuda":
-            torch.cuda.current_stream(self.dev).synchronize()
             au = self.enc.encode(self.wy.data_ptr(), self.wuv.data_ptr(), force_idr)
         else:
-            au = self.enc.encode(self.wy.cpu().numpy()[: self.geo.height], self.wuv.cpu().numpy()[: self.geo.height // 2],
+            au = self.enc.encode(self.wy.numpy()[: self.geo.height], self.wuv.numpy()[: self.geo.height // 2],
                                  force_idr)
         st = self.enc.stats
-        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, self.geo.width, self.geo.height)
+        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, self.geo.width, self.geo.height,
+                            codec_id=self.codec_id)
 
     def stop(self) -> None:
         super().stop()
@@ -211,9 +265,49 @@ class WallPipeline(StreamPipeline):
             pass
 
 
+class TilePipeline(WallPipeline):
+    """``MXDESK_WALL_MODE=tiles``: this rank's tile of the wall as an independent stream (no
+    exchange, no composite) -- the fallback for clients that cannot decode the whole wall's
+    level; a client shows the tiles side by side."""
+
+    def __init__(self, geo: WallGeometry, fps: int, rank: int, device: torch.device, bitrate_kbps: int = 8000,
+                 codec: str | None = None, **kw):
+        self.tile_geo = WallGeometry(1, 1, geo.tile_w, geo.tile_h)
+        self.full_geo, self.rank, self.dev = geo, rank, device
+        self.renderer = TileRenderer(geo, rank, device)
+        self._fid = 0
+        self._pending = None
+        self.geo = self.tile_geo  # the encoder / composite see a 1x1 wall of this tile
+        StreamPipeline.__init__(self, geo.tile_w, geo.tile_h, fps, backend="gpu" if device.type == "cuda" else "cpu",
+                                device=device.index or 0, bitrate_kbps=bitrate_kbps,
+                                codec=codec or ("hevc" if geo.tile_w > 4096 else "h264"), **kw)
+
+    def _produce(self, force_idr: bool) -> EncodedFrame:
+        from .. import native
+
+        t_cap = native().now_us()
+        fid = self._fid
+        self._fid += 1
+        tile = self.renderer.render(fid, fid / self.fps, t_cap)
+        composite_nv12(tile, self.tile_geo, self.wy, self.wuv)
+        if self.dev.type == "cuda":
+            au = self.enc.encode(self.wy.data_ptr(), self.wuv.data_ptr(), force_idr)
+        else:
+            g = self.tile_geo
+            au = self.enc.encode(self.wy.numpy()[: g.height], self.wuv.numpy()[: g.height // 2], force_idr)
+        st = self.enc.stats
+        g = self.tile_geo
+        return EncodedFrame(fid, t_cap, native().now_us(), bool(st.idr), st.qp, au, g.width, g.height,
+                            codec_id=self.codec_id)
+
+    def stop(self) -> None:
+        StreamPipeline.stop(self)
+
+
 def follower_loop(geo: WallGeometry, rank: int, world: int, device: torch.device, exchange: str = "gather",
                   fps: int = 60) -> int:
-    """Ranks != 0: render + send tiles in lockstep until rank 0 broadcasts stop."""
+    """Ranks != 0: render + send tiles in lockstep until rank 0 broadcasts stop (the host reads
+    the control tensor once per frame: the follower has nothing to overlap with)."""
     renderer = TileRenderer(geo, rank, device)
     xchg = TileExchange(geo, rank, world, device, exchange)
     ctrl = torch.zeros(4, dtype=torch.int64, device=device)
@@ -253,6 +347,19 @@ def wall_main(cfg: Any, layout: str = "2x2") -> None:
         return
     geo = WallGeometry(cols, rows, cfg.sizew, cfg.sizeh)
     exchange = os.environ.get("MXDESK_WALL_EXCHANGE", "gather")
+    if os.environ.get("MXDESK_WALL_MODE", "composite") == "tiles":
+        from ..server.app import MediaServer, run_forever, ssl_context
+
+        pipe = TilePipeline(geo, cfg.stream_fps, rank, device, bitrate_kbps=cfg.video_bitrate)
+        port = cfg.port + rank
+        print(f"mxdesk wall {cols}x{rows} tiles: rank {rank} serves its {geo.tile_w}x{geo.tile_h} tile at "
+              f"{geo.origin(rank)} on :{port}", flush=True)
+        try:
+            run_forever(MediaServer(pipe, cfg), cfg.addr, port, ssl_context(cfg))
+        finally:
+            pipe.stop()
+            dist.destroy_process_group()
+        return
     if rank != 0:
         follower_loop(geo, rank, world, device, exchange, cfg.stream_fps)
         dist.destroy_process_group()

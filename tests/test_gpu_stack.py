@@ -169,6 +169,47 @@ def test_gpu_wall_single_rank_rccl(gpu):
         dist.destroy_process_group()
 
 
+def test_gpu_composite_nv12_kernel_matches_copies(gpu):
+    """k_composite_nv12 (one launch for all tiles and both planes) == per-tile tensor copies."""
+    from mxdesk.parallel.wall import WallGeometry
+
+    geo = WallGeometry(2, 2, 96, 32)
+    tiles = torch.randint(0, 256, (4 * geo.tile_bytes,), dtype=torch.uint8, device="cuda")
+    pitch = 256
+    y = torch.zeros((geo.height, pitch), dtype=torch.uint8, device="cuda")
+    uv = torch.zeros((geo.height // 2, pitch), dtype=torch.uint8, device="cuda")
+    gpu.composite_nv12(tiles.data_ptr(), geo.tile_w, geo.tile_h, 2, 2, y.data_ptr(), uv.data_ptr(), pitch,
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ry, ruv = torch.zeros_like(y), torch.zeros_like(uv)
+    tb, tw, th = geo.tile_bytes, geo.tile_w, geo.tile_h
+    for r in range(4):
+        ox, oy = geo.origin(r)
+        t = tiles[r * tb:(r + 1) * tb]
+        ry[oy:oy + th, ox:ox + tw] = t[: tw * th].view(th, tw)
+        ruv[oy // 2:oy // 2 + th // 2, ox:ox + tw] = t[tw * th:].view(th // 2, tw)
+    assert torch.equal(y, ry) and torch.equal(uv, ruv)
+
+
+def test_gpu_wall_hevc_single_rank(gpu):
+    """The wall's HEVC path (its codec above 4K) through RCCL with one rank."""
+    import torch.distributed as dist
+
+    from mxdesk.codec.hevc_decoder import Decoder as HevcDecoder
+    from mxdesk.parallel.wall import WallGeometry, WallPipeline
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pipe = WallPipeline(WallGeometry(1, 1, 320, 192), 60, 0, 1, torch.device("cuda", 0), "gather",
+                            bitrate_kbps=0, codec="hevc")
+        stream = b"".join(pipe.step().au for _ in range(3))
+        frames = HevcDecoder().decode(stream)
+        assert len(frames) == 3 and read_barcode(frames[2][0])[0] == 2
+    finally:
+        dist.destroy_process_group()
+
+
 def test_gpu_telemetry_sysfs(gpu):
     """amdgpu sysfs telemetry of the visible GPU feeds the mxdesk_gpu gauges of /metrics."""
     from mxdesk.utils import devices as D
