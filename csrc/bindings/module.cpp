@@ -396,7 +396,7 @@ PYBIND11_MODULE(_native, m) {
         "scale_to_nv12",
         [](uintptr_t in, int in_pitch, int in_w, int in_h, int out_w, int out_h, uintptr_t x0, uintptr_t wx, int taps_x,
            uintptr_t y0, uintptr_t wy, int taps_y, uintptr_t y, uintptr_t uv, int out_pitch, int cw, int ch,
-           uintptr_t stream) {
+           uintptr_t stream, bool mfma) {
             if ((out_w & 1) || (out_h & 1) || cw < out_w || ch < out_h || (cw & 1) || (ch & 1))
                 throw std::invalid_argument("scale_to_nv12: bad geometry");
             pix::LanczosTables t{out_w,
@@ -407,14 +407,31 @@ PYBIND11_MODULE(_native, m) {
                                  as_ptr<const float>(wx),
                                  as_ptr<const int>(y0),
                                  as_ptr<const float>(wy)};
+            void* frags = nullptr;
+            if (mfma) {  // test path: tables back to the host, fragments built and uploaded per call
+                std::vector<int> hx0(out_w), hy0(out_h);
+                std::vector<float> hwx((size_t)out_w * taps_x), hwy((size_t)out_h * taps_y);
+                HIP_CHECK(hipMemcpy(hx0.data(), t.x0, hx0.size() * 4, hipMemcpyDeviceToHost));
+                HIP_CHECK(hipMemcpy(hy0.data(), t.y0, hy0.size() * 4, hipMemcpyDeviceToHost));
+                HIP_CHECK(hipMemcpy(hwx.data(), t.wx, hwx.size() * 4, hipMemcpyDeviceToHost));
+                HIP_CHECK(hipMemcpy(hwy.data(), t.wy, hwy.size() * 4, hipMemcpyDeviceToHost));
+                pix::ScaleFragsHost fr;
+                if (!pix::build_scale_frags(in_w, in_h, out_w, out_h, cw, ch, hx0, hwx, taps_x, hy0, hwy, taps_y, fr))
+                    throw std::invalid_argument("scale_to_nv12: scale factor outside the MFMA kernel's range");
+                pix::upload_scale_frags(fr, &frags, t.mf);
+            }
             pix::launch_scale_to_nv12(as_ptr<const uint8_t>(in), in_pitch, in_w, in_h, t, as_ptr<uint8_t>(y),
                                       as_ptr<uint8_t>(uv), out_pitch, cw, ch, as_stream(stream));
             HIP_CHECK(hipGetLastError());
+            if (frags) {
+                HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+                HIP_CHECK(hipFree(frags));
+            }
         },
         py::arg("in_ptr"), py::arg("in_pitch"), py::arg("in_w"), py::arg("in_h"), py::arg("out_w"), py::arg("out_h"),
         py::arg("x0_ptr"), py::arg("wx_ptr"), py::arg("taps_x"), py::arg("y0_ptr"), py::arg("wy_ptr"),
         py::arg("taps_y"), py::arg("y_ptr"), py::arg("uv_ptr"), py::arg("out_pitch"), py::arg("coded_w"),
-        py::arg("coded_h"), py::arg("stream") = 0);
+        py::arg("coded_h"), py::arg("stream") = 0, py::arg("mfma") = false);
     m.def(
         "composite",
         [](uintptr_t tile, int tile_pitch, int tw, int th, uintptr_t dst, int dst_pitch, int dx, int dy,
@@ -457,6 +474,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("mask_y0", &SessionConfig::mask_y0)
         .def_readwrite("mask_x1", &SessionConfig::mask_x1)
         .def_readwrite("mask_y1", &SessionConfig::mask_y1)
+        .def_readwrite("scale_valu", &SessionConfig::scale_valu)
         .def_readwrite("enc", &SessionConfig::enc);
 
     py::class_<FrameResult>(m, "FrameResult")

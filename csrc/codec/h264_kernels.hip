@@ -1443,6 +1443,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
                                                        OutHeader* __restrict__ hdr, uint32_t* __restrict__ quad_unit) {
     __shared__ uint32_t sb[kScanTile];
     __shared__ uint32_t s_base[kMaxSlices];
+    __shared__ uint32_t s_first_rank[kMaxSlices + 1], s_trail[kMaxSlices];  // LDS copies: no global re-reads
     __shared__ uint32_t wsum[kScanThreads / 64 + 1];
     __shared__ int wmax[kScanThreads / 64];
     __shared__ uint32_t s_overflow;
@@ -1452,6 +1453,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     const int ns = fs->num_slices;
     const bool idr = fs->idr != 0;
     if (t == 0) s_overflow = 0;
+    // distortion partials: issued now, reduced at the end (their latency hides behind the scan)
+    const int nparts = idr ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
+    constexpr int kPartsPer = 8;  // partials per thread held in registers (<= 8192 per channel)
+    unsigned long long pacc[4] = {0, 0, 0, 0};
+    const bool pregs = nparts <= kPartsPer * kScanThreads;
+    if (pregs) {
+#pragma unroll
+        for (int k = 0; k < kPartsPer; ++k) {
+            const int i = t + k * kScanThreads;
+            if (i < nparts)
+                for (int c = 0; c < 4; ++c) pacc[c] += fs->sse_part[c * kSsePartStride + i];
+        }
+    }
     int carry_last = -1;      // last coded MB index before the current tile
     uint32_t carry_bits = 0;  // unit bits before the current tile
     uint32_t carry_rank = 0;  // coded MBs before the current tile
@@ -1491,7 +1505,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
             const int slast = min(first + per_slice, nmb) - 1;
             const int pv = max(prev, first - 1);
             uint32_t b = sb[j];
-            if (i == first) slice_info[kSliceInfo * s + 6] = rank;  // coded MBs before the slice
+            if (i == first) {
+                slice_info[kSliceInfo * s + 6] = rank;  // coded MBs before the slice
+                s_first_rank[s] = rank;
+            }
             if (b != 0) {
                 coded_list[rank++] = (uint32_t)i;
                 if (b == 0xffffffffu) {
@@ -1506,7 +1523,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
             } else {
                 skip_run[i] = -1;
             }
-            if (i == slast) slice_info[kSliceInfo * s + 3] = (b != 0) ? 0u : (uint32_t)(i - pv);
+            if (i == slast) {
+                const uint32_t tr = (b != 0) ? 0u : (uint32_t)(i - pv);
+                slice_info[kSliceInfo * s + 3] = tr;
+                s_trail[s] = tr;
+            }
             local += ub[k];
             ubk[k] = ub[k];
         }
@@ -1528,21 +1549,22 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         __syncthreads();
     }
     const uint32_t grand_total = carry_bits;
+    if (t == 0) s_first_rank[ns] = carry_rank;
     __syncthreads();
-    if (t < ns) slice_info[kSliceInfo * t + 7] = (t + 1 < ns ? slice_info[kSliceInfo * (t + 1) + 6] : carry_rank);
-    __syncthreads();
+    if (t < ns) slice_info[kSliceInfo * t + 7] = s_first_rank[t + 1];
     // per slice sizes (one thread per slice; ns <= kMaxSlices <= kScanThreads)
     uint32_t sbytes = 0, ebase = 0, eend = 0, hbits = 0, trail = 0;
+    const bool one_tile = nmb <= kScanTile;  // unit offsets still in LDS (sb)
     if (t < ns) {
         const int first = t * per_slice;
         const int slast = min(first + per_slice, nmb) - 1;
-        ebase = unit_off[first];
-        eend = (slast + 1 < nmb) ? unit_off[slast + 1] : grand_total;
+        ebase = one_tile ? sb[first] : unit_off[first];
+        eend = (slast + 1 < nmb) ? (one_tile ? sb[slast + 1] : unit_off[slast + 1]) : grand_total;
         BitCounter bc;
         bc.init(nullptr);
         write_slice_header(bc, slice_params(fs, t, g.mb_w));
         hbits = bc.bits;
-        trail = idr ? 0u : slice_info[kSliceInfo * t + 3];
+        trail = idr ? 0u : s_trail[t];
         const uint32_t bits = hbits + (eend - ebase) + (trail ? ue_len(trail) : 0) + 1;
         sbytes = (bits + 7) >> 3;
     }
@@ -1593,9 +1615,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
         }
     }
     if (t < ns && total_bytes <= out_bytes) {  // header and trailer quads of the slice
-        mark_quads(soff * 8, hbits, slice_info[kSliceInfo * t + 6]);
+        mark_quads(soff * 8, hbits, s_first_rank[t]);
         const uint32_t dend = soff * 8 + hbits + (eend - ebase);
-        mark_quads(dend, soff * 8 + sbytes * 8 - dend, slice_info[kSliceInfo * t + 7]);
+        mark_quads(dend, soff * 8 + sbytes * 8 - dend, s_first_rank[t + 1]);
     }
     if (t == 0) {
         const bool over = total_bytes > out_bytes;
@@ -1606,11 +1628,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameSt
     // distortion: block-wide reduction of the per-MB partials
     {
         // partials: one per intra MB row (IDR) or per inter workgroup (4 MBs) + the per-row
-        // intra deltas of k_intra_wave (P pictures with intra macroblocks)
-        const int nparts = idr ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
-        unsigned long long acc[4] = {0, 0, 0, 0};
-        for (int i = t; i < nparts; i += kScanThreads)
-            for (int c = 0; c < 4; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
+        // intra deltas of k_intra_wave / k_intra_p (P pictures with intra macroblocks);
+        // prefetched into registers at the start when they fit
+        unsigned long long acc[4] = {pacc[0], pacc[1], pacc[2], pacc[3]};
+        if (!pregs)
+            for (int i = t; i < nparts; i += kScanThreads)
+                for (int c = 0; c < 4; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
         __shared__ unsigned long long red[4][kScanThreads / 64];
         for (int c = 0; c < 4; ++c) {
             unsigned long long v = acc[c];

@@ -1,6 +1,8 @@
 // Pixel kernels (SURVEY.md C40 synthetic desktop, C42 CSC/scale, K7 composite).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <vector>
 #include <stdint.h>
 
 namespace mx {
@@ -40,13 +42,39 @@ void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_
 
 // Fused separable Lanczos-3 resample (in_w x in_h -> out_w x out_h) + BT.709 CSC into
 // NV12, LDS-tiled.  `weights` from make_lanczos_tables (device memory).
+// MFMA form of the scaler (see build_scale_frags): per 32-column group the first staged
+// input column and K-step count, per 32-row group the first input row, row-block count and
+// row span, and the weights pre-laid-out as f16 MFMA operand fragments.
+struct ScaleMfma {
+    const int* gx = nullptr;    // [ngx][2] kabs, nks
+    const int* gy = nullptr;    // [ngy][3] ylo, nrb, nr
+    const void* fh = nullptr;   // [ngx][kMaxKs][64 lanes] 8 x f16 horizontal weight fragments
+    const float* sh = nullptr;  // [ngx][32] sum of each column's f16 weights (input bias removal)
+    const void* fv = nullptr;   // [ngy][kMaxRb][2][64 lanes] 8 x f16 vertical weight fragments
+    int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0;
+};
 struct LanczosTables {
     int out_w, out_h, taps_x, taps_y;
     const int* x0;      // [out_w] first input column
     const float* wx;    // [out_w * taps_x]
     const int* y0;      // [out_h]
     const float* wy;    // [out_h * taps_y]
+    ScaleMfma mf{};     // gx == nullptr: LDS/VALU kernel
 };
+
+// Host side of the MFMA scaler: fragment tables for one (in, out, coded) geometry, packed in
+// one blob (`blob`) that upload_scale_frags copies to the device.  Returns false when the
+// scale factor is outside what the MFMA kernel's register tiles hold (then the VALU kernel runs).
+struct ScaleFragsHost {
+    std::vector<uint8_t> blob;
+    size_t off_gx = 0, off_gy = 0, off_fh = 0, off_sh = 0, off_fv = 0;
+    int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0;
+};
+bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, int coded_h,
+                       const std::vector<int>& x0, const std::vector<float>& wx, int tx, const std::vector<int>& y0,
+                       const std::vector<float>& wy, int ty, ScaleFragsHost& out);
+// Copies the blob to `dev` (hipMalloc'ed here; caller frees) and fills `mf`.
+void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf);
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
                           uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream);
 

@@ -10,6 +10,10 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 #include "pixel.h"
@@ -318,35 +322,52 @@ __global__ __launch_bounds__(256) void k_bgrx_to_nv12(const uint8_t* __restrict_
 
 // ---- fused Lanczos scale + CSC.  Output tile 64 x 16 luma pixels, 256 threads, each
 // thread produces a 2x2 output block (4 Y + one UV pair).
+//  * the input footprint is staged into LDS with 16-byte loads from a 4-pixel aligned start
+//    (clamped per pixel only at picture borders);
+//  * the horizontal pass keeps its result as int16 fixed point (x16, 6 B per pixel instead of
+//    12 B of float RGB), so a 4K->1080p tile needs ~42 KB of LDS instead of ~62 KB and three
+//    workgroups fit a CU;
+//  * the UV pair of a 2x2 block is one 16-bit store.
+// (The first version -- 4-byte footprint loads, float RGB intermediate, byte UV stores -- is
+// measured in profiles/r02_scale.)
 constexpr int kTileW = 64, kTileH = 16;
+constexpr float kHFix = 16.f;  // horizontal-pass fixed-point scale
 
 __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict__ in, int in_pitch, int in_w,
                                                        int in_h, LanczosTables t, uint8_t* __restrict__ yp,
                                                        uint8_t* __restrict__ uvp, int out_pitch, int coded_w,
-                                                       int coded_h, int max_nc, int max_nr) {
+                                                       int coded_h, int max_nc, int max_nr, int vec) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int ox0 = blockIdx.x * kTileW, oy0 = blockIdx.y * kTileH;
     const int tid = threadIdx.x;
     const int oxl = min(ox0 + kTileW - 1, t.out_w - 1), oyl = min(oy0 + kTileH - 1, t.out_h - 1);
     const int oxf = min(ox0, t.out_w - 1), oyf = min(oy0, t.out_h - 1);
-    const int xlo = t.x0[oxf], xhi = t.x0[oxl] + t.taps_x - 1;
+    const int xlo = t.x0[oxf] & ~3, xhi = t.x0[oxl] + t.taps_x - 1;  // 4-pixel aligned footprint start
     const int ylo = t.y0[oyf], yhi = t.y0[oyl] + t.taps_y - 1;
-    const int nc = xhi - xlo + 1, nr = yhi - ylo + 1;
+    const int nq = (xhi - xlo + 4) >> 2, nr = yhi - ylo + 1;  // footprint: nq pixel quads x nr rows
     const int tx = t.taps_x, ty = t.taps_y;
-    // LDS: input footprint [nr][max_nc] BGRx | horizontal result [nr][kTileW] x RGB float |
+    // LDS: footprint [nr][max_nc] BGRx | horizontal result [3][nr][kTileW] int16 |
     //      this tile's filter weights [kTileW][tx] + [kTileH][ty] and first-tap offsets
     uint32_t* lin = reinterpret_cast<uint32_t*>(smem);
-    float* hr = reinterpret_cast<float*>(smem + (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15));
-    float* hg = hr + max_nr * kTileW;
-    float* hb = hg + max_nr * kTileW;
-    float* wxs = hb + max_nr * kTileW;
+    int16_t* hrgb = reinterpret_cast<int16_t*>(smem + (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15));
+    float* wxs = reinterpret_cast<float*>(hrgb + ((3 * max_nr * kTileW + 7) & ~7));
     float* wys = wxs + kTileW * tx;
     int* bx = reinterpret_cast<int*>(wys + kTileH * ty);
     int* by = bx + kTileW;
-    for (int i = tid; i < nr * nc; i += 256) {
-        const int r = i / nc, c = i - r * nc;
-        const int sy = min(max(ylo + r, 0), in_h - 1), sx = min(max(xlo + c, 0), in_w - 1);
-        lin[r * max_nc + c] = *reinterpret_cast<const uint32_t*>(in + (size_t)sy * in_pitch + sx * 4);
+    for (int i = tid; i < nr * nq; i += 256) {
+        const int r = i / nq, q = i - r * nq;
+        const int sy = min(max(ylo + r, 0), in_h - 1), sx = xlo + 4 * q;
+        const uint8_t* row = in + (size_t)sy * in_pitch;
+        uint4 v;
+        if (vec && sx >= 0 && sx + 4 <= in_w) {  // (vec: 16-byte aligned rows)
+            v = *reinterpret_cast<const uint4*>(row + (size_t)sx * 4);
+        } else {
+            v.x = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx, 0), in_w - 1) * 4);
+            v.y = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 1, 0), in_w - 1) * 4);
+            v.z = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 2, 0), in_w - 1) * 4);
+            v.w = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 3, 0), in_w - 1) * 4);
+        }
+        *reinterpret_cast<uint4*>(lin + r * max_nc + 4 * q) = v;
     }
     for (int i = tid; i < kTileW * tx; i += 256) {
         const int c = i / tx, k = i - c * tx;
@@ -359,62 +380,262 @@ __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict
     if (tid < kTileW) bx[tid] = t.x0[min(ox0 + tid, t.out_w - 1)] - xlo;
     if (tid < kTileH) by[tid] = t.y0[min(oy0 + tid, t.out_h - 1)] - ylo;
     __syncthreads();
-    for (int i = tid; i < nr * kTileW; i += 256) {
-        const int r = i / kTileW, c = i - r * kTileW;
-        const uint32_t* src = lin + r * max_nc + bx[c];
-        const float* w = wxs + c * tx;
-        float R = 0.f, G = 0.f, B = 0.f;
-        for (int k = 0; k < tx; ++k) {
-            const uint32_t v = src[k];
-            const float wk = w[k];
-            B += wk * (float)(v & 0xff);
-            G += wk * (float)((v >> 8) & 0xff);
-            R += wk * (float)((v >> 16) & 0xff);
+    // horizontal pass: a thread keeps one output column (tid % 64) for all its rows, so that
+    // column's taps / weights stay in registers; R and G accumulate as a packed float pair
+    // (v_pk_fma_f32), B on its own.  Result: int16 fixed point, R|G packed in one dword
+    // plane and B in another, so the vertical pass reads two adjacent columns per load.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int hplane = max_nr * kTileW;
+    uint32_t* hrg = reinterpret_cast<uint32_t*>(hrgb);  // [nr][kTileW] (R | G << 16)
+    int16_t* hb = hrgb + 2 * hplane;                     // [nr][kTileW]
+    {
+        const int c = tid & (kTileW - 1);
+        constexpr int kRegTaps = 20;
+        float wr[kRegTaps];
+#pragma unroll
+        for (int k = 0; k < kRegTaps; ++k) wr[k] = k < tx ? wxs[c * tx + k] : 0.f;
+        const int c0 = bx[c];
+        for (int r = tid >> 6; r < nr; r += 256 / kTileW) {
+            const uint32_t* src = lin + r * max_nc + c0;
+            f2 rg = {0.f, 0.f};
+            float B = 0.f;
+            if (tx <= kRegTaps) {
+#pragma unroll
+                for (int k = 0; k < kRegTaps; ++k) {
+                    if (k >= tx) break;
+                    const uint32_t v = src[k];
+                    const f2 p = {(float)((v >> 16) & 0xffu) /* R */, (float)((v >> 8) & 0xffu)};
+                    rg = __builtin_elementwise_fma((f2){wr[k], wr[k]}, p, rg);
+                    B = fmaf(wr[k], (float)((v >> 0) & 0xffu), B);
+                }
+            } else {  // very large scale factors: weights from LDS
+                for (int k = 0; k < tx; ++k) {
+                    const uint32_t v = src[k];
+                    const float wk = wxs[c * tx + k];
+                    const f2 p = {(float)((v >> 16) & 0xffu), (float)((v >> 8) & 0xffu)};
+                    rg = __builtin_elementwise_fma((f2){wk, wk}, p, rg);
+                    B = fmaf(wk, (float)((v >> 0) & 0xffu), B);
+                }
+            }
+            const int R16 = (int)lrintf(rg.x * kHFix), G16 = (int)lrintf(rg.y * kHFix);
+            hrg[r * kTileW + c] = (uint32_t)(R16 & 0xffff) | ((uint32_t)G16 << 16);
+            hb[r * kTileW + c] = (int16_t)lrintf(B * kHFix);
         }
-        hr[r * kTileW + c] = R;
-        hg[r * kTileW + c] = G;
-        hb[r * kTileW + c] = B;
     }
     __syncthreads();
+    // vertical pass: 2x2 outputs per thread; each tap reads R|G of both columns (two dwords)
+    // and B of both columns (one dword)
     const int lx = (tid & 31) * 2, ly = (tid >> 5) * 2;
     int Rq[2][2], Gq[2][2], Bq[2][2];
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
         const int base = by[ly + dy];
         const float* w = wys + (ly + dy) * ty;
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-            const int c = lx + dx;
-            float R = 0.f, G = 0.f, B = 0.f;
-            for (int k = 0; k < ty; ++k) {
-                const float wk = w[k];
-                const int o = (base + k) * kTileW + c;
-                R += wk * hr[o];
-                G += wk * hg[o];
-                B += wk * hb[o];
-            }
-            Rq[dy][dx] = min(max((int)lrintf(R), 0), 255);
-            Gq[dy][dx] = min(max((int)lrintf(G), 0), 255);
-            Bq[dy][dx] = min(max((int)lrintf(B), 0), 255);
+        f2 rg0 = {0.f, 0.f}, rg1 = {0.f, 0.f}, b01 = {0.f, 0.f};
+        for (int k = 0; k < ty; ++k) {
+            const float wk = w[k];
+            const int o = (base + k) * kTileW + lx;
+            const uint2 q = *reinterpret_cast<const uint2*>(hrg + o);       // columns lx, lx + 1
+            const uint32_t bb = *reinterpret_cast<const uint32_t*>(hb + o);  // B of both columns
+            const f2 p0 = {(float)(int16_t)(q.x & 0xffff), (float)(int16_t)(q.x >> 16)};
+            const f2 p1 = {(float)(int16_t)(q.y & 0xffff), (float)(int16_t)(q.y >> 16)};
+            const f2 pb = {(float)(int16_t)(bb & 0xffff), (float)(int16_t)(bb >> 16)};
+            const f2 ww = {wk, wk};
+            rg0 = __builtin_elementwise_fma(ww, p0, rg0);
+            rg1 = __builtin_elementwise_fma(ww, p1, rg1);
+            b01 = __builtin_elementwise_fma(ww, pb, b01);
         }
+        const float inv = 1.f / kHFix;
+        Rq[dy][0] = min(max((int)lrintf(rg0.x * inv), 0), 255);
+        Gq[dy][0] = min(max((int)lrintf(rg0.y * inv), 0), 255);
+        Rq[dy][1] = min(max((int)lrintf(rg1.x * inv), 0), 255);
+        Gq[dy][1] = min(max((int)lrintf(rg1.y * inv), 0), 255);
+        Bq[dy][0] = min(max((int)lrintf(b01.x * inv), 0), 255);
+        Bq[dy][1] = min(max((int)lrintf(b01.y * inv), 0), 255);
     }
     const int x = ox0 + lx, y = oy0 + ly;
     if (x >= coded_w || y >= coded_h) return;
     // output pixels beyond out_w/out_h replicate the last column/row (coded padding)
+    // (selects, not dynamic indices: keeps the 2x2 block in registers)
+    if (y + 1 >= t.out_h) {
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) Rq[1][dx] = Rq[0][dx], Gq[1][dx] = Gq[0][dx], Bq[1][dx] = Bq[0][dx];
+    }
+    if (x + 1 >= t.out_w) {
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) Rq[dy][1] = Rq[dy][0], Gq[dy][1] = Gq[dy][0], Bq[dy][1] = Bq[dy][0];
+    }
+#pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
-        const int srcdy = (y + dy < t.out_h) ? dy : 0;
-        uint16_t pair = 0;
-        for (int dx = 0; dx < 2; ++dx) {
-            const int srcdx = (x + dx < t.out_w) ? dx : 0;
-            pair |= (uint16_t)(y709(Rq[srcdy][srcdx], Gq[srcdy][srcdx], Bq[srcdy][srcdx]) << (8 * dx));
-        }
+        const uint16_t pair = (uint16_t)(y709(Rq[dy][0], Gq[dy][0], Bq[dy][0]) |
+                                         (y709(Rq[dy][1], Gq[dy][1], Bq[dy][1]) << 8));
         *reinterpret_cast<uint16_t*>(yp + (size_t)(y + dy) * out_pitch + x) = pair;
     }
     const int R = (Rq[0][0] + Rq[0][1] + Rq[1][0] + Rq[1][1] + 2) >> 2;
     const int G = (Gq[0][0] + Gq[0][1] + Gq[1][0] + Gq[1][1] + 2) >> 2;
     const int B = (Bq[0][0] + Bq[0][1] + Bq[1][0] + Bq[1][1] + 2) >> 2;
-    uvp[(size_t)(y / 2) * out_pitch + x] = (uint8_t)u709(R, G, B);
-    uvp[(size_t)(y / 2) * out_pitch + x + 1] = (uint8_t)v709(R, G, B);
+    *reinterpret_cast<uint16_t*>(uvp + (size_t)(y / 2) * out_pitch + x) =
+        (uint16_t)(u709(R, G, B) | (v709(R, G, B) << 8));
+}
+
+// ---------------------------------------------------------------- MFMA Lanczos scaler
+// Both resampling passes are banded matrix products, so they run on the matrix cores
+// (v_mfma_f32_32x32x16_f16).  A workgroup (2 waves) owns a 64 x 32 output tile; each wave a
+// 32 x 32 block.  Per 32-row block b of the input footprint and colour channel c:
+//   X = In_c[rows of b][K window] * Wh[K window][32 output columns]      (horizontal)
+//   Y_c += Wv[32 output rows][rows of b] * X                              (vertical)
+// X's accumulator (output column on the lane, input rows in registers) is the vertical
+// product's B operand as it stands (rows in the permuted k order of the fragment map; the
+// host lays Wv's fragments out in that order), so X never goes through LDS.  Input pixels
+// are f16 (1024 + p): v_perm gathers one channel byte of two pixels and an OR with
+// 0x6400 makes the f16 -- the 1024 * sum(w) bias leaves per column (`sh`).  The footprint
+// is staged global -> LDS with 16-byte LDS-DMA (global_load_lds_dwordx4); only quads that
+// cross the left/right image edge are rewritten with clamped pixels.
+constexpr int kMfKs = 8;  // max horizontal K-steps (16 input columns each) per 32 output columns
+constexpr int kMfRb = 4;  // max 32-row input blocks per 32 output rows
+typedef _Float16 mf_h8 __attribute__((ext_vector_type(8)));
+typedef float mf_f16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ mf_h8 mf_chan(const uint4& a, const uint4& b, uint32_t sel) {
+    uint4 r;
+    r.x = __builtin_amdgcn_perm(a.y, a.x, sel) | 0x64006400u;
+    r.y = __builtin_amdgcn_perm(a.w, a.z, sel) | 0x64006400u;
+    r.z = __builtin_amdgcn_perm(b.y, b.x, sel) | 0x64006400u;
+    r.w = __builtin_amdgcn_perm(b.w, b.z, sel) | 0x64006400u;
+    return __builtin_bit_cast(mf_h8, r);
+}
+
+__device__ __forceinline__ int clamp255(float v) { return min(max((int)__builtin_rintf(v), 0), 255); }
+
+// Stage rows [r0, r0 + 32) of the footprint (clipped to nr) into `buf` with LDS-DMA, one
+// footprint row per wave instruction: lane q < nq copies input pixels xlo + 4q .. +3 (its
+// clamped byte offset `loff`) of input row ylo + r0 + r to LDS quad r * nq + q.
+__device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ in, int in_pitch, int in_h, int ylo, int r0,
+                                         int nr, int nq, uint32_t loff, char* buf, int wave, int lane) {
+    const int rows = min(32, nr - r0);
+    for (int r = wave; r < rows; r += 2) {
+        const int sy = min(max(ylo + r0 + r, 0), in_h - 1);
+        if (lane < nq)
+            __builtin_amdgcn_global_load_lds(in + (size_t)sy * in_pitch + loff,
+                                             (lds_void_t*)(buf + (size_t)r * nq * 16), 16, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
+                                                    ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
+                                                    int out_pitch, int coded_w, int coded_h, int dbg) {
+    // LDS: two 32-row footprint buffers [32][lds_cols] BGRx; row block b + 1 streams in
+    // (LDS-DMA) while block b's products run
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g0 = 2 * blockIdx.x, gw = min(g0 + wave, m.ngx - 1), v = blockIdx.y;
+    const int xlo = m.gx[2 * g0];
+    const int ylo = m.gy[3 * v], nrb = m.gy[3 * v + 1], nr = m.gy[3 * v + 2];
+    const int nq = m.lds_cols >> 2;
+    const size_t buf_bytes = (size_t)32 * m.lds_cols * 4;
+    const uint32_t loff = (uint32_t)min(max(xlo + 4 * lane, 0), in_w - 4) * 4;
+    mf_stage(in, in_pitch, in_h, ylo, 0, nr, nq, loff, smem, wave, lane);
+    // weight fragments, while the first block streams in
+    const int nks = m.gx[2 * gw + 1], kb = m.gx[2 * gw] - xlo;
+    const uint4* fh = reinterpret_cast<const uint4*>(m.fh) + (size_t)gw * kMfKs * 64 + lane;
+    const uint4* fv = reinterpret_cast<const uint4*>(m.fv) + (size_t)v * kMfRb * 128 + lane;
+    mf_h8 bh[kMfKs], av[kMfRb][2];
+#pragma unroll
+    for (int s = 0; s < kMfKs; ++s) bh[s] = __builtin_bit_cast(mf_h8, s < nks ? fh[s * 64] : make_uint4(0, 0, 0, 0));
+#pragma unroll
+    for (int b = 0; b < kMfRb; ++b) {
+        av[b][0] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128] : make_uint4(0, 0, 0, 0));
+        av[b][1] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128 + 64] : make_uint4(0, 0, 0, 0));
+    }
+    const float bias = 1024.f * m.sh[gw * 32 + l32];  // f16 input bias: 1024 * sum(w)
+    const bool edge = xlo < 0 || xlo + 4 * nq > in_w;  // workgroup-uniform
+    // channel c of pixels (2p, 2p+1) -> f16 pair: byte c of each into the low byte of a half
+    constexpr uint32_t kSel[3] = {0x0c040c00u, 0x0c050c01u, 0x0c060c02u};  // B, G, R
+    mf_f16 Y[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        Y[c] = (mf_f16){};
+#pragma unroll
+    for (int b = 0; b < kMfRb; ++b) {
+        if (b > 0 && b >= nrb) break;  // nrb >= 1
+        char* buf = smem + (b & 1) * buf_bytes;
+        __syncthreads();  // block b landed; every wave is done with block b - 1's buffer
+        if (b + 1 < nrb)
+            mf_stage(in, in_pitch, in_h, ylo, 32 * (b + 1), nr, nq, loff, smem + ((b + 1) & 1) * buf_bytes, wave,
+                     lane);
+        if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
+            const int rows = min(32, nr - 32 * b);
+            for (int r = wave; r < rows; r += 2) {
+                const int sx = xlo + 4 * lane;
+                if (lane >= nq || (sx >= 0 && sx + 4 <= in_w)) continue;
+                const uint8_t* row = in + (size_t)min(max(ylo + 32 * b + r, 0), in_h - 1) * in_pitch;
+                uint4 px;
+                px.x = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx, 0), in_w - 1) * 4);
+                px.y = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 1, 0), in_w - 1) * 4);
+                px.z = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 2, 0), in_w - 1) * 4);
+                px.w = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 3, 0), in_w - 1) * 4);
+                *reinterpret_cast<uint4*>(buf + ((size_t)r * nq + lane) * 16) = px;
+            }
+            __syncthreads();
+        }
+        const uint32_t* rp =
+            reinterpret_cast<const uint32_t*>(buf) + min(l32, nr - 1 - 32 * b) * m.lds_cols + kb + 8 * h;
+        if (dbg == 1) {
+            Y[0][0] += __builtin_bit_cast(float, rp[0]) * 1e-30f;
+            continue;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {  // one channel at a time: a single 16-register X accumulator
+            mf_f16 X = {};
+#pragma unroll
+            for (int s = 0; s < kMfKs; ++s) {
+                if (s > 0 && s >= nks) break;  // nks >= 1
+                const uint4 p0 = *reinterpret_cast<const uint4*>(rp + 16 * s);
+                const uint4 p1 = *reinterpret_cast<const uint4*>(rp + 16 * s + 4);
+                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(mf_chan(p0, p1, kSel[c]), bh[s], X, 0, 0, 0);
+            }
+            mf_h8 x0, x1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                x0[j] = (_Float16)(X[j] - bias);
+                x1[j] = (_Float16)(X[8 + j] - bias);
+            }
+            Y[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[b][0], x0, Y[c], 0, 0, 0);
+            Y[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[b][1], x1, Y[c], 0, 0, 0);
+        }
+    }
+    // epilogue: Y[c][rho] is output column ox, row oy0 + (rho & 3) + 8 * (rho >> 2) + 4h;
+    // two rows at a time in packed 16-bit lanes (BT.709 sums stay below 2^16)
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const int ox = 32 * (g0 + wave) + l32, oy0 = 32 * v + 4 * h;
+    const bool xin = ox < coded_w;
+#pragma unroll
+    for (int rho = 0; rho < 16; rho += 2) {
+        const int oy = oy0 + (rho & 3) + 8 * (rho >> 2);
+        auto q8 = [](float f) { return (unsigned short)min(max((int)__builtin_rintf(f), 0), 255); };
+        const u16x2 R = {q8(Y[2][rho]), q8(Y[2][rho + 1])};
+        const u16x2 G = {q8(Y[1][rho]), q8(Y[1][rho + 1])};
+        const u16x2 B = {q8(Y[0][rho]), q8(Y[0][rho + 1])};
+        const u16x2 L = ((u16x2)(47) * R + (u16x2)(157) * G + (u16x2)(16) * B + (u16x2)(128)) >> (u16x2)(8);
+        const bool yin = xin && oy < coded_h;
+        if (yin) {
+            const uint32_t o = (uint32_t)oy * (uint32_t)out_pitch + (uint32_t)ox;
+            yp[o] = (uint8_t)(L.x + 16);
+            yp[o + (uint32_t)out_pitch] = (uint8_t)(L.y + 16);
+        }
+        // 2x2 chroma: this lane's row pair plus the neighbouring column's (lane ^ 1)
+        const int packed = (R.x + R.y) | ((G.x + G.y) << 10) | ((B.x + B.y) << 20);
+        const int other = __shfl_xor(packed, 1);
+        if (yin && !(lane & 1)) {
+            const int Rc = ((packed & 1023) + (other & 1023) + 2) >> 2;
+            const int Gc = (((packed >> 10) & 1023) + ((other >> 10) & 1023) + 2) >> 2;
+            const int Bc = (((packed >> 20) & 1023) + ((other >> 20) & 1023) + 2) >> 2;
+            *reinterpret_cast<uint16_t*>(uvp + ((uint32_t)(oy >> 1) * (uint32_t)out_pitch + (uint32_t)ox)) =
+                (uint16_t)(u709(Rc, Gc, Bc) | (v709(Rc, Gc, Bc) << 8));
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_composite(const uint8_t* __restrict__ tile, int tile_pitch, int tw, int th,
@@ -555,14 +776,139 @@ void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_
                        coded_h);
 }
 
+bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, int coded_h,
+                       const std::vector<int>& x0, const std::vector<float>& wx, int tx, const std::vector<int>& y0,
+                       const std::vector<float>& wy, int ty, ScaleFragsHost& out) {
+    if (in_w < 4 || out_w < 1 || out_h < 1) return false;
+    const int ngx = (coded_w + 31) / 32, ngy = (coded_h + 31) / 32;
+    auto f16 = [](float w) {  // weights below the f16 normal range are dropped (matrix-core flush)
+        const _Float16 hv = (_Float16)(std::fabs(w) < 6.103515625e-05f ? 0.f : w);
+        uint16_t bits;
+        std::memcpy(&bits, &hv, 2);
+        return std::make_pair(bits, (float)hv);
+    };
+    std::vector<int> gx(2 * (size_t)ngx), gy(3 * (size_t)ngy);
+    std::vector<uint16_t> fh((size_t)ngx * kMfKs * 64 * 8, 0), fv((size_t)ngy * kMfRb * 2 * 64 * 8, 0);
+    std::vector<float> sh((size_t)ngx * 32, 0.f);
+    for (int g = 0; g < ngx; ++g) {
+        const int kabs = x0[std::min(32 * g, out_w - 1)] & ~3;
+        const int kend = x0[std::min(32 * g + 31, out_w - 1)] + tx;
+        const int nks = (kend - kabs + 15) / 16;
+        if (nks > kMfKs) return false;
+        gx[2 * g] = kabs;
+        gx[2 * g + 1] = nks;
+        for (int l = 0; l < 64; ++l) {
+            const int cc = std::min(32 * g + (l & 31), out_w - 1), hh = l >> 5;
+            for (int s = 0; s < nks; ++s)
+                for (int j = 0; j < 8; ++j) {
+                    const int tap = kabs + 16 * s + 8 * hh + j - x0[cc];
+                    if (tap < 0 || tap >= tx) continue;
+                    const auto hv = f16(wx[(size_t)cc * tx + tap]);
+                    fh[(((size_t)g * kMfKs + s) * 64 + l) * 8 + j] = hv.first;
+                }
+        }
+        for (int c = 0; c < 32; ++c) {  // exact in f32: few f16 terms of bounded exponent range
+            const int cc = std::min(32 * g + c, out_w - 1);
+            float sum = 0.f;
+            for (int k = 0; k < tx; ++k) sum += f16(wx[(size_t)cc * tx + k]).second;
+            sh[(size_t)g * 32 + c] = sum;
+        }
+    }
+    int lds_cols = 0, lds_rows = 0;
+    for (int g0 = 0; g0 < ngx; g0 += 2)
+        for (int w = 0; w < 2; ++w) {
+            const int g = std::min(g0 + w, ngx - 1);
+            lds_cols = std::max(lds_cols, gx[2 * g] - gx[2 * g0] + 16 * gx[2 * g + 1]);
+        }
+    lds_cols = (lds_cols + 3) & ~3;
+    if (((lds_cols >> 2) & 1) == 0) lds_cols += 4;  // odd quad pitch: conflict-free row-parallel b128 reads
+    for (int v = 0; v < ngy; ++v) {
+        const int ylo = y0[std::min(32 * v, out_h - 1)];
+        const int nr = y0[std::min(32 * v + 31, out_h - 1)] + ty - ylo;
+        const int nrb = (nr + 31) / 32;
+        if (nrb > kMfRb) return false;
+        gy[3 * v] = ylo;
+        gy[3 * v + 1] = nrb;
+        gy[3 * v + 2] = nr;
+        lds_rows = std::max(lds_rows, nr);
+        for (int l = 0; l < 64; ++l) {
+            const int oy = std::min(32 * v + (l & 31), out_h - 1), hh = l >> 5;
+            for (int b = 0; b < nrb; ++b)
+                for (int t = 0; t < 2; ++t)
+                    for (int j = 0; j < 8; ++j) {
+                        // element j of lane half hh in k-step t holds accumulator row
+                        // 16t + 8(j >> 2) + 4hh + (j & 3) of the 32-row block
+                        const int q = 16 * t + 8 * (j >> 2) + 4 * hh + (j & 3);
+                        const int tap = ylo + 32 * b + q - y0[oy];
+                        if (tap < 0 || tap >= ty) continue;
+                        fv[((((size_t)v * kMfRb + b) * 2 + t) * 64 + l) * 8 + j] = f16(wy[(size_t)oy * ty + tap]).first;
+                    }
+        }
+    }
+    if ((size_t)2 * 32 * lds_cols * 4 > 160 * 1024 || lds_cols > 256) return false;  // one row per wave load
+    auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    out.off_gx = 0;
+    out.off_gy = align(gx.size() * 4);
+    out.off_sh = out.off_gy + align(gy.size() * 4);
+    out.off_fh = out.off_sh + align(sh.size() * 4);
+    out.off_fv = out.off_fh + align(fh.size() * 2);
+    out.blob.assign(out.off_fv + align(fv.size() * 2), 0);
+    std::memcpy(out.blob.data() + out.off_gx, gx.data(), gx.size() * 4);
+    std::memcpy(out.blob.data() + out.off_gy, gy.data(), gy.size() * 4);
+    std::memcpy(out.blob.data() + out.off_sh, sh.data(), sh.size() * 4);
+    std::memcpy(out.blob.data() + out.off_fh, fh.data(), fh.size() * 2);
+    std::memcpy(out.blob.data() + out.off_fv, fv.data(), fv.size() * 2);
+    out.lds_cols = lds_cols;
+    out.lds_rows = lds_rows;
+    out.ngx = ngx;
+    out.ngy = ngy;
+    (void)in_h;
+    return true;
+}
+
+void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf) {
+    if (hipMalloc(dev, h.blob.size()) != hipSuccess) throw std::runtime_error("upload_scale_frags: hipMalloc");
+    if (hipMemcpy(*dev, h.blob.data(), h.blob.size(), hipMemcpyHostToDevice) != hipSuccess)
+        throw std::runtime_error("upload_scale_frags: hipMemcpy");
+    const char* b = static_cast<const char*>(*dev);
+    mf.gx = reinterpret_cast<const int*>(b + h.off_gx);
+    mf.gy = reinterpret_cast<const int*>(b + h.off_gy);
+    mf.sh = reinterpret_cast<const float*>(b + h.off_sh);
+    mf.fh = b + h.off_fh;
+    mf.fv = b + h.off_fv;
+    mf.lds_cols = h.lds_cols;
+    mf.lds_rows = h.lds_rows;
+    mf.ngx = h.ngx;
+    mf.ngy = h.ngy;
+}
+
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
                           uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream) {
+    if (t.mf.gx && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 && in_w >= 4) {
+        const size_t lds = (size_t)2 * 32 * t.mf.lds_cols * 4;
+        if (lds > 64 * 1024) {
+            static bool raised = false;
+            if (!raised) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scale_mfma),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                raised = true;
+            }
+        }
+        dim3 grid((coded_w + 63) / 64, (coded_h + 31) / 32);
+        static const int dbg = getenv("MXDESK_SCALE_DBG") ? atoi(getenv("MXDESK_SCALE_DBG")) : 0;
+        hipLaunchKernelGGL(k_scale_mfma, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv,
+                           out_pitch, coded_w, coded_h, dbg);
+        return;
+    }
     // worst-case footprint of a tile: scale * tile + taps
     const float sx = (float)in_w / t.out_w, sy = (float)in_h / t.out_h;
-    const int max_nc = (int)ceilf(sx * kTileW) + t.taps_x + 2;
+    // +4 columns for the aligned start, rounded to whole quads (16-byte LDS stores)
+    const int max_nc = (((int)ceilf(sx * kTileW) + t.taps_x + 2 + 4) + 3) & ~3;
     const int max_nr = (int)ceilf(sy * kTileH) + t.taps_y + 2;
-    const size_t lds = (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15) + (size_t)max_nr * kTileW * 12 +
+    const size_t lds = (((size_t)max_nr * max_nc * 4 + 15) & ~(size_t)15) +
+                       ((3 * (size_t)max_nr * kTileW + 7) & ~(size_t)7) * 2 +
                        (size_t)(kTileW * t.taps_x + kTileH * t.taps_y) * 4 + (kTileW + kTileH) * 4;
+    const int vec = ((in_pitch & 15) == 0 && (reinterpret_cast<uintptr_t>(bgrx) & 15) == 0) ? 1 : 0;
     if (lds > 160 * 1024) throw std::runtime_error("scale_to_nv12: scale factor too large for one LDS tile");
     if (lds > 64 * 1024) {
         static bool raised = false;
@@ -574,7 +920,7 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     }
     dim3 grid((coded_w + kTileW - 1) / kTileW, (coded_h + kTileH - 1) / kTileH);
     hipLaunchKernelGGL(k_scale_to_nv12, grid, dim3(256), lds, stream, bgrx, in_pitch, in_w, in_h, t, y, uv, out_pitch,
-                       coded_w, coded_h, max_nc, max_nr);
+                       coded_w, coded_h, max_nc, max_nr, vec);
 }
 
 void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,

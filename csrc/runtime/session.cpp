@@ -120,6 +120,12 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         p += wx.size() * 4;
         lt_.wy = reinterpret_cast<const float*>(p);
         HIP_CHECK(hipMemcpy(p, wy.data(), wy.size() * 4, hipMemcpyHostToDevice));
+        // matrix-core form of the scaler (falls back to the VALU kernel outside its range)
+        const h264::Geometry& eg = enc_->geometry();
+        pix::ScaleFragsHost fr;
+        if (!cfg_.scale_valu && pix::build_scale_frags(cfg_.width, cfg_.height, cfg_.out_width, cfg_.out_height,
+                                                       eg.coded_w, eg.coded_h, sx, wx, tx, sy, wy, ty, fr))
+            pix::upload_scale_frags(fr, &lt_mf_mem_, lt_.mf);
     }
     for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
     mask_in_encoder_ = std::string(enc_->codec()) == "h264";
@@ -158,6 +164,7 @@ Session::~Session() {
     for (int k = 0; k < 2; ++k)
         if (staging_[k]) (void)hipHostFree(staging_[k]);
     if (lt_mem_) hipFree(lt_mem_);
+    if (lt_mf_mem_) hipFree(lt_mf_mem_);
     for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
     if (mask_dev_) (void)hipFree(mask_dev_);
     if (mask_counter_) (void)hipFree(mask_counter_);

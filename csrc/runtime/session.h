@@ -62,6 +62,7 @@ struct SessionConfig {
     // optional quality report: luma PSNR with a rectangle (encoded-picture coordinates) left
     // out, e.g. the incompressible noise panel of the synthetic desktop; mask_x1 <= mask_x0 = off
     int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;
+    int scale_valu = 0;     // 1: the LDS/VALU Lanczos kernel instead of the matrix-core one
     h264::EncoderConfig enc;  // width/height overwritten from out size
 };
 
@@ -131,6 +132,7 @@ class Session {
     bool scale_ = false;
     pix::LanczosTables lt_{};
     void* lt_mem_ = nullptr;
+    void* lt_mf_mem_ = nullptr;  // MFMA scaler fragment tables
     // frames in flight (pipeline depth 1 or 2): per-frame start event / staging buffer
     struct Inflight {
         uint32_t frame_id;

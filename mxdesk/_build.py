@@ -69,6 +69,11 @@ def _flags() -> list[str]:
     ]
 
 
+# per-source extra flags: the scaler's MFMA accumulators in arch VGPRs (no AGPR copies
+# around the f16 conversion between its two products; profiles/r02_scale)
+_EXTRA = {"kernels/pixel.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _newest_header() -> float:
     return max((p.stat().st_mtime for p in CSRC.rglob("*.h")), default=0.0)
 
@@ -79,7 +84,8 @@ def _compile(src: Path, force: bool, hdr_mtime: float) -> tuple[Path, str]:
         return obj, ""
     obj.parent.mkdir(parents=True, exist_ok=True)
     lang = ["-x", "hip"]
-    cmd = [_hipcc(), *lang, *_flags(), *_includes(), "-c", str(src), "-o", str(obj)]
+    extra = _EXTRA.get(str(src.relative_to(CSRC)), [])
+    cmd = [_hipcc(), *lang, *_flags(), *extra, *_includes(), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {shlex.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -53,8 +53,10 @@ def _lanczos_ref(img, xs, wx, ys, wy):
     return np.clip(np.rint(out), 0, 255)
 
 
-@pytest.mark.parametrize("src_hw,dst_hw", [((96, 160), (48, 80)), ((64, 96), (96, 128)), ((90, 150), (60, 100))])
-def test_lanczos_scale_matches_reference(gpu, src_hw, dst_hw):
+@pytest.mark.parametrize("mfma", [False, True])
+@pytest.mark.parametrize("src_hw,dst_hw", [((96, 160), (48, 80)), ((64, 96), (96, 128)), ((90, 150), (60, 100)),
+                                           ((270, 500), (108, 200)), ((200, 330), (100, 166))])
+def test_lanczos_scale_matches_reference(gpu, src_hw, dst_hw, mfma):
     rng = np.random.default_rng(1)
     (h, w), (oh, ow) = src_hw, dst_hw
     yy, xx = np.mgrid[0:h, 0:w]
@@ -70,14 +72,43 @@ def test_lanczos_scale_matches_reference(gpu, src_hw, dst_hw):
     y = torch.zeros((ch, cw), dtype=torch.uint8, device="cuda")
     uv = torch.zeros((ch // 2, cw), dtype=torch.uint8, device="cuda")
     gpu.scale_to_nv12(d_in.data_ptr(), w * 4, w, h, ow, oh, dx.data_ptr(), dwx.data_ptr(), tx, dy.data_ptr(),
-                      dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), cw, cw, ch, _stream())
+                      dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), cw, cw, ch, _stream(), mfma=mfma)
     torch.cuda.synchronize()
     rgb = _lanczos_ref(img, xs, wx, ys, wy)
     ref_bgrx = np.zeros((oh, ow, 4), np.uint8)
     ref_bgrx[..., :3] = rgb.astype(np.uint8)
-    ry, _, _ = bt709_nv12_reference(ref_bgrx)
+    ry, ru, rv = bt709_nv12_reference(ref_bgrx)
     Y = y.cpu().numpy()[:oh, :ow].astype(np.float64)
     assert np.abs(Y - ry).max() <= 1.5
+    UV = uv.cpu().numpy().astype(np.float64)
+    assert np.abs(UV[: oh // 2, 0:ow:2] - ru).max() <= 2.0
+    assert np.abs(UV[: oh // 2, 1:ow:2] - rv).max() <= 2.0
+    # coded padding replicates the last column / row
+    Yc = y.cpu().numpy()
+    assert np.array_equal(Yc[:oh, ow:cw], np.repeat(Yc[:oh, ow - 1: ow], cw - ow, axis=1))
+    assert np.array_equal(Yc[oh:ch, :], np.repeat(Yc[oh - 1: oh, :], ch - oh, axis=0))
+
+
+def test_lanczos_mfma_matches_valu_at_4k_to_1080p(gpu):
+    """Production size: the matrix-core scaler against the VALU one on a synthetic 4K desktop."""
+    w, h, ow, oh = 3840, 2160, 1920, 1080
+    src = torch.zeros((h, w * 4), dtype=torch.uint8, device="cuda")
+    gpu.synth(src.data_ptr(), w, h, w * 4, frame_id=7, t=0.25, noise=1, stream=_stream())
+    xs, wx, tx = gpu.lanczos_table(w, ow)
+    ys, wy, ty = gpu.lanczos_table(h, oh)
+    dx, dwx, dy, dwy = to_dev(xs), to_dev(wx), to_dev(ys), to_dev(wy)
+    out = {}
+    for mfma in (False, True):
+        y = torch.zeros((1088, 1920), dtype=torch.uint8, device="cuda")
+        uv = torch.zeros((544, 1920), dtype=torch.uint8, device="cuda")
+        gpu.scale_to_nv12(src.data_ptr(), w * 4, w, h, ow, oh, dx.data_ptr(), dwx.data_ptr(), tx, dy.data_ptr(),
+                          dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), 1920, 1920, 1088, _stream(), mfma=mfma)
+        torch.cuda.synchronize()
+        out[mfma] = (y.cpu().numpy().astype(np.int32), uv.cpu().numpy().astype(np.int32))
+    dyp = np.abs(out[True][0] - out[False][0])
+    duv = np.abs(out[True][1] - out[False][1])
+    assert dyp.max() <= 1 and duv.max() <= 1, (dyp.max(), duv.max())
+    assert (dyp > 0).mean() < 0.02 and (duv > 0).mean() < 0.02, ((dyp > 0).mean(), (duv > 0).mean())
 
 
 def _read_barcode(y_plane, cell, bx, by):
