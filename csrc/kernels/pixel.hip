@@ -12,7 +12,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -509,62 +508,58 @@ __device__ __forceinline__ mf_h8 mf_chan(const uint4& a, const uint4& b, uint32_
 __device__ __forceinline__ int clamp255(float v) { return min(max((int)__builtin_rintf(v), 0), 255); }
 
 // Stage rows [r0, r0 + 32) of the footprint (clipped to nr) into `buf` with LDS-DMA, one
-// footprint row per wave instruction: lane q < nq copies input pixels xlo + 4q .. +3 (its
-// clamped byte offset `loff`) of input row ylo + r0 + r to LDS quad r * nq + q.
+// footprint row per wave instruction (rows wave, wave + 2, ...: 16 instructions per wave for a
+// full block): lane q < nq copies input pixels xlo + 4q .. +3 (its clamped byte offset `loff`)
+// of input row ylo + r0 + r to LDS quad r * nq + q.
 __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ in, int in_pitch, int in_h, int ylo, int r0,
                                          int nr, int nq, uint32_t loff, char* buf, int wave, int lane) {
     const int rows = min(32, nr - r0);
-    for (int r = wave; r < rows; r += 2) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r = wave + 2 * i;
         const int sy = min(max(ylo + r0 + r, 0), in_h - 1);
-        if (lane < nq)
+        if (r < rows && lane < nq)
             __builtin_amdgcn_global_load_lds(in + (size_t)sy * in_pitch + loff,
                                              (lds_void_t*)(buf + (size_t)r * nq * 16), 16, 0, 0);
     }
 }
 
-__global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
-                                                    ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
-                                                    int out_pitch, int coded_w, int coded_h, int dbg) {
-    // LDS: two 32-row footprint buffers [32][lds_cols] BGRx; row block b + 1 streams in
-    // (LDS-DMA) while block b's products run
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g0 = 2 * blockIdx.x, gw = min(g0 + wave, m.ngx - 1), v = blockIdx.y;
-    const int xlo = m.gx[2 * g0];
-    const int ylo = m.gy[3 * v], nrb = m.gy[3 * v + 1], nr = m.gy[3 * v + 2];
-    const int nq = m.lds_cols >> 2;
-    const size_t buf_bytes = (size_t)32 * m.lds_cols * 4;
-    const uint32_t loff = (uint32_t)min(max(xlo + 4 * lane, 0), in_w - 4) * 4;
-    mf_stage(in, in_pitch, in_h, ylo, 0, nr, nq, loff, smem, wave, lane);
-    // weight fragments, while the first block streams in
-    const int nks = m.gx[2 * gw + 1], kb = m.gx[2 * gw] - xlo;
-    const uint4* fh = reinterpret_cast<const uint4*>(m.fh) + (size_t)gw * kMfKs * 64 + lane;
-    const uint4* fv = reinterpret_cast<const uint4*>(m.fv) + (size_t)v * kMfRb * 128 + lane;
-    mf_h8 bh[kMfKs], av[kMfRb][2];
-#pragma unroll
-    for (int s = 0; s < kMfKs; ++s) bh[s] = __builtin_bit_cast(mf_h8, s < nks ? fh[s * 64] : make_uint4(0, 0, 0, 0));
-#pragma unroll
-    for (int b = 0; b < kMfRb; ++b) {
-        av[b][0] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128] : make_uint4(0, 0, 0, 0));
-        av[b][1] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128 + 64] : make_uint4(0, 0, 0, 0));
-    }
-    const float bias = 1024.f * m.sh[gw * 32 + l32];  // f16 input bias: 1024 * sum(w)
+// Workgroup barrier that leaves LDS-DMA in flight: __syncthreads() makes hipcc drain vmcnt
+// to 0 first; the waits that matter here are explicit (LDS accesses: lgkmcnt(0)).
+__device__ __forceinline__ void mf_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+}
+
+// The block pipeline of one workgroup.  Blocks alternate between buf0 and buf1; blocks 0 and
+// 1 are posted up front and block b + 2 as soon as every wave is done with block b, so two
+// blocks' LDS-DMA are in flight at the start and one while each block's products run.  buf0 / buf1 are
+// __restrict__: the compiler then sees the ds_reads of one buffer as independent of the DMA
+// into the other and waits only for the DMA they depend on (a counted vmcnt, not vmcnt(0)).
+__device__ __forceinline__ void mf_main(char* __restrict__ buf0, char* __restrict__ buf1,
+                                        const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h, int xlo,
+                                        int ylo, int nr, int nrb, int nq, int lds_cols, uint32_t loff, int kb, int nks,
+                                        int wave, int lane, const mf_h8* bh, const mf_h8 (*av)[2], float bias,
+                                        mf_f16* Y) {
+    const int h = lane >> 5, l32 = lane & 31;
     const bool edge = xlo < 0 || xlo + 4 * nq > in_w;  // workgroup-uniform
+    mf_stage(in, in_pitch, in_h, ylo, 0, nr, nq, loff, buf0, wave, lane);
+    if (nrb > 1) mf_stage(in, in_pitch, in_h, ylo, 32, nr, nq, loff, buf1, wave, lane);
     // channel c of pixels (2p, 2p+1) -> f16 pair: byte c of each into the low byte of a half
     constexpr uint32_t kSel[3] = {0x0c040c00u, 0x0c050c01u, 0x0c060c02u};  // B, G, R
-    mf_f16 Y[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-        Y[c] = (mf_f16){};
 #pragma unroll
     for (int b = 0; b < kMfRb; ++b) {
         if (b > 0 && b >= nrb) break;  // nrb >= 1
-        char* buf = smem + (b & 1) * buf_bytes;
-        __syncthreads();  // block b landed; every wave is done with block b - 1's buffer
-        if (b + 1 < nrb)
-            mf_stage(in, in_pitch, in_h, ylo, 32 * (b + 1), nr, nq, loff, smem + ((b + 1) & 1) * buf_bytes, wave,
-                     lane);
+        char* cur = (b & 1) ? buf1 : buf0;
+        // this wave's DMA of block b retired (__syncthreads() alone does not wait for LDS-DMA).
+        // Block 0 waits for everything (blocks 0 and 1 and the weight fragments, which were all
+        // in flight together); from block 1 on, the DMA of block b + 1 (posted one block
+        // earlier, at most 16 instructions) stays in flight.
+        if (b > 0 && b + 1 < nrb)
+            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        mf_barrier();
         if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
             const int rows = min(32, nr - 32 * b);
             for (int r = wave; r < rows; r += 2) {
@@ -576,16 +571,12 @@ __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ 
                 px.y = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 1, 0), in_w - 1) * 4);
                 px.z = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 2, 0), in_w - 1) * 4);
                 px.w = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 3, 0), in_w - 1) * 4);
-                *reinterpret_cast<uint4*>(buf + ((size_t)r * nq + lane) * 16) = px;
+                *reinterpret_cast<uint4*>(cur + ((size_t)r * nq + lane) * 16) = px;
             }
             __syncthreads();
         }
         const uint32_t* rp =
-            reinterpret_cast<const uint32_t*>(buf) + min(l32, nr - 1 - 32 * b) * m.lds_cols + kb + 8 * h;
-        if (dbg == 1) {
-            Y[0][0] += __builtin_bit_cast(float, rp[0]) * 1e-30f;
-            continue;
-        }
+            reinterpret_cast<const uint32_t*>(cur) + min(l32, nr - 1 - 32 * b) * lds_cols + kb + 8 * h;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {  // one channel at a time: a single 16-register X accumulator
             mf_f16 X = {};
@@ -605,7 +596,56 @@ __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ 
             Y[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[b][0], x0, Y[c], 0, 0, 0);
             Y[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[b][1], x1, Y[c], 0, 0, 0);
         }
+        if (b + 2 < nrb) {  // block b + 2 into this buffer once every wave has read it
+            mf_barrier();
+            mf_stage(in, in_pitch, in_h, ylo, 32 * (b + 2), nr, nq, loff, cur, wave, lane);
+        }
     }
+}
+
+__global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
+                                                    ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
+                                                    int out_pitch, int coded_w, int coded_h) {
+    // LDS: two 32-row footprint buffers [32][lds_cols] BGRx (see mf_main)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // XCD-aware tile order: dispatch round-robins workgroups over the 8 XCDs (each with its own
+    // L2), so the linear id is remapped to give every XCD a contiguous band of tiles -- the
+    // footprint overlap between neighbouring tiles then hits in that XCD's L2
+    int tx_, ty_;
+    {
+        const int nwg = gridDim.x * gridDim.y, id = blockIdx.y * gridDim.x + blockIdx.x;
+        const int per = nwg >> 3, xcd = id & 7, k = id >> 3;
+        const int lin = k >= per ? id : xcd * per + k;  // the last partial round keeps its id
+        tx_ = lin % gridDim.x;
+        ty_ = lin / gridDim.x;
+    }
+    const int g0 = 2 * tx_, gw = min(g0 + wave, m.ngx - 1), v = ty_;
+    const int xlo = m.gx[2 * g0];
+    const int ylo = m.gy[3 * v], nrb = m.gy[3 * v + 1], nr = m.gy[3 * v + 2];
+    const int nq = m.lds_cols >> 2;
+    const size_t buf_bytes = (size_t)32 * m.lds_cols * 4;
+    const uint32_t loff = (uint32_t)min(max(xlo + 4 * lane, 0), in_w - 4) * 4;
+    // weight fragments (ordinary loads first: a later vmcnt wait for them would also drain
+    // the LDS-DMA issued after them)
+    const int nks = m.gx[2 * gw + 1], kb = m.gx[2 * gw] - xlo;
+    const uint4* fh = reinterpret_cast<const uint4*>(m.fh) + (size_t)gw * kMfKs * 64 + lane;
+    const uint4* fv = reinterpret_cast<const uint4*>(m.fv) + (size_t)v * kMfRb * 128 + lane;
+    mf_h8 bh[kMfKs], av[kMfRb][2];
+#pragma unroll
+    for (int s = 0; s < kMfKs; ++s) bh[s] = __builtin_bit_cast(mf_h8, s < nks ? fh[s * 64] : make_uint4(0, 0, 0, 0));
+#pragma unroll
+    for (int b = 0; b < kMfRb; ++b) {
+        av[b][0] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128] : make_uint4(0, 0, 0, 0));
+        av[b][1] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128 + 64] : make_uint4(0, 0, 0, 0));
+    }
+    const float bias = 1024.f * m.sh[gw * 32 + l32];  // f16 input bias: 1024 * sum(w)
+    mf_f16 Y[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Y[c] = (mf_f16){};
+    mf_main(smem, smem + buf_bytes, in, in_pitch, in_w, in_h, xlo, ylo, nr, nrb, nq, m.lds_cols, loff, kb, nks, wave,
+            lane, bh, av, bias, Y);
     // epilogue: Y[c][rho] is output column ox, row oy0 + (rho & 3) + 8 * (rho >> 2) + 4h;
     // two rows at a time in packed 16-bit lanes (BT.709 sums stay below 2^16)
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -895,9 +935,8 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
             }
         }
         dim3 grid((coded_w + 63) / 64, (coded_h + 31) / 32);
-        static const int dbg = getenv("MXDESK_SCALE_DBG") ? atoi(getenv("MXDESK_SCALE_DBG")) : 0;
         hipLaunchKernelGGL(k_scale_mfma, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv,
-                           out_pitch, coded_w, coded_h, dbg);
+                           out_pitch, coded_w, coded_h);
         return;
     }
     // worst-case footprint of a tile: scale * tile + taps
