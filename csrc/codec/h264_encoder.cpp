@@ -246,9 +246,8 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.coef, sizeof(int16_t) * kCoefStride * nmb));
     HIP_CHECK(hipMalloc(&b.slot, sizeof(uint32_t) * kSlotWords * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.slot_bits, sizeof(uint32_t) * nmb));
-    HIP_CHECK(hipMalloc(&b.unit_off, sizeof(uint32_t) * nmb));
-    HIP_CHECK(hipMalloc(&b.skip_run, sizeof(int32_t) * nmb));
-    HIP_CHECK(hipMalloc(&b.coded_list, sizeof(uint32_t) * nmb));
+    HIP_CHECK(hipMalloc(&b.row_agg, sizeof(uint4) * (size_t)geom_.mb_h));
+    HIP_CHECK(hipMalloc(&b.row_sse, sizeof(unsigned long long) * 4 * 512));
     HIP_CHECK(hipMalloc(&b.coded_info, sizeof(uint4) * nmb));
     HIP_CHECK(hipMalloc(&b.slice_info, sizeof(uint32_t) * kSliceInfo * kMaxSlices));
     HIP_CHECK(hipMemsetAsync(b.slice_info, 0, sizeof(uint32_t) * kSliceInfo * kMaxSlices, stream_));
@@ -273,8 +272,8 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
 
 void GpuH264Encoder::free_slot(FrameSlot& sl) {
     DeviceBuffers& b = sl.buf;
-    for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.unit_off,
-                    (void*)b.skip_run, (void*)b.coded_list, (void*)b.coded_info, (void*)b.slice_info,
+    for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.row_agg,
+                    (void*)b.row_sse, (void*)b.coded_info, (void*)b.slice_info,
                     (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.wave_line, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);

@@ -106,7 +106,7 @@ static_assert(sizeof(OutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
 // slice_info fields: 0 header bits, 1 byte offset, 2 bytes, 3 trailing skip run,
 // 4 data-end bit (trailer start), 5 unit-bit prefix at the slice's first MB,
-// 6 / 7 first / end rank of the slice's coded MBs in coded_list
+// 6 / 7 first / end rank of the slice's coded MBs in coded_info
 constexpr int kSliceInfo = 8;
 // host buffer: OutHeader | uint32 slice_off[kMaxSlices] | uint32 slice_len[kMaxSlices] | payload
 constexpr size_t kOutPayloadOffset = sizeof(OutHeader) + 2 * kMaxSlices * sizeof(uint32_t);
@@ -125,9 +125,8 @@ struct DeviceBuffers {
     int16_t* coef;          // [nmb * kCoefStride]
     uint32_t* slot;         // [nmb * kSlotWords]
     uint32_t* slot_bits;    // [nmb]
-    uint32_t* unit_off;     // [nmb] absolute bit offset of the MB unit (incl. skip run prefix)
-    int32_t* skip_run;      // [nmb] skip run preceding a coded MB, -1 for skipped MBs
-    uint32_t* coded_list;   // [nmb] indices of coded (non-skipped) MBs, in order
+    uint4* row_agg;         // [mb_h] per MB row: first / last coded MB, coded count | overflow, unit bits
+    unsigned long long* row_sse;  // [4][512] per-row distortion sums (k_scan_rows)
     uint4* coded_info;      // [nmb] per coded rank: {absolute bit offset, MB index, unit bits, skip run}
     uint32_t* quad_unit;    // [out_bytes / 16] per 128-bit output quad: rank of the unit holding its first bit
     uint32_t* slice_info;   // [kSliceInfo * kMaxSlices]

@@ -1305,17 +1305,33 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     // macroblock with residual); skipped / residual-free MBs inherit it.  Half-wave-parallel
     // backward search, 32 MBs per step (the ballot holds active lanes only; this half's bits
     // are taken).  I slices: every MB is at the slice QP.
+    // 128 MBs per step: each lane tests 4 (independent loads, one latency per step) and carries
+    // the QP along, so the predictor comes from a shuffle rather than another dependent load.
     int dqp = 0;
     if (!skip && !fs->idr && carries_dqp(m)) {
         const int per_slice = fs->slice_rows * g.mb_w, first = (mbi / per_slice) * per_slice;
         int pred = fs->qp;
-        for (int j0 = mbi - 1; j0 >= first; j0 -= 32) {
-            const int j = j0 - lane;
-            const unsigned long long bal = __ballot(j >= first && carries_dqp(mbs[j]));
-            const uint32_t hb = (uint32_t)(bal >> (32 * hw));
-            if (hb) {
-                pred = mbs[j0 - (__ffs(hb) - 1)].qp;
-                break;
+        bool found = false;
+        for (int j0 = mbi - 1; j0 >= first && !found; j0 -= 128) {
+            int qv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = j0 - 32 * k - lane;
+                qv[k] = -1;
+                if (j >= first) {
+                    const MbInfo& mj = mbs[j];
+                    if (carries_dqp(mj)) qv[k] = mj.qp;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned long long bal = __ballot(qv[k] >= 0);
+                const uint32_t hb = (uint32_t)(bal >> (32 * hw));
+                const int q = __shfl(qv[k], hb ? (int)(__ffs(hb) - 1) : 0, 32);
+                if (!found && hb) {
+                    pred = q;
+                    found = true;
+                }
             }
         }
         dqp = qp_delta(m.qp, pred);
@@ -1365,290 +1381,297 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     }
 }
 
-// ------------------------------------------------------------------ scan
-constexpr int kScanThreads = 1024;
-constexpr int kScanPer = 8;
-constexpr int kScanTile = kScanThreads * kScanPer;
+// ------------------------------------------------------------------ scan (two passes, one workgroup per MB row)
+// The bitstream layout needs, for every coded MB, its unit's absolute bit offset: unit bits =
+// ue(skip run) + MB bits, slices byte-aligned behind their headers.  Pass 1 (k_scan_rows)
+// summarises each MB row; pass 2 (k_scan_out) has every workgroup rebuild the row / slice
+// prefixes from those summaries (a few hundred values) and lay out its own row.  Both passes
+// spread the work over mb_h workgroups (a single-workgroup scan was latency bound at ~25 us).
+constexpr int kScanThreads = 256;
+constexpr int kScanRowPer = 2;   // MBs per thread in a row: mb_w <= 512
+constexpr int kScanMaxRows = 512;
+
+template <typename T, typename Op>
+__device__ __forceinline__ T blk_excl_scan(T v, T init, Op op, T* wbuf, T* total) {
+    constexpr int kW = kScanThreads / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const T t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl = op(incl, t);
+    }
+    T excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = init;
+    if (lane == 63) wbuf[w] = incl;
+    __syncthreads();
+    T before = init, all = init;
+    for (int k = 0; k < kW; ++k) {
+        if (k < w) before = op(before, wbuf[k]);
+        all = op(all, wbuf[k]);
+    }
+    __syncthreads();
+    *total = all;
+    return op(before, excl);
+}
+
+__device__ __forceinline__ uint32_t blk_excl_sum(uint32_t v, uint32_t* wbuf, uint32_t* total) {
+    return blk_excl_scan<uint32_t>(v, 0u, [](uint32_t a, uint32_t b) { return a + b; }, wbuf, total);
+}
+__device__ __forceinline__ int blk_excl_max(int v, int init, int* wbuf, int* total) {
+    return blk_excl_scan<int>(v, init, [](int a, int b) { return max(a, b); }, wbuf, total);
+}
 
 __device__ __forceinline__ SliceParams slice_params(const FrameState* fs, int s, int mb_w) {
     return make_slice_params(s * fs->slice_rows * mb_w, fs->idr, fs->frame_num, fs->log2_max_frame_num,
                              fs->idr_pic_id, fs->qp - fs->pic_init_qp, fs->deblock_off);
 }
 
-// Block-wide exclusive scans over 1024 threads (16 waves): wave shuffles + one LDS pass.
-__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* wsum, uint32_t* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    if (w == 0) {
-        uint32_t x = lane < kScanThreads / 64 ? wsum[lane] : 0;
-        uint32_t xi = x;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(xi, o, 64);
-            if (lane >= o) xi += t;
-        }
-        if (lane < kScanThreads / 64) wsum[lane] = xi - x;
-        if (lane == kScanThreads / 64 - 1) wsum[kScanThreads / 64] = xi;
-    }
-    __syncthreads();
-    const uint32_t r = wsum[w] + incl - v;
-    *total = wsum[kScanThreads / 64];
-    __syncthreads();
-    return r;
-}
-
-__device__ __forceinline__ int block_excl_max(int v, int* wmax, int init) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl = max(incl, t);
-    }
-    int excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) excl = init;
-    if (lane == 63) wmax[w] = incl;
-    __syncthreads();
-    if (w == 0) {
-        int x = lane < kScanThreads / 64 ? wmax[lane] : init;
-        int xi = x;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(xi, o, 64);
-            if (lane >= o) xi = max(xi, t);
-        }
-        int xe = __shfl_up(xi, 1, 64);
-        if (lane == 0) xe = init;
-        if (lane < kScanThreads / 64) wmax[lane] = xe;
-    }
-    __syncthreads();
-    const int r = max(wmax[w], excl);
-    __syncthreads();
-    return r;
-}
-
+// Pass 1, row r: {first coded MB or -1, last coded MB or -1, coded count | overflow << 31,
+// unit bits of the row excluding the skip-run prefix of its first coded MB (that run depends
+// on earlier rows)}; and this row's share of the distortion partials.
 // slot_bits[i]: 0 = P_Skip, 0xffffffff = slot overflow, else coded MB bits (>= 1).
-// Outputs: unit_off[i] bit offset of MB i's unit (skip-run prefix + MB bits) within the
-// concatenated slice data (k_pack reads the absolute offsets from coded_info),
-// skip_run[i] (-1 for skipped MBs), slice_info[kSliceInfo * s + ...].
-__global__ __launch_bounds__(kScanThreads) void k_scan(Geometry g, const FrameState* __restrict__ fs,
-                                                       const uint32_t* __restrict__ slot_bits,
-                                                       uint32_t* __restrict__ unit_off, int32_t* __restrict__ skip_run,
-                                                       uint32_t* __restrict__ coded_list,
-                                                       uint4* __restrict__ coded_info,
-                                                       uint32_t* __restrict__ slice_info, size_t out_bytes,
-                                                       OutHeader* __restrict__ hdr, uint32_t* __restrict__ quad_unit) {
-    __shared__ uint32_t sb[kScanTile];
-    __shared__ uint32_t s_base[kMaxSlices];
-    __shared__ uint32_t s_first_rank[kMaxSlices + 1], s_trail[kMaxSlices];  // LDS copies: no global re-reads
-    __shared__ uint32_t wsum[kScanThreads / 64 + 1];
-    __shared__ int wmax[kScanThreads / 64];
-    __shared__ uint32_t s_overflow;
-    const int t = threadIdx.x;
-    const int nmb = g.mb_w * g.mb_h;
-    const int per_slice = fs->slice_rows * g.mb_w;
-    const int ns = fs->num_slices;
+__global__ __launch_bounds__(kScanThreads) void k_scan_rows(Geometry g, const FrameState* __restrict__ fs,
+                                                            const uint32_t* __restrict__ slot_bits,
+                                                            uint4* __restrict__ row_agg,
+                                                            unsigned long long* __restrict__ row_sse) {
+    __shared__ int wi[kScanThreads / 64];
+    __shared__ uint32_t wu[kScanThreads / 64];
+    const int t = threadIdx.x, r = blockIdx.x, base = r * g.mb_w;
     const bool idr = fs->idr != 0;
-    if (t == 0) s_overflow = 0;
-    // distortion partials: issued now, reduced at the end (their latency hides behind the scan)
+    // distortion partials of this row's share (one per intra MB row or per 4-MB inter workgroup,
+    // plus the per-row intra deltas of k_intra_wave / k_intra_p)
+    const int nmb = g.mb_w * g.mb_h;
     const int nparts = idr ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
-    constexpr int kPartsPer = 8;  // partials per thread held in registers (<= 8192 per channel)
-    unsigned long long pacc[4] = {0, 0, 0, 0};
-    const bool pregs = nparts <= kPartsPer * kScanThreads;
-    if (pregs) {
+    const int p0 = (int)((long long)nparts * r / g.mb_h), p1 = (int)((long long)nparts * (r + 1) / g.mb_h);
+    unsigned long long acc[4] = {0, 0, 0, 0};
+    for (int i = p0 + t; i < p1; i += kScanThreads)
+        for (int c = 0; c < 4; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
+    uint32_t b[kScanRowPer];
+    int last = -1, first = 0x7fffffff;
+    uint32_t ncoded = 0, over = 0;
 #pragma unroll
-        for (int k = 0; k < kPartsPer; ++k) {
-            const int i = t + k * kScanThreads;
-            if (i < nparts)
-                for (int c = 0; c < 4; ++c) pacc[c] += fs->sse_part[c * kSsePartStride + i];
+    for (int k = 0; k < kScanRowPer; ++k) {
+        const int j = t * kScanRowPer + k;
+        b[k] = j < g.mb_w ? slot_bits[base + j] : 0u;
+        if (b[k] == 0xffffffffu) {
+            over = 1;
+            b[k] = 1;
+        }
+        if (b[k]) {
+            last = base + j;
+            first = min(first, base + j);
+            ++ncoded;
         }
     }
-    int carry_last = -1;      // last coded MB index before the current tile
-    uint32_t carry_bits = 0;  // unit bits before the current tile
-    uint32_t carry_rank = 0;  // coded MBs before the current tile
-    // single-tile pictures (<= 8192 MBs, 1080p) keep each thread's MB records in registers for
-    // the final coded_info pass (no dependent global reloads)
-    uint32_t ubk[kScanPer];
-    int runk[kScanPer];
-    uint32_t rank0 = 0;
-    for (int base = 0; base < nmb; base += kScanTile) {
-        const int n = min(kScanTile, nmb - base);
-        for (int j = t; j < n; j += kScanThreads) sb[j] = slot_bits[base + j];
-        __syncthreads();
-        const int j0 = t * kScanPer;
-        int last = -1;
-        uint32_t ncoded = 0;
-        for (int k = 0; k < kScanPer; ++k)
-            if (j0 + k < n && sb[j0 + k] != 0) {
-                last = base + j0 + k;
-                ++ncoded;
-            }
-        uint32_t tile_coded;
-        uint32_t rank = carry_rank + block_excl_sum(ncoded, wsum, &tile_coded);
-        rank0 = rank;
-        int prev = block_excl_max(last, wmax, -1);
-        prev = max(prev, carry_last);
-        uint32_t local = 0;
-        uint32_t ub[kScanPer];
-        int s = (base + j0) / per_slice;  // slice of the thread's first MB; advanced, not divided, per MB
-        for (int k = 0; k < kScanPer; ++k) {
-            ub[k] = 0;
-            runk[k] = -1;
-            const int j = j0 + k;
-            if (j >= n) continue;
-            const int i = base + j;
-            if (i >= (s + 1) * per_slice) ++s;
-            const int first = s * per_slice;
-            const int slast = min(first + per_slice, nmb) - 1;
-            const int pv = max(prev, first - 1);
-            uint32_t b = sb[j];
-            if (i == first) {
-                slice_info[kSliceInfo * s + 6] = rank;  // coded MBs before the slice
-                s_first_rank[s] = rank;
-            }
-            if (b != 0) {
-                coded_list[rank++] = (uint32_t)i;
-                if (b == 0xffffffffu) {
-                    s_overflow = 1;
-                    b = 1;
-                }
-                const int run = i - pv - 1;
-                skip_run[i] = run;
-                runk[k] = run;
-                ub[k] = (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b;
-                prev = i;
-            } else {
-                skip_run[i] = -1;
-            }
-            if (i == slast) {
-                const uint32_t tr = (b != 0) ? 0u : (uint32_t)(i - pv);
-                slice_info[kSliceInfo * s + 3] = tr;
-                s_trail[s] = tr;
-            }
-            local += ub[k];
-            ubk[k] = ub[k];
-        }
-        uint32_t tile_total;
-        const uint32_t ex = block_excl_sum(local, wsum, &tile_total);
-        uint32_t run_sum = carry_bits + ex;
-        for (int k = 0; k < kScanPer; ++k) {
-            if (j0 + k < n) sb[j0 + k] = run_sum;  // E[i]: exclusive prefix of unit bits
-            run_sum += ub[k];
-        }
-        __syncthreads();
-        for (int j = t; j < n; j += kScanThreads) unit_off[base + j] = sb[j];
-        // carry: the last thread's running `prev` is the last coded MB up to the tile end
-        if (t == kScanThreads - 1) wmax[0] = prev;
-        __syncthreads();
-        carry_last = wmax[0];
-        carry_bits += tile_total;
-        carry_rank += tile_coded;
-        __syncthreads();
+    int lastall;
+    int prev = blk_excl_max(last, -1, wi, &lastall);  // last coded MB of the row before this thread
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < kScanRowPer; ++k) {
+        if (!b[k]) continue;
+        const int i = base + t * kScanRowPer + k;
+        if (prev >= 0 && !idr) bits += (uint32_t)ue_len((uint32_t)(i - prev - 1));
+        bits += b[k];
+        prev = i;
     }
-    const uint32_t grand_total = carry_bits;
-    if (t == 0) s_first_rank[ns] = carry_rank;
+    uint32_t tb, tc, to;
+    (void)blk_excl_sum(bits, wu, &tb);
+    (void)blk_excl_sum(ncoded, wu, &tc);
+    (void)blk_excl_sum(over, wu, &to);
+    int firstall;
+    (void)blk_excl_scan<int>(first, 0x7fffffff, [](int x, int y) { return min(x, y); }, wi, &firstall);
+    if (t == 0)
+        row_agg[r] = make_uint4((uint32_t)(lastall >= 0 ? firstall : -1), (uint32_t)lastall,
+                                tc | (to ? 0x80000000u : 0u), tb);
+    __shared__ unsigned long long red[4][kScanThreads / 64];
+    for (int c = 0; c < 4; ++c) {
+        unsigned long long v = acc[c];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((t & 63) == 0) red[c][t >> 6] = v;
+    }
     __syncthreads();
-    if (t < ns) slice_info[kSliceInfo * t + 7] = s_first_rank[t + 1];
-    // per slice sizes (one thread per slice; ns <= kMaxSlices <= kScanThreads)
-    uint32_t sbytes = 0, ebase = 0, eend = 0, hbits = 0, trail = 0;
-    const bool one_tile = nmb <= kScanTile;  // unit offsets still in LDS (sb)
+    if (t < 4) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) v += red[t][w];
+        row_sse[t * kScanMaxRows + r] = v;
+    }
+}
+
+// Pass 2, row r: row / slice prefixes from all rows' summaries, then this row's units:
+// coded_info[rank] = {absolute bit offset, MB index, unit bits, skip run} and the quad -> unit
+// table for k_pack (rank of the unit -- or of the slice's first / end unit for header /
+// trailer bits -- holding each 128-bit output quad's first bit).  The workgroup of a slice's
+// first row writes slice_info; row 0 writes the header and the frame distortion.
+__global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const FrameState* __restrict__ fs,
+                                                           const uint32_t* __restrict__ slot_bits,
+                                                           const uint4* __restrict__ row_agg,
+                                                           const unsigned long long* __restrict__ row_sse,
+                                                           uint4* __restrict__ coded_info,
+                                                           uint32_t* __restrict__ slice_info, size_t out_bytes,
+                                                           OutHeader* __restrict__ hdr,
+                                                           uint32_t* __restrict__ quad_unit) {
+    __shared__ int s_lbraw[kScanMaxRows + 1];    // last coded MB before row j (any slice), -1 = none
+    __shared__ uint32_t s_P[kScanMaxRows + 1];   // unit bits before row j (frame-wide running sum)
+    __shared__ uint32_t s_R[kScanMaxRows + 1];   // coded MBs before row j
+    __shared__ uint32_t s_soff[kScanThreads + 1], s_sbytes[kScanThreads], s_hbits[kScanThreads];
+    __shared__ int wi[kScanThreads / 64];
+    __shared__ uint32_t wu[kScanThreads / 64];
+    const int t = threadIdx.x, r = blockIdx.x, mb_w = g.mb_w, mb_h = g.mb_h;
+    const bool idr = fs->idr != 0;
+    const int srows = fs->slice_rows, ns = fs->num_slices;
+    // rows t*2, t*2+1 of the frame per thread (mb_h <= kScanMaxRows)
+    uint4 ag[2];
+    int lastr = -1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int j = 2 * t + k;
+        ag[k] = j < mb_h ? row_agg[j] : make_uint4(0xffffffffu, 0xffffffffu, 0u, 0u);
+        lastr = max(lastr, (int)ag[k].y);
+    }
+    int dummy, lastframe;
+    int lb = blk_excl_max(lastr, -1, wi, &lastframe);
+    uint32_t contrib[2], nc[2], over = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int j = 2 * t + k;
+        contrib[k] = 0;
+        nc[k] = ag[k].z & 0x7fffffffu;
+        over |= ag[k].z >> 31;
+        if (j < mb_h) {
+            s_lbraw[j] = lb;
+            const int sfirst = (j / srows) * srows * mb_w;
+            const int pv = max(lb, sfirst - 1);
+            contrib[k] = ag[k].w;
+            if ((int)ag[k].x >= 0 && !idr) contrib[k] += (uint32_t)ue_len((uint32_t)((int)ag[k].x - pv - 1));
+        }
+        lb = max(lb, (int)ag[k].y);
+    }
+    uint32_t ptot, rtot, otot;
+    uint32_t pex = blk_excl_sum(contrib[0] + contrib[1], wu, &ptot);
+    uint32_t rex = blk_excl_sum(nc[0] + nc[1], wu, &rtot);
+    (void)blk_excl_sum(over, wu, &otot);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int j = 2 * t + k;
+        if (j < mb_h) {
+            s_P[j] = pex;
+            s_R[j] = rex;
+        }
+        pex += contrib[k];
+        rex += nc[k];
+    }
+    if (t == 0) {
+        s_P[mb_h] = ptot;
+        s_R[mb_h] = rtot;
+        s_lbraw[mb_h] = lastframe;
+    }
+    __syncthreads();
+    // slice sizes (ns <= kScanThreads: IDR slices are >= mb_h / 16 rows, P pictures one slice)
+    uint32_t sbytes = 0, hb = 0;
     if (t < ns) {
-        const int first = t * per_slice;
-        const int slast = min(first + per_slice, nmb) - 1;
-        ebase = one_tile ? sb[first] : unit_off[first];
-        eend = (slast + 1 < nmb) ? (one_tile ? sb[slast + 1] : unit_off[slast + 1]) : grand_total;
+        const int fr = t * srows, er = min(fr + srows, mb_h);
+        const int sfirst = fr * mb_w, slast = er * mb_w - 1;
+        const uint32_t data = s_P[er] - s_P[fr];
+        const int lastin = max(s_lbraw[er], sfirst - 1);
+        const uint32_t trail = idr ? 0u : (uint32_t)(slast - lastin);
         BitCounter bc;
         bc.init(nullptr);
-        write_slice_header(bc, slice_params(fs, t, g.mb_w));
-        hbits = bc.bits;
-        trail = idr ? 0u : s_trail[t];
-        const uint32_t bits = hbits + (eend - ebase) + (trail ? ue_len(trail) : 0) + 1;
+        write_slice_header(bc, slice_params(fs, t, mb_w));
+        hb = bc.bits;
+        const uint32_t bits = hb + data + (trail ? ue_len(trail) : 0) + 1;
         sbytes = (bits + 7) >> 3;
     }
     uint32_t total_bytes;
-    const uint32_t soff = block_excl_sum(sbytes, wsum, &total_bytes);
+    const uint32_t soff = blk_excl_sum(sbytes, wu, &total_bytes);
     if (t < ns) {
-        slice_info[kSliceInfo * t + 0] = hbits;
-        slice_info[kSliceInfo * t + 1] = soff;
-        slice_info[kSliceInfo * t + 2] = sbytes;
-        slice_info[kSliceInfo * t + 4] = soff * 8 + hbits + (eend - ebase);  // data end (trailer start)
-        slice_info[kSliceInfo * t + 5] = ebase;
+        s_soff[t] = soff;
+        s_sbytes[t] = sbytes;
+        s_hbits[t] = hb;
     }
-    __syncthreads();
-    // dense per-rank unit records for k_pack: one 16-byte load per unit instead of the
-    // coded_list -> unit_off / skip_run / slot_bits chains; and the quad -> unit table: for
-    // every 128-bit output quad, the rank of the unit (or the slice's first / end rank for
-    // header / trailer bits) holding the quad's first bit, so k_pack needs no search
-    if (t < ns) s_base[t] = soff * 8 + hbits - ebase;  // output bit of the slice's unit offset 0
     __syncthreads();
     const uint32_t nquads_max = (uint32_t)((out_bytes + 15) / 16);
-    auto mark_quads = [&](uint32_t a, uint32_t len, uint32_t r) {  // quads starting in [a, a + len)
+    auto mark_quads = [&](uint32_t a, uint32_t len, uint32_t rk) {  // quads starting in [a, a + len)
         if (len == 0) return;
         const uint32_t qe = min((a + len - 1) >> 7, nquads_max - 1);
-        for (uint32_t q = (a + 127) >> 7; q <= qe; ++q) quad_unit[q] = r;
+        for (uint32_t q = (a + 127) >> 7; q <= qe; ++q) quad_unit[q] = rk;
     };
-    if (nmb <= kScanTile) {
-        uint32_t r = rank0;
-        const int j0 = t * kScanPer;
-        for (int k = 0; k < kScanPer; ++k) {
-            const int j = j0 + k;
-            if (j >= nmb || ubk[k] == 0) continue;
-            const uint32_t off = s_base[j / per_slice] + sb[j];
-            coded_info[r] = make_uint4(off, (uint32_t)j, ubk[k], (uint32_t)runk[k]);
-            mark_quads(off, ubk[k], r);
-            ++r;
-        }
-    } else {
-        for (uint32_t r = t; r < carry_rank; r += kScanThreads) {
-            const int i = (int)coded_list[r];
-            const int s = i / per_slice;
-            const uint32_t off = s_base[s] + unit_off[i];
-            const int run = skip_run[i];
-            uint32_t b = slot_bits[i];
-            if (b == 0xffffffffu) b = 1;
-            const uint32_t len = (idr ? 0u : (uint32_t)ue_len((uint32_t)run)) + b;
-            coded_info[r] = make_uint4(off, (uint32_t)i, len, (uint32_t)run);
-            mark_quads(off, len, r);
+    const int s = r / srows, fr = s * srows, er = min(fr + srows, mb_h);
+    const uint32_t sbase = s_soff[s] * 8 + s_hbits[s];  // output bit of the slice's first unit
+    // slice-level records (the slice's first row)
+    if (r == fr && t == 0) {
+        const uint32_t data = s_P[er] - s_P[fr];
+        const int sfirst = fr * mb_w, slast = er * mb_w - 1;
+        const int lastin = max(s_lbraw[er], sfirst - 1);
+        const uint32_t trail = idr ? 0u : (uint32_t)(slast - lastin);
+        uint32_t* si = slice_info + kSliceInfo * s;
+        si[0] = s_hbits[s];
+        si[1] = s_soff[s];
+        si[2] = s_sbytes[s];
+        si[3] = trail;
+        si[4] = sbase + data;  // data end (trailer start)
+        si[5] = s_P[fr];
+        si[6] = s_R[fr];  // coded MBs before the slice
+        si[7] = s_R[er];
+        if (total_bytes <= out_bytes) {  // header and trailer quads of the slice
+            mark_quads(s_soff[s] * 8, s_hbits[s], s_R[fr]);
+            const uint32_t dend = sbase + data;
+            mark_quads(dend, s_soff[s] * 8 + s_sbytes[s] * 8 - dend, s_R[er]);
         }
     }
-    if (t < ns && total_bytes <= out_bytes) {  // header and trailer quads of the slice
-        mark_quads(soff * 8, hbits, s_first_rank[t]);
-        const uint32_t dend = soff * 8 + hbits + (eend - ebase);
-        mark_quads(dend, soff * 8 + sbytes * 8 - dend, s_first_rank[t + 1]);
-    }
-    if (t == 0) {
-        const bool over = total_bytes > out_bytes;
-        hdr->total_bytes = over ? 0 : total_bytes;
-        hdr->num_slices = ns;
-        hdr->overflow = s_overflow | (over ? 2u : 0u);
-    }
-    // distortion: block-wide reduction of the per-MB partials
-    {
-        // partials: one per intra MB row (IDR) or per inter workgroup (4 MBs) + the per-row
-        // intra deltas of k_intra_wave / k_intra_p (P pictures with intra macroblocks);
-        // prefetched into registers at the start when they fit
-        unsigned long long acc[4] = {pacc[0], pacc[1], pacc[2], pacc[3]};
-        if (!pregs)
-            for (int i = t; i < nparts; i += kScanThreads)
-                for (int c = 0; c < 4; ++c) acc[c] += fs->sse_part[c * kSsePartStride + i];
-        __shared__ unsigned long long red[4][kScanThreads / 64];
-        for (int c = 0; c < 4; ++c) {
-            unsigned long long v = acc[c];
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            if ((t & 63) == 0) red[c][t >> 6] = v;
+    if (r == 0 && t < 4) {
+        unsigned long long v = 0;
+        for (int j = 0; j < mb_h; ++j) v += row_sse[t * kScanMaxRows + j];
+        if (t < 3)
+            hdr->sse[t] = v;
+        else
+            hdr->sse_masked = v;
+        if (t == 0) {
+            const bool over_b = total_bytes > out_bytes;
+            hdr->total_bytes = over_b ? 0 : total_bytes;
+            hdr->num_slices = ns;
+            hdr->overflow = (otot ? 1u : 0u) | (over_b ? 2u : 0u);
         }
-        __syncthreads();
-        if (t < 4) {
-            unsigned long long v = 0;
-            for (int w = 0; w < kScanThreads / 64; ++w) v += red[t][w];
-            if (t < 3)
-                hdr->sse[t] = v;
-            else
-                hdr->sse_masked = v;
+    }
+    // this row's units
+    const int base = r * mb_w;
+    const int sfirst = fr * mb_w;
+    uint32_t b[kScanRowPer];
+    int last = -1;
+    uint32_t ncod = 0;
+#pragma unroll
+    for (int k = 0; k < kScanRowPer; ++k) {
+        const int j = t * kScanRowPer + k;
+        b[k] = j < mb_w ? slot_bits[base + j] : 0u;
+        if (b[k] == 0xffffffffu) b[k] = 1;
+        if (b[k]) {
+            last = base + j;
+            ++ncod;
         }
+    }
+    int prev = blk_excl_max(last, max(s_lbraw[r], sfirst - 1), wi, &dummy);
+    uint32_t ub[kScanRowPer], run[kScanRowPer], ltot = 0;
+#pragma unroll
+    for (int k = 0; k < kScanRowPer; ++k) {
+        ub[k] = 0;
+        run[k] = 0;
+        if (!b[k]) continue;
+        const int i = base + t * kScanRowPer + k;
+        run[k] = (uint32_t)(i - prev - 1);
+        ub[k] = (idr ? 0u : (uint32_t)ue_len(run[k])) + b[k];
+        ltot += ub[k];
+        prev = i;
+    }
+    uint32_t rowbits, rowcoded;
+    uint32_t off = sbase + (s_P[r] - s_P[fr]) + blk_excl_sum(ltot, wu, &rowbits);
+    uint32_t rk = s_R[r] + blk_excl_sum(ncod, wu, &rowcoded);
+#pragma unroll
+    for (int k = 0; k < kScanRowPer; ++k) {
+        if (!ub[k]) continue;
+        const int i = base + t * kScanRowPer + k;
+        coded_info[rk] = make_uint4(off, (uint32_t)i, ub[k], run[k]);
+        mark_quads(off, ub[k], rk);
+        off += ub[k];
+        ++rk;
     }
 }
 
@@ -1816,8 +1839,12 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + kCavlcMbPerBlock - 1) / kCavlcMbPerBlock), dim3(256), 0, stream, g, b.fs,
                        b.mb, b.coef, b.slot,
                        b.slot_bits);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.unit_off, b.skip_run,
-                       b.coded_list, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr, b.quad_unit);
+    if (g.mb_h > kScanMaxRows || g.mb_w > kScanThreads * kScanRowPer)
+        throw std::runtime_error("launch_entropy: frame too large for the row scan");
+    hipLaunchKernelGGL(k_scan_rows, dim3(g.mb_h), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.row_agg,
+                       b.row_sse);
+    hipLaunchKernelGGL(k_scan_out, dim3(g.mb_h), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.row_agg,
+                       b.row_sse, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr, b.quad_unit);
     hipLaunchKernelGGL(k_pack, dim3(256), dim3(256), 0, stream, g, b.fs, b.slot, b.coded_info, b.slice_info,
                        b.out_hdr, host_out, b.quad_unit);
 }
