@@ -1288,6 +1288,7 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     static_assert(kNumRoles < 32, "the roles of one MB (plus the total slot) must fit a half-wave");
     __shared__ uint32_t rbuf[kCavlcMbPerBlock][kNumRoles][kRoleWords];
     __shared__ uint32_t roff[kCavlcMbPerBlock][kNumRoles + 1];
+    __shared__ __attribute__((aligned(16))) int16_t cbuf[kCavlcMbPerBlock][kCoefStride];
     const int hw = (threadIdx.x >> 5) & 1, lane = threadIdx.x & 31;  // hw: half of the wave; lane = role
     const int wave = threadIdx.x >> 5;                                   // MB slot in the block (half-wave)
     const int nmb = g.mb_w * g.mb_h;
@@ -1336,11 +1337,22 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
         }
         dqp = qp_delta(m.qp, pred);
     }
+    // the MB's coefficients into LDS first (one 16-byte load per lane and pass): the CAVLC
+    // scans re-read them in data-dependent loops, which from global memory were chains of
+    // dependent L2 round trips
+    if (!skip) {
+        const uint4* src = reinterpret_cast<const uint4*>(mc);
+        uint4* dst = reinterpret_cast<uint4*>(cbuf[wave]);
+        for (int q = lane; q < kCoefStride / 8; q += 32) dst[q] = src[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t bits = 0;
     if (!skip && lane < kNumRoles) {
         BitWriter w;
         w.init(rbuf[wave][lane]);
-        code_role(w, lane, g, fs->idr, mbs, m, mc, mbi, av, mvdx, mvdy, dqp);
+        code_role(w, lane, g, fs->idr, mbs, m, cbuf[wave], mbi, av, mvdx, mvdy, dqp);
         w.flush();
         bits = w.bits;
     }
