@@ -173,9 +173,16 @@ def main() -> None:
     sessions = [N.Session(cfg) for _ in range(K)]
 
     def run(n_frames: int, record: bool):
-        """n_frames per session; K sessions interleaved, up to `depth` frames in flight each."""
+        """n_frames per session, up to `depth` frames in flight each.  K > 1: one native host
+        thread per session (mxdesk runtime run_sessions); K == 1: this thread."""
         out = []
         depth = max(1, args.depth)
+        if K > 1:
+            per = N.run_sessions(sessions, n_frames, depth)
+            if record:
+                for f in range(n_frames):
+                    out.extend(per[k][f] for k in range(K))
+            return out
         sent = [0] * K
         for k, s in enumerate(sessions):
             while sent[k] < min(depth, n_frames):

@@ -490,6 +490,14 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("psnr_y_masked", &FrameResult::psnr_y_masked)
         .def_property_readonly("au", [](const FrameResult& r) { return to_bytes(r.au); });
 
+    m.def(
+        "run_sessions",
+        [](std::vector<Session*> ss, int n_frames, int depth) {
+            py::gil_scoped_release rel;
+            return run_sessions(ss, n_frames, depth);
+        },
+        py::arg("sessions"), py::arg("n_frames"), py::arg("depth") = 2,
+        "K sessions driven concurrently, one host thread each; returns [[FrameResult]] per session");
     py::class_<Session>(m, "Session")
         .def(py::init<const SessionConfig&>())
         .def(

@@ -1531,6 +1531,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const Fra
     const int t = threadIdx.x, r = blockIdx.x, mb_w = g.mb_w, mb_h = g.mb_h;
     const bool idr = fs->idr != 0;
     const int srows = fs->slice_rows, ns = fs->num_slices;
+    // this row's MB bits, loaded up front (independent of the prefix work below)
+    const int base = r * mb_w;
+    uint32_t b[kScanRowPer];
+#pragma unroll
+    for (int k = 0; k < kScanRowPer; ++k) {
+        const int j = t * kScanRowPer + k;
+        b[k] = j < mb_w ? slot_bits[base + j] : 0u;
+    }
+    // frame distortion (row 0): the per-row sums, reduced by the whole workgroup
+    unsigned long long dsum[4] = {0, 0, 0, 0};
+    if (r == 0)
+        for (int j = t; j < mb_h; j += kScanThreads)
+            for (int c = 0; c < 4; ++c) dsum[c] += row_sse[c * kScanMaxRows + j];
     // rows t*2, t*2+1 of the frame per thread (mb_h <= kScanMaxRows)
     uint4 ag[2];
     int lastr = -1;
@@ -1630,13 +1643,22 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const Fra
             mark_quads(dend, s_soff[s] * 8 + s_sbytes[s] * 8 - dend, s_R[er]);
         }
     }
-    if (r == 0 && t < 4) {
-        unsigned long long v = 0;
-        for (int j = 0; j < mb_h; ++j) v += row_sse[t * kScanMaxRows + j];
-        if (t < 3)
-            hdr->sse[t] = v;
-        else
-            hdr->sse_masked = v;
+    if (r == 0) {
+        __shared__ unsigned long long red[4][kScanThreads / 64];
+        for (int c = 0; c < 4; ++c) {
+            unsigned long long v = dsum[c];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if ((t & 63) == 0) red[c][t >> 6] = v;
+        }
+        __syncthreads();
+        if (t < 4) {
+            unsigned long long v = 0;
+            for (int w = 0; w < kScanThreads / 64; ++w) v += red[t][w];
+            if (t < 3)
+                hdr->sse[t] = v;
+            else
+                hdr->sse_masked = v;
+        }
         if (t == 0) {
             const bool over_b = total_bytes > out_bytes;
             hdr->total_bytes = over_b ? 0 : total_bytes;
@@ -1645,15 +1667,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const Fra
         }
     }
     // this row's units
-    const int base = r * mb_w;
     const int sfirst = fr * mb_w;
-    uint32_t b[kScanRowPer];
     int last = -1;
     uint32_t ncod = 0;
 #pragma unroll
     for (int k = 0; k < kScanRowPer; ++k) {
         const int j = t * kScanRowPer + k;
-        b[k] = j < mb_w ? slot_bits[base + j] : 0u;
         if (b[k] == 0xffffffffu) b[k] = 1;
         if (b[k]) {
             last = base + j;

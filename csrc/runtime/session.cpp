@@ -1,5 +1,8 @@
 #include "session.h"
 
+#include <exception>
+#include <thread>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -325,6 +328,44 @@ FrameResult Session::collect() {
         r.psnr_y_masked = psnr(mask_host_[fl.k], ny - mw * mh);
     }
     return r;
+}
+
+std::vector<std::vector<FrameResult>> run_sessions(const std::vector<Session*>& sessions, int n_frames, int depth) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    const size_t k = sessions.size();
+    std::vector<std::vector<FrameResult>> out(k);
+    std::vector<std::exception_ptr> err(k);
+    std::vector<std::thread> th;
+    th.reserve(k);
+    for (size_t i = 0; i < k; ++i) {
+        th.emplace_back([&, i]() {
+            try {
+                HIP_CHECK(hipSetDevice(dev));
+                Session& s = *sessions[i];
+                const int d = std::max(1, std::min(depth, s.depth()));
+                out[i].reserve((size_t)n_frames);
+                int sent = 0;
+                while (sent < std::min(d, n_frames)) {
+                    s.submit_synthetic(false);
+                    ++sent;
+                }
+                for (int f = 0; f < n_frames; ++f) {
+                    out[i].push_back(s.collect());
+                    if (sent < n_frames) {
+                        s.submit_synthetic(false);
+                        ++sent;
+                    }
+                }
+            } catch (...) {
+                err[i] = std::current_exception();
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+    return out;
 }
 
 }  // namespace mx

@@ -78,6 +78,13 @@ struct FrameResult {
     std::vector<uint8_t> au;
 };
 
+class Session;
+// Drives several sessions concurrently, one host thread per session (submit / collect with up
+// to `depth` frames in flight each): the per-frame launch sequence is host work, so one
+// thread interleaving K sessions leaves the GPU waiting on it.  Returns each session's
+// results in frame order.  The calling thread's HIP device is used by every worker.
+std::vector<std::vector<FrameResult>> run_sessions(const std::vector<Session*>& sessions, int n_frames, int depth);
+
 class Session {
    public:
     explicit Session(const SessionConfig& cfg);
