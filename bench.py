@@ -105,6 +105,9 @@ def main() -> None:
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
+    ap.add_argument("--aq", type=int, default=None,
+                    help="adaptive quantisation: 0 off, 1 coarser QP for noise-like MBs, 2 + rate-distortion "
+                         "residual drop for them (default: the encoder's)")
     ap.add_argument("--intra-in-p", type=int, default=None,
                     help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
     ap.add_argument("--depth", type=int, default=2,
@@ -159,6 +162,8 @@ def main() -> None:
         cfg.enc.tu_split = args.tu_split
     if args.intra_in_p is not None:
         cfg.enc.intra_in_p = args.intra_in_p
+    if args.aq is not None:
+        cfg.enc.aq = args.aq
     cfg.noise = args.noise
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth

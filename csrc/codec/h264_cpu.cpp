@@ -313,21 +313,38 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             int16_t* mc = coef_.data() + (size_t)mbi * kCoefStride;
             int cbp = 0;
             uint32_t satd = 0;
+            int zsb[16][16], rrb[16][16], nzb[16];
+            long long d_pred = 0, d_coded = 0;
+            uint32_t bits = 0;
             for (int b = 0; b < 16; ++b) {
                 const int bx = kBlkX[b], by = kBlkY[b];
-                int x[16], zs[16], rr[16];
+                int x[16];
                 for (int i = 0; i < 4; ++i)
                     for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[(by * 4 + i) * 16 + bx * 4 + j];
                 satd += satd4x4(x);
-                const int nz = luma_block_inter(x, qp, zs, rr);
-                for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
+                nzb[b] = luma_block_inter(x, qp, zsb[b], rrb[b]);
+                bits += block_bits_est(nzb[b]);
+                for (int i = 0; i < 16; ++i) {
+                    const int pv = pred[(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)];
+                    const int e = pv + x[i] - clip255(pv + rrb[b][i]);
+                    d_pred += x[i] * x[i];
+                    d_coded += e * e;
+                }
+            }
+            const bool drop = drop_residual(cfg_.aq, lsad, qp, d_pred, d_coded, bits);
+            for (int b = 0; b < 16; ++b) {
+                const int bx = kBlkX[b], by = kBlkY[b];
+                const int nz = drop ? 0 : nzb[b];
+                for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)(drop ? 0 : zsb[b][k]);
                 m.nz_luma[by * 4 + bx] = (uint8_t)nz;
                 if (nz) cbp |= 1 << (b >> 2);
                 for (int i = 0; i < 4; ++i)
                     for (int j = 0; j < 4; ++j)
-                        rec_y[(y0 + by * 4 + i) * cw_ + x0 + bx * 4 + j] =
-                            (uint8_t)clip255(pred[(by * 4 + i) * 16 + bx * 4 + j] + rr[i * 4 + j]);
+                        rec_y[(y0 + by * 4 + i) * cw_ + x0 + bx * 4 + j] = (uint8_t)clip255(
+                            pred[(by * 4 + i) * 16 + bx * 4 + j] + (drop ? 0 : rrb[b][i * 4 + j]));
             }
+            if (drop)  // chroma residual goes with the luma decision
+                for (int i = 256; i < 384; ++i) res[i] = 0;
             bool any_ac = false, any_dc = false;
             for (int comp = 0; comp < 2; ++comp) {
                 int z[4][16], dcin[4];

@@ -33,7 +33,9 @@ struct EncoderConfig {
     int search_range = 16;    // integer-pel full search radius (<= 32)
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
-    int aq = 1;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta)
+    int aq = 2;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta); 2 adds the
+                              // rate-distortion residual drop for them (drop_residual; +0.6-0.9 dB masked
+                              // Y-PSNR at 8 Mbps on the bench desktop, profiles/r02_bench)
     int deblock = 1;          // HEVC in-loop deblocking filter (the H.264 encoder always disables it)
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)

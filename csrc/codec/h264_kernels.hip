@@ -467,7 +467,8 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         }
     }
     __syncthreads();
-    const int qp = aq_mb_qp(fs->qp, (uint32_t)wave_sum(lsad), fs->aq);  // wave-uniform
+    const uint32_t lsad_mb = (uint32_t)wave_sum(lsad);
+    const int qp = aq_mb_qp(fs->qp, lsad_mb, fs->aq);  // wave-uniform
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
 
     int z[16];
@@ -475,14 +476,32 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     int sse_y = 0, sse_c = 0;
     uint32_t satd = 0;
     int16_t* mc = coef + (size_t)(valid ? mbi : 0) * kCoefStride;
+    // luma transform / quant first; outputs wait for the MB-level residual-drop decision
+    int x[16], zs[16], r[16];
+    int d_pred = 0, d_coded = 0;
+    uint32_t bits = 0;
     if (valid && lane < 16) {
         const int b = lane, bx = kBlkX[b], by = kBlkY[b];
-        int x[16];
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[wave][(by * 4 + i) * 16 + bx * 4 + j];
         satd = satd4x4(x);
-        int zs[16], r[16];
         nz = luma_block_inter(x, qp, zs, r);
+        bits = block_bits_est(nz);
+        for (int i = 0; i < 16; ++i) {
+            const int pv = pred[wave][(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)];
+            const int e = pv + x[i] - clip255(pv + r[i]);
+            d_pred += x[i] * x[i];
+            d_coded += e * e;
+        }
+    }
+    const bool drop = drop_residual(fs->aq, lsad_mb, qp, wave_sum(d_pred), wave_sum(d_coded),
+                                    (uint32_t)wave_sum((int)bits));  // wave-uniform
+    if (valid && lane < 16) {
+        const int b = lane, bx = kBlkX[b], by = kBlkY[b];
+        if (drop) {
+            nz = 0;
+            for (int k = 0; k < 16; ++k) zs[k] = r[k] = 0;
+        }
         for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
         mbs[mbi].nz_luma[by * 4 + bx] = (uint8_t)nz;
         const bool vis_x = x0 + bx * 4 < g.width;
@@ -500,9 +519,10 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         }
     } else if (valid && lane < 24) {
         const int comp = (lane - 16) >> 2, cb = (lane - 16) & 3, bx = cb & 1, by = cb >> 1;
-        int x[16], y[16];
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[wave][256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
+        int y[16];
+        for (int i = 0; i < 4; ++i)  // a dropped MB codes no chroma residual either
+            for (int j = 0; j < 4; ++j)
+                x[i * 4 + j] = drop ? 0 : res[wave][256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
         fdct4x4(x, y);
         cdc[wave][comp * 4 + cb] = y[0];
         nz = quant4x4(y, z, qpc, false, 1);

@@ -165,6 +165,26 @@ MXHD int aq_mb_qp(int frame_qp, uint32_t sad, int aq) {
     return q > 51 ? 51 : q;
 }
 
+// Rate-distortion residual drop for noise-like P macroblocks (EncoderConfig::aq >= 2).  A
+// macroblock in an AQ noise class (mean |luma residual| above 32 per pixel) keeps its residual
+// only if coding it lowers the luma distortion by more than lambda * (estimated bits):
+// refining incompressible content at the QPs a CBR budget allows costs far more than it
+// returns, and the rate controller hands those bits to the rest of the picture.  lambda is
+// the H.264 reference mode-decision lambda 0.85 * 2^((qp - 12) / 3) (SSE domain), the bit
+// estimate 2 + 6 per non-zero coefficient per 4x4 block.
+MXHD int lambda_sse(int qp) {
+    constexpr int tab[52] = {0,   0,   0,   0,   0,   0,   0,   0,   0,    0,    1,    1,    1,    1,
+                             1,   2,   2,   3,   3,   4,   5,   7,   9,    11,   14,   17,   22,   27,
+                             34,  43,  54,  69,  86,  109, 137, 173, 218,  274,  345,  435,  548,  691,
+                             870, 1097, 1382, 1741, 2193, 2763, 3482, 4387, 5527, 6963};
+    return tab[qp < 0 ? 0 : (qp > 51 ? 51 : qp)];
+}
+MXHD uint32_t block_bits_est(int nz) { return nz ? 2u + 6u * (uint32_t)nz : 0u; }
+MXHD bool drop_residual(int aq, uint32_t lsad, int qp, long long d_pred, long long d_coded, uint32_t bits) {
+    if (aq < 2 || lsad <= 256u * 32) return false;
+    return d_pred - d_coded < (long long)lambda_sse(qp) * (long long)bits;
+}
+
 // Inter cost of a P16x16 macroblock for the intra decision: luma SATD of the motion-
 // compensated residual + mv rate at the frame lambda.
 MXHD uint32_t inter_cost(uint32_t satd, int frame_qp, int mvx, int mvy) {

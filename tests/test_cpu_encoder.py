@@ -133,6 +133,13 @@ def test_adaptive_quantisation_roundtrip_and_saves_bits(native):
     s_on, rec_on = run(1)
     s_off, _ = run(0)
     assert len(s_on) < 0.9 * len(s_off)
+    # aq=2 adds the rate-distortion residual drop for noise-like MBs: fewer bits again
+    s_drop, rec_drop = run(2)
+    assert len(s_drop) <= len(s_on)
+    dec2 = Decoder()
+    dec2.decode(s_drop)
+    for (y, u, v), (ry, ruv) in zip(dec2.frames_coded, rec_drop):
+        assert np.array_equal(y, ry) and np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
     dec = Decoder()
     dec.decode(s_on)
     for (y, u, v), (ry, ruv) in zip(dec.frames_coded, rec_on):

@@ -145,6 +145,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     cfg.search_range = kw.get("search_range", 8)
     cfg.subpel = kw.get("subpel", 1)
     cfg.intra_in_p = kw.get("intra_in_p", 1)
+    cfg.aq = kw.get("aq", 1)
     genc = gpu.GpuH264Encoder(cfg, _stream())
     cenc = gpu.CpuH264Encoder(cfg)
     gs, cs, grec = b"", b"", []
@@ -174,6 +175,18 @@ def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr, fresh):
     for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
         assert np.array_equal(y, ry)
         assert np.array_equal(u, ruv[:, 0::2])
+
+
+@pytest.mark.parametrize("qp", [30, 44])
+def test_gpu_residual_drop_bit_exact_vs_cpu(gpu, qp):
+    """aq=2: noise-like MBs keep their residual only when it pays at lambda(QP); GPU == CPU
+    bitstream and the decoder reproduces the reconstruction."""
+    stream, grec = _gpu_cpu_encode(gpu, 160, 96, 4, fresh_noise=1, qp=qp, aq=2)
+    dec = Decoder()
+    dec.decode(stream)
+    for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
+        assert np.array_equal(y, ry)
+        assert np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
 
 
 def test_session_stream_decodes_with_barcodes(gpu):
