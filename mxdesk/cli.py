@@ -151,8 +151,11 @@ def main(argv: list[str] | None = None) -> None:
 
         from .utils import devices as D
 
+        from .display.desktop import icd_report
+
         gpus = D.visible_gpus(D.enumerate_gpus())
-        print(json.dumps([asdict(g) | {"xorg_busid": g.xorg_busid} for g in gpus], indent=1))
+        print(json.dumps({"gpus": [asdict(g) | {"xorg_busid": g.xorg_busid} for g in gpus], "icds": icd_report()},
+                         indent=1))
     elif cmd == "xorg-conf":
         from .display.xorg import DisplaySettings, render_xorg_conf
         from .utils import devices as D

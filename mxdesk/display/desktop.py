@@ -91,6 +91,45 @@ def joystick_placeholders(dev_input: str = "/dev/input", n: int = 4) -> list[str
     return made
 
 
+# GL userspace hygiene for the desktop's clients (reference Dockerfile:196 sets NVIDIA's
+# __GL_SYNC_TO_VBLANK=0): Mesa's equivalent is vblank_mode=0 -- a virtual display has no
+# vblank to wait for, and a synced swap would cap every GL client at the dummy refresh.
+GL_ENV = {"vblank_mode": "0", "__GL_SYNC_TO_VBLANK": "0", "KWIN_X11_NO_SYNC_TO_VBLANK": "1"}
+
+
+def desktop_env(env: dict | None = None) -> dict:
+    """Environment for the desktop session: GL_ENV unless already set by the user."""
+    out = dict(os.environ if env is None else env)
+    for k, v in GL_ENV.items():
+        out.setdefault(k, v)
+    return out
+
+
+def icd_report(opencl_dirs=("/etc/OpenCL/vendors",),
+               vulkan_dirs=("/usr/share/vulkan/icd.d", "/etc/vulkan/icd.d")) -> dict:
+    """Registered OpenCL / Vulkan ICDs (reference Dockerfile:170-187 provisions NVIDIA's):
+    {"opencl": [(file, library)], "vulkan": [(file, library_path)]}.  On MI355X the ROCm
+    OpenCL ICD (libamdocl64.so) is the expected OpenCL entry; Vulkan has no CDNA driver, so
+    only software ICDs (lavapipe) can appear."""
+    import json
+
+    rep: dict = {"opencl": [], "vulkan": []}
+    for d in opencl_dirs:
+        for f in sorted(Path(d).glob("*.icd")) if Path(d).is_dir() else []:
+            try:
+                rep["opencl"].append((str(f), f.read_text().strip()))
+            except OSError:
+                continue
+    for d in vulkan_dirs:
+        for f in sorted(Path(d).glob("*.json")) if Path(d).is_dir() else []:
+            try:
+                lib = json.loads(f.read_text()).get("ICD", {}).get("library_path", "")
+            except (OSError, ValueError):
+                continue
+            rep["vulkan"].append((str(f), lib))
+    return rep
+
+
 def desktop_command(env: dict | None = None) -> list[str]:
     env = os.environ if env is None else env
     cmd = env.get("MXDESK_DESKTOP_CMD")
@@ -130,12 +169,16 @@ def run_display_session(cfg, conf_dir: str = "/tmp/mxdesk-x") -> int:
         _terminate(xproc)
         return 1
     os.environ["DISPLAY"] = cfg.display
+    icds = icd_report()
+    log.info("ICDs: OpenCL %s, Vulkan %s", [lib for _, lib in icds["opencl"]] or "none",
+             [lib for _, lib in icds["vulkan"]] or "none")
+    env = desktop_env()
     children = []
-    cmd = desktop_command()
+    cmd = desktop_command(env)
     if cmd:
-        children.append(subprocess.Popen(cmd, start_new_session=True))
+        children.append(subprocess.Popen(cmd, start_new_session=True, env=env))
     if shutil.which("fcitx"):
-        children.append(subprocess.Popen(["fcitx"], start_new_session=True))
+        children.append(subprocess.Popen(["fcitx"], start_new_session=True, env=env))
     print(f"mxdesk: display {cfg.display} ready ({cfg.sizew}x{cfg.sizeh}@{cfg.refresh}, driver {driver})", flush=True)
 
     def _stop(signum, frame):

@@ -54,3 +54,22 @@ def test_session_programs_pin_one_gpu_each():
     assert [p.environment["HIP_VISIBLE_DEVICES"] for p in progs] == ["0", "0", "1", "1", "2", "2", "3", "3"]
     assert [p.environment["SELKIES_PORT"] for p in progs] == [str(9000 + i) for i in range(8)]
     assert all(p.ready.kind == "tcp" and p.command[1:4] == ["-m", "mxdesk", "serve"] for p in progs)
+
+
+def test_desktop_env_gl_hygiene_and_icd_report(tmp_path):
+    from mxdesk.display.desktop import GL_ENV, desktop_env, icd_report
+
+    env = desktop_env({"PATH": "/bin", "vblank_mode": "1"})
+    assert env["vblank_mode"] == "1"  # a user's explicit choice wins
+    assert env["__GL_SYNC_TO_VBLANK"] == "0" and env["PATH"] == "/bin"
+    assert desktop_env({})["vblank_mode"] == GL_ENV["vblank_mode"] == "0"
+    ocl = tmp_path / "ocl"
+    vk = tmp_path / "vk"
+    ocl.mkdir()
+    vk.mkdir()
+    (ocl / "amdocl64.icd").write_text("libamdocl64.so\n")
+    (vk / "lvp_icd.x86_64.json").write_text('{"ICD": {"library_path": "libvulkan_lvp.so"}}')
+    (vk / "broken.json").write_text("{not json")
+    rep = icd_report((str(ocl),), (str(vk), str(tmp_path / "missing")))
+    assert rep["opencl"] == [(str(ocl / "amdocl64.icd"), "libamdocl64.so")]
+    assert rep["vulkan"] == [(str(vk / "lvp_icd.x86_64.json"), "libvulkan_lvp.so")]
