@@ -526,6 +526,18 @@ PYBIND11_MODULE(_native, m) {
                 s.submit_bgrx(p, pitch, force_idr);
             },
             py::arg("frame"), py::arg("force_idr") = false)
+        .def("register_host_buffer",
+             [](Session& s, uintptr_t addr, size_t bytes) { s.register_host_buffer(as_ptr<const void>(addr), bytes); },
+             py::arg("addr"), py::arg("nbytes"))
+        .def(
+            "submit_bgrx_ptr",
+            [](Session& s, uintptr_t addr, int pitch, bool force_idr) {
+                if (pitch < s.config().width * 4) throw std::invalid_argument("pitch < width * 4");
+                py::gil_scoped_release rel;
+                s.submit_bgrx(as_ptr<const uint8_t>(addr), pitch, force_idr);
+            },
+            py::arg("addr"), py::arg("pitch"), py::arg("force_idr") = false,
+            "BGRx frame at a host address (zero-copy when inside a registered buffer)")
         .def("collect",
              [](Session& s) {
                  py::gil_scoped_release rel;

@@ -168,6 +168,8 @@ Session::~Session() {
         if (staging_[k]) (void)hipHostFree(staging_[k]);
     if (lt_mem_) hipFree(lt_mem_);
     if (lt_mf_mem_) hipFree(lt_mf_mem_);
+    for (const auto& r : host_regs_) (void)hipHostUnregister(const_cast<uint8_t*>(r.first));
+    if (ev_upload_) (void)hipEventDestroy(ev_upload_);
     for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
     if (mask_dev_) (void)hipFree(mask_dev_);
     if (mask_counter_) (void)hipFree(mask_counter_);
@@ -283,12 +285,36 @@ void Session::submit_synthetic(bool force_idr) {
     enqueue_mask_sse(k);
 }
 
+void Session::register_host_buffer(const void* p, size_t bytes) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (const auto& r : host_regs_)
+        if (r.first == b && r.second == bytes) return;
+    HIP_CHECK(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault));
+    host_regs_.emplace_back(b, bytes);
+    if (!ev_upload_) HIP_CHECK(hipEventCreateWithFlags(&ev_upload_, hipEventDisableTiming));
+}
+
 void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
     TraceRange tr("mxdesk.submit_bgrx(upload)");
+    const int row = cfg_.width * 4;
+    const size_t span = (size_t)host_pitch * (cfg_.height - 1) + row;
+    for (const auto& r : host_regs_) {
+        if (host_bgrx < r.first || host_bgrx + span > r.first + r.second) continue;
+        // zero-copy: DMA straight from the registered capture buffer
+        const int k = begin_frame();
+        ++frame_id_;
+        const int slot = pool_->acquire();
+        HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+        HIP_CHECK(hipMemcpy2DAsync(pool_->data(slot), pool_->pitch(), host_bgrx, host_pitch, row, cfg_.height,
+                                   hipMemcpyHostToDevice, stream_));
+        HIP_CHECK(hipEventRecord(ev_upload_, stream_));
+        convert_and_encode(slot, force_idr);
+        HIP_CHECK(hipEventSynchronize(ev_upload_));  // the caller may overwrite the buffer now
+        return;
+    }
     const int k = begin_frame();
     ++frame_id_;
     const int slot = pool_->acquire();
-    const int row = cfg_.width * 4;
     for (int r = 0; r < cfg_.height; ++r)
         std::memcpy(staging_[k] + (size_t)r * pool_->pitch(), host_bgrx + (size_t)r * host_pitch, row);
     HIP_CHECK(hipEventRecord(ev_start_[k], stream_));

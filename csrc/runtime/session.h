@@ -98,6 +98,10 @@ class Session {
     int depth() const { return depth_; }
     // Externally captured BGRx frame (host memory, e.g. X11 SHM) -> upload -> encode.
     void submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr = false);
+    // Page-locks a host buffer the capture writes frames into (e.g. the XShm segment):
+    // submit_bgrx from inside it is a direct 2D DMA, with no copy into the staging buffer, and
+    // returns once the DMA has read the frame (the buffer may then be overwritten).
+    void register_host_buffer(const void* p, size_t bytes);
     FrameResult collect();
     FrameResult step(bool force_idr = false) {
         submit_synthetic(force_idr);
@@ -140,6 +144,8 @@ class Session {
     pix::LanczosTables lt_{};
     void* lt_mem_ = nullptr;
     void* lt_mf_mem_ = nullptr;  // MFMA scaler fragment tables
+    std::vector<std::pair<const uint8_t*, size_t>> host_regs_;  // register_host_buffer ranges
+    hipEvent_t ev_upload_ = nullptr;
     // frames in flight (pipeline depth 1 or 2): per-frame start event / staging buffer
     struct Inflight {
         uint32_t frame_id;

@@ -170,6 +170,23 @@ class X11Capture:
         self.x11.XFree(ci)
         return out
 
+    def shm_buffer(self) -> tuple[int, int] | None:
+        """(address, size) of the MIT-SHM segment frames land in, or None (XGetImage path)."""
+        if self.shm is None:
+            return None
+        info, _, size = self.shm
+        return int(info.shmaddr), int(size)
+
+    def grab_shm(self) -> tuple[int, int] | None:
+        """Capture into the SHM segment without touching the pixels on the CPU: returns
+        (address, row pitch in bytes) for Session.submit_bgrx_ptr, or None without SHM."""
+        if self.shm is None:
+            return None
+        info, img, _ = self.shm
+        if not self.xext.XShmGetImage(self.dpy, self.root, img, 0, 0, AllPlanes):
+            raise OSError("XShmGetImage failed")
+        return int(info.shmaddr), int(self.pitch)
+
     def grab(self) -> np.ndarray:
         """One frame as an (H, W, 4) uint8 BGRx array."""
         if self.shm is not None:

@@ -104,23 +104,37 @@ class TileRenderer:
         return self.out
 
 
+def host_staged(device: torch.device) -> bool:
+    """GPU tiles over a gloo process group (no RCCL, e.g. several ranks sharing one GPU): the
+    exchange and the control broadcast go through host tensors."""
+    return device.type == "cuda" and dist.is_initialized() and dist.get_backend() == "gloo"
+
+
 class TileExchange:
     def __init__(self, geo: WallGeometry, rank: int, world: int, device: torch.device, mode: str = "gather",
                  root: int = 0):
         if world != geo.cols * geo.rows:
             raise ValueError(f"wall {geo.cols}x{geo.rows} needs {geo.cols * geo.rows} ranks, got {world}")
         self.geo, self.rank, self.world, self.mode, self.root = geo, rank, world, mode, root
-        self.tiles = torch.empty(world * geo.tile_bytes, dtype=torch.uint8, device=device) \
-            if (rank == root or mode == "allgather") else None
+        holds = rank == root or mode == "allgather"
+        self.tiles = torch.empty(world * geo.tile_bytes, dtype=torch.uint8, device=device) if holds else None
+        self.staged = host_staged(device)
+        if self.staged:
+            self._tile_h = torch.empty(geo.tile_bytes, dtype=torch.uint8).pin_memory()
+            self._tiles_h = torch.empty(world * geo.tile_bytes, dtype=torch.uint8).pin_memory() if holds else None
 
     def post(self, tile: torch.Tensor) -> list:
         """Start the exchange of this rank's tile; returns the requests to wait for."""
+        tiles = self.tiles
+        if self.staged:
+            self._tile_h.copy_(tile)  # synchronous: the send reads host memory
+            tile, tiles = self._tile_h, self._tiles_h
         if self.mode == "allgather":
-            return [dist.all_gather_into_tensor(self.tiles, tile, async_op=True)]
+            return [dist.all_gather_into_tensor(tiles, tile, async_op=True)]
         tb = self.geo.tile_bytes
         if self.rank == self.root:
-            self.tiles[self.root * tb:(self.root + 1) * tb].copy_(tile)
-            ops = [dist.P2POp(dist.irecv, self.tiles[r * tb:(r + 1) * tb], r) for r in range(self.world)
+            tiles[self.root * tb:(self.root + 1) * tb].copy_(tile)
+            ops = [dist.P2POp(dist.irecv, tiles[r * tb:(r + 1) * tb], r) for r in range(self.world)
                    if r != self.root]
         else:
             ops = [dist.P2POp(dist.isend, tile, self.root)]
@@ -129,6 +143,8 @@ class TileExchange:
     def wait(self, reqs: list) -> torch.Tensor | None:
         for req in reqs:
             req.wait()
+        if self.tiles is not None and self.staged:
+            self.tiles.copy_(self._tiles_h, non_blocking=True)
         return self.tiles if self.rank == self.root else None
 
     def exchange(self, tile: torch.Tensor) -> torch.Tensor | None:
@@ -160,8 +176,10 @@ class WallPipeline(StreamPipeline):
         self.geo, self.rank, self.world, self.dev = geo, rank, world, device
         self.renderer = TileRenderer(geo, rank, device)
         self.xchg = TileExchange(geo, rank, world, device, exchange)
-        self.ctrl = torch.zeros(4, dtype=torch.int64, device=device)
-        self._ctrl_host = torch.zeros(4, dtype=torch.int64).pin_memory() if device.type == "cuda" else self.ctrl
+        staged = host_staged(device)
+        self.ctrl = torch.zeros(4, dtype=torch.int64, device="cpu" if staged else device)
+        self._ctrl_host = torch.zeros(4, dtype=torch.int64).pin_memory() \
+            if (device.type == "cuda" and not staged) else self.ctrl
         self._t0 = time.monotonic()
         self._fid = 0
         self._pending = None  # (frame id, capture us, exchange requests) of the posted frame
@@ -310,7 +328,7 @@ def follower_loop(geo: WallGeometry, rank: int, world: int, device: torch.device
     the control tensor once per frame: the follower has nothing to overlap with)."""
     renderer = TileRenderer(geo, rank, device)
     xchg = TileExchange(geo, rank, world, device, exchange)
-    ctrl = torch.zeros(4, dtype=torch.int64, device=device)
+    ctrl = torch.zeros(4, dtype=torch.int64, device="cpu" if host_staged(device) else device)
     n = 0
     while True:
         dist.broadcast(ctrl, 0)

@@ -187,8 +187,17 @@ class StreamPipeline:
             s = self._sess
             s.set_cursor(*self._cursor)
             if self.capture is not None:
-                img = self.capture.grab()
-                s.submit_bgrx(img, force_idr)
+                # zero-copy when the capture lands in a registered MIT-SHM segment: the GPU DMAs
+                # the frame straight out of it (no CPU copy into the staging buffer)
+                shm = getattr(self.capture, "shm_buffer", lambda: None)()
+                if shm is not None:
+                    if getattr(self, "_shm_reg", None) != shm:
+                        s.register_host_buffer(*shm)
+                        self._shm_reg = shm
+                    addr, pitch = self.capture.grab_shm()
+                    s.submit_bgrx_ptr(addr, pitch, force_idr)
+                else:
+                    s.submit_bgrx(self.capture.grab(), force_idr)
                 r = s.collect()
             else:
                 r = s.step(force_idr)

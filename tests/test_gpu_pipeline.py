@@ -381,3 +381,30 @@ def test_synth_static_cache_matches_full_render(gpu):
                       static_bg=bg.data_ptr())
             torch.cuda.synchronize()
             assert torch.equal(a, b), (w, h, t)
+
+
+def test_zero_copy_registered_capture_matches_staged_upload(gpu):
+    """A frame inside a registered (page-locked) host buffer -- the XShm segment in production --
+    is DMA'd straight to the GPU; the access units equal the staged-copy path's."""
+    w, h, pitch = 320, 192, 320 * 4 + 256  # padded rows like an XImage
+    rng = np.random.default_rng(3)
+    frames = [rng.integers(0, 256, (h, pitch), dtype=np.uint8) for _ in range(3)]
+
+    def session():
+        cfg = gpu.SessionConfig()
+        cfg.width, cfg.height, cfg.fps = w, h, 60
+        cfg.enc.bitrate_kbps = 0
+        cfg.enc.qp = 26
+        return gpu.Session(cfg)
+
+    staged, zc = session(), session()
+    buf = np.zeros((h, pitch), np.uint8)  # the "capture segment", registered once
+    zc.register_host_buffer(buf.ctypes.data, buf.nbytes)
+    for f in frames:
+        staged.submit_bgrx(np.ascontiguousarray(f[:, : w * 4]).reshape(h, w, 4), False)
+        a = staged.collect().au
+        buf[:] = f
+        zc.submit_bgrx_ptr(buf.ctypes.data, pitch, False)
+        buf[:] = 0  # the DMA has read the frame when submit returns
+        b = zc.collect().au
+        assert a == b

@@ -219,3 +219,65 @@ def test_gpu_telemetry_sysfs(gpu):
     t = D.gpu_telemetry(vis[0].pci_bdf)
     print("telemetry", vis[0].pci_bdf, t)
     assert "vram_total_bytes" in t or "busy_percent" in t
+
+
+def _gpu_wall_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from mxdesk.parallel.wall import WallGeometry, WallPipeline, follower_loop
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    geo = WallGeometry(2, 1, 160, 96)
+    try:
+        if rank != 0:
+            follower_loop(geo, rank, world, dev, "gather", fps=60)
+            return
+        pipe = WallPipeline(geo, 60, 0, world, dev, "gather", bitrate_kbps=0)
+        stream = b"".join(pipe.step().au for _ in range(3))
+        torch.cuda.synchronize()
+        wall_y = pipe.wy.cpu().numpy()[: geo.height, : geo.width].copy()
+        pipe.lockstep_frame(False, stop=True)
+        q.put((stream, wall_y))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_wall_two_processes_one_gpu():
+    """Two wall ranks as two processes on the one GPU (gloo, host-staged tile exchange): the
+    HIP render / composite / encode path of a multi-rank wall, decoded and compared with one
+    render of the full wall."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_wall_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        stream, wall_y = q.get(timeout=150)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    frames = Decoder().decode(stream)
+    assert len(frames) == 3 and frames[0][0].shape == (96, 320)
+    assert read_barcode(frames[2][0])[0] == 2
+    # the composite equals one render of the full wall (frame 2; barcode timestamp row aside)
+    from mxdesk import native
+
+    N = native()
+    w, h = 320, 96
+    a = torch.zeros((h, w * 4), dtype=torch.uint8, device="cuda")
+    N.synth(a.data_ptr(), w, h, w * 4, frame_id=2, t=2 / 60, stream=torch.cuda.current_stream().cuda_stream)
+    y = torch.zeros((h, w), dtype=torch.uint8, device="cuda")
+    uv = torch.zeros((h // 2, w), dtype=torch.uint8, device="cuda")
+    N.bgrx_to_nv12(a.data_ptr(), w * 4, w, h, y.data_ptr(), uv.data_ptr(), w, w, h,
+                   torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = y.cpu().numpy()
+    mask = np.ones_like(ref, bool)
+    mask[8 + 8: 8 + 16, :] = False  # timestamp cells (capture time)
+    assert np.array_equal(wall_y[mask], ref[mask])
