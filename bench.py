@@ -104,6 +104,8 @@ def main() -> None:
                     help="HEVC: let inter CUs split their transform tree into 8x8 / 4x4 TUs (default: encoder default)")
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
+    ap.add_argument("--me-coarse", type=int, default=None,
+                    help="1: even-offset grid + integer neighbours, 0: exhaustive search (encoder default)")
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
     ap.add_argument("--aq", type=int, default=None,
                     help="adaptive quantisation: 0 off, 1 coarser QP for noise-like MBs, 2 + rate-distortion "
@@ -164,6 +166,8 @@ def main() -> None:
         cfg.enc.intra_in_p = args.intra_in_p
     if args.aq is not None:
         cfg.enc.aq = args.aq
+    if args.me_coarse is not None:
+        cfg.enc.me_coarse = args.me_coarse
     cfg.noise = args.noise
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth

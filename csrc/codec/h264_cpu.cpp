@@ -37,7 +37,7 @@ void pad_nv12(const uint8_t* y, const uint8_t* uv, int w, int h, int pitch, int 
 // rules as k_me_full (static-block exit, cost = SAD + lambda * mv bits, tie -> shorter vector
 // then lower candidate index).  Shared by the CPU H.264 and HEVC encoders.
 void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, int ch_, int x0, int y0,
-                   int frame_qp, int search_range, int subpel, int* out_mvx, int* out_mvy) {
+                   int frame_qp, int search_range, int subpel, int* out_mvx, int* out_mvy, int coarse) {
     const int lambda = lambda_sad(frame_qp);
     const int R = me_range(search_range);
     const int side = 2 * R + 1;
@@ -48,7 +48,7 @@ void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, 
             sad0 += std::abs((int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + k, y0 + r));
     const bool is_static = sad0 <= static_sad(frame_qp);
     unsigned long long best = ~0ull;
-    for (int c = 0; c < (is_static ? 0 : side * side); ++c) {
+    auto key_of = [&](int c) {
         const int dy = c / side - R, dx = c % side - R;
         uint32_t sad = 0;
         for (int r = 0; r < 16; ++r)
@@ -57,9 +57,22 @@ void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, 
                                 ref_px(ref_y, cw_, cw_, ch_, x0 + dx + k, y0 + dy + r));
         const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
         const uint32_t dist = (uint32_t)(std::abs(dx) + std::abs(dy));
-        const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
-        best = std::min(best, key);
+        return ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
+    };
+    if (!is_static && coarse) {  // even-offset grid, then the 8 integer neighbours of its best
+        for (int dyr = 0; dyr < side; dyr += 2)
+            for (int dxr = 0; dxr < side; dxr += 2) best = std::min(best, key_of(dyr * side + dxr));
+        const int cb0 = (int)(best & 0xffff), bxr = cb0 % side, byr = cb0 / side;
+        unsigned long long nb = best;
+        for (int k = 0; k < 8; ++k) {
+            int ddx, ddy;
+            subpel_offset(k, &ddx, &ddy);
+            const int nxr = bxr + ddx, nyr = byr + ddy;
+            if (nxr >= 0 && nxr < side && nyr >= 0 && nyr < side) nb = std::min(nb, key_of(nyr * side + nxr));
+        }
+        best = nb;
     }
+    for (int c = 0; c < (is_static || coarse ? 0 : side * side); ++c) best = std::min(best, key_of(c));
     const int cb = (int)(best & 0xffff);
     int mvx = is_static ? 0 : 4 * ((cb % side) - R), mvy = is_static ? 0 : 4 * ((cb / side) - R);
     if (subpel && !is_static) {
@@ -285,7 +298,8 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             MbInfo& m = mb_[mbi];
             std::memset(&m, 0, sizeof m);
             int mvx = 0, mvy = 0;
-            me_search_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &mvx, &mvy);
+            me_search_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &mvx, &mvy,
+                          cfg_.me_coarse);
             m.mvx = (int16_t)mvx;
             m.mvy = (int16_t)mvy;
             m.type = kMbP16x16;

@@ -31,6 +31,9 @@ struct EncoderConfig {
     int qp_max = 46;
     int keyint = 0;           // IDR period in frames, 0 = only on demand (infinite GOP)
     int search_range = 16;    // integer-pel full search radius (<= 32)
+    int me_coarse = 0;        // 1: ME over the even-offset grid + the 8 integer neighbours of its best (4x
+                              // fewer SADs: +5.7 % fps, -0.4 dB masked Y-PSNR at 8 Mbps, profiles/r02_me);
+                              // 0: exhaustive +-range search
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
     int aq = 2;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta); 2 adds the
@@ -261,7 +264,7 @@ class CpuH264Encoder {
 // CPU motion search of one 16x16 block (same rules as the GPU k_me_full); shared by the
 // CPU H.264 and HEVC encoders.
 void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw, int ch, int x0, int y0, int qp,
-                   int search_range, int subpel, int* mvx, int* mvy);
+                   int search_range, int subpel, int* mvx, int* mvy, int coarse);
 
 // Pad a display-sized NV12 frame to the coded size by edge replication (what the CSC
 // kernel does on the GPU side).  Returns pitch = coded width.

@@ -287,7 +287,8 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
 
     // static-block early exit first: SAD of the zero vector from one source and one reference
     // pixel per thread (same rule as the CPU encoder), so the ~70 % static MBs of a desktop
-    // never load the search window
+    // never load the search window (a separate static pre-pass kernel feeding a list of the
+    // moving MBs was measured slower: its atomic list append serialises, profiles/r02_me)
     constexpr int kWs4 = kWinStride / 4;
     {
         const int r = tid >> 4, c = tid & 15;  // 256 threads = 16 rows x 16 px
@@ -321,7 +322,40 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     // (instead of 5 per candidate), 12 v_alignbyte and 16 v_sad_u8.
     const int side = 2 * R + 1, gw = (side + 3) >> 2, ngroups = side * gw;
     unsigned long long best = ~0ull;
-    for (int q = tid; q < ngroups; q += 256) {
+    const bool coarse = fs->me_coarse != 0;
+    // coarse mode (me_coarse): the even-offset grid first -- two candidates per thread (window
+    // shifts 0 and 2 of a dword group), (R + 1) * gw tasks in one pass -- then the 8 integer
+    // neighbours of its best (me_search_cpu does the same)
+    const int ntask = coarse ? (R + 1) * gw : 0;
+    for (int q = tid; q < ntask; q += 256) {
+        const int dyr = 2 * (q / gw), g = q % gw;
+        uint32_t s0a = 0, s2a = 0;
+#pragma unroll 4
+        for (int r = 0; r < 16; ++r) {
+            const int a = (dyr + r) * kWs4 + g;
+            const uint32_t w0 = win32[a], w1 = win32[a + 1], w2 = win32[a + 2], w3 = win32[a + 3], w4 = win32[a + 4];
+            const uint32_t s0 = srcw[r * 4 + 0], s1 = srcw[r * 4 + 1], s2 = srcw[r * 4 + 2], s3 = srcw[r * 4 + 3];
+            s0a = __builtin_amdgcn_sad_u8(w0, s0, s0a);
+            s0a = __builtin_amdgcn_sad_u8(w1, s1, s0a);
+            s0a = __builtin_amdgcn_sad_u8(w2, s2, s0a);
+            s0a = __builtin_amdgcn_sad_u8(w3, s3, s0a);
+            s2a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 2), s0, s2a);
+            s2a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w2, w1, 2), s1, s2a);
+            s2a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w3, w2, 2), s2, s2a);
+            s2a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w4, w3, 2), s3, s2a);
+        }
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int dxr = 4 * g + 2 * h2;
+            if (dxr >= side) break;
+            const int dx = dxr - R, dy = dyr - R, c = dyr * side + dxr;
+            const uint32_t cost = me_cost(h2 ? s2a : s0a, lambda, 4 * dx, 4 * dy);
+            const uint32_t dist = (uint32_t)(abs(dx) + abs(dy));
+            const unsigned long long key = ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
+            best = key < best ? key : best;
+        }
+    }
+    for (int q = tid; q < (coarse ? 0 : ngroups); q += 256) {
         const int dyr = q / gw, g = q - dyr * gw;
         uint32_t sad[4] = {0, 0, 0, 0};
 #pragma unroll 2
@@ -362,6 +396,31 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     __syncthreads();
     unsigned long long b = red[0];
     for (int i = 1; i < 4; ++i) b = red[i] < b ? red[i] : b;
+    if (coarse) {  // the 8 integer neighbours of the grid best: one per 32-lane group
+        __shared__ unsigned long long nkey[8];
+        const int cb0 = (int)(b & 0xffff), bxr = cb0 % side, byr = cb0 / side;
+        const int k = tid >> 5, sub = tid & 31, py = sub >> 1, px0 = (sub & 1) * 8;
+        int ddx, ddy;
+        subpel_offset(k, &ddx, &ddy);
+        const int nxr = bxr + ddx, nyr = byr + ddy;
+        const bool inside = nxr >= 0 && nxr < side && nyr >= 0 && nyr < side;  // uniform per group
+        int d = 0;
+        if (inside) {
+            const uint8_t* wrow = reinterpret_cast<const uint8_t*>(win32) + (nyr + py) * kWinStride + nxr + px0;
+            const uint32_t s0 = srcw[py * 4 + (px0 >> 2)], s1 = srcw[py * 4 + (px0 >> 2) + 1];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d += abs((int)(((j < 4 ? s0 : s1) >> (8 * (j & 3))) & 0xff) - (int)wrow[j]);
+        }
+        for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (sub == 0) {
+            const int dx = nxr - R, dy = nyr - R;
+            const uint32_t cost = me_cost((uint32_t)d, lambda, 4 * dx, 4 * dy);
+            const uint32_t dist = (uint32_t)(abs(dx) + abs(dy));
+            nkey[k] = inside ? (((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)(nyr * side + nxr)) : ~0ull;
+        }
+        __syncthreads();
+        for (int i = 0; i < 8; ++i) b = nkey[i] < b ? nkey[i] : b;
+    }
     const int cbest = (int)(b & 0xffff);
     int mvx = 4 * ((cbest % side) - R), mvy = 4 * ((cbest / side) - R);
 

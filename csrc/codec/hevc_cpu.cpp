@@ -391,7 +391,7 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
             const int i = y * W + x;
             int mvx = 0, mvy = 0;
             h264::me_search_cpu(sy, pitch, ref_y, cw_, ch_, x * 16, y * 16, fqp, cfg_.search_range, cfg_.subpel, &mvx,
-                                &mvy);
+                                &mvy, cfg_.me_coarse);
             mv_[2 * i] = (int16_t)mvx;
             mv_[2 * i + 1] = (int16_t)mvy;
         }

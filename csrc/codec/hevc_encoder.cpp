@@ -128,6 +128,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     m.ref_uv = rec_uv_[ref];
     m.qp = qp;
     m.search_range = h264::me_range(cfg_.search_range);
+    m.me_coarse = cfg_.me_coarse;
     m.subpel = cfg_.subpel;
     m.hp_pitch = hp_pitch_;
     m.hp_f = hp_[0] + org;

@@ -146,6 +146,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     cfg.subpel = kw.get("subpel", 1)
     cfg.intra_in_p = kw.get("intra_in_p", 1)
     cfg.aq = kw.get("aq", 1)
+    cfg.me_coarse = kw.get("me_coarse", 1)
     genc = gpu.GpuH264Encoder(cfg, _stream())
     cenc = gpu.CpuH264Encoder(cfg)
     gs, cs, grec = b"", b"", []
@@ -175,6 +176,17 @@ def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr, fresh):
     for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
         assert np.array_equal(y, ry)
         assert np.array_equal(u, ruv[:, 0::2])
+
+
+@pytest.mark.parametrize("me_coarse,sr", [(0, 16), (1, 16), (1, 32)])
+def test_gpu_me_modes_bit_exact_vs_cpu(gpu, me_coarse, sr):
+    """Exhaustive and coarse-grid (even offsets + integer neighbours) motion search: GPU ==
+    CPU oracle, decodes to the reconstruction."""
+    stream, grec = _gpu_cpu_encode(gpu, 160, 96, 4, search_range=sr, fresh_noise=0, qp=26, me_coarse=me_coarse)
+    dec = Decoder()
+    dec.decode(stream)
+    for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
+        assert np.array_equal(y, ry)
 
 
 @pytest.mark.parametrize("qp", [30, 44])
