@@ -481,20 +481,29 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
 }
 
 // ------------------------------------------------------------------ inter encode
+// Two MBs per wave, one per 32-lane half: lanes 0..15 of a half code the 16 luma 4x4 blocks,
+// 16..23 the 8 chroma blocks (a whole wave per MB left 40 of 64 lanes idle in the transform
+// phase, which dominates).  8 MBs per workgroup; the distortion partials stay one per 4 MBs.
+__device__ __forceinline__ int half_sum(int v) {
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameState* __restrict__ fs,
                                                        const uint8_t* __restrict__ src_y,
                                                        const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
                                                        int16_t* __restrict__ coef, uint32_t* __restrict__ mb_sse,
                                                        int* __restrict__ wave_prog) {
-    __shared__ uint8_t pred[4][384];
-    __shared__ int16_t res[4][384];
-    __shared__ int cdc[4][8];
-    __shared__ int cdc_nz[4][2];
+    __shared__ uint8_t pred[8][384];
+    __shared__ int16_t res[8][384];
+    __shared__ int cdc[8][8];
+    __shared__ int cdc_nz[8][2];
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, hf = lane >> 5, hl = lane & 31;
+    const int ms = (threadIdx.x >> 6) * 2 + hf;  // MB slot in the workgroup
     const int nmb = g.mb_w * g.mb_h;
     const int bid = blockIdx.x;
-    const int mbi = bid * 4 + wave;
+    const int mbi = bid * 8 + ms;
     if (bid == 0 && threadIdx.x == 0) wave_prog[1] = 0;  // k_intra_analyze's candidate list (next kernel)
     const bool valid = mbi < nmb;
     const int mbx = valid ? mbi % g.mb_w : 0, mby = valid ? mbi / g.mb_w : 0;
@@ -507,27 +516,32 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     if (valid) {
         mvx = mbs[mbi].mvx;
         mvy = mbs[mbi].mvy;
-        const int r = lane >> 2, c0 = (lane & 3) * 4;
-        const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
-        for (int k = 0; k < 4; ++k) {
+        const int r = hl >> 1, c0 = (hl & 1) * 8;  // 8 luma samples per lane
+        const uint2 sw = *reinterpret_cast<const uint2*>(src_y + (y0 + r) * g.pitch + x0 + c0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
             const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
-            const int d = (int)((sw >> (8 * k)) & 0xff) - p;
-            pred[wave][r * 16 + c0 + k] = (uint8_t)p;
-            res[wave][r * 16 + c0 + k] = (int16_t)d;
+            const int d = (int)(((k < 4 ? sw.x : sw.y) >> (8 * (k & 3))) & 0xff) - p;
+            pred[ms][r * 16 + c0 + k] = (uint8_t)p;
+            res[ms][r * 16 + c0 + k] = (int16_t)d;
             lsad += d < 0 ? -d : d;
         }
-        const int cr_ = lane >> 3, cc = lane & 7;
-        const int xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
-        for (int comp = 0; comp < 2; ++comp) {
-            const int p = chroma_pred8(ref_uv, g.pitch, cw, ch, comp, xc * 8 + mvx, yc * 8 + mvy);
-            const int s = src_uv[yc * g.pitch + 2 * xc + comp];
-            pred[wave][256 + comp * 64 + cr_ * 8 + cc] = (uint8_t)p;
-            res[wave][256 + comp * 64 + cr_ * 8 + cc] = (int16_t)(s - p);
+        const int cr_ = hl >> 2, cc0 = (hl & 3) * 2;  // 2 chroma positions x 2 planes per lane
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int cc = cc0 + e, xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
+#pragma unroll
+            for (int comp = 0; comp < 2; ++comp) {
+                const int p = chroma_pred8(ref_uv, g.pitch, cw, ch, comp, xc * 8 + mvx, yc * 8 + mvy);
+                const int sv = src_uv[yc * g.pitch + 2 * xc + comp];
+                pred[ms][256 + comp * 64 + cr_ * 8 + cc] = (uint8_t)p;
+                res[ms][256 + comp * 64 + cr_ * 8 + cc] = (int16_t)(sv - p);
+            }
         }
     }
     __syncthreads();
-    const uint32_t lsad_mb = (uint32_t)wave_sum(lsad);
-    const int qp = aq_mb_qp(fs->qp, lsad_mb, fs->aq);  // wave-uniform
+    const uint32_t lsad_mb = (uint32_t)half_sum(lsad);
+    const int qp = aq_mb_qp(fs->qp, lsad_mb, fs->aq);  // uniform over the half
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
 
     int z[16];
@@ -539,24 +553,24 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     int x[16], zs[16], r[16];
     int d_pred = 0, d_coded = 0;
     uint32_t bits = 0;
-    if (valid && lane < 16) {
-        const int b = lane, bx = kBlkX[b], by = kBlkY[b];
+    if (valid && hl < 16) {
+        const int b = hl, bx = kBlkX[b], by = kBlkY[b];
         for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[wave][(by * 4 + i) * 16 + bx * 4 + j];
+            for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[ms][(by * 4 + i) * 16 + bx * 4 + j];
         satd = satd4x4(x);
         nz = luma_block_inter(x, qp, zs, r);
         bits = block_bits_est(nz);
         for (int i = 0; i < 16; ++i) {
-            const int pv = pred[wave][(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)];
+            const int pv = pred[ms][(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)];
             const int e = pv + x[i] - clip255(pv + r[i]);
             d_pred += x[i] * x[i];
             d_coded += e * e;
         }
     }
-    const bool drop = drop_residual(fs->aq, lsad_mb, qp, wave_sum(d_pred), wave_sum(d_coded),
-                                    (uint32_t)wave_sum((int)bits));  // wave-uniform
-    if (valid && lane < 16) {
-        const int b = lane, bx = kBlkX[b], by = kBlkY[b];
+    const bool drop = drop_residual(fs->aq, lsad_mb, qp, half_sum(d_pred), half_sum(d_coded),
+                                    (uint32_t)half_sum((int)bits));  // uniform over the half
+    if (valid && hl < 16) {
+        const int b = hl, bx = kBlkX[b], by = kBlkY[b];
         if (drop) {
             nz = 0;
             for (int k = 0; k < 16; ++k) zs[k] = r[k] = 0;
@@ -568,7 +582,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
             uint32_t packed = 0;
             const bool vis = vis_x && (y0 + by * 4 + i) < g.height;
             for (int j = 0; j < 4; ++j) {
-                const int pv = pred[wave][(by * 4 + i) * 16 + bx * 4 + j];
+                const int pv = pred[ms][(by * 4 + i) * 16 + bx * 4 + j];
                 const int v = clip255(pv + r[i * 4 + j]);
                 const int e = pv + x[i * 4 + j] - v;
                 sse_y += vis ? e * e : 0;
@@ -576,75 +590,78 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
             }
             *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + by * 4 + i) * g.pitch + x0 + bx * 4) = packed;
         }
-    } else if (valid && lane < 24) {
-        const int comp = (lane - 16) >> 2, cb = (lane - 16) & 3, bx = cb & 1, by = cb >> 1;
+    } else if (valid && hl < 24) {
+        const int comp = (hl - 16) >> 2, cb = (hl - 16) & 3, bx = cb & 1, by = cb >> 1;
         int y[16];
         for (int i = 0; i < 4; ++i)  // a dropped MB codes no chroma residual either
             for (int j = 0; j < 4; ++j)
-                x[i * 4 + j] = drop ? 0 : res[wave][256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
+                x[i * 4 + j] = drop ? 0 : res[ms][256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
         fdct4x4(x, y);
-        cdc[wave][comp * 4 + cb] = y[0];
+        cdc[ms][comp * 4 + cb] = y[0];
         nz = quant4x4(y, z, qpc, false, 1);
         for (int k = 1; k < 16; ++k) mc[kCoefChromaAc + (comp * 4 + cb) * 16 + k] = (int16_t)z[kZigzag4x4[k]];
         (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
     }
     __syncthreads();
-    if (valid && (lane == 16 || lane == 20)) {
-        const int comp = (lane - 16) >> 2;
+    if (valid && (hl == 16 || hl == 20)) {
+        const int comp = (hl - 16) >> 2;
         int in[4], zd[4], dq[4];
-        for (int i = 0; i < 4; ++i) in[i] = cdc[wave][comp * 4 + i];
+        for (int i = 0; i < 4; ++i) in[i] = cdc[ms][comp * 4 + i];
         const int n = quant_dc_chroma(in, zd, qpc, false);
         for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zd[i];
         dequant_dc_chroma(zd, dq, qpc);
-        for (int i = 0; i < 4; ++i) cdc[wave][comp * 4 + i] = dq[i];
-        cdc_nz[wave][comp] = n;
+        for (int i = 0; i < 4; ++i) cdc[ms][comp * 4 + i] = dq[i];
+        cdc_nz[ms][comp] = n;
     }
     __syncthreads();
-    if (valid && lane >= 16 && lane < 24) {
-        const int comp = (lane - 16) >> 2, cb = (lane - 16) & 3, bx = cb & 1, by = cb >> 1;
-        int d[16], r[16];
+    if (valid && hl >= 16 && hl < 24) {
+        const int comp = (hl - 16) >> 2, cb = (hl - 16) & 3, bx = cb & 1, by = cb >> 1;
+        int d[16], rr[16];
         dequant4x4(z, d, qpc, 1);
-        d[0] = cdc[wave][comp * 4 + cb];
-        idct4x4(d, r);
+        d[0] = cdc[ms][comp * 4 + cb];
+        idct4x4(d, rr);
         const int xc = x0 / 2 + bx * 4, yc = y0 / 2 + by * 4;
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) {
                 const int o = 256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j;
-                const int v = clip255(pred[wave][o] + r[i * 4 + j]);
-                const int e = pred[wave][o] + res[wave][o] - v;
+                const int v = clip255(pred[ms][o] + rr[i * 4 + j]);
+                const int e = pred[ms][o] + res[ms][o] - v;
                 sse_c += (2 * (xc + j) < g.width && 2 * (yc + i) < g.height) ? e * e : 0;
                 fs->rec_uv[(yc + i) * g.pitch + 2 * (xc + j) + comp] = (uint8_t)v;
             }
     }
-    const uint32_t satd_mb = (uint32_t)wave_sum((int)satd);
+    const uint32_t satd_mb = (uint32_t)half_sum((int)satd);
     {
-        // Y on lanes 0..15, U on 16..19, V on 20..23
-        const int sy = wave_sum(sse_y);
-        const int su = wave_sum((lane >= 16 && lane < 20) ? sse_c : 0);
-        const int sv = wave_sum((lane >= 20 && lane < 24) ? sse_c : 0);
-        if (valid && fs->intra_in_p && lane < 3)  // per-MB copy: replaced if the MB switches to intra
-            mb_sse[lane * nmb + mbi] = (uint32_t)(lane == 0 ? sy : (lane == 1 ? su : sv));
-        __shared__ uint32_t part[4][4];
-        if (lane == 0) {
-            part[0][wave] = valid ? (uint32_t)sy : 0u;
-            part[1][wave] = valid ? (uint32_t)su : 0u;
-            part[2][wave] = valid ? (uint32_t)sv : 0u;
-            part[3][wave] = (valid && mb_unmasked(fs, mbx, mby)) ? (uint32_t)sy : 0u;
+        // Y on lanes 0..15 of the half, U on 16..19, V on 20..23
+        const int sy = half_sum(sse_y);
+        const int su = half_sum((hl >= 16 && hl < 20) ? sse_c : 0);
+        const int sv = half_sum((hl >= 20 && hl < 24) ? sse_c : 0);
+        if (valid && fs->intra_in_p && hl < 3)  // per-MB copy: replaced if the MB switches to intra
+            mb_sse[hl * nmb + mbi] = (uint32_t)(hl == 0 ? sy : (hl == 1 ? su : sv));
+        __shared__ uint32_t part[4][8];
+        if (hl == 0) {
+            part[0][ms] = valid ? (uint32_t)sy : 0u;
+            part[1][ms] = valid ? (uint32_t)su : 0u;
+            part[2][ms] = valid ? (uint32_t)sv : 0u;
+            part[3][ms] = (valid && mb_unmasked(fs, mbx, mby)) ? (uint32_t)sy : 0u;
         }
         __syncthreads();
-        if (threadIdx.x < 4) {
-            const int c = threadIdx.x;
-            fs->sse_part[c * kSsePartStride + bid] =
-                (unsigned long long)part[c][0] + part[c][1] + part[c][2] + part[c][3];
+        if (threadIdx.x < 8) {  // one partial per 4 MBs (the layout k_scan_rows reduces)
+            const int c = threadIdx.x & 3, grp = threadIdx.x >> 2;
+            if (bid * 8 + grp * 4 < nmb)
+                fs->sse_part[c * kSsePartStride + bid * 2 + grp] = (unsigned long long)part[c][grp * 4] +
+                                                                   part[c][grp * 4 + 1] + part[c][grp * 4 + 2] +
+                                                                   part[c][grp * 4 + 3];
         }
     }
-    const unsigned long long luma_mask = __ballot(valid && lane < 16 && nz > 0);
-    const unsigned long long chroma_mask = __ballot(valid && lane >= 16 && lane < 24 && nz > 0);
-    if (valid && lane == 0) {
+    const unsigned long long luma_bal = __ballot(valid && hl < 16 && nz > 0);
+    const unsigned long long chroma_bal = __ballot(valid && hl >= 16 && hl < 24 && nz > 0);
+    const uint32_t luma_mask = (uint32_t)(luma_bal >> (32 * hf)), chroma_mask = (uint32_t)(chroma_bal >> (32 * hf));
+    if (valid && hl == 0) {
         int cbp = 0;
         for (int i8 = 0; i8 < 4; ++i8)
             if ((luma_mask >> (4 * i8)) & 0xf) cbp |= 1 << i8;
-        const int cc = (chroma_mask != 0) ? 2 : ((cdc_nz[wave][0] | cdc_nz[wave][1]) ? 1 : 0);
+        const int cc = (chroma_mask != 0) ? 2 : ((cdc_nz[ms][0] | cdc_nz[ms][1]) ? 1 : 0);
         cbp |= cc << 4;
         MbInfo& m = mbs[mbi];
         m.type = kMbP16x16;
@@ -1914,7 +1931,7 @@ void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, 
 void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream) {
     const int nmb = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_inter_encode, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, src_y, src_uv, b.mb,
+    hipLaunchKernelGGL(k_inter_encode, dim3((nmb + 7) / 8), dim3(256), 0, stream, g, b.fs, src_y, src_uv, b.mb,
                        b.coef, b.mb_sse, b.wave_prog);
 }
 
