@@ -291,12 +291,15 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     // moving MBs was measured slower: its atomic list append serialises, profiles/r02_me)
     constexpr int kWs4 = kWinStride / 4;
     {
-        const int r = tid >> 4, c = tid & 15;  // 256 threads = 16 rows x 16 px
-        int d = abs((int)src_y[(y0 + r) * g.pitch + x0 + c] - (int)P.f[(y0 + r) * P.pitch + x0 + c]);
-        d = wave_sum(d);
-        if (lane == 0) s_sad0[tid >> 6] = d;
+        if (tid < 64) {  // one wave: a dword of source and reference per lane, v_sad_u8
+            const int r = tid >> 2, c4 = (tid & 3) * 4;
+            const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c4);
+            const uint32_t rw = *reinterpret_cast<const uint32_t*>(P.f + (y0 + r) * P.pitch + x0 + c4);
+            const int d = wave_sum((int)__builtin_amdgcn_sad_u8(sw, rw, 0u));
+            if (tid == 0) s_sad0[0] = (uint32_t)d;
+        }
         __syncthreads();
-        const uint32_t sad0 = s_sad0[0] + s_sad0[1] + s_sad0[2] + s_sad0[3];
+        const uint32_t sad0 = s_sad0[0];
         if (sad0 <= static_sad(fs->qp)) {
             if (tid == 0) {
                 mbs[mbi].mvx = 0;
