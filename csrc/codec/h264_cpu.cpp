@@ -450,7 +450,8 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         for (int mbi = first; mbi < last; ++mbi) {
             const Avail av = mb_avail(g, mbi % g.mb_w, mbi / g.mb_w, slice_rows);
             int mvdx, mvdy;
-            const bool skip = decide_skip(g, mb_.data(), mbi, av, &mvdx, &mvdy);
+            const MbNbrs nb = mb_nbrs(mb_.data(), mbi, g.mb_w);
+            const bool skip = decide_skip(nb, av, &mvdx, &mvdy);
             mb_[mbi].skip = skip;
             if (skip) {
                 ++run;
@@ -467,7 +468,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
                 qp_pred = mb_[mbi].qp;
             }
             for (int role = 0; role < kNumRoles; ++role)
-                code_role(w, role, g, idr, mb_.data(), mb_[mbi], mc, mbi, av, mvdx, mvdy, dqp);
+                code_role(w, role, g, idr, nb, mc, av, mvdx, mvdy, dqp);
         }
         if (!idr && run > 0) put_ue(w, (uint32_t)run);
         w.put(1, 1);

@@ -1388,6 +1388,8 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     __shared__ uint32_t rbuf[kCavlcMbPerBlock][kNumRoles][kRoleWords];
     __shared__ uint32_t roff[kCavlcMbPerBlock][kNumRoles + 1];
     __shared__ __attribute__((aligned(16))) int16_t cbuf[kCavlcMbPerBlock][kCoefStride];
+    __shared__ MbInfo nbuf[kCavlcMbPerBlock][5];  // self, left, top, top-right, top-left
+    static_assert(sizeof(MbInfo) % 4 == 0, "MbInfo copied as dwords");
     const int hw = (threadIdx.x >> 5) & 1, lane = threadIdx.x & 31;  // hw: half of the wave; lane = role
     const int wave = threadIdx.x >> 5;                                   // MB slot in the block (half-wave)
     const int nmb = g.mb_w * g.mb_h;
@@ -1395,12 +1397,28 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     if (mbi >= nmb) return;  // a whole half exits; only half-local shuffles below, no workgroup barrier
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w;
     const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
-    const MbInfo& m = mbs[mbi];  // by reference: a private copy with dynamically indexed nz arrays spills to scratch
+    // the MB's and its available neighbours' MbInfo into LDS (12 dwords each, one load round):
+    // the role coders read their fields in data-dependent order, from global memory that was
+    // a chain of L2 round trips
+    {
+        const int src[5] = {mbi, mbi - 1, mbi - g.mb_w, mbi - g.mb_w + 1, mbi - g.mb_w - 1};
+        const bool ok[5] = {true, av.left, av.top, av.topright, av.topleft};
+        constexpr int kW = (int)(sizeof(MbInfo) / 4);
+        for (int q = lane; q < 5 * kW; q += 32) {
+            const int k = q / kW, d = q - k * kW;
+            if (ok[k]) reinterpret_cast<uint32_t*>(&nbuf[wave][k])[d] = reinterpret_cast<const uint32_t*>(&mbs[src[k]])[d];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const MbNbrs nb{&nbuf[wave][0], &nbuf[wave][1], &nbuf[wave][2], &nbuf[wave][3], &nbuf[wave][4]};
+    const MbInfo& m = nbuf[wave][0];
     const int16_t* mc = coef + (size_t)mbi * kCoefStride;
 
     // motion vector prediction + P_Skip decision (every lane computes the same values)
     int mvdx = 0, mvdy = 0;
-    const bool skip = decide_skip(g, mbs, mbi, av, &mvdx, &mvdy);
+    const bool skip = decide_skip(nb, av, &mvdx, &mvdy);
     // mb_qp_delta: QP predictor = QP of the previous MB in the slice that carried one (a P
     // macroblock with residual); skipped / residual-free MBs inherit it.  Half-wave-parallel
     // backward search, 32 MBs per step (the ballot holds active lanes only; this half's bits
@@ -1451,7 +1469,7 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     if (!skip && lane < kNumRoles) {
         BitWriter w;
         w.init(rbuf[wave][lane]);
-        code_role(w, lane, g, fs->idr, mbs, m, cbuf[wave], mbi, av, mvdx, mvdy, dqp);
+        code_role(w, lane, g, fs->idr, nb, cbuf[wave], av, mvdx, mvdy, dqp);
         w.flush();
         bits = w.bits;
     }

@@ -34,13 +34,27 @@ MXHD int combine_nc(bool ha, int na, bool hb, int nb) {
     return 0;
 }
 
-MXHD MvNb mv_nb(const MbInfo* mbs, int idx, bool avail) {
+// A macroblock and its neighbours (left, top, top-right, top-left) as the entropy coder reads
+// them: pointers into the frame's MbInfo array (CPU) or into LDS copies (k_cavlc).  A pointer
+// is only dereferenced when the neighbour is available.
+struct MbNbrs {
+    const MbInfo* self;
+    const MbInfo* left;
+    const MbInfo* top;
+    const MbInfo* topright;
+    const MbInfo* topleft;
+};
+MXHD MbNbrs mb_nbrs(const MbInfo* mbs, int mbi, int mb_w) {
+    return MbNbrs{&mbs[mbi], &mbs[mbi - 1], &mbs[mbi - mb_w], &mbs[mbi - mb_w + 1], &mbs[mbi - mb_w - 1]};
+}
+
+MXHD MvNb mv_nb(const MbInfo* p, bool avail) {
     MvNb n;
     n.avail = avail;
     n.ref = -1;
     n.mv = Mv{0, 0};
     if (!avail) return n;
-    const MbInfo& m = mbs[idx];
+    const MbInfo& m = *p;
     if (m.type == kMbP16x16) {
         n.ref = 0;
         n.mv = Mv{m.mvx, m.mvy};
@@ -49,15 +63,15 @@ MXHD MvNb mv_nb(const MbInfo* mbs, int idx, bool avail) {
 }
 
 // P_Skip decision + mvd for macroblock mbi (type P16x16).  Returns true for P_Skip.
-MXHD bool decide_skip(const Geometry& g, const MbInfo* mbs, int mbi, const Avail& av, int* mvdx, int* mvdy) {
-    const MbInfo& m = mbs[mbi];
+MXHD bool decide_skip(const MbNbrs& nb, const Avail& av, int* mvdx, int* mvdy) {
+    const MbInfo& m = *nb.self;
     *mvdx = 0;
     *mvdy = 0;
     if (m.type != kMbP16x16) return false;
-    const MvNb a = mv_nb(mbs, mbi - 1, av.left);
-    const MvNb b = mv_nb(mbs, mbi - g.mb_w, av.top);
-    MvNb c = mv_nb(mbs, mbi - g.mb_w + 1, av.topright);
-    if (!av.topright) c = mv_nb(mbs, mbi - g.mb_w - 1, av.topleft);
+    const MvNb a = mv_nb(nb.left, av.left);
+    const MvNb b = mv_nb(nb.top, av.top);
+    MvNb c = mv_nb(nb.topright, av.topright);
+    if (!av.topright) c = mv_nb(nb.topleft, av.topleft);
     const Mv pskip = predict_mv_skip(a, b, c);
     const Mv p = predict_mv16x16(a, b, c);
     *mvdx = m.mvx - p.x;
@@ -66,13 +80,14 @@ MXHD bool decide_skip(const Geometry& g, const MbInfo* mbs, int mbi, const Avail
 }
 
 template <class W>
-MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbInfo* mbs, const MbInfo& m,
-                    const int16_t* mc, int mbi, const Avail& av, int mvdx, int mvdy, int dqp = 0) {
+MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbNbrs& nb, const int16_t* mc,
+                    const Avail& av, int mvdx, int mvdy, int dqp = 0) {
+    const MbInfo& m = *nb.self;
     const bool intra = m.type == kMbI16x16;  // Intra16x16: DC / AC split of the luma residual
     const int cbp = m.cbp;
     const int cbp_l = cbp & 15, cbp_c = cbp >> 4;
-    const MbInfo* ml = av.left ? &mbs[mbi - 1] : nullptr;
-    const MbInfo* mt = av.top ? &mbs[mbi - g.mb_w] : nullptr;
+    const MbInfo* ml = av.left ? nb.left : nullptr;
+    const MbInfo* mt = av.top ? nb.top : nullptr;
     if (role == 0) {
         if (intra) {
             const int mbtype = 1 + m.i16_mode + 4 * cbp_c + (cbp_l ? 12 : 0);
