@@ -106,6 +106,7 @@ def main() -> None:
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--me-coarse", type=int, default=None,
                     help="1: even-offset grid + integer neighbours, 0: exhaustive search (encoder default)")
+    ap.add_argument("--intra4x4", type=int, default=None, help="0: intra MBs Intra16x16 only")
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
     ap.add_argument("--aq", type=int, default=None,
                     help="adaptive quantisation: 0 off, 1 coarser QP for noise-like MBs, 2 + rate-distortion "
@@ -168,6 +169,8 @@ def main() -> None:
         cfg.enc.aq = args.aq
     if args.me_coarse is not None:
         cfg.enc.me_coarse = args.me_coarse
+    if args.intra4x4 is not None:
+        cfg.enc.intra4x4 = args.intra4x4
     cfg.noise = args.noise
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth

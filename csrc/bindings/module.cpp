@@ -149,6 +149,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("keyint", &h264::EncoderConfig::keyint)
         .def_readwrite("search_range", &h264::EncoderConfig::search_range)
         .def_readwrite("me_coarse", &h264::EncoderConfig::me_coarse)
+        .def_readwrite("intra4x4", &h264::EncoderConfig::intra4x4)
         .def_readwrite("subpel", &h264::EncoderConfig::subpel)
         .def_readwrite("chroma_qp_offset", &h264::EncoderConfig::chroma_qp_offset)
         .def_readwrite("pipeline_depth", &h264::EncoderConfig::pipeline_depth)

@@ -134,7 +134,7 @@ static Geometry geom_of(const EncoderCommon& c, int cw, int ch) {
 // Open-loop intra analysis of one macroblock (source neighbours): the same costs and decision
 // as k_intra_analyze.
 static IntraDecision analyze_intra_mb(const Geometry& g, const uint8_t* sy, const uint8_t* suv, int pitch, int mbx,
-                                      int mby, int slice_rows, int qp) {
+                                      int mby, int slice_rows, int qp, bool allow4) {
     const Avail av = mb_avail(g, mbx, mby, slice_rows);
     const int x0 = mbx * 16, y0 = mby * 16;
     IntraCosts c;
@@ -164,7 +164,7 @@ static IntraDecision analyze_intra_mb(const Geometry& g, const uint8_t* sy, cons
         }
         c.cc[m] = t;
     }
-    return decide_intra(c, qp);
+    return decide_intra(c, qp, allow4);
 }
 
 static void set_intra(MbInfo& m, const IntraDecision& d, int qp) {
@@ -405,7 +405,7 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
     std::vector<IntraDecision> dec(nmb);
     for (int mbi = 0; mbi < nmb; ++mbi) {
         if (!intra_candidate(mb_[mbi].cost)) continue;
-        dec[mbi] = analyze_intra_mb(g, sy, suv, pitch, mbi % g.mb_w, mbi / g.mb_w, g.mb_h, frame_qp);
+        dec[mbi] = analyze_intra_mb(g, sy, suv, pitch, mbi % g.mb_w, mbi / g.mb_w, g.mb_h, frame_qp, cfg_.intra4x4 != 0);
         gain[mbi] = intra_gain(dec[mbi].cost_luma, mb_[mbi].cost, frame_qp);
     }
     for (int mbi = 0; mbi < nmb; ++mbi)
@@ -425,7 +425,7 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
     for (int mbi = 0; mbi < g.mb_w * g.mb_h; ++mbi) {
         MbInfo& m = mb_[mbi];
         std::memset(&m, 0, sizeof m);
-        set_intra(m, analyze_intra_mb(g, sy, suv, pitch, mbi % g.mb_w, mbi / g.mb_w, rows, qp), qp);
+        set_intra(m, analyze_intra_mb(g, sy, suv, pitch, mbi % g.mb_w, mbi / g.mb_w, rows, qp, cfg_.intra4x4 != 0), qp);
     }
     for (int mbi = 0; mbi < g.mb_w * g.mb_h; ++mbi)
         code_intra_mb(g, sy, suv, pitch, rec_y, rec_uv, cw_, mbi % g.mb_w, mbi / g.mb_w, rows, qp, cfg_.chroma_qp_offset,

@@ -374,6 +374,7 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.num_slices = (geom_.mb_h + f.slice_rows - 1) / f.slice_rows;
     f.search_range = me_range(cfg_.search_range);
     f.me_coarse = cfg_.me_coarse;
+    f.intra4x4 = cfg_.intra4x4;
     f.subpel = cfg_.subpel;
     f.deblock_off = 1;
     f.pic_init_qp = common_.pic_init_qp();

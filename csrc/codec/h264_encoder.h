@@ -31,6 +31,7 @@ struct EncoderConfig {
     int qp_max = 46;
     int keyint = 0;           // IDR period in frames, 0 = only on demand (infinite GOP)
     int search_range = 16;    // integer-pel full search radius (<= 32)
+    int intra4x4 = 1;         // Intra4x4 allowed for intra MBs (0: Intra16x16 only -- cheaper IDR wavefront)
     int me_coarse = 0;        // 1: ME over the even-offset grid + the 8 integer neighbours of its best (4x
                               // fewer SADs: +5.7 % fps, -0.4 dB masked Y-PSNR at 8 Mbps, profiles/r02_me);
                               // 0: exhaustive +-range search

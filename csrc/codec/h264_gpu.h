@@ -71,6 +71,7 @@ struct FrameState {
     int32_t search_range;  // integer-pel full-search radius
     int32_t subpel;        // 1 = quarter-pel refinement
     int32_t me_coarse;     // 1 = even-offset grid + integer neighbours instead of the full search
+    int32_t intra4x4;      // 0 = intra MBs are Intra16x16 only
     int32_t deblock_off;   // disable_deblocking_filter_idc
     int32_t pic_init_qp;
     int32_t chroma_qp_offset;

@@ -248,7 +248,7 @@ struct IntraDecision {
 // Estimated predicted-mode flag cost inside the MB: internal neighbours use the modes just
 // chosen; neighbours in other macroblocks are unknown during the parallel analysis and are
 // taken as DC (the actual coding uses the true predictor).
-MXHD IntraDecision decide_intra(const IntraCosts& c, int qp) {
+MXHD IntraDecision decide_intra(const IntraCosts& c, int qp, bool allow4 = true) {
     const uint32_t lam = (uint32_t)lambda_sad(qp);
     IntraDecision d{};
     int m4[16];  // raster
@@ -291,6 +291,7 @@ MXHD IntraDecision decide_intra(const IntraCosts& c, int qp) {
             bc = m;
         }
     }
+    if (!allow4) cost4 = kCostInf;  // EncoderConfig::intra4x4 = 0: Intra16x16 only (faster IDR reconstruction)
     d.type = cost4 < cost16 ? 2 /* kMbI4x4 */ : 1 /* kMbI16x16 */;
     d.i16_mode = b16;
     d.chroma_mode = bc;

@@ -810,7 +810,7 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane == 0) {
-        const IntraDecision d = decide_intra(c, fs->qp);
+        const IntraDecision d = decide_intra(c, fs->qp, fs->intra4x4 != 0);
         MbInfo& m = mbs[mbi];
         const int32_t gn = fs->idr ? 1 : intra_gain(d.cost_luma, m.cost, fs->qp);
         if (!fs->idr) {

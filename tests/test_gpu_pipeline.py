@@ -147,6 +147,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     cfg.intra_in_p = kw.get("intra_in_p", 1)
     cfg.aq = kw.get("aq", 1)
     cfg.me_coarse = kw.get("me_coarse", 1)
+    cfg.intra4x4 = kw.get("intra4x4", 1)
     genc = gpu.GpuH264Encoder(cfg, _stream())
     cenc = gpu.CpuH264Encoder(cfg)
     gs, cs, grec = b"", b"", []
@@ -183,6 +184,15 @@ def test_gpu_me_modes_bit_exact_vs_cpu(gpu, me_coarse, sr):
     """Exhaustive and coarse-grid (even offsets + integer neighbours) motion search: GPU ==
     CPU oracle, decodes to the reconstruction."""
     stream, grec = _gpu_cpu_encode(gpu, 160, 96, 4, search_range=sr, fresh_noise=0, qp=26, me_coarse=me_coarse)
+    dec = Decoder()
+    dec.decode(stream)
+    for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
+        assert np.array_equal(y, ry)
+
+
+def test_gpu_intra16x16_only_bit_exact_vs_cpu(gpu):
+    """intra4x4=0 (the fast-IDR setting): GPU == CPU oracle, decodes to the reconstruction."""
+    stream, grec = _gpu_cpu_encode(gpu, 160, 96, 3, fresh_noise=1, qp=28, intra4x4=0)
     dec = Decoder()
     dec.decode(stream)
     for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
