@@ -484,12 +484,78 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
 }
 
 // ------------------------------------------------------------------ inter encode
-// Two MBs per wave, one per 32-lane half: lanes 0..15 of a half code the 16 luma 4x4 blocks,
-// 16..23 the 8 chroma blocks (a whole wave per MB left 40 of 64 lanes idle in the transform
-// phase, which dominates).  8 MBs per workgroup; the distortion partials stay one per 4 MBs.
-__device__ __forceinline__ int half_sum(int v) {
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
-    return v;
+// One MB per wave, 4x4 blocks in "row" layout: lane 4b + r holds row r of block b (luma: all
+// 64 lanes = 16 blocks; chroma: lanes 0..31 = 8 blocks).  Both 1-D passes of every transform
+// run in-lane on a row, the column pass gathers the block's four rows with DPP quad
+// broadcasts (no LDS round trips); the integer arithmetic is exactly fdct4x4 / idct4x4 /
+// hadamard4x4 / quant4x4 / dequant4x4 (rows first, then columns), so the bitstream is
+// unchanged.  A block-per-lane layout left 40 of 64 lanes idle in the transform phase.
+template <int K>
+__device__ __forceinline__ int qbc(int v) {  // lane K of this lane's quad (quad_perm [K,K,K,K])
+    return __builtin_amdgcn_mov_dpp(v, K * 0x55, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int quad_sum(int v) { return qbc<0>(v) + qbc<1>(v) + qbc<2>(v) + qbc<3>(v); }
+
+// forward core transform of row r of a block whose rows sit in the quad: y = row r of Cf X Cf^T
+__device__ __forceinline__ void fdct_row(const int* x, int r, int* y) {
+    const int s03 = x[0] + x[3], d03 = x[0] - x[3], s12 = x[1] + x[2], d12 = x[1] - x[2];
+    const int t[4] = {s03 + s12, 2 * d03 + d12, s03 - s12, d03 - 2 * d12};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int a0 = qbc<0>(t[c]), a1 = qbc<1>(t[c]), a2 = qbc<2>(t[c]), a3 = qbc<3>(t[c]);
+        const int u03 = a0 + a3, e03 = a0 - a3, u12 = a1 + a2, e12 = a1 - a2;
+        y[c] = r == 0 ? u03 + u12 : r == 1 ? 2 * e03 + e12 : r == 2 ? u03 - u12 : e03 - 2 * e12;
+    }
+}
+// inverse core transform: residual row r from dequantised row d
+__device__ __forceinline__ void idct_row(const int* d, int r, int* out) {
+    const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+    const int f[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int b0 = qbc<0>(f[c]), b1 = qbc<1>(f[c]), b2 = qbc<2>(f[c]), b3 = qbc<3>(f[c]);
+        const int g0 = b0 + b2, g1 = b0 - b2, g2 = (b1 >> 1) - b3, g3 = b1 + (b3 >> 1);
+        const int v = r == 0 ? g0 + g3 : r == 1 ? g1 + g2 : r == 2 ? g1 - g2 : g0 - g3;
+        out[c] = (v + 32) >> 6;
+    }
+}
+// sum |Hadamard coefficients| of row r (satd4x4 before its halving)
+__device__ __forceinline__ int had_row_abs(const int* x, int r) {
+    const int t[4] = {x[0] + x[1] + x[2] + x[3], x[0] + x[1] - x[2] - x[3], x[0] - x[1] - x[2] + x[3],
+                      x[0] - x[1] + x[2] - x[3]};
+    int s = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int a = qbc<0>(t[c]), b = qbc<1>(t[c]), cc = qbc<2>(t[c]), d = qbc<3>(t[c]);
+        const int v = r == 0 ? a + b + cc + d : r == 1 ? a + b - cc - d : r == 2 ? a - b - cc + d : a - b + cc - d;
+        s += v < 0 ? -v : v;
+    }
+    return s;
+}
+// quant4x4 / dequant4x4 on row r (start = 1: the DC position is skipped)
+__device__ __forceinline__ int quant_row(const int* y, int r, int qp, bool intra, int start, int* z) {
+    const int qm = qp % 6, qbits = 15 + qp / 6;
+    const int f = intra ? ((1 << qbits) / 3) : ((1 << qbits) / 6);
+    int nz = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int i = r * 4 + c;
+        if (i < start) {
+            z[c] = 0;
+            continue;
+        }
+        const int a = y[c] < 0 ? -y[c] : y[c];
+        int q = (int)(((int64_t)a * kQuantMF[qm][kPosClass[i]] + f) >> qbits);
+        q = q > kMaxLevel ? kMaxLevel : q;
+        z[c] = y[c] < 0 ? -q : q;
+        nz += (q != 0);
+    }
+    return nz;
+}
+__device__ __forceinline__ void dequant_row(const int* z, int r, int qp, int* d) {
+    const int qm = qp % 6, qs = qp / 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) d[c] = z[c] * kDequantV[qm][kPosClass[r * 4 + c]] * (1 << qs);
 }
 
 __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameState* __restrict__ fs,
@@ -497,16 +563,15 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
                                                        const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
                                                        int16_t* __restrict__ coef, uint32_t* __restrict__ mb_sse,
                                                        int* __restrict__ wave_prog) {
-    __shared__ uint8_t pred[8][384];
-    __shared__ int16_t res[8][384];
-    __shared__ int cdc[8][8];
-    __shared__ int cdc_nz[8][2];
+    __shared__ uint8_t pred[4][384];
+    __shared__ int16_t res[4][384];
+    __shared__ int cdc[4][8];
+    __shared__ int cdc_nz[4][2];
 
-    const int lane = threadIdx.x & 63, hf = lane >> 5, hl = lane & 31;
-    const int ms = (threadIdx.x >> 6) * 2 + hf;  // MB slot in the workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nmb = g.mb_w * g.mb_h;
     const int bid = blockIdx.x;
-    const int mbi = bid * 8 + ms;
+    const int mbi = bid * 4 + wave;
     if (bid == 0 && threadIdx.x == 0) wave_prog[1] = 0;  // k_intra_analyze's candidate list (next kernel)
     const bool valid = mbi < nmb;
     const int mbx = valid ? mbi % g.mb_w : 0, mby = valid ? mbi / g.mb_w : 0;
@@ -519,152 +584,154 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     if (valid) {
         mvx = mbs[mbi].mvx;
         mvy = mbs[mbi].mvy;
-        const int r = hl >> 1, c0 = (hl & 1) * 8;  // 8 luma samples per lane
-        const uint2 sw = *reinterpret_cast<const uint2*>(src_y + (y0 + r) * g.pitch + x0 + c0);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        const int r = lane >> 2, c0 = (lane & 3) * 4;
+        const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
+        for (int k = 0; k < 4; ++k) {
             const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
-            const int d = (int)(((k < 4 ? sw.x : sw.y) >> (8 * (k & 3))) & 0xff) - p;
-            pred[ms][r * 16 + c0 + k] = (uint8_t)p;
-            res[ms][r * 16 + c0 + k] = (int16_t)d;
+            const int d = (int)((sw >> (8 * k)) & 0xff) - p;
+            pred[wave][r * 16 + c0 + k] = (uint8_t)p;
+            res[wave][r * 16 + c0 + k] = (int16_t)d;
             lsad += d < 0 ? -d : d;
         }
-        const int cr_ = hl >> 2, cc0 = (hl & 3) * 2;  // 2 chroma positions x 2 planes per lane
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int cc = cc0 + e, xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
-#pragma unroll
-            for (int comp = 0; comp < 2; ++comp) {
-                const int p = chroma_pred8(ref_uv, g.pitch, cw, ch, comp, xc * 8 + mvx, yc * 8 + mvy);
-                const int sv = src_uv[yc * g.pitch + 2 * xc + comp];
-                pred[ms][256 + comp * 64 + cr_ * 8 + cc] = (uint8_t)p;
-                res[ms][256 + comp * 64 + cr_ * 8 + cc] = (int16_t)(sv - p);
-            }
+        const int cr_ = lane >> 3, cc = lane & 7;
+        const int xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
+        for (int comp = 0; comp < 2; ++comp) {
+            const int p = chroma_pred8(ref_uv, g.pitch, cw, ch, comp, xc * 8 + mvx, yc * 8 + mvy);
+            const int sv = src_uv[yc * g.pitch + 2 * xc + comp];
+            pred[wave][256 + comp * 64 + cr_ * 8 + cc] = (uint8_t)p;
+            res[wave][256 + comp * 64 + cr_ * 8 + cc] = (int16_t)(sv - p);
         }
     }
     __syncthreads();
-    const uint32_t lsad_mb = (uint32_t)half_sum(lsad);
-    const int qp = aq_mb_qp(fs->qp, lsad_mb, fs->aq);  // uniform over the half
+    const uint32_t lsad_mb = (uint32_t)wave_sum(lsad);
+    const int qp = aq_mb_qp(fs->qp, lsad_mb, fs->aq);  // wave-uniform
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
-
-    int z[16];
-    int nz = 0;
-    int sse_y = 0, sse_c = 0;
-    uint32_t satd = 0;
     int16_t* mc = coef + (size_t)(valid ? mbi : 0) * kCoefStride;
-    // luma transform / quant first; outputs wait for the MB-level residual-drop decision
-    int x[16], zs[16], r[16];
-    int d_pred = 0, d_coded = 0;
-    uint32_t bits = 0;
-    if (valid && hl < 16) {
-        const int b = hl, bx = kBlkX[b], by = kBlkY[b];
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) x[i * 4 + j] = res[ms][(by * 4 + i) * 16 + bx * 4 + j];
-        satd = satd4x4(x);
-        nz = luma_block_inter(x, qp, zs, r);
-        bits = block_bits_est(nz);
-        for (int i = 0; i < 16; ++i) {
-            const int pv = pred[ms][(by * 4 + (i >> 2)) * 16 + bx * 4 + (i & 3)];
-            const int e = pv + x[i] - clip255(pv + r[i]);
-            d_pred += x[i] * x[i];
-            d_coded += e * e;
-        }
+
+    // ---- luma: lane = 4 * blkIdx + row
+    const int lb = lane >> 2, rr = lane & 3, lbx = kBlkX[lb], lby = kBlkY[lb];
+    int x[4], y[4], z[4], rres[4];
+    const int ro = (lby * 4 + rr) * 16 + lbx * 4;  // row offset in the MB's pred / res
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = res[wave][ro + c];
+    const int hs = quad_sum(had_row_abs(x, rr));
+    fdct_row(x, rr, y);
+    const int nzb = quad_sum(quant_row(y, rr, qp, false, 0, z));
+    {
+        int d[4];
+        dequant_row(z, rr, qp, d);
+        idct_row(d, rr, rres);
     }
-    const bool drop = drop_residual(fs->aq, lsad_mb, qp, half_sum(d_pred), half_sum(d_coded),
-                                    (uint32_t)half_sum((int)bits));  // uniform over the half
-    if (valid && hl < 16) {
-        const int b = hl, bx = kBlkX[b], by = kBlkY[b];
-        if (drop) {
-            nz = 0;
-            for (int k = 0; k < 16; ++k) zs[k] = r[k] = 0;
+    int d_pred = 0, d_coded = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int pv = pred[wave][ro + c];
+        const int e = pv + x[c] - clip255(pv + rres[c]);
+        d_pred += x[c] * x[c];
+        d_coded += e * e;
+    }
+    const uint32_t bits = rr == 0 ? block_bits_est(nzb) : 0u;
+    const bool drop = valid && drop_residual(fs->aq, lsad_mb, qp, wave_sum(d_pred), wave_sum(d_coded),
+                                             (uint32_t)wave_sum((int)bits));  // wave-uniform
+    const int nz_l = drop ? 0 : nzb;
+    int sse_y = 0;
+    if (valid) {
+        uint32_t packed = 0;
+        const bool vis = x0 + lbx * 4 < g.width && (y0 + lby * 4 + rr) < g.height;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (drop) z[c] = rres[c] = 0;
+            mc[kCoefLuma + lb * 16 + kZigzagInv4x4[rr * 4 + c]] = (int16_t)z[c];
+            const int pv = pred[wave][ro + c];
+            const int v = clip255(pv + rres[c]);
+            const int e = pv + x[c] - v;
+            sse_y += vis ? e * e : 0;
+            packed |= (uint32_t)v << (8 * c);
         }
-        for (int k = 0; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)zs[k];
-        mbs[mbi].nz_luma[by * 4 + bx] = (uint8_t)nz;
-        const bool vis_x = x0 + bx * 4 < g.width;
-        for (int i = 0; i < 4; ++i) {
-            uint32_t packed = 0;
-            const bool vis = vis_x && (y0 + by * 4 + i) < g.height;
-            for (int j = 0; j < 4; ++j) {
-                const int pv = pred[ms][(by * 4 + i) * 16 + bx * 4 + j];
-                const int v = clip255(pv + r[i * 4 + j]);
-                const int e = pv + x[i * 4 + j] - v;
-                sse_y += vis ? e * e : 0;
-                packed |= (uint32_t)v << (8 * j);
-            }
-            *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + by * 4 + i) * g.pitch + x0 + bx * 4) = packed;
+        *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + lby * 4 + rr) * g.pitch + x0 + lbx * 4) = packed;
+        if (rr == 0) mbs[mbi].nz_luma[lby * 4 + lbx] = (uint8_t)nz_l;
+    }
+    const uint32_t satd_mb = (uint32_t)wave_sum(rr == 0 ? (hs + 1) >> 1 : 0);
+
+    // ---- chroma: lanes 0..31, lane = 4 * (comp * 4 + blk) + row
+    const int cbk = lane >> 2, ccomp = (cbk >> 2) & 1, cblk = cbk & 3, cbx = cblk & 1, cby = cblk >> 1;
+    const int co = 256 + ccomp * 64 + (cby * 4 + rr) * 8 + cbx * 4;
+    const bool clane = lane < 32;
+    int cz[4], nzc = 0;
+    if (clane) {
+        int cx[4], cy[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cx[c] = drop ? 0 : res[wave][co + c];  // a dropped MB codes no chroma residual
+        fdct_row(cx, rr, cy);
+        if (rr == 0) cdc[wave][ccomp * 4 + cblk] = cy[0];
+        nzc = quant_row(cy, rr, qpc, false, 1, cz);
+    }
+    nzc = quad_sum(nzc);
+    if (valid && clane) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int i = rr * 4 + c;
+            if (i > 0) mc[kCoefChromaAc + (ccomp * 4 + cblk) * 16 + kZigzagInv4x4[i]] = (int16_t)cz[c];
         }
-    } else if (valid && hl < 24) {
-        const int comp = (hl - 16) >> 2, cb = (hl - 16) & 3, bx = cb & 1, by = cb >> 1;
-        int y[16];
-        for (int i = 0; i < 4; ++i)  // a dropped MB codes no chroma residual either
-            for (int j = 0; j < 4; ++j)
-                x[i * 4 + j] = drop ? 0 : res[ms][256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j];
-        fdct4x4(x, y);
-        cdc[ms][comp * 4 + cb] = y[0];
-        nz = quant4x4(y, z, qpc, false, 1);
-        for (int k = 1; k < 16; ++k) mc[kCoefChromaAc + (comp * 4 + cb) * 16 + k] = (int16_t)z[kZigzag4x4[k]];
-        (comp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cb] = (uint8_t)nz;
+        if (rr == 0) (ccomp ? mbs[mbi].nz_cr : mbs[mbi].nz_cb)[cblk] = (uint8_t)nzc;
     }
     __syncthreads();
-    if (valid && (hl == 16 || hl == 20)) {
-        const int comp = (hl - 16) >> 2;
+    if (valid && (lane == 0 || lane == 16)) {
+        const int comp = lane >> 4;
         int in[4], zd[4], dq[4];
-        for (int i = 0; i < 4; ++i) in[i] = cdc[ms][comp * 4 + i];
+        for (int i = 0; i < 4; ++i) in[i] = cdc[wave][comp * 4 + i];
         const int n = quant_dc_chroma(in, zd, qpc, false);
         for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zd[i];
         dequant_dc_chroma(zd, dq, qpc);
-        for (int i = 0; i < 4; ++i) cdc[ms][comp * 4 + i] = dq[i];
-        cdc_nz[ms][comp] = n;
+        for (int i = 0; i < 4; ++i) cdc[wave][comp * 4 + i] = dq[i];
+        cdc_nz[wave][comp] = n;
     }
     __syncthreads();
-    if (valid && hl >= 16 && hl < 24) {
-        const int comp = (hl - 16) >> 2, cb = (hl - 16) & 3, bx = cb & 1, by = cb >> 1;
-        int d[16], rr[16];
-        dequant4x4(z, d, qpc, 1);
-        d[0] = cdc[ms][comp * 4 + cb];
-        idct4x4(d, rr);
-        const int xc = x0 / 2 + bx * 4, yc = y0 / 2 + by * 4;
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) {
-                const int o = 256 + comp * 64 + (by * 4 + i) * 8 + bx * 4 + j;
-                const int v = clip255(pred[ms][o] + rr[i * 4 + j]);
-                const int e = pred[ms][o] + res[ms][o] - v;
-                sse_c += (2 * (xc + j) < g.width && 2 * (yc + i) < g.height) ? e * e : 0;
-                fs->rec_uv[(yc + i) * g.pitch + 2 * (xc + j) + comp] = (uint8_t)v;
+    int sse_c = 0;
+    if (clane) {
+        int d[4], cr[4];
+        dequant_row(cz, rr, qpc, d);
+        if (rr == 0) d[0] = cdc[wave][ccomp * 4 + cblk];
+        idct_row(d, rr, cr);
+        if (valid) {
+            const int xc = x0 / 2 + cbx * 4, yc = y0 / 2 + cby * 4 + rr;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int v = clip255(pred[wave][co + c] + cr[c]);
+                const int e = pred[wave][co + c] + res[wave][co + c] - v;
+                sse_c += (2 * (xc + c) < g.width && 2 * yc < g.height) ? e * e : 0;
+                fs->rec_uv[yc * g.pitch + 2 * (xc + c) + ccomp] = (uint8_t)v;
             }
+        }
     }
-    const uint32_t satd_mb = (uint32_t)half_sum((int)satd);
     {
-        // Y on lanes 0..15 of the half, U on 16..19, V on 20..23
-        const int sy = half_sum(sse_y);
-        const int su = half_sum((hl >= 16 && hl < 20) ? sse_c : 0);
-        const int sv = half_sum((hl >= 20 && hl < 24) ? sse_c : 0);
-        if (valid && fs->intra_in_p && hl < 3)  // per-MB copy: replaced if the MB switches to intra
-            mb_sse[hl * nmb + mbi] = (uint32_t)(hl == 0 ? sy : (hl == 1 ? su : sv));
-        __shared__ uint32_t part[4][8];
-        if (hl == 0) {
-            part[0][ms] = valid ? (uint32_t)sy : 0u;
-            part[1][ms] = valid ? (uint32_t)su : 0u;
-            part[2][ms] = valid ? (uint32_t)sv : 0u;
-            part[3][ms] = (valid && mb_unmasked(fs, mbx, mby)) ? (uint32_t)sy : 0u;
+        // Y on all lanes, U on lanes 0..15, V on 16..31
+        const int sy = wave_sum(sse_y);
+        const int su = wave_sum(lane < 16 ? sse_c : 0);
+        const int sv = wave_sum((lane >= 16 && lane < 32) ? sse_c : 0);
+        if (valid && fs->intra_in_p && lane < 3)  // per-MB copy: replaced if the MB switches to intra
+            mb_sse[lane * nmb + mbi] = (uint32_t)(lane == 0 ? sy : (lane == 1 ? su : sv));
+        __shared__ uint32_t part[4][4];
+        if (lane == 0) {
+            part[0][wave] = valid ? (uint32_t)sy : 0u;
+            part[1][wave] = valid ? (uint32_t)su : 0u;
+            part[2][wave] = valid ? (uint32_t)sv : 0u;
+            part[3][wave] = (valid && mb_unmasked(fs, mbx, mby)) ? (uint32_t)sy : 0u;
         }
         __syncthreads();
-        if (threadIdx.x < 8) {  // one partial per 4 MBs (the layout k_scan_rows reduces)
-            const int c = threadIdx.x & 3, grp = threadIdx.x >> 2;
-            if (bid * 8 + grp * 4 < nmb)
-                fs->sse_part[c * kSsePartStride + bid * 2 + grp] = (unsigned long long)part[c][grp * 4] +
-                                                                   part[c][grp * 4 + 1] + part[c][grp * 4 + 2] +
-                                                                   part[c][grp * 4 + 3];
+        if (threadIdx.x < 4) {
+            const int c = threadIdx.x;
+            fs->sse_part[c * kSsePartStride + bid] =
+                (unsigned long long)part[c][0] + part[c][1] + part[c][2] + part[c][3];
         }
     }
-    const unsigned long long luma_bal = __ballot(valid && hl < 16 && nz > 0);
-    const unsigned long long chroma_bal = __ballot(valid && hl >= 16 && hl < 24 && nz > 0);
-    const uint32_t luma_mask = (uint32_t)(luma_bal >> (32 * hf)), chroma_mask = (uint32_t)(chroma_bal >> (32 * hf));
-    if (valid && hl == 0) {
+    const unsigned long long luma_mask = __ballot(valid && rr == 0 && nz_l > 0);    // bit 4b: block b
+    const unsigned long long chroma_mask = __ballot(valid && clane && rr == 0 && nzc > 0);
+    if (valid && lane == 0) {
         int cbp = 0;
-        for (int i8 = 0; i8 < 4; ++i8)
-            if ((luma_mask >> (4 * i8)) & 0xf) cbp |= 1 << i8;
-        const int cc = (chroma_mask != 0) ? 2 : ((cdc_nz[ms][0] | cdc_nz[ms][1]) ? 1 : 0);
+        for (int b8 = 0; b8 < 4; ++b8)
+            if ((luma_mask >> (16 * b8)) & 0x1111ull) cbp |= 1 << b8;
+        const int cc = (chroma_mask != 0) ? 2 : ((cdc_nz[wave][0] | cdc_nz[wave][1]) ? 1 : 0);
         cbp |= cc << 4;
         MbInfo& m = mbs[mbi];
         m.type = kMbP16x16;
@@ -1952,7 +2019,7 @@ void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, 
 void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream) {
     const int nmb = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_inter_encode, dim3((nmb + 7) / 8), dim3(256), 0, stream, g, b.fs, src_y, src_uv, b.mb,
+    hipLaunchKernelGGL(k_inter_encode, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, b.fs, src_y, src_uv, b.mb,
                        b.coef, b.mb_sse, b.wave_prog);
 }
 
