@@ -22,6 +22,7 @@
 
 #include <cstddef>
 
+#include "../common/hip_check.h"
 #include "h264_core.h"
 #include "h264_gpu.h"
 #include "h264_mb.h"
@@ -921,48 +922,6 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
 // inter distortion of the switched macroblocks by a per-row delta partial.
 
 
-// Cross-workgroup hand-off between MB rows.  The 8 XCDs' L2 caches are not coherent with each
-// other, so an agent-scope release / acquire fence writes back / invalidates the whole L2 --
-// ~20 us per macroblock when the first version fenced every MB (profiles/r02_l), and a
-// progress counter behind a store-completion wait still cost a memory round trip per MB on
-// the critical path (profiles/r02_n).  Instead the data carries its own flag: every dword of
-// an intra MB's bottom sample line is stored as one 64-bit agent-coherent (L2-bypassing)
-// atomic {frame tag, 4 samples}; a reader polls exactly the words it needs until they carry
-// this frame's tag.  No fences, no counters, and the writer never waits.
-__device__ __forceinline__ uint64_t load_line(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_line(uint64_t* p, uint32_t tag, uint32_t v) {
-    __hip_atomic_store(p, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// 4x4 forward / inverse core transform of one block held one coefficient per lane (lane
-// r*4 + c of a 16-lane group); the same integer butterflies as fdct4x4 / idct4x4.
-__device__ __forceinline__ int fdct_lane(int x, int base, int r, int c) {
-    const int x0 = __shfl(x, base + r * 4 + 0, 64), x1 = __shfl(x, base + r * 4 + 1, 64);
-    const int x2 = __shfl(x, base + r * 4 + 2, 64), x3 = __shfl(x, base + r * 4 + 3, 64);
-    const int s03 = x0 + x3, d03 = x0 - x3, s12 = x1 + x2, d12 = x1 - x2;
-    const int t = c == 0 ? s03 + s12 : c == 1 ? 2 * d03 + d12 : c == 2 ? s03 - s12 : d03 - 2 * d12;
-    const int t0 = __shfl(t, base + 0 * 4 + c, 64), t1 = __shfl(t, base + 1 * 4 + c, 64);
-    const int t2 = __shfl(t, base + 2 * 4 + c, 64), t3 = __shfl(t, base + 3 * 4 + c, 64);
-    const int u03 = t0 + t3, e03 = t0 - t3, u12 = t1 + t2, e12 = t1 - t2;
-    return r == 0 ? u03 + u12 : r == 1 ? 2 * e03 + e12 : r == 2 ? u03 - u12 : e03 - 2 * e12;
-}
-__device__ __forceinline__ int idct_lane(int d, int base, int r, int c) {
-    const int d0 = __shfl(d, base + r * 4 + 0, 64), d1 = __shfl(d, base + r * 4 + 1, 64);
-    const int d2 = __shfl(d, base + r * 4 + 2, 64), d3 = __shfl(d, base + r * 4 + 3, 64);
-    const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
-    const int f = c == 0 ? e0 + e3 : c == 1 ? e1 + e2 : c == 2 ? e1 - e2 : e0 - e3;
-    const int f0 = __shfl(f, base + 0 * 4 + c, 64), f1 = __shfl(f, base + 1 * 4 + c, 64);
-    const int f2 = __shfl(f, base + 2 * 4 + c, 64), f3 = __shfl(f, base + 3 * 4 + c, 64);
-    const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
-    const int v = r == 0 ? g0 + g3 : r == 1 ? g1 + g2 : r == 2 ? g1 - g2 : g0 - g3;
-    return (v + 32) >> 6;
-}
-
-// Intra4x4 schedule: blocks (raster index by*4+bx) of each of the 10 dependency steps.
-__constant__ int8_t kI4Step[10][2] = {{0, -1}, {1, -1}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {14, -1}, {15, -1}};
-
 // Per-MB fields the reconstruction needs, read once (prefetched a macroblock ahead).
 struct MbFields {
     int type, qp, i16_mode, chroma_mode;
@@ -985,149 +944,257 @@ static_assert(offsetof(MbInfo, type) == 4 && offsetof(MbInfo, i16_mode) == 6 && 
                   offsetof(MbInfo, qp) == 33 && offsetof(MbInfo, i4) == 36,
               "load_fields() layout");
 
-// ls: the macroblock's source luma in LDS (16 x 16, pitch 16).
-__device__ void intra_luma_mb(const Geometry& g, const MbFields& f, const uint8_t* ls, MbInfo& m,
+
+// Quantiser constants of one QP, read with wave-uniform indices (scalar loads) and picked per
+// coefficient position with selects: a lane-indexed table read is a vector memory round trip,
+// and in the wavefront every one of them sits on the critical path (profiles/r02_idr).
+struct QpTab {
+    int mf0, mf1, mf2;  // kQuantMF[qp % 6][class]
+    int dv0, dv1, dv2;  // kDequantV[qp % 6][class]
+    int qbits, qs;
+    uint32_t f_intra;
+    __device__ int mf(int cls) const { return cls == 0 ? mf0 : (cls == 1 ? mf1 : mf2); }
+    __device__ int dv(int cls) const { return cls == 0 ? dv0 : (cls == 1 ? dv1 : dv2); }
+};
+__device__ __forceinline__ QpTab qp_tab(int qp) {
+    QpTab t;
+    const int qm = qp % 6;
+    t.mf0 = kQuantMF[qm][0];
+    t.mf1 = kQuantMF[qm][1];
+    t.mf2 = kQuantMF[qm][2];
+    t.dv0 = kDequantV[qm][0];
+    t.dv1 = kDequantV[qm][1];
+    t.dv2 = kDequantV[qm][2];
+    t.qbits = 15 + qp / 6;
+    t.qs = qp / 6;
+    t.f_intra = (1u << t.qbits) / 3;
+    return t;
+}
+// kPosClass of raster position (r, c): 0 both even, 1 both odd, 2 mixed
+__device__ __forceinline__ int pos_class(int r, int c) { return ((r | c) & 1) == 0 ? 0 : (((r & c) & 1) ? 1 : 2); }
+// kZigzagInv4x4 as nibbles of one 64-bit immediate
+constexpr uint64_t zz_inv_packed() {
+    uint64_t v = 0;
+    for (int i = 0; i < 16; ++i) v |= (uint64_t)kZigzagInv4x4[i] << (4 * i);
+    return v;
+}
+__device__ __forceinline__ int zz_inv(int i) { return (int)((zz_inv_packed() >> (4 * i)) & 15u); }
+// blkIdx <-> raster 4x4 block position (6.4.3), arithmetic
+__device__ __forceinline__ int blk_x(int b) { return (b & 1) | ((b >> 1) & 2); }
+__device__ __forceinline__ int blk_y(int b) { return ((b >> 1) & 1) | ((b >> 2) & 2); }
+// Intra4x4 schedule: raster block of quad group `grp` (0, 1) at dependency step t (block
+// (bx, by) at step bx + 2 by), -1 if none
+__device__ __forceinline__ int i4_step_block(int t, int grp) {
+    const int by = (t >= 2 ? (t - 2) >> 1 : 0) + grp, bx = t - 2 * by;
+    return (bx >= 0 && bx <= 3 && by <= 3) ? by * 4 + bx : -1;
+}
+__device__ __forceinline__ int raster_to_blk(int rb) {
+    const int bx = rb & 3, by = rb >> 2;
+    return ((by >> 1) << 3) | ((bx >> 1) << 2) | ((by & 1) << 1) | (bx & 1);
+}
+// quant4x4 / dequant4x4 of row r (intra rounding), 32-bit: |y| * MF + f < 2^31 for 8-bit video
+__device__ __forceinline__ int quant_row_i(const int* y, int r, const QpTab& t, int start, int* z) {
+    int nz = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int a = y[c] < 0 ? -y[c] : y[c];
+        int q = (int)(((uint32_t)a * (uint32_t)t.mf(pos_class(r, c)) + t.f_intra) >> t.qbits);
+        q = q > kMaxLevel ? kMaxLevel : q;
+        q = (r * 4 + c) < start ? 0 : q;
+        z[c] = y[c] < 0 ? -q : q;
+        nz += (q != 0);
+    }
+    return nz;
+}
+__device__ __forceinline__ void dequant_row_t(const int* z, int r, const QpTab& t, int* d) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) d[c] = z[c] * t.dv(pos_class(r, c)) * (1 << t.qs);
+}
+// Hadamard of row r of a 4x4 block whose rows sit in the quad (hadamard4x4, rows then columns)
+__device__ __forceinline__ void had_row(const int* x, int r, int* y) {
+    const int t[4] = {x[0] + x[1] + x[2] + x[3], x[0] + x[1] - x[2] - x[3], x[0] - x[1] - x[2] + x[3],
+                      x[0] - x[1] + x[2] - x[3]};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int a = qbc<0>(t[c]), b = qbc<1>(t[c]), cc = qbc<2>(t[c]), d = qbc<3>(t[c]);
+        y[c] = r == 0 ? a + b + cc + d : r == 1 ? a + b - cc - d : r == 2 ? a - b - cc + d : a - b + cc - d;
+    }
+}
+
+// Closed-loop coding of one intra macroblock's luma, in the 4x4 "row" layout of
+// k_inter_encode (lane 4b + r = row r of block b): every transform pass is in-lane or a DPP
+// quad broadcast, the quantiser tables are scalar.  ls: the MB's source luma (16 rows x 4
+// dwords); lt: the LDS tile with the neighbours at row 0 / column 0, reconstructed in place.
+//  * Intra4x4: the 16 blocks in 10 dependency steps (block (bx,by) at step bx + 2*by, up to
+//    two blocks = two quads per step).
+//  * Intra16x16: all 16 blocks at once; the DC Hadamard / quantiser on quad 0 (row layout of
+//    the 4x4 DC matrix).
+__device__ void intra_luma_mb(const Geometry& g, const MbFields& f, const uint32_t* ls, MbInfo& m,
                               int16_t* __restrict__ mc, int mbx, int mby, const Avail& av, uint8_t (*lt)[kLT],
                               int* ldc, int lane, uint32_t& sse) {
     const int x0 = mbx * 16, y0 = mby * 16;
-    const int qp = f.qp;
+    const QpTab T = qp_tab(f.qp);
     const uint8_t* tile = &lt[1][1];
+    const int r = lane & 3;
     int cbp_l = 0;
     if (f.type == kMbI4x4) {
-        const int grp = lane >> 4, base = grp << 4, r = (lane >> 2) & 3, c = lane & 3, i = r * 4 + c;
-        const int qm = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
+        const int grp = lane >> 2;
         for (int t = 0; t < 10; ++t) {
-            const int rb = lane < 32 ? kI4Step[t][grp] : -1;
+            const int rb = grp < 2 ? i4_step_block(t, grp) : -1;  // uniform per quad
             int nzb = 0;
             if (rb >= 0) {
-                const int bx = rb & 3, by = rb >> 2;
+                const int bx = rb & 3, by = rb >> 2, py = 4 * by + r;
                 const Nb4 n = nb4_from_plane(tile, kLT, 0, 0, bx, by, av.left, av.top, av.topright, av.topleft);
-                const int pred = pred4x4_px(f.i4(rb), n, c, r);
-                const int xs = x0 + 4 * bx + c, ys = y0 + 4 * by + r;
-                const int sv = ls[(4 * by + r) * 16 + 4 * bx + c];
-                const int res = sv - pred;
-                const int y = fdct_lane(res, base, r, c);
-                const int a = y < 0 ? -y : y;
-                int q = (int)(((int64_t)a * kQuantMF[qm][kPosClass[i]] + fq) >> qbits);
-                q = q > kMaxLevel ? kMaxLevel : q;
-                const int z = y < 0 ? -q : q;
-                const unsigned long long bal = __ballot(z != 0);
-                nzb = __popcll((bal >> base) & 0xffffull);
-                mc[kCoefLuma + kRasterToBlk[rb] * 16 + kZigzagInv4x4[i]] = (int16_t)z;
-                const int d = z * kDequantV[qm][kPosClass[i]] * (1 << (qp / 6));
-                const int rec = clip255(pred + idct_lane(d, base, r, c));
-                lt[1 + 4 * by + r][1 + 4 * bx + c] = (uint8_t)rec;
-                const int e = sv - rec;
-                sse += (xs < g.width && ys < g.height) ? (uint32_t)(e * e) : 0u;
-                if (i == 0) {
-                    m.nz_luma[rb] = (uint8_t)nzb;
+                const int mode = f.i4(rb);
+                const uint32_t sw = ls[py * 4 + bx];
+                int pv[4], x[4], y[4], z[4], d[4], rr[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    pv[c] = pred4x4_px(mode, n, c, r);
+                    x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
                 }
+                fdct_row(x, r, y);
+                nzb = quad_sum(quant_row_i(y, r, T, 0, z));
+                const int b = raster_to_blk(rb);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) mc[kCoefLuma + b * 16 + zz_inv(r * 4 + c)] = (int16_t)z[c];
+                dequant_row_t(z, r, T, d);
+                idct_row(d, r, rr);
+                const bool vis = y0 + py < g.height;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int rec = clip255(pv[c] + rr[c]);
+                    lt[1 + py][1 + 4 * bx + c] = (uint8_t)rec;
+                    const int e = x[c] + pv[c] - rec;
+                    sse += (vis && x0 + 4 * bx + c < g.width) ? (uint32_t)(e * e) : 0u;
+                }
+                if (r == 0) m.nz_luma[rb] = (uint8_t)nzb;
             }
-            const unsigned long long any = __ballot(rb >= 0 && i == 0 && nzb > 0);
+            const unsigned long long any = __ballot(rb >= 0 && r == 0 && nzb > 0);
             for (int gq = 0; gq < 2; ++gq)
-                if ((any >> (16 * gq)) & 1ull) cbp_l |= 1 << (kRasterToBlk[kI4Step[t][gq]] >> 2);
+                if ((any >> (4 * gq)) & 1ull) cbp_l |= 1 << (raster_to_blk(i4_step_block(t, gq)) >> 2);
             wave_sync_lds();
         }
-    } else {  // Intra16x16: lane b (blkIdx) < 16 codes one 4x4 block
+    } else {  // Intra16x16
         const NbMb n = nbmb_from_plane(tile, kLT, 0, 0, 16, 1, 0, av.left, av.top, av.topleft);
         const PredMb p = prep_i16(f.i16_mode, n);
-        int z[16], nz = 0;
-        const int b = lane, bx = kBlkX[b & 15], by = kBlkY[b & 15];
-        if (lane < 16) {
-            int x[16], y[16];
-            for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j)
-                    x[i * 4 + j] = (int)ls[(4 * by + i) * 16 + 4 * bx + j] - pred16_px(p, n, 4 * bx + j, 4 * by + i);
-            fdct4x4(x, y);
-            ldc[by * 4 + bx] = y[0];
-            nz = quant4x4(y, z, qp, true, 1);
-            for (int k = 1; k < 16; ++k) mc[kCoefLuma + b * 16 + k] = (int16_t)z[kZigzag4x4[k]];
-            mc[kCoefLuma + b * 16] = 0;
+        const int b = lane >> 2, bx = blk_x(b), by = blk_y(b), py = 4 * by + r;
+        const uint32_t sw = ls[py * 4 + bx];
+        int pv[4], x[4], y[4], z[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            pv[c] = pred16_px(p, n, 4 * bx + c, py);
+            x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
         }
+        fdct_row(x, r, y);
+        if (r == 0) ldc[by * 4 + bx] = y[0];
+        const int nz = quad_sum(quant_row_i(y, r, T, 1, z));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) mc[kCoefLuma + b * 16 + zz_inv(r * 4 + c)] = (int16_t)z[c];
         wave_sync_lds();
-        if (lane == 0) {
-            int zd[16], dq[16];
-            quant_dc_luma(ldc, zd, qp);
-            for (int k = 0; k < 16; ++k) mc[kCoefLumaDc + k] = (int16_t)zd[kZigzag4x4[k]];
-            dequant_dc_luma(zd, dq, qp);
-            for (int k = 0; k < 16; ++k) ldc[k] = dq[k];
-        }
-        wave_sync_lds();
-        const bool luma_ac = __ballot(lane < 16 && nz > 0) != 0;
-        if (lane < 16) {
-            int d[16], rr[16];
-            if (luma_ac) {
-                dequant4x4(z, d, qp, 1);
-            } else {
-                for (int i = 1; i < 16; ++i) d[i] = 0;
+        if (lane < 4) {  // DC matrix row `lane`: Hadamard, /2, quantise (quant_dc_luma), then dequant_dc_luma
+            int dc[4], h[4], zd[4], fh[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) dc[c] = ldc[lane * 4 + c];
+            had_row(dc, lane, h);
+            const uint32_t qb = (uint32_t)(T.qbits + 1), fd = 2u * ((1u << (qb - 1)) / 3);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int v = h[c] >> 1;
+                const int a = v < 0 ? -v : v;
+                int q = (int)(((uint32_t)a * (uint32_t)T.mf0 + fd) >> qb);
+                q = q > kMaxLevel ? kMaxLevel : q;
+                zd[c] = v < 0 ? -q : q;
+                mc[kCoefLumaDc + zz_inv(lane * 4 + c)] = (int16_t)zd[c];
             }
-            d[0] = ldc[by * 4 + bx];
-            idct4x4(d, rr);
-            for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j) {
-                    const int xs = x0 + 4 * bx + j, ys = y0 + 4 * by + i;
-                    const int rec = clip255(pred16_px(p, n, 4 * bx + j, 4 * by + i) + rr[i * 4 + j]);
-                    const int e = (int)ls[(4 * by + i) * 16 + 4 * bx + j] - rec;
-                    sse += (xs < g.width && ys < g.height) ? (uint32_t)(e * e) : 0u;
-                    lt[1 + 4 * by + i][1 + 4 * bx + j] = (uint8_t)rec;
-                }
-            m.nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nz : 0);
+            had_row(zd, lane, fh);
+            const int ls16 = 16 * T.dv0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                ldc[lane * 4 + c] = f.qp >= 36 ? fh[c] * ls16 * (1 << (T.qs - 6))
+                                               : (fh[c] * ls16 + (1 << (5 - T.qs))) >> (6 - T.qs);
         }
+        wave_sync_lds();
+        const bool luma_ac = __ballot(r == 0 && nz > 0) != 0;
+        int d[4], rr[4];
+        dequant_row_t(z, r, T, d);
+        if (r == 0) d[0] = ldc[by * 4 + bx];
+        idct_row(d, r, rr);
+        const bool vis = y0 + py < g.height;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int rec = clip255(pv[c] + rr[c]);
+            lt[1 + py][1 + 4 * bx + c] = (uint8_t)rec;
+            const int e = x[c] + pv[c] - rec;
+            sse += (vis && x0 + 4 * bx + c < g.width) ? (uint32_t)(e * e) : 0u;
+        }
+        if (r == 0) m.nz_luma[by * 4 + bx] = (uint8_t)(luma_ac ? nz : 0);
         cbp_l = luma_ac ? 15 : 0;
         wave_sync_lds();
     }
     if (lane == 0) m.cbp = (uint8_t)cbp_l;  // chroma bits merged at the end of the row
 }
 
-// cs: the macroblock's source chroma in LDS (8 rows x 16 interleaved bytes).
-__device__ void intra_chroma_mb(const Geometry& g, const FrameState* fs, const MbFields& f, const uint8_t* cs,
+// Chroma of one intra macroblock, row layout on lanes 0..31 (lane 4 (comp * 4 + blk) + r).
+// cs: the MB's source chroma (8 rows x 4 dwords of interleaved Cb/Cr).
+__device__ void intra_chroma_mb(const Geometry& g, int chroma_qp_offset, const MbFields& f, const uint32_t* cs,
                                 MbInfo& m, int16_t* __restrict__ mc, int mbx, int mby, const Avail& av,
                                 uint8_t (*ct)[9][kCT], int* cdc, int lane, uint32_t& sse_u, uint32_t& sse_v) {
     const int xc0 = mbx * 8, yc0 = mby * 8;
-    const int qpc = chroma_qp(f.qp, fs->chroma_qp_offset);
-    const int comp = lane >> 2, cb = lane & 3, bx = cb & 1, by = cb >> 1;
-    int z[16], nz = 0;
-    NbMb n;
-    PredMb p;
-    if (lane < 8) {
-        n = nbmb_from_plane(&ct[comp][1][1], kCT, 0, 0, 8, 1, 0, av.left, av.top, av.topleft);
-        p = prep_chroma(f.chroma_mode, n);
-        int x[16], y[16];
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j)
-                x[i * 4 + j] = (int)cs[(4 * by + i) * 16 + 2 * (4 * bx + j) + comp] - predc_px(p, n, 4 * bx + j, 4 * by + i);
-        fdct4x4(x, y);
-        cdc[comp * 4 + cb] = y[0];
-        nz = quant4x4(y, z, qpc, true, 1);
-        for (int k = 1; k < 16; ++k) mc[kCoefChromaAc + (comp * 4 + cb) * 16 + k] = (int16_t)z[kZigzag4x4[k]];
-        (comp ? m.nz_cr : m.nz_cb)[cb] = (uint8_t)nz;
+    const int qpc = chroma_qp(f.qp, chroma_qp_offset);
+    const QpTab T = qp_tab(qpc);
+    const int r = lane & 3, cbk = (lane >> 2) & 7, comp = cbk >> 2, cb = cbk & 3, bx = cb & 1, by = cb >> 1;
+    const int py = 4 * by + r;
+    const bool clane = lane < 32;
+    int pv[4] = {0, 0, 0, 0}, x[4] = {0, 0, 0, 0}, z[4] = {0, 0, 0, 0}, nz = 0;
+    if (clane) {
+        const NbMb n = nbmb_from_plane(&ct[comp][1][1], kCT, 0, 0, 8, 1, 0, av.left, av.top, av.topleft);
+        const PredMb p = prep_chroma(f.chroma_mode, n);
+        // samples 4bx .. 4bx+3 of this plane = bytes 8bx + 2c + comp of the interleaved row
+        const uint32_t w0 = cs[py * 4 + 2 * bx], w1 = cs[py * 4 + 2 * bx + 1];
+        int y[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t w = c < 2 ? w0 : w1;
+            pv[c] = predc_px(p, n, 4 * bx + c, py);
+            x[c] = (int)((w >> (8 * (2 * (c & 1) + comp))) & 0xff) - pv[c];
+        }
+        fdct_row(x, r, y);
+        if (r == 0) cdc[comp * 4 + cb] = y[0];
+        nz = quad_sum(quant_row_i(y, r, T, 1, z));
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (r * 4 + c > 0) mc[kCoefChromaAc + (comp * 4 + cb) * 16 + zz_inv(r * 4 + c)] = (int16_t)z[c];
+        if (r == 0) (comp ? m.nz_cr : m.nz_cb)[cb] = (uint8_t)nz;
     }
     wave_sync_lds();
     int ndc = 0;
-    if (lane == 0 || lane == 4) {
+    if (lane == 0 || lane == 16) {
+        const int cp = lane >> 4;
         int in[4], zd[4], dq[4];
-        for (int i = 0; i < 4; ++i) in[i] = cdc[comp * 4 + i];
+        for (int i = 0; i < 4; ++i) in[i] = cdc[cp * 4 + i];
         ndc = quant_dc_chroma(in, zd, qpc, true);
-        for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + comp * 4 + i] = (int16_t)zd[i];
+        for (int i = 0; i < 4; ++i) mc[kCoefChromaDc + cp * 4 + i] = (int16_t)zd[i];
         dequant_dc_chroma(zd, dq, qpc);
-        for (int i = 0; i < 4; ++i) cdc[comp * 4 + i] = dq[i];
+        for (int i = 0; i < 4; ++i) cdc[cp * 4 + i] = dq[i];
     }
     wave_sync_lds();
-    const bool any_ac = __ballot(lane < 8 && nz > 0) != 0, any_dc = __ballot(ndc > 0) != 0;
-    if (lane < 8) {
-        int d[16], rr[16];
-        dequant4x4(z, d, qpc, 1);
-        d[0] = cdc[comp * 4 + cb];
-        idct4x4(d, rr);
+    const bool any_ac = __ballot(clane && nz > 0) != 0, any_dc = __ballot(ndc > 0) != 0;
+    if (clane) {
+        int d[4], rr[4];
+        dequant_row_t(z, r, T, d);
+        if (r == 0) d[0] = cdc[comp * 4 + cb];
+        idct_row(d, r, rr);
         uint32_t s = 0;
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) {
-                const int xc = xc0 + 4 * bx + j, yc = yc0 + 4 * by + i;
-                const int rec = clip255(predc_px(p, n, 4 * bx + j, 4 * by + i) + rr[i * 4 + j]);
-                const int e = (int)cs[(4 * by + i) * 16 + 2 * (4 * bx + j) + comp] - rec;
-                s += (2 * xc < g.width && 2 * yc < g.height) ? (uint32_t)(e * e) : 0u;
-                ct[comp][1 + 4 * by + i][1 + 4 * bx + j] = (uint8_t)rec;
-            }
+        const bool vis = 2 * (yc0 + py) < g.height;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int xc = xc0 + 4 * bx + c;
+            const int rec = clip255(pv[c] + rr[c]);
+            const int e = x[c] + pv[c] - rec;
+            s += (vis && 2 * xc < g.width) ? (uint32_t)(e * e) : 0u;
+            ct[comp][1 + py][1 + 4 * bx + c] = (uint8_t)rec;
+        }
         if (comp)
             sse_v += s;
         else
@@ -1137,163 +1204,116 @@ __device__ void intra_chroma_mb(const Geometry& g, const FrameState* fs, const M
     wave_sync_lds();
 }
 
-constexpr int kMaxMbW = 512;  // 8192 samples
 
-// Top neighbour byte at position x of the row above's bottom line (luma samples, or interleaved
-// chroma bytes), owned by macroblock x >> 4: intra MBs of this picture publish it through the
-// tagged line buffer (polled until written), inter MBs are final in the picture since
-// k_inter_encode.  Every lane of the wave calls this (inactive lanes with need = false).
-__device__ __forceinline__ uint8_t top_sample(bool need, bool owner_intra, const uint8_t* __restrict__ pic_row,
-                                              const uint64_t* __restrict__ line, int x, uint32_t tag) {
-    uint64_t v = 0;
-    bool pending = need && owner_intra;
-    while (true) {
-        if (pending) {
-            v = load_line(line + (x >> 2));
-            pending = (uint32_t)(v >> 32) != tag;
-        }
-        if (__ballot(pending) == 0) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (!need) return 0;
-    return owner_intra ? (uint8_t)(v >> (8 * (x & 3))) : pic_row[x];
-}
+// IDR reconstruction: one workgroup per (slice, plane) -- every MB row of the slice is one wave
+// of the workgroup (idr_slice_rows() <= 8), luma and chroma are separate workgroups (the two
+// planes' intra predictions are independent).  The diagonal wavefront's row-to-row hand-off
+// stays inside the CU: a row publishes each macroblock's bottom sample line into an LDS line
+// buffer and then its progress counter; the row below waits on that counter (luma: the MB
+// above-right, chroma: the MB above).  LDS operations of one wave complete in issue order,
+// so a reader that sees the counter sees the line.  The cross-CU version of this hand-off
+// (tagged L2-bypassing line words between per-row workgroups) spent most of its time waiting
+// for the stores to become visible (profiles/r02_idr).
+struct IntraWaveTiles {
+    uint8_t lt[17][kLT];    // luma tile: row 0 = top neighbours, column 0 = left neighbours
+    uint8_t ct[2][9][kCT];  // chroma tiles (Cb, Cr)
+    uint32_t src[64];       // source of the current MB (luma 16 x 16 / chroma 8 rows x 16 bytes)
+    int dc[16];             // luma DC / chroma DC scratch
+};
 
-__global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState* __restrict__ fs,
-                                                    const uint8_t* __restrict__ src_y,
-                                                    const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
-                                                    int16_t* __restrict__ coef, int* __restrict__ wave_prog,
-                                                    uint64_t* __restrict__ wave_line,
-                                                    const uint32_t* __restrict__ mb_sse) {
-    __shared__ uint8_t lt[17][kLT];      // luma tile: row 0 = top neighbours, column 0 = left neighbours
-    __shared__ uint8_t ct[2][9][kCT];    // chroma tiles (Cb, Cr)
-    __shared__ uint32_t ls[64];          // source luma of the current MB (16 x 16)
-    __shared__ uint32_t cs[32];          // source chroma of the current MB (8 rows x 16 interleaved bytes)
-    __shared__ int ldc[16], cdc[8];
-    __shared__ int s_row;
-    __shared__ unsigned long long s_sse[4];
-    __shared__ uint8_t rintra[2][kMaxMbW];  // intra flags of this row's / the row above's macroblocks
+// One plane's rows of the slice.
+template <bool chroma>
+__device__ __forceinline__ void intra_wave_rows(const Geometry& g, const FrameState* __restrict__ fs,
+                                             const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
+                                             MbInfo* __restrict__ mbs, int16_t* __restrict__ coef, uint8_t* s_line,
+                                             IntraWaveTiles* tiles, int* prog) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // rows are taken in dispatch order (ticket): a row only ever waits on rows already running
-    if (threadIdx.x == 0) s_row = atomicAdd(&wave_prog[0], 1);
-    const bool idr = fs->idr != 0;
-    const uint32_t tag = (uint32_t)fs->frame_tag;
-    __syncthreads();
-    const int mby = s_row;
-    for (int x = threadIdx.x; x < g.mb_w; x += 128) {
-        rintra[0][x] = (uint8_t)(idr || is_intra(mbs[mby * g.mb_w + x]));
-        rintra[1][x] = (uint8_t)(mby > 0 && (idr || is_intra(mbs[(mby - 1) * g.mb_w + x])));
-    }
-    __syncthreads();
-    // bottom-line buffers: per MB row, coded_w / 4 luma words then coded_w / 4 chroma words
-    const int line_words = g.coded_w / 2;
-    uint64_t* my_line = wave_line + (size_t)mby * line_words + (wave ? g.coded_w / 4 : 0);
-    const uint64_t* up_line = wave_line + (size_t)(mby > 0 ? mby - 1 : 0) * line_words + (wave ? g.coded_w / 4 : 0);
-    int last_coded = -2;  // the left neighbour's reconstruction is in the tile when last_coded == mbx - 1
-    uint32_t sse_a = 0, sse_b = 0;  // luma wave: Y; chroma wave: U, V
-    uint32_t sse_m = 0;             // luma wave: Y of the MBs outside the quality-report mask
-    uint32_t old_a = 0, old_b = 0, old_c = 0, old_m = 0;  // P pictures: inter distortion of the replaced MBs
-    // software pipeline: the source samples and fields of the next intra MB are loaded while the
-    // current one is coded (one dword of source per lane)
-    auto next_intra = [&](int from) {
-        int x = from;
-        while (x < g.mb_w && !rintra[0][x]) ++x;
-        return x;
-    };
+    const int slice_rows = fs->slice_rows, cqp_off = fs->chroma_qp_offset;
+    uint8_t* const rec_y = fs->rec_y;
+    uint8_t* const rec_uv = fs->rec_uv;
+    const int mby = blockIdx.x * slice_rows + wave;
+    const bool active = mby < g.mb_h;  // the last slice may be shorter (whole waves)
+    if (!active) return;  // no workgroup barriers below
+    IntraWaveTiles& T = tiles[wave];
+    uint8_t* my_line = s_line + (size_t)wave * g.coded_w;
+    const uint8_t* up_line = s_line + (size_t)(wave > 0 ? wave - 1 : 0) * g.coded_w;
+    uint32_t sse_a = 0, sse_b = 0;  // luma: Y; chroma: U, V
+    uint32_t sse_m = 0;             // luma: Y of the MBs outside the quality-report mask
+    // software pipeline: the next MB's source dword and fields load while this one is coded
     auto fetch_src = [&](int mbx) -> uint32_t {
         if (mbx >= g.mb_w) return 0u;
-        if (wave == 0) {
-            const int r = lane >> 2, c4 = (lane & 3) * 4;
-            return *reinterpret_cast<const uint32_t*>(src_y + (size_t)(mby * 16 + r) * g.pitch + mbx * 16 + c4);
-        }
-        if (lane >= 32) return 0u;
         const int r = lane >> 2, c4 = (lane & 3) * 4;
+        if (!chroma) return *reinterpret_cast<const uint32_t*>(src_y + (size_t)(mby * 16 + r) * g.pitch + mbx * 16 + c4);
+        if (lane >= 32) return 0u;
         return *reinterpret_cast<const uint32_t*>(src_uv + (size_t)(mby * 8 + r) * g.pitch + mbx * 16 + c4);
     };
-    int nxt = next_intra(0);
-    uint32_t nsrc = fetch_src(nxt);
-    MbFields nf = load_fields(&mbs[mby * g.mb_w + (nxt < g.mb_w ? nxt : 0)]);
-    for (int mbx = nxt; mbx < g.mb_w; mbx = nxt) {
+    uint32_t nsrc = fetch_src(0);
+    MbFields nf = load_fields(&mbs[mby * g.mb_w]);
+    for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int mbi = mby * g.mb_w + mbx;
         MbInfo& m = mbs[mbi];
-        const bool left_in_tile = last_coded == mbx - 1;
         const MbFields f = nf;
-        if (wave == 0) ls[lane] = nsrc;
-        else if (lane < 32) cs[lane] = nsrc;
-        const Avail av = mb_avail(g, mbx, mby, fs->slice_rows);
+        T.src[lane] = nsrc;
+        nsrc = fetch_src(mbx + 1);
+        nf = load_fields(&mbs[mby * g.mb_w + (mbx + 1 < g.mb_w ? mbx + 1 : mbx)]);
+        const Avail av = mb_avail(g, mbx, mby, slice_rows);
         int16_t* mc = coef + (size_t)mbi * kCoefStride;
-        if (wave == 0) {
+        if (av.top) {  // wait for the row above (uniform)
+            const int need = chroma ? mbx + 1 : (av.topright ? mbx + 2 : mbx + 1);
+            while (__hip_atomic_load(&prog[wave - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+                __builtin_amdgcn_s_sleep(1);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        }
+        if (!chroma) {
             const int x0 = mbx * 16, y0 = mby * 16;
-            // left column: keep the previous MB's right column from the tile, or load it
-            const uint8_t keep = (lane < 16 && left_in_tile) ? lt[1 + lane][16] : 0;
-            const uint8_t lft = (lane < 16 && !left_in_tile && av.left) ? fs->rec_y[(y0 + lane) * g.pitch + x0 - 1] : 0;
+            // the left column is the previous MB's right column, already in the tile
+            const uint8_t keep = lane < 16 ? T.lt[1 + lane][16] : 0;
             const int x = x0 - 1 + lane;
             const bool need = lane < 21 && (lane == 0 ? av.topleft : (lane <= 16 ? av.top : av.topright));
-            const uint8_t top = top_sample(need, need && rintra[1][x >> 4],
-                                           fs->rec_y + (size_t)(y0 > 0 ? y0 - 1 : 0) * g.pitch, up_line, x, tag);
-            nxt = next_intra(mbx + 1);  // prefetch the next intra MB behind this one's neighbour loads
-            nsrc = fetch_src(nxt);
-            nf = load_fields(&mbs[mby * g.mb_w + (nxt < g.mb_w ? nxt : mbx)]);
+            const uint8_t top = need ? up_line[x] : 0;
             wave_sync_lds();
-            if (lane < 16) lt[1 + lane][0] = left_in_tile ? keep : lft;
-            if (lane < 21) lt[0][lane] = top;
+            if (lane < 16) T.lt[1 + lane][0] = av.left ? keep : 0;
+            if (lane < 21) T.lt[0][lane] = top;
             wave_sync_lds();
             uint32_t sse_mb = 0;
-            intra_luma_mb(g, f, reinterpret_cast<const uint8_t*>(ls), m, mc, mbx, mby, av, lt, ldc, lane, sse_mb);
+            intra_luma_mb(g, f, T.src, m, mc, mbx, mby, av, T.lt, T.dc, lane, sse_mb);
             sse_a += sse_mb;
-            const bool unmasked = mb_unmasked(fs, mbx, mby);
-            if (unmasked) sse_m += sse_mb;
-            if (!idr && unmasked && lane == 0) old_m += mb_sse[mbi];
-            {  // tile -> reconstruction: 16 rows x 16 bytes, one dword per lane; bottom line -> buffer
-                const int r = lane >> 2, c4 = (lane & 3) * 4;
-                const uint32_t v = (uint32_t)lt[1 + r][1 + c4] | ((uint32_t)lt[1 + r][2 + c4] << 8) |
-                                   ((uint32_t)lt[1 + r][3 + c4] << 16) | ((uint32_t)lt[1 + r][4 + c4] << 24);
-                *reinterpret_cast<uint32_t*>(fs->rec_y + (y0 + r) * g.pitch + x0 + c4) = v;
-                if (r == 15) store_line(my_line + (x0 + c4) / 4, tag, v);
-            }
-            if (!idr && lane == 0) old_a += mb_sse[mbi];
+            if (mb_unmasked(fs, mbx, mby)) sse_m += sse_mb;
+            // tile -> reconstruction: 16 rows x 16 bytes, one dword per lane; bottom line -> LDS
+            const int r = lane >> 2, c4 = (lane & 3) * 4;
+            const uint32_t v = (uint32_t)T.lt[1 + r][1 + c4] | ((uint32_t)T.lt[1 + r][2 + c4] << 8) |
+                               ((uint32_t)T.lt[1 + r][3 + c4] << 16) | ((uint32_t)T.lt[1 + r][4 + c4] << 24);
+            *reinterpret_cast<uint32_t*>(rec_y + (size_t)(y0 + r) * g.pitch + x0 + c4) = v;
+            if (r == 15) *reinterpret_cast<uint32_t*>(my_line + x0 + c4) = v;
         } else {
             const int xc0 = mbx * 8, yc0 = mby * 8;
-            uint8_t keep = 0, lft = 0;
-            if (lane < 16) {
-                const int comp = lane >> 3, r = lane & 7;
-                keep = left_in_tile ? ct[comp][1 + r][8] : 0;
-                lft = (!left_in_tile && av.left) ? fs->rec_uv[(yc0 + r) * g.pitch + 2 * (xc0 - 1) + comp] : 0;
-            }
+            uint8_t keep = 0;
+            if (lane < 16) keep = T.ct[lane >> 3][1 + (lane & 7)][8];
             // top: lanes 16..33 -> (comp, cx 0..8 = x -1..7), byte 2*(xc0-1+cx)+comp of the line
             const int k = lane - 16, comp_t = k >= 9 ? 1 : 0, cx = k - 9 * comp_t;
             const int x = 2 * (xc0 - 1 + cx) + comp_t;
             const bool need = lane >= 16 && lane < 34 && (cx == 0 ? av.topleft : av.top);
-            const uint8_t top = top_sample(need, need && rintra[1][x >> 4],
-                                           fs->rec_uv + (size_t)(yc0 > 0 ? yc0 - 1 : 0) * g.pitch, up_line, x, tag);
-            nxt = next_intra(mbx + 1);
-            nsrc = fetch_src(nxt);
-            nf = load_fields(&mbs[mby * g.mb_w + (nxt < g.mb_w ? nxt : mbx)]);
+            const uint8_t top = need ? up_line[x] : 0;
             wave_sync_lds();
-            if (lane < 16) {
-                ct[lane >> 3][1 + (lane & 7)][0] = left_in_tile ? keep : lft;
-            } else if (lane < 34) {
-                ct[comp_t][0][cx] = top;
-            }
+            if (lane < 16)
+                T.ct[lane >> 3][1 + (lane & 7)][0] = av.left ? keep : 0;
+            else if (lane < 34)
+                T.ct[comp_t][0][cx] = top;
             wave_sync_lds();
-            intra_chroma_mb(g, fs, f, reinterpret_cast<const uint8_t*>(cs), m, mc, mbx, mby, av, ct, cdc, lane, sse_a,
-                            sse_b);
+            intra_chroma_mb(g, cqp_off, f, T.src, m, mc, mbx, mby, av, T.ct, T.dc, lane, sse_a, sse_b);
             if (lane < 32) {  // 8 rows x 16 interleaved bytes, one dword (2 samples x 2 planes) per lane
                 const int r = lane >> 2, c2 = (lane & 3) * 2;
-                const uint32_t v = (uint32_t)ct[0][1 + r][1 + c2] | ((uint32_t)ct[1][1 + r][1 + c2] << 8) |
-                                   ((uint32_t)ct[0][1 + r][2 + c2] << 16) | ((uint32_t)ct[1][1 + r][2 + c2] << 24);
-                *reinterpret_cast<uint32_t*>(fs->rec_uv + (yc0 + r) * g.pitch + 2 * (xc0 + c2)) = v;
-                if (r == 7) store_line(my_line + (2 * (xc0 + c2)) / 4, tag, v);
-            }
-            if (!idr && lane == 0) {
-                old_b += mb_sse[g.mb_w * g.mb_h + mbi];
-                old_c += mb_sse[2 * g.mb_w * g.mb_h + mbi];
+                const uint32_t v = (uint32_t)T.ct[0][1 + r][1 + c2] | ((uint32_t)T.ct[1][1 + r][1 + c2] << 8) |
+                                   ((uint32_t)T.ct[0][1 + r][2 + c2] << 16) | ((uint32_t)T.ct[1][1 + r][2 + c2] << 24);
+                *reinterpret_cast<uint32_t*>(rec_uv + (size_t)(yc0 + r) * g.pitch + 2 * (xc0 + c2)) = v;
+                if (r == 7) *reinterpret_cast<uint32_t*>(my_line + 2 * (xc0 + c2)) = v;
             }
         }
-        last_coded = mbx;
+        // publish: the line stores above were issued first, and LDS completes them in order
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) __hip_atomic_store(&prog[wave], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // distortion of the row: absolute (IDR: one partial per row) or, in P pictures, the delta
-    // of the switched macroblocks against their inter distortion (modulo-2^64 sums)
+    // distortion of the row (one partial per row and channel)
     unsigned long long a = sse_a, b = sse_b, mm = sse_m;
     for (int o = 32; o > 0; o >>= 1) {
         a += __shfl_xor(a, o, 64);
@@ -1301,23 +1321,37 @@ __global__ __launch_bounds__(128) void k_intra_wave(Geometry g, const FrameState
         mm += __shfl_xor(mm, o, 64);
     }
     if (lane == 0) {
-        if (wave == 0) {
-            s_sse[0] = a - old_a;
-            s_sse[3] = mm - old_m;
+        if (!chroma) {
+            fs->sse_part[0 * kSsePartStride + mby] = a;
+            fs->sse_part[3 * kSsePartStride + mby] = mm;
         } else {
-            s_sse[1] = a - old_b;
-            s_sse[2] = b - old_c;
+            fs->sse_part[1 * kSsePartStride + mby] = a;
+            fs->sse_part[2 * kSsePartStride + mby] = b;
         }
     }
+}
+
+__global__ __launch_bounds__(512) void k_intra_wave(Geometry g, const FrameState* __restrict__ fs,
+                                                     const uint8_t* __restrict__ src_y,
+                                                     const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
+                                                     int16_t* __restrict__ coef) {
+    extern __shared__ uint8_t s_line[];  // [slice rows][coded_w]: bottom sample line of every coded MB
+    __shared__ IntraWaveTiles tiles[8];
+    __shared__ int prog[8];              // macroblocks of the row whose bottom line is in s_line
+    if ((threadIdx.x & 63) == 0) prog[threadIdx.x >> 6] = 0;
     __syncthreads();
-    for (int mbx = threadIdx.x; mbx < g.mb_w; mbx += 128) {
-        MbInfo& m = mbs[mby * g.mb_w + mbx];
-        if (idr || is_intra(m)) m.cbp = (uint8_t)((m.cbp & 15) | (m.cbp_c << 4));
-    }
-    if (threadIdx.x < 4) {
-        const int slot = idr ? mby : (g.mb_w * g.mb_h + 3) / 4 + mby;
-        fs->sse_part[threadIdx.x * kSsePartStride + slot] = s_sse[threadIdx.x];
-    }
+    if (blockIdx.y == 0)
+        intra_wave_rows<false>(g, fs, src_y, src_uv, mbs, coef, s_line, tiles, prog);
+    else
+        intra_wave_rows<true>(g, fs, src_y, src_uv, mbs, coef, s_line, tiles, prog);
+}
+
+// IDR: luma and chroma coded bits merged into the MB's cbp once both planes are done.
+__global__ __launch_bounds__(256) void k_intra_cbp(Geometry g, MbInfo* __restrict__ mbs) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= g.mb_w * g.mb_h) return;
+    MbInfo& m = mbs[i];
+    m.cbp = (uint8_t)((m.cbp & 15) | (m.cbp_c << 4));
 }
 
 // Intra macroblocks of P pictures (independent by construction, see intra_selected()): one
@@ -1361,7 +1395,7 @@ __device__ void intra_p_mb(const Geometry& g, const FrameState* __restrict__ fs,
             lt[0][lane] = ok ? fs->rec_y[(y0 - 1) * g.pitch + x0 - 1 + lane] : 0;
         }
         wave_sync_lds();
-        intra_luma_mb(g, f, reinterpret_cast<const uint8_t*>(ls), m, mc, mbx, mby, av, lt, ldc, lane, s0);
+        intra_luma_mb(g, f, ls, m, mc, mbx, mby, av, lt, ldc, lane, s0);
         const int r = lane >> 2, c4 = (lane & 3) * 4;
         const uint32_t v = (uint32_t)lt[1 + r][1 + c4] | ((uint32_t)lt[1 + r][2 + c4] << 8) |
                            ((uint32_t)lt[1 + r][3 + c4] << 16) | ((uint32_t)lt[1 + r][4 + c4] << 24);
@@ -1381,7 +1415,7 @@ __device__ void intra_p_mb(const Geometry& g, const FrameState* __restrict__ fs,
             ct[comp][0][cx] = ok ? fs->rec_uv[(yc0 - 1) * g.pitch + 2 * (xc0 - 1 + cx) + comp] : 0;
         }
         wave_sync_lds();
-        intra_chroma_mb(g, fs, f, reinterpret_cast<const uint8_t*>(cs), m, mc, mbx, mby, av, ct, cdc, lane, s0, s1);
+        intra_chroma_mb(g, fs->chroma_qp_offset, f, cs, m, mc, mbx, mby, av, ct, cdc, lane, s0, s1);
         if (lane < 32) {
             const int r = lane >> 2, c2 = (lane & 3) * 2;
             const uint32_t v = (uint32_t)ct[0][1 + r][1 + c2] | ((uint32_t)ct[1][1 + r][1 + c2] << 8) |
@@ -2045,8 +2079,18 @@ void launch_intra_in_p(const Geometry& g, const DeviceBuffers& b, const uint8_t*
 void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream, const FrameState* publish) {
     launch_analyze(g, b, src_y, src_uv, stream, publish);
-    hipLaunchKernelGGL(k_intra_wave, dim3(g.mb_h), dim3(128), 0, stream, g, b.fs, src_y, src_uv, b.mb, b.coef,
-                       b.wave_prog, b.wave_line, b.mb_sse);
+    // one workgroup per (slice, plane), one wave per slice row; LDS line buffers of the rows
+    const int rows = idr_slice_rows(g.mb_h), slices = (g.mb_h + rows - 1) / rows;
+    const size_t lds = (size_t)rows * g.coded_w;
+    static bool attr_set = false;  // line buffers above the default dynamic-LDS limit (8K: 61 KB + tiles)
+    if (!attr_set) {
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_intra_wave),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)sizeof(IntraWaveTiles) * 8 - 32));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_intra_wave, dim3(slices, 2), dim3(64 * rows), lds, stream, g, b.fs, src_y, src_uv, b.mb,
+                       b.coef);
+    hipLaunchKernelGGL(k_intra_cbp, dim3((g.mb_w * g.mb_h + 255) / 256), dim3(256), 0, stream, g, b.mb);
 }
 
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream) {

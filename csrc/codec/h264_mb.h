@@ -207,10 +207,11 @@ MXHD uint32_t inter_cost(uint32_t satd, int frame_qp, int mvx, int mvy) {
 }
 
 // Rows per slice of an IDR picture: intra macroblocks are reconstructed in a diagonal
-// wavefront per slice, so the critical path is mb_w + 2 * (rows - 1) macroblocks; ~16-row
-// slices keep it near mb_w at every size (one slice = 254 MB steps at 1080p, 5 slices = 146).
+// wavefront per slice, so the critical path is mb_w + 2 * (rows - 1) macroblocks; <= 8-row
+// slices keep it near mb_w at every size (one slice = 254 MB steps at 1080p, 9 slices = 134)
+// and let one workgroup hold a whole slice (k_intra_wave's LDS row hand-off).
 MXHD int idr_slice_rows(int mb_h) {
-    const int ns = (mb_h + 15) / 16;
+    const int ns = (mb_h + 7) / 8;  // <= 8 rows: one wave per row in k_intra_wave's workgroups
     return (mb_h + ns - 1) / ns;
 }
 
