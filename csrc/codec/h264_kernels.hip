@@ -1021,6 +1021,46 @@ __device__ __forceinline__ void had_row(const int* x, int r, int* y) {
     }
 }
 
+// The 4 prediction samples of row r of an Intra4x4 block: one switch on the mode per row
+// (the per-sample pred4x4_px switch, unrolled over the row, evaluated 4 mode switches with
+// the quads' different modes as divergent branch chains); same formulas, constant-folded.
+template <int M>
+__device__ __forceinline__ void pred4x4_row_m(const Nb4& n, int r, int* pv) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pv[c] = pred4x4_px(M, n, c, r);
+}
+__device__ __forceinline__ void pred4x4_row(int mode, const Nb4& n, int r, int* pv) {
+    switch (mode) {
+        case 0: pred4x4_row_m<0>(n, r, pv); break;
+        case 1: pred4x4_row_m<1>(n, r, pv); break;
+        case 2: pred4x4_row_m<2>(n, r, pv); break;
+        case 3: pred4x4_row_m<3>(n, r, pv); break;
+        case 4: pred4x4_row_m<4>(n, r, pv); break;
+        case 5: pred4x4_row_m<5>(n, r, pv); break;
+        case 6: pred4x4_row_m<6>(n, r, pv); break;
+        case 7: pred4x4_row_m<7>(n, r, pv); break;
+        default: pred4x4_row_m<8>(n, r, pv); break;
+    }
+}
+
+// Intra16x16 / chroma prediction of 4 samples of one row, the mode switch hoisted out of the row
+template <int M, bool C>
+__device__ __forceinline__ void predmb_row_m(const PredMb& p, const NbMb& n, int x0, int y, int* pv) {
+    PredMb q = p;
+    q.mode = M;  // constant mode: the helpers' switches fold
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pv[c] = C ? predc_px(q, n, x0 + c, y) : pred16_px(q, n, x0 + c, y);
+}
+template <bool C>
+__device__ __forceinline__ void predmb_row(const PredMb& p, const NbMb& n, int x0, int y, int* pv) {
+    switch (p.mode) {
+        case 0: predmb_row_m<0, C>(p, n, x0, y, pv); break;
+        case 1: predmb_row_m<1, C>(p, n, x0, y, pv); break;
+        case 2: predmb_row_m<2, C>(p, n, x0, y, pv); break;
+        default: predmb_row_m<3, C>(p, n, x0, y, pv); break;
+    }
+}
+
 // Closed-loop coding of one intra macroblock's luma, in the 4x4 "row" layout of
 // k_inter_encode (lane 4b + r = row r of block b): every transform pass is in-lane or a DPP
 // quad broadcast, the quantiser tables are scalar.  ls: the MB's source luma (16 rows x 4
@@ -1048,11 +1088,9 @@ __device__ void intra_luma_mb(const Geometry& g, const MbFields& f, const uint32
                 const int mode = f.i4(rb);
                 const uint32_t sw = ls[py * 4 + bx];
                 int pv[4], x[4], y[4], z[4], d[4], rr[4];
+                pred4x4_row(mode, n, r, pv);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    pv[c] = pred4x4_px(mode, n, c, r);
-                    x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
-                }
+                for (int c = 0; c < 4; ++c) x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
                 fdct_row(x, r, y);
                 nzb = quad_sum(quant_row_i(y, r, T, 0, z));
                 const int b = raster_to_blk(rb);
@@ -1081,11 +1119,9 @@ __device__ void intra_luma_mb(const Geometry& g, const MbFields& f, const uint32
         const int b = lane >> 2, bx = blk_x(b), by = blk_y(b), py = 4 * by + r;
         const uint32_t sw = ls[py * 4 + bx];
         int pv[4], x[4], y[4], z[4];
+        predmb_row<false>(p, n, 4 * bx, py, pv);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            pv[c] = pred16_px(p, n, 4 * bx + c, py);
-            x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
-        }
+        for (int c = 0; c < 4; ++c) x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
         fdct_row(x, r, y);
         if (r == 0) ldc[by * 4 + bx] = y[0];
         const int nz = quad_sum(quant_row_i(y, r, T, 1, z));
@@ -1153,10 +1189,10 @@ __device__ void intra_chroma_mb(const Geometry& g, int chroma_qp_offset, const M
         // samples 4bx .. 4bx+3 of this plane = bytes 8bx + 2c + comp of the interleaved row
         const uint32_t w0 = cs[py * 4 + 2 * bx], w1 = cs[py * 4 + 2 * bx + 1];
         int y[4];
+        predmb_row<true>(p, n, 4 * bx, py, pv);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const uint32_t w = c < 2 ? w0 : w1;
-            pv[c] = predc_px(p, n, 4 * bx + c, py);
             x[c] = (int)((w >> (8 * (2 * (c & 1) + comp))) & 0xff) - pv[c];
         }
         fdct_row(x, r, y);
