@@ -1285,6 +1285,9 @@ __device__ __forceinline__ void intra_wave_rows(const Geometry& g, const FrameSt
     };
     uint32_t nsrc = fetch_src(0);
     MbFields nf = load_fields(&mbs[mby * g.mb_w]);
+#ifdef MX_IDR_TIMING
+    const unsigned long long t_start = wall_clock64();
+#endif
     for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int mbi = mby * g.mb_w + mbx;
         MbInfo& m = mbs[mbi];
@@ -1349,6 +1352,10 @@ __device__ __forceinline__ void intra_wave_rows(const Geometry& g, const FrameSt
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (lane == 0) __hip_atomic_store(&prog[wave], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+#ifdef MX_IDR_TIMING
+    if (lane == 0 && blockIdx.x == 1)
+        printf("MXIDR plane %d row %d wall_ticks %llu\n", (int)chroma, wave, wall_clock64() - t_start);
+#endif
     // distortion of the row (one partial per row and channel)
     unsigned long long a = sse_a, b = sse_b, mm = sse_m;
     for (int o = 32; o > 0; o >>= 1) {
