@@ -1061,6 +1061,37 @@ __device__ __forceinline__ void predmb_row(const PredMb& p, const NbMb& n, int x
     }
 }
 
+// One Intra4x4 block on a quad (row r on this lane): predict from the tile, transform,
+// quantise, store the levels, reconstruct into the tile.  Returns the block's level count.
+__device__ __forceinline__ int i4_code_block(const Geometry& g, int rb, int r, int mode, const QpTab& T,
+                                             const uint32_t* ls, uint8_t (*lt)[kLT], int16_t* __restrict__ mc, int x0,
+                                             int y0, const Avail& av, uint32_t& sse) {
+    const uint8_t* tile = &lt[1][1];
+    const int bx = rb & 3, by = rb >> 2, py = 4 * by + r;
+    const Nb4 n = nb4_from_plane(tile, kLT, 0, 0, bx, by, av.left, av.top, av.topright, av.topleft);
+    const uint32_t sw = ls[py * 4 + bx];
+    int pv[4], x[4], y[4], z[4], d[4], rr[4];
+    pred4x4_row(mode, n, r, pv);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
+    fdct_row(x, r, y);
+    const int nzb = quad_sum(quant_row_i(y, r, T, 0, z));
+    const int b = raster_to_blk(rb);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) mc[kCoefLuma + b * 16 + zz_inv(r * 4 + c)] = (int16_t)z[c];
+    dequant_row_t(z, r, T, d);
+    idct_row(d, r, rr);
+    const bool vis = y0 + py < g.height;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int rec = clip255(pv[c] + rr[c]);
+        lt[1 + py][1 + 4 * bx + c] = (uint8_t)rec;
+        const int e = x[c] + pv[c] - rec;
+        sse += (vis && x0 + 4 * bx + c < g.width) ? (uint32_t)(e * e) : 0u;
+    }
+    return nzb;
+}
+
 // Closed-loop coding of one intra macroblock's luma, in the 4x4 "row" layout of
 // k_inter_encode (lane 4b + r = row r of block b): every transform pass is in-lane or a DPP
 // quad broadcast, the quantiser tables are scalar.  ls: the MB's source luma (16 rows x 4
@@ -1083,29 +1114,7 @@ __device__ void intra_luma_mb(const Geometry& g, const MbFields& f, const uint32
             const int rb = grp < 2 ? i4_step_block(t, grp) : -1;  // uniform per quad
             int nzb = 0;
             if (rb >= 0) {
-                const int bx = rb & 3, by = rb >> 2, py = 4 * by + r;
-                const Nb4 n = nb4_from_plane(tile, kLT, 0, 0, bx, by, av.left, av.top, av.topright, av.topleft);
-                const int mode = f.i4(rb);
-                const uint32_t sw = ls[py * 4 + bx];
-                int pv[4], x[4], y[4], z[4], d[4], rr[4];
-                pred4x4_row(mode, n, r, pv);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
-                fdct_row(x, r, y);
-                nzb = quad_sum(quant_row_i(y, r, T, 0, z));
-                const int b = raster_to_blk(rb);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) mc[kCoefLuma + b * 16 + zz_inv(r * 4 + c)] = (int16_t)z[c];
-                dequant_row_t(z, r, T, d);
-                idct_row(d, r, rr);
-                const bool vis = y0 + py < g.height;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int rec = clip255(pv[c] + rr[c]);
-                    lt[1 + py][1 + 4 * bx + c] = (uint8_t)rec;
-                    const int e = x[c] + pv[c] - rec;
-                    sse += (vis && x0 + 4 * bx + c < g.width) ? (uint32_t)(e * e) : 0u;
-                }
+                nzb = i4_code_block(g, rb, r, f.i4(rb), T, ls, lt, mc, x0, y0, av, sse);
                 if (r == 0) m.nz_luma[rb] = (uint8_t)nzb;
             }
             const unsigned long long any = __ballot(rb >= 0 && r == 0 && nzb > 0);
@@ -1353,8 +1362,8 @@ __device__ __forceinline__ void intra_wave_rows(const Geometry& g, const FrameSt
         if (lane == 0) __hip_atomic_store(&prog[wave], mbx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #ifdef MX_IDR_TIMING
-    if (lane == 0 && blockIdx.x == 1)
-        printf("MXIDR plane %d row %d wall_ticks %llu\n", (int)chroma, wave, wall_clock64() - t_start);
+    if (lane == 0)
+        printf("MXIDR plane %d slice %d row %d wall_ticks %llu\n", (int)chroma, (int)blockIdx.x, wave, wall_clock64() - t_start);
 #endif
     // distortion of the row (one partial per row and channel)
     unsigned long long a = sse_a, b = sse_b, mm = sse_m;
@@ -1374,17 +1383,190 @@ __device__ __forceinline__ void intra_wave_rows(const Geometry& g, const FrameSt
     }
 }
 
+// Luma rows with consecutive Intra4x4 macroblocks pipelined: block (bx, by) of the k-th MB of
+// a run of Intra4x4 MBs runs at step 4k + bx + 2by.  Its left neighbours (block (3, by) of
+// MB k-1, step 4k - 1 + 2by) and top-left are done a step earlier, and the predecessor copies
+// each finished right-column block into the successor's tile; so up to three MBs are in
+// flight (one quad pair each, lanes 8j .. 8j+7 for tile slot j = mbx % 3) and a run of n
+// such MBs takes 4n + 6 dependent steps instead of 10n.  Intra16x16 MBs (the whole MB's DC
+// transform couples all blocks) are coded alone between runs.  The IDR picture QP is
+// uniform (k_intra_analyze), so one quantiser table serves every MB in flight.
+struct LumaPipeTiles {
+    uint8_t lt[3][17][kLT];  // tile slot mbx % 3: row 0 = top neighbours, column 0 = left neighbours
+    uint32_t src[3][64];     // the slot MB's source (16 rows x 4 dwords)
+    int dc[16];              // Intra16x16 DC scratch
+};
+
+__device__ __forceinline__ void intra_luma_rows_pl(const Geometry& g, const FrameState* __restrict__ fs,
+                                                   const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs,
+                                                   int16_t* __restrict__ coef, uint8_t* s_line, LumaPipeTiles* tiles,
+                                                   int* prog) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slice_rows = fs->slice_rows;
+    uint8_t* const rec_y = fs->rec_y;
+    const int mby = blockIdx.x * slice_rows + wave;
+    if (mby >= g.mb_h) return;  // the last slice may be shorter (whole waves); no barriers below
+    LumaPipeTiles& P = tiles[wave];
+    uint8_t* my_line = s_line + (size_t)wave * g.coded_w;
+    const uint8_t* up_line = s_line + (size_t)(wave > 0 ? wave - 1 : 0) * g.coded_w;
+    const int y0 = mby * 16;
+    const QpTab T = qp_tab(fs->qp);
+    uint32_t sse_a = 0, sse_m = 0;
+    auto fetch_src = [&](int mbx) -> uint32_t {
+        if (mbx >= g.mb_w) return 0u;
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        return *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * g.pitch + mbx * 16 + c4);
+    };
+    uint32_t nsrc = fetch_src(0);
+    MbFields nf = load_fields(&mbs[mby * g.mb_w]);
+    // stage MB x into its slot: source, top neighbours (after the row above published them) and,
+    // if `left`, the left column from the completed previous MB's slot
+    auto stage = [&](int x, bool left) {
+        const int j = x % 3;
+        P.src[j][lane] = nsrc;
+        nsrc = fetch_src(x + 1);
+        const Avail av = mb_avail(g, x, mby, slice_rows);
+        if (av.top) {
+            const int need = av.topright ? x + 2 : x + 1;
+            while (__hip_atomic_load(&prog[wave - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+                __builtin_amdgcn_s_sleep(1);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        }
+        const bool need = lane < 21 && (lane == 0 ? av.topleft : (lane <= 16 ? av.top : av.topright));
+        const uint8_t top = need ? up_line[x * 16 - 1 + lane] : 0;
+        uint8_t lft = 0;
+        if (left && lane < 16 && av.left) lft = P.lt[(x + 2) % 3][1 + lane][16];
+        wave_sync_lds();
+        if (lane < 21) P.lt[j][0][lane] = top;
+        if (left && lane < 16) P.lt[j][1 + lane][0] = lft;
+        wave_sync_lds();
+    };
+    // MB x is complete: tile -> reconstruction, bottom line -> LDS, then publish it
+    auto finish = [&](int x) {
+        const int j = x % 3, x0 = x * 16;
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        const uint32_t v = (uint32_t)P.lt[j][1 + r][1 + c4] | ((uint32_t)P.lt[j][1 + r][2 + c4] << 8) |
+                           ((uint32_t)P.lt[j][1 + r][3 + c4] << 16) | ((uint32_t)P.lt[j][1 + r][4 + c4] << 24);
+        *reinterpret_cast<uint32_t*>(rec_y + (size_t)(y0 + r) * g.pitch + x0 + c4) = v;
+        if (r == 15) *reinterpret_cast<uint32_t*>(my_line + x0 + c4) = v;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // LDS completes the line stores before the counter
+        if (lane == 0) __hip_atomic_store(&prog[wave], x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#ifdef MX_IDR_TIMING
+    const unsigned long long t_start = wall_clock64();
+#endif
+    int next = 0;  // next MB to start
+    while (next < g.mb_w) {
+        if (nf.type != kMbI4x4) {  // Intra16x16: alone
+            const int x = next;
+            const MbFields f = nf;
+            nf = load_fields(&mbs[mby * g.mb_w + (x + 1 < g.mb_w ? x + 1 : x)]);
+            stage(x, true);
+            const int j = x % 3, mbi = mby * g.mb_w + x;
+            uint32_t sse_mb = 0;
+            intra_luma_mb(g, f, P.src[j], mbs[mbi], coef + (size_t)mbi * kCoefStride, x, mby,
+                          mb_avail(g, x, mby, slice_rows), P.lt[j], P.dc, lane, sse_mb);
+            sse_a += sse_mb;
+            if (mb_unmasked(fs, x, mby)) sse_m += sse_mb;
+            finish(x);
+            ++next;
+            continue;
+        }
+        // a run of Intra4x4 MBs from `base`; MB base + k starts at step 4k while the run lasts
+        const int base = next;
+        int started = 0;
+        bool open = true;
+        uint32_t mlo[3] = {0, 0, 0}, mhi[3] = {0, 0, 0};  // Intra4x4 modes per slot (uniform)
+        int cbp[3] = {0, 0, 0};
+        for (int t = 0;; ++t) {
+            if ((t & 3) == 0 && open) {
+                if (base + started < g.mb_w && nf.type == kMbI4x4) {
+                    const int x = base + started, j = x % 3;
+                    const MbFields f = nf;
+                    nf = load_fields(&mbs[mby * g.mb_w + (x + 1 < g.mb_w ? x + 1 : x)]);
+#pragma unroll
+                    for (int s = 0; s < 3; ++s)
+                        if (s == j) {
+                            mlo[s] = f.i4lo;
+                            mhi[s] = f.i4hi;
+                            cbp[s] = 0;
+                        }
+                    stage(x, started == 0);  // later MBs get their left column from the predecessor
+                    ++started;
+                } else {
+                    open = false;
+                }
+            }
+            if (!open && t > 4 * (started - 1) + 9) break;
+            // this lane's MB (slot j = lane / 8, quad group grp) and its local step
+            const int j = lane >> 3, grp = (lane >> 2) & 1, r = lane & 3;
+            const int kk = t >> 2;
+            const int k = kk - (kk + base - j + 3) % 3;
+            const int sl = t - 4 * k;
+            const bool mine = lane < 24 && k >= 0 && k < started && sl <= 9;
+            const int rb = mine ? i4_step_block(sl, grp) : -1;  // uniform per quad
+            int nzb = 0;
+            if (rb >= 0) {
+                const int x = base + k, mbi = mby * g.mb_w + x;
+                const uint32_t lo = j == 0 ? mlo[0] : (j == 1 ? mlo[1] : mlo[2]);
+                const uint32_t hi = j == 0 ? mhi[0] : (j == 1 ? mhi[1] : mhi[2]);
+                const int mode = (int)(((rb < 8 ? lo : hi) >> (4 * (rb & 7))) & 15u);
+                uint32_t e2 = 0;
+                nzb = i4_code_block(g, rb, r, mode, T, P.src[j], P.lt[j], coef + (size_t)mbi * kCoefStride, x * 16, y0,
+                                    mb_avail(g, x, mby, slice_rows), e2);
+                sse_a += e2;
+                if (mb_unmasked(fs, x, mby)) sse_m += e2;
+                if (r == 0) mbs[mbi].nz_luma[rb] = (uint8_t)nzb;
+            }
+            const unsigned long long any = __ballot(rb >= 0 && r == 0 && nzb > 0);
+            wave_sync_lds();
+            // per slot (uniform): coded-block bits, right-column hand-off, completion
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                const int ks = kk - (kk + base - s + 3) % 3, ss = t - 4 * ks;
+                if (ks < 0 || ks >= started || ss > 9) continue;
+#pragma unroll
+                for (int gq = 0; gq < 2; ++gq)
+                    if ((any >> (8 * s + 4 * gq)) & 1ull) cbp[s] |= 1 << (raster_to_blk(i4_step_block(ss, gq)) >> 2);
+                if (ss >= 3 && (ss & 1)) {  // block (3, by) done: successor's left column rows 4by .. 4by+3
+                    const int by = (ss - 3) >> 1, jn = (base + ks + 1) % 3;
+                    if (lane < 4) P.lt[jn][1 + 4 * by + lane][0] = P.lt[s][1 + 4 * by + lane][16];
+                }
+                if (ss == 9) {
+                    if (lane == 0) mbs[mby * g.mb_w + base + ks].cbp = (uint8_t)cbp[s];
+                    finish(base + ks);
+                }
+            }
+            wave_sync_lds();
+        }
+        next = base + started;
+    }
+#ifdef MX_IDR_TIMING
+    if (lane == 0) printf("MXIDR plane 0 slice %d row %d wall_ticks %llu\n", (int)blockIdx.x, wave, wall_clock64() - t_start);
+#endif
+    unsigned long long a = sse_a, mm = sse_m;
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        mm += __shfl_xor(mm, o, 64);
+    }
+    if (lane == 0) {
+        fs->sse_part[0 * kSsePartStride + mby] = a;
+        fs->sse_part[3 * kSsePartStride + mby] = mm;
+    }
+}
+
 __global__ __launch_bounds__(512) void k_intra_wave(Geometry g, const FrameState* __restrict__ fs,
                                                      const uint8_t* __restrict__ src_y,
                                                      const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
                                                      int16_t* __restrict__ coef) {
     extern __shared__ uint8_t s_line[];  // [slice rows][coded_w]: bottom sample line of every coded MB
-    __shared__ IntraWaveTiles tiles[8];
+    __shared__ IntraWaveTiles tiles[8];     // chroma workgroups
+    __shared__ LumaPipeTiles ltiles[8];     // luma workgroups
     __shared__ int prog[8];              // macroblocks of the row whose bottom line is in s_line
     if ((threadIdx.x & 63) == 0) prog[threadIdx.x >> 6] = 0;
     __syncthreads();
     if (blockIdx.y == 0)
-        intra_wave_rows<false>(g, fs, src_y, src_uv, mbs, coef, s_line, tiles, prog);
+        intra_luma_rows_pl(g, fs, src_y, mbs, coef, s_line, ltiles, prog);
     else
         intra_wave_rows<true>(g, fs, src_y, src_uv, mbs, coef, s_line, tiles, prog);
 }
@@ -2128,7 +2310,8 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
     static bool attr_set = false;  // line buffers above the default dynamic-LDS limit (8K: 61 KB + tiles)
     if (!attr_set) {
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_intra_wave),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)sizeof(IntraWaveTiles) * 8 - 32));
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024 - (int)(sizeof(IntraWaveTiles) + sizeof(LumaPipeTiles)) * 8 - 32));
         attr_set = true;
     }
     hipLaunchKernelGGL(k_intra_wave, dim3(slices, 2), dim3(64 * rows), lds, stream, g, b.fs, src_y, src_uv, b.mb,

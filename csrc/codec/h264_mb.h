@@ -207,11 +207,13 @@ MXHD uint32_t inter_cost(uint32_t satd, int frame_qp, int mvx, int mvy) {
 }
 
 // Rows per slice of an IDR picture: intra macroblocks are reconstructed in a diagonal
-// wavefront per slice, so the critical path is mb_w + 2 * (rows - 1) macroblocks; <= 8-row
-// slices keep it near mb_w at every size (one slice = 254 MB steps at 1080p, 9 slices = 134)
-// and let one workgroup hold a whole slice (k_intra_wave's LDS row hand-off).
+// wavefront per slice (one workgroup per slice, one wave per row, k_intra_wave), so a slice
+// takes about as long as its most expensive MB row plus a 2-MB lag per row.  <= 4-row slices
+// (17 at 1080p) keep one row wave per SIMD and spread the text-heavy rows over more
+// workgroups: 1,059 -> 914 us per 1080p IDR against 8-row slices for +0.7 % IDR bytes
+// (profiles/r02_idr).
 MXHD int idr_slice_rows(int mb_h) {
-    const int ns = (mb_h + 7) / 8;  // <= 8 rows: one wave per row in k_intra_wave's workgroups
+    const int ns = (mb_h + 3) / 4;  // <= 4 rows
     return (mb_h + ns - 1) / ns;
 }
 

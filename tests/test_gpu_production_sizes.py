@@ -72,10 +72,10 @@ def _encode_both(gpu, w, h, frames, kbps, search_range=16):
 
 def test_1080p_bit_exact_and_idr_slices_decode(gpu):
     aus, recons, genc = _encode_both(gpu, 1920, 1080, 3, 8000)
-    # the IDR is 9 slices of 8/4 MB rows: decode the first and the last independently
+    # the IDR is 17 slices of 4 MB rows: decode the first and the last independently
     nals = raw_nals(aus[0])
     slices = [n for n in nals if (n[0] & 0x1F) == 5]
-    assert len(slices) == 9, len(slices)
+    assert len(slices) == 17, len(slices)
     params = [n for n in nals if (n[0] & 0x1F) in (7, 8)]
     sc = b"\x00\x00\x00\x01"
     dec = Decoder()
@@ -83,9 +83,9 @@ def test_1080p_bit_exact_and_idr_slices_decode(gpu):
     dec.decode(b"".join(sc + n for n in params + [slices[0], slices[-1]]))
     y_dec = dec.frames_coded[0][0]
     y_rec = recons[0][0]
-    rows = 8 * 16
+    rows = 4 * 16
     assert np.array_equal(y_dec[:rows], y_rec[:rows]), "first IDR slice"
-    last0 = 8 * 8 * 16
+    last0 = 16 * 4 * 16
     assert np.array_equal(y_dec[last0:1088], y_rec[last0:1088]), "last IDR slice"
     d = Decoder()
     d.allow_partial = True
@@ -94,9 +94,9 @@ def test_1080p_bit_exact_and_idr_slices_decode(gpu):
 
 
 def test_4k_bit_exact_multi_tile_scan(gpu):
-    # 240 x 135 = 32400 MBs: four k_scan tiles; IDR of 17 slices (8 MB rows)
+    # 240 x 135 = 32400 MBs: four k_scan tiles; IDR of 34 slices (4 MB rows)
     aus, _, _ = _encode_both(gpu, 3840, 2160, 2, 25000, search_range=8)
-    assert sum((n[0] & 0x1F) == 5 for n in raw_nals(aus[0])) == 17
+    assert sum((n[0] & 0x1F) == 5 for n in raw_nals(aus[0])) == 34
 
 
 def test_8k_bit_exact(gpu):
