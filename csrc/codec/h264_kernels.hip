@@ -1478,18 +1478,23 @@ __device__ __forceinline__ void intra_luma_rows_pl(const Geometry& g, const Fram
         bool open = true;
         uint32_t mlo[3] = {0, 0, 0}, mhi[3] = {0, 0, 0};  // Intra4x4 modes per slot (uniform)
         int cbp[3] = {0, 0, 0};
+        int sk[3] = {-16, -16, -16};      // run index k of the MB in each slot (uniform)
+        bool um[3] = {false, false, false};  // the slot MB counts towards the masked PSNR
         for (int t = 0;; ++t) {
             if ((t & 3) == 0 && open) {
                 if (base + started < g.mb_w && nf.type == kMbI4x4) {
                     const int x = base + started, j = x % 3;
                     const MbFields f = nf;
                     nf = load_fields(&mbs[mby * g.mb_w + (x + 1 < g.mb_w ? x + 1 : x)]);
+                    const bool unm = mb_unmasked(fs, x, mby);
 #pragma unroll
                     for (int s = 0; s < 3; ++s)
                         if (s == j) {
                             mlo[s] = f.i4lo;
                             mhi[s] = f.i4hi;
                             cbp[s] = 0;
+                            sk[s] = started;
+                            um[s] = unm;
                         }
                     stage(x, started == 0);  // later MBs get their left column from the predecessor
                     ++started;
@@ -1500,10 +1505,9 @@ __device__ __forceinline__ void intra_luma_rows_pl(const Geometry& g, const Fram
             if (!open && t > 4 * (started - 1) + 9) break;
             // this lane's MB (slot j = lane / 8, quad group grp) and its local step
             const int j = lane >> 3, grp = (lane >> 2) & 1, r = lane & 3;
-            const int kk = t >> 2;
-            const int k = kk - (kk + base - j + 3) % 3;
+            const int k = j == 0 ? sk[0] : (j == 1 ? sk[1] : sk[2]);
             const int sl = t - 4 * k;
-            const bool mine = lane < 24 && k >= 0 && k < started && sl <= 9;
+            const bool mine = lane < 24 && k >= 0 && sl <= 9;
             const int rb = mine ? i4_step_block(sl, grp) : -1;  // uniform per quad
             int nzb = 0;
             if (rb >= 0) {
@@ -1515,7 +1519,7 @@ __device__ __forceinline__ void intra_luma_rows_pl(const Geometry& g, const Fram
                 nzb = i4_code_block(g, rb, r, mode, T, P.src[j], P.lt[j], coef + (size_t)mbi * kCoefStride, x * 16, y0,
                                     mb_avail(g, x, mby, slice_rows), e2);
                 sse_a += e2;
-                if (mb_unmasked(fs, x, mby)) sse_m += e2;
+                if (j == 0 ? um[0] : (j == 1 ? um[1] : um[2])) sse_m += e2;
                 if (r == 0) mbs[mbi].nz_luma[rb] = (uint8_t)nzb;
             }
             const unsigned long long any = __ballot(rb >= 0 && r == 0 && nzb > 0);
@@ -1523,13 +1527,13 @@ __device__ __forceinline__ void intra_luma_rows_pl(const Geometry& g, const Fram
             // per slot (uniform): coded-block bits, right-column hand-off, completion
 #pragma unroll
             for (int s = 0; s < 3; ++s) {
-                const int ks = kk - (kk + base - s + 3) % 3, ss = t - 4 * ks;
-                if (ks < 0 || ks >= started || ss > 9) continue;
+                const int ks = sk[s], ss = t - 4 * ks;
+                if (ks < 0 || ss > 9) continue;
 #pragma unroll
                 for (int gq = 0; gq < 2; ++gq)
                     if ((any >> (8 * s + 4 * gq)) & 1ull) cbp[s] |= 1 << (raster_to_blk(i4_step_block(ss, gq)) >> 2);
                 if (ss >= 3 && (ss & 1)) {  // block (3, by) done: successor's left column rows 4by .. 4by+3
-                    const int by = (ss - 3) >> 1, jn = (base + ks + 1) % 3;
+                    const int by = (ss - 3) >> 1, jn = s == 2 ? 0 : s + 1;  // slot of MB base + ks + 1
                     if (lane < 4) P.lt[jn][1 + 4 * by + lane][0] = P.lt[s][1 + 4 * by + lane][16];
                 }
                 if (ss == 9) {
