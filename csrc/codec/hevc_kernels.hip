@@ -687,6 +687,34 @@ __device__ __forceinline__ int pred_sample(int mode, int log2n, bool luma, const
     return (luma && y == 0) ? clip255(L[1] + ((T[1 + x] - T[0]) >> 1)) : L[1 + y];  // mode 10
 }
 
+// Reference sample i (0 .. 4N, the spec's search order from p[-1][2N-1] up to the corner and
+// right to p[2N-1][-1]) after 8.4.4.2.2 substitution, in closed form over the five segments
+// (bottom-left, left, corner, top, top-right; bit s of avl = segment s available): an
+// unavailable segment takes the last sample of the nearest available segment before it, or,
+// when none precedes, the first sample of the first available one; none available: 128.
+__device__ __forceinline__ int ref_subst(int i, int N, int avl, const uint8_t* lpx, const uint8_t* tpx,
+                                         const uint8_t* trx, int corner) {
+    if (avl == 0) return 128;
+    const int n2 = 2 * N;
+    const int seg = i < N ? 0 : (i < n2 ? 1 : (i == n2 ? 2 : (i <= 3 * N ? 3 : 4)));
+    int j = i;
+    if (!((avl >> seg) & 1)) {
+        const int below = avl & ((1 << seg) - 1);
+        if (below) {
+            const int p = 31 - __clz(below);  // last sample of segment p
+            j = p == 0 ? N - 1 : (p == 1 ? n2 - 1 : (p == 2 ? n2 : (p == 3 ? 3 * N : 4 * N)));
+        } else {
+            const int f = __ffs(avl) - 1;  // first sample of segment f
+            j = f == 0 ? 0 : (f == 1 ? N : (f == 2 ? n2 : (f == 3 ? n2 + 1 : 3 * N + 1)));
+        }
+    }
+    // j lies in an available segment (never the bottom-left here)
+    if (j < n2) return lpx[n2 - 1 - j];
+    if (j == n2) return corner;
+    if (j <= 3 * N) return tpx[j - n2 - 1];
+    return trx[j - 3 * N - 1];
+}
+
 __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, const HevcFrameState* __restrict__ fs,
                                                       const uint8_t* __restrict__ src_y,
                                                       const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
@@ -741,27 +769,48 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             }
         }
         __syncthreads();
-        // ---- reference substitution + planar filter (lane 0 luma, lanes 1/2 chroma)
-        if (valid && lane < 3) {
-            if (lane == 0) {
-                intra_refs(16, al, false, at, atr, ac, R.lpx, R.lpx, R.tpx, R.trx, R.corner, R.L, R.T);
-                R.LF[0] = R.TF[0] = (R.L[1] + 2 * R.L[0] + R.T[1] + 2) >> 2;
-                for (int k = 1; k < 32; ++k) {
+        // ---- reference substitution (8.4.4.2.2) for every sample at once, then the planar
+        // filter and DC sums; the same values as intra_refs() + the lane-serial loops this
+        // replaced (their availability/pointer lambdas lived in scratch: two dependent memory
+        // round trips per reference sample on the wavefront's critical path)
+        if (valid) {
+            const int avl = (al ? 2 : 0) | (ac ? 4 : 0) | (at ? 8 : 0) | (atr ? 16 : 0);  // no bottom-left
+            for (int i = lane; i <= 64; i += 64) {
+                const int v = ref_subst(i, 16, avl, R.lpx, R.tpx, R.trx, R.corner);
+                if (i < 32) R.L[32 - i] = v;
+                else if (i == 32) R.L[0] = R.T[0] = v;
+                else R.T[i - 32] = v;
+            }
+            for (int k = lane; k < 66; k += 64) {
+                const int comp = k >= 33 ? 1 : 0, i = k - 33 * comp;
+                const int v = ref_subst(i, 8, avl, R.lc[comp], R.tc[comp], R.trc[comp], R.corner_c[comp]);
+                if (i < 16) R.Lc[comp][16 - i] = v;
+                else if (i == 16) R.Lc[comp][0] = R.Tc[comp][0] = v;
+                else R.Tc[comp][i - 16] = v;
+            }
+        }
+        __syncthreads();
+        if (valid) {
+            if (lane <= 32) {
+                const int k = lane;
+                if (k == 0) {
+                    R.LF[0] = R.TF[0] = (R.L[1] + 2 * R.L[0] + R.T[1] + 2) >> 2;
+                } else if (k == 32) {
+                    R.LF[32] = R.L[32];
+                    R.TF[32] = R.T[32];
+                } else {
                     R.LF[k] = (R.L[k + 1] + 2 * R.L[k] + R.L[k - 1] + 2) >> 2;
                     R.TF[k] = (R.T[k + 1] + 2 * R.T[k] + R.T[k - 1] + 2) >> 2;
                 }
-                R.LF[32] = R.L[32];
-                R.TF[32] = R.T[32];
-                int s = 16;
-                for (int k = 1; k <= 16; ++k) s += R.L[k] + R.T[k];
-                R.dc = s >> 5;
-            } else {
-                const int comp = lane - 1;
-                intra_refs(8, al, false, at, atr, ac, R.lc[comp], R.lc[comp], R.tc[comp], R.trc[comp],
-                           R.corner_c[comp], R.Lc[comp], R.Tc[comp]);
-                int s = 8;
-                for (int k = 1; k <= 8; ++k) s += R.Lc[comp][k] + R.Tc[comp][k];
-                R.dcc[comp] = s >> 4;
+            }
+            const int sl = lane < 16 ? R.L[1 + lane] + R.T[1 + lane] : 0;
+            const int c0 = (lane >= 16 && lane < 24) ? R.Lc[0][lane - 15] + R.Tc[0][lane - 15] : 0;
+            const int c1 = (lane >= 24 && lane < 32) ? R.Lc[1][lane - 23] + R.Tc[1][lane - 23] : 0;
+            const int s_l = wsum(sl), s_c0 = wsum(c0), s_c1 = wsum(c1);
+            if (lane == 0) {
+                R.dc = (s_l + 16) >> 5;
+                R.dcc[0] = (s_c0 + 8) >> 4;
+                R.dcc[1] = (s_c1 + 8) >> 4;
             }
         }
         __syncthreads();
