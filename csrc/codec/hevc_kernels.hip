@@ -746,10 +746,22 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     IntraRefs& R = rf[wave];
     unsigned long long acc[3] = {0, 0, 0};
     const int steps = g.mb_w + 2 * (sr - 1);
+    // this lane's source samples of the CTU, loaded a step ahead (off the critical path):
+    // luma row lane / 4, columns 4 (lane % 4) .. +3; chroma row lane / 8, Cb/Cr pair lane % 8
+    auto load_src = [&](int xx, uint32_t& ly, uint32_t& lc) {
+        if (!row_ok || xx < 0 || xx >= g.mb_w) return;
+        const int r = lane >> 2, cb = (lane & 3) * 4, rc = lane >> 3, cc = lane & 7;
+        ly = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y * 16 + r) * g.pitch + xx * 16 + cb);
+        lc = *reinterpret_cast<const uint16_t*>(src_uv + (size_t)(y * 8 + rc) * g.pitch + xx * 16 + 2 * cc);
+    };
+    uint32_t nsy = 0, nsc = 0;
+    load_src(-2 * wave, nsy, nsc);
     for (int step = 0; step < steps; ++step) {
         const int x = step - 2 * wave;
         const bool valid = row_ok && x >= 0 && x < g.mb_w;
         const int x0 = x * 16, y0 = y * 16;
+        const uint32_t sy4 = nsy, sc2 = nsc;
+        load_src(x + 1, nsy, nsc);
         const bool al = x > 0, at = wave > 0, atr = at && x + 1 < g.mb_w, ac = at && x > 0;
         // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
         if (valid) {
@@ -824,7 +836,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 int sad = 0;
                 for (int j = 0; j < 4; ++j) {
                     const int p = pred_sample(md, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
-                    const int d = (int)src_y[(size_t)(y0 + r) * g.pitch + x0 + cb + j] - p;
+                    const int d = (int)((sy4 >> (8 * j)) & 0xff) - p;
                     sad += d < 0 ? -d : d;
                 }
                 sad = wsum(sad);
@@ -841,15 +853,14 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             for (int j = 0; j < 4; ++j) {
                 const int p = pred_sample(mode, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
                 t.pred[r * 16 + cb + j] = (uint8_t)p;
-                t.res[r * 16 + cb + j] = (int16_t)((int)src_y[(size_t)(y0 + r) * g.pitch + x0 + cb + j] - p);
+                t.res[r * 16 + cb + j] = (int16_t)((int)((sy4 >> (8 * j)) & 0xff) - p);
             }
             const int rc = lane >> 3, cc = lane & 7;
             for (int comp = 0; comp < 2; ++comp) {
                 const int p = pred_sample(mode, 3, false, R.Lc[comp], R.Tc[comp], R.Lc[comp], R.Tc[comp], R.dcc[comp],
                                           cc, rc);
                 t.pred[256 + comp * 64 + rc * 8 + cc] = (uint8_t)p;
-                t.res[256 + comp * 64 + rc * 8 + cc] =
-                    (int16_t)((int)src_uv[(size_t)(y0 / 2 + rc) * g.pitch + x0 + 2 * cc + comp] - p);
+                t.res[256 + comp * 64 + rc * 8 + cc] = (int16_t)((int)((sc2 >> (8 * comp)) & 0xff) - p);
             }
         }
         __syncthreads();
