@@ -81,8 +81,15 @@ struct OrWriter {
     }
 };
 
+// Wave sum, every lane gets it (whole wave active): quad and row-of-16 sums with DPP
+// (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8), the four rows with two lane shuffles.
 __device__ __forceinline__ int wave_sum(int v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
     return v;
 }
 
