@@ -816,16 +816,16 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
         int t[4] = {d0 + d1 + d2 + d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3, d0 - d1 + d2 - d3};
         uint32_t sum = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4; ++j) {  // column butterflies over the quad: DPP quad_perm xor 1 / xor 2
             int v = t[j];
-            int o = __shfl_xor(v, 1, 64);
+            int o = __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
             v = (r & 1) ? o - v : v + o;
-            o = __shfl_xor(v, 2, 64);
+            o = __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
             v = (r & 2) ? o - v : v + o;
             sum += (uint32_t)(v < 0 ? -v : v);
         }
-        sum += __shfl_xor(sum, 1, 64);
-        sum += __shfl_xor(sum, 2, 64);
+        sum += (uint32_t)__builtin_amdgcn_mov_dpp((int)sum, 0xB1, 0xF, 0xF, false);
+        sum += (uint32_t)__builtin_amdgcn_mov_dpp((int)sum, 0x4E, 0xF, 0xF, false);
         return (sum + 1) >> 1;  // satd of the block, in all 4 lanes
     };
     {
@@ -855,7 +855,10 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
                     d[j] = (int)sy[(4 * by + r) * kLT + 4 * bx + j] - pred16_px(p, n, 4 * bx + j, 4 * by + r);
                 t = satd_quad(d[0], d[1], d[2], d[3]);
                 t = r == 0 ? t : 0u;
-                for (int o = 4; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+                t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x124, 0xF, 0xF, false);  // lanes l ^ 4, 8, 12
+                t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x128, 0xF, 0xF, false);
+                t += __shfl_xor(t, 16, 64);
+                t += __shfl_xor(t, 32, 64);
             }
             if (lane == 0) c.c16[m] = ok ? t : kCostInf;
         }
@@ -876,7 +879,10 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
                                      : 0;
                 t = satd_quad(d[0], d[1], d[2], d[3]);
                 t = (r == 0 && lane < 32) ? t : 0u;
-                for (int o = 4; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+                t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x124, 0xF, 0xF, false);  // lanes l ^ 4, 8, 12
+                t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x128, 0xF, 0xF, false);
+                t += __shfl_xor(t, 16, 64);
+                t += __shfl_xor(t, 32, 64);
             }
             if (lane == 0) c.cc[m] = ok ? t : kCostInf;
         }
