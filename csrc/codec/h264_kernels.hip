@@ -1817,11 +1817,14 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
         bits = w.bits;
     }
     // exclusive prefix sum of bits over the half's lanes -> role offsets in the MB slot
+    // (DPP: shift-add scan within rows of 16, then row_bcast:15 into the odd rows -- rows 0-1 and
+    // 2-3 are the two halves -- instead of five lane-shuffle round trips)
     uint32_t incl = bits;
-    for (int o = 1; o < 32; o <<= 1) {
-        uint32_t v = __shfl_up(incl, o, 32);
-        if (lane >= o) incl += v;
-    }
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xF, 0xF, false);  // row_shr:1
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xF, 0xF, false);  // row_shr:2
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xF, 0xF, false);  // row_shr:4
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xF, 0xF, false);  // row_shr:8
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x142, 0xA, 0xF, false);  // row_bcast:15
     const uint32_t total = __shfl(incl, 31, 32);
     if (lane < kNumRoles) roff[wave][lane] = incl - bits;
     if (lane == kNumRoles) roff[wave][kNumRoles] = total;
