@@ -533,13 +533,13 @@ PYBIND11_MODULE(_native, m) {
              py::arg("addr"), py::arg("nbytes"))
         .def(
             "submit_bgrx_ptr",
-            [](Session& s, uintptr_t addr, int pitch, bool force_idr) {
-                if (pitch < s.config().width * 4) throw std::invalid_argument("pitch < width * 4");
+            [](Session& s, uintptr_t addr, int pitch, size_t nbytes, bool force_idr) {
                 py::gil_scoped_release rel;
-                s.submit_bgrx(as_ptr<const uint8_t>(addr), pitch, force_idr);
+                s.submit_bgrx_span(as_ptr<const uint8_t>(addr), pitch, nbytes, force_idr);
             },
-            py::arg("addr"), py::arg("pitch"), py::arg("force_idr") = false,
-            "BGRx frame at a host address (zero-copy when inside a registered buffer)")
+            py::arg("addr"), py::arg("pitch"), py::arg("nbytes"), py::arg("force_idr") = false,
+            "BGRx frame at a host address with `nbytes` readable (zero-copy inside a registered buffer; "
+            "ValueError if the frame does not fit)")
         .def("collect",
              [](Session& s) {
                  py::gil_scoped_release rel;

@@ -260,8 +260,6 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.mb_sse, sizeof(uint32_t) * 3 * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.intra_gain, sizeof(int32_t) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.intra_cand, sizeof(int) * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.wave_line, sizeof(uint64_t) * (size_t)geom_.mb_h * geom_.coded_w / 2));
-    HIP_CHECK(hipMemsetAsync(b.wave_line, 0, sizeof(uint64_t) * (size_t)geom_.mb_h * geom_.coded_w / 2, stream_));
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
     std::memset(sl.host_out, 0, kOutPayloadOffset);
@@ -274,7 +272,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     DeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.row_agg,
                     (void*)b.row_sse, (void*)b.coded_info, (void*)b.slice_info,
-                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.wave_line, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit})
+                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);
@@ -384,7 +382,6 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.hp_pitch = hp_pitch_;
     f.aq = cfg_.aq;
     f.intra_in_p = cfg_.intra_in_p;
-    f.frame_tag = (int32_t)++frame_tag_;  // tags start at 1: the zeroed line buffer never matches
     f.mask_mx0 = mask_mb_[0];
     f.mask_my0 = mask_mb_[1];
     f.mask_mx1 = mask_mb_[2];

@@ -224,7 +224,6 @@ class GpuH264Encoder final : public VideoEncoder {
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
-    uint32_t frame_tag_ = 0;
     int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
     int64_t masked_pixels_ = 0;
     std::vector<uint8_t> au_;

@@ -79,7 +79,6 @@ struct FrameState {
     int32_t hp_pitch;  // pitch of the padded half-pel planes
     int32_t aq;        // adaptive quantisation on/off (P frames)
     int32_t intra_in_p;  // P frames: k_intra_analyze / k_intra_wave run (distortion deltas included)
-    int32_t frame_tag;   // nonzero, new every frame: validity tag of k_intra_wave's line buffer words
     // quality report: MBs in [mask_mx0, mask_mx1) x [mask_my0, mask_my1) are left out of the 4th
     // distortion channel (e.g. the synthetic desktop's noise panel); empty rect = no mask
     int32_t mask_mx0, mask_my0, mask_mx1, mask_my1;
@@ -135,8 +134,7 @@ struct DeviceBuffers {
     size_t out_bytes;       // payload capacity of the host output buffer
     OutHeader* out_hdr;     // device header
     unsigned long long* sse_part;       // [4 * kSsePartStride] distortion partials
-    int* wave_prog;         // [0] k_intra_wave row ticket, [1] intra candidate count
-    uint64_t* wave_line;    // [mb_h * coded_w / 2] k_intra_wave: tagged bottom sample lines of intra MBs
+    int* wave_prog;         // [1] intra candidate count of P pictures ([0] unused)
     int32_t* intra_gain;    // [nmb] P frames: gain of switching each MB to intra (0 = stays inter)
     int* intra_cand;        // [nmb] P frames: MBs with a positive gain (count in wave_prog[1])
     uint32_t* mb_sse;       // [3 * nmb] P frames: per-MB inter distortion (replaced for intra MBs)

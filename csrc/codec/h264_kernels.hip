@@ -780,7 +780,6 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
     publish_state(sa);
     const FrameState* fs = &state_of(sa);
     if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) wave_prog[0] = 0;  // k_intra_wave's row ticket
         if (!fs->idr)  // k_intra_p's per-row distortion deltas (atomically accumulated)
             for (int i = threadIdx.x; i < 4 * g.mb_h; i += 256)
                 fs->sse_part[(i / g.mb_h) * kSsePartStride + (g.mb_w * g.mb_h + 3) / 4 + i % g.mb_h] = 0;
@@ -2327,13 +2326,9 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
     // one workgroup per (slice, plane), one wave per slice row; LDS line buffers of the rows
     const int rows = idr_slice_rows(g.mb_h), slices = (g.mb_h + rows - 1) / rows;
     const size_t lds = (size_t)rows * g.coded_w;
-    static bool attr_set = false;  // line buffers above the default dynamic-LDS limit (8K: 61 KB + tiles)
-    if (!attr_set) {
-        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_intra_wave),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024 - (int)(sizeof(IntraWaveTiles) + sizeof(LumaPipeTiles)) * 8 - 32));
-        attr_set = true;
-    }
+    // line buffers above the default dynamic-LDS limit (8K: 61 KB + tiles); per device, once
+    ensure_func_attr(reinterpret_cast<const void*>(&k_intra_wave), hipFuncAttributeMaxDynamicSharedMemorySize,
+                     160 * 1024 - (int)(sizeof(IntraWaveTiles) + sizeof(LumaPipeTiles)) * 8 - 32);
     hipLaunchKernelGGL(k_intra_wave, dim3(slices, 2), dim3(64 * rows), lds, stream, g, b.fs, src_y, src_uv, b.mb,
                        b.coef);
     hipLaunchKernelGGL(k_intra_cbp, dim3((g.mb_w * g.mb_h + 255) / 256), dim3(256), 0, stream, g, b.mb);

@@ -13,3 +13,24 @@
             throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " +   \
                                      __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);        \
     } while (0)
+
+#include <mutex>
+#include <set>
+#include <tuple>
+
+namespace mx {
+// Function attributes (e.g. the dynamic-LDS limit) are per device: raise one once for every
+// (device, kernel, attribute, value), thread-safe -- sessions of one process run on several
+// host threads (run_sessions) and a process may drive more than one GPU.
+inline void ensure_func_attr(const void* fn, hipFuncAttribute attr, int value) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    static std::mutex mu;
+    static std::set<std::tuple<int, const void*, int, int>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(dev, fn, (int)attr, value);
+    if (done.count(key)) return;
+    HIP_CHECK(hipFuncSetAttribute(fn, attr, value));
+    done.insert(key);
+}
+}  // namespace mx

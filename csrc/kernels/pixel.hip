@@ -16,6 +16,7 @@
 #include <stdexcept>
 
 #include "pixel.h"
+#include "../common/hip_check.h"
 
 namespace mx {
 namespace pix {
@@ -927,12 +928,8 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     if (t.mf.gx && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 && in_w >= 4) {
         const size_t lds = (size_t)2 * 32 * t.mf.lds_cols * 4;
         if (lds > 64 * 1024) {
-            static bool raised = false;
-            if (!raised) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scale_mfma),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                raised = true;
-            }
+            ensure_func_attr(reinterpret_cast<const void*>(&k_scale_mfma),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         }
         dim3 grid((coded_w + 63) / 64, (coded_h + 31) / 32);
         hipLaunchKernelGGL(k_scale_mfma, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv,
@@ -950,12 +947,8 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     const int vec = ((in_pitch & 15) == 0 && (reinterpret_cast<uintptr_t>(bgrx) & 15) == 0) ? 1 : 0;
     if (lds > 160 * 1024) throw std::runtime_error("scale_to_nv12: scale factor too large for one LDS tile");
     if (lds > 64 * 1024) {
-        static bool raised = false;
-        if (!raised) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scale_to_nv12),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            raised = true;
-        }
+        ensure_func_attr(reinterpret_cast<const void*>(&k_scale_to_nv12),
+                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
     dim3 grid((coded_w + kTileW - 1) / kTileW, (coded_h + kTileH - 1) / kTileH);
     hipLaunchKernelGGL(k_scale_to_nv12, grid, dim3(256), lds, stream, bgrx, in_pitch, in_w, in_h, t, y, uv, out_pitch,

@@ -170,6 +170,10 @@ Session::~Session() {
     if (lt_mf_mem_) hipFree(lt_mf_mem_);
     for (const auto& r : host_regs_) (void)hipHostUnregister(const_cast<uint8_t*>(r.first));
     if (ev_upload_) (void)hipEventDestroy(ev_upload_);
+    if (upload_stream_) {
+        (void)hipStreamSynchronize(upload_stream_);
+        (void)hipStreamDestroy(upload_stream_);
+    }
     for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
     if (mask_dev_) (void)hipFree(mask_dev_);
     if (mask_counter_) (void)hipFree(mask_counter_);
@@ -203,10 +207,23 @@ void Session::enqueue_mask_sse(int k) {
     // by the next frame's conversion, which is later on the same stream)
     if (!masked() || mask_in_encoder_) return;
     const h264::EncoderConfig& e = enc_->rc().config();
-    pix::launch_sse_masked(nv12_y_, enc_->recon_y(), enc_->pitch(), e.width, e.height, cfg_.mask_x0, cfg_.mask_y0,
-                           cfg_.mask_x1, cfg_.mask_y1, mask_dev_ + (size_t)k * mask_stride_, mask_counter_ + k,
-                           mask_host_ + k, stream_);  // mapped: the kernel stores the total to the host
+    int r[4];
+    mask_rect_mb(r);
+    pix::launch_sse_masked(nv12_y_, enc_->recon_y(), enc_->pitch(), e.width, e.height, r[0], r[1], r[2], r[3],
+                           mask_dev_ + (size_t)k * mask_stride_, mask_counter_ + k, mask_host_ + k,
+                           stream_);  // mapped: the kernel stores the total to the host
     HIP_CHECK(hipEventRecord(ev_mask_[k], stream_));
+}
+
+void Session::mask_rect_mb(int r[4]) const {
+    // the quality mask widened to whole 16x16 macroblocks and clipped to the picture: the same
+    // region the H.264 encoder leaves out of its masked distortion channel, so both codecs'
+    // masked PSNR figures cover the same pixels
+    const h264::EncoderConfig& e = enc_->rc().config();
+    r[0] = std::max(0, cfg_.mask_x0) / 16 * 16;
+    r[1] = std::max(0, cfg_.mask_y0) / 16 * 16;
+    r[2] = std::min(e.width, (cfg_.mask_x1 + 15) / 16 * 16);
+    r[3] = std::min(e.height, (cfg_.mask_y1 + 15) / 16 * 16);
 }
 
 int Session::begin_frame() {
@@ -292,6 +309,16 @@ void Session::register_host_buffer(const void* p, size_t bytes) {
     HIP_CHECK(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault));
     host_regs_.emplace_back(b, bytes);
     if (!ev_upload_) HIP_CHECK(hipEventCreateWithFlags(&ev_upload_, hipEventDisableTiming));
+    if (!upload_stream_) HIP_CHECK(hipStreamCreateWithFlags(&upload_stream_, hipStreamNonBlocking));
+}
+
+void Session::submit_bgrx_span(const uint8_t* host_bgrx, int host_pitch, size_t bytes, bool force_idr) {
+    if (host_pitch < cfg_.width * 4) throw std::invalid_argument("pitch < width * 4");
+    const size_t span = (size_t)host_pitch * (cfg_.height - 1) + (size_t)cfg_.width * 4;
+    if (host_bgrx == nullptr || bytes < span)
+        throw std::invalid_argument("frame span (" + std::to_string(span) + " B) exceeds the buffer (" +
+                                    std::to_string(bytes) + " B)");
+    submit_bgrx(host_bgrx, host_pitch, force_idr);
 }
 
 void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_idr) {
@@ -305,9 +332,15 @@ void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_i
         ++frame_id_;
         const int slot = pool_->acquire();
         HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+        // the DMA runs on its own stream, so waiting for it below does not also wait for the
+        // previous frame's analysis kernels queued on stream_ (keeps the depth-2 overlap); the
+        // slot's last reader (the conversion pool_slots frames ago) finished before that
+        // frame was collected
+        HIP_CHECK(hipStreamWaitEvent(upload_stream_, ev_start_[k], 0));
         HIP_CHECK(hipMemcpy2DAsync(pool_->data(slot), pool_->pitch(), host_bgrx, host_pitch, row, cfg_.height,
-                                   hipMemcpyHostToDevice, stream_));
-        HIP_CHECK(hipEventRecord(ev_upload_, stream_));
+                                   hipMemcpyHostToDevice, upload_stream_));
+        HIP_CHECK(hipEventRecord(ev_upload_, upload_stream_));
+        HIP_CHECK(hipStreamWaitEvent(stream_, ev_upload_, 0));
         convert_and_encode(slot, force_idr);
         HIP_CHECK(hipEventSynchronize(ev_upload_));  // the caller may overwrite the buffer now
         return;
@@ -349,9 +382,10 @@ FrameResult Session::collect() {
         r.psnr_y_masked = psnr(st.sse_masked, (double)std::max<int64_t>(1, st.masked_pixels));
     } else if (masked()) {
         HIP_CHECK(hipEventSynchronize(ev_mask_[fl.k]));
-        const double mw = std::max(0, std::min(cfg_.mask_x1, enc_->rc().config().width) - std::max(0, cfg_.mask_x0));
-        const double mh = std::max(0, std::min(cfg_.mask_y1, enc_->rc().config().height) - std::max(0, cfg_.mask_y0));
-        r.psnr_y_masked = psnr(mask_host_[fl.k], ny - mw * mh);
+        int m[4];
+        mask_rect_mb(m);
+        const double mw = std::max(0, m[2] - m[0]), mh = std::max(0, m[3] - m[1]);
+        r.psnr_y_masked = psnr(mask_host_[fl.k], std::max(1.0, ny - mw * mh));
     }
     return r;
 }

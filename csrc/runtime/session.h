@@ -102,6 +102,9 @@ class Session {
     // submit_bgrx from inside it is a direct 2D DMA, with no copy into the staging buffer, and
     // returns once the DMA has read the frame (the buffer may then be overwritten).
     void register_host_buffer(const void* p, size_t bytes);
+    // submit_bgrx from a raw host address whose readable extent is `bytes`: throws
+    // std::invalid_argument unless the frame span (pitch * (height - 1) + width * 4) fits.
+    void submit_bgrx_span(const uint8_t* host_bgrx, int host_pitch, size_t bytes, bool force_idr = false);
     FrameResult collect();
     FrameResult step(bool force_idr = false) {
         submit_synthetic(force_idr);
@@ -146,6 +149,7 @@ class Session {
     void* lt_mf_mem_ = nullptr;  // MFMA scaler fragment tables
     std::vector<std::pair<const uint8_t*, size_t>> host_regs_;  // register_host_buffer ranges
     hipEvent_t ev_upload_ = nullptr;
+    hipStream_t upload_stream_ = nullptr;  // zero-copy DMA from registered capture buffers
     // frames in flight (pipeline depth 1 or 2): per-frame start event / staging buffer
     struct Inflight {
         uint32_t frame_id;
@@ -163,6 +167,7 @@ class Session {
     bool masked() const { return cfg_.mask_x1 > cfg_.mask_x0 && cfg_.mask_y1 > cfg_.mask_y0; }
     bool mask_in_encoder_ = false;  // H.264: the encoder reports the masked distortion itself
     void enqueue_mask_sse(int k);
+    void mask_rect_mb(int r[4]) const;  // mask rectangle aligned out to macroblocks, clipped
     int next_k_ = 0;
     int depth_ = 1;
     // hipGraph replay: pinned + device synth parameters, one executable graph per

@@ -12,8 +12,8 @@ Supported: VPS/SPS/PPS (incl. VUI), I and P slices (one reference picture, short
 from the SPS), coding quadtrees with split_cu_flag, PartMode 2Nx2N (intra and inter),
 transform trees with split_transform_flag, residual coding for 4x4..32x32 TUs (scanIdx
 0/1/2, no sign hiding, no transform skip), cu_qp_delta, conformance window cropping.
-Deblocking and SAO must be disabled, TMVP off (mxdesk's encoder guarantees all three);
-anything else raises ``NotImplementedError``.  Slow; meant for small test pictures.
+The in-loop deblocking filter (8.7.2) is implemented; SAO must be disabled and TMVP off
+(mxdesk's encoder guarantees both); anything else raises ``NotImplementedError``.  Slow; meant for small test pictures.
 """
 from __future__ import annotations
 

@@ -190,12 +190,20 @@ class StreamPipeline:
                 # zero-copy when the capture lands in a registered MIT-SHM segment: the GPU DMAs
                 # the frame straight out of it (no CPU copy into the staging buffer)
                 shm = getattr(self.capture, "shm_buffer", lambda: None)()
-                if shm is not None:
-                    if getattr(self, "_shm_reg", None) != shm:
+                if shm is not None and (getattr(self.capture, "w", self.width), getattr(self.capture, "h", self.height)) \
+                        != (self.width, self.height):
+                    shm = None  # capture resized but the session not yet: copy path (size-checked)
+                if shm is not None and getattr(self, "_shm_reg", None) != shm:
+                    try:
                         s.register_host_buffer(*shm)
                         self._shm_reg = shm
+                    except RuntimeError as e:  # page-locking refused: keep the staging copy path
+                        log.warning("register_host_buffer failed (%s); using the staging copy", e)
+                        shm = None
+                        self.capture_zero_copy = False
+                if shm is not None and getattr(self, "capture_zero_copy", True):
                     addr, pitch = self.capture.grab_shm()
-                    s.submit_bgrx_ptr(addr, pitch, force_idr)
+                    s.submit_bgrx_ptr(addr, pitch, shm[1] - (addr - shm[0]), force_idr)
                 else:
                     s.submit_bgrx(self.capture.grab(), force_idr)
                 r = s.collect()

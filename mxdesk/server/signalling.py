@@ -87,8 +87,14 @@ class SignallingRelay:
                         if other not in self.peers:
                             await ws.send_str(f"ERROR peer {other!r} not found")
                             continue
-                        if srv is not None and self.sessions.get(uid) == srv.uid:
-                            srv.on_leave(uid)  # the browser chose another peer
+                        # both browsers leave the streaming peer they were linked to (otherwise
+                        # the peer's socket, timers and pipeline consumer would be orphaned)
+                        for u in (uid, other):
+                            if srv is not None and self.sessions.get(u) == srv.uid:
+                                srv.on_leave(u)
+                            prev = self.sessions.get(u)
+                            if prev is not None and prev not in (srv.uid if srv else None, uid, other):
+                                self.sessions.pop(prev, None)  # a third browser loses its link
                         self.sessions[uid] = other
                         self.sessions[other] = uid
                     await ws.send_str("SESSION_OK")
@@ -112,7 +118,7 @@ class SignallingRelay:
                     other = self.sessions.pop(uid, None)
                     if srv is not None and other == srv.uid:
                         srv.on_leave(uid)
-                    elif other is not None:
+                    elif other is not None and self.sessions.get(other) == uid:
                         self.sessions.pop(other, None)
                         peer = self.peers.get(other)
                         if peer is not None and not peer.closed:

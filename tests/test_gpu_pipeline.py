@@ -426,7 +426,10 @@ def test_zero_copy_registered_capture_matches_staged_upload(gpu):
         staged.submit_bgrx(np.ascontiguousarray(f[:, : w * 4]).reshape(h, w, 4), False)
         a = staged.collect().au
         buf[:] = f
-        zc.submit_bgrx_ptr(buf.ctypes.data, pitch, False)
+        zc.submit_bgrx_ptr(buf.ctypes.data, pitch, buf.nbytes, False)
         buf[:] = 0  # the DMA has read the frame when submit returns
         b = zc.collect().au
         assert a == b
+    # a span that does not fit the declared buffer is refused before any copy (no overread)
+    with pytest.raises(ValueError):
+        zc.submit_bgrx_ptr(buf.ctypes.data, pitch, buf.nbytes - 1, False)

@@ -60,3 +60,65 @@ def test_selkies_client_gets_offer_media_and_input_channel(native, monkeypatch):
     idr = [i for i, au in enumerate(res.aus) if any((n[0] & 0x1F) == 5 for n in native.net.split_annexb(au))]
     assert idr[0] == 0 and any(i >= 4 for i in idr[1:])
     assert not sessions  # the client's disconnect closed its peer
+
+
+def test_browser_to_browser_session_releases_streaming_peers():
+    """two browsers that link to each other leave their streaming-peer sessions,
+    and disconnecting afterwards leaves no peer behind (no orphaned WebRtcPeer)."""
+    import aiohttp
+    from aiohttp import web
+
+    from mxdesk.server.selkies_peer import SelkiesServerPeer
+    from mxdesk.server.signalling import SignallingRelay
+
+    class FakePeer:
+        closed = 0
+        id = "fake"
+
+        async def start_offer(self):
+            return "v=0"
+
+        def close(self):
+            FakePeer.closed += 1
+
+    relay = SignallingRelay()
+    srv = SelkiesServerPeer(relay, FakePeer)
+    relay.attach_server(srv)
+
+    async def go():
+        app = web.Application()
+        app.router.add_get("/ws", relay.handler)
+        runner = web.AppRunner(app)
+        await runner.setup()
+        port = free_port()
+        site = web.TCPSite(runner, "127.0.0.1", port)
+        await site.start()
+        try:
+            async with aiohttp.ClientSession() as cs:
+                a = await cs.ws_connect(f"http://127.0.0.1:{port}/ws")
+                b = await cs.ws_connect(f"http://127.0.0.1:{port}/ws")
+                await a.send_str("HELLO A")
+                await b.send_str("HELLO B")
+                for ws in (a, b):
+                    assert (await ws.receive_str()) == "HELLO"
+                    assert "offer" in (await ws.receive_str())  # the streaming peer's offer
+                assert set(srv.sessions) == {"A", "B"}
+                await a.send_str("SESSION B")
+                assert (await a.receive_str()) == "SESSION_OK"
+                assert not srv.sessions and relay.sessions == {"A": "B", "B": "A"}
+                await a.send_str('{"sdp": "x"}')  # relayed browser -> browser
+                assert (await b.receive_str()) == '{"sdp": "x"}'
+                await a.close()
+                msg = await b.receive_str()
+                assert msg == "ERROR peer A disconnected"
+                await b.close()
+                for _ in range(50):
+                    if not relay.peers:
+                        break
+                    await asyncio.sleep(0.02)
+        finally:
+            await runner.cleanup()
+
+    asyncio.run(go())
+    assert not srv.sessions and not relay.sessions and not relay.peers
+    assert FakePeer.closed == 2

@@ -4,6 +4,7 @@ full WHEP loopback (ICE-lite -> DTLS -> SRTP -> H.264 depacketize -> independent
 barcode) with NACK retransmission and PLI -> IDR."""
 import asyncio
 import os
+import random
 import struct
 
 import pytest
@@ -229,9 +230,16 @@ def test_answer_lists_every_host_candidate():
 
 def test_h265_packetizer_depacketizer_roundtrip(native):
     net = native.net
-    vps, sps, pps = b"\x40\x01" + os.urandom(20), b"\x42\x01" + os.urandom(30), b"\x44\x01" + os.urandom(6)
-    idr = b"\x26\x01" + os.urandom(4000)  # IDR_W_RADL slice
-    small = b"\x02\x01" + os.urandom(50)  # TRAIL_R slice
+    rng = random.Random(1234)
+
+    def body(n):  # seeded; a NAL never ends in 0x00 (ambiguous in Annex-B: it would read as a start code)
+        b = bytearray(rng.getrandbits(8) for _ in range(n))
+        b[-1] |= 1
+        return bytes(b)
+
+    vps, sps, pps = b"\x40\x01" + body(20), b"\x42\x01" + body(30), b"\x44\x01" + body(6)
+    idr = b"\x26\x01" + body(4000)  # IDR_W_RADL slice
+    small = b"\x02\x01" + body(50)  # TRAIL_R slice
     au = _annexb([vps, sps, pps, idr, small])
     pk = net.RtpH265Packetizer(0x1234, 104, 1150, 7)
     pkts = pk.packetize(au, 999)
