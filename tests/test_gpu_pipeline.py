@@ -432,4 +432,4 @@ def test_zero_copy_registered_capture_matches_staged_upload(gpu):
         assert a == b
     # a span that does not fit the declared buffer is refused before any copy (no overread)
     with pytest.raises(ValueError):
-        zc.submit_bgrx_ptr(buf.ctypes.data, pitch, buf.nbytes - 1, False)
+        zc.submit_bgrx_ptr(buf.ctypes.data, pitch, pitch * (h - 1) + w * 4 - 1, False)
