@@ -207,6 +207,26 @@ PYBIND11_MODULE(_native, m) {
                  std::memcpy(uv.mutable_data(), e.recon_uv().data(), (size_t)cw * ch / 2);
                  return py::make_tuple(y, uv);
              })
+        .def("mb_bits",
+             [](h264::CpuH264Encoder& e) {
+                 const auto& v = e.mb_bits();
+                 py::array_t<uint32_t> a((py::ssize_t)v.size());
+                 std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
+                 return a.reshape({e.common().mb_h(), e.common().mb_w()});
+             })
+        .def("mb_info",
+             [](h264::CpuH264Encoder& e) {  // (mb_h, mb_w, 8): type, qp, cbp, skip, mvx, mvy, nz_luma sum, cost
+                 const auto& v = e.mb_info();
+                 py::array_t<int32_t> a({(py::ssize_t)v.size(), (py::ssize_t)8});
+                 int32_t* d = a.mutable_data();
+                 for (size_t i = 0; i < v.size(); ++i) {
+                     int nz = 0;
+                     for (int k = 0; k < 16; ++k) nz += v[i].nz_luma[k];
+                     const int32_t r[8] = {v[i].type, v[i].qp, v[i].cbp, v[i].skip, v[i].mvx, v[i].mvy, nz, (int32_t)v[i].cost};
+                     std::memcpy(d + 8 * i, r, sizeof r);
+                 }
+                 return a.reshape({e.common().mb_h(), e.common().mb_w(), 8});
+             })
         .def("request_idr", [](h264::CpuH264Encoder& e) { e.common().request_idr(); })
         .def("set_bitrate", [](h264::CpuH264Encoder& e, int k) { e.common().set_bitrate(k); })
         .def_property_readonly("stats", &h264::CpuH264Encoder::last_stats);

@@ -313,7 +313,18 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                     res[r * 16 + k] = sy[(y0 + r) * pitch + x0 + k] - p;
                     lsad += (uint32_t)std::abs(res[r * 16 + k]);
                 }
-            const int qp = aq_mb_qp(frame_qp, lsad, cfg_.aq);
+            // temporal class: the source's change against the previous source, displaced by the
+            // integer part of the vector (aq 3)
+            uint32_t tsad = 0;
+            if (cfg_.aq >= 3 && !prev_src_.empty()) {
+                const int ix = mvx >> 2, iy = mvy >> 2;
+                for (int r = 0; r < 16; ++r)
+                    for (int k = 0; k < 16; ++k)
+                        tsad += (uint32_t)std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
+                                                   (int)ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + k + ix, y0 + r + iy));
+            }
+            const int tcls = temporal_class(tsad);
+            const int qp = mb_qp_for(frame_qp, lsad, tcls, cfg_.aq);
             const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
             m.qp = (uint8_t)qp;
             for (int comp = 0; comp < 2; ++comp)
@@ -345,7 +356,7 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                     d_coded += e * e;
                 }
             }
-            const bool drop = drop_residual(cfg_.aq, lsad, qp, d_pred, d_coded, bits);
+            const bool drop = drop_luma_for(cfg_.aq, lsad, tcls, qp, d_pred, d_coded, bits);
             for (int b = 0; b < 16; ++b) {
                 const int bx = kBlkX[b], by = kBlkY[b];
                 const int nz = drop ? 0 : nzb[b];
@@ -357,7 +368,7 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                         rec_y[(y0 + by * 4 + i) * cw_ + x0 + bx * 4 + j] = (uint8_t)clip255(
                             pred[(by * 4 + i) * 16 + bx * 4 + j] + (drop ? 0 : rrb[b][i * 4 + j]));
             }
-            if (drop)  // chroma residual goes with the luma decision
+            if (drop_chroma_for(cfg_.aq, tcls, drop))  // chroma residual goes with the luma decision
                 for (int i = 256; i < 384; ++i) res[i] = 0;
             bool any_ac = false, any_dc = false;
             for (int comp = 0; comp < 2; ++comp) {
@@ -439,6 +450,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
     const int per_slice = slice_rows * g.mb_w;
     const int nmb = g.mb_w * g.mb_h;
     std::vector<uint32_t> words((size_t)nmb * kSlotWords / 4 + 4096);
+    mb_bits_.assign(nmb, 0);
     for (int first = 0; first < nmb; first += per_slice) {
         const int last = std::min(first + per_slice, nmb);
         BitWriter w;
@@ -457,6 +469,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
                 ++run;
                 continue;
             }
+            const uint32_t b0 = w.bits;
             if (!idr) {
                 put_ue(w, (uint32_t)run);
                 run = 0;
@@ -469,6 +482,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
             }
             for (int role = 0; role < kNumRoles; ++role)
                 code_role(w, role, g, idr, nb, mc, av, mvdx, mvdy, dqp);
+            mb_bits_[mbi] = w.bits - b0;
         }
         if (!idr && run > 0) put_ue(w, (uint32_t)run);
         w.put(1, 1);
@@ -492,6 +506,16 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     }
     common_.begin_frame(force_idr || !have_ref_);
     cur_ ^= 1;
+    // this frame's source becomes the previous source of the next one (temporal AQ classes)
+    struct SaveSrc {
+        std::vector<uint8_t>& d;
+        const uint8_t* y;
+        int pitch, cw, ch;
+        ~SaveSrc() {
+            d.resize((size_t)cw * ch);
+            for (int r = 0; r < ch; ++r) std::memcpy(d.data() + (size_t)r * cw, y + (size_t)r * pitch, cw);
+        }
+    } save_src{prev_src_, y, pitch, cw_, ch_};
     if (common_.cur_idr())
         encode_intra(y, uv, pitch);
     else

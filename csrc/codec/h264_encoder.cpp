@@ -91,10 +91,10 @@ void EncoderCommon::begin_frame(bool force_idr) {
         if (x_p_ > 0) {
             q = qp_for(x_p_, budget, alpha_p_);
         } else if (x_i_ > 0) {
-            // no P picture finished yet: assume a P picture costs half an I picture at equal QP
-            // (pessimistic for desktops -- undershooting for a frame or two is cheaper than a
-            // latency spike; the model has real P data two frames later)
-            q = qp_for(0.5 * x_i_, budget, 1.0);
+            // no P picture finished yet: assume a P picture costs kPPrior of an I picture at equal
+            // QP (desktop P pictures cost 10-20 % of the IDR; the former 0.5 starved the first P
+            // pictures at QP 46 after every IDR; the model has real P data two frames later)
+            q = qp_for(kPPrior * x_i_, budget, 1.0);
         } else {
             q = (last_i_qp_ >= 0 ? last_i_qp_ : cfg_.qp) + 2;
         }
@@ -303,6 +303,8 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMalloc(&rec_uv_[i], uvsz));
         HIP_CHECK(hipMemsetAsync(rec_y_[i], 16, ysz, stream_));
         HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
+        HIP_CHECK(hipMalloc(&src_keep_[i], ysz));
+        HIP_CHECK(hipMemsetAsync(src_keep_[i], 16, ysz, stream_));
     }
     if (cfg.mask_x1 > cfg.mask_x0 && cfg.mask_y1 > cfg.mask_y0) {
         mask_mb_[0] = std::max(0, cfg.mask_x0) / 16;
@@ -332,6 +334,7 @@ GpuH264Encoder::~GpuH264Encoder() {
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);
+        (void)hipFree(src_keep_[i]);
     }
     for (int i = 0; i < 4; ++i) (void)hipFree(hp_[i]);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
@@ -342,6 +345,8 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     const FrameState* pub = publish ? sl.fs_host : nullptr;
     if (idr) {
         launch_intra(geom_, sl.buf, src_y, src_uv, stream_, pub);
+        if (cfg_.aq >= 3)  // the next P picture's previous source (P pictures: k_inter_encode stores it)
+            launch_save_src(geom_, sl.buf, src_y, stream_);
     } else {
         launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
         launch_me(geom_, sl.buf, src_y, stream_);
@@ -391,6 +396,8 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.hp_v = hp_[2] + org;
     f.hp_j = hp_[3] + org;
     f.sse_part = sl.buf.sse_part;
+    f.prev_src = src_keep_[ref];
+    f.save_src = src_keep_[cur];
 }
 
 int GpuH264Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp) {

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <deque>
 #include <string>
 #include <vector>
@@ -37,9 +38,10 @@ struct EncoderConfig {
                               // 0: exhaustive +-range search
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
-    int aq = 2;               // adaptive quantisation of noise-like P macroblocks (mb_qp_delta); 2 adds the
-                              // rate-distortion residual drop for them (drop_residual; +0.6-0.9 dB masked
-                              // Y-PSNR at 8 Mbps on the bench desktop, profiles/r02_bench)
+    int aq = 3;               // adaptive quantisation of P macroblocks (mb_qp_delta): 1 coarser QP for
+                              // noise-like residuals, 2 adds their rate-distortion residual drop, 3 (H.264
+                              // default) temporal classes of the source -- persistent content finer, changing
+                              // content coarser (h264_mb.h temporal_class; HEVC treats 3 as 2)
     int deblock = 1;          // HEVC in-loop deblocking filter (the H.264 encoder always disables it)
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
@@ -108,11 +110,12 @@ class EncoderCommon {
     int probe_qp() const;                 // QP to probe next
     void add_probe(int qp, int bytes);    // result of a probe encode of the first picture
     double vbv_excess_bits() const { return vbv_; }
-    static constexpr int kDrainFrames = 8;
-    static constexpr double kIdrBudget = 3.0;  // IDR budget in frames
+    static constexpr int kDrainFrames = 4;
+    static constexpr double kPPrior = 0.3;  // first P picture after an IDR: bits ~ kPPrior x the IDR's at equal QP
+    static constexpr double kIdrBudget = 5.0;  // IDR budget in frames (tools/region_report.py sweep)
     static constexpr int kMaxProbes = 2;
-    static constexpr int kMaxStep = 3;  // max P-picture QP rise per frame (damps the pipelined loop)
-    static constexpr int kMaxDown = 2;  // max P-picture QP fall per frame (bounds refinement spikes)
+    static constexpr int kMaxStep = 4;  // max P-picture QP rise per frame (damps the pipelined loop)
+    static constexpr int kMaxDown = 3;  // max P-picture QP fall per frame (bounds refinement spikes)
 
    private:
     int qp_for(double x, double bits, double alpha) const;
@@ -222,6 +225,7 @@ class GpuH264Encoder final : public VideoEncoder {
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
+    uint8_t* src_keep_[2] = {nullptr, nullptr};  // source luma of the last two frames (temporal AQ classes)
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
     int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
@@ -241,6 +245,9 @@ class CpuH264Encoder {
     const std::vector<uint8_t>& recon_y() const { return rec_y_[cur_]; }
     const std::vector<uint8_t>& recon_uv() const { return rec_uv_[cur_]; }
     int coded_pitch() const { return cw_; }
+    // analysis hooks: per-MB coded bits of the last frame (0 = skipped) and the MB records
+    const std::vector<uint32_t>& mb_bits() const { return mb_bits_; }
+    const std::vector<MbInfo>& mb_info() const { return mb_; }
 
    private:
     void encode_intra(const uint8_t* y, const uint8_t* uv, int pitch);
@@ -257,6 +264,8 @@ class CpuH264Encoder {
     bool have_ref_ = false;
     std::vector<MbInfo> mb_;
     std::vector<int16_t> coef_;
+    std::vector<uint32_t> mb_bits_;
+    std::vector<uint8_t> prev_src_;  // previous source luma (coded size), temporal AQ classes
     std::vector<uint8_t> au_;
     FrameStats stats_;
 };

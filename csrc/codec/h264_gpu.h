@@ -82,6 +82,10 @@ struct FrameState {
     // quality report: MBs in [mask_mx0, mask_mx1) x [mask_my0, mask_my1) are left out of the 4th
     // distortion channel (e.g. the synthetic desktop's noise panel); empty rect = no mask
     int32_t mask_mx0, mask_my0, mask_mx1, mask_my1;
+    // temporal AQ classes (aq 3): previous frame's source luma (read) and this frame's copy (written
+    // by k_inter_encode per MB, by a copy for IDR pictures); coded size, luma pitch
+    const uint8_t* prev_src;
+    uint8_t* save_src;
     // padded reference planes (origin at picture (0,0), valid for x,y in [-kHpelPad, size+kHpelPad))
     const uint8_t* hp_f;  // full-sample (edge-replicated)
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
@@ -153,6 +157,9 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
 // each hp_pitch x (coded_h + 2*kHpelPad), origin offset applied by the caller via FrameState).
 void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
                  hipStream_t stream, const FrameState* publish = nullptr);
+// Copy the source luma into FrameState::save_src (IDR pictures; the pointer is read on the device
+// so a captured graph stays valid while the buffers alternate).
+void launch_save_src(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream);
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
 // P pictures, after launch_inter: open-loop intra analysis of every MB (intra vs inter) and the
 // closed-loop reconstruction of the MBs that switched to intra.

@@ -589,11 +589,21 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     const int cw = g.coded_w / 2, ch = g.coded_h / 2;
     int mvx = 0, mvy = 0;
     int lsad = 0;  // this lane's share of sum |luma residual| (adaptive quantisation)
+    int tsad = 0;  // this lane's share of sum |src - previous src| (temporal class, aq 3)
     if (valid) {
         mvx = mbs[mbi].mvx;
         mvy = mbs[mbi].mvy;
         const int r = lane >> 2, c0 = (lane & 3) * 4;
         const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
+        if (fs->aq >= 3) {
+            // temporal class (h264_mb.h temporal_class): the source against the previous source,
+            // displaced by the vector's integer part; this MB's source becomes the next frame's
+            const int ix = mvx >> 2, iy = mvy >> 2;
+            for (int k = 0; k < 4; ++k)
+                tsad += abs((int)((sw >> (8 * k)) & 0xff) -
+                            ref_px(fs->prev_src, g.pitch, g.coded_w, g.coded_h, x0 + c0 + k + ix, y0 + r + iy));
+            *reinterpret_cast<uint32_t*>(fs->save_src + (y0 + r) * g.pitch + x0 + c0) = sw;
+        }
         for (int k = 0; k < 4; ++k) {
             const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
             const int d = (int)((sw >> (8 * k)) & 0xff) - p;
@@ -612,7 +622,8 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     }
     __syncthreads();
     const uint32_t lsad_mb = (uint32_t)wave_sum(lsad);
-    const int qp = aq_mb_qp(fs->qp, lsad_mb, fs->aq);  // wave-uniform
+    const int tcls = temporal_class((uint32_t)wave_sum(tsad));
+    const int qp = mb_qp_for(fs->qp, lsad_mb, tcls, fs->aq);  // wave-uniform
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     int16_t* mc = coef + (size_t)(valid ? mbi : 0) * kCoefStride;
 
@@ -639,8 +650,9 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         d_coded += e * e;
     }
     const uint32_t bits = rr == 0 ? block_bits_est(nzb) : 0u;
-    const bool drop = valid && drop_residual(fs->aq, lsad_mb, qp, wave_sum(d_pred), wave_sum(d_coded),
+    const bool drop = valid && drop_luma_for(fs->aq, lsad_mb, tcls, qp, wave_sum(d_pred), wave_sum(d_coded),
                                              (uint32_t)wave_sum((int)bits));  // wave-uniform
+    const bool drop_c = drop_chroma_for(fs->aq, tcls, drop);
     const int nz_l = drop ? 0 : nzb;
     int sse_y = 0;
     if (valid) {
@@ -669,7 +681,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     if (clane) {
         int cx[4], cy[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) cx[c] = drop ? 0 : res[wave][co + c];  // a dropped MB codes no chroma residual
+        for (int c = 0; c < 4; ++c) cx[c] = drop_c ? 0 : res[wave][co + c];  // a dropped MB codes no chroma residual
         fdct_row(cx, rr, cy);
         if (rr == 0) cdc[wave][ccomp * 4 + cblk] = cy[0];
         nzc = quant_row(cy, rr, qpc, false, 1, cz);
@@ -2332,6 +2344,18 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
     hipLaunchKernelGGL(k_intra_wave, dim3(slices, 2), dim3(64 * rows), lds, stream, g, b.fs, src_y, src_uv, b.mb,
                        b.coef);
     hipLaunchKernelGGL(k_intra_cbp, dim3((g.mb_w * g.mb_h + 255) / 256), dim3(256), 0, stream, g, b.mb);
+}
+
+__global__ __launch_bounds__(256) void k_save_src(Geometry g, const FrameState* __restrict__ fs,
+                                                   const uint8_t* __restrict__ src_y) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // 16-byte chunk
+    const size_t n = (size_t)g.pitch * g.coded_h / 16;
+    if (i < n) reinterpret_cast<uint4*>(fs->save_src)[i] = reinterpret_cast<const uint4*>(src_y)[i];
+}
+
+void launch_save_src(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream) {
+    const size_t n = (size_t)g.pitch * g.coded_h / 16;  // pitch is a multiple of 256
+    hipLaunchKernelGGL(k_save_src, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, g, b.fs, src_y);
 }
 
 void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream) {

@@ -174,7 +174,7 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbNbrs& nb
 // it returns -- and the rate controller hands those bits to the rest of the picture (text,
 // UI edges).  sad = sum |src - pred| over the 16x16 luma block.
 MXHD int aq_mb_qp(int frame_qp, uint32_t sad, int aq) {
-    if (!aq) return frame_qp;
+    if (!aq) return frame_qp;  // (aq 3 -- the temporal classes below -- falls back to this rule in HEVC)
     const int off = sad > 256u * 48 ? 12 : (sad > 256u * 32 ? 6 : 0);
     const int q = frame_qp + off;
     return q > 51 ? 51 : q;
@@ -198,6 +198,45 @@ MXHD uint32_t block_bits_est(int nz) { return nz ? 2u + 6u * (uint32_t)nz : 0u; 
 MXHD bool drop_residual(int aq, uint32_t lsad, int qp, long long d_pred, long long d_coded, uint32_t bits) {
     if (aq < 2 || lsad <= 256u * 32) return false;
     return d_pred - d_coded < (long long)lambda_sse(qp) * (long long)bits;
+}
+
+// Temporal classes (EncoderConfig::aq == 3, the H.264 default).  The residual-energy rule above
+// cannot tell incompressible content from well-predictable content whose reference is still
+// coarse: text coded at a high QP in the IDR leaves a large residual too, and was then quantised
+// 6-12 QP coarser -- never refined (the document window stayed at 28 dB over the driver window,
+// tools/region_report.py).  The classes here use the SOURCE's own temporal change instead:
+// tsad = sum |src_n - src_(n-1)| over the 16x16 luma block displaced by the integer part of the
+// chosen motion vector.
+//  * changing content (tsad > 24 / pixel: e.g. animated noise, video): its bits are thrown away
+//    with the next picture -> 6 QP coarser, luma residual kept only if it pays for its bits
+//    (drop_residual's rate-distortion rule), chroma residual dropped;
+//  * persistent content (tsad <= 2 / pixel: static or moving rigidly): everything coded now is
+//    re-used by every later picture (the static desktop refines once and is then skipped) ->
+//    6 QP finer -- a one-step form of x264's macroblock-tree propagation without a lookahead;
+//  * anything else at the frame QP.
+constexpr uint32_t kTsadChanging = 256u * 24, kTsadPersistent = 256u * 2;
+constexpr int kAqChangingOffset = 6, kAqPersistentOffset = -6;
+enum TClass : int { kTcNormal = 0, kTcPersistent = 1, kTcChanging = 2 };
+MXHD int temporal_class(uint32_t tsad) {
+    return tsad > kTsadChanging ? kTcChanging : (tsad <= kTsadPersistent ? kTcPersistent : kTcNormal);
+}
+MXHD int aq3_mb_qp(int frame_qp, int tclass) {
+    const int q = frame_qp + (tclass == kTcChanging ? kAqChangingOffset
+                                                    : (tclass == kTcPersistent ? kAqPersistentOffset : 0));
+    return q < 0 ? 0 : (q > 51 ? 51 : q);
+}
+// MB QP and residual-drop decision of a P macroblock for any aq mode (aq >= 3 uses tclass).
+MXHD int mb_qp_for(int frame_qp, uint32_t lsad, int tclass, int aq) {
+    return aq >= 3 ? aq3_mb_qp(frame_qp, tclass) : aq_mb_qp(frame_qp, lsad, aq);
+}
+MXHD bool drop_luma_for(int aq, uint32_t lsad, int tclass, int qp, long long d_pred, long long d_coded,
+                        uint32_t bits) {
+    if (aq >= 3)
+        return tclass == kTcChanging && d_pred - d_coded < (long long)lambda_sse(qp) * (long long)bits;
+    return drop_residual(aq, lsad, qp, d_pred, d_coded, bits);
+}
+MXHD bool drop_chroma_for(int aq, int tclass, bool luma_dropped) {
+    return luma_dropped || (aq >= 3 && tclass == kTcChanging);
 }
 
 // Inter cost of a P16x16 macroblock for the intra decision: luma SATD of the motion-
