@@ -7,6 +7,7 @@
 #include <stdexcept>
 
 #include "h264_encoder.h"
+#include "h264_deblock.h"
 #include "h264_mb.h"
 
 namespace mx {
@@ -456,7 +457,8 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         BitWriter w;
         w.init(words.data());
         write_slice_header(w, make_slice_params(first, idr, common_.cur_frame_num(), common_.log2_max_frame_num(),
-                                                common_.cur_idr_pic_id(), frame_qp_() - common_.pic_init_qp(), 1));
+                                                common_.cur_idr_pic_id(), frame_qp_() - common_.pic_init_qp(),
+                                                cfg_.deblock ? 0 : 1));
         int run = 0;
         int qp_pred = frame_qp_();  // mb_qp_delta predictor: QP of the last MB that carried one
         for (int mbi = first; mbi < last; ++mbi) {
@@ -523,6 +525,14 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     std::vector<uint8_t> payload;
     std::vector<uint32_t> soff, slen;
     entropy(payload, soff, slen);
+    if (cfg_.deblock) {  // in-loop filter: the next picture predicts from the filtered one
+        const Geometry g = geom_of(common_, cw_, ch_);
+        std::vector<uint8_t> qpe(mb_.size());
+        db_qp_eff(mb_.data(), (int)mb_.size(), g.mb_w, common_.cur_idr() ? idr_slice_rows(g.mb_h) : g.mb_h,
+                  frame_qp_(), common_.cur_idr(), qpe.data());
+        deblock_picture_cpu(g, mb_.data(), qpe.data(), cfg_.chroma_qp_offset, rec_y_[cur_].data(), rec_uv_[cur_].data(),
+                            cw_);
+    }
     au_.clear();
     if (common_.cur_idr()) common_.write_parameter_sets(au_);
     int skipped = 0;

@@ -260,11 +260,20 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.mb_sse, sizeof(uint32_t) * 3 * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.intra_gain, sizeof(int32_t) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.intra_cand, sizeof(int) * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.db_rec, sizeof(uint4) * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.db_rowq, sizeof(int) * (size_t)geom_.mb_h));
+    HIP_CHECK(hipMalloc(&b.db_glb, sizeof(uint64_t) * 2 * 8 * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.db_glq, sizeof(uint32_t) * 2 * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.db_gprog, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h));
+    HIP_CHECK(hipMemsetAsync(b.db_gprog, 0, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h, stream_));
+    HIP_CHECK(hipHostMalloc(&b.db_err, sizeof(int), hipHostMallocMapped));
+    *b.db_err = 0;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
     std::memset(sl.host_out, 0, kOutPayloadOffset);
     HIP_CHECK(hipEventCreate(&sl.start));
     HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.deblock_done, hipEventDisableTiming));
     HIP_CHECK(hipEventCreate(&sl.done));
 }
 
@@ -272,11 +281,13 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     DeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.row_agg,
                     (void*)b.row_sse, (void*)b.coded_info, (void*)b.slice_info,
-                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit})
+                    (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit,
+                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.db_glq, (void*)b.db_gprog})
         if (p) (void)hipFree(p);
+    if (b.db_err) (void)hipHostFree(b.db_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);
-    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.done})
+    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.deblock_done, sl.done})
         if (e) (void)hipEventDestroy(e);
 }
 
@@ -359,7 +370,16 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
         HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
         es = stream_e_;
     }
-    launch_entropy(geom_, sl.buf, sl.host_out, es);
+    hipEvent_t sse_ready = nullptr;
+    if (cfg_.deblock) {  // in-loop filter on the analysis stream: the next frame predicts from it,
+                         // while this frame's CAVLC runs beside it on the entropy stream
+        launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
+        if (stream_e_) {
+            HIP_CHECK(hipEventRecord(sl.deblock_done, stream_));
+            sse_ready = sl.deblock_done;
+        }
+    }
+    launch_entropy(geom_, sl.buf, sl.host_out, es, sse_ready);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -379,7 +399,9 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.me_coarse = cfg_.me_coarse;
     f.intra4x4 = cfg_.intra4x4;
     f.subpel = cfg_.subpel;
-    f.deblock_off = 1;
+    f.deblock_off = cfg_.deblock ? 0 : 1;
+    if (++db_epoch_ > 0xfffffu) db_epoch_ = 1;  // 20-bit tag, never 0
+    f.db_epoch = (int32_t)db_epoch_;
     f.pic_init_qp = common_.pic_init_qp();
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
     f.log2_max_frame_num = common_.log2_max_frame_num();
@@ -472,6 +494,12 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, sl.start, sl.done);
     const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);
+    if (*sl.buf.db_err) {  // a deblocking hand-off spin timed out: the reference is unreliable
+        *sl.buf.db_err = 0;
+        common_.end_frame(0, sl.idr);
+        have_ref_ = false;
+        throw std::runtime_error("h264 gpu encoder: deblocking hand-off timed out");
+    }
     if (hdr.overflow) {
         common_.end_frame(0, sl.idr);
         have_ref_ = false;  // reference is incomplete: next frame must be IDR

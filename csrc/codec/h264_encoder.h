@@ -42,7 +42,7 @@ struct EncoderConfig {
                               // noise-like residuals, 2 adds their rate-distortion residual drop, 3 (H.264
                               // default) temporal classes of the source -- persistent content finer, changing
                               // content coarser (h264_mb.h temporal_class; HEVC treats 3 as 2)
-    int deblock = 1;          // HEVC in-loop deblocking filter (the H.264 encoder always disables it)
+    int deblock = 1;          // in-loop deblocking filter (H.264 8.7: k_deblock; HEVC 8.7.2)
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
@@ -202,7 +202,7 @@ class GpuH264Encoder final : public VideoEncoder {
         DeviceBuffers buf{};
         FrameState* fs_host = nullptr;  // pinned
         uint8_t* host_out = nullptr;    // pinned, mapped: OutHeader | slice tables | payload
-        hipEvent_t start = nullptr, analysis_done = nullptr, done = nullptr;
+        hipEvent_t start = nullptr, analysis_done = nullptr, deblock_done = nullptr, done = nullptr;
         bool idr = false;
         int qp = 0;
     };
@@ -228,6 +228,7 @@ class GpuH264Encoder final : public VideoEncoder {
     uint8_t* src_keep_[2] = {nullptr, nullptr};  // source luma of the last two frames (temporal AQ classes)
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
+    uint32_t db_epoch_ = 0;
     int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
     int64_t masked_pixels_ = 0;
     std::vector<uint8_t> au_;

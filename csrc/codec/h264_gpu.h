@@ -72,7 +72,8 @@ struct FrameState {
     int32_t subpel;        // 1 = quarter-pel refinement
     int32_t me_coarse;     // 1 = even-offset grid + integer neighbours instead of the full search
     int32_t intra4x4;      // 0 = intra MBs are Intra16x16 only
-    int32_t deblock_off;   // disable_deblocking_filter_idc
+    int32_t deblock_off;   // disable_deblocking_filter_idc (0: k_deblock filters the reconstruction)
+    int32_t db_epoch;      // nonzero, new every frame: tag of k_deblock's cross-workgroup progress words
     int32_t pic_init_qp;
     int32_t chroma_qp_offset;
     int32_t log2_max_frame_num;
@@ -142,6 +143,13 @@ struct DeviceBuffers {
     int32_t* intra_gain;    // [nmb] P frames: gain of switching each MB to intra (0 = stays inter)
     int* intra_cand;        // [nmb] P frames: MBs with a positive gain (count in wave_prog[1])
     uint32_t* mb_sse;       // [3 * nmb] P frames: per-MB inter distortion (replaced for intra MBs)
+    // in-loop deblocking (h264_deblock.hip)
+    uint4* db_rec;          // [nmb] boundary strengths + QP record per MB (k_db_prep)
+    int* db_rowq;           // [mb_h] QP of each row's last mb_qp_delta MB (-1: none)
+    uint64_t* db_glb;       // [2][mb_h][mb_w][8] band-boundary hand-off lines
+    uint32_t* db_glq;       // [2][mb_h][mb_w] their QP
+    uint32_t* db_gprog;     // [2][mb_h] band-boundary progress words (epoch << 12 | count)
+    int* db_err;            // mapped host word: nonzero if a deblocking spin timed out
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.
@@ -157,10 +165,17 @@ void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
 // each hp_pitch x (coded_h + 2*kHpelPad), origin offset applied by the caller via FrameState).
 void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const planes[4], int hp_pitch,
                  hipStream_t stream, const FrameState* publish = nullptr);
+// In-loop deblocking of the reconstruction (FrameState::rec_y / rec_uv, in place) + the distortion
+// partials of the filtered picture (h264_deblock.hip); after the analysis kernels.
+void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                    hipStream_t stream);
 // Copy the source luma into FrameState::save_src (IDR pictures; the pointer is read on the device
 // so a captured graph stays valid while the buffers alternate).
 void launch_save_src(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream);
-void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream);
+// wait_for_sse: event the stream waits on after k_cavlc, before the distortion partials are
+// reduced (the deblocking kernels' completion on the analysis stream), or nullptr
+void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream,
+                    hipEvent_t wait_for_sse = nullptr);
 // P pictures, after launch_inter: open-loop intra analysis of every MB (intra vs inter) and the
 // closed-loop reconstruction of the MBs that switched to intra.
 void launch_intra_in_p(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,

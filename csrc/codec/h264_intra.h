@@ -1,10 +1,10 @@
 // H.264 intra prediction (Intra4x4 9 modes, Intra16x16 4 modes, chroma 4 modes), the
-// open-loop intra mode decision, Intra4x4 mode prediction, and the in-loop deblocking
-// filter (8.7) -- shared, __host__ __device__, by the HIP kernels (h264_kernels.hip) and the
-// CPU encoder (h264_cpu.cpp), so both make identical decisions and reconstructions.
+// open-loop intra mode decision and Intra4x4 mode prediction -- shared, __host__ __device__, by
+// the HIP kernels (h264_kernels.hip) and the CPU encoder (h264_cpu.cpp), so both make identical
+// decisions and reconstructions.  The in-loop deblocking filter lives in h264_deblock.h.
 //
 // Replaces NVENC's intra toolset and loop filter behind `nvh264enc` (reference
-// Dockerfile:210, README.md:21).  Formulas follow ITU-T H.264 8.3.1.2, 8.3.3, 8.3.4, 8.7.
+// Dockerfile:210, README.md:21).  Formulas follow ITU-T H.264 8.3.1.2, 8.3.3, 8.3.4.
 #pragma once
 #include "h264_core.h"
 
@@ -438,73 +438,6 @@ MXHD bool intra_selected(const int32_t* gain, int mb_w, int mb_h, int mbx, int m
             if (h > g || (h == g && j < i)) return false;
         }
     return true;
-}
-
-// ---------------------------------------------------------------- deblocking (8.7)
-constexpr uint8_t kAlpha[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   0,   0,   4,   4,
-                                5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20,  22,  25,  28,  32,  36,  40,  45,
-                                50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
-constexpr uint8_t kBeta[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  0,  0,  2,  2,  2,  3,  3,  3,  3,  4,  4, 4,
-                               6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
-constexpr uint8_t kTc0[52][3] = {
-    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
-    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
-    {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
-    {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4},
-    {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
-    {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
-
-MXHD int iabs(int v) { return v < 0 ? -v : v; }
-MXHD int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// Filter one line of luma samples across an edge: s[0..3] = p3..p0... stored as
-// p[k] = p_k (p[0] nearest the edge) and q[k] = q_k.  indexA = clip(qPav) (offsets 0).
-MXHD void db_luma_line(int* p, int* q, int bS, int indexA) {
-    const int alpha = kAlpha[indexA], beta = kBeta[indexA];
-    const int p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3], q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
-    const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
-    if (bS < 4) {
-        const int tc0 = kTc0[indexA][bS - 1];
-        const int tc = tc0 + (ap < beta ? 1 : 0) + (aq < beta ? 1 : 0);
-        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + (p1 - q1) + 4) >> 3));
-        p[0] = clip255(p0 + delta);
-        q[0] = clip255(q0 - delta);
-        if (ap < beta) p[1] = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1);
-        if (aq < beta) q[1] = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1);
-        return;
-    }
-    const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
-    if (ap < beta && strong) {
-        p[0] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
-        p[1] = (p2 + p1 + p0 + q0 + 2) >> 2;
-        p[2] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
-    } else {
-        p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
-    }
-    if (aq < beta && strong) {
-        q[0] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
-        q[1] = (p0 + q0 + q1 + q2 + 2) >> 2;
-        q[2] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-    } else {
-        q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
-    }
-}
-
-// Chroma line (chromaStyleFilteringFlag): p[0..1], q[0..1].
-MXHD void db_chroma_line(int* p, int* q, int bS, int indexA) {
-    const int alpha = kAlpha[indexA], beta = kBeta[indexA];
-    const int p0 = p[0], p1 = p[1], q0 = q[0], q1 = q[1];
-    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
-    if (bS < 4) {
-        const int tc = kTc0[indexA][bS - 1] + 1;
-        const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + (p1 - q1) + 4) >> 3));
-        p[0] = clip255(p0 + delta);
-        q[0] = clip255(q0 - delta);
-        return;
-    }
-    p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
-    q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
 }
 
 }  // namespace h264

@@ -1925,9 +1925,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_rows(Geometry g, const Fr
     const int t = threadIdx.x, r = blockIdx.x, base = r * g.mb_w;
     const bool idr = fs->idr != 0;
     // distortion partials of this row's share (one per intra MB row or per 4-MB inter workgroup,
-    // plus the per-row intra deltas of k_intra_wave / k_intra_p)
+    // plus the per-row intra deltas of k_intra_wave / k_intra_p; one per MB row from k_db_sse
+    // when the in-loop filter is on)
     const int nmb = g.mb_w * g.mb_h;
-    const int nparts = idr ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
+    const int nparts = (idr || !fs->deblock_off) ? g.mb_h : (nmb + 3) / 4 + (fs->intra_in_p ? g.mb_h : 0);
     const int p0 = (int)((long long)nparts * r / g.mb_h), p1 = (int)((long long)nparts * (r + 1) / g.mb_h);
     unsigned long long acc[4] = {0, 0, 0, 0};
     for (int i = p0 + t; i < p1; i += kScanThreads)
@@ -2358,11 +2359,13 @@ void launch_save_src(const Geometry& g, const DeviceBuffers& b, const uint8_t* s
     hipLaunchKernelGGL(k_save_src, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, g, b.fs, src_y);
 }
 
-void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream) {
+void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out, hipStream_t stream,
+                    hipEvent_t wait_for_sse) {
     const int nmb = g.mb_w * g.mb_h;
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + kCavlcMbPerBlock - 1) / kCavlcMbPerBlock), dim3(256), 0, stream, g, b.fs,
                        b.mb, b.coef, b.slot,
                        b.slot_bits);
+    if (wait_for_sse) HIP_CHECK(hipStreamWaitEvent(stream, wait_for_sse, 0));
     if (g.mb_h > kScanMaxRows || g.mb_w > kScanThreads * kScanRowPer)
         throw std::runtime_error("launch_entropy: frame too large for the row scan");
     hipLaunchKernelGGL(k_scan_rows, dim3(g.mb_h), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.row_agg,

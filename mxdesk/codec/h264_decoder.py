@@ -6,8 +6,10 @@ the spec's parsing/decoding processes (7.3, 8.3, 8.4, 8.5, 9.2).
 
 Supported: SPS/PPS (baseline subset incl. VUI skip), I and P slices, I_NxN (Intra4x4),
 Intra16x16, I_PCM, P_L0_16x16 / 16x8 / 8x16, P_Skip, one reference frame, CAVLC,
-frame cropping.  Deblocking must be disabled (disable_deblocking_filter_idc == 1) or the
-decoder raises -- mxdesk's encoder always disables it.
+frame cropping, and the in-loop deblocking filter (8.7: bS derivation 8.7.2.1, the alpha / beta /
+tC0 tables 8-16 / 8-17, bS < 4 and bS == 4 luma and chroma filters, disable_deblocking_filter_idc
+0 / 1 / 2 with the slice's alpha / beta offsets), applied per macroblock in raster order when a
+picture is complete.
 
 Slow (pure Python); intended for small test pictures.
 """
@@ -383,6 +385,7 @@ class MbState:
     nz_cr: list = field(default_factory=lambda: [[0] * 2 for _ in range(2)])
     i4modes: list = field(default_factory=lambda: [[2] * 4 for _ in range(4)])
     i4: bool = False
+    qp: int = 0  # QP_Y of the macroblock as decoded (skipped / residual-free MBs: the predictor)
 
 
 def _clip(a):
@@ -449,6 +452,7 @@ class Decoder:
         )
         self.mbs = [MbState() for _ in range(s.mb_w * s.mb_h)]
         self.decoded_mbs = 0
+        self.slice_db = {}
 
     def finish_picture(self) -> None:
         if self.cur is None:
@@ -456,6 +460,7 @@ class Decoder:
         s = self.sps
         if self.decoded_mbs != s.mb_w * s.mb_h and not self.allow_partial:
             raise DecodeError(f"incomplete picture: {self.decoded_mbs}/{s.mb_w * s.mb_h} MBs")
+        self.deblock_picture()
         y, u, v = (p.astype(np.uint8) for p in self.cur)
         self.frames_coded.append((y, u, v))
         cl, cr, ct, cb = s.crop
@@ -505,19 +510,21 @@ class Decoder:
             elif r.bit():
                 raise DecodeError("adaptive ref pic marking not supported")
         qp = p.pic_init_qp + r.se()
+        off_a = off_b = 0
         if p.deblocking_filter_control_present:
             idc = r.ue()
+            if idc not in (0, 1, 2):
+                raise DecodeError(f"disable_deblocking_filter_idc {idc}")
             if idc != 1:
-                r.se()
-                r.se()
+                off_a = r.se() * 2
+                off_b = r.se() * 2
         else:
             idc = 0
-        if idc != 1:
-            raise DecodeError("deblocking filter not implemented in the test decoder")
         if slice_type == 0 and self.ref is None:
             raise DecodeError("P slice without reference")
         self.slice_count += 1
         sid = self.slice_count
+        self.slice_db[sid] = (idc, off_a, off_b)
         self.num_ref = num_ref
         self.qp = qp
         addr = first_mb
@@ -1036,6 +1043,8 @@ class Decoder:
         mv = self._skip_mv(addr, sid)
         parts = {(bx, by): (0, mv) for by in range(4) for bx in range(4)}
         self._store_inter(addr, sid, parts, skip=True)
+        self.mbs[addr].qp = self.qp
+        self.mbs[addr].nz_luma = [[0] * 4 for _ in range(4)]
         x0, y0 = (addr % s.mb_w) * 16, (addr // s.mb_w) * 16
         self.cur[0][y0: y0 + 16, x0: x0 + 16] = self.pred_luma_inter(x0, y0, 16, 16, mv[0], mv[1])
         for c in range(2):
@@ -1069,6 +1078,8 @@ class Decoder:
                     for x in range(8):
                         self.cur[1 + c][y0 // 2 + y, x0 // 2 + x] = r.u(8)
             m.pcm = True
+            m.qp = 0  # qPp of an I_PCM macroblock (8.7.2.2)
+            m.nz_luma = [[16] * 4 for _ in range(4)]
             self.decoded_mbs += 1
             self.stats["pcm"] += 1
             return
@@ -1094,6 +1105,7 @@ class Decoder:
         if i16 or cbp_l or cbp_c:
             self.qp = (self.qp + r.se() + 52) % 52
         qp = self.qp
+        m.qp = qp
         if i16:
             nc = self._nc(addr, sid, 0, 0, "y")
             dcl = self.residual_block(r, nc, 16)
@@ -1206,6 +1218,90 @@ class Decoder:
         x0, y0 = (addr % s.mb_w) * 8, (addr // s.mb_w) * 8
         self.cur[1 + comp][y0: y0 + 8, x0: x0 + 8] = _clip(pred + res)
 
+    # ------------------------------------------------------------------ deblocking (8.7)
+    def deblock_picture(self) -> None:
+        s = self.sps
+        Y, U, V = self.cur
+        off_c = self.pps.chroma_qp_offset
+        qpc = lambda q: QPC[max(0, min(51, q + off_c))]  # noqa: E731
+        for addr in range(s.mb_w * s.mb_h):
+            m = self.mbs[addr]
+            if not m.available:
+                continue
+            idc, off_a, off_b = self.slice_db.get(m.slice_id, (1, 0, 0))
+            if idc == 1:
+                continue
+            mx, my = addr % s.mb_w, addr // s.mb_w
+            left = self.mbs[addr - 1] if mx > 0 else None
+            top = self.mbs[addr - s.mb_w] if my > 0 else None
+            if left is not None and (not left.available or (idc == 2 and left.slice_id != m.slice_id)):
+                left = None
+            if top is not None and (not top.available or (idc == 2 and top.slice_id != m.slice_id)):
+                top = None
+            x0, y0 = mx * 16, my * 16
+            # bS per edge (0..3) and 4-line segment; vertical edges then horizontal ones
+            bsv = np.zeros((4, 4), int)
+            bsh = np.zeros((4, 4), int)
+            for e in range(4):
+                for sg in range(4):
+                    if e == 0:
+                        bsv[e, sg] = _bs(left, 3, sg, m, 0, sg, True) if left is not None else 0
+                        bsh[e, sg] = _bs(top, sg, 3, m, sg, 0, True) if top is not None else 0
+                    else:
+                        bsv[e, sg] = _bs(m, e - 1, sg, m, e, sg, False)
+                        bsh[e, sg] = _bs(m, sg, e - 1, m, sg, e, False)
+            # luma
+            for vert in (True, False):
+                bsx = bsv if vert else bsh
+                nb = left if vert else top
+                for e in range(4):
+                    if not bsx[e].any():
+                        continue
+                    qpav = ((nb.qp if e == 0 else m.qp) + m.qp + 1) >> 1
+                    bs_line = np.repeat(bsx[e], 4)
+                    if vert:
+                        c = x0 + 4 * e
+                        pl = Y[y0:y0 + 16, c - 4:c][:, ::-1].astype(np.int64)
+                        qd = Y[y0:y0 + 16, c:c + 4].astype(np.int64)
+                        _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, False)
+                        Y[y0:y0 + 16, c - 4:c] = pl[:, ::-1]
+                        Y[y0:y0 + 16, c:c + 4] = qd
+                    else:
+                        r0 = y0 + 4 * e
+                        pl = Y[r0 - 4:r0, x0:x0 + 16][::-1, :].T.astype(np.int64)
+                        qd = Y[r0:r0 + 4, x0:x0 + 16].T.astype(np.int64)
+                        _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, False)
+                        Y[r0 - 4:r0, x0:x0 + 16] = pl.T[::-1, :]
+                        Y[r0:r0 + 4, x0:x0 + 16] = qd.T
+            # chroma: edges 0 and 4 of the 8x8 block take the bS of luma edges 0 and 8, line k
+            # the bS of luma line 2k
+            for P in (U, V):
+                cx0, cy0 = x0 // 2, y0 // 2
+                for vert in (True, False):
+                    bsx = bsv if vert else bsh
+                    nb = left if vert else top
+                    for ce in range(2):
+                        e = 2 * ce
+                        if not bsx[e].any():
+                            continue
+                        qpav = (qpc(nb.qp if e == 0 else m.qp) + qpc(m.qp) + 1) >> 1
+                        bs_line = np.repeat(bsx[e], 2)
+                        z = np.zeros((8, 2), np.int64)
+                        if vert:
+                            c = cx0 + 4 * ce
+                            pl = np.concatenate([P[cy0:cy0 + 8, c - 2:c][:, ::-1].astype(np.int64), z], axis=1)
+                            qd = np.concatenate([P[cy0:cy0 + 8, c:c + 2].astype(np.int64), z], axis=1)
+                            _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, True)
+                            P[cy0:cy0 + 8, c - 2:c] = pl[:, :2][:, ::-1]
+                            P[cy0:cy0 + 8, c:c + 2] = qd[:, :2]
+                        else:
+                            r0 = cy0 + 4 * ce
+                            pl = np.concatenate([P[r0 - 2:r0, cx0:cx0 + 8][::-1, :].T.astype(np.int64), z], axis=1)
+                            qd = np.concatenate([P[r0:r0 + 2, cx0:cx0 + 8].T.astype(np.int64), z], axis=1)
+                            _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, True)
+                            P[r0 - 2:r0, cx0:cx0 + 8] = pl[:, :2].T[::-1, :]
+                            P[r0:r0 + 2, cx0:cx0 + 8] = qd[:, :2].T
+
     def decode_inter_mb(self, r, addr, sid, mb_type, x0, y0):
         if mb_type >= 3:
             raise DecodeError("P_8x8 not supported")
@@ -1241,6 +1337,7 @@ class Decoder:
         if cbp:
             self.qp = (self.qp + r.se() + 52) % 52
         qp = self.qp
+        m.qp = qp
         ac = {}
         for b in range(16):
             bx, by = BLK_XY[b]
@@ -1270,6 +1367,78 @@ class Decoder:
             self._recon_chroma(comp, addr, cpred[comp], chroma, qp)
         self.decoded_mbs += 1
         self.stats["p"] += 1
+
+
+# ----------------------------------------------------------------------------- deblocking (8.7)
+# Table 8-16 (alpha', beta' by indexA / indexB) and Table 8-17 (tC0' by indexA and bS = 1, 2, 3),
+# 8-bit video; typed in from the tables, independently of the encoder's copy.
+_DB_ALPHA = [0] * 16 + [4, 4, 5, 6, 7, 8, 9, 10, 12, 13, 15, 17, 20, 22, 25, 28, 32, 36, 40, 45, 50, 56, 63, 71,
+                        80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255]
+_DB_BETA = [0] * 16 + [2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12,
+                       13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18]
+_DB_TC0 = [(0, 0, 0)] * 17 + [
+    (0, 0, 1), (0, 0, 1), (0, 0, 1), (0, 0, 1), (0, 1, 1), (0, 1, 1), (1, 1, 1), (1, 1, 1), (1, 1, 1),
+    (1, 1, 1), (1, 1, 2), (1, 1, 2), (1, 1, 2), (1, 1, 2), (1, 2, 3), (1, 2, 3), (2, 2, 3), (2, 2, 4),
+    (2, 3, 4), (2, 3, 4), (3, 3, 5), (3, 4, 6), (3, 4, 6), (4, 5, 7), (4, 5, 8), (4, 6, 9), (5, 7, 10),
+    (6, 8, 11), (6, 8, 13), (7, 10, 14), (8, 11, 16), (9, 12, 18), (10, 13, 20), (11, 15, 23), (13, 17, 25)]
+assert len(_DB_ALPHA) == len(_DB_BETA) == len(_DB_TC0) == 52
+
+
+def _filter_edge(pl, qd, bs, qpav, off_a, off_b, chroma):
+    """Filter one edge: ``pl`` / ``qd`` are int arrays (lines, 4) holding p0..p3 / q0..q3 per line
+    (index 0 nearest the edge; chroma uses p0, p1 / q0, q1 only); ``bs`` per line.  In place."""
+    ia = min(max(qpav + off_a, 0), 51)
+    ib = min(max(qpav + off_b, 0), 51)
+    alpha, beta = _DB_ALPHA[ia], _DB_BETA[ib]
+    p0, p1, p2, p3 = pl[:, 0].copy(), pl[:, 1].copy(), pl[:, 2].copy(), pl[:, 3].copy()
+    q0, q1, q2, q3 = qd[:, 0].copy(), qd[:, 1].copy(), qd[:, 2].copy(), qd[:, 3].copy()
+    f = (bs > 0) & (np.abs(p0 - q0) < alpha) & (np.abs(p1 - p0) < beta) & (np.abs(q1 - q0) < beta)
+    if not f.any():
+        return
+    ap, aq = np.abs(p2 - p0), np.abs(q2 - q0)
+    weak = f & (bs < 4)
+    strong = f & (bs == 4)
+    if weak.any():
+        tc0 = np.array([_DB_TC0[ia][b - 1] if b > 0 else 0 for b in bs])
+        tc = tc0 + 1 if chroma else tc0 + (ap < beta) + (aq < beta)
+        d = np.clip((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc, tc)
+        pl[weak, 0] = np.clip(p0 + d, 0, 255)[weak]
+        qd[weak, 0] = np.clip(q0 - d, 0, 255)[weak]
+        if not chroma:
+            mp = weak & (ap < beta)
+            pl[mp, 1] = (p1 + np.clip((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0, tc0))[mp]
+            mq = weak & (aq < beta)
+            qd[mq, 1] = (q1 + np.clip((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0, tc0))[mq]
+    if strong.any():
+        if chroma:
+            pl[strong, 0] = ((2 * p1 + p0 + q1 + 2) >> 2)[strong]
+            qd[strong, 0] = ((2 * q1 + q0 + p1 + 2) >> 2)[strong]
+            return
+        small = np.abs(p0 - q0) < ((alpha >> 2) + 2)
+        sp = strong & (ap < beta) & small
+        wp = strong & ~((ap < beta) & small)
+        pl[sp, 0] = ((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3)[sp]
+        pl[sp, 1] = ((p2 + p1 + p0 + q0 + 2) >> 2)[sp]
+        pl[sp, 2] = ((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3)[sp]
+        pl[wp, 0] = ((2 * p1 + p0 + q1 + 2) >> 2)[wp]
+        sq = strong & (aq < beta) & small
+        wq = strong & ~((aq < beta) & small)
+        qd[sq, 0] = ((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3)[sq]
+        qd[sq, 1] = ((p0 + q0 + q1 + q2 + 2) >> 2)[sq]
+        qd[sq, 2] = ((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3)[sq]
+        qd[wq, 0] = ((2 * q1 + q0 + p1 + 2) >> 2)[wq]
+
+
+def _bs(mp: MbState, bxp, byp, mq: MbState, bxq, byq, mb_edge: bool) -> int:
+    """Boundary strength (8.7.2.1, frame macroblocks, one reference list)."""
+    if mp.intra or mq.intra:
+        return 4 if mb_edge else 3
+    if mp.nz_luma[byp][bxp] or mq.nz_luma[byq][bxq]:
+        return 2
+    if mp.ref4[byp][bxp] != mq.ref4[byq][bxq]:
+        return 1
+    a, b = mp.mv4[byp][bxp], mq.mv4[byq][bxq]
+    return 1 if (abs(a[0] - b[0]) >= 4 or abs(a[1] - b[1]) >= 4) else 0
 
 
 def decode_annexb(stream: bytes) -> list[tuple[np.ndarray, np.ndarray, np.ndarray]]:
