@@ -657,6 +657,10 @@ class Decoder:
     @staticmethod
     def idct4(d: np.ndarray) -> np.ndarray:
         d = d.astype(np.int64)
+        if not d.any():
+            return np.zeros((4, 4), np.int64)
+        if not d.ravel()[1:].any():  # DC only: every output sample is (dc + 32) >> 6
+            return np.full((4, 4), (int(d[0, 0]) + 32) >> 6, np.int64)
         f = np.zeros((4, 4), np.int64)
         for i in range(4):
             e0 = d[i, 0] + d[i, 2]
@@ -684,6 +688,8 @@ class Decoder:
     @staticmethod
     def dequant(c: np.ndarray, qp: int, skip_dc: bool) -> np.ndarray:
         d = np.zeros((4, 4), np.int64)
+        if not c.any():
+            return d
         for y in range(4):
             for x in range(4):
                 if skip_dc and x == 0 and y == 0:
@@ -910,7 +916,7 @@ class Decoder:
 
     # ------------------------------------------------------------------ inter prediction
     def _ref_padded(self):
-        if getattr(self, "_ref_id", None) is not id(self.ref):
+        if getattr(self, "_ref_id", None) != id(self.ref):
             P = self.PAD
             self._refp = [np.pad(pl.astype(np.int64), P, mode="edge") for pl in self.ref]
             self._ref_id = id(self.ref)
@@ -1220,87 +1226,120 @@ class Decoder:
 
     # ------------------------------------------------------------------ deblocking (8.7)
     def deblock_picture(self) -> None:
+        """8.7 over the whole picture.  The process is defined macroblock by macroblock in raster
+        order; macroblocks on one anti-diagonal x + 2y = t never touch each other's samples (a
+        macroblock depends on its left, upper and upper-right neighbours only), so each diagonal
+        is filtered as one vectorised step -- the same result as the raster order, in
+        mb_w + 2 mb_h steps instead of mb_w * mb_h."""
         s = self.sps
-        Y, U, V = self.cur
+        mw, mh = s.mb_w, s.mb_h
+        n = mw * mh
         off_c = self.pps.chroma_qp_offset
-        qpc = lambda q: QPC[max(0, min(51, q + off_c))]  # noqa: E731
-        for addr in range(s.mb_w * s.mb_h):
-            m = self.mbs[addr]
-            if not m.available:
+        # per-MB records
+        idc = np.ones(n, int)
+        offa = np.zeros(n, int)
+        offb = np.zeros(n, int)
+        qp = np.zeros(n, int)
+        for i, m in enumerate(self.mbs):
+            if m.available:
+                idc[i], offa[i], offb[i] = self.slice_db.get(m.slice_id, (1, 0, 0))
+                qp[i] = m.qp
+        if (idc == 1).all():
+            return
+        bsv = np.zeros((n, 4, 4), int)  # [mb, edge, segment]
+        bsh = np.zeros((n, 4, 4), int)
+        for i, m in enumerate(self.mbs):
+            if idc[i] == 1 or not m.available:
                 continue
-            idc, off_a, off_b = self.slice_db.get(m.slice_id, (1, 0, 0))
-            if idc == 1:
-                continue
-            mx, my = addr % s.mb_w, addr // s.mb_w
-            left = self.mbs[addr - 1] if mx > 0 else None
-            top = self.mbs[addr - s.mb_w] if my > 0 else None
-            if left is not None and (not left.available or (idc == 2 and left.slice_id != m.slice_id)):
+            mx, my = i % mw, i // mw
+            left = self.mbs[i - 1] if mx > 0 else None
+            top = self.mbs[i - mw] if my > 0 else None
+            if left is not None and (not left.available or (idc[i] == 2 and left.slice_id != m.slice_id)):
                 left = None
-            if top is not None and (not top.available or (idc == 2 and top.slice_id != m.slice_id)):
+            if top is not None and (not top.available or (idc[i] == 2 and top.slice_id != m.slice_id)):
                 top = None
-            x0, y0 = mx * 16, my * 16
-            # bS per edge (0..3) and 4-line segment; vertical edges then horizontal ones
-            bsv = np.zeros((4, 4), int)
-            bsh = np.zeros((4, 4), int)
-            for e in range(4):
-                for sg in range(4):
-                    if e == 0:
-                        bsv[e, sg] = _bs(left, 3, sg, m, 0, sg, True) if left is not None else 0
-                        bsh[e, sg] = _bs(top, sg, 3, m, sg, 0, True) if top is not None else 0
-                    else:
-                        bsv[e, sg] = _bs(m, e - 1, sg, m, e, sg, False)
-                        bsh[e, sg] = _bs(m, sg, e - 1, m, sg, e, False)
-            # luma
-            for vert in (True, False):
-                bsx = bsv if vert else bsh
-                nb = left if vert else top
+            for sg in range(4):
+                bsv[i, 0, sg] = _bs(left, 3, sg, m, 0, sg, True) if left is not None else 0
+                bsh[i, 0, sg] = _bs(top, sg, 3, m, sg, 0, True) if top is not None else 0
+                for e in range(1, 4):
+                    bsv[i, e, sg] = _bs(m, e - 1, sg, m, e, sg, False)
+                    bsh[i, e, sg] = _bs(m, sg, e - 1, m, sg, e, False)
+        qpc = np.array(QPC)[np.clip(qp + off_c, 0, 51)]
+        Yp = np.pad(self.cur[0], ((4, 0), (4, 0)))
+        Cp = [np.pad(c, ((2, 0), (2, 0))) for c in self.cur[1:]]
+        for t in range(mw + 2 * (mh - 1) + 1):
+            ys = np.arange(max(0, (t - mw + 2) // 2), min(mh - 1, t // 2) + 1)
+            xs = t - 2 * ys
+            ok = (xs >= 0) & (xs < mw)
+            ys, xs = ys[ok], xs[ok]
+            if len(ys) == 0:
+                continue
+            ids = ys * mw + xs
+            keep = idc[ids] != 1
+            ys, xs, ids = ys[keep], xs[keep], ids[keep]
+            if len(ids) == 0:
+                continue
+            qn = qp[ids]
+            ql = qp[np.maximum(ids - 1, 0)]
+            qt = qp[np.maximum(ids - mw, 0)]
+            # luma: region rows 16y-4 .. 16y+15, cols 16x-4 .. 16x+15 (padded coordinates + 4)
+            rr = (ys[:, None] * 16 + np.arange(20))[:, :, None]
+            cc = (xs[:, None] * 16 + np.arange(20))[:, None, :]
+            R = Yp[rr, cc].astype(np.int64)
+            for vert, bsx in ((True, bsv), (False, bsh)):
                 for e in range(4):
-                    if not bsx[e].any():
+                    b = np.repeat(bsx[ids, e], 4, axis=1)  # (k, 16 lines)
+                    if not b.any():
                         continue
-                    qpav = ((nb.qp if e == 0 else m.qp) + m.qp + 1) >> 1
-                    bs_line = np.repeat(bsx[e], 4)
+                    qa = (((ql if vert else qt) if e == 0 else qn) + qn + 1) >> 1
+                    k = 4 + 4 * e
                     if vert:
-                        c = x0 + 4 * e
-                        pl = Y[y0:y0 + 16, c - 4:c][:, ::-1].astype(np.int64)
-                        qd = Y[y0:y0 + 16, c:c + 4].astype(np.int64)
-                        _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, False)
-                        Y[y0:y0 + 16, c - 4:c] = pl[:, ::-1]
-                        Y[y0:y0 + 16, c:c + 4] = qd
+                        pl = R[:, 4:20, k - 4:k][:, :, ::-1]
+                        qd = R[:, 4:20, k:k + 4]
                     else:
-                        r0 = y0 + 4 * e
-                        pl = Y[r0 - 4:r0, x0:x0 + 16][::-1, :].T.astype(np.int64)
-                        qd = Y[r0:r0 + 4, x0:x0 + 16].T.astype(np.int64)
-                        _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, False)
-                        Y[r0 - 4:r0, x0:x0 + 16] = pl.T[::-1, :]
-                        Y[r0:r0 + 4, x0:x0 + 16] = qd.T
-            # chroma: edges 0 and 4 of the 8x8 block take the bS of luma edges 0 and 8, line k
-            # the bS of luma line 2k
-            for P in (U, V):
-                cx0, cy0 = x0 // 2, y0 // 2
-                for vert in (True, False):
-                    bsx = bsv if vert else bsh
-                    nb = left if vert else top
+                        pl = R[:, k - 4:k, 4:20][:, ::-1, :].transpose(0, 2, 1)
+                        qd = R[:, k:k + 4, 4:20].transpose(0, 2, 1)
+                    P2, Q2 = pl.reshape(-1, 4).copy(), qd.reshape(-1, 4).copy()
+                    _filter_lines(P2, Q2, b.reshape(-1), np.repeat(qa, 16), np.repeat(offa[ids], 16),
+                                  np.repeat(offb[ids], 16), False)
+                    if vert:
+                        R[:, 4:20, k - 4:k] = P2.reshape(-1, 16, 4)[:, :, ::-1]
+                        R[:, 4:20, k:k + 4] = Q2.reshape(-1, 16, 4)
+                    else:
+                        R[:, k - 4:k, 4:20] = P2.reshape(-1, 16, 4).transpose(0, 2, 1)[:, ::-1, :]
+                        R[:, k:k + 4, 4:20] = Q2.reshape(-1, 16, 4).transpose(0, 2, 1)
+            Yp[rr, cc] = R
+            # chroma: region rows 8y-2 .. 8y+7, cols 8x-2 .. 8x+7; edges 0 / 4 take luma edges 0 / 8
+            rr = (ys[:, None] * 8 + np.arange(10))[:, :, None]
+            cc = (xs[:, None] * 8 + np.arange(10))[:, None, :]
+            qcn, qcl, qct = qpc[ids], qpc[np.maximum(ids - 1, 0)], qpc[np.maximum(ids - mw, 0)]
+            for Pc in Cp:
+                R = Pc[rr, cc].astype(np.int64)
+                for vert, bsx in ((True, bsv), (False, bsh)):
                     for ce in range(2):
-                        e = 2 * ce
-                        if not bsx[e].any():
+                        b = np.repeat(bsx[ids, 2 * ce], 2, axis=1)  # (k, 8 lines)
+                        if not b.any():
                             continue
-                        qpav = (qpc(nb.qp if e == 0 else m.qp) + qpc(m.qp) + 1) >> 1
-                        bs_line = np.repeat(bsx[e], 2)
-                        z = np.zeros((8, 2), np.int64)
+                        qa = (((qcl if vert else qct) if ce == 0 else qcn) + qcn + 1) >> 1
+                        k = 2 + 4 * ce
+                        z = np.zeros((len(ids), 8, 2), np.int64)
                         if vert:
-                            c = cx0 + 4 * ce
-                            pl = np.concatenate([P[cy0:cy0 + 8, c - 2:c][:, ::-1].astype(np.int64), z], axis=1)
-                            qd = np.concatenate([P[cy0:cy0 + 8, c:c + 2].astype(np.int64), z], axis=1)
-                            _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, True)
-                            P[cy0:cy0 + 8, c - 2:c] = pl[:, :2][:, ::-1]
-                            P[cy0:cy0 + 8, c:c + 2] = qd[:, :2]
+                            pl = np.concatenate([R[:, 2:10, k - 2:k][:, :, ::-1], z], axis=2)
+                            qd = np.concatenate([R[:, 2:10, k:k + 2], z], axis=2)
                         else:
-                            r0 = cy0 + 4 * ce
-                            pl = np.concatenate([P[r0 - 2:r0, cx0:cx0 + 8][::-1, :].T.astype(np.int64), z], axis=1)
-                            qd = np.concatenate([P[r0:r0 + 2, cx0:cx0 + 8].T.astype(np.int64), z], axis=1)
-                            _filter_edge(pl, qd, bs_line, qpav, off_a, off_b, True)
-                            P[r0 - 2:r0, cx0:cx0 + 8] = pl[:, :2].T[::-1, :]
-                            P[r0:r0 + 2, cx0:cx0 + 8] = qd[:, :2].T
+                            pl = np.concatenate([R[:, k - 2:k, 2:10][:, ::-1, :].transpose(0, 2, 1), z], axis=2)
+                            qd = np.concatenate([R[:, k:k + 2, 2:10].transpose(0, 2, 1), z], axis=2)
+                        P2, Q2 = pl.reshape(-1, 4).copy(), qd.reshape(-1, 4).copy()
+                        _filter_lines(P2, Q2, b.reshape(-1), np.repeat(qa, 8), np.repeat(offa[ids], 8),
+                                      np.repeat(offb[ids], 8), True)
+                        if vert:
+                            R[:, 2:10, k - 2:k] = P2.reshape(-1, 8, 4)[:, :, 1::-1]
+                            R[:, 2:10, k:k + 2] = Q2.reshape(-1, 8, 4)[:, :, :2]
+                        else:
+                            R[:, k - 2:k, 2:10] = P2.reshape(-1, 8, 4)[:, :, 1::-1].transpose(0, 2, 1)
+                            R[:, k:k + 2, 2:10] = Q2.reshape(-1, 8, 4)[:, :, :2].transpose(0, 2, 1)
+                Pc[rr, cc] = R
+        self.cur = (Yp[4:, 4:], Cp[0][2:, 2:], Cp[1][2:, 2:])
 
     def decode_inter_mb(self, r, addr, sid, mb_type, x0, y0):
         if mb_type >= 3:
@@ -1384,30 +1423,35 @@ _DB_TC0 = [(0, 0, 0)] * 17 + [
 assert len(_DB_ALPHA) == len(_DB_BETA) == len(_DB_TC0) == 52
 
 
-def _filter_edge(pl, qd, bs, qpav, off_a, off_b, chroma):
-    """Filter one edge: ``pl`` / ``qd`` are int arrays (lines, 4) holding p0..p3 / q0..q3 per line
-    (index 0 nearest the edge; chroma uses p0, p1 / q0, q1 only); ``bs`` per line.  In place."""
-    ia = min(max(qpav + off_a, 0), 51)
-    ib = min(max(qpav + off_b, 0), 51)
-    alpha, beta = _DB_ALPHA[ia], _DB_BETA[ib]
-    p0, p1, p2, p3 = pl[:, 0].copy(), pl[:, 1].copy(), pl[:, 2].copy(), pl[:, 3].copy()
-    q0, q1, q2, q3 = qd[:, 0].copy(), qd[:, 1].copy(), qd[:, 2].copy(), qd[:, 3].copy()
+_A_T = np.array(_DB_ALPHA)
+_B_T = np.array(_DB_BETA)
+_TC_T = np.array(_DB_TC0)
+
+
+def _filter_lines(pl, qd, bs, qpav, off_a, off_b, chroma):
+    """Vectorised 8.7.2.3 / 8.7.2.4 over lines with per-line bS, qPav and slice offsets;
+    ``pl`` / ``qd``: (lines, 4) p0..p3 / q0..q3 (index 0 nearest the edge).  In place."""
+    ia = np.clip(qpav + off_a, 0, 51)
+    ib = np.clip(qpav + off_b, 0, 51)
+    alpha, beta = _A_T[ia], _B_T[ib]
+    p0, p1, p2, p3 = (pl[:, i].copy() for i in range(4))
+    q0, q1, q2, q3 = (qd[:, i].copy() for i in range(4))
     f = (bs > 0) & (np.abs(p0 - q0) < alpha) & (np.abs(p1 - p0) < beta) & (np.abs(q1 - q0) < beta)
     if not f.any():
         return
-    ap, aq = np.abs(p2 - p0), np.abs(q2 - q0)
+    ap, aq = np.abs(p2 - p0) < beta, np.abs(q2 - q0) < beta
     weak = f & (bs < 4)
     strong = f & (bs == 4)
     if weak.any():
-        tc0 = np.array([_DB_TC0[ia][b - 1] if b > 0 else 0 for b in bs])
-        tc = tc0 + 1 if chroma else tc0 + (ap < beta) + (aq < beta)
+        tc0 = np.where(bs > 0, _TC_T[ia, np.clip(bs - 1, 0, 2)], 0)
+        tc = tc0 + 1 if chroma else tc0 + ap + aq
         d = np.clip((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc, tc)
         pl[weak, 0] = np.clip(p0 + d, 0, 255)[weak]
         qd[weak, 0] = np.clip(q0 - d, 0, 255)[weak]
         if not chroma:
-            mp = weak & (ap < beta)
+            mp = weak & ap
             pl[mp, 1] = (p1 + np.clip((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0, tc0))[mp]
-            mq = weak & (aq < beta)
+            mq = weak & aq
             qd[mq, 1] = (q1 + np.clip((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0, tc0))[mq]
     if strong.any():
         if chroma:
@@ -1415,14 +1459,12 @@ def _filter_edge(pl, qd, bs, qpav, off_a, off_b, chroma):
             qd[strong, 0] = ((2 * q1 + q0 + p1 + 2) >> 2)[strong]
             return
         small = np.abs(p0 - q0) < ((alpha >> 2) + 2)
-        sp = strong & (ap < beta) & small
-        wp = strong & ~((ap < beta) & small)
+        sp, wp = strong & ap & small, strong & ~(ap & small)
         pl[sp, 0] = ((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3)[sp]
         pl[sp, 1] = ((p2 + p1 + p0 + q0 + 2) >> 2)[sp]
         pl[sp, 2] = ((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3)[sp]
         pl[wp, 0] = ((2 * p1 + p0 + q1 + 2) >> 2)[wp]
-        sq = strong & (aq < beta) & small
-        wq = strong & ~((aq < beta) & small)
+        sq, wq = strong & aq & small, strong & ~(aq & small)
         qd[sq, 0] = ((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3)[sq]
         qd[sq, 1] = ((p0 + q0 + q1 + q2 + 2) >> 2)[sq]
         qd[sq, 2] = ((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3)[sq]
