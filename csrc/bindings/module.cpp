@@ -10,6 +10,7 @@
 
 #include "../codec/h264_core.h"
 #include "../codec/h264_encoder.h"
+#include "../codec/vp8_encoder.h"
 #include "../codec/hevc_encoder.h"
 #include "../common/hip_check.h"
 #include "../common/trace.h"
@@ -230,6 +231,57 @@ PYBIND11_MODULE(_native, m) {
         .def("request_idr", [](h264::CpuH264Encoder& e) { e.common().request_idr(); })
         .def("set_bitrate", [](h264::CpuH264Encoder& e, int k) { e.common().set_bitrate(k); })
         .def_property_readonly("stats", &h264::CpuH264Encoder::last_stats);
+
+    py::class_<vp8::CpuVp8Encoder>(m, "CpuVp8Encoder")
+        .def(py::init<const h264::EncoderConfig&>())
+        .def(
+            "encode",
+            [](vp8::CpuVp8Encoder& e, py::array_t<uint8_t, py::array::c_style> y,
+               py::array_t<uint8_t, py::array::c_style> uv, bool force_idr) {
+                if (y.ndim() != 2 || uv.ndim() != 2 || y.shape(1) != uv.shape(1))
+                    throw std::invalid_argument("y (H,P) and uv (H/2,P) planes with equal pitch");
+                const int pitch = (int)y.shape(1);
+                const int cw = e.coded_pitch();
+                const auto& cfg = e.common().config();
+                const int ch = e.common().mb_h() * 16;
+                std::vector<uint8_t> py_, puv;
+                const uint8_t* yy = y.data();
+                const uint8_t* uu = uv.data();
+                int p = pitch;
+                if (y.shape(0) < ch || pitch < cw) {
+                    h264::pad_nv12(yy, uu, cfg.width, cfg.height, pitch, cw, ch, py_, puv);
+                    yy = py_.data();
+                    uu = puv.data();
+                    p = cw;
+                }
+                const auto& au = e.encode(yy, uu, p, force_idr);
+                return to_bytes(au);
+            },
+            py::arg("y"), py::arg("uv"), py::arg("force_idr") = false)
+        .def("recon",
+             [](vp8::CpuVp8Encoder& e) {
+                 const int cw = e.coded_pitch(), ch = e.common().mb_h() * 16;
+                 py::array_t<uint8_t> y({ch, cw}), uv({ch / 2, cw});
+                 std::memcpy(y.mutable_data(), e.recon_y().data(), (size_t)cw * ch);
+                 std::memcpy(uv.mutable_data(), e.recon_uv().data(), (size_t)cw * ch / 2);
+                 return py::make_tuple(y, uv);
+             })
+        .def("mb_info",
+             [](vp8::CpuVp8Encoder& e) {  // (nmb, 4): ymode, uvmode, mvx, mvy (1/8 samples)
+                 const auto& v = e.mb_info();
+                 py::array_t<int32_t> a({(py::ssize_t)v.size(), (py::ssize_t)4});
+                 int32_t* d = a.mutable_data();
+                 for (size_t i = 0; i < v.size(); ++i) {
+                     d[4 * i] = v[i].ymode;
+                     d[4 * i + 1] = v[i].uvmode;
+                     d[4 * i + 2] = v[i].mvx;
+                     d[4 * i + 3] = v[i].mvy;
+                 }
+                 return a;
+             })
+        .def("request_idr", [](vp8::CpuVp8Encoder& e) { e.common().request_idr(); })
+        .def("set_bitrate", [](vp8::CpuVp8Encoder& e, int k) { e.common().set_bitrate(k); })
+        .def_property_readonly("stats", &vp8::CpuVp8Encoder::last_stats);
 
     py::class_<hevc::CpuHevcEncoder>(m, "CpuHevcEncoder")
         .def(py::init<const h264::EncoderConfig&>())

@@ -1,0 +1,391 @@
+// VP8 frame writer (RFC 6386 sections 9, 13, 16, 17, 19): frame tag, key-frame start code and
+// size, the first partition (frame header + per-macroblock modes and motion vectors) and the
+// token partitions (one per MB row modulo the partition count, written concurrently -- a token
+// partition's contexts depend only on the coefficients, which are known before coding starts).
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "vp8_encoder.h"
+
+namespace mx {
+namespace vp8 {
+
+namespace {
+
+inline const uint8_t* coef_probs(int type, int band, int ctx) { return kCoefProbs0 + ((type * 8 + band) * 3 + ctx) * 11; }
+
+void put_extra(BoolEncoder& e, int v, const uint8_t* p, int n) {
+    for (int k = n - 1; k >= 0; --k) e.put(p[n - 1 - k], (v >> k) & 1);
+}
+
+// One block's tokens (13.2 / 13.3); returns whether it has a non-zero level.
+void put_block(BoolEncoder& e, const int16_t* lv, int first, int type, int ctx) {
+    int last = 15;
+    while (last >= first && lv[last] == 0) --last;
+    if (last < first) {
+        e.put(coef_probs(type, kBand[first], ctx)[0], 0);  // EOB
+        return;
+    }
+    bool prev_zero = false;
+    for (int i = first; i <= last; ++i) {
+        const uint8_t* P = coef_probs(type, kBand[i], ctx);
+        if (!prev_zero) e.put(P[0], 1);  // not EOB
+        const int v = lv[i], a = v < 0 ? -v : v;
+        if (a == 0) {
+            e.put(P[1], 0);
+            ctx = 0;
+            prev_zero = true;
+            continue;
+        }
+        e.put(P[1], 1);
+        if (a == 1) {
+            e.put(P[2], 0);
+        } else {
+            e.put(P[2], 1);
+            if (a <= 4) {
+                e.put(P[3], 0);
+                if (a == 2) {
+                    e.put(P[4], 0);
+                } else {
+                    e.put(P[4], 1);
+                    e.put(P[5], a == 4);
+                }
+            } else {
+                e.put(P[3], 1);
+                if (a <= 10) {
+                    e.put(P[6], 0);
+                    if (a <= 6) {
+                        e.put(P[7], 0);
+                        put_extra(e, a - 5, kPcat1, 1);
+                    } else {
+                        e.put(P[7], 1);
+                        put_extra(e, a - 7, kPcat2, 2);
+                    }
+                } else {
+                    e.put(P[6], 1);
+                    if (a <= 34) {
+                        e.put(P[8], 0);
+                        if (a <= 18) {
+                            e.put(P[9], 0);
+                            put_extra(e, a - 11, kPcat3, 3);
+                        } else {
+                            e.put(P[9], 1);
+                            put_extra(e, a - 19, kPcat4, 4);
+                        }
+                    } else {
+                        e.put(P[8], 1);
+                        if (a <= 66) {
+                            e.put(P[10], 0);
+                            put_extra(e, a - 35, kPcat5, 5);
+                        } else {
+                            e.put(P[10], 1);
+                            put_extra(e, a - 67, kPcat6, 11);
+                        }
+                    }
+                }
+            }
+        }
+        e.put(128, v < 0);
+        ctx = a == 1 ? 1 : 2;
+        prev_zero = false;
+    }
+    if (last < 15) e.put(coef_probs(type, kBand[last + 1], ctx)[0], 0);  // EOB
+}
+
+inline int nzb(const Vp8Mb& m, int b) { return (m.nz >> b) & 1; }
+
+// Token partition `p`: MB rows p, p + n, ...
+void write_tokens(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels, int p, int n,
+                  std::vector<uint8_t>& out) {
+    BoolEncoder e(out);
+    for (int mby = p; mby < f.mb_h; mby += n) {
+        int left[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // Y0..3 (rows), U0..1, V0..1, Y2
+        for (int mbx = 0; mbx < f.mb_w; ++mbx) {
+            const int i = mby * f.mb_w + mbx;
+            const Vp8Mb& m = mbs[i];
+            if (m.nz == 0) {  // mb_skip_coeff: no tokens, contexts reset (the MB has a Y2 block)
+                for (int& l : left) l = 0;
+                continue;
+            }
+            const Vp8Mb* up = mby > 0 ? &mbs[i - f.mb_w] : nullptr;
+            const int16_t* lv = levels(i);
+            // Y2 (type 1)
+            {
+                const int ctx = (up ? nzb(*up, kY2) : 0) + left[8];
+                put_block(e, lv + kY2 * 16, 0, 1, ctx);
+                left[8] = nzb(m, kY2);
+            }
+            for (int b = 0; b < 16; ++b) {  // Y after Y2 (type 0, from coefficient 1)
+                const int bx = b & 3, by = b >> 2;
+                const int above = by > 0 ? nzb(m, b - 4) : (up ? nzb(*up, 12 + bx) : 0);
+                put_block(e, lv + b * 16, 1, 0, above + left[by]);
+                left[by] = nzb(m, b);
+            }
+            for (int c = 0; c < 2; ++c)
+                for (int b = 0; b < 4; ++b) {  // chroma (type 2)
+                    const int blk = 16 + 4 * c + b, bx = b & 1, by = b >> 1;
+                    const int above = by > 0 ? nzb(m, blk - 2) : (up ? nzb(*up, blk + 2) : 0);
+                    put_block(e, lv + blk * 16, 0, 2, above + left[4 + 2 * c + by]);
+                    left[4 + 2 * c + by] = nzb(m, blk);
+                }
+        }
+    }
+    e.flush();
+}
+
+inline void clamp_mv(int mv[2], int mb_w, int mb_h, int mbx, int mby) {
+    // vp8_clamp_mv2: the block may reach 16 samples beyond the picture (1/8-sample units)
+    const int lo_x = -((mbx * 16) << 3) - (16 << 3), hi_x = (((mb_w - 1 - mbx) * 16) << 3) + (16 << 3);
+    const int lo_y = -((mby * 16) << 3) - (16 << 3), hi_y = (((mb_h - 1 - mby) * 16) << 3) + (16 << 3);
+    mv[0] = std::clamp(mv[0], lo_x, hi_x);
+    mv[1] = std::clamp(mv[1], lo_y, hi_y);
+}
+
+void put_mv_component(BoolEncoder& e, int v, const uint8_t* p) {
+    // v in quarter samples (the decoder doubles it)
+    const int a = v < 0 ? -v : v;
+    if (a < 8) {
+        e.put(p[0], 0);
+        // small tree: {2, 8, 4, 6, -0, -1, -2, -3, 10, 12, -4, -5, -6, -7}, probabilities p[2 + node / 2]
+        e.put(p[2], a >= 4);
+        if (a < 4) {
+            e.put(p[3], a >= 2);
+            e.put(p[a < 2 ? 4 : 5], a & 1);
+        } else {
+            e.put(p[6], a >= 6);
+            e.put(p[a < 6 ? 7 : 8], a & 1);
+        }
+        if (a) e.put(p[1], v < 0);
+        return;
+    }
+    e.put(p[0], 1);
+    for (int i = 0; i < 3; ++i) e.put(p[9 + i], (a >> i) & 1);
+    for (int i = 9; i > 3; --i) e.put(p[9 + i], (a >> i) & 1);
+    if (a & 0xfff0) e.put(p[9 + 3], (a >> 3) & 1);
+    e.put(p[1], v < 0);
+}
+
+}  // namespace
+
+void find_near_mvs(const Vp8Mb* mbs, int mb_w, int mb_h, int mbx, int mby, int near_mv[3][2], int cnt[4]) {
+    int mv[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
+    int idx = 0;  // index of the last distinct vector stored
+    auto is_inter = [&](int x, int y) { return x >= 0 && y >= 0 && x < mb_w && mbs[y * mb_w + x].ymode == kInter; };
+    auto mv_of = [&](int x, int y, int o[2]) {
+        o[0] = mbs[y * mb_w + x].mvx;
+        o[1] = mbs[y * mb_w + x].mvy;
+    };
+    // above (weight 2), left (2), above-left (1); outside the picture counts as intra
+    const int nx[3] = {mbx, mbx - 1, mbx - 1}, ny[3] = {mby - 1, mby, mby - 1}, wt[3] = {2, 2, 1};
+    for (int k = 0; k < 3; ++k) {
+        if (!is_inter(nx[k], ny[k])) continue;
+        int t[2];
+        mv_of(nx[k], ny[k], t);
+        if (t[0] | t[1]) {
+            if (k == 0 || t[0] != mv[idx][0] || t[1] != mv[idx][1]) {
+                ++idx;
+                mv[idx][0] = t[0];
+                mv[idx][1] = t[1];
+            }
+            cnt[idx] += wt[k];
+        } else {
+            cnt[0] += wt[k];
+        }
+    }
+    // three distinct vectors and the last equals the first: the nearest gains a vote
+    if (cnt[3] && mv[idx][0] == mv[1][0] && mv[idx][1] == mv[1][1]) cnt[1] += 1;
+    cnt[3] = 0;  // no SPLITMV neighbours
+    if (cnt[2] > cnt[1]) {
+        std::swap(cnt[1], cnt[2]);
+        std::swap(mv[1][0], mv[2][0]);
+        std::swap(mv[1][1], mv[2][1]);
+    }
+    if (cnt[1] >= cnt[0]) {
+        mv[0][0] = mv[1][0];
+        mv[0][1] = mv[1][1];
+    }
+    for (int k = 0; k < 3; ++k) {
+        near_mv[k][0] = mv[k][0];
+        near_mv[k][1] = mv[k][1];
+        clamp_mv(near_mv[k], mb_w, mb_h, mbx, mby);
+    }
+}
+
+void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels,
+                 std::vector<uint8_t>& out,
+                 const std::function<void(int, const std::function<void(int)>&)>& run_parallel) {
+    const int nmb = f.mb_w * f.mb_h;
+    const int nparts = 1 << f.log2_parts;
+    int coded = 0;
+    for (int i = 0; i < nmb; ++i) coded += mbs[i].nz != 0;
+    const int prob_skip_false = std::clamp((coded * 256 + nmb / 2) / std::max(1, nmb), 1, 255);
+    // ---- first partition
+    std::vector<uint8_t> p1;
+    p1.reserve(16 + (size_t)nmb / 2);
+    {
+        BoolEncoder e(p1);
+        if (f.key) {
+            e.literal(0, 1);  // color_space
+            e.literal(0, 1);  // clamping_type (decoder clamps reconstructed samples)
+        }
+        e.literal(0, 1);  // segmentation_enabled
+        e.literal(0, 1);  // filter_type (normal)
+        e.literal(0, 6);  // loop_filter_level 0: no loop filter
+        e.literal(0, 3);  // sharpness_level
+        e.literal(0, 1);  // loop_filter_adj_enable
+        e.literal((uint32_t)f.log2_parts, 2);
+        e.literal((uint32_t)f.qindex, 7);  // y_ac_qi
+        for (int k = 0; k < 5; ++k) e.literal(0, 1);  // no quantiser deltas
+        if (f.key) {
+            e.literal(0, 1);  // refresh_entropy_probs: probabilities of this frame not kept
+        } else {
+            e.literal(0, 1);  // refresh_golden_frame
+            e.literal(0, 1);  // refresh_alternate_frame
+            e.literal(0, 2);  // copy_buffer_to_golden: none
+            e.literal(0, 2);  // copy_buffer_to_alternate: none
+            e.literal(0, 1);  // sign_bias_golden
+            e.literal(0, 1);  // sign_bias_alternate
+            e.literal(0, 1);  // refresh_entropy_probs
+            e.literal(1, 1);  // refresh_last
+        }
+        for (int k = 0; k < 1056; ++k) e.put(kCoefUpdateProbs[k], 0);  // no token probability updates
+        e.literal(1, 1);  // mb_no_skip_coeff
+        e.literal((uint32_t)prob_skip_false, 8);
+        const int prob_intra = 1, prob_last = 255, prob_gf = 128;
+        if (!f.key) {
+            e.literal(prob_intra, 8);
+            e.literal(prob_last, 8);
+            e.literal(prob_gf, 8);
+            e.literal(0, 1);  // intra_16x16_prob_update_flag
+            e.literal(0, 1);  // intra_chroma_prob_update_flag
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 19; ++k) e.put(kMvUpdateProbs[c][k], 0);  // no mv probability updates
+        }
+        for (int mby = 0; mby < f.mb_h; ++mby)
+            for (int mbx = 0; mbx < f.mb_w; ++mbx) {
+                const Vp8Mb& m = mbs[mby * f.mb_w + mbx];
+                e.put(prob_skip_false, m.nz == 0);
+                if (f.key) {
+                    const uint8_t* p = kKfYModeProb;  // tree: B_PRED "0", DC "100", V "101", H "110", TM "111"
+                    e.put(p[0], 1);
+                    e.put(p[1], m.ymode >= kHPred);
+                    e.put(m.ymode >= kHPred ? p[3] : p[2], m.ymode == kVPred || m.ymode == kTmPred);
+                    const uint8_t* q = kKfUvModeProb;  // DC "0", V "10", H "110", TM "111"
+                    e.put(q[0], m.uvmode != kDcPred);
+                    if (m.uvmode != kDcPred) {
+                        e.put(q[1], m.uvmode != kVPred);
+                        if (m.uvmode != kVPred) e.put(q[2], m.uvmode == kTmPred);
+                    }
+                    continue;
+                }
+                if (m.ymode != kInter) throw std::logic_error("vp8 writer: intra MB in an inter frame");
+                e.put(prob_intra, 1);  // is_inter_mb
+                e.put(prob_last, 0);   // reference: last frame
+                int near[3][2], cnt[4];
+                find_near_mvs(mbs, f.mb_w, f.mb_h, mbx, mby, near, cnt);
+                const uint8_t pr[4] = {kModeContexts[cnt[0]][0], kModeContexts[cnt[1]][1], kModeContexts[cnt[2]][2],
+                                       kModeContexts[cnt[3]][3]};
+                if (m.mvx == 0 && m.mvy == 0) {
+                    e.put(pr[0], 0);  // ZEROMV
+                    continue;
+                }
+                e.put(pr[0], 1);
+                if (m.mvx == near[1][0] && m.mvy == near[1][1]) {
+                    e.put(pr[1], 0);  // NEARESTMV
+                    continue;
+                }
+                e.put(pr[1], 1);
+                if (m.mvx == near[2][0] && m.mvy == near[2][1]) {
+                    e.put(pr[2], 0);  // NEARMV
+                    continue;
+                }
+                e.put(pr[2], 1);
+                e.put(pr[3], 0);  // NEWMV (not SPLITMV)
+                put_mv_component(e, (m.mvy - near[0][1]) / 2, kMvDefault[0]);  // row first
+                put_mv_component(e, (m.mvx - near[0][0]) / 2, kMvDefault[1]);
+            }
+        e.flush();
+    }
+    if (p1.size() >= (1u << 19)) throw std::runtime_error("vp8 writer: first partition too large");
+    // ---- token partitions, concurrently
+    std::vector<std::vector<uint8_t>> parts((size_t)nparts);
+    run_parallel(nparts, [&](int p) {
+        parts[(size_t)p].reserve(4096);
+        write_tokens(f, mbs, levels, p, nparts, parts[(size_t)p]);
+    });
+    // ---- assemble: frame tag, key-frame start code + size, partition 1, partition sizes, data
+    const uint32_t tag = (f.key ? 0u : 1u) | (0u << 1) | (1u << 4) | ((uint32_t)p1.size() << 5);
+    out.push_back((uint8_t)tag);
+    out.push_back((uint8_t)(tag >> 8));
+    out.push_back((uint8_t)(tag >> 16));
+    if (f.key) {
+        const uint8_t sc[3] = {0x9d, 0x01, 0x2a};
+        out.insert(out.end(), sc, sc + 3);
+        out.push_back((uint8_t)(f.width & 0xff));
+        out.push_back((uint8_t)((f.width >> 8) & 0x3f));
+        out.push_back((uint8_t)(f.height & 0xff));
+        out.push_back((uint8_t)((f.height >> 8) & 0x3f));
+    }
+    out.insert(out.end(), p1.begin(), p1.end());
+    for (int p = 0; p + 1 < nparts; ++p) {
+        const uint32_t n = (uint32_t)parts[(size_t)p].size();
+        out.push_back((uint8_t)n);
+        out.push_back((uint8_t)(n >> 8));
+        out.push_back((uint8_t)(n >> 16));
+    }
+    for (const auto& p : parts) out.insert(out.end(), p.begin(), p.end());
+}
+
+// ------------------------------------------------------------------ partition worker pool
+PartitionPool::PartitionPool(int n) {
+    for (int i = 0; i < n; ++i)
+        th_.emplace_back([this]() {
+            uint64_t seen = 0;
+            std::unique_lock<std::mutex> lk(mu_);
+            for (;;) {
+                cv_.wait(lk, [&] { return stop_ || (gen_ != seen && next_ < total_); });
+                if (stop_) return;
+                if (next_ >= total_) {
+                    seen = gen_;
+                    continue;
+                }
+                const int k = next_++;
+                const std::function<void(int)>* fn = job_;
+                lk.unlock();
+                (*fn)(k);
+                lk.lock();
+                if (++finished_ == total_) done_cv_.notify_all();
+            }
+        });
+}
+
+PartitionPool::~PartitionPool() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+}
+
+void PartitionPool::run(int n, const std::function<void(int)>& fn) {
+    if (th_.empty() || n <= 1) {
+        for (int k = 0; k < n; ++k) fn(k);
+        return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = &fn;
+    next_ = 0;
+    total_ = n;
+    finished_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    done_cv_.wait(lk, [&] { return finished_ == total_; });
+    job_ = nullptr;
+    total_ = 0;
+}
+
+}  // namespace vp8
+}  // namespace mx

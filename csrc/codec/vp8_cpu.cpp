@@ -1,0 +1,174 @@
+// CPU VP8 encoder: the decisions and arithmetic of the HIP kernels (vp8_kernels.hip), serially.
+// The bit-exact oracle for the GPU encoder and the no-GPU fallback behind WEBRTC_ENCODER=vp8enc
+// (the reference's libvpx `vp8enc`, README.md:21,35).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+
+#include "h264_core.h"
+#include "vp8_encoder.h"
+
+namespace mx {
+namespace vp8 {
+
+namespace {
+
+// Neighbour edges of the n x n block at (x0, y0) of a plane (cw x ch, interleave `step`, component
+// offset `comp`) from the reconstruction, with VP8's frame-edge values.
+Edge edge_of(const uint8_t* p, int pitch, int step, int comp, int x0, int y0, int n) {
+    Edge e;
+    e.have_above = y0 > 0;
+    e.have_left = x0 > 0;
+    for (int i = 0; i < n; ++i) {
+        e.above[i] = y0 > 0 ? p[(y0 - 1) * pitch + (x0 + i) * step + comp] : 127;
+        e.left[i] = x0 > 0 ? p[(y0 + i) * pitch + (x0 - 1) * step + comp] : 129;
+    }
+    e.corner = y0 == 0 ? 127 : (x0 == 0 ? 129 : p[(y0 - 1) * pitch + (x0 - 1) * step + comp]);
+    return e;
+}
+
+}  // namespace
+
+CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
+    mb_w_ = common_.mb_w();
+    mb_h_ = common_.mb_h();
+    cw_ = mb_w_ * 16;
+    ch_ = mb_h_ * 16;
+    for (int i = 0; i < 2; ++i) {
+        rec_y_[i].assign((size_t)cw_ * ch_, 0);
+        rec_uv_[i].assign((size_t)cw_ * ch_ / 2, 128);
+    }
+    mb_.resize((size_t)mb_w_ * mb_h_);
+    lv_.resize(mb_.size() * kCoefPerMb);
+}
+
+void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bool key, int qindex) {
+    const Quant Q = quant_of(qindex);
+    uint8_t* ry = rec_y_[cur_].data();
+    uint8_t* ruv = rec_uv_[cur_].data();
+    const uint8_t* fy = rec_y_[cur_ ^ 1].data();
+    const uint8_t* fuv = rec_uv_[cur_ ^ 1].data();
+    const int qp = common_.cur_qp();
+    for (int mby = 0; mby < mb_h_; ++mby)
+        for (int mbx = 0; mbx < mb_w_; ++mbx) {
+            const int i = mby * mb_w_ + mbx, x0 = mbx * 16, y0 = mby * 16;
+            Vp8Mb& m = mb_[i];
+            std::memset(&m, 0, sizeof m);
+            int16_t* lv = lv_.data() + (size_t)i * kCoefPerMb;
+            int pred[256], res[256], rec[256], cp[2][64], cres[2][64], crec[2][64];
+            if (key) {
+                const Edge e = edge_of(ry, cw_, 1, 0, x0, y0, 16);
+                const int dc = dc_of(e, 16);
+                uint32_t best = ~0u;
+                for (int mode = 0; mode < 4; ++mode) {
+                    uint32_t sad = 0;
+                    for (int y = 0; y < 16; ++y)
+                        for (int x = 0; x < 16; ++x)
+                            sad += (uint32_t)std::abs((int)sy[(y0 + y) * pitch + x0 + x] - pred_px(mode, e, 16, x, y, dc));
+                    if (sad < best) {
+                        best = sad;
+                        m.ymode = (uint8_t)mode;
+                    }
+                }
+                for (int y = 0; y < 16; ++y)
+                    for (int x = 0; x < 16; ++x) pred[y * 16 + x] = pred_px(m.ymode, e, 16, x, y, dc);
+                const Edge eu = edge_of(ruv, cw_, 2, 0, x0 / 2, y0 / 2, 8), ev = edge_of(ruv, cw_, 2, 1, x0 / 2, y0 / 2, 8);
+                const int du = dc_of(eu, 8), dv = dc_of(ev, 8);
+                best = ~0u;
+                for (int mode = 0; mode < 4; ++mode) {
+                    uint32_t sad = 0;
+                    for (int y = 0; y < 8; ++y)
+                        for (int x = 0; x < 8; ++x) {
+                            const int o = (y0 / 2 + y) * pitch + (x0 + 2 * x);
+                            sad += (uint32_t)std::abs((int)suv[o] - pred_px(mode, eu, 8, x, y, du));
+                            sad += (uint32_t)std::abs((int)suv[o + 1] - pred_px(mode, ev, 8, x, y, dv));
+                        }
+                    if (sad < best) {
+                        best = sad;
+                        m.uvmode = (uint8_t)mode;
+                    }
+                }
+                for (int y = 0; y < 8; ++y)
+                    for (int x = 0; x < 8; ++x) {
+                        cp[0][y * 8 + x] = pred_px(m.uvmode, eu, 8, x, y, du);
+                        cp[1][y * 8 + x] = pred_px(m.uvmode, ev, 8, x, y, dv);
+                    }
+            } else {
+                int mvx = 0, mvy = 0;  // quarter samples; full-sample search
+                h264::me_search_cpu(sy, pitch, fy, cw_, ch_, x0, y0, qp, cfg_.search_range, 0, &mvx, &mvy,
+                                    cfg_.me_coarse);
+                int lo_x, hi_x, lo_y, hi_y;
+                mv_bounds(mb_w_, mb_h_, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
+                const int ix = std::clamp(mvx / 4, lo_x, hi_x), iy = std::clamp(mvy / 4, lo_y, hi_y);
+                m.ymode = kInter;
+                m.mvx = (int16_t)(ix * 8);
+                m.mvy = (int16_t)(iy * 8);
+                for (int y = 0; y < 16; ++y)
+                    for (int x = 0; x < 16; ++x) pred[y * 16 + x] = h264::ref_px(fy, cw_, cw_, ch_, x0 + x + ix, y0 + y + iy);
+                // chroma: the luma vector halved, in 1/8 chroma samples (odd full-sample luma
+                // vectors land on the half-sample six-tap phase)
+                const int cvx = chroma_mv(m.mvx), cvy = chroma_mv(m.mvy);
+                for (int c = 0; c < 2; ++c) {
+                    auto at = [&](int xx, int yy) {
+                        xx = std::clamp(xx, 0, cw_ / 2 - 1);
+                        yy = std::clamp(yy, 0, ch_ / 2 - 1);
+                        return (int)fuv[yy * cw_ + 2 * xx + c];
+                    };
+                    for (int y = 0; y < 8; ++y)
+                        for (int x = 0; x < 8; ++x)
+                            cp[c][y * 8 + x] = sixtap_px(at, x0 / 2 + x + (cvx >> 3), y0 / 2 + y + (cvy >> 3), cvx & 7, cvy & 7);
+                }
+            }
+            for (int y = 0; y < 16; ++y)
+                for (int x = 0; x < 16; ++x) res[y * 16 + x] = sy[(y0 + y) * pitch + x0 + x] - pred[y * 16 + x];
+            for (int c = 0; c < 2; ++c)
+                for (int y = 0; y < 8; ++y)
+                    for (int x = 0; x < 8; ++x)
+                        cres[c][y * 8 + x] = suv[(y0 / 2 + y) * pitch + x0 + 2 * x + c] - cp[c][y * 8 + x];
+            m.nz = code_luma16(res, pred, Q, lv, rec);
+            m.nz |= code_chroma8(cres[0], cp[0], Q, lv, crec[0], 16);
+            m.nz |= code_chroma8(cres[1], cp[1], Q, lv, crec[1], 20);
+            for (int y = 0; y < 16; ++y)
+                for (int x = 0; x < 16; ++x) ry[(y0 + y) * cw_ + x0 + x] = (uint8_t)rec[y * 16 + x];
+            for (int c = 0; c < 2; ++c)
+                for (int y = 0; y < 8; ++y)
+                    for (int x = 0; x < 8; ++x) ruv[(y0 / 2 + y) * cw_ + x0 + 2 * x + c] = (uint8_t)crec[c][y * 8 + x];
+        }
+}
+
+const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
+    auto run_serial = [](int n, const std::function<void(int)>& fn) {
+        for (int k = 0; k < n; ++k) fn(k);
+    };
+    const int log2_parts = mb_h_ >= 8 ? 3 : (mb_h_ >= 4 ? 2 : (mb_h_ >= 2 ? 1 : 0));
+    while (common_.wants_probe()) {  // size the first key frame, as the GPU encoder does
+        const int q = common_.probe_qp();
+        analyse(y, uv, pitch, true, qindex_for_qp(q));
+        std::vector<uint8_t> tmp;
+        write_frame(FrameDesc{true, cfg_.width, cfg_.height, mb_w_, mb_h_, qindex_for_qp(q), log2_parts}, mb_.data(),
+                    [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, tmp, run_serial);
+        common_.add_probe(q, (int)tmp.size());
+    }
+    common_.begin_frame(force_idr || !have_ref_);
+    cur_ ^= 1;
+    const bool key = common_.cur_idr();
+    const int qindex = qindex_for_qp(common_.cur_qp());
+    analyse(y, uv, pitch, key, qindex);
+    au_.clear();
+    write_frame(FrameDesc{key, cfg_.width, cfg_.height, mb_w_, mb_h_, qindex, log2_parts}, mb_.data(),
+                [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, au_, run_serial);
+    int skipped = 0;
+    for (const Vp8Mb& m : mb_) skipped += m.nz == 0;
+    stats_.frame_index = common_.frames();
+    stats_.idr = key;
+    stats_.qp = common_.cur_qp();
+    stats_.bytes = (int)au_.size();
+    stats_.skipped_mbs = skipped;
+    common_.end_frame((int)au_.size(), key);
+    have_ref_ = true;
+    return au_;
+}
+
+}  // namespace vp8
+}  // namespace mx

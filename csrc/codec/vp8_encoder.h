@@ -1,0 +1,225 @@
+// VP8 encoders (RFC 6386): GpuVp8Encoder (HIP analysis -- motion search shared with H.264,
+// transforms, quantisation, reconstruction -- plus boolean-coded partitions written by host
+// threads, one per token partition) and CpuVp8Encoder (the same decisions serially; the bit-exact
+// oracle for the GPU path and the no-GPU fallback).  Selected by WEBRTC_ENCODER=vp8enc, the
+// reference's libvpx choice (reference README.md:21,35).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "h264_encoder.h"
+#include "video_encoder.h"
+#include "vp8_core.h"
+
+namespace mx {
+namespace vp8 {
+
+// RFC 6386 section 7 boolean entropy encoder (libvpx's carry-propagating form).
+class BoolEncoder {
+   public:
+    explicit BoolEncoder(std::vector<uint8_t>& out) : out_(out) {}
+    void put(int prob, int bit) {
+        const uint32_t split = 1 + (((range_ - 1) * (uint32_t)prob) >> 8);
+        if (bit) {
+            bottom_ += split;
+            range_ -= split;
+        } else {
+            range_ = split;
+        }
+        while (range_ < 128) {
+            range_ <<= 1;
+            if (bottom_ & (1u << 31)) carry();
+            bottom_ <<= 1;
+            if (!--bit_count_) {
+                out_.push_back((uint8_t)(bottom_ >> 24));
+                bottom_ &= (1u << 24) - 1;
+                bit_count_ = 8;
+            }
+        }
+    }
+    void literal(uint32_t v, int n) {
+        for (int i = n - 1; i >= 0; --i) put(128, (v >> i) & 1);
+    }
+    void flush() {
+        for (int i = 0; i < 32; ++i) put(128, 0);
+    }
+
+   private:
+    void carry() {
+        for (size_t i = out_.size(); i-- > 0;) {
+            if (out_[i] == 255) {
+                out_[i] = 0;
+            } else {
+                ++out_[i];
+                return;
+            }
+        }
+    }
+    std::vector<uint8_t>& out_;
+    uint32_t range_ = 255, bottom_ = 0;
+    int bit_count_ = 24;
+};
+
+struct FrameDesc {
+    bool key;
+    int width, height, mb_w, mb_h;
+    int qindex;
+    int log2_parts;  // token partitions: 1 << log2_parts
+};
+
+// Writes a complete VP8 frame (frame tag, key-frame header, first partition, token partitions)
+// from per-macroblock records and levels.  `levels(i)` returns macroblock i's 400 levels (only
+// read for macroblocks with nz != 0).  Token partitions are coded concurrently on `run_parallel`.
+void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels,
+                 std::vector<uint8_t>& out,
+                 const std::function<void(int, const std::function<void(int)>&)>& run_parallel);
+
+// Near / nearest / best motion vectors of macroblock (mbx, mby) (RFC 6386 find_near_mvs, with
+// the decoder's clamping); every macroblock of the picture is inter (P frames).  cnt[4] out.
+void find_near_mvs(const Vp8Mb* mbs, int mb_w, int mb_h, int mbx, int mby, int near_mv[3][2], int cnt[4]);
+// Legal full-sample vector range of a macroblock: the decoder never clamps vectors inside it.
+inline void mv_bounds(int mb_w, int mb_h, int mbx, int mby, int* lo_x, int* hi_x, int* lo_y, int* hi_y) {
+    *lo_x = -(mbx * 16 + 16) + 3;
+    *hi_x = (mb_w - 1 - mbx) * 16 + 16 - 3;
+    *lo_y = -(mby * 16 + 16) + 3;
+    *hi_y = (mb_h - 1 - mby) * 16 + 16 - 3;
+}
+
+// Small persistent worker pool for the token partitions.
+class PartitionPool {
+   public:
+    explicit PartitionPool(int n);
+    ~PartitionPool();
+    void run(int n, const std::function<void(int)>& fn);
+
+   private:
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* job_ = nullptr;
+    int next_ = 0, total_ = 0, finished_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+class CpuVp8Encoder {
+   public:
+    explicit CpuVp8Encoder(const h264::EncoderConfig& cfg);
+    const std::vector<uint8_t>& encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr = false);
+    const h264::FrameStats& last_stats() const { return stats_; }
+    h264::EncoderCommon& common() { return common_; }
+    const std::vector<uint8_t>& recon_y() const { return rec_y_[cur_]; }
+    const std::vector<uint8_t>& recon_uv() const { return rec_uv_[cur_]; }
+    int coded_pitch() const { return cw_; }
+    const std::vector<Vp8Mb>& mb_info() const { return mb_; }
+
+   private:
+    void analyse(const uint8_t* y, const uint8_t* uv, int pitch, bool key, int qindex);
+    h264::EncoderConfig cfg_;
+    h264::EncoderCommon common_;
+    int cw_, ch_, mb_w_, mb_h_;
+    std::vector<uint8_t> rec_y_[2], rec_uv_[2];
+    int cur_ = 0;
+    bool have_ref_ = false;
+    std::vector<Vp8Mb> mb_;
+    std::vector<int16_t> lv_;
+    std::vector<uint8_t> au_;
+    h264::FrameStats stats_;
+};
+
+// Device layout of the GPU encoder
+struct Vp8FrameState {
+    const uint8_t* ref_y;
+    const uint8_t* ref_uv;
+    uint8_t* rec_y;
+    uint8_t* rec_uv;
+    const uint8_t* hp_f;  // padded full-sample reference (shared H.264 k_hpel), origin applied
+    int32_t hp_pitch;
+    int32_t key;
+    int32_t qindex;
+    int32_t epoch;  // nonzero, new every frame: key-frame wavefront progress tag
+};
+struct Vp8DeviceBuffers {
+    Vp8FrameState* fs;
+    Vp8Mb* mb;             // [nmb] records
+    int16_t* lv;           // [nmb * 400] levels
+    uint32_t* prog;        // [mb_h] key-frame wavefront progress (epoch << 12 | MBs done)
+    uint64_t* line;        // [mb_h][coded_w / 8 * 2] key-frame hand-off: bottom luma + chroma rows
+    h264::DeviceBuffers me;  // shared H.264 motion search state (frame state + MbInfo with vectors)
+};
+void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y,
+                      const uint8_t* src_uv, hipStream_t stream);
+void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                    hipStream_t stream);
+
+class GpuVp8Encoder final : public VideoEncoder {
+   public:
+    const char* codec() const override { return "vp8"; }
+    static constexpr int kMaxInFlight = 2;
+    GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream);
+    ~GpuVp8Encoder();
+    GpuVp8Encoder(const GpuVp8Encoder&) = delete;
+    GpuVp8Encoder& operator=(const GpuVp8Encoder&) = delete;
+    const h264::Geometry& geometry() const override { return geom_; }
+    int pitch() const override { return geom_.pitch; }
+    int depth() const override { return depth_; }
+    void submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr = false) override;
+    const std::vector<uint8_t>& collect() override;
+    const h264::FrameStats& last_stats() const override { return stats_; }
+    h264::EncoderCommon& rc() override { return common_; }
+    const uint8_t* recon_y() const override { return rec_y_[cur_]; }
+    const uint8_t* recon_uv() const override { return rec_uv_[cur_]; }
+    hipEvent_t done_event() const override { return last_done_; }
+    bool prepare(bool force_idr) override;
+    void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
+    void record_start() override;
+    void record_done() override;
+
+   private:
+    struct Slot {
+        Vp8DeviceBuffers buf{};
+        Vp8FrameState* fs_host = nullptr;
+        h264::FrameState* me_fs_host = nullptr;
+        Vp8Mb* mb_host = nullptr;   // pinned copies of the records / levels (D2H after analysis)
+        int16_t* lv_host = nullptr;
+        hipEvent_t start = nullptr, done = nullptr;
+        bool key = false;
+        int qp = 0, qindex = 0;
+    };
+    void alloc_slot(Slot& s);
+    void free_slot(Slot& s);
+    void fill_state(Slot& s, bool key, int qp, int ref, int cur);
+    int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
+    void write_slot(Slot& s, std::vector<uint8_t>& out);
+
+    h264::EncoderConfig cfg_;
+    h264::EncoderCommon common_;
+    hipStream_t stream_;
+    int depth_ = 1;
+    h264::Geometry geom_;
+    Slot slots_[kMaxInFlight];
+    int next_slot_ = 0, prep_slot_ = 0;
+    std::deque<int> inflight_;
+    hipEvent_t last_done_ = nullptr;
+    uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};
+    int hp_pitch_ = 0;
+    uint8_t* rec_y_[2] = {nullptr, nullptr};
+    uint8_t* rec_uv_[2] = {nullptr, nullptr};
+    int cur_ = 0;
+    bool have_ref_ = false;
+    uint32_t epoch_ = 0;
+    int log2_parts_ = 0;
+    PartitionPool pool_;
+    std::vector<uint8_t> au_;
+    h264::FrameStats stats_;
+};
+
+}  // namespace vp8
+}  // namespace mx

@@ -1,0 +1,541 @@
+"""Pure-Python VP8 decoder (RFC 6386) for the subset mxdesk's VP8 encoder emits: the oracle for
+its inter frames (no libvpx / ffmpeg in this image; key frames are also checked against libwebp
+through Pillow, tests/test_vp8.py).
+
+Written from the decoding side of the RFC: boolean decoder (7), frame header (9, 19.2), token
+probability and motion-vector probability updates (13.4, 17.2), key-frame and inter-frame mode
+parsing (11, 16) with the near-vector search (16.3), token decoding with contexts (13),
+dequantisation (14.1), inverse WHT / DCT (14.3, 14.4), 16x16 and chroma intra prediction with the
+127 / 129 frame edges (12), and six-tap inter prediction (18).
+
+Supported: key and inter frames, 16x16 intra modes, 16x16 inter macroblocks (ZERO / NEAREST / NEAR /
+NEW vectors, last-frame reference), token partitions, probability updates, skip flags.  Raises
+``NotImplementedError`` for B_PRED, SPLITMV, segmentation, a non-zero loop-filter level and
+golden / altref references.  Slow; for test pictures.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .vp8_tables import AC_Q, COEF_PROBS0, COEF_UPDATE_PROBS, DC_Q
+
+ZIGZAG = [0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15]
+BANDS = [0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0]
+PCAT = [[159], [165, 145], [173, 148, 140], [176, 155, 140, 135], [180, 157, 141, 134, 130],
+        [254, 254, 243, 230, 196, 177, 153, 140, 133, 130, 129]]
+CAT_BASE = [5, 7, 11, 19, 35, 67]
+KF_YMODE_PROB = [145, 156, 163, 128]
+KF_UVMODE_PROB = [142, 114, 183]
+YMODE_PROB = [112, 86, 140, 37]
+UVMODE_PROB = [162, 101, 204]
+MV_DEFAULT = [[162, 128, 225, 146, 172, 147, 214, 39, 156, 128, 129, 132, 75, 145, 178, 206, 239, 254, 254],
+              [164, 128, 204, 170, 119, 235, 140, 230, 228, 128, 130, 130, 74, 148, 180, 203, 236, 254, 254]]
+MV_UPDATE = [[237, 246, 253, 253, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 250, 250, 252, 254, 254],
+             [231, 243, 245, 253, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 251, 251, 254, 254, 254]]
+MODE_CONTEXTS = [[7, 1, 1, 143], [14, 18, 14, 107], [135, 64, 57, 68], [60, 56, 128, 65], [159, 134, 128, 34],
+                 [234, 188, 128, 28]]
+SUBPEL = [[0, 0, 128, 0, 0, 0], [0, -6, 123, 12, -1, 0], [2, -11, 108, 36, -8, 1], [0, -9, 93, 50, -6, 0],
+          [3, -16, 77, 77, -16, 3], [0, -6, 50, 93, -9, 0], [1, -8, 36, 108, -11, 2], [0, -1, 12, 123, -6, 0]]
+DC_PRED, V_PRED, H_PRED, TM_PRED, B_PRED = 0, 1, 2, 3, 4
+
+
+class Vp8Error(Exception):
+    pass
+
+
+class BoolDecoder:
+    """RFC 6386 section 7.3."""
+
+    def __init__(self, data: bytes, start: int = 0, end: int | None = None):
+        self.d = data
+        self.pos = start
+        self.end = len(data) if end is None else end
+        self.value = (self._byte() << 8) | self._byte()
+        self.range = 255
+        self.bit_count = 0
+
+    def _byte(self) -> int:
+        if self.pos < self.end:
+            b = self.d[self.pos]
+            self.pos += 1
+            return b
+        self.pos += 1
+        return 0
+
+    def bool(self, prob: int) -> int:
+        split = 1 + (((self.range - 1) * prob) >> 8)
+        big = split << 8
+        if self.value >= big:
+            ret = 1
+            self.range -= split
+            self.value -= big
+        else:
+            ret = 0
+            self.range = split
+        while self.range < 128:
+            self.value <<= 1
+            self.range <<= 1
+            self.bit_count += 1
+            if self.bit_count == 8:
+                self.bit_count = 0
+                self.value |= self._byte()
+        return ret
+
+    def lit(self, n: int) -> int:
+        v = 0
+        for _ in range(n):
+            v = (v << 1) | self.bool(128)
+        return v
+
+    def signed(self, n: int) -> int:
+        v = self.lit(n)
+        return -v if self.bool(128) else v
+
+
+def _iwht(c):
+    t = [0] * 16
+    for i in range(4):
+        a1, b1 = c[i] + c[12 + i], c[4 + i] + c[8 + i]
+        c1, d1 = c[4 + i] - c[8 + i], c[i] - c[12 + i]
+        t[i], t[4 + i], t[8 + i], t[12 + i] = a1 + b1, c1 + d1, a1 - b1, d1 - c1
+    out = [0] * 16
+    for i in range(4):
+        a1, b1 = t[4 * i] + t[4 * i + 3], t[4 * i + 1] + t[4 * i + 2]
+        c1, d1 = t[4 * i + 1] - t[4 * i + 2], t[4 * i] - t[4 * i + 3]
+        out[4 * i:4 * i + 4] = [(a1 + b1 + 3) >> 3, (c1 + d1 + 3) >> 3, (a1 - b1 + 3) >> 3, (d1 - c1 + 3) >> 3]
+    return out
+
+
+def _idct(c):
+    C8, S8 = 20091, 35468
+    if not any(c[1:]):
+        return [(c[0] + 4) >> 3] * 16
+    t = [0] * 16
+    for i in range(4):
+        i0, i4, i8, i12 = c[i], c[4 + i], c[8 + i], c[12 + i]
+        a1, b1 = i0 + i8, i0 - i8
+        c1 = ((i4 * S8) >> 16) - (i12 + ((i12 * C8) >> 16))
+        d1 = (i4 + ((i4 * C8) >> 16)) + ((i12 * S8) >> 16)
+        t[i], t[12 + i], t[4 + i], t[8 + i] = a1 + d1, a1 - d1, b1 + c1, b1 - c1
+    out = [0] * 16
+    for i in range(4):
+        r = t[4 * i:4 * i + 4]
+        a1, b1 = r[0] + r[2], r[0] - r[2]
+        c1 = ((r[1] * S8) >> 16) - (r[3] + ((r[3] * C8) >> 16))
+        d1 = (r[1] + ((r[1] * C8) >> 16)) + ((r[3] * S8) >> 16)
+        out[4 * i:4 * i + 4] = [(a1 + d1 + 4) >> 3, (b1 + c1 + 4) >> 3, (b1 - c1 + 4) >> 3, (a1 - d1 + 4) >> 3]
+    return out
+
+
+class Decoder:
+    """``decode(frames)`` -> list of (Y, U, V) uint8 planes (display size); ``frames_coded`` keeps
+    the macroblock-aligned planes; ``modes`` the last frame's per-MB (ymode, mv) records."""
+
+    def __init__(self):
+        self.frames = []
+        self.frames_coded = []
+        self.last = None
+        self.w = self.h = 0
+        self.stats = {"key": 0, "inter": 0, "skip": 0, "zero": 0, "nearest": 0, "near": 0, "new": 0}
+
+    # ------------------------------------------------------------------ frame
+    def decode(self, frames: list[bytes]):
+        for f in frames:
+            self.decode_frame(f)
+        return self.frames
+
+    def decode_frame(self, buf: bytes):
+        if len(buf) < 3:
+            raise Vp8Error("truncated frame tag")
+        tag = buf[0] | (buf[1] << 8) | (buf[2] << 16)
+        key = not (tag & 1)
+        version = (tag >> 1) & 7
+        first_size = tag >> 5
+        if version != 0:
+            raise NotImplementedError(f"version {version} (bilinear / full-pixel filters)")
+        pos = 3
+        if key:
+            if buf[3:6] != b"\x9d\x01\x2a":
+                raise Vp8Error("bad key-frame start code")
+            self.w = (buf[6] | (buf[7] << 8)) & 0x3FFF
+            self.h = (buf[8] | (buf[9] << 8)) & 0x3FFF
+            pos = 10
+            self.coef = list(COEF_PROBS0)
+            self.mvp = [list(MV_DEFAULT[0]), list(MV_DEFAULT[1])]
+            self.ymode_prob, self.uvmode_prob = list(YMODE_PROB), list(UVMODE_PROB)
+        elif self.last is None:
+            raise Vp8Error("inter frame without a key frame")
+        mw, mh = (self.w + 15) // 16, (self.h + 15) // 16
+        self.mw, self.mh = mw, mh
+        bd = BoolDecoder(buf, pos, pos + first_size)
+        if key:
+            bd.lit(1)  # color space
+            self.clamping = bd.lit(1)
+        if bd.lit(1):
+            raise NotImplementedError("segmentation")
+        bd.lit(1)  # filter type
+        level = bd.lit(6)
+        bd.lit(3)  # sharpness
+        if level:
+            raise NotImplementedError("loop filter")
+        if bd.lit(1):  # loop_filter_adj_enable
+            if bd.lit(1):
+                for _ in range(8):
+                    if bd.lit(1):
+                        bd.signed(6)
+        nparts = 1 << bd.lit(2)
+        qi = bd.lit(7)
+        deltas = [bd.signed(4) if bd.lit(1) else 0 for _ in range(5)]  # y_dc, y2_dc, y2_ac, uv_dc, uv_ac
+        q = lambda base, d: min(127, max(0, base + d))  # noqa: E731
+        self.q = {
+            "y1dc": DC_Q[q(qi, deltas[0])], "y1ac": AC_Q[qi],
+            "y2dc": 2 * DC_Q[q(qi, deltas[1])], "y2ac": max(8, AC_Q[q(qi, deltas[2])] * 155 // 100),
+            "uvdc": min(132, DC_Q[q(qi, deltas[3])]), "uvac": AC_Q[q(qi, deltas[4])],
+        }
+        saved = None
+        if key:
+            refresh_probs = bd.lit(1)
+        else:
+            if bd.lit(1) or bd.lit(1):
+                raise NotImplementedError("golden / altref refresh")
+            bd.lit(2)
+            bd.lit(2)  # copy_buffer_to_golden / altref (ignored: never referenced)
+            bd.lit(1)
+            bd.lit(1)  # sign bias
+            refresh_probs = bd.lit(1)
+            bd.lit(1)  # refresh_last
+        if not refresh_probs:
+            saved = (list(self.coef), [list(p) for p in self.mvp], list(self.ymode_prob), list(self.uvmode_prob))
+        for i in range(1056):
+            if bd.bool(COEF_UPDATE_PROBS[i]):
+                self.coef[i] = bd.lit(8)
+        skip_on = bd.lit(1)
+        prob_skip = bd.lit(8) if skip_on else 0
+        if not key:
+            prob_intra, prob_last = bd.lit(8), bd.lit(8)
+            bd.lit(8)  # prob_gf
+            if bd.lit(1):
+                self.ymode_prob = [bd.lit(8) for _ in range(4)]
+            if bd.lit(1):
+                self.uvmode_prob = [bd.lit(8) for _ in range(3)]
+            for c in range(2):
+                for k in range(19):
+                    if bd.bool(MV_UPDATE[c][k]):
+                        x = bd.lit(7)
+                        self.mvp[c][k] = (x << 1) if x else 1
+        # ---- per-MB modes
+        mbs = []
+        for my in range(mh):
+            for mx in range(mw):
+                skip = bd.bool(prob_skip) if skip_on else 0
+                if key:
+                    ym = self._tree_kf_ymode(bd)
+                    uvm = self._tree_uv(bd, KF_UVMODE_PROB)
+                    mbs.append({"inter": False, "y": ym, "uv": uvm, "skip": skip, "mv": (0, 0)})
+                    continue
+                if not bd.bool(prob_intra):
+                    ym = self._tree_ymode(bd)
+                    uvm = self._tree_uv(bd, self.uvmode_prob)
+                    mbs.append({"inter": False, "y": ym, "uv": uvm, "skip": skip, "mv": (0, 0)})
+                    continue
+                if bd.bool(prob_last):
+                    raise NotImplementedError("golden / altref reference")
+                near, cnt = self._near_mvs(mbs, mx, my)
+                p = [MODE_CONTEXTS[cnt[i]][i] for i in range(4)]
+                if not bd.bool(p[0]):
+                    mv, kind = (0, 0), "zero"
+                elif not bd.bool(p[1]):
+                    mv, kind = near[1], "nearest"
+                elif not bd.bool(p[2]):
+                    mv, kind = near[2], "near"
+                elif not bd.bool(p[3]):
+                    dy = self._mv_component(bd, self.mvp[0]) * 2
+                    dx = self._mv_component(bd, self.mvp[1]) * 2
+                    mv, kind = (near[0][0] + dx, near[0][1] + dy), "new"
+                    lo_x, hi_x, lo_y, hi_y = self._mv_limits(mx, my)
+                    if not (lo_x <= mv[0] <= hi_x and lo_y <= mv[1] <= hi_y):
+                        raise NotImplementedError("vector outside the clamping range")
+                else:
+                    raise NotImplementedError("SPLITMV")
+                self.stats[kind] += 1
+                mbs.append({"inter": True, "y": None, "uv": None, "skip": skip, "mv": mv})
+        self.modes = mbs
+        # ---- token partitions
+        p0 = pos + first_size
+        sizes_at = p0
+        data_at = p0 + 3 * (nparts - 1)
+        parts = []
+        for k in range(nparts):
+            if k < nparts - 1:
+                n = buf[sizes_at + 3 * k] | (buf[sizes_at + 3 * k + 1] << 8) | (buf[sizes_at + 3 * k + 2] << 16)
+            else:
+                n = len(buf) - data_at
+            parts.append(BoolDecoder(buf, data_at, data_at + n))
+            data_at += n
+        # ---- reconstruction
+        Y = np.zeros((mh * 16, mw * 16), np.int32)
+        U = np.zeros((mh * 8, mw * 8), np.int32)
+        V = np.zeros((mh * 8, mw * 8), np.int32)
+        above = [[0] * 9 for _ in range(mw)]
+        for my in range(mh):
+            bd = parts[my % nparts]
+            left = [0] * 9
+            for mx in range(mw):
+                m = mbs[my * mw + mx]
+                if m["skip"]:
+                    self.stats["skip"] += 1
+                    coefs = [[0] * 16 for _ in range(25)]
+                    for k in range(9):  # the MB has a Y2 block: every context resets
+                        above[mx][k] = left[k] = 0
+                else:
+                    coefs = self._tokens(bd, above[mx], left)
+                self._recon(Y, U, V, mx, my, m, coefs, key)
+        if saved is not None:
+            self.coef, self.mvp, self.ymode_prob, self.uvmode_prob = saved
+        self.stats["key" if key else "inter"] += 1
+        self.last = (Y, U, V)
+        y8, u8, v8 = (p.astype(np.uint8) for p in (Y, U, V))
+        self.frames_coded.append((y8, u8, v8))
+        self.frames.append((y8[:self.h, :self.w], u8[:(self.h + 1) // 2, :(self.w + 1) // 2],
+                            v8[:(self.h + 1) // 2, :(self.w + 1) // 2]))
+
+    # ------------------------------------------------------------------ modes
+    @staticmethod
+    def _tree_kf_ymode(bd):
+        p = KF_YMODE_PROB
+        if not bd.bool(p[0]):
+            raise NotImplementedError("B_PRED")
+        if not bd.bool(p[1]):
+            return V_PRED if bd.bool(p[2]) else DC_PRED
+        return TM_PRED if bd.bool(p[3]) else H_PRED
+
+    def _tree_ymode(self, bd):
+        p = self.ymode_prob  # DC "0", V "100", H "101", TM "110", B_PRED "111"
+        if not bd.bool(p[0]):
+            return DC_PRED
+        if not bd.bool(p[1]):
+            return H_PRED if bd.bool(p[2]) else V_PRED
+        if bd.bool(p[3]):
+            raise NotImplementedError("B_PRED")
+        return TM_PRED
+
+    @staticmethod
+    def _tree_uv(bd, p):
+        if not bd.bool(p[0]):
+            return DC_PRED
+        if not bd.bool(p[1]):
+            return V_PRED
+        return TM_PRED if bd.bool(p[2]) else H_PRED
+
+    def _mv_limits(self, mx, my):
+        return (-((mx * 16) << 3) - 128, (((self.mw - 1 - mx) * 16) << 3) + 128,
+                -((my * 16) << 3) - 128, (((self.mh - 1 - my) * 16) << 3) + 128)
+
+    def _near_mvs(self, mbs, mx, my):
+        mv = [(0, 0)] * 4
+        cnt = [0, 0, 0, 0]
+        idx = 0
+        for nx, ny, w in ((mx, my - 1, 2), (mx - 1, my, 2), (mx - 1, my - 1, 1)):
+            if nx < 0 or ny < 0:
+                continue
+            n = mbs[ny * self.mw + nx]
+            if not n["inter"]:
+                continue
+            if n["mv"] != (0, 0):
+                if idx == 0 or n["mv"] != mv[idx]:
+                    idx += 1
+                    mv[idx] = n["mv"]
+                cnt[idx] += w
+            else:
+                cnt[0] += w
+        if cnt[3] and mv[idx] == mv[1]:
+            cnt[1] += 1
+        cnt[3] = 0  # SPLITMV neighbours (none decoded)
+        if cnt[2] > cnt[1]:
+            cnt[1], cnt[2] = cnt[2], cnt[1]
+            mv[1], mv[2] = mv[2], mv[1]
+        if cnt[1] >= cnt[0]:
+            mv[0] = mv[1]
+        lo_x, hi_x, lo_y, hi_y = self._mv_limits(mx, my)
+        near = [(min(max(v[0], lo_x), hi_x), min(max(v[1], lo_y), hi_y)) for v in mv[:3]]
+        return near, cnt
+
+    @staticmethod
+    def _mv_component(bd, p):
+        if bd.bool(p[0]):
+            x = 0
+            for i in range(3):
+                x += bd.bool(p[9 + i]) << i
+            for i in range(9, 3, -1):
+                x += bd.bool(p[9 + i]) << i
+            if not (x & 0xFFF0) or bd.bool(p[9 + 3]):
+                x += 8
+        else:
+            if not bd.bool(p[2]):
+                x = (2 + bd.bool(p[5])) if bd.bool(p[3]) else bd.bool(p[4])
+            else:
+                x = (6 + bd.bool(p[8])) if bd.bool(p[6]) else (4 + bd.bool(p[7]))
+        if x and bd.bool(p[1]):
+            x = -x
+        return x
+
+    # ------------------------------------------------------------------ tokens
+    def _block(self, bd, typ, first, ctx):
+        out = [0] * 16
+        i = first
+        prev_zero = False
+        while i < 16:
+            b0 = ((typ * 8 + BANDS[i]) * 3 + ctx) * 11
+            p = self.coef[b0:b0 + 11]
+            if not prev_zero and not bd.bool(p[0]):
+                break  # EOB
+            if not bd.bool(p[1]):
+                ctx, prev_zero = 0, True
+                i += 1
+                continue
+            if not bd.bool(p[2]):
+                v = 1
+            elif not bd.bool(p[3]):
+                if not bd.bool(p[4]):
+                    v = 2
+                else:
+                    v = 4 if bd.bool(p[5]) else 3
+            elif not bd.bool(p[6]):
+                cat = 1 if bd.bool(p[7]) else 0
+                v = CAT_BASE[cat] + self._extra(bd, PCAT[cat])
+            elif not bd.bool(p[8]):
+                cat = 3 if bd.bool(p[9]) else 2
+                v = CAT_BASE[cat] + self._extra(bd, PCAT[cat])
+            else:
+                cat = 5 if bd.bool(p[10]) else 4
+                v = CAT_BASE[cat] + self._extra(bd, PCAT[cat])
+            ctx = 1 if v == 1 else 2
+            if bd.bool(128):
+                v = -v
+            out[i] = v
+            prev_zero = False
+            i += 1
+        return out
+
+    @staticmethod
+    def _extra(bd, probs):
+        v = 0
+        for p in probs:
+            v = (v << 1) | bd.bool(p)
+        return v
+
+    def _tokens(self, bd, above, left):
+        coefs = [None] * 25
+        nz = lambda c, first: int(any(c[first:]))  # noqa: E731
+        c = self._block(bd, 1, 0, above[8] + left[8])
+        coefs[24] = c
+        above[8] = left[8] = nz(c, 0)
+        for b in range(16):
+            bx, by = b & 3, b >> 2
+            c = self._block(bd, 0, 1, above[bx] + left[by])
+            coefs[b] = c
+            above[bx] = left[by] = nz(c, 1)
+        for comp in range(2):
+            for b in range(4):
+                bx, by = b & 1, b >> 1
+                k = 4 + 2 * comp
+                c = self._block(bd, 2, 0, above[k + bx] + left[k + by])
+                coefs[16 + 4 * comp + b] = c
+                above[k + bx] = left[k + by] = nz(c, 0)
+        return coefs
+
+    # ------------------------------------------------------------------ reconstruction
+    def _recon(self, Y, U, V, mx, my, m, coefs, key):
+        q = self.q
+        x0, y0 = mx * 16, my * 16
+        if m["inter"]:
+            pred = self._inter_pred(self.last[0], x0, y0, 16, m["mv"][0], m["mv"][1])
+            # chroma vector: the luma vector halved, rounded away from zero (18.4)
+            half = lambda v: (v + 1) // 2 if v >= 0 else -((1 - v) // 2)  # noqa: E731
+            cvx, cvy = half(m["mv"][0]), half(m["mv"][1])
+            cpred = [self._inter_pred(P, x0 // 2, y0 // 2, 8, cvx, cvy) for P in self.last[1:]]
+        else:
+            pred = self._intra_pred(Y, x0, y0, 16, m["y"])
+            cpred = [self._intra_pred(P, x0 // 2, y0 // 2, 8, m["uv"]) for P in (U, V)]
+        # luma with Y2
+        y2 = [0] * 16
+        for k, v in enumerate(coefs[24]):
+            y2[ZIGZAG[k]] = v * (q["y2dc"] if k == 0 else q["y2ac"])
+        dcs = _iwht(y2)
+        res = np.zeros((16, 16), np.int64)
+        for b in range(16):
+            c = [0] * 16
+            for k in range(1, 16):
+                c[ZIGZAG[k]] = coefs[b][k] * q["y1ac"]
+            c[0] = dcs[b]
+            r = _idct(c)
+            bx, by = b & 3, b >> 2
+            res[by * 4:by * 4 + 4, bx * 4:bx * 4 + 4] = np.array(r).reshape(4, 4)
+        Y[y0:y0 + 16, x0:x0 + 16] = np.clip(pred + res, 0, 255)
+        for comp, P in enumerate((U, V)):
+            cres = np.zeros((8, 8), np.int64)
+            for b in range(4):
+                c = [0] * 16
+                for k, v in enumerate(coefs[16 + 4 * comp + b]):
+                    c[ZIGZAG[k]] = v * (q["uvdc"] if k == 0 else q["uvac"])
+                bx, by = b & 1, b >> 1
+                cres[by * 4:by * 4 + 4, bx * 4:bx * 4 + 4] = np.array(_idct(c)).reshape(4, 4)
+            P[y0 // 2:y0 // 2 + 8, x0 // 2:x0 // 2 + 8] = np.clip(cpred[comp] + cres, 0, 255)
+
+    @staticmethod
+    def _intra_pred(P, x0, y0, n, mode):
+        above = P[y0 - 1, x0:x0 + n].astype(np.int64) if y0 > 0 else np.full(n, 127, np.int64)
+        left = P[y0:y0 + n, x0 - 1].astype(np.int64) if x0 > 0 else np.full(n, 129, np.int64)
+        corner = 127 if y0 == 0 else (129 if x0 == 0 else int(P[y0 - 1, x0 - 1]))
+        if mode == DC_PRED:
+            s, cnt = 0, 0
+            if y0 > 0:
+                s += int(above.sum())
+                cnt += 1
+            if x0 > 0:
+                s += int(left.sum())
+                cnt += 1
+            if cnt == 0:
+                return np.full((n, n), 128, np.int64)
+            shift = (3 if n == 16 else 2) + cnt
+            return np.full((n, n), (s + (1 << (shift - 1))) >> shift, np.int64)
+        if mode == V_PRED:
+            return np.tile(above, (n, 1))
+        if mode == H_PRED:
+            return np.tile(left[:, None], (1, n))
+        return np.clip(left[:, None] + above[None, :] - corner, 0, 255)
+
+    @staticmethod
+    def _inter_pred(P, x0, y0, n, mvx, mvy):
+        """Six-tap prediction of an n x n block (vector in 1/8 samples of this plane), edge-extended."""
+        H, W = P.shape
+        ix, iy, fx, fy = mvx >> 3, mvy >> 3, mvx & 7, mvy & 7
+        ys = np.clip(np.arange(y0 + iy - 2, y0 + iy + n + 3), 0, H - 1)
+        xs = np.clip(np.arange(x0 + ix - 2, x0 + ix + n + 3), 0, W - 1)
+        R = P[np.ix_(ys, xs)].astype(np.int64)  # (n+5, n+5)
+        hf, vf = SUBPEL[fx], SUBPEL[fy]
+        t = sum(hf[k] * R[:, k:k + n] for k in range(6))
+        t = np.clip((t + 64) >> 7, 0, 255)
+        o = sum(vf[k] * t[k:k + n, :] for k in range(6))
+        return np.clip((o + 64) >> 7, 0, 255)
+
+
+def ivf_frames(data: bytes) -> list[bytes]:
+    """Frames of an IVF file (the container libvpx tools use)."""
+    if data[:4] != b"DKIF":
+        raise Vp8Error("not an IVF file")
+    hl = data[6] | (data[7] << 8)
+    pos, out = hl, []
+    while pos + 12 <= len(data):
+        n = int.from_bytes(data[pos:pos + 4], "little")
+        out.append(data[pos + 12:pos + 12 + n])
+        pos += 12 + n
+    return out
+
+
+def webp_container(key_frame: bytes) -> bytes:
+    """Wrap a VP8 key frame in a RIFF/WEBP container (lossy WebP *is* a VP8 key frame), for
+    decoding through libwebp (Pillow)."""
+    chunk = key_frame + (b"\x00" if len(key_frame) & 1 else b"")
+    body = b"WEBP" + b"VP8 " + len(key_frame).to_bytes(4, "little") + chunk
+    return b"RIFF" + len(body).to_bytes(4, "little") + body

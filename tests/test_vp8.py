@@ -1,0 +1,142 @@
+"""VP8 encoder (RFC 6386; WEBRTC_ENCODER=vp8enc, reference README.md:21,35).
+
+Key frames are pinned to a real VP8 decoder: lossy WebP *is* a VP8 key frame, so the encoder's
+key frames, wrapped in a RIFF/WEBP container, go through libwebp (Pillow) and must come out as
+exactly the encoder's reconstruction -- luma through libwebp's YUV->RGB formula, chroma through a
+model of its 'fancy' (9-3-3-1) upsampler, every RGB sample equal.  Inter frames have no decoder
+in the image besides the in-tree one (mxdesk/codec/vp8_decoder.py, written from the decoding
+side of the RFC), so their parity beyond it is unpinned."""
+import io
+
+import numpy as np
+import pytest
+
+from mxdesk.codec.vp8_decoder import Decoder, webp_container
+
+from .test_cpu_encoder import synthetic_nv12
+
+Image = pytest.importorskip("PIL.Image")
+pytestmark = pytest.mark.skipif(not __import__("PIL.features").features.check("webp"), reason="Pillow without WebP")
+
+
+def libwebp_rgb(Y, U, V):
+    """libwebp's RGB output for 4:2:0 planes: fancy upsampling (row pairs, 9-3-3-1 weights) then
+    the 14-bit fixed-point YUV->RGB of its yuv.h."""
+    h, w = Y.shape
+    out = np.zeros((h, w, 3), np.int64)
+    mh = lambda v, c: (v * c) >> 8  # noqa: E731
+
+    def emit(yrow, u, v, dst):
+        dst[:, 0] = np.clip((mh(yrow, 19077) + mh(v, 26149) - 14234) >> 6, 0, 255)
+        dst[:, 1] = np.clip((mh(yrow, 19077) - mh(u, 6419) - mh(v, 13320) + 8708) >> 6, 0, 255)
+        dst[:, 2] = np.clip((mh(yrow, 19077) + mh(u, 33050) - 17685) >> 6, 0, 255)
+
+    def pair(tu, cu, n):
+        top, bot = np.zeros(n, np.int64), np.zeros(n, np.int64)
+        tl, lf = int(tu[0]), int(cu[0])
+        top[0], bot[0] = (3 * tl + lf + 2) >> 2, (3 * lf + tl + 2) >> 2
+        for x in range(1, ((n - 1) >> 1) + 1):
+            t, c = int(tu[x]), int(cu[x])
+            avg = tl + t + lf + c + 8
+            d12, d03 = (avg + 2 * (t + lf)) >> 3, (avg + 2 * (tl + c)) >> 3
+            top[2 * x - 1], top[2 * x] = (d12 + tl) >> 1, (d03 + t) >> 1
+            bot[2 * x - 1], bot[2 * x] = (d03 + lf) >> 1, (d12 + c) >> 1
+            tl, lf = t, c
+        if not n & 1:
+            top[n - 1], bot[n - 1] = (3 * tl + lf + 2) >> 2, (3 * lf + tl + 2) >> 2
+        return top, bot
+
+    emit(Y[0], pair(U[0], U[0], w)[0], pair(V[0], V[0], w)[0], out[0])
+    k = 1
+    while 2 * k - 1 < h:
+        ut, ub = pair(U[k - 1], U[min(k, U.shape[0] - 1)], w)
+        vt, vb = pair(V[k - 1], V[min(k, V.shape[0] - 1)], w)
+        emit(Y[2 * k - 1], ut, vt, out[2 * k - 1])
+        if 2 * k < h:
+            emit(Y[2 * k], ub, vb, out[2 * k])
+        k += 1
+    if not h & 1:
+        emit(Y[h - 1], pair(U[h // 2 - 1], U[h // 2 - 1], w)[0], pair(V[h // 2 - 1], V[h // 2 - 1], w)[0], out[h - 1])
+    return out
+
+
+def _picture(w, h, seed):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    y = (40 + 60 * np.sin(xx / 7.0) + 50 * np.cos(yy / 5.0) + rng.integers(0, 40, (h, w))).clip(16, 235)
+    cy, cx = np.mgrid[0:h // 2, 0:w // 2]
+    u = (128 + 50 * np.sin(cx / 5.0) + rng.integers(-20, 20, (h // 2, w // 2))).clip(16, 240)
+    v = (128 + 50 * np.cos(cy / 4.0) + rng.integers(-20, 20, (h // 2, w // 2))).clip(16, 240)
+    uv = np.zeros((h // 2, w), np.uint8)
+    uv[:, 0::2], uv[:, 1::2] = u, v
+    return y.astype(np.uint8), uv
+
+
+def _encoder(native, w, h, **kw):
+    c = native.EncoderConfig()
+    c.width, c.height = w, h
+    c.bitrate_kbps, c.qp, c.search_range = kw.get("kbps", 0), kw.get("qp", 30), kw.get("sr", 8)
+    return native.CpuVp8Encoder(c)
+
+
+@pytest.mark.parametrize("w,h,qp", [(96, 64, 20), (176, 144, 30), (64, 48, 44), (100, 60, 26)])
+def test_key_frame_decodes_through_libwebp(native, w, h, qp):
+    y, uv = _picture(w, h, qp)
+    enc = _encoder(native, w, h, qp=qp)
+    frame = enc.encode(y, uv)
+    assert enc.stats.idr == 1 and not frame[0] & 1  # frame tag: key frame
+    ry, ruv = enc.recon()
+    rgb = np.asarray(Image.open(io.BytesIO(webp_container(frame))).convert("RGB")).astype(np.int64)
+    ref = libwebp_rgb(ry[:h, :w].astype(np.int64), ruv[:h // 2, 0:w:2].astype(np.int64),
+                      ruv[:h // 2, 1:w:2].astype(np.int64))
+    assert rgb.shape == ref.shape and np.array_equal(rgb, ref), int((rgb != ref).any(axis=2).sum())
+
+
+def test_gray_key_frame_luma_through_libwebp(native):
+    # constant chroma: libwebp's RGB is a function of the luma alone -> equal to the formula
+    w, h = 176, 96
+    y, _ = _picture(w, h, 3)
+    uv = np.full((h // 2, w), 128, np.uint8)
+    enc = _encoder(native, w, h, qp=24)
+    frame = enc.encode(y, uv)
+    ry, ruv = enc.recon()
+    assert (ruv == 128).all()
+    rgb = np.asarray(Image.open(io.BytesIO(webp_container(frame))).convert("RGB")).astype(np.int64)
+    Y = ry[:h, :w].astype(np.int64)
+    assert np.array_equal(rgb[..., 0], np.clip((((Y * 19077) >> 8) + ((128 * 26149) >> 8) - 14234) >> 6, 0, 255))
+
+
+@pytest.mark.parametrize("w,h,kbps,qp", [(96, 64, 0, 28), (160, 96, 0, 40), (100, 60, 300, 30), (320, 192, 600, 30)])
+def test_inter_frames_decode_to_reconstruction(native, w, h, kbps, qp):
+    """I + P frames of a moving scene (full-sample vectors of every parity -> the chroma six-tap
+    half-sample phase), a forced key frame in the middle, rate control on / off."""
+    enc = _encoder(native, w, h, kbps=kbps, qp=qp)
+    frames, recs = [], []
+    for t in range(7):
+        y, uv = synthetic_nv12(w, h, t, seed=t % 3)
+        frames.append(enc.encode(y, uv, t == 4))
+        recs.append(tuple(a.copy() for a in enc.recon()))
+    dec = Decoder()
+    dec.decode(frames)
+    for t, ((yy, u, v), (ry, ruv)) in enumerate(zip(dec.frames_coded, recs)):
+        assert np.array_equal(yy, ry), f"frame {t} luma"
+        assert np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2]), f"frame {t} chroma"
+    assert dec.stats["key"] == 2 and dec.stats["inter"] == 5
+    assert dec.stats["new"] > 0  # coded vectors
+
+
+def test_vp8_psnr_and_motion(native):
+    # the encoder tracks a translating picture: P frames are far smaller than the key frame
+    w, h = 192, 128
+    base, uv0 = _picture(w + 32, h, 7)
+    enc = _encoder(native, w, h, qp=26, sr=16)
+    sizes, psnrs = [], []
+    for t in range(5):
+        y = np.ascontiguousarray(base[:, 2 * t: 2 * t + w])
+        uv = np.ascontiguousarray(uv0[:, 2 * t: 2 * t + w])
+        sizes.append(len(enc.encode(y, uv)))
+        ry, _ = enc.recon()
+        mse = np.mean((ry[:h, :w].astype(float) - y) ** 2)
+        psnrs.append(10 * np.log10(255 ** 2 / mse))
+    assert min(psnrs) > 32, psnrs
+    assert max(sizes[1:]) < sizes[0] / 3, sizes
