@@ -34,6 +34,13 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 
+# codec -> (name, encoder element, bitstream profile)
+CODEC_LABEL = {
+    "h264": ("H.264", "mxh264enc", "H.264 Constrained Baseline"),
+    "hevc": ("HEVC", "mxh265enc", "HEVC Main profile"),
+    "vp8": ("VP8", "mxvp8enc", "VP8 (RFC 6386) key + inter frames"),
+}
+
 def density_probe(N, cfg, fps: int, ks=(8, 16, 32, 48, 64, 96, 128), seconds: float = 1.0) -> dict:
     """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1), every
     1/fps slot each submits one frame and collects it; K is sustained if no slot overran
@@ -98,8 +105,9 @@ def main() -> None:
     ap.add_argument("--out-width", type=int, default=0, help="encode width (0 = desktop width; else fused Lanczos-3 + CSC)")
     ap.add_argument("--out-height", type=int, default=0)
     ap.add_argument("--bitrate-kbps", type=int, default=8000)
-    ap.add_argument("--codec", default="h264", choices=["h264", "hevc"],
-                    help="h264 (headline, mxh264enc) or hevc (mxh265enc, BASELINE config '4K60 HEVC')")
+    ap.add_argument("--codec", default="h264", choices=["h264", "hevc", "vp8"],
+                    help="h264 (headline, mxh264enc), hevc (mxh265enc, BASELINE config '4K60 HEVC') or vp8 "
+                         "(mxvp8enc, the reference's WEBRTC_ENCODER=vp8enc)")
     ap.add_argument("--tu-split", type=int, default=None,
                     help="HEVC: let inter CUs split their transform tree into 8x8 / 4x4 TUs (default: encoder default)")
     ap.add_argument("--search-range", type=int, default=16)
@@ -128,6 +136,8 @@ def main() -> None:
                          "multi-rank plumbing with several ranks on one GPU)")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
+    if args.codec == "vp8":
+        args.subpel = 0  # VP8 vectors here are full-sample (the reported ME setting says so)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -259,9 +269,9 @@ def main() -> None:
     if rank == 0:
         out = {
             # BASELINE.json's metric verbatim for the headline configuration
-            "metric": "encoded FPS + p50 end-to-end latency at 1080p60 H.264; concurrent sessions/node"
-                      if args.codec == "h264" else
-                      "encoded FPS (HEVC desktop session, aggregate over GPUs) + p50 E2E latency",
+            "metric": {"h264": "encoded FPS + p50 end-to-end latency at 1080p60 H.264; concurrent sessions/node",
+                       "hevc": "encoded FPS (HEVC desktop session, aggregate over GPUs) + p50 E2E latency",
+                       "vp8": "encoded FPS (VP8 desktop session, aggregate over GPUs) + p50 E2E latency"}[args.codec],
             "value": round(fps_total, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -287,14 +297,13 @@ def main() -> None:
             # GPU from one host thread, every frame of every session encoded within its 1/fps slot
             "sessions_per_gpu_at_60fps_measured": density["sustained"] if density else None,
             "density_probe": density,
-            "dtype": "uint8 video (8-bit 4:2:0), " + ("H.264 Constrained Baseline" if args.codec == "h264"
-                                                       else "HEVC Main profile"),
+            "dtype": "uint8 video (8-bit 4:2:0), " + CODEC_LABEL[args.codec][2],
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",
             "config": {
-                "model": f"{args.width}x{args.height}@{args.fps} {'H.264' if args.codec == 'h264' else 'HEVC'}"
+                "model": f"{args.width}x{args.height}@{args.fps} {CODEC_LABEL[args.codec][0]}"
                          " desktop session"
                          + (f" scaled to {args.out_width}x{args.out_height}" if args.out_width else "")
-                         + f" ({'mxh264enc' if args.codec == 'h264' else 'mxh265enc'}, CBR "
+                         + f" ({CODEC_LABEL[args.codec][1]}, CBR "
                          f"{args.bitrate_kbps} kbps, ME +/-{args.search_range} qpel={args.subpel})",
                 "global_batch": world * K,
                 "seq_len": args.width * args.height,

@@ -283,6 +283,62 @@ PYBIND11_MODULE(_native, m) {
         .def("set_bitrate", [](vp8::CpuVp8Encoder& e, int k) { e.common().set_bitrate(k); })
         .def_property_readonly("stats", &vp8::CpuVp8Encoder::last_stats);
 
+    py::class_<vp8::GpuVp8Encoder>(m, "GpuVp8Encoder")
+        .def(py::init([](const h264::EncoderConfig& c, uintptr_t stream) {
+                 return new vp8::GpuVp8Encoder(c, as_stream(stream));
+             }),
+             py::arg("config"), py::arg("stream") = 0)
+        .def_property_readonly("pitch", &vp8::GpuVp8Encoder::pitch)
+        .def_property_readonly("coded_height", [](vp8::GpuVp8Encoder& e) { return e.geometry().coded_h; })
+        .def(
+            "encode",
+            [](vp8::GpuVp8Encoder& e, uintptr_t y, uintptr_t uv, bool force_idr) {
+                std::vector<uint8_t> au;
+                {
+                    py::gil_scoped_release rel;
+                    e.submit(as_ptr<const uint8_t>(y), as_ptr<const uint8_t>(uv), force_idr);
+                    au = e.collect();
+                }
+                return to_bytes(au);
+            },
+            py::arg("y_ptr"), py::arg("uv_ptr"), py::arg("force_idr") = false)
+        .def("submit", [](vp8::GpuVp8Encoder& e, uintptr_t y, uintptr_t uv,
+                          bool force_idr) { e.submit(as_ptr<const uint8_t>(y), as_ptr<const uint8_t>(uv), force_idr); })
+        .def("collect",
+             [](vp8::GpuVp8Encoder& e) {
+                 std::vector<uint8_t> au;
+                 {
+                     py::gil_scoped_release rel;
+                     au = e.collect();
+                 }
+                 return to_bytes(au);
+             })
+        .def("recon",
+             [](vp8::GpuVp8Encoder& e) {
+                 const auto& g = e.geometry();
+                 return py::make_tuple(copy_plane(e.recon_y(), g.pitch, g.coded_w, g.coded_h),
+                                       copy_plane(e.recon_uv(), g.pitch, g.coded_w, g.coded_h / 2));
+             })
+        .def("mb_info",
+             [](vp8::GpuVp8Encoder& e) {  // (nmb, 4) of the last collected frame, as CpuVp8Encoder.mb_info
+                 const auto& g = e.geometry();
+                 const size_t n = (size_t)g.mb_w * g.mb_h;
+                 py::array_t<int32_t> a({(py::ssize_t)n, (py::ssize_t)4});
+                 int32_t* d = a.mutable_data();
+                 const vp8::Vp8Mb* v = e.last_mb_info();
+                 if (!v) throw std::logic_error("GpuVp8Encoder: no frame collected");
+                 for (size_t i = 0; i < n; ++i) {
+                     d[4 * i] = v[i].ymode;
+                     d[4 * i + 1] = v[i].uvmode;
+                     d[4 * i + 2] = v[i].mvx;
+                     d[4 * i + 3] = v[i].mvy;
+                 }
+                 return a;
+             })
+        .def("request_idr", [](vp8::GpuVp8Encoder& e) { e.common().request_idr(); })
+        .def("set_bitrate", [](vp8::GpuVp8Encoder& e, int k) { e.common().set_bitrate(k); })
+        .def_property_readonly("stats", &vp8::GpuVp8Encoder::last_stats);
+
     py::class_<hevc::CpuHevcEncoder>(m, "CpuHevcEncoder")
         .def(py::init<const h264::EncoderConfig&>())
         .def(

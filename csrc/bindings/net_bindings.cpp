@@ -5,6 +5,7 @@
 #include "../net/dtls.h"
 #include "../net/rtp_h264.h"
 #include "../net/rtp_h265.h"
+#include "../net/rtp_vp8.h"
 #include "../net/sctp.h"
 #include "../net/srtp.h"
 
@@ -147,5 +148,14 @@ void register_net(py::module& m) {
         .def_property_readonly("ssrc", &RtpH265Packetizer::ssrc)
         .def_property_readonly("packets", &RtpH265Packetizer::packets)
         .def_property_readonly("octets", &RtpH265Packetizer::octets);
+    py::class_<RtpVp8Packetizer>(n, "RtpVp8Packetizer")
+        .def(py::init<uint32_t, uint8_t, size_t, uint16_t, uint16_t>(), py::arg("ssrc"), py::arg("payload_type"),
+             py::arg("max_payload") = 1150, py::arg("first_seq") = 0, py::arg("first_picture_id") = 0)
+        .def("packetize", [](RtpVp8Packetizer& p, py::bytes frame, uint32_t ts) { return BV(p.packetize(frame, ts)); })
+        .def_property_readonly("next_seq", &RtpVp8Packetizer::next_seq)
+        .def_property_readonly("next_picture_id", &RtpVp8Packetizer::next_picture_id)
+        .def_property_readonly("ssrc", &RtpVp8Packetizer::ssrc)
+        .def_property_readonly("packets", &RtpVp8Packetizer::packets)
+        .def_property_readonly("octets", &RtpVp8Packetizer::octets);
     n.def("split_annexb", [](py::bytes au) { return BV(split_annexb(au)); });
 }

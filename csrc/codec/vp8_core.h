@@ -37,9 +37,11 @@ struct Vp8Mb {
     uint8_t uvmode;    // DC / V / H / TM
     uint8_t pad0, pad1;
     uint32_t nz;       // bit b: block b (0..24) has a non-zero level
+    uint32_t slot;     // GPU: index of the macroblock's levels in the compacted level buffer
+    uint32_t sse[3];   // GPU: Y / U / V distortion over the display area
     uint32_t pad2;
 };
-static_assert(sizeof(Vp8Mb) == 16, "Vp8Mb layout");
+static_assert(sizeof(Vp8Mb) == 32, "Vp8Mb layout");
 
 // zigzag scan -> raster position, coefficient bands (13.3)
 constexpr uint8_t kZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};

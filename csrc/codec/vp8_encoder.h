@@ -85,7 +85,7 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
 // the decoder's clamping); every macroblock of the picture is inter (P frames).  cnt[4] out.
 void find_near_mvs(const Vp8Mb* mbs, int mb_w, int mb_h, int mbx, int mby, int near_mv[3][2], int cnt[4]);
 // Legal full-sample vector range of a macroblock: the decoder never clamps vectors inside it.
-inline void mv_bounds(int mb_w, int mb_h, int mbx, int mby, int* lo_x, int* hi_x, int* lo_y, int* hi_y) {
+MXV8 void mv_bounds(int mb_w, int mb_h, int mbx, int mby, int* lo_x, int* hi_x, int* lo_y, int* hi_y) {
     *lo_x = -(mbx * 16 + 16) + 3;
     *hi_x = (mb_w - 1 - mbx) * 16 + 16 - 3;
     *lo_y = -(mby * 16 + 16) + 3;
@@ -136,28 +136,42 @@ class CpuVp8Encoder {
 
 // Device layout of the GPU encoder
 struct Vp8FrameState {
-    const uint8_t* ref_y;
+    const uint8_t* ref_y;   // previous reconstruction (P frames)
     const uint8_t* ref_uv;
-    uint8_t* rec_y;
+    uint8_t* rec_y;         // this frame's reconstruction
     uint8_t* rec_uv;
-    const uint8_t* hp_f;  // padded full-sample reference (shared H.264 k_hpel), origin applied
+    uint8_t* hp_f;          // padded full-sample reference (origin applied; k_vp8_pad writes it)
     int32_t hp_pitch;
     int32_t key;
     int32_t qindex;
-    int32_t epoch;  // nonzero, new every frame: key-frame wavefront progress tag
+    int32_t epoch;          // nonzero, new every frame: key-frame wavefront progress tag (20 bits)
+    int32_t q[6];           // Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
+    uint32_t qm[6];         // ceil(2^32 / (3 q)): the dead-zone quantiser's division as a multiply-high
+};
+// Both per-frame states in one block: one host->device copy per frame.
+struct Vp8States {
+    Vp8FrameState v;
+    h264::FrameState me;  // motion search state of the shared H.264 kernel (qp, range, planes)
 };
 struct Vp8DeviceBuffers {
-    Vp8FrameState* fs;
-    Vp8Mb* mb;             // [nmb] records
-    int16_t* lv;           // [nmb * 400] levels
+    Vp8States* st;         // device copy of the frame states
+    Vp8Mb* mb;             // [nmb] records (device)
+    int16_t* lv;           // [nmb * 400] levels (device)
     uint32_t* prog;        // [mb_h] key-frame wavefront progress (epoch << 12 | MBs done)
-    uint64_t* line;        // [mb_h][coded_w / 8 * 2] key-frame hand-off: bottom luma + chroma rows
-    h264::DeviceBuffers me;  // shared H.264 motion search state (frame state + MbInfo with vectors)
+    uint64_t* line;        // [mb_h][coded_w / 4] key-frame hand-off: bottom luma + chroma rows
+    int* err;              // mapped host word: nonzero if a wavefront spin timed out
+    Vp8Mb* mb_host;        // mapped host: records with their level slots (k_vp8_gather)
+    int16_t* lv_host;      // mapped host: levels of the coded macroblocks, row-compacted
+    h264::DeviceBuffers me;  // shared H.264 motion search (fs = &st->me, mb = vectors)
 };
+// P frames: pad the reference, shared integer motion search, then one wave per macroblock.
 void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y,
                       const uint8_t* src_uv, hipStream_t stream);
+// Key frames: one wave per macroblock row, rows handing their bottom edges down (wavefront).
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream);
+// Records + the coded macroblocks' levels into the mapped host buffers (per-row compaction).
+void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream);
 
 class GpuVp8Encoder final : public VideoEncoder {
    public:
@@ -181,14 +195,14 @@ class GpuVp8Encoder final : public VideoEncoder {
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void record_start() override;
     void record_done() override;
+    h264::EncoderCommon& common() { return common_; }
+    // records of the last collected frame (valid until that slot is submitted again)
+    const Vp8Mb* last_mb_info() const { return last_mb_; }
 
    private:
     struct Slot {
         Vp8DeviceBuffers buf{};
-        Vp8FrameState* fs_host = nullptr;
-        h264::FrameState* me_fs_host = nullptr;
-        Vp8Mb* mb_host = nullptr;   // pinned copies of the records / levels (D2H after analysis)
-        int16_t* lv_host = nullptr;
+        Vp8States* st_host = nullptr;  // pinned: copied to buf.st at the start of the frame
         hipEvent_t start = nullptr, done = nullptr;
         bool key = false;
         int qp = 0, qindex = 0;
@@ -197,7 +211,8 @@ class GpuVp8Encoder final : public VideoEncoder {
     void free_slot(Slot& s);
     void fill_state(Slot& s, bool key, int qp, int ref, int cur);
     int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
-    void write_slot(Slot& s, std::vector<uint8_t>& out);
+    void check_slot(Slot& s);
+    void write_slot(const Slot& s, std::vector<uint8_t>& out);
 
     h264::EncoderConfig cfg_;
     h264::EncoderCommon common_;
@@ -208,7 +223,8 @@ class GpuVp8Encoder final : public VideoEncoder {
     int next_slot_ = 0, prep_slot_ = 0;
     std::deque<int> inflight_;
     hipEvent_t last_done_ = nullptr;
-    uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};
+    const Vp8Mb* last_mb_ = nullptr;
+    uint8_t* hp_ = nullptr;  // padded full-sample reference
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};

@@ -1,0 +1,249 @@
+// GpuVp8Encoder: HIP analysis (vp8_kernels.hip) + host boolean coding (vp8_bitstream.cpp).
+//
+// Per frame, on the caller's stream: one host->device copy of the frame states, the analysis
+// kernels (P: pad + shared motion search + k_vp8_inter; key: the k_vp8_key wavefront), then
+// k_vp8_gather, which leaves the records and the coded macroblocks' levels in mapped host memory.
+// collect() codes the first partition on the calling thread and the token partitions (one per
+// group of macroblock rows) on a small worker pool; with pipeline depth 2 that host work overlaps
+// the GPU analysis of the next frame.  Decisions and samples equal CpuVp8Encoder's (tests/test_gpu_vp8.py).
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "../common/hip_check.h"
+#include "h264_core.h"
+#include "h264_mb.h"
+#include "vp8_encoder.h"
+
+namespace mx {
+namespace vp8 {
+
+namespace {
+int pool_threads() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::clamp(hc ? hc / 2 : 1u, 1u, 8u);
+}
+int log2_parts_for(int mb_h) { return mb_h >= 8 ? 3 : (mb_h >= 4 ? 2 : (mb_h >= 2 ? 1 : 0)); }
+}  // namespace
+
+void GpuVp8Encoder::alloc_slot(Slot& s) {
+    const int nmb = geom_.mb_w * geom_.mb_h;
+    Vp8DeviceBuffers& b = s.buf;
+    HIP_CHECK(hipMalloc(&b.st, sizeof(Vp8States)));
+    HIP_CHECK(hipMalloc(&b.mb, sizeof(Vp8Mb) * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.prog, sizeof(uint32_t) * (size_t)geom_.mb_h));
+    HIP_CHECK(hipMemsetAsync(b.prog, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
+    HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * (size_t)geom_.mb_h * (geom_.coded_w / 4)));
+    HIP_CHECK(hipHostMalloc(&b.err, sizeof(int), hipHostMallocMapped));
+    *b.err = 0;
+    HIP_CHECK(hipHostMalloc(&b.mb_host, sizeof(Vp8Mb) * (size_t)nmb, hipHostMallocMapped));
+    HIP_CHECK(hipHostMalloc(&b.lv_host, sizeof(int16_t) * kCoefPerMb * (size_t)nmb, hipHostMallocMapped));
+    HIP_CHECK(hipMalloc(&b.me.mb, sizeof(h264::MbInfo) * (size_t)nmb));
+    b.me.fs = &b.st->me;
+    HIP_CHECK(hipHostMalloc(&s.st_host, sizeof(Vp8States), hipHostMallocDefault));
+    std::memset(s.st_host, 0, sizeof(Vp8States));
+    HIP_CHECK(hipEventCreate(&s.start));
+    HIP_CHECK(hipEventCreate(&s.done));
+}
+
+void GpuVp8Encoder::free_slot(Slot& s) {
+    Vp8DeviceBuffers& b = s.buf;
+    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.prog, (void*)b.line, (void*)b.me.mb})
+        if (p) (void)hipFree(p);
+    for (void* p : {(void*)b.err, (void*)b.mb_host, (void*)b.lv_host, (void*)s.st_host})
+        if (p) (void)hipHostFree(p);
+    for (hipEvent_t e : {s.start, s.done})
+        if (e) (void)hipEventDestroy(e);
+}
+
+GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
+    : cfg_(cfg), common_(cfg), stream_(stream), pool_(pool_threads()) {
+    if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
+        throw std::invalid_argument("pipeline_depth must be 1 or 2");
+    if (cfg.width > 16383 || cfg.height > 16383) throw std::invalid_argument("vp8: picture larger than 16383");
+    depth_ = cfg.pipeline_depth;
+    geom_.width = cfg.width;
+    geom_.height = cfg.height;
+    geom_.mb_w = common_.mb_w();
+    geom_.mb_h = common_.mb_h();
+    geom_.coded_w = geom_.mb_w * 16;
+    geom_.coded_h = geom_.mb_h * 16;
+    geom_.pitch = (geom_.coded_w + 255) & ~255;
+    if (geom_.mb_w > 512) throw std::invalid_argument("vp8: picture too wide (k_vp8_gather ranks <= 512 MBs per row)");
+    log2_parts_ = log2_parts_for(geom_.mb_h);
+    const size_t ysz = (size_t)geom_.pitch * geom_.coded_h, uvsz = ysz / 2;
+    for (int i = 0; i < 2; ++i) {
+        HIP_CHECK(hipMalloc(&rec_y_[i], ysz));
+        HIP_CHECK(hipMalloc(&rec_uv_[i], uvsz));
+        HIP_CHECK(hipMemsetAsync(rec_y_[i], 0, ysz, stream_));
+        HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
+    }
+    hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
+    HIP_CHECK(hipMalloc(&hp_, (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad)));
+    for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+GpuVp8Encoder::~GpuVp8Encoder() {
+    (void)hipStreamSynchronize(stream_);
+    for (int i = 0; i < 2; ++i) {
+        (void)hipFree(rec_y_[i]);
+        (void)hipFree(rec_uv_[i]);
+    }
+    (void)hipFree(hp_);
+    for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
+}
+
+void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
+    const size_t org = (size_t)h264::kHpelPad * hp_pitch_ + h264::kHpelPad;
+    Vp8FrameState& f = s.st_host->v;
+    f.ref_y = rec_y_[ref];
+    f.ref_uv = rec_uv_[ref];
+    f.rec_y = rec_y_[cur];
+    f.rec_uv = rec_uv_[cur];
+    f.hp_f = hp_ + org;
+    f.hp_pitch = hp_pitch_;
+    f.key = key ? 1 : 0;
+    s.qindex = qindex_for_qp(qp);
+    f.qindex = s.qindex;
+    if (++epoch_ > 0xfffffu) epoch_ = 1;  // 20-bit tag, never 0
+    f.epoch = (int32_t)epoch_;
+    const Quant Q = quant_of(s.qindex);
+    const int q[6] = {Q.y1dc, Q.y1ac, Q.y2dc, Q.y2ac, Q.uvdc, Q.uvac};
+    for (int i = 0; i < 6; ++i) {
+        f.q[i] = q[i];
+        f.qm[i] = 0xffffffffu / (uint32_t)(3 * q[i]) + 1u;  // ceil(2^32 / 3q)
+    }
+    h264::FrameState& m = s.st_host->me;
+    std::memset(&m, 0, sizeof m);
+    m.ref_y = rec_y_[ref];
+    m.ref_uv = rec_uv_[ref];
+    m.qp = qp;
+    m.search_range = h264::me_range(cfg_.search_range);
+    m.me_coarse = cfg_.me_coarse;
+    m.subpel = 0;  // VP8 vectors here are full-sample
+    m.hp_pitch = hp_pitch_;
+    m.hp_f = m.hp_h = m.hp_v = m.hp_j = hp_ + org;
+}
+
+void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* src_uv) {
+    Slot& s = slots_[prep_slot_];
+    HIP_CHECK(hipMemcpyAsync(s.buf.st, s.st_host, sizeof(Vp8States), hipMemcpyHostToDevice, stream_));
+    if (key)
+        launch_vp8_key(geom_, s.buf, src_y, src_uv, stream_);
+    else
+        launch_vp8_inter(geom_, s.buf, src_y, src_uv, stream_);
+    launch_vp8_gather(geom_, s.buf, stream_);
+    HIP_CHECK(hipGetLastError());
+}
+
+void GpuVp8Encoder::check_slot(Slot& s) {
+    if (*s.buf.err) {  // a key-frame hand-off spin timed out: the reconstruction is unreliable
+        *s.buf.err = 0;
+        have_ref_ = false;
+        throw std::runtime_error("vp8 gpu encoder: key-frame wavefront hand-off timed out");
+    }
+}
+
+void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out) {
+    const Vp8Mb* mbs = s.buf.mb_host;
+    const int16_t* lv = s.buf.lv_host;
+    write_frame(FrameDesc{s.key, cfg_.width, cfg_.height, geom_.mb_w, geom_.mb_h, s.qindex, log2_parts_}, mbs,
+                [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
+                [&](int n, const std::function<void(int)>& fn) { pool_.run(n, fn); });
+}
+
+int GpuVp8Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp) {
+    // synchronous key frame at `qp` (the rate controller's first-frame probe); the real first
+    // frame overwrites the reconstruction
+    if (!inflight_.empty()) throw std::logic_error("GpuVp8Encoder: probe with frames in flight");
+    prep_slot_ = 0;
+    Slot& s = slots_[0];
+    s.key = true;
+    fill_state(s, true, qp, cur_ ^ 1, cur_);
+    enqueue_body(true, src_y, src_uv);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    check_slot(s);
+    std::vector<uint8_t> tmp;
+    write_slot(s, tmp);
+    return (int)tmp.size();
+}
+
+bool GpuVp8Encoder::prepare(bool force_idr) {
+    if ((int)inflight_.size() >= depth_) throw std::logic_error("GpuVp8Encoder: collect() a frame first (pipeline full)");
+    const int n = (depth_ == 1) ? 0 : next_slot_;
+    next_slot_ = (next_slot_ + 1) % depth_;
+    prep_slot_ = n;
+    Slot& s = slots_[n];
+    common_.begin_frame(force_idr || !have_ref_);
+    have_ref_ = true;
+    s.key = common_.cur_idr();
+    s.qp = common_.cur_qp();
+    const int ref = cur_;
+    cur_ ^= 1;
+    fill_state(s, s.key, s.qp, ref, cur_);
+    return s.key;
+}
+
+void GpuVp8Encoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
+
+void GpuVp8Encoder::record_done() {
+    HIP_CHECK(hipEventRecord(slots_[prep_slot_].done, stream_));
+    inflight_.push_back(prep_slot_);
+}
+
+void GpuVp8Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
+    while (common_.wants_probe()) {
+        const int q = common_.probe_qp();
+        common_.add_probe(q, probe_bytes(src_y, src_uv, q));
+    }
+    const bool key = prepare(force_idr);
+    record_start();
+    enqueue_body(key, src_y, src_uv);
+    record_done();
+}
+
+const std::vector<uint8_t>& GpuVp8Encoder::collect() {
+    if (inflight_.empty()) throw std::logic_error("GpuVp8Encoder: nothing submitted");
+    const int n = inflight_.front();
+    inflight_.pop_front();
+    Slot& s = slots_[n];
+    HIP_CHECK(hipEventSynchronize(s.done));
+    last_done_ = s.done;
+    last_mb_ = s.buf.mb_host;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, s.start, s.done);
+    try {
+        check_slot(s);
+    } catch (...) {
+        common_.end_frame(0, s.key);
+        throw;
+    }
+    au_.clear();
+    write_slot(s, au_);
+    const int nmb = geom_.mb_w * geom_.mb_h;
+    uint64_t sse[3] = {0, 0, 0};
+    int skipped = 0;
+    for (int i = 0; i < nmb; ++i) {
+        const Vp8Mb& m = s.buf.mb_host[i];
+        for (int c = 0; c < 3; ++c) sse[c] += m.sse[c];
+        skipped += m.nz == 0;
+    }
+    stats_.frame_index = common_.frames();
+    stats_.idr = s.key;
+    stats_.qp = s.qp;
+    stats_.bytes = (int)au_.size();
+    stats_.encode_ms = ms;
+    stats_.skipped_mbs = skipped;
+    for (int c = 0; c < 3; ++c) stats_.sse[c] = sse[c];
+    stats_.sse_masked = sse[0];
+    stats_.masked_pixels = (int64_t)cfg_.width * cfg_.height;
+    common_.end_frame((int)au_.size(), s.key);
+    return au_;
+}
+
+}  // namespace vp8
+}  // namespace mx

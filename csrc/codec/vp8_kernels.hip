@@ -1,0 +1,566 @@
+// HIP analysis kernels of the VP8 encoder (RFC 6386; WEBRTC_ENCODER=vp8enc, reference
+// README.md:21,35): every decision and sample of CpuVp8Encoder::analyse (vp8_cpu.cpp), on the GPU.
+//
+//   P frame:   k_vp8_pad -> k_me_full (shared with H.264, full-sample search) -> k_vp8_inter
+//              -> k_vp8_gather
+//   key frame: k_vp8_key -> k_vp8_gather
+//
+// One 64-lane wave codes one macroblock: lanes 0..15 own the luma 4x4 blocks, 16..23 the chroma
+// blocks, lane 24 the second-order Y2 block -- the block index of a lane is its token block index,
+// so the non-zero mask is one ballot.  The dead-zone division of the quantiser is an exact
+// multiply-high (Vp8FrameState::qm, exact for every coefficient the transforms produce).
+// Key frames predict from reconstructed neighbours: one wave per macroblock row walks its row,
+// the row below follows one macroblock behind, fed the bottom sample rows through an agent-scope
+// hand-off line and an epoch-tagged progress word (bounded spins; a timeout raises the mapped
+// error word instead of hanging).  The boolean coder runs on host threads (vp8_bitstream.cpp);
+// k_vp8_gather hands it only the coded macroblocks' levels, compacted per row, in mapped memory.
+#include <hip/hip_runtime.h>
+
+#include "../common/hip_check.h"
+#include "h264_core.h"
+#include "h264_gpu.h"
+#include "vp8_encoder.h"
+
+namespace mx {
+namespace vp8 {
+
+namespace {
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+constexpr unsigned kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// dead-zone quantiser of vp8_core.h quantize(): (3|c| + q) / (3q) as a multiply-high
+__device__ __forceinline__ int qz(int c, int q, uint32_t m) {
+    const int a = c < 0 ? -c : c;
+    int l = (int)__umulhi((uint32_t)(3 * a + q), m);
+    l = l > 2048 ? 2048 : l;
+    return c < 0 ? -l : l;
+}
+
+// Staged samples of the macroblock being coded (one wave).
+struct MbLds {
+    uint8_t src[256], pred[256], rec[256];
+    uint8_t su[64], sv[64], pu[64], pv[64], ru[64], rv[64];
+    int dc[16], dcr[16];
+};
+
+// Transform, quantise and reconstruct the staged macroblock (s.src / s.pred -> s.rec, levels to
+// lv[400]); returns the non-zero block mask (bit b = block b), wave-uniform.  code_luma16 +
+// code_chroma8 of vp8_core.h, one block per lane.
+__device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restrict__ lv, int lane) {
+    int lvl[16], dq[16];
+    bool nz = false;
+    const bool luma = lane < 16, chroma = lane >= 16 && lane < 24;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lvl[k] = dq[k] = 0;
+    if (luma || chroma) {
+        int in[16];
+        if (luma) {
+            const int bx = lane & 3, by = lane >> 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = (by * 4 + i) * 16 + bx * 4 + j;
+                    in[i * 4 + j] = (int)s.src[o] - (int)s.pred[o];
+                }
+        } else {
+            const int b = (lane - 16) & 3, bx = b & 1, by = b >> 1;
+            const uint8_t* S = lane < 20 ? s.su : s.sv;
+            const uint8_t* P = lane < 20 ? s.pu : s.pv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = (by * 4 + i) * 8 + bx * 4 + j;
+                    in[i * 4 + j] = (int)S[o] - (int)P[o];
+                }
+        }
+        int coef[16];
+        fdct4x4(in, coef);
+        if (luma) s.dc[lane] = coef[0];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (luma && k == 0) continue;  // the DC travels in Y2
+            const int pos = kZigzag[k];
+            const int qi = luma ? 1 : (k == 0 ? 4 : 5);
+            const int q = F.q[qi];
+            const int l = qz(coef[pos], q, F.qm[qi]);
+            lvl[k] = l;
+            dq[pos] = l * q;
+            nz |= l != 0;
+        }
+    }
+    __syncthreads();
+    if (lane == kY2) {
+        int dcv[16], y2[16], y2q[16], dcr[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) dcv[b] = s.dc[b];
+        fwht4x4(dcv, y2);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int pos = kZigzag[k];
+            const int qi = k == 0 ? 2 : 3;
+            const int l = qz(y2[pos], F.q[qi], F.qm[qi]);
+            lvl[k] = l;
+            y2q[pos] = l * F.q[qi];
+            nz |= l != 0;
+        }
+        iwht4x4(y2q, dcr);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) s.dcr[b] = dcr[b];
+    }
+    __syncthreads();
+    if (luma || chroma) {
+        if (luma) dq[0] = s.dcr[lane];
+        int r[16];
+        idct4x4(dq, r);
+        if (luma) {
+            const int bx = lane & 3, by = lane >> 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = (by * 4 + i) * 16 + bx * 4 + j;
+                    s.rec[o] = (uint8_t)v8_clamp255((int)s.pred[o] + r[i * 4 + j]);
+                }
+        } else {
+            const int b = (lane - 16) & 3, bx = b & 1, by = b >> 1;
+            const uint8_t* P = lane < 20 ? s.pu : s.pv;
+            uint8_t* R = lane < 20 ? s.ru : s.rv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = (by * 4 + i) * 8 + bx * 4 + j;
+                    R[o] = (uint8_t)v8_clamp255((int)P[o] + r[i * 4 + j]);
+                }
+        }
+    }
+    if (lane < kBlocks) {
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = (uint32_t)(uint16_t)lvl[2 * k] | ((uint32_t)(uint16_t)lvl[2 * k + 1] << 16);
+        uint4* d = reinterpret_cast<uint4*>(lv + lane * 16);
+        d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+    const uint32_t mask = (uint32_t)__ballot(nz) & ((1u << kBlocks) - 1);
+    __syncthreads();
+    return mask;
+}
+
+// Source of the macroblock at (x0, y0) into LDS: luma one dword per lane, chroma (interleaved
+// rows) deinterleaved by the first 32 lanes.
+__device__ __forceinline__ void stage_src(MbLds& s, const h264::Geometry& g, const uint8_t* __restrict__ sy,
+                                          const uint8_t* __restrict__ suv, int x0, int y0, int lane) {
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    *reinterpret_cast<uint32_t*>(s.src + r * 16 + c4) =
+        *reinterpret_cast<const uint32_t*>(sy + (size_t)(y0 + r) * g.pitch + x0 + c4);
+    if (lane < 32) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(suv + (size_t)(y0 / 2 + r) * g.pitch + x0 + c4);
+        const int o = r * 8 + (c4 >> 1);
+        s.su[o] = (uint8_t)w;  // U V U V
+        s.sv[o] = (uint8_t)(w >> 8);
+        s.su[o + 1] = (uint8_t)(w >> 16);
+        s.sv[o + 1] = (uint8_t)(w >> 24);
+    }
+}
+
+// Reconstruction of the staged macroblock to the picture, and its distortion over the display
+// area (Y, U, V) -- wave-uniform sums.
+__device__ __forceinline__ void store_rec(const MbLds& s, const h264::Geometry& g, const Vp8FrameState& F, int x0,
+                                          int y0, int lane, uint32_t sse[3]) {
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    *reinterpret_cast<uint32_t*>(F.rec_y + (size_t)(y0 + r) * g.pitch + x0 + c4) =
+        *reinterpret_cast<const uint32_t*>(s.rec + r * 16 + c4);
+    int ey = 0;
+    if (y0 + r < g.height)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = (int)s.src[r * 16 + c4 + j] - (int)s.rec[r * 16 + c4 + j];
+            ey += x0 + c4 + j < g.width ? e * e : 0;
+        }
+    if (lane < 32) {
+        const int o = r * 8 + (c4 >> 1);
+        const uint32_t w = (uint32_t)s.ru[o] | ((uint32_t)s.rv[o] << 8) | ((uint32_t)s.ru[o + 1] << 16) |
+                           ((uint32_t)s.rv[o + 1] << 24);
+        *reinterpret_cast<uint32_t*>(F.rec_uv + (size_t)(y0 / 2 + r) * g.pitch + x0 + c4) = w;
+    }
+    const int cx = lane & 7, cy = lane >> 3;
+    const bool vis = 2 * (x0 / 2 + cx) < g.width && 2 * (y0 / 2 + cy) < g.height;
+    const int eu = (int)s.su[cy * 8 + cx] - (int)s.ru[cy * 8 + cx];
+    const int ev = (int)s.sv[cy * 8 + cx] - (int)s.rv[cy * 8 + cx];
+    sse[0] = (uint32_t)wsum(ey);
+    sse[1] = (uint32_t)wsum(vis ? eu * eu : 0);
+    sse[2] = (uint32_t)wsum(vis ? ev * ev : 0);
+}
+
+__device__ __forceinline__ void store_record(Vp8Mb* __restrict__ rec, int mvx, int mvy, int ymode, int uvmode,
+                                             uint32_t nz, const uint32_t sse[3], int lane) {
+    if (lane == 0) {
+        Vp8Mb m;
+        m.mvx = (int16_t)mvx;
+        m.mvy = (int16_t)mvy;
+        m.ymode = (uint8_t)ymode;
+        m.uvmode = (uint8_t)uvmode;
+        m.pad0 = m.pad1 = 0;
+        m.nz = nz;
+        m.slot = 0;
+        m.sse[0] = sse[0];
+        m.sse[1] = sse[1];
+        m.sse[2] = sse[2];
+        m.pad2 = 0;
+        *rec = m;
+    }
+}
+
+// ------------------------------------------------------------------ P frames
+// Padded full-sample reference (edge replicated, kHpelPad around the coded picture) for k_me_full
+// and the luma prediction; one dword per thread.
+__global__ __launch_bounds__(256) void k_vp8_pad(h264::Geometry g, const Vp8States* __restrict__ st) {
+    const Vp8FrameState& F = st->v;
+    const int W = g.coded_w + 2 * h264::kHpelPad, H = g.coded_h + 2 * h264::kHpelPad;
+    const int x4 = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y;
+    if (x4 >= W || y >= H) return;
+    const int sy = min(max(y - h264::kHpelPad, 0), g.coded_h - 1);
+    const uint8_t* row = F.ref_y + (size_t)sy * g.pitch;
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int sx = min(max(x4 + k - h264::kHpelPad, 0), g.coded_w - 1);
+        w |= (uint32_t)row[sx] << (8 * k);
+    }
+    uint8_t* dst = F.hp_f - (size_t)h264::kHpelPad * F.hp_pitch - h264::kHpelPad;
+    *reinterpret_cast<uint32_t*>(dst + (size_t)y * F.hp_pitch + x4) = w;
+}
+
+// Chroma inter prediction sample: sixtap_px of vp8_core.h with the pass of a zero phase skipped
+// (the 128 tap is exact), so the common full-sample cases load 1 or 6 samples instead of 36.
+template <class A>
+__device__ __forceinline__ int chroma_px(const A& at, int x, int y, int fx, int fy) {
+    if ((fx | fy) == 0) return at(x, y);
+    if (fy == 0) {
+        int h = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) h += kSubpel[fx][k] * at(x - 2 + k, y);
+        return v8_clamp255((h + 64) >> 7);
+    }
+    if (fx == 0) {
+        int v = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) v += kSubpel[fy][r] * at(x, y - 2 + r);
+        return v8_clamp255((v + 64) >> 7);
+    }
+    return sixtap_px(at, x, y, fx, fy);
+}
+
+__global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                   const uint8_t* __restrict__ src_y,
+                                                   const uint8_t* __restrict__ src_uv,
+                                                   const h264::MbInfo* __restrict__ me, Vp8Mb* __restrict__ mbs,
+                                                   int16_t* __restrict__ lv) {
+    __shared__ MbLds s;
+    const Vp8FrameState& F = st->v;
+    const int mbi = blockIdx.x, lane = threadIdx.x;
+    const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
+    int lo_x, hi_x, lo_y, hi_y;
+    mv_bounds(g.mb_w, g.mb_h, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
+    const int ix = min(max(me[mbi].mvx / 4, lo_x), hi_x), iy = min(max(me[mbi].mvy / 4, lo_y), hi_y);
+    stage_src(s, g, src_y, src_uv, x0, y0, lane);
+    {  // luma prediction: the padded reference covers every legal vector (mv_bounds)
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        const uint8_t* p = F.hp_f + (ptrdiff_t)(y0 + r + iy) * F.hp_pitch + x0 + c4 + ix;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = p[j];
+    }
+    const int mvx = ix * 8, mvy = iy * 8;
+    const int cvx = chroma_mv(mvx), cvy = chroma_mv(mvy);
+    {
+        const int cx = lane & 7, cy = lane >> 3, cw = g.coded_w / 2, ch = g.coded_h / 2;
+        const uint8_t* ref = F.ref_uv;
+        const int pitch = g.pitch;
+        auto at_u = [&](int xx, int yy) {
+            xx = min(max(xx, 0), cw - 1);
+            yy = min(max(yy, 0), ch - 1);
+            return (int)ref[(size_t)yy * pitch + 2 * xx];
+        };
+        auto at_v = [&](int xx, int yy) {
+            xx = min(max(xx, 0), cw - 1);
+            yy = min(max(yy, 0), ch - 1);
+            return (int)ref[(size_t)yy * pitch + 2 * xx + 1];
+        };
+        const int px = x0 / 2 + cx + (cvx >> 3), py = y0 / 2 + cy + (cvy >> 3);
+        s.pu[cy * 8 + cx] = (uint8_t)chroma_px(at_u, px, py, cvx & 7, cvy & 7);
+        s.pv[cy * 8 + cx] = (uint8_t)chroma_px(at_v, px, py, cvx & 7, cvy & 7);
+    }
+    __syncthreads();
+    const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane);
+    uint32_t sse[3];
+    store_rec(s, g, F, x0, y0, lane, sse);
+    store_record(mbs + mbi, mvx, mvy, kInter, kDcPred, nz, sse, lane);
+}
+
+// ------------------------------------------------------------------ key frames
+struct KeyEdges {
+    int ay[16], ly[16], au[8], lu[8], av[8], lvv[8];
+    int cy, cu, cv;
+};
+
+__device__ __forceinline__ int pred_of(int mode, int above, int left, int corner, int dc) {
+    switch (mode) {
+        case kVPred:
+            return above;
+        case kHPred:
+            return left;
+        case kTmPred:
+            return v8_clamp255(left + above - corner);
+        default:
+            return dc;
+    }
+}
+
+__device__ __forceinline__ int dc_value(int sum, int cnt, int log2n) {
+    if (cnt == 0) return 128;
+    const int shift = log2n + cnt;
+    return (sum + (1 << (shift - 1))) >> shift;
+}
+
+// bounded spin on the progress word of the row above (epoch << 12 | count)
+__device__ __forceinline__ void wait_row(const uint32_t* p, uint32_t epoch, int need, int* err) {
+    for (unsigned s = 0;; ++s) {
+        const uint32_t v = __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 12) == epoch && (int)(v & 0xfffu) >= need) break;
+        if (s > kSpinLimit) {
+            *err = 1;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the edge words are read with sc1 loads
+}
+
+__global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                 const uint8_t* __restrict__ src_y,
+                                                 const uint8_t* __restrict__ src_uv, Vp8Mb* __restrict__ mbs,
+                                                 int16_t* __restrict__ lv, uint32_t* __restrict__ prog,
+                                                 uint64_t* __restrict__ line, int* __restrict__ err) {
+    __shared__ MbLds s;
+    __shared__ KeyEdges E;
+    const Vp8FrameState& F = st->v;
+    const int mby = blockIdx.x, lane = threadIdx.x, y0 = mby * 16;
+    const uint32_t epoch = (uint32_t)F.epoch;
+    const int words = g.coded_w / 8;  // luma words per hand-off row; chroma follows
+    const bool top = mby == 0, bottom = mby == g.mb_h - 1;
+    const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * 2 * words;
+    uint64_t* my_line = line + (size_t)mby * 2 * words;
+    for (int mbx = 0; mbx < g.mb_w; ++mbx) {
+        const int x0 = mbx * 16, mbi = mby * g.mb_w + mbx;
+        const bool left = mbx > 0;
+        stage_src(s, g, src_y, src_uv, x0, y0, lane);
+        // ---- edges: above row and corner from the row above (hand-off line), left from our last MB
+        if (!top) {
+            if (lane == 0) wait_row(prog + mby - 1, epoch, mbx + 1, err);
+            __syncthreads();
+            if (lane < 6) {
+                int wi = lane < 2 ? 2 * mbx + lane : (lane < 4 ? words + 2 * mbx + lane - 2 : (lane == 4 ? 2 * mbx - 1 : words + 2 * mbx - 1));
+                const bool need = lane < 4 || left;
+                const uint64_t w = need ? __hip_atomic_load((const gu64*)(above_line + wi), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0;
+                if (lane < 2) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) E.ay[8 * lane + k] = (int)((w >> (8 * k)) & 0xff);
+                } else if (lane < 4) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        E.au[4 * (lane - 2) + k] = (int)((w >> (16 * k)) & 0xff);
+                        E.av[4 * (lane - 2) + k] = (int)((w >> (16 * k + 8)) & 0xff);
+                    }
+                } else if (lane == 4) {
+                    E.cy = left ? (int)(w >> 56) : 129;
+                } else {
+                    E.cu = left ? (int)((w >> 48) & 0xff) : 129;
+                    E.cv = left ? (int)(w >> 56) : 129;
+                }
+            }
+        } else {
+            if (lane < 16) E.ay[lane] = 127;
+            if (lane < 8) E.au[lane] = E.av[lane] = 127;
+            if (lane == 0) E.cy = E.cu = E.cv = 127;
+        }
+        if (!left) {
+            if (lane < 16) E.ly[lane] = 129;
+            if (lane < 8) E.lu[lane] = E.lvv[lane] = 129;
+        }
+        __syncthreads();
+        // ---- mode decisions: SAD of the four 16x16 modes (4 samples per lane), the four chroma modes
+        const int nav = top ? 0 : 1, nlf = left ? 1 : 0;
+        const int dcy = dc_value(wsum((lane < 16 && !top ? E.ay[lane] : 0) + (lane >= 16 && lane < 32 && left ? E.ly[lane - 16] : 0)),
+                                 nav + nlf, 3);
+        const int dcu = dc_value(wsum((lane < 8 && !top ? E.au[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lu[lane - 8] : 0)),
+                                 nav + nlf, 2);
+        const int dcv = dc_value(wsum((lane < 8 && !top ? E.av[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lvv[lane - 8] : 0)),
+                                 nav + nlf, 2);
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        int ymode = 0, uvmode = 0;
+        {
+            int sad[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int sv = s.src[r * 16 + c4 + j];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) sad[m] += abs(sv - pred_of(m, E.ay[c4 + j], E.ly[r], E.cy, dcy));
+            }
+            uint32_t best = ~0u;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t t = (uint32_t)wsum(sad[m]);
+                if (t < best) {
+                    best = t;
+                    ymode = m;
+                }
+            }
+        }
+        const int cx = lane & 7, cy = lane >> 3;
+        {
+            int sad[4] = {0, 0, 0, 0};
+            const int su = s.su[cy * 8 + cx], sv = s.sv[cy * 8 + cx];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                sad[m] = abs(su - pred_of(m, E.au[cx], E.lu[cy], E.cu, dcu)) +
+                         abs(sv - pred_of(m, E.av[cx], E.lvv[cy], E.cv, dcv));
+            uint32_t best = ~0u;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t t = (uint32_t)wsum(sad[m]);
+                if (t < best) {
+                    best = t;
+                    uvmode = m;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = (uint8_t)pred_of(ymode, E.ay[c4 + j], E.ly[r], E.cy, dcy);
+        s.pu[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.au[cx], E.lu[cy], E.cu, dcu);
+        s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
+        __syncthreads();
+        const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane);
+        // ---- hand the bottom rows down, then publish progress
+        if (!bottom && lane < 4) {
+            uint64_t w = 0;
+            if (lane < 2) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) w |= (uint64_t)s.rec[15 * 16 + 8 * lane + k] << (8 * k);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    w |= ((uint64_t)s.ru[7 * 8 + 4 * (lane - 2) + k] << (16 * k)) |
+                         ((uint64_t)s.rv[7 * 8 + 4 * (lane - 2) + k] << (16 * k + 8));
+            }
+            const int wi = lane < 2 ? 2 * mbx + lane : words + 2 * mbx + lane - 2;
+            __hip_atomic_store((gu64*)(my_line + wi), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!bottom) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // hand-off drained before the flag
+            if (lane == 0)
+                __hip_atomic_store((gu32*)(prog + mby), (epoch << 12) | (uint32_t)(mbx + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint32_t sse[3];
+        store_rec(s, g, F, x0, y0, lane, sse);
+        store_record(mbs + mbi, 0, 0, ymode, uvmode, nz, sse, lane);
+        // left edges of the next macroblock
+        if (lane < 16) E.ly[lane] = s.rec[lane * 16 + 15];
+        if (lane < 8) {
+            E.lu[lane] = s.ru[lane * 8 + 7];
+            E.lvv[lane] = s.rv[lane * 8 + 7];
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ hand-off to the host writer
+// One workgroup per macroblock row: the rank of each coded macroblock within its row (ballots),
+// its 800 level bytes to the mapped host buffer at slot row * mb_w + rank, every record with its
+// slot.  Only coded macroblocks cross the bus.
+__global__ __launch_bounds__(256) void k_vp8_gather(h264::Geometry g, const Vp8Mb* __restrict__ mbs,
+                                                     const int16_t* __restrict__ lv, Vp8Mb* __restrict__ mb_host,
+                                                     int16_t* __restrict__ lv_host) {
+    __shared__ int wave_cnt[4];
+    const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = g.mb_w, base = row * n;
+    // each wave owns two 64-MB chunks (mb_w <= 512)
+    uint64_t bal[2];
+    int cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int i = wave * 128 + c * 64 + lane;
+        const bool coded = i < n && mbs[base + i].nz != 0;
+        bal[c] = __ballot(coded);
+        cnt += __popcll(bal[c]);
+    }
+    if (lane == 0) wave_cnt[wave] = cnt;
+    __syncthreads();
+    int off = 0;
+    for (int w = 0; w < wave; ++w) off += wave_cnt[w];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int i = wave * 128 + c * 64 + lane;
+        const int rank = off + (c ? __popcll(bal[0]) : 0) + __popcll(bal[c] & ((1ull << lane) - 1));
+        if (i < n) {
+            Vp8Mb m = mbs[base + i];
+            m.slot = (uint32_t)(base + rank);
+            const uint4* srcw = reinterpret_cast<const uint4*>(&m);
+            uint4* dst = reinterpret_cast<uint4*>(mb_host + base + i);
+            dst[0] = srcw[0];
+            dst[1] = srcw[1];
+        }
+    }
+    // levels of the coded macroblocks: one macroblock per wave step, 50 uint4 per macroblock
+    int r0 = off;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        uint64_t b = bal[c];
+        while (b) {
+            const int k = __builtin_ctzll(b);
+            b &= b - 1;
+            const int i = wave * 128 + c * 64 + k;
+            if (lane < kCoefPerMb / 8)
+                reinterpret_cast<uint4*>(lv_host + (size_t)(base + r0) * kCoefPerMb)[lane] =
+                    reinterpret_cast<const uint4*>(lv + (size_t)(base + i) * kCoefPerMb)[lane];
+            ++r0;
+        }
+    }
+}
+
+}  // namespace
+
+void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y,
+                      const uint8_t* src_uv, hipStream_t stream) {
+    const int W = g.coded_w + 2 * h264::kHpelPad, H = g.coded_h + 2 * h264::kHpelPad;
+    hipLaunchKernelGGL(k_vp8_pad, dim3((W / 4 + 255) / 256, H), dim3(256), 0, stream, g, b.st);
+    h264::launch_me(g, b.me, src_y, stream);
+    hipLaunchKernelGGL(k_vp8_inter, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.me.mb, b.mb,
+                       b.lv);
+}
+
+void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                    hipStream_t stream) {
+    hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv, b.prog,
+                       b.line, b.err);
+}
+
+void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream) {
+    hipLaunchKernelGGL(k_vp8_gather, dim3(g.mb_h), dim3(256), 0, stream, g, b.mb, b.lv, b.mb_host, b.lv_host);
+}
+
+}  // namespace vp8
+}  // namespace mx

@@ -11,6 +11,7 @@
 #include "../common/hip_check.h"
 #include "../common/trace.h"
 #include "../codec/hevc_encoder.h"
+#include "../codec/vp8_encoder.h"
 
 namespace mx {
 
@@ -88,8 +89,10 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         enc_ = std::make_unique<h264::GpuH264Encoder>(cfg_.enc, stream_);
     else if (cfg_.codec == "hevc" || cfg_.codec == "h265")
         enc_ = std::make_unique<hevc::GpuHevcEncoder>(cfg_.enc, stream_);
+    else if (cfg_.codec == "vp8")
+        enc_ = std::make_unique<vp8::GpuVp8Encoder>(cfg_.enc, stream_);
     else
-        throw std::invalid_argument("Session: unknown codec '" + cfg_.codec + "' (h264 | hevc)");
+        throw std::invalid_argument("Session: unknown codec '" + cfg_.codec + "' (h264 | hevc | vp8)");
     const h264::Geometry& g = enc_->geometry();
     HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
     HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));

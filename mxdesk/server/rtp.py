@@ -1,4 +1,4 @@
-"""RTP/RTCP helpers in Python: H.264 depacketizer (RFC 6184) for test peers and RTCP
+"""RTP/RTCP helpers in Python: H.264 / H.265 / VP8 depacketizers (RFC 6184 / 7798 / 7741) for test peers and RTCP
 packet builders/parsers (RFC 3550 SR/RR/SDES, RFC 4585 generic NACK + PLI, RFC 5104 FIR,
 REMB receiver bandwidth estimates)."""
 from __future__ import annotations
@@ -97,6 +97,57 @@ class H265Depacketizer:
             au = b"".join(b"\x00\x00\x00\x01" + n for n in self.nals)
             self.nals = []
             return au
+        return None
+
+
+class Vp8Depacketizer:
+    """Reassembles VP8 frames from RFC 7741 packets: parses the payload descriptor (X, N, S, PID
+    and the optional PictureID / TL0PICIDX / TID / KEYIDX extensions), starts a frame at S = 1 with
+    PID 0, ends it at the marker bit.  A frame with a lost packet is dropped."""
+
+    def __init__(self):
+        self.buf: bytearray | None = None
+        self.last_seq: int | None = None
+        self.lost = 0
+        self.picture_ids: list[int] = []
+
+    @staticmethod
+    def descriptor(p: bytes) -> tuple[int, dict]:
+        b0 = p[0]
+        d = {"N": bool(b0 & 0x20), "S": bool(b0 & 0x10), "PID": b0 & 0x07, "picture_id": None}
+        off = 1
+        if b0 & 0x80:  # X
+            x = p[off]
+            off += 1
+            if x & 0x80:  # I
+                if p[off] & 0x80:  # M: 15-bit picture id
+                    d["picture_id"] = ((p[off] & 0x7F) << 8) | p[off + 1]
+                    off += 2
+                else:
+                    d["picture_id"] = p[off] & 0x7F
+                    off += 1
+            if x & 0x40:  # L: TL0PICIDX
+                off += 1
+            if x & 0x30:  # T or K: TID|Y|KEYIDX byte
+                off += 1
+        return off, d
+
+    def push(self, pkt: bytes) -> bytes | None:
+        h = rtp_header(pkt)
+        gap = self.last_seq is not None and ((h["seq"] - self.last_seq) & 0xFFFF) != 1
+        if gap:
+            self.lost += 1
+            self.buf = None
+        self.last_seq = h["seq"]
+        off, d = self.descriptor(h["payload"])
+        if d["S"] and d["PID"] == 0:
+            self.buf = bytearray()
+            self.picture_ids.append(d["picture_id"])
+        if self.buf is not None:
+            self.buf += h["payload"][off:]
+        if h["marker"] and self.buf is not None:
+            frame, self.buf = bytes(self.buf), None
+            return frame
         return None
 
 

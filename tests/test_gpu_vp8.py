@@ -1,0 +1,117 @@
+"""HIP VP8 encoder (WEBRTC_ENCODER=vp8enc, reference README.md:21,35).
+
+The GPU encoder's frames are byte-for-byte the CPU oracle's (tests/test_vp8.py pins the oracle to
+libwebp for key frames and to the in-tree RFC 6386 decoder for inter frames), reconstructions
+included; GPU key frames also go through libwebp (Pillow) directly, at 1080p too."""
+import io
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from mxdesk.codec.vp8_decoder import Decoder, webp_container  # noqa: E402
+
+from .gpu_util import pitched  # noqa: E402
+from .test_cpu_encoder import synthetic_nv12  # noqa: E402
+from .test_gpu_production_sizes import _stream, desktop_nv12  # noqa: E402
+from .test_vp8 import _picture, libwebp_rgb  # noqa: E402
+
+
+def _pair(gpu, w, h, kbps=0, qp=30, sr=8, depth=1):
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps = w, h, 60
+    cfg.bitrate_kbps, cfg.qp, cfg.search_range = kbps, qp, sr
+    cfg.pipeline_depth = depth
+    return gpu.GpuVp8Encoder(cfg, _stream()), gpu.CpuVp8Encoder(cfg)
+
+
+def _dev(genc, y, uv):
+    ch = genc.coded_height
+    dy, duv = pitched(y, genc.pitch, ch), pitched(uv, genc.pitch, ch // 2, uv=True)
+    torch.cuda.synchronize()
+    return dy, duv
+
+
+def _check(genc, cenc, gau, cau, w, h, t):
+    gm, cm = genc.mb_info(), cenc.mb_info()
+    bad = np.nonzero((gm != cm).any(axis=1))[0]
+    assert bad.size == 0, f"{w}x{h} frame {t}: MB {bad[:5]} GPU {gm[bad[:3]]} CPU {cm[bad[:3]]}"
+    gy, guv = genc.recon()
+    cy, cuv = cenc.recon()
+    assert np.array_equal(gy, cy), f"{w}x{h} frame {t}: luma reconstruction"
+    assert np.array_equal(guv, cuv), f"{w}x{h} frame {t}: chroma reconstruction"
+    assert gau == cau, f"{w}x{h} frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
+
+
+@pytest.mark.parametrize("w,h,kbps,qp", [(96, 64, 0, 28), (100, 60, 300, 30), (320, 192, 600, 24), (176, 144, 0, 44)])
+def test_gpu_vp8_bit_exact_vs_cpu(gpu, w, h, kbps, qp):
+    """Key + P frames of a moving scene (vectors of both chroma phases), a forced key frame, rate
+    control on / off: bitstreams, reconstructions and decisions equal the CPU oracle's."""
+    genc, cenc = _pair(gpu, w, h, kbps=kbps, qp=qp)
+    frames = []
+    for t in range(7):
+        y, uv = synthetic_nv12(w, h, t, seed=t % 3)
+        dy, duv = _dev(genc, y, uv)
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), t == 4)
+        cau = cenc.encode(y, uv, t == 4)
+        _check(genc, cenc, gau, cau, w, h, t)
+        frames.append(gau)
+    dec = Decoder()
+    dec.decode(frames)
+    assert dec.stats["key"] == 2 and dec.stats["inter"] == 5
+
+
+def test_gpu_vp8_key_frame_through_libwebp(gpu):
+    pil = pytest.importorskip("PIL.Image")
+    w, h = 176, 144
+    y, uv = _picture(w, h, 5)
+    genc, _ = _pair(gpu, w, h, qp=26)
+    dy, duv = _dev(genc, y, uv)
+    frame = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+    ry, ruv = genc.recon()
+    rgb = np.asarray(pil.open(io.BytesIO(webp_container(frame))).convert("RGB")).astype(np.int64)
+    ref = libwebp_rgb(ry[:h, :w].astype(np.int64), ruv[:h // 2, 0:w:2].astype(np.int64),
+                      ruv[:h // 2, 1:w:2].astype(np.int64))
+    assert np.array_equal(rgb, ref)
+
+
+def test_gpu_vp8_1080p_desktop(gpu):
+    """The synthetic desktop at 1920x1080 with rate control: GPU == CPU for a key frame and P
+    frames; the key frame decodes through libwebp to the encoder's reconstruction."""
+    pil = pytest.importorskip("PIL.Image")
+    w, h = 1920, 1080
+    genc, cenc = _pair(gpu, w, h, kbps=8000, sr=16)
+    for t in range(3):
+        y, uv = desktop_nv12(gpu, w, h, t)
+        dy, duv = _dev(genc, y, uv)
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        _check(genc, cenc, gau, cau, w, h, t)
+        if t == 0:
+            ry, ruv = genc.recon()
+            rgb = np.asarray(pil.open(io.BytesIO(webp_container(gau))).convert("RGB")).astype(np.int64)
+            ref = libwebp_rgb(ry[:h, :w].astype(np.int64), ruv[:h // 2, 0:w:2].astype(np.int64),
+                              ruv[:h // 2, 1:w:2].astype(np.int64))
+            assert np.array_equal(rgb, ref)
+    st = genc.stats
+    assert not st.idr and st.skipped_mbs > 0
+
+
+def test_gpu_vp8_pipelined_depth2_matches(gpu):
+    """Depth 2 (host partition coding of frame n overlapping the GPU analysis of frame n+1)
+    produces the depth-1 bitstream (fixed QP: with rate control the pipelined QP lags a frame)."""
+    w, h = 320, 192
+    a, _ = _pair(gpu, w, h, qp=30)
+    b, _ = _pair(gpu, w, h, qp=30, depth=2)
+    srcs = [_dev(a, *synthetic_nv12(w, h, t, seed=1)) for t in range(6)]
+    ref = [a.encode(dy.data_ptr(), duv.data_ptr(), False) for dy, duv in srcs]
+    out = []
+    b.submit(srcs[0][0].data_ptr(), srcs[0][1].data_ptr(), False)
+    for t in range(1, 6):
+        b.submit(srcs[t][0].data_ptr(), srcs[t][1].data_ptr(), False)
+        out.append(b.collect())
+    out.append(b.collect())
+    assert out == ref
