@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
-from ..pipeline.stream import EncodedFrame, StreamPipeline
+from ..pipeline.stream import EncodedFrame, StreamPipeline, cpu_encoder_class
 
 log = logging.getLogger("mxdesk.wall")
 
@@ -198,15 +198,14 @@ class WallPipeline(StreamPipeline):
         ec.bitrate_kbps = self._enc_args["bitrate_kbps"]
         ec.search_range = self._enc_args["search_range"]
         ec.subpel = 1 if self._enc_args["subpel"] else 0
-        hevc = self.codec == "hevc"
         if self.dev.type == "cuda":
-            cls = N.GpuHevcEncoder if hevc else N.GpuH264Encoder
+            cls = {"h264": N.GpuH264Encoder, "hevc": N.GpuHevcEncoder, "vp8": N.GpuVp8Encoder}[self.codec]
             self.enc = cls(ec, torch.cuda.current_stream(self.dev).cuda_stream)
             pitch = self.enc.pitch
         else:
             ec.search_range = min(ec.search_range, 4)
             ec.subpel = 0
-            self.enc = (N.CpuHevcEncoder if hevc else N.CpuH264Encoder)(ec)
+            self.enc = cpu_encoder_class(N, self.codec)(ec)
             pitch = cw
         self.wy = torch.zeros((ch, pitch), dtype=torch.uint8, device=self.dev)
         self.wuv = torch.zeros((ch // 2, pitch), dtype=torch.uint8, device=self.dev)

@@ -40,7 +40,7 @@ class EncodedFrame:
     width: int
     height: int
     gpu_ms: float = 0.0
-    codec_id: int = 1  # media header codec byte: 1 = H.264, 2 = HEVC
+    codec_id: int = 1  # media header codec byte: 1 = H.264, 2 = HEVC, 3 = VP8
 
 
 def hevc_codec_string(width: int, height: int, fps: int) -> str:
@@ -50,8 +50,18 @@ def hevc_codec_string(width: int, height: int, fps: int) -> str:
     return f"hvc1.1.6.L{native().hevc_level(width, height, fps)}.B0"
 
 
+CODEC_IDS = {"h264": 1, "hevc": 2, "vp8": 3}
+
+
 def codec_string(codec: str, width: int, height: int, fps: int) -> str:
+    if codec == "vp8":
+        return "vp8"  # WebCodecs codec string of VP8
     return hevc_codec_string(width, height, fps) if codec == "hevc" else h264_codec_string(width, height, fps)
+
+
+def cpu_encoder_class(N, codec: str):
+    """The serial CPU encoder of a codec (no-GPU plumbing backend, CPU wall tiles)."""
+    return {"h264": N.CpuH264Encoder, "hevc": N.CpuHevcEncoder, "vp8": N.CpuVp8Encoder}[codec]
 
 
 def h264_codec_string(width: int, height: int, fps: int) -> str:
@@ -97,10 +107,10 @@ class StreamPipeline:
                  noise: bool = True, out_width: int = 0, out_height: int = 0, session_name: str = "0",
                  capture: Any = None, metrics: SessionMetrics | None = None, queue_frames: int = 8,
                  stall_s: float = 2.0, paced: bool = True, codec: str = "h264"):
-        if codec not in ("h264", "hevc"):
-            raise ValueError(f"unknown codec {codec!r} (h264 | hevc)")
+        if codec not in CODEC_IDS:
+            raise ValueError(f"unknown codec {codec!r} (h264 | hevc | vp8)")
         self.codec = codec
-        self.codec_id = 2 if codec == "hevc" else 1
+        self.codec_id = CODEC_IDS[codec]
         self.width, self.height, self.fps = width, height, fps
         self.out_w = out_width or width
         self.out_h = out_height or height
@@ -170,7 +180,7 @@ class StreamPipeline:
             ec.keyint = a["keyint"]
             ec.search_range = min(a["search_range"], 4)  # keep the serial encoder real-time
             ec.subpel = 0
-            self._cpu = N.CpuHevcEncoder(ec) if self.codec == "hevc" else N.CpuH264Encoder(ec)
+            self._cpu = cpu_encoder_class(N, self.codec)(ec)
             self._desk = CpuSyntheticDesktop(self.width, self.height, a["noise"])
             self._sess = None
             self._cpu_frame = 0

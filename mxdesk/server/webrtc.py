@@ -124,6 +124,26 @@ def pick_h265(md: MediaDesc) -> str | None:
     return None
 
 
+def pick_vp8(md: MediaDesc) -> str | None:
+    """Payload type of the offer's VP8 (RFC 7741) codec."""
+    return next((r.split()[0] for r in md.attrs_named("rtpmap") if re.search(r"\sVP8/90000", r, re.I)), None)
+
+
+_PICKERS = {"h264": pick_h264, "hevc": pick_h265, "vp8": pick_vp8}
+_MISSING = {"h264": "offer has no H.264 (packetization-mode=1, baseline-compatible) video section",
+            "hevc": "offer has no H.265 (Main profile) video section",
+            "vp8": "offer has no VP8 video section"}
+
+
+def codec_sdp(codec: str, level_idc: int) -> tuple[str, str]:
+    """(rtpmap, fmtp) of the stream's codec; an empty fmtp means no a=fmtp line (VP8)."""
+    if codec == "hevc":
+        return "H265/90000", f"profile-id=1;tier-flag=0;level-id={level_idc};tx-mode=SRST"
+    if codec == "vp8":
+        return "VP8/90000", ""
+    return "H264/90000", f"level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}"
+
+
 @dataclass
 class Answer:
     sdp: str
@@ -146,17 +166,13 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
                  level_idc: int = 0x2A, audio_ssrc: int | None = None, extra_hosts: list[str] | None = None,
                  codec: str = "h264", datachannel: bool = True, max_message: int = 262144,
                  relay_candidates: list[str] | None = None) -> Answer:
-    """Answer one video section in the stream's codec (H.264 packetization-mode 1, or H.265
-    with ``codec="hevc"``; ``level_idc`` is then general_level_idc) and, with ``audio_ssrc``,
+    """Answer one video section in the stream's codec (H.264 packetization-mode 1, H.265 with
+    ``codec="hevc"`` -- ``level_idc`` is then general_level_idc -- or VP8) and, with ``audio_ssrc``,
     one PCMU audio section, and with ``datachannel`` one ``UDP/DTLS/SCTP webrtc-datachannel``
     section (RFC 8841); everything else is rejected with port 0.  All accepted sections are
     BUNDLEd onto the single ICE-lite host candidate."""
-    pick = pick_h265 if codec == "hevc" else pick_h264
-    if codec == "hevc":
-        rtpmap, fmtp = "H265/90000", f"profile-id=1;tier-flag=0;level-id={level_idc};tx-mode=SRST"
-    else:
-        rtpmap = "H264/90000"
-        fmtp = f"level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}"
+    pick = _PICKERS[codec]
+    rtpmap, fmtp = codec_sdp(codec, level_idc)
     offer = parse_sdp(offer_text)
     lines = ["v=0", f"o=mxdesk {secrets.randbelow(1 << 62)} 2 IN IP4 {host}", "s=mxdesk", "t=0 0", "a=ice-lite",
              "a=msid-semantic: WMS mxdesk"]
@@ -182,7 +198,8 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
             out_media += [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport,
                           f"a=mid:{mid}", "a=sendonly", "a=rtcp-mux", "a=rtcp-rsize",
                           f"a=rtpmap:{pt} {rtpmap}", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
-                          f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb", f"a=fmtp:{pt} {fmtp}",
+                          f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb",
+                          *([f"a=fmtp:{pt} {fmtp}"] if fmtp else []),
                           f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
             continue
         if md.kind == "audio" and audio is None and audio_ssrc is not None and _has_pcmu(md):
@@ -203,8 +220,7 @@ def build_answer(offer_text: str, ice_ufrag: str, ice_pwd: str, fingerprint: str
         out_media += [f"m={md.kind} 0 {md.proto} {md.fmts[0] if md.fmts else '0'}", "c=IN IP4 0.0.0.0",
                       f"a=mid:{mid}", "a=inactive"]
     if chosen is None:
-        raise ValueError("offer has no H.265 (Main profile) video section" if codec == "hevc" else
-                         "offer has no H.264 (packetization-mode=1, baseline-compatible) video section")
+        raise ValueError(_MISSING[codec])
     if audio is not None:
         chosen.audio_pt, chosen.audio_mid = audio
     if dc is not None:
@@ -222,11 +238,7 @@ def build_offer(ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port:
     (upstream webrtcbin): one sendonly video section in the stream's codec, optionally one
     PCMU audio section and one SCTP data-channel section, all BUNDLEd on the ICE-lite host
     candidate(s), DTLS ``actpass`` (browsers answer ``active``: we stay the DTLS server)."""
-    if codec == "hevc":
-        rtpmap, fmtp = "H265/90000", f"profile-id=1;tier-flag=0;level-id={level_idc};tx-mode=SRST"
-    else:
-        rtpmap = "H264/90000"
-        fmtp = f"level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e0{level_idc:02x}"
+    rtpmap, fmtp = codec_sdp(codec, level_idc)
     hosts = [host] + [h for h in (extra_hosts or []) if h != host]
     cands = [f"a=candidate:{k + 1} 1 udp {2130706431 - k} {h} {port} typ host" for k, h in enumerate(hosts)]
     cands += list(relay_candidates or [])
@@ -236,7 +248,7 @@ def build_offer(ice_ufrag: str, ice_pwd: str, fingerprint: str, host: str, port:
     mids = ["0"]
     media = [f"m=video {port} UDP/TLS/RTP/SAVPF {pt}", *transport, "a=mid:0", "a=sendonly", "a=rtcp-mux",
              "a=rtcp-rsize", f"a=rtpmap:{pt} {rtpmap}", f"a=rtcp-fb:{pt} nack", f"a=rtcp-fb:{pt} nack pli",
-             f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb", f"a=fmtp:{pt} {fmtp}",
+             f"a=rtcp-fb:{pt} ccm fir", f"a=rtcp-fb:{pt} goog-remb", *([f"a=fmtp:{pt} {fmtp}"] if fmtp else []),
              f"a=ssrc:{ssrc} cname:mxdesk", f"a=ssrc:{ssrc} msid:mxdesk video0"]
     if audio_ssrc is not None:
         mids.append(str(len(mids)))
@@ -436,8 +448,12 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         return codec, level
 
     def _media_ready(self, codec: str) -> None:
-        packetizer = _native().net.RtpH265Packetizer if codec == "hevc" else _native().net.RtpH264Packetizer
-        self.pkt = packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
+        net = _native().net
+        if codec == "vp8":
+            self.pkt = net.RtpVp8Packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16), secrets.randbits(15))
+        else:
+            packetizer = net.RtpH265Packetizer if codec == "hevc" else net.RtpH264Packetizer
+            self.pkt = packetizer(self.ssrc, self.answer.pt, 1150, secrets.randbits(16))
         self.tasks.append(asyncio.create_task(self._timers()))
 
     async def start(self) -> str:

@@ -258,7 +258,11 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
         last_tick = time.monotonic()
         my_ssrc = secrets.randbits(32)
         hevc = " H265/90000" in res.answer
-        depk = R.H265Depacketizer() if hevc else R.H264Depacketizer()
+        vp8 = " VP8/90000" in res.answer
+
+        def new_depk():
+            return R.Vp8Depacketizer() if vp8 else (R.H265Depacketizer() if hevc else R.H264Depacketizer())
+        depk = new_depk()
         pending: dict[int, bytes] = {}
         next_seq = None
         n_pkts = 0
@@ -276,6 +280,8 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
             return (a - b) & 0xFFFF
 
         def is_idr(au: bytes) -> bool:
+            if vp8:  # frame tag bit 0: 0 = key frame
+                return len(au) > 0 and not au[0] & 1
             for n in N.net.split_annexb(au):
                 t = (n[0] >> 1) & 0x3F if hevc else n[0] & 0x1F
                 if (16 <= t <= 21) if hevc else t == 5:
@@ -317,7 +323,7 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                 res.gave_up += 1
                 tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
                 next_seq = min(pending, key=lambda q: dist(q, next_seq))
-                depk = R.H265Depacketizer() if hevc else R.H264Depacketizer()
+                depk = new_depk()
                 await_idr = True
                 gap_since = None
                 deliver()

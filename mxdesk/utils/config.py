@@ -50,12 +50,17 @@ ENCODER_ALIASES = {
     "mxh265enc": "mxh265enc",
     "x265enc": "cpuh265enc",
     "cpuh265enc": "cpuh265enc",
+    # the reference's libvpx choice (README.md:21,35) -> the HIP VP8 encoder
+    "vp8enc": "mxvp8enc",
+    "vaapivp8enc": "mxvp8enc",
+    "mxvp8enc": "mxvp8enc",
+    "cpuvp8enc": "cpuvp8enc",
 }
-GPU_ENCODERS = {"mxh264enc", "mxh265enc"}
+GPU_ENCODERS = {"mxh264enc", "mxh265enc", "mxvp8enc"}
 # selkies encoders without an mxdesk implementation: the session falls back to the GPU H.264
 # encoder (every WebRTC browser decodes H.264) with a startup warning instead of failing
-FALLBACK_ENCODERS = {"vp8enc": "mxh264enc", "vp9enc": "mxh264enc", "av1enc": "mxh264enc",
-                     "vaapivp8enc": "mxh264enc", "vaapivp9enc": "mxh264enc", "vaapiav1enc": "mxh264enc"}
+FALLBACK_ENCODERS = {"vp9enc": "mxh264enc", "av1enc": "mxh264enc", "vaapivp9enc": "mxh264enc",
+                     "vaapiav1enc": "mxh264enc"}
 
 
 @dataclass
@@ -212,8 +217,9 @@ class Config:
 
     @property
     def codec(self) -> str:
-        """Bitstream format of the selected encoder: "h264" or "hevc"."""
-        return "hevc" if "265" in self.encoder_backend else "h264"
+        """Bitstream format of the selected encoder: "h264", "hevc" or "vp8"."""
+        b = self.encoder_backend
+        return "hevc" if "265" in b else ("vp8" if "vp8" in b else "h264")
 
     @property
     def gpu_encoder(self) -> bool:

@@ -253,12 +253,22 @@ def test_json_log_format():
 
 
 def test_unimplemented_selkies_encoders_fall_back_to_h264():
-    cfg = C.load(env={"WEBRTC_ENCODER": "vp8enc"}, argv=[])
+    cfg = C.load(env={"WEBRTC_ENCODER": "vp9enc"}, argv=[])
     assert cfg.encoder_backend == "mxh264enc" and cfg.codec == "h264" and cfg.gpu_encoder
-    assert "vp8enc" in cfg.encoder_fallback
+    assert "vp9enc" in cfg.encoder_fallback
     assert C.load(env={"WEBRTC_ENCODER": "nvh264enc"}, argv=[]).encoder_fallback is None
     with pytest.raises(ValueError):
         C.load(env={"WEBRTC_ENCODER": "bogusenc"}, argv=[]).encoder_backend
+
+
+def test_vp8enc_selects_the_vp8_encoder():
+    # the reference's libvpx choice (README.md:21,35) is implemented: no fallback
+    for name in ("vp8enc", "vaapivp8enc", "mxvp8enc"):
+        cfg = C.load(env={"WEBRTC_ENCODER": name}, argv=[])
+        assert cfg.encoder_backend == "mxvp8enc" and cfg.codec == "vp8" and cfg.gpu_encoder
+        assert cfg.encoder_fallback is None
+    cfg = C.load(env={"WEBRTC_ENCODER": "cpuvp8enc"}, argv=[])
+    assert cfg.codec == "vp8" and not cfg.gpu_encoder
 
 
 def test_serve_wires_xtest_injector_for_x11_capture(monkeypatch):

@@ -1,6 +1,7 @@
 // Host-side ASan/UBSan driver for the native code that parses or produces untrusted /
-// variable-length data: CPU H.264 encoder (same MB core as the HIP
-// kernels), SRTP/SRTCP, DTLS-SRTP handshake, RTP H.264 packetizer, Annex-B splitter.
+// variable-length data: CPU H.264 / HEVC / VP8 encoders (same MB cores as the
+// HIP kernels), SRTP/SRTCP, DTLS-SRTP handshake, RTP H.264 / H.265 / VP8 packetizers, Annex-B
+// splitter.
 // Built by tools/sanitize.sh with -fsanitize on the host side only; no GPU is touched.
 #include <cstdio>
 #include <cstdlib>
@@ -10,9 +11,11 @@
 
 #include "../csrc/codec/h264_encoder.h"
 #include "../csrc/codec/hevc_encoder.h"
+#include "../csrc/codec/vp8_encoder.h"
 #include "../csrc/net/dtls.h"
 #include "../csrc/net/rtp_h264.h"
 #include "../csrc/net/rtp_h265.h"
+#include "../csrc/net/rtp_vp8.h"
 #include "../csrc/net/sctp.h"
 #include "../csrc/net/srtp.h"
 
@@ -79,6 +82,30 @@ static void hevc_pass(std::mt19937& rng) {
     }
 }
 
+static void vp8_pass(std::mt19937& rng) {
+    const int sizes[][2] = {{176, 144}, {100, 60}, {64, 48}, {320, 192}};
+    for (auto& s : sizes) {
+        h264::EncoderConfig c;
+        c.width = s[0];
+        c.height = s[1];
+        c.bitrate_kbps = (rng() & 1) ? 0 : 300;
+        c.qp = 4 + (int)(rng() % 46);
+        c.search_range = 8;
+        vp8::CpuVp8Encoder enc(c);
+        const int cw = enc.coded_pitch(), ch = (s[1] + 15) / 16 * 16;
+        std::vector<uint8_t> y((size_t)cw * ch), uv((size_t)cw * ch / 2);
+        for (int f = 0; f < 5; ++f) {
+            for (int r = 0; r < ch; ++r)
+                for (int x = 0; x < cw; ++x)
+                    y[(size_t)r * cw + x] = (uint8_t)(((x + 3 * f) * 3 + r * 2) ^ ((r > ch / 2) ? (rng() & 255) : 0));
+            for (auto& v : uv) v = (uint8_t)(128 + (int)(rng() % 64) - 32);
+            const auto& fr = enc.encode(y.data(), uv.data(), cw, f == 3);
+            CHECK(fr.size() > 3);
+            CHECK(((fr[0] & 1) == 0) == (f == 0 || f == 3));  // frame tag: key frames
+        }
+    }
+}
+
 static std::string rnd(std::mt19937& rng, size_t n) {
     std::string s(n, '\0');
     for (auto& ch : s) ch = (char)(rng() & 0xff);
@@ -116,6 +143,8 @@ static void rtp_pass(std::mt19937& rng) {
         for (const auto& p : pk.packetize(au, (uint32_t)rng())) CHECK(p.size() >= 12);
         net::RtpH265Packetizer pk5((uint32_t)rng(), 97, 64 + rng() % 1200, (uint16_t)rng());
         for (const auto& p : pk5.packetize(au, (uint32_t)rng())) CHECK(p.size() >= 12);
+        net::RtpVp8Packetizer pk8((uint32_t)rng(), 98, 64 + rng() % 1200, (uint16_t)rng(), (uint16_t)rng());
+        for (const auto& p : pk8.packetize(au, (uint32_t)rng())) CHECK(p.size() > 16);
         (void)net::split_annexb(au);
     }
 }
@@ -192,6 +221,7 @@ int main() {
     std::mt19937 rng(12345);
     encoder_pass(rng);
     hevc_pass(rng);
+    vp8_pass(rng);
     srtp_pass(rng);
     rtp_pass(rng);
     dtls_pass();
