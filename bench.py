@@ -119,6 +119,8 @@ def main() -> None:
     ap.add_argument("--aq", type=int, default=None,
                     help="adaptive quantisation: 0 off, 1 coarser QP for noise-like MBs, 2 + rate-distortion "
                          "residual drop for them (default: the encoder's)")
+    ap.add_argument("--deblock", type=int, default=None,
+                    help="in-loop deblocking filter 0/1 (default: the encoder's)")
     ap.add_argument("--intra-in-p", type=int, default=None,
                     help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
     ap.add_argument("--depth", type=int, default=2,
@@ -175,6 +177,8 @@ def main() -> None:
         cfg.enc.tu_split = args.tu_split
     if args.intra_in_p is not None:
         cfg.enc.intra_in_p = args.intra_in_p
+    if args.deblock is not None:
+        cfg.enc.deblock = args.deblock
     if args.aq is not None:
         cfg.enc.aq = args.aq
     if args.me_coarse is not None:
@@ -288,6 +292,7 @@ def main() -> None:
             "sessions_per_gpu": K,
             "hip_graph": bool(args.graph),
             "pipeline_depth": args.depth,
+            "deblock": int(cfg.enc.deblock),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),
             "mean_qp": round(statistics.mean(qps), 2),

@@ -458,7 +458,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         w.init(words.data());
         write_slice_header(w, make_slice_params(first, idr, common_.cur_frame_num(), common_.log2_max_frame_num(),
                                                 common_.cur_idr_pic_id(), frame_qp_() - common_.pic_init_qp(),
-                                                cfg_.deblock ? 0 : 1));
+                                                cfg_.h264_deblock() ? 0 : 1));
         int run = 0;
         int qp_pred = frame_qp_();  // mb_qp_delta predictor: QP of the last MB that carried one
         for (int mbi = first; mbi < last; ++mbi) {
@@ -525,7 +525,7 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     std::vector<uint8_t> payload;
     std::vector<uint32_t> soff, slen;
     entropy(payload, soff, slen);
-    if (cfg_.deblock) {  // in-loop filter: the next picture predicts from the filtered one
+    if (cfg_.h264_deblock()) {  // in-loop filter: the next picture predicts from the filtered one
         const Geometry g = geom_of(common_, cw_, ch_);
         std::vector<uint8_t> qpe(mb_.size());
         db_qp_eff(mb_.data(), (int)mb_.size(), g.mb_w, common_.cur_idr() ? idr_slice_rows(g.mb_h) : g.mb_h,

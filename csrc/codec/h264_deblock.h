@@ -68,16 +68,15 @@ MXHD uint32_t db_edge_bs4(const MbInfo& q, const MbInfo* nb, int e, bool vertica
 // Per-edge filter parameters: alpha, beta, tC0[bS-1] for qPav (offsets 0: indexA = indexB = qPav).
 struct DbParams {
     int alpha, beta;
-    int tc0[3];
+    uint32_t tc0;  // tC0 for bS 1, 2, 3 in bits 0..4, 5..9, 10..14 (packed: no indexed array on the GPU)
 };
+MXHD int db_tc0(const DbParams& d, int bs) { return (int)((d.tc0 >> (5 * (bs - 1))) & 31u); }
 MXHD DbParams db_params(int qpav) {
     const int ia = db_clip3(0, 51, qpav);
     DbParams d;
     d.alpha = kDbAlpha[ia];
     d.beta = kDbBeta[ia];
-    d.tc0[0] = kDbTc0[ia][0];
-    d.tc0[1] = kDbTc0[ia][1];
-    d.tc0[2] = kDbTc0[ia][2];
+    d.tc0 = (uint32_t)kDbTc0[ia][0] | ((uint32_t)kDbTc0[ia][1] << 5) | ((uint32_t)kDbTc0[ia][2] << 10);
     return d;
 }
 
@@ -89,7 +88,7 @@ MXHD void db_luma_line(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, int
     if (bs == 0 || !(db_abs(P0 - Q0) < d.alpha && db_abs(P1 - P0) < d.beta && db_abs(Q1 - Q0) < d.beta)) return;
     const bool ap = db_abs(P2 - P0) < d.beta, aq = db_abs(Q2 - Q0) < d.beta;
     if (bs < 4) {
-        const int tc0 = bs == 1 ? d.tc0[0] : (bs == 2 ? d.tc0[1] : d.tc0[2]);
+        const int tc0 = db_tc0(d, bs);
         const int tc = tc0 + (ap ? 1 : 0) + (aq ? 1 : 0);
         const int delta = db_clip3(-tc, tc, (((Q0 - P0) * 4) + (P1 - Q1) + 4) >> 3);
         p0 = clip255(P0 + delta);
@@ -120,7 +119,7 @@ MXHD void db_chroma_line(int p1, int& p0, int& q0, int q1, int bs, const DbParam
     const int P0 = p0, Q0 = q0;
     if (bs == 0 || !(db_abs(P0 - Q0) < d.alpha && db_abs(p1 - P0) < d.beta && db_abs(q1 - Q0) < d.beta)) return;
     if (bs < 4) {
-        const int tc = (bs == 1 ? d.tc0[0] : (bs == 2 ? d.tc0[1] : d.tc0[2])) + 1;
+        const int tc = db_tc0(d, bs) + 1;
         const int delta = db_clip3(-tc, tc, (((Q0 - P0) * 4) + (p1 - q1) + 4) >> 3);
         p0 = clip255(P0 + delta);
         q0 = clip255(Q0 - delta);

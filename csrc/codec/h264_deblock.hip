@@ -36,6 +36,8 @@ namespace {
 
 constexpr int kDbRows = 8;   // MB rows (waves per plane) per workgroup
 constexpr int kDbRing = 16;  // LDS hand-off slots per row
+constexpr int kDbMaxW = 512; // MBs per row (the encoder's limit): the band's records live in LDS
+constexpr int kDbPf = 8;     // macroblocks of sample lines prefetched ahead (one batch)
 constexpr unsigned kDbSpinLimit = 1u << 22;
 // global-memory words shared between workgroups: address-space-1 (global_*, never flat_*) atomics
 typedef __attribute__((address_space(1))) uint64_t gu64;
@@ -91,7 +93,24 @@ struct DbShared {
     int prog[2][kDbRows];                    // ring entries published (MB count)
     int cons[2][kDbRows];                    // MB steps finished by the row (for the row above's ring reuse)
     uint8_t tile[2 * kDbRows][20][16];       // per-wave transposition tile
+    uint4 recs[kDbRows + 1][kDbMaxW];        // the band's records + the next row's (bS, QP)
+    uint4 stage[2 * kDbRows][kDbPf][16];     // per-wave prefetched sample lines (lane-private slots)
+    uint32_t params[52];                     // alpha | beta << 8 | packed tC0 << 13, by indexA
+    uint8_t cqp[52];                         // QP_C of a clipped qP_I (Table 8-15)
 };
+__device__ __forceinline__ int lds_cqp(const DbShared& S, int qp, int offset) {
+    const int q = qp + offset;
+    return S.cqp[q < 0 ? 0 : (q > 51 ? 51 : q)];
+}
+__device__ __forceinline__ DbParams lds_params(const DbShared& S, int qpav) {
+    const uint32_t w = S.params[qpav < 0 ? 0 : (qpav > 51 ? 51 : qpav)];
+    DbParams d;
+    d.alpha = (int)(w & 0xff);
+    d.beta = (int)((w >> 8) & 31);
+    d.tc0 = w >> 13;
+    return d;
+}
+
 
 __device__ __forceinline__ void lds_sync_wave() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -99,12 +118,33 @@ __device__ __forceinline__ void lds_sync_wave() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// LDS-only ordering: the ring hand-off never passes global data between waves of a workgroup, so
+// the progress words need no global-memory drain (a workgroup-scope release waits vmcnt(0) every
+// step, draining the prefetched lines and the pixel stores).
+// LDS operations of a wave execute in order, so the producer only drains its own LDS writes
+// (lgkmcnt) before the progress word and the consumer needs a compiler barrier after reading it.
 __device__ __forceinline__ int lds_load(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    return v;
 }
 // publish an LDS progress value: the ring bytes written before it are visible to the reader
 __device__ __forceinline__ void lds_store(int* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// 16-byte global load / store through address-space-1 pointers of a native vector type (a generic
+// access -- or one through HIP's uint4 class, whose copy constructor takes a generic reference --
+// compiles to flat_*, which also counts on lgkmcnt and so stalls every later LDS wait)
+typedef unsigned DbV4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) DbV4 GDbV4;
+__device__ __forceinline__ uint4 gld16(const uint8_t* p) {
+    const DbV4 v = *(const GDbV4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gst16(uint8_t* p, const uint4& v) {
+    const DbV4 d = {v.x, v.y, v.z, v.w};
+    *(GDbV4*)p = d;
 }
 
 // bounded spin until *p >= need (LDS, same workgroup); false on timeout
@@ -185,15 +225,30 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
     bool prev_mod = false;      // MB x-1 was modified (its own edges)
     int seen_above = 0;         // band-first rows: progress of the row above already observed
     for (int k = 0; k < 16; ++k) P[k] = 0;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (act) nxt = *reinterpret_cast<const uint4*>(Y + (size_t)(mby * 16 + lane) * pitch);
+    // sample lines: batches of kDbPf macroblocks loaded one batch ahead into registers and parked in
+    // the wave's LDS stage when their batch starts, so a load's latency spans kDbPf steps
+    uint4 pf[kDbPf];
+    uint4(*stage)[16] = S.stage[band_row];
+    const uint8_t* line = Y + (size_t)(mby * 16 + (act ? lane : 0)) * pitch;
+    auto issue = [&](int xb) {
+#pragma unroll
+        for (int j = 0; j < kDbPf; ++j)
+            pf[j] = (act && xb + j < mb_w) ? gld16(line + 16 * (xb + j)) : make_uint4(0, 0, 0, 0);
+    };
+    issue(0);
     for (int x = 0; x <= mb_w; ++x) {
         const bool have = x < mb_w;
+        if (x % kDbPf == 0) {
+            if (act) {
+#pragma unroll
+                for (int j = 0; j < kDbPf; ++j) stage[j][lane] = pf[j];
+            }
+            issue(x + kDbPf);
+        }
         uint4 r = make_uint4(0, 0, 0, 0);
         if (have) {
-            unpack16(nxt, C);
-            r = rec[mby * mb_w + x];
-            if (x + 1 < mb_w && act) nxt = *reinterpret_cast<const uint4*>(Y + (size_t)(mby * 16 + lane) * pitch + 16 * (x + 1));
+            if (act) unpack16(stage[x % kDbPf][lane], C);
+            r = S.recs[band_row][x];
         }
         if (have && (r.w >> 30) & 1) qrun = (r.w >> 24) & 63;
         const int qp = qrun;
@@ -205,7 +260,7 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                 if (!b4) continue;
                 vmod = true;
                 const int bs = (b4 >> (3 * (lane >> 2))) & 7;
-                const DbParams d = db_params(((e == 0 ? qprev : qp) + qp + 1) >> 1);
+                const DbParams d = lds_params(S, ((e == 0 ? qprev : qp) + qp + 1) >> 1);
                 if (e == 0) {
                     v0 = true;
                     if (act) db_luma_line(P[12], P[13], P[14], P[15], C[0], C[1], C[2], C[3], bs, d);
@@ -221,9 +276,9 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
         // ---- MB x-1 is final (except rows 13..15 when the row below filters its top edge there)
         if (x > 0) {
             const int xp = x - 1;
-            const bool below_top = !pic_last && rec_edge(rec[(mby + 1) * mb_w + xp], 1, 0) != 0;
+            const bool below_top = !pic_last && rec_edge(S.recs[band_row + 1][xp], 1, 0) != 0;
             if ((prev_mod || v0) && act && (lane <= 12 || !below_top))
-                *reinterpret_cast<uint4*>(Y + (size_t)(mby * 16 + lane) * pitch + 16 * xp) = pack16(P);
+                gst16(Y + (size_t)(mby * 16 + lane) * pitch + 16 * xp, pack16(P));
             if (below_top) {
                 if (!band_last) {
                     const int slot = xp % kDbRing;
@@ -294,7 +349,7 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                 const uint32_t b4 = rec_edge(r, 1, e);
                 if (!b4) continue;
                 const int bs = (b4 >> (3 * (lane >> 2))) & 7;
-                const DbParams d = db_params(((e == 0 ? qtop : qp) + qp + 1) >> 1);
+                const DbParams d = lds_params(S, ((e == 0 ? qtop : qp) + qp + 1) >> 1);
                 if (!act) continue;
                 if (e == 0)
                     db_luma_line(col[0], col[1], col[2], col[3], col[4], col[5], col[6], col[7], bs, d);
@@ -313,8 +368,7 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
             if (act) unpack16(*reinterpret_cast<const uint4*>(tile[4 + lane]), C);
             // the upper neighbour's rows 13..15: this row is their writer when it filters its top edge
             if (t0 && lane >= 1 && lane < 4)
-                *reinterpret_cast<uint4*>(Y + (size_t)(mby * 16 - 4 + lane) * pitch + 16 * x) =
-                    *reinterpret_cast<const uint4*>(tile[lane]);
+                gst16(Y + (size_t)(mby * 16 - 4 + lane) * pitch + 16 * x, *reinterpret_cast<const uint4*>(tile[lane]));
         }
         // step done: the row above may reuse the ring slot of MB x
         if (!band_first && lane == 0) lds_store(cons_me, x + 1);
@@ -348,8 +402,7 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
     bool prev_mod = false;
     int seen_above = 0;
     for (int k = 0; k < 8; ++k) P[k] = 0;
-    auto load_line = [&](int x, int* o) {
-        const uint4 v = *reinterpret_cast<const uint4*>(UV + (size_t)(mby * 8 + ln) * pitch + 16 * x);
+    auto load_line = [&](const uint4& v, int* o) {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = (w[k >> 1] >> (16 * (k & 1) + 8 * comp)) & 0xff;
@@ -359,12 +412,28 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
 #pragma unroll
         for (int k = 0; k < 8; ++k) tile[row][2 * k + comp] = (uint8_t)o[k];
     };
+    uint4 pf[kDbPf];
+    uint4(*stage)[16] = S.stage[kDbRows + band_row];
+    const uint8_t* line = UV + (size_t)(mby * 8 + ln) * pitch;
+    auto issue = [&](int xb) {
+#pragma unroll
+        for (int j = 0; j < kDbPf; ++j)
+            pf[j] = (act && xb + j < mb_w) ? gld16(line + 16 * (xb + j)) : make_uint4(0, 0, 0, 0);
+    };
+    issue(0);
     for (int x = 0; x <= mb_w; ++x) {
         const bool have = x < mb_w;
+        if (x % kDbPf == 0) {
+            if (act) {
+#pragma unroll
+                for (int j = 0; j < kDbPf; ++j) stage[j][lane] = pf[j];
+            }
+            issue(x + kDbPf);
+        }
         uint4 r = make_uint4(0, 0, 0, 0);
         if (have) {
-            if (act) load_line(x, C);
-            r = rec[mby * mb_w + x];
+            if (act) load_line(stage[x % kDbPf][lane], C);
+            r = S.recs[band_row][x];
         }
         if (have && (r.w >> 30) & 1) qrun = (r.w >> 24) & 63;
         const int qp = qrun;
@@ -375,8 +444,8 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                 if (!b4) continue;
                 vmod = true;
                 const int bs = (b4 >> (3 * (ln >> 1))) & 7;
-                const DbParams d = db_params(
-                    (chroma_qp(ce == 0 ? qprev : qp, cqo) + chroma_qp(qp, cqo) + 1) >> 1);
+                const DbParams d = lds_params(S, 
+                    (lds_cqp(S, ce == 0 ? qprev : qp, cqo) + lds_cqp(S, qp, cqo) + 1) >> 1);
                 if (ce == 0) {
                     v0 = true;
                     if (act) db_chroma_line(P[6], P[7], C[0], C[1], bs, d);
@@ -387,14 +456,13 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
         }
         if (x > 0) {
             const int xp = x - 1;
-            const bool below_top = !pic_last && rec_edge(rec[(mby + 1) * mb_w + xp], 1, 0) != 0;
+            const bool below_top = !pic_last && rec_edge(S.recs[band_row + 1][xp], 1, 0) != 0;
             if (prev_mod || v0 || below_top) {
                 // MB x-1's rows through the tile (the two components interleave)
                 if (act) to_tile(2 + ln, P);
                 lds_sync_wave();
                 if ((prev_mod || v0) && lane < 8 && (lane <= 6 || !below_top))
-                    *reinterpret_cast<uint4*>(UV + (size_t)(mby * 8 + lane) * pitch + 16 * xp) =
-                        *reinterpret_cast<const uint4*>(tile[2 + lane]);
+                    gst16(UV + (size_t)(mby * 8 + lane) * pitch + 16 * xp, *reinterpret_cast<const uint4*>(tile[2 + lane]));
                 if (below_top) {
                     if (!band_last) {
                         const int slot = xp % kDbRing;
@@ -466,8 +534,8 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                 const uint32_t b4 = rec_edge(r, 1, 2 * ce);
                 if (!b4) continue;
                 const int bs = (b4 >> (3 * (ln >> 1))) & 7;
-                const DbParams d = db_params(
-                    (chroma_qp(ce == 0 ? qtop : qp, cqo) + chroma_qp(qp, cqo) + 1) >> 1);
+                const DbParams d = lds_params(S, 
+                    (lds_cqp(S, ce == 0 ? qtop : qp, cqo) + lds_cqp(S, qp, cqo) + 1) >> 1);
                 if (!act) continue;
                 if (ce == 0)
                     db_chroma_line(col[0], col[1], col[2], col[3], bs, d);
@@ -484,8 +552,7 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                 for (int k = 0; k < 8; ++k) C[k] = tile[2 + ln][2 * k + comp];
             }
             if (t0 && lane == 1)  // the upper neighbour's row 7
-                *reinterpret_cast<uint4*>(UV + (size_t)(mby * 8 - 1) * pitch + 16 * x) =
-                    *reinterpret_cast<const uint4*>(tile[1]);
+                gst16(UV + (size_t)(mby * 8 - 1) * pitch + 16 * x, *reinterpret_cast<const uint4*>(tile[1]));
             lds_sync_wave();
         }
         if (!band_first && lane == 0) lds_store(cons_me, x + 1);
@@ -497,15 +564,29 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
     if (lane == 0) lds_store(cons_me, mb_w + 1);
 }
 
-__global__ __launch_bounds__(1024) void k_deblock(Geometry g, const FrameState* __restrict__ fs,
-                                                  const uint4* __restrict__ rec, const int* __restrict__ row_lastq,
-                                                  DbGlobal G) {
+__global__ __launch_bounds__(64 * kDbRows) void k_deblock(Geometry g, const FrameState* __restrict__ fs,
+                                                          const uint4* __restrict__ rec,
+                                                          const int* __restrict__ row_lastq, DbGlobal G) {
+    // one workgroup per (band, plane): 8 waves of 512 threads leave each wave 256 VGPRs for the
+    // line registers and the prefetch batch
     __shared__ DbShared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int band_row = wave % kDbRows, plane = wave / kDbRows;
+    const int band_row = wave, plane = blockIdx.y;
     if (threadIdx.x < 2 * kDbRows) {
         S.prog[threadIdx.x / kDbRows][threadIdx.x % kDbRows] = 0;
         S.cons[threadIdx.x / kDbRows][threadIdx.x % kDbRows] = 0;
+    }
+    if (threadIdx.x < 52) {
+        const DbParams d = db_params((int)threadIdx.x);
+        S.params[threadIdx.x] = (uint32_t)d.alpha | ((uint32_t)d.beta << 8) | (d.tc0 << 13);
+        S.cqp[threadIdx.x] = (uint8_t)chroma_qp((int)threadIdx.x, 0);
+    }
+    {  // the band's records and the next row's (their top-edge bS decides who writes rows 13..15)
+        const int r0 = blockIdx.x * kDbRows, nrow = min(kDbRows + 1, g.mb_h - r0);
+        for (int i = threadIdx.x; i < nrow * g.mb_w; i += blockDim.x) {
+            const int rr = i / g.mb_w, xx = i - rr * g.mb_w;
+            S.recs[rr][xx] = rec[(size_t)(r0 + rr) * g.mb_w + xx];
+        }
     }
     __syncthreads();
     const int mby = blockIdx.x * kDbRows + band_row;
@@ -568,10 +649,10 @@ __global__ __launch_bounds__(256) void k_db_sse(Geometry g, const FrameState* __
 
 void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream) {
-    if (g.mb_w > 4095 || g.mb_h > kMaxSlices) throw std::invalid_argument("launch_deblock: picture too large");
+    if (g.mb_w > kDbMaxW || g.mb_h > kMaxSlices) throw std::invalid_argument("launch_deblock: picture too large");
     hipLaunchKernelGGL(k_db_prep, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, b.mb, b.db_rec, b.db_rowq);
     DbGlobal G{b.db_glb, b.db_glq, b.db_gprog, b.db_err};
-    hipLaunchKernelGGL(k_deblock, dim3((g.mb_h + kDbRows - 1) / kDbRows), dim3(64 * 2 * kDbRows), 0, stream, g, b.fs,
+    hipLaunchKernelGGL(k_deblock, dim3((g.mb_h + kDbRows - 1) / kDbRows, 2), dim3(64 * kDbRows), 0, stream, g, b.fs,
                        b.db_rec, b.db_rowq, G);
     hipLaunchKernelGGL(k_db_sse, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, src_y, src_uv);
 }

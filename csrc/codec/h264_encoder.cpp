@@ -371,7 +371,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
         es = stream_e_;
     }
     hipEvent_t sse_ready = nullptr;
-    if (cfg_.deblock) {  // in-loop filter on the analysis stream: the next frame predicts from it,
+    if (cfg_.h264_deblock()) {  // in-loop filter on the analysis stream: the next frame predicts from it,
                          // while this frame's CAVLC runs beside it on the entropy stream
         launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
         if (stream_e_) {
@@ -399,7 +399,7 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.me_coarse = cfg_.me_coarse;
     f.intra4x4 = cfg_.intra4x4;
     f.subpel = cfg_.subpel;
-    f.deblock_off = cfg_.deblock ? 0 : 1;
+    f.deblock_off = cfg_.h264_deblock() ? 0 : 1;
     if (++db_epoch_ > 0xfffffu) db_epoch_ = 1;  // 20-bit tag, never 0
     f.db_epoch = (int32_t)db_epoch_;
     f.pic_init_qp = common_.pic_init_qp();

@@ -42,7 +42,12 @@ struct EncoderConfig {
                               // noise-like residuals, 2 adds their rate-distortion residual drop, 3 (H.264
                               // default) temporal classes of the source -- persistent content finer, changing
                               // content coarser (h264_mb.h temporal_class; HEVC treats 3 as 2)
-    int deblock = 1;          // in-loop deblocking filter (H.264 8.7: k_deblock; HEVC 8.7.2)
+    // in-loop deblocking filter: 1 on, 0 off, -1 the codec's default -- HEVC on (8.7.2, fully
+    // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it cost
+    // 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)
+    int deblock = -1;
+    bool h264_deblock() const { return deblock > 0; }
+    bool hevc_deblock() const { return deblock != 0; }
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)

@@ -240,7 +240,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.put(0, 1);  // transquant_bypass_enabled_flag
         w.put(0, 1);  // tiles_enabled_flag
         w.put(0, 1);  // entropy_coding_sync_enabled_flag
-        const bool db = c.deblock != 0;
+        const bool db = c.hevc_deblock();
         w.put(db, 1);  // pps_loop_filter_across_slices_enabled_flag (CU edges on slice borders too)
         w.put(1, 1);   // deblocking_filter_control_present_flag
         w.put(0, 1);   //   deblocking_filter_override_enabled_flag
@@ -281,7 +281,7 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
         w.ue(4);      // five_minus_max_num_merge_cand -> MaxNumMergeCand 1
     }
     w.se(qp - 26);  // slice_qp_delta
-    if (config().deblock) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
+    if (config().hevc_deblock()) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
     w.trailing();   // byte_alignment()
     std::vector<uint8_t> rbsp = std::move(w.b);
     rbsp.insert(rbsp.end(), data, data + n);
@@ -508,7 +508,7 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         analyse_inter(y, uv, pitch);
     }
     const int W = common_.ctb_w(), H = common_.ctb_h();
-    if (cfg_.deblock) {  // in-loop deblocking: all vertical CU edges, then all horizontal ones
+    if (cfg_.hevc_deblock()) {  // in-loop deblocking: all vertical CU edges, then all horizontal ones
         std::vector<uint8_t> qpy((size_t)W * H);
         for (size_t s = 0; s < slices_.size(); ++s) {
             const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;

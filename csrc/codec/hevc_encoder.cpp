@@ -121,7 +121,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.tu_split = cfg_.tu_split ? 1 : 0;
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
     // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
-    f.n_sse_parts = (idr || cfg_.deblock) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
+    f.n_sse_parts = (idr || cfg_.hevc_deblock()) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
     f.sse_part = sl.buf.sse_part;
     h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
     m.ref_y = rec_y_[ref];
@@ -182,7 +182,7 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
         h264::launch_me(geom_, sl.buf.me, src_y, stream_);
         launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
-    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.deblock != 0, src_y, src_uv, stream_);
+    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_deblock(), src_y, src_uv, stream_);
     hipStream_t es = stream_;
     if (stream_e_) {
         HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));

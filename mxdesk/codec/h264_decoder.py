@@ -916,10 +916,11 @@ class Decoder:
 
     # ------------------------------------------------------------------ inter prediction
     def _ref_padded(self):
-        if getattr(self, "_ref_id", None) != id(self.ref):
+        # keyed by the reference object itself (held, so its id cannot be reused by a new picture)
+        if getattr(self, "_ref_key", None) is not self.ref:
             P = self.PAD
             self._refp = [np.pad(pl.astype(np.int64), P, mode="edge") for pl in self.ref]
-            self._ref_id = id(self.ref)
+            self._ref_key = self.ref
         return self._refp
 
     def pred_luma_inter(self, x0, y0, w, h, mvx, mvy) -> np.ndarray:

@@ -20,6 +20,7 @@ from .test_cpu_encoder import synthetic_nv12
 def _encode(native, frames, w, h, **cfg_kw):
     cfg = native.EncoderConfig()
     cfg.width, cfg.height = w, h
+    cfg.deblock = 1  # H.264 default is off (EncoderConfig::deblock); these tests are about the filter
     for k, v in cfg_kw.items():
         setattr(cfg, k, v)
     enc = native.CpuH264Encoder(cfg)
@@ -81,4 +82,19 @@ def test_decoder_matches_filtered_reconstruction_1080p(native):
         y, uv = bgrx_to_nv12(desk.render(t, t / 60.0, t * 16667))
         frames.append((y, uv, False))
     stream, recons = _encode(native, frames, 1920, 1080, bitrate_kbps=8000, search_range=8)
+    _check(stream, recons)
+
+
+def test_decoder_reference_cache_survives_forced_idr(native):
+    """Regression: the decoder's padded-reference cache was keyed by id() of the reference, which
+    Python reuses once a picture is freed -- after a forced IDR (unfiltered stream) a P picture was
+    predicted from a stale padded copy."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    desk = CpuSyntheticDesktop(320, 96, True)
+    frames = []
+    for t in range(8):
+        y, uv = bgrx_to_nv12(desk.render(t + 1, t / 30, 1000 * t))
+        frames.append((y, uv, t == 5))
+    stream, recons = _encode(native, frames, 320, 96, bitrate_kbps=0, search_range=4, subpel=0, deblock=0)
     _check(stream, recons)

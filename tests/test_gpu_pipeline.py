@@ -148,6 +148,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     cfg.aq = kw.get("aq", 1)
     cfg.me_coarse = kw.get("me_coarse", 1)
     cfg.intra4x4 = kw.get("intra4x4", 1)
+    cfg.deblock = kw.get("deblock", 0)
     genc = gpu.GpuH264Encoder(cfg, _stream())
     cenc = gpu.CpuH264Encoder(cfg)
     gs, cs, grec = b"", b"", []
@@ -166,12 +167,15 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
     return gs, grec
 
 
-@pytest.mark.parametrize("w,h,subpel,sr,fresh", [(64, 48, 1, 8, 0), (160, 96, 0, 16, 0), (100, 60, 1, 16, 0),
-                                                 (320, 192, 1, 32, 0), (96, 64, 1, 8, 1),
-                                                 (80, 48, 1, 8, 1), (48, 48, 0, 8, 1), (576, 64, 1, 8, 1)])
-def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr, fresh):
-    # fresh=1: new noise every frame -> adaptive quantisation (mb_qp_delta != 0) is exercised
-    stream, grec = _gpu_cpu_encode(gpu, w, h, 4, subpel=subpel, search_range=sr, fresh_noise=fresh, qp=24)
+@pytest.mark.parametrize("w,h,subpel,sr,fresh,db", [(64, 48, 1, 8, 0, 1), (160, 96, 0, 16, 0, 0),
+                                                    (100, 60, 1, 16, 0, 1), (320, 192, 1, 32, 0, 1),
+                                                    (96, 64, 1, 8, 1, 1), (80, 48, 1, 8, 1, 0),
+                                                    (48, 48, 0, 8, 1, 1), (576, 64, 1, 8, 1, 1)])
+def test_gpu_encoder_bit_exact_vs_cpu(gpu, w, h, subpel, sr, fresh, db):
+    # fresh=1: new noise every frame -> adaptive quantisation (mb_qp_delta != 0) is exercised;
+    # db=1: in-loop deblocking (k_deblock) on
+    stream, grec = _gpu_cpu_encode(gpu, w, h, 4, subpel=subpel, search_range=sr, fresh_noise=fresh, qp=24,
+                                   deblock=db)
     dec = Decoder()
     dec.decode(stream)
     for (y, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
