@@ -39,6 +39,11 @@ from ..pipeline.stream import EncodedFrame, StreamPipeline, cpu_encoder_class
 
 log = logging.getLogger("mxdesk.wall")
 
+# Followers read the control tensor on the host only every CTRL_POLL frames (to see `stop` and
+# check lockstep); in between they enqueue broadcast, render and exchange without a host sync.
+# The leader therefore stops only at a frame id that is a multiple of CTRL_POLL.
+CTRL_POLL = 8
+
 
 def parse_layout(layout: str) -> tuple[int, int]:
     c, r = layout.lower().split("x")
@@ -199,6 +204,9 @@ class WallPipeline(StreamPipeline):
         ec.search_range = self._enc_args["search_range"]
         ec.subpel = 1 if self._enc_args["subpel"] else 0
         if self.dev.type == "cuda":
+            # two frames in flight: submit(n + 1) before collect(n), so the host composites and
+            # launches frame n + 1 while the GPU still encodes (and entropy-codes) frame n
+            ec.pipeline_depth = 2
             cls = {"h264": N.GpuH264Encoder, "hevc": N.GpuHevcEncoder, "vp8": N.GpuVp8Encoder}[self.codec]
             self.enc = cls(ec, torch.cuda.current_stream(self.dev).cuda_stream)
             pitch = self.enc.pitch
@@ -207,8 +215,11 @@ class WallPipeline(StreamPipeline):
             ec.subpel = 0
             self.enc = cpu_encoder_class(N, self.codec)(ec)
             pitch = cw
-        self.wy = torch.zeros((ch, pitch), dtype=torch.uint8, device=self.dev)
-        self.wuv = torch.zeros((ch // 2, pitch), dtype=torch.uint8, device=self.dev)
+        nbuf = 2 if self.dev.type == "cuda" else 1  # the encoder may still read the previous wall frame
+        self._walls = [(torch.zeros((ch, pitch), dtype=torch.uint8, device=self.dev),
+                        torch.zeros((ch // 2, pitch), dtype=torch.uint8, device=self.dev)) for _ in range(nbuf)]
+        self.wy, self.wuv = self._walls[0]
+        self._submitted: list[tuple[int, int]] = []  # (frame id, capture us) submitted, not collected
         self._sess = None
         self._cpu = self.enc if self.dev.type != "cuda" else None
 
@@ -239,6 +250,8 @@ class WallPipeline(StreamPipeline):
             self._drain()
             from .. import native
 
+            while self._fid % CTRL_POLL:  # followers look at the control word on these frames only
+                self.xchg.wait(self.post_frame()[2])
             self._broadcast_ctrl(self._fid, True, native().now_us())
             return None
         self._drain()
@@ -249,25 +262,40 @@ class WallPipeline(StreamPipeline):
         return tiles
 
     def _drain(self) -> None:
+        while getattr(self, "_submitted", None):  # frames still in the encoder
+            self.enc.collect()
+            self._submitted.pop(0)
         if self._pending is not None:
             self.xchg.wait(self._pending[2])
             self._pending = None
 
-    def _produce(self, force_idr: bool) -> EncodedFrame:
-        from .. import native
-
+    def _composite_next(self) -> tuple[int, int]:
+        """Wait for the posted frame's tiles, composite them into the next wall buffer, post the
+        following frame's render + exchange (followers and the RCCL stream run it while this frame
+        encodes; the receive is ordered after the composite on the device -- RCCL waits on the
+        current stream -- so one tile buffer suffices)."""
         if self._pending is None:
             self._pending = self.post_frame()
         fid, t_cap, reqs = self._pending
         tiles = self.xchg.wait(reqs)
+        self.wy, self.wuv = self._walls[fid % len(self._walls)]
         composite_nv12(tiles, self.geo, self.wy, self.wuv)
-        # frame fid+1's render + exchange run (followers, RCCL stream) while frame fid encodes;
-        # the receive is ordered after the composite above on the device (RCCL waits on the
-        # current stream), so one tile buffer suffices
         self._pending = self.post_frame()
+        return fid, t_cap
+
+    def _produce(self, force_idr: bool) -> EncodedFrame:
+        from .. import native
+
         if self.dev.type == "cuda":
-            au = self.enc.encode(self.wy.data_ptr(), self.wuv.data_ptr(), force_idr)
+            while len(self._submitted) < 2:  # keep two frames in the encoder
+                fid, t_cap = self._composite_next()
+                self.enc.submit(self.wy.data_ptr(), self.wuv.data_ptr(), force_idr)
+                self._submitted.append((fid, t_cap))
+                force_idr = False
+            au = self.enc.collect()
+            fid, t_cap = self._submitted.pop(0)
         else:
+            fid, t_cap = self._composite_next()
             au = self.enc.encode(self.wy.numpy()[: self.geo.height], self.wuv.numpy()[: self.geo.height // 2],
                                  force_idr)
         st = self.enc.stats
@@ -323,19 +351,25 @@ class TilePipeline(WallPipeline):
 
 def follower_loop(geo: WallGeometry, rank: int, world: int, device: torch.device, exchange: str = "gather",
                   fps: int = 60) -> int:
-    """Ranks != 0: render + send tiles in lockstep until rank 0 broadcasts stop (the host reads
-    the control tensor once per frame: the follower has nothing to overlap with)."""
+    """Ranks != 0: render + send tiles in lockstep until rank 0 broadcasts stop.  The frame id
+    advances by one per lockstep frame on every rank, so a follower renders from its own counter
+    and reads the control tensor on the host only every CTRL_POLL frames (stop + a lockstep
+    check); the frames between are enqueued without a host sync.  The capture timestamp only
+    feeds the barcode, which lies in rank 0's tile."""
     renderer = TileRenderer(geo, rank, device)
     xchg = TileExchange(geo, rank, world, device, exchange)
     ctrl = torch.zeros(4, dtype=torch.int64, device="cpu" if host_staged(device) else device)
-    n = 0
+    fid = 0
     while True:
         dist.broadcast(ctrl, 0)
-        fid, _, stop, t_cap = (int(x) for x in ctrl.tolist())
-        if stop:
-            return n
-        xchg.exchange(renderer.render(fid, fid / fps, t_cap))
-        n += 1
+        if fid % CTRL_POLL == 0:
+            lfid, _, stop, _ = (int(x) for x in ctrl.tolist())
+            if stop:
+                return fid
+            if lfid != fid:
+                raise RuntimeError(f"wall: rank {rank} out of lockstep (frame {fid}, leader {lfid})")
+        xchg.exchange(renderer.render(fid, fid / fps, 0))
+        fid += 1
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int, torch.device]:

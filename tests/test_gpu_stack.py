@@ -237,7 +237,8 @@ def _gpu_wall_worker(rank, world, port, q):
         pipe = WallPipeline(geo, 60, 0, world, dev, "gather", bitrate_kbps=0)
         stream = b"".join(pipe.step().au for _ in range(3))
         torch.cuda.synchronize()
-        wall_y = pipe.wy.cpu().numpy()[: geo.height, : geo.width].copy()
+        # two frames in flight on the encode rank: frame 2's composite is in wall buffer 2 % 2
+        wall_y = pipe._walls[2 % len(pipe._walls)][0].cpu().numpy()[: geo.height, : geo.width].copy()
         pipe.lockstep_frame(False, stop=True)
         q.put((stream, wall_y))
     finally:
