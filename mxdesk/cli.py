@@ -46,12 +46,12 @@ def _setup_logging(cfg: C.Config) -> None:
         logging.basicConfig(level=level, format="%(asctime)s %(name)s %(levelname)s %(message)s")
 
 
-def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0"):
+def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0", capture_allowed: bool = True):
     from .pipeline.stream import StreamPipeline
 
     backend = "gpu" if cfg.gpu_encoder else "cpu"
     capture = None
-    if cfg.source == "x11" or (cfg.source == "auto" and _x_available(cfg.display)):
+    if capture_allowed and (cfg.source == "x11" or (cfg.source == "auto" and _x_available(cfg.display))):
         from .models.x11 import X11Capture
 
         capture = X11Capture(cfg.display, cfg.sizew, cfg.sizeh)
@@ -97,9 +97,45 @@ def _clipboard_in(cfg: C.Config) -> bool:
     return C.clipboard_directions(getattr(cfg, "enable_clipboard", "true"))[0]
 
 
+def session_config(cfg: C.Config, i: int) -> C.Config:
+    """Session i of a multi-session process: its own HTTP port and (if fixed) WebRTC UDP port;
+    the process-wide singletons -- gamepad sockets, desktop audio capture -- stay with session 0."""
+    c = C.Config(values=dict(cfg.values), sources=dict(cfg.sources))
+    c.values["port"] = cfg.port + i
+    if cfg.webrtc_udp_port:
+        c.values["webrtc_udp_port"] = cfg.webrtc_udp_port + i
+    if i > 0:
+        c.values["enable_gamepad"] = False
+        c.values["enable_audio"] = False
+    return c
+
+
+def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
+    """`mxdesk serve --sessions K`: K independent sessions from one process on one GPU (VERDICT r2
+    #6) -- each a StreamPipeline with its own HIP stream and encode thread and its own
+    MediaServer on port + i, all on one event loop.  Synthetic desktops: an X display is one
+    desktop, so only K == 1 captures it."""
+    from .server.app import MediaServer, run_forever_multi, ssl_context
+
+    if cfg.source == "x11":
+        raise SystemExit("serve --sessions K > 1 streams synthetic desktops; MXDESK_SOURCE=x11 serves one")
+    device = _gpu_index(cfg) if cfg.gpu_encoder else 0
+    servers = []
+    for i in range(k):
+        ci = session_config(cfg, i)
+        pipe = build_pipeline(ci, device, session_name=str(i), capture_allowed=False)
+        servers.append(MediaServer(pipe, ci))
+    print(f"mxdesk: serving {k} sessions {cfg.sizew}x{cfg.sizeh}@{cfg.stream_fps} ({cfg.encoder_backend}) on "
+          f"{cfg.addr}:{cfg.port}..{cfg.port + k - 1}", flush=True)
+    run_forever_multi(servers, cfg.addr, [cfg.port + i for i in range(k)], ssl_context(cfg))
+
+
 def cmd_serve(cfg: C.Config, args) -> None:
     from .server.app import MediaServer, run_forever, ssl_context
 
+    if cfg.sessions > 1:
+        cmd_serve_sessions(cfg, cfg.sessions)
+        return
     device = _gpu_index(cfg) if cfg.gpu_encoder else 0
     pipe = build_pipeline(cfg, device)
     injector = make_injector(cfg, pipe)
@@ -173,7 +209,7 @@ def main(argv: list[str] | None = None) -> None:
     elif cmd == "launch":
         from .parallel.launcher import launch_sessions
 
-        launch_sessions(cfg, base_port=args.base_port or cfg.port)
+        launch_sessions(cfg, base_port=args.base_port or cfg.port, sessions_per_gpu=max(1, cfg.sessions))
     elif cmd == "wall":
         from .parallel.wall import wall_main
 

@@ -17,18 +17,21 @@ from ..utils.supervisor import Program, Ready, Supervisor
 
 def session_programs(n_gpus: int, base_port: int = 8080, extra_args: list[str] | None = None,
                      sessions_per_gpu: int = 1, python: str = sys.executable) -> list[Program]:
+    """One `mxdesk serve` process per GPU; with sessions_per_gpu K > 1 that process serves K
+    sessions (`--sessions K`, ports base + K*gpu ..), so a node is not capped by a per-GPU
+    process limit and the sessions share one HIP context."""
     progs = []
-    k = 0
+    k = max(1, sessions_per_gpu)
     for gpu in range(n_gpus):
-        for s in range(sessions_per_gpu):
-            port = base_port + k
-            env = {"HIP_VISIBLE_DEVICES": str(gpu), "MXDESK_GPU": "0", "SELKIES_PORT": str(port),
-                   "MXDESK_SESSION": str(k)}
-            progs.append(Program(name=f"session{k}-gpu{gpu}", command=[python, "-m", "mxdesk", "serve",
-                                                                       "--port", str(port), *(extra_args or [])],
-                                 priority=10 + k, environment=env, ready=Ready("tcp", f"127.0.0.1:{port}", 120.0),
-                                 wait_ready=False, startsecs=2.0, startretries=5))
-            k += 1
+        port = base_port + k * gpu
+        env = {"HIP_VISIBLE_DEVICES": str(gpu), "MXDESK_GPU": "0", "SELKIES_PORT": str(port),
+               "MXDESK_SESSION": str(gpu)}
+        cmd = [python, "-m", "mxdesk", "serve", "--port", str(port)]
+        if k > 1:
+            cmd += ["--sessions", str(k)]
+        progs.append(Program(name=f"gpu{gpu}" + (f"-x{k}" if k > 1 else ""), command=cmd + list(extra_args or []),
+                             priority=10 + gpu, environment=env, ready=Ready("tcp", f"127.0.0.1:{port}", 120.0),
+                             wait_ready=False, startsecs=2.0, startretries=5))
     return progs
 
 
@@ -38,8 +41,9 @@ def launch_sessions(cfg: Any, base_port: int = 8080, n_gpus: int | None = None, 
     if n_gpus is None:
         n_gpus = len(D.visible_gpus(D.enumerate_gpus())) or 1
     progs = session_programs(n_gpus, base_port, sessions_per_gpu=sessions_per_gpu)
-    print(f"mxdesk launch: {len(progs)} session(s) on {n_gpus} GPU(s), ports {base_port}..{base_port + len(progs) - 1}",
-          flush=True)
+    k = max(1, sessions_per_gpu)
+    print(f"mxdesk launch: {n_gpus * k} session(s) in {len(progs)} process(es) on {n_gpus} GPU(s), ports "
+          f"{base_port}..{base_port + n_gpus * k - 1}", flush=True)
     Supervisor(progs, log_dir=getattr(cfg, "log_dir", "/tmp")).run()
 
 

@@ -426,5 +426,23 @@ def run_forever(server: MediaServer, host: str, port: int, ssl_ctx: ssl.SSLConte
         pass
 
 
+def run_forever_multi(servers: list[MediaServer], host: str, ports: list[int],
+                      ssl_ctx: ssl.SSLContext | None = None) -> None:
+    """Several MediaServers (one per session) on one event loop, each on its own port."""
+    async def main():
+        runners = [await serve(s, host, p, ssl_ctx) for s, p in zip(servers, ports)]
+        try:
+            while True:
+                await asyncio.sleep(3600)
+        finally:
+            for r in runners:
+                await r.cleanup()
+
+    try:
+        asyncio.run(main())
+    except KeyboardInterrupt:
+        pass
+
+
 def now_ms() -> float:
     return time.monotonic() * 1000.0

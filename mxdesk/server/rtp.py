@@ -227,6 +227,9 @@ def parse_rtcp(buf: bytes) -> list[dict]:
                 d["remb_bps"] = mant << exp
         elif pt in (200, 201) and len(body) >= 4:
             d["ssrc"] = struct.unpack_from("!I", body)[0]
+            if pt == 200 and len(body) >= 24:  # sender info: NTP <-> RTP time of one instant
+                ntp_s, ntp_f, d["rtp_ts"], d["packets"], d["octets"] = struct.unpack_from("!IIIII", body, 4)
+                d["ntp"] = ntp_s + ntp_f / 2.0 ** 32
             blocks = []
             k = 24 if pt == 200 else 4
             for _ in range(fmt):  # report blocks (fmt = reception report count)

@@ -765,7 +765,10 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                     self.dc_send(self._dc_stats())
                     self._last_dc_stats = now
             if self.srtp_tx is not None and self.remote is not None and now - last_sr > 1.0:
-                sr = R.build_sr(self.ssrc, getattr(self, "last_ts", 0), self.pkt.packets, self.pkt.octets)
+                # the SR's RTP timestamp is the RTP clock NOW (capture clock, 90 kHz), so a receiver
+                # maps any frame's timestamp to the wall clock (A/V sync; end-to-end latency)
+                rtp_now = ((_native().now_us() - self.ts0) * 9 // 100) & 0xFFFFFFFF if self.ts0 is not None else 0
+                sr = R.build_sr(self.ssrc, rtp_now, self.pkt.packets, self.pkt.octets)
                 self._sendto(self.srtp_tx.protect_rtcp(sr), self.remote)
                 if self.srtp_tx_audio is not None and getattr(self, "audio_packets", 0):
                     asr = R.build_sr(self.audio_ssrc, self.audio_ts, self.audio_packets, self.audio_octets)

@@ -62,6 +62,8 @@ class WhepResult:
     connect_ms: float = 0.0
     stream: bytes = b""
     arrival_us: list[int] = field(default_factory=list)  # CLOCK_MONOTONIC us when each AU completed
+    arrival_wall: list[float] = field(default_factory=list)  # time.time() when each AU completed
+    sr_map: tuple[float, int] | None = None  # last RTCP SR: (NTP seconds, RTP timestamp) of one instant
     audio_payloads: list[bytes] = field(default_factory=list)  # PCMU packets (20 ms each)
     audio_seqs: list[int] = field(default_factory=list)
     nacked: int = 0        # RTP packets NACKed after a real (not test-injected) loss
@@ -72,6 +74,21 @@ class WhepResult:
     dc_audio: list[bytes] = field(default_factory=list)   # MXA1 chunks from the "audio" channel
     dc_sent: int = 0
     dc_labels: list[str] = field(default_factory=list)  # server-opened channels (selkies "input")
+
+
+def e2e_latency_ms(res: WhepResult) -> list[float]:
+    """Capture -> viewer latency of every received access unit, from the sender's RTCP SR
+    (RFC 3550 6.4.1: NTP time and RTP timestamp of one instant) -- valid when sender and viewer
+    share a clock (same host).  Empty before the first SR."""
+    if res.sr_map is None:
+        return []
+    ntp, rtp_sr = res.sr_map
+    wall_sr = ntp - R.NTP_EPOCH_OFFSET
+    out = []
+    for ts, arr in zip(res.rtp_ts, res.arrival_wall):
+        d = ((ts - rtp_sr + 0x80000000) & 0xFFFFFFFF) - 0x80000000  # signed 32-bit RTP distance
+        out.append((arr - (wall_sr + d / 90000.0)) * 1e3)
+    return out
 
 
 class _Client(asyncio.DatagramProtocol):
@@ -305,6 +322,7 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                 res.aus.append(au)
                 res.rtp_ts.append(R.rtp_header(pk)["ts"])
                 res.arrival_us.append(time.monotonic_ns() // 1000)
+                res.arrival_wall.append(time.time())
                 if pli_after and len(res.aus) == pli_after and not sent_pli:
                     tr.sendto(tx.protect_rtcp(R.build_pli(my_ssrc, media_ssrc)))
                     sent_pli = True
@@ -357,8 +375,11 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                 continue
             if 192 <= d[1] <= 223:
                 p = rx_for(d).unprotect_rtcp(d)
-                if p and any(x["pt"] == 200 for x in R.parse_rtcp(p)):
-                    res.srs += 1
+                for x in (R.parse_rtcp(p) if p else []):
+                    if x["pt"] == 200:
+                        res.srs += 1
+                        if "ntp" in x and x["ssrc"] == media_ssrc:  # the video sender's SR
+                            res.sr_map = (x["ntp"], x["rtp_ts"])
                 continue
             p = rx_for(d).unprotect_rtp(d)
             if not p:

@@ -152,7 +152,10 @@ SCHEMA: list[Var] = [
     Var("subpel", ["MXDESK_SUBPEL"], True, bool, "quarter-pel motion refinement"),
     Var("noise", ["MXDESK_NOISE"], True, bool, "synthetic desktop: animated-noise panel"),
     Var("wall", ["MXDESK_WALL"], "", str, "tiled wall layout, e.g. '2x2' (one tile per GPU)"),
-    Var("sessions", ["MXDESK_SESSIONS"], 0, int, "sessions to launch (0 = one per visible GPU)"),
+    Var("sessions", ["MXDESK_SESSIONS"], 1, int,
+        "sessions per process: `serve` streams K independent desktops from one process on one GPU "
+        "(ports port .. port+K-1, one HIP stream and native encode thread each); `launch` starts one such "
+        "process per visible GPU"),
     Var("enable_gamepad", ["MXDESK_GAMEPAD", "SELKIES_ENABLE_GAMEPAD"], True, bool,
         "browser gamepads -> /dev/input/jsN via the LD_PRELOAD interposer", ref="Dockerfile:473-476"),
     Var("js_dir", ["MXDESK_JS_DIR"], "/tmp", str, "directory of the joystick interposer sockets"),

@@ -49,11 +49,56 @@ def test_x11_capture_without_server_fails_cleanly():
 
 
 def test_session_programs_pin_one_gpu_each():
+    # K sessions per GPU live in ONE process per GPU (serve --sessions K), ports base + K*gpu ..
     progs = session_programs(4, base_port=9000, sessions_per_gpu=2)
-    assert len(progs) == 8
-    assert [p.environment["HIP_VISIBLE_DEVICES"] for p in progs] == ["0", "0", "1", "1", "2", "2", "3", "3"]
-    assert [p.environment["SELKIES_PORT"] for p in progs] == [str(9000 + i) for i in range(8)]
+    assert len(progs) == 4
+    assert [p.environment["HIP_VISIBLE_DEVICES"] for p in progs] == ["0", "1", "2", "3"]
+    assert [p.environment["SELKIES_PORT"] for p in progs] == ["9000", "9002", "9004", "9006"]
     assert all(p.ready.kind == "tcp" and p.command[1:4] == ["-m", "mxdesk", "serve"] for p in progs)
+    assert all(p.command[-2:] == ["--sessions", "2"] for p in progs)
+    single = session_programs(2, base_port=9000)
+    assert [p.environment["SELKIES_PORT"] for p in single] == ["9000", "9001"]
+    assert all("--sessions" not in p.command for p in single)
+
+
+def test_serve_sessions_streams_k_sessions_from_one_process(native, monkeypatch):
+    """`mxdesk serve --sessions 3` (CPU plumbing backend here): three MediaServers on consecutive
+    ports in one event loop, each streaming its own desktop over /mxws."""
+    import asyncio
+    import threading
+
+    from mxdesk import cli
+    from mxdesk.server import app as A
+    from mxdesk.utils import config as C
+
+    from .test_server import free_port, view
+
+    base = free_port()
+    cfg = C.load(env={"WEBRTC_ENCODER": "x264enc", "SIZEW": "160", "SIZEH": "96", "REFRESH": "30",
+                      "ENABLE_BASIC_AUTH": "false", "SELKIES_ENABLE_AUDIO": "false", "MXDESK_GAMEPAD": "false",
+                      "MXDESK_SOURCE": "synthetic"}, argv=["--port", str(base), "--sessions", "3"])
+    assert cfg.sessions == 3
+    started = {}
+
+    def fake_run(servers, host, ports, ssl_ctx=None):
+        started["servers"], started["ports"] = servers, ports
+
+        async def main():
+            runners = [await A.serve(s, "127.0.0.1", p) for s, p in zip(servers, ports)]
+            try:
+                return [await view(f"http://127.0.0.1:{p}/mxws", 3) for p in ports]
+            finally:
+                for r in runners:
+                    await r.cleanup()
+        started["results"] = asyncio.run(main())
+
+    monkeypatch.setattr(A, "run_forever_multi", fake_run)
+    cli.cmd_serve(cfg, None)
+    assert started["ports"] == [base, base + 1, base + 2]
+    assert len({id(s.pipeline) for s in started["servers"]}) == 3
+    assert [len(r.frames) for r in started["results"]] == [3, 3, 3]
+    assert all(r.frames[0]["key"] for r in started["results"])
+    assert threading.active_count() < 50
 
 
 def test_desktop_env_gl_hygiene_and_icd_report(tmp_path):

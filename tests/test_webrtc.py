@@ -372,3 +372,28 @@ def test_whep_client_repairs_real_loss_with_nack(native, monkeypatch):
     frames = Decoder().decode(res.stream)
     ids = [read_barcode(y)[0] for y, _, _ in frames]
     assert len(ids) == 15 and all(b == a + 1 for a, b in zip(ids, ids[1:]))
+
+
+def test_rtcp_sr_maps_rtp_to_wall_clock(native, monkeypatch):
+    """The sender report carries the RTP clock of the moment it is sent, so the viewer maps every
+    frame's RTP timestamp to the capture wall-clock time: the end-to-end latencies derived from
+    it are small and positive on one host (tools/bench_density.py relies on this)."""
+    from mxdesk.server.whep_client import e2e_latency_ms
+
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
+    from mxdesk.server.app import serve
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await whep_view(f"http://127.0.0.1:{port}/whep", 45)
+        finally:
+            await runner.cleanup()
+
+    res = asyncio.run(go())
+    assert res.srs >= 1 and res.sr_map is not None
+    lat = e2e_latency_ms(res)
+    assert len(lat) == 45
+    assert all(-2.0 < v < 500.0 for v in lat), lat  # same host: capture precedes arrival (ms resolution)
