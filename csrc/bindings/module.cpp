@@ -161,6 +161,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("mask_x1", &h264::EncoderConfig::mask_x1)
         .def_readwrite("mask_y1", &h264::EncoderConfig::mask_y1)
         .def_readwrite("deblock", &h264::EncoderConfig::deblock)
+        .def_readwrite("partitions", &h264::EncoderConfig::partitions)
         .def_readwrite("tu_split", &h264::EncoderConfig::tu_split);
 
     py::class_<h264::FrameStats>(m, "FrameStats")
@@ -216,17 +217,18 @@ PYBIND11_MODULE(_native, m) {
                  return a.reshape({e.common().mb_h(), e.common().mb_w()});
              })
         .def("mb_info",
-             [](h264::CpuH264Encoder& e) {  // (mb_h, mb_w, 8): type, qp, cbp, skip, mvx, mvy, nz_luma sum, cost
+             [](h264::CpuH264Encoder& e) {  // (mb_h, mb_w, 9): type, qp, cbp, skip, mvx, mvy, nz_luma sum, cost, part
                  const auto& v = e.mb_info();
-                 py::array_t<int32_t> a({(py::ssize_t)v.size(), (py::ssize_t)8});
+                 py::array_t<int32_t> a({(py::ssize_t)v.size(), (py::ssize_t)9});
                  int32_t* d = a.mutable_data();
                  for (size_t i = 0; i < v.size(); ++i) {
                      int nz = 0;
                      for (int k = 0; k < 16; ++k) nz += v[i].nz_luma[k];
-                     const int32_t r[8] = {v[i].type, v[i].qp, v[i].cbp, v[i].skip, v[i].mvx, v[i].mvy, nz, (int32_t)v[i].cost};
-                     std::memcpy(d + 8 * i, r, sizeof r);
+                     const int32_t r[9] = {v[i].type, v[i].qp, v[i].cbp, v[i].skip, v[i].mvx, v[i].mvy, nz,
+                                           (int32_t)v[i].cost, v[i].part};
+                     std::memcpy(d + 9 * i, r, sizeof r);
                  }
-                 return a.reshape({e.common().mb_h(), e.common().mb_w(), 8});
+                 return a.reshape({e.common().mb_h(), e.common().mb_w(), 9});
              })
         .def("request_idr", [](h264::CpuH264Encoder& e) { e.common().request_idr(); })
         .def("set_bitrate", [](h264::CpuH264Encoder& e, int k) { e.common().set_bitrate(k); })

@@ -109,6 +109,139 @@ void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, 
     *out_mvy = mvy;
 }
 
+// Partition-aware search (the rules of k_me_full with FrameState::partitions):
+//  * every integer candidate's SAD is kept per 8x8 quadrant, so one pass scores the 16x16 block
+//    and the four partitions (16x8 top / bottom, 8x16 left / right), each with its own best key
+//    (cost = SAD + lambda * vector bits, ties -> shorter vector, then lower candidate index);
+//  * coarse mode: the even-offset grid, then the 8 integer neighbours of EACH shape's grid best;
+//  * shape: 16x16 unless a partitioning's two costs + 2 lambda (mb_type ue(1) / ue(2) vs ue(0))
+//    are lower (16x8 before 8x16 on ties);
+//  * quarter-pel refinement (half, then quarter) of the chosen shape's vector(s), each over its
+//    own rectangle.
+void me_search_parts_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw_, int ch_, int x0, int y0,
+                         int frame_qp, int search_range, int subpel, int coarse, MbInfo& m) {
+    const int lambda = lambda_sad(frame_qp);
+    const int R = me_range(search_range);
+    const int side = 2 * R + 1;
+    uint32_t sad0 = 0;
+    for (int r = 0; r < 16; ++r)
+        for (int k = 0; k < 16; ++k)
+            sad0 += std::abs((int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + k, y0 + r));
+    m.part = kPart16x16;
+    m.mvx = m.mvy = 0;
+    for (int i = 0; i < 4; ++i) m.pmv[i] = 0;
+    if (sad0 <= static_sad(frame_qp)) return;
+    // shapes: 0 = 16x16, 1 = top, 2 = bottom, 3 = left, 4 = right (quadrants TL, TR, BL, BR)
+    auto quads = [&](int c, uint32_t q[4]) {
+        const int dy = c / side - R, dx = c % side - R;
+        q[0] = q[1] = q[2] = q[3] = 0;
+        for (int r = 0; r < 16; ++r)
+            for (int k = 0; k < 16; ++k)
+                q[(r >= 8 ? 2 : 0) + (k >= 8 ? 1 : 0)] += (uint32_t)std::abs(
+                    (int)sy[(y0 + r) * pitch + x0 + k] - ref_px(ref_y, cw_, cw_, ch_, x0 + dx + k, y0 + dy + r));
+    };
+    auto shape_sad = [](const uint32_t q[4], int s) {
+        switch (s) {
+            case 0: return q[0] + q[1] + q[2] + q[3];
+            case 1: return q[0] + q[1];
+            case 2: return q[2] + q[3];
+            case 3: return q[0] + q[2];
+            default: return q[1] + q[3];
+        }
+    };
+    auto key = [&](uint32_t sad, int c) {
+        const int dy = c / side - R, dx = c % side - R;
+        const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
+        const uint32_t dist = (uint32_t)(std::abs(dx) + std::abs(dy));
+        return ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)c;
+    };
+    unsigned long long best[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+    auto visit = [&](int c, unsigned long long* b) {
+        uint32_t q[4];
+        quads(c, q);
+        for (int s = 0; s < 5; ++s) b[s] = std::min(b[s], key(shape_sad(q, s), c));
+    };
+    if (coarse) {
+        for (int dyr = 0; dyr < side; dyr += 2)
+            for (int dxr = 0; dxr < side; dxr += 2) visit(dyr * side + dxr, best);
+        unsigned long long nb[5];
+        for (int s = 0; s < 5; ++s) nb[s] = best[s];
+        for (int s = 0; s < 5; ++s) {
+            const int cb0 = (int)(best[s] & 0xffff), bxr = cb0 % side, byr = cb0 / side;
+            for (int k = 0; k < 8; ++k) {
+                int ddx, ddy;
+                subpel_offset(k, &ddx, &ddy);
+                const int nxr = bxr + ddx, nyr = byr + ddy;
+                if (nxr < 0 || nxr >= side || nyr < 0 || nyr >= side) continue;
+                uint32_t q[4];
+                quads(nyr * side + nxr, q);
+                nb[s] = std::min(nb[s], key(shape_sad(q, s), nyr * side + nxr));
+            }
+        }
+        for (int s = 0; s < 5; ++s) best[s] = nb[s];
+    } else {
+        for (int c = 0; c < side * side; ++c) visit(c, best);
+    }
+    auto cost_of = [](unsigned long long k) { return (uint32_t)(k >> 32); };
+    const uint32_t c16 = cost_of(best[0]);
+    const uint32_t ch = cost_of(best[1]) + cost_of(best[2]) + 2u * (uint32_t)lambda;
+    const uint32_t cv = cost_of(best[3]) + cost_of(best[4]) + 2u * (uint32_t)lambda;
+    const int part = (c16 <= ch && c16 <= cv) ? kPart16x16 : (ch <= cv ? kPart16x8 : kPart8x16);
+    // rectangle of each shape (x, y, w, h) and the refinement
+    constexpr int kRect[5][4] = {{0, 0, 16, 16}, {0, 0, 16, 8}, {0, 8, 16, 8}, {0, 0, 8, 16}, {8, 0, 8, 16}};
+    auto refine = [&](int s, int* vx, int* vy) {
+        const int cb = (int)(best[s] & 0xffff);
+        *vx = 4 * ((cb % side) - R);
+        *vy = 4 * ((cb / side) - R);
+        if (!subpel) return;
+        const int rx = kRect[s][0], ry = kRect[s][1], rw = kRect[s][2], rh = kRect[s][3];
+        auto sad_at = [&](int cx, int cy) {
+            uint32_t t = 0;
+            for (int r = ry; r < ry + rh; ++r)
+                for (int k = rx; k < rx + rw; ++k)
+                    t += std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
+                                  luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + cx, (y0 + r) * 4 + cy));
+            return t;
+        };
+        uint32_t cur = cost_of(best[s]);
+        for (int step = 2; step >= 1; step >>= 1) {
+            int bdx = 0, bdy = 0;
+            uint32_t bcost = cur;
+            for (int k = 0; k < 8; ++k) {
+                int ddx, ddy;
+                subpel_offset(k, &ddx, &ddy);
+                const int cx = *vx + ddx * step, cy = *vy + ddy * step;
+                const uint32_t cost = me_cost(sad_at(cx, cy), lambda, cx, cy);
+                if (cost < bcost) {
+                    bcost = cost;
+                    bdx = ddx * step;
+                    bdy = ddy * step;
+                }
+            }
+            *vx += bdx;
+            *vy += bdy;
+            cur = bcost;
+        }
+    };
+    int vx, vy;
+    if (part == kPart16x16) {
+        refine(0, &vx, &vy);
+        m.mvx = (int16_t)vx;
+        m.mvy = (int16_t)vy;
+        return;
+    }
+    const int cb = (int)(best[0] & 0xffff);  // the 16x16 vector stays integer here
+    m.mvx = (int16_t)(4 * ((cb % side) - R));
+    m.mvy = (int16_t)(4 * ((cb / side) - R));
+    m.part = (uint8_t)part;
+    const int s0 = part == kPart16x8 ? 1 : 3;
+    for (int i = 0; i < 2; ++i) {
+        refine(s0 + i, &vx, &vy);
+        m.pmv[2 * i] = (int16_t)vx;
+        m.pmv[2 * i + 1] = (int16_t)vy;
+    }
+}
+
 CpuH264Encoder::CpuH264Encoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
     cw_ = common_.mb_w() * 16;
     ch_ = common_.mb_h() * 16;
@@ -298,31 +431,39 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             const int mbi = mby * g.mb_w + mbx, x0 = mbx * 16, y0 = mby * 16;
             MbInfo& m = mb_[mbi];
             std::memset(&m, 0, sizeof m);
-            int mvx = 0, mvy = 0;
-            me_search_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &mvx, &mvy,
-                          cfg_.me_coarse);
-            m.mvx = (int16_t)mvx;
-            m.mvy = (int16_t)mvy;
+            if (cfg_.partitions) {
+                me_search_parts_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel,
+                                    cfg_.me_coarse, m);
+            } else {
+                int vx = 0, vy = 0;
+                me_search_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &vx, &vy,
+                              cfg_.me_coarse);
+                m.mvx = (int16_t)vx;
+                m.mvy = (int16_t)vy;
+            }
             m.type = kMbP16x16;
-            // ---- prediction + residual
+            // ---- prediction + residual (per partition: each sample's vector)
             int pred[384], res[384];
             uint32_t lsad = 0;
             for (int r = 0; r < 16; ++r)
                 for (int k = 0; k < 16; ++k) {
-                    const int p = luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
+                    const Mv v = px_mv(m, k, r);
+                    const int p = luma_qpel(ref_y, cw_, cw_, ch_, (x0 + k) * 4 + v.x, (y0 + r) * 4 + v.y);
                     pred[r * 16 + k] = p;
                     res[r * 16 + k] = sy[(y0 + r) * pitch + x0 + k] - p;
                     lsad += (uint32_t)std::abs(res[r * 16 + k]);
                 }
             // temporal class: the source's change against the previous source, displaced by the
-            // integer part of the vector (aq 3)
+            // integer part of each sample's vector (aq 3)
             uint32_t tsad = 0;
             if (cfg_.aq >= 3 && !prev_src_.empty()) {
-                const int ix = mvx >> 2, iy = mvy >> 2;
                 for (int r = 0; r < 16; ++r)
-                    for (int k = 0; k < 16; ++k)
+                    for (int k = 0; k < 16; ++k) {
+                        const Mv v = px_mv(m, k, r);
                         tsad += (uint32_t)std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
-                                                   (int)ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + k + ix, y0 + r + iy));
+                                                   (int)ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + k + (v.x >> 2),
+                                                               y0 + r + (v.y >> 2)));
+                    }
             }
             const int tcls = temporal_class(tsad);
             const int qp = mb_qp_for(frame_qp, lsad, tcls, cfg_.aq);
@@ -332,7 +473,8 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
                 for (int r = 0; r < 8; ++r)
                     for (int k = 0; k < 8; ++k) {
                         const int xc = x0 / 2 + k, yc = y0 / 2 + r;
-                        const int p = chroma_pred8(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc * 8 + mvx, yc * 8 + mvy);
+                        const Mv v = px_mv(m, 2 * k, 2 * r);
+                        const int p = chroma_pred8(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc * 8 + v.x, yc * 8 + v.y);
                         pred[256 + comp * 64 + r * 8 + k] = p;
                         res[256 + comp * 64 + r * 8 + k] = suv[yc * pitch + 2 * xc + comp] - p;
                     }
@@ -406,7 +548,7 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             }
             cbp |= (any_ac ? 2 : (any_dc ? 1 : 0)) << 4;
             m.cbp = (uint8_t)cbp;
-            m.cost = inter_cost(satd, frame_qp, mvx, mvy);
+            m.cost = inter_cost_mb(satd, frame_qp, m);
         }
     // intra macroblocks in the P slice: open-loop decision against the inter cost, local-maximum
     // selection (independent intra MBs), then their coding from the final inter reconstruction
@@ -463,9 +605,9 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         int qp_pred = frame_qp_();  // mb_qp_delta predictor: QP of the last MB that carried one
         for (int mbi = first; mbi < last; ++mbi) {
             const Avail av = mb_avail(g, mbi % g.mb_w, mbi / g.mb_w, slice_rows);
-            int mvdx, mvdy;
+            int mvd[4];
             const MbNbrs nb = mb_nbrs(mb_.data(), mbi, g.mb_w);
-            const bool skip = decide_skip(nb, av, &mvdx, &mvdy);
+            const bool skip = decide_skip(nb, av, mvd);
             mb_[mbi].skip = skip;
             if (skip) {
                 ++run;
@@ -483,7 +625,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
                 qp_pred = mb_[mbi].qp;
             }
             for (int role = 0; role < kNumRoles; ++role)
-                code_role(w, role, g, idr, nb, mc, av, mvdx, mvdy, dqp);
+                code_role(w, role, g, idr, nb, mc, av, mvd, dqp);
             mb_bits_[mbi] = w.bits - b0;
         }
         if (!idr && run > 0) put_ue(w, (uint32_t)run);

@@ -32,9 +32,15 @@ MXHD int db_clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v
 
 // Motion vector of raster 4x4 block `blk` (by * 4 + bx) of an inter macroblock.
 MXHD void db_blk_mv(const MbInfo& m, int blk, int* mvx, int* mvy) {
-    (void)blk;  // P16x16: one vector per macroblock
-    *mvx = m.mvx;
-    *mvy = m.mvy;
+    const int bx = blk & 3, by = blk >> 2;
+    const bool second = (m.part == kPart16x8 && by >= 2) || (m.part == kPart8x16 && bx >= 2);
+    if (m.part == kPart16x16) {
+        *mvx = m.mvx;
+        *mvy = m.mvy;
+    } else {
+        *mvx = m.pmv[second ? 2 : 0];
+        *mvy = m.pmv[second ? 3 : 1];
+    }
 }
 
 // Boundary strength (8.7.2.1) of the edge between raster 4x4 luma block bp of macroblock p and

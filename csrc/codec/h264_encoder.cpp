@@ -409,6 +409,7 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.hp_pitch = hp_pitch_;
     f.aq = cfg_.aq;
     f.intra_in_p = cfg_.intra_in_p;
+    f.partitions = cfg_.partitions ? 1 : 0;
     f.mask_mx0 = mask_mb_[0];
     f.mask_my0 = mask_mb_[1];
     f.mask_mx1 = mask_mb_[2];

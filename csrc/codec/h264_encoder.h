@@ -46,6 +46,9 @@ struct EncoderConfig {
     // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it cost
     // 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)
     int deblock = -1;
+    // P pictures: also search 16x8 / 8x16 partitionings (two vectors per macroblock) and take one
+    // when its SAD + lambda * vector rate beats the 16x16 vector's
+    int partitions = 1;
     bool h264_deblock() const { return deblock > 0; }
     bool hevc_deblock() const { return deblock != 0; }
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
@@ -280,6 +283,10 @@ class CpuH264Encoder {
 // CPU H.264 and HEVC encoders.
 void me_search_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw, int ch, int x0, int y0, int qp,
                    int search_range, int subpel, int* mvx, int* mvy, int coarse);
+// The same search plus 16x8 / 8x16 partitionings (k_me_full with FrameState::partitions): writes
+// m.mvx / mvy (best 16x16 vector), m.part and m.pmv.
+void me_search_parts_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int cw, int ch, int x0, int y0, int qp,
+                         int search_range, int subpel, int coarse, MbInfo& m);
 
 // Pad a display-sized NV12 frame to the coded size by edge replication (what the CSC
 // kernel does on the GPU side).  Returns pitch = coded width.

@@ -43,8 +43,15 @@ struct MbInfo {
     uint8_t itype; // P pictures: the intra type k_intra_analyze decided (applied if k_intra_p selects the MB)
     uint8_t i4[8];     // Intra4x4 prediction modes, two per byte, raster block order
     uint32_t cost;     // P pictures: inter luma SATD cost (+ mv rate), for the intra decision
+    // inter partitioning (H.264 P pictures): part 0 = P_L0_16x16 (vector mvx / mvy), 1 = 16x8,
+    // 2 = 8x16 with the vectors of partitions 0 / 1 in pmv[0..1] / pmv[2..3] (quarter-pel).
+    // mvx / mvy always keep the best 16x16 vector (the HEVC and VP8 encoders read only those).
+    int16_t pmv[4];
+    uint8_t part;
+    uint8_t pad_[7];
 };
-static_assert(sizeof(MbInfo) == 48, "MbInfo layout");
+static_assert(sizeof(MbInfo) == 64, "MbInfo layout");
+enum MbPart : uint8_t { kPart16x16 = 0, kPart16x8 = 1, kPart8x16 = 2 };
 
 MXHD_GPU bool is_intra(const MbInfo& m) { return m.type != kMbP16x16; }
 // Whether macroblock (mbx, mby) is outside the quality-report mask of the frame state.
@@ -80,6 +87,7 @@ struct FrameState {
     int32_t hp_pitch;  // pitch of the padded half-pel planes
     int32_t aq;        // adaptive quantisation on/off (P frames)
     int32_t intra_in_p;  // P frames: k_intra_analyze / k_intra_wave run (distortion deltas included)
+    int32_t partitions;  // P frames: k_me_full also searches 16x8 / 8x16 partitionings (H.264)
     // quality report: MBs in [mask_mx0, mask_mx1) x [mask_my0, mask_my1) are left out of the 4th
     // distortion channel (e.g. the synthetic desktop's noise panel); empty rect = no mask
     int32_t mask_mx0, mask_my0, mask_mx1, mask_my1;

@@ -310,8 +310,11 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         const uint32_t sad0 = s_sad0[0];
         if (sad0 <= static_sad(fs->qp)) {
             if (tid == 0) {
-                mbs[mbi].mvx = 0;
-                mbs[mbi].mvy = 0;
+                MbInfo& m = mbs[mbi];
+                m.mvx = 0;
+                m.mvy = 0;
+                m.part = kPart16x16;
+                m.pmv[0] = m.pmv[1] = m.pmv[2] = m.pmv[3] = 0;
             }
             return;  // uniform across the workgroup
         }
@@ -337,7 +340,67 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     // coarse mode (me_coarse): the even-offset grid first -- two candidates per thread (window
     // shifts 0 and 2 of a dword group), (R + 1) * gw tasks in one pass -- then the 8 integer
     // neighbours of its best (me_search_cpu does the same)
-    const int ntask = coarse ? (R + 1) * gw : 0;
+    const bool parts = fs->partitions != 0;  // 16x8 / 8x16 partitionings searched too (me_search_parts_cpu)
+    const int ntask = (coarse && !parts) ? (R + 1) * gw : 0;
+    auto mkey = [&](uint32_t sad, int dxr, int dyr) {
+        const int dx = dxr - R, dy = dyr - R;
+        const uint32_t cost = me_cost(sad, lambda, 4 * dx, 4 * dy);
+        const uint32_t dist = (uint32_t)(abs(dx) + abs(dy));
+        return ((unsigned long long)cost << 32) | (dist << 16) | (uint32_t)(dyr * side + dxr);
+    };
+    // partitions: per candidate the SAD of each 8x8 quadrant (TL, TR, BL, BR); the 16x16 key is
+    // their sum (so the 16x16 decision is unchanged) and shapes T / B / L / R keep their own best
+    unsigned long long pb[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    auto kmin = [](unsigned long long a, unsigned long long c) { return c < a ? c : a; };
+    auto visit_quads = [&](const uint32_t* qd, int dxr, int dyr) {
+        best = kmin(best, mkey(qd[0] + qd[1] + qd[2] + qd[3], dxr, dyr));
+        pb[0] = kmin(pb[0], mkey(qd[0] + qd[1], dxr, dyr));
+        pb[1] = kmin(pb[1], mkey(qd[2] + qd[3], dxr, dyr));
+        pb[2] = kmin(pb[2], mkey(qd[0] + qd[2], dxr, dyr));
+        pb[3] = kmin(pb[3], mkey(qd[1] + qd[3], dxr, dyr));
+    };
+    if (parts) {
+        // tasks: the even grid (coarse, shifts 0 and 2 of a dword group) or every group (shifts 0..3)
+        const int nsh = coarse ? 2 : 4, ntp = coarse ? (R + 1) * gw : ngroups;
+        for (int q = tid; q < ntp; q += 256) {
+            const int dyr = coarse ? 2 * (q / gw) : q / gw, g = q % gw;
+            uint32_t acc[4][4];  // [shift index][quadrant]
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0;
+#pragma unroll 2
+            for (int r = 0; r < 16; ++r) {
+                const int a = (dyr + r) * kWs4 + g, hq = r < 8 ? 0 : 2;
+                const uint32_t w0 = win32[a], w1 = win32[a + 1], w2 = win32[a + 2], w3 = win32[a + 3], w4 = win32[a + 4];
+                const uint32_t s0 = srcw[r * 4 + 0], s1 = srcw[r * 4 + 1], s2 = srcw[r * 4 + 2], s3 = srcw[r * 4 + 3];
+#pragma unroll
+                for (int si = 0; si < 4; ++si) {
+                    if (si >= nsh) break;
+                    const int sh = coarse ? 2 * si : si;
+                    const uint32_t a0 = sh ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w0;
+                    const uint32_t a1 = sh ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w1;
+                    const uint32_t a2 = sh ? __builtin_amdgcn_alignbyte(w3, w2, sh) : w2;
+                    const uint32_t a3 = sh ? __builtin_amdgcn_alignbyte(w4, w3, sh) : w3;
+                    uint32_t lft = hq ? acc[si][2] : acc[si][0], rgt = hq ? acc[si][3] : acc[si][1];
+                    lft = __builtin_amdgcn_sad_u8(a1, s1, __builtin_amdgcn_sad_u8(a0, s0, lft));
+                    rgt = __builtin_amdgcn_sad_u8(a3, s3, __builtin_amdgcn_sad_u8(a2, s2, rgt));
+                    if (hq) {
+                        acc[si][2] = lft;
+                        acc[si][3] = rgt;
+                    } else {
+                        acc[si][0] = lft;
+                        acc[si][1] = rgt;
+                    }
+                }
+            }
+#pragma unroll
+            for (int si = 0; si < 4; ++si) {
+                if (si >= nsh) break;
+                const int dxr = 4 * g + (coarse ? 2 * si : si);
+                if (dxr >= side) break;
+                visit_quads(acc[si], dxr, dyr);
+            }
+        }
+    }
     for (int q = tid; q < ntask; q += 256) {
         const int dyr = 2 * (q / gw), g = q % gw;
         uint32_t s0a = 0, s2a = 0;
@@ -366,7 +429,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             best = key < best ? key : best;
         }
     }
-    for (int q = tid; q < (coarse ? 0 : ngroups); q += 256) {
+    for (int q = tid; q < ((coarse || parts) ? 0 : ngroups); q += 256) {
         const int dyr = q / gw, g = q - dyr * gw;
         uint32_t sad[4] = {0, 0, 0, 0};
 #pragma unroll 2
@@ -404,9 +467,54 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         best = other < best ? other : best;
     }
     if (lane == 0) red[tid >> 6] = best;
+    __shared__ unsigned long long pred4[4][4];  // partitions: [shape][wave]
+    if (parts) {
+#pragma unroll
+        for (int sh = 0; sh < 4; ++sh) {
+            unsigned long long v = pb[sh];
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long other = __shfl_xor(v, o, 64);
+                v = other < v ? other : v;
+            }
+            if (lane == 0) pred4[sh][tid >> 6] = v;
+        }
+    }
     __syncthreads();
     unsigned long long b = red[0];
     for (int i = 1; i < 4; ++i) b = red[i] < b ? red[i] : b;
+    unsigned long long pbest[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    if (parts)
+        for (int sh = 0; sh < 4; ++sh)
+            for (int i = 0; i < 4; ++i) pbest[sh] = pred4[sh][i] < pbest[sh] ? pred4[sh][i] : pbest[sh];
+    if (parts && coarse) {
+        // the 8 integer neighbours of each partition's grid best: 32 (shape, neighbour) pairs of
+        // 128-sample rectangles, 8 lanes (16 samples) each
+        __shared__ unsigned long long pnkey[4][8];
+        const int ev = tid >> 3, sub = tid & 7, sh = ev >> 3, k = ev & 7;
+        const int cb0 = (int)(pbest[sh] & 0xffff), bxr = cb0 % side, byr = cb0 / side;
+        int ddx, ddy;
+        subpel_offset(k, &ddx, &ddy);
+        const int nxr = bxr + ddx, nyr = byr + ddy;
+        const bool inside = nxr >= 0 && nxr < side && nyr >= 0 && nyr < side;  // uniform per 8-lane group
+        int d = 0;
+        if (inside) {
+            // T / B: one 16-sample row each (row sub of the half); L / R: two 8-sample rows
+            const uint8_t* wb = reinterpret_cast<const uint8_t*>(win32);
+            const uint8_t* sb = reinterpret_cast<const uint8_t*>(srcw);
+            for (int part_row = 0; part_row < 2; ++part_row) {
+                const int rr = sh < 2 ? (sh == 0 ? sub : 8 + sub) : 2 * sub + part_row;
+                const int c0 = sh < 2 ? 8 * part_row : (sh == 2 ? 0 : 8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    d += abs((int)sb[rr * 16 + c0 + j] - (int)wb[(nyr + rr) * kWinStride + nxr + c0 + j]);
+            }
+        }
+        for (int o = 4; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (sub == 0) pnkey[sh][k] = inside ? mkey((uint32_t)d, nxr, nyr) : ~0ull;
+        __syncthreads();
+        for (int s2 = 0; s2 < 4; ++s2)
+            for (int i = 0; i < 8; ++i) pbest[s2] = pnkey[s2][i] < pbest[s2] ? pnkey[s2][i] : pbest[s2];
+    }
     if (coarse) {  // the 8 integer neighbours of the grid best: one per 32-lane group
         __shared__ unsigned long long nkey[8];
         const int cb0 = (int)(b & 0xffff), bxr = cb0 % side, byr = cb0 / side;
@@ -434,6 +542,91 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     }
     const int cbest = (int)(b & 0xffff);
     int mvx = 4 * ((cbest % side) - R), mvy = 4 * ((cbest / side) - R);
+
+    if (parts) {
+        // shape decision on the integer costs: 16x16 unless a partitioning's two costs + 2 lambda
+        // (mb_type bits) are lower, 16x8 before 8x16 on ties
+        const uint32_t c16 = (uint32_t)(b >> 32);
+        const uint32_t chz = (uint32_t)(pbest[0] >> 32) + (uint32_t)(pbest[1] >> 32) + 2u * (uint32_t)lambda;
+        const uint32_t cvt = (uint32_t)(pbest[2] >> 32) + (uint32_t)(pbest[3] >> 32) + 2u * (uint32_t)lambda;
+        const int part = (c16 <= chz && c16 <= cvt) ? kPart16x16 : (chz <= cvt ? kPart16x8 : kPart8x16);
+        if (part != kPart16x16) {
+            const int s0 = part == kPart16x8 ? 0 : 2;  // pbest index of partition 0
+            int pvx[2], pvy[2];
+            uint32_t pcost[2];
+            for (int i = 0; i < 2; ++i) {
+                const int cb = (int)(pbest[s0 + i] & 0xffff);
+                pvx[i] = 4 * ((cb % side) - R);
+                pvy[i] = 4 * ((cb / side) - R);
+                pcost[i] = (uint32_t)(pbest[s0 + i] >> 32);
+            }
+            if (fs->subpel) {
+                // half then quarter pel per partition over its own rectangle: an 18x18 footprint
+                // per partition, 16 lanes (8 samples each) per candidate, both partitions at once
+                __shared__ uint8_t psp[2][4][18][kSpW];
+                __shared__ uint32_t pcand[2][8];
+                for (int i = tid; i < 2 * 4 * 18 * 18; i += 256) {
+                    const int pi = i / (4 * 324), rem0 = i - pi * 4 * 324;
+                    const int pl = rem0 / 324, rem = rem0 - pl * 324, r = rem / 18, c = rem - r * 18;
+                    const uint8_t* base = pl == 0 ? P.f : pl == 1 ? P.h : pl == 2 ? P.v : P.j;
+                    const int ix = x0 + (pvx[pi] >> 2) - 1, iy = y0 + (pvy[pi] >> 2) - 1;
+                    psp[pi][pl][r][c] = base[(iy + r) * P.pitch + ix + c];
+                }
+                __syncthreads();
+                const int pi = tid >> 7, k = (tid >> 4) & 7, sub = tid & 15;
+                // the 8 samples of this lane inside the partition rectangle
+                const int rx = part == kPart8x16 ? 8 * pi : 0, ry = part == kPart16x8 ? 8 * pi : 0;
+                const int prow = part == kPart16x8 ? (sub >> 1) : sub, pcol = part == kPart16x8 ? (sub & 1) * 8 : 0;
+                const int yy = ry + prow, xx = rx + pcol;
+                const uint32_t s0w = srcw[yy * 4 + (xx >> 2)], s1w = srcw[yy * 4 + (xx >> 2) + 1];
+                const int ivx = pvx[pi], ivy = pvy[pi];  // the integer match the footprint is staged around
+                const int base_x4 = xx * 4 + 4 - ivx, base_y4 = yy * 4 + 4 - ivy;
+                for (int step = 2; step >= 1; step >>= 1) {
+                    int ddx, ddy;
+                    subpel_offset(k, &ddx, &ddy);
+                    const int cx = pvx[pi] + ddx * step, cy = pvy[pi] + ddy * step;
+                    int d = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int sv = (int)(((j < 4 ? s0w : s1w) >> (8 * (j & 3))) & 0xff);
+                        d += abs(sv - qpel_lds(psp[pi], base_x4 + 4 * j + cx, base_y4 + cy));
+                    }
+                    for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+                    __syncthreads();  // the previous step's readers are done with pcand
+                    if (sub == 0) pcand[pi][k] = me_cost((uint32_t)d, lambda, cx, cy);
+                    __syncthreads();
+                    for (int q = 0; q < 2; ++q) {
+                        int bdx = 0, bdy = 0;
+                        uint32_t bcost = pcost[q];
+                        for (int kk = 0; kk < 8; ++kk) {
+                            const uint32_t cc = pcand[q][kk];
+                            if (cc < bcost) {
+                                int ex, ey;
+                                subpel_offset(kk, &ex, &ey);
+                                bcost = cc;
+                                bdx = ex * step;
+                                bdy = ey * step;
+                            }
+                        }
+                        pvx[q] += bdx;
+                        pvy[q] += bdy;
+                        pcost[q] = bcost;
+                    }
+                }
+            }
+            if (tid == 0) {
+                MbInfo& m = mbs[mbi];
+                m.mvx = (int16_t)mvx;  // the integer 16x16 vector (unused by the partitioned MB)
+                m.mvy = (int16_t)mvy;
+                m.part = (uint8_t)part;
+                m.pmv[0] = (int16_t)pvx[0];
+                m.pmv[1] = (int16_t)pvy[0];
+                m.pmv[2] = (int16_t)pvx[1];
+                m.pmv[3] = (int16_t)pvy[1];
+            }
+            return;  // uniform
+        }
+    }
 
     if (fs->subpel) {
         // half-pel then quarter-pel around the integer match.  Every candidate of both steps
@@ -486,8 +679,11 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         }
     }
     if (tid == 0) {
-        mbs[mbi].mvx = (int16_t)mvx;
-        mbs[mbi].mvy = (int16_t)mvy;
+        MbInfo& m = mbs[mbi];
+        m.mvx = (int16_t)mvx;
+        m.mvy = (int16_t)mvy;
+        m.part = kPart16x16;
+        m.pmv[0] = m.pmv[1] = m.pmv[2] = m.pmv[3] = 0;
     }
 }
 
@@ -590,10 +786,14 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     int mvx = 0, mvy = 0;
     int lsad = 0;  // this lane's share of sum |luma residual| (adaptive quantisation)
     int tsad = 0;  // this lane's share of sum |src - previous src| (temporal class, aq 3)
+    MbInfo mi;      // this MB's motion (16x16 or two partitions: each lane's samples use their own vector)
+    mi.part = kPart16x16;
     if (valid) {
-        mvx = mbs[mbi].mvx;
-        mvy = mbs[mbi].mvy;
+        mi = mbs[mbi];
         const int r = lane >> 2, c0 = (lane & 3) * 4;
+        const Mv lv = px_mv(mi, c0, r);  // the lane's 4 luma samples lie in one partition
+        mvx = lv.x;
+        mvy = lv.y;
         const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (y0 + r) * g.pitch + x0 + c0);
         if (fs->aq >= 3) {
             // temporal class (h264_mb.h temporal_class): the source against the previous source,
@@ -613,8 +813,9 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         }
         const int cr_ = lane >> 3, cc = lane & 7;
         const int xc = x0 / 2 + cc, yc = y0 / 2 + cr_;
+        const Mv cv = px_mv(mi, 2 * cc, 2 * cr_);
         for (int comp = 0; comp < 2; ++comp) {
-            const int p = chroma_pred8(ref_uv, g.pitch, cw, ch, comp, xc * 8 + mvx, yc * 8 + mvy);
+            const int p = chroma_pred8(ref_uv, g.pitch, cw, ch, comp, xc * 8 + cv.x, yc * 8 + cv.y);
             const int sv = src_uv[yc * g.pitch + 2 * xc + comp];
             pred[wave][256 + comp * 64 + cr_ * 8 + cc] = (uint8_t)p;
             res[wave][256 + comp * 64 + cr_ * 8 + cc] = (int16_t)(sv - p);
@@ -759,7 +960,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
         m.qp = (uint8_t)qp;
         m.i16_mode = 0;
         m.chroma_mode = 0;
-        m.cost = inter_cost(satd_mb, fs->qp, mvx, mvy);
+        m.cost = inter_cost_mb(satd_mb, fs->qp, mi);
     }
 }
 
@@ -1771,8 +1972,8 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     const int16_t* mc = coef + (size_t)mbi * kCoefStride;
 
     // motion vector prediction + P_Skip decision (every lane computes the same values)
-    int mvdx = 0, mvdy = 0;
-    const bool skip = decide_skip(nb, av, &mvdx, &mvdy);
+    int mvd[4];
+    const bool skip = decide_skip(nb, av, mvd);
     // mb_qp_delta: QP predictor = QP of the previous MB in the slice that carried one (a P
     // macroblock with residual); skipped / residual-free MBs inherit it.  Half-wave-parallel
     // backward search, 32 MBs per step (the ballot holds active lanes only; this half's bits
@@ -1823,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     if (!skip && lane < kNumRoles) {
         BitWriter w;
         w.init(rbuf[wave][lane]);
-        code_role(w, lane, g, fs->idr, nb, cbuf[wave], av, mvdx, mvdy, dqp);
+        code_role(w, lane, g, fs->idr, nb, cbuf[wave], av, mvd, dqp);
         w.flush();
         bits = w.bits;
     }

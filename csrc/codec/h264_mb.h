@@ -48,7 +48,17 @@ MXHD MbNbrs mb_nbrs(const MbInfo* mbs, int mbi, int mb_w) {
     return MbNbrs{&mbs[mbi], &mbs[mbi - 1], &mbs[mbi - mb_w], &mbs[mbi - mb_w + 1], &mbs[mbi - mb_w - 1]};
 }
 
-MXHD MvNb mv_nb(const MbInfo* p, bool avail) {
+// Vector of 4x4 block (bx, by) of an inter macroblock (partition-aware).
+MXHD Mv blk_mv(const MbInfo& m, int bx, int by) {
+    if (m.part == kPart16x8) return by < 2 ? Mv{m.pmv[0], m.pmv[1]} : Mv{m.pmv[2], m.pmv[3]};
+    if (m.part == kPart8x16) return bx < 2 ? Mv{m.pmv[0], m.pmv[1]} : Mv{m.pmv[2], m.pmv[3]};
+    return Mv{m.mvx, m.mvy};
+}
+// Vector of luma sample (x, y) of the macroblock.
+MXHD Mv px_mv(const MbInfo& m, int x, int y) { return blk_mv(m, x >> 2, y >> 2); }
+
+// Neighbour for motion-vector prediction: block (bx, by) of macroblock p.
+MXHD MvNb mv_nb_blk(const MbInfo* p, bool avail, int bx, int by) {
     MvNb n;
     n.avail = avail;
     n.ref = -1;
@@ -57,31 +67,78 @@ MXHD MvNb mv_nb(const MbInfo* p, bool avail) {
     const MbInfo& m = *p;
     if (m.type == kMbP16x16) {
         n.ref = 0;
-        n.mv = Mv{m.mvx, m.mvy};
+        n.mv = blk_mv(m, bx, by);
     }
     return n;
 }
 
-// P_Skip decision + mvd for macroblock mbi (type P16x16).  Returns true for P_Skip.
-MXHD bool decide_skip(const MbNbrs& nb, const Avail& av, int* mvdx, int* mvdy) {
+// 8.4.1.3 prediction of partition `idx` (0 / 1) of a 16x8 / 8x16 macroblock: neighbours A, B, C
+// of the partition (C replaced by D when unavailable; blocks of the right neighbour are never
+// available yet), the directional rules, else the median.  mv0: this MB's partition 0 vector.
+MXHD Mv predict_mv_part(const MbNbrs& nb, const Avail& av, int part, int idx, Mv mv0) {
+    MvNb own;
+    own.avail = true;
+    own.ref = 0;
+    own.mv = mv0;
+    MvNb a, b, c;
+    if (part == kPart16x8) {
+        if (idx == 0) {
+            a = mv_nb_blk(nb.left, av.left, 3, 0);
+            b = mv_nb_blk(nb.top, av.top, 0, 3);
+            c = av.topright ? mv_nb_blk(nb.topright, true, 0, 3) : mv_nb_blk(nb.topleft, av.topleft, 3, 3);
+            if (b.ref == 0) return b.mv;
+        } else {
+            a = mv_nb_blk(nb.left, av.left, 3, 2);
+            b = own;
+            c = mv_nb_blk(nb.left, av.left, 3, 1);  // C = (16, 7) not yet decoded -> D = (-1, 7)
+            if (a.ref == 0) return a.mv;
+        }
+    } else {
+        if (idx == 0) {
+            a = mv_nb_blk(nb.left, av.left, 3, 0);
+            b = mv_nb_blk(nb.top, av.top, 0, 3);
+            c = av.top ? mv_nb_blk(nb.top, true, 2, 3) : mv_nb_blk(nb.topleft, av.topleft, 3, 3);
+            if (a.ref == 0) return a.mv;
+        } else {
+            a = own;
+            b = mv_nb_blk(nb.top, av.top, 2, 3);
+            c = av.topright ? mv_nb_blk(nb.topright, true, 0, 3) : mv_nb_blk(nb.top, av.top, 1, 3);
+            if (c.ref == 0) return c.mv;
+        }
+    }
+    return predict_mv16x16(a, b, c);
+}
+
+// P_Skip decision + the motion vector differences of a P macroblock: mvd[0..1] (16x16 or
+// partition 0), mvd[2..3] (partition 1).  Returns true for P_Skip (16x16 only).
+MXHD bool decide_skip(const MbNbrs& nb, const Avail& av, int* mvd) {
     const MbInfo& m = *nb.self;
-    *mvdx = 0;
-    *mvdy = 0;
+    mvd[0] = mvd[1] = mvd[2] = mvd[3] = 0;
     if (m.type != kMbP16x16) return false;
-    const MvNb a = mv_nb(nb.left, av.left);
-    const MvNb b = mv_nb(nb.top, av.top);
-    MvNb c = mv_nb(nb.topright, av.topright);
-    if (!av.topright) c = mv_nb(nb.topleft, av.topleft);
+    if (m.part != kPart16x16) {
+        const Mv v0{m.pmv[0], m.pmv[1]}, v1{m.pmv[2], m.pmv[3]};
+        const Mv p0 = predict_mv_part(nb, av, m.part, 0, v0);
+        const Mv p1 = predict_mv_part(nb, av, m.part, 1, v0);
+        mvd[0] = v0.x - p0.x;
+        mvd[1] = v0.y - p0.y;
+        mvd[2] = v1.x - p1.x;
+        mvd[3] = v1.y - p1.y;
+        return false;
+    }
+    const MvNb a = mv_nb_blk(nb.left, av.left, 3, 0);
+    const MvNb b = mv_nb_blk(nb.top, av.top, 0, 3);
+    MvNb c = mv_nb_blk(nb.topright, av.topright, 0, 3);
+    if (!av.topright) c = mv_nb_blk(nb.topleft, av.topleft, 3, 3);
     const Mv pskip = predict_mv_skip(a, b, c);
     const Mv p = predict_mv16x16(a, b, c);
-    *mvdx = m.mvx - p.x;
-    *mvdy = m.mvy - p.y;
+    mvd[0] = m.mvx - p.x;
+    mvd[1] = m.mvy - p.y;
     return m.cbp == 0 && m.mvx == pskip.x && m.mvy == pskip.y;
 }
 
 template <class W>
 MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbNbrs& nb, const int16_t* mc,
-                    const Avail& av, int mvdx, int mvdy, int dqp = 0) {
+                    const Avail& av, const int* mvd, int dqp = 0) {
     const MbInfo& m = *nb.self;
     const bool intra = m.type == kMbI16x16;  // Intra16x16: DC / AC split of the luma residual
     const int cbp = m.cbp;
@@ -119,9 +176,13 @@ MXHD void code_role(W& w, int role, const Geometry& g, int idr, const MbNbrs& nb
             put_ue(w, (uint32_t)cbp_to_codenum(cbp, true));
             if (cbp) put_se(w, dqp);
         } else {
-            put_ue(w, 0);  // P_L0_16x16
-            put_se(w, mvdx);
-            put_se(w, mvdy);
+            put_ue(w, m.part);  // P_L0_16x16 / P_L0_L0_16x8 / P_L0_L0_8x16 (one reference: no ref_idx)
+            put_se(w, mvd[0]);
+            put_se(w, mvd[1]);
+            if (m.part != kPart16x16) {
+                put_se(w, mvd[2]);
+                put_se(w, mvd[3]);
+            }
             put_ue(w, (uint32_t)cbp_to_codenum(cbp, false));
             if (cbp) put_se(w, dqp);  // mb_qp_delta (adaptive quantisation)
         }
@@ -243,6 +304,12 @@ MXHD bool drop_chroma_for(int aq, int tclass, bool luma_dropped) {
 // compensated residual + mv rate at the frame lambda.
 MXHD uint32_t inter_cost(uint32_t satd, int frame_qp, int mvx, int mvy) {
     return satd + (uint32_t)(lambda_sad(frame_qp) * (mvd_bits(mvx) + mvd_bits(mvy)));
+}
+// ... of a partitioned macroblock: both vectors' rate
+MXHD uint32_t inter_cost_mb(uint32_t satd, int frame_qp, const MbInfo& m) {
+    if (m.part == kPart16x16) return inter_cost(satd, frame_qp, m.mvx, m.mvy);
+    return satd + (uint32_t)(lambda_sad(frame_qp) *
+                             (mvd_bits(m.pmv[0]) + mvd_bits(m.pmv[1]) + mvd_bits(m.pmv[2]) + mvd_bits(m.pmv[3])));
 }
 
 // Rows per slice of an IDR picture: intra macroblocks are reconstructed in a diagonal

@@ -130,6 +130,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     m.search_range = h264::me_range(cfg_.search_range);
     m.me_coarse = cfg_.me_coarse;
     m.subpel = cfg_.subpel;
+    m.partitions = 0;  // HEVC codes 16x16 prediction units from the 16x16 vectors
     m.hp_pitch = hp_pitch_;
     m.hp_f = hp_[0] + org;
     m.hp_h = hp_[1] + org;
