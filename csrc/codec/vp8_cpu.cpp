@@ -7,6 +7,7 @@
 #include <stdexcept>
 
 #include "h264_core.h"
+#include "h264_mb.h"
 #include "vp8_encoder.h"
 
 namespace mx {
@@ -129,6 +130,31 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
             m.nz = code_luma16(res, pred, Q, lv, rec);
             m.nz |= code_chroma8(cres[0], cp[0], Q, lv, crec[0], 16);
             m.nz |= code_chroma8(cres[1], cp[1], Q, lv, crec[1], 20);
+            if (!key) {  // noise-like residual that does not pay for its bits: prediction only
+                uint32_t lsad = 0, bits = 0;
+                long long dp = 0, dc = 0;
+                for (int i = 0; i < 256; ++i) {
+                    const int e = sy[(y0 + i / 16) * pitch + x0 + i % 16] - rec[i];
+                    lsad += (uint32_t)std::abs(res[i]);
+                    dp += res[i] * res[i];
+                    dc += e * e;
+                }
+                for (int b = 0; b < 16; ++b) {
+                    int n = 0;
+                    for (int k = 1; k < 16; ++k) n += lv[b * 16 + k] != 0;
+                    bits += vp8_block_bits(n);
+                }
+                int n2 = 0;
+                for (int k = 0; k < 16; ++k) n2 += lv[kY2 * 16 + k] != 0;
+                bits += vp8_block_bits(n2);
+                if (vp8_drop_residual(lsad, dp, dc, bits, h264::lambda_sse(qp))) {
+                    m.nz = 0;
+                    std::memset(lv, 0, sizeof(int16_t) * kCoefPerMb);
+                    for (int i = 0; i < 256; ++i) rec[i] = pred[i];
+                    for (int c = 0; c < 2; ++c)
+                        for (int i = 0; i < 64; ++i) crec[c][i] = cp[c][i];
+                }
+            }
             for (int y = 0; y < 16; ++y)
                 for (int x = 0; x < 16; ++x) ry[(y0 + y) * cw_ + x0 + x] = (uint8_t)rec[y * 16 + x];
             for (int c = 0; c < 2; ++c)

@@ -92,6 +92,18 @@ MXV8 void mv_bounds(int mb_w, int mb_h, int mbx, int mby, int* lo_x, int* hi_x, 
     *hi_y = (mb_h - 1 - mby) * 16 + 16 - 3;
 }
 
+// Rate-distortion residual drop of noise-like inter macroblocks (the rule of the H.264 encoder's
+// aq 2, h264_mb.h drop_residual): a macroblock whose prediction residual stays above 32 per luma
+// sample on average keeps its residual only if coding it lowers the luma SSE by more than
+// lambda * (estimated bits); else it goes out as prediction only (no tokens, skipped).
+// Incompressible content (the bench desktop's noise panel, video) otherwise takes the bits the
+// rest of the picture needs: VP8 has no per-macroblock quantiser here to send it coarser.
+// bits: sum over the 16 luma blocks (AC levels) and Y2 of 2 + 6 * non-zero levels.
+MXV8 bool vp8_drop_residual(uint32_t lsad, long long d_pred, long long d_coded, uint32_t bits, int lambda) {
+    return lsad > 256u * 32 && d_pred - d_coded < (long long)lambda * (long long)bits;
+}
+MXV8 uint32_t vp8_block_bits(int nz) { return nz ? 2u + 6u * (uint32_t)nz : 0u; }
+
 // Small persistent worker pool for the token partitions.
 class PartitionPool {
    public:
@@ -147,6 +159,7 @@ struct Vp8FrameState {
     int32_t epoch;          // nonzero, new every frame: key-frame wavefront progress tag (20 bits)
     int32_t q[6];           // Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
     uint32_t qm[6];         // ceil(2^32 / (3 q)): the dead-zone quantiser's division as a multiply-high
+    int32_t drop_lambda;    // P frames: lambda_sse of the frame QP for vp8_drop_residual
 };
 // Both per-frame states in one block: one host->device copy per frame.
 struct Vp8States {

@@ -117,6 +117,7 @@ void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
         f.q[i] = q[i];
         f.qm[i] = 0xffffffffu / (uint32_t)(3 * q[i]) + 1u;  // ceil(2^32 / 3q)
     }
+    f.drop_lambda = h264::lambda_sse(qp);
     h264::FrameState& m = s.st_host->me;
     std::memset(&m, 0, sizeof m);
     m.ref_y = rec_y_[ref];

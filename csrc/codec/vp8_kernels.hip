@@ -54,9 +54,13 @@ struct MbLds {
 // Transform, quantise and reconstruct the staged macroblock (s.src / s.pred -> s.rec, levels to
 // lv[400]); returns the non-zero block mask (bit b = block b), wave-uniform.  code_luma16 +
 // code_chroma8 of vp8_core.h, one block per lane.
-__device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restrict__ lv, int lane) {
+// drop_lambda >= 0 (inter macroblocks): vp8_drop_residual may turn the macroblock into prediction
+// only (levels zero, reconstruction = prediction) -- the decision is wave-uniform.
+__device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restrict__ lv, int lane,
+                            int drop_lambda = -1) {
     int lvl[16], dq[16];
     bool nz = false;
+    int st_lsad = 0, st_dp = 0, st_dc = 0, st_bits = 0;  // drop statistics (luma lanes, Y2 lane)
     const bool luma = lane < 16, chroma = lane >= 16 && lane < 24;
 #pragma unroll
     for (int k = 0; k < 16; ++k) lvl[k] = dq[k] = 0;
@@ -83,6 +87,12 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
                     in[i * 4 + j] = (int)S[o] - (int)P[o];
                 }
         }
+        if (luma)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                st_lsad += in[k] < 0 ? -in[k] : in[k];
+                st_dp += in[k] * in[k];
+            }
         int coef[16];
         fdct4x4(in, coef);
         if (luma) s.dc[lane] = coef[0];
@@ -116,6 +126,10 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
         iwht4x4(y2q, dcr);
 #pragma unroll
         for (int b = 0; b < 16; ++b) s.dcr[b] = dcr[b];
+        int n = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) n += lvl[k] != 0;
+        st_bits = (int)vp8_block_bits(n);
     }
     __syncthreads();
     if (luma || chroma) {
@@ -129,8 +143,15 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int o = (by * 4 + i) * 16 + bx * 4 + j;
-                    s.rec[o] = (uint8_t)v8_clamp255((int)s.pred[o] + r[i * 4 + j]);
+                    const int v = v8_clamp255((int)s.pred[o] + r[i * 4 + j]);
+                    s.rec[o] = (uint8_t)v;
+                    const int e = (int)s.src[o] - v;
+                    st_dc += e * e;
                 }
+            int n = 0;
+#pragma unroll
+            for (int k = 1; k < 16; ++k) n += lvl[k] != 0;
+            st_bits = (int)vp8_block_bits(n);
         } else {
             const int b = (lane - 16) & 3, bx = b & 1, by = b >> 1;
             const uint8_t* P = lane < 20 ? s.pu : s.pv;
@@ -141,6 +162,37 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
                 for (int j = 0; j < 4; ++j) {
                     const int o = (by * 4 + i) * 8 + bx * 4 + j;
                     R[o] = (uint8_t)v8_clamp255((int)P[o] + r[i * 4 + j]);
+                }
+        }
+    }
+    bool drop = false;
+    if (drop_lambda >= 0) {  // wave-uniform
+        const uint32_t lsad = (uint32_t)wsum(st_lsad), bits = (uint32_t)wsum(st_bits);
+        drop = vp8_drop_residual(lsad, (long long)wsum(st_dp), (long long)wsum(st_dc), bits, drop_lambda);
+    }
+    if (drop) {
+        nz = false;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) lvl[k] = 0;
+        if (luma) {
+            const int bx = lane & 3, by = lane >> 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = (by * 4 + i) * 16 + bx * 4 + j;
+                    s.rec[o] = s.pred[o];
+                }
+        } else if (chroma) {
+            const int b = (lane - 16) & 3, bx = b & 1, by = b >> 1;
+            const uint8_t* P = lane < 20 ? s.pu : s.pv;
+            uint8_t* R = lane < 20 ? s.ru : s.rv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = (by * 4 + i) * 8 + bx * 4 + j;
+                    R[o] = P[o];
                 }
         }
     }
@@ -302,7 +354,7 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
         s.pv[cy * 8 + cx] = (uint8_t)chroma_px(at_v, px, py, cvx & 7, cvy & 7);
     }
     __syncthreads();
-    const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane);
+    const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, F.drop_lambda);
     uint32_t sse[3];
     store_rec(s, g, F, x0, y0, lane, sse);
     store_record(mbs + mbi, mvx, mvy, kInter, kDcPred, nz, sse, lane);
