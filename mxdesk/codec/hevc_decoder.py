@@ -12,8 +12,9 @@ Supported: VPS/SPS/PPS (incl. VUI), I and P slices (one reference picture, short
 from the SPS), coding quadtrees with split_cu_flag, PartMode 2Nx2N (intra and inter),
 transform trees with split_transform_flag, residual coding for 4x4..32x32 TUs (scanIdx
 0/1/2, no sign hiding, no transform skip), cu_qp_delta, conformance window cropping.
-The in-loop deblocking filter (8.7.2) is implemented; SAO must be disabled and TMVP off
-(mxdesk's encoder guarantees both); anything else raises ``NotImplementedError``.  Slow; meant for small test pictures.
+Both in-loop filters are implemented: deblocking (8.7.2) and sample adaptive offset (8.7.3,
+band and edge offsets with CTB merge-left/up, 7.3.8.3).  TMVP must be off (mxdesk's encoder
+guarantees it); anything else raises ``NotImplementedError``.  Slow; meant for small test pictures.
 """
 from __future__ import annotations
 
@@ -87,6 +88,8 @@ _INIT = {
          154, 152, 167, 182]),
     "coeff_abs_level_greater2_flag": ([138, 153, 136, 167, 152, 152], [107, 167, 91, 122, 107, 167],
                                       [107, 167, 91, 107, 107, 167]),
+    "sao_merge_flag": ([153], [153], [153]),       # sao_merge_left_flag and sao_merge_up_flag share it
+    "sao_type_idx": ([200], [185], [160]),          # first bin of sao_type_idx_luma / _chroma
 }
 _INIT["last_sig_coeff_y_prefix"] = _INIT["last_sig_coeff_x_prefix"]
 
@@ -101,6 +104,9 @@ _LEVEL_SCALE = [40, 45, 51, 57, 64, 72]
 # deblocking beta' (Table 8-12, Q = 0..51) and tC' (Q = 0..53)
 _DB_BETA = [0] * 16 + [6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18] + list(range(20, 66, 2))
 _DB_TC = [0] * 18 + [1] * 9 + [2] * 4 + [3] * 4 + [4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24]
+# SAO edge classes (Table 8-13 hPos/vPos): neighbours a, b of each sample
+_SAO_EO_NB = [((-1, 0), (1, 0)), ((0, -1), (0, 1)), ((-1, -1), (1, 1)), ((1, -1), (-1, 1))]
+_SAO_EDGE_CAT = np.array([1, 2, 0, 3, 4])  # edgeIdx 2 + sign + sign -> offset category (8.7.3.2)
 _QPC_TABLE = {30: 29, 31: 30, 32: 31, 33: 32, 34: 33, 35: 33, 36: 34, 37: 34, 38: 35, 39: 35, 40: 36, 41: 36,
               42: 37, 43: 37}
 
@@ -578,6 +584,8 @@ class Decoder:
         p = self.cur
         if any(not sp["db_disabled"] for sp in self.slice_params.values()):
             self._deblock()
+        if self.sao_params:
+            self._sao()
         self.frames_coded.append((p.y.copy(), p.u.copy(), p.v.copy()))
         l, r, t, b = s.conf
         h, w = p.y.shape
@@ -585,6 +593,96 @@ class Decoder:
                             p.u[t:h // 2 - b, l:w // 2 - r].copy(), p.v[t:h // 2 - b, l:w // 2 - r].copy()))
         self.ref = p
         self.cur = None
+
+    # ---------------------------------------------------------------- SAO (8.7.3)
+    def _sao(self) -> None:
+        """Sample adaptive offset over the deblocked picture: every CTB reads the deblocked
+        samples (never an already offset neighbour) and writes the output picture."""
+        s = self.sps
+        ctbs_w = (s.width + (1 << s.log2_ctb) - 1) >> s.log2_ctb
+        planes = (self.cur.y, self.cur.u, self.cur.v)
+        src = [pl.copy() for pl in planes]
+        for ctb, params in self.sao_params.items():
+            cx, cy = ctb % ctbs_w, ctb // ctbs_w
+            x_l, y_l = cx << s.log2_ctb, cy << s.log2_ctb
+            prm = self.slice_params[int(self.slice_map[y_l >> 2, x_l >> 2])]
+            for c in range(3):
+                if not (prm["sao_luma"] if c == 0 else prm["sao_chroma"]):
+                    continue
+                typ, off, band, eo = params[c]
+                if typ == 0:
+                    continue
+                sh = 0 if c == 0 else 1
+                pic = src[c]
+                H, W = pic.shape
+                sz = 1 << (s.log2_ctb - sh)
+                x0, y0 = cx * sz, cy * sz
+                x1, y1 = min(x0 + sz, W), min(y0 + sz, H)
+                blk = pic[y0:y1, x0:x1]
+                if typ == 1:  # band offset: four consecutive bands of width 8 from sao_band_position
+                    table = np.zeros(32, np.int32)
+                    for k in range(4):
+                        table[(k + band) & 31] = off[k]
+                    delta = table[blk >> 3]
+                else:  # edge offset along class eo
+                    ys, xs = np.mgrid[y0:y1, x0:x1]
+                    cur_sid = self.slice_map[(ys << sh) >> 2, (xs << sh) >> 2]
+                    valid = np.ones(blk.shape, bool)
+                    signs = 2
+                    for dx, dy in _SAO_EO_NB[eo]:
+                        ny, nx = ys + dy, xs + dx
+                        inside = (ny >= 0) & (ny < H) & (nx >= 0) & (nx < W)
+                        nyc, nxc = np.clip(ny, 0, H - 1), np.clip(nx, 0, W - 1)
+                        nb_sid = self.slice_map[(nyc << sh) >> 2, (nxc << sh) >> 2]
+                        # across a slice border the later slice's slice_loop_filter_across_slices_enabled_flag rules
+                        later = np.maximum(cur_sid, nb_sid)
+                        across = np.vectorize(lambda a: self.slice_params[int(a)]["lf_across"])(later) if (
+                            (nb_sid != cur_sid).any()) else np.ones(blk.shape, np.int32)
+                        valid &= inside & ((nb_sid == cur_sid) | (across != 0))
+                        signs = signs + np.sign(blk - pic[nyc, nxc])
+                    offv = np.array([0, off[0], off[1], off[2], off[3]], np.int32)
+                    delta = np.where(valid, offv[_SAO_EDGE_CAT[signs]], 0)
+                planes[c][y0:y1, x0:x1] = np.clip(blk + delta, 0, 255)
+
+    def _sao_syntax(self, cab: Cabac, ctb: int, ctbs_w: int, slice_addr: int, luma: int, chroma: int) -> None:
+        """sao(rx, ry) (7.3.8.3): merge left / up, else per component type, offsets, band
+        position or edge class.  Stored as (SaoTypeIdx, SaoOffsetVal[1..4], band, eo_class)."""
+        rx, ry = ctb % ctbs_w, ctb // ctbs_w
+        if rx > 0 and ctb - 1 >= slice_addr and cab.decision("sao_merge_flag"):
+            self.sao_params[ctb] = self.sao_params[ctb - 1]
+            return
+        if ry > 0 and ctb - ctbs_w >= slice_addr and cab.decision("sao_merge_flag"):
+            self.sao_params[ctb] = self.sao_params[ctb - ctbs_w]
+            return
+        out = []
+        for c in range(3):
+            if not (luma if c == 0 else chroma):
+                out.append((0, (0, 0, 0, 0), 0, 0))
+                continue
+            if c == 2:
+                typ, eo = out[1][0], out[1][3]
+            else:
+                typ = 0 if not cab.decision("sao_type_idx") else (1 if not cab.bypass() else 2)
+                eo = 0
+            if typ == 0:
+                out.append((0, (0, 0, 0, 0), 0, 0))
+                continue
+            absv = []
+            for _ in range(4):  # TR, cMax = (1 << (min(bitDepth, 10) - 5)) - 1 = 7, bypass
+                v = 0
+                while v < 7 and cab.bypass():
+                    v += 1
+                absv.append(v)
+            band = 0
+            if typ == 1:
+                offs = tuple(-a if a and cab.bypass() else a for a in absv)
+                band = cab.bypass_bits(5)
+            else:
+                offs = (absv[0], absv[1], -absv[2], -absv[3])
+                if c < 2:
+                    eo = cab.bypass_bits(2)
+            out.append((typ, offs, band, eo))
+        self.sao_params[ctb] = tuple(out)
 
     # ---------------------------------------------------------------- deblocking (8.7.2)
     def _deblock(self) -> None:
@@ -737,11 +835,13 @@ class Decoder:
             self.edge_v = np.zeros(n4, bool)     # transform/prediction edge on the left of the 4x4 block
             self.edge_h = np.zeros(n4, bool)     # ... on the top
             self.slice_params = {}
+            self.sao_params = {}
             self.prev_poc_tid0 = poc
         elif self.cur is None:
             raise ValueError("slice of a picture whose first slice is missing")
-        if s.sao and (r.u(1) | r.u(1)):
-            raise NotImplementedError("SAO")
+        sao_luma = sao_chroma = 0
+        if s.sao:
+            sao_luma, sao_chroma = r.u(1), r.u(1)
         max_merge = 5
         if slice_type != 2:
             if slice_type != 1:
@@ -770,9 +870,10 @@ class Decoder:
             raise NotImplementedError("deblocking override")
         db_disabled = p.deblocking_disabled
         lf_across = p.loop_filter_across_slices
-        if p.loop_filter_across_slices and not db_disabled:  # (no SAO)
+        if p.loop_filter_across_slices and (sao_luma or sao_chroma or not db_disabled):
             lf_across = r.u(1)
         self.slice_params[addr] = {"db_disabled": db_disabled, "lf_across": lf_across,
+                                   "sao_luma": sao_luma, "sao_chroma": sao_chroma,
                                    "beta_offset": 2 * p.beta_offset_div2, "tc_offset": 2 * p.tc_offset_div2}
         r.byte_alignment()
         self.stats["slices"] += 1
@@ -785,6 +886,8 @@ class Decoder:
         ctb = addr
         while True:
             cx, cy = ctb % ctbs_w, ctb // ctbs_w
+            if sao_luma or sao_chroma:
+                self._sao_syntax(cab, ctb, ctbs_w, addr, sao_luma, sao_chroma)
             self._coding_quadtree(cab, cx << s.log2_ctb, cy << s.log2_ctb, s.log2_ctb, 0)
             if cab.terminate():
                 cab.check_slice_end()
