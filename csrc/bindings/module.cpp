@@ -162,7 +162,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("mask_y1", &h264::EncoderConfig::mask_y1)
         .def_readwrite("deblock", &h264::EncoderConfig::deblock)
         .def_readwrite("partitions", &h264::EncoderConfig::partitions)
-        .def_readwrite("tu_split", &h264::EncoderConfig::tu_split);
+        .def_readwrite("tu_split", &h264::EncoderConfig::tu_split)
+        .def_readwrite("sao", &h264::EncoderConfig::sao);
 
     py::class_<h264::FrameStats>(m, "FrameStats")
         .def_readonly("frame_index", &h264::FrameStats::frame_index)
@@ -384,6 +385,19 @@ PYBIND11_MODULE(_native, m) {
                  std::vector<int> t;
                  for (const auto& c : e.cus()) t.push_back(c.type);
                  return t;
+             })
+        .def("cu_info",  // (type, qp, cbf, tu_split) per CU of the last picture
+             [](hevc::CpuHevcEncoder& e) {
+                 const auto& cus = e.cus();
+                 py::array_t<int32_t> a({(py::ssize_t)cus.size(), (py::ssize_t)4});
+                 auto m = a.mutable_unchecked<2>();
+                 for (size_t i = 0; i < cus.size(); ++i) {
+                     m(i, 0) = cus[i].type;
+                     m(i, 1) = cus[i].qp;
+                     m(i, 2) = cus[i].cbf;
+                     m(i, 3) = cus[i].tu_split;
+                 }
+                 return a;
              })
         .def_property_readonly("slice_rows", [](hevc::CpuHevcEncoder& e) { return e.common().slice_rows(); })
         .def_property_readonly("level_idc", [](hevc::CpuHevcEncoder& e) { return e.common().level_idc(); })

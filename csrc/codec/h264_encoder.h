@@ -41,7 +41,9 @@ struct EncoderConfig {
     int aq = 3;               // adaptive quantisation of P macroblocks (mb_qp_delta): 1 coarser QP for
                               // noise-like residuals, 2 adds their rate-distortion residual drop, 3 (H.264
                               // default) temporal classes of the source -- persistent content finer, changing
-                              // content coarser (h264_mb.h temporal_class; HEVC treats 3 as 2)
+                              // content coarser, its chroma dropped and its luma residual kept only when it
+                              // pays for its bits (h264_mb.h temporal_class; HEVC has 0, 1 and 3, and treats
+                              // 2 as 1)
     // in-loop deblocking filter: 1 on, 0 off, -1 the codec's default -- HEVC on (8.7.2, fully
     // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it cost
     // 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)
@@ -54,6 +56,7 @@ struct EncoderConfig {
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
+    int sao = 1;              // HEVC: sample adaptive offset (8.7.3), band / edge offsets decided per CTB
     // quality report: luma distortion outside the macroblocks touching this pixel rectangle
     // (FrameStats::sse_masked; mask_x1 <= mask_x0 = no mask)
     int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;

@@ -410,7 +410,9 @@ enum Ctx : int {
     C_GT2 = 130,           // 6
     C_SPLIT_TRANSFORM = 136,  // 3
     C_SPLIT_CU = 139,      // 3
-    C_NUM = 142
+    C_SAO_MERGE = 142,     // 1 (sao_merge_left_flag and sao_merge_up_flag)
+    C_SAO_TYPE = 143,      // 1 (first bin of sao_type_idx_luma / _chroma)
+    C_NUM = 144
 };
 
 // initValue per initType (0: I, 1: P without cabac_init_flag, 2: B), Tables 9-5..9-37
@@ -432,7 +434,8 @@ constexpr uint8_t kCtxInit[3][C_NUM] = {
      122, 197,
      138, 153, 136, 167, 152, 152,
      153, 138, 138,
-     139, 141, 157},
+     139, 141, 157,
+     153, 200},
     {// P (initType 1)
      197, 185, 201,
      110, 122, 149,
@@ -450,7 +453,8 @@ constexpr uint8_t kCtxInit[3][C_NUM] = {
      137, 182,
      107, 167, 91, 122, 107, 167,
      124, 138, 94,
-     107, 139, 126},
+     107, 139, 126,
+     153, 185},
     {// B (initType 2)
      197, 185, 201,
      154, 137, 134,
@@ -468,7 +472,8 @@ constexpr uint8_t kCtxInit[3][C_NUM] = {
      167, 182,
      107, 167, 91, 107, 107, 167,
      224, 167, 122,
-     107, 139, 126}};
+     107, 139, 126,
+     153, 160}};
 
 // Context state byte: (pStateIdx << 1) | valMps (9.3.2.2)
 MXHD uint8_t ctx_init_state(int init_value, int qp) {
@@ -1064,10 +1069,238 @@ MXHD void code_cu(CabacEnc& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf&
     e.terminate(end_of_slice ? 1 : 0);
 }
 
+// ---------------------------------------------------------------- sample adaptive offset (8.7.3)
+// Decided per CTB on the deblocked picture: for every component the rate-distortion best of
+// off / band offset (four consecutive 8-wide bands) / edge offset (classes 0..3), with offsets
+// from the rounded mean error of each category, shortened toward 0 while that lowers
+// 16 * dSSE + lambda16 * bits (kLambdaSse16).  Cb and Cr share the type and edge class.  The
+// choice depends on the CTB's own statistics only, and sao_merge_left / _up are sent exactly when
+// the neighbour's parameters are identical -- so the decision is CTB-parallel on the GPU and
+// merging never changes a CTB's parameters.
+//
+// One component's parameters in a word: bits 0-1 SaoTypeIdx (0 off, 1 band, 2 edge), 2-3 edge
+// class, 4-8 sao_band_position, 12 + 4k .. 15 + 4k SaoOffsetVal[k + 1] (4-bit two's complement).
+MXHD uint32_t sao_pack(int type, int eo, int band, const int* off) {
+    uint32_t w = (uint32_t)type | ((uint32_t)eo << 2) | ((uint32_t)band << 4);
+    for (int k = 0; k < 4; ++k) w |= ((uint32_t)off[k] & 15u) << (12 + 4 * k);
+    return w;
+}
+MXHD int sao_type(uint32_t w) { return (int)(w & 3); }
+MXHD int sao_eo(uint32_t w) { return (int)((w >> 2) & 3); }
+MXHD int sao_band(uint32_t w) { return (int)((w >> 4) & 31); }
+MXHD int sao_off(uint32_t w, int k) { return (int)(w << (16 - 4 * k)) >> 28; }
+
+// edge classes (Table 8-13 hPos / vPos): neighbours a = (x + dx[0], y + dy[0]), b = (x + dx[1], ..)
+constexpr int8_t kSaoDx[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
+constexpr int8_t kSaoDy[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
+// edge category 0..4 of sample c between a and b (8.7.3.2: edgeIdx 0,1,2 -> 1,2,0)
+MXHD int sao_edge_cat(int c, int a, int b) {
+    const int e = 2 + ((c > a) - (c < a)) + ((c > b) - (c < b));
+    return e == 2 ? 0 : (e < 2 ? e + 1 : e);
+}
+
+// One component of one CTB: sums of (source - deblocked) and sample counts per edge class and
+// category (1..4 -> index 0..3), and per band (sample >> 3).
+struct SaoStats {
+    int32_t eo_sum[4][4];
+    int32_t eo_cnt[4][4];
+    int32_t bo_sum[32];
+    int32_t bo_cnt[32];
+};
+
+// Statistics of the n x n block at (x0, y0) of a W x H plane: rec / src at (x, y) are
+// p[y * pitch + x * step] (step 2: one component of interleaved chroma).  Samples whose
+// neighbour lies outside the picture are not modified by an edge class (8.7.3.2) and are left
+// out of its statistics.
+MXHD void sao_stats_block(const uint8_t* rec, int rpitch, const uint8_t* src, int spitch, int step, int x0, int y0,
+                          int n, int W, int H, SaoStats& st) {
+    for (int k = 0; k < 4; ++k)
+        for (int c = 0; c < 4; ++c) st.eo_sum[k][c] = st.eo_cnt[k][c] = 0;
+    for (int b = 0; b < 32; ++b) st.bo_sum[b] = st.bo_cnt[b] = 0;
+    for (int y = y0; y < y0 + n; ++y)
+        for (int x = x0; x < x0 + n; ++x) {
+            const int c = rec[y * rpitch + x * step];
+            const int d = (int)src[y * spitch + x * step] - c;
+            st.bo_sum[c >> 3] += d;
+            st.bo_cnt[c >> 3] += 1;
+            for (int k = 0; k < 4; ++k) {
+                const int ax = x + kSaoDx[k][0], ay = y + kSaoDy[k][0], bx = x + kSaoDx[k][1], by = y + kSaoDy[k][1];
+                if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= W || bx >= W || ay >= H || by >= H) continue;
+                const int cat = sao_edge_cat(c, rec[ay * rpitch + ax * step], rec[by * rpitch + bx * step]);
+                if (cat) {
+                    st.eo_sum[k][cat - 1] += d;
+                    st.eo_cnt[k][cat - 1] += 1;
+                }
+            }
+        }
+}
+
+MXHD int sao_offset_bits(int a) { return a < 7 ? a + 1 : 7; }  // sao_offset_abs: TR, cMax 7, bypass
+// Best offset in [lo, hi] for a category / band with error sum s over n samples: start at the
+// rounded mean, step toward 0, keep the lowest 16 * (n o^2 - 2 o s) + lambda16 * bits (o = 0:
+// no distortion change, one bin).  Returns that cost.
+MXHD long long sao_best_offset(int s, int n, int lo, int hi, bool sign_bit, uint32_t lam16, int* o_out) {
+    int o = 0;
+    if (n > 0) o = s >= 0 ? (s + n / 2) / n : -((-s + n / 2) / n);
+    o = o < lo ? lo : (o > hi ? hi : o);
+    long long best = (long long)lam16;
+    int best_o = 0;
+    for (int v = o; v != 0; v += v > 0 ? -1 : 1) {
+        const int a = v < 0 ? -v : v;
+        const long long j = 16LL * ((long long)n * v * v - 2LL * v * s) +
+                            (long long)lam16 * (sao_offset_bits(a) + (sign_bit ? 1 : 0));
+        if (j < best) {
+            best = j;
+            best_o = v;
+        }
+    }
+    *o_out = best_o;
+    return best;
+}
+
+// Per-component candidates: each edge class with its four offsets, and the best band window.
+struct SaoCompChoice {
+    long long j_eo[4];
+    long long j_bo;
+    int eo_off[4][4];
+    int bo_off[4];
+    int band;
+};
+MXHD void sao_eval_comp(const SaoStats& st, uint32_t lam16, SaoCompChoice& ch) {
+    for (int k = 0; k < 4; ++k) {
+        long long j = 0;
+        for (int c = 0; c < 4; ++c)  // categories 1, 2 (valleys) positive, 3, 4 (peaks) negative
+            j += sao_best_offset(st.eo_sum[k][c], st.eo_cnt[k][c], c < 2 ? 0 : -7, c < 2 ? 7 : 0, false, lam16,
+                                 &ch.eo_off[k][c]);
+        ch.j_eo[k] = j;
+    }
+    long long jb[32];
+    int ob[32];
+    for (int b = 0; b < 32; ++b) jb[b] = sao_best_offset(st.bo_sum[b], st.bo_cnt[b], -7, 7, true, lam16, &ob[b]);
+    ch.j_bo = 0;
+    ch.band = 0;
+    for (int p = 0; p < 32; ++p) {
+        const long long j = jb[p] + jb[(p + 1) & 31] + jb[(p + 2) & 31] + jb[(p + 3) & 31];
+        if (p == 0 || j < ch.j_bo) {
+            ch.j_bo = j;
+            ch.band = p;
+        }
+    }
+    for (int k = 0; k < 4; ++k) ch.bo_off[k] = ob[(ch.band + k) & 31];
+}
+// Final parameters of a CTB (w[0] luma, w[1] Cb, w[2] Cr) from the three components' candidates.
+// Syntax bits beyond the offsets: type (1 context bin + 1 bypass), band position 5, edge class 2.
+MXHD void sao_combine(const SaoCompChoice& y, const SaoCompChoice& cb, const SaoCompChoice& cr, uint32_t lam16,
+                      uint32_t* w) {
+    const int zero[4] = {0, 0, 0, 0};
+    {
+        long long best = (long long)lam16;  // off: one bin
+        w[0] = 0;
+        const long long jb = y.j_bo + (long long)lam16 * 7;
+        if (jb < best) {
+            best = jb;
+            w[0] = sao_pack(1, 0, y.band, y.bo_off);
+        }
+        for (int k = 0; k < 4; ++k) {
+            const long long je = y.j_eo[k] + (long long)lam16 * 4;
+            if (je < best) {
+                best = je;
+                w[0] = sao_pack(2, k, 0, y.eo_off[k]);
+            }
+        }
+    }
+    long long best = (long long)lam16;
+    w[1] = sao_pack(0, 0, 0, zero);
+    w[2] = w[1];
+    const long long jb = cb.j_bo + cr.j_bo + (long long)lam16 * 12;
+    if (jb < best) {
+        best = jb;
+        w[1] = sao_pack(1, 0, cb.band, cb.bo_off);
+        w[2] = sao_pack(1, 0, cr.band, cr.bo_off);
+    }
+    for (int k = 0; k < 4; ++k) {
+        const long long je = cb.j_eo[k] + cr.j_eo[k] + (long long)lam16 * 4;
+        if (je < best) {
+            best = je;
+            w[1] = sao_pack(2, k, 0, cb.eo_off[k]);
+            w[2] = sao_pack(2, k, 0, cr.eo_off[k]);
+        }
+    }
+}
+
+// SAO output of sample c (deblocked) with parameters w; a / b: its class-eo neighbours, or -1
+// when one lies outside the picture (edge offset: unmodified).
+MXHD int sao_sample(uint32_t w, int c, int a, int b) {
+    const int type = sao_type(w);
+    int o = 0;
+    if (type == 1) {
+        const int k = ((c >> 3) - sao_band(w)) & 31;
+        o = k < 4 ? sao_off(w, k) : 0;
+    } else if (type == 2 && a >= 0 && b >= 0) {
+        const int cat = sao_edge_cat(c, a, b);
+        o = cat ? sao_off(w, cat - 1) : 0;
+    }
+    const int v = c + o;
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+// Apply w to the n x n block at (x0, y0): reads the deblocked plane rec, writes out (a different
+// buffer: every CTB reads its neighbours' deblocked samples).
+MXHD void sao_apply_block(const uint8_t* rec, uint8_t* out, int pitch, int step, int x0, int y0, int n, int W, int H,
+                          uint32_t w) {
+    const int k = sao_eo(w);
+    for (int y = y0; y < y0 + n; ++y)
+        for (int x = x0; x < x0 + n; ++x) {
+            const int ax = x + kSaoDx[k][0], ay = y + kSaoDy[k][0], bx = x + kSaoDx[k][1], by = y + kSaoDy[k][1];
+            const bool in = ax >= 0 && ay >= 0 && bx >= 0 && by >= 0 && ax < W && bx < W && ay < H && by < H;
+            const int a = in ? rec[ay * pitch + ax * step] : -1, b = in ? rec[by * pitch + bx * step] : -1;
+            out[y * pitch + x * step] = (uint8_t)sao_sample(w, rec[y * pitch + x * step], a, b);
+        }
+}
+
+// sao(rx, ry) syntax (7.3.8.3) of a CTB with parameters p[3]; left / up: the neighbour CTB's
+// parameters when it is in the slice (else nullptr).
+template <class Ctx>
+MXHD void code_sao(CabacEnc& e, Ctx& ctx, const uint32_t* p, const uint32_t* left, const uint32_t* up) {
+    if (left) {
+        const bool m = left[0] == p[0] && left[1] == p[1] && left[2] == p[2];
+        e.bin(ctx, C_SAO_MERGE, m ? 1 : 0);
+        if (m) return;
+    }
+    if (up) {
+        const bool m = up[0] == p[0] && up[1] == p[1] && up[2] == p[2];
+        e.bin(ctx, C_SAO_MERGE, m ? 1 : 0);
+        if (m) return;
+    }
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t w = p[c];
+        const int type = sao_type(w);
+        if (c < 2) {
+            e.bin(ctx, C_SAO_TYPE, type != 0 ? 1 : 0);
+            if (type) e.bypass(type == 2 ? 1 : 0);
+        }
+        if (!type) continue;
+        for (int k = 0; k < 4; ++k) {
+            const int o = sao_off(w, k), a = o < 0 ? -o : o;
+            if (a < 7)
+                e.bypass_bits(((1u << a) - 1u) << 1, a + 1);  // a ones, then a zero
+            else
+                e.bypass_bits(0x7fu, 7);
+        }
+        if (type == 1) {
+            for (int k = 0; k < 4; ++k)
+                if (sao_off(w, k)) e.bypass(sao_off(w, k) < 0 ? 1 : 0);
+            e.bypass_bits((uint32_t)sao_band(w), 5);
+        } else if (c < 2) {
+            e.bypass_bits((uint32_t)sao_eo(w), 2);
+        }
+    }
+}
+
+
 // Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row).
 // Returns the number of payload bytes (> cap means overflow).
 MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
-                         int first, int count, int ctb_w, uint8_t* ctx_mem) {
+                         int first, int count, int ctb_w, uint8_t* ctx_mem, const uint32_t* sao = nullptr) {
     ctx_init_all(ctx_mem, islice ? 0 : 1, slice_qp);
     ArrCtx ctx{ctx_mem};
     CabacEnc e;
@@ -1079,6 +1312,9 @@ MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, 
         const CuInfo* left = (x > 0 && k > 0) ? &cus[i - 1] : nullptr;
         const CuInfo* above = (k >= ctb_w) ? &cus[i - ctb_w] : nullptr;
         const CoefArray cf{coef + (size_t)i * kCoefPerCu};
+        if (sao)  // sao parameters: 4 words per CTB (luma, Cb, Cr, unused)
+            code_sao(e, ctx, sao + 4 * (size_t)i, (x > 0 && k > 0) ? sao + 4 * (size_t)(i - 1) : nullptr,
+                     k >= ctb_w ? sao + 4 * (size_t)(i - ctb_w) : nullptr);
         code_cu(e, ctx, islice, cus[i], cf, cu_nb(left, above), qp_prev, k == count - 1);
     }
     e.finish_slice();
@@ -1486,6 +1722,7 @@ MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, 
     else
         db_luma_seg(ry + (size_t)(y * 16 + 8) * pitch + x * 16 + seg * 4, pitch, 1, 1, qpy[i], qpy[i]);
 }
+
 
 // ---------------------------------------------------------------- inter transform-tree decision
 // ---------------------------------------------------------------- adaptive slice layout (P)

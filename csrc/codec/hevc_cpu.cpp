@@ -181,7 +181,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.ue(0);  // max_transform_hierarchy_depth_intra
         w.put(0, 1);  // scaling_list_enabled_flag
         w.put(0, 1);  // amp_enabled_flag
-        w.put(0, 1);  // sample_adaptive_offset_enabled_flag
+        w.put(c.sao ? 1 : 0, 1);  // sample_adaptive_offset_enabled_flag
         w.put(0, 1);  // pcm_enabled_flag
         w.ue(1);      // num_short_term_ref_pic_sets
         w.ue(1);      // st_ref_pic_set(0): num_negative_pics
@@ -241,7 +241,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.put(0, 1);  // tiles_enabled_flag
         w.put(0, 1);  // entropy_coding_sync_enabled_flag
         const bool db = c.hevc_deblock();
-        w.put(db, 1);  // pps_loop_filter_across_slices_enabled_flag (CU edges on slice borders too)
+        w.put(db || c.sao, 1);  // pps_loop_filter_across_slices_enabled_flag (CU edges on slice borders too)
         w.put(1, 1);   // deblocking_filter_control_present_flag
         w.put(0, 1);   //   deblocking_filter_override_enabled_flag
         w.put(!db, 1);  //   pps_deblocking_filter_disabled_flag
@@ -276,12 +276,17 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
         w.put((uint32_t)(poc & 255), 8);  // slice_pic_order_cnt_lsb
         w.put(1, 1);                      // short_term_ref_pic_set_sps_flag
     }
+    const bool sao = config().sao != 0;
+    if (sao) {
+        w.put(1, 1);  // slice_sao_luma_flag
+        w.put(1, 1);  // slice_sao_chroma_flag
+    }
     if (!idr) {
         w.put(0, 1);  // num_ref_idx_active_override_flag
         w.ue(4);      // five_minus_max_num_merge_cand -> MaxNumMergeCand 1
     }
     w.se(qp - 26);  // slice_qp_delta
-    if (config().hevc_deblock()) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
+    if (config().hevc_deblock() || sao) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
     w.trailing();   // byte_alignment()
     std::vector<uint8_t> rbsp = std::move(w.b);
     rbsp.insert(rbsp.end(), data, data + n);
@@ -411,8 +416,19 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                     res[r * 16 + q] = sy[(y0 + r) * pitch + x0 + q] - p;
                     lsad += (uint32_t)std::abs(res[r * 16 + q]);
                 }
-            const int qp = h264::aq_mb_qp(fqp, lsad, cfg_.aq);
+            // temporal class (aq 3): the source's change against the previous source, displaced by
+            // the integer part of the vector
+            uint32_t tsad = 0;
+            if (cfg_.aq >= 3 && !prev_src_.empty())
+                for (int r = 0; r < 16; ++r)
+                    for (int q = 0; q < 16; ++q)
+                        tsad += (uint32_t)std::abs((int)sy[(y0 + r) * pitch + x0 + q] -
+                                                   h264::ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + q + (c.mvx >> 2),
+                                                                y0 + r + (c.mvy >> 2)));
+            const int tcls = h264::temporal_class(tsad);
+            const int qp = h264::mb_qp_for(fqp, lsad, tcls, cfg_.aq);
             const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+            const bool changing = cfg_.aq >= 3 && tcls == h264::kTcChanging;
             c.qp = (uint8_t)qp;
             int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
             int pc[2][64], rc[2][64];
@@ -422,7 +438,7 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                     for (int q = 0; q < 8; ++q) {
                         const int p = chroma_mc(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc + q, yc + r, c.mvx, c.mvy);
                         pc[comp][r * 8 + q] = p;
-                        rc[comp][r * 8 + q] = suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
+                        rc[comp][r * 8 + q] = changing ? 0 : suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
                     }
             // option 1: one 16x16 luma TU, 8x8 chroma TUs
             int rrc[2][64];
@@ -454,6 +470,25 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                     std::memcpy(co, co2, sizeof co2);
                     std::memcpy(rr, rr2, sizeof rr2);
                     std::memcpy(rrc, rrc2, sizeof rrc2);
+                }
+            }
+            if (changing) {
+                // rate-distortion residual drop (h264_mb.h drop_luma_for): the luma residual must
+                // lower the distortion by more than lambda * (estimated bits of the chosen tree)
+                long long d_pred = 0, d_coded = 0;
+                for (int k = 0; k < 256; ++k) {
+                    const int e = pred[k] + res[k] - clip255(pred[k] + rr[k]);
+                    d_pred += res[k] * res[k];
+                    d_coded += e * e;
+                }
+                uint32_t bits = 0;
+                if (c.tu_split == 2)
+                    for (int k = 0; k < 4; ++k) bits += tu_bits_est(co + 64 * k, 64);
+                else
+                    bits = tu_bits_est(co, 256);
+                if (h264::drop_luma_for(cfg_.aq, lsad, tcls, qp, d_pred, d_coded, bits)) {
+                    for (int k = 0; k < 256; ++k) co[k] = 0, rr[k] = 0;
+                    c.tu_split = cfg_.tu_split ? 1 : 0;
                 }
             }
             for (int r = 0; r < 16; ++r)
@@ -523,6 +558,27 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
                     db_internal_seg(rec_y_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir, seg);
                 }
     }
+    if (cfg_.sao) {  // SAO per CTB on the deblocked picture (a copy: CTBs read deblocked neighbours)
+        const std::vector<uint8_t> pre_y = rec_y_[cur_], pre_uv = rec_uv_[cur_];
+        sao_.assign((size_t)W * H * 4, 0u);
+        const uint32_t lam16 = kLambdaSse16[qp];
+        for (int i = 0; i < W * H; ++i) {
+            const int x0 = (i % W) * kCtb, y0 = (i / W) * kCtb;
+            SaoStats st[3];
+            sao_stats_block(pre_y.data(), cw_, y, pitch, 1, x0, y0, kCtb, cw_, ch_, st[0]);
+            for (int c = 0; c < 2; ++c)
+                sao_stats_block(pre_uv.data() + c, cw_, uv + c, pitch, 2, x0 / 2, y0 / 2, kCtb / 2, cw_ / 2, ch_ / 2,
+                                st[1 + c]);
+            SaoCompChoice ch[3];
+            for (int c = 0; c < 3; ++c) sao_eval_comp(st[c], lam16, ch[c]);
+            uint32_t* w = sao_.data() + 4 * (size_t)i;
+            sao_combine(ch[0], ch[1], ch[2], lam16, w);
+            sao_apply_block(pre_y.data(), rec_y_[cur_].data(), cw_, 1, x0, y0, kCtb, cw_, ch_, w[0]);
+            for (int c = 0; c < 2; ++c)
+                sao_apply_block(pre_uv.data() + c, rec_uv_[cur_].data() + c, cw_, 2, x0 / 2, y0 / 2, kCtb / 2, cw_ / 2,
+                                ch_ / 2, w[1 + c]);
+        }
+    }
     au_.clear();
     if (idr) common_.write_parameter_sets(au_);
     std::vector<uint8_t> buf;
@@ -531,7 +587,8 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
         const uint32_t cap = (uint32_t)count * 1024 + 1024;
         buf.resize(cap);
-        const uint32_t n = code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count, W, ctx);
+        const uint32_t n = code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count, W, ctx,
+                                      cfg_.sao ? sao_.data() : nullptr);
         if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
         common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n);
     }
@@ -559,6 +616,10 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     for (const auto& cu : cu_) stats_.skipped_mbs += cu.type == kCuSkip;
     for (int k = 0; k < 3; ++k) stats_.sse[k] = sse[k];
     rc.end_frame((int)au_.size(), idr);
+    if (cfg_.aq >= 3) {  // this frame's source becomes the previous source of the next one
+        prev_src_.resize((size_t)cw_ * ch_);
+        for (int r = 0; r < ch_; ++r) std::memcpy(prev_src_.data() + (size_t)r * cw_, y + (size_t)r * pitch, cw_);
+    }
     return au_;
 }
 

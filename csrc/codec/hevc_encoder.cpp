@@ -35,6 +35,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.qpy, ncu));
     HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * ncu));
     HIP_CHECK(hipMalloc(&b.qpc, ncu));
+    HIP_CHECK(hipMalloc(&b.sao, sizeof(uint32_t) * 4 * (size_t)ncu));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
@@ -51,7 +52,7 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
                     (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
-                    (void*)b.sse_part})
+                    (void*)b.sse_part, (void*)b.sao})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.me_fs_host) (void)hipHostFree(sl.me_fs_host);
@@ -81,6 +82,12 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMalloc(&rec_uv_[i], uvsz));
         HIP_CHECK(hipMemsetAsync(rec_y_[i], 16, ysz, stream_));
         HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
+        HIP_CHECK(hipMalloc(&src_keep_[i], ysz));
+        HIP_CHECK(hipMemsetAsync(src_keep_[i], 16, ysz, stream_));
+    }
+    if (cfg.sao) {
+        HIP_CHECK(hipMalloc(&pre_y_, ysz));
+        HIP_CHECK(hipMalloc(&pre_uv_, uvsz));
     }
     hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
@@ -99,18 +106,26 @@ GpuHevcEncoder::~GpuHevcEncoder() {
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);
+        (void)hipFree(src_keep_[i]);
     }
     for (int i = 0; i < 4; ++i) (void)hipFree(hp_[i]);
+    if (pre_y_) (void)hipFree(pre_y_);
+    if (pre_uv_) (void)hipFree(pre_uv_);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
 }
 
-void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur) {
+void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur, bool probe) {
     const size_t org = (size_t)h264::kHpelPad * hp_pitch_ + h264::kHpelPad;
     HevcFrameState& f = *sl.fs_host;
     f.ref_y = rec_y_[ref];
     f.ref_uv = rec_uv_[ref];
-    f.rec_y = rec_y_[cur];
-    f.rec_uv = rec_uv_[cur];
+    // the rate-control probe codes without SAO (as the CPU encoder's probe)
+    f.sao = (cfg_.sao && !probe) ? 1 : 0;
+    f.pad_ = 0;
+    f.rec_y = f.sao ? pre_y_ : rec_y_[cur];
+    f.rec_uv = f.sao ? pre_uv_ : rec_uv_[cur];
+    f.sao_y = rec_y_[cur];
+    f.sao_uv = rec_uv_[cur];
     f.hp_f = hp_[0] + org;
     f.hp_pitch = hp_pitch_;
     f.idr = idr ? 1 : 0;
@@ -121,8 +136,10 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.tu_split = cfg_.tu_split ? 1 : 0;
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
     // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
-    f.n_sse_parts = (idr || cfg_.hevc_deblock()) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
+    f.n_sse_parts = (idr || cfg_.hevc_deblock() || f.sao) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
     f.sse_part = sl.buf.sse_part;
+    f.prev_src = src_keep_[ref];
+    f.save_src = src_keep_[cur];
     h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
     m.ref_y = rec_y_[ref];
     m.ref_uv = rec_uv_[ref];
@@ -145,7 +162,7 @@ int GpuHevcEncoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     if (!inflight_.empty()) throw std::logic_error("GpuHevcEncoder: probe with frames in flight");
     prep_slot_ = 0;
     FrameSlot& sl = slots_[0];
-    fill_state(sl, true, qp, cur_ ^ 1, cur_);
+    fill_state(sl, true, qp, cur_ ^ 1, cur_, true);
     enqueue_body(true, src_y, src_uv);
     HIP_CHECK(hipStreamSynchronize(stream_));
     if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
@@ -176,6 +193,9 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(HevcFrameState), hipMemcpyHostToDevice, stream_));
     if (idr) {
+        if (cfg_.aq >= 3)  // the next P picture's temporal classes compare against this source
+            HIP_CHECK(hipMemcpyAsync(sl.fs_host->save_src, src_y, (size_t)geom_.pitch * geom_.coded_h,
+                                     hipMemcpyDeviceToDevice, stream_));
         launch_hevc_intra(geom_, sl.buf, common_.slice_rows(), common_.num_slices(), src_y, src_uv, stream_);
     } else {
         HIP_CHECK(hipMemcpyAsync(sl.buf.me.fs, sl.me_fs_host, sizeof(h264::FrameState), hipMemcpyHostToDevice, stream_));
@@ -183,7 +203,8 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
         h264::launch_me(geom_, sl.buf.me, src_y, stream_);
         launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
-    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_deblock(), src_y, src_uv, stream_);
+    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_deblock(), sl.fs_host->sao != 0, src_y,
+                       src_uv, stream_);
     hipStream_t es = stream_;
     if (stream_e_) {
         HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));

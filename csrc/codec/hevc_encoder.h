@@ -89,6 +89,8 @@ class CpuHevcEncoder {
     std::vector<int> slices_;  // first CTU of every slice of the current picture
     std::vector<int16_t> coef_;
     std::vector<uint8_t> au_;
+    std::vector<uint8_t> prev_src_;  // previous source luma (coded size), temporal AQ classes
+    std::vector<uint32_t> sao_;      // SAO parameters, 4 words per CTB (hevc_core.h sao_pack)
     FrameStats stats_;
 };
 
@@ -114,6 +116,16 @@ struct HevcFrameState {
     int32_t n_sse_parts;  // distortion partials written this frame (P: one per 4 CUs, I: one per CTU row)
     int32_t tu_split;     // inter CUs may split their transform tree (EncoderConfig.tu_split)
     unsigned long long* sse_part;  // [3][kSsePartStride] per-workgroup distortion partials
+    // temporal AQ classes (aq 3, h264_mb.h temporal_class): previous frame's source luma (read)
+    // and this frame's copy (written by k_hevc_inter; IDR pictures copy it on the stream)
+    const uint8_t* prev_src;
+    uint8_t* save_src;
+    // SAO (EncoderConfig::sao): the analysis kernels reconstruct into rec_*, deblocking filters
+    // it in place, k_hevc_sao writes the final picture to sao_* (the reference of the next frame)
+    int32_t sao;
+    int32_t pad_;
+    uint8_t* sao_y;
+    uint8_t* sao_uv;
 };
 
 struct HevcOutHeader {
@@ -144,6 +156,7 @@ struct HevcDeviceBuffers {
     uint8_t* qpy;            // [ncu] QpY per CU (deblocking)
     uint32_t* cost;          // [ncu] CABAC cost estimate (slice layout)
     uint8_t* qpc;            // [ncu] QP of CUs that code a residual, else 255 (QP chain)
+    uint32_t* sao;           // [ncu][4] SAO parameters per CTB (hevc_core.h sao_pack; luma, Cb, Cr, 0)
     size_t out_bytes;
     unsigned long long* sse_part;
 };
@@ -155,7 +168,7 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
 // Slice layout, per-slice decisions and (with deblock) the in-loop filter + final distortion:
 // runs on the analysis stream because the deblocked picture is the next frame's reference.
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
-                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
+                        bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s);
 
@@ -198,7 +211,7 @@ class GpuHevcEncoder final : public VideoEncoder {
     };
     void alloc_slot(FrameSlot& sl);
     void free_slot(FrameSlot& sl);
-    void fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur);
+    void fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur, bool probe = false);
     int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
 
     EncoderConfig cfg_;
@@ -215,6 +228,9 @@ class GpuHevcEncoder final : public VideoEncoder {
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
+    uint8_t* src_keep_[2] = {nullptr, nullptr};  // source luma of the last two frames (temporal AQ classes)
+    uint8_t* pre_y_ = nullptr;   // SAO: reconstruction before SAO (deblocked in place)
+    uint8_t* pre_uv_ = nullptr;
     int cur_ = 0;
     bool have_ref_ = false;
     std::vector<uint8_t> au_;

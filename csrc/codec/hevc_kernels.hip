@@ -104,7 +104,9 @@ struct TuResult {
     int nz[3];
     int sse[3];     // over the display area (PSNR)
     int sse_full;   // over the whole CU (transform-tree decision, as the CPU encoder)
+    int sse_y_full; // luma only, whole CU (residual drop)
     uint32_t bits;  // cu_bits_est of the levels (unsplit tree)
+    uint32_t bits_y;  // tu_bits_est of the luma TU
 };
 
 __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool intra, bool valid,
@@ -258,6 +260,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     {
         const int bl = wsum(lbits), bcb = wsum(comp == 0 ? cbits : 0), bcr = wsum(comp == 1 ? cbits : 0);
         out.bits = (uint32_t)((out.nz[0] ? bl + 4 : 1) + (out.nz[1] ? bcb + 4 : 1) + (out.nz[2] ? bcr + 4 : 1));
+        out.bits_y = (uint32_t)(out.nz[0] ? bl + 4 : 1);
     }
     __syncthreads();
     // ---- inverse stage 1 (columns): a[y][x] = clip16((sum_k T[k][y] b[k][x] + 64) >> 7)
@@ -280,7 +283,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     }
     __syncthreads();
     // ---- inverse stage 2 (rows) + reconstruction
-    int sy = 0, sc = 0, sf = 0;
+    int sy = 0, sc = 0, sf = 0, syf = 0;
     if (valid) {
         const int y = lane >> 2, xb = (lane & 3) * 4;
         uint32_t packed = 0;
@@ -295,6 +298,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             const int e = p + t.res[y * 16 + x] - v;
             sy += (x0 + x < disp_w && y0 + y < disp_h) ? e * e : 0;
             sf += e * e;
+            syf += e * e;
             packed |= (uint32_t)v << (8 * j);
             t.pred[y * 16 + x] = (uint8_t)v;  // reconstruction stays readable in LDS
         }
@@ -322,6 +326,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     out.sse[1] = wsum(comp == 0 ? sc : 0);
     out.sse[2] = wsum(comp == 1 ? sc : 0);
     out.sse_full = wsum(sf);
+    out.sse_y_full = wsum(syf);
     return out;
 }
 
@@ -335,6 +340,8 @@ struct SplitResult {
     int sse_full;
     int sse[3];
     uint32_t bits;
+    int sse_y_full;   // luma only, whole CU (residual drop)
+    uint32_t bits_y;  // tu_bits_est sum of the four luma TUs
 };
 __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool valid, int16_t* lv,
                                                 uint8_t* rec, int x0, int y0, int disp_w, int disp_h) {
@@ -467,6 +474,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     bc = gsum<8>(bc);
     SplitResult out;
     out.bits = (uint32_t)wsum(((lane & 15) == 0 ? (nzl ? bl + 4 : 1) : 0) + ((lane & 7) == 0 ? (nzc ? bc + 4 : 1) : 0));
+    out.bits_y = (uint32_t)wsum((lane & 15) == 0 ? (nzl ? bl + 4 : 1) : 0);
     __syncthreads();
     // ---- inverse stage 1 (columns)
     if (valid) {
@@ -487,7 +495,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     }
     __syncthreads();
     // ---- inverse stage 2 (rows) + reconstruction
-    int sf = 0, sy = 0, sc = 0;
+    int sf = 0, sy = 0, sc = 0, syf = 0;
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = (lane & 15) * 4 + j, y = idx >> 3, x = idx & 7;
@@ -498,6 +506,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
             const int o = (lby + y) * 16 + lbx + x, p = t.pred[o];
             const int v = clip255(p + r), e = p + t.res[o] - v;
             sf += e * e;
+            syf += e * e;
             sy += (x0 + lbx + x < disp_w && y0 + lby + y < disp_h) ? e * e : 0;
             rec[o] = (uint8_t)v;
         }
@@ -515,6 +524,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
         }
     }
     out.sse_full = wsum(sf);
+    out.sse_y_full = wsum(syf);
     out.sse[0] = wsum(sy);
     out.sse[1] = wsum(comp == 0 ? sc : 0);
     out.sse[2] = wsum(comp == 1 ? sc : 0);
@@ -558,6 +568,10 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     const int x0 = x * 16, y0 = y * 16;
     TuBuf& t = tb[wave];
     int mvx = 0, mvy = 0, lsad = 0;
+    int tsad = 0;           // this lane's share of sum |src - previous src| (temporal class, aq 3)
+    int dpf = 0, dpm = 0;   // sum res^2 of the lane's luma samples: whole CU / display area
+    uint32_t pred_px = 0;   // the lane's 4 luma prediction samples (residual drop)
+    int dcp[2] = {0, 0};    // sum (src - pred)^2 of the lane's chroma samples in the display area
     if (valid) {
         mvx = mbs[i].mvx;
         mvy = mbs[i].mvy;
@@ -596,6 +610,18 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
             t.pred[r * 16 + cb + j] = (uint8_t)p;
             t.res[r * 16 + cb + j] = (int16_t)d;
             lsad += d < 0 ? -d : d;
+            pred_px |= (uint32_t)p << (8 * j);
+            dpf += d * d;
+            dpm += (x0 + cb + j < g.width && y0 + r < g.height) ? d * d : 0;
+        }
+        if (fs->aq >= 3) {
+            // temporal class: the source against the previous source displaced by the vector's
+            // integer part; this CU's source becomes the next frame's previous source
+            const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * g.pitch + x0 + cb);
+            for (int j = 0; j < 4; ++j)
+                tsad += abs((int)((sw >> (8 * j)) & 0xff) - h264::ref_px(fs->prev_src, g.pitch, g.coded_w, g.coded_h,
+                                                                          x0 + cb + j + (mvx >> 2), y0 + r + (mvy >> 2)));
+            *reinterpret_cast<uint32_t*>(fs->save_src + (size_t)(y0 + r) * g.pitch + x0 + cb) = sw;
         }
         // chroma: one sample per lane and component
         const int rc = lane >> 3, cc = lane & 7;
@@ -605,15 +631,23 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
             const int s = src_uv[(size_t)yc * g.pitch + 2 * xc + comp];
             t.pred[256 + comp * 64 + rc * 8 + cc] = (uint8_t)p;
             t.res[256 + comp * 64 + rc * 8 + cc] = (int16_t)(s - p);
+            dcp[comp] = (2 * xc < g.width && 2 * yc < g.height) ? (s - p) * (s - p) : 0;
         }
     }
-    const int qp = h264::aq_mb_qp(fs->qp, (uint32_t)wsum(lsad), fs->aq);  // wave-uniform
+    const int tcls = h264::temporal_class((uint32_t)wsum(tsad));
+    const int qp = h264::mb_qp_for(fs->qp, (uint32_t)wsum(lsad), tcls, fs->aq);  // wave-uniform
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
+    // changing content (aq 3): chroma residual dropped, luma kept only if it pays for its bits
+    const bool changing = fs->aq >= 3 && tcls == h264::kTcChanging;
+    if (changing && valid) {
+        const int rc = lane >> 3, cc = lane & 7;
+        for (int comp = 0; comp < 2; ++comp) t.res[256 + comp * 64 + rc * 8 + cc] = 0;
+    }
     __syncthreads();
     int16_t* co = coef + (size_t)(valid ? i : 0) * kCoefPerCu;
     // option 2, the split transform tree (split_encode of the CPU encoder), whole wave
     const bool try_split = fs->tu_split != 0;  // uniform over the grid: barriers inside are safe
-    SplitResult r2 = {0, {0, 0, 0}, 0};
+    SplitResult r2 = {0, {0, 0, 0}, 0, 0, 0};
     if (try_split)
         r2 = split_tus(t, M, qp, qpc, valid, lv2[wave], rec2[wave], x0, y0, g.width, g.height);
     const int sse2 = r2.sse_full, bits2 = (int)r2.bits;
@@ -634,10 +668,23 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         for (int comp = 0; comp < 2; ++comp)
             fs->rec_uv[(size_t)(y0 / 2 + rc) * g.pitch + 2 * (x0 / 2 + cc) + comp] = rec2[wave][256 + comp * 64 + rc * 8 + cc];
     }
+    // rate-distortion residual drop of changing content (h264_mb.h drop_luma_for): the luma
+    // residual must lower the distortion by more than lambda * (estimated bits)
+    const long long d_pred = wsum(dpf);
+    const bool drop = changing && valid &&
+                      d_pred - (long long)(split ? r2.sse_y_full : r.sse_y_full) <
+                          (long long)h264::lambda_sse(qp) * (long long)(split ? r2.bits_y : r.bits_y);  // wave-uniform
+    const int dp_disp = wsum(dpm);
+    const int dcp_u = wsum(dcp[0]), dcp_v = wsum(dcp[1]);  // chroma distortion when its residual is dropped
+    if (drop) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // after this lane's coded levels / reconstruction
+        for (int k = lane; k < 256; k += 64) co[k] = 0;
+        *reinterpret_cast<uint32_t*>(fs->rec_y + (size_t)(y0 + (lane >> 2)) * g.pitch + x0 + (lane & 3) * 4) = pred_px;
+    }
     if (lane == 0) {
-        part[0][wave] = valid ? (unsigned long long)(split ? sse2y : r.sse[0]) : 0ull;
-        part[1][wave] = valid ? (unsigned long long)(split ? sse2u : r.sse[1]) : 0ull;
-        part[2][wave] = valid ? (unsigned long long)(split ? sse2v : r.sse[2]) : 0ull;
+        part[0][wave] = valid ? (unsigned long long)(drop ? dp_disp : (split ? sse2y : r.sse[0])) : 0ull;
+        part[1][wave] = valid ? (unsigned long long)(changing ? dcp_u : (split ? sse2u : r.sse[1])) : 0ull;
+        part[2][wave] = valid ? (unsigned long long)(changing ? dcp_v : (split ? sse2v : r.sse[2])) : 0ull;
     }
     if (valid && lane == 0) {
         CuInfo c;
@@ -652,6 +699,13 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         if (try_split) {
             c.tu_split = split ? 2 : 1;
             if (split) cu_summarise(c, lv2[wave]);
+        }
+        if (drop) {  // no residual left (chroma was dropped before coding): cu_summarise of zeros
+            c.tu_split = try_split ? 1 : 0;
+            c.cbf = c.cbf_y4 = c.cbf_c4 = 0;
+            c.last[0] = c.last[1] = c.last[2] = 0;
+            c.csbf_y = 0;
+            c.csbf_c[0] = c.csbf_c[1] = 0;
         }
         cus[i] = c;  // skip / merge / AMVP are decided by k_hevc_decide once the slices are laid out
         cost[i] = cu_cost(c);
@@ -1054,10 +1108,12 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
                                                     uint8_t* __restrict__ slice_data, uint32_t slice_cap,
                                                     uint32_t* __restrict__ slice_len,
                                                     const int* __restrict__ slice_first,
-                                                    const uint32_t* __restrict__ nslices) {
+                                                    const uint32_t* __restrict__ nslices,
+                                                    const uint32_t* __restrict__ sao) {
     const int s = blockIdx.x, lane = threadIdx.x;
     const int ns = (int)*nslices;
     if (s >= ns) return;
+    const bool sao_on = fs->sao != 0;
     const int first = slice_first[s];
     const int count = (s + 1 < ns ? slice_first[s + 1] : g.mb_w * g.mb_h) - first;
     const bool islice = fs->idr != 0;
@@ -1110,6 +1166,15 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
         nb.left_type = (x > 0 && k > 0) ? prev_type : -1;
         nb.left_mode = prev_mode;
         nb.above_type = k >= g.mb_w ? (int)load_cu(cus, i - g.mb_w).type : -1;
+        if (sao_on) {
+            uint32_t p[3], pl[3], pu[3];
+            for (int q = 0; q < 3; ++q) {
+                p[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sao[4 * (size_t)i + q]);
+                pl[q] = (x > 0 && k > 0) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sao[4 * (size_t)(i - 1) + q]) : 0u;
+                pu[q] = k >= g.mb_w ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sao[4 * (size_t)(i - g.mb_w) + q]) : 0u;
+            }
+            code_sao(e, ctx, p, (x > 0 && k > 0) ? pl : nullptr, k >= g.mb_w ? pu : nullptr);
+        }
         code_cu(e, ctx, islice, c, cf, nb, qp_prev, k == count - 1);
         prev_type = c.type;
         prev_mode = c.intra_mode;
@@ -1168,6 +1233,203 @@ __global__ __launch_bounds__(256) void k_hevc_deblock(Geometry g, const HevcFram
     db_internal_seg(fs->rec_y, g.pitch, g.mb_w, cus, qpy, i, dir, seg);
 }
 
+// ------------------------------------------------------------------ sample adaptive offset
+// One wave per CTB (4 per workgroup), after deblocking: statistics of the deblocked picture
+// (fs->rec_y / rec_uv) against the source, the per-CTB decision of hevc_core.h (sao_eval_comp /
+// sao_combine, here spread over the lanes: 48 edge (component, class, category) offsets, 96 band
+// offsets, 96 band windows), then the offsets applied into fs->sao_y / sao_uv -- a separate
+// picture, so every CTB reads deblocked neighbours.  Lane mapping: luma row lane >> 2, columns
+// 4 (lane & 3) .. + 3; chroma sample (lane & 7, lane >> 3) of both components.  Statistics are
+// packed (count << 20) + sum (|sum| <= 255 * 256 < 2^19, count <= 256).
+struct SaoWave {
+    int32_t eo[3][16];  // [comp][class * 4 + category - 1], packed
+    int32_t bo[3][32];  // [comp][band], packed
+    long long jeo[3][16];
+    int32_t oeo[3][16];
+    long long jb[3][32];
+    int32_t ob[3][32];
+    long long jwin[3];
+    int32_t band[3];
+    uint32_t w[3];
+};
+__device__ __forceinline__ int sao_unpack_sum(int v) { return (int)((uint32_t)v << 12) >> 12; }
+__device__ __forceinline__ int sao_unpack_cnt(int v) { return (v - sao_unpack_sum(v)) >> 20; }
+__device__ __forceinline__ int sao_px(const uint8_t* p, int pitch, int step, int W, int H, int x, int y) {
+    return (x < 0 || y < 0 || x >= W || y >= H) ? -1 : (int)p[(size_t)y * pitch + (size_t)x * step];
+}
+// edge-offset statistics of one sample c (error d) with its 3x3 neighbourhood n (-1 outside)
+__device__ __forceinline__ void sao_acc(int* e, int c, int d, const int (*n)[3]) {
+    const int v = (1 << 20) + d;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int a = n[1 + kSaoDy[k][0]][1 + kSaoDx[k][0]], b = n[1 + kSaoDy[k][1]][1 + kSaoDx[k][1]];
+        const int cat = (a < 0 || b < 0) ? 0 : sao_edge_cat(c, a, b);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) e[k * 4 + q] += cat == q + 1 ? v : 0;
+    }
+}
+__device__ __forceinline__ int sao_out(uint32_t w, int c, const int (*n)[3]) {
+    const int k = sao_eo(w);
+    return sao_sample(w, c, n[1 + kSaoDy[k][0]][1 + kSaoDx[k][0]], n[1 + kSaoDy[k][1]][1 + kSaoDx[k][1]]);
+}
+
+__global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                   const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
+                                                   uint32_t* __restrict__ prm) {
+    __shared__ SaoWave sw[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ncu = g.mb_w * g.mb_h;
+    const int i = blockIdx.x * 4 + wave;
+    const bool valid = i < ncu;
+    const int x0 = valid ? (i % g.mb_w) * kCtb : 0, y0 = valid ? (i / g.mb_w) * kCtb : 0;
+    SaoWave& S = sw[wave];
+    const uint8_t* ry = fs->rec_y;
+    const uint8_t* ruv = fs->rec_uv;
+    const int W = g.coded_w, H = g.coded_h, Wc = W / 2, Hc = H / 2;
+    for (int k = lane; k < 96; k += 64) (&S.bo[0][0])[k] = 0;
+    __syncthreads();
+    // ---- gather: luma 4 samples (3 x 6 window), chroma 1 sample per component (3 x 3 windows)
+    const int r = lane >> 2, c0 = (lane & 3) * 4;
+    const int rc = lane >> 3, cc = lane & 7;
+    int L[3][6], C[2][3][3];
+    int ly[4] = {0, 0, 0, 0}, dy[4] = {0, 0, 0, 0}, lc[2] = {0, 0}, dc[2] = {0, 0};
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) L[j][q] = sao_px(ry, g.pitch, 1, W, H, x0 + c0 + q - 1, y0 + r + j - 1);
+        const uint32_t sv = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * g.pitch + x0 + c0);
+        int e[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) e[q] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = L[1][1 + j];
+            const int d = (int)((sv >> (8 * j)) & 255) - c;
+            ly[j] = c;
+            dy[j] = d;
+            int n[3][3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) n[a][b] = L[a][j + b];
+            sao_acc(e, c, d, n);
+            atomicAdd(&S.bo[0][c >> 3], (1 << 20) + d);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int t = wsum(e[q]);
+            if (lane == 0) S.eo[0][q] = t;
+        }
+        const int xc = x0 / 2 + cc, yc = y0 / 2 + rc;
+#pragma unroll
+        for (int comp = 0; comp < 2; ++comp) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    C[comp][a][b] = sao_px(ruv + comp, g.pitch, 2, Wc, Hc, xc + b - 1, yc + a - 1);
+            const int c = C[comp][1][1];
+            const int d = (int)src_uv[(size_t)yc * g.pitch + 2 * xc + comp] - c;
+            lc[comp] = c;
+            dc[comp] = d;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) e[q] = 0;
+            sao_acc(e, c, d, C[comp]);
+            atomicAdd(&S.bo[1 + comp][c >> 3], (1 << 20) + d);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int t = wsum(e[q]);
+                if (lane == 0) S.eo[1 + comp][q] = t;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- candidates: offsets per (comp, class, category) and per (comp, band)
+    const uint32_t lam16 = kLambdaSse16[fs->qp < 0 ? 0 : (fs->qp > 51 ? 51 : fs->qp)];
+    if (valid) {
+        if (lane < 48) {
+            const int comp = lane >> 4, q = lane & 15, cat = q & 3;
+            const int v = S.eo[comp][q];
+            int o;
+            S.jeo[comp][q] = sao_best_offset(sao_unpack_sum(v), sao_unpack_cnt(v), cat < 2 ? 0 : -7, cat < 2 ? 7 : 0,
+                                             false, lam16, &o);
+            S.oeo[comp][q] = o;
+        }
+        for (int t = lane; t < 96; t += 64) {
+            const int comp = t >> 5, b = t & 31;
+            const int v = S.bo[comp][b];
+            int o;
+            S.jb[comp][b] = sao_best_offset(sao_unpack_sum(v), sao_unpack_cnt(v), -7, 7, true, lam16, &o);
+            S.ob[comp][b] = o;
+        }
+    }
+    __syncthreads();
+    // ---- best band window per component: lexicographic min of (cost, position) over 32 lanes
+    if (valid) {
+        for (int pass = 0; pass < 2; ++pass) {
+            const int comp = pass * 2 + (lane >> 5), p = lane & 31;
+            const bool on = comp < 3;
+            long long j = 0;
+            if (on) j = S.jb[comp][p] + S.jb[comp][(p + 1) & 31] + S.jb[comp][(p + 2) & 31] + S.jb[comp][(p + 3) & 31];
+            int bp = p;
+            for (int o = 16; o > 0; o >>= 1) {
+                const long long jo = __shfl_xor(j, o, 64);
+                const int po = __shfl_xor(bp, o, 64);
+                if (jo < j || (jo == j && po < bp)) {
+                    j = jo;
+                    bp = po;
+                }
+            }
+            if (on && p == 0) {
+                S.jwin[comp] = j;
+                S.band[comp] = bp;
+            }
+        }
+    }
+    __syncthreads();
+    if (valid && lane == 0) {
+        SaoCompChoice ch[3];
+        for (int comp = 0; comp < 3; ++comp) {
+            for (int k = 0; k < 4; ++k) {
+                ch[comp].j_eo[k] = S.jeo[comp][4 * k] + S.jeo[comp][4 * k + 1] + S.jeo[comp][4 * k + 2] +
+                                   S.jeo[comp][4 * k + 3];
+                for (int q = 0; q < 4; ++q) ch[comp].eo_off[k][q] = S.oeo[comp][4 * k + q];
+            }
+            ch[comp].j_bo = S.jwin[comp];
+            ch[comp].band = S.band[comp];
+            for (int k = 0; k < 4; ++k) ch[comp].bo_off[k] = S.ob[comp][(S.band[comp] + k) & 31];
+        }
+        uint32_t w[3];
+        sao_combine(ch[0], ch[1], ch[2], lam16, w);
+        S.w[0] = w[0];
+        S.w[1] = w[1];
+        S.w[2] = w[2];
+        *reinterpret_cast<uint4*>(prm + 4 * (size_t)i) = make_uint4(w[0], w[1], w[2], 0u);
+    }
+    __syncthreads();
+    // ---- apply into the output picture
+    if (valid) {
+        const uint32_t wy = S.w[0], wu = S.w[1], wv = S.w[2];
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int n[3][3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) n[a][b] = L[a][j + b];
+            packed |= (uint32_t)sao_out(wy, ly[j], n) << (8 * j);
+        }
+        *reinterpret_cast<uint32_t*>(fs->sao_y + (size_t)(y0 + r) * g.pitch + x0 + c0) = packed;
+        const int xc = x0 / 2 + cc, yc = y0 / 2 + rc;
+        const uint32_t u = (uint32_t)sao_out(wu, lc[0], C[0]), v = (uint32_t)sao_out(wv, lc[1], C[1]);
+        *reinterpret_cast<uint16_t*>(fs->sao_uv + (size_t)yc * g.pitch + 2 * xc) = (uint16_t)(u | (v << 8));
+    }
+    (void)dy;
+    (void)dc;
+}
+
 // Distortion of the final (deblocked) picture over the display area: one workgroup per CTU
 // row, partial sums per row for k_hevc_pack.
 __global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameState* __restrict__ fs,
@@ -1191,8 +1453,10 @@ __global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameSta
         }
     };
     const int rows = min(16, g.height - r * 16), crows = min(8, g.height / 2 - r * 8);
-    for (int k = tid; k < rows * quads; k += 256) acc(src_y, fs->rec_y, r * 16 + k / quads, k % quads, false);
-    for (int k = tid; k < crows * quads; k += 256) acc(src_uv, fs->rec_uv, r * 8 + k / quads, k % quads, true);
+    const uint8_t* fy = fs->sao ? fs->sao_y : fs->rec_y;  // the final picture
+    const uint8_t* fuv = fs->sao ? fs->sao_uv : fs->rec_uv;
+    for (int k = tid; k < rows * quads; k += 256) acc(src_y, fy, r * 16 + k / quads, k % quads, false);
+    for (int k = tid; k < crows * quads; k += 256) acc(src_uv, fuv, r * 8 + k / quads, k % quads, true);
     for (int o = 32; o > 0; o >>= 1) {
         e[0] += __shfl_xor(e[0], o, 64);
         e[1] += __shfl_xor(e[1], o, 64);
@@ -1298,7 +1562,7 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
 }
 
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
-                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
+                        bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
     hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, b.slice_first,
                        b.slice_of_cu, b.nslices);
@@ -1310,14 +1574,15 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
                            b.qpy);
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
-        hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
     }
+    if (sao) hipLaunchKernelGGL(k_hevc_sao, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.sao);
+    if (deblock || sao) hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
 }
 
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_cabac, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
-                       b.slice_cap, b.slice_len, b.slice_first, b.nslices);
+                       b.slice_cap, b.slice_len, b.slice_first, b.nslices, b.sao);
     hipLaunchKernelGGL(k_hevc_pack, dim3(max_slices), dim3(256), 0, s, b.fs, b.nslices, b.slice_first, b.slice_data,
                        b.slice_cap, b.slice_len, host_out, b.out_bytes);
 }

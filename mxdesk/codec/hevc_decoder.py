@@ -650,9 +650,11 @@ class Decoder:
         rx, ry = ctb % ctbs_w, ctb // ctbs_w
         if rx > 0 and ctb - 1 >= slice_addr and cab.decision("sao_merge_flag"):
             self.sao_params[ctb] = self.sao_params[ctb - 1]
+            self.stats["sao_merge"] = self.stats.get("sao_merge", 0) + 1
             return
         if ry > 0 and ctb - ctbs_w >= slice_addr and cab.decision("sao_merge_flag"):
             self.sao_params[ctb] = self.sao_params[ctb - ctbs_w]
+            self.stats["sao_merge"] = self.stats.get("sao_merge", 0) + 1
             return
         out = []
         for c in range(3):
@@ -682,6 +684,8 @@ class Decoder:
                 if c < 2:
                     eo = cab.bypass_bits(2)
             out.append((typ, offs, band, eo))
+            key = "sao_band" if typ == 1 else "sao_edge"
+            self.stats[key] = self.stats.get(key, 0) + 1
         self.sao_params[ctb] = tuple(out)
 
     # ---------------------------------------------------------------- deblocking (8.7.2)

@@ -159,19 +159,28 @@ def test_decoder_rejects_truncated_stream(native):
 
 
 # ---------------------------------------------------------------------------- GPU tier
-def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0):
+def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, aq=1, desktop=False, sao=1):
     import torch
 
     from .gpu_util import pitched
 
-    cfg = _cfg(gpu, w, h, fps, qp, sr=sr, tu_split=tu_split)
+    cfg = _cfg(gpu, w, h, fps, qp, sr=sr, tu_split=tu_split, aq=aq)
+    cfg.sao = sao
+    desk = None
+    if desktop:
+        from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+        desk = CpuSyntheticDesktop(w, h, True)
     stream = torch.cuda.current_stream().cuda_stream
     genc = gpu.GpuHevcEncoder(cfg, stream)
     cenc = gpu.CpuHevcEncoder(cfg)
     ch = genc.coded_height
     gs, grec = b"", []
     for t in range(frames):
-        y, uv = synthetic_nv12(w, h, t, seed=t if fresh else 0)
+        if desk is not None:
+            y, uv = bgrx_to_nv12(desk.render(t, t / 60, 0))
+        else:
+            y, uv = synthetic_nv12(w, h, t, seed=t if fresh else 0)
         dy = pitched(y, genc.pitch, ch)
         duv = pitched(uv, genc.pitch, ch // 2, uv=True)
         torch.cuda.synchronize()
@@ -205,6 +214,23 @@ def test_gpu_hevc_tu_split_bit_exact_vs_cpu(gpu, w, h, qp):
     """Split transform trees (8x8 luma / 4x4 chroma TUs), chosen per CU by the same rule on
     both sides: GPU bitstream == CPU bitstream, decoded == reconstruction (deblocking on)."""
     _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,qp,tu_split", [(320, 192, 30, 0), (320, 192, 26, 1), (1920, 1080, 34, 1)])
+def test_gpu_hevc_temporal_classes_bit_exact_vs_cpu(gpu, w, h, qp, tu_split):
+    """aq 3 on the synthetic desktop (animated noise panel = changing content, static windows =
+    persistent): temporal classes, chroma drop and the luma residual drop decide the same on the
+    GPU and the CPU, bit for bit, and the stream decodes to the GPU reconstruction."""
+    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=tu_split, aq=3, desktop=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,qp,sao", [(160, 96, 30, 0), (320, 192, 38, 1), (1920, 1080, 40, 1)])
+def test_gpu_hevc_sao_bit_exact_vs_cpu(gpu, w, h, qp, sao):
+    """SAO on the GPU (k_hevc_sao: CTB-parallel statistics, decision and offsets, CABAC sao()
+    syntax) == the CPU encoder, bit for bit, at toy size and 1080p; sao=0 keeps the plain path."""
+    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=1, aq=3, desktop=True, sao=sao)
 
 
 @pytest.mark.gpu
@@ -284,3 +310,74 @@ def test_cpu_hevc_tu_split_saves_bits_on_desktop_content(native):
                 err += float(((enc.recon()[0][:192, :320].astype(np.int64) - y) ** 2).sum())
         res[split] = (nbytes, err)
     assert res[1][0] < res[0][0] and res[1][1] <= res[0][1] * 1.02
+
+
+@pytest.mark.parametrize("tu_split", [0, 1])
+def test_cpu_hevc_temporal_classes(native, tu_split):
+    """Temporal AQ classes (aq 3, shared with H.264: h264_mb.h temporal_class): on the synthetic
+    desktop the animated noise panel is 'changing' (QP + 6, chroma residual dropped, luma kept
+    only when it pays for its bits), static content 'persistent' (QP - 6); the stream decodes to
+    the reconstruction and noise CUs actually drop their residual."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    w, h, qp = 320, 192, 40
+    enc = native.CpuHevcEncoder(_cfg(native, w, h, qp=qp, aq=3, tu_split=tu_split))
+    desk = CpuSyntheticDesktop(w, h, True)
+    stream, recon, infos = b"", [], []
+    for f in range(6):
+        y, uv = bgrx_to_nv12(desk.render(f, f / 60, 0))
+        stream += enc.encode(y, uv, False)
+        recon.append(tuple(p.copy() for p in enc.recon()))
+        if f:
+            infos.append(enc.cu_info())
+    info = np.concatenate(infos)
+    qps = set(info[:, 1].tolist())
+    assert qp + 6 in qps and qp - 6 in qps, qps
+    changing = info[info[:, 1] == qp + 6]
+    if not tu_split:  # (8x8 TUs code noise efficiently enough to keep it at this QP)
+        assert (changing[:, 2] == 0).sum() > 0, "no changing CU dropped its residual"
+    assert not (changing[:, 2] & 6).any(), "changing CUs must not code chroma"
+    dec = Decoder()
+    dec.decode(stream)
+    for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
+        assert np.array_equal(yy, ry) and np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
+
+
+def test_cpu_hevc_sao(native):
+    """Sample adaptive offset (8.7.3): CTBs choose band and edge offsets (and merge with equal
+    neighbours); the decoder's SAO output equals the encoder's reconstruction, and at equal QP
+    SAO lowers the distortion of the synthetic desktop (text / window edges ring at coarse QPs)."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    w, h = 320, 192
+    res = {}
+    for sao in (0, 1):
+        cfg = _cfg(native, w, h, qp=38, aq=3, tu_split=1)
+        cfg.sao = sao
+        enc = native.CpuHevcEncoder(cfg)
+        desk = CpuSyntheticDesktop(w, h, True)
+        stream, recon, err = b"", [], 0
+        for f in range(4):
+            y, uv = bgrx_to_nv12(desk.render(f, f / 60, 0))
+            stream += enc.encode(y, uv, False)
+            recon.append(tuple(p.copy() for p in enc.recon()))
+            err += sum(enc.stats.sse)
+        dec = Decoder()
+        dec.decode(stream)
+        for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
+            assert np.array_equal(yy, ry) and np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
+        res[sao] = (err, len(stream), dec.stats)
+    st = res[1][2]
+    assert st.get("sao_band", 0) > 0 and st.get("sao_edge", 0) > 0 and st.get("sao_merge", 0) > 0, st
+    assert "sao_band" not in res[0][2]
+    assert res[1][0] < res[0][0] * 0.97, (res[0][:2], res[1][:2])
+
+
+def test_hevc_sao_edge_categories():
+    """The decoder's edge-offset categories follow 8.7.3.2 (edgeIdx = 2 + sign + sign, with
+    0, 1, 2 remapped to 1, 2, 0)."""
+    # edge categories: valley, concave corner, flat, convex corner, peak
+    cat = hd._SAO_EDGE_CAT
+    for c, a, b, want in [(1, 5, 5, 1), (1, 1, 5, 2), (3, 3, 3, 0), (5, 5, 1, 3), (9, 1, 1, 4), (2, 1, 3, 0)]:
+        e = 2 + int(np.sign(c - a)) + int(np.sign(c - b))
+        assert cat[e] == want, (c, a, b)
