@@ -441,6 +441,7 @@ PYBIND11_MODULE(_native, m) {
                  return py::make_tuple(copy_plane(e.recon_y(), g.pitch, g.coded_w, g.coded_h),
                                        copy_plane(e.recon_uv(), g.pitch, g.coded_w, g.coded_h / 2));
              })
+        .def("slice_timing", &hevc::GpuHevcEncoder::slice_timing)
         .def("request_idr", [](hevc::GpuHevcEncoder& e) { e.common().rc().request_idr(); })
         .def("set_bitrate", [](hevc::GpuHevcEncoder& e, int k) { e.common().rc().set_bitrate(k); })
         .def_property_readonly("stats", &hevc::GpuHevcEncoder::last_stats);

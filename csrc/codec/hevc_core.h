@@ -1138,17 +1138,17 @@ MXHD void sao_stats_block(const uint8_t* rec, int rpitch, const uint8_t* src, in
 MXHD int sao_offset_bits(int a) { return a < 7 ? a + 1 : 7; }  // sao_offset_abs: TR, cMax 7, bypass
 // Best offset in [lo, hi] for a category / band with error sum s over n samples: start at the
 // rounded mean, step toward 0, keep the lowest 16 * (n o^2 - 2 o s) + lambda16 * bits (o = 0:
-// no distortion change, one bin).  Returns that cost.
-MXHD long long sao_best_offset(int s, int n, int lo, int hi, bool sign_bit, uint32_t lam16, int* o_out) {
+// no distortion change, one bin).  Returns that cost.  All costs fit 32 bits: n <= 256,
+// |s| <= 255 n, |o| <= 7 give |16 dSSE| < 15M per offset and < 36M for a whole CTB choice.
+MXHD int sao_best_offset(int s, int n, int lo, int hi, bool sign_bit, uint32_t lam16, int* o_out) {
     int o = 0;
     if (n > 0) o = s >= 0 ? (s + n / 2) / n : -((-s + n / 2) / n);
     o = o < lo ? lo : (o > hi ? hi : o);
-    long long best = (long long)lam16;
+    int best = (int)lam16;
     int best_o = 0;
     for (int v = o; v != 0; v += v > 0 ? -1 : 1) {
         const int a = v < 0 ? -v : v;
-        const long long j = 16LL * ((long long)n * v * v - 2LL * v * s) +
-                            (long long)lam16 * (sao_offset_bits(a) + (sign_bit ? 1 : 0));
+        const int j = 16 * (n * v * v - 2 * v * s) + (int)lam16 * (sao_offset_bits(a) + (sign_bit ? 1 : 0));
         if (j < best) {
             best = j;
             best_o = v;
@@ -1160,27 +1160,28 @@ MXHD long long sao_best_offset(int s, int n, int lo, int hi, bool sign_bit, uint
 
 // Per-component candidates: each edge class with its four offsets, and the best band window.
 struct SaoCompChoice {
-    long long j_eo[4];
-    long long j_bo;
+    int j_eo[4];
+    int j_bo;
     int eo_off[4][4];
     int bo_off[4];
     int band;
 };
+// Band window of four consecutive bands (wrapping) with the lowest summed cost; the first
+// position wins ties.
 MXHD void sao_eval_comp(const SaoStats& st, uint32_t lam16, SaoCompChoice& ch) {
     for (int k = 0; k < 4; ++k) {
-        long long j = 0;
+        int j = 0;
         for (int c = 0; c < 4; ++c)  // categories 1, 2 (valleys) positive, 3, 4 (peaks) negative
             j += sao_best_offset(st.eo_sum[k][c], st.eo_cnt[k][c], c < 2 ? 0 : -7, c < 2 ? 7 : 0, false, lam16,
                                  &ch.eo_off[k][c]);
         ch.j_eo[k] = j;
     }
-    long long jb[32];
-    int ob[32];
+    int jb[32], ob[32];
     for (int b = 0; b < 32; ++b) jb[b] = sao_best_offset(st.bo_sum[b], st.bo_cnt[b], -7, 7, true, lam16, &ob[b]);
     ch.j_bo = 0;
     ch.band = 0;
     for (int p = 0; p < 32; ++p) {
-        const long long j = jb[p] + jb[(p + 1) & 31] + jb[(p + 2) & 31] + jb[(p + 3) & 31];
+        const int j = jb[p] + jb[(p + 1) & 31] + jb[(p + 2) & 31] + jb[(p + 3) & 31];
         if (p == 0 || j < ch.j_bo) {
             ch.j_bo = j;
             ch.band = p;
@@ -1192,34 +1193,33 @@ MXHD void sao_eval_comp(const SaoStats& st, uint32_t lam16, SaoCompChoice& ch) {
 // Syntax bits beyond the offsets: type (1 context bin + 1 bypass), band position 5, edge class 2.
 MXHD void sao_combine(const SaoCompChoice& y, const SaoCompChoice& cb, const SaoCompChoice& cr, uint32_t lam16,
                       uint32_t* w) {
-    const int zero[4] = {0, 0, 0, 0};
+    const int lam = (int)lam16;
     {
-        long long best = (long long)lam16;  // off: one bin
+        int best = lam;  // off: one bin
         w[0] = 0;
-        const long long jb = y.j_bo + (long long)lam16 * 7;
+        const int jb = y.j_bo + lam * 7;
         if (jb < best) {
             best = jb;
             w[0] = sao_pack(1, 0, y.band, y.bo_off);
         }
         for (int k = 0; k < 4; ++k) {
-            const long long je = y.j_eo[k] + (long long)lam16 * 4;
+            const int je = y.j_eo[k] + lam * 4;
             if (je < best) {
                 best = je;
                 w[0] = sao_pack(2, k, 0, y.eo_off[k]);
             }
         }
     }
-    long long best = (long long)lam16;
-    w[1] = sao_pack(0, 0, 0, zero);
-    w[2] = w[1];
-    const long long jb = cb.j_bo + cr.j_bo + (long long)lam16 * 12;
+    int best = lam;
+    w[1] = w[2] = 0;
+    const int jb = cb.j_bo + cr.j_bo + lam * 12;
     if (jb < best) {
         best = jb;
         w[1] = sao_pack(1, 0, cb.band, cb.bo_off);
         w[2] = sao_pack(1, 0, cr.band, cr.bo_off);
     }
     for (int k = 0; k < 4; ++k) {
-        const long long je = cb.j_eo[k] + cr.j_eo[k] + (long long)lam16 * 4;
+        const int je = cb.j_eo[k] + cr.j_eo[k] + lam * 4;
         if (je < best) {
             best = je;
             w[1] = sao_pack(2, k, 0, cb.eo_off[k]);
@@ -1230,18 +1230,22 @@ MXHD void sao_combine(const SaoCompChoice& y, const SaoCompChoice& cb, const Sao
 
 // SAO output of sample c (deblocked) with parameters w; a / b: its class-eo neighbours, or -1
 // when one lies outside the picture (edge offset: unmodified).
-MXHD int sao_sample(uint32_t w, int c, int a, int b) {
+// SAO output of sample c with parameters w when its edge category (class sao_eo(w)) is cat
+// (0: flat, or a neighbour outside the picture).
+MXHD int sao_sample_cat(uint32_t w, int c, int cat) {
     const int type = sao_type(w);
     int o = 0;
     if (type == 1) {
         const int k = ((c >> 3) - sao_band(w)) & 31;
         o = k < 4 ? sao_off(w, k) : 0;
-    } else if (type == 2 && a >= 0 && b >= 0) {
-        const int cat = sao_edge_cat(c, a, b);
+    } else if (type == 2) {
         o = cat ? sao_off(w, cat - 1) : 0;
     }
     const int v = c + o;
     return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+MXHD int sao_sample(uint32_t w, int c, int a, int b) {
+    return sao_sample_cat(w, c, (a >= 0 && b >= 0) ? sao_edge_cat(c, a, b) : 0);
 }
 // Apply w to the n x n block at (x0, y0): reads the deblocked plane rec, writes out (a different
 // buffer: every CTB reads its neighbours' deblocked samples).
@@ -1257,22 +1261,24 @@ MXHD void sao_apply_block(const uint8_t* rec, uint8_t* out, int pitch, int step,
         }
 }
 
-// sao(rx, ry) syntax (7.3.8.3) of a CTB with parameters p[3]; left / up: the neighbour CTB's
-// parameters when it is in the slice (else nullptr).
+// sao(rx, ry) syntax (7.3.8.3) of a CTB with parameters (p0, p1, p2); the left / up neighbour
+// CTB's parameters count only when it is in the slice (has_l / has_u).  Values, not pointers:
+// on the device every argument stays in (wave-uniform) registers.
 template <class Ctx>
-MXHD void code_sao(CabacEnc& e, Ctx& ctx, const uint32_t* p, const uint32_t* left, const uint32_t* up) {
-    if (left) {
-        const bool m = left[0] == p[0] && left[1] == p[1] && left[2] == p[2];
+MXHD void code_sao_w(CabacEnc& e, Ctx& ctx, uint32_t p0, uint32_t p1, uint32_t p2, bool has_l, uint32_t l0,
+                     uint32_t l1, uint32_t l2, bool has_u, uint32_t u0, uint32_t u1, uint32_t u2) {
+    if (has_l) {
+        const bool m = l0 == p0 && l1 == p1 && l2 == p2;
         e.bin(ctx, C_SAO_MERGE, m ? 1 : 0);
         if (m) return;
     }
-    if (up) {
-        const bool m = up[0] == p[0] && up[1] == p[1] && up[2] == p[2];
+    if (has_u) {
+        const bool m = u0 == p0 && u1 == p1 && u2 == p2;
         e.bin(ctx, C_SAO_MERGE, m ? 1 : 0);
         if (m) return;
     }
     for (int c = 0; c < 3; ++c) {
-        const uint32_t w = p[c];
+        const uint32_t w = c == 0 ? p0 : (c == 1 ? p1 : p2);
         const int type = sao_type(w);
         if (c < 2) {
             e.bin(ctx, C_SAO_TYPE, type != 0 ? 1 : 0);
@@ -1295,7 +1301,11 @@ MXHD void code_sao(CabacEnc& e, Ctx& ctx, const uint32_t* p, const uint32_t* lef
         }
     }
 }
-
+template <class Ctx>
+MXHD void code_sao(CabacEnc& e, Ctx& ctx, const uint32_t* p, const uint32_t* left, const uint32_t* up) {
+    code_sao_w(e, ctx, p[0], p[1], p[2], left != nullptr, left ? left[0] : 0u, left ? left[1] : 0u,
+               left ? left[2] : 0u, up != nullptr, up ? up[0] : 0u, up ? up[1] : 0u, up ? up[2] : 0u);
+}
 
 // Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row).
 // Returns the number of payload bytes (> cap means overflow).

@@ -36,6 +36,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * ncu));
     HIP_CHECK(hipMalloc(&b.qpc, ncu));
     HIP_CHECK(hipMalloc(&b.sao, sizeof(uint32_t) * 4 * (size_t)ncu));
+    HIP_CHECK(hipMalloc(&b.slice_clk, sizeof(unsigned long long) * 2 * (size_t)ns));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
@@ -52,7 +53,7 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
                     (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
-                    (void*)b.sse_part, (void*)b.sao})
+                    (void*)b.sse_part, (void*)b.sao, (void*)b.slice_clk})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.me_fs_host) (void)hipHostFree(sl.me_fs_host);
@@ -135,8 +136,10 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.aq = cfg_.aq;
     f.tu_split = cfg_.tu_split ? 1 : 0;
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
-    // distortion partials: k_hevc_sse (one per CTU row) after deblocking, else the analysis kernels'
-    f.n_sse_parts = (idr || cfg_.hevc_deblock() || f.sao) ? geom_.mb_h : (geom_.mb_w * geom_.mb_h + 3) / 4;
+    // distortion partials: k_hevc_sao (one per 4 CTUs) with SAO, else k_hevc_sse (one per CTU row)
+    // after deblocking, else the analysis kernels' (P: one per 4 CUs, I: one per CTU row)
+    const int ncu = geom_.mb_w * geom_.mb_h;
+    f.n_sse_parts = f.sao ? (ncu + 3) / 4 : ((idr || cfg_.hevc_deblock()) ? geom_.mb_h : (ncu + 3) / 4);
     f.sse_part = sl.buf.sse_part;
     f.prev_src = src_keep_[ref];
     f.save_src = src_keep_[cur];
@@ -255,6 +258,9 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     const uint32_t* slen = soff + kMaxSlices;
     const uint32_t* saddr = soff + 2 * kMaxSlices;
     const uint8_t* payload = sl.host_out + kOutPayloadOffset;
+    last_slot_ = s;
+    last_first_.assign(saddr, saddr + hdr.num_slices);
+    last_len_.assign(slen, slen + hdr.num_slices);
     au_.clear();
     au_.reserve(hdr.total_bytes + hdr.total_bytes / 64 + 64 * hdr.num_slices + 256);
     if (sl.idr) common_.write_parameter_sets(au_);
@@ -268,6 +274,21 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
     rc.end_frame((int)au_.size(), sl.idr);
     return au_;
+}
+
+std::vector<std::array<uint64_t, 4>> GpuHevcEncoder::slice_timing() const {
+    std::vector<std::array<uint64_t, 4>> out;
+    if (last_slot_ < 0) return out;
+    const size_t n = last_first_.size();
+    std::vector<unsigned long long> clk(2 * n);
+    HIP_CHECK(hipMemcpy(clk.data(), slots_[last_slot_].buf.slice_clk, sizeof(unsigned long long) * 2 * n,
+                        hipMemcpyDeviceToHost));
+    const uint64_t ncu = (uint64_t)geom_.mb_w * geom_.mb_h;
+    for (size_t k = 0; k < n; ++k) {
+        const uint64_t end = k + 1 < n ? last_first_[k + 1] : ncu;
+        out.push_back({last_first_[k], end - last_first_[k], last_len_[k], clk[2 * k + 1] - clk[2 * k]});
+    }
+    return out;
 }
 
 }  // namespace hevc

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <array>
 #include <deque>
 #include <vector>
 
@@ -157,6 +158,7 @@ struct HevcDeviceBuffers {
     uint32_t* cost;          // [ncu] CABAC cost estimate (slice layout)
     uint8_t* qpc;            // [ncu] QP of CUs that code a residual, else 255 (QP chain)
     uint32_t* sao;           // [ncu][4] SAO parameters per CTB (hevc_core.h sao_pack; luma, Cb, Cr, 0)
+    unsigned long long* slice_clk;  // [max_slices][2] k_hevc_cabac start / end (wall_clock64, 100 MHz)
     size_t out_bytes;
     unsigned long long* sse_part;
 };
@@ -192,6 +194,9 @@ class GpuHevcEncoder final : public VideoEncoder {
     const uint8_t* recon_y() const override { return rec_y_[cur_]; }
     const uint8_t* recon_uv() const override { return rec_uv_[cur_]; }
     hipEvent_t done_event() const override { return last_done_; }
+    // Per-slice CABAC timing of the last collected picture (diagnostics, synchronous copy):
+    // (first CTU, CTUs, payload bytes, wave ticks at 100 MHz) per slice.
+    std::vector<std::array<uint64_t, 4>> slice_timing() const;
     // split form (same as GpuH264Encoder) for the session's graph path
     bool prepare(bool force_idr) override;
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
@@ -221,7 +226,8 @@ class GpuHevcEncoder final : public VideoEncoder {
     int depth_ = 1;
     Geometry geom_;
     FrameSlot slots_[kMaxInFlight];
-    int next_slot_ = 0, prep_slot_ = 0;
+    int next_slot_ = 0, prep_slot_ = 0, last_slot_ = -1;
+    std::vector<uint32_t> last_first_, last_len_;  // slice layout of the last collected picture
     std::deque<int> inflight_;
     hipEvent_t last_done_ = nullptr;
     uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};

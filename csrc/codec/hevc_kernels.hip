@@ -1103,16 +1103,31 @@ __device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
     return c;
 }
 
+// CU descriptors are staged through LDS kCabacChunk CUs at a time (one bulk vector load per
+// chunk: the descriptor words, the above CU's type and the SAO parameters of the CU and of the
+// CU above), so a skipped CU costs its few bins and no memory round trip; the levels of a coded
+// CU are loaded one coded CU ahead (the next coded CU found through a ballot of the chunk).
+constexpr int kCabacChunk = 128;
+struct CabacStage {
+    uint32_t w[kCabacChunk * kCuWords];
+    uint32_t above[kCabacChunk];  // type of the CU above (255: not in the slice)
+    uint4 sao[kCabacChunk];
+    uint4 sao_up[kCabacChunk];
+};
+
 __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameState* __restrict__ fs,
                                                     const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
                                                     uint8_t* __restrict__ slice_data, uint32_t slice_cap,
                                                     uint32_t* __restrict__ slice_len,
                                                     const int* __restrict__ slice_first,
                                                     const uint32_t* __restrict__ nslices,
-                                                    const uint32_t* __restrict__ sao) {
+                                                    const uint32_t* __restrict__ sao,
+                                                    unsigned long long* __restrict__ slice_clk) {
+    __shared__ CabacStage st;
     const int s = blockIdx.x, lane = threadIdx.x;
     const int ns = (int)*nslices;
     if (s >= ns) return;
+    const unsigned long long clk0 = wall_clock64();
     const bool sao_on = fs->sao != 0;
     const int first = slice_first[s];
     const int count = (s + 1 < ns ? slice_first[s + 1] : g.mb_w * g.mb_h) - first;
@@ -1133,54 +1148,112 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
     e.start(slice_data + (size_t)s * slice_cap, slice_cap);
     int qp_prev = qp;
     int prev_type = -1, prev_mode = 1;
-    // software pipeline: the next CU's descriptor words and levels are loaded (vector loads
-    // in flight) while the current CU is coded
+    uint32_t pl0 = 0u, pl1 = 0u, pl2 = 0u;  // SAO parameters of the previous CU (merge-left candidate)
     const uint32_t* cuw = reinterpret_cast<const uint32_t*>(cus);
-    uint32_t raw[kCuWords];
-    int vn[6];
-    for (int q = 0; q < kCuWords; ++q) raw[q] = cuw[(size_t)first * kCuWords + q];
-    for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)first * kCoefPerCu + q * 64 + lane];
-    for (int k = 0; k < count; ++k) {
-        const int i = first + k;
-        const int x = i % g.mb_w;
-        CuInfo c;
-        {
-            uint32_t w[kCuWords];
-            for (int q = 0; q < kCuWords; ++q) w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)raw[q]);
-            __builtin_memcpy(&c, w, sizeof c);
-        }
-        int v[6];
-        for (int q = 0; q < 6; ++q) v[q] = vn[q];
-        if (k + 1 < count) {
-            for (int q = 0; q < kCuWords; ++q) raw[q] = cuw[(size_t)(i + 1) * kCuWords + q];
-            for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)(i + 1) * kCoefPerCu + q * 64 + lane];
-        }
-        WaveCoef cf;
-        for (int q = 0; q < 6; ++q) {
-            const bool use = c.type != kCuSkip && c.cbf;
-            cf.sigm[q] = use ? __ballot(v[q] != 0) : 0ull;
-            cf.negm[q] = use ? __ballot(v[q] < 0) : 0ull;
-            cf.a[q] = v[q] < 0 ? -v[q] : v[q];
-        }
-        CuNb nb;
-        nb.left_type = (x > 0 && k > 0) ? prev_type : -1;
-        nb.left_mode = prev_mode;
-        nb.above_type = k >= g.mb_w ? (int)load_cu(cus, i - g.mb_w).type : -1;
-        if (sao_on) {
-            uint32_t p[3], pl[3], pu[3];
-            for (int q = 0; q < 3; ++q) {
-                p[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sao[4 * (size_t)i + q]);
-                pl[q] = (x > 0 && k > 0) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sao[4 * (size_t)(i - 1) + q]) : 0u;
-                pu[q] = k >= g.mb_w ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sao[4 * (size_t)(i - g.mb_w) + q]) : 0u;
+    const uint4* sao4 = reinterpret_cast<const uint4*>(sao);
+    int vn[6] = {0, 0, 0, 0, 0, 0};
+    int pf = -1;  // CU whose levels are in vn (-1: none in flight)
+    for (int base = 0; base < count; base += kCabacChunk) {
+        const int n = min(kCabacChunk, count - base);
+        __syncthreads();  // the previous chunk's descriptors are no longer read
+        for (int t = lane; t < n * kCuWords; t += 64) st.w[t] = cuw[(size_t)(first + base) * kCuWords + t];
+        uint64_t coded_lo = 0, coded_hi = 0;  // CUs of the chunk with levels to code
+        for (int t = lane; t < kCabacChunk; t += 64) {
+            const int k = base + t, i = first + k;
+            bool coded = false;
+            if (t < n) {
+                const uint32_t w0 = cuw[(size_t)i * kCuWords];  // type, intra mode, qp, cbf
+                coded = (w0 & 0xff) != kCuSkip && (w0 >> 24) != 0;
+                st.above[t] = k >= g.mb_w ? (cuw[(size_t)(i - g.mb_w) * kCuWords] & 0xff) : 255u;
+                if (sao_on) {
+                    st.sao[t] = sao4[i];
+                    st.sao_up[t] = k >= g.mb_w ? sao4[i - g.mb_w] : make_uint4(0, 0, 0, 0);
+                }
             }
-            code_sao(e, ctx, p, (x > 0 && k > 0) ? pl : nullptr, k >= g.mb_w ? pu : nullptr);
+            const uint64_t m = __ballot(coded);
+            if (t < 64) coded_lo = m; else coded_hi = m;
         }
-        code_cu(e, ctx, islice, c, cf, nb, qp_prev, k == count - 1);
-        prev_type = c.type;
-        prev_mode = c.intra_mode;
+        __syncthreads();
+        auto next_coded = [&](int from) -> int {  // first coded CU of the chunk at index >= from
+            if (from < 64) {
+                const uint64_t m = coded_lo & (~0ull << from);
+                if (m) return __builtin_ctzll(m);
+                from = 64;
+            }
+            if (from < kCabacChunk) {
+                const uint64_t m = coded_hi & (~0ull << (from - 64));
+                if (m) return 64 + __builtin_ctzll(m);
+            }
+            return -1;
+        };
+        if (pf < 0) {
+            const int t0 = next_coded(0);
+            if (t0 >= 0) {
+                pf = first + base + t0;
+                for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)pf * kCoefPerCu + q * 64 + lane];
+            }
+        }
+        for (int t = 0; t < n; ++t) {
+            const int k = base + t, i = first + k;
+            const int x = i % g.mb_w;
+            CuInfo c;
+            {
+                uint32_t w[kCuWords];
+                for (int q = 0; q < kCuWords; ++q)
+                    w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)st.w[t * kCuWords + q]);
+                __builtin_memcpy(&c, w, sizeof c);
+            }
+            const bool use = c.type != kCuSkip && c.cbf;
+            WaveCoef cf;
+            if (use) {
+                int v[6];
+                for (int q = 0; q < 6; ++q) v[q] = vn[q];  // pf == i: every coded CU is prefetched
+                pf = -1;
+                const int tn = next_coded(t + 1);
+                if (tn >= 0) {
+                    pf = first + base + tn;
+                    for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)pf * kCoefPerCu + q * 64 + lane];
+                }
+                for (int q = 0; q < 6; ++q) {
+                    cf.sigm[q] = __ballot(v[q] != 0);
+                    cf.negm[q] = __ballot(v[q] < 0);
+                    cf.a[q] = v[q] < 0 ? -v[q] : v[q];
+                }
+            } else {
+                for (int q = 0; q < 6; ++q) {
+                    cf.sigm[q] = cf.negm[q] = 0ull;
+                    cf.a[q] = 0;
+                }
+            }
+            CuNb nb;
+            nb.left_type = (x > 0 && k > 0) ? prev_type : -1;
+            nb.left_mode = prev_mode;
+            const int up_t = (int)(uint32_t)__builtin_amdgcn_readfirstlane((int)st.above[t]);
+            nb.above_type = up_t == 255 ? -1 : up_t;
+            if (sao_on) {
+                const uint4 p4 = st.sao[t], u4 = st.sao_up[t];
+                const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p4.x),
+                               p1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p4.y),
+                               p2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p4.z);
+                code_sao_w(e, ctx, p0, p1, p2, x > 0 && k > 0, pl0, pl1, pl2, k >= g.mb_w,
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)u4.x),
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)u4.y),
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)u4.z));
+                pl0 = p0;
+                pl1 = p1;
+                pl2 = p2;
+            }
+            code_cu(e, ctx, islice, c, cf, nb, qp_prev, k == count - 1);
+            prev_type = c.type;
+            prev_mode = c.intra_mode;
+        }
     }
     e.finish_slice();
-    if (lane == 0) slice_len[s] = e.pos;
+    if (lane == 0) {
+        slice_len[s] = e.pos;
+        slice_clk[2 * s] = clk0;  // diagnostics: this wave's span (GpuHevcEncoder::slice_timing)
+        slice_clk[2 * s + 1] = wall_clock64();
+    }
 }
 
 // ------------------------------------------------------------------ deblocking
@@ -1236,47 +1309,113 @@ __global__ __launch_bounds__(256) void k_hevc_deblock(Geometry g, const HevcFram
 // ------------------------------------------------------------------ sample adaptive offset
 // One wave per CTB (4 per workgroup), after deblocking: statistics of the deblocked picture
 // (fs->rec_y / rec_uv) against the source, the per-CTB decision of hevc_core.h (sao_eval_comp /
-// sao_combine, here spread over the lanes: 48 edge (component, class, category) offsets, 96 band
+// sao_combine, spread over the lanes: 48 edge (component, class, category) offsets, 96 band
 // offsets, 96 band windows), then the offsets applied into fs->sao_y / sao_uv -- a separate
-// picture, so every CTB reads deblocked neighbours.  Lane mapping: luma row lane >> 2, columns
-// 4 (lane & 3) .. + 3; chroma sample (lane & 7, lane >> 3) of both components.  Statistics are
-// packed (count << 20) + sum (|sum| <= 255 * 256 < 2^19, count <= 256).
+// picture, so every CTB reads deblocked neighbours -- with the final distortion over the display
+// area accumulated on the way (one partial per workgroup, k_hevc_pack sums them).
+// Lane mapping: luma row lane >> 2, columns 4 (lane & 3) .. + 3; chroma sample (lane & 7,
+// lane >> 3) of both components.  Statistics are packed (count << 20) + sum (|sum| <= 255 * 256
+// < 2^19, count <= 256).
 struct SaoWave {
     int32_t eo[3][16];  // [comp][class * 4 + category - 1], packed
     int32_t bo[3][32];  // [comp][band], packed
-    long long jeo[3][16];
+    int32_t jeo[3][16];
     int32_t oeo[3][16];
-    long long jb[3][32];
+    int32_t jb[3][32];
     int32_t ob[3][32];
-    long long jwin[3];
-    int32_t band[3];
+    SaoCompChoice ch[3];
     uint32_t w[3];
 };
+typedef __attribute__((address_space(1))) uint32_t sao_gu32;
+typedef __attribute__((address_space(1))) uint16_t sao_gu16;
+typedef __attribute__((address_space(1))) uint8_t sao_gu8;
 __device__ __forceinline__ int sao_unpack_sum(int v) { return (int)((uint32_t)v << 12) >> 12; }
 __device__ __forceinline__ int sao_unpack_cnt(int v) { return (v - sao_unpack_sum(v)) >> 20; }
-__device__ __forceinline__ int sao_px(const uint8_t* p, int pitch, int step, int W, int H, int x, int y) {
-    return (x < 0 || y < 0 || x >= W || y >= H) ? -1 : (int)p[(size_t)y * pitch + (size_t)x * step];
-}
-// edge-offset statistics of one sample c (error d) with its 3x3 neighbourhood n (-1 outside)
-__device__ __forceinline__ void sao_acc(int* e, int c, int d, const int (*n)[3]) {
-    const int v = (1 << 20) + d;
+
+// 3x3 neighbourhood rows of the lane's luma samples: n[row][0..5] = columns c0 - 1 .. c0 + 4
+// (-1 outside the picture); the middle four come from one dword load.
+__device__ __forceinline__ void sao_luma_window(const uint8_t* p, int pitch, int W, int H, int x, int y, int (*n)[6]) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int a = n[1 + kSaoDy[k][0]][1 + kSaoDx[k][0]], b = n[1 + kSaoDy[k][1]][1 + kSaoDx[k][1]];
-        const int cat = (a < 0 || b < 0) ? 0 : sao_edge_cat(c, a, b);
+    for (int j = 0; j < 3; ++j) {
+        const int yy = y + j - 1;
+        if (yy < 0 || yy >= H) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) e[k * 4 + q] += cat == q + 1 ? v : 0;
+            for (int q = 0; q < 6; ++q) n[j][q] = -1;
+            continue;
+        }
+        const sao_gu8* row = (const sao_gu8*)(p + (size_t)yy * pitch);
+        const uint32_t mid = *(const sao_gu32*)(row + x);
+        n[j][0] = x > 0 ? (int)row[x - 1] : -1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) n[j][1 + q] = (int)((mid >> (8 * q)) & 255);
+        n[j][5] = x + 4 < W ? (int)row[x + 4] : -1;
     }
 }
-__device__ __forceinline__ int sao_out(uint32_t w, int c, const int (*n)[3]) {
+// 3x3 neighbourhood of chroma sample (x, y) for both components (interleaved NV12 pairs)
+__device__ __forceinline__ void sao_chroma_window(const uint8_t* p, int pitch, int W, int H, int x, int y,
+                                                  int (*u)[3], int (*v)[3]) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int yy = y + j - 1;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int xx = x + q - 1;
+            const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
+            const uint32_t pr = in ? *(const sao_gu16*)(p + (size_t)yy * pitch + 2 * xx) : 0xffffffffu;
+            u[j][q] = in ? (int)(pr & 255) : -1;
+            v[j][q] = in ? (int)(pr >> 8) : -1;
+        }
+    }
+}
+// edge category of the centre of a 3x3 neighbourhood for class k (0 when a neighbour is outside)
+template <int K>
+__device__ __forceinline__ int sao_cat3(const int (*n)[3]) {
+    const int a = n[1 + kSaoDy[K][0]][1 + kSaoDx[K][0]], b = n[1 + kSaoDy[K][1]][1 + kSaoDx[K][1]];
+    return (a < 0 || b < 0) ? 0 : sao_edge_cat(n[1][1], a, b);
+}
+__device__ __forceinline__ void sao_acc(int* e, int d, const int (*n)[3]) {
+    const int v = (1 << 20) + d;
+    const int c0 = sao_cat3<0>(n), c1 = sao_cat3<1>(n), c2 = sao_cat3<2>(n), c3 = sao_cat3<3>(n);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        e[q] += c0 == q + 1 ? v : 0;
+        e[4 + q] += c1 == q + 1 ? v : 0;
+        e[8 + q] += c2 == q + 1 ? v : 0;
+        e[12 + q] += c3 == q + 1 ? v : 0;
+    }
+}
+// SAO output of the centre of n: the four class categories are computed and the one of class
+// sao_eo(w) selected (a select between loaded neighbours would become a scratch-indexed load)
+__device__ __forceinline__ int sao_out3(uint32_t w, const int (*n)[3]) {
     const int k = sao_eo(w);
-    return sao_sample(w, c, n[1 + kSaoDy[k][0]][1 + kSaoDx[k][0]], n[1 + kSaoDy[k][1]][1 + kSaoDx[k][1]]);
+    const int c0 = sao_cat3<0>(n), c1 = sao_cat3<1>(n), c2 = sao_cat3<2>(n), c3 = sao_cat3<3>(n);
+    return sao_sample_cat(w, n[1][1], k == 0 ? c0 : (k == 1 ? c1 : (k == 2 ? c2 : c3)));
+}
+// Sum of 16 per-lane values over the wave in 17 shuffles: four halving exchanges (xor 32, 16,
+// 8, 4) leave value (lane >> 2) & 15 summed over 16 lanes, two more steps finish the sum;
+// lanes with (lane & 3) == 0 return value index (lane >> 2) & 15.
+__device__ __forceinline__ int sao_reduce16(int* v, int lane) {
+#pragma unroll
+    for (int h = 8, bit = 32; h >= 1; h >>= 1, bit >>= 1) {
+        const bool hi = (lane & bit) != 0;
+#pragma unroll
+        for (int j = 0; j < h; ++j) {
+            const int send = hi ? v[j] : v[h + j];
+            const int keep = hi ? v[h + j] : v[j];
+            v[j] = keep + __shfl_xor(send, bit, 64);
+        }
+    }
+    int t = v[0];
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    return t;
 }
 
 __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameState* __restrict__ fs,
                                                    const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
                                                    uint32_t* __restrict__ prm) {
     __shared__ SaoWave sw[4];
+    __shared__ unsigned long long part[3][4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ncu = g.mb_w * g.mb_h;
     const int i = blockIdx.x * 4 + wave;
@@ -1288,64 +1427,48 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     const int W = g.coded_w, H = g.coded_h, Wc = W / 2, Hc = H / 2;
     for (int k = lane; k < 96; k += 64) (&S.bo[0][0])[k] = 0;
     __syncthreads();
-    // ---- gather: luma 4 samples (3 x 6 window), chroma 1 sample per component (3 x 3 windows)
     const int r = lane >> 2, c0 = (lane & 3) * 4;
-    const int rc = lane >> 3, cc = lane & 7;
-    int L[3][6], C[2][3][3];
-    int ly[4] = {0, 0, 0, 0}, dy[4] = {0, 0, 0, 0}, lc[2] = {0, 0}, dc[2] = {0, 0};
+    const int xc = x0 / 2 + (lane & 7), yc = y0 / 2 + (lane >> 3);
+    // ---- statistics
     if (valid) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) L[j][q] = sao_px(ry, g.pitch, 1, W, H, x0 + c0 + q - 1, y0 + r + j - 1);
-        const uint32_t sv = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * g.pitch + x0 + c0);
+        int L[3][6];
+        sao_luma_window(ry, g.pitch, W, H, x0 + c0, y0 + r, L);
+        const uint32_t sv = *(const sao_gu32*)(src_y + (size_t)(y0 + r) * g.pitch + x0 + c0);
         int e[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) e[q] = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int c = L[1][1 + j];
-            const int d = (int)((sv >> (8 * j)) & 255) - c;
-            ly[j] = c;
-            dy[j] = d;
             int n[3][3];
 #pragma unroll
             for (int a = 0; a < 3; ++a)
 #pragma unroll
                 for (int b = 0; b < 3; ++b) n[a][b] = L[a][j + b];
-            sao_acc(e, c, d, n);
-            atomicAdd(&S.bo[0][c >> 3], (1 << 20) + d);
+            const int d = (int)((sv >> (8 * j)) & 255) - n[1][1];
+            sao_acc(e, d, n);
+            atomicAdd(&S.bo[0][n[1][1] >> 3], (1 << 20) + d);
         }
+        int t = sao_reduce16(e, lane);
+        if ((lane & 3) == 0) S.eo[0][(lane >> 2) & 15] = t;
+        int U[3][3], V[3][3];
+        sao_chroma_window(ruv, g.pitch, Wc, Hc, xc, yc, U, V);
+        const uint32_t spair = *(const sao_gu16*)(src_uv + (size_t)yc * g.pitch + 2 * xc);
+        const int du = (int)(spair & 255) - U[1][1], dv = (int)(spair >> 8) - V[1][1];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int t = wsum(e[q]);
-            if (lane == 0) S.eo[0][q] = t;
-        }
-        const int xc = x0 / 2 + cc, yc = y0 / 2 + rc;
+        for (int q = 0; q < 16; ++q) e[q] = 0;
+        sao_acc(e, du, U);
+        atomicAdd(&S.bo[1][U[1][1] >> 3], (1 << 20) + du);
+        t = sao_reduce16(e, lane);
+        if ((lane & 3) == 0) S.eo[1][(lane >> 2) & 15] = t;
 #pragma unroll
-        for (int comp = 0; comp < 2; ++comp) {
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    C[comp][a][b] = sao_px(ruv + comp, g.pitch, 2, Wc, Hc, xc + b - 1, yc + a - 1);
-            const int c = C[comp][1][1];
-            const int d = (int)src_uv[(size_t)yc * g.pitch + 2 * xc + comp] - c;
-            lc[comp] = c;
-            dc[comp] = d;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) e[q] = 0;
-            sao_acc(e, c, d, C[comp]);
-            atomicAdd(&S.bo[1 + comp][c >> 3], (1 << 20) + d);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int t = wsum(e[q]);
-                if (lane == 0) S.eo[1 + comp][q] = t;
-            }
-        }
+        for (int q = 0; q < 16; ++q) e[q] = 0;
+        sao_acc(e, dv, V);
+        atomicAdd(&S.bo[2][V[1][1] >> 3], (1 << 20) + dv);
+        t = sao_reduce16(e, lane);
+        if ((lane & 3) == 0) S.eo[2][(lane >> 2) & 15] = t;
     }
     __syncthreads();
-    // ---- candidates: offsets per (comp, class, category) and per (comp, band)
+    // ---- candidate offsets per (comp, class, category) and per (comp, band)
     const uint32_t lam16 = kLambdaSse16[fs->qp < 0 ? 0 : (fs->qp > 51 ? 51 : fs->qp)];
     if (valid) {
         if (lane < 48) {
@@ -1365,52 +1488,53 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         }
     }
     __syncthreads();
-    // ---- best band window per component: lexicographic min of (cost, position) over 32 lanes
+    // ---- per component: best band window (lexicographic min of (cost, position) over 32 lanes)
+    //      and the edge-class sums
     if (valid) {
         for (int pass = 0; pass < 2; ++pass) {
             const int comp = pass * 2 + (lane >> 5), p = lane & 31;
             const bool on = comp < 3;
-            long long j = 0;
+            int j = 0x7fffffff;
             if (on) j = S.jb[comp][p] + S.jb[comp][(p + 1) & 31] + S.jb[comp][(p + 2) & 31] + S.jb[comp][(p + 3) & 31];
             int bp = p;
             for (int o = 16; o > 0; o >>= 1) {
-                const long long jo = __shfl_xor(j, o, 64);
-                const int po = __shfl_xor(bp, o, 64);
+                const int jo = __shfl_xor(j, o, 64), po = __shfl_xor(bp, o, 64);
                 if (jo < j || (jo == j && po < bp)) {
                     j = jo;
                     bp = po;
                 }
             }
             if (on && p == 0) {
-                S.jwin[comp] = j;
-                S.band[comp] = bp;
+                SaoCompChoice& c = S.ch[comp];
+                c.j_bo = j;
+                c.band = bp;
+                for (int k = 0; k < 4; ++k) c.bo_off[k] = S.ob[comp][(bp + k) & 31];
             }
+        }
+        if (lane < 12) {
+            const int comp = lane >> 2, k = lane & 3;
+            SaoCompChoice& c = S.ch[comp];
+            c.j_eo[k] = S.jeo[comp][4 * k] + S.jeo[comp][4 * k + 1] + S.jeo[comp][4 * k + 2] + S.jeo[comp][4 * k + 3];
+            for (int q = 0; q < 4; ++q) c.eo_off[k][q] = S.oeo[comp][4 * k + q];
         }
     }
     __syncthreads();
     if (valid && lane == 0) {
-        SaoCompChoice ch[3];
-        for (int comp = 0; comp < 3; ++comp) {
-            for (int k = 0; k < 4; ++k) {
-                ch[comp].j_eo[k] = S.jeo[comp][4 * k] + S.jeo[comp][4 * k + 1] + S.jeo[comp][4 * k + 2] +
-                                   S.jeo[comp][4 * k + 3];
-                for (int q = 0; q < 4; ++q) ch[comp].eo_off[k][q] = S.oeo[comp][4 * k + q];
-            }
-            ch[comp].j_bo = S.jwin[comp];
-            ch[comp].band = S.band[comp];
-            for (int k = 0; k < 4; ++k) ch[comp].bo_off[k] = S.ob[comp][(S.band[comp] + k) & 31];
-        }
         uint32_t w[3];
-        sao_combine(ch[0], ch[1], ch[2], lam16, w);
+        sao_combine(S.ch[0], S.ch[1], S.ch[2], lam16, w);
         S.w[0] = w[0];
         S.w[1] = w[1];
         S.w[2] = w[2];
         *reinterpret_cast<uint4*>(prm + 4 * (size_t)i) = make_uint4(w[0], w[1], w[2], 0u);
     }
     __syncthreads();
-    // ---- apply into the output picture
+    // ---- apply into the output picture; distortion over the display area
+    int ey = 0, eu = 0, ev = 0;
     if (valid) {
         const uint32_t wy = S.w[0], wu = S.w[1], wv = S.w[2];
+        int L[3][6];
+        sao_luma_window(ry, g.pitch, W, H, x0 + c0, y0 + r, L);
+        const uint32_t sv = *(const sao_gu32*)(src_y + (size_t)(y0 + r) * g.pitch + x0 + c0);
         uint32_t packed = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1419,15 +1543,35 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
             for (int a = 0; a < 3; ++a)
 #pragma unroll
                 for (int b = 0; b < 3; ++b) n[a][b] = L[a][j + b];
-            packed |= (uint32_t)sao_out(wy, ly[j], n) << (8 * j);
+            const int o = sao_out3(wy, n);
+            packed |= (uint32_t)o << (8 * j);
+            const int d = (int)((sv >> (8 * j)) & 255) - o;
+            ey += (x0 + c0 + j < g.width && y0 + r < g.height) ? d * d : 0;
         }
-        *reinterpret_cast<uint32_t*>(fs->sao_y + (size_t)(y0 + r) * g.pitch + x0 + c0) = packed;
-        const int xc = x0 / 2 + cc, yc = y0 / 2 + rc;
-        const uint32_t u = (uint32_t)sao_out(wu, lc[0], C[0]), v = (uint32_t)sao_out(wv, lc[1], C[1]);
-        *reinterpret_cast<uint16_t*>(fs->sao_uv + (size_t)yc * g.pitch + 2 * xc) = (uint16_t)(u | (v << 8));
+        *(sao_gu32*)(fs->sao_y + (size_t)(y0 + r) * g.pitch + x0 + c0) = packed;
+        int U[3][3], V[3][3];
+        sao_chroma_window(ruv, g.pitch, Wc, Hc, xc, yc, U, V);
+        const int u = sao_out3(wu, U), v = sao_out3(wv, V);
+        *(sao_gu16*)(fs->sao_uv + (size_t)yc * g.pitch + 2 * xc) = (uint16_t)(u | (v << 8));
+        const uint32_t spair = *(const sao_gu16*)(src_uv + (size_t)yc * g.pitch + 2 * xc);
+        const bool disp = 2 * xc < g.width && 2 * yc < g.height;
+        const int du = (int)(spair & 255) - u, dv = (int)(spair >> 8) - v;
+        eu = disp ? du * du : 0;
+        ev = disp ? dv * dv : 0;
     }
-    (void)dy;
-    (void)dc;
+    ey = wsum(ey);
+    eu = wsum(eu);
+    ev = wsum(ev);
+    if (lane == 0) {
+        part[0][wave] = (unsigned long long)ey;
+        part[1][wave] = (unsigned long long)eu;
+        part[2][wave] = (unsigned long long)ev;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int c = threadIdx.x;
+        fs->sse_part[c * h264::kSsePartStride + blockIdx.x] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
+    }
 }
 
 // Distortion of the final (deblocked) picture over the display area: one workgroup per CTU
@@ -1453,8 +1597,8 @@ __global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameSta
         }
     };
     const int rows = min(16, g.height - r * 16), crows = min(8, g.height / 2 - r * 8);
-    const uint8_t* fy = fs->sao ? fs->sao_y : fs->rec_y;  // the final picture
-    const uint8_t* fuv = fs->sao ? fs->sao_uv : fs->rec_uv;
+    const uint8_t* fy = fs->rec_y;  // the final (deblocked) picture
+    const uint8_t* fuv = fs->rec_uv;
     for (int k = tid; k < rows * quads; k += 256) acc(src_y, fy, r * 16 + k / quads, k % quads, false);
     for (int k = tid; k < crows * quads; k += 256) acc(src_uv, fuv, r * 8 + k / quads, k % quads, true);
     for (int o = 32; o > 0; o >>= 1) {
@@ -1575,14 +1719,16 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
     }
-    if (sao) hipLaunchKernelGGL(k_hevc_sao, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.sao);
-    if (deblock || sao) hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
+    if (sao)  // SAO, with the final distortion (one partial per 4 CTBs)
+        hipLaunchKernelGGL(k_hevc_sao, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.sao);
+    else if (deblock)
+        hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
 }
 
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_cabac, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
-                       b.slice_cap, b.slice_len, b.slice_first, b.nslices, b.sao);
+                       b.slice_cap, b.slice_len, b.slice_first, b.nslices, b.sao, b.slice_clk);
     hipLaunchKernelGGL(k_hevc_pack, dim3(max_slices), dim3(256), 0, s, b.fs, b.nslices, b.slice_first, b.slice_data,
                        b.slice_cap, b.slice_len, host_out, b.out_bytes);
 }
