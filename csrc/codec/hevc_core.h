@@ -1746,7 +1746,10 @@ MXHD uint32_t cu_cost(const CuInfo& c) {
     if (c.cbf & 4) k += c.last[2] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_c[1]);
     return k;
 }
-constexpr uint32_t kCostPerSlice = 4096;  // below this much work per slice, fewer slices
+// Below this much work per slice, fewer slices.  One unit is about 0.35 us of k_hevc_cabac wave
+// time (tools/hevc_cabac_timing.py: 0.79 us per CU + 1.45 us per payload byte, 4K and 1080p), so
+// 1024 units keep a slice near 0.35 ms; the level's slice limit usually binds first at 4K.
+constexpr uint32_t kCostPerSlice = 1024;
 // Number of slices for a P picture of total cost T, bounded by the level's slice limit.
 MXHD int plan_num_slices(uint64_t total, int max_slices) {
     const uint64_t s = total / kCostPerSlice;

@@ -968,29 +968,35 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
 
 // ------------------------------------------------------------------ slice layout
 // One 1024-thread workgroup.  I pictures: fixed slices of slice_rows CTU rows.  P pictures:
-// cost-balanced raster runs (hevc_core.h plan_*): block prefix sum of cu_cost, slice id of
-// every CU from its exclusive prefix, starts compacted by a second scan.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
-    const int t = threadIdx.x, n = blockDim.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int o = 1; o < n; o <<= 1) {
-        const uint32_t add = t >= o ? sh[t - o] : 0u;
-        __syncthreads();
-        sh[t] += add;
-        __syncthreads();
+// cost-balanced raster runs (hevc_core.h plan_*): each thread owns a chunk of CUs; a wave-level
+// prefix sum of the chunk costs gives every CU its exclusive cost prefix, and the slice id
+// floor(prefix * S / total) is tracked against the next slice's threshold ceil(s * total / S), so
+// a 64-bit division happens per slice start rather than per CU (that division loop cost ~60 us at
+// 4K).  Starts are compacted by a second prefix sum.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wtot, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+    uint32_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
     }
-    const uint32_t incl = sh[t];
-    *total = sh[n - 1];
+    if (lane == 63) wtot[wave] = incl;
     __syncthreads();
-    return incl - v;
+    uint32_t before = 0, all = 0;
+    for (int w = 0; w < nw; ++w) {
+        before += w < wave ? wtot[w] : 0u;
+        all += wtot[w];
+    }
+    __syncthreads();
+    *total = all;
+    return before + incl - v;
 }
 
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ cost, int ncu, int ctb_w,
                                                        int max_slices, int* __restrict__ slice_first,
                                                        int* __restrict__ slice_of_cu, uint32_t* __restrict__ nslices) {
-    __shared__ uint32_t sh[1024];
+    __shared__ uint32_t wtot[16];
     const int tid = threadIdx.x;
     if (fs->idr) {
         const int sr = fs->slice_rows, S = fs->num_slices;
@@ -1004,28 +1010,37 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     uint32_t local = 0;
     for (int i = i0; i < i1; ++i) local += cost[i];
     uint32_t total;
-    const uint32_t pre0 = block_excl_scan(local, sh, &total);
+    const uint32_t pre0 = block_excl_scan(local, wtot, &total);
     const int S = plan_num_slices(total, max_slices);
-    // starts in this chunk
-    int prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
-    uint32_t pre = pre0, nst = 0;
-    for (int i = i0; i < i1; ++i) {
-        const int id = plan_slice_of(pre, total, S);
-        nst += id != prev;
-        prev = id;
-        pre += cost[i];
+    // slice id of a prefix p is the number of thresholds T_s = ceil(s * total / S) (s >= 1) <= p
+    auto thr = [&](int s2) -> uint64_t {
+        return s2 >= S ? ~0ull : ((uint64_t)s2 * total + (uint64_t)S - 1) / (uint64_t)S;
+    };
+    const int id0 = i0 < i1 ? plan_slice_of(pre0, total, S) : 0;
+    const int prev0 = i0 > 0 && i0 < i1 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
+    uint32_t nst = 0;
+    {
+        int cid = id0, prev = prev0;
+        uint64_t tnext = thr(cid + 1), pre = pre0;
+        for (int i = i0; i < i1; ++i) {
+            while (pre >= tnext) tnext = thr(++cid + 1);
+            nst += cid != prev;
+            prev = cid;
+            pre += cost[i];
+        }
     }
     uint32_t nstarts;
-    const uint32_t base = block_excl_scan(nst, sh, &nstarts);
-    prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
-    pre = pre0;
-    int rank = (int)base - 1;
-    for (int i = i0; i < i1; ++i) {
-        const int id = plan_slice_of(pre, total, S);
-        if (id != prev) slice_first[++rank] = i;
-        slice_of_cu[i] = rank;
-        prev = id;
-        pre += cost[i];
+    const uint32_t base = block_excl_scan(nst, wtot, &nstarts);
+    {
+        int cid = id0, prev = prev0, rank = (int)base - 1;
+        uint64_t tnext = thr(cid + 1), pre = pre0;
+        for (int i = i0; i < i1; ++i) {
+            while (pre >= tnext) tnext = thr(++cid + 1);
+            if (cid != prev) slice_first[++rank] = i;
+            slice_of_cu[i] = rank;
+            prev = cid;
+            pre += cost[i];
+        }
     }
     if (tid == 0) *nslices = nstarts;
 }
@@ -1411,6 +1426,14 @@ __device__ __forceinline__ int sao_reduce16(int* v, int lane) {
     return t;
 }
 
+// Each wave works on its own CTB: the phases only need the wave's own LDS writes visible
+// (LDS operations of a wave complete in order), not a workgroup barrier.
+__device__ __forceinline__ void sao_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameState* __restrict__ fs,
                                                    const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
                                                    uint32_t* __restrict__ prm) {
@@ -1426,7 +1449,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     const uint8_t* ruv = fs->rec_uv;
     const int W = g.coded_w, H = g.coded_h, Wc = W / 2, Hc = H / 2;
     for (int k = lane; k < 96; k += 64) (&S.bo[0][0])[k] = 0;
-    __syncthreads();
+    sao_wave_sync();
     const int r = lane >> 2, c0 = (lane & 3) * 4;
     const int xc = x0 / 2 + (lane & 7), yc = y0 / 2 + (lane >> 3);
     // ---- statistics
@@ -1467,7 +1490,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         t = sao_reduce16(e, lane);
         if ((lane & 3) == 0) S.eo[2][(lane >> 2) & 15] = t;
     }
-    __syncthreads();
+    sao_wave_sync();
     // ---- candidate offsets per (comp, class, category) and per (comp, band)
     const uint32_t lam16 = kLambdaSse16[fs->qp < 0 ? 0 : (fs->qp > 51 ? 51 : fs->qp)];
     if (valid) {
@@ -1487,7 +1510,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
             S.ob[comp][b] = o;
         }
     }
-    __syncthreads();
+    sao_wave_sync();
     // ---- per component: best band window (lexicographic min of (cost, position) over 32 lanes)
     //      and the edge-class sums
     if (valid) {
@@ -1518,7 +1541,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
             for (int q = 0; q < 4; ++q) c.eo_off[k][q] = S.oeo[comp][4 * k + q];
         }
     }
-    __syncthreads();
+    sao_wave_sync();
     if (valid && lane == 0) {
         uint32_t w[3];
         sao_combine(S.ch[0], S.ch[1], S.ch[2], lam16, w);
@@ -1527,7 +1550,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         S.w[2] = w[2];
         *reinterpret_cast<uint4*>(prm + 4 * (size_t)i) = make_uint4(w[0], w[1], w[2], 0u);
     }
-    __syncthreads();
+    sao_wave_sync();
     // ---- apply into the output picture; distortion over the display area
     int ey = 0, eu = 0, ev = 0;
     if (valid) {

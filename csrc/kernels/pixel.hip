@@ -770,9 +770,17 @@ __global__ __launch_bounds__(256) void k_sse_masked(const uint8_t* __restrict__ 
 
 }  // namespace
 
-int sse_masked_blocks(int w, int h) {
+// Rows per workgroup: at least one thread per 16-pixel quad, and at most ~128 workgroups so the
+// device-scope completion counter sees few atomics (one per workgroup, serialised in L2: with one
+// row per workgroup at 4K the 2160 atomics cost ~45 us of a 54 us kernel, profiles/r03_hevc).
+static int sse_masked_rows(int w, int h) {
     const int nq = (w + 15) >> 4;
     const int rows = nq >= 256 ? 1 : 256 / nq;
+    const int min_rows = (h + 127) / 128;
+    return rows > min_rows ? rows : min_rows;
+}
+int sse_masked_blocks(int w, int h) {
+    const int rows = sse_masked_rows(w, h);
     return (h + rows - 1) / rows;
 }
 
@@ -782,8 +790,7 @@ void launch_sse_masked(const uint8_t* a, const uint8_t* b, int pitch, int w, int
     if ((pitch & 15) != 0 || pitch < ((w + 15) & ~15) || (reinterpret_cast<uintptr_t>(a) & 15) ||
         (reinterpret_cast<uintptr_t>(b) & 15))
         throw std::invalid_argument("sse_masked: planes and pitch must be 16-byte aligned, pitch >= width");
-    const int nq = (w + 15) >> 4;
-    const int rows = nq >= 256 ? 1 : 256 / nq;
+    const int rows = sse_masked_rows(w, h);
     hipLaunchKernelGGL(k_sse_masked, dim3(sse_masked_blocks(w, h)), dim3(256), 0, stream, a, b, pitch, w, h, rows,
                        mx0, my0, mx1, my1, part, counter, host_out);
 }
