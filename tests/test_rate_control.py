@@ -57,10 +57,14 @@ def test_cbr_recovers_after_forced_idr(native):
 
 def test_cbr_hevc_shares_the_controller(native):
     fps, kbps = 30, 600
-    bits, qps, _ = _run(native, native.CpuHevcEncoder, 160, 96, fps, kbps, 25)
+    bits, qps, _ = _run(native, native.CpuHevcEncoder, 160, 96, fps, kbps, 40)
     T = kbps * 1000.0 / fps
     assert bits[0] < 8.0 * T
-    assert abs(bits[5:].mean() / T - 1.0) < 0.12, bits[5:].mean() / T
+    # fresh noise at the QP floor: the IDR and the first P pictures overspend and the controller
+    # pays the excess back over the drain window (frames 5-20 sit below the line, as H.264 does on
+    # this content), so the stream as a whole is on budget and the steady state is on the line
+    assert abs(bits.mean() / T - 1.0) < 0.08, bits.mean() / T
+    assert abs(bits[20:].mean() / T - 1.0) < 0.06, bits[20:].mean() / T
 
 
 def test_constant_qp_mode_untouched(native):
