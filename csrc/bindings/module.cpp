@@ -342,6 +342,7 @@ PYBIND11_MODULE(_native, m) {
         .def("set_bitrate", [](vp8::GpuVp8Encoder& e, int k) { e.common().set_bitrate(k); })
         .def_property_readonly("stats", &vp8::GpuVp8Encoder::last_stats);
 
+    m.def("hevc_token_selftest", &hevc::token_selftest, py::arg("seed"), py::arg("slices"));
     py::class_<hevc::CpuHevcEncoder>(m, "CpuHevcEncoder")
         .def(py::init<const h264::EncoderConfig&>())
         .def(

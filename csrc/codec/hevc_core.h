@@ -653,18 +653,22 @@ struct CabacEnc {
         n += pad;
         for (int i = n - 8; i >= 0; i -= 8) put_byte((v >> i) & 0xff);
     }
-    // k-th order Exp-Golomb, bypass coded (9.3.3.3): m ones, a zero, then k + m suffix bits
-    MXHD void egk(uint32_t v, int k) {
-        int m = 0;
-        while (v >= (1u << k)) {
-            v -= 1u << k;
-            ++k;
-            ++m;
-        }
-        bypass_bits((1u << m) - 1, m);
-        bypass_bits(v, k + 1);  // leading zero + k bits
-    }
 };
+
+// k-th order Exp-Golomb, bypass coded (9.3.3.3): m ones, a zero, then k + m suffix bits.  E is
+// the arithmetic coder (CabacEnc) or the bin recorder (BinRec) -- the syntax coders below are
+// templates over both.
+template <class E>
+MXHD void code_egk(E& e, uint32_t v, int k) {
+    int m = 0;
+    while (v >= (1u << k)) {
+        v -= 1u << k;
+        ++k;
+        ++m;
+    }
+    e.bypass_bits((1u << m) - 1, m);
+    e.bypass_bits(v, k + 1);  // leading zero + k bits
+}
 
 // ---------------------------------------------------------------- CU description
 enum CuType : uint8_t { kCuSkip = 0, kCuMerge = 1, kCuAmvp = 2, kCuIntra = 3 };
@@ -757,8 +761,8 @@ MXHD int last_group(int pos) {
 }
 MXHD int last_min(int g) { return g < 4 ? g : (1 << ((g >> 1) - 1)) * (2 + (g & 1)); }
 
-template <class Ctx>
-MXHD void code_last_prefix(CabacEnc& e, Ctx& ctx, int base, int pos, int log2n, int cidx) {
+template <class E, class Ctx>
+MXHD void code_last_prefix(E& e, Ctx& ctx, int base, int pos, int log2n, int cidx) {
     const int off = cidx ? 15 : 3 * (log2n - 2) + ((log2n - 1) >> 2);
     const int shift = cidx ? log2n - 2 : (log2n + 1) >> 2;
     const int prefix = last_group(pos);
@@ -766,19 +770,21 @@ MXHD void code_last_prefix(CabacEnc& e, Ctx& ctx, int base, int pos, int log2n, 
     for (int b = 0; b < prefix; ++b) e.bin(ctx, base + off + (b >> shift), 1);
     if (prefix < cmax) e.bin(ctx, base + off + (prefix >> shift), 0);
 }
-MXHD void code_last_suffix(CabacEnc& e, int pos) {
+template <class E>
+MXHD void code_last_suffix(E& e, int pos) {
     const int prefix = last_group(pos);
     if (prefix > 3) e.bypass_bits((uint32_t)(pos - last_min(prefix)), (prefix >> 1) - 1);
 }
 
 // coeff_abs_level_remaining (9.3.3.11)
-MXHD void code_remaining(CabacEnc& e, uint32_t v, int rice) {
+template <class E>
+MXHD void code_remaining(E& e, uint32_t v, int rice) {
     if (v < (4u << rice)) {
         const uint32_t pre = v >> rice;  // pre ones, a zero, rice LSBs
         e.bypass_bits((((1u << pre) - 1) << (rice + 1)) | (v & ((1u << rice) - 1)), (int)pre + 1 + rice);
     } else {
         e.bypass_bits(15, 4);
-        e.egk(v - (4u << rice), rice + 1);
+        code_egk(e, v - (4u << rice), rice + 1);
     }
 }
 
@@ -823,8 +829,8 @@ MXHD int tu_last(const Cf& cf, int sb0, int nsb, uint32_t* csbf) {
 }
 
 // One TU of size 2^log2n (4, 8 or 16; scanIdx 0) whose sub-blocks start at CU sub-block sb0.
-template <class Ctx, class Cf>
-MXHD void code_residual(CabacEnc& e, Ctx& ctx, const Cf& cf, int sb0, int log2n, int cidx, int last_idx,
+template <class E, class Ctx, class Cf>
+MXHD void code_residual(E& e, Ctx& ctx, const Cf& cf, int sb0, int log2n, int cidx, int last_idx,
                         uint32_t csbf_mask) {
     int lx, ly;
     scan_pos(log2n, last_idx, &lx, &ly);
@@ -939,19 +945,19 @@ MXHD void code_residual(CabacEnc& e, Ctx& ctx, const Cf& cf, int sb0, int log2n,
 }
 
 // ---------------------------------------------------------------- CU syntax (7.3.8.5)
-template <class Ctx>
-MXHD void code_mvd(CabacEnc& e, Ctx& ctx, int dx, int dy) {
+template <class E, class Ctx>
+MXHD void code_mvd(E& e, Ctx& ctx, int dx, int dy) {
     const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
     e.bin(ctx, C_MVD_G0, ax > 0);
     e.bin(ctx, C_MVD_G0, ay > 0);
     if (ax > 0) e.bin(ctx, C_MVD_G1, ax > 1);
     if (ay > 0) e.bin(ctx, C_MVD_G1, ay > 1);
     if (ax > 0) {
-        if (ax > 1) e.egk((uint32_t)(ax - 2), 1);
+        if (ax > 1) code_egk(e, (uint32_t)(ax - 2), 1);
         e.bypass(dx < 0);
     }
     if (ay > 0) {
-        if (ay > 1) e.egk((uint32_t)(ay - 2), 1);
+        if (ay > 1) code_egk(e, (uint32_t)(ay - 2), 1);
         e.bypass(dy < 0);
     }
 }
@@ -959,13 +965,13 @@ MXHD void code_mvd(CabacEnc& e, Ctx& ctx, int dx, int dy) {
 MXHD int qp_delta_wrap(int qp, int pred) { return ((qp - pred + 26 + 52) % 52) - 26; }
 
 // cu_qp_delta_abs (TU prefix of 5 context bins + EG0 suffix) and its sign
-template <class Ctx>
-MXHD void code_qp_delta(CabacEnc& e, Ctx& ctx, int d) {
+template <class E, class Ctx>
+MXHD void code_qp_delta(E& e, Ctx& ctx, int d) {
     const int a = d < 0 ? -d : d;
     const int pre = a < 5 ? a : 5;
     for (int k = 0; k < pre; ++k) e.bin(ctx, C_QP_DELTA + (k ? 1 : 0), 1);
     if (pre < 5) e.bin(ctx, C_QP_DELTA + (pre ? 1 : 0), 0);
-    if (a >= 5) e.egk((uint32_t)(a - 5), 0);
+    if (a >= 5) code_egk(e, (uint32_t)(a - 5), 0);
     if (a) e.bypass(d < 0);
 }
 
@@ -979,8 +985,8 @@ MXHD CuNb cu_nb(const CuInfo* left, const CuInfo* above) {
     return CuNb{left ? (int)left->type : -1, left ? (int)left->intra_mode : 1, above ? (int)above->type : -1};
 }
 
-template <class Ctx, class Cf>
-MXHD void code_cu(CabacEnc& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf& cf, CuNb nb, int& qp_prev,
+template <class E, class Ctx, class Cf>
+MXHD void code_cu(E& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf& cf, CuNb nb, int& qp_prev,
                   bool end_of_slice) {
     if (!islice) {
         const int inc = (nb.left_type == kCuSkip ? 1 : 0) + (nb.above_type == kCuSkip ? 1 : 0);
@@ -1264,8 +1270,8 @@ MXHD void sao_apply_block(const uint8_t* rec, uint8_t* out, int pitch, int step,
 // sao(rx, ry) syntax (7.3.8.3) of a CTB with parameters (p0, p1, p2); the left / up neighbour
 // CTB's parameters count only when it is in the slice (has_l / has_u).  Values, not pointers:
 // on the device every argument stays in (wave-uniform) registers.
-template <class Ctx>
-MXHD void code_sao_w(CabacEnc& e, Ctx& ctx, uint32_t p0, uint32_t p1, uint32_t p2, bool has_l, uint32_t l0,
+template <class E, class Ctx>
+MXHD void code_sao_w(E& e, Ctx& ctx, uint32_t p0, uint32_t p1, uint32_t p2, bool has_l, uint32_t l0,
                      uint32_t l1, uint32_t l2, bool has_u, uint32_t u0, uint32_t u1, uint32_t u2) {
     if (has_l) {
         const bool m = l0 == p0 && l1 == p1 && l2 == p2;
@@ -1301,16 +1307,127 @@ MXHD void code_sao_w(CabacEnc& e, Ctx& ctx, uint32_t p0, uint32_t p1, uint32_t p
         }
     }
 }
-template <class Ctx>
-MXHD void code_sao(CabacEnc& e, Ctx& ctx, const uint32_t* p, const uint32_t* left, const uint32_t* up) {
+template <class E, class Ctx>
+MXHD void code_sao(E& e, Ctx& ctx, const uint32_t* p, const uint32_t* left, const uint32_t* up) {
     code_sao_w(e, ctx, p[0], p[1], p[2], left != nullptr, left ? left[0] : 0u, left ? left[1] : 0u,
                left ? left[2] : 0u, up != nullptr, up ? up[0] : 0u, up ? up[1] : 0u, up ? up[2] : 0u);
 }
 
-// Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row).
-// Returns the number of payload bytes (> cap means overflow).
+// ---------------------------------------------------------------- bin tokens
+// Entropy coding in two phases: a CTU's syntax is first *binarised* into 16-bit tokens (which
+// bins, with which context -- a pure function of the CTU, its neighbours' descriptors and the
+// QP predictor, so every CTU of a picture can be binarised in parallel), then a slice's token
+// stream runs through the arithmetic coder, the only serial part (a short loop per token with
+// no syntax logic).  Token layout:
+//   bit 15 = 0: context-coded bin, bits 1..8 context index (kTokTerm: end_of_slice terminate
+//               bin), bit 0 the bin value;
+//   bit 15 = 1: a run of n = bits 11..14 + 1 (<= 11) bypass bins, value bits 0..10 (MSB first).
+constexpr uint32_t kTokTerm = 255;
+constexpr int kTokBypassMax = 11;
+// Upper bound of the tokens of one CTU: 24 coded sub-blocks of at most 1 csbf + 16 sig + 8 gt1 +
+// 1 gt2 + 2 sign + 16 * 5 remaining (escape prefix, EGk prefix and suffix split at 11 bins), plus
+// the last-position, CU and SAO syntax.
+constexpr uint32_t kMaxCuTokens = 24 * 108 + 256;
+
+// Records bins as tokens (same interface as CabacEnc).  Consecutive bypass bins are merged.
+struct BinRec {
+    uint16_t* out;
+    uint32_t n, cap;
+    uint32_t pv;
+    int pn;
+    MXHD void start(uint16_t* o, uint32_t c) {
+        out = o;
+        n = 0;
+        cap = c;
+        pv = 0;
+        pn = 0;
+    }
+    MXHD void put(uint32_t t) {
+        if (n < cap) out[n] = (uint16_t)t;
+        ++n;
+    }
+    MXHD void flush() {
+        if (pn) put(0x8000u | ((uint32_t)(pn - 1) << 11) | pv);
+        pv = 0;
+        pn = 0;
+    }
+    template <class Ctx>
+    MXHD void bin(Ctx&, int idx, int b) {
+        flush();
+        put(((uint32_t)idx << 1) | (uint32_t)b);
+    }
+    MXHD void terminate(int b) {
+        flush();
+        put((kTokTerm << 1) | (uint32_t)b);
+    }
+    MXHD void bypass_bits(uint32_t v, int n) {
+        while (n > 0) {
+            const int k = n < kTokBypassMax - pn ? n : kTokBypassMax - pn;
+            n -= k;
+            pv = (pv << k) | ((v >> n) & ((1u << k) - 1u));
+            pn += k;
+            if (pn == kTokBypassMax) flush();
+        }
+    }
+    MXHD void bypass(int b) { bypass_bits((uint32_t)b, 1); }
+};
+struct NoCtx {};
+
+// Token -> arithmetic coder.
+template <class Ctx>
+MXHD void code_token(CabacEnc& e, Ctx& ctx, uint32_t t) {
+    if (t & 0x8000u)
+        e.bypass_bits(t & 0x7ffu, (int)((t >> 11) & 15u) + 1);
+    else if ((t >> 1) == kTokTerm)
+        e.terminate((int)(t & 1u));
+    else
+        e.bin(ctx, (int)(t >> 1), (int)(t & 1u));
+}
+
+// Binarise CTU i (the k-th of a slice of `count` CTUs): SAO syntax (when sao != null), then the
+// CU, then end_of_slice_segment_flag.  qp_prev: QP predictor (QpY of the previous CU that coded a
+// residual in the slice, else the slice QP); updated as code_cu does.  Returns the token count
+// (> rec.cap: truncated).
+MXHD uint32_t binarise_ctu(BinRec& rec, bool islice, const CuInfo* cus, const int16_t* coef, const uint32_t* sao,
+                           int i, int k, int count, int ctb_w, int& qp_prev) {
+    NoCtx nc;
+    const int x = i % ctb_w;
+    const bool has_l = x > 0 && k > 0, has_u = k >= ctb_w;
+    if (sao)
+        code_sao(rec, nc, sao + 4 * (size_t)i, has_l ? sao + 4 * (size_t)(i - 1) : nullptr,
+                 has_u ? sao + 4 * (size_t)(i - ctb_w) : nullptr);
+    const CoefArray cf{coef + (size_t)i * kCoefPerCu};
+    code_cu(rec, nc, islice, cus[i], cf, cu_nb(has_l ? &cus[i - 1] : nullptr, has_u ? &cus[i - ctb_w] : nullptr),
+            qp_prev, k == count - 1);
+    rec.flush();
+    return rec.n;
+}
+
+// Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row)
+// through the token path (binarise every CTU, then run the tokens through the coder -- what
+// the GPU kernels do).  tok: scratch of kMaxCuTokens tokens.  Returns the payload bytes.
 MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
-                         int first, int count, int ctb_w, uint8_t* ctx_mem, const uint32_t* sao = nullptr) {
+                         int first, int count, int ctb_w, uint8_t* ctx_mem, const uint32_t* sao, uint16_t* tok) {
+    ctx_init_all(ctx_mem, islice ? 0 : 1, slice_qp);
+    ArrCtx ctx{ctx_mem};
+    CabacEnc e;
+    e.start(out, cap);
+    int qp_prev = slice_qp;
+    for (int k = 0; k < count; ++k) {
+        BinRec rec;
+        rec.start(tok, kMaxCuTokens);
+        const uint32_t n = binarise_ctu(rec, islice, cus, coef, sao, first + k, k, count, ctb_w, qp_prev);
+        for (uint32_t j = 0; j < n && j < kMaxCuTokens; ++j) code_token(e, ctx, tok[j]);
+    }
+    e.finish_slice();
+    return e.pos;
+}
+
+// The same slice coded directly (syntax coders driving the arithmetic coder, no tokens): the
+// reference the token path is tested against.
+MXHD uint32_t code_slice_direct(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus,
+                                const int16_t* coef, int first, int count, int ctb_w, uint8_t* ctx_mem,
+                                const uint32_t* sao = nullptr) {
     ctx_init_all(ctx_mem, islice ? 0 : 1, slice_qp);
     ArrCtx ctx{ctx_mem};
     CabacEnc e;

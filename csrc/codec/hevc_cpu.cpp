@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
+#include <string>
+#include <vector>
 
 #include "h264_mb.h"
 #include "hevc_encoder.h"
@@ -526,7 +528,8 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
             const int first = rows[s], count = (s + 1 < rows.size() ? rows[s + 1] : W * H) - first;
             const uint32_t cap = (uint32_t)count * 1024 + 1024;
             buf.resize(cap);
-            total += code_slice(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(), first, count, W, ctx) + 12;
+            total += code_slice(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(), first, count, W, ctx,
+                                nullptr, tok_.data()) + 12;
         }
         rc.add_probe(qp_override_, (int)total + 64);
         qp_override_ = -1;
@@ -588,7 +591,7 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         const uint32_t cap = (uint32_t)count * 1024 + 1024;
         buf.resize(cap);
         const uint32_t n = code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count, W, ctx,
-                                      cfg_.sao ? sao_.data() : nullptr);
+                                      cfg_.sao ? sao_.data() : nullptr, tok_.data());
         if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
         common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n);
     }
@@ -621,6 +624,77 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         for (int r = 0; r < ch_; ++r) std::memcpy(prev_src_.data() + (size_t)r * cw_, y + (size_t)r * pitch, cw_);
     }
     return au_;
+}
+
+}  // namespace hevc
+}  // namespace mx
+
+namespace mx {
+namespace hevc {
+
+// Random slices (every CU type, split and unsplit transform trees, levels up to the escape
+// range, SAO parameters) coded twice -- directly and through the bin-token path -- must give
+// identical bytes.  Returns the number of slices checked; throws on the first mismatch.
+int token_selftest(uint32_t seed, int slices) {
+    uint32_t r = seed * 2654435761u + 1u;
+    auto rnd = [&r](uint32_t n) {
+        r ^= r << 13;
+        r ^= r >> 17;
+        r ^= r << 5;
+        return n ? r % n : 0u;
+    };
+    const int ctb_w = 7;
+    for (int sl = 0; sl < slices; ++sl) {
+        const int count = 1 + (int)rnd(40);
+        const bool islice = rnd(4) == 0;
+        const int qp = 10 + (int)rnd(40);
+        std::vector<CuInfo> cus((size_t)count);
+        std::vector<int16_t> coef((size_t)count * kCoefPerCu, 0);
+        std::vector<uint32_t> sao((size_t)count * 4, 0);
+        for (int i = 0; i < count; ++i) {
+            CuInfo& c = cus[(size_t)i];
+            std::memset(&c, 0, sizeof c);
+            c.type = islice ? kCuIntra : (uint8_t)rnd(4);
+            c.intra_mode = (uint8_t)rnd(35);
+            c.qp = (uint8_t)(10 + rnd(40));
+            c.mvdx = (int16_t)((int)rnd(2000) - 1000);
+            c.mvdy = (int16_t)((int)rnd(64) - 32);
+            c.mvp_idx = (uint8_t)rnd(2);
+            c.tu_split = c.type == kCuIntra ? 0 : (uint8_t)rnd(3);
+            if (c.type != kCuSkip) {
+                const int density = (int)rnd(4);  // 0: empty, 1: sparse, 2: dense, 3: escapes
+                int16_t* co = coef.data() + (size_t)i * kCoefPerCu;
+                for (int k = 0; k < kCoefPerCu && density; ++k) {
+                    if (rnd(density == 1 ? 40 : 3)) continue;
+                    int v = 1 + (int)rnd(density == 3 ? 3000 : 4);
+                    if (density == 3 && rnd(50) == 0) v = 30000;
+                    co[k] = (int16_t)(rnd(2) ? -v : v);
+                }
+                cu_summarise(c, co);
+                if (c.type == kCuIntra && c.tu_split) c.tu_split = 0;
+            }
+            for (int w = 0; w < 3; ++w) {
+                const int kind = (int)rnd(4);
+                int off[4];
+                for (int k = 0; k < 4; ++k) off[k] = (int)rnd(15) - 7;
+                if (kind == 1) sao[(size_t)i * 4 + w] = sao_pack(1, 0, (int)rnd(32), off);
+                if (kind == 2) sao[(size_t)i * 4 + w] = sao_pack(2, (int)rnd(4), 0, off);
+                if (kind == 3 && i > 0) sao[(size_t)i * 4 + w] = sao[(size_t)(i - 1) * 4 + w];  // merge candidates
+            }
+        }
+        const bool use_sao = rnd(2) != 0;
+        const uint32_t cap = (uint32_t)count * 4096 + 1024;
+        std::vector<uint8_t> a(cap), b(cap);
+        std::vector<uint16_t> tok(kMaxCuTokens);
+        uint8_t ctx[C_NUM];
+        const uint32_t na = code_slice_direct(a.data(), cap, islice, qp, cus.data(), coef.data(), 0, count, ctb_w, ctx,
+                                              use_sao ? sao.data() : nullptr);
+        const uint32_t nb = code_slice(b.data(), cap, islice, qp, cus.data(), coef.data(), 0, count, ctb_w, ctx,
+                                       use_sao ? sao.data() : nullptr, tok.data());
+        if (na != nb || std::memcmp(a.data(), b.data(), na) != 0)
+            throw std::runtime_error("hevc token path differs from direct coding (slice " + std::to_string(sl) + ")");
+    }
+    return slices;
 }
 
 }  // namespace hevc

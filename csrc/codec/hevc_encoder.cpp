@@ -37,6 +37,11 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.qpc, ncu));
     HIP_CHECK(hipMalloc(&b.sao, sizeof(uint32_t) * 4 * (size_t)ncu));
     HIP_CHECK(hipMalloc(&b.slice_clk, sizeof(unsigned long long) * 2 * (size_t)ns));
+    HIP_CHECK(hipMalloc(&b.tok, sizeof(uint16_t) * kMaxCuTokens * (size_t)ncu));
+    HIP_CHECK(hipMalloc(&b.ntok, sizeof(uint32_t) * (size_t)ncu));
+    HIP_CHECK(hipMalloc(&b.tok_off, sizeof(uint32_t) * ((size_t)ncu + 1)));
+    // + one chunk of padding: k_hevc_arith reads whole 256-token chunks
+    HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
@@ -53,7 +58,8 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
                     (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
-                    (void*)b.sse_part, (void*)b.sao, (void*)b.slice_clk})
+                    (void*)b.sse_part, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
+                    (void*)b.tok_dense})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.me_fs_host) (void)hipHostFree(sl.me_fs_host);

@@ -60,6 +60,9 @@ class HevcCommon {
     int max_slices_ = 1;
 };
 
+// Direct vs bin-token CABAC on random slices (hevc_cpu.cpp); returns the slices checked.
+int token_selftest(uint32_t seed, int slices);
+
 class CpuHevcEncoder {
    public:
     explicit CpuHevcEncoder(const EncoderConfig& cfg);
@@ -92,6 +95,7 @@ class CpuHevcEncoder {
     std::vector<uint8_t> au_;
     std::vector<uint8_t> prev_src_;  // previous source luma (coded size), temporal AQ classes
     std::vector<uint32_t> sao_;      // SAO parameters, 4 words per CTB (hevc_core.h sao_pack)
+    std::vector<uint16_t> tok_ = std::vector<uint16_t>(kMaxCuTokens);  // bin tokens of one CTU
     FrameStats stats_;
 };
 
@@ -158,7 +162,11 @@ struct HevcDeviceBuffers {
     uint32_t* cost;          // [ncu] CABAC cost estimate (slice layout)
     uint8_t* qpc;            // [ncu] QP of CUs that code a residual, else 255 (QP chain)
     uint32_t* sao;           // [ncu][4] SAO parameters per CTB (hevc_core.h sao_pack; luma, Cb, Cr, 0)
-    unsigned long long* slice_clk;  // [max_slices][2] k_hevc_cabac start / end (wall_clock64, 100 MHz)
+    unsigned long long* slice_clk;  // [max_slices][2] k_hevc_arith start / end (wall_clock64, 100 MHz)
+    uint16_t* tok;                  // [ncu][kMaxCuTokens] bin tokens per CTU (k_hevc_bins)
+    uint32_t* ntok;                 // [ncu] token count per CTU
+    uint32_t* tok_off;              // [ncu + 1] exclusive prefix of ntok
+    uint16_t* tok_dense;            // [ncu * kMaxCuTokens + 512] tokens in decoding order
     size_t out_bytes;
     unsigned long long* sse_part;
 };

@@ -10,8 +10,10 @@
 //  * k_hevc_intra  one workgroup per slice, one wave per CTU row; the rows of a slice run
 //                  as a wavefront (row r two CTUs behind row r-1) with the left column
 //                  and the bottom rows of the row above exchanged through LDS.
-//  * k_hevc_cabac  one wave per slice running the shared CABAC CU coder (hevc_core.h
-//                  code_cu) in lockstep on wave-uniform state (see the section comment).
+//  * k_hevc_bins / k_hevc_tokscan / k_hevc_tokgather / k_hevc_arith  CABAC in two phases:
+//                  every CTU binarised at once (one thread per CTU, hevc_core.h
+//                  binarise_ctu) into bin tokens laid out densely in decoding order, then
+//                  one wave per slice runs its token run through the arithmetic coder.
 //  * k_hevc_layout / k_hevc_decide  slice layout (rows for I, cost-balanced raster runs for
 //                  P) and the per-slice skip / merge / AMVP decisions.
 //  * k_hevc_qpy + k_hevc_deblock + k_hevc_sse  in-loop deblocking (QP chain per slice, one
@@ -1061,99 +1063,124 @@ __global__ __launch_bounds__(256) void k_hevc_decide(Geometry g, const h264::MbI
 }
 
 // ------------------------------------------------------------------ CABAC
-// The whole wave runs the slice coder in lockstep on identical (wave-uniform) values, so
-// the arithmetic-coder state lives in SGPRs and every table lookup is a register read:
-//  * context states: lane l of r0/r1/r2 holds state 64*j + l, read with v_readlane and
-//    written with v_writelane (no memory round trip per bin);
-//  * rangeTabLps / transIdxLps: lane s holds row s (4 packed bytes / next state);
-//  * coefficients of the CU being coded: lane l holds levels l, 64+l, ..., 320+l; their
-//    significance / sign masks come from six ballots, magnitudes from v_readlane.
-struct LaneCtx {
-    uint32_t r0, r1, r2;
+// Two phases (hevc_core.h "bin tokens").  Binarisation is a pure function of a CTU, its
+// neighbours' descriptors and its QP predictor (qpy of the previous CTU in the slice), so
+// k_hevc_bins binarises every CTU of the picture at once, one thread per CTU, into a fixed slot
+// of kMaxCuTokens tokens; k_hevc_tokscan / k_hevc_tokgather lay the tokens of the picture out
+// densely in decoding order.  Only the arithmetic coder is serial: k_hevc_arith runs one wave per
+// slice over that slice's token run -- a short loop with no syntax logic, whose coder state lives
+// in SGPRs and whose 144 context states sit four to a lane in one VGPR (v_readlane /
+// v_writelane), so the serial part is a few dozen scalar instructions per token and fits the
+// instruction cache (the former single-phase kernel was 16 k instructions of CU syntax per wave
+// and took ~0.8 us per skipped CTU: profiles/r03_cabac).
+__global__ __launch_bounds__(256) void k_hevc_bins(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                    const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
+                                                    const uint32_t* __restrict__ sao,
+                                                    const int* __restrict__ slice_first,
+                                                    const int* __restrict__ slice_of_cu,
+                                                    const uint32_t* __restrict__ nslices,
+                                                    const uint8_t* __restrict__ qpy, uint16_t* __restrict__ tok,
+                                                    uint32_t* __restrict__ ntok) {
+    const int ncu = g.mb_w * g.mb_h;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ncu) return;
+    const int ns = (int)*nslices;
+    const int s = slice_of_cu[i];
+    const int first = slice_first[s];
+    const int end = s + 1 < ns ? slice_first[s + 1] : ncu;
+    const int k = i - first;
+    int qp_prev = k > 0 ? (int)qpy[i - 1] : fs->qp;
+    BinRec rec;
+    rec.start(tok + (size_t)i * kMaxCuTokens, kMaxCuTokens);
+    const uint32_t n = binarise_ctu(rec, fs->idr != 0, cus, coef, fs->sao ? sao : nullptr, i, k, end - first, g.mb_w,
+                                    qp_prev);
+    ntok[i] = n < kMaxCuTokens ? n : kMaxCuTokens;  // > cap cannot happen (kMaxCuTokens is a bound)
+}
+
+// Exclusive prefix of the token counts in decoding (raster) order: off[i], off[ncu] = total.
+// One 1024-thread workgroup, a chunk of consecutive CTUs per thread.
+__global__ __launch_bounds__(1024) void k_hevc_tokscan(const uint32_t* __restrict__ ntok, int ncu,
+                                                        uint32_t* __restrict__ off) {
+    __shared__ uint32_t wtot[16];
+    const int tid = threadIdx.x;
+    const int chunk = (ncu + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int i0 = min(ncu, tid * chunk), i1 = min(ncu, i0 + chunk);
+    uint32_t local = 0;
+    for (int i = i0; i < i1; ++i) local += ntok[i];
+    uint32_t total;
+    uint32_t pre = block_excl_scan(local, wtot, &total);
+    for (int i = i0; i < i1; ++i) {
+        off[i] = pre;
+        pre += ntok[i];
+    }
+    if (tid == 0) off[ncu] = total;
+}
+
+// One wave per CTU: copy its tokens from the fixed slot to the dense run.
+__global__ __launch_bounds__(256) void k_hevc_tokgather(const uint16_t* __restrict__ tok,
+                                                         const uint32_t* __restrict__ ntok,
+                                                         const uint32_t* __restrict__ off, int ncu,
+                                                         uint16_t* __restrict__ dense) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= ncu) return;
+    const uint32_t n = ntok[i], o = off[i];
+    const uint16_t* src = tok + (size_t)i * kMaxCuTokens;
+    for (uint32_t t = lane; t < n; t += 64) dense[o + t] = src[t];
+}
+
+// Context states for the serial coder: lane l of `st` holds states 4l .. 4l+3 (one byte each),
+// lane s of lps_row / next holds rangeTabLps[s][0..3] and transIdxLps[s].
+struct PackedCtx {
+    uint32_t st;
     uint32_t lps_row, next;
     int lane;
     __device__ __forceinline__ uint32_t get(int i) const {
-        const uint32_t v = i < 64 ? r0 : (i < 128 ? r1 : r2);
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, i & 63);
+        return ((uint32_t)__builtin_amdgcn_readlane((int)st, i >> 2) >> ((i & 3) * 8)) & 0xffu;
     }
     __device__ __forceinline__ void set(int i, uint32_t v) {
-        const bool me = lane == (i & 63);  // v_cndmask: only the owning lane takes the new state
-        if (i < 64)
-            r0 = me ? v : r0;
-        else if (i < 128)
-            r1 = me ? v : r1;
-        else
-            r2 = me ? v : r2;
+        const int sh = (i & 3) * 8;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)st, i >> 2);
+        const uint32_t nw = (w & ~(0xffu << sh)) | (v << sh);
+        st = lane == (i >> 2) ? nw : st;  // v_cndmask: only the owning lane takes the new word
     }
     __device__ __forceinline__ uint32_t lps(uint32_t s, uint32_t q) const {
-        return ((uint32_t)__builtin_amdgcn_readlane((int)lps_row, (int)s) >> (8 * q)) & 0xff;
+        return ((uint32_t)__builtin_amdgcn_readlane((int)lps_row, (int)s) >> (8 * q)) & 0xffu;
     }
     __device__ __forceinline__ uint32_t next_lps(uint32_t s) const {
         return (uint32_t)__builtin_amdgcn_readlane((int)next, (int)s);
     }
 };
 
-__device__ __forceinline__ uint64_t sel6(const uint64_t* v, int k) {
-    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : k == 3 ? v[3] : k == 4 ? v[4] : v[5];
-}
-__device__ __forceinline__ int sel6i(const int* v, int k) {
-    return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : k == 3 ? v[3] : k == 4 ? v[4] : v[5];
-}
-
-struct WaveCoef {
-    uint64_t sigm[6], negm[6];  // wave-uniform ballots
-    int a[6];                   // this lane's magnitudes
-    __device__ __forceinline__ uint32_t sig(int sb) const { return (uint32_t)(sel6(sigm, sb >> 2) >> ((sb & 3) * 16)) & 0xffffu; }
-    __device__ __forceinline__ uint32_t neg(int sb) const { return (uint32_t)(sel6(negm, sb >> 2) >> ((sb & 3) * 16)) & 0xffffu; }
-    __device__ __forceinline__ int absval(int i) const { return __builtin_amdgcn_readlane(sel6i(a, i >> 6), i & 63); }
-};
-
-__device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
-    // kCuWords dwords (CuInfo is 24 bytes, 4-byte aligned in the array) -> wave-uniform values
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(cus) + (size_t)i * kCuWords;
-    uint32_t w[kCuWords];
-    for (int k = 0; k < kCuWords; ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[k]);
-    CuInfo c;
-    __builtin_memcpy(&c, w, sizeof c);
-    return c;
-}
-
-// CU descriptors are staged through LDS kCabacChunk CUs at a time (one bulk vector load per
-// chunk: the descriptor words, the above CU's type and the SAO parameters of the CU and of the
-// CU above), so a skipped CU costs its few bins and no memory round trip; the levels of a coded
-// CU are loaded one coded CU ahead (the next coded CU found through a ballot of the chunk).
-constexpr int kCabacChunk = 128;
-struct CabacStage {
-    uint32_t w[kCabacChunk * kCuWords];
-    uint32_t above[kCabacChunk];  // type of the CU above (255: not in the slice)
-    uint4 sao[kCabacChunk];
-    uint4 sao_up[kCabacChunk];
-};
-
-__global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameState* __restrict__ fs,
-                                                    const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
-                                                    uint8_t* __restrict__ slice_data, uint32_t slice_cap,
-                                                    uint32_t* __restrict__ slice_len,
+// One wave per slice: the slice's dense token run through the arithmetic coder.  Tokens arrive
+// 256 at a time (8 bytes per lane, the next chunk in flight while this one is coded) and are
+// read out of the chunk with v_readlane.
+constexpr uint32_t kTokChunk = 256;
+__global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                    const uint16_t* __restrict__ dense,
+                                                    const uint32_t* __restrict__ off,
                                                     const int* __restrict__ slice_first,
                                                     const uint32_t* __restrict__ nslices,
-                                                    const uint32_t* __restrict__ sao,
+                                                    uint8_t* __restrict__ slice_data, uint32_t slice_cap,
+                                                    uint32_t* __restrict__ slice_len,
                                                     unsigned long long* __restrict__ slice_clk) {
-    __shared__ CabacStage st;
     const int s = blockIdx.x, lane = threadIdx.x;
     const int ns = (int)*nslices;
     if (s >= ns) return;
     const unsigned long long clk0 = wall_clock64();
-    const bool sao_on = fs->sao != 0;
+    const int ncu = g.mb_w * g.mb_h;
     const int first = slice_first[s];
-    const int count = (s + 1 < ns ? slice_first[s + 1] : g.mb_w * g.mb_h) - first;
-    const bool islice = fs->idr != 0;
+    const int end = s + 1 < ns ? slice_first[s + 1] : ncu;
+    const uint32_t t0 = uni(off[first]), t1 = uni(off[end]);
     const int qp = fs->qp;
-    LaneCtx ctx;
+    PackedCtx ctx;
     {
-        const int t = islice ? 0 : 1;
-        ctx.r0 = ctx_init_state(kCtxInit[t][lane], qp);
-        ctx.r1 = ctx_init_state(kCtxInit[t][64 + lane], qp);
-        ctx.r2 = 128 + lane < C_NUM ? ctx_init_state(kCtxInit[t][128 + lane], qp) : 0u;
+        const int t = fs->idr ? 0 : 1;
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int j = 4 * lane + b;
+            w |= (j < C_NUM ? (uint32_t)ctx_init_state(kCtxInit[t][j], qp) : 0u) << (8 * b);
+        }
+        ctx.st = w;
         ctx.lps_row = (uint32_t)kLps[lane][0] | ((uint32_t)kLps[lane][1] << 8) | ((uint32_t)kLps[lane][2] << 16) |
                       ((uint32_t)kLps[lane][3] << 24);
         ctx.next = kNextLps[lane];
@@ -1161,107 +1188,24 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(Geometry g, const HevcFrameSt
     }
     CabacEnc e;
     e.start(slice_data + (size_t)s * slice_cap, slice_cap);
-    int qp_prev = qp;
-    int prev_type = -1, prev_mode = 1;
-    uint32_t pl0 = 0u, pl1 = 0u, pl2 = 0u;  // SAO parameters of the previous CU (merge-left candidate)
-    const uint32_t* cuw = reinterpret_cast<const uint32_t*>(cus);
-    const uint4* sao4 = reinterpret_cast<const uint4*>(sao);
-    int vn[6] = {0, 0, 0, 0, 0, 0};
-    int pf = -1;  // CU whose levels are in vn (-1: none in flight)
-    for (int base = 0; base < count; base += kCabacChunk) {
-        const int n = min(kCabacChunk, count - base);
-        __syncthreads();  // the previous chunk's descriptors are no longer read
-        for (int t = lane; t < n * kCuWords; t += 64) st.w[t] = cuw[(size_t)(first + base) * kCuWords + t];
-        uint64_t coded_lo = 0, coded_hi = 0;  // CUs of the chunk with levels to code
-        for (int t = lane; t < kCabacChunk; t += 64) {
-            const int k = base + t, i = first + k;
-            bool coded = false;
-            if (t < n) {
-                const uint32_t w0 = cuw[(size_t)i * kCuWords];  // type, intra mode, qp, cbf
-                coded = (w0 & 0xff) != kCuSkip && (w0 >> 24) != 0;
-                st.above[t] = k >= g.mb_w ? (cuw[(size_t)(i - g.mb_w) * kCuWords] & 0xff) : 255u;
-                if (sao_on) {
-                    st.sao[t] = sao4[i];
-                    st.sao_up[t] = k >= g.mb_w ? sao4[i - g.mb_w] : make_uint4(0, 0, 0, 0);
-                }
-            }
-            const uint64_t m = __ballot(coded);
-            if (t < 64) coded_lo = m; else coded_hi = m;
+    const uint32_t a0 = t0 & ~3u;  // 8-byte aligned chunk starts
+    const uint2* src = reinterpret_cast<const uint2*>(dense + a0);
+    uint2 cur = src[lane];
+    for (uint32_t c = a0; c < t1; c += kTokChunk) {
+        const uint2 nxt = c + kTokChunk < t1 ? src[(c + kTokChunk - a0) / 4 + lane] : make_uint2(0u, 0u);
+        const uint32_t j0 = c < t0 ? t0 - c : 0u;
+        const uint32_t j1 = t1 - c < kTokChunk ? t1 - c : kTokChunk;
+        // the chunk's registers are consumed here, once: otherwise the wait for them lands inside the
+        // token loop as a vmcnt(0) that also drains the prefetch and the coder's byte stores
+        uint32_t cx = cur.x, cy = cur.y;
+        asm volatile("" : "+v"(cx), "+v"(cy));
+        for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t wx = (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)(j >> 2));
+            const uint32_t wy = (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)(j >> 2));
+            const uint32_t w = (j & 2) ? wy : wx;
+            code_token(e, ctx, uni((w >> ((j & 1) * 16)) & 0xffffu));
         }
-        __syncthreads();
-        auto next_coded = [&](int from) -> int {  // first coded CU of the chunk at index >= from
-            if (from < 64) {
-                const uint64_t m = coded_lo & (~0ull << from);
-                if (m) return __builtin_ctzll(m);
-                from = 64;
-            }
-            if (from < kCabacChunk) {
-                const uint64_t m = coded_hi & (~0ull << (from - 64));
-                if (m) return 64 + __builtin_ctzll(m);
-            }
-            return -1;
-        };
-        if (pf < 0) {
-            const int t0 = next_coded(0);
-            if (t0 >= 0) {
-                pf = first + base + t0;
-                for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)pf * kCoefPerCu + q * 64 + lane];
-            }
-        }
-        for (int t = 0; t < n; ++t) {
-            const int k = base + t, i = first + k;
-            const int x = i % g.mb_w;
-            CuInfo c;
-            {
-                uint32_t w[kCuWords];
-                for (int q = 0; q < kCuWords; ++q)
-                    w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)st.w[t * kCuWords + q]);
-                __builtin_memcpy(&c, w, sizeof c);
-            }
-            const bool use = c.type != kCuSkip && c.cbf;
-            WaveCoef cf;
-            if (use) {
-                int v[6];
-                for (int q = 0; q < 6; ++q) v[q] = vn[q];  // pf == i: every coded CU is prefetched
-                pf = -1;
-                const int tn = next_coded(t + 1);
-                if (tn >= 0) {
-                    pf = first + base + tn;
-                    for (int q = 0; q < 6; ++q) vn[q] = coef[(size_t)pf * kCoefPerCu + q * 64 + lane];
-                }
-                for (int q = 0; q < 6; ++q) {
-                    cf.sigm[q] = __ballot(v[q] != 0);
-                    cf.negm[q] = __ballot(v[q] < 0);
-                    cf.a[q] = v[q] < 0 ? -v[q] : v[q];
-                }
-            } else {
-                for (int q = 0; q < 6; ++q) {
-                    cf.sigm[q] = cf.negm[q] = 0ull;
-                    cf.a[q] = 0;
-                }
-            }
-            CuNb nb;
-            nb.left_type = (x > 0 && k > 0) ? prev_type : -1;
-            nb.left_mode = prev_mode;
-            const int up_t = (int)(uint32_t)__builtin_amdgcn_readfirstlane((int)st.above[t]);
-            nb.above_type = up_t == 255 ? -1 : up_t;
-            if (sao_on) {
-                const uint4 p4 = st.sao[t], u4 = st.sao_up[t];
-                const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p4.x),
-                               p1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p4.y),
-                               p2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p4.z);
-                code_sao_w(e, ctx, p0, p1, p2, x > 0 && k > 0, pl0, pl1, pl2, k >= g.mb_w,
-                           (uint32_t)__builtin_amdgcn_readfirstlane((int)u4.x),
-                           (uint32_t)__builtin_amdgcn_readfirstlane((int)u4.y),
-                           (uint32_t)__builtin_amdgcn_readfirstlane((int)u4.z));
-                pl0 = p0;
-                pl1 = p1;
-                pl2 = p2;
-            }
-            code_cu(e, ctx, islice, c, cf, nb, qp_prev, k == count - 1);
-            prev_type = c.type;
-            prev_mode = c.intra_mode;
-        }
+        cur = nxt;
     }
     e.finish_slice();
     if (lane == 0) {
@@ -1736,9 +1680,10 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
     if (!idr)
         hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
                            b.slice_of_cu, b.cu);
+    // QpY chain: the deblocking filter's QP and the entropy coder's QP predictor
+    hipLaunchKernelGGL(k_hevc_qpy, dim3(max_slices), dim3(256), 0, s, b.fs, b.qpc, ncu, b.slice_first, b.nslices,
+                       b.qpy);
     if (deblock) {
-        hipLaunchKernelGGL(k_hevc_qpy, dim3(max_slices), dim3(256), 0, s, b.fs, b.qpc, ncu, b.slice_first, b.nslices,
-                           b.qpy);
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
     }
@@ -1750,8 +1695,14 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
 
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_hevc_cabac, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.slice_data,
-                       b.slice_cap, b.slice_len, b.slice_first, b.nslices, b.sao, b.slice_clk);
+    const int ncu = g.mb_w * g.mb_h;
+    hipLaunchKernelGGL(k_hevc_bins, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.coef, b.sao,
+                       b.slice_first, b.slice_of_cu, b.nslices, b.qpy, b.tok, b.ntok);
+    hipLaunchKernelGGL(k_hevc_tokscan, dim3(1), dim3(1024), 0, s, b.ntok, ncu, b.tok_off);
+    hipLaunchKernelGGL(k_hevc_tokgather, dim3((ncu + 3) / 4), dim3(256), 0, s, b.tok, b.ntok, b.tok_off, ncu,
+                       b.tok_dense);
+    hipLaunchKernelGGL(k_hevc_arith, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.tok_dense, b.tok_off,
+                       b.slice_first, b.nslices, b.slice_data, b.slice_cap, b.slice_len, b.slice_clk);
     hipLaunchKernelGGL(k_hevc_pack, dim3(max_slices), dim3(256), 0, s, b.fs, b.nslices, b.slice_first, b.slice_data,
                        b.slice_cap, b.slice_len, host_out, b.out_bytes);
 }

@@ -6,6 +6,7 @@
 # OUT is a directory name under gpurun_out/.  Steps run in order; every GPU step has its own
 # time limit, and the script stops at the first failure, time-out, abort or crash.
 #   tests               pytest -m gpu (one process)
+#   pytest:NAME:ARGS    pytest -m gpu ARGS (test files / -k filters) -> OUT/pytest_NAME.log
 #   smoke               __graft_entry__.smoke()
 #   bench:NAME[:ARGS]   python bench.py ARGS  -> OUT/NAME.json  (ARGS: comma-separated flags)
 #   prof:NAME[:ARGS]    rocprofv3 --kernel-trace --stats around bench.py ARGS -> OUT/prof_NAME/
@@ -32,6 +33,10 @@ for step in "$@"; do
         tests)
             timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 240 --timeout-method thread \
                 > "$OUT/pytest_gpu.log" 2>&1 || fail "pytest rc=$?" ;;
+        pytest)
+            # shellcheck disable=SC2046
+            timeout -k 10 600 python -u -m pytest -x -v -m gpu --timeout 240 --timeout-method thread $(args_of "$extra") \
+                > "$OUT/pytest_$name.log" 2>&1 || fail "pytest $name rc=$?" ;;
         smoke)
             timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
                 || fail "smoke rc=$?" ;;
