@@ -136,6 +136,8 @@ def main() -> None:
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse the "
                          "multi-rank plumbing with several ranks on one GPU)")
+    ap.add_argument("--py-loop", type=int, default=0,
+                    help="1: drive a single session from this Python thread instead of the native session driver")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
     if args.codec == "vp8":
@@ -199,11 +201,12 @@ def main() -> None:
     sessions = [N.Session(cfg) for _ in range(K)]
 
     def run(n_frames: int, record: bool):
-        """n_frames per session, up to `depth` frames in flight each.  K > 1: one native host
-        thread per session (mxdesk runtime run_sessions); K == 1: this thread."""
+        """n_frames per session, up to `depth` frames in flight each, driven by the native session
+        runtime (run_sessions: one host thread per session, submit / collect in C++ -- as the
+        serving path's pipeline thread does); --py-loop 1: this Python thread."""
         out = []
         depth = max(1, args.depth)
-        if K > 1:
+        if K > 1 or not args.py_loop:
             per = N.run_sessions(sessions, n_frames, depth)
             if record:
                 for f in range(n_frames):

@@ -3,6 +3,8 @@
 #include "h264_encoder.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -332,12 +334,22 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
-    if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
+    if (depth_ > 1) {
+        HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
+        const char* hv = std::getenv("MXDESK_HANDOFF");
+        if (hv && std::string(hv) == "value") {
+            void* p = nullptr;
+            HIP_CHECK(hipExtMallocWithFlags(&p, 64, hipMallocSignalMemory));
+            hand_seq_ = static_cast<uint32_t*>(p);
+            HIP_CHECK(hipMemsetAsync(hand_seq_, 0, 4, stream_));
+        }
+    }
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 GpuH264Encoder::~GpuH264Encoder() {
     (void)hipStreamSynchronize(stream_);
+    if (hand_seq_) (void)hipFree(hand_seq_);
     if (stream_e_) {
         (void)hipStreamSynchronize(stream_e_);
         (void)hipStreamDestroy(stream_e_);
@@ -366,8 +378,17 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     }
     hipStream_t es = stream_;
     if (stream_e_) {  // entropy of this frame overlaps the analysis of the next one
-        HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
-        HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+        if (hand_seq_) {
+            // hand-off through a signal-memory word: the analysis stream writes the frame's
+            // sequence number, the entropy stream's WAIT_REG_MEM polls it (an event wait on an
+            // idle queue resolved only ~14 us later, at the next doorbell: profiles/r03_h264)
+            ++hand_val_;
+            HIP_CHECK(hipStreamWriteValue32(stream_, hand_seq_, hand_val_, 0));
+            HIP_CHECK(hipStreamWaitValue32(stream_e_, hand_seq_, hand_val_, hipStreamWaitValueGte, 0xffffffffu));
+        } else {
+            HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
+            HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+        }
         es = stream_e_;
     }
     hipEvent_t sse_ready = nullptr;

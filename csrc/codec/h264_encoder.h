@@ -226,6 +226,8 @@ class GpuH264Encoder final : public VideoEncoder {
     EncoderCommon common_;
     hipStream_t stream_;
     hipStream_t stream_e_ = nullptr;  // entropy stream (depth 2)
+    uint32_t* hand_seq_ = nullptr;    // analysis -> entropy hand-off word (MXDESK_HANDOFF=value)
+    uint32_t hand_val_ = 0;
     int depth_ = 1;
     Geometry geom_;
     FrameSlot slots_[kMaxInFlight];

@@ -828,119 +828,161 @@ MXHD int tu_last(const Cf& cf, int sb0, int nsb, uint32_t* csbf) {
     return last;
 }
 
-// One TU of size 2^log2n (4, 8 or 16; scanIdx 0) whose sub-blocks start at CU sub-block sb0.
-template <class E, class Ctx, class Cf>
-MXHD void code_residual(E& e, Ctx& ctx, const Cf& cf, int sb0, int log2n, int cidx, int last_idx,
-                        uint32_t csbf_mask) {
+// One TU of a CU for the residual coder: size 2^log2n (4, 8 or 16; scanIdx 0), sub-blocks from
+// CU sub-block sb0, last significant scan index, coded sub-blocks (bit = scan index in the TU).
+struct TuDesc {
+    int sb0, log2n, cidx, last_idx;
+    uint32_t csbf_mask;
+};
+// coded (or inferred: DC and last) sub-blocks of a TU as a raster mask
+MXHD uint32_t tu_csbf_raster(const TuDesc& t) {
+    const int last_sb = t.last_idx >> 4, sbw = 1 << (t.log2n - 2);
+    uint32_t r = 0;
+    for (int i = 0; i <= last_sb; ++i) {
+        const int sx = t.log2n == 4 ? diag4x(i) : (i >> 1), sy = t.log2n == 4 ? diag4y(i) : (i & 1);
+        if (i == 0 || i == last_sb || ((t.csbf_mask >> i) & 1)) r |= 1u << (sy * sbw + sx);
+    }
+    return r;
+}
+
+// last_sig_coeff_x / _y prefix and suffix of a TU
+template <class E, class Ctx>
+MXHD void code_tu_last(E& e, Ctx& ctx, const TuDesc& t) {
     int lx, ly;
-    scan_pos(log2n, last_idx, &lx, &ly);
-    code_last_prefix(e, ctx, C_LAST_X, lx, log2n, cidx);
-    code_last_prefix(e, ctx, C_LAST_Y, ly, log2n, cidx);
+    scan_pos(t.log2n, t.last_idx, &lx, &ly);
+    code_last_prefix(e, ctx, C_LAST_X, lx, t.log2n, t.cidx);
+    code_last_prefix(e, ctx, C_LAST_Y, ly, t.log2n, t.cidx);
     code_last_suffix(e, lx);
     code_last_suffix(e, ly);
-    const int last_sb = last_idx >> 4, last_n = last_idx & 15;
-    const int sbw = 1 << (log2n - 2);  // sub-blocks per row
-    // coded_sub_block_flag per raster sub-block: coded / inferred (DC and last sub-block)
-    uint32_t csbf_r = 0;
-    for (int i = 0; i <= last_sb; ++i) {
-        const int sx = log2n == 4 ? diag4x(i) : (i >> 1), sy = log2n == 4 ? diag4y(i) : (i & 1);
-        if (i == 0 || i == last_sb || ((csbf_mask >> i) & 1)) csbf_r |= 1u << (sy * sbw + sx);
+}
+
+// greater1Ctx after a sub-block with levels is 0 iff one of its first 8 coded levels (scan
+// positions high to low) exceeds 1: the next coded sub-block of the TU then uses ctxSet + 1.
+template <class Cf>
+MXHD bool sb_any_gt1(const Cf& cf, int sb, uint32_t sig) {
+    int k = 0;
+    for (uint32_t m = sig; m && k < 8; ++k) {
+        const int n = msb16(m);
+        m &= ~(1u << n);
+        if (cf.absval(sb * 16 + n) > 1) return true;
     }
-    int g1ctx_prev = -1;  // greater1Ctx carried from the previous sub-block with levels (-1: none yet)
-    for (int i = last_sb; i >= 0; --i) {
-        const int sx = log2n == 4 ? diag4x(i) : (i >> 1), sy = log2n == 4 ? diag4y(i) : (i & 1);
-        const bool right = sx + 1 < sbw && ((csbf_r >> (sy * sbw + sx + 1)) & 1);
-        const bool below = sy + 1 < sbw && ((csbf_r >> ((sy + 1) * sbw + sx)) & 1);
-        bool infer_dc = false;
-        if (i < last_sb && i > 0) {
-            const int coded = (csbf_mask >> i) & 1;
-            e.bin(ctx, C_CSBF + (cidx ? 2 : 0) + ((right || below) ? 1 : 0), coded);
-            if (!coded) continue;
-            infer_dc = true;
-        }
-        const uint32_t sig = cf.sig(sb0 + i);
-        // significance
-        const int prev_csbf = (right ? 1 : 0) | (below ? 2 : 0);
-        const int nstart = (i == last_sb) ? last_n - 1 : 15;
-        for (int n = nstart; n >= 0; --n) {
-            if (n == 0 && infer_dc) break;
-            const int bit = (sig >> n) & 1;
-            const int xp = diag4x(n), yp = diag4y(n);
-            int sc;
-            if (log2n == 2) {
-                sc = kCtxIdxMap4x4[(yp << 2) + xp];
-            } else if (i == 0 && n == 0) {
-                sc = 0;
+    return false;
+}
+
+// Sub-block i of TU t (coded_sub_block_flag, significance, greater1 / greater2, signs, remaining
+// levels).  csbf_r: tu_csbf_raster(t).  prev_gt1: for the previous sub-block with levels in this
+// TU (coding order), whether it had a greater1 flag set (sb_any_gt1); -1: none.  Every sub-block
+// of a TU is independent given these, so the GPU binarises them in parallel.
+template <class E, class Ctx, class Cf>
+MXHD void code_sub_block(E& e, Ctx& ctx, const Cf& cf, const TuDesc& t, uint32_t csbf_r, int i, int prev_gt1) {
+    const int log2n = t.log2n, cidx = t.cidx;
+    const int last_sb = t.last_idx >> 4, last_n = t.last_idx & 15;
+    const int sbw = 1 << (log2n - 2);
+    const int sx = log2n == 4 ? diag4x(i) : (i >> 1), sy = log2n == 4 ? diag4y(i) : (i & 1);
+    const bool right = sx + 1 < sbw && ((csbf_r >> (sy * sbw + sx + 1)) & 1);
+    const bool below = sy + 1 < sbw && ((csbf_r >> ((sy + 1) * sbw + sx)) & 1);
+    bool infer_dc = false;
+    if (i < last_sb && i > 0) {
+        const int coded = (t.csbf_mask >> i) & 1;
+        e.bin(ctx, C_CSBF + (cidx ? 2 : 0) + ((right || below) ? 1 : 0), coded);
+        if (!coded) return;
+        infer_dc = true;
+    }
+    const uint32_t sig = cf.sig(t.sb0 + i);
+    // significance
+    const int prev_csbf = (right ? 1 : 0) | (below ? 2 : 0);
+    const int nstart = (i == last_sb) ? last_n - 1 : 15;
+    for (int n = nstart; n >= 0; --n) {
+        if (n == 0 && infer_dc) break;
+        const int bit = (sig >> n) & 1;
+        const int xp = diag4x(n), yp = diag4y(n);
+        int sc;
+        if (log2n == 2) {
+            sc = kCtxIdxMap4x4[(yp << 2) + xp];
+        } else if (i == 0 && n == 0) {
+            sc = 0;
+        } else {
+            if (prev_csbf == 0)
+                sc = (xp + yp == 0) ? 2 : (xp + yp < 3 ? 1 : 0);
+            else if (prev_csbf == 1)
+                sc = yp == 0 ? 2 : (yp == 1 ? 1 : 0);
+            else if (prev_csbf == 2)
+                sc = xp == 0 ? 2 : (xp == 1 ? 1 : 0);
+            else
+                sc = 2;
+            if (cidx == 0) {
+                if (i > 0) sc += 3;
+                sc += log2n == 3 ? 9 : 21;
             } else {
-                if (prev_csbf == 0)
-                    sc = (xp + yp == 0) ? 2 : (xp + yp < 3 ? 1 : 0);
-                else if (prev_csbf == 1)
-                    sc = yp == 0 ? 2 : (yp == 1 ? 1 : 0);
-                else if (prev_csbf == 2)
-                    sc = xp == 0 ? 2 : (xp == 1 ? 1 : 0);
-                else
-                    sc = 2;
-                if (cidx == 0) {
-                    if (i > 0) sc += 3;
-                    sc += log2n == 3 ? 9 : 21;
-                } else {
-                    sc += log2n == 3 ? 9 : 12;
-                }
+                sc += log2n == 3 ? 9 : 12;
             }
-            e.bin(ctx, C_SIG + (cidx ? 27 : 0) + sc, bit);
-            if (bit) infer_dc = false;
         }
-        if (!sig) continue;
-        // levels of the nonzero coefficients, n = 15 down to 0 (greater1 flags for the first 8)
-        const int base_i = (sb0 + i) * 16;
-        int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
-        if (g1ctx_prev == 0) ++ctx_set;
-        int g1ctx = 1, g2_pos = -1, k = 0;
-        for (uint32_t m = sig; m && k < 8; ++k) {
+        e.bin(ctx, C_SIG + (cidx ? 27 : 0) + sc, bit);
+        if (bit) infer_dc = false;
+    }
+    if (!sig) return;
+    // levels of the nonzero coefficients, n = 15 down to 0 (greater1 flags for the first 8)
+    const int base_i = (t.sb0 + i) * 16;
+    int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+    if (prev_gt1 == 1) ++ctx_set;
+    int g1ctx = 1, g2_pos = -1, k = 0;
+    for (uint32_t m = sig; m && k < 8; ++k) {
+        const int n = msb16(m);
+        m &= ~(1u << n);
+        const int g1 = cf.absval(base_i + n) > 1 ? 1 : 0;
+        e.bin(ctx, C_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + (g1ctx < 3 ? g1ctx : 3), g1);
+        if (g1) {
+            g1ctx = 0;
+            if (g2_pos < 0) g2_pos = n;
+        } else if (g1ctx > 0) {
+            ++g1ctx;
+        }
+    }
+    if (g2_pos >= 0) e.bin(ctx, C_GT2 + (cidx ? 4 : 0) + ctx_set, cf.absval(base_i + g2_pos) > 2);
+    {  // sign bits of the nonzero levels, n = 15 down to 0, as one bypass run
+        const uint32_t neg = cf.neg(t.sb0 + i);
+        uint32_t bits = 0;
+        int nb = 0;
+        for (uint32_t m = sig; m; ++nb) {
             const int n = msb16(m);
             m &= ~(1u << n);
-            const int g1 = cf.absval(base_i + n) > 1 ? 1 : 0;
-            e.bin(ctx, C_GT1 + (cidx ? 16 : 0) + ctx_set * 4 + (g1ctx < 3 ? g1ctx : 3), g1);
-            if (g1) {
-                g1ctx = 0;
-                if (g2_pos < 0) g2_pos = n;
-            } else if (g1ctx > 0) {
-                ++g1ctx;
-            }
+            bits = (bits << 1) | ((neg >> n) & 1);
         }
-        g1ctx_prev = g1ctx;
-        if (g2_pos >= 0) e.bin(ctx, C_GT2 + (cidx ? 4 : 0) + ctx_set, cf.absval(base_i + g2_pos) > 2);
-        {  // sign bits of the nonzero levels, n = 15 down to 0, as one bypass run
-            const uint32_t neg = cf.neg(sb0 + i);
-            uint32_t bits = 0;
-            int nb = 0;
-            for (uint32_t m = sig; m; ++nb) {
-                const int n = msb16(m);
-                m &= ~(1u << n);
-                bits = (bits << 1) | ((neg >> n) & 1);
-            }
-            e.bypass_bits(bits, nb);
+        e.bypass_bits(bits, nb);
+    }
+    int rice = 0;
+    k = 0;
+    for (uint32_t m = sig; m; ++k) {
+        const int n = msb16(m);
+        m &= ~(1u << n);
+        if (k < 8 && n != g2_pos && g2_pos < 0) continue;  // all levels 1: nothing left to code
+        const int a = cf.absval(base_i + n);
+        int base, thr;
+        if (k < 8) {
+            base = 1 + (a > 1 ? 1 : 0) + (n == g2_pos && a > 2 ? 1 : 0);
+            thr = (n == g2_pos) ? 3 : 2;
+        } else {
+            base = 1;
+            thr = 1;
         }
-        int rice = 0;
-        k = 0;
-        for (uint32_t m = sig; m; ++k) {
-            const int n = msb16(m);
-            m &= ~(1u << n);
-            if (k < 8 && n != g2_pos && g2_pos < 0) continue;  // all levels 1: nothing left to code
-            const int a = cf.absval(base_i + n);
-            int base, thr;
-            if (k < 8) {
-                base = 1 + (a > 1 ? 1 : 0) + (n == g2_pos && a > 2 ? 1 : 0);
-                thr = (n == g2_pos) ? 3 : 2;
-            } else {
-                base = 1;
-                thr = 1;
-            }
-            if (base == thr) {
-                code_remaining(e, (uint32_t)(a - base), rice);
-                if (a > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
-            }
+        if (base == thr) {
+            code_remaining(e, (uint32_t)(a - base), rice);
+            if (a > 3 * (1 << rice)) rice = rice + 1 < 4 ? rice + 1 : 4;
         }
+    }
+}
+
+// One TU: last position, then its sub-blocks from the last one down to the DC sub-block.
+template <class E, class Ctx, class Cf>
+MXHD void code_residual(E& e, Ctx& ctx, const Cf& cf, const TuDesc& t) {
+    code_tu_last(e, ctx, t);
+    const uint32_t csbf_r = tu_csbf_raster(t);
+    int prev_gt1 = -1;
+    for (int i = t.last_idx >> 4; i >= 0; --i) {
+        code_sub_block(e, ctx, cf, t, csbf_r, i, prev_gt1);
+        const uint32_t sig = cf.sig(t.sb0 + i);
+        if (sig && (i == 0 || i == (t.last_idx >> 4) || ((t.csbf_mask >> i) & 1)))
+            prev_gt1 = sb_any_gt1(cf, t.sb0 + i, sig) ? 1 : 0;
     }
 }
 
@@ -985,93 +1027,136 @@ MXHD CuNb cu_nb(const CuInfo* left, const CuInfo* above) {
     return CuNb{left ? (int)left->type : -1, left ? (int)left->intra_mode : 1, above ? (int)above->type : -1};
 }
 
-template <class E, class Ctx, class Cf>
-MXHD void code_cu(E& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf& cf, CuNb nb, int& qp_prev,
-                  bool end_of_slice) {
+// How a CU's residual is laid out after its header (code_cu_head): none, one transform unit
+// per component (cbf flags and cu_qp_delta already in the head), or the depth-1 transform tree
+// (four children, each with its own cbf flags; cu_qp_delta with the first coded child).
+enum CuResidual { kResNone = 0, kResFlat = 1, kResSplit = 2 };
+MXHD int cu_residual_kind(const CuInfo& c) {
+    if (c.type == kCuSkip) return kResNone;
+    const bool intra = c.type == kCuIntra;
+    const bool root = c.type != kCuAmvp || c.cbf != 0;
+    if (!root) return kResNone;
+    if (!intra && c.tu_split == 2) return kResSplit;
+    return c.cbf ? kResFlat : kResNone;
+}
+
+// CU syntax up to its residual: skip / prediction / motion, rqt_root_cbf, split_transform_flag,
+// and for an unsplit tree the cbf flags and cu_qp_delta; for a split tree the parent's chroma cbf.
+template <class E, class Ctx>
+MXHD void code_cu_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, CuNb nb, int qp_prev) {
     if (!islice) {
         const int inc = (nb.left_type == kCuSkip ? 1 : 0) + (nb.above_type == kCuSkip ? 1 : 0);
         e.bin(ctx, C_SKIP + inc, c.type == kCuSkip);
     }
-    if (c.type != kCuSkip) {
-        const bool intra = c.type == kCuIntra;
-        if (!islice) e.bin(ctx, C_PRED_MODE, intra);
-        e.bin(ctx, C_PART_MODE, 1);  // PART_2Nx2N
-        if (intra) {
-            const int cand_a = nb.left_type == kCuIntra ? nb.left_mode : 1;
-            int l[3];
-            mpm_list(cand_a, 1, l);
-            const int m = c.intra_mode;
-            const int hit = (m == l[0]) ? 0 : (m == l[1] ? 1 : (m == l[2] ? 2 : -1));
-            e.bin(ctx, C_PREV_INTRA, hit >= 0);
-            if (hit >= 0) {
-                e.bypass(hit > 0);
-                if (hit > 0) e.bypass(hit > 1);
-            } else {
-                int rem = m;
-                for (int k = 0; k < 3; ++k) rem -= (l[k] < m) ? 1 : 0;
-                e.bypass_bits((uint32_t)rem, 5);
-            }
-            e.bin(ctx, C_CHROMA_PRED, 0);  // intra_chroma_pred_mode 4 (DM)
+    if (c.type == kCuSkip) return;
+    const bool intra = c.type == kCuIntra;
+    if (!islice) e.bin(ctx, C_PRED_MODE, intra);
+    e.bin(ctx, C_PART_MODE, 1);  // PART_2Nx2N
+    if (intra) {
+        const int cand_a = nb.left_type == kCuIntra ? nb.left_mode : 1;
+        int l[3];
+        mpm_list(cand_a, 1, l);
+        const int m = c.intra_mode;
+        const int hit = (m == l[0]) ? 0 : (m == l[1] ? 1 : (m == l[2] ? 2 : -1));
+        e.bin(ctx, C_PREV_INTRA, hit >= 0);
+        if (hit >= 0) {
+            e.bypass(hit > 0);
+            if (hit > 0) e.bypass(hit > 1);
         } else {
-            const bool merge = c.type == kCuMerge;
-            e.bin(ctx, C_MERGE_FLAG, merge);
-            if (!merge) {
-                code_mvd(e, ctx, c.mvdx, c.mvdy);
-                e.bin(ctx, C_MVP, c.mvp_idx);
-            }
+            int rem = m;
+            for (int k = 0; k < 3; ++k) rem -= (l[k] < m) ? 1 : 0;
+            e.bypass_bits((uint32_t)rem, 5);
         }
-        bool root = true;
-        if (c.type == kCuAmvp) {
-            root = c.cbf != 0;
-            e.bin(ctx, C_RQT_ROOT, root);
-        }
-        if (root && !intra && c.tu_split) e.bin(ctx, C_SPLIT_TRANSFORM + 1, c.tu_split == 2);  // 5 - log2(16)
-        if (root && !intra && c.tu_split == 2) {
-            // transform_tree depth 1: per 8x8 child cbf_cb / cbf_cr (if the parent's is set),
-            // cbf_luma, then its transform_unit; cu_qp_delta with the first coded TU
-            const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1;
-            e.bin(ctx, C_CBF_CHROMA + 0, cb);
-            e.bin(ctx, C_CBF_CHROMA + 0, cr);
-            bool qp_done = false;
-#pragma unroll 1
-            for (int k = 0; k < 4; ++k) {
-                const int yk = (c.cbf_y4 >> k) & 1, cbk = (c.cbf_c4 >> k) & 1, crk = (c.cbf_c4 >> (4 + k)) & 1;
-                if (cb) e.bin(ctx, C_CBF_CHROMA + 1, cbk);
-                if (cr) e.bin(ctx, C_CBF_CHROMA + 1, crk);
-                e.bin(ctx, C_CBF_LUMA + 0, yk);
-                if ((yk | cbk | crk) && !qp_done) {
-                    code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
-                    qp_prev = c.qp;
-                    qp_done = true;
-                }
-#pragma unroll 1
-                for (int t = 0; t < 3; ++t) {
-                    if (!((t == 0 ? yk : (t == 1 ? cbk : crk)))) continue;
-                    const int sb0 = t == 0 ? 4 * k : (t == 1 ? 16 + k : 20 + k);
-                    uint32_t csbf;
-                    const int last = tu_last(cf, sb0, t == 0 ? 4 : 1, &csbf);
-                    code_residual(e, ctx, cf, sb0, t == 0 ? 3 : 2, t, last, csbf);
-                }
-            }
-        } else if (root) {
-            const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
-            e.bin(ctx, C_CBF_CHROMA + 0, cb);
-            e.bin(ctx, C_CBF_CHROMA + 0, cr);
-            if (intra || cb || cr) e.bin(ctx, C_CBF_LUMA + 1, cy);
-            if (c.cbf) {
-                code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
-                qp_prev = c.qp;
-                // one call site for the three TUs keeps the (inlined) device code small
-#pragma unroll 1
-                for (int t = 0; t < 3; ++t) {
-                    if (!((c.cbf >> t) & 1)) continue;
-                    const int last = t == 0 ? c.last[0] : (t == 1 ? c.last[1] : c.last[2]);
-                    const uint32_t csbf = t == 0 ? c.csbf_y : (t == 1 ? c.csbf_c[0] : c.csbf_c[1]);
-                    code_residual(e, ctx, cf, t == 0 ? 0 : (t == 1 ? 16 : 20), t == 0 ? 4 : 3, t, last, csbf);
-                }
-            }
+        e.bin(ctx, C_CHROMA_PRED, 0);  // intra_chroma_pred_mode 4 (DM)
+    } else {
+        const bool merge = c.type == kCuMerge;
+        e.bin(ctx, C_MERGE_FLAG, merge);
+        if (!merge) {
+            code_mvd(e, ctx, c.mvdx, c.mvdy);
+            e.bin(ctx, C_MVP, c.mvp_idx);
         }
     }
+    bool root = true;
+    if (c.type == kCuAmvp) {
+        root = c.cbf != 0;
+        e.bin(ctx, C_RQT_ROOT, root);
+    }
+    if (!root) return;
+    if (!intra && c.tu_split) e.bin(ctx, C_SPLIT_TRANSFORM + 1, c.tu_split == 2);  // 5 - log2(16)
+    const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
+    e.bin(ctx, C_CBF_CHROMA + 0, cb);
+    e.bin(ctx, C_CBF_CHROMA + 0, cr);
+    if (!intra && c.tu_split == 2) return;
+    if (intra || cb || cr) e.bin(ctx, C_CBF_LUMA + 1, cy);
+    if (c.cbf) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
+}
+
+// Split tree: child k's cbf_cb / cbf_cr (when the parent's is set) and cbf_luma, then
+// cu_qp_delta when k is the first child with a coded TU.
+MXHD int split_first_coded_child(const CuInfo& c) {
+    for (int k = 0; k < 4; ++k)
+        if (((c.cbf_y4 >> k) & 1) | ((c.cbf_c4 >> k) & 1) | ((c.cbf_c4 >> (4 + k)) & 1)) return k;
+    return 4;
+}
+template <class E, class Ctx>
+MXHD void code_child_head(E& e, Ctx& ctx, const CuInfo& c, int k, int qp_prev) {
+    const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1;
+    const int yk = (c.cbf_y4 >> k) & 1, cbk = (c.cbf_c4 >> k) & 1, crk = (c.cbf_c4 >> (4 + k)) & 1;
+    if (cb) e.bin(ctx, C_CBF_CHROMA + 1, cbk);
+    if (cr) e.bin(ctx, C_CBF_CHROMA + 1, crk);
+    e.bin(ctx, C_CBF_LUMA + 0, yk);
+    if (k == split_first_coded_child(c)) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
+}
+// Whether TU t (0 Y, 1 Cb, 2 Cr) of split child k is coded, and its first CU sub-block.
+MXHD bool split_tu_coded(const CuInfo& c, int k, int t) {
+    return t == 0 ? ((c.cbf_y4 >> k) & 1) : ((c.cbf_c4 >> (t == 1 ? k : 4 + k)) & 1);
+}
+MXHD int split_tu_sb0(int k, int t) { return t == 0 ? 4 * k : (t == 1 ? 16 + k : 20 + k); }
+// TU descriptor of a split child's TU / an unsplit CU's TU
+template <class Cf>
+MXHD TuDesc split_tu_desc(const Cf& cf, int k, int t) {
+    TuDesc d;
+    d.sb0 = split_tu_sb0(k, t);
+    d.log2n = t == 0 ? 3 : 2;
+    d.cidx = t;
+    d.last_idx = tu_last(cf, d.sb0, t == 0 ? 4 : 1, &d.csbf_mask);
+    return d;
+}
+MXHD TuDesc flat_tu_desc(const CuInfo& c, int t) {
+    TuDesc d;
+    d.sb0 = t == 0 ? 0 : (t == 1 ? 16 : 20);
+    d.log2n = t == 0 ? 4 : 3;
+    d.cidx = t;
+    d.last_idx = t == 0 ? c.last[0] : (t == 1 ? c.last[1] : c.last[2]);
+    d.csbf_mask = t == 0 ? c.csbf_y : (t == 1 ? c.csbf_c[0] : c.csbf_c[1]);
+    return d;
+}
+// QP predictor of the next CU: c.qp when c coded cu_qp_delta
+MXHD int cu_next_qp_prev(const CuInfo& c, int qp_prev) {
+    return (cu_residual_kind(c) != kResNone && c.cbf) ? (int)c.qp : qp_prev;
+}
+
+// The whole CU: head, residual TUs, end_of_slice_segment_flag.
+template <class E, class Ctx, class Cf>
+MXHD void code_cu(E& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf& cf, CuNb nb, int& qp_prev,
+                  bool end_of_slice) {
+    code_cu_head(e, ctx, islice, c, nb, qp_prev);
+    const int kind = cu_residual_kind(c);
+    if (kind == kResSplit) {
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            code_child_head(e, ctx, c, k, qp_prev);
+#pragma unroll 1
+            for (int t = 0; t < 3; ++t)
+                if (split_tu_coded(c, k, t)) code_residual(e, ctx, cf, split_tu_desc(cf, k, t));
+        }
+    } else if (kind == kResFlat) {
+        // one call site for the three TUs keeps the (inlined) device code small
+#pragma unroll 1
+        for (int t = 0; t < 3; ++t)
+            if ((c.cbf >> t) & 1) code_residual(e, ctx, cf, flat_tu_desc(c, t));
+    }
+    qp_prev = cu_next_qp_prev(c, qp_prev);
     e.terminate(end_of_slice ? 1 : 0);
 }
 
@@ -1384,22 +1469,105 @@ MXHD void code_token(CabacEnc& e, Ctx& ctx, uint32_t t) {
         e.bin(ctx, (int)(t >> 1), (int)(t & 1u));
 }
 
-// Binarise CTU i (the k-th of a slice of `count` CTUs): SAO syntax (when sao != null), then the
-// CU, then end_of_slice_segment_flag.  qp_prev: QP predictor (QpY of the previous CU that coded a
-// residual in the slice, else the slice QP); updated as code_cu does.  Returns the token count
-// (> rec.cap: truncated).
+// A CTU's token stream is the concatenation of independent *parts* in coding order: the head
+// (SAO + code_cu_head), per split child its cbf / cu_qp_delta head, per TU its last position and
+// its sub-blocks (last to DC), and the end_of_slice_segment_flag.  Each part depends only on
+// the CTU's data, so the GPU binarises one part per lane (k_hevc_bins); the CPU walks them in
+// order.  At most 1 + 4 + 12 + 24 + 1 = 42 parts; a part is at most kPartTokens tokens.
+enum PartKind { kPartHead = 0, kPartChild = 1, kPartTuLast = 2, kPartSb = 3, kPartEnd = 4 };
+struct CtuPart {
+    int kind, k, t, i;  // split child, component TU, sub-block index within the TU
+    TuDesc d;           // TU of kPartTuLast / kPartSb
+};
+constexpr int kMaxCtuParts = 42;
+constexpr uint32_t kPartTokens = 112;
+
+// Calls f(part) for every part of CU c in coding order; returns the number of parts.
+template <class Cf, class F>
+MXHD int for_each_part(const CuInfo& c, const Cf& cf, F f) {
+    int n = 0;
+    CtuPart pt;
+    pt.kind = kPartHead;
+    pt.k = pt.t = pt.i = 0;
+    f(pt, n++);
+    const int kind = cu_residual_kind(c);
+#pragma unroll 1
+    for (int k = 0; k < (kind == kResSplit ? 4 : 1); ++k) {
+        if (kind == kResNone) break;
+        if (kind == kResSplit) {
+            pt.kind = kPartChild;
+            pt.k = k;
+            f(pt, n++);
+        }
+#pragma unroll 1
+        for (int t = 0; t < 3; ++t) {
+            const bool coded = kind == kResSplit ? split_tu_coded(c, k, t) : (((c.cbf >> t) & 1) != 0);
+            if (!coded) continue;
+            pt.d = kind == kResSplit ? split_tu_desc(cf, k, t) : flat_tu_desc(c, t);
+            pt.k = k;
+            pt.t = t;
+            pt.kind = kPartTuLast;
+            f(pt, n++);
+            pt.kind = kPartSb;
+#pragma unroll 1
+            for (int i = pt.d.last_idx >> 4; i >= 0; --i) {
+                pt.i = i;
+                f(pt, n++);
+            }
+        }
+    }
+    pt.kind = kPartEnd;
+    f(pt, n++);
+    return n;
+}
+
+// Binarise one part of CTU i (the k-th of a slice of `count` CTUs; qp_prev: its QP predictor).
+template <class E, class Cf>
+MXHD void binarise_part(E& rec, const CtuPart& pt, bool islice, const CuInfo* cus, const Cf& cf,
+                        const uint32_t* sao, int i, int k, int count, int ctb_w, int qp_prev) {
+    NoCtx nc;
+    const CuInfo& c = cus[i];
+    if (pt.kind == kPartHead) {
+        const int x = i % ctb_w;
+        const bool has_l = x > 0 && k > 0, has_u = k >= ctb_w;
+        if (sao)
+            code_sao(rec, nc, sao + 4 * (size_t)i, has_l ? sao + 4 * (size_t)(i - 1) : nullptr,
+                     has_u ? sao + 4 * (size_t)(i - ctb_w) : nullptr);
+        code_cu_head(rec, nc, islice, c, cu_nb(has_l ? &cus[i - 1] : nullptr, has_u ? &cus[i - ctb_w] : nullptr),
+                     qp_prev);
+    } else if (pt.kind == kPartChild) {
+        code_child_head(rec, nc, c, pt.k, qp_prev);
+    } else if (pt.kind == kPartTuLast) {
+        code_tu_last(rec, nc, pt.d);
+    } else if (pt.kind == kPartSb) {
+        // the previous sub-block with levels in this TU (coding order: higher scan index)
+        const int last_sb = pt.d.last_idx >> 4;
+        int prev_gt1 = -1;
+        for (int j = pt.i + 1; j <= last_sb; ++j) {
+            if (!(j == last_sb || ((pt.d.csbf_mask >> j) & 1))) continue;
+            const uint32_t sg = cf.sig(pt.d.sb0 + j);
+            if (!sg) continue;
+            prev_gt1 = sb_any_gt1(cf, pt.d.sb0 + j, sg) ? 1 : 0;
+            break;
+        }
+        code_sub_block(rec, nc, cf, pt.d, tu_csbf_raster(pt.d), pt.i, prev_gt1);
+    } else {
+        rec.terminate(k == count - 1 ? 1 : 0);
+    }
+    rec.flush();
+}
+
+// Binarise CTU i (the k-th of a slice of `count` CTUs) part by part.  qp_prev: QP predictor
+// (QpY of the previous CU that coded a residual in the slice, else the slice QP); updated as
+// code_cu does.  Returns the token count (> rec.cap: truncated).
 MXHD uint32_t binarise_ctu(BinRec& rec, bool islice, const CuInfo* cus, const int16_t* coef, const uint32_t* sao,
                            int i, int k, int count, int ctb_w, int& qp_prev) {
-    NoCtx nc;
-    const int x = i % ctb_w;
-    const bool has_l = x > 0 && k > 0, has_u = k >= ctb_w;
-    if (sao)
-        code_sao(rec, nc, sao + 4 * (size_t)i, has_l ? sao + 4 * (size_t)(i - 1) : nullptr,
-                 has_u ? sao + 4 * (size_t)(i - ctb_w) : nullptr);
     const CoefArray cf{coef + (size_t)i * kCoefPerCu};
-    code_cu(rec, nc, islice, cus[i], cf, cu_nb(has_l ? &cus[i - 1] : nullptr, has_u ? &cus[i - ctb_w] : nullptr),
-            qp_prev, k == count - 1);
-    rec.flush();
+    const int qp_in = qp_prev;
+    for_each_part(cus[i], cf, [&](const CtuPart& pt, int) {
+        binarise_part(rec, pt, islice, cus, cf, sao, i, k, count, ctb_w, qp_in);
+    });
+    qp_prev = cu_next_qp_prev(cus[i], qp_prev);
     return rec.n;
 }
 
@@ -1874,8 +2042,16 @@ MXHD int plan_num_slices(uint64_t total, int max_slices) {
 }
 // Slice of a CU whose exclusive cost prefix is `pre`: floor(pre * S / T) -- non-decreasing in
 // raster order, so every slice is a raster run and equal-cost runs share the work evenly.
+// floor(num / den) for num < 2^52 through one double division and an exact integer fix-up (a
+// 64-bit integer division is a ~150-instruction loop on the GPU)
+MXHD uint64_t floor_div52(uint64_t num, uint64_t den) {
+    uint64_t q = (uint64_t)((double)num / (double)den);
+    if (q * den > num) --q;
+    else if ((q + 1) * den <= num) ++q;
+    return q;
+}
 MXHD int plan_slice_of(uint64_t pre, uint64_t total, int S) {
-    const uint64_t id = pre * (uint64_t)S / total;
+    const uint64_t id = floor_div52(pre * (uint64_t)S, total);
     return id >= (uint64_t)S ? S - 1 : (int)id;
 }
 

@@ -33,13 +33,17 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.slice_of_cu, sizeof(int) * ncu));
     HIP_CHECK(hipMalloc(&b.nslices, sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&b.qpy, ncu));
-    HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * ncu));
+    // per-CU arrays scanned in 4096-CU tiles of 16-byte loads: padded with zeros to a whole tile
+    const size_t ncu_pad = ((size_t)ncu + kScanTilePad - 1) / kScanTilePad * kScanTilePad + 4;
+    HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * ncu_pad));
+    HIP_CHECK(hipMemsetAsync(b.cost, 0, sizeof(uint32_t) * ncu_pad, stream_));
     HIP_CHECK(hipMalloc(&b.qpc, ncu));
     HIP_CHECK(hipMalloc(&b.sao, sizeof(uint32_t) * 4 * (size_t)ncu));
     HIP_CHECK(hipMalloc(&b.slice_clk, sizeof(unsigned long long) * 2 * (size_t)ns));
     HIP_CHECK(hipMalloc(&b.tok, sizeof(uint16_t) * kMaxCuTokens * (size_t)ncu));
-    HIP_CHECK(hipMalloc(&b.ntok, sizeof(uint32_t) * (size_t)ncu));
-    HIP_CHECK(hipMalloc(&b.tok_off, sizeof(uint32_t) * ((size_t)ncu + 1)));
+    HIP_CHECK(hipMalloc(&b.ntok, sizeof(uint32_t) * ncu_pad));
+    HIP_CHECK(hipMemsetAsync(b.ntok, 0, sizeof(uint32_t) * ncu_pad, stream_));
+    HIP_CHECK(hipMalloc(&b.tok_off, sizeof(uint32_t) * ncu_pad));
     // + one chunk of padding: k_hevc_arith reads whole 256-token chunks
     HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));

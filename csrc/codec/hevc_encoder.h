@@ -143,6 +143,7 @@ struct HevcOutHeader {
 };
 static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
+constexpr size_t kScanTilePad = 4096;  // per-CU scan arrays padded to this (hevc_kernels.hip kScanTile)
 constexpr int kMaxSliceRows = 4;  // CTU rows per slice the intra wavefront kernel supports
 // host buffer: header | slice payload offset[kMaxSlices] | length[] | first CTU[] | payloads
 constexpr size_t kOutPayloadOffset = sizeof(HevcOutHeader) + 3 * kMaxSlices * sizeof(uint32_t);

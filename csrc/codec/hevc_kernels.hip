@@ -11,8 +11,8 @@
 //                  as a wavefront (row r two CTUs behind row r-1) with the left column
 //                  and the bottom rows of the row above exchanged through LDS.
 //  * k_hevc_bins / k_hevc_tokscan / k_hevc_tokgather / k_hevc_arith  CABAC in two phases:
-//                  every CTU binarised at once (one thread per CTU, hevc_core.h
-//                  binarise_ctu) into bin tokens laid out densely in decoding order, then
+//                  every CTU binarised at once (one wave per CTU, one lane per syntax part,
+//                  hevc_core.h binarise_part) into bin tokens laid out densely in decoding order, then
 //                  one wave per slice runs its token run through the arithmetic coder.
 //  * k_hevc_layout / k_hevc_decide  slice layout (rows for I, cost-balanced raster runs for
 //                  P) and the per-slice skip / merge / AMVP decisions.
@@ -23,6 +23,8 @@
 //                  pinned host memory at 16-byte aligned offsets; workgroup 0 writes the
 //                  header (lengths, overflow, distortion totals).
 #include <hip/hip_runtime.h>
+
+#include <stdexcept>
 
 #include "h264_core.h"
 #include "h264_gpu.h"
@@ -994,6 +996,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wtot, 
     return before + incl - v;
 }
 
+// Scans over per-CU arrays run in tiles of 1024 threads x 4 consecutive CUs (arrays padded with
+// zeros to a whole tile: HevcDeviceBuffers).
+constexpr int kScanTile = 4096;
+constexpr int kMaxScanTiles = 64;
+__device__ __forceinline__ uint4 ld4(const uint32_t* p, int i) { return *reinterpret_cast<const uint4*>(p + i); }
+
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ cost, int ncu, int ctb_w,
                                                        int max_slices, int* __restrict__ slice_first,
@@ -1007,44 +1015,62 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
         if (tid == 0) *nslices = (uint32_t)S;
         return;
     }
-    const int chunk = (ncu + (int)blockDim.x - 1) / (int)blockDim.x;
-    const int i0 = min(ncu, tid * chunk), i1 = min(ncu, i0 + chunk);
-    uint32_t local = 0;
-    for (int i = i0; i < i1; ++i) local += cost[i];
-    uint32_t total;
-    const uint32_t pre0 = block_excl_scan(local, wtot, &total);
+    // tiles of kScanTile CUs, 4 consecutive per thread with one 16-byte load (coalesced; the
+    // former per-thread contiguous chunks made every load touch 64 cache lines of one CU's
+    // memory pipeline: 67 us at 4K).  Pass 1: per-tile prefixes and the total.
+    __shared__ uint32_t tile_pre[kMaxScanTiles];
+    uint32_t carry = 0;
+    int nt = 0;
+    for (int base = 0; base < ncu; base += kScanTile, ++nt) {
+        const uint4 v = ld4(cost, base + 4 * tid);
+        uint32_t tt;
+        (void)block_excl_scan(v.x + v.y + v.z + v.w, wtot, &tt);
+        if (tid == 0) tile_pre[nt] = carry;
+        carry += tt;
+    }
+    __syncthreads();
+    const uint32_t total = carry;
     const int S = plan_num_slices(total, max_slices);
-    // slice id of a prefix p is the number of thresholds T_s = ceil(s * total / S) (s >= 1) <= p
+    // slice id of a prefix p is the number of thresholds T_s = ceil(s * total / S) (s >= 1) <= p:
+    // one division per thread and tile, then threshold tracking across its 4 CUs
     auto thr = [&](int s2) -> uint64_t {
-        return s2 >= S ? ~0ull : ((uint64_t)s2 * total + (uint64_t)S - 1) / (uint64_t)S;
+        return s2 >= S ? ~0ull : floor_div52((uint64_t)s2 * total + (uint64_t)S - 1, (uint64_t)S);
     };
-    const int id0 = i0 < i1 ? plan_slice_of(pre0, total, S) : 0;
-    const int prev0 = i0 > 0 && i0 < i1 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
-    uint32_t nst = 0;
-    {
-        int cid = id0, prev = prev0;
-        uint64_t tnext = thr(cid + 1), pre = pre0;
-        for (int i = i0; i < i1; ++i) {
-            while (pre >= tnext) tnext = thr(++cid + 1);
-            nst += cid != prev;
-            prev = cid;
-            pre += cost[i];
+    uint32_t rank_carry = 0;
+    for (int t = 0, base = 0; base < ncu; base += kScanTile, ++t) {
+        const int i0 = base + 4 * tid;
+        const uint4 v = ld4(cost, i0);
+        const uint32_t c4[4] = {v.x, v.y, v.z, v.w};
+        uint32_t tt;
+        const uint32_t pre0 = tile_pre[t] + block_excl_scan(v.x + v.y + v.z + v.w, wtot, &tt);
+        int ids[4];
+        uint32_t nst = 0;
+        if (i0 < ncu) {
+            int cid = plan_slice_of(pre0, total, S);
+            int prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
+            uint64_t tnext = thr(cid + 1), pre = pre0;
+            for (int e = 0; e < 4; ++e) {
+                while (pre >= tnext) tnext = thr(++cid + 1);
+                ids[e] = cid;
+                nst += (i0 + e < ncu && cid != prev) ? 1u : 0u;
+                prev = cid;
+                pre += c4[e];
+            }
         }
-    }
-    uint32_t nstarts;
-    const uint32_t base = block_excl_scan(nst, wtot, &nstarts);
-    {
-        int cid = id0, prev = prev0, rank = (int)base - 1;
-        uint64_t tnext = thr(cid + 1), pre = pre0;
-        for (int i = i0; i < i1; ++i) {
-            while (pre >= tnext) tnext = thr(++cid + 1);
-            if (cid != prev) slice_first[++rank] = i;
-            slice_of_cu[i] = rank;
-            prev = cid;
-            pre += cost[i];
+        uint32_t tile_starts;
+        const uint32_t rbase = rank_carry + block_excl_scan(nst, wtot, &tile_starts);
+        if (i0 < ncu) {
+            int rank = (int)rbase - 1;
+            int prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
+            for (int e = 0; e < 4 && i0 + e < ncu; ++e) {
+                if (ids[e] != prev) slice_first[++rank] = i0 + e;
+                slice_of_cu[i0 + e] = rank;
+                prev = ids[e];
+            }
         }
+        rank_carry += tile_starts;
     }
-    if (tid == 0) *nslices = nstarts;
+    if (tid == 0) *nslices = rank_carry;
 }
 
 // Skip / merge / AMVP of every CU of a P picture against its slice's neighbours.
@@ -1062,58 +1088,87 @@ __global__ __launch_bounds__(256) void k_hevc_decide(Geometry g, const h264::MbI
     cus[i] = c;
 }
 
+__device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
+    // kCuWords dwords (CuInfo is 24 bytes, 4-byte aligned in the array) -> wave-uniform values
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(cus) + (size_t)i * kCuWords;
+    uint32_t w[kCuWords];
+    for (int q = 0; q < kCuWords; ++q) w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[q]);
+    CuInfo c;
+    __builtin_memcpy(&c, w, sizeof c);
+    return c;
+}
+
 // ------------------------------------------------------------------ CABAC
 // Two phases (hevc_core.h "bin tokens").  Binarisation is a pure function of a CTU, its
 // neighbours' descriptors and its QP predictor (qpy of the previous CTU in the slice), so
-// k_hevc_bins binarises every CTU of the picture at once, one thread per CTU, into a fixed slot
-// of kMaxCuTokens tokens; k_hevc_tokscan / k_hevc_tokgather lay the tokens of the picture out
+// k_hevc_bins binarises every CTU of the picture at once -- one wave per CTU, one lane per part
+// (hevc_core.h for_each_part: head, split-child heads, TU last positions, sub-blocks) staged in
+// LDS and concatenated by a wave prefix sum -- into a fixed slot of kMaxCuTokens tokens; k_hevc_tokscan / k_hevc_tokgather lay the tokens of the picture out
 // densely in decoding order.  Only the arithmetic coder is serial: k_hevc_arith runs one wave per
 // slice over that slice's token run -- a short loop with no syntax logic, whose coder state lives
 // in SGPRs and whose 144 context states sit four to a lane in one VGPR (v_readlane /
 // v_writelane), so the serial part is a few dozen scalar instructions per token and fits the
 // instruction cache (the former single-phase kernel was 16 k instructions of CU syntax per wave
 // and took ~0.8 us per skipped CTU: profiles/r03_cabac).
-__global__ __launch_bounds__(256) void k_hevc_bins(Geometry g, const HevcFrameState* __restrict__ fs,
-                                                    const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
-                                                    const uint32_t* __restrict__ sao,
-                                                    const int* __restrict__ slice_first,
-                                                    const int* __restrict__ slice_of_cu,
-                                                    const uint32_t* __restrict__ nslices,
-                                                    const uint8_t* __restrict__ qpy, uint16_t* __restrict__ tok,
-                                                    uint32_t* __restrict__ ntok) {
+__global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                   const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
+                                                   const uint32_t* __restrict__ sao,
+                                                   const int* __restrict__ slice_first,
+                                                   const int* __restrict__ slice_of_cu,
+                                                   const uint32_t* __restrict__ nslices,
+                                                   const uint8_t* __restrict__ qpy, uint16_t* __restrict__ tok,
+                                                   uint32_t* __restrict__ ntok) {
+    __shared__ uint16_t stage[64 * kPartTokens];
     const int ncu = g.mb_w * g.mb_h;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ncu) return;
-    const int ns = (int)*nslices;
-    const int s = slice_of_cu[i];
-    const int first = slice_first[s];
-    const int end = s + 1 < ns ? slice_first[s + 1] : ncu;
+    const int i = blockIdx.x, lane = threadIdx.x;
+    const int ns = (int)uni(*nslices);
+    const int s = uni(slice_of_cu[i]);
+    const int first = uni(slice_first[s]);
+    const int end = s + 1 < ns ? uni(slice_first[s + 1]) : ncu;
     const int k = i - first;
-    int qp_prev = k > 0 ? (int)qpy[i - 1] : fs->qp;
+    const int qp_prev = k > 0 ? (int)uni((uint32_t)qpy[i - 1]) : fs->qp;
+    const CuInfo c = load_cu(cus, i);
+    const CoefArray cf{coef + (size_t)i * kCoefPerCu};
+    // lane p binarises part p of the CTU (coding order) into its LDS run
+    CtuPart mine;
+    bool have = false;
+    for_each_part(c, cf, [&](const CtuPart& pt, int idx) {
+        if (idx == lane) {
+            mine = pt;
+            have = true;
+        }
+    });
     BinRec rec;
-    rec.start(tok + (size_t)i * kMaxCuTokens, kMaxCuTokens);
-    const uint32_t n = binarise_ctu(rec, fs->idr != 0, cus, coef, fs->sao ? sao : nullptr, i, k, end - first, g.mb_w,
-                                    qp_prev);
-    ntok[i] = n < kMaxCuTokens ? n : kMaxCuTokens;  // > cap cannot happen (kMaxCuTokens is a bound)
+    rec.start(stage + lane * kPartTokens, kPartTokens);
+    if (have) binarise_part(rec, mine, fs->idr != 0, cus, cf, fs->sao ? sao : nullptr, i, k, end - first, g.mb_w, qp_prev);
+    const uint32_t n = have ? min(rec.n, kPartTokens) : 0u;
+    uint32_t incl = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    uint16_t* dst = tok + (size_t)i * kMaxCuTokens + (incl - n);
+    const uint16_t* src = stage + lane * kPartTokens;
+    for (uint32_t j = 0; j < n; ++j) dst[j] = src[j];
+    if (lane == 63) ntok[i] = incl;
 }
 
 // Exclusive prefix of the token counts in decoding (raster) order: off[i], off[ncu] = total.
-// One 1024-thread workgroup, a chunk of consecutive CTUs per thread.
+// One 1024-thread workgroup over tiles of kScanTile counts (16-byte loads and stores).
 __global__ __launch_bounds__(1024) void k_hevc_tokscan(const uint32_t* __restrict__ ntok, int ncu,
                                                         uint32_t* __restrict__ off) {
     __shared__ uint32_t wtot[16];
     const int tid = threadIdx.x;
-    const int chunk = (ncu + (int)blockDim.x - 1) / (int)blockDim.x;
-    const int i0 = min(ncu, tid * chunk), i1 = min(ncu, i0 + chunk);
-    uint32_t local = 0;
-    for (int i = i0; i < i1; ++i) local += ntok[i];
-    uint32_t total;
-    uint32_t pre = block_excl_scan(local, wtot, &total);
-    for (int i = i0; i < i1; ++i) {
-        off[i] = pre;
-        pre += ntok[i];
+    uint32_t carry = 0;
+    for (int base = 0; base < ncu; base += kScanTile) {
+        const int i = base + 4 * tid;
+        const uint4 v = ld4(ntok, i);
+        uint32_t tt;
+        const uint32_t pre = carry + block_excl_scan(v.x + v.y + v.z + v.w, wtot, &tt);
+        *reinterpret_cast<uint4*>(off + i) = make_uint4(pre, pre + v.x, pre + v.x + v.y, pre + v.x + v.y + v.z);
+        carry += tt;
     }
-    if (tid == 0) off[ncu] = total;
+    if (tid == 0) off[ncu] = carry;
 }
 
 // One wave per CTU: copy its tokens from the fixed slot to the dense run.
@@ -1148,6 +1203,47 @@ struct PackedCtx {
     }
     __device__ __forceinline__ uint32_t next_lps(uint32_t s) const {
         return (uint32_t)__builtin_amdgcn_readlane((int)next, (int)s);
+    }
+};
+
+// Token -> arithmetic coder, written for the scalar unit: one wave issues at most one instruction
+// every 4 cycles, so the per-token instruction count is the coder's speed.  The context bin is
+// branch-free (both successor states formed, one selected; one renormalisation shift from the
+// leading-zero count); the coder registers and the output position live in SGPRs and the bytes
+// are stored by every lane (same address).  Same arithmetic as hevc_core.h CabacEnc, which
+// finishes the slice (its registers are handed over).
+struct LeanCoder {
+    CabacEnc e;
+    __device__ __forceinline__ void token(PackedCtx& ctx, uint32_t t) {
+        if (!(t & 0x8000u)) {
+            const uint32_t idx = t >> 1, b = t & 1u;
+            if (idx != kTokTerm) {
+                const uint32_t li = idx >> 2, sh = (idx & 3u) * 8u;
+                const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)ctx.st, (int)li);
+                const uint32_t s7 = (w >> sh) & 0xffu, ps = s7 >> 1, mps = s7 & 1u;
+                const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)ctx.lps_row, (int)ps);
+                const uint32_t nl = (uint32_t)__builtin_amdgcn_readlane((int)ctx.next, (int)ps);
+                const uint32_t lps = (row >> (((e.range >> 6) & 3u) * 8u)) & 0xffu;
+                const uint32_t rm = e.range - lps;
+                const bool is_lps = b != mps;
+                const uint32_t ns_lps = (nl << 1) | (mps ^ ((ps - 1u) >> 31));  // valMps flips on an LPS in state 0
+                const uint32_t ns_mps = ((ps < 62u ? ps + 1u : 62u) << 1) | mps;
+                const uint32_t nw = (w & ~(0xffu << sh)) | ((is_lps ? ns_lps : ns_mps) << sh);
+                // one v_writelane (operands from the scalar unit; no exec-masked region)
+                asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(ctx.st) : "s"(nw), "{m0}"(li));
+                e.low += is_lps ? rm : 0u;
+                const uint32_t r = is_lps ? lps : rm;
+                const int n = __builtin_clz(r) - 23;
+                e.low <<= n;
+                e.range = r << n;
+                e.bits_left -= n;
+                if (e.bits_left < 12) e.write_out();
+                return;
+            }
+            e.terminate((int)b);
+            return;
+        }
+        e.bypass_bits(t & 0x7ffu, (int)((t >> 11) & 15u) + 1);
     }
 };
 
@@ -1186,8 +1282,8 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
         ctx.next = kNextLps[lane];
         ctx.lane = lane;
     }
-    CabacEnc e;
-    e.start(slice_data + (size_t)s * slice_cap, slice_cap);
+    LeanCoder lc;
+    lc.e.start(slice_data + (size_t)s * slice_cap, slice_cap);
     const uint32_t a0 = t0 & ~3u;  // 8-byte aligned chunk starts
     const uint2* src = reinterpret_cast<const uint2*>(dense + a0);
     uint2 cur = src[lane];
@@ -1199,14 +1295,25 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
         // token loop as a vmcnt(0) that also drains the prefetch and the coder's byte stores
         uint32_t cx = cur.x, cy = cur.y;
         asm volatile("" : "+v"(cx), "+v"(cy));
-        for (uint32_t j = j0; j < j1; ++j) {
-            const uint32_t wx = (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)(j >> 2));
-            const uint32_t wy = (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)(j >> 2));
-            const uint32_t w = (j & 2) ? wy : wx;
-            code_token(e, ctx, uni((w >> ((j & 1) * 16)) & 0xffffu));
+        // lane l holds tokens 4l .. 4l+3; whole lanes in the middle of the run, partial ones at its ends
+        for (uint32_t l = j0 >> 2; l < (j1 + 3) >> 2; ++l) {
+            const uint32_t wx = (uint32_t)__builtin_amdgcn_readlane((int)cx, (int)l);
+            const uint32_t wy = (uint32_t)__builtin_amdgcn_readlane((int)cy, (int)l);
+            const uint32_t j = 4 * l;
+            if (j >= j0 && j + 4 <= j1) {
+                lc.token(ctx, wx & 0xffffu);
+                lc.token(ctx, wx >> 16);
+                lc.token(ctx, wy & 0xffffu);
+                lc.token(ctx, wy >> 16);
+            } else {
+#pragma unroll 1
+                for (uint32_t q = 0; q < 4; ++q)
+                    if (j + q >= j0 && j + q < j1) lc.token(ctx, ((q & 2) ? wy : wx) >> ((q & 1) * 16) & 0xffffu);
+            }
         }
         cur = nxt;
     }
+    CabacEnc& e = lc.e;
     e.finish_slice();
     if (lane == 0) {
         slice_len[s] = e.pos;
@@ -1696,7 +1803,8 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_hevc_bins, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.coef, b.sao,
+    if ((ncu + kScanTile - 1) / kScanTile > kMaxScanTiles) throw std::invalid_argument("hevc: picture too large");
+    hipLaunchKernelGGL(k_hevc_bins, dim3(ncu), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.sao,
                        b.slice_first, b.slice_of_cu, b.nslices, b.qpy, b.tok, b.ntok);
     hipLaunchKernelGGL(k_hevc_tokscan, dim3(1), dim3(1024), 0, s, b.ntok, ncu, b.tok_off);
     hipLaunchKernelGGL(k_hevc_tokgather, dim3((ncu + 3) / 4), dim3(256), 0, s, b.tok, b.ntok, b.tok_off, ncu,
