@@ -3,8 +3,6 @@
 #include "h264_encoder.h"
 
 #include <algorithm>
-#include <cstdlib>
-#include <string>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -334,22 +332,12 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
-    if (depth_ > 1) {
-        HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
-        const char* hv = std::getenv("MXDESK_HANDOFF");
-        if (hv && std::string(hv) == "value") {
-            void* p = nullptr;
-            HIP_CHECK(hipExtMallocWithFlags(&p, 64, hipMallocSignalMemory));
-            hand_seq_ = static_cast<uint32_t*>(p);
-            HIP_CHECK(hipMemsetAsync(hand_seq_, 0, 4, stream_));
-        }
-    }
+    if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 GpuH264Encoder::~GpuH264Encoder() {
     (void)hipStreamSynchronize(stream_);
-    if (hand_seq_) (void)hipFree(hand_seq_);
     if (stream_e_) {
         (void)hipStreamSynchronize(stream_e_);
         (void)hipStreamDestroy(stream_e_);
@@ -363,7 +351,7 @@ GpuH264Encoder::~GpuH264Encoder() {
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
 }
 
-void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
+void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
     FrameSlot& sl = slots_[prep_slot_];
     const FrameState* pub = publish ? sl.fs_host : nullptr;
     if (idr) {
@@ -376,21 +364,25 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
         launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
         if (cfg_.intra_in_p) launch_intra_in_p(geom_, sl.buf, src_y, src_uv, stream_);
     }
-    hipStream_t es = stream_;
-    if (stream_e_) {  // entropy of this frame overlaps the analysis of the next one
-        if (hand_seq_) {
-            // hand-off through a signal-memory word: the analysis stream writes the frame's
-            // sequence number, the entropy stream's WAIT_REG_MEM polls it (an event wait on an
-            // idle queue resolved only ~14 us later, at the next doorbell: profiles/r03_h264)
-            ++hand_val_;
-            HIP_CHECK(hipStreamWriteValue32(stream_, hand_seq_, hand_val_, 0));
-            HIP_CHECK(hipStreamWaitValue32(stream_e_, hand_seq_, hand_val_, hipStreamWaitValueGte, 0xffffffffu));
-        } else {
-            HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
-            HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
-        }
-        es = stream_e_;
-    }
+}
+
+void GpuH264Encoder::link_entropy() {
+    if (!stream_e_) return;  // entropy of this frame overlaps the analysis of the next one
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
+    HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+}
+
+void GpuH264Encoder::enqueue_entropy() {
+    FrameSlot& sl = slots_[prep_slot_];
+    launch_entropy(geom_, sl.buf, sl.host_out, stream_e_ ? stream_e_ : stream_, nullptr);
+}
+
+void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
+    FrameSlot& sl = slots_[prep_slot_];
+    enqueue_analysis_kernels(idr, src_y, src_uv, publish);
+    link_entropy();
+    hipStream_t es = stream_e_ ? stream_e_ : stream_;
     hipEvent_t sse_ready = nullptr;
     if (cfg_.h264_deblock()) {  // in-loop filter on the analysis stream: the next frame predicts from it,
                          // while this frame's CAVLC runs beside it on the entropy stream
@@ -487,6 +479,12 @@ void GpuH264Encoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
     enqueue_kernels(idr, src_y, src_uv, false);
 }
 
+void GpuH264Encoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
+    enqueue_analysis_kernels(idr, src_y, src_uv, false);
+}
+
 void GpuH264Encoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
 
 void GpuH264Encoder::record_done() {
@@ -511,7 +509,7 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     const int s = inflight_.front();
     inflight_.pop_front();
     FrameSlot& sl = slots_[s];
-    HIP_CHECK(hipEventSynchronize(sl.done));
+    wait_event(sl.done);
     last_done_ = sl.done;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, sl.start, sl.done);

@@ -202,11 +202,21 @@ class GpuH264Encoder final : public VideoEncoder {
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void record_start() override;
     void record_done() override;
+    // depth-2 graph form (VideoEncoder): deblocking needs an extra event inside the entropy
+    // chain, so the split form is offered only with the filter off (the default)
+    bool supports_split() const override { return !cfg_.h264_deblock(); }
+    int prep_slot() const override { return prep_slot_; }
+    hipStream_t entropy_stream() const override { return stream_e_; }
+    void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
+    void enqueue_entropy() override;
+    void link_entropy() override;
     // Completion event of the last collected frame.
     hipEvent_t done_event() const override { return last_done_; }
+    hipEvent_t pending_done_event() const override { return inflight_.empty() ? last_done_ : slots_[inflight_.front()].done; }
     // publish: the first kernel takes the frame state by value and stores it (eager launches);
     // otherwise the kernels read the device copy uploaded by enqueue_body's memcpy node.
     void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish);
+    void enqueue_analysis_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish);
 
    private:
     struct FrameSlot {  // per-frame-in-flight state
@@ -226,8 +236,6 @@ class GpuH264Encoder final : public VideoEncoder {
     EncoderCommon common_;
     hipStream_t stream_;
     hipStream_t stream_e_ = nullptr;  // entropy stream (depth 2)
-    uint32_t* hand_seq_ = nullptr;    // analysis -> entropy hand-off word (MXDESK_HANDOFF=value)
-    uint32_t hand_val_ = 0;
     int depth_ = 1;
     Geometry geom_;
     FrameSlot slots_[kMaxInFlight];

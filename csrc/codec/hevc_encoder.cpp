@@ -202,7 +202,7 @@ bool GpuHevcEncoder::prepare(bool force_idr) {
     return idr;
 }
 
-void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+void GpuHevcEncoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(HevcFrameState), hipMemcpyHostToDevice, stream_));
     if (idr) {
@@ -218,13 +218,24 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
     }
     launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_deblock(), sl.fs_host->sao != 0, src_y,
                        src_uv, stream_);
-    hipStream_t es = stream_;
-    if (stream_e_) {
-        HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
-        HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
-        es = stream_e_;
-    }
-    launch_hevc_entropy(geom_, sl.buf, common_.max_slices(), sl.host_out, es);
+}
+
+void GpuHevcEncoder::link_entropy() {
+    if (!stream_e_) return;
+    FrameSlot& sl = slots_[prep_slot_];
+    HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
+    HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+}
+
+void GpuHevcEncoder::enqueue_entropy() {
+    FrameSlot& sl = slots_[prep_slot_];
+    launch_hevc_entropy(geom_, sl.buf, common_.max_slices(), sl.host_out, stream_e_ ? stream_e_ : stream_);
+}
+
+void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    enqueue_analysis(idr, src_y, src_uv);
+    link_entropy();
+    enqueue_entropy();
     HIP_CHECK(hipGetLastError());
 }
 
@@ -253,7 +264,7 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     const int s = inflight_.front();
     inflight_.pop_front();
     FrameSlot& sl = slots_[s];
-    HIP_CHECK(hipEventSynchronize(sl.done));
+    wait_event(sl.done);
     last_done_ = sl.done;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, sl.start, sl.done);

@@ -203,6 +203,7 @@ class GpuHevcEncoder final : public VideoEncoder {
     const uint8_t* recon_y() const override { return rec_y_[cur_]; }
     const uint8_t* recon_uv() const override { return rec_uv_[cur_]; }
     hipEvent_t done_event() const override { return last_done_; }
+    hipEvent_t pending_done_event() const override { return inflight_.empty() ? last_done_ : slots_[inflight_.front()].done; }
     // Per-slice CABAC timing of the last collected picture (diagnostics, synchronous copy):
     // (first CTU, CTUs, payload bytes, wave ticks at 100 MHz) per slice.
     std::vector<std::array<uint64_t, 4>> slice_timing() const;
@@ -211,6 +212,12 @@ class GpuHevcEncoder final : public VideoEncoder {
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void record_start() override;
     void record_done() override;
+    bool supports_split() const override { return true; }
+    int prep_slot() const override { return prep_slot_; }
+    hipStream_t entropy_stream() const override { return stream_e_; }
+    void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
+    void enqueue_entropy() override;
+    void link_entropy() override;
 
    private:
     struct FrameSlot {

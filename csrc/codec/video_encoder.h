@@ -29,11 +29,23 @@ class VideoEncoder {
     virtual const uint8_t* recon_y() const = 0;
     virtual const uint8_t* recon_uv() const = 0;
     virtual hipEvent_t done_event() const = 0;
-    // split form for hipGraph capture (pipeline depth 1)
+    // completion event of the oldest frame in flight (the next collect() waits for it)
+    virtual hipEvent_t pending_done_event() const = 0;
+    // split form for hipGraph capture (pipeline depth 1: enqueue_body on one stream)
     virtual bool prepare(bool force_idr) = 0;
     virtual void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) = 0;
     virtual void record_start() = 0;
     virtual void record_done() = 0;
+    // depth-2 graph form: the frame state upload + analysis kernels on the session stream and the
+    // entropy kernels on entropy_stream(), captured as two graphs per (frame slot, encoder slot,
+    // picture type) and linked per frame by link_entropy() (analysis event -> entropy stream).
+    // supports_split() false: eager submission only.
+    virtual bool supports_split() const { return false; }
+    virtual int prep_slot() const { return 0; }
+    virtual hipStream_t entropy_stream() const { return nullptr; }
+    virtual void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) { (void)idr; (void)src_y; (void)src_uv; }
+    virtual void enqueue_entropy() {}
+    virtual void link_entropy() {}
 };
 
 }  // namespace mx

@@ -204,6 +204,7 @@ class GpuVp8Encoder final : public VideoEncoder {
     const uint8_t* recon_y() const override { return rec_y_[cur_]; }
     const uint8_t* recon_uv() const override { return rec_uv_[cur_]; }
     hipEvent_t done_event() const override { return last_done_; }
+    hipEvent_t pending_done_event() const override { return inflight_.empty() ? last_done_ : slots_[inflight_.front()].done; }
     bool prepare(bool force_idr) override;
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void record_start() override;

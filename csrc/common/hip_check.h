@@ -34,3 +34,26 @@ inline void ensure_func_attr(const void* fn, hipFuncAttribute attr, int value) {
     done.insert(key);
 }
 }  // namespace mx
+
+#include <cstdlib>
+#include <thread>
+
+namespace mx {
+// Wait for a frame's completion event.  MXDESK_WAIT=spin polls hipEventQuery (the collecting
+// thread owns a core: wake-up within ~1 us of the GPU finishing); default hipEventSynchronize.
+inline void wait_event(hipEvent_t e) {
+    static const bool spin = [] {
+        const char* v = std::getenv("MXDESK_WAIT");
+        return v && std::string(v) == "spin";
+    }();
+    if (!spin) {
+        HIP_CHECK(hipEventSynchronize(e));
+        return;
+    }
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r == hipSuccess) return;
+        if (r != hipErrorNotReady) HIP_CHECK(r);
+    }
+}
+}  // namespace mx

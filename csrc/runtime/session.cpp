@@ -1,5 +1,9 @@
 #include "session.h"
 
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+
 #include <exception>
 #include <thread>
 
@@ -97,7 +101,8 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
     HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));
     depth_ = enc_->depth();
-    if (depth_ > 1 && cfg_.use_graph) throw std::invalid_argument("hipGraph replay needs pipeline_depth 1");
+    if (depth_ > 1 && cfg_.use_graph && !enc_->supports_split())
+        throw std::invalid_argument("hipGraph replay with pipeline_depth 2 needs an encoder with the split form");
     if (depth_ >= cfg_.pool_slots) throw std::invalid_argument("pool_slots must exceed pipeline_depth");
     for (int k = 0; k < depth_; ++k)
         HIP_CHECK(hipHostMalloc(&staging_[k], (size_t)pool_->pitch() * cfg_.height, hipHostMallocDefault));
@@ -145,18 +150,24 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         HIP_CHECK(hipHostMalloc(&mask_host_, 2 * sizeof(unsigned long long), hipHostMallocMapped));
         for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_mask_[k], hipEventDisableTiming));
     }
-    HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams), hipHostMallocDefault));
+    // one parameter block per frame slot: with two frames in flight a captured memcpy node may
+    // run after the host has already written the next frame's parameters
+    HIP_CHECK(hipHostMalloc(&synth_host_, sizeof(pix::SynthParams) * cfg_.pool_slots, hipHostMallocDefault));
     // static layer of the synthetic desktop, rendered once (k_synth copies it outside the
     // animated elements)
     HIP_CHECK(hipMalloc(&synth_bg_, (size_t)pool_->pitch() * cfg_.height));
     pix::launch_synth_static(synth_bg_, synth_params(), stream_);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams)));
-    graphs_.assign((size_t)cfg_.pool_slots * 2, nullptr);
+    HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams) * cfg_.pool_slots));
+    // [frame slot][encoder slot][IDR][analysis, entropy]
+    graphs_.assign((size_t)cfg_.pool_slots * 2 * 2 * 2, nullptr);
     t0_us_ = now_us();
 }
 
 Session::~Session() {
+    if (ht_n_ > 0 && std::getenv("MXDESK_HOST_TIMING"))
+        std::fprintf(stderr, "[mxdesk] host us/frame over %lld frames: submit %.1f, wait %.1f, collect %.1f\n",
+                     (long long)ht_n_, ht_submit_ / ht_n_, ht_wait_ / ht_n_, ht_post_ / ht_n_);
     if (stream_) hipStreamSynchronize(stream_);
     for (auto g : graphs_)
         if (g) hipGraphExecDestroy(g);
@@ -257,22 +268,18 @@ pix::SynthParams Session::synth_params() {
     return p;
 }
 
-hipGraphExec_t Session::capture_frame_graph(int slot, bool idr) {
-    TraceRange tr("mxdesk.graph.capture");
+hipGraphExec_t Session::capture_on(hipStream_t st, const std::function<void()>& body) {
     hipGraph_t graph = nullptr;
-    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     try {
-        HIP_CHECK(hipMemcpyAsync(synth_dev_, synth_host_, sizeof(pix::SynthParams), hipMemcpyHostToDevice, stream_));
-        pix::launch_synth_dev(pool_->data(slot), synth_dev_, cfg_.width, cfg_.height, stream_, synth_bg_);
+        body();
         HIP_CHECK(hipGetLastError());
-        convert(slot);
-        enc_->enqueue_body(idr, nv12_y_, nv12_uv_);
     } catch (...) {
-        hipStreamEndCapture(stream_, &graph);  // leave capture mode before propagating
+        hipStreamEndCapture(st, &graph);  // leave capture mode before propagating
         if (graph) hipGraphDestroy(graph);
         throw;
     }
-    HIP_CHECK(hipStreamEndCapture(stream_, &graph));
+    HIP_CHECK(hipStreamEndCapture(st, &graph));
     hipGraphExec_t exec = nullptr;
     HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     HIP_CHECK(hipGraphDestroy(graph));
@@ -280,7 +287,45 @@ hipGraphExec_t Session::capture_frame_graph(int slot, bool idr) {
     return exec;
 }
 
+// Per-frame chain as graphs: with one frame in flight the whole chain on the session stream;
+// with two, the analysis part (parameter upload, desktop render, conversion, frame-state
+// upload, analysis kernels) on the session stream and the entropy part on the encoder's
+// entropy stream, linked per frame by an event outside the graphs -- two graph launches and
+// four event operations per frame instead of ~9 kernel launches plus those events (the host
+// issue rate was the frame-rate limit: profiles/r03_h264).
+void Session::capture_frame_graphs(int slot, bool idr, hipGraphExec_t* ga, hipGraphExec_t* ge) {
+    TraceRange tr("mxdesk.graph.capture");
+    pix::SynthParams* dev = synth_dev_ + slot;
+    const pix::SynthParams* host = synth_host_ + slot;
+    auto analysis = [&]() {
+        HIP_CHECK(hipMemcpyAsync(dev, host, sizeof(pix::SynthParams), hipMemcpyHostToDevice, stream_));
+        pix::launch_synth_dev(pool_->data(slot), dev, cfg_.width, cfg_.height, stream_, synth_bg_);
+        HIP_CHECK(hipGetLastError());
+        convert(slot);
+    };
+    if (depth_ == 1) {
+        *ga = capture_on(stream_, [&]() {
+            analysis();
+            enc_->enqueue_body(idr, nv12_y_, nv12_uv_);
+        });
+        *ge = nullptr;
+        return;
+    }
+    *ga = capture_on(stream_, [&]() {
+        analysis();
+        enc_->enqueue_analysis(idr, nv12_y_, nv12_uv_);
+    });
+    hipStream_t es = enc_->entropy_stream() ? enc_->entropy_stream() : stream_;
+    *ge = capture_on(es, [&]() { enc_->enqueue_entropy(); });
+}
+
 void Session::submit_synthetic(bool force_idr) {
+    const auto t_in = std::chrono::steady_clock::now();
+    struct Acc {
+        double& a;
+        std::chrono::steady_clock::time_point t;
+        ~Acc() { a += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count(); }
+    } acc{ht_submit_, t_in};
     TraceRange tr("mxdesk.submit_synthetic");
     const int k = begin_frame();
     const int slot = pool_->acquire();
@@ -294,13 +339,18 @@ void Session::submit_synthetic(bool force_idr) {
         convert_and_encode(slot, force_idr);
         return;
     }
-    *synth_host_ = p;  // read by the graph's memcpy node (previous frame already collected)
+    synth_host_[slot] = p;  // read by this slot's graph memcpy node (its previous frame was collected)
     const bool idr = enc_->prepare(force_idr);
+    const int es = depth_ > 1 ? enc_->prep_slot() : 0;
     HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
     enc_->record_start();
-    hipGraphExec_t& exec = graphs_[(size_t)slot * 2 + (idr ? 1 : 0)];
-    if (!exec) exec = capture_frame_graph(slot, idr);
-    HIP_CHECK(hipGraphLaunch(exec, stream_));
+    const size_t key = (((size_t)slot * 2 + (size_t)es) * 2 + (idr ? 1 : 0)) * 2;
+    if (!graphs_[key]) capture_frame_graphs(slot, idr, &graphs_[key], &graphs_[key + 1]);
+    HIP_CHECK(hipGraphLaunch(graphs_[key], stream_));
+    if (graphs_[key + 1]) {
+        enc_->link_entropy();
+        HIP_CHECK(hipGraphLaunch(graphs_[key + 1], enc_->entropy_stream() ? enc_->entropy_stream() : stream_));
+    }
     enc_->record_done();
     enqueue_mask_sse(k);
 }
@@ -365,8 +415,18 @@ FrameResult Session::collect() {
     inflight_.pop_front();
     FrameResult r;
     TraceRange tr("mxdesk.collect(wait+annexb)");
+    const auto t_in = std::chrono::steady_clock::now();
+    HIP_CHECK(hipEventSynchronize(enc_->pending_done_event()));
+    const auto t_w = std::chrono::steady_clock::now();
     const std::vector<uint8_t>& au = enc_->collect();
     r.t_encoded_us = now_us();
+    ht_wait_ += std::chrono::duration<double, std::micro>(t_w - t_in).count();
+    ++ht_n_;
+    struct Acc {
+        double& a;
+        std::chrono::steady_clock::time_point t;
+        ~Acc() { a += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count(); }
+    } acc{ht_post_, t_w};
     r.au = au;
     r.frame_id = fl.frame_id;
     r.t_capture_us = fl.t_capture;  // steady clock (CLOCK_MONOTONIC) microseconds

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <deque>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -133,7 +134,8 @@ class Session {
     void convert(int slot);
     void convert_and_encode(int slot, bool force_idr);
     pix::SynthParams synth_params();
-    hipGraphExec_t capture_frame_graph(int slot, bool idr);
+    hipGraphExec_t capture_on(hipStream_t st, const std::function<void()>& body);
+    void capture_frame_graphs(int slot, bool idr, hipGraphExec_t* ga, hipGraphExec_t* ge);
 
     SessionConfig cfg_;
     hipStream_t stream_ = nullptr;
@@ -179,6 +181,10 @@ class Session {
     int graphs_built_ = 0;
     uint32_t frame_id_ = 0;  // id of the next submitted frame
     int64_t t0_us_ = 0;
+    // host-side time per frame (MXDESK_HOST_TIMING=1 prints the means when the session ends):
+    // submit, collect (wait for the GPU), collect (after the wait)
+    double ht_submit_ = 0, ht_wait_ = 0, ht_post_ = 0;
+    int64_t ht_n_ = 0;
     int64_t t_capture_ = 0;
     int cursor_x_ = -1, cursor_y_ = -1;
     int begin_frame();  // reserve an in-flight entry, returns its k

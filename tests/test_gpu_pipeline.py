@@ -437,3 +437,34 @@ def test_zero_copy_registered_capture_matches_staged_upload(gpu):
     # a span that does not fit the declared buffer is refused before any copy (no overread)
     with pytest.raises(ValueError):
         zc.submit_bgrx_ptr(buf.ctypes.data, pitch, pitch * (h - 1) + w * 4 - 1, False)
+
+
+@pytest.mark.parametrize("codec", ["h264", "hevc"])
+def test_graph_replay_depth2_matches_eager(gpu, codec):
+    """Two frames in flight with the per-frame chain replayed as two hipGraphs (analysis on the
+    session stream, entropy on the encoder's entropy stream, linked by an event per frame):
+    bit-identical to eager launches under CBR, across every (frame slot, encoder slot) pair and
+    a forced IDR."""
+    def run(use_graph, n=12):
+        cfg = gpu.SessionConfig()
+        cfg.width, cfg.height, cfg.fps = 320, 192, 60
+        cfg.codec = codec
+        cfg.enc.bitrate_kbps = 600
+        cfg.enc.pipeline_depth = 2
+        cfg.use_graph = use_graph
+        cfg.fake_clock = 1
+        s = gpu.Session(cfg)
+        out = []
+        s.submit(False)
+        for i in range(n):
+            if i + 1 < n:
+                s.submit(i + 1 == 7)
+            out.append(s.collect())
+        assert s.in_flight == 0
+        return [r.au for r in out], s.graphs_built
+
+    eager, g0 = run(0)
+    graph, g1 = run(1)
+    assert g0 == 0 and g1 >= 4
+    for i, (a, b) in enumerate(zip(eager, graph)):
+        assert a == b, f"frame {i} differs"
