@@ -5,6 +5,7 @@
 #include "../net/dtls.h"
 #include "../net/rtp_h264.h"
 #include "../net/rtp_h265.h"
+#include "../net/rtp_sender.h"
 #include "../net/rtp_vp8.h"
 #include "../net/sctp.h"
 #include "../net/srtp.h"
@@ -37,6 +38,28 @@ void register_net(py::module& m) {
         .def_static("aes_cm_keystream", [](py::bytes k, py::bytes iv, size_t n) {
             return B(SrtpSession::aes_cm_keystream(k, iv, n));
         });
+    py::class_<RtpHistory>(n, "RtpHistory")
+        .def(py::init<size_t>(), py::arg("n") = 1024)
+        .def("get", [](const RtpHistory& h, uint16_t seq) -> py::object {
+            const std::string* p = h.get(seq);
+            return p ? py::object(py::bytes(*p)) : py::object(py::none());
+        });
+    py::class_<UdpPeer>(n, "UdpPeer")
+        .def(py::init<int, const std::string&, int>(), py::arg("fd"), py::arg("host"), py::arg("port"))
+        .def_property_readonly("fd", &UdpPeer::fd);
+    // packetize + history + SRTP + sendto of one access unit, GIL released
+    auto send_au = [](auto& pk, SrtpSession& srtp, RtpHistory& hist, const UdpPeer& peer, py::bytes au,
+                      uint32_t ts) {
+        std::string a = au;
+        py::gil_scoped_release rel;
+        return send_rtp_packets(pk.packetize(a, ts), srtp, hist, peer);
+    };
+    n.def("send_au", [send_au](RtpH264Packetizer& p, SrtpSession& s, RtpHistory& h, const UdpPeer& u, py::bytes au,
+                               uint32_t ts) { return send_au(p, s, h, u, au, ts); });
+    n.def("send_au", [send_au](RtpH265Packetizer& p, SrtpSession& s, RtpHistory& h, const UdpPeer& u, py::bytes au,
+                               uint32_t ts) { return send_au(p, s, h, u, au, ts); });
+    n.def("send_au", [send_au](RtpVp8Packetizer& p, SrtpSession& s, RtpHistory& h, const UdpPeer& u, py::bytes au,
+                               uint32_t ts) { return send_au(p, s, h, u, au, ts); });
     py::class_<DtlsEndpoint>(n, "DtlsEndpoint")
         .def(py::init<bool, int>(), py::arg("server"), py::arg("mtu") = 1200)
         .def_property_readonly("fingerprint", &DtlsEndpoint::fingerprint)

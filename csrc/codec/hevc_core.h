@@ -2034,10 +2034,10 @@ MXHD uint32_t cu_cost(const CuInfo& c) {
 // Below this much work per slice, fewer slices.  One unit is about 0.35 us of k_hevc_cabac wave
 // time (tools/hevc_cabac_timing.py: 0.79 us per CU + 1.45 us per payload byte, 4K and 1080p), so
 // 1024 units keep a slice near 0.35 ms; the level's slice limit usually binds first at 4K.
-constexpr uint32_t kCostPerSlice = 1024;
+constexpr uint32_t kCostPerSlice = 1024;  // EncoderConfig::hevc_slice_cost default
 // Number of slices for a P picture of total cost T, bounded by the level's slice limit.
-MXHD int plan_num_slices(uint64_t total, int max_slices) {
-    const uint64_t s = total / kCostPerSlice;
+MXHD int plan_num_slices(uint64_t total, int max_slices, uint32_t cost_per_slice = kCostPerSlice) {
+    const uint64_t s = total / (cost_per_slice ? cost_per_slice : 1u);
     return s < 1 ? 1 : (s > (uint64_t)max_slices ? max_slices : (int)s);
 }
 // Slice of a CU whose exclusive cost prefix is `pre`: floor(pre * S / T) -- non-decreasing in

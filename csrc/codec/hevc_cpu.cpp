@@ -113,7 +113,7 @@ std::vector<int> HevcCommon::row_slices() const {
 std::vector<int> HevcCommon::plan_p_slices(const std::vector<CuInfo>& cus) const {
     uint64_t total = 0;
     for (const auto& c : cus) total += cu_cost(c);
-    const int S = plan_num_slices(total, max_slices_);
+    const int S = plan_num_slices(total, max_slices_, (uint32_t)rc_.config().hevc_slice_cost);
     std::vector<int> f;
     uint64_t pre = 0;
     int prev = -1;

@@ -216,7 +216,7 @@ void GpuHevcEncoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint
         h264::launch_me(geom_, sl.buf.me, src_y, stream_);
         launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
-    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_deblock(), sl.fs_host->sao != 0, src_y,
+    launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_slice_cost, cfg_.hevc_deblock(), sl.fs_host->sao != 0, src_y,
                        src_uv, stream_);
 }
 

@@ -178,7 +178,7 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
 // Slice layout, per-slice decisions and (with deblock) the in-loop filter + final distortion:
 // runs on the analysis stream because the deblocked picture is the next frame's reference.
-void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
+void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,
                         bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s);

@@ -1004,7 +1004,7 @@ __device__ __forceinline__ uint4 ld4(const uint32_t* p, int i) { return *reinter
 
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ cost, int ncu, int ctb_w,
-                                                       int max_slices, int* __restrict__ slice_first,
+                                                       int max_slices, int slice_cost, int* __restrict__ slice_first,
                                                        int* __restrict__ slice_of_cu, uint32_t* __restrict__ nslices) {
     __shared__ uint32_t wtot[16];
     const int tid = threadIdx.x;
@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     }
     __syncthreads();
     const uint32_t total = carry;
-    const int S = plan_num_slices(total, max_slices);
+    const int S = plan_num_slices(total, max_slices, (uint32_t)slice_cost);
     // slice id of a prefix p is the number of thresholds T_s = ceil(s * total / S) (s >= 1) <= p:
     // one division per thread and tile, then threshold tracking across its 4 CUs
     auto thr = [&](int s2) -> uint64_t {
@@ -1779,10 +1779,10 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
                        b.coef, b.cost, b.qpc);
 }
 
-void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, bool deblock,
+void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,
                         bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, b.slice_first,
+    hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, slice_cost, b.slice_first,
                        b.slice_of_cu, b.nslices);
     if (!idr)
         hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,

@@ -133,6 +133,7 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
 def cmd_serve(cfg: C.Config, args) -> None:
     from .server.app import MediaServer, run_forever, ssl_context
 
+
     if cfg.sessions > 1:
         cmd_serve_sessions(cfg, cfg.sessions)
         return

@@ -416,6 +416,10 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         self.srtp_rx = None
         self.pkt = None
         self.history: OrderedDict[int, bytes] = OrderedDict()
+        # native send path (packetize + NACK history + SRTP + sendto in one GIL-free call) for a
+        # direct UDP remote; relayed remotes keep the Python path
+        self._tx_peer = None  # (remote, net.UdpPeer)
+        self._tx_hist = None  # net.RtpHistory
         self.answer: Answer | None = None
         self.sub = None
         self.tasks: list[asyncio.Task] = []
@@ -701,7 +705,9 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             elif p["pt"] == 205 and p["fmt"] == 1:
                 self.stats["nack"] += 1
                 for seq in p.get("nack", []):
-                    raw = self.history.get(seq)
+                    raw = self._tx_hist.get(seq) if self._tx_hist is not None else None
+                    if raw is None:
+                        raw = self.history.get(seq)
                     if raw is not None and self.remote is not None:
                         self._sendto(self.srtp_tx.protect_rtp(raw), self.remote)
                         self.stats["rtx"] += 1
@@ -715,6 +721,13 @@ class WebRtcPeer(asyncio.DatagramProtocol):
             if self.ts0 is None:
                 self.ts0 = fr.t_capture_us
             ts = ((fr.t_capture_us - self.ts0) * 9 // 100) & 0xFFFFFFFF  # 90 kHz
+            peer = self._native_peer()
+            if peer is not None:
+                with trace("mxdesk.webrtc.send_au(native)"):
+                    self.stats["rtp_out"] += _native().net.send_au(self.pkt, self.srtp_tx, self._tx_hist, peer,
+                                                                   fr.au, ts)
+                self.last_ts = ts
+                continue
             with trace("mxdesk.webrtc.packetize+srtp+send"):
                 for raw in self.pkt.packetize(fr.au, ts):
                     seq = struct.unpack_from("!H", raw, 2)[0]
@@ -724,6 +737,25 @@ class WebRtcPeer(asyncio.DatagramProtocol):
                     self._sendto(self.srtp_tx.protect_rtp(raw), self.remote)
                     self.stats["rtp_out"] += 1
             self.last_ts = ts
+
+    def _native_peer(self):
+        """net.UdpPeer for the current remote when it is a direct UDP address (None: relayed or
+        no socket -- the Python path sends)."""
+        r = self.remote
+        if r is None or isinstance(r, RelayAddr) or self.transport is None:
+            return None
+        if self._tx_peer is None or self._tx_peer[0] != r:
+            sock = self.transport.get_extra_info("socket")
+            if sock is None:
+                return None
+            try:
+                peer = _native().net.UdpPeer(sock.fileno(), str(r[0]), int(r[1]))
+            except (ValueError, OSError):
+                return None
+            self._tx_peer = (r, peer)
+            if self._tx_hist is None:
+                self._tx_hist = _native().net.RtpHistory(self.HISTORY)
+        return self._tx_peer[1]
 
     async def _audio_loop(self) -> None:
         """48 kHz stereo chunks -> 8 kHz mono (native FIR decimator) -> 20 ms PCMU packets."""
