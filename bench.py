@@ -110,6 +110,7 @@ def main() -> None:
                          "(mxvp8enc, the reference's WEBRTC_ENCODER=vp8enc)")
     ap.add_argument("--tu-split", type=int, default=None,
                     help="HEVC: let inter CUs split their transform tree into 8x8 / 4x4 TUs (default: encoder default)")
+    ap.add_argument("--sao", type=int, default=None, help="HEVC sample adaptive offset (default on)")
     ap.add_argument("--hevc-slice-cost", type=int, default=None,
                     help="HEVC P-picture slice work target (more = fewer, longer slices)")
     ap.add_argument("--search-range", type=int, default=16)
@@ -179,6 +180,8 @@ def main() -> None:
     cfg.enc.subpel = args.subpel
     if args.tu_split is not None:
         cfg.enc.tu_split = args.tu_split
+    if args.sao is not None:
+        cfg.enc.sao = args.sao
     if args.hevc_slice_cost is not None:
         cfg.enc.hevc_slice_cost = args.hevc_slice_cost
     if args.intra_in_p is not None:

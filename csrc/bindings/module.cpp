@@ -163,6 +163,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("deblock", &h264::EncoderConfig::deblock)
         .def_readwrite("partitions", &h264::EncoderConfig::partitions)
         .def_readwrite("tu_split", &h264::EncoderConfig::tu_split)
+        .def_readwrite("hevc_slice_cost", &h264::EncoderConfig::hevc_slice_cost)
         .def_readwrite("sao", &h264::EncoderConfig::sao);
 
     py::class_<h264::FrameStats>(m, "FrameStats")

@@ -206,6 +206,7 @@ class GpuH264Encoder final : public VideoEncoder {
     // depth-2 graph form (VideoEncoder): deblocking needs an extra event inside the entropy
     // chain, so the split form is offered only with the filter off (the default)
     bool supports_split() const override { return !cfg_.h264_deblock(); }
+    bool masked_sse_in_encoder() const override { return true; }
     int prep_slot() const override { return prep_slot_; }
     hipStream_t entropy_stream() const override { return stream_e_; }
     void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;

@@ -10,7 +10,7 @@
 //   EncoderConfig.tu_split an inter CU may instead split its transform tree once (four 8x8
 //   luma TUs, eight 4x4 chroma TUs: max_transform_hierarchy_depth_inter 1), chosen per CU by
 //   SSE + lambda * estimated bits, I slices of intra CUs, P slices of skip / merge /
-//   AMVP CUs with one reference picture, MaxNumMergeCand 1, no TMVP, no SAO, no
+//   AMVP CUs with one reference picture, MaxNumMergeCand 5, no TMVP, no
 //   deblocking, no sign hiding, cu_qp_delta per CU (adaptive quantisation), one slice per
 //   CTU row so every slice is entropy coded by its own GPU wave.
 //
@@ -28,6 +28,7 @@ namespace mx {
 namespace hevc {
 
 constexpr int kCtb = 16;  // CTB = CU size
+constexpr int kMaxMergeCand = 5;  // MaxNumMergeCand (slice header five_minus_max_num_merge_cand 0)
 constexpr int kCoefPerCu = 384;  // 256 luma + 64 Cb + 64 Cr, each TU in scan order
 
 // ---------------------------------------------------------------- scans (6.5.3)
@@ -1040,6 +1041,13 @@ MXHD int cu_residual_kind(const CuInfo& c) {
     return c.cbf ? kResFlat : kResNone;
 }
 
+// merge_idx: truncated rice, cMax MaxNumMergeCand - 1, first bin context coded, rest bypass
+template <class E, class Ctx>
+MXHD void code_merge_idx(E& e, Ctx& ctx, int idx) {
+    e.bin(ctx, C_MERGE_IDX, idx > 0);
+    for (int k = 1; k < kMaxMergeCand - 1 && k <= idx; ++k) e.bypass(idx > k);
+}
+
 // CU syntax up to its residual: skip / prediction / motion, rqt_root_cbf, split_transform_flag,
 // and for an unsplit tree the cbf flags and cu_qp_delta; for a split tree the parent's chroma cbf.
 template <class E, class Ctx>
@@ -1048,7 +1056,10 @@ MXHD void code_cu_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, CuNb nb, in
         const int inc = (nb.left_type == kCuSkip ? 1 : 0) + (nb.above_type == kCuSkip ? 1 : 0);
         e.bin(ctx, C_SKIP + inc, c.type == kCuSkip);
     }
-    if (c.type == kCuSkip) return;
+    if (c.type == kCuSkip) {
+        code_merge_idx(e, ctx, c.mvp_idx);
+        return;
+    }
     const bool intra = c.type == kCuIntra;
     if (!islice) e.bin(ctx, C_PRED_MODE, intra);
     e.bin(ctx, C_PART_MODE, 1);  // PART_2Nx2N
@@ -1071,6 +1082,7 @@ MXHD void code_cu_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, CuNb nb, in
     } else {
         const bool merge = c.type == kCuMerge;
         e.bin(ctx, C_MERGE_FLAG, merge);
+        if (merge) code_merge_idx(e, ctx, c.mvp_idx);
         if (!merge) {
             code_mvd(e, ctx, c.mvdx, c.mvdy);
             e.bin(ctx, C_MVP, c.mvp_idx);
@@ -1797,14 +1809,25 @@ struct MvCand {
     int x, y;
 };
 
-// Merge candidate 0 (8.5.3.2.2-8.5.3.2.4 with MaxNumMergeCand 1, no TMVP): the first
-// available of A1, B1, B0, B2, else the zero candidate.
-MXHD MvCand merge_cand(MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
-    if (a1.avail) return a1;
-    if (b1.avail) return b1;
-    if (b0.avail) return b0;
-    if (b2.avail) return b2;
-    return MvCand{true, 0, 0};
+// Merge candidate list (8.5.3.2.2-8.5.3.2.4, MaxNumMergeCand kMaxMergeCand, no TMVP, one
+// reference picture): A1, B1 (unless equal to A1), B0 (unless equal to B1), A0 (never
+// available: the next CTU row), B2 (unless equal to A1 or B1, and only while fewer than four),
+// then zero candidates.
+MXHD bool mv_eq(MvCand a, MvCand b) { return a.x == b.x && a.y == b.y; }
+// Index of vector (mx, my) in the merge list (the first matching entry), -1 if absent.  Walks the
+// list without materialising it (no dynamically indexed array: registers only on the GPU).
+MXHD int merge_index_of(MvCand a1, MvCand b1, MvCand b0, MvCand b2, int mx, int my) {
+    int n = 0, found = -1;
+    auto add = [&](MvCand c) {
+        if (found < 0 && c.x == mx && c.y == my) found = n;
+        ++n;
+    };
+    if (a1.avail) add(a1);
+    if (b1.avail && !(a1.avail && mv_eq(b1, a1))) add(b1);
+    if (b0.avail && !(b1.avail && mv_eq(b0, b1))) add(b0);
+    if (b2.avail && n < 4 && !(a1.avail && mv_eq(b2, a1)) && !(b1.avail && mv_eq(b2, b1))) add(b2);
+    while (n < kMaxMergeCand) add(MvCand{true, 0, 0});
+    return found;
 }
 
 // AMVP list (8.5.3.2.6/7, one reference picture so no scaling): A = A1; B = first of
@@ -1841,12 +1864,15 @@ MXHD int mvd_cost_bits(int d) {
 }
 
 // Fill type / mvp / mvd of an inter CU (c.mvx/mvy/cbf set) from its neighbours' motion.
+// Merge / skip when the CU's vector is in the merge list (mvp_idx then holds merge_idx: the
+// first matching entry, the cheapest to signal), else AMVP with the cheaper predictor.
 MXHD void decide_inter(CuInfo& c, MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
-    const MvCand m = merge_cand(a1, b1, b0, b2);
     c.mvp_idx = 0;
     c.mvdx = c.mvdy = 0;
-    if (c.mvx == m.x && c.mvy == m.y) {
+    const int k = merge_index_of(a1, b1, b0, b2, c.mvx, c.mvy);
+    if (k >= 0) {
         c.type = c.cbf ? kCuMerge : kCuSkip;
+        c.mvp_idx = (uint8_t)k;
         return;
     }
     c.type = kCuAmvp;

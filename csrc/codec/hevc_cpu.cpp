@@ -285,7 +285,7 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
     }
     if (!idr) {
         w.put(0, 1);  // num_ref_idx_active_override_flag
-        w.ue(4);      // five_minus_max_num_merge_cand -> MaxNumMergeCand 1
+        w.ue(5 - kMaxMergeCand);  // five_minus_max_num_merge_cand -> MaxNumMergeCand 5
     }
     w.se(qp - 26);  // slice_qp_delta
     if (config().hevc_deblock() || sao) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag

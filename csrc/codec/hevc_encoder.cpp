@@ -46,7 +46,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.tok_off, sizeof(uint32_t) * ncu_pad));
     // + one chunk of padding: k_hevc_arith reads whole 256-token chunks
     HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
-    HIP_CHECK(hipMalloc(&b.sse_part, 3 * sizeof(unsigned long long) * h264::kSsePartStride));
+    HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * h264::kSsePartStride));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.me_fs_host, sizeof(h264::FrameState), hipHostMallocDefault));
@@ -100,6 +100,17 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMalloc(&pre_y_, ysz));
         HIP_CHECK(hipMalloc(&pre_uv_, uvsz));
     }
+    if (cfg.mask_x1 > cfg.mask_x0 && cfg.mask_y1 > cfg.mask_y0) {  // CTB = 16: the H.264 MB-aligned region
+        mask_c_[0] = std::max(0, cfg.mask_x0) / kCtb;
+        mask_c_[1] = std::max(0, cfg.mask_y0) / kCtb;
+        mask_c_[2] = std::min(geom_.mb_w, (cfg.mask_x1 + kCtb - 1) / kCtb);
+        mask_c_[3] = std::min(geom_.mb_h, (cfg.mask_y1 + kCtb - 1) / kCtb);
+    }
+    masked_pixels_ = (int64_t)cfg.width * cfg.height;
+    for (int cy = mask_c_[1]; cy < mask_c_[3]; ++cy)
+        for (int cx = mask_c_[0]; cx < mask_c_[2]; ++cx)
+            masked_pixels_ -= (int64_t)std::max(0, std::min(kCtb, cfg.width - kCtb * cx)) *
+                              std::max(0, std::min(kCtb, cfg.height - kCtb * cy));
     hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
@@ -151,6 +162,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     const int ncu = geom_.mb_w * geom_.mb_h;
     f.n_sse_parts = f.sao ? (ncu + 3) / 4 : ((idr || cfg_.hevc_deblock()) ? geom_.mb_h : (ncu + 3) / 4);
     f.sse_part = sl.buf.sse_part;
+    for (int k = 0; k < 4; ++k) f.mask_c[k] = mask_c_[k];
     f.prev_src = src_keep_[ref];
     f.save_src = src_keep_[cur];
     h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
@@ -293,6 +305,8 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     stats_.bytes = (int)au_.size();
     stats_.encode_ms = ms;
     for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
+    stats_.sse_masked = hdr.sse_masked;
+    stats_.masked_pixels = masked_pixels_;
     rc.end_frame((int)au_.size(), sl.idr);
     return au_;
 }

@@ -131,6 +131,9 @@ struct HevcFrameState {
     int32_t pad_;
     uint8_t* sao_y;
     uint8_t* sao_uv;
+    // quality-report mask in CTBs (x0, y0, x1, y1; x1 <= x0: none): k_hevc_sao adds a 4th
+    // distortion channel, luma of the CTBs outside it (EncoderConfig::mask_*)
+    int32_t mask_c[4];
 };
 
 struct HevcOutHeader {
@@ -139,7 +142,7 @@ struct HevcOutHeader {
     uint32_t overflow;
     uint32_t pad;
     uint64_t sse[3];
-    uint64_t pad2;
+    uint64_t sse_masked;  // luma outside the mask CTBs (SAO path; 0 otherwise)
 };
 static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
@@ -207,12 +210,18 @@ class GpuHevcEncoder final : public VideoEncoder {
     // Per-slice CABAC timing of the last collected picture (diagnostics, synchronous copy):
     // (first CTU, CTUs, payload bytes, wave ticks at 100 MHz) per slice.
     std::vector<std::array<uint64_t, 4>> slice_timing() const;
+   private:
+    int mask_c_[4] = {0, 0, 0, 0};
+    int64_t masked_pixels_ = 0;
+   public:
     // split form (same as GpuH264Encoder) for the session's graph path
     bool prepare(bool force_idr) override;
     void enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void record_start() override;
     void record_done() override;
     bool supports_split() const override { return true; }
+    // masked luma distortion computed by k_hevc_sao (a mask is set and SAO is on)
+    bool masked_sse_in_encoder() const override { return cfg_.sao != 0 && mask_c_[2] > mask_c_[0]; }
     int prep_slot() const override { return prep_slot_; }
     hipStream_t entropy_stream() const override { return stream_e_; }
     void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;

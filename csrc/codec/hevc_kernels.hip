@@ -1489,7 +1489,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
                                                    const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
                                                    uint32_t* __restrict__ prm) {
     __shared__ SaoWave sw[4];
-    __shared__ unsigned long long part[3][4];
+    __shared__ unsigned long long part[4][4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ncu = g.mb_w * g.mb_h;
     const int i = blockIdx.x * 4 + wave;
@@ -1637,12 +1637,16 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     eu = wsum(eu);
     ev = wsum(ev);
     if (lane == 0) {
+        // 4th channel: luma of CTBs outside the quality-report mask
+        const int cx = i % g.mb_w, cy = i / g.mb_w;
+        const bool in_mask = cx >= fs->mask_c[0] && cx < fs->mask_c[2] && cy >= fs->mask_c[1] && cy < fs->mask_c[3];
         part[0][wave] = (unsigned long long)ey;
         part[1][wave] = (unsigned long long)eu;
         part[2][wave] = (unsigned long long)ev;
+        part[3][wave] = valid && !in_mask ? (unsigned long long)ey : 0ull;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 4) {
         const int c = threadIdx.x;
         fs->sse_part[c * h264::kSsePartStride + blockIdx.x] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
     }
@@ -1702,7 +1706,7 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
                                                     uint32_t slice_cap, const uint32_t* __restrict__ slice_len,
                                                     uint8_t* __restrict__ host_out, size_t out_bytes) {
     __shared__ uint32_t red[256];
-    __shared__ unsigned long long red64[3][256];
+    __shared__ unsigned long long red64[4][256];
     const int s = blockIdx.x, tid = threadIdx.x;
     const int num_slices = (int)*nslices;
     if (s >= num_slices) return;
@@ -1736,21 +1740,35 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
         tot += (min(slice_len[k], slice_cap) + 15) & ~15u;
         ovf |= slice_len[k] > slice_cap ? 1u : 0u;
     }
-    unsigned long long e[3] = {0, 0, 0};
+    // distortion partials: 4 channels (the 4th, masked luma, only from k_hevc_sao), loads batched
+    unsigned long long e[4] = {0, 0, 0, 0};
     const int num_sse_parts = fs->n_sse_parts;
+    const int nch = fs->sao ? 4 : 3;
+#pragma unroll 4
     for (int k = tid; k < num_sse_parts; k += 256)
-        for (int c = 0; c < 3; ++c) e[c] += fs->sse_part[c * h264::kSsePartStride + k];
+        for (int c = 0; c < 4; ++c)
+            if (c < nch) e[c] += fs->sse_part[c * h264::kSsePartStride + k];
+    // wave reductions (the former thread-0 loop over 256 x 5 LDS values was ~20 us of the
+    // entropy stream's tail), then 4 partials per value
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int o = 32; o > 0; o >>= 1) {
+        tot += __shfl_xor(tot, o, 64);
+        ovf |= __shfl_xor(ovf, o, 64);
+        for (int c = 0; c < 4; ++c) e[c] += __shfl_xor(e[c], o, 64);
+    }
     __syncthreads();
-    red[tid] = tot | (ovf << 31);
-    for (int c = 0; c < 3; ++c) red64[c][tid] = e[c];
+    if (lane == 0) {
+        red[wv] = tot | (ovf << 31);
+        for (int c = 0; c < 4; ++c) red64[c][wv] = e[c];
+    }
     __syncthreads();
     if (tid == 0) {
         uint32_t T = 0, O = 0;
-        unsigned long long E[3] = {0, 0, 0};
-        for (int k = 0; k < 256; ++k) {
+        unsigned long long E[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; ++k) {
             T += red[k] & 0x7fffffffu;
             O |= red[k] >> 31;
-            for (int c = 0; c < 3; ++c) E[c] += red64[c][k];
+            for (int c = 0; c < 4; ++c) E[c] += red64[c][k];
         }
         HevcOutHeader h;
         h.total_bytes = T;
@@ -1758,7 +1776,7 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
         h.overflow = (O || T > out_bytes) ? 1u : 0u;
         h.pad = 0;
         for (int c = 0; c < 3; ++c) h.sse[c] = E[c];
-        h.pad2 = 0;
+        h.sse_masked = E[3];
         *reinterpret_cast<HevcOutHeader*>(host_out) = h;
     }
 }

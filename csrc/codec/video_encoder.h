@@ -41,6 +41,8 @@ class VideoEncoder {
     // picture type) and linked per frame by link_entropy() (analysis event -> entropy stream).
     // supports_split() false: eager submission only.
     virtual bool supports_split() const { return false; }
+    // FrameStats::sse_masked / masked_pixels are filled by the encoder itself (no separate pass)
+    virtual bool masked_sse_in_encoder() const { return false; }
     virtual int prep_slot() const { return 0; }
     virtual hipStream_t entropy_stream() const { return nullptr; }
     virtual void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) { (void)idr; (void)src_y; (void)src_uv; }

@@ -139,7 +139,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
             pix::upload_scale_frags(fr, &lt_mf_mem_, lt_.mf);
     }
     for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
-    mask_in_encoder_ = std::string(enc_->codec()) == "h264";
+    mask_in_encoder_ = enc_->masked_sse_in_encoder();
     if (masked() && !mask_in_encoder_) {
         const h264::Geometry& eg = enc_->geometry();
         const int nb = pix::sse_masked_blocks(eg.width, eg.height);

@@ -468,3 +468,32 @@ def test_graph_replay_depth2_matches_eager(gpu, codec):
     assert g0 == 0 and g1 >= 4
     for i, (a, b) in enumerate(zip(eager, graph)):
         assert a == b, f"frame {i} differs"
+
+
+def test_session_hevc_masked_psnr_from_encoder(gpu):
+    """HEVC with SAO: k_hevc_sao's 4th distortion channel (luma of the CTBs outside the mask
+    rectangle, the same 16-aligned region as H.264's) equals the PSNR of the decoded picture
+    over those samples, IDR and P pictures; no separate masked-SSE pass runs."""
+    from mxdesk.codec.hevc_decoder import Decoder as HevcDecoder
+
+    cfg = gpu.SessionConfig()
+    cfg.width, cfg.height, cfg.fps = 200, 120, 60
+    cfg.codec = "hevc"
+    cfg.enc.bitrate_kbps = 0
+    cfg.enc.qp = 30
+    cfg.mask_x0, cfg.mask_y0, cfg.mask_x1, cfg.mask_y1 = 20, 40, 90, 75  # -> CTBs x 1..5, y 2..4
+    s = gpu.Session(cfg)
+    stream, res, srcs = b"", [], []
+    for _ in range(4):
+        r = s.step(False)
+        stream += r.au
+        res.append(r)
+        srcs.append(s.nv12()[0][:120, :200].astype(np.float64))
+    frames = HevcDecoder().decode(stream)
+    assert len(frames) == 4
+    keep = np.ones((120, 200), bool)
+    keep[32:80, 16:96] = False
+    for (dy, _, _), sy, r in zip(frames, srcs, res):
+        mse = np.mean(((dy[:120, :200].astype(np.float64) - sy) ** 2)[keep])
+        want = 99.0 if mse == 0 else min(99.0, 10 * np.log10(255.0 ** 2 / mse))
+        assert abs(want - r.psnr_y_masked) < 1e-6, (want, r.psnr_y_masked)
