@@ -47,6 +47,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     // + one chunk of padding: k_hevc_arith reads whole 256-token chunks
     HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * h264::kSsePartStride));
+    HIP_CHECK(hipMalloc(&b.sse_tot, 4 * sizeof(unsigned long long)));
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.me_fs_host, sizeof(h264::FrameState), hipHostMallocDefault));
@@ -62,7 +63,7 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
                     (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
-                    (void*)b.sse_part, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
+                    (void*)b.sse_part, (void*)b.sse_tot, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
                     (void*)b.tok_dense})
         if (p) (void)hipFree(p);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
@@ -162,6 +163,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     const int ncu = geom_.mb_w * geom_.mb_h;
     f.n_sse_parts = f.sao ? (ncu + 3) / 4 : ((idr || cfg_.hevc_deblock()) ? geom_.mb_h : (ncu + 3) / 4);
     f.sse_part = sl.buf.sse_part;
+    f.sse_tot = sl.buf.sse_tot;
     for (int k = 0; k < 4; ++k) f.mask_c[k] = mask_c_[k];
     f.prev_src = src_keep_[ref];
     f.save_src = src_keep_[cur];

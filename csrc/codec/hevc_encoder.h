@@ -134,6 +134,9 @@ struct HevcFrameState {
     // quality-report mask in CTBs (x0, y0, x1, y1; x1 <= x0: none): k_hevc_sao adds a 4th
     // distortion channel, luma of the CTBs outside it (EncoderConfig::mask_*)
     int32_t mask_c[4];
+    // k_hevc_sao's distortion totals (4 channels), accumulated with one atomic per workgroup and
+    // channel; zeroed by k_hevc_layout earlier on the same stream
+    unsigned long long* sse_tot;
 };
 
 struct HevcOutHeader {
@@ -173,6 +176,7 @@ struct HevcDeviceBuffers {
     uint16_t* tok_dense;            // [ncu * kMaxCuTokens + 512] tokens in decoding order
     size_t out_bytes;
     unsigned long long* sse_part;
+    unsigned long long* sse_tot;  // [4] k_hevc_sao distortion totals
 };
 
 void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,

@@ -1008,6 +1008,7 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
                                                        int* __restrict__ slice_of_cu, uint32_t* __restrict__ nslices) {
     __shared__ uint32_t wtot[16];
     const int tid = threadIdx.x;
+    if (tid < 4) fs->sse_tot[tid] = 0ull;  // k_hevc_sao accumulates into these next
     if (fs->idr) {
         const int sr = fs->slice_rows, S = fs->num_slices;
         for (int k = tid; k < S; k += blockDim.x) slice_first[k] = k * sr * ctb_w;
@@ -1646,9 +1647,9 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         part[3][wave] = valid && !in_mask ? (unsigned long long)ey : 0ull;
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < 4) {  // one atomic per workgroup and channel (k_hevc_pack reads the totals)
         const int c = threadIdx.x;
-        fs->sse_part[c * h264::kSsePartStride + blockIdx.x] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
+        atomicAdd(fs->sse_tot + c, part[c][0] + part[c][1] + part[c][2] + part[c][3]);
     }
 }
 
@@ -1742,12 +1743,15 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
     }
     // distortion partials: 4 channels (the 4th, masked luma, only from k_hevc_sao), loads batched
     unsigned long long e[4] = {0, 0, 0, 0};
-    const int num_sse_parts = fs->n_sse_parts;
-    const int nch = fs->sao ? 4 : 3;
+    if (fs->sao) {  // totals accumulated by k_hevc_sao (a serial walk over 8,100 partials x 4 was
+                    // ~30 us at the end of the entropy stream)
+        if (tid < 4) e[tid] = fs->sse_tot[tid];
+    } else {
+        const int num_sse_parts = fs->n_sse_parts;
 #pragma unroll 4
-    for (int k = tid; k < num_sse_parts; k += 256)
-        for (int c = 0; c < 4; ++c)
-            if (c < nch) e[c] += fs->sse_part[c * h264::kSsePartStride + k];
+        for (int k = tid; k < num_sse_parts; k += 256)
+            for (int c = 0; c < 3; ++c) e[c] += fs->sse_part[c * h264::kSsePartStride + k];
+    }
     // wave reductions (the former thread-0 loop over 256 x 5 LDS values was ~20 us of the
     // entropy stream's tail), then 4 partials per value
     const int lane = tid & 63, wv = tid >> 6;
