@@ -1976,19 +1976,21 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
     const bool skip = decide_skip(nb, av, mvd);
     // mb_qp_delta: QP predictor = QP of the previous MB in the slice that carried one (a P
     // macroblock with residual); skipped / residual-free MBs inherit it.  Half-wave-parallel
-    // backward search, 32 MBs per step (the ballot holds active lanes only; this half's bits
-    // are taken).  I slices: every MB is at the slice QP.
-    // 128 MBs per step: each lane tests 4 (independent loads, one latency per step) and carries
-    // the QP along, so the predictor comes from a shuffle rather than another dependent load.
+    // backward search (the ballot holds active lanes only; this half's bits are taken), 512 MBs
+    // per step: each lane tests 16 (independent loads, one latency per step) -- static desktop
+    // areas are long skip runs, and at 128 MBs per step the dependent steps through them were
+    // ~7 us of k_cavlc (a separate scan kernel cost more than it saved: profiles/r03_h264).
+    // I slices: every MB is at the slice QP.
     int dqp = 0;
     if (!skip && !fs->idr && carries_dqp(m)) {
         const int per_slice = fs->slice_rows * g.mb_w, first = (mbi / per_slice) * per_slice;
         int pred = fs->qp;
         bool found = false;
-        for (int j0 = mbi - 1; j0 >= first && !found; j0 -= 128) {
-            int qv[4];
+        constexpr int kPer = 16;
+        for (int j0 = mbi - 1; j0 >= first && !found; j0 -= 32 * kPer) {
+            int qv[kPer];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < kPer; ++k) {
                 const int j = j0 - 32 * k - lane;
                 qv[k] = -1;
                 if (j >= first) {
@@ -1997,7 +1999,7 @@ __global__ __launch_bounds__(256) void k_cavlc(Geometry g, const FrameState* __r
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < kPer; ++k) {
                 const unsigned long long bal = __ballot(qv[k] >= 0);
                 const uint32_t hb = (uint32_t)(bal >> (32 * hw));
                 const int q = __shfl(qv[k], hb ? (int)(__ffs(hb) - 1) : 0, 32);
