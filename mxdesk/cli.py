@@ -119,6 +119,10 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
 
     if cfg.source == "x11":
         raise SystemExit("serve --sessions K > 1 streams synthetic desktops; MXDESK_SOURCE=x11 serves one")
+    # every session drives two HIP streams; with HIP's default of 4 hardware queues per process,
+    # K sessions' streams share 4 queues and serialise behind each other.  Must be set before
+    # the HIP runtime initialises (the first pipeline below); an explicit setting wins.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(16, 2 * k))))
     device = _gpu_index(cfg) if cfg.gpu_encoder else 0
     servers = []
     for i in range(k):
