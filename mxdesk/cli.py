@@ -123,11 +123,15 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
     # K sessions' streams share 4 queues and serialise behind each other.  Must be set before
     # the HIP runtime initialises (the first pipeline below); an explicit setting wins.
     os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(16, 2 * k))))
+    # K frame threads and the event loop trade the GIL every frame; with the default 5 ms switch
+    # interval a thread that wants it can wait a whole interval behind a busy one
+    sys.setswitchinterval(float(os.environ.get("MXDESK_SWITCH_INTERVAL", "0.0005")))
     device = _gpu_index(cfg) if cfg.gpu_encoder else 0
     servers = []
     for i in range(k):
         ci = session_config(cfg, i)
         pipe = build_pipeline(ci, device, session_name=str(i), capture_allowed=False)
+        pipe.pace_phase = i / (k * max(1.0, float(ci.stream_fps)))  # spread the K sessions over the period
         servers.append(MediaServer(pipe, ci))
     print(f"mxdesk: serving {k} sessions {cfg.sizew}x{cfg.sizeh}@{cfg.stream_fps} ({cfg.encoder_backend}) on "
           f"{cfg.addr}:{cfg.port}..{cfg.port + k - 1}", flush=True)

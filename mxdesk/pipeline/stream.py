@@ -317,7 +317,11 @@ class StreamPipeline:
         return fr
 
     def _run(self) -> None:
-        next_t = time.monotonic()
+        # pacing phase (seconds into the frame period): sessions of one process start staggered
+        # so their frames do not all reach the GPU in the same instant of every period
+        next_t = time.monotonic() + float(getattr(self, "pace_phase", 0.0))
+        if self.paced and next_t > time.monotonic():
+            self._stop.wait(next_t - time.monotonic())
         while not self._stop.is_set():
             try:
                 self.step()

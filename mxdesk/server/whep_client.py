@@ -182,9 +182,21 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
         req = S.StunMessage(S.BINDING_REQUEST, None, [
             (S.A_USERNAME, f"{r_ufrag}:{ufrag}".encode()), (S.A_PRIORITY, struct.pack("!I", 1853824767)),
             (S.A_ICE_CONTROLLING, os.urandom(8)), (S.A_USE_CANDIDATE, b"")])
-        tr.sendto(req.encode(r_pwd.encode()))
+        # retransmitted like a browser's ICE agent (RFC 8445 / 5389: RTO from 250 ms, doubling):
+        # a single lost check must not stall the session until the deadline
+        req_bytes = req.encode(r_pwd.encode())
+        tr.sendto(req_bytes)
+        rto, next_tx = 0.25, time.monotonic() + 0.25
         while True:
-            d = await asyncio.wait_for(cl.q.get(), max(0.1, deadline - time.monotonic()))
+            try:
+                d = await asyncio.wait_for(cl.q.get(), max(0.02, min(next_tx, deadline) - time.monotonic()))
+            except asyncio.TimeoutError:
+                if time.monotonic() > deadline:
+                    raise
+                tr.sendto(req_bytes)
+                rto = min(rto * 2, 2.0)
+                next_tx = time.monotonic() + rto
+                continue
             if S.is_stun(d):
                 m = S.StunMessage.decode(d)
                 if m.type == S.BINDING_SUCCESS and m.tid == req.tid:
