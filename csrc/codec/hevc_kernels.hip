@@ -1019,18 +1019,31 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     // tiles of kScanTile CUs, 4 consecutive per thread with one 16-byte load (coalesced; the
     // former per-thread contiguous chunks made every load touch 64 cache lines of one CU's
     // memory pipeline: 67 us at 4K).  Pass 1: per-tile prefixes and the total.
+    // Tile totals by wave reductions and one LDS atomic per wave and tile (no workgroup barrier
+    // per tile), then their exclusive prefix.
     __shared__ uint32_t tile_pre[kMaxScanTiles];
-    uint32_t carry = 0;
+    __shared__ uint32_t tile_sum[kMaxScanTiles];
+    __shared__ uint32_t total_sh;
+    for (int k = tid; k < kMaxScanTiles; k += (int)blockDim.x) tile_sum[k] = 0;
+    __syncthreads();
     int nt = 0;
     for (int base = 0; base < ncu; base += kScanTile, ++nt) {
         const uint4 v = ld4(cost, base + 4 * tid);
-        uint32_t tt;
-        (void)block_excl_scan(v.x + v.y + v.z + v.w, wtot, &tt);
-        if (tid == 0) tile_pre[nt] = carry;
-        carry += tt;
+        uint32_t w = v.x + v.y + v.z + v.w;
+        for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+        if ((tid & 63) == 0) atomicAdd(&tile_sum[nt], w);
     }
     __syncthreads();
-    const uint32_t total = carry;
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int t = 0; t < nt; ++t) {
+            tile_pre[t] = run;
+            run += tile_sum[t];
+        }
+        total_sh = run;
+    }
+    __syncthreads();
+    const uint32_t total = total_sh;
     const int S = plan_num_slices(total, max_slices, (uint32_t)slice_cost);
     // slice id of a prefix p is the number of thresholds T_s = ceil(s * total / S) (s >= 1) <= p:
     // one division per thread and tile, then threshold tracking across its 4 CUs
