@@ -11,7 +11,7 @@ SRC=("$ROOT/tools/sanitize_main.cpp" "$ROOT/csrc/codec/h264_encoder.cpp" "$ROOT/
      "$ROOT/csrc/codec/h264_kernels.hip" "$ROOT/csrc/codec/h264_deblock.hip" "$ROOT/csrc/codec/hevc_cpu.cpp" "$ROOT/csrc/codec/hevc_encoder.cpp"
      "$ROOT/csrc/codec/hevc_kernels.hip" "$ROOT/csrc/codec/vp8_bitstream.cpp" "$ROOT/csrc/codec/vp8_cpu.cpp"
      "$ROOT/csrc/codec/vp8_gpu.cpp" "$ROOT/csrc/codec/vp8_kernels.hip" "$ROOT/csrc/net/srtp.cpp" "$ROOT/csrc/net/dtls.cpp"
-     "$ROOT/csrc/net/rtp_h264.cpp" "$ROOT/csrc/net/rtp_h265.cpp" "$ROOT/csrc/net/rtp_vp8.cpp" "$ROOT/csrc/net/sctp.cpp")
+     "$ROOT/csrc/net/rtp_h264.cpp" "$ROOT/csrc/net/rtp_h265.cpp" "$ROOT/csrc/net/rtp_vp8.cpp" "$ROOT/csrc/net/sctp.cpp" "$ROOT/csrc/net/rtp_sender.cpp")
 objs=()
 for s in "${SRC[@]}"; do
   o="$OUT/$(basename "$s").o"

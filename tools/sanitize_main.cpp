@@ -3,7 +3,11 @@
 // HIP kernels), SRTP/SRTCP, DTLS-SRTP handshake, RTP H.264 / H.265 / VP8 packetizers, Annex-B
 // splitter.
 // Built by tools/sanitize.sh with -fsanitize on the host side only; no GPU is touched.
+#include <arpa/inet.h>
 #include <cstdio>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
 #include <cstdlib>
 #include <random>
 #include <string>
@@ -15,6 +19,7 @@
 #include "../csrc/net/dtls.h"
 #include "../csrc/net/rtp_h264.h"
 #include "../csrc/net/rtp_h265.h"
+#include "../csrc/net/rtp_sender.h"
 #include "../csrc/net/rtp_vp8.h"
 #include "../csrc/net/sctp.h"
 #include "../csrc/net/srtp.h"
@@ -217,8 +222,46 @@ static void sctp_pass(std::mt19937& rng) {
     CHECK(a.sctp().buffered_amount() == 0);
 }
 
+// Two-phase HEVC CABAC (bin tokens) against direct coding on random slices, and the native RTP
+// send path (packetize -> NACK history -> SRTP -> sendto) into a local UDP socket.
+static void token_and_sender_pass(std::mt19937& rng) {
+    CHECK(hevc::token_selftest(rng() & 0xffff, 60) == 60);
+    const int rx = socket(AF_INET, SOCK_DGRAM, 0), tx = socket(AF_INET, SOCK_DGRAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    CHECK(bind(rx, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0);
+    socklen_t len = sizeof a;
+    CHECK(getsockname(rx, reinterpret_cast<sockaddr*>(&a), &len) == 0);
+    net::UdpPeer peer(tx, "127.0.0.1", ntohs(a.sin_port));
+    net::RtpHistory hist(64);
+    net::SrtpSession srtp(std::string(16, 'k'), std::string(14, 's'));
+    net::RtpH264Packetizer pk(0x1234, 96, 1150, 100);
+    std::string au;
+    for (int n = 0; n < 3; ++n) {
+        au += std::string("\x00\x00\x00\x01", 4);
+        const size_t nal = 100 + rng() % 4000;
+        au.push_back((char)0x65);
+        for (size_t i = 1; i < nal; ++i) au.push_back((char)(1 + rng() % 255));
+    }
+    const std::vector<std::string> raw = pk.packetize(au, 9000);
+    CHECK(net::send_rtp_packets(raw, srtp, hist, peer) == (int)raw.size());
+    for (const std::string& p : raw) {
+        const uint16_t seq = (uint16_t)(((uint8_t)p[2] << 8) | (uint8_t)p[3]);
+        const std::string* h = hist.get(seq);
+        CHECK(h != nullptr && *h == p);
+    }
+    char buf[2048];
+    int got = 0;
+    while (got < (int)raw.size() && recv(rx, buf, sizeof buf, MSG_DONTWAIT) > 0) ++got;
+    CHECK(got == (int)raw.size());
+    close(rx);
+    close(tx);
+}
+
 int main() {
     std::mt19937 rng(12345);
+    token_and_sender_pass(rng);
     encoder_pass(rng);
     hevc_pass(rng);
     vp8_pass(rng);
