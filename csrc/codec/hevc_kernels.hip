@@ -1453,9 +1453,14 @@ __device__ __forceinline__ int sao_cat3(const int (*n)[3]) {
     const int a = n[1 + kSaoDy[K][0]][1 + kSaoDx[K][0]], b = n[1 + kSaoDy[K][1]][1 + kSaoDx[K][1]];
     return (a < 0 || b < 0) ? 0 : sao_edge_cat(n[1][1], a, b);
 }
-__device__ __forceinline__ void sao_acc(int* e, int d, const int (*n)[3]) {
+// the four class categories of the centre of n, 3 bits each (class k at bits 3k..3k+2)
+__device__ __forceinline__ uint32_t sao_cats(const int (*n)[3]) {
+    return (uint32_t)sao_cat3<0>(n) | ((uint32_t)sao_cat3<1>(n) << 3) | ((uint32_t)sao_cat3<2>(n) << 6) |
+           ((uint32_t)sao_cat3<3>(n) << 9);
+}
+__device__ __forceinline__ void sao_acc(int* e, int d, uint32_t cats) {
     const int v = (1 << 20) + d;
-    const int c0 = sao_cat3<0>(n), c1 = sao_cat3<1>(n), c2 = sao_cat3<2>(n), c3 = sao_cat3<3>(n);
+    const int c0 = (int)(cats & 7), c1 = (int)((cats >> 3) & 7), c2 = (int)((cats >> 6) & 7), c3 = (int)((cats >> 9) & 7);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         e[q] += c0 == q + 1 ? v : 0;
@@ -1463,13 +1468,6 @@ __device__ __forceinline__ void sao_acc(int* e, int d, const int (*n)[3]) {
         e[8 + q] += c2 == q + 1 ? v : 0;
         e[12 + q] += c3 == q + 1 ? v : 0;
     }
-}
-// SAO output of the centre of n: the four class categories are computed and the one of class
-// sao_eo(w) selected (a select between loaded neighbours would become a scratch-indexed load)
-__device__ __forceinline__ int sao_out3(uint32_t w, const int (*n)[3]) {
-    const int k = sao_eo(w);
-    const int c0 = sao_cat3<0>(n), c1 = sao_cat3<1>(n), c2 = sao_cat3<2>(n), c3 = sao_cat3<3>(n);
-    return sao_sample_cat(w, n[1][1], k == 0 ? c0 : (k == 1 ? c1 : (k == 2 ? c2 : c3)));
 }
 // Sum of 16 per-lane values over the wave in 17 shuffles: four halving exchanges (xor 32, 16,
 // 8, 4) leave value (lane >> 2) & 15 summed over 16 lanes, two more steps finish the sum;
@@ -1517,7 +1515,9 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     sao_wave_sync();
     const int r = lane >> 2, c0 = (lane & 3) * 4;
     const int xc = x0 / 2 + (lane & 7), yc = y0 / 2 + (lane >> 3);
-    // ---- statistics
+    // ---- statistics (the edge categories and centre samples are kept for the apply phase)
+    uint64_t cat_y = 0;
+    uint32_t cen_y = 0, cat_u = 0, cat_v = 0, cen_uv = 0;
     if (valid) {
         int L[3][6];
         sao_luma_window(ry, g.pitch, W, H, x0 + c0, y0 + r, L);
@@ -1533,9 +1533,12 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
 #pragma unroll
                 for (int b = 0; b < 3; ++b) n[a][b] = L[a][j + b];
             const int d = (int)((sv >> (8 * j)) & 255) - n[1][1];
-            sao_acc(e, d, n);
+            const uint32_t ck = sao_cats(n);
+            cat_y |= (uint64_t)ck << (12 * j);  // re-used by the apply phase
+            sao_acc(e, d, ck);
             atomicAdd(&S.bo[0][n[1][1] >> 3], (1 << 20) + d);
         }
+        cen_y = (uint32_t)L[1][1] | ((uint32_t)L[1][2] << 8) | ((uint32_t)L[1][3] << 16) | ((uint32_t)L[1][4] << 24);
         int t = sao_reduce16(e, lane);
         if ((lane & 3) == 0) S.eo[0][(lane >> 2) & 15] = t;
         int U[3][3], V[3][3];
@@ -1544,13 +1547,16 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         const int du = (int)(spair & 255) - U[1][1], dv = (int)(spair >> 8) - V[1][1];
 #pragma unroll
         for (int q = 0; q < 16; ++q) e[q] = 0;
-        sao_acc(e, du, U);
+        cat_u = sao_cats(U);
+        cat_v = sao_cats(V);
+        cen_uv = (uint32_t)U[1][1] | ((uint32_t)V[1][1] << 8);
+        sao_acc(e, du, cat_u);
         atomicAdd(&S.bo[1][U[1][1] >> 3], (1 << 20) + du);
         t = sao_reduce16(e, lane);
         if ((lane & 3) == 0) S.eo[1][(lane >> 2) & 15] = t;
 #pragma unroll
         for (int q = 0; q < 16; ++q) e[q] = 0;
-        sao_acc(e, dv, V);
+        sao_acc(e, dv, cat_v);
         atomicAdd(&S.bo[2][V[1][1] >> 3], (1 << 20) + dv);
         t = sao_reduce16(e, lane);
         if ((lane & 3) == 0) S.eo[2][(lane >> 2) & 15] = t;
@@ -1620,26 +1626,20 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     int ey = 0, eu = 0, ev = 0;
     if (valid) {
         const uint32_t wy = S.w[0], wu = S.w[1], wv = S.w[2];
-        int L[3][6];
-        sao_luma_window(ry, g.pitch, W, H, x0 + c0, y0 + r, L);
         const uint32_t sv = *(const sao_gu32*)(src_y + (size_t)(y0 + r) * g.pitch + x0 + c0);
         uint32_t packed = 0;
+        const int ky = 3 * sao_eo(wy);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            int n[3][3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) n[a][b] = L[a][j + b];
-            const int o = sao_out3(wy, n);
+            const int cat = (int)((cat_y >> (12 * j + ky)) & 7);
+            const int o = sao_sample_cat(wy, (int)((cen_y >> (8 * j)) & 255), cat);
             packed |= (uint32_t)o << (8 * j);
             const int d = (int)((sv >> (8 * j)) & 255) - o;
             ey += (x0 + c0 + j < g.width && y0 + r < g.height) ? d * d : 0;
         }
         *(sao_gu32*)(fs->sao_y + (size_t)(y0 + r) * g.pitch + x0 + c0) = packed;
-        int U[3][3], V[3][3];
-        sao_chroma_window(ruv, g.pitch, Wc, Hc, xc, yc, U, V);
-        const int u = sao_out3(wu, U), v = sao_out3(wv, V);
+        const int u = sao_sample_cat(wu, (int)(cen_uv & 255), (int)((cat_u >> (3 * sao_eo(wu))) & 7));
+        const int v = sao_sample_cat(wv, (int)(cen_uv >> 8), (int)((cat_v >> (3 * sao_eo(wv))) & 7));
         *(sao_gu16*)(fs->sao_uv + (size_t)yc * g.pitch + 2 * xc) = (uint16_t)(u | (v << 8));
         const uint32_t spair = *(const sao_gu16*)(src_uv + (size_t)yc * g.pitch + 2 * xc);
         const bool disp = 2 * xc < g.width && 2 * yc < g.height;
