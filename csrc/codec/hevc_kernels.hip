@@ -73,25 +73,43 @@ __device__ __forceinline__ uint32_t wor(uint32_t v) {
 }
 
 // Transform matrices in LDS (filled once per workgroup).
-struct Mats {
+struct alignas(16) Mats {
     int16_t t16[256];
     int16_t t8[64];
     int16_t t4[16];
+    int16_t tt16[256];  // transposed: tt16[y * 16 + k] = t16[k * 16 + y] (inverse stages)
+    int16_t tt8[64];
 };
 __device__ __forceinline__ void fill_mats(Mats& m) {
     for (int i = threadIdx.x; i < 256 + 64 + 16; i += blockDim.x) {
-        if (i < 256)
+        if (i < 256) {
             m.t16[i] = (int16_t)dct_coef(4, i >> 4, i & 15);
-        else if (i < 320)
+            m.tt16[i] = (int16_t)dct_coef(4, i & 15, i >> 4);
+        } else if (i < 320) {
             m.t8[i - 256] = (int16_t)dct_coef(3, (i - 256) >> 3, (i - 256) & 7);
-        else
+            m.tt8[i - 256] = (int16_t)dct_coef(3, (i - 256) & 7, (i - 256) >> 3);
+        } else {
             m.t4[i - 320] = (int16_t)dct_coef(2, (i - 320) >> 2, (i - 320) & 3);
+        }
     }
 }
 
+// Integer dot products of 16 / 8 int16 pairs from 16-byte aligned LDS rows with v_dot2 (two
+// multiply-adds per VALU instruction, one ds_read_b128 per 8 values).  Exact: int32 sums.
+typedef short mx_short2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int dot2acc(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(mx_short2, a), __builtin_bit_cast(mx_short2, b), c, false);
+}
+__device__ __forceinline__ int dot8(const int16_t* a, const int16_t* b) {
+    const uint4 x = *reinterpret_cast<const uint4*>(a), y = *reinterpret_cast<const uint4*>(b);
+    return dot2acc(x.w, y.w, dot2acc(x.z, y.z, dot2acc(x.y, y.y, dot2acc(x.x, y.x, 0))));
+}
+__device__ __forceinline__ int dot16(const int16_t* a, const int16_t* b) { return dot8(a, b) + dot8(a + 8, b + 8); }
+
 // Per-wave TU scratch: residual / prediction / two int32 stage buffers for 256 luma +
-// 2 x 64 chroma samples.
-struct TuBuf {
+// 2 x 64 chroma samples (code_tus keeps int16 stage values in them, laid out so that every
+// transform stage reads contiguous 16-byte rows: see its comments).
+struct alignas(16) TuBuf {
     int16_t res[384];
     uint8_t pred[384];
     int32_t a[384];
@@ -118,22 +136,24 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
                                              int y0, int disp_w, int disp_h) {
     const int lane = threadIdx.x & 63;
     const int comp = lane >> 5, cl = lane & 31;
+    // int16 views of the stage buffers: aT = forward stage 1 transposed (aT[k][y]), bT = the
+    // dequantised levels transposed (bT[x][k]), a16 = inverse stage 1 (a16[y][x]); forward
+    // stage 1 fits 16 bits (|res| <= 255, row sums of |T| <= 1024 before the >> 3 / >> 2)
+    int16_t* aT = reinterpret_cast<int16_t*>(t.a);
+    int16_t* a16 = reinterpret_cast<int16_t*>(t.a);
+    int16_t* bT = reinterpret_cast<int16_t*>(t.b);
     // ---- forward stage 1 (rows): a[y][k] = sum_n T[k][n] res[y][n]
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = lane * 4 + j, y = idx >> 4, k = idx & 15;
-            int s = 0;
-#pragma unroll
-            for (int n = 0; n < 16; ++n) s += M.t16[k * 16 + n] * t.res[y * 16 + n];
-            t.a[idx] = (s + 4) >> 3;
+            const int s = dot16(M.t16 + k * 16, t.res + y * 16);
+            aT[k * 16 + y] = (int16_t)((s + 4) >> 3);
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = cl * 2 + j, y = idx >> 3, k = idx & 7;
             const int16_t* r = t.res + 256 + comp * 64;
-            int s = 0;
-#pragma unroll
-            for (int n = 0; n < 8; ++n) s += M.t8[k * 8 + n] * r[y * 8 + n];
-            t.a[256 + comp * 64 + idx] = (s + 2) >> 2;
+            const int s = dot8(M.t8 + k * 8, r + y * 8);
+            aT[256 + comp * 64 + k * 8 + y] = (int16_t)((s + 2) >> 2);
         }
     }
     __syncthreads();
@@ -146,19 +166,14 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = lane * 4 + j, k2 = idx >> 4, k = idx & 15;
-            int s = 0;
-#pragma unroll
-            for (int y = 0; y < 16; ++y) s += M.t16[k2 * 16 + y] * t.a[y * 16 + k];
+            const int s = dot16(M.t16 + k2 * 16, aT + k * 16);
             ll[j] = quant_coef((s + 512) >> 10, qp, 4, intra);
             nzl += ll[j] != 0;
             mxl = max(mxl, abs(ll[j]));
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = cl * 2 + j, k2 = idx >> 3, k = idx & 7;
-            const int32_t* a = t.a + 256 + comp * 64;
-            int s = 0;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) s += M.t8[k2 * 8 + y] * a[y * 8 + k];
+            const int s = dot8(M.t8 + k2 * 8, aT + 256 + comp * 64 + k * 8);
             lc[j] = quant_coef((s + 256) >> 9, qpc, 3, intra);
             nzc += lc[j] != 0;
             mxc = max(mxc, abs(lc[j]));
@@ -228,7 +243,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             if (l) lbits += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
             const int si = scan_index(4, k, k2);
             coef[si] = (int16_t)l;
-            t.b[idx] = dequant_coef(l, qp, 4);
+            bT[k * 16 + k2] = (int16_t)dequant_coef(l, qp, 4);
             if (l) {
                 ++nzl;
                 lastl = si > lastl ? si : lastl;
@@ -241,7 +256,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             if (l) cbits += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
             const int si = scan_index(3, k, k2);
             coef[256 + comp * 64 + si] = (int16_t)l;
-            t.b[256 + comp * 64 + idx] = dequant_coef(l, qpc, 3);
+            bT[256 + comp * 64 + k * 8 + k2] = (int16_t)dequant_coef(l, qpc, 3);
             if (l) {
                 ++nzc;
                 lastc = si > lastc ? si : lastc;
@@ -271,18 +286,13 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = lane * 4 + j, y = idx >> 4, x = idx & 15;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) s += M.t16[k * 16 + y] * t.b[k * 16 + x];
-            t.a[idx] = clip16((s + 64) >> 7);
+            const int s = dot16(M.tt16 + y * 16, bT + x * 16);
+            a16[idx] = (int16_t)clip16((s + 64) >> 7);
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = cl * 2 + j, y = idx >> 3, x = idx & 7;
-            const int32_t* b = t.b + 256 + comp * 64;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + y] * b[k * 8 + x];
-            t.a[256 + comp * 64 + idx] = clip16((s + 64) >> 7);
+            const int s = dot8(M.tt8 + y * 8, bT + 256 + comp * 64 + x * 8);
+            a16[256 + comp * 64 + idx] = (int16_t)clip16((s + 64) >> 7);
         }
     }
     __syncthreads();
@@ -293,9 +303,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         uint32_t packed = 0;
         for (int j = 0; j < 4; ++j) {
             const int x = xb + j;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) s += M.t16[k * 16 + x] * t.a[y * 16 + k];
+            const int s = dot16(M.tt16 + x * 16, a16 + y * 16);
             const int r = out.nz[0] ? (s + 2048) >> 12 : 0;
             const int p = t.pred[y * 16 + x];
             const int v = clip255(p + r);
@@ -310,10 +318,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         const int nzcomp = comp ? out.nz[2] : out.nz[1];
         for (int j = 0; j < 2; ++j) {
             const int idx = cl * 2 + j, yy = idx >> 3, x = idx & 7;
-            const int32_t* a = t.a + 256 + comp * 64;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + x] * a[yy * 8 + k];
+            const int s = dot8(M.tt8 + x * 8, a16 + 256 + comp * 64 + yy * 8);
             const int r = nzcomp ? (s + 2048) >> 12 : 0;
             const int o = 256 + comp * 64 + idx;
             const int p = t.pred[o];
@@ -340,6 +345,62 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
 // the trailing trim per TU through segmented shuffle reductions.  Levels go to lv (CU
 // layout), the reconstruction to rec (TuBuf layout); t.a / t.b are the stage buffers.
 // Called by every wave of the workgroup (barriers inside).
+// cu_summarise (hevc_core.h) of a split transform tree, by the whole wave: one ballot per
+// luma TU (lane = scan index) and one per chroma component (lane = 16 * TU + scan index) give
+// the coded masks, the rest is scalar (lane 0 alone walking 384 LDS levels cost ~1,100 VALU).
+struct SplitSummary {
+    uint8_t cbf, cbf_y4, cbf_c4, last[3], csbf_c[2];
+    uint16_t csbf_y;
+    __device__ void apply(CuInfo& c) const {
+        c.cbf = cbf;
+        c.cbf_y4 = cbf_y4;
+        c.cbf_c4 = cbf_c4;
+        c.last[0] = last[0];
+        c.last[1] = last[1];
+        c.last[2] = last[2];
+        c.csbf_y = csbf_y;
+        c.csbf_c[0] = csbf_c[0];
+        c.csbf_c[1] = csbf_c[1];
+    }
+};
+__device__ SplitSummary split_summary_wave(const int16_t* co, int lane) {
+    SplitSummary s = {};
+    uint32_t lsum = 0, csy = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t b = __ballot(co[64 * k + lane] != 0);
+        if (b) {
+            s.cbf_y4 |= (uint8_t)(1u << k);
+            lsum += (uint32_t)(64 - __builtin_clzll(b));
+            uint32_t m = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m |= ((b >> (16 * q)) & 0xffffu) ? 1u << q : 0u;
+            csy |= m << (4 * k);
+        }
+    }
+    s.cbf = s.cbf_y4 ? 1 : 0;
+    s.last[0] = (uint8_t)(lsum ? (lsum > 256 ? 255 : lsum - 1) : 0);
+    s.csbf_y = (uint16_t)csy;
+#pragma unroll
+    for (int comp = 0; comp < 2; ++comp) {
+        const uint64_t b = __ballot(co[256 + 64 * comp + lane] != 0);
+        uint32_t csum = 0, cm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t f = (uint32_t)((b >> (16 * k)) & 0xffffu);
+            if (f) {
+                s.cbf_c4 |= (uint8_t)(1u << (4 * comp + k));
+                csum += (uint32_t)(32 - __builtin_clz(f));
+                cm |= 1u << k;
+            }
+        }
+        if (cm) s.cbf |= (uint8_t)(2 << comp);
+        s.last[1 + comp] = (uint8_t)(csum ? csum - 1 : 0);
+        s.csbf_c[comp] = (uint8_t)cm;
+    }
+    return s;
+}
+
 struct SplitResult {
     int sse_full;
     int sse[3];
@@ -577,39 +638,65 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     uint32_t pred_px = 0;   // the lane's 4 luma prediction samples (residual drop)
     int dcp[2] = {0, 0};    // sum (src - pred)^2 of the lane's chroma samples in the display area
     if (valid) {
-        mvx = mbs[i].mvx;
-        mvy = mbs[i].mvy;
-        // luma: 4 samples per lane from the edge-padded reference (|mv| stays inside the pad)
+        // the CU's vector is wave-uniform: scalar registers, so the filter taps are scalar too
+        mvx = __builtin_amdgcn_readfirstlane(mbs[i].mvx);
+        mvy = __builtin_amdgcn_readfirstlane(mbs[i].mvy);
+        // luma: 4 samples per lane from the edge-padded reference (|mv| stays inside the pad),
+        // separable: each of the (up to 8) reference rows is loaded once (11 bytes) and filtered
+        // horizontally for all 4 samples before the vertical taps
         const int r = lane >> 2, cb = (lane & 3) * 4;
         const uint8_t* F = fs->hp_f;
         const int P = fs->hp_pitch;
         const int fx = mvx & 3, fy = mvy & 3;
         const int xi = x0 + cb + (mvx >> 2), yi = y0 + r + (mvy >> 2);
-        for (int j = 0; j < 4; ++j) {
-            int v;
-            if (!fx && !fy) {
-                v = F[yi * P + xi + j] << 6;
-            } else if (!fy) {
-                v = 0;
+        int vv[4];
+        if (!fx && !fy) {
+            const uint8_t* row = F + yi * P + xi;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v += kLumaTap[fx][k] * F[yi * P + xi + j + k - 3];
-            } else if (!fx) {
-                v = 0;
+            for (int j = 0; j < 4; ++j) vv[j] = row[j] << 6;
+        } else if (!fy) {
+            const uint8_t* row = F + yi * P + xi - 3;
+            int px[11];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v += kLumaTap[fy][k] * F[(yi + k - 3) * P + xi + j];
-            } else {
-                int s = 0;
+            for (int q = 0; q < 11; ++q) px[q] = row[q];
 #pragma unroll
-                for (int n = 0; n < 8; ++n) {
-                    int h = 0;
-                    const uint8_t* row = F + (yi + n - 3) * P + xi + j - 3;
+            for (int j = 0; j < 4; ++j) {
+                int v = 0;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) h += kLumaTap[fx][k] * row[k];
-                    s += kLumaTap[fy][n] * h;
-                }
-                v = s >> 6;
+                for (int k = 0; k < 8; ++k) v += kLumaTap[fx][k] * px[j + k];
+                vv[j] = v;
             }
-            const int p = clip255((v + 32) >> 6);
+        } else if (!fx) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vv[j] = 0;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const uint8_t* row = F + (yi + n - 3) * P + xi;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) vv[j] += kLumaTap[fy][n] * row[j];
+            }
+        } else {
+            int sv[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const uint8_t* row = F + (yi + n - 3) * P + xi - 3;
+                int px[11];
+#pragma unroll
+                for (int q = 0; q < 11; ++q) px[q] = row[q];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int h = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) h += kLumaTap[fx][k] * px[j + k];
+                    sv[j] += kLumaTap[fy][n] * h;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vv[j] = sv[j] >> 6;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = clip255((vv[j] + 32) >> 6);
             const int d = (int)src_y[(size_t)(y0 + r) * g.pitch + x0 + cb + j] - p;
             t.pred[r * 16 + cb + j] = (uint8_t)p;
             t.res[r * 16 + cb + j] = (int16_t)d;
@@ -690,6 +777,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         part[1][wave] = valid ? (unsigned long long)(changing ? dcp_u : (split ? sse2u : r.sse[1])) : 0ull;
         part[2][wave] = valid ? (unsigned long long)(changing ? dcp_v : (split ? sse2v : r.sse[2])) : 0ull;
     }
+    SplitSummary ss = {};
+    if (split) ss = split_summary_wave(lv2[wave], lane);  // wave-uniform branch
     if (valid && lane == 0) {
         CuInfo c;
         c.type = kCuAmvp;
@@ -702,7 +791,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         fill_cu(c, r);
         if (try_split) {
             c.tu_split = split ? 2 : 1;
-            if (split) cu_summarise(c, lv2[wave]);
+            if (split) ss.apply(c);
         }
         if (drop) {  // no residual left (chroma was dropped before coding): cu_summarise of zeros
             c.tu_split = try_split ? 1 : 0;
@@ -1475,11 +1564,15 @@ __device__ __forceinline__ void sao_acc(int* e, int d, uint32_t cats) {
 __device__ __forceinline__ int sao_reduce16(int* v, int lane) {
 #pragma unroll
     for (int h = 8, bit = 32; h >= 1; h >>= 1, bit >>= 1) {
-        const bool hi = (lane & bit) != 0;
+        // an opaque all-ones/zero mask: a plain `hi ? v[j] : v[h + j]` is folded into a
+        // dynamically indexed v[] (16-way compare/select chains, ~2,700 VALU per wave)
+        int m = (lane & bit) != 0 ? -1 : 0;
+        asm volatile("" : "+v"(m));
 #pragma unroll
         for (int j = 0; j < h; ++j) {
-            const int send = hi ? v[j] : v[h + j];
-            const int keep = hi ? v[h + j] : v[j];
+            const int a = v[j], b = v[h + j];
+            const int send = (a & m) | (b & ~m);
+            const int keep = (b & m) | (a & ~m);
             v[j] = keep + __shfl_xor(send, bit, 64);
         }
     }
