@@ -79,6 +79,7 @@ struct alignas(16) Mats {
     int16_t t4[16];
     int16_t tt16[256];  // transposed: tt16[y * 16 + k] = t16[k * 16 + y] (inverse stages)
     int16_t tt8[64];
+    int16_t tt4[16];
 };
 __device__ __forceinline__ void fill_mats(Mats& m) {
     for (int i = threadIdx.x; i < 256 + 64 + 16; i += blockDim.x) {
@@ -90,6 +91,7 @@ __device__ __forceinline__ void fill_mats(Mats& m) {
             m.tt8[i - 256] = (int16_t)dct_coef(3, (i - 256) & 7, (i - 256) >> 3);
         } else {
             m.t4[i - 320] = (int16_t)dct_coef(2, (i - 320) >> 2, (i - 320) & 3);
+            m.tt4[i - 320] = (int16_t)dct_coef(2, (i - 320) & 3, (i - 320) >> 2);
         }
     }
 }
@@ -103,6 +105,10 @@ __device__ __forceinline__ int dot2acc(uint32_t a, uint32_t b, int c) {
 __device__ __forceinline__ int dot8(const int16_t* a, const int16_t* b) {
     const uint4 x = *reinterpret_cast<const uint4*>(a), y = *reinterpret_cast<const uint4*>(b);
     return dot2acc(x.w, y.w, dot2acc(x.z, y.z, dot2acc(x.y, y.y, dot2acc(x.x, y.x, 0))));
+}
+__device__ __forceinline__ int dot4(const int16_t* a, const int16_t* b) {  // 8-byte aligned rows
+    const uint2 x = *reinterpret_cast<const uint2*>(a), y = *reinterpret_cast<const uint2*>(b);
+    return dot2acc(x.y, y.y, dot2acc(x.x, y.x, 0));
 }
 __device__ __forceinline__ int dot16(const int16_t* a, const int16_t* b) { return dot8(a, b) + dot8(a + 8, b + 8); }
 
@@ -414,21 +420,21 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     const int tk = lane >> 4, lbx = (tk & 1) * 8, lby = (tk >> 1) * 8, lbase = 64 * tk;  // luma TU of the lane
     const int ct = lane >> 3, comp = ct >> 2, ck = ct & 3;                                 // chroma TU of the lane
     const int cbx = (ck & 1) * 4, cby = (ck >> 1) * 4, cbase = 256 + 64 * comp + 16 * ck;
+    // int16 stage views with the layouts of code_tus (aT[k][y], bT[x][k], a16[y][x] per TU)
+    int16_t* aT = reinterpret_cast<int16_t*>(t.a);
+    int16_t* a16 = reinterpret_cast<int16_t*>(t.a);
+    int16_t* bT = reinterpret_cast<int16_t*>(t.b);
     // ---- forward stage 1 (rows)
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = (lane & 15) * 4 + j, y = idx >> 3, k = idx & 7;
-            int s = 0;
-#pragma unroll
-            for (int n = 0; n < 8; ++n) s += M.t8[k * 8 + n] * t.res[(lby + y) * 16 + lbx + n];
-            t.a[lbase + idx] = (s + 2) >> 2;
+            const int s = dot8(M.t8 + k * 8, t.res + (lby + y) * 16 + lbx);
+            aT[lbase + k * 8 + y] = (int16_t)((s + 2) >> 2);
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = (lane & 7) * 2 + j, y = idx >> 2, k = idx & 3;
-            int s = 0;
-#pragma unroll
-            for (int n = 0; n < 4; ++n) s += M.t4[k * 4 + n] * t.res[256 + comp * 64 + (cby + y) * 8 + cbx + n];
-            t.a[cbase + idx] = (s + 1) >> 1;
+            const int s = dot4(M.t4 + k * 4, t.res + 256 + comp * 64 + (cby + y) * 8 + cbx);
+            aT[cbase + k * 4 + y] = (int16_t)((s + 1) >> 1);
         }
     }
     __syncthreads();
@@ -438,17 +444,13 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = (lane & 15) * 4 + j, k2 = idx >> 3, k = idx & 7;
-            int s = 0;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) s += M.t8[k2 * 8 + y] * t.a[lbase + y * 8 + k];
+            const int s = dot8(M.t8 + k2 * 8, aT + lbase + k * 8);
             ll[j] = quant_coef((s + 256) >> 9, qp, 3, false);
             sil[j] = scan_index(3, k, k2);
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = (lane & 7) * 2 + j, k2 = idx >> 2, k = idx & 3;
-            int s = 0;
-#pragma unroll
-            for (int y = 0; y < 4; ++y) s += M.t4[k2 * 4 + y] * t.a[cbase + y * 4 + k];
+            const int s = dot4(M.t4 + k2 * 4, aT + cbase + k * 4);
             lc[j] = quant_coef((s + 128) >> 8, qpc, 2, false);
             sic[j] = scan_index(2, k, k2);
         }
@@ -516,7 +518,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
             const int idx = (lane & 15) * 4 + j, k2 = idx >> 3, k = idx & 7;
             const int l = ll[j];
             lv[lbase + sil[j]] = (int16_t)l;
-            t.b[lbase + k2 * 8 + k] = dequant_coef(l, qp, 3);
+            bT[lbase + k * 8 + k2] = (int16_t)dequant_coef(l, qp, 3);
             if (l) {
                 ++nzl;
                 bl += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
@@ -526,7 +528,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
             const int idx = (lane & 7) * 2 + j, k2 = idx >> 2, k = idx & 3;
             const int l = lc[j];
             lv[cbase + sic[j]] = (int16_t)l;
-            t.b[cbase + k2 * 4 + k] = dequant_coef(l, qpc, 2);
+            bT[cbase + k * 4 + k2] = (int16_t)dequant_coef(l, qpc, 2);
             if (l) {
                 ++nzc;
                 bc += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
@@ -545,17 +547,13 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = (lane & 15) * 4 + j, y = idx >> 3, x = idx & 7;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + y] * t.b[lbase + k * 8 + x];
-            t.a[lbase + idx] = clip16((s + 64) >> 7);
+            const int s = dot8(M.tt8 + y * 8, bT + lbase + x * 8);
+            a16[lbase + idx] = (int16_t)clip16((s + 64) >> 7);
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = (lane & 7) * 2 + j, y = idx >> 2, x = idx & 3;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) s += M.t4[k * 4 + y] * t.b[cbase + k * 4 + x];
-            t.a[cbase + idx] = clip16((s + 64) >> 7);
+            const int s = dot4(M.tt4 + y * 4, bT + cbase + x * 4);
+            a16[cbase + idx] = (int16_t)clip16((s + 64) >> 7);
         }
     }
     __syncthreads();
@@ -564,9 +562,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     if (valid) {
         for (int j = 0; j < 4; ++j) {
             const int idx = (lane & 15) * 4 + j, y = idx >> 3, x = idx & 7;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += M.t8[k * 8 + x] * t.a[lbase + y * 8 + k];
+            const int s = dot8(M.tt8 + x * 8, a16 + lbase + y * 8);
             const int r = nzl ? (s + 2048) >> 12 : 0;
             const int o = (lby + y) * 16 + lbx + x, p = t.pred[o];
             const int v = clip255(p + r), e = p + t.res[o] - v;
@@ -577,9 +573,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
         }
         for (int j = 0; j < 2; ++j) {
             const int idx = (lane & 7) * 2 + j, y = idx >> 2, x = idx & 3;
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) s += M.t4[k * 4 + x] * t.a[cbase + y * 4 + k];
+            const int s = dot4(M.tt4 + x * 4, a16 + cbase + y * 4);
             const int r = nzc ? (s + 2048) >> 12 : 0;
             const int o = 256 + comp * 64 + (cby + y) * 8 + cbx + x, p = t.pred[o];
             const int v = clip255(p + r), e = p + t.res[o] - v;
