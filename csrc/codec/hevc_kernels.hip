@@ -37,17 +37,32 @@ namespace hevc {
 
 namespace {
 
+// Cross-row exchanges without LDS (CDNA4 v_permlane16/32_swap with both operands = v): the
+// swapped pair holds {v, v ^ 16} (resp. {v, v ^ 32}) in some order on every lane, so their
+// sum / max / or is the xor-16 (xor-32) step of a butterfly -- no ds_bpermute round trip.
+__device__ __forceinline__ void xrow16(uint32_t v, uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    a = r[0];
+    b = r[1];
+}
+__device__ __forceinline__ void xrow32(uint32_t v, uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    a = r[0];
+    b = r[1];
+}
 // Wave sum, every lane gets it (called with the whole wave active): quad and row-of-16 sums
-// with DPP (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8), then the four rows with two
-// lane shuffles -- 4 DPP moves + 2 ds_bpermute instead of 6 ds_bpermute round trips.
+// with DPP (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8), then the four rows with the
+// two permlane swaps -- all VALU, no LDS latency on the (often serial) reduction chains.
 __device__ __forceinline__ int wsum(int v) {
     v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
     v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
     v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
     v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
+    uint32_t a, b;
+    xrow16((uint32_t)v, a, b);
+    v = (int)(a + b);
+    xrow32((uint32_t)v, a, b);
+    return (int)(a + b);
 }
 // reductions inside aligned groups of G lanes (G = 8 or 16): every lane gets its group's value
 template <int G>
@@ -60,16 +75,27 @@ __device__ __forceinline__ int gmax(int v) {
     for (int o = G / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return v;
 }
+// wave max / or: the same DPP + permlane butterfly as wsum
 __device__ __forceinline__ int wmax(int v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const int t = __shfl_xor(v, o, 64);
-        v = t > v ? t : v;
-    }
-    return v;
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false));
+    uint32_t a, b;
+    xrow16((uint32_t)v, a, b);
+    v = max((int)a, (int)b);
+    xrow32((uint32_t)v, a, b);
+    return max((int)a, (int)b);
 }
 __device__ __forceinline__ uint32_t wor(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-    return v;
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);
+    v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+    uint32_t a, b;
+    xrow16(v, a, b);
+    xrow32(a | b, a, b);
+    return a | b;
 }
 
 // Transform matrices in LDS (filled once per workgroup).
