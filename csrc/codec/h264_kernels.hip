@@ -81,16 +81,23 @@ struct OrWriter {
     }
 };
 
+// Sum of the four rows of 16 lanes, every lane gets it (whole wave active): v_permlane16_swap
+// and v_permlane32_swap with both operands = v leave {v, v ^ 16} (then {v, v ^ 32}) on every
+// lane, so the pair sum is the xor-16 / xor-32 butterfly step without a ds_bpermute round trip.
+__device__ __forceinline__ uint32_t rows_sum(uint32_t v) {
+    const auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = r16[0] + r16[1];
+    const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return r32[0] + r32[1];
+}
 // Wave sum, every lane gets it (whole wave active): quad and row-of-16 sums with DPP
-// (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8), the four rows with two lane shuffles.
+// (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8), then rows_sum.
 __device__ __forceinline__ int wave_sum(int v) {
     v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
     v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
     v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
     v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
+    return (int)rows_sum((uint32_t)v);
 }
 
 // ------------------------------------------------------------------ half-pel planes
@@ -1069,8 +1076,7 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
                 t = r == 0 ? t : 0u;
                 t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x124, 0xF, 0xF, false);  // lanes l ^ 4, 8, 12
                 t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x128, 0xF, 0xF, false);
-                t += __shfl_xor(t, 16, 64);
-                t += __shfl_xor(t, 32, 64);
+                t = rows_sum(t);
             }
             if (lane == 0) c.c16[m] = ok ? t : kCostInf;
         }
@@ -1093,8 +1099,7 @@ __global__ __launch_bounds__(256) void k_intra_analyze(Geometry g, StateArg sa, 
                 t = (r == 0 && lane < 32) ? t : 0u;
                 t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x124, 0xF, 0xF, false);  // lanes l ^ 4, 8, 12
                 t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x128, 0xF, 0xF, false);
-                t += __shfl_xor(t, 16, 64);
-                t += __shfl_xor(t, 32, 64);
+                t = rows_sum(t);
             }
             if (lane == 0) c.cc[m] = ok ? t : kCostInf;
         }
