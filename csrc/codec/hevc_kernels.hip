@@ -1105,6 +1105,14 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wtot, 
     return before + incl - v;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
 // Scans over per-CU arrays run in tiles of 1024 threads x 4 consecutive CUs (arrays padded with
 // zeros to a whole tile: HevcDeviceBuffers).
 constexpr int kScanTile = 4096;
@@ -1130,24 +1138,25 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     // memory pipeline: 67 us at 4K).  Pass 1: per-tile prefixes and the total.
     // Tile totals by wave reductions and one LDS atomic per wave and tile (no workgroup barrier
     // per tile), then their exclusive prefix.
+    // The per-wave totals of every tile are kept, so pass 2's cost prefix needs only a wave
+    // scan plus the earlier waves' totals (no workgroup barrier per tile).
     __shared__ uint32_t tile_pre[kMaxScanTiles];
-    __shared__ uint32_t tile_sum[kMaxScanTiles];
+    __shared__ uint32_t wave_tot[kMaxScanTiles][16];
     __shared__ uint32_t total_sh;
-    for (int k = tid; k < kMaxScanTiles; k += (int)blockDim.x) tile_sum[k] = 0;
-    __syncthreads();
+    const int wv = tid >> 6, nwv = (int)blockDim.x >> 6;
     int nt = 0;
     for (int base = 0; base < ncu; base += kScanTile, ++nt) {
         const uint4 v = ld4(cost, base + 4 * tid);
         uint32_t w = v.x + v.y + v.z + v.w;
         for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
-        if ((tid & 63) == 0) atomicAdd(&tile_sum[nt], w);
+        if ((tid & 63) == 0) wave_tot[nt][wv] = w;
     }
     __syncthreads();
     if (tid == 0) {
         uint32_t run = 0;
         for (int t = 0; t < nt; ++t) {
             tile_pre[t] = run;
-            run += tile_sum[t];
+            for (int w = 0; w < nwv; ++w) run += wave_tot[t][w];
         }
         total_sh = run;
     }
@@ -1164,8 +1173,10 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
         const int i0 = base + 4 * tid;
         const uint4 v = ld4(cost, i0);
         const uint32_t c4[4] = {v.x, v.y, v.z, v.w};
-        uint32_t tt;
-        const uint32_t pre0 = tile_pre[t] + block_excl_scan(v.x + v.y + v.z + v.w, wtot, &tt);
+        const uint32_t sum4 = v.x + v.y + v.z + v.w;
+        uint32_t before = 0;
+        for (int w = 0; w < wv; ++w) before += wave_tot[t][w];
+        const uint32_t pre0 = tile_pre[t] + before + wave_incl_scan(sum4) - sum4;
         int ids[4];
         uint32_t nst = 0;
         if (i0 < ncu) {
