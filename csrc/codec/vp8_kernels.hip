@@ -30,10 +30,18 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 constexpr unsigned kSpinLimit = 1u << 22;
 
+// Wave sum, every lane gets it (whole wave active): DPP within rows of 16 (quad_perm
+// [1,0,3,2], [2,3,0,1], row_ror 4, row_ror 8), then v_permlane16/32_swap with both operands = v,
+// whose pair holds {v, v ^ 16} / {v, v ^ 32} -- no ds_bpermute round trips.
 __device__ __forceinline__ int wsum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
+    const auto r16 = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+    const uint32_t u = r16[0] + r16[1];
+    const auto r32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return (int)(r32[0] + r32[1]);
 }
 
 // dead-zone quantiser of vp8_core.h quantize(): (3|c| + q) / (3q) as a multiply-high
