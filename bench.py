@@ -41,18 +41,18 @@ CODEC_LABEL = {
     "vp8": ("VP8", "mxvp8enc", "VP8 (RFC 6386) key + inter frames"),
 }
 
-def density_probe(N, cfg, fps: int, ks=(8, 16, 32, 48, 64, 96, 128), seconds: float = 1.0) -> dict:
-    """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1), every
-    1/fps slot each submits one frame and collects it; K is sustained if no slot overran
-    (all K frames of every slot encoded before the next slot starts) over `seconds`.  K grows
-    until a slot is missed; the whole serving path per session (render, CSC, encode, bitstream
-    to host) runs, but a single host thread drives all sessions."""
-    import time as _t
+def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: float = 1.0,
+                  threads: int = 8) -> dict:
+    """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1) driven by
+    `threads` host threads (N.run_sessions_paced: every 1/fps slot each thread submits one frame
+    per session it owns, then collects them); K is sustained if no slot overran (every frame of
+    every session encoded before the next slot starts) over `seconds`.  K doubles from k0 until a
+    K fails, then bisects between the last sustained and the first failing K (to within 1/16), so
+    `sustained` is a measured limit -- the first failing K minus the resolution -- not a list cap.
+    The whole serving path per session (render, CSC, encode, bitstream to host) runs."""
+    out = {"fps": fps, "seconds": seconds, "threads": threads, "tried": {}}
 
-    period = 1.0 / fps
-    out = {"fps": fps, "seconds": seconds, "tried": {}}
-    best = 0
-    for K in ks:
+    def trial(K: int) -> bool:
         sess = []
         try:
             for _ in range(K):
@@ -64,33 +64,36 @@ def density_probe(N, cfg, fps: int, ks=(8, 16, 32, 48, 64, 96, 128), seconds: fl
                 sess.append(N.Session(c))
             for s in sess:  # warm-up: first IDR + rate-control probe
                 s.step(False)
-            n = max(1, int(seconds * fps))
-            late, lat = 0, []
-            t0 = _t.perf_counter()
-            for f in range(n):
-                tick = t0 + f * period
-                d = tick - _t.perf_counter()
-                if d > 0:
-                    _t.sleep(d)
-                for s in sess:
-                    s.submit(False)
-                for s in sess:
-                    r = s.collect()
-                    lat.append((r.t_encoded_us - r.t_capture_us) / 1000.0)
-                if _t.perf_counter() > tick + period:
-                    late += 1
-            lat.sort()
-            out["tried"][K] = {"late_slots": late, "p50_ms": round(lat[len(lat) // 2], 3),
+            st = N.run_sessions_paced(sess, fps, seconds, min(threads, K))
+            lat = sorted(st.lat_ms)
+            out["tried"][K] = {"late_slots": st.late_slots, "slots": st.slots,
+                               "p50_ms": round(lat[len(lat) // 2], 3),
                                "p99_ms": round(lat[int(0.99 * (len(lat) - 1))], 3)}
-        except RuntimeError as e:  # out of device memory etc.: the previous K stands
+            return st.late_slots == 0
+        except RuntimeError as e:  # out of device memory etc.: counts as a failing K
             out["tried"][K] = {"error": str(e)[:120]}
-            break
+            return False
         finally:
             del sess
-        if late:
+
+    good, bad = 0, None
+    K = k0
+    while K <= k_max:
+        if trial(K):
+            good = K
+            K *= 2
+        else:
+            bad = K
             break
-        best = K
-    out["sustained"] = best
+    if bad is not None:
+        while bad - good > max(1, good // 16):
+            mid = (good + bad) // 2
+            if trial(mid):
+                good = mid
+            else:
+                bad = mid
+    out["sustained"] = good
+    out["first_failing"] = bad
     return out
 
 
@@ -126,16 +129,18 @@ def main() -> None:
                     help="in-loop deblocking filter 0/1 (default: the encoder's)")
     ap.add_argument("--intra-in-p", type=int, default=None,
                     help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
-    ap.add_argument("--depth", type=int, default=2,
+    ap.add_argument("--depth", type=int, default=3,
                     help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1; "
-                         "1: strictly one frame at a time, lowest back-to-back latency)")
+                         "3: also the next frame's launches stay queued while the host collects, so the host "
+                         "turnaround overlaps GPU work; 1: strictly one frame at a time, lowest back-to-back latency)")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
                     help="concurrent sessions per GPU (density): each has its own HIP stream and one frame in flight")
     ap.add_argument("--density-probe", type=int, default=1,
                     help="after the timed run, measure how many paced 1080p60 sessions this GPU sustains in this "
-                         "process (doubling K until a 60 fps slot is missed); reported, never part of `value`")
+                         "process (doubling K until a 60 fps slot is missed, then bisecting); reported, never part "
+                         "of `value`")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse the "
                          "multi-rank plumbing with several ranks on one GPU)")
@@ -309,7 +314,8 @@ def main() -> None:
             "mean_psnr_y_db": round(statistics.mean(psnrs), 2),
             "mean_psnr_y_db_noise_masked": round(statistics.mean(psnrs_m), 2),
             # measured, not extrapolated: K paced sessions (one HIP stream each, depth 1) on this
-            # GPU from one host thread, every frame of every session encoded within its 1/fps slot
+            # GPU from `threads` host threads, every frame of every session encoded within its 1/fps
+            # slot; K found by doubling then bisecting up to the first failing K
             "sessions_per_gpu_at_60fps_measured": density["sustained"] if density else None,
             "density_probe": density,
             "dtype": "uint8 video (8-bit 4:2:0), " + CODEC_LABEL[args.codec][2],

@@ -647,6 +647,18 @@ PYBIND11_MODULE(_native, m) {
         },
         py::arg("sessions"), py::arg("n_frames"), py::arg("depth") = 2,
         "K sessions driven concurrently, one host thread each; returns [[FrameResult]] per session");
+    py::class_<PacedStats>(m, "PacedStats")
+        .def_readonly("slots", &PacedStats::slots)
+        .def_readonly("late_slots", &PacedStats::late_slots)
+        .def_readonly("lat_ms", &PacedStats::lat_ms);
+    m.def(
+        "run_sessions_paced",
+        [](std::vector<Session*> ss, int fps, double seconds, int threads) {
+            py::gil_scoped_release rel;
+            return run_sessions_paced(ss, fps, seconds, threads);
+        },
+        py::arg("sessions"), py::arg("fps"), py::arg("seconds"), py::arg("threads") = 8,
+        "K sessions paced at fps for `seconds` by `threads` host threads (one frame in flight each)");
     py::class_<Session>(m, "Session")
         .def(py::init<const SessionConfig&>())
         .def(

@@ -266,15 +266,17 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.db_glq, sizeof(uint32_t) * 2 * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.db_gprog, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h));
     HIP_CHECK(hipMemsetAsync(b.db_gprog, 0, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h, stream_));
+    HIP_CHECK(hipMalloc(&b.pack_done, sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(b.pack_done, 0, sizeof(uint32_t), stream_));
     HIP_CHECK(hipHostMalloc(&b.db_err, sizeof(int), hipHostMallocMapped));
     *b.db_err = 0;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
     std::memset(sl.host_out, 0, kOutPayloadOffset);
-    HIP_CHECK(hipEventCreate(&sl.start));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.start, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&sl.deblock_done, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreate(&sl.done));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
 }
 
 void GpuH264Encoder::free_slot(FrameSlot& sl) {
@@ -282,7 +284,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.row_agg,
                     (void*)b.row_sse, (void*)b.coded_info, (void*)b.slice_info,
                     (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit,
-                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.db_glq, (void*)b.db_gprog})
+                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.db_glq, (void*)b.db_gprog, (void*)b.pack_done})
         if (p) (void)hipFree(p);
     if (b.db_err) (void)hipHostFree(b.db_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
@@ -294,7 +296,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
 GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     : cfg_(cfg), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
-        throw std::invalid_argument("pipeline_depth must be 1 or 2");
+        throw std::invalid_argument("pipeline_depth must be 1, 2 or 3");
     depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;
     geom_.height = cfg.height;
@@ -332,6 +334,7 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
+    clock_khz_ = device_clock_khz();
     if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
@@ -485,7 +488,9 @@ void GpuH264Encoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint
     enqueue_analysis_kernels(idr, src_y, src_uv, false);
 }
 
-void GpuH264Encoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
+// GPU time comes from the device clock stamps in OutHeader (t_start by the first kernel, t_end by
+// k_pack): no event between the kernels of a frame
+void GpuH264Encoder::record_start() {}
 
 void GpuH264Encoder::record_done() {
     FrameSlot& sl = slots_[prep_slot_];
@@ -511,9 +516,9 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     FrameSlot& sl = slots_[s];
     wait_event(sl.done);
     last_done_ = sl.done;
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, sl.start, sl.done);
     const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);
+    last_t_end_ = hdr.t_end;
+    const double ms = hdr.t_end > hdr.t_start ? (double)(hdr.t_end - hdr.t_start) / clock_khz_ : 0.0;
     if (*sl.buf.db_err) {  // a deblocking hand-off spin timed out: the reference is unreliable
         *sl.buf.db_err = 0;
         common_.end_frame(0, sl.idr);

@@ -62,7 +62,9 @@ struct EncoderConfig {
     // (FrameStats::sse_masked; mask_x1 <= mask_x0 = no mask)
     int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;
     int pipeline_depth = 1;   // GPU frames in flight: 2 overlaps frame n's entropy coding with
-                              // frame n+1's analysis on a second HIP stream (rate control lags a frame)
+                              // frame n+1's analysis on a second HIP stream (rate control lags a frame);
+                              // 3 also keeps the next frame's launches queued while the host collects
+                              // frame n (the host turnaround then overlaps GPU work; H.264 / HEVC)
 };
 
 struct FrameStats {
@@ -171,7 +173,7 @@ class GpuH264Encoder final : public VideoEncoder {
    public:
     const char* codec() const override { return "h264"; }
     EncoderCommon& rc() override { return common_; }
-    static constexpr int kMaxInFlight = 2;
+    static constexpr int kMaxInFlight = 3;
     GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream);
     ~GpuH264Encoder();
     GpuH264Encoder(const GpuH264Encoder&) = delete;
@@ -214,6 +216,8 @@ class GpuH264Encoder final : public VideoEncoder {
     void link_entropy() override;
     // Completion event of the last collected frame.
     hipEvent_t done_event() const override { return last_done_; }
+    bool device_clock() const override { return true; }
+    uint64_t last_t_end() const override { return last_t_end_; }
     hipEvent_t pending_done_event() const override { return inflight_.empty() ? last_done_ : slots_[inflight_.front()].done; }
     // publish: the first kernel takes the frame state by value and stores it (eager launches);
     // otherwise the kernels read the device copy uploaded by enqueue_body's memcpy node.
@@ -244,6 +248,8 @@ class GpuH264Encoder final : public VideoEncoder {
     int next_slot_ = 0, prep_slot_ = 0;
     std::deque<int> inflight_;
     hipEvent_t last_done_ = nullptr;
+    uint64_t last_t_end_ = 0;   // device clock at the end of the last collected frame
+    double clock_khz_ = 100000;  // device wall-clock rate
     uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};  // padded F/H/V/J reference planes
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};

@@ -115,6 +115,11 @@ struct OutHeader {
     uint32_t pad;
     uint64_t sse[3];       // source vs reconstruction squared error (Y, U, V)
     uint64_t sse_masked;   // Y outside the mask macroblocks (FrameState::mask_*)
+    // device wall clock (hipDeviceAttributeWallClockRate): start of the frame's first encoder kernel,
+    // end of its last (k_pack) -- per-frame GPU time without timing events on the streams (an
+    // event record between kernels cost ~5 us of idle GPU each: profiles/r04_h264)
+    uint64_t t_start;
+    uint64_t t_end;
 };
 static_assert(sizeof(OutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
@@ -158,6 +163,7 @@ struct DeviceBuffers {
     uint32_t* db_glq;       // [2][mb_h][mb_w] their QP
     uint32_t* db_gprog;     // [2][mb_h] band-boundary progress words (epoch << 12 | count)
     int* db_err;            // mapped host word: nonzero if a deblocking spin timed out
+    uint32_t* pack_done;    // [1] k_pack workgroups finished (the last one stamps t_end and resets it)
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.

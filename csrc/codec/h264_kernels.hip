@@ -162,9 +162,11 @@ struct StateArg {
     FrameState v;
     FrameState* dst;
     int publish;
+    uint64_t* t_start;  // OutHeader::t_start of the frame (device), or nullptr
 };
 __device__ __forceinline__ void publish_state(const StateArg& a) {
     static_assert(sizeof(FrameState) % 4 == 0, "FrameState is copied as dwords");
+    if (a.t_start && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.t_start = wall_clock64();
     if (a.publish && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < sizeof(FrameState) / 4)
         reinterpret_cast<uint32_t*>(a.dst)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&a.v)[threadIdx.x];
 }
@@ -2405,13 +2407,33 @@ __device__ __forceinline__ uint32_t slot_get(const uint32_t* slot, uint32_t b, i
 // trailer bits that overlap it, and lane 0 of the quad gathers the four words with lane
 // shuffles and writes them with one 16-byte store straight into pinned host memory.
 // No atomics, no zero-fill pass, short dependent-load chains (latency-bound kernel).
+__device__ void pack_body(const Geometry& g, const FrameState* __restrict__ fs, const uint32_t* __restrict__ slot,
+                          const uint4* __restrict__ coded_info, const uint32_t* __restrict__ slice_info,
+                          const OutHeader& h, uint8_t* __restrict__ host, const uint32_t* __restrict__ quad_unit);
+
 __global__ __launch_bounds__(256) void k_pack(Geometry g, const FrameState* __restrict__ fs,
                                               const uint32_t* __restrict__ slot,
                                               const uint4* __restrict__ coded_info,
                                               const uint32_t* __restrict__ slice_info,
                                               const OutHeader* __restrict__ hdr, uint8_t* __restrict__ host,
-                                              const uint32_t* __restrict__ quad_unit) {
+                                              const uint32_t* __restrict__ quad_unit, uint32_t* __restrict__ done) {
     const OutHeader h = *hdr;
+    pack_body(g, fs, slot, coded_info, slice_info, h, host, quad_unit);
+    // the last workgroup to finish stamps the frame's end time into the host header (the host
+    // reads it after the frame's completion event) and re-arms the counter for the next frame
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            reinterpret_cast<OutHeader*>(host)->t_end = wall_clock64();
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+__device__ void pack_body(const Geometry& g, const FrameState* __restrict__ fs, const uint32_t* __restrict__ slot,
+                          const uint4* __restrict__ coded_info, const uint32_t* __restrict__ slice_info,
+                          const OutHeader& h, uint8_t* __restrict__ host, const uint32_t* __restrict__ quad_unit) {
     const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * 256;
     if (gid == 0) *reinterpret_cast<OutHeader*>(host) = h;
@@ -2506,6 +2528,7 @@ void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const plane
     if (publish) sa.v = *publish;
     sa.dst = b.fs;
     sa.publish = publish ? 1 : 0;
+    sa.t_start = b.out_hdr ? &b.out_hdr->t_start : nullptr;
     hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, sa, planes[0], planes[1], planes[2], planes[3],
                        hp_pitch);
 }
@@ -2523,19 +2546,21 @@ void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_
 }
 
 static void launch_analyze(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                           hipStream_t stream, const FrameState* publish) {
+                           hipStream_t stream, const FrameState* publish, bool first) {
     const int nmb = g.mb_w * g.mb_h;
     StateArg sa{};
     if (publish) sa.v = *publish;
     sa.dst = b.fs;
     sa.publish = publish ? 1 : 0;
+    // the first kernel of an I picture stamps the start; in a P picture k_hpel did
+    sa.t_start = (b.out_hdr && first) ? &b.out_hdr->t_start : nullptr;
     hipLaunchKernelGGL(k_intra_analyze, dim3((nmb + 3) / 4), dim3(256), 0, stream, g, sa, src_y, src_uv, b.mb,
                        b.wave_prog, b.intra_gain, b.intra_cand);
 }
 
 void launch_intra_in_p(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                        hipStream_t stream) {
-    launch_analyze(g, b, src_y, src_uv, stream, nullptr);
+    launch_analyze(g, b, src_y, src_uv, stream, nullptr, false);
     // a fixed grid over k_intra_analyze's candidate list (a few percent of the MBs)
     hipLaunchKernelGGL(k_intra_p, dim3(256), dim3(128), 0, stream, g, b.fs, src_y, src_uv, b.mb, b.coef,
                        b.intra_gain, b.mb_sse, b.wave_prog, b.intra_cand);
@@ -2543,7 +2568,7 @@ void launch_intra_in_p(const Geometry& g, const DeviceBuffers& b, const uint8_t*
 
 void launch_intra(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream, const FrameState* publish) {
-    launch_analyze(g, b, src_y, src_uv, stream, publish);
+    launch_analyze(g, b, src_y, src_uv, stream, publish, true);
     // one workgroup per (slice, plane), one wave per slice row; LDS line buffers of the rows
     const int rows = idr_slice_rows(g.mb_h), slices = (g.mb_h + rows - 1) / rows;
     const size_t lds = (size_t)rows * g.coded_w;
@@ -2581,7 +2606,7 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
     hipLaunchKernelGGL(k_scan_out, dim3(g.mb_h), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.row_agg,
                        b.row_sse, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr, b.quad_unit);
     hipLaunchKernelGGL(k_pack, dim3(256), dim3(256), 0, stream, g, b.fs, b.slot, b.coded_info, b.slice_info,
-                       b.out_hdr, host_out, b.quad_unit);
+                       b.out_hdr, host_out, b.quad_unit, b.pack_done);
 }
 
 }  // namespace h264

@@ -76,7 +76,7 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
 GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     : cfg_(cfg), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
-        throw std::invalid_argument("pipeline_depth must be 1 or 2");
+        throw std::invalid_argument("pipeline_depth must be 1, 2 or 3");
     if (common_.slice_rows() > kMaxSliceRows) throw std::invalid_argument("hevc: too many CTU rows per slice");
     depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;
@@ -221,8 +221,7 @@ void GpuHevcEncoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint
     HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(HevcFrameState), hipMemcpyHostToDevice, stream_));
     if (idr) {
         if (cfg_.aq >= 3)  // the next P picture's temporal classes compare against this source
-            HIP_CHECK(hipMemcpyAsync(sl.fs_host->save_src, src_y, (size_t)geom_.pitch * geom_.coded_h,
-                                     hipMemcpyDeviceToDevice, stream_));
+            launch_hevc_save_src(geom_, sl.buf, src_y, stream_);
         launch_hevc_intra(geom_, sl.buf, common_.slice_rows(), common_.num_slices(), src_y, src_uv, stream_);
     } else {
         HIP_CHECK(hipMemcpyAsync(sl.buf.me.fs, sl.me_fs_host, sizeof(h264::FrameState), hipMemcpyHostToDevice, stream_));

@@ -179,6 +179,8 @@ struct HevcDeviceBuffers {
     unsigned long long* sse_tot;  // [4] k_hevc_sao distortion totals
 };
 
+// IDR + temporal AQ: the source luma into fs->save_src (pointer read on the device)
+void launch_hevc_save_src(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, hipStream_t s);
 void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                        hipStream_t s);
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
@@ -194,7 +196,7 @@ class GpuHevcEncoder final : public VideoEncoder {
    public:
     const char* codec() const override { return "hevc"; }
     h264::EncoderCommon& rc() override { return common_.rc(); }
-    static constexpr int kMaxInFlight = 2;
+    static constexpr int kMaxInFlight = 3;
     GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream);
     ~GpuHevcEncoder();
     GpuHevcEncoder(const GpuHevcEncoder&) = delete;

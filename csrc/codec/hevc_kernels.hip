@@ -1922,7 +1922,22 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
     }
 }
 
+// IDR pictures with temporal AQ: copy the source luma to save_src.  The destination is read from
+// the device copy of the frame state, so a captured graph stays valid while the two source
+// buffers alternate (a memcpy node would freeze the pointer of the frame it was captured for).
+__global__ __launch_bounds__(256) void k_hevc_save_src(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                        const uint8_t* __restrict__ src_y) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // 16-byte chunk
+    const size_t n = (size_t)g.pitch * g.coded_h / 16;
+    if (i < n) reinterpret_cast<uint4*>(fs->save_src)[i] = reinterpret_cast<const uint4*>(src_y)[i];
+}
+
 }  // namespace
+
+void launch_hevc_save_src(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, hipStream_t s) {
+    const size_t n = (size_t)g.pitch * g.coded_h / 16;  // pitch is a multiple of 256
+    hipLaunchKernelGGL(k_hevc_save_src, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, b.fs, src_y);
+}
 
 void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                        hipStream_t s) {

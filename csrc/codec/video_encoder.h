@@ -29,6 +29,10 @@ class VideoEncoder {
     virtual const uint8_t* recon_y() const = 0;
     virtual const uint8_t* recon_uv() const = 0;
     virtual hipEvent_t done_event() const = 0;
+    // device_clock(): the encoder stamps its frames with the device wall clock (no timing events);
+    // last_t_end() is the end stamp of the last collected frame (device_clock_khz() ticks per ms)
+    virtual bool device_clock() const { return false; }
+    virtual uint64_t last_t_end() const { return 0; }
     // completion event of the oldest frame in flight (the next collect() waits for it)
     virtual hipEvent_t pending_done_event() const = 0;
     // split form for hipGraph capture (pipeline depth 1: enqueue_body on one stream)

@@ -41,6 +41,14 @@ inline void ensure_func_attr(const void* fn, hipFuncAttribute attr, int value) {
 namespace mx {
 // Wait for a frame's completion event.  MXDESK_WAIT=spin polls hipEventQuery (the collecting
 // thread owns a core: wake-up within ~1 us of the GPU finishing); default hipEventSynchronize.
+// Rate of the device wall clock (wall_clock64() / s_memrealtime) in kHz = ticks per ms.
+inline double device_clock_khz() {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        khz <= 0)
+        return 100000.0;  // 100 MHz on CDNA
+    return (double)khz;
+}
 inline void wait_event(hipEvent_t e) {
     static const bool spin = [] {
         const char* v = std::getenv("MXDESK_WAIT");

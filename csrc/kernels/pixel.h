@@ -20,6 +20,7 @@ struct SynthParams {
     int wall_w, wall_h;     // full desktop size (== width/height for a single session)
     int noise;              // 1 = animated-noise panel on
     int cursor_x, cursor_y; // remote cursor position (-1 = hidden)
+    uint64_t* ts = nullptr; // if set: device wall clock at the render's start (frame GPU time)
 };
 
 // Barcode geometry: 64 bits (frame_id, timestamp_us), 8x8-pixel cells, two rows of 32
@@ -37,8 +38,9 @@ void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int
 
 // BGRx -> NV12 (BT.709 limited range), padding the output to (coded_w, coded_h) by edge
 // replication.  Output Y plane pitch = UV plane pitch = out_pitch.
+// ts: if set, the device wall clock at the kernel's start is stored there (frame GPU time).
 void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_t* y, uint8_t* uv, int out_pitch,
-                         int coded_w, int coded_h, hipStream_t stream);
+                         int coded_w, int coded_h, hipStream_t stream, uint64_t* ts = nullptr);
 
 // Fused separable Lanczos-3 resample (in_w x in_h -> out_w x out_h) + BT.709 CSC into
 // NV12, LDS-tiled.  `weights` from make_lanczos_tables (device memory).
@@ -76,7 +78,8 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
 // Copies the blob to `dev` (hipMalloc'ed here; caller frees) and fills `mf`.
 void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf);
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
-                          uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream);
+                          uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream,
+                          uint64_t* ts = nullptr);
 
 // Luma squared error between two planes over [0,w) x [0,h) excluding the rectangle
 // [mx0,mx1) x [my0,my1) (quality report with a panel masked out), in one dispatch: `part`

@@ -33,6 +33,11 @@ __device__ __forceinline__ uint32_t hash3(uint32_t x, uint32_t y, uint32_t z) {
     return h;
 }
 
+// Frame start stamp: the first thread of the grid stores the device wall clock.
+__device__ __forceinline__ void stamp_start(uint64_t* ts) {
+    if (ts && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) *ts = wall_clock64();
+}
+
 __device__ __forceinline__ uint32_t bgrx(int r, int g, int b) {
     r = r < 0 ? 0 : (r > 255 ? 255 : r);
     g = g < 0 ? 0 : (g > 255 ? 255 : g);
@@ -231,6 +236,7 @@ __device__ __attribute__((noinline)) uint32_t static_px(int gx, int gy, const Sy
 // bg: the session's static-layer cache (same size / pitch / origin), or nullptr.
 __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const SynthParams& p,
                                            const uint8_t* __restrict__ bg) {
+    stamp_start(p.ts);
     const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     if (y >= p.height || x4 >= p.width) return;
@@ -276,7 +282,8 @@ __device__ __forceinline__ int v709(int r, int g, int b) { return ((112 * r - 10
 
 __global__ __launch_bounds__(256) void k_bgrx_to_nv12(const uint8_t* __restrict__ in, int in_pitch, int w, int h,
                                                       uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
-                                                      int out_pitch, int coded_w, int coded_h) {
+                                                      int out_pitch, int coded_w, int coded_h, uint64_t* ts) {
+    stamp_start(ts);
     const int bx = blockIdx.x * blockDim.x + threadIdx.x;  // 4-pixel column group
     const int by = blockIdx.y * blockDim.y + threadIdx.y;  // 2-row group
     const int x = bx * 4, y = by * 2;
@@ -336,7 +343,8 @@ constexpr float kHFix = 16.f;  // horizontal-pass fixed-point scale
 __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict__ in, int in_pitch, int in_w,
                                                        int in_h, LanczosTables t, uint8_t* __restrict__ yp,
                                                        uint8_t* __restrict__ uvp, int out_pitch, int coded_w,
-                                                       int coded_h, int max_nc, int max_nr, int vec) {
+                                                       int coded_h, int max_nc, int max_nr, int vec, uint64_t* ts) {
+    stamp_start(ts);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int ox0 = blockIdx.x * kTileW, oy0 = blockIdx.y * kTileH;
     const int tid = threadIdx.x;
@@ -606,7 +614,8 @@ __device__ __forceinline__ void mf_main(char* __restrict__ buf0, char* __restric
 
 __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
                                                     ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
-                                                    int out_pitch, int coded_w, int coded_h) {
+                                                    int out_pitch, int coded_w, int coded_h, uint64_t* ts) {
+    stamp_start(ts);
     // LDS: two 32-row footprint buffers [32][lds_cols] BGRx (see mf_main)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
@@ -817,11 +826,11 @@ void launch_synth_dev(uint8_t* bgrx, const SynthParams* d_params, int width, int
 }
 
 void launch_bgrx_to_nv12(const uint8_t* bgrx, int in_pitch, int w, int h, uint8_t* y, uint8_t* uv, int out_pitch,
-                         int coded_w, int coded_h, hipStream_t stream) {
+                         int coded_w, int coded_h, hipStream_t stream, uint64_t* ts) {
     dim3 block(64, 4);
     dim3 grid((coded_w / 4 + 63) / 64, (coded_h / 2 + 3) / 4);
     hipLaunchKernelGGL(k_bgrx_to_nv12, grid, block, 0, stream, bgrx, in_pitch, w, h, y, uv, out_pitch, coded_w,
-                       coded_h);
+                       coded_h, ts);
 }
 
 bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, int coded_h,
@@ -931,7 +940,7 @@ void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf) {
 }
 
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
-                          uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream) {
+                          uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream, uint64_t* ts) {
     if (t.mf.gx && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 && in_w >= 4) {
         const size_t lds = (size_t)2 * 32 * t.mf.lds_cols * 4;
         if (lds > 64 * 1024) {
@@ -940,7 +949,7 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
         }
         dim3 grid((coded_w + 63) / 64, (coded_h + 31) / 32);
         hipLaunchKernelGGL(k_scale_mfma, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv,
-                           out_pitch, coded_w, coded_h);
+                           out_pitch, coded_w, coded_h, ts);
         return;
     }
     // worst-case footprint of a tile: scale * tile + taps
@@ -959,7 +968,7 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     }
     dim3 grid((coded_w + kTileW - 1) / kTileW, (coded_h + kTileH - 1) / kTileH);
     hipLaunchKernelGGL(k_scale_to_nv12, grid, dim3(256), lds, stream, bgrx, in_pitch, in_w, in_h, t, y, uv, out_pitch,
-                       coded_w, coded_h, max_nc, max_nr, vec);
+                       coded_w, coded_h, max_nc, max_nr, vec, ts);
 }
 
 void launch_composite(const uint8_t* tile, int tile_pitch, int tw, int th, uint8_t* dst, int dst_pitch, int dx, int dy,

@@ -101,6 +101,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
     HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));
     depth_ = enc_->depth();
+    if (depth_ > kMaxDepth) throw std::invalid_argument("Session: encoder pipeline depth above kMaxDepth");
     if (depth_ > 1 && cfg_.use_graph && !enc_->supports_split())
         throw std::invalid_argument("hipGraph replay with pipeline_depth 2 needs an encoder with the split form");
     if (depth_ >= cfg_.pool_slots) throw std::invalid_argument("pool_slots must exceed pipeline_depth");
@@ -138,17 +139,21 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
                                                        eg.coded_w, eg.coded_h, sx, wx, tx, sy, wy, ty, fr))
             pix::upload_scale_frags(fr, &lt_mf_mem_, lt_.mf);
     }
-    for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
+    for (int k = 0; k < kMaxDepth; ++k) HIP_CHECK(hipEventCreate(&ev_start_[k]));
+    devclk_ = enc_->device_clock();
+    clock_khz_ = device_clock_khz();
+    HIP_CHECK(hipHostMalloc(&ts_, sizeof(uint64_t) * cfg_.pool_slots, hipHostMallocMapped));
+    std::memset(ts_, 0, sizeof(uint64_t) * cfg_.pool_slots);
     mask_in_encoder_ = enc_->masked_sse_in_encoder();
     if (masked() && !mask_in_encoder_) {
         const h264::Geometry& eg = enc_->geometry();
         const int nb = pix::sse_masked_blocks(eg.width, eg.height);
-        HIP_CHECK(hipMalloc(&mask_dev_, 2 * (size_t)nb * sizeof(unsigned long long)));
-        HIP_CHECK(hipMalloc(&mask_counter_, 2 * sizeof(unsigned int)));
-        HIP_CHECK(hipMemset(mask_counter_, 0, 2 * sizeof(unsigned int)));
+        HIP_CHECK(hipMalloc(&mask_dev_, kMaxDepth * (size_t)nb * sizeof(unsigned long long)));
+        HIP_CHECK(hipMalloc(&mask_counter_, kMaxDepth * sizeof(unsigned int)));
+        HIP_CHECK(hipMemset(mask_counter_, 0, kMaxDepth * sizeof(unsigned int)));
         mask_stride_ = nb;
-        HIP_CHECK(hipHostMalloc(&mask_host_, 2 * sizeof(unsigned long long), hipHostMallocMapped));
-        for (int k = 0; k < 2; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_mask_[k], hipEventDisableTiming));
+        HIP_CHECK(hipHostMalloc(&mask_host_, kMaxDepth * sizeof(unsigned long long), hipHostMallocMapped));
+        for (int k = 0; k < kMaxDepth; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_mask_[k], hipEventDisableTiming));
     }
     // one parameter block per frame slot: with two frames in flight a captured memcpy node may
     // run after the host has already written the next frame's parameters
@@ -160,7 +165,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams) * cfg_.pool_slots));
     // [frame slot][encoder slot][IDR][analysis, entropy]
-    graphs_.assign((size_t)cfg_.pool_slots * 2 * 2 * 2, nullptr);
+    graphs_.assign((size_t)cfg_.pool_slots * kMaxDepth * 2 * 2, nullptr);
     t0_us_ = now_us();
 }
 
@@ -172,13 +177,14 @@ Session::~Session() {
     for (auto g : graphs_)
         if (g) hipGraphExecDestroy(g);
     hipHostFree(synth_host_);
+    if (ts_) hipHostFree(ts_);
     if (synth_bg_) hipFree(synth_bg_);
     hipFree(synth_dev_);
     enc_.reset();
     pool_.reset();
     hipFree(nv12_y_);
     hipFree(nv12_uv_);
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < kMaxDepth; ++k)
         if (staging_[k]) (void)hipHostFree(staging_[k]);
     if (lt_mem_) hipFree(lt_mem_);
     if (lt_mf_mem_) hipFree(lt_mf_mem_);
@@ -188,30 +194,30 @@ Session::~Session() {
         (void)hipStreamSynchronize(upload_stream_);
         (void)hipStreamDestroy(upload_stream_);
     }
-    for (int k = 0; k < 2; ++k) (void)hipEventDestroy(ev_start_[k]);
+    for (int k = 0; k < kMaxDepth; ++k) (void)hipEventDestroy(ev_start_[k]);
     if (mask_dev_) (void)hipFree(mask_dev_);
     if (mask_counter_) (void)hipFree(mask_counter_);
     if (mask_host_) (void)hipHostFree(mask_host_);
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < kMaxDepth; ++k)
         if (ev_mask_[k]) (void)hipEventDestroy(ev_mask_[k]);
     hipStreamDestroy(stream_);
 }
 
-void Session::convert(int slot) {
+void Session::convert(int slot, uint64_t* ts) {
     const h264::Geometry& g = enc_->geometry();
     if (scale_) {
         pix::launch_scale_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, lt_, nv12_y_, nv12_uv_,
-                                  g.pitch, g.coded_w, g.coded_h, stream_);
+                                  g.pitch, g.coded_w, g.coded_h, stream_, ts);
     } else {
         pix::launch_bgrx_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, nv12_y_, nv12_uv_,
-                                 g.pitch, g.coded_w, g.coded_h, stream_);
+                                 g.pitch, g.coded_w, g.coded_h, stream_, ts);
     }
     HIP_CHECK(hipGetLastError());
 }
 
-void Session::convert_and_encode(int slot, bool force_idr) {
+void Session::convert_and_encode(int slot, bool force_idr, bool stamp) {
     TraceRange tr("mxdesk.convert+encode.enqueue");
-    convert(slot);
+    convert(slot, (stamp && devclk_) ? ts_ + slot : nullptr);
     enc_->submit(nv12_y_, nv12_uv_, force_idr);
     enqueue_mask_sse(inflight_.back().k);
 }
@@ -240,11 +246,11 @@ void Session::mask_rect_mb(int r[4]) const {
     r[3] = std::min(e.height, (cfg_.mask_y1 + 15) / 16 * 16);
 }
 
-int Session::begin_frame() {
+int Session::begin_frame(int slot) {
     if ((int)inflight_.size() >= depth_) throw std::logic_error("Session: collect() before the next submit");
     const int k = next_k_;
     next_k_ = (next_k_ + 1) % depth_;
-    inflight_.push_back(Inflight{frame_id_, now_us(), k});
+    inflight_.push_back(Inflight{frame_id_, now_us(), k, slot});
     t_capture_ = inflight_.back().t_capture;
     return k;
 }
@@ -327,24 +333,25 @@ void Session::submit_synthetic(bool force_idr) {
         ~Acc() { a += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count(); }
     } acc{ht_submit_, t_in};
     TraceRange tr("mxdesk.submit_synthetic");
-    const int k = begin_frame();
     const int slot = pool_->acquire();
-    const pix::SynthParams p = synth_params();
+    const int k = begin_frame(slot);
+    pix::SynthParams p = synth_params();
+    if (devclk_) p.ts = ts_ + slot;
     ++frame_id_;
     // the first CBR frame runs eagerly: its rate-control probe encodes synchronously
     if (!cfg_.use_graph || enc_->rc().wants_probe()) {
-        HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+        if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
         pix::launch_synth(pool_->data(slot), p, stream_, synth_bg_);
         HIP_CHECK(hipGetLastError());
-        convert_and_encode(slot, force_idr);
+        convert_and_encode(slot, force_idr, false);
         return;
     }
     synth_host_[slot] = p;  // read by this slot's graph memcpy node (its previous frame was collected)
     const bool idr = enc_->prepare(force_idr);
     const int es = depth_ > 1 ? enc_->prep_slot() : 0;
-    HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+    if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
     enc_->record_start();
-    const size_t key = (((size_t)slot * 2 + (size_t)es) * 2 + (idr ? 1 : 0)) * 2;
+    const size_t key = (((size_t)slot * kMaxDepth + (size_t)es) * 2 + (idr ? 1 : 0)) * 2;
     if (!graphs_[key]) capture_frame_graphs(slot, idr, &graphs_[key], &graphs_[key + 1]);
     HIP_CHECK(hipGraphLaunch(graphs_[key], stream_));
     if (graphs_[key + 1]) {
@@ -381,32 +388,32 @@ void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_i
     for (const auto& r : host_regs_) {
         if (host_bgrx < r.first || host_bgrx + span > r.first + r.second) continue;
         // zero-copy: DMA straight from the registered capture buffer
-        const int k = begin_frame();
-        ++frame_id_;
         const int slot = pool_->acquire();
-        HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
-        // the DMA runs on its own stream, so waiting for it below does not also wait for the
-        // previous frame's analysis kernels queued on stream_ (keeps the depth-2 overlap); the
-        // slot's last reader (the conversion pool_slots frames ago) finished before that
-        // frame was collected
-        HIP_CHECK(hipStreamWaitEvent(upload_stream_, ev_start_[k], 0));
+        const int k = begin_frame(slot);
+        ++frame_id_;
+        if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+        // the DMA runs on its own stream with no dependency on stream_, so waiting for it below
+        // does not also wait for the previous frames' analysis kernels queued there (keeps the
+        // pipelined overlap).  The pool slot needs no ordering: its last reader (the conversion
+        // pool_slots > depth frames ago) finished before that frame was collected, and a frame is
+        // collected only after its whole chain completed.
         HIP_CHECK(hipMemcpy2DAsync(pool_->data(slot), pool_->pitch(), host_bgrx, host_pitch, row, cfg_.height,
                                    hipMemcpyHostToDevice, upload_stream_));
         HIP_CHECK(hipEventRecord(ev_upload_, upload_stream_));
         HIP_CHECK(hipStreamWaitEvent(stream_, ev_upload_, 0));
-        convert_and_encode(slot, force_idr);
+        convert_and_encode(slot, force_idr, true);  // GPU time from the conversion (DMA excluded)
         HIP_CHECK(hipEventSynchronize(ev_upload_));  // the caller may overwrite the buffer now
         return;
     }
-    const int k = begin_frame();
-    ++frame_id_;
     const int slot = pool_->acquire();
+    const int k = begin_frame(slot);
+    ++frame_id_;
     for (int r = 0; r < cfg_.height; ++r)
         std::memcpy(staging_[k] + (size_t)r * pool_->pitch(), host_bgrx + (size_t)r * host_pitch, row);
-    HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+    if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
     HIP_CHECK(hipMemcpyAsync(pool_->data(slot), staging_[k], (size_t)pool_->pitch() * cfg_.height,
                              hipMemcpyHostToDevice, stream_));
-    convert_and_encode(slot, force_idr);
+    convert_and_encode(slot, force_idr, true);  // GPU time from the conversion (upload excluded)
 }
 
 FrameResult Session::collect() {
@@ -416,7 +423,7 @@ FrameResult Session::collect() {
     FrameResult r;
     TraceRange tr("mxdesk.collect(wait+annexb)");
     const auto t_in = std::chrono::steady_clock::now();
-    HIP_CHECK(hipEventSynchronize(enc_->pending_done_event()));
+    wait_event(enc_->pending_done_event());  // MXDESK_WAIT=spin polls instead of blocking
     const auto t_w = std::chrono::steady_clock::now();
     const std::vector<uint8_t>& au = enc_->collect();
     r.t_encoded_us = now_us();
@@ -433,9 +440,14 @@ FrameResult Session::collect() {
     const h264::FrameStats& st = enc_->last_stats();
     r.idr = st.idr;
     r.qp = st.qp;
-    float ms = 0;
-    hipEventElapsedTime(&ms, ev_start_[fl.k], enc_->done_event());
-    r.gpu_ms = ms;  // render/upload start -> bitstream written
+    if (devclk_) {  // device clock: first kernel of the frame (render / conversion) -> end of its pack kernel
+        const uint64_t t0 = ts_[fl.slot], t1 = enc_->last_t_end();
+        r.gpu_ms = t1 > t0 ? (double)(t1 - t0) / clock_khz_ : 0.0;
+    } else {  // render/upload start -> bitstream written (events)
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev_start_[fl.k], enc_->done_event());
+        r.gpu_ms = ms;
+    }
     const double ny = (double)enc_->rc().config().width * enc_->rc().config().height, nc = ny / 4;
     auto psnr = [](uint64_t sse, double n) { return sse == 0 ? 99.0 : std::min(99.0, 10.0 * std::log10(65025.0 * n / (double)sse)); };
     r.psnr_y = psnr(st.sse[0], ny);
@@ -453,6 +465,55 @@ FrameResult Session::collect() {
     return r;
 }
 
+PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, double seconds, int threads) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    const int k = (int)sessions.size();
+    threads = std::max(1, std::min(threads, k));
+    const int slots = std::max(1, (int)std::lround(seconds * fps));
+    const auto period = std::chrono::nanoseconds((int64_t)(1e9 / std::max(1, fps)));
+    std::vector<std::vector<uint8_t>> late(threads, std::vector<uint8_t>(slots, 0));
+    std::vector<std::vector<double>> lat(threads);
+    std::vector<std::exception_ptr> err(threads);
+    // every thread starts on the same slot grid (a little ahead, so all are waiting for slot 0)
+    const auto t0 = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) {
+        th.emplace_back([&, t]() {
+            try {
+                HIP_CHECK(hipSetDevice(dev));
+                std::vector<Session*> mine;
+                for (int i = t; i < k; i += threads) mine.push_back(sessions[i]);
+                lat[t].reserve(mine.size() * (size_t)slots);
+                for (int f = 0; f < slots; ++f) {
+                    const auto tick = t0 + f * period;
+                    std::this_thread::sleep_until(tick);
+                    for (Session* s : mine) s->submit_synthetic(false);
+                    for (Session* s : mine) {
+                        const FrameResult r = s->collect();
+                        lat[t].push_back((r.t_encoded_us - r.t_capture_us) / 1000.0);
+                    }
+                    late[t][f] = std::chrono::steady_clock::now() > tick + period ? 1 : 0;
+                }
+            } catch (...) {
+                err[t] = std::current_exception();
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+    PacedStats st;
+    st.slots = slots;
+    for (int f = 0; f < slots; ++f) {
+        bool l = false;
+        for (int t = 0; t < threads; ++t) l |= late[t][f] != 0;
+        st.late_slots += l ? 1 : 0;
+    }
+    for (auto& v : lat) st.lat_ms.insert(st.lat_ms.end(), v.begin(), v.end());
+    return st;
+}
+
 std::vector<std::vector<FrameResult>> run_sessions(const std::vector<Session*>& sessions, int n_frames, int depth) {
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
@@ -461,8 +522,7 @@ std::vector<std::vector<FrameResult>> run_sessions(const std::vector<Session*>& 
     std::vector<std::exception_ptr> err(k);
     std::vector<std::thread> th;
     th.reserve(k);
-    for (size_t i = 0; i < k; ++i) {
-        th.emplace_back([&, i]() {
+    auto drive = [&](size_t i) {
             try {
                 HIP_CHECK(hipSetDevice(dev));
                 Session& s = *sessions[i];
@@ -483,9 +543,14 @@ std::vector<std::vector<FrameResult>> run_sessions(const std::vector<Session*>& 
             } catch (...) {
                 err[i] = std::current_exception();
             }
-        });
+    };
+    // one session runs on the calling thread (no thread start-up inside a caller's timed region)
+    if (k == 1) {
+        drive(0);
+    } else {
+        for (size_t i = 0; i < k; ++i) th.emplace_back(drive, i);
+        for (auto& t : th) t.join();
     }
-    for (auto& t : th) t.join();
     for (auto& e : err)
         if (e) std::rethrow_exception(e);
     return out;

@@ -55,7 +55,7 @@ struct SessionConfig {
     int out_height = 0;
     int fps = 60;
     int noise = 1;          // synthetic animated-noise panel
-    int pool_slots = 3;
+    int pool_slots = 4;     // > encoder pipeline depth (<= kMaxDepth)
     int use_graph = 0;      // replay the per-frame chain as a hipGraph (measured slower than eager
                             // launches on ROCm 7.2 for this chain: profiles/r01_graph)
     int fake_clock = 0;     // barcode timestamp = frame_id * 1e6 / fps (deterministic streams for tests)
@@ -80,6 +80,16 @@ struct FrameResult {
 };
 
 class Session;
+// Paced serving load: K sessions at `fps` for `seconds`, driven by `threads` host threads (session
+// i on thread i % threads, one frame in flight per session).  Every 1/fps slot each thread
+// submits a frame on each of its sessions, then collects them; a slot is late when any thread
+// finished it after the next slot's start.  Latency = capture -> access unit on the host.
+struct PacedStats {
+    int slots = 0;
+    int late_slots = 0;
+    std::vector<double> lat_ms;  // every frame of every session (slot order)
+};
+PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, double seconds, int threads);
 // Drives several sessions concurrently, one host thread per session (submit / collect with up
 // to `depth` frames in flight each): the per-frame launch sequence is host work, so one
 // thread interleaving K sessions leaves the GPU waiting on it.  Returns each session's
@@ -131,8 +141,10 @@ class Session {
     int graphs_built() const { return graphs_built_; }
 
    private:
-    void convert(int slot);
-    void convert_and_encode(int slot, bool force_idr);
+    void convert(int slot, uint64_t* ts = nullptr);
+    // stamp: the conversion stores the frame's start clock (capture paths; the synthetic path's
+    // render stamps it)
+    void convert_and_encode(int slot, bool force_idr, bool stamp);
     pix::SynthParams synth_params();
     hipGraphExec_t capture_on(hipStream_t st, const std::function<void()>& body);
     void capture_frame_graphs(int slot, bool idr, hipGraphExec_t* ga, hipGraphExec_t* ge);
@@ -143,7 +155,8 @@ class Session {
     std::unique_ptr<VideoEncoder> enc_;
     uint8_t* nv12_y_ = nullptr;
     uint8_t* nv12_uv_ = nullptr;
-    uint8_t* staging_[2] = {nullptr, nullptr};  // pinned upload buffers (one per frame in flight)
+    static constexpr int kMaxDepth = 3;  // frames in flight per session (encoder pipeline depth)
+    uint8_t* staging_[kMaxDepth] = {};  // pinned upload buffers (one per frame in flight)
     // Lanczos tables (device) when out size != desktop size
     bool scale_ = false;
     pix::LanczosTables lt_{};
@@ -152,20 +165,26 @@ class Session {
     std::vector<std::pair<const uint8_t*, size_t>> host_regs_;  // register_host_buffer ranges
     hipEvent_t ev_upload_ = nullptr;
     hipStream_t upload_stream_ = nullptr;  // zero-copy DMA from registered capture buffers
-    // frames in flight (pipeline depth 1 or 2): per-frame start event / staging buffer
+    // frames in flight (pipeline depth 1..kMaxDepth): per-frame start event / staging buffer
     struct Inflight {
         uint32_t frame_id;
         int64_t t_capture;
-        int k;  // index into ev_start_ / staging_
+        int k;     // index into ev_start_ / staging_
+        int slot;  // frame-pool slot (index into ts_)
     };
     std::deque<Inflight> inflight_;
-    hipEvent_t ev_start_[2] = {nullptr, nullptr};
+    hipEvent_t ev_start_[kMaxDepth] = {};  // encoders without device clock stamps only
+    // device clock at each frame's first kernel (render or conversion), per pool slot (mapped pinned):
+    // with an encoder's end stamp it gives the frame's GPU time without events between kernels
+    uint64_t* ts_ = nullptr;
+    bool devclk_ = false;
+    double clock_khz_ = 100000;
     // masked-PSNR accumulators (device) + their host copies, one per frame in flight
     unsigned long long* mask_dev_ = nullptr;
     unsigned long long* mask_host_ = nullptr;  // mapped pinned, one word per frame in flight
     unsigned int* mask_counter_ = nullptr;     // single-pass reduction counters (device)
     int mask_stride_ = 0;
-    hipEvent_t ev_mask_[2] = {nullptr, nullptr};
+    hipEvent_t ev_mask_[kMaxDepth] = {};
     bool masked() const { return cfg_.mask_x1 > cfg_.mask_x0 && cfg_.mask_y1 > cfg_.mask_y0; }
     bool mask_in_encoder_ = false;  // H.264: the encoder reports the masked distortion itself
     void enqueue_mask_sse(int k);
@@ -187,7 +206,7 @@ class Session {
     int64_t ht_n_ = 0;
     int64_t t_capture_ = 0;
     int cursor_x_ = -1, cursor_y_ = -1;
-    int begin_frame();  // reserve an in-flight entry, returns its k
+    int begin_frame(int slot);  // reserve an in-flight entry for a frame in pool slot `slot`, returns its k
 };
 
 // Host-side Lanczos-3 table generation (shared with the Python reference in tests).

@@ -323,36 +323,40 @@ def test_graph_replay_matches_stream_launches(gpu):
     assert len(Decoder().decode(b"".join(graph))) == 9
 
 
-def test_pipelined_depth2_matches_depth1(gpu):
-    """Two frames in flight (entropy of frame n on a second stream, overlapping analysis of
-    n+1): constant-QP output is bit-identical to depth 1; with CBR the stream still decodes and
-    frame ids / capture times come back in submission order."""
-    def run(depth, kbps, n=8):
-        cfg = gpu.SessionConfig()
-        cfg.width, cfg.height, cfg.fps = 320, 192, 60
-        cfg.enc.bitrate_kbps = kbps
-        cfg.enc.pipeline_depth = depth
-        cfg.fake_clock = 1
-        s = gpu.Session(cfg)
-        out = []
-        s.submit(False)
-        for i in range(n):
-            if i + 1 < n:
-                if depth == 2:
-                    s.submit(i + 1 == 5)  # forced IDR mid-stream
-                    out.append(s.collect())
-                else:
-                    out.append(s.collect())
-                    s.submit(i + 1 == 5)
-            else:
-                out.append(s.collect())
-        assert s.in_flight == 0
-        return out
+def _run_pipelined(gpu, depth, kbps, n=8, codec="h264", idr_at=5, use_graph=0):
+    """n frames with up to `depth` in flight (submit ahead, then collect / submit), a forced IDR
+    at frame idr_at."""
+    cfg = gpu.SessionConfig()
+    cfg.width, cfg.height, cfg.fps = 320, 192, 60
+    cfg.codec = codec
+    cfg.enc.bitrate_kbps = kbps
+    cfg.enc.pipeline_depth = depth
+    cfg.use_graph = use_graph
+    cfg.fake_clock = 1
+    s = gpu.Session(cfg)
+    out, sent = [], 0
+    while sent < min(depth, n):
+        s.submit(sent == idr_at)
+        sent += 1
+    for _ in range(n):
+        out.append(s.collect())
+        if sent < n:
+            s.submit(sent == idr_at)
+            sent += 1
+    assert s.in_flight == 0
+    return out, s.graphs_built
 
-    a, b = run(1, 0), run(2, 0)
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_pipelined_depth_matches_depth1(gpu, depth):
+    """Two / three frames in flight (entropy of frame n on a second stream, overlapping analysis
+    of n+1; with three the next frame's launches queue while the host collects): constant-QP
+    output is bit-identical to depth 1; with CBR the stream still decodes and frame ids / capture
+    times come back in submission order."""
+    a, b = _run_pipelined(gpu, 1, 0)[0], _run_pipelined(gpu, depth, 0)[0]
     assert [r.au for r in a] == [r.au for r in b]
     assert [r.frame_id for r in b] == list(range(8)) and [r.idr for r in b][5] == 1
-    c = run(2, 600)
+    c = _run_pipelined(gpu, depth, 600)[0]
     frames = Decoder().decode(b"".join(r.au for r in c))
     ids = [_read_barcode(y, gpu.BARCODE_CELL, gpu.BARCODE_X, gpu.BARCODE_Y)[0] for y, _, _ in frames]
     assert ids == list(range(8))
@@ -440,6 +444,42 @@ def test_zero_copy_registered_capture_matches_staged_upload(gpu):
 
 
 @pytest.mark.parametrize("codec", ["h264", "hevc"])
+def test_depth3_hevc_h264_match_depth1(gpu, codec):
+    """Three frames in flight == one, constant QP, both codecs (eager and graph replay)."""
+    a = _run_pipelined(gpu, 1, 0, n=10, codec=codec)[0]
+    b = _run_pipelined(gpu, 3, 0, n=10, codec=codec)[0]
+    g, built = _run_pipelined(gpu, 3, 0, n=10, codec=codec, use_graph=1)
+    assert built >= 4
+    for i, (x, y, z) in enumerate(zip(a, b, g)):
+        assert x.au == y.au == z.au, f"frame {i} differs"
+
+
+def test_hevc_graph_depth1_idr_same_key_matches_eager(gpu):
+    """HEVC, one frame in flight, temporal AQ: forced IDRs at frames 3 and 6 (frame 0, the CBR
+    probe frame, runs eagerly) reuse the same graph key (pool slot 0 of 3, encoder slot) with the
+    reconstruction / source buffers swapped; the IDR's source copy
+    must follow the frame (read on the device), or the next P picture's temporal classes compare
+    against a stale source and the graph output diverges from eager launches."""
+    def run(use_graph):
+        cfg = gpu.SessionConfig()
+        cfg.width, cfg.height, cfg.fps = 320, 192, 60
+        cfg.codec = "hevc"
+        cfg.enc.bitrate_kbps = 600
+        cfg.enc.aq = 3
+        cfg.pool_slots = 3
+        cfg.use_graph = use_graph
+        cfg.fake_clock = 1
+        s = gpu.Session(cfg)
+        return [s.step(i in (3, 6)).au for i in range(9)], s.graphs_built
+
+    eager, _ = run(0)
+    graph, built = run(1)
+    assert built >= 2
+    for i, (a, b) in enumerate(zip(eager, graph)):
+        assert a == b, f"frame {i} differs"
+
+
+@pytest.mark.parametrize("codec", ["h264", "hevc"])
 def test_graph_replay_depth2_matches_eager(gpu, codec):
     """Two frames in flight with the per-frame chain replayed as two hipGraphs (analysis on the
     session stream, entropy on the encoder's entropy stream, linked by an event per frame):
@@ -497,3 +537,20 @@ def test_session_hevc_masked_psnr_from_encoder(gpu):
         mse = np.mean(((dy[:120, :200].astype(np.float64) - sy) ** 2)[keep])
         want = 99.0 if mse == 0 else min(99.0, 10 * np.log10(255.0 ** 2 / mse))
         assert abs(want - r.psnr_y_masked) < 1e-6, (want, r.psnr_y_masked)
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_device_clock_frame_times(gpu, depth):
+    """H.264 frames carry device wall-clock stamps (render start, encoder first kernel, end of
+    k_pack) instead of timing events: every frame reports a positive GPU time, the encoder's own
+    share is no larger than the whole frame's, and both stay below the frame's host latency."""
+    out = _run_pipelined(gpu, depth, 600, n=10)[0]
+    for r in out:
+        host_ms = (r.t_encoded_us - r.t_capture_us) / 1000.0
+        assert 0.0 < r.gpu_ms < host_ms + 0.5, (r.frame_id, r.gpu_ms, host_ms)
+    cfg = gpu.SessionConfig()
+    cfg.width, cfg.height = 320, 192
+    s = gpu.Session(cfg)
+    for _ in range(3):
+        r = s.step(False)
+        assert 0.0 < s.stats.encode_ms <= r.gpu_ms + 1e-6

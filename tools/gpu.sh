@@ -12,6 +12,7 @@
 #   prof:NAME[:ARGS]    rocprofv3 --kernel-trace --stats around bench.py ARGS -> OUT/prof_NAME/
 #   pmc:NAME:CTRS[:ARGS] rocprofv3 --pmc CTRS (comma list) around bench.py ARGS -> OUT/pmc_NAME/
 #   py:NAME:SCRIPT[:ARGS] python SCRIPT ARGS -> OUT/NAME.log
+#   env:VAR=VALUE       export VAR=VALUE for the following steps (env:VAR= unsets it)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:?usage: gpu.sh OUT STEP...}
@@ -62,6 +63,10 @@ for step in "$@"; do
             # shellcheck disable=SC2046
             timeout -k 10 600 python -u "$script" $(args_of "$pargs") > "$OUT/$name.log" 2>&1 \
                 || fail "py $name rc=$?" ;;
+        env)
+            var=${rest%%=*}
+            val=${rest#*=}
+            if [ -n "$val" ]; then export "$var=$val"; else unset "$var"; fi ;;
         *) fail "unknown step $step" ;;
     esac
 done
