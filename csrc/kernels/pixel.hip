@@ -82,16 +82,14 @@ __device__ __attribute__((noinline)) uint32_t static_px(int gx, int gy, const Sy
 struct DynBoxes {
     int x0[6], y0[6], x1[6], y1[6];
 };
-__device__ __forceinline__ DynBoxes dyn_boxes(const SynthParams& p) {
+__device__ __forceinline__ DynBoxes dyn_boxes(const SynthParams& p, int wx, int wy, int mw, int mh) {
     const int W = p.wall_w, H = p.wall_h;
     DynBoxes b;
     b.x0[0] = kBarX - kBarCell; b.y0[0] = kBarY - kBarCell;
     b.x1[0] = kBarX + 33 * kBarCell; b.y1[0] = kBarY + 3 * kBarCell;
     b.x0[1] = p.cursor_x >= 0 ? p.cursor_x : 0; b.y0[1] = p.cursor_y;
     b.x1[1] = p.cursor_x >= 0 ? p.cursor_x + 12 : 0; b.y1[1] = p.cursor_y + 19;
-    const int mw = W / 8 > 48 ? W / 8 : 48, mh = H / 8 > 32 ? H / 8 : 32;
-    b.x0[2] = (int)(W * 0.5f + W * 0.18f * sinf(p.t * 0.7f)) - mw / 2;
-    b.y0[2] = (int)(H * 0.62f + H * 0.12f * sinf(p.t * 1.1f)) - mh / 2;
+    b.x0[2] = wx; b.y0[2] = wy;  // the moving window, from the same per-frame constants desktop_px uses
     b.x1[2] = b.x0[2] + mw; b.y1[2] = b.y0[2] + mh;
     b.x0[3] = (int)(W * 0.55f); b.y0[3] = (int)(H * 0.10f);
     b.x1[3] = b.x0[3] + (int)(W * 0.38f); b.y1[3] = b.y0[3] + (int)(H * 0.50f);
@@ -101,9 +99,8 @@ __device__ __forceinline__ DynBoxes dyn_boxes(const SynthParams& p) {
     b.x1[5] = p.noise ? b.x0[5] + (int)(W * 0.16f) : b.x0[5]; b.y1[5] = b.y0[5] + (int)(H * 0.22f);
     return b;
 }
-// Whether any of pixels [gx, gx+n) of row gy lies in an animated element's bounds.
-// (2-pixel margin: the moving window's float position may round differently here than in
-// desktop_px() under FMA contraction; margin pixels are rendered exactly, not copied)
+// Whether any of pixels [gx, gx+n) of row gy lies in an animated element's bounds (2-pixel
+// margin kept from when the window position was computed twice under different FMA contraction).
 __device__ __forceinline__ bool in_dyn(const DynBoxes& b, int gx, int n, int gy) {
     bool hit = false;
 #pragma unroll
@@ -112,7 +109,28 @@ __device__ __forceinline__ bool in_dyn(const DynBoxes& b, int gx, int n, int gy)
     return hit;
 }
 
-__device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
+// Per-frame constants of the animated elements, formed once per thread (the per-pixel sinf of
+// the moving window's path and the gear angles were most of k_synth's VALU work)
+struct FrameConsts {
+    int wx, wy, mw, mh;       // moving window
+    float gear_a[3];          // gear rotation angles
+};
+__device__ __forceinline__ FrameConsts frame_consts(const SynthParams& p) {
+    const int W = p.wall_w, H = p.wall_h;
+    FrameConsts f;
+    f.mw = W / 8 > 48 ? W / 8 : 48;
+    f.mh = H / 8 > 32 ? H / 8 : 32;
+    const float cxm = W * 0.5f, cym = H * 0.62f;
+    f.wx = (int)(cxm + W * 0.18f * sinf(p.t * 0.7f)) - f.mw / 2;
+    f.wy = (int)(cym + H * 0.12f * sinf(p.t * 1.1f)) - f.mh / 2;
+    const float a = p.t * 1.5707963f;  // 90 deg/s like glxgears' default speed order
+    f.gear_a[0] = a;
+    f.gear_a[1] = -2.f * a - 0.157f;
+    f.gear_a[2] = -2.f * a - 0.436f;
+    return f;
+}
+
+__device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p, const FrameConsts& fc) {
     const int W = p.wall_w, H = p.wall_h;
     // ---- barcode (frame id + timestamp), always on top
     if (gy >= kBarY - kBarCell && gy < kBarY + 2 * kBarCell + kBarCell && gx >= kBarX - kBarCell &&
@@ -134,10 +152,7 @@ __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
     }
     // ---- moving window (Lissajous path, sub-pixel speeds)
     {
-        const int mw = W / 8 > 48 ? W / 8 : 48, mh = H / 8 > 32 ? H / 8 : 32;
-        const float cxm = W * 0.5f, cym = H * 0.62f;
-        const int wx = (int)(cxm + W * 0.18f * sinf(p.t * 0.7f)) - mw / 2;
-        const int wy = (int)(cym + H * 0.12f * sinf(p.t * 1.1f)) - mh / 2;
+        const int mw = fc.mw, mh = fc.mh, wx = fc.wx, wy = fc.wy;
         if (gx >= wx && gx < wx + mw && gy >= wy && gy < wy + mh) {
             if (gy - wy < 10) return bgrx(40, 90, 200);
             const int u = (gx - wx) * 255 / mw, v = (gy - wy) * 255 / mh;
@@ -152,13 +167,12 @@ __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p) {
             if (gy - y0 < 12) return bgrx(60, 60, 70);  // title bar
             const float s = 16.f / (ww < wh ? ww : wh);
             const float sx = (gx - x0 - ww * 0.5f) * s, sy = -((gy - y0 - 6) - (wh - 12) * 0.5f) * s - 1.0f;
-            const float a = p.t * 1.5707963f;  // 90 deg/s like glxgears' default speed order
             float sh;
-            if (gear_hit(sx + 3.0f, sy + 2.0f, 1.0f, 4.0f, 0.7f, 20, a, &sh))
+            if (gear_hit(sx + 3.0f, sy + 2.0f, 1.0f, 4.0f, 0.7f, 20, fc.gear_a[0], &sh))
                 return bgrx((int)(204 * sh), (int)(25 * sh), 0);
-            if (gear_hit(sx - 3.1f, sy + 2.0f, 0.5f, 2.0f, 0.7f, 10, -2.f * a - 0.157f, &sh))
+            if (gear_hit(sx - 3.1f, sy + 2.0f, 0.5f, 2.0f, 0.7f, 10, fc.gear_a[1], &sh))
                 return bgrx(0, (int)(204 * sh), (int)(50 * sh));
-            if (gear_hit(sx + 3.1f, sy - 4.2f, 1.3f, 2.0f, 0.7f, 10, -2.f * a - 0.436f, &sh))
+            if (gear_hit(sx + 3.1f, sy - 4.2f, 1.3f, 2.0f, 0.7f, 10, fc.gear_a[2], &sh))
                 return bgrx((int)(50 * sh), (int)(50 * sh), (int)(255 * sh));
             return bgrx(0, 0, 0);
         }
@@ -242,12 +256,13 @@ __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const Synt
     if (y >= p.height || x4 >= p.width) return;
     uint32_t v[4];
     const int gx = p.origin_x + x4, gy = p.origin_y + y;
-    if (bg != nullptr && x4 + 4 <= p.width && !in_dyn(dyn_boxes(p), gx, 4, gy)) {
+    const FrameConsts fc = frame_consts(p);
+    if (bg != nullptr && x4 + 4 <= p.width && !in_dyn(dyn_boxes(p, fc.wx, fc.wy, fc.mw, fc.mh), gx, 4, gy)) {
         const uint4 c = *reinterpret_cast<const uint4*>(bg + (size_t)y * p.pitch + 4 * x4);
         v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (x4 + k < p.width) ? desktop_px(gx + k, gy, p) : 0u;
+        for (int k = 0; k < 4; ++k) v[k] = (x4 + k < p.width) ? desktop_px(gx + k, gy, p, fc) : 0u;
     }
     uint32_t* row = reinterpret_cast<uint32_t*>(out + (size_t)y * p.pitch);
     if (x4 + 4 <= p.width) {
