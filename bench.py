@@ -41,6 +41,72 @@ CODEC_LABEL = {
     "vp8": ("VP8", "mxvp8enc", "VP8 (RFC 6386) key + inter frames"),
 }
 
+REGION_NAMES = ["wallpaper", "taskbar", "document", "noise", "terminal", "gears", "barcode", "video"]
+
+
+def desktop_regions(W: int, H: int):
+    """Pixel class map of the synthetic desktop in desktop coordinates (the renderer's layout,
+    csrc/kernels/pixel.hip static_px / desktop_px; indices into REGION_NAMES)."""
+    import numpy as np
+
+    cls = np.zeros((H, W), np.int8)
+    boxes = {  # (x0, y0, x1, y1), later entries on top as in the renderer's order
+        2: (int(W * .25), int(H * .52), int(W * .25) + int(W * .24), int(H * .52) + int(H * .36)),
+        1: (0, H - 32, W, H),
+        3: (int(W * .04), int(H * .55), int(W * .04) + int(W * .16), int(H * .55) + int(H * .22)),
+        4: (int(W * .04), int(H * .10), int(W * .04) + int(W * .42), int(H * .10) + int(H * .38)),
+        5: (int(W * .55), int(H * .10), int(W * .55) + int(W * .38), int(H * .10) + int(H * .50)),
+    }
+    for k in (2, 1, 3, 4, 5):
+        x0, y0, x1, y1 = boxes[k]
+        cls[y0:y1, x0:x1] = k
+    return cls
+
+
+def quality_probe(s, W: int, H: int, content: int, noise: int, n: int = 30) -> dict:
+    """Not timed: n more frames of the same session with the source and the reconstruction read
+    back, for per-region luma PSNR (regions of the renderer's layout; with motion content the
+    desktop regions pan under the screen-fixed barcode and video panel) and chroma PSNR."""
+    import numpy as np
+
+    base = desktop_regions(W, H)
+    if not noise:
+        base[base == 3] = 0
+    sse = np.zeros(len(REGION_NAMES))
+    cnt = np.zeros(len(REGION_NAMES))
+    suv = [0.0, 0.0]
+    for _ in range(n):
+        r = s.step(False)
+        sy, su = s.nv12()
+        ry, ru = s.recon()
+        if content == 1:
+            f = r.frame_id
+            px, py = (3 * f) % W, f % H
+            cls = np.roll(base, (-py, -px), axis=(0, 1))
+            vx0, vy0 = int(W * 0.60), int(H * 0.56)
+            cls[vy0:vy0 + int(H * 0.36), vx0:vx0 + int(W * 0.34)] = 7
+        else:
+            cls = base.copy()
+        cls[0:8 + 3 * 8, 0:8 + 33 * 8] = 6  # barcode (screen-fixed, kBarX/kBarY/kBarCell = 8)
+        e = (ry[:H, :W].astype(np.int64) - sy[:H, :W].astype(np.int64)) ** 2
+        sse += np.bincount(cls.ravel(), weights=e.ravel(), minlength=len(REGION_NAMES))
+        cnt += np.bincount(cls.ravel(), minlength=len(REGION_NAMES))
+        for c in range(2):
+            d = ru[:H // 2, c:W:2].astype(np.int64) - su[:H // 2, c:W:2].astype(np.int64)
+            suv[c] += float((d * d).sum())
+
+    def psnr(e, k):
+        return 99.0 if e <= 0 else round(min(99.0, 10 * np.log10(65025.0 * k / e)), 2)
+
+    regions = {REGION_NAMES[k]: psnr(sse[k], cnt[k]) for k in range(len(REGION_NAMES)) if cnt[k] > 0}
+    y = psnr(sse.sum(), cnt.sum())
+    out = {"frames": n, "psnr_y_db": y, "psnr_u_db": psnr(suv[0], n * (W // 2) * (H // 2)),
+           "psnr_v_db": psnr(suv[1], n * (W // 2) * (H // 2)), "regions_psnr_y_db": regions}
+    scored = {k: v for k, v in regions.items() if k not in ("noise", "barcode")}
+    out["worst_region_below_frame_db"] = round(y - min(scored.values()), 2) if scored else None
+    return out
+
+
 def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: float = 1.0,
                   threads: int = 8) -> dict:
     """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1) driven by
@@ -116,12 +182,19 @@ def main() -> None:
     ap.add_argument("--sao", type=int, default=None, help="HEVC sample adaptive offset (default on)")
     ap.add_argument("--hevc-slice-cost", type=int, default=None,
                     help="HEVC P-picture slice work target (more = fewer, longer slices)")
+    ap.add_argument("--hevc-wpp", type=int, default=None,
+                    help="HEVC wavefront substreams (1, default) or cost-balanced slices (0)")
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--me-coarse", type=int, default=None,
                     help="1: even-offset grid + integer neighbours, 0: exhaustive search (encoder default)")
     ap.add_argument("--intra4x4", type=int, default=None, help="0: intra MBs Intra16x16 only")
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
+    ap.add_argument("--content", default="desktop", choices=["desktop", "motion"],
+                    help="synthetic source: the desktop, or motion content (the whole desktop pans 3 px / frame "
+                         "under a screen-fixed video-like panel; no noise panel)")
+    ap.add_argument("--quality-probe", type=int, default=30,
+                    help="untimed frames after the run with per-region / chroma PSNR read back (0: off)")
     ap.add_argument("--aq", type=int, default=None,
                     help="adaptive quantisation: 0 off, 1 coarser QP for noise-like MBs, 2 + rate-distortion "
                          "residual drop for them (default: the encoder's)")
@@ -150,6 +223,9 @@ def main() -> None:
     args = ap.parse_args()
     if args.codec == "vp8":
         args.subpel = 0  # VP8 vectors here are full-sample (the reported ME setting says so)
+    content = 1 if args.content == "motion" else 0
+    if content:
+        args.noise = 0  # the motion content has a video panel instead of the noise panel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -189,6 +265,8 @@ def main() -> None:
         cfg.enc.sao = args.sao
     if args.hevc_slice_cost is not None:
         cfg.enc.hevc_slice_cost = args.hevc_slice_cost
+    if args.hevc_wpp is not None:
+        cfg.enc.hevc_wpp = args.hevc_wpp
     if args.intra_in_p is not None:
         cfg.enc.intra_in_p = args.intra_in_p
     if args.deblock is not None:
@@ -200,6 +278,7 @@ def main() -> None:
     if args.intra4x4 is not None:
         cfg.enc.intra4x4 = args.intra4x4
     cfg.noise = args.noise
+    cfg.content = content
     cfg.use_graph = args.graph
     cfg.enc.pipeline_depth = args.depth
     cfg.codec = args.codec
@@ -249,7 +328,7 @@ def main() -> None:
 
     barrier()
     t0 = time.perf_counter()
-    lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m = [], [], [], [], [], []
+    lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m, psnr_uv = [], [], [], [], [], [], []
     if K == 1 and args.depth == 1:
         results = [sessions[0].step(False) for _ in range(args.steps)]
     else:
@@ -262,8 +341,12 @@ def main() -> None:
         qps.append(r.qp)
         psnrs.append(r.psnr_y)
         psnrs_m.append(r.psnr_y_masked if args.noise else r.psnr_y)
+        psnr_uv.append((r.psnr_u, r.psnr_v))
         gpu_ms.append(r.gpu_ms)
 
+    quality = None
+    if args.quality_probe > 0 and rank == 0 and not args.out_width:
+        quality = quality_probe(sessions[0], args.width, args.height, content, args.noise, args.quality_probe)
     density = density_probe(N, cfg, args.fps) if args.density_probe else None
 
     if dist is not None:
@@ -313,6 +396,10 @@ def main() -> None:
             "mean_qp": round(statistics.mean(qps), 2),
             "mean_psnr_y_db": round(statistics.mean(psnrs), 2),
             "mean_psnr_y_db_noise_masked": round(statistics.mean(psnrs_m), 2),
+            "mean_psnr_u_db": round(statistics.mean(u for u, _ in psnr_uv), 2),
+            "mean_psnr_v_db": round(statistics.mean(v for _, v in psnr_uv), 2),
+            "content": args.content,
+            "quality_probe": quality,
             # measured, not extrapolated: K paced sessions (one HIP stream each, depth 1) on this
             # GPU from `threads` host threads, every frame of every session encoded within its 1/fps
             # slot; K found by doubling then bisecting up to the first failing K

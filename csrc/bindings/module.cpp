@@ -164,6 +164,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("partitions", &h264::EncoderConfig::partitions)
         .def_readwrite("tu_split", &h264::EncoderConfig::tu_split)
         .def_readwrite("hevc_slice_cost", &h264::EncoderConfig::hevc_slice_cost)
+        .def_readwrite("hevc_wpp", &h264::EncoderConfig::hevc_wpp)
         .def_readwrite("sao", &h264::EncoderConfig::sao);
 
     py::class_<h264::FrameStats>(m, "FrameStats")
@@ -500,16 +501,17 @@ PYBIND11_MODULE(_native, m) {
     m.def(
         "synth",
         [](uintptr_t out, int w, int h, int pitch, uint32_t frame_id, uint32_t ts, float t, int noise, int ox, int oy,
-           int wall_w, int wall_h, int cx, int cy, uintptr_t stream, uintptr_t static_bg) {
+           int wall_w, int wall_h, int cx, int cy, uintptr_t stream, uintptr_t static_bg, int content) {
             pix::SynthParams p{w, h, pitch, frame_id, ts, t, ox, oy, wall_w > 0 ? wall_w : w, wall_h > 0 ? wall_h : h,
                                noise, cx, cy};
+            p.content = content;
             pix::launch_synth(as_ptr<uint8_t>(out), p, as_stream(stream), as_ptr<const uint8_t>(static_bg));
             HIP_CHECK(hipGetLastError());
         },
         py::arg("out_ptr"), py::arg("width"), py::arg("height"), py::arg("pitch"), py::arg("frame_id") = 0,
         py::arg("timestamp_us") = 0, py::arg("t") = 0.f, py::arg("noise") = 1, py::arg("origin_x") = 0,
         py::arg("origin_y") = 0, py::arg("wall_w") = 0, py::arg("wall_h") = 0, py::arg("cursor_x") = -1,
-        py::arg("cursor_y") = -1, py::arg("stream") = 0, py::arg("static_bg") = 0);
+        py::arg("cursor_y") = -1, py::arg("stream") = 0, py::arg("static_bg") = 0, py::arg("content") = 0);
     m.def(
         "composite_nv12",
         [](uintptr_t tiles, int tw, int th, int cols, int rows, uintptr_t y, uintptr_t uv, int pitch,
@@ -615,6 +617,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("out_height", &SessionConfig::out_height)
         .def_readwrite("fps", &SessionConfig::fps)
         .def_readwrite("noise", &SessionConfig::noise)
+        .def_readwrite("content", &SessionConfig::content)
         .def_readwrite("pool_slots", &SessionConfig::pool_slots)
         .def_readwrite("use_graph", &SessionConfig::use_graph)
         .def_readwrite("fake_clock", &SessionConfig::fake_clock)

@@ -14,8 +14,10 @@
 //    through a per-wave LDS tile.  A row hands each finished macroblock's bottom lines (luma rows
 //    12..15, chroma rows 6..7: the p samples of the next row's top edge) down through an LDS ring
 //    with a progress counter (the row below waits only where its own top edge is filtered); the
-//    band's last row hands them to the next workgroup through global memory (sc1 64-bit stores,
-//    vmcnt drain, agent-scope flag; sc1 loads on the consumer: cdna_hip_programming.md Guideline 16).
+//    band's last row hands them to the next workgroup through global memory (agent-scope 64-bit
+//    atomic stores, an agent-scope release fence, then the progress flag with a release store; the
+//    consumer spins with relaxed loads and takes an agent-scope acquire fence before the payload:
+//    the HIP memory model's release / acquire pairing, cdna_hip_programming.md Guideline 16).
 //    Every sample byte has exactly one writer: rows 13..15 of a macroblock whose lower neighbour
 //    filters its top edge are written by the row below, else by their own row.
 //    Macroblocks with every bS == 0 (static desktop, skips with equal vectors) cost a record read
@@ -164,7 +166,7 @@ __device__ __forceinline__ int wait_glb(uint32_t* p, uint32_t epoch, int need, i
     for (unsigned s = 0;; ++s) {
         const uint32_t v = __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((v >> 12) == epoch && (int)(v & 0xfffu) >= need) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // payload read with sc1 loads below
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
             return (int)(v & 0xfffu);
         }
         if (s > kDbSpinLimit) {
@@ -304,9 +306,10 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                 lds_sync_wave();
                 if (lane == 0) lds_store(prog_me, x);
             } else if (!pic_last && below_top) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // payload drained before the flag
+                // every lane's payload stores ordered before the flag (agent-scope release)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 if (lane == 0)
-                    __hip_atomic_store((gu32*)(G.gprog) + 0 * g.mb_h + mby, (epoch << 12) | (uint32_t)x, __ATOMIC_RELAXED,
+                    __hip_atomic_store((gu32*)(G.gprog) + 0 * g.mb_h + mby, (epoch << 12) | (uint32_t)x, __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
         }
@@ -491,9 +494,9 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                 lds_sync_wave();
                 if (lane == 0) lds_store(prog_me, x);
             } else if (!pic_last && below_top) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // payload drained before the flag
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // payload before the flag
                 if (lane == 0)
-                    __hip_atomic_store((gu32*)(G.gprog) + 1 * g.mb_h + mby, (epoch << 12) | (uint32_t)x, __ATOMIC_RELAXED,
+                    __hip_atomic_store((gu32*)(G.gprog) + 1 * g.mb_h + mby, (epoch << 12) | (uint32_t)x, __ATOMIC_RELEASE,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
         }

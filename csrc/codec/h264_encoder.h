@@ -56,7 +56,11 @@ struct EncoderConfig {
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
-    int hevc_slice_cost = 1024;  // HEVC: P-picture slice work target (hevc_core.h cu_cost units; more = fewer slices)
+    int hevc_slice_cost = 1024;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
+    // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): one slice per P picture,
+    // every CTU row its own CABAC substream (one GPU wave each) that starts from the contexts the row
+    // above had after its second CTU; 0: cost-balanced slices, one substream per slice
+    int hevc_wpp = 1;
     int sao = 1;              // HEVC: sample adaptive offset (8.7.3), band / edge offsets decided per CTB
     // quality report: luma distortion outside the macroblocks touching this pixel rectangle
     // (FrameStats::sse_masked; mask_x1 <= mask_x0 = no mask)

@@ -285,11 +285,15 @@ constexpr int kMaxRange = 32;
 static_assert(kMaxRange + 2 <= kHpelPad, "search window must stay inside the padded planes");
 constexpr int kWinStride = 16 + 2 * kMaxRange + 8;  // bytes per LDS window row (dword padded)
 
-__global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* __restrict__ fs,
+// Five waves: the +-16 search is 33 x 9 = 297 candidate tasks (four adjacent offsets each), one
+// pass of 320 threads instead of 1.16 passes of 256 (the second pass ran 41 tasks on a full
+// workgroup); the refinement phases below are laid out for 256 threads and leave wave 4 idle.
+constexpr int kMeThreads = 320, kMeWaves = kMeThreads / 64;
+__global__ __launch_bounds__(kMeThreads) void k_me_full(Geometry g, const FrameState* __restrict__ fs,
                                                   const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs) {
     __shared__ uint32_t win32[(16 + 2 * kMaxRange) * kWinStride / 4];
     __shared__ uint32_t srcw[64];
-    __shared__ unsigned long long red[4];
+    __shared__ unsigned long long red[kMeWaves];
     __shared__ uint32_t cand_cost[8];
     __shared__ uint32_t s_sad0[4];
 
@@ -330,7 +334,8 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     }
     // search window from the padded full-sample plane with dword loads (x0 - R is a
     // multiple of 4 and R + 2 <= kHpelPad: no clamping, no byte gathers)
-    for (int i = tid; i < W * kWs4; i += 256) {
+    const bool t256 = tid < 256;  // the threads of the 256-thread refinement layouts
+    for (int i = tid; i < W * kWs4; i += kMeThreads) {
         const int wy = i / kWs4, wx4 = (i - wy * kWs4) * 4;
         win32[i] = (wx4 < W) ? *reinterpret_cast<const uint32_t*>(P.f + (y0 - R + wy) * P.pitch + (x0 - R + wx4)) : 0u;
     }
@@ -371,7 +376,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     if (parts) {
         // tasks: the even grid (coarse, shifts 0 and 2 of a dword group) or every group (shifts 0..3)
         const int nsh = coarse ? 2 : 4, ntp = coarse ? (R + 1) * gw : ngroups;
-        for (int q = tid; q < ntp; q += 256) {
+        for (int q = tid; q < ntp; q += kMeThreads) {
             const int dyr = coarse ? 2 * (q / gw) : q / gw, g = q % gw;
             uint32_t acc[4][4];  // [shift index][quadrant]
 #pragma unroll
@@ -410,7 +415,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             }
         }
     }
-    for (int q = tid; q < ntask; q += 256) {
+    for (int q = tid; q < ntask; q += kMeThreads) {
         const int dyr = 2 * (q / gw), g = q % gw;
         uint32_t s0a = 0, s2a = 0;
 #pragma unroll 4
@@ -438,7 +443,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             best = key < best ? key : best;
         }
     }
-    for (int q = tid; q < ((coarse || parts) ? 0 : ngroups); q += 256) {
+    for (int q = tid; q < ((coarse || parts) ? 0 : ngroups); q += kMeThreads) {
         const int dyr = q / gw, g = q - dyr * gw;
         uint32_t sad[4] = {0, 0, 0, 0};
 #pragma unroll 2
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         best = other < best ? other : best;
     }
     if (lane == 0) red[tid >> 6] = best;
-    __shared__ unsigned long long pred4[4][4];  // partitions: [shape][wave]
+    __shared__ unsigned long long pred4[4][kMeWaves];  // partitions: [shape][wave]
     if (parts) {
 #pragma unroll
         for (int sh = 0; sh < 4; ++sh) {
@@ -490,21 +495,21 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     }
     __syncthreads();
     unsigned long long b = red[0];
-    for (int i = 1; i < 4; ++i) b = red[i] < b ? red[i] : b;
+    for (int i = 1; i < kMeWaves; ++i) b = red[i] < b ? red[i] : b;
     unsigned long long pbest[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     if (parts)
         for (int sh = 0; sh < 4; ++sh)
-            for (int i = 0; i < 4; ++i) pbest[sh] = pred4[sh][i] < pbest[sh] ? pred4[sh][i] : pbest[sh];
+            for (int i = 0; i < kMeWaves; ++i) pbest[sh] = pred4[sh][i] < pbest[sh] ? pred4[sh][i] : pbest[sh];
     if (parts && coarse) {
         // the 8 integer neighbours of each partition's grid best: 32 (shape, neighbour) pairs of
         // 128-sample rectangles, 8 lanes (16 samples) each
         __shared__ unsigned long long pnkey[4][8];
-        const int ev = tid >> 3, sub = tid & 7, sh = ev >> 3, k = ev & 7;
+        const int ev = (tid & 255) >> 3, sub = tid & 7, sh = ev >> 3, k = ev & 7;
         const int cb0 = (int)(pbest[sh] & 0xffff), bxr = cb0 % side, byr = cb0 / side;
         int ddx, ddy;
         subpel_offset(k, &ddx, &ddy);
         const int nxr = bxr + ddx, nyr = byr + ddy;
-        const bool inside = nxr >= 0 && nxr < side && nyr >= 0 && nyr < side;  // uniform per 8-lane group
+        const bool inside = t256 && nxr >= 0 && nxr < side && nyr >= 0 && nyr < side;  // uniform per 8-lane group
         int d = 0;
         if (inside) {
             // T / B: one 16-sample row each (row sub of the half); L / R: two 8-sample rows
@@ -519,7 +524,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             }
         }
         for (int o = 4; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (sub == 0) pnkey[sh][k] = inside ? mkey((uint32_t)d, nxr, nyr) : ~0ull;
+        if (t256 && sub == 0) pnkey[sh][k] = inside ? mkey((uint32_t)d, nxr, nyr) : ~0ull;
         __syncthreads();
         for (int s2 = 0; s2 < 4; ++s2)
             for (int i = 0; i < 8; ++i) pbest[s2] = pnkey[s2][i] < pbest[s2] ? pnkey[s2][i] : pbest[s2];
@@ -527,11 +532,11 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
     if (coarse) {  // the 8 integer neighbours of the grid best: one per 32-lane group
         __shared__ unsigned long long nkey[8];
         const int cb0 = (int)(b & 0xffff), bxr = cb0 % side, byr = cb0 / side;
-        const int k = tid >> 5, sub = tid & 31, py = sub >> 1, px0 = (sub & 1) * 8;
+        const int k = (tid & 255) >> 5, sub = tid & 31, py = sub >> 1, px0 = (sub & 1) * 8;
         int ddx, ddy;
         subpel_offset(k, &ddx, &ddy);
         const int nxr = bxr + ddx, nyr = byr + ddy;
-        const bool inside = nxr >= 0 && nxr < side && nyr >= 0 && nyr < side;  // uniform per group
+        const bool inside = t256 && nxr >= 0 && nxr < side && nyr >= 0 && nyr < side;  // uniform per group
         int d = 0;
         if (inside) {
             const uint8_t* wrow = reinterpret_cast<const uint8_t*>(win32) + (nyr + py) * kWinStride + nxr + px0;
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             for (int j = 0; j < 8; ++j) d += abs((int)(((j < 4 ? s0 : s1) >> (8 * (j & 3))) & 0xff) - (int)wrow[j]);
         }
         for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (sub == 0) {
+        if (t256 && sub == 0) {
             const int dx = nxr - R, dy = nyr - R;
             const uint32_t cost = me_cost((uint32_t)d, lambda, 4 * dx, 4 * dy);
             const uint32_t dist = (uint32_t)(abs(dx) + abs(dy));
@@ -574,7 +579,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
                 // per partition, 16 lanes (8 samples each) per candidate, both partitions at once
                 __shared__ uint8_t psp[2][4][18][kSpW];
                 __shared__ uint32_t pcand[2][8];
-                for (int i = tid; i < 2 * 4 * 18 * 18; i += 256) {
+                for (int i = tid; i < 2 * 4 * 18 * 18; i += kMeThreads) {
                     const int pi = i / (4 * 324), rem0 = i - pi * 4 * 324;
                     const int pl = rem0 / 324, rem = rem0 - pl * 324, r = rem / 18, c = rem - r * 18;
                     const uint8_t* base = pl == 0 ? P.f : pl == 1 ? P.h : pl == 2 ? P.v : P.j;
@@ -582,7 +587,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
                     psp[pi][pl][r][c] = base[(iy + r) * P.pitch + ix + c];
                 }
                 __syncthreads();
-                const int pi = tid >> 7, k = (tid >> 4) & 7, sub = tid & 15;
+                const int pi = (tid & 255) >> 7, k = (tid >> 4) & 7, sub = tid & 15;
                 // the 8 samples of this lane inside the partition rectangle
                 const int rx = part == kPart8x16 ? 8 * pi : 0, ry = part == kPart16x8 ? 8 * pi : 0;
                 const int prow = part == kPart16x8 ? (sub >> 1) : sub, pcol = part == kPart16x8 ? (sub & 1) * 8 : 0;
@@ -602,7 +607,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
                     }
                     for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
                     __syncthreads();  // the previous step's readers are done with pcand
-                    if (sub == 0) pcand[pi][k] = me_cost((uint32_t)d, lambda, cx, cy);
+                    if (t256 && sub == 0) pcand[pi][k] = me_cost((uint32_t)d, lambda, cx, cy);
                     __syncthreads();
                     for (int q = 0; q < 2; ++q) {
                         int bdx = 0, bdy = 0;
@@ -645,14 +650,14 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
         // srcw), a 5-step xor shuffle reduces each group, one barrier publishes the costs.
         __shared__ uint8_t sp[4][18][kSpW];
         const int ix = x0 + (mvx >> 2) - 1, iy = y0 + (mvy >> 2) - 1;
-        for (int i = tid; i < 4 * 18 * 18; i += 256) {
+        for (int i = tid; i < 4 * 18 * 18; i += kMeThreads) {
             const int pl = i / 324, rem = i - pl * 324, r = rem / 18, c = rem - r * 18;
             const uint8_t* base = pl == 0 ? P.f : pl == 1 ? P.h : pl == 2 ? P.v : P.j;
             sp[pl][r][c] = base[(iy + r) * P.pitch + ix + c];
         }
         __syncthreads();
         uint32_t cur_cost = (uint32_t)(b >> 32);
-        const int k = tid >> 5, sub = tid & 31;
+        const int k = (tid & 255) >> 5, sub = tid & 31;
         const int py = sub >> 1, px0 = (sub & 1) * 8;
         const uint32_t s0 = srcw[py * 4 + (px0 >> 2)], s1 = srcw[py * 4 + (px0 >> 2) + 1];
         const int base_x4 = px0 * 4 + 4 - mvx, base_y4 = py * 4 + 4 - mvy;  // local qpel coords = base + candidate mv
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(256) void k_me_full(Geometry g, const FrameState* _
             }
             for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
             __syncthreads();  // previous step's readers are done with cand_cost
-            if (sub == 0) cand_cost[k] = me_cost((uint32_t)d, lambda, cx, cy);
+            if (t256 && sub == 0) cand_cost[k] = me_cost((uint32_t)d, lambda, cx, cy);
             __syncthreads();
             int bdx = 0, bdy = 0;
             uint32_t bcost = cur_cost;
@@ -2535,7 +2540,7 @@ void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const plane
 
 void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream) {
     const int nmb = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_me_full, dim3(nmb), dim3(256), 0, stream, g, b.fs, src_y, b.mb);
+    hipLaunchKernelGGL(k_me_full, dim3(nmb), dim3(kMeThreads), 0, stream, g, b.fs, src_y, b.mb);
 }
 
 void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,

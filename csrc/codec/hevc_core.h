@@ -5,14 +5,20 @@
 // __host__ __device__, so the GPU kernels and the CPU oracle share one definition of
 // every bit and every sample.
 //
-// Coding subset (fixed by the SPS/PPS that hevc_encoder.cpp writes):
+// Coding subset (fixed by the SPS/PPS that hevc_cpu.cpp writes):
 //   CTB = CU = 16x16 (no split_cu_flag), PU 2Nx2N, TU 16x16 luma / 8x8 chroma; with
 //   EncoderConfig.tu_split an inter CU may instead split its transform tree once (four 8x8
 //   luma TUs, eight 4x4 chroma TUs: max_transform_hierarchy_depth_inter 1), chosen per CU by
-//   SSE + lambda * estimated bits, I slices of intra CUs, P slices of skip / merge /
-//   AMVP CUs with one reference picture, MaxNumMergeCand 5, no TMVP, no
-//   deblocking, no sign hiding, cu_qp_delta per CU (adaptive quantisation), one slice per
-//   CTU row so every slice is entropy coded by its own GPU wave.
+//   SSE + lambda * estimated bits; I slices of intra CUs, P slices of skip / merge / AMVP CUs
+//   with one reference picture, MaxNumMergeCand 5, no TMVP, no sign hiding, cu_qp_delta per CU
+//   (adaptive quantisation); in-loop deblocking (8.7.2) and sample adaptive offset (8.7.3, band /
+//   edge per CTB) on by default.
+// Slices and CABAC substreams (EncoderConfig.hevc_wpp, default on): wavefront parallel
+//   processing -- I pictures in slices of up to kMaxSliceRows CTU rows (the intra wavefront's
+//   workgroup), P pictures one slice; every CTU row is a CABAC substream entropy coded by its
+//   own GPU wave, starting from the contexts the row above had after its second CTU, with entry
+//   points in the slice header.  hevc_wpp 0: cost-balanced P slices (plan_num_slices), one
+//   substream each.
 //
 // Replaces NVENC HEVC behind the reference's GStreamer stack (nvh264enc default encoder,
 // reference Dockerfile:210 / README.md:21; BASELINE.json config "4K60 HEVC").
@@ -1534,9 +1540,11 @@ MXHD int for_each_part(const CuInfo& c, const Cf& cf, F f) {
 }
 
 // Binarise one part of CTU i (the k-th of a slice of `count` CTUs; qp_prev: its QP predictor).
+// wpp: entropy_coding_sync_enabled_flag -- a CTU row's last CTU (not the slice's last) ends its
+// substream with end_of_subset_one_bit after end_of_slice_segment_flag (7.3.8.1).
 template <class E, class Cf>
 MXHD void binarise_part(E& rec, const CtuPart& pt, bool islice, const CuInfo* cus, const Cf& cf,
-                        const uint32_t* sao, int i, int k, int count, int ctb_w, int qp_prev) {
+                        const uint32_t* sao, int i, int k, int count, int ctb_w, int qp_prev, bool wpp = false) {
     NoCtx nc;
     const CuInfo& c = cus[i];
     if (pt.kind == kPartHead) {
@@ -1564,20 +1572,25 @@ MXHD void binarise_part(E& rec, const CtuPart& pt, bool islice, const CuInfo* cu
         }
         code_sub_block(rec, nc, cf, pt.d, tu_csbf_raster(pt.d), pt.i, prev_gt1);
     } else {
-        rec.terminate(k == count - 1 ? 1 : 0);
+        const bool eos = k == count - 1;
+        rec.terminate(eos ? 1 : 0);
+        if (wpp && !eos && (i + 1) % ctb_w == 0) rec.terminate(1);  // end_of_subset_one_bit
     }
     rec.flush();
 }
+// WPP (8.6.1): the QP predictor restarts from the slice QP at the first quantization group of
+// every CTU row; without WPP only at the slice start.
+MXHD bool qp_prev_resets(int i, int k, int ctb_w, bool wpp) { return k == 0 || (wpp && i % ctb_w == 0); }
 
 // Binarise CTU i (the k-th of a slice of `count` CTUs) part by part.  qp_prev: QP predictor
 // (QpY of the previous CU that coded a residual in the slice, else the slice QP); updated as
 // code_cu does.  Returns the token count (> rec.cap: truncated).
 MXHD uint32_t binarise_ctu(BinRec& rec, bool islice, const CuInfo* cus, const int16_t* coef, const uint32_t* sao,
-                           int i, int k, int count, int ctb_w, int& qp_prev) {
+                           int i, int k, int count, int ctb_w, int& qp_prev, bool wpp = false) {
     const CoefArray cf{coef + (size_t)i * kCoefPerCu};
     const int qp_in = qp_prev;
     for_each_part(cus[i], cf, [&](const CtuPart& pt, int) {
-        binarise_part(rec, pt, islice, cus, cf, sao, i, k, count, ctb_w, qp_in);
+        binarise_part(rec, pt, islice, cus, cf, sao, i, k, count, ctb_w, qp_in, wpp);
     });
     qp_prev = cu_next_qp_prev(cus[i], qp_prev);
     return rec.n;
@@ -1630,8 +1643,10 @@ MXHD uint32_t code_slice_direct(uint8_t* out, uint32_t cap, bool islice, int sli
 
 // ---------------------------------------------------------------- encoder decisions
 // Intra candidates tried by the encoder, in tie-break order (any of the 35 modes decodes).
-constexpr int kNumIntraCands = 4;
-constexpr uint8_t kIntraCands[kNumIntraCands] = {1, 0, 26, 10};  // DC, planar, vertical, horizontal
+// DC, planar, vertical, horizontal, then the three 45-degree diagonals (down-right, down-left,
+// up-right) and the near-vertical 22 -- UI edges, text strokes and rotated / natural content
+constexpr int kNumIntraCands = 8;
+constexpr uint8_t kIntraCands[kNumIntraCands] = {1, 0, 26, 10, 18, 2, 34, 22};
 // Approximate luma mode signalling cost in bins given the left neighbour's MPM candidate.
 MXHD int intra_mode_bits(int mode, int cand_a) {
     int l[3];
@@ -1994,9 +2009,11 @@ MXHD void db_chroma_lines(uint8_t* q0, int step, int line, int nlines, int qp_p,
 
 // QpY of every CU (8.6.1): the coded QP where residual was sent, else the prediction = the
 // previous CU's QpY in the slice (slice QP at its start).
-MXHD void slice_qpy(const CuInfo* cus, int first, int count, int slice_qp, uint8_t* qpy) {
+MXHD void slice_qpy(const CuInfo* cus, int first, int count, int slice_qp, uint8_t* qpy, int ctb_w = 1,
+                     bool wpp = false) {
     int prev = slice_qp;
     for (int k = 0; k < count; ++k) {
+        if (wpp && (first + k) % ctb_w == 0) prev = slice_qp;  // WPP: the predictor restarts every CTU row
         const CuInfo& c = cus[first + k];
         if (c.type != kCuSkip && c.cbf) prev = c.qp;
         qpy[first + k] = (uint8_t)prev;

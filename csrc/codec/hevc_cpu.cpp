@@ -111,6 +111,7 @@ std::vector<int> HevcCommon::row_slices() const {
 }
 
 std::vector<int> HevcCommon::plan_p_slices(const std::vector<CuInfo>& cus) const {
+    if (wpp()) return {0};  // one slice, one substream per CTU row
     uint64_t total = 0;
     for (const auto& c : cus) total += cu_cost(c);
     const int S = plan_num_slices(total, max_slices_, (uint32_t)rc_.config().hevc_slice_cost);
@@ -241,7 +242,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.put(0, 1);  // weighted_bipred_flag
         w.put(0, 1);  // transquant_bypass_enabled_flag
         w.put(0, 1);  // tiles_enabled_flag
-        w.put(0, 1);  // entropy_coding_sync_enabled_flag
+        w.put(wpp() ? 1 : 0, 1);  // entropy_coding_sync_enabled_flag
         const bool db = c.hevc_deblock();
         w.put(db || c.sao, 1);  // pps_loop_filter_across_slices_enabled_flag (CU edges on slice borders too)
         w.put(1, 1);   // deblocking_filter_control_present_flag
@@ -262,7 +263,8 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
 }
 
 void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp,
-                                 const uint8_t* data, size_t n) const {
+                                 const uint8_t* data, size_t n, const uint32_t* sub_len, int nsub,
+                                 const uint32_t* sub_off) const {
     const int ctbs = ctb_w() * ctb_h();
     Bits w;
     w.put(addr == 0, 1);  // first_slice_segment_in_pic_flag
@@ -289,10 +291,83 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
     }
     w.se(qp - 26);  // slice_qp_delta
     if (config().hevc_deblock() || sao) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
-    w.trailing();   // byte_alignment()
-    std::vector<uint8_t> rbsp = std::move(w.b);
-    rbsp.insert(rbsp.end(), data, data + n);
-    nal(out, idr ? 19 : 1, rbsp);  // IDR_W_RADL / TRAIL_R
+    if (!wpp()) {
+        w.trailing();   // byte_alignment()
+        std::vector<uint8_t> rbsp = std::move(w.b);
+        rbsp.insert(rbsp.end(), data, data + n);
+        nal(out, idr ? 19 : 1, rbsp);  // IDR_W_RADL / TRAIL_R
+        return;
+    }
+    // entry points: every substream ends in a byte holding its alignment one-bit, so emulation
+    // prevention never spans two substreams and each can be escaped on its own
+    std::vector<uint8_t> esc;
+    std::vector<uint32_t> esc_len;
+    size_t at = 0, total = 0;
+    for (int k = 0; k < nsub; ++k) {
+        const size_t before = esc.size();
+        if (sub_off) at = sub_off[k];
+        h264::emulation_prevent(esc, data + at, sub_len[k]);
+        esc_len.push_back((uint32_t)(esc.size() - before));
+        at += sub_len[k];
+        total += sub_len[k];
+    }
+    if (total != n) throw std::logic_error("hevc: substream sizes do not add up to the slice payload");
+    w.ue((uint32_t)(nsub > 0 ? nsub - 1 : 0));  // num_entry_point_offsets
+    if (nsub > 1) {
+        uint32_t mx = 0;
+        for (int k = 0; k + 1 < nsub; ++k) mx = std::max(mx, esc_len[k] - 1);
+        int len = 1;
+        while (len < 32 && (mx >> len)) ++len;
+        w.ue((uint32_t)(len - 1));  // offset_len_minus1
+        for (int k = 0; k + 1 < nsub; ++k) w.put(esc_len[k] - 1, len);  // entry_point_offset_minus1
+    }
+    w.trailing();  // byte_alignment()
+    static const uint8_t sc[4] = {0, 0, 0, 1};
+    out.insert(out.end(), sc, sc + 4);
+    out.push_back((uint8_t)((idr ? 19 : 1) << 1));
+    out.push_back(1);
+    h264::emulation_prevent(out, w.b.data(), w.b.size());  // the header ends in its alignment one-bit too
+    out.insert(out.end(), esc.begin(), esc.end());
+}
+
+uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
+                        int first, int count, int ctb_w, const uint32_t* sao, uint16_t* tok,
+                        std::vector<uint32_t>& sub_len) {
+    sub_len.clear();
+    uint8_t ctx[C_NUM], saved[C_NUM];
+    bool have_saved = false;
+    uint32_t pos = 0;
+    CabacEnc e;
+    ArrCtx cx{ctx};
+    int qp_prev = slice_qp;
+    for (int k = 0; k < count; ++k) {
+        const int i = first + k;
+        const int x = i % ctb_w;
+        if (k == 0 || x == 0) {  // a substream starts
+            if (k > 0 && have_saved && ctb_w >= 2)
+                std::memcpy(ctx, saved, C_NUM);  // sync from the row above after its second CTU (9.3.2.4)
+            else
+                ctx_init_all(ctx, islice ? 0 : 1, slice_qp);
+            have_saved = false;
+            e.start(out + pos, cap > pos ? cap - pos : 0);
+        }
+        if (qp_prev_resets(i, k, ctb_w, true)) qp_prev = slice_qp;
+        BinRec rec;
+        rec.start(tok, kMaxCuTokens);
+        const uint32_t nt = binarise_ctu(rec, islice, cus, coef, sao, i, k, count, ctb_w, qp_prev, true);
+        for (uint32_t j = 0; j < nt && j < kMaxCuTokens; ++j) code_token(e, cx, tok[j]);
+        if (x == 1) {  // storage after the row's second CTU (9.3.2.2 end)
+            std::memcpy(saved, ctx, C_NUM);
+            have_saved = true;
+        }
+        if (k == count - 1 || x == ctb_w - 1) {  // substream ends: end_of_slice / end_of_subset coded
+            e.finish_slice();
+            if (e.overflow) return cap + 1;
+            sub_len.push_back(e.pos);
+            pos += e.pos;
+        }
+    }
+    return pos;
 }
 
 // ------------------------------------------------------------------ CPU encoder
@@ -522,14 +597,18 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         const std::vector<int> rows = common_.row_slices();
         const int W = common_.ctb_w(), H = common_.ctb_h();
         std::vector<uint8_t> buf;
+        std::vector<uint32_t> sub_len;
         uint8_t ctx[C_NUM];
         size_t total = 0;
         for (size_t s = 0; s < rows.size(); ++s) {
             const int first = rows[s], count = (s + 1 < rows.size() ? rows[s + 1] : W * H) - first;
             const uint32_t cap = (uint32_t)count * 1024 + 1024;
             buf.resize(cap);
-            total += code_slice(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(), first, count, W, ctx,
-                                nullptr, tok_.data()) + 12;
+            total += (common_.wpp() ? code_slice_wpp(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(),
+                                                     first, count, W, nullptr, tok_.data(), sub_len)
+                                    : code_slice(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(), first,
+                                                 count, W, ctx, nullptr, tok_.data())) +
+                     12;
         }
         rc.add_probe(qp_override_, (int)total + 64);
         qp_override_ = -1;
@@ -550,7 +629,7 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         std::vector<uint8_t> qpy((size_t)W * H);
         for (size_t s = 0; s < slices_.size(); ++s) {
             const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
-            slice_qpy(cu_.data(), first, count, qp, qpy.data());
+            slice_qpy(cu_.data(), first, count, qp, qpy.data(), W, common_.wpp());
         }
         for (int dir = 0; dir < 2; ++dir)
             for (int i = 0; i < W * H; ++i)
@@ -585,15 +664,20 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     au_.clear();
     if (idr) common_.write_parameter_sets(au_);
     std::vector<uint8_t> buf;
+    std::vector<uint32_t> sub_len;
     uint8_t ctx[C_NUM];
     for (size_t s = 0; s < slices_.size(); ++s) {
         const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
         const uint32_t cap = (uint32_t)count * 1024 + 1024;
         buf.resize(cap);
-        const uint32_t n = code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count, W, ctx,
-                                      cfg_.sao ? sao_.data() : nullptr, tok_.data());
+        const uint32_t* saop = cfg_.sao ? sao_.data() : nullptr;
+        const uint32_t n = common_.wpp() ? code_slice_wpp(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first,
+                                                          count, W, saop, tok_.data(), sub_len)
+                                         : code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count,
+                                                      W, ctx, saop, tok_.data());
         if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
-        common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n);
+        common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n,
+                                common_.wpp() ? sub_len.data() : nullptr, (int)sub_len.size());
     }
     // distortion over the display area
     const EncoderConfig& c = common_.config();

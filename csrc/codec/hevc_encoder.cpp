@@ -15,7 +15,7 @@ namespace hevc {
 
 void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     const int ncu = geom_.mb_w * geom_.mb_h;
-    const int ns = common_.max_slices();
+    const int ns = std::max(common_.max_slices(), geom_.mb_h);  // substreams: slices, or CTU rows with WPP
     HevcDeviceBuffers& b = sl.buf;
     HIP_CHECK(hipMalloc(&b.fs, sizeof(HevcFrameState)));
     HIP_CHECK(hipMalloc(&b.me.fs, sizeof(h264::FrameState)));
@@ -25,7 +25,8 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.coef, sizeof(int16_t) * kCoefPerCu * (size_t)ncu));
     // per-slice CABAC output slot: room for 1 KiB per CTU of an even share of the picture plus
     // one CTU row (slices are cost-balanced, so a slice of many cheap CTUs stays small)
-    const size_t ctus_per_slot = (size_t)(ncu + ns - 1) / ns + (size_t)common_.slice_rows() * geom_.mb_w;
+    const size_t ctus_per_slot = std::max((size_t)(ncu + ns - 1) / ns + (size_t)common_.slice_rows() * geom_.mb_w,
+                                          (size_t)geom_.mb_w);
     b.slice_cap = (uint32_t)((ctus_per_slot * 1024 + 15) & ~(size_t)15);
     HIP_CHECK(hipMalloc(&b.slice_data, (size_t)b.slice_cap * ns));
     HIP_CHECK(hipMalloc(&b.slice_len, sizeof(uint32_t) * ns));
@@ -48,6 +49,11 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * h264::kSsePartStride));
     HIP_CHECK(hipMalloc(&b.sse_tot, 4 * sizeof(unsigned long long)));
+    HIP_CHECK(hipMalloc(&b.wpp_ctx, sizeof(uint32_t) * kWppCtxWords * (size_t)geom_.mb_h));
+    HIP_CHECK(hipMalloc(&b.wpp_flag, sizeof(uint32_t) * (size_t)geom_.mb_h));
+    HIP_CHECK(hipMemsetAsync(b.wpp_flag, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
+    HIP_CHECK(hipHostMalloc(&b.wpp_err, sizeof(int), hipHostMallocMapped));
+    *b.wpp_err = 0;
     b.out_bytes = (size_t)ncu * 768;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(HevcFrameState), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(&sl.me_fs_host, sizeof(h264::FrameState), hipHostMallocDefault));
@@ -64,8 +70,9 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
                     (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
                     (void*)b.sse_part, (void*)b.sse_tot, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
-                    (void*)b.tok_dense})
+                    (void*)b.tok_dense, (void*)b.wpp_ctx, (void*)b.wpp_flag})
         if (p) (void)hipFree(p);
+    if (b.wpp_err) (void)hipHostFree(b.wpp_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.me_fs_host) (void)hipHostFree(sl.me_fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);
@@ -167,6 +174,12 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     for (int k = 0; k < 4; ++k) f.mask_c[k] = mask_c_[k];
     f.prev_src = src_keep_[ref];
     f.save_src = src_keep_[cur];
+    f.wpp = cfg_.hevc_wpp ? 1 : 0;
+    if (++wpp_epoch_ == 0) wpp_epoch_ = 1;
+    f.wpp_epoch = wpp_epoch_;
+    f.wpp_ctx = sl.buf.wpp_ctx;
+    f.wpp_flag = sl.buf.wpp_flag;
+    f.wpp_err = sl.buf.wpp_err;
     h264::FrameState& m = *sl.me_fs_host;  // motion search state (shared H.264 kernels)
     m.ref_y = rec_y_[ref];
     m.ref_uv = rec_uv_[ref];
@@ -194,7 +207,8 @@ int GpuHevcEncoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     HIP_CHECK(hipStreamSynchronize(stream_));
     if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
     const HevcOutHeader hdr = *reinterpret_cast<const HevcOutHeader*>(sl.host_out);
-    return hdr.overflow ? (int)sl.buf.out_bytes : (int)(hdr.total_bytes + hdr.num_slices * 12 + 64);
+    // (header records are substreams; the per-NAL allowance counts slices, as the CPU encoder's probe)
+    return hdr.overflow ? (int)sl.buf.out_bytes : (int)(hdr.total_bytes + common_.num_slices() * 12 + 64);
 }
 
 bool GpuHevcEncoder::prepare(bool force_idr) {
@@ -288,18 +302,38 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
         have_ref_ = false;  // reference incomplete: the next frame must be IDR
         throw std::runtime_error("hevc gpu encoder: output overflow");
     }
+    if (*sl.buf.wpp_err) {  // a WPP substream gave up waiting for the row above: contexts unreliable
+        *sl.buf.wpp_err = 0;
+        rc.end_frame(0, sl.idr);
+        have_ref_ = false;
+        throw std::runtime_error("hevc gpu encoder: WPP context hand-off timed out");
+    }
+    // substream records: a slice each, or with WPP one per CTU row, grouped into slices by the
+    // slice-start flag
     const uint32_t* soff = reinterpret_cast<const uint32_t*>(sl.host_out + sizeof(HevcOutHeader));
     const uint32_t* slen = soff + kMaxSlices;
     const uint32_t* saddr = soff + 2 * kMaxSlices;
     const uint8_t* payload = sl.host_out + kOutPayloadOffset;
+    const uint32_t nsub = hdr.num_slices;
     last_slot_ = s;
-    last_first_.assign(saddr, saddr + hdr.num_slices);
-    last_len_.assign(slen, slen + hdr.num_slices);
+    last_first_.resize(nsub);
+    for (uint32_t k = 0; k < nsub; ++k) last_first_[k] = saddr[k] & ~kSubSliceStart;
+    last_len_.assign(slen, slen + nsub);
     au_.clear();
-    au_.reserve(hdr.total_bytes + hdr.total_bytes / 64 + 64 * hdr.num_slices + 256);
+    au_.reserve(hdr.total_bytes + hdr.total_bytes / 64 + 64 * nsub + 256);
     if (sl.idr) common_.write_parameter_sets(au_);
-    for (uint32_t k = 0; k < hdr.num_slices; ++k)
-        common_.write_slice_nal(au_, (int)saddr[k], sl.idr, sl.poc, sl.qp, payload + soff[k], slen[k]);
+    if (!common_.wpp()) {
+        for (uint32_t k = 0; k < nsub; ++k)
+            common_.write_slice_nal(au_, (int)last_first_[k], sl.idr, sl.poc, sl.qp, payload + soff[k], slen[k]);
+    } else {
+        for (uint32_t k = 0; k < nsub;) {
+            uint32_t e = k + 1, n = slen[k];
+            while (e < nsub && !(saddr[e] & kSubSliceStart)) n += slen[e++];
+            common_.write_slice_nal(au_, (int)last_first_[k], sl.idr, sl.poc, sl.qp, payload, n, slen + k, (int)(e - k),
+                                    soff + k);
+            k = e;
+        }
+    }
     stats_.frame_index = rc.frames();
     stats_.idr = sl.idr;
     stats_.qp = sl.qp;

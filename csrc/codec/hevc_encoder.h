@@ -45,9 +45,14 @@ class HevcCommon {
     int poc() const { return rc_.cur_frame_num(); }
     void write_parameter_sets(std::vector<uint8_t>& out) const;
     // One slice segment NAL (slice starting at CTU `addr`): start code, NAL header, header +
-    // payload with emulation prevention.
+    // payload with emulation prevention.  WPP: data holds the slice's substreams back to back,
+    // sub_len[0..nsub) their raw sizes; the header carries their entry points (sizes after
+    // emulation prevention, 7.4.7.1).
+    // sub_off: byte offsets of the substreams in data (nullptr: back to back).
     void write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp, const uint8_t* data,
-                         size_t n) const;
+                         size_t n, const uint32_t* sub_len = nullptr, int nsub = 0,
+                         const uint32_t* sub_off = nullptr) const;
+    bool wpp() const { return config().hevc_wpp != 0; }
     // Slice layout: I pictures one slice per slice_rows() CTU rows (the intra wavefront needs a
     // fixed layout), P pictures cost-balanced raster runs (plan_p_slices).  Returns first CTUs.
     std::vector<int> row_slices() const;
@@ -62,6 +67,13 @@ class HevcCommon {
 
 // Direct vs bin-token CABAC on random slices (hevc_cpu.cpp); returns the slices checked.
 int token_selftest(uint32_t seed, int slices);
+// Entropy-code one slice with wavefront parallel processing (host): every CTU row of the slice is a
+// substream (fresh contexts in the slice's first row -- or when the picture is one CTU wide --
+// else the contexts the row above had after its second CTU), written to `out` back to back;
+// sub_len receives one size per row.  Returns the total bytes.
+uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
+                        int first, int count, int ctb_w, const uint32_t* sao, uint16_t* tok,
+                        std::vector<uint32_t>& sub_len);
 
 class CpuHevcEncoder {
    public:
@@ -137,6 +149,14 @@ struct HevcFrameState {
     // k_hevc_sao's distortion totals (4 channels), accumulated with one atomic per workgroup and
     // channel; zeroed by k_hevc_layout earlier on the same stream
     unsigned long long* sse_tot;
+    // wavefront parallel processing (EncoderConfig::hevc_wpp): one CABAC substream per CTU row; a
+    // row's wave publishes its contexts after its second CTU (wpp_ctx[row][36 words], then
+    // wpp_flag[row] = wpp_epoch with release semantics) and the next row's wave acquires them
+    int32_t wpp;
+    uint32_t wpp_epoch;  // nonzero, new every frame
+    uint32_t* wpp_ctx;
+    uint32_t* wpp_flag;
+    int* wpp_err;  // mapped host word: nonzero if a substream gave up waiting for the row above
 };
 
 struct HevcOutHeader {
@@ -151,7 +171,10 @@ static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligne
 constexpr int kMaxSlices = 1024;
 constexpr size_t kScanTilePad = 4096;  // per-CU scan arrays padded to this (hevc_kernels.hip kScanTile)
 constexpr int kMaxSliceRows = 4;  // CTU rows per slice the intra wavefront kernel supports
-// host buffer: header | slice payload offset[kMaxSlices] | length[] | first CTU[] | payloads
+constexpr int kWppCtxWords = (C_NUM + 3) / 4;  // context states, four per dword
+constexpr uint32_t kSubSliceStart = 0x80000000u;  // substream record: this substream begins a slice
+// host buffer: header | substream payload offset[kMaxSlices] | length[] | first CTU[] | payloads
+// (a substream is a slice without WPP, a CTU row of a slice with it)
 constexpr size_t kOutPayloadOffset = sizeof(HevcOutHeader) + 3 * kMaxSlices * sizeof(uint32_t);
 
 struct HevcDeviceBuffers {
@@ -174,6 +197,9 @@ struct HevcDeviceBuffers {
     uint32_t* ntok;                 // [ncu] token count per CTU
     uint32_t* tok_off;              // [ncu + 1] exclusive prefix of ntok
     uint16_t* tok_dense;            // [ncu * kMaxCuTokens + 512] tokens in decoding order
+    uint32_t* wpp_ctx;              // [ctb_h][kWppCtxWords] context snapshots (WPP)
+    uint32_t* wpp_flag;             // [ctb_h] snapshot-ready epochs
+    int* wpp_err;                   // mapped host word
     size_t out_bytes;
     unsigned long long* sse_part;
     unsigned long long* sse_tot;  // [4] k_hevc_sao distortion totals
@@ -258,7 +284,8 @@ class GpuHevcEncoder final : public VideoEncoder {
     Geometry geom_;
     FrameSlot slots_[kMaxInFlight];
     int next_slot_ = 0, prep_slot_ = 0, last_slot_ = -1;
-    std::vector<uint32_t> last_first_, last_len_;  // slice layout of the last collected picture
+    std::vector<uint32_t> last_first_, last_len_;  // substream layout of the last collected picture
+    uint32_t wpp_epoch_ = 0;
     std::deque<int> inflight_;
     hipEvent_t last_done_ = nullptr;
     uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -24,6 +24,8 @@
 //                  header (lengths, overflow, distortion totals).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <stdexcept>
 
 #include "h264_core.h"
@@ -901,7 +903,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     __shared__ TuBuf tb[kMaxSliceRows];
     __shared__ IntraRefs rf[kMaxSliceRows];
     __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
-    __shared__ int mode_cost[kMaxSliceRows][4];
+    __shared__ int mode_cost[kMaxSliceRows][kNumIntraCands];
     __shared__ int prev_mode[kMaxSliceRows];
     fill_mats(M);
     __syncthreads();
@@ -1006,16 +1008,22 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         if (valid) {
             const int cand_a = al ? prev_mode[wave] : 1;
             const int r = lane >> 2, cb = (lane & 3) * 4;
+            // every candidate's partial SAD first (independent work), then the wave reductions
+            int sad[kNumIntraCands];
+#pragma unroll
             for (int m = 0; m < kNumIntraCands; ++m) {
                 const int md = kIntraCands[m];
-                int sad = 0;
+                sad[m] = 0;
                 for (int j = 0; j < 4; ++j) {
                     const int p = pred_sample(md, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
                     const int d = (int)((sy4 >> (8 * j)) & 0xff) - p;
-                    sad += d < 0 ? -d : d;
+                    sad[m] += d < 0 ? -d : d;
                 }
-                sad = wsum(sad);
-                if (lane == 0) mode_cost[wave][m] = sad + lambda * intra_mode_bits(md, cand_a);
+            }
+#pragma unroll
+            for (int m = 0; m < kNumIntraCands; ++m) {
+                const int s = wsum(sad[m]);
+                if (lane == 0) mode_cost[wave][m] = s + lambda * intra_mode_bits(kIntraCands[m], cand_a);
             }
         }
         __syncthreads();
@@ -1126,8 +1134,8 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     __shared__ uint32_t wtot[16];
     const int tid = threadIdx.x;
     if (tid < 4) fs->sse_tot[tid] = 0ull;  // k_hevc_sao accumulates into these next
-    if (fs->idr) {
-        const int sr = fs->slice_rows, S = fs->num_slices;
+    if (fs->idr || fs->wpp) {  // I: fixed row slices; P with WPP: one slice (a substream per CTU row)
+        const int sr = fs->idr ? fs->slice_rows : ncu / ctb_w, S = fs->idr ? fs->num_slices : 1;
         for (int k = tid; k < S; k += blockDim.x) slice_first[k] = k * sr * ctb_w;
         for (int i = tid; i < ncu; i += blockDim.x) slice_of_cu[i] = (i / ctb_w) / sr;
         if (tid == 0) *nslices = (uint32_t)S;
@@ -1260,7 +1268,8 @@ __global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameSta
     const int first = uni(slice_first[s]);
     const int end = s + 1 < ns ? uni(slice_first[s + 1]) : ncu;
     const int k = i - first;
-    const int qp_prev = k > 0 ? (int)uni((uint32_t)qpy[i - 1]) : fs->qp;
+    const bool wpp = fs->wpp != 0;
+    const int qp_prev = qp_prev_resets(i, k, g.mb_w, wpp) ? fs->qp : (int)uni((uint32_t)qpy[i - 1]);
     const CuInfo c = load_cu(cus, i);
     const CoefArray cf{coef + (size_t)i * kCoefPerCu};
     // lane p binarises part p of the CTU (coding order) into its LDS run
@@ -1274,7 +1283,9 @@ __global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameSta
     });
     BinRec rec;
     rec.start(stage + lane * kPartTokens, kPartTokens);
-    if (have) binarise_part(rec, mine, fs->idr != 0, cus, cf, fs->sao ? sao : nullptr, i, k, end - first, g.mb_w, qp_prev);
+    if (have)
+        binarise_part(rec, mine, fs->idr != 0, cus, cf, fs->sao ? sao : nullptr, i, k, end - first, g.mb_w, qp_prev,
+                      wpp);
     const uint32_t n = have ? min(rec.n, kPartTokens) : 0u;
     uint32_t incl = n;
     for (int o = 1; o < 64; o <<= 1) {
@@ -1381,43 +1392,24 @@ struct LeanCoder {
     }
 };
 
-// One wave per slice: the slice's dense token run through the arithmetic coder.  Tokens arrive
-// 256 at a time (8 bytes per lane, the next chunk in flight while this one is coded) and are
-// read out of the chunk with v_readlane.
+// One wave per substream -- a slice, or with WPP a CTU row of a slice -- running its dense token
+// run through the arithmetic coder.  Tokens arrive 256 at a time (8 bytes per lane, the next chunk
+// in flight while this one is coded) and are read out of the chunk with v_readlane.
+//
+// WPP (9.3.1, 9.3.2.2): a row's wave starts from the contexts the row above had after its second
+// CTU -- unless the row starts its slice or the picture is one CTU wide -- so it first waits for the
+// row above to publish them: lane 0 of the publisher stores the 36 state words and then the frame's
+// epoch into the row's flag with an agent-scope release store; the waiting wave spins on the flag
+// with relaxed loads and, once it holds the epoch, issues an agent-scope acquire fence before
+// reading the words.  Rows are dispatched in
+// order and the publisher never waits on a later row, so the chain always drains; a bounded spin
+// flags a timeout instead of hanging (GpuHevcEncoder::collect throws).
 constexpr uint32_t kTokChunk = 256;
-__global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameState* __restrict__ fs,
-                                                    const uint16_t* __restrict__ dense,
-                                                    const uint32_t* __restrict__ off,
-                                                    const int* __restrict__ slice_first,
-                                                    const uint32_t* __restrict__ nslices,
-                                                    uint8_t* __restrict__ slice_data, uint32_t slice_cap,
-                                                    uint32_t* __restrict__ slice_len,
-                                                    unsigned long long* __restrict__ slice_clk) {
-    const int s = blockIdx.x, lane = threadIdx.x;
-    const int ns = (int)*nslices;
-    if (s >= ns) return;
-    const unsigned long long clk0 = wall_clock64();
-    const int ncu = g.mb_w * g.mb_h;
-    const int first = slice_first[s];
-    const int end = s + 1 < ns ? slice_first[s + 1] : ncu;
-    const uint32_t t0 = uni(off[first]), t1 = uni(off[end]);
-    const int qp = fs->qp;
-    PackedCtx ctx;
-    {
-        const int t = fs->idr ? 0 : 1;
-        uint32_t w = 0;
-        for (int b = 0; b < 4; ++b) {
-            const int j = 4 * lane + b;
-            w |= (j < C_NUM ? (uint32_t)ctx_init_state(kCtxInit[t][j], qp) : 0u) << (8 * b);
-        }
-        ctx.st = w;
-        ctx.lps_row = (uint32_t)kLps[lane][0] | ((uint32_t)kLps[lane][1] << 8) | ((uint32_t)kLps[lane][2] << 16) |
-                      ((uint32_t)kLps[lane][3] << 24);
-        ctx.next = kNextLps[lane];
-        ctx.lane = lane;
-    }
-    LeanCoder lc;
-    lc.e.start(slice_data + (size_t)s * slice_cap, slice_cap);
+constexpr uint32_t kWppSpinLimit = 1u << 22;
+
+__device__ __forceinline__ void arith_run(LeanCoder& lc, PackedCtx& ctx, const uint16_t* __restrict__ dense,
+                                          uint32_t t0, uint32_t t1, int lane) {
+    if (t0 >= t1) return;
     const uint32_t a0 = t0 & ~3u;  // 8-byte aligned chunk starts
     const uint2* src = reinterpret_cast<const uint2*>(dense + a0);
     uint2 cur = src[lane];
@@ -1447,12 +1439,91 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
         }
         cur = nxt;
     }
+}
+
+__global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                    const uint16_t* __restrict__ dense,
+                                                    const uint32_t* __restrict__ off,
+                                                    const int* __restrict__ slice_first,
+                                                    const int* __restrict__ slice_of_cu,
+                                                    const uint32_t* __restrict__ nslices,
+                                                    uint8_t* __restrict__ slice_data, uint32_t slice_cap,
+                                                    uint32_t* __restrict__ slice_len,
+                                                    unsigned long long* __restrict__ slice_clk) {
+    const int u = blockIdx.x, lane = threadIdx.x;
+    const bool wpp = fs->wpp != 0;
+    const int ncu = g.mb_w * g.mb_h;
+    const int nsub = wpp ? g.mb_h : (int)*nslices;
+    if (u >= nsub) return;
+    const unsigned long long clk0 = wall_clock64();
+    int first, end;
+    bool fresh = true, store = false;
+    if (wpp) {
+        first = u * g.mb_w;
+        end = first + g.mb_w;
+        const int s = slice_of_cu[first];
+        fresh = first == slice_first[s] || g.mb_w < 2;
+        store = g.mb_w >= 2 && end < ncu && slice_of_cu[end] == s;
+    } else {
+        const int ns = nsub;
+        first = slice_first[u];
+        end = u + 1 < ns ? slice_first[u + 1] : ncu;
+    }
+    const uint32_t t0 = uni(off[first]), t1 = uni(off[end]);
+    const int qp = fs->qp;
+    PackedCtx ctx;
+    ctx.lps_row = (uint32_t)kLps[lane][0] | ((uint32_t)kLps[lane][1] << 8) | ((uint32_t)kLps[lane][2] << 16) |
+                  ((uint32_t)kLps[lane][3] << 24);
+    ctx.next = kNextLps[lane];
+    ctx.lane = lane;
+    const uint32_t epoch = fs->wpp_epoch;
+    bool sync_ok = true;
+    if (!fresh) {
+        const uint32_t* flag = fs->wpp_flag + (u - 1);
+        uint32_t n = 0;
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++n > kWppSpinLimit) {
+                sync_ok = false;
+                break;
+            }
+        }
+        sync_ok = __builtin_amdgcn_readfirstlane(sync_ok ? 1 : 0) != 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the publisher's release store
+        if (!sync_ok && lane == 0) *fs->wpp_err = 1;
+    }
+    if (!fresh && sync_ok) {
+        ctx.st = lane < kWppCtxWords ? fs->wpp_ctx[(size_t)(u - 1) * kWppCtxWords + lane] : 0u;
+    } else {
+        const int t = fs->idr ? 0 : 1;
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int j = 4 * lane + b;
+            w |= (j < C_NUM ? (uint32_t)ctx_init_state(kCtxInit[t][j], qp) : 0u) << (8 * b);
+        }
+        ctx.st = w;
+    }
+    LeanCoder lc;
+    lc.e.start(slice_data + (size_t)u * slice_cap, slice_cap);
+    if (store) {
+        // the row's first two CTUs, then publish the contexts (storage process after CTU 1)
+        const uint32_t ts = uni(off[first + 2]);
+        arith_run(lc, ctx, dense, t0, ts, lane);
+        if (lane == 0) {
+            uint32_t* dst = fs->wpp_ctx + (size_t)u * kWppCtxWords;
+            for (int k = 0; k < kWppCtxWords; ++k) dst[k] = (uint32_t)__builtin_amdgcn_readlane((int)ctx.st, k);
+            __hip_atomic_store(fs->wpp_flag + u, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        arith_run(lc, ctx, dense, ts, t1, lane);
+    } else {
+        arith_run(lc, ctx, dense, t0, t1, lane);
+    }
     CabacEnc& e = lc.e;
-    e.finish_slice();
+    e.finish_slice();  // flush + the stop / alignment one-bit and zero bits (slice end or end of subset)
     if (lane == 0) {
-        slice_len[s] = e.pos;
-        slice_clk[2 * s] = clk0;  // diagnostics: this wave's span (GpuHevcEncoder::slice_timing)
-        slice_clk[2 * s + 1] = wall_clock64();
+        slice_len[u] = e.pos;
+        slice_clk[2 * u] = clk0;  // diagnostics: this wave's span (GpuHevcEncoder::slice_timing)
+        slice_clk[2 * u + 1] = wall_clock64();
     }
 }
 
@@ -1461,15 +1532,17 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
 // that coded a residual, else the slice QP.  One workgroup per slice; qpc holds (QP or 255) per
 // CU from the analysis kernels; a block max-scan of (index << 8 | QP) over 256-CU chunks with
 // the previous chunk's maximum carried in.
+// With WPP the chain restarts at every CTU row (8.6.1), so the workgroups take rows instead.
 __global__ __launch_bounds__(256) void k_hevc_qpy(const HevcFrameState* __restrict__ fs,
-                                                   const uint8_t* __restrict__ qpc, int ncu,
+                                                   const uint8_t* __restrict__ qpc, int ncu, int ctb_w,
                                                    const int* __restrict__ slice_first,
                                                    const uint32_t* __restrict__ nslices, uint8_t* __restrict__ qpy) {
     __shared__ int wmaxv[4];
     const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ns = (int)*nslices;
+    const int ns = fs->wpp ? ncu / ctb_w : (int)*nslices;
     if (s >= ns) return;
-    const int first = slice_first[s], end = s + 1 < ns ? slice_first[s + 1] : ncu;
+    const int first = fs->wpp ? s * ctb_w : slice_first[s];
+    const int end = fs->wpp ? first + ctb_w : (s + 1 < ns ? slice_first[s + 1] : ncu);
     int carry = -1;
     for (int base = first; base < end; base += 256) {
         const int i = base + tid;
@@ -1837,16 +1910,21 @@ __global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameSta
 }
 
 // ------------------------------------------------------------------ pack
-__global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restrict__ fs,
+// One workgroup per substream (a slice, or with WPP a CTU row): its payload to a 16-byte aligned
+// place in the host buffer, and its (offset, length, first CTU | kSubSliceStart when it begins a
+// slice) record; workgroup 0 also writes the header.
+__global__ __launch_bounds__(256) void k_hevc_pack(Geometry g, const HevcFrameState* __restrict__ fs,
                                                     const uint32_t* __restrict__ nslices,
                                                     const int* __restrict__ slice_first,
+                                                    const int* __restrict__ slice_of_cu,
                                                     const uint8_t* __restrict__ slice_data,
                                                     uint32_t slice_cap, const uint32_t* __restrict__ slice_len,
                                                     uint8_t* __restrict__ host_out, size_t out_bytes) {
     __shared__ uint32_t red[256];
     __shared__ unsigned long long red64[4][256];
     const int s = blockIdx.x, tid = threadIdx.x;
-    const int num_slices = (int)*nslices;
+    const bool wpp = fs->wpp != 0;
+    const int num_slices = wpp ? g.mb_h : (int)*nslices;  // substreams
     if (s >= num_slices) return;
     // offset of this slice: sum of the 16-byte rounded lengths before it
     uint32_t part = 0;
@@ -1869,7 +1947,9 @@ __global__ __launch_bounds__(256) void k_hevc_pack(const HevcFrameState* __restr
         uint32_t* offs = reinterpret_cast<uint32_t*>(host_out + sizeof(HevcOutHeader));
         offs[s] = off;
         offs[kMaxSlices + s] = len;
-        offs[2 * kMaxSlices + s] = (uint32_t)slice_first[s];
+        const int fc = wpp ? s * g.mb_w : slice_first[s];
+        const bool starts = !wpp || slice_first[slice_of_cu[fc]] == fc;
+        offs[2 * kMaxSlices + s] = (uint32_t)fc | (starts ? kSubSliceStart : 0u);
     }
     if (s != 0) return;
     // header: totals, overflow, distortion
@@ -1962,8 +2042,8 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
         hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
                            b.slice_of_cu, b.cu);
     // QpY chain: the deblocking filter's QP and the entropy coder's QP predictor
-    hipLaunchKernelGGL(k_hevc_qpy, dim3(max_slices), dim3(256), 0, s, b.fs, b.qpc, ncu, b.slice_first, b.nslices,
-                       b.qpy);
+    hipLaunchKernelGGL(k_hevc_qpy, dim3(std::max(max_slices, g.mb_h)), dim3(256), 0, s, b.fs, b.qpc, ncu, g.mb_w,
+                       b.slice_first, b.nslices, b.qpy);
     if (deblock) {
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
@@ -1983,10 +2063,11 @@ void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_
     hipLaunchKernelGGL(k_hevc_tokscan, dim3(1), dim3(1024), 0, s, b.ntok, ncu, b.tok_off);
     hipLaunchKernelGGL(k_hevc_tokgather, dim3((ncu + 3) / 4), dim3(256), 0, s, b.tok, b.ntok, b.tok_off, ncu,
                        b.tok_dense);
-    hipLaunchKernelGGL(k_hevc_arith, dim3(max_slices), dim3(64), 0, s, g, b.fs, b.tok_dense, b.tok_off,
-                       b.slice_first, b.nslices, b.slice_data, b.slice_cap, b.slice_len, b.slice_clk);
-    hipLaunchKernelGGL(k_hevc_pack, dim3(max_slices), dim3(256), 0, s, b.fs, b.nslices, b.slice_first, b.slice_data,
-                       b.slice_cap, b.slice_len, host_out, b.out_bytes);
+    const int max_subs = std::max(max_slices, g.mb_h);  // substreams: slices, or CTU rows with WPP
+    hipLaunchKernelGGL(k_hevc_arith, dim3(max_subs), dim3(64), 0, s, g, b.fs, b.tok_dense, b.tok_off,
+                       b.slice_first, b.slice_of_cu, b.nslices, b.slice_data, b.slice_cap, b.slice_len, b.slice_clk);
+    hipLaunchKernelGGL(k_hevc_pack, dim3(max_subs), dim3(256), 0, s, g, b.fs, b.nslices, b.slice_first, b.slice_of_cu,
+                       b.slice_data, b.slice_cap, b.slice_len, host_out, b.out_bytes);
 }
 
 }  // namespace hevc

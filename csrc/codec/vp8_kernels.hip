@@ -404,7 +404,7 @@ __device__ __forceinline__ void wait_row(const uint32_t* p, uint32_t epoch, int 
         }
         __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the edge words are read with sc1 loads
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
 }
 
 __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8States* __restrict__ st,
@@ -529,9 +529,10 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
             __hip_atomic_store((gu64*)(my_line + wi), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (!bottom) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // hand-off drained before the flag
+            // every lane's hand-off words ordered before the flag: agent-scope release fence + store
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             if (lane == 0)
-                __hip_atomic_store((gu32*)(prog + mby), (epoch << 12) | (uint32_t)(mbx + 1), __ATOMIC_RELAXED,
+                __hip_atomic_store((gu32*)(prog + mby), (epoch << 12) | (uint32_t)(mbx + 1), __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
         uint32_t sse[3];

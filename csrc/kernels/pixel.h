@@ -21,7 +21,14 @@ struct SynthParams {
     int noise;              // 1 = animated-noise panel on
     int cursor_x, cursor_y; // remote cursor position (-1 = hidden)
     uint64_t* ts = nullptr; // if set: device wall clock at the render's start (frame GPU time)
+    // 0: the desktop (static windows + animated elements); 1: motion content -- the whole desktop
+    // pans (3 px right, 1 px down per frame at 60 fps, wrapping) under a screen-fixed video-like
+    // panel of smooth, colourful, non-rigidly moving texture (kVideo* rectangle), as games and
+    // video playback look to the encoder; the barcode stays put
+    int content = 0;
 };
+// video panel of the motion content, fractions of the wall (screen coordinates)
+constexpr float kVideoX = 0.60f, kVideoY = 0.56f, kVideoW = 0.34f, kVideoH = 0.36f;
 
 // Barcode geometry: 64 bits (frame_id, timestamp_us), 8x8-pixel cells, two rows of 32
 // cells, drawn at the top-left of the desktop with a one-cell quiet zone.

@@ -130,10 +130,54 @@ __device__ __forceinline__ FrameConsts frame_consts(const SynthParams& p) {
     return f;
 }
 
+// ---- motion content (SynthParams::content 1)
+__device__ __forceinline__ bool in_barcode(int gx, int gy) {
+    return gy >= kBarY - kBarCell && gy < kBarY + 3 * kBarCell && gx >= kBarX - kBarCell && gx < kBarX + 33 * kBarCell;
+}
+__device__ __forceinline__ void video_rect(const SynthParams& p, int* x0, int* y0, int* x1, int* y1) {
+    *x0 = (int)(p.wall_w * kVideoX);
+    *y0 = (int)(p.wall_h * kVideoY);
+    *x1 = *x0 + (int)(p.wall_w * kVideoW);
+    *y1 = *y0 + (int)(p.wall_h * kVideoH);
+}
+// pan offset of frame time t: 3 px / frame right, 1 px / frame down at 60 fps (integer, wrapping)
+__device__ __forceinline__ void pan_of(const SynthParams& p, int* px, int* py) {
+    const int f = (int)(p.t * 60.f + 0.5f);
+    *px = (3 * f) % p.wall_w;
+    *py = f % p.wall_h;
+}
+// smooth value noise: bilinear, smoothstep-weighted interpolation of a hashed integer lattice
+__device__ __forceinline__ float vnoise(float x, float y, uint32_t seed) {
+    const float fx = floorf(x), fy = floorf(y);
+    const int ix = (int)fx, iy = (int)fy;
+    float u = x - fx, v = y - fy;
+    u = u * u * (3.f - 2.f * u);
+    v = v * v * (3.f - 2.f * v);
+    const float a = (float)(hash3((uint32_t)ix, (uint32_t)iy, seed) & 1023u);
+    const float b = (float)(hash3((uint32_t)ix + 1u, (uint32_t)iy, seed) & 1023u);
+    const float c = (float)(hash3((uint32_t)ix, (uint32_t)iy + 1u, seed) & 1023u);
+    const float d = (float)(hash3((uint32_t)ix + 1u, (uint32_t)iy + 1u, seed) & 1023u);
+    return ((a + (b - a) * u) + ((c + (d - c) * u) - (a + (b - a) * u)) * v) * (1.f / 1023.f);
+}
+// video-like texture at panel coordinates (u, v): three octaves of value noise drifting at
+// different speeds (so the motion is not one translation), mapped through phase-shifted colour
+// waves that also cycle slowly
+__device__ uint32_t video_px(int u, int v, float t) {
+    const float x = u * (1.f / 96.f), y = v * (1.f / 96.f);
+    const float n = 0.55f * vnoise(x + 0.35f * t, y + 0.12f * t, 11u) +
+                    0.30f * vnoise(2.1f * x - 0.6f * t, 2.1f * y + 0.25f * t, 23u) +
+                    0.15f * vnoise(4.3f * x + 0.9f * t, 4.3f * y - 0.7f * t, 37u);
+    const float ph = 6.2831853f * n;
+    const int r = (int)(128.f + 100.f * __sinf(ph + 0.4f * t));
+    const int g = (int)(128.f + 90.f * __sinf(1.3f * ph + 2.1f));
+    const int b = (int)(128.f + 100.f * __sinf(0.8f * ph + 4.2f - 0.3f * t));
+    return bgrx(r, g, b);
+}
+
 __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p, const FrameConsts& fc) {
     const int W = p.wall_w, H = p.wall_h;
     // ---- barcode (frame id + timestamp), always on top
-    if (gy >= kBarY - kBarCell && gy < kBarY + 2 * kBarCell + kBarCell && gx >= kBarX - kBarCell &&
+    if (p.content == 0 && gy >= kBarY - kBarCell && gy < kBarY + 2 * kBarCell + kBarCell && gx >= kBarX - kBarCell &&
         gx < kBarX + 32 * kBarCell + kBarCell) {
         const int cx = (gx - kBarX), cy = (gy - kBarY);
         if (cx < 0 || cy < 0 || cx >= 32 * kBarCell || cy >= 2 * kBarCell) return bgrx(96, 96, 96);  // quiet zone
@@ -247,6 +291,31 @@ __device__ __attribute__((noinline)) uint32_t static_px(int gx, int gy, const Sy
     return bgrx((int)(20 + 40 * fy + 20 * band), (int)(40 + 60 * fy + 10 * band), (int)(90 + 110 * (1.f - fy * 0.5f)));
 }
 
+// barcode pixel (frame id + timestamp) at screen coordinates inside in_barcode()
+__device__ __forceinline__ uint32_t barcode_px(int gx, int gy, const SynthParams& p) {
+    const int cx = (gx - kBarX), cy = (gy - kBarY);
+    if (cx < 0 || cy < 0 || cx >= 32 * kBarCell || cy >= 2 * kBarCell) return bgrx(96, 96, 96);  // quiet zone
+    const int bit = 31 - cx / kBarCell;
+    const uint32_t word = (cy / kBarCell) == 0 ? p.frame_id : p.timestamp_us;
+    const int v = ((word >> bit) & 1) ? 255 : 0;
+    return bgrx(v, v, v);
+}
+
+// Motion content: screen pixel (gx, gy) -- barcode and video panel screen-fixed, the rest the
+// panned desktop (static layer from the cache when given).
+__device__ __forceinline__ uint32_t motion_px(int gx, int gy, const SynthParams& p, const FrameConsts& fc,
+                                              const uint8_t* __restrict__ bg, int px, int py, int vx0, int vy0,
+                                              int vx1, int vy1, const DynBoxes& boxes) {
+    if (in_barcode(gx, gy)) return barcode_px(gx, gy, p);
+    if (gx >= vx0 && gx < vx1 && gy >= vy0 && gy < vy1) return video_px(gx - vx0, gy - vy0, p.t);
+    int dx = gx + px, dy = gy + py;
+    dx -= dx >= p.wall_w ? p.wall_w : 0;
+    dy -= dy >= p.wall_h ? p.wall_h : 0;
+    if (bg != nullptr && p.origin_x == 0 && p.origin_y == 0 && !in_dyn(boxes, dx, 1, dy))
+        return *reinterpret_cast<const uint32_t*>(bg + (size_t)dy * p.pitch + 4 * dx);
+    return desktop_px(dx, dy, p, fc);
+}
+
 // bg: the session's static-layer cache (same size / pitch / origin), or nullptr.
 __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const SynthParams& p,
                                            const uint8_t* __restrict__ bg) {
@@ -257,6 +326,21 @@ __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const Synt
     uint32_t v[4];
     const int gx = p.origin_x + x4, gy = p.origin_y + y;
     const FrameConsts fc = frame_consts(p);
+    if (p.content == 1) {
+        int px, py, vx0, vy0, vx1, vy1;
+        pan_of(p, &px, &py);
+        video_rect(p, &vx0, &vy0, &vx1, &vy1);
+        const DynBoxes boxes = dyn_boxes(p, fc.wx, fc.wy, fc.mw, fc.mh);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = (x4 + k < p.width) ? motion_px(gx + k, gy, p, fc, bg, px, py, vx0, vy0, vx1, vy1, boxes) : 0u;
+        uint32_t* row = reinterpret_cast<uint32_t*>(out + (size_t)y * p.pitch);
+        if (x4 + 4 <= p.width)
+            *reinterpret_cast<uint4*>(row + x4) = make_uint4(v[0], v[1], v[2], v[3]);
+        else
+            for (int k = 0; k < 4 && x4 + k < p.width; ++k) row[x4 + k] = v[k];
+        return;
+    }
     if (bg != nullptr && x4 + 4 <= p.width && !in_dyn(dyn_boxes(p, fc.wx, fc.wy, fc.mw, fc.mh), gx, 4, gy)) {
         const uint4 c = *reinterpret_cast<const uint4*>(bg + (size_t)y * p.pitch + 4 * x4);
         v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;

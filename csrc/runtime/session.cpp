@@ -269,6 +269,7 @@ pix::SynthParams Session::synth_params() {
     p.wall_w = cfg_.width;
     p.wall_h = cfg_.height;
     p.noise = cfg_.noise;
+    p.content = cfg_.content;
     p.cursor_x = cursor_x_;
     p.cursor_y = cursor_y_;
     return p;

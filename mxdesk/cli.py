@@ -119,6 +119,10 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
 
     if cfg.source == "x11":
         raise SystemExit("serve --sessions K > 1 streams synthetic desktops; MXDESK_SOURCE=x11 serves one")
+    if cfg.novnc_enable:
+        # the RFB fallback front end exists per single session (cmd_serve); K WebRTC sessions
+        # with NOVNC_ENABLE set would silently serve the wrong front end
+        raise SystemExit("serve --sessions K > 1 serves WebRTC sessions; NOVNC_ENABLE=true needs a single session")
     # every session drives two HIP streams; with HIP's default of 4 hardware queues per process,
     # K sessions' streams share 4 queues and serialise behind each other.  Must be set before
     # the HIP runtime initialises (the first pipeline below); an explicit setting wins.
@@ -132,7 +136,9 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
         ci = session_config(cfg, i)
         pipe = build_pipeline(ci, device, session_name=str(i), capture_allowed=False)
         pipe.pace_phase = i / (k * max(1.0, float(ci.stream_fps)))  # spread the K sessions over the period
-        servers.append(MediaServer(pipe, ci))
+        # input of a synthetic session drives its own cursor (make_injector -> MediaServer's
+        # SyntheticInjector), as in single-session serve
+        servers.append(MediaServer(pipe, ci, injector=make_injector(ci, pipe)))
     print(f"mxdesk: serving {k} sessions {cfg.sizew}x{cfg.sizeh}@{cfg.stream_fps} ({cfg.encoder_backend}) on "
           f"{cfg.addr}:{cfg.port}..{cfg.port + k - 1}", flush=True)
     run_forever_multi(servers, cfg.addr, [cfg.port + i for i in range(k)], ssl_context(cfg))

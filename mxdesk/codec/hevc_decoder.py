@@ -172,6 +172,19 @@ def split_nal_units(stream: bytes) -> list[bytes]:
     return out
 
 
+def escape(rbsp: bytes) -> bytes:
+    """Emulation prevention (7.4.2): 0x03 after two zero bytes before a byte <= 3."""
+    out = bytearray()
+    zeros = 0
+    for b in rbsp:
+        if zeros >= 2 and b <= 3:
+            out.append(3)
+            zeros = 0
+        out.append(b)
+        zeros = zeros + 1 if b == 0 else 0
+    return bytes(out)
+
+
 def unescape(nal: bytes) -> bytes:
     out = bytearray()
     zeros = 0
@@ -395,8 +408,8 @@ def parse_pps(rbsp: bytes) -> PPS:
     p.transquant_bypass = r.u(1)
     p.tiles = r.u(1)
     p.entropy_sync = r.u(1)
-    if p.tiles or p.entropy_sync:
-        raise NotImplementedError("tiles / WPP")
+    if p.tiles:
+        raise NotImplementedError("tiles")
     p.loop_filter_across_slices = r.u(1)
     if r.u(1):  # deblocking_filter_control_present_flag
         p.deblocking_override_enabled = r.u(1)
@@ -415,7 +428,16 @@ def parse_pps(rbsp: bytes) -> PPS:
 class Cabac:
     def __init__(self, data: bytes, byte_pos: int, slice_type: int, qp: int, cabac_init_flag: int = 0):
         self.data = data
+        self.init_contexts(slice_type, qp, cabac_init_flag)
+        self.init_engine(byte_pos)
+
+    def init_engine(self, byte_pos: int) -> None:
+        """Arithmetic decoding engine initialisation (9.3.2.5) at a byte position."""
         self.pos = byte_pos * 8
+        self.range = 510
+        self.offset = self.bits(9)
+
+    def init_contexts(self, slice_type: int, qp: int, cabac_init_flag: int = 0) -> None:
         init_type = 0 if slice_type == 2 else (2 if cabac_init_flag else 1) if slice_type == 1 else (
             1 if cabac_init_flag else 2)
         self.ctx: dict[str, list[list[int]]] = {}
@@ -428,8 +450,23 @@ class Cabac:
                 pre = min(max(((m * qpc) >> 4) + n, 1), 126)
                 states.append([pre - 64, 1] if pre > 63 else [63 - pre, 0])
             self.ctx[name] = states
-        self.range = 510
-        self.offset = self.bits(9)
+
+    def save_contexts(self) -> dict:
+        return {k: [list(s) for s in v] for k, v in self.ctx.items()}
+
+    def restore_contexts(self, saved: dict) -> None:
+        self.ctx = {k: [list(s) for s in v] for k, v in saved.items()}
+
+    def end_substream(self) -> int:
+        """After end_of_subset_one_bit == 1: the last bit read is alignment_bit_equal_to_one, zero
+        bits follow up to the byte boundary; returns the byte position of the next substream."""
+        last = self.pos - 1
+        if (self.data[last >> 3] >> (7 - (last & 7))) & 1 != 1:
+            raise ValueError("substream does not end with alignment_bit_equal_to_one")
+        while self.pos & 7:
+            if self.bit():
+                raise ValueError("nonzero alignment bit after a substream")
+        return self.pos >> 3
 
     def bit(self) -> int:
         i = self.pos >> 3
@@ -876,6 +913,12 @@ class Decoder:
         lf_across = p.loop_filter_across_slices
         if p.loop_filter_across_slices and (sao_luma or sao_chroma or not db_disabled):
             lf_across = r.u(1)
+        entry = []
+        if p.entropy_sync:
+            n_entry = r.ue()
+            if n_entry:
+                olen = r.ue() + 1
+                entry = [r.u(olen) + 1 for _ in range(n_entry)]
         self.slice_params[addr] = {"db_disabled": db_disabled, "lf_across": lf_across,
                                    "sao_luma": sao_luma, "sao_chroma": sao_chroma,
                                    "beta_offset": 2 * p.beta_offset_div2, "tc_offset": 2 * p.tc_offset_div2}
@@ -888,17 +931,46 @@ class Decoder:
         self.qp_prev = slice_qp
         cab = Cabac(rbsp, r.pos >> 3, slice_type, slice_qp)
         ctb = addr
+        sub_starts = [r.pos >> 3]  # rbsp byte position of every substream (WPP)
+        wpp_saved = None
         while True:
             cx, cy = ctb % ctbs_w, ctb // ctbs_w
+            if p.entropy_sync and cx == 0 and ctb != addr:
+                # 9.3.1: the contexts of a CTU row's first CTB come from the row above after its
+                # second CTB when the top-right CTB is available (same slice), else fresh
+                tr_ok = ctbs_w >= 2 and (ctb - ctbs_w + 1) >= addr
+                if tr_ok and wpp_saved is not None:
+                    cab.restore_contexts(wpp_saved)
+                else:
+                    cab.init_contexts(slice_type, slice_qp)
+                wpp_saved = None
+                self.qp_prev = slice_qp  # 8.6.1: first QG of a CTB row with WPP
             if sao_luma or sao_chroma:
                 self._sao_syntax(cab, ctb, ctbs_w, addr, sao_luma, sao_chroma)
             self._coding_quadtree(cab, cx << s.log2_ctb, cy << s.log2_ctb, s.log2_ctb, 0)
+            if p.entropy_sync and cx == 1:
+                wpp_saved = cab.save_contexts()  # storage after the row's second CTB (9.3.2.2)
             if cab.terminate():
                 cab.check_slice_end()
                 break
             ctb += 1
             if ctb >= ctbs_w * ctbs_h:
                 raise ValueError("slice runs past the last CTB")
+            if p.entropy_sync and ctb % ctbs_w == 0:
+                if not cab.terminate():
+                    raise ValueError("end_of_subset_one_bit is not 1")
+                nxt = cab.end_substream()
+                sub_starts.append(nxt)
+                cab.init_engine(nxt)
+        if p.entropy_sync:
+            # entry points = substream sizes after emulation prevention (7.4.7.1)
+            if len(entry) != len(sub_starts) - 1:
+                raise ValueError(f"{len(entry)} entry points for {len(sub_starts)} substreams")
+            for k, e in enumerate(entry):
+                got = len(escape(rbsp[sub_starts[k]:sub_starts[k + 1]]))
+                if got != e:
+                    raise ValueError(f"entry point {k}: {e} bytes signalled, substream is {got}")
+            self.stats["substreams"] = self.stats.get("substreams", 0) + len(sub_starts)
 
     # ---------------------------------------------------------------- availability (6.4.1)
     def _avail(self, xc: int, yc: int, xn: int, yn: int) -> bool:

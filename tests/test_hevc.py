@@ -84,7 +84,30 @@ def test_cpu_hevc_two_row_slices(native):
     # exercises above-neighbour intra references, merge/AMVP B candidates and skip contexts
     _, _, _, dec, enc = _cpu_roundtrip(native, 352, 288, 2, fps=30, qp=30)
     assert enc.slice_rows == 2
-    assert dec.stats["slices"] > 9  # 9 two-row slices in the IDR picture, cost-balanced ones in P
+    assert dec.stats["slices"] >= 10  # 9 two-row slices in the IDR picture, one WPP slice per P picture
+    assert dec.stats["substreams"] == 18 + 18  # one per CTU row: 9 slices x 2 rows, then 18 rows
+
+
+@pytest.mark.parametrize("w,h,wpp", [(16, 64, 1), (32, 48, 1), (160, 96, 1), (160, 96, 0), (200, 120, 1)])
+def test_cpu_hevc_wpp_substreams_decode(native, w, h, wpp):
+    """Wavefront substreams (one per CTU row; context sync from the row above's second CTU, none
+    for a one-CTU-wide picture; QP predictor reset per row; entry points = escaped substream
+    sizes, checked by the decoder) decode to the reconstruction, I and P pictures, with the
+    slice-per-substream layout (wpp 0) as the control."""
+    cfg = _cfg(native, w, h, qp=26, aq=1)
+    cfg.hevc_wpp = wpp
+    enc = native.CpuHevcEncoder(cfg)
+    stream, recon = b"", []
+    for t in range(4):
+        y, uv = synthetic_nv12(w, h, t, seed=t)
+        stream += enc.encode(y, uv, t == 2)
+        recon.append(tuple(p.copy() for p in enc.recon()))
+    dec = Decoder()
+    dec.decode(stream)
+    for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
+        assert np.array_equal(yy, ry) and np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
+    rows = (h + 15) // 16
+    assert dec.stats.get("substreams", 0) == (4 * rows if wpp else 0)
 
 
 def test_cpu_hevc_cost_balanced_p_slices(native):
@@ -94,7 +117,9 @@ def test_cpu_hevc_cost_balanced_p_slices(native):
     from mxdesk.codec import hevc_decoder as hd
 
     w, h = 320, 192
-    enc = native.CpuHevcEncoder(_cfg(native, w, h, qp=22, aq=0))
+    cfg = _cfg(native, w, h, qp=22, aq=0)
+    cfg.hevc_wpp = 0  # cost-balanced slices are the layout without wavefront substreams
+    enc = native.CpuHevcEncoder(cfg)
     rng = np.random.default_rng(5)
     stream, recon = b"", []
     for t in range(3):
