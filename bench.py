@@ -184,6 +184,8 @@ def main() -> None:
                     help="HEVC P-picture slice work target (more = fewer, longer slices)")
     ap.add_argument("--hevc-wpp", type=int, default=None,
                     help="HEVC wavefront substreams (1, default) or cost-balanced slices (0)")
+    ap.add_argument("--hevc-wpp-rows", type=int, default=None,
+                    help="HEVC with WPP: CTU rows per P slice (0 = one slice per picture)")
     ap.add_argument("--search-range", type=int, default=16)
     ap.add_argument("--subpel", type=int, default=1)
     ap.add_argument("--me-coarse", type=int, default=None,
@@ -267,6 +269,8 @@ def main() -> None:
         cfg.enc.hevc_slice_cost = args.hevc_slice_cost
     if args.hevc_wpp is not None:
         cfg.enc.hevc_wpp = args.hevc_wpp
+    if args.hevc_wpp_rows is not None:
+        cfg.enc.hevc_wpp_rows = args.hevc_wpp_rows
     if args.intra_in_p is not None:
         cfg.enc.intra_in_p = args.intra_in_p
     if args.deblock is not None:

@@ -165,6 +165,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("tu_split", &h264::EncoderConfig::tu_split)
         .def_readwrite("hevc_slice_cost", &h264::EncoderConfig::hevc_slice_cost)
         .def_readwrite("hevc_wpp", &h264::EncoderConfig::hevc_wpp)
+        .def_readwrite("hevc_wpp_rows", &h264::EncoderConfig::hevc_wpp_rows)
         .def_readwrite("sao", &h264::EncoderConfig::sao);
 
     py::class_<h264::FrameStats>(m, "FrameStats")

@@ -611,6 +611,7 @@ MXHD int chroma_pred8(const uint8_t* uv, int pitch, int cw, int ch, int comp, in
         y = y < 0 ? 0 : (y >= ch ? ch - 1 : y);
         return (int)uv[y * pitch + 2 * x + comp];
     };
+    if ((xf | yf) == 0) return g(xi, yi);  // full-sample vector: the weights are 64, 0, 0, 0
     const int A = g(xi, yi), B = g(xi + 1, yi), C = g(xi, yi + 1), D = g(xi + 1, yi + 1);
     return ((8 - xf) * (8 - yf) * A + xf * (8 - yf) * B + (8 - xf) * yf * C + xf * yf * D + 32) >> 6;
 }

@@ -61,6 +61,11 @@ struct EncoderConfig {
     // every CTU row its own CABAC substream (one GPU wave each) that starts from the contexts the row
     // above had after its second CTU; 0: cost-balanced slices, one substream per slice
     int hevc_wpp = 1;
+    // HEVC with WPP: CTU rows per P slice (0 = the whole picture).  A substream row is a serial
+    // chain and a slice's rows start two CTUs apart, so a slice of R rows takes ~2R + row-length
+    // CTU times: short slices keep the wavefront's fill out of the frame time (at 4K one slice
+    // took ~3 ms of CABAC waves, 8-row slices ~1.4 ms; profiles/r04_hevc)
+    int hevc_wpp_rows = 8;
     int sao = 1;              // HEVC: sample adaptive offset (8.7.3), band / edge offsets decided per CTB
     // quality report: luma distortion outside the macroblocks touching this pixel rectangle
     // (FrameStats::sse_masked; mask_x1 <= mask_x0 = no mask)

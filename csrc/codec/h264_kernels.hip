@@ -285,10 +285,10 @@ constexpr int kMaxRange = 32;
 static_assert(kMaxRange + 2 <= kHpelPad, "search window must stay inside the padded planes");
 constexpr int kWinStride = 16 + 2 * kMaxRange + 8;  // bytes per LDS window row (dword padded)
 
-// Five waves: the +-16 search is 33 x 9 = 297 candidate tasks (four adjacent offsets each), one
-// pass of 320 threads instead of 1.16 passes of 256 (the second pass ran 41 tasks on a full
-// workgroup); the refinement phases below are laid out for 256 threads and leave wave 4 idle.
-constexpr int kMeThreads = 320, kMeWaves = kMeThreads / 64;
+// Four waves.  (Five -- the +-16 search's 297 candidate tasks in one pass of 320 threads instead
+// of 1.16 passes of 256 -- measured slower: 45 -> 54 us at 1080p, 78 -> 110 us at 4K, the larger
+// workgroups costing more in occupancy than the shorter second pass saved: profiles/r04_h264.)
+constexpr int kMeThreads = 256, kMeWaves = kMeThreads / 64;
 __global__ __launch_bounds__(kMeThreads) void k_me_full(Geometry g, const FrameState* __restrict__ fs,
                                                   const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs) {
     __shared__ uint32_t win32[(16 + 2 * kMaxRange) * kWinStride / 4];
@@ -813,17 +813,44 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
             // temporal class (h264_mb.h temporal_class): the source against the previous source,
             // displaced by the vector's integer part; this MB's source becomes the next frame's
             const int ix = mvx >> 2, iy = mvy >> 2;
-            for (int k = 0; k < 4; ++k)
-                tsad += abs((int)((sw >> (8 * k)) & 0xff) -
-                            ref_px(fs->prev_src, g.pitch, g.coded_w, g.coded_h, x0 + c0 + k + ix, y0 + r + iy));
+            const int px = x0 + c0 + ix, py = y0 + r + iy;
+            // inside the picture (no clamping): the 4 samples from one aligned dword, or two when
+            // unaligned and the second stays inside the row's pitch
+            if (px >= 0 && px + 4 <= g.coded_w && py >= 0 && py < g.coded_h &&
+                ((px & 3) == 0 || (px & ~3) + 8 <= g.pitch)) {
+                const uint32_t* qa = reinterpret_cast<const uint32_t*>(fs->prev_src + (size_t)py * g.pitch + (px & ~3));
+                const uint32_t sh = (uint32_t)(px & 3);
+                const uint32_t pw = sh ? __builtin_amdgcn_alignbyte(qa[1], qa[0], sh) : qa[0];
+                tsad = (int)__builtin_amdgcn_sad_u8(sw, pw, 0u);
+            } else {
+                for (int k = 0; k < 4; ++k)
+                    tsad += abs((int)((sw >> (8 * k)) & 0xff) -
+                                ref_px(fs->prev_src, g.pitch, g.coded_w, g.coded_h, x0 + c0 + k + ix, y0 + r + iy));
+            }
             *reinterpret_cast<uint32_t*>(fs->save_src + (y0 + r) * g.pitch + x0 + c0) = sw;
         }
-        for (int k = 0; k < 4; ++k) {
-            const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
-            const int d = (int)((sw >> (8 * k)) & 0xff) - p;
-            pred[wave][r * 16 + c0 + k] = (uint8_t)p;
-            res[wave][r * 16 + c0 + k] = (int16_t)d;
-            lsad += d < 0 ? -d : d;
+        if (((mvx | mvy) & 3) == 0) {
+            // full-sample vector (static desktop, scrolled text): the 4 predictions are 4 bytes of the
+            // padded full-sample plane, from two aligned dwords instead of 4 byte gathers
+            const uint8_t* q = P.f + (size_t)((y0 + r) + (mvy >> 2)) * P.pitch + (x0 + c0 + (mvx >> 2));
+            const uint32_t* qa = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(q) & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(q) & 3);
+            const uint32_t pw = sh ? __builtin_amdgcn_alignbyte(qa[1], qa[0], sh) : qa[0];
+            for (int k = 0; k < 4; ++k) {
+                const int p = (int)((pw >> (8 * k)) & 0xff);
+                const int d = (int)((sw >> (8 * k)) & 0xff) - p;
+                pred[wave][r * 16 + c0 + k] = (uint8_t)p;
+                res[wave][r * 16 + c0 + k] = (int16_t)d;
+                lsad += d < 0 ? -d : d;
+            }
+        } else {
+            for (int k = 0; k < 4; ++k) {
+                const int p = qpel_planes(P, (x0 + c0 + k) * 4 + mvx, (y0 + r) * 4 + mvy);
+                const int d = (int)((sw >> (8 * k)) & 0xff) - p;
+                pred[wave][r * 16 + c0 + k] = (uint8_t)p;
+                res[wave][r * 16 + c0 + k] = (int16_t)d;
+                lsad += d < 0 ? -d : d;
+            }
         }
         const int cr_ = lane >> 3, cc = lane & 7;
         const int xc = x0 / 2 + cc, yc = y0 / 2 + cr_;

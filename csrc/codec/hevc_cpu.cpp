@@ -111,7 +111,11 @@ std::vector<int> HevcCommon::row_slices() const {
 }
 
 std::vector<int> HevcCommon::plan_p_slices(const std::vector<CuInfo>& cus) const {
-    if (wpp()) return {0};  // one slice, one substream per CTU row
+    if (wpp()) {  // slices of wpp_rows() CTU rows, one substream per CTU row
+        std::vector<int> f;
+        for (int y = 0; y < ctb_h(); y += wpp_rows()) f.push_back(y * ctb_w());
+        return f;
+    }
     uint64_t total = 0;
     for (const auto& c : cus) total += cu_cost(c);
     const int S = plan_num_slices(total, max_slices_, (uint32_t)rc_.config().hevc_slice_cost);

@@ -123,16 +123,18 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
-    if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
+    if (depth_ > 1)
+        for (int i = 0; i < depth_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_[i], hipStreamNonBlocking));
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 GpuHevcEncoder::~GpuHevcEncoder() {
     (void)hipStreamSynchronize(stream_);
-    if (stream_e_) {
-        (void)hipStreamSynchronize(stream_e_);
-        (void)hipStreamDestroy(stream_e_);
-    }
+    for (hipStream_t s : stream_e_)
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);
@@ -175,6 +177,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.prev_src = src_keep_[ref];
     f.save_src = src_keep_[cur];
     f.wpp = cfg_.hevc_wpp ? 1 : 0;
+    f.wpp_rows = common_.wpp_rows();
     if (++wpp_epoch_ == 0) wpp_epoch_ = 1;
     f.wpp_epoch = wpp_epoch_;
     f.wpp_ctx = sl.buf.wpp_ctx;
@@ -205,7 +208,7 @@ int GpuHevcEncoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     fill_state(sl, true, qp, cur_ ^ 1, cur_, true);
     enqueue_body(true, src_y, src_uv);
     HIP_CHECK(hipStreamSynchronize(stream_));
-    if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
+    HIP_CHECK(hipStreamSynchronize(es(0)));
     const HevcOutHeader hdr = *reinterpret_cast<const HevcOutHeader*>(sl.host_out);
     // (header records are substreams; the per-NAL allowance counts slices, as the CPU encoder's probe)
     return hdr.overflow ? (int)sl.buf.out_bytes : (int)(hdr.total_bytes + common_.num_slices() * 12 + 64);
@@ -248,15 +251,15 @@ void GpuHevcEncoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint
 }
 
 void GpuHevcEncoder::link_entropy() {
-    if (!stream_e_) return;
+    if (!stream_e_[prep_slot_]) return;
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
-    HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+    HIP_CHECK(hipStreamWaitEvent(stream_e_[prep_slot_], sl.analysis_done, 0));
 }
 
 void GpuHevcEncoder::enqueue_entropy() {
     FrameSlot& sl = slots_[prep_slot_];
-    launch_hevc_entropy(geom_, sl.buf, common_.max_slices(), sl.host_out, stream_e_ ? stream_e_ : stream_);
+    launch_hevc_entropy(geom_, sl.buf, common_.max_slices(), sl.host_out, es(prep_slot_));
 }
 
 void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
@@ -270,7 +273,7 @@ void GpuHevcEncoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_
 
 void GpuHevcEncoder::record_done() {
     FrameSlot& sl = slots_[prep_slot_];
-    HIP_CHECK(hipEventRecord(sl.done, stream_e_ ? stream_e_ : stream_));
+    HIP_CHECK(hipEventRecord(sl.done, es(prep_slot_)));
     inflight_.push_back(prep_slot_);
 }
 
@@ -346,17 +349,23 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     return au_;
 }
 
-std::vector<std::array<uint64_t, 4>> GpuHevcEncoder::slice_timing() const {
-    std::vector<std::array<uint64_t, 4>> out;
+std::vector<std::array<uint64_t, 6>> GpuHevcEncoder::slice_timing() const {
+    std::vector<std::array<uint64_t, 6>> out;
     if (last_slot_ < 0) return out;
     const size_t n = last_first_.size();
+    const uint64_t ncu = (uint64_t)geom_.mb_w * geom_.mb_h;
     std::vector<unsigned long long> clk(2 * n);
+    std::vector<uint32_t> off(ncu + 1);
     HIP_CHECK(hipMemcpy(clk.data(), slots_[last_slot_].buf.slice_clk, sizeof(unsigned long long) * 2 * n,
                         hipMemcpyDeviceToHost));
-    const uint64_t ncu = (uint64_t)geom_.mb_w * geom_.mb_h;
+    HIP_CHECK(hipMemcpy(off.data(), slots_[last_slot_].buf.tok_off, sizeof(uint32_t) * (ncu + 1),
+                        hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull;
+    for (size_t k = 0; k < n; ++k) t0 = std::min(t0, clk[2 * k]);
     for (size_t k = 0; k < n; ++k) {
         const uint64_t end = k + 1 < n ? last_first_[k + 1] : ncu;
-        out.push_back({last_first_[k], end - last_first_[k], last_len_[k], clk[2 * k + 1] - clk[2 * k]});
+        out.push_back({last_first_[k], end - last_first_[k], last_len_[k], clk[2 * k + 1] - clk[2 * k],
+                       clk[2 * k] - t0, off[end] - off[last_first_[k]]});
     }
     return out;
 }

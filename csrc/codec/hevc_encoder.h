@@ -53,6 +53,11 @@ class HevcCommon {
                          size_t n, const uint32_t* sub_len = nullptr, int nsub = 0,
                          const uint32_t* sub_off = nullptr) const;
     bool wpp() const { return config().hevc_wpp != 0; }
+    // CTU rows per P slice with WPP (the whole picture when 0 or larger)
+    int wpp_rows() const {
+        const int r = config().hevc_wpp_rows;
+        return (r <= 0 || r > ctb_h()) ? ctb_h() : std::max(r, slice_rows_);  // level slice cap
+    }
     // Slice layout: I pictures one slice per slice_rows() CTU rows (the intra wavefront needs a
     // fixed layout), P pictures cost-balanced raster runs (plan_p_slices).  Returns first CTUs.
     std::vector<int> row_slices() const;
@@ -153,6 +158,7 @@ struct HevcFrameState {
     // row's wave publishes its contexts after its second CTU (wpp_ctx[row][36 words], then
     // wpp_flag[row] = wpp_epoch with release semantics) and the next row's wave acquires them
     int32_t wpp;
+    int32_t wpp_rows;    // CTU rows per P slice with WPP
     uint32_t wpp_epoch;  // nonzero, new every frame
     uint32_t* wpp_ctx;
     uint32_t* wpp_flag;
@@ -241,7 +247,9 @@ class GpuHevcEncoder final : public VideoEncoder {
     hipEvent_t pending_done_event() const override { return inflight_.empty() ? last_done_ : slots_[inflight_.front()].done; }
     // Per-slice CABAC timing of the last collected picture (diagnostics, synchronous copy):
     // (first CTU, CTUs, payload bytes, wave ticks at 100 MHz) per slice.
-    std::vector<std::array<uint64_t, 4>> slice_timing() const;
+    // per substream of the last picture: first CTU, CTUs, bytes, wave ticks (100 MHz), start tick
+    // relative to the earliest wave, tokens coded
+    std::vector<std::array<uint64_t, 6>> slice_timing() const;
    private:
     int mask_c_[4] = {0, 0, 0, 0};
     int64_t masked_pixels_ = 0;
@@ -255,7 +263,10 @@ class GpuHevcEncoder final : public VideoEncoder {
     // masked luma distortion computed by k_hevc_sao (a mask is set and SAO is on)
     bool masked_sse_in_encoder() const override { return cfg_.sao != 0 && mask_c_[2] > mask_c_[0]; }
     int prep_slot() const override { return prep_slot_; }
-    hipStream_t entropy_stream() const override { return stream_e_; }
+    // one entropy stream per frame slot: the CABAC of consecutive frames is independent (only the
+    // analysis chain carries the reference), so with 2-3 frames in flight their serial arithmetic
+    // coders run side by side instead of queueing behind each other
+    hipStream_t entropy_stream() const override { return stream_e_[prep_slot_]; }
     void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void enqueue_entropy() override;
     void link_entropy() override;
@@ -279,7 +290,8 @@ class GpuHevcEncoder final : public VideoEncoder {
     EncoderConfig cfg_;
     HevcCommon common_;
     hipStream_t stream_;
-    hipStream_t stream_e_ = nullptr;
+    hipStream_t stream_e_[kMaxInFlight] = {};  // per slot (depth > 1)
+    hipStream_t es(int slot) const { return stream_e_[slot] ? stream_e_[slot] : stream_; }
     int depth_ = 1;
     Geometry geom_;
     FrameSlot slots_[kMaxInFlight];

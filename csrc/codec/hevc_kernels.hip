@@ -844,11 +844,30 @@ struct IntraRefs {
     int dc, dcc[2];
 };
 
-// Sample (x, y) of the prediction for one of the candidate modes (planar, DC, 26, 10);
-// equals intra_predict() for those modes.
+// Sample (x, y) of the prediction of any intra mode; equals intra_predict().  L / T: the
+// references (index 0 = corner), LF / TF the [1 2 1]-filtered ones (8.4.4.2.3, luma only).
 __device__ __forceinline__ int pred_sample(int mode, int log2n, bool luma, const int* L, const int* T, const int* LF,
                                            const int* TF, int dc, int x, int y) {
     const int N = 1 << log2n;
+    if (mode >= 2 && mode != 10 && mode != 26) {  // angular (8.4.4.2.6)
+        const int d1 = mode > 26 ? mode - 26 : 26 - mode, d2 = mode > 10 ? mode - 10 : 10 - mode;
+        const int thres = N == 8 ? 7 : (N == 16 ? 1 : 0);
+        const bool filt = luma && N != 4 && (d1 < d2 ? d1 : d2) > thres;
+        const bool vert = mode >= 18;
+        const int* mainr = vert ? (filt ? TF : T) : (filt ? LF : L);
+        const int* side = vert ? (filt ? LF : L) : (filt ? TF : T);
+        const int angle = kIntraAngle[mode];
+        const int a = vert ? y : x, b = vert ? x : y;  // a: distance along the prediction, b: across it
+        const int pos = (a + 1) * angle, idx = pos >> 5, fact = pos & 31;
+        const int k = b + idx + 1;
+        // ref[k] for k >= 0 is the main array; negative k (negative angles) projects onto the side
+        // array through the inverse angle, as intra_predict() extends ref[]
+        const int ia = angle < 0 ? inv_angle(angle) : 0;
+        const int r0 = k >= 0 ? mainr[k] : side[(k * ia + 128) >> 8];
+        if (!fact) return r0;
+        const int r1 = k + 1 >= 0 ? mainr[k + 1] : side[((k + 1) * ia + 128) >> 8];
+        return ((32 - fact) * r0 + fact * r1 + 16) >> 5;
+    }
     if (mode == 0)
         return ((N - 1 - x) * LF[1 + y] + (x + 1) * TF[1 + N] + (N - 1 - y) * TF[1 + x] + (y + 1) * LF[1 + N] + N) >>
                (log2n + 1);
@@ -1134,8 +1153,10 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     __shared__ uint32_t wtot[16];
     const int tid = threadIdx.x;
     if (tid < 4) fs->sse_tot[tid] = 0ull;  // k_hevc_sao accumulates into these next
-    if (fs->idr || fs->wpp) {  // I: fixed row slices; P with WPP: one slice (a substream per CTU row)
-        const int sr = fs->idr ? fs->slice_rows : ncu / ctb_w, S = fs->idr ? fs->num_slices : 1;
+    if (fs->idr || fs->wpp) {  // I: fixed row slices; P with WPP: slices of wpp_rows rows (a substream per row)
+        const int rows = ncu / ctb_w;
+        const int sr = fs->idr ? fs->slice_rows : fs->wpp_rows;
+        const int S = fs->idr ? fs->num_slices : (rows + sr - 1) / sr;
         for (int k = tid; k < S; k += blockDim.x) slice_first[k] = k * sr * ctb_w;
         for (int i = tid; i < ncu; i += blockDim.x) slice_of_cu[i] = (i / ctb_w) / sr;
         if (tid == 0) *nslices = (uint32_t)S;
@@ -1505,18 +1526,18 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
     }
     LeanCoder lc;
     lc.e.start(slice_data + (size_t)u * slice_cap, slice_cap);
-    if (store) {
-        // the row's first two CTUs, then publish the contexts (storage process after CTU 1)
-        const uint32_t ts = uni(off[first + 2]);
-        arith_run(lc, ctx, dense, t0, ts, lane);
-        if (lane == 0) {
+    // two segments through one copy of the coder loop (the kernel stays inside the instruction
+    // cache): the row's first two CTUs, the context publication (storage process after CTU 1),
+    // then the rest; without a publication the first segment is empty
+    const uint32_t ts = store ? uni(off[first + 2]) : t0;
+#pragma unroll 1
+    for (int seg = 0; seg < 2; ++seg) {
+        arith_run(lc, ctx, dense, seg ? ts : t0, seg ? t1 : ts, lane);
+        if (seg == 0 && store && lane == 0) {
             uint32_t* dst = fs->wpp_ctx + (size_t)u * kWppCtxWords;
             for (int k = 0; k < kWppCtxWords; ++k) dst[k] = (uint32_t)__builtin_amdgcn_readlane((int)ctx.st, k);
             __hip_atomic_store(fs->wpp_flag + u, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
-        arith_run(lc, ctx, dense, ts, t1, lane);
-    } else {
-        arith_run(lc, ctx, dense, t0, t1, lane);
     }
     CabacEnc& e = lc.e;
     e.finish_slice();  // flush + the stop / alignment one-bit and zero bits (slice end or end of subset)

@@ -51,3 +51,16 @@ def test_gpu_cbr_hevc_4k_on_budget(gpu):
     T = 25000e3 / 60
     assert bits[0] < 7 * T
     assert abs(bits[5:].mean() / T - 1) < 0.10, bits[5:].mean() / T
+
+
+def test_gpu_cbr_desktop_keyframes_pinned(gpu):
+    """The loosened bounds above cover any content; on the bench desktop itself the intended
+    behaviour is tighter and pinned here: every IDR (first picture and a forced one) within 5.5
+    frame budgets -- its send time on the wire stays about 90 ms at the headline rate -- and the
+    driver's 20-frame window within +-10 %."""
+    s = _session(gpu)
+    bits, _, idr = _run(s, 40, idr_at=(25,))
+    T = 8000e3 / 60
+    assert idr[0] == 1 and idr[25] == 1
+    assert bits[0] <= 5.5 * T and bits[25] <= 5.5 * T, (bits[0] / T, bits[25] / T)
+    assert abs(bits[5:25].mean() / T - 1) < 0.10, bits[5:25].mean() / T

@@ -1,8 +1,9 @@
 """Per-slice CABAC timing of the HIP HEVC encoder (GPU): every k_hevc_cabac wave records its
 start / end wall clock (100 MHz), GpuHevcEncoder.slice_timing() returns (first CTU, CTUs,
-bytes, ticks) per slice of the last picture.  Fits ticks ~ a * CTUs + b * bytes over all
-slices, to tell the per-CU fixed cost from the per-byte (per-bin) cost, and reports the
-slowest slice -- the one that sets the kernel's time.
+bytes, ticks, start tick, tokens) per substream (slice, or WPP CTU row) of the last picture.
+Fits ticks ~ a * CTUs + b * tokens over all substreams, to tell the per-CU fixed cost from the
+per-token cost, and reports the slowest substream and (WPP) the latest start -- the wavefront
+fill.
 
     python tools/hevc_cabac_timing.py --width 3840 --height 2160 --bitrate-kbps 25000 --frames 24
 """
@@ -24,6 +25,8 @@ def main():
     ap.add_argument("--bitrate-kbps", type=int, default=25000)
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--report", type=int, default=4)
+    ap.add_argument("--wpp", type=int, default=1)
+    ap.add_argument("--wpp-rows", type=int, default=8)
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     import torch
@@ -37,6 +40,7 @@ def main():
     cfg = N.EncoderConfig()
     cfg.width, cfg.height, cfg.fps = a.width, a.height, 60
     cfg.bitrate_kbps = a.bitrate_kbps
+    cfg.hevc_wpp, cfg.hevc_wpp_rows = a.wpp, a.wpp_rows
     enc = N.GpuHevcEncoder(cfg, torch.cuda.current_stream().cuda_stream)
     desk = CpuSyntheticDesktop(a.width, a.height, True)
     rows, allx, ally = [], [], []
@@ -48,19 +52,22 @@ def main():
         au = enc.encode(dy.data_ptr(), duv.data_ptr(), False)
         if f < a.frames - a.report or enc.stats.idr:
             continue
-        t = np.array(enc.slice_timing(), dtype=np.float64)  # first, ctus, bytes, ticks
+        t = np.array(enc.slice_timing(), dtype=np.float64)  # first, ctus, bytes, ticks, start, tokens
         us = t[:, 3] / 100.0
+        end_us = (t[:, 3] + t[:, 4]) / 100.0
         k = int(np.argmax(us))
-        allx.append(t[:, 1:3])
+        allx.append(t[:, [1, 5]])
         ally.append(us)
-        rows.append({"frame": f, "au_bytes": len(au), "slices": int(len(t)), "max_us": round(float(us[k]), 1),
-                     "median_us": round(float(np.median(us)), 1), "slowest_ctus": int(t[k, 1]),
-                     "slowest_bytes": int(t[k, 2]), "max_ctus": int(t[:, 1].max()), "max_bytes": int(t[:, 2].max())})
+        rows.append({"frame": f, "au_bytes": len(au), "substreams": int(len(t)), "tokens": int(t[:, 5].sum()),
+                     "span_us": round(float(end_us.max()), 1), "max_us": round(float(us[k]), 1),
+                     "median_us": round(float(np.median(us)), 1), "latest_start_us": round(float(t[:, 4].max() / 100), 1),
+                     "slowest_ctus": int(t[k, 1]), "slowest_tokens": int(t[k, 5]), "slowest_bytes": int(t[k, 2]),
+                     "max_tokens": int(t[:, 5].max()), "ns_per_token_slowest": round(1e3 * float(us[k] / max(t[k, 5], 1)), 1)})
         print(json.dumps(rows[-1]), flush=True)
     X = np.concatenate(allx)
     Y = np.concatenate(ally)
     coef, *_ = np.linalg.lstsq(X, Y, rcond=None)
-    fit = {"us_per_ctu": round(float(coef[0]), 4), "us_per_byte": round(float(coef[1]), 4)}
+    fit = {"us_per_ctu": round(float(coef[0]), 4), "ns_per_token": round(1e3 * float(coef[1]), 2)}
     print(json.dumps({"fit": fit}), flush=True)
     if a.json_out:
         Path(a.json_out).parent.mkdir(parents=True, exist_ok=True)
