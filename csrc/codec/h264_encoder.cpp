@@ -276,6 +276,7 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipEventCreateWithFlags(&sl.start, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&sl.deblock_done, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.hpel_done, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
 }
 
@@ -289,7 +290,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     if (b.db_err) (void)hipHostFree(b.db_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);
-    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.deblock_done, sl.done})
+    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.deblock_done, sl.done, sl.hpel_done})
         if (e) (void)hipEventDestroy(e);
 }
 
@@ -335,7 +336,12 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     clock_khz_ = device_clock_khz();
-    if (depth_ > 1) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
+    if (depth_ > 1) {
+        HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&stream_a_, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&ref_ready_, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(ref_ready_, stream_));
+    }
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
@@ -344,6 +350,11 @@ GpuH264Encoder::~GpuH264Encoder() {
     if (stream_e_) {
         (void)hipStreamSynchronize(stream_e_);
         (void)hipStreamDestroy(stream_e_);
+    }
+    if (stream_a_) {
+        (void)hipStreamSynchronize(stream_a_);
+        (void)hipStreamDestroy(stream_a_);
+        (void)hipEventDestroy(ref_ready_);
     }
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
@@ -362,7 +373,14 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
         if (cfg_.aq >= 3)  // the next P picture's previous source (P pictures: k_inter_encode stores it)
             launch_save_src(geom_, sl.buf, src_y, stream_);
     } else {
-        launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
+        if (stream_a_ && pub && ref_seq_ + 1 == seq_) {  // the previous picture recorded ref_ready_
+            HIP_CHECK(hipStreamWaitEvent(stream_a_, ref_ready_, 0));
+            launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_a_, pub);
+            HIP_CHECK(hipEventRecord(sl.hpel_done, stream_a_));
+            HIP_CHECK(hipStreamWaitEvent(stream_, sl.hpel_done, 0));
+        } else {
+            launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
+        }
         launch_me(geom_, sl.buf, src_y, stream_);
         launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
         if (cfg_.intra_in_p) launch_intra_in_p(geom_, sl.buf, src_y, src_uv, stream_);
@@ -394,6 +412,10 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
             HIP_CHECK(hipEventRecord(sl.deblock_done, stream_));
             sse_ready = sl.deblock_done;
         }
+    }
+    if (stream_a_ && publish) {  // the next picture's reference is final
+        HIP_CHECK(hipEventRecord(ref_ready_, stream_));
+        ref_seq_ = seq_;
     }
     launch_entropy(geom_, sl.buf, sl.host_out, es, sse_ready);
     HIP_CHECK(hipGetLastError());
@@ -462,6 +484,7 @@ bool GpuH264Encoder::prepare(bool force_idr) {
     const int s = (depth_ == 1) ? 0 : next_slot_;
     next_slot_ = (next_slot_ + 1) % depth_;
     prep_slot_ = s;
+    ++seq_;
     FrameSlot& sl = slots_[s];
     common_.begin_frame(force_idr || !have_ref_);
     have_ref_ = true;  // this frame becomes the reference of the next one

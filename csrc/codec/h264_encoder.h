@@ -57,10 +57,14 @@ struct EncoderConfig {
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
     int hevc_slice_cost = 1024;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
-    // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): one slice per P picture,
-    // every CTU row its own CABAC substream (one GPU wave each) that starts from the contexts the row
-    // above had after its second CTU; 0: cost-balanced slices, one substream per slice
-    int hevc_wpp = 1;
+    // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): P pictures in slices of
+    // hevc_wpp_rows CTU rows, every CTU row its own CABAC substream (one GPU wave each) that starts
+    // from the contexts the row above had after its second CTU.  Off by default: a CTU row is a
+    // serial coder chain, and the rows through the desktop's detailed regions carry the most bins,
+    // so at 4K / 25 Mbps WPP gave +0.27 dB masked for half the frame rate (817 vs 1,619 fps, with
+    // 2- to 16-row slices all within 2 %: profiles/r04_hevc); cost-balanced slices split those
+    // regions instead.  0: cost-balanced slices, one substream per slice
+    int hevc_wpp = 0;
     // HEVC with WPP: CTU rows per P slice (0 = the whole picture).  A substream row is a serial
     // chain and a slice's rows start two CTUs apart, so a slice of R rows takes ~2R + row-length
     // CTU times: short slices keep the wavefront's fill out of the frame time (at 4K one slice
@@ -239,6 +243,7 @@ class GpuH264Encoder final : public VideoEncoder {
         FrameState* fs_host = nullptr;  // pinned
         uint8_t* host_out = nullptr;    // pinned, mapped: OutHeader | slice tables | payload
         hipEvent_t start = nullptr, analysis_done = nullptr, deblock_done = nullptr, done = nullptr;
+        hipEvent_t hpel_done = nullptr;
         bool idr = false;
         int qp = 0;
     };
@@ -251,6 +256,13 @@ class GpuH264Encoder final : public VideoEncoder {
     EncoderCommon common_;
     hipStream_t stream_;
     hipStream_t stream_e_ = nullptr;  // entropy stream (depth 2)
+    // depth > 1, eager launches: k_hpel of a P picture runs on its own stream as soon as the
+    // reference is final (ref_ready_, recorded after the previous picture's last reconstruction
+    // kernel), beside the capture and colour conversion of the new picture, which it does not
+    // depend on; k_me_full waits for it (profiles/r04_h264)
+    hipStream_t stream_a_ = nullptr;
+    hipEvent_t ref_ready_ = nullptr;
+    uint64_t seq_ = 0, ref_seq_ = ~0ull;  // pictures prepared; the one whose reconstruction ref_ready_ marks
     int depth_ = 1;
     Geometry geom_;
     FrameSlot slots_[kMaxInFlight];

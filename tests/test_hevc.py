@@ -31,8 +31,11 @@ def _cfg(native, w, h, fps=60, qp=28, bitrate=0, aq=1, sr=8, tu_split=0):
     return cfg
 
 
-def _cpu_roundtrip(native, w, h, frames, fps=60, qp=28, bitrate=0, fresh=False, idr_at=(), tu_split=0):
-    enc = native.CpuHevcEncoder(_cfg(native, w, h, fps, qp, bitrate, tu_split=tu_split))
+def _cpu_roundtrip(native, w, h, frames, fps=60, qp=28, bitrate=0, fresh=False, idr_at=(), tu_split=0, wpp=None):
+    cfg = _cfg(native, w, h, fps, qp, bitrate, tu_split=tu_split)
+    if wpp is not None:
+        cfg.hevc_wpp = wpp
+    enc = native.CpuHevcEncoder(cfg)
     stream, recon, src, sizes = b"", [], [], []
     for t in range(frames):
         y, uv = synthetic_nv12(w, h, t, seed=t if fresh else 0)
@@ -82,7 +85,7 @@ def test_cpu_hevc_rate_control_and_idr(native):
 def test_cpu_hevc_two_row_slices(native):
     # 352x288 @ 30 fps is level 2 (16 slice segments) -> 18 CTU rows need 2-row slices, which
     # exercises above-neighbour intra references, merge/AMVP B candidates and skip contexts
-    _, _, _, dec, enc = _cpu_roundtrip(native, 352, 288, 2, fps=30, qp=30)
+    _, _, _, dec, enc = _cpu_roundtrip(native, 352, 288, 2, fps=30, qp=30, wpp=1)
     assert enc.slice_rows == 2
     assert dec.stats["slices"] == 9 + 3  # 9 two-row slices in the IDR picture, 8-row WPP slices in the P picture
     assert dec.stats["substreams"] == 18 + 18  # one per CTU row: 9 slices x 2 rows, then 18 rows
@@ -189,13 +192,15 @@ def test_decoder_rejects_truncated_stream(native):
 
 
 # ---------------------------------------------------------------------------- GPU tier
-def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, aq=1, desktop=False, sao=1):
+def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, aq=1, desktop=False, sao=1,
+                wpp=0, wpp_rows=8):
     import torch
 
     from .gpu_util import pitched
 
     cfg = _cfg(gpu, w, h, fps, qp, sr=sr, tu_split=tu_split, aq=aq)
     cfg.sao = sao
+    cfg.hevc_wpp, cfg.hevc_wpp_rows = wpp, wpp_rows
     desk = None
     if desktop:
         from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
@@ -261,6 +266,15 @@ def test_gpu_hevc_sao_bit_exact_vs_cpu(gpu, w, h, qp, sao):
     """SAO on the GPU (k_hevc_sao: CTB-parallel statistics, decision and offsets, CABAC sao()
     syntax) == the CPU encoder, bit for bit, at toy size and 1080p; sao=0 keeps the plain path."""
     _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=1, aq=3, desktop=True, sao=sao)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,qp,rows", [(320, 192, 26, 0), (320, 192, 30, 2), (200, 120, 30, 0), (1920, 1080, 34, 8)])
+def test_gpu_hevc_wpp_bit_exact_vs_cpu(gpu, w, h, qp, rows):
+    """Wavefront substreams on the GPU (one k_hevc_arith wave per CTU row, contexts handed down
+    from the row above's second CTU by release/acquire flags; slices of `rows` CTU rows, 0 = one
+    per picture) == the CPU encoder bit for bit, and the decoder checks the entry points."""
+    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=1, aq=3, desktop=True, wpp=1, wpp_rows=rows)
 
 
 @pytest.mark.gpu
