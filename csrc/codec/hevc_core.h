@@ -1356,6 +1356,12 @@ MXHD int sao_sample_cat(uint32_t w, int c, int cat) {
 MXHD int sao_sample(uint32_t w, int c, int a, int b) {
     return sao_sample_cat(w, c, (a >= 0 && b >= 0) ? sao_edge_cat(c, a, b) : 0);
 }
+// Encoder decision shared by both encoders: a CTB of a P picture whose CU coded no residual keeps
+// its samples (SAO off) without gathering statistics.  Its prediction came from a picture SAO
+// already corrected (static or rigidly moving content: most of a desktop), so a second offset pass
+// finds ~nothing, and the statistics pass is the bulk of k_hevc_sao's time.
+MXHD bool sao_keep_ctb(bool idr, const CuInfo& c) { return !idr && c.cbf == 0; }
+
 // Apply w to the n x n block at (x0, y0): reads the deblocked plane rec, writes out (a different
 // buffer: every CTB reads its neighbours' deblocked samples).
 MXHD void sao_apply_block(const uint8_t* rec, uint8_t* out, int pitch, int step, int x0, int y0, int n, int W, int H,

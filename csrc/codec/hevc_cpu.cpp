@@ -650,6 +650,14 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         const uint32_t lam16 = kLambdaSse16[qp];
         for (int i = 0; i < W * H; ++i) {
             const int x0 = (i % W) * kCtb, y0 = (i / W) * kCtb;
+            uint32_t* w = sao_.data() + 4 * (size_t)i;
+            if (sao_keep_ctb(idr, cu_[i])) {  // no residual in a P picture: SAO off, samples kept
+                sao_apply_block(pre_y.data(), rec_y_[cur_].data(), cw_, 1, x0, y0, kCtb, cw_, ch_, 0u);
+                for (int c = 0; c < 2; ++c)
+                    sao_apply_block(pre_uv.data() + c, rec_uv_[cur_].data() + c, cw_, 2, x0 / 2, y0 / 2, kCtb / 2,
+                                    cw_ / 2, ch_ / 2, 0u);
+                continue;
+            }
             SaoStats st[3];
             sao_stats_block(pre_y.data(), cw_, y, pitch, 1, x0, y0, kCtb, cw_, ch_, st[0]);
             for (int c = 0; c < 2; ++c)
@@ -657,7 +665,6 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
                                 st[1 + c]);
             SaoCompChoice ch[3];
             for (int c = 0; c < 3; ++c) sao_eval_comp(st[c], lam16, ch[c]);
-            uint32_t* w = sao_.data() + 4 * (size_t)i;
             sao_combine(ch[0], ch[1], ch[2], lam16, w);
             sao_apply_block(pre_y.data(), rec_y_[cur_].data(), cw_, 1, x0, y0, kCtb, cw_, ch_, w[0]);
             for (int c = 0; c < 2; ++c)

@@ -1717,7 +1717,7 @@ __device__ __forceinline__ void sao_wave_sync() {
 
 __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameState* __restrict__ fs,
                                                    const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv,
-                                                   uint32_t* __restrict__ prm) {
+                                                   const CuInfo* __restrict__ cus, uint32_t* __restrict__ prm) {
     __shared__ SaoWave sw[4];
     __shared__ unsigned long long part[4][4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1733,10 +1733,15 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     sao_wave_sync();
     const int r = lane >> 2, c0 = (lane & 3) * 4;
     const int xc = x0 / 2 + (lane & 7), yc = y0 / 2 + (lane >> 3);
+    // no residual in a P picture (sao_keep_ctb): SAO off, the samples are only copied and measured
+    const bool keep = valid && sao_keep_ctb(fs->idr != 0, cus[i]);  // wave-uniform (one CTB per wave)
     // ---- statistics (the edge categories and centre samples are kept for the apply phase)
     uint64_t cat_y = 0;
     uint32_t cen_y = 0, cat_u = 0, cat_v = 0, cen_uv = 0;
-    if (valid) {
+    if (keep) {
+        cen_y = *(const sao_gu32*)(ry + (size_t)(y0 + r) * g.pitch + x0 + c0);
+        cen_uv = *(const sao_gu16*)(ruv + (size_t)yc * g.pitch + 2 * xc);
+    } else if (valid) {
         int L[3][6];
         sao_luma_window(ry, g.pitch, W, H, x0 + c0, y0 + r, L);
         const uint32_t sv = *(const sao_gu32*)(src_y + (size_t)(y0 + r) * g.pitch + x0 + c0);
@@ -1782,7 +1787,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     sao_wave_sync();
     // ---- candidate offsets per (comp, class, category) and per (comp, band)
     const uint32_t lam16 = kLambdaSse16[fs->qp < 0 ? 0 : (fs->qp > 51 ? 51 : fs->qp)];
-    if (valid) {
+    if (valid && !keep) {
         if (lane < 48) {
             const int comp = lane >> 4, q = lane & 15, cat = q & 3;
             const int v = S.eo[comp][q];
@@ -1802,7 +1807,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     sao_wave_sync();
     // ---- per component: best band window (lexicographic min of (cost, position) over 32 lanes)
     //      and the edge-class sums
-    if (valid) {
+    if (valid && !keep) {
         for (int pass = 0; pass < 2; ++pass) {
             const int comp = pass * 2 + (lane >> 5), p = lane & 31;
             const bool on = comp < 3;
@@ -1832,8 +1837,8 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     }
     sao_wave_sync();
     if (valid && lane == 0) {
-        uint32_t w[3];
-        sao_combine(S.ch[0], S.ch[1], S.ch[2], lam16, w);
+        uint32_t w[3] = {0u, 0u, 0u};
+        if (!keep) sao_combine(S.ch[0], S.ch[1], S.ch[2], lam16, w);
         S.w[0] = w[0];
         S.w[1] = w[1];
         S.w[2] = w[2];
@@ -2070,7 +2075,7 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
     }
     if (sao)  // SAO, with the final distortion (one partial per 4 CTBs)
-        hipLaunchKernelGGL(k_hevc_sao, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.sao);
+        hipLaunchKernelGGL(k_hevc_sao, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.cu, b.sao);
     else if (deblock)
         hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
 }
