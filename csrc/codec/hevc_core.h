@@ -696,7 +696,7 @@ struct CuInfo {
     uint8_t tu_split;
     uint8_t cbf_y4;  // split: bit k = luma TU k coded
     uint8_t cbf_c4;  // split: bit k = Cb TU k, bit 4+k = Cr TU k coded
-    uint8_t pad;
+    uint8_t est_bytes;  // entropy-coder work estimate of a coded CU: cu_bits_est / 8, capped 255 (set_est_bytes)
 };
 static_assert(sizeof(CuInfo) == 24, "CuInfo layout");
 constexpr int kCuWords = (int)(sizeof(CuInfo) / 4);
@@ -1783,6 +1783,11 @@ MXHD uint32_t tu_bits_est(const int16_t* lv, int n) {
     return any ? b + 4 : 1;
 }
 // Split wins when its SSE + lambda * bits is lower (costs in 1/16 units).
+// The split tree is tried only for CUs whose unsplit tree coded at least one level: a residual
+// that quantises to nothing in 16x16 / 8x8 TUs is (nearly always) coding noise of a static or
+// well-predicted block, and skipping the second tree there halves the transform work of a desktop
+// P picture.  Shared by both encoders.
+MXHD bool split_worth_trying(int levels_unsplit) { return levels_unsplit > 0; }
 MXHD bool choose_split(uint64_t sse16, uint32_t bits16, uint64_t sse8, uint32_t bits8, int qp) {
     const uint64_t l = kLambdaSse16[qp < 0 ? 0 : (qp > 51 ? 51 : qp)];
     return sse8 * 16 + l * bits8 < sse16 * 16 + l * bits16;
@@ -2073,17 +2078,21 @@ MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, 
 // Entropy-coding cost estimate of a CU in CABAC work units: significance bins up to the
 // last position of every coded TU plus a few bins per coded sub-block, on top of the CU
 // header.  Used only to balance slices; identical on the CPU and the GPU.
-MXHD uint32_t cu_cost(const CuInfo& c) {
-    uint32_t k = 4;
-    if (c.cbf & 1) k += c.last[0] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_y);
-    if (c.cbf & 2) k += c.last[1] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_c[0]);
-    if (c.cbf & 4) k += c.last[2] + 1 + 8 * (uint32_t)__builtin_popcount(c.csbf_c[1]);
-    return k;
+// Serial arithmetic-coder work of a CU, in units of ~0.11 us of k_hevc_arith wave time: the
+// two-phase coder's measured cost is 0.44 us per CTU + 0.63 us per payload byte
+// (profiles/r03_cabac/arith_timing_lean.log), so 4 units per CU + 6 per estimated byte.  (The
+// previous model -- last position + 8 per coded sub-block -- priced dense noise-like CUs at half
+// their real time, so the 4-CU slices through the noise panel ran 1.8x the median slice.)
+MXHD uint32_t cu_cost(const CuInfo& c) { return 4u + (c.cbf ? 6u * (uint32_t)c.est_bytes : 0u); }
+MXHD uint8_t est_bytes_of(uint32_t bits) {
+    const uint32_t b = (bits + 7) >> 3;
+    return (uint8_t)(b > 255u ? 255u : b);
 }
-// Below this much work per slice, fewer slices.  One unit is about 0.35 us of k_hevc_cabac wave
-// time (tools/hevc_cabac_timing.py: 0.79 us per CU + 1.45 us per payload byte, 4K and 1080p), so
-// 1024 units keep a slice near 0.35 ms; the level's slice limit usually binds first at 4K.
-constexpr uint32_t kCostPerSlice = 1024;  // EncoderConfig::hevc_slice_cost default
+// est_bytes of a summarised CU from the bits estimate of its final levels (cu_bits_est)
+MXHD void set_est_bytes(CuInfo& c, uint32_t bits) { c.est_bytes = c.cbf ? est_bytes_of(bits) : (uint8_t)0; }
+// Below this much work per slice, fewer slices: 3072 units keep a slice near 0.35 ms; the level's
+// slice limit usually binds first at 4K.
+constexpr uint32_t kCostPerSlice = 3072;  // EncoderConfig::hevc_slice_cost default
 // Number of slices for a P picture of total cost T, bounded by the level's slice limit.
 MXHD int plan_num_slices(uint64_t total, int max_slices, uint32_t cost_per_slice = kCostPerSlice) {
     const uint64_t s = total / (cost_per_slice ? cost_per_slice : 1u);

@@ -390,7 +390,10 @@ CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cf
 
 namespace {
 // Finish a CU's residual bookkeeping: cbf / last / coded sub-block masks.
-void summarise(CuInfo& c, const int16_t* coef) { cu_summarise(c, coef); }
+void summarise(CuInfo& c, const int16_t* coef) {
+    cu_summarise(c, coef);
+    set_est_bytes(c, cu_bits_est(coef, c.tu_split == 2));
+}
 }  // namespace
 
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
@@ -526,7 +529,9 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
             tu_encode(4, res, qp, false, co, rr);
             for (int comp = 0; comp < 2; ++comp) tu_encode(3, rc[comp], qpc, false, co + 256 + 64 * comp, rrc[comp]);
             c.tu_split = cfg_.tu_split ? 1 : 0;
-            if (cfg_.tu_split) {
+            int levels1 = 0;
+            for (int k = 0; k < kCoefPerCu; ++k) levels1 += co[k] != 0;
+            if (cfg_.tu_split && split_worth_trying(levels1)) {
                 // option 2: four 8x8 luma TUs, eight 4x4 chroma TUs; keep the cheaper by SSE + lambda * bits
                 int16_t co2[kCoefPerCu];
                 int rr2[256], rrc2[2][64];

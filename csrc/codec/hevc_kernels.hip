@@ -100,6 +100,25 @@ __device__ __forceinline__ uint32_t wor(uint32_t v) {
     return a | b;
 }
 
+// LDS hand-off between the lanes of ONE wave (its own LDS writes visible to its own later reads;
+// LDS operations of a wave complete in order): no workgroup barrier, so the waves of a workgroup
+// may take different branches around it.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// Stage separator of the TU helpers: a workgroup barrier when the waves of the workgroup run in
+// lockstep (the intra wavefront), else a wave-local one (inter CUs: every wave has its own LDS
+// scratch and may skip work the others do).
+template <bool kWaveLocal>
+__device__ __forceinline__ void tu_sync() {
+    if (kWaveLocal)
+        wave_lds_sync();
+    else
+        __syncthreads();
+}
+
 // Transform matrices in LDS (filled once per workgroup).
 struct alignas(16) Mats {
     int16_t t16[256];
@@ -152,8 +171,10 @@ struct alignas(16) TuBuf {
 
 // One wave transforms, quantises and reconstructs its CU's three TUs.  Lane mapping per
 // stage: luma outputs lane*4 .. lane*4+3, chroma outputs (lane&31)*2 .. +1 of component
-// lane>>5.  __syncthreads() separate the stages, so every wave of the workgroup calls this
-// the same number of times (idle waves with valid == false).
+// lane>>5.  tu_sync<kInterCu>() separates the stages: intra CUs (kInterCu false) run in lockstep
+// with workgroup barriers, so every wave of the workgroup calls this the same number of times
+// (idle waves with valid == false), and keep their reconstruction in t.pred for the neighbours;
+// inter CUs sync per wave and leave t.pred (the prediction) intact for the split tree after it.
 struct TuResult {
     int last[3];
     uint32_t csbf[3];
@@ -165,6 +186,7 @@ struct TuResult {
     uint32_t bits_y;  // tu_bits_est of the luma TU
 };
 
+template <bool kInterCu>
 __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool intra, bool valid,
                                              int16_t* coef, uint8_t* rec_y, int pitch_y, uint8_t* rec_uv, int x0,
                                              int y0, int disp_w, int disp_h) {
@@ -190,7 +212,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             aT[256 + comp * 64 + k * 8 + y] = (int16_t)((s + 2) >> 2);
         }
     }
-    __syncthreads();
+    tu_sync<kInterCu>();
     TuResult out;
     int lastl = -1, lastc = -1, nzl = 0, nzc = 0;
     uint32_t csl = 0, csc = 0;
@@ -315,7 +337,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
         out.bits = (uint32_t)((out.nz[0] ? bl + 4 : 1) + (out.nz[1] ? bcb + 4 : 1) + (out.nz[2] ? bcr + 4 : 1));
         out.bits_y = (uint32_t)(out.nz[0] ? bl + 4 : 1);
     }
-    __syncthreads();
+    tu_sync<kInterCu>();
     // ---- inverse stage 1 (columns): a[y][x] = clip16((sum_k T[k][y] b[k][x] + 64) >> 7)
     if (valid) {
         for (int j = 0; j < 4; ++j) {
@@ -329,7 +351,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             a16[256 + comp * 64 + idx] = (int16_t)clip16((s + 64) >> 7);
         }
     }
-    __syncthreads();
+    tu_sync<kInterCu>();
     // ---- inverse stage 2 (rows) + reconstruction
     int sy = 0, sc = 0, sf = 0, syf = 0;
     if (valid) {
@@ -346,7 +368,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             sf += e * e;
             syf += e * e;
             packed |= (uint32_t)v << (8 * j);
-            t.pred[y * 16 + x] = (uint8_t)v;  // reconstruction stays readable in LDS
+            if (!kInterCu) t.pred[y * 16 + x] = (uint8_t)v;  // intra: reconstruction stays readable in LDS
         }
         *reinterpret_cast<uint32_t*>(rec_y + (size_t)(y0 + y) * pitch_y + x0 + xb) = packed;
         const int nzcomp = comp ? out.nz[2] : out.nz[1];
@@ -358,7 +380,7 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
             const int p = t.pred[o];
             const int v = clip255(p + r);
             const int e = p + t.res[o] - v;
-            t.pred[o] = (uint8_t)v;
+            if (!kInterCu) t.pred[o] = (uint8_t)v;
             const int xc = x0 / 2 + x, yc = y0 / 2 + yy;
             sc += (2 * xc < disp_w && 2 * yc < disp_h) ? e * e : 0;
             sf += e * e;
@@ -378,7 +400,6 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
 // coefficients each, chroma TU (comp, k) = lanes 8(4comp+k).. with 2 each; decimation and
 // the trailing trim per TU through segmented shuffle reductions.  Levels go to lv (CU
 // layout), the reconstruction to rec (TuBuf layout); t.a / t.b are the stage buffers.
-// Called by every wave of the workgroup (barriers inside).
 // cu_summarise (hevc_core.h) of a split transform tree, by the whole wave: one ballot per
 // luma TU (lane = scan index) and one per chroma component (lane = 16 * TU + scan index) give
 // the coded masks, the rest is scalar (lane 0 alone walking 384 LDS levels cost ~1,100 VALU).
@@ -465,7 +486,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
             aT[cbase + k * 4 + y] = (int16_t)((s + 1) >> 1);
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     // ---- forward stage 2 (columns) + quantisation
     int ll[4] = {0, 0, 0, 0}, lc[2] = {0, 0};
     int sil[4], sic[2];
@@ -570,7 +591,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     SplitResult out;
     out.bits = (uint32_t)wsum(((lane & 15) == 0 ? (nzl ? bl + 4 : 1) : 0) + ((lane & 7) == 0 ? (nzc ? bc + 4 : 1) : 0));
     out.bits_y = (uint32_t)wsum((lane & 15) == 0 ? (nzl ? bl + 4 : 1) : 0);
-    __syncthreads();
+    wave_lds_sync();
     // ---- inverse stage 1 (columns)
     if (valid) {
         for (int j = 0; j < 4; ++j) {
@@ -584,7 +605,7 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
             a16[cbase + idx] = (int16_t)clip16((s + 64) >> 7);
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     // ---- inverse stage 2 (rows) + reconstruction
     int sf = 0, sy = 0, sc = 0, syf = 0;
     if (valid) {
@@ -615,14 +636,14 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     out.sse[0] = wsum(sy);
     out.sse[1] = wsum(comp == 0 ? sc : 0);
     out.sse[2] = wsum(comp == 1 ? sc : 0);
-    __syncthreads();
+    wave_lds_sync();
     return out;
 }
 
 __device__ __forceinline__ void fill_cu(CuInfo& c, const TuResult& r) {
     c.tu_split = 0;
     c.cbf_y4 = c.cbf_c4 = 0;
-    c.pad = 0;
+    c.est_bytes = 0;
     c.cbf = (uint8_t)((r.nz[0] ? 1 : 0) | (r.nz[1] ? 2 : 0) | (r.nz[2] ? 4 : 0));
     c.last[0] = (uint8_t)(r.last[0] < 0 ? 0 : r.last[0]);
     c.last[1] = (uint8_t)(r.last[1] < 0 ? 0 : r.last[1]);
@@ -756,19 +777,20 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         const int rc = lane >> 3, cc = lane & 7;
         for (int comp = 0; comp < 2; ++comp) t.res[256 + comp * 64 + rc * 8 + cc] = 0;
     }
-    __syncthreads();
+    wave_lds_sync();  // from here on every wave works alone (wave-local syncs, per-wave LDS)
     int16_t* co = coef + (size_t)(valid ? i : 0) * kCoefPerCu;
-    // option 2, the split transform tree (split_encode of the CPU encoder), whole wave
-    const bool try_split = fs->tu_split != 0;  // uniform over the grid: barriers inside are safe
+    // option 1, one 16x16 luma TU (writes its levels and reconstruction; t.pred keeps the prediction)
+    const TuResult r = code_tus<true>(t, M, qp, qpc, false, valid, co, fs->rec_y, g.pitch, fs->rec_uv, x0, y0,
+                                      g.width, g.height);
+    // option 2, the split transform tree (split_encode of the CPU encoder), whole wave -- only
+    // when option 1 coded something (split_worth_trying, as the CPU encoder)
+    const bool try_split = fs->tu_split != 0 && valid && split_worth_trying(r.nz[0] + r.nz[1] + r.nz[2]);  // wave-uniform
     SplitResult r2 = {0, {0, 0, 0}, 0, 0, 0};
     if (try_split)
         r2 = split_tus(t, M, qp, qpc, valid, lv2[wave], rec2[wave], x0, y0, g.width, g.height);
     const int sse2 = r2.sse_full, bits2 = (int)r2.bits;
     const int sse2y = r2.sse[0], sse2u = r2.sse[1], sse2v = r2.sse[2];
-    // option 1, one 16x16 luma TU (writes its levels and reconstruction)
-    const TuResult r = code_tus(t, M, qp, qpc, false, valid, co, fs->rec_y, g.pitch, fs->rec_uv, x0, y0, g.width,
-                                g.height);
-    const bool split = try_split && valid &&
+    const bool split = try_split &&
                        choose_split((uint64_t)r.sse_full, r.bits, (uint64_t)sse2, (uint32_t)bits2, qp);  // wave-uniform
     if (split) {  // the split tree wins: overwrite option 1's levels and reconstruction
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -811,17 +833,18 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         c.mvdx = c.mvdy = 0;
         c.mvp_idx = 0;
         fill_cu(c, r);
-        if (try_split) {
+        if (fs->tu_split) {
             c.tu_split = split ? 2 : 1;
             if (split) ss.apply(c);
         }
         if (drop) {  // no residual left (chroma was dropped before coding): cu_summarise of zeros
-            c.tu_split = try_split ? 1 : 0;
+            c.tu_split = fs->tu_split ? 1 : 0;
             c.cbf = c.cbf_y4 = c.cbf_c4 = 0;
             c.last[0] = c.last[1] = c.last[2] = 0;
             c.csbf_y = 0;
             c.csbf_c[0] = c.csbf_c[1] = 0;
         }
+        set_est_bytes(c, split ? r2.bits : r.bits);
         cus[i] = c;  // skip / merge / AMVP are decided by k_hevc_decide once the slices are laid out
         cost[i] = cu_cost(c);
         qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
@@ -1067,7 +1090,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         }
         __syncthreads();
         const int i = valid ? y * g.mb_w + x : 0;
-        const TuResult res = code_tus(t, M, qp, qpc, true, valid, coef + (size_t)i * kCoefPerCu, fs->rec_y, g.pitch,
+        const TuResult res = code_tus<false>(t, M, qp, qpc, true, valid, coef + (size_t)i * kCoefPerCu, fs->rec_y, g.pitch,
                                       fs->rec_uv, x0, y0, g.width, g.height);
         if (valid) {
             acc[0] += (unsigned)res.sse[0];
@@ -1081,6 +1104,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 c.mvx = c.mvy = c.mvdx = c.mvdy = 0;
                 c.mvp_idx = 0;
                 fill_cu(c, res);
+                set_est_bytes(c, res.bits);
                 cus[i] = c;
                 cost[i] = cu_cost(c);
                 qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;

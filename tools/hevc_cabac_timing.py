@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--report", type=int, default=4)
     ap.add_argument("--wpp", type=int, default=1)
     ap.add_argument("--wpp-rows", type=int, default=8)
+    ap.add_argument("--slice-cost", type=int, default=0, help="P-slice work target (0: encoder default)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     import torch
@@ -41,6 +42,8 @@ def main():
     cfg.width, cfg.height, cfg.fps = a.width, a.height, 60
     cfg.bitrate_kbps = a.bitrate_kbps
     cfg.hevc_wpp, cfg.hevc_wpp_rows = a.wpp, a.wpp_rows
+    if a.slice_cost:
+        cfg.hevc_slice_cost = a.slice_cost
     enc = N.GpuHevcEncoder(cfg, torch.cuda.current_stream().cuda_stream)
     desk = CpuSyntheticDesktop(a.width, a.height, True)
     rows, allx, ally = [], [], []

@@ -18,3 +18,4 @@ for r in rows:
     n = re.sub(r"^.*::", "", n).replace("void ", "")
     print(f"{n:32s} calls={int(r['Calls']):5d} avg_us={float(r['AverageNs'])/1000:9.1f} pct={float(r['Percentage']):6.2f}")
 PY
+rm -rf $out/prof
