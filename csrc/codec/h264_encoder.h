@@ -56,7 +56,7 @@ struct EncoderConfig {
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
-    int hevc_slice_cost = 3072;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
+    int hevc_slice_cost = 2048;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
     // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): P pictures in slices of
     // hevc_wpp_rows CTU rows, every CTU row its own CABAC substream (one GPU wave each) that starts
     // from the contexts the row above had after its second CTU.  Off by default: a CTU row is a

@@ -2078,24 +2078,30 @@ MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, 
 // Entropy-coding cost estimate of a CU in CABAC work units: significance bins up to the
 // last position of every coded TU plus a few bins per coded sub-block, on top of the CU
 // header.  Used only to balance slices; identical on the CPU and the GPU.
-// Serial arithmetic-coder work of a CU, in units of ~0.11 us of k_hevc_arith wave time: the
-// two-phase coder's measured cost is 0.44 us per CTU + 0.63 us per payload byte
-// (profiles/r03_cabac/arith_timing_lean.log), so 4 units per CU + 6 per estimated byte.  (The
-// previous model -- last position + 8 per coded sub-block -- priced dense noise-like CUs at half
-// their real time, so the 4-CU slices through the noise panel ran 1.8x the median slice.)
-MXHD uint32_t cu_cost(const CuInfo& c) { return 4u + (c.cbf ? 6u * (uint32_t)c.est_bytes : 0u); }
+// Serial arithmetic-coder work of a CU in bin tokens (k_hevc_arith runs ~170 ns per token and
+// nothing measurable per CTU: tools/hevc_cabac_timing.py fit, profiles/r04_hevc/NOTES.md): ~7
+// tokens of CU / SAO syntax per CTU plus ~6 per payload byte of residual.  (The previous model --
+// last position + 8 per coded sub-block, 4 per CU -- priced dense noise-like CUs at half their
+// real time and static runs at half theirs, so slices ran up to 2.3x the median.)
+MXHD uint32_t cu_cost(const CuInfo& c) { return 7u + (c.cbf ? 6u * (uint32_t)c.est_bytes : 0u); }
 MXHD uint8_t est_bytes_of(uint32_t bits) {
     const uint32_t b = (bits + 7) >> 3;
     return (uint8_t)(b > 255u ? 255u : b);
 }
 // est_bytes of a summarised CU from the bits estimate of its final levels (cu_bits_est)
 MXHD void set_est_bytes(CuInfo& c, uint32_t bits) { c.est_bytes = c.cbf ? est_bytes_of(bits) : (uint8_t)0; }
-// Below this much work per slice, fewer slices: 3072 units keep a slice near 0.35 ms; the level's
+// Below this much work per slice, fewer slices: 2048 tokens keep a slice near 0.35 ms; the level's
 // slice limit usually binds first at 4K.
-constexpr uint32_t kCostPerSlice = 3072;  // EncoderConfig::hevc_slice_cost default
-// Number of slices for a P picture of total cost T, bounded by the level's slice limit.
+constexpr uint32_t kCostPerSlice = 2048;  // EncoderConfig::hevc_slice_cost default
+// Largest cu_cost (est_bytes is capped at 255).
+constexpr uint32_t kMaxCuCost = 7u + 6u * 255u;
+// Number of slices for a P picture of total cost T, bounded by the level's slice limit.  At least
+// kMaxCuCost + 1 per slice: then consecutive thresholds ceil(s * T / S) lie further apart than any
+// CU's cost, no CU spans two of them, and plan_slice_of() is also a CU's slice rank (the GPU layout
+// places every CU from its own prefix).
 MXHD int plan_num_slices(uint64_t total, int max_slices, uint32_t cost_per_slice = kCostPerSlice) {
-    const uint64_t s = total / (cost_per_slice ? cost_per_slice : 1u);
+    const uint32_t cps = cost_per_slice > kMaxCuCost ? cost_per_slice : kMaxCuCost + 1u;
+    const uint64_t s = total / cps;
     return s < 1 ? 1 : (s > (uint64_t)max_slices ? max_slices : (int)s);
 }
 // Slice of a CU whose exclusive cost prefix is `pre`: floor(pre * S / T) -- non-decreasing in

@@ -48,7 +48,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     // + one chunk of padding: k_hevc_arith reads whole 256-token chunks
     HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * h264::kSsePartStride));
-    HIP_CHECK(hipMalloc(&b.sse_tot, 4 * sizeof(unsigned long long)));
+    HIP_CHECK(hipMalloc(&b.sse_tot, kSseSlots * kSseSlotWords * sizeof(unsigned long long)));
     HIP_CHECK(hipMalloc(&b.wpp_ctx, sizeof(uint32_t) * kWppCtxWords * (size_t)geom_.mb_h));
     HIP_CHECK(hipMalloc(&b.wpp_flag, sizeof(uint32_t) * (size_t)geom_.mb_h));
     HIP_CHECK(hipMemsetAsync(b.wpp_flag, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));

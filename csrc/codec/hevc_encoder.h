@@ -175,6 +175,9 @@ struct HevcOutHeader {
 };
 static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
+// k_hevc_sao distortion totals: kSseSlots slots of one 64-byte line each (workgroup w adds into
+// slot w % kSseSlots), summed by k_hevc_pack
+constexpr int kSseSlots = 64, kSseSlotWords = 8;
 constexpr size_t kScanTilePad = 4096;  // per-CU scan arrays padded to this (hevc_kernels.hip kScanTile)
 constexpr int kMaxSliceRows = 4;  // CTU rows per slice the intra wavefront kernel supports
 constexpr int kWppCtxWords = (C_NUM + 3) / 4;  // context states, four per dword
@@ -208,7 +211,7 @@ struct HevcDeviceBuffers {
     int* wpp_err;                   // mapped host word
     size_t out_bytes;
     unsigned long long* sse_part;
-    unsigned long long* sse_tot;  // [4] k_hevc_sao distortion totals
+    unsigned long long* sse_tot;  // [kSseSlots][kSseSlotWords] k_hevc_sao distortion totals (4 used per slot)
 };
 
 // IDR + temporal AQ: the source luma into fs->save_src (pointer read on the device)

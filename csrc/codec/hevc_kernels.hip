@@ -1170,94 +1170,86 @@ constexpr int kScanTile = 4096;
 constexpr int kMaxScanTiles = 64;
 __device__ __forceinline__ uint4 ld4(const uint32_t* p, int i) { return *reinterpret_cast<const uint4*>(p + i); }
 
+// Tile prefixes of a per-CU array (tiles of kScanTile CUs, 4 per thread with one 16-byte load,
+// arrays zero-padded to whole tiles), computed by EVERY workgroup of a one-workgroup-per-tile
+// launch: the per-wave tile totals (wave_tot[t][w]) and the tiles' exclusive prefixes (tile_pre[t]);
+// returns the array total.  Re-reading the whole array per workgroup is a few 16-byte loads per
+// thread from L2 -- cheaper than a chained hand-off between the tiles' workgroups.
+__device__ __forceinline__ uint32_t tile_prefixes(const uint32_t* __restrict__ a, int ncu, uint32_t (*wave_tot)[16],
+                                                  uint32_t* tile_pre, uint32_t* total_sh) {
+    const int tid = threadIdx.x, wv = tid >> 6, nwv = (int)blockDim.x >> 6;
+    int nt = 0;
+#pragma unroll 4
+    for (int base = 0; base < ncu; base += kScanTile) {
+        const uint4 v = ld4(a, base + 4 * tid);
+        uint32_t w = v.x + v.y + v.z + v.w;
+        for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+        if ((tid & 63) == 0) wave_tot[nt][wv] = w;
+        ++nt;
+    }
+    __syncthreads();
+    if (tid < 64) {  // one wave: tile totals and their exclusive prefix (nt <= kMaxScanTiles = 64)
+        uint32_t sum = 0;
+        if (tid < nt)
+            for (int w = 0; w < nwv; ++w) sum += wave_tot[tid][w];
+        const uint32_t incl = wave_incl_scan(sum);
+        if (tid < nt) tile_pre[tid] = incl - sum;
+        if (tid == 63) *total_sh = incl;
+    }
+    __syncthreads();
+    return *total_sh;
+}
+// exclusive prefix of this thread's first CU in tile t (after tile_prefixes)
+__device__ __forceinline__ uint32_t tile_thread_prefix(const uint32_t (*wave_tot)[16], const uint32_t* tile_pre, int t,
+                                                       uint32_t sum4) {
+    const int wv = threadIdx.x >> 6;
+    uint32_t before = tile_pre[t];
+    for (int w = 0; w < wv; ++w) before += wave_tot[t][w];
+    return before + wave_incl_scan(sum4) - sum4;
+}
+
+// Slice layout, one workgroup per scan tile.  P pictures: cost-balanced raster runs --
+// plan_num_slices keeps every slice above the largest CU cost, so no CU spans two slice
+// thresholds and a CU's slice id (plan_slice_of of its cost prefix) is also its slice's rank:
+// every CU places itself from its prefix alone (the former one-workgroup kernel walked the
+// tiles in sequence: 39 us at 4K).
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ cost, int ncu, int ctb_w,
                                                        int max_slices, int slice_cost, int* __restrict__ slice_first,
                                                        int* __restrict__ slice_of_cu, uint32_t* __restrict__ nslices) {
-    __shared__ uint32_t wtot[16];
-    const int tid = threadIdx.x;
-    if (tid < 4) fs->sse_tot[tid] = 0ull;  // k_hevc_sao accumulates into these next
+    const int tid = threadIdx.x, t = blockIdx.x;
+    if (t == 0)
+        for (int k = tid; k < kSseSlots * kSseSlotWords; k += blockDim.x) fs->sse_tot[k] = 0ull;  // k_hevc_sao adds into these next
     if (fs->idr || fs->wpp) {  // I: fixed row slices; P with WPP: slices of wpp_rows rows (a substream per row)
         const int rows = ncu / ctb_w;
         const int sr = fs->idr ? fs->slice_rows : fs->wpp_rows;
         const int S = fs->idr ? fs->num_slices : (rows + sr - 1) / sr;
-        for (int k = tid; k < S; k += blockDim.x) slice_first[k] = k * sr * ctb_w;
-        for (int i = tid; i < ncu; i += blockDim.x) slice_of_cu[i] = (i / ctb_w) / sr;
-        if (tid == 0) *nslices = (uint32_t)S;
+        const int stride = (int)(gridDim.x * blockDim.x);
+        for (int k = t * (int)blockDim.x + tid; k < S; k += stride) slice_first[k] = k * sr * ctb_w;
+        for (int i = t * (int)blockDim.x + tid; i < ncu; i += stride) slice_of_cu[i] = (i / ctb_w) / sr;
+        if (t == 0 && tid == 0) *nslices = (uint32_t)S;
         return;
     }
-    // tiles of kScanTile CUs, 4 consecutive per thread with one 16-byte load (coalesced; the
-    // former per-thread contiguous chunks made every load touch 64 cache lines of one CU's
-    // memory pipeline: 67 us at 4K).  Pass 1: per-tile prefixes and the total.
-    // Tile totals by wave reductions and one LDS atomic per wave and tile (no workgroup barrier
-    // per tile), then their exclusive prefix.
-    // The per-wave totals of every tile are kept, so pass 2's cost prefix needs only a wave
-    // scan plus the earlier waves' totals (no workgroup barrier per tile).
     __shared__ uint32_t tile_pre[kMaxScanTiles];
     __shared__ uint32_t wave_tot[kMaxScanTiles][16];
     __shared__ uint32_t total_sh;
-    const int wv = tid >> 6, nwv = (int)blockDim.x >> 6;
-    int nt = 0;
-    for (int base = 0; base < ncu; base += kScanTile, ++nt) {
-        const uint4 v = ld4(cost, base + 4 * tid);
-        uint32_t w = v.x + v.y + v.z + v.w;
-        for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
-        if ((tid & 63) == 0) wave_tot[nt][wv] = w;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (int t = 0; t < nt; ++t) {
-            tile_pre[t] = run;
-            for (int w = 0; w < nwv; ++w) run += wave_tot[t][w];
-        }
-        total_sh = run;
-    }
-    __syncthreads();
-    const uint32_t total = total_sh;
+    const uint32_t total = tile_prefixes(cost, ncu, wave_tot, tile_pre, &total_sh);
     const int S = plan_num_slices(total, max_slices, (uint32_t)slice_cost);
-    // slice id of a prefix p is the number of thresholds T_s = ceil(s * total / S) (s >= 1) <= p:
-    // one division per thread and tile, then threshold tracking across its 4 CUs
-    auto thr = [&](int s2) -> uint64_t {
-        return s2 >= S ? ~0ull : floor_div52((uint64_t)s2 * total + (uint64_t)S - 1, (uint64_t)S);
-    };
-    uint32_t rank_carry = 0;
-    for (int t = 0, base = 0; base < ncu; base += kScanTile, ++t) {
-        const int i0 = base + 4 * tid;
-        const uint4 v = ld4(cost, i0);
-        const uint32_t c4[4] = {v.x, v.y, v.z, v.w};
-        const uint32_t sum4 = v.x + v.y + v.z + v.w;
-        uint32_t before = 0;
-        for (int w = 0; w < wv; ++w) before += wave_tot[t][w];
-        const uint32_t pre0 = tile_pre[t] + before + wave_incl_scan(sum4) - sum4;
-        int ids[4];
-        uint32_t nst = 0;
-        if (i0 < ncu) {
-            int cid = plan_slice_of(pre0, total, S);
-            int prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
-            uint64_t tnext = thr(cid + 1), pre = pre0;
-            for (int e = 0; e < 4; ++e) {
-                while (pre >= tnext) tnext = thr(++cid + 1);
-                ids[e] = cid;
-                nst += (i0 + e < ncu && cid != prev) ? 1u : 0u;
-                prev = cid;
-                pre += c4[e];
-            }
+    const int i0 = t * kScanTile + 4 * tid;
+    const uint4 v = ld4(cost, i0);
+    const uint32_t c4[4] = {v.x, v.y, v.z, v.w};
+    uint64_t pre = tile_thread_prefix(wave_tot, tile_pre, t, v.x + v.y + v.z + v.w);
+    if (i0 < ncu) {
+        int prev = i0 > 0 ? plan_slice_of(pre - cost[i0 - 1], total, S) : -1;
+        for (int e = 0; e < 4 && i0 + e < ncu; ++e) {
+            const int id = plan_slice_of(pre, total, S);
+            if (id != prev) slice_first[id] = i0 + e;
+            slice_of_cu[i0 + e] = id;
+            prev = id;
+            pre += c4[e];
         }
-        uint32_t tile_starts;
-        const uint32_t rbase = rank_carry + block_excl_scan(nst, wtot, &tile_starts);
-        if (i0 < ncu) {
-            int rank = (int)rbase - 1;
-            int prev = i0 > 0 ? plan_slice_of(pre0 - cost[i0 - 1], total, S) : -1;
-            for (int e = 0; e < 4 && i0 + e < ncu; ++e) {
-                if (ids[e] != prev) slice_first[++rank] = i0 + e;
-                slice_of_cu[i0 + e] = rank;
-                prev = ids[e];
-            }
-        }
-        rank_carry += tile_starts;
     }
-    if (tid == 0) *nslices = rank_carry;
+    if (t == 0 && tid == 0) *nslices = (uint32_t)S;
 }
 
 // Skip / merge / AMVP of every CU of a P picture against its slice's neighbours.
@@ -1344,21 +1336,19 @@ __global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameSta
 }
 
 // Exclusive prefix of the token counts in decoding (raster) order: off[i], off[ncu] = total.
-// One 1024-thread workgroup over tiles of kScanTile counts (16-byte loads and stores).
+// One 1024-thread workgroup per scan tile (tile_prefixes), 16-byte loads and stores.
 __global__ __launch_bounds__(1024) void k_hevc_tokscan(const uint32_t* __restrict__ ntok, int ncu,
                                                         uint32_t* __restrict__ off) {
-    __shared__ uint32_t wtot[16];
-    const int tid = threadIdx.x;
-    uint32_t carry = 0;
-    for (int base = 0; base < ncu; base += kScanTile) {
-        const int i = base + 4 * tid;
-        const uint4 v = ld4(ntok, i);
-        uint32_t tt;
-        const uint32_t pre = carry + block_excl_scan(v.x + v.y + v.z + v.w, wtot, &tt);
-        *reinterpret_cast<uint4*>(off + i) = make_uint4(pre, pre + v.x, pre + v.x + v.y, pre + v.x + v.y + v.z);
-        carry += tt;
-    }
-    if (tid == 0) off[ncu] = carry;
+    __shared__ uint32_t tile_pre[kMaxScanTiles];
+    __shared__ uint32_t wave_tot[kMaxScanTiles][16];
+    __shared__ uint32_t total_sh;
+    const int tid = threadIdx.x, t = blockIdx.x;
+    const uint32_t total = tile_prefixes(ntok, ncu, wave_tot, tile_pre, &total_sh);
+    const int i = t * kScanTile + 4 * tid;
+    const uint4 v = ld4(ntok, i);
+    const uint32_t pre = tile_thread_prefix(wave_tot, tile_pre, t, v.x + v.y + v.z + v.w);
+    *reinterpret_cast<uint4*>(off + i) = make_uint4(pre, pre + v.x, pre + v.x + v.y, pre + v.x + v.y + v.z);
+    if (t == 0 && tid == 0) off[ncu] = total;  // (the padded tail of the last tile holds the total too)
 }
 
 // One wave per CTU: copy its tokens from the fixed slot to the dense run.
@@ -1907,9 +1897,12 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         part[3][wave] = valid && !in_mask ? (unsigned long long)ey : 0ull;
     }
     __syncthreads();
-    if (threadIdx.x < 4) {  // one atomic per workgroup and channel (k_hevc_pack reads the totals)
+    if (threadIdx.x < 4) {  // one atomic per workgroup and channel into one of kSseSlots 64-byte slots
+        // (8,100 workgroups adding into the same 4 words serialised in one L2 channel: ~100 us of
+        // k_hevc_sao at 4K); k_hevc_pack sums the slots
         const int c = threadIdx.x;
-        atomicAdd(fs->sse_tot + c, part[c][0] + part[c][1] + part[c][2] + part[c][3]);
+        atomicAdd(fs->sse_tot + (size_t)(blockIdx.x % kSseSlots) * kSseSlotWords + c,
+                  part[c][0] + part[c][1] + part[c][2] + part[c][3]);
     }
 }
 
@@ -2012,7 +2005,7 @@ __global__ __launch_bounds__(256) void k_hevc_pack(Geometry g, const HevcFrameSt
     unsigned long long e[4] = {0, 0, 0, 0};
     if (fs->sao) {  // totals accumulated by k_hevc_sao (a serial walk over 8,100 partials x 4 was
                     // ~30 us at the end of the entropy stream)
-        if (tid < 4) e[tid] = fs->sse_tot[tid];
+        if (tid < 4 * kSseSlots) e[tid & 3] = fs->sse_tot[(size_t)(tid >> 2) * kSseSlotWords + (tid & 3)];
     } else {
         const int num_sse_parts = fs->n_sse_parts;
 #pragma unroll 4
@@ -2086,7 +2079,7 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,
                         bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_hevc_layout, dim3(1), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, slice_cost, b.slice_first,
+    hipLaunchKernelGGL(k_hevc_layout, dim3((ncu + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, slice_cost, b.slice_first,
                        b.slice_of_cu, b.nslices);
     if (!idr)
         hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
@@ -2110,7 +2103,7 @@ void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_
     if ((ncu + kScanTile - 1) / kScanTile > kMaxScanTiles) throw std::invalid_argument("hevc: picture too large");
     hipLaunchKernelGGL(k_hevc_bins, dim3(ncu), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.sao,
                        b.slice_first, b.slice_of_cu, b.nslices, b.qpy, b.tok, b.ntok);
-    hipLaunchKernelGGL(k_hevc_tokscan, dim3(1), dim3(1024), 0, s, b.ntok, ncu, b.tok_off);
+    hipLaunchKernelGGL(k_hevc_tokscan, dim3((ncu + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.ntok, ncu, b.tok_off);
     hipLaunchKernelGGL(k_hevc_tokgather, dim3((ncu + 3) / 4), dim3(256), 0, s, b.tok, b.ntok, b.tok_off, ncu,
                        b.tok_dense);
     const int max_subs = std::max(max_slices, g.mb_h);  // substreams: slices, or CTU rows with WPP
