@@ -731,5 +731,17 @@ PYBIND11_MODULE(_native, m) {
                  return py::make_tuple(copy_plane(s.encoder().recon_y(), g.pitch, g.coded_w, g.coded_h),
                                        copy_plane(s.encoder().recon_uv(), g.pitch, g.coded_w, g.coded_h / 2));
              })
-        .def_property_readonly("stats", [](Session& s) { return s.encoder().last_stats(); });
+        .def_property_readonly("stats", [](Session& s) { return s.encoder().last_stats(); })
+        .def("slice_timing",
+             [](Session& s) {
+                 // HEVC only: per-substream CABAC timing of the last collected picture (GpuHevcEncoder)
+                 auto* e = dynamic_cast<hevc::GpuHevcEncoder*>(&s.encoder());
+                 if (!e) throw std::invalid_argument("slice_timing: HEVC sessions only");
+                 return e->slice_timing();
+             })
+        .def("cu_token_table", [](Session& s) {
+            auto* e = dynamic_cast<hevc::GpuHevcEncoder*>(&s.encoder());
+            if (!e) throw std::invalid_argument("cu_token_table: HEVC sessions only");
+            return e->cu_token_table();
+        });
 }

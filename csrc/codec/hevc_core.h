@@ -2079,11 +2079,20 @@ MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, 
 // last position of every coded TU plus a few bins per coded sub-block, on top of the CU
 // header.  Used only to balance slices; identical on the CPU and the GPU.
 // Serial arithmetic-coder work of a CU in bin tokens (k_hevc_arith runs ~170 ns per token and
-// nothing measurable per CTU: tools/hevc_cabac_timing.py fit, profiles/r04_hevc/NOTES.md): ~7
-// tokens of CU / SAO syntax per CTU plus ~6 per payload byte of residual.  (The previous model --
-// last position + 8 per coded sub-block, 4 per CU -- priced dense noise-like CUs at half their
-// real time and static runs at half theirs, so slices ran up to 2.3x the median.)
-MXHD uint32_t cu_cost(const CuInfo& c) { return 7u + (c.cbf ? 6u * (uint32_t)c.est_bytes : 0u); }
+// nothing measurable per CTU: tools/hevc_cabac_timing.py).  Least-squares fit over the CUs of 4K
+// bench P pictures (tools/hevc_session_timing.py --dump, profiles/r04_hevc/NOTES.md): a CU
+// without residual ~4 tokens; a coded CU 1 + (sum of last+1) / 4 + 15 per coded sub-block + 2.6
+// per estimated payload byte, 2.2 % mean error.  (The earlier byte-only model, 6 tokens per byte,
+// missed the ~13 tokens per byte of the noise panel's small levels: its slices ran 2.4x the
+// median.)
+MXHD uint32_t cu_cost(const CuInfo& c) {
+    if (!c.cbf) return 4u;
+    uint32_t lsum = 0, sb = 0;
+    if (c.cbf & 1) lsum += c.last[0] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_y);
+    if (c.cbf & 2) lsum += c.last[1] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[0]);
+    if (c.cbf & 4) lsum += c.last[2] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[1]);
+    return 1u + (lsum >> 2) + 15u * sb + ((21u * (uint32_t)c.est_bytes) >> 3);
+}
 MXHD uint8_t est_bytes_of(uint32_t bits) {
     const uint32_t b = (bits + 7) >> 3;
     return (uint8_t)(b > 255u ? 255u : b);
@@ -2093,8 +2102,8 @@ MXHD void set_est_bytes(CuInfo& c, uint32_t bits) { c.est_bytes = c.cbf ? est_by
 // Below this much work per slice, fewer slices: 2048 tokens keep a slice near 0.35 ms; the level's
 // slice limit usually binds first at 4K.
 constexpr uint32_t kCostPerSlice = 2048;  // EncoderConfig::hevc_slice_cost default
-// Largest cu_cost (est_bytes is capped at 255).
-constexpr uint32_t kMaxCuCost = 7u + 6u * 255u;
+// Largest cu_cost (last+1 <= 256 + 64 + 64, 16 + 4 + 4 sub-blocks, est_bytes <= 255).
+constexpr uint32_t kMaxCuCost = 1u + (384u >> 2) + 15u * 24u + ((21u * 255u) >> 3);
 // Number of slices for a P picture of total cost T, bounded by the level's slice limit.  At least
 // kMaxCuCost + 1 per slice: then consecutive thresholds ceil(s * T / S) lie further apart than any
 // CU's cost, no CU spans two of them, and plan_slice_of() is also a CU's slice rank (the GPU layout

@@ -370,5 +370,24 @@ std::vector<std::array<uint64_t, 6>> GpuHevcEncoder::slice_timing() const {
     return out;
 }
 
+std::vector<std::array<uint32_t, 6>> GpuHevcEncoder::cu_token_table() const {
+    std::vector<std::array<uint32_t, 6>> out;
+    if (last_slot_ < 0) return out;
+    const size_t ncu = (size_t)geom_.mb_w * geom_.mb_h;
+    std::vector<CuInfo> cus(ncu);
+    std::vector<uint32_t> ntok(ncu);
+    HIP_CHECK(hipMemcpy(cus.data(), slots_[last_slot_].buf.cu, sizeof(CuInfo) * ncu, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(ntok.data(), slots_[last_slot_].buf.ntok, sizeof(uint32_t) * ncu, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ncu; ++i) {
+        const CuInfo& c = cus[i];
+        uint32_t lsum = 0, sb = 0;
+        if (c.cbf & 1) lsum += c.last[0] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_y);
+        if (c.cbf & 2) lsum += c.last[1] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[0]);
+        if (c.cbf & 4) lsum += c.last[2] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[1]);
+        out.push_back({c.type, c.cbf, lsum, sb, c.est_bytes, ntok[i]});
+    }
+    return out;
+}
+
 }  // namespace hevc
 }  // namespace mx

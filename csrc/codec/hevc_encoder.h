@@ -253,6 +253,9 @@ class GpuHevcEncoder final : public VideoEncoder {
     // per substream of the last picture: first CTU, CTUs, bytes, wave ticks (100 MHz), start tick
     // relative to the earliest wave, tokens coded
     std::vector<std::array<uint64_t, 6>> slice_timing() const;
+    // diagnostics: per-CU (type, cbf, sum of last+1, coded sub-blocks, est_bytes, tokens) of the last
+    // collected picture (the CU cost model's calibration data, tools/hevc_session_timing.py)
+    std::vector<std::array<uint32_t, 6>> cu_token_table() const;
    private:
     int mask_c_[4] = {0, 0, 0, 0};
     int64_t masked_pixels_ = 0;
