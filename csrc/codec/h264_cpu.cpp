@@ -456,16 +456,18 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             // temporal class: the source's change against the previous source, displaced by the
             // integer part of each sample's vector (aq 3)
             uint32_t tsad = 0;
+            bool zero_mv = true;
             if (cfg_.aq >= 3 && !prev_src_.empty()) {
                 for (int r = 0; r < 16; ++r)
                     for (int k = 0; k < 16; ++k) {
                         const Mv v = px_mv(m, k, r);
+                        zero_mv = zero_mv && v.x == 0 && v.y == 0;
                         tsad += (uint32_t)std::abs((int)sy[(y0 + r) * pitch + x0 + k] -
                                                    (int)ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + k + (v.x >> 2),
                                                                y0 + r + (v.y >> 2)));
                     }
             }
-            const int tcls = temporal_class(tsad);
+            const int tcls = temporal_class(tsad, zero_mv);
             const int qp = mb_qp_for(frame_qp, lsad, tcls, cfg_.aq);
             const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
             m.qp = (uint8_t)qp;

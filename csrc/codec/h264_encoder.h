@@ -38,12 +38,15 @@ struct EncoderConfig {
                               // 0: exhaustive +-range search
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
-    int aq = 3;               // adaptive quantisation of P macroblocks (mb_qp_delta): 1 coarser QP for
-                              // noise-like residuals, 2 adds their rate-distortion residual drop, 3 (H.264
-                              // default) temporal classes of the source -- persistent content finer, changing
-                              // content coarser, its chroma dropped and its luma residual kept only when it
-                              // pays for its bits (h264_mb.h temporal_class; HEVC has 0, 1 and 3, and treats
-                              // 2 as 1)
+    int aq = 4;               // adaptive quantisation of P macroblocks (mb_qp_delta): 1 coarser QP for
+                              // noise-like residuals, 2 adds their rate-distortion residual drop, 3 temporal
+                              // classes of the source -- persistent content 6 QP finer, changing content 6
+                              // coarser, its chroma dropped and its luma residual kept only when it pays for
+                              // its bits (h264_mb.h temporal_class); 4 (default), 5, 6: as 3 with static
+                              // content (identical source, zero vector) 9 / 12 / 15 QP finer -- 4K desktop
+                              // +0.6 dB (H.264) / +1.4 dB (HEVC) masked Y-PSNR at equal rate, motion content
+                              // unchanged (profiles/r04_hevc/NOTES.md).  HEVC has 0, 1 and 3+, and treats 2
+                              // as 1
     // in-loop deblocking filter: 1 on, 0 off, -1 the codec's default -- HEVC on (8.7.2, fully
     // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it cost
     // 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)

@@ -864,7 +864,7 @@ __global__ __launch_bounds__(256) void k_inter_encode(Geometry g, const FrameSta
     }
     __syncthreads();
     const uint32_t lsad_mb = (uint32_t)wave_sum(lsad);
-    const int tcls = temporal_class((uint32_t)wave_sum(tsad));
+    const int tcls = temporal_class((uint32_t)wave_sum(tsad), __ballot((mvx | mvy) != 0) == 0ull);
     const int qp = mb_qp_for(fs->qp, lsad_mb, tcls, fs->aq);  // wave-uniform
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     int16_t* mc = coef + (size_t)(valid ? mbi : 0) * kCoefStride;

@@ -277,18 +277,28 @@ MXHD bool drop_residual(int aq, uint32_t lsad, int qp, long long d_pred, long lo
 //  * anything else at the frame QP.
 constexpr uint32_t kTsadChanging = 256u * 24, kTsadPersistent = 256u * 2;
 constexpr int kAqChangingOffset = 6, kAqPersistentOffset = -6;
-enum TClass : int { kTcNormal = 0, kTcPersistent = 1, kTcChanging = 2 };
-MXHD int temporal_class(uint32_t tsad) {
-    return tsad > kTsadChanging ? kTcChanging : (tsad <= kTsadPersistent ? kTcPersistent : kTcNormal);
+// Static content (aq >= 4): a block whose source is bit-identical to the previous source with a zero
+// vector is coded once and then skipped for as long as it stays -- refined 9 / 12 / 15 QP finer
+// (aq 4 / 5 / 6) than the frame QP; only rigidly MOVING persistent content (a pan, a scroll) keeps
+// -6, since there every frame re-spends the finer QP on the newly exposed / re-predicted blocks and
+// the rate control raises the frame QP for everything (profiles/r04_hevc/NOTES.md: aq 5 on the
+// motion content cost 5 dB when the offset applied to every persistent block).
+MXHD int aq_static_offset(int aq) { return kAqPersistentOffset - 3 * ((aq > 6 ? 6 : aq) - 3); }
+enum TClass : int { kTcNormal = 0, kTcPersistent = 1, kTcChanging = 2, kTcStatic = 3 };
+MXHD int temporal_class(uint32_t tsad, bool zero_mv) {
+    return tsad > kTsadChanging ? kTcChanging
+                                : (tsad == 0 && zero_mv ? kTcStatic : (tsad <= kTsadPersistent ? kTcPersistent : kTcNormal));
 }
-MXHD int aq3_mb_qp(int frame_qp, int tclass) {
-    const int q = frame_qp + (tclass == kTcChanging ? kAqChangingOffset
-                                                    : (tclass == kTcPersistent ? kAqPersistentOffset : 0));
+MXHD int aq3_mb_qp(int frame_qp, int tclass, int aq = 3) {
+    const int q = frame_qp + (tclass == kTcChanging     ? kAqChangingOffset
+                              : tclass == kTcStatic     ? aq_static_offset(aq)
+                              : tclass == kTcPersistent ? kAqPersistentOffset
+                                                        : 0);
     return q < 0 ? 0 : (q > 51 ? 51 : q);
 }
 // MB QP and residual-drop decision of a P macroblock for any aq mode (aq >= 3 uses tclass).
 MXHD int mb_qp_for(int frame_qp, uint32_t lsad, int tclass, int aq) {
-    return aq >= 3 ? aq3_mb_qp(frame_qp, tclass) : aq_mb_qp(frame_qp, lsad, aq);
+    return aq >= 3 ? aq3_mb_qp(frame_qp, tclass, aq) : aq_mb_qp(frame_qp, lsad, aq);
 }
 MXHD bool drop_luma_for(int aq, uint32_t lsad, int tclass, int qp, long long d_pred, long long d_coded,
                         uint32_t bits) {

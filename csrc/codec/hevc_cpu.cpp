@@ -509,7 +509,7 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                         tsad += (uint32_t)std::abs((int)sy[(y0 + r) * pitch + x0 + q] -
                                                    h264::ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + q + (c.mvx >> 2),
                                                                 y0 + r + (c.mvy >> 2)));
-            const int tcls = h264::temporal_class(tsad);
+            const int tcls = h264::temporal_class(tsad, c.mvx == 0 && c.mvy == 0);
             const int qp = h264::mb_qp_for(fqp, lsad, tcls, cfg_.aq);
             const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
             const bool changing = cfg_.aq >= 3 && tcls == h264::kTcChanging;

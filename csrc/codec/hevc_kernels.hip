@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
             dcp[comp] = (2 * xc < g.width && 2 * yc < g.height) ? (s - p) * (s - p) : 0;
         }
     }
-    const int tcls = h264::temporal_class((uint32_t)wsum(tsad));
+    const int tcls = h264::temporal_class((uint32_t)wsum(tsad), mvx == 0 && mvy == 0);  // vector wave-uniform
     const int qp = h264::mb_qp_for(fs->qp, (uint32_t)wsum(lsad), tcls, fs->aq);  // wave-uniform
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     // changing content (aq 3): chroma residual dropped, luma kept only if it pays for its bits

@@ -61,8 +61,8 @@ def test_static_content_skips(native):
     enc = native.CpuH264Encoder(cfg)
     y, uv = synthetic_nv12(64, 48, 0)
     big = len(enc.encode(y, uv, False))
-    # aq 3 (default): the unchanged source is "persistent" content, refined once 6 QP finer
-    # than the IDR, then skipped
+    # aq 4 (default): the unchanged source (zero vector) is "static" content, refined once 9 QP
+    # finer than the IDR, then skipped
     enc.encode(y, uv, False)
     small = len(enc.encode(y, uv, False))
     assert enc.stats.skipped_mbs >= 6

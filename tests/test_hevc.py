@@ -252,12 +252,14 @@ def test_gpu_hevc_tu_split_bit_exact_vs_cpu(gpu, w, h, qp):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,qp,tu_split", [(320, 192, 30, 0), (320, 192, 26, 1), (1920, 1080, 34, 1)])
-def test_gpu_hevc_temporal_classes_bit_exact_vs_cpu(gpu, w, h, qp, tu_split):
-    """aq 3 on the synthetic desktop (animated noise panel = changing content, static windows =
-    persistent): temporal classes, chroma drop and the luma residual drop decide the same on the
-    GPU and the CPU, bit for bit, and the stream decodes to the GPU reconstruction."""
-    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=tu_split, aq=3, desktop=True)
+@pytest.mark.parametrize("w,h,qp,tu_split,aq", [(320, 192, 30, 0, 3), (320, 192, 26, 1, 3), (1920, 1080, 34, 1, 3),
+                                                 (320, 192, 30, 1, 4), (1920, 1080, 34, 1, 6)])
+def test_gpu_hevc_temporal_classes_bit_exact_vs_cpu(gpu, w, h, qp, tu_split, aq):
+    """aq 3+ on the synthetic desktop (animated noise panel = changing content, static windows =
+    static / persistent; aq 4+ refines the static class 9+ QP finer): temporal classes, chroma drop
+    and the luma residual drop decide the same on the GPU and the CPU, bit for bit, and the stream
+    decodes to the GPU reconstruction."""
+    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=tu_split, aq=aq, desktop=True)
 
 
 @pytest.mark.gpu
