@@ -13,12 +13,13 @@
 //   with one reference picture, MaxNumMergeCand 5, no TMVP, no sign hiding, cu_qp_delta per CU
 //   (adaptive quantisation); in-loop deblocking (8.7.2) and sample adaptive offset (8.7.3, band /
 //   edge per CTB) on by default.
-// Slices and CABAC substreams (EncoderConfig.hevc_wpp, default on): wavefront parallel
-//   processing -- I pictures in slices of up to kMaxSliceRows CTU rows (the intra wavefront's
-//   workgroup), P pictures one slice; every CTU row is a CABAC substream entropy coded by its
-//   own GPU wave, starting from the contexts the row above had after its second CTU, with entry
-//   points in the slice header.  hevc_wpp 0: cost-balanced P slices (plan_num_slices), one
-//   substream each.
+// Slices and CABAC substreams: I pictures in slices of up to kMaxSliceRows CTU rows (the intra
+//   wavefront's workgroup); P pictures (default, EncoderConfig.hevc_wpp 0) in up to the level's
+//   slice limit of raster runs balanced on an estimate of their bin tokens (cu_cost,
+//   plan_num_slices), one substream each.  hevc_wpp 1: wavefront parallel processing -- slices of
+//   hevc_wpp_rows CTU rows, every CTU row a CABAC substream entropy coded by its own GPU wave,
+//   starting from the contexts the row above had after its second CTU, with entry points in the
+//   slice header (+0.3 dB at half the 4K rate: profiles/r04_hevc/NOTES.md).
 //
 // Replaces NVENC HEVC behind the reference's GStreamer stack (nvh264enc default encoder,
 // reference Dockerfile:210 / README.md:21; BASELINE.json config "4K60 HEVC").
