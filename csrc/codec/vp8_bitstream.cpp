@@ -221,6 +221,14 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
     int coded = 0;
     for (int i = 0; i < nmb; ++i) coded += mbs[i].nz != 0;
     const int prob_skip_false = std::clamp((coded * 256 + nmb / 2) / std::max(1, nmb), 1, 255);
+    // segment tree probabilities (9.3, mb_segment_tree {2, 4, -0, -1, -2, -3}) from this frame's
+    // segment histogram: p0 = P(segment < 2), p1 = P(1 | < 2), p2 = P(3 | >= 2)
+    int seg_n[kNumSegs] = {0, 0, 0, 0};
+    if (f.segmented)
+        for (int i = 0; i < nmb; ++i) ++seg_n[mbs[i].seg & 3];
+    auto prob_of = [](int zero, int total) { return total ? std::clamp((zero * 256 + total / 2) / total, 1, 255) : 255; };
+    const int seg_p[3] = {prob_of(seg_n[0] + seg_n[1], nmb), prob_of(seg_n[0], seg_n[0] + seg_n[1]),
+                          prob_of(seg_n[2], seg_n[2] + seg_n[3])};
     // ---- first partition
     std::vector<uint8_t> p1;
     p1.reserve(16 + (size_t)nmb / 2);
@@ -230,7 +238,22 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
             e.literal(0, 1);  // color_space
             e.literal(0, 1);  // clamping_type (decoder clamps reconstructed samples)
         }
-        e.literal(0, 1);  // segmentation_enabled
+        e.literal(f.segmented ? 1 : 0, 1);  // segmentation_enabled
+        if (f.segmented) {
+            e.literal(1, 1);  // update_mb_segmentation_map
+            e.literal(1, 1);  // update_segment_feature_data
+            e.literal(1, 1);  // segment_feature_mode: absolute values
+            for (int k = 0; k < kNumSegs; ++k) {  // quantizer: the segment's y_ac_qi
+                e.literal(1, 1);
+                e.literal((uint32_t)f.seg_qindex[k], 7);
+                e.literal(0, 1);  // sign
+            }
+            for (int k = 0; k < kNumSegs; ++k) e.literal(0, 1);  // no loop-filter level updates
+            for (int k = 0; k < 3; ++k) {  // segment tree probabilities
+                e.literal(1, 1);
+                e.literal((uint32_t)seg_p[k], 8);
+            }
+        }
         e.literal(0, 1);  // filter_type (normal)
         e.literal(0, 6);  // loop_filter_level 0: no loop filter
         e.literal(0, 3);  // sharpness_level
@@ -266,6 +289,11 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         for (int mby = 0; mby < f.mb_h; ++mby)
             for (int mbx = 0; mbx < f.mb_w; ++mbx) {
                 const Vp8Mb& m = mbs[mby * f.mb_w + mbx];
+                if (f.segmented) {  // segment_id
+                    const int sg = m.seg & 3;
+                    e.put(seg_p[0], sg >= 2);
+                    e.put(sg >= 2 ? seg_p[2] : seg_p[1], sg & 1);
+                }
                 e.put(prob_skip_false, m.nz == 0);
                 if (f.key) {
                     const uint8_t* p = kKfYModeProb;  // tree: B_PRED "0", DC "100", V "101", H "110", TM "111"

@@ -10,7 +10,9 @@
 // Coding subset (what this encoder emits): key frames of 16x16-predicted macroblocks (DC / V / H /
 // TM luma, DC / V / H / TM chroma, Y2 second-order block); inter frames of 16x16 inter macroblocks
 // predicting from the last frame with full-sample vectors (ZEROMV / NEARESTMV / NEARMV / NEWMV);
-// one quantiser per frame; loop filter level 0; token partitions by MB row; default probabilities.
+// inter frames segmented (9.3) by the temporal classes of the H.264 encoder's adaptive
+// quantisation -- four segment quantisers, a per-macroblock segment map -- key frames one
+// quantiser; loop filter level 0; token partitions by MB row; default probabilities.
 #pragma once
 #include <stdint.h>
 
@@ -35,7 +37,8 @@ struct Vp8Mb {
     int16_t mvx, mvy;  // luma vector, 1/8-sample units (always a multiple of 8 here: full samples)
     uint8_t ymode;     // YMode
     uint8_t uvmode;    // DC / V / H / TM
-    uint8_t pad0, pad1;
+    uint8_t seg;       // segment (Seg; 0 in key frames)
+    uint8_t pad1;
     uint32_t nz;       // bit b: block b (0..24) has a non-zero level
     uint32_t slot;     // GPU: index of the macroblock's levels in the compacted level buffer
     uint32_t sse[3];   // GPU: Y / U / V distortion over the display area
@@ -70,6 +73,16 @@ constexpr uint8_t kModeContexts[6][4] = {{7, 1, 1, 143},     {14, 18, 14, 107}, 
                                          {60, 56, 128, 65},  {159, 134, 128, 34}, {234, 188, 128, 28}};
 
 MXV8 int v8_clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// ---------------------------------------------------------------- segments (9.3)
+// Inter-frame segments = the temporal classes of h264_mb.h (temporal_class / aq3_mb_qp): the
+// segment quantiser is the class's QP offset from the frame QP, sent as absolute quantiser
+// indices; segment ids are coded in every inter frame's macroblock headers.
+enum Seg : uint8_t { kSegNormal = 0, kSegStatic = 1, kSegPersistent = 2, kSegChanging = 3 };
+constexpr int kNumSegs = 4;
+// h264_mb.h TClass (kTcNormal 0, kTcPersistent 1, kTcChanging 2, kTcStatic 3) -> Seg, and back
+MXV8 int seg_of_tclass(int tc) { return tc == 1 ? kSegPersistent : (tc == 2 ? kSegChanging : (tc == 3 ? kSegStatic : kSegNormal)); }
+MXV8 int tclass_of_seg(int seg) { return seg == kSegPersistent ? 1 : (seg == kSegChanging ? 2 : (seg == kSegStatic ? 3 : 0)); }
 
 // ---------------------------------------------------------------- quantisers (14.1, 9.6)
 struct Quant {

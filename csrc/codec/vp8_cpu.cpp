@@ -46,6 +46,7 @@ CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg) : cfg_(cfg), common
 
 void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bool key, int qindex) {
     const Quant Q = quant_of(qindex);
+    if (cfg_.aq >= 3) next_src_.assign((size_t)cw_ * ch_, 0);
     uint8_t* ry = rec_y_[cur_].data();
     uint8_t* ruv = rec_uv_[cur_].data();
     const uint8_t* fy = rec_y_[cur_ ^ 1].data();
@@ -102,6 +103,14 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 int lo_x, hi_x, lo_y, hi_y;
                 mv_bounds(mb_w_, mb_h_, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
                 const int ix = std::clamp(mvx / 4, lo_x, hi_x), iy = std::clamp(mvy / 4, lo_y, hi_y);
+                if (cfg_.aq >= 3) {  // temporal class of the macroblock -> its segment (quantiser)
+                    uint32_t tsad = 0;
+                    for (int y = 0; y < 16; ++y)
+                        for (int x = 0; x < 16; ++x)
+                            tsad += (uint32_t)std::abs((int)sy[(y0 + y) * pitch + x0 + x] -
+                                                       h264::ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + x + ix, y0 + y + iy));
+                    m.seg = (uint8_t)seg_of_tclass(h264::temporal_class(tsad, ix == 0 && iy == 0));
+                }
                 m.ymode = kInter;
                 m.mvx = (int16_t)(ix * 8);
                 m.mvy = (int16_t)(iy * 8);
@@ -127,9 +136,10 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 for (int y = 0; y < 8; ++y)
                     for (int x = 0; x < 8; ++x)
                         cres[c][y * 8 + x] = suv[(y0 / 2 + y) * pitch + x0 + 2 * x + c] - cp[c][y * 8 + x];
-            m.nz = code_luma16(res, pred, Q, lv, rec);
-            m.nz |= code_chroma8(cres[0], cp[0], Q, lv, crec[0], 16);
-            m.nz |= code_chroma8(cres[1], cp[1], Q, lv, crec[1], 20);
+            const Quant Qm = m.seg ? quant_of(seg_qindex_[m.seg]) : (key ? Q : quant_of(seg_qindex_[0]));
+            m.nz = code_luma16(res, pred, Qm, lv, rec);
+            m.nz |= code_chroma8(cres[0], cp[0], Qm, lv, crec[0], 16);
+            m.nz |= code_chroma8(cres[1], cp[1], Qm, lv, crec[1], 20);
             if (!key) {  // noise-like residual that does not pay for its bits: prediction only
                 uint32_t lsad = 0, bits = 0;
                 long long dp = 0, dc = 0;
@@ -157,6 +167,8 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
             }
             for (int y = 0; y < 16; ++y)
                 for (int x = 0; x < 16; ++x) ry[(y0 + y) * cw_ + x0 + x] = (uint8_t)rec[y * 16 + x];
+            if (cfg_.aq >= 3)  // the next frame's previous source
+                for (int y = 0; y < 16; ++y) std::memcpy(&next_src_[(size_t)(y0 + y) * cw_ + x0], sy + (y0 + y) * pitch + x0, 16);
             for (int c = 0; c < 2; ++c)
                 for (int y = 0; y < 8; ++y)
                     for (int x = 0; x < 8; ++x) ruv[(y0 / 2 + y) * cw_ + x0 + 2 * x + c] = (uint8_t)crec[c][y * 8 + x];
@@ -180,10 +192,16 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     cur_ ^= 1;
     const bool key = common_.cur_idr();
     const int qindex = qindex_for_qp(common_.cur_qp());
+    FrameDesc fd{key, cfg_.width, cfg_.height, mb_w_, mb_h_, qindex, log2_parts};
+    fd.segmented = !key && cfg_.aq >= 3;
+    for (int k = 0; k < kNumSegs; ++k) seg_qindex_[k] = qindex;
+    if (fd.segmented) segment_qindices(common_.cur_qp(), cfg_.aq, seg_qindex_);
+    for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = seg_qindex_[k];
     analyse(y, uv, pitch, key, qindex);
+    if (cfg_.aq >= 3) prev_src_.swap(next_src_);
     au_.clear();
-    write_frame(FrameDesc{key, cfg_.width, cfg_.height, mb_w_, mb_h_, qindex, log2_parts}, mb_.data(),
-                [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, au_, run_serial);
+    write_frame(fd, mb_.data(), [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, au_,
+                run_serial);
     int skipped = 0;
     for (const Vp8Mb& m : mb_) skipped += m.nz == 0;
     stats_.frame_index = common_.frames();

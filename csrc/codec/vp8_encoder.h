@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "h264_encoder.h"
+#include "h264_mb.h"
 #include "video_encoder.h"
 #include "vp8_core.h"
 
@@ -72,7 +73,13 @@ struct FrameDesc {
     int width, height, mb_w, mb_h;
     int qindex;
     int log2_parts;  // token partitions: 1 << log2_parts
+    bool segmented = false;          // inter frames with aq >= 3: segment map + segment quantisers
+    int seg_qindex[kNumSegs] = {0, 0, 0, 0};
 };
+// Segment quantiser indices of an inter frame at frame QP `qp` (the classes' QPs of aq3_mb_qp).
+inline void segment_qindices(int qp, int aq, int out[kNumSegs]) {
+    for (int s = 0; s < kNumSegs; ++s) out[s] = qindex_for_qp(h264::aq3_mb_qp(qp, tclass_of_seg(s), aq));
+}
 
 // Writes a complete VP8 frame (frame tag, key-frame header, first partition, token partitions)
 // from per-macroblock records and levels.  `levels(i)` returns macroblock i's 400 levels (only
@@ -138,6 +145,8 @@ class CpuVp8Encoder {
     h264::EncoderCommon common_;
     int cw_, ch_, mb_w_, mb_h_;
     std::vector<uint8_t> rec_y_[2], rec_uv_[2];
+    std::vector<uint8_t> prev_src_, next_src_;  // aq >= 3: previous / this frame's source luma (temporal classes)
+    int seg_qindex_[kNumSegs] = {0, 0, 0, 0};
     int cur_ = 0;
     bool have_ref_ = false;
     std::vector<Vp8Mb> mb_;
@@ -153,12 +162,16 @@ struct Vp8FrameState {
     uint8_t* rec_y;         // this frame's reconstruction
     uint8_t* rec_uv;
     uint8_t* hp_f;          // padded full-sample reference (origin applied; k_vp8_pad writes it)
+    const uint8_t* prev_src;  // aq >= 3: previous frame's source luma (temporal classes; pitch g.pitch)
+    uint8_t* save_src;        // aq >= 3: this frame's source luma, kept for the next frame
     int32_t hp_pitch;
     int32_t key;
     int32_t qindex;
     int32_t epoch;          // nonzero, new every frame: key-frame wavefront progress tag (20 bits)
-    int32_t q[6];           // Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
-    uint32_t qm[6];         // ceil(2^32 / (3 q)): the dead-zone quantiser's division as a multiply-high
+    int32_t segmented;      // inter frame with segment quantisers (temporal classes)
+    int32_t aq;
+    int32_t q[kNumSegs][6];   // per segment: Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
+    uint32_t qm[kNumSegs][6]; // ceil(2^32 / (3 q)): the dead-zone quantiser's division as a multiply-high
     int32_t drop_lambda;    // P frames: lambda_sse of the frame QP for vp8_drop_residual
 };
 // Both per-frame states in one block: one host->device copy per frame.
@@ -182,7 +195,7 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const 
                       const uint8_t* src_uv, hipStream_t stream);
 // Key frames: one wave per macroblock row, rows handing their bottom edges down (wavefront).
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                    hipStream_t stream);
+                    hipStream_t stream, bool save_src);
 // Records + the coded macroblocks' levels into the mapped host buffers (per-row compaction).
 void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream);
 
@@ -220,6 +233,8 @@ class GpuVp8Encoder final : public VideoEncoder {
         hipEvent_t start = nullptr, done = nullptr;
         bool key = false;
         int qp = 0, qindex = 0;
+        bool segmented = false;
+        int seg_qindex[kNumSegs] = {0, 0, 0, 0};
     };
     void alloc_slot(Slot& s);
     void free_slot(Slot& s);
@@ -242,6 +257,7 @@ class GpuVp8Encoder final : public VideoEncoder {
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
+    uint8_t* src_keep_[2] = {nullptr, nullptr};  // aq >= 3: source luma of the frames in rec_y_[k]
     int cur_ = 0;
     bool have_ref_ = false;
     uint32_t epoch_ = 0;

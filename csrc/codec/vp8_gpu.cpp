@@ -80,6 +80,10 @@ GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMalloc(&rec_uv_[i], uvsz));
         HIP_CHECK(hipMemsetAsync(rec_y_[i], 0, ysz, stream_));
         HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
+        if (cfg.aq >= 3) {
+            HIP_CHECK(hipMalloc(&src_keep_[i], ysz));
+            HIP_CHECK(hipMemsetAsync(src_keep_[i], 0, ysz, stream_));
+        }
     }
     hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
     HIP_CHECK(hipMalloc(&hp_, (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad)));
@@ -92,6 +96,7 @@ GpuVp8Encoder::~GpuVp8Encoder() {
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);
+        if (src_keep_[i]) (void)hipFree(src_keep_[i]);
     }
     (void)hipFree(hp_);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
@@ -111,11 +116,21 @@ void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
     f.qindex = s.qindex;
     if (++epoch_ > 0xfffffu) epoch_ = 1;  // 20-bit tag, never 0
     f.epoch = (int32_t)epoch_;
-    const Quant Q = quant_of(s.qindex);
-    const int q[6] = {Q.y1dc, Q.y1ac, Q.y2dc, Q.y2ac, Q.uvdc, Q.uvac};
-    for (int i = 0; i < 6; ++i) {
-        f.q[i] = q[i];
-        f.qm[i] = 0xffffffffu / (uint32_t)(3 * q[i]) + 1u;  // ceil(2^32 / 3q)
+    // inter frames with temporal classes: segment quantisers; key frames: the frame quantiser
+    s.segmented = !key && cfg_.aq >= 3;
+    for (int k = 0; k < kNumSegs; ++k) s.seg_qindex[k] = s.qindex;
+    if (s.segmented) segment_qindices(qp, cfg_.aq, s.seg_qindex);
+    f.segmented = s.segmented ? 1 : 0;
+    f.aq = cfg_.aq;
+    f.prev_src = src_keep_[ref];
+    f.save_src = src_keep_[cur];
+    for (int k = 0; k < kNumSegs; ++k) {
+        const Quant Q = quant_of(s.seg_qindex[k]);
+        const int q[6] = {Q.y1dc, Q.y1ac, Q.y2dc, Q.y2ac, Q.uvdc, Q.uvac};
+        for (int i = 0; i < 6; ++i) {
+            f.q[k][i] = q[i];
+            f.qm[k][i] = 0xffffffffu / (uint32_t)(3 * q[i]) + 1u;  // ceil(2^32 / 3q)
+        }
     }
     f.drop_lambda = h264::lambda_sse(qp);
     h264::FrameState& m = s.st_host->me;
@@ -134,7 +149,7 @@ void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* 
     Slot& s = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(s.buf.st, s.st_host, sizeof(Vp8States), hipMemcpyHostToDevice, stream_));
     if (key)
-        launch_vp8_key(geom_, s.buf, src_y, src_uv, stream_);
+        launch_vp8_key(geom_, s.buf, src_y, src_uv, stream_, cfg_.aq >= 3);
     else
         launch_vp8_inter(geom_, s.buf, src_y, src_uv, stream_);
     launch_vp8_gather(geom_, s.buf, stream_);
@@ -152,8 +167,10 @@ void GpuVp8Encoder::check_slot(Slot& s) {
 void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out) {
     const Vp8Mb* mbs = s.buf.mb_host;
     const int16_t* lv = s.buf.lv_host;
-    write_frame(FrameDesc{s.key, cfg_.width, cfg_.height, geom_.mb_w, geom_.mb_h, s.qindex, log2_parts_}, mbs,
-                [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
+    FrameDesc fd{s.key, cfg_.width, cfg_.height, geom_.mb_w, geom_.mb_h, s.qindex, log2_parts_};
+    fd.segmented = s.segmented;
+    for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = s.seg_qindex[k];
+    write_frame(fd, mbs, [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
                 [&](int n, const std::function<void(int)>& fn) { pool_.run(n, fn); });
 }
 

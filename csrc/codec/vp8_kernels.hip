@@ -19,6 +19,7 @@
 #include "../common/hip_check.h"
 #include "h264_core.h"
 #include "h264_gpu.h"
+#include "h264_mb.h"
 #include "vp8_encoder.h"
 
 namespace mx {
@@ -65,7 +66,9 @@ struct MbLds {
 // drop_lambda >= 0 (inter macroblocks): vp8_drop_residual may turn the macroblock into prediction
 // only (levels zero, reconstruction = prediction) -- the decision is wave-uniform.
 __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restrict__ lv, int lane,
-                            int drop_lambda = -1) {
+                            int drop_lambda = -1, int seg = 0) {
+    const int32_t* Fq = F.q[seg];      // the macroblock's segment quantiser (wave-uniform)
+    const uint32_t* Fqm = F.qm[seg];
     int lvl[16], dq[16];
     bool nz = false;
     int st_lsad = 0, st_dp = 0, st_dc = 0, st_bits = 0;  // drop statistics (luma lanes, Y2 lane)
@@ -109,8 +112,8 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
             if (luma && k == 0) continue;  // the DC travels in Y2
             const int pos = kZigzag[k];
             const int qi = luma ? 1 : (k == 0 ? 4 : 5);
-            const int q = F.q[qi];
-            const int l = qz(coef[pos], q, F.qm[qi]);
+            const int q = Fq[qi];
+            const int l = qz(coef[pos], q, Fqm[qi]);
             lvl[k] = l;
             dq[pos] = l * q;
             nz |= l != 0;
@@ -126,9 +129,9 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
         for (int k = 0; k < 16; ++k) {
             const int pos = kZigzag[k];
             const int qi = k == 0 ? 2 : 3;
-            const int l = qz(y2[pos], F.q[qi], F.qm[qi]);
+            const int l = qz(y2[pos], Fq[qi], Fqm[qi]);
             lvl[k] = l;
-            y2q[pos] = l * F.q[qi];
+            y2q[pos] = l * Fq[qi];
             nz |= l != 0;
         }
         iwht4x4(y2q, dcr);
@@ -264,14 +267,15 @@ __device__ __forceinline__ void store_rec(const MbLds& s, const h264::Geometry& 
 }
 
 __device__ __forceinline__ void store_record(Vp8Mb* __restrict__ rec, int mvx, int mvy, int ymode, int uvmode,
-                                             uint32_t nz, const uint32_t sse[3], int lane) {
+                                             uint32_t nz, const uint32_t sse[3], int lane, int seg = 0) {
     if (lane == 0) {
         Vp8Mb m;
         m.mvx = (int16_t)mvx;
         m.mvy = (int16_t)mvy;
         m.ymode = (uint8_t)ymode;
         m.uvmode = (uint8_t)uvmode;
-        m.pad0 = m.pad1 = 0;
+        m.seg = (uint8_t)seg;
+        m.pad1 = 0;
         m.nz = nz;
         m.slot = 0;
         m.sse[0] = sse[0];
@@ -341,6 +345,20 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
 #pragma unroll
         for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = p[j];
     }
+    // temporal class (h264_mb.h temporal_class) -> segment: the source against the previous source
+    // displaced by the vector; this macroblock's source becomes the next frame's previous source
+    int seg = kSegNormal;
+    if (F.segmented) {  // frame-uniform
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+        const uint32_t sw = *reinterpret_cast<const uint32_t*>(s.src + r * 16 + c4);
+        int tsad = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            tsad += abs((int)((sw >> (8 * j)) & 0xff) -
+                        h264::ref_px(F.prev_src, g.pitch, g.coded_w, g.coded_h, x0 + c4 + j + ix, y0 + r + iy));
+        *reinterpret_cast<uint32_t*>(F.save_src + (size_t)(y0 + r) * g.pitch + x0 + c4) = sw;
+        seg = seg_of_tclass(h264::temporal_class((uint32_t)wsum(tsad), ix == 0 && iy == 0));  // wave-uniform
+    }
     const int mvx = ix * 8, mvy = iy * 8;
     const int cvx = chroma_mv(mvx), cvy = chroma_mv(mvy);
     {
@@ -362,10 +380,20 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
         s.pv[cy * 8 + cx] = (uint8_t)chroma_px(at_v, px, py, cvx & 7, cvy & 7);
     }
     __syncthreads();
-    const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, F.drop_lambda);
+    const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, F.drop_lambda, seg);
     uint32_t sse[3];
     store_rec(s, g, F, x0, y0, lane, sse);
-    store_record(mbs + mbi, mvx, mvy, kInter, kDcPred, nz, sse, lane);
+    store_record(mbs + mbi, mvx, mvy, kInter, kDcPred, nz, sse, lane, seg);
+}
+
+// Key frames with temporal classes: the source luma into the frame state's save buffer (the
+// pointer read on the device, as h264 k_save_src), one dword per thread.
+__global__ __launch_bounds__(256) void k_vp8_save_src(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                      const uint8_t* __restrict__ src_y) {
+    const int x4 = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y;
+    if (x4 >= g.coded_w || y >= g.coded_h) return;
+    const size_t o = (size_t)y * g.pitch + x4;
+    *reinterpret_cast<uint32_t*>(st->v.save_src + o) = *reinterpret_cast<const uint32_t*>(src_y + o);
 }
 
 // ------------------------------------------------------------------ key frames
@@ -614,7 +642,10 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const 
 }
 
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                    hipStream_t stream) {
+                    hipStream_t stream, bool save_src) {
+    if (save_src)  // the next inter frame's temporal classes compare against this source
+        hipLaunchKernelGGL(k_vp8_save_src, dim3((g.coded_w / 4 + 255) / 256, g.coded_h), dim3(256), 0, stream, g, b.st,
+                           src_y);
     hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv, b.prog,
                        b.line, b.err);
 }

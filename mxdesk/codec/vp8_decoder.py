@@ -5,13 +5,13 @@ through Pillow, tests/test_vp8.py).
 Written from the decoding side of the RFC: boolean decoder (7), frame header (9, 19.2), token
 probability and motion-vector probability updates (13.4, 17.2), key-frame and inter-frame mode
 parsing (11, 16) with the near-vector search (16.3), token decoding with contexts (13),
-dequantisation (14.1), inverse WHT / DCT (14.3, 14.4), 16x16 and chroma intra prediction with the
-127 / 129 frame edges (12), and six-tap inter prediction (18).
+dequantisation (14.1) with per-segment quantisers (9.3), inverse WHT / DCT (14.3, 14.4), 16x16 and
+chroma intra prediction with the 127 / 129 frame edges (12), and six-tap inter prediction (18).
 
 Supported: key and inter frames, 16x16 intra modes, 16x16 inter macroblocks (ZERO / NEAREST / NEAR /
-NEW vectors, last-frame reference), token partitions, probability updates, skip flags.  Raises
-``NotImplementedError`` for B_PRED, SPLITMV, segmentation, a non-zero loop-filter level and
-golden / altref references.  Slow; for test pictures.
+NEW vectors, last-frame reference), segmentation (segment map, absolute / delta segment quantisers),
+token partitions, probability updates, skip flags.  Raises ``NotImplementedError`` for B_PRED,
+SPLITMV, a non-zero loop-filter level and golden / altref references.  Slow; for test pictures.
 """
 from __future__ import annotations
 
@@ -171,8 +171,21 @@ class Decoder:
         if key:
             bd.lit(1)  # color space
             self.clamping = bd.lit(1)
-        if bd.lit(1):
-            raise NotImplementedError("segmentation")
+        seg_on = bd.lit(1)
+        update_map = 0
+        if key:
+            self.seg_abs, self.seg_q = 0, [0, 0, 0, 0]
+            self.seg_probs = [255, 255, 255]
+        if seg_on:  # 9.3: segment quantisers (absolute or delta) and the segment map's tree probabilities
+            update_map = bd.lit(1)
+            if bd.lit(1):  # update_segment_feature_data
+                self.seg_abs = bd.lit(1)
+                self.seg_q = [(bd.signed(7) if bd.lit(1) else 0) for _ in range(4)]
+                for _ in range(4):  # loop-filter levels per segment (no loop filter here)
+                    if bd.lit(1) and bd.signed(6):
+                        raise NotImplementedError("loop filter")
+            if update_map:
+                self.seg_probs = [bd.lit(8) if bd.lit(1) else 255 for _ in range(3)]
         bd.lit(1)  # filter type
         level = bd.lit(6)
         bd.lit(3)  # sharpness
@@ -187,11 +200,17 @@ class Decoder:
         qi = bd.lit(7)
         deltas = [bd.signed(4) if bd.lit(1) else 0 for _ in range(5)]  # y_dc, y2_dc, y2_ac, uv_dc, uv_ac
         q = lambda base, d: min(127, max(0, base + d))  # noqa: E731
-        self.q = {
-            "y1dc": DC_Q[q(qi, deltas[0])], "y1ac": AC_Q[qi],
-            "y2dc": 2 * DC_Q[q(qi, deltas[1])], "y2ac": max(8, AC_Q[q(qi, deltas[2])] * 155 // 100),
-            "uvdc": min(132, DC_Q[q(qi, deltas[3])]), "uvac": AC_Q[q(qi, deltas[4])],
-        }
+
+        def quant(qb):
+            return {
+                "y1dc": DC_Q[q(qb, deltas[0])], "y1ac": AC_Q[q(qb, 0)],
+                "y2dc": 2 * DC_Q[q(qb, deltas[1])], "y2ac": max(8, AC_Q[q(qb, deltas[2])] * 155 // 100),
+                "uvdc": min(132, DC_Q[q(qb, deltas[3])]), "uvac": AC_Q[q(qb, deltas[4])],
+            }
+        self.q = quant(qi)
+        # per-segment quantisers (segment_feature_mode 1: absolute indices, 0: deltas on y_ac_qi)
+        self.seg_quant = [quant(self.seg_q[k] if self.seg_abs else q(qi, self.seg_q[k])) for k in range(4)] \
+            if seg_on else [self.q] * 4
         saved = None
         if key:
             refresh_probs = bd.lit(1)
@@ -225,8 +244,15 @@ class Decoder:
                         self.mvp[c][k] = (x << 1) if x else 1
         # ---- per-MB modes
         mbs = []
+        if not hasattr(self, "seg_map") or len(self.seg_map) != mw * mh or key:
+            self.seg_map = [0] * (mw * mh)
         for my in range(mh):
             for mx in range(mw):
+                if update_map:  # segment_id (tree {2, 4, -0, -1, -2, -3})
+                    sp = self.seg_probs
+                    self.seg_map[my * mw + mx] = (2 + bd.bool(sp[2])) if bd.bool(sp[0]) else bd.bool(sp[1])
+                    k = "seg%d" % self.seg_map[my * mw + mx]
+                    self.stats[k] = self.stats.get(k, 0) + 1
                 skip = bd.bool(prob_skip) if skip_on else 0
                 if key:
                     ym = self._tree_kf_ymode(bd)
@@ -446,7 +472,7 @@ class Decoder:
 
     # ------------------------------------------------------------------ reconstruction
     def _recon(self, Y, U, V, mx, my, m, coefs, key):
-        q = self.q
+        q = self.seg_quant[self.seg_map[my * self.mw + mx]]
         x0, y0 = mx * 16, my * 16
         if m["inter"]:
             pred = self._inter_pred(self.last[0], x0, y0, 16, m["mv"][0], m["mv"][1])

@@ -76,6 +76,7 @@ def _encoder(native, w, h, **kw):
     c = native.EncoderConfig()
     c.width, c.height = w, h
     c.bitrate_kbps, c.qp, c.search_range = kw.get("kbps", 0), kw.get("qp", 30), kw.get("sr", 8)
+    c.aq = kw.get("aq", c.aq)
     return native.CpuVp8Encoder(c)
 
 
@@ -127,9 +128,10 @@ def test_inter_frames_decode_to_reconstruction(native, w, h, kbps, qp):
 
 def test_vp8_psnr_and_motion(native):
     # the encoder tracks a translating picture: P frames are far smaller than the key frame
+    # (aq 2: one quantiser; with the temporal classes the first P frame refines the moving picture)
     w, h = 192, 128
     base, uv0 = _picture(w + 32, h, 7)
-    enc = _encoder(native, w, h, qp=26, sr=16)
+    enc = _encoder(native, w, h, qp=26, sr=16, aq=2)
     sizes, psnrs = [], []
     for t in range(5):
         y = np.ascontiguousarray(base[:, 2 * t: 2 * t + w])
@@ -140,3 +142,43 @@ def test_vp8_psnr_and_motion(native):
         psnrs.append(10 * np.log10(255 ** 2 / mse))
     assert min(psnrs) > 32, psnrs
     assert max(sizes[1:]) < sizes[0] / 3, sizes
+
+
+@pytest.mark.parametrize("aq", [3, 4])
+def test_segmented_inter_frames_decode_to_reconstruction(native, aq):
+    """Inter frames segmented by the temporal classes (9.3: static / persistent windows finer,
+    the animated noise panel coarser, segment map in every inter frame, absolute segment
+    quantisers): the in-tree decoder reproduces the reconstruction and sees several segments; the
+    static class lowers the distortion of the unchanged windows against aq 2."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    w, h = 640, 368
+    desk = CpuSyntheticDesktop(w, h, True)
+    srcs = [bgrx_to_nv12(desk.render(t, t / 60, 0)) for t in range(4)]
+
+    def run(a):
+        enc = _encoder(native, w, h, qp=34, sr=8, aq=a)
+        frames, recs = [], []
+        for y, uv in srcs:
+            frames.append(enc.encode(y, uv))
+            recs.append(tuple(x.copy() for x in enc.recon()))
+        return frames, recs
+
+    frames, recs = run(aq)
+    dec = Decoder()
+    dec.decode(frames)
+    for t, ((yy, u, v), (ry, ruv)) in enumerate(zip(dec.frames_coded, recs)):
+        assert np.array_equal(yy, ry), f"frame {t} luma"
+        assert np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2]), f"frame {t} chroma"
+    segs = {k: v for k, v in dec.stats.items() if k.startswith("seg")}
+    assert len(segs) >= 2, segs
+    if aq >= 4:
+        assert segs.get("seg1", 0) > 0, segs  # the static class
+    y4, _ = srcs[-1]
+    flat, _ = run(2)
+    dflat = Decoder()
+    dflat.decode(flat)
+    keep = np.ones((h, w), bool)  # outside the animated noise panel (the renderer's rectangle, bench.py)
+    keep[int(h * 0.55) - 16:int(h * 0.77) + 17, int(w * 0.04) - 16:int(w * 0.20) + 17] = False
+    err = lambda d: float(np.mean(((d.frames_coded[-1][0][:h, :w].astype(float) - y4[:h, :w]) ** 2)[keep]))  # noqa: E731
+    assert err(dec) < 0.5 * err(dflat), (err(dec), err(dflat))
