@@ -3,6 +3,8 @@
 // token partitions (one per MB row modulo the partition count, written concurrently -- a token
 // partition's contexts depend only on the coefficients, which are known before coding starts).
 #include <algorithm>
+#include <array>
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 
@@ -13,92 +15,108 @@ namespace vp8 {
 
 namespace {
 
-inline const uint8_t* coef_probs(int type, int band, int ctx) { return kCoefProbs0 + ((type * 8 + band) * 3 + ctx) * 11; }
+inline int coef_index(int type, int band, int ctx) { return ((type * 8 + band) * 3 + ctx) * 11; }
 
-void put_extra(BoolEncoder& e, int v, const uint8_t* p, int n) {
-    for (int k = n - 1; k >= 0; --k) e.put(p[n - 1 - k], (v >> k) & 1);
+// Token coding over a probability table: Enc::tok(table index, bit) codes (or counts) a
+// context-coded token branch, Enc::fix(prob, bit) a fixed-probability bit (extra bits, sign).
+struct TokWriter {
+    BoolEncoder& e;
+    const uint8_t* probs;
+    void tok(int idx, int bit) { e.put(probs[idx], bit); }
+    void fix(int prob, int bit) { e.put(prob, bit); }
+};
+struct TokCounter {  // branch statistics for the per-frame probability updates (13.4)
+    uint32_t (*n)[2];
+    void tok(int idx, int bit) { ++n[idx][bit]; }
+    void fix(int, int) {}
+};
+
+template <class Enc>
+void put_extra(Enc& e, int v, const uint8_t* p, int n) {
+    for (int k = n - 1; k >= 0; --k) e.fix(p[n - 1 - k], (v >> k) & 1);
 }
 
-// One block's tokens (13.2 / 13.3); returns whether it has a non-zero level.
-void put_block(BoolEncoder& e, const int16_t* lv, int first, int type, int ctx) {
+// One block's tokens (13.2 / 13.3).
+template <class Enc>
+void put_block(Enc& e, const int16_t* lv, int first, int type, int ctx) {
     int last = 15;
     while (last >= first && lv[last] == 0) --last;
     if (last < first) {
-        e.put(coef_probs(type, kBand[first], ctx)[0], 0);  // EOB
+        e.tok(coef_index(type, kBand[first], ctx) + 0, 0);  // EOB
         return;
     }
     bool prev_zero = false;
     for (int i = first; i <= last; ++i) {
-        const uint8_t* P = coef_probs(type, kBand[i], ctx);
-        if (!prev_zero) e.put(P[0], 1);  // not EOB
+        const int P = coef_index(type, kBand[i], ctx);
+        if (!prev_zero) e.tok(P + 0, 1);  // not EOB
         const int v = lv[i], a = v < 0 ? -v : v;
         if (a == 0) {
-            e.put(P[1], 0);
+            e.tok(P + 1, 0);
             ctx = 0;
             prev_zero = true;
             continue;
         }
-        e.put(P[1], 1);
+        e.tok(P + 1, 1);
         if (a == 1) {
-            e.put(P[2], 0);
+            e.tok(P + 2, 0);
         } else {
-            e.put(P[2], 1);
+            e.tok(P + 2, 1);
             if (a <= 4) {
-                e.put(P[3], 0);
+                e.tok(P + 3, 0);
                 if (a == 2) {
-                    e.put(P[4], 0);
+                    e.tok(P + 4, 0);
                 } else {
-                    e.put(P[4], 1);
-                    e.put(P[5], a == 4);
+                    e.tok(P + 4, 1);
+                    e.tok(P + 5, a == 4);
                 }
             } else {
-                e.put(P[3], 1);
+                e.tok(P + 3, 1);
                 if (a <= 10) {
-                    e.put(P[6], 0);
+                    e.tok(P + 6, 0);
                     if (a <= 6) {
-                        e.put(P[7], 0);
+                        e.tok(P + 7, 0);
                         put_extra(e, a - 5, kPcat1, 1);
                     } else {
-                        e.put(P[7], 1);
+                        e.tok(P + 7, 1);
                         put_extra(e, a - 7, kPcat2, 2);
                     }
                 } else {
-                    e.put(P[6], 1);
+                    e.tok(P + 6, 1);
                     if (a <= 34) {
-                        e.put(P[8], 0);
+                        e.tok(P + 8, 0);
                         if (a <= 18) {
-                            e.put(P[9], 0);
+                            e.tok(P + 9, 0);
                             put_extra(e, a - 11, kPcat3, 3);
                         } else {
-                            e.put(P[9], 1);
+                            e.tok(P + 9, 1);
                             put_extra(e, a - 19, kPcat4, 4);
                         }
                     } else {
-                        e.put(P[8], 1);
+                        e.tok(P + 8, 1);
                         if (a <= 66) {
-                            e.put(P[10], 0);
+                            e.tok(P + 10, 0);
                             put_extra(e, a - 35, kPcat5, 5);
                         } else {
-                            e.put(P[10], 1);
+                            e.tok(P + 10, 1);
                             put_extra(e, a - 67, kPcat6, 11);
                         }
                     }
                 }
             }
         }
-        e.put(128, v < 0);
+        e.fix(128, v < 0);
         ctx = a == 1 ? 1 : 2;
         prev_zero = false;
     }
-    if (last < 15) e.put(coef_probs(type, kBand[last + 1], ctx)[0], 0);  // EOB
+    if (last < 15) e.tok(coef_index(type, kBand[last + 1], ctx) + 0, 0);  // EOB
 }
 
 inline int nzb(const Vp8Mb& m, int b) { return (m.nz >> b) & 1; }
 
 // Token partition `p`: MB rows p, p + n, ...
-void write_tokens(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels, int p, int n,
-                  std::vector<uint8_t>& out) {
-    BoolEncoder e(out);
+template <class Enc>
+void code_tokens(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels, int p, int n,
+                 Enc& e) {
     for (int mby = p; mby < f.mb_h; mby += n) {
         int left[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // Y0..3 (rows), U0..1, V0..1, Y2
         for (int mbx = 0; mbx < f.mb_w; ++mbx) {
@@ -131,7 +149,39 @@ void write_tokens(const FrameDesc& f, const Vp8Mb* mbs, const std::function<cons
                 }
         }
     }
-    e.flush();
+}
+
+// Cost in 1/256 bit of coding `bit` at probability `prob` (of a zero): -256 log2(p).
+inline int bit_cost256(int prob, int bit) {
+    static const auto tab = [] {
+        std::array<int, 256> t{};
+        for (int k = 1; k < 256; ++k) t[k] = (int)std::lround(-256.0 * std::log2(k / 256.0));
+        t[0] = t[1];
+        return t;
+    }();
+    return tab[bit ? 256 - prob : prob];
+}
+
+// Per-frame coefficient probability updates (13.4): a probability is replaced by its frame's
+// optimum when the branch statistics save more than the update costs (the flag at its update
+// probability + 8 bits).  refresh_entropy_probs stays 0, so every frame updates against the
+// defaults.  upd[k] = the new probability or 0.
+void plan_prob_updates(const uint32_t (*n)[2], uint8_t* upd, uint8_t* probs) {
+    for (int k = 0; k < 1056; ++k) {
+        upd[k] = 0;
+        probs[k] = kCoefProbs0[k];
+        const uint32_t n0 = n[k][0], n1 = n[k][1], t = n0 + n1;
+        if (t == 0) continue;
+        const int np = std::clamp((int)((n0 * 256ull + t / 2) / t), 1, 255);
+        if (np == kCoefProbs0[k]) continue;
+        const long long old_c = (long long)n0 * bit_cost256(kCoefProbs0[k], 0) + (long long)n1 * bit_cost256(kCoefProbs0[k], 1);
+        const long long new_c = (long long)n0 * bit_cost256(np, 0) + (long long)n1 * bit_cost256(np, 1);
+        const long long flag = bit_cost256(kCoefUpdateProbs[k], 1) - bit_cost256(kCoefUpdateProbs[k], 0);
+        if (old_c - new_c > flag + 8 * 256) {
+            upd[k] = (uint8_t)np;
+            probs[k] = (uint8_t)np;
+        }
+    }
 }
 
 inline void clamp_mv(int mv[2], int mb_w, int mb_h, int mbx, int mby) {
@@ -229,6 +279,19 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
     auto prob_of = [](int zero, int total) { return total ? std::clamp((zero * 256 + total / 2) / total, 1, 255) : 255; };
     const int seg_p[3] = {prob_of(seg_n[0] + seg_n[1], nmb), prob_of(seg_n[0], seg_n[0] + seg_n[1]),
                           prob_of(seg_n[2], seg_n[2] + seg_n[3])};
+    // ---- branch statistics of every token partition (concurrently), then the probability updates
+    std::vector<std::array<uint32_t, 2>> cnt((size_t)nparts * 1056, std::array<uint32_t, 2>{0u, 0u});
+    run_parallel(nparts, [&](int p) {
+        TokCounter c{reinterpret_cast<uint32_t(*)[2]>(cnt[(size_t)p * 1056].data())};
+        code_tokens(f, mbs, levels, p, nparts, c);
+    });
+    for (int p = 1; p < nparts; ++p)
+        for (int k = 0; k < 1056; ++k) {
+            cnt[k][0] += cnt[(size_t)p * 1056 + k][0];
+            cnt[k][1] += cnt[(size_t)p * 1056 + k][1];
+        }
+    uint8_t upd[1056], probs[1056];
+    plan_prob_updates(reinterpret_cast<const uint32_t(*)[2]>(cnt[0].data()), upd, probs);
     // ---- first partition
     std::vector<uint8_t> p1;
     p1.reserve(16 + (size_t)nmb / 2);
@@ -273,7 +336,10 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
             e.literal(0, 1);  // refresh_entropy_probs
             e.literal(1, 1);  // refresh_last
         }
-        for (int k = 0; k < 1056; ++k) e.put(kCoefUpdateProbs[k], 0);  // no token probability updates
+        for (int k = 0; k < 1056; ++k) {  // token probability updates (plan_prob_updates)
+            e.put(kCoefUpdateProbs[k], upd[k] != 0);
+            if (upd[k]) e.literal(upd[k], 8);
+        }
         e.literal(1, 1);  // mb_no_skip_coeff
         e.literal((uint32_t)prob_skip_false, 8);
         const int prob_intra = 1, prob_last = 255, prob_gf = 128;
@@ -337,11 +403,14 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         e.flush();
     }
     if (p1.size() >= (1u << 19)) throw std::runtime_error("vp8 writer: first partition too large");
-    // ---- token partitions, concurrently
+    // ---- token partitions, concurrently, over the updated probabilities
     std::vector<std::vector<uint8_t>> parts((size_t)nparts);
     run_parallel(nparts, [&](int p) {
         parts[(size_t)p].reserve(4096);
-        write_tokens(f, mbs, levels, p, nparts, parts[(size_t)p]);
+        BoolEncoder e(parts[(size_t)p]);
+        TokWriter w{e, probs};
+        code_tokens(f, mbs, levels, p, nparts, w);
+        e.flush();
     });
     // ---- assemble: frame tag, key-frame start code + size, partition 1, partition sizes, data
     const uint32_t tag = (f.key ? 0u : 1u) | (0u << 1) | (1u << 4) | ((uint32_t)p1.size() << 5);
