@@ -951,15 +951,21 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int sr = fs->slice_rows;
-    const int y = blockIdx.x * sr + wave;  // CTU row of this wave
-    const bool row_ok = wave < sr && y < g.mb_h;
+    // H waves per CTU row (launch: kMaxSliceRows / slice_rows): the row's main wave (sub 0) codes
+    // the CU; its helpers share the intra mode search (every H-th candidate each) -- 1-row slices
+    // (4K, 1080p) would otherwise leave one wave per workgroup walking 240 CTUs alone
+    const int H = max(1, ((int)blockDim.x >> 6) / sr);
+    const int row = wave / H, sub = wave - row * H, mw = row * H;
+    const bool main_w = sub == 0;
+    const int y = blockIdx.x * sr + row;  // CTU row of this wave
+    const bool row_ok = row < sr && y < g.mb_h;
     const int qp = fs->qp;
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     const int lambda = h264::lambda_sad(qp);
     const int cw = g.coded_w;
-    uint8_t* bot_y = bottom + (size_t)wave * 2 * cw;
+    uint8_t* bot_y = bottom + (size_t)row * 2 * cw;
     uint8_t* bot_c = bot_y + cw;
-    const uint8_t* up_y = bottom + (size_t)(wave - 1) * 2 * cw;  // row above (same slice), valid if wave > 0
+    const uint8_t* up_y = bottom + (size_t)(row - 1) * 2 * cw;  // row above (same slice), valid if row > 0
     const uint8_t* up_c = up_y + cw;
     TuBuf& t = tb[wave];
     IntraRefs& R = rf[wave];
@@ -974,23 +980,23 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         lc = *reinterpret_cast<const uint16_t*>(src_uv + (size_t)(y * 8 + rc) * g.pitch + xx * 16 + 2 * cc);
     };
     uint32_t nsy = 0, nsc = 0;
-    load_src(-2 * wave, nsy, nsc);
+    load_src(-2 * row, nsy, nsc);
     for (int step = 0; step < steps; ++step) {
-        const int x = step - 2 * wave;
+        const int x = step - 2 * row;
         const bool valid = row_ok && x >= 0 && x < g.mb_w;
         const int x0 = x * 16, y0 = y * 16;
         const uint32_t sy4 = nsy, sc2 = nsc;
         load_src(x + 1, nsy, nsc);
-        const bool al = x > 0, at = wave > 0, atr = at && x + 1 < g.mb_w, ac = at && x > 0;
+        const bool al = x > 0, at = row > 0, atr = at && x + 1 < g.mb_w, ac = at && x > 0;
         // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
         if (valid) {
             if (lane < 16) {
-                R.lpx[lane] = al ? leftc[wave][lane] : 0;
+                R.lpx[lane] = al ? leftc[mw][lane] : 0;
                 R.tpx[lane] = at ? up_y[x0 + lane] : 0;
                 R.trx[lane] = atr ? up_y[x0 + 16 + lane] : 0;
             } else if (lane < 32) {
                 const int k = lane - 16, comp = k >> 3, q = k & 7;
-                R.lc[comp][q] = al ? leftc[wave][16 + comp * 8 + q] : 0;
+                R.lc[comp][q] = al ? leftc[mw][16 + comp * 8 + q] : 0;
                 R.tc[comp][q] = at ? up_c[x0 + 2 * q + comp] : 0;
                 R.trc[comp][q] = atr ? up_c[x0 + 16 + 2 * q + comp] : 0;
             } else if (lane == 32) {
@@ -1048,7 +1054,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         // ---- mode decision: SAD of each candidate, 4 samples per lane
         int mode = 1;
         if (valid) {
-            const int cand_a = al ? prev_mode[wave] : 1;
+            const int cand_a = al ? prev_mode[row] : 1;
             const int r = lane >> 2, cb = (lane & 3) * 4;
             // every candidate's partial SAD first (independent work), then the wave reductions
             int sad[kNumIntraCands];
@@ -1056,6 +1062,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             for (int m = 0; m < kNumIntraCands; ++m) {
                 const int md = kIntraCands[m];
                 sad[m] = 0;
+                if (m % H != sub) continue;  // wave-uniform: this wave's share of the candidates
                 for (int j = 0; j < 4; ++j) {
                     const int p = pred_sample(md, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
                     const int d = (int)((sy4 >> (8 * j)) & 0xff) - p;
@@ -1064,15 +1071,16 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             }
 #pragma unroll
             for (int m = 0; m < kNumIntraCands; ++m) {
+                if (m % H != sub) continue;
                 const int s = wsum(sad[m]);
-                if (lane == 0) mode_cost[wave][m] = s + lambda * intra_mode_bits(kIntraCands[m], cand_a);
+                if (lane == 0) mode_cost[row][m] = s + lambda * intra_mode_bits(kIntraCands[m], cand_a);
             }
         }
         __syncthreads();
-        if (valid) {
+        if (valid && main_w) {
             int bm = 0;
             for (int m = 1; m < kNumIntraCands; ++m)
-                if (mode_cost[wave][m] < mode_cost[wave][bm]) bm = m;
+                if (mode_cost[row][m] < mode_cost[row][bm]) bm = m;
             mode = kIntraCands[bm];
             const int r = lane >> 2, cb = (lane & 3) * 4;
             for (int j = 0; j < 4; ++j) {
@@ -1090,9 +1098,9 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         }
         __syncthreads();
         const int i = valid ? y * g.mb_w + x : 0;
-        const TuResult res = code_tus<false>(t, M, qp, qpc, true, valid, coef + (size_t)i * kCoefPerCu, fs->rec_y, g.pitch,
-                                      fs->rec_uv, x0, y0, g.width, g.height);
-        if (valid) {
+        const TuResult res = code_tus<false>(t, M, qp, qpc, true, valid && main_w, coef + (size_t)i * kCoefPerCu,
+                                             fs->rec_y, g.pitch, fs->rec_uv, x0, y0, g.width, g.height);
+        if (valid && main_w) {
             acc[0] += (unsigned)res.sse[0];
             acc[1] += (unsigned)res.sse[1];
             acc[2] += (unsigned)res.sse[2];
@@ -1108,25 +1116,25 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 cus[i] = c;
                 cost[i] = cu_cost(c);
                 qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
-                prev_mode[wave] = mode;
+                prev_mode[row] = mode;
             }
         }
         __syncthreads();
-        if (valid) {
+        if (valid && main_w) {
             // reconstruction edges (kept in t.pred by code_tus): right column -> left
-            // neighbour of this wave's next CU, bottom rows -> the wave of the row below
+            // neighbour of this row's next CU, bottom rows -> the waves of the row below
             if (lane < 16) {
-                leftc[wave][lane] = t.pred[lane * 16 + 15];
+                leftc[mw][lane] = t.pred[lane * 16 + 15];
                 bot_y[x0 + lane] = t.pred[15 * 16 + lane];
                 bot_c[x0 + lane] = t.pred[256 + (lane & 1) * 64 + 7 * 8 + (lane >> 1)];
             } else if (lane < 32) {
                 const int k = lane - 16, comp = k >> 3, q = k & 7;
-                leftc[wave][16 + comp * 8 + q] = t.pred[256 + comp * 64 + q * 8 + 7];
+                leftc[mw][16 + comp * 8 + q] = t.pred[256 + comp * 64 + q * 8 + 7];
             }
         }
         __syncthreads();
     }
-    if (row_ok && lane < 3)  // wave sums (identical in every lane)
+    if (row_ok && main_w && lane < 3)  // wave sums (identical in every lane)
         fs->sse_part[lane * h264::kSsePartStride + y] = lane == 0 ? acc[0] : (lane == 1 ? acc[1] : acc[2]);
 }
 
@@ -2072,8 +2080,9 @@ void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const size_t lds = (size_t)slice_rows * 2 * g.coded_w;
-    hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows), lds, s, g, b.fs, src_y, src_uv, b.cu,
-                       b.coef, b.cost, b.qpc);
+    const int helpers = std::max(1, kMaxSliceRows / slice_rows);  // waves per CTU row (k_hevc_intra)
+    hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows * helpers), lds, s, g, b.fs, src_y, src_uv,
+                       b.cu, b.coef, b.cost, b.qpc);
 }
 
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,

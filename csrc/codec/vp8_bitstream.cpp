@@ -25,10 +25,15 @@ struct TokWriter {
     void tok(int idx, int bit) { e.put(probs[idx], bit); }
     void fix(int prob, int bit) { e.put(prob, bit); }
 };
-struct TokCounter {  // branch statistics for the per-frame probability updates (13.4)
+struct TokWriterCount {  // coding + branch statistics for the next frame's probability updates (13.4)
+    BoolEncoder& e;
+    const uint8_t* probs;
     uint32_t (*n)[2];
-    void tok(int idx, int bit) { ++n[idx][bit]; }
-    void fix(int, int) {}
+    void tok(int idx, int bit) {
+        e.put(probs[idx], bit);
+        ++n[idx][bit];
+    }
+    void fix(int prob, int bit) { e.put(prob, bit); }
 };
 
 template <class Enc>
@@ -265,7 +270,7 @@ void find_near_mvs(const Vp8Mb* mbs, int mb_w, int mb_h, int mbx, int mby, int n
 
 void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels,
                  std::vector<uint8_t>& out,
-                 const std::function<void(int, const std::function<void(int)>&)>& run_parallel) {
+                 const std::function<void(int, const std::function<void(int)>&)>& run_parallel, TokenStats* stats) {
     const int nmb = f.mb_w * f.mb_h;
     const int nparts = 1 << f.log2_parts;
     int coded = 0;
@@ -279,19 +284,14 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
     auto prob_of = [](int zero, int total) { return total ? std::clamp((zero * 256 + total / 2) / total, 1, 255) : 255; };
     const int seg_p[3] = {prob_of(seg_n[0] + seg_n[1], nmb), prob_of(seg_n[0], seg_n[0] + seg_n[1]),
                           prob_of(seg_n[2], seg_n[2] + seg_n[3])};
-    // ---- branch statistics of every token partition (concurrently), then the probability updates
-    std::vector<std::array<uint32_t, 2>> cnt((size_t)nparts * 1056, std::array<uint32_t, 2>{0u, 0u});
-    run_parallel(nparts, [&](int p) {
-        TokCounter c{reinterpret_cast<uint32_t(*)[2]>(cnt[(size_t)p * 1056].data())};
-        code_tokens(f, mbs, levels, p, nparts, c);
-    });
-    for (int p = 1; p < nparts; ++p)
-        for (int k = 0; k < 1056; ++k) {
-            cnt[k][0] += cnt[(size_t)p * 1056 + k][0];
-            cnt[k][1] += cnt[(size_t)p * 1056 + k][1];
-        }
+    // ---- probability updates planned from the previous frame's branch statistics of this type
     uint8_t upd[1056], probs[1056];
-    plan_prob_updates(reinterpret_cast<const uint32_t(*)[2]>(cnt[0].data()), upd, probs);
+    if (stats && stats->valid) {
+        plan_prob_updates(reinterpret_cast<const uint32_t(*)[2]>(stats->n[0].data()), upd, probs);
+    } else {
+        std::memset(upd, 0, sizeof upd);
+        std::memcpy(probs, kCoefProbs0, sizeof probs);
+    }
     // ---- first partition
     std::vector<uint8_t> p1;
     p1.reserve(16 + (size_t)nmb / 2);
@@ -403,15 +403,31 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         e.flush();
     }
     if (p1.size() >= (1u << 19)) throw std::runtime_error("vp8 writer: first partition too large");
-    // ---- token partitions, concurrently, over the updated probabilities
+    // ---- token partitions, concurrently, over the updated probabilities (counting this frame's
+    // branch statistics on the way when the caller keeps them)
     std::vector<std::vector<uint8_t>> parts((size_t)nparts);
+    std::vector<std::array<uint32_t, 2>> cnt(stats ? (size_t)nparts * 1056 : 0, std::array<uint32_t, 2>{0u, 0u});
     run_parallel(nparts, [&](int p) {
         parts[(size_t)p].reserve(4096);
         BoolEncoder e(parts[(size_t)p]);
-        TokWriter w{e, probs};
-        code_tokens(f, mbs, levels, p, nparts, w);
+        if (stats) {
+            TokWriterCount w{e, probs, reinterpret_cast<uint32_t(*)[2]>(cnt[(size_t)p * 1056].data())};
+            code_tokens(f, mbs, levels, p, nparts, w);
+        } else {
+            TokWriter w{e, probs};
+            code_tokens(f, mbs, levels, p, nparts, w);
+        }
         e.flush();
     });
+    if (stats) {
+        stats->n.assign(1056, std::array<uint32_t, 2>{0u, 0u});
+        for (int p = 0; p < nparts; ++p)
+            for (int k = 0; k < 1056; ++k) {
+                stats->n[k][0] += cnt[(size_t)p * 1056 + k][0];
+                stats->n[k][1] += cnt[(size_t)p * 1056 + k][1];
+            }
+        stats->valid = true;
+    }
     // ---- assemble: frame tag, key-frame start code + size, partition 1, partition sizes, data
     const uint32_t tag = (f.key ? 0u : 1u) | (0u << 1) | (1u << 4) | ((uint32_t)p1.size() << 5);
     out.push_back((uint8_t)tag);

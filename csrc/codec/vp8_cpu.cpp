@@ -103,14 +103,6 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 int lo_x, hi_x, lo_y, hi_y;
                 mv_bounds(mb_w_, mb_h_, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
                 const int ix = std::clamp(mvx / 4, lo_x, hi_x), iy = std::clamp(mvy / 4, lo_y, hi_y);
-                if (cfg_.aq >= 3) {  // temporal class of the macroblock -> its segment (quantiser)
-                    uint32_t tsad = 0;
-                    for (int y = 0; y < 16; ++y)
-                        for (int x = 0; x < 16; ++x)
-                            tsad += (uint32_t)std::abs((int)sy[(y0 + y) * pitch + x0 + x] -
-                                                       h264::ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + x + ix, y0 + y + iy));
-                    m.seg = (uint8_t)seg_of_tclass(h264::temporal_class(tsad, ix == 0 && iy == 0));
-                }
                 m.ymode = kInter;
                 m.mvx = (int16_t)(ix * 8);
                 m.mvy = (int16_t)(iy * 8);
@@ -136,6 +128,15 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 for (int y = 0; y < 8; ++y)
                     for (int x = 0; x < 8; ++x)
                         cres[c][y * 8 + x] = suv[(y0 / 2 + y) * pitch + x0 + 2 * x + c] - cp[c][y * 8 + x];
+            if (!key && cfg_.aq >= 3) {  // temporal class of the macroblock -> its segment (quantiser)
+                const int ix = m.mvx / 8, iy = m.mvy / 8;
+                uint32_t tsad = 0;
+                for (int y = 0; y < 16; ++y)
+                    for (int x = 0; x < 16; ++x)
+                        tsad += (uint32_t)std::abs((int)sy[(y0 + y) * pitch + x0 + x] -
+                                                   h264::ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + x + ix, y0 + y + iy));
+                m.seg = (uint8_t)seg_of_tclass(h264::temporal_class(tsad, ix == 0 && iy == 0));
+            }
             const Quant Qm = m.seg ? quant_of(seg_qindex_[m.seg]) : (key ? Q : quant_of(seg_qindex_[0]));
             m.nz = code_luma16(res, pred, Qm, lv, rec);
             m.nz |= code_chroma8(cres[0], cp[0], Qm, lv, crec[0], 16);
@@ -201,7 +202,7 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     if (cfg_.aq >= 3) prev_src_.swap(next_src_);
     au_.clear();
     write_frame(fd, mb_.data(), [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, au_,
-                run_serial);
+                run_serial, &tok_stats_[key ? 1 : 0]);
     int skipped = 0;
     for (const Vp8Mb& m : mb_) skipped += m.nz == 0;
     stats_.frame_index = common_.frames();

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <array>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -81,12 +82,23 @@ inline void segment_qindices(int qp, int aq, int out[kNumSegs]) {
     for (int s = 0; s < kNumSegs; ++s) out[s] = qindex_for_qp(h264::aq3_mb_qp(qp, tclass_of_seg(s), aq));
 }
 
+// Token branch statistics of the last coded frame of one type (13.4): the coefficient probability
+// updates of the next frame of that type are planned from them, so coding needs no separate
+// counting pass over the tokens.
+struct TokenStats {
+    std::vector<std::array<uint32_t, 2>> n;  // [1056] (zeros, ones) per probability
+    bool valid = false;
+};
+
 // Writes a complete VP8 frame (frame tag, key-frame header, first partition, token partitions)
 // from per-macroblock records and levels.  `levels(i)` returns macroblock i's 400 levels (only
 // read for macroblocks with nz != 0).  Token partitions are coded concurrently on `run_parallel`.
+// stats (may be null: no probability updates, e.g. rate-control probes): in, the previous frame's
+// branch statistics of this frame type; out, this frame's.
 void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels,
                  std::vector<uint8_t>& out,
-                 const std::function<void(int, const std::function<void(int)>&)>& run_parallel);
+                 const std::function<void(int, const std::function<void(int)>&)>& run_parallel,
+                 TokenStats* stats = nullptr);
 
 // Near / nearest / best motion vectors of macroblock (mbx, mby) (RFC 6386 find_near_mvs, with
 // the decoder's clamping); every macroblock of the picture is inter (P frames).  cnt[4] out.
@@ -146,6 +158,7 @@ class CpuVp8Encoder {
     int cw_, ch_, mb_w_, mb_h_;
     std::vector<uint8_t> rec_y_[2], rec_uv_[2];
     std::vector<uint8_t> prev_src_, next_src_;  // aq >= 3: previous / this frame's source luma (temporal classes)
+    TokenStats tok_stats_[2];                     // [key]: branch statistics for the probability updates
     int seg_qindex_[kNumSegs] = {0, 0, 0, 0};
     int cur_ = 0;
     bool have_ref_ = false;
@@ -241,7 +254,7 @@ class GpuVp8Encoder final : public VideoEncoder {
     void fill_state(Slot& s, bool key, int qp, int ref, int cur);
     int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
     void check_slot(Slot& s);
-    void write_slot(const Slot& s, std::vector<uint8_t>& out);
+    void write_slot(const Slot& s, std::vector<uint8_t>& out, bool probe = false);
 
     h264::EncoderConfig cfg_;
     h264::EncoderCommon common_;
@@ -258,6 +271,7 @@ class GpuVp8Encoder final : public VideoEncoder {
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     uint8_t* src_keep_[2] = {nullptr, nullptr};  // aq >= 3: source luma of the frames in rec_y_[k]
+    TokenStats tok_stats_[2];                     // [key]: branch statistics for the probability updates
     int cur_ = 0;
     bool have_ref_ = false;
     uint32_t epoch_ = 0;

@@ -33,7 +33,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     Vp8DeviceBuffers& b = s.buf;
     HIP_CHECK(hipMalloc(&b.st, sizeof(Vp8States)));
     HIP_CHECK(hipMalloc(&b.mb, sizeof(Vp8Mb) * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)(nmb + 1)));  // + k_vp8_key's idle-step slot
     HIP_CHECK(hipMalloc(&b.prog, sizeof(uint32_t) * (size_t)geom_.mb_h));
     HIP_CHECK(hipMemsetAsync(b.prog, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
     HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * (size_t)geom_.mb_h * (geom_.coded_w / 4)));
@@ -164,14 +164,15 @@ void GpuVp8Encoder::check_slot(Slot& s) {
     }
 }
 
-void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out) {
+void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out, bool probe) {
     const Vp8Mb* mbs = s.buf.mb_host;
     const int16_t* lv = s.buf.lv_host;
     FrameDesc fd{s.key, cfg_.width, cfg_.height, geom_.mb_w, geom_.mb_h, s.qindex, log2_parts_};
     fd.segmented = s.segmented;
     for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = s.seg_qindex[k];
     write_frame(fd, mbs, [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
-                [&](int n, const std::function<void(int)>& fn) { pool_.run(n, fn); });
+                [&](int n, const std::function<void(int)>& fn) { pool_.run(n, fn); },
+                probe ? nullptr : &tok_stats_[s.key ? 1 : 0]);
 }
 
 int GpuVp8Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp) {
@@ -186,7 +187,7 @@ int GpuVp8Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int 
     HIP_CHECK(hipStreamSynchronize(stream_));
     check_slot(s);
     std::vector<uint8_t> tmp;
-    write_slot(s, tmp);
+    write_slot(s, tmp, true);
     return (int)tmp.size();
 }
 

@@ -85,6 +85,31 @@ def _worker(rank, world, port, cols, rows, tw, th, frames, codec, backend, q):
             pend_r.append(("c", e0, e1))
         W.composite_nv12 = comp
 
+        # host time of the other per-frame stages (the step exceeded the sum of
+        # render + exchange + composite + encode by 0.45 ms)
+        class _TimedEncoder:  # the native encoder takes no attributes: a forwarding proxy
+            def __init__(self, inner):
+                self._inner = inner
+
+            def __getattr__(self, n):
+                return getattr(self._inner, n)
+
+        pipe.enc = _TimedEncoder(pipe.enc)
+        for name, obj, attr in (("ctrl_host", pipe, "_broadcast_ctrl"), ("post_host", pipe.xchg, "post"),
+                                ("submit_host", pipe.enc, "submit"), ("collect_host", pipe.enc, "collect")):
+            if not hasattr(obj, attr):
+                continue
+            rec[name] = []
+
+            def timed(*a, _f=getattr(obj, attr), _n=name, **k):  # noqa: B023
+                t = time.perf_counter()
+                out = _f(*a, **k)
+                rec[_n].append((time.perf_counter() - t) * 1e3)
+                return out
+            try:
+                setattr(obj, attr, timed)
+            except (AttributeError, TypeError):  # native objects may not take attributes
+                del rec[name]
         enc_ms, step_ms = [], []
         for i in range(frames):
             t = time.perf_counter()
@@ -103,6 +128,8 @@ def _worker(rank, world, port, cols, rows, tw, th, frames, codec, backend, q):
         summ["encode"] = round(statistics.median(enc_ms[warm:]), 4)
         summ["step"] = round(statistics.median(step_ms[warm:]), 4)
         summ["fps"] = round(1e3 / statistics.mean(step_ms[warm:]), 2)
+        host = [k for k in ("ctrl_host", "post_host", "exchange", "submit_host", "collect_host") if k in summ]
+        summ["host_unaccounted"] = round(summ["step"] - sum(summ[k] for k in host), 4)
         q.put({"layout": f"{cols}x{rows}", "tile": f"{tw}x{th}", "wall": f"{geo.width}x{geo.height}", "codec": pipe.codec,
                "ranks": world, "gpus": ndev, "backend": backend, "frames": frames, "median_ms": summ,
                "last_au_bytes": len(fr.au)})
