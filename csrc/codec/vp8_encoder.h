@@ -27,6 +27,12 @@ namespace vp8 {
 class BoolEncoder {
    public:
     explicit BoolEncoder(std::vector<uint8_t>& out) : out_(out) {}
+    // The RFC's one-bit-at-a-time normalisation, batched: the shift count comes from the leading
+    // zeros of the range and is applied up to the next byte boundary at a time.  A carry can only
+    // leave the 32-bit window on the shift that completes a byte (the low end holds at most
+    // 24 + 7 bits plus one split before it), so it is applied right before that byte goes out --
+    // where the per-bit loop applies it.  Same bits as the per-bit form (tests: libwebp key
+    // frames, the in-tree decoder, GPU == CPU streams).
     void put(int prob, int bit) {
         const uint32_t split = 1 + (((range_ - 1) * (uint32_t)prob) >> 8);
         if (bit) {
@@ -35,11 +41,16 @@ class BoolEncoder {
         } else {
             range_ = split;
         }
-        while (range_ < 128) {
-            range_ <<= 1;
-            if (bottom_ & (1u << 31)) carry();
-            bottom_ <<= 1;
-            if (!--bit_count_) {
+        int s = __builtin_clz(range_) - 24;  // range_ in [1, 255]: shifts to bring it to [128, 255]
+        if (s <= 0) return;
+        range_ <<= s;
+        while (s > 0) {
+            const int k = s < bit_count_ ? s : bit_count_;
+            bottom_ <<= k;
+            s -= k;
+            bit_count_ -= k;
+            if (bit_count_ == 0) {
+                if (bottom_ >> 32) carry();
                 out_.push_back((uint8_t)(bottom_ >> 24));
                 bottom_ &= (1u << 24) - 1;
                 bit_count_ = 8;
@@ -65,7 +76,8 @@ class BoolEncoder {
         }
     }
     std::vector<uint8_t>& out_;
-    uint32_t range_ = 255, bottom_ = 0;
+    uint32_t range_ = 255;
+    uint64_t bottom_ = 0;  // 32-bit low end; bit 32 is a carry out of the window (put)
     int bit_count_ = 24;
 };
 
