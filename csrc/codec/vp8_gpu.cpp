@@ -33,7 +33,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     Vp8DeviceBuffers& b = s.buf;
     HIP_CHECK(hipMalloc(&b.st, sizeof(Vp8States)));
     HIP_CHECK(hipMalloc(&b.mb, sizeof(Vp8Mb) * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)(nmb + 1)));  // + k_vp8_key's idle-step slot
+    HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.prog, sizeof(uint32_t) * (size_t)geom_.mb_h));
     HIP_CHECK(hipMemsetAsync(b.prog, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
     HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * (size_t)geom_.mb_h * (geom_.coded_w / 4)));

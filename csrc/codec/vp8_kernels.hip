@@ -9,16 +9,15 @@
 // blocks, lane 24 the second-order Y2 block -- the block index of a lane is its token block index,
 // so the non-zero mask is one ballot.  The dead-zone division of the quantiser is an exact
 // multiply-high (Vp8FrameState::qm, exact for every coefficient the transforms produce).
-// Key frames predict from reconstructed neighbours: one wave per macroblock row, rows one
-// macroblock behind the row above; the rows of a workgroup (up to 4) step in lockstep with their
-// hand-off lines in LDS, and only a group's first row waits on the group above through an
-// agent-scope hand-off line and an epoch-tagged progress word (bounded spins; a timeout raises
-// the mapped error word instead of hanging).  Inter frames segment their macroblocks by the
-// temporal AQ classes (segment quantisers, vp8_core.h Seg).  The boolean coder runs on host threads (vp8_bitstream.cpp);
+// Key frames predict from reconstructed neighbours: one wave per macroblock row walks its row,
+// the row below follows one macroblock behind, fed the bottom sample rows through an agent-scope
+// hand-off line and an epoch-tagged progress word (bounded spins; a timeout raises the mapped
+// error word instead of hanging).  (Rows stepping in lockstep groups with LDS hand-off lines
+// measured slower -- 2.0 ms with 4-row, 4.1 ms with 16-row groups against 1.41 ms at 1080p:
+// the per-macroblock chain, not the hand-off, bounds the key frame; profiles/r04_vp8/NOTES.md.)
+// Inter frames segment their macroblocks by the temporal AQ classes (vp8_core.h Seg).  The boolean coder runs on host threads (vp8_bitstream.cpp);
 // k_vp8_gather hands it only the coded macroblocks' levels, compacted per row, in mapped memory.
 #include <hip/hip_runtime.h>
-
-#include <algorithm>
 
 #include "../common/hip_check.h"
 #include "h264_core.h"
@@ -439,78 +438,34 @@ __device__ __forceinline__ void wait_row(const uint32_t* p, uint32_t epoch, int 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
 }
 
-// Key frames: one workgroup per group of R macroblock rows (R waves, up to kKeyMaxRows), the
-// rows of a group in a lockstep diagonal -- at step t wave w codes macroblock t - w of its row --
-// with the row-to-row hand-off (bottom luma / chroma rows) in LDS lines: the macroblock above
-// was coded a step earlier, behind the step's workgroup barriers.  Only the first row of a group
-// waits on the previous group's last row, through the global hand-off line and its progress word
-// (agent-scope release / acquire, bounded spin), polled for the macroblock one step ahead so the
-// wait overlaps the current step.  (One wave per row with every hand-off through global memory
-// spent most of the key frame waiting for those stores to become visible: 1.41 ms at 1080p.)
-// 4 rows = one wave per SIMD: 16 rows in one workgroup shared 4 SIMDs per lockstep step and ran
-// the key frame 3x slower than one wave per row (4.1 vs 1.41 ms at 1080p, profiles/r04_vp8).
-constexpr int kKeyMaxRows = 4;
-
-__global__ __launch_bounds__(64 * kKeyMaxRows) void k_vp8_key(h264::Geometry g, const Vp8States* __restrict__ st,
-                                                              const uint8_t* __restrict__ src_y,
-                                                              const uint8_t* __restrict__ src_uv,
-                                                              Vp8Mb* __restrict__ mbs, int16_t* __restrict__ lv,
-                                                              uint32_t* __restrict__ prog, uint64_t* __restrict__ line,
-                                                              int* __restrict__ err, int rows_per_group) {
-    extern __shared__ uint8_t lline[];  // [R][2][coded_w]: bottom luma row, bottom chroma (NV12) row
-    __shared__ MbLds sw[kKeyMaxRows];
-    __shared__ KeyEdges Ew[kKeyMaxRows];
+__global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                 const uint8_t* __restrict__ src_y,
+                                                 const uint8_t* __restrict__ src_uv, Vp8Mb* __restrict__ mbs,
+                                                 int16_t* __restrict__ lv, uint32_t* __restrict__ prog,
+                                                 uint64_t* __restrict__ line, int* __restrict__ err) {
+    __shared__ MbLds s;
+    __shared__ KeyEdges E;
     const Vp8FrameState& F = st->v;
-    const int R = rows_per_group, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int grp = blockIdx.x, mby = grp * R + wave;
-    const int nrows = min(R, g.mb_h - grp * R);  // rows of this group
-    const bool row_ok = wave < nrows;
-    const int y0 = mby * 16, cw = g.coded_w;
+    const int mby = blockIdx.x, lane = threadIdx.x, y0 = mby * 16;
     const uint32_t epoch = (uint32_t)F.epoch;
-    const int words = cw / 8;  // luma words per global hand-off row; chroma follows
+    const int words = g.coded_w / 8;  // luma words per hand-off row; chroma follows
     const bool top = mby == 0, bottom = mby == g.mb_h - 1;
-    const bool global_above = wave == 0 && !top;            // first row of a group: the previous group's last row
-    const bool global_below = wave == nrows - 1 && !bottom;  // last row of a group hands down through memory
     const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * 2 * words;
     uint64_t* my_line = line + (size_t)mby * 2 * words;
-    MbLds& s = sw[wave];
-    KeyEdges& E = Ew[wave];
-    uint8_t* my_ly = lline + (size_t)wave * 2 * cw;
-    uint8_t* my_lc = my_ly + cw;
-    const uint8_t* up_ly = lline + (size_t)(wave > 0 ? wave - 1 : 0) * 2 * cw;
-    const uint8_t* up_lc = up_ly + cw;
-    int16_t* const lv_dummy = lv + (size_t)g.mb_w * g.mb_h * kCoefPerMb;  // levels of idle steps (never read)
-    // global hand-off words of the macroblock above, fetched a step ahead (first row of a group)
-    uint64_t gw = 0;
-    auto fetch_above = [&](int x) {  // lanes 0..5: luma words 2x, 2x+1; chroma words; corners
-        if (!global_above || x < 0 || x >= g.mb_w) return;
-        if (lane == 0) wait_row(prog + mby - 1, epoch, x + 1, err);
-        // (the other lanes' loads follow lane 0's acquire: a wave executes in order, and the
-        // acquire fence inside wait_row is wave-wide)
-        if (lane < 6) {
-            const int wi = lane < 2 ? 2 * x + lane : (lane < 4 ? words + 2 * x + lane - 2 : (lane == 4 ? 2 * x - 1 : words + 2 * x - 1));
-            const bool need = lane < 4 || x > 0;
-            gw = need ? __hip_atomic_load((const gu64*)(above_line + wi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        }
-    };
-    fetch_above(0 - 0);
-    const int steps = g.mb_w + nrows - 1;
-    for (int step = 0; step < steps; ++step) {
-        const int mbx = step - wave;
-        const bool valid = row_ok && mbx >= 0 && mbx < g.mb_w;
+    for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int x0 = mbx * 16, mbi = mby * g.mb_w + mbx;
         const bool left = mbx > 0;
-        const uint64_t gcur = gw;
-        if (valid) stage_src(s, g, src_y, src_uv, x0, y0, lane);
-        // ---- edges: above row and corner (LDS line of the wave above, or the global hand-off
-        // line for a group's first row), left from this wave's previous macroblock
-        if (valid) {
-            if (top) {
-                if (lane < 16) E.ay[lane] = 127;
-                if (lane < 8) E.au[lane] = E.av[lane] = 127;
-                if (lane == 0) E.cy = E.cu = E.cv = 127;
-            } else if (global_above) {
-                const uint64_t w = gcur;
+        stage_src(s, g, src_y, src_uv, x0, y0, lane);
+        // ---- edges: above row and corner from the row above (hand-off line), left from our last MB
+        if (!top) {
+            if (lane == 0) wait_row(prog + mby - 1, epoch, mbx + 1, err);
+            __syncthreads();
+            if (lane < 6) {
+                int wi = lane < 2 ? 2 * mbx + lane : (lane < 4 ? words + 2 * mbx + lane - 2 : (lane == 4 ? 2 * mbx - 1 : words + 2 * mbx - 1));
+                const bool need = lane < 4 || left;
+                const uint64_t w = need ? __hip_atomic_load((const gu64*)(above_line + wi), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0;
                 if (lane < 2) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) E.ay[8 * lane + k] = (int)((w >> (8 * k)) & 0xff);
@@ -522,118 +477,103 @@ __global__ __launch_bounds__(64 * kKeyMaxRows) void k_vp8_key(h264::Geometry g, 
                     }
                 } else if (lane == 4) {
                     E.cy = left ? (int)(w >> 56) : 129;
-                } else if (lane == 5) {
+                } else {
                     E.cu = left ? (int)((w >> 48) & 0xff) : 129;
                     E.cv = left ? (int)(w >> 56) : 129;
                 }
-            } else {
-                if (lane < 16) E.ay[lane] = up_ly[x0 + lane];
-                else if (lane < 24) E.au[lane - 16] = up_lc[x0 + 2 * (lane - 16)];
-                else if (lane < 32) E.av[lane - 24] = up_lc[x0 + 2 * (lane - 24) + 1];
-                else if (lane == 32) E.cy = left ? up_ly[x0 - 1] : 129;
-                else if (lane == 33) E.cu = left ? up_lc[x0 - 2] : 129;
-                else if (lane == 34) E.cv = left ? up_lc[x0 - 1] : 129;
             }
-            if (!left) {
-                if (lane < 16) E.ly[lane] = 129;
-                if (lane < 8) E.lu[lane] = E.lvv[lane] = 129;
-            }
+        } else {
+            if (lane < 16) E.ay[lane] = 127;
+            if (lane < 8) E.au[lane] = E.av[lane] = 127;
+            if (lane == 0) E.cy = E.cu = E.cv = 127;
         }
-        fetch_above(mbx + 1);  // next step's words (overlaps this step's work)
+        if (!left) {
+            if (lane < 16) E.ly[lane] = 129;
+            if (lane < 8) E.lu[lane] = E.lvv[lane] = 129;
+        }
         __syncthreads();
         // ---- mode decisions: SAD of the four 16x16 modes (4 samples per lane), the four chroma modes
+        const int nav = top ? 0 : 1, nlf = left ? 1 : 0;
+        const int dcy = dc_value(wsum((lane < 16 && !top ? E.ay[lane] : 0) + (lane >= 16 && lane < 32 && left ? E.ly[lane - 16] : 0)),
+                                 nav + nlf, 3);
+        const int dcu = dc_value(wsum((lane < 8 && !top ? E.au[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lu[lane - 8] : 0)),
+                                 nav + nlf, 2);
+        const int dcv = dc_value(wsum((lane < 8 && !top ? E.av[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lvv[lane - 8] : 0)),
+                                 nav + nlf, 2);
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
         int ymode = 0, uvmode = 0;
-        if (valid) {
-            const int nav = top ? 0 : 1, nlf = left ? 1 : 0;
-            const int dcy = dc_value(wsum((lane < 16 && !top ? E.ay[lane] : 0) + (lane >= 16 && lane < 32 && left ? E.ly[lane - 16] : 0)),
-                                     nav + nlf, 3);
-            const int dcu = dc_value(wsum((lane < 8 && !top ? E.au[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lu[lane - 8] : 0)),
-                                     nav + nlf, 2);
-            const int dcv = dc_value(wsum((lane < 8 && !top ? E.av[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lvv[lane - 8] : 0)),
-                                     nav + nlf, 2);
-            const int r = lane >> 2, c4 = (lane & 3) * 4;
-            {
-                int sad[4] = {0, 0, 0, 0};
+        {
+            int sad[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int sv = s.src[r * 16 + c4 + j];
+            for (int j = 0; j < 4; ++j) {
+                const int sv = s.src[r * 16 + c4 + j];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) sad[m] += abs(sv - pred_of(m, E.ay[c4 + j], E.ly[r], E.cy, dcy));
-                }
-                uint32_t best = ~0u;
+                for (int m = 0; m < 4; ++m) sad[m] += abs(sv - pred_of(m, E.ay[c4 + j], E.ly[r], E.cy, dcy));
+            }
+            uint32_t best = ~0u;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const uint32_t t = (uint32_t)wsum(sad[m]);
-                    if (t < best) {
-                        best = t;
-                        ymode = m;
-                    }
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t t = (uint32_t)wsum(sad[m]);
+                if (t < best) {
+                    best = t;
+                    ymode = m;
                 }
             }
-            const int cx = lane & 7, cy = lane >> 3;
-            {
-                int sad[4] = {0, 0, 0, 0};
-                const int su = s.su[cy * 8 + cx], sv = s.sv[cy * 8 + cx];
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    sad[m] = abs(su - pred_of(m, E.au[cx], E.lu[cy], E.cu, dcu)) +
-                             abs(sv - pred_of(m, E.av[cx], E.lvv[cy], E.cv, dcv));
-                uint32_t best = ~0u;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const uint32_t t = (uint32_t)wsum(sad[m]);
-                    if (t < best) {
-                        best = t;
-                        uvmode = m;
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = (uint8_t)pred_of(ymode, E.ay[c4 + j], E.ly[r], E.cy, dcy);
-            s.pu[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.au[cx], E.lu[cy], E.cu, dcu);
-            s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
         }
-        __syncthreads();
-        // every wave codes (idle steps into the dummy level slot: code_mb holds workgroup barriers)
-        const uint32_t nz = code_mb(s, F, valid ? lv + (size_t)mbi * kCoefPerMb : lv_dummy, lane);
-        if (valid) {
-            // ---- bottom rows into this wave's LDS line (the wave below reads them next step), and
-            // for a group's last row also down through memory, then its progress word
-            if (lane < 16) my_ly[x0 + lane] = s.rec[15 * 16 + lane];
-            else if (lane < 32) {
-                const int k = lane - 16;
-                my_lc[x0 + k] = (k & 1) ? s.rv[7 * 8 + (k >> 1)] : s.ru[7 * 8 + (k >> 1)];
-            }
-            if (global_below && lane < 4) {
-                uint64_t w = 0;
-                if (lane < 2) {
+        const int cx = lane & 7, cy = lane >> 3;
+        {
+            int sad[4] = {0, 0, 0, 0};
+            const int su = s.su[cy * 8 + cx], sv = s.sv[cy * 8 + cx];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) w |= (uint64_t)s.rec[15 * 16 + 8 * lane + k] << (8 * k);
-                } else {
+            for (int m = 0; m < 4; ++m)
+                sad[m] = abs(su - pred_of(m, E.au[cx], E.lu[cy], E.cu, dcu)) +
+                         abs(sv - pred_of(m, E.av[cx], E.lvv[cy], E.cv, dcv));
+            uint32_t best = ~0u;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        w |= ((uint64_t)s.ru[7 * 8 + 4 * (lane - 2) + k] << (16 * k)) |
-                             ((uint64_t)s.rv[7 * 8 + 4 * (lane - 2) + k] << (16 * k + 8));
+            for (int m = 0; m < 4; ++m) {
+                const uint32_t t = (uint32_t)wsum(sad[m]);
+                if (t < best) {
+                    best = t;
+                    uvmode = m;
                 }
-                const int wi = lane < 2 ? 2 * mbx + lane : words + 2 * mbx + lane - 2;
-                __hip_atomic_store((gu64*)(my_line + wi), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (global_below) {
-                // every lane's hand-off words ordered before the flag: agent-scope release fence + store
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                if (lane == 0)
-                    __hip_atomic_store((gu32*)(prog + mby), (epoch << 12) | (uint32_t)(mbx + 1), __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = (uint8_t)pred_of(ymode, E.ay[c4 + j], E.ly[r], E.cy, dcy);
+        s.pu[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.au[cx], E.lu[cy], E.cu, dcu);
+        s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
+        __syncthreads();
+        const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane);
+        // ---- hand the bottom rows down, then publish progress
+        if (!bottom && lane < 4) {
+            uint64_t w = 0;
+            if (lane < 2) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) w |= (uint64_t)s.rec[15 * 16 + 8 * lane + k] << (8 * k);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    w |= ((uint64_t)s.ru[7 * 8 + 4 * (lane - 2) + k] << (16 * k)) |
+                         ((uint64_t)s.rv[7 * 8 + 4 * (lane - 2) + k] << (16 * k + 8));
             }
-            uint32_t sse[3];
-            store_rec(s, g, F, x0, y0, lane, sse);
-            store_record(mbs + mbi, 0, 0, ymode, uvmode, nz, sse, lane);
-            // left edges of the next macroblock
-            if (lane < 16) E.ly[lane] = s.rec[lane * 16 + 15];
-            if (lane < 8) {
-                E.lu[lane] = s.ru[lane * 8 + 7];
-                E.lvv[lane] = s.rv[lane * 8 + 7];
-            }
+            const int wi = lane < 2 ? 2 * mbx + lane : words + 2 * mbx + lane - 2;
+            __hip_atomic_store((gu64*)(my_line + wi), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!bottom) {
+            // every lane's hand-off words ordered before the flag: agent-scope release fence + store
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (lane == 0)
+                __hip_atomic_store((gu32*)(prog + mby), (epoch << 12) | (uint32_t)(mbx + 1), __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint32_t sse[3];
+        store_rec(s, g, F, x0, y0, lane, sse);
+        store_record(mbs + mbi, 0, 0, ymode, uvmode, nz, sse, lane);
+        // left edges of the next macroblock
+        if (lane < 16) E.ly[lane] = s.rec[lane * 16 + 15];
+        if (lane < 8) {
+            E.lu[lane] = s.ru[lane * 8 + 7];
+            E.lvv[lane] = s.rv[lane * 8 + 7];
         }
         __syncthreads();
     }
@@ -704,23 +644,13 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const 
                        b.lv);
 }
 
-// Rows per key-frame group: as many as the LDS hand-off lines (2 x coded_w bytes per row) allow
-// beside the static per-wave state, at most kKeyMaxRows.
-int key_rows_per_group(int coded_w) {
-    const int budget = 160 * 1024 - (int)(kKeyMaxRows * (sizeof(MbLds) + sizeof(KeyEdges))) - 1024;
-    return std::max(1, std::min(kKeyMaxRows, budget / (2 * coded_w)));
-}
-
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream, bool save_src) {
     if (save_src)  // the next inter frame's temporal classes compare against this source
         hipLaunchKernelGGL(k_vp8_save_src, dim3((g.coded_w / 4 + 255) / 256, g.coded_h), dim3(256), 0, stream, g, b.st,
                            src_y);
-    const int R = key_rows_per_group(g.coded_w);
-    const size_t lds = (size_t)R * 2 * g.coded_w;
-    ensure_func_attr(reinterpret_cast<const void*>(&k_vp8_key), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_vp8_key, dim3((g.mb_h + R - 1) / R), dim3(64 * R), lds, stream, g, b.st, src_y, src_uv, b.mb,
-                       b.lv, b.prog, b.line, b.err, R);
+    hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv, b.prog,
+                       b.line, b.err);
 }
 
 void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream) {
