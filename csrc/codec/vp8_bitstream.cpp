@@ -2,6 +2,7 @@
 // size, the first partition (frame header + per-macroblock modes and motion vectors) and the
 // token partitions (one per MB row modulo the partition count, written concurrently -- a token
 // partition's contexts depend only on the coefficients, which are known before coding starts).
+#include <exception>
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -292,10 +293,10 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         std::memset(upd, 0, sizeof upd);
         std::memcpy(probs, kCoefProbs0, sizeof probs);
     }
-    // ---- first partition
+    // ---- first partition (a job beside the token partitions: it reads only modes / vectors)
     std::vector<uint8_t> p1;
     p1.reserve(16 + (size_t)nmb / 2);
-    {
+    auto code_first = [&]() {
         BoolEncoder e(p1);
         if (f.key) {
             e.literal(0, 1);  // color_space
@@ -401,13 +402,22 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                 put_mv_component(e, (m.mvx - near[0][0]) / 2, kMvDefault[1]);
             }
         e.flush();
-    }
-    if (p1.size() >= (1u << 19)) throw std::runtime_error("vp8 writer: first partition too large");
+    };
     // ---- token partitions, concurrently, over the updated probabilities (counting this frame's
     // branch statistics on the way when the caller keeps them)
     std::vector<std::vector<uint8_t>> parts((size_t)nparts);
     std::vector<std::array<uint32_t, 2>> cnt(stats ? (size_t)nparts * 1056 : 0, std::array<uint32_t, 2>{0u, 0u});
-    run_parallel(nparts, [&](int p) {
+    std::exception_ptr first_err;
+    run_parallel(nparts + 1, [&](int j) {
+        if (j == 0) {
+            try {
+                code_first();
+            } catch (...) {
+                first_err = std::current_exception();
+            }
+            return;
+        }
+        const int p = j - 1;
         parts[(size_t)p].reserve(4096);
         BoolEncoder e(parts[(size_t)p]);
         if (stats) {
@@ -419,6 +429,8 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         }
         e.flush();
     });
+    if (first_err) std::rethrow_exception(first_err);
+    if (p1.size() >= (1u << 19)) throw std::runtime_error("vp8 writer: first partition too large");
     if (stats) {
         stats->n.assign(1056, std::array<uint32_t, 2>{0u, 0u});
         for (int p = 0; p < nparts; ++p)
@@ -495,6 +507,13 @@ void PartitionPool::run(int n, const std::function<void(int)>& fn) {
     finished_ = 0;
     ++gen_;
     cv_.notify_all();
+    while (next_ < total_) {  // the caller takes jobs too (it is awake already)
+        const int k = next_++;
+        lk.unlock();
+        fn(k);
+        lk.lock();
+        ++finished_;
+    }
     done_cv_.wait(lk, [&] { return finished_ == total_; });
     job_ = nullptr;
     total_ = 0;
