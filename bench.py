@@ -208,6 +208,10 @@ def main() -> None:
                     help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1; "
                          "3: also the next frame's launches stay queued while the host collects, so the host "
                          "turnaround overlaps GPU work; 1: strictly one frame at a time, lowest back-to-back latency)")
+    ap.add_argument("--capture-stream", type=int, default=-1,
+                    help="depth > 1: render + convert on a capture stream, one NV12 buffer per frame in flight "
+                         "(frame n+1's capture overlaps frame n's analysis); -1 = H.264 only (measured gain), "
+                         "1 = every codec, 0 = one analysis stream")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")
     ap.add_argument("--sessions-per-gpu", type=int, default=1,
@@ -285,6 +289,7 @@ def main() -> None:
     cfg.noise = args.noise
     cfg.content = content
     cfg.use_graph = args.graph
+    cfg.capture_stream = args.capture_stream
     cfg.enc.pipeline_depth = args.depth
     cfg.codec = args.codec
     ow, oh = (args.out_width or args.width), (args.out_height or args.height)
@@ -394,6 +399,7 @@ def main() -> None:
             "encoded_fps_per_gpu": round(per_gpu, 2),
             "sessions_per_gpu": K,
             "hip_graph": bool(args.graph),
+            "capture_stream": bool(sessions[0].capture_stream_active),
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),

@@ -287,7 +287,9 @@ PYBIND11_MODULE(_native, m) {
              })
         .def("request_idr", [](vp8::CpuVp8Encoder& e) { e.common().request_idr(); })
         .def("set_bitrate", [](vp8::CpuVp8Encoder& e, int k) { e.common().set_bitrate(k); })
-        .def_property_readonly("stats", &vp8::CpuVp8Encoder::last_stats);
+        .def_property_readonly("stats", &vp8::CpuVp8Encoder::last_stats)
+        .def_property_readonly("writer_first_us", &vp8::CpuVp8Encoder::writer_first_us)
+        .def_property_readonly("writer_tokens_us", &vp8::CpuVp8Encoder::writer_tokens_us);
 
     py::class_<vp8::GpuVp8Encoder>(m, "GpuVp8Encoder")
         .def(py::init([](const h264::EncoderConfig& c, uintptr_t stream) {
@@ -628,6 +630,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("mask_x1", &SessionConfig::mask_x1)
         .def_readwrite("mask_y1", &SessionConfig::mask_y1)
         .def_readwrite("scale_valu", &SessionConfig::scale_valu)
+        .def_readwrite("capture_stream", &SessionConfig::capture_stream)
         .def_readwrite("enc", &SessionConfig::enc);
 
     py::class_<FrameResult>(m, "FrameResult")
@@ -712,6 +715,7 @@ PYBIND11_MODULE(_native, m) {
         .def("request_idr", &Session::request_idr)
         .def("set_bitrate", &Session::set_bitrate)
         .def_property_readonly("stream", [](Session& s) { return reinterpret_cast<uintptr_t>(s.stream()); })
+        .def_property_readonly("capture_stream_active", &Session::capture_stream_active)
         .def_property_readonly("nv12_y_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_y()); })
         .def_property_readonly("nv12_uv_ptr", [](Session& s) { return reinterpret_cast<uintptr_t>(s.nv12_uv()); })
         .def_property_readonly("nv12_pitch", &Session::nv12_pitch)

@@ -373,7 +373,7 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
         if (cfg_.aq >= 3)  // the next P picture's previous source (P pictures: k_inter_encode stores it)
             launch_save_src(geom_, sl.buf, src_y, stream_);
     } else {
-        if (stream_a_ && pub && ref_seq_ + 1 == seq_) {  // the previous picture recorded ref_ready_
+        if (stream_a_ && hpel_side_ && pub && ref_seq_ + 1 == seq_) {  // the previous picture recorded ref_ready_
             HIP_CHECK(hipStreamWaitEvent(stream_a_, ref_ready_, 0));
             launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_a_, pub);
             HIP_CHECK(hipEventRecord(sl.hpel_done, stream_a_));
@@ -413,7 +413,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
             sse_ready = sl.deblock_done;
         }
     }
-    if (stream_a_ && publish) {  // the next picture's reference is final
+    if (stream_a_ && hpel_side_ && publish) {  // the next picture's reference is final
         HIP_CHECK(hipEventRecord(ref_ready_, stream_));
         ref_seq_ = seq_;
     }

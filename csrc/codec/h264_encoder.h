@@ -230,6 +230,7 @@ class GpuH264Encoder final : public VideoEncoder {
     void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void enqueue_entropy() override;
     void link_entropy() override;
+    void set_hpel_side_stream(bool on) override { hpel_side_ = on; }
     // Completion event of the last collected frame.
     hipEvent_t done_event() const override { return last_done_; }
     bool device_clock() const override { return true; }
@@ -264,6 +265,7 @@ class GpuH264Encoder final : public VideoEncoder {
     // kernel), beside the capture and colour conversion of the new picture, which it does not
     // depend on; k_me_full waits for it (profiles/r04_h264)
     hipStream_t stream_a_ = nullptr;
+    bool hpel_side_ = true;  // set_hpel_side_stream
     hipEvent_t ref_ready_ = nullptr;
     uint64_t seq_ = 0, ref_seq_ = ~0ull;  // pictures prepared; the one whose reconstruction ref_ready_ marks
     int depth_ = 1;

@@ -52,6 +52,10 @@ class VideoEncoder {
     virtual void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) { (void)idr; (void)src_y; (void)src_uv; }
     virtual void enqueue_entropy() {}
     virtual void link_entropy() {}
+    // false: the reference half-pel planes are interpolated on the analysis stream itself (the
+    // session converts the next frame on a capture stream, so nothing on the analysis stream
+    // would overlap a side-stream interpolation -- it would only add two cross-queue hand-offs)
+    virtual void set_hpel_side_stream(bool on) { (void)on; }
 };
 
 }  // namespace mx

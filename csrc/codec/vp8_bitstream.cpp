@@ -5,6 +5,7 @@
 #include <exception>
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -378,6 +379,18 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                 if (m.ymode != kInter) throw std::logic_error("vp8 writer: intra MB in an inter frame");
                 e.put(prob_intra, 1);  // is_inter_mb
                 e.put(prob_last, 0);   // reference: last frame
+                if (m.mvx == 0 && m.mvy == 0) {
+                    // ZEROMV needs only cnt[0] of find_near_mvs: the weights of the inter
+                    // neighbours (above 2, left 2, above-left 1) with a zero vector
+                    auto zero_at = [&](int x, int y) {
+                        if (x < 0 || y < 0) return false;
+                        const Vp8Mb& q = mbs[y * f.mb_w + x];
+                        return q.ymode == kInter && q.mvx == 0 && q.mvy == 0;
+                    };
+                    const int c0 = 2 * zero_at(mbx, mby - 1) + 2 * zero_at(mbx - 1, mby) + zero_at(mbx - 1, mby - 1);
+                    e.put(kModeContexts[c0][0], 0);
+                    continue;
+                }
                 int near[3][2], cnt[4];
                 find_near_mvs(mbs, f.mb_w, f.mb_h, mbx, mby, near, cnt);
                 const uint8_t pr[4] = {kModeContexts[cnt[0]][0], kModeContexts[cnt[1]][1], kModeContexts[cnt[2]][2],
@@ -408,7 +421,14 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
     std::vector<std::vector<uint8_t>> parts((size_t)nparts);
     std::vector<std::array<uint32_t, 2>> cnt(stats ? (size_t)nparts * 1056 : 0, std::array<uint32_t, 2>{0u, 0u});
     std::exception_ptr first_err;
+    std::vector<double> job_us((size_t)nparts + 1, 0.0);
     run_parallel(nparts + 1, [&](int j) {
+        const auto t0 = std::chrono::steady_clock::now();
+        struct Acc {
+            double& a;
+            std::chrono::steady_clock::time_point t;
+            ~Acc() { a = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count(); }
+        } acc{job_us[(size_t)j], t0};
         if (j == 0) {
             try {
                 code_first();
@@ -439,6 +459,9 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                 stats->n[k][1] += cnt[(size_t)p * 1056 + k][1];
             }
         stats->valid = true;
+        stats->us_first = job_us[0];
+        stats->us_tokens = 0;
+        for (int p = 0; p < nparts; ++p) stats->us_tokens += job_us[(size_t)p + 1];
     }
     // ---- assemble: frame tag, key-frame start code + size, partition 1, partition sizes, data
     const uint32_t tag = (f.key ? 0u : 1u) | (0u << 1) | (1u << 4) | ((uint32_t)p1.size() << 5);

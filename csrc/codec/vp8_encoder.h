@@ -28,34 +28,23 @@ class BoolEncoder {
    public:
     explicit BoolEncoder(std::vector<uint8_t>& out) : out_(out) {}
     // The RFC's one-bit-at-a-time normalisation, batched: the shift count comes from the leading
-    // zeros of the range and is applied up to the next byte boundary at a time.  A carry can only
-    // leave the 32-bit window on the shift that completes a byte (the low end holds at most
-    // 24 + 7 bits plus one split before it), so it is applied right before that byte goes out --
-    // where the per-bit loop applies it.  Same bits as the per-bit form (tests: libwebp key
-    // frames, the in-tree decoder, GPU == CPU streams).
+    // zeros of the range and the whole shift is applied at once to a 64-bit low end that keeps
+    // up to 38 pending bits; whole bytes leave once 32 bits are pending (where the per-bit form
+    // emits its byte, so the byte alignment is the same), each after the carry that reached
+    // above them (one bit: low + range never exceeds the interval) went into the bytes already
+    // written.  The coded bit selects with masks instead of a branch (the bits of a picture are
+    // close to random: a branch on them mispredicts).  Same bits as the per-bit form (tests:
+    // libwebp key frames, the in-tree decoder, GPU == CPU streams).
     void put(int prob, int bit) {
         const uint32_t split = 1 + (((range_ - 1) * (uint32_t)prob) >> 8);
-        if (bit) {
-            bottom_ += split;
-            range_ -= split;
-        } else {
-            range_ = split;
-        }
-        int s = __builtin_clz(range_) - 24;  // range_ in [1, 255]: shifts to bring it to [128, 255]
-        if (s <= 0) return;
+        const uint32_t m = 0u - (uint32_t)(bit != 0);
+        low_ += split & m;
+        range_ = ((range_ - split) & m) | (split & ~m);
+        const int s = __builtin_clz(range_) - 24;  // range_ in [1, 255]: shifts to bring it to [128, 255]
         range_ <<= s;
-        while (s > 0) {
-            const int k = s < bit_count_ ? s : bit_count_;
-            bottom_ <<= k;
-            s -= k;
-            bit_count_ -= k;
-            if (bit_count_ == 0) {
-                if (bottom_ >> 32) carry();
-                out_.push_back((uint8_t)(bottom_ >> 24));
-                bottom_ &= (1u << 24) - 1;
-                bit_count_ = 8;
-            }
-        }
+        low_ <<= s;
+        pend_ += s;
+        if (pend_ >= 32) emit();
     }
     void literal(uint32_t v, int n) {
         for (int i = n - 1; i >= 0; --i) put(128, (v >> i) & 1);
@@ -65,20 +54,28 @@ class BoolEncoder {
     }
 
    private:
-    void carry() {
-        for (size_t i = out_.size(); i-- > 0;) {
-            if (out_[i] == 255) {
-                out_[i] = 0;
-            } else {
-                ++out_[i];
-                return;
+    void emit() {  // pend_ >= 32: the bytes above the low 24 pending bits go out
+        while (pend_ >= 32) {
+            if (low_ >> pend_) {  // carry into the bytes already written
+                for (size_t i = out_.size(); i-- > 0;) {
+                    if (out_[i] == 255) {
+                        out_[i] = 0;
+                    } else {
+                        ++out_[i];
+                        break;
+                    }
+                }
+                low_ &= (uint64_t(1) << pend_) - 1;
             }
+            pend_ -= 8;
+            out_.push_back((uint8_t)(low_ >> pend_));
+            low_ &= (uint64_t(1) << pend_) - 1;
         }
     }
     std::vector<uint8_t>& out_;
     uint32_t range_ = 255;
-    uint64_t bottom_ = 0;  // 32-bit low end; bit 32 is a carry out of the window (put)
-    int bit_count_ = 24;
+    uint64_t low_ = 0;  // pend_ pending bits (bit pend_: a carry not yet added to out_)
+    int pend_ = 8;      // the 8-bit window counts: the first byte leaves after 24 shifts
 };
 
 struct FrameDesc {
@@ -100,6 +97,8 @@ inline void segment_qindices(int qp, int aq, int out[kNumSegs]) {
 struct TokenStats {
     std::vector<std::array<uint32_t, 2>> n;  // [1056] (zeros, ones) per probability
     bool valid = false;
+    // diagnostics of the last write_frame: first partition / sum over token partitions (host us)
+    double us_first = 0, us_tokens = 0;
 };
 
 // Writes a complete VP8 frame (frame tag, key-frame header, first partition, token partitions)
@@ -162,6 +161,9 @@ class CpuVp8Encoder {
     const std::vector<uint8_t>& recon_uv() const { return rec_uv_[cur_]; }
     int coded_pitch() const { return cw_; }
     const std::vector<Vp8Mb>& mb_info() const { return mb_; }
+    // last frame's bitstream writer time split (host us): first partition, token partitions
+    double writer_first_us() const { return tok_stats_[stats_.idr ? 1 : 0].us_first; }
+    double writer_tokens_us() const { return tok_stats_[stats_.idr ? 1 : 0].us_tokens; }
 
    private:
     void analyse(const uint8_t* y, const uint8_t* uv, int pitch, bool key, int qindex);
@@ -252,6 +254,8 @@ class GpuVp8Encoder final : public VideoEncoder {
     const Vp8Mb* last_mb_info() const { return last_mb_; }
 
    private:
+    double wt_us_ = 0;  // host bitstream-writer time (MXDESK_HOST_TIMING report)
+    long long wt_n_ = 0;
     struct Slot {
         Vp8DeviceBuffers buf{};
         Vp8States* st_host = nullptr;  // pinned: copied to buf.st at the start of the frame

@@ -7,6 +7,9 @@
 // group of macroblock rows) on a small worker pool; with pipeline depth 2 that host work overlaps
 // the GPU analysis of the next frame.  Decisions and samples equal CpuVp8Encoder's (tests/test_gpu_vp8.py).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -92,6 +95,9 @@ GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
 }
 
 GpuVp8Encoder::~GpuVp8Encoder() {
+    if (wt_n_ > 0 && std::getenv("MXDESK_HOST_TIMING"))
+        std::fprintf(stderr, "[mxdesk] vp8 bitstream writer: %.1f us/frame over %lld frames\n", wt_us_ / wt_n_,
+                     (long long)wt_n_);
     (void)hipStreamSynchronize(stream_);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
@@ -242,7 +248,10 @@ const std::vector<uint8_t>& GpuVp8Encoder::collect() {
         throw;
     }
     au_.clear();
+    const auto t_w = std::chrono::steady_clock::now();
     write_slot(s, au_);
+    wt_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_w).count();
+    ++wt_n_;
     const int nmb = geom_.mb_w * geom_.mb_h;
     uint64_t sse[3] = {0, 0, 0};
     int skipped = 0;

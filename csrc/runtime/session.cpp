@@ -98,10 +98,18 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     else
         throw std::invalid_argument("Session: unknown codec '" + cfg_.codec + "' (h264 | hevc | vp8)");
     const h264::Geometry& g = enc_->geometry();
-    HIP_CHECK(hipMalloc(&nv12_y_, (size_t)g.pitch * g.coded_h));
-    HIP_CHECK(hipMalloc(&nv12_uv_, (size_t)g.pitch * g.coded_h / 2));
     depth_ = enc_->depth();
     if (depth_ > kMaxDepth) throw std::invalid_argument("Session: encoder pipeline depth above kMaxDepth");
+    for (int k = 0; k < depth_; ++k) {
+        HIP_CHECK(hipMalloc(&nv12_y_[k], (size_t)g.pitch * g.coded_h));
+        HIP_CHECK(hipMalloc(&nv12_uv_[k], (size_t)g.pitch * g.coded_h / 2));
+    }
+    const bool cap = cfg_.capture_stream > 0 || (cfg_.capture_stream < 0 && std::string(enc_->codec()) == "h264");
+    if (depth_ > 1 && cap && !cfg_.use_graph) {
+        HIP_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
+        for (int k = 0; k < depth_; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_conv_[k], hipEventDisableTiming));
+        enc_->set_hpel_side_stream(false);
+    }
     if (depth_ > 1 && cfg_.use_graph && !enc_->supports_split())
         throw std::invalid_argument("hipGraph replay with pipeline_depth 2 needs an encoder with the split form");
     if (depth_ >= cfg_.pool_slots) throw std::invalid_argument("pool_slots must exceed pipeline_depth");
@@ -182,8 +190,15 @@ Session::~Session() {
     hipFree(synth_dev_);
     enc_.reset();
     pool_.reset();
-    hipFree(nv12_y_);
-    hipFree(nv12_uv_);
+    if (cap_stream_) {
+        (void)hipStreamSynchronize(cap_stream_);
+        (void)hipStreamDestroy(cap_stream_);
+    }
+    for (int k = 0; k < kMaxDepth; ++k) {
+        if (nv12_y_[k]) (void)hipFree(nv12_y_[k]);
+        if (nv12_uv_[k]) (void)hipFree(nv12_uv_[k]);
+        if (ev_conv_[k]) (void)hipEventDestroy(ev_conv_[k]);
+    }
     for (int k = 0; k < kMaxDepth; ++k)
         if (staging_[k]) (void)hipHostFree(staging_[k]);
     if (lt_mem_) hipFree(lt_mem_);
@@ -203,23 +218,29 @@ Session::~Session() {
     hipStreamDestroy(stream_);
 }
 
-void Session::convert(int slot, uint64_t* ts) {
+void Session::convert(int slot, hipStream_t st, uint64_t* ts) {
     const h264::Geometry& g = enc_->geometry();
+    uint8_t* y = nv12_y_[cur_k_];
+    uint8_t* uv = nv12_uv_[cur_k_];
     if (scale_) {
-        pix::launch_scale_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, lt_, nv12_y_, nv12_uv_,
-                                  g.pitch, g.coded_w, g.coded_h, stream_, ts);
+        pix::launch_scale_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, lt_, y, uv, g.pitch,
+                                  g.coded_w, g.coded_h, st, ts);
     } else {
-        pix::launch_bgrx_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, nv12_y_, nv12_uv_,
-                                 g.pitch, g.coded_w, g.coded_h, stream_, ts);
+        pix::launch_bgrx_to_nv12(pool_->data(slot), pool_->pitch(), cfg_.width, cfg_.height, y, uv, g.pitch,
+                                 g.coded_w, g.coded_h, st, ts);
     }
     HIP_CHECK(hipGetLastError());
 }
 
 void Session::convert_and_encode(int slot, bool force_idr, bool stamp) {
     TraceRange tr("mxdesk.convert+encode.enqueue");
-    convert(slot, (stamp && devclk_) ? ts_ + slot : nullptr);
-    enc_->submit(nv12_y_, nv12_uv_, force_idr);
-    enqueue_mask_sse(inflight_.back().k);
+    convert(slot, stream_, (stamp && devclk_) ? ts_ + slot : nullptr);
+    encode_converted(force_idr);
+}
+
+void Session::encode_converted(bool force_idr) {
+    enc_->submit(nv12_y_[cur_k_], nv12_uv_[cur_k_], force_idr);
+    enqueue_mask_sse(cur_k_);
 }
 
 void Session::enqueue_mask_sse(int k) {
@@ -229,7 +250,7 @@ void Session::enqueue_mask_sse(int k) {
     const h264::EncoderConfig& e = enc_->rc().config();
     int r[4];
     mask_rect_mb(r);
-    pix::launch_sse_masked(nv12_y_, enc_->recon_y(), enc_->pitch(), e.width, e.height, r[0], r[1], r[2], r[3],
+    pix::launch_sse_masked(nv12_y_[k], enc_->recon_y(), enc_->pitch(), e.width, e.height, r[0], r[1], r[2], r[3],
                            mask_dev_ + (size_t)k * mask_stride_, mask_counter_ + k, mask_host_ + k,
                            stream_);  // mapped: the kernel stores the total to the host
     HIP_CHECK(hipEventRecord(ev_mask_[k], stream_));
@@ -252,6 +273,7 @@ int Session::begin_frame(int slot) {
     next_k_ = (next_k_ + 1) % depth_;
     inflight_.push_back(Inflight{frame_id_, now_us(), k, slot});
     t_capture_ = inflight_.back().t_capture;
+    cur_k_ = last_k_ = k;
     return k;
 }
 
@@ -308,19 +330,19 @@ void Session::capture_frame_graphs(int slot, bool idr, hipGraphExec_t* ga, hipGr
         HIP_CHECK(hipMemcpyAsync(dev, host, sizeof(pix::SynthParams), hipMemcpyHostToDevice, stream_));
         pix::launch_synth_dev(pool_->data(slot), dev, cfg_.width, cfg_.height, stream_, synth_bg_);
         HIP_CHECK(hipGetLastError());
-        convert(slot);
+        convert(slot, stream_);
     };
     if (depth_ == 1) {
         *ga = capture_on(stream_, [&]() {
             analysis();
-            enc_->enqueue_body(idr, nv12_y_, nv12_uv_);
+            enc_->enqueue_body(idr, nv12_y_[cur_k_], nv12_uv_[cur_k_]);
         });
         *ge = nullptr;
         return;
     }
     *ga = capture_on(stream_, [&]() {
         analysis();
-        enc_->enqueue_analysis(idr, nv12_y_, nv12_uv_);
+        enc_->enqueue_analysis(idr, nv12_y_[cur_k_], nv12_uv_[cur_k_]);
     });
     hipStream_t es = enc_->entropy_stream() ? enc_->entropy_stream() : stream_;
     *ge = capture_on(es, [&]() { enc_->enqueue_entropy(); });
@@ -341,15 +363,26 @@ void Session::submit_synthetic(bool force_idr) {
     ++frame_id_;
     // the first CBR frame runs eagerly: its rate-control probe encodes synchronously
     if (!cfg_.use_graph || enc_->rc().wants_probe()) {
-        if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
-        pix::launch_synth(pool_->data(slot), p, stream_, synth_bg_);
+        // capture stream: the render + conversion of this frame may run beside the previous
+        // frame's analysis; the analysis stream waits only for this frame's conversion
+        hipStream_t cs = cap_stream_ ? cap_stream_ : stream_;
+        if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], cs));
+        pix::launch_synth(pool_->data(slot), p, cs, synth_bg_);
         HIP_CHECK(hipGetLastError());
-        convert_and_encode(slot, force_idr, false);
+        TraceRange tr2("mxdesk.convert+encode.enqueue");
+        convert(slot, cs);
+        if (cap_stream_) {
+            HIP_CHECK(hipEventRecord(ev_conv_[k], cs));
+            HIP_CHECK(hipStreamWaitEvent(stream_, ev_conv_[k], 0));
+        }
+        encode_converted(force_idr);
         return;
     }
     synth_host_[slot] = p;  // read by this slot's graph memcpy node (its previous frame was collected)
     const bool idr = enc_->prepare(force_idr);
     const int es = depth_ > 1 ? enc_->prep_slot() : 0;
+    if (es != (depth_ > 1 ? k : 0))  // the graph bakes in the NV12 buffer of k
+        throw std::logic_error("Session: encoder slot out of step with the session's frame index");
     if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
     enc_->record_start();
     const size_t key = (((size_t)slot * kMaxDepth + (size_t)es) * 2 + (idr ? 1 : 0)) * 2;
@@ -401,8 +434,15 @@ void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_i
         HIP_CHECK(hipMemcpy2DAsync(pool_->data(slot), pool_->pitch(), host_bgrx, host_pitch, row, cfg_.height,
                                    hipMemcpyHostToDevice, upload_stream_));
         HIP_CHECK(hipEventRecord(ev_upload_, upload_stream_));
-        HIP_CHECK(hipStreamWaitEvent(stream_, ev_upload_, 0));
-        convert_and_encode(slot, force_idr, true);  // GPU time from the conversion (DMA excluded)
+        if (cap_stream_) {  // the conversion follows the DMA on its stream (overlaps earlier frames' analysis)
+            convert(slot, upload_stream_, devclk_ ? ts_ + slot : nullptr);
+            HIP_CHECK(hipEventRecord(ev_conv_[k], upload_stream_));
+            HIP_CHECK(hipStreamWaitEvent(stream_, ev_conv_[k], 0));
+            encode_converted(force_idr);
+        } else {
+            HIP_CHECK(hipStreamWaitEvent(stream_, ev_upload_, 0));
+            convert_and_encode(slot, force_idr, true);  // GPU time from the conversion (DMA excluded)
+        }
         HIP_CHECK(hipEventSynchronize(ev_upload_));  // the caller may overwrite the buffer now
         return;
     }
