@@ -229,7 +229,7 @@ def main() -> None:
     args = ap.parse_args()
     if args.codec == "vp8":
         args.subpel = 0  # VP8 vectors here are full-sample (the reported ME setting says so)
-        args.depth = min(args.depth, 2)  # the VP8 encoder keeps at most two frames in flight
+        args.depth = min(args.depth, 3)  # the VP8 encoder keeps at most three frames in flight
     content = 1 if args.content == "motion" else 0
     if content:
         args.noise = 0  # the motion content has a video panel instead of the noise panel

@@ -297,7 +297,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
 GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     : cfg_(cfg), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
-        throw std::invalid_argument("pipeline_depth must be 1, 2 or 3");
+        throw std::invalid_argument("pipeline_depth must be 1 to 4");
     depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;
     geom_.height = cfg.height;

@@ -189,7 +189,7 @@ class GpuH264Encoder final : public VideoEncoder {
    public:
     const char* codec() const override { return "h264"; }
     EncoderCommon& rc() override { return common_; }
-    static constexpr int kMaxInFlight = 3;
+    static constexpr int kMaxInFlight = 4;
     GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream);
     ~GpuH264Encoder();
     GpuH264Encoder(const GpuH264Encoder&) = delete;

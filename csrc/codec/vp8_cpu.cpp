@@ -202,7 +202,8 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     if (cfg_.aq >= 3) prev_src_.swap(next_src_);
     au_.clear();
     write_frame(fd, mb_.data(), [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, au_,
-                run_serial, &tok_stats_[key ? 1 : 0]);
+                run_serial, &tok_stats_[key ? 1 : 0][frames_ % kStatsLag]);
+    ++frames_;
     int skipped = 0;
     for (const Vp8Mb& m : mb_) skipped += m.nz == 0;
     stats_.frame_index = common_.frames();

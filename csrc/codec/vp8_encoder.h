@@ -10,6 +10,8 @@
 #include <array>
 #include <condition_variable>
 #include <deque>
+#include <exception>
+#include <memory>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -94,6 +96,10 @@ inline void segment_qindices(int qp, int aq, int out[kNumSegs]) {
 // Token branch statistics of the last coded frame of one type (13.4): the coefficient probability
 // updates of the next frame of that type are planned from them, so coding needs no separate
 // counting pass over the tokens.
+// Frames whose bitstreams may be written at once (GPU encoder pipeline depth); also the distance
+// from the frame whose branch statistics plan a frame's probability updates.
+constexpr int kStatsLag = 3;
+
 struct TokenStats {
     std::vector<std::array<uint32_t, 2>> n;  // [1056] (zeros, ones) per probability
     bool valid = false;
@@ -162,8 +168,8 @@ class CpuVp8Encoder {
     int coded_pitch() const { return cw_; }
     const std::vector<Vp8Mb>& mb_info() const { return mb_; }
     // last frame's bitstream writer time split (host us): first partition, token partitions
-    double writer_first_us() const { return tok_stats_[stats_.idr ? 1 : 0].us_first; }
-    double writer_tokens_us() const { return tok_stats_[stats_.idr ? 1 : 0].us_tokens; }
+    double writer_first_us() const { return tok_stats_[stats_.idr ? 1 : 0][(frames_ - 1) % kStatsLag].us_first; }
+    double writer_tokens_us() const { return tok_stats_[stats_.idr ? 1 : 0][(frames_ - 1) % kStatsLag].us_tokens; }
 
    private:
     void analyse(const uint8_t* y, const uint8_t* uv, int pitch, bool key, int qindex);
@@ -172,7 +178,11 @@ class CpuVp8Encoder {
     int cw_, ch_, mb_w_, mb_h_;
     std::vector<uint8_t> rec_y_[2], rec_uv_[2];
     std::vector<uint8_t> prev_src_, next_src_;  // aq >= 3: previous / this frame's source luma (temporal classes)
-    TokenStats tok_stats_[2];                     // [key]: branch statistics for the probability updates
+    // [key][frame % kStatsLag]: branch statistics for the probability updates -- frame n plans
+    // from the statistics frame n - kStatsLag left (the GPU encoder writes up to kStatsLag frames
+    // concurrently)
+    TokenStats tok_stats_[2][kStatsLag];
+    long long frames_ = 0;
     int seg_qindex_[kNumSegs] = {0, 0, 0, 0};
     int cur_ = 0;
     bool have_ref_ = false;
@@ -229,7 +239,7 @@ void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipSt
 class GpuVp8Encoder final : public VideoEncoder {
    public:
     const char* codec() const override { return "vp8"; }
-    static constexpr int kMaxInFlight = 2;
+    static constexpr int kMaxInFlight = kStatsLag;
     GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream);
     ~GpuVp8Encoder();
     GpuVp8Encoder(const GpuVp8Encoder&) = delete;
@@ -254,8 +264,9 @@ class GpuVp8Encoder final : public VideoEncoder {
     const Vp8Mb* last_mb_info() const { return last_mb_; }
 
    private:
-    double wt_us_ = 0;  // host bitstream-writer time (MXDESK_HOST_TIMING report)
-    long long wt_n_ = 0;
+    // Each frame slot has a writer thread (and its own partition pool): it waits for the slot's
+    // GPU work and writes the frame's bitstream at once, so with two frames in flight both frames'
+    // bitstreams are written concurrently; collect() only waits for the writer of the oldest.
     struct Slot {
         Vp8DeviceBuffers buf{};
         Vp8States* st_host = nullptr;  // pinned: copied to buf.st at the start of the frame
@@ -264,7 +275,20 @@ class GpuVp8Encoder final : public VideoEncoder {
         int qp = 0, qindex = 0;
         bool segmented = false;
         int seg_qindex[kNumSegs] = {0, 0, 0, 0};
+        long long fidx = 0;  // frame index (statistics parity)
+        // writer (job / ready under wmu_)
+        std::thread writer;
+        std::unique_ptr<PartitionPool> pool;
+        bool job = false, ready = false, timeout = false;
+        std::exception_ptr err;
+        std::vector<uint8_t> au;
+        uint64_t sse[3] = {0, 0, 0};
+        int skipped = 0;
+        float ms = 0;
+        double wt_us = 0;  // writer time (MXDESK_HOST_TIMING report)
+        long long wt_n = 0;
     };
+    void writer_loop(Slot& s);
     void alloc_slot(Slot& s);
     void free_slot(Slot& s);
     void fill_state(Slot& s, bool key, int qp, int ref, int cur);
@@ -287,12 +311,16 @@ class GpuVp8Encoder final : public VideoEncoder {
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     uint8_t* src_keep_[2] = {nullptr, nullptr};  // aq >= 3: source luma of the frames in rec_y_[k]
-    TokenStats tok_stats_[2];                     // [key]: branch statistics for the probability updates
+    TokenStats tok_stats_[2][kStatsLag];          // [key][frame % kStatsLag], as CpuVp8Encoder
+    long long frames_ = 0;
     int cur_ = 0;
     bool have_ref_ = false;
     uint32_t epoch_ = 0;
     int log2_parts_ = 0;
-    PartitionPool pool_;
+    int device_ = 0;
+    std::mutex wmu_;
+    std::condition_variable wcv_;
+    bool wstop_ = false;
     std::vector<uint8_t> au_;
     h264::FrameStats stats_;
 };

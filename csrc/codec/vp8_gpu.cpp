@@ -8,6 +8,8 @@
 // the GPU analysis of the next frame.  Decisions and samples equal CpuVp8Encoder's (tests/test_gpu_vp8.py).
 #include <algorithm>
 #include <chrono>
+#include <memory>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,9 +65,9 @@ void GpuVp8Encoder::free_slot(Slot& s) {
 }
 
 GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
-    : cfg_(cfg), common_(cfg), stream_(stream), pool_(pool_threads()) {
+    : cfg_(cfg), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
-        throw std::invalid_argument("pipeline_depth must be 1 or 2");
+        throw std::invalid_argument("pipeline_depth must be 1 to 3");
     if (cfg.width > 16383 || cfg.height > 16383) throw std::invalid_argument("vp8: picture larger than 16383");
     depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;
@@ -92,12 +94,69 @@ GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
     HIP_CHECK(hipMalloc(&hp_, (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad)));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     HIP_CHECK(hipStreamSynchronize(stream_));
+    HIP_CHECK(hipGetDevice(&device_));
+    for (int i = 0; i < depth_; ++i) {
+        slots_[i].pool = std::make_unique<PartitionPool>(pool_threads());
+        slots_[i].writer = std::thread([this, i]() { writer_loop(slots_[i]); });
+    }
+}
+
+void GpuVp8Encoder::writer_loop(Slot& s) {
+    (void)hipSetDevice(device_);
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(wmu_);
+            wcv_.wait(lk, [&] { return wstop_ || s.job; });
+            if (!s.job) return;  // stopping with no frame pending
+            s.job = false;
+        }
+        try {
+            HIP_CHECK(hipEventSynchronize(s.done));
+            if (*s.buf.err) {  // a key-frame hand-off spin timed out: collect() reports it
+                s.timeout = true;
+            } else {
+                const auto t0 = std::chrono::steady_clock::now();
+                s.au.clear();
+                write_slot(s, s.au);
+                s.wt_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+                ++s.wt_n;
+                const int nmb = geom_.mb_w * geom_.mb_h;
+                s.sse[0] = s.sse[1] = s.sse[2] = 0;
+                s.skipped = 0;
+                for (int i = 0; i < nmb; ++i) {
+                    const Vp8Mb& m = s.buf.mb_host[i];
+                    for (int c = 0; c < 3; ++c) s.sse[c] += m.sse[c];
+                    s.skipped += m.nz == 0;
+                }
+                s.ms = 0;
+                (void)hipEventElapsedTime(&s.ms, s.start, s.done);
+            }
+        } catch (...) {
+            s.err = std::current_exception();
+        }
+        {
+            std::lock_guard<std::mutex> lk(wmu_);
+            s.ready = true;
+        }
+        wcv_.notify_all();
+    }
 }
 
 GpuVp8Encoder::~GpuVp8Encoder() {
-    if (wt_n_ > 0 && std::getenv("MXDESK_HOST_TIMING"))
-        std::fprintf(stderr, "[mxdesk] vp8 bitstream writer: %.1f us/frame over %lld frames\n", wt_us_ / wt_n_,
-                     (long long)wt_n_);
+    {
+        std::lock_guard<std::mutex> lk(wmu_);
+        wstop_ = true;
+    }
+    wcv_.notify_all();
+    double wt_us = 0;
+    long long wt_n = 0;
+    for (int i = 0; i < depth_; ++i) {
+        if (slots_[i].writer.joinable()) slots_[i].writer.join();
+        wt_us += slots_[i].wt_us;
+        wt_n += slots_[i].wt_n;
+    }
+    if (wt_n > 0 && std::getenv("MXDESK_HOST_TIMING"))
+        std::fprintf(stderr, "[mxdesk] vp8 bitstream writer: %.1f us/frame over %lld frames\n", wt_us / wt_n, wt_n);
     (void)hipStreamSynchronize(stream_);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
@@ -177,8 +236,8 @@ void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out, bool pr
     fd.segmented = s.segmented;
     for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = s.seg_qindex[k];
     write_frame(fd, mbs, [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
-                [&](int n, const std::function<void(int)>& fn) { pool_.run(n, fn); },
-                probe ? nullptr : &tok_stats_[s.key ? 1 : 0]);
+                [&](int n, const std::function<void(int)>& fn) { s.pool->run(n, fn); },
+                probe ? nullptr : &tok_stats_[s.key ? 1 : 0][s.fidx % kStatsLag]);
 }
 
 int GpuVp8Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp) {
@@ -207,6 +266,7 @@ bool GpuVp8Encoder::prepare(bool force_idr) {
     have_ref_ = true;
     s.key = common_.cur_idr();
     s.qp = common_.cur_qp();
+    s.fidx = frames_++;
     const int ref = cur_;
     cur_ ^= 1;
     fill_state(s, s.key, s.qp, ref, cur_);
@@ -216,8 +276,15 @@ bool GpuVp8Encoder::prepare(bool force_idr) {
 void GpuVp8Encoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
 
 void GpuVp8Encoder::record_done() {
-    HIP_CHECK(hipEventRecord(slots_[prep_slot_].done, stream_));
+    Slot& s = slots_[prep_slot_];
+    HIP_CHECK(hipEventRecord(s.done, stream_));
     inflight_.push_back(prep_slot_);
+    {
+        std::lock_guard<std::mutex> lk(wmu_);
+        s.job = true;
+        s.ready = false;
+    }
+    wcv_.notify_all();
 }
 
 void GpuVp8Encoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool force_idr) {
@@ -236,38 +303,31 @@ const std::vector<uint8_t>& GpuVp8Encoder::collect() {
     const int n = inflight_.front();
     inflight_.pop_front();
     Slot& s = slots_[n];
-    HIP_CHECK(hipEventSynchronize(s.done));
+    {
+        std::unique_lock<std::mutex> lk(wmu_);
+        wcv_.wait(lk, [&] { return s.ready; });
+        s.ready = false;
+    }
     last_done_ = s.done;
     last_mb_ = s.buf.mb_host;
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, s.start, s.done);
-    try {
-        check_slot(s);
-    } catch (...) {
+    if (s.timeout || s.err) {
+        std::exception_ptr e = s.err;
+        s.err = nullptr;
+        const bool timeout = s.timeout;
+        s.timeout = false;
         common_.end_frame(0, s.key);
-        throw;
+        if (timeout) check_slot(s);  // clears the error word, drops the reference, throws
+        std::rethrow_exception(e);
     }
-    au_.clear();
-    const auto t_w = std::chrono::steady_clock::now();
-    write_slot(s, au_);
-    wt_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_w).count();
-    ++wt_n_;
-    const int nmb = geom_.mb_w * geom_.mb_h;
-    uint64_t sse[3] = {0, 0, 0};
-    int skipped = 0;
-    for (int i = 0; i < nmb; ++i) {
-        const Vp8Mb& m = s.buf.mb_host[i];
-        for (int c = 0; c < 3; ++c) sse[c] += m.sse[c];
-        skipped += m.nz == 0;
-    }
+    au_.swap(s.au);
     stats_.frame_index = common_.frames();
     stats_.idr = s.key;
     stats_.qp = s.qp;
     stats_.bytes = (int)au_.size();
-    stats_.encode_ms = ms;
-    stats_.skipped_mbs = skipped;
-    for (int c = 0; c < 3; ++c) stats_.sse[c] = sse[c];
-    stats_.sse_masked = sse[0];
+    stats_.encode_ms = s.ms;
+    stats_.skipped_mbs = s.skipped;
+    for (int c = 0; c < 3; ++c) stats_.sse[c] = s.sse[c];
+    stats_.sse_masked = s.sse[0];
     stats_.masked_pixels = (int64_t)cfg_.width * cfg_.height;
     common_.end_frame((int)au_.size(), s.key);
     return au_;

@@ -56,7 +56,7 @@ struct SessionConfig {
     int fps = 60;
     int noise = 1;          // synthetic animated-noise panel
     int content = 0;        // synthetic source: 0 desktop, 1 motion content (pan + video panel, pix::SynthParams)
-    int pool_slots = 4;     // > encoder pipeline depth (<= kMaxDepth)
+    int pool_slots = 5;     // > encoder pipeline depth (<= kMaxDepth)
     int use_graph = 0;      // replay the per-frame chain as a hipGraph (measured slower than eager
                             // launches on ROCm 7.2 for this chain: profiles/r01_graph)
     int fake_clock = 0;     // barcode timestamp = frame_id * 1e6 / fps (deterministic streams for tests)
@@ -162,7 +162,7 @@ class Session {
     hipStream_t stream_ = nullptr;
     std::unique_ptr<FramePool> pool_;
     std::unique_ptr<VideoEncoder> enc_;
-    static constexpr int kMaxDepth = 3;  // frames in flight per session (encoder pipeline depth)
+    static constexpr int kMaxDepth = 4;  // frames in flight per session (encoder pipeline depth)
     // NV12 encoder input per frame in flight: the buffer of frame n is rewritten by frame
     // n + depth, whose submit follows collect(n) (analysis, entropy and masked SSE complete)
     uint8_t* nv12_y_[kMaxDepth] = {};

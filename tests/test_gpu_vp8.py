@@ -100,18 +100,21 @@ def test_gpu_vp8_1080p_desktop(gpu):
     assert not st.idr and st.skipped_mbs > 0
 
 
-def test_gpu_vp8_pipelined_depth2_matches(gpu):
-    """Depth 2 (host partition coding of frame n overlapping the GPU analysis of frame n+1)
-    produces the depth-1 bitstream (fixed QP: with rate control the pipelined QP lags a frame)."""
+@pytest.mark.parametrize("depth", [2, 3])
+def test_gpu_vp8_pipelined_matches(gpu, depth):
+    """Depth 2 / 3 (the bitstreams of the frames in flight written concurrently by per-slot
+    writer threads, beside the GPU analysis of the next frame) produce the depth-1 bitstream
+    (fixed QP: with rate control the pipelined QP lags)."""
     w, h = 320, 192
     a, _ = _pair(gpu, w, h, qp=30)
-    b, _ = _pair(gpu, w, h, qp=30, depth=2)
-    srcs = [_dev(a, *synthetic_nv12(w, h, t, seed=1)) for t in range(6)]
+    b, _ = _pair(gpu, w, h, qp=30, depth=depth)
+    srcs = [_dev(a, *synthetic_nv12(w, h, t, seed=1)) for t in range(8)]
     ref = [a.encode(dy.data_ptr(), duv.data_ptr(), False) for dy, duv in srcs]
     out = []
-    b.submit(srcs[0][0].data_ptr(), srcs[0][1].data_ptr(), False)
-    for t in range(1, 6):
+    for t in range(len(srcs)):
+        if t >= depth:
+            out.append(b.collect())
         b.submit(srcs[t][0].data_ptr(), srcs[t][1].data_ptr(), False)
+    while len(out) < len(srcs):
         out.append(b.collect())
-    out.append(b.collect())
     assert out == ref

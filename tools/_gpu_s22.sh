@@ -1,0 +1,13 @@
+set -o pipefail
+o=gpurun_out/s22; mkdir -p $o
+timeout -k 10 300 python -u -m pytest tests/test_gpu_vp8.py -x -q --timeout 120 --timeout-method thread > $o/vp8tests.log 2>&1 || exit 1
+for c in desktop motion; do
+  MXDESK_HOST_TIMING=1 timeout -k 10 200 python bench.py --codec vp8 --steps 100 --warmup 10 --density-probe 0 --content $c > $o/vp8_$c.json 2> $o/vp8_$c.err || exit 1
+done
+MXDESK_HOST_TIMING=1 timeout -k 10 200 python bench.py --codec vp8 --steps 20 --warmup 5 --quality-probe 0 --density-probe 0 > $o/vp8_20.json 2> $o/vp8_20.err || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pipeline.py -x -q --timeout 120 --timeout-method thread > $o/pipeline.log 2>&1 || exit 1
+for d in 3 4; do
+  for st in 20 300; do
+    MXDESK_HOST_TIMING=1 timeout -k 10 200 python bench.py --steps $st --warmup 5 --quality-probe 0 --density-probe 0 --depth $d > $o/h264_d${d}_$st.json 2> $o/h264_d${d}_$st.err || exit 1
+  done
+done
