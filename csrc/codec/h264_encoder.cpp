@@ -237,6 +237,10 @@ std::vector<std::vector<uint8_t>> hpel_planes_for_test(const uint8_t* ref, int c
 }
 
 // ------------------------------------------------------------------ GpuH264Encoder
+// Events that only order GPU work between this device's queues: a device-scope release when
+// recorded (the default system-scope release writes the caches back for the host each time).
+constexpr unsigned kDeviceEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+
 void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     const int nmb = geom_.mb_w * geom_.mb_h;
     DeviceBuffers& b = sl.buf;
@@ -274,9 +278,9 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipHostMalloc(&sl.host_out, kOutPayloadOffset + b.out_bytes + 16, hipHostMallocMapped));
     std::memset(sl.host_out, 0, kOutPayloadOffset);
     HIP_CHECK(hipEventCreateWithFlags(&sl.start, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&sl.deblock_done, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&sl.hpel_done, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, kDeviceEvent));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.deblock_done, kDeviceEvent));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.hpel_done, kDeviceEvent));
     HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
 }
 
@@ -339,13 +343,70 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     if (depth_ > 1) {
         HIP_CHECK(hipStreamCreateWithFlags(&stream_e_, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&stream_a_, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&ref_ready_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ref_ready_, kDeviceEvent));
         HIP_CHECK(hipEventRecord(ref_ready_, stream_));
     }
     HIP_CHECK(hipStreamSynchronize(stream_));
+    const char* et = std::getenv("MXDESK_ENTROPY_THREAD");
+    if (stream_e_ && !(et && et[0] == '0')) {
+        HIP_CHECK(hipGetDevice(&device_));
+        launcher_ = std::thread([this]() { launcher_loop(); });
+    }
+}
+
+void GpuH264Encoder::launcher_loop() {
+    (void)hipSetDevice(device_);
+    for (;;) {
+        EntropyJob j;
+        {
+            std::unique_lock<std::mutex> lk(lmu_);
+            lcv_.wait(lk, [&] { return lstop_ || !ljobs_.empty(); });
+            if (ljobs_.empty()) return;  // stopping, nothing pending
+            j = ljobs_.front();
+            ljobs_.pop_front();
+        }
+        try {
+            FrameSlot& sl = slots_[j.slot];
+            HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
+            launch_entropy(geom_, sl.buf, sl.host_out, stream_e_, j.sse_ready);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipEventRecord(sl.done, stream_e_));
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(lmu_);
+            lerr_ = std::current_exception();
+        }
+        {
+            std::lock_guard<std::mutex> lk(lmu_);
+            ++l_done_;
+        }
+        lcv_.notify_all();
+    }
+}
+
+void GpuH264Encoder::drain_launcher() const {
+    // graph capture / replay issues entropy-stream work from this thread: the launcher's queued
+    // eager frames go first (and none of its operations may land inside a capture)
+    if (!launcher_.joinable()) return;
+    std::unique_lock<std::mutex> lk(lmu_);
+    lcv_.wait(lk, [&] { return l_done_ >= l_pushed_ || lerr_; });
+    if (lerr_) std::rethrow_exception(lerr_);
+}
+
+void GpuH264Encoder::wait_launched(int slot) const {
+    std::unique_lock<std::mutex> lk(lmu_);
+    lcv_.wait(lk, [&] { return l_done_ >= slot_job_[slot] || lerr_; });
+    if (lerr_) std::rethrow_exception(lerr_);
 }
 
 GpuH264Encoder::~GpuH264Encoder() {
+    if (launcher_.joinable()) {  // issues what is queued, then exits
+        {
+            std::lock_guard<std::mutex> lk(lmu_);
+            lstop_ = true;
+        }
+        lcv_.notify_all();
+        launcher_.join();
+    }
     (void)hipStreamSynchronize(stream_);
     if (stream_e_) {
         (void)hipStreamSynchronize(stream_e_);
@@ -368,7 +429,13 @@ GpuH264Encoder::~GpuH264Encoder() {
 void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
     FrameSlot& sl = slots_[prep_slot_];
     const FrameState* pub = publish ? sl.fs_host : nullptr;
+    auto wait_input = [&]() {
+        if (!in_ev_) return;
+        HIP_CHECK(hipStreamWaitEvent(stream_, in_ev_, 0));
+        in_ev_ = nullptr;
+    };
     if (idr) {
+        wait_input();
         launch_intra(geom_, sl.buf, src_y, src_uv, stream_, pub);
         if (cfg_.aq >= 3)  // the next P picture's previous source (P pictures: k_inter_encode stores it)
             launch_save_src(geom_, sl.buf, src_y, stream_);
@@ -381,6 +448,7 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
         } else {
             launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
         }
+        wait_input();
         launch_me(geom_, sl.buf, src_y, stream_);
         launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
         if (cfg_.intra_in_p) launch_intra_in_p(geom_, sl.buf, src_y, src_uv, stream_);
@@ -388,13 +456,15 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
 }
 
 void GpuH264Encoder::link_entropy() {
-    if (!stream_e_) return;  // entropy of this frame overlaps the analysis of the next one
+    if (!stream_e_) return;
+    drain_launcher();  // entropy of this frame overlaps the analysis of the next one
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
     HIP_CHECK(hipStreamWaitEvent(stream_e_, sl.analysis_done, 0));
 }
 
 void GpuH264Encoder::enqueue_entropy() {
+    drain_launcher();
     FrameSlot& sl = slots_[prep_slot_];
     launch_entropy(geom_, sl.buf, sl.host_out, stream_e_ ? stream_e_ : stream_, nullptr);
 }
@@ -402,6 +472,29 @@ void GpuH264Encoder::enqueue_entropy() {
 void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
     FrameSlot& sl = slots_[prep_slot_];
     enqueue_analysis_kernels(idr, src_y, src_uv, publish);
+    async_frame_ = launcher_.joinable() && publish && !sync_launch_;
+    if (async_frame_) {  // entropy chain to the launcher thread (its stream operations only there)
+        HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
+        hipEvent_t sse_ready = nullptr;
+        if (cfg_.h264_deblock()) {
+            launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
+            HIP_CHECK(hipEventRecord(sl.deblock_done, stream_));
+            sse_ready = sl.deblock_done;
+        }
+        if (stream_a_ && hpel_side_ && publish) {
+            HIP_CHECK(hipEventRecord(ref_ready_, stream_));
+            ref_seq_ = seq_;
+        }
+        HIP_CHECK(hipGetLastError());
+        {
+            std::lock_guard<std::mutex> lk(lmu_);
+            if (lerr_) std::rethrow_exception(lerr_);
+            ljobs_.push_back(EntropyJob{prep_slot_, sse_ready});
+            slot_job_[prep_slot_] = ++l_pushed_;
+        }
+        lcv_.notify_all();
+        return;
+    }
     link_entropy();
     hipStream_t es = stream_e_ ? stream_e_ : stream_;
     hipEvent_t sse_ready = nullptr;
@@ -470,7 +563,9 @@ int GpuH264Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     fill_state(sl, true, qp, cur_ ^ 1, cur_);
     sl.fs_host->frame_num = 0;
     sl.fs_host->idr_pic_id = 0;
+    sync_launch_ = true;
     enqueue_kernels(true, src_y, src_uv, true);
+    sync_launch_ = false;
     HIP_CHECK(hipStreamSynchronize(stream_));
     if (stream_e_) HIP_CHECK(hipStreamSynchronize(stream_e_));
     const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);
@@ -500,12 +595,14 @@ bool GpuH264Encoder::prepare(bool force_idr) {
 void GpuH264Encoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
     // hipGraph form: frame-state upload node + kernels that read the device copy (depends
     // only on fixed buffers, so with depth 1 the same graph replays every frame of a type)
+    drain_launcher();
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
     enqueue_kernels(idr, src_y, src_uv, false);
 }
 
 void GpuH264Encoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    drain_launcher();
     FrameSlot& sl = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(FrameState), hipMemcpyHostToDevice, stream_));
     enqueue_analysis_kernels(idr, src_y, src_uv, false);
@@ -517,7 +614,12 @@ void GpuH264Encoder::record_start() {}
 
 void GpuH264Encoder::record_done() {
     FrameSlot& sl = slots_[prep_slot_];
-    HIP_CHECK(hipEventRecord(sl.done, stream_e_ ? stream_e_ : stream_));
+    if (async_frame_) {
+        async_frame_ = false;  // the launcher records sl.done after the entropy kernels
+    } else {
+        slot_job_[prep_slot_] = 0;
+        HIP_CHECK(hipEventRecord(sl.done, stream_e_ ? stream_e_ : stream_));
+    }
     inflight_.push_back(prep_slot_);
 }
 
@@ -537,6 +639,7 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     const int s = inflight_.front();
     inflight_.pop_front();
     FrameSlot& sl = slots_[s];
+    wait_launched(s);
     wait_event(sl.done);
     last_done_ = sl.done;
     const OutHeader hdr = *reinterpret_cast<const OutHeader*>(sl.host_out);

@@ -10,9 +10,13 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <deque>
+#include <exception>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "h264_core.h"
@@ -231,11 +235,22 @@ class GpuH264Encoder final : public VideoEncoder {
     void enqueue_entropy() override;
     void link_entropy() override;
     void set_hpel_side_stream(bool on) override { hpel_side_ = on; }
+    void quiesce() override { drain_launcher(); }
+    // P pictures: the wait goes after k_hpel (which reads only the reference), so the
+    // interpolation of the new reference runs without waiting for the capture hand-off
+    bool set_input_event(hipEvent_t ev) override {
+        in_ev_ = ev;
+        return true;
+    }
     // Completion event of the last collected frame.
     hipEvent_t done_event() const override { return last_done_; }
     bool device_clock() const override { return true; }
     uint64_t last_t_end() const override { return last_t_end_; }
-    hipEvent_t pending_done_event() const override { return inflight_.empty() ? last_done_ : slots_[inflight_.front()].done; }
+    hipEvent_t pending_done_event() const override {
+        if (inflight_.empty()) return last_done_;
+        wait_launched(inflight_.front());  // the launcher thread has recorded it
+        return slots_[inflight_.front()].done;
+    }
     // publish: the first kernel takes the frame state by value and stores it (eager launches);
     // otherwise the kernels read the device copy uploaded by enqueue_body's memcpy node.
     void enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish);
@@ -255,6 +270,29 @@ class GpuH264Encoder final : public VideoEncoder {
     void free_slot(FrameSlot& sl);
     void fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur);
     int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
+    // Entropy launcher (depth > 1, eager launches): a thread issues each frame's entropy chain --
+    // the wait for its analysis, the CAVLC / scan / pack launches and its completion event, all
+    // on the entropy stream -- while the calling thread returns to the next frame's capture and
+    // analysis launches (the host launch sequence bounds the single-session rate,
+    // profiles/r04_capture).  MXDESK_ENTROPY_THREAD=0 keeps every launch on the calling thread.
+    struct EntropyJob {
+        int slot;
+        hipEvent_t sse_ready;
+    };
+    void launcher_loop();
+    void wait_launched(int slot) const;  // the job that records slots_[slot].done was issued
+    void drain_launcher() const;         // every queued job issued
+    std::thread launcher_;
+    mutable std::mutex lmu_;
+    mutable std::condition_variable lcv_;
+    std::deque<EntropyJob> ljobs_;
+    uint64_t l_pushed_ = 0, l_done_ = 0;
+    uint64_t slot_job_[kMaxInFlight] = {};  // job number that records the slot's done event (0: none)
+    bool lstop_ = false;
+    std::exception_ptr lerr_;
+    bool sync_launch_ = false;  // probe: everything on the calling thread
+    bool async_frame_ = false;  // the frame being submitted went to the launcher
+    int device_ = 0;
 
     EncoderConfig cfg_;
     EncoderCommon common_;
@@ -266,6 +304,7 @@ class GpuH264Encoder final : public VideoEncoder {
     // depend on; k_me_full waits for it (profiles/r04_h264)
     hipStream_t stream_a_ = nullptr;
     bool hpel_side_ = true;  // set_hpel_side_stream
+    hipEvent_t in_ev_ = nullptr;  // set_input_event, consumed by the next analysis launch
     hipEvent_t ref_ready_ = nullptr;
     uint64_t seq_ = 0, ref_seq_ = ~0ull;  // pictures prepared; the one whose reconstruction ref_ready_ marks
     int depth_ = 1;

@@ -56,6 +56,13 @@ class VideoEncoder {
     // session converts the next frame on a capture stream, so nothing on the analysis stream
     // would overlap a side-stream interpolation -- it would only add two cross-queue hand-offs)
     virtual void set_hpel_side_stream(bool on) { (void)on; }
+    // every launch this encoder queued on a helper thread has been issued (before the caller
+    // captures or replays graphs on the encoder's streams)
+    virtual void quiesce() {}
+    // The next submit's source is ready when `ev` completes: the encoder waits for it on its
+    // analysis stream right before the first kernel that reads the source.  Returns false if
+    // the encoder does not take the event (the caller then waits before submitting).
+    virtual bool set_input_event(hipEvent_t ev) { (void)ev; return false; }
 };
 
 }  // namespace mx

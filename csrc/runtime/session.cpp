@@ -107,7 +107,8 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     const bool cap = cfg_.capture_stream > 0 || (cfg_.capture_stream < 0 && std::string(enc_->codec()) == "h264");
     if (depth_ > 1 && cap && !cfg_.use_graph) {
         HIP_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
-        for (int k = 0; k < depth_; ++k) HIP_CHECK(hipEventCreateWithFlags(&ev_conv_[k], hipEventDisableTiming));
+        for (int k = 0; k < depth_; ++k)  // GPU-to-GPU only: device-scope release
+            HIP_CHECK(hipEventCreateWithFlags(&ev_conv_[k], hipEventDisableTiming | hipEventReleaseToDevice));
         enc_->set_hpel_side_stream(false);
     }
     if (depth_ > 1 && cfg_.use_graph && !enc_->supports_split())
@@ -373,11 +374,13 @@ void Session::submit_synthetic(bool force_idr) {
         convert(slot, cs);
         if (cap_stream_) {
             HIP_CHECK(hipEventRecord(ev_conv_[k], cs));
-            HIP_CHECK(hipStreamWaitEvent(stream_, ev_conv_[k], 0));
+            // the encoder waits right before its first source read (or here, if it cannot)
+            if (!enc_->set_input_event(ev_conv_[k])) HIP_CHECK(hipStreamWaitEvent(stream_, ev_conv_[k], 0));
         }
         encode_converted(force_idr);
         return;
     }
+    enc_->quiesce();        // no helper-thread launch may land inside a capture or after a replay
     synth_host_[slot] = p;  // read by this slot's graph memcpy node (its previous frame was collected)
     const bool idr = enc_->prepare(force_idr);
     const int es = depth_ > 1 ? enc_->prep_slot() : 0;
