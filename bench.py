@@ -204,10 +204,11 @@ def main() -> None:
                     help="in-loop deblocking filter 0/1 (default: the encoder's)")
     ap.add_argument("--intra-in-p", type=int, default=None,
                     help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
-    ap.add_argument("--depth", type=int, default=3,
+    ap.add_argument("--depth", type=int, default=None,
                     help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1; "
                          "3: also the next frame's launches stay queued while the host collects, so the host "
-                         "turnaround overlaps GPU work; 1: strictly one frame at a time, lowest back-to-back latency)")
+                         "turnaround overlaps GPU work; 1: strictly one frame at a time, lowest back-to-back latency; "
+                         "default 3, VP8 4: its host bitstream writers run one per frame in flight)")
     ap.add_argument("--capture-stream", type=int, default=-1,
                     help="depth > 1: render + convert on a capture stream, one NV12 buffer per frame in flight "
                          "(frame n+1's capture overlaps frame n's analysis); -1 = H.264 only (measured gain), "
@@ -229,7 +230,9 @@ def main() -> None:
     args = ap.parse_args()
     if args.codec == "vp8":
         args.subpel = 0  # VP8 vectors here are full-sample (the reported ME setting says so)
-        args.depth = min(args.depth, 3)  # the VP8 encoder keeps at most three frames in flight
+        args.depth = min(args.depth or 4, 4)  # the VP8 encoder keeps at most four frames in flight
+    if args.depth is None:
+        args.depth = 3
     content = 1 if args.content == "motion" else 0
     if content:
         args.noise = 0  # the motion content has a video panel instead of the noise panel

@@ -98,7 +98,7 @@ inline void segment_qindices(int qp, int aq, int out[kNumSegs]) {
 // counting pass over the tokens.
 // Frames whose bitstreams may be written at once (GPU encoder pipeline depth); also the distance
 // from the frame whose branch statistics plan a frame's probability updates.
-constexpr int kStatsLag = 3;
+constexpr int kStatsLag = 4;
 
 struct TokenStats {
     std::vector<std::array<uint32_t, 2>> n;  // [1056] (zeros, ones) per probability

@@ -67,7 +67,7 @@ void GpuVp8Encoder::free_slot(Slot& s) {
 GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
     : cfg_(cfg), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
-        throw std::invalid_argument("pipeline_depth must be 1 to 3");
+        throw std::invalid_argument("pipeline_depth must be 1 to 4");
     if (cfg.width > 16383 || cfg.height > 16383) throw std::invalid_argument("vp8: picture larger than 16383");
     depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;

@@ -100,7 +100,7 @@ def test_gpu_vp8_1080p_desktop(gpu):
     assert not st.idr and st.skipped_mbs > 0
 
 
-@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("depth", [2, 3, 4])
 def test_gpu_vp8_pipelined_matches(gpu, depth):
     """Depth 2 / 3 (the bitstreams of the frames in flight written concurrently by per-slot
     writer threads, beside the GPU analysis of the next frame) produce the depth-1 bitstream
