@@ -2,6 +2,7 @@
 // H.264 driver: per-frame slots (pinned frame state, zero-copy output), optional second
 // HIP stream for entropy coding so frame n's CABAC overlaps frame n+1's analysis.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -123,18 +124,24 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
-    if (depth_ > 1)
-        for (int i = 0; i < depth_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_[i], hipStreamNonBlocking));
+    if (depth_ > 1) {
+        // entropy streams: MXDESK_HEVC_ESTREAMS of them (default one per slot), slots beyond
+        // share them round-robin -- every stream of a process takes a hardware queue
+        // (GPU_MAX_HW_QUEUES, 4 by default) and streams beyond that share queues in turn
+        const char* ne = std::getenv("MXDESK_HEVC_ESTREAMS");
+        n_es_ = std::clamp(ne ? std::atoi(ne) : depth_, 1, depth_);
+        for (int i = 0; i < n_es_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_[i], hipStreamNonBlocking));
+        for (int i = n_es_; i < depth_; ++i) stream_e_[i] = stream_e_[i % n_es_];
+    }
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 GpuHevcEncoder::~GpuHevcEncoder() {
     (void)hipStreamSynchronize(stream_);
-    for (hipStream_t s : stream_e_)
-        if (s) {
-            (void)hipStreamSynchronize(s);
-            (void)hipStreamDestroy(s);
-        }
+    for (int i = 0; i < n_es_; ++i) {
+        (void)hipStreamSynchronize(stream_e_[i]);
+        (void)hipStreamDestroy(stream_e_[i]);
+    }
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);

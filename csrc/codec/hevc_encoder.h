@@ -296,7 +296,8 @@ class GpuHevcEncoder final : public VideoEncoder {
     EncoderConfig cfg_;
     HevcCommon common_;
     hipStream_t stream_;
-    hipStream_t stream_e_[kMaxInFlight] = {};  // per slot (depth > 1)
+    hipStream_t stream_e_[kMaxInFlight] = {};  // per slot (depth > 1; the first n_es_ own their stream)
+    int n_es_ = 0;
     hipStream_t es(int slot) const { return stream_e_[slot] ? stream_e_[slot] : stream_; }
     int depth_ = 1;
     Geometry geom_;
