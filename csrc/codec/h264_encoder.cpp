@@ -354,6 +354,15 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     }
 }
 
+void GpuH264Encoder::set_hpel_side_stream(bool on) {
+    hpel_side_ = on;
+    if (!on && stream_a_) {  // its hardware queue is better left to the session's other streams
+        HIP_CHECK(hipStreamSynchronize(stream_a_));
+        HIP_CHECK(hipStreamDestroy(stream_a_));
+        stream_a_ = nullptr;
+    }
+}
+
 void GpuH264Encoder::launcher_loop() {
     (void)hipSetDevice(device_);
     for (;;) {
@@ -415,8 +424,8 @@ GpuH264Encoder::~GpuH264Encoder() {
     if (stream_a_) {
         (void)hipStreamSynchronize(stream_a_);
         (void)hipStreamDestroy(stream_a_);
-        (void)hipEventDestroy(ref_ready_);
     }
+    if (ref_ready_) (void)hipEventDestroy(ref_ready_);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);

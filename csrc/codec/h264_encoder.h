@@ -234,7 +234,7 @@ class GpuH264Encoder final : public VideoEncoder {
     void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void enqueue_entropy() override;
     void link_entropy() override;
-    void set_hpel_side_stream(bool on) override { hpel_side_ = on; }
+    void set_hpel_side_stream(bool on) override;
     void quiesce() override { drain_launcher(); }
     // P pictures: the wait goes after k_hpel (which reads only the reference), so the
     // interpolation of the new reference runs without waiting for the capture hand-off
