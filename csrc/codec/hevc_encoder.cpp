@@ -50,6 +50,8 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * h264::kSsePartStride));
     HIP_CHECK(hipMalloc(&b.sse_tot, kSseSlots * kSseSlotWords * sizeof(unsigned long long)));
+    HIP_CHECK(hipMalloc(&b.pack_done, sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(b.pack_done, 0, sizeof(uint32_t), stream_));
     HIP_CHECK(hipMalloc(&b.wpp_ctx, sizeof(uint32_t) * kWppCtxWords * (size_t)geom_.mb_h));
     HIP_CHECK(hipMalloc(&b.wpp_flag, sizeof(uint32_t) * (size_t)geom_.mb_h));
     HIP_CHECK(hipMemsetAsync(b.wpp_flag, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
@@ -71,7 +73,7 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
                     (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
                     (void*)b.sse_part, (void*)b.sse_tot, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
-                    (void*)b.tok_dense, (void*)b.wpp_ctx, (void*)b.wpp_flag})
+                    (void*)b.tok_dense, (void*)b.wpp_ctx, (void*)b.wpp_flag, (void*)b.pack_done})
         if (p) (void)hipFree(p);
     if (b.wpp_err) (void)hipHostFree(b.wpp_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
@@ -133,6 +135,7 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
         for (int i = 0; i < n_es_; ++i) HIP_CHECK(hipStreamCreateWithFlags(&stream_e_[i], hipStreamNonBlocking));
         for (int i = n_es_; i < depth_; ++i) stream_e_[i] = stream_e_[i % n_es_];
     }
+    clock_khz_ = device_clock_khz();
     HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
@@ -241,14 +244,26 @@ bool GpuHevcEncoder::prepare(bool force_idr) {
 }
 
 void GpuHevcEncoder::enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) {
+    enqueue_analysis_impl(idr, src_y, src_uv, false);
+}
+
+void GpuHevcEncoder::enqueue_analysis_impl(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
     FrameSlot& sl = slots_[prep_slot_];
-    HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(HevcFrameState), hipMemcpyHostToDevice, stream_));
+    HevcOutHeader* hdr = reinterpret_cast<HevcOutHeader*>(sl.host_out);
+    if (publish) {  // eager: states as kernel arguments, start clock stamped on the device
+        launch_hevc_publish(sl.buf, *sl.fs_host, idr ? nullptr : sl.me_fs_host, &hdr->t_start, stream_);
+    } else {  // graph form: copy nodes from the pinned states (no start stamp)
+        hdr->t_start = 0;
+        HIP_CHECK(hipMemcpyAsync(sl.buf.fs, sl.fs_host, sizeof(HevcFrameState), hipMemcpyHostToDevice, stream_));
+        if (!idr)
+            HIP_CHECK(hipMemcpyAsync(sl.buf.me.fs, sl.me_fs_host, sizeof(h264::FrameState), hipMemcpyHostToDevice,
+                                     stream_));
+    }
     if (idr) {
         if (cfg_.aq >= 3)  // the next P picture's temporal classes compare against this source
             launch_hevc_save_src(geom_, sl.buf, src_y, stream_);
         launch_hevc_intra(geom_, sl.buf, common_.slice_rows(), common_.num_slices(), src_y, src_uv, stream_);
     } else {
-        HIP_CHECK(hipMemcpyAsync(sl.buf.me.fs, sl.me_fs_host, sizeof(h264::FrameState), hipMemcpyHostToDevice, stream_));
         h264::launch_hpel(geom_, sl.buf.me, hp_, hp_pitch_, stream_);
         h264::launch_me(geom_, sl.buf.me, src_y, stream_);
         launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
@@ -276,7 +291,11 @@ void GpuHevcEncoder::enqueue_body(bool idr, const uint8_t* src_y, const uint8_t*
     HIP_CHECK(hipGetLastError());
 }
 
-void GpuHevcEncoder::record_start() { HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_)); }
+// eager frames time themselves with device clock stamps (k_hevc_publish / k_hevc_pack); graph
+// frames keep the timing event
+void GpuHevcEncoder::record_start() {
+    if (!eager_) HIP_CHECK(hipEventRecord(slots_[prep_slot_].start, stream_));
+}
 
 void GpuHevcEncoder::record_done() {
     FrameSlot& sl = slots_[prep_slot_];
@@ -291,9 +310,14 @@ void GpuHevcEncoder::submit(const uint8_t* src_y, const uint8_t* src_uv, bool fo
         rc.add_probe(q, probe_bytes(src_y, src_uv, q));
     }
     const bool idr = prepare(force_idr);
+    eager_ = true;
     record_start();
-    enqueue_body(idr, src_y, src_uv);
+    enqueue_analysis_impl(idr, src_y, src_uv, true);
+    link_entropy();
+    enqueue_entropy();
+    HIP_CHECK(hipGetLastError());
     record_done();
+    eager_ = false;
 }
 
 const std::vector<uint8_t>& GpuHevcEncoder::collect() {
@@ -303,9 +327,13 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     FrameSlot& sl = slots_[s];
     wait_event(sl.done);
     last_done_ = sl.done;
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, sl.start, sl.done);
     const HevcOutHeader hdr = *reinterpret_cast<const HevcOutHeader*>(sl.host_out);
+    last_t_end_ = hdr.t_end;
+    float ms = 0;
+    if (hdr.t_start != 0)  // eager frame: device clock stamps
+        ms = hdr.t_end > hdr.t_start ? (float)((double)(hdr.t_end - hdr.t_start) / clock_khz_) : 0.f;
+    else
+        (void)hipEventElapsedTime(&ms, sl.start, sl.done);
     h264::EncoderCommon& rc = common_.rc();
     if (hdr.overflow) {
         rc.end_frame(0, sl.idr);

@@ -172,6 +172,8 @@ struct HevcOutHeader {
     uint32_t pad;
     uint64_t sse[3];
     uint64_t sse_masked;  // luma outside the mask CTBs (SAO path; 0 otherwise)
+    uint64_t t_start;     // device clock: k_hevc_publish (eager frames; 0 otherwise)
+    uint64_t t_end;       // device clock: the last k_hevc_pack workgroup
 };
 static_assert(sizeof(HevcOutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
@@ -212,7 +214,13 @@ struct HevcDeviceBuffers {
     size_t out_bytes;
     unsigned long long* sse_part;
     unsigned long long* sse_tot;  // [kSseSlots][kSseSlotWords] k_hevc_sao distortion totals (4 used per slot)
+    uint32_t* pack_done;          // [1] k_hevc_pack workgroups finished (the last stamps t_end, re-arms it)
 };
+// Eager frames: one kernel stores both frame states (kernel arguments) to the device and stamps
+// the frame's start clock -- instead of two host-to-device copies (two blit kernels on the
+// analysis stream) and a timing event.
+void launch_hevc_publish(const HevcDeviceBuffers& b, const HevcFrameState& fs, const h264::FrameState* me_fs,
+                         uint64_t* t_start, hipStream_t s);
 
 // IDR + temporal AQ: the source luma into fs->save_src (pointer read on the device)
 void launch_hevc_save_src(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, hipStream_t s);
@@ -273,6 +281,9 @@ class GpuHevcEncoder final : public VideoEncoder {
     // analysis chain carries the reference), so with 2-3 frames in flight their serial arithmetic
     // coders run side by side instead of queueing behind each other
     hipStream_t entropy_stream() const override { return stream_e_[prep_slot_]; }
+    // frame GPU time from device clock stamps (the session's render stamp -> k_hevc_pack's end stamp)
+    bool device_clock() const override { return true; }
+    uint64_t last_t_end() const override { return last_t_end_; }
     void enqueue_analysis(bool idr, const uint8_t* src_y, const uint8_t* src_uv) override;
     void enqueue_entropy() override;
     void link_entropy() override;
@@ -297,6 +308,10 @@ class GpuHevcEncoder final : public VideoEncoder {
     HevcCommon common_;
     hipStream_t stream_;
     hipStream_t stream_e_[kMaxInFlight] = {};  // per slot (depth > 1; the first n_es_ own their stream)
+    bool eager_ = false;        // submit(): states published by a kernel, device clock timing
+    uint64_t last_t_end_ = 0;   // device clock at the end of the last collected frame
+    double clock_khz_ = 100000;
+    void enqueue_analysis_impl(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish);
     int n_es_ = 0;
     hipStream_t es(int slot) const { return stream_e_[slot] ? stream_e_[slot] : stream_; }
     int depth_ = 1;

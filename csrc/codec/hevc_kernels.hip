@@ -1964,13 +1964,37 @@ __global__ __launch_bounds__(256) void k_hevc_sse(Geometry g, const HevcFrameSta
 // One workgroup per substream (a slice, or with WPP a CTU row): its payload to a 16-byte aligned
 // place in the host buffer, and its (offset, length, first CTU | kSubSliceStart when it begins a
 // slice) record; workgroup 0 also writes the header.
+__device__ void pack_body(Geometry g, const HevcFrameState* __restrict__ fs, const uint32_t* __restrict__ nslices,
+                          const int* __restrict__ slice_first, const int* __restrict__ slice_of_cu,
+                          const uint8_t* __restrict__ slice_data, uint32_t slice_cap,
+                          const uint32_t* __restrict__ slice_len, uint8_t* __restrict__ host_out, size_t out_bytes);
+
 __global__ __launch_bounds__(256) void k_hevc_pack(Geometry g, const HevcFrameState* __restrict__ fs,
                                                     const uint32_t* __restrict__ nslices,
                                                     const int* __restrict__ slice_first,
                                                     const int* __restrict__ slice_of_cu,
                                                     const uint8_t* __restrict__ slice_data,
                                                     uint32_t slice_cap, const uint32_t* __restrict__ slice_len,
-                                                    uint8_t* __restrict__ host_out, size_t out_bytes) {
+                                                    uint8_t* __restrict__ host_out, size_t out_bytes,
+                                                    uint32_t* __restrict__ done) {
+    const int tid = threadIdx.x;
+    pack_body(g, fs, nslices, slice_first, slice_of_cu, slice_data, slice_cap, slice_len, host_out, out_bytes);
+    // the last workgroup to finish stamps the frame's end clock into the host header (read after
+    // the frame's completion event) and re-arms the counter for the next frame
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            reinterpret_cast<HevcOutHeader*>(host_out)->t_end = wall_clock64();
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+__device__ void pack_body(Geometry g, const HevcFrameState* __restrict__ fs, const uint32_t* __restrict__ nslices,
+                          const int* __restrict__ slice_first, const int* __restrict__ slice_of_cu,
+                          const uint8_t* __restrict__ slice_data, uint32_t slice_cap,
+                          const uint32_t* __restrict__ slice_len, uint8_t* __restrict__ host_out, size_t out_bytes) {
     __shared__ uint32_t red[256];
     __shared__ unsigned long long red64[4][256];
     const int s = blockIdx.x, tid = threadIdx.x;
@@ -2042,14 +2066,26 @@ __global__ __launch_bounds__(256) void k_hevc_pack(Geometry g, const HevcFrameSt
             O |= red[k] >> 31;
             for (int c = 0; c < 4; ++c) E[c] += red64[c][k];
         }
-        HevcOutHeader h;
+        HevcOutHeader& h = *reinterpret_cast<HevcOutHeader*>(host_out);  // not t_start / t_end
         h.total_bytes = T;
         h.num_slices = (uint32_t)num_slices;
         h.overflow = (O || T > out_bytes) ? 1u : 0u;
         h.pad = 0;
         for (int c = 0; c < 3; ++c) h.sse[c] = E[c];
         h.sse_masked = E[3];
-        *reinterpret_cast<HevcOutHeader*>(host_out) = h;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_hevc_publish(HevcFrameState* __restrict__ dfs, HevcFrameState v,
+                                                      h264::FrameState* __restrict__ dme, h264::FrameState vme,
+                                                      int has_me, uint64_t* __restrict__ t_start) {
+    const int t = threadIdx.x;
+    if (t == 0 && t_start) *t_start = wall_clock64();
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(&v);
+    for (int i = t; i < (int)(sizeof(HevcFrameState) / 4); i += 64) reinterpret_cast<uint32_t*>(dfs)[i] = a[i];
+    if (has_me) {
+        const uint32_t* m = reinterpret_cast<const uint32_t*>(&vme);
+        for (int i = t; i < (int)(sizeof(h264::FrameState) / 4); i += 64) reinterpret_cast<uint32_t*>(dme)[i] = m[i];
     }
 }
 
@@ -2119,7 +2155,15 @@ void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_
     hipLaunchKernelGGL(k_hevc_arith, dim3(max_subs), dim3(64), 0, s, g, b.fs, b.tok_dense, b.tok_off,
                        b.slice_first, b.slice_of_cu, b.nslices, b.slice_data, b.slice_cap, b.slice_len, b.slice_clk);
     hipLaunchKernelGGL(k_hevc_pack, dim3(max_subs), dim3(256), 0, s, g, b.fs, b.nslices, b.slice_first, b.slice_of_cu,
-                       b.slice_data, b.slice_cap, b.slice_len, host_out, b.out_bytes);
+                       b.slice_data, b.slice_cap, b.slice_len, host_out, b.out_bytes, b.pack_done);
+}
+
+void launch_hevc_publish(const HevcDeviceBuffers& b, const HevcFrameState& fs, const h264::FrameState* me_fs,
+                         uint64_t* t_start, hipStream_t s) {
+    static_assert(sizeof(HevcFrameState) % 4 == 0 && sizeof(h264::FrameState) % 4 == 0, "word copies");
+    const h264::FrameState none{};
+    hipLaunchKernelGGL(k_hevc_publish, dim3(1), dim3(64), 0, s, b.fs, fs, b.me.fs, me_fs ? *me_fs : none,
+                       me_fs ? 1 : 0, t_start);
 }
 
 }  // namespace hevc
