@@ -452,6 +452,24 @@ PYBIND11_MODULE(_native, m) {
         .def("set_bitrate", [](hevc::GpuHevcEncoder& e, int k) { e.common().rc().set_bitrate(k); })
         .def_property_readonly("stats", &hevc::GpuHevcEncoder::last_stats);
     m.def("hevc_level", &hevc::pick_level, py::arg("width"), py::arg("height"), py::arg("fps"));
+    // Test hook: the VP8 boolean encoder (vp8_encoder.h BoolEncoder) over (probability, bit)
+    // pairs, flushed -- checked against the RFC 6386 per-bit form in tests/test_vp8_bool.py
+    m.def(
+        "vp8_bool_encode",
+        [](py::array_t<int32_t, py::array::c_style> probs, py::array_t<int32_t, py::array::c_style> bits) {
+            if (probs.size() != bits.size()) throw std::invalid_argument("probs and bits differ in length");
+            std::vector<uint8_t> out;
+            vp8::BoolEncoder e(out);
+            const int32_t* p = probs.data();
+            const int32_t* b = bits.data();
+            for (py::ssize_t i = 0; i < probs.size(); ++i) {
+                if (p[i] < 1 || p[i] > 255) throw std::invalid_argument("probability outside 1..255");
+                e.put(p[i], b[i] != 0);
+            }
+            e.flush();
+            return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
+        },
+        py::arg("probs"), py::arg("bits"));
 
     py::class_<h264::GpuH264Encoder>(m, "GpuH264Encoder")
         .def(py::init([](const h264::EncoderConfig& c, uintptr_t stream) {
