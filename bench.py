@@ -202,6 +202,9 @@ def main() -> None:
                          "residual drop for them (default: the encoder's)")
     ap.add_argument("--deblock", type=int, default=None,
                     help="in-loop deblocking filter 0/1 (default: the encoder's)")
+    ap.add_argument("--chroma-qp-offset", type=int, default=None,
+                    help="chroma QP offset against luma (H.264 chroma_qp_index_offset / HEVC pps_cb/cr_qp_offset; "
+                         "default: the encoder's)")
     ap.add_argument("--intra-in-p", type=int, default=None,
                     help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
     ap.add_argument("--depth", type=int, default=None,
@@ -279,6 +282,8 @@ def main() -> None:
         cfg.enc.hevc_wpp = args.hevc_wpp
     if args.hevc_wpp_rows is not None:
         cfg.enc.hevc_wpp_rows = args.hevc_wpp_rows
+    if args.chroma_qp_offset is not None:
+        cfg.enc.chroma_qp_offset = args.chroma_qp_offset
     if args.intra_in_p is not None:
         cfg.enc.intra_in_p = args.intra_in_p
     if args.deblock is not None:
