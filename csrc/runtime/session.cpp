@@ -106,11 +106,13 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     }
     const bool cap = cfg_.capture_stream > 0 || (cfg_.capture_stream < 0 && std::string(enc_->codec()) == "h264");
     if (depth_ > 1 && cap && !cfg_.use_graph) {
-        // the capture stream at the lowest priority, so its render / conversion kernels yield
-        // compute units to the previous frame's analysis (4K H.264 4,491 -> 4,613 fps,
-        // profiles/r04_capture); MXDESK_CAPTURE_PRIORITY=normal for the default priority
+        // MXDESK_CAPTURE_PRIORITY=low: the capture stream at the lowest priority, so its render /
+        // conversion kernels yield compute units to the previous frame's analysis (4K H.264
+        // 4,491 -> 4,613 fps).  Not the default: a stream of another priority takes a hardware
+        // queue of its own for the whole process, and the other sessions' streams then share
+        // fewer queues (paced density 200 -> 136 sessions, profiles/r04_capture)
         const char* cp = std::getenv("MXDESK_CAPTURE_PRIORITY");
-        if (!(cp && std::string(cp) == "normal")) {
+        if (cp && std::string(cp) == "low") {
             int least = 0, greatest = 0;
             HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             HIP_CHECK(hipStreamCreateWithPriority(&cap_stream_, hipStreamNonBlocking, least));
