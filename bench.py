@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -163,6 +164,72 @@ def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: flo
     return out
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without WORLD_SIZE: run N rank processes of this script (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them, rendezvous on
+    127.0.0.1), wait for all of them and return the first non-zero exit code.  Rank 0 prints the
+    JSON line; the ranks share this process's stdout."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+class CpuSession:
+    """The plumbing configuration's session (BASELINE config 1, no GPU): the numpy desktop
+    (mxdesk.models.synthetic.CpuSyntheticDesktop) -> BT.709 NV12 -> the C++ CPU H.264 encoder
+    (the GPU encoder's bit-exact oracle).  step() returns the FrameResult fields bench.py reads."""
+
+    def __init__(self, N, cfg, noise: int):
+        from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+        self._conv = bgrx_to_nv12
+        self.desk = CpuSyntheticDesktop(cfg.width, cfg.height, noise=bool(noise))
+        cfg.enc.width, cfg.enc.height, cfg.enc.fps = cfg.width, cfg.height, cfg.fps
+        self.enc = N.CpuH264Encoder(cfg.enc)
+        self.fps = cfg.fps
+        self.n = 0
+
+    def step(self, force_idr: bool = False):
+        import types
+
+        import numpy as np
+
+        t0 = time.monotonic()
+        img = self.desk.render(self.n, self.n / self.fps, int(t0 * 1e6))
+        y, uv = self._conv(img)
+        au = self.enc.encode(y, uv, force_idr)
+        t1 = time.monotonic()
+        st = self.enc.stats
+        self.n += 1
+        w, h = self.desk.w, self.desk.h
+        ry, ruv = self.enc.recon()
+
+        def sse(a, b):
+            d = a.astype(np.int64) - b.astype(np.int64)
+            return float((d * d).sum())
+
+        def psnr(e, k):
+            return 99.0 if e <= 0 else min(99.0, 10 * math.log10(65025.0 * k / e))
+
+        py_ = psnr(sse(ry[:h, :w], y[:h, :w]), w * h)
+        su = sse(ruv[:h // 2, 0:w:2], uv[:h // 2, 0:w:2])
+        sv = sse(ruv[:h // 2, 1:w:2], uv[:h // 2, 1:w:2])
+        return types.SimpleNamespace(au=au, qp=st.qp, psnr_y=py_, psnr_y_masked=py_, psnr_u=psnr(su, w * h / 4),
+                                     psnr_v=psnr(sv, w * h / 4), gpu_ms=0.0, t_capture_us=t0 * 1e6,
+                                     t_encoded_us=t1 * 1e6)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -183,7 +250,7 @@ def main() -> None:
     ap.add_argument("--hevc-slice-cost", type=int, default=None,
                     help="HEVC P-picture slice work target (more = fewer, longer slices)")
     ap.add_argument("--hevc-wpp", type=int, default=None,
-                    help="HEVC wavefront substreams (1, default) or cost-balanced slices (0)")
+                    help="HEVC wavefront substreams (1) or cost-balanced slices (0, default)")
     ap.add_argument("--hevc-wpp-rows", type=int, default=None,
                     help="HEVC with WPP: CTU rows per P slice (0 = one slice per picture)")
     ap.add_argument("--search-range", type=int, default=16)
@@ -230,7 +297,25 @@ def main() -> None:
     ap.add_argument("--py-loop", type=int, default=0,
                     help="1: drive a single session from this Python thread instead of the native session driver")
     ap.add_argument("--json-out", type=str, default="")
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                    help="cpu: the no-GPU plumbing configuration (BASELINE config 1): numpy-rendered desktop + the "
+                         "C++ CPU H.264 encoder, one process per rank over gloo; never the headline number")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} (one rank per GPU: "
+                  "launch with --nproc-per-node equal to --gpus)", file=sys.stderr)
+            sys.exit(2)
+    elif args.gpus > 1:
+        # no launcher: start one fresh rank process per GPU ourselves.  Nothing in this parent has
+        # touched the GPU (no torch / HIP import yet); the ranks are children, never an exec.
+        sys.exit(launch_ranks(args.gpus))
+    gpu = args.device == "gpu"
+    if not gpu:  # plumbing configuration: CPU encoder, gloo, no GPU-only probes
+        args.codec, args.backend, args.density_probe, args.quality_probe = "h264", "gloo", 0, 0
+        args.depth, args.sessions_per_gpu, args.out_width, args.out_height = 1, 1, 0, 0
     if args.codec == "vp8":
         args.subpel = 0  # VP8 vectors here are full-sample (the reported ME setting says so)
         args.depth = min(args.depth or 4, 4)  # the VP8 encoder keeps at most four frames in flight
@@ -247,25 +332,27 @@ def main() -> None:
     import torch
 
     # one rank per GPU; the modulo only matters when rehearsing several ranks on fewer GPUs
-    ndev = max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count()) if gpu else 1
     dev_index = local_rank % ndev
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
-        torch.cuda.set_device(dev_index)
+        if gpu:
+            torch.cuda.set_device(dev_index)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group(args.backend)
-    else:
+    elif gpu:
         torch.cuda.set_device(dev_index)
-    coll_dev = "cuda" if (dist is None or args.backend == "nccl") else "cpu"
+    coll_dev = "cuda" if gpu and (dist is None or args.backend == "nccl") else "cpu"
 
     import mxdesk
 
     N = mxdesk.native()
-    N.set_device(dev_index)
+    if gpu:
+        N.set_device(dev_index)
     cfg = N.SessionConfig()
     cfg.width, cfg.height, cfg.fps = args.width, args.height, args.fps
     cfg.out_width, cfg.out_height = args.out_width, args.out_height
@@ -307,7 +394,7 @@ def main() -> None:
         cfg.mask_x0, cfg.mask_y0 = int(ow * 0.04), int(oh * 0.55)
         cfg.mask_x1, cfg.mask_y1 = cfg.mask_x0 + int(ow * 0.16) + 1, cfg.mask_y0 + int(oh * 0.22) + 1
     K = max(1, args.sessions_per_gpu)
-    sessions = [N.Session(cfg) for _ in range(K)]
+    sessions = [N.Session(cfg) if gpu else CpuSession(N, cfg, args.noise) for _ in range(K)]
 
     def run(n_frames: int, record: bool):
         """n_frames per session, up to `depth` frames in flight each, driven by the native session
@@ -315,6 +402,9 @@ def main() -> None:
         serving path's pipeline thread does); --py-loop 1: this Python thread."""
         out = []
         depth = max(1, args.depth)
+        if not gpu:
+            res = [sessions[0].step(False) for _ in range(n_frames)]
+            return res if record else []
         if K > 1 or not args.py_loop:
             per = N.run_sessions(sessions, n_frames, depth)
             if record:
@@ -339,15 +429,17 @@ def main() -> None:
     run(args.warmup, False)
 
     def barrier():
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
 
     barrier()
     t0 = time.perf_counter()
     lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m, psnr_uv = [], [], [], [], [], [], []
-    if K == 1 and args.depth == 1:
+    if K == 1 and args.depth == 1 and gpu:
         results = [sessions[0].step(False) for _ in range(args.steps)]
     else:
         results = run(args.steps, True)
@@ -391,7 +483,8 @@ def main() -> None:
             # BASELINE.json's metric verbatim for the headline configuration
             "metric": {"h264": "encoded FPS + p50 end-to-end latency at 1080p60 H.264; concurrent sessions/node",
                        "hevc": "encoded FPS (HEVC desktop session, aggregate over GPUs) + p50 E2E latency",
-                       "vp8": "encoded FPS (VP8 desktop session, aggregate over GPUs) + p50 E2E latency"}[args.codec],
+                       "vp8": "encoded FPS (VP8 desktop session, aggregate over GPUs) + p50 E2E latency"}[args.codec]
+            if gpu else "encoded FPS, CPU plumbing configuration (numpy desktop + C++ CPU H.264; no GPU)",
             "value": round(fps_total, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -407,7 +500,8 @@ def main() -> None:
             "encoded_fps_per_gpu": round(per_gpu, 2),
             "sessions_per_gpu": K,
             "hip_graph": bool(args.graph),
-            "capture_stream": bool(sessions[0].capture_stream_active),
+            "capture_stream": bool(sessions[0].capture_stream_active) if gpu else False,
+            "device": args.device,
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
@@ -425,7 +519,8 @@ def main() -> None:
             "sessions_per_gpu_at_60fps_measured": density["sustained"] if density else None,
             "density_probe": density,
             "dtype": "uint8 video (8-bit 4:2:0), " + CODEC_LABEL[args.codec][2],
-            "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)",
+            "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)" if gpu
+            else "synthetic (numpy-rendered desktop, mxdesk.models.synthetic.CpuSyntheticDesktop)",
             "config": {
                 "model": f"{args.width}x{args.height}@{args.fps} {CODEC_LABEL[args.codec][0]}"
                          " desktop session"

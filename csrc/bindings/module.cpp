@@ -191,6 +191,8 @@ PYBIND11_MODULE(_native, m) {
                 const int cw = e.coded_pitch();
                 const auto& cfg = e.common().config();
                 const int ch = e.common().mb_h() * 16;
+                if (y.shape(0) < cfg.height || pitch < cfg.width || uv.shape(0) < cfg.height / 2)
+                    throw std::invalid_argument("planes smaller than the encoder's configured picture");
                 std::vector<uint8_t> py_, puv;
                 const uint8_t* yy = y.data();
                 const uint8_t* uu = uv.data();
@@ -250,6 +252,8 @@ PYBIND11_MODULE(_native, m) {
                 const int cw = e.coded_pitch();
                 const auto& cfg = e.common().config();
                 const int ch = e.common().mb_h() * 16;
+                if (y.shape(0) < cfg.height || pitch < cfg.width || uv.shape(0) < cfg.height / 2)
+                    throw std::invalid_argument("planes smaller than the encoder's configured picture");
                 std::vector<uint8_t> py_, puv;
                 const uint8_t* yy = y.data();
                 const uint8_t* uu = uv.data();

@@ -61,7 +61,8 @@ struct EncoderConfig {
     bool h264_deblock() const { return deblock > 0; }
     bool hevc_deblock() const { return deblock != 0; }
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
-                              // default: +0.26 dB masked PSNR for -33 % fps on the 1080p desktop (profiles/r02_intra)
+                              // default: it costs -35 % fps on the 1080p desktop (k_intra_analyze + k_intra_p on
+                              // the analysis queue, profiles/r04_toolset/NOTES.md)
     int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
     int hevc_slice_cost = 2048;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
     // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): P pictures in slices of

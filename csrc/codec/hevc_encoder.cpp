@@ -16,7 +16,8 @@ namespace hevc {
 
 void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     const int ncu = geom_.mb_w * geom_.mb_h;
-    const int ns = std::max(common_.max_slices(), geom_.mb_h);  // substreams: slices, or CTU rows with WPP
+    // substreams: cost-balanced slices, or (WPP) every CTU row
+    const int ns = cfg_.hevc_wpp ? std::max(common_.max_slices(), geom_.mb_h) : common_.max_slices();
     HevcDeviceBuffers& b = sl.buf;
     HIP_CHECK(hipMalloc(&b.fs, sizeof(HevcFrameState)));
     HIP_CHECK(hipMalloc(&b.me.fs, sizeof(h264::FrameState)));

@@ -12,7 +12,8 @@
 // predicting from the last frame with full-sample vectors (ZEROMV / NEARESTMV / NEARMV / NEWMV);
 // inter frames segmented (9.3) by the temporal classes of the H.264 encoder's adaptive
 // quantisation -- four segment quantisers, a per-macroblock segment map -- key frames one
-// quantiser; loop filter level 0; token partitions by MB row; default probabilities.
+// quantiser; loop filter level 0; token partitions by MB row; coefficient probabilities updated per
+// frame from the token statistics of frame n - kStatsLag (vp8_encoder.h).
 #pragma once
 #include <stdint.h>
 

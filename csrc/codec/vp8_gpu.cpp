@@ -96,7 +96,9 @@ GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
     HIP_CHECK(hipStreamSynchronize(stream_));
     HIP_CHECK(hipGetDevice(&device_));
     for (int i = 0; i < depth_; ++i) {
-        slots_[i].pool = std::make_unique<PartitionPool>(pool_threads());
+        // the slot writers only overlap across slots: share the machine's pool size among them
+        // (at depth 4 a session otherwise held up to 36 host threads)
+        slots_[i].pool = std::make_unique<PartitionPool>(std::max(1, pool_threads() / depth_));
         slots_[i].writer = std::thread([this, i]() { writer_loop(slots_[i]); });
     }
 }

@@ -184,6 +184,10 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     HIP_CHECK(hipMalloc(&synth_bg_, (size_t)pool_->pitch() * cfg_.height));
     pix::launch_synth_static(synth_bg_, synth_params(), stream_);
     HIP_CHECK(hipGetLastError());
+    // k_synth reads the static layer from cap_stream_ (a non-blocking stream with no order
+    // against stream_) or from the upload stream: the layer must be complete before the first
+    // frame is rendered on any of them
+    HIP_CHECK(hipStreamSynchronize(stream_));
     HIP_CHECK(hipMalloc(&synth_dev_, sizeof(pix::SynthParams) * cfg_.pool_slots));
     // [frame slot][encoder slot][IDR][analysis, entropy]
     graphs_.assign((size_t)cfg_.pool_slots * kMaxDepth * 2 * 2, nullptr);
@@ -194,19 +198,21 @@ Session::~Session() {
     if (ht_n_ > 0 && std::getenv("MXDESK_HOST_TIMING"))
         std::fprintf(stderr, "[mxdesk] host us/frame over %lld frames: submit %.1f, wait %.1f, collect %.1f\n",
                      (long long)ht_n_, ht_submit_ / ht_n_, ht_wait_ / ht_n_, ht_post_ / ht_n_);
-    if (stream_) hipStreamSynchronize(stream_);
+    // drain every stream that can still touch the pinned stamp block, the synth parameters or
+    // the static layer (frames in flight on the capture / upload streams and in the encoder)
+    // before anything is freed
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    if (cap_stream_) (void)hipStreamSynchronize(cap_stream_);
+    if (upload_stream_) (void)hipStreamSynchronize(upload_stream_);
+    enc_.reset();
     for (auto g : graphs_)
         if (g) hipGraphExecDestroy(g);
     hipHostFree(synth_host_);
     if (ts_) hipHostFree(ts_);
     if (synth_bg_) hipFree(synth_bg_);
     hipFree(synth_dev_);
-    enc_.reset();
     pool_.reset();
-    if (cap_stream_) {
-        (void)hipStreamSynchronize(cap_stream_);
-        (void)hipStreamDestroy(cap_stream_);
-    }
+    if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
     for (int k = 0; k < kMaxDepth; ++k) {
         if (nv12_y_[k]) (void)hipFree(nv12_y_[k]);
         if (nv12_uv_[k]) (void)hipFree(nv12_uv_[k]);

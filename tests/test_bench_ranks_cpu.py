@@ -1,0 +1,72 @@
+"""bench.py's multi-rank contract on the CPU (VERDICT r4 "Next round" #4).
+
+`bench.py --gpus N` must never silently measure one GPU: without WORLD_SIZE it starts N rank
+processes itself (before anything touches a GPU), under torch.distributed.run WORLD_SIZE must
+equal --gpus.  Both launch forms are run here with the CPU plumbing session (`--device cpu`,
+gloo), and the JSON's aggregate is checked against its own clock: value = N * steps over the
+slowest rank's timed region."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+ARGS = ["--device", "cpu", "--steps", "6", "--warmup", "1", "--width", "256", "--height", "144",
+        "--bitrate-kbps", "800"]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _check(r, n):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints exactly one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["config"]["global_batch"] == n and out["device"] == "cpu"
+    steps = out["steps"]
+    assert out["value"] == pytest.approx(n * steps / (out["ms_per_step"] * steps / 1000.0), rel=2e-3)
+    assert out["encoded_fps_per_gpu"] == pytest.approx(out["value"] / n, rel=1e-3)
+    return out
+
+
+def test_bench_self_launches_ranks_without_world_size():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"] + ARGS, cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    _check(r, 2)
+
+
+def test_bench_under_torchrun():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py"), "--gpus", "2"] + ARGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    _check(r, 2)
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    env = dict(_env(), WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4"] + ARGS, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_single_gpu_default():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py")] + ARGS, cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    out = _check(r, 1)
+    assert out["mean_psnr_y_db"] > 30
