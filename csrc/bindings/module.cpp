@@ -396,16 +396,17 @@ PYBIND11_MODULE(_native, m) {
                  for (const auto& c : e.cus()) t.push_back(c.type);
                  return t;
              })
-        .def("cu_info",  // (type, qp, cbf, tu_split) per CU of the last picture
+        .def("cu_info",  // (type, qp, cbf, tu_split, coding-tree depth) per 16x16 unit of the last picture
              [](hevc::CpuHevcEncoder& e) {
                  const auto& cus = e.cus();
-                 py::array_t<int32_t> a({(py::ssize_t)cus.size(), (py::ssize_t)4});
+                 py::array_t<int32_t> a({(py::ssize_t)cus.size(), (py::ssize_t)5});
                  auto m = a.mutable_unchecked<2>();
                  for (size_t i = 0; i < cus.size(); ++i) {
                      m(i, 0) = cus[i].type;
                      m(i, 1) = cus[i].qp;
                      m(i, 2) = cus[i].cbf;
                      m(i, 3) = cus[i].tu_split;
+                     m(i, 4) = cus[i].ct;
                  }
                  return a;
              })

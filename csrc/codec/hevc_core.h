@@ -6,20 +6,25 @@
 // every bit and every sample.
 //
 // Coding subset (fixed by the SPS/PPS that hevc_cpu.cpp writes):
-//   CTB = CU = 16x16 (no split_cu_flag), PU 2Nx2N, TU 16x16 luma / 8x8 chroma; with
-//   EncoderConfig.tu_split an inter CU may instead split its transform tree once (four 8x8
-//   luma TUs, eight 4x4 chroma TUs: max_transform_hierarchy_depth_inter 1), chosen per CU by
-//   SSE + lambda * estimated bits; I slices of intra CUs, P slices of skip / merge / AMVP CUs
-//   with one reference picture, MaxNumMergeCand 5, no TMVP, no sign hiding, cu_qp_delta per CU
-//   (adaptive quantisation); in-loop deblocking (8.7.2) and sample adaptive offset (8.7.3, band /
+//   CTB 32x32 with a coding quadtree (split_cu_flag): a CTB is one CU32 or four CU16.  The
+//   encoder analyses 16x16 *units* (kCtb below is the unit size, not the CTB's); a CU32 joins the
+//   four units of a CTB when their prediction (type, vector) and QP agree, and its transform tree
+//   -- split by size at depth 0 (32 > the 16-sample maximum TB) -- has exactly the units' 16x16
+//   trees as its depth-1 nodes, so the units keep their own levels (see "coding tree" below).
+//   PU 2Nx2N, TU 16x16 luma / 8x8 chroma; with EncoderConfig.tu_split an inter unit may split its
+//   transform tree once more (four 8x8 luma TUs, eight 4x4 chroma TUs), chosen per unit by SSE +
+//   lambda * estimated bits; I slices of intra CUs, P slices of skip / merge / AMVP CUs with one
+//   reference picture, MaxNumMergeCand 5 (A1 B1 B0 A0 B2), no TMVP, no sign hiding, cu_qp_delta
+//   per 16x16 quantization group (adaptive quantisation; QP prediction from the left / above QG
+//   inside the CTB, 8.6.1); in-loop deblocking (8.7.2) and sample adaptive offset (8.7.3, band /
 //   edge per CTB) on by default.
-// Slices and CABAC substreams: I pictures in slices of up to kMaxSliceRows CTU rows (the intra
-//   wavefront's workgroup); P pictures (default, EncoderConfig.hevc_wpp 0) in up to the level's
-//   slice limit of raster runs balanced on an estimate of their bin tokens (cu_cost,
-//   plan_num_slices), one substream each.  hevc_wpp 1: wavefront parallel processing -- slices of
-//   hevc_wpp_rows CTU rows, every CTU row a CABAC substream entropy coded by its own GPU wave,
-//   starting from the contexts the row above had after its second CTU, with entry points in the
-//   slice header (+0.3 dB at half the 4K rate: profiles/r04_hevc/NOTES.md).
+// Slices and CABAC substreams (CTB aligned): I pictures in slices of up to kMaxSliceRows / 2 CTB
+//   rows (the intra wavefront's workgroup); P pictures (default, EncoderConfig.hevc_wpp 0) in up to
+//   the level's slice limit of raster runs of CTBs balanced on an estimate of their bin tokens
+//   (cu_cost, plan_num_slices), one substream each.  hevc_wpp 1: wavefront parallel processing --
+//   slices of hevc_wpp_rows CTB rows, every CTB row a CABAC substream entropy coded by its own GPU
+//   wave, starting from the contexts the row above had after its second CTB, with entry points in
+//   the slice header.
 //
 // Replaces NVENC HEVC behind the reference's GStreamer stack (nvh264enc default encoder,
 // reference Dockerfile:210 / README.md:21; BASELINE.json config "4K60 HEVC").
@@ -34,7 +39,10 @@
 namespace mx {
 namespace hevc {
 
-constexpr int kCtb = 16;  // CTB = CU size
+constexpr int kCtb = 16;  // analysis unit (16x16; a CU16, or a quadrant of a CU32)
+constexpr int kCtbLog2 = 5;     // CTB 32x32
+constexpr int kMinCbLog2 = 4;   // smallest CU 16x16
+constexpr int kMaxTbLog2 = 4;   // largest TU 16x16 (a CU32's tree splits at depth 0 by size)
 constexpr int kMaxMergeCand = 5;  // MaxNumMergeCand (slice header five_minus_max_num_merge_cand 0)
 constexpr int kCoefPerCu = 384;  // 256 luma + 64 Cb + 64 Cr, each TU in scan order
 
@@ -286,8 +294,34 @@ MXHD void intra_predict(int mode, int log2n, int cidx, const int* left_in, const
     }
 }
 
-// Most probable modes (8.4.2); cand_b is always DC here because the CU above lies in
-// another CTB, but the function is general.
+// Intra modes whose N x N prediction never reads the below-left references p[-1][N .. 2N-1] (not
+// even through the [1 2 1] reference filter), bit m = mode m, for luma (cidx 0) or chroma.  The
+// first unit of a CTB has its below-left neighbour (the left CTB's last unit) available to the
+// decoder but not yet reconstructed by the encoder's raster wavefront; it restricts itself to
+// these modes and predicts with the below-left treated as unavailable -- for these modes the
+// same samples as the decoder's.  Found by perturbing the below-left samples.
+inline uint64_t bl_safe_modes(int log2n, int cidx) {
+    const int N = 1 << log2n;
+    int L[65], T[65], L2[65], p0[32 * 32], p1[32 * 32], p2[32 * 32];
+    for (int k = 0; k <= 2 * N; ++k) {
+        L[k] = (k * 37 + 11) & 255;
+        T[k] = (k * 53 + 7) & 255;
+    }
+    uint64_t m = 0;
+    for (int mode = 0; mode < 35; ++mode) {
+        intra_predict(mode, log2n, cidx, L, T, p0);
+        bool same = true;
+        for (int v = 1; v <= 2 && same; ++v) {
+            for (int k = 0; k <= 2 * N; ++k) L2[k] = k > N ? (L[k] + 97 * v) & 255 : L[k];
+            intra_predict(mode, log2n, cidx, L2, T, v == 1 ? p1 : p2);
+            for (int i = 0; i < N * N; ++i) same = same && (v == 1 ? p1[i] : p2[i]) == p0[i];
+        }
+        if (same) m |= 1ull << mode;
+    }
+    return m;
+}
+
+// Most probable modes (8.4.2) from the left / above candidates (the above one only inside the CTB).
 MXHD void mpm_list(int cand_a, int cand_b, int* l) {
     if (cand_a == cand_b) {
         if (cand_a < 2) {
@@ -636,6 +670,7 @@ struct CabacEnc {
         test_write_out();
     }
     // Flush after the final terminate(1) and append rbsp_slice_segment_trailing_bits.
+    MXHD void flush() {}  // (BinRec interface: nothing buffered here)
     MXHD void finish_slice() {
         if (low >> (32 - bits_left)) {
             put_byte(buffered + 1);
@@ -698,8 +733,13 @@ struct CuInfo {
     uint8_t cbf_y4;  // split: bit k = luma TU k coded
     uint8_t cbf_c4;  // split: bit k = Cb TU k, bit 4+k = Cr TU k coded
     uint8_t est_bytes;  // entropy-coder work estimate of a coded CU: cu_bits_est / 8, capped 255 (set_est_bytes)
+    // coding-tree depth of this 16x16 unit: 0 = one of the four units of a CU32 (type, vector, QP
+    // and mvp / mvd equal in all four; the CU's prediction syntax lives in the z-order first unit),
+    // 1 = a CU16
+    uint8_t ct;
+    uint8_t rsv[7];
 };
-static_assert(sizeof(CuInfo) == 24, "CuInfo layout");
+static_assert(sizeof(CuInfo) == 32, "CuInfo layout");
 constexpr int kCuWords = (int)(sizeof(CuInfo) / 4);
 
 // Per-TU summary (cbf, last position, coded sub-blocks) of coefficients in scan order.
@@ -1025,28 +1065,61 @@ MXHD void code_qp_delta(E& e, Ctx& ctx, int d) {
     if (a) e.bypass(d < 0);
 }
 
-// One CTU (= one CU).  left / above: neighbouring CUs in the same slice or null.
-// qp_prev: QP predictor (QpY of the previous CU in decoding order, slice QP at start).
-// Neighbour facts the CU syntax needs (type -1: not available in the slice).
-struct CuNb {
-    int left_type, left_mode, above_type;
-};
-MXHD CuNb cu_nb(const CuInfo* left, const CuInfo* above) {
-    return CuNb{left ? (int)left->type : -1, left ? (int)left->intra_mode : 1, above ? (int)above->type : -1};
+// sao() syntax of a CTB (defined with SAO below)
+template <class E, class Ctx>
+MXHD void code_sao_w(E& e, Ctx& ctx, uint32_t p0, uint32_t p1, uint32_t p2, bool has_l, uint32_t l0, uint32_t l1,
+                     uint32_t l2, bool has_u, uint32_t u0, uint32_t u1, uint32_t u2);
+
+// ---------------------------------------------------------------- coding tree (7.3.8.2-7.3.8.10)
+// The CTB grid over the 16x16 units (mb_w x mb_h units, cw x ch CTBs) and the decoding order:
+// CTBs in raster order, the (up to four) units of a CTB in z order.  A unit's *coding position* is
+// 4 * ctb + z; positions of units outside the picture stay empty.
+MXHD int ctb_cols(int mb_w) { return (mb_w + 1) >> 1; }
+MXHD int ctb_rows(int mb_h) { return (mb_h + 1) >> 1; }
+MXHD int ctb_of(int x, int y, int cw) { return (y >> 1) * cw + (x >> 1); }
+MXHD int cpos_of(int x, int y, int cw) { return (ctb_of(x, y, cw) << 2) | ((y & 1) << 1) | (x & 1); }
+MXHD void cpos_xy(int k, int cw, int* x, int* y) {
+    const int c = k >> 2;
+    *x = ((c % cw) << 1) | (k & 1);
+    *y = ((c / cw) << 1) | ((k >> 1) & 1);
+}
+// CTB c lies entirely inside the picture (its split_cu_flag is coded; else it is inferred 1)
+MXHD bool ctb_whole(int c, int cw, int mb_w, int mb_h) {
+    return 2 * (c % cw) + 1 < mb_w && 2 * (c / cw) + 1 < mb_h;
+}
+// z index of the last unit of CTB c inside the picture
+MXHD int ctb_last_z(int c, int cw, int mb_w, int mb_h) {
+    const bool r = 2 * (c % cw) + 1 < mb_w, b = 2 * (c / cw) + 1 < mb_h;
+    return (r && b) ? 3 : (b ? 2 : (r ? 1 : 0));
 }
 
-// How a CU's residual is laid out after its header (code_cu_head): none, one transform unit
-// per component (cbf flags and cu_qp_delta already in the head), or the depth-1 transform tree
-// (four children, each with its own cbf flags; cu_qp_delta with the first coded child).
-enum CuResidual { kResNone = 0, kResFlat = 1, kResSplit = 2 };
-MXHD int cu_residual_kind(const CuInfo& c) {
-    if (c.type == kCuSkip) return kResNone;
-    const bool intra = c.type == kCuIntra;
-    const bool root = c.type != kCuAmvp || c.cbf != 0;
-    if (!root) return kResNone;
-    if (!intra && c.tu_split == 2) return kResSplit;
-    return c.cbf ? kResFlat : kResNone;
+// Neighbour facts of a CU at its origin unit (x, y) for the CU syntax: the units left of and above
+// the origin (type -1: not available -- outside the picture or in an earlier slice; every other
+// earlier unit precedes in decoding order), their coding-tree depths (split_cu_flag contexts) and
+// intra modes for the MPM list (8.4.2: the above unit only counts inside the same CTB, else DC).
+struct CuNb {
+    int left_type, left_mode, above_type, above_mode, left_ct, above_ct;
+};
+// get(u): the CuInfo of raster unit u
+template <class Get>
+MXHD CuNb cu_nb_at(const Get& get, int x, int y, int mb_w, int cw, int first_ctb) {
+    CuNb nb{-1, 1, -1, 1, 0, 0};
+    if (x > 0 && ctb_of(x - 1, y, cw) >= first_ctb) {
+        const CuInfo l = get(y * mb_w + x - 1);
+        nb.left_type = l.type;
+        nb.left_mode = l.intra_mode;
+        nb.left_ct = l.ct;
+    }
+    if (y > 0 && ctb_of(x, y - 1, cw) >= first_ctb) {
+        const CuInfo a = get((y - 1) * mb_w + x);
+        nb.above_type = a.type;
+        nb.above_mode = (y & 1) ? (int)a.intra_mode : 1;
+        nb.above_ct = a.ct;
+    }
+    return nb;
 }
+MXHD int mpm_cand_a(const CuNb& nb) { return nb.left_type == kCuIntra ? nb.left_mode : 1; }
+MXHD int mpm_cand_b(const CuNb& nb) { return nb.above_type == kCuIntra ? nb.above_mode : 1; }
 
 // merge_idx: truncated rice, cMax MaxNumMergeCand - 1, first bin context coded, rest bypass
 template <class E, class Ctx>
@@ -1055,25 +1128,26 @@ MXHD void code_merge_idx(E& e, Ctx& ctx, int idx) {
     for (int k = 1; k < kMaxMergeCand - 1 && k <= idx; ++k) e.bypass(idx > k);
 }
 
-// CU syntax up to its residual: skip / prediction / motion, rqt_root_cbf, split_transform_flag,
-// and for an unsplit tree the cbf flags and cu_qp_delta; for a split tree the parent's chroma cbf.
+// Prediction syntax of a CU of size 2^log2cb: cu_skip_flag, pred_mode_flag, part_mode (2Nx2N;
+// coded for inter CUs and for intra CUs of the minimum size), the intra luma / chroma modes or
+// merge_flag / merge_idx / mvd / mvp flag, and rqt_root_cbf (AMVP).  root_cbf: a level is coded
+// somewhere in the CU.  Returns whether a transform tree follows (inferred for intra and merge).
 template <class E, class Ctx>
-MXHD void code_cu_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, CuNb nb, int qp_prev) {
+MXHD bool code_pred_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, const CuNb& nb, bool root_cbf, int log2cb) {
     if (!islice) {
         const int inc = (nb.left_type == kCuSkip ? 1 : 0) + (nb.above_type == kCuSkip ? 1 : 0);
         e.bin(ctx, C_SKIP + inc, c.type == kCuSkip);
     }
     if (c.type == kCuSkip) {
         code_merge_idx(e, ctx, c.mvp_idx);
-        return;
+        return false;
     }
     const bool intra = c.type == kCuIntra;
     if (!islice) e.bin(ctx, C_PRED_MODE, intra);
-    e.bin(ctx, C_PART_MODE, 1);  // PART_2Nx2N
+    if (!intra || log2cb == kMinCbLog2) e.bin(ctx, C_PART_MODE, 1);  // PART_2Nx2N
     if (intra) {
-        const int cand_a = nb.left_type == kCuIntra ? nb.left_mode : 1;
         int l[3];
-        mpm_list(cand_a, 1, l);
+        mpm_list(mpm_cand_a(nb), mpm_cand_b(nb), l);
         const int m = c.intra_mode;
         const int hit = (m == l[0]) ? 0 : (m == l[1] ? 1 : (m == l[2] ? 2 : -1));
         e.bin(ctx, C_PREV_INTRA, hit >= 0);
@@ -1081,57 +1155,71 @@ MXHD void code_cu_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, CuNb nb, in
             e.bypass(hit > 0);
             if (hit > 0) e.bypass(hit > 1);
         } else {
+            // rem_intra_luma_pred_mode: the mode's rank among the 32 modes outside the list
             int rem = m;
             for (int k = 0; k < 3; ++k) rem -= (l[k] < m) ? 1 : 0;
             e.bypass_bits((uint32_t)rem, 5);
         }
         e.bin(ctx, C_CHROMA_PRED, 0);  // intra_chroma_pred_mode 4 (DM)
-    } else {
-        const bool merge = c.type == kCuMerge;
-        e.bin(ctx, C_MERGE_FLAG, merge);
-        if (merge) code_merge_idx(e, ctx, c.mvp_idx);
-        if (!merge) {
-            code_mvd(e, ctx, c.mvdx, c.mvdy);
-            e.bin(ctx, C_MVP, c.mvp_idx);
-        }
+        return true;
     }
-    bool root = true;
-    if (c.type == kCuAmvp) {
-        root = c.cbf != 0;
-        e.bin(ctx, C_RQT_ROOT, root);
+    const bool merge = c.type == kCuMerge;
+    e.bin(ctx, C_MERGE_FLAG, merge);
+    if (merge) {
+        code_merge_idx(e, ctx, c.mvp_idx);
+        return true;
     }
-    if (!root) return;
-    if (!intra && c.tu_split) e.bin(ctx, C_SPLIT_TRANSFORM + 1, c.tu_split == 2);  // 5 - log2(16)
-    const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
-    e.bin(ctx, C_CBF_CHROMA + 0, cb);
-    e.bin(ctx, C_CBF_CHROMA + 0, cr);
-    if (!intra && c.tu_split == 2) return;
-    if (intra || cb || cr) e.bin(ctx, C_CBF_LUMA + 1, cy);
-    if (c.cbf) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
+    code_mvd(e, ctx, c.mvdx, c.mvdy);
+    e.bin(ctx, C_MVP, c.mvp_idx);
+    e.bin(ctx, C_RQT_ROOT, root_cbf);
+    return root_cbf;
 }
 
-// Split tree: child k's cbf_cb / cbf_cr (when the parent's is set) and cbf_luma, then
-// cu_qp_delta when k is the first child with a coded TU.
+// One 16x16 transform node of unit c at depth d (0: a CU16's tree, 1: a quadrant of a CU32's),
+// up to its children / residual: split_transform_flag (while d < depth_inter = max_transform_
+// hierarchy_depth_inter; intra depth 0), chroma cbf (coded at depth 0, else when the parent's is
+// set; context = depth), and for an unsplit node cbf_luma (inferred 1 for an inter node at depth 0
+// without chroma; context 1 at depth 0) and cu_qp_delta when a level is coded and the CU's delta is
+// still pending.
+template <class E, class Ctx>
+MXHD void code_node16(E& e, Ctx& ctx, const CuInfo& c, int d, int pcb, int pcr, int depth_inter, bool qp_pending,
+                      int qp_pred) {
+    const bool intra = c.type == kCuIntra;
+    const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
+    const bool split = !intra && c.tu_split == 2;
+    if (!intra && d < depth_inter) e.bin(ctx, C_SPLIT_TRANSFORM + 1, split);  // ctxInc 5 - log2(16)
+    if (d == 0 || pcb) e.bin(ctx, C_CBF_CHROMA + d, cb);
+    if (d == 0 || pcr) e.bin(ctx, C_CBF_CHROMA + d, cr);
+    if (split) return;
+    if (intra || d > 0 || cb || cr) e.bin(ctx, C_CBF_LUMA + (d == 0 ? 1 : 0), cy);
+    if (c.cbf && qp_pending) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_pred));
+}
+
+// Split tree: the first 8x8 child with a coded TU (its transform unit carries cu_qp_delta)
 MXHD int split_first_coded_child(const CuInfo& c) {
     for (int k = 0; k < 4; ++k)
         if (((c.cbf_y4 >> k) & 1) | ((c.cbf_c4 >> k) & 1) | ((c.cbf_c4 >> (4 + k)) & 1)) return k;
     return 4;
 }
+// 8x8 child k (depth d + 1) of a split 16x16 node at depth d; its chroma TUs are 4x4 at this node:
+// split_transform_flag (0: no 4x4 luma TUs) while d + 1 < depth_inter, chroma cbf when the
+// parent's is set, cbf_luma (context 0), cu_qp_delta at the first coded child while pending.
 template <class E, class Ctx>
-MXHD void code_child_head(E& e, Ctx& ctx, const CuInfo& c, int k, int qp_prev) {
+MXHD void code_child8(E& e, Ctx& ctx, const CuInfo& c, int k, int d, int depth_inter, bool qp_pending, int qp_pred) {
     const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1;
     const int yk = (c.cbf_y4 >> k) & 1, cbk = (c.cbf_c4 >> k) & 1, crk = (c.cbf_c4 >> (4 + k)) & 1;
-    if (cb) e.bin(ctx, C_CBF_CHROMA + 1, cbk);
-    if (cr) e.bin(ctx, C_CBF_CHROMA + 1, crk);
+    if (d + 1 < depth_inter) e.bin(ctx, C_SPLIT_TRANSFORM + 2, 0);  // ctxInc 5 - log2(8)
+    if (cb) e.bin(ctx, C_CBF_CHROMA + d + 1, cbk);
+    if (cr) e.bin(ctx, C_CBF_CHROMA + d + 1, crk);
     e.bin(ctx, C_CBF_LUMA + 0, yk);
-    if (k == split_first_coded_child(c)) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_prev));
+    if (qp_pending && k == split_first_coded_child(c)) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_pred));
 }
 // Whether TU t (0 Y, 1 Cb, 2 Cr) of split child k is coded, and its first CU sub-block.
 MXHD bool split_tu_coded(const CuInfo& c, int k, int t) {
     return t == 0 ? ((c.cbf_y4 >> k) & 1) : ((c.cbf_c4 >> (t == 1 ? k : 4 + k)) & 1);
 }
 MXHD int split_tu_sb0(int k, int t) { return t == 0 ? 4 * k : (t == 1 ? 16 + k : 20 + k); }
-// TU descriptor of a split child's TU / an unsplit CU's TU
+// TU descriptor of a split child's TU / an unsplit unit's TU
 template <class Cf>
 MXHD TuDesc split_tu_desc(const Cf& cf, int k, int t) {
     TuDesc d;
@@ -1150,33 +1238,127 @@ MXHD TuDesc flat_tu_desc(const CuInfo& c, int t) {
     d.csbf_mask = t == 0 ? c.csbf_y : (t == 1 ? c.csbf_c[0] : c.csbf_c[1]);
     return d;
 }
-// QP predictor of the next CU: c.qp when c coded cu_qp_delta
-MXHD int cu_next_qp_prev(const CuInfo& c, int qp_prev) {
-    return (cu_residual_kind(c) != kResNone && c.cbf) ? (int)c.qp : qp_prev;
+
+// Everything the syntax of one unit needs beyond its own CuInfo and levels (unit_syn builds it).
+struct UnitSyn {
+    bool islice;
+    bool ctb_first;    // z == 0: sao() and the CTB's split_cu_flag precede the unit
+    bool split_coded;  // the CTB lies inside the picture (else split_cu_flag is inferred 1)
+    int split_inc;     // split_cu_flag ctxInc at depth 0
+    bool cu32;         // the CTB is one CU32
+    bool root;         // a transform tree follows the CU's prediction syntax
+    int cb0, cr0;      // CU32: depth-0 chroma cbf (OR over the units)
+    bool qp_pending;   // the CU has not sent cu_qp_delta before this unit
+    int qp_pred;       // qPY_PRED of the CU's quantization group (slice_qp_chain)
+    CuNb nb;           // neighbours of the CU origin (a CU32: its first unit)
+    CuInfo head;       // CU32: prediction info of the first unit with cbf = OR over the units
+    bool last_unit;    // the CTB's last unit inside the picture: end_of_slice_segment_flag follows
+    bool eos;          // ... equal to 1 (the slice's last CTB)
+    bool end_subset;   // WPP: end_of_subset_one_bit (the last CTB of a CTB row, not of the slice)
+    int depth_inter;   // max_transform_hierarchy_depth_inter
+    bool sao_on, has_l, has_u;
+    uint32_t sao[3], sao_l[3], sao_u[3];
+};
+
+// Build the syntax context of unit (x, y) of a slice of CTBs [first_ctb, end_ctb).  get(u): CuInfo
+// of raster unit u; sao: 4 words per CTB (nullptr: SAO off); qp_pred: the unit's QP predictor.
+template <class Get>
+MXHD UnitSyn unit_syn(const Get& get, const uint32_t* sao, int x, int y, int mb_w, int mb_h, bool islice,
+                      int first_ctb, int end_ctb, bool wpp, int depth_inter, int qp_pred) {
+    UnitSyn u;
+    const int cw = ctb_cols(mb_w);
+    const int c = ctb_of(x, y, cw), z = ((y & 1) << 1) | (x & 1);
+    const int x0 = x & ~1, y0 = y & ~1;
+    const CuInfo me = get(y * mb_w + x);
+    u.islice = islice;
+    u.ctb_first = z == 0;
+    u.split_coded = ctb_whole(c, cw, mb_w, mb_h);
+    u.cu32 = me.ct == 0;
+    u.depth_inter = depth_inter;
+    u.qp_pred = qp_pred;
+    u.nb = cu_nb_at(get, u.cu32 ? x0 : x, u.cu32 ? y0 : y, mb_w, cw, first_ctb);
+    u.split_inc = 0;
+    if (x0 > 0 && c - 1 >= first_ctb) u.split_inc += get(y0 * mb_w + x0 - 1).ct > 0 ? 1 : 0;
+    if (y0 > 0 && c - cw >= first_ctb) u.split_inc += get((y0 - 1) * mb_w + x0).ct > 0 ? 1 : 0;
+    u.qp_pending = true;
+    u.cb0 = u.cr0 = 0;
+    if (u.cu32) {
+        u.head = get(y0 * mb_w + x0);
+        uint32_t any = 0;
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t cb = get((y0 + (q >> 1)) * mb_w + x0 + (q & 1)).cbf;
+            any |= cb;
+            if (q < z && cb) u.qp_pending = false;
+        }
+        u.head.cbf = (uint8_t)any;
+        u.cb0 = (int)((any >> 1) & 1);
+        u.cr0 = (int)((any >> 2) & 1);
+        u.root = u.head.type == kCuMerge || (u.head.type == kCuAmvp && any != 0) || u.head.type == kCuIntra;
+    } else {
+        u.head = me;
+        u.root = me.type == kCuIntra || me.type == kCuMerge || (me.type == kCuAmvp && me.cbf != 0);
+    }
+    const int lz = ctb_last_z(c, cw, mb_w, mb_h);
+    u.last_unit = z == lz;
+    u.eos = c == end_ctb - 1;
+    u.end_subset = wpp && !u.eos && (c % cw) == cw - 1;
+    u.sao_on = sao != nullptr;
+    u.has_l = (c % cw) > 0 && c - 1 >= first_ctb;
+    u.has_u = c - cw >= first_ctb;
+    for (int k = 0; k < 3; ++k) {
+        u.sao[k] = sao ? sao[4 * (size_t)c + k] : 0u;
+        u.sao_l[k] = (sao && u.has_l) ? sao[4 * (size_t)(c - 1) + k] : 0u;
+        u.sao_u[k] = (sao && u.has_u) ? sao[4 * (size_t)(c - cw) + k] : 0u;
+    }
+    return u;
 }
 
-// The whole CU: head, residual TUs, end_of_slice_segment_flag.
-template <class E, class Ctx, class Cf>
-MXHD void code_cu(E& e, Ctx& ctx, bool islice, const CuInfo& c, const Cf& cf, CuNb nb, int& qp_prev,
-                  bool end_of_slice) {
-    code_cu_head(e, ctx, islice, c, nb, qp_prev);
-    const int kind = cu_residual_kind(c);
-    if (kind == kResSplit) {
-#pragma unroll 1
-        for (int k = 0; k < 4; ++k) {
-            code_child_head(e, ctx, c, k, qp_prev);
-#pragma unroll 1
-            for (int t = 0; t < 3; ++t)
-                if (split_tu_coded(c, k, t)) code_residual(e, ctx, cf, split_tu_desc(cf, k, t));
-        }
-    } else if (kind == kResFlat) {
-        // one call site for the three TUs keeps the (inlined) device code small
-#pragma unroll 1
-        for (int t = 0; t < 3; ++t)
-            if ((c.cbf >> t) & 1) code_residual(e, ctx, cf, flat_tu_desc(c, t));
+// How a unit's residual is laid out after its head part (code_unit_head): none, one transform
+// unit per component, or the split tree (four 8x8 children, each with its own flags).
+enum CuResidual { kResNone = 0, kResFlat = 1, kResSplit = 2 };
+MXHD int unit_res_kind(const CuInfo& c, const UnitSyn& u) {
+    if (!u.root) return kResNone;
+    if (c.type != kCuIntra && c.tu_split == 2) return kResSplit;
+    return c.cbf ? kResFlat : kResNone;
+}
+
+// The unit's syntax before its split children / residual: [first unit of a CTB: sao() and
+// split_cu_flag], then a CU32's prediction syntax and depth-0 chroma cbf (first unit) and the
+// unit's depth-1 node, or a CU16's prediction syntax and depth-0 node.
+template <class E, class Ctx>
+MXHD void code_unit_head(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u) {
+    if (u.ctb_first) {
+        if (u.sao_on)
+            code_sao_w(e, ctx, u.sao[0], u.sao[1], u.sao[2], u.has_l, u.sao_l[0], u.sao_l[1], u.sao_l[2], u.has_u,
+                       u.sao_u[0], u.sao_u[1], u.sao_u[2]);
+        if (u.split_coded) e.bin(ctx, C_SPLIT_CU + u.split_inc, u.cu32 ? 0 : 1);
     }
-    qp_prev = cu_next_qp_prev(c, qp_prev);
-    e.terminate(end_of_slice ? 1 : 0);
+    if (u.cu32) {
+        if (u.ctb_first) {
+            code_pred_head(e, ctx, u.islice, u.head, u.nb, u.head.cbf != 0, kCtbLog2);
+            if (u.root) {
+                e.bin(ctx, C_CBF_CHROMA + 0, u.cb0);
+                e.bin(ctx, C_CBF_CHROMA + 0, u.cr0);
+            }
+        }
+        if (u.root) code_node16(e, ctx, c, 1, u.cb0, u.cr0, u.depth_inter, u.qp_pending, u.qp_pred);
+        return;
+    }
+    // a CU16 (no split_cu_flag at depth 1 while the minimum CU is 16x16)
+    if (code_pred_head(e, ctx, u.islice, c, u.nb, c.cbf != 0, kMinCbLog2))
+        code_node16(e, ctx, c, 0, 0, 0, u.depth_inter, true, u.qp_pred);
+}
+// split child k's head at the unit's tree depth
+template <class E, class Ctx>
+MXHD void code_unit_child(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, int k) {
+    code_child8(e, ctx, c, k, u.cu32 ? 1 : 0, u.depth_inter, u.qp_pending, u.qp_pred);
+}
+// end_of_slice_segment_flag after the CTB's last unit (+ end_of_subset_one_bit with WPP)
+template <class E>
+MXHD void code_unit_end(E& e, const UnitSyn& u) {
+    if (!u.last_unit) return;
+    e.terminate(u.eos ? 1 : 0);
+    if (u.end_subset) e.terminate(1);
 }
 
 // ---------------------------------------------------------------- sample adaptive offset (8.7.3)
@@ -1218,17 +1400,17 @@ struct SaoStats {
     int32_t bo_cnt[32];
 };
 
-// Statistics of the n x n block at (x0, y0) of a W x H plane: rec / src at (x, y) are
+// Statistics of the nw x nh block at (x0, y0) of a W x H plane: rec / src at (x, y) are
 // p[y * pitch + x * step] (step 2: one component of interleaved chroma).  Samples whose
 // neighbour lies outside the picture are not modified by an edge class (8.7.3.2) and are left
 // out of its statistics.
 MXHD void sao_stats_block(const uint8_t* rec, int rpitch, const uint8_t* src, int spitch, int step, int x0, int y0,
-                          int n, int W, int H, SaoStats& st) {
+                          int nw, int nh, int W, int H, SaoStats& st) {
     for (int k = 0; k < 4; ++k)
         for (int c = 0; c < 4; ++c) st.eo_sum[k][c] = st.eo_cnt[k][c] = 0;
     for (int b = 0; b < 32; ++b) st.bo_sum[b] = st.bo_cnt[b] = 0;
-    for (int y = y0; y < y0 + n; ++y)
-        for (int x = x0; x < x0 + n; ++x) {
+    for (int y = y0; y < y0 + nh; ++y)
+        for (int x = x0; x < x0 + nw; ++x) {
             const int c = rec[y * rpitch + x * step];
             const int d = (int)src[y * spitch + x * step] - c;
             st.bo_sum[c >> 3] += d;
@@ -1361,15 +1543,16 @@ MXHD int sao_sample(uint32_t w, int c, int a, int b) {
 // its samples (SAO off) without gathering statistics.  Its prediction came from a picture SAO
 // already corrected (static or rigidly moving content: most of a desktop), so a second offset pass
 // finds ~nothing, and the statistics pass is the bulk of k_hevc_sao's time.
-MXHD bool sao_keep_ctb(bool idr, const CuInfo& c) { return !idr && c.cbf == 0; }
+// (A CTB of several units keeps its samples when none of them coded a level.)
+MXHD bool sao_keep_ctb(bool idr, uint32_t cbf_any) { return !idr && cbf_any == 0; }
 
-// Apply w to the n x n block at (x0, y0): reads the deblocked plane rec, writes out (a different
+// Apply w to the nw x nh block at (x0, y0): reads the deblocked plane rec, writes out (a different
 // buffer: every CTB reads its neighbours' deblocked samples).
-MXHD void sao_apply_block(const uint8_t* rec, uint8_t* out, int pitch, int step, int x0, int y0, int n, int W, int H,
-                          uint32_t w) {
+MXHD void sao_apply_block(const uint8_t* rec, uint8_t* out, int pitch, int step, int x0, int y0, int nw, int nh, int W,
+                          int H, uint32_t w) {
     const int k = sao_eo(w);
-    for (int y = y0; y < y0 + n; ++y)
-        for (int x = x0; x < x0 + n; ++x) {
+    for (int y = y0; y < y0 + nh; ++y)
+        for (int x = x0; x < x0 + nw; ++x) {
             const int ax = x + kSaoDx[k][0], ay = y + kSaoDy[k][0], bx = x + kSaoDx[k][1], by = y + kSaoDy[k][1];
             const bool in = ax >= 0 && ay >= 0 && bx >= 0 && by >= 0 && ax < W && bx < W && ay < H && by < H;
             const int a = in ? rec[ay * pitch + ax * step] : -1, b = in ? rec[by * pitch + bx * step] : -1;
@@ -1494,11 +1677,13 @@ MXHD void code_token(CabacEnc& e, Ctx& ctx, uint32_t t) {
         e.bin(ctx, (int)(t >> 1), (int)(t & 1u));
 }
 
-// A CTU's token stream is the concatenation of independent *parts* in coding order: the head
-// (SAO + code_cu_head), per split child its cbf / cu_qp_delta head, per TU its last position and
-// its sub-blocks (last to DC), and the end_of_slice_segment_flag.  Each part depends only on
-// the CTU's data, so the GPU binarises one part per lane (k_hevc_bins); the CPU walks them in
-// order.  At most 1 + 4 + 12 + 24 + 1 = 42 parts; a part is at most kPartTokens tokens.
+// A unit's token stream is the concatenation of independent *parts* in coding order: the head
+// (code_unit_head: sao() and split_cu_flag on a CTB's first unit, the prediction syntax, the
+// 16x16 transform node), per split child its flags / cu_qp_delta, per TU its last position and
+// its sub-blocks (last to DC), and on the CTB's last unit the end_of_slice_segment_flag.  Each part
+// depends only on the unit, its neighbours' descriptors and UnitSyn, so the GPU binarises one
+// part per lane (k_hevc_bins); the CPU walks them in order.  At most 1 + 4 + 12 + 24 + 1 = 42
+// parts; a part is at most kPartTokens tokens.
 enum PartKind { kPartHead = 0, kPartChild = 1, kPartTuLast = 2, kPartSb = 3, kPartEnd = 4 };
 struct CtuPart {
     int kind, k, t, i;  // split child, component TU, sub-block index within the TU
@@ -1507,15 +1692,15 @@ struct CtuPart {
 constexpr int kMaxCtuParts = 42;
 constexpr uint32_t kPartTokens = 112;
 
-// Calls f(part) for every part of CU c in coding order; returns the number of parts.
+// Calls f(part, index) for every part of unit c in coding order; returns the number of parts.
 template <class Cf, class F>
-MXHD int for_each_part(const CuInfo& c, const Cf& cf, F f) {
+MXHD int for_each_part(const CuInfo& c, const UnitSyn& u, const Cf& cf, F f) {
     int n = 0;
     CtuPart pt;
     pt.kind = kPartHead;
     pt.k = pt.t = pt.i = 0;
     f(pt, n++);
-    const int kind = cu_residual_kind(c);
+    const int kind = unit_res_kind(c, u);
 #pragma unroll 1
     for (int k = 0; k < (kind == kResSplit ? 4 : 1); ++k) {
         if (kind == kResNone) break;
@@ -1541,31 +1726,22 @@ MXHD int for_each_part(const CuInfo& c, const Cf& cf, F f) {
             }
         }
     }
-    pt.kind = kPartEnd;
-    f(pt, n++);
+    if (u.last_unit) {
+        pt.kind = kPartEnd;
+        f(pt, n++);
+    }
     return n;
 }
 
-// Binarise one part of CTU i (the k-th of a slice of `count` CTUs; qp_prev: its QP predictor).
-// wpp: entropy_coding_sync_enabled_flag -- a CTU row's last CTU (not the slice's last) ends its
-// substream with end_of_subset_one_bit after end_of_slice_segment_flag (7.3.8.1).
-template <class E, class Cf>
-MXHD void binarise_part(E& rec, const CtuPart& pt, bool islice, const CuInfo* cus, const Cf& cf,
-                        const uint32_t* sao, int i, int k, int count, int ctb_w, int qp_prev, bool wpp = false) {
-    NoCtx nc;
-    const CuInfo& c = cus[i];
+// Binarise one part of unit c (E: BinRec with NoCtx, or the arithmetic coder with ArrCtx).
+template <class E, class Ctx, class Cf>
+MXHD void binarise_part(E& rec, Ctx& ctx, const CtuPart& pt, const CuInfo& c, const UnitSyn& u, const Cf& cf) {
     if (pt.kind == kPartHead) {
-        const int x = i % ctb_w;
-        const bool has_l = x > 0 && k > 0, has_u = k >= ctb_w;
-        if (sao)
-            code_sao(rec, nc, sao + 4 * (size_t)i, has_l ? sao + 4 * (size_t)(i - 1) : nullptr,
-                     has_u ? sao + 4 * (size_t)(i - ctb_w) : nullptr);
-        code_cu_head(rec, nc, islice, c, cu_nb(has_l ? &cus[i - 1] : nullptr, has_u ? &cus[i - ctb_w] : nullptr),
-                     qp_prev);
+        code_unit_head(rec, ctx, c, u);
     } else if (pt.kind == kPartChild) {
-        code_child_head(rec, nc, c, pt.k, qp_prev);
+        code_unit_child(rec, ctx, c, u, pt.k);
     } else if (pt.kind == kPartTuLast) {
-        code_tu_last(rec, nc, pt.d);
+        code_tu_last(rec, ctx, pt.d);
     } else if (pt.kind == kPartSb) {
         // the previous sub-block with levels in this TU (coding order: higher scan index)
         const int last_sb = pt.d.last_idx >> 4;
@@ -1577,73 +1753,86 @@ MXHD void binarise_part(E& rec, const CtuPart& pt, bool islice, const CuInfo* cu
             prev_gt1 = sb_any_gt1(cf, pt.d.sb0 + j, sg) ? 1 : 0;
             break;
         }
-        code_sub_block(rec, nc, cf, pt.d, tu_csbf_raster(pt.d), pt.i, prev_gt1);
+        code_sub_block(rec, ctx, cf, pt.d, tu_csbf_raster(pt.d), pt.i, prev_gt1);
     } else {
-        const bool eos = k == count - 1;
-        rec.terminate(eos ? 1 : 0);
-        if (wpp && !eos && (i + 1) % ctb_w == 0) rec.terminate(1);  // end_of_subset_one_bit
+        code_unit_end(rec, u);
     }
     rec.flush();
 }
-// WPP (8.6.1): the QP predictor restarts from the slice QP at the first quantization group of
-// every CTU row; without WPP only at the slice start.
-MXHD bool qp_prev_resets(int i, int k, int ctb_w, bool wpp) { return k == 0 || (wpp && i % ctb_w == 0); }
 
-// Binarise CTU i (the k-th of a slice of `count` CTUs) part by part.  qp_prev: QP predictor
-// (QpY of the previous CU that coded a residual in the slice, else the slice QP); updated as
-// code_cu does.  Returns the token count (> rec.cap: truncated).
-MXHD uint32_t binarise_ctu(BinRec& rec, bool islice, const CuInfo* cus, const int16_t* coef, const uint32_t* sao,
-                           int i, int k, int count, int ctb_w, int& qp_prev, bool wpp = false) {
-    const CoefArray cf{coef + (size_t)i * kCoefPerCu};
-    const int qp_in = qp_prev;
-    for_each_part(cus[i], cf, [&](const CtuPart& pt, int) {
-        binarise_part(rec, pt, islice, cus, cf, sao, i, k, count, ctb_w, qp_in, wpp);
-    });
-    qp_prev = cu_next_qp_prev(cus[i], qp_prev);
-    return rec.n;
+// A unit coded straight through the syntax coders (the residual coder walks each TU in one
+// pass): the reference the part-wise token path is tested against.
+template <class E, class Ctx, class Cf>
+MXHD void code_unit_direct(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, const Cf& cf) {
+    code_unit_head(e, ctx, c, u);
+    const int kind = unit_res_kind(c, u);
+    if (kind == kResSplit) {
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            code_unit_child(e, ctx, c, u, k);
+#pragma unroll 1
+            for (int t = 0; t < 3; ++t)
+                if (split_tu_coded(c, k, t)) code_residual(e, ctx, cf, split_tu_desc(cf, k, t));
+        }
+    } else if (kind == kResFlat) {
+#pragma unroll 1
+        for (int t = 0; t < 3; ++t)
+            if ((c.cbf >> t) & 1) code_residual(e, ctx, cf, flat_tu_desc(c, t));
+    }
+    code_unit_end(e, u);
 }
 
-// Entropy-code one slice of CTUs [first, first + count) (raster order, ctb_w CTUs per row)
-// through the token path (binarise every CTU, then run the tokens through the coder -- what
-// the GPU kernels do).  tok: scratch of kMaxCuTokens tokens.  Returns the payload bytes.
-MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
-                         int first, int count, int ctb_w, uint8_t* ctx_mem, const uint32_t* sao, uint16_t* tok) {
-    ctx_init_all(ctx_mem, islice ? 0 : 1, slice_qp);
-    ArrCtx ctx{ctx_mem};
-    CabacEnc e;
-    e.start(out, cap);
-    int qp_prev = slice_qp;
-    for (int k = 0; k < count; ++k) {
+// What the entropy coder reads of a picture: raster CuInfo / levels per unit, the QP predictor per
+// unit (slice_qp_chain), SAO words per CTB (nullptr: off).
+struct PicSyn {
+    const CuInfo* cus;
+    const int16_t* coef;
+    const uint8_t* qp_pred;
+    const uint32_t* sao;
+    int mb_w, mb_h;
+    int depth_inter;  // max_transform_hierarchy_depth_inter
+};
+struct ArrGet {  // raster CuInfo lookup for unit_syn
+    const CuInfo* p;
+    MXHD const CuInfo& operator()(int u) const { return p[u]; }
+};
+MXHD UnitSyn pic_unit_syn(const PicSyn& ps, int x, int y, bool islice, int first, int end, bool wpp) {
+    return unit_syn(ArrGet{ps.cus}, ps.sao, x, y, ps.mb_w, ps.mb_h, islice, first, end, wpp, ps.depth_inter,
+                    ps.qp_pred[y * ps.mb_w + x]);
+}
+
+// Entropy-code CTB c of the slice [first, end) into e: every unit inside the picture, in z order,
+// through the token path (binarise, then the tokens through the coder -- what the GPU does) or
+// directly (direct = true).
+MXHD void code_ctb(CabacEnc& e, ArrCtx& ctx, const PicSyn& ps, bool islice, int c, int first, int end, bool wpp,
+                   uint16_t* tok, bool direct) {
+    const int cw = ctb_cols(ps.mb_w);
+    for (int z = 0; z < 4; ++z) {
+        const int x = 2 * (c % cw) + (z & 1), y = 2 * (c / cw) + (z >> 1);
+        if (x >= ps.mb_w || y >= ps.mb_h) continue;
+        const int i = y * ps.mb_w + x;
+        const UnitSyn u = pic_unit_syn(ps, x, y, islice, first, end, wpp);
+        const CoefArray cf{ps.coef + (size_t)i * kCoefPerCu};
+        if (direct) {
+            code_unit_direct(e, ctx, ps.cus[i], u, cf);
+            continue;
+        }
         BinRec rec;
         rec.start(tok, kMaxCuTokens);
-        const uint32_t n = binarise_ctu(rec, islice, cus, coef, sao, first + k, k, count, ctb_w, qp_prev);
-        for (uint32_t j = 0; j < n && j < kMaxCuTokens; ++j) code_token(e, ctx, tok[j]);
+        NoCtx nc;
+        for_each_part(ps.cus[i], u, cf, [&](const CtuPart& pt, int) { binarise_part(rec, nc, pt, ps.cus[i], u, cf); });
+        for (uint32_t j = 0; j < rec.n && j < kMaxCuTokens; ++j) code_token(e, ctx, tok[j]);
     }
-    e.finish_slice();
-    return e.pos;
 }
 
-// The same slice coded directly (syntax coders driving the arithmetic coder, no tokens): the
-// reference the token path is tested against.
-MXHD uint32_t code_slice_direct(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus,
-                                const int16_t* coef, int first, int count, int ctb_w, uint8_t* ctx_mem,
-                                const uint32_t* sao = nullptr) {
+// Entropy-code the slice of CTBs [first, end) (one substream).  Returns the payload bytes.
+MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const PicSyn& ps, int first, int end,
+                         uint8_t* ctx_mem, uint16_t* tok, bool direct = false) {
     ctx_init_all(ctx_mem, islice ? 0 : 1, slice_qp);
     ArrCtx ctx{ctx_mem};
     CabacEnc e;
     e.start(out, cap);
-    int qp_prev = slice_qp;
-    for (int k = 0; k < count; ++k) {
-        const int i = first + k;
-        const int x = i % ctb_w;
-        const CuInfo* left = (x > 0 && k > 0) ? &cus[i - 1] : nullptr;
-        const CuInfo* above = (k >= ctb_w) ? &cus[i - ctb_w] : nullptr;
-        const CoefArray cf{coef + (size_t)i * kCoefPerCu};
-        if (sao)  // sao parameters: 4 words per CTB (luma, Cb, Cr, unused)
-            code_sao(e, ctx, sao + 4 * (size_t)i, (x > 0 && k > 0) ? sao + 4 * (size_t)(i - 1) : nullptr,
-                     k >= ctb_w ? sao + 4 * (size_t)(i - ctb_w) : nullptr);
-        code_cu(e, ctx, islice, cus[i], cf, cu_nb(left, above), qp_prev, k == count - 1);
-    }
+    for (int c = first; c < end; ++c) code_ctb(e, ctx, ps, islice, c, first, end, false, tok, direct);
     e.finish_slice();
     return e.pos;
 }
@@ -1654,10 +1843,10 @@ MXHD uint32_t code_slice_direct(uint8_t* out, uint32_t cap, bool islice, int sli
 // up-right) and the near-vertical 22 -- UI edges, text strokes and rotated / natural content
 constexpr int kNumIntraCands = 8;
 constexpr uint8_t kIntraCands[kNumIntraCands] = {1, 0, 26, 10, 18, 2, 34, 22};
-// Approximate luma mode signalling cost in bins given the left neighbour's MPM candidate.
-MXHD int intra_mode_bits(int mode, int cand_a) {
+// Approximate luma mode signalling cost in bins given the MPM candidates of the left / above PU.
+MXHD int intra_mode_bits(int mode, int cand_a, int cand_b) {
     int l[3];
-    mpm_list(cand_a, 1, l);
+    mpm_list(cand_a, cand_b, l);
     if (mode == l[0]) return 2;
     if (mode == l[1] || mode == l[2]) return 3;
     return 6;
@@ -1828,44 +2017,49 @@ MXHD uint32_t cu_bits_est(const int16_t* co, bool split) {
     return b;
 }
 
-// Spatial neighbour motion of a 16x16 PU (every CU of a P slice is inter, so "available"
-// means inside the picture, inside the slice and already coded).  A0 (below-left) is
-// never available: it lies in the next CTU row.
+// Spatial neighbour motion of a PU (every CU of a P slice is inter, so "available" means inside
+// the picture, inside the slice and earlier in decoding order).
 struct MvCand {
     bool avail;
     int x, y;
 };
+// The five spatial neighbours (8.5.3.2.2 / 8.5.3.2.7) of a PU.
+struct PuNb {
+    MvCand a1, b1, b0, a0, b2;
+};
 
 // Merge candidate list (8.5.3.2.2-8.5.3.2.4, MaxNumMergeCand kMaxMergeCand, no TMVP, one
-// reference picture): A1, B1 (unless equal to A1), B0 (unless equal to B1), A0 (never
-// available: the next CTU row), B2 (unless equal to A1 or B1, and only while fewer than four),
-// then zero candidates.
+// reference picture): A1, B1 (unless equal to A1), B0 (unless equal to B1), A0 (unless equal to
+// A1), B2 (unless equal to A1 or B1, and only while fewer than four), then zero candidates.
 MXHD bool mv_eq(MvCand a, MvCand b) { return a.x == b.x && a.y == b.y; }
 // Index of vector (mx, my) in the merge list (the first matching entry), -1 if absent.  Walks the
 // list without materialising it (no dynamically indexed array: registers only on the GPU).
-MXHD int merge_index_of(MvCand a1, MvCand b1, MvCand b0, MvCand b2, int mx, int my) {
+MXHD int merge_index_of(const PuNb& nb, int mx, int my) {
     int n = 0, found = -1;
     auto add = [&](MvCand c) {
         if (found < 0 && c.x == mx && c.y == my) found = n;
         ++n;
     };
-    if (a1.avail) add(a1);
-    if (b1.avail && !(a1.avail && mv_eq(b1, a1))) add(b1);
-    if (b0.avail && !(b1.avail && mv_eq(b0, b1))) add(b0);
-    if (b2.avail && n < 4 && !(a1.avail && mv_eq(b2, a1)) && !(b1.avail && mv_eq(b2, b1))) add(b2);
+    if (nb.a1.avail) add(nb.a1);
+    if (nb.b1.avail && !(nb.a1.avail && mv_eq(nb.b1, nb.a1))) add(nb.b1);
+    if (nb.b0.avail && !(nb.b1.avail && mv_eq(nb.b0, nb.b1))) add(nb.b0);
+    if (nb.a0.avail && !(nb.a1.avail && mv_eq(nb.a0, nb.a1))) add(nb.a0);
+    if (nb.b2.avail && n < 4 && !(nb.a1.avail && mv_eq(nb.b2, nb.a1)) && !(nb.b1.avail && mv_eq(nb.b2, nb.b1)))
+        add(nb.b2);
     while (n < kMaxMergeCand) add(MvCand{true, 0, 0});
     return found;
 }
 
-// AMVP list (8.5.3.2.6/7, one reference picture so no scaling): A = A1; B = first of
+// AMVP list (8.5.3.2.6/7, one reference picture so no scaling): A = A0, else A1; B = the first of
 // B0, B1, B2; without A the B vector moves into A; duplicates removed; zero padding.
-MXHD void amvp_list(MvCand a1, MvCand b1, MvCand b0, MvCand b2, int* lx, int* ly) {
-    const MvCand b = b0.avail ? b0 : (b1.avail ? b1 : b2);
+MXHD void amvp_list(const PuNb& nb, int* lx, int* ly) {
+    const MvCand a = nb.a0.avail ? nb.a0 : nb.a1;
+    const MvCand b = nb.b0.avail ? nb.b0 : (nb.b1.avail ? nb.b1 : nb.b2);
     lx[1] = ly[1] = 0;
-    if (a1.avail) {
-        lx[0] = a1.x;
-        ly[0] = a1.y;
-        if (b.avail && (b.x != a1.x || b.y != a1.y)) {
+    if (a.avail) {
+        lx[0] = a.x;
+        ly[0] = a.y;
+        if (b.avail && (b.x != a.x || b.y != a.y)) {
             lx[1] = b.x;
             ly[1] = b.y;
         }
@@ -1893,10 +2087,10 @@ MXHD int mvd_cost_bits(int d) {
 // Fill type / mvp / mvd of an inter CU (c.mvx/mvy/cbf set) from its neighbours' motion.
 // Merge / skip when the CU's vector is in the merge list (mvp_idx then holds merge_idx: the
 // first matching entry, the cheapest to signal), else AMVP with the cheaper predictor.
-MXHD void decide_inter(CuInfo& c, MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
+MXHD void decide_inter(CuInfo& c, const PuNb& nb) {
     c.mvp_idx = 0;
     c.mvdx = c.mvdy = 0;
-    const int k = merge_index_of(a1, b1, b0, b2, c.mvx, c.mvy);
+    const int k = merge_index_of(nb, c.mvx, c.mvy);
     if (k >= 0) {
         c.type = c.cbf ? kCuMerge : kCuSkip;
         c.mvp_idx = (uint8_t)k;
@@ -1904,7 +2098,7 @@ MXHD void decide_inter(CuInfo& c, MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
     }
     c.type = kCuAmvp;
     int lx[2], ly[2];
-    amvp_list(a1, b1, b0, b2, lx, ly);
+    amvp_list(nb, lx, ly);
     const int c0 = mvd_cost_bits(c.mvx - lx[0]) + mvd_cost_bits(c.mvy - ly[0]);
     const int c1 = mvd_cost_bits(c.mvx - lx[1]) + mvd_cost_bits(c.mvy - ly[1]);
     const int idx = c1 < c0 ? 1 : 0;
@@ -1913,24 +2107,63 @@ MXHD void decide_inter(CuInfo& c, MvCand a1, MvCand b1, MvCand b0, MvCand b2) {
     c.mvdy = (int16_t)(c.mvy - ly[idx]);
 }
 
-// Neighbour candidates of CU i = (x, y) in a picture of ctb_w CTUs whose slice starts at CU
-// `first` (slices are raster runs, so an earlier CU j is in the same slice iff j >= first);
-// mv: per-CU quarter-pel motion, (x, y) at mv[i*stride], mv[i*stride+1].
-MXHD void inter_neighbours(const int16_t* mv, int stride, int x, int y, int ctb_w, int first, MvCand* a1,
-                           MvCand* b1, MvCand* b0, MvCand* b2) {
-    const int i = y * ctb_w + x;
-    auto at = [&](bool ok, int j) {
-        MvCand c{ok, 0, 0};
-        if (ok) {
-            c.x = mv[(size_t)j * stride];
-            c.y = mv[(size_t)j * stride + 1];
-        }
+// Neighbours of the PU of n x n units (1: a CU16, 2: a CU32) at unit (x, y) of a picture of
+// mb_w x mb_h units whose slice starts at CTB first_ctb: A1 (x - 1, y + n - 1), B1 (x + n - 1,
+// y - 1), B0 (x + n, y - 1), A0 (x - 1, y + n), B2 (x - 1, y - 1), each available when inside the
+// picture, in the slice and earlier in decoding order (z order inside a CTB: e.g. the A0 of a CTB's
+// first unit lies in the left CTB and is available, the B0 of its last unit is not).  mv: per unit
+// quarter-pel motion, (x, y) at mv[u * stride], mv[u * stride + 1].
+MXHD PuNb pu_neighbours(const int16_t* mv, int stride, int x, int y, int n, int mb_w, int mb_h, int first_ctb) {
+    const int cw = ctb_cols(mb_w), cur = cpos_of(x, y, cw);
+    auto at = [&](int xn, int yn) {
+        MvCand c{false, 0, 0};
+        if (xn < 0 || yn < 0 || xn >= mb_w || yn >= mb_h) return c;
+        if (ctb_of(xn, yn, cw) < first_ctb || cpos_of(xn, yn, cw) >= cur) return c;
+        c.avail = true;
+        c.x = mv[(size_t)(yn * mb_w + xn) * stride];
+        c.y = mv[(size_t)(yn * mb_w + xn) * stride + 1];
         return c;
     };
-    *a1 = at(x > 0 && i - 1 >= first, i - 1);
-    *b1 = at(i - ctb_w >= first, i - ctb_w);
-    *b0 = at(x + 1 < ctb_w && i - ctb_w + 1 >= first, i - ctb_w + 1);
-    *b2 = at(x > 0 && i - ctb_w - 1 >= first, i - ctb_w - 1);
+    PuNb r;
+    r.a1 = at(x - 1, y + n - 1);
+    r.b1 = at(x + n - 1, y - 1);
+    r.b0 = at(x + n, y - 1);
+    r.a0 = at(x - 1, y + n);
+    r.b2 = at(x - 1, y - 1);
+    return r;
+}
+
+// Skip / merge / AMVP of the units of CTB (x0, y0) (u[z]: z-order copies, in[z]: inside the
+// picture) against the slice's neighbours, then the coding tree: the four units become one CU32
+// when all lie inside the picture with one vector and one QP, and the CU32's merge list holds the
+// vector (one skip / merge_idx instead of four) or its first unit needs AMVP anyway (one mvd).
+// Shared by both encoders (k_hevc_decide: one thread per CTB).
+MXHD void decide_ctb(CuInfo* u, const bool* in, const int16_t* mv, int stride, int x0, int y0, int mb_w, int mb_h,
+                     int first_ctb) {
+    for (int z = 0; z < 4; ++z) {
+        if (!in[z]) continue;
+        decide_inter(u[z], pu_neighbours(mv, stride, x0 + (z & 1), y0 + (z >> 1), 1, mb_w, mb_h, first_ctb));
+        u[z].ct = 1;
+    }
+    if (!(in[0] && in[1] && in[2] && in[3])) return;
+    uint32_t any = 0;
+    for (int z = 0; z < 4; ++z) {
+        if (u[z].mvx != u[0].mvx || u[z].mvy != u[0].mvy || u[z].qp != u[0].qp) return;
+        any |= u[z].cbf;
+    }
+    const PuNb nb = pu_neighbours(mv, stride, x0, y0, 2, mb_w, mb_h, first_ctb);
+    const int k = merge_index_of(nb, u[0].mvx, u[0].mvy);
+    if (k < 0 && u[0].type != kCuAmvp) return;
+    CuInfo h = u[0];
+    h.cbf = (uint8_t)any;
+    decide_inter(h, nb);
+    for (int z = 0; z < 4; ++z) {
+        u[z].type = h.type;
+        u[z].mvp_idx = h.mvp_idx;
+        u[z].mvdx = h.mvdx;
+        u[z].mvdy = h.mvdy;
+        u[z].ct = 0;
+    }
 }
 
 // ---------------------------------------------------------------- deblocking (8.7.2)
@@ -2019,16 +2252,43 @@ MXHD void db_chroma_lines(uint8_t* q0, int step, int line, int nlines, int qp_p,
     }
 }
 
-// QpY of every CU (8.6.1): the coded QP where residual was sent, else the prediction = the
-// previous CU's QpY in the slice (slice QP at its start).
-MXHD void slice_qpy(const CuInfo* cus, int first, int count, int slice_qp, uint8_t* qpy, int ctb_w = 1,
-                     bool wpp = false) {
+// QpY chain of the slice of CTBs [first, end) (8.6.1; quantization groups of 16x16 -- a CU16, or a
+// whole CU32): qPY_PRED of a group is the average of the QpY of its left and above groups when
+// those lie in the same CTB, else qPY_PREV (the QpY of the previous group in decoding order; the
+// slice QP at the slice start and, with WPP, at every CTB row start); a CU that sends cu_qp_delta
+// (one with a coded level) has QpY = its QP, any other QpY = qPY_PRED.  Writes qp_pred (the
+// entropy coder's delta base) and qpy (deblocking) per unit (raster).
+MXHD void slice_qp_chain(const CuInfo* cus, int mb_w, int mb_h, int first, int end, int slice_qp, bool wpp,
+                         uint8_t* qp_pred, uint8_t* qpy) {
+    const int cw = ctb_cols(mb_w);
     int prev = slice_qp;
-    for (int k = 0; k < count; ++k) {
-        if (wpp && (first + k) % ctb_w == 0) prev = slice_qp;  // WPP: the predictor restarts every CTU row
-        const CuInfo& c = cus[first + k];
-        if (c.type != kCuSkip && c.cbf) prev = c.qp;
-        qpy[first + k] = (uint8_t)prev;
+    for (int c = first; c < end; ++c) {
+        if (wpp && c % cw == 0) prev = slice_qp;
+        const int x0 = 2 * (c % cw), y0 = 2 * (c / cw);
+        if (cus[y0 * mb_w + x0].ct == 0) {  // CU32: one group, all four units inside
+            bool coded = false;
+            for (int z = 0; z < 4; ++z) coded |= cus[(y0 + (z >> 1)) * mb_w + x0 + (z & 1)].cbf != 0;
+            const int q = coded ? (int)cus[y0 * mb_w + x0].qp : prev;
+            for (int z = 0; z < 4; ++z) {
+                qp_pred[(y0 + (z >> 1)) * mb_w + x0 + (z & 1)] = (uint8_t)prev;
+                qpy[(y0 + (z >> 1)) * mb_w + x0 + (z & 1)] = (uint8_t)q;
+            }
+            prev = q;
+            continue;
+        }
+        for (int z = 0; z < 4; ++z) {
+            const int x = x0 + (z & 1), y = y0 + (z >> 1);
+            if (x >= mb_w || y >= mb_h) continue;
+            const int i = y * mb_w + x;
+            const int qa = (z & 1) ? (int)qpy[i - 1] : prev;
+            const int qb = (z & 2) ? (int)qpy[i - mb_w] : prev;
+            const int pred = (qa + qb + 1) >> 1;
+            const CuInfo& c = cus[i];
+            const int q = (c.type != kCuSkip && c.cbf) ? (int)c.qp : pred;
+            qp_pred[i] = (uint8_t)pred;
+            qpy[i] = (uint8_t)q;
+            prev = q;
+        }
     }
 }
 
@@ -2105,12 +2365,14 @@ MXHD void set_est_bytes(CuInfo& c, uint32_t bits) { c.est_bytes = c.cbf ? est_by
 constexpr uint32_t kCostPerSlice = 2048;  // EncoderConfig::hevc_slice_cost default
 // Largest cu_cost (last+1 <= 256 + 64 + 64, 16 + 4 + 4 sub-blocks, est_bytes <= 255).
 constexpr uint32_t kMaxCuCost = 1u + (384u >> 2) + 15u * 24u + ((21u * 255u) >> 3);
+// Slices are laid out in whole CTBs: the largest CTB cost (four units)
+constexpr uint32_t kMaxCtbCost = 4u * kMaxCuCost;
 // Number of slices for a P picture of total cost T, bounded by the level's slice limit.  At least
-// kMaxCuCost + 1 per slice: then consecutive thresholds ceil(s * T / S) lie further apart than any
+// kMaxCtbCost + 1 per slice: then consecutive thresholds ceil(s * T / S) lie further apart than any
 // CU's cost, no CU spans two of them, and plan_slice_of() is also a CU's slice rank (the GPU layout
 // places every CU from its own prefix).
 MXHD int plan_num_slices(uint64_t total, int max_slices, uint32_t cost_per_slice = kCostPerSlice) {
-    const uint32_t cps = cost_per_slice > kMaxCuCost ? cost_per_slice : kMaxCuCost + 1u;
+    const uint32_t cps = cost_per_slice > kMaxCtbCost ? cost_per_slice : kMaxCtbCost + 1u;
     const uint64_t s = total / cps;
     return s < 1 ? 1 : (s > (uint64_t)max_slices ? max_slices : (int)s);
 }

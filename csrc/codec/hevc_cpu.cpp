@@ -99,34 +99,38 @@ HevcCommon::HevcCommon(const EncoderConfig& c) : rc_(c) {
     level_ = pick_level(c.width, c.height, c.fps);
     const int maxs = max_slices_for_level(level_);
     slice_rows_ = 1;
-    while ((ctb_h() + slice_rows_ - 1) / slice_rows_ > maxs) ++slice_rows_;
+    while ((c32_h() + slice_rows_ - 1) / slice_rows_ > maxs) ++slice_rows_;
     if (num_slices() > kMaxSlices) throw std::invalid_argument("hevc: too many slices");
-    max_slices_ = std::min({maxs, kMaxSlices, ctb_w() * ctb_h()});
+    max_slices_ = std::min({maxs, kMaxSlices, num_ctbs()});
 }
 
 std::vector<int> HevcCommon::row_slices() const {
     std::vector<int> f;
-    for (int s = 0; s < num_slices(); ++s) f.push_back(s * slice_rows_ * ctb_w());
+    for (int s = 0; s < num_slices(); ++s) f.push_back(s * slice_rows_ * c32_w());
     return f;
 }
 
 std::vector<int> HevcCommon::plan_p_slices(const std::vector<CuInfo>& cus) const {
-    if (wpp()) {  // slices of wpp_rows() CTU rows, one substream per CTU row
+    if (wpp()) {  // slices of wpp_rows() CTB rows, one substream per CTB row
         std::vector<int> f;
-        for (int y = 0; y < ctb_h(); y += wpp_rows()) f.push_back(y * ctb_w());
+        for (int y = 0; y < c32_h(); y += wpp_rows()) f.push_back(y * c32_w());
         return f;
     }
+    // the cost of a CTB: the sum over its units
+    std::vector<uint32_t> cc((size_t)num_ctbs(), 0u);
+    for (int y = 0; y < ctb_h(); ++y)
+        for (int x = 0; x < ctb_w(); ++x) cc[(size_t)ctb_of(x, y, c32_w())] += cu_cost(cus[(size_t)(y * ctb_w() + x)]);
     uint64_t total = 0;
-    for (const auto& c : cus) total += cu_cost(c);
+    for (uint32_t v : cc) total += v;
     const int S = plan_num_slices(total, max_slices_, (uint32_t)rc_.config().hevc_slice_cost);
     std::vector<int> f;
     uint64_t pre = 0;
     int prev = -1;
-    for (size_t i = 0; i < cus.size(); ++i) {
+    for (size_t i = 0; i < cc.size(); ++i) {
         const int id = plan_slice_of(pre, total, S);
         if (id != prev) f.push_back((int)i);
         prev = id;
-        pre += cu_cost(cus[i]);
+        pre += cc[i];
     }
     return f;
 }
@@ -180,11 +184,11 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.ue(1);
         w.ue(0);
         w.ue(0);
-        w.ue(1);  // log2_min_luma_coding_block_size_minus3 (16)
-        w.ue(0);  // log2_diff_max_min_luma_coding_block_size (CTB 16)
+        w.ue(kMinCbLog2 - 3);          // log2_min_luma_coding_block_size_minus3 (16)
+        w.ue(kCtbLog2 - kMinCbLog2);   // log2_diff_max_min_luma_coding_block_size (CTB 32)
         w.ue(0);  // log2_min_luma_transform_block_size_minus2 (4)
-        w.ue(2);  // log2_diff_max_min_luma_transform_block_size (16)
-        w.ue(c.tu_split ? 1 : 0);  // max_transform_hierarchy_depth_inter
+        w.ue(kMaxTbLog2 - 2);  // log2_diff_max_min_luma_transform_block_size (16)
+        w.ue((uint32_t)depth_inter());  // max_transform_hierarchy_depth_inter
         w.ue(0);  // max_transform_hierarchy_depth_intra
         w.put(0, 1);  // scaling_list_enabled_flag
         w.put(0, 1);  // amp_enabled_flag
@@ -238,7 +242,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.put(0, 1);  // constrained_intra_pred_flag
         w.put(0, 1);  // transform_skip_enabled_flag
         w.put(1, 1);  // cu_qp_delta_enabled_flag
-        w.ue(0);      //   diff_cu_qp_delta_depth (one QP per 16x16 CU)
+        w.ue(kCtbLog2 - 4);  // diff_cu_qp_delta_depth: 16x16 quantization groups
         w.se(c.chroma_qp_offset);  // pps_cb_qp_offset
         w.se(c.chroma_qp_offset);  // pps_cr_qp_offset
         w.put(0, 1);  // pps_slice_chroma_qp_offsets_present_flag
@@ -269,7 +273,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
 void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp,
                                  const uint8_t* data, size_t n, const uint32_t* sub_len, int nsub,
                                  const uint32_t* sub_off) const {
-    const int ctbs = ctb_w() * ctb_h();
+    const int ctbs = num_ctbs();
     Bits w;
     w.put(addr == 0, 1);  // first_slice_segment_in_pic_flag
     if (idr) w.put(0, 1);  // no_output_of_prior_pics_flag
@@ -334,37 +338,31 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
     out.insert(out.end(), esc.begin(), esc.end());
 }
 
-uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
-                        int first, int count, int ctb_w, const uint32_t* sao, uint16_t* tok,
-                        std::vector<uint32_t>& sub_len) {
+uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const PicSyn& ps, int first, int end,
+                        uint16_t* tok, std::vector<uint32_t>& sub_len) {
     sub_len.clear();
+    const int cw = ctb_cols(ps.mb_w);
     uint8_t ctx[C_NUM], saved[C_NUM];
     bool have_saved = false;
     uint32_t pos = 0;
     CabacEnc e;
     ArrCtx cx{ctx};
-    int qp_prev = slice_qp;
-    for (int k = 0; k < count; ++k) {
-        const int i = first + k;
-        const int x = i % ctb_w;
-        if (k == 0 || x == 0) {  // a substream starts
-            if (k > 0 && have_saved && ctb_w >= 2)
-                std::memcpy(ctx, saved, C_NUM);  // sync from the row above after its second CTU (9.3.2.4)
+    for (int c = first; c < end; ++c) {
+        const int x = c % cw;
+        if (c == first || x == 0) {  // a substream starts
+            if (c > first && have_saved && cw >= 2)
+                std::memcpy(ctx, saved, C_NUM);  // sync from the row above after its second CTB (9.3.2.4)
             else
                 ctx_init_all(ctx, islice ? 0 : 1, slice_qp);
             have_saved = false;
             e.start(out + pos, cap > pos ? cap - pos : 0);
         }
-        if (qp_prev_resets(i, k, ctb_w, true)) qp_prev = slice_qp;
-        BinRec rec;
-        rec.start(tok, kMaxCuTokens);
-        const uint32_t nt = binarise_ctu(rec, islice, cus, coef, sao, i, k, count, ctb_w, qp_prev, true);
-        for (uint32_t j = 0; j < nt && j < kMaxCuTokens; ++j) code_token(e, cx, tok[j]);
-        if (x == 1) {  // storage after the row's second CTU (9.3.2.2 end)
+        code_ctb(e, cx, ps, islice, c, first, end, true, tok, false);
+        if (x == 1) {  // storage after the row's second CTB (9.3.2.2 end)
             std::memcpy(saved, ctx, C_NUM);
             have_saved = true;
         }
-        if (k == count - 1 || x == ctb_w - 1) {  // substream ends: end_of_slice / end_of_subset coded
+        if (c == end - 1 || x == cw - 1) {  // substream ends: end_of_slice / end_of_subset coded
             e.finish_slice();
             if (e.overflow) return cap + 1;
             sub_len.push_back(e.pos);
@@ -386,6 +384,9 @@ CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cf
     cu_.resize(n);
     mv_.resize(2 * n);
     coef_.resize(n * kCoefPerCu);
+    qp_pred_.assign(n, 0);
+    qpy_.assign(n, 0);
+    bl_safe_ = bl_safe_modes(4, 0) & bl_safe_modes(3, 1);  // the 16x16 luma mode and its DM chroma
 }
 
 namespace {
@@ -399,16 +400,22 @@ void summarise(CuInfo& c, const int16_t* coef) {
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
     uint8_t* ry = rec_y_[cur_].data();
     uint8_t* ruv = rec_uv_[cur_].data();
-    const int W = common_.ctb_w(), H = common_.ctb_h(), sr = common_.slice_rows();
+    const int W = common_.ctb_w(), H = common_.ctb_h(), sr = 2 * common_.slice_rows();  // unit rows per I slice
     const int qp = frame_qp_();
     const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
     const int lambda = h264::lambda_sad(qp);
+    // units in raster order (the GPU's row wavefront); availability as the decoder sees it in z
+    // order: no above-right for a CTB's last unit, and a CTB's first unit has a below-left (the
+    // left CTB's last unit) that is not reconstructed yet -- it keeps to the modes that do not
+    // read it (bl_safe_modes)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             const int i = y * W + x, x0 = x * 16, y0 = y * 16;
+            const int z = ((y & 1) << 1) | (x & 1);
             CuInfo& c = cu_[i];
             std::memset(&c, 0, sizeof c);
-            const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < W, ac = at && x > 0;
+            const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < W && z != 3, ac = at && x > 0;
+            const bool bl_pending = z == 0 && x > 0 && y + 1 < H;
             uint8_t lp[16], tp[16], tr[16];
             for (int k = 0; k < 16; ++k) {
                 lp[k] = al ? ry[(y0 + k) * cw_ + x0 - 1] : 0;
@@ -419,15 +426,17 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             int L[33], T[33];
             intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
             const int cand_a = al ? cu_[i - 1].intra_mode : 1;
+            const int cand_b = (at && (y & 1)) ? cu_[i - W].intra_mode : 1;  // above only inside the CTB
             int best = -1, best_cost = 0;
             int pred[256];
             for (int k = 0; k < kNumIntraCands; ++k) {
                 const int m = kIntraCands[k];
+                if (bl_pending && !((bl_safe_ >> m) & 1)) continue;
                 intra_predict(m, 4, 0, L, T, pred);
                 int sad = 0;
                 for (int r = 0; r < 16; ++r)
                     for (int q = 0; q < 16; ++q) sad += std::abs((int)sy[(y0 + r) * pitch + x0 + q] - pred[r * 16 + q]);
-                const int cost = sad + lambda * intra_mode_bits(m, cand_a);
+                const int cost = sad + lambda * intra_mode_bits(m, cand_a, cand_b);
                 if (best < 0 || cost < best_cost) {
                     best = m;
                     best_cost = cost;
@@ -436,6 +445,7 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             c.type = kCuIntra;
             c.intra_mode = (uint8_t)best;
             c.qp = (uint8_t)qp;
+            c.ct = 1;
             int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
             intra_predict(best, 4, 0, L, T, pred);
             int res[256], rr[256];
@@ -586,37 +596,54 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                             (uint8_t)clip255(pc[comp][r * 8 + q] + rrc[comp][r * 8 + q]);
             summarise(c, co);
         }
-    // cost-balanced slices, then the merge / AMVP decisions against each slice's neighbours
+    // cost-balanced slices of CTBs, then per CTB the skip / merge / AMVP decisions against the
+    // slice's neighbours and the coding tree (CU32 or four CU16)
     slices_ = common_.plan_p_slices(cu_);
-    int s = 0;
-    for (int i = 0; i < W * H; ++i) {
-        while (s + 1 < (int)slices_.size() && slices_[s + 1] <= i) ++s;
-        MvCand a1, b1, b0, b2;
-        inter_neighbours(mv_.data(), 2, i % W, i / W, W, slices_[s], &a1, &b1, &b0, &b2);
-        decide_inter(cu_[i], a1, b1, b0, b2);
+    const int cw = common_.c32_w(), nctb = common_.num_ctbs();
+    for (size_t s = 0; s < slices_.size(); ++s) {
+        const int first = slices_[s], end = s + 1 < slices_.size() ? slices_[s + 1] : nctb;
+        for (int c = first; c < end; ++c) {
+            const int x0 = 2 * (c % cw), y0 = 2 * (c / cw);
+            CuInfo u[4];
+            bool in[4];
+            for (int z = 0; z < 4; ++z) {
+                const int x = x0 + (z & 1), y = y0 + (z >> 1);
+                in[z] = x < W && y < H;
+                if (in[z]) u[z] = cu_[(size_t)(y * W + x)];
+            }
+            decide_ctb(u, in, mv_.data(), 2, x0, y0, W, H, first);
+            for (int z = 0; z < 4; ++z)
+                if (in[z]) cu_[(size_t)((y0 + (z >> 1)) * W + x0 + (z & 1))] = u[z];
+        }
     }
     (void)sr;
 }
 
 const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
     h264::EncoderCommon& rc = common_.rc();
+    const int W = common_.ctb_w(), H = common_.ctb_h(), nctb = common_.num_ctbs();
+    auto slice_end = [&](size_t s) { return s + 1 < slices_.size() ? slices_[s + 1] : nctb; };
+    auto qp_chain = [&](int qp) {  // QP predictors / QpY of every unit, slice by slice
+        for (size_t s = 0; s < slices_.size(); ++s)
+            slice_qp_chain(cu_.data(), W, H, slices_[s], slice_end(s), qp, common_.wpp(), qp_pred_.data(), qpy_.data());
+    };
     while (rc.wants_probe()) {  // size the first IDR (rate control), as the GPU encoder does
         qp_override_ = rc.probe_qp();
         analyse_intra(y, uv, pitch);
-        const std::vector<int> rows = common_.row_slices();
-        const int W = common_.ctb_w(), H = common_.ctb_h();
+        slices_ = common_.row_slices();
+        qp_chain(qp_override_);
+        const PicSyn ps{cu_.data(), coef_.data(), qp_pred_.data(), nullptr, W, H, common_.depth_inter()};
         std::vector<uint8_t> buf;
         std::vector<uint32_t> sub_len;
         uint8_t ctx[C_NUM];
         size_t total = 0;
-        for (size_t s = 0; s < rows.size(); ++s) {
-            const int first = rows[s], count = (s + 1 < rows.size() ? rows[s + 1] : W * H) - first;
-            const uint32_t cap = (uint32_t)count * 1024 + 1024;
+        for (size_t s = 0; s < slices_.size(); ++s) {
+            const int first = slices_[s], end = slice_end(s);
+            const uint32_t cap = (uint32_t)(end - first) * 4096 + 1024;
             buf.resize(cap);
-            total += (common_.wpp() ? code_slice_wpp(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(),
-                                                     first, count, W, nullptr, tok_.data(), sub_len)
-                                    : code_slice(buf.data(), cap, true, qp_override_, cu_.data(), coef_.data(), first,
-                                                 count, W, ctx, nullptr, tok_.data())) +
+            total += (common_.wpp() ? code_slice_wpp(buf.data(), cap, true, qp_override_, ps, first, end, tok_.data(),
+                                                     sub_len)
+                                    : code_slice(buf.data(), cap, true, qp_override_, ps, first, end, ctx, tok_.data())) +
                      12;
         }
         rc.add_probe(qp_override_, (int)total + 64);
@@ -633,48 +660,45 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     } else {
         analyse_inter(y, uv, pitch);
     }
-    const int W = common_.ctb_w(), H = common_.ctb_h();
-    if (cfg_.hevc_deblock()) {  // in-loop deblocking: all vertical CU edges, then all horizontal ones
-        std::vector<uint8_t> qpy((size_t)W * H);
-        for (size_t s = 0; s < slices_.size(); ++s) {
-            const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
-            slice_qpy(cu_.data(), first, count, qp, qpy.data(), W, common_.wpp());
-        }
+    qp_chain(qp);
+    if (cfg_.hevc_deblock()) {  // in-loop deblocking: all vertical edges, then all horizontal ones
         for (int dir = 0; dir < 2; ++dir)
             for (int i = 0; i < W * H; ++i)
                 for (int seg = 0; seg < 4; ++seg) {
                     if (dir == 0 ? (i % W) != 0 : (i / W) != 0)
-                        db_edge_seg(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir,
+                        db_edge_seg(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, W, cu_.data(), qpy_.data(), i, dir,
                                     seg, cfg_.chroma_qp_offset);
-                    db_internal_seg(rec_y_[cur_].data(), cw_, W, cu_.data(), qpy.data(), i, dir, seg);
+                    db_internal_seg(rec_y_[cur_].data(), cw_, W, cu_.data(), qpy_.data(), i, dir, seg);
                 }
     }
-    if (cfg_.sao) {  // SAO per CTB on the deblocked picture (a copy: CTBs read deblocked neighbours)
+    if (cfg_.sao) {  // SAO per 32x32 CTB on the deblocked picture (a copy: CTBs read deblocked neighbours)
         const std::vector<uint8_t> pre_y = rec_y_[cur_], pre_uv = rec_uv_[cur_];
-        sao_.assign((size_t)W * H * 4, 0u);
+        sao_.assign((size_t)nctb * 4, 0u);
         const uint32_t lam16 = kLambdaSse16[qp];
-        for (int i = 0; i < W * H; ++i) {
-            const int x0 = (i % W) * kCtb, y0 = (i / W) * kCtb;
-            uint32_t* w = sao_.data() + 4 * (size_t)i;
-            if (sao_keep_ctb(idr, cu_[i])) {  // no residual in a P picture: SAO off, samples kept
-                sao_apply_block(pre_y.data(), rec_y_[cur_].data(), cw_, 1, x0, y0, kCtb, cw_, ch_, 0u);
-                for (int c = 0; c < 2; ++c)
-                    sao_apply_block(pre_uv.data() + c, rec_uv_[cur_].data() + c, cw_, 2, x0 / 2, y0 / 2, kCtb / 2,
-                                    cw_ / 2, ch_ / 2, 0u);
-                continue;
+        const int cw = common_.c32_w();
+        for (int c = 0; c < nctb; ++c) {
+            const int x0 = (c % cw) * 32, y0 = (c / cw) * 32;
+            const int nw = std::min(32, cw_ - x0), nh = std::min(32, ch_ - y0);
+            uint32_t* w = sao_.data() + 4 * (size_t)c;
+            uint32_t any = 0;
+            for (int z = 0; z < 4; ++z) {
+                const int ux = 2 * (c % cw) + (z & 1), uy = 2 * (c / cw) + (z >> 1);
+                if (ux < W && uy < H) any |= cu_[(size_t)(uy * W + ux)].cbf;
             }
-            SaoStats st[3];
-            sao_stats_block(pre_y.data(), cw_, y, pitch, 1, x0, y0, kCtb, cw_, ch_, st[0]);
-            for (int c = 0; c < 2; ++c)
-                sao_stats_block(pre_uv.data() + c, cw_, uv + c, pitch, 2, x0 / 2, y0 / 2, kCtb / 2, cw_ / 2, ch_ / 2,
-                                st[1 + c]);
-            SaoCompChoice ch[3];
-            for (int c = 0; c < 3; ++c) sao_eval_comp(st[c], lam16, ch[c]);
-            sao_combine(ch[0], ch[1], ch[2], lam16, w);
-            sao_apply_block(pre_y.data(), rec_y_[cur_].data(), cw_, 1, x0, y0, kCtb, cw_, ch_, w[0]);
-            for (int c = 0; c < 2; ++c)
-                sao_apply_block(pre_uv.data() + c, rec_uv_[cur_].data() + c, cw_, 2, x0 / 2, y0 / 2, kCtb / 2, cw_ / 2,
-                                ch_ / 2, w[1 + c]);
+            if (!sao_keep_ctb(idr, any)) {
+                SaoStats st[3];
+                sao_stats_block(pre_y.data(), cw_, y, pitch, 1, x0, y0, nw, nh, cw_, ch_, st[0]);
+                for (int k = 0; k < 2; ++k)
+                    sao_stats_block(pre_uv.data() + k, cw_, uv + k, pitch, 2, x0 / 2, y0 / 2, nw / 2, nh / 2, cw_ / 2,
+                                    ch_ / 2, st[1 + k]);
+                SaoCompChoice ch[3];
+                for (int k = 0; k < 3; ++k) sao_eval_comp(st[k], lam16, ch[k]);
+                sao_combine(ch[0], ch[1], ch[2], lam16, w);
+            }  // else SAO off, the samples are kept
+            sao_apply_block(pre_y.data(), rec_y_[cur_].data(), cw_, 1, x0, y0, nw, nh, cw_, ch_, w[0]);
+            for (int k = 0; k < 2; ++k)
+                sao_apply_block(pre_uv.data() + k, rec_uv_[cur_].data() + k, cw_, 2, x0 / 2, y0 / 2, nw / 2, nh / 2,
+                                cw_ / 2, ch_ / 2, w[1 + k]);
         }
     }
     au_.clear();
@@ -682,15 +706,14 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     std::vector<uint8_t> buf;
     std::vector<uint32_t> sub_len;
     uint8_t ctx[C_NUM];
+    const PicSyn ps{cu_.data(), coef_.data(), qp_pred_.data(), cfg_.sao ? sao_.data() : nullptr, W, H,
+                    common_.depth_inter()};
     for (size_t s = 0; s < slices_.size(); ++s) {
-        const int first = slices_[s], count = (s + 1 < slices_.size() ? slices_[s + 1] : W * H) - first;
-        const uint32_t cap = (uint32_t)count * 1024 + 1024;
+        const int first = slices_[s], end = slice_end(s);
+        const uint32_t cap = (uint32_t)(end - first) * 4096 + 1024;
         buf.resize(cap);
-        const uint32_t* saop = cfg_.sao ? sao_.data() : nullptr;
-        const uint32_t n = common_.wpp() ? code_slice_wpp(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first,
-                                                          count, W, saop, tok_.data(), sub_len)
-                                         : code_slice(buf.data(), cap, idr, qp, cu_.data(), coef_.data(), first, count,
-                                                      W, ctx, saop, tok_.data());
+        const uint32_t n = common_.wpp() ? code_slice_wpp(buf.data(), cap, idr, qp, ps, first, end, tok_.data(), sub_len)
+                                         : code_slice(buf.data(), cap, idr, qp, ps, first, end, ctx, tok_.data());
         if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
         common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n,
                                 common_.wpp() ? sub_len.data() : nullptr, (int)sub_len.size());
@@ -732,9 +755,10 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
 namespace mx {
 namespace hevc {
 
-// Random slices (every CU type, split and unsplit transform trees, levels up to the escape
-// range, SAO parameters) coded twice -- directly and through the bin-token path -- must give
-// identical bytes.  Returns the number of slices checked; throws on the first mismatch.
+// Random slices (every CU type, CU32 and CU16 coding trees, split and unsplit transform trees,
+// levels up to the escape range, SAO parameters) coded twice -- directly and through the
+// bin-token path -- must give identical bytes.  Returns the number of slices checked; throws on
+// the first mismatch.
 int token_selftest(uint32_t seed, int slices) {
     uint32_t r = seed * 2654435761u + 1u;
     auto rnd = [&r](uint32_t n) {
@@ -743,54 +767,79 @@ int token_selftest(uint32_t seed, int slices) {
         r ^= r << 5;
         return n ? r % n : 0u;
     };
-    const int ctb_w = 7;
     for (int sl = 0; sl < slices; ++sl) {
-        const int count = 1 + (int)rnd(40);
+        const int mb_w = 1 + (int)rnd(9), mb_h = 1 + (int)rnd(7);
+        const int cw = ctb_cols(mb_w), nctb = cw * ctb_rows(mb_h);
+        const int first = (int)rnd((uint32_t)nctb), end = first + 1 + (int)rnd((uint32_t)(nctb - first));
         const bool islice = rnd(4) == 0;
         const int qp = 10 + (int)rnd(40);
-        std::vector<CuInfo> cus((size_t)count);
-        std::vector<int16_t> coef((size_t)count * kCoefPerCu, 0);
-        std::vector<uint32_t> sao((size_t)count * 4, 0);
-        for (int i = 0; i < count; ++i) {
-            CuInfo& c = cus[(size_t)i];
-            std::memset(&c, 0, sizeof c);
-            c.type = islice ? kCuIntra : (uint8_t)rnd(4);
-            c.intra_mode = (uint8_t)rnd(35);
-            c.qp = (uint8_t)(10 + rnd(40));
-            c.mvdx = (int16_t)((int)rnd(2000) - 1000);
-            c.mvdy = (int16_t)((int)rnd(64) - 32);
-            c.mvp_idx = (uint8_t)rnd(2);
-            c.tu_split = c.type == kCuIntra ? 0 : (uint8_t)rnd(3);
-            if (c.type != kCuSkip) {
-                const int density = (int)rnd(4);  // 0: empty, 1: sparse, 2: dense, 3: escapes
-                int16_t* co = coef.data() + (size_t)i * kCoefPerCu;
-                for (int k = 0; k < kCoefPerCu && density; ++k) {
-                    if (rnd(density == 1 ? 40 : 3)) continue;
-                    int v = 1 + (int)rnd(density == 3 ? 3000 : 4);
-                    if (density == 3 && rnd(50) == 0) v = 30000;
-                    co[k] = (int16_t)(rnd(2) ? -v : v);
+        const int nu = mb_w * mb_h;
+        std::vector<CuInfo> cus((size_t)nu);
+        std::vector<int16_t> coef((size_t)nu * kCoefPerCu, 0);
+        std::vector<uint8_t> qpp((size_t)nu);
+        std::vector<uint32_t> sao((size_t)nctb * 4, 0);
+        auto fill_levels = [&](CuInfo& c, int i) {
+            const int density = (int)rnd(4);  // 0: empty, 1: sparse, 2: dense, 3: escapes
+            int16_t* co = coef.data() + (size_t)i * kCoefPerCu;
+            for (int k = 0; k < kCoefPerCu && density; ++k) {
+                if (rnd(density == 1 ? 40 : 3)) continue;
+                int v = 1 + (int)rnd(density == 3 ? 3000 : 4);
+                if (density == 3 && rnd(50) == 0) v = 30000;
+                co[k] = (int16_t)(rnd(2) ? -v : v);
+            }
+            cu_summarise(c, co);
+        };
+        for (int c = 0; c < nctb; ++c) {
+            const int x0 = 2 * (c % cw), y0 = 2 * (c / cw);
+            const bool cu32 = !islice && ctb_whole(c, cw, mb_w, mb_h) && rnd(2);
+            CuInfo h;
+            std::memset(&h, 0, sizeof h);
+            h.type = (uint8_t)rnd(3);  // skip / merge / AMVP
+            h.qp = (uint8_t)(10 + rnd(40));
+            h.mvx = (int16_t)((int)rnd(200) - 100);
+            h.mvdx = (int16_t)((int)rnd(2000) - 1000);
+            h.mvdy = (int16_t)((int)rnd(64) - 32);
+            h.mvp_idx = (uint8_t)(h.type == kCuAmvp ? rnd(2) : rnd(5));
+            for (int z = 0; z < 4; ++z) {
+                const int x = x0 + (z & 1), y = y0 + (z >> 1);
+                if (x >= mb_w || y >= mb_h) continue;
+                const int i = y * mb_w + x;
+                CuInfo& cu = cus[(size_t)i];
+                std::memset(&cu, 0, sizeof cu);
+                if (cu32) {
+                    cu = h;
+                    cu.ct = 0;
+                } else {
+                    cu.ct = 1;
+                    cu.type = islice ? kCuIntra : (uint8_t)rnd(4);
+                    cu.intra_mode = (uint8_t)rnd(35);
+                    cu.qp = (uint8_t)(10 + rnd(40));
+                    cu.mvdx = (int16_t)((int)rnd(2000) - 1000);
+                    cu.mvdy = (int16_t)((int)rnd(64) - 32);
+                    cu.mvp_idx = (uint8_t)(cu.type == kCuAmvp ? rnd(2) : rnd(5));
                 }
-                cu_summarise(c, co);
-                if (c.type == kCuIntra && c.tu_split) c.tu_split = 0;
+                cu.tu_split = cu.type == kCuIntra ? 1 : (uint8_t)(1 + rnd(2));
+                if (cu.type != kCuSkip) fill_levels(cu, i);
+                qpp[(size_t)i] = (uint8_t)(10 + rnd(40));
             }
             for (int w = 0; w < 3; ++w) {
                 const int kind = (int)rnd(4);
                 int off[4];
                 for (int k = 0; k < 4; ++k) off[k] = (int)rnd(15) - 7;
-                if (kind == 1) sao[(size_t)i * 4 + w] = sao_pack(1, 0, (int)rnd(32), off);
-                if (kind == 2) sao[(size_t)i * 4 + w] = sao_pack(2, (int)rnd(4), 0, off);
-                if (kind == 3 && i > 0) sao[(size_t)i * 4 + w] = sao[(size_t)(i - 1) * 4 + w];  // merge candidates
+                if (kind == 1) sao[(size_t)c * 4 + w] = sao_pack(1, 0, (int)rnd(32), off);
+                if (kind == 2) sao[(size_t)c * 4 + w] = sao_pack(2, (int)rnd(4), 0, off);
+                if (kind == 3 && c > 0) sao[(size_t)c * 4 + w] = sao[(size_t)(c - 1) * 4 + w];  // merge candidates
             }
         }
         const bool use_sao = rnd(2) != 0;
-        const uint32_t cap = (uint32_t)count * 4096 + 1024;
+        const PicSyn ps{cus.data(), coef.data(), qpp.data(), use_sao ? sao.data() : nullptr, mb_w, mb_h,
+                        rnd(2) ? 3 : 0};
+        const uint32_t cap = (uint32_t)(end - first) * 16384 + 1024;
         std::vector<uint8_t> a(cap), b(cap);
         std::vector<uint16_t> tok(kMaxCuTokens);
         uint8_t ctx[C_NUM];
-        const uint32_t na = code_slice_direct(a.data(), cap, islice, qp, cus.data(), coef.data(), 0, count, ctb_w, ctx,
-                                              use_sao ? sao.data() : nullptr);
-        const uint32_t nb = code_slice(b.data(), cap, islice, qp, cus.data(), coef.data(), 0, count, ctb_w, ctx,
-                                       use_sao ? sao.data() : nullptr, tok.data());
+        const uint32_t na = code_slice(a.data(), cap, islice, qp, ps, first, end, ctx, tok.data(), true);
+        const uint32_t nb = code_slice(b.data(), cap, islice, qp, ps, first, end, ctx, tok.data(), false);
         if (na != nb || std::memcmp(a.data(), b.data(), na) != 0)
             throw std::runtime_error("hevc token path differs from direct coding (slice " + std::to_string(sl) + ")");
     }

@@ -15,9 +15,10 @@ namespace mx {
 namespace hevc {
 
 void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
-    const int ncu = geom_.mb_w * geom_.mb_h;
-    // substreams: cost-balanced slices, or (WPP) every CTU row
-    const int ns = cfg_.hevc_wpp ? std::max(common_.max_slices(), geom_.mb_h) : common_.max_slices();
+    const int ncu = geom_.mb_w * geom_.mb_h;                // 16x16 units
+    const int nctb = common_.num_ctbs(), npos = 4 * nctb;  // 32x32 CTBs, coding positions
+    // substreams: cost-balanced slices, or (WPP) every CTB row
+    const int ns = cfg_.hevc_wpp ? std::max(common_.max_slices(), common_.c32_h()) : common_.max_slices();
     HevcDeviceBuffers& b = sl.buf;
     HIP_CHECK(hipMalloc(&b.fs, sizeof(HevcFrameState)));
     HIP_CHECK(hipMalloc(&b.me.fs, sizeof(h264::FrameState)));
@@ -25,37 +26,40 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMemsetAsync(b.me.mb, 0, sizeof(h264::MbInfo) * ncu, stream_));
     HIP_CHECK(hipMalloc(&b.cu, sizeof(CuInfo) * ncu));
     HIP_CHECK(hipMalloc(&b.coef, sizeof(int16_t) * kCoefPerCu * (size_t)ncu));
-    // per-slice CABAC output slot: room for 1 KiB per CTU of an even share of the picture plus
-    // one CTU row (slices are cost-balanced, so a slice of many cheap CTUs stays small)
-    const size_t ctus_per_slot = std::max((size_t)(ncu + ns - 1) / ns + (size_t)common_.slice_rows() * geom_.mb_w,
-                                          (size_t)geom_.mb_w);
-    b.slice_cap = (uint32_t)((ctus_per_slot * 1024 + 15) & ~(size_t)15);
+    // per-substream CABAC output slot: room for 1 KiB per unit of an even share of the picture plus
+    // one slice of CTB rows (slices are cost-balanced, so a slice of many cheap CTBs stays small)
+    const size_t units_per_slot = std::max((size_t)(ncu + ns - 1) / ns + (size_t)2 * common_.slice_rows() * geom_.mb_w,
+                                           (size_t)2 * geom_.mb_w);
+    b.slice_cap = (uint32_t)((units_per_slot * 1024 + 15) & ~(size_t)15);
     HIP_CHECK(hipMalloc(&b.slice_data, (size_t)b.slice_cap * ns));
     HIP_CHECK(hipMalloc(&b.slice_len, sizeof(uint32_t) * ns));
     HIP_CHECK(hipMalloc(&b.slice_first, sizeof(int) * ns));
-    HIP_CHECK(hipMalloc(&b.slice_of_cu, sizeof(int) * ncu));
+    HIP_CHECK(hipMalloc(&b.slice_of_cu, sizeof(int) * nctb));
     HIP_CHECK(hipMalloc(&b.nslices, sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&b.qpy, ncu));
-    // per-CU arrays scanned in 4096-CU tiles of 16-byte loads: padded with zeros to a whole tile
-    const size_t ncu_pad = ((size_t)ncu + kScanTilePad - 1) / kScanTilePad * kScanTilePad + 4;
-    HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * ncu_pad));
-    HIP_CHECK(hipMemsetAsync(b.cost, 0, sizeof(uint32_t) * ncu_pad, stream_));
+    HIP_CHECK(hipMalloc(&b.qp_pred, ncu));
+    // arrays scanned in 4096-entry tiles of 16-byte loads (per CTB costs, per coding position token
+    // counts): padded with zeros to a whole tile
+    auto pad = [](size_t n) { return (n + kScanTilePad - 1) / kScanTilePad * kScanTilePad + 4; };
+    const size_t nctb_pad = pad((size_t)nctb), npos_pad = pad((size_t)npos);
+    HIP_CHECK(hipMalloc(&b.cost, sizeof(uint32_t) * nctb_pad));
+    HIP_CHECK(hipMemsetAsync(b.cost, 0, sizeof(uint32_t) * nctb_pad, stream_));
     HIP_CHECK(hipMalloc(&b.qpc, ncu));
-    HIP_CHECK(hipMalloc(&b.sao, sizeof(uint32_t) * 4 * (size_t)ncu));
+    HIP_CHECK(hipMalloc(&b.sao, sizeof(uint32_t) * 4 * (size_t)nctb));
     HIP_CHECK(hipMalloc(&b.slice_clk, sizeof(unsigned long long) * 2 * (size_t)ns));
-    HIP_CHECK(hipMalloc(&b.tok, sizeof(uint16_t) * kMaxCuTokens * (size_t)ncu));
-    HIP_CHECK(hipMalloc(&b.ntok, sizeof(uint32_t) * ncu_pad));
-    HIP_CHECK(hipMemsetAsync(b.ntok, 0, sizeof(uint32_t) * ncu_pad, stream_));
-    HIP_CHECK(hipMalloc(&b.tok_off, sizeof(uint32_t) * ncu_pad));
+    HIP_CHECK(hipMalloc(&b.tok, sizeof(uint16_t) * kMaxCuTokens * (size_t)npos));
+    HIP_CHECK(hipMalloc(&b.ntok, sizeof(uint32_t) * npos_pad));
+    HIP_CHECK(hipMemsetAsync(b.ntok, 0, sizeof(uint32_t) * npos_pad, stream_));
+    HIP_CHECK(hipMalloc(&b.tok_off, sizeof(uint32_t) * npos_pad));
     // + one chunk of padding: k_hevc_arith reads whole 256-token chunks
-    HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)ncu + 512)));
+    HIP_CHECK(hipMalloc(&b.tok_dense, sizeof(uint16_t) * (kMaxCuTokens * (size_t)npos + 512)));
     HIP_CHECK(hipMalloc(&b.sse_part, 4 * sizeof(unsigned long long) * h264::kSsePartStride));
     HIP_CHECK(hipMalloc(&b.sse_tot, kSseSlots * kSseSlotWords * sizeof(unsigned long long)));
     HIP_CHECK(hipMalloc(&b.pack_done, sizeof(uint32_t)));
     HIP_CHECK(hipMemsetAsync(b.pack_done, 0, sizeof(uint32_t), stream_));
-    HIP_CHECK(hipMalloc(&b.wpp_ctx, sizeof(uint32_t) * kWppCtxWords * (size_t)geom_.mb_h));
-    HIP_CHECK(hipMalloc(&b.wpp_flag, sizeof(uint32_t) * (size_t)geom_.mb_h));
-    HIP_CHECK(hipMemsetAsync(b.wpp_flag, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
+    HIP_CHECK(hipMalloc(&b.wpp_ctx, sizeof(uint32_t) * kWppCtxWords * (size_t)common_.c32_h()));
+    HIP_CHECK(hipMalloc(&b.wpp_flag, sizeof(uint32_t) * (size_t)common_.c32_h()));
+    HIP_CHECK(hipMemsetAsync(b.wpp_flag, 0, sizeof(uint32_t) * (size_t)common_.c32_h(), stream_));
     HIP_CHECK(hipHostMalloc(&b.wpp_err, sizeof(int), hipHostMallocMapped));
     *b.wpp_err = 0;
     b.out_bytes = (size_t)ncu * 768;
@@ -72,7 +76,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
 void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
-                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.cost, (void*)b.qpc,
+                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.qp_pred, (void*)b.cost, (void*)b.qpc,
                     (void*)b.sse_part, (void*)b.sse_tot, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
                     (void*)b.tok_dense, (void*)b.wpp_ctx, (void*)b.wpp_flag, (void*)b.pack_done})
         if (p) (void)hipFree(p);
@@ -88,7 +92,7 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     : cfg_(cfg), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
         throw std::invalid_argument("pipeline_depth must be 1, 2 or 3");
-    if (common_.slice_rows() > kMaxSliceRows) throw std::invalid_argument("hevc: too many CTU rows per slice");
+    if (2 * common_.slice_rows() > kMaxSliceRows) throw std::invalid_argument("hevc: too many CTB rows per slice");
     depth_ = cfg.pipeline_depth;
     geom_.width = cfg.width;
     geom_.height = cfg.height;
@@ -98,7 +102,9 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     geom_.coded_h = geom_.mb_h * kCtb;
     geom_.pitch = (geom_.coded_w + 255) & ~255;
     const int ncu = geom_.mb_w * geom_.mb_h;
-    if ((ncu + 3) / 4 > h264::kSsePartStride) throw std::invalid_argument("frame too large for the distortion partials");
+    if (std::max((ncu + 3) / 4, common_.num_ctbs()) > h264::kSsePartStride)
+        throw std::invalid_argument("frame too large for the distortion partials");
+    bl_safe_ = bl_safe_modes(4, 0) & bl_safe_modes(3, 1);
     const size_t ysz = (size_t)geom_.pitch * geom_.coded_h, uvsz = ysz / 2;
     for (int i = 0; i < 2; ++i) {
         HIP_CHECK(hipMalloc(&rec_y_[i], ysz));
@@ -173,15 +179,18 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.hp_pitch = hp_pitch_;
     f.idr = idr ? 1 : 0;
     f.qp = qp;
-    f.slice_rows = common_.slice_rows();
+    f.slice_rows = 2 * common_.slice_rows();  // in 16x16-unit rows
     f.num_slices = common_.num_slices();
+    f.bl_safe = bl_safe_;
+    f.depth_inter = common_.depth_inter();
+    f.pad2_ = 0;
     f.aq = cfg_.aq;
     f.tu_split = cfg_.tu_split ? 1 : 0;
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
-    // distortion partials: k_hevc_sao (one per 4 CTUs) with SAO, else k_hevc_sse (one per CTU row)
-    // after deblocking, else the analysis kernels' (P: one per 4 CUs, I: one per CTU row)
-    const int ncu = geom_.mb_w * geom_.mb_h;
-    f.n_sse_parts = f.sao ? (ncu + 3) / 4 : ((idr || cfg_.hevc_deblock()) ? geom_.mb_h : (ncu + 3) / 4);
+    // distortion partials: k_hevc_sao (totals) with SAO, else k_hevc_sse (one per unit row) after
+    // deblocking, else the analysis kernels' (P: one per CTB, I: one per unit row)
+    f.n_sse_parts = f.sao ? common_.num_ctbs()
+                          : ((idr || cfg_.hevc_deblock()) ? geom_.mb_h : common_.num_ctbs());
     f.sse_part = sl.buf.sse_part;
     f.sse_tot = sl.buf.sse_tot;
     for (int k = 0; k < 4; ++k) f.mask_c[k] = mask_c_[k];
@@ -263,7 +272,7 @@ void GpuHevcEncoder::enqueue_analysis_impl(bool idr, const uint8_t* src_y, const
     if (idr) {
         if (cfg_.aq >= 3)  // the next P picture's temporal classes compare against this source
             launch_hevc_save_src(geom_, sl.buf, src_y, stream_);
-        launch_hevc_intra(geom_, sl.buf, common_.slice_rows(), common_.num_slices(), src_y, src_uv, stream_);
+        launch_hevc_intra(geom_, sl.buf, 2 * common_.slice_rows(), common_.num_slices(), src_y, src_uv, stream_);
     } else {
         h264::launch_hpel(geom_, sl.buf.me, hp_, hp_pitch_, stream_);
         h264::launch_me(geom_, sl.buf.me, src_y, stream_);
@@ -389,19 +398,19 @@ std::vector<std::array<uint64_t, 6>> GpuHevcEncoder::slice_timing() const {
     std::vector<std::array<uint64_t, 6>> out;
     if (last_slot_ < 0) return out;
     const size_t n = last_first_.size();
-    const uint64_t ncu = (uint64_t)geom_.mb_w * geom_.mb_h;
+    const uint64_t nctb = (uint64_t)common_.num_ctbs();
     std::vector<unsigned long long> clk(2 * n);
-    std::vector<uint32_t> off(ncu + 1);
+    std::vector<uint32_t> off(4 * nctb + 1);
     HIP_CHECK(hipMemcpy(clk.data(), slots_[last_slot_].buf.slice_clk, sizeof(unsigned long long) * 2 * n,
                         hipMemcpyDeviceToHost));
-    HIP_CHECK(hipMemcpy(off.data(), slots_[last_slot_].buf.tok_off, sizeof(uint32_t) * (ncu + 1),
+    HIP_CHECK(hipMemcpy(off.data(), slots_[last_slot_].buf.tok_off, sizeof(uint32_t) * (4 * nctb + 1),
                         hipMemcpyDeviceToHost));
     unsigned long long t0 = ~0ull;
     for (size_t k = 0; k < n; ++k) t0 = std::min(t0, clk[2 * k]);
-    for (size_t k = 0; k < n; ++k) {
-        const uint64_t end = k + 1 < n ? last_first_[k + 1] : ncu;
+    for (size_t k = 0; k < n; ++k) {  // (first CTB, CTBs, ...)
+        const uint64_t end = k + 1 < n ? last_first_[k + 1] : nctb;
         out.push_back({last_first_[k], end - last_first_[k], last_len_[k], clk[2 * k + 1] - clk[2 * k],
-                       clk[2 * k] - t0, off[end] - off[last_first_[k]]});
+                       clk[2 * k] - t0, off[4 * end] - off[4 * last_first_[k]]});
     }
     return out;
 }
@@ -409,18 +418,19 @@ std::vector<std::array<uint64_t, 6>> GpuHevcEncoder::slice_timing() const {
 std::vector<std::array<uint32_t, 6>> GpuHevcEncoder::cu_token_table() const {
     std::vector<std::array<uint32_t, 6>> out;
     if (last_slot_ < 0) return out;
-    const size_t ncu = (size_t)geom_.mb_w * geom_.mb_h;
+    const size_t ncu = (size_t)geom_.mb_w * geom_.mb_h, npos = 4 * (size_t)common_.num_ctbs();
     std::vector<CuInfo> cus(ncu);
-    std::vector<uint32_t> ntok(ncu);
+    std::vector<uint32_t> ntok(npos);
     HIP_CHECK(hipMemcpy(cus.data(), slots_[last_slot_].buf.cu, sizeof(CuInfo) * ncu, hipMemcpyDeviceToHost));
-    HIP_CHECK(hipMemcpy(ntok.data(), slots_[last_slot_].buf.ntok, sizeof(uint32_t) * ncu, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(ntok.data(), slots_[last_slot_].buf.ntok, sizeof(uint32_t) * npos, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < ncu; ++i) {
+        const int kpos = cpos_of((int)(i % geom_.mb_w), (int)(i / geom_.mb_w), common_.c32_w());
         const CuInfo& c = cus[i];
         uint32_t lsum = 0, sb = 0;
         if (c.cbf & 1) lsum += c.last[0] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_y);
         if (c.cbf & 2) lsum += c.last[1] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[0]);
         if (c.cbf & 4) lsum += c.last[2] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[1]);
-        out.push_back({c.type, c.cbf, lsum, sb, c.est_bytes, ntok[i]});
+        out.push_back({c.type, c.cbf, lsum, sb, c.est_bytes, ntok[(size_t)kpos]});
     }
     return out;
 }

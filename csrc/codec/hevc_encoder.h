@@ -35,16 +35,23 @@ class HevcCommon {
     h264::EncoderCommon& rc() { return rc_; }
     const h264::EncoderCommon& rc() const { return rc_; }
     const EncoderConfig& config() const { return rc_.config(); }
+    // 16x16 analysis units (the encoder's CU grid; historical names) and the 32x32 CTB grid
     int ctb_w() const { return rc_.mb_w(); }
     int ctb_h() const { return rc_.mb_h(); }
-    int slice_rows() const { return slice_rows_; }
-    int num_slices() const { return (ctb_h() + slice_rows_ - 1) / slice_rows_; }
+    int c32_w() const { return ctb_cols(ctb_w()); }
+    int c32_h() const { return ctb_rows(ctb_h()); }
+    int num_ctbs() const { return c32_w() * c32_h(); }
+    // max_transform_hierarchy_depth_inter: 3 with split inter transform trees (a CU32's 16x16
+    // quadrants at depth 1 may split too), else 0
+    int depth_inter() const { return config().tu_split ? 3 : 0; }
+    int slice_rows() const { return slice_rows_; }  // CTB rows per I slice
+    int num_slices() const { return (c32_h() + slice_rows_ - 1) / slice_rows_; }
     int level_idc() const { return level_; }
     int max_slices() const { return max_slices_; }  // level limit (MaxSliceSegmentsPerPicture), capped
     // POC LSB (8 bits) of the current frame = frames since the last IDR.
     int poc() const { return rc_.cur_frame_num(); }
     void write_parameter_sets(std::vector<uint8_t>& out) const;
-    // One slice segment NAL (slice starting at CTU `addr`): start code, NAL header, header +
+    // One slice segment NAL (slice starting at CTB `addr`): start code, NAL header, header +
     // payload with emulation prevention.  WPP: data holds the slice's substreams back to back,
     // sub_len[0..nsub) their raw sizes; the header carries their entry points (sizes after
     // emulation prevention, 7.4.7.1).
@@ -53,13 +60,13 @@ class HevcCommon {
                          size_t n, const uint32_t* sub_len = nullptr, int nsub = 0,
                          const uint32_t* sub_off = nullptr) const;
     bool wpp() const { return config().hevc_wpp != 0; }
-    // CTU rows per P slice with WPP (the whole picture when 0 or larger)
+    // CTB rows per P slice with WPP (the whole picture when 0 or larger)
     int wpp_rows() const {
         const int r = config().hevc_wpp_rows;
-        return (r <= 0 || r > ctb_h()) ? ctb_h() : std::max(r, slice_rows_);  // level slice cap
+        return (r <= 0 || r > c32_h()) ? c32_h() : std::max(r, slice_rows_);  // level slice cap
     }
-    // Slice layout: I pictures one slice per slice_rows() CTU rows (the intra wavefront needs a
-    // fixed layout), P pictures cost-balanced raster runs (plan_p_slices).  Returns first CTUs.
+    // Slice layout: I pictures one slice per slice_rows() CTB rows (the intra wavefront needs a
+    // fixed layout), P pictures cost-balanced raster runs of CTBs (plan_p_slices).  Returns first CTBs.
     std::vector<int> row_slices() const;
     std::vector<int> plan_p_slices(const std::vector<CuInfo>& cus) const;
 
@@ -72,13 +79,12 @@ class HevcCommon {
 
 // Direct vs bin-token CABAC on random slices (hevc_cpu.cpp); returns the slices checked.
 int token_selftest(uint32_t seed, int slices);
-// Entropy-code one slice with wavefront parallel processing (host): every CTU row of the slice is a
-// substream (fresh contexts in the slice's first row -- or when the picture is one CTU wide --
-// else the contexts the row above had after its second CTU), written to `out` back to back;
+// Entropy-code the slice of CTBs [first, end) with wavefront parallel processing (host): every CTB
+// row of the slice is a substream (fresh contexts in the slice's first row -- or when the picture
+// is one CTB wide -- else the contexts the row above had after its second CTB), written to `out` back to back;
 // sub_len receives one size per row.  Returns the total bytes.
-uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const CuInfo* cus, const int16_t* coef,
-                        int first, int count, int ctb_w, const uint32_t* sao, uint16_t* tok,
-                        std::vector<uint32_t>& sub_len);
+uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, const PicSyn& ps, int first, int end,
+                        uint16_t* tok, std::vector<uint32_t>& sub_len);
 
 class CpuHevcEncoder {
    public:
@@ -107,11 +113,13 @@ class CpuHevcEncoder {
     bool have_ref_ = false;
     std::vector<CuInfo> cu_;
     std::vector<int16_t> mv_;  // per CU (x, y)
-    std::vector<int> slices_;  // first CTU of every slice of the current picture
+    std::vector<int> slices_;  // first CTB of every slice of the current picture
+    std::vector<uint8_t> qp_pred_, qpy_;  // per unit: QP predictor / QpY (slice_qp_chain)
+    uint64_t bl_safe_ = 0;     // intra modes safe with a pending below-left (bl_safe_modes, luma 16 & chroma 8)
     std::vector<int16_t> coef_;
     std::vector<uint8_t> au_;
     std::vector<uint8_t> prev_src_;  // previous source luma (coded size), temporal AQ classes
-    std::vector<uint32_t> sao_;      // SAO parameters, 4 words per CTB (hevc_core.h sao_pack)
+    std::vector<uint32_t> sao_;      // SAO parameters, 4 words per CTB32 (hevc_core.h sao_pack)
     std::vector<uint16_t> tok_ = std::vector<uint16_t>(kMaxCuTokens);  // bin tokens of one CTU
     FrameStats stats_;
 };
@@ -131,7 +139,7 @@ struct HevcFrameState {
     int32_t hp_pitch;
     int32_t idr;
     int32_t qp;
-    int32_t slice_rows;
+    int32_t slice_rows;  // 16x16-unit rows per I slice (two per CTB row)
     int32_t num_slices;
     int32_t aq;
     int32_t chroma_qp_offset;
@@ -163,6 +171,11 @@ struct HevcFrameState {
     uint32_t* wpp_ctx;
     uint32_t* wpp_flag;
     int* wpp_err;  // mapped host word: nonzero if a substream gave up waiting for the row above
+    // intra modes a CTB's first unit may use while its below-left is not reconstructed yet
+    // (hevc_core.h bl_safe_modes: 16x16 luma and its DM 8x8 chroma)
+    uint64_t bl_safe;
+    int32_t depth_inter;  // max_transform_hierarchy_depth_inter of the SPS
+    int32_t pad2_;
 };
 
 struct HevcOutHeader {
@@ -181,7 +194,8 @@ constexpr int kMaxSlices = 1024;
 // slot w % kSseSlots), summed by k_hevc_pack
 constexpr int kSseSlots = 64, kSseSlotWords = 8;
 constexpr size_t kScanTilePad = 4096;  // per-CU scan arrays padded to this (hevc_kernels.hip kScanTile)
-constexpr int kMaxSliceRows = 4;  // CTU rows per slice the intra wavefront kernel supports
+constexpr int kMaxSliceRows = 4;  // 16x16-unit rows per slice the intra wavefront kernel supports (2 CTB rows)
+constexpr int kIntraMaxMbW = 512;  // units per row the intra wavefront's LDS mode rows hold (8K)
 constexpr int kWppCtxWords = (C_NUM + 3) / 4;  // context states, four per dword
 constexpr uint32_t kSubSliceStart = 0x80000000u;  // substream record: this substream begins a slice
 // host buffer: header | substream payload offset[kMaxSlices] | length[] | first CTU[] | payloads
@@ -196,20 +210,21 @@ struct HevcDeviceBuffers {
     uint8_t* slice_data;     // [max_slices * slice_cap]
     uint32_t* slice_len;     // [max_slices]
     uint32_t slice_cap;
-    int* slice_first;        // [max_slices] first CTU of every slice (k_hevc_layout)
-    int* slice_of_cu;        // [ncu]
+    int* slice_first;        // [max_slices] first CTB of every slice (k_hevc_layout)
+    int* slice_of_cu;        // [nctb] slice of every CTB
     uint32_t* nslices;       // slice count of the frame
-    uint8_t* qpy;            // [ncu] QpY per CU (deblocking)
-    uint32_t* cost;          // [ncu] CABAC cost estimate (slice layout)
-    uint8_t* qpc;            // [ncu] QP of CUs that code a residual, else 255 (QP chain)
-    uint32_t* sao;           // [ncu][4] SAO parameters per CTB (hevc_core.h sao_pack; luma, Cb, Cr, 0)
+    uint8_t* qpy;            // [ncu] QpY per unit (deblocking)
+    uint8_t* qp_pred;        // [ncu] QP predictor per unit (entropy coder)
+    uint32_t* cost;          // [nctb] CABAC cost estimate per CTB (slice layout)
+    uint8_t* qpc;            // [ncu] QP of units that code a residual, else 255
+    uint32_t* sao;           // [nctb][4] SAO parameters per CTB (hevc_core.h sao_pack; luma, Cb, Cr, 0)
     unsigned long long* slice_clk;  // [max_slices][2] k_hevc_arith start / end (wall_clock64, 100 MHz)
-    uint16_t* tok;                  // [ncu][kMaxCuTokens] bin tokens per CTU (k_hevc_bins)
-    uint32_t* ntok;                 // [ncu] token count per CTU
-    uint32_t* tok_off;              // [ncu + 1] exclusive prefix of ntok
-    uint16_t* tok_dense;            // [ncu * kMaxCuTokens + 512] tokens in decoding order
-    uint32_t* wpp_ctx;              // [ctb_h][kWppCtxWords] context snapshots (WPP)
-    uint32_t* wpp_flag;             // [ctb_h] snapshot-ready epochs
+    uint16_t* tok;                  // [4 nctb][kMaxCuTokens] bin tokens per coding position (k_hevc_bins)
+    uint32_t* ntok;                 // [4 nctb] token count per coding position (0 outside the picture)
+    uint32_t* tok_off;              // [4 nctb + 1] exclusive prefix of ntok
+    uint16_t* tok_dense;            // [4 nctb * kMaxCuTokens + 512] tokens in decoding order
+    uint32_t* wpp_ctx;              // [ctb rows][kWppCtxWords] context snapshots (WPP)
+    uint32_t* wpp_flag;             // [ctb rows] snapshot-ready epochs
     int* wpp_err;                   // mapped host word
     size_t out_bytes;
     unsigned long long* sse_part;
@@ -327,6 +342,7 @@ class GpuHevcEncoder final : public VideoEncoder {
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     uint8_t* src_keep_[2] = {nullptr, nullptr};  // source luma of the last two frames (temporal AQ classes)
+    uint64_t bl_safe_ = 0;       // hevc_core.h bl_safe_modes (16x16 luma & DM chroma)
     uint8_t* pre_y_ = nullptr;   // SAO: reconstruction before SAO (deblocked in place)
     uint8_t* pre_uv_ = nullptr;
     int cur_ = 0;

@@ -665,14 +665,18 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     __shared__ unsigned long long part[3][4];
     __shared__ int16_t lv2[4][kCoefPerCu];  // split transform tree: levels and reconstruction
     __shared__ uint8_t rec2[4][384];
+    __shared__ uint32_t unit_cost[4];
     fill_mats(M);
     __syncthreads();
+    // one workgroup per 32x32 CTB, wave z = its unit in z order (the slice layout balances CTBs:
+    // the workgroup adds up the CTB's cost)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ncu = g.mb_w * g.mb_h;
     const int bid = blockIdx.x;
-    const int i = bid * 4 + wave;
-    const bool valid = i < ncu;
-    const int x = valid ? i % g.mb_w : 0, y = valid ? i / g.mb_w : 0;
+    const int cw = ctb_cols(g.mb_w);
+    const int ux = 2 * (bid % cw) + (wave & 1), uy = 2 * (bid / cw) + (wave >> 1);
+    const bool valid = ux < g.mb_w && uy < g.mb_h;
+    const int i = valid ? uy * g.mb_w + ux : 0;
+    const int x = valid ? ux : 0, y = valid ? uy : 0;
     const int x0 = x * 16, y0 = y * 16;
     TuBuf& t = tb[wave];
     int mvx = 0, mvy = 0, lsad = 0;
@@ -845,11 +849,15 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
             c.csbf_c[0] = c.csbf_c[1] = 0;
         }
         set_est_bytes(c, split ? r2.bits : r.bits);
-        cus[i] = c;  // skip / merge / AMVP are decided by k_hevc_decide once the slices are laid out
-        cost[i] = cu_cost(c);
+        c.ct = 1;
+        for (int k = 0; k < 7; ++k) c.rsv[k] = 0;
+        cus[i] = c;  // skip / merge / AMVP and the coding tree are decided by k_hevc_decide once the slices are laid out
         qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
+        unit_cost[wave] = cu_cost(c);
     }
+    if (!valid && lane == 0) unit_cost[wave] = 0u;
     __syncthreads();
+    if (threadIdx.x == 0) cost[bid] = unit_cost[0] + unit_cost[1] + unit_cost[2] + unit_cost[3];
     if (threadIdx.x < 3) {
         const int c = threadIdx.x;
         fs->sse_part[c * h264::kSsePartStride + bid] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
@@ -947,6 +955,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
     __shared__ int mode_cost[kMaxSliceRows][kNumIntraCands];
     __shared__ int prev_mode[kMaxSliceRows];
+    __shared__ uint8_t row_mode[kMaxSliceRows][kIntraMaxMbW];  // each row's modes (MPM of the row below)
     fill_mats(M);
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -987,7 +996,12 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         const int x0 = x * 16, y0 = y * 16;
         const uint32_t sy4 = nsy, sc2 = nsc;
         load_src(x + 1, nsy, nsc);
-        const bool al = x > 0, at = row > 0, atr = at && x + 1 < g.mb_w, ac = at && x > 0;
+        // availability in the decoder's z order: a CTB's last unit has no above-right; its first
+        // unit's below-left (the left CTB's last unit) is available there but not reconstructed yet
+        // by this raster wavefront, so that unit keeps to the modes that never read it
+        const int z = ((y & 1) << 1) | (x & 1);
+        const bool al = x > 0, at = row > 0, atr = at && x + 1 < g.mb_w && z != 3, ac = at && x > 0;
+        const bool bl_pending = z == 0 && x > 0 && y + 1 < g.mb_h;
         // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
         if (valid) {
             if (lane < 16) {
@@ -1055,6 +1069,8 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         int mode = 1;
         if (valid) {
             const int cand_a = al ? prev_mode[row] : 1;
+            const int cand_b = (at && (y & 1)) ? (int)row_mode[row - 1][x] : 1;  // above only inside the CTB
+            const uint64_t safe = fs->bl_safe;
             const int r = lane >> 2, cb = (lane & 3) * 4;
             // every candidate's partial SAD first (independent work), then the wave reductions
             int sad[kNumIntraCands];
@@ -1073,7 +1089,8 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             for (int m = 0; m < kNumIntraCands; ++m) {
                 if (m % H != sub) continue;
                 const int s = wsum(sad[m]);
-                if (lane == 0) mode_cost[row][m] = s + lambda * intra_mode_bits(kIntraCands[m], cand_a);
+                const bool ok = !bl_pending || ((safe >> kIntraCands[m]) & 1);
+                if (lane == 0) mode_cost[row][m] = ok ? s + lambda * intra_mode_bits(kIntraCands[m], cand_a, cand_b) : 0x7fffffff;
             }
         }
         __syncthreads();
@@ -1112,11 +1129,14 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 c.mvx = c.mvy = c.mvdx = c.mvdy = 0;
                 c.mvp_idx = 0;
                 fill_cu(c, res);
+                c.ct = 1;
+                for (int k = 0; k < 7; ++k) c.rsv[k] = 0;
                 set_est_bytes(c, res.bits);
                 cus[i] = c;
-                cost[i] = cu_cost(c);
+                // (no slice cost: I pictures use fixed CTB-row slices)
                 qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
                 prev_mode[row] = mode;
+                row_mode[row][x] = (uint8_t)mode;
             }
         }
         __syncthreads();
@@ -1221,6 +1241,7 @@ __device__ __forceinline__ uint32_t tile_thread_prefix(const uint32_t (*wave_tot
 // thresholds and a CU's slice id (plan_slice_of of its cost prefix) is also its slice's rank:
 // every CU places itself from its prefix alone (the former one-workgroup kernel walked the
 // tiles in sequence: 39 us at 4K).
+// (Everything here counts 32x32 CTBs: ncu = the CTB count, ctb_w = CTBs per row, cost per CTB.)
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ cost, int ncu, int ctb_w,
                                                        int max_slices, int slice_cost, int* __restrict__ slice_first,
@@ -1230,7 +1251,7 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
         for (int k = tid; k < kSseSlots * kSseSlotWords; k += blockDim.x) fs->sse_tot[k] = 0ull;  // k_hevc_sao adds into these next
     if (fs->idr || fs->wpp) {  // I: fixed row slices; P with WPP: slices of wpp_rows rows (a substream per row)
         const int rows = ncu / ctb_w;
-        const int sr = fs->idr ? fs->slice_rows : fs->wpp_rows;
+        const int sr = fs->idr ? fs->slice_rows / 2 : fs->wpp_rows;  // (slice_rows counts 16x16-unit rows)
         const int S = fs->idr ? fs->num_slices : (rows + sr - 1) / sr;
         const int stride = (int)(gridDim.x * blockDim.x);
         for (int k = t * (int)blockDim.x + tid; k < S; k += stride) slice_first[k] = k * sr * ctb_w;
@@ -1260,19 +1281,28 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     if (t == 0 && tid == 0) *nslices = (uint32_t)S;
 }
 
-// Skip / merge / AMVP of every CU of a P picture against its slice's neighbours.
+// Skip / merge / AMVP of the units of a P picture against their slice's neighbours and the coding
+// tree of every CTB (hevc_core.h decide_ctb): one thread per CTB.
 __global__ __launch_bounds__(256) void k_hevc_decide(Geometry g, const h264::MbInfo* __restrict__ mbs,
                                                       const int* __restrict__ slice_first,
-                                                      const int* __restrict__ slice_of_cu, CuInfo* __restrict__ cus) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= g.mb_w * g.mb_h) return;
+                                                      const int* __restrict__ slice_of_ctb, CuInfo* __restrict__ cus) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int cw = ctb_cols(g.mb_w);
+    if (c >= cw * ctb_rows(g.mb_h)) return;
     constexpr int kStride = sizeof(h264::MbInfo) / sizeof(int16_t);
-    MvCand a1, b1, b0, b2;
-    inter_neighbours(&mbs[0].mvx, kStride, i % g.mb_w, i / g.mb_w, g.mb_w, slice_first[slice_of_cu[i]], &a1, &b1, &b0,
-                     &b2);
-    CuInfo c = cus[i];
-    decide_inter(c, a1, b1, b0, b2);
-    cus[i] = c;
+    const int x0 = 2 * (c % cw), y0 = 2 * (c / cw);
+    CuInfo u[4];
+    bool in[4];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+        const int x = x0 + (z & 1), y = y0 + (z >> 1);
+        in[z] = x < g.mb_w && y < g.mb_h;
+        if (in[z]) u[z] = cus[y * g.mb_w + x];
+    }
+    decide_ctb(u, in, &mbs[0].mvx, kStride, x0, y0, g.mb_w, g.mb_h, slice_first[slice_of_ctb[c]]);
+#pragma unroll
+    for (int z = 0; z < 4; ++z)
+        if (in[z]) cus[(y0 + (z >> 1)) * g.mb_w + x0 + (z & 1)] = u[z];
 }
 
 __device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
@@ -1297,30 +1327,41 @@ __device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
 // v_writelane), so the serial part is a few dozen scalar instructions per token and fits the
 // instruction cache (the former single-phase kernel was 16 k instructions of CU syntax per wave
 // and took ~0.8 us per skipped CTU: profiles/r03_cabac).
+// One wave per coding position (4 per CTB, z order; positions outside the picture emit nothing).
+struct CuGet {  // wave-uniform CuInfo loads for unit_syn
+    const CuInfo* p;
+    __device__ __forceinline__ CuInfo operator()(int u) const { return load_cu(p, u); }
+};
 __global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameState* __restrict__ fs,
                                                    const CuInfo* __restrict__ cus, const int16_t* __restrict__ coef,
                                                    const uint32_t* __restrict__ sao,
                                                    const int* __restrict__ slice_first,
-                                                   const int* __restrict__ slice_of_cu,
+                                                   const int* __restrict__ slice_of_ctb,
                                                    const uint32_t* __restrict__ nslices,
-                                                   const uint8_t* __restrict__ qpy, uint16_t* __restrict__ tok,
+                                                   const uint8_t* __restrict__ qp_pred, uint16_t* __restrict__ tok,
                                                    uint32_t* __restrict__ ntok) {
     __shared__ uint16_t stage[64 * kPartTokens];
-    const int ncu = g.mb_w * g.mb_h;
-    const int i = blockIdx.x, lane = threadIdx.x;
+    const int k = blockIdx.x, lane = threadIdx.x;
+    const int cw = ctb_cols(g.mb_w), nctb = cw * ctb_rows(g.mb_h);
+    int x, y;
+    cpos_xy(k, cw, &x, &y);
+    if (x >= g.mb_w || y >= g.mb_h) {
+        if (lane == 0) ntok[k] = 0;
+        return;
+    }
+    const int i = y * g.mb_w + x, c = k >> 2;
     const int ns = (int)uni(*nslices);
-    const int s = uni(slice_of_cu[i]);
+    const int s = uni(slice_of_ctb[c]);
     const int first = uni(slice_first[s]);
-    const int end = s + 1 < ns ? uni(slice_first[s + 1]) : ncu;
-    const int k = i - first;
-    const bool wpp = fs->wpp != 0;
-    const int qp_prev = qp_prev_resets(i, k, g.mb_w, wpp) ? fs->qp : (int)uni((uint32_t)qpy[i - 1]);
-    const CuInfo c = load_cu(cus, i);
+    const int end = s + 1 < ns ? uni(slice_first[s + 1]) : nctb;
+    const UnitSyn u = unit_syn(CuGet{cus}, fs->sao ? sao : nullptr, x, y, g.mb_w, g.mb_h, fs->idr != 0, first, end,
+                               fs->wpp != 0, fs->depth_inter, (int)uni((uint32_t)qp_pred[i]));
+    const CuInfo cu = load_cu(cus, i);
     const CoefArray cf{coef + (size_t)i * kCoefPerCu};
-    // lane p binarises part p of the CTU (coding order) into its LDS run
+    // lane p binarises part p of the unit (coding order) into its LDS run
     CtuPart mine;
     bool have = false;
-    for_each_part(c, cf, [&](const CtuPart& pt, int idx) {
+    for_each_part(cu, u, cf, [&](const CtuPart& pt, int idx) {
         if (idx == lane) {
             mine = pt;
             have = true;
@@ -1328,22 +1369,21 @@ __global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameSta
     });
     BinRec rec;
     rec.start(stage + lane * kPartTokens, kPartTokens);
-    if (have)
-        binarise_part(rec, mine, fs->idr != 0, cus, cf, fs->sao ? sao : nullptr, i, k, end - first, g.mb_w, qp_prev,
-                      wpp);
+    NoCtx nc;
+    if (have) binarise_part(rec, nc, mine, cu, u, cf);
     const uint32_t n = have ? min(rec.n, kPartTokens) : 0u;
     uint32_t incl = n;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(incl, o, 64);
         if (lane >= o) incl += t;
     }
-    uint16_t* dst = tok + (size_t)i * kMaxCuTokens + (incl - n);
+    uint16_t* dst = tok + (size_t)k * kMaxCuTokens + (incl - n);
     const uint16_t* src = stage + lane * kPartTokens;
     for (uint32_t j = 0; j < n; ++j) dst[j] = src[j];
-    if (lane == 63) ntok[i] = incl;
+    if (lane == 63) ntok[k] = incl;
 }
 
-// Exclusive prefix of the token counts in decoding (raster) order: off[i], off[ncu] = total.
+// Exclusive prefix of the token counts in decoding order (coding positions): off[k], off[n] = total.
 // One 1024-thread workgroup per scan tile (tile_prefixes), 16-byte loads and stores.
 __global__ __launch_bounds__(1024) void k_hevc_tokscan(const uint32_t* __restrict__ ntok, int ncu,
                                                         uint32_t* __restrict__ off) {
@@ -1493,26 +1533,27 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
                                                     uint8_t* __restrict__ slice_data, uint32_t slice_cap,
                                                     uint32_t* __restrict__ slice_len,
                                                     unsigned long long* __restrict__ slice_clk) {
+    // (slices and substreams in CTBs; a CTB's tokens are coding positions 4 c .. 4 c + 3)
     const int u = blockIdx.x, lane = threadIdx.x;
     const bool wpp = fs->wpp != 0;
-    const int ncu = g.mb_w * g.mb_h;
-    const int nsub = wpp ? g.mb_h : (int)*nslices;
+    const int cw = ctb_cols(g.mb_w), nctb = cw * ctb_rows(g.mb_h);
+    const int nsub = wpp ? ctb_rows(g.mb_h) : (int)*nslices;
     if (u >= nsub) return;
     const unsigned long long clk0 = wall_clock64();
     int first, end;
     bool fresh = true, store = false;
     if (wpp) {
-        first = u * g.mb_w;
-        end = first + g.mb_w;
+        first = u * cw;
+        end = first + cw;
         const int s = slice_of_cu[first];
-        fresh = first == slice_first[s] || g.mb_w < 2;
-        store = g.mb_w >= 2 && end < ncu && slice_of_cu[end] == s;
+        fresh = first == slice_first[s] || cw < 2;
+        store = cw >= 2 && end < nctb && slice_of_cu[end] == s;
     } else {
         const int ns = nsub;
         first = slice_first[u];
-        end = u + 1 < ns ? slice_first[u + 1] : ncu;
+        end = u + 1 < ns ? slice_first[u + 1] : nctb;
     }
-    const uint32_t t0 = uni(off[first]), t1 = uni(off[end]);
+    const uint32_t t0 = uni(off[4 * first]), t1 = uni(off[4 * end]);
     const int qp = fs->qp;
     PackedCtx ctx;
     ctx.lps_row = (uint32_t)kLps[lane][0] | ((uint32_t)kLps[lane][1] << 8) | ((uint32_t)kLps[lane][2] << 16) |
@@ -1551,7 +1592,7 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
     // two segments through one copy of the coder loop (the kernel stays inside the instruction
     // cache): the row's first two CTUs, the context publication (storage process after CTU 1),
     // then the rest; without a publication the first segment is empty
-    const uint32_t ts = store ? uni(off[first + 2]) : t0;
+    const uint32_t ts = store ? uni(off[4 * (first + 2)]) : t0;
 #pragma unroll 1
     for (int seg = 0; seg < 2; ++seg) {
         arith_run(lc, ctx, dense, seg ? ts : t0, seg ? t1 : ts, lane);
@@ -1570,42 +1611,85 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
     }
 }
 
-// ------------------------------------------------------------------ deblocking
-// QpY of every CU (hevc_core.h slice_qpy): the QP of the last CU at or before it in its slice
-// that coded a residual, else the slice QP.  One workgroup per slice; qpc holds (QP or 255) per
-// CU from the analysis kernels; a block max-scan of (index << 8 | QP) over 256-CU chunks with
-// the previous chunk's maximum carried in.
-// With WPP the chain restarts at every CTU row (8.6.1), so the workgroups take rows instead.
-__global__ __launch_bounds__(256) void k_hevc_qpy(const HevcFrameState* __restrict__ fs,
-                                                   const uint8_t* __restrict__ qpc, int ncu, int ctb_w,
+// ------------------------------------------------------------------ QP chain
+// qPY_PRED / QpY of every unit (hevc_core.h slice_qp_chain): one workgroup per chain -- a slice, or
+// with WPP a CTB row (the chain restarts at every row).  The chain is serial but cheap once its
+// inputs sit in LDS: the threads stage 256 CTBs at a time (the four units' coded QP -- qpc, 255
+// when the unit sends no cu_qp_delta -- and the CTB's coding-tree depth), thread 0 walks them,
+// then every thread stores its CTB's results.
+__global__ __launch_bounds__(256) void k_hevc_qpy(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                   const CuInfo* __restrict__ cus, const uint8_t* __restrict__ qpc,
                                                    const int* __restrict__ slice_first,
-                                                   const uint32_t* __restrict__ nslices, uint8_t* __restrict__ qpy) {
-    __shared__ int wmaxv[4];
-    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ns = fs->wpp ? ncu / ctb_w : (int)*nslices;
+                                                   const uint32_t* __restrict__ nslices,
+                                                   uint8_t* __restrict__ qp_pred, uint8_t* __restrict__ qpy) {
+    __shared__ uint32_t q4[256], pr4[256], qy4[256];
+    __shared__ uint8_t info[256];  // bits 0-3: unit z inside the picture, bit 4: CU32
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const int cw = ctb_cols(g.mb_w), ch = ctb_rows(g.mb_h), nctb = cw * ch;
+    const bool wpp = fs->wpp != 0;
+    const int ns = wpp ? ch : (int)*nslices;
     if (s >= ns) return;
-    const int first = fs->wpp ? s * ctb_w : slice_first[s];
-    const int end = fs->wpp ? first + ctb_w : (s + 1 < ns ? slice_first[s + 1] : ncu);
-    int carry = -1;
+    const int first = wpp ? s * cw : slice_first[s];
+    const int end = wpp ? first + cw : (s + 1 < ns ? slice_first[s + 1] : nctb);
+    int prev = fs->qp;  // thread 0's chain state
     for (int base = first; base < end; base += 256) {
-        const int i = base + tid;
-        const int q = i < end ? qpc[i] : 255;
-        int key = q != 255 ? ((i << 8) | q) : -1;
-        for (int o = 1; o < 64; o <<= 1) {  // inclusive max-scan within the wave
-            const int t = __shfl_up(key, o, 64);
-            if (lane >= o) key = max(key, t);
+        const int c = base + tid;
+        const int x0 = 2 * (c % cw), y0 = 2 * (c / cw);
+        if (c < end) {
+            uint32_t w = 0, in = 0;
+            for (int z = 0; z < 4; ++z) {
+                const int x = x0 + (z & 1), y = y0 + (z >> 1);
+                const bool inside = x < g.mb_w && y < g.mb_h;
+                w |= (inside ? (uint32_t)qpc[y * g.mb_w + x] : 255u) << (8 * z);
+                in |= inside ? 1u << z : 0u;
+            }
+            q4[tid] = w;
+            info[tid] = (uint8_t)(in | (cus[y0 * g.mb_w + x0].ct == 0 ? 16u : 0u));
         }
-        if (lane == 63) wmaxv[wave] = key;
         __syncthreads();
-        for (int w = 0; w < wave; ++w) key = max(key, wmaxv[w]);
-        key = max(key, carry);
-        if (i < end) qpy[i] = (uint8_t)(key >= 0 ? (key & 255) : fs->qp);
-        const int chunk_max = max(max(wmaxv[0], wmaxv[1]), max(wmaxv[2], wmaxv[3]));
-        carry = max(carry, chunk_max);
+        if (tid == 0) {
+            const int n = min(256, end - base);
+            for (int j = 0; j < n; ++j) {
+                const uint32_t w = q4[j], f = info[j];
+                uint32_t pw = 0, qw = 0;
+                if (f & 16) {  // CU32: one quantization group, one QP
+                    int q = prev;
+                    for (int z = 0; z < 4; ++z)
+                        if (((w >> (8 * z)) & 255u) != 255u) q = (int)((w >> (8 * z)) & 255u);
+                    pw = (uint32_t)prev * 0x01010101u;
+                    qw = (uint32_t)q * 0x01010101u;
+                    prev = q;
+                } else {
+                    int qz[4] = {0, 0, 0, 0};
+                    for (int z = 0; z < 4; ++z) {
+                        if (!((f >> z) & 1)) continue;
+                        const int qa = (z & 1) ? qz[z - 1] : prev, qb = (z & 2) ? qz[z - 2] : prev;
+                        const int pred = (qa + qb + 1) >> 1;
+                        const uint32_t v = (w >> (8 * z)) & 255u;
+                        const int q = v != 255u ? (int)v : pred;
+                        qz[z] = q;
+                        pw |= (uint32_t)pred << (8 * z);
+                        qw |= (uint32_t)q << (8 * z);
+                        prev = q;
+                    }
+                }
+                pr4[j] = pw;
+                qy4[j] = qw;
+            }
+        }
+        __syncthreads();
+        if (c < end)
+            for (int z = 0; z < 4; ++z) {
+                const int x = x0 + (z & 1), y = y0 + (z >> 1);
+                if (x >= g.mb_w || y >= g.mb_h) continue;
+                qp_pred[y * g.mb_w + x] = (uint8_t)(pr4[tid] >> (8 * z));
+                qpy[y * g.mb_w + x] = (uint8_t)(qy4[tid] >> (8 * z));
+            }
         __syncthreads();
     }
 }
 
+// ------------------------------------------------------------------ deblocking
 // One thread per 4-sample segment of a CU's left (dir 0) or top (dir 1) edge.  Vertical
 // edges are 16 samples apart and a filter reads p3..q3 / writes p2..q2, so all segments of a
 // direction are independent; the horizontal pass runs as a second launch on its output.
@@ -1742,21 +1826,32 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
                                                    const CuInfo* __restrict__ cus, uint32_t* __restrict__ prm) {
     __shared__ SaoWave sw[4];
     __shared__ unsigned long long part[4][4];
+    // one workgroup per 32x32 CTB, wave z = its 16x16 unit in z order: every wave gathers its unit's
+    // statistics, then every wave decides from the CTB's sums (the same words in each) and applies
+    // the offsets to its own unit
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ncu = g.mb_w * g.mb_h;
-    const int i = blockIdx.x * 4 + wave;
-    const bool valid = i < ncu;
-    const int x0 = valid ? (i % g.mb_w) * kCtb : 0, y0 = valid ? (i / g.mb_w) * kCtb : 0;
+    const int bid = blockIdx.x, cw = ctb_cols(g.mb_w);
+    const int ux = 2 * (bid % cw) + (wave & 1), uy = 2 * (bid / cw) + (wave >> 1);
+    const bool valid = ux < g.mb_w && uy < g.mb_h;
+    const int i = valid ? uy * g.mb_w + ux : 0;
+    const int x0 = valid ? ux * kCtb : 0, y0 = valid ? uy * kCtb : 0;
     SaoWave& S = sw[wave];
     const uint8_t* ry = fs->rec_y;
     const uint8_t* ruv = fs->rec_uv;
     const int W = g.coded_w, H = g.coded_h, Wc = W / 2, Hc = H / 2;
     for (int k = lane; k < 96; k += 64) (&S.bo[0][0])[k] = 0;
+    if (lane < 48) (&S.eo[0][0])[lane] = 0;
     sao_wave_sync();
     const int r = lane >> 2, c0 = (lane & 3) * 4;
     const int xc = x0 / 2 + (lane & 7), yc = y0 / 2 + (lane >> 3);
-    // no residual in a P picture (sao_keep_ctb): SAO off, the samples are only copied and measured
-    const bool keep = valid && sao_keep_ctb(fs->idr != 0, cus[i]);  // wave-uniform (one CTB per wave)
+    // no residual anywhere in the CTB of a P picture (sao_keep_ctb): SAO off, the samples are only
+    // copied and measured
+    uint32_t any = 0;
+    for (int z = 0; z < 4; ++z) {
+        const int x = 2 * (bid % cw) + (z & 1), y = 2 * (bid / cw) + (z >> 1);
+        if (x < g.mb_w && y < g.mb_h) any |= cus[y * g.mb_w + x].cbf;
+    }
+    const bool keep = sao_keep_ctb(fs->idr != 0, any);  // workgroup-uniform
     // ---- statistics (the edge categories and centre samples are kept for the apply phase)
     uint64_t cat_y = 0;
     uint32_t cen_y = 0, cat_u = 0, cat_v = 0, cen_uv = 0;
@@ -1806,13 +1901,14 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         t = sao_reduce16(e, lane);
         if ((lane & 3) == 0) S.eo[2][(lane >> 2) & 15] = t;
     }
-    sao_wave_sync();
-    // ---- candidate offsets per (comp, class, category) and per (comp, band)
+    __syncthreads();  // the CTB's four units' statistics
+    // ---- candidate offsets per (comp, class, category) and per (comp, band) from the CTB's sums
+    // (packed counts add up: at most 1,024 samples per CTB component)
     const uint32_t lam16 = kLambdaSse16[fs->qp < 0 ? 0 : (fs->qp > 51 ? 51 : fs->qp)];
     if (valid && !keep) {
         if (lane < 48) {
             const int comp = lane >> 4, q = lane & 15, cat = q & 3;
-            const int v = S.eo[comp][q];
+            const int v = sw[0].eo[comp][q] + sw[1].eo[comp][q] + sw[2].eo[comp][q] + sw[3].eo[comp][q];
             int o;
             S.jeo[comp][q] = sao_best_offset(sao_unpack_sum(v), sao_unpack_cnt(v), cat < 2 ? 0 : -7, cat < 2 ? 7 : 0,
                                              false, lam16, &o);
@@ -1820,7 +1916,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         }
         for (int t = lane; t < 96; t += 64) {
             const int comp = t >> 5, b = t & 31;
-            const int v = S.bo[comp][b];
+            const int v = sw[0].bo[comp][b] + sw[1].bo[comp][b] + sw[2].bo[comp][b] + sw[3].bo[comp][b];
             int o;
             S.jb[comp][b] = sao_best_offset(sao_unpack_sum(v), sao_unpack_cnt(v), -7, 7, true, lam16, &o);
             S.ob[comp][b] = o;
@@ -1864,7 +1960,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
         S.w[0] = w[0];
         S.w[1] = w[1];
         S.w[2] = w[2];
-        *reinterpret_cast<uint4*>(prm + 4 * (size_t)i) = make_uint4(w[0], w[1], w[2], 0u);
+        if (wave == 0) *reinterpret_cast<uint4*>(prm + 4 * (size_t)bid) = make_uint4(w[0], w[1], w[2], 0u);
     }
     sao_wave_sync();
     // ---- apply into the output picture; distortion over the display area
@@ -1896,8 +1992,8 @@ __global__ __launch_bounds__(256) void k_hevc_sao(Geometry g, const HevcFrameSta
     eu = wsum(eu);
     ev = wsum(ev);
     if (lane == 0) {
-        // 4th channel: luma of CTBs outside the quality-report mask
-        const int cx = i % g.mb_w, cy = i / g.mb_w;
+        // 4th channel: luma of units outside the quality-report mask
+        const int cx = ux, cy = uy;
         const bool in_mask = cx >= fs->mask_c[0] && cx < fs->mask_c[2] && cy >= fs->mask_c[1] && cy < fs->mask_c[3];
         part[0][wave] = (unsigned long long)ey;
         part[1][wave] = (unsigned long long)eu;
@@ -1999,7 +2095,8 @@ __device__ void pack_body(Geometry g, const HevcFrameState* __restrict__ fs, con
     __shared__ unsigned long long red64[4][256];
     const int s = blockIdx.x, tid = threadIdx.x;
     const bool wpp = fs->wpp != 0;
-    const int num_slices = wpp ? g.mb_h : (int)*nslices;  // substreams
+    const int cw = ctb_cols(g.mb_w);
+    const int num_slices = wpp ? ctb_rows(g.mb_h) : (int)*nslices;  // substreams
     if (s >= num_slices) return;
     // offset of this slice: sum of the 16-byte rounded lengths before it
     uint32_t part = 0;
@@ -2022,7 +2119,7 @@ __device__ void pack_body(Geometry g, const HevcFrameState* __restrict__ fs, con
         uint32_t* offs = reinterpret_cast<uint32_t*>(host_out + sizeof(HevcOutHeader));
         offs[s] = off;
         offs[kMaxSlices + s] = len;
-        const int fc = wpp ? s * g.mb_w : slice_first[s];
+        const int fc = wpp ? s * cw : slice_first[s];  // first CTB
         const bool starts = !wpp || slice_first[slice_of_cu[fc]] == fc;
         offs[2 * kMaxSlices + s] = (uint32_t)fc | (starts ? kSubSliceStart : 0u);
     }
@@ -2108,15 +2205,16 @@ void launch_hevc_save_src(const Geometry& g, const HevcDeviceBuffers& b, const u
 
 void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                        hipStream_t s) {
-    const int ncu = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_hevc_inter, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, b.me.mb, src_y, src_uv, b.cu,
-                       b.coef, b.cost, b.qpc);
+    const int nctb = ctb_cols(g.mb_w) * ctb_rows(g.mb_h);
+    hipLaunchKernelGGL(k_hevc_inter, dim3(nctb), dim3(256), 0, s, g, b.fs, b.me.mb, src_y, src_uv, b.cu, b.coef, b.cost,
+                       b.qpc);
 }
 
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
+    if (g.mb_w > kIntraMaxMbW) throw std::invalid_argument("hevc: picture too wide for the intra wavefront");
     const size_t lds = (size_t)slice_rows * 2 * g.coded_w;
-    const int helpers = std::max(1, kMaxSliceRows / slice_rows);  // waves per CTU row (k_hevc_intra)
+    const int helpers = std::max(1, kMaxSliceRows / slice_rows);  // waves per unit row (k_hevc_intra)
     hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows * helpers), lds, s, g, b.fs, src_y, src_uv,
                        b.cu, b.coef, b.cost, b.qpc);
 }
@@ -2124,34 +2222,36 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,
                         bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
     const int ncu = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_hevc_layout, dim3((ncu + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.fs, b.cost, ncu, g.mb_w, max_slices, slice_cost, b.slice_first,
-                       b.slice_of_cu, b.nslices);
+    const int cw = ctb_cols(g.mb_w), nctb = cw * ctb_rows(g.mb_h);
+    hipLaunchKernelGGL(k_hevc_layout, dim3((nctb + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.fs, b.cost, nctb, cw,
+                       max_slices, slice_cost, b.slice_first, b.slice_of_cu, b.nslices);
     if (!idr)
-        hipLaunchKernelGGL(k_hevc_decide, dim3((ncu + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
+        hipLaunchKernelGGL(k_hevc_decide, dim3((nctb + 255) / 256), dim3(256), 0, s, g, b.me.mb, b.slice_first,
                            b.slice_of_cu, b.cu);
     // QpY chain: the deblocking filter's QP and the entropy coder's QP predictor
-    hipLaunchKernelGGL(k_hevc_qpy, dim3(std::max(max_slices, g.mb_h)), dim3(256), 0, s, b.fs, b.qpc, ncu, g.mb_w,
-                       b.slice_first, b.nslices, b.qpy);
+    hipLaunchKernelGGL(k_hevc_qpy, dim3(std::max(max_slices, ctb_rows(g.mb_h))), dim3(256), 0, s, g, b.fs, b.cu, b.qpc,
+                       b.slice_first, b.nslices, b.qp_pred, b.qpy);
     if (deblock) {
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
     }
-    if (sao)  // SAO, with the final distortion (one partial per 4 CTBs)
-        hipLaunchKernelGGL(k_hevc_sao, dim3((ncu + 3) / 4), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.cu, b.sao);
+    if (sao)  // SAO per CTB, with the final distortion (one partial per CTB)
+        hipLaunchKernelGGL(k_hevc_sao, dim3(nctb), dim3(256), 0, s, g, b.fs, src_y, src_uv, b.cu, b.sao);
     else if (deblock)
         hipLaunchKernelGGL(k_hevc_sse, dim3(g.mb_h), dim3(256), 0, s, g, b.fs, src_y, src_uv);
 }
 
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s) {
-    const int ncu = g.mb_w * g.mb_h;
-    if ((ncu + kScanTile - 1) / kScanTile > kMaxScanTiles) throw std::invalid_argument("hevc: picture too large");
-    hipLaunchKernelGGL(k_hevc_bins, dim3(ncu), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.sao,
-                       b.slice_first, b.slice_of_cu, b.nslices, b.qpy, b.tok, b.ntok);
-    hipLaunchKernelGGL(k_hevc_tokscan, dim3((ncu + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.ntok, ncu, b.tok_off);
-    hipLaunchKernelGGL(k_hevc_tokgather, dim3((ncu + 3) / 4), dim3(256), 0, s, b.tok, b.ntok, b.tok_off, ncu,
+    const int npos = 4 * ctb_cols(g.mb_w) * ctb_rows(g.mb_h);  // coding positions
+    if ((npos + kScanTile - 1) / kScanTile > kMaxScanTiles) throw std::invalid_argument("hevc: picture too large");
+    hipLaunchKernelGGL(k_hevc_bins, dim3(npos), dim3(64), 0, s, g, b.fs, b.cu, b.coef, b.sao, b.slice_first,
+                       b.slice_of_cu, b.nslices, b.qp_pred, b.tok, b.ntok);
+    hipLaunchKernelGGL(k_hevc_tokscan, dim3((npos + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.ntok, npos,
+                       b.tok_off);
+    hipLaunchKernelGGL(k_hevc_tokgather, dim3((npos + 3) / 4), dim3(256), 0, s, b.tok, b.ntok, b.tok_off, npos,
                        b.tok_dense);
-    const int max_subs = std::max(max_slices, g.mb_h);  // substreams: slices, or CTU rows with WPP
+    const int max_subs = std::max(max_slices, ctb_rows(g.mb_h));  // substreams: slices, or CTB rows with WPP
     hipLaunchKernelGGL(k_hevc_arith, dim3(max_subs), dim3(64), 0, s, g, b.fs, b.tok_dense, b.tok_off,
                        b.slice_first, b.slice_of_cu, b.nslices, b.slice_data, b.slice_cap, b.slice_len, b.slice_clk);
     hipLaunchKernelGGL(k_hevc_pack, dim3(max_subs), dim3(256), 0, s, g, b.fs, b.nslices, b.slice_first, b.slice_of_cu,

@@ -83,22 +83,22 @@ def test_cpu_hevc_rate_control_and_idr(native):
 
 
 def test_cpu_hevc_two_row_slices(native):
-    # 352x288 @ 30 fps is level 2 (16 slice segments) -> 18 CTU rows need 2-row slices, which
+    # 192x544 @ 30 fps is level 2 (16 slice segments) -> 17 CTB rows need 2-row slices, which
     # exercises above-neighbour intra references, merge/AMVP B candidates and skip contexts
-    _, _, _, dec, enc = _cpu_roundtrip(native, 352, 288, 2, fps=30, qp=30, wpp=1)
+    _, _, _, dec, enc = _cpu_roundtrip(native, 192, 544, 2, fps=30, qp=30, wpp=1)
     assert enc.slice_rows == 2
     assert dec.stats["slices"] == 9 + 3  # 9 two-row slices in the IDR picture, 8-row WPP slices in the P picture
-    assert dec.stats["substreams"] == 18 + 18  # one per CTU row: 9 slices x 2 rows, then 18 rows
+    assert dec.stats["substreams"] == 17 + 17  # one per CTB row: 9 slices (8 x 2 rows + 1), then 17 rows
 
 
 @pytest.mark.parametrize("w,h,wpp,rows", [(16, 64, 1, 0), (32, 48, 1, 0), (160, 96, 1, 0), (160, 96, 0, 0),
                                            (200, 120, 1, 0), (160, 96, 1, 2), (200, 120, 1, 3)])
 def test_cpu_hevc_wpp_substreams_decode(native, w, h, wpp, rows):
-    """Wavefront substreams (one per CTU row; context sync from the row above's second CTU, none
-    for a one-CTU-wide picture; QP predictor reset per row; entry points = escaped substream
+    """Wavefront substreams (one per CTB row; context sync from the row above's second CTB, none
+    for a one-CTB-wide picture; QP predictor reset per row; entry points = escaped substream
     sizes, checked by the decoder) decode to the reconstruction, I and P pictures, with the
     slice-per-substream layout (wpp 0) as the control; rows > 0 splits P pictures into slices of
-    that many CTU rows, each with its own wavefront (fresh contexts at every slice start)."""
+    that many CTB rows, each with its own wavefront (fresh contexts at every slice start)."""
     cfg = _cfg(native, w, h, qp=26, aq=1)
     cfg.hevc_wpp = wpp
     cfg.hevc_wpp_rows = rows
@@ -112,7 +112,7 @@ def test_cpu_hevc_wpp_substreams_decode(native, w, h, wpp, rows):
     dec.decode(stream)
     for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
         assert np.array_equal(yy, ry) and np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
-    ctb_h = (h + 15) // 16
+    ctb_h = (h + 31) // 32  # 32x32 CTB rows
     assert dec.stats.get("substreams", 0) == (4 * ctb_h if wpp else 0)
     if wpp and rows:
         assert dec.stats["slices"] >= 4 * -(-ctb_h // rows)
