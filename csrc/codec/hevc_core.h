@@ -1838,11 +1838,6 @@ MXHD uint32_t code_slice(uint8_t* out, uint32_t cap, bool islice, int slice_qp, 
 }
 
 // ---------------------------------------------------------------- encoder decisions
-// Intra candidates tried by the encoder, in tie-break order (any of the 35 modes decodes).
-// DC, planar, vertical, horizontal, then the three 45-degree diagonals (down-right, down-left,
-// up-right) and the near-vertical 22 -- UI edges, text strokes and rotated / natural content
-constexpr int kNumIntraCands = 8;
-constexpr uint8_t kIntraCands[kNumIntraCands] = {1, 0, 26, 10, 18, 2, 34, 22};
 // Approximate luma mode signalling cost in bins given the MPM candidates of the left / above PU.
 MXHD int intra_mode_bits(int mode, int cand_a, int cand_b) {
     int l[3];

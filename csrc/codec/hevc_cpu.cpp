@@ -397,17 +397,67 @@ void summarise(CuInfo& c, const int16_t* coef) {
 }
 }  // namespace
 
+// Open-loop intra mode of the 16x16 unit (x, y) of a picture of mb_w x mb_h units in I slices of
+// sr unit rows (k_hevc_intra_modes on the GPU): all 35 modes predicted from the *source*
+// neighbours with the decoder's z-order availability (never the below-left; a CTB's first unit only
+// uses the modes in `safe` -- bl_safe_modes -- because the raster wavefront reconstructs it before
+// its below-left), scored by the 4x4 Hadamard SATD of the residual + lambda * mode bits; the lowest
+// cost wins, ties to the lower mode.
+int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int qp, uint64_t safe) {
+    const int x0 = x * 16, y0 = y * 16, z = ((y & 1) << 1) | (x & 1);
+    const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < mb_w && z != 3, ac = at && x > 0;
+    const bool bl_pending = z == 0 && x > 0 && y + 1 < mb_h;
+    uint8_t lp[16], tp[16], tr[16];
+    for (int k = 0; k < 16; ++k) {
+        lp[k] = al ? sy[(size_t)(y0 + k) * pitch + x0 - 1] : 0;
+        tp[k] = at ? sy[(size_t)(y0 - 1) * pitch + x0 + k] : 0;
+        tr[k] = atr ? sy[(size_t)(y0 - 1) * pitch + x0 + 16 + k] : 0;
+    }
+    const int corner = ac ? sy[(size_t)(y0 - 1) * pitch + x0 - 1] : 0;
+    int L[33], T[33], pred[256];
+    intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
+    const int lambda = h264::lambda_sad(qp);
+    int best = 1, best_cost = 0x7fffffff;
+    for (int m = 0; m < 35; ++m) {
+        if (bl_pending && !((safe >> m) & 1)) continue;
+        intra_predict(m, 4, 0, L, T, pred);
+        int satd = 0;
+        for (int by = 0; by < 16; by += 4)
+            for (int bx = 0; bx < 16; bx += 4) {
+                int d[4][4], h[4][4];
+                for (int r = 0; r < 4; ++r)
+                    for (int q = 0; q < 4; ++q)
+                        d[r][q] = (int)sy[(size_t)(y0 + by + r) * pitch + x0 + bx + q] - pred[(by + r) * 16 + bx + q];
+                for (int r = 0; r < 4; ++r) {  // rows, then columns: 4-point Walsh-Hadamard
+                    const int a0 = d[r][0] + d[r][1], a1 = d[r][0] - d[r][1], a2 = d[r][2] + d[r][3], a3 = d[r][2] - d[r][3];
+                    h[r][0] = a0 + a2;
+                    h[r][1] = a1 + a3;
+                    h[r][2] = a0 - a2;
+                    h[r][3] = a1 - a3;
+                }
+                for (int q = 0; q < 4; ++q) {
+                    const int a0 = h[0][q] + h[1][q], a1 = h[0][q] - h[1][q], a2 = h[2][q] + h[3][q], a3 = h[2][q] - h[3][q];
+                    satd += std::abs(a0 + a2) + std::abs(a1 + a3) + std::abs(a0 - a2) + std::abs(a1 - a3);
+                }
+            }
+        const int cost = satd + lambda * intra_mode_bits(m, 1, 1);
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = m;
+        }
+    }
+    return best;
+}
+
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
     uint8_t* ry = rec_y_[cur_].data();
     uint8_t* ruv = rec_uv_[cur_].data();
     const int W = common_.ctb_w(), H = common_.ctb_h(), sr = 2 * common_.slice_rows();  // unit rows per I slice
     const int qp = frame_qp_();
     const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
-    const int lambda = h264::lambda_sad(qp);
-    // units in raster order (the GPU's row wavefront); availability as the decoder sees it in z
-    // order: no above-right for a CTB's last unit, and a CTB's first unit has a below-left (the
-    // left CTB's last unit) that is not reconstructed yet -- it keeps to the modes that do not
-    // read it (bl_safe_modes)
+    // units in raster order (the GPU's row wavefront) with the modes decided open-loop on the
+    // source (intra_decide_mode); availability as the decoder sees it in z order: no above-right
+    // for a CTB's last unit, no below-left reads by a CTB's first unit (see bl_safe_modes)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             const int i = y * W + x, x0 = x * 16, y0 = y * 16;
@@ -415,7 +465,6 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             CuInfo& c = cu_[i];
             std::memset(&c, 0, sizeof c);
             const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < W && z != 3, ac = at && x > 0;
-            const bool bl_pending = z == 0 && x > 0 && y + 1 < H;
             uint8_t lp[16], tp[16], tr[16];
             for (int k = 0; k < 16; ++k) {
                 lp[k] = al ? ry[(y0 + k) * cw_ + x0 - 1] : 0;
@@ -425,23 +474,8 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             const int corner = ac ? ry[(y0 - 1) * cw_ + x0 - 1] : 0;
             int L[33], T[33];
             intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
-            const int cand_a = al ? cu_[i - 1].intra_mode : 1;
-            const int cand_b = (at && (y & 1)) ? cu_[i - W].intra_mode : 1;  // above only inside the CTB
-            int best = -1, best_cost = 0;
+            const int best = intra_decide_mode(sy, pitch, W, H, x, y, sr, qp, bl_safe_);
             int pred[256];
-            for (int k = 0; k < kNumIntraCands; ++k) {
-                const int m = kIntraCands[k];
-                if (bl_pending && !((bl_safe_ >> m) & 1)) continue;
-                intra_predict(m, 4, 0, L, T, pred);
-                int sad = 0;
-                for (int r = 0; r < 16; ++r)
-                    for (int q = 0; q < 16; ++q) sad += std::abs((int)sy[(y0 + r) * pitch + x0 + q] - pred[r * 16 + q]);
-                const int cost = sad + lambda * intra_mode_bits(m, cand_a, cand_b);
-                if (best < 0 || cost < best_cost) {
-                    best = m;
-                    best_cost = cost;
-                }
-            }
             c.type = kCuIntra;
             c.intra_mode = (uint8_t)best;
             c.qp = (uint8_t)qp;

@@ -38,6 +38,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.nslices, sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&b.qpy, ncu));
     HIP_CHECK(hipMalloc(&b.qp_pred, ncu));
+    HIP_CHECK(hipMalloc(&b.imode, ncu));
     // arrays scanned in 4096-entry tiles of 16-byte loads (per CTB costs, per coding position token
     // counts): padded with zeros to a whole tile
     auto pad = [](size_t n) { return (n + kScanTilePad - 1) / kScanTilePad * kScanTilePad + 4; };
@@ -76,7 +77,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
 void GpuHevcEncoder::free_slot(FrameSlot& sl) {
     HevcDeviceBuffers& b = sl.buf;
     for (void* p : {(void*)b.fs, (void*)b.me.fs, (void*)b.me.mb, (void*)b.cu, (void*)b.coef, (void*)b.slice_data,
-                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.qp_pred, (void*)b.cost, (void*)b.qpc,
+                    (void*)b.slice_len, (void*)b.slice_first, (void*)b.slice_of_cu, (void*)b.nslices, (void*)b.qpy, (void*)b.qp_pred, (void*)b.imode, (void*)b.cost, (void*)b.qpc,
                     (void*)b.sse_part, (void*)b.sse_tot, (void*)b.sao, (void*)b.slice_clk, (void*)b.tok, (void*)b.ntok, (void*)b.tok_off,
                     (void*)b.tok_dense, (void*)b.wpp_ctx, (void*)b.wpp_flag, (void*)b.pack_done})
         if (p) (void)hipFree(p);

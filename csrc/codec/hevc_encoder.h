@@ -77,6 +77,8 @@ class HevcCommon {
     int max_slices_ = 1;
 };
 
+// Open-loop intra mode of a 16x16 unit (hevc_cpu.cpp; the GPU's k_hevc_intra_modes).
+int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int qp, uint64_t safe);
 // Direct vs bin-token CABAC on random slices (hevc_cpu.cpp); returns the slices checked.
 int token_selftest(uint32_t seed, int slices);
 // Entropy-code the slice of CTBs [first, end) with wavefront parallel processing (host): every CTB
@@ -195,7 +197,6 @@ constexpr int kMaxSlices = 1024;
 constexpr int kSseSlots = 64, kSseSlotWords = 8;
 constexpr size_t kScanTilePad = 4096;  // per-CU scan arrays padded to this (hevc_kernels.hip kScanTile)
 constexpr int kMaxSliceRows = 4;  // 16x16-unit rows per slice the intra wavefront kernel supports (2 CTB rows)
-constexpr int kIntraMaxMbW = 512;  // units per row the intra wavefront's LDS mode rows hold (8K)
 constexpr int kWppCtxWords = (C_NUM + 3) / 4;  // context states, four per dword
 constexpr uint32_t kSubSliceStart = 0x80000000u;  // substream record: this substream begins a slice
 // host buffer: header | substream payload offset[kMaxSlices] | length[] | first CTU[] | payloads
@@ -215,6 +216,7 @@ struct HevcDeviceBuffers {
     uint32_t* nslices;       // slice count of the frame
     uint8_t* qpy;            // [ncu] QpY per unit (deblocking)
     uint8_t* qp_pred;        // [ncu] QP predictor per unit (entropy coder)
+    uint8_t* imode;          // [ncu] intra mode per unit (k_hevc_intra_modes, I pictures)
     uint32_t* cost;          // [nctb] CABAC cost estimate per CTB (slice layout)
     uint8_t* qpc;            // [ncu] QP of units that code a residual, else 255
     uint32_t* sao;           // [nctb][4] SAO parameters per CTB (hevc_core.h sao_pack; luma, Cb, Cr, 0)

@@ -942,10 +942,94 @@ __device__ __forceinline__ int ref_subst(int i, int N, int avl, const uint8_t* l
     return trx[j - 3 * N - 1];
 }
 
+// ------------------------------------------------------------------ intra mode decision (I)
+// Open-loop, every unit of an I picture at once (one wave per unit, a workgroup per CTB): the 35
+// modes predicted from the *source* neighbours with the decoder's z-order availability (never the
+// below-left; a CTB's first unit keeps to bl_safe_modes, as k_hevc_intra reconstructs it before
+// its below-left), scored by 4x4 Hadamard SATD + lambda * mode bits -- hevc_cpu.cpp
+// intra_decide_mode.  The IDR wavefront (k_hevc_intra) then only reconstructs.
+__global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const HevcFrameState* __restrict__ fs,
+                                                           const uint8_t* __restrict__ src_y,
+                                                           uint8_t* __restrict__ imode) {
+    __shared__ IntraRefs rf[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int bid = blockIdx.x, cw = ctb_cols(g.mb_w);
+    const int x = 2 * (bid % cw) + (wave & 1), y = 2 * (bid / cw) + (wave >> 1);
+    if (x >= g.mb_w || y >= g.mb_h) return;  // wave-uniform; no workgroup barrier below
+    IntraRefs& R = rf[wave];
+    const int sr = fs->slice_rows, z = ((y & 1) << 1) | (x & 1);
+    const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < g.mb_w && z != 3, ac = at && x > 0;
+    const bool bl_pending = z == 0 && x > 0 && y + 1 < g.mb_h;
+    const int x0 = x * 16, y0 = y * 16, P = g.pitch;
+    if (lane < 16) {
+        R.lpx[lane] = al ? src_y[(size_t)(y0 + lane) * P + x0 - 1] : 0;
+        R.tpx[lane] = at ? src_y[(size_t)(y0 - 1) * P + x0 + lane] : 0;
+        R.trx[lane] = atr ? src_y[(size_t)(y0 - 1) * P + x0 + 16 + lane] : 0;
+    } else if (lane == 16) {
+        R.corner = ac ? src_y[(size_t)(y0 - 1) * P + x0 - 1] : 0;
+    }
+    wave_lds_sync();
+    const int avl = (al ? 2 : 0) | (ac ? 4 : 0) | (at ? 8 : 0) | (atr ? 16 : 0);
+    for (int i = lane; i <= 64; i += 64) {
+        const int v = ref_subst(i, 16, avl, R.lpx, R.tpx, R.trx, R.corner);
+        if (i < 32) R.L[32 - i] = v;
+        else if (i == 32) R.L[0] = R.T[0] = v;
+        else R.T[i - 32] = v;
+    }
+    wave_lds_sync();
+    if (lane <= 32) {
+        const int k = lane;
+        if (k == 0) {
+            R.LF[0] = R.TF[0] = (R.L[1] + 2 * R.L[0] + R.T[1] + 2) >> 2;
+        } else if (k == 32) {
+            R.LF[32] = R.L[32];
+            R.TF[32] = R.T[32];
+        } else {
+            R.LF[k] = (R.L[k + 1] + 2 * R.L[k] + R.L[k - 1] + 2) >> 2;
+            R.TF[k] = (R.T[k + 1] + 2 * R.T[k] + R.T[k - 1] + 2) >> 2;
+        }
+    }
+    const int sdc = wsum(lane < 16 ? R.L[1 + lane] + R.T[1 + lane] : 0);
+    if (lane == 0) R.dc = (sdc + 16) >> 5;
+    wave_lds_sync();
+    // this lane: row r, columns cb .. cb + 3; a 4x4 block's rows sit in lanes ^4 / ^8
+    const int r = lane >> 2, cb = (lane & 3) * 4;
+    const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * P + x0 + cb);
+    const int lambda = h264::lambda_sad(fs->qp);
+    const uint64_t safe = fs->bl_safe;
+    int best = 1, best_cost = 0x7fffffff;
+#pragma unroll 1
+    for (int m = 0; m < 35; ++m) {
+        if (bl_pending && !((safe >> m) & 1)) continue;  // wave-uniform
+        int d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            d[j] = (int)((sw >> (8 * j)) & 0xff) - pred_sample(m, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
+        const int a0 = d[0] + d[1], a1 = d[0] - d[1], a2 = d[2] + d[3], a3 = d[2] - d[3];
+        int h[4] = {a0 + a2, a1 + a3, a0 - a2, a1 - a3};
+        int sad = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int v = h[k];
+            int o = __shfl_xor(v, 4, 64);
+            v = (lane & 4) ? o - v : v + o;
+            o = __shfl_xor(v, 8, 64);
+            v = (lane & 8) ? o - v : v + o;
+            sad += v < 0 ? -v : v;
+        }
+        const int cost = wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = m;
+        }
+    }
+    if (lane == 0) imode[y * g.mb_w + x] = (uint8_t)best;
+}
+
 __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, const HevcFrameState* __restrict__ fs,
                                                       const uint8_t* __restrict__ src_y,
                                                       const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
-                                                      int16_t* __restrict__ coef, uint32_t* __restrict__ cost,
+                                                      int16_t* __restrict__ coef, const uint8_t* __restrict__ imode,
                                                       uint8_t* __restrict__ qp_coded) {
     // dynamic LDS: per row of the slice, the bottom luma row and bottom chroma (NV12) row
     extern __shared__ uint8_t bottom[];
@@ -953,16 +1037,11 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     __shared__ TuBuf tb[kMaxSliceRows];
     __shared__ IntraRefs rf[kMaxSliceRows];
     __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
-    __shared__ int mode_cost[kMaxSliceRows][kNumIntraCands];
-    __shared__ int prev_mode[kMaxSliceRows];
-    __shared__ uint8_t row_mode[kMaxSliceRows][kIntraMaxMbW];  // each row's modes (MPM of the row below)
     fill_mats(M);
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int sr = fs->slice_rows;
-    // H waves per CTU row (launch: kMaxSliceRows / slice_rows): the row's main wave (sub 0) codes
-    // the CU; its helpers share the intra mode search (every H-th candidate each) -- 1-row slices
-    // (4K, 1080p) would otherwise leave one wave per workgroup walking 240 CTUs alone
+    // one wave per unit row (the launch may add idle helper waves: H per row)
     const int H = max(1, ((int)blockDim.x >> 6) / sr);
     const int row = wave / H, sub = wave - row * H, mw = row * H;
     const bool main_w = sub == 0;
@@ -970,7 +1049,6 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     const bool row_ok = row < sr && y < g.mb_h;
     const int qp = fs->qp;
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
-    const int lambda = h264::lambda_sad(qp);
     const int cw = g.coded_w;
     uint8_t* bot_y = bottom + (size_t)row * 2 * cw;
     uint8_t* bot_c = bot_y + cw;
@@ -998,10 +1076,9 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         load_src(x + 1, nsy, nsc);
         // availability in the decoder's z order: a CTB's last unit has no above-right; its first
         // unit's below-left (the left CTB's last unit) is available there but not reconstructed yet
-        // by this raster wavefront, so that unit keeps to the modes that never read it
+        // by this raster wavefront: k_hevc_intra_modes gave that unit a mode that never reads it
         const int z = ((y & 1) << 1) | (x & 1);
         const bool al = x > 0, at = row > 0, atr = at && x + 1 < g.mb_w && z != 3, ac = at && x > 0;
-        const bool bl_pending = z == 0 && x > 0 && y + 1 < g.mb_h;
         // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
         if (valid) {
             if (lane < 16) {
@@ -1065,40 +1142,10 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             }
         }
         __syncthreads();
-        // ---- mode decision: SAD of each candidate, 4 samples per lane
+        // ---- the mode decided open-loop by k_hevc_intra_modes
         int mode = 1;
-        if (valid) {
-            const int cand_a = al ? prev_mode[row] : 1;
-            const int cand_b = (at && (y & 1)) ? (int)row_mode[row - 1][x] : 1;  // above only inside the CTB
-            const uint64_t safe = fs->bl_safe;
-            const int r = lane >> 2, cb = (lane & 3) * 4;
-            // every candidate's partial SAD first (independent work), then the wave reductions
-            int sad[kNumIntraCands];
-#pragma unroll
-            for (int m = 0; m < kNumIntraCands; ++m) {
-                const int md = kIntraCands[m];
-                sad[m] = 0;
-                if (m % H != sub) continue;  // wave-uniform: this wave's share of the candidates
-                for (int j = 0; j < 4; ++j) {
-                    const int p = pred_sample(md, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
-                    const int d = (int)((sy4 >> (8 * j)) & 0xff) - p;
-                    sad[m] += d < 0 ? -d : d;
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < kNumIntraCands; ++m) {
-                if (m % H != sub) continue;
-                const int s = wsum(sad[m]);
-                const bool ok = !bl_pending || ((safe >> kIntraCands[m]) & 1);
-                if (lane == 0) mode_cost[row][m] = ok ? s + lambda * intra_mode_bits(kIntraCands[m], cand_a, cand_b) : 0x7fffffff;
-            }
-        }
-        __syncthreads();
         if (valid && main_w) {
-            int bm = 0;
-            for (int m = 1; m < kNumIntraCands; ++m)
-                if (mode_cost[row][m] < mode_cost[row][bm]) bm = m;
-            mode = kIntraCands[bm];
+            mode = (int)imode[y * g.mb_w + x];  // (wave-uniform)
             const int r = lane >> 2, cb = (lane & 3) * 4;
             for (int j = 0; j < 4; ++j) {
                 const int p = pred_sample(mode, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
@@ -1135,8 +1182,6 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 cus[i] = c;
                 // (no slice cost: I pictures use fixed CTB-row slices)
                 qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
-                prev_mode[row] = mode;
-                row_mode[row][x] = (uint8_t)mode;
             }
         }
         __syncthreads();
@@ -2212,11 +2257,11 @@ void launch_hevc_inter(const Geometry& g, const HevcDeviceBuffers& b, const uint
 
 void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_rows, int num_slices,
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
-    if (g.mb_w > kIntraMaxMbW) throw std::invalid_argument("hevc: picture too wide for the intra wavefront");
+    const int nctb = ctb_cols(g.mb_w) * ctb_rows(g.mb_h);
+    hipLaunchKernelGGL(k_hevc_intra_modes, dim3(nctb), dim3(256), 0, s, g, b.fs, src_y, b.imode);
     const size_t lds = (size_t)slice_rows * 2 * g.coded_w;
-    const int helpers = std::max(1, kMaxSliceRows / slice_rows);  // waves per unit row (k_hevc_intra)
-    hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows * helpers), lds, s, g, b.fs, src_y, src_uv,
-                       b.cu, b.coef, b.cost, b.qpc);
+    hipLaunchKernelGGL(k_hevc_intra, dim3(num_slices), dim3(64 * slice_rows), lds, s, g, b.fs, src_y, src_uv, b.cu,
+                       b.coef, b.imode, b.qpc);
 }
 
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,

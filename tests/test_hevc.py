@@ -366,7 +366,7 @@ def test_cpu_hevc_temporal_classes(native, tu_split):
     the reconstruction and noise CUs actually drop their residual."""
     from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
 
-    w, h, qp = 320, 192, 40
+    w, h, qp = 640, 384, 40  # (a noise panel of ~12 units: some drop their residual)
     enc = native.CpuHevcEncoder(_cfg(native, w, h, qp=qp, aq=3, tu_split=tu_split))
     desk = CpuSyntheticDesktop(w, h, True)
     stream, recon, infos = b"", [], []
