@@ -396,10 +396,10 @@ PYBIND11_MODULE(_native, m) {
                  for (const auto& c : e.cus()) t.push_back(c.type);
                  return t;
              })
-        .def("cu_info",  // (type, qp, cbf, tu_split, coding-tree depth) per 16x16 unit of the last picture
+        .def("cu_info",  // (type, qp, cbf, tu_split, coding-tree depth, 4x4 luma node mask) per 16x16 unit
              [](hevc::CpuHevcEncoder& e) {
                  const auto& cus = e.cus();
-                 py::array_t<int32_t> a({(py::ssize_t)cus.size(), (py::ssize_t)5});
+                 py::array_t<int32_t> a({(py::ssize_t)cus.size(), (py::ssize_t)6});
                  auto m = a.mutable_unchecked<2>();
                  for (size_t i = 0; i < cus.size(); ++i) {
                      m(i, 0) = cus[i].type;
@@ -407,6 +407,7 @@ PYBIND11_MODULE(_native, m) {
                      m(i, 2) = cus[i].cbf;
                      m(i, 3) = cus[i].tu_split;
                      m(i, 4) = cus[i].ct;
+                     m(i, 5) = cus[i].tu4;
                  }
                  return a;
              })

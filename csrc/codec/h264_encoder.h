@@ -63,7 +63,8 @@ struct EncoderConfig {
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: it costs -35 % fps on the 1080p desktop (k_intra_analyze + k_intra_p on
                               // the analysis queue, profiles/r04_toolset/NOTES.md)
-    int tu_split = 1;         // HEVC: inter CUs may split their transform tree into 8x8 / 4x4 TUs (SSE + lambda * bits)
+    int tu_split = 2;         // HEVC: inter transform trees may split into 8x8 luma / 4x4 chroma TUs (1), and each
+                              // 8x8 luma node again into four 4x4 TUs (2), per node by SSE + lambda * bits
     int hevc_slice_cost = 2048;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
     // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): P pictures in slices of
     // hevc_wpp_rows CTU rows, every CTU row its own CABAC substream (one GPU wave each) that starts

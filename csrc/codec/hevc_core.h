@@ -737,7 +737,12 @@ struct CuInfo {
     // and mvp / mvd equal in all four; the CU's prediction syntax lives in the z-order first unit),
     // 1 = a CU16
     uint8_t ct;
-    uint8_t rsv[7];
+    // split transform tree (tu_split 2): bit k = the 8x8 luma node k split again into four 4x4
+    // luma TUs (sub-blocks 4k + j, z order; its chroma stays one 4x4 TU per component), and the
+    // coded flags of those 4x4 TUs (bit 4k + j)
+    uint8_t tu4;
+    uint16_t cbf_y16;
+    uint8_t rsv[4];
 };
 static_assert(sizeof(CuInfo) == 32, "CuInfo layout");
 constexpr int kCuWords = (int)(sizeof(CuInfo) / 4);
@@ -764,6 +769,8 @@ MXHD void cu_summarise(CuInfo& c, const int16_t* co) {
     c.cbf = 0;
     c.cbf_y4 = c.cbf_c4 = 0;
     if (c.tu_split != 2) {
+        c.tu4 = 0;
+        c.cbf_y16 = 0;
         if (tu_summary(co, 256, &c.last[0], &m)) c.cbf |= 1;
         c.csbf_y = (uint16_t)m;
         if (tu_summary(co + 256, 64, &c.last[1], &m)) c.cbf |= 2;
@@ -773,9 +780,18 @@ MXHD void cu_summarise(CuInfo& c, const int16_t* co) {
         return;
     }
     uint32_t lsum = 0, csy = 0;
+    c.cbf_y16 = 0;
     for (int k = 0; k < 4; ++k) {
         uint8_t l;
-        if (tu_summary(co + 64 * k, 64, &l, &m)) {
+        if ((c.tu4 >> k) & 1) {  // four 4x4 TUs (one sub-block each)
+            for (int j = 0; j < 4; ++j)
+                if (tu_summary(co + 64 * k + 16 * j, 16, &l, &m)) {
+                    c.cbf_y16 |= (uint16_t)(1u << (4 * k + j));
+                    c.cbf_y4 |= (uint8_t)(1u << k);
+                    lsum += l + 1u;
+                    csy |= 1u << (4 * k + j);
+                }
+        } else if (tu_summary(co + 64 * k, 64, &l, &m)) {
             c.cbf_y4 |= (uint8_t)(1u << k);
             lsum += l + 1u;
             csy |= m << (4 * k);
@@ -1195,24 +1211,43 @@ MXHD void code_node16(E& e, Ctx& ctx, const CuInfo& c, int d, int pcb, int pcr, 
     if (c.cbf && qp_pending) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_pred));
 }
 
-// Split tree: the first 8x8 child with a coded TU (its transform unit carries cu_qp_delta)
-MXHD int split_first_coded_child(const CuInfo& c) {
-    for (int k = 0; k < 4; ++k)
-        if (((c.cbf_y4 >> k) & 1) | ((c.cbf_c4 >> k) & 1) | ((c.cbf_c4 >> (4 + k)) & 1)) return k;
-    return 4;
+// Split tree: the transform unit that carries cu_qp_delta -- the first one in decoding order with a
+// coded luma level or coded chroma at its node (a 4x4 luma TU sees its 8x8 node's chroma, 7.3.8.10
+// cbfDepthC): 4k + j for 4x4 TU j of node k, 16 + k for an unsplit 8x8 node k, -1 for none.
+MXHD int split_qp_tu(const CuInfo& c) {
+    for (int k = 0; k < 4; ++k) {
+        const bool ck = ((c.cbf_c4 >> k) & 1) | ((c.cbf_c4 >> (4 + k)) & 1);
+        if ((c.tu4 >> k) & 1) {
+            for (int j = 0; j < 4; ++j)
+                if (ck || ((c.cbf_y16 >> (4 * k + j)) & 1)) return 4 * k + j;
+        } else if (ck || ((c.cbf_y4 >> k) & 1)) {
+            return 16 + k;
+        }
+    }
+    return -1;
 }
 // 8x8 child k (depth d + 1) of a split 16x16 node at depth d; its chroma TUs are 4x4 at this node:
-// split_transform_flag (0: no 4x4 luma TUs) while d + 1 < depth_inter, chroma cbf when the
-// parent's is set, cbf_luma (context 0), cu_qp_delta at the first coded child while pending.
+// split_transform_flag (tu4: four 4x4 luma TUs) while d + 1 < depth_inter, chroma cbf when the
+// parent's is set, and for an unsplit child cbf_luma (context 0) and cu_qp_delta when pending and
+// this is its TU.
 template <class E, class Ctx>
 MXHD void code_child8(E& e, Ctx& ctx, const CuInfo& c, int k, int d, int depth_inter, bool qp_pending, int qp_pred) {
     const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1;
     const int yk = (c.cbf_y4 >> k) & 1, cbk = (c.cbf_c4 >> k) & 1, crk = (c.cbf_c4 >> (4 + k)) & 1;
-    if (d + 1 < depth_inter) e.bin(ctx, C_SPLIT_TRANSFORM + 2, 0);  // ctxInc 5 - log2(8)
+    const int s4 = (c.tu4 >> k) & 1;
+    if (d + 1 < depth_inter) e.bin(ctx, C_SPLIT_TRANSFORM + 2, s4);  // ctxInc 5 - log2(8)
     if (cb) e.bin(ctx, C_CBF_CHROMA + d + 1, cbk);
     if (cr) e.bin(ctx, C_CBF_CHROMA + d + 1, crk);
+    if (s4) return;  // the four 4x4 TUs code their own cbf_luma (code_grand4)
     e.bin(ctx, C_CBF_LUMA + 0, yk);
-    if (qp_pending && k == split_first_coded_child(c)) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_pred));
+    if (qp_pending && split_qp_tu(c) == 16 + k) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_pred));
+}
+// 4x4 luma TU j of split child k (depth d + 2): cbf_luma (context 0), cu_qp_delta when pending
+// and this is its TU
+template <class E, class Ctx>
+MXHD void code_grand4(E& e, Ctx& ctx, const CuInfo& c, int k, int j, bool qp_pending, int qp_pred) {
+    e.bin(ctx, C_CBF_LUMA + 0, (c.cbf_y16 >> (4 * k + j)) & 1);
+    if (qp_pending && split_qp_tu(c) == 4 * k + j) code_qp_delta(e, ctx, qp_delta_wrap(c.qp, qp_pred));
 }
 // Whether TU t (0 Y, 1 Cb, 2 Cr) of split child k is coded, and its first CU sub-block.
 MXHD bool split_tu_coded(const CuInfo& c, int k, int t) {
@@ -1227,6 +1262,16 @@ MXHD TuDesc split_tu_desc(const Cf& cf, int k, int t) {
     d.log2n = t == 0 ? 3 : 2;
     d.cidx = t;
     d.last_idx = tu_last(cf, d.sb0, t == 0 ? 4 : 1, &d.csbf_mask);
+    return d;
+}
+// the 4x4 luma TU j of split child k (one sub-block: 4k + j)
+template <class Cf>
+MXHD TuDesc luma4_tu_desc(const Cf& cf, int k, int j) {
+    TuDesc d;
+    d.sb0 = 4 * k + j;
+    d.log2n = 2;
+    d.cidx = 0;
+    d.last_idx = tu_last(cf, d.sb0, 1, &d.csbf_mask);
     return d;
 }
 MXHD TuDesc flat_tu_desc(const CuInfo& c, int t) {
@@ -1348,10 +1393,14 @@ MXHD void code_unit_head(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u) {
     if (code_pred_head(e, ctx, u.islice, c, u.nb, c.cbf != 0, kMinCbLog2))
         code_node16(e, ctx, c, 0, 0, 0, u.depth_inter, true, u.qp_pred);
 }
-// split child k's head at the unit's tree depth
+// split child k's head at the unit's tree depth, and the flags of its 4x4 TU j
 template <class E, class Ctx>
 MXHD void code_unit_child(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, int k) {
     code_child8(e, ctx, c, k, u.cu32 ? 1 : 0, u.depth_inter, u.qp_pending, u.qp_pred);
+}
+template <class E, class Ctx>
+MXHD void code_unit_grand(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, int k, int j) {
+    code_grand4(e, ctx, c, k, j, u.qp_pending, u.qp_pred);
 }
 // end_of_slice_segment_flag after the CTB's last unit (+ end_of_subset_one_bit with WPP)
 template <class E>
@@ -1684,12 +1733,15 @@ MXHD void code_token(CabacEnc& e, Ctx& ctx, uint32_t t) {
 // depends only on the unit, its neighbours' descriptors and UnitSyn, so the GPU binarises one
 // part per lane (k_hevc_bins); the CPU walks them in order.  At most 1 + 4 + 12 + 24 + 1 = 42
 // parts; a part is at most kPartTokens tokens.
-enum PartKind { kPartHead = 0, kPartChild = 1, kPartTuLast = 2, kPartSb = 3, kPartEnd = 4 };
+// A split child whose luma is four 4x4 TUs has one part per 4x4 TU (kPartGrand: its cbf_luma,
+// cu_qp_delta and, when coded, its last position) followed by the TU's one sub-block, then its
+// chroma TUs.  Worst case 1 + 4 + 16 x 2 + 8 x 2 + 1 = 54 parts (one wave).
+enum PartKind { kPartHead = 0, kPartChild = 1, kPartTuLast = 2, kPartSb = 3, kPartEnd = 4, kPartGrand = 5 };
 struct CtuPart {
-    int kind, k, t, i;  // split child, component TU, sub-block index within the TU
-    TuDesc d;           // TU of kPartTuLast / kPartSb
+    int kind, k, t, i;  // split child, component TU (or 4x4 luma TU j of kPartGrand), sub-block index within the TU
+    TuDesc d;           // TU of kPartTuLast / kPartSb / a coded kPartGrand
 };
-constexpr int kMaxCtuParts = 42;
+constexpr int kMaxCtuParts = 54;
 constexpr uint32_t kPartTokens = 112;
 
 // Calls f(part, index) for every part of unit c in coding order; returns the number of parts.
@@ -1709,8 +1761,25 @@ MXHD int for_each_part(const CuInfo& c, const UnitSyn& u, const Cf& cf, F f) {
             pt.k = k;
             f(pt, n++);
         }
+        const bool s4 = kind == kResSplit && ((c.tu4 >> k) & 1);
+        if (s4) {
 #pragma unroll 1
-        for (int t = 0; t < 3; ++t) {
+            for (int j = 0; j < 4; ++j) {
+                const bool coded = (c.cbf_y16 >> (4 * k + j)) & 1;
+                if (coded) pt.d = luma4_tu_desc(cf, k, j);
+                pt.k = k;
+                pt.t = j;
+                pt.kind = kPartGrand;
+                f(pt, n++);
+                if (coded) {
+                    pt.kind = kPartSb;
+                    pt.i = 0;
+                    f(pt, n++);
+                }
+            }
+        }
+#pragma unroll 1
+        for (int t = s4 ? 1 : 0; t < 3; ++t) {
             const bool coded = kind == kResSplit ? split_tu_coded(c, k, t) : (((c.cbf >> t) & 1) != 0);
             if (!coded) continue;
             pt.d = kind == kResSplit ? split_tu_desc(cf, k, t) : flat_tu_desc(c, t);
@@ -1740,6 +1809,9 @@ MXHD void binarise_part(E& rec, Ctx& ctx, const CtuPart& pt, const CuInfo& c, co
         code_unit_head(rec, ctx, c, u);
     } else if (pt.kind == kPartChild) {
         code_unit_child(rec, ctx, c, u, pt.k);
+    } else if (pt.kind == kPartGrand) {
+        code_unit_grand(rec, ctx, c, u, pt.k, pt.t);
+        if ((c.cbf_y16 >> (4 * pt.k + pt.t)) & 1) code_tu_last(rec, ctx, pt.d);
     } else if (pt.kind == kPartTuLast) {
         code_tu_last(rec, ctx, pt.d);
     } else if (pt.kind == kPartSb) {
@@ -1770,8 +1842,14 @@ MXHD void code_unit_direct(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, co
 #pragma unroll 1
         for (int k = 0; k < 4; ++k) {
             code_unit_child(e, ctx, c, u, k);
+            const bool s4 = (c.tu4 >> k) & 1;
+            if (s4)
+                for (int j = 0; j < 4; ++j) {
+                    code_unit_grand(e, ctx, c, u, k, j);
+                    if ((c.cbf_y16 >> (4 * k + j)) & 1) code_residual(e, ctx, cf, luma4_tu_desc(cf, k, j));
+                }
 #pragma unroll 1
-            for (int t = 0; t < 3; ++t)
+            for (int t = s4 ? 1 : 0; t < 3; ++t)
                 if (split_tu_coded(c, k, t)) code_residual(e, ctx, cf, split_tu_desc(cf, k, t));
         }
     } else if (kind == kResFlat) {
@@ -1973,17 +2051,27 @@ MXHD uint32_t tu_bits_est(const int16_t* lv, int n) {
 // well-predicted block, and skipping the second tree there halves the transform work of a desktop
 // P picture.  Shared by both encoders.
 MXHD bool split_worth_trying(int levels_unsplit) { return levels_unsplit > 0; }
+MXHD int tu_levels(const int16_t* lv, int n) {
+    int k = 0;
+    for (int i = 0; i < n; ++i) k += lv[i] != 0;
+    return k;
+}
 MXHD bool choose_split(uint64_t sse16, uint32_t bits16, uint64_t sse8, uint32_t bits8, int qp) {
     const uint64_t l = kLambdaSse16[qp < 0 ? 0 : (qp > 51 ? 51 : qp)];
     return sse8 * 16 + l * bits8 < sse16 * 16 + l * bits16;
 }
 
-// The split transform tree of an inter CU: luma TU k is the 8x8 block (k & 1, k >> 1) of the
+// The split transform tree of an inter CU: luma node k is the 8x8 block (k & 1, k >> 1) of the
 // 16x16 residual, chroma TU k the 4x4 block (k & 1, k >> 1) of each 8x8 chroma residual; levels
 // go to the CU's sub-blocks 4k.. (luma), 16 + k (Cb), 20 + k (Cr), i.e. co + 64k,
 // co + 256 + 16k, co + 320 + 16k, each TU in scan order.  rr / rrc: reconstructed residuals.
-MXHD void split_encode(const int* res, const int (*rc)[64], int qp, int qpc, int16_t* co, int* rr, int (*rrc)[64]) {
+// With try4 a luma node is also coded as four 4x4 TUs (sub-block 4k + j = the 4x4 block (j & 1,
+// j >> 1) of the node) and keeps them when their luma SSE + lambda * bits is lower (choose_split,
+// the node's own distortion against pred + res); returns the mask of such nodes (CuInfo::tu4).
+MXHD int split_encode(const int* res, const int (*rc)[64], int qp, int qpc, int16_t* co, int* rr, int (*rrc)[64],
+                      const int* pred = nullptr, bool try4 = false) {
     int blk[64], rb[64];
+    int tu4 = 0;
     for (int k = 0; k < 4; ++k) {
         const int bx = (k & 1) * 8, by = (k >> 1) * 8;
         for (int r = 0; r < 8; ++r)
@@ -1991,6 +2079,33 @@ MXHD void split_encode(const int* res, const int (*rc)[64], int qp, int qpc, int
         tu_encode(3, blk, qp, false, co + 64 * k, rb);
         for (int r = 0; r < 8; ++r)
             for (int q = 0; q < 8; ++q) rr[(by + r) * 16 + bx + q] = rb[r * 8 + q];
+        if (!try4 || !split_worth_trying(tu_levels(co + 64 * k, 64))) continue;
+        int16_t l4[64];
+        int r4[64], b4[16], rb4[16];
+        for (int j = 0; j < 4; ++j) {
+            const int jx = (j & 1) * 4, jy = (j >> 1) * 4;
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q) b4[r * 4 + q] = blk[(jy + r) * 8 + jx + q];
+            tu_encode(2, b4, qp, false, l4 + 16 * j, rb4);
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q) r4[(jy + r) * 8 + jx + q] = rb4[r * 4 + q];
+        }
+        uint64_t s8 = 0, s4 = 0;
+        for (int r = 0; r < 8; ++r)
+            for (int q = 0; q < 8; ++q) {
+                const int o = (by + r) * 16 + bx + q, src = pred[o] + res[o];
+                const int e8 = src - clip255(pred[o] + rb[r * 8 + q]), e4 = src - clip255(pred[o] + r4[r * 8 + q]);
+                s8 += (uint64_t)(e8 * e8);
+                s4 += (uint64_t)(e4 * e4);
+            }
+        uint32_t b4bits = 0;
+        for (int j = 0; j < 4; ++j) b4bits += tu_bits_est(l4 + 16 * j, 16);
+        if (choose_split(s8, tu_bits_est(co + 64 * k, 64), s4, b4bits, qp)) {
+            tu4 |= 1 << k;
+            for (int i = 0; i < 64; ++i) co[64 * k + i] = l4[i];
+            for (int r = 0; r < 8; ++r)
+                for (int q = 0; q < 8; ++q) rr[(by + r) * 16 + bx + q] = r4[r * 8 + q];
+        }
     }
     for (int comp = 0; comp < 2; ++comp)
         for (int k = 0; k < 4; ++k) {
@@ -2001,14 +2116,34 @@ MXHD void split_encode(const int* res, const int (*rc)[64], int qp, int qpc, int
             for (int r = 0; r < 4; ++r)
                 for (int q = 0; q < 4; ++q) rrc[comp][(by + r) * 8 + bx + q] = rb[r * 4 + q];
         }
+    return tu4;
 }
 
-// Estimated level bits of a CU's transform tree (unsplit: 16x16 + 2 x 8x8; split: 4 x 8x8 + 8 x 4x4).
-MXHD uint32_t cu_bits_est(const int16_t* co, bool split) {
+// Estimated level bits of a CU's transform tree (unsplit: 16x16 + 2 x 8x8; split: per luma node
+// one 8x8 or (tu4) four 4x4, + 8 x 4x4 chroma).
+MXHD uint32_t cu_bits_est(const int16_t* co, bool split, int tu4 = 0) {
     if (!split) return tu_bits_est(co, 256) + tu_bits_est(co + 256, 64) + tu_bits_est(co + 320, 64);
     uint32_t b = 0;
-    for (int k = 0; k < 4; ++k) b += tu_bits_est(co + 64 * k, 64);
+    for (int k = 0; k < 4; ++k) {
+        if ((tu4 >> k) & 1)
+            for (int j = 0; j < 4; ++j) b += tu_bits_est(co + 64 * k + 16 * j, 16);
+        else
+            b += tu_bits_est(co + 64 * k, 64);
+    }
     for (int k = 0; k < 8; ++k) b += tu_bits_est(co + 256 + 16 * k, 16);
+    return b;
+}
+
+// Estimated bits of the luma levels alone (the residual drop of changing content)
+MXHD uint32_t luma_bits_est(const int16_t* co, bool split, int tu4) {
+    if (!split) return tu_bits_est(co, 256);
+    uint32_t b = 0;
+    for (int k = 0; k < 4; ++k) {
+        if ((tu4 >> k) & 1)
+            for (int j = 0; j < 4; ++j) b += tu_bits_est(co + 64 * k + 16 * j, 16);
+        else
+            b += tu_bits_est(co + 64 * k, 64);
+    }
     return b;
 }
 
@@ -2172,7 +2307,11 @@ constexpr uint8_t kDbTc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0
 
 // Luma cbf of the TU of CU c that holds its 4x4 block (bx, by), 0..3 each.
 MXHD bool tu_cbf_at(const CuInfo& c, int bx, int by) {
-    if (c.tu_split == 2) return (c.cbf_y4 >> ((by >> 1) * 2 + (bx >> 1))) & 1;
+    if (c.tu_split == 2) {
+        const int k = (by >> 1) * 2 + (bx >> 1);
+        if ((c.tu4 >> k) & 1) return (c.cbf_y16 >> (4 * k + (by & 1) * 2 + (bx & 1))) & 1;
+        return (c.cbf_y4 >> k) & 1;
+    }
     return c.cbf & 1;
 }
 

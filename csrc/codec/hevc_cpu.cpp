@@ -393,7 +393,7 @@ namespace {
 // Finish a CU's residual bookkeeping: cbf / last / coded sub-block masks.
 void summarise(CuInfo& c, const int16_t* coef) {
     cu_summarise(c, coef);
-    set_est_bytes(c, cu_bits_est(coef, c.tu_split == 2));
+    set_est_bytes(c, cu_bits_est(coef, c.tu_split == 2, c.tu4));
 }
 }  // namespace
 
@@ -575,11 +575,13 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
             c.tu_split = cfg_.tu_split ? 1 : 0;
             int levels1 = 0;
             for (int k = 0; k < kCoefPerCu; ++k) levels1 += co[k] != 0;
+            c.tu4 = 0;
             if (cfg_.tu_split && split_worth_trying(levels1)) {
-                // option 2: four 8x8 luma TUs, eight 4x4 chroma TUs; keep the cheaper by SSE + lambda * bits
+                // option 2: four 8x8 luma nodes (each one 8x8 TU or, tu_split 2, four 4x4 TUs), eight
+                // 4x4 chroma TUs; keep the cheaper by SSE + lambda * bits
                 int16_t co2[kCoefPerCu];
                 int rr2[256], rrc2[2][64];
-                split_encode(res, rc, qp, qpc, co2, rr2, rrc2);
+                const int tu4 = split_encode(res, rc, qp, qpc, co2, rr2, rrc2, pred, cfg_.tu_split >= 2);
                 uint64_t sse1 = 0, sse2 = 0;
                 for (int k = 0; k < 256; ++k) {
                     const int s0 = pred[k] + res[k];
@@ -595,8 +597,9 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                         sse1 += (uint64_t)(e1 * e1);
                         sse2 += (uint64_t)(e2 * e2);
                     }
-                if (choose_split(sse1, cu_bits_est(co, false), sse2, cu_bits_est(co2, true), qp)) {
+                if (choose_split(sse1, cu_bits_est(co, false), sse2, cu_bits_est(co2, true, tu4), qp)) {
                     c.tu_split = 2;
+                    c.tu4 = (uint8_t)tu4;
                     std::memcpy(co, co2, sizeof co2);
                     std::memcpy(rr, rr2, sizeof rr2);
                     std::memcpy(rrc, rrc2, sizeof rrc2);
@@ -611,14 +614,11 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                     d_pred += res[k] * res[k];
                     d_coded += e * e;
                 }
-                uint32_t bits = 0;
-                if (c.tu_split == 2)
-                    for (int k = 0; k < 4; ++k) bits += tu_bits_est(co + 64 * k, 64);
-                else
-                    bits = tu_bits_est(co, 256);
+                const uint32_t bits = luma_bits_est(co, c.tu_split == 2, c.tu4);
                 if (h264::drop_luma_for(cfg_.aq, lsad, tcls, qp, d_pred, d_coded, bits)) {
                     for (int k = 0; k < 256; ++k) co[k] = 0, rr[k] = 0;
                     c.tu_split = cfg_.tu_split ? 1 : 0;
+                    c.tu4 = 0;
                 }
             }
             for (int r = 0; r < 16; ++r)
@@ -853,6 +853,7 @@ int token_selftest(uint32_t seed, int slices) {
                     cu.mvp_idx = (uint8_t)(cu.type == kCuAmvp ? rnd(2) : rnd(5));
                 }
                 cu.tu_split = cu.type == kCuIntra ? 1 : (uint8_t)(1 + rnd(2));
+                cu.tu4 = cu.tu_split == 2 ? (uint8_t)rnd(16) : 0;  // 8x8 nodes split into 4x4 TUs
                 if (cu.type != kCuSkip) fill_levels(cu, i);
                 qpp[(size_t)i] = (uint8_t)(10 + rnd(40));
             }

@@ -186,7 +186,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.depth_inter = common_.depth_inter();
     f.pad2_ = 0;
     f.aq = cfg_.aq;
-    f.tu_split = cfg_.tu_split ? 1 : 0;
+    f.tu_split = cfg_.tu_split;  // 0 none, 1 8x8 nodes, 2 also 4x4 luma TUs
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
     // distortion partials: k_hevc_sao (totals) with SAO, else k_hevc_sse (one per unit row) after
     // deblocking, else the analysis kernels' (P: one per CTB, I: one per unit row)

@@ -146,7 +146,7 @@ struct HevcFrameState {
     int32_t aq;
     int32_t chroma_qp_offset;
     int32_t n_sse_parts;  // distortion partials written this frame (P: one per 4 CUs, I: one per CTU row)
-    int32_t tu_split;     // inter CUs may split their transform tree (EncoderConfig.tu_split)
+    int32_t tu_split;     // inter split transform trees (EncoderConfig.tu_split: 1 8x8 nodes, 2 also 4x4 luma TUs)
     unsigned long long* sse_part;  // [3][kSsePartStride] per-workgroup distortion partials
     // temporal AQ classes (aq 3, h264_mb.h temporal_class): previous frame's source luma (read)
     // and this frame's copy (written by k_hevc_inter; IDR pictures copy it on the stream)

@@ -404,11 +404,13 @@ __device__ __forceinline__ TuResult code_tus(TuBuf& t, const Mats& M, int qp, in
 // luma TU (lane = scan index) and one per chroma component (lane = 16 * TU + scan index) give
 // the coded masks, the rest is scalar (lane 0 alone walking 384 LDS levels cost ~1,100 VALU).
 struct SplitSummary {
-    uint8_t cbf, cbf_y4, cbf_c4, last[3], csbf_c[2];
-    uint16_t csbf_y;
+    uint8_t cbf, cbf_y4, cbf_c4, last[3], csbf_c[2], tu4;
+    uint16_t csbf_y, cbf_y16;
     __device__ void apply(CuInfo& c) const {
         c.cbf = cbf;
         c.cbf_y4 = cbf_y4;
+        c.tu4 = tu4;
+        c.cbf_y16 = cbf_y16;
         c.cbf_c4 = cbf_c4;
         c.last[0] = last[0];
         c.last[1] = last[1];
@@ -418,13 +420,24 @@ struct SplitSummary {
         c.csbf_c[1] = csbf_c[1];
     }
 };
-__device__ SplitSummary split_summary_wave(const int16_t* co, int lane) {
+__device__ SplitSummary split_summary_wave(const int16_t* co, int lane, int tu4) {
     SplitSummary s = {};
+    s.tu4 = (uint8_t)tu4;
     uint32_t lsum = 0, csy = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint64_t b = __ballot(co[64 * k + lane] != 0);
-        if (b) {
+        if ((tu4 >> k) & 1) {  // four 4x4 TUs of 16 coefficients (lane = 16 j + scan index)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t f = (uint32_t)((b >> (16 * j)) & 0xffffu);
+                if (!f) continue;
+                s.cbf_y16 |= (uint16_t)(1u << (4 * k + j));
+                s.cbf_y4 |= (uint8_t)(1u << k);
+                lsum += (uint32_t)(32 - __builtin_clz(f));
+                csy |= 1u << (4 * k + j);
+            }
+        } else if (b) {
             s.cbf_y4 |= (uint8_t)(1u << k);
             lsum += (uint32_t)(64 - __builtin_clzll(b));
             uint32_t m = 0;
@@ -462,6 +475,9 @@ struct SplitResult {
     uint32_t bits;
     int sse_y_full;   // luma only, whole CU (residual drop)
     uint32_t bits_y;  // tu_bits_est sum of the four luma TUs
+    // per 8x8 luma node k: SSE over the node, SSE over its display area, tu_bits_est, levels coded
+    int node_sse[4], node_disp[4], node_lv[4];
+    uint32_t node_bits[4];
 };
 __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp, int qpc, bool valid, int16_t* lv,
                                                 uint8_t* rec, int x0, int y0, int disp_w, int disp_h) {
@@ -636,6 +652,121 @@ __device__ __forceinline__ SplitResult split_tus(TuBuf& t, const Mats& M, int qp
     out.sse[0] = wsum(sy);
     out.sse[1] = wsum(comp == 0 ? sc : 0);
     out.sse[2] = wsum(comp == 1 ? sc : 0);
+    {  // per luma node: the 16-lane group sums, read from the group's first lane
+        const int gs = gsum<16>(syf), gd = gsum<16>(sy);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            out.node_sse[k] = __builtin_amdgcn_readlane(gs, 16 * k);
+            out.node_disp[k] = __builtin_amdgcn_readlane(gd, 16 * k);
+            out.node_lv[k] = __builtin_amdgcn_readlane(nzl, 16 * k);
+            out.node_bits[k] = (uint32_t)__builtin_amdgcn_readlane(nzl ? bl + 4 : 1, 16 * k);
+        }
+    }
+    wave_lds_sync();
+    return out;
+}
+
+// The 4x4 option of the split tree's luma nodes (split_encode's try4 on the CPU), whole wave: 4x4
+// TU j16 = lane >> 2 (node k = j16 >> 2, TU j = j16 & 3 in z order), lane l4 = lane & 3 takes row l4
+// of the forward row stage, column l4 of the column stage and row l4 of both inverse stages;
+// decimation and the trailing trim per TU over its 4 lanes (tu_encode_t<2> rules).  Levels to lv4
+// (node k TU j at 64k + 16j, scan order), reconstruction to rec4 (16x16 luma, TuBuf layout);
+// per-node SSE (node / display area) and bits in the result.
+struct Split4Result {
+    int node_sse[4], node_disp[4];
+    uint32_t node_bits[4];
+};
+__device__ __forceinline__ Split4Result split4_luma(TuBuf& t, const Mats& M, int qp, bool valid, int16_t* lv4,
+                                                    uint8_t* rec4, int x0, int y0, int disp_w, int disp_h) {
+    const int lane = threadIdx.x & 63, j16 = lane >> 2, l4 = lane & 3;
+    const int k = j16 >> 2, j = j16 & 3;
+    const int tx = (k & 1) * 8 + (j & 1) * 4, ty = (k >> 1) * 8 + (j >> 1) * 4;  // TU origin in the CU
+    const int base = 16 * j16;
+    int16_t* aT = reinterpret_cast<int16_t*>(t.a);
+    int16_t* a16 = reinterpret_cast<int16_t*>(t.a);
+    int16_t* bT = reinterpret_cast<int16_t*>(t.b);
+    if (valid)  // forward stage 1 (rows): row l4, outputs kk
+        for (int kk = 0; kk < 4; ++kk) {
+            const int s = dot4(M.t4 + kk * 4, t.res + (ty + l4) * 16 + tx);
+            aT[base + kk * 4 + l4] = (int16_t)((s + 1) >> 1);
+        }
+    wave_lds_sync();
+    int ll[4] = {0, 0, 0, 0}, si[4] = {0, 0, 0, 0};
+    if (valid)  // forward stage 2 (columns): column kk = l4, vertical frequency k2
+        for (int k2 = 0; k2 < 4; ++k2) {
+            const int s = dot4(M.t4 + k2 * 4, aT + base + l4 * 4);
+            ll[k2] = quant_coef((s + 128) >> 8, qp, 2, false);
+            si[k2] = scan_index(2, l4, k2);
+        }
+    {  // decimation per TU
+        int nz = 0, mx = 0;
+        for (int q = 0; q < 4; ++q) {
+            nz += ll[q] != 0;
+            mx = max(mx, abs(ll[q]));
+        }
+        if (tu_decimate(2, false, gsum<4>(nz), gmax<4>(mx)))
+            for (int q = 0; q < 4; ++q) ll[q] = 0;
+    }
+    {  // trailing isolated +-1 trim per TU (a stopped TU stays stopped)
+        bool on = true;
+        for (int it = 0; it < kTrimIters; ++it) {
+            int last = -1;
+            for (int q = 0; q < 4; ++q)
+                if (ll[q]) last = max(last, si[q]);
+            last = gmax<4>(last);
+            int prev = -1, lvv = 0;
+            for (int q = 0; q < 4; ++q) {
+                if (ll[q] && si[q] < last) prev = max(prev, si[q]);
+                if (ll[q] && si[q] == last) lvv = abs(ll[q]);
+            }
+            prev = gmax<4>(prev);
+            lvv = gmax<4>(lvv);
+            if (last < 0 || lvv != 1 || last - prev <= kTrimGap) on = false;
+            if (on)
+                for (int q = 0; q < 4; ++q)
+                    if (si[q] == last) ll[q] = 0;
+        }
+    }
+    int nz = 0, bl = 0;
+    if (valid)
+        for (int k2 = 0; k2 < 4; ++k2) {
+            const int l = ll[k2];
+            lv4[64 * k + 16 * j + si[k2]] = (int16_t)l;
+            bT[base + l4 * 4 + k2] = (int16_t)dequant_coef(l, qp, 2);
+            if (l) {
+                ++nz;
+                bl += 4 + 2 * (31 - __builtin_clz((uint32_t)abs(l)));
+            }
+        }
+    nz = gsum<4>(nz);
+    bl = gsum<4>(bl);
+    wave_lds_sync();
+    if (valid)  // inverse stage 1 (columns): row y = l4 of the intermediate
+        for (int x = 0; x < 4; ++x) {
+            const int s = dot4(M.tt4 + l4 * 4, bT + base + x * 4);
+            a16[base + l4 * 4 + x] = (int16_t)clip16((s + 64) >> 7);
+        }
+    wave_lds_sync();
+    int sf = 0, sd = 0;
+    if (valid)  // inverse stage 2 (rows) + reconstruction: row l4
+        for (int x = 0; x < 4; ++x) {
+            const int s = dot4(M.tt4 + x * 4, a16 + base + l4 * 4);
+            const int r = nz ? (s + 2048) >> 12 : 0;
+            const int o = (ty + l4) * 16 + tx + x, p = t.pred[o];
+            const int v = clip255(p + r), e = p + t.res[o] - v;
+            sf += e * e;
+            sd += (x0 + tx + x < disp_w && y0 + ty + l4 < disp_h) ? e * e : 0;
+            rec4[o] = (uint8_t)v;
+        }
+    Split4Result out;
+    const int gs = gsum<16>(sf), gd = gsum<16>(sd);
+    const int gb = gsum<16>(l4 == 0 ? (nz ? bl + 4 : 1) : 0);  // the node's four TUs
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        out.node_sse[q] = __builtin_amdgcn_readlane(gs, 16 * q);
+        out.node_disp[q] = __builtin_amdgcn_readlane(gd, 16 * q);
+        out.node_bits[q] = (uint32_t)__builtin_amdgcn_readlane(gb, 16 * q);
+    }
     wave_lds_sync();
     return out;
 }
@@ -665,6 +796,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     __shared__ unsigned long long part[3][4];
     __shared__ int16_t lv2[4][kCoefPerCu];  // split transform tree: levels and reconstruction
     __shared__ uint8_t rec2[4][384];
+    __shared__ int16_t lv4[4][256];          // its 4x4 luma option (tu_split 2)
+    __shared__ uint8_t rec4[4][256];
     __shared__ uint32_t unit_cost[4];
     fill_mats(M);
     __syncthreads();
@@ -789,9 +922,34 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     // option 2, the split transform tree (split_encode of the CPU encoder), whole wave -- only
     // when option 1 coded something (split_worth_trying, as the CPU encoder)
     const bool try_split = fs->tu_split != 0 && valid && split_worth_trying(r.nz[0] + r.nz[1] + r.nz[2]);  // wave-uniform
-    SplitResult r2 = {0, {0, 0, 0}, 0, 0, 0};
+    SplitResult r2 = {};
     if (try_split)
         r2 = split_tus(t, M, qp, qpc, valid, lv2[wave], rec2[wave], x0, y0, g.width, g.height);
+    // tu_split 2: every node whose 8x8 TU coded a level may become four 4x4 TUs (split_encode try4)
+    int tu4 = 0;
+    if (try_split && fs->tu_split >= 2 &&
+        split_worth_trying(r2.node_lv[0] + r2.node_lv[1] + r2.node_lv[2] + r2.node_lv[3])) {  // wave-uniform
+        const Split4Result r4 = split4_luma(t, M, qp, valid, lv4[wave], rec4[wave], x0, y0, g.width, g.height);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!split_worth_trying(r2.node_lv[k])) continue;
+            if (!choose_split((uint64_t)r2.node_sse[k], r2.node_bits[k], (uint64_t)r4.node_sse[k], r4.node_bits[k], qp))
+                continue;
+            tu4 |= 1 << k;
+            r2.sse_full += r4.node_sse[k] - r2.node_sse[k];
+            r2.sse_y_full += r4.node_sse[k] - r2.node_sse[k];
+            r2.sse[0] += r4.node_disp[k] - r2.node_disp[k];
+            r2.bits += r4.node_bits[k] - r2.node_bits[k];
+            r2.bits_y += r4.node_bits[k] - r2.node_bits[k];
+            // node k's levels and luma reconstruction from the 4x4 option
+            lv2[wave][64 * k + lane] = lv4[wave][64 * k + lane];
+            {
+                const int ry = (k >> 1) * 8 + (lane >> 3), rx = (k & 1) * 8 + (lane & 7);
+                rec2[wave][ry * 16 + rx] = rec4[wave][ry * 16 + rx];
+            }
+        }
+        wave_lds_sync();
+    }
     const int sse2 = r2.sse_full, bits2 = (int)r2.bits;
     const int sse2y = r2.sse[0], sse2u = r2.sse[1], sse2v = r2.sse[2];
     const bool split = try_split &&
@@ -826,9 +984,9 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         part[2][wave] = valid ? (unsigned long long)(changing ? dcp_v : (split ? sse2v : r.sse[2])) : 0ull;
     }
     SplitSummary ss = {};
-    if (split) ss = split_summary_wave(lv2[wave], lane);  // wave-uniform branch
+    if (split) ss = split_summary_wave(lv2[wave], lane, tu4);  // wave-uniform branch
     if (valid && lane == 0) {
-        CuInfo c;
+        CuInfo c{};
         c.type = kCuAmvp;
         c.intra_mode = 1;
         c.qp = (uint8_t)qp;
@@ -844,13 +1002,14 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
         if (drop) {  // no residual left (chroma was dropped before coding): cu_summarise of zeros
             c.tu_split = fs->tu_split ? 1 : 0;
             c.cbf = c.cbf_y4 = c.cbf_c4 = 0;
+            c.tu4 = 0;
+            c.cbf_y16 = 0;
             c.last[0] = c.last[1] = c.last[2] = 0;
             c.csbf_y = 0;
             c.csbf_c[0] = c.csbf_c[1] = 0;
         }
         set_est_bytes(c, split ? r2.bits : r.bits);
         c.ct = 1;
-        for (int k = 0; k < 7; ++k) c.rsv[k] = 0;
         cus[i] = c;  // skip / merge / AMVP and the coding tree are decided by k_hevc_decide once the slices are laid out
         qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
         unit_cost[wave] = cu_cost(c);
@@ -1169,7 +1328,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             acc[1] += (unsigned)res.sse[1];
             acc[2] += (unsigned)res.sse[2];
             if (lane == 0) {
-                CuInfo c;
+                CuInfo c{};
                 c.type = kCuIntra;
                 c.intra_mode = (uint8_t)mode;
                 c.qp = (uint8_t)qp;
@@ -1177,7 +1336,6 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 c.mvp_idx = 0;
                 fill_cu(c, res);
                 c.ct = 1;
-                for (int k = 0; k < 7; ++k) c.rsv[k] = 0;
                 set_est_bytes(c, res.bits);
                 cus[i] = c;
                 // (no slice cost: I pictures use fixed CTB-row slices)
@@ -1355,7 +1513,7 @@ __device__ __forceinline__ CuInfo load_cu(const CuInfo* cus, int i) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(cus) + (size_t)i * kCuWords;
     uint32_t w[kCuWords];
     for (int q = 0; q < kCuWords; ++q) w[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[q]);
-    CuInfo c;
+    CuInfo c{};
     __builtin_memcpy(&c, w, sizeof c);
     return c;
 }

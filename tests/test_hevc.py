@@ -252,6 +252,16 @@ def test_gpu_hevc_tu_split_bit_exact_vs_cpu(gpu, w, h, qp):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("w,h,qp,desktop", [(64, 48, 26, False), (160, 96, 30, False), (320, 192, 28, True),
+                                            (1920, 1080, 34, True)])
+def test_gpu_hevc_4x4_luma_tus_bit_exact_vs_cpu(gpu, w, h, qp, desktop):
+    """tu_split 2 on the GPU (split4_luma: sixteen 4x4 luma TUs on 4 lanes each, per-node SSE +
+    lambda * bits choice against the 8x8 TU) == the CPU encoder, bit for bit; decoded ==
+    reconstruction (CU32 / CU16 coding trees, deblocking, SAO on)."""
+    _gpu_vs_cpu(gpu, w, h, 4, qp=qp, tu_split=2, aq=4 if desktop else 1, desktop=desktop)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("w,h,qp,tu_split,aq", [(320, 192, 30, 0, 3), (320, 192, 26, 1, 3), (1920, 1080, 34, 1, 3),
                                                  (320, 192, 30, 1, 4), (1920, 1080, 34, 1, 6)])
 def test_gpu_hevc_temporal_classes_bit_exact_vs_cpu(gpu, w, h, qp, tu_split, aq):
@@ -336,6 +346,46 @@ def test_cpu_hevc_tu_split_decodes_to_reconstruction(native, w, h, qp):
     reproduce the reconstruction exactly and must actually see split trees."""
     out, src, sizes, dec, _ = _cpu_roundtrip(native, w, h, 4, qp=qp, fresh=True, tu_split=1)
     assert dec.stats.get("tu_split", 0) > 0
+
+
+@pytest.mark.parametrize("w,h,qp", [(64, 48, 26), (160, 96, 30), (320, 192, 34)])
+def test_cpu_hevc_4x4_luma_tus_decode_to_reconstruction(native, w, h, qp):
+    """tu_split 2: 8x8 luma nodes of split inter trees may code four 4x4 TUs (split_transform_flag
+    at the 8x8 node, cbf_luma and cu_qp_delta per 4x4 TU, the node's chroma after the fourth) --
+    the decoder reproduces the reconstruction and sees 4x4 trees."""
+    cfg = _cfg(native, w, h, qp=qp, tu_split=2)
+    enc = native.CpuHevcEncoder(cfg)
+    stream, recon, n4 = b"", [], 0
+    for t in range(4):
+        y, uv = synthetic_nv12(w, h, t, seed=t)
+        stream += enc.encode(y, uv, False)
+        recon.append(tuple(p.copy() for p in enc.recon()))
+        n4 += int((enc.cu_info()[:, 5] != 0).sum())
+    dec = Decoder()
+    dec.decode(stream)
+    for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, recon):
+        assert np.array_equal(yy, ry) and np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2])
+    assert n4 > 0, "no unit chose 4x4 luma TUs"
+
+
+def test_cpu_hevc_4x4_luma_tus_save_bits_on_desktop(native):
+    """On the synthetic desktop (text, window edges) 4x4 luma TUs code P pictures in fewer bytes at
+    no worse PSNR than 8x8-only split trees."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    res = {}
+    for split in (1, 2):
+        enc = native.CpuHevcEncoder(_cfg(native, 320, 192, qp=30, tu_split=split, aq=4))
+        desk = CpuSyntheticDesktop(320, 192, False)
+        nbytes, err = 0, 0.0
+        for f in range(8):
+            y, uv = bgrx_to_nv12(desk.render(f, f / 60, 0))
+            au = enc.encode(y, uv, False)
+            if f:
+                nbytes += len(au)
+                err += float(((enc.recon()[0][:192, :320].astype(np.int64) - y) ** 2).sum())
+        res[split] = (nbytes, err)
+    assert res[2][0] < res[1][0] * 0.95 and res[2][1] <= res[1][1], res
 
 
 def test_cpu_hevc_tu_split_saves_bits_on_desktop_content(native):
