@@ -61,6 +61,12 @@ struct ScaleMfma {
     const float* sh = nullptr;  // [ngx][32] sum of each column's f16 weights (input bias removal)
     const void* fv = nullptr;   // [ngy][kMaxRb][2][64 lanes] 8 x f16 vertical weight fragments
     int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0;
+    // strip form (k_scale_strip: `strip` consecutive 32-row tiles per workgroup, 0 = unavailable):
+    // per tile (first input row of its strip, first block | blocks << 8 relative to it, 0) and the
+    // vertical fragments against those strip-relative 32-row blocks
+    const int* gy2 = nullptr;   // [ngy][3]
+    const void* fv2 = nullptr;  // [ngy][kMaxRb][2][64 lanes]
+    int strip = 0;
 };
 struct LanczosTables {
     int out_w, out_h, taps_x, taps_y;
@@ -76,8 +82,8 @@ struct LanczosTables {
 // scale factor is outside what the MFMA kernel's register tiles hold (then the VALU kernel runs).
 struct ScaleFragsHost {
     std::vector<uint8_t> blob;
-    size_t off_gx = 0, off_gy = 0, off_fh = 0, off_sh = 0, off_fv = 0;
-    int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0;
+    size_t off_gx = 0, off_gy = 0, off_fh = 0, off_sh = 0, off_fv = 0, off_gy2 = 0, off_fv2 = 0;
+    int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0, strip = 0;
 };
 bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, int coded_h,
                        const std::vector<int>& x0, const std::vector<float>& wx, int tx, const std::vector<int>& y0,

@@ -600,6 +600,8 @@ __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict
 // cross the left/right image edge are rewritten with clamped pixels.
 constexpr int kMfKs = 8;  // max horizontal K-steps (16 input columns each) per 32 output columns
 constexpr int kMfRb = 4;  // max 32-row input blocks per 32 output rows
+constexpr int kStripRing = 3;  // k_scale_strip: LDS ring of 32-row input blocks (one computed, two in flight)
+constexpr int kStripMaxT = 4;  // k_scale_strip: most 32-row output tiles per workgroup
 typedef _Float16 mf_h8 __attribute__((ext_vector_type(8)));
 typedef float mf_f16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -711,6 +713,9 @@ __device__ __forceinline__ void mf_main(char* __restrict__ buf0, char* __restric
     }
 }
 
+__device__ __forceinline__ void mf_epilogue(const mf_f16* Y, int g0, int wave, int v, int lane, uint8_t* __restrict__ yp,
+                                            uint8_t* __restrict__ uvp, int out_pitch, int coded_w, int coded_h);
+
 __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
                                                     ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
                                                     int out_pitch, int coded_w, int coded_h, uint64_t* ts) {
@@ -755,9 +760,16 @@ __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ 
     for (int c = 0; c < 3; ++c) Y[c] = (mf_f16){};
     mf_main(smem, smem + buf_bytes, in, in_pitch, in_w, in_h, xlo, ylo, nr, nrb, nq, m.lds_cols, loff, kb, nks, wave,
             lane, bh, av, bias, Y);
-    // epilogue: Y[c][rho] is output column ox, row oy0 + (rho & 3) + 8 * (rho >> 2) + 4h;
-    // two rows at a time in packed 16-bit lanes (BT.709 sums stay below 2^16)
+    mf_epilogue(Y, g0, wave, v, lane, yp, uvp, out_pitch, coded_w, coded_h);
+}
+
+// Output of one wave's 32 x 32 block: Y[c][rho] is output column ox, row oy0 + (rho & 3) + 8 *
+// (rho >> 2) + 4h; two rows at a time in packed 16-bit lanes (BT.709 sums stay below 2^16), the
+// 2x2 chroma with the neighbouring column's lane
+__device__ __forceinline__ void mf_epilogue(const mf_f16* Y, int g0, int wave, int v, int lane, uint8_t* __restrict__ yp,
+                                            uint8_t* __restrict__ uvp, int out_pitch, int coded_w, int coded_h) {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const int h = lane >> 5, l32 = lane & 31;
     const int ox = 32 * (g0 + wave) + l32, oy0 = 32 * v + 4 * h;
     const bool xin = ox < coded_w;
 #pragma unroll
@@ -783,6 +795,147 @@ __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ 
             const int Bc = (((packed >> 20) & 1023) + ((other >> 20) & 1023) + 2) >> 2;
             *reinterpret_cast<uint16_t*>(uvp + ((uint32_t)(oy >> 1) * (uint32_t)out_pitch + (uint32_t)ox)) =
                 (uint16_t)(u709(Rc, Gc, Bc) | (v709(Rc, Gc, Bc) << 8));
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------- MFMA scaler, strip form
+// One workgroup (2 waves, 64 output columns) per column strip of up to kStripMaxT consecutive
+// 32-row output tiles.  The strip's input rows are staged in 32-row blocks counted from its first
+// tap row through an LDS ring of kStripRing blocks: the DMA of the next two blocks is in flight
+// while the current one's products run, and a block that two vertically adjacent tiles both read
+// is loaded once and its horizontal product (X = In * Wh) computed once, then accumulated into
+// both tiles' vertical products (two accumulator sets: the tile being finished and the next).
+// The one-tile-per-workgroup form (k_scale_mfma) ran load, products and stores as three
+// machine-wide phases, each workgroup's chain unhidden (profiles/r02_scale/NOTES.md).
+__global__ __launch_bounds__(128) void k_scale_strip(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
+                                                     ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
+                                                     int out_pitch, int coded_w, int coded_h, uint64_t* ts) {
+    stamp_start(ts);
+    // LDS: the ring of 32-row footprint blocks [32][lds_cols] BGRx, then the strip's vertical
+    // weight fragments [tile][kMfRb][2][64 lanes]
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int sx, sy;
+    {  // XCD-aware order: every XCD a contiguous band of strips (neighbouring footprints share its L2)
+        const int nwg = gridDim.x * gridDim.y, id = blockIdx.y * gridDim.x + blockIdx.x;
+        const int per = nwg >> 3, xcd = id & 7, k = id >> 3;
+        const int lin = k >= per ? id : xcd * per + k;
+        sx = lin % gridDim.x;
+        sy = lin / gridDim.x;
+    }
+    const int T = m.strip;
+    const int g0 = 2 * sx, gw = min(g0 + wave, m.ngx - 1);
+    const int v0 = sy * T, v1 = min(v0 + T, m.ngy), nt = v1 - v0;
+    const int base = m.gy2[3 * v0];
+    const int lastinfo = m.gy2[3 * (v1 - 1) + 1];
+    const int nb = (lastinfo & 255) + (lastinfo >> 8);  // blocks of the strip
+    const int xlo = m.gx[2 * g0];
+    const int nq = m.lds_cols >> 2;
+    const size_t buf_bytes = (size_t)32 * m.lds_cols * 4;
+    uint4* fvl = reinterpret_cast<uint4*>(smem + kStripRing * buf_bytes);
+    const uint32_t loff = (uint32_t)min(max(xlo + 4 * lane, 0), in_w - 4) * 4;
+    // weights (ordinary loads, all waited for before the first block's DMA is issued, so the DMA
+    // waits below count blocks only)
+    const int nks = m.gx[2 * gw + 1], kb = m.gx[2 * gw] - xlo;
+    const uint4* fh = reinterpret_cast<const uint4*>(m.fh) + (size_t)gw * kMfKs * 64 + lane;
+    mf_h8 bh[kMfKs];
+#pragma unroll
+    for (int s = 0; s < kMfKs; ++s) bh[s] = __builtin_bit_cast(mf_h8, s < nks ? fh[s * 64] : make_uint4(0, 0, 0, 0));
+    const uint4* fv = reinterpret_cast<const uint4*>(m.fv2) + (size_t)v0 * kMfRb * 128;
+    for (int k = tid; k < nt * kMfRb * 128; k += 128) fvl[k] = fv[k];
+    const float bias = 1024.f * m.sh[gw * 32 + l32];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    const bool edge = xlo < 0 || xlo + 4 * nq > in_w;  // workgroup-uniform
+    for (int i = 0; i < kStripRing - 1 && i < nb; ++i)
+        mf_stage(in, in_pitch, in_h, base, 32 * i, 32 * nb, nq, loff, smem + (size_t)(i % kStripRing) * buf_bytes, wave,
+                 lane);
+    constexpr uint32_t kSel[3] = {0x0c040c00u, 0x0c050c01u, 0x0c060c02u};  // B, G, R
+    mf_f16 Y0[3], Y1[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Y0[c] = Y1[c] = (mf_f16){};
+    int vt = v0;  // the oldest tile not stored yet (Y0); vt + 1 accumulates in Y1
+#pragma unroll 1
+    for (int i = 0; i < nb; ++i) {
+        if (i > 0) mf_barrier();  // every wave is done with block i - 1, whose slot is refilled now
+        const int nxt = i + kStripRing - 1;
+        if (nxt < nb)
+            mf_stage(in, in_pitch, in_h, base, 32 * nxt, 32 * nb, nq, loff,
+                     smem + (size_t)(nxt % kStripRing) * buf_bytes, wave, lane);
+        // this wave's DMA of block i retired: the blocks issued after it (16 row loads each) may stay in flight
+        const int ahead = min(nxt, nb - 1) - i;
+        if (ahead >= 2)
+            __builtin_amdgcn_s_waitcnt(0x8F70);  // vmcnt(32)
+        else if (ahead == 1)
+            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        mf_barrier();
+        char* cur = smem + (size_t)(i % kStripRing) * buf_bytes;
+        if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
+            for (int r = wave; r < 32; r += 2) {
+                const int sx4 = xlo + 4 * lane;
+                if (lane >= nq || (sx4 >= 0 && sx4 + 4 <= in_w)) continue;
+                const uint8_t* row = in + (size_t)min(max(base + 32 * i + r, 0), in_h - 1) * in_pitch;
+                uint4 px;
+                px.x = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4, 0), in_w - 1) * 4);
+                px.y = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4 + 1, 0), in_w - 1) * 4);
+                px.z = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4 + 2, 0), in_w - 1) * 4);
+                px.w = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4 + 3, 0), in_w - 1) * 4);
+                *reinterpret_cast<uint4*>(cur + ((size_t)r * nq + lane) * 16) = px;
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // (these loads are the only ones left in flight)
+            __syncthreads();
+        }
+        // the tiles block i feeds: vt and / or vt + 1 (wave-uniform)
+        const int i0 = m.gy2[3 * vt + 1], b0 = i0 & 255, n0 = i0 >> 8;
+        const bool use0 = i >= b0 && i < b0 + n0;
+        bool use1 = false;
+        int b1 = 0;
+        if (vt + 1 < v1) {
+            const int i1 = m.gy2[3 * (vt + 1) + 1];
+            b1 = i1 & 255;
+            use1 = i >= b1 && i < b1 + (i1 >> 8);
+        }
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(cur) + l32 * m.lds_cols + kb + 8 * h;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            mf_f16 X = {};
+#pragma unroll
+            for (int s = 0; s < kMfKs; ++s) {
+                if (s > 0 && s >= nks) break;
+                const uint4 p0 = *reinterpret_cast<const uint4*>(rp + 16 * s);
+                const uint4 p1 = *reinterpret_cast<const uint4*>(rp + 16 * s + 4);
+                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(mf_chan(p0, p1, kSel[c]), bh[s], X, 0, 0, 0);
+            }
+            mf_h8 x0, x1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                x0[j] = (_Float16)(X[j] - bias);
+                x1[j] = (_Float16)(X[8 + j] - bias);
+            }
+            if (use0) {
+                const uint4* f = fvl + ((size_t)(vt - v0) * kMfRb + (i - b0)) * 128 + lane;
+                Y0[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[0]), x0, Y0[c], 0, 0, 0);
+                Y0[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[64]), x1, Y0[c], 0, 0, 0);
+            }
+            if (use1) {
+                const uint4* f = fvl + ((size_t)(vt + 1 - v0) * kMfRb + (i - b1)) * 128 + lane;
+                Y1[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[0]), x0, Y1[c], 0, 0, 0);
+                Y1[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[64]), x1, Y1[c], 0, 0, 0);
+            }
+        }
+        if (use0 && i == b0 + n0 - 1) {  // tile vt is complete
+            mf_epilogue(Y0, g0, wave, vt, lane, yp, uvp, out_pitch, coded_w, coded_h);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                Y0[c] = Y1[c];
+                Y1[c] = (mf_f16){};
+            }
+            ++vt;
         }
     }
 }
@@ -1002,13 +1155,61 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
         }
     }
     if ((size_t)2 * 32 * lds_cols * 4 > 160 * 1024 || lds_cols > 256) return false;  // one row per wave load
+    // strip form: tiles v0 .. v0 + T - 1 share one workgroup; blocks of 32 input rows counted from the
+    // strip's first tap row; every block may feed at most two tiles (the kernel's two accumulators)
+    std::vector<int> gy2(3 * (size_t)ngy, 0);
+    std::vector<uint16_t> fv2((size_t)ngy * kMfRb * 2 * 64 * 8, 0);
+    int strip = kStripMaxT;
+    for (; strip >= 1; --strip) {
+        bool ok = (size_t)kStripRing * 32 * lds_cols * 4 + (size_t)strip * kMfRb * 128 * 16 <= 152 * 1024;
+        for (int v = 0; v < ngy && ok; ++v) {
+            const int v0 = v - v % strip;
+            const int base = y0[std::min(32 * v0, out_h - 1)];
+            const int first = y0[std::min(32 * v, out_h - 1)], last = y0[std::min(32 * v + 31, out_h - 1)] + ty - 1;
+            const int blo = (first - base) >> 5, nrb = ((last - base) >> 5) - blo + 1;
+            if (nrb > kMfRb || blo > 255) ok = false;
+            // tile v + 2 of the strip must not reach back into the blocks of tile v
+            if (v >= v0 + 2) {
+                const int pfirst = y0[std::min(32 * (v - 2), out_h - 1)];
+                const int plast = y0[std::min(32 * (v - 2) + 31, out_h - 1)] + ty - 1;
+                (void)pfirst;
+                if (((plast - base) >> 5) >= blo) ok = false;
+            }
+            gy2[3 * v] = base;
+            gy2[3 * v + 1] = blo | (nrb << 8);
+        }
+        if (ok) break;
+    }
+    if (strip >= 1) {
+        for (int v = 0; v < ngy; ++v) {
+            const int base = gy2[3 * v], blo = gy2[3 * v + 1] & 255, nrb = gy2[3 * v + 1] >> 8;
+            for (int l = 0; l < 64; ++l) {
+                const int oy = std::min(32 * v + (l & 31), out_h - 1), hh = l >> 5;
+                for (int b = 0; b < nrb; ++b)
+                    for (int t = 0; t < 2; ++t)
+                        for (int j = 0; j < 8; ++j) {
+                            const int q = 16 * t + 8 * (j >> 2) + 4 * hh + (j & 3);
+                            const int tap = base + 32 * (blo + b) + q - y0[oy];
+                            if (tap < 0 || tap >= ty) continue;
+                            fv2[((((size_t)v * kMfRb + b) * 2 + t) * 64 + l) * 8 + j] = f16(wy[(size_t)oy * ty + tap]).first;
+                        }
+            }
+        }
+    } else {
+        strip = 0;
+    }
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     out.off_gx = 0;
     out.off_gy = align(gx.size() * 4);
     out.off_sh = out.off_gy + align(gy.size() * 4);
     out.off_fh = out.off_sh + align(sh.size() * 4);
     out.off_fv = out.off_fh + align(fh.size() * 2);
-    out.blob.assign(out.off_fv + align(fv.size() * 2), 0);
+    out.off_gy2 = out.off_fv + align(fv.size() * 2);
+    out.off_fv2 = out.off_gy2 + align(gy2.size() * 4);
+    out.blob.assign(out.off_fv2 + align(fv2.size() * 2), 0);
+    std::memcpy(out.blob.data() + out.off_gy2, gy2.data(), gy2.size() * 4);
+    std::memcpy(out.blob.data() + out.off_fv2, fv2.data(), fv2.size() * 2);
+    out.strip = strip;
     std::memcpy(out.blob.data() + out.off_gx, gx.data(), gx.size() * 4);
     std::memcpy(out.blob.data() + out.off_gy, gy.data(), gy.size() * 4);
     std::memcpy(out.blob.data() + out.off_sh, sh.data(), sh.size() * 4);
@@ -1036,10 +1237,27 @@ void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf) {
     mf.lds_rows = h.lds_rows;
     mf.ngx = h.ngx;
     mf.ngy = h.ngy;
+    mf.gy2 = reinterpret_cast<const int*>(b + h.off_gy2);
+    mf.fv2 = b + h.off_fv2;
+    mf.strip = h.strip;
 }
 
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
                           uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream, uint64_t* ts) {
+    static const bool legacy = [] {
+        const char* e = std::getenv("MXDESK_SCALER");
+        return e && std::string(e) == "tile";
+    }();
+    if (t.mf.gx && t.mf.strip > 0 && !legacy && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 &&
+        in_w >= 4) {
+        const size_t lds = (size_t)kStripRing * 32 * t.mf.lds_cols * 4 + (size_t)t.mf.strip * kMfRb * 128 * 16;
+        ensure_func_attr(reinterpret_cast<const void*>(&k_scale_strip), hipFuncAttributeMaxDynamicSharedMemorySize,
+                         160 * 1024);
+        dim3 grid((coded_w + 63) / 64, (t.mf.ngy + t.mf.strip - 1) / t.mf.strip);
+        hipLaunchKernelGGL(k_scale_strip, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv,
+                           out_pitch, coded_w, coded_h, ts);
+        return;
+    }
     if (t.mf.gx && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 && in_w >= 4) {
         const size_t lds = (size_t)2 * 32 * t.mf.lds_cols * 4;
         if (lds > 64 * 1024) {

@@ -53,10 +53,10 @@ def _lanczos_ref(img, xs, wx, ys, wy):
     return np.clip(np.rint(out), 0, 255)
 
 
-@pytest.mark.parametrize("mfma", [False, True])
+@pytest.mark.parametrize("mfma,strip", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("src_hw,dst_hw", [((96, 160), (48, 80)), ((64, 96), (96, 128)), ((90, 150), (60, 100)),
-                                           ((270, 500), (108, 200)), ((200, 330), (100, 166))])
-def test_lanczos_scale_matches_reference(gpu, src_hw, dst_hw, mfma):
+                                           ((270, 500), (108, 200)), ((200, 330), (100, 166)), ((540, 960), (270, 480))])
+def test_lanczos_scale_matches_reference(gpu, src_hw, dst_hw, mfma, strip):
     rng = np.random.default_rng(1)
     (h, w), (oh, ow) = src_hw, dst_hw
     yy, xx = np.mgrid[0:h, 0:w]
@@ -72,7 +72,7 @@ def test_lanczos_scale_matches_reference(gpu, src_hw, dst_hw, mfma):
     y = torch.zeros((ch, cw), dtype=torch.uint8, device="cuda")
     uv = torch.zeros((ch // 2, cw), dtype=torch.uint8, device="cuda")
     gpu.scale_to_nv12(d_in.data_ptr(), w * 4, w, h, ow, oh, dx.data_ptr(), dwx.data_ptr(), tx, dy.data_ptr(),
-                      dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), cw, cw, ch, _stream(), mfma=mfma)
+                      dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), cw, cw, ch, _stream(), mfma=mfma, strip=strip)
     torch.cuda.synchronize()
     rgb = _lanczos_ref(img, xs, wx, ys, wy)
     ref_bgrx = np.zeros((oh, ow, 4), np.uint8)
@@ -98,17 +98,19 @@ def test_lanczos_mfma_matches_valu_at_4k_to_1080p(gpu):
     ys, wy, ty = gpu.lanczos_table(h, oh)
     dx, dwx, dy, dwy = to_dev(xs), to_dev(wx), to_dev(ys), to_dev(wy)
     out = {}
-    for mfma in (False, True):
+    for form in ("valu", "tile", "strip"):
         y = torch.zeros((1088, 1920), dtype=torch.uint8, device="cuda")
         uv = torch.zeros((544, 1920), dtype=torch.uint8, device="cuda")
         gpu.scale_to_nv12(src.data_ptr(), w * 4, w, h, ow, oh, dx.data_ptr(), dwx.data_ptr(), tx, dy.data_ptr(),
-                          dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), 1920, 1920, 1088, _stream(), mfma=mfma)
+                          dwy.data_ptr(), ty, y.data_ptr(), uv.data_ptr(), 1920, 1920, 1088, _stream(),
+                          mfma=form != "valu", strip=form == "strip")
         torch.cuda.synchronize()
-        out[mfma] = (y.cpu().numpy().astype(np.int32), uv.cpu().numpy().astype(np.int32))
-    dyp = np.abs(out[True][0] - out[False][0])
-    duv = np.abs(out[True][1] - out[False][1])
-    assert dyp.max() <= 1 and duv.max() <= 1, (dyp.max(), duv.max())
-    assert (dyp > 0).mean() < 0.02 and (duv > 0).mean() < 0.02, ((dyp > 0).mean(), (duv > 0).mean())
+        out[form] = (y.cpu().numpy().astype(np.int32), uv.cpu().numpy().astype(np.int32))
+    for form in ("tile", "strip"):  # both matrix-core forms against the VALU kernel
+        dyp = np.abs(out[form][0] - out["valu"][0])
+        duv = np.abs(out[form][1] - out["valu"][1])
+        assert dyp.max() <= 1 and duv.max() <= 1, (form, dyp.max(), duv.max())
+        assert (dyp > 0).mean() < 0.02 and (duv > 0).mean() < 0.02, (form, (dyp > 0).mean(), (duv > 0).mean())
 
 
 def _read_barcode(y_plane, cell, bx, by):
