@@ -268,7 +268,8 @@ def main() -> None:
                     help="adaptive quantisation: 0 off, 1 coarser QP for noise-like MBs, 2 + rate-distortion "
                          "residual drop for them (default: the encoder's)")
     ap.add_argument("--deblock", type=int, default=None,
-                    help="in-loop deblocking filter 0/1 (default: the encoder's)")
+                    help="in-loop deblocking filter 0 off / 1 on / 2 adaptive per picture (H.264: "
+                         "from the picture's temporal classes; default: the encoder's)")
     ap.add_argument("--chroma-qp-offset", type=int, default=None,
                     help="chroma QP offset against luma (H.264 chroma_qp_index_offset / HEVC pps_cb/cr_qp_offset; "
                          "default: the encoder's)")
@@ -438,7 +439,7 @@ def main() -> None:
 
     barrier()
     t0 = time.perf_counter()
-    lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m, psnr_uv = [], [], [], [], [], [], []
+    lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m, psnr_uv, dbk = [], [], [], [], [], [], [], []
     if K == 1 and args.depth == 1 and gpu:
         results = [sessions[0].step(False) for _ in range(args.steps)]
     else:
@@ -453,6 +454,7 @@ def main() -> None:
         psnrs_m.append(r.psnr_y_masked if args.noise else r.psnr_y)
         psnr_uv.append((r.psnr_u, r.psnr_v))
         gpu_ms.append(r.gpu_ms)
+        dbk.append(getattr(r, "deblocked", 0))
 
     quality = None
     if args.quality_probe > 0 and rank == 0 and not args.out_width:
@@ -504,6 +506,7 @@ def main() -> None:
             "device": args.device,
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
+            "deblocked_frames_pct": round(100.0 * sum(dbk) / max(1, len(dbk)), 1),
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),
             "mean_qp": round(statistics.mean(qps), 2),

@@ -177,7 +177,10 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("encode_ms", &h264::FrameStats::encode_ms)
         .def_property_readonly("sse", [](const h264::FrameStats& s) { return py::make_tuple(s.sse[0], s.sse[1], s.sse[2]); })
         .def_readonly("sse_masked", &h264::FrameStats::sse_masked)
-        .def_readonly("masked_pixels", &h264::FrameStats::masked_pixels);
+        .def_readonly("masked_pixels", &h264::FrameStats::masked_pixels)
+        .def_readonly("deblocked", &h264::FrameStats::deblocked)
+        .def_readonly("db_coherent", &h264::FrameStats::db_coherent)
+        .def_readonly("db_changed", &h264::FrameStats::db_changed);
 
     py::class_<h264::CpuH264Encoder>(m, "CpuH264Encoder")
         .def(py::init<const h264::EncoderConfig&>())
@@ -669,6 +672,7 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("psnr_u", &FrameResult::psnr_u)
         .def_readonly("psnr_v", &FrameResult::psnr_v)
         .def_readonly("psnr_y_masked", &FrameResult::psnr_y_masked)
+        .def_readonly("deblocked", &FrameResult::deblocked)
         .def_property_readonly("au", [](const FrameResult& r) { return to_bytes(r.au); });
 
     m.def(

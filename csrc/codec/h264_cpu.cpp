@@ -588,6 +588,18 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
                       mb_[mbi], coef_.data() + (size_t)mbi * kCoefStride);
 }
 
+void CpuH264Encoder::decide_deblock() {
+    db_counts_ = DbAutoCounts{};
+    deblock_now_ = cfg_.h264_deblock();
+    if (!cfg_.h264_deblock_auto()) return;
+    if (!common_.cur_idr()) {  // an IDR picture keeps the last P decision
+        const Geometry g = geom_of(common_, cw_, ch_);
+        for (int i = 0; i < g.mb_w * g.mb_h; ++i) db_auto_count(mb_.data(), g.mb_w, i, db_counts_);
+        db_prev_on_ = db_auto_decide(db_counts_, g.mb_w * g.mb_h, db_prev_on_);
+    }
+    deblock_now_ = db_prev_on_;
+}
+
 void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& soff, std::vector<uint32_t>& slen) {
     const Geometry g = geom_of(common_, cw_, ch_);
     const bool idr = common_.cur_idr();
@@ -602,7 +614,7 @@ void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t
         w.init(words.data());
         write_slice_header(w, make_slice_params(first, idr, common_.cur_frame_num(), common_.log2_max_frame_num(),
                                                 common_.cur_idr_pic_id(), frame_qp_() - common_.pic_init_qp(),
-                                                cfg_.h264_deblock() ? 0 : 1));
+                                                deblock_now_ ? 0 : 1));
         int run = 0;
         int qp_pred = frame_qp_();  // mb_qp_delta predictor: QP of the last MB that carried one
         for (int mbi = first; mbi < last; ++mbi) {
@@ -666,10 +678,11 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
         encode_intra(y, uv, pitch);
     else
         encode_inter(y, uv, pitch);
+    decide_deblock();
     std::vector<uint8_t> payload;
     std::vector<uint32_t> soff, slen;
     entropy(payload, soff, slen);
-    if (cfg_.h264_deblock()) {  // in-loop filter: the next picture predicts from the filtered one
+    if (deblock_now_) {  // in-loop filter: the next picture predicts from the filtered one
         const Geometry g = geom_of(common_, cw_, ch_);
         std::vector<uint8_t> qpe(mb_.size());
         db_qp_eff(mb_.data(), (int)mb_.size(), g.mb_w, common_.cur_idr() ? idr_slice_rows(g.mb_h) : g.mb_h,
@@ -688,6 +701,9 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     stats_.qp = common_.cur_qp();
     stats_.bytes = (int)au_.size();
     stats_.skipped_mbs = skipped;
+    stats_.deblocked = deblock_now_ ? 1 : 0;
+    stats_.db_coherent = (int)db_counts_.coherent;
+    stats_.db_changed = (int)db_counts_.changed;
     common_.end_frame((int)au_.size(), common_.cur_idr());
     have_ref_ = true;
     return au_;

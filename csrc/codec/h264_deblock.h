@@ -5,7 +5,8 @@
 // implements the same clause from the spec side and checks the result.
 //
 // Subset: frame macroblocks, one reference picture, disable_deblocking_filter_idc 0 with zero
-// alpha / beta offsets (the slice header writes idc 0 when EncoderConfig::deblock is on).
+// alpha / beta offsets (the slice header writes idc 0 when EncoderConfig::deblock is on, per
+// picture by db_auto_decide when it is adaptive).
 #pragma once
 #include "h264_core.h"
 #include "h264_gpu.h"
@@ -133,6 +134,39 @@ MXHD void db_chroma_line(int p1, int& p0, int& q0, int q1, int bs, const DbParam
     }
     p0 = (2 * p1 + P0 + q1 + 2) >> 2;
     q0 = (2 * q1 + Q0 + p1 + 2) >> 2;
+}
+
+// Adaptive in-loop filtering (EncoderConfig::deblock 2): disable_deblocking_filter_idc of a picture
+// chosen from its temporal classes.  Filtering pays on moving content (sub-sample motion
+// compensation of a pan or a video leaves block edges the filter smooths: +1.3 dB on the motion
+// bench, profiles/r04_toolset/NOTES.md) and costs on a still desktop (it softens text and window
+// edges the encoder codes exactly: -1.1 dB).  The class is taken from the coded macroblocks:
+//  * coherent: an inter MB with a nonzero vector equal to its left or upper neighbour's (a pan, a
+//    scroll, a moving video -- not the random vectors of noise);
+//  * changed: an intra MB, or an inter MB with residual and a zero vector (text updates, cursor).
+// A P picture is filtered when coherent motion covers 1/8 of it (1/32 while the previous decision
+// was on: hysteresis, so a slowing pan does not toggle the filter every frame); an IDR picture
+// keeps the previous decision.  Same integer rule in k_db_prep and the CPU encoder.
+struct DbAutoCounts {
+    uint32_t coherent = 0, changed = 0;
+};
+MXHD void db_auto_count(const MbInfo* mbs, int mb_w, int i, DbAutoCounts& c) {
+    const MbInfo& m = mbs[i];
+    if (is_intra(m)) {
+        ++c.changed;
+        return;
+    }
+    const bool moving = m.mvx != 0 || m.mvy != 0;
+    if (!moving) {
+        if (m.cbp) ++c.changed;
+        return;
+    }
+    const int x = i % mb_w;
+    auto same = [&](const MbInfo& n) { return !is_intra(n) && n.mvx == m.mvx && n.mvy == m.mvy; };
+    if ((x > 0 && same(mbs[i - 1])) || (i >= mb_w && same(mbs[i - mb_w]))) ++c.coherent;
+}
+MXHD bool db_auto_decide(const DbAutoCounts& c, int nmb, bool prev_on) {
+    return (uint64_t)c.coherent * (prev_on ? 32u : 8u) >= (uint64_t)nmb;
 }
 
 // QP_Y of every macroblock as a decoder sees it: the MB's own QP where it carries mb_qp_delta,

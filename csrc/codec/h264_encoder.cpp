@@ -272,6 +272,7 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMemsetAsync(b.db_gprog, 0, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h, stream_));
     HIP_CHECK(hipMalloc(&b.pack_done, sizeof(uint32_t)));
     HIP_CHECK(hipMemsetAsync(b.pack_done, 0, sizeof(uint32_t), stream_));
+    b.db_auto = db_auto_;
     HIP_CHECK(hipHostMalloc(&b.db_err, sizeof(int), hipHostMallocMapped));
     *b.db_err = 0;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
@@ -338,6 +339,8 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     hp_pitch_ = (geom_.coded_w + 2 * kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
+    HIP_CHECK(hipMalloc(&db_auto_, sizeof(uint32_t) * 4));
+    HIP_CHECK(hipMemsetAsync(db_auto_, 0, sizeof(uint32_t) * 4, stream_));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     clock_khz_ = device_clock_khz();
     if (depth_ > 1) {
@@ -433,6 +436,7 @@ GpuH264Encoder::~GpuH264Encoder() {
     }
     for (int i = 0; i < 4; ++i) (void)hipFree(hp_[i]);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
+    if (db_auto_) (void)hipFree(db_auto_);
 }
 
 void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
@@ -539,7 +543,10 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.me_coarse = cfg_.me_coarse;
     f.intra4x4 = cfg_.intra4x4;
     f.subpel = cfg_.subpel;
-    f.deblock_off = cfg_.h264_deblock() ? 0 : 1;
+    f.deblock_off = cfg_.h264_deblock() ? 0 : 1;  // adaptive: k_db_prep overwrites it on the device
+    f.deblock_auto = cfg_.h264_deblock_auto() ? 1 : 0;
+    f.db_coherent = 0;
+    f.db_changed = 0;
     if (++db_epoch_ > 0xfffffu) db_epoch_ = 1;  // 20-bit tag, never 0
     f.db_epoch = (int32_t)db_epoch_;
     f.pic_init_qp = common_.pic_init_qp();
@@ -680,6 +687,9 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
     stats_.sse_masked = hdr.sse_masked;
     stats_.masked_pixels = masked_pixels_;
+    stats_.deblocked = (int)hdr.deblocked;
+    stats_.db_coherent = (int)hdr.db_coherent;
+    stats_.db_changed = (int)hdr.db_changed;
     common_.end_frame((int)au_.size(), sl.idr);
     return au_;
 }

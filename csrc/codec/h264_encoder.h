@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "h264_core.h"
+#include "h264_deblock.h"
 #include "h264_gpu.h"
 #include "video_encoder.h"
 
@@ -51,14 +52,16 @@ struct EncoderConfig {
                               // +0.6 dB (H.264) / +1.4 dB (HEVC) masked Y-PSNR at equal rate, motion content
                               // unchanged (profiles/r04_hevc/NOTES.md).  HEVC has 0, 1 and 3+, and treats 2
                               // as 1
-    // in-loop deblocking filter: 1 on, 0 off, -1 the codec's default -- HEVC on (8.7.2, fully
-    // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it cost
-    // 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)
+    // in-loop deblocking filter: 1 on, 0 off, 2 adaptive (H.264: per picture from its temporal
+    // classes, h264_deblock.h db_auto_decide; HEVC: on), -1 the codec's default -- HEVC on (8.7.2,
+    // fully parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it
+    // cost 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)
     int deblock = -1;
     // P pictures: also search 16x8 / 8x16 partitionings (two vectors per macroblock) and take one
     // when its SAD + lambda * vector rate beats the 16x16 vector's
     int partitions = 1;
-    bool h264_deblock() const { return deblock > 0; }
+    bool h264_deblock() const { return deblock > 0; }  // the filter kernels run (on, or adaptive)
+    bool h264_deblock_auto() const { return deblock == 2; }
     bool hevc_deblock() const { return deblock != 0; }
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: it costs -35 % fps on the 1080p desktop (k_intra_analyze + k_intra_p on
@@ -99,6 +102,8 @@ struct FrameStats {
     uint64_t sse[3] = {0, 0, 0};  // source vs reconstruction (Y, U, V), display area
     uint64_t sse_masked = 0;      // Y outside the mask macroblocks (EncoderConfig::mask_*)
     int64_t masked_pixels = 0;    // display luma samples outside them (the PSNR denominator)
+    int deblocked = 0;            // H.264: the in-loop filter ran on this picture (idc 0)
+    int db_coherent = 0, db_changed = 0;  // adaptive filter: the picture's class counts (db_auto_count)
 };
 
 // Annex-B / rate-control logic shared by both encoders.
@@ -325,6 +330,7 @@ class GpuH264Encoder final : public VideoEncoder {
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
     uint32_t db_epoch_ = 0;
+    uint32_t* db_auto_ = nullptr;  // adaptive filter state (DeviceBuffers::db_auto), shared by the slots
     int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
     int64_t masked_pixels_ = 0;
     std::vector<uint8_t> au_;
@@ -351,6 +357,10 @@ class CpuH264Encoder {
     void encode_inter(const uint8_t* y, const uint8_t* uv, int pitch);
     void entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& slice_off, std::vector<uint32_t>& slice_len);
     int frame_qp_() const { return qp_override_ >= 0 ? qp_override_ : common_.cur_qp(); }
+    // the picture's in-loop filter decision (EncoderConfig::deblock; adaptive: db_auto_decide, as k_db_prep)
+    void decide_deblock();
+    bool deblock_now_ = false, db_prev_on_ = false;
+    DbAutoCounts db_counts_;
     int qp_override_ = -1;  // rate-control probe of the first picture
 
     EncoderConfig cfg_;

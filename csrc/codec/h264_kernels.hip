@@ -2381,6 +2381,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const Fra
             hdr->total_bytes = over_b ? 0 : total_bytes;
             hdr->num_slices = ns;
             hdr->overflow = (otot ? 1u : 0u) | (over_b ? 2u : 0u);
+            hdr->deblocked = fs->deblock_off ? 0u : 1u;
+            hdr->db_coherent = (uint32_t)fs->db_coherent;
+            hdr->db_changed = (uint32_t)fs->db_changed;
         }
     }
     // this row's units

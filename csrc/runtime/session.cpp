@@ -502,6 +502,7 @@ FrameResult Session::collect() {
     const h264::FrameStats& st = enc_->last_stats();
     r.idr = st.idr;
     r.qp = st.qp;
+    r.deblocked = st.deblocked;
     if (devclk_) {  // device clock: first kernel of the frame (render / conversion) -> end of its pack kernel
         const uint64_t t0 = ts_[fl.slot], t1 = enc_->last_t_end();
         r.gpu_ms = t1 > t0 ? (double)(t1 - t0) / clock_khz_ : 0.0;

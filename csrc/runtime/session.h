@@ -82,6 +82,7 @@ struct FrameResult {
     int qp = 0;
     double psnr_y = 0, psnr_u = 0, psnr_v = 0;  // encoder reconstruction vs source (dB, cap 99)
     double psnr_y_masked = 0;                   // luma PSNR outside SessionConfig::mask_* (0 = off)
+    int deblocked = 0;                          // H.264: the in-loop filter ran on this picture
     std::vector<uint8_t> au;
 };
 

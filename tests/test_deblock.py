@@ -98,3 +98,54 @@ def test_decoder_reference_cache_survives_forced_idr(native):
         frames.append((y, uv, t == 5))
     stream, recons = _encode(native, frames, 320, 96, bitrate_kbps=0, search_range=4, subpel=0, deblock=0)
     _check(stream, recons)
+
+
+def _pan_frames(w, h, n, step=3, still=False):
+    """A textured scene panning `step` px per frame (coherent motion), or standing still with a
+    small changing patch (`still`): the two temporal classes of the adaptive filter."""
+    rng = np.random.default_rng(7)
+    big = rng.integers(0, 256, (h // 8 + 2, (w + n * step) // 8 + 2)).astype(np.float64)
+    big = np.kron(big, np.ones((8, 8)))  # 8x8 blocks of flat texture: block edges to filter
+    yy, xx = np.mgrid[0:big.shape[0], 0:big.shape[1]]
+    big = (0.6 * big + 40 * np.sin(xx / 5.0) + 30 * np.cos(yy / 4.0) + 20).clip(0, 255)
+    frames = []
+    for t in range(n):
+        off = 0 if still else t * step
+        y = big[:h, off:off + w].astype(np.uint8).copy()
+        if still:
+            y[8:24, 8:40] = (t * 37) % 256  # a changing "text" patch, zero motion
+        uv = np.full((h // 2, w), 128, np.uint8)
+        uv[:, 0::2] = (128 + 0.2 * (y[::2, ::2].astype(int) - 128)).astype(np.uint8)
+        frames.append((y, uv))
+    return frames
+
+
+def test_adaptive_filter_follows_motion_and_decodes(native):
+    """deblock=2: P pictures of a pan are filtered (coherent vectors cover the picture), a forced
+    IDR keeps the decision, a still scene stays unfiltered; per-picture idc decodes exactly."""
+    w, h = 192, 96
+    pan = [(y, uv, t == 4) for t, (y, uv) in enumerate(_pan_frames(w, h, 6))]
+    cfg = native.EncoderConfig()
+    cfg.width, cfg.height = w, h
+    cfg.bitrate_kbps, cfg.qp, cfg.search_range, cfg.deblock = 0, 34, 8, 2
+    enc = native.CpuH264Encoder(cfg)
+    stream, recons, flags = b"", [], []
+    for y, uv, idr in pan:
+        stream += enc.encode(y, uv, idr)
+        ry, ruv = enc.recon()
+        recons.append((ry.copy(), ruv.copy()))
+        flags.append((enc.stats.deblocked, enc.stats.db_coherent))
+    assert flags[0][0] == 0  # the first IDR: nothing decided yet (off)
+    assert all(d == 1 for d, _ in flags[1:]), flags  # the pan's P pictures, and the forced IDR at 4
+    assert all(c * 8 >= (w // 16) * (h // 16) for _, c in flags[1:4]), flags
+    _check(stream, recons)
+
+    still = [(y, uv, False) for y, uv in _pan_frames(w, h, 5, still=True)]
+    stream, recons = b"", []
+    enc = native.CpuH264Encoder(cfg)
+    for y, uv, idr in still:
+        stream += enc.encode(y, uv, idr)
+        assert enc.stats.deblocked == 0 and enc.stats.db_coherent * 8 < (w // 16) * (h // 16)
+        ry, ruv = enc.recon()
+        recons.append((ry.copy(), ruv.copy()))
+    _check(stream, recons)

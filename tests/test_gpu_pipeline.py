@@ -587,3 +587,35 @@ def test_device_clock_frame_times(gpu, depth):
     for _ in range(3):
         r = s.step(False)
         assert 0.0 < s.stats.encode_ms <= r.gpu_ms + 1e-6
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
+    """deblock=2: k_db_prep's per-picture decision (last-workgroup vote over the class counts)
+    equals the CPU encoder's, so the streams match bit for bit through a pan, a forced IDR and a
+    still stretch, with frames in flight (depth 3: the decision state is shared by the slots)."""
+    from .test_deblock import _pan_frames
+
+    w, h = 192, 96
+    frames = [(y, uv, t == 4) for t, (y, uv) in enumerate(_pan_frames(w, h, 6))]
+    frames += [(y, uv, False) for y, uv in _pan_frames(w, h, 5, still=True)]
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height = w, h
+    cfg.bitrate_kbps, cfg.qp, cfg.search_range, cfg.deblock = 0, 34, 8, 2
+    cfg.pipeline_depth = depth
+    genc = gpu.GpuH264Encoder(cfg, _stream())
+    cenc = gpu.CpuH264Encoder(cfg)
+    ch = genc.coded_height
+    flags = []
+    for t, (y, uv, idr) in enumerate(frames):
+        dy = pitched(y, genc.pitch, ch)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
+        torch.cuda.synchronize()
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), idr)
+        cau = cenc.encode(y, uv, idr)
+        assert gau == cau, f"frame {t}: GPU bitstream differs from CPU encoder"
+        assert (genc.stats.deblocked, genc.stats.db_coherent, genc.stats.db_changed) == \
+            (cenc.stats.deblocked, cenc.stats.db_coherent, cenc.stats.db_changed), t
+        assert np.array_equal(genc.recon()[0], cenc.recon()[0]), t
+        flags.append(genc.stats.deblocked)
+    assert flags[1:5] == [1, 1, 1, 1] and flags[-1] == 0, flags
