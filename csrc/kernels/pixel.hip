@@ -641,6 +641,28 @@ __device__ __forceinline__ void mf_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
+// Quads crossing the left / right image edge, after their block's DMA landed: the DMA read the
+// clamped quad (pixels p0 .. p0 + 3, p0 = clamp(sx, 0, in_w - 4)), which holds every pixel the
+// quad's clamped positions clamp(sx + k, 0, in_w - 1) name -- so the fix-up is a shuffle of the
+// lane's own LDS quad (no global load, whose wait would also drain the DMA in flight).  The
+// caller brackets it with barriers.
+__device__ __forceinline__ void mf_fix_edges(char* buf, int rows, int nq, int xlo, int in_w, int wave, int lane) {
+    const int sx = xlo + 4 * lane;
+    if (lane >= nq || (sx >= 0 && sx + 4 <= in_w)) return;
+    const int p0 = min(max(sx, 0), in_w - 4);
+    int idx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) idx[k] = min(max(sx + k, 0), in_w - 1) - p0;
+    for (int r = wave; r < rows; r += 2) {
+        uint4* q = reinterpret_cast<uint4*>(buf + ((size_t)r * nq + lane) * 16);
+        const uint4 v = *q;
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = idx[k] == 0 ? v.x : idx[k] == 1 ? v.y : idx[k] == 2 ? v.z : v.w;
+        *q = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 // The block pipeline of one workgroup.  Blocks alternate between buf0 and buf1; blocks 0 and
 // 1 are posted up front and block b + 2 as soon as every wave is done with block b, so two
 // blocks' LDS-DMA are in flight at the start and one while each block's products run.  buf0 / buf1 are
@@ -671,19 +693,8 @@ __device__ __forceinline__ void mf_main(char* __restrict__ buf0, char* __restric
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         mf_barrier();
         if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
-            const int rows = min(32, nr - 32 * b);
-            for (int r = wave; r < rows; r += 2) {
-                const int sx = xlo + 4 * lane;
-                if (lane >= nq || (sx >= 0 && sx + 4 <= in_w)) continue;
-                const uint8_t* row = in + (size_t)min(max(ylo + 32 * b + r, 0), in_h - 1) * in_pitch;
-                uint4 px;
-                px.x = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx, 0), in_w - 1) * 4);
-                px.y = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 1, 0), in_w - 1) * 4);
-                px.z = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 2, 0), in_w - 1) * 4);
-                px.w = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx + 3, 0), in_w - 1) * 4);
-                *reinterpret_cast<uint4*>(cur + ((size_t)r * nq + lane) * 16) = px;
-            }
-            __syncthreads();
+            mf_fix_edges(cur, min(32, nr - 32 * b), nq, xlo, in_w, wave, lane);
+            mf_barrier();
         }
         const uint32_t* rp =
             reinterpret_cast<const uint32_t*>(cur) + min(l32, nr - 1 - 32 * b) * lds_cols + kb + 8 * h;
@@ -801,6 +812,112 @@ __device__ __forceinline__ void mf_epilogue(const mf_f16* Y, int g0, int wave, i
 
 
 // ---------------------------------------------------------------- MFMA scaler, strip form
+// The block loop of k_scale_strip over a ring of three LDS buffers, unrolled by three so every
+// access names its buffer through its own __restrict__ parameter: the compiler then sees a ds_read
+// of the block being computed as independent of the LDS-DMA into the other two and waits only for
+// its own block (a ring slot picked by a run-time index made it wait vmcnt(0) before every LDS
+// read, draining the DMA in flight: 72 us for 4K -> 1080p instead of the pipelined time).
+__device__ __forceinline__ void strip_main(char* __restrict__ r0, char* __restrict__ r1, char* __restrict__ r2,
+                                           const uint4* __restrict__ fvl, const uint8_t* __restrict__ in,
+                                           int in_pitch, int in_w, int in_h, int base, int nb, int nq, int lds_cols,
+                                           uint32_t loff, int kb, int nks, int xlo, bool edge, int v0, int v1,
+                                           const int* ti, const mf_h8* bh, float bias, int g0, int wave, int lane,
+                                           uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp, int out_pitch,
+                                           int coded_w, int coded_h) {
+    const int h = lane >> 5, l32 = lane & 31;
+    auto tinfo = [&](int v) {
+        const int k = v - v0;
+        return k == 0 ? ti[0] : k == 1 ? ti[1] : k == 2 ? ti[2] : ti[3];
+    };
+    mf_stage(in, in_pitch, in_h, base, 0, 32 * nb, nq, loff, r0, wave, lane);
+    if (nb > 1) mf_stage(in, in_pitch, in_h, base, 32, 32 * nb, nq, loff, r1, wave, lane);
+    constexpr uint32_t kSel[3] = {0x0c040c00u, 0x0c050c01u, 0x0c060c02u};  // B, G, R
+    mf_f16 Y0[3], Y1[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Y0[c] = Y1[c] = (mf_f16){};
+    int vt = v0;  // the oldest tile not stored yet (Y0); vt + 1 accumulates in Y1
+    // block i computed from `cur`; block i + 2 posted into `nx` (the slot block i - 1 used)
+    auto step = [&](char* __restrict__ cur, char* __restrict__ nx, int i) {
+        if (i > 0) mf_barrier();  // every wave is done with block i - 1, whose slot is refilled now
+        if (i + 2 < nb) mf_stage(in, in_pitch, in_h, base, 32 * (i + 2), 32 * nb, nq, loff, nx, wave, lane);
+        // this wave's DMA of block i retired (the blocks posted after it, 16 row loads each, and
+        // an epilogue's stores may stay in flight), then every wave's: the barrier
+        const int ahead = min(i + 2, nb - 1) - i;
+        if (ahead >= 2)
+            __builtin_amdgcn_s_waitcnt(0x8F70);  // vmcnt(32)
+        else if (ahead == 1)
+            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        mf_barrier();
+        if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
+            mf_fix_edges(cur, 32, nq, xlo, in_w, wave, lane);
+            mf_barrier();
+        }
+        // the tiles block i feeds: vt and / or vt + 1 (wave-uniform)
+        const int i0 = tinfo(vt), b0 = i0 & 255, n0 = i0 >> 8;
+        const bool use0 = i >= b0 && i < b0 + n0;
+        bool use1 = false;
+        int b1 = 0;
+        if (vt + 1 < v1) {
+            const int i1 = tinfo(vt + 1);
+            b1 = i1 & 255;
+            use1 = i >= b1 && i < b1 + (i1 >> 8);
+        }
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(cur) + l32 * lds_cols + kb + 8 * h;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            mf_f16 X = {};
+#pragma unroll
+            for (int s = 0; s < kMfKs; ++s) {
+                if (s > 0 && s >= nks) break;
+                const uint4 p0 = *reinterpret_cast<const uint4*>(rp + 16 * s);
+                const uint4 p1 = *reinterpret_cast<const uint4*>(rp + 16 * s + 4);
+                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(mf_chan(p0, p1, kSel[c]), bh[s], X, 0, 0, 0);
+            }
+            mf_h8 x0, x1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                x0[j] = (_Float16)(X[j] - bias);
+                x1[j] = (_Float16)(X[8 + j] - bias);
+            }
+            if (use0) {
+                const uint4* f = fvl + ((size_t)(vt - v0) * kMfRb + (i - b0)) * 128 + lane;
+                Y0[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[0]), x0, Y0[c], 0, 0, 0);
+                Y0[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[64]), x1, Y0[c], 0, 0, 0);
+            }
+            if (use1) {
+                const uint4* f = fvl + ((size_t)(vt + 1 - v0) * kMfRb + (i - b1)) * 128 + lane;
+                Y1[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[0]), x0, Y1[c], 0, 0, 0);
+                Y1[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[64]), x1, Y1[c], 0, 0, 0);
+            }
+        }
+        // tile vt complete -- and then possibly vt + 1 too, when its last block is this one as well
+        // (a short last tile, or an upscale: both tiles' footprints end in block i)
+#pragma unroll 1
+        for (int k = 0; k < 2 && vt < v1; ++k) {
+            const int ik = tinfo(vt);
+            if (i != (ik & 255) + (ik >> 8) - 1) break;
+            mf_epilogue(Y0, g0, wave, vt, lane, yp, uvp, out_pitch, coded_w, coded_h);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                Y0[c] = Y1[c];
+                Y1[c] = (mf_f16){};
+            }
+            ++vt;
+        }
+    };
+#pragma unroll 1
+    for (int i = 0; i < nb; i += 3) {
+        step(r0, r2, i);
+        if (i + 1 >= nb) break;
+        step(r1, r0, i + 1);
+        if (i + 2 >= nb) break;
+        step(r2, r1, i + 2);
+    }
+}
+
+
 // One workgroup (2 waves, 64 output columns) per column strip of up to kStripMaxT consecutive
 // 32-row output tiles.  The strip's input rows are staged in 32-row blocks counted from its first
 // tap row through an LDS ring of kStripRing blocks: the DMA of the next two blocks is in flight
@@ -830,7 +947,16 @@ __global__ __launch_bounds__(128) void k_scale_strip(const uint8_t* __restrict__
     const int g0 = 2 * sx, gw = min(g0 + wave, m.ngx - 1);
     const int v0 = sy * T, v1 = min(v0 + T, m.ngy), nt = v1 - v0;
     const int base = m.gy2[3 * v0];
-    const int lastinfo = m.gy2[3 * (v1 - 1) + 1];
+    // the tiles' block ranges, held in scalar registers: a global load inside the block loop would
+    // wait vmcnt(0) and so drain the ring's DMA in flight
+    int ti[kStripMaxT];
+#pragma unroll
+    for (int k = 0; k < kStripMaxT; ++k) ti[k] = __builtin_amdgcn_readfirstlane(v0 + k < v1 ? m.gy2[3 * (v0 + k) + 1] : 0);
+    auto tinfo = [&](int v) {
+        const int k = v - v0;
+        return k == 0 ? ti[0] : k == 1 ? ti[1] : k == 2 ? ti[2] : ti[3];
+    };
+    const int lastinfo = tinfo(v1 - 1);
     const int nb = (lastinfo & 255) + (lastinfo >> 8);  // blocks of the strip
     const int xlo = m.gx[2 * g0];
     const int nq = m.lds_cols >> 2;
@@ -850,94 +976,8 @@ __global__ __launch_bounds__(128) void k_scale_strip(const uint8_t* __restrict__
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
     const bool edge = xlo < 0 || xlo + 4 * nq > in_w;  // workgroup-uniform
-    for (int i = 0; i < kStripRing - 1 && i < nb; ++i)
-        mf_stage(in, in_pitch, in_h, base, 32 * i, 32 * nb, nq, loff, smem + (size_t)(i % kStripRing) * buf_bytes, wave,
-                 lane);
-    constexpr uint32_t kSel[3] = {0x0c040c00u, 0x0c050c01u, 0x0c060c02u};  // B, G, R
-    mf_f16 Y0[3], Y1[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) Y0[c] = Y1[c] = (mf_f16){};
-    int vt = v0;  // the oldest tile not stored yet (Y0); vt + 1 accumulates in Y1
-#pragma unroll 1
-    for (int i = 0; i < nb; ++i) {
-        if (i > 0) mf_barrier();  // every wave is done with block i - 1, whose slot is refilled now
-        const int nxt = i + kStripRing - 1;
-        if (nxt < nb)
-            mf_stage(in, in_pitch, in_h, base, 32 * nxt, 32 * nb, nq, loff,
-                     smem + (size_t)(nxt % kStripRing) * buf_bytes, wave, lane);
-        // this wave's DMA of block i retired: the blocks issued after it (16 row loads each) may stay in flight
-        const int ahead = min(nxt, nb - 1) - i;
-        if (ahead >= 2)
-            __builtin_amdgcn_s_waitcnt(0x8F70);  // vmcnt(32)
-        else if (ahead == 1)
-            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
-        else
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        mf_barrier();
-        char* cur = smem + (size_t)(i % kStripRing) * buf_bytes;
-        if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
-            for (int r = wave; r < 32; r += 2) {
-                const int sx4 = xlo + 4 * lane;
-                if (lane >= nq || (sx4 >= 0 && sx4 + 4 <= in_w)) continue;
-                const uint8_t* row = in + (size_t)min(max(base + 32 * i + r, 0), in_h - 1) * in_pitch;
-                uint4 px;
-                px.x = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4, 0), in_w - 1) * 4);
-                px.y = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4 + 1, 0), in_w - 1) * 4);
-                px.z = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4 + 2, 0), in_w - 1) * 4);
-                px.w = *reinterpret_cast<const uint32_t*>(row + (size_t)min(max(sx4 + 3, 0), in_w - 1) * 4);
-                *reinterpret_cast<uint4*>(cur + ((size_t)r * nq + lane) * 16) = px;
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // (these loads are the only ones left in flight)
-            __syncthreads();
-        }
-        // the tiles block i feeds: vt and / or vt + 1 (wave-uniform)
-        const int i0 = m.gy2[3 * vt + 1], b0 = i0 & 255, n0 = i0 >> 8;
-        const bool use0 = i >= b0 && i < b0 + n0;
-        bool use1 = false;
-        int b1 = 0;
-        if (vt + 1 < v1) {
-            const int i1 = m.gy2[3 * (vt + 1) + 1];
-            b1 = i1 & 255;
-            use1 = i >= b1 && i < b1 + (i1 >> 8);
-        }
-        const uint32_t* rp = reinterpret_cast<const uint32_t*>(cur) + l32 * m.lds_cols + kb + 8 * h;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            mf_f16 X = {};
-#pragma unroll
-            for (int s = 0; s < kMfKs; ++s) {
-                if (s > 0 && s >= nks) break;
-                const uint4 p0 = *reinterpret_cast<const uint4*>(rp + 16 * s);
-                const uint4 p1 = *reinterpret_cast<const uint4*>(rp + 16 * s + 4);
-                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(mf_chan(p0, p1, kSel[c]), bh[s], X, 0, 0, 0);
-            }
-            mf_h8 x0, x1;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                x0[j] = (_Float16)(X[j] - bias);
-                x1[j] = (_Float16)(X[8 + j] - bias);
-            }
-            if (use0) {
-                const uint4* f = fvl + ((size_t)(vt - v0) * kMfRb + (i - b0)) * 128 + lane;
-                Y0[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[0]), x0, Y0[c], 0, 0, 0);
-                Y0[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[64]), x1, Y0[c], 0, 0, 0);
-            }
-            if (use1) {
-                const uint4* f = fvl + ((size_t)(vt + 1 - v0) * kMfRb + (i - b1)) * 128 + lane;
-                Y1[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[0]), x0, Y1[c], 0, 0, 0);
-                Y1[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(mf_h8, f[64]), x1, Y1[c], 0, 0, 0);
-            }
-        }
-        if (use0 && i == b0 + n0 - 1) {  // tile vt is complete
-            mf_epilogue(Y0, g0, wave, vt, lane, yp, uvp, out_pitch, coded_w, coded_h);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                Y0[c] = Y1[c];
-                Y1[c] = (mf_f16){};
-            }
-            ++vt;
-        }
-    }
+    strip_main(smem, smem + buf_bytes, smem + 2 * buf_bytes, fvl, in, in_pitch, in_w, in_h, base, nb, nq, m.lds_cols,
+               loff, kb, nks, xlo, edge, v0, v1, ti, bh, bias, g0, wave, lane, yp, uvp, out_pitch, coded_w, coded_h);
 }
 
 __global__ __launch_bounds__(256) void k_composite(const uint8_t* __restrict__ tile, int tile_pitch, int tw, int th,
