@@ -600,7 +600,7 @@ PYBIND11_MODULE(_native, m) {
                 if (!pix::build_scale_frags(in_w, in_h, out_w, out_h, cw, ch, hx0, hwx, taps_x, hy0, hwy, taps_y, fr))
                     throw std::invalid_argument("scale_to_nv12: scale factor outside the MFMA kernel's range");
                 pix::upload_scale_frags(fr, &frags, t.mf);
-                if (!strip) t.mf.strip = 0;  // the one-tile-per-workgroup MFMA kernel
+                t.mf.force_strip = strip;  // else the one-tile-per-workgroup MFMA kernel
             }
             pix::launch_scale_to_nv12(as_ptr<const uint8_t>(in), in_pitch, in_w, in_h, t, as_ptr<uint8_t>(y),
                                       as_ptr<uint8_t>(uv), out_pitch, cw, ch, as_stream(stream));
@@ -613,7 +613,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("in_ptr"), py::arg("in_pitch"), py::arg("in_w"), py::arg("in_h"), py::arg("out_w"), py::arg("out_h"),
         py::arg("x0_ptr"), py::arg("wx_ptr"), py::arg("taps_x"), py::arg("y0_ptr"), py::arg("wy_ptr"),
         py::arg("taps_y"), py::arg("y_ptr"), py::arg("uv_ptr"), py::arg("out_pitch"), py::arg("coded_w"),
-        py::arg("coded_h"), py::arg("stream") = 0, py::arg("mfma") = false, py::arg("strip") = true);
+        py::arg("coded_h"), py::arg("stream") = 0, py::arg("mfma") = false, py::arg("strip") = false);
     m.def(
         "composite",
         [](uintptr_t tile, int tile_pitch, int tw, int th, uintptr_t dst, int dst_pitch, int dx, int dy,

@@ -273,7 +273,8 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
     auto issue = [&](int xb) {
 #pragma unroll
         for (int j = 0; j < kDbPf; ++j)
-            pf[j] = (act && xb + j < mb_w) ? gld16(line + 16 * (xb + j)) : make_uint4(0, 0, 0, 0);
+            pf[j] = gld16(line + 16 * min(xb + j, mb_w - 1));  // unconditional: a select on the
+                                                               // loaded value would wait for it here
     };
     issue(0);
     for (int x = 0; x <= mb_w; ++x) {
@@ -294,13 +295,16 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
         const int qp = qrun;
         // ---- vertical edges of MB x (lines); edge 0 also finishes MB x-1's columns 13..15
         bool vmod = false, v0 = false;
+        // the MB's filter parameters: its own QP (internal edges, and the horizontal ones) and the
+        // left edge's average -- both fetched before the edges, one LDS round trip
+        const DbParams dq = lds_params(S, qp), dl = lds_params(S, (qprev + qp + 1) >> 1);
         if (have) {
             for (int e = 0; e < 4; ++e) {
                 const uint32_t b4 = rec_edge(r, 0, e);
                 if (!b4) continue;
                 vmod = true;
                 const int bs = (b4 >> (3 * (lane >> 2))) & 7;
-                const DbParams d = lds_params(S, ((e == 0 ? qprev : qp) + qp + 1) >> 1);
+                const DbParams d = e == 0 ? dl : dq;
                 if (e == 0) {
                     v0 = true;
                     if (act) db_luma_line(P[12], P[13], P[14], P[15], C[0], C[1], C[2], C[3], bs, d);
@@ -377,9 +381,14 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                     }
                     qtop = (int)__hip_atomic_load((const gu32*)(G.glq) + (size_t)(0 * g.mb_h + mby - 1) * mb_w + x, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    // retire the hand-off loads here: left pending, the compiler's wait at the
+                    // merge below (every row's H phase) would be a vmcnt(0) on all rows, draining
+                    // their line prefetch and stores every macroblock
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                 }
             }
             if (act) *reinterpret_cast<uint4*>(tile[4 + lane]) = pack16(C);
+            const DbParams dt = lds_params(S, (qtop + qp + 1) >> 1);
             lds_sync_wave();
             int col[20];
             if (act) {
@@ -390,7 +399,7 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                 const uint32_t b4 = rec_edge(r, 1, e);
                 if (!b4) continue;
                 const int bs = (b4 >> (3 * (lane >> 2))) & 7;
-                const DbParams d = lds_params(S, ((e == 0 ? qtop : qp) + qp + 1) >> 1);
+                const DbParams d = e == 0 ? dt : dq;
                 if (!act) continue;
                 if (e == 0)
                     db_luma_line(col[0], col[1], col[2], col[3], col[4], col[5], col[6], col[7], bs, d);
@@ -459,7 +468,8 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
     auto issue = [&](int xb) {
 #pragma unroll
         for (int j = 0; j < kDbPf; ++j)
-            pf[j] = (act && xb + j < mb_w) ? gld16(line + 16 * (xb + j)) : make_uint4(0, 0, 0, 0);
+            pf[j] = gld16(line + 16 * min(xb + j, mb_w - 1));  // unconditional: a select on the
+                                                               // loaded value would wait for it here
     };
     issue(0);
     for (int x = 0; x <= mb_w; ++x) {
@@ -479,14 +489,15 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
         if (have && (r.w >> 30) & 1) qrun = (r.w >> 24) & 63;
         const int qp = qrun;
         bool vmod = false, v0 = false;
+        const int cq = lds_cqp(S, qp, cqo), cqp = lds_cqp(S, qprev, cqo);
+        const DbParams dq = lds_params(S, cq), dl = lds_params(S, (cqp + cq + 1) >> 1);
         if (have) {
             for (int ce = 0; ce < 2; ++ce) {
                 const uint32_t b4 = rec_edge(r, 0, 2 * ce);
                 if (!b4) continue;
                 vmod = true;
                 const int bs = (b4 >> (3 * (ln >> 1))) & 7;
-                const DbParams d = lds_params(S, 
-                    (lds_cqp(S, ce == 0 ? qprev : qp, cqo) + lds_cqp(S, qp, cqo) + 1) >> 1);
+                const DbParams d = ce == 0 ? dl : dq;
                 if (ce == 0) {
                     v0 = true;
                     if (act) db_chroma_line(P[6], P[7], C[0], C[1], bs, d);
@@ -562,9 +573,14 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                     }
                     qtop = (int)__hip_atomic_load((const gu32*)(G.glq) + (size_t)(1 * g.mb_h + mby - 1) * mb_w + x, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    // retire the hand-off loads here: left pending, the compiler's wait at the
+                    // merge below (every row's H phase) would be a vmcnt(0) on all rows, draining
+                    // their line prefetch and stores every macroblock
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                 }
             }
             if (act) to_tile(2 + ln, C);
+            const DbParams dt = lds_params(S, (lds_cqp(S, qtop, cqo) + cq + 1) >> 1);
             lds_sync_wave();
             int col[10];
             if (act) {
@@ -575,8 +591,7 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                 const uint32_t b4 = rec_edge(r, 1, 2 * ce);
                 if (!b4) continue;
                 const int bs = (b4 >> (3 * (ln >> 1))) & 7;
-                const DbParams d = lds_params(S, 
-                    (lds_cqp(S, ce == 0 ? qtop : qp, cqo) + lds_cqp(S, qp, cqo) + 1) >> 1);
+                const DbParams d = ce == 0 ? dt : dq;
                 if (!act) continue;
                 if (ce == 0)
                     db_chroma_line(col[0], col[1], col[2], col[3], bs, d);

@@ -67,6 +67,7 @@ struct ScaleMfma {
     const int* gy2 = nullptr;   // [ngy][3]
     const void* fv2 = nullptr;  // [ngy][kMaxRb][2][64 lanes]
     int strip = 0;
+    bool force_strip = false;  // use the strip form (else only with MXDESK_SCALER=strip)
 };
 struct LanczosTables {
     int out_w, out_h, taps_x, taps_y;

@@ -12,8 +12,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 
 #include "pixel.h"
 #include "../common/hip_check.h"
@@ -1200,6 +1202,8 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
     std::vector<int> gy2(3 * (size_t)ngy, 0);
     std::vector<uint16_t> fv2((size_t)ngy * kMfRb * 2 * 64 * 8, 0);
     int strip = kStripMaxT;
+    if (const char* e = std::getenv("MXDESK_SCALER_STRIP"))  // experiments: cap the tiles per strip
+        strip = std::max(1, std::min(kStripMaxT, std::atoi(e)));
     for (; strip >= 1; --strip) {
         bool ok = (size_t)kStripRing * 32 * lds_cols * 4 + (size_t)strip * kMfRb * 128 * 16 <= 152 * 1024;
         for (int v = 0; v < ngy && ok; ++v) {
@@ -1284,11 +1288,14 @@ void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf) {
 
 void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h, const LanczosTables& t, uint8_t* y,
                           uint8_t* uv, int out_pitch, int coded_w, int coded_h, hipStream_t stream, uint64_t* ts) {
-    static const bool legacy = [] {
+    // the strip form runs only on request (MXDESK_SCALER=strip, or the binding's strip=True): with
+    // one 2-wave workgroup per CU it leaves half the SIMDs idle and measured 80 us against the tile
+    // kernel's 26 us for 4K -> 1080p (profiles/r05_scale/NOTES.md)
+    static const bool want_strip = [] {
         const char* e = std::getenv("MXDESK_SCALER");
-        return e && std::string(e) == "tile";
+        return e && std::string(e) == "strip";
     }();
-    if (t.mf.gx && t.mf.strip > 0 && !legacy && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 &&
+    if (t.mf.gx && t.mf.strip > 0 && (want_strip || t.mf.force_strip) && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 &&
         in_w >= 4) {
         const size_t lds = (size_t)kStripRing * 32 * t.mf.lds_cols * 4 + (size_t)t.mf.strip * kMfRb * 128 * 16;
         ensure_func_attr(reinterpret_cast<const void*>(&k_scale_strip), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -12,6 +12,8 @@
 #   prof:NAME[:ARGS]    rocprofv3 --kernel-trace --stats around bench.py ARGS -> OUT/prof_NAME/
 #   pmc:NAME:CTRS[:ARGS] rocprofv3 --pmc CTRS (comma list) around bench.py ARGS -> OUT/pmc_NAME/
 #   py:NAME:SCRIPT[:ARGS] python SCRIPT ARGS -> OUT/NAME.log
+#   pyprof:NAME:SCRIPT[:ARGS] the same under rocprofv3 --kernel-trace --stats -> OUT/prof_NAME/
+#   pypmc:NAME:CTRS:SCRIPT[:ARGS] the same under rocprofv3 --pmc CTRS -> OUT/pmc_NAME/
 #   env:VAR=VALUE       export VAR=VALUE for the following steps (env:VAR= unsets it)
 set -o pipefail
 export TMPDIR=/tmp
@@ -56,6 +58,22 @@ for step in "$@"; do
             # shellcheck disable=SC2046
             timeout -s KILL 120 rocprofv3 --pmc $(args_of "$ctrs") --output-format csv -d "$OUT/pmc_$name" -o run \
                 -- python3 bench.py $(args_of "$bargs") > "$OUT/pmc_$name.log" 2>&1 || fail "pmc $name rc=$?" ;;
+        pyprof)
+            script=${extra%%:*}
+            pargs=""
+            [ "$extra" != "$script" ] && pargs=${extra#*:}
+            # shellcheck disable=SC2046
+            timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run \
+                -- python3 -u "$script" $(args_of "$pargs") > "$OUT/prof_$name.log" 2>&1 || fail "pyprof $name rc=$?" ;;
+        pypmc)
+            ctrs=${extra%%:*}
+            rest2=${extra#*:}
+            script=${rest2%%:*}
+            pargs=""
+            [ "$rest2" != "$script" ] && pargs=${rest2#*:}
+            # shellcheck disable=SC2046
+            timeout -s KILL 120 rocprofv3 --pmc $(args_of "$ctrs") --output-format csv -d "$OUT/pmc_$name" -o run \
+                -- python3 -u "$script" $(args_of "$pargs") > "$OUT/pmc_$name.log" 2>&1 || fail "pypmc $name rc=$?" ;;
         py)
             script=${extra%%:*}
             pargs=""
