@@ -180,7 +180,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("masked_pixels", &h264::FrameStats::masked_pixels)
         .def_readonly("deblocked", &h264::FrameStats::deblocked)
         .def_readonly("db_coherent", &h264::FrameStats::db_coherent)
-        .def_readonly("db_changed", &h264::FrameStats::db_changed);
+        .def_readonly("db_changed", &h264::FrameStats::db_changed)
+        .def_readonly("db_moving", &h264::FrameStats::db_moving);
 
     py::class_<h264::CpuH264Encoder>(m, "CpuH264Encoder")
         .def(py::init<const h264::EncoderConfig&>())

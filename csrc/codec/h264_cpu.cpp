@@ -589,15 +589,15 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
 }
 
 void CpuH264Encoder::decide_deblock() {
+    deblock_now_ = cfg_.deblock == 1 || (cfg_.h264_deblock_auto() && db_prev_on_);
+}
+
+void CpuH264Encoder::update_deblock_decision() {
     db_counts_ = DbAutoCounts{};
-    deblock_now_ = cfg_.h264_deblock();
-    if (!cfg_.h264_deblock_auto()) return;
-    if (!common_.cur_idr()) {  // an IDR picture keeps the last P decision
-        const Geometry g = geom_of(common_, cw_, ch_);
-        for (int i = 0; i < g.mb_w * g.mb_h; ++i) db_auto_count(mb_.data(), g.mb_w, i, db_counts_);
-        db_prev_on_ = db_auto_decide(db_counts_, g.mb_w * g.mb_h, db_prev_on_);
-    }
-    deblock_now_ = db_prev_on_;
+    if (common_.cur_idr()) return;  // an IDR picture keeps the last P decision
+    const Geometry g = geom_of(common_, cw_, ch_);
+    for (int i = 0; i < g.mb_w * g.mb_h; ++i) db_auto_count(mb_.data(), g.mb_w, i, db_counts_);
+    if (cfg_.h264_deblock_auto()) db_prev_on_ = db_auto_decide(db_counts_, g.mb_w * g.mb_h, db_prev_on_);
 }
 
 void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& soff, std::vector<uint32_t>& slen) {
@@ -690,6 +690,7 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
         deblock_picture_cpu(g, mb_.data(), qpe.data(), cfg_.chroma_qp_offset, rec_y_[cur_].data(), rec_uv_[cur_].data(),
                             cw_);
     }
+    update_deblock_decision();
     au_.clear();
     if (common_.cur_idr()) common_.write_parameter_sets(au_);
     int skipped = 0;
@@ -704,6 +705,7 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     stats_.deblocked = deblock_now_ ? 1 : 0;
     stats_.db_coherent = (int)db_counts_.coherent;
     stats_.db_changed = (int)db_counts_.changed;
+    stats_.db_moving = (int)db_counts_.moving;
     common_.end_frame((int)au_.size(), common_.cur_idr());
     have_ref_ = true;
     return au_;

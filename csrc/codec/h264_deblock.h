@@ -141,14 +141,19 @@ MXHD void db_chroma_line(int p1, int& p0, int& q0, int q1, int bs, const DbParam
 // compensation of a pan or a video leaves block edges the filter smooths: +1.3 dB on the motion
 // bench, profiles/r04_toolset/NOTES.md) and costs on a still desktop (it softens text and window
 // edges the encoder codes exactly: -1.1 dB).  The class is taken from the coded macroblocks:
-//  * coherent: an inter MB with a nonzero vector equal to its left or upper neighbour's (a pan, a
-//    scroll, a moving video -- not the random vectors of noise);
-//  * changed: an intra MB, or an inter MB with residual and a zero vector (text updates, cursor).
-// A P picture is filtered when coherent motion covers 1/8 of it (1/32 while the previous decision
-// was on: hysteresis, so a slowing pan does not toggle the filter every frame); an IDR picture
-// keeps the previous decision.  Same integer rule in k_db_prep and the CPU encoder.
+//  * moving: an inter MB with a nonzero vector;
+//  * coherent: a moving MB whose vector equals its left or upper neighbour's (a pan, a scroll, a
+//    moving video -- not the random vectors of noise);
+//  * changed: an intra MB, or an inter MB with residual and a zero vector (text updates, cursor;
+//    reported only).
+// A P picture is filtered when at least half of the moving MBs move coherently and they cover
+// 1/64 of the picture (flat areas of a pan keep a zero vector, so the moving share of a picture
+// varies with resolution; noise moves incoherently); while the previous decision was on, a third
+// and 1/128 keep it on (hysteresis: a slowing pan does not toggle the filter every frame).  An
+// IDR picture keeps the previous decision.  Same integer rule in k_db_prep, k_hevc_db_auto and the
+// CPU encoders.
 struct DbAutoCounts {
-    uint32_t coherent = 0, changed = 0;
+    uint32_t coherent = 0, changed = 0, moving = 0;
 };
 MXHD void db_auto_count(const MbInfo* mbs, int mb_w, int i, DbAutoCounts& c) {
     const MbInfo& m = mbs[i];
@@ -161,12 +166,23 @@ MXHD void db_auto_count(const MbInfo* mbs, int mb_w, int i, DbAutoCounts& c) {
         if (m.cbp) ++c.changed;
         return;
     }
+    ++c.moving;
     const int x = i % mb_w;
     auto same = [&](const MbInfo& n) { return !is_intra(n) && n.mvx == m.mvx && n.mvy == m.mvy; };
     if ((x > 0 && same(mbs[i - 1])) || (i >= mb_w && same(mbs[i - mb_w]))) ++c.coherent;
 }
+// The coherent count from motion vectors alone (HEVC: the 16x16 motion-search vectors of its
+// units; unit i's vector at mv[i * stride], mv[i * stride + 1]).
+MXHD void db_auto_count_mv(const int16_t* mv, int stride, int mb_w, int i, DbAutoCounts& c) {
+    const int x = mv[(size_t)i * stride], y = mv[(size_t)i * stride + 1];
+    if (x == 0 && y == 0) return;
+    ++c.moving;
+    auto same = [&](int j) { return mv[(size_t)j * stride] == x && mv[(size_t)j * stride + 1] == y; };
+    if ((i % mb_w > 0 && same(i - 1)) || (i >= mb_w && same(i - mb_w))) ++c.coherent;
+}
 MXHD bool db_auto_decide(const DbAutoCounts& c, int nmb, bool prev_on) {
-    return (uint64_t)c.coherent * (prev_on ? 32u : 8u) >= (uint64_t)nmb;
+    const uint64_t co = c.coherent;
+    return co * (prev_on ? 3u : 2u) >= (uint64_t)c.moving && co * (prev_on ? 128u : 64u) >= (uint64_t)nmb && co > 0;
 }
 
 // QP_Y of every macroblock as a decoder sees it: the MB's own QP where it carries mb_qp_delta,

@@ -52,14 +52,11 @@ __device__ __forceinline__ uint32_t rec_edge(const uint4& r, int dir, int e) {
     return (w >> (12 * (e & 1))) & 0xfffu;
 }
 
-__global__ __launch_bounds__(256) void k_db_prep(Geometry g, FrameState* __restrict__ fs,
+__global__ __launch_bounds__(256) void k_db_prep(Geometry g, const FrameState* __restrict__ fs,
                                                  const MbInfo* __restrict__ mbs, uint4* __restrict__ rec,
-                                                 int* __restrict__ row_lastq, uint32_t* __restrict__ db_auto) {
+                                                 int* __restrict__ row_lastq) {
     const int mby = blockIdx.x;
     __shared__ int best[4];
-    __shared__ uint32_t cnt[2][4];
-    const bool autod = fs->deblock_auto != 0, count = autod && !fs->idr;
-    DbAutoCounts ac;
     int last = -1;  // (mbx << 8) | qp of the last dqp-carrying MB this thread saw
     for (int mbx = threadIdx.x; mbx < g.mb_w; mbx += 256) {
         const int i = mby * g.mb_w + mbx;
@@ -80,7 +77,6 @@ __global__ __launch_bounds__(256) void k_db_prep(Geometry g, FrameState* __restr
         r.w = h[2] | (h[3] << 12) | ((uint32_t)(q.qp & 63) << 24) | (dq ? 1u << 30 : 0u);
         rec[i] = r;
         if (dq) last = (mbx << 8) | q.qp;
-        if (count) db_auto_count(mbs, g.mb_w, i, ac);
     }
     // row maximum of `last` (largest mbx wins)
     for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o, 64));
@@ -90,40 +86,6 @@ __global__ __launch_bounds__(256) void k_db_prep(Geometry g, FrameState* __restr
         const int b = max(max(best[0], best[1]), max(best[2], best[3]));
         row_lastq[mby] = b < 0 ? -1 : (b & 0xff);
     }
-    if (!autod) return;
-    // adaptive filter: the picture's class counts, and the last workgroup decides (db_auto_decide)
-    uint32_t co = ac.coherent, ch = ac.changed;
-    for (int o = 32; o > 0; o >>= 1) {
-        co += __shfl_xor(co, o, 64);
-        ch += __shfl_xor(ch, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        cnt[0][threadIdx.x >> 6] = co;
-        cnt[1][threadIdx.x >> 6] = ch;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    co = cnt[0][0] + cnt[0][1] + cnt[0][2] + cnt[0][3];
-    ch = cnt[1][0] + cnt[1][1] + cnt[1][2] + cnt[1][3];
-    if (co) atomicAdd(&db_auto[1], co);
-    if (ch) atomicAdd(&db_auto[2], ch);
-    __threadfence();  // the counts before the ticket
-    if (atomicAdd(&db_auto[3], 1u) != (uint32_t)g.mb_h - 1) return;
-    __threadfence();
-    DbAutoCounts tot;
-    tot.coherent = atomicAdd(&db_auto[1], 0u);
-    tot.changed = atomicAdd(&db_auto[2], 0u);
-    bool on = db_auto[0] != 0;
-    if (!fs->idr) {
-        on = db_auto_decide(tot, g.mb_w * g.mb_h, on);
-        db_auto[0] = on ? 1u : 0u;
-    }
-    fs->deblock_off = on ? 0 : 1;
-    fs->db_coherent = (int32_t)tot.coherent;
-    fs->db_changed = (int32_t)tot.changed;
-    db_auto[1] = 0;
-    db_auto[2] = 0;
-    db_auto[3] = 0;
 }
 
 struct DbShared {
@@ -626,7 +588,6 @@ __global__ __launch_bounds__(64 * kDbRows) void k_deblock(Geometry g, const Fram
     // one workgroup per (band, plane): 8 waves of 512 threads leave each wave 256 VGPRs for the
     // line registers and the prefetch batch
     __shared__ DbShared S;
-    if (fs->deblock_off) return;  // adaptive filter: k_db_prep switched this picture's filter off
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int band_row = wave, plane = blockIdx.y;
     if (threadIdx.x < 2 * kDbRows) {
@@ -658,7 +619,6 @@ __global__ __launch_bounds__(64 * kDbRows) void k_deblock(Geometry g, const Fram
 // quality mask (sse_part[c][row]; k_scan_rows takes mb_h partials when the filter is on).
 __global__ __launch_bounds__(256) void k_db_sse(Geometry g, const FrameState* __restrict__ fs,
                                                 const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv) {
-    if (fs->deblock_off) return;  // the analysis kernels' partials stand
     const int mby = blockIdx.x;
     unsigned long long sy = 0, su = 0, sv = 0, sm = 0;
     const int nchunk = g.mb_w * 16;  // 4-byte chunks in 16 rows of a MB row (luma)
@@ -708,7 +668,7 @@ __global__ __launch_bounds__(256) void k_db_sse(Geometry g, const FrameState* __
 void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream) {
     if (g.mb_w > kDbMaxW || g.mb_h > kMaxSlices) throw std::invalid_argument("launch_deblock: picture too large");
-    hipLaunchKernelGGL(k_db_prep, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, b.mb, b.db_rec, b.db_rowq, b.db_auto);
+    hipLaunchKernelGGL(k_db_prep, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, b.mb, b.db_rec, b.db_rowq);
     DbGlobal G{b.db_glb, b.db_glq, b.db_gprog, b.db_err};
     hipLaunchKernelGGL(k_deblock, dim3((g.mb_h + kDbRows - 1) / kDbRows, 2), dim3(64 * kDbRows), 0, stream, g, b.fs,
                        b.db_rec, b.db_rowq, G);

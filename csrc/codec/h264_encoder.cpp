@@ -272,7 +272,8 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMemsetAsync(b.db_gprog, 0, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h, stream_));
     HIP_CHECK(hipMalloc(&b.pack_done, sizeof(uint32_t)));
     HIP_CHECK(hipMemsetAsync(b.pack_done, 0, sizeof(uint32_t), stream_));
-    b.db_auto = db_auto_;
+    HIP_CHECK(hipMalloc(&b.db_cnt, sizeof(uint32_t) * 4));
+    HIP_CHECK(hipMemsetAsync(b.db_cnt, 0, sizeof(uint32_t) * 4, stream_));
     HIP_CHECK(hipHostMalloc(&b.db_err, sizeof(int), hipHostMallocMapped));
     *b.db_err = 0;
     HIP_CHECK(hipHostMalloc(&sl.fs_host, sizeof(FrameState), hipHostMallocDefault));
@@ -290,7 +291,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.row_agg,
                     (void*)b.row_sse, (void*)b.coded_info, (void*)b.slice_info,
                     (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit,
-                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.db_glq, (void*)b.db_gprog, (void*)b.pack_done})
+                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.db_glq, (void*)b.db_gprog, (void*)b.pack_done, (void*)b.db_cnt})
         if (p) (void)hipFree(p);
     if (b.db_err) (void)hipHostFree(b.db_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
@@ -339,8 +340,6 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     hp_pitch_ = (geom_.coded_w + 2 * kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
-    HIP_CHECK(hipMalloc(&db_auto_, sizeof(uint32_t) * 4));
-    HIP_CHECK(hipMemsetAsync(db_auto_, 0, sizeof(uint32_t) * 4, stream_));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     clock_khz_ = device_clock_khz();
     if (depth_ > 1) {
@@ -436,7 +435,6 @@ GpuH264Encoder::~GpuH264Encoder() {
     }
     for (int i = 0; i < 4; ++i) (void)hipFree(hp_[i]);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
-    if (db_auto_) (void)hipFree(db_auto_);
 }
 
 void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
@@ -489,7 +487,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     if (async_frame_) {  // entropy chain to the launcher thread (its stream operations only there)
         HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
         hipEvent_t sse_ready = nullptr;
-        if (cfg_.h264_deblock()) {
+        if (sl.deblock) {
             launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
             HIP_CHECK(hipEventRecord(sl.deblock_done, stream_));
             sse_ready = sl.deblock_done;
@@ -511,7 +509,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     link_entropy();
     hipStream_t es = stream_e_ ? stream_e_ : stream_;
     hipEvent_t sse_ready = nullptr;
-    if (cfg_.h264_deblock()) {  // in-loop filter on the analysis stream: the next frame predicts from it,
+    if (sl.deblock) {  // in-loop filter on the analysis stream: the next frame predicts from it,
                          // while this frame's CAVLC runs beside it on the entropy stream
         launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
         if (stream_e_) {
@@ -543,10 +541,8 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.me_coarse = cfg_.me_coarse;
     f.intra4x4 = cfg_.intra4x4;
     f.subpel = cfg_.subpel;
-    f.deblock_off = cfg_.h264_deblock() ? 0 : 1;  // adaptive: k_db_prep overwrites it on the device
-    f.deblock_auto = cfg_.h264_deblock_auto() ? 1 : 0;
-    f.db_coherent = 0;
-    f.db_changed = 0;
+    sl.deblock = deblock_on();
+    f.deblock_off = sl.deblock ? 0 : 1;
     if (++db_epoch_ > 0xfffffu) db_epoch_ = 1;  // 20-bit tag, never 0
     f.db_epoch = (int32_t)db_epoch_;
     f.pic_init_qp = common_.pic_init_qp();
@@ -690,6 +686,10 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     stats_.deblocked = (int)hdr.deblocked;
     stats_.db_coherent = (int)hdr.db_coherent;
     stats_.db_changed = (int)hdr.db_changed;
+    stats_.db_moving = (int)hdr.db_moving;
+    if (cfg_.h264_deblock_auto() && !sl.idr)  // the next picture's filter, from this one's classes
+        db_prev_on_ = db_auto_decide(DbAutoCounts{hdr.db_coherent, hdr.db_changed, hdr.db_moving},
+                                     geom_.mb_w * geom_.mb_h, db_prev_on_);
     common_.end_frame((int)au_.size(), sl.idr);
     return au_;
 }

@@ -52,10 +52,10 @@ struct EncoderConfig {
                               // +0.6 dB (H.264) / +1.4 dB (HEVC) masked Y-PSNR at equal rate, motion content
                               // unchanged (profiles/r04_hevc/NOTES.md).  HEVC has 0, 1 and 3+, and treats 2
                               // as 1
-    // in-loop deblocking filter: 1 on, 0 off, 2 adaptive (H.264: per picture from its temporal
-    // classes, h264_deblock.h db_auto_decide; HEVC: on), -1 the codec's default -- HEVC on (8.7.2,
-    // fully parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: on the bench desktop it
-    // cost 3.3x throughput and 0.7 dB noise-masked Y-PSNR at equal rate, profiles/r03_deblock/NOTES.md)
+    // in-loop deblocking filter: 1 on, 0 off, 2 adaptive (per picture from its temporal classes,
+    // h264_deblock.h db_auto_decide), -1 the codec's default -- HEVC adaptive (8.7.2 is fully
+    // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: adaptive filtering switches
+    // it on for motion content, +1.3 dB for -76 % throughput, profiles/r05_deblock/NOTES.md)
     int deblock = -1;
     // P pictures: also search 16x8 / 8x16 partitionings (two vectors per macroblock) and take one
     // when its SAD + lambda * vector rate beats the 16x16 vector's
@@ -63,6 +63,9 @@ struct EncoderConfig {
     bool h264_deblock() const { return deblock > 0; }  // the filter kernels run (on, or adaptive)
     bool h264_deblock_auto() const { return deblock == 2; }
     bool hevc_deblock() const { return deblock != 0; }
+    // HEVC's default is adaptive: deblocking costs the still desktop 0.3 dB (its text regions
+    // 4.5 dB) and gains 0.2 dB on motion content at 4K 18 Mbps (profiles/r05_hevc/NOTES.md)
+    bool hevc_deblock_auto() const { return deblock == 2 || deblock < 0; }
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: it costs -35 % fps on the 1080p desktop (k_intra_analyze + k_intra_p on
                               // the analysis queue, profiles/r04_toolset/NOTES.md)
@@ -103,7 +106,7 @@ struct FrameStats {
     uint64_t sse_masked = 0;      // Y outside the mask macroblocks (EncoderConfig::mask_*)
     int64_t masked_pixels = 0;    // display luma samples outside them (the PSNR denominator)
     int deblocked = 0;            // H.264: the in-loop filter ran on this picture (idc 0)
-    int db_coherent = 0, db_changed = 0;  // adaptive filter: the picture's class counts (db_auto_count)
+    int db_coherent = 0, db_changed = 0, db_moving = 0;  // adaptive filter: the picture's class counts (db_auto_count)
 };
 
 // Annex-B / rate-control logic shared by both encoders.
@@ -271,6 +274,7 @@ class GpuH264Encoder final : public VideoEncoder {
         hipEvent_t start = nullptr, analysis_done = nullptr, deblock_done = nullptr, done = nullptr;
         hipEvent_t hpel_done = nullptr;
         bool idr = false;
+        bool deblock = false;  // the picture's in-loop filter (decided when it is prepared)
         int qp = 0;
     };
     void alloc_slot(FrameSlot& sl);
@@ -330,7 +334,10 @@ class GpuH264Encoder final : public VideoEncoder {
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
     uint32_t db_epoch_ = 0;
-    uint32_t* db_auto_ = nullptr;  // adaptive filter state (DeviceBuffers::db_auto), shared by the slots
+    // adaptive filter: the next picture's decision, from the last collected P picture's classes
+    // (OutHeader::db_*); a picture's filter is fixed when it is prepared (FrameSlot::deblock)
+    bool db_prev_on_ = false;
+    bool deblock_on() const { return cfg_.deblock == 1 || (cfg_.h264_deblock_auto() && db_prev_on_); }
     int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
     int64_t masked_pixels_ = 0;
     std::vector<uint8_t> au_;
@@ -357,8 +364,10 @@ class CpuH264Encoder {
     void encode_inter(const uint8_t* y, const uint8_t* uv, int pitch);
     void entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& slice_off, std::vector<uint32_t>& slice_len);
     int frame_qp_() const { return qp_override_ >= 0 ? qp_override_ : common_.cur_qp(); }
-    // the picture's in-loop filter decision (EncoderConfig::deblock; adaptive: db_auto_decide, as k_db_prep)
+    // the picture's in-loop filter (EncoderConfig::deblock; adaptive: the decision db_auto_decide
+    // took from the previous P picture's classes, as the GPU encoder's host side) / the update after it
     void decide_deblock();
+    void update_deblock_decision();
     bool deblock_now_ = false, db_prev_on_ = false;
     DbAutoCounts db_counts_;
     int qp_override_ = -1;  // rate-control probe of the first picture

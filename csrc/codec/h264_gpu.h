@@ -81,8 +81,6 @@ struct FrameState {
     int32_t intra4x4;      // 0 = intra MBs are Intra16x16 only
     int32_t deblock_off;   // disable_deblocking_filter_idc (0: k_deblock filters the reconstruction)
     int32_t db_epoch;      // nonzero, new every frame: tag of k_deblock's cross-workgroup progress words
-    int32_t deblock_auto;  // 1: k_db_prep decides deblock_off on the device (db_auto_decide)
-    int32_t db_coherent, db_changed;  // written by k_db_prep (adaptive filter): the picture's class counts
     int32_t pic_init_qp;
     int32_t chroma_qp_offset;
     int32_t log2_max_frame_num;
@@ -122,8 +120,10 @@ struct OutHeader {
     // event record between kernels cost ~5 us of idle GPU each: profiles/r04_h264)
     uint64_t t_start;
     uint64_t t_end;
-    uint32_t db_coherent, db_changed;  // adaptive filter: the picture's class counts (db_auto_count)
-    uint32_t pad[2];
+    // adaptive filter (EncoderConfig::deblock 2): the P picture's class counts (h264_deblock.h
+    // db_auto_count, k_scan_rows), from which the host decides the next picture's filter
+    uint32_t db_coherent, db_changed, db_moving;
+    uint32_t pad;
 };
 static_assert(sizeof(OutHeader) % 16 == 0, "payload must stay 16-byte aligned");
 constexpr int kMaxSlices = 1024;
@@ -167,9 +167,7 @@ struct DeviceBuffers {
     uint32_t* db_glq;       // [2][mb_h][mb_w] their QP
     uint32_t* db_gprog;     // [2][mb_h] band-boundary progress words (epoch << 12 | count)
     int* db_err;            // mapped host word: nonzero if a deblocking spin timed out
-    // adaptive filter state, shared by the encoder's frame slots (the analysis stream orders the
-    // frames): [0] last P decision, [1] coherent / [2] changed counts, [3] k_db_prep ticket
-    uint32_t* db_auto;
+    uint32_t* db_cnt;       // [3] adaptive filter: coherent / changed / moving counts (k_scan_rows, zeroed by k_scan_out)
     uint32_t* pack_done;    // [1] k_pack workgroups finished (the last one stamps t_end and resets it)
 };
 

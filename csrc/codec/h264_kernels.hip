@@ -24,6 +24,7 @@
 
 #include "../common/hip_check.h"
 #include "h264_core.h"
+#include "h264_deblock.h"
 #include "h264_gpu.h"
 #include "h264_mb.h"
 
@@ -2161,7 +2162,8 @@ __device__ __forceinline__ SliceParams slice_params(const FrameState* fs, int s,
 __global__ __launch_bounds__(kScanThreads) void k_scan_rows(Geometry g, const FrameState* __restrict__ fs,
                                                             const uint32_t* __restrict__ slot_bits,
                                                             uint4* __restrict__ row_agg,
-                                                            unsigned long long* __restrict__ row_sse) {
+                                                            unsigned long long* __restrict__ row_sse,
+                                                            const MbInfo* __restrict__ mbs, uint32_t* __restrict__ db_cnt) {
     __shared__ int wi[kScanThreads / 64];
     __shared__ uint32_t wu[kScanThreads / 64];
     const int t = threadIdx.x, r = blockIdx.x, base = r * g.mb_w;
@@ -2224,6 +2226,22 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_rows(Geometry g, const Fr
         for (int w = 0; w < kScanThreads / 64; ++w) v += red[t][w];
         row_sse[t * kScanMaxRows + r] = v;
     }
+    if (idr || !db_cnt) return;
+    // adaptive in-loop filter: this row's temporal-class counts (h264_deblock.h db_auto_count)
+    DbAutoCounts ac;
+    for (int j = t; j < g.mb_w; j += kScanThreads) db_auto_count(mbs, g.mb_w, base + j, ac);
+    uint32_t cv[3] = {ac.coherent, ac.changed, ac.moving};
+    __shared__ uint32_t cred[3][kScanThreads / 64];
+    for (int c = 0; c < 3; ++c) {
+        for (int o = 32; o > 0; o >>= 1) cv[c] += __shfl_xor(cv[c], o);
+        if ((t & 63) == 0) cred[c][t >> 6] = cv[c];
+    }
+    __syncthreads();
+    if (t < 3) {
+        uint32_t v = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) v += cred[t][w];
+        if (v) atomicAdd(&db_cnt[t], v);
+    }
 }
 
 // Pass 2, row r: row / slice prefixes from all rows' summaries, then this row's units:
@@ -2238,7 +2256,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const Fra
                                                            uint4* __restrict__ coded_info,
                                                            uint32_t* __restrict__ slice_info, size_t out_bytes,
                                                            OutHeader* __restrict__ hdr,
-                                                           uint32_t* __restrict__ quad_unit) {
+                                                           uint32_t* __restrict__ quad_unit, uint32_t* __restrict__ db_cnt) {
     __shared__ int s_lbraw[kScanMaxRows + 1];    // last coded MB before row j (any slice), -1 = none
     __shared__ uint32_t s_P[kScanMaxRows + 1];   // unit bits before row j (frame-wide running sum)
     __shared__ uint32_t s_R[kScanMaxRows + 1];   // coded MBs before row j
@@ -2382,8 +2400,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_out(Geometry g, const Fra
             hdr->num_slices = ns;
             hdr->overflow = (otot ? 1u : 0u) | (over_b ? 2u : 0u);
             hdr->deblocked = fs->deblock_off ? 0u : 1u;
-            hdr->db_coherent = (uint32_t)fs->db_coherent;
-            hdr->db_changed = (uint32_t)fs->db_changed;
+            hdr->db_coherent = db_cnt ? db_cnt[0] : 0u;
+            hdr->db_changed = db_cnt ? db_cnt[1] : 0u;
+            hdr->db_moving = db_cnt ? db_cnt[2] : 0u;
+            if (db_cnt) db_cnt[0] = db_cnt[1] = db_cnt[2] = 0;  // re-armed for the slot's next frame
         }
     }
     // this row's units
@@ -2637,9 +2657,9 @@ void launch_entropy(const Geometry& g, const DeviceBuffers& b, uint8_t* host_out
     if (g.mb_h > kScanMaxRows || g.mb_w > kScanThreads * kScanRowPer)
         throw std::runtime_error("launch_entropy: frame too large for the row scan");
     hipLaunchKernelGGL(k_scan_rows, dim3(g.mb_h), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.row_agg,
-                       b.row_sse);
+                       b.row_sse, b.mb, b.db_cnt);
     hipLaunchKernelGGL(k_scan_out, dim3(g.mb_h), dim3(kScanThreads), 0, stream, g, b.fs, b.slot_bits, b.row_agg,
-                       b.row_sse, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr, b.quad_unit);
+                       b.row_sse, b.coded_info, b.slice_info, b.out_bytes, b.out_hdr, b.quad_unit, b.db_cnt);
     hipLaunchKernelGGL(k_pack, dim3(256), dim3(256), 0, stream, g, b.fs, b.slot, b.coded_info, b.slice_info,
                        b.out_hdr, host_out, b.quad_unit, b.pack_done);
 }

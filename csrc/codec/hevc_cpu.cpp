@@ -254,7 +254,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         const bool db = c.hevc_deblock();
         w.put(db || c.sao, 1);  // pps_loop_filter_across_slices_enabled_flag (CU edges on slice borders too)
         w.put(1, 1);   // deblocking_filter_control_present_flag
-        w.put(0, 1);   //   deblocking_filter_override_enabled_flag
+        w.put(c.hevc_deblock_auto(), 1);  //   deblocking_filter_override_enabled_flag (adaptive: per slice)
         w.put(!db, 1);  //   pps_deblocking_filter_disabled_flag
         if (db) {
             w.se(0);  //   pps_beta_offset_div2
@@ -270,7 +270,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
     }
 }
 
-void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp,
+void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp, bool deblock,
                                  const uint8_t* data, size_t n, const uint32_t* sub_len, int nsub,
                                  const uint32_t* sub_off) const {
     const int ctbs = num_ctbs();
@@ -298,7 +298,12 @@ void HevcCommon::write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, 
         w.ue(5 - kMaxMergeCand);  // five_minus_max_num_merge_cand -> MaxNumMergeCand 5
     }
     w.se(qp - 26);  // slice_qp_delta
-    if (config().hevc_deblock() || sao) w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
+    if (config().hevc_deblock_auto()) {  // adaptive filter: override the PPS (filter on) where it is off
+        w.put(!deblock, 1);       // deblocking_filter_override_flag
+        if (!deblock) w.put(1, 1);  // slice_deblocking_filter_disabled_flag
+    }
+    if ((config().hevc_deblock() || sao) && (sao || deblock))
+        w.put(1, 1);  // slice_loop_filter_across_slices_enabled_flag
     if (!wpp()) {
         w.trailing();   // byte_alignment()
         std::vector<uint8_t> rbsp = std::move(w.b);
@@ -695,7 +700,16 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         analyse_inter(y, uv, pitch);
     }
     qp_chain(qp);
-    if (cfg_.hevc_deblock()) {  // in-loop deblocking: all vertical edges, then all horizontal ones
+    deblock_now_ = cfg_.hevc_deblock();
+    if (cfg_.hevc_deblock_auto()) {  // adaptive: k_hevc_db_auto's rule over the units' motion-search vectors
+        if (!idr) {
+            h264::DbAutoCounts c;
+            for (int i = 0; i < W * H; ++i) h264::db_auto_count_mv(mv_.data(), 2, W, i, c);
+            db_prev_on_ = h264::db_auto_decide(c, W * H, db_prev_on_);
+        }
+        deblock_now_ = db_prev_on_;
+    }
+    if (deblock_now_) {  // in-loop deblocking: all vertical edges, then all horizontal ones
         for (int dir = 0; dir < 2; ++dir)
             for (int i = 0; i < W * H; ++i)
                 for (int seg = 0; seg < 4; ++seg) {
@@ -749,7 +763,7 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         const uint32_t n = common_.wpp() ? code_slice_wpp(buf.data(), cap, idr, qp, ps, first, end, tok_.data(), sub_len)
                                          : code_slice(buf.data(), cap, idr, qp, ps, first, end, ctx, tok_.data());
         if (n > cap) throw std::runtime_error("hevc cpu encoder: slice buffer overflow");
-        common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, buf.data(), n,
+        common_.write_slice_nal(au_, first, idr, idr ? 0 : common_.poc(), qp, deblock_now_, buf.data(), n,
                                 common_.wpp() ? sub_len.data() : nullptr, (int)sub_len.size());
     }
     // distortion over the display area
@@ -772,6 +786,7 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     stats_.idr = idr;
     stats_.qp = qp;
     stats_.bytes = (int)au_.size();
+    stats_.deblocked = deblock_now_ ? 1 : 0;
     stats_.skipped_mbs = 0;
     for (const auto& cu : cu_) stats_.skipped_mbs += cu.type == kCuSkip;
     for (int k = 0; k < 3; ++k) stats_.sse[k] = sse[k];

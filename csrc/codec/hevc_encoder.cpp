@@ -61,6 +61,7 @@ void GpuHevcEncoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.wpp_ctx, sizeof(uint32_t) * kWppCtxWords * (size_t)common_.c32_h()));
     HIP_CHECK(hipMalloc(&b.wpp_flag, sizeof(uint32_t) * (size_t)common_.c32_h()));
     HIP_CHECK(hipMemsetAsync(b.wpp_flag, 0, sizeof(uint32_t) * (size_t)common_.c32_h(), stream_));
+    b.db_state = db_state_;
     HIP_CHECK(hipHostMalloc(&b.wpp_err, sizeof(int), hipHostMallocMapped));
     *b.wpp_err = 0;
     b.out_bytes = (size_t)ncu * 768;
@@ -133,6 +134,8 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
+    HIP_CHECK(hipMalloc(&db_state_, sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(db_state_, 0, sizeof(uint32_t), stream_));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     if (depth_ > 1) {
         // entropy streams: MXDESK_HEVC_ESTREAMS of them (default one per slot), slots beyond
@@ -162,6 +165,7 @@ GpuHevcEncoder::~GpuHevcEncoder() {
     if (pre_y_) (void)hipFree(pre_y_);
     if (pre_uv_) (void)hipFree(pre_uv_);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
+    if (db_state_) (void)hipFree(db_state_);
 }
 
 void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur, bool probe) {
@@ -171,7 +175,8 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.ref_uv = rec_uv_[ref];
     // the rate-control probe codes without SAO (as the CPU encoder's probe)
     f.sao = (cfg_.sao && !probe) ? 1 : 0;
-    f.pad_ = 0;
+    f.deblock_on = cfg_.hevc_deblock() ? 1 : 0;  // adaptive: k_hevc_db_auto overwrites it on the device
+    f.deblock_auto = cfg_.hevc_deblock_auto() ? 1 : 0;
     f.rec_y = f.sao ? pre_y_ : rec_y_[cur];
     f.rec_uv = f.sao ? pre_uv_ : rec_uv_[cur];
     f.sao_y = rec_y_[cur];
@@ -184,7 +189,6 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.num_slices = common_.num_slices();
     f.bl_safe = bl_safe_;
     f.depth_inter = common_.depth_inter();
-    f.pad2_ = 0;
     f.aq = cfg_.aq;
     f.tu_split = cfg_.tu_split;  // 0 none, 1 8x8 nodes, 2 also 4x4 luma TUs
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
@@ -280,7 +284,7 @@ void GpuHevcEncoder::enqueue_analysis_impl(bool idr, const uint8_t* src_y, const
         launch_hevc_inter(geom_, sl.buf, src_y, src_uv, stream_);
     }
     launch_hevc_layout(geom_, sl.buf, idr, common_.max_slices(), cfg_.hevc_slice_cost, cfg_.hevc_deblock(), sl.fs_host->sao != 0, src_y,
-                       src_uv, stream_);
+                       src_uv, stream_, cfg_.hevc_deblock_auto());
 }
 
 void GpuHevcEncoder::link_entropy() {
@@ -373,13 +377,14 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     if (sl.idr) common_.write_parameter_sets(au_);
     if (!common_.wpp()) {
         for (uint32_t k = 0; k < nsub; ++k)
-            common_.write_slice_nal(au_, (int)last_first_[k], sl.idr, sl.poc, sl.qp, payload + soff[k], slen[k]);
+            common_.write_slice_nal(au_, (int)last_first_[k], sl.idr, sl.poc, sl.qp, hdr.deblocked != 0, payload + soff[k],
+                                    slen[k]);
     } else {
         for (uint32_t k = 0; k < nsub;) {
             uint32_t e = k + 1, n = slen[k];
             while (e < nsub && !(saddr[e] & kSubSliceStart)) n += slen[e++];
-            common_.write_slice_nal(au_, (int)last_first_[k], sl.idr, sl.poc, sl.qp, payload, n, slen + k, (int)(e - k),
-                                    soff + k);
+            common_.write_slice_nal(au_, (int)last_first_[k], sl.idr, sl.poc, sl.qp, hdr.deblocked != 0, payload, n,
+                                    slen + k, (int)(e - k), soff + k);
             k = e;
         }
     }
@@ -391,6 +396,7 @@ const std::vector<uint8_t>& GpuHevcEncoder::collect() {
     for (int c = 0; c < 3; ++c) stats_.sse[c] = hdr.sse[c];
     stats_.sse_masked = hdr.sse_masked;
     stats_.masked_pixels = masked_pixels_;
+    stats_.deblocked = (int)hdr.deblocked;
     rc.end_frame((int)au_.size(), sl.idr);
     return au_;
 }

@@ -56,8 +56,9 @@ class HevcCommon {
     // sub_len[0..nsub) their raw sizes; the header carries their entry points (sizes after
     // emulation prevention, 7.4.7.1).
     // sub_off: byte offsets of the substreams in data (nullptr: back to back).
-    void write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp, const uint8_t* data,
-                         size_t n, const uint32_t* sub_len = nullptr, int nsub = 0,
+    // deblock: the picture's filter decision (adaptive filtering overrides the PPS per slice)
+    void write_slice_nal(std::vector<uint8_t>& out, int addr, bool idr, int poc, int qp, bool deblock,
+                         const uint8_t* data, size_t n, const uint32_t* sub_len = nullptr, int nsub = 0,
                          const uint32_t* sub_off = nullptr) const;
     bool wpp() const { return config().hevc_wpp != 0; }
     // CTB rows per P slice with WPP (the whole picture when 0 or larger)
@@ -106,6 +107,8 @@ class CpuHevcEncoder {
     void analyse_inter(const uint8_t* y, const uint8_t* uv, int pitch);
     int frame_qp_() { return qp_override_ >= 0 ? qp_override_ : common_.rc().cur_qp(); }
     int qp_override_ = -1;  // rate-control probe of the first picture
+    // the picture's in-loop filter decision (EncoderConfig::deblock; adaptive: as k_hevc_db_auto)
+    bool deblock_now_ = false, db_prev_on_ = false;
 
     EncoderConfig cfg_;
     HevcCommon common_;
@@ -155,7 +158,7 @@ struct HevcFrameState {
     // SAO (EncoderConfig::sao): the analysis kernels reconstruct into rec_*, deblocking filters
     // it in place, k_hevc_sao writes the final picture to sao_* (the reference of the next frame)
     int32_t sao;
-    int32_t pad_;
+    int32_t deblock_on;  // the in-loop filter runs on this picture (EncoderConfig::deblock 2: set by k_hevc_db_auto)
     uint8_t* sao_y;
     uint8_t* sao_uv;
     // quality-report mask in CTBs (x0, y0, x1, y1; x1 <= x0: none): k_hevc_sao adds a 4th
@@ -177,14 +180,14 @@ struct HevcFrameState {
     // (hevc_core.h bl_safe_modes: 16x16 luma and its DM 8x8 chroma)
     uint64_t bl_safe;
     int32_t depth_inter;  // max_transform_hierarchy_depth_inter of the SPS
-    int32_t pad2_;
+    int32_t deblock_auto;  // EncoderConfig::deblock 2: k_hevc_db_auto decides deblock_on (h264_deblock.h rule)
 };
 
 struct HevcOutHeader {
     uint32_t total_bytes;
     uint32_t num_slices;
     uint32_t overflow;
-    uint32_t pad;
+    uint32_t deblocked;  // the picture was deblocked (slice_deblocking_filter_disabled_flag 0)
     uint64_t sse[3];
     uint64_t sse_masked;  // luma outside the mask CTBs (SAO path; 0 otherwise)
     uint64_t t_start;     // device clock: k_hevc_publish (eager frames; 0 otherwise)
@@ -232,6 +235,7 @@ struct HevcDeviceBuffers {
     unsigned long long* sse_part;
     unsigned long long* sse_tot;  // [kSseSlots][kSseSlotWords] k_hevc_sao distortion totals (4 used per slot)
     uint32_t* pack_done;          // [1] k_hevc_pack workgroups finished (the last stamps t_end, re-arms it)
+    uint32_t* db_state;           // [1] adaptive filter: the last P decision (shared by the frame slots)
 };
 // Eager frames: one kernel stores both frame states (kernel arguments) to the device and stamps
 // the frame's start clock -- instead of two host-to-device copies (two blit kernels on the
@@ -247,8 +251,9 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
                        const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
 // Slice layout, per-slice decisions and (with deblock) the in-loop filter + final distortion:
 // runs on the analysis stream because the deblocked picture is the next frame's reference.
+// deblock_auto: k_hevc_db_auto decides the picture's filter first (EncoderConfig::deblock 2)
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,
-                        bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s);
+                        bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s, bool deblock_auto = false);
 void launch_hevc_entropy(const Geometry& g, const HevcDeviceBuffers& b, int max_slices, uint8_t* host_out,
                          hipStream_t s);
 
@@ -347,6 +352,7 @@ class GpuHevcEncoder final : public VideoEncoder {
     uint64_t bl_safe_ = 0;       // hevc_core.h bl_safe_modes (16x16 luma & DM chroma)
     uint8_t* pre_y_ = nullptr;   // SAO: reconstruction before SAO (deblocked in place)
     uint8_t* pre_uv_ = nullptr;
+    uint32_t* db_state_ = nullptr;  // adaptive filter state (HevcDeviceBuffers::db_state)
     int cur_ = 0;
     bool have_ref_ = false;
     std::vector<uint8_t> au_;

@@ -1896,9 +1896,45 @@ __global__ __launch_bounds__(256) void k_hevc_qpy(Geometry g, const HevcFrameSta
 // One thread per 4-sample segment of a CU's left (dir 0) or top (dir 1) edge.  Vertical
 // edges are 16 samples apart and a filter reads p3..q3 / writes p2..q2, so all segments of a
 // direction are independent; the horizontal pass runs as a second launch on its output.
+// Adaptive in-loop filtering (EncoderConfig::deblock 2): the picture's decision by the rule of
+// h264_deblock.h (coherent motion over 1/8 of the units, hysteresis; an IDR keeps the last P
+// decision), from the motion-search vectors of the 16x16 units.  One workgroup.
+__global__ __launch_bounds__(1024) void k_hevc_db_auto(Geometry g, HevcFrameState* __restrict__ fs,
+                                                       const h264::MbInfo* __restrict__ mb, uint32_t* __restrict__ st) {
+    __shared__ uint32_t part[2][16];
+    const int n = g.mb_w * g.mb_h;
+    const bool idr = fs->idr != 0;
+    h264::DbAutoCounts c;
+    if (!idr)
+        for (int i = threadIdx.x; i < n; i += 1024) h264::db_auto_count_mv(&mb[0].mvx, (int)(sizeof(h264::MbInfo) / 2), g.mb_w, i, c);
+    uint32_t co = c.coherent, mv = c.moving;
+    for (int o = 32; o > 0; o >>= 1) {
+        co += __shfl_xor(co, o, 64);
+        mv += __shfl_xor(mv, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = co;
+        part[1][threadIdx.x >> 6] = mv;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    h264::DbAutoCounts tot;
+    for (int k = 0; k < 16; ++k) {
+        tot.coherent += part[0][k];
+        tot.moving += part[1][k];
+    }
+    bool on = st[0] != 0;
+    if (!idr) {
+        on = h264::db_auto_decide(tot, n, on);
+        st[0] = on ? 1u : 0u;
+    }
+    fs->deblock_on = on ? 1 : 0;
+}
+
 __global__ __launch_bounds__(256) void k_hevc_deblock(Geometry g, const HevcFrameState* __restrict__ fs,
                                                       const CuInfo* __restrict__ cus, const uint8_t* __restrict__ qpy,
                                                       int dir) {
+    if (!fs->deblock_on) return;  // adaptive filter: off for this picture
     const int t = blockIdx.x * 256 + threadIdx.x;
     const int ncu = g.mb_w * g.mb_h;
     if (t >= ncu * 4) return;
@@ -2370,7 +2406,7 @@ __device__ void pack_body(Geometry g, const HevcFrameState* __restrict__ fs, con
         h.total_bytes = T;
         h.num_slices = (uint32_t)num_slices;
         h.overflow = (O || T > out_bytes) ? 1u : 0u;
-        h.pad = 0;
+        h.deblocked = (uint32_t)fs->deblock_on;
         for (int c = 0; c < 3; ++c) h.sse[c] = E[c];
         h.sse_masked = E[3];
     }
@@ -2423,7 +2459,7 @@ void launch_hevc_intra(const Geometry& g, const HevcDeviceBuffers& b, int slice_
 }
 
 void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr, int max_slices, int slice_cost, bool deblock,
-                        bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s) {
+                        bool sao, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t s, bool deblock_auto) {
     const int ncu = g.mb_w * g.mb_h;
     const int cw = ctb_cols(g.mb_w), nctb = cw * ctb_rows(g.mb_h);
     hipLaunchKernelGGL(k_hevc_layout, dim3((nctb + kScanTile - 1) / kScanTile), dim3(1024), 0, s, b.fs, b.cost, nctb, cw,
@@ -2435,6 +2471,8 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
     hipLaunchKernelGGL(k_hevc_qpy, dim3(std::max(max_slices, ctb_rows(g.mb_h))), dim3(256), 0, s, g, b.fs, b.cu, b.qpc,
                        b.slice_first, b.nslices, b.qp_pred, b.qpy);
     if (deblock) {
+        if (deblock_auto)
+            hipLaunchKernelGGL(k_hevc_db_auto, dim3(1), dim3(1024), 0, s, g, b.fs, b.me.mb, b.db_state);
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
     }

@@ -907,9 +907,12 @@ class Decoder:
         if p.slice_chroma_qp_offsets_present:
             r.se()
             r.se()
-        if p.deblocking_override_enabled and r.u(1):
-            raise NotImplementedError("deblocking override")
         db_disabled = p.deblocking_disabled
+        beta_div2, tc_div2 = p.beta_offset_div2, p.tc_offset_div2
+        if p.deblocking_override_enabled and r.u(1):  # deblocking_filter_override_flag
+            db_disabled = r.u(1)  # slice_deblocking_filter_disabled_flag
+            if not db_disabled:
+                beta_div2, tc_div2 = r.se(), r.se()
         lf_across = p.loop_filter_across_slices
         if p.loop_filter_across_slices and (sao_luma or sao_chroma or not db_disabled):
             lf_across = r.u(1)
@@ -921,7 +924,7 @@ class Decoder:
                 entry = [r.u(olen) + 1 for _ in range(n_entry)]
         self.slice_params[addr] = {"db_disabled": db_disabled, "lf_across": lf_across,
                                    "sao_luma": sao_luma, "sao_chroma": sao_chroma,
-                                   "beta_offset": 2 * p.beta_offset_div2, "tc_offset": 2 * p.tc_offset_div2}
+                                   "beta_offset": 2 * beta_div2, "tc_offset": 2 * tc_div2}
         r.byte_alignment()
         self.stats["slices"] += 1
         self.slice_type = slice_type

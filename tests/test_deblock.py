@@ -121,8 +121,9 @@ def _pan_frames(w, h, n, step=3, still=False):
 
 
 def test_adaptive_filter_follows_motion_and_decodes(native):
-    """deblock=2: P pictures of a pan are filtered (coherent vectors cover the picture), a forced
-    IDR keeps the decision, a still scene stays unfiltered; per-picture idc decodes exactly."""
+    """deblock=2: a picture's filter follows the previous P picture's classes -- the pan's pictures
+    after its first P picture are filtered, a forced IDR keeps the decision, a still scene stays
+    unfiltered; the per-picture idc decodes exactly."""
     w, h = 192, 96
     pan = [(y, uv, t == 4) for t, (y, uv) in enumerate(_pan_frames(w, h, 6))]
     cfg = native.EncoderConfig()
@@ -135,9 +136,9 @@ def test_adaptive_filter_follows_motion_and_decodes(native):
         ry, ruv = enc.recon()
         recons.append((ry.copy(), ruv.copy()))
         flags.append((enc.stats.deblocked, enc.stats.db_coherent))
-    assert flags[0][0] == 0  # the first IDR: nothing decided yet (off)
-    assert all(d == 1 for d, _ in flags[1:]), flags  # the pan's P pictures, and the forced IDR at 4
-    assert all(c * 8 >= (w // 16) * (h // 16) for _, c in flags[1:4]), flags
+    assert flags[0][0] == 0 and flags[1][0] == 0  # nothing decided before the first P picture
+    assert all(d == 1 for d, _ in flags[2:]), flags  # the pan's later pictures, and the forced IDR at 4
+    assert all(c * 8 >= (w // 16) * (h // 16) for _, c in flags[1:4]), flags  # the P pictures' classes
     _check(stream, recons)
 
     still = [(y, uv, False) for y, uv in _pan_frames(w, h, 5, still=True)]

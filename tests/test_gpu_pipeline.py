@@ -591,9 +591,9 @@ def test_device_clock_frame_times(gpu, depth):
 
 @pytest.mark.parametrize("depth", [1, 3])
 def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
-    """deblock=2: k_db_prep's per-picture decision (last-workgroup vote over the class counts)
-    equals the CPU encoder's, so the streams match bit for bit through a pan, a forced IDR and a
-    still stretch, with frames in flight (depth 3: the decision state is shared by the slots)."""
+    """deblock=2: the class counts k_scan_rows reports and the host's decision for the next picture
+    equal the CPU encoder's, so the streams match bit for bit through a pan, a forced IDR and a
+    still stretch (depth 3: the slots' counters and the shared decision)."""
     from .test_deblock import _pan_frames
 
     w, h = 192, 96
@@ -614,8 +614,9 @@ def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), idr)
         cau = cenc.encode(y, uv, idr)
         assert gau == cau, f"frame {t}: GPU bitstream differs from CPU encoder"
-        assert (genc.stats.deblocked, genc.stats.db_coherent, genc.stats.db_changed) == \
-            (cenc.stats.deblocked, cenc.stats.db_coherent, cenc.stats.db_changed), t
+        gst, cst = genc.stats, cenc.stats
+        assert (gst.deblocked, gst.db_coherent, gst.db_changed, gst.db_moving) == \
+            (cst.deblocked, cst.db_coherent, cst.db_changed, cst.db_moving), t
         assert np.array_equal(genc.recon()[0], cenc.recon()[0]), t
         flags.append(genc.stats.deblocked)
-    assert flags[1:5] == [1, 1, 1, 1] and flags[-1] == 0, flags
+    assert flags[2:6] == [1, 1, 1, 1] and flags[-1] == 0, flags

@@ -486,3 +486,58 @@ def test_token_path_matches_direct_cabac(native):
     levels, long motion-vector differences and SAO merge / band / edge parameters."""
     for seed in (1, 2, 3, 4):
         assert native.hevc_token_selftest(seed, 200) == 200
+
+
+def _adaptive_frames(w, h):
+    from .test_deblock import _pan_frames
+
+    frames = [(y, uv, t == 4) for t, (y, uv) in enumerate(_pan_frames(w, h, 6))]
+    return frames + [(y, uv, False) for y, uv in _pan_frames(w, h, 5, still=True)]
+
+
+def test_cpu_hevc_adaptive_deblocking_follows_motion(native):
+    """deblock=2: the pan's P pictures (and the forced IDR after them) are filtered, the still
+    stretch is not; the PPS enables the slice override and every picture decodes exactly."""
+    w, h = 192, 96
+    cfg = _cfg(native, w, h, qp=34)
+    cfg.deblock = 2
+    enc = native.CpuHevcEncoder(cfg)
+    stream, recon, flags = b"", [], []
+    for y, uv, idr in _adaptive_frames(w, h):
+        stream += enc.encode(y, uv, idr)
+        recon.append(tuple(p.copy() for p in enc.recon()))
+        flags.append(enc.stats.deblocked)
+    assert flags[0] == 0 and flags[1:5] == [1, 1, 1, 1] and flags[-1] == 0, flags
+    dec = Decoder()
+    dec.decode(stream)
+    for i, ((yy, u, v), (ry, ruv)) in enumerate(zip(dec.frames_coded, recon)):
+        assert np.array_equal(yy, ry), f"frame {i}"
+        assert np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2]), f"frame {i}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sao", [0, 1])
+def test_gpu_hevc_adaptive_deblocking_bit_exact_vs_cpu(gpu, sao):
+    """k_hevc_db_auto's decision equals the CPU encoder's: identical streams through a pan, a
+    forced IDR and a still stretch."""
+    import torch
+
+    from .gpu_util import pitched
+
+    w, h = 192, 96
+    cfg = _cfg(gpu, w, h, qp=34)
+    cfg.deblock, cfg.sao = 2, sao
+    genc = gpu.GpuHevcEncoder(cfg, torch.cuda.current_stream().cuda_stream)
+    cenc = gpu.CpuHevcEncoder(cfg)
+    ch = genc.coded_height
+    flags = []
+    for t, (y, uv, idr) in enumerate(_adaptive_frames(w, h)):
+        dy = pitched(y, genc.pitch, ch)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
+        torch.cuda.synchronize()
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), idr)
+        cau = cenc.encode(y, uv, idr)
+        assert gau == cau, f"frame {t}: GPU HEVC bitstream differs from the CPU encoder"
+        assert genc.stats.deblocked == cenc.stats.deblocked, t
+        flags.append(genc.stats.deblocked)
+    assert flags[1:5] == [1, 1, 1, 1], flags  # (the still stretch's decisions depend on the SAO setting)
