@@ -585,6 +585,8 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
 __global__ __launch_bounds__(64 * kDbRows) void k_deblock(Geometry g, const FrameState* __restrict__ fs,
                                                           const uint4* __restrict__ rec,
                                                           const int* __restrict__ row_lastq, DbGlobal G) {
+    // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
+    __builtin_amdgcn_s_setprio(3);
     // one workgroup per (band, plane): 8 waves of 512 threads leave each wave 256 VGPRs for the
     // line registers and the prefetch batch
     __shared__ DbShared S;

@@ -1828,6 +1828,8 @@ __global__ __launch_bounds__(512) void k_intra_wave(Geometry g, const FrameState
                                                      const uint8_t* __restrict__ src_y,
                                                      const uint8_t* __restrict__ src_uv, MbInfo* __restrict__ mbs,
                                                      int16_t* __restrict__ coef) {
+    // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
+    __builtin_amdgcn_s_setprio(3);
     extern __shared__ uint8_t s_line[];  // [slice rows][coded_w]: bottom sample line of every coded MB
     __shared__ IntraWaveTiles tiles[8];     // chroma workgroups
     __shared__ LumaPipeTiles ltiles[8];     // luma workgroups

@@ -134,8 +134,8 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
-    HIP_CHECK(hipMalloc(&db_state_, sizeof(uint32_t)));
-    HIP_CHECK(hipMemsetAsync(db_state_, 0, sizeof(uint32_t), stream_));
+    HIP_CHECK(hipMalloc(&db_state_, sizeof(uint32_t) * 4));
+    HIP_CHECK(hipMemsetAsync(db_state_, 0, sizeof(uint32_t) * 4, stream_));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     if (depth_ > 1) {
         // entropy streams: MXDESK_HEVC_ESTREAMS of them (default one per slot), slots beyond

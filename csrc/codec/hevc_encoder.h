@@ -235,7 +235,7 @@ struct HevcDeviceBuffers {
     unsigned long long* sse_part;
     unsigned long long* sse_tot;  // [kSseSlots][kSseSlotWords] k_hevc_sao distortion totals (4 used per slot)
     uint32_t* pack_done;          // [1] k_hevc_pack workgroups finished (the last stamps t_end, re-arms it)
-    uint32_t* db_state;           // [1] adaptive filter: the last P decision (shared by the frame slots)
+    uint32_t* db_state;           // [4] adaptive filter: the last P decision, counters, ticket (shared by the slots)
 };
 // Eager frames: one kernel stores both frame states (kernel arguments) to the device and stamps
 // the frame's start clock -- instead of two host-to-device copies (two blit kernels on the

@@ -1190,6 +1190,8 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                                                       const uint8_t* __restrict__ src_uv, CuInfo* __restrict__ cus,
                                                       int16_t* __restrict__ coef, const uint8_t* __restrict__ imode,
                                                       uint8_t* __restrict__ qp_coded) {
+    // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
+    __builtin_amdgcn_s_setprio(3);
     // dynamic LDS: per row of the slice, the bottom luma row and bottom chroma (NV12) row
     extern __shared__ uint8_t bottom[];
     __shared__ Mats M;
@@ -1736,6 +1738,8 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
                                                     uint8_t* __restrict__ slice_data, uint32_t slice_cap,
                                                     uint32_t* __restrict__ slice_len,
                                                     unsigned long long* __restrict__ slice_clk) {
+    // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
+    __builtin_amdgcn_s_setprio(3);
     // (slices and substreams in CTBs; a CTB's tokens are coding positions 4 c .. 4 c + 3)
     const int u = blockIdx.x, lane = threadIdx.x;
     const bool wpp = fs->wpp != 0;
@@ -1816,18 +1820,27 @@ __global__ __launch_bounds__(64) void k_hevc_arith(Geometry g, const HevcFrameSt
 
 // ------------------------------------------------------------------ QP chain
 // qPY_PRED / QpY of every unit (hevc_core.h slice_qp_chain): one workgroup per chain -- a slice, or
-// with WPP a CTB row (the chain restarts at every row).  The chain is serial but cheap once its
-// inputs sit in LDS: the threads stage 256 CTBs at a time (the four units' coded QP -- qpc, 255
-// when the unit sends no cu_qp_delta -- and the CTB's coding-tree depth), thread 0 walks them,
-// then every thread stores its CTB's results.
+// with WPP a CTB row (the chain restarts at every row).  The threads stage 256 CTBs at a time (the
+// four units' coded QP -- qpc, 255 when the unit sends no cu_qp_delta -- and the CTB's coding-tree
+// depth).  A CTB none of whose units codes a QP passes the chain value through unchanged (every
+// unit's prediction and QpY is the value entering it), so only the CTBs that code one are walked
+// serially, by thread 0, in order; every other CTB then takes the value the last coded CTB before it
+// left (a prefix count).  Cost-balanced slices make the static desktop a few long slices of skipped
+// CTBs: the walk over all of them was the kernel's 56 us (profiles/r05_hevc/kernels_hevc4k_18M.txt).
 __global__ __launch_bounds__(256) void k_hevc_qpy(Geometry g, const HevcFrameState* __restrict__ fs,
                                                    const CuInfo* __restrict__ cus, const uint8_t* __restrict__ qpc,
                                                    const int* __restrict__ slice_first,
                                                    const uint32_t* __restrict__ nslices,
                                                    uint8_t* __restrict__ qp_pred, uint8_t* __restrict__ qpy) {
+    // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
+    __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t q4[256], pr4[256], qy4[256];
-    __shared__ uint8_t info[256];  // bits 0-3: unit z inside the picture, bit 4: CU32
-    const int s = blockIdx.x, tid = threadIdx.x;
+    __shared__ uint8_t info[256];   // bits 0-3: unit z inside the picture, bit 4: CU32
+    __shared__ uint16_t list[256];  // the chunk's QP-coding CTBs, in order
+    __shared__ uint8_t after[256];  // the chain value each of them leaves
+    __shared__ uint32_t wcnt[4];
+    __shared__ int chunk_in;
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int cw = ctb_cols(g.mb_w), ch = ctb_rows(g.mb_h), nctb = cw * ch;
     const bool wpp = fs->wpp != 0;
     const int ns = wpp ? ch : (int)*nslices;
@@ -1838,21 +1851,33 @@ __global__ __launch_bounds__(256) void k_hevc_qpy(Geometry g, const HevcFrameSta
     for (int base = first; base < end; base += 256) {
         const int c = base + tid;
         const int x0 = 2 * (c % cw), y0 = 2 * (c / cw);
+        bool coded = false;
         if (c < end) {
             uint32_t w = 0, in = 0;
             for (int z = 0; z < 4; ++z) {
                 const int x = x0 + (z & 1), y = y0 + (z >> 1);
                 const bool inside = x < g.mb_w && y < g.mb_h;
-                w |= (inside ? (uint32_t)qpc[y * g.mb_w + x] : 255u) << (8 * z);
+                const uint32_t v = inside ? (uint32_t)qpc[y * g.mb_w + x] : 255u;
+                w |= v << (8 * z);
                 in |= inside ? 1u << z : 0u;
+                coded |= v != 255u;
             }
             q4[tid] = w;
             info[tid] = (uint8_t)(in | (cus[y0 * g.mb_w + x0].ct == 0 ? 16u : 0u));
         }
+        // position of this CTB among the chunk's coding CTBs (exclusive count)
+        const unsigned long long bal = __ballot(coded);
+        if (lane == 0) wcnt[wv] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        for (int k = 0; k < wv; ++k) before += wcnt[k];
+        const uint32_t ncoded = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (coded) list[before] = (uint16_t)tid;
         __syncthreads();
         if (tid == 0) {
-            const int n = min(256, end - base);
-            for (int j = 0; j < n; ++j) {
+            chunk_in = prev;
+            for (uint32_t k = 0; k < ncoded; ++k) {
+                const int j = list[k];
                 const uint32_t w = q4[j], f = info[j];
                 uint32_t pw = 0, qw = 0;
                 if (f & 16) {  // CU32: one quantization group, one QP
@@ -1878,16 +1903,22 @@ __global__ __launch_bounds__(256) void k_hevc_qpy(Geometry g, const HevcFrameSta
                 }
                 pr4[j] = pw;
                 qy4[j] = qw;
+                after[k] = (uint8_t)prev;
             }
         }
         __syncthreads();
-        if (c < end)
+        if (c < end) {
+            if (!coded) {  // the value the last coding CTB before it left (or the chunk's entry value)
+                const uint32_t v = before > 0 ? (uint32_t)after[before - 1] : (uint32_t)chunk_in;
+                pr4[tid] = qy4[tid] = v * 0x01010101u;
+            }
             for (int z = 0; z < 4; ++z) {
                 const int x = x0 + (z & 1), y = y0 + (z >> 1);
                 if (x >= g.mb_w || y >= g.mb_h) continue;
                 qp_pred[y * g.mb_w + x] = (uint8_t)(pr4[tid] >> (8 * z));
                 qpy[y * g.mb_w + x] = (uint8_t)(qy4[tid] >> (8 * z));
             }
+        }
         __syncthreads();
     }
 }
@@ -1897,16 +1928,18 @@ __global__ __launch_bounds__(256) void k_hevc_qpy(Geometry g, const HevcFrameSta
 // edges are 16 samples apart and a filter reads p3..q3 / writes p2..q2, so all segments of a
 // direction are independent; the horizontal pass runs as a second launch on its output.
 // Adaptive in-loop filtering (EncoderConfig::deblock 2): the picture's decision by the rule of
-// h264_deblock.h (coherent motion over 1/8 of the units, hysteresis; an IDR keeps the last P
-// decision), from the motion-search vectors of the 16x16 units.  One workgroup.
+// h264_deblock.h (coherent motion, hysteresis; an IDR keeps the last P decision), from the
+// motion-search vectors of the 16x16 units.  One workgroup per 1024 units adds its counts to
+// st[1..2]; the last one (ticket st[3]) decides, st[0] keeping the decision for the next picture,
+// and re-arms the counters.
 __global__ __launch_bounds__(1024) void k_hevc_db_auto(Geometry g, HevcFrameState* __restrict__ fs,
                                                        const h264::MbInfo* __restrict__ mb, uint32_t* __restrict__ st) {
     __shared__ uint32_t part[2][16];
     const int n = g.mb_w * g.mb_h;
     const bool idr = fs->idr != 0;
     h264::DbAutoCounts c;
-    if (!idr)
-        for (int i = threadIdx.x; i < n; i += 1024) h264::db_auto_count_mv(&mb[0].mvx, (int)(sizeof(h264::MbInfo) / 2), g.mb_w, i, c);
+    const int i = blockIdx.x * 1024 + threadIdx.x;
+    if (!idr && i < n) h264::db_auto_count_mv(&mb[0].mvx, (int)(sizeof(h264::MbInfo) / 2), g.mb_w, i, c);
     uint32_t co = c.coherent, mv = c.moving;
     for (int o = 32; o > 0; o >>= 1) {
         co += __shfl_xor(co, o, 64);
@@ -1918,17 +1951,28 @@ __global__ __launch_bounds__(1024) void k_hevc_db_auto(Geometry g, HevcFrameStat
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    h264::DbAutoCounts tot;
+    co = mv = 0;
     for (int k = 0; k < 16; ++k) {
-        tot.coherent += part[0][k];
-        tot.moving += part[1][k];
+        co += part[0][k];
+        mv += part[1][k];
     }
+    if (co) atomicAdd(&st[1], co);
+    if (mv) atomicAdd(&st[2], mv);
+    __threadfence();  // the counts before the ticket
+    if (atomicAdd(&st[3], 1u) != gridDim.x - 1) return;
+    __threadfence();
+    h264::DbAutoCounts tot;
+    tot.coherent = atomicAdd(&st[1], 0u);
+    tot.moving = atomicAdd(&st[2], 0u);
     bool on = st[0] != 0;
     if (!idr) {
         on = h264::db_auto_decide(tot, n, on);
         st[0] = on ? 1u : 0u;
     }
     fs->deblock_on = on ? 1 : 0;
+    st[1] = 0;
+    st[2] = 0;
+    st[3] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_hevc_deblock(Geometry g, const HevcFrameState* __restrict__ fs,
@@ -2472,7 +2516,7 @@ void launch_hevc_layout(const Geometry& g, const HevcDeviceBuffers& b, bool idr,
                        b.slice_first, b.nslices, b.qp_pred, b.qpy);
     if (deblock) {
         if (deblock_auto)
-            hipLaunchKernelGGL(k_hevc_db_auto, dim3(1), dim3(1024), 0, s, g, b.fs, b.me.mb, b.db_state);
+            hipLaunchKernelGGL(k_hevc_db_auto, dim3((ncu + 1023) / 1024), dim3(1024), 0, s, g, b.fs, b.me.mb, b.db_state);
         for (int dir = 0; dir < 2; ++dir)
             hipLaunchKernelGGL(k_hevc_deblock, dim3((ncu * 4 + 255) / 256), dim3(256), 0, s, g, b.fs, b.cu, b.qpy, dir);
     }

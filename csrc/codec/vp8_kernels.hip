@@ -443,6 +443,8 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
                                                  const uint8_t* __restrict__ src_uv, Vp8Mb* __restrict__ mbs,
                                                  int16_t* __restrict__ lv, uint32_t* __restrict__ prog,
                                                  uint64_t* __restrict__ line, int* __restrict__ err) {
+    // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
+    __builtin_amdgcn_s_setprio(3);
     __shared__ MbLds s;
     __shared__ KeyEdges E;
     const Vp8FrameState& F = st->v;
