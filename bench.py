@@ -109,15 +109,17 @@ def quality_probe(s, W: int, H: int, content: int, noise: int, n: int = 30) -> d
 
 
 def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: float = 1.0,
-                  threads: int = 8) -> dict:
+                  threads: int = 8, idr_storm: bool = False) -> dict:
     """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1) driven by
     `threads` host threads (N.run_sessions_paced: every 1/fps slot each thread submits one frame
     per session it owns, then collects them); K is sustained if no slot overran (every frame of
     every session encoded before the next slot starts) over `seconds`.  K doubles from k0 until a
     K fails, then bisects between the last sustained and the first failing K (to within 1/16), so
     `sustained` is a measured limit -- the first failing K minus the resolution -- not a list cap.
-    The whole serving path per session (render, CSC, encode, bitstream to host) runs."""
-    out = {"fps": fps, "seconds": seconds, "threads": threads, "tried": {}}
+    The whole serving path per session (render, CSC, encode, bitstream to host) runs.
+    idr_storm: in the middle slot every session codes a forced IDR picture (viewers joining at once,
+    a PLI burst); K is sustained only if that slot, too, finishes within its period."""
+    out = {"fps": fps, "seconds": seconds, "threads": threads, "idr_storm": idr_storm, "tried": {}}
 
     def trial(K: int) -> bool:
         sess = []
@@ -131,11 +133,16 @@ def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: flo
                 sess.append(N.Session(c))
             for s in sess:  # warm-up: first IDR + rate-control probe
                 s.step(False)
-            st = N.run_sessions_paced(sess, fps, seconds, min(threads, K))
+            slots = max(1, round(seconds * fps))
+            st = N.run_sessions_paced(sess, fps, seconds, min(threads, K), slots // 2 if idr_storm else -1)
             lat = sorted(st.lat_ms)
-            out["tried"][K] = {"late_slots": st.late_slots, "slots": st.slots,
-                               "p50_ms": round(lat[len(lat) // 2], 3),
-                               "p99_ms": round(lat[int(0.99 * (len(lat) - 1))], 3)}
+            rec = {"late_slots": st.late_slots, "slots": st.slots, "p50_ms": round(lat[len(lat) // 2], 3),
+                   "p99_ms": round(lat[int(0.99 * (len(lat) - 1))], 3)}
+            if idr_storm:
+                il = sorted(st.idr_lat_ms)
+                rec.update(idr_slot_late=bool(st.idr_late), idr_p50_ms=round(il[len(il) // 2], 3),
+                           idr_max_ms=round(il[-1], 3))
+            out["tried"][K] = rec
             return st.late_slots == 0
         except RuntimeError as e:  # out of device memory etc.: counts as a failing K
             out["tried"][K] = {"error": str(e)[:120]}
@@ -460,6 +467,9 @@ def main() -> None:
     if args.quality_probe > 0 and rank == 0 and not args.out_width:
         quality = quality_probe(sessions[0], args.width, args.height, content, args.noise, args.quality_probe)
     density = density_probe(N, cfg, args.fps) if args.density_probe else None
+    # the same probe with every session's IDR in one slot, from a quarter of the steady-state K
+    storm = (density_probe(N, cfg, args.fps, k0=max(4, (density["sustained"] or 16) // 4), idr_storm=True)
+             if args.density_probe and gpu else None)
 
     if dist is not None:
         t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
@@ -521,6 +531,9 @@ def main() -> None:
             # slot; K found by doubling then bisecting up to the first failing K
             "sessions_per_gpu_at_60fps_measured": density["sustained"] if density else None,
             "density_probe": density,
+            # measured: the sustained K when every session codes a forced IDR in the same slot
+            "sessions_per_gpu_idr_storm_measured": storm["sustained"] if storm else None,
+            "density_probe_idr_storm": storm,
             "dtype": "uint8 video (8-bit 4:2:0), " + CODEC_LABEL[args.codec][2],
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)" if gpu
             else "synthetic (numpy-rendered desktop, mxdesk.models.synthetic.CpuSyntheticDesktop)",

@@ -687,15 +687,18 @@ PYBIND11_MODULE(_native, m) {
     py::class_<PacedStats>(m, "PacedStats")
         .def_readonly("slots", &PacedStats::slots)
         .def_readonly("late_slots", &PacedStats::late_slots)
-        .def_readonly("lat_ms", &PacedStats::lat_ms);
+        .def_readonly("lat_ms", &PacedStats::lat_ms)
+        .def_readonly("idr_late", &PacedStats::idr_late)
+        .def_readonly("idr_lat_ms", &PacedStats::idr_lat_ms);
     m.def(
         "run_sessions_paced",
-        [](std::vector<Session*> ss, int fps, double seconds, int threads) {
+        [](std::vector<Session*> ss, int fps, double seconds, int threads, int idr_slot) {
             py::gil_scoped_release rel;
-            return run_sessions_paced(ss, fps, seconds, threads);
+            return run_sessions_paced(ss, fps, seconds, threads, idr_slot);
         },
-        py::arg("sessions"), py::arg("fps"), py::arg("seconds"), py::arg("threads") = 8,
-        "K sessions paced at fps for `seconds` by `threads` host threads (one frame in flight each)");
+        py::arg("sessions"), py::arg("fps"), py::arg("seconds"), py::arg("threads") = 8, py::arg("idr_slot") = -1,
+        "K sessions paced at fps for `seconds` by `threads` host threads (one frame in flight each); "
+        "idr_slot >= 0: every session codes a forced IDR in that slot");
     py::class_<Session>(m, "Session")
         .def(py::init<const SessionConfig&>())
         .def(

@@ -528,7 +528,8 @@ FrameResult Session::collect() {
     return r;
 }
 
-PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, double seconds, int threads) {
+PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, double seconds, int threads,
+                              int idr_slot) {
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
     const int k = (int)sessions.size();
@@ -536,7 +537,7 @@ PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, do
     const int slots = std::max(1, (int)std::lround(seconds * fps));
     const auto period = std::chrono::nanoseconds((int64_t)(1e9 / std::max(1, fps)));
     std::vector<std::vector<uint8_t>> late(threads, std::vector<uint8_t>(slots, 0));
-    std::vector<std::vector<double>> lat(threads);
+    std::vector<std::vector<double>> lat(threads), idr_lat(threads);
     std::vector<std::exception_ptr> err(threads);
     // every thread starts on the same slot grid (a little ahead, so all are waiting for slot 0)
     const auto t0 = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
@@ -551,10 +552,13 @@ PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, do
                 for (int f = 0; f < slots; ++f) {
                     const auto tick = t0 + f * period;
                     std::this_thread::sleep_until(tick);
-                    for (Session* s : mine) s->submit_synthetic(false);
+                    const bool storm = f == idr_slot;  // every session's key frame in one slot
+                    for (Session* s : mine) s->submit_synthetic(storm);
                     for (Session* s : mine) {
                         const FrameResult r = s->collect();
-                        lat[t].push_back((r.t_encoded_us - r.t_capture_us) / 1000.0);
+                        const double ms = (r.t_encoded_us - r.t_capture_us) / 1000.0;
+                        lat[t].push_back(ms);
+                        if (storm) idr_lat[t].push_back(ms);
                     }
                     late[t][f] = std::chrono::steady_clock::now() > tick + period ? 1 : 0;
                 }
@@ -574,6 +578,9 @@ PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, do
         st.late_slots += l ? 1 : 0;
     }
     for (auto& v : lat) st.lat_ms.insert(st.lat_ms.end(), v.begin(), v.end());
+    for (auto& v : idr_lat) st.idr_lat_ms.insert(st.idr_lat_ms.end(), v.begin(), v.end());
+    if (idr_slot >= 0 && idr_slot < slots)
+        for (int t = 0; t < threads; ++t) st.idr_late |= late[t][idr_slot] != 0;
     return st;
 }
 

@@ -91,12 +91,17 @@ class Session;
 // i on thread i % threads, one frame in flight per session).  Every 1/fps slot each thread
 // submits a frame on each of its sessions, then collects them; a slot is late when any thread
 // finished it after the next slot's start.  Latency = capture -> access unit on the host.
+// idr_slot >= 0: in that slot every session codes a forced IDR picture (an IDR storm: viewers
+// joining together, a PLI burst after a network event).
 struct PacedStats {
     int slots = 0;
     int late_slots = 0;
     std::vector<double> lat_ms;  // every frame of every session (slot order)
+    int idr_late = 0;            // the storm slot overran
+    std::vector<double> idr_lat_ms;  // the storm slot's frames
 };
-PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, double seconds, int threads);
+PacedStats run_sessions_paced(const std::vector<Session*>& sessions, int fps, double seconds, int threads,
+                              int idr_slot = -1);
 // Drives several sessions concurrently, one host thread per session (submit / collect with up
 // to `depth` frames in flight each): the per-frame launch sequence is host work, so one
 // thread interleaving K sessions leaves the GPU waiting on it.  Returns each session's

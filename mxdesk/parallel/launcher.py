@@ -15,23 +15,37 @@ from typing import Any
 from ..utils.supervisor import Program, Ready, Supervisor
 
 
+# Sessions per serving process: one event loop carries the WebRTC stack (ICE, DTLS, SRTP, SCTP
+# timers, pacing) of its sessions; 4 processes x 16 sessions held 64 1080p60 viewers per GPU at
+# p95 2.2 ms where one process topped out at 48 (profiles/r05_density/NOTES.md).
+SESSIONS_PER_PROCESS = 16
+
+
 def session_programs(n_gpus: int, base_port: int = 8080, extra_args: list[str] | None = None,
-                     sessions_per_gpu: int = 1, python: str = sys.executable) -> list[Program]:
-    """One `mxdesk serve` process per GPU; with sessions_per_gpu K > 1 that process serves K
-    sessions (`--sessions K`, ports base + K*gpu ..), so a node is not capped by a per-GPU
-    process limit and the sessions share one HIP context."""
+                     sessions_per_gpu: int = 1, python: str = sys.executable,
+                     sessions_per_process: int = SESSIONS_PER_PROCESS) -> list[Program]:
+    """`mxdesk serve` processes for every GPU: K sessions per GPU on ports base + K*gpu .., split
+    over ceil(K / sessions_per_process) processes of that GPU (each `--sessions n`, one HIP context
+    and one event loop), so a node is capped neither by a per-GPU process limit nor by one event
+    loop's serving rate."""
     progs = []
     k = max(1, sessions_per_gpu)
+    per = max(1, sessions_per_process)
+    nproc = (k + per - 1) // per
     for gpu in range(n_gpus):
         port = base_port + k * gpu
-        env = {"HIP_VISIBLE_DEVICES": str(gpu), "MXDESK_GPU": "0", "SELKIES_PORT": str(port),
-               "MXDESK_SESSION": str(gpu)}
-        cmd = [python, "-m", "mxdesk", "serve", "--port", str(port)]
-        if k > 1:
-            cmd += ["--sessions", str(k)]
-        progs.append(Program(name=f"gpu{gpu}" + (f"-x{k}" if k > 1 else ""), command=cmd + list(extra_args or []),
-                             priority=10 + gpu, environment=env, ready=Ready("tcp", f"127.0.0.1:{port}", 120.0),
-                             wait_ready=False, startsecs=2.0, startretries=5))
+        for j in range(nproc):
+            n = k // nproc + (1 if j < k % nproc else 0)
+            env = {"HIP_VISIBLE_DEVICES": str(gpu), "MXDESK_GPU": "0", "SELKIES_PORT": str(port),
+                   "MXDESK_SESSION": str(gpu) if nproc == 1 else f"{gpu}.{j}"}
+            cmd = [python, "-m", "mxdesk", "serve", "--port", str(port)]
+            if k > 1:
+                cmd += ["--sessions", str(n)]
+            name = f"gpu{gpu}" + (f"-x{k}" if k > 1 else "") + (f"-p{j}" if nproc > 1 else "")
+            progs.append(Program(name=name, command=cmd + list(extra_args or []), priority=10 + gpu,
+                                 environment=env, ready=Ready("tcp", f"127.0.0.1:{port}", 120.0),
+                                 wait_ready=False, startsecs=2.0, startretries=5))
+            port += n
     return progs
 
 

@@ -59,6 +59,11 @@ def test_session_programs_pin_one_gpu_each():
     single = session_programs(2, base_port=9000)
     assert [p.environment["SELKIES_PORT"] for p in single] == ["9000", "9001"]
     assert all("--sessions" not in p.command for p in single)
+    # more sessions than one event loop serves: split over processes of the same GPU
+    many = session_programs(2, base_port=9000, sessions_per_gpu=40, sessions_per_process=16)
+    assert len(many) == 6 and [p.environment["HIP_VISIBLE_DEVICES"] for p in many] == ["0"] * 3 + ["1"] * 3
+    assert [p.environment["SELKIES_PORT"] for p in many] == ["9000", "9014", "9027", "9040", "9054", "9067"]
+    assert [int(p.command[-1]) for p in many] == [14, 13, 13, 14, 13, 13]
 
 
 def test_serve_sessions_streams_k_sessions_from_one_process(native, monkeypatch):

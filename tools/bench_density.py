@@ -81,7 +81,7 @@ def _client_proc(ports, frames, q):
     q.put(asyncio.run(main()))
 
 
-def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1):
+def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir=""):
     import multiprocessing as mp
 
     base = _free_port_block(k)
@@ -93,9 +93,15 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1):
     n_srv = max(1, min(server_procs, k))
     split = [k // n_srv + (1 if i < k % n_srv else 0) for i in range(n_srv)]
     srvs, at = [], base
-    for n in split:
+    logs = []
+    for j, n in enumerate(split):
+        out = subprocess.DEVNULL
+        if log_dir:
+            Path(log_dir).mkdir(parents=True, exist_ok=True)
+            out = open(Path(log_dir) / f"serve_k{k}_{j}_port{at}.log", "w")
+            logs.append(out)
         srvs.append(subprocess.Popen([sys.executable, "-m", "mxdesk", "serve", "--port", str(at), "--sessions", str(n)],
-                                     cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, text=True))
+                                     cwd=ROOT, env=env, stdout=out, stderr=subprocess.STDOUT, text=True))
         at += n
     try:
         ports = [base + i for i in range(k)]
@@ -119,6 +125,8 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1):
                 srv.wait(timeout=30)
             except subprocess.TimeoutExpired:
                 srv.kill()
+        for f in logs:
+            f.close()
     errs = [r for r in results if "error" in r]
     ok = [r for r in results if "error" not in r]
     lat = sorted(v for r in ok for v in r["lat"])
@@ -128,7 +136,8 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1):
     passed = not errs and len(ok) == k and min(fps) >= 59.5 and p95 < 5.0
     return {"k": k, "passed": passed, "min_fps": round(min(fps), 2) if fps else 0.0,
             "mean_fps": round(statistics.mean(fps), 2) if fps else 0.0, "p50_e2e_ms": round(p50, 3),
-            "p95_e2e_ms": round(p95, 3), "lost_packets": sum(r["lost"] for r in ok), "errors": [e["error"] for e in errs][:3]}
+            "p95_e2e_ms": round(p95, 3), "lost_packets": sum(r["lost"] for r in ok), "errors": [e["error"] for e in errs][:3],
+            "failed_ports": sorted(e["port"] - base for e in errs)}
 
 
 def main():
@@ -140,11 +149,12 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--encoder", default="mxh264enc")
     ap.add_argument("--server-procs", type=int, default=1, help="serve processes sharing the GPU (sessions split evenly)")
+    ap.add_argument("--log-dir", default="", help="write each serve process's output here")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     rows, sustained = [], 0
-    for k in (int(v) for v in a.sweep.split(",")):
-        r = run_k(k, a.frames, a.per_proc, a.width, a.height, a.encoder, a.server_procs)
+    for k in (int(v) for v in a.sweep.replace("+", ",").split(",")):
+        r = run_k(k, a.frames, a.per_proc, a.width, a.height, a.encoder, a.server_procs, a.log_dir)
         r["server_procs"] = min(a.server_procs, k)
         rows.append(r)
         print(json.dumps(r), flush=True)
