@@ -490,21 +490,17 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
 PartitionPool::PartitionPool(int n) {
     for (int i = 0; i < n; ++i)
         th_.emplace_back([this]() {
-            uint64_t seen = 0;
             std::unique_lock<std::mutex> lk(mu_);
             for (;;) {
-                cv_.wait(lk, [&] { return stop_ || (gen_ != seen && next_ < total_); });
+                cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
                 if (stop_) return;
-                if (next_ >= total_) {
-                    seen = gen_;
-                    continue;
-                }
-                const int k = next_++;
-                const std::function<void(int)>* fn = job_;
+                Job* j = jobs_.front();  // the oldest job with tasks left
+                const int k = j->next++;
+                if (j->next >= j->total) jobs_.pop_front();
                 lk.unlock();
-                (*fn)(k);
+                (*j->fn)(k);
                 lk.lock();
-                if (++finished_ == total_) done_cv_.notify_all();
+                if (++j->finished == j->total) done_cv_.notify_all();
             }
         });
 }
@@ -523,23 +519,21 @@ void PartitionPool::run(int n, const std::function<void(int)>& fn) {
         for (int k = 0; k < n; ++k) fn(k);
         return;
     }
+    Job j;
+    j.fn = &fn;
+    j.total = n;
     std::unique_lock<std::mutex> lk(mu_);
-    job_ = &fn;
-    next_ = 0;
-    total_ = n;
-    finished_ = 0;
-    ++gen_;
+    jobs_.push_back(&j);
     cv_.notify_all();
-    while (next_ < total_) {  // the caller takes jobs too (it is awake already)
-        const int k = next_++;
+    while (j.next < j.total) {  // the caller works on its own job too (it is awake already)
+        const int k = j.next++;
+        if (j.next >= j.total) jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &j));
         lk.unlock();
         fn(k);
         lk.lock();
-        ++finished_;
+        ++j.finished;
     }
-    done_cv_.wait(lk, [&] { return finished_ == total_; });
-    job_ = nullptr;
-    total_ = 0;
+    done_cv_.wait(lk, [&] { return j.finished == j.total; });
 }
 
 }  // namespace vp8

@@ -97,17 +97,26 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                         cp[1][y * 8 + x] = pred_px(m.uvmode, ev, 8, x, y, dv);
                     }
             } else {
-                int mvx = 0, mvy = 0;  // quarter samples; full-sample search
-                h264::me_search_cpu(sy, pitch, fy, cw_, ch_, x0, y0, qp, cfg_.search_range, 0, &mvx, &mvy,
-                                    cfg_.me_coarse);
+                int mvx = 0, mvy = 0;  // quarter samples (full samples without subpel)
+                h264::me_search_cpu(sy, pitch, fy, cw_, ch_, x0, y0, qp, cfg_.search_range, cfg_.subpel ? 1 : 0, &mvx,
+                                    &mvy, cfg_.me_coarse);
+                if (!cfg_.subpel) {  // the full-sample search's vector, as k_vp8_inter reads it
+                    mvx = (mvx / 4) * 4;
+                    mvy = (mvy / 4) * 4;
+                }
                 int lo_x, hi_x, lo_y, hi_y;
                 mv_bounds(mb_w_, mb_h_, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
-                const int ix = std::clamp(mvx / 4, lo_x, hi_x), iy = std::clamp(mvy / 4, lo_y, hi_y);
+                int vx, vy;
+                inter_vector(mvx, mvy, lo_x, hi_x, lo_y, hi_y, &vx, &vy);
                 m.ymode = kInter;
-                m.mvx = (int16_t)(ix * 8);
-                m.mvy = (int16_t)(iy * 8);
+                m.mvx = (int16_t)vx;
+                m.mvy = (int16_t)vy;
+                const int ix = vx >> 3, iy = vy >> 3;
+                auto at_y = [&](int xx, int yy) { return (int)h264::ref_px(fy, cw_, cw_, ch_, xx, yy); };
                 for (int y = 0; y < 16; ++y)
-                    for (int x = 0; x < 16; ++x) pred[y * 16 + x] = h264::ref_px(fy, cw_, cw_, ch_, x0 + x + ix, y0 + y + iy);
+                    for (int x = 0; x < 16; ++x)
+                        pred[y * 16 + x] = ((vx | vy) & 7) == 0 ? at_y(x0 + x + ix, y0 + y + iy)
+                                                                 : sixtap_px(at_y, x0 + x + ix, y0 + y + iy, vx & 7, vy & 7);
                 // chroma: the luma vector halved, in 1/8 chroma samples (odd full-sample luma
                 // vectors land on the half-sample six-tap phase)
                 const int cvx = chroma_mv(m.mvx), cvy = chroma_mv(m.mvy);
@@ -129,13 +138,13 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                     for (int x = 0; x < 8; ++x)
                         cres[c][y * 8 + x] = suv[(y0 / 2 + y) * pitch + x0 + 2 * x + c] - cp[c][y * 8 + x];
             if (!key && cfg_.aq >= 3) {  // temporal class of the macroblock -> its segment (quantiser)
-                const int ix = m.mvx / 8, iy = m.mvy / 8;
+                const int ix = m.mvx >> 3, iy = m.mvy >> 3;
                 uint32_t tsad = 0;
                 for (int y = 0; y < 16; ++y)
                     for (int x = 0; x < 16; ++x)
                         tsad += (uint32_t)std::abs((int)sy[(y0 + y) * pitch + x0 + x] -
                                                    h264::ref_px(prev_src_.data(), cw_, cw_, ch_, x0 + x + ix, y0 + y + iy));
-                m.seg = (uint8_t)seg_of_tclass(h264::temporal_class(tsad, ix == 0 && iy == 0));
+                m.seg = (uint8_t)seg_of_tclass(h264::temporal_class(tsad, m.mvx == 0 && m.mvy == 0));
             }
             const Quant Qm = m.seg ? quant_of(seg_qindex_[m.seg]) : (key ? Q : quant_of(seg_qindex_[0]));
             m.nz = code_luma16(res, pred, Qm, lv, rec);

@@ -128,6 +128,14 @@ MXV8 void mv_bounds(int mb_w, int mb_h, int mbx, int mby, int* lo_x, int* hi_x, 
     *hi_y = (mb_h - 1 - mby) * 16 + 16 - 3;
 }
 
+// The inter vector of a macroblock in 1/8 samples from the motion search's quarter-sample vector
+// (luma vectors are quarter-sample in VP8: even 1/8 phases), clamped to mv_bounds.
+MXV8 void inter_vector(int qx, int qy, int lo_x, int hi_x, int lo_y, int hi_y, int* mvx, int* mvy) {
+    const int vx = 2 * qx, vy = 2 * qy;
+    *mvx = vx < 8 * lo_x ? 8 * lo_x : (vx > 8 * hi_x ? 8 * hi_x : vx);
+    *mvy = vy < 8 * lo_y ? 8 * lo_y : (vy > 8 * hi_y ? 8 * hi_y : vy);
+}
+
 // Rate-distortion residual drop of noise-like inter macroblocks (the rule of the H.264 encoder's
 // aq 2, h264_mb.h drop_residual): a macroblock whose prediction residual stays above 32 per luma
 // sample on average keeps its residual only if coding it lowers the luma SSE by more than
@@ -145,15 +153,19 @@ class PartitionPool {
    public:
     explicit PartitionPool(int n);
     ~PartitionPool();
+    // Run fn(0 .. n-1) on the pool and the calling thread; several callers (the frame slots'
+    // writer threads) may run jobs at once -- their tasks queue in call order on the shared threads.
     void run(int n, const std::function<void(int)>& fn);
 
    private:
+    struct Job {
+        const std::function<void(int)>* fn = nullptr;
+        int next = 0, total = 0, finished = 0;
+    };
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    const std::function<void(int)>* job_ = nullptr;
-    int next_ = 0, total_ = 0, finished_ = 0;
-    uint64_t gen_ = 0;
+    std::deque<Job*> jobs_;  // jobs with tasks not yet taken
     bool stop_ = false;
 };
 
@@ -228,7 +240,10 @@ struct Vp8DeviceBuffers {
     h264::DeviceBuffers me;  // shared H.264 motion search (fs = &st->me, mb = vectors)
 };
 // P frames: pad the reference, shared integer motion search, then one wave per macroblock.
-void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y,
+// hp_planes: the four padded F / H / V / J planes (h264::launch_hpel) when the motion search refines
+// to quarter samples (EncoderConfig::subpel), else hp_planes[0] only (the padded full-sample plane)
+void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_t* const hp_planes[4], int hp_pitch,
+                      bool subpel, const uint8_t* src_y,
                       const uint8_t* src_uv, hipStream_t stream);
 // Key frames: one wave per macroblock row, rows handing their bottom edges down (wavefront).
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
@@ -264,9 +279,10 @@ class GpuVp8Encoder final : public VideoEncoder {
     const Vp8Mb* last_mb_info() const { return last_mb_; }
 
    private:
-    // Each frame slot has a writer thread (and its own partition pool): it waits for the slot's
-    // GPU work and writes the frame's bitstream at once, so with two frames in flight both frames'
-    // bitstreams are written concurrently; collect() only waits for the writer of the oldest.
+    // Each frame slot has a writer thread: it waits for the slot's GPU work and writes the frame's
+    // bitstream at once, so with several frames in flight their bitstreams are written concurrently;
+    // collect() only waits for the writer of the oldest.  The writers' token partitions share one
+    // pool (pool_), sized to the machine, not one per slot.
     struct Slot {
         Vp8DeviceBuffers buf{};
         Vp8States* st_host = nullptr;  // pinned: copied to buf.st at the start of the frame
@@ -278,7 +294,6 @@ class GpuVp8Encoder final : public VideoEncoder {
         long long fidx = 0;  // frame index (statistics parity)
         // writer (job / ready under wmu_)
         std::thread writer;
-        std::unique_ptr<PartitionPool> pool;
         bool job = false, ready = false, timeout = false;
         std::exception_ptr err;
         std::vector<uint8_t> au;
@@ -288,6 +303,7 @@ class GpuVp8Encoder final : public VideoEncoder {
         double wt_us = 0;  // writer time (MXDESK_HOST_TIMING report)
         long long wt_n = 0;
     };
+    std::unique_ptr<PartitionPool> pool_;
     void writer_loop(Slot& s);
     void alloc_slot(Slot& s);
     void free_slot(Slot& s);
@@ -307,6 +323,7 @@ class GpuVp8Encoder final : public VideoEncoder {
     hipEvent_t last_done_ = nullptr;
     const Vp8Mb* last_mb_ = nullptr;
     uint8_t* hp_ = nullptr;  // padded full-sample reference
+    uint8_t* hp_sub_[3] = {nullptr, nullptr, nullptr};  // subpel: the padded H / V / J half-sample planes
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};

@@ -28,7 +28,7 @@ namespace vp8 {
 namespace {
 int pool_threads() {
     const unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::clamp(hc ? hc / 2 : 1u, 1u, 8u);
+    return (int)std::clamp(hc ? hc / 2 : 1u, 1u, 16u);
 }
 int log2_parts_for(int mb_h) { return mb_h >= 8 ? 3 : (mb_h >= 4 ? 2 : (mb_h >= 2 ? 1 : 0)); }
 }  // namespace
@@ -92,15 +92,16 @@ GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
     }
     hp_pitch_ = (geom_.coded_w + 2 * h264::kHpelPad + 255) & ~255;
     HIP_CHECK(hipMalloc(&hp_, (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad)));
+    if (cfg.subpel)
+        for (auto& p : hp_sub_) HIP_CHECK(hipMalloc(&p, (size_t)hp_pitch_ * (geom_.coded_h + 2 * h264::kHpelPad)));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     HIP_CHECK(hipStreamSynchronize(stream_));
     HIP_CHECK(hipGetDevice(&device_));
-    for (int i = 0; i < depth_; ++i) {
-        // the slot writers only overlap across slots: share the machine's pool size among them
-        // (at depth 4 a session otherwise held up to 36 host threads)
-        slots_[i].pool = std::make_unique<PartitionPool>(std::max(1, pool_threads() / depth_));
-        slots_[i].writer = std::thread([this, i]() { writer_loop(slots_[i]); });
-    }
+    // one partition pool for all slot writers (a per-slot pool held up to 36 threads per session at
+    // depth 4; a per-slot share of 8 threads cost 40 % of the single-session rate, 7,014 -> 4,413 fps:
+    // profiles/r05_vp8/NOTES.md)
+    pool_ = std::make_unique<PartitionPool>(pool_threads());
+    for (int i = 0; i < depth_; ++i) slots_[i].writer = std::thread([this, i]() { writer_loop(slots_[i]); });
 }
 
 void GpuVp8Encoder::writer_loop(Slot& s) {
@@ -166,6 +167,8 @@ GpuVp8Encoder::~GpuVp8Encoder() {
         if (src_keep_[i]) (void)hipFree(src_keep_[i]);
     }
     (void)hipFree(hp_);
+    for (auto p : hp_sub_)
+        if (p) (void)hipFree(p);
     for (int i = 0; i < depth_; ++i) free_slot(slots_[i]);
 }
 
@@ -207,9 +210,12 @@ void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
     m.qp = qp;
     m.search_range = h264::me_range(cfg_.search_range);
     m.me_coarse = cfg_.me_coarse;
-    m.subpel = 0;  // VP8 vectors here are full-sample
+    m.subpel = cfg_.subpel ? 1 : 0;  // quarter-sample vectors (VP8 luma precision), six-tap prediction
     m.hp_pitch = hp_pitch_;
-    m.hp_f = m.hp_h = m.hp_v = m.hp_j = hp_ + org;
+    m.hp_f = hp_ + org;
+    m.hp_h = (cfg_.subpel ? hp_sub_[0] : hp_) + org;
+    m.hp_v = (cfg_.subpel ? hp_sub_[1] : hp_) + org;
+    m.hp_j = (cfg_.subpel ? hp_sub_[2] : hp_) + org;
 }
 
 void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* src_uv) {
@@ -218,7 +224,10 @@ void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* 
     if (key)
         launch_vp8_key(geom_, s.buf, src_y, src_uv, stream_, cfg_.aq >= 3);
     else
-        launch_vp8_inter(geom_, s.buf, src_y, src_uv, stream_);
+    {
+        uint8_t* const planes[4] = {hp_, hp_sub_[0], hp_sub_[1], hp_sub_[2]};
+        launch_vp8_inter(geom_, s.buf, planes, hp_pitch_, cfg_.subpel != 0, src_y, src_uv, stream_);
+    }
     launch_vp8_gather(geom_, s.buf, stream_);
     HIP_CHECK(hipGetLastError());
 }
@@ -238,7 +247,7 @@ void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out, bool pr
     fd.segmented = s.segmented;
     for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = s.seg_qindex[k];
     write_frame(fd, mbs, [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
-                [&](int n, const std::function<void(int)>& fn) { s.pool->run(n, fn); },
+                [&](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); },
                 probe ? nullptr : &tok_stats_[s.key ? 1 : 0][s.fidx % kStatsLag]);
 }
 

@@ -340,13 +340,28 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
     int lo_x, hi_x, lo_y, hi_y;
     mv_bounds(g.mb_w, g.mb_h, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
-    const int ix = min(max(me[mbi].mvx / 4, lo_x), hi_x), iy = min(max(me[mbi].mvy / 4, lo_y), hi_y);
+    // the search's quarter-sample vector (full samples without subpel) in VP8's 1/8-sample units,
+    // kept inside the range the decoder never clamps (inter_vector, as the CPU encoder)
+    int mvx, mvy;
+    inter_vector(me[mbi].mvx, me[mbi].mvy, lo_x, hi_x, lo_y, hi_y, &mvx, &mvy);
+    mvx = __builtin_amdgcn_readfirstlane(mvx);
+    mvy = __builtin_amdgcn_readfirstlane(mvy);
+    const int ix = mvx >> 3, iy = mvy >> 3;
     stage_src(s, g, src_y, src_uv, x0, y0, lane);
-    {  // luma prediction: the padded reference covers every legal vector (mv_bounds)
+    {  // luma prediction: the padded reference covers every legal vector (mv_bounds) and its taps
         const int r = lane >> 2, c4 = (lane & 3) * 4;
-        const uint8_t* p = F.hp_f + (ptrdiff_t)(y0 + r + iy) * F.hp_pitch + x0 + c4 + ix;
+        const uint8_t* base = F.hp_f;
+        const int pitch = F.hp_pitch;
+        if (((mvx | mvy) & 7) == 0) {
+            const uint8_t* p = base + (ptrdiff_t)(y0 + r + iy) * pitch + x0 + c4 + ix;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = p[j];
+            for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = p[j];
+        } else {  // six-tap (18.3), the 2-D filter of sixtap_px with a zero phase's pass skipped
+            auto at = [&](int xx, int yy) { return (int)base[(ptrdiff_t)yy * pitch + xx]; };
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                s.pred[r * 16 + c4 + j] = (uint8_t)chroma_px(at, x0 + c4 + j + ix, y0 + r + iy, mvx & 7, mvy & 7);
+        }
     }
     // temporal class (h264_mb.h temporal_class) -> segment: the source against the previous source
     // displaced by the vector; this macroblock's source becomes the next frame's previous source
@@ -360,9 +375,8 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
             tsad += abs((int)((sw >> (8 * j)) & 0xff) -
                         h264::ref_px(F.prev_src, g.pitch, g.coded_w, g.coded_h, x0 + c4 + j + ix, y0 + r + iy));
         *reinterpret_cast<uint32_t*>(F.save_src + (size_t)(y0 + r) * g.pitch + x0 + c4) = sw;
-        seg = seg_of_tclass(h264::temporal_class((uint32_t)wsum(tsad), ix == 0 && iy == 0));  // wave-uniform
+        seg = seg_of_tclass(h264::temporal_class((uint32_t)wsum(tsad), mvx == 0 && mvy == 0));  // wave-uniform
     }
-    const int mvx = ix * 8, mvy = iy * 8;
     const int cvx = chroma_mv(mvx), cvy = chroma_mv(mvy);
     {
         const int cx = lane & 7, cy = lane >> 3, cw = g.coded_w / 2, ch = g.coded_h / 2;
@@ -637,10 +651,13 @@ __global__ __launch_bounds__(256) void k_vp8_gather(h264::Geometry g, const Vp8M
 
 }  // namespace
 
-void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y,
-                      const uint8_t* src_uv, hipStream_t stream) {
+void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_t* const hp_planes[4], int hp_pitch,
+                      bool subpel, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t stream) {
     const int W = g.coded_w + 2 * h264::kHpelPad, H = g.coded_h + 2 * h264::kHpelPad;
-    hipLaunchKernelGGL(k_vp8_pad, dim3((W / 4 + 255) / 256, H), dim3(256), 0, stream, g, b.st);
+    if (subpel)  // F (the same padded plane k_vp8_pad writes) plus the half-sample planes of the search
+        h264::launch_hpel(g, b.me, hp_planes, hp_pitch, stream);
+    else
+        hipLaunchKernelGGL(k_vp8_pad, dim3((W / 4 + 255) / 256, H), dim3(256), 0, stream, g, b.st);
     h264::launch_me(g, b.me, src_y, stream);
     hipLaunchKernelGGL(k_vp8_inter, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.me.mb, b.mb,
                        b.lv);
