@@ -451,6 +451,13 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
         if (cfg_.aq >= 3)  // the next P picture's previous source (P pictures: k_inter_encode stores it)
             launch_save_src(geom_, sl.buf, src_y, stream_);
     } else {
+        // MXDESK_INPUT_WAIT=early: the capture hand-off waited before k_hpel (next to the previous
+        // frame's analysis_done record) instead of after it -- experiment on queue barrier costs
+        static const bool early = [] {
+            const char* e = std::getenv("MXDESK_INPUT_WAIT");
+            return e && std::string(e) == "early";
+        }();
+        if (early) wait_input();
         if (stream_a_ && hpel_side_ && pub && ref_seq_ + 1 == seq_) {  // the previous picture recorded ref_ready_
             HIP_CHECK(hipStreamWaitEvent(stream_a_, ref_ready_, 0));
             launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_a_, pub);
