@@ -277,6 +277,8 @@ def main() -> None:
     ap.add_argument("--deblock", type=int, default=None,
                     help="in-loop deblocking filter 0 off / 1 on / 2 adaptive per picture (H.264: "
                          "from the picture's temporal classes; default: the encoder's)")
+    ap.add_argument("--hevc-chroma-keep", type=int, default=None,
+                    help="HEVC: changing content keeps its chroma residual (1) instead of dropping it (0)")
     ap.add_argument("--chroma-qp-offset", type=int, default=None,
                     help="chroma QP offset against luma (H.264 chroma_qp_index_offset / HEVC pps_cb/cr_qp_offset; "
                          "default: the encoder's)")
@@ -377,6 +379,8 @@ def main() -> None:
         cfg.enc.hevc_wpp = args.hevc_wpp
     if args.hevc_wpp_rows is not None:
         cfg.enc.hevc_wpp_rows = args.hevc_wpp_rows
+    if args.hevc_chroma_keep is not None:
+        cfg.enc.hevc_chroma_keep = args.hevc_chroma_keep
     if args.chroma_qp_offset is not None:
         cfg.enc.chroma_qp_offset = args.chroma_qp_offset
     if args.intra_in_p is not None:

@@ -242,7 +242,7 @@ void me_search_parts_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int
     }
 }
 
-CpuH264Encoder::CpuH264Encoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
+CpuH264Encoder::CpuH264Encoder(const EncoderConfig& cfg) : cfg_(cfg.with_aq_default(4)), common_(cfg) {
     cw_ = common_.mb_w() * 16;
     ch_ = common_.mb_h() * 16;
     for (int i = 0; i < 2; ++i) {

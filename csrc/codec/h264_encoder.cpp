@@ -301,7 +301,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
 }
 
 GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
-    : cfg_(cfg), common_(cfg), stream_(stream) {
+    : cfg_(cfg.with_aq_default(4)), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
         throw std::invalid_argument("pipeline_depth must be 1 to 4");
     depth_ = cfg.pipeline_depth;

@@ -43,7 +43,7 @@ struct EncoderConfig {
                               // 0: exhaustive +-range search
     int subpel = 1;           // quarter-pel refinement
     int chroma_qp_offset = 0;
-    int aq = 4;               // adaptive quantisation of P macroblocks (mb_qp_delta): 1 coarser QP for
+    int aq = -1;              // adaptive quantisation of P macroblocks (mb_qp_delta): 1 coarser QP for
                               // noise-like residuals, 2 adds their rate-distortion residual drop, 3 temporal
                               // classes of the source -- persistent content 6 QP finer, changing content 6
                               // coarser, its chroma dropped and its luma residual kept only when it pays for
@@ -51,7 +51,8 @@ struct EncoderConfig {
                               // content (identical source, zero vector) 9 / 12 / 15 QP finer -- 4K desktop
                               // +0.6 dB (H.264) / +1.4 dB (HEVC) masked Y-PSNR at equal rate, motion content
                               // unchanged (profiles/r04_hevc/NOTES.md).  HEVC has 0, 1 and 3+, and treats 2
-                              // as 1
+                              // as 1.  -1: the codec's default -- H.264 / VP8 4, HEVC 6 (4K 18 Mbps desktop
+                              // +1.6 dB over aq 4, motion +0.1 dB, profiles/r05_hevc/NOTES.md)
     // in-loop deblocking filter: 1 on, 0 off, 2 adaptive (per picture from its temporal classes,
     // h264_deblock.h db_auto_decide), -1 the codec's default -- HEVC adaptive (8.7.2 is fully
     // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: adaptive filtering switches
@@ -60,6 +61,12 @@ struct EncoderConfig {
     // P pictures: also search 16x8 / 8x16 partitionings (two vectors per macroblock) and take one
     // when its SAD + lambda * vector rate beats the 16x16 vector's
     int partitions = 1;
+    // a copy with aq < 0 resolved to the codec's default (each encoder keeps one as cfg_)
+    EncoderConfig with_aq_default(int def) const {
+        EncoderConfig c = *this;
+        if (c.aq < 0) c.aq = def;
+        return c;
+    }
     bool h264_deblock() const { return deblock > 0; }  // the filter kernels run (on, or adaptive)
     bool h264_deblock_auto() const { return deblock == 2; }
     bool hevc_deblock() const { return deblock != 0; }
@@ -86,6 +93,9 @@ struct EncoderConfig {
     // took ~3 ms of CABAC waves, 8-row slices ~1.4 ms; profiles/r04_hevc)
     int hevc_wpp_rows = 8;
     int sao = 1;              // HEVC: sample adaptive offset (8.7.3), band / edge offsets decided per CTB
+    // HEVC, aq >= 3: changing content (video, animation) keeps its residual, chroma included, coded
+    // at its class QP, instead of the chroma drop and the luma rate-distortion drop
+    int hevc_chroma_keep = 0;
     // quality report: luma distortion outside the macroblocks touching this pixel rectangle
     // (FrameStats::sse_masked; mask_x1 <= mask_x0 = no mask)
     int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;

@@ -378,7 +378,7 @@ uint32_t code_slice_wpp(uint8_t* out, uint32_t cap, bool islice, int slice_qp, c
 }
 
 // ------------------------------------------------------------------ CPU encoder
-CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
+CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg.with_aq_default(6)), common_(cfg) {
     cw_ = common_.ctb_w() * kCtb;
     ch_ = common_.ctb_h() * kCtb;
     for (int i = 0; i < 2; ++i) {
@@ -571,7 +571,7 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                     for (int q = 0; q < 8; ++q) {
                         const int p = chroma_mc(ref_uv, cw_, cw_ / 2, ch_ / 2, comp, xc + q, yc + r, c.mvx, c.mvy);
                         pc[comp][r * 8 + q] = p;
-                        rc[comp][r * 8 + q] = changing ? 0 : suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
+                        rc[comp][r * 8 + q] = (changing && !cfg_.hevc_chroma_keep) ? 0 : suv[(yc + r) * pitch + 2 * (xc + q) + comp] - p;
                     }
             // option 1: one 16x16 luma TU, 8x8 chroma TUs
             int rrc[2][64];
@@ -610,7 +610,7 @@ void CpuHevcEncoder::analyse_inter(const uint8_t* sy, const uint8_t* suv, int pi
                     std::memcpy(rrc, rrc2, sizeof rrc2);
                 }
             }
-            if (changing) {
+            if (changing && !cfg_.hevc_chroma_keep) {
                 // rate-distortion residual drop (h264_mb.h drop_luma_for): the luma residual must
                 // lower the distortion by more than lambda * (estimated bits of the chosen tree)
                 long long d_pred = 0, d_coded = 0;

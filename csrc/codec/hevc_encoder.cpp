@@ -91,7 +91,7 @@ void GpuHevcEncoder::free_slot(FrameSlot& sl) {
 }
 
 GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
-    : cfg_(cfg), common_(cfg), stream_(stream) {
+    : cfg_(cfg.with_aq_default(6)), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
         throw std::invalid_argument("pipeline_depth must be 1, 2 or 3");
     if (2 * common_.slice_rows() > kMaxSliceRows) throw std::invalid_argument("hevc: too many CTB rows per slice");
@@ -177,6 +177,8 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.sao = (cfg_.sao && !probe) ? 1 : 0;
     f.deblock_on = cfg_.hevc_deblock() ? 1 : 0;  // adaptive: k_hevc_db_auto overwrites it on the device
     f.deblock_auto = cfg_.hevc_deblock_auto() ? 1 : 0;
+    f.chroma_keep = cfg_.hevc_chroma_keep ? 1 : 0;
+    f.pad3_ = 0;
     f.rec_y = f.sao ? pre_y_ : rec_y_[cur];
     f.rec_uv = f.sao ? pre_uv_ : rec_uv_[cur];
     f.sao_y = rec_y_[cur];

@@ -181,6 +181,8 @@ struct HevcFrameState {
     uint64_t bl_safe;
     int32_t depth_inter;  // max_transform_hierarchy_depth_inter of the SPS
     int32_t deblock_auto;  // EncoderConfig::deblock 2: k_hevc_db_auto decides deblock_on (h264_deblock.h rule)
+    int32_t chroma_keep;   // EncoderConfig::hevc_chroma_keep: changing content keeps its chroma residual
+    int32_t pad3_;
 };
 
 struct HevcOutHeader {

@@ -910,7 +910,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     // changing content (aq 3): chroma residual dropped, luma kept only if it pays for its bits
     const bool changing = fs->aq >= 3 && tcls == h264::kTcChanging;
-    if (changing && valid) {
+    const bool cdrop = changing && !fs->chroma_keep;  // wave-uniform
+    if (cdrop && valid) {
         const int rc = lane >> 3, cc = lane & 7;
         for (int comp = 0; comp < 2; ++comp) t.res[256 + comp * 64 + rc * 8 + cc] = 0;
     }
@@ -968,7 +969,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     // rate-distortion residual drop of changing content (h264_mb.h drop_luma_for): the luma
     // residual must lower the distortion by more than lambda * (estimated bits)
     const long long d_pred = wsum(dpf);
-    const bool drop = changing && valid &&
+    const bool drop = cdrop && valid &&
                       d_pred - (long long)(split ? r2.sse_y_full : r.sse_y_full) <
                           (long long)h264::lambda_sse(qp) * (long long)(split ? r2.bits_y : r.bits_y);  // wave-uniform
     const int dp_disp = wsum(dpm);
@@ -980,8 +981,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(Geometry g, const HevcFrameS
     }
     if (lane == 0) {
         part[0][wave] = valid ? (unsigned long long)(drop ? dp_disp : (split ? sse2y : r.sse[0])) : 0ull;
-        part[1][wave] = valid ? (unsigned long long)(changing ? dcp_u : (split ? sse2u : r.sse[1])) : 0ull;
-        part[2][wave] = valid ? (unsigned long long)(changing ? dcp_v : (split ? sse2v : r.sse[2])) : 0ull;
+        part[1][wave] = valid ? (unsigned long long)(cdrop ? dcp_u : (split ? sse2u : r.sse[1])) : 0ull;
+        part[2][wave] = valid ? (unsigned long long)(cdrop ? dcp_v : (split ? sse2v : r.sse[2])) : 0ull;
     }
     SplitSummary ss = {};
     if (split) ss = split_summary_wave(lv2[wave], lane, tu4);  // wave-uniform branch

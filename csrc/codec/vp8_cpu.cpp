@@ -31,7 +31,7 @@ Edge edge_of(const uint8_t* p, int pitch, int step, int comp, int x0, int y0, in
 
 }  // namespace
 
-CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg) : cfg_(cfg), common_(cfg) {
+CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg) : cfg_(cfg.with_aq_default(4)), common_(cfg) {
     mb_w_ = common_.mb_w();
     mb_h_ = common_.mb_h();
     cw_ = mb_w_ * 16;

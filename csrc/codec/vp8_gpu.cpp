@@ -65,7 +65,7 @@ void GpuVp8Encoder::free_slot(Slot& s) {
 }
 
 GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
-    : cfg_(cfg), common_(cfg), stream_(stream) {
+    : cfg_(cfg.with_aq_default(4)), common_(cfg), stream_(stream) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
         throw std::invalid_argument("pipeline_depth must be 1 to 4");
     if (cfg.width > 16383 || cfg.height > 16383) throw std::invalid_argument("vp8: picture larger than 16383");
@@ -85,7 +85,7 @@ GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipMalloc(&rec_uv_[i], uvsz));
         HIP_CHECK(hipMemsetAsync(rec_y_[i], 0, ysz, stream_));
         HIP_CHECK(hipMemsetAsync(rec_uv_[i], 128, uvsz, stream_));
-        if (cfg.aq >= 3) {
+        if (cfg_.aq >= 3) {
             HIP_CHECK(hipMalloc(&src_keep_[i], ysz));
             HIP_CHECK(hipMemsetAsync(src_keep_[i], 0, ysz, stream_));
         }
