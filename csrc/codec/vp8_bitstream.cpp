@@ -313,14 +313,24 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                 e.literal((uint32_t)f.seg_qindex[k], 7);
                 e.literal(0, 1);  // sign
             }
-            for (int k = 0; k < kNumSegs; ++k) e.literal(0, 1);  // no loop-filter level updates
+            for (int k = 0; k < kNumSegs; ++k) {  // loop-filter level: the segment's (absolute)
+                e.literal(f.lf_level[k] != 0, 1);
+                if (f.lf_level[k]) {
+                    e.literal((uint32_t)f.lf_level[k], 6);
+                    e.literal(0, 1);  // sign
+                }
+            }
             for (int k = 0; k < 3; ++k) {  // segment tree probabilities
                 e.literal(1, 1);
                 e.literal((uint32_t)seg_p[k], 8);
             }
         }
+        // the frame level only switches the filter on (segmented frames: each segment's own level)
+        int frame_level = f.lf_level[0];
+        if (f.segmented)
+            for (int k = 1; k < kNumSegs; ++k) frame_level = std::max(frame_level, f.lf_level[k]);
         e.literal(0, 1);  // filter_type (normal)
-        e.literal(0, 6);  // loop_filter_level 0: no loop filter
+        e.literal((uint32_t)frame_level, 6);  // loop_filter_level (0: no loop filter)
         e.literal(0, 3);  // sharpness_level
         e.literal(0, 1);  // loop_filter_adj_enable
         e.literal((uint32_t)f.log2_parts, 2);

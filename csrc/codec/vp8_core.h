@@ -9,11 +9,12 @@
 //
 // Coding subset (what this encoder emits): key frames of 16x16-predicted macroblocks (DC / V / H /
 // TM luma, DC / V / H / TM chroma, Y2 second-order block); inter frames of 16x16 inter macroblocks
-// predicting from the last frame with full-sample vectors (ZEROMV / NEARESTMV / NEARMV / NEWMV);
+// predicting from the last frame with quarter-sample vectors (ZEROMV / NEARESTMV / NEARMV / NEWMV);
 // inter frames segmented (9.3) by the temporal classes of the H.264 encoder's adaptive
 // quantisation -- four segment quantisers, a per-macroblock segment map -- key frames one
-// quantiser; loop filter level 0; token partitions by MB row; coefficient probabilities updated per
-// frame from the token statistics of frame n - kStatsLag (vp8_encoder.h).
+// quantiser; the normal loop filter with per-segment levels (section 15; adaptive by default:
+// on for coherent motion, vp8_encoder.h LfDecision); token partitions by MB row; coefficient
+// probabilities updated per frame from the token statistics of frame n - kStatsLag (vp8_encoder.h).
 #pragma once
 #include <stdint.h>
 
@@ -35,7 +36,7 @@ enum MvMode : uint8_t { kMvZero = 0, kMvNearest = 1, kMvNear = 2, kMvNew = 3 };
 
 // Per-macroblock record written by the analysis (GPU or CPU), read by the bitstream writer.
 struct Vp8Mb {
-    int16_t mvx, mvy;  // luma vector, 1/8-sample units (always a multiple of 8 here: full samples)
+    int16_t mvx, mvy;  // luma vector, 1/8-sample units (even: quarter-sample luma vectors)
     uint8_t ymode;     // YMode
     uint8_t uvmode;    // DC / V / H / TM
     uint8_t seg;       // segment (Seg; 0 in key frames)
@@ -283,6 +284,126 @@ MXV8 int sixtap_px(const F& at, int x, int y, int fx, int fy) {
 // Chroma vector (1/8 chroma samples) of a 16x16 luma vector in 1/8 luma samples (18.4):
 // halved, rounded away from zero.
 MXV8 int chroma_mv(int v) { return (v + (v < 0 ? -1 : 1)) / 2; }
+
+// ---------------------------------------------------------------- loop filter (15)
+// The normal filter (filter_type 0, sharpness 0, no mode / reference level deltas): per
+// macroblock a level from its segment; macroblock edges take the wide filter (15.3 MB edges),
+// the inner 4x4 edges (only in macroblocks with a non-zero coefficient -- all 16x16-predicted
+// here) the subblock filter.  Arithmetic as libvpx's C reference (the RFC's normative source):
+// the edge test 2|p0-q0| + |p1-q1|/2 <= limit, interior |p_i - p_i+1| <= interior limit, high
+// edge variance |p1-p0| or |q1-q0| above the frame-type threshold.
+struct LfParams {
+    int mblim, blim, lim, hev;  // MB-edge / subblock-edge limits, interior limit, hev threshold
+};
+MXV8 LfParams lf_params(int level, bool key) {
+    LfParams f;
+    f.lim = level < 1 ? 1 : level;  // interior limit (sharpness 0)
+    f.mblim = (level + 2) * 2 + f.lim;
+    f.blim = level * 2 + f.lim;
+    f.hev = key ? (level >= 40 ? 2 : (level >= 15 ? 1 : 0)) : (level >= 40 ? 3 : (level >= 20 ? 2 : (level >= 15 ? 1 : 0)));
+    return f;
+}
+MXV8 int lf_s8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+MXV8 int lf_abs(int v) { return v < 0 ? -v : v; }
+// p[0..7] = p3 p2 p1 p0 q0 q1 q2 q3 across the edge
+MXV8 bool lf_mask(const int* p, int lim, int elim) {
+    return lf_abs(p[3] - p[4]) * 2 + (lf_abs(p[2] - p[5]) >> 1) <= elim && lf_abs(p[0] - p[1]) <= lim &&
+           lf_abs(p[1] - p[2]) <= lim && lf_abs(p[2] - p[3]) <= lim && lf_abs(p[7] - p[6]) <= lim &&
+           lf_abs(p[6] - p[5]) <= lim && lf_abs(p[5] - p[4]) <= lim;
+}
+// macroblock edge: p2 .. q2 change (without high edge variance; else p0 / q0 as the subblock filter)
+MXV8 void lf_mb_edge(int* p, const LfParams& f) {
+    if (!lf_mask(p, f.lim, f.mblim)) return;
+    const int ps2 = p[1] - 128, ps1 = p[2] - 128, ps0 = p[3] - 128, qs0 = p[4] - 128, qs1 = p[5] - 128, qs2 = p[6] - 128;
+    const bool hev = lf_abs(p[2] - p[3]) > f.hev || lf_abs(p[5] - p[4]) > f.hev;
+    const int w = lf_s8(lf_s8(ps1 - qs1) + 3 * (qs0 - ps0));
+    if (hev) {
+        p[4] = lf_s8(qs0 - (lf_s8(w + 4) >> 3)) + 128;
+        p[3] = lf_s8(ps0 + (lf_s8(w + 3) >> 3)) + 128;
+        return;
+    }
+    int a = lf_s8((27 * w + 63) >> 7);
+    p[4] = lf_s8(qs0 - a) + 128;
+    p[3] = lf_s8(ps0 + a) + 128;
+    a = lf_s8((18 * w + 63) >> 7);
+    p[5] = lf_s8(qs1 - a) + 128;
+    p[2] = lf_s8(ps1 + a) + 128;
+    a = lf_s8((9 * w + 63) >> 7);
+    p[6] = lf_s8(qs2 - a) + 128;
+    p[1] = lf_s8(ps2 + a) + 128;
+}
+// subblock edge: p1 .. q1 change (p0 / q0 only with high edge variance)
+MXV8 void lf_sub_edge(int* p, const LfParams& f) {
+    if (!lf_mask(p, f.lim, f.blim)) return;
+    const int ps1 = p[2] - 128, ps0 = p[3] - 128, qs0 = p[4] - 128, qs1 = p[5] - 128;
+    const bool hev = lf_abs(p[2] - p[3]) > f.hev || lf_abs(p[5] - p[4]) > f.hev;
+    const int a = lf_s8((hev ? lf_s8(ps1 - qs1) : 0) + 3 * (qs0 - ps0));
+    const int f1 = lf_s8(a + 4) >> 3, f2 = lf_s8(a + 3) >> 3;
+    p[4] = lf_s8(qs0 - f1) + 128;
+    p[3] = lf_s8(ps0 + f2) + 128;
+    if (!hev) {
+        const int o = (f1 + 1) >> 1;
+        p[5] = lf_s8(qs1 - o) + 128;
+        p[2] = lf_s8(ps1 + o) + 128;
+    }
+}
+// Level of a segment coded at quantiser index q (libvpx's encoder searches it per frame; a fixed
+// map here): num / 16 of the index, at most 63.
+MXV8 int lf_level_for(int q, int num) {
+    const int l = (q * num) >> 4;
+    return l > 63 ? 63 : (l < 0 ? 0 : l);
+}
+constexpr int kLfNumDefault = 5;
+
+// One plane of one macroblock (n x n samples at (x0, y0); `step` 1 for luma, 2 for a component of
+// interleaved chroma): left edge, inner vertical edges, top edge, inner horizontal edges (15.1).
+inline void lf_plane_mb(uint8_t* base, int step, int pitch, int x0, int y0, int n, bool left, bool top, bool inner,
+                        const LfParams& f) {
+    auto at = [&](int x, int y) -> uint8_t& { return base[(size_t)y * pitch + (size_t)x * step]; };
+    int p[8];
+    auto vedge = [&](int xe, bool mb) {
+        for (int r = 0; r < n; ++r) {
+            for (int k = 0; k < 8; ++k) p[k] = at(xe - 4 + k, y0 + r);
+            if (mb)
+                lf_mb_edge(p, f);
+            else
+                lf_sub_edge(p, f);
+            for (int k = 1; k < 7; ++k) at(xe - 4 + k, y0 + r) = (uint8_t)p[k];
+        }
+    };
+    auto hedge = [&](int ye, bool mb) {
+        for (int c = 0; c < n; ++c) {
+            for (int k = 0; k < 8; ++k) p[k] = at(x0 + c, ye - 4 + k);
+            if (mb)
+                lf_mb_edge(p, f);
+            else
+                lf_sub_edge(p, f);
+            for (int k = 1; k < 7; ++k) at(x0 + c, ye - 4 + k) = (uint8_t)p[k];
+        }
+    };
+    if (left) vedge(x0, true);
+    if (inner)
+        for (int e = 4; e < n; e += 4) vedge(x0 + e, false);
+    if (top) hedge(y0, true);
+    if (inner)
+        for (int e = 4; e < n; e += 4) hedge(y0 + e, false);
+}
+// The whole reconstructed frame in place, macroblocks in raster order (the serial reference of
+// k_vp8_lf): level levels[segment] (0: the macroblock is not filtered), inner edges where the
+// macroblock has a non-zero coefficient.  y / uv (interleaved chroma) `pitch` wide.
+inline void loop_filter_frame(uint8_t* y, uint8_t* uv, int pitch, int mb_w, int mb_h, const Vp8Mb* mbs,
+                              const int* levels, bool key) {
+    for (int mby = 0; mby < mb_h; ++mby)
+        for (int mbx = 0; mbx < mb_w; ++mbx) {
+            const Vp8Mb& m = mbs[mby * mb_w + mbx];
+            const int level = levels[m.seg & 3];
+            if (!level) continue;
+            const LfParams f = lf_params(level, key);
+            const bool inner = m.nz != 0;
+            lf_plane_mb(y, 1, pitch, mbx * 16, mby * 16, 16, mbx > 0, mby > 0, inner, f);
+            for (int c = 0; c < 2; ++c) lf_plane_mb(uv + c, 2, pitch, mbx * 8, mby * 8, 8, mbx > 0, mby > 0, inner, f);
+        }
+}
 
 // ---------------------------------------------------------------- macroblock coding (shared)
 // Quantise + reconstruct the 16 luma blocks of a macroblock with a second-order Y2 block.

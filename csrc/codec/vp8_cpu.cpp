@@ -31,7 +31,13 @@ Edge edge_of(const uint8_t* p, int pitch, int step, int comp, int x0, int y0, in
 
 }  // namespace
 
-CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg) : cfg_(cfg.with_aq_default(4)), common_(cfg) {
+int lf_num_from_env() {
+    const char* e = std::getenv("MXDESK_VP8_LF_NUM");
+    return e && *e ? std::clamp(std::atoi(e), 0, 64) : kLfNumDefault;
+}
+
+CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg)
+    : cfg_(cfg.with_aq_default(4)), common_(cfg), lf_(cfg.vp8_deblock_mode()), lf_num_(lf_num_from_env()) {
     mb_w_ = common_.mb_w();
     mb_h_ = common_.mb_h();
     cw_ = mb_w_ * 16;
@@ -207,7 +213,12 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     for (int k = 0; k < kNumSegs; ++k) seg_qindex_[k] = qindex;
     if (fd.segmented) segment_qindices(common_.cur_qp(), cfg_.aq, seg_qindex_);
     for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = seg_qindex_[k];
+    lf_levels(lf_.decide(frames_, key), fd.segmented, qindex, seg_qindex_, lf_num_, fd.lf_level);
     analyse(y, uv, pitch, key, qindex);
+    // the loop filter over the whole reconstruction (the next frame's reference, the decoder's output)
+    if (fd.lf_level[0] | fd.lf_level[1] | fd.lf_level[2] | fd.lf_level[3])
+        loop_filter_frame(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, mb_w_, mb_h_, mb_.data(), fd.lf_level, key);
+    lf_.record(frames_, key, mb_.data(), mb_w_, mb_h_);
     if (cfg_.aq >= 3) prev_src_.swap(next_src_);
     au_.clear();
     write_frame(fd, mb_.data(), [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, au_,
@@ -220,6 +231,7 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     stats_.qp = common_.cur_qp();
     stats_.bytes = (int)au_.size();
     stats_.skipped_mbs = skipped;
+    stats_.deblocked = (fd.lf_level[0] | fd.lf_level[1] | fd.lf_level[2] | fd.lf_level[3]) != 0;
     common_.end_frame((int)au_.size(), key);
     have_ref_ = true;
     return au_;

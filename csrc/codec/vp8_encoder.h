@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "h264_deblock.h"
 #include "h264_encoder.h"
 #include "h264_mb.h"
 #include "video_encoder.h"
@@ -87,11 +88,21 @@ struct FrameDesc {
     int log2_parts;  // token partitions: 1 << log2_parts
     bool segmented = false;          // inter frames with aq >= 3: segment map + segment quantisers
     int seg_qindex[kNumSegs] = {0, 0, 0, 0};
+    int lf_level[kNumSegs] = {0, 0, 0, 0};  // loop-filter level per segment ([0]: unsegmented); 0 = off
 };
 // Segment quantiser indices of an inter frame at frame QP `qp` (the classes' QPs of aq3_mb_qp).
 inline void segment_qindices(int qp, int aq, int out[kNumSegs]) {
     for (int s = 0; s < kNumSegs; ++s) out[s] = qindex_for_qp(h264::aq3_mb_qp(qp, tclass_of_seg(s), aq));
 }
+
+// Per-segment loop-filter levels of a frame (all zero: the filter is off): from each segment's
+// quantiser (lf_level_for), the static segment (identical source, zero vector) unfiltered.
+inline void lf_levels(bool on, bool segmented, int qindex, const int seg_qindex[kNumSegs], int num, int out[kNumSegs]) {
+    for (int s = 0; s < kNumSegs; ++s)
+        out[s] = !on ? 0 : (!segmented ? lf_level_for(qindex, num) : (s == kSegStatic ? 0 : lf_level_for(seg_qindex[s], num)));
+}
+// lf_level_for's numerator: MXDESK_VP8_LF_NUM (tuning), else kLfNumDefault
+int lf_num_from_env();
 
 // Token branch statistics of the last coded frame of one type (13.4): the coefficient probability
 // updates of the next frame of that type are planned from them, so coding needs no separate
@@ -148,6 +159,47 @@ MXV8 bool vp8_drop_residual(uint32_t lsad, long long d_pred, long long d_coded, 
 }
 MXV8 uint32_t vp8_block_bits(int nz) { return nz ? 2u + 6u * (uint32_t)nz : 0u; }
 
+// Loop-filter decision per frame (EncoderConfig::deblock: 0 off, 1 on, 2 or -1 (the VP8 default)
+// adaptive).  Adaptive is the H.264 encoder's rule (h264_deblock.h db_auto_decide: filter when the
+// moving macroblocks move coherently -- pans, scrolls, video -- not for a still desktop, whose text
+// the filter only blurs) on the vectors of the inter frame kStatsLag frames back: the newest frame
+// whose records the host holds when a frame is prepared at any pipeline depth, so the CPU and GPU
+// encoders decide alike.  A key frame keeps the last decision.
+class LfDecision {
+   public:
+    explicit LfDecision(int mode) : mode_(mode) {}
+    // the decision for frame `fidx`, before it is analysed (called in frame order)
+    bool decide(long long fidx, bool key) {
+        if (mode_ != 2) return on_ = mode_ == 1;
+        const Rec& r = ring_[fidx % kStatsLag];
+        if (!key && r.valid && r.fidx == fidx - kStatsLag) on_ = h264::db_auto_decide(r.c, r.nmb, on_);
+        return on_;
+    }
+    // frame `fidx`'s records, once analysed (any thread; each frame's slot is its own)
+    void record(long long fidx, bool key, const Vp8Mb* mbs, int mb_w, int mb_h) {
+        Rec& r = ring_[fidx % kStatsLag];
+        r.fidx = fidx;
+        r.nmb = mb_w * mb_h;
+        r.c = h264::DbAutoCounts{};
+        r.valid = !key && mode_ == 2;
+        if (!r.valid) return;
+        static_assert(sizeof(Vp8Mb) % sizeof(int16_t) == 0, "Vp8Mb: vector words at its start");
+        const int16_t* mv = reinterpret_cast<const int16_t*>(mbs);
+        for (int i = 0; i < r.nmb; ++i) h264::db_auto_count_mv(mv, (int)(sizeof(Vp8Mb) / sizeof(int16_t)), mb_w, i, r.c);
+    }
+
+   private:
+    struct Rec {
+        long long fidx = -1;
+        int nmb = 0;
+        bool valid = false;
+        h264::DbAutoCounts c;
+    };
+    int mode_;
+    bool on_ = false;
+    Rec ring_[kStatsLag];
+};
+
 // Small persistent worker pool for the token partitions.
 class PartitionPool {
    public:
@@ -196,6 +248,8 @@ class CpuVp8Encoder {
     TokenStats tok_stats_[2][kStatsLag];
     long long frames_ = 0;
     int seg_qindex_[kNumSegs] = {0, 0, 0, 0};
+    LfDecision lf_;
+    int lf_num_ = kLfNumDefault;
     int cur_ = 0;
     bool have_ref_ = false;
     std::vector<Vp8Mb> mb_;
@@ -222,6 +276,7 @@ struct Vp8FrameState {
     int32_t q[kNumSegs][6];   // per segment: Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
     uint32_t qm[kNumSegs][6]; // ceil(2^32 / (3 q)): the dead-zone quantiser's division as a multiply-high
     int32_t drop_lambda;    // P frames: lambda_sse of the frame QP for vp8_drop_residual
+    int32_t lf_level[kNumSegs];  // loop-filter level per segment (k_vp8_lf; all 0: not launched)
 };
 // Both per-frame states in one block: one host->device copy per frame.
 struct Vp8States {
@@ -235,6 +290,8 @@ struct Vp8DeviceBuffers {
     uint32_t* prog;        // [mb_h] key-frame wavefront progress (epoch << 12 | MBs done)
     uint64_t* line;        // [mb_h][coded_w / 4] key-frame hand-off: bottom luma + chroma rows
     int* err;              // mapped host word: nonzero if a wavefront spin timed out
+    unsigned long long* lf_line;  // loop-filter hand-off lines (k_vp8_lf: epoch-tagged, per workgroup) + scratch
+    unsigned long long* lf_sse;  // mapped host [mb_h][3]: Y / U / V distortion of the filtered picture
     Vp8Mb* mb_host;        // mapped host: records with their level slots (k_vp8_gather)
     int16_t* lv_host;      // mapped host: levels of the coded macroblocks, row-compacted
     h264::DeviceBuffers me;  // shared H.264 motion search (fs = &st->me, mb = vectors)
@@ -248,6 +305,9 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_
 // Key frames: one wave per macroblock row, rows handing their bottom edges down (wavefront).
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream, bool save_src);
+// Loop filter of the reconstruction in place (Vp8FrameState::lf_level), its distortion per row.
+void launch_vp8_lf(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                   hipStream_t stream);
 // Records + the coded macroblocks' levels into the mapped host buffers (per-row compaction).
 void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream);
 
@@ -291,6 +351,8 @@ class GpuVp8Encoder final : public VideoEncoder {
         int qp = 0, qindex = 0;
         bool segmented = false;
         int seg_qindex[kNumSegs] = {0, 0, 0, 0};
+        int lf_level[kNumSegs] = {0, 0, 0, 0};  // loop filter (all 0: off)
+        bool lf_on = false;
         long long fidx = 0;  // frame index (statistics parity)
         // writer (job / ready under wmu_)
         std::thread writer;
@@ -329,6 +391,8 @@ class GpuVp8Encoder final : public VideoEncoder {
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     uint8_t* src_keep_[2] = {nullptr, nullptr};  // aq >= 3: source luma of the frames in rec_y_[k]
     TokenStats tok_stats_[2][kStatsLag];          // [key][frame % kStatsLag], as CpuVp8Encoder
+    LfDecision lf_;
+    int lf_num_ = kLfNumDefault;
     long long frames_ = 0;
     int cur_ = 0;
     bool have_ref_ = false;

@@ -42,6 +42,12 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     HIP_CHECK(hipMalloc(&b.prog, sizeof(uint32_t) * (size_t)geom_.mb_h));
     HIP_CHECK(hipMemsetAsync(b.prog, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
     HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * (size_t)geom_.mb_h * (geom_.coded_w / 4)));
+    // hand-off lines: 32 tagged words per macroblock per workgroup of rows, then 1 KB scratch per
+    // row (k_vp8_lf); tags start at 0, never a frame's epoch
+    const size_t lf_bytes = sizeof(uint64_t) * 32 * (size_t)geom_.mb_h * geom_.mb_w + 1024 * (size_t)(geom_.mb_h + 16);
+    HIP_CHECK(hipMalloc(&b.lf_line, lf_bytes));
+    HIP_CHECK(hipMemsetAsync(b.lf_line, 0, lf_bytes, stream_));
+    HIP_CHECK(hipHostMalloc(&b.lf_sse, sizeof(unsigned long long) * 3 * (size_t)geom_.mb_h, hipHostMallocMapped));
     HIP_CHECK(hipHostMalloc(&b.err, sizeof(int), hipHostMallocMapped));
     *b.err = 0;
     HIP_CHECK(hipHostMalloc(&b.mb_host, sizeof(Vp8Mb) * (size_t)nmb, hipHostMallocMapped));
@@ -56,16 +62,20 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
 
 void GpuVp8Encoder::free_slot(Slot& s) {
     Vp8DeviceBuffers& b = s.buf;
-    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.prog, (void*)b.line, (void*)b.me.mb})
+    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.prog, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line})
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)b.err, (void*)b.mb_host, (void*)b.lv_host, (void*)s.st_host})
+    for (void* p : {(void*)b.err, (void*)b.mb_host, (void*)b.lv_host, (void*)s.st_host, (void*)b.lf_sse})
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : {s.start, s.done})
         if (e) (void)hipEventDestroy(e);
 }
 
 GpuVp8Encoder::GpuVp8Encoder(const h264::EncoderConfig& cfg, hipStream_t stream)
-    : cfg_(cfg.with_aq_default(4)), common_(cfg), stream_(stream) {
+    : cfg_(cfg.with_aq_default(4)),
+      common_(cfg),
+      stream_(stream),
+      lf_(cfg.vp8_deblock_mode()),
+      lf_num_(lf_num_from_env()) {
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
         throw std::invalid_argument("pipeline_depth must be 1 to 4");
     if (cfg.width > 16383 || cfg.height > 16383) throw std::invalid_argument("vp8: picture larger than 16383");
@@ -131,6 +141,12 @@ void GpuVp8Encoder::writer_loop(Slot& s) {
                     for (int c = 0; c < 3; ++c) s.sse[c] += m.sse[c];
                     s.skipped += m.nz == 0;
                 }
+                if (s.lf_on) {  // the filtered picture's distortion (k_vp8_lf, per row)
+                    s.sse[0] = s.sse[1] = s.sse[2] = 0;
+                    for (int r = 0; r < geom_.mb_h; ++r)
+                        for (int c = 0; c < 3; ++c) s.sse[c] += s.buf.lf_sse[3 * r + c];
+                }
+                lf_.record(s.fidx, s.key, s.buf.mb_host, geom_.mb_w, geom_.mb_h);
                 s.ms = 0;
                 (void)hipEventElapsedTime(&s.ms, s.start, s.done);
             }
@@ -203,6 +219,8 @@ void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
         }
     }
     f.drop_lambda = h264::lambda_sse(qp);
+    for (int k = 0; k < kNumSegs; ++k) f.lf_level[k] = s.lf_level[k] = 0;  // prepare() decides the filter
+    s.lf_on = false;
     h264::FrameState& m = s.st_host->me;
     std::memset(&m, 0, sizeof m);
     m.ref_y = rec_y_[ref];
@@ -228,6 +246,7 @@ void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* 
         uint8_t* const planes[4] = {hp_, hp_sub_[0], hp_sub_[1], hp_sub_[2]};
         launch_vp8_inter(geom_, s.buf, planes, hp_pitch_, cfg_.subpel != 0, src_y, src_uv, stream_);
     }
+    if (s.lf_on) launch_vp8_lf(geom_, s.buf, src_y, src_uv, stream_);
     launch_vp8_gather(geom_, s.buf, stream_);
     HIP_CHECK(hipGetLastError());
 }
@@ -245,7 +264,10 @@ void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out, bool pr
     const int16_t* lv = s.buf.lv_host;
     FrameDesc fd{s.key, cfg_.width, cfg_.height, geom_.mb_w, geom_.mb_h, s.qindex, log2_parts_};
     fd.segmented = s.segmented;
-    for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = s.seg_qindex[k];
+    for (int k = 0; k < kNumSegs; ++k) {
+        fd.seg_qindex[k] = s.seg_qindex[k];
+        fd.lf_level[k] = s.lf_level[k];
+    }
     write_frame(fd, mbs, [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
                 [&](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); },
                 probe ? nullptr : &tok_stats_[s.key ? 1 : 0][s.fidx % kStatsLag]);
@@ -281,6 +303,11 @@ bool GpuVp8Encoder::prepare(bool force_idr) {
     const int ref = cur_;
     cur_ ^= 1;
     fill_state(s, s.key, s.qp, ref, cur_);
+    lf_levels(lf_.decide(s.fidx, s.key), s.segmented, s.qindex, s.seg_qindex, lf_num_, s.lf_level);
+    for (int k = 0; k < kNumSegs; ++k) {
+        s.st_host->v.lf_level[k] = s.lf_level[k];
+        s.lf_on = s.lf_on || s.lf_level[k] != 0;
+    }
     return s.key;
 }
 
@@ -337,6 +364,7 @@ const std::vector<uint8_t>& GpuVp8Encoder::collect() {
     stats_.bytes = (int)au_.size();
     stats_.encode_ms = s.ms;
     stats_.skipped_mbs = s.skipped;
+    stats_.deblocked = s.lf_on;
     for (int c = 0; c < 3; ++c) stats_.sse[c] = s.sse[c];
     stats_.sse_masked = s.sse[0];
     stats_.masked_pixels = (int64_t)cfg_.width * cfg_.height;

@@ -1,9 +1,10 @@
 // HIP analysis kernels of the VP8 encoder (RFC 6386; WEBRTC_ENCODER=vp8enc, reference
 // README.md:21,35): every decision and sample of CpuVp8Encoder::analyse (vp8_cpu.cpp), on the GPU.
 //
-//   P frame:   k_vp8_pad -> k_me_full (shared with H.264, full-sample search) -> k_vp8_inter
-//              -> k_vp8_gather
-//   key frame: k_vp8_key -> k_vp8_gather
+//   P frame:   k_vp8_pad (or the H.264 k_hpel planes with subpel) -> k_me_full (shared with
+//              H.264) -> k_vp8_inter [-> k_vp8_lf] -> k_vp8_gather
+//   key frame: k_vp8_key [-> k_vp8_lf] -> k_vp8_gather
+//   (k_vp8_lf: the loop filter, when the frame's levels are not all zero)
 //
 // One 64-lane wave codes one macroblock: lanes 0..15 own the luma 4x4 blocks, 16..23 the chroma
 // blocks, lane 24 the second-order Y2 block -- the block index of a lane is its token block index,
@@ -595,6 +596,328 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
     }
 }
 
+// ------------------------------------------------------------------ loop filter (15)
+// The whole reconstruction in place, bit-exact with vp8_core.h loop_filter_frame.  Section 15.1 is
+// a raster-order chain: a macroblock's left edge reads the columns its left neighbour's inner and
+// horizontal edges left, its top edge the rows the row above left after that row's next
+// macroblock filtered its left edge.  So: one wave per macroblock row walking the row, the row
+// below two macroblocks behind; kLfRows rows per workgroup.  Lanes 0..15 own luma lines, 16..23
+// Cb, 24..31 Cr: the vertical edges run on sample rows in registers (elements 0..3 the left
+// neighbour's last four columns, 4.. the macroblock), the horizontal edges on columns after a
+// transpose through the wave's LDS tile (elements 0..3 the four rows above).
+// Hand-offs: inside a workgroup a row passes each finished macroblock's bottom rows 12..15 to the
+// row below through an LDS ring (progress words, back-pressure at kLfRing entries); across
+// workgroups (other XCDs, other L2s) the last row stores the same rows, column-packed, into a
+// hand-off line of 64-bit words -- four samples and the frame's epoch tag -- with agent-scope
+// atomic stores (device-coherent: no L2 write-back fence, no separate progress word to order
+// after them); the next workgroup's first row polls its words with agent-scope atomic loads until
+// every lane holds this frame's tag.  Every
+// sample has one writer: a row writes rows 0..12 of its macroblock x - 1 once x's left edge is
+// done; rows 13..15 go out with the row below's top-edge strip.  The distortion against the
+// source of every final sample is summed per row (the frame statistics; the records' figures are
+// the unfiltered picture's).  The macroblocks' levels and inner-edge flags are staged in LDS
+// first.  Global accesses go through address-space-1 pointers (flat ones would also count on
+// lgkmcnt and stall every LDS wait); the transposes order LDS with compiler barriers only (a
+// wave's LDS operations execute in order; a fence would wait for the prefetched loads).
+constexpr int kLfRows = 8;
+constexpr int kLfRing = 8;
+struct LfWave {
+    uint8_t T[512];                // transposes: luma 16x16 at 0, Cb 8x8 at 256, Cr 8x8 at 320
+    uint8_t ring[kLfRing][128];    // rows 12..15 of a macroblock: luma 4 x 16, then chroma 4 x 16 interleaved
+    uint8_t info[512];             // per macroblock of the row: level | inner-edges << 7
+    int prod;                      // ring entries written (macroblocks 0 .. prod - 1)
+    int cons;                      // entries of the row above's ring this row has read
+};
+typedef __attribute__((address_space(1))) uint8_t g8;
+typedef unsigned LfV4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) LfV4 GLfV4;
+__device__ __forceinline__ uint4 lf_ld16(const uint8_t* p) {
+    const LfV4 v = *(const GLfV4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lf_st16(uint8_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const LfV4 v = {a, b, c, d};
+    *(GLfV4*)p = v;
+}
+__device__ __forceinline__ uint32_t byte_of(const uint4& w, int j) {
+    const uint32_t d = j < 4 ? w.x : (j < 8 ? w.y : (j < 12 ? w.z : w.w));
+    return (d >> (8 * (j & 3))) & 0xffu;
+}
+__device__ __forceinline__ void lf_sync_wave() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int lf_lds_load(const int* p) {
+    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    return v;
+}
+__device__ __forceinline__ void lf_lds_store(int* p, int v) {  // LDS writes before it visible first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lf_wait_lds(const int* p, int need, int* err) {
+    for (unsigned s = 0; lf_lds_load(p) < need; ++s) {
+        if (s > kSpinLimit) {
+            *err = 1;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Lanes 32..63 mirror lanes 0..31 (same loads, same values, same stores): every vector memory
+// instruction of the loop then runs unconditionally (no lane-divergent branch around it), so the
+// compiler's vmcnt waits for a prefetched row count only the operations issued after it instead
+// of falling back to vmcnt(0) at every join -- which drained the prefetches and the stores.
+// Stores a lane must not make (rows 13..15, Cr lanes' halves) go to the wave's scratch words.
+__global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                          const uint8_t* __restrict__ src_y,
+                                                          const uint8_t* __restrict__ src_uv,
+                                                          const Vp8Mb* __restrict__ mbs,
+                                                          unsigned long long* __restrict__ line,
+                                                          unsigned long long* __restrict__ sse_rows,
+                                                          int* __restrict__ err) {
+    __builtin_amdgcn_s_setprio(3);  // a serial chain on few waves
+    __shared__ LfWave W[kLfRows];
+    const int wr = threadIdx.x >> 6, lane = threadIdx.x & 63, ml = lane & 31;
+    const int mby = blockIdx.x * kLfRows + wr;
+    if (threadIdx.x < kLfRows) W[threadIdx.x].prod = W[threadIdx.x].cons = 0;
+    __syncthreads();
+    if (mby >= g.mb_h) return;
+    const Vp8FrameState& F = st->v;
+    LfWave& S = W[wr];
+    const int y0 = mby * 16, cy0 = mby * 8;
+    const uint32_t epoch = (uint32_t)F.epoch;
+    const bool is_y = ml < 16, is_u = ml >= 16 && ml < 24;
+    const int li = is_y ? ml : (ml - 16) & 7;  // the lane's line (row, then column) of its plane
+    const int comp = is_u ? 0 : 1;             // chroma component byte in an interleaved pair
+    const int pitch = g.pitch;
+    const bool bottom = mby == g.mb_h - 1;
+    const bool wg_last = wr == kLfRows - 1 && !bottom;  // hands off to the next workgroup
+    const bool ring_out = wr < kLfRows - 1 && !bottom;  // hands off to the next wave
+    const bool glb_in = wr == 0 && mby > 0;              // rows above from the previous workgroup
+    const bool key = F.key != 0;
+    uint8_t* const rec_y = F.rec_y;
+    uint8_t* const rec_uv = F.rec_uv;
+    const size_t line_words = (size_t)32 * g.mb_w * (size_t)((g.mb_h + kLfRows - 1) / kLfRows);  // 64-bit
+    uint8_t* const scratch = reinterpret_cast<uint8_t*>(line + line_words) + (size_t)(blockIdx.x * kLfRows + wr) * 1024;
+    // row-phase line of this lane (luma row li / chroma row li, interleaved) and its source
+    uint8_t* const rrow = is_y ? rec_y + (size_t)(y0 + li) * pitch : rec_uv + (size_t)(cy0 + li) * pitch;
+    const uint8_t* const srow = is_y ? src_y + (size_t)(y0 + li) * pitch : src_uv + (size_t)(cy0 + li) * pitch;
+    // column-phase sample (x0 + col) of row y0 - 4 + k of this lane's plane: byte offset
+    auto col_off = [&](int x0, int k) -> size_t {
+        return is_y ? (size_t)(y0 - 4 + k) * pitch + x0 + li : (size_t)(cy0 - 4 + k) * pitch + x0 + 2 * li + comp;
+    };
+    uint8_t* const cplane = is_y ? rec_y : rec_uv;
+    const uint8_t* const csrc = is_y ? src_y : src_uv;
+    const int tb = is_y ? 0 : (is_u ? 256 : 320), tstride = is_y ? 16 : 8;
+    const bool row_vis = is_y ? y0 + li < g.height : 2 * (cy0 + li) < g.height;
+    // rows this lane writes back: rows 13..15 (chroma 5..7) belong to the row below's strip; a Cr
+    // lane's samples go out interleaved by its Cb lane
+    const bool writes_row = (is_y || is_u) && (bottom || (is_y ? li <= 12 : li <= 4));
+    const bool final_row = lane < 32 && row_vis && (bottom || (is_y ? li <= 12 : li <= 4));
+    // stage the row's macroblock levels and inner-edge flags
+    for (int i = lane; i < g.mb_w; i += 64) {
+        const Vp8Mb& m = mbs[mby * g.mb_w + i];
+        S.info[i] = (uint8_t)(F.lf_level[m.seg & 3] | (m.nz ? 0x80 : 0));
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the staged bytes before any lane reads them
+    lf_sync_wave();
+    int px[20], fin[16];
+#pragma unroll
+    for (int j = 0; j < 20; ++j) px[j] = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) fin[j] = 0;
+    uint32_t acc = 0;  // this lane's distortion of the samples it finalised
+    uint4 own = lf_ld16(rrow);                 // macroblock 0's row
+    uint4 srcn = make_uint4(0u, 0u, 0u, 0u);   // source row of the macroblock to account
+    auto account_mb = [&](int mbx_done, const uint4& s) {
+        if (!final_row) return;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const bool in = is_y ? mbx_done * 16 + j < g.width : (j < 8 && 2 * (mbx_done * 8 + j) < g.width);
+            const int e = fin[j] - (int)byte_of(s, is_y ? j : (2 * (j & 7) + comp));
+            acc += in ? (uint32_t)(e * e) : 0u;
+        }
+    };
+    auto store_mb = [&](int mbx_done) {
+        uint32_t d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            d[k] = (uint32_t)fin[4 * k] | ((uint32_t)fin[4 * k + 1] << 8) | ((uint32_t)fin[4 * k + 2] << 16) |
+                   ((uint32_t)fin[4 * k + 3] << 24);
+        // Cr lanes hand their 8 samples to the Cb lane of the same row
+        const uint32_t vlo = (uint32_t)__shfl((int)d[0], (lane + 8) & 63, 64);
+        const uint32_t vhi = (uint32_t)__shfl((int)d[1], (lane + 8) & 63, 64);
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t uw = d[k >> 1] >> (16 * (k & 1)), vw = (k < 2 ? vlo : vhi) >> (16 * (k & 1));
+            const uint32_t c = (uw & 0xffu) | ((vw & 0xffu) << 8) | (((uw >> 8) & 0xffu) << 16) |
+                               (((vw >> 8) & 0xffu) << 24);
+            o[k] = is_y ? d[k] : c;
+        }
+        lf_st16(writes_row ? rrow + mbx_done * 16 : scratch + 16 * lane, o[0], o[1], o[2], o[3]);
+    };
+    // rows 12..15 (chroma 4..7) of the finished macroblock into the ring for the row below (the
+    // workgroup's last row: into the hand-off line for the next workgroup, through its ring entry)
+    unsigned long long* const line_out = line + (size_t)blockIdx.x * g.mb_w * 32;
+    auto ring_put = [&](int mbx_done) {
+        if (!ring_out && !wg_last) return;
+        if (ring_out) lf_wait_lds(&W[wr + 1].cons, mbx_done - kLfRing + 1, err);  // back-pressure
+        uint8_t* e = S.ring[mbx_done % kLfRing];
+        if (is_y && li >= 12) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) e[(li - 12) * 16 + j] = (uint8_t)fin[j];
+        } else if (!is_y && li >= 4) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) e[64 + (li - 4) * 16 + 2 * j + comp] = (uint8_t)fin[j];
+        }
+        if (wg_last) {  // column-packed line word ml: luma column, then Cb, Cr columns
+            lf_sync_wave();
+            const int o = is_y ? li : 64 + 2 * li + comp;
+            const uint32_t w = (uint32_t)e[o] | ((uint32_t)e[o + 16] << 8) | ((uint32_t)e[o + 32] << 16) |
+                               ((uint32_t)e[o + 48] << 24);
+            __hip_atomic_store((gu64*)(line_out + (size_t)mbx_done * 32 + ml), (uint64_t)w | ((uint64_t)epoch << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lf_sync_wave();
+        } else {
+            lf_lds_store(&S.prod, mbx_done + 1);
+        }
+    };
+    for (int mbx = 0; mbx < g.mb_w; ++mbx) {
+        const int x0 = mbx * 16;
+        const int inf = __builtin_amdgcn_readfirstlane((int)S.info[mbx]);
+        const int level = inf & 63;  // wave-uniform
+        const LfParams f = lf_params(level, key);
+        const bool inner = (inf & 0x80) != 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) px[4 + j] = is_y ? (int)byte_of(own, j) : (j < 8 ? (int)byte_of(own, 2 * j + comp) : 0);
+        // ---- vertical edges: left macroblock edge, inner edges (luma 4 / 8 / 12, chroma 4)
+        if (level) {
+            if (mbx > 0) lf_mb_edge(px, f);
+            if (inner) {
+                lf_sub_edge(px + 4, f);
+                if (is_y) {
+                    lf_sub_edge(px + 8, f);
+                    lf_sub_edge(px + 12, f);
+                }
+            }
+        }
+        // macroblock mbx - 1 is final for this row now
+        if (mbx > 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (is_y)
+                    fin[12 + k] = px[k];
+                else
+                    fin[4 + k] = px[k];
+            }
+            ring_put(mbx - 1);
+            store_mb(mbx - 1);
+            account_mb(mbx - 1, srcn);
+        }
+        // ---- the four rows above this macroblock (columns) and their source
+        int cl[20];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) cl[k] = 0;
+        if (glb_in) {
+            const gu64* p = (const gu64*)(line + ((size_t)(blockIdx.x - 1) * g.mb_w + mbx) * 32 + ml);
+            uint64_t w = 0;
+            for (unsigned sp = 0;; ++sp) {
+                w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!__any((uint32_t)(w >> 32) != epoch)) break;
+                if (sp > kSpinLimit) {
+                    *err = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cl[k] = (int)((w >> (8 * k)) & 0xffu);
+        } else if (mby > 0) {
+            lf_wait_lds(&W[wr - 1].prod, mbx + 1, err);
+            const uint8_t* e = W[wr - 1].ring[mbx % kLfRing];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cl[k] = (int)e[is_y ? k * 16 + li : 64 + k * 16 + 2 * li + comp];
+            lf_lds_store(&S.cons, mbx + 1);  // (waits for the reads above)
+        }
+        // the strip's source; prefetch this macroblock's source row (accounted next step) and the
+        // next macroblock's row.  (Unconditional vector memory instructions -- the top row uses
+        // its scratch words -- so the waits below count exactly.)
+        int ss[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 1; k < 4; ++k) ss[k] = (int)*(const g8*)(mby > 0 ? csrc + col_off(x0, k) : scratch + 64 * k + lane);
+        srcn = lf_ld16(srow + x0);
+        own = lf_ld16(rrow + (mbx + 1 < g.mb_w ? x0 + 16 : x0));
+        if (level) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (is_y || j < 8) S.T[tb + li * tstride + j] = (uint8_t)px[4 + j];
+            lf_sync_wave();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cl[4 + r] = is_y || r < 8 ? (int)S.T[tb + r * tstride + li] : 0;
+            lf_sync_wave();
+            if (mby > 0) lf_mb_edge(cl, f);
+            if (inner) {
+                lf_sub_edge(cl + 4, f);
+                if (is_y) {
+                    lf_sub_edge(cl + 8, f);
+                    lf_sub_edge(cl + 12, f);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (is_y || r < 8) S.T[tb + r * tstride + li] = (uint8_t)cl[4 + r];
+            lf_sync_wave();
+#pragma unroll
+            for (int j = 0; j < 16; ++j) fin[j] = is_y || j < 8 ? (int)S.T[tb + li * tstride + j] : 0;
+            lf_sync_wave();
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) fin[j] = px[4 + j];
+        }
+        // the strip above (rows 13..15 of the macroblock above): final now -- written back by this
+        // row (the row above wrote rows 0..12 only) and accounted here
+        {
+            const int xs = is_y ? x0 + li : (x0 >> 1) + li;  // sample column in its plane
+            const bool vis = mby > 0 && lane < 32 && (is_y ? xs < g.width : 2 * xs < g.width);
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                *(g8*)(mby > 0 ? cplane + col_off(x0, k) : scratch + 64 * k + lane) = (uint8_t)cl[k];
+                const bool rv = is_y ? y0 - 4 + k < g.height : 2 * (cy0 - 4 + k) < g.height;
+                const int e = cl[k] - ss[k];
+                acc += vis && rv ? (uint32_t)(e * e) : 0u;
+            }
+        }
+        // left context of the next macroblock
+#pragma unroll
+        for (int k = 0; k < 4; ++k) px[k] = is_y ? fin[12 + k] : fin[4 + k];
+        // the prefetched rows are taken here, inside the iteration (their waits count only the
+        // strip stores after them; taken at the top of the next iteration, the join with the
+        // loop entry made them a full vmcnt(0))
+        {
+            uint32_t a0 = own.x, a1 = own.y, a2 = own.z, a3 = own.w, b0 = srcn.x, b1 = srcn.y, b2 = srcn.z, b3 = srcn.w;
+            asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+            own = make_uint4(a0, a1, a2, a3);
+            srcn = make_uint4(b0, b1, b2, b3);
+        }
+    }
+    ring_put(g.mb_w - 1);
+    store_mb(g.mb_w - 1);
+    account_mb(g.mb_w - 1, srcn);
+    const uint32_t sy = (uint32_t)wsum(lane < 32 && is_y ? (int)acc : 0), su = (uint32_t)wsum(lane < 32 && is_u ? (int)acc : 0),
+                   sv = (uint32_t)wsum(lane < 32 && !is_y && !is_u ? (int)acc : 0);
+    if (lane == 0) {
+        sse_rows[3 * mby] = sy;
+        sse_rows[3 * mby + 1] = su;
+        sse_rows[3 * mby + 2] = sv;
+    }
+}
+
 // ------------------------------------------------------------------ hand-off to the host writer
 // One workgroup per macroblock row: the rank of each coded macroblock within its row (ballots),
 // its 800 level bytes to the mapped host buffer at slot row * mb_w + rank, every record with its
@@ -670,6 +993,12 @@ void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const ui
                            src_y);
     hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv, b.prog,
                        b.line, b.err);
+}
+
+void launch_vp8_lf(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
+                   hipStream_t stream) {
+    hipLaunchKernelGGL(k_vp8_lf, dim3((g.mb_h + kLfRows - 1) / kLfRows), dim3(64 * kLfRows), 0, stream, g, b.st, src_y,
+                       src_uv, b.mb, b.lf_line, b.lf_sse, b.err);
 }
 
 void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream) {

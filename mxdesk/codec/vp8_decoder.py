@@ -9,9 +9,10 @@ dequantisation (14.1) with per-segment quantisers (9.3), inverse WHT / DCT (14.3
 chroma intra prediction with the 127 / 129 frame edges (12), and six-tap inter prediction (18).
 
 Supported: key and inter frames, 16x16 intra modes, 16x16 inter macroblocks (ZERO / NEAREST / NEAR /
-NEW vectors, last-frame reference), segmentation (segment map, absolute / delta segment quantisers),
-token partitions, probability updates, skip flags.  Raises ``NotImplementedError`` for B_PRED,
-SPLITMV, a non-zero loop-filter level and golden / altref references.  Slow; for test pictures.
+NEW vectors, last-frame reference), segmentation (segment map, absolute / delta segment quantisers
+and loop-filter levels), the normal loop filter (15), token partitions, probability updates, skip
+flags.  Raises ``NotImplementedError`` for B_PRED, SPLITMV, the simple filter, filter sharpness,
+mode / reference filter deltas and golden / altref references.  Slow; for test pictures.
 """
 from __future__ import annotations
 
@@ -174,28 +175,32 @@ class Decoder:
         seg_on = bd.lit(1)
         update_map = 0
         if key:
-            self.seg_abs, self.seg_q = 0, [0, 0, 0, 0]
+            self.seg_abs, self.seg_q, self.seg_lf = 0, [0, 0, 0, 0], [0, 0, 0, 0]
             self.seg_probs = [255, 255, 255]
-        if seg_on:  # 9.3: segment quantisers (absolute or delta) and the segment map's tree probabilities
+            self.lf_deltas = [0] * 8
+        if seg_on:  # 9.3: segment quantisers and loop-filter levels (absolute or delta), map probabilities
             update_map = bd.lit(1)
             if bd.lit(1):  # update_segment_feature_data
                 self.seg_abs = bd.lit(1)
                 self.seg_q = [(bd.signed(7) if bd.lit(1) else 0) for _ in range(4)]
-                for _ in range(4):  # loop-filter levels per segment (no loop filter here)
-                    if bd.lit(1) and bd.signed(6):
-                        raise NotImplementedError("loop filter")
+                self.seg_lf = [(bd.signed(6) if bd.lit(1) else 0) for _ in range(4)]
             if update_map:
                 self.seg_probs = [bd.lit(8) if bd.lit(1) else 255 for _ in range(3)]
-        bd.lit(1)  # filter type
+        simple = bd.lit(1)  # filter type
         level = bd.lit(6)
-        bd.lit(3)  # sharpness
-        if level:
-            raise NotImplementedError("loop filter")
-        if bd.lit(1):  # loop_filter_adj_enable
+        sharpness = bd.lit(3)
+        if bd.lit(1):  # loop_filter_adj_enable: reference / mode level deltas (persist between frames)
             if bd.lit(1):
-                for _ in range(8):
+                for k in range(8):
                     if bd.lit(1):
-                        bd.signed(6)
+                        self.lf_deltas[k] = bd.signed(6)
+            if any(self.lf_deltas):
+                raise NotImplementedError("loop-filter mode / reference deltas")
+        if level and (simple or sharpness):
+            raise NotImplementedError("simple loop filter / sharpness")
+        # 15.1: per-segment filter levels (absolute or added to the frame level), 0..63
+        lf_seg = [min(63, max(0, (self.seg_lf[k] if self.seg_abs else level + self.seg_lf[k]) if seg_on else level))
+                  for k in range(4)]
         nparts = 1 << bd.lit(2)
         qi = bd.lit(7)
         deltas = [bd.signed(4) if bd.lit(1) else 0 for _ in range(5)]  # y_dc, y2_dc, y2_ac, uv_dc, uv_ac
@@ -315,7 +320,11 @@ class Decoder:
                         above[mx][k] = left[k] = 0
                 else:
                     coefs = self._tokens(bd, above[mx], left)
+                m["coded"] = any(any(c) for c in coefs)  # inner edges are filtered
                 self._recon(Y, U, V, mx, my, m, coefs, key)
+        if level:  # section 15: after the whole frame is reconstructed (intra prediction saw it unfiltered)
+            self._loop_filter(Y, U, V, mbs, [lf_seg[self.seg_map[i]] if seg_on else level for i in range(mw * mh)], key)
+            self.stats["filtered"] = self.stats.get("filtered", 0) + 1
         if saved is not None:
             self.coef, self.mvp, self.ymode_prob, self.uvmode_prob = saved
         self.stats["key" if key else "inter"] += 1
@@ -530,6 +539,61 @@ class Decoder:
         if mode == H_PRED:
             return np.tile(left[:, None], (1, n))
         return np.clip(left[:, None] + above[None, :] - corner, 0, 255)
+
+    # ------------------------------------------------------------------ loop filter (15)
+    @staticmethod
+    def _lf_edge(P, mb, level, key):
+        """Filter the sample lines across one edge: P (8, n) = p3 p2 p1 p0 q0 q1 q2 q3 (int64),
+        in place -- the normal filter of 15.3 (libvpx's arithmetic)."""
+        lim = max(level, 1)
+        elim = (level + 2) * 2 + lim if mb else level * 2 + lim
+        t = ((2 if level >= 40 else 1 if level >= 15 else 0) if key else
+             (3 if level >= 40 else 2 if level >= 20 else 1 if level >= 15 else 0))
+        p3, p2, p1, p0, q0, q1, q2, q3 = P
+        mask = ((np.abs(p0 - q0) * 2 + (np.abs(p1 - q1) >> 1) <= elim) & (np.abs(p3 - p2) <= lim)
+                & (np.abs(p2 - p1) <= lim) & (np.abs(p1 - p0) <= lim) & (np.abs(q3 - q2) <= lim)
+                & (np.abs(q2 - q1) <= lim) & (np.abs(q1 - q0) <= lim))
+        hev = (np.abs(p1 - p0) > t) | (np.abs(q1 - q0) > t)
+        s8 = lambda v: np.clip(v, -128, 127)  # noqa: E731
+        ps2, ps1, ps0, qs0, qs1, qs2 = p2 - 128, p1 - 128, p0 - 128, q0 - 128, q1 - 128, q2 - 128
+        if mb:
+            w = s8(s8(ps1 - qs1) + 3 * (qs0 - ps0))
+            a27, a18, a9 = s8((27 * w + 63) >> 7), s8((18 * w + 63) >> 7), s8((9 * w + 63) >> 7)
+            n = [np.where(hev, ps2, s8(ps2 + a9)), np.where(hev, ps1, s8(ps1 + a18)),
+                 np.where(hev, s8(ps0 + (s8(w + 3) >> 3)), s8(ps0 + a27)),
+                 np.where(hev, s8(qs0 - (s8(w + 4) >> 3)), s8(qs0 - a27)),
+                 np.where(hev, qs1, s8(qs1 - a18)), np.where(hev, qs2, s8(qs2 - a9))]
+        else:
+            a = s8(np.where(hev, s8(ps1 - qs1), 0) + 3 * (qs0 - ps0))
+            f1, f2 = s8(a + 4) >> 3, s8(a + 3) >> 3
+            o = (f1 + 1) >> 1
+            n = [ps2, np.where(hev, ps1, s8(ps1 + o)), s8(ps0 + f2), s8(qs0 - f1), np.where(hev, qs1, s8(qs1 - o)), qs2]
+        for k in range(6):
+            P[1 + k] = np.where(mask, n[k] + 128, P[1 + k])
+
+    def _loop_filter(self, Y, U, V, mbs, levels, key):
+        """15.1: macroblocks in raster order; per macroblock and plane the left edge, the inner
+        vertical edges, the top edge, the inner horizontal edges (inner ones only where the
+        macroblock has coefficients)."""
+        for my in range(self.mh):
+            for mx in range(self.mw):
+                i = my * self.mw + mx
+                level = levels[i]
+                if not level:
+                    continue
+                inner = mbs[i]["coded"]
+                for P, n in ((Y, 16), (U, 8), (V, 8)):
+                    x0, y0 = mx * n, my * n
+                    edges_v = ([(x0, True)] if mx else []) + ([(x0 + e, False) for e in range(4, n, 4)] if inner else [])
+                    for xe, mb in edges_v:
+                        T = P[y0:y0 + n, xe - 4:xe + 4].T.copy()
+                        self._lf_edge(T, mb, level, key)
+                        P[y0:y0 + n, xe - 4:xe + 4] = T.T
+                    edges_h = ([(y0, True)] if my else []) + ([(y0 + e, False) for e in range(4, n, 4)] if inner else [])
+                    for ye, mb in edges_h:
+                        T = P[ye - 4:ye + 4, x0:x0 + n].copy()
+                        self._lf_edge(T, mb, level, key)
+                        P[ye - 4:ye + 4, x0:x0 + n] = T
 
     @staticmethod
     def _inter_pred(P, x0, y0, n, mvx, mvy):

@@ -118,3 +118,67 @@ def test_gpu_vp8_pipelined_matches(gpu, depth):
     while len(out) < len(srcs):
         out.append(b.collect())
     assert out == ref
+
+
+def _sse(ry, ruv, y, uv, w, h):
+    e = lambda a, b: int(((a.astype(np.int64) - b.astype(np.int64)) ** 2).sum())  # noqa: E731
+    cw, chh = (w + 1) // 2, (h + 1) // 2
+    return (e(ry[:h, :w], y[:h, :w]), e(ruv[:chh, 0:2 * cw:2], uv[:chh, 0:2 * cw:2]),
+            e(ruv[:chh, 1:2 * cw:2], uv[:chh, 1:2 * cw:2]))
+
+
+@pytest.mark.parametrize("w,h,qp,aq", [(96, 64, 28, 4), (100, 60, 44, 2), (320, 192, 24, 4), (176, 144, 54, 4)])
+def test_gpu_vp8_loop_filter_bit_exact_vs_cpu(gpu, w, h, qp, aq):
+    """The loop filter forced on (deblock 1): k_vp8_lf's wavefront gives the CPU oracle's filtered
+    reconstruction, bitstream and records for key and inter frames (per-segment levels with aq 4);
+    the frame statistics' distortion is the filtered picture's; the in-tree decoder agrees."""
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps, cfg.qp, cfg.bitrate_kbps, cfg.search_range = w, h, 60, qp, 0, 8
+    cfg.deblock, cfg.aq = 1, aq
+    genc, cenc = gpu.GpuVp8Encoder(cfg, _stream()), gpu.CpuVp8Encoder(cfg)
+    frames = []
+    for t in range(7):
+        y, uv = synthetic_nv12(w, h, t, seed=t % 3)
+        dy, duv = _dev(genc, y, uv)
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), t == 4)
+        cau = cenc.encode(y, uv, t == 4)
+        _check(genc, cenc, gau, cau, w, h, t)
+        gy, guv = genc.recon()
+        assert tuple(genc.stats.sse) == _sse(gy, guv, y, uv, w, h), f"frame {t}"
+        frames.append(gau)
+    dec = Decoder()
+    dec.decode(frames)
+    assert dec.stats["filtered"] == 7
+
+
+def test_gpu_vp8_adaptive_loop_filter_1080p_pan(gpu):
+    """1080p synthetic desktop panning 2 px per frame (coherent motion), adaptive filter (the
+    default): GPU == CPU through the switch-on kStatsLag frames in, and depth 4 (frames in flight,
+    writer threads) gives the depth-1 bitstream."""
+    w, h = 1920, 1080
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps, cfg.qp, cfg.bitrate_kbps, cfg.search_range = w, h, 60, 34, 0, 16
+    genc, cenc = gpu.GpuVp8Encoder(cfg, _stream()), gpu.CpuVp8Encoder(cfg)
+    y0, uv0 = desktop_nv12(gpu, w + 64, h, 0)
+    srcs = [(np.ascontiguousarray(y0[:, 2 * t:2 * t + w]), np.ascontiguousarray(uv0[:, 2 * t:2 * t + w]))
+            for t in range(8)]
+    devs = [_dev(genc, y, uv) for y, uv in srcs]
+    ref, flags = [], []
+    for t, ((y, uv), (dy, duv)) in enumerate(zip(srcs, devs)):
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        _check(genc, cenc, gau, cau, w, h, t)
+        assert genc.stats.deblocked == cenc.stats.deblocked
+        flags.append(int(genc.stats.deblocked))
+        ref.append(gau)
+    assert flags == [0, 0, 0, 0, 0, 1, 1, 1], flags
+    cfg.pipeline_depth = 4
+    b = gpu.GpuVp8Encoder(cfg, _stream())
+    out = []
+    for t, (dy, duv) in enumerate(devs):
+        if t >= 4:
+            out.append(b.collect())
+        b.submit(dy.data_ptr(), duv.data_ptr(), False)
+    while len(out) < len(devs):
+        out.append(b.collect())
+    assert out == ref

@@ -182,3 +182,77 @@ def test_segmented_inter_frames_decode_to_reconstruction(native, aq):
     keep[int(h * 0.55) - 16:int(h * 0.77) + 17, int(w * 0.04) - 16:int(w * 0.20) + 17] = False
     err = lambda d: float(np.mean(((d.frames_coded[-1][0][:h, :w].astype(float) - y4[:h, :w]) ** 2)[keep]))  # noqa: E731
     assert err(dec) < 0.5 * err(dflat), (err(dec), err(dflat))
+
+
+@pytest.mark.parametrize("w,h,qp", [(96, 64, 20), (176, 144, 34), (100, 60, 44), (64, 48, 54)])
+def test_loop_filtered_key_frame_through_libwebp(native, w, h, qp):
+    """The normal loop filter (section 15; levels 6..40 here, every hev threshold): libwebp's
+    decode of the filtered key frame is the encoder's reconstruction -- which pins the filter's
+    arithmetic, its edge order and intra prediction from the unfiltered picture to a real decoder."""
+    y, uv = _picture(w, h, qp + 1)
+    c = native.EncoderConfig()
+    c.width, c.height, c.qp, c.bitrate_kbps, c.deblock = w, h, qp, 0, 1
+    enc = native.CpuVp8Encoder(c)
+    frame = enc.encode(y, uv)
+    ry, ruv = enc.recon()
+    rgb = np.asarray(Image.open(io.BytesIO(webp_container(frame))).convert("RGB")).astype(np.int64)
+    ref = libwebp_rgb(ry[:h, :w].astype(np.int64), ruv[:h // 2, 0:w:2].astype(np.int64),
+                      ruv[:h // 2, 1:w:2].astype(np.int64))
+    assert np.array_equal(rgb, ref), int((rgb != ref).any(axis=2).sum())
+    dec = Decoder()
+    dec.decode([frame])
+    assert dec.stats.get("filtered") == 1 and np.array_equal(dec.frames_coded[0][0], ry)
+    c.deblock = 0  # the filter changed the picture
+    ry0, _ = (lambda e: (e.encode(y, uv), e.recon())[1])(native.CpuVp8Encoder(c))
+    assert not np.array_equal(ry0, ry)
+
+
+@pytest.mark.parametrize("aq", [2, 4])
+def test_loop_filtered_inter_frames_decode_to_reconstruction(native, aq):
+    """Filtered key and inter frames (aq 4: per-segment levels, the static segment unfiltered):
+    the in-tree decoder reproduces every reconstruction."""
+    w, h = 160, 96
+    c = native.EncoderConfig()
+    c.width, c.height, c.qp, c.bitrate_kbps, c.search_range, c.deblock, c.aq = w, h, 36, 0, 8, 1, aq
+    enc = native.CpuVp8Encoder(c)
+    frames, recs = [], []
+    for t in range(7):
+        y, uv = synthetic_nv12(w, h, t, seed=t % 3)
+        frames.append(enc.encode(y, uv, t == 4))
+        recs.append(tuple(a.copy() for a in enc.recon()))
+    dec = Decoder()
+    dec.decode(frames)
+    for t, ((yy, u, v), (ry, ruv)) in enumerate(zip(dec.frames_coded, recs)):
+        assert np.array_equal(yy, ry), f"frame {t} luma"
+        assert np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2]), f"frame {t} chroma"
+    assert dec.stats["filtered"] == 7
+
+
+def test_adaptive_loop_filter_follows_coherent_motion(native):
+    """deblock -1 (the VP8 default, adaptive): a still picture is never filtered; a pan switches
+    the filter on kStatsLag (4) frames after the first panned frame, and the bitstream says so."""
+    w, h = 192, 128
+    base, uv0 = _picture(w + 64, h, 9)
+
+    def run(pan):
+        c = native.EncoderConfig()
+        c.width, c.height, c.qp, c.bitrate_kbps, c.search_range = w, h, 32, 0, 16
+        enc = native.CpuVp8Encoder(c)
+        frames = []
+        for t in range(9):
+            s = 2 * t if pan else 0
+            frames.append(enc.encode(np.ascontiguousarray(base[:, s:s + w]), np.ascontiguousarray(uv0[:, s:s + w])))
+        return frames
+
+    for pan, want in ((False, 0), (True, 4)):
+        frames = run(pan)
+        dec = Decoder()
+        filtered = []
+        for f in frames:
+            n = dec.stats.get("filtered", 0)
+            dec.decode_frame(f)
+            filtered.append(dec.stats.get("filtered", 0) - n)
+        if pan:
+            assert filtered[:5] == [0] * 5 and filtered[5:] == [1] * 4, filtered
+        else:
+            assert sum(filtered) == want, filtered
