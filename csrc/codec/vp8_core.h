@@ -12,7 +12,7 @@
 // predicting from the last frame with quarter-sample vectors (ZEROMV / NEARESTMV / NEARMV / NEWMV);
 // inter frames segmented (9.3) by the temporal classes of the H.264 encoder's adaptive
 // quantisation -- four segment quantisers, a per-macroblock segment map -- key frames one
-// quantiser; the normal loop filter with per-segment levels (section 15; adaptive by default:
+// quantiser; the normal loop filter with per-segment levels (section 15; opt-in, on or adaptive:
 // on for coherent motion, vp8_encoder.h LfDecision); token partitions by MB row; coefficient
 // probabilities updated per frame from the token statistics of frame n - kStatsLag (vp8_encoder.h).
 #pragma once

@@ -20,6 +20,8 @@
 // k_vp8_gather hands it only the coded macroblocks' levels, compacted per row, in mapped memory.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../common/hip_check.h"
 #include "h264_core.h"
 #include "h264_gpu.h"
@@ -619,7 +621,7 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
 // first.  Global accesses go through address-space-1 pointers (flat ones would also count on
 // lgkmcnt and stall every LDS wait); the transposes order LDS with compiler barriers only (a
 // wave's LDS operations execute in order; a fence would wait for the prefetched loads).
-constexpr int kLfRows = 8;
+constexpr int kLfRows = 4;  // one wave per SIMD (8 rows, two per SIMD, measured 5 % slower)
 constexpr int kLfRing = 8;
 struct LfWave {
     uint8_t T[512];                // transposes: luma 16x16 at 0, Cb 8x8 at 256, Cr 8x8 at 320
@@ -670,21 +672,20 @@ __device__ __forceinline__ void lf_wait_lds(const int* p, int need, int* err) {
 
 // Lanes 32..63 mirror lanes 0..31 (same loads, same values, same stores): every vector memory
 // instruction of the loop then runs unconditionally (no lane-divergent branch around it), so the
-// compiler's vmcnt waits for a prefetched row count only the operations issued after it instead
-// of falling back to vmcnt(0) at every join -- which drained the prefetches and the stores.
-// Stores a lane must not make (rows 13..15, Cr lanes' halves) go to the wave's scratch words.
-__global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const Vp8States* __restrict__ st,
-                                                          const uint8_t* __restrict__ src_y,
-                                                          const uint8_t* __restrict__ src_uv,
-                                                          const Vp8Mb* __restrict__ mbs,
-                                                          unsigned long long* __restrict__ line,
-                                                          unsigned long long* __restrict__ sse_rows,
-                                                          int* __restrict__ err) {
+// compiler's vmcnt wait for the prefetched row counts only the operations issued after it instead
+// of falling back to vmcnt(0) at a join -- which drained the prefetch and the stores.  Stores a
+// lane must not make (rows 13..15, Cr lanes' halves) go to the wave's scratch words.  The
+// distortion of the filtered picture is k_vp8_lf_sse's (fully parallel, off this chain).
+template <int kRows>
+__global__ __launch_bounds__(64 * kRows) void k_vp8_lf(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                        const Vp8Mb* __restrict__ mbs,
+                                                        unsigned long long* __restrict__ line,
+                                                        int* __restrict__ err) {
     __builtin_amdgcn_s_setprio(3);  // a serial chain on few waves
-    __shared__ LfWave W[kLfRows];
+    __shared__ LfWave W[kRows];
     const int wr = threadIdx.x >> 6, lane = threadIdx.x & 63, ml = lane & 31;
-    const int mby = blockIdx.x * kLfRows + wr;
-    if (threadIdx.x < kLfRows) W[threadIdx.x].prod = W[threadIdx.x].cons = 0;
+    const int mby = blockIdx.x * kRows + wr;
+    if (threadIdx.x < kRows) W[threadIdx.x].prod = W[threadIdx.x].cons = 0;
     __syncthreads();
     if (mby >= g.mb_h) return;
     const Vp8FrameState& F = st->v;
@@ -696,29 +697,26 @@ __global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const
     const int comp = is_u ? 0 : 1;             // chroma component byte in an interleaved pair
     const int pitch = g.pitch;
     const bool bottom = mby == g.mb_h - 1;
-    const bool wg_last = wr == kLfRows - 1 && !bottom;  // hands off to the next workgroup
-    const bool ring_out = wr < kLfRows - 1 && !bottom;  // hands off to the next wave
-    const bool glb_in = wr == 0 && mby > 0;              // rows above from the previous workgroup
+    const bool wg_last = wr == kRows - 1 && !bottom;  // hands off to the next workgroup
+    const bool ring_out = wr < kRows - 1 && !bottom;  // hands off to the next wave
+    const bool glb_in = wr == 0 && mby > 0;            // rows above from the previous workgroup
     const bool key = F.key != 0;
     uint8_t* const rec_y = F.rec_y;
     uint8_t* const rec_uv = F.rec_uv;
-    const size_t line_words = (size_t)32 * g.mb_w * (size_t)((g.mb_h + kLfRows - 1) / kLfRows);  // 64-bit
-    uint8_t* const scratch = reinterpret_cast<uint8_t*>(line + line_words) + (size_t)(blockIdx.x * kLfRows + wr) * 1024;
-    // row-phase line of this lane (luma row li / chroma row li, interleaved) and its source
+    const size_t line_words = (size_t)32 * g.mb_w * (size_t)((g.mb_h + kRows - 1) / kRows);  // 64-bit
+    uint8_t* const scratch = reinterpret_cast<uint8_t*>(line + line_words) + (size_t)(blockIdx.x * kRows + wr) * 1024;
+    // row-phase line of this lane (luma row li / chroma row li, interleaved)
     uint8_t* const rrow = is_y ? rec_y + (size_t)(y0 + li) * pitch : rec_uv + (size_t)(cy0 + li) * pitch;
-    const uint8_t* const srow = is_y ? src_y + (size_t)(y0 + li) * pitch : src_uv + (size_t)(cy0 + li) * pitch;
     // column-phase sample (x0 + col) of row y0 - 4 + k of this lane's plane: byte offset
     auto col_off = [&](int x0, int k) -> size_t {
         return is_y ? (size_t)(y0 - 4 + k) * pitch + x0 + li : (size_t)(cy0 - 4 + k) * pitch + x0 + 2 * li + comp;
     };
     uint8_t* const cplane = is_y ? rec_y : rec_uv;
-    const uint8_t* const csrc = is_y ? src_y : src_uv;
+    // transposes: luma 16x16 at T + 0 (row-major), Cb / Cr 8x8 at 256 / 320
     const int tb = is_y ? 0 : (is_u ? 256 : 320), tstride = is_y ? 16 : 8;
-    const bool row_vis = is_y ? y0 + li < g.height : 2 * (cy0 + li) < g.height;
     // rows this lane writes back: rows 13..15 (chroma 5..7) belong to the row below's strip; a Cr
     // lane's samples go out interleaved by its Cb lane
     const bool writes_row = (is_y || is_u) && (bottom || (is_y ? li <= 12 : li <= 4));
-    const bool final_row = lane < 32 && row_vis && (bottom || (is_y ? li <= 12 : li <= 4));
     // stage the row's macroblock levels and inner-edge flags
     for (int i = lane; i < g.mb_w; i += 64) {
         const Vp8Mb& m = mbs[mby * g.mb_w + i];
@@ -731,27 +729,27 @@ __global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const
     for (int j = 0; j < 20; ++j) px[j] = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) fin[j] = 0;
-    uint32_t acc = 0;  // this lane's distortion of the samples it finalised
-    uint4 own = lf_ld16(rrow);                 // macroblock 0's row
-    uint4 srcn = make_uint4(0u, 0u, 0u, 0u);   // source row of the macroblock to account
-    auto account_mb = [&](int mbx_done, const uint4& s) {
-        if (!final_row) return;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const bool in = is_y ? mbx_done * 16 + j < g.width : (j < 8 && 2 * (mbx_done * 8 + j) < g.width);
-            const int e = fin[j] - (int)byte_of(s, is_y ? j : (2 * (j & 7) + comp));
-            acc += in ? (uint32_t)(e * e) : 0u;
-        }
+    uint4 own = lf_ld16(rrow);  // macroblock 0's row
+    int cons_seen = 0;          // the row below's ring progress last read (back-pressure)
+    // the first row of a workgroup: line word of the next macroblock, loaded a step ahead (other
+    // rows load their scratch: the same instruction stream) -- a workgroup boundary then costs one
+    // hand-off latency once, not a global round trip every step
+    const unsigned long long* const line_in =
+        glb_in ? line + ((size_t)(blockIdx.x - 1) * g.mb_w) * 32 + ml : reinterpret_cast<const unsigned long long*>(scratch) + 64 + ml;
+    const int line_step = glb_in ? 32 : 0;
+    uint64_t pre = __hip_atomic_load((const gu64*)line_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto pack4 = [&](int k) -> uint32_t {
+        return (uint32_t)fin[4 * k] | ((uint32_t)fin[4 * k + 1] << 8) | ((uint32_t)fin[4 * k + 2] << 16) |
+               ((uint32_t)fin[4 * k + 3] << 24);
     };
     auto store_mb = [&](int mbx_done) {
         uint32_t d[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            d[k] = (uint32_t)fin[4 * k] | ((uint32_t)fin[4 * k + 1] << 8) | ((uint32_t)fin[4 * k + 2] << 16) |
-                   ((uint32_t)fin[4 * k + 3] << 24);
-        // Cr lanes hand their 8 samples to the Cb lane of the same row
-        const uint32_t vlo = (uint32_t)__shfl((int)d[0], (lane + 8) & 63, 64);
-        const uint32_t vhi = (uint32_t)__shfl((int)d[1], (lane + 8) & 63, 64);
+        for (int k = 0; k < 4; ++k) d[k] = pack4(k);
+        // Cr lanes hand their 8 samples to the Cb lane of the same row: DPP row_ror:8 (lane l of a
+        // 16-lane row reads lane l ^ 8)
+        const uint32_t vlo = (uint32_t)__builtin_amdgcn_mov_dpp((int)d[0], 0x128, 0xF, 0xF, false);
+        const uint32_t vhi = (uint32_t)__builtin_amdgcn_mov_dpp((int)d[1], 0x128, 0xF, 0xF, false);
         uint32_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -767,11 +765,14 @@ __global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const
     unsigned long long* const line_out = line + (size_t)blockIdx.x * g.mb_w * 32;
     auto ring_put = [&](int mbx_done) {
         if (!ring_out && !wg_last) return;
-        if (ring_out) lf_wait_lds(&W[wr + 1].cons, mbx_done - kLfRing + 1, err);  // back-pressure
+        if (ring_out && cons_seen < mbx_done - kLfRing + 1) {  // back-pressure
+            lf_wait_lds(&W[wr + 1].cons, mbx_done - kLfRing + 1, err);
+            cons_seen = lf_lds_load(&W[wr + 1].cons);
+        }
         uint8_t* e = S.ring[mbx_done % kLfRing];
         if (is_y && li >= 12) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) e[(li - 12) * 16 + j] = (uint8_t)fin[j];
+            for (int k = 0; k < 4; ++k) *reinterpret_cast<uint32_t*>(e + (li - 12) * 16 + 4 * k) = pack4(k);
         } else if (!is_y && li >= 4) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) e[64 + (li - 4) * 16 + 2 * j + comp] = (uint8_t)fin[j];
@@ -818,23 +819,24 @@ __global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const
             }
             ring_put(mbx - 1);
             store_mb(mbx - 1);
-            account_mb(mbx - 1, srcn);
         }
-        // ---- the four rows above this macroblock (columns) and their source
+        // ---- the four rows above this macroblock (columns)
         int cl[20];
 #pragma unroll
         for (int k = 0; k < 20; ++k) cl[k] = 0;
         if (glb_in) {
-            const gu64* p = (const gu64*)(line + ((size_t)(blockIdx.x - 1) * g.mb_w + mbx) * 32 + ml);
-            uint64_t w = 0;
-            for (unsigned sp = 0;; ++sp) {
-                w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!__any((uint32_t)(w >> 32) != epoch)) break;
-                if (sp > kSpinLimit) {
-                    *err = 1;
-                    break;
+            uint64_t w = pre;
+            if (__any((uint32_t)(w >> 32) != epoch)) {  // not there yet: poll
+                const gu64* p = (const gu64*)(line_in + (size_t)mbx * line_step);
+                for (unsigned sp = 0;; ++sp) {
+                    __builtin_amdgcn_s_sleep(1);
+                    w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (!__any((uint32_t)(w >> 32) != epoch)) break;
+                    if (sp > kSpinLimit) {
+                        *err = 1;
+                        break;
+                    }
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) cl[k] = (int)((w >> (8 * k)) & 0xffu);
@@ -845,18 +847,24 @@ __global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const
             for (int k = 0; k < 4; ++k) cl[k] = (int)e[is_y ? k * 16 + li : 64 + k * 16 + 2 * li + comp];
             lf_lds_store(&S.cons, mbx + 1);  // (waits for the reads above)
         }
-        // the strip's source; prefetch this macroblock's source row (accounted next step) and the
-        // next macroblock's row.  (Unconditional vector memory instructions -- the top row uses
-        // its scratch words -- so the waits below count exactly.)
-        int ss[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 1; k < 4; ++k) ss[k] = (int)*(const g8*)(mby > 0 ? csrc + col_off(x0, k) : scratch + 64 * k + lane);
-        srcn = lf_ld16(srow + x0);
+        // prefetch the next macroblock's line word and row (unconditional: the waits count exactly)
+        pre = __hip_atomic_load((const gu64*)(line_in + (size_t)(mbx + 1 < g.mb_w ? mbx + 1 : mbx) * line_step),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         own = lf_ld16(rrow + (mbx + 1 < g.mb_w ? x0 + 16 : x0));
         if (level) {
+            if (is_y) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (is_y || j < 8) S.T[tb + li * tstride + j] = (uint8_t)px[4 + j];
+                for (int k = 0; k < 4; ++k)
+                    *reinterpret_cast<uint32_t*>(S.T + li * 16 + 4 * k) =
+                        (uint32_t)px[4 + 4 * k] | ((uint32_t)px[5 + 4 * k] << 8) | ((uint32_t)px[6 + 4 * k] << 16) |
+                        ((uint32_t)px[7 + 4 * k] << 24);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+                    *reinterpret_cast<uint32_t*>(S.T + tb + li * 8 + 4 * k) =
+                        (uint32_t)px[4 + 4 * k] | ((uint32_t)px[5 + 4 * k] << 8) | ((uint32_t)px[6 + 4 * k] << 16) |
+                        ((uint32_t)px[7 + 4 * k] << 24);
+            }
             lf_sync_wave();
 #pragma unroll
             for (int r = 0; r < 16; ++r) cl[4 + r] = is_y || r < 8 ? (int)S.T[tb + r * tstride + li] : 0;
@@ -873,49 +881,91 @@ __global__ __launch_bounds__(64 * kLfRows) void k_vp8_lf(h264::Geometry g, const
             for (int r = 0; r < 16; ++r)
                 if (is_y || r < 8) S.T[tb + r * tstride + li] = (uint8_t)cl[4 + r];
             lf_sync_wave();
+            if (is_y) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) fin[j] = is_y || j < 8 ? (int)S.T[tb + li * tstride + j] : 0;
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(S.T + li * 16 + 4 * k);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) fin[4 * k + b] = (int)((w >> (8 * b)) & 0xffu);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(S.T + tb + li * 8 + 4 * k);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) fin[4 * k + b] = (int)((w >> (8 * b)) & 0xffu);
+                }
+#pragma unroll
+                for (int j = 8; j < 16; ++j) fin[j] = 0;
+            }
             lf_sync_wave();
         } else {
 #pragma unroll
             for (int j = 0; j < 16; ++j) fin[j] = px[4 + j];
         }
-        // the strip above (rows 13..15 of the macroblock above): final now -- written back by this
-        // row (the row above wrote rows 0..12 only) and accounted here
-        {
-            const int xs = is_y ? x0 + li : (x0 >> 1) + li;  // sample column in its plane
-            const bool vis = mby > 0 && lane < 32 && (is_y ? xs < g.width : 2 * xs < g.width);
+        // the strip above (rows 13..15 of the macroblock above): final now, written back by this
+        // row (the row above wrote rows 0..12 only); the top row stores to its scratch words
 #pragma unroll
-            for (int k = 1; k < 4; ++k) {
-                *(g8*)(mby > 0 ? cplane + col_off(x0, k) : scratch + 64 * k + lane) = (uint8_t)cl[k];
-                const bool rv = is_y ? y0 - 4 + k < g.height : 2 * (cy0 - 4 + k) < g.height;
-                const int e = cl[k] - ss[k];
-                acc += vis && rv ? (uint32_t)(e * e) : 0u;
-            }
-        }
+        for (int k = 1; k < 4; ++k) *(g8*)(mby > 0 ? cplane + col_off(x0, k) : scratch + 64 * k + lane) = (uint8_t)cl[k];
         // left context of the next macroblock
 #pragma unroll
         for (int k = 0; k < 4; ++k) px[k] = is_y ? fin[12 + k] : fin[4 + k];
-        // the prefetched rows are taken here, inside the iteration (their waits count only the
-        // strip stores after them; taken at the top of the next iteration, the join with the
-        // loop entry made them a full vmcnt(0))
+        // the prefetched row is taken here, inside the iteration (its wait counts only the strip
+        // stores after it; taken at the top of the next iteration, the join with the loop entry
+        // made it a full vmcnt(0))
         {
-            uint32_t a0 = own.x, a1 = own.y, a2 = own.z, a3 = own.w, b0 = srcn.x, b1 = srcn.y, b2 = srcn.z, b3 = srcn.w;
-            asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3));
+            uint32_t a0 = own.x, a1 = own.y, a2 = own.z, a3 = own.w, p0 = (uint32_t)pre, p1 = (uint32_t)(pre >> 32);
+            asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(p0), "+v"(p1));
             own = make_uint4(a0, a1, a2, a3);
-            srcn = make_uint4(b0, b1, b2, b3);
+            pre = (uint64_t)p0 | ((uint64_t)p1 << 32);
         }
     }
     ring_put(g.mb_w - 1);
     store_mb(g.mb_w - 1);
-    account_mb(g.mb_w - 1, srcn);
-    const uint32_t sy = (uint32_t)wsum(lane < 32 && is_y ? (int)acc : 0), su = (uint32_t)wsum(lane < 32 && is_u ? (int)acc : 0),
-                   sv = (uint32_t)wsum(lane < 32 && !is_y && !is_u ? (int)acc : 0);
-    if (lane == 0) {
-        sse_rows[3 * mby] = sy;
-        sse_rows[3 * mby + 1] = su;
-        sse_rows[3 * mby + 2] = sv;
+}
+
+// Distortion of the filtered picture against the source: one workgroup per macroblock row,
+// partials per row and channel over the display area (the frame statistics).
+__global__ __launch_bounds__(256) void k_vp8_lf_sse(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                     const uint8_t* __restrict__ src_y,
+                                                     const uint8_t* __restrict__ src_uv,
+                                                     unsigned long long* __restrict__ sse_rows) {
+    __shared__ uint32_t part[3][4];
+    const Vp8FrameState& F = st->v;
+    const int mby = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t e[3] = {0, 0, 0};
+    // luma: 16 rows x coded_w, 4 samples per step; chroma: 8 rows x coded_w interleaved
+    const int lw4 = g.coded_w / 4;
+    for (int i = tid; i < 16 * lw4; i += 256) {
+        const int r = i / lw4, x = (i % lw4) * 4, y = mby * 16 + r;
+        if (y >= g.height) continue;
+        const uint32_t a = *reinterpret_cast<const uint32_t*>(F.rec_y + (size_t)y * g.pitch + x);
+        const uint32_t b = *reinterpret_cast<const uint32_t*>(src_y + (size_t)y * g.pitch + x);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int d = (int)((a >> (8 * k)) & 0xff) - (int)((b >> (8 * k)) & 0xff);
+            e[0] += x + k < g.width ? (uint32_t)(d * d) : 0u;
+        }
     }
+    for (int i = tid; i < 8 * lw4; i += 256) {
+        const int r = i / lw4, x = (i % lw4) * 4, cy = mby * 8 + r;
+        if (2 * cy >= g.height) continue;
+        const uint32_t a = *reinterpret_cast<const uint32_t*>(F.rec_uv + (size_t)cy * g.pitch + x);
+        const uint32_t b = *reinterpret_cast<const uint32_t*>(src_uv + (size_t)cy * g.pitch + x);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int d = (int)((a >> (8 * k)) & 0xff) - (int)((b >> (8 * k)) & 0xff);
+            e[1 + (k & 1)] += 2 * ((x + k) >> 1) < g.width ? (uint32_t)(d * d) : 0u;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t w = (uint32_t)wsum((int)e[c]);
+        if (lane == 0) part[c][wave] = w;
+    }
+    __syncthreads();
+    if (tid < 3)
+        sse_rows[3 * mby + tid] = (unsigned long long)part[tid][0] + part[tid][1] + part[tid][2] + part[tid][3];
 }
 
 // ------------------------------------------------------------------ hand-off to the host writer
@@ -997,8 +1047,9 @@ void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const ui
 
 void launch_vp8_lf(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                    hipStream_t stream) {
-    hipLaunchKernelGGL(k_vp8_lf, dim3((g.mb_h + kLfRows - 1) / kLfRows), dim3(64 * kLfRows), 0, stream, g, b.st, src_y,
-                       src_uv, b.mb, b.lf_line, b.lf_sse, b.err);
+    hipLaunchKernelGGL(k_vp8_lf<kLfRows>, dim3((g.mb_h + kLfRows - 1) / kLfRows), dim3(64 * kLfRows), 0, stream, g, b.st,
+                       b.mb, b.lf_line, b.err);
+    hipLaunchKernelGGL(k_vp8_lf_sse, dim3(g.mb_h), dim3(256), 0, stream, g, b.st, src_y, src_uv, b.lf_sse);
 }
 
 void launch_vp8_gather(const h264::Geometry& g, const Vp8DeviceBuffers& b, hipStream_t stream) {

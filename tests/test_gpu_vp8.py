@@ -152,12 +152,13 @@ def test_gpu_vp8_loop_filter_bit_exact_vs_cpu(gpu, w, h, qp, aq):
 
 
 def test_gpu_vp8_adaptive_loop_filter_1080p_pan(gpu):
-    """1080p synthetic desktop panning 2 px per frame (coherent motion), adaptive filter (the
-    default): GPU == CPU through the switch-on kStatsLag frames in, and depth 4 (frames in flight,
-    writer threads) gives the depth-1 bitstream."""
+    """1080p synthetic desktop panning 2 px per frame (coherent motion), adaptive filter
+    (deblock 2): GPU == CPU through the switch-on kStatsLag frames in, and depth 4 (frames in
+    flight, writer threads) gives the depth-1 bitstream."""
     w, h = 1920, 1080
     cfg = gpu.EncoderConfig()
     cfg.width, cfg.height, cfg.fps, cfg.qp, cfg.bitrate_kbps, cfg.search_range = w, h, 60, 34, 0, 16
+    cfg.deblock = 2
     genc, cenc = gpu.GpuVp8Encoder(cfg, _stream()), gpu.CpuVp8Encoder(cfg)
     y0, uv0 = desktop_nv12(gpu, w + 64, h, 0)
     srcs = [(np.ascontiguousarray(y0[:, 2 * t:2 * t + w]), np.ascontiguousarray(uv0[:, 2 * t:2 * t + w]))

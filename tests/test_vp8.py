@@ -229,14 +229,15 @@ def test_loop_filtered_inter_frames_decode_to_reconstruction(native, aq):
 
 
 def test_adaptive_loop_filter_follows_coherent_motion(native):
-    """deblock -1 (the VP8 default, adaptive): a still picture is never filtered; a pan switches
-    the filter on kStatsLag (4) frames after the first panned frame, and the bitstream says so."""
+    """deblock 2 (adaptive): a still picture is never filtered; a pan switches the filter on
+    kStatsLag (4) frames after the first panned frame, and the bitstream says so.  (The default,
+    -1, is off: no frame filtered.)"""
     w, h = 192, 128
     base, uv0 = _picture(w + 64, h, 9)
 
     def run(pan):
         c = native.EncoderConfig()
-        c.width, c.height, c.qp, c.bitrate_kbps, c.search_range = w, h, 32, 0, 16
+        c.width, c.height, c.qp, c.bitrate_kbps, c.search_range, c.deblock = w, h, 32, 0, 16, 2
         enc = native.CpuVp8Encoder(c)
         frames = []
         for t in range(9):
@@ -244,6 +245,8 @@ def test_adaptive_loop_filter_follows_coherent_motion(native):
             frames.append(enc.encode(np.ascontiguousarray(base[:, s:s + w]), np.ascontiguousarray(uv0[:, s:s + w])))
         return frames
 
+    dflt = native.EncoderConfig()
+    assert dflt.deblock == -1
     for pan, want in ((False, 0), (True, 4)):
         frames = run(pan)
         dec = Decoder()
