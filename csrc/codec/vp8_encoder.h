@@ -270,7 +270,7 @@ struct Vp8FrameState {
     int32_t hp_pitch;
     int32_t key;
     int32_t qindex;
-    int32_t epoch;          // nonzero, new every frame: key-frame wavefront progress tag (20 bits)
+    int32_t epoch;          // nonzero, new every frame: tag of the wavefront hand-off words (20 bits)
     int32_t segmented;      // inter frame with segment quantisers (temporal classes)
     int32_t aq;
     int32_t q[kNumSegs][6];   // per segment: Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
@@ -287,8 +287,7 @@ struct Vp8DeviceBuffers {
     Vp8States* st;         // device copy of the frame states
     Vp8Mb* mb;             // [nmb] records (device)
     int16_t* lv;           // [nmb * 400] levels (device)
-    uint32_t* prog;        // [mb_h] key-frame wavefront progress (epoch << 12 | MBs done)
-    uint64_t* line;        // [mb_h][coded_w / 4] key-frame hand-off: bottom luma + chroma rows
+    uint64_t* line;        // [mb_h][mb_w][8] key-frame hand-off: bottom luma + chroma rows, epoch-tagged
     int* err;              // mapped host word: nonzero if a wavefront spin timed out
     unsigned long long* lf_line;  // loop-filter hand-off lines (k_vp8_lf: epoch-tagged, per workgroup) + scratch
     unsigned long long* lf_sse;  // mapped host [mb_h][3]: Y / U / V distortion of the filtered picture

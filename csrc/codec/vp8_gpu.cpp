@@ -39,9 +39,8 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     HIP_CHECK(hipMalloc(&b.st, sizeof(Vp8States)));
     HIP_CHECK(hipMalloc(&b.mb, sizeof(Vp8Mb) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.prog, sizeof(uint32_t) * (size_t)geom_.mb_h));
-    HIP_CHECK(hipMemsetAsync(b.prog, 0, sizeof(uint32_t) * (size_t)geom_.mb_h, stream_));
-    HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * (size_t)geom_.mb_h * (geom_.coded_w / 4)));
+    HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * 8 * (size_t)geom_.mb_h * geom_.mb_w));
+    HIP_CHECK(hipMemsetAsync(b.line, 0, sizeof(uint64_t) * 8 * (size_t)geom_.mb_h * geom_.mb_w, stream_));  // tag 0: no frame
     // hand-off lines: 32 tagged words per macroblock per workgroup of rows, then 1 KB scratch per
     // row (k_vp8_lf); tags start at 0, never a frame's epoch
     const size_t lf_bytes = sizeof(uint64_t) * 32 * (size_t)geom_.mb_h * geom_.mb_w + 1024 * (size_t)(geom_.mb_h + 16);
@@ -62,7 +61,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
 
 void GpuVp8Encoder::free_slot(Slot& s) {
     Vp8DeviceBuffers& b = s.buf;
-    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.prog, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line})
+    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)b.err, (void*)b.mb_host, (void*)b.lv_host, (void*)s.st_host, (void*)b.lf_sse})
         if (p) (void)hipHostFree(p);

@@ -11,9 +11,9 @@
 // so the non-zero mask is one ballot.  The dead-zone division of the quantiser is an exact
 // multiply-high (Vp8FrameState::qm, exact for every coefficient the transforms produce).
 // Key frames predict from reconstructed neighbours: one wave per macroblock row walks its row,
-// the row below follows one macroblock behind, fed the bottom sample rows through an agent-scope
-// hand-off line and an epoch-tagged progress word (bounded spins; a timeout raises the mapped
-// error word instead of hanging).  (Rows stepping in lockstep groups with LDS hand-off lines
+// the row below follows one macroblock behind, fed the bottom sample rows through a hand-off
+// line of epoch-tagged 64-bit agent-scope atomics (bounded polls; a timeout raises the mapped
+// error word instead of hanging; no release fence per macroblock).  (Rows stepping in lockstep groups with LDS hand-off lines
 // measured slower -- 2.0 ms with 4-row, 4.1 ms with 16-row groups against 1.41 ms at 1080p:
 // the per-macroblock chain, not the hand-off, bounds the key frame; profiles/r04_vp8/NOTES.md.)
 // Inter frames segment their macroblocks by the temporal AQ classes (vp8_core.h Seg).  The boolean coder runs on host threads (vp8_bitstream.cpp);
@@ -272,6 +272,30 @@ __device__ __forceinline__ void store_rec(const MbLds& s, const h264::Geometry& 
     sse[2] = (uint32_t)wsum(vis ? ev * ev : 0);
 }
 
+// store_rec without the stores: the reconstruction's words (luma one per lane, chroma one per lane
+// < 32) and the distortion, for a store issued later (k_vp8_key defers it past the next poll)
+__device__ __forceinline__ void rec_words(const MbLds& s, const h264::Geometry& g, int x0, int y0, int lane,
+                                          uint32_t& wy, uint32_t& wuv, uint32_t sse[3]) {
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    wy = *reinterpret_cast<const uint32_t*>(s.rec + r * 16 + c4);
+    int ey = 0;
+    if (y0 + r < g.height)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = (int)s.src[r * 16 + c4 + j] - (int)s.rec[r * 16 + c4 + j];
+            ey += x0 + c4 + j < g.width ? e * e : 0;
+        }
+    const int o = (r & 7) * 8 + (c4 >> 1);
+    wuv = (uint32_t)s.ru[o] | ((uint32_t)s.rv[o] << 8) | ((uint32_t)s.ru[o + 1] << 16) | ((uint32_t)s.rv[o + 1] << 24);
+    const int cx = lane & 7, cy = lane >> 3;
+    const bool vis = 2 * (x0 / 2 + cx) < g.width && 2 * (y0 / 2 + cy) < g.height;
+    const int eu = (int)s.su[cy * 8 + cx] - (int)s.ru[cy * 8 + cx];
+    const int ev = (int)s.sv[cy * 8 + cx] - (int)s.rv[cy * 8 + cx];
+    sse[0] = (uint32_t)wsum(ey);
+    sse[1] = (uint32_t)wsum(vis ? eu * eu : 0);
+    sse[2] = (uint32_t)wsum(vis ? ev * ev : 0);
+}
+
 __device__ __forceinline__ void store_record(Vp8Mb* __restrict__ rec, int mvx, int mvy, int ymode, int uvmode,
                                              uint32_t nz, const uint32_t sse[3], int lane, int seg = 0) {
     if (lane == 0) {
@@ -441,24 +465,10 @@ __device__ __forceinline__ int dc_value(int sum, int cnt, int log2n) {
     return (sum + (1 << (shift - 1))) >> shift;
 }
 
-// bounded spin on the progress word of the row above (epoch << 12 | count)
-__device__ __forceinline__ void wait_row(const uint32_t* p, uint32_t epoch, int need, int* err) {
-    for (unsigned s = 0;; ++s) {
-        const uint32_t v = __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((v >> 12) == epoch && (int)(v & 0xfffu) >= need) break;
-        if (s > kSpinLimit) {
-            *err = 1;
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
-}
-
 __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8States* __restrict__ st,
                                                  const uint8_t* __restrict__ src_y,
                                                  const uint8_t* __restrict__ src_uv, Vp8Mb* __restrict__ mbs,
-                                                 int16_t* __restrict__ lv, uint32_t* __restrict__ prog,
+                                                 int16_t* __restrict__ lv,
                                                  uint64_t* __restrict__ line, int* __restrict__ err) {
     // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
     __builtin_amdgcn_s_setprio(3);
@@ -467,39 +477,80 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
     const Vp8FrameState& F = st->v;
     const int mby = blockIdx.x, lane = threadIdx.x, y0 = mby * 16;
     const uint32_t epoch = (uint32_t)F.epoch;
-    const int words = g.coded_w / 8;  // luma words per hand-off row; chroma follows
     const bool top = mby == 0, bottom = mby == g.mb_h - 1;
-    const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * 2 * words;
-    uint64_t* my_line = line + (size_t)mby * 2 * words;
+    // hand-off words of a macroblock: 0..3 its bottom luma row, 4..7 its bottom chroma row
+    // (interleaved), 32 samples each with the frame's epoch tag above them
+    const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * g.mb_w * 8;
+    uint64_t* my_line = line + (size_t)mby * g.mb_w * 8;
+    // the source of the next macroblock is fetched one macroblock ahead (registers), staged in LDS
+    // at the top of the iteration; the fetch is taken at the bottom of the iteration that issued
+    // it, so its wait counts the stores after it, not a vmcnt(0) at the loop's join
+    const int sr = lane >> 2, sc4 = (lane & 3) * 4;
+    auto fetch = [&](int x0n, uint32_t& wy, uint32_t& wuv) {
+        wy = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + sr) * g.pitch + x0n + sc4);
+        wuv = *reinterpret_cast<const uint32_t*>(src_uv + (size_t)(y0 / 2 + (sr & 7)) * g.pitch + x0n + sc4);
+    };
+    uint32_t nwy, nwuv;
+    fetch(0, nwy, nwuv);
+    // the finished macroblock's reconstruction words and record, stored one macroblock late (after
+    // the next poll, whose vmcnt(0) would otherwise wait for these stores)
+    uint32_t pwy = 0, pwuv = 0, psse[3] = {0, 0, 0};
+    int pmbx = -1, pym = 0, puvm = 0;
+    uint32_t pnz = 0;
+    auto flush = [&]() {
+        if (pmbx < 0) return;
+        const int r = lane >> 2, c4 = (lane & 3) * 4, px0 = pmbx * 16;
+        *reinterpret_cast<uint32_t*>(F.rec_y + (size_t)(y0 + r) * g.pitch + px0 + c4) = pwy;
+        if (lane < 32) *reinterpret_cast<uint32_t*>(F.rec_uv + (size_t)(y0 / 2 + r) * g.pitch + px0 + c4) = pwuv;
+        store_record(mbs + mby * g.mb_w + pmbx, 0, 0, pym, puvm, pnz, psse, lane);
+        pmbx = -1;
+    };
     for (int mbx = 0; mbx < g.mb_w; ++mbx) {
         const int x0 = mbx * 16, mbi = mby * g.mb_w + mbx;
         const bool left = mbx > 0;
-        stage_src(s, g, src_y, src_uv, x0, y0, lane);
+        {  // stage_src from the fetched words
+            *reinterpret_cast<uint32_t*>(s.src + sr * 16 + sc4) = nwy;
+            if (lane < 32) {
+                const int o = sr * 8 + (sc4 >> 1);
+                s.su[o] = (uint8_t)nwuv;  // U V U V
+                s.sv[o] = (uint8_t)(nwuv >> 8);
+                s.su[o + 1] = (uint8_t)(nwuv >> 16);
+                s.sv[o + 1] = (uint8_t)(nwuv >> 24);
+            }
+        }
         // ---- edges: above row and corner from the row above (hand-off line), left from our last MB
         if (!top) {
-            if (lane == 0) wait_row(prog + mby - 1, epoch, mbx + 1, err);
-            __syncthreads();
-            if (lane < 6) {
-                int wi = lane < 2 ? 2 * mbx + lane : (lane < 4 ? words + 2 * mbx + lane - 2 : (lane == 4 ? 2 * mbx - 1 : words + 2 * mbx - 1));
-                const bool need = lane < 4 || left;
-                const uint64_t w = need ? __hip_atomic_load((const gu64*)(above_line + wi), __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT)
-                                        : 0;
-                if (lane < 2) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) E.ay[8 * lane + k] = (int)((w >> (8 * k)) & 0xff);
-                } else if (lane < 4) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        E.au[4 * (lane - 2) + k] = (int)((w >> (16 * k)) & 0xff);
-                        E.av[4 * (lane - 2) + k] = (int)((w >> (16 * k + 8)) & 0xff);
-                    }
-                } else if (lane == 4) {
-                    E.cy = left ? (int)(w >> 56) : 129;
-                } else {
-                    E.cu = left ? (int)((w >> 48) & 0xff) : 129;
-                    E.cv = left ? (int)(w >> 56) : 129;
+            // the row above's words of this macroblock (lanes 0..7) and of the one before it (lanes
+            // 8, 9: the corner samples), polled until every needed word carries this frame's tag
+            // (tagged 64-bit agent-scope atomics: no release fence -- an L2 write-back -- per MB)
+            const bool need = lane < 8 || (lane < 10 && left);
+            const int wi = lane < 8 ? 8 * mbx + lane : 8 * (mbx - 1) + (lane == 8 ? 3 : 7);
+            const gu64* wp = (const gu64*)(above_line + (need ? wi : 0));
+            uint64_t w = 0;
+            for (unsigned sp = 0;; ++sp) {
+                w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!__any(need && (uint32_t)(w >> 32) != epoch)) break;
+                if (sp > kSpinLimit) {
+                    *err = 1;
+                    break;
                 }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            const uint32_t d = (uint32_t)w;
+            if (lane < 4) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) E.ay[4 * lane + k] = (int)((d >> (8 * k)) & 0xff);
+            } else if (lane < 8) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    E.au[2 * (lane - 4) + k] = (int)((d >> (16 * k)) & 0xff);
+                    E.av[2 * (lane - 4) + k] = (int)((d >> (16 * k + 8)) & 0xff);
+                }
+            } else if (lane == 8) {
+                E.cy = left ? (int)(d >> 24) : 129;
+            } else if (lane == 9) {
+                E.cu = left ? (int)((d >> 16) & 0xff) : 129;
+                E.cv = left ? (int)(d >> 24) : 129;
             }
         } else {
             if (lane < 16) E.ay[lane] = 127;
@@ -510,6 +561,8 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
             if (lane < 16) E.ly[lane] = 129;
             if (lane < 8) E.lu[lane] = E.lvv[lane] = 129;
         }
+        fetch(mbx + 1 < g.mb_w ? x0 + 16 : x0, nwy, nwuv);  // (after the poll: its waits drain all loads)
+        flush();  // the previous macroblock's reconstruction and record (after the poll, likewise)
         __syncthreads();
         // ---- mode decisions: SAD of the four 16x16 modes (4 samples per lane), the four chroma modes
         const int nav = top ? 0 : 1, nlf = left ? 1 : 0;
@@ -563,39 +616,36 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
         s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
         __syncthreads();
         const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane);
-        // ---- hand the bottom rows down, then publish progress
-        if (!bottom && lane < 4) {
-            uint64_t w = 0;
-            if (lane < 2) {
+        // ---- hand the bottom rows down: eight tagged words
+        if (!bottom && lane < 8) {
+            uint32_t d = 0;
+            if (lane < 4) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) w |= (uint64_t)s.rec[15 * 16 + 8 * lane + k] << (8 * k);
+                for (int k = 0; k < 4; ++k) d |= (uint32_t)s.rec[15 * 16 + 4 * lane + k] << (8 * k);
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    w |= ((uint64_t)s.ru[7 * 8 + 4 * (lane - 2) + k] << (16 * k)) |
-                         ((uint64_t)s.rv[7 * 8 + 4 * (lane - 2) + k] << (16 * k + 8));
+                for (int k = 0; k < 2; ++k)
+                    d |= ((uint32_t)s.ru[7 * 8 + 2 * (lane - 4) + k] << (16 * k)) |
+                         ((uint32_t)s.rv[7 * 8 + 2 * (lane - 4) + k] << (16 * k + 8));
             }
-            const int wi = lane < 2 ? 2 * mbx + lane : words + 2 * mbx + lane - 2;
-            __hip_atomic_store((gu64*)(my_line + wi), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gu64*)(my_line + 8 * mbx + lane), (uint64_t)d | ((uint64_t)epoch << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (!bottom) {
-            // every lane's hand-off words ordered before the flag: agent-scope release fence + store
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            if (lane == 0)
-                __hip_atomic_store((gu32*)(prog + mby), (epoch << 12) | (uint32_t)(mbx + 1), __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        uint32_t sse[3];
-        store_rec(s, g, F, x0, y0, lane, sse);
-        store_record(mbs + mbi, 0, 0, ymode, uvmode, nz, sse, lane);
+        rec_words(s, g, x0, y0, lane, pwy, pwuv, psse);
+        pmbx = mbx;
+        pym = ymode;
+        puvm = uvmode;
+        pnz = nz;
         // left edges of the next macroblock
         if (lane < 16) E.ly[lane] = s.rec[lane * 16 + 15];
         if (lane < 8) {
             E.lu[lane] = s.ru[lane * 8 + 7];
             E.lvv[lane] = s.rv[lane * 8 + 7];
         }
+        asm volatile("" : "+v"(nwy), "+v"(nwuv));  // the next source, fetched a macroblock ago
         __syncthreads();
     }
+    flush();
 }
 
 // ------------------------------------------------------------------ loop filter (15)
@@ -1041,7 +1091,7 @@ void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const ui
     if (save_src)  // the next inter frame's temporal classes compare against this source
         hipLaunchKernelGGL(k_vp8_save_src, dim3((g.coded_w / 4 + 255) / 256, g.coded_h), dim3(256), 0, stream, g, b.st,
                            src_y);
-    hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv, b.prog,
+    hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv,
                        b.line, b.err);
 }
 
