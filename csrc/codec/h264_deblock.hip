@@ -14,10 +14,10 @@
 //    through a per-wave LDS tile.  A row hands each finished macroblock's bottom lines (luma rows
 //    12..15, chroma rows 6..7: the p samples of the next row's top edge) down through an LDS ring
 //    with a progress counter (the row below waits only where its own top edge is filtered); the
-//    band's last row hands them to the next workgroup through global memory (agent-scope 64-bit
-//    atomic stores, an agent-scope release fence, then the progress flag with a release store; the
-//    consumer spins with relaxed loads and takes an agent-scope acquire fence before the payload:
-//    the HIP memory model's release / acquire pairing, cdna_hip_programming.md Guideline 16).
+//    band's last row hands them to the next workgroup (another XCD, another L2) through global
+//    memory as epoch-tagged 64-bit agent-scope atomic words -- 32 sample bits and the frame's tag
+//    -- which the consumer polls directly: no agent-scope release fence per macroblock (on gfx950
+//    a write-back of the XCD's whole L2, which set the pace of every row below the band).
 //    Every sample byte has exactly one writer: rows 13..15 of a macroblock whose lower neighbour
 //    filters its top edge are written by the row below, else by their own row.
 //    Macroblocks with every bS == 0 (static desktop, skips with equal vectors) cost a record read
@@ -161,22 +161,6 @@ __device__ __forceinline__ bool wait_lds(const int* p, int need, int* err) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     return true;
 }
-// bounded spin on a global progress word (epoch << 12 | count); returns the count seen
-__device__ __forceinline__ int wait_glb(uint32_t* p, uint32_t epoch, int need, int* err) {
-    for (unsigned s = 0;; ++s) {
-        const uint32_t v = __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((v >> 12) == epoch && (int)(v & 0xfffu) >= need) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
-            return (int)(v & 0xfffu);
-        }
-        if (s > kDbSpinLimit) {
-            *err = 1;
-            return need;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
 __device__ __forceinline__ void unpack16(const uint4& v, int* o) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -201,12 +185,34 @@ __device__ __forceinline__ int row_entry_qp(const FrameState* fs, const int* row
     return fs->qp;
 }
 
+// Band-boundary hand-off words: [plane][mb_h][mb_w][kDbGlbWords], each 32 payload bits (luma rows
+// 12..15 of the band's last row: words 0..15; chroma rows 6..7 interleaved: words 0..7; then the
+// MB's QP_Y) with the frame's epoch tag above them -- the consumer polls the words themselves, so
+// the producer needs no agent-scope release fence (a write-back of the XCD's L2) per macroblock.
+constexpr int kDbGlbWords = 24;
+constexpr int kDbQWord = 16;  // QP_Y word (luma; chroma uses word 8)
 struct DbGlobal {
-    uint64_t* glb;    // [2][mb_h][mb_w][8] hand-off lines of band-last rows (luma 8 x u64, chroma 4)
-    uint32_t* glq;    // [2][mb_h][mb_w] their QP_Y
-    uint32_t* gprog;  // [2][mb_h] epoch << 12 | MBs published
+    uint64_t* glb;    // [2][mb_h][mb_w][kDbGlbWords] tagged hand-off words of band-last rows
     int* err;         // mapped host word: a bounded spin timed out
 };
+// poll tagged words (lanes with need) until every one carries `epoch`; returns this lane's payload
+__device__ __forceinline__ uint32_t poll_tagged(const uint64_t* p, bool need, uint32_t epoch, int* err) {
+    uint64_t w = 0;
+    const gu64* wp = (const gu64*)p;
+    for (unsigned s = 0;; ++s) {
+        if (need) w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!__any(need && (uint32_t)(w >> 32) != epoch)) break;
+        if (s > kDbSpinLimit) {
+            *err = 1;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return (uint32_t)w;
+}
+__device__ __forceinline__ void put_tagged(uint64_t* p, uint32_t v, uint32_t epoch) {
+    __hip_atomic_store((gu64*)p, (uint64_t)v | ((uint64_t)epoch << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---------------------------------------------------------------- luma row engine
 __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4* __restrict__ rec,
@@ -225,7 +231,6 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
     int qprev = qrun;           // QP_Y of MB x-1
     int P[16], C[16];           // MB x-1 (row `lane`, post-H) and MB x (row `lane`)
     bool prev_mod = false;      // MB x-1 was modified (its own edges)
-    int seen_above = 0;         // band-first rows: progress of the row above already observed
     for (int k = 0; k < 16; ++k) P[k] = 0;
     // sample lines: batches of kDbPf macroblocks loaded one batch ahead into registers and parked in
     // the wave's LDS stage when their batch starts, so a load's latency spans kDbPf steps
@@ -293,28 +298,20 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                         *reinterpret_cast<uint4*>(S.lring[band_row][slot][lane - 12]) = pack16(P);
                     if (lane == 0) S.ringq[0][band_row][slot] = (uint8_t)qprev;
                 } else {
-                    uint64_t* dst = G.glb + ((size_t)(0 * g.mb_h + mby) * mb_w + xp) * 8;
+                    uint64_t* dst = G.glb + ((size_t)(0 * g.mb_h + mby) * mb_w + xp) * kDbGlbWords;
                     if (lane >= 12 && act) {
                         const uint4 v = pack16(P);
-                        __hip_atomic_store((gu64*)(dst + 2 * (lane - 12)), (uint64_t)v.x | ((uint64_t)v.y << 32),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store((gu64*)(dst + 2 * (lane - 12) + 1), (uint64_t)v.z | ((uint64_t)v.w << 32),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        put_tagged(dst + 4 * (lane - 12), v.x, epoch);
+                        put_tagged(dst + 4 * (lane - 12) + 1, v.y, epoch);
+                        put_tagged(dst + 4 * (lane - 12) + 2, v.z, epoch);
+                        put_tagged(dst + 4 * (lane - 12) + 3, v.w, epoch);
                     }
-                    if (lane == 0)
-                        __hip_atomic_store((gu32*)(G.glq) + (size_t)(0 * g.mb_h + mby) * mb_w + xp, (uint32_t)qprev,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) put_tagged(dst + kDbQWord, (uint32_t)qprev, epoch);
                 }
             }
             if (!band_last) {
                 lds_sync_wave();
                 if (lane == 0) lds_store(prog_me, x);
-            } else if (!pic_last && below_top) {
-                // every lane's payload stores ordered before the flag (agent-scope release)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                if (lane == 0)
-                    __hip_atomic_store((gu32*)(G.gprog) + 0 * g.mb_h + mby, (epoch << 12) | (uint32_t)x, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         if (!have) break;
@@ -333,20 +330,13 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                             *reinterpret_cast<const uint4*>(S.lring[band_row - 1][slot][lane]);
                     qtop = S.ringq[0][band_row - 1][slot];
                 } else {
-                    if (seen_above < x + 1) seen_above = wait_glb(G.gprog + 0 * g.mb_h + mby - 1, epoch, x + 1, G.err);
-                    const uint64_t* src = G.glb + ((size_t)(0 * g.mb_h + mby - 1) * mb_w + x) * 8;
-                    if (lane < 4) {
-                        const uint64_t a = __hip_atomic_load((const gu64*)(src + 2 * lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t b = __hip_atomic_load((const gu64*)(src + 2 * lane + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        *reinterpret_cast<uint4*>(tile[lane]) =
-                            make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-                    }
-                    qtop = (int)__hip_atomic_load((const gu32*)(G.glq) + (size_t)(0 * g.mb_h + mby - 1) * mb_w + x, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                    // retire the hand-off loads here: left pending, the compiler's wait at the
-                    // merge below (every row's H phase) would be a vmcnt(0) on all rows, draining
-                    // their line prefetch and stores every macroblock
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                    // rows 12..15 of the band above (lanes 0..15, a word each) and its QP_Y (lane 16);
+                    // the poll retires its loads here (left pending, the compiler's wait at the merge
+                    // below would be a vmcnt(0) on every row's H phase)
+                    const uint64_t* src = G.glb + ((size_t)(0 * g.mb_h + mby - 1) * mb_w + x) * kDbGlbWords;
+                    const uint32_t v = poll_tagged(src + (lane <= kDbQWord ? lane : 0), lane <= kDbQWord, epoch, G.err);
+                    if (lane < 16) *reinterpret_cast<uint32_t*>(&tile[lane >> 2][4 * (lane & 3)]) = v;
+                    qtop = __builtin_amdgcn_readlane((int)v, kDbQWord);
                 }
             }
             if (act) *reinterpret_cast<uint4*>(tile[4 + lane]) = pack16(C);
@@ -412,7 +402,6 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
     int qprev = qrun;
     int P[8], C[8];
     bool prev_mod = false;
-    int seen_above = 0;
     for (int k = 0; k < 8; ++k) P[k] = 0;
     auto load_line = [&](const uint4& v, int* o) {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -486,17 +475,11 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                                 *reinterpret_cast<const uint4*>(tile[8 + lane]);
                         if (lane == 0) S.ringq[1][band_row][slot] = (uint8_t)qprev;
                     } else {
-                        uint64_t* dst = G.glb + ((size_t)(1 * g.mb_h + mby) * mb_w + xp) * 8;
-                        if (lane < 2) {
-                            const uint4 v = *reinterpret_cast<const uint4*>(tile[8 + lane]);
-                            __hip_atomic_store((gu64*)(dst + 2 * lane), (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                            __hip_atomic_store((gu64*)(dst + 2 * lane + 1), (uint64_t)v.z | ((uint64_t)v.w << 32),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        if (lane == 0)
-                            __hip_atomic_store((gu32*)(G.glq) + (size_t)(1 * g.mb_h + mby) * mb_w + xp, (uint32_t)qprev,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        uint64_t* dst = G.glb + ((size_t)(1 * g.mb_h + mby) * mb_w + xp) * kDbGlbWords;
+                        if (lane < 8)
+                            put_tagged(dst + lane, *reinterpret_cast<const uint32_t*>(&tile[8 + (lane >> 2)][4 * (lane & 3)]),
+                                       epoch);
+                        if (lane == 0) put_tagged(dst + 8, (uint32_t)qprev, epoch);
                     }
                 }
                 lds_sync_wave();  // tile reads done before it is rewritten
@@ -504,11 +487,6 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
             if (!band_last) {
                 lds_sync_wave();
                 if (lane == 0) lds_store(prog_me, x);
-            } else if (!pic_last && below_top) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // payload before the flag
-                if (lane == 0)
-                    __hip_atomic_store((gu32*)(G.gprog) + 1 * g.mb_h + mby, (epoch << 12) | (uint32_t)x, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         if (!have) break;
@@ -525,20 +503,10 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                             *reinterpret_cast<const uint4*>(S.cring[band_row - 1][slot][lane]);
                     qtop = S.ringq[1][band_row - 1][slot];
                 } else {
-                    if (seen_above < x + 1) seen_above = wait_glb(G.gprog + 1 * g.mb_h + mby - 1, epoch, x + 1, G.err);
-                    const uint64_t* src = G.glb + ((size_t)(1 * g.mb_h + mby - 1) * mb_w + x) * 8;
-                    if (lane < 2) {
-                        const uint64_t a = __hip_atomic_load((const gu64*)(src + 2 * lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t b = __hip_atomic_load((const gu64*)(src + 2 * lane + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        *reinterpret_cast<uint4*>(tile[lane]) =
-                            make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-                    }
-                    qtop = (int)__hip_atomic_load((const gu32*)(G.glq) + (size_t)(1 * g.mb_h + mby - 1) * mb_w + x, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                    // retire the hand-off loads here: left pending, the compiler's wait at the
-                    // merge below (every row's H phase) would be a vmcnt(0) on all rows, draining
-                    // their line prefetch and stores every macroblock
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                    const uint64_t* src = G.glb + ((size_t)(1 * g.mb_h + mby - 1) * mb_w + x) * kDbGlbWords;
+                    const uint32_t v = poll_tagged(src + (lane <= 8 ? lane : 0), lane <= 8, epoch, G.err);
+                    if (lane < 8) *reinterpret_cast<uint32_t*>(&tile[lane >> 2][4 * (lane & 3)]) = v;
+                    qtop = __builtin_amdgcn_readlane((int)v, 8);
                 }
             }
             if (act) to_tile(2 + ln, C);
@@ -671,7 +639,7 @@ void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* sr
                     hipStream_t stream) {
     if (g.mb_w > kDbMaxW || g.mb_h > kMaxSlices) throw std::invalid_argument("launch_deblock: picture too large");
     hipLaunchKernelGGL(k_db_prep, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, b.mb, b.db_rec, b.db_rowq);
-    DbGlobal G{b.db_glb, b.db_glq, b.db_gprog, b.db_err};
+    DbGlobal G{b.db_glb, b.db_err};
     hipLaunchKernelGGL(k_deblock, dim3((g.mb_h + kDbRows - 1) / kDbRows, 2), dim3(64 * kDbRows), 0, stream, g, b.fs,
                        b.db_rec, b.db_rowq, G);
     hipLaunchKernelGGL(k_db_sse, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, src_y, src_uv);

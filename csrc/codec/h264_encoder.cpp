@@ -266,10 +266,8 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipMalloc(&b.intra_cand, sizeof(int) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.db_rec, sizeof(uint4) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.db_rowq, sizeof(int) * (size_t)geom_.mb_h));
-    HIP_CHECK(hipMalloc(&b.db_glb, sizeof(uint64_t) * 2 * 8 * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.db_glq, sizeof(uint32_t) * 2 * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.db_gprog, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h));
-    HIP_CHECK(hipMemsetAsync(b.db_gprog, 0, sizeof(uint32_t) * 2 * (size_t)geom_.mb_h, stream_));
+    HIP_CHECK(hipMalloc(&b.db_glb, sizeof(uint64_t) * 2 * 24 * (size_t)nmb));
+    HIP_CHECK(hipMemsetAsync(b.db_glb, 0, sizeof(uint64_t) * 2 * 24 * (size_t)nmb, stream_));  // tag 0: no frame
     HIP_CHECK(hipMalloc(&b.pack_done, sizeof(uint32_t)));
     HIP_CHECK(hipMemsetAsync(b.pack_done, 0, sizeof(uint32_t), stream_));
     HIP_CHECK(hipMalloc(&b.db_cnt, sizeof(uint32_t) * 4));
@@ -291,7 +289,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     for (void* p : {(void*)b.fs, (void*)b.mb, (void*)b.coef, (void*)b.slot, (void*)b.slot_bits, (void*)b.row_agg,
                     (void*)b.row_sse, (void*)b.coded_info, (void*)b.slice_info,
                     (void*)b.out_hdr, (void*)b.sse_part, (void*)b.wave_prog, (void*)b.mb_sse, (void*)b.intra_gain, (void*)b.intra_cand, (void*)b.quad_unit,
-                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.db_glq, (void*)b.db_gprog, (void*)b.pack_done, (void*)b.db_cnt})
+                    (void*)b.db_rec, (void*)b.db_rowq, (void*)b.db_glb, (void*)b.pack_done, (void*)b.db_cnt})
         if (p) (void)hipFree(p);
     if (b.db_err) (void)hipHostFree(b.db_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);

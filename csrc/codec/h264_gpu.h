@@ -80,7 +80,7 @@ struct FrameState {
     int32_t me_coarse;     // 1 = even-offset grid + integer neighbours instead of the full search
     int32_t intra4x4;      // 0 = intra MBs are Intra16x16 only
     int32_t deblock_off;   // disable_deblocking_filter_idc (0: k_deblock filters the reconstruction)
-    int32_t db_epoch;      // nonzero, new every frame: tag of k_deblock's cross-workgroup progress words
+    int32_t db_epoch;      // nonzero, new every frame: tag of k_deblock's cross-workgroup hand-off words
     int32_t pic_init_qp;
     int32_t chroma_qp_offset;
     int32_t log2_max_frame_num;
@@ -163,9 +163,7 @@ struct DeviceBuffers {
     // in-loop deblocking (h264_deblock.hip)
     uint4* db_rec;          // [nmb] boundary strengths + QP record per MB (k_db_prep)
     int* db_rowq;           // [mb_h] QP of each row's last mb_qp_delta MB (-1: none)
-    uint64_t* db_glb;       // [2][mb_h][mb_w][8] band-boundary hand-off lines
-    uint32_t* db_glq;       // [2][mb_h][mb_w] their QP
-    uint32_t* db_gprog;     // [2][mb_h] band-boundary progress words (epoch << 12 | count)
+    uint64_t* db_glb;       // [2][mb_h][mb_w][24] band-boundary hand-off words (epoch-tagged, k_deblock)
     int* db_err;            // mapped host word: nonzero if a deblocking spin timed out
     uint32_t* db_cnt;       // [3] adaptive filter: coherent / changed / moving counts (k_scan_rows, zeroed by k_scan_out)
     uint32_t* pack_done;    // [1] k_pack workgroups finished (the last one stamps t_end and resets it)
