@@ -2501,12 +2501,12 @@ constexpr uint32_t kCostPerSlice = 2048;  // EncoderConfig::hevc_slice_cost defa
 constexpr uint32_t kMaxCuCost = 1u + (384u >> 2) + 15u * 24u + ((21u * 255u) >> 3);
 // Slices are laid out in whole CTBs: the largest CTB cost (four units)
 constexpr uint32_t kMaxCtbCost = 4u * kMaxCuCost;
-// Number of slices for a P picture of total cost T, bounded by the level's slice limit.  At least
-// kMaxCtbCost + 1 per slice: then consecutive thresholds ceil(s * T / S) lie further apart than any
-// CU's cost, no CU spans two of them, and plan_slice_of() is also a CU's slice rank (the GPU layout
-// places every CU from its own prefix).
+// Number of slice thresholds for a P picture of total cost T, bounded by the level's slice limit.
+// A CTB costlier than the spacing T / S spans several thresholds, so the picture may get fewer
+// slices than S: slices start where plan_slice_of changes and are ranked by those starts
+// (plan_p_slices; k_hevc_layout compacts the ranks).
 MXHD int plan_num_slices(uint64_t total, int max_slices, uint32_t cost_per_slice = kCostPerSlice) {
-    const uint32_t cps = cost_per_slice > kMaxCtbCost ? cost_per_slice : kMaxCtbCost + 1u;
+    const uint32_t cps = cost_per_slice > 0 ? cost_per_slice : 1u;
     const uint64_t s = total / cps;
     return s < 1 ? 1 : (s > (uint64_t)max_slices ? max_slices : (int)s);
 }

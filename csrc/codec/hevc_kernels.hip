@@ -1442,12 +1442,13 @@ __device__ __forceinline__ uint32_t tile_thread_prefix(const uint32_t (*wave_tot
     return before + wave_incl_scan(sum4) - sum4;
 }
 
-// Slice layout, one workgroup per scan tile.  P pictures: cost-balanced raster runs --
-// plan_num_slices keeps every slice above the largest CU cost, so no CU spans two slice
-// thresholds and a CU's slice id (plan_slice_of of its cost prefix) is also its slice's rank:
-// every CU places itself from its prefix alone (the former one-workgroup kernel walked the
-// tiles in sequence: 39 us at 4K).
-// (Everything here counts 32x32 CTBs: ncu = the CTB count, ctb_w = CTBs per row, cost per CTB.)
+// Slice layout, one workgroup per scan tile.  P pictures: cost-balanced raster runs -- a CTB's
+// slice id is plan_slice_of of its cost prefix, a slice starts where the id changes, and a slice's
+// rank counts the starts before it: a CTB heavier than the slice spacing skips ids, so ranks are
+// compacted (every workgroup counts the starts of the tiles before its own -- a block reduction per
+// earlier tile, cheaper than chaining the workgroups).  (Until round 5 the spacing was kept above
+// the largest possible CTB cost so that ids were ranks; with CTB32 that cost is 4,504 and held a 4K
+// P picture to ~107 slices of the level's 200: the slowest CABAC substream 870 us.)
 __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __restrict__ fs,
                                                        const uint32_t* __restrict__ cost, int ncu, int ctb_w,
                                                        int max_slices, int slice_cost, int* __restrict__ slice_first,
@@ -1468,23 +1469,52 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
     __shared__ uint32_t tile_pre[kMaxScanTiles];
     __shared__ uint32_t wave_tot[kMaxScanTiles][16];
     __shared__ uint32_t total_sh;
+    __shared__ uint32_t wave_starts[16];
     const uint32_t total = tile_prefixes(cost, ncu, wave_tot, tile_pre, &total_sh);
     const int S = plan_num_slices(total, max_slices, (uint32_t)slice_cost);
-    const int i0 = t * kScanTile + 4 * tid;
-    const uint4 v = ld4(cost, i0);
-    const uint32_t c4[4] = {v.x, v.y, v.z, v.w};
-    uint64_t pre = tile_thread_prefix(wave_tot, tile_pre, t, v.x + v.y + v.z + v.w);
-    if (i0 < ncu) {
-        int prev = i0 > 0 ? plan_slice_of(pre - cost[i0 - 1], total, S) : -1;
-        for (int e = 0; e < 4 && i0 + e < ncu; ++e) {
-            const int id = plan_slice_of(pre, total, S);
-            if (id != prev) slice_first[id] = i0 + e;
-            slice_of_cu[i0 + e] = id;
-            prev = id;
+    const int wv = tid >> 6, nwv = (int)blockDim.x >> 6;
+    uint32_t base = 0;  // slice starts in the tiles before this one
+    for (int tt = 0; tt <= t; ++tt) {
+        const int i0 = tt * kScanTile + 4 * tid;
+        const uint4 v = ld4(cost, i0);
+        const uint32_t c4[4] = {v.x, v.y, v.z, v.w};
+        uint64_t pre = tile_thread_prefix(wave_tot, tile_pre, tt, v.x + v.y + v.z + v.w);
+        int id[4];
+        uint32_t st = 0;  // bit e: CTB i0 + e starts a slice
+        int prev = i0 > 0 && i0 < ncu ? plan_slice_of(pre - cost[i0 - 1], total, S) : -1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            id[e] = plan_slice_of(pre, total, S);
+            if (i0 + e < ncu && id[e] != prev) st |= 1u << e;
+            prev = id[e];
             pre += c4[e];
         }
+        const uint32_t cnt = (uint32_t)__popc(st);
+        const uint32_t incl = wave_incl_scan(cnt);
+        if ((tid & 63) == 63) wave_starts[wv] = incl;
+        __syncthreads();
+        uint32_t before = base, tile_cnt = 0;
+        for (int w = 0; w < nwv; ++w) {
+            if (w < wv) before += wave_starts[w];
+            tile_cnt += wave_starts[w];
+        }
+        __syncthreads();
+        if (tt < t) {
+            base += tile_cnt;
+            continue;
+        }
+        int r = (int)(before + incl - cnt) - 1;  // rank of the slice holding the CTB before i0
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (i0 + e >= ncu) break;
+            if ((st >> e) & 1u) {
+                ++r;
+                slice_first[r] = i0 + e;
+            }
+            slice_of_cu[i0 + e] = r;
+        }
+        if (tid == 0 && (t + 1) * kScanTile >= ncu) *nslices = base + tile_cnt;  // the last tile's workgroup
     }
-    if (t == 0 && tid == 0) *nslices = (uint32_t)S;
 }
 
 // Skip / merge / AMVP of the units of a P picture against their slice's neighbours and the coding
