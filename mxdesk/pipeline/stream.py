@@ -5,8 +5,10 @@ desktop + CPU H.264 encoder for the plumbing configuration), produces frames at 
 rate on a dedicated thread and pushes each encoded access unit to every subscriber queue
 (asyncio-safe).  Policies:
   * a new viewer or a PLI/keyframe request forces an IDR on the next frame;
-  * a viewer whose queue overflows is resynchronised: its backlog is dropped and it waits
-    for the next IDR (counted in ``mxdesk_dropped_frames``);
+  * a viewer whose queue overflows is resynchronised: its backlog is dropped, it waits for the
+    next IDR and the pipeline forces one (counted in ``mxdesk_dropped_frames``; without the
+    forced IDR such a viewer received nothing more -- no gap to NACK, no PLI -- until the
+    stream's next key frame: the stalls of the 96-viewer density runs, profiles/r05_density);
   * a watchdog restarts the encoder session if no frame was produced for ``stall_s``;
   * ``MXDESK_FAULT`` (tests only) injects failures: ``drop:N`` drops every Nth frame,
     ``stall:S`` stalls the producer once for S seconds, ``crash:N`` raises at frame N.
@@ -313,8 +315,14 @@ class StreamPipeline:
         with self._lock:
             subs = list(self._subs)
         for s in subs:
-            s.offer(fr, self.metrics.on_drop)
+            s.offer(fr, self._on_sub_overflow)
         return fr
+
+    def _on_sub_overflow(self, n: int) -> None:
+        """A viewer's queue overflowed (event-loop thread): count the dropped frames and force an
+        IDR so that viewer resynchronises at the next frame."""
+        self.metrics.on_drop(n)
+        self._force_idr = True
 
     def _run(self) -> None:
         # pacing phase (seconds into the frame period): sessions of one process start staggered

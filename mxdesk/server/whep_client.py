@@ -74,6 +74,9 @@ class WhepResult:
     dc_audio: list[bytes] = field(default_factory=list)   # MXA1 chunks from the "audio" channel
     dc_sent: int = 0
     dc_labels: list[str] = field(default_factory=list)  # server-opened channels (selkies "input")
+    stage: str = "post"    # diagnostics: post / ice / dtls / media -- where a failed session stopped
+    ice_tx: int = 0        # ICE binding requests sent (retransmissions included)
+    datagrams: int = 0     # datagrams received
 
 
 def e2e_latency_ms(res: WhepResult) -> list[float]:
@@ -140,6 +143,9 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
                             drop_seq_every=drop_seq_every, pli_after=pli_after, dc_messages=dc_messages,
                             dc_wait_stats=dc_wait_stats, via_relay=via_relay, dc_audio_chunks=dc_audio_chunks,
                             simulate_loss=simulate_loss)
+    except Exception as e:
+        e.whep_result = res  # (the diagnostics of a failed session: stage, counters)
+        raise
     finally:
         try:
             async with aiohttp.ClientSession(headers={"Authorization": auth.encode()} if auth else None) as s:
@@ -185,7 +191,9 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
         # retransmitted like a browser's ICE agent (RFC 8445 / 5389: RTO from 250 ms, doubling):
         # a single lost check must not stall the session until the deadline
         req_bytes = req.encode(r_pwd.encode())
+        res.stage = "ice"
         tr.sendto(req_bytes)
+        res.ice_tx += 1
         rto, next_tx = 0.25, time.monotonic() + 0.25
         while True:
             try:
@@ -194,15 +202,18 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                 if time.monotonic() > deadline:
                     raise
                 tr.sendto(req_bytes)
+                res.ice_tx += 1
                 rto = min(rto * 2, 2.0)
                 next_tx = time.monotonic() + rto
                 continue
+            res.datagrams += 1
             if S.is_stun(d):
                 m = S.StunMessage.decode(d)
                 if m.type == S.BINDING_SUCCESS and m.tid == req.tid:
                     if not m.check_integrity(r_pwd.encode()):
                         raise RuntimeError("bad MESSAGE-INTEGRITY in binding response")
                     break
+        res.stage = "dtls"
         for dg in dtls.start():
             tr.sendto(dg)
         while not dtls.handshake_done:
@@ -366,6 +377,7 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
             auto_nacked.update(new)
             res.nacked += len(new)
 
+        res.stage = "media"
         while len(res.aus) < n_frames or dc_pending():
             if dc is not None and time.monotonic() - last_tick > 0.05:
                 sctp_out(dc.tick())

@@ -174,6 +174,9 @@ def test_pipeline_fault_injection_restarts(monkeypatch):
 
 
 def test_slow_client_resync():
+    """A viewer whose queue overflows loses its backlog and waits for an IDR -- which the overflow
+    itself forces, so the viewer resumes at the next frame (without it the viewer stalled until
+    the stream's next key frame)."""
     pipe = StreamPipeline(64, 48, 60, backend="cpu", bitrate_kbps=0, queue_frames=2)
 
     async def go():
@@ -184,11 +187,18 @@ def test_slow_client_resync():
         got = []
         while not sub.queue.empty():
             got.append(sub.queue.get_nowait())
-        return sub, got
+        state = (sub.dropped, sub.need_idr)
+        fr = pipe.step()
+        await asyncio.sleep(0.05)
+        after = []
+        while not sub.queue.empty():
+            after.append(sub.queue.get_nowait())
+        return sub, state, fr, after
 
-    sub, got = run(go())
-    assert sub.dropped > 0 and sub.need_idr  # backlog dropped, waiting for the next IDR
+    sub, (dropped, waiting), fr, after = run(go())
+    assert dropped > 0 and waiting  # backlog dropped, waiting for the next IDR
     assert pipe.metrics.dropped.labels("0")._value.get() > 0
+    assert fr.idr and after and after[0].idr and not sub.need_idr  # the forced IDR resynchronised it
 
 
 def test_hevc_stream_over_websocket():

@@ -67,7 +67,11 @@ def _client_proc(ports, frames, q):
         try:
             res = await whep_view(f"http://127.0.0.1:{p}/whep", frames, timeout=frames / 30.0 + 60)
         except Exception as e:  # a stalled session is a failure of this K, not of the tool
-            return {"port": p, "error": repr(e)}
+            r = getattr(e, "whep_result", None)
+            diag = {} if r is None else {"stage": r.stage, "ice_tx": r.ice_tx, "datagrams": r.datagrams,
+                                          "aus": len(r.aus), "nacked": r.nacked, "gave_up": r.gave_up,
+                                          "dropped_aus": r.dropped_aus}
+            return {"port": p, "error": repr(e), "diag": diag}
         arr = res.arrival_wall
         warm = min(30, len(arr) // 4)
         span = arr[-1] - arr[warm] if len(arr) > warm + 1 else 0.0
@@ -137,7 +141,7 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir
     return {"k": k, "passed": passed, "min_fps": round(min(fps), 2) if fps else 0.0,
             "mean_fps": round(statistics.mean(fps), 2) if fps else 0.0, "p50_e2e_ms": round(p50, 3),
             "p95_e2e_ms": round(p95, 3), "lost_packets": sum(r["lost"] for r in ok), "errors": [e["error"] for e in errs][:3],
-            "failed_ports": sorted(e["port"] - base for e in errs)}
+            "failed_ports": sorted(e["port"] - base for e in errs), "failed_diag": [e.get("diag") for e in errs][:16]}
 
 
 def main():
