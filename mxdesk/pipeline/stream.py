@@ -107,7 +107,7 @@ class StreamPipeline:
     def __init__(self, width: int, height: int, fps: int, *, backend: str = "gpu", device: int = 0,
                  bitrate_kbps: int = 8000, keyint: int = 0, search_range: int = 16, subpel: bool = True,
                  noise: bool = True, out_width: int = 0, out_height: int = 0, session_name: str = "0",
-                 capture: Any = None, metrics: SessionMetrics | None = None, queue_frames: int = 8,
+                 capture: Any = None, metrics: SessionMetrics | None = None, queue_frames: int | None = None,
                  stall_s: float = 2.0, paced: bool = True, codec: str = "h264"):
         if codec not in CODEC_IDS:
             raise ValueError(f"unknown codec {codec!r} (h264 | hevc | vp8)")
@@ -120,7 +120,9 @@ class StreamPipeline:
         self.device = device
         self.capture = capture
         self.metrics = metrics or SessionMetrics(session_name)
-        self.queue_frames = queue_frames
+        # frames a viewer may fall behind before it is resynchronised (MXDESK_VIEWER_QUEUE; 16 =
+        # 267 ms at 60 fps: 8 resynchronised viewers of busy serve processes, profiles/r05_density)
+        self.queue_frames = int(queue_frames or os.environ.get("MXDESK_VIEWER_QUEUE", "") or 16)
         self.stall_s = stall_s
         self.paced = paced
         self.bitrate_kbps = bitrate_kbps  # configured CBR target (congestion control upper bound)

@@ -108,7 +108,7 @@ class _Client(asyncio.DatagramProtocol):
 async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
                     timeout: float = 30.0, dc_messages: list[str] | None = None,
                     dc_wait_stats: bool = False, via_relay: bool = False, dc_audio_chunks: int = 0,
-                    simulate_loss: float = 0.0) -> WhepResult:
+                    simulate_loss: float = 0.0, lite: bool = False) -> WhepResult:
     """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
 
     ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
@@ -122,6 +122,11 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     the client's automatic NACK / PLI repair brings them back.
     ``via_relay``: connect to the server's TURN relay candidate instead of its host candidate
     (the offer then carries a host candidate so the server can create the TURN permission).
+    ``lite``: count frames from the plaintext RTP headers (a frame = the packets of one timestamp,
+    complete when its marker packet arrives with no sequence gap) instead of decrypting and
+    depacketising every packet -- ICE, DTLS, the server's SRTP and RTCP sender reports are the
+    same; for density runs where a hundred Python viewers share the server's host (``aus`` then
+    holds empty placeholders).
     """
     import aiohttp
 
@@ -142,7 +147,7 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
         await media_session(res, res.answer, dtls, ufrag, N, n_frames, t0, timeout=timeout,
                             drop_seq_every=drop_seq_every, pli_after=pli_after, dc_messages=dc_messages,
                             dc_wait_stats=dc_wait_stats, via_relay=via_relay, dc_audio_chunks=dc_audio_chunks,
-                            simulate_loss=simulate_loss)
+                            simulate_loss=simulate_loss, lite=lite)
     except Exception as e:
         e.whep_result = res  # (the diagnostics of a failed session: stage, counters)
         raise
@@ -161,7 +166,7 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                         timeout: float = 30.0, drop_seq_every: int = 0, pli_after: int = 0,
                         dc_messages: list[str] | None = None, dc_wait_stats: bool = False, via_relay: bool = False,
                         dc_audio_chunks: int = 0, simulate_loss: float = 0.0,
-                        server_channel: str | None = None) -> None:
+                        server_channel: str | None = None, lite: bool = False) -> None:
     """The browser side of an established negotiation (remote SDP = the server's answer for
     WHEP, its offer for the selkies protocol): ICE check, DTLS client, SRTP receive with NACK /
     PLI repair, data channels.  ``server_channel``: the server opens that channel (selkies
@@ -378,6 +383,9 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
             res.nacked += len(new)
 
         res.stage = "media"
+        lite_ts = None       # lite: timestamp of the frame being received, its next expected seq
+        lite_next = None
+        lite_ok = True
         while len(res.aus) < n_frames or dc_pending():
             if dc is not None and time.monotonic() - last_tick > 0.05:
                 sctp_out(dc.tick())
@@ -404,6 +412,28 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                         res.srs += 1
                         if "ntp" in x and x["ssrc"] == media_ssrc:  # the video sender's SR
                             res.sr_map = (x["ntp"], x["rtp_ts"])
+                continue
+            if lite:
+                pt = d[1] & 0x7F
+                if pt == 0:  # PCMU audio
+                    continue
+                seq, ts, ssrc = struct.unpack_from("!HII", d, 2)
+                media_ssrc = ssrc
+                res.packets += 1
+                if ts != lite_ts:  # a new frame begins
+                    lite_ts, lite_ok = ts, lite_next is None or seq == lite_next
+                elif seq != lite_next:
+                    lite_ok = False
+                if lite_next is not None and seq != lite_next:
+                    res.lost += (seq - lite_next) & 0xFFFF if ((seq - lite_next) & 0xFFFF) < 0x8000 else 0
+                lite_next = (seq + 1) & 0xFFFF
+                if d[1] & 0x80:  # marker: the frame's last packet
+                    if lite_ok and len(res.aus) < n_frames:
+                        res.aus.append(b"")
+                        res.rtp_ts.append(ts)
+                        res.arrival_us.append(time.monotonic_ns() // 1000)
+                        res.arrival_wall.append(time.time())
+                    lite_ts = None
                 continue
             p = rx_for(d).unprotect_rtp(d)
             if not p:

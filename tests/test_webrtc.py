@@ -397,3 +397,27 @@ def test_rtcp_sr_maps_rtp_to_wall_clock(native, monkeypatch):
     lat = e2e_latency_ms(res)
     assert len(lat) == 45
     assert all(-2.0 < v < 500.0 for v in lat), lat  # same host: capture precedes arrival (ms resolution)
+
+
+def test_whep_lite_viewer_counts_frames(native, monkeypatch):
+    """The density harness's lite viewer (tools/bench_density.py --client lite): frames counted
+    from the plaintext RTP headers of the SRTP stream (one timestamp, marker bit, no sequence gap)
+    after the same ICE / DTLS set-up; RTCP sender reports still decrypted for the latency map."""
+    from mxdesk.server.whep_client import e2e_latency_ms
+
+    monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false", "WEBRTC_ENCODER": "x264enc"})
+    from mxdesk.server.app import serve
+
+    async def go():
+        port = free_port()
+        runner = await serve(srv, "127.0.0.1", port)
+        try:
+            return await whep_view(f"http://127.0.0.1:{port}/whep", 70, lite=True)
+        finally:
+            await runner.cleanup()
+
+    res = asyncio.run(go())
+    assert len(res.aus) == 70 and res.lost == 0 and res.packets >= 70
+    assert res.stage == "media" and len(set(res.rtp_ts)) == 70
+    assert res.srs >= 1 and len(e2e_latency_ms(res)) > 0  # an SR arrived within ~1.2 s of frames

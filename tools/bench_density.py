@@ -60,12 +60,12 @@ def _wait_ready(ports, timeout=180.0):
         raise RuntimeError(f"sessions not ready: {sorted(pending)[:5]}")
 
 
-def _client_proc(ports, frames, q):
+def _client_proc(ports, frames, q, lite=False):
     from mxdesk.server.whep_client import e2e_latency_ms, whep_view
 
     async def one(p):
         try:
-            res = await whep_view(f"http://127.0.0.1:{p}/whep", frames, timeout=frames / 30.0 + 60)
+            res = await whep_view(f"http://127.0.0.1:{p}/whep", frames, timeout=frames / 30.0 + 60, lite=lite)
         except Exception as e:  # a stalled session is a failure of this K, not of the tool
             r = getattr(e, "whep_result", None)
             diag = {} if r is None else {"stage": r.stage, "ice_tx": r.ice_tx, "datagrams": r.datagrams,
@@ -85,7 +85,7 @@ def _client_proc(ports, frames, q):
     q.put(asyncio.run(main()))
 
 
-def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir=""):
+def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir="", lite=False):
     import multiprocessing as mp
 
     base = _free_port_block(k)
@@ -113,7 +113,7 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         groups = [ports[i:i + per_proc] for i in range(0, k, per_proc)]
-        procs = [ctx.Process(target=_client_proc, args=(g, frames, q)) for g in groups]
+        procs = [ctx.Process(target=_client_proc, args=(g, frames, q, lite)) for g in groups]
         for p in procs:
             p.start()
         results = []
@@ -154,12 +154,16 @@ def main():
     ap.add_argument("--encoder", default="mxh264enc")
     ap.add_argument("--server-procs", type=int, default=1, help="serve processes sharing the GPU (sessions split evenly)")
     ap.add_argument("--log-dir", default="", help="write each serve process's output here")
+    ap.add_argument("--client", choices=["full", "lite"], default="full",
+                    help="viewer: full (decrypt + depacketise every packet) or lite (frames from the plaintext RTP "
+                         "headers; the server side is identical -- for K where the Python viewers saturate the host)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     rows, sustained = [], 0
     for k in (int(v) for v in a.sweep.replace("+", ",").split(",")):
-        r = run_k(k, a.frames, a.per_proc, a.width, a.height, a.encoder, a.server_procs, a.log_dir)
+        r = run_k(k, a.frames, a.per_proc, a.width, a.height, a.encoder, a.server_procs, a.log_dir, a.client == "lite")
         r["server_procs"] = min(a.server_procs, k)
+        r["client"] = a.client
         rows.append(r)
         print(json.dumps(r), flush=True)
         if not r["passed"]:
@@ -168,6 +172,7 @@ def main():
     out = {"metric": f"concurrent 1080p60 WebRTC sessions from {a.server_procs} serve process(es) on one GPU",
            "sustained": sustained, "server_procs": a.server_procs,
            "first_failing": rows[-1]["k"] if rows and not rows[-1]["passed"] else None, "frames_per_viewer": a.frames,
+           "client": a.client,
            "criteria": "every viewer >= 59.5 fps and p95 capture->viewer latency < 5 ms", "runs": rows}
     line = json.dumps(out)
     print(line, flush=True)
