@@ -2393,7 +2393,10 @@ __global__ __launch_bounds__(256) void k_hevc_pack(Geometry g, const HevcFrameSt
     // the frame's completion event) and re-arms the counter for the next frame
     __syncthreads();
     if (tid == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        // relaxed: only the count matters (the host reads the header after the frame's completion
+        // event); acq_rel put an L2 write-back (buffer_wbl2) + invalidate around it in every one of
+        // the workgroups
+        const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == gridDim.x - 1) {
             reinterpret_cast<HevcOutHeader*>(host_out)->t_end = wall_clock64();
             __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
