@@ -58,9 +58,10 @@ struct ScaleMfma {
     const int* gx = nullptr;    // [ngx][2] kabs, nks
     const int* gy = nullptr;    // [ngy][3] ylo, nrb, nr
     const void* fh = nullptr;   // [ngx][kMaxKs][64 lanes] 8 x f16 horizontal weight fragments
-    const float* sh = nullptr;  // [ngx][32] sum of each column's f16 weights (input bias removal)
     const void* fv = nullptr;   // [ngy][kMaxRb][2][64 lanes] 8 x f16 vertical weight fragments
     int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0;
+    int nk = 0;       // K-steps k_scale_mfma is instantiated for (max over the groups, rounded up)
+    int nrb_max = 0;  // most 32-row input blocks of a row group
     // strip form (k_scale_strip: `strip` consecutive 32-row tiles per workgroup, 0 = unavailable):
     // per tile (first input row of its strip, first block | blocks << 8 relative to it, 0) and the
     // vertical fragments against those strip-relative 32-row blocks
@@ -83,8 +84,8 @@ struct LanczosTables {
 // scale factor is outside what the MFMA kernel's register tiles hold (then the VALU kernel runs).
 struct ScaleFragsHost {
     std::vector<uint8_t> blob;
-    size_t off_gx = 0, off_gy = 0, off_fh = 0, off_sh = 0, off_fv = 0, off_gy2 = 0, off_fv2 = 0;
-    int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0, strip = 0;
+    size_t off_gx = 0, off_gy = 0, off_fh = 0, off_fv = 0, off_gy2 = 0, off_fv2 = 0;
+    int lds_cols = 0, lds_rows = 0, ngx = 0, ngy = 0, strip = 0, nk = 0, nrb_max = 0;
 };
 bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, int coded_h,
                        const std::vector<int>& x0, const std::vector<float>& wx, int tx, const std::vector<int>& y0,

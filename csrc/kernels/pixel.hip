@@ -16,6 +16,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #include "pixel.h"
 #include "../common/hip_check.h"
@@ -596,11 +597,17 @@ __global__ __launch_bounds__(256) void k_scale_to_nv12(const uint8_t* __restrict
 // X's accumulator (output column on the lane, input rows in registers) is the vertical
 // product's B operand as it stands (rows in the permuted k order of the fragment map; the
 // host lays Wv's fragments out in that order), so X never goes through LDS.  Input pixels
-// are f16 (1024 + p): v_perm gathers one channel byte of two pixels and an OR with
-// 0x6400 makes the f16 -- the 1024 * sum(w) bias leaves per column (`sh`).  The footprint
-// is staged global -> LDS with 16-byte LDS-DMA (global_load_lds_dwordx4); only quads that
-// cross the left/right image edge are rewritten with clamped pixels.
+// enter as f16 subnormals: v_perm puts one channel byte of two pixels in the low bytes of two
+// halves (0x00pp = p * 2^-24, exact), one instruction per dword and no bias to remove.  The
+// horizontal weights carry 2^14 and the vertical ones 2^10, so X = 2^-10 * (filtered row),
+// a normal f16 with the precision of the former 1024 + p form, and Y is in pixel units.
+// The footprint is staged global -> LDS with 16-byte LDS-DMA (global_load_lds_dwordx4); the
+// weights of taps outside the picture are folded into its edge column, so only quads that
+// straddle the right edge (input widths not a multiple of 4) are rewritten with clamped pixels.
+constexpr float kMfHScale = 16384.f, kMfVScale = 1024.f;  // 2^14 * 2^10 * 2^-24 = 1
 constexpr int kMfKs = 8;  // max horizontal K-steps (16 input columns each) per 32 output columns
+// K-step counts k_scale_mfma is instantiated for: the smallest one >= n (n <= kMfKs)
+constexpr int scale_mfma_nk(int n) { return n <= 2 ? 2 : n <= 6 ? n : 8; }
 constexpr int kMfRb = 4;  // max 32-row input blocks per 32 output rows
 constexpr int kStripRing = 3;  // k_scale_strip: LDS ring of 32-row input blocks (one computed, two in flight)
 constexpr int kStripMaxT = 4;  // k_scale_strip: most 32-row output tiles per workgroup
@@ -608,12 +615,27 @@ typedef _Float16 mf_h8 __attribute__((ext_vector_type(8)));
 typedef float mf_f16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// Per-workgroup phase stamps of k_scale_mfma for tools/scale_stamps.hip (compiled out unless
+// MX_SCALE_STAMPS is defined): [wg][0] = s_memrealtime at entry, [wg][1..6] = s_memtime at the
+// phases named in mf_main / k_scale_mfma, [wg][7] = s_memrealtime at exit.
+#ifdef MX_SCALE_STAMPS
+__device__ uint64_t g_scale_stamps[4096 * 8];
+#define MF_STAMP(k, v)                                                                                  \
+    do {                                                                                                \
+        if (threadIdx.x == 0) g_scale_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = (v);    \
+    } while (0)
+#else
+#define MF_STAMP(k, v) \
+    do {               \
+    } while (0)
+#endif
+
 __device__ __forceinline__ mf_h8 mf_chan(const uint4& a, const uint4& b, uint32_t sel) {
     uint4 r;
-    r.x = __builtin_amdgcn_perm(a.y, a.x, sel) | 0x64006400u;
-    r.y = __builtin_amdgcn_perm(a.w, a.z, sel) | 0x64006400u;
-    r.z = __builtin_amdgcn_perm(b.y, b.x, sel) | 0x64006400u;
-    r.w = __builtin_amdgcn_perm(b.w, b.z, sel) | 0x64006400u;
+    r.x = __builtin_amdgcn_perm(a.y, a.x, sel);
+    r.y = __builtin_amdgcn_perm(a.w, a.z, sel);
+    r.z = __builtin_amdgcn_perm(b.y, b.x, sel);
+    r.w = __builtin_amdgcn_perm(b.w, b.z, sel);
     return __builtin_bit_cast(mf_h8, r);
 }
 
@@ -623,16 +645,40 @@ __device__ __forceinline__ int clamp255(float v) { return min(max((int)__builtin
 // footprint row per wave instruction (rows wave, wave + 2, ...: 16 instructions per wave for a
 // full block): lane q < nq copies input pixels xlo + 4q .. +3 (its clamped byte offset `loff`)
 // of input row ylo + r0 + r to LDS quad r * nq + q.
+// Through a buffer resource over the picture: the lane's byte offset in the vector offset and
+// the row's in the scalar offset, so a row costs no per-lane address arithmetic.
 __device__ __forceinline__ void mf_stage(const uint8_t* __restrict__ in, int in_pitch, int in_h, int ylo, int r0,
                                          int nr, int nq, uint32_t loff, char* buf, int wave, int lane) {
     const int rows = min(32, nr - r0);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(in), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int r = wave + 2 * i;
         const int sy = min(max(ylo + r0 + r, 0), in_h - 1);
         if (r < rows && lane < nq)
-            __builtin_amdgcn_global_load_lds(in + (size_t)sy * in_pitch + loff,
-                                             (lds_void_t*)(buf + (size_t)r * nq * 16), 16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(buf + (size_t)r * nq * 16), 16, (int)loff,
+                                                     sy * in_pitch, 0, 0);
+    }
+}
+
+// DMA instructions mf_stage issues for the block at row r0 (wave-uniform).
+__device__ __forceinline__ int mf_stage_count(int r0, int nr, int wave) {
+    const int rows = min(32, nr - r0);
+    return rows > wave ? (rows - wave + 1) >> 1 : 0;
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in 0..16 (the immediate must be a constant)
+template <int N = 16>
+__device__ __forceinline__ void wait_vm_le(int n) {
+    if constexpr (N == 0) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+    } else {
+        if (n >= N) {
+            __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+            return;
+        }
+        wait_vm_le<N - 1>(n);
     }
 }
 
@@ -670,55 +716,74 @@ __device__ __forceinline__ void mf_fix_edges(char* buf, int rows, int nq, int xl
 // blocks' LDS-DMA are in flight at the start and one while each block's products run.  buf0 / buf1 are
 // __restrict__: the compiler then sees the ds_reads of one buffer as independent of the DMA
 // into the other and waits only for the DMA they depend on (a counted vmcnt, not vmcnt(0)).
+template <int NK, int NRB>
 __device__ __forceinline__ void mf_main(char* __restrict__ buf0, char* __restrict__ buf1,
                                         const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h, int xlo,
-                                        int ylo, int nr, int nrb, int nq, int lds_cols, uint32_t loff, int kb, int nks,
-                                        int wave, int lane, const mf_h8* bh, const mf_h8 (*av)[2], float bias,
-                                        mf_f16* Y) {
+                                        int ylo, int nr, int nrb, int nq, int lds_cols, uint32_t loff, int kb,
+                                        int wave, int lane, const mf_h8* bh, const mf_h8 (*av)[2], mf_f16* Y) {
     const int h = lane >> 5, l32 = lane & 31;
-    const bool edge = xlo < 0 || xlo + 4 * nq > in_w;  // workgroup-uniform
-    mf_stage(in, in_pitch, in_h, ylo, 0, nr, nq, loff, buf0, wave, lane);
-    if (nrb > 1) mf_stage(in, in_pitch, in_h, ylo, 32, nr, nq, loff, buf1, wave, lane);
+    // quads straddling the right picture edge (xlo is a multiple of 4, so only when in_w is not);
+    // columns wholly outside carry weight 0 (build_scale_frags folds the edge taps)
+    const bool edge = (in_w & 3) != 0 && xlo + 4 * nq > in_w;  // workgroup-uniform
+    // (block 0 landed and block 1 posted by the caller)
     // channel c of pixels (2p, 2p+1) -> f16 pair: byte c of each into the low byte of a half
     constexpr uint32_t kSel[3] = {0x0c040c00u, 0x0c050c01u, 0x0c060c02u};  // B, G, R
 #pragma unroll
-    for (int b = 0; b < kMfRb; ++b) {
+    for (int b = 0; b < NRB; ++b) {
         if (b > 0 && b >= nrb) break;  // nrb >= 1
         char* cur = (b & 1) ? buf1 : buf0;
         // this wave's DMA of block b retired (__syncthreads() alone does not wait for LDS-DMA).
-        // Block 0 waits for everything (blocks 0 and 1 and the weight fragments, which were all
-        // in flight together); from block 1 on, the DMA of block b + 1 (posted one block
-        // earlier, at most 16 instructions) stays in flight.
-        if (b > 0 && b + 1 < nrb)
-            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
-        else
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        // Vector-memory operations retire in order, so waiting until no more than block b + 1's
+        // own DMA instructions (if posted) remain leaves exactly those in flight: block 0 starts
+        // its products as soon as it and the weight fragments have landed.
+        wait_vm_le(b + 1 < nrb ? mf_stage_count(32 * (b + 1), nr, wave) : 0);
         mf_barrier();
+        if (b == 0) MF_STAMP(2, __builtin_amdgcn_s_memtime());
+        if (b == 1) MF_STAMP(4, __builtin_amdgcn_s_memtime());
         if (edge) {  // quads crossing the left/right image edge: per-pixel clamp
             mf_fix_edges(cur, min(32, nr - 32 * b), nq, xlo, in_w, wave, lane);
             mf_barrier();
         }
         const uint32_t* rp =
             reinterpret_cast<const uint32_t*>(cur) + min(l32, nr - 1 - 32 * b) * lds_cols + kb + 8 * h;
+        // the block's K window read once (one LDS latency, not one per step and channel), then
+        // the three channels' X chains interleaved step by step, so consecutive MFMAs never wait
+        // on each other's accumulator; X -> f16 of one channel overlaps the others' products
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 pv[NK][2];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {  // one channel at a time: a single 16-register X accumulator
-            mf_f16 X = {};
+        for (int s = 0; s < NK; ++s) {
+            pv[s][0] = *reinterpret_cast<const u32x4*>(rp + 16 * s);
+            pv[s][1] = *reinterpret_cast<const u32x4*>(rp + 16 * s + 4);
+        }
+        // all reads in flight before the first product (else the scheduler re-serialises them
+        // behind the MFMAs to save registers: one LDS latency per step); whole 128-bit operands,
+        // so the loaded quads stay where ds_read_b128 put them
 #pragma unroll
-            for (int s = 0; s < kMfKs; ++s) {
-                if (s > 0 && s >= nks) break;  // nks >= 1
-                const uint4 p0 = *reinterpret_cast<const uint4*>(rp + 16 * s);
-                const uint4 p1 = *reinterpret_cast<const uint4*>(rp + 16 * s + 4);
-                X = __builtin_amdgcn_mfma_f32_32x32x16_f16(mf_chan(p0, p1, kSel[c]), bh[s], X, 0, 0, 0);
-            }
+        for (int s = 0; s < NK; ++s) asm volatile("" : "+v"(pv[s][0]), "+v"(pv[s][1]));
+        uint4 pk[NK][2];
+#pragma unroll
+        for (int s = 0; s < NK; ++s)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) pk[s][t] = make_uint4(pv[s][t].x, pv[s][t].y, pv[s][t].z, pv[s][t].w);
+        mf_f16 X[3] = {{}, {}, {}};
+#pragma unroll
+        for (int s = 0; s < NK; ++s)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                X[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(mf_chan(pk[s][0], pk[s][1], kSel[c]), bh[s], X[c], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
             mf_h8 x0, x1;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                x0[j] = (_Float16)(X[j] - bias);
-                x1[j] = (_Float16)(X[8 + j] - bias);
+                x0[j] = (_Float16)X[c][j];
+                x1[j] = (_Float16)X[c][8 + j];
             }
             Y[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[b][0], x0, Y[c], 0, 0, 0);
             Y[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[b][1], x1, Y[c], 0, 0, 0);
         }
+        if (b == 0) MF_STAMP(3, __builtin_amdgcn_s_memtime());
         if (b + 2 < nrb) {  // block b + 2 into this buffer once every wave has read it
             mf_barrier();
             mf_stage(in, in_pitch, in_h, ylo, 32 * (b + 2), nr, nq, loff, cur, wave, lane);
@@ -729,10 +794,13 @@ __device__ __forceinline__ void mf_main(char* __restrict__ buf0, char* __restric
 __device__ __forceinline__ void mf_epilogue(const mf_f16* Y, int g0, int wave, int v, int lane, uint8_t* __restrict__ yp,
                                             uint8_t* __restrict__ uvp, int out_pitch, int coded_w, int coded_h);
 
+template <int NK, int NRB>
 __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ in, int in_pitch, int in_w, int in_h,
                                                     ScaleMfma m, uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp,
                                                     int out_pitch, int coded_w, int coded_h, uint64_t* ts) {
     stamp_start(ts);
+    MF_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    MF_STAMP(1, __builtin_amdgcn_s_memtime());
     // LDS: two 32-row footprint buffers [32][lds_cols] BGRx (see mf_main)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
@@ -752,28 +820,40 @@ __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ 
     const int xlo = m.gx[2 * g0];
     const int ylo = m.gy[3 * v], nrb = m.gy[3 * v + 1], nr = m.gy[3 * v + 2];
     const int nq = m.lds_cols >> 2;
-    const size_t buf_bytes = (size_t)32 * m.lds_cols * 4;
     const uint32_t loff = (uint32_t)min(max(xlo + 4 * lane, 0), in_w - 4) * 4;
-    // weight fragments (ordinary loads first: a later vmcnt wait for them would also drain
-    // the LDS-DMA issued after them)
-    const int nks = m.gx[2 * gw + 1], kb = m.gx[2 * gw] - xlo;
+    // Block 0's DMA, then the weight fragments (ordinary loads), one vmcnt(0) for both, then
+    // block 1's DMA: block 1 lands while block 0's products run.  (The compiler's own wait for
+    // a fragment counts every vector-memory operation issued after it -- the DMA's count is not
+    // static -- so fragments loaded with two blocks in flight behind them would hold block 0's
+    // products until block 1 had landed too: profiles/r05_scale/NOTES.md.)
+    const size_t buf_bytes = (size_t)32 * m.lds_cols * 4;
+    // (NRB >= nrb: every fragment load unconditional -- a load under a branch turns the
+    // compiler's wait for it into vmcnt(0) -- those past nrb repeat the last block's)
+    const int kb = __builtin_amdgcn_readfirstlane(m.gx[2 * gw]) - xlo;  // (zero fragments past the group's K-steps)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the scalars above, before any DMA
+    mf_stage(in, in_pitch, in_h, ylo, 0, nr, nq, loff, smem, wave, lane);
     const uint4* fh = reinterpret_cast<const uint4*>(m.fh) + (size_t)gw * kMfKs * 64 + lane;
     const uint4* fv = reinterpret_cast<const uint4*>(m.fv) + (size_t)v * kMfRb * 128 + lane;
-    mf_h8 bh[kMfKs], av[kMfRb][2];
+    mf_h8 bh[NK], av[NRB][2];
 #pragma unroll
-    for (int s = 0; s < kMfKs; ++s) bh[s] = __builtin_bit_cast(mf_h8, s < nks ? fh[s * 64] : make_uint4(0, 0, 0, 0));
+    for (int s = 0; s < NK; ++s) bh[s] = __builtin_bit_cast(mf_h8, fh[s * 64]);
 #pragma unroll
-    for (int b = 0; b < kMfRb; ++b) {
-        av[b][0] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128] : make_uint4(0, 0, 0, 0));
-        av[b][1] = __builtin_bit_cast(mf_h8, b < nrb ? fv[b * 128 + 64] : make_uint4(0, 0, 0, 0));
+    for (int b = 0; b < NRB; ++b) {
+        const int bb = min(b, nrb - 1);
+        av[b][0] = __builtin_bit_cast(mf_h8, fv[bb * 128]);
+        av[b][1] = __builtin_bit_cast(mf_h8, fv[bb * 128 + 64]);
     }
-    const float bias = 1024.f * m.sh[gw * 32 + l32];  // f16 input bias: 1024 * sum(w)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (nrb > 1) mf_stage(in, in_pitch, in_h, ylo, 32, nr, nq, loff, smem + buf_bytes, wave, lane);
     mf_f16 Y[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) Y[c] = (mf_f16){};
-    mf_main(smem, smem + buf_bytes, in, in_pitch, in_w, in_h, xlo, ylo, nr, nrb, nq, m.lds_cols, loff, kb, nks, wave,
-            lane, bh, av, bias, Y);
+    mf_main<NK, NRB>(smem, smem + buf_bytes, in, in_pitch, in_w, in_h, xlo, ylo, nr, nrb, nq, m.lds_cols, loff, kb, wave,
+                lane, bh, av, Y);
+    MF_STAMP(5, __builtin_amdgcn_s_memtime());
     mf_epilogue(Y, g0, wave, v, lane, yp, uvp, out_pitch, coded_w, coded_h);
+    MF_STAMP(6, __builtin_amdgcn_s_memtime());
+    MF_STAMP(7, __builtin_amdgcn_s_memrealtime());
 }
 
 // Output of one wave's 32 x 32 block: Y[c][rho] is output column ox, row oy0 + (rho & 3) + 8 *
@@ -781,34 +861,76 @@ __global__ __launch_bounds__(128) void k_scale_mfma(const uint8_t* __restrict__ 
 // 2x2 chroma with the neighbouring column's lane
 __device__ __forceinline__ void mf_epilogue(const mf_f16* Y, int g0, int wave, int v, int lane, uint8_t* __restrict__ yp,
                                             uint8_t* __restrict__ uvp, int out_pitch, int coded_w, int coded_h) {
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    const int h = lane >> 5, l32 = lane & 31;
-    const int ox = 32 * (g0 + wave) + l32, oy0 = 32 * v + 4 * h;
-    const bool xin = ox < coded_w;
+    // Store-issue bound (every wave of the grid reaches it at once): 16 byte + 8 short stores per
+    // wave became 4 + 4 dword stores.  Per pixel, R, G, B are rounded and saturated into the
+    // bytes of one dword (v_cvt_pk_u8_f32), luma is one v_dot4_u32_u8 against the BT.709
+    // weights and the 2x2 chroma means go through byte dot products too.  Each group of 4
+    // consecutive rows is then transposed inside lane quads (DPP broadcasts + v_perm), so lane
+    // k of a quad holds row k's four luma bytes and lanes 0 / 2 the two chroma rows' U V U V.
+    // Stores go through buffer resources (row in the scalar offset); lanes with nothing to
+    // store -- past the coded width or height, odd lanes for chroma -- get an offset past
+    // num_records, which the hardware drops, so no store sits under a branch.
+    const int h = lane >> 5, l32 = lane & 31, k = lane & 3;
+    const int colq = 32 * (g0 + wave) + (l32 & ~3);  // first column of the lane's quad
+    const bool qin = colq < coded_w;                 // (coded_w % 4 == 0: quads wholly in or out)
+    constexpr uint32_t kLuma = 47u | (157u << 8) | (16u << 16);  // y709's weights (R, G, B bytes)
+    constexpr int kOob = 0x7fffffff;
+    const uint32_t pitch = (uint32_t)out_pitch;
+    const int rows_left = coded_h - 32 * v;  // rows of this tile inside the picture (> 0, even)
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(yp, (short)0, kOob, 0x00020000);
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(uvp, (short)0, kOob, 0x00020000);
+    const uint32_t sel01 = (uint32_t)k | ((uint32_t)(4 + k) << 8) | 0x0c0c0000u;   // byte k of B0, B1
+    const uint32_t sel23 = 0x00000c0cu | ((uint32_t)k << 16) | ((uint32_t)(4 + k) << 24);  // of B2, B3
+    const uint32_t csel = (k & 2) ? 0x07060302u : 0x05040100u;  // high / low halves of C0, C2
 #pragma unroll
-    for (int rho = 0; rho < 16; rho += 2) {
-        const int oy = oy0 + (rho & 3) + 8 * (rho >> 2);
-        auto q8 = [](float f) { return (unsigned short)min(max((int)__builtin_rintf(f), 0), 255); };
-        const u16x2 R = {q8(Y[2][rho]), q8(Y[2][rho + 1])};
-        const u16x2 G = {q8(Y[1][rho]), q8(Y[1][rho + 1])};
-        const u16x2 B = {q8(Y[0][rho]), q8(Y[0][rho + 1])};
-        const u16x2 L = ((u16x2)(47) * R + (u16x2)(157) * G + (u16x2)(16) * B + (u16x2)(128)) >> (u16x2)(8);
-        const bool yin = xin && oy < coded_h;
-        if (yin) {
-            const uint32_t o = (uint32_t)oy * (uint32_t)out_pitch + (uint32_t)ox;
-            yp[o] = (uint8_t)(L.x + 16);
-            yp[o + (uint32_t)out_pitch] = (uint8_t)(L.y + 16);
+    for (int m = 0; m < 4; ++m) {  // rows 8m + 4h + 0..3 (accumulator rows rho = 4m .. 4m + 3)
+        uint32_t Lp = 0, Cw = 0;
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2) {
+            const int rho = 4 * m + 2 * r2;
+            uint32_t P[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(Y[2][rho + t], 0, 0u);  // R
+                q = __builtin_amdgcn_cvt_pk_u8_f32(Y[1][rho + t], 1, q);           // G
+                P[t] = __builtin_amdgcn_cvt_pk_u8_f32(Y[0][rho + t], 2, q);        // B
+            }
+            const uint32_t L0 = (__builtin_amdgcn_udot4(P[0], kLuma, 128u, false) >> 8) + 16;
+            const uint32_t L1 = (__builtin_amdgcn_udot4(P[1], kLuma, 128u, false) >> 8) + 16;
+            Lp |= (L0 | (L1 << 8)) << (16 * r2);
+            // 2x2 chroma: this lane's row pair plus the neighbouring column's (lane ^ 1); the
+            // rounded means as bytes R, G, B of one dword (each sum <= 1020: B's shifted-in bits
+            // land in R's masked-off high byte); u709 / v709 as differences of byte dot products
+            uint32_t rb = (P[0] & 0x00ff00ffu) + (P[1] & 0x00ff00ffu);  // R | B << 16
+            uint32_t gg = ((P[0] >> 8) & 0xffu) + ((P[1] >> 8) & 0xffu);
+            rb += (uint32_t)__builtin_amdgcn_mov_dpp((int)rb, 0xb1, 0xf, 0xf, false);  // quad_perm 1,0,3,2
+            gg += (uint32_t)__builtin_amdgcn_mov_dpp((int)gg, 0xb1, 0xf, 0xf, false);
+            const uint32_t C = (((rb + 0x00020002u) >> 2) & 0x00ff00ffu) | (((gg + 2u) >> 2) << 8);
+            const int U = ((int)(__builtin_amdgcn_udot4(C, 112u << 16, 128u, false) -
+                                 __builtin_amdgcn_udot4(C, 26u | (86u << 8), 0u, false)) >> 8) + 128;
+            const int V = ((int)(__builtin_amdgcn_udot4(C, 112u, 128u, false) -
+                                 __builtin_amdgcn_udot4(C, (102u << 8) | (10u << 16), 0u, false)) >> 8) + 128;
+            Cw |= ((uint32_t)U | ((uint32_t)V << 8)) << (16 * r2);
         }
-        // 2x2 chroma: this lane's row pair plus the neighbouring column's (lane ^ 1)
-        const int packed = (R.x + R.y) | ((G.x + G.y) << 10) | ((B.x + B.y) << 20);
-        const int other = __shfl_xor(packed, 1);
-        if (yin && !(lane & 1)) {
-            const int Rc = ((packed & 1023) + (other & 1023) + 2) >> 2;
-            const int Gc = (((packed >> 10) & 1023) + ((other >> 10) & 1023) + 2) >> 2;
-            const int Bc = (((packed >> 20) & 1023) + ((other >> 20) & 1023) + 2) >> 2;
-            *reinterpret_cast<uint16_t*>(uvp + ((uint32_t)(oy >> 1) * (uint32_t)out_pitch + (uint32_t)ox)) =
-                (uint16_t)(u709(Rc, Gc, Bc) | (v709(Rc, Gc, Bc) << 8));
-        }
+        // luma: lane k of the quad takes byte k (row 8m + 4h + k) of the four lanes' Lp
+        const uint32_t B0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Lp, 0x00, 0xf, 0xf, false);
+        const uint32_t B1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Lp, 0x55, 0xf, 0xf, false);
+        const uint32_t B2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Lp, 0xaa, 0xf, 0xf, false);
+        const uint32_t B3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Lp, 0xff, 0xf, 0xf, false);
+        const uint32_t yw = __builtin_amdgcn_perm(B1, B0, sel01) | __builtin_amdgcn_perm(B3, B2, sel23);
+        const int yrow = 8 * m + 4 * h + k;
+        const int yvo = (qin && yrow < rows_left) ? (int)((uint32_t)(4 * h + k) * pitch + (uint32_t)colq) : kOob;
+        __builtin_amdgcn_raw_buffer_store_b32(yw, yr, yvo, (int)((uint32_t)(32 * v + 8 * m) * pitch), 0);
+        // chroma rows 4m + 2h (lane 0 of the quad) and 4m + 2h + 1 (lane 2): U V of columns
+        // 4q and 4q + 2, from the even lanes' Cw halves
+        const uint32_t C0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Cw, 0x00, 0xf, 0xf, false);
+        const uint32_t C2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)Cw, 0xaa, 0xf, 0xf, false);
+        const uint32_t cw = __builtin_amdgcn_perm(C2, C0, csel);
+        const int crow = 8 * m + 4 * h + 2 * (k >> 1);  // its first luma row
+        const int cvo = (qin && !(k & 1) && crow < rows_left)
+                            ? (int)((uint32_t)(2 * h + (k >> 1)) * pitch + (uint32_t)colq)
+                            : kOob;
+        __builtin_amdgcn_raw_buffer_store_b32(cw, cr, cvo, (int)((uint32_t)(16 * v + 4 * m) * pitch), 0);
     }
 }
 
@@ -823,7 +945,7 @@ __device__ __forceinline__ void strip_main(char* __restrict__ r0, char* __restri
                                            const uint4* __restrict__ fvl, const uint8_t* __restrict__ in,
                                            int in_pitch, int in_w, int in_h, int base, int nb, int nq, int lds_cols,
                                            uint32_t loff, int kb, int nks, int xlo, bool edge, int v0, int v1,
-                                           const int* ti, const mf_h8* bh, float bias, int g0, int wave, int lane,
+                                           const int* ti, const mf_h8* bh, int g0, int wave, int lane,
                                            uint8_t* __restrict__ yp, uint8_t* __restrict__ uvp, int out_pitch,
                                            int coded_w, int coded_h) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -880,8 +1002,8 @@ __device__ __forceinline__ void strip_main(char* __restrict__ r0, char* __restri
             mf_h8 x0, x1;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                x0[j] = (_Float16)(X[j] - bias);
-                x1[j] = (_Float16)(X[8 + j] - bias);
+                x0[j] = (_Float16)X[j];
+                x1[j] = (_Float16)X[8 + j];
             }
             if (use0) {
                 const uint4* f = fvl + ((size_t)(vt - v0) * kMfRb + (i - b0)) * 128 + lane;
@@ -974,12 +1096,13 @@ __global__ __launch_bounds__(128) void k_scale_strip(const uint8_t* __restrict__
     for (int s = 0; s < kMfKs; ++s) bh[s] = __builtin_bit_cast(mf_h8, s < nks ? fh[s * 64] : make_uint4(0, 0, 0, 0));
     const uint4* fv = reinterpret_cast<const uint4*>(m.fv2) + (size_t)v0 * kMfRb * 128;
     for (int k = tid; k < nt * kMfRb * 128; k += 128) fvl[k] = fv[k];
-    const float bias = 1024.f * m.sh[gw * 32 + l32];
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();
-    const bool edge = xlo < 0 || xlo + 4 * nq > in_w;  // workgroup-uniform
+    // quads straddling the right picture edge (xlo is a multiple of 4, so only when in_w is not);
+    // columns wholly outside carry weight 0 (build_scale_frags folds the edge taps)
+    const bool edge = (in_w & 3) != 0 && xlo + 4 * nq > in_w;  // workgroup-uniform
     strip_main(smem, smem + buf_bytes, smem + 2 * buf_bytes, fvl, in, in_pitch, in_w, in_h, base, nb, nq, m.lds_cols,
-               loff, kb, nks, xlo, edge, v0, v1, ti, bh, bias, g0, wave, lane, yp, uvp, out_pitch, coded_w, coded_h);
+               loff, kb, nks, xlo, edge, v0, v1, ti, bh, g0, wave, lane, yp, uvp, out_pitch, coded_w, coded_h);
 }
 
 __global__ __launch_bounds__(256) void k_composite(const uint8_t* __restrict__ tile, int tile_pitch, int tw, int th,
@@ -1140,7 +1263,6 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
     };
     std::vector<int> gx(2 * (size_t)ngx), gy(3 * (size_t)ngy);
     std::vector<uint16_t> fh((size_t)ngx * kMfKs * 64 * 8, 0), fv((size_t)ngy * kMfRb * 2 * 64 * 8, 0);
-    std::vector<float> sh((size_t)ngx * 32, 0.f);
     for (int g = 0; g < ngx; ++g) {
         const int kabs = x0[std::min(32 * g, out_w - 1)] & ~3;
         const int kend = x0[std::min(32 * g + 31, out_w - 1)] + tx;
@@ -1148,28 +1270,36 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
         if (nks > kMfKs) return false;
         gx[2 * g] = kabs;
         gx[2 * g + 1] = nks;
-        for (int l = 0; l < 64; ++l) {
-            const int cc = std::min(32 * g + (l & 31), out_w - 1), hh = l >> 5;
-            for (int s = 0; s < nks; ++s)
-                for (int j = 0; j < 8; ++j) {
-                    const int tap = kabs + 16 * s + 8 * hh + j - x0[cc];
-                    if (tap < 0 || tap >= tx) continue;
-                    const auto hv = f16(wx[(size_t)cc * tx + tap]);
-                    fh[(((size_t)g * kMfKs + s) * 64 + l) * 8 + j] = hv.first;
-                }
-        }
-        for (int c = 0; c < 32; ++c) {  // exact in f32: few f16 terms of bounded exponent range
+        // Taps outside the picture read its edge column (clamp), so their weights are folded
+        // into that column's: the K window's columns outside [0, in_w) get weight 0 and the
+        // kernels need no per-pixel clamp of the staged footprint (which cost the picture's
+        // edge workgroups twice the others' time: profiles/r05_scale/NOTES.md)
+        std::vector<float> eff(16 * (size_t)kMfKs);
+        for (int c = 0; c < 32; ++c) {
             const int cc = std::min(32 * g + c, out_w - 1);
-            float sum = 0.f;
-            for (int k = 0; k < tx; ++k) sum += f16(wx[(size_t)cc * tx + k]).second;
-            sh[(size_t)g * 32 + c] = sum;
+            std::fill(eff.begin(), eff.end(), 0.f);
+            for (int k = 0; k < tx; ++k) {
+                const int col = std::min(std::max(x0[cc] + k, 0), in_w - 1) - kabs;
+                if (col >= 0 && col < 16 * nks) eff[col] += wx[(size_t)cc * tx + k];
+            }
+            for (int s = 0; s < nks; ++s)
+                for (int hh = 0; hh < 2; ++hh)
+                    for (int j = 0; j < 8; ++j)
+                        fh[(((size_t)g * kMfKs + s) * 64 + 32 * hh + c) * 8 + j] =
+                            f16(kMfHScale * eff[16 * s + 8 * hh + j]).first;
         }
     }
-    int lds_cols = 0, lds_rows = 0;
+    // k_scale_mfma runs a compile-time K-step count (every group's products unrolled without
+    // branches); groups with fewer steps have zero fragments beyond theirs, and the footprint is
+    // sized for the instantiated count so those steps read inside the staged rows
+    int nk = 0;
+    for (int g = 0; g < ngx; ++g) nk = std::max(nk, gx[2 * g + 1]);
+    nk = scale_mfma_nk(nk);
+    int lds_cols = 0, lds_rows = 0, nrb_max = 1;
     for (int g0 = 0; g0 < ngx; g0 += 2)
         for (int w = 0; w < 2; ++w) {
             const int g = std::min(g0 + w, ngx - 1);
-            lds_cols = std::max(lds_cols, gx[2 * g] - gx[2 * g0] + 16 * gx[2 * g + 1]);
+            lds_cols = std::max(lds_cols, gx[2 * g] - gx[2 * g0] + 16 * std::max(nk, gx[2 * g + 1]));
         }
     lds_cols = (lds_cols + 3) & ~3;
     if (((lds_cols >> 2) & 1) == 0) lds_cols += 4;  // odd quad pitch: conflict-free row-parallel b128 reads
@@ -1178,6 +1308,7 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
         const int nr = y0[std::min(32 * v + 31, out_h - 1)] + ty - ylo;
         const int nrb = (nr + 31) / 32;
         if (nrb > kMfRb) return false;
+        nrb_max = std::max(nrb_max, nrb);
         gy[3 * v] = ylo;
         gy[3 * v + 1] = nrb;
         gy[3 * v + 2] = nr;
@@ -1192,7 +1323,7 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
                         const int q = 16 * t + 8 * (j >> 2) + 4 * hh + (j & 3);
                         const int tap = ylo + 32 * b + q - y0[oy];
                         if (tap < 0 || tap >= ty) continue;
-                        fv[((((size_t)v * kMfRb + b) * 2 + t) * 64 + l) * 8 + j] = f16(wy[(size_t)oy * ty + tap]).first;
+                        fv[((((size_t)v * kMfRb + b) * 2 + t) * 64 + l) * 8 + j] = f16(kMfVScale * wy[(size_t)oy * ty + tap]).first;
                     }
         }
     }
@@ -1235,7 +1366,7 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
                             const int q = 16 * t + 8 * (j >> 2) + 4 * hh + (j & 3);
                             const int tap = base + 32 * (blo + b) + q - y0[oy];
                             if (tap < 0 || tap >= ty) continue;
-                            fv2[((((size_t)v * kMfRb + b) * 2 + t) * 64 + l) * 8 + j] = f16(wy[(size_t)oy * ty + tap]).first;
+                            fv2[((((size_t)v * kMfRb + b) * 2 + t) * 64 + l) * 8 + j] = f16(kMfVScale * wy[(size_t)oy * ty + tap]).first;
                         }
             }
         }
@@ -1245,8 +1376,7 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     out.off_gx = 0;
     out.off_gy = align(gx.size() * 4);
-    out.off_sh = out.off_gy + align(gy.size() * 4);
-    out.off_fh = out.off_sh + align(sh.size() * 4);
+    out.off_fh = out.off_gy + align(gy.size() * 4);
     out.off_fv = out.off_fh + align(fh.size() * 2);
     out.off_gy2 = out.off_fv + align(fv.size() * 2);
     out.off_fv2 = out.off_gy2 + align(gy2.size() * 4);
@@ -1256,11 +1386,12 @@ bool build_scale_frags(int in_w, int in_h, int out_w, int out_h, int coded_w, in
     out.strip = strip;
     std::memcpy(out.blob.data() + out.off_gx, gx.data(), gx.size() * 4);
     std::memcpy(out.blob.data() + out.off_gy, gy.data(), gy.size() * 4);
-    std::memcpy(out.blob.data() + out.off_sh, sh.data(), sh.size() * 4);
     std::memcpy(out.blob.data() + out.off_fh, fh.data(), fh.size() * 2);
     std::memcpy(out.blob.data() + out.off_fv, fv.data(), fv.size() * 2);
     out.lds_cols = lds_cols;
     out.lds_rows = lds_rows;
+    out.nk = nk;
+    out.nrb_max = nrb_max;
     out.ngx = ngx;
     out.ngy = ngy;
     (void)in_h;
@@ -1274,11 +1405,12 @@ void upload_scale_frags(const ScaleFragsHost& h, void** dev, ScaleMfma& mf) {
     const char* b = static_cast<const char*>(*dev);
     mf.gx = reinterpret_cast<const int*>(b + h.off_gx);
     mf.gy = reinterpret_cast<const int*>(b + h.off_gy);
-    mf.sh = reinterpret_cast<const float*>(b + h.off_sh);
     mf.fh = b + h.off_fh;
     mf.fv = b + h.off_fv;
     mf.lds_cols = h.lds_cols;
     mf.lds_rows = h.lds_rows;
+    mf.nk = h.nk;
+    mf.nrb_max = h.nrb_max;
     mf.ngx = h.ngx;
     mf.ngy = h.ngy;
     mf.gy2 = reinterpret_cast<const int*>(b + h.off_gy2);
@@ -1307,13 +1439,30 @@ void launch_scale_to_nv12(const uint8_t* bgrx, int in_pitch, int in_w, int in_h,
     }
     if (t.mf.gx && t.mf.ngx == (coded_w + 31) / 32 && t.mf.ngy == (coded_h + 31) / 32 && in_w >= 4) {
         const size_t lds = (size_t)2 * 32 * t.mf.lds_cols * 4;
-        if (lds > 64 * 1024) {
-            ensure_func_attr(reinterpret_cast<const void*>(&k_scale_mfma),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        }
-        dim3 grid((coded_w + 63) / 64, (coded_h + 31) / 32);
-        hipLaunchKernelGGL(k_scale_mfma, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv,
-                           out_pitch, coded_w, coded_h, ts);
+        auto go = [&](auto kern) {
+            if (lds > 64 * 1024)
+                ensure_func_attr(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024);
+            dim3 grid((coded_w + 63) / 64, (coded_h + 31) / 32);
+            hipLaunchKernelGGL(kern, grid, dim3(128), lds, stream, bgrx, in_pitch, in_w, in_h, t.mf, y, uv, out_pitch,
+                               coded_w, coded_h, ts);
+        };
+        auto by_nk = [&](auto nrb) {
+            constexpr int R = decltype(nrb)::value;
+            switch (t.mf.nk) {  // scale_mfma_nk's values
+                case 2: go(&k_scale_mfma<2, R>); break;
+                case 3: go(&k_scale_mfma<3, R>); break;
+                case 4: go(&k_scale_mfma<4, R>); break;
+                case 5: go(&k_scale_mfma<5, R>); break;
+                case 6: go(&k_scale_mfma<6, R>); break;
+                case 8: go(&k_scale_mfma<8, R>); break;
+                default: throw std::logic_error("scale_to_nv12: fragment tables without a K-step count");
+            }
+        };
+        if (t.mf.nrb_max <= 3)
+            by_nk(std::integral_constant<int, 3>{});
+        else
+            by_nk(std::integral_constant<int, kMfRb>{});
         return;
     }
     // worst-case footprint of a tile: scale * tile + taps
