@@ -81,7 +81,7 @@ struct EncoderConfig {
                               // the analysis queue, profiles/r04_toolset/NOTES.md)
     int tu_split = 2;         // HEVC: inter transform trees may split into 8x8 luma / 4x4 chroma TUs (1), and each
                               // 8x8 luma node again into four 4x4 TUs (2), per node by SSE + lambda * bits
-    int hevc_slice_cost = 2048;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
+    int hevc_slice_cost = 1536;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
     // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): P pictures in slices of
     // hevc_wpp_rows CTU rows, every CTU row its own CABAC substream (one GPU wave each) that starts
     // from the contexts the row above had after its second CTU.  Off by default: a CTU row is a

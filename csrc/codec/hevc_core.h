@@ -2473,20 +2473,23 @@ MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, 
 // Entropy-coding cost estimate of a CU in CABAC work units: significance bins up to the
 // last position of every coded TU plus a few bins per coded sub-block, on top of the CU
 // header.  Used only to balance slices; identical on the CPU and the GPU.
-// Serial arithmetic-coder work of a CU in bin tokens (k_hevc_arith runs ~170 ns per token and
-// nothing measurable per CTU: tools/hevc_cabac_timing.py).  Least-squares fit over the CUs of 4K
-// bench P pictures (tools/hevc_session_timing.py --dump, profiles/r04_hevc/NOTES.md): a CU
-// without residual ~4 tokens; a coded CU 1 + (sum of last+1) / 4 + 15 per coded sub-block + 2.6
-// per estimated payload byte, 2.2 % mean error.  (The earlier byte-only model, 6 tokens per byte,
-// missed the ~13 tokens per byte of the noise panel's small levels: its slices ran 2.4x the
-// median.)
+// Serial arithmetic-coder work of a CU in bin tokens (k_hevc_arith runs ~165 ns per token and
+// nothing measurable per CTU: tools/hevc_cabac_timing.py).  Least-squares fit over the 16x16 units
+// of round-5 4K desktop P pictures (CTB 32 quadtree, 18 Mbps; tools/hevc_session_timing.py --dump,
+// tools/hevc_cost_fit.py, profiles/r05_hevc_slices/NOTES.md): a unit without residual 1 token
+// (mostly skips: 1.4 measured; merge 5.4, AMVP 12 -- but skip / merge / AMVP are decided after
+// the slices are laid out, so the model cannot use them), a coded unit 0.25 per (last + 1) + 13
+// per coded sub-block + 3.9 per estimated payload byte - 4.  Replaces round 4's fit (CTB 16),
+// which priced a unit without residual at 4 tokens: slices over static areas then held a third
+// of their estimate and the slowest slice ran 1.4x the median.
 MXHD uint32_t cu_cost(const CuInfo& c) {
-    if (!c.cbf) return 4u;
+    if (!c.cbf) return 1u;
     uint32_t lsum = 0, sb = 0;
     if (c.cbf & 1) lsum += c.last[0] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_y);
     if (c.cbf & 2) lsum += c.last[1] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[0]);
     if (c.cbf & 4) lsum += c.last[2] + 1u, sb += (uint32_t)__builtin_popcount(c.csbf_c[1]);
-    return 1u + (lsum >> 2) + 15u * sb + ((21u * (uint32_t)c.est_bytes) >> 3);
+    const uint32_t v = (2u * lsum + 104u * sb + 31u * (uint32_t)c.est_bytes) >> 3;
+    return v > 5u ? v - 4u : 1u;
 }
 MXHD uint8_t est_bytes_of(uint32_t bits) {
     const uint32_t b = (bits + 7) >> 3;
@@ -2494,11 +2497,11 @@ MXHD uint8_t est_bytes_of(uint32_t bits) {
 }
 // est_bytes of a summarised CU from the bits estimate of its final levels (cu_bits_est)
 MXHD void set_est_bytes(CuInfo& c, uint32_t bits) { c.est_bytes = c.cbf ? est_bytes_of(bits) : (uint8_t)0; }
-// Below this much work per slice, fewer slices: 2048 tokens keep a slice near 0.35 ms; the level's
+// Below this much work per slice, fewer slices: 1536 tokens keep a slice near 0.25 ms; the level's
 // slice limit usually binds first at 4K.
-constexpr uint32_t kCostPerSlice = 2048;  // EncoderConfig::hevc_slice_cost default
+constexpr uint32_t kCostPerSlice = 1536;  // EncoderConfig::hevc_slice_cost default
 // Largest cu_cost (last+1 <= 256 + 64 + 64, 16 + 4 + 4 sub-blocks, est_bytes <= 255).
-constexpr uint32_t kMaxCuCost = 1u + (384u >> 2) + 15u * 24u + ((21u * 255u) >> 3);
+constexpr uint32_t kMaxCuCost = ((2u * 384u + 104u * 24u + 31u * 255u) >> 3) - 4u;
 // Slices are laid out in whole CTBs: the largest CTB cost (four units)
 constexpr uint32_t kMaxCtbCost = 4u * kMaxCuCost;
 // Number of slice thresholds for a P picture of total cost T, bounded by the level's slice limit.
