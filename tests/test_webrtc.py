@@ -421,3 +421,32 @@ def test_whep_lite_viewer_counts_frames(native, monkeypatch):
     assert len(res.aus) == 70 and res.lost == 0 and res.packets >= 70
     assert res.stage == "media" and len(set(res.rtp_ts)) == 70
     assert res.srs >= 1 and len(e2e_latency_ms(res)) > 0  # an SR arrived within ~1.2 s of frames
+
+
+def test_send_au_batches_more_than_one_sendmmsg(native):
+    """An access unit of ~150 packets goes out through several sendmmsg batches (64 each,
+    csrc/net/rtp_sender.cpp): every datagram arrives once, in order, and decrypts to the packetizer's
+    packet; the return value counts them."""
+    import socket
+    net = native.net
+    rx_sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx_sock.bind(("127.0.0.1", 0))
+    rx_sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+    rx_sock.settimeout(2.0)
+    tx_sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        k, salt = os.urandom(16), os.urandom(14)
+        tx, rx = net.SrtpSession(k, salt), net.SrtpSession(k, salt)
+        peer = net.UdpPeer(tx_sock.fileno(), "127.0.0.1", rx_sock.getsockname()[1])
+        pk = net.RtpH264Packetizer(0x1234, 96, 1150, 100)
+        au = b"\x00\x00\x00\x01\x65" + os.urandom(170_000)  # one IDR NAL: FU-A fragments
+        hist = net.RtpHistory(1024)
+        n = net.send_au(pk, tx, hist, peer, au, 9000)
+        assert n == pk.packets > 128
+        got = [rx.unprotect_rtp(rx_sock.recv(2048)) for _ in range(n)]
+        seqs = [struct.unpack("!H", g[2:4])[0] for g in got]
+        assert seqs == list(range(100, 100 + n))
+        assert all(hist.get(s) == g for s, g in zip(seqs, got))
+    finally:
+        rx_sock.close()
+        tx_sock.close()
