@@ -2508,6 +2508,13 @@ constexpr uint32_t kMaxCtbCost = 4u * kMaxCuCost;
 // A CTB costlier than the spacing T / S spans several thresholds, so the picture may get fewer
 // slices than S: slices start where plan_slice_of changes and are ranked by those starts
 // (plan_p_slices; k_hevc_layout compacts the ranks).
+// I pictures: each slice is one segment of a CTB row (two per row when the level's slice count
+// allows), so the intra wavefront of a slice runs over half the row.  The 16x16-unit column range
+// [xb, xe) of the segment holding unit column x, segments seg_w units wide.
+MXHD void i_seg_range(int x, int seg_w, int mb_w, int& xb, int& xe) {
+    xb = (x / seg_w) * seg_w;
+    xe = xb + seg_w < mb_w ? xb + seg_w : mb_w;
+}
 MXHD int plan_num_slices(uint64_t total, int max_slices, uint32_t cost_per_slice = kCostPerSlice) {
     const uint32_t cps = cost_per_slice > 0 ? cost_per_slice : 1u;
     const uint64_t s = total / cps;

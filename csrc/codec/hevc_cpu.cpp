@@ -100,13 +100,17 @@ HevcCommon::HevcCommon(const EncoderConfig& c) : rc_(c) {
     const int maxs = max_slices_for_level(level_);
     slice_rows_ = 1;
     while ((c32_h() + slice_rows_ - 1) / slice_rows_ > maxs) ++slice_rows_;
+    // two I slices per CTB row when the level allows: each intra wavefront then runs over half a
+    // row (the 4K IDR's chain of 242 unit steps becomes 122, profiles/r05_SUMMARY.md)
+    const int rows = (c32_h() + slice_rows_ - 1) / slice_rows_;
+    i_split_ = (!c.hevc_wpp && c32_w() >= 2 && 2 * rows <= std::min(maxs, kMaxSlices)) ? 2 : 1;  // (WPP: row substreams)
     if (num_slices() > kMaxSlices) throw std::invalid_argument("hevc: too many slices");
     max_slices_ = std::min({maxs, kMaxSlices, num_ctbs()});
 }
 
 std::vector<int> HevcCommon::row_slices() const {
     std::vector<int> f;
-    for (int s = 0; s < num_slices(); ++s) f.push_back(s * slice_rows_ * c32_w());
+    for (int s = 0; s < num_slices(); ++s) f.push_back((s / i_split_) * slice_rows_ * c32_w() + (s % i_split_) * (i_seg_w() / 2));
     return f;
 }
 
@@ -408,10 +412,13 @@ void summarise(CuInfo& c, const int16_t* coef) {
 // uses the modes in `safe` -- bl_safe_modes -- because the raster wavefront reconstructs it before
 // its below-left), scored by the 4x4 Hadamard SATD of the residual + lambda * mode bits; the lowest
 // cost wins, ties to the lower mode.
-int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int qp, uint64_t safe) {
+int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int seg_w, int qp,
+                      uint64_t safe) {
     const int x0 = x * 16, y0 = y * 16, z = ((y & 1) << 1) | (x & 1);
-    const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < mb_w && z != 3, ac = at && x > 0;
-    const bool bl_pending = z == 0 && x > 0 && y + 1 < mb_h;
+    int xb, xe;
+    i_seg_range(x, seg_w, mb_w, xb, xe);
+    const bool al = x > xb, at = (y % sr) != 0, atr = at && x + 1 < xe && z != 3, ac = at && x > xb;
+    const bool bl_pending = z == 0 && x > xb && y + 1 < mb_h;
     uint8_t lp[16], tp[16], tr[16];
     for (int k = 0; k < 16; ++k) {
         lp[k] = al ? sy[(size_t)(y0 + k) * pitch + x0 - 1] : 0;
@@ -469,7 +476,9 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             const int z = ((y & 1) << 1) | (x & 1);
             CuInfo& c = cu_[i];
             std::memset(&c, 0, sizeof c);
-            const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < W && z != 3, ac = at && x > 0;
+            int xb, xe;
+            i_seg_range(x, common_.i_seg_w(), W, xb, xe);
+            const bool al = x > xb, at = (y % sr) != 0, atr = at && x + 1 < xe && z != 3, ac = at && x > xb;
             uint8_t lp[16], tp[16], tr[16];
             for (int k = 0; k < 16; ++k) {
                 lp[k] = al ? ry[(y0 + k) * cw_ + x0 - 1] : 0;
@@ -479,7 +488,7 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             const int corner = ac ? ry[(y0 - 1) * cw_ + x0 - 1] : 0;
             int L[33], T[33];
             intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
-            const int best = intra_decide_mode(sy, pitch, W, H, x, y, sr, qp, bl_safe_);
+            const int best = intra_decide_mode(sy, pitch, W, H, x, y, sr, common_.i_seg_w(), qp, bl_safe_);
             int pred[256];
             c.type = kCuIntra;
             c.intra_mode = (uint8_t)best;

@@ -188,6 +188,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.idr = idr ? 1 : 0;
     f.qp = qp;
     f.slice_rows = 2 * common_.slice_rows();  // in 16x16-unit rows
+    f.i_seg_w = common_.i_seg_w();
     f.num_slices = common_.num_slices();
     f.bl_safe = bl_safe_;
     f.depth_inter = common_.depth_inter();
@@ -197,7 +198,7 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     // distortion partials: k_hevc_sao (totals) with SAO, else k_hevc_sse (one per unit row) after
     // deblocking, else the analysis kernels' (P: one per CTB, I: one per unit row)
     f.n_sse_parts = f.sao ? common_.num_ctbs()
-                          : ((idr || cfg_.hevc_deblock()) ? geom_.mb_h : common_.num_ctbs());
+                          : (cfg_.hevc_deblock() ? geom_.mb_h : (idr ? geom_.mb_h * common_.i_split() : common_.num_ctbs()));
     f.sse_part = sl.buf.sse_part;
     f.sse_tot = sl.buf.sse_tot;
     for (int k = 0; k < 4; ++k) f.mask_c[k] = mask_c_[k];

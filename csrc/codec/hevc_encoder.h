@@ -45,7 +45,9 @@ class HevcCommon {
     // quadrants at depth 1 may split too), else 0
     int depth_inter() const { return config().tu_split ? 3 : 0; }
     int slice_rows() const { return slice_rows_; }  // CTB rows per I slice
-    int num_slices() const { return (c32_h() + slice_rows_ - 1) / slice_rows_; }
+    int i_split() const { return i_split_; }        // I slices per CTB row (segments)
+    int i_seg_w() const { return 2 * ((c32_w() + i_split_ - 1) / i_split_); }  // 16x16-unit columns per segment
+    int num_slices() const { return (c32_h() + slice_rows_ - 1) / slice_rows_ * i_split_; }
     int level_idc() const { return level_; }
     int max_slices() const { return max_slices_; }  // level limit (MaxSliceSegmentsPerPicture), capped
     // POC LSB (8 bits) of the current frame = frames since the last IDR.
@@ -74,12 +76,14 @@ class HevcCommon {
    private:
     h264::EncoderCommon rc_;
     int slice_rows_ = 1;
+    int i_split_ = 1;
     int level_ = 0;
     int max_slices_ = 1;
 };
 
 // Open-loop intra mode of a 16x16 unit (hevc_cpu.cpp; the GPU's k_hevc_intra_modes).
-int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int qp, uint64_t safe);
+int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int seg_w, int qp,
+                      uint64_t safe);
 // Direct vs bin-token CABAC on random slices (hevc_cpu.cpp); returns the slices checked.
 int token_selftest(uint32_t seed, int slices);
 // Entropy-code the slice of CTBs [first, end) with wavefront parallel processing (host): every CTB
@@ -145,6 +149,7 @@ struct HevcFrameState {
     int32_t idr;
     int32_t qp;
     int32_t slice_rows;  // 16x16-unit rows per I slice (two per CTB row)
+    int32_t i_seg_w;     // 16x16-unit columns per I slice (a CTB row in one or two segments)
     int32_t num_slices;
     int32_t aq;
     int32_t chroma_qp_offset;

@@ -1118,8 +1118,10 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
     if (x >= g.mb_w || y >= g.mb_h) return;  // wave-uniform; no workgroup barrier below
     IntraRefs& R = rf[wave];
     const int sr = fs->slice_rows, z = ((y & 1) << 1) | (x & 1);
-    const bool al = x > 0, at = (y % sr) != 0, atr = at && x + 1 < g.mb_w && z != 3, ac = at && x > 0;
-    const bool bl_pending = z == 0 && x > 0 && y + 1 < g.mb_h;
+    int xb, xe;
+    i_seg_range(x, fs->i_seg_w, g.mb_w, xb, xe);
+    const bool al = x > xb, at = (y % sr) != 0, atr = at && x + 1 < xe && z != 3, ac = at && x > xb;
+    const bool bl_pending = z == 0 && x > xb && y + 1 < g.mb_h;
     const int x0 = x * 16, y0 = y * 16, P = g.pitch;
     if (lane < 16) {
         R.lpx[lane] = al ? src_y[(size_t)(y0 + lane) * P + x0 - 1] : 0;
@@ -1207,7 +1209,10 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     const int H = max(1, ((int)blockDim.x >> 6) / sr);
     const int row = wave / H, sub = wave - row * H, mw = row * H;
     const bool main_w = sub == 0;
-    const int y = blockIdx.x * sr + row;  // CTU row of this wave
+    // slice blockIdx.x: segment seg of CTB row band blockIdx.x / split (unit columns [xb, xe))
+    const int seg_w = fs->i_seg_w, split = (g.mb_w + seg_w - 1) / seg_w;
+    const int seg = (int)blockIdx.x % split, xb = seg * seg_w, xe = min(g.mb_w, xb + seg_w);
+    const int y = ((int)blockIdx.x / split) * sr + row;  // CTU row of this wave
     const bool row_ok = row < sr && y < g.mb_h;
     const int qp = fs->qp;
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
@@ -1219,20 +1224,20 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     TuBuf& t = tb[wave];
     IntraRefs& R = rf[wave];
     unsigned long long acc[3] = {0, 0, 0};
-    const int steps = g.mb_w + 2 * (sr - 1);
+    const int steps = (xe - xb) + 2 * (sr - 1);
     // this lane's source samples of the CTU, loaded a step ahead (off the critical path):
     // luma row lane / 4, columns 4 (lane % 4) .. +3; chroma row lane / 8, Cb/Cr pair lane % 8
     auto load_src = [&](int xx, uint32_t& ly, uint32_t& lc) {
-        if (!row_ok || xx < 0 || xx >= g.mb_w) return;
+        if (!row_ok || xx < xb || xx >= xe) return;
         const int r = lane >> 2, cb = (lane & 3) * 4, rc = lane >> 3, cc = lane & 7;
         ly = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y * 16 + r) * g.pitch + xx * 16 + cb);
         lc = *reinterpret_cast<const uint16_t*>(src_uv + (size_t)(y * 8 + rc) * g.pitch + xx * 16 + 2 * cc);
     };
     uint32_t nsy = 0, nsc = 0;
-    load_src(-2 * row, nsy, nsc);
+    load_src(xb - 2 * row, nsy, nsc);
     for (int step = 0; step < steps; ++step) {
-        const int x = step - 2 * row;
-        const bool valid = row_ok && x >= 0 && x < g.mb_w;
+        const int x = xb + step - 2 * row;
+        const bool valid = row_ok && x >= xb && x < xe;
         const int x0 = x * 16, y0 = y * 16;
         const uint32_t sy4 = nsy, sc2 = nsc;
         load_src(x + 1, nsy, nsc);
@@ -1240,7 +1245,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         // unit's below-left (the left CTB's last unit) is available there but not reconstructed yet
         // by this raster wavefront: k_hevc_intra_modes gave that unit a mode that never reads it
         const int z = ((y & 1) << 1) | (x & 1);
-        const bool al = x > 0, at = row > 0, atr = at && x + 1 < g.mb_w && z != 3, ac = at && x > 0;
+        const bool al = x > xb, at = row > 0, atr = at && x + 1 < xe && z != 3, ac = at && x > xb;
         // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
         if (valid) {
             if (lane < 16) {
@@ -1361,7 +1366,7 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         __syncthreads();
     }
     if (row_ok && main_w && lane < 3)  // wave sums (identical in every lane)
-        fs->sse_part[lane * h264::kSsePartStride + y] = lane == 0 ? acc[0] : (lane == 1 ? acc[1] : acc[2]);
+        fs->sse_part[lane * h264::kSsePartStride + y * split + seg] = lane == 0 ? acc[0] : (lane == 1 ? acc[1] : acc[2]);
 }
 
 // ------------------------------------------------------------------ slice layout
@@ -1460,9 +1465,13 @@ __global__ __launch_bounds__(1024) void k_hevc_layout(const HevcFrameState* __re
         const int rows = ncu / ctb_w;
         const int sr = fs->idr ? fs->slice_rows / 2 : fs->wpp_rows;  // (slice_rows counts 16x16-unit rows)
         const int S = fs->idr ? fs->num_slices : (rows + sr - 1) / sr;
+        // I: segments of segc CTBs (split per row band, i_seg_range); WPP: whole rows
+        const int segc = fs->idr ? fs->i_seg_w / 2 : ctb_w, split = (ctb_w + segc - 1) / segc;
         const int stride = (int)(gridDim.x * blockDim.x);
-        for (int k = t * (int)blockDim.x + tid; k < S; k += stride) slice_first[k] = k * sr * ctb_w;
-        for (int i = t * (int)blockDim.x + tid; i < ncu; i += stride) slice_of_cu[i] = (i / ctb_w) / sr;
+        for (int k = t * (int)blockDim.x + tid; k < S; k += stride)
+            slice_first[k] = (k / split) * sr * ctb_w + (k % split) * segc;
+        for (int i = t * (int)blockDim.x + tid; i < ncu; i += stride)
+            slice_of_cu[i] = ((i / ctb_w) / sr) * split + (i % ctb_w) / segc;
         if (t == 0 && tid == 0) *nslices = (uint32_t)S;
         return;
     }
