@@ -76,6 +76,7 @@ def quality_probe(s, W: int, H: int, content: int, noise: int, n: int = 30) -> d
     sse = np.zeros(len(REGION_NAMES))
     cnt = np.zeros(len(REGION_NAMES))
     suv = [0.0, 0.0]
+    suv_m, cnt_m = [0.0, 0.0], 0
     for _ in range(n):
         r = s.step(False)
         sy, su = s.nv12()
@@ -92,9 +93,12 @@ def quality_probe(s, W: int, H: int, content: int, noise: int, n: int = 30) -> d
         e = (ry[:H, :W].astype(np.int64) - sy[:H, :W].astype(np.int64)) ** 2
         sse += np.bincount(cls.ravel(), weights=e.ravel(), minlength=len(REGION_NAMES))
         cnt += np.bincount(cls.ravel(), minlength=len(REGION_NAMES))
+        keep = cls[0:H - H % 2:2, 0:W - W % 2:2] != 3  # chroma samples outside the noise panel
+        cnt_m += int(keep.sum())
         for c in range(2):
             d = ru[:H // 2, c:W:2].astype(np.int64) - su[:H // 2, c:W:2].astype(np.int64)
             suv[c] += float((d * d).sum())
+            suv_m[c] += float((d * d)[keep].sum())
 
     def psnr(e, k):
         return 99.0 if e <= 0 else round(min(99.0, 10 * np.log10(65025.0 * k / e)), 2)
@@ -102,14 +106,16 @@ def quality_probe(s, W: int, H: int, content: int, noise: int, n: int = 30) -> d
     regions = {REGION_NAMES[k]: psnr(sse[k], cnt[k]) for k in range(len(REGION_NAMES)) if cnt[k] > 0}
     y = psnr(sse.sum(), cnt.sum())
     out = {"frames": n, "psnr_y_db": y, "psnr_u_db": psnr(suv[0], n * (W // 2) * (H // 2)),
-           "psnr_v_db": psnr(suv[1], n * (W // 2) * (H // 2)), "regions_psnr_y_db": regions}
+           "psnr_v_db": psnr(suv[1], n * (W // 2) * (H // 2)), "regions_psnr_y_db": regions,
+           # chroma with the incompressible noise panel left out, as the masked luma figure
+           "psnr_u_db_noise_masked": psnr(suv_m[0], cnt_m), "psnr_v_db_noise_masked": psnr(suv_m[1], cnt_m)}
     scored = {k: v for k, v in regions.items() if k not in ("noise", "barcode")}
     out["worst_region_below_frame_db"] = round(y - min(scored.values()), 2) if scored else None
     return out
 
 
 def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: float = 1.0,
-                  threads: int = 8, idr_storm: bool = False) -> dict:
+                  threads: int = 8, idr_storm: bool = False, cpu_noise: int | None = None) -> dict:
     """Paced concurrent sessions on this GPU: K sessions (same config, pipeline depth 1) driven by
     `threads` host threads (N.run_sessions_paced: every 1/fps slot each thread submits one frame
     per session it owns, then collects them); K is sustained if no slot overran (every frame of
@@ -118,10 +124,41 @@ def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: flo
     `sustained` is a measured limit -- the first failing K minus the resolution -- not a list cap.
     The whole serving path per session (render, CSC, encode, bitstream to host) runs.
     idr_storm: in the middle slot every session codes a forced IDR picture (viewers joining at once,
-    a PLI burst); K is sustained only if that slot, too, finishes within its period."""
+    a PLI burst); K is sustained only if that slot, too, finishes within its period.
+    cpu_noise not None: the no-GPU plumbing configuration -- K CpuSessions (numpy desktop + C++
+    CPU encoder) stepped from this thread, each slot's frames due within the slot."""
     out = {"fps": fps, "seconds": seconds, "threads": threads, "idr_storm": idr_storm, "tried": {}}
 
+    def cpu_trial(K: int) -> bool:
+        sess = []
+        for _ in range(K):
+            c = N.SessionConfig()
+            c.width, c.height, c.fps = cfg.width, cfg.height, cfg.fps
+            c.enc.bitrate_kbps = cfg.enc.bitrate_kbps
+            sess.append(CpuSession(N, c, cpu_noise))
+        for s in sess:
+            s.step(False)
+        slots = max(1, round(seconds * fps))
+        late, lat = 0, []
+        t_next = time.perf_counter()
+        for k in range(slots):
+            t_next += 1.0 / fps
+            for s in sess:
+                r = s.step(idr_storm and k == slots // 2, quality=False)
+                lat.append((r.t_encoded_us - r.t_capture_us) / 1000.0)
+            now = time.perf_counter()
+            if now > t_next:
+                late += 1
+                t_next = now
+            else:
+                time.sleep(t_next - now)
+        lat.sort()
+        out["tried"][K] = {"late_slots": late, "slots": slots, "p50_ms": round(lat[len(lat) // 2], 3)}
+        return late == 0
+
     def trial(K: int) -> bool:
+        if cpu_noise is not None:
+            return cpu_trial(K)
         sess = []
         try:
             for _ in range(K):
@@ -171,14 +208,20 @@ def density_probe(N, cfg, fps: int, k0: int = 8, k_max: int = 1024, seconds: flo
     return out
 
 
-def launch_ranks(n: int) -> int:
+def launch_ranks(n: int, timeout_s: float | None = None) -> int:
     """`bench.py --gpus N` without WORLD_SIZE: run N rank processes of this script (RANK /
     LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them, rendezvous on
-    127.0.0.1), wait for all of them and return the first non-zero exit code.  Rank 0 prints the
-    JSON line; the ranks share this process's stdout."""
+    127.0.0.1) and return the first non-zero exit code.  Rank 0 prints the JSON line; the ranks
+    share this process's stdout.  All children are polled: when one fails (e.g. before or during
+    init_process_group, which would leave the others blocked in the rendezvous) the rest are
+    terminated and its code returned; an overall time limit (MXDESK_BENCH_TIMEOUT seconds,
+    default 1800) ends a hung job with 124."""
+    import signal
     import socket
     import subprocess
 
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("MXDESK_BENCH_TIMEOUT", "") or 1800)
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
@@ -187,9 +230,34 @@ def launch_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        t_kill = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    deadline = time.monotonic() + timeout_s
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            print(f"bench.py: a rank exited with {bad[0]}; stopping the others", file=sys.stderr)
+            stop_all()
+            return bad[0]
+        if all(c == 0 for c in codes):
+            return 0
+        if time.monotonic() > deadline:
+            print(f"bench.py: ranks still running after {timeout_s:.0f} s; stopping them", file=sys.stderr)
+            stop_all()
+            return 124
+        time.sleep(0.05)
 
 
 class CpuSession:
@@ -207,7 +275,7 @@ class CpuSession:
         self.fps = cfg.fps
         self.n = 0
 
-    def step(self, force_idr: bool = False):
+    def step(self, force_idr: bool = False, quality: bool = True):
         import types
 
         import numpy as np
@@ -219,6 +287,8 @@ class CpuSession:
         t1 = time.monotonic()
         st = self.enc.stats
         self.n += 1
+        if not quality:
+            return types.SimpleNamespace(au=au, qp=st.qp, t_capture_us=t0 * 1e6, t_encoded_us=t1 * 1e6)
         w, h = self.desk.w, self.desk.h
         ry, ruv = self.enc.recon()
 
@@ -324,10 +394,9 @@ def main() -> None:
         sys.exit(launch_ranks(args.gpus))
     gpu = args.device == "gpu"
     if not gpu:  # plumbing configuration: CPU encoder, gloo, no GPU-only probes
-        args.codec, args.backend, args.density_probe, args.quality_probe = "h264", "gloo", 0, 0
+        args.codec, args.backend, args.quality_probe = "h264", "gloo", 0
         args.depth, args.sessions_per_gpu, args.out_width, args.out_height = 1, 1, 0, 0
     if args.codec == "vp8":
-        args.subpel = 0  # VP8 vectors here are full-sample (the reported ME setting says so)
         args.depth = min(args.depth or 4, 4)  # the VP8 encoder keeps at most four frames in flight
     if args.depth is None:
         args.depth = 3
@@ -338,6 +407,9 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MXDESK_BENCH_FAIL_RANK", "") == str(rank):  # tests: a rank dying before rendezvous
+        print(f"bench.py: rank {rank} fails (MXDESK_BENCH_FAIL_RANK)", file=sys.stderr)
+        sys.exit(3)
 
     import torch
 
@@ -470,7 +542,11 @@ def main() -> None:
     quality = None
     if args.quality_probe > 0 and rank == 0 and not args.out_width:
         quality = quality_probe(sessions[0], args.width, args.height, content, args.noise, args.quality_probe)
-    density = density_probe(N, cfg, args.fps) if args.density_probe else None
+    if args.density_probe:
+        density = (density_probe(N, cfg, args.fps) if gpu else
+                   density_probe(N, cfg, args.fps, k0=1, k_max=64, seconds=0.25, cpu_noise=args.noise))
+    else:
+        density = None
     # the same probe with every session's IDR in one slot, from a quarter of the steady-state K
     storm = (density_probe(N, cfg, args.fps, k0=max(4, (density["sustained"] or 16) // 4), idr_storm=True)
              if args.density_probe and gpu else None)
@@ -485,8 +561,17 @@ def main() -> None:
         gsz = [None] * world
         dist.all_gather_object(gsz, sizes)
         all_sizes = [x for g in gsz for x in g]
+        # every rank probed its own GPU: the node's figure is the sum over ranks
+        gd = [None] * world
+        dist.all_gather_object(gd, [density["sustained"] if density else None, storm["sustained"] if storm else None])
+        rank_density, rank_storm = [d[0] for d in gd], [d[1] for d in gd]
     else:
         elapsed_max, all_lat, all_sizes = elapsed, lat_ms, sizes
+        rank_density = [density["sustained"] if density else None]
+        rank_storm = [storm["sustained"] if storm else None]
+
+    def node_sum(v):
+        return None if any(x is None for x in v) else sum(v)
 
     total_frames = args.steps * world * K
     fps_total = total_frames / elapsed_max
@@ -528,6 +613,8 @@ def main() -> None:
             "mean_psnr_y_db_noise_masked": round(statistics.mean(psnrs_m), 2),
             "mean_psnr_u_db": round(statistics.mean(u for u, _ in psnr_uv), 2),
             "mean_psnr_v_db": round(statistics.mean(v for _, v in psnr_uv), 2),
+            "mean_psnr_u_db_noise_masked": quality["psnr_u_db_noise_masked"] if quality else None,
+            "mean_psnr_v_db_noise_masked": quality["psnr_v_db_noise_masked"] if quality else None,
             "content": args.content,
             "quality_probe": quality,
             # measured, not extrapolated: K paced sessions (one HIP stream each, depth 1) on this
@@ -535,6 +622,13 @@ def main() -> None:
             # slot; K found by doubling then bisecting up to the first failing K
             "sessions_per_gpu_at_60fps_measured": density["sustained"] if density else None,
             "density_probe": density,
+            # the node metric (BASELINE "concurrent sessions/node"): every rank's own measured K,
+            # all-gathered, and their sum -- not rank 0's figure times N
+            "sessions_per_node_measured": node_sum(rank_density),
+            "sessions_per_gpu_measured_min": min(rank_density) if node_sum(rank_density) is not None else None,
+            "sessions_per_gpu_measured_max": max(rank_density) if node_sum(rank_density) is not None else None,
+            "sessions_per_gpu_measured_by_rank": rank_density,
+            "sessions_per_node_idr_storm_measured": node_sum(rank_storm),
             # measured: the sustained K when every session codes a forced IDR in the same slot
             "sessions_per_gpu_idr_storm_measured": storm["sustained"] if storm else None,
             "density_probe_idr_storm": storm,

@@ -228,7 +228,7 @@ def main(argv: list[str] | None = None) -> None:
     elif cmd == "wall":
         from .parallel.wall import wall_main
 
-        wall_main(cfg, layout=args.layout or cfg.wall or "2x2")
+        sys.exit(wall_main(cfg, layout=args.layout or cfg.wall or "2x2", argv=rest))
     else:
         print(f"unknown command {cmd}\n{__doc__}")
         sys.exit(2)

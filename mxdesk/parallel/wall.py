@@ -386,8 +386,25 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, torch.device
     return rank, world, device
 
 
-def wall_main(cfg: Any, layout: str = "2x2") -> None:
+def wall_main(cfg: Any, layout: str = "2x2", argv: list[str] | None = None) -> int:
+    """``mxdesk wall``: one rank per tile.  Started bare (no WORLD_SIZE) it starts the cols x rows
+    rank processes itself (``ranks.run_ranks``: fresh children of the same command, before any
+    GPU call, signals forwarded) and returns their exit code; under torchrun WORLD_SIZE must equal
+    cols x rows (else 2: a wall never runs with a rank per tile missing)."""
+    import sys
+
     cols, rows = parse_layout(layout)
+    need = cols * rows
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and need > 1:
+        from .ranks import run_ranks
+
+        print(f"mxdesk wall {cols}x{rows}: starting {need} rank processes", flush=True)
+        return run_ranks([sys.executable, "-m", "mxdesk", "wall"] + list(argv or ["--layout", layout]), need)
+    if ws is not None and int(ws) != need:
+        print(f"mxdesk wall {cols}x{rows} needs {need} ranks (one per tile) but WORLD_SIZE={ws}: start it bare "
+              f"(it launches its ranks) or with --nproc-per-node {need}", file=sys.stderr, flush=True)
+        return 2
     try:
         rank, world, device = init_distributed()
     except Exception as e:  # degrade to per-GPU sessions (SURVEY.md §5.3)
@@ -395,7 +412,7 @@ def wall_main(cfg: Any, layout: str = "2x2") -> None:
         from .launcher import launch_sessions
 
         launch_sessions(cfg)
-        return
+        return 0
     geo = WallGeometry(cols, rows, cfg.sizew, cfg.sizeh)
     exchange = os.environ.get("MXDESK_WALL_EXCHANGE", "gather")
     if os.environ.get("MXDESK_WALL_MODE", "composite") == "tiles":
@@ -410,11 +427,11 @@ def wall_main(cfg: Any, layout: str = "2x2") -> None:
         finally:
             pipe.stop()
             dist.destroy_process_group()
-        return
+        return 0
     if rank != 0:
         follower_loop(geo, rank, world, device, exchange, cfg.stream_fps)
         dist.destroy_process_group()
-        return
+        return 0
     from ..server.app import MediaServer, run_forever, ssl_context
 
     pipe = WallPipeline(geo, cfg.stream_fps, rank, world, device, exchange, bitrate_kbps=cfg.video_bitrate * 4)
@@ -424,3 +441,4 @@ def wall_main(cfg: Any, layout: str = "2x2") -> None:
     finally:
         pipe.stop()
         dist.destroy_process_group()
+    return 0

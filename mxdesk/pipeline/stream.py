@@ -4,11 +4,14 @@ A ``StreamPipeline`` owns one encoder session (GPU: the native HIP session; CPU:
 desktop + CPU H.264 encoder for the plumbing configuration), produces frames at the stream
 rate on a dedicated thread and pushes each encoded access unit to every subscriber queue
 (asyncio-safe).  Policies:
-  * a new viewer or a PLI/keyframe request forces an IDR on the next frame;
+  * a new viewer or a PLI/keyframe request forces an IDR on the next frame -- through the
+    session's ``KeyframeCoalescer``: requests arriving while an IDR is pending or just sent join
+    it, and forced IDRs are at least ``MXDESK_IDR_MIN_INTERVAL`` (0.25 s) apart;
   * a viewer whose queue overflows is resynchronised: its backlog is dropped, it waits for the
-    next IDR and the pipeline forces one (counted in ``mxdesk_dropped_frames``; without the
-    forced IDR such a viewer received nothing more -- no gap to NACK, no PLI -- until the
+    next IDR and the pipeline requests one (counted in ``mxdesk_dropped_frames``; without the
+    request such a viewer received nothing more -- no gap to NACK, no PLI -- until the
     stream's next key frame: the stalls of the 96-viewer density runs, profiles/r05_density);
+    a viewer that overflows again before draining asks with an exponential backoff;
   * a watchdog restarts the encoder session if no frame was produced for ``stall_s``;
   * ``MXDESK_FAULT`` (tests only) injects failures: ``drop:N`` drops every Nth frame,
     ``stall:S`` stalls the producer once for S seconds, ``crash:N`` raises at frame N.
@@ -17,6 +20,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import math
 import os
 import threading
 import time
@@ -75,14 +79,98 @@ def h264_codec_string(width: int, height: int, fps: int) -> str:
     return f"avc1.42C0{level:02X}"
 
 
+class KeyframeCoalescer:
+    """Per-session keyframe-request coalescer (ADVICE r5 stream.py:323).
+
+    Every source of a forced IDR -- RTCP PLI / FIR, the WebSocket client's ``pli``, a new viewer,
+    a viewer whose queue overflowed, an encoder restart -- goes through :meth:`request`.  An IDR
+    costs about five frame-times of link time at CBR (the IDR budget, h264_encoder.h), and a
+    burst of PLIs (every viewer of a lossy link, a browser repeating its request until a key frame
+    arrives) used to code one IDR per request.  The rules:
+
+      * a request while an IDR is already pending (requested, not yet coded) joins it;
+      * a PLI / FIR / client request within ``min_interval`` of the last IDR is covered by that
+        IDR (it is still on its way to the viewer that asked) and is dropped;
+      * a request that needs a *new* key frame (a new viewer, a resynchronising viewer) is kept
+        but not coded before ``last IDR + min_interval``, so the IDR rate of a session is bounded
+        by 1 / min_interval whatever the viewers do;
+      * any IDR the encoder codes (periodic, first frame, forced) satisfies what is pending.
+
+    ``min_interval`` defaults to ``MXDESK_IDR_MIN_INTERVAL`` seconds (0.25: four IDRs per second at
+    most).  Counts per reason, coalesced requests and forced IDRs are exported on ``/metrics``.
+    The reference has no equivalent: ``nvh264enc`` codes an IDR per upstream force-key-unit event
+    (reference Dockerfile:210, selkies-gstreamer [UP])."""
+
+    COVERED_BY_RECENT = ("pli", "fir", "client")
+
+    def __init__(self, min_interval_s: float | None = None, clock: Callable[[], float] = time.monotonic,
+                 metrics: SessionMetrics | None = None):
+        if min_interval_s is None:
+            min_interval_s = float(os.environ.get("MXDESK_IDR_MIN_INTERVAL", "") or 0.25)
+        self.min_interval = max(0.0, float(min_interval_s))
+        self.clock = clock
+        self.metrics = metrics
+        self._lock = threading.Lock()
+        self.pending = False
+        self.not_before = 0.0
+        self.last_idr_t = -math.inf
+        self.requests: dict[str, int] = {}
+        self.coalesced = 0
+        self.forced = 0
+
+    def request(self, reason: str = "api") -> bool:
+        """Ask for a key frame; returns True if this request scheduled one (False: it joined a
+        pending IDR or was covered by the one just coded)."""
+        now = self.clock()
+        with self._lock:
+            self.requests[reason] = self.requests.get(reason, 0) + 1
+            joined = self.pending or (reason in self.COVERED_BY_RECENT and now - self.last_idr_t < self.min_interval)
+            if joined:
+                self.coalesced += 1
+            else:
+                self.pending = True
+                self.not_before = self.last_idr_t + self.min_interval
+        if self.metrics is not None:
+            self.metrics.on_keyframe_request(reason, joined)
+        return not joined
+
+    def take(self) -> bool:
+        """Producer, once per frame: True if this frame must be coded as an IDR."""
+        with self._lock:
+            if self.pending and self.clock() >= self.not_before:
+                self.pending = False
+                self.forced += 1
+                return True
+            return False
+
+    def on_idr(self) -> None:
+        """An IDR was coded (forced or not): it satisfies every pending request."""
+        with self._lock:
+            self.last_idr_t = self.clock()
+            self.pending = False
+
+    def snapshot(self) -> dict:
+        with self._lock:
+            return {"requests": dict(self.requests), "coalesced": self.coalesced, "forced": self.forced,
+                    "pending": self.pending, "min_interval_s": self.min_interval}
+
+
 class _Subscriber:
+    # a viewer that keeps overflowing (a stalled socket) asks for its resynchronising IDR with an
+    # exponential backoff: 0, 0.5, 1, 2, 4 s after its previous one; reset once it drains
+    BACKOFF_S = (0.0, 0.5, 1.0, 2.0, 4.0)
+
     def __init__(self, loop: asyncio.AbstractEventLoop, maxsize: int):
         self.loop = loop
         self.queue: asyncio.Queue = asyncio.Queue(maxsize=maxsize)
         self.need_idr = True
         self.dropped = 0
+        self.overflows = 0        # consecutive overflows without the viewer reading in between
+        self.last_resync_t = -math.inf
+        self._queued = 0          # frames put since the queue was last cleared
+        self.resync_at: float | None = None  # backed-off resynchronising IDR request, due then
 
-    def offer(self, fr: EncodedFrame, on_drop: Callable[[int], None]) -> None:
+    def offer(self, fr: EncodedFrame, on_drop: Callable[["_Subscriber", int], None]) -> None:
         def put():
             if self.need_idr and not fr.idr:
                 return
@@ -91,10 +179,14 @@ class _Subscriber:
                 while not self.queue.empty():
                     self.queue.get_nowait()
                 self.dropped += n
-                on_drop(n)
                 self.need_idr = True
+                self._queued = 0
+                on_drop(self, n)
                 return
             self.need_idr = False
+            if self.queue.qsize() < self._queued:
+                self.overflows = 0  # the viewer reads its queue again
+            self._queued = self.queue.qsize() + 1
             self.queue.put_nowait(fr)
 
         try:
@@ -108,7 +200,8 @@ class StreamPipeline:
                  bitrate_kbps: int = 8000, keyint: int = 0, search_range: int = 16, subpel: bool = True,
                  noise: bool = True, out_width: int = 0, out_height: int = 0, session_name: str = "0",
                  capture: Any = None, metrics: SessionMetrics | None = None, queue_frames: int | None = None,
-                 stall_s: float = 2.0, paced: bool = True, codec: str = "h264"):
+                 stall_s: float = 2.0, paced: bool = True, codec: str = "h264",
+                 idr_min_interval_s: float | None = None):
         if codec not in CODEC_IDS:
             raise ValueError(f"unknown codec {codec!r} (h264 | hevc | vp8)")
         self.codec = codec
@@ -132,7 +225,8 @@ class StreamPipeline:
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
-        self._force_idr = True
+        self.keyframes = KeyframeCoalescer(idr_min_interval_s, metrics=self.metrics)
+        self.keyframes.request("viewer")  # the first frame is an IDR anyway
         self._pending_bitrate: int | None = None
         self._cursor = (-1, -1)
         self._pending_resize: tuple[int, int] | None = None
@@ -238,8 +332,10 @@ class StreamPipeline:
                             codec_id=self.codec_id)
 
     # ------------------------------------------------------------------ control
-    def request_idr(self) -> None:
-        self._force_idr = True
+    def request_idr(self, reason: str = "api") -> bool:
+        """Ask for a key frame (PLI / FIR / a client request / a new viewer ...); requests are
+        coalesced and rate-limited per session (KeyframeCoalescer)."""
+        return self.keyframes.request(reason)
 
     def set_bitrate(self, kbps: int) -> None:
         self._pending_bitrate = int(max(100, min(kbps, 200_000)))
@@ -268,7 +364,7 @@ class StreamPipeline:
         self.width, self.height = w, h
         self.out_w, self.out_h = w, h
         self._make_session()
-        self._force_idr = True
+        self.keyframes.request("resize")
         self.resizes += 1
         log.info("session resized to %dx%d", w, h)
 
@@ -280,7 +376,7 @@ class StreamPipeline:
         with self._lock:
             self._subs.append(sub)
             self.metrics.set_clients(len(self._subs))
-        self.request_idr()
+        self.request_idr("viewer")
         return sub
 
     def unsubscribe(self, sub: _Subscriber) -> None:
@@ -300,14 +396,16 @@ class StreamPipeline:
         pending, self._pending_resize = self._pending_resize, None
         if pending is not None:
             self._apply_resize(*pending)
-        force = self._force_idr
-        self._force_idr = False
+        self._due_resyncs()
+        force = self.keyframes.take()
         n = self.frames_out
         if "crash" in self._fault and n == int(self._fault["crash"]):
             raise RuntimeError("injected encoder crash")
         if "stall" in self._fault and n == 3:
             time.sleep(self._fault.pop("stall"))
         fr = self._produce(force)
+        if fr.idr:
+            self.keyframes.on_idr()
         self.frames_out += 1
         self.last_frame_t = time.monotonic()
         self.metrics.on_frame(len(fr.au), (fr.t_encoded_us - fr.t_capture_us) / 1000.0, fr.gpu_ms, fr.qp, fr.idr)
@@ -320,11 +418,31 @@ class StreamPipeline:
             s.offer(fr, self._on_sub_overflow)
         return fr
 
-    def _on_sub_overflow(self, n: int) -> None:
-        """A viewer's queue overflowed (event-loop thread): count the dropped frames and force an
-        IDR so that viewer resynchronises at the next frame."""
+    def _on_sub_overflow(self, sub: _Subscriber, n: int) -> None:
+        """A viewer's queue overflowed (event-loop thread): count the dropped frames and ask for an
+        IDR so that viewer resynchronises at the next key frame.  The request goes through the
+        session's coalescer (rate-bounded), and a viewer that overflows again before it drained
+        asks with an exponential backoff (a stalled socket does not drive the session's IDR rate)."""
         self.metrics.on_drop(n)
-        self._force_idr = True
+        now = self.keyframes.clock()
+        wait = sub.BACKOFF_S[min(sub.overflows, len(sub.BACKOFF_S) - 1)]
+        sub.overflows += 1
+        if now - sub.last_resync_t >= wait:
+            sub.last_resync_t = now
+            sub.resync_at = None
+            self.request_idr("overflow")
+        else:  # asked again when its backoff has passed (step() checks)
+            sub.resync_at = sub.last_resync_t + wait
+            self.metrics.on_keyframe_request("overflow_backoff", True)
+
+    def _due_resyncs(self) -> None:
+        now = self.keyframes.clock()
+        with self._lock:
+            due = [s for s in self._subs if s.resync_at is not None and now >= s.resync_at]
+        for s in due:
+            s.resync_at = None
+            s.last_resync_t = now
+            self.request_idr("overflow")
 
     def _run(self) -> None:
         # pacing phase (seconds into the frame period): sessions of one process start staggered
@@ -344,7 +462,7 @@ class StreamPipeline:
                     self._make_session()
                 except Exception:
                     log.exception("session restart failed")
-                self.request_idr()
+                self.request_idr("restart")
                 self._stop.wait(min(2.0, 0.1 * self.restarts))  # back off on repeated failures
             if self.paced:
                 next_t += 1.0 / (getattr(self, "pace_fps", None) or self.fps)
@@ -372,7 +490,8 @@ class StreamPipeline:
     def status(self) -> dict:
         return {"backend": self.backend, "device": self.device, "width": self.out_w, "height": self.out_h,
                 "fps": self.fps, "frames": self.frames_out, "clients": self.subscribers, "restarts": self.restarts,
-                "last_error": self.last_error, "resizes": self.resizes, **self.metrics.summary()}
+                "last_error": self.last_error, "resizes": self.resizes, "keyframes": self.keyframes.snapshot(),
+                **self.metrics.summary()}
 
 
 def frame_header(fr: EncodedFrame, t_send_us: int) -> bytes:

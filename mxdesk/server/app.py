@@ -306,7 +306,7 @@ class MediaServer:
             return
         p = self.pipeline
         if ev.kind == "pli":
-            p.request_idr()
+            p.request_idr("client")
         elif ev.kind == "bitrate":
             p.set_bitrate(int(ev.value))
         elif ev.kind == "ack":

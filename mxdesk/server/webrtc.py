@@ -695,7 +695,7 @@ class WebRtcPeer(asyncio.DatagramProtocol):
         for p in R.parse_rtcp(pkt):
             if p["pt"] == 206 and p["fmt"] in (1, 4):  # PLI / FIR
                 self.stats["pli"] += 1
-                self.pipeline.request_idr()
+                self.pipeline.request_idr("pli" if p["fmt"] == 1 else "fir")
             elif "remb_bps" in p:
                 self.cc.on_remb(p["remb_bps"])
             elif p["pt"] in (200, 201) and p.get("reports"):

@@ -54,6 +54,12 @@ class SessionMetrics:
                                 buckets=LAT_BUCKETS_MS, registry=self.registry)
         self.gpu_ms = Histogram("mxdesk_gpu_encode_ms", "GPU encode time (ms)", lab, buckets=LAT_BUCKETS_MS,
                                 registry=self.registry)
+        self.kf_requests = Counter("mxdesk_keyframe_requests", "Keyframe requests by reason (pli, fir, client, viewer, "
+                                   "overflow, overflow_backoff, restart, resize)", ["session", "reason"],
+                                   registry=self.registry)
+        self.kf_coalesced = Counter("mxdesk_keyframe_requests_coalesced", "Keyframe requests that joined a pending "
+                                    "or just-coded IDR (or waited out a viewer's backoff)", lab,
+                                    registry=self.registry)
         self.qp = Gauge("mxdesk_qp", "Current QP", lab, registry=self.registry)
         self.bitrate = Gauge("mxdesk_bitrate_kbps", "Measured bitrate (kbps, 1 s window)", lab,
                              registry=self.registry)
@@ -90,6 +96,11 @@ class SessionMetrics:
     def on_client_latency(self, ms: float) -> None:
         self.e2e_ms.labels(self.session).observe(ms)
         self.roll_e2e.add(ms)
+
+    def on_keyframe_request(self, reason: str, coalesced: bool) -> None:
+        self.kf_requests.labels(self.session, reason).inc()
+        if coalesced:
+            self.kf_coalesced.labels(self.session).inc()
 
     def on_drop(self, n: int = 1) -> None:
         self.dropped.labels(self.session).inc(n)
