@@ -243,6 +243,7 @@ void me_search_parts_cpu(const uint8_t* sy, int pitch, const uint8_t* ref_y, int
 }
 
 CpuH264Encoder::CpuH264Encoder(const EncoderConfig& cfg) : cfg_(cfg.with_aq_default(4)), common_(cfg) {
+    db_lag_.reset(cfg_.h264_deblock_mode());
     cw_ = common_.mb_w() * 16;
     ch_ = common_.mb_h() * 16;
     for (int i = 0; i < 2; ++i) {
@@ -588,16 +589,14 @@ void CpuH264Encoder::encode_intra(const uint8_t* sy, const uint8_t* suv, int pit
                       mb_[mbi], coef_.data() + (size_t)mbi * kCoefStride);
 }
 
-void CpuH264Encoder::decide_deblock() {
-    deblock_now_ = cfg_.deblock == 1 || (cfg_.h264_deblock_auto() && db_prev_on_);
-}
+void CpuH264Encoder::decide_deblock() { deblock_now_ = db_lag_.decide((long long)enc_seq_, common_.cur_idr()); }
 
 void CpuH264Encoder::update_deblock_decision() {
     db_counts_ = DbAutoCounts{};
-    if (common_.cur_idr()) return;  // an IDR picture keeps the last P decision
     const Geometry g = geom_of(common_, cw_, ch_);
-    for (int i = 0; i < g.mb_w * g.mb_h; ++i) db_auto_count(mb_.data(), g.mb_w, i, db_counts_);
-    if (cfg_.h264_deblock_auto()) db_prev_on_ = db_auto_decide(db_counts_, g.mb_w * g.mb_h, db_prev_on_);
+    if (!common_.cur_idr())  // an IDR picture's record is invalid: its lag picture keeps the decision
+        for (int i = 0; i < g.mb_w * g.mb_h; ++i) db_auto_count(mb_.data(), g.mb_w, i, db_counts_);
+    db_lag_.record((long long)enc_seq_, common_.cur_idr(), db_counts_, g.mb_w * g.mb_h);
 }
 
 void CpuH264Encoder::entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& soff, std::vector<uint32_t>& slen) {
@@ -664,6 +663,7 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     }
     common_.begin_frame(force_idr || !have_ref_);
     cur_ ^= 1;
+    ++enc_seq_;
     // this frame's source becomes the previous source of the next one (temporal AQ classes)
     struct SaveSrc {
         std::vector<uint8_t>& d;

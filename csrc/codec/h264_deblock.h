@@ -185,6 +185,46 @@ MXHD bool db_auto_decide(const DbAutoCounts& c, int nmb, bool prev_on) {
     return co * (prev_on ? 3u : 2u) >= (uint64_t)c.moving && co * (prev_on ? 128u : 64u) >= (uint64_t)nmb && co > 0;
 }
 
+// The adaptive decision at a fixed lag (ADVICE r5 h264_encoder.cpp:696): picture n is filtered
+// according to the classes of picture n - kDbLag, the newest picture whose records the host holds
+// when picture n is prepared at any pipeline depth (<= 4 frames in flight), so the GPU encoder
+// decides the same at depth 1 and 4 and the CPU oracle matches it frame for frame (the decision
+// used to come from whichever picture had been collected last).  An IDR picture, or a lag picture
+// that was an IDR, keeps the last decision.  mode: 0 off, 1 on, 2 adaptive.
+constexpr int kDbLag = 4;
+class DbLagDecision {
+   public:
+    explicit DbLagDecision(int mode = 0) : mode_(mode) {}
+    void reset(int mode) { *this = DbLagDecision(mode); }
+    // picture `fidx`'s filter, when it is prepared (in picture order)
+    bool decide(long long fidx, bool idr) {
+        if (mode_ != 2) return on_ = mode_ == 1;
+        const Rec& r = ring_[(size_t)(fidx % kDbLag + kDbLag) % kDbLag];
+        if (!idr && r.valid && r.fidx == fidx - kDbLag) on_ = db_auto_decide(r.c, r.nmb, on_);
+        return on_;
+    }
+    bool on() const { return on_; }
+    // picture `fidx`'s class counts, once it is coded
+    void record(long long fidx, bool idr, const DbAutoCounts& c, int nmb) {
+        Rec& r = ring_[(size_t)(fidx % kDbLag + kDbLag) % kDbLag];
+        r.fidx = fidx;
+        r.nmb = nmb;
+        r.c = c;
+        r.valid = !idr && mode_ == 2;
+    }
+
+   private:
+    struct Rec {
+        long long fidx = -1;
+        int nmb = 0;
+        bool valid = false;
+        DbAutoCounts c;
+    };
+    int mode_;
+    bool on_ = false;
+    Rec ring_[kDbLag];
+};
+
 // QP_Y of every macroblock as a decoder sees it: the MB's own QP where it carries mb_qp_delta,
 // else the predictor (the last such MB's QP in decoding order within the slice, the slice QP at
 // its start).  I slices code every MB at the slice QP.

@@ -220,7 +220,7 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
                             int mby, int lane) {
     uint8_t* Y = fs->rec_y;
     const int pitch = g.pitch, mb_w = g.mb_w;
-    const uint32_t epoch = (uint32_t)fs->db_epoch & 0xfffffu;
+    const uint32_t epoch = (uint32_t)fs->db_epoch;  // full 32-bit tag above the 32 payload bits
     const bool band_first = band_row == 0, band_last = band_row == kDbRows - 1 || mby == g.mb_h - 1;
     const bool pic_last = mby == g.mb_h - 1;
     const bool act = lane < 16;
@@ -389,7 +389,7 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
                               int mby, int lane) {
     uint8_t* UV = fs->rec_uv;
     const int pitch = g.pitch, mb_w = g.mb_w;
-    const uint32_t epoch = (uint32_t)fs->db_epoch & 0xfffffu;
+    const uint32_t epoch = (uint32_t)fs->db_epoch;  // full 32-bit tag above the 32 payload bits
     const bool band_first = band_row == 0, band_last = band_row == kDbRows - 1 || mby == g.mb_h - 1;
     const bool pic_last = mby == g.mb_h - 1;
     const bool act = lane < 16;

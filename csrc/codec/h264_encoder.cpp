@@ -303,6 +303,7 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     if (cfg.pipeline_depth < 1 || cfg.pipeline_depth > kMaxInFlight)
         throw std::invalid_argument("pipeline_depth must be 1 to 4");
     depth_ = cfg.pipeline_depth;
+    db_lag_.reset(cfg_.h264_deblock_mode());
     geom_.width = cfg.width;
     geom_.height = cfg.height;
     geom_.mb_w = common_.mb_w();
@@ -546,9 +547,8 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.me_coarse = cfg_.me_coarse;
     f.intra4x4 = cfg_.intra4x4;
     f.subpel = cfg_.subpel;
-    sl.deblock = deblock_on();
     f.deblock_off = sl.deblock ? 0 : 1;
-    if (++db_epoch_ > 0xfffffu) db_epoch_ = 1;  // 20-bit tag, never 0
+    if (++db_epoch_ == 0) db_epoch_ = 1;  // 32-bit tag (bits 32..63 of the hand-off words), never 0
     f.db_epoch = (int32_t)db_epoch_;
     f.pic_init_qp = common_.pic_init_qp();
     f.chroma_qp_offset = cfg_.chroma_qp_offset;
@@ -577,6 +577,7 @@ int GpuH264Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     if (!inflight_.empty()) throw std::logic_error("GpuH264Encoder: probe with frames in flight");
     prep_slot_ = 0;
     FrameSlot& sl = slots_[0];
+    sl.deblock = cfg_.deblock == 1;
     fill_state(sl, true, qp, cur_ ^ 1, cur_);
     sl.fs_host->frame_num = 0;
     sl.fs_host->idr_pic_id = 0;
@@ -605,6 +606,8 @@ bool GpuH264Encoder::prepare(bool force_idr) {
     sl.qp = common_.cur_qp();
     const int ref = cur_;
     cur_ ^= 1;
+    sl.fidx = seq_;
+    sl.deblock = db_lag_.decide((long long)seq_, idr);
     fill_state(sl, idr, sl.qp, ref, cur_);
     return idr;
 }
@@ -692,9 +695,9 @@ const std::vector<uint8_t>& GpuH264Encoder::collect() {
     stats_.db_coherent = (int)hdr.db_coherent;
     stats_.db_changed = (int)hdr.db_changed;
     stats_.db_moving = (int)hdr.db_moving;
-    if (cfg_.h264_deblock_auto() && !sl.idr)  // the next picture's filter, from this one's classes
-        db_prev_on_ = db_auto_decide(DbAutoCounts{hdr.db_coherent, hdr.db_changed, hdr.db_moving},
-                                     geom_.mb_w * geom_.mb_h, db_prev_on_);
+    // picture fidx + kDbLag's filter, from this one's classes
+    db_lag_.record((long long)sl.fidx, sl.idr, DbAutoCounts{hdr.db_coherent, hdr.db_changed, hdr.db_moving},
+                   geom_.mb_w * geom_.mb_h);
     common_.end_frame((int)au_.size(), sl.idr);
     return au_;
 }

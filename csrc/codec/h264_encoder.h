@@ -71,6 +71,7 @@ struct EncoderConfig {
     }
     bool h264_deblock() const { return deblock > 0; }  // the filter kernels run (on, or adaptive)
     bool h264_deblock_auto() const { return deblock == 2; }
+    int h264_deblock_mode() const { return deblock == 1 ? 1 : (deblock == 2 ? 2 : 0); }  // DbLagDecision mode
     bool hevc_deblock() const { return deblock != 0; }
     // HEVC's default is adaptive: deblocking costs the still desktop 0.3 dB (its text regions
     // 4.5 dB) and gains 0.2 dB on motion content at 4K 18 Mbps (profiles/r05_hevc/NOTES.md)
@@ -289,6 +290,7 @@ class GpuH264Encoder final : public VideoEncoder {
         bool idr = false;
         bool deblock = false;  // the picture's in-loop filter (decided when it is prepared)
         int qp = 0;
+        uint64_t fidx = 0;     // picture number (seq_ when prepared)
     };
     void alloc_slot(FrameSlot& sl);
     void free_slot(FrameSlot& sl);
@@ -347,10 +349,9 @@ class GpuH264Encoder final : public VideoEncoder {
     int cur_ = 0;  // index of the frame being reconstructed
     bool have_ref_ = false;
     uint32_t db_epoch_ = 0;
-    // adaptive filter: the next picture's decision, from the last collected P picture's classes
-    // (OutHeader::db_*); a picture's filter is fixed when it is prepared (FrameSlot::deblock)
-    bool db_prev_on_ = false;
-    bool deblock_on() const { return cfg_.deblock == 1 || (cfg_.h264_deblock_auto() && db_prev_on_); }
+    // adaptive filter: picture n's decision from the classes of picture n - kDbLag (OutHeader::db_*,
+    // recorded when it is collected); a picture's filter is fixed when it is prepared (FrameSlot::deblock)
+    DbLagDecision db_lag_;
     int mask_mb_[4] = {0, 0, 0, 0};  // quality-report mask in macroblocks (x0, y0, x1, y1)
     int64_t masked_pixels_ = 0;
     std::vector<uint8_t> au_;
@@ -377,11 +378,13 @@ class CpuH264Encoder {
     void encode_inter(const uint8_t* y, const uint8_t* uv, int pitch);
     void entropy(std::vector<uint8_t>& payload, std::vector<uint32_t>& slice_off, std::vector<uint32_t>& slice_len);
     int frame_qp_() const { return qp_override_ >= 0 ? qp_override_ : common_.cur_qp(); }
-    // the picture's in-loop filter (EncoderConfig::deblock; adaptive: the decision db_auto_decide
-    // took from the previous P picture's classes, as the GPU encoder's host side) / the update after it
+    // the picture's in-loop filter (EncoderConfig::deblock; adaptive: DbLagDecision on the classes of
+    // picture n - kDbLag, as the GPU encoder's host side) / the record of this picture's classes
     void decide_deblock();
     void update_deblock_decision();
-    bool deblock_now_ = false, db_prev_on_ = false;
+    bool deblock_now_ = false;
+    DbLagDecision db_lag_;
+    uint64_t enc_seq_ = 0;  // pictures encoded (the GPU encoder's seq_)
     DbAutoCounts db_counts_;
     int qp_override_ = -1;  // rate-control probe of the first picture
 

@@ -270,7 +270,7 @@ struct Vp8FrameState {
     int32_t hp_pitch;
     int32_t key;
     int32_t qindex;
-    int32_t epoch;          // nonzero, new every frame: tag of the wavefront hand-off words (20 bits)
+    int32_t epoch;          // nonzero, new every frame: tag of the wavefront hand-off words (32 bits)
     int32_t segmented;      // inter frame with segment quantisers (temporal classes)
     int32_t aq;
     int32_t q[kNumSegs][6];   // per segment: Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps

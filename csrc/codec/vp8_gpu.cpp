@@ -199,7 +199,7 @@ void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
     f.key = key ? 1 : 0;
     s.qindex = qindex_for_qp(qp);
     f.qindex = s.qindex;
-    if (++epoch_ > 0xfffffu) epoch_ = 1;  // 20-bit tag, never 0
+    if (++epoch_ == 0) epoch_ = 1;  // 32-bit tag (bits 32..63 of the hand-off words), never 0
     f.epoch = (int32_t)epoch_;
     // inter frames with temporal classes: segment quantisers; key frames: the frame quantiser
     s.segmented = !key && cfg_.aq >= 3;

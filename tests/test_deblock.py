@@ -121,11 +121,12 @@ def _pan_frames(w, h, n, step=3, still=False):
 
 
 def test_adaptive_filter_follows_motion_and_decodes(native):
-    """deblock=2: a picture's filter follows the previous P picture's classes -- the pan's pictures
-    after its first P picture are filtered, a forced IDR keeps the decision, a still scene stays
-    unfiltered; the per-picture idc decodes exactly."""
+    """deblock=2: picture n's filter follows the classes of picture n - 4 (h264_deblock.h kDbLag: the
+    same at every pipeline depth) -- the pan is filtered from the fourth picture after its first P
+    picture, a forced IDR keeps the decision, a still scene stays unfiltered; the per-picture idc
+    decodes exactly."""
     w, h = 192, 96
-    pan = [(y, uv, t == 4) for t, (y, uv) in enumerate(_pan_frames(w, h, 6))]
+    pan = [(y, uv, t == 6) for t, (y, uv) in enumerate(_pan_frames(w, h, 10))]
     cfg = native.EncoderConfig()
     cfg.width, cfg.height = w, h
     cfg.bitrate_kbps, cfg.qp, cfg.search_range, cfg.deblock = 0, 34, 8, 2
@@ -136,8 +137,8 @@ def test_adaptive_filter_follows_motion_and_decodes(native):
         ry, ruv = enc.recon()
         recons.append((ry.copy(), ruv.copy()))
         flags.append((enc.stats.deblocked, enc.stats.db_coherent))
-    assert flags[0][0] == 0 and flags[1][0] == 0  # nothing decided before the first P picture
-    assert all(d == 1 for d, _ in flags[2:]), flags  # the pan's later pictures, and the forced IDR at 4
+    assert all(d == 0 for d, _ in flags[:5]), flags  # nothing decided before picture 1 + kDbLag
+    assert all(d == 1 for d, _ in flags[5:]), flags  # the pan's later pictures, and the forced IDR at 6
     assert all(c * 8 >= (w // 16) * (h // 16) for _, c in flags[1:4]), flags  # the P pictures' classes
     _check(stream, recons)
 

@@ -589,16 +589,21 @@ def test_device_clock_frame_times(gpu, depth):
         assert 0.0 < s.stats.encode_ms <= r.gpu_ms + 1e-6
 
 
-@pytest.mark.parametrize("depth", [1, 3])
-def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
-    """deblock=2: the class counts k_scan_rows reports and the host's decision for the next picture
-    equal the CPU encoder's, so the streams match bit for bit through a pan, a forced IDR and a
-    still stretch (depth 3: the slots' counters and the shared decision)."""
+def _adaptive_frames():
     from .test_deblock import _pan_frames
 
     w, h = 192, 96
-    frames = [(y, uv, t == 4) for t, (y, uv) in enumerate(_pan_frames(w, h, 6))]
-    frames += [(y, uv, False) for y, uv in _pan_frames(w, h, 5, still=True)]
+    frames = [(y, uv, t == 6) for t, (y, uv) in enumerate(_pan_frames(w, h, 10))]
+    frames += [(y, uv, False) for y, uv in _pan_frames(w, h, 6, still=True)]
+    return w, h, frames
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
+    """deblock=2: the class counts k_scan_rows reports and the host's fixed-lag decision (picture n
+    from picture n - kDbLag) equal the CPU encoder's, so the streams match bit for bit through a
+    pan, a forced IDR and a still stretch (synchronous encode() at depth 1 and 3)."""
+    w, h, frames = _adaptive_frames()
     cfg = gpu.EncoderConfig()
     cfg.width, cfg.height = w, h
     cfg.bitrate_kbps, cfg.qp, cfg.search_range, cfg.deblock = 0, 34, 8, 2
@@ -619,4 +624,39 @@ def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
             (cst.deblocked, cst.db_coherent, cst.db_changed, cst.db_moving), t
         assert np.array_equal(genc.recon()[0], cenc.recon()[0]), t
         flags.append(genc.stats.deblocked)
-    assert flags[2:6] == [1, 1, 1, 1] and flags[-1] == 0, flags
+    assert flags[:5] == [0] * 5 and flags[5:10] == [1] * 5 and flags[-1] == 0, flags
+
+
+@pytest.mark.parametrize("depth", [3, 4])
+def test_gpu_adaptive_deblock_in_flight_vs_cpu(gpu, depth):
+    """ADVICE r5 h264_encoder.cpp:696: with `depth` frames really in flight (submit ahead, collect
+    behind) the adaptive decision of every picture is still the CPU oracle's -- it comes from
+    picture n - kDbLag, whose classes the host always holds when picture n is prepared."""
+    w, h, frames = _adaptive_frames()
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height = w, h
+    cfg.bitrate_kbps, cfg.qp, cfg.search_range, cfg.deblock = 0, 34, 8, 2
+    cfg.pipeline_depth = depth
+    genc = gpu.GpuH264Encoder(cfg, _stream())
+    cenc = gpu.CpuH264Encoder(cfg)
+    ch = genc.coded_height
+    want, flags_c = [], []
+    for y, uv, idr in frames:
+        want.append(cenc.encode(y, uv, idr))
+        flags_c.append(cenc.stats.deblocked)
+    keep, got, flags = [], [], []
+    for t, (y, uv, idr) in enumerate(frames):
+        if len(keep) - len(got) == depth:  # pipeline full: collect the oldest frame first
+            got.append(genc.collect())
+            flags.append(genc.stats.deblocked)
+        dy = pitched(y, genc.pitch, ch)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
+        torch.cuda.synchronize()
+        keep.append((dy, duv))
+        genc.submit(dy.data_ptr(), duv.data_ptr(), idr)
+    while len(got) < len(frames):
+        got.append(genc.collect())
+        flags.append(genc.stats.deblocked)
+    for t, (g, c) in enumerate(zip(got, want)):
+        assert g == c, f"frame {t}: GPU bitstream (depth {depth}, in flight) differs from CPU encoder"
+    assert flags == flags_c and 1 in flags and flags[-1] == 0, (flags, flags_c)
