@@ -81,9 +81,10 @@ def quality_probe(s, W: int, H: int, content: int, noise: int, n: int = 30) -> d
         r = s.step(False)
         sy, su = s.nv12()
         ry, ru = s.recon()
-        if content == 1:
+        if content in (1, 2):
             f = r.frame_id
-            px, py = (3 * f) % W, f % H
+            # the renderer's pan (pix pan_of / pan_q4), to the nearest sample for the region map
+            px, py = ((3 * f) % W, f % H) if content == 1 else (((10 * f) % (4 * W) + 2) // 4, ((3 * f) % (4 * H) + 2) // 4)
             cls = np.roll(base, (-py, -px), axis=(0, 1))
             vx0, vy0 = int(W * 0.60), int(H * 0.56)
             cls[vy0:vy0 + int(H * 0.36), vx0:vx0 + int(W * 0.34)] = 7
@@ -336,9 +337,11 @@ def main() -> None:
                     help="1: even-offset grid + integer neighbours, 0: exhaustive search (encoder default)")
     ap.add_argument("--intra4x4", type=int, default=None, help="0: intra MBs Intra16x16 only")
     ap.add_argument("--noise", type=int, default=1, help="animated white-noise panel (incompressible content)")
-    ap.add_argument("--content", default="desktop", choices=["desktop", "motion"],
-                    help="synthetic source: the desktop, or motion content (the whole desktop pans 3 px / frame "
-                         "under a screen-fixed video-like panel; no noise panel)")
+    ap.add_argument("--content", default="desktop", choices=["desktop", "motion", "subpel"],
+                    help="synthetic source: the desktop, motion content (the whole desktop pans 3 px / frame "
+                         "under a screen-fixed video-like panel; no noise panel), or subpel (a fractional pan of "
+                         "2.5 px right / 0.75 px down per frame, bilinearly resampled, under a zooming video panel: "
+                         "quarter-sample motion, the interpolation filters and the deblocking decision exercised)")
     ap.add_argument("--quality-probe", type=int, default=30,
                     help="untimed frames after the run with per-region / chroma PSNR read back (0: off)")
     ap.add_argument("--aq", type=int, default=None,
@@ -400,7 +403,7 @@ def main() -> None:
         args.depth = min(args.depth or 4, 4)  # the VP8 encoder keeps at most four frames in flight
     if args.depth is None:
         args.depth = 3
-    content = 1 if args.content == "motion" else 0
+    content = {"desktop": 0, "motion": 1, "subpel": 2}[args.content]
     if content:
         args.noise = 0  # the motion content has a video panel instead of the noise panel
 

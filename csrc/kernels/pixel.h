@@ -24,7 +24,9 @@ struct SynthParams {
     // 0: the desktop (static windows + animated elements); 1: motion content -- the whole desktop
     // pans (3 px right, 1 px down per frame at 60 fps, wrapping) under a screen-fixed video-like
     // panel of smooth, colourful, non-rigidly moving texture (kVideo* rectangle), as games and
-    // video playback look to the encoder; the barcode stays put
+    // video playback look to the encoder; the barcode stays put.  2: sub-sample motion -- the pan
+    // moves 2.5 px right and 0.75 px down per frame (bilinear resampling of the desktop) and the
+    // video panel's texture zooms (a scaled video), so the motion is fractional
     int content = 0;
 };
 // video panel of the motion content, fractions of the wall (screen coordinates)

@@ -149,6 +149,14 @@ __device__ __forceinline__ void pan_of(const SynthParams& p, int* px, int* py) {
     *px = (3 * f) % p.wall_w;
     *py = f % p.wall_h;
 }
+// sub-sample pan of frame time t (content 2), in quarter samples: 2.5 px / frame right, 0.75 px /
+// frame down at 60 fps, so consecutive frames differ by fractional displacements (qpel motion
+// search, the six-tap / eight-tap interpolation and the deblocking decision all get exercised)
+__device__ __forceinline__ void pan_q4(const SynthParams& p, int* qx, int* qy) {
+    const int f = (int)(p.t * 60.f + 0.5f);
+    *qx = (10 * f) % (4 * p.wall_w);
+    *qy = (3 * f) % (4 * p.wall_h);
+}
 // smooth value noise: bilinear, smoothstep-weighted interpolation of a hashed integer lattice
 __device__ __forceinline__ float vnoise(float x, float y, uint32_t seed) {
     const float fx = floorf(x), fy = floorf(y);
@@ -165,7 +173,7 @@ __device__ __forceinline__ float vnoise(float x, float y, uint32_t seed) {
 // video-like texture at panel coordinates (u, v): three octaves of value noise drifting at
 // different speeds (so the motion is not one translation), mapped through phase-shifted colour
 // waves that also cycle slowly
-__device__ uint32_t video_px(int u, int v, float t) {
+__device__ uint32_t video_pxf(float u, float v, float t) {
     const float x = u * (1.f / 96.f), y = v * (1.f / 96.f);
     const float n = 0.55f * vnoise(x + 0.35f * t, y + 0.12f * t, 11u) +
                     0.30f * vnoise(2.1f * x - 0.6f * t, 2.1f * y + 0.25f * t, 23u) +
@@ -176,6 +184,7 @@ __device__ uint32_t video_px(int u, int v, float t) {
     const int b = (int)(128.f + 100.f * __sinf(0.8f * ph + 4.2f - 0.3f * t));
     return bgrx(r, g, b);
 }
+__device__ __forceinline__ uint32_t video_px(int u, int v, float t) { return video_pxf((float)u, (float)v, t); }
 
 __device__ uint32_t desktop_px(int gx, int gy, const SynthParams& p, const FrameConsts& fc) {
     const int W = p.wall_w, H = p.wall_h;
@@ -319,6 +328,43 @@ __device__ __forceinline__ uint32_t motion_px(int gx, int gy, const SynthParams&
     return desktop_px(dx, dy, p, fc);
 }
 
+// Sub-sample motion content (content 2): the desktop pans by a fractional displacement (pan_q4),
+// sampled bilinearly from the four covering desktop pixels (quarter-sample weights, per channel),
+// and the video panel's texture zooms continuously (scale 0.8 .. 1.1 over ~12 s) -- a scaled video.
+__device__ __forceinline__ uint32_t desk_at(int dx, int dy, const SynthParams& p, const FrameConsts& fc,
+                                            const uint8_t* __restrict__ bg, const DynBoxes& boxes) {
+    dx -= dx >= p.wall_w ? p.wall_w : 0;
+    dy -= dy >= p.wall_h ? p.wall_h : 0;
+    if (bg != nullptr && p.origin_x == 0 && p.origin_y == 0 && !in_dyn(boxes, dx, 1, dy))
+        return *reinterpret_cast<const uint32_t*>(bg + (size_t)dy * p.pitch + 4 * dx);
+    return desktop_px(dx, dy, p, fc);
+}
+__device__ __forceinline__ uint32_t subpel_px(int gx, int gy, const SynthParams& p, const FrameConsts& fc,
+                                              const uint8_t* __restrict__ bg, int qx, int qy, int vx0, int vy0,
+                                              int vx1, int vy1, const DynBoxes& boxes) {
+    if (in_barcode(gx, gy)) return barcode_px(gx, gy, p);
+    if (gx >= vx0 && gx < vx1 && gy >= vy0 && gy < vy1) {
+        const float s = 0.95f + 0.15f * __sinf(0.5f * p.t);
+        const float cu = 0.5f * (vx1 - vx0), cv = 0.5f * (vy1 - vy0);
+        return video_pxf(cu + ((float)(gx - vx0) - cu) * s, cv + ((float)(gy - vy0) - cv) * s, p.t);
+    }
+    const int ix = gx + (qx >> 2), iy = gy + (qy >> 2), fx = qx & 3, fy = qy & 3;
+    const uint32_t a = desk_at(ix, iy, p, fc, bg, boxes);
+    if ((fx | fy) == 0) return a;
+    const uint32_t b = desk_at(ix + 1, iy, p, fc, bg, boxes), c = desk_at(ix, iy + 1, p, fc, bg, boxes),
+                   d = desk_at(ix + 1, iy + 1, p, fc, bg, boxes);
+    const int wa = (4 - fx) * (4 - fy), wb = fx * (4 - fy), wc = (4 - fx) * fy, wd = fx * fy;
+    uint32_t out = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const int sh = 8 * ch;
+        const int v = (wa * (int)((a >> sh) & 0xff) + wb * (int)((b >> sh) & 0xff) + wc * (int)((c >> sh) & 0xff) +
+                       wd * (int)((d >> sh) & 0xff) + 8) >> 4;
+        out |= (uint32_t)v << sh;
+    }
+    return out;
+}
+
 // bg: the session's static-layer cache (same size / pitch / origin), or nullptr.
 __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const SynthParams& p,
                                            const uint8_t* __restrict__ bg) {
@@ -329,14 +375,19 @@ __device__ __forceinline__ void synth_body(uint8_t* __restrict__ out, const Synt
     uint32_t v[4];
     const int gx = p.origin_x + x4, gy = p.origin_y + y;
     const FrameConsts fc = frame_consts(p);
-    if (p.content == 1) {
+    if (p.content == 1 || p.content == 2) {
         int px, py, vx0, vy0, vx1, vy1;
-        pan_of(p, &px, &py);
+        if (p.content == 1)
+            pan_of(p, &px, &py);
+        else
+            pan_q4(p, &px, &py);
         video_rect(p, &vx0, &vy0, &vx1, &vy1);
         const DynBoxes boxes = dyn_boxes(p, fc.wx, fc.wy, fc.mw, fc.mh);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            v[k] = (x4 + k < p.width) ? motion_px(gx + k, gy, p, fc, bg, px, py, vx0, vy0, vx1, vy1, boxes) : 0u;
+            v[k] = (x4 + k >= p.width) ? 0u
+                   : p.content == 1 ? motion_px(gx + k, gy, p, fc, bg, px, py, vx0, vy0, vx1, vy1, boxes)
+                                    : subpel_px(gx + k, gy, p, fc, bg, px, py, vx0, vy0, vx1, vy1, boxes);
         uint32_t* row = reinterpret_cast<uint32_t*>(out + (size_t)y * p.pitch);
         if (x4 + 4 <= p.width)
             *reinterpret_cast<uint4*>(row + x4) = make_uint4(v[0], v[1], v[2], v[3]);

@@ -55,7 +55,8 @@ struct SessionConfig {
     int out_height = 0;
     int fps = 60;
     int noise = 1;          // synthetic animated-noise panel
-    int content = 0;        // synthetic source: 0 desktop, 1 motion content (pan + video panel, pix::SynthParams)
+    int content = 0;        // synthetic source: 0 desktop, 1 motion content (pan + video panel, pix::SynthParams),
+                            // 2 sub-sample motion (2.5 / 0.75 px per frame pan, zooming video panel)
     int pool_slots = 5;     // > encoder pipeline depth (<= kMaxDepth)
     int use_graph = 0;      // replay the per-frame chain as a hipGraph (measured slower than eager
                             // launches on ROCm 7.2 for this chain: profiles/r01_graph)

@@ -95,3 +95,38 @@ def test_4k_bit_exact_multi_tile_scan(gpu):
 def test_8k_bit_exact(gpu):
     aus, recons, genc = _encode_both(gpu, 7680, 4320, 2, 60000, search_range=4)
     assert len(aus[1]) > 0 and genc.coded_height == 4320
+
+
+def _hevc_encode_both(gpu, w, h, frames, kbps):
+    """The HEVC encoder at its defaults (CTB 32 quadtree, 4x4 luma TUs, SAO, adaptive deblocking,
+    aq 6, half-row I slices, cost-balanced P slices) on the HIP desktop: GPU == CPU oracle."""
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height, cfg.fps = w, h, 60
+    cfg.bitrate_kbps = kbps
+    genc = gpu.GpuHevcEncoder(cfg, _stream())
+    cenc = gpu.CpuHevcEncoder(cfg)
+    ch = genc.coded_height
+    aus = []
+    for t in range(frames):
+        y, uv = desktop_nv12(gpu, w, h, t)
+        dy = pitched(y, genc.pitch, ch)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
+        torch.cuda.synchronize()
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        assert gau == cau, f"HEVC {w}x{h} frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
+        assert tuple(genc.stats.sse) == tuple(cenc.stats.sse), t
+        aus.append(gau)
+    return aus, genc
+
+
+def test_hevc_4k_bit_exact(gpu):
+    # BASELINE config 3 (4K60 HEVC): IDR with two I slices per CTB row, then P pictures
+    aus, genc = _hevc_encode_both(gpu, 3840, 2160, 3, 18000)
+    assert len(aus[0]) > len(aus[1]) > 0
+
+
+def test_hevc_8k_bit_exact(gpu):
+    # the wall's encode rank (BASELINE config 5: 2x2 tiled 8K60, HEVC level 6.1)
+    aus, genc = _hevc_encode_both(gpu, 7680, 4320, 2, 60000)
+    assert genc.coded_height == 4320 and len(aus[1]) > 0
