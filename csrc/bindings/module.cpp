@@ -527,6 +527,9 @@ PYBIND11_MODULE(_native, m) {
 
     // ---------------------------------------------------------------- pixel kernels
     // roctx ranges from Python (packetize / send stages of the streaming pipeline)
+    m.def("h264_deblock_row_stamps", &h264::deblock_row_stamps, py::arg("mb_h"),
+          "device wall-clock (start, end) of each k_deblock row wave of the last picture: luma rows, then chroma");
+    m.def("device_clock_khz", &device_clock_khz);
     m.def("trace_push", [](const std::string& name) { roctxRangePushA(name.c_str()); });
     m.def("trace_pop", []() { roctxRangePop(); });
     m.def("trace_mark", [](const std::string& name) { roctxMarkA(name.c_str()); });

@@ -9,22 +9,32 @@
 //    16-byte record; per row, the QP of the last macroblock carrying mb_qp_delta (so a row can start
 //    its running QP_Y without walking the picture).
 //  * k_deblock: one wave per (MB row, plane) -- luma and chroma are independent -- walking its row
-//    left to right; 8 rows x 2 planes = 16 waves per workgroup.  A lane owns one sample line: the
-//    vertical edges run on lines in registers, the horizontal edges on columns after a transpose
-//    through a per-wave LDS tile.  A row hands each finished macroblock's bottom lines (luma rows
-//    12..15, chroma rows 6..7: the p samples of the next row's top edge) down through an LDS ring
-//    with a progress counter (the row below waits only where its own top edge is filtered); the
-//    band's last row hands them to the next workgroup (another XCD, another L2) through global
-//    memory as epoch-tagged 64-bit agent-scope atomic words -- 32 sample bits and the frame's tag
-//    -- which the consumer polls directly: no agent-scope release fence per macroblock (on gfx950
-//    a write-back of the XCD's whole L2, which set the pace of every row below the band).
-//    Every sample byte has exactly one writer: rows 13..15 of a macroblock whose lower neighbour
-//    filters its top edge are written by the row below, else by their own row.
+//    left to right; R = 4 rows per workgroup (one row wave per SIMD; the LDS is padded so no other
+//    deblocking workgroup shares the CU) or 8 (MXDESK_DB_ROWS).  All edges of one direction of a
+//    macroblock are filtered at once, one lane per (line, edge), and settled in 1-3 passes (the
+//    luma engine's comment has the dependency argument); vertical edges run on row dwords in
+//    registers (quad DPP moves carry the neighbouring edge's samples), horizontal edges on bytes
+//    read back transposed from a per-wave LDS tile.  The step's control is scalar: the band's
+//    boundary-strength records sit in VGPRs (lane j: MB xb + j) and are read with v_readlane, the
+//    alpha / beta / tC0 and QP_C tables likewise (no memory access on the serial chain).  A row
+//    hands each finished macroblock's bottom lines (luma rows 12..15, chroma rows 6..7: the p
+//    samples of the next row's top edge) down through an LDS ring with a progress counter (the row
+//    below waits only where its own top edge is filtered); the band's last row hands them to the
+//    next workgroup (another XCD, another L2) through global memory as epoch-tagged 64-bit
+//    agent-scope atomic words -- 32 sample bits and the frame's tag -- which the consumer polls
+//    directly: no agent-scope release fence per macroblock (on gfx950 a write-back of the XCD's
+//    whole L2).  Every sample byte has exactly one writer: rows 13..15 of a macroblock whose lower
+//    neighbour filters its top edge are written by the row below, else by their own row.
 //    Macroblocks with every bS == 0 (static desktop, skips with equal vectors) cost a record read
-//    and a counter update, so P pictures pay for the changing areas only.
+//    and a counter update, so P pictures pay for the changing areas only.  1080p pan (every MB
+//    filtered): 332 -> ~220 us per picture against the earlier one-edge-at-a-time engine
+//    (profiles/r06_deblock/NOTES.md).
 //  * k_db_sse: the distortion of the filtered picture (one partial per MB row and channel), which
 //    replaces the analysis kernels' unfiltered figures in the frame statistics.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <vector>
 
 #include "../common/hip_check.h"
 #include "h264_deblock.h"
@@ -36,7 +46,10 @@ namespace h264 {
 
 namespace {
 
-constexpr int kDbRows = 8;   // MB rows (waves per plane) per workgroup
+// MB rows (waves per plane) per workgroup: 8 (two row waves per SIMD) or 4 (one; the workgroup's
+// LDS is padded past half the CU's so no other deblocking workgroup shares its SIMDs);
+// MXDESK_DB_ROWS picks one at run time for measurement
+constexpr int kDbRowsDefault = 4;
 constexpr int kDbRing = 16;  // LDS hand-off slots per row
 constexpr int kDbMaxW = 512; // MBs per row (the encoder's limit): the band's records live in LDS
 constexpr int kDbPf = 8;     // macroblocks of sample lines prefetched ahead (one batch)
@@ -88,23 +101,27 @@ __global__ __launch_bounds__(256) void k_db_prep(Geometry g, const FrameState* _
     }
 }
 
+template <int R>
 struct DbShared {
-    uint8_t lring[kDbRows][kDbRing][4][16];  // luma rows 12..15 of a finished MB
-    uint8_t cring[kDbRows][kDbRing][2][16];  // chroma rows 6..7 (interleaved U/V)
-    uint8_t ringq[2][kDbRows][kDbRing];      // the MB's QP_Y (per plane's own running value)
-    int prog[2][kDbRows];                    // ring entries published (MB count)
-    int cons[2][kDbRows];                    // MB steps finished by the row (for the row above's ring reuse)
-    uint8_t tile[2 * kDbRows][20][16];       // per-wave transposition tile
-    uint4 recs[kDbRows + 1][kDbMaxW];        // the band's records + the next row's (bS, QP)
-    uint4 stage[2 * kDbRows][kDbPf][16];     // per-wave prefetched sample lines (lane-private slots)
+    uint8_t lring[R][kDbRing][4][16];  // luma rows 12..15 of a finished MB
+    uint8_t cring[R][kDbRing][2][16];  // chroma rows 6..7 (interleaved U/V)
+    uint8_t ringq[2][R][kDbRing];      // the MB's QP_Y (per plane's own running value)
+    int prog[2][R];                    // ring entries published (MB count)
+    int cons[2][R];                    // MB steps finished by the row (for the row above's ring reuse)
+    uint8_t tile[2 * R][20][16];       // per-wave transposition tile
+    uint4 recs[R + 1][kDbMaxW];        // the band's records + the next row's (bS, QP)
+    uint4 stage[2 * R][kDbPf][16];     // per-wave prefetched sample lines (lane-private slots)
     uint32_t params[52];                     // alpha | beta << 8 | packed tC0 << 13, by indexA
     uint8_t cqp[52];                         // QP_C of a clipped qP_I (Table 8-15)
+    uint8_t pad[R == 4 ? 20480 : 4];         // R 4: > 80 KiB, one deblocking workgroup per CU
 };
-__device__ __forceinline__ int lds_cqp(const DbShared& S, int qp, int offset) {
+template <int R>
+__device__ __forceinline__ int lds_cqp(const DbShared<R>& S, int qp, int offset) {
     const int q = qp + offset;
     return S.cqp[q < 0 ? 0 : (q > 51 ? 51 : q)];
 }
-__device__ __forceinline__ DbParams lds_params(const DbShared& S, int qpav) {
+template <int R>
+__device__ __forceinline__ DbParams lds_params(const DbShared<R>& S, int qpav) {
     const uint32_t w = S.params[qpav < 0 ? 0 : (qpav > 51 ? 51 : qpav)];
     DbParams d;
     d.alpha = (int)(w & 0xff);
@@ -135,6 +152,56 @@ __device__ __forceinline__ void lds_store(int* p, int v) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// publish an LDS progress value without draining: a wave's LDS operations are performed in issue
+// order, so a reader that sees the value sees the ring bytes written before it (the compiler fence
+// keeps the stores in that order)
+__device__ __forceinline__ void lds_publish(int* p, int v) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Filter parameters and chroma QP as scalar-memory tables (uniform index: s_load, no LDS round
+// trip on the row's serial chain)
+struct DbTabs {
+    uint32_t par[52];  // alpha | beta << 8 | packed tC0 << 13, by indexA
+    uint32_t cqp[52];  // QP_C of a clipped qP_I (Table 8-15)
+};
+constexpr DbTabs make_db_tabs() {
+    DbTabs t{};
+    for (int i = 0; i < 52; ++i) {
+        t.par[i] = (uint32_t)kDbAlpha[i] | ((uint32_t)kDbBeta[i] << 8) |
+                   (((uint32_t)kDbTc0[i][0] | ((uint32_t)kDbTc0[i][1] << 5) | ((uint32_t)kDbTc0[i][2] << 10)) << 13);
+        t.cqp[i] = (uint32_t)kChromaQp[i];
+    }
+    return t;
+}
+__constant__ DbTabs c_db_tabs = make_db_tabs();
+// The tables live in two VGPRs of every row wave (lane i: entry i), read with v_readlane: no
+// memory access on the chain (a scalar load would also drain the wave's pending LDS reads, which
+// share its lgkmcnt counter)
+struct DbLaneTabs {
+    uint32_t par, cqp;
+};
+__device__ __forceinline__ DbLaneTabs load_lane_tabs(int lane) {
+    const int i = lane < 52 ? lane : 51;
+    return DbLaneTabs{c_db_tabs.par[i], c_db_tabs.cqp[i]};
+}
+__device__ __forceinline__ DbParams spar(const DbLaneTabs& T, int qpav) {
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)T.par, qpav < 0 ? 0 : (qpav > 51 ? 51 : qpav));
+    DbParams d;
+    d.alpha = (int)(w & 0xff);
+    d.beta = (int)((w >> 8) & 31);
+    d.tc0 = w >> 13;
+    return d;
+}
+__device__ __forceinline__ int scqp(const DbLaneTabs& T, int qp, int offset) {
+    const int q = qp + offset;
+    return __builtin_amdgcn_readlane((int)T.cqp, q < 0 ? 0 : (q > 51 ? 51 : q));
+}
+__device__ __forceinline__ uint4 rd_lane(const uint4& v, int j) {
+    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)v.x, j), (uint32_t)__builtin_amdgcn_readlane((int)v.y, j),
+                      (uint32_t)__builtin_amdgcn_readlane((int)v.z, j), (uint32_t)__builtin_amdgcn_readlane((int)v.w, j));
+}
+
 // 16-byte global load / store through address-space-1 pointers of a native vector type (a generic
 // access -- or one through HIP's uint4 class, whose copy constructor takes a generic reference --
 // compiles to flat_*, which also counts on lgkmcnt and so stalls every later LDS wait)
@@ -214,355 +281,456 @@ __device__ __forceinline__ void put_tagged(uint64_t* p, uint32_t v, uint32_t epo
     __hip_atomic_store((gu64*)p, (uint64_t)v | ((uint64_t)epoch << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Diagnostics: device wall-clock (start, end) of the last picture's row waves, [plane][mby][2], and
+// the ticks each row wave spent waiting (ring slot free, row above's progress, band hand-off
+// words) (read by deblock_row_stamps(); a few stores per wave per picture)
+__device__ unsigned long long g_db_stamps[2][kMaxSlices][2];
+__device__ unsigned long long g_db_clk[2][kMaxSlices];  // shader-clock cycles of each row wave
+__device__ unsigned long long g_db_waits[2][kMaxSlices][3];
+__device__ unsigned long long g_db_phase[kMaxSlices][4];  // luma: ticks in step head, V, final, H
+
 // ---------------------------------------------------------------- luma row engine
+// Edge-parallel form.  8.7 orders a macroblock's luma edges (vertical 0..3, then horizontal
+// 0..3), but the data dependencies between consecutive edges of one direction are shallow: for
+// the normal filter (bS < 4, every internal edge) q1' depends on p1, p0, q0, q1, q2 only -- never
+// on p2 or p3, the two samples the previous edge may have written -- so an edge's outputs depend
+// on its left (upper) neighbour edge only through p2 = that edge's q1' (and, behind a bS-4 MB
+// edge, p1 = its q2').  All four edges of a direction are therefore computed at once, one lane
+// per (line, edge) -- 16 lines x 4 edges = the whole wave -- and corrected by re-evaluating each
+// edge with its neighbour's outputs: two passes settle every edge, a third one an edge 2 behind a
+// strong (bS 4) edge 0.  Layouts: vertical edges, lane 4r + e holds row r, columns 4e..4e+3 (one
+// dword); horizontal edges, lane 4c + e holds column c, rows 4e-4..4e+3 as bytes read from a
+// per-wave LDS tile.  Quad DPP moves carry the neighbour values.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xf, 0xf, false);
+}
+constexpr int kQuadShr1 = 0x90;   // lane e of a quad reads quad lane max(e - 1, 0)
+constexpr int kQuadShl1 = 0xF9;   // quad lane min(e + 1, 3)
+constexpr int kQuadBcast0 = 0x00; // quad lane 0
+constexpr int kQuadBcast3 = 0xFF; // quad lane 3
+struct Px8 {
+    int p3, p2, p1, p0, q0, q1, q2, q3;
+};
+__device__ __forceinline__ Px8 px8(uint32_t p, uint32_t q) {
+    return Px8{(int)(p & 0xff), (int)((p >> 8) & 0xff), (int)((p >> 16) & 0xff), (int)(p >> 24),
+               (int)(q & 0xff), (int)((q >> 8) & 0xff), (int)((q >> 16) & 0xff), (int)(q >> 24)};
+}
+__device__ __forceinline__ Px8 edge_eval(Px8 v, int bs, const DbParams& d) {
+    db_luma_line(v.p3, v.p2, v.p1, v.p0, v.q0, v.q1, v.q2, v.q3, bs, d);
+    return v;
+}
+// Settle the four edges of one direction (see above): `in` = the lane's samples before any edge
+// of the direction, `passes` 1..3.  Lane e >= 1 re-reads its p3 / p2 / p1 from edge e - 1's
+// q0' / q1' / q2' (quad lane e - 1) each pass.
+__device__ __forceinline__ Px8 settle_edges(const Px8& in, int bs, const DbParams& d, int e, int passes) {
+    Px8 o = edge_eval(in, bs, d);
+    for (int k = 1; k < passes; ++k) {
+        const uint32_t l = qperm<kQuadShr1>((uint32_t)o.q0 | ((uint32_t)o.q1 << 8) | ((uint32_t)o.q2 << 16));
+        Px8 v = in;
+        if (e >= 1) {
+            v.p3 = (int)(l & 0xff);
+            v.p2 = (int)((l >> 8) & 0xff);
+            v.p1 = (int)((l >> 16) & 0xff);
+        }
+        o = edge_eval(v, bs, d);
+    }
+    return o;
+}
+// passes to settle a direction: 1 with only edge 0 filtered; 2 when an internal edge is (or edge 1
+// must take up a strong edge 0's q2' as its p1); 3 when both (edge 2 behind edge 1's changed q1')
+__device__ __forceinline__ int edge_passes(bool internal, bool strong0) {
+    return 1 + ((internal || strong0) ? 1 : 0) + ((internal && strong0) ? 1 : 0);
+}
+__device__ __forceinline__ uint32_t pk4(int a, int b, int c, int d) {
+    return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
+}
+__device__ __forceinline__ DbParams sel_params(bool first, const DbParams& a, const DbParams& b) {
+    DbParams d;
+    d.alpha = first ? a.alpha : b.alpha;
+    d.beta = first ? a.beta : b.beta;
+    d.tc0 = first ? a.tc0 : b.tc0;
+    return d;
+}
+typedef __attribute__((address_space(1))) uint32_t GDbU32;
+__device__ __forceinline__ uint32_t gld4(const uint8_t* p) { return *(const GDbU32*)p; }
+__device__ __forceinline__ void gst4(uint8_t* p, uint32_t v) { *(GDbU32*)p = v; }
+
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dppmov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xf, 0xf, false);
+}
+constexpr int kRowShl2 = 0x102, kRowShl6 = 0x106, kRowShr2 = 0x112, kRowShr6 = 0x116;
+constexpr int kQuadSwap1 = 0xB1;  // quad_perm [1,0,3,2]: the other component's lane
+__device__ __forceinline__ uint32_t blend(uint32_t a, uint32_t b, bool take_a) {
+    return b ^ ((a ^ b) & (take_a ? 0xffffffffu : 0u));
+}
+
+template <int R>
 __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4* __restrict__ rec,
-                            const int* __restrict__ row_lastq, DbShared& S, const DbGlobal& G, int band_row,
+                            const int* __restrict__ row_lastq, DbShared<R>& S, const DbGlobal& G, int band_row,
                             int mby, int lane) {
+    unsigned long long w_cons = 0, w_prog = 0, w_glb = 0;  // diagnostics: ticks spent waiting
     uint8_t* Y = fs->rec_y;
     const int pitch = g.pitch, mb_w = g.mb_w;
     const uint32_t epoch = (uint32_t)fs->db_epoch;  // full 32-bit tag above the 32 payload bits
-    const bool band_first = band_row == 0, band_last = band_row == kDbRows - 1 || mby == g.mb_h - 1;
+    const bool band_first = band_row == 0, band_last = band_row == R - 1 || mby == g.mb_h - 1;
     const bool pic_last = mby == g.mb_h - 1;
-    const bool act = lane < 16;
+    const int r = lane >> 2, e = lane & 3;  // vertical layout: row r, columns 4e..; horizontal: column r, rows 4e-4..
     int* prog_me = &S.prog[0][band_row];
     int* cons_me = &S.cons[0][band_row];
     uint8_t(*tile)[16] = S.tile[band_row];
-    int qrun = row_entry_qp(fs, row_lastq, mby, lane);
-    int qprev = qrun;           // QP_Y of MB x-1
-    int P[16], C[16];           // MB x-1 (row `lane`, post-H) and MB x (row `lane`)
-    bool prev_mod = false;      // MB x-1 was modified (its own edges)
-    for (int k = 0; k < 16; ++k) P[k] = 0;
-    // sample lines: batches of kDbPf macroblocks loaded one batch ahead into registers and parked in
-    // the wave's LDS stage when their batch starts, so a load's latency spans kDbPf steps
-    uint4 pf[kDbPf];
-    uint4(*stage)[16] = S.stage[band_row];
-    const uint8_t* line = Y + (size_t)(mby * 16 + (act ? lane : 0)) * pitch;
+    const DbLaneTabs T = load_lane_tabs(lane);
+    int qrun = __builtin_amdgcn_readfirstlane(row_entry_qp(fs, row_lastq, mby, lane));
+    int qprev = qrun;
+    uint32_t prev = 0;      // MB x-1, vertical layout, final after its horizontal edges (cols 13..15 aside)
+    bool prev_mod = false;  // MB x-1 was modified (its own edges)
+    // sample dwords: batches of kDbPf macroblocks loaded one batch ahead into registers and parked
+    // in the wave's LDS stage; each step reads the next step's dword from the stage, so no LDS
+    // latency sits at the head of a step
+    uint32_t pf[kDbPf];
+    uint32_t(*stage)[64] = reinterpret_cast<uint32_t(*)[64]>(S.stage[band_row]);
+    const uint8_t* line = Y + (size_t)(mby * 16 + r) * pitch + 4 * e;
     auto issue = [&](int xb) {
 #pragma unroll
-        for (int j = 0; j < kDbPf; ++j)
-            pf[j] = gld16(line + 16 * min(xb + j, mb_w - 1));  // unconditional: a select on the
-                                                               // loaded value would wait for it here
+        for (int j = 0; j < kDbPf; ++j) pf[j] = gld4(line + 16 * min(xb + j, mb_w - 1));
+    };
+    auto park = [&]() {
+#pragma unroll
+        for (int j = 0; j < kDbPf; ++j) stage[j][lane] = pf[j];
     };
     issue(0);
+    park();
+    issue(kDbPf);
+    uint32_t cur_nx = stage[0][lane];
+    // the band's records in registers, 64 macroblocks per batch (lane j: MB xb + j), read per step
+    // with v_readlane: the step's control flow is scalar
+    uint4 rb = make_uint4(0, 0, 0, 0);
+    uint32_t rbt = 0;          // the row below's top-edge bS of the same macroblocks
+    bool below_prev = false;   // the row below filters the top edge of MB x-1
     for (int x = 0; x <= mb_w; ++x) {
         const bool have = x < mb_w;
-        if (x % kDbPf == 0) {
-            if (act) {
-#pragma unroll
-                for (int j = 0; j < kDbPf; ++j) stage[j][lane] = pf[j];
-            }
-            issue(x + kDbPf);
+        if (have && (x & 63) == 0) {
+            const int xm = min(x + lane, mb_w - 1);
+            rb = S.recs[band_row][xm];
+            rbt = pic_last ? 0u : (S.recs[band_row + 1][xm].z & 0xfffu);
         }
-        uint4 r = make_uint4(0, 0, 0, 0);
+        uint4 rr = make_uint4(0, 0, 0, 0);
+        bool below_cur = false;
         if (have) {
-            if (act) unpack16(stage[x % kDbPf][lane], C);
-            r = S.recs[band_row][x];
+            rr = rd_lane(rb, x & 63);
+            below_cur = __builtin_amdgcn_readlane((int)rbt, x & 63) != 0;
         }
-        if (have && (r.w >> 30) & 1) qrun = (r.w >> 24) & 63;
+        uint32_t cur = cur_nx;
+        if ((x + 1) % kDbPf == 0) {
+            park();
+            issue(x + 1 + kDbPf);
+        }
+        cur_nx = stage[(x + 1) % kDbPf][lane];
+        if (have && (rr.w >> 30) & 1) qrun = (rr.w >> 24) & 63;
         const int qp = qrun;
-        // ---- vertical edges of MB x (lines); edge 0 also finishes MB x-1's columns 13..15
-        bool vmod = false, v0 = false;
-        // the MB's filter parameters: its own QP (internal edges, and the horizontal ones) and the
-        // left edge's average -- both fetched before the edges, one LDS round trip
-        const DbParams dq = lds_params(S, qp), dl = lds_params(S, (qprev + qp + 1) >> 1);
-        if (have) {
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t b4 = rec_edge(r, 0, e);
-                if (!b4) continue;
-                vmod = true;
-                const int bs = (b4 >> (3 * (lane >> 2))) & 7;
-                const DbParams d = e == 0 ? dl : dq;
-                if (e == 0) {
-                    v0 = true;
-                    if (act) db_luma_line(P[12], P[13], P[14], P[15], C[0], C[1], C[2], C[3], bs, d);
-                } else if (e == 1) {
-                    if (act) db_luma_line(C[0], C[1], C[2], C[3], C[4], C[5], C[6], C[7], bs, d);
-                } else if (e == 2) {
-                    if (act) db_luma_line(C[4], C[5], C[6], C[7], C[8], C[9], C[10], C[11], bs, d);
-                } else {
-                    if (act) db_luma_line(C[8], C[9], C[10], C[11], C[12], C[13], C[14], C[15], bs, d);
-                }
-            }
+        const DbParams dq = spar(T, qp), dl = spar(T, (qprev + qp + 1) >> 1);
+        // ---- vertical edges of MB x; edge 0 also finishes MB x-1's columns 13..15
+        const bool vmod = have && (rr.x | rr.y) != 0, v0 = have && (rr.x & 0xfffu) != 0;
+        if (vmod) {
+            const uint32_t w = e < 2 ? rr.x : rr.y;
+            const int bs = (int)((w >> (12 * (e & 1) + 3 * (r >> 2))) & 7u);
+            // both moves on every lane, then a bitwise blend (blend()): a select of two DPP results lets
+            // the compiler branch on it and run each move with only its own lanes enabled, so the
+            // source lanes of the other side read as 0
+            const uint32_t pw = blend(qperm<kQuadBcast3>(prev), qperm<kQuadShr1>(cur), e == 0);
+            const bool internal = ((rr.x >> 12) | rr.y) != 0;
+            const bool strong0 = __any(e == 0 && bs == 4);
+            const Px8 o = settle_edges(px8(pw, cur), bs, sel_params(e == 0, dl, dq), e, edge_passes(internal, strong0));
+            const uint32_t mine = pk4(o.q0, o.q1, o.q2, o.q3), pside = pk4(o.p3, o.p2, o.p1, o.p0);
+            const uint32_t nxt = qperm<kQuadShl1>(pside), e0p = qperm<kQuadBcast0>(pside);
+            cur = blend((mine & 0xffffu) | (nxt & 0xffff0000u), mine, e < 3);
+            prev = blend(e0p, prev, e == 3 && v0);
         }
-        // ---- MB x-1 is final (except rows 13..15 when the row below filters its top edge there)
+        // ---- MB x-1 is final (except rows 13..15 when the row below filters its top edge)
         if (x > 0) {
             const int xp = x - 1;
-            const bool below_top = !pic_last && rec_edge(S.recs[band_row + 1][xp], 1, 0) != 0;
-            if ((prev_mod || v0) && act && (lane <= 12 || !below_top))
-                gst16(Y + (size_t)(mby * 16 + lane) * pitch + 16 * xp, pack16(P));
+            const bool below_top = below_prev;
+            if ((prev_mod || v0) && (r <= 12 || !below_top))
+                gst4(Y + (size_t)(mby * 16 + r) * pitch + 16 * xp + 4 * e, prev);
             if (below_top) {
                 if (!band_last) {
                     const int slot = xp % kDbRing;
-                    wait_lds(&S.cons[0][band_row + 1], xp - kDbRing + 1, G.err);  // ring slot free
-                    if (lane >= 12 && act)
-                        *reinterpret_cast<uint4*>(S.lring[band_row][slot][lane - 12]) = pack16(P);
+                    { const unsigned long long t = wall_clock64(); wait_lds(&S.cons[0][band_row + 1], xp - kDbRing + 1, G.err); w_cons += wall_clock64() - t; }  // ring slot free
+                    if (r >= 12) *reinterpret_cast<uint32_t*>(&S.lring[band_row][slot][r - 12][4 * e]) = prev;
                     if (lane == 0) S.ringq[0][band_row][slot] = (uint8_t)qprev;
                 } else {
                     uint64_t* dst = G.glb + ((size_t)(0 * g.mb_h + mby) * mb_w + xp) * kDbGlbWords;
-                    if (lane >= 12 && act) {
-                        const uint4 v = pack16(P);
-                        put_tagged(dst + 4 * (lane - 12), v.x, epoch);
-                        put_tagged(dst + 4 * (lane - 12) + 1, v.y, epoch);
-                        put_tagged(dst + 4 * (lane - 12) + 2, v.z, epoch);
-                        put_tagged(dst + 4 * (lane - 12) + 3, v.w, epoch);
-                    }
+                    if (r >= 12) put_tagged(dst + lane - 48, prev, epoch);
                     if (lane == 0) put_tagged(dst + kDbQWord, (uint32_t)qprev, epoch);
                 }
             }
-            if (!band_last) {
-                lds_sync_wave();
-                if (lane == 0) lds_store(prog_me, x);
-            }
+            if (!band_last && lane == 0) lds_publish(prog_me, x);
         }
         if (!have) break;
-        // ---- horizontal edges of MB x (columns, after a transpose through the tile)
-        const uint32_t t0 = rec_edge(r, 1, 0);
-        bool hmod = false;
-        for (int e = 0; e < 4; ++e) hmod |= rec_edge(r, 1, e) != 0;
+        // ---- horizontal edges of MB x (columns: lane 4c + e reads rows 4e-4 .. 4e+3 of the tile)
+        const uint32_t t0 = rec_edge(rr, 1, 0);
+        const bool hmod = (rr.z | (rr.w & 0xffffffu)) != 0;
         if (hmod) {
             int qtop = qp;
-            if (t0) {  // the row above's bottom lines of MB x
+            if (t0) {  // the row above's bottom lines of MB x -> tile rows 0..3
                 if (!band_first) {
-                    wait_lds(&S.prog[0][band_row - 1], x + 1, G.err);
+                    { const unsigned long long t = wall_clock64(); wait_lds(&S.prog[0][band_row - 1], x + 1, G.err); w_prog += wall_clock64() - t; }
                     const int slot = x % kDbRing;
-                    if (lane < 4)
-                        *reinterpret_cast<uint4*>(tile[lane]) =
-                            *reinterpret_cast<const uint4*>(S.lring[band_row - 1][slot][lane]);
-                    qtop = S.ringq[0][band_row - 1][slot];
+                    if (lane < 16)
+                        *reinterpret_cast<uint32_t*>(&tile[lane >> 2][4 * (lane & 3)]) =
+                            *reinterpret_cast<const uint32_t*>(&S.lring[band_row - 1][slot][lane >> 2][4 * (lane & 3)]);
+                    qtop = __builtin_amdgcn_readfirstlane(S.ringq[0][band_row - 1][slot]);
                 } else {
                     // rows 12..15 of the band above (lanes 0..15, a word each) and its QP_Y (lane 16);
-                    // the poll retires its loads here (left pending, the compiler's wait at the merge
-                    // below would be a vmcnt(0) on every row's H phase)
+                    // the poll retires its loads here (a vmcnt(0) at the merge below otherwise)
                     const uint64_t* src = G.glb + ((size_t)(0 * g.mb_h + mby - 1) * mb_w + x) * kDbGlbWords;
+                    const unsigned long long tq = wall_clock64();
                     const uint32_t v = poll_tagged(src + (lane <= kDbQWord ? lane : 0), lane <= kDbQWord, epoch, G.err);
+                    w_glb += wall_clock64() - tq;
                     if (lane < 16) *reinterpret_cast<uint32_t*>(&tile[lane >> 2][4 * (lane & 3)]) = v;
                     qtop = __builtin_amdgcn_readlane((int)v, kDbQWord);
                 }
             }
-            if (act) *reinterpret_cast<uint4*>(tile[4 + lane]) = pack16(C);
-            const DbParams dt = lds_params(S, (qtop + qp + 1) >> 1);
+            *reinterpret_cast<uint32_t*>(&tile[4 + r][4 * e]) = cur;
+            const DbParams dt = spar(T, (qtop + qp + 1) >> 1);
             lds_sync_wave();
-            int col[20];
-            if (act) {
-#pragma unroll
-                for (int k = 0; k < 20; ++k) col[k] = tile[k][lane];
-            }
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t b4 = rec_edge(r, 1, e);
-                if (!b4) continue;
-                const int bs = (b4 >> (3 * (lane >> 2))) & 7;
-                const DbParams d = e == 0 ? dt : dq;
-                if (!act) continue;
-                if (e == 0)
-                    db_luma_line(col[0], col[1], col[2], col[3], col[4], col[5], col[6], col[7], bs, d);
-                else if (e == 1)
-                    db_luma_line(col[4], col[5], col[6], col[7], col[8], col[9], col[10], col[11], bs, d);
-                else if (e == 2)
-                    db_luma_line(col[8], col[9], col[10], col[11], col[12], col[13], col[14], col[15], bs, d);
-                else
-                    db_luma_line(col[12], col[13], col[14], col[15], col[16], col[17], col[18], col[19], bs, d);
-            }
-            if (act) {
-#pragma unroll
-                for (int k = 1; k < 20; ++k) tile[k][lane] = (uint8_t)col[k];
-            }
+            Px8 in;
+            in.p3 = tile[4 * e][r];
+            in.p2 = tile[4 * e + 1][r];
+            in.p1 = tile[4 * e + 2][r];
+            in.p0 = tile[4 * e + 3][r];
+            in.q0 = tile[4 * e + 4][r];
+            in.q1 = tile[4 * e + 5][r];
+            in.q2 = tile[4 * e + 6][r];
+            in.q3 = tile[4 * e + 7][r];
+            const uint32_t w = e < 2 ? rr.z : rr.w;
+            const int bs = (int)((w >> (12 * (e & 1) + 3 * (r >> 2))) & 7u);
+            const bool internal = ((rr.z >> 12) | (rr.w & 0xffffffu)) != 0;
+            const bool strong0 = __any(e == 0 && bs == 4);
+            const Px8 o = settle_edges(in, bs, sel_params(e == 0, dt, dq), e, edge_passes(internal, strong0));
+            lds_sync_wave();  // every lane's reads done before the tile is rewritten
+            // Each lane writes rows no other lane writes (the compiler may reorder one lane's stores,
+            // so lanes must not race on a byte): edge e's q0' / q1' (rows 4e+4, 4e+5) and p1' / p0'
+            // (rows 4e+2, 4e+3).  Edge e's q2' is edge e+1's p1 input, which that edge's p1' already
+            // carries after the passes; an internal edge's p2' is its neighbour's q1'; only a strong
+            // edge 0 writes p2' (row 1: the upper neighbour's row 13).
+            tile[4 * e + 4][r] = (uint8_t)o.q0;
+            tile[4 * e + 5][r] = (uint8_t)o.q1;
+            if (strong0 && e == 0) tile[1][r] = (uint8_t)o.p2;
+            tile[4 * e + 2][r] = (uint8_t)o.p1;
+            tile[4 * e + 3][r] = (uint8_t)o.p0;
             lds_sync_wave();
-            if (act) unpack16(*reinterpret_cast<const uint4*>(tile[4 + lane]), C);
+            cur = *reinterpret_cast<const uint32_t*>(&tile[4 + r][4 * e]);
             // the upper neighbour's rows 13..15: this row is their writer when it filters its top edge
-            if (t0 && lane >= 1 && lane < 4)
-                gst16(Y + (size_t)(mby * 16 - 4 + lane) * pitch + 16 * x, *reinterpret_cast<const uint4*>(tile[lane]));
+            if (t0 && r >= 1 && r < 4)
+                gst4(Y + (size_t)(mby * 16 - 4 + r) * pitch + 16 * x + 4 * e,
+                     *reinterpret_cast<const uint32_t*>(&tile[r][4 * e]));
         }
         // step done: the row above may reuse the ring slot of MB x
-        if (!band_first && lane == 0) lds_store(cons_me, x + 1);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) P[k] = C[k];
+        if (!band_first && lane == 0) lds_publish(cons_me, x + 1);
+        prev = cur;
         prev_mod = vmod || hmod;
         qprev = qp;
+        below_prev = below_cur;
+    }
+    if (lane == 0) {
+        g_db_waits[0][mby][0] = w_cons;
+        g_db_waits[0][mby][1] = w_prog;
+        g_db_waits[0][mby][2] = w_glb;
     }
     if (lane == 0) lds_store(cons_me, mb_w + 1);
 }
 
 // ---------------------------------------------------------------- chroma row engine
-// lane l < 16: component l >> 3 (0 = Cb, 1 = Cr), line / column l & 7
+// Chroma edges (at chroma columns / rows 0 and 4) modify p0 / q0 only and read p1 / q1, so the two
+// edges of a direction never touch each other's samples: one pass, all in parallel.  Vertical
+// layout: lane 8k + 2q + c holds line k (0..7) of the MB's 16 interleaved Cb/Cr bytes as dword q
+// (chroma columns 2q, 2q+1) and filters component c of the edge whose q side starts in that dword
+// (q 0: the MB edge, p side in the left MB's dword 3; q 2: the internal edge, p side in dword 1).
+// Horizontal layout: lane 16ce + b filters byte column b (chroma column b / 2, component b % 2) of
+// edge ce, reading rows 4ce-2 .. 4ce+1 from a per-wave tile (rows 0..1: the MB above's rows 6..7).
+template <int R>
 __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uint4* __restrict__ rec,
-                              const int* __restrict__ row_lastq, DbShared& S, const DbGlobal& G, int band_row,
+                              const int* __restrict__ row_lastq, DbShared<R>& S, const DbGlobal& G, int band_row,
                               int mby, int lane) {
+    unsigned long long w_cons = 0, w_prog = 0, w_glb = 0;  // diagnostics: ticks spent waiting
     uint8_t* UV = fs->rec_uv;
     const int pitch = g.pitch, mb_w = g.mb_w;
     const uint32_t epoch = (uint32_t)fs->db_epoch;  // full 32-bit tag above the 32 payload bits
-    const bool band_first = band_row == 0, band_last = band_row == kDbRows - 1 || mby == g.mb_h - 1;
+    const bool band_first = band_row == 0, band_last = band_row == R - 1 || mby == g.mb_h - 1;
     const bool pic_last = mby == g.mb_h - 1;
-    const bool act = lane < 16;
-    const int comp = (lane >> 3) & 1, ln = lane & 7;
+    const int k = lane >> 3, dq4 = (lane >> 1) & 3, comp = lane & 1;  // vertical layout
+    const int hb = lane & 15, hce = (lane >> 4) & 1;                   // horizontal layout (lanes < 32)
     int* prog_me = &S.prog[1][band_row];
     int* cons_me = &S.cons[1][band_row];
-    uint8_t(*tile)[16] = S.tile[kDbRows + band_row];
+    uint8_t(*tile)[16] = S.tile[R + band_row];
     const int cqo = fs->chroma_qp_offset;
-    int qrun = row_entry_qp(fs, row_lastq, mby, lane);
+    const DbLaneTabs T = load_lane_tabs(lane);
+    int qrun = __builtin_amdgcn_readfirstlane(row_entry_qp(fs, row_lastq, mby, lane));
     int qprev = qrun;
-    int P[8], C[8];
+    uint32_t prev = 0;
     bool prev_mod = false;
-    for (int k = 0; k < 8; ++k) P[k] = 0;
-    auto load_line = [&](const uint4& v, int* o) {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = (w[k >> 1] >> (16 * (k & 1) + 8 * comp)) & 0xff;
-    };
-    // write this lane's 8 samples into tile row `row` (interleaved with the other component)
-    auto to_tile = [&](int row, const int* o) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) tile[row][2 * k + comp] = (uint8_t)o[k];
-    };
-    uint4 pf[kDbPf];
-    uint4(*stage)[16] = S.stage[kDbRows + band_row];
-    const uint8_t* line = UV + (size_t)(mby * 8 + ln) * pitch;
+    uint32_t pf[kDbPf];
+    uint32_t(*stage)[64] = reinterpret_cast<uint32_t(*)[64]>(S.stage[R + band_row]);
+    const uint8_t* line = UV + (size_t)(mby * 8 + k) * pitch + 4 * dq4;
     auto issue = [&](int xb) {
 #pragma unroll
-        for (int j = 0; j < kDbPf; ++j)
-            pf[j] = gld16(line + 16 * min(xb + j, mb_w - 1));  // unconditional: a select on the
-                                                               // loaded value would wait for it here
+        for (int j = 0; j < kDbPf; ++j) pf[j] = gld4(line + 16 * min(xb + j, mb_w - 1));
+    };
+    auto park = [&]() {
+#pragma unroll
+        for (int j = 0; j < kDbPf; ++j) stage[j][lane] = pf[j];
     };
     issue(0);
+    park();
+    issue(kDbPf);
+    uint32_t cur_nx = stage[0][lane];
+    const int cs = 8 * comp;  // bit offset of this component's byte in a dword (bytes c and 2 + c)
+    uint4 rb = make_uint4(0, 0, 0, 0);
+    uint32_t rbt = 0;
+    bool below_prev = false;
     for (int x = 0; x <= mb_w; ++x) {
         const bool have = x < mb_w;
-        if (x % kDbPf == 0) {
-            if (act) {
-#pragma unroll
-                for (int j = 0; j < kDbPf; ++j) stage[j][lane] = pf[j];
-            }
-            issue(x + kDbPf);
+        if (have && (x & 63) == 0) {
+            const int xm = min(x + lane, mb_w - 1);
+            rb = S.recs[band_row][xm];
+            rbt = pic_last ? 0u : (S.recs[band_row + 1][xm].z & 0xfffu);
         }
-        uint4 r = make_uint4(0, 0, 0, 0);
+        uint4 rr = make_uint4(0, 0, 0, 0);
+        bool below_cur = false;
         if (have) {
-            if (act) load_line(stage[x % kDbPf][lane], C);
-            r = S.recs[band_row][x];
+            rr = rd_lane(rb, x & 63);
+            below_cur = __builtin_amdgcn_readlane((int)rbt, x & 63) != 0;
         }
-        if (have && (r.w >> 30) & 1) qrun = (r.w >> 24) & 63;
+        uint32_t cur = cur_nx;
+        if ((x + 1) % kDbPf == 0) {
+            park();
+            issue(x + 1 + kDbPf);
+        }
+        cur_nx = stage[(x + 1) % kDbPf][lane];
+        if (have && (rr.w >> 30) & 1) qrun = (rr.w >> 24) & 63;
         const int qp = qrun;
-        bool vmod = false, v0 = false;
-        const int cq = lds_cqp(S, qp, cqo), cqp = lds_cqp(S, qprev, cqo);
-        const DbParams dq = lds_params(S, cq), dl = lds_params(S, (cqp + cq + 1) >> 1);
-        if (have) {
-            for (int ce = 0; ce < 2; ++ce) {
-                const uint32_t b4 = rec_edge(r, 0, 2 * ce);
-                if (!b4) continue;
-                vmod = true;
-                const int bs = (b4 >> (3 * (ln >> 1))) & 7;
-                const DbParams d = ce == 0 ? dl : dq;
-                if (ce == 0) {
-                    v0 = true;
-                    if (act) db_chroma_line(P[6], P[7], C[0], C[1], bs, d);
-                } else if (act) {
-                    db_chroma_line(C[2], C[3], C[4], C[5], bs, d);
-                }
-            }
+        const int cq = scqp(T, qp, cqo), cqp = scqp(T, qprev, cqo);
+        const DbParams dq = spar(T, cq), dl = spar(T, (cqp + cq + 1) >> 1);
+        // ---- vertical chroma edges (luma edges 0 and 2)
+        const uint32_t ve0 = rec_edge(rr, 0, 0), ve2 = rec_edge(rr, 0, 2);
+        const bool vmod = have && (ve0 | ve2) != 0, v0 = have && ve0 != 0;
+        if (vmod) {
+            const uint32_t pa = dppmov<kRowShl6>(prev), pb = dppmov<kRowShr2>(cur);
+            const uint32_t pw = blend(pa, pb, dq4 == 0);  // p side: the left MB's dword 3 / this MB's dword 1
+            const uint32_t b4 = dq4 == 0 ? ve0 : ve2;
+            const bool edge_lane = dq4 == 0 || dq4 == 2;
+            const int bs = edge_lane ? (int)((b4 >> (3 * (k >> 1))) & 7u) : 0;
+            int p1 = (int)((pw >> cs) & 0xff), p0 = (int)((pw >> (16 + cs)) & 0xff);
+            int q0 = (int)((cur >> cs) & 0xff);
+            const int q1 = (int)((cur >> (16 + cs)) & 0xff);
+            db_chroma_line(p1, p0, q0, q1, bs, sel_params(dq4 == 0, dl, dq));
+            // this component's bytes of the two dwords; the other component's lane has the rest
+            const uint32_t nq = (cur & ~(0xffu << cs)) | ((uint32_t)q0 << cs);
+            const uint32_t np = (pw & ~(0xffu << (16 + cs))) | ((uint32_t)p0 << (16 + cs));
+            const uint32_t oq = dppmov<kQuadSwap1>(nq), op = dppmov<kQuadSwap1>(np);
+            const uint32_t cmask = comp ? 0x00ff00ffu : 0xff00ff00u;  // the other component's bytes
+            const uint32_t fq = (nq & ~cmask) | (oq & cmask), fp = (np & ~cmask) | (op & cmask);
+            // dword 1 <- edge 2's p side (lane + 2); the left MB's dword 3 <- edge 0's p side (lane - 6)
+            const uint32_t from_e2 = dppmov<kRowShl2>(fp), from_e0 = dppmov<kRowShr6>(fp);
+            const uint32_t own = blend(fq, cur, edge_lane);
+            cur = blend(from_e2, own, dq4 == 1 && ve2 != 0);  // blends, never selects (see the luma engine)
+            prev = blend(from_e0, prev, dq4 == 3 && v0);
         }
         if (x > 0) {
             const int xp = x - 1;
-            const bool below_top = !pic_last && rec_edge(S.recs[band_row + 1][xp], 1, 0) != 0;
-            if (prev_mod || v0 || below_top) {
-                // MB x-1's rows through the tile (the two components interleave)
-                if (act) to_tile(2 + ln, P);
-                lds_sync_wave();
-                if ((prev_mod || v0) && lane < 8 && (lane <= 6 || !below_top))
-                    gst16(UV + (size_t)(mby * 8 + lane) * pitch + 16 * xp, *reinterpret_cast<const uint4*>(tile[2 + lane]));
-                if (below_top) {
-                    if (!band_last) {
-                        const int slot = xp % kDbRing;
-                        wait_lds(&S.cons[1][band_row + 1], xp - kDbRing + 1, G.err);
-                        if (lane < 2)
-                            *reinterpret_cast<uint4*>(S.cring[band_row][slot][lane]) =
-                                *reinterpret_cast<const uint4*>(tile[8 + lane]);
-                        if (lane == 0) S.ringq[1][band_row][slot] = (uint8_t)qprev;
-                    } else {
-                        uint64_t* dst = G.glb + ((size_t)(1 * g.mb_h + mby) * mb_w + xp) * kDbGlbWords;
-                        if (lane < 8)
-                            put_tagged(dst + lane, *reinterpret_cast<const uint32_t*>(&tile[8 + (lane >> 2)][4 * (lane & 3)]),
-                                       epoch);
-                        if (lane == 0) put_tagged(dst + 8, (uint32_t)qprev, epoch);
-                    }
+            const bool below_top = below_prev;
+            if ((prev_mod || v0) && comp == 0 && (k <= 6 || !below_top))
+                gst4(UV + (size_t)(mby * 8 + k) * pitch + 16 * xp + 4 * dq4, prev);
+            if (below_top) {
+                if (!band_last) {
+                    const int slot = xp % kDbRing;
+                    { const unsigned long long t = wall_clock64(); wait_lds(&S.cons[1][band_row + 1], xp - kDbRing + 1, G.err); w_cons += wall_clock64() - t; }
+                    if (k >= 6 && comp == 0)
+                        *reinterpret_cast<uint32_t*>(&S.cring[band_row][slot][k - 6][4 * dq4]) = prev;
+                    if (lane == 0) S.ringq[1][band_row][slot] = (uint8_t)qprev;
+                } else {
+                    uint64_t* dst = G.glb + ((size_t)(1 * g.mb_h + mby) * mb_w + xp) * kDbGlbWords;
+                    if (k >= 6 && comp == 0) put_tagged(dst + 4 * (k - 6) + dq4, prev, epoch);
+                    if (lane == 0) put_tagged(dst + 8, (uint32_t)qprev, epoch);
                 }
-                lds_sync_wave();  // tile reads done before it is rewritten
             }
-            if (!band_last) {
-                lds_sync_wave();
-                if (lane == 0) lds_store(prog_me, x);
-            }
+            if (!band_last && lane == 0) lds_publish(prog_me, x);
         }
         if (!have) break;
-        const uint32_t t0 = rec_edge(r, 1, 0);
-        const bool hmod = t0 != 0 || rec_edge(r, 1, 2) != 0;
+        // ---- horizontal chroma edges (luma edges 0 and 2)
+        const uint32_t t0 = rec_edge(rr, 1, 0), he2 = rec_edge(rr, 1, 2);
+        const bool hmod = (t0 | he2) != 0;
         if (hmod) {
             int qtop = qp;
-            if (t0) {
+            if (t0) {  // the row above's bottom chroma rows 6..7 of MB x -> tile rows 0..1
                 if (!band_first) {
-                    wait_lds(&S.prog[1][band_row - 1], x + 1, G.err);
+                    { const unsigned long long t = wall_clock64(); wait_lds(&S.prog[1][band_row - 1], x + 1, G.err); w_prog += wall_clock64() - t; }
                     const int slot = x % kDbRing;
-                    if (lane < 2)
-                        *reinterpret_cast<uint4*>(tile[lane]) =
-                            *reinterpret_cast<const uint4*>(S.cring[band_row - 1][slot][lane]);
-                    qtop = S.ringq[1][band_row - 1][slot];
+                    if (lane < 8)
+                        *reinterpret_cast<uint32_t*>(&tile[lane >> 2][4 * (lane & 3)]) =
+                            *reinterpret_cast<const uint32_t*>(&S.cring[band_row - 1][slot][lane >> 2][4 * (lane & 3)]);
+                    qtop = __builtin_amdgcn_readfirstlane(S.ringq[1][band_row - 1][slot]);
                 } else {
                     const uint64_t* src = G.glb + ((size_t)(1 * g.mb_h + mby - 1) * mb_w + x) * kDbGlbWords;
+                    const unsigned long long tq = wall_clock64();
                     const uint32_t v = poll_tagged(src + (lane <= 8 ? lane : 0), lane <= 8, epoch, G.err);
+                    w_glb += wall_clock64() - tq;
                     if (lane < 8) *reinterpret_cast<uint32_t*>(&tile[lane >> 2][4 * (lane & 3)]) = v;
                     qtop = __builtin_amdgcn_readlane((int)v, 8);
                 }
             }
-            if (act) to_tile(2 + ln, C);
-            const DbParams dt = lds_params(S, (lds_cqp(S, qtop, cqo) + cq + 1) >> 1);
+            if (comp == 0) *reinterpret_cast<uint32_t*>(&tile[2 + k][4 * dq4]) = cur;
+            const DbParams dt = spar(T, (scqp(T, qtop, cqo) + cq + 1) >> 1);
             lds_sync_wave();
-            int col[10];
-            if (act) {
-#pragma unroll
-                for (int k = 0; k < 10; ++k) col[k] = tile[k][2 * ln + comp];
-            }
-            for (int ce = 0; ce < 2; ++ce) {
-                const uint32_t b4 = rec_edge(r, 1, 2 * ce);
-                if (!b4) continue;
-                const int bs = (b4 >> (3 * (ln >> 1))) & 7;
-                const DbParams d = ce == 0 ? dt : dq;
-                if (!act) continue;
-                if (ce == 0)
-                    db_chroma_line(col[0], col[1], col[2], col[3], bs, d);
-                else
-                    db_chroma_line(col[4], col[5], col[6], col[7], bs, d);
-            }
-            if (act) {
-#pragma unroll
-                for (int k = 1; k < 10; ++k) tile[k][2 * ln + comp] = (uint8_t)col[k];
+            const bool hl = lane < 32;
+            const int r0 = 4 * hce;  // tile rows r0 .. r0+3 = p1, p0, q0, q1
+            int p1 = tile[r0][hb], p0 = tile[r0 + 1][hb], q0 = tile[r0 + 2][hb];
+            const int q1 = tile[r0 + 3][hb];
+            const uint32_t b4 = hce ? he2 : t0;
+            const int bs = hl ? (int)((b4 >> (3 * (hb >> 2))) & 7u) : 0;
+            db_chroma_line(p1, p0, q0, q1, bs, sel_params(hce == 0, dt, dq));
+            lds_sync_wave();
+            if (hl) {
+                tile[r0 + 1][hb] = (uint8_t)p0;
+                tile[r0 + 2][hb] = (uint8_t)q0;
             }
             lds_sync_wave();
-            if (act) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) C[k] = tile[2 + ln][2 * k + comp];
-            }
-            if (t0 && lane == 1)  // the upper neighbour's row 7
-                gst16(UV + (size_t)(mby * 8 - 1) * pitch + 16 * x, *reinterpret_cast<const uint4*>(tile[1]));
+            cur = *reinterpret_cast<const uint32_t*>(&tile[2 + k][4 * dq4]);
+            if (t0 && lane < 4)  // the upper neighbour's row 7
+                gst4(UV + (size_t)(mby * 8 - 1) * pitch + 16 * x + 4 * lane,
+                     *reinterpret_cast<const uint32_t*>(&tile[1][4 * lane]));
             lds_sync_wave();
         }
-        if (!band_first && lane == 0) lds_store(cons_me, x + 1);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) P[k] = C[k];
+        if (!band_first && lane == 0) lds_publish(cons_me, x + 1);
+        prev = cur;
         prev_mod = vmod || hmod;
         qprev = qp;
+        below_prev = below_cur;
+    }
+    if (lane == 0) {
+        g_db_waits[1][mby][0] = w_cons;
+        g_db_waits[1][mby][1] = w_prog;
+        g_db_waits[1][mby][2] = w_glb;
     }
     if (lane == 0) lds_store(cons_me, mb_w + 1);
 }
 
-__global__ __launch_bounds__(64 * kDbRows) void k_deblock(Geometry g, const FrameState* __restrict__ fs,
+template <int R>
+__global__ __launch_bounds__(64 * R) void k_deblock(Geometry g, const FrameState* __restrict__ fs,
                                                           const uint4* __restrict__ rec,
                                                           const int* __restrict__ row_lastq, DbGlobal G) {
     // a serial chain on few waves: issue priority over the bulk kernels sharing its SIMDs
     __builtin_amdgcn_s_setprio(3);
     // one workgroup per (band, plane): 8 waves of 512 threads leave each wave 256 VGPRs for the
     // line registers and the prefetch batch
-    __shared__ DbShared S;
+    __shared__ DbShared<R> S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int band_row = wave, plane = blockIdx.y;
-    if (threadIdx.x < 2 * kDbRows) {
-        S.prog[threadIdx.x / kDbRows][threadIdx.x % kDbRows] = 0;
-        S.cons[threadIdx.x / kDbRows][threadIdx.x % kDbRows] = 0;
+    if (threadIdx.x < 2 * R) {
+        S.prog[threadIdx.x / R][threadIdx.x % R] = 0;
+        S.cons[threadIdx.x / R][threadIdx.x % R] = 0;
     }
     if (threadIdx.x < 52) {
         const DbParams d = db_params((int)threadIdx.x);
@@ -570,19 +738,25 @@ __global__ __launch_bounds__(64 * kDbRows) void k_deblock(Geometry g, const Fram
         S.cqp[threadIdx.x] = (uint8_t)chroma_qp((int)threadIdx.x, 0);
     }
     {  // the band's records and the next row's (their top-edge bS decides who writes rows 13..15)
-        const int r0 = blockIdx.x * kDbRows, nrow = min(kDbRows + 1, g.mb_h - r0);
+        const int r0 = blockIdx.x * R, nrow = min(R + 1, g.mb_h - r0);
         for (int i = threadIdx.x; i < nrow * g.mb_w; i += blockDim.x) {
             const int rr = i / g.mb_w, xx = i - rr * g.mb_w;
             S.recs[rr][xx] = rec[(size_t)(r0 + rr) * g.mb_w + xx];
         }
     }
     __syncthreads();
-    const int mby = blockIdx.x * kDbRows + band_row;
+    const int mby = blockIdx.x * R + band_row;
     if (mby >= g.mb_h) return;  // no row above a missing row waits on it (rows below are missing too)
+    const unsigned long long t_start = wall_clock64(), c_start = __builtin_amdgcn_s_memtime();
     if (plane == 0)
-        db_luma_row(g, fs, rec, row_lastq, S, G, band_row, mby, lane);
+        db_luma_row<R>(g, fs, rec, row_lastq, S, G, band_row, mby, lane);
     else
-        db_chroma_row(g, fs, rec, row_lastq, S, G, band_row, mby, lane);
+        db_chroma_row<R>(g, fs, rec, row_lastq, S, G, band_row, mby, lane);
+    if (lane == 0) {
+        g_db_stamps[plane][mby][0] = t_start;
+        g_db_stamps[plane][mby][1] = wall_clock64();
+        g_db_clk[plane][mby] = __builtin_amdgcn_s_memtime() - c_start;
+    }
 }
 
 // Distortion of the filtered picture: one workgroup per MB row, partials Y, U, V, Y outside the
@@ -635,13 +809,42 @@ __global__ __launch_bounds__(256) void k_db_sse(Geometry g, const FrameState* __
 
 }  // namespace
 
+std::vector<unsigned long long> deblock_row_stamps(int mb_h) {
+    std::vector<unsigned long long> v((size_t)2 * kMaxSlices * 2), w((size_t)2 * kMaxSlices * 3);
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_db_stamps), v.size() * sizeof(unsigned long long)));
+    HIP_CHECK(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_db_waits), w.size() * sizeof(unsigned long long)));
+    std::vector<unsigned long long> ph((size_t)kMaxSlices * 4);
+    HIP_CHECK(hipMemcpyFromSymbol(ph.data(), HIP_SYMBOL(g_db_phase), ph.size() * sizeof(unsigned long long)));
+    std::vector<unsigned long long> out;  // per plane and row: start, end, wait ring, wait above, wait band
+    for (int p = 0; p < 2; ++p)
+        for (int y = 0; y < mb_h; ++y) {
+            out.push_back(v[((size_t)p * kMaxSlices + y) * 2]);
+            out.push_back(v[((size_t)p * kMaxSlices + y) * 2 + 1]);
+            for (int k = 0; k < 3; ++k) out.push_back(w[((size_t)p * kMaxSlices + y) * 3 + k]);
+        }
+    for (int y = 0; y < mb_h; ++y)  // then the luma rows' phase ticks: head, V, final, H
+        for (int k = 0; k < 4; ++k) out.push_back(ph[(size_t)y * 4 + k]);
+    std::vector<unsigned long long> ck((size_t)2 * kMaxSlices);
+    HIP_CHECK(hipMemcpyFromSymbol(ck.data(), HIP_SYMBOL(g_db_clk), ck.size() * sizeof(unsigned long long)));
+    for (int p = 0; p < 2; ++p)  // then each row wave's shader-clock cycles
+        for (int y = 0; y < mb_h; ++y) out.push_back(ck[(size_t)p * kMaxSlices + y]);
+    return out;
+}
+
 void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream) {
     if (g.mb_w > kDbMaxW || g.mb_h > kMaxSlices) throw std::invalid_argument("launch_deblock: picture too large");
     hipLaunchKernelGGL(k_db_prep, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, b.mb, b.db_rec, b.db_rowq);
     DbGlobal G{b.db_glb, b.db_err};
-    hipLaunchKernelGGL(k_deblock, dim3((g.mb_h + kDbRows - 1) / kDbRows, 2), dim3(64 * kDbRows), 0, stream, g, b.fs,
-                       b.db_rec, b.db_rowq, G);
+    static const int rows = [] {
+        const char* e = std::getenv("MXDESK_DB_ROWS");
+        return e && std::atoi(e) == 8 ? 8 : (e && std::atoi(e) == 4 ? 4 : kDbRowsDefault);
+    }();
+    if (rows == 8)
+        hipLaunchKernelGGL(k_deblock<8>, dim3((g.mb_h + 7) / 8, 2), dim3(64 * 8), 0, stream, g, b.fs, b.db_rec, b.db_rowq, G);
+    else
+        hipLaunchKernelGGL(k_deblock<4>, dim3((g.mb_h + 3) / 4, 2), dim3(64 * 4), 0, stream, g, b.fs, b.db_rec, b.db_rowq, G);
     hipLaunchKernelGGL(k_db_sse, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, src_y, src_uv);
 }
 

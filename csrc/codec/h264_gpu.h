@@ -11,6 +11,7 @@
 // Only the slice payloads (RBSP, byte aligned) leave the GPU; the host adds start
 // codes, NAL headers and emulation-prevention bytes (h264_encoder.cpp).
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -184,6 +185,9 @@ void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const plane
                  hipStream_t stream, const FrameState* publish = nullptr);
 // In-loop deblocking of the reconstruction (FrameState::rec_y / rec_uv, in place) + the distortion
 // partials of the filtered picture (h264_deblock.hip); after the analysis kernels.
+// diagnostics: device wall-clock (start, end) of every row wave of the last k_deblock, luma rows
+// then chroma rows
+std::vector<unsigned long long> deblock_row_stamps(int mb_h);
 void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream);
 // Copy the source luma into FrameState::save_src (IDR pictures; the pointer is read on the device

@@ -660,3 +660,37 @@ def test_gpu_adaptive_deblock_in_flight_vs_cpu(gpu, depth):
     for t, (g, c) in enumerate(zip(got, want)):
         assert g == c, f"frame {t}: GPU bitstream (depth {depth}, in flight) differs from CPU encoder"
     assert flags == flags_c and 1 in flags and flags[-1] == 0, (flags, flags_c)
+
+
+@pytest.mark.parametrize("w,h,qp", [(320, 192, 40), (352, 288, 46), (1920, 1088, 44)])
+def test_gpu_deblock_strong_filtering_bit_exact_vs_cpu(gpu, w, h, qp):
+    """The edge-parallel k_deblock (all four edges of a direction settled in 1-3 passes) against the
+    CPU's serial 8.7 order at high QP (large alpha / beta / tC0: most edges filter, bS 4 strong
+    filters on the IDR and on intra macroblocks of P pictures): GPU == CPU, decoded == recon."""
+    from .test_deblock import _pan_frames
+
+    cfg = gpu.EncoderConfig()
+    cfg.width, cfg.height = w, h
+    cfg.bitrate_kbps, cfg.qp, cfg.search_range, cfg.deblock, cfg.intra_in_p = 0, qp, 8, 1, 1
+    genc = gpu.GpuH264Encoder(cfg, _stream())
+    cenc = gpu.CpuH264Encoder(cfg)
+    ch = genc.coded_height
+    stream, grec = b"", []
+    for t, (y, uv) in enumerate(_pan_frames(w, h, 4)):
+        if t == 2:
+            y = y.copy()
+            y[16:64, 32:96] = 255 - y[16:64, 32:96]  # new content: intra macroblocks in a P picture
+        dy = pitched(y, genc.pitch, ch)
+        duv = pitched(uv, genc.pitch, ch // 2, uv=True)
+        torch.cuda.synchronize()
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        assert gau == cau, f"frame {t}"
+        assert np.array_equal(genc.recon()[0], cenc.recon()[0]) and np.array_equal(genc.recon()[1], cenc.recon()[1])
+        stream += gau
+        grec.append(genc.recon())
+    if w * h <= 352 * 288:
+        dec = Decoder()
+        dec.decode(stream)
+        for (yy, u, v), (ry, ruv) in zip(dec.frames_coded, grec):
+            assert np.array_equal(yy, ry[:h, :w]) and np.array_equal(u, ruv[:h // 2, 0:w:2])
