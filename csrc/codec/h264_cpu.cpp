@@ -424,6 +424,9 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
     const Geometry g = geom_of(common_, cw_, ch_);
     const uint8_t* ref_y = rec_y_[cur_ ^ 1].data();
     const uint8_t* ref_uv = rec_uv_[cur_ ^ 1].data();
+    // the motion search reads the reference before its in-loop filter (the GPU encoder searches
+    // beside k_deblock); prediction uses the filtered reference
+    const uint8_t* me_ref = ref_deblocked_ ? rec_unf_y_.data() : ref_y;
     uint8_t* rec_y = rec_y_[cur_].data();
     uint8_t* rec_uv = rec_uv_[cur_].data();
     const int frame_qp = frame_qp_();
@@ -433,11 +436,11 @@ void CpuH264Encoder::encode_inter(const uint8_t* sy, const uint8_t* suv, int pit
             MbInfo& m = mb_[mbi];
             std::memset(&m, 0, sizeof m);
             if (cfg_.partitions) {
-                me_search_parts_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel,
+                me_search_parts_cpu(sy, pitch, me_ref, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel,
                                     cfg_.me_coarse, m);
             } else {
                 int vx = 0, vy = 0;
-                me_search_cpu(sy, pitch, ref_y, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &vx, &vy,
+                me_search_cpu(sy, pitch, me_ref, cw_, ch_, x0, y0, frame_qp, cfg_.search_range, cfg_.subpel, &vx, &vy,
                               cfg_.me_coarse);
                 m.mvx = (int16_t)vx;
                 m.mvy = (int16_t)vy;
@@ -683,6 +686,7 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
     std::vector<uint32_t> soff, slen;
     entropy(payload, soff, slen);
     if (deblock_now_) {  // in-loop filter: the next picture predicts from the filtered one
+        rec_unf_y_ = rec_y_[cur_];  // and searches the unfiltered one
         const Geometry g = geom_of(common_, cw_, ch_);
         std::vector<uint8_t> qpe(mb_.size());
         db_qp_eff(mb_.data(), (int)mb_.size(), g.mb_w, common_.cur_idr() ? idr_slice_rows(g.mb_h) : g.mb_h,
@@ -691,6 +695,7 @@ const std::vector<uint8_t>& CpuH264Encoder::encode(const uint8_t* y, const uint8
                             cw_);
     }
     update_deblock_decision();
+    ref_deblocked_ = deblock_now_;
     au_.clear();
     if (common_.cur_idr()) common_.write_parameter_sets(au_);
     int skipped = 0;

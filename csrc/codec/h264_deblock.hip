@@ -29,8 +29,10 @@
 //    and a counter update, so P pictures pay for the changing areas only.  1080p pan (every MB
 //    filtered): 332 -> ~220 us per picture against the earlier one-edge-at-a-time engine
 //    (profiles/r06_deblock/NOTES.md).
-//  * k_db_sse: the distortion of the filtered picture (one partial per MB row and channel), which
-//    replaces the analysis kernels' unfiltered figures in the frame statistics.
+//  * the distortion of the filtered picture (one partial per MB row and channel, replacing the
+//    analysis kernels' unfiltered figures in the frame statistics) is summed by the row waves
+//    themselves once their row is done, each over the samples it wrote (db_luma_sse): no separate
+//    pass on the frame's chain (it was 25 us at 1080p).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -261,6 +263,8 @@ constexpr int kDbQWord = 16;  // QP_Y word (luma; chroma uses word 8)
 struct DbGlobal {
     uint64_t* glb;    // [2][mb_h][mb_w][kDbGlbWords] tagged hand-off words of band-last rows
     int* err;         // mapped host word: a bounded spin timed out
+    const uint8_t* src_y;   // the picture's source (distortion of the filtered picture)
+    const uint8_t* src_uv;
 };
 // poll tagged words (lanes with need) until every one carries `epoch`; returns this lane's payload
 __device__ __forceinline__ uint32_t poll_tagged(const uint64_t* p, bool need, uint32_t epoch, int* err) {
@@ -364,6 +368,109 @@ constexpr int kRowShl2 = 0x102, kRowShl6 = 0x106, kRowShr2 = 0x112, kRowShr6 = 0
 constexpr int kQuadSwap1 = 0xB1;  // quad_perm [1,0,3,2]: the other component's lane
 __device__ __forceinline__ uint32_t blend(uint32_t a, uint32_t b, bool take_a) {
     return b ^ ((a ^ b) & (take_a ? 0xffffffffu : 0u));
+}
+
+// Distortion of the filtered picture, accounted by each sample's writer once the writer's row is
+// done (replaces a separate k_db_sse pass on the frame's chain): a row wave sums its own
+// macroblocks' rows 0..12, and rows 13..15 where the row below leaves them, plus the upper row's
+// rows 13..15 it wrote itself (its filtered top edges); every lane re-reads only dwords it wrote
+// or that nobody in this kernel writes, so no cross-wave visibility is involved.  Partials:
+// sse_part[c][mby] (Y, U, V, Y outside the quality mask), the layout k_scan_rows sums.
+__device__ void db_luma_sse(const Geometry& g, const FrameState* fs, const uint4* __restrict__ rec,
+                            const uint8_t* __restrict__ src_y, int mby, int lane) {
+    const int r = lane >> 2, e = lane & 3, mb_w = g.mb_w, pitch = g.pitch;
+    const bool pic_last = mby == g.mb_h - 1;
+    const uint8_t* Y = fs->rec_y;
+    unsigned long long sy = 0, sm = 0;
+    auto sse4 = [](uint32_t a, uint32_t b, int nvis) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int d = (int)((a >> (8 * k)) & 0xff) - (int)((b >> (8 * k)) & 0xff);
+            acc += k < nvis ? (uint32_t)(d * d) : 0u;
+        }
+        return acc;
+    };
+    for (int xb = 0; xb < mb_w; xb += 64) {
+        const int xm = min(xb + lane, mb_w - 1);
+        const uint32_t t0v = rec[(size_t)mby * mb_w + xm].z & 0xfffu;
+        const uint32_t btv = pic_last ? 0u : (rec[(size_t)(mby + 1) * mb_w + xm].z & 0xfffu);
+        const int xe = min(mb_w, xb + 64);
+        for (int x = xb; x < xe; ++x) {
+            const bool t0 = __builtin_amdgcn_readlane((int)t0v, x - xb) != 0;
+            const bool below = __builtin_amdgcn_readlane((int)btv, x - xb) != 0;
+            const int cx = 16 * x + 4 * e, nvis = min(4, max(0, g.width - cx));
+            const int yy = mby * 16 + r;
+            uint32_t acc = 0, accm = 0;
+            if ((r <= 12 || !below) && yy < g.height) {
+                const uint32_t a = gld4(src_y + (size_t)yy * pitch + cx), b = gld4(Y + (size_t)yy * pitch + cx);
+                acc = sse4(a, b, nvis);
+                if (mb_unmasked(fs, x, mby)) accm = acc;
+            }
+            if (t0 && r >= 1 && r < 4) {  // the upper macroblock's rows 13..15, written by this row
+                const int ya = mby * 16 - 4 + r;
+                const uint32_t a = gld4(src_y + (size_t)ya * pitch + cx), b = gld4(Y + (size_t)ya * pitch + cx);
+                const uint32_t v = sse4(a, b, nvis);
+                acc += v;
+                if (mb_unmasked(fs, x, mby - 1)) accm += v;
+            }
+            sy += acc;
+            sm += accm;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sy += __shfl_xor(sy, o, 64);
+        sm += __shfl_xor(sm, o, 64);
+    }
+    if (lane == 0) {
+        fs->sse_part[0 * kSsePartStride + mby] = sy;
+        fs->sse_part[3 * kSsePartStride + mby] = sm;
+    }
+}
+// Chroma: rows 0..6 (and 7 where the row below leaves it) and the upper row's row 7 it wrote.
+__device__ void db_chroma_sse(const Geometry& g, const FrameState* fs, const uint4* __restrict__ rec,
+                              const uint8_t* __restrict__ src_uv, int mby, int lane) {
+    const int k = lane >> 3, dq4 = (lane >> 1) & 3, comp = lane & 1, mb_w = g.mb_w, pitch = g.pitch;
+    const bool pic_last = mby == g.mb_h - 1;
+    const uint8_t* UV = fs->rec_uv;
+    unsigned long long su = 0, sv = 0;
+    auto sse2 = [](uint32_t a, uint32_t b, int nvis, uint32_t* u, uint32_t* v) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int d = (int)((a >> (8 * kk)) & 0xff) - (int)((b >> (8 * kk)) & 0xff);
+            const uint32_t e2 = kk < nvis ? (uint32_t)(d * d) : 0u;
+            if (kk & 1) *v += e2; else *u += e2;
+        }
+    };
+    for (int xb = 0; xb < mb_w; xb += 64) {
+        const int xm = min(xb + lane, mb_w - 1);
+        const uint32_t t0v = rec[(size_t)mby * mb_w + xm].z & 0xfffu;
+        const uint32_t btv = pic_last ? 0u : (rec[(size_t)(mby + 1) * mb_w + xm].z & 0xfffu);
+        const int xe = min(mb_w, xb + 64);
+        for (int x = xb; x < xe; ++x) {
+            const bool t0 = __builtin_amdgcn_readlane((int)t0v, x - xb) != 0;
+            const bool below = __builtin_amdgcn_readlane((int)btv, x - xb) != 0;
+            const int cx = 16 * x + 4 * dq4, nvis = min(4, max(0, g.width - cx));
+            const int yy = mby * 8 + k;
+            uint32_t u = 0, v = 0;
+            if (comp == 0 && (k <= 6 || !below) && 2 * yy < g.height)
+                sse2(gld4(src_uv + (size_t)yy * pitch + cx), gld4(UV + (size_t)yy * pitch + cx), nvis, &u, &v);
+            if (t0 && lane < 4) {  // the upper macroblock's row 7: dword `lane`, as the H phase stored it
+                const int ya = mby * 8 - 1, cxa = 16 * x + 4 * lane, nva = min(4, max(0, g.width - cxa));
+                sse2(gld4(src_uv + (size_t)ya * pitch + cxa), gld4(UV + (size_t)ya * pitch + cxa), nva, &u, &v);
+            }
+            su += u;
+            sv += v;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        su += __shfl_xor(su, o, 64);
+        sv += __shfl_xor(sv, o, 64);
+    }
+    if (lane == 0) {
+        fs->sse_part[1 * kSsePartStride + mby] = su;
+        fs->sse_part[2 * kSsePartStride + mby] = sv;
+    }
 }
 
 template <int R>
@@ -540,6 +647,7 @@ __device__ void db_luma_row(const Geometry& g, const FrameState* fs, const uint4
         g_db_waits[0][mby][2] = w_glb;
     }
     if (lane == 0) lds_store(cons_me, mb_w + 1);
+    db_luma_sse(g, fs, rec, G.src_y, mby, lane);
 }
 
 // ---------------------------------------------------------------- chroma row engine
@@ -715,6 +823,7 @@ __device__ void db_chroma_row(const Geometry& g, const FrameState* fs, const uin
         g_db_waits[1][mby][2] = w_glb;
     }
     if (lane == 0) lds_store(cons_me, mb_w + 1);
+    db_chroma_sse(g, fs, rec, G.src_uv, mby, lane);
 }
 
 template <int R>
@@ -759,54 +868,6 @@ __global__ __launch_bounds__(64 * R) void k_deblock(Geometry g, const FrameState
     }
 }
 
-// Distortion of the filtered picture: one workgroup per MB row, partials Y, U, V, Y outside the
-// quality mask (sse_part[c][row]; k_scan_rows takes mb_h partials when the filter is on).
-__global__ __launch_bounds__(256) void k_db_sse(Geometry g, const FrameState* __restrict__ fs,
-                                                const uint8_t* __restrict__ src_y, const uint8_t* __restrict__ src_uv) {
-    const int mby = blockIdx.x;
-    unsigned long long sy = 0, su = 0, sv = 0, sm = 0;
-    const int nchunk = g.mb_w * 16;  // 4-byte chunks in 16 rows of a MB row (luma)
-    for (int c = threadIdx.x; c < nchunk * 4; c += 256) {
-        const int row = c / (g.mb_w * 4), x4 = (c % (g.mb_w * 4)) * 4;
-        const int yy = mby * 16 + row;
-        if (yy >= g.height || x4 >= g.width) continue;
-        const uint32_t a = *reinterpret_cast<const uint32_t*>(src_y + (size_t)yy * g.pitch + x4);
-        const uint32_t b = *reinterpret_cast<const uint32_t*>(fs->rec_y + (size_t)yy * g.pitch + x4);
-        unsigned s = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int d = (int)((a >> (8 * k)) & 0xff) - (int)((b >> (8 * k)) & 0xff);
-            s += (x4 + k < g.width) ? (unsigned)(d * d) : 0u;
-        }
-        sy += s;
-        if (mb_unmasked(fs, x4 >> 4, mby)) sm += s;
-    }
-    for (int c = threadIdx.x; c < g.mb_w * 4 * 8; c += 256) {  // 8 chroma rows, 4-byte chunks (2 U + 2 V)
-        const int row = c / (g.mb_w * 4), x4 = (c % (g.mb_w * 4)) * 4;
-        const int yy = mby * 8 + row;
-        if (2 * yy >= g.height || x4 >= g.width) continue;
-        const uint32_t a = *reinterpret_cast<const uint32_t*>(src_uv + (size_t)yy * g.pitch + x4);
-        const uint32_t b = *reinterpret_cast<const uint32_t*>(fs->rec_uv + (size_t)yy * g.pitch + x4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int d = (int)((a >> (8 * k)) & 0xff) - (int)((b >> (8 * k)) & 0xff);
-            const unsigned e = (x4 + k < g.width) ? (unsigned)(d * d) : 0u;
-            if (k & 1) sv += e; else su += e;
-        }
-    }
-    __shared__ unsigned long long part[4][4];
-    unsigned long long v[4] = {sy, su, sv, sm};
-    for (int c = 0; c < 4; ++c)
-        for (int o = 32; o > 0; o >>= 1) v[c] += __shfl_xor(v[c], o, 64);
-    if ((threadIdx.x & 63) == 0)
-        for (int c = 0; c < 4; ++c) part[c][threadIdx.x >> 6] = v[c];
-    __syncthreads();
-    if (threadIdx.x < 4) {
-        const int c = threadIdx.x;
-        fs->sse_part[c * kSsePartStride + mby] = part[c][0] + part[c][1] + part[c][2] + part[c][3];
-    }
-}
-
 }  // namespace
 
 std::vector<unsigned long long> deblock_row_stamps(int mb_h) {
@@ -836,7 +897,7 @@ void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* sr
                     hipStream_t stream) {
     if (g.mb_w > kDbMaxW || g.mb_h > kMaxSlices) throw std::invalid_argument("launch_deblock: picture too large");
     hipLaunchKernelGGL(k_db_prep, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, b.mb, b.db_rec, b.db_rowq);
-    DbGlobal G{b.db_glb, b.db_err};
+    DbGlobal G{b.db_glb, b.db_err, src_y, src_uv};
     static const int rows = [] {
         const char* e = std::getenv("MXDESK_DB_ROWS");
         return e && std::atoi(e) == 8 ? 8 : (e && std::atoi(e) == 4 ? 4 : kDbRowsDefault);
@@ -845,7 +906,7 @@ void launch_deblock(const Geometry& g, const DeviceBuffers& b, const uint8_t* sr
         hipLaunchKernelGGL(k_deblock<8>, dim3((g.mb_h + 7) / 8, 2), dim3(64 * 8), 0, stream, g, b.fs, b.db_rec, b.db_rowq, G);
     else
         hipLaunchKernelGGL(k_deblock<4>, dim3((g.mb_h + 3) / 4, 2), dim3(64 * 4), 0, stream, g, b.fs, b.db_rec, b.db_rowq, G);
-    hipLaunchKernelGGL(k_db_sse, dim3(g.mb_h), dim3(256), 0, stream, g, b.fs, src_y, src_uv);
+    // (the filtered picture's distortion is summed by k_deblock's row waves: no k_db_sse pass)
 }
 
 }  // namespace h264

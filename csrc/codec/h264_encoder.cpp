@@ -2,6 +2,8 @@
 // the CPU encoder.  See h264_gpu.h for the kernel chain.
 #include "h264_encoder.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -281,6 +283,7 @@ void GpuH264Encoder::alloc_slot(FrameSlot& sl) {
     HIP_CHECK(hipEventCreateWithFlags(&sl.analysis_done, kDeviceEvent));
     HIP_CHECK(hipEventCreateWithFlags(&sl.deblock_done, kDeviceEvent));
     HIP_CHECK(hipEventCreateWithFlags(&sl.hpel_done, kDeviceEvent));
+    HIP_CHECK(hipEventCreateWithFlags(&sl.me_done, kDeviceEvent));
     HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
 }
 
@@ -294,7 +297,7 @@ void GpuH264Encoder::free_slot(FrameSlot& sl) {
     if (b.db_err) (void)hipHostFree(b.db_err);
     if (sl.fs_host) (void)hipHostFree(sl.fs_host);
     if (sl.host_out) (void)hipHostFree(sl.host_out);
-    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.deblock_done, sl.done, sl.hpel_done})
+    for (hipEvent_t e : {sl.start, sl.analysis_done, sl.deblock_done, sl.done, sl.hpel_done, sl.me_done})
         if (e) (void)hipEventDestroy(e);
 }
 
@@ -339,6 +342,8 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
     hp_pitch_ = (geom_.coded_w + 2 * kHpelPad + 255) & ~255;
     const size_t hp_bytes = (size_t)hp_pitch_ * (geom_.coded_h + 2 * kHpelPad);
     for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hp_[i], hp_bytes));
+    if (cfg_.h264_deblock())
+        for (int i = 0; i < 4; ++i) HIP_CHECK(hipMalloc(&hpu_[i], hp_bytes));
     for (int i = 0; i < depth_; ++i) alloc_slot(slots_[i]);
     clock_khz_ = device_clock_khz();
     if (depth_ > 1) {
@@ -346,6 +351,24 @@ GpuH264Encoder::GpuH264Encoder(const EncoderConfig& cfg, hipStream_t stream)
         HIP_CHECK(hipStreamCreateWithFlags(&stream_a_, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&ref_ready_, kDeviceEvent));
         HIP_CHECK(hipEventRecord(ref_ready_, stream_));
+        if (cfg_.h264_deblock()) {
+            // The side-stream search may keep every CU busy just as the previous picture's
+            // k_deblock starts: MXDESK_ME_CU_RESERVE=n (default 0) keeps the search off n compute
+            // units (a CU mask on its stream), so the filter's row waves find CUs of their own
+            const char* rv = std::getenv("MXDESK_ME_CU_RESERVE");
+            const int reserve = rv ? std::atoi(rv) : 0;
+            int ncu = 0;
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+            if (reserve > 0 && reserve < ncu) {
+                std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+                for (int c = 0; c < ncu - reserve; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+                HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_m_, (uint32_t)mask.size(), mask.data()));
+            } else {
+                HIP_CHECK(hipStreamCreateWithFlags(&stream_m_, hipStreamNonBlocking));
+            }
+            HIP_CHECK(hipEventCreateWithFlags(&ev_hpu_, kDeviceEvent));
+            HIP_CHECK(hipEventRecord(ev_hpu_, stream_));
+        }
     }
     HIP_CHECK(hipStreamSynchronize(stream_));
     const char* et = std::getenv("MXDESK_ENTROPY_THREAD");
@@ -427,6 +450,13 @@ GpuH264Encoder::~GpuH264Encoder() {
         (void)hipStreamDestroy(stream_a_);
     }
     if (ref_ready_) (void)hipEventDestroy(ref_ready_);
+    if (stream_m_) {
+        (void)hipStreamSynchronize(stream_m_);
+        (void)hipStreamDestroy(stream_m_);
+    }
+    if (ev_hpu_) (void)hipEventDestroy(ev_hpu_);
+    for (int i = 0; i < 4; ++i)
+        if (hpu_[i]) (void)hipFree(hpu_[i]);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(rec_y_[i]);
         (void)hipFree(rec_uv_[i]);
@@ -457,6 +487,18 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
             return e && std::string(e) == "early";
         }();
         if (early) wait_input();
+        // the search of a picture whose reference was deblocked reads that reference's unfiltered
+        // planes (hpu_): on the side stream, it overlaps the reference's k_deblock
+        const bool side_me = stream_m_ && pub && sl.me_unf;
+        if (side_me) {
+            HIP_CHECK(hipStreamWaitEvent(stream_m_, ev_hpu_, 0));
+            if (in_ev_) {
+                HIP_CHECK(hipStreamWaitEvent(stream_m_, in_ev_, 0));
+                in_ev_ = nullptr;  // the analysis stream waits for the search, so for the input too
+            }
+            launch_me(geom_, sl.buf, src_y, stream_m_, pub);
+            HIP_CHECK(hipEventRecord(sl.me_done, stream_m_));
+        }
         if (stream_a_ && hpel_side_ && pub && ref_seq_ + 1 == seq_) {  // the previous picture recorded ref_ready_
             HIP_CHECK(hipStreamWaitEvent(stream_a_, ref_ready_, 0));
             launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_a_, pub);
@@ -466,7 +508,10 @@ void GpuH264Encoder::enqueue_analysis_kernels(bool idr, const uint8_t* src_y, co
             launch_hpel(geom_, sl.buf, hp_, hp_pitch_, stream_, pub);
         }
         wait_input();
-        launch_me(geom_, sl.buf, src_y, stream_);
+        if (side_me)
+            HIP_CHECK(hipStreamWaitEvent(stream_, sl.me_done, 0));
+        else
+            launch_me(geom_, sl.buf, src_y, stream_);
         launch_inter(geom_, sl.buf, src_y, src_uv, stream_);
         if (cfg_.intra_in_p) launch_intra_in_p(geom_, sl.buf, src_y, src_uv, stream_);
     }
@@ -486,6 +531,13 @@ void GpuH264Encoder::enqueue_entropy() {
     launch_entropy(geom_, sl.buf, sl.host_out, stream_e_ ? stream_e_ : stream_, nullptr);
 }
 
+void GpuH264Encoder::unfiltered_planes(FrameSlot& sl) {
+    // F/H/V/J planes of this picture's reconstruction before k_deblock filters it in place: the
+    // next picture's motion search (FrameState::me_*) reads them on the side stream
+    launch_hpel_of(geom_, sl.fs_host->rec_y, hpu_, hp_pitch_, stream_);
+    if (stream_m_) HIP_CHECK(hipEventRecord(ev_hpu_, stream_));
+}
+
 void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8_t* src_uv, bool publish) {
     FrameSlot& sl = slots_[prep_slot_];
     enqueue_analysis_kernels(idr, src_y, src_uv, publish);
@@ -494,6 +546,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
         HIP_CHECK(hipEventRecord(sl.analysis_done, stream_));
         hipEvent_t sse_ready = nullptr;
         if (sl.deblock) {
+            unfiltered_planes(sl);
             launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
             HIP_CHECK(hipEventRecord(sl.deblock_done, stream_));
             sse_ready = sl.deblock_done;
@@ -517,6 +570,7 @@ void GpuH264Encoder::enqueue_kernels(bool idr, const uint8_t* src_y, const uint8
     hipEvent_t sse_ready = nullptr;
     if (sl.deblock) {  // in-loop filter on the analysis stream: the next frame predicts from it,
                          // while this frame's CAVLC runs beside it on the entropy stream
+        unfiltered_planes(sl);
         launch_deblock(geom_, sl.buf, src_y, src_uv, stream_);
         if (stream_e_) {
             HIP_CHECK(hipEventRecord(sl.deblock_done, stream_));
@@ -566,6 +620,10 @@ void GpuH264Encoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.hp_h = hp_[1] + org;
     f.hp_v = hp_[2] + org;
     f.hp_j = hp_[3] + org;
+    f.me_f = sl.me_unf ? hpu_[0] + org : nullptr;
+    f.me_h = sl.me_unf ? hpu_[1] + org : nullptr;
+    f.me_v = sl.me_unf ? hpu_[2] + org : nullptr;
+    f.me_j = sl.me_unf ? hpu_[3] + org : nullptr;
     f.sse_part = sl.buf.sse_part;
     f.prev_src = src_keep_[ref];
     f.save_src = src_keep_[cur];
@@ -578,6 +636,7 @@ int GpuH264Encoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     prep_slot_ = 0;
     FrameSlot& sl = slots_[0];
     sl.deblock = cfg_.deblock == 1;
+    sl.me_unf = false;
     fill_state(sl, true, qp, cur_ ^ 1, cur_);
     sl.fs_host->frame_num = 0;
     sl.fs_host->idr_pic_id = 0;
@@ -607,7 +666,9 @@ bool GpuH264Encoder::prepare(bool force_idr) {
     const int ref = cur_;
     cur_ ^= 1;
     sl.fidx = seq_;
+    sl.me_unf = !idr && last_deblock_;
     sl.deblock = db_lag_.decide((long long)seq_, idr);
+    last_deblock_ = sl.deblock;
     fill_state(sl, idr, sl.qp, ref, cur_);
     return idr;
 }

@@ -289,12 +289,15 @@ class GpuH264Encoder final : public VideoEncoder {
         hipEvent_t hpel_done = nullptr;
         bool idr = false;
         bool deblock = false;  // the picture's in-loop filter (decided when it is prepared)
+        bool me_unf = false;   // the reference was deblocked: the search uses its unfiltered planes (hpu_)
         int qp = 0;
         uint64_t fidx = 0;     // picture number (seq_ when prepared)
+        hipEvent_t me_done = nullptr;  // the side-stream motion search of this picture
     };
     void alloc_slot(FrameSlot& sl);
     void free_slot(FrameSlot& sl);
     void fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cur);
+    void unfiltered_planes(FrameSlot& sl);
     int probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int qp);
     // Entropy launcher (depth > 1, eager launches): a thread issues each frame's entropy chain --
     // the wait for its analysis, the CAVLC / scan / pack launches and its completion event, all
@@ -342,6 +345,14 @@ class GpuH264Encoder final : public VideoEncoder {
     uint64_t last_t_end_ = 0;   // device clock at the end of the last collected frame
     double clock_khz_ = 100000;  // device wall-clock rate
     uint8_t* hp_[4] = {nullptr, nullptr, nullptr, nullptr};  // padded F/H/V/J reference planes
+    // With the in-loop filter on, the motion search of picture n+1 reads the F/H/V/J planes of
+    // picture n's reconstruction before the filter (hpu_, k_hpel right after the reconstruction)
+    // and runs on stream_m_ beside picture n's k_deblock; the analysis stream waits for it only
+    // before k_inter_encode (whose prediction uses the filtered planes hp_)
+    uint8_t* hpu_[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t stream_m_ = nullptr;
+    hipEvent_t ev_hpu_ = nullptr;  // hpu_ of the last deblocked picture written
+    bool last_deblock_ = false;    // the last prepared picture is deblocked
     int hp_pitch_ = 0;
     uint8_t* rec_y_[2] = {nullptr, nullptr};
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
@@ -383,6 +394,8 @@ class CpuH264Encoder {
     void decide_deblock();
     void update_deblock_decision();
     bool deblock_now_ = false;
+    bool ref_deblocked_ = false;       // the reference picture was deblocked: search its unfiltered copy
+    std::vector<uint8_t> rec_unf_y_;   // the last picture's luma reconstruction before the filter
     DbLagDecision db_lag_;
     uint64_t enc_seq_ = 0;  // pictures encoded (the GPU encoder's seq_)
     DbAutoCounts db_counts_;

@@ -101,6 +101,14 @@ struct FrameState {
     const uint8_t* hp_h;  // horizontal half sample b at (x+1/2, y)
     const uint8_t* hp_v;  // vertical half sample h at (x, y+1/2)
     const uint8_t* hp_j;  // centre half sample j at (x+1/2, y+1/2)
+    // motion-search planes (k_me_full): the padded F / H / V / J planes of the reference picture's
+    // reconstruction BEFORE its in-loop filter when that picture was deblocked -- the next
+    // picture's search then depends only on the reconstruction, not on the filter, and runs beside
+    // it on another stream (profiles/r06_deblock) -- nullptr: the hp_* planes
+    const uint8_t* me_f;
+    const uint8_t* me_h;
+    const uint8_t* me_v;
+    const uint8_t* me_j;
     // distortion partials (Y, U, V, Y outside the mask MBs) over the display area, [4][kSsePartStride]: one per
     // inter workgroup / intra MB row, reduced by k_scan into OutHeader (no atomics)
     unsigned long long* sse_part;
@@ -171,7 +179,13 @@ struct DeviceBuffers {
 };
 
 // Kernel launchers (h264_kernels.hip).  All enqueue on `stream`; no host sync.
-void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream);
+// state: the frame state by value (the search runs on a side stream before the analysis stream's
+// first kernel has published it), or nullptr to read the published copy
+void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream,
+               const FrameState* state = nullptr);
+// F / H / V / J planes of an explicit luma picture (the unfiltered reconstruction of a picture the
+// in-loop filter is about to modify), for the next picture's motion search (FrameState::me_*)
+void launch_hpel_of(const Geometry& g, const uint8_t* luma, uint8_t* const planes[4], int hp_pitch, hipStream_t stream);
 void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                   hipStream_t stream);
 // The first kernel of a frame (launch_intra for I, launch_hpel for P) publishes the frame

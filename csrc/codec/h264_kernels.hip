@@ -109,6 +109,10 @@ struct Planes {
 __device__ __forceinline__ Planes planes_of(const FrameState* fs) {
     return Planes{fs->hp_f, fs->hp_h, fs->hp_v, fs->hp_j, fs->hp_pitch};
 }
+// the motion search's planes (FrameState::me_*: the reference's unfiltered reconstruction)
+__device__ __forceinline__ Planes me_planes_of(const FrameState* fs) {
+    return fs->me_f ? Planes{fs->me_f, fs->me_h, fs->me_v, fs->me_j, fs->hp_pitch} : planes_of(fs);
+}
 // Quarter-sample luma value from the precomputed planes (Table 8-12); identical to
 // luma_qpel() on the clamped reference.
 __device__ __forceinline__ int qpel_planes(const Planes& P, int x4, int y4) {
@@ -175,11 +179,12 @@ __device__ __forceinline__ const FrameState& state_of(const StateArg& a) { retur
 
 __global__ __launch_bounds__(256) void k_hpel(Geometry g, StateArg sa, uint8_t* __restrict__ pf,
                                               uint8_t* __restrict__ ph, uint8_t* __restrict__ pv,
-                                              uint8_t* __restrict__ pj, int hp_pitch) {
+                                              uint8_t* __restrict__ pj, int hp_pitch,
+                                              const uint8_t* __restrict__ src) {
     __shared__ uint32_t smp[kHpTH + 5][kHpSW / 4];
     __shared__ int4 b1[kHpTH + 5][kHpTW / 4];  // 4 columns per entry
     publish_state(sa);
-    const uint8_t* __restrict__ ref = state_of(sa).ref_y;
+    const uint8_t* __restrict__ ref = src ? src : state_of(sa).ref_y;  // src: an explicit picture
     const int px0 = blockIdx.x * kHpTW, py0 = blockIdx.y * kHpTH;  // padded-plane coordinates
     const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
     const int tid = threadIdx.x;
@@ -290,8 +295,8 @@ constexpr int kWinStride = 16 + 2 * kMaxRange + 8;  // bytes per LDS window row 
 // of 1.16 passes of 256 -- measured slower: 45 -> 54 us at 1080p, 78 -> 110 us at 4K, the larger
 // workgroups costing more in occupancy than the shorter second pass saved: profiles/r04_h264.)
 constexpr int kMeThreads = 256, kMeWaves = kMeThreads / 64;
-__global__ __launch_bounds__(kMeThreads) void k_me_full(Geometry g, const FrameState* __restrict__ fs,
-                                                  const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs) {
+__device__ __forceinline__ void me_full_body(const Geometry& g, const FrameState* __restrict__ fs,
+                                             const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs) {
     __shared__ uint32_t win32[(16 + 2 * kMaxRange) * kWinStride / 4];
     __shared__ uint32_t srcw[64];
     __shared__ unsigned long long red[kMeWaves];
@@ -304,7 +309,7 @@ __global__ __launch_bounds__(kMeThreads) void k_me_full(Geometry g, const FrameS
     const int tid = threadIdx.x, lane = tid & 63;
     const int R = me_range(fs->search_range);
     const int W = 16 + 2 * R;
-    const Planes P = planes_of(fs);
+    const Planes P = me_planes_of(fs);  // the unfiltered reference when it was deblocked
     const int lambda = lambda_sad(fs->qp);
 
     // static-block early exit first: SAD of the zero vector from one source and one reference
@@ -700,6 +705,18 @@ __global__ __launch_bounds__(kMeThreads) void k_me_full(Geometry g, const FrameS
         m.part = kPart16x16;
         m.pmv[0] = m.pmv[1] = m.pmv[2] = m.pmv[3] = 0;
     }
+}
+
+// The search reads the published frame state (the analysis stream's first kernel wrote it) or,
+// on the side stream beside the previous picture's in-loop filter, a copy passed by value
+// (a separate kernel, so the common launch keeps its small argument block)
+__global__ __launch_bounds__(kMeThreads) void k_me_full(Geometry g, const FrameState* __restrict__ fs,
+                                                  const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs) {
+    me_full_body(g, fs, src_y, mbs);
+}
+__global__ __launch_bounds__(kMeThreads) void k_me_full_val(Geometry g, FrameState fs,
+                                                      const uint8_t* __restrict__ src_y, MbInfo* __restrict__ mbs) {
+    me_full_body(g, &fs, src_y, mbs);
 }
 
 // ------------------------------------------------------------------ inter encode
@@ -2590,12 +2607,24 @@ void launch_hpel(const Geometry& g, const DeviceBuffers& b, uint8_t* const plane
     sa.publish = publish ? 1 : 0;
     sa.t_start = b.out_hdr ? &b.out_hdr->t_start : nullptr;
     hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, sa, planes[0], planes[1], planes[2], planes[3],
-                       hp_pitch);
+                       hp_pitch, (const uint8_t*)nullptr);
 }
 
-void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream) {
+void launch_hpel_of(const Geometry& g, const uint8_t* luma, uint8_t* const planes[4], int hp_pitch, hipStream_t stream) {
+    const int W = g.coded_w + 2 * kHpelPad, H = g.coded_h + 2 * kHpelPad;
+    dim3 grid((W + kHpTW - 1) / kHpTW, (H + kHpTH - 1) / kHpTH);
+    StateArg sa{};  // no state: the picture is given
+    hipLaunchKernelGGL(k_hpel, grid, dim3(256), 0, stream, g, sa, planes[0], planes[1], planes[2], planes[3], hp_pitch,
+                       luma);
+}
+
+void launch_me(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, hipStream_t stream,
+               const FrameState* state) {
     const int nmb = g.mb_w * g.mb_h;
-    hipLaunchKernelGGL(k_me_full, dim3(nmb), dim3(kMeThreads), 0, stream, g, b.fs, src_y, b.mb);
+    if (state)
+        hipLaunchKernelGGL(k_me_full_val, dim3(nmb), dim3(kMeThreads), 0, stream, g, *state, src_y, b.mb);
+    else
+        hipLaunchKernelGGL(k_me_full, dim3(nmb), dim3(kMeThreads), 0, stream, g, b.fs, src_y, b.mb);
 }
 
 void launch_inter(const Geometry& g, const DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,

@@ -1154,31 +1154,45 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
     const int sdc = wsum(lane < 16 ? R.L[1 + lane] + R.T[1 + lane] : 0);
     if (lane == 0) R.dc = (sdc + 16) >> 5;
     wave_lds_sync();
-    // this lane: row r, columns cb .. cb + 3; a 4x4 block's rows sit in lanes ^4 / ^8
-    const int r = lane >> 2, cb = (lane & 3) * 4;
+    // 4x4 Hadamard SATD of all sixteen 4x4 blocks of the unit on the matrix cores: with the
+    // residual R (16 x 16) and H16 = diag(H4, H4, H4, H4) (H4 the order-4 Hadamard matrix,
+    // symmetric), S = H16 R H16 holds every block's transform, SATD = sum |S|.  Two
+    // v_mfma_f32_16x16x16_f16 per mode: T = R H16 (A = R), then S = H16 T, whose B operand layout
+    // (lane l: rows 4(l>>4)..+3 of column l&15) is exactly T's accumulator layout, so T goes
+    // across as four f16 conversions.  Exact: |R| <= 255 and |T| <= 1020 are integers f16 holds,
+    // S (<= 4080) accumulates in f32.  The lane computes the residual of row l & 15, columns
+    // 4 (l >> 4) .. + 3 -- the A operand's layout.
+    typedef _Float16 mf_h4 __attribute__((ext_vector_type(4)));
+    typedef float mf_f4 __attribute__((ext_vector_type(4)));
+    const int r = lane & 15, cb = (lane >> 4) * 4;
     const uint32_t sw = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + r) * P + x0 + cb);
+    mf_h4 hm;  // H16[l & 15][4 (l >> 4) + j]: the B operand of the first product, the A of the second
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = lane & 15, k = cb + j;
+        // H4[a][b] = (-1)^(popcount(a & b)) for the order a = {++++, +-+-, ++--, +--+}
+        const int sgn = __popc((row & 3) & (k & 3)) & 1 ? -1 : 1;
+        hm[j] = (_Float16)((row >> 2) == (k >> 2) ? sgn : 0);
+    }
+    const mf_f4 zero = {0.f, 0.f, 0.f, 0.f};
     const int lambda = h264::lambda_sad(fs->qp);
     const uint64_t safe = fs->bl_safe;
     int best = 1, best_cost = 0x7fffffff;
 #pragma unroll 1
     for (int m = 0; m < 35; ++m) {
         if (bl_pending && !((safe >> m) & 1)) continue;  // wave-uniform
-        int d[4];
+        mf_h4 a;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            d[j] = (int)((sw >> (8 * j)) & 0xff) - pred_sample(m, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
-        const int a0 = d[0] + d[1], a1 = d[0] - d[1], a2 = d[2] + d[3], a3 = d[2] - d[3];
-        int h[4] = {a0 + a2, a1 + a3, a0 - a2, a1 - a3};
-        int sad = 0;
+            a[j] = (_Float16)((int)((sw >> (8 * j)) & 0xff) -
+                              pred_sample(m, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r));
+        const mf_f4 t = __builtin_amdgcn_mfma_f32_16x16x16f16(a, hm, zero, 0, 0, 0);
+        mf_h4 tb;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            int v = h[k];
-            int o = __shfl_xor(v, 4, 64);
-            v = (lane & 4) ? o - v : v + o;
-            o = __shfl_xor(v, 8, 64);
-            v = (lane & 8) ? o - v : v + o;
-            sad += v < 0 ? -v : v;
-        }
+        for (int i = 0; i < 4; ++i) tb[i] = (_Float16)t[i];
+        const mf_f4 sm = __builtin_amdgcn_mfma_f32_16x16x16f16(hm, tb, zero, 0, 0, 0);
+        const int sad = (int)(__builtin_fabsf(sm[0]) + __builtin_fabsf(sm[1]) + __builtin_fabsf(sm[2]) +
+                              __builtin_fabsf(sm[3]));
         const int cost = wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
         if (cost < best_cost) {
             best_cost = cost;
