@@ -525,7 +525,7 @@ def main() -> None:
 
     barrier()
     t0 = time.perf_counter()
-    lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m, psnr_uv, dbk = [], [], [], [], [], [], [], []
+    lat_ms, sizes, qps, gpu_ms, psnrs, psnrs_m, psnr_uv, dbk, dbc = [], [], [], [], [], [], [], [], []
     if K == 1 and args.depth == 1 and gpu:
         results = [sessions[0].step(False) for _ in range(args.steps)]
     else:
@@ -541,6 +541,7 @@ def main() -> None:
         psnr_uv.append((r.psnr_u, r.psnr_v))
         gpu_ms.append(r.gpu_ms)
         dbk.append(getattr(r, "deblocked", 0))
+        dbc.append((getattr(r, "db_coherent", 0), getattr(r, "db_moving", 0)))
 
     quality = None
     if args.quality_probe > 0 and rank == 0 and not args.out_width:
@@ -609,6 +610,10 @@ def main() -> None:
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
             "deblocked_frames_pct": round(100.0 * sum(dbk) / max(1, len(dbk)), 1),
+            # the adaptive filter's inputs (h264_deblock.h db_auto_decide): mean coherent / moving
+            # macroblocks per picture
+            "db_classes_mean": [round(statistics.mean(c for c, _ in dbc), 1), round(statistics.mean(m for _, m in dbc), 1)]
+            if dbc else None,
             "mean_gpu_encode_ms": round(statistics.mean(gpu_ms), 3),
             "mean_bitrate_kbps_at_60fps": round(kbps, 1),
             "mean_qp": round(statistics.mean(qps), 2),

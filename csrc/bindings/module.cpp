@@ -156,6 +156,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("pipeline_depth", &h264::EncoderConfig::pipeline_depth)
         .def_readwrite("aq", &h264::EncoderConfig::aq)
         .def_readwrite("intra_in_p", &h264::EncoderConfig::intra_in_p)
+        .def_readwrite("vp8_bpred", &h264::EncoderConfig::vp8_bpred)
+        .def_readwrite("vp8_intra", &h264::EncoderConfig::vp8_intra)
         .def_readwrite("mask_x0", &h264::EncoderConfig::mask_x0)
         .def_readwrite("mask_y0", &h264::EncoderConfig::mask_y0)
         .def_readwrite("mask_x1", &h264::EncoderConfig::mask_x1)
@@ -678,6 +680,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readonly("psnr_v", &FrameResult::psnr_v)
         .def_readonly("psnr_y_masked", &FrameResult::psnr_y_masked)
         .def_readonly("deblocked", &FrameResult::deblocked)
+        .def_readonly("db_coherent", &FrameResult::db_coherent)
+        .def_readonly("db_moving", &FrameResult::db_moving)
         .def_property_readonly("au", [](const FrameResult& r) { return to_bytes(r.au); });
 
     m.def(

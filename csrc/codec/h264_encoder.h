@@ -80,6 +80,10 @@ struct EncoderConfig {
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: it costs -35 % fps on the 1080p desktop (k_intra_analyze + k_intra_p on
                               // the analysis queue, profiles/r04_toolset/NOTES.md)
+    int vp8_intra = 1;        // VP8 inter frames: intra macroblocks (two parallel passes, vp8_core.h
+                              // vp8_intra_candidate)
+    int vp8_bpred = 1;        // VP8 key frames: macroblocks may take B_PRED (16 4x4 sub-block modes, vp8_core.h
+                              // bpred_luma) when its SAD + lambda * mode bits beat the 16x16 mode's
     int tu_split = 2;         // HEVC: inter transform trees may split into 8x8 luma / 4x4 chroma TUs (1), and each
                               // 8x8 luma node again into four 4x4 TUs (2), per node by SSE + lambda * bits
     int hevc_slice_cost = 1536;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)

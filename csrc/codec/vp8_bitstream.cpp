@@ -120,6 +120,39 @@ void put_block(Enc& e, const int16_t* lv, int first, int type, int ctx) {
 
 inline int nzb(const Vp8Mb& m, int b) { return (m.nz >> b) & 1; }
 
+// A sub-block mode through the bmode tree (11.2; bmode_cost256 walks the same branches).
+template <class Enc>
+void put_bmode(Enc& e, int m, const uint8_t* p) {
+    e.put(p[0], m != kBDc);
+    if (m == kBDc) return;
+    e.put(p[1], m != kBTm);
+    if (m == kBTm) return;
+    e.put(p[2], m != kBVe);
+    if (m == kBVe) return;
+    const bool far = !(m == kBHe || m == kBRd || m == kBVr);
+    e.put(p[3], far);
+    if (!far) {
+        e.put(p[4], m != kBHe);
+        if (m != kBHe) e.put(p[5], m == kBVr);
+        return;
+    }
+    e.put(p[6], m != kBLd);
+    if (m == kBLd) return;
+    e.put(p[7], m != kBVl);
+    if (m != kBVl) e.put(p[8], m == kBHu);
+}
+
+// Y2 "above" context of macroblock (mbx, mby): the Y2 block's non-zero bit of the nearest macroblock
+// above with a Y2 block -- B_PRED macroblocks have none and leave the column's context as it was
+// (a skipped 16x16 macroblock resets it: its nz bits are 0)
+inline int y2_above(const Vp8Mb* mbs, int mb_w, int mbx, int mby) {
+    for (int y = mby - 1; y >= 0; --y) {
+        const Vp8Mb& u = mbs[y * mb_w + mbx];
+        if (u.ymode != kBPred) return nzb(u, kY2);
+    }
+    return 0;
+}
+
 // Token partition `p`: MB rows p, p + n, ...
 template <class Enc>
 void code_tokens(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const int16_t*(int)>& levels, int p, int n,
@@ -129,22 +162,23 @@ void code_tokens(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         for (int mbx = 0; mbx < f.mb_w; ++mbx) {
             const int i = mby * f.mb_w + mbx;
             const Vp8Mb& m = mbs[i];
-            if (m.nz == 0) {  // mb_skip_coeff: no tokens, contexts reset (the MB has a Y2 block)
-                for (int& l : left) l = 0;
+            const bool y2 = m.ymode != kBPred;
+            if (m.nz == 0) {  // mb_skip_coeff: no tokens, contexts reset (Y2's only with a Y2 block)
+                for (int k = 0; k < 8; ++k) left[k] = 0;
+                if (y2) left[8] = 0;
                 continue;
             }
             const Vp8Mb* up = mby > 0 ? &mbs[i - f.mb_w] : nullptr;
             const int16_t* lv = levels(i);
-            // Y2 (type 1)
-            {
-                const int ctx = (up ? nzb(*up, kY2) : 0) + left[8];
+            if (y2) {  // Y2 (type 1)
+                const int ctx = y2_above(mbs, f.mb_w, mbx, mby) + left[8];
                 put_block(e, lv + kY2 * 16, 0, 1, ctx);
                 left[8] = nzb(m, kY2);
             }
-            for (int b = 0; b < 16; ++b) {  // Y after Y2 (type 0, from coefficient 1)
+            for (int b = 0; b < 16; ++b) {  // Y: after Y2 type 0 from coefficient 1; B_PRED type 3 from 0
                 const int bx = b & 3, by = b >> 2;
                 const int above = by > 0 ? nzb(m, b - 4) : (up ? nzb(*up, 12 + bx) : 0);
-                put_block(e, lv + b * 16, 1, 0, above + left[by]);
+                put_block(e, lv + b * 16, y2 ? 1 : 0, y2 ? 0 : 3, above + left[by]);
                 left[by] = nzb(m, b);
             }
             for (int c = 0; c < 2; ++c)
@@ -275,9 +309,14 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                  const std::function<void(int, const std::function<void(int)>&)>& run_parallel, TokenStats* stats) {
     const int nmb = f.mb_w * f.mb_h;
     const int nparts = 1 << f.log2_parts;
-    int coded = 0;
-    for (int i = 0; i < nmb; ++i) coded += mbs[i].nz != 0;
+    int coded = 0, intra = 0;
+    for (int i = 0; i < nmb; ++i) {
+        coded += mbs[i].nz != 0;
+        intra += mbs[i].ymode != kInter;
+    }
     const int prob_skip_false = std::clamp((coded * 256 + nmb / 2) / std::max(1, nmb), 1, 255);
+    // inter frames: the probability of an intra macroblock (intra_pass), from this frame's count
+    const int prob_intra = std::clamp((intra * 256 + nmb / 2) / std::max(1, nmb), 1, 255);
     // segment tree probabilities (9.3, mb_segment_tree {2, 4, -0, -1, -2, -3}) from this frame's
     // segment histogram: p0 = P(segment < 2), p1 = P(1 | < 2), p2 = P(3 | >= 2)
     int seg_n[kNumSegs] = {0, 0, 0, 0};
@@ -354,7 +393,7 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
         }
         e.literal(1, 1);  // mb_no_skip_coeff
         e.literal((uint32_t)prob_skip_false, 8);
-        const int prob_intra = 1, prob_last = 255, prob_gf = 128;
+        const int prob_last = 255, prob_gf = 128;
         if (!f.key) {
             e.literal(prob_intra, 8);
             e.literal(prob_last, 8);
@@ -375,9 +414,18 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                 e.put(prob_skip_false, m.nz == 0);
                 if (f.key) {
                     const uint8_t* p = kKfYModeProb;  // tree: B_PRED "0", DC "100", V "101", H "110", TM "111"
-                    e.put(p[0], 1);
-                    e.put(p[1], m.ymode >= kHPred);
-                    e.put(m.ymode >= kHPred ? p[3] : p[2], m.ymode == kVPred || m.ymode == kTmPred);
+                    e.put(p[0], m.ymode != kBPred);
+                    if (m.ymode == kBPred) {  // 16 sub-block modes under their above / left contexts
+                        for (int b = 0; b < 16; ++b) {
+                            const int bx = b & 3, by = b >> 2;
+                            const int a = by > 0 ? bmode_of(m, b - 4) : bctx_above(mbs, f.mb_w, mbx, mby, bx);
+                            const int l = bx > 0 ? bmode_of(m, b - 1) : bctx_left(mbs, f.mb_w, mbx, mby, by);
+                            put_bmode(e, bmode_of(m, b), kKfBModeProb + (a * kNumBModes + l) * 9);
+                        }
+                    } else {
+                        e.put(p[1], m.ymode >= kHPred);
+                        e.put(m.ymode >= kHPred ? p[3] : p[2], m.ymode == kVPred || m.ymode == kTmPred);
+                    }
                     const uint8_t* q = kKfUvModeProb;  // DC "0", V "10", H "110", TM "111"
                     e.put(q[0], m.uvmode != kDcPred);
                     if (m.uvmode != kDcPred) {
@@ -386,7 +434,26 @@ void write_frame(const FrameDesc& f, const Vp8Mb* mbs, const std::function<const
                     }
                     continue;
                 }
-                if (m.ymode != kInter) throw std::logic_error("vp8 writer: intra MB in an inter frame");
+                if (m.ymode != kInter) {  // intra macroblock (16x16 modes): the inter-frame mode trees
+                    if (m.ymode > kTmPred) throw std::logic_error("vp8 writer: B_PRED in an inter frame");
+                    e.put(prob_intra, 0);     // is_inter_mb
+                    const uint8_t* p = kYModeProb;  // DC "0", V "100", H "101", TM "110", B_PRED "111"
+                    e.put(p[0], m.ymode != kDcPred);
+                    if (m.ymode != kDcPred) {
+                        e.put(p[1], m.ymode == kTmPred);
+                        if (m.ymode == kTmPred)
+                            e.put(p[3], 0);
+                        else
+                            e.put(p[2], m.ymode == kHPred);
+                    }
+                    const uint8_t* q = kUvModeProb;  // DC "0", V "10", H "110", TM "111"
+                    e.put(q[0], m.uvmode != kDcPred);
+                    if (m.uvmode != kDcPred) {
+                        e.put(q[1], m.uvmode != kVPred);
+                        if (m.uvmode != kVPred) e.put(q[2], m.uvmode == kTmPred);
+                    }
+                    continue;
+                }
                 e.put(prob_intra, 1);  // is_inter_mb
                 e.put(prob_last, 0);   // reference: last frame
                 if (m.mvx == 0 && m.mvy == 0) {

@@ -8,7 +8,10 @@
 // mxdesk/codec/vp8_decoder.py; key frames are additionally decoded by libwebp through Pillow.
 //
 // Coding subset (what this encoder emits): key frames of 16x16-predicted macroblocks (DC / V / H /
-// TM luma, DC / V / H / TM chroma, Y2 second-order block); inter frames of 16x16 inter macroblocks
+// TM luma, DC / V / H / TM chroma, Y2 second-order block) and B_PRED macroblocks (ten 4x4
+// sub-block modes under the key-frame contexts kKfBModeProb, each sub-block predicted from the
+// ones reconstructed before it, no Y2 block), chosen per macroblock by prediction SAD plus
+// lambda * mode bits; inter frames of 16x16 inter macroblocks
 // predicting from the last frame with quarter-sample vectors (ZEROMV / NEARESTMV / NEARMV / NEWMV);
 // inter frames segmented (9.3) by the temporal classes of the H.264 encoder's adaptive
 // quantisation -- four segment quantisers, a per-macroblock segment map -- key frames one
@@ -31,12 +34,17 @@ constexpr int kBlocks = 25;        // 16 Y, 4 U, 4 V, Y2
 constexpr int kCoefPerMb = 25 * 16;  // int16 levels per macroblock, zigzag (scan) order per block
 constexpr int kY2 = 24;
 
-enum YMode : uint8_t { kDcPred = 0, kVPred = 1, kHPred = 2, kTmPred = 3, kInter = 4 };
+enum YMode : uint8_t { kDcPred = 0, kVPred = 1, kHPred = 2, kTmPred = 3, kInter = 4, kBPred = 5 };
+// B_PRED sub-block modes in the bmode tree's leaf order (= the index order of kKfBModeProb):
+// B_DC "0", B_TM "10", B_VE "110", B_HE "11100", B_RD "111010", B_VR "111011", B_LD "111101",
+// B_VL "1111100", B_HD "11111010", B_HU "11111011"
+enum BMode : uint8_t { kBDc = 0, kBTm, kBVe, kBHe, kBRd, kBVr, kBLd, kBVl, kBHd, kBHu, kNumBModes };
 enum MvMode : uint8_t { kMvZero = 0, kMvNearest = 1, kMvNear = 2, kMvNew = 3 };
 
 // Per-macroblock record written by the analysis (GPU or CPU), read by the bitstream writer.
 struct Vp8Mb {
-    int16_t mvx, mvy;  // luma vector, 1/8-sample units (even: quarter-sample luma vectors)
+    int16_t mvx, mvy;  // luma vector, 1/8-sample units (even: quarter-sample luma vectors); a key-frame
+                       // B_PRED macroblock (no vector) keeps sub-block modes 0..7 here (bmode_of)
     uint8_t ymode;     // YMode
     uint8_t uvmode;    // DC / V / H / TM
     uint8_t seg;       // segment (Seg; 0 in key frames)
@@ -44,9 +52,24 @@ struct Vp8Mb {
     uint32_t nz;       // bit b: block b (0..24) has a non-zero level
     uint32_t slot;     // GPU: index of the macroblock's levels in the compacted level buffer
     uint32_t sse[3];   // GPU: Y / U / V distortion over the display area
-    uint32_t pad2;
+    uint32_t bmodes_hi;  // B_PRED: sub-block modes 8..15 (4 bits each); inter macroblocks: the luma
+                         // prediction SAD (the intra pass's comparison, vp8_intra_candidate)
 };
 static_assert(sizeof(Vp8Mb) == 32, "Vp8Mb layout");
+// B_PRED sub-block modes, 4 bits each in raster order: 0..7 in the vector fields, 8..15 in bmodes_hi
+MXV8 int bmode_of(const Vp8Mb& m, int b) {
+    const uint32_t w = b < 8 ? ((uint32_t)(uint16_t)m.mvx | ((uint32_t)(uint16_t)m.mvy << 16)) : m.bmodes_hi;
+    return (int)((w >> (4 * (b & 7))) & 15u);
+}
+MXV8 void set_bmodes(Vp8Mb& m, uint32_t lo, uint32_t hi) {
+    m.mvx = (int16_t)(uint16_t)(lo & 0xffffu);
+    m.mvy = (int16_t)(uint16_t)(lo >> 16);
+    m.bmodes_hi = hi;
+}
+// the sub-block mode a 16x16-predicted macroblock stands for as a B_PRED context (11.3)
+MXV8 int implied_bmode(int ymode) {
+    return ymode == kVPred ? kBVe : (ymode == kHPred ? kBHe : (ymode == kTmPred ? kBTm : kBDc));
+}
 
 // zigzag scan -> raster position, coefficient bands (13.3)
 constexpr uint8_t kZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -75,6 +98,10 @@ constexpr uint8_t kModeContexts[6][4] = {{7, 1, 1, 143},     {14, 18, 14, 107}, 
                                          {60, 56, 128, 65},  {159, 134, 128, 34}, {234, 188, 128, 28}};
 
 MXV8 int v8_clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+// -256 log2(p / 256): the cost in 1/256 bit of coding a branch of probability p / 256 (the
+// writer's bit_cost256, as a table both encoders share)
+constexpr uint16_t kProbCost256[256] = {2048, 2048, 1792, 1642, 1536, 1454, 1386, 1329, 1280, 1236, 1198, 1162, 1130, 1101, 1073, 1048, 1024, 1002, 980, 961, 942, 924, 906, 890, 874, 859, 845, 831, 817, 804, 792, 780, 768, 757, 746, 735, 724, 714, 705, 695, 686, 676, 668, 659, 650, 642, 634, 626, 618, 611, 603, 596, 589, 582, 575, 568, 561, 555, 548, 542, 536, 530, 524, 518, 512, 506, 501, 495, 490, 484, 479, 474, 468, 463, 458, 453, 449, 444, 439, 434, 430, 425, 420, 416, 412, 407, 403, 399, 394, 390, 386, 382, 378, 374, 370, 366, 362, 358, 355, 351, 347, 343, 340, 336, 333, 329, 326, 322, 319, 315, 312, 309, 305, 302, 299, 296, 292, 289, 286, 283, 280, 277, 274, 271, 268, 265, 262, 259, 256, 253, 250, 247, 245, 242, 239, 236, 234, 231, 228, 226, 223, 220, 218, 215, 212, 210, 207, 205, 202, 200, 197, 195, 193, 190, 188, 185, 183, 181, 178, 176, 174, 171, 169, 167, 164, 162, 160, 158, 156, 153, 151, 149, 147, 145, 143, 140, 138, 136, 134, 132, 130, 128, 126, 124, 122, 120, 118, 116, 114, 112, 110, 108, 106, 104, 102, 101, 99, 97, 95, 93, 91, 89, 87, 86, 84, 82, 80, 78, 77, 75, 73, 71, 70, 68, 66, 64, 63, 61, 59, 58, 56, 54, 53, 51, 49, 48, 46, 44, 43, 41, 40, 38, 36, 35, 33, 32, 30, 28, 27, 25, 24, 22, 21, 19, 18, 16, 15, 13, 12, 10, 9, 7, 6, 4, 3, 1};
+MXV8 int branch_cost(int prob, int bit) { return (int)kProbCost256[bit ? 256 - prob : prob]; }
 
 // ---------------------------------------------------------------- segments (9.3)
 // Inter-frame segments = the temporal classes of h264_mb.h (temporal_class / aq3_mb_qp): the
@@ -262,6 +289,76 @@ MXV8 int dc_of(const Edge& e, int n) {
     return (s + (1 << (shift - 1))) >> shift;
 }
 
+// ---------------------------------------------------------------- B_PRED sub-blocks (12.3)
+// Neighbours of a 4x4 luma sub-block: A[0..7] the row above (4..7 above-right), L[0..3] the column
+// to the left, P the corner, with VP8's rules: frame edges 127 above / 129 left (the corner 127 in
+// the top row, else 129 in the left column); a macroblock's above-right comes from the row above
+// the macroblock -- the above-right macroblock's bottom row, at the right frame edge the above
+// macroblock's last sample repeated -- and the right column's lower sub-blocks reuse that same
+// above-right (the decoder has not reconstructed anything to their right yet).
+struct SubEdge {
+    int A[8], L[4], P;
+};
+MXV8 int avg2(int a, int b) { return (a + b + 1) >> 1; }
+MXV8 int avg3(int a, int b, int c) { return (a + 2 * b + c + 2) >> 2; }
+// The eight directional modes as 2- / 3-tap averages over one edge array X[15] = L3 L3 L2 L1 L0 P
+// A0 .. A7 A7 (bpred_edge): entry s | 16 is avg3(X[s], X[s+1], X[s+2]), s alone avg2(X[s], X[s+1]),
+// per mode (B_VE .. B_HU) and sample (y * 4 + x) -- the formulas of RFC 6386 12.3 (subblock_intra_predict),
+// tabulated (tools: the table is written out from them; the duplicated L3 / A7 ends give the
+// clamped taps of B_HE / B_HU / B_LD)
+constexpr uint8_t kBPredTap[8][16] = {
+    {21, 22, 23, 24, 21, 22, 23, 24, 21, 22, 23, 24, 21, 22, 23, 24},
+    {19, 19, 19, 19, 18, 18, 18, 18, 17, 17, 17, 17, 16, 16, 16, 16},
+    {20, 21, 22, 23, 19, 20, 21, 22, 18, 19, 20, 21, 17, 18, 19, 20},
+    {5, 6, 7, 8, 20, 21, 22, 23, 19, 5, 6, 7, 18, 20, 21, 22},
+    {22, 23, 24, 25, 23, 24, 25, 26, 24, 25, 26, 27, 25, 26, 27, 28},
+    {6, 7, 8, 9, 22, 23, 24, 25, 7, 8, 9, 26, 23, 24, 25, 27},
+    {4, 20, 21, 22, 3, 19, 4, 20, 2, 18, 3, 19, 1, 17, 2, 18},
+    {3, 18, 2, 17, 2, 17, 1, 16, 1, 16, 0, 0, 0, 0, 0, 0}};
+MXV8 void bpred_edge(const SubEdge& e, int* X) {
+    X[0] = X[1] = e.L[3];
+    X[2] = e.L[2];
+    X[3] = e.L[1];
+    X[4] = e.L[0];
+    X[5] = e.P;
+    for (int i = 0; i < 8; ++i) X[6 + i] = e.A[i];
+    X[14] = e.A[7];
+}
+// predicted sample (x, y) of mode m from the edge array X (bpred_edge)
+MXV8 int bpred_px(int m, const int* X, int x, int y) {
+    if (m == kBDc) return (X[6] + X[7] + X[8] + X[9] + X[1] + X[2] + X[3] + X[4] + 4) >> 3;
+    if (m == kBTm) return v8_clamp255(X[4 - y] + X[6 + x] - X[5]);
+    const int t = kBPredTap[m - 2][y * 4 + x], s = t & 15;
+    return (t & 16) ? (X[s] + 2 * X[s + 1] + X[s + 2] + 2) >> 2 : (X[s] + X[s + 1] + 1) >> 1;
+}
+// Modes this encoder considers for sub-block column bx of macroblock (mbx, mby): in the right column
+// not B_VE / B_LD / B_VL (the modes that read the above-right samples) while those come from the
+// above-right macroblock -- the GPU's row below then never waits for that macroblock (k_vp8_key).
+MXV8 bool bmode_allowed(int m, int bx, int mbx, int mby, int mb_w) {
+    return !(bx == 3 && mby > 0 && mbx + 1 < mb_w && (m == kBVe || m == kBLd || m == kBVl));
+}
+// Cost in 1/256 bit of sub-block mode m in a key frame after above / left modes a / l (the bmode
+// tree under kKfBModeProb[a][l])
+MXV8 int bmode_cost256(int m, int a, int l) {
+    const uint8_t* p = kKfBModeProb + (a * kNumBModes + l) * 9;
+    if (m == kBDc) return branch_cost(p[0], 0);
+    int c = branch_cost(p[0], 1);
+    if (m == kBTm) return c + branch_cost(p[1], 0);
+    c += branch_cost(p[1], 1);
+    if (m == kBVe) return c + branch_cost(p[2], 0);
+    c += branch_cost(p[2], 1);
+    if (m == kBHe || m == kBRd || m == kBVr) {
+        c += branch_cost(p[3], 0);
+        if (m == kBHe) return c + branch_cost(p[4], 0);
+        return c + branch_cost(p[4], 1) + branch_cost(p[5], m == kBVr);
+    }
+    c += branch_cost(p[3], 1);
+    if (m == kBLd) return c + branch_cost(p[6], 0);
+    c += branch_cost(p[6], 1);
+    if (m == kBVl) return c + branch_cost(p[7], 0);
+    return c + branch_cost(p[7], 1) + branch_cost(p[8], m == kBHu);
+}
+
 // ---------------------------------------------------------------- inter prediction (18.3)
 // Six-tap sub-sample filters by 1/8-sample phase; luma vectors are quarter-sample (even phases),
 // chroma vectors (luma / 2) reach every phase.
@@ -288,8 +385,8 @@ MXV8 int chroma_mv(int v) { return (v + (v < 0 ? -1 : 1)) / 2; }
 // ---------------------------------------------------------------- loop filter (15)
 // The normal filter (filter_type 0, sharpness 0, no mode / reference level deltas): per
 // macroblock a level from its segment; macroblock edges take the wide filter (15.3 MB edges),
-// the inner 4x4 edges (only in macroblocks with a non-zero coefficient -- all 16x16-predicted
-// here) the subblock filter.  Arithmetic as libvpx's C reference (the RFC's normative source):
+// the inner 4x4 edges (in macroblocks with a non-zero coefficient, and always in B_PRED
+// macroblocks) the subblock filter.  Arithmetic as libvpx's C reference (the RFC's normative source):
 // the edge test 2|p0-q0| + |p1-q1|/2 <= limit, interior |p_i - p_i+1| <= interior limit, high
 // edge variance |p1-p0| or |q1-q0| above the frame-type threshold.
 struct LfParams {
@@ -399,7 +496,7 @@ inline void loop_filter_frame(uint8_t* y, uint8_t* uv, int pitch, int mb_w, int 
             const int level = levels[m.seg & 3];
             if (!level) continue;
             const LfParams f = lf_params(level, key);
-            const bool inner = m.nz != 0;
+            const bool inner = m.nz != 0 || m.ymode == kBPred;  // B_PRED: inner edges always (15.1)
             lf_plane_mb(y, 1, pitch, mbx * 16, mby * 16, 16, mbx > 0, mby > 0, inner, f);
             for (int c = 0; c < 2; ++c) lf_plane_mb(uv + c, 2, pitch, mbx * 8, mby * 8, 8, mbx > 0, mby > 0, inner, f);
         }
@@ -453,6 +550,147 @@ MXV8 uint32_t code_luma16(const int* res, const int* pred, const Quant& Q, int16
     }
     return nz;
 }
+// One B_PRED luma sub-block b (4x4, no second-order block: type 3, the DC quantised with y1dc):
+// res / pred raster 4x4, levels in scan order to lv[b * 16 ..], reconstruction to rec (4x4 raster);
+// returns whether a level is non-zero.
+MXV8 bool code_sub4(const int* res, const int* pred, const Quant& Q, int16_t* lv, int* rec) {
+    int coef[16], dq[16], r[16];
+    fdct4x4(res, coef);
+    bool nz = false;
+    for (int k = 0; k < 16; ++k) {
+        const int pos = kZigzag[k];
+        const int q = k == 0 ? Q.y1dc : Q.y1ac;
+        const int l = quantize(coef[pos], q);
+        lv[k] = (int16_t)l;
+        dq[pos] = l * q;
+        nz |= l != 0;
+    }
+    idct4x4(dq, r);
+    for (int i = 0; i < 16; ++i) rec[i] = v8_clamp255(pred[i] + r[i]);
+    return nz;
+}
+// Sub-block neighbours (SubEdge) of sub-block (bx, by) of macroblock (mbx, mby): `at(x, y)` reads
+// the frame's reconstruction at luma (x, y) (this macroblock's earlier sub-blocks included).
+template <class F>
+MXV8 SubEdge sub_edge(const F& at, int mbx, int mby, int mb_w, int bx, int by) {
+    SubEdge e;
+    const int x0 = mbx * 16 + bx * 4, y0 = mby * 16 + by * 4;
+    const bool top = mby == 0 && by == 0, left = mbx == 0 && bx == 0;
+    for (int i = 0; i < 4; ++i) e.A[i] = top ? 127 : at(x0 + i, y0 - 1);
+    for (int i = 0; i < 4; ++i) e.L[i] = left ? 129 : at(x0 - 1, y0 + i);
+    e.P = top ? 127 : (left ? 129 : at(x0 - 1, y0 - 1));
+    // above-right: in the sub-block row above inside the macroblock, else from the row above the
+    // macroblock (the right column's lower sub-blocks reuse the macroblock's above-right)
+    if (bx < 3 && by > 0) {
+        for (int i = 0; i < 4; ++i) e.A[4 + i] = at(x0 + 4 + i, y0 - 1);
+    } else if (mby == 0) {
+        for (int i = 0; i < 4; ++i) e.A[4 + i] = 127;
+    } else if (bx < 3) {
+        for (int i = 0; i < 4; ++i) e.A[4 + i] = at(x0 + 4 + i, mby * 16 - 1);
+    } else if (mbx + 1 < mb_w) {
+        for (int i = 0; i < 4; ++i) e.A[4 + i] = at(mbx * 16 + 16 + i, mby * 16 - 1);
+    } else {
+        for (int i = 0; i < 4; ++i) e.A[4 + i] = at(mbx * 16 + 15, mby * 16 - 1);
+    }
+    return e;
+}
+// Cost in 1/256 bit of a key-frame luma mode (kKfYModeProb tree: B_PRED "0", DC "100", V "101",
+// H "110", TM "111")
+MXV8 int kf_ymode_cost256(int ymode) {
+    const uint8_t* p = kKfYModeProb;
+    if (ymode == kBPred) return branch_cost(p[0], 0);
+    return branch_cost(p[0], 1) + branch_cost(p[1], ymode >= kHPred) +
+           branch_cost(ymode >= kHPred ? p[3] : p[2], ymode == kVPred || ymode == kTmPred);
+}
+
+// B_PRED contexts (11.3): the sub-block mode above / left of a macroblock's edge sub-block column
+// bx / row by; a 16x16-predicted neighbour stands for its implied mode, outside the frame B_DC.
+MXV8 int bctx_above(const Vp8Mb* mbs, int mb_w, int mbx, int mby, int bx) {
+    if (mby == 0) return kBDc;
+    const Vp8Mb& n = mbs[(mby - 1) * mb_w + mbx];
+    return n.ymode == kBPred ? bmode_of(n, 12 + bx) : implied_bmode(n.ymode);
+}
+MXV8 int bctx_left(const Vp8Mb* mbs, int mb_w, int mbx, int mby, int by) {
+    if (mbx == 0) return kBDc;
+    const Vp8Mb& n = mbs[mby * mb_w + mbx - 1];
+    return n.ymode == kBPred ? bmode_of(n, 4 * by + 3) : implied_bmode(n.ymode);
+}
+// B_PRED luma of a key-frame macroblock, closed loop (the serial reference of k_vp8_key's
+// sub-block steps): every sub-block in raster order takes the allowed mode (bmode_allowed) of least
+// 256 SAD + lam * bmode_cost256 under its above / left contexts (the lower mode on ties), then is
+// coded (code_sub4) into rec (16x16 raster) and lv blocks 0..15, so the next one predicts from it.
+// src: the macroblock's source (pitch); at(x, y): the frame's reconstruction outside the macroblock;
+// actx / lctx: bctx_above / bctx_left of the macroblock.  Returns the summed cost plus the B_PRED
+// luma mode bits (same units as 256 SAD + lam * kf_ymode_cost256 of a 16x16 mode); the modes packed
+// 4 bits each into lo (0..7) / hi (8..15); the blocks' non-zero bits in *nz.
+template <class F>
+inline uint32_t bpred_luma(const uint8_t* src, int pitch, const F& at, int mbx, int mby, int mb_w, const Quant& Q,
+                           int lam, const int* actx, const int* lctx, int16_t* lv, int* rec, uint32_t* lo,
+                           uint32_t* hi, uint32_t* nz) {
+    const int x0 = mbx * 16, y0 = mby * 16;
+    auto px = [&](int x, int y) {  // reconstruction: this macroblock's coded sub-blocks, else the frame
+        return x >= x0 && x < x0 + 16 && y >= y0 && y < y0 + 16 ? rec[(y - y0) * 16 + x - x0] : at(x, y);
+    };
+    int modes[16];
+    uint32_t total = (uint32_t)(lam * kf_ymode_cost256(kBPred));
+    *lo = *hi = 0;
+    *nz = 0;
+    for (int b = 0; b < 16; ++b) {
+        const int bx = b & 3, by = b >> 2;
+        const SubEdge e = sub_edge(px, mbx, mby, mb_w, bx, by);
+        int X[15];
+        bpred_edge(e, X);
+        const int a = by > 0 ? modes[b - 4] : actx[bx], l = bx > 0 ? modes[b - 1] : lctx[by];
+        uint32_t best = ~0u;
+        int bm = kBDc;
+        for (int m = 0; m < kNumBModes; ++m) {
+            if (!bmode_allowed(m, bx, mbx, mby, mb_w)) continue;
+            uint32_t sad = 0;
+            for (int y = 0; y < 4; ++y)
+                for (int x = 0; x < 4; ++x) {
+                    const int d = (int)src[(by * 4 + y) * pitch + bx * 4 + x] - bpred_px(m, X, x, y);
+                    sad += (uint32_t)(d < 0 ? -d : d);
+                }
+            const uint32_t c = 256u * sad + (uint32_t)(lam * bmode_cost256(m, a, l));
+            if (c < best) {
+                best = c;
+                bm = m;
+            }
+        }
+        modes[b] = bm;
+        total += best;
+        int res[16], pred[16], r4[16];
+        for (int y = 0; y < 4; ++y)
+            for (int x = 0; x < 4; ++x) {
+                pred[y * 4 + x] = bpred_px(bm, X, x, y);
+                res[y * 4 + x] = (int)src[(by * 4 + y) * pitch + bx * 4 + x] - pred[y * 4 + x];
+            }
+        if (code_sub4(res, pred, Q, lv + b * 16, r4)) *nz |= 1u << b;
+        for (int y = 0; y < 4; ++y)
+            for (int x = 0; x < 4; ++x) rec[(by * 4 + y) * 16 + bx * 4 + x] = r4[y * 4 + x];
+        if (b < 8)
+            *lo |= (uint32_t)bm << (4 * b);
+        else
+            *hi |= (uint32_t)bm << (4 * (b - 8));
+    }
+    return total;
+}
+
+// ---------------------------------------------------------------- intra macroblocks in inter frames
+// Two passes after every macroblock was coded inter (its prediction SAD kept in bmodes_hi): a
+// macroblock is an intra candidate when its best 16x16 intra mode, predicted from the inter
+// reconstruction of its neighbours, beats the inter prediction by more than the mode bits
+// (kIntraBits256, lambda-weighted); a candidate switches to intra when none of its causal
+// neighbours (left, above, above-left) is a candidate -- then the neighbours it predicts from stay
+// inter (their reconstruction is final) and no macroblock that predicts from it switches, so both
+// passes run over all macroblocks in parallel (k_vp8_intra_cand / k_vp8_intra_code) and the
+// serial encoder reproduces them exactly.
+constexpr uint32_t kIntraMinSad = 512;   // inter prediction SAD at or below: never a candidate
+constexpr int kIntraBits256 = 8 * 256;    // is_inter_mb + y / uv modes, less the vector, in 1/256 bit
+MXV8 bool vp8_intra_candidate(uint32_t inter_sad, uint32_t intra_sad, int lam) {
+    return inter_sad > kIntraMinSad && 256ull * intra_sad + (unsigned long long)lam * kIntraBits256 < 256ull * inter_sad;
+}
+
 // One chroma component (8x8): blocks 16..19 (U) or 20..23 (V).
 MXV8 uint32_t code_chroma8(const int* res, const int* pred, const Quant& Q, int16_t* lv, int* rec, int first_block) {
     uint32_t nz = 0;

@@ -50,14 +50,13 @@ CpuVp8Encoder::CpuVp8Encoder(const h264::EncoderConfig& cfg)
     lv_.resize(mb_.size() * kCoefPerMb);
 }
 
-void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bool key, int qindex) {
+void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bool key, int qindex, int qp) {
     const Quant Q = quant_of(qindex);
     if (cfg_.aq >= 3) next_src_.assign((size_t)cw_ * ch_, 0);
     uint8_t* ry = rec_y_[cur_].data();
     uint8_t* ruv = rec_uv_[cur_].data();
     const uint8_t* fy = rec_y_[cur_ ^ 1].data();
     const uint8_t* fuv = rec_uv_[cur_ ^ 1].data();
-    const int qp = common_.cur_qp();
     for (int mby = 0; mby < mb_h_; ++mby)
         for (int mbx = 0; mbx < mb_w_; ++mbx) {
             const int i = mby * mb_w_ + mbx, x0 = mbx * 16, y0 = mby * 16;
@@ -65,6 +64,7 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
             std::memset(&m, 0, sizeof m);
             int16_t* lv = lv_.data() + (size_t)i * kCoefPerMb;
             int pred[256], res[256], rec[256], cp[2][64], cres[2][64], crec[2][64];
+            uint32_t bpred_nz = 0;  // B_PRED: the luma blocks' non-zero bits (luma coded already, no Y2)
             if (key) {
                 const Edge e = edge_of(ry, cw_, 1, 0, x0, y0, 16);
                 const int dc = dc_of(e, 16);
@@ -81,6 +81,23 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 }
                 for (int y = 0; y < 16; ++y)
                     for (int x = 0; x < 16; ++x) pred[y * 16 + x] = pred_px(m.ymode, e, 16, x, y, dc);
+                if (cfg_.vp8_bpred) {  // B_PRED when its sub-block predictions + mode bits cost less
+                    const int lam = h264::lambda_sad(qp);
+                    int actx[4], lctx[4];
+                    for (int k = 0; k < 4; ++k) {
+                        actx[k] = bctx_above(mb_.data(), mb_w_, mbx, mby, k);
+                        lctx[k] = bctx_left(mb_.data(), mb_w_, mbx, mby, k);
+                    }
+                    auto at = [&](int x, int y) { return (int)ry[(size_t)y * cw_ + x]; };
+                    uint32_t lo, hi, bnz;
+                    const uint32_t costb = bpred_luma(sy + (size_t)y0 * pitch + x0, pitch, at, mbx, mby, mb_w_, Q, lam, actx,
+                                                      lctx, lv, rec, &lo, &hi, &bnz);
+                    if (costb < 256u * best + (uint32_t)(lam * kf_ymode_cost256(m.ymode))) {
+                        m.ymode = kBPred;
+                        set_bmodes(m, lo, hi);
+                        bpred_nz = bnz;
+                    }
+                }
                 const Edge eu = edge_of(ruv, cw_, 2, 0, x0 / 2, y0 / 2, 8), ev = edge_of(ruv, cw_, 2, 1, x0 / 2, y0 / 2, 8);
                 const int du = dc_of(eu, 8), dv = dc_of(ev, 8);
                 best = ~0u;
@@ -153,7 +170,12 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 m.seg = (uint8_t)seg_of_tclass(h264::temporal_class(tsad, m.mvx == 0 && m.mvy == 0));
             }
             const Quant Qm = m.seg ? quant_of(seg_qindex_[m.seg]) : (key ? Q : quant_of(seg_qindex_[0]));
-            m.nz = code_luma16(res, pred, Qm, lv, rec);
+            if (m.ymode == kBPred) {
+                m.nz = bpred_nz;
+                for (int k = 0; k < 16; ++k) lv[kY2 * 16 + k] = 0;
+            } else {
+                m.nz = code_luma16(res, pred, Qm, lv, rec);
+            }
             m.nz |= code_chroma8(cres[0], cp[0], Qm, lv, crec[0], 16);
             m.nz |= code_chroma8(cres[1], cp[1], Qm, lv, crec[1], 20);
             if (!key) {  // noise-like residual that does not pay for its bits: prediction only
@@ -165,6 +187,7 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                     dp += res[i] * res[i];
                     dc += e * e;
                 }
+                m.bmodes_hi = lsad;  // the inter prediction SAD (intra_pass)
                 for (int b = 0; b < 16; ++b) {
                     int n = 0;
                     for (int k = 1; k < 16; ++k) n += lv[b * 16 + k] != 0;
@@ -191,6 +214,90 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
         }
 }
 
+// Intra macroblocks in an inter frame, after every macroblock was coded inter: candidates from
+// the inter reconstruction, then the candidates without a candidate causal neighbour coded intra
+// (vp8_core.h vp8_intra_candidate; k_vp8_intra_cand / k_vp8_intra_code on the GPU).
+void CpuVp8Encoder::intra_pass(const uint8_t* sy, const uint8_t* suv, int pitch, int qp) {
+    uint8_t* ry = rec_y_[cur_].data();
+    uint8_t* ruv = rec_uv_[cur_].data();
+    const int lam = h264::lambda_sad(qp);
+    const size_t nmb = mb_.size();
+    std::vector<uint8_t> cand(nmb, 0), mode(nmb, 0);
+    auto best16 = [&](int x0, int y0, int* bm) {
+        const Edge e = edge_of(ry, cw_, 1, 0, x0, y0, 16);
+        const int dc = dc_of(e, 16);
+        uint32_t best = ~0u;
+        for (int md = 0; md < 4; ++md) {
+            uint32_t sad = 0;
+            for (int y = 0; y < 16; ++y)
+                for (int x = 0; x < 16; ++x)
+                    sad += (uint32_t)std::abs((int)sy[(y0 + y) * pitch + x0 + x] - pred_px(md, e, 16, x, y, dc));
+            if (sad < best) {
+                best = sad;
+                *bm = md;
+            }
+        }
+        return best;
+    };
+    for (int mby = 0; mby < mb_h_; ++mby)
+        for (int mbx = 0; mbx < mb_w_; ++mbx) {
+            const int i = mby * mb_w_ + mbx;
+            if (mb_[i].bmodes_hi <= kIntraMinSad) continue;
+            int bm = 0;
+            const uint32_t s = best16(mbx * 16, mby * 16, &bm);
+            cand[i] = vp8_intra_candidate(mb_[i].bmodes_hi, s, lam);
+            mode[i] = (uint8_t)bm;
+        }
+    for (int mby = 0; mby < mb_h_; ++mby)
+        for (int mbx = 0; mbx < mb_w_; ++mbx) {
+            const int i = mby * mb_w_ + mbx, x0 = mbx * 16, y0 = mby * 16;
+            if (!cand[i] || (mbx > 0 && cand[i - 1]) || (mby > 0 && cand[i - mb_w_]) ||
+                (mbx > 0 && mby > 0 && cand[i - mb_w_ - 1]))
+                continue;
+            Vp8Mb& m = mb_[i];
+            int16_t* lv = lv_.data() + (size_t)i * kCoefPerMb;
+            int pred[256], res[256], rec[256], cp[2][64], cres[2][64], crec[2][64];
+            const Edge e = edge_of(ry, cw_, 1, 0, x0, y0, 16);
+            const int dc = dc_of(e, 16);
+            m.ymode = mode[i];
+            for (int y = 0; y < 16; ++y)
+                for (int x = 0; x < 16; ++x) pred[y * 16 + x] = pred_px(m.ymode, e, 16, x, y, dc);
+            const Edge eu = edge_of(ruv, cw_, 2, 0, x0 / 2, y0 / 2, 8), ev = edge_of(ruv, cw_, 2, 1, x0 / 2, y0 / 2, 8);
+            const int du = dc_of(eu, 8), dv = dc_of(ev, 8);
+            uint32_t best = ~0u;
+            for (int md = 0; md < 4; ++md) {
+                uint32_t sad = 0;
+                for (int y = 0; y < 8; ++y)
+                    for (int x = 0; x < 8; ++x) {
+                        const int o = (y0 / 2 + y) * pitch + (x0 + 2 * x);
+                        sad += (uint32_t)std::abs((int)suv[o] - pred_px(md, eu, 8, x, y, du));
+                        sad += (uint32_t)std::abs((int)suv[o + 1] - pred_px(md, ev, 8, x, y, dv));
+                    }
+                if (sad < best) {
+                    best = sad;
+                    m.uvmode = (uint8_t)md;
+                }
+            }
+            for (int y = 0; y < 8; ++y)
+                for (int x = 0; x < 8; ++x) {
+                    cp[0][y * 8 + x] = pred_px(m.uvmode, eu, 8, x, y, du);
+                    cp[1][y * 8 + x] = pred_px(m.uvmode, ev, 8, x, y, dv);
+                }
+            for (int k = 0; k < 256; ++k) res[k] = sy[(y0 + k / 16) * pitch + x0 + k % 16] - pred[k];
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 64; ++k) cres[c][k] = suv[(y0 / 2 + k / 8) * pitch + x0 + 2 * (k % 8) + c] - cp[c][k];
+            const Quant Qm = quant_of(seg_qindex_[m.seg & 3]);
+            m.mvx = m.mvy = 0;
+            m.bmodes_hi = 0;
+            m.nz = code_luma16(res, pred, Qm, lv, rec);
+            m.nz |= code_chroma8(cres[0], cp[0], Qm, lv, crec[0], 16);
+            m.nz |= code_chroma8(cres[1], cp[1], Qm, lv, crec[1], 20);
+            for (int k = 0; k < 256; ++k) ry[(size_t)(y0 + k / 16) * cw_ + x0 + k % 16] = (uint8_t)rec[k];
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 64; ++k) ruv[(size_t)(y0 / 2 + k / 8) * cw_ + x0 + 2 * (k % 8) + c] = (uint8_t)crec[c][k];
+        }
+}
+
 const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_t* uv, int pitch, bool force_idr) {
     auto run_serial = [](int n, const std::function<void(int)>& fn) {
         for (int k = 0; k < n; ++k) fn(k);
@@ -198,7 +305,7 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     const int log2_parts = mb_h_ >= 8 ? 3 : (mb_h_ >= 4 ? 2 : (mb_h_ >= 2 ? 1 : 0));
     while (common_.wants_probe()) {  // size the first key frame, as the GPU encoder does
         const int q = common_.probe_qp();
-        analyse(y, uv, pitch, true, qindex_for_qp(q));
+        analyse(y, uv, pitch, true, qindex_for_qp(q), q);
         std::vector<uint8_t> tmp;
         write_frame(FrameDesc{true, cfg_.width, cfg_.height, mb_w_, mb_h_, qindex_for_qp(q), log2_parts}, mb_.data(),
                     [&](int i) { return (const int16_t*)lv_.data() + (size_t)i * kCoefPerMb; }, tmp, run_serial);
@@ -214,7 +321,8 @@ const std::vector<uint8_t>& CpuVp8Encoder::encode(const uint8_t* y, const uint8_
     if (fd.segmented) segment_qindices(common_.cur_qp(), cfg_.aq, seg_qindex_);
     for (int k = 0; k < kNumSegs; ++k) fd.seg_qindex[k] = seg_qindex_[k];
     lf_levels(lf_.decide(frames_, key), fd.segmented, qindex, seg_qindex_, lf_num_, fd.lf_level);
-    analyse(y, uv, pitch, key, qindex);
+    analyse(y, uv, pitch, key, qindex, common_.cur_qp());
+    if (!key && cfg_.vp8_intra) intra_pass(y, uv, pitch, common_.cur_qp());
     // the loop filter over the whole reconstruction (the next frame's reference, the decoder's output)
     if (fd.lf_level[0] | fd.lf_level[1] | fd.lf_level[2] | fd.lf_level[3])
         loop_filter_frame(rec_y_[cur_].data(), rec_uv_[cur_].data(), cw_, mb_w_, mb_h_, mb_.data(), fd.lf_level, key);

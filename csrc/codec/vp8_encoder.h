@@ -236,7 +236,8 @@ class CpuVp8Encoder {
     double writer_tokens_us() const { return tok_stats_[stats_.idr ? 1 : 0][(frames_ - 1) % kStatsLag].us_tokens; }
 
    private:
-    void analyse(const uint8_t* y, const uint8_t* uv, int pitch, bool key, int qindex);
+    void analyse(const uint8_t* y, const uint8_t* uv, int pitch, bool key, int qindex, int qp);
+    void intra_pass(const uint8_t* y, const uint8_t* uv, int pitch, int qp);  // inter frames (vp8_core.h)
     h264::EncoderConfig cfg_;
     h264::EncoderCommon common_;
     int cw_, ch_, mb_w_, mb_h_;
@@ -259,6 +260,7 @@ class CpuVp8Encoder {
 };
 
 // Device layout of the GPU encoder
+constexpr int kKeyLineWords = 9;  // k_vp8_key hand-off words per macroblock
 struct Vp8FrameState {
     const uint8_t* ref_y;   // previous reconstruction (P frames)
     const uint8_t* ref_uv;
@@ -276,6 +278,8 @@ struct Vp8FrameState {
     int32_t q[kNumSegs][6];   // per segment: Y1 DC, Y1 AC, Y2 DC, Y2 AC, UV DC, UV AC quantiser steps
     uint32_t qm[kNumSegs][6]; // ceil(2^32 / (3 q)): the dead-zone quantiser's division as a multiply-high
     int32_t drop_lambda;    // P frames: lambda_sse of the frame QP for vp8_drop_residual
+    int32_t bpred_lambda;   // key frames: lambda_sad of the frame QP for the B_PRED decision (0: no B_PRED)
+    int32_t intra_lambda;   // inter frames: lambda_sad of the frame QP for vp8_intra_candidate
     int32_t lf_level[kNumSegs];  // loop-filter level per segment (k_vp8_lf; all 0: not launched)
 };
 // Both per-frame states in one block: one host->device copy per frame.
@@ -287,20 +291,22 @@ struct Vp8DeviceBuffers {
     Vp8States* st;         // device copy of the frame states
     Vp8Mb* mb;             // [nmb] records (device)
     int16_t* lv;           // [nmb * 400] levels (device)
-    uint64_t* line;        // [mb_h][mb_w][8] key-frame hand-off: bottom luma + chroma rows, epoch-tagged
+    uint64_t* line;        // [mb_h][mb_w][kKeyLineWords] key-frame hand-off: bottom luma + chroma rows and
+                           // the bottom sub-block modes (B_PRED contexts), epoch-tagged
     int* err;              // mapped host word: nonzero if a wavefront spin timed out
     unsigned long long* lf_line;  // loop-filter hand-off lines (k_vp8_lf: epoch-tagged, per workgroup) + scratch
     unsigned long long* lf_sse;  // mapped host [mb_h][3]: Y / U / V distortion of the filtered picture
     Vp8Mb* mb_host;        // mapped host: records with their level slots (k_vp8_gather)
     int16_t* lv_host;      // mapped host: levels of the coded macroblocks, row-compacted
     h264::DeviceBuffers me;  // shared H.264 motion search (fs = &st->me, mb = vectors)
+    uint8_t* icand;        // [nmb] inter frames' intra pass: candidate << 7 | best 16x16 mode
 };
 // P frames: pad the reference, shared integer motion search, then one wave per macroblock.
 // hp_planes: the four padded F / H / V / J planes (h264::launch_hpel) when the motion search refines
 // to quarter samples (EncoderConfig::subpel), else hp_planes[0] only (the padded full-sample plane)
 void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_t* const hp_planes[4], int hp_pitch,
                       bool subpel, const uint8_t* src_y,
-                      const uint8_t* src_uv, hipStream_t stream);
+                      const uint8_t* src_uv, hipStream_t stream, bool intra = false);
 // Key frames: one wave per macroblock row, rows handing their bottom edges down (wavefront).
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                     hipStream_t stream, bool save_src);

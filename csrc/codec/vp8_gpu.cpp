@@ -39,8 +39,8 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     HIP_CHECK(hipMalloc(&b.st, sizeof(Vp8States)));
     HIP_CHECK(hipMalloc(&b.mb, sizeof(Vp8Mb) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.lv, sizeof(int16_t) * kCoefPerMb * (size_t)nmb));
-    HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * 8 * (size_t)geom_.mb_h * geom_.mb_w));
-    HIP_CHECK(hipMemsetAsync(b.line, 0, sizeof(uint64_t) * 8 * (size_t)geom_.mb_h * geom_.mb_w, stream_));  // tag 0: no frame
+    HIP_CHECK(hipMalloc(&b.line, sizeof(uint64_t) * kKeyLineWords * (size_t)geom_.mb_h * geom_.mb_w));
+    HIP_CHECK(hipMemsetAsync(b.line, 0, sizeof(uint64_t) * kKeyLineWords * (size_t)geom_.mb_h * geom_.mb_w, stream_));  // tag 0: no frame
     // hand-off lines: 32 tagged words per macroblock per workgroup of rows, then 1 KB scratch per
     // row (k_vp8_lf); tags start at 0, never a frame's epoch
     const size_t lf_bytes = sizeof(uint64_t) * 32 * (size_t)geom_.mb_h * geom_.mb_w + 1024 * (size_t)(geom_.mb_h + 16);
@@ -52,6 +52,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     HIP_CHECK(hipHostMalloc(&b.mb_host, sizeof(Vp8Mb) * (size_t)nmb, hipHostMallocMapped));
     HIP_CHECK(hipHostMalloc(&b.lv_host, sizeof(int16_t) * kCoefPerMb * (size_t)nmb, hipHostMallocMapped));
     HIP_CHECK(hipMalloc(&b.me.mb, sizeof(h264::MbInfo) * (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.icand, (size_t)nmb));
     b.me.fs = &b.st->me;
     HIP_CHECK(hipHostMalloc(&s.st_host, sizeof(Vp8States), hipHostMallocDefault));
     std::memset(s.st_host, 0, sizeof(Vp8States));
@@ -61,7 +62,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
 
 void GpuVp8Encoder::free_slot(Slot& s) {
     Vp8DeviceBuffers& b = s.buf;
-    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line})
+    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line, (void*)b.icand})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)b.err, (void*)b.mb_host, (void*)b.lv_host, (void*)s.st_host, (void*)b.lf_sse})
         if (p) (void)hipHostFree(p);
@@ -218,6 +219,8 @@ void GpuVp8Encoder::fill_state(Slot& s, bool key, int qp, int ref, int cur) {
         }
     }
     f.drop_lambda = h264::lambda_sse(qp);
+    f.bpred_lambda = cfg_.vp8_bpred ? h264::lambda_sad(qp) : 0;
+    f.intra_lambda = h264::lambda_sad(qp);
     for (int k = 0; k < kNumSegs; ++k) f.lf_level[k] = s.lf_level[k] = 0;  // prepare() decides the filter
     s.lf_on = false;
     h264::FrameState& m = s.st_host->me;
@@ -243,7 +246,7 @@ void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* 
     else
     {
         uint8_t* const planes[4] = {hp_, hp_sub_[0], hp_sub_[1], hp_sub_[2]};
-        launch_vp8_inter(geom_, s.buf, planes, hp_pitch_, cfg_.subpel != 0, src_y, src_uv, stream_);
+        launch_vp8_inter(geom_, s.buf, planes, hp_pitch_, cfg_.subpel != 0, src_y, src_uv, stream_, cfg_.vp8_intra != 0);
     }
     if (s.lf_on) launch_vp8_lf(geom_, s.buf, src_y, src_uv, stream_);
     launch_vp8_gather(geom_, s.buf, stream_);

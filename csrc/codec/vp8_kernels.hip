@@ -71,14 +71,16 @@ struct MbLds {
 // code_chroma8 of vp8_core.h, one block per lane.
 // drop_lambda >= 0 (inter macroblocks): vp8_drop_residual may turn the macroblock into prediction
 // only (levels zero, reconstruction = prediction) -- the decision is wave-uniform.
+// luma_coded (B_PRED key-frame macroblocks): the luma is coded already (levels, s.rec) -- only the
+// chroma blocks here, and a zero Y2 block.
 __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restrict__ lv, int lane,
-                            int drop_lambda = -1, int seg = 0) {
+                            int drop_lambda = -1, int seg = 0, bool luma_coded = false) {
     const int32_t* Fq = F.q[seg];      // the macroblock's segment quantiser (wave-uniform)
     const uint32_t* Fqm = F.qm[seg];
     int lvl[16], dq[16];
     bool nz = false;
     int st_lsad = 0, st_dp = 0, st_dc = 0, st_bits = 0;  // drop statistics (luma lanes, Y2 lane)
-    const bool luma = lane < 16, chroma = lane >= 16 && lane < 24;
+    const bool luma = lane < 16 && !luma_coded, chroma = lane >= 16 && lane < 24;
 #pragma unroll
     for (int k = 0; k < 16; ++k) lvl[k] = dq[k] = 0;
     if (luma || chroma) {
@@ -126,7 +128,7 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
         }
     }
     __syncthreads();
-    if (lane == kY2) {
+    if (lane == kY2 && !luma_coded) {
         int dcv[16], y2[16], y2q[16], dcr[16];
 #pragma unroll
         for (int b = 0; b < 16; ++b) dcv[b] = s.dc[b];
@@ -213,7 +215,7 @@ __device__ uint32_t code_mb(MbLds& s, const Vp8FrameState& F, int16_t* __restric
                 }
         }
     }
-    if (lane < kBlocks) {
+    if (lane < kBlocks && (luma || lane >= 16)) {
         uint32_t w[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) w[k] = (uint32_t)(uint16_t)lvl[2 * k] | ((uint32_t)(uint16_t)lvl[2 * k + 1] << 16);
@@ -297,7 +299,8 @@ __device__ __forceinline__ void rec_words(const MbLds& s, const h264::Geometry& 
 }
 
 __device__ __forceinline__ void store_record(Vp8Mb* __restrict__ rec, int mvx, int mvy, int ymode, int uvmode,
-                                             uint32_t nz, const uint32_t sse[3], int lane, int seg = 0) {
+                                             uint32_t nz, const uint32_t sse[3], int lane, int seg = 0,
+                                             uint32_t bmodes_hi = 0) {
     if (lane == 0) {
         Vp8Mb m;
         m.mvx = (int16_t)mvx;
@@ -311,7 +314,7 @@ __device__ __forceinline__ void store_record(Vp8Mb* __restrict__ rec, int mvx, i
         m.sse[0] = sse[0];
         m.sse[1] = sse[1];
         m.sse[2] = sse[2];
-        m.pad2 = 0;
+        m.bmodes_hi = bmodes_hi;
         *rec = m;
     }
 }
@@ -424,11 +427,19 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
         s.pv[cy * 8 + cx] = (uint8_t)chroma_px(at_v, px, py, cvx & 7, cvy & 7);
     }
     __syncthreads();
+    int psad = 0;  // the luma prediction SAD: the intra pass compares against it
+    {
+        const int r = lane >> 2, c4 = (lane & 3) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) psad += abs((int)s.src[r * 16 + c4 + j] - (int)s.pred[r * 16 + c4 + j]);
+    }
+    psad = wsum(psad);
     const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, F.drop_lambda, seg);
     uint32_t sse[3];
     store_rec(s, g, F, x0, y0, lane, sse);
-    store_record(mbs + mbi, mvx, mvy, kInter, kDcPred, nz, sse, lane, seg);
+    store_record(mbs + mbi, mvx, mvy, kInter, kDcPred, nz, sse, lane, seg, (uint32_t)psad);
 }
+
 
 // Key frames with temporal classes: the source luma into the frame state's save buffer (the
 // pointer read on the device, as h264 k_save_src), one dword per thread.
@@ -444,7 +455,143 @@ __global__ __launch_bounds__(256) void k_vp8_save_src(h264::Geometry g, const Vp
 struct KeyEdges {
     int ay[16], ly[16], au[8], lu[8], av[8], lvv[8];
     int cy, cu, cv;
+    int actx;  // B_PRED contexts: the above macroblock's bottom sub-block modes, 4 bits each
 };
+// B_PRED sub-block steps: the edge array (vp8_core.h bpred_edge) and the transform's stages
+struct BpLds {
+    int X[16];
+    int T[4][16];
+};
+// raster position -> scan index (the inverse of kZigzag)
+constexpr uint8_t kInvZigzag[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
+
+// Wave minimum, every lane gets it (whole wave active): wsum's network with min.
+__device__ __forceinline__ uint32_t wmin(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));
+    const auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const uint32_t u = min(r16[0], r16[1]);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return min(r32[0], r32[1]);
+}
+
+// B_PRED luma of the staged macroblock (vp8_core.h bpred_luma, step for step): 16 sub-blocks in
+// raster order; per sub-block lanes 0..14 gather the edge array, lanes 0..39 price the ten modes
+// (mode lane / 4, sample row lane % 4; the allowed mode of least 256 SAD + lam * bits, the lower
+// on ties, by one wave minimum of cost << 4 | mode), lanes 0..15 code the chosen one (one sample
+// each: forward DCT, quantiser, inverse DCT through the BpLds stages) into s.rec and the levels of
+// blocks 0..15.  Returns the summed cost (+ the B_PRED mode bits); modes packed into lo / hi, the
+// blocks' non-zero bits into *nz (all wave-uniform).
+__device__ uint32_t bpred_mb(MbLds& s, BpLds& B, const KeyEdges& E, const Vp8FrameState& F, int16_t* __restrict__ lv,
+                             int lane, int mbx, int mby, int mb_w, int lctx, uint32_t& lo, uint32_t& hi, uint32_t& nz) {
+    const int lam = F.bpred_lambda;
+    const bool top = mby == 0, left = mbx > 0;
+    uint32_t total = (uint32_t)(lam * kf_ymode_cost256(kBPred));
+    lo = hi = nz = 0;
+    const int r = (lane >> 2) & 3, c = lane & 3;
+    for (int b = 0; b < 16; ++b) {
+        const int bx = b & 3, by = b >> 2, xs = bx * 4, ys = by * 4;
+        if (lane < 15) {  // X: L3 L3 L2 L1 L0 P A0 .. A7 A7
+            int v;
+            if (lane <= 4) {
+                const int j = lane == 0 ? 3 : 4 - lane;
+                v = bx > 0 ? s.rec[(ys + j) * 16 + xs - 1] : (left ? E.ly[ys + j] : 129);
+            } else if (lane == 5) {
+                v = (top && by == 0) ? 127
+                    : ((!left && bx == 0) ? 129
+                                          : (by > 0 ? (bx > 0 ? s.rec[(ys - 1) * 16 + xs - 1] : E.ly[ys - 1])
+                                                    : (bx > 0 ? E.ay[xs - 1] : E.cy)));
+            } else {
+                const int i = lane == 14 ? 7 : lane - 6;
+                if (i < 4)
+                    v = (top && by == 0) ? 127 : (by > 0 ? s.rec[(ys - 1) * 16 + xs + i] : E.ay[xs + i]);
+                else if (by > 0 && bx < 3)
+                    v = s.rec[(ys - 1) * 16 + xs + i];
+                else if (top)
+                    v = 127;
+                else if (bx < 3)
+                    v = E.ay[xs + i];
+                else
+                    v = mbx + 1 < mb_w ? 0 : E.ay[15];  // (0: read by no allowed mode, bmode_allowed)
+            }
+            B.X[lane] = v;
+        }
+        __syncthreads();
+        auto mode_at = [&](int k) { return (int)((k < 8 ? lo >> (4 * k) : hi >> (4 * (k - 8))) & 15u); };
+        const int a = by > 0 ? mode_at(b - 4) : (E.actx >> (4 * bx)) & 15;
+        const int l = bx > 0 ? mode_at(b - 1) : (lctx >> (4 * by)) & 15;
+        // ---- mode search (lanes 4m .. 4m + 3: mode m, rows 0..3)
+        const int m = lane >> 2, sr = lane & 3;
+        int sad = 0;
+        if (lane < 40)
+#pragma unroll
+            for (int x = 0; x < 4; ++x) sad += abs((int)s.src[(ys + sr) * 16 + xs + x] - bpred_px(m, B.X, x, sr));
+        sad += __builtin_amdgcn_mov_dpp(sad, 0xB1, 0xF, 0xF, false);
+        sad += __builtin_amdgcn_mov_dpp(sad, 0x4E, 0xF, 0xF, false);
+        uint32_t key = 0xffffffffu;
+        if (lane < 40 && bmode_allowed(m, bx, mbx, mby, mb_w))
+            key = ((256u * (uint32_t)sad + (uint32_t)(lam * bmode_cost256(m, a, l))) << 4) | (uint32_t)m;
+        key = __builtin_amdgcn_readfirstlane(wmin(key));
+        const int bm = (int)(key & 15u);
+        total += key >> 4;
+        if (b < 8)
+            lo |= (uint32_t)bm << (4 * b);
+        else
+            hi |= (uint32_t)bm << (4 * (b - 8));
+        // ---- coding (lanes 0..15: sample (c, r) of the sub-block)
+        const bool cl = lane < 16;
+        const int pred = cl ? bpred_px(bm, B.X, c, r) : 0;
+        if (cl) B.T[0][lane] = (int)s.src[(ys + r) * 16 + xs + c] - pred;
+        __syncthreads();
+        if (cl) {  // forward DCT, rows (vp8_core.h fdct4x4)
+            const int* ip = B.T[0] + 4 * r;
+            const int a1 = (ip[0] + ip[3]) * 8, b1 = (ip[1] + ip[2]) * 8, c1 = (ip[1] - ip[2]) * 8, d1 = (ip[0] - ip[3]) * 8;
+            B.T[1][lane] = c == 0 ? a1 + b1
+                           : c == 2 ? a1 - b1
+                           : c == 1 ? (c1 * 2217 + d1 * 5352 + 14500) >> 12
+                                    : (d1 * 2217 - c1 * 5352 + 7500) >> 12;
+        }
+        __syncthreads();
+        bool lnz = false;
+        if (cl) {  // columns, then the quantiser (DC at Y1 DC: type 3, no Y2)
+            const int* t = B.T[1];
+            const int a1 = t[c] + t[12 + c], b1 = t[4 + c] + t[8 + c], c1 = t[4 + c] - t[8 + c], d1 = t[c] - t[12 + c];
+            const int co = r == 0 ? (a1 + b1 + 7) >> 4
+                           : r == 2 ? (a1 - b1 + 7) >> 4
+                           : r == 1 ? ((c1 * 2217 + d1 * 5352 + 12000) >> 16) + (d1 != 0 ? 1 : 0)
+                                    : (d1 * 2217 - c1 * 5352 + 51000) >> 16;
+            const int qi = lane == 0 ? 0 : 1;
+            const int lvl = qz(co, F.q[0][qi], F.qm[0][qi]);
+            lv[b * 16 + kInvZigzag[lane]] = (int16_t)lvl;
+            B.T[2][lane] = lvl * F.q[0][qi];
+            lnz = lvl != 0;
+        }
+        if (__ballot(lnz)) nz |= 1u << b;
+        __syncthreads();
+        constexpr int c8 = 20091, s8 = 35468;
+        if (cl) {  // inverse DCT, columns (vp8_core.h idct4x4)
+            const int* in = B.T[2];
+            const int i0 = in[c], i4 = in[4 + c], i8 = in[8 + c], i12 = in[12 + c];
+            const int a1 = i0 + i8, b1 = i0 - i8;
+            const int c1 = ((i4 * s8) >> 16) - (i12 + ((i12 * c8) >> 16));
+            const int d1 = (i4 + ((i4 * c8) >> 16)) + ((i12 * s8) >> 16);
+            B.T[3][lane] = r == 0 ? a1 + d1 : (r == 1 ? b1 + c1 : (r == 2 ? b1 - c1 : a1 - d1));
+        }
+        __syncthreads();
+        if (cl) {  // rows, then the reconstruction
+            const int* ip = B.T[3] + 4 * r;
+            const int a1 = ip[0] + ip[2], b1 = ip[0] - ip[2];
+            const int c1 = ((ip[1] * s8) >> 16) - (ip[3] + ((ip[3] * c8) >> 16));
+            const int d1 = (ip[1] + ((ip[1] * c8) >> 16)) + ((ip[3] * s8) >> 16);
+            const int o = c == 0 ? (a1 + d1 + 4) >> 3 : (c == 1 ? (b1 + c1 + 4) >> 3 : (c == 2 ? (b1 - c1 + 4) >> 3 : (a1 - d1 + 4) >> 3));
+            s.rec[(ys + r) * 16 + xs + c] = (uint8_t)v8_clamp255(pred + o);
+        }
+        __syncthreads();
+    }
+    return total;
+}
 
 __device__ __forceinline__ int pred_of(int mode, int above, int left, int corner, int dc) {
     switch (mode) {
@@ -474,14 +621,16 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
     __builtin_amdgcn_s_setprio(3);
     __shared__ MbLds s;
     __shared__ KeyEdges E;
+    __shared__ BpLds B;
     const Vp8FrameState& F = st->v;
     const int mby = blockIdx.x, lane = threadIdx.x, y0 = mby * 16;
     const uint32_t epoch = (uint32_t)F.epoch;
     const bool top = mby == 0, bottom = mby == g.mb_h - 1;
     // hand-off words of a macroblock: 0..3 its bottom luma row, 4..7 its bottom chroma row
     // (interleaved), 32 samples each with the frame's epoch tag above them
-    const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * g.mb_w * 8;
-    uint64_t* my_line = line + (size_t)mby * g.mb_w * 8;
+    constexpr int W = kKeyLineWords;  // + word 8: the bottom sub-block modes (B_PRED contexts)
+    const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * g.mb_w * W;
+    uint64_t* my_line = line + (size_t)mby * g.mb_w * W;
     // the source of the next macroblock is fetched one macroblock ahead (registers), staged in LDS
     // at the top of the iteration; the fetch is taken at the bottom of the iteration that issued
     // it, so its wait counts the stores after it, not a vmcnt(0) at the loop's join
@@ -496,13 +645,15 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
     // the next poll, whose vmcnt(0) would otherwise wait for these stores)
     uint32_t pwy = 0, pwuv = 0, psse[3] = {0, 0, 0};
     int pmbx = -1, pym = 0, puvm = 0;
-    uint32_t pnz = 0;
+    uint32_t pnz = 0, pblo = 0, pbhi = 0;
+    int lctx = 0;  // B_PRED contexts of the next macroblock: its left neighbour's right sub-block modes
     auto flush = [&]() {
         if (pmbx < 0) return;
         const int r = lane >> 2, c4 = (lane & 3) * 4, px0 = pmbx * 16;
         *reinterpret_cast<uint32_t*>(F.rec_y + (size_t)(y0 + r) * g.pitch + px0 + c4) = pwy;
         if (lane < 32) *reinterpret_cast<uint32_t*>(F.rec_uv + (size_t)(y0 / 2 + r) * g.pitch + px0 + c4) = pwuv;
-        store_record(mbs + mby * g.mb_w + pmbx, 0, 0, pym, puvm, pnz, psse, lane);
+        store_record(mbs + mby * g.mb_w + pmbx, (int)(int16_t)(pblo & 0xffffu), (int)(int16_t)(pblo >> 16), pym, puvm,
+                     pnz, psse, lane, 0, pbhi);
         pmbx = -1;
     };
     for (int mbx = 0; mbx < g.mb_w; ++mbx) {
@@ -523,8 +674,8 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
             // the row above's words of this macroblock (lanes 0..7) and of the one before it (lanes
             // 8, 9: the corner samples), polled until every needed word carries this frame's tag
             // (tagged 64-bit agent-scope atomics: no release fence -- an L2 write-back -- per MB)
-            const bool need = lane < 8 || (lane < 10 && left);
-            const int wi = lane < 8 ? 8 * mbx + lane : 8 * (mbx - 1) + (lane == 8 ? 3 : 7);
+            const bool need = lane < 8 || (lane < 10 && left) || lane == 10;
+            const int wi = lane < 8 ? W * mbx + lane : (lane == 10 ? W * mbx + 8 : W * (mbx - 1) + (lane == 8 ? 3 : 7));
             const gu64* wp = (const gu64*)(above_line + (need ? wi : 0));
             uint64_t w = 0;
             for (unsigned sp = 0;; ++sp) {
@@ -551,11 +702,14 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
             } else if (lane == 9) {
                 E.cu = left ? (int)((d >> 16) & 0xff) : 129;
                 E.cv = left ? (int)(d >> 24) : 129;
+            } else if (lane == 10) {
+                E.actx = (int)(d & 0xffffu);
             }
         } else {
             if (lane < 16) E.ay[lane] = 127;
             if (lane < 8) E.au[lane] = E.av[lane] = 127;
             if (lane == 0) E.cy = E.cu = E.cv = 127;
+            if (lane == 0) E.actx = 0;  // B_DC above the frame
         }
         if (!left) {
             if (lane < 16) E.ly[lane] = 129;
@@ -574,6 +728,7 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
                                  nav + nlf, 2);
         const int r = lane >> 2, c4 = (lane & 3) * 4;
         int ymode = 0, uvmode = 0;
+        uint32_t best16 = ~0u;
         {
             int sad[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -582,12 +737,11 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
 #pragma unroll
                 for (int m = 0; m < 4; ++m) sad[m] += abs(sv - pred_of(m, E.ay[c4 + j], E.ly[r], E.cy, dcy));
             }
-            uint32_t best = ~0u;
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 const uint32_t t = (uint32_t)wsum(sad[m]);
-                if (t < best) {
-                    best = t;
+                if (t < best16) {
+                    best16 = t;
                     ymode = m;
                 }
             }
@@ -615,11 +769,32 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
         s.pu[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.au[cx], E.lu[cy], E.cu, dcu);
         s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
         __syncthreads();
-        const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane);
-        // ---- hand the bottom rows down: eight tagged words
-        if (!bottom && lane < 8) {
+        // ---- B_PRED when its sub-block predictions + mode bits cost less than the 16x16 mode's
+        uint32_t blo = 0, bhi = 0, bnz = 0;
+        bool bp = false;
+        if (F.bpred_lambda) {
+            const uint32_t costb = bpred_mb(s, B, E, F, lv + (size_t)mbi * kCoefPerMb, lane, mbx, mby, g.mb_w, lctx, blo,
+                                            bhi, bnz);
+            bp = costb < 256u * best16 + (uint32_t)(F.bpred_lambda * kf_ymode_cost256(ymode));
+        }
+        uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, -1, 0, bp);
+        int ctx_bottom, ctx_right;  // this macroblock's bottom / right sub-block modes (contexts)
+        if (bp) {
+            nz |= bnz;
+            ymode = kBPred;
+            ctx_bottom = (int)(bhi >> 16);
+            ctx_right = (int)(((blo >> 12) & 15u) | (((blo >> 28) & 15u) << 4) | (((bhi >> 12) & 15u) << 8) |
+                              (((bhi >> 28) & 15u) << 12));
+        } else {
+            blo = bhi = 0;
+            ctx_bottom = ctx_right = implied_bmode(ymode) * 0x1111;
+        }
+        // ---- hand the bottom rows down: nine tagged words
+        if (!bottom && lane < W) {
             uint32_t d = 0;
-            if (lane < 4) {
+            if (lane == 8) {
+                d = (uint32_t)ctx_bottom;
+            } else if (lane < 4) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) d |= (uint32_t)s.rec[15 * 16 + 4 * lane + k] << (8 * k);
             } else {
@@ -628,7 +803,7 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
                     d |= ((uint32_t)s.ru[7 * 8 + 2 * (lane - 4) + k] << (16 * k)) |
                          ((uint32_t)s.rv[7 * 8 + 2 * (lane - 4) + k] << (16 * k + 8));
             }
-            __hip_atomic_store((gu64*)(my_line + 8 * mbx + lane), (uint64_t)d | ((uint64_t)epoch << 32), __ATOMIC_RELAXED,
+            __hip_atomic_store((gu64*)(my_line + W * mbx + lane), (uint64_t)d | ((uint64_t)epoch << 32), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         rec_words(s, g, x0, y0, lane, pwy, pwuv, psse);
@@ -636,6 +811,9 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
         pym = ymode;
         puvm = uvmode;
         pnz = nz;
+        pblo = blo;
+        pbhi = bhi;
+        lctx = ctx_right;
         // left edges of the next macroblock
         if (lane < 16) E.ly[lane] = s.rec[lane * 16 + 15];
         if (lane < 8) {
@@ -646,6 +824,137 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
         __syncthreads();
     }
     flush();
+}
+
+// ------------------------------------------------------------------ intra macroblocks in P frames
+// vp8_core.h vp8_intra_candidate, CpuVp8Encoder::intra_pass: two fully parallel passes after
+// k_vp8_inter (one wave per macroblock each).  Edges of a macroblock from the frame's
+// reconstruction with VP8's frame-edge values (lanes 0..15 luma row / column, 16..23 the chroma
+// rows, 24..31 the chroma columns, 32 the corners).
+__device__ __forceinline__ void rec_edges(KeyEdges& E, const h264::Geometry& g, const Vp8FrameState& F, int x0, int y0,
+                                          int lane) {
+    const bool top = y0 == 0, left = x0 > 0;
+    const size_t P = g.pitch;
+    if (lane < 16) {
+        E.ay[lane] = top ? 127 : F.rec_y[(size_t)(y0 - 1) * P + x0 + lane];
+        E.ly[lane] = left ? F.rec_y[(size_t)(y0 + lane) * P + x0 - 1] : 129;
+    } else if (lane < 24) {
+        const int k = lane - 16;
+        E.au[k] = top ? 127 : F.rec_uv[(size_t)(y0 / 2 - 1) * P + x0 + 2 * k];
+        E.av[k] = top ? 127 : F.rec_uv[(size_t)(y0 / 2 - 1) * P + x0 + 2 * k + 1];
+    } else if (lane < 32) {
+        const int k = lane - 24;
+        E.lu[k] = left ? F.rec_uv[(size_t)(y0 / 2 + k) * P + x0 - 2] : 129;
+        E.lvv[k] = left ? F.rec_uv[(size_t)(y0 / 2 + k) * P + x0 - 1] : 129;
+    } else if (lane == 32) {
+        E.cy = top ? 127 : (!left ? 129 : F.rec_y[(size_t)(y0 - 1) * P + x0 - 1]);
+        E.cu = top ? 127 : (!left ? 129 : F.rec_uv[(size_t)(y0 / 2 - 1) * P + x0 - 2]);
+        E.cv = top ? 127 : (!left ? 129 : F.rec_uv[(size_t)(y0 / 2 - 1) * P + x0 - 1]);
+    }
+}
+
+// 16x16 luma mode of least SAD against the staged source (ties: the lower mode), its SAD
+__device__ __forceinline__ int best_luma16(const MbLds& s, const KeyEdges& E, bool top, bool left, int lane,
+                                           uint32_t& best) {
+    const int dcy = dc_value(wsum((lane < 16 && !top ? E.ay[lane] : 0) + (lane >= 16 && lane < 32 && left ? E.ly[lane - 16] : 0)),
+                             (top ? 0 : 1) + (left ? 1 : 0), 3);
+    const int r = lane >> 2, c4 = (lane & 3) * 4;
+    int sad[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int sv = s.src[r * 16 + c4 + j];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) sad[m] += abs(sv - pred_of(m, E.ay[c4 + j], E.ly[r], E.cy, dcy));
+    }
+    int mode = 0;
+    best = ~0u;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t t = (uint32_t)wsum(sad[m]);
+        if (t < best) {
+            best = t;
+            mode = m;
+        }
+    }
+    return mode;
+}
+
+__global__ __launch_bounds__(64) void k_vp8_intra_cand(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                        const uint8_t* __restrict__ src_y,
+                                                        const uint8_t* __restrict__ src_uv,
+                                                        const Vp8Mb* __restrict__ mbs, uint8_t* __restrict__ icand) {
+    __shared__ MbLds s;
+    __shared__ KeyEdges E;
+    const Vp8FrameState& F = st->v;
+    const int mbi = blockIdx.x, lane = threadIdx.x;
+    const uint32_t psad = mbs[mbi].bmodes_hi;
+    if (psad <= kIntraMinSad) {  // (workgroup-uniform)
+        if (lane == 0) icand[mbi] = 0;
+        return;
+    }
+    const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
+    stage_src(s, g, src_y, src_uv, x0, y0, lane);
+    rec_edges(E, g, F, x0, y0, lane);
+    __syncthreads();
+    uint32_t best;
+    const int mode = best_luma16(s, E, mby == 0, mbx > 0, lane, best);
+    if (lane == 0) icand[mbi] = (uint8_t)((vp8_intra_candidate(psad, best, F.intra_lambda) ? 0x80 : 0) | mode);
+}
+
+__global__ __launch_bounds__(64) void k_vp8_intra_code(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                        const uint8_t* __restrict__ src_y,
+                                                        const uint8_t* __restrict__ src_uv, Vp8Mb* __restrict__ mbs,
+                                                        int16_t* __restrict__ lv, const uint8_t* __restrict__ icand) {
+    __shared__ MbLds s;
+    __shared__ KeyEdges E;
+    const Vp8FrameState& F = st->v;
+    const int mbi = blockIdx.x, lane = threadIdx.x;
+    const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
+    const int ic = icand[mbi];
+    // a candidate without a candidate causal neighbour (workgroup-uniform)
+    if (!(ic & 0x80) || (mbx > 0 && (icand[mbi - 1] & 0x80)) || (mby > 0 && (icand[mbi - g.mb_w] & 0x80)) ||
+        (mbx > 0 && mby > 0 && (icand[mbi - g.mb_w - 1] & 0x80)))
+        return;
+    const int seg = mbs[mbi].seg;
+    stage_src(s, g, src_y, src_uv, x0, y0, lane);
+    rec_edges(E, g, F, x0, y0, lane);
+    __syncthreads();
+    const bool top = mby == 0, left = mbx > 0;
+    const int ymode = ic & 3;
+    const int nav = top ? 0 : 1, nlf = left ? 1 : 0;
+    const int dcy = dc_value(wsum((lane < 16 && !top ? E.ay[lane] : 0) + (lane >= 16 && lane < 32 && left ? E.ly[lane - 16] : 0)),
+                             nav + nlf, 3);
+    const int dcu = dc_value(wsum((lane < 8 && !top ? E.au[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lu[lane - 8] : 0)),
+                             nav + nlf, 2);
+    const int dcv = dc_value(wsum((lane < 8 && !top ? E.av[lane] : 0) + (lane >= 8 && lane < 16 && left ? E.lvv[lane - 8] : 0)),
+                             nav + nlf, 2);
+    const int r = lane >> 2, c4 = (lane & 3) * 4, cx = lane & 7, cy = lane >> 3;
+    int uvmode = 0;
+    {
+        int sad[4];
+        const int su = s.su[cy * 8 + cx], sv = s.sv[cy * 8 + cx];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            sad[m] = abs(su - pred_of(m, E.au[cx], E.lu[cy], E.cu, dcu)) + abs(sv - pred_of(m, E.av[cx], E.lvv[cy], E.cv, dcv));
+        uint32_t best = ~0u;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t t = (uint32_t)wsum(sad[m]);
+            if (t < best) {
+                best = t;
+                uvmode = m;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = (uint8_t)pred_of(ymode, E.ay[c4 + j], E.ly[r], E.cy, dcy);
+    s.pu[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.au[cx], E.lu[cy], E.cu, dcu);
+    s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
+    __syncthreads();
+    const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, -1, seg);
+    uint32_t sse[3];
+    store_rec(s, g, F, x0, y0, lane, sse);
+    store_record(mbs + mbi, 0, 0, ymode, uvmode, nz, sse, lane, seg, 0);
 }
 
 // ------------------------------------------------------------------ loop filter (15)
@@ -770,7 +1079,7 @@ __global__ __launch_bounds__(64 * kRows) void k_vp8_lf(h264::Geometry g, const V
     // stage the row's macroblock levels and inner-edge flags
     for (int i = lane; i < g.mb_w; i += 64) {
         const Vp8Mb& m = mbs[mby * g.mb_w + i];
-        S.info[i] = (uint8_t)(F.lf_level[m.seg & 3] | (m.nz ? 0x80 : 0));
+        S.info[i] = (uint8_t)(F.lf_level[m.seg & 3] | ((m.nz || m.ymode == kBPred) ? 0x80 : 0));  // B_PRED: inner edges always
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the staged bytes before any lane reads them
     lf_sync_wave();
@@ -1075,7 +1384,7 @@ __global__ __launch_bounds__(256) void k_vp8_gather(h264::Geometry g, const Vp8M
 }  // namespace
 
 void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_t* const hp_planes[4], int hp_pitch,
-                      bool subpel, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t stream) {
+                      bool subpel, const uint8_t* src_y, const uint8_t* src_uv, hipStream_t stream, bool intra) {
     const int W = g.coded_w + 2 * h264::kHpelPad, H = g.coded_h + 2 * h264::kHpelPad;
     if (subpel)  // F (the same padded plane k_vp8_pad writes) plus the half-sample planes of the search
         h264::launch_hpel(g, b.me, hp_planes, hp_pitch, stream);
@@ -1084,6 +1393,12 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_
     h264::launch_me(g, b.me, src_y, stream);
     hipLaunchKernelGGL(k_vp8_inter, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.me.mb, b.mb,
                        b.lv);
+    if (intra) {
+        hipLaunchKernelGGL(k_vp8_intra_cand, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb,
+                           b.icand);
+        hipLaunchKernelGGL(k_vp8_intra_code, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb,
+                           b.lv, b.icand);
+    }
 }
 
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,

@@ -503,6 +503,8 @@ FrameResult Session::collect() {
     r.idr = st.idr;
     r.qp = st.qp;
     r.deblocked = st.deblocked;
+    r.db_coherent = st.db_coherent;
+    r.db_moving = st.db_moving;
     if (devclk_) {  // device clock: first kernel of the frame (render / conversion) -> end of its pack kernel
         const uint64_t t0 = ts_[fl.slot], t1 = enc_->last_t_end();
         r.gpu_ms = t1 > t0 ? (double)(t1 - t0) / clock_khz_ : 0.0;

@@ -84,6 +84,7 @@ struct FrameResult {
     double psnr_y = 0, psnr_u = 0, psnr_v = 0;  // encoder reconstruction vs source (dB, cap 99)
     double psnr_y_masked = 0;                   // luma PSNR outside SessionConfig::mask_* (0 = off)
     int deblocked = 0;                          // H.264: the in-loop filter ran on this picture
+    int db_coherent = 0, db_moving = 0;         // H.264: the picture's adaptive-filter classes (h264_deblock.h)
     std::vector<uint8_t> au;
 };
 

@@ -8,17 +8,19 @@ parsing (11, 16) with the near-vector search (16.3), token decoding with context
 dequantisation (14.1) with per-segment quantisers (9.3), inverse WHT / DCT (14.3, 14.4), 16x16 and
 chroma intra prediction with the 127 / 129 frame edges (12), and six-tap inter prediction (18).
 
-Supported: key and inter frames, 16x16 intra modes, 16x16 inter macroblocks (ZERO / NEAREST / NEAR /
-NEW vectors, last-frame reference), segmentation (segment map, absolute / delta segment quantisers
-and loop-filter levels), the normal loop filter (15), token partitions, probability updates, skip
-flags.  Raises ``NotImplementedError`` for B_PRED, SPLITMV, the simple filter, filter sharpness,
+Supported: key and inter frames, 16x16 intra modes, key-frame B_PRED macroblocks (the ten 4x4
+sub-block modes of 12.3 under the contextual key-frame probabilities, no Y2 block, the Y2 entropy
+context carried past them), 16x16 inter macroblocks (ZERO / NEAREST / NEAR / NEW vectors, last-frame
+reference), segmentation (segment map, absolute / delta segment quantisers and loop-filter levels),
+the normal loop filter (15), token partitions, probability updates, skip flags.  Raises
+``NotImplementedError`` for B_PRED in inter frames, SPLITMV, the simple filter, filter sharpness,
 mode / reference filter deltas and golden / altref references.  Slow; for test pictures.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .vp8_tables import AC_Q, COEF_PROBS0, COEF_UPDATE_PROBS, DC_Q
+from .vp8_tables import AC_Q, COEF_PROBS0, COEF_UPDATE_PROBS, DC_Q, KF_BMODE_PROB
 
 ZIGZAG = [0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15]
 BANDS = [0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0]
@@ -38,6 +40,9 @@ MODE_CONTEXTS = [[7, 1, 1, 143], [14, 18, 14, 107], [135, 64, 57, 68], [60, 56, 
 SUBPEL = [[0, 0, 128, 0, 0, 0], [0, -6, 123, 12, -1, 0], [2, -11, 108, 36, -8, 1], [0, -9, 93, 50, -6, 0],
           [3, -16, 77, 77, -16, 3], [0, -6, 50, 93, -9, 0], [1, -8, 36, 108, -11, 2], [0, -1, 12, 123, -6, 0]]
 DC_PRED, V_PRED, H_PRED, TM_PRED, B_PRED = 0, 1, 2, 3, 4
+# sub-block modes, in the bmode tree's leaf order (the index order of KF_BMODE_PROB [above][left][9])
+B_DC, B_TM, B_VE, B_HE, B_RD, B_VR, B_LD, B_VL, B_HD, B_HU = range(10)
+IMPLIED_BMODE = {DC_PRED: B_DC, V_PRED: B_VE, H_PRED: B_HE, TM_PRED: B_TM}
 
 
 class Vp8Error(Exception):
@@ -261,12 +266,23 @@ class Decoder:
                 skip = bd.bool(prob_skip) if skip_on else 0
                 if key:
                     ym = self._tree_kf_ymode(bd)
+                    if ym == B_PRED:  # 16 sub-block modes, each under its above / left sub-block's mode
+                        bm = [0] * 16
+                        for b in range(16):
+                            bx, by = b & 3, b >> 2
+                            a = bm[b - 4] if by else (mbs[(my - 1) * mw + mx]["b"][12 + bx] if my else B_DC)
+                            lm = bm[b - 1] if bx else (mbs[my * mw + mx - 1]["b"][4 * by + 3] if mx else B_DC)
+                            bm[b] = self._tree_bmode(bd, KF_BMODE_PROB[(a * 10 + lm) * 9:(a * 10 + lm) * 9 + 9])
+                        self.stats["bpred"] = self.stats.get("bpred", 0) + 1
+                    else:
+                        bm = [IMPLIED_BMODE[ym]] * 16
                     uvm = self._tree_uv(bd, KF_UVMODE_PROB)
-                    mbs.append({"inter": False, "y": ym, "uv": uvm, "skip": skip, "mv": (0, 0)})
+                    mbs.append({"inter": False, "y": ym, "uv": uvm, "skip": skip, "mv": (0, 0), "b": bm})
                     continue
                 if not bd.bool(prob_intra):
                     ym = self._tree_ymode(bd)
                     uvm = self._tree_uv(bd, self.uvmode_prob)
+                    self.stats["intra_p"] = self.stats.get("intra_p", 0) + 1
                     mbs.append({"inter": False, "y": ym, "uv": uvm, "skip": skip, "mv": (0, 0)})
                     continue
                 if bd.bool(prob_last):
@@ -313,14 +329,16 @@ class Decoder:
             left = [0] * 9
             for mx in range(mw):
                 m = mbs[my * mw + mx]
+                has_y2 = m["y"] != B_PRED
                 if m["skip"]:
                     self.stats["skip"] += 1
                     coefs = [[0] * 16 for _ in range(25)]
-                    for k in range(9):  # the MB has a Y2 block: every context resets
+                    for k in range(9 if has_y2 else 8):  # contexts reset (Y2's only with a Y2 block)
                         above[mx][k] = left[k] = 0
                 else:
-                    coefs = self._tokens(bd, above[mx], left)
-                m["coded"] = any(any(c) for c in coefs)  # inner edges are filtered
+                    coefs = self._tokens(bd, above[mx], left, has_y2)
+                # inner edges are filtered where a coefficient is coded, and always in B_PRED
+                m["coded"] = any(any(c) for c in coefs) or not has_y2
                 self._recon(Y, U, V, mx, my, m, coefs, key)
         if level:  # section 15: after the whole frame is reconstructed (intra prediction saw it unfiltered)
             self._loop_filter(Y, U, V, mbs, [lf_seg[self.seg_map[i]] if seg_on else level for i in range(mw * mh)], key)
@@ -339,7 +357,7 @@ class Decoder:
     def _tree_kf_ymode(bd):
         p = KF_YMODE_PROB
         if not bd.bool(p[0]):
-            raise NotImplementedError("B_PRED")
+            return B_PRED
         if not bd.bool(p[1]):
             return V_PRED if bd.bool(p[2]) else DC_PRED
         return TM_PRED if bd.bool(p[3]) else H_PRED
@@ -353,6 +371,24 @@ class Decoder:
         if bd.bool(p[3]):
             raise NotImplementedError("B_PRED")
         return TM_PRED
+
+    @staticmethod
+    def _tree_bmode(bd, p):  # 11.2 bmode_tree
+        if not bd.bool(p[0]):
+            return B_DC
+        if not bd.bool(p[1]):
+            return B_TM
+        if not bd.bool(p[2]):
+            return B_VE
+        if not bd.bool(p[3]):
+            if not bd.bool(p[4]):
+                return B_HE
+            return B_VR if bd.bool(p[5]) else B_RD
+        if not bd.bool(p[6]):
+            return B_LD
+        if not bd.bool(p[7]):
+            return B_VL
+        return B_HU if bd.bool(p[8]) else B_HD
 
     @staticmethod
     def _tree_uv(bd, p):
@@ -459,17 +495,21 @@ class Decoder:
             v = (v << 1) | bd.bool(p)
         return v
 
-    def _tokens(self, bd, above, left):
+    def _tokens(self, bd, above, left, has_y2=True):
         coefs = [None] * 25
         nz = lambda c, first: int(any(c[first:]))  # noqa: E731
-        c = self._block(bd, 1, 0, above[8] + left[8])
-        coefs[24] = c
-        above[8] = left[8] = nz(c, 0)
+        if has_y2:
+            c = self._block(bd, 1, 0, above[8] + left[8])
+            coefs[24] = c
+            above[8] = left[8] = nz(c, 0)
+        else:
+            coefs[24] = [0] * 16
+        typ, first = (0, 1) if has_y2 else (3, 0)
         for b in range(16):
             bx, by = b & 3, b >> 2
-            c = self._block(bd, 0, 1, above[bx] + left[by])
+            c = self._block(bd, typ, first, above[bx] + left[by])
             coefs[b] = c
-            above[bx] = left[by] = nz(c, 1)
+            above[bx] = left[by] = nz(c, first)
         for comp in range(2):
             for b in range(4):
                 bx, by = b & 1, b >> 1
@@ -489,9 +529,23 @@ class Decoder:
             half = lambda v: (v + 1) // 2 if v >= 0 else -((1 - v) // 2)  # noqa: E731
             cvx, cvy = half(m["mv"][0]), half(m["mv"][1])
             cpred = [self._inter_pred(P, x0 // 2, y0 // 2, 8, cvx, cvy) for P in self.last[1:]]
+        elif m["y"] == B_PRED:
+            cpred = [self._intra_pred(P, x0 // 2, y0 // 2, 8, m["uv"]) for P in (U, V)]
+            for b in range(16):  # raster order, each sub-block predicted from the ones before it
+                bx, by = b & 3, b >> 2
+                c = [0] * 16
+                for k in range(16):
+                    c[ZIGZAG[k]] = coefs[b][k] * (q["y1dc"] if k == 0 else q["y1ac"])
+                pr = self._bpred(Y, mx, my, bx, by, m["b"][b])
+                xs, ys = x0 + 4 * bx, y0 + 4 * by
+                Y[ys:ys + 4, xs:xs + 4] = np.clip(pr + np.array(_idct(c)).reshape(4, 4), 0, 255)
+            pred = None
         else:
             pred = self._intra_pred(Y, x0, y0, 16, m["y"])
             cpred = [self._intra_pred(P, x0 // 2, y0 // 2, 8, m["uv"]) for P in (U, V)]
+        if pred is None:
+            self._recon_chroma(U, V, x0, y0, coefs, cpred, q)
+            return
         # luma with Y2
         y2 = [0] * 16
         for k, v in enumerate(coefs[24]):
@@ -507,6 +561,10 @@ class Decoder:
             bx, by = b & 3, b >> 2
             res[by * 4:by * 4 + 4, bx * 4:bx * 4 + 4] = np.array(r).reshape(4, 4)
         Y[y0:y0 + 16, x0:x0 + 16] = np.clip(pred + res, 0, 255)
+        self._recon_chroma(U, V, x0, y0, coefs, cpred, q)
+
+    @staticmethod
+    def _recon_chroma(U, V, x0, y0, coefs, cpred, q):
         for comp, P in enumerate((U, V)):
             cres = np.zeros((8, 8), np.int64)
             for b in range(4):
@@ -516,6 +574,75 @@ class Decoder:
                 bx, by = b & 1, b >> 1
                 cres[by * 4:by * 4 + 4, bx * 4:bx * 4 + 4] = np.array(_idct(c)).reshape(4, 4)
             P[y0 // 2:y0 // 2 + 8, x0 // 2:x0 // 2 + 8] = np.clip(cpred[comp] + cres, 0, 255)
+
+    def _bpred(self, Y, mx, my, bx, by, mode):
+        """12.3: sub-block (bx, by) of macroblock (mx, my) in `mode` from the reconstruction Y.
+        Above-right: inside the macroblock from the sub-block row above; otherwise (the top row, the
+        right column) from the row above the macroblock -- the above-right macroblock's bottom row,
+        at the right frame edge the above macroblock's last sample repeated, 127 above the frame."""
+        x, y = mx * 16 + 4 * bx, my * 16 + 4 * by
+        A = [int(v) for v in Y[y - 1, x:x + 4]] if y > 0 else [127] * 4
+        if by > 0 and bx < 3:
+            A += [int(v) for v in Y[y - 1, x + 4:x + 8]]
+        elif my == 0:
+            A += [127] * 4
+        elif bx < 3:
+            A += [int(v) for v in Y[my * 16 - 1, x + 4:x + 8]]
+        elif mx + 1 < self.mw:
+            A += [int(v) for v in Y[my * 16 - 1, mx * 16 + 16:mx * 16 + 20]]
+        else:
+            A += [int(Y[my * 16 - 1, mx * 16 + 15])] * 4
+        L = [int(v) for v in Y[y:y + 4, x - 1]] if x > 0 else [129] * 4
+        P = 127 if y == 0 else (129 if x == 0 else int(Y[y - 1, x - 1]))
+        E = [L[3], L[2], L[1], L[0], P] + A  # the edge from the bottom-left around to the top-right
+        a3 = lambda a, b, c: (a + 2 * b + c + 2) >> 2  # noqa: E731
+        a2 = lambda a, b: (a + b + 1) >> 1  # noqa: E731
+        B = np.zeros((4, 4), np.int64)
+        for r in range(4):
+            for c in range(4):
+                if mode == B_DC:
+                    v = (sum(A[:4]) + sum(L) + 4) >> 3
+                elif mode == B_TM:
+                    v = min(255, max(0, L[r] + A[c] - P))
+                elif mode == B_VE:
+                    v = a3(E[4 + c], E[5 + c], E[6 + c])
+                elif mode == B_HE:
+                    v = a3(E[4 - r], E[3 - r], E[2 - r]) if r < 3 else a3(L[2], L[3], L[3])
+                elif mode == B_LD:
+                    v = a3(A[r + c], A[r + c + 1], A[min(r + c + 2, 7)])
+                elif mode == B_RD:
+                    v = a3(E[3 - r + c], E[4 - r + c], E[5 - r + c])
+                elif mode == B_VR:
+                    z = 2 * c - r
+                    if z < 0:  # down the left edge
+                        v = a3(E[4 + z], E[5 + z], E[6 + z])
+                    elif z & 1:
+                        v = a3(E[3 + (z + 1) // 2], E[4 + (z + 1) // 2], E[5 + (z + 1) // 2])
+                    else:
+                        v = a2(E[4 + z // 2], E[5 + z // 2])
+                elif mode == B_VL:
+                    if (r, c) == (2, 3):
+                        v = a3(A[4], A[5], A[6])
+                    elif (r, c) == (3, 3):
+                        v = a3(A[5], A[6], A[7])
+                    elif r & 1:
+                        v = a3(A[c + r // 2], A[c + r // 2 + 1], A[c + r // 2 + 2])
+                    else:
+                        v = a2(A[c + r // 2], A[c + r // 2 + 1])
+                elif mode == B_HD:
+                    z = 2 * r - c
+                    if z < 0:  # along the top edge
+                        v = a3(E[2 - z], E[3 - z], E[4 - z])
+                    elif z & 1:
+                        v = a3(E[3 - (z + 1) // 2], E[4 - (z + 1) // 2], E[5 - (z + 1) // 2])
+                    else:
+                        v = a2(E[3 - z // 2], E[4 - z // 2])
+                else:  # B_HU
+                    k = c + 2 * r
+                    Lx = L + [L[3], L[3]]
+                    v = L[3] if k > 5 else (a3(Lx[k // 2], Lx[k // 2 + 1], Lx[k // 2 + 2]) if k & 1 else a2(Lx[k // 2], Lx[k // 2 + 1]))
+                B[r, c] = v
+        return B
 
     @staticmethod
     def _intra_pred(P, x0, y0, n, mode):

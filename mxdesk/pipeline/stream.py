@@ -89,25 +89,29 @@ class KeyframeCoalescer:
     arrives) used to code one IDR per request.  The rules:
 
       * a request while an IDR is already pending (requested, not yet coded) joins it;
-      * a PLI / FIR / client request within ``min_interval`` of the last IDR is covered by that
-        IDR (it is still on its way to the viewer that asked) and is dropped;
+      * a PLI / FIR / client request within ``cover`` (0.1 s: about a round trip plus a frame) of
+        the last IDR is covered by that IDR (it was sent before the viewer received it) and is
+        dropped; a later one reports a loss after the IDR and schedules a new one;
       * a request that needs a *new* key frame (a new viewer, a resynchronising viewer) is kept
         but not coded before ``last IDR + min_interval``, so the IDR rate of a session is bounded
         by 1 / min_interval whatever the viewers do;
       * any IDR the encoder codes (periodic, first frame, forced) satisfies what is pending.
 
     ``min_interval`` defaults to ``MXDESK_IDR_MIN_INTERVAL`` seconds (0.25: four IDRs per second at
-    most).  Counts per reason, coalesced requests and forced IDRs are exported on ``/metrics``.
+    most), ``cover`` to ``MXDESK_IDR_COVER`` seconds (at most ``min_interval``).  Counts per reason, coalesced requests and forced IDRs are exported on ``/metrics``.
     The reference has no equivalent: ``nvh264enc`` codes an IDR per upstream force-key-unit event
     (reference Dockerfile:210, selkies-gstreamer [UP])."""
 
     COVERED_BY_RECENT = ("pli", "fir", "client")
 
     def __init__(self, min_interval_s: float | None = None, clock: Callable[[], float] = time.monotonic,
-                 metrics: SessionMetrics | None = None):
+                 metrics: SessionMetrics | None = None, cover_s: float | None = None):
         if min_interval_s is None:
             min_interval_s = float(os.environ.get("MXDESK_IDR_MIN_INTERVAL", "") or 0.25)
         self.min_interval = max(0.0, float(min_interval_s))
+        if cover_s is None:
+            cover_s = float(os.environ.get("MXDESK_IDR_COVER", "") or 0.1)
+        self.cover = min(max(0.0, float(cover_s)), self.min_interval)
         self.clock = clock
         self.metrics = metrics
         self._lock = threading.Lock()
@@ -124,7 +128,7 @@ class KeyframeCoalescer:
         now = self.clock()
         with self._lock:
             self.requests[reason] = self.requests.get(reason, 0) + 1
-            joined = self.pending or (reason in self.COVERED_BY_RECENT and now - self.last_idr_t < self.min_interval)
+            joined = self.pending or (reason in self.COVERED_BY_RECENT and now - self.last_idr_t < self.cover)
             if joined:
                 self.coalesced += 1
             else:
@@ -152,7 +156,7 @@ class KeyframeCoalescer:
     def snapshot(self) -> dict:
         with self._lock:
             return {"requests": dict(self.requests), "coalesced": self.coalesced, "forced": self.forced,
-                    "pending": self.pending, "min_interval_s": self.min_interval}
+                    "pending": self.pending, "min_interval_s": self.min_interval, "cover_s": self.cover}
 
 
 class _Subscriber:

@@ -20,11 +20,11 @@ from .test_gpu_production_sizes import _stream, desktop_nv12  # noqa: E402
 from .test_vp8 import _picture, libwebp_rgb  # noqa: E402
 
 
-def _pair(gpu, w, h, kbps=0, qp=30, sr=8, depth=1):
+def _pair(gpu, w, h, kbps=0, qp=30, sr=8, depth=1, deblock=-1):
     cfg = gpu.EncoderConfig()
     cfg.width, cfg.height, cfg.fps = w, h, 60
     cfg.bitrate_kbps, cfg.qp, cfg.search_range = kbps, qp, sr
-    cfg.pipeline_depth = depth
+    cfg.pipeline_depth, cfg.deblock = depth, deblock
     return gpu.GpuVp8Encoder(cfg, _stream()), gpu.CpuVp8Encoder(cfg)
 
 
@@ -183,3 +183,46 @@ def test_gpu_vp8_adaptive_loop_filter_1080p_pan(gpu):
     while len(out) < len(devs):
         out.append(b.collect())
     assert out == ref
+
+
+@pytest.mark.parametrize("w,h,qp,lf", [(640, 368, 20, 0), (640, 368, 34, 1), (1920, 1080, 46, 1), (100, 60, 30, 1)])
+def test_gpu_vp8_bpred_key_frames_bit_exact_vs_cpu(gpu, w, h, qp, lf):
+    """B_PRED key frames (k_vp8_key's sub-block steps, the modes handed down the wavefront as
+    contexts; the loop filter's inner edges in every B_PRED macroblock): GPU == CPU, B_PRED
+    macroblocks present, then P frames on top of the B_PRED reference."""
+    genc, cenc = _pair(gpu, w, h, qp=qp, deblock=lf)
+    frames = []
+    for t in range(3):
+        y, uv = desktop_nv12(gpu, w, h, t)
+        dy, duv = _dev(genc, y, uv)
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        _check(genc, cenc, gau, cau, w, h, t)
+        frames.append(gau)
+    if w * h > 640 * 368:  # (the pure-Python decoder: small pictures only)
+        assert genc.stats.bytes > 0
+        return
+    dec = Decoder()
+    dec.decode(frames)
+    assert dec.stats.get("bpred", 0) > 0 and dec.stats["key"] == 1
+    assert np.array_equal(dec.frames_coded[-1][0], genc.recon()[0])
+
+
+@pytest.mark.parametrize("qp,lf", [(24, 0), (44, 1)])
+def test_gpu_vp8_intra_in_inter_bit_exact_vs_cpu(gpu, qp, lf):
+    """Intra macroblocks in inter frames (k_vp8_intra_cand / k_vp8_intra_code after k_vp8_inter):
+    GPU == CPU, the stream decodes to the reconstruction, intra macroblocks present."""
+    w, h = 320, 192
+    genc, cenc = _pair(gpu, w, h, qp=qp, deblock=lf)
+    frames = []
+    for t in range(5):
+        y, uv = synthetic_nv12(w, h, t, seed=t % 3)
+        dy, duv = _dev(genc, y, uv)
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
+        cau = cenc.encode(y, uv, False)
+        _check(genc, cenc, gau, cau, w, h, t)
+        frames.append(gau)
+    dec = Decoder()
+    dec.decode(frames)
+    assert dec.stats.get("intra_p", 0) > 0
+    assert np.array_equal(dec.frames_coded[-1][0], genc.recon()[0])

@@ -24,6 +24,10 @@ def test_offer_answer_roundtrip():
 
 def test_selkies_client_gets_offer_media_and_input_channel(native, monkeypatch):
     monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    # the PLI comes a few frames after the first IDR: a short coalescing interval (the coalescer's
+    # own timing is tests/test_server.py's) so its IDR lands inside the short stream
+    monkeypatch.setenv("MXDESK_IDR_MIN_INTERVAL", "0.02")
+    monkeypatch.setenv("MXDESK_IDR_COVER", "0.01")
     cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
     from mxdesk.server.app import serve
 

@@ -259,3 +259,63 @@ def test_adaptive_loop_filter_follows_coherent_motion(native):
             assert filtered[:5] == [0] * 5 and filtered[5:] == [1] * 4, filtered
         else:
             assert sum(filtered) == want, filtered
+
+
+@pytest.mark.parametrize("qp", [20, 34, 46])
+def test_bpred_key_frame_through_libwebp(native, qp):
+    """B_PRED key frames (12.3 sub-block modes under the contextual key-frame probabilities, no Y2
+    block, type-3 luma tokens, the Y2 context carried past B_PRED macroblocks, inner loop-filter
+    edges always): on the synthetic desktop the macroblocks mix B_PRED and 16x16 modes, skipped and
+    coded; libwebp and the in-tree decoder both reproduce the reconstruction, and B_PRED saves bits
+    at equal or better PSNR."""
+    from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
+
+    w, h = 640, 368
+    y, uv = bgrx_to_nv12(CpuSyntheticDesktop(w, h, True).render(0, 0, 0))
+    out = {}
+    for bp, lf in ((0, 0), (1, 0), (1, 1)):
+        c = native.EncoderConfig()
+        c.width, c.height, c.qp, c.bitrate_kbps, c.deblock, c.vp8_bpred = w, h, qp, 0, lf, bp
+        enc = native.CpuVp8Encoder(c)
+        frame = enc.encode(y, uv)
+        ry, ruv = enc.recon()
+        dec = Decoder()
+        dec.decode([frame])
+        assert np.array_equal(dec.frames_coded[0][0], ry) and np.array_equal(dec.frames_coded[0][1], ruv[:, 0::2])
+        rgb = np.asarray(Image.open(io.BytesIO(webp_container(frame))).convert("RGB")).astype(np.int64)
+        ref = libwebp_rgb(ry[:h, :w].astype(np.int64), ruv[:h // 2, 0:w:2].astype(np.int64),
+                          ruv[:h // 2, 1:w:2].astype(np.int64))
+        assert np.array_equal(rgb, ref), int((rgb != ref).any(axis=2).sum())
+        mse = float(np.mean((ry[:h, :w].astype(float) - y) ** 2))
+        out[(bp, lf)] = (len(frame), 10 * np.log10(255 ** 2 / max(mse, 1e-9)), dec.stats.get("bpred", 0),
+                         dec.stats.get("skip", 0))
+    nb = out[(1, 0)][2]
+    assert 0 < nb < (w // 16) * (h // 16) and out[(0, 0)][2] == 0, out
+    assert out[(1, 0)][0] < out[(0, 0)][0] and out[(1, 0)][1] > out[(0, 0)][1] - 0.05, out
+
+
+@pytest.mark.parametrize("qp,lf", [(24, 0), (34, 1), (44, 1)])
+def test_intra_macroblocks_in_inter_frames(native, qp, lf):
+    """Intra macroblocks in inter frames (vp8_core.h vp8_intra_candidate: the two parallel passes
+    after the inter coding -- candidates from the inter reconstruction, then the candidates without
+    a candidate causal neighbour): the in-tree decoder parses them (is_inter_mb 0, the inter-frame
+    mode trees, intra prediction from the frame being decoded) and reproduces the reconstruction,
+    with the loop filter too; vp8_intra = 0 codes none."""
+    w, h = 320, 192
+    counts = {}
+    for vi in (0, 1):
+        c = native.EncoderConfig()
+        c.width, c.height, c.qp, c.bitrate_kbps, c.deblock, c.vp8_intra = w, h, qp, 0, lf, vi
+        enc = native.CpuVp8Encoder(c)
+        frames, recs = [], []
+        for t in range(5):
+            y, uv = synthetic_nv12(w, h, t, seed=t % 3)
+            frames.append(enc.encode(y, uv))
+            recs.append(tuple(a.copy() for a in enc.recon()))
+        dec = Decoder()
+        dec.decode(frames)
+        for t, ((yy, u, v), (ry, ruv)) in enumerate(zip(dec.frames_coded, recs)):
+            assert np.array_equal(yy, ry), f"frame {t} luma"
+            assert np.array_equal(u, ruv[:, 0::2]) and np.array_equal(v, ruv[:, 1::2]), f"frame {t} chroma"
+        counts[vi] = dec.stats.get("intra_p", 0)
+    assert counts[0] == 0 and counts[1] > 0, counts

@@ -155,6 +155,10 @@ def test_sdp_answer():
 
 def test_whep_loopback_decodes_with_nack_and_pli(native, monkeypatch):
     monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
+    # the PLI comes a few frames after the first IDR: a short coalescing interval (the coalescer's
+    # own timing is tests/test_server.py's) so its IDR lands inside the short stream
+    monkeypatch.setenv("MXDESK_IDR_MIN_INTERVAL", "0.02")
+    monkeypatch.setenv("MXDESK_IDR_COVER", "0.01")
     cfg, pipe, srv = make_server({"ENABLE_BASIC_AUTH": "false"})
     from mxdesk.server.app import serve
 
