@@ -181,8 +181,11 @@ MXHD void db_auto_count_mv(const int16_t* mv, int stride, int mb_w, int i, DbAut
     if ((i % mb_w > 0 && same(i - 1)) || (i >= mb_w && same(i - mb_w))) ++c.coherent;
 }
 MXHD bool db_auto_decide(const DbAutoCounts& c, int nmb, bool prev_on) {
+    // on when coherent motion is at least half of the motion and a tenth of the picture (off below
+    // a twelfth once on): the 1080p pan content has 15 % coherent macroblocks and gains 1.3 dB
+    // filtered, the desktop with its moving window 6.7 % and gains 0.2 dB (r06_defaults/NOTES.md)
     const uint64_t co = c.coherent;
-    return co * (prev_on ? 3u : 2u) >= (uint64_t)c.moving && co * (prev_on ? 128u : 64u) >= (uint64_t)nmb && co > 0;
+    return co * (prev_on ? 3u : 2u) >= (uint64_t)c.moving && co * (prev_on ? 12u : 10u) >= (uint64_t)nmb && co > 0;
 }
 
 // The adaptive decision at a fixed lag (ADVICE r5 h264_encoder.cpp:696): picture n is filtered

@@ -53,10 +53,12 @@ struct EncoderConfig {
                               // unchanged (profiles/r04_hevc/NOTES.md).  HEVC has 0, 1 and 3+, and treats 2
                               // as 1.  -1: the codec's default -- H.264 / VP8 4, HEVC 6 (4K 18 Mbps desktop
                               // +1.6 dB over aq 4, motion +0.1 dB, profiles/r05_hevc/NOTES.md)
-    // in-loop deblocking filter: 1 on, 0 off, 2 adaptive (per picture from its temporal classes,
-    // h264_deblock.h db_auto_decide), -1 the codec's default -- HEVC adaptive (8.7.2 is fully
-    // parallel), H.264 off (8.7 is a picture-wide wavefront, k_deblock: adaptive filtering switches
-    // it on for motion content, +1.3 dB for -76 % throughput, profiles/r05_deblock/NOTES.md), VP8
+    // in-loop deblocking filter: 1 on, 0 off, 2 adaptive (per picture from the coherent-motion
+    // classes of the picture kDbLag back, h264_deblock.h db_auto_decide), -1 the codec's default --
+    // HEVC adaptive (8.7.2 is fully parallel), H.264 adaptive (8.7 is a picture-wide wavefront,
+    // k_deblock: on when at least a tenth of the picture moves coherently, where it gains 1.3 dB,
+    // off on a mostly static desktop, where it gains 0.2 dB for -64 % single-session throughput;
+    // paced density is 200 sessions either way, profiles/r06_defaults/NOTES.md), VP8
     // off (section 15 is the same raster-order chain, k_vp8_lf: +1.4 dB on motion content for
     // -77 % throughput, profiles/r05_vp8/NOTES.md; 2 = adaptive, vp8_encoder.h LfDecision)
     int deblock = -1;
@@ -69,9 +71,9 @@ struct EncoderConfig {
         if (c.aq < 0) c.aq = def;
         return c;
     }
-    bool h264_deblock() const { return deblock > 0; }  // the filter kernels run (on, or adaptive)
-    bool h264_deblock_auto() const { return deblock == 2; }
-    int h264_deblock_mode() const { return deblock == 1 ? 1 : (deblock == 2 ? 2 : 0); }  // DbLagDecision mode
+    bool h264_deblock() const { return deblock != 0; }  // the filter kernels run (on, or adaptive)
+    bool h264_deblock_auto() const { return deblock == 2 || deblock < 0; }
+    int h264_deblock_mode() const { return deblock == 1 ? 1 : (deblock == 0 ? 0 : 2); }  // DbLagDecision mode
     bool hevc_deblock() const { return deblock != 0; }
     // HEVC's default is adaptive: deblocking costs the still desktop 0.3 dB (its text regions
     // 4.5 dB) and gains 0.2 dB on motion content at 4K 18 Mbps (profiles/r05_hevc/NOTES.md)
@@ -254,7 +256,7 @@ class GpuH264Encoder final : public VideoEncoder {
     void record_start() override;
     void record_done() override;
     // depth-2 graph form (VideoEncoder): deblocking needs an extra event inside the entropy
-    // chain, so the split form is offered only with the filter off (the default)
+    // chain, so the split form is offered only with the filter off (Session sets it off for graphs)
     bool supports_split() const override { return !cfg_.h264_deblock(); }
     bool masked_sse_in_encoder() const override { return true; }
     int prep_slot() const override { return prep_slot_; }

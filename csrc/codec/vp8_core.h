@@ -337,10 +337,8 @@ MXV8 int bpred_px(int m, const int* X, int x, int y) {
 MXV8 bool bmode_allowed(int m, int bx, int mbx, int mby, int mb_w) {
     return !(bx == 3 && mby > 0 && mbx + 1 < mb_w && (m == kBVe || m == kBLd || m == kBVl));
 }
-// Cost in 1/256 bit of sub-block mode m in a key frame after above / left modes a / l (the bmode
-// tree under kKfBModeProb[a][l])
-MXV8 int bmode_cost256(int m, int a, int l) {
-    const uint8_t* p = kKfBModeProb + (a * kNumBModes + l) * 9;
+// Cost in 1/256 bit of sub-block mode m through the bmode tree under probabilities p[9]
+MXV8 int bmode_tree_cost256(int m, const uint8_t* p) {
     if (m == kBDc) return branch_cost(p[0], 0);
     int c = branch_cost(p[0], 1);
     if (m == kBTm) return c + branch_cost(p[1], 0);
@@ -358,6 +356,12 @@ MXV8 int bmode_cost256(int m, int a, int l) {
     if (m == kBVl) return c + branch_cost(p[7], 0);
     return c + branch_cost(p[7], 1) + branch_cost(p[8], m == kBHu);
 }
+// ... after above / left modes a / l in a key frame (kKfBModeProb[a][l]: what the writer codes)
+MXV8 int bmode_cost256(int m, int a, int l) { return bmode_tree_cost256(m, kKfBModeProb + (a * kNumBModes + l) * 9); }
+// ... without contexts: the plan's estimate (the context-free sub-block mode probabilities VP8 uses
+// in inter frames; the plan runs before any neighbour's modes are known)
+constexpr uint8_t kBModeProbPlan[9] = {120, 90, 79, 133, 87, 85, 80, 111, 151};
+MXV8 int bmode_plan_cost256(int m) { return bmode_tree_cost256(m, kBModeProbPlan); }
 
 // ---------------------------------------------------------------- inter prediction (18.3)
 // Six-tap sub-sample filters by 1/8-sample phase; luma vectors are quarter-sample (even phases),
@@ -615,32 +619,42 @@ MXV8 int bctx_left(const Vp8Mb* mbs, int mb_w, int mbx, int mby, int by) {
     const Vp8Mb& n = mbs[mby * mb_w + mbx - 1];
     return n.ymode == kBPred ? bmode_of(n, 4 * by + 3) : implied_bmode(n.ymode);
 }
-// B_PRED luma of a key-frame macroblock, closed loop (the serial reference of k_vp8_key's
-// sub-block steps): every sub-block in raster order takes the allowed mode (bmode_allowed) of least
-// 256 SAD + lam * bmode_cost256 under its above / left contexts (the lower mode on ties), then is
-// coded (code_sub4) into rec (16x16 raster) and lv blocks 0..15, so the next one predicts from it.
-// src: the macroblock's source (pitch); at(x, y): the frame's reconstruction outside the macroblock;
-// actx / lctx: bctx_above / bctx_left of the macroblock.  Returns the summed cost plus the B_PRED
-// luma mode bits (same units as 256 SAD + lam * kf_ymode_cost256 of a 16x16 mode); the modes packed
-// 4 bits each into lo (0..7) / hi (8..15); the blocks' non-zero bits in *nz.
-template <class F>
-inline uint32_t bpred_luma(const uint8_t* src, int pitch, const F& at, int mbx, int mby, int mb_w, const Quant& Q,
-                           int lam, const int* actx, const int* lctx, int16_t* lv, int* rec, uint32_t* lo,
-                           uint32_t* hi, uint32_t* nz) {
+// B_PRED plan of a key-frame macroblock, open loop -- every macroblock at once (k_vp8_bpred_plan:
+// one wave per macroblock, ahead of the k_vp8_key wavefront): predictions from the *source*
+// neighbours with the frame-edge rules; each sub-block takes the allowed mode (bmode_allowed) of
+// least 256 SAD + lam * bmode_plan_cost256 (the lower mode on ties), and the macroblock goes B_PRED
+// when their sum plus the B_PRED mode bits is below the best 16x16 mode's 256 SAD + lam * mode bits.
+// src(x, y): the source luma.  Modes packed 4 bits each into lo (0..7) / hi (8..15).
+template <class S>
+MXV8 bool bpred_plan(const S& src, int mbx, int mby, int mb_w, int lam, uint32_t* lo, uint32_t* hi) {
     const int x0 = mbx * 16, y0 = mby * 16;
-    auto px = [&](int x, int y) {  // reconstruction: this macroblock's coded sub-blocks, else the frame
-        return x >= x0 && x < x0 + 16 && y >= y0 && y < y0 + 16 ? rec[(y - y0) * 16 + x - x0] : at(x, y);
-    };
-    int modes[16];
-    uint32_t total = (uint32_t)(lam * kf_ymode_cost256(kBPred));
+    Edge e;
+    e.have_above = y0 > 0;
+    e.have_left = x0 > 0;
+    for (int i = 0; i < 16; ++i) {
+        e.above[i] = y0 > 0 ? src(x0 + i, y0 - 1) : 127;
+        e.left[i] = x0 > 0 ? src(x0 - 1, y0 + i) : 129;
+    }
+    e.corner = y0 == 0 ? 127 : (x0 == 0 ? 129 : src(x0 - 1, y0 - 1));
+    const int dc = dc_of(e, 16);
+    uint32_t cost16 = ~0u;
+    for (int m = 0; m < 4; ++m) {
+        uint32_t sad = 0;
+        for (int y = 0; y < 16; ++y)
+            for (int x = 0; x < 16; ++x) {
+                const int d = src(x0 + x, y0 + y) - pred_px(m, e, 16, x, y, dc);
+                sad += (uint32_t)(d < 0 ? -d : d);
+            }
+        const uint32_t c = 256u * sad + (uint32_t)(lam * kf_ymode_cost256(m));
+        if (c < cost16) cost16 = c;
+    }
+    uint32_t costb = (uint32_t)(lam * kf_ymode_cost256(kBPred));
     *lo = *hi = 0;
-    *nz = 0;
     for (int b = 0; b < 16; ++b) {
         const int bx = b & 3, by = b >> 2;
-        const SubEdge e = sub_edge(px, mbx, mby, mb_w, bx, by);
+        const SubEdge se = sub_edge(src, mbx, mby, mb_w, bx, by);
         int X[15];
-        bpred_edge(e, X);
-        const int a = by > 0 ? modes[b - 4] : actx[bx], l = bx > 0 ? modes[b - 1] : lctx[by];
+        bpred_edge(se, X);
         uint32_t best = ~0u;
         int bm = kBDc;
         for (int m = 0; m < kNumBModes; ++m) {
@@ -648,32 +662,52 @@ inline uint32_t bpred_luma(const uint8_t* src, int pitch, const F& at, int mbx, 
             uint32_t sad = 0;
             for (int y = 0; y < 4; ++y)
                 for (int x = 0; x < 4; ++x) {
-                    const int d = (int)src[(by * 4 + y) * pitch + bx * 4 + x] - bpred_px(m, X, x, y);
+                    const int d = src(x0 + bx * 4 + x, y0 + by * 4 + y) - bpred_px(m, X, x, y);
                     sad += (uint32_t)(d < 0 ? -d : d);
                 }
-            const uint32_t c = 256u * sad + (uint32_t)(lam * bmode_cost256(m, a, l));
+            const uint32_t c = 256u * sad + (uint32_t)(lam * bmode_plan_cost256(m));
             if (c < best) {
                 best = c;
                 bm = m;
             }
         }
-        modes[b] = bm;
-        total += best;
+        costb += best;
+        if (b < 8)
+            *lo |= (uint32_t)bm << (4 * b);
+        else
+            *hi |= (uint32_t)bm << (4 * (b - 8));
+    }
+    return costb < cost16;
+}
+// B_PRED luma of a planned macroblock, closed loop: the sub-blocks in raster order, each predicted
+// in its planned mode from the reconstruction (this macroblock's earlier sub-blocks included) and
+// coded (code_sub4) into rec (16x16 raster) and lv blocks 0..15.  src: the macroblock's source
+// (pitch); at(x, y): the frame's reconstruction outside the macroblock.  Returns the blocks'
+// non-zero bits.
+template <class F>
+inline uint32_t bpred_code(const uint8_t* src, int pitch, const F& at, int mbx, int mby, int mb_w, const Quant& Q,
+                           uint32_t lo, uint32_t hi, int16_t* lv, int* rec) {
+    const int x0 = mbx * 16, y0 = mby * 16;
+    auto px = [&](int x, int y) {
+        return x >= x0 && x < x0 + 16 && y >= y0 && y < y0 + 16 ? rec[(y - y0) * 16 + x - x0] : at(x, y);
+    };
+    uint32_t nz = 0;
+    for (int b = 0; b < 16; ++b) {
+        const int bx = b & 3, by = b >> 2;
+        const int bm = (int)(((b < 8 ? lo >> (4 * b) : hi >> (4 * (b - 8)))) & 15u);
+        int X[15];
+        bpred_edge(sub_edge(px, mbx, mby, mb_w, bx, by), X);
         int res[16], pred[16], r4[16];
         for (int y = 0; y < 4; ++y)
             for (int x = 0; x < 4; ++x) {
                 pred[y * 4 + x] = bpred_px(bm, X, x, y);
                 res[y * 4 + x] = (int)src[(by * 4 + y) * pitch + bx * 4 + x] - pred[y * 4 + x];
             }
-        if (code_sub4(res, pred, Q, lv + b * 16, r4)) *nz |= 1u << b;
+        if (code_sub4(res, pred, Q, lv + b * 16, r4)) nz |= 1u << b;
         for (int y = 0; y < 4; ++y)
             for (int x = 0; x < 4; ++x) rec[(by * 4 + y) * 16 + bx * 4 + x] = r4[y * 4 + x];
-        if (b < 8)
-            *lo |= (uint32_t)bm << (4 * b);
-        else
-            *hi |= (uint32_t)bm << (4 * (b - 8));
     }
-    return total;
+    return nz;
 }
 
 // ---------------------------------------------------------------- intra macroblocks in inter frames

@@ -81,22 +81,13 @@ void CpuVp8Encoder::analyse(const uint8_t* sy, const uint8_t* suv, int pitch, bo
                 }
                 for (int y = 0; y < 16; ++y)
                     for (int x = 0; x < 16; ++x) pred[y * 16 + x] = pred_px(m.ymode, e, 16, x, y, dc);
-                if (cfg_.vp8_bpred) {  // B_PRED when its sub-block predictions + mode bits cost less
-                    const int lam = h264::lambda_sad(qp);
-                    int actx[4], lctx[4];
-                    for (int k = 0; k < 4; ++k) {
-                        actx[k] = bctx_above(mb_.data(), mb_w_, mbx, mby, k);
-                        lctx[k] = bctx_left(mb_.data(), mb_w_, mbx, mby, k);
-                    }
+                uint32_t lo = 0, hi = 0;  // B_PRED: the open-loop plan, then the closed-loop coding
+                auto src = [&](int x, int y) { return (int)sy[(size_t)y * pitch + x]; };
+                if (cfg_.vp8_bpred && bpred_plan(src, mbx, mby, mb_w_, h264::lambda_sad(qp), &lo, &hi)) {
                     auto at = [&](int x, int y) { return (int)ry[(size_t)y * cw_ + x]; };
-                    uint32_t lo, hi, bnz;
-                    const uint32_t costb = bpred_luma(sy + (size_t)y0 * pitch + x0, pitch, at, mbx, mby, mb_w_, Q, lam, actx,
-                                                      lctx, lv, rec, &lo, &hi, &bnz);
-                    if (costb < 256u * best + (uint32_t)(lam * kf_ymode_cost256(m.ymode))) {
-                        m.ymode = kBPred;
-                        set_bmodes(m, lo, hi);
-                        bpred_nz = bnz;
-                    }
+                    m.ymode = kBPred;
+                    set_bmodes(m, lo, hi);
+                    bpred_nz = bpred_code(sy + (size_t)y0 * pitch + x0, pitch, at, mbx, mby, mb_w_, Q, lo, hi, lv, rec);
                 }
                 const Edge eu = edge_of(ruv, cw_, 2, 0, x0 / 2, y0 / 2, 8), ev = edge_of(ruv, cw_, 2, 1, x0 / 2, y0 / 2, 8);
                 const int du = dc_of(eu, 8), dv = dc_of(ev, 8);

@@ -260,7 +260,7 @@ class CpuVp8Encoder {
 };
 
 // Device layout of the GPU encoder
-constexpr int kKeyLineWords = 9;  // k_vp8_key hand-off words per macroblock
+constexpr int kKeyLineWords = 8;  // k_vp8_key hand-off words per macroblock
 struct Vp8FrameState {
     const uint8_t* ref_y;   // previous reconstruction (P frames)
     const uint8_t* ref_uv;
@@ -291,8 +291,7 @@ struct Vp8DeviceBuffers {
     Vp8States* st;         // device copy of the frame states
     Vp8Mb* mb;             // [nmb] records (device)
     int16_t* lv;           // [nmb * 400] levels (device)
-    uint64_t* line;        // [mb_h][mb_w][kKeyLineWords] key-frame hand-off: bottom luma + chroma rows and
-                           // the bottom sub-block modes (B_PRED contexts), epoch-tagged
+    uint64_t* line;        // [mb_h][mb_w][kKeyLineWords] key-frame hand-off: bottom luma + chroma rows, epoch-tagged
     int* err;              // mapped host word: nonzero if a wavefront spin timed out
     unsigned long long* lf_line;  // loop-filter hand-off lines (k_vp8_lf: epoch-tagged, per workgroup) + scratch
     unsigned long long* lf_sse;  // mapped host [mb_h][3]: Y / U / V distortion of the filtered picture
@@ -309,7 +308,7 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_
                       const uint8_t* src_uv, hipStream_t stream, bool intra = false);
 // Key frames: one wave per macroblock row, rows handing their bottom edges down (wavefront).
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                    hipStream_t stream, bool save_src);
+                    hipStream_t stream, bool save_src, bool bpred = false);
 // Loop filter of the reconstruction in place (Vp8FrameState::lf_level), its distortion per row.
 void launch_vp8_lf(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
                    hipStream_t stream);

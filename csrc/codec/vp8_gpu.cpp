@@ -242,7 +242,7 @@ void GpuVp8Encoder::enqueue_body(bool key, const uint8_t* src_y, const uint8_t* 
     Slot& s = slots_[prep_slot_];
     HIP_CHECK(hipMemcpyAsync(s.buf.st, s.st_host, sizeof(Vp8States), hipMemcpyHostToDevice, stream_));
     if (key)
-        launch_vp8_key(geom_, s.buf, src_y, src_uv, stream_, cfg_.aq >= 3);
+        launch_vp8_key(geom_, s.buf, src_y, src_uv, stream_, cfg_.aq >= 3, cfg_.vp8_bpred != 0);
     else
     {
         uint8_t* const planes[4] = {hp_, hp_sub_[0], hp_sub_[1], hp_sub_[2]};

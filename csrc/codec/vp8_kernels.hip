@@ -455,44 +455,77 @@ __global__ __launch_bounds__(256) void k_vp8_save_src(h264::Geometry g, const Vp
 struct KeyEdges {
     int ay[16], ly[16], au[8], lu[8], av[8], lvv[8];
     int cy, cu, cv;
-    int actx;  // B_PRED contexts: the above macroblock's bottom sub-block modes, 4 bits each
 };
-// B_PRED sub-block steps: the edge array (vp8_core.h bpred_edge) and the transform's stages
-struct BpLds {
-    int X[16];
-    int T[4][16];
-};
-// raster position -> scan index (the inverse of kZigzag)
-constexpr uint8_t kInvZigzag[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
-
-// Wave minimum, every lane gets it (whole wave active): wsum's network with min.
-__device__ __forceinline__ uint32_t wmin(uint32_t v) {
-    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));
-    const auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    const uint32_t u = min(r16[0], r16[1]);
-    const auto r32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return min(r32[0], r32[1]);
+__device__ __forceinline__ int pred_of(int mode, int above, int left, int corner, int dc) {
+    switch (mode) {
+        case kVPred:
+            return above;
+        case kHPred:
+            return left;
+        case kTmPred:
+            return v8_clamp255(left + above - corner);
+        default:
+            return dc;
+    }
 }
 
-// B_PRED luma of the staged macroblock (vp8_core.h bpred_luma, step for step): 16 sub-blocks in
-// raster order; per sub-block lanes 0..14 gather the edge array, lanes 0..39 price the ten modes
-// (mode lane / 4, sample row lane % 4; the allowed mode of least 256 SAD + lam * bits, the lower
-// on ties, by one wave minimum of cost << 4 | mode), lanes 0..15 code the chosen one (one sample
-// each: forward DCT, quantiser, inverse DCT through the BpLds stages) into s.rec and the levels of
-// blocks 0..15.  Returns the summed cost (+ the B_PRED mode bits); modes packed into lo / hi, the
-// blocks' non-zero bits into *nz (all wave-uniform).
-__device__ uint32_t bpred_mb(MbLds& s, BpLds& B, const KeyEdges& E, const Vp8FrameState& F, int16_t* __restrict__ lv,
-                             int lane, int mbx, int mby, int mb_w, int lctx, uint32_t& lo, uint32_t& hi, uint32_t& nz) {
-    const int lam = F.bpred_lambda;
+__device__ __forceinline__ int dc_value(int sum, int cnt, int log2n) {
+    if (cnt == 0) return 128;
+    const int shift = log2n + cnt;
+    return (sum + (1 << (shift - 1))) >> shift;
+}
+
+// B_PRED sub-block steps of k_vp8_key: the edge array (vp8_core.h bpred_edge)
+struct BpLds {
+    int X[16];
+};
+__device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes before its later reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// raster position -> scan index (the inverse of kZigzag), 4 bits each
+constexpr uint64_t kInvZigzagPacked = 0xFEA9DB83C7426510ull;
+// v[i] of i in 0..3 as bitwise blends (no select the compiler could turn into a branch)
+__device__ __forceinline__ int pick4(int i, int a, int b, int c, int d) {
+    return (a & -(int)(i == 0)) | (b & -(int)(i == 1)) | (c & -(int)(i == 2)) | (d & -(int)(i == 3));
+}
+// quad broadcast of lane 4 (l / 4) + k; rotation within a row of 16: lane i <- lane (i - n) & 15
+template <int k>
+__device__ __forceinline__ int qbc(int v) { return __builtin_amdgcn_mov_dpp(v, k * 0x55, 0xF, 0xF, false); }
+template <int n>
+__device__ __forceinline__ int rror(int v) { return __builtin_amdgcn_mov_dpp(v, 0x120 + n, 0xF, 0xF, false); }
+// the values of column c (rows 0..3) for lane 4 r + c of every 16-lane row: rows r, r-1, r-2, r-3
+// arrive by rotations 0 / 4 / 8 / 12 and are put in row order with bitwise blends (no selects
+// of DPP results: the compiler may sink those into divergent branches)
+__device__ __forceinline__ void col4(int v, int r, int out[4]) {
+    const int v1 = rror<4>(v), v2 = rror<8>(v), v3 = rror<12>(v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int d = (r - k) & 3;
+        out[k] = (v & -(int)(d == 0)) | (v1 & -(int)(d == 1)) | (v2 & -(int)(d == 2)) | (v3 & -(int)(d == 3));
+    }
+}
+
+// B_PRED luma of the staged macroblock in its planned modes (vp8_core.h bpred_code): 16 sub-blocks
+// in raster order; per sub-block lanes 0..14 gather the edge array from s.rec / the edges, then
+// every 16-lane row computes the sub-block (lane 4 r + c: sample (c, r)) -- prediction, forward
+// DCT (rows by quad broadcasts, columns by row rotations), quantiser, inverse DCT -- and lanes
+// 0..15 store the levels of block b and the reconstruction into s.rec.  No workgroup barrier:
+// one wave, its LDS operations in order.  taplo / taphi: kBPredTap of this lane's sample for the
+// modes B_VE .. B_HE / B_RD .. B_HU, a byte each.  Returns the blocks' non-zero bits.
+__device__ uint32_t bpred_code_gpu(MbLds& s, BpLds& B, const KeyEdges& E, const Vp8FrameState& F,
+                                   int16_t* __restrict__ lv, int lane, int mbx, int mby, uint32_t lo, uint32_t hi,
+                                   uint32_t taplo, uint32_t taphi) {
     const bool top = mby == 0, left = mbx > 0;
-    uint32_t total = (uint32_t)(lam * kf_ymode_cost256(kBPred));
-    lo = hi = nz = 0;
-    const int r = (lane >> 2) & 3, c = lane & 3;
+    const int q = lane & 15, r = q >> 2, c = q & 3;
+    const int qdc = F.q[0][0], qac = F.q[0][1];
+    const uint32_t mdc = F.qm[0][0], mac = F.qm[0][1];
+    const int kq = (int)((kInvZigzagPacked >> (4 * q)) & 15u);
+    uint32_t nz = 0;
     for (int b = 0; b < 16; ++b) {
         const int bx = b & 3, by = b >> 2, xs = bx * 4, ys = by * 4;
+        const int bm = (int)(((b < 8 ? lo >> (4 * b) : hi >> (4 * (b - 8)))) & 15u);  // (uniform)
         if (lane < 15) {  // X: L3 L3 L2 L1 L0 P A0 .. A7 A7
             int v;
             if (lane <= 4) {
@@ -514,102 +547,147 @@ __device__ uint32_t bpred_mb(MbLds& s, BpLds& B, const KeyEdges& E, const Vp8Fra
                 else if (bx < 3)
                     v = E.ay[xs + i];
                 else
-                    v = mbx + 1 < mb_w ? 0 : E.ay[15];  // (0: read by no allowed mode, bmode_allowed)
+                    v = E.ay[15];  // (the right column: only at the frame's right edge may a mode read it)
             }
             B.X[lane] = v;
         }
-        __syncthreads();
-        auto mode_at = [&](int k) { return (int)((k < 8 ? lo >> (4 * k) : hi >> (4 * (k - 8))) & 15u); };
-        const int a = by > 0 ? mode_at(b - 4) : (E.actx >> (4 * bx)) & 15;
-        const int l = bx > 0 ? mode_at(b - 1) : (lctx >> (4 * by)) & 15;
-        // ---- mode search (lanes 4m .. 4m + 3: mode m, rows 0..3)
-        const int m = lane >> 2, sr = lane & 3;
-        int sad = 0;
-        if (lane < 40)
+        wave_lds_sync();
+        int pred;
+        if (bm == kBDc) {
+            pred = (B.X[6] + B.X[7] + B.X[8] + B.X[9] + B.X[1] + B.X[2] + B.X[3] + B.X[4] + 4) >> 3;
+        } else if (bm == kBTm) {
+            pred = v8_clamp255(B.X[4 - r] + B.X[6 + c] - B.X[5]);
+        } else {
+            const int t = (int)(((bm < 6 ? taplo >> (8 * (bm - 2)) : taphi >> (8 * (bm - 6)))) & 0xffu), k = t & 15;
+            pred = (t & 16) ? (B.X[k] + 2 * B.X[k + 1] + B.X[k + 2] + 2) >> 2 : (B.X[k] + B.X[k + 1] + 1) >> 1;
+        }
+        const int res = (int)s.src[(ys + r) * 16 + xs + c] - pred;
+        // forward DCT (vp8_core.h fdct4x4): rows, then columns
+        int t;
+        {
+            const int i0 = qbc<0>(res), i1 = qbc<1>(res), i2 = qbc<2>(res), i3 = qbc<3>(res);
+            const int a1 = (i0 + i3) * 8, b1 = (i1 + i2) * 8, c1 = (i1 - i2) * 8, d1 = (i0 - i3) * 8;
+            const int o0 = a1 + b1, o2 = a1 - b1, o1 = (c1 * 2217 + d1 * 5352 + 14500) >> 12,
+                      o3 = (d1 * 2217 - c1 * 5352 + 7500) >> 12;
+            t = pick4(c, o0, o1, o2, o3);
+        }
+        int co;
+        {
+            int tc[4];
+            col4(t, r, tc);
+            const int a1 = tc[0] + tc[3], b1 = tc[1] + tc[2], c1 = tc[1] - tc[2], d1 = tc[0] - tc[3];
+            const int o0 = (a1 + b1 + 7) >> 4, o2 = (a1 - b1 + 7) >> 4;
+            const int o1 = ((c1 * 2217 + d1 * 5352 + 12000) >> 16) + (d1 != 0 ? 1 : 0);
+            const int o3 = (d1 * 2217 - c1 * 5352 + 51000) >> 16;
+            co = pick4(r, o0, o1, o2, o3);
+        }
+        // quantiser (type 3: the DC at Y1 DC), levels in scan order
+        const int qs = q == 0 ? qdc : qac;
+        const int lvl = qz(co, qs, q == 0 ? mdc : mac);
+        if (lane < 16) lv[b * 16 + kq] = (int16_t)lvl;
+        if (__ballot(lane < 16 && lvl != 0)) nz |= 1u << b;
+        const int dq = lvl * qs;
+        // inverse DCT (vp8_core.h idct4x4): columns, then rows
+        constexpr int c8 = 20091, s8 = 35468;
+        int u;
+        {
+            int ic[4];
+            col4(dq, r, ic);
+            const int a1 = ic[0] + ic[2], b1 = ic[0] - ic[2];
+            const int c1 = ((ic[1] * s8) >> 16) - (ic[3] + ((ic[3] * c8) >> 16));
+            const int d1 = (ic[1] + ((ic[1] * c8) >> 16)) + ((ic[3] * s8) >> 16);
+            u = pick4(r, a1 + d1, b1 + c1, b1 - c1, a1 - d1);
+        }
+        {
+            const int p0 = qbc<0>(u), p1 = qbc<1>(u), p2 = qbc<2>(u), p3 = qbc<3>(u);
+            const int a1 = p0 + p2, b1 = p0 - p2;
+            const int c1 = ((p1 * s8) >> 16) - (p3 + ((p3 * c8) >> 16));
+            const int d1 = (p1 + ((p1 * c8) >> 16)) + ((p3 * s8) >> 16);
+            const int o = pick4(c, (a1 + d1 + 4) >> 3, (b1 + c1 + 4) >> 3, (b1 - c1 + 4) >> 3, (a1 - d1 + 4) >> 3);
+            if (lane < 16) s.rec[(ys + r) * 16 + xs + c] = (uint8_t)v8_clamp255(pred + o);
+        }
+        wave_lds_sync();
+    }
+    return nz;
+}
+
+// B_PRED plans of every macroblock of a key frame (vp8_core.h bpred_plan), one wave per
+// macroblock, ahead of the k_vp8_key wavefront: the source footprint staged in LDS, lane
+// 4 b + r = sub-block b, sample row r, the ten modes in turn; the plan goes into the record
+// (ymode kBPred or 0, the modes in the vector words and bmodes_hi), which k_vp8_key reads
+// before it writes the macroblock's final record.
+__global__ __launch_bounds__(256) void k_vp8_bpred_plan(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                        const uint8_t* __restrict__ src_y, Vp8Mb* __restrict__ mbs) {
+    __shared__ int Xs[4][16][16];
+    __shared__ uint8_t tile[4][17][21];  // rows y0 - 1 .. y0 + 15, columns x0 - 1 .. x0 + 19
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mbi = blockIdx.x * 4 + wave;
+    if (mbi >= g.mb_w * g.mb_h) return;  // (wave-uniform; wave-level LDS ordering only below)
+    const Vp8FrameState& F = st->v;
+    const int lam = F.bpred_lambda;
+    const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
+    for (int i = lane; i < 17 * 21; i += 64) {
+        const int rr = i / 21, cc = i - rr * 21, x = x0 - 1 + cc, y = y0 - 1 + rr;
+        tile[wave][rr][cc] = (x >= 0 && y >= 0 && x < g.coded_w) ? src_y[(size_t)y * g.pitch + x] : 0;
+    }
+    wave_lds_sync();
+    auto src = [&](int x, int y) { return (int)tile[wave][y - y0 + 1][x - x0 + 1]; };
+    const int b = lane >> 2, rr = lane & 3, bx = b & 3, by = b >> 2;
+    if (rr == 0) {
+        int X[15];
+        bpred_edge(sub_edge(src, mbx, mby, g.mb_w, bx, by), X);
 #pragma unroll
-            for (int x = 0; x < 4; ++x) sad += abs((int)s.src[(ys + sr) * 16 + xs + x] - bpred_px(m, B.X, x, sr));
+        for (int i = 0; i < 15; ++i) Xs[wave][b][i] = X[i];
+    }
+    // 16x16 modes (lane: row lane / 4, columns 4 (lane % 4) .. + 3)
+    const bool at = y0 > 0, al = x0 > 0;
+    const int r16 = lane >> 2, c4 = (lane & 3) * 4;
+    const int corner = !at ? 127 : (!al ? 129 : src(x0 - 1, y0 - 1));
+    const int lft = al ? src(x0 - 1, y0 + r16) : 129;
+    const int dcy = dc_value(wsum((lane < 16 && at ? src(x0 + lane, y0 - 1) : 0) + (lane >= 16 && lane < 32 && al ? src(x0 - 1, y0 + lane - 16) : 0)),
+                             (at ? 1 : 0) + (al ? 1 : 0), 3);
+    uint32_t cost16 = ~0u;
+    {
+        int sad[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int sv = src(x0 + c4 + j, y0 + r16), abv = at ? src(x0 + c4 + j, y0 - 1) : 127;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) sad[m] += abs(sv - pred_of(m, abv, lft, corner, dcy));
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t cst = 256u * (uint32_t)wsum(sad[m]) + (uint32_t)(lam * kf_ymode_cost256(m));
+            cost16 = cst < cost16 ? cst : cost16;
+        }
+    }
+    wave_lds_sync();
+    // sub-block modes
+    uint32_t best = ~0u;
+    int bm = kBDc;
+    const int* X = Xs[wave][b];
+    for (int m = 0; m < kNumBModes; ++m) {
+        int sad = 0;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) sad += abs(src(x0 + bx * 4 + x, y0 + by * 4 + rr) - bpred_px(m, X, x, rr));
         sad += __builtin_amdgcn_mov_dpp(sad, 0xB1, 0xF, 0xF, false);
         sad += __builtin_amdgcn_mov_dpp(sad, 0x4E, 0xF, 0xF, false);
-        uint32_t key = 0xffffffffu;
-        if (lane < 40 && bmode_allowed(m, bx, mbx, mby, mb_w))
-            key = ((256u * (uint32_t)sad + (uint32_t)(lam * bmode_cost256(m, a, l))) << 4) | (uint32_t)m;
-        key = __builtin_amdgcn_readfirstlane(wmin(key));
-        const int bm = (int)(key & 15u);
-        total += key >> 4;
-        if (b < 8)
-            lo |= (uint32_t)bm << (4 * b);
-        else
-            hi |= (uint32_t)bm << (4 * (b - 8));
-        // ---- coding (lanes 0..15: sample (c, r) of the sub-block)
-        const bool cl = lane < 16;
-        const int pred = cl ? bpred_px(bm, B.X, c, r) : 0;
-        if (cl) B.T[0][lane] = (int)s.src[(ys + r) * 16 + xs + c] - pred;
-        __syncthreads();
-        if (cl) {  // forward DCT, rows (vp8_core.h fdct4x4)
-            const int* ip = B.T[0] + 4 * r;
-            const int a1 = (ip[0] + ip[3]) * 8, b1 = (ip[1] + ip[2]) * 8, c1 = (ip[1] - ip[2]) * 8, d1 = (ip[0] - ip[3]) * 8;
-            B.T[1][lane] = c == 0 ? a1 + b1
-                           : c == 2 ? a1 - b1
-                           : c == 1 ? (c1 * 2217 + d1 * 5352 + 14500) >> 12
-                                    : (d1 * 2217 - c1 * 5352 + 7500) >> 12;
+        const uint32_t cst = 256u * (uint32_t)sad + (uint32_t)(lam * bmode_plan_cost256(m));
+        if (bmode_allowed(m, bx, mbx, mby, g.mb_w) && cst < best) {
+            best = cst;
+            bm = m;
         }
-        __syncthreads();
-        bool lnz = false;
-        if (cl) {  // columns, then the quantiser (DC at Y1 DC: type 3, no Y2)
-            const int* t = B.T[1];
-            const int a1 = t[c] + t[12 + c], b1 = t[4 + c] + t[8 + c], c1 = t[4 + c] - t[8 + c], d1 = t[c] - t[12 + c];
-            const int co = r == 0 ? (a1 + b1 + 7) >> 4
-                           : r == 2 ? (a1 - b1 + 7) >> 4
-                           : r == 1 ? ((c1 * 2217 + d1 * 5352 + 12000) >> 16) + (d1 != 0 ? 1 : 0)
-                                    : (d1 * 2217 - c1 * 5352 + 51000) >> 16;
-            const int qi = lane == 0 ? 0 : 1;
-            const int lvl = qz(co, F.q[0][qi], F.qm[0][qi]);
-            lv[b * 16 + kInvZigzag[lane]] = (int16_t)lvl;
-            B.T[2][lane] = lvl * F.q[0][qi];
-            lnz = lvl != 0;
-        }
-        if (__ballot(lnz)) nz |= 1u << b;
-        __syncthreads();
-        constexpr int c8 = 20091, s8 = 35468;
-        if (cl) {  // inverse DCT, columns (vp8_core.h idct4x4)
-            const int* in = B.T[2];
-            const int i0 = in[c], i4 = in[4 + c], i8 = in[8 + c], i12 = in[12 + c];
-            const int a1 = i0 + i8, b1 = i0 - i8;
-            const int c1 = ((i4 * s8) >> 16) - (i12 + ((i12 * c8) >> 16));
-            const int d1 = (i4 + ((i4 * c8) >> 16)) + ((i12 * s8) >> 16);
-            B.T[3][lane] = r == 0 ? a1 + d1 : (r == 1 ? b1 + c1 : (r == 2 ? b1 - c1 : a1 - d1));
-        }
-        __syncthreads();
-        if (cl) {  // rows, then the reconstruction
-            const int* ip = B.T[3] + 4 * r;
-            const int a1 = ip[0] + ip[2], b1 = ip[0] - ip[2];
-            const int c1 = ((ip[1] * s8) >> 16) - (ip[3] + ((ip[3] * c8) >> 16));
-            const int d1 = (ip[1] + ((ip[1] * c8) >> 16)) + ((ip[3] * s8) >> 16);
-            const int o = c == 0 ? (a1 + d1 + 4) >> 3 : (c == 1 ? (b1 + c1 + 4) >> 3 : (c == 2 ? (b1 - c1 + 4) >> 3 : (a1 - d1 + 4) >> 3));
-            s.rec[(ys + r) * 16 + xs + c] = (uint8_t)v8_clamp255(pred + o);
-        }
-        __syncthreads();
     }
-    return total;
-}
-
-__device__ __forceinline__ int pred_of(int mode, int above, int left, int corner, int dc) {
-    switch (mode) {
-        case kVPred:
-            return above;
-        case kHPred:
-            return left;
-        case kTmPred:
-            return v8_clamp255(left + above - corner);
-        default:
-            return dc;
+    const uint32_t costb = (uint32_t)(lam * kf_ymode_cost256(kBPred)) + (uint32_t)wsum(rr == 0 ? (int)best : 0);
+    const uint32_t lo = (uint32_t)wsum(rr == 0 && b < 8 ? (int)((uint32_t)bm << (4 * b)) : 0);
+    const uint32_t hi = (uint32_t)wsum(rr == 0 && b >= 8 ? (int)((uint32_t)bm << (4 * (b - 8))) : 0);
+    if (lane == 0) {
+        Vp8Mb& m = mbs[mbi];
+        m.mvx = (int16_t)(uint16_t)(lo & 0xffffu);
+        m.mvy = (int16_t)(uint16_t)(lo >> 16);
+        m.ymode = (uint8_t)(costb < cost16 ? kBPred : 0);
+        m.bmodes_hi = hi;
     }
-}
-
-__device__ __forceinline__ int dc_value(int sum, int cnt, int log2n) {
-    if (cnt == 0) return 128;
-    const int shift = log2n + cnt;
-    return (sum + (1 << (shift - 1))) >> shift;
 }
 
 __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8States* __restrict__ st,
@@ -628,25 +706,38 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
     const bool top = mby == 0, bottom = mby == g.mb_h - 1;
     // hand-off words of a macroblock: 0..3 its bottom luma row, 4..7 its bottom chroma row
     // (interleaved), 32 samples each with the frame's epoch tag above them
-    constexpr int W = kKeyLineWords;  // + word 8: the bottom sub-block modes (B_PRED contexts)
+    constexpr int W = kKeyLineWords;
     const uint64_t* above_line = line + (size_t)(mby > 0 ? mby - 1 : 0) * g.mb_w * W;
     uint64_t* my_line = line + (size_t)mby * g.mb_w * W;
     // the source of the next macroblock is fetched one macroblock ahead (registers), staged in LDS
     // at the top of the iteration; the fetch is taken at the bottom of the iteration that issued
     // it, so its wait counts the stores after it, not a vmcnt(0) at the loop's join
     const int sr = lane >> 2, sc4 = (lane & 3) * 4;
-    auto fetch = [&](int x0n, uint32_t& wy, uint32_t& wuv) {
+    // ... and so is its B_PRED plan (k_vp8_bpred_plan: the record's vector words, ymode, bmodes_hi)
+    const bool bpred = F.bpred_lambda != 0;
+    auto fetch = [&](int x0n, uint32_t& wy, uint32_t& wuv, uint4& pl) {
         wy = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y0 + sr) * g.pitch + x0n + sc4);
         wuv = *reinterpret_cast<const uint32_t*>(src_uv + (size_t)(y0 / 2 + (sr & 7)) * g.pitch + x0n + sc4);
+        if (bpred) {
+            const uint32_t* pw = reinterpret_cast<const uint32_t*>(mbs + mby * g.mb_w + x0n / 16);
+            pl = make_uint4(pw[0], pw[1], pw[7], 0u);
+        }
     };
     uint32_t nwy, nwuv;
-    fetch(0, nwy, nwuv);
+    uint4 npl = make_uint4(0u, 0u, 0u, 0u);
+    fetch(0, nwy, nwuv, npl);
+    // kBPredTap of this lane's sample (lane % 16) for the eight table modes, a byte each
+    uint32_t taplo = 0, taphi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        taplo |= (uint32_t)kBPredTap[k][lane & 15] << (8 * k);
+        taphi |= (uint32_t)kBPredTap[4 + k][lane & 15] << (8 * k);
+    }
     // the finished macroblock's reconstruction words and record, stored one macroblock late (after
     // the next poll, whose vmcnt(0) would otherwise wait for these stores)
     uint32_t pwy = 0, pwuv = 0, psse[3] = {0, 0, 0};
     int pmbx = -1, pym = 0, puvm = 0;
     uint32_t pnz = 0, pblo = 0, pbhi = 0;
-    int lctx = 0;  // B_PRED contexts of the next macroblock: its left neighbour's right sub-block modes
     auto flush = [&]() {
         if (pmbx < 0) return;
         const int r = lane >> 2, c4 = (lane & 3) * 4, px0 = pmbx * 16;
@@ -674,8 +765,8 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
             // the row above's words of this macroblock (lanes 0..7) and of the one before it (lanes
             // 8, 9: the corner samples), polled until every needed word carries this frame's tag
             // (tagged 64-bit agent-scope atomics: no release fence -- an L2 write-back -- per MB)
-            const bool need = lane < 8 || (lane < 10 && left) || lane == 10;
-            const int wi = lane < 8 ? W * mbx + lane : (lane == 10 ? W * mbx + 8 : W * (mbx - 1) + (lane == 8 ? 3 : 7));
+            const bool need = lane < 8 || (lane < 10 && left);
+            const int wi = lane < 8 ? W * mbx + lane : W * (mbx - 1) + (lane == 8 ? 3 : 7);
             const gu64* wp = (const gu64*)(above_line + (need ? wi : 0));
             uint64_t w = 0;
             for (unsigned sp = 0;; ++sp) {
@@ -702,20 +793,20 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
             } else if (lane == 9) {
                 E.cu = left ? (int)((d >> 16) & 0xff) : 129;
                 E.cv = left ? (int)(d >> 24) : 129;
-            } else if (lane == 10) {
-                E.actx = (int)(d & 0xffffu);
             }
         } else {
             if (lane < 16) E.ay[lane] = 127;
             if (lane < 8) E.au[lane] = E.av[lane] = 127;
             if (lane == 0) E.cy = E.cu = E.cv = 127;
-            if (lane == 0) E.actx = 0;  // B_DC above the frame
         }
         if (!left) {
             if (lane < 16) E.ly[lane] = 129;
             if (lane < 8) E.lu[lane] = E.lvv[lane] = 129;
         }
-        fetch(mbx + 1 < g.mb_w ? x0 + 16 : x0, nwy, nwuv);  // (after the poll: its waits drain all loads)
+        // this macroblock's plan (wave-uniform), then the next macroblock's fetch
+        const bool bp = bpred && (npl.y & 0xffu) == kBPred;
+        const uint32_t blo = bp ? npl.x : 0u, bhi = bp ? npl.z : 0u;
+        fetch(mbx + 1 < g.mb_w ? x0 + 16 : x0, nwy, nwuv, npl);  // (after the poll: its waits drain all loads)
         flush();  // the previous macroblock's reconstruction and record (after the poll, likewise)
         __syncthreads();
         // ---- mode decisions: SAD of the four 16x16 modes (4 samples per lane), the four chroma modes
@@ -728,8 +819,8 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
                                  nav + nlf, 2);
         const int r = lane >> 2, c4 = (lane & 3) * 4;
         int ymode = 0, uvmode = 0;
-        uint32_t best16 = ~0u;
-        {
+        if (!bp) {
+            uint32_t best16 = ~0u;
             int sad[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -764,37 +855,24 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
                 }
             }
         }
+        if (!bp)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = (uint8_t)pred_of(ymode, E.ay[c4 + j], E.ly[r], E.cy, dcy);
+            for (int j = 0; j < 4; ++j) s.pred[r * 16 + c4 + j] = (uint8_t)pred_of(ymode, E.ay[c4 + j], E.ly[r], E.cy, dcy);
         s.pu[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.au[cx], E.lu[cy], E.cu, dcu);
         s.pv[cy * 8 + cx] = (uint8_t)pred_of(uvmode, E.av[cx], E.lvv[cy], E.cv, dcv);
         __syncthreads();
-        // ---- B_PRED when its sub-block predictions + mode bits cost less than the 16x16 mode's
-        uint32_t blo = 0, bhi = 0, bnz = 0;
-        bool bp = false;
-        if (F.bpred_lambda) {
-            const uint32_t costb = bpred_mb(s, B, E, F, lv + (size_t)mbi * kCoefPerMb, lane, mbx, mby, g.mb_w, lctx, blo,
-                                            bhi, bnz);
-            bp = costb < 256u * best16 + (uint32_t)(F.bpred_lambda * kf_ymode_cost256(ymode));
-        }
-        uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, -1, 0, bp);
-        int ctx_bottom, ctx_right;  // this macroblock's bottom / right sub-block modes (contexts)
+        // ---- B_PRED (planned): the sub-blocks coded in turn into s.rec, then the chroma
+        uint32_t bnz = 0;
         if (bp) {
-            nz |= bnz;
+            bnz = bpred_code_gpu(s, B, E, F, lv + (size_t)mbi * kCoefPerMb, lane, mbx, mby, blo, bhi, taplo, taphi);
             ymode = kBPred;
-            ctx_bottom = (int)(bhi >> 16);
-            ctx_right = (int)(((blo >> 12) & 15u) | (((blo >> 28) & 15u) << 4) | (((bhi >> 12) & 15u) << 8) |
-                              (((bhi >> 28) & 15u) << 12));
-        } else {
-            blo = bhi = 0;
-            ctx_bottom = ctx_right = implied_bmode(ymode) * 0x1111;
+            __syncthreads();
         }
-        // ---- hand the bottom rows down: nine tagged words
+        const uint32_t nz = code_mb(s, F, lv + (size_t)mbi * kCoefPerMb, lane, -1, 0, bp) | bnz;
+        // ---- hand the bottom rows down: eight tagged words
         if (!bottom && lane < W) {
             uint32_t d = 0;
-            if (lane == 8) {
-                d = (uint32_t)ctx_bottom;
-            } else if (lane < 4) {
+            if (lane < 4) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) d |= (uint32_t)s.rec[15 * 16 + 4 * lane + k] << (8 * k);
             } else {
@@ -813,14 +891,13 @@ __global__ __launch_bounds__(64) void k_vp8_key(h264::Geometry g, const Vp8State
         pnz = nz;
         pblo = blo;
         pbhi = bhi;
-        lctx = ctx_right;
         // left edges of the next macroblock
         if (lane < 16) E.ly[lane] = s.rec[lane * 16 + 15];
         if (lane < 8) {
             E.lu[lane] = s.ru[lane * 8 + 7];
             E.lvv[lane] = s.rv[lane * 8 + 7];
         }
-        asm volatile("" : "+v"(nwy), "+v"(nwuv));  // the next source, fetched a macroblock ago
+        asm volatile("" : "+v"(nwy), "+v"(nwuv), "+v"(npl.x), "+v"(npl.y), "+v"(npl.z));  // fetched a macroblock ago
         __syncthreads();
     }
     flush();
@@ -1402,10 +1479,12 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_
 }
 
 void launch_vp8_key(const h264::Geometry& g, const Vp8DeviceBuffers& b, const uint8_t* src_y, const uint8_t* src_uv,
-                    hipStream_t stream, bool save_src) {
+                    hipStream_t stream, bool save_src, bool bpred) {
     if (save_src)  // the next inter frame's temporal classes compare against this source
         hipLaunchKernelGGL(k_vp8_save_src, dim3((g.coded_w / 4 + 255) / 256, g.coded_h), dim3(256), 0, stream, g, b.st,
                            src_y);
+    if (bpred)  // the B_PRED plans, every macroblock at once, before the wavefront reads them
+        hipLaunchKernelGGL(k_vp8_bpred_plan, dim3((g.mb_w * g.mb_h + 3) / 4), dim3(256), 0, stream, g, b.st, src_y, b.mb);
     hipLaunchKernelGGL(k_vp8_key, dim3(g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb, b.lv,
                        b.line, b.err);
 }

@@ -89,6 +89,14 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     cfg_.enc.mask_y1 = cfg_.mask_y1;
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     pool_ = std::make_unique<FramePool>(cfg_.width, cfg_.height, cfg_.pool_slots);
+    if ((cfg_.codec == "h264" || cfg_.codec == "avc") && cfg_.use_graph && cfg_.enc.deblock != 0 &&
+        cfg_.enc.deblock != 1) {
+        // the adaptive filter changes the picture's kernel sequence, a replayed graph cannot:
+        // graph replay takes the filter off unless it is set on for every picture
+        if (cfg_.enc.deblock > 1)
+            throw std::invalid_argument("hipGraph replay needs a fixed H.264 filter (deblock 0 or 1), not adaptive");
+        cfg_.enc.deblock = 0;
+    }
     if (cfg_.codec == "h264" || cfg_.codec == "avc")
         enc_ = std::make_unique<h264::GpuH264Encoder>(cfg_.enc, stream_);
     else if (cfg_.codec == "hevc" || cfg_.codec == "h265")
