@@ -4,6 +4,7 @@
 
 #include "../net/dtls.h"
 #include "../net/rtp_h264.h"
+#include "../net/rtp_counter.h"
 #include "../net/rtp_h265.h"
 #include "../net/rtp_sender.h"
 #include "../net/rtp_vp8.h"
@@ -181,4 +182,27 @@ void register_net(py::module& m) {
         .def_property_readonly("packets", &RtpVp8Packetizer::packets)
         .def_property_readonly("octets", &RtpVp8Packetizer::octets);
     n.def("split_annexb", [](py::bytes au) { return BV(split_annexb(au)); });
+    n.def(
+        "count_rtp_frames",
+        [](int fd, int n_frames, double timeout_s, int64_t ts, int next, bool ok) {
+            RtpFrameCount r;
+            {
+                py::gil_scoped_release rel;
+                r = count_rtp_frames(fd, n_frames, timeout_s, RtpLiteState{ts, next, ok});
+            }
+            py::dict d;
+            d["rtp_ts"] = r.rtp_ts;
+            d["arrival_us"] = r.arrival_us;
+            d["arrival_wall"] = r.arrival_wall;
+            d["rtcp"] = BV(r.rtcp);
+            d["packets"] = r.packets;
+            d["lost"] = r.lost;
+            d["datagrams"] = r.datagrams;
+            d["timed_out"] = r.timed_out;
+            return d;
+        },
+        py::arg("fd"), py::arg("n_frames"), py::arg("timeout_s"), py::arg("ts") = -1, py::arg("next") = -1,
+        py::arg("ok") = true,
+        "Count complete RTP frames on a connected UDP socket (recvmmsg, GIL released): rtp_ts, arrival times, "
+        "the last RTCP datagrams raw, packets, lost sequence numbers");
 }

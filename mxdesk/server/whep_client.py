@@ -108,7 +108,7 @@ class _Client(asyncio.DatagramProtocol):
 async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0, pli_after: int = 0,
                     timeout: float = 30.0, dc_messages: list[str] | None = None,
                     dc_wait_stats: bool = False, via_relay: bool = False, dc_audio_chunks: int = 0,
-                    simulate_loss: float = 0.0, lite: bool = False) -> WhepResult:
+                    simulate_loss: float = 0.0, lite: bool | str = False) -> WhepResult:
     """Connect to ``url`` (http://host:port/whep), receive ``n_frames`` access units.
 
     ``drop_seq_every``: discard every Nth RTP packet and recover it with a generic NACK.
@@ -126,7 +126,8 @@ async def whep_view(url: str, n_frames: int, auth=None, drop_seq_every: int = 0,
     complete when its marker packet arrives with no sequence gap) instead of decrypting and
     depacketising every packet -- ICE, DTLS, the server's SRTP and RTCP sender reports are the
     same; for density runs where a hundred Python viewers share the server's host (``aus`` then
-    holds empty placeholders).
+    holds empty placeholders).  ``lite="native"``: the same count by the native receive loop
+    (``_native.net.count_rtp_frames``: recvmmsg batches with the GIL released) once DTLS is up.
     """
     import aiohttp
 
@@ -166,7 +167,7 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
                         timeout: float = 30.0, drop_seq_every: int = 0, pli_after: int = 0,
                         dc_messages: list[str] | None = None, dc_wait_stats: bool = False, via_relay: bool = False,
                         dc_audio_chunks: int = 0, simulate_loss: float = 0.0,
-                        server_channel: str | None = None, lite: bool = False) -> None:
+                        server_channel: str | None = None, lite: bool | str = False) -> None:
     """The browser side of an established negotiation (remote SDP = the server's answer for
     WHEP, its offer for the selkies protocol): ICE check, DTLS client, SRTP receive with NACK /
     PLI repair, data channels.  ``server_channel``: the server opens that channel (selkies
@@ -386,6 +387,62 @@ async def media_session(res: WhepResult, remote_sdp: str, dtls, ufrag: str, N, n
         lite_ts = None       # lite: timestamp of the frame being received, its next expected seq
         lite_next = None
         lite_ok = True
+        if lite == "native" and dc is None:
+            # hand the socket to the native receive loop: stop the event loop's reader, count the
+            # datagrams it already queued here, then recvmmsg() with the GIL released
+            sock = tr.get_extra_info("socket")
+            # (the transport owns the fd: the public remove_reader refuses it, and datagram
+            # transports have no pause_reading -- the selector loop's own removal)
+            loop._remove_reader(sock.fileno())
+            rtcp = []
+            while not cl.q.empty():
+                d = cl.q.get_nowait()
+                if not 128 <= d[0] <= 191:
+                    continue
+                if 192 <= d[1] <= 223:
+                    rtcp.append(d)
+                    continue
+                if d[1] & 0x7F == 0:
+                    continue
+                seq, ts = struct.unpack_from("!HI", d, 2)
+                res.packets += 1
+                if ts != lite_ts:
+                    lite_ts, lite_ok = ts, lite_next is None or seq == lite_next
+                elif seq != lite_next:
+                    lite_ok = False
+                if lite_next is not None and seq != lite_next and ((seq - lite_next) & 0xFFFF) < 0x8000:
+                    res.lost += (seq - lite_next) & 0xFFFF
+                lite_next = (seq + 1) & 0xFFFF
+                if d[1] & 0x80:
+                    if lite_ok and len(res.aus) < n_frames:
+                        res.aus.append(b"")
+                        res.rtp_ts.append(ts)
+                        res.arrival_us.append(time.monotonic_ns() // 1000)
+                        res.arrival_wall.append(time.time())
+                    lite_ts = None
+            left = n_frames - len(res.aus)
+            r = await loop.run_in_executor(
+                None, lambda: N.net.count_rtp_frames(sock.fileno(), left, max(0.1, deadline - time.monotonic()),
+                                                     -1 if lite_ts is None else lite_ts,
+                                                     -1 if lite_next is None else lite_next, lite_ok))
+            res.aus += [b""] * len(r["rtp_ts"])
+            res.rtp_ts += r["rtp_ts"]
+            res.arrival_us += r["arrival_us"]
+            res.arrival_wall += r["arrival_wall"]
+            res.packets += r["packets"]
+            res.lost += r["lost"]
+            res.datagrams += r["datagrams"]
+            for d in rtcp + list(r["rtcp"]):  # the sender reports: RTP time <-> wall time
+                p = rx_for(d).unprotect_rtcp(d)
+                for x in (R.parse_rtcp(p) if p else []):
+                    if x["pt"] == 200:
+                        res.srs += 1
+                        if "ntp" in x:
+                            res.sr_map = (x["ntp"], x["rtp_ts"])
+            if r["timed_out"]:
+                raise asyncio.TimeoutError()
+            res.stream = b""
+            return
         while len(res.aus) < n_frames or dc_pending():
             if dc is not None and time.monotonic() - last_tick > 0.05:
                 sctp_out(dc.tick())

@@ -403,10 +403,13 @@ def test_rtcp_sr_maps_rtp_to_wall_clock(native, monkeypatch):
     assert all(-2.0 < v < 500.0 for v in lat), lat  # same host: capture precedes arrival (ms resolution)
 
 
-def test_whep_lite_viewer_counts_frames(native, monkeypatch):
+@pytest.mark.parametrize("mode", [True, "native"])
+def test_whep_lite_viewer_counts_frames(native, monkeypatch, mode):
     """The density harness's lite viewer (tools/bench_density.py --client lite): frames counted
     from the plaintext RTP headers of the SRTP stream (one timestamp, marker bit, no sequence gap)
-    after the same ICE / DTLS set-up; RTCP sender reports still decrypted for the latency map."""
+    after the same ICE / DTLS set-up; RTCP sender reports still decrypted for the latency map.
+    "native": the count by the native recvmmsg loop (--client native), the socket handed over
+    after DTLS."""
     from mxdesk.server.whep_client import e2e_latency_ms
 
     monkeypatch.setenv("MXDESK_WEBRTC_HOST", "127.0.0.1")
@@ -417,7 +420,7 @@ def test_whep_lite_viewer_counts_frames(native, monkeypatch):
         port = free_port()
         runner = await serve(srv, "127.0.0.1", port)
         try:
-            return await whep_view(f"http://127.0.0.1:{port}/whep", 70, lite=True)
+            return await whep_view(f"http://127.0.0.1:{port}/whep", 70, lite=mode)
         finally:
             await runner.cleanup()
 

@@ -154,14 +154,15 @@ def main():
     ap.add_argument("--encoder", default="mxh264enc")
     ap.add_argument("--server-procs", type=int, default=1, help="serve processes sharing the GPU (sessions split evenly)")
     ap.add_argument("--log-dir", default="", help="write each serve process's output here")
-    ap.add_argument("--client", choices=["full", "lite"], default="full",
-                    help="viewer: full (decrypt + depacketise every packet) or lite (frames from the plaintext RTP "
-                         "headers; the server side is identical -- for K where the Python viewers saturate the host)")
+    ap.add_argument("--client", choices=["full", "lite", "native"], default="full",
+                    help="viewer: full (decrypt + depacketise every packet), lite (frames from the plaintext RTP "
+                         "headers; the server side is identical -- for K where the Python viewers saturate the host) "
+                         "or native (the lite count by a native recvmmsg loop, GIL released)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     rows, sustained = [], 0
     for k in (int(v) for v in a.sweep.replace("+", ",").split(",")):
-        r = run_k(k, a.frames, a.per_proc, a.width, a.height, a.encoder, a.server_procs, a.log_dir, a.client == "lite")
+        r = run_k(k, a.frames, a.per_proc, a.width, a.height, a.encoder, a.server_procs, a.log_dir, {"full": False, "lite": True, "native": "native"}[a.client])
         r["server_procs"] = min(a.server_procs, k)
         r["client"] = a.client
         rows.append(r)
