@@ -299,6 +299,7 @@ struct Vp8DeviceBuffers {
     int16_t* lv_host;      // mapped host: levels of the coded macroblocks, row-compacted
     h264::DeviceBuffers me;  // shared H.264 motion search (fs = &st->me, mb = vectors)
     uint8_t* icand;        // [nmb] inter frames' intra pass: candidate << 7 | best 16x16 mode
+    int* ilist;            // [1 + nmb] the intra pass's candidates: count, then macroblock indices
 };
 // P frames: pad the reference, shared integer motion search, then one wave per macroblock.
 // hp_planes: the four padded F / H / V / J planes (h264::launch_hpel) when the motion search refines

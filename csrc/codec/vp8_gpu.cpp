@@ -53,6 +53,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
     HIP_CHECK(hipHostMalloc(&b.lv_host, sizeof(int16_t) * kCoefPerMb * (size_t)nmb, hipHostMallocMapped));
     HIP_CHECK(hipMalloc(&b.me.mb, sizeof(h264::MbInfo) * (size_t)nmb));
     HIP_CHECK(hipMalloc(&b.icand, (size_t)nmb));
+    HIP_CHECK(hipMalloc(&b.ilist, sizeof(int) * (size_t)(nmb + 1)));
     b.me.fs = &b.st->me;
     HIP_CHECK(hipHostMalloc(&s.st_host, sizeof(Vp8States), hipHostMallocDefault));
     std::memset(s.st_host, 0, sizeof(Vp8States));
@@ -62,7 +63,7 @@ void GpuVp8Encoder::alloc_slot(Slot& s) {
 
 void GpuVp8Encoder::free_slot(Slot& s) {
     Vp8DeviceBuffers& b = s.buf;
-    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line, (void*)b.icand})
+    for (void* p : {(void*)b.st, (void*)b.mb, (void*)b.lv, (void*)b.line, (void*)b.me.mb, (void*)b.lf_line, (void*)b.icand, (void*)b.ilist})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)b.err, (void*)b.mb_host, (void*)b.lv_host, (void*)s.st_host, (void*)b.lf_sse})
         if (p) (void)hipHostFree(p);

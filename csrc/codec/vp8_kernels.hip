@@ -363,10 +363,11 @@ __global__ __launch_bounds__(64) void k_vp8_inter(h264::Geometry g, const Vp8Sta
                                                    const uint8_t* __restrict__ src_y,
                                                    const uint8_t* __restrict__ src_uv,
                                                    const h264::MbInfo* __restrict__ me, Vp8Mb* __restrict__ mbs,
-                                                   int16_t* __restrict__ lv) {
+                                                   int16_t* __restrict__ lv, int* __restrict__ ilist) {
     __shared__ MbLds s;
     const Vp8FrameState& F = st->v;
     const int mbi = blockIdx.x, lane = threadIdx.x;
+    if (mbi == 0 && lane == 0) ilist[0] = 0;  // the intra pass's candidate count (k_vp8_intra_cand)
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
     int lo_x, hi_x, lo_y, hi_y;
     mv_bounds(g.mb_w, g.mb_h, mbx, mby, &lo_x, &hi_x, &lo_y, &hi_y);
@@ -956,42 +957,61 @@ __device__ __forceinline__ int best_luma16(const MbLds& s, const KeyEdges& E, bo
     return mode;
 }
 
-__global__ __launch_bounds__(64) void k_vp8_intra_cand(h264::Geometry g, const Vp8States* __restrict__ st,
-                                                        const uint8_t* __restrict__ src_y,
-                                                        const uint8_t* __restrict__ src_uv,
-                                                        const Vp8Mb* __restrict__ mbs, uint8_t* __restrict__ icand) {
-    __shared__ MbLds s;
-    __shared__ KeyEdges E;
+// candidates: one wave per macroblock, four per workgroup (most macroblocks leave at once: the
+// inter prediction is good); a candidate appends itself to ilist (ilist[0] = the count, reset by
+// k_vp8_inter)
+__global__ __launch_bounds__(256) void k_vp8_intra_cand(h264::Geometry g, const Vp8States* __restrict__ st,
+                                                         const uint8_t* __restrict__ src_y,
+                                                         const uint8_t* __restrict__ src_uv,
+                                                         const Vp8Mb* __restrict__ mbs, uint8_t* __restrict__ icand,
+                                                         int* __restrict__ ilist) {
+    __shared__ MbLds sh[4];
+    __shared__ KeyEdges Eh[4];
     const Vp8FrameState& F = st->v;
-    const int mbi = blockIdx.x, lane = threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mbi = blockIdx.x * 4 + wave;
+    if (mbi >= g.mb_w * g.mb_h) return;  // (wave-uniform; wave-level LDS ordering only below)
+    MbLds& s = sh[wave];
+    KeyEdges& E = Eh[wave];
     const uint32_t psad = mbs[mbi].bmodes_hi;
-    if (psad <= kIntraMinSad) {  // (workgroup-uniform)
+    if (psad <= kIntraMinSad) {
         if (lane == 0) icand[mbi] = 0;
         return;
     }
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
     stage_src(s, g, src_y, src_uv, x0, y0, lane);
     rec_edges(E, g, F, x0, y0, lane);
-    __syncthreads();
+    wave_lds_sync();
     uint32_t best;
     const int mode = best_luma16(s, E, mby == 0, mbx > 0, lane, best);
-    if (lane == 0) icand[mbi] = (uint8_t)((vp8_intra_candidate(psad, best, F.intra_lambda) ? 0x80 : 0) | mode);
+    const bool cand = vp8_intra_candidate(psad, best, F.intra_lambda);
+    if (lane == 0) {
+        icand[mbi] = (uint8_t)((cand ? 0x80 : 0) | mode);
+        if (cand) ilist[1 + atomicAdd(&ilist[0], 1)] = mbi;
+    }
 }
 
+// the candidates without a candidate causal neighbour, coded intra: a fixed grid over the
+// candidate list (a few percent of the macroblocks at most), one macroblock per workgroup step
+constexpr int kIntraCodeGrid = 256;
 __global__ __launch_bounds__(64) void k_vp8_intra_code(h264::Geometry g, const Vp8States* __restrict__ st,
                                                         const uint8_t* __restrict__ src_y,
                                                         const uint8_t* __restrict__ src_uv, Vp8Mb* __restrict__ mbs,
-                                                        int16_t* __restrict__ lv, const uint8_t* __restrict__ icand) {
+                                                        int16_t* __restrict__ lv, const uint8_t* __restrict__ icand,
+                                                        const int* __restrict__ ilist) {
     __shared__ MbLds s;
     __shared__ KeyEdges E;
     const Vp8FrameState& F = st->v;
-    const int mbi = blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x;
+    const int n = ilist[0];
+    for (int li = blockIdx.x; li < n; li += gridDim.x) {
+    const int mbi = ilist[1 + li];
     const int mbx = mbi % g.mb_w, mby = mbi / g.mb_w, x0 = mbx * 16, y0 = mby * 16;
     const int ic = icand[mbi];
     // a candidate without a candidate causal neighbour (workgroup-uniform)
-    if (!(ic & 0x80) || (mbx > 0 && (icand[mbi - 1] & 0x80)) || (mby > 0 && (icand[mbi - g.mb_w] & 0x80)) ||
+    if ((mbx > 0 && (icand[mbi - 1] & 0x80)) || (mby > 0 && (icand[mbi - g.mb_w] & 0x80)) ||
         (mbx > 0 && mby > 0 && (icand[mbi - g.mb_w - 1] & 0x80)))
-        return;
+        continue;
     const int seg = mbs[mbi].seg;
     stage_src(s, g, src_y, src_uv, x0, y0, lane);
     rec_edges(E, g, F, x0, y0, lane);
@@ -1032,6 +1052,8 @@ __global__ __launch_bounds__(64) void k_vp8_intra_code(h264::Geometry g, const V
     uint32_t sse[3];
     store_rec(s, g, F, x0, y0, lane, sse);
     store_record(mbs + mbi, 0, 0, ymode, uvmode, nz, sse, lane, seg, 0);
+    __syncthreads();  // (LDS reuse by the next list entry)
+    }
 }
 
 // ------------------------------------------------------------------ loop filter (15)
@@ -1469,12 +1491,12 @@ void launch_vp8_inter(const h264::Geometry& g, const Vp8DeviceBuffers& b, uint8_
         hipLaunchKernelGGL(k_vp8_pad, dim3((W / 4 + 255) / 256, H), dim3(256), 0, stream, g, b.st);
     h264::launch_me(g, b.me, src_y, stream);
     hipLaunchKernelGGL(k_vp8_inter, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.me.mb, b.mb,
-                       b.lv);
+                       b.lv, b.ilist);
     if (intra) {
-        hipLaunchKernelGGL(k_vp8_intra_cand, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb,
-                           b.icand);
-        hipLaunchKernelGGL(k_vp8_intra_code, dim3(g.mb_w * g.mb_h), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb,
-                           b.lv, b.icand);
+        hipLaunchKernelGGL(k_vp8_intra_cand, dim3((g.mb_w * g.mb_h + 3) / 4), dim3(256), 0, stream, g, b.st, src_y,
+                           src_uv, b.mb, b.icand, b.ilist);
+        hipLaunchKernelGGL(k_vp8_intra_code, dim3(kIntraCodeGrid), dim3(64), 0, stream, g, b.st, src_y, src_uv, b.mb,
+                           b.lv, b.icand, b.ilist);
     }
 }
 
