@@ -116,7 +116,9 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
     MediaServer on port + i, all on one event loop.  Synthetic desktops: an X display is one
     desktop, so only K == 1 captures it."""
     from .server.app import MediaServer, run_forever_multi, ssl_context
+    from .utils.sampler import install_from_env
 
+    install_from_env()  # MXDESK_PYPROFILE: per-thread stack samples of this serve process
     if cfg.source == "x11":
         raise SystemExit("serve --sessions K > 1 streams synthetic desktops; MXDESK_SOURCE=x11 serves one")
     if cfg.novnc_enable:

@@ -13,6 +13,7 @@ import argparse
 import asyncio
 import json
 import os
+import resource
 import socket
 import statistics
 import subprocess
@@ -20,6 +21,8 @@ import sys
 import time
 import urllib.request
 from pathlib import Path
+
+import psutil
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
@@ -82,7 +85,13 @@ def _client_proc(ports, frames, q, lite=False):
     async def main():
         return await asyncio.gather(*(one(p) for p in ports))
 
-    q.put(asyncio.run(main()))
+    out = asyncio.run(main())
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    for r in out:  # this client process's CPU seconds, on its first result
+        r["client_cpu_s"] = 0.0
+    if out:
+        out[0]["client_cpu_s"] = ru.ru_utime + ru.ru_stime
+    q.put(out)
 
 
 def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir="", lite=False):
@@ -114,6 +123,18 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir
         q = ctx.Queue()
         groups = [ports[i:i + per_proc] for i in range(0, k, per_proc)]
         procs = [ctx.Process(target=_client_proc, args=(g, frames, q, lite)) for g in groups]
+        def server_cpu_s():
+            tot = 0.0
+            for srv in srvs:
+                try:
+                    ct = psutil.Process(srv.pid).cpu_times()
+                    tot += ct.user + ct.system
+                except psutil.Error:
+                    pass
+            return tot
+
+        cpu0 = server_cpu_s()
+        t_clients = time.monotonic()
         for p in procs:
             p.start()
         results = []
@@ -121,6 +142,8 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir
             results += q.get(timeout=frames / 30.0 + 240)
         for p in procs:
             p.join(timeout=30)
+        t_run = time.monotonic() - t_clients
+        server_cpu = server_cpu_s() - cpu0
     finally:
         for srv in srvs:
             srv.terminate()
@@ -141,7 +164,11 @@ def run_k(k, frames, per_proc, width, height, codec_env, server_procs=1, log_dir
     return {"k": k, "passed": passed, "min_fps": round(min(fps), 2) if fps else 0.0,
             "mean_fps": round(statistics.mean(fps), 2) if fps else 0.0, "p50_e2e_ms": round(p50, 3),
             "p95_e2e_ms": round(p95, 3), "lost_packets": sum(r["lost"] for r in ok), "errors": [e["error"] for e in errs][:3],
-            "failed_ports": sorted(e["port"] - base for e in errs), "failed_diag": [e.get("diag") for e in errs][:16]}
+            "failed_ports": sorted(e["port"] - base for e in errs), "failed_diag": [e.get("diag") for e in errs][:16],
+            # host CPU: cores kept busy on average over the clients' run (ICE / DTLS set-up included)
+            "cpus": len(os.sched_getaffinity(0)), "client_run_s": round(t_run, 2),
+            "client_cores": round(sum(r.get("client_cpu_s", 0.0) for r in results) / max(t_run, 1e-6), 2),
+            "server_cores": round(server_cpu / max(t_run, 1e-6), 2)}
 
 
 def main():
