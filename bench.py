@@ -357,6 +357,8 @@ def main() -> None:
                          "default: the encoder's)")
     ap.add_argument("--intra-in-p", type=int, default=None,
                     help="H.264: P-slice macroblocks may switch to intra (default: encoder default)")
+    ap.add_argument("--vp8-bpred", type=int, default=None, help="VP8 key frames: B_PRED macroblocks (default 1)")
+    ap.add_argument("--vp8-intra", type=int, default=None, help="VP8 inter frames: intra macroblocks (default 1)")
     ap.add_argument("--depth", type=int, default=None,
                     help="GPU frames in flight per session (2: entropy coding of frame n overlaps analysis of n+1; "
                          "3: also the next frame's launches stay queued while the host collects, so the host "
@@ -460,6 +462,10 @@ def main() -> None:
         cfg.enc.chroma_qp_offset = args.chroma_qp_offset
     if args.intra_in_p is not None:
         cfg.enc.intra_in_p = args.intra_in_p
+    if args.vp8_bpred is not None:
+        cfg.enc.vp8_bpred = args.vp8_bpred
+    if args.vp8_intra is not None:
+        cfg.enc.vp8_intra = args.vp8_intra
     if args.deblock is not None:
         cfg.enc.deblock = args.deblock
     if args.aq is not None:
@@ -609,6 +615,8 @@ def main() -> None:
             "device": args.device,
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
+            "intra_in_p": int(cfg.enc.intra_in_p),
+            "vp8_tools": {"bpred": int(cfg.enc.vp8_bpred), "intra": int(cfg.enc.vp8_intra)} if args.codec == "vp8" else None,
             "deblocked_frames_pct": round(100.0 * sum(dbk) / max(1, len(dbk)), 1),
             # the adaptive filter's inputs (h264_deblock.h db_auto_decide): mean coherent / moving
             # macroblocks per picture

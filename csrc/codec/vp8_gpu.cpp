@@ -271,7 +271,23 @@ void GpuVp8Encoder::write_slot(const Slot& s, std::vector<uint8_t>& out, bool pr
         fd.seg_qindex[k] = s.seg_qindex[k];
         fd.lf_level[k] = s.lf_level[k];
     }
-    write_frame(fd, mbs, [&](int i) { return lv + (size_t)mbs[i].slot * kCoefPerMb; }, out,
+    // k_vp8_gather sent only the blocks with a non-zero level (16 levels each, from block `slot`):
+    // expanded into the 25-block layout the token writer reads, one macroblock at a time per thread
+    auto levels = [&](int i) -> const int16_t* {
+        thread_local int16_t full[kCoefPerMb];
+        const Vp8Mb& m = mbs[i];
+        const int16_t* p = lv + (size_t)m.slot * 16;
+        for (int b = 0; b < kBlocks; ++b) {
+            if ((m.nz >> b) & 1u) {
+                std::memcpy(full + b * 16, p, 16 * sizeof(int16_t));
+                p += 16;
+            } else {
+                std::memset(full + b * 16, 0, 16 * sizeof(int16_t));
+            }
+        }
+        return full;
+    };
+    write_frame(fd, mbs, levels, out,
                 [&](int n, const std::function<void(int)>& fn) { pool_->run(n, fn); },
                 probe ? nullptr : &tok_stats_[s.key ? 1 : 0][s.fidx % kStatsLag]);
 }

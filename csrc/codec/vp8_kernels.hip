@@ -1433,56 +1433,63 @@ __global__ __launch_bounds__(256) void k_vp8_lf_sse(h264::Geometry g, const Vp8S
 __global__ __launch_bounds__(256) void k_vp8_gather(h264::Geometry g, const Vp8Mb* __restrict__ mbs,
                                                      const int16_t* __restrict__ lv, Vp8Mb* __restrict__ mb_host,
                                                      int16_t* __restrict__ lv_host) {
-    __shared__ int wave_cnt[4];
-    __shared__ uint16_t col[4][128];  // per wave: the columns of its coded macroblocks, in rank order
+    // The records of a macroblock row and the levels of its coded macroblocks go to mapped host
+    // memory -- over the host link, so only the blocks with a non-zero level travel (16 levels
+    // each, compacted per row in macroblock order; a record's slot is its first block's index).
+    // The writer expands them (vp8_gpu.cpp).  Each wave owns two 64-macroblock chunks of the row.
+    __shared__ int wave_blk[4];
+    __shared__ uint16_t bmap[4][128 * 25];  // per wave: (macroblock column << 5 | block) of every block to copy
     const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = g.mb_w, base = row * n;
-    // each wave owns two 64-MB chunks (mb_w <= 512)
-    uint64_t bal[2];
-    int cnt = 0;
+    int nb[2] = {0, 0}, ex[2] = {0, 0};  // this lane's macroblock: blocks to copy, their offset in the wave
+    uint32_t nzm[2] = {0u, 0u};
+    int tot = 0;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int i = wave * 128 + c * 64 + lane;
-        const bool coded = i < n && mbs[base + i].nz != 0;
-        bal[c] = __ballot(coded);
-        cnt += __popcll(bal[c]);
+        nzm[c] = i < n ? (mbs[base + i].nz & 0x1FFFFFFu) : 0u;
+        nb[c] = __popc(nzm[c]);
+        int incl = nb[c];  // inclusive scan over the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        ex[c] = tot + incl - nb[c];
+        tot += __shfl(incl, 63, 64);
     }
-    if (lane == 0) wave_cnt[wave] = cnt;
+    if (lane == 0) wave_blk[wave] = tot;
     __syncthreads();
     int off = 0;
-    for (int w = 0; w < wave; ++w) off += wave_cnt[w];
+    for (int w = 0; w < wave; ++w) off += wave_blk[w];
+    const size_t row_blk = (size_t)base * kBlocks;  // the row's first block in lv_host
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int i = wave * 128 + c * 64 + lane;
-        const int rank = off + (c ? __popcll(bal[0]) : 0) + __popcll(bal[c] & ((1ull << lane) - 1));
         if (i < n) {
             Vp8Mb m = mbs[base + i];
-            m.slot = (uint32_t)(base + rank);
+            m.slot = (uint32_t)(row_blk + off + ex[c]);
             const uint4* srcw = reinterpret_cast<const uint4*>(&m);
             uint4* dst = reinterpret_cast<uint4*>(mb_host + base + i);
             dst[0] = srcw[0];
             dst[1] = srcw[1];
         }
-    }
-    // levels of the coded macroblocks, 50 uint4 each: the wave's (macroblock, uint4) pairs spread
-    // over its lanes, four independent copies in flight per lane (one macroblock per wave step left
-    // a load latency per macroblock on the critical path: 58 us per 1080p motion picture)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int i = wave * 128 + c * 64 + lane;
-        if ((bal[c] >> lane) & 1ull)
-            col[wave][(c ? __popcll(bal[0]) : 0) + __popcll(bal[c] & ((1ull << lane) - 1))] = (uint16_t)i;
+        uint32_t z = nzm[c];
+        for (int k = ex[c]; z; ++k) {
+            const int bb = __builtin_ctz(z);
+            z &= z - 1;
+            bmap[wave][k] = (uint16_t)((i << 5) | bb);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int kU4 = kCoefPerMb / 8;
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(lv) + (size_t)base * kU4;
-    uint4* __restrict__ dst = reinterpret_cast<uint4*>(lv_host) + (size_t)(base + off) * kU4;
+    // two uint4 per block, spread over the lanes: many copies in flight per wave
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(lv + (size_t)base * kCoefPerMb);
+    uint4* __restrict__ dst = reinterpret_cast<uint4*>(lv_host + (row_blk + off) * 16);
 #pragma unroll 4
-    for (int t = lane; t < cnt * kU4; t += 64) {
-        const int k = t / kU4, j = t - k * kU4;
-        dst[t] = src[(size_t)col[wave][k] * kU4 + j];
+    for (int t = lane; t < 2 * tot; t += 64) {
+        const int e = bmap[wave][t >> 1];
+        dst[t] = src[(size_t)(e >> 5) * (kCoefPerMb / 8) + (e & 31) * 2 + (t & 1)];
     }
 }
 

@@ -35,12 +35,16 @@ inline void ensure_func_attr(const void* fn, hipFuncAttribute attr, int value) {
 }
 }  // namespace mx
 
+#include <chrono>
 #include <cstdlib>
 #include <thread>
 
 namespace mx {
 // Wait for a frame's completion event.  MXDESK_WAIT=spin polls hipEventQuery (the collecting
-// thread owns a core: wake-up within ~1 us of the GPU finishing); default hipEventSynchronize.
+// thread owns a core: wake-up within ~1 us of the GPU finishing); MXDESK_WAIT=sleep polls it
+// every 25 us and sleeps in between (many sessions per process: a hundred frame threads waiting
+// in hipEventSynchronize kept the serve processes' host CPUs busy, profiles/r06_density); default
+// hipEventSynchronize.
 // Rate of the device wall clock (wall_clock64() / s_memrealtime) in kHz = ticks per ms.
 inline double device_clock_khz() {
     int dev = 0, khz = 0;
@@ -50,11 +54,12 @@ inline double device_clock_khz() {
     return (double)khz;
 }
 inline void wait_event(hipEvent_t e) {
-    static const bool spin = [] {
+    static const int mode = [] {
         const char* v = std::getenv("MXDESK_WAIT");
-        return v && std::string(v) == "spin";
+        const std::string s = v ? v : "";
+        return s == "spin" ? 1 : (s == "sleep" ? 2 : 0);
     }();
-    if (!spin) {
+    if (mode == 0) {
         HIP_CHECK(hipEventSynchronize(e));
         return;
     }
@@ -62,6 +67,7 @@ inline void wait_event(hipEvent_t e) {
         const hipError_t r = hipEventQuery(e);
         if (r == hipSuccess) return;
         if (r != hipErrorNotReady) HIP_CHECK(r);
+        if (mode == 2) std::this_thread::sleep_for(std::chrono::microseconds(25));
     }
 }
 }  // namespace mx

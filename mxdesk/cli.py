@@ -129,6 +129,9 @@ def cmd_serve_sessions(cfg: C.Config, k: int) -> None:
     # K sessions' streams share 4 queues and serialise behind each other.  Must be set before
     # the HIP runtime initialises (the first pipeline below); an explicit setting wins.
     os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(16, 2 * k))))
+    # K frame threads waiting for their frames: poll-and-sleep instead of hipEventSynchronize, whose
+    # waiting kept the host CPUs busy at 32 sessions per process (profiles/r06_density/NOTES.md)
+    os.environ.setdefault("MXDESK_WAIT", "sleep")
     # K frame threads and the event loop trade the GIL every frame; with the default 5 ms switch
     # interval a thread that wants it can wait a whole interval behind a busy one
     sys.setswitchinterval(float(os.environ.get("MXDESK_SWITCH_INTERVAL", "0.0005")))
