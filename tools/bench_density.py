@@ -11,6 +11,7 @@ density is that K minus one step.
 """
 import argparse
 import asyncio
+import http.client
 import json
 import os
 import resource
@@ -29,11 +30,18 @@ sys.path.insert(0, str(ROOT))
 
 
 def _free_port_block(n: int) -> int:
-    for _ in range(50):
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            base = s.getsockname()[1]
-        if base + n < 65000 and all(_port_free(base + i) for i in range(n)):
+    # below the ephemeral range: a readiness probe to a port nobody listens on yet can otherwise
+    # connect to itself (source port == destination port) and read its own request back
+    import random
+
+    lo = 20000
+    try:
+        lo = min(lo, int(Path("/proc/sys/net/ipv4/ip_local_port_range").read_text().split()[0]) - n - 1)
+    except (OSError, ValueError, IndexError):
+        pass
+    for _ in range(200):
+        base = random.randint(10000, max(10001, lo))
+        if all(_port_free(base + i) for i in range(n)):
             return base
     raise RuntimeError("no free port block")
 
@@ -56,7 +64,7 @@ def _wait_ready(ports, timeout=180.0):
                 with urllib.request.urlopen(f"http://127.0.0.1:{p}/health", timeout=1.0) as r:
                     if r.status == 200:
                         pending.discard(p)
-            except OSError:
+            except (OSError, http.client.HTTPException):
                 pass
         time.sleep(0.5)
     if pending:
