@@ -343,6 +343,7 @@ def test_graph_replay_matches_stream_launches(gpu):
         cfg.width, cfg.height, cfg.fps = 320, 192, 60
         cfg.enc.bitrate_kbps = 500  # rate control active: QP changes between frames
         cfg.use_graph = use_graph
+        cfg.enc.deblock = 0  # graph replay needs a fixed H.264 filter (Session: adaptive -> off); eager alike
         cfg.fake_clock = 1
         s = gpu.Session(cfg)
         aus = [s.step(i == 5).au for i in range(9)]
@@ -365,6 +366,8 @@ def _run_pipelined(gpu, depth, kbps, n=8, codec="h264", idr_at=5, use_graph=0):
     cfg.enc.bitrate_kbps = kbps
     cfg.enc.pipeline_depth = depth
     cfg.use_graph = use_graph
+    if codec == "h264":  # graph replay needs a fixed H.264 filter (Session: adaptive -> off)
+        cfg.enc.deblock = 0
     cfg.fake_clock = 1
     s = gpu.Session(cfg)
     out, sent = [], 0
@@ -525,6 +528,8 @@ def test_graph_replay_depth2_matches_eager(gpu, codec):
         cfg.enc.bitrate_kbps = 600
         cfg.enc.pipeline_depth = 2
         cfg.use_graph = use_graph
+        if codec == "h264":  # graph replay needs a fixed H.264 filter (Session: adaptive -> off)
+            cfg.enc.deblock = 0
         cfg.fake_clock = 1
         s = gpu.Session(cfg)
         out = []
