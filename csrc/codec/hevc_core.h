@@ -1925,6 +1925,39 @@ MXHD int intra_mode_bits(int mode, int cand_a, int cand_b) {
     return 6;
 }
 
+// Coarse-to-fine order of the open-loop intra mode search (intra_decide_mode, k_hevc_intra_modes):
+// planar, DC and every fourth angular mode, then the modes two and one away from the best angular
+// mode so far -- at most 15 of the 35 predictions.  cost(m): the mode's cost, kIntraNoMode when the
+// mode may not be used; the lowest cost wins, ties to the lower mode.
+constexpr int kIntraCoarse[11] = {0, 1, 2, 6, 10, 14, 18, 22, 26, 30, 34};
+constexpr int kIntraNoMode = 0x7fffffff;
+template <class F>
+MXHD int intra_mode_search(const F& cost) {
+    int best = 1, bc = kIntraNoMode, ba = -1, bac = kIntraNoMode;
+    auto visit = [&](int m) {
+        const int c = cost(m);
+        if (c == kIntraNoMode) return;
+        if (c < bc || (c == bc && m < best)) {
+            bc = c;
+            best = m;
+        }
+        if (m >= 2 && (c < bac || (c == bac && m < ba))) {
+            bac = c;
+            ba = m;
+        }
+    };
+    for (int i = 0; i < 11; ++i) visit(kIntraCoarse[i]);
+    if (ba >= 2) {
+        const int a = ba;
+        if (a - 2 >= 2) visit(a - 2);
+        if (a + 2 <= 34) visit(a + 2);
+        const int b = ba;
+        if (b - 1 >= 2) visit(b - 1);
+        if (b + 1 <= 34) visit(b + 1);
+    }
+    return best;
+}
+
 // Residual (raster NxN) -> quantised levels in scan order + reconstructed residual (raster).
 // Returns the number of nonzero levels.
 // Inter TU decimation: a TU whose only levels are a few +-1s is zeroed (it costs many

@@ -410,8 +410,9 @@ void summarise(CuInfo& c, const int16_t* coef) {
 // sr unit rows (k_hevc_intra_modes on the GPU): all 35 modes predicted from the *source*
 // neighbours with the decoder's z-order availability (never the below-left; a CTB's first unit only
 // uses the modes in `safe` -- bl_safe_modes -- because the raster wavefront reconstructs it before
-// its below-left), scored by the 4x4 Hadamard SATD of the residual + lambda * mode bits; the lowest
-// cost wins, ties to the lower mode.
+// its below-left), scored by the 4x4 Hadamard SATD of the residual + lambda * mode bits, searched
+// coarse-to-fine (intra_mode_search: at most 15 of the 35 modes); the lowest cost wins, ties to the
+// lower mode.
 int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int seg_w, int qp,
                       uint64_t safe) {
     const int x0 = x * 16, y0 = y * 16, z = ((y & 1) << 1) | (x & 1);
@@ -429,9 +430,8 @@ int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, i
     int L[33], T[33], pred[256];
     intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
     const int lambda = h264::lambda_sad(qp);
-    int best = 1, best_cost = 0x7fffffff;
-    for (int m = 0; m < 35; ++m) {
-        if (bl_pending && !((safe >> m) & 1)) continue;
+    auto cost = [&](int m) {
+        if (bl_pending && !((safe >> m) & 1)) return kIntraNoMode;
         intra_predict(m, 4, 0, L, T, pred);
         int satd = 0;
         for (int by = 0; by < 16; by += 4)
@@ -452,13 +452,9 @@ int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, i
                     satd += std::abs(a0 + a2) + std::abs(a1 + a3) + std::abs(a0 - a2) + std::abs(a1 - a3);
                 }
             }
-        const int cost = satd + lambda * intra_mode_bits(m, 1, 1);
-        if (cost < best_cost) {
-            best_cost = cost;
-            best = m;
-        }
-    }
-    return best;
+        return satd + lambda * intra_mode_bits(m, 1, 1);
+    };
+    return intra_mode_search(cost);
 }
 
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {

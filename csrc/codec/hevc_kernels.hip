@@ -1103,10 +1103,11 @@ __device__ __forceinline__ int ref_subst(int i, int N, int avl, const uint8_t* l
 }
 
 // ------------------------------------------------------------------ intra mode decision (I)
-// Open-loop, every unit of an I picture at once (one wave per unit, a workgroup per CTB): the 35
+// Open-loop, every unit of an I picture at once (one wave per unit, a workgroup per CTB): the
 // modes predicted from the *source* neighbours with the decoder's z-order availability (never the
 // below-left; a CTB's first unit keeps to bl_safe_modes, as k_hevc_intra reconstructs it before
-// its below-left), scored by 4x4 Hadamard SATD + lambda * mode bits -- hevc_cpu.cpp
+// its below-left), scored by 4x4 Hadamard SATD + lambda * mode bits, searched coarse-to-fine
+// (intra_mode_search: at most 15 of the 35 modes) -- hevc_cpu.cpp
 // intra_decide_mode.  The IDR wavefront (k_hevc_intra) then only reconstructs.
 __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const HevcFrameState* __restrict__ fs,
                                                            const uint8_t* __restrict__ src_y,
@@ -1177,10 +1178,8 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
     const mf_f4 zero = {0.f, 0.f, 0.f, 0.f};
     const int lambda = h264::lambda_sad(fs->qp);
     const uint64_t safe = fs->bl_safe;
-    int best = 1, best_cost = 0x7fffffff;
-#pragma unroll 1
-    for (int m = 0; m < 35; ++m) {
-        if (bl_pending && !((safe >> m) & 1)) continue;  // wave-uniform
+    auto cost = [&](int m) {
+        if (bl_pending && !((safe >> m) & 1)) return kIntraNoMode;  // wave-uniform
         mf_h4 a;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1193,12 +1192,9 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
         const mf_f4 sm = __builtin_amdgcn_mfma_f32_16x16x16f16(hm, tb, zero, 0, 0, 0);
         const int sad = (int)(__builtin_fabsf(sm[0]) + __builtin_fabsf(sm[1]) + __builtin_fabsf(sm[2]) +
                               __builtin_fabsf(sm[3]));
-        const int cost = wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
-        if (cost < best_cost) {
-            best_cost = cost;
-            best = m;
-        }
-    }
+        return wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
+    };
+    const int best = intra_mode_search(cost);  // coarse-to-fine: at most 15 of the 35 modes
     if (lane == 0) imode[y * g.mb_w + x] = (uint8_t)best;
 }
 
