@@ -615,6 +615,9 @@ def main() -> None:
             "device": args.device,
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
+            # -1 resolves per codec: H.264 / HEVC adaptive, VP8 off (csrc/codec/h264_encoder.h deblock)
+            "deblock_mode": {0: "off", 1: "on", 2: "adaptive"}.get(
+                int(cfg.enc.deblock), "off" if args.codec == "vp8" else "adaptive"),
             "intra_in_p": int(cfg.enc.intra_in_p),
             "vp8_tools": {"bpred": int(cfg.enc.vp8_bpred), "intra": int(cfg.enc.vp8_intra)} if args.codec == "vp8" else None,
             "deblocked_frames_pct": round(100.0 * sum(dbk) / max(1, len(dbk)), 1),
