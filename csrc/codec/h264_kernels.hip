@@ -1325,40 +1325,6 @@ __device__ __forceinline__ void pred4x4_row(int mode, const Nb4& n, int r, int* 
     }
 }
 
-// The 4 prediction samples of row r of an Intra4x4 block from one tap table instead of the mode
-// switch: the quads of a step code blocks in different modes, and the switch ran every mode's
-// branch with only its quads' lanes on.  Over the edge array X[15] = L3 L3 L2 L1 L0 P A0 .. A7 A7
-// (A4..A7 substituted by A3 without the top-right, as Nb4::t), byte c of kI4Tap[mode][r] is
-// s | type << 4: type 0 avg2(X[s], X[s+1]), 1 avg3(X[s], X[s+1], X[s+2]), 2 X[s].  The table was
-// generated from pred4x4_px (8.3.1.2.1 - 8.3.1.2.9) by exhaustive matching on random edges; DC
-// keeps the availability-dependent mean.
-constexpr uint32_t kI4Tap[9][4] = {
-    {0x29282726u, 0x29282726u, 0x29282726u, 0x29282726u},
-    {0x24242424u, 0x23232323u, 0x22222222u, 0x20202020u},
-    {0u, 0u, 0u, 0u},
-    {0x19181716u, 0x1A191817u, 0x1B1A1918u, 0x1C1B1A19u},
-    {0x17161514u, 0x16151413u, 0x15141312u, 0x14131211u},
-    {0x08070605u, 0x17161514u, 0x07060513u, 0x16151412u},
-    {0x16151404u, 0x14041303u, 0x13031202u, 0x12021101u},
-    {0x09080706u, 0x19181716u, 0x0A090807u, 0x1A191817u},
-    {0x11021203u, 0x10011102u, 0x20201001u, 0x20202020u}};
-__device__ __forceinline__ void pred4x4_row_tab(int mode, const Nb4& n, int r, int* pv) {
-    if (mode == kI4DC) {
-        const int d = pred4x4_px(kI4DC, n, 0, 0);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pv[c] = d;
-        return;
-    }
-    auto X = [&](int i) { return i <= 4 ? n.l(i == 0 ? 3 : 4 - i) : (i == 5 ? n.tl() : n.t(i >= 14 ? 7 : i - 6)); };
-    const uint32_t w = kI4Tap[mode][r];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int t = (int)((w >> (8 * c)) & 0xffu), s = t & 15, typ = t >> 4;
-        const int a = X(s), b = X(s + 1), e = X(s + 2);
-        pv[c] = typ == 2 ? a : (typ == 0 ? (a + b + 1) >> 1 : (a + 2 * b + e + 2) >> 2);
-    }
-}
-
 // Intra16x16 / chroma prediction of 4 samples of one row, the mode switch hoisted out of the row
 template <int M, bool C>
 __device__ __forceinline__ void predmb_row_m(const PredMb& p, const NbMb& n, int x0, int y, int* pv) {
@@ -1387,7 +1353,7 @@ __device__ __forceinline__ int i4_code_block(const Geometry& g, int rb, int r, i
     const Nb4 n = nb4_from_plane(tile, kLT, 0, 0, bx, by, av.left, av.top, av.topright, av.topleft);
     const uint32_t sw = ls[py * 4 + bx];
     int pv[4], x[4], y[4], z[4], d[4], rr[4];
-    pred4x4_row_tab(mode, n, r, pv);
+    pred4x4_row(mode, n, r, pv);
 #pragma unroll
     for (int c = 0; c < 4; ++c) x[c] = (int)((sw >> (8 * c)) & 0xff) - pv[c];
     fdct_row(x, r, y);
