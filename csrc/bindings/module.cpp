@@ -169,7 +169,8 @@ PYBIND11_MODULE(_native, m) {
         .def_readwrite("hevc_wpp", &h264::EncoderConfig::hevc_wpp)
         .def_readwrite("hevc_wpp_rows", &h264::EncoderConfig::hevc_wpp_rows)
         .def_readwrite("sao", &h264::EncoderConfig::sao)
-        .def_readwrite("hevc_chroma_keep", &h264::EncoderConfig::hevc_chroma_keep);
+        .def_readwrite("hevc_chroma_keep", &h264::EncoderConfig::hevc_chroma_keep)
+        .def_readwrite("hevc_intra_split", &h264::EncoderConfig::hevc_intra_split);
 
     py::class_<h264::FrameStats>(m, "FrameStats")
         .def_readonly("frame_index", &h264::FrameStats::frame_index)

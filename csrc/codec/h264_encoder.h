@@ -88,6 +88,10 @@ struct EncoderConfig {
                               // bpred_luma) when its SAD + lambda * mode bits beat the 16x16 mode's
     int tu_split = 2;         // HEVC: inter transform trees may split into 8x8 luma / 4x4 chroma TUs (1), and each
                               // 8x8 luma node again into four 4x4 TUs (2), per node by SSE + lambda * bits
+    // HEVC I pictures: a 16x16 intra unit may code its transform tree as four 8x8 luma / 4x4 chroma TUs,
+    // each predicted from the reconstruction of the TUs before it (same mode; mode-dependent scans),
+    // decided open-loop from the source (hevc_core.h intra_split_wins)
+    int hevc_intra_split = 1;
     int hevc_slice_cost = 1536;  // HEVC without WPP: P-picture slice work target (hevc_core.h cu_cost units)
     // HEVC wavefront parallel processing (entropy_coding_sync_enabled_flag): P pictures in slices of
     // hevc_wpp_rows CTU rows, every CTU row its own CABAC substream (one GPU wave each) that starts

@@ -76,6 +76,53 @@ MXHD void scan_pos(int log2n, int idx, int* x, int* y) {
     *y = sy * 4 + diag4y(n);
 }
 
+// scanIdx (7.4.9.11): 0 up-right diagonal, 1 horizontal, 2 vertical.  Intra 4x4 / 8x8 luma TUs and
+// 4x4 chroma TUs scan by their prediction mode (intra_scan_idx); every other TU diagonally.  The
+// horizontal scan is raster order (sub-blocks of an 8x8 TU too), the vertical one its transpose; the
+// 2x2 sub-block grid's diagonal order equals the vertical one.  Levels are stored per TU in the
+// TU's own scan order.
+MXHD int intra_scan_idx(int mode) { return (mode >= 6 && mode <= 14) ? 2 : ((mode >= 22 && mode <= 30) ? 1 : 0); }
+// position (x, y) in a 4x4 sub-block of scan position n
+MXHD void sb_pos(int scan, int n, int* x, int* y) {
+    if (scan == 0) {
+        *x = diag4x(n);
+        *y = diag4y(n);
+    } else if (scan == 1) {
+        *x = n & 3;
+        *y = n >> 2;
+    } else {
+        *x = n >> 2;
+        *y = n & 3;
+    }
+}
+// sub-block (x, y) of sub-block scan index i in a TU of log2n (sub-block grid 1x1, 2x2 or 4x4;
+// scanIdx 1 / 2 only occur up to 8x8)
+MXHD void sb_grid_pos(int log2n, int scan, int i, int* x, int* y) {
+    if (log2n == 4) {
+        *x = diag4x(i);
+        *y = diag4y(i);
+    } else if (log2n == 3) {
+        *x = scan == 1 ? (i & 1) : (i >> 1);
+        *y = scan == 1 ? (i >> 1) : (i & 1);
+    } else {
+        *x = *y = 0;
+    }
+}
+MXHD void scan_pos_s(int log2n, int scan, int idx, int* x, int* y) {
+    int sx, sy, px, py;
+    sb_grid_pos(log2n, scan, idx >> 4, &sx, &sy);
+    sb_pos(scan, idx & 15, &px, &py);
+    *x = sx * 4 + px;
+    *y = sy * 4 + py;
+}
+MXHD int scan_index_s(int log2n, int scan, int x, int y) {
+    if (scan == 0) return scan_index(log2n, x, y);
+    const int px = x & 3, py = y & 3, sx = x >> 2, sy = y >> 2;
+    const int n = scan == 1 ? py * 4 + px : px * 4 + py;
+    const int sb = log2n == 3 ? (scan == 1 ? sy * 2 + sx : sx * 2 + sy) : 0;
+    return sb * 16 + n;
+}
+
 // ---------------------------------------------------------------- core transform (8.6.4.2)
 // 32-point matrix coefficients by angle index m (cos(pi*m/64) scaled); every N-point
 // matrix row k is row k*32/N of the 32-point matrix.
@@ -897,23 +944,28 @@ MXHD int tu_last(const Cf& cf, int sb0, int nsb, uint32_t* csbf) {
 struct TuDesc {
     int sb0, log2n, cidx, last_idx;
     uint32_t csbf_mask;
+    int scan;  // scanIdx (intra_scan_idx for intra 4x4 / 8x8 luma and 4x4 chroma TUs, else 0)
 };
 // coded (or inferred: DC and last) sub-blocks of a TU as a raster mask
 MXHD uint32_t tu_csbf_raster(const TuDesc& t) {
     const int last_sb = t.last_idx >> 4, sbw = 1 << (t.log2n - 2);
     uint32_t r = 0;
     for (int i = 0; i <= last_sb; ++i) {
-        const int sx = t.log2n == 4 ? diag4x(i) : (i >> 1), sy = t.log2n == 4 ? diag4y(i) : (i & 1);
+        int sx, sy;
+        sb_grid_pos(t.log2n, t.scan, i, &sx, &sy);
         if (i == 0 || i == last_sb || ((t.csbf_mask >> i) & 1)) r |= 1u << (sy * sbw + sx);
     }
     return r;
 }
 
-// last_sig_coeff_x / _y prefix and suffix of a TU
+// last_sig_coeff_x / _y prefix and suffix of a TU (the vertical scan codes the pair swapped)
 template <class E, class Ctx>
 MXHD void code_tu_last(E& e, Ctx& ctx, const TuDesc& t) {
     int lx, ly;
-    scan_pos(t.log2n, t.last_idx, &lx, &ly);
+    if (t.scan == 2)
+        scan_pos_s(t.log2n, t.scan, t.last_idx, &ly, &lx);
+    else
+        scan_pos_s(t.log2n, t.scan, t.last_idx, &lx, &ly);
     code_last_prefix(e, ctx, C_LAST_X, lx, t.log2n, t.cidx);
     code_last_prefix(e, ctx, C_LAST_Y, ly, t.log2n, t.cidx);
     code_last_suffix(e, lx);
@@ -942,7 +994,8 @@ MXHD void code_sub_block(E& e, Ctx& ctx, const Cf& cf, const TuDesc& t, uint32_t
     const int log2n = t.log2n, cidx = t.cidx;
     const int last_sb = t.last_idx >> 4, last_n = t.last_idx & 15;
     const int sbw = 1 << (log2n - 2);
-    const int sx = log2n == 4 ? diag4x(i) : (i >> 1), sy = log2n == 4 ? diag4y(i) : (i & 1);
+    int sx, sy;
+    sb_grid_pos(log2n, t.scan, i, &sx, &sy);
     const bool right = sx + 1 < sbw && ((csbf_r >> (sy * sbw + sx + 1)) & 1);
     const bool below = sy + 1 < sbw && ((csbf_r >> ((sy + 1) * sbw + sx)) & 1);
     bool infer_dc = false;
@@ -959,7 +1012,8 @@ MXHD void code_sub_block(E& e, Ctx& ctx, const Cf& cf, const TuDesc& t, uint32_t
     for (int n = nstart; n >= 0; --n) {
         if (n == 0 && infer_dc) break;
         const int bit = (sig >> n) & 1;
-        const int xp = diag4x(n), yp = diag4y(n);
+        int xp, yp;
+        sb_pos(t.scan, n, &xp, &yp);
         int sc;
         if (log2n == 2) {
             sc = kCtxIdxMap4x4[(yp << 2) + xp];
@@ -976,7 +1030,7 @@ MXHD void code_sub_block(E& e, Ctx& ctx, const Cf& cf, const TuDesc& t, uint32_t
                 sc = 2;
             if (cidx == 0) {
                 if (i > 0) sc += 3;
-                sc += log2n == 3 ? 9 : 21;
+                sc += log2n == 3 ? (t.scan == 0 ? 9 : 15) : 21;
             } else {
                 sc += log2n == 3 ? 9 : 12;
             }
@@ -1192,18 +1246,18 @@ MXHD bool code_pred_head(E& e, Ctx& ctx, bool islice, const CuInfo& c, const CuN
 }
 
 // One 16x16 transform node of unit c at depth d (0: a CU16's tree, 1: a quadrant of a CU32's),
-// up to its children / residual: split_transform_flag (while d < depth_inter = max_transform_
-// hierarchy_depth_inter; intra depth 0), chroma cbf (coded at depth 0, else when the parent's is
-// set; context = depth), and for an unsplit node cbf_luma (inferred 1 for an inter node at depth 0
+// up to its children / residual: split_transform_flag (while d < depth = max_transform_hierarchy_
+// depth_inter or _intra, by the CU's prediction), chroma cbf (coded at depth 0, else when the parent's
+// is set; context = depth), and for an unsplit node cbf_luma (inferred 1 for an inter node at depth 0
 // without chroma; context 1 at depth 0) and cu_qp_delta when a level is coded and the CU's delta is
 // still pending.
 template <class E, class Ctx>
-MXHD void code_node16(E& e, Ctx& ctx, const CuInfo& c, int d, int pcb, int pcr, int depth_inter, bool qp_pending,
+MXHD void code_node16(E& e, Ctx& ctx, const CuInfo& c, int d, int pcb, int pcr, int depth, bool qp_pending,
                       int qp_pred) {
     const bool intra = c.type == kCuIntra;
     const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1, cy = c.cbf & 1;
-    const bool split = !intra && c.tu_split == 2;
-    if (!intra && d < depth_inter) e.bin(ctx, C_SPLIT_TRANSFORM + 1, split);  // ctxInc 5 - log2(16)
+    const bool split = c.tu_split == 2;
+    if (d < depth) e.bin(ctx, C_SPLIT_TRANSFORM + 1, split);  // ctxInc 5 - log2(16)
     if (d == 0 || pcb) e.bin(ctx, C_CBF_CHROMA + d, cb);
     if (d == 0 || pcr) e.bin(ctx, C_CBF_CHROMA + d, cr);
     if (split) return;
@@ -1227,15 +1281,15 @@ MXHD int split_qp_tu(const CuInfo& c) {
     return -1;
 }
 // 8x8 child k (depth d + 1) of a split 16x16 node at depth d; its chroma TUs are 4x4 at this node:
-// split_transform_flag (tu4: four 4x4 luma TUs) while d + 1 < depth_inter, chroma cbf when the
-// parent's is set, and for an unsplit child cbf_luma (context 0) and cu_qp_delta when pending and
-// this is its TU.
+// split_transform_flag (tu4: four 4x4 luma TUs) while d + 1 < depth (the CU's max_transform_
+// hierarchy_depth), chroma cbf when the parent's is set, and for an unsplit child cbf_luma (context 0)
+// and cu_qp_delta when pending and this is its TU.
 template <class E, class Ctx>
-MXHD void code_child8(E& e, Ctx& ctx, const CuInfo& c, int k, int d, int depth_inter, bool qp_pending, int qp_pred) {
+MXHD void code_child8(E& e, Ctx& ctx, const CuInfo& c, int k, int d, int depth, bool qp_pending, int qp_pred) {
     const int cb = (c.cbf >> 1) & 1, cr = (c.cbf >> 2) & 1;
     const int yk = (c.cbf_y4 >> k) & 1, cbk = (c.cbf_c4 >> k) & 1, crk = (c.cbf_c4 >> (4 + k)) & 1;
     const int s4 = (c.tu4 >> k) & 1;
-    if (d + 1 < depth_inter) e.bin(ctx, C_SPLIT_TRANSFORM + 2, s4);  // ctxInc 5 - log2(8)
+    if (d + 1 < depth) e.bin(ctx, C_SPLIT_TRANSFORM + 2, s4);  // ctxInc 5 - log2(8)
     if (cb) e.bin(ctx, C_CBF_CHROMA + d + 1, cbk);
     if (cr) e.bin(ctx, C_CBF_CHROMA + d + 1, crk);
     if (s4) return;  // the four 4x4 TUs code their own cbf_luma (code_grand4)
@@ -1254,28 +1308,33 @@ MXHD bool split_tu_coded(const CuInfo& c, int k, int t) {
     return t == 0 ? ((c.cbf_y4 >> k) & 1) : ((c.cbf_c4 >> (t == 1 ? k : 4 + k)) & 1);
 }
 MXHD int split_tu_sb0(int k, int t) { return t == 0 ? 4 * k : (t == 1 ? 16 + k : 20 + k); }
+// scanIdx of the split tree's TUs of CU c (8x8 / 4x4 luma and 4x4 chroma; DM chroma)
+MXHD int split_scan(const CuInfo& c) { return c.type == kCuIntra ? intra_scan_idx(c.intra_mode) : 0; }
 // TU descriptor of a split child's TU / an unsplit unit's TU
 template <class Cf>
-MXHD TuDesc split_tu_desc(const Cf& cf, int k, int t) {
+MXHD TuDesc split_tu_desc(const Cf& cf, int k, int t, int scan) {
     TuDesc d;
     d.sb0 = split_tu_sb0(k, t);
     d.log2n = t == 0 ? 3 : 2;
     d.cidx = t;
     d.last_idx = tu_last(cf, d.sb0, t == 0 ? 4 : 1, &d.csbf_mask);
+    d.scan = scan;
     return d;
 }
 // the 4x4 luma TU j of split child k (one sub-block: 4k + j)
 template <class Cf>
-MXHD TuDesc luma4_tu_desc(const Cf& cf, int k, int j) {
+MXHD TuDesc luma4_tu_desc(const Cf& cf, int k, int j, int scan) {
     TuDesc d;
     d.sb0 = 4 * k + j;
     d.log2n = 2;
     d.cidx = 0;
     d.last_idx = tu_last(cf, d.sb0, 1, &d.csbf_mask);
+    d.scan = scan;
     return d;
 }
 MXHD TuDesc flat_tu_desc(const CuInfo& c, int t) {
     TuDesc d;
+    d.scan = 0;
     d.sb0 = t == 0 ? 0 : (t == 1 ? 16 : 20);
     d.log2n = t == 0 ? 4 : 3;
     d.cidx = t;
@@ -1301,6 +1360,8 @@ struct UnitSyn {
     bool eos;          // ... equal to 1 (the slice's last CTB)
     bool end_subset;   // WPP: end_of_subset_one_bit (the last CTB of a CTB row, not of the slice)
     int depth_inter;   // max_transform_hierarchy_depth_inter
+    int depth_intra;   // max_transform_hierarchy_depth_intra
+    MXHD int depth_of(const CuInfo& c) const { return c.type == kCuIntra ? depth_intra : depth_inter; }
     bool sao_on, has_l, has_u;
     uint32_t sao[3], sao_l[3], sao_u[3];
 };
@@ -1309,7 +1370,7 @@ struct UnitSyn {
 // of raster unit u; sao: 4 words per CTB (nullptr: SAO off); qp_pred: the unit's QP predictor.
 template <class Get>
 MXHD UnitSyn unit_syn(const Get& get, const uint32_t* sao, int x, int y, int mb_w, int mb_h, bool islice,
-                      int first_ctb, int end_ctb, bool wpp, int depth_inter, int qp_pred) {
+                      int first_ctb, int end_ctb, bool wpp, int depth_inter, int depth_intra, int qp_pred) {
     UnitSyn u;
     const int cw = ctb_cols(mb_w);
     const int c = ctb_of(x, y, cw), z = ((y & 1) << 1) | (x & 1);
@@ -1320,6 +1381,7 @@ MXHD UnitSyn unit_syn(const Get& get, const uint32_t* sao, int x, int y, int mb_
     u.split_coded = ctb_whole(c, cw, mb_w, mb_h);
     u.cu32 = me.ct == 0;
     u.depth_inter = depth_inter;
+    u.depth_intra = depth_intra;
     u.qp_pred = qp_pred;
     u.nb = cu_nb_at(get, u.cu32 ? x0 : x, u.cu32 ? y0 : y, mb_w, cw, first_ctb);
     u.split_inc = 0;
@@ -1363,7 +1425,7 @@ MXHD UnitSyn unit_syn(const Get& get, const uint32_t* sao, int x, int y, int mb_
 enum CuResidual { kResNone = 0, kResFlat = 1, kResSplit = 2 };
 MXHD int unit_res_kind(const CuInfo& c, const UnitSyn& u) {
     if (!u.root) return kResNone;
-    if (c.type != kCuIntra && c.tu_split == 2) return kResSplit;
+    if (c.tu_split == 2) return kResSplit;
     return c.cbf ? kResFlat : kResNone;
 }
 
@@ -1386,17 +1448,17 @@ MXHD void code_unit_head(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u) {
                 e.bin(ctx, C_CBF_CHROMA + 0, u.cr0);
             }
         }
-        if (u.root) code_node16(e, ctx, c, 1, u.cb0, u.cr0, u.depth_inter, u.qp_pending, u.qp_pred);
+        if (u.root) code_node16(e, ctx, c, 1, u.cb0, u.cr0, u.depth_of(c), u.qp_pending, u.qp_pred);
         return;
     }
     // a CU16 (no split_cu_flag at depth 1 while the minimum CU is 16x16)
     if (code_pred_head(e, ctx, u.islice, c, u.nb, c.cbf != 0, kMinCbLog2))
-        code_node16(e, ctx, c, 0, 0, 0, u.depth_inter, true, u.qp_pred);
+        code_node16(e, ctx, c, 0, 0, 0, u.depth_of(c), true, u.qp_pred);
 }
 // split child k's head at the unit's tree depth, and the flags of its 4x4 TU j
 template <class E, class Ctx>
 MXHD void code_unit_child(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, int k) {
-    code_child8(e, ctx, c, k, u.cu32 ? 1 : 0, u.depth_inter, u.qp_pending, u.qp_pred);
+    code_child8(e, ctx, c, k, u.cu32 ? 1 : 0, u.depth_of(c), u.qp_pending, u.qp_pred);
 }
 template <class E, class Ctx>
 MXHD void code_unit_grand(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, int k, int j) {
@@ -1766,7 +1828,7 @@ MXHD int for_each_part(const CuInfo& c, const UnitSyn& u, const Cf& cf, F f) {
 #pragma unroll 1
             for (int j = 0; j < 4; ++j) {
                 const bool coded = (c.cbf_y16 >> (4 * k + j)) & 1;
-                if (coded) pt.d = luma4_tu_desc(cf, k, j);
+                if (coded) pt.d = luma4_tu_desc(cf, k, j, split_scan(c));
                 pt.k = k;
                 pt.t = j;
                 pt.kind = kPartGrand;
@@ -1782,7 +1844,7 @@ MXHD int for_each_part(const CuInfo& c, const UnitSyn& u, const Cf& cf, F f) {
         for (int t = s4 ? 1 : 0; t < 3; ++t) {
             const bool coded = kind == kResSplit ? split_tu_coded(c, k, t) : (((c.cbf >> t) & 1) != 0);
             if (!coded) continue;
-            pt.d = kind == kResSplit ? split_tu_desc(cf, k, t) : flat_tu_desc(c, t);
+            pt.d = kind == kResSplit ? split_tu_desc(cf, k, t, split_scan(c)) : flat_tu_desc(c, t);
             pt.k = k;
             pt.t = t;
             pt.kind = kPartTuLast;
@@ -1846,11 +1908,11 @@ MXHD void code_unit_direct(E& e, Ctx& ctx, const CuInfo& c, const UnitSyn& u, co
             if (s4)
                 for (int j = 0; j < 4; ++j) {
                     code_unit_grand(e, ctx, c, u, k, j);
-                    if ((c.cbf_y16 >> (4 * k + j)) & 1) code_residual(e, ctx, cf, luma4_tu_desc(cf, k, j));
+                    if ((c.cbf_y16 >> (4 * k + j)) & 1) code_residual(e, ctx, cf, luma4_tu_desc(cf, k, j, split_scan(c)));
                 }
 #pragma unroll 1
             for (int t = s4 ? 1 : 0; t < 3; ++t)
-                if (split_tu_coded(c, k, t)) code_residual(e, ctx, cf, split_tu_desc(cf, k, t));
+                if (split_tu_coded(c, k, t)) code_residual(e, ctx, cf, split_tu_desc(cf, k, t, split_scan(c)));
         }
     } else if (kind == kResFlat) {
 #pragma unroll 1
@@ -1869,6 +1931,7 @@ struct PicSyn {
     const uint32_t* sao;
     int mb_w, mb_h;
     int depth_inter;  // max_transform_hierarchy_depth_inter
+    int depth_intra;  // max_transform_hierarchy_depth_intra
 };
 struct ArrGet {  // raster CuInfo lookup for unit_syn
     const CuInfo* p;
@@ -1876,7 +1939,7 @@ struct ArrGet {  // raster CuInfo lookup for unit_syn
 };
 MXHD UnitSyn pic_unit_syn(const PicSyn& ps, int x, int y, bool islice, int first, int end, bool wpp) {
     return unit_syn(ArrGet{ps.cus}, ps.sao, x, y, ps.mb_w, ps.mb_h, islice, first, end, wpp, ps.depth_inter,
-                    ps.qp_pred[y * ps.mb_w + x]);
+                    ps.depth_intra, ps.qp_pred[y * ps.mb_w + x]);
 }
 
 // Entropy-code CTB c of the slice [first, end) into e: every unit inside the picture, in z order,
@@ -1929,6 +1992,30 @@ MXHD int intra_mode_bits(int mode, int cand_a, int cand_b) {
 // planar, DC and every fourth angular mode, then the modes two and one away from the best angular
 // mode so far -- at most 15 of the 35 predictions.  cost(m): the mode's cost, kIntraNoMode when the
 // mode may not be used; the lowest cost wins, ties to the lower mode.
+// Intra transform-tree split of a 16x16 unit (EncoderConfig::hevc_intra_split): four 8x8 luma TUs
+// and per chroma component four 4x4 TUs, in z order, each predicted in the unit's mode (DM chroma)
+// from the reconstruction of the TUs before it.  split_tu_avl: reference availability of TU k (bit 0
+// below-left, 1 left, 2 corner, 3 top, 4 top-right -- the segments of intra_refs / ref_subst) from
+// the unit's left / corner / top / top-right.  Inside the unit every decoded neighbour is there; not
+// decoded yet: the below-left of TUs 1 and 3 and the top-right of TU 3.  TU 2's below-left is the
+// unit below-left, which the decoder has only in a CTB's first unit (bl_pending) and the raster
+// wavefront has not reconstructed then: such a unit splits only in a mode that never reads it
+// (bl_safe_split) and predicts as if it were absent, as the unsplit unit does with bl_safe_modes.
+MXHD int split_tu_avl(int k, bool al, bool ac, bool at, bool atr) {
+    if (k == 0) return (al ? 3 : 0) | (ac ? 4 : 0) | (at ? 24 : 0);
+    if (k == 1) return 2 | (at ? 12 : 0) | (atr ? 16 : 0);
+    if (k == 2) return (al ? 6 : 0) | 24;
+    return 14;
+}
+// modes whose 8x8 luma and 4x4 DM chroma predictions never read the below-left references
+inline uint64_t bl_safe_split() { return bl_safe_modes(3, 0) & bl_safe_modes(2, 1); }
+// Open-loop choice (from the source, luma only, the mode decided for the unsplit unit): split when
+// the four TUs' 4x4 Hadamard SATD plus lambda * kIntraSplitBits (the split tree's extra cbf flags)
+// is below the unsplit prediction's.  The imode byte carries it in bit 6.
+constexpr int kIntraSplitBits = 6;
+constexpr int kIntraSplitFlag = 64;
+MXHD bool intra_split_wins(int satd16, int satd8, int lambda) { return satd8 + lambda * kIntraSplitBits < satd16; }
+
 constexpr int kIntraCoarse[11] = {0, 1, 2, 6, 10, 14, 18, 22, 26, 30, 34};
 constexpr int kIntraNoMode = 0x7fffffff;
 template <class F>
@@ -2011,7 +2098,7 @@ MXHD void inv_transform_t(const int* d, int* r) {
 }
 
 template <int L>
-MXHD int tu_encode_t(const int* res, int qp, bool intra, int16_t* levels, int* rres) {
+MXHD int tu_encode_t(const int* res, int qp, bool intra, int16_t* levels, int* rres, int scan = 0) {
     constexpr int N = 1 << L;
     const int log2n = L;
     int c[N * N], d[N * N];
@@ -2026,7 +2113,7 @@ MXHD int tu_encode_t(const int* res, int qp, bool intra, int16_t* levels, int* r
         }
     const bool drop = tu_decimate(log2n, intra, nz, mx);
     for (int v = 0; v < N; ++v)
-        for (int u = 0; u < N; ++u) levels[scan_index(log2n, u, v)] = (int16_t)(drop ? 0 : c[v * N + u]);
+        for (int u = 0; u < N; ++u) levels[scan_index_s(log2n, scan, u, v)] = (int16_t)(drop ? 0 : c[v * N + u]);
     if (!intra) {  // trailing isolated +-1 levels (same rule as the GPU kernel)
         for (int it = 0; it < kTrimIters; ++it) {
             int last = -1, prev = -1;
@@ -2042,7 +2129,7 @@ MXHD int tu_encode_t(const int* res, int qp, bool intra, int16_t* levels, int* r
     nz = 0;
     for (int v = 0; v < N; ++v)
         for (int u = 0; u < N; ++u) {
-            const int l = levels[scan_index(log2n, u, v)];
+            const int l = levels[scan_index_s(log2n, scan, u, v)];
             nz += l != 0;
             d[v * N + u] = dequant_coef(l, qp, log2n);
         }
@@ -2053,9 +2140,9 @@ MXHD int tu_encode_t(const int* res, int qp, bool intra, int16_t* levels, int* r
     return nz;
 }
 
-MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* levels, int* rres) {
-    if (log2n == 2) return tu_encode_t<2>(res, qp, intra, levels, rres);
-    if (log2n == 3) return tu_encode_t<3>(res, qp, intra, levels, rres);
+MXHD int tu_encode(int log2n, const int* res, int qp, bool intra, int16_t* levels, int* rres, int scan = 0) {
+    if (log2n == 2) return tu_encode_t<2>(res, qp, intra, levels, rres, scan);
+    if (log2n == 3) return tu_encode_t<3>(res, qp, intra, levels, rres, scan);
     return tu_encode_t<4>(res, qp, intra, levels, rres);
 }
 
@@ -2490,14 +2577,16 @@ MXHD void db_internal_seg(uint8_t* ry, int pitch, int ctb_w, const CuInfo* cus, 
                           int seg) {
     const CuInfo& c = cus[i];
     if (c.tu_split != 2) return;
-    const bool coded = dir == 0 ? (tu_cbf_at(c, 1, seg) || tu_cbf_at(c, 2, seg)) : (tu_cbf_at(c, seg, 1) ||
-                                                                                      tu_cbf_at(c, seg, 2));
+    // an intra unit's TU edges: Bs 2 (luma only: chroma edges lie on the 16-sample luma grid)
+    const bool intra = c.type == kCuIntra;
+    const bool coded = intra || (dir == 0 ? (tu_cbf_at(c, 1, seg) || tu_cbf_at(c, 2, seg))
+                                          : (tu_cbf_at(c, seg, 1) || tu_cbf_at(c, seg, 2)));
     if (!coded) return;
-    const int x = i % ctb_w, y = i / ctb_w;
+    const int x = i % ctb_w, y = i / ctb_w, bs = intra ? 2 : 1;
     if (dir == 0)
-        db_luma_seg(ry + (size_t)(y * 16 + seg * 4) * pitch + x * 16 + 8, 1, pitch, 1, qpy[i], qpy[i]);
+        db_luma_seg(ry + (size_t)(y * 16 + seg * 4) * pitch + x * 16 + 8, 1, pitch, bs, qpy[i], qpy[i]);
     else
-        db_luma_seg(ry + (size_t)(y * 16 + 8) * pitch + x * 16 + seg * 4, pitch, 1, 1, qpy[i], qpy[i]);
+        db_luma_seg(ry + (size_t)(y * 16 + 8) * pitch + x * 16 + seg * 4, pitch, 1, bs, qpy[i], qpy[i]);
 }
 
 

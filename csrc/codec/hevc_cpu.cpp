@@ -193,7 +193,7 @@ void HevcCommon::write_parameter_sets(std::vector<uint8_t>& out) const {
         w.ue(0);  // log2_min_luma_transform_block_size_minus2 (4)
         w.ue(kMaxTbLog2 - 2);  // log2_diff_max_min_luma_transform_block_size (16)
         w.ue((uint32_t)depth_inter());  // max_transform_hierarchy_depth_inter
-        w.ue(0);  // max_transform_hierarchy_depth_intra
+        w.ue((uint32_t)depth_intra());  // max_transform_hierarchy_depth_intra
         w.put(0, 1);  // scaling_list_enabled_flag
         w.put(0, 1);  // amp_enabled_flag
         w.put(c.sao ? 1 : 0, 1);  // sample_adaptive_offset_enabled_flag
@@ -396,6 +396,7 @@ CpuHevcEncoder::CpuHevcEncoder(const EncoderConfig& cfg) : cfg_(cfg.with_aq_defa
     qp_pred_.assign(n, 0);
     qpy_.assign(n, 0);
     bl_safe_ = bl_safe_modes(4, 0) & bl_safe_modes(3, 1);  // the 16x16 luma mode and its DM chroma
+    bl_safe_split_ = bl_safe_split();
 }
 
 namespace {
@@ -403,6 +404,47 @@ namespace {
 void summarise(CuInfo& c, const int16_t* coef) {
     cu_summarise(c, coef);
     set_est_bytes(c, cu_bits_est(coef, c.tu_split == 2, c.tu4));
+}
+
+// 4x4 Hadamard SATD of the 16x16 source block at (x0, y0) against pred (raster 16x16): the sum over
+// its sixteen 4x4 blocks (k_hevc_intra_modes: the same sums on the matrix cores).
+int satd16(const uint8_t* sy, int pitch, int x0, int y0, const int* pred) {
+    int satd = 0;
+    for (int by = 0; by < 16; by += 4)
+        for (int bx = 0; bx < 16; bx += 4) {
+            int d[4][4], h[4][4];
+            for (int r = 0; r < 4; ++r)
+                for (int q = 0; q < 4; ++q)
+                    d[r][q] = (int)sy[(size_t)(y0 + by + r) * pitch + x0 + bx + q] - pred[(by + r) * 16 + bx + q];
+            for (int r = 0; r < 4; ++r) {  // rows, then columns: 4-point Walsh-Hadamard
+                const int a0 = d[r][0] + d[r][1], a1 = d[r][0] - d[r][1], a2 = d[r][2] + d[r][3], a3 = d[r][2] - d[r][3];
+                h[r][0] = a0 + a2;
+                h[r][1] = a1 + a3;
+                h[r][2] = a0 - a2;
+                h[r][3] = a1 - a3;
+            }
+            for (int q = 0; q < 4; ++q) {
+                const int a0 = h[0][q] + h[1][q], a1 = h[0][q] - h[1][q], a2 = h[2][q] + h[3][q], a3 = h[2][q] - h[3][q];
+                satd += std::abs(a0 + a2) + std::abs(a1 + a3) + std::abs(a0 - a2) + std::abs(a1 - a3);
+            }
+        }
+    return satd;
+}
+
+// Substituted references (intra_refs) of the N x N block at (x, y) of a plane -- step 1: luma, 2: one
+// NV12 chroma component (p at its first sample) -- with availability avl (split_tu_avl bits).
+void block_refs(const uint8_t* p, int pitch, int step, int x, int y, int N, int avl, int* L, int* T) {
+    uint8_t lp[16], bp[16], tp[16], tr[16];
+    auto px = [&](int xx, int yy) { return p[(size_t)yy * pitch + (size_t)xx * step]; };
+    for (int k = 0; k < N; ++k) {
+        lp[k] = (avl & 2) ? px(x - 1, y + k) : 0;
+        bp[k] = (avl & 1) ? px(x - 1, y + N + k) : 0;
+        tp[k] = (avl & 8) ? px(x + k, y - 1) : 0;
+        tr[k] = (avl & 16) ? px(x + N + k, y - 1) : 0;
+    }
+    const int corner = (avl & 4) ? px(x - 1, y - 1) : 0;
+    intra_refs(N, (avl & 2) != 0, (avl & 1) != 0, (avl & 8) != 0, (avl & 16) != 0, (avl & 4) != 0, lp, bp, tp, tr,
+               corner, L, T);
 }
 }  // namespace
 
@@ -412,9 +454,11 @@ void summarise(CuInfo& c, const int16_t* coef) {
 // uses the modes in `safe` -- bl_safe_modes -- because the raster wavefront reconstructs it before
 // its below-left), scored by the 4x4 Hadamard SATD of the residual + lambda * mode bits, searched
 // coarse-to-fine (intra_mode_search: at most 15 of the 35 modes); the lowest cost wins, ties to the
-// lower mode.
+// lower mode.  With split, the chosen mode is also predicted as four 8x8 TUs from the source
+// (split_tu_avl; a CTB's first unit only in a safe_split mode) and kIntraSplitFlag is set when
+// intra_split_wins.
 int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int seg_w, int qp,
-                      uint64_t safe) {
+                      uint64_t safe, uint64_t safe_split, bool split) {
     const int x0 = x * 16, y0 = y * 16, z = ((y & 1) << 1) | (x & 1);
     int xb, xe;
     i_seg_range(x, seg_w, mb_w, xb, xe);
@@ -433,28 +477,21 @@ int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, i
     auto cost = [&](int m) {
         if (bl_pending && !((safe >> m) & 1)) return kIntraNoMode;
         intra_predict(m, 4, 0, L, T, pred);
-        int satd = 0;
-        for (int by = 0; by < 16; by += 4)
-            for (int bx = 0; bx < 16; bx += 4) {
-                int d[4][4], h[4][4];
-                for (int r = 0; r < 4; ++r)
-                    for (int q = 0; q < 4; ++q)
-                        d[r][q] = (int)sy[(size_t)(y0 + by + r) * pitch + x0 + bx + q] - pred[(by + r) * 16 + bx + q];
-                for (int r = 0; r < 4; ++r) {  // rows, then columns: 4-point Walsh-Hadamard
-                    const int a0 = d[r][0] + d[r][1], a1 = d[r][0] - d[r][1], a2 = d[r][2] + d[r][3], a3 = d[r][2] - d[r][3];
-                    h[r][0] = a0 + a2;
-                    h[r][1] = a1 + a3;
-                    h[r][2] = a0 - a2;
-                    h[r][3] = a1 - a3;
-                }
-                for (int q = 0; q < 4; ++q) {
-                    const int a0 = h[0][q] + h[1][q], a1 = h[0][q] - h[1][q], a2 = h[2][q] + h[3][q], a3 = h[2][q] - h[3][q];
-                    satd += std::abs(a0 + a2) + std::abs(a1 + a3) + std::abs(a0 - a2) + std::abs(a1 - a3);
-                }
-            }
-        return satd + lambda * intra_mode_bits(m, 1, 1);
+        return satd16(sy, pitch, x0, y0, pred) + lambda * intra_mode_bits(m, 1, 1);
     };
-    return intra_mode_search(cost);
+    const int best = intra_mode_search(cost);
+    if (!split || (bl_pending && !((safe_split >> best) & 1))) return best;
+    intra_predict(best, 4, 0, L, T, pred);
+    const int s16 = satd16(sy, pitch, x0, y0, pred);
+    for (int k = 0; k < 4; ++k) {
+        const int bx = (k & 1) * 8, by = (k >> 1) * 8;
+        int Lk[17], Tk[17], p8[64];
+        block_refs(sy, pitch, 1, x0 + bx, y0 + by, 8, split_tu_avl(k, al, ac, at, atr), Lk, Tk);
+        intra_predict(best, 3, 0, Lk, Tk, p8);
+        for (int r = 0; r < 8; ++r)
+            for (int q = 0; q < 8; ++q) pred[(by + r) * 16 + bx + q] = p8[r * 8 + q];
+    }
+    return intra_split_wins(s16, satd16(sy, pitch, x0, y0, pred), lambda) ? best | kIntraSplitFlag : best;
 }
 
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {
@@ -463,6 +500,7 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
     const int W = common_.ctb_w(), H = common_.ctb_h(), sr = 2 * common_.slice_rows();  // unit rows per I slice
     const int qp = frame_qp_();
     const int qpc = chroma_qp(qp, cfg_.chroma_qp_offset);
+    const bool split_on = common_.depth_intra() > 0;
     // units in raster order (the GPU's row wavefront) with the modes decided open-loop on the
     // source (intra_decide_mode); availability as the decoder sees it in z order: no above-right
     // for a CTB's last unit, no below-left reads by a CTB's first unit (see bl_safe_modes)
@@ -475,6 +513,48 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             int xb, xe;
             i_seg_range(x, common_.i_seg_w(), W, xb, xe);
             const bool al = x > xb, at = (y % sr) != 0, atr = at && x + 1 < xe && z != 3, ac = at && x > xb;
+            const int dm = intra_decide_mode(sy, pitch, W, H, x, y, sr, common_.i_seg_w(), qp, bl_safe_, bl_safe_split_,
+                                             split_on);
+            const int best = dm & (kIntraSplitFlag - 1);
+            c.type = kCuIntra;
+            c.intra_mode = (uint8_t)best;
+            c.qp = (uint8_t)qp;
+            c.ct = 1;
+            int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
+            if (dm & kIntraSplitFlag) {
+                // four 8x8 luma TUs, then per TU its two 4x4 chroma TUs, each predicted from the
+                // reconstruction so far (ry / ruv hold it as the TUs complete)
+                c.tu_split = 2;
+                const int scan = intra_scan_idx(best);
+                for (int k = 0; k < 4; ++k) {
+                    const int avl = split_tu_avl(k, al, ac, at, atr);
+                    const int bx = x0 + (k & 1) * 8, by = y0 + (k >> 1) * 8;
+                    int Lk[17], Tk[17], p8[64], r8[64], rr8[64];
+                    block_refs(ry, cw_, 1, bx, by, 8, avl, Lk, Tk);
+                    intra_predict(best, 3, 0, Lk, Tk, p8);
+                    for (int r = 0; r < 8; ++r)
+                        for (int q = 0; q < 8; ++q) r8[r * 8 + q] = sy[(size_t)(by + r) * pitch + bx + q] - p8[r * 8 + q];
+                    tu_encode(3, r8, qp, true, co + 64 * k, rr8, scan);
+                    for (int r = 0; r < 8; ++r)
+                        for (int q = 0; q < 8; ++q) ry[(by + r) * cw_ + bx + q] = (uint8_t)clip255(p8[r * 8 + q] + rr8[r * 8 + q]);
+                    const int cx = bx / 2, cy = by / 2;
+                    for (int comp = 0; comp < 2; ++comp) {
+                        int Lc[9], Tc[9], p4[16], r4[16], rr4[16];
+                        block_refs(ruv + comp, cw_, 2, cx, cy, 4, avl, Lc, Tc);
+                        intra_predict(best, 2, 1 + comp, Lc, Tc, p4);
+                        for (int r = 0; r < 4; ++r)
+                            for (int q = 0; q < 4; ++q)
+                                r4[r * 4 + q] = suv[(size_t)(cy + r) * pitch + 2 * (cx + q) + comp] - p4[r * 4 + q];
+                        tu_encode(2, r4, qpc, true, co + 256 + 64 * comp + 16 * k, rr4, scan);
+                        for (int r = 0; r < 4; ++r)
+                            for (int q = 0; q < 4; ++q)
+                                ruv[(cy + r) * cw_ + 2 * (cx + q) + comp] = (uint8_t)clip255(p4[r * 4 + q] + rr4[r * 4 + q]);
+                    }
+                }
+                summarise(c, co);
+                mv_[2 * i] = mv_[2 * i + 1] = 0;
+                continue;
+            }
             uint8_t lp[16], tp[16], tr[16];
             for (int k = 0; k < 16; ++k) {
                 lp[k] = al ? ry[(y0 + k) * cw_ + x0 - 1] : 0;
@@ -484,13 +564,7 @@ void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pi
             const int corner = ac ? ry[(y0 - 1) * cw_ + x0 - 1] : 0;
             int L[33], T[33];
             intra_refs(16, al, false, at, atr, ac, lp, lp, tp, tr, corner, L, T);
-            const int best = intra_decide_mode(sy, pitch, W, H, x, y, sr, common_.i_seg_w(), qp, bl_safe_);
             int pred[256];
-            c.type = kCuIntra;
-            c.intra_mode = (uint8_t)best;
-            c.qp = (uint8_t)qp;
-            c.ct = 1;
-            int16_t* co = coef_.data() + (size_t)i * kCoefPerCu;
             intra_predict(best, 4, 0, L, T, pred);
             int res[256], rr[256];
             for (int r = 0; r < 16; ++r)
@@ -676,7 +750,8 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
         analyse_intra(y, uv, pitch);
         slices_ = common_.row_slices();
         qp_chain(qp_override_);
-        const PicSyn ps{cu_.data(), coef_.data(), qp_pred_.data(), nullptr, W, H, common_.depth_inter()};
+        const PicSyn ps{cu_.data(), coef_.data(), qp_pred_.data(), nullptr, W, H, common_.depth_inter(),
+                        common_.depth_intra()};
         std::vector<uint8_t> buf;
         std::vector<uint32_t> sub_len;
         uint8_t ctx[C_NUM];
@@ -760,7 +835,7 @@ const std::vector<uint8_t>& CpuHevcEncoder::encode(const uint8_t* y, const uint8
     std::vector<uint32_t> sub_len;
     uint8_t ctx[C_NUM];
     const PicSyn ps{cu_.data(), coef_.data(), qp_pred_.data(), cfg_.sao ? sao_.data() : nullptr, W, H,
-                    common_.depth_inter()};
+                    common_.depth_inter(), common_.depth_intra()};
     for (size_t s = 0; s < slices_.size(); ++s) {
         const int first = slices_[s], end = slice_end(s);
         const uint32_t cap = (uint32_t)(end - first) * 4096 + 1024;
@@ -872,8 +947,8 @@ int token_selftest(uint32_t seed, int slices) {
                     cu.mvdy = (int16_t)((int)rnd(64) - 32);
                     cu.mvp_idx = (uint8_t)(cu.type == kCuAmvp ? rnd(2) : rnd(5));
                 }
-                cu.tu_split = cu.type == kCuIntra ? 1 : (uint8_t)(1 + rnd(2));
-                cu.tu4 = cu.tu_split == 2 ? (uint8_t)rnd(16) : 0;  // 8x8 nodes split into 4x4 TUs
+                cu.tu_split = (uint8_t)(1 + rnd(2));  // intra too (max_transform_hierarchy_depth_intra 1 below)
+                cu.tu4 = (cu.tu_split == 2 && cu.type != kCuIntra) ? (uint8_t)rnd(16) : 0;  // 8x8 nodes into 4x4 TUs
                 if (cu.type != kCuSkip) fill_levels(cu, i);
                 qpp[(size_t)i] = (uint8_t)(10 + rnd(40));
             }
@@ -888,7 +963,7 @@ int token_selftest(uint32_t seed, int slices) {
         }
         const bool use_sao = rnd(2) != 0;
         const PicSyn ps{cus.data(), coef.data(), qpp.data(), use_sao ? sao.data() : nullptr, mb_w, mb_h,
-                        rnd(2) ? 3 : 0};
+                        rnd(2) ? 3 : 0, 1};
         const uint32_t cap = (uint32_t)(end - first) * 16384 + 1024;
         std::vector<uint8_t> a(cap), b(cap);
         std::vector<uint16_t> tok(kMaxCuTokens);

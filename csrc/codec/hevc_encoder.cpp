@@ -107,6 +107,7 @@ GpuHevcEncoder::GpuHevcEncoder(const EncoderConfig& cfg, hipStream_t stream)
     if (std::max((ncu + 3) / 4, common_.num_ctbs()) > h264::kSsePartStride)
         throw std::invalid_argument("frame too large for the distortion partials");
     bl_safe_ = bl_safe_modes(4, 0) & bl_safe_modes(3, 1);
+    bl_safe_split_ = bl_safe_split();
     const size_t ysz = (size_t)geom_.pitch * geom_.coded_h, uvsz = ysz / 2;
     for (int i = 0; i < 2; ++i) {
         HIP_CHECK(hipMalloc(&rec_y_[i], ysz));
@@ -178,7 +179,6 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.deblock_on = cfg_.hevc_deblock() ? 1 : 0;  // adaptive: k_hevc_db_auto overwrites it on the device
     f.deblock_auto = cfg_.hevc_deblock_auto() ? 1 : 0;
     f.chroma_keep = cfg_.hevc_chroma_keep ? 1 : 0;
-    f.pad3_ = 0;
     f.rec_y = f.sao ? pre_y_ : rec_y_[cur];
     f.rec_uv = f.sao ? pre_uv_ : rec_uv_[cur];
     f.sao_y = rec_y_[cur];
@@ -191,7 +191,9 @@ void GpuHevcEncoder::fill_state(FrameSlot& sl, bool idr, int qp, int ref, int cu
     f.i_seg_w = common_.i_seg_w();
     f.num_slices = common_.num_slices();
     f.bl_safe = bl_safe_;
+    f.bl_safe_split = bl_safe_split_;
     f.depth_inter = common_.depth_inter();
+    f.depth_intra = common_.depth_intra();
     f.aq = cfg_.aq;
     f.tu_split = cfg_.tu_split;  // 0 none, 1 8x8 nodes, 2 also 4x4 luma TUs
     f.chroma_qp_offset = cfg_.chroma_qp_offset;

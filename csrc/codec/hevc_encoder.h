@@ -44,6 +44,9 @@ class HevcCommon {
     // max_transform_hierarchy_depth_inter: 3 with split inter transform trees (a CU32's 16x16
     // quadrants at depth 1 may split too), else 0
     int depth_inter() const { return config().tu_split ? 3 : 0; }
+    // max_transform_hierarchy_depth_intra: 1 when intra CU16s may split into four 8x8 luma / 4x4 chroma
+    // TUs (EncoderConfig::hevc_intra_split), else 0
+    int depth_intra() const { return config().hevc_intra_split ? 1 : 0; }
     int slice_rows() const { return slice_rows_; }  // CTB rows per I slice
     int i_split() const { return i_split_; }        // I slices per CTB row (segments)
     int i_seg_w() const { return 2 * ((c32_w() + i_split_ - 1) / i_split_); }  // 16x16-unit columns per segment
@@ -81,9 +84,10 @@ class HevcCommon {
     int max_slices_ = 1;
 };
 
-// Open-loop intra mode of a 16x16 unit (hevc_cpu.cpp; the GPU's k_hevc_intra_modes).
+// Open-loop intra mode of a 16x16 unit (hevc_cpu.cpp; the GPU's k_hevc_intra_modes), with
+// kIntraSplitFlag set when split (nonzero safe_split) codes it as four 8x8 TUs.
 int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int seg_w, int qp,
-                      uint64_t safe);
+                      uint64_t safe, uint64_t safe_split = 0, bool split = false);
 // Direct vs bin-token CABAC on random slices (hevc_cpu.cpp); returns the slices checked.
 int token_selftest(uint32_t seed, int slices);
 // Entropy-code the slice of CTBs [first, end) with wavefront parallel processing (host): every CTB
@@ -125,6 +129,7 @@ class CpuHevcEncoder {
     std::vector<int> slices_;  // first CTB of every slice of the current picture
     std::vector<uint8_t> qp_pred_, qpy_;  // per unit: QP predictor / QpY (slice_qp_chain)
     uint64_t bl_safe_ = 0;     // intra modes safe with a pending below-left (bl_safe_modes, luma 16 & chroma 8)
+    uint64_t bl_safe_split_ = 0;  // ... of a split unit (bl_safe_split: luma 8 & chroma 4)
     std::vector<int16_t> coef_;
     std::vector<uint8_t> au_;
     std::vector<uint8_t> prev_src_;  // previous source luma (coded size), temporal AQ classes
@@ -184,10 +189,11 @@ struct HevcFrameState {
     // intra modes a CTB's first unit may use while its below-left is not reconstructed yet
     // (hevc_core.h bl_safe_modes: 16x16 luma and its DM 8x8 chroma)
     uint64_t bl_safe;
+    uint64_t bl_safe_split;  // the same for a unit coded as four 8x8 TUs (hevc_core.h bl_safe_split)
     int32_t depth_inter;  // max_transform_hierarchy_depth_inter of the SPS
     int32_t deblock_auto;  // EncoderConfig::deblock 2: k_hevc_db_auto decides deblock_on (h264_deblock.h rule)
     int32_t chroma_keep;   // EncoderConfig::hevc_chroma_keep: changing content keeps its chroma residual
-    int32_t pad3_;
+    int32_t depth_intra;   // max_transform_hierarchy_depth_intra of the SPS (1: intra units may split)
 };
 
 struct HevcOutHeader {
@@ -357,6 +363,7 @@ class GpuHevcEncoder final : public VideoEncoder {
     uint8_t* rec_uv_[2] = {nullptr, nullptr};
     uint8_t* src_keep_[2] = {nullptr, nullptr};  // source luma of the last two frames (temporal AQ classes)
     uint64_t bl_safe_ = 0;       // hevc_core.h bl_safe_modes (16x16 luma & DM chroma)
+    uint64_t bl_safe_split_ = 0; // hevc_core.h bl_safe_split (8x8 luma & DM 4x4 chroma)
     uint8_t* pre_y_ = nullptr;   // SAO: reconstruction before SAO (deblocked in place)
     uint8_t* pre_uv_ = nullptr;
     uint32_t* db_state_ = nullptr;  // adaptive filter state (HevcDeviceBuffers::db_state)

@@ -1102,17 +1102,59 @@ __device__ __forceinline__ int ref_subst(int i, int N, int avl, const uint8_t* l
     return trx[j - 3 * N - 1];
 }
 
+// References of the four 8x8 TUs of a split intra unit (hevc_core.h split_tu_avl): raw samples (left
+// then below-left, top, top-right, corner), substituted L / T, the [1 2 1]-filtered LF / TF, DC.
+struct SplitRefs {
+    uint8_t lp[4][16], tp[4][8], tr[4][8];
+    int corner[4];
+    int L[4][17], T[4][17], LF[4][17], TF[4][17];
+    int dc[4];
+};
+// Substitution, filtering and DC of SplitRefs whose raw samples are in place (whole wave; ends
+// with the wave's LDS hand-off).
+__device__ __forceinline__ void split_refs_finish(SplitRefs& S, bool al, bool ac, bool at, bool atr, int lane) {
+    for (int i = lane; i < 4 * 33; i += 64) {
+        const int k = i / 33, q = i - k * 33;
+        const int v = ref_subst(q, 8, split_tu_avl(k, al, ac, at, atr), S.lp[k], S.tp[k], S.tr[k], S.corner[k]);
+        if (q < 16) S.L[k][16 - q] = v;
+        else if (q == 16) S.L[k][0] = S.T[k][0] = v;
+        else S.T[k][q - 16] = v;
+    }
+    wave_lds_sync();
+    for (int i = lane; i < 4 * 17; i += 64) {
+        const int k = i / 17, q = i - k * 17;
+        if (q == 0) {
+            S.LF[k][0] = S.TF[k][0] = (S.L[k][1] + 2 * S.L[k][0] + S.T[k][1] + 2) >> 2;
+        } else if (q == 16) {
+            S.LF[k][16] = S.L[k][16];
+            S.TF[k][16] = S.T[k][16];
+        } else {
+            S.LF[k][q] = (S.L[k][q + 1] + 2 * S.L[k][q] + S.L[k][q - 1] + 2) >> 2;
+            S.TF[k][q] = (S.T[k][q + 1] + 2 * S.T[k][q] + S.T[k][q - 1] + 2) >> 2;
+        }
+    }
+    {
+        const int k = lane >> 4, q = lane & 15;
+        const int sum = gsum<16>(q < 8 ? S.L[k][1 + q] : S.T[k][1 + q - 8]);
+        if (q == 0) S.dc[k] = (sum + 8) >> 4;
+    }
+    wave_lds_sync();
+}
+
 // ------------------------------------------------------------------ intra mode decision (I)
 // Open-loop, every unit of an I picture at once (one wave per unit, a workgroup per CTB): the
 // modes predicted from the *source* neighbours with the decoder's z-order availability (never the
 // below-left; a CTB's first unit keeps to bl_safe_modes, as k_hevc_intra reconstructs it before
 // its below-left), scored by 4x4 Hadamard SATD + lambda * mode bits, searched coarse-to-fine
 // (intra_mode_search: at most 15 of the 35 modes) -- hevc_cpu.cpp
-// intra_decide_mode.  The IDR wavefront (k_hevc_intra) then only reconstructs.
+// intra_decide_mode.  With intra splits on, the chosen mode is also predicted as four 8x8 TUs from
+// the source (split_tu_avl) and kIntraSplitFlag set when intra_split_wins.  The IDR wavefront
+// (k_hevc_intra) then only reconstructs.
 __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const HevcFrameState* __restrict__ fs,
                                                            const uint8_t* __restrict__ src_y,
                                                            uint8_t* __restrict__ imode) {
     __shared__ IntraRefs rf[4];
+    __shared__ SplitRefs srf[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int bid = blockIdx.x, cw = ctb_cols(g.mb_w);
     const int x = 2 * (bid % cw) + (wave & 1), y = 2 * (bid / cw) + (wave >> 1);
@@ -1195,7 +1237,223 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
         return wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
     };
     const int best = intra_mode_search(cost);  // coarse-to-fine: at most 15 of the 35 modes
-    if (lane == 0) imode[y * g.mb_w + x] = (uint8_t)best;
+    int out = best;
+    if (fs->depth_intra > 0 && (!bl_pending || ((fs->bl_safe_split >> best) & 1))) {  // wave-uniform
+        SplitRefs& S = srf[wave];
+        for (int i = lane; i < 4 * 33; i += 64) {  // raw references of the four TUs, from the source
+            const int k = i / 33, q = i - k * 33;
+            const int bx = x0 + (k & 1) * 8, by = y0 + (k >> 1) * 8;
+            const int avl = split_tu_avl(k, al, ac, at, atr);
+            if (q < 16) {  // left (q < 8), below-left
+                S.lp[k][q] = (avl & (q < 8 ? 2 : 1)) ? src_y[(size_t)(by + q) * P + bx - 1] : 0;
+            } else if (q < 24) {
+                S.tp[k][q - 16] = (avl & 8) ? src_y[(size_t)(by - 1) * P + bx + q - 16] : 0;
+            } else if (q < 32) {
+                S.tr[k][q - 24] = (avl & 16) ? src_y[(size_t)(by - 1) * P + bx + 8 + q - 24] : 0;
+            } else {
+                S.corner[k] = (avl & 4) ? src_y[(size_t)(by - 1) * P + bx - 1] : 0;
+            }
+        }
+        wave_lds_sync();
+        split_refs_finish(S, al, ac, at, atr, lane);
+        const int kq = ((r >> 3) << 1) | (cb >> 3);  // the lane's four samples lie in one TU
+        mf_h4 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            a[j] = (_Float16)((int)((sw >> (8 * j)) & 0xff) -
+                              pred_sample(best, 3, true, S.L[kq], S.T[kq], S.LF[kq], S.TF[kq], S.dc[kq], (cb + j) & 7, r & 7));
+        const mf_f4 t = __builtin_amdgcn_mfma_f32_16x16x16f16(a, hm, zero, 0, 0, 0);
+        mf_h4 tb;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tb[i] = (_Float16)t[i];
+        const mf_f4 sm = __builtin_amdgcn_mfma_f32_16x16x16f16(hm, tb, zero, 0, 0, 0);
+        const int s8 = wsum((int)(__builtin_fabsf(sm[0]) + __builtin_fabsf(sm[1]) + __builtin_fabsf(sm[2]) +
+                                  __builtin_fabsf(sm[3])));
+        const int s16 = cost(best) - lambda * intra_mode_bits(best, 1, 1);
+        if (intra_split_wins(s16, s8, lambda)) out |= kIntraSplitFlag;
+    }
+    if (lane == 0) imode[y * g.mb_w + x] = (uint8_t)out;
+}
+
+// A split intra unit (kIntraSplitFlag) in the IDR wavefront, by its wave alone (wave-local LDS
+// hand-offs): TU k = 0..3 in z order, each its 8x8 luma (lane = sample y * 8 + x) and its two 4x4
+// chroma TUs (lanes 0..31: component lane >> 4, sample (lane >> 2) & 3, lane & 3) -- references from
+// the unit's neighbours (R) and the reconstruction of the TUs before it (t.pred), prediction in the
+// unit's mode, then forward transform, quantisation (intra: no decimation, no trim), levels in the
+// mode's scan order, inverse transform and reconstruction into t.pred / rec -- as tu_encode_t<3> /
+// <2> of the CPU encoder's analyse_intra.  src: the unit's source (t.pred layout); lv: LDS copy of
+// the unit's levels (CU layout); the raw references go through S.
+struct SplitIntraResult {
+    int sse[3];
+    uint32_t bits;  // cu_bits_est of the split tree
+};
+__device__ SplitIntraResult split_intra_code(TuBuf& t, SplitRefs& S, const IntraRefs& R, const Mats& M,
+                                             const uint8_t* src, int16_t* lv, int mode, int qp, int qpc, bool al,
+                                             bool ac, bool at, bool atr, int16_t* coef, uint8_t* rec_y,
+                                             uint8_t* rec_uv, int pitch, int x0, int y0, int disp_w, int disp_h) {
+    const int lane = threadIdx.x & 63;
+    const int scan = intra_scan_idx(mode);
+    const int ly = lane >> 3, lx = lane & 7;                            // luma sample / coefficient
+    const int comp = (lane >> 4) & 1, cy = (lane >> 2) & 3, cx = lane & 3;  // chroma (lanes < 32)
+    const bool cl = lane < 32;
+    int16_t* aT = reinterpret_cast<int16_t*>(t.a);  // stage buffers: luma [0, 64), chroma 64 + 16 comp
+    int16_t* bT = reinterpret_cast<int16_t*>(t.b);
+    int sse_y = 0, sse_c = 0;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+        const int bx = (k & 1) * 8, by = (k >> 1) * 8, cbx = bx >> 1, cby = by >> 1;
+        const int avl = split_tu_avl(k, al, ac, at, atr);
+        // ---- raw references: luma into S.*[0], chroma component c into S.*[1 + c] (4-sample arrays)
+        if (lane < 32) {
+            const int q = lane;
+            if (q < 16) {  // left, then below-left (TU 0 only)
+                const int v = q < 8 ? (bx == 0 ? R.lpx[by + q] : t.pred[(by + q) * 16 + bx - 1]) : (k == 0 ? R.lpx[q] : 0);
+                S.lp[0][q] = (uint8_t)v;
+            } else if (q < 24) {
+                const int c = q - 16;
+                S.tp[0][c] = by == 0 ? R.tpx[bx + c] : t.pred[7 * 16 + bx + c];
+            } else {
+                const int c = q - 24;
+                S.tr[0][c] = k == 0 ? R.tpx[8 + c] : (k == 1 ? R.trx[c] : (k == 2 ? t.pred[7 * 16 + 8 + c] : 0));
+            }
+        } else {
+            const int q = (lane - 32) & 15, c = (lane - 32) >> 4;
+            const uint8_t* up = t.pred + 256 + c * 64;
+            if (q < 8) {  // left, then below-left
+                const int v = q < 4 ? (cbx == 0 ? R.lc[c][cby + q] : up[(cby + q) * 8 + cbx - 1]) : (k == 0 ? R.lc[c][q] : 0);
+                S.lp[1 + c][q] = (uint8_t)v;
+            } else if (q < 12) {
+                const int d = q - 8;
+                S.tp[1 + c][d] = cby == 0 ? R.tc[c][cbx + d] : up[3 * 8 + cbx + d];
+            } else {
+                const int d = q - 12;
+                S.tr[1 + c][d] = k == 0 ? R.tc[c][4 + d] : (k == 1 ? R.trc[c][d] : (k == 2 ? up[3 * 8 + 4 + d] : 0));
+            }
+        }
+        if (lane < 2) {
+            const uint8_t* up = t.pred + 256 + lane * 64;
+            S.corner[1 + lane] = k == 0 ? R.corner_c[lane] : (k == 1 ? R.tc[lane][3] : (k == 2 ? R.lc[lane][3] : up[3 * 8 + 3]));
+        } else if (lane == 2) {
+            S.corner[0] = k == 0 ? R.corner : (k == 1 ? R.tpx[7] : (k == 2 ? R.lpx[7] : t.pred[7 * 16 + 7]));
+        }
+        wave_lds_sync();
+        // ---- substitution (luma 33 samples, chroma 2 x 17), luma [1 2 1] filter, DC
+        for (int i = lane; i < 33 + 34; i += 64) {
+            if (i < 33) {
+                const int v = ref_subst(i, 8, avl, S.lp[0], S.tp[0], S.tr[0], S.corner[0]);
+                if (i < 16) S.L[0][16 - i] = v;
+                else if (i == 16) S.L[0][0] = S.T[0][0] = v;
+                else S.T[0][i - 16] = v;
+            } else {
+                const int c = (i - 33) / 17, q = (i - 33) - c * 17;
+                const int v = ref_subst(q, 4, avl, S.lp[1 + c], S.tp[1 + c], S.tr[1 + c], S.corner[1 + c]);
+                if (q < 8) S.L[1 + c][8 - q] = v;
+                else if (q == 8) S.L[1 + c][0] = S.T[1 + c][0] = v;
+                else S.T[1 + c][q - 8] = v;
+            }
+        }
+        wave_lds_sync();
+        if (lane < 17) {
+            const int q = lane;
+            if (q == 0) {
+                S.LF[0][0] = S.TF[0][0] = (S.L[0][1] + 2 * S.L[0][0] + S.T[0][1] + 2) >> 2;
+            } else if (q == 16) {
+                S.LF[0][16] = S.L[0][16];
+                S.TF[0][16] = S.T[0][16];
+            } else {
+                S.LF[0][q] = (S.L[0][q + 1] + 2 * S.L[0][q] + S.L[0][q - 1] + 2) >> 2;
+                S.TF[0][q] = (S.T[0][q + 1] + 2 * S.T[0][q] + S.T[0][q - 1] + 2) >> 2;
+            }
+        }
+        {  // DC sums: lanes 0..15 luma, 16..23 Cb, 24..31 Cr
+            const int v = lane < 16 ? (lane < 8 ? S.L[0][1 + lane] : S.T[0][1 + lane - 8])
+                                    : (lane < 32 ? ((lane & 7) < 4 ? S.L[1 + ((lane >> 3) & 1)][1 + (lane & 3)]
+                                                                   : S.T[1 + ((lane >> 3) & 1)][1 + (lane & 3)])
+                                                 : 0);
+            const int g8 = gsum<8>(v);
+            const int g16 = gsum<16>(v);
+            if (lane == 0) S.dc[0] = (g16 + 8) >> 4;
+            if (lane == 16) S.dc[1] = (g8 + 4) >> 3;
+            if (lane == 24) S.dc[2] = (g8 + 4) >> 3;
+        }
+        wave_lds_sync();
+        // ---- prediction and residual
+        const int pl = pred_sample(mode, 3, true, S.L[0], S.T[0], S.LF[0], S.TF[0], S.dc[0], lx, ly);
+        const int ol = (by + ly) * 16 + bx + lx;
+        t.res[lane] = (int16_t)((int)src[ol] - pl);
+        int pc = 0, oc = 0;
+        if (cl) {
+            pc = pred_sample(mode, 2, false, S.L[1 + comp], S.T[1 + comp], S.L[1 + comp], S.T[1 + comp], S.dc[1 + comp],
+                             cx, cy);
+            oc = 256 + comp * 64 + (cby + cy) * 8 + cbx + cx;
+            t.res[64 + comp * 16 + cy * 4 + cx] = (int16_t)((int)src[oc] - pc);
+        }
+        wave_lds_sync();
+        // ---- forward stage 1 (rows): aT[k][y]
+        aT[lx * 8 + ly] = (int16_t)((dot8(M.t8 + lx * 8, t.res + ly * 8) + 2) >> 2);
+        if (cl) aT[64 + comp * 16 + cx * 4 + cy] = (int16_t)((dot4(M.t4 + cx * 4, t.res + 64 + comp * 16 + cy * 4) + 1) >> 1);
+        wave_lds_sync();
+        // ---- forward stage 2 (columns) + quantisation: lane (k2 = ly, k = lx)
+        {
+            const int l = quant_coef((dot8(M.t8 + ly * 8, aT + lx * 8) + 256) >> 9, qp, 3, true);
+            const int si = scan_index_s(3, scan, lx, ly);
+            coef[64 * k + si] = (int16_t)l;
+            lv[64 * k + si] = (int16_t)l;
+            bT[lx * 8 + ly] = (int16_t)dequant_coef(l, qp, 3);
+        }
+        if (cl) {
+            const int l = quant_coef((dot4(M.t4 + cy * 4, aT + 64 + comp * 16 + cx * 4) + 128) >> 8, qpc, 2, true);
+            const int si = 256 + 64 * comp + 16 * k + scan_index_s(2, scan, cx, cy);
+            coef[si] = (int16_t)l;
+            lv[si] = (int16_t)l;
+            bT[64 + comp * 16 + cx * 4 + cy] = (int16_t)dequant_coef(l, qpc, 2);
+        }
+        wave_lds_sync();
+        // ---- inverse stage 1 (columns): a16[y][x]
+        aT[ly * 8 + lx] = (int16_t)clip16((dot8(M.tt8 + ly * 8, bT + lx * 8) + 64) >> 7);
+        if (cl) aT[64 + comp * 16 + cy * 4 + cx] = (int16_t)clip16((dot4(M.tt4 + cy * 4, bT + 64 + comp * 16 + cx * 4) + 64) >> 7);
+        wave_lds_sync();
+        // ---- inverse stage 2 (rows) + reconstruction
+        {
+            const int v = clip255(pl + ((dot8(M.tt8 + lx * 8, aT + ly * 8) + 2048) >> 12));
+            const int e = (int)src[ol] - v;
+            sse_y += (x0 + bx + lx < disp_w && y0 + by + ly < disp_h) ? e * e : 0;
+            t.pred[ol] = (uint8_t)v;
+            rec_y[(size_t)(y0 + by + ly) * pitch + x0 + bx + lx] = (uint8_t)v;
+        }
+        if (cl) {
+            const int v = clip255(pc + ((dot4(M.tt4 + cx * 4, aT + 64 + comp * 16 + cy * 4) + 2048) >> 12));
+            const int e = (int)src[oc] - v;
+            const int xc = x0 / 2 + cbx + cx, yc = y0 / 2 + cby + cy;
+            sse_c += (2 * xc < disp_w && 2 * yc < disp_h) ? e * e : 0;
+            t.pred[oc] = (uint8_t)v;
+            rec_uv[(size_t)yc * pitch + 2 * xc + comp] = (uint8_t)v;
+        }
+        wave_lds_sync();
+    }
+    SplitIntraResult out;
+    out.sse[0] = wsum(sse_y);
+    out.sse[1] = wsum(comp == 0 && cl ? sse_c : 0);
+    out.sse[2] = wsum(comp == 1 && cl ? sse_c : 0);
+    // cu_bits_est (split, no 4x4 luma): per TU 4 + 2 floor(log2 |l|) per level, + 4 if coded, else 1
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int l = lv[64 * j + lane], a = l < 0 ? -l : l;
+        const int b = a ? 4 + 2 * (31 - __builtin_clz((uint32_t)a)) : 0;
+        if (j < 4) {
+            const int sum = wsum(b);
+            bits += (uint32_t)(__ballot(a != 0) ? sum + 4 : 1);
+        } else {  // four 4x4 chroma TUs of 16 levels
+            const int sum = gsum<16>(b);
+            const uint64_t any = __ballot(a != 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                bits += (uint32_t)(((any >> (16 * q)) & 0xffffu) ? __builtin_amdgcn_readlane(sum, 16 * q) + 4 : 1);
+        }
+    }
+    out.bits = bits;
+    return out;
 }
 
 __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, const HevcFrameState* __restrict__ fs,
@@ -1211,6 +1469,8 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     __shared__ TuBuf tb[kMaxSliceRows];
     __shared__ IntraRefs rf[kMaxSliceRows];
     __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
+    __shared__ SplitRefs srf[kMaxSliceRows];          // split units: TU references (split_intra_code)
+    __shared__ alignas(16) uint8_t srcs[kMaxSliceRows][384];  // split units: the unit's source (t.pred layout)
     fill_mats(M);
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1319,10 +1579,15 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
             }
         }
         __syncthreads();
-        // ---- the mode decided open-loop by k_hevc_intra_modes
+        // ---- the mode (and the split) decided open-loop by k_hevc_intra_modes
         int mode = 1;
+        bool split = false;
         if (valid && main_w) {
-            mode = (int)imode[y * g.mb_w + x];  // (wave-uniform)
+            const int im = (int)imode[y * g.mb_w + x];  // (wave-uniform)
+            mode = im & (kIntraSplitFlag - 1);
+            split = (im & kIntraSplitFlag) != 0;
+        }
+        if (valid && main_w && !split) {
             const int r = lane >> 2, cb = (lane & 3) * 4;
             for (int j = 0; j < 4; ++j) {
                 const int p = pred_sample(mode, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
@@ -1339,9 +1604,40 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         }
         __syncthreads();
         const int i = valid ? y * g.mb_w + x : 0;
-        const TuResult res = code_tus<false>(t, M, qp, qpc, true, valid && main_w, coef + (size_t)i * kCoefPerCu,
-                                             fs->rec_y, g.pitch, fs->rec_uv, x0, y0, g.width, g.height);
-        if (valid && main_w) {
+        const TuResult res = code_tus<false>(t, M, qp, qpc, true, valid && main_w && !split,
+                                             coef + (size_t)i * kCoefPerCu, fs->rec_y, g.pitch, fs->rec_uv, x0, y0,
+                                             g.width, g.height);
+        if (valid && main_w && split) {
+            // four 8x8 TUs, wave-local (the other waves wait at the step's next barrier)
+            uint8_t* sb = srcs[wave];
+            {
+                const int r = lane >> 2, cb = (lane & 3) * 4, rc = lane >> 3, cc = lane & 7;
+                *reinterpret_cast<uint32_t*>(sb + r * 16 + cb) = sy4;
+                sb[256 + rc * 8 + cc] = (uint8_t)(sc2 & 0xff);
+                sb[256 + 64 + rc * 8 + cc] = (uint8_t)(sc2 >> 8);
+            }
+            wave_lds_sync();
+            int16_t* lvs = reinterpret_cast<int16_t*>(t.b) + 384;
+            const SplitIntraResult sres =
+                split_intra_code(t, srf[wave], R, M, sb, lvs, mode, qp, qpc, al, ac, at, atr, coef + (size_t)i * kCoefPerCu,
+                                 fs->rec_y, fs->rec_uv, g.pitch, x0, y0, g.width, g.height);
+            acc[0] += (unsigned)sres.sse[0];
+            acc[1] += (unsigned)sres.sse[1];
+            acc[2] += (unsigned)sres.sse[2];
+            const SplitSummary ss = split_summary_wave(lvs, lane, 0);
+            if (lane == 0) {
+                CuInfo c{};
+                c.type = kCuIntra;
+                c.intra_mode = (uint8_t)mode;
+                c.qp = (uint8_t)qp;
+                c.tu_split = 2;
+                ss.apply(c);
+                c.ct = 1;
+                set_est_bytes(c, sres.bits);
+                cus[i] = c;
+                qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
+            }
+        } else if (valid && main_w) {
             acc[0] += (unsigned)res.sse[0];
             acc[1] += (unsigned)res.sse[1];
             acc[2] += (unsigned)res.sse[2];
@@ -1610,7 +1906,7 @@ __global__ __launch_bounds__(64) void k_hevc_bins(Geometry g, const HevcFrameSta
     const int first = uni(slice_first[s]);
     const int end = s + 1 < ns ? uni(slice_first[s + 1]) : nctb;
     const UnitSyn u = unit_syn(CuGet{cus}, fs->sao ? sao : nullptr, x, y, g.mb_w, g.mb_h, fs->idr != 0, first, end,
-                               fs->wpp != 0, fs->depth_inter, (int)uni((uint32_t)qp_pred[i]));
+                               fs->wpp != 0, fs->depth_inter, fs->depth_intra, (int)uni((uint32_t)qp_pred[i]));
     const CuInfo cu = load_cu(cus, i);
     const CoefArray cf{coef + (size_t)i * kCoefPerCu};
     // lane p binarises part p of the unit (coding order) into its LDS run

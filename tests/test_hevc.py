@@ -348,6 +348,38 @@ def test_cpu_hevc_tu_split_decodes_to_reconstruction(native, w, h, qp):
     assert dec.stats.get("tu_split", 0) > 0
 
 
+@pytest.mark.parametrize("qp", [22, 30, 38])
+def test_cpu_hevc_intra_split_decodes_to_reconstruction(native, qp):
+    """Intra units coded as four 8x8 luma / 4x4 chroma TUs, each predicted from the TUs before it,
+    with the mode-dependent (horizontal / vertical) scans: the independent decoder reproduces the
+    reconstruction exactly (IDR pictures, inter frames after them), sees split intra trees with
+    every scanIdx, and with hevc_intra_split = 0 none."""
+    from mxdesk.codec import hevc_decoder
+
+    seen = set()
+    orig = hevc_decoder.Decoder._residual
+
+    def spy(self, cab, log2, cidx, intra_mode):
+        if intra_mode is not None and (log2 == 2 or (log2 == 3 and cidx == 0)):
+            seen.add(2 if 6 <= intra_mode <= 14 else (1 if 22 <= intra_mode <= 30 else 0))
+        return orig(self, cab, log2, cidx, intra_mode)
+
+    hevc_decoder.Decoder._residual = spy
+    try:
+        out, src, sizes, dec, _ = _cpu_roundtrip(native, 320, 192, 3, qp=qp, fresh=True, idr_at=(2,))
+    finally:
+        hevc_decoder.Decoder._residual = orig
+    assert dec.stats.get("tu_split", 0) > 0
+    assert seen == {0, 1, 2}
+    cfg = _cfg(native, 320, 192, qp=qp)
+    cfg.hevc_intra_split = 0
+    enc = native.CpuHevcEncoder(cfg)
+    y, uv = synthetic_nv12(320, 192, 0, seed=0)
+    dec0 = Decoder()
+    dec0.decode(enc.encode(y, uv, True))
+    assert dec0.stats.get("tu_split", 0) == 0
+
+
 @pytest.mark.parametrize("w,h,qp", [(64, 48, 26), (160, 96, 30), (320, 192, 34)])
 def test_cpu_hevc_4x4_luma_tus_decode_to_reconstruction(native, w, h, qp):
     """tu_split 2: 8x8 luma nodes of split inter trees may code four 4x4 TUs (split_transform_flag
