@@ -2009,12 +2009,12 @@ MXHD int split_tu_avl(int k, bool al, bool ac, bool at, bool atr) {
 }
 // modes whose 8x8 luma and 4x4 DM chroma predictions never read the below-left references
 inline uint64_t bl_safe_split() { return bl_safe_modes(3, 0) & bl_safe_modes(2, 1); }
-// Open-loop choice (from the source, luma only, the mode decided for the unsplit unit): split when
-// the four TUs' 4x4 Hadamard SATD plus lambda * kIntraSplitBits (the split tree's extra cbf flags)
-// is below the unsplit prediction's.  The imode byte carries it in bit 6.
+// Open-loop choice (from the source, luma only): split when the best split mode's cost (four TUs'
+// 4x4 Hadamard SATD + lambda * mode bits) plus lambda * kIntraSplitBits (the split tree's extra cbf
+// flags) is below the best unsplit mode's.  The imode byte carries it in bit 6.
 constexpr int kIntraSplitBits = 6;
 constexpr int kIntraSplitFlag = 64;
-MXHD bool intra_split_wins(int satd16, int satd8, int lambda) { return satd8 + lambda * kIntraSplitBits < satd16; }
+MXHD bool intra_split_wins(int cost16, int cost8, int lambda) { return cost8 + lambda * kIntraSplitBits < cost16; }
 
 constexpr int kIntraCoarse[11] = {0, 1, 2, 6, 10, 14, 18, 22, 26, 30, 34};
 constexpr int kIntraNoMode = 0x7fffffff;

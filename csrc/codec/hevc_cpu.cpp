@@ -454,9 +454,9 @@ void block_refs(const uint8_t* p, int pitch, int step, int x, int y, int N, int 
 // uses the modes in `safe` -- bl_safe_modes -- because the raster wavefront reconstructs it before
 // its below-left), scored by the 4x4 Hadamard SATD of the residual + lambda * mode bits, searched
 // coarse-to-fine (intra_mode_search: at most 15 of the 35 modes); the lowest cost wins, ties to the
-// lower mode.  With split, the chosen mode is also predicted as four 8x8 TUs from the source
-// (split_tu_avl; a CTB's first unit only in a safe_split mode) and kIntraSplitFlag is set when
-// intra_split_wins.
+// lower mode.  With split, the modes are searched again (same order) for the unit predicted as four
+// 8x8 TUs from the source (split_tu_avl; a CTB's first unit only in safe_split modes), and that mode
+// with kIntraSplitFlag wins when intra_split_wins over the unsplit cost (mode bits included).
 int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, int y, int sr, int seg_w, int qp,
                       uint64_t safe, uint64_t safe_split, bool split) {
     const int x0 = x * 16, y0 = y * 16, z = ((y & 1) << 1) | (x & 1);
@@ -480,18 +480,23 @@ int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, i
         return satd16(sy, pitch, x0, y0, pred) + lambda * intra_mode_bits(m, 1, 1);
     };
     const int best = intra_mode_search(cost);
-    if (!split || (bl_pending && !((safe_split >> best) & 1))) return best;
-    intra_predict(best, 4, 0, L, T, pred);
-    const int s16 = satd16(sy, pitch, x0, y0, pred);
-    for (int k = 0; k < 4; ++k) {
-        const int bx = (k & 1) * 8, by = (k >> 1) * 8;
-        int Lk[17], Tk[17], p8[64];
-        block_refs(sy, pitch, 1, x0 + bx, y0 + by, 8, split_tu_avl(k, al, ac, at, atr), Lk, Tk);
-        intra_predict(best, 3, 0, Lk, Tk, p8);
-        for (int r = 0; r < 8; ++r)
-            for (int q = 0; q < 8; ++q) pred[(by + r) * 16 + bx + q] = p8[r * 8 + q];
-    }
-    return intra_split_wins(s16, satd16(sy, pitch, x0, y0, pred), lambda) ? best | kIntraSplitFlag : best;
+    if (!split) return best;
+    int Lk[4][17], Tk[4][17];
+    for (int k = 0; k < 4; ++k)
+        block_refs(sy, pitch, 1, x0 + (k & 1) * 8, y0 + (k >> 1) * 8, 8, split_tu_avl(k, al, ac, at, atr), Lk[k], Tk[k]);
+    auto cost_split = [&](int m) {
+        if (bl_pending && !((safe_split >> m) & 1)) return kIntraNoMode;
+        for (int k = 0; k < 4; ++k) {
+            const int bx = (k & 1) * 8, by = (k >> 1) * 8;
+            int p8[64];
+            intra_predict(m, 3, 0, Lk[k], Tk[k], p8);
+            for (int r = 0; r < 8; ++r)
+                for (int q = 0; q < 8; ++q) pred[(by + r) * 16 + bx + q] = p8[r * 8 + q];
+        }
+        return satd16(sy, pitch, x0, y0, pred) + lambda * intra_mode_bits(m, 1, 1);
+    };
+    const int best_s = intra_mode_search(cost_split);
+    return intra_split_wins(cost(best), cost_split(best_s), lambda) ? best_s | kIntraSplitFlag : best;
 }
 
 void CpuHevcEncoder::analyse_intra(const uint8_t* sy, const uint8_t* suv, int pitch) {

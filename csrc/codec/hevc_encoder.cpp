@@ -240,8 +240,13 @@ int GpuHevcEncoder::probe_bytes(const uint8_t* src_y, const uint8_t* src_uv, int
     HIP_CHECK(hipStreamSynchronize(stream_));
     HIP_CHECK(hipStreamSynchronize(es(0)));
     const HevcOutHeader hdr = *reinterpret_cast<const HevcOutHeader*>(sl.host_out);
-    // (header records are substreams; the per-NAL allowance counts slices, as the CPU encoder's probe)
-    return hdr.overflow ? (int)sl.buf.out_bytes : (int)(hdr.total_bytes + common_.num_slices() * 12 + 64);
+    if (hdr.overflow) return (int)sl.buf.out_bytes;
+    // the exact substream lengths (total_bytes counts the 16-byte aligned payload slots), plus the
+    // per-NAL allowance per slice, as the CPU encoder's probe: the two must pick the same QP
+    const uint32_t* len = reinterpret_cast<const uint32_t*>(sl.host_out + sizeof(HevcOutHeader)) + kMaxSlices;
+    size_t total = 0;
+    for (uint32_t k = 0; k < hdr.num_slices && k < (uint32_t)kMaxSlices; ++k) total += len[k];
+    return (int)(total + common_.num_slices() * 12 + 64);
 }
 
 bool GpuHevcEncoder::prepare(bool force_idr) {

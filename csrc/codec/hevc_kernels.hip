@@ -1147,8 +1147,8 @@ __device__ __forceinline__ void split_refs_finish(SplitRefs& S, bool al, bool ac
 // below-left; a CTB's first unit keeps to bl_safe_modes, as k_hevc_intra reconstructs it before
 // its below-left), scored by 4x4 Hadamard SATD + lambda * mode bits, searched coarse-to-fine
 // (intra_mode_search: at most 15 of the 35 modes) -- hevc_cpu.cpp
-// intra_decide_mode.  With intra splits on, the chosen mode is also predicted as four 8x8 TUs from
-// the source (split_tu_avl) and kIntraSplitFlag set when intra_split_wins.  The IDR wavefront
+// intra_decide_mode.  With intra splits on, the modes are searched again for four 8x8 TUs predicted
+// from the source (split_tu_avl), and kIntraSplitFlag is set with that mode when intra_split_wins.  The IDR wavefront
 // (k_hevc_intra) then only reconstructs.
 __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const HevcFrameState* __restrict__ fs,
                                                            const uint8_t* __restrict__ src_y,
@@ -1238,7 +1238,7 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
     };
     const int best = intra_mode_search(cost);  // coarse-to-fine: at most 15 of the 35 modes
     int out = best;
-    if (fs->depth_intra > 0 && (!bl_pending || ((fs->bl_safe_split >> best) & 1))) {  // wave-uniform
+    if (fs->depth_intra > 0) {  // the split tree: its own mode search over the four TUs' predictions
         SplitRefs& S = srf[wave];
         for (int i = lane; i < 4 * 33; i += 64) {  // raw references of the four TUs, from the source
             const int k = i / 33, q = i - k * 33;
@@ -1257,20 +1257,25 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
         wave_lds_sync();
         split_refs_finish(S, al, ac, at, atr, lane);
         const int kq = ((r >> 3) << 1) | (cb >> 3);  // the lane's four samples lie in one TU
-        mf_h4 a;
+        const uint64_t safe_s = fs->bl_safe_split;
+        auto cost_split = [&](int m) {
+            if (bl_pending && !((safe_s >> m) & 1)) return kIntraNoMode;  // wave-uniform
+            mf_h4 a;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            a[j] = (_Float16)((int)((sw >> (8 * j)) & 0xff) -
-                              pred_sample(best, 3, true, S.L[kq], S.T[kq], S.LF[kq], S.TF[kq], S.dc[kq], (cb + j) & 7, r & 7));
-        const mf_f4 t = __builtin_amdgcn_mfma_f32_16x16x16f16(a, hm, zero, 0, 0, 0);
-        mf_h4 tb;
+            for (int j = 0; j < 4; ++j)
+                a[j] = (_Float16)((int)((sw >> (8 * j)) & 0xff) - pred_sample(m, 3, true, S.L[kq], S.T[kq], S.LF[kq],
+                                                                               S.TF[kq], S.dc[kq], (cb + j) & 7, r & 7));
+            const mf_f4 t = __builtin_amdgcn_mfma_f32_16x16x16f16(a, hm, zero, 0, 0, 0);
+            mf_h4 tb;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tb[i] = (_Float16)t[i];
-        const mf_f4 sm = __builtin_amdgcn_mfma_f32_16x16x16f16(hm, tb, zero, 0, 0, 0);
-        const int s8 = wsum((int)(__builtin_fabsf(sm[0]) + __builtin_fabsf(sm[1]) + __builtin_fabsf(sm[2]) +
-                                  __builtin_fabsf(sm[3])));
-        const int s16 = cost(best) - lambda * intra_mode_bits(best, 1, 1);
-        if (intra_split_wins(s16, s8, lambda)) out |= kIntraSplitFlag;
+            for (int i = 0; i < 4; ++i) tb[i] = (_Float16)t[i];
+            const mf_f4 sm = __builtin_amdgcn_mfma_f32_16x16x16f16(hm, tb, zero, 0, 0, 0);
+            const int sad = (int)(__builtin_fabsf(sm[0]) + __builtin_fabsf(sm[1]) + __builtin_fabsf(sm[2]) +
+                                  __builtin_fabsf(sm[3]));
+            return wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
+        };
+        const int best_s = intra_mode_search(cost_split);
+        if (intra_split_wins(cost(best), cost_split(best_s), lambda)) out = best_s | kIntraSplitFlag;
     }
     if (lane == 0) imode[y * g.mb_w + x] = (uint8_t)out;
 }

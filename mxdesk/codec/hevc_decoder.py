@@ -147,6 +147,10 @@ def _transform_matrix() -> np.ndarray:
 _T32 = _transform_matrix()
 
 
+# 4x4 DST-VII (8.6.4.2, trType 1: intra 4x4 luma), rows = basis functions
+_DST4 = np.array([[29, 55, 74, 84], [74, 74, 0, -74], [84, -29, -74, 55], [55, -84, 74, -29]], np.int64)
+
+
 def _tmat(n: int) -> np.ndarray:
     return _T32[:: 32 // n, :n]
 
@@ -1290,8 +1294,6 @@ class Decoder:
             self.qp_y = ((self.qp_pred + a + 52) % 52)
         mode, mode_c = self.cu_intra_modes
         n = 1 << log2
-        if intra and log2 == 2:
-            raise NotImplementedError("4x4 intra luma (DST)")
         # luma
         res = self._residual(cab, log2, 0, mode if intra else None) if cbf_luma else None
         tb4 = (slice(y0 >> 2, (y0 + n) >> 2), slice(x0 >> 2, (x0 + n) >> 2))
@@ -1300,7 +1302,7 @@ class Decoder:
         self.edge_h[y0 >> 2, tb4[1]] = True
         if intra:
             self._intra_predict(x0, y0, log2, 0, mode)
-        self._add_residual(self.cur.y, x0, y0, n, res, self.qp_y, log2)
+        self._add_residual(self.cur.y, x0, y0, n, res, self.qp_y, log2, dst=intra and log2 == 2)
         b4 = (slice(y0 >> 2, (y0 + n) >> 2), slice(x0 >> 2, (x0 + n) >> 2))
         self.slice_map[b4] = self.slice_addr
         # chroma (4:2:0)
@@ -1320,13 +1322,15 @@ class Decoder:
             qpc = qpi if qpi < 30 else (qpi - 6 if qpi > 43 else _QPC_TABLE[qpi])
             self._add_residual(plane, xc, yc, 1 << lc, r, qpc, lc)
 
-    def _add_residual(self, plane, x0, y0, n, levels, qp, log2):
+    def _add_residual(self, plane, x0, y0, n, levels, qp, log2, dst=False):
+        """Scaling (8.6.2/8.6.3) and the inverse transform (8.6.4.2): the DCT-like core transform,
+        or for a 4x4 intra luma TU the DST-VII matrix (8.6.4.2 trType 1)."""
         if levels is None:
             return
         d = (levels.astype(np.int64) * 16 * _LEVEL_SCALE[qp % 6]) << (qp // 6)
         bd = 8 + log2 - 5
         d = np.clip((d + (1 << (bd - 1))) >> bd, -32768, 32767)
-        t = _tmat(n)
+        t = _DST4 if dst else _tmat(n)
         # d is indexed [y][x] (row = vertical frequency); columns first, then rows
         e = t.T @ d
         g = np.clip((e + 64) >> 7, -32768, 32767)

@@ -30,7 +30,7 @@ def test_gpu_partitions_bit_exact(gpu, vertical, coarse, subpel):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
-        assert gau == cau, f"frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
+        assert bool(gau == cau), f"frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
         stream += gau
         grec.append(genc.recon())
         nparts += int((cenc.mb_info()[..., 8] > 0).sum())

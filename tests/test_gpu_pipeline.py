@@ -165,7 +165,7 @@ def _gpu_cpu_encode(gpu, w, h, frames, **kw):
         gs += gau
         cs += cau
         grec.append(genc.recon())
-        assert gau == cau, f"frame {t}: GPU bitstream differs from CPU encoder ({len(gau)} vs {len(cau)} bytes)"
+        assert bool(gau == cau), f"frame {t}: GPU bitstream differs from CPU encoder ({len(gau)} vs {len(cau)} bytes)"
     return gs, grec
 
 
@@ -191,7 +191,7 @@ def test_gpu_temporal_classes_desktop_bit_exact_vs_cpu(gpu, w, h, aq):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
-        assert gau == cau, f"aq {aq} frame {t}: GPU bitstream differs from CPU encoder ({len(gau)} vs {len(cau)} bytes)"
+        assert bool(gau == cau), f"aq {aq} frame {t}: GPU bitstream differs from CPU encoder ({len(gau)} vs {len(cau)} bytes)"
         gs += gau
         grec.append(genc.recon())
     dec = Decoder()
@@ -623,7 +623,7 @@ def test_gpu_adaptive_deblock_bit_exact_vs_cpu(gpu, depth):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), idr)
         cau = cenc.encode(y, uv, idr)
-        assert gau == cau, f"frame {t}: GPU bitstream differs from CPU encoder"
+        assert bool(gau == cau), f"frame {t}: GPU bitstream differs from CPU encoder"
         gst, cst = genc.stats, cenc.stats
         assert (gst.deblocked, gst.db_coherent, gst.db_changed, gst.db_moving) == \
             (cst.deblocked, cst.db_coherent, cst.db_changed, cst.db_moving), t
@@ -690,7 +690,7 @@ def test_gpu_deblock_strong_filtering_bit_exact_vs_cpu(gpu, w, h, qp):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
-        assert gau == cau, f"frame {t}"
+        assert bool(gau == cau), f"frame {t}"
         assert np.array_equal(genc.recon()[0], cenc.recon()[0]) and np.array_equal(genc.recon()[1], cenc.recon()[1])
         stream += gau
         grec.append(genc.recon())

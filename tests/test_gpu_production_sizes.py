@@ -64,7 +64,7 @@ def _encode_both(gpu, w, h, frames, kbps, search_range=16, deblock=1):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
-        assert gau == cau, f"{w}x{h} frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
+        assert bool(gau == cau), f"{w}x{h} frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
         aus.append(gau)
         recons.append(genc.recon())
     return aus, recons, genc
@@ -114,7 +114,7 @@ def _hevc_encode_both(gpu, w, h, frames, kbps):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
-        assert gau == cau, f"HEVC {w}x{h} frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
+        assert bool(gau == cau), f"HEVC {w}x{h} frame {t}: GPU {len(gau)} B vs CPU {len(cau)} B"
         assert tuple(genc.stats.sse) == tuple(cenc.stats.sse), t
         aus.append(gau)
     return aus, genc

@@ -221,7 +221,7 @@ def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, 
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
         cau = cenc.encode(y, uv, False)
-        assert gau == cau, f"frame {t}: GPU HEVC bitstream differs from the CPU encoder ({len(gau)} vs {len(cau)})"
+        assert bool(gau == cau), f"frame {t}: GPU HEVC bitstream differs from the CPU encoder ({len(gau)} vs {len(cau)})"
         gs += gau
         grec.append(genc.recon())
         cs = cenc.stats
@@ -569,7 +569,7 @@ def test_gpu_hevc_adaptive_deblocking_bit_exact_vs_cpu(gpu, sao):
         torch.cuda.synchronize()
         gau = genc.encode(dy.data_ptr(), duv.data_ptr(), idr)
         cau = cenc.encode(y, uv, idr)
-        assert gau == cau, f"frame {t}: GPU HEVC bitstream differs from the CPU encoder"
+        assert bool(gau == cau), f"frame {t}: GPU HEVC bitstream differs from the CPU encoder"
         assert genc.stats.deblocked == cenc.stats.deblocked, t
         flags.append(genc.stats.deblocked)
     assert flags[1:5] == [1, 1, 1, 1], flags  # (the still stretch's decisions depend on the SAO setting)
