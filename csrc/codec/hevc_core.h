@@ -2012,7 +2012,7 @@ inline uint64_t bl_safe_split() { return bl_safe_modes(3, 0) & bl_safe_modes(2, 
 // Open-loop choice (from the source, luma only): split when the best split mode's cost (four TUs'
 // 4x4 Hadamard SATD + lambda * mode bits) plus lambda * kIntraSplitBits (the split tree's extra cbf
 // flags) is below the best unsplit mode's.  The imode byte carries it in bit 6.
-constexpr int kIntraSplitBits = 6;
+constexpr int kIntraSplitBits = 10;
 constexpr int kIntraSplitFlag = 64;
 MXHD bool intra_split_wins(int cost16, int cost8, int lambda) { return cost8 + lambda * kIntraSplitBits < cost16; }
 

@@ -1102,6 +1102,22 @@ __device__ __forceinline__ int ref_subst(int i, int N, int avl, const uint8_t* l
     return trx[j - 3 * N - 1];
 }
 
+// ref_subst's source index: the search-order position whose sample reference i takes (-1: none
+// available, the value 128)
+__device__ __forceinline__ int ref_subst_idx(int i, int N, int avl) {
+    if (avl == 0) return -1;
+    const int n2 = 2 * N;
+    const int seg = i < N ? 0 : (i < n2 ? 1 : (i == n2 ? 2 : (i <= 3 * N ? 3 : 4)));
+    if ((avl >> seg) & 1) return i;
+    const int below = avl & ((1 << seg) - 1);
+    if (below) {
+        const int p = 31 - __clz(below);
+        return p == 0 ? N - 1 : (p == 1 ? n2 - 1 : (p == 2 ? n2 : (p == 3 ? 3 * N : 4 * N)));
+    }
+    const int f = __ffs(avl) - 1;
+    return f == 0 ? 0 : (f == 1 ? N : (f == 2 ? n2 : (f == 3 ? n2 + 1 : 3 * N + 1)));
+}
+
 // References of the four 8x8 TUs of a split intra unit (hevc_core.h split_tu_avl): raw samples (left
 // then below-left, top, top-right, corner), substituted L / T, the [1 2 1]-filtered LF / TF, DC.
 struct SplitRefs {
@@ -1308,88 +1324,88 @@ __device__ SplitIntraResult split_intra_code(TuBuf& t, SplitRefs& S, const Intra
     for (int k = 0; k < 4; ++k) {
         const int bx = (k & 1) * 8, by = (k >> 1) * 8, cbx = bx >> 1, cby = by >> 1;
         const int avl = split_tu_avl(k, al, ac, at, atr);
-        // ---- raw references: luma into S.*[0], chroma component c into S.*[1 + c] (4-sample arrays)
-        if (lane < 32) {
-            const int q = lane;
-            if (q < 16) {  // left, then below-left (TU 0 only)
-                const int v = q < 8 ? (bx == 0 ? R.lpx[by + q] : t.pred[(by + q) * 16 + bx - 1]) : (k == 0 ? R.lpx[q] : 0);
-                S.lp[0][q] = (uint8_t)v;
-            } else if (q < 24) {
-                const int c = q - 16;
-                S.tp[0][c] = by == 0 ? R.tpx[bx + c] : t.pred[7 * 16 + bx + c];
-            } else {
-                const int c = q - 24;
-                S.tr[0][c] = k == 0 ? R.tpx[8 + c] : (k == 1 ? R.trx[c] : (k == 2 ? t.pred[7 * 16 + 8 + c] : 0));
-            }
-        } else {
-            const int q = (lane - 32) & 15, c = (lane - 32) >> 4;
-            const uint8_t* up = t.pred + 256 + c * 64;
-            if (q < 8) {  // left, then below-left
-                const int v = q < 4 ? (cbx == 0 ? R.lc[c][cby + q] : up[(cby + q) * 8 + cbx - 1]) : (k == 0 ? R.lc[c][q] : 0);
-                S.lp[1 + c][q] = (uint8_t)v;
-            } else if (q < 12) {
-                const int d = q - 8;
-                S.tp[1 + c][d] = cby == 0 ? R.tc[c][cbx + d] : up[3 * 8 + cbx + d];
-            } else {
-                const int d = q - 12;
-                S.tr[1 + c][d] = k == 0 ? R.tc[c][4 + d] : (k == 1 ? R.trc[c][d] : (k == 2 ? up[3 * 8 + 4 + d] : 0));
-            }
-        }
-        if (lane < 2) {
-            const uint8_t* up = t.pred + 256 + lane * 64;
-            S.corner[1 + lane] = k == 0 ? R.corner_c[lane] : (k == 1 ? R.tc[lane][3] : (k == 2 ? R.lc[lane][3] : up[3 * 8 + 3]));
-        } else if (lane == 2) {
-            S.corner[0] = k == 0 ? R.corner : (k == 1 ? R.tpx[7] : (k == 2 ? R.lpx[7] : t.pred[7 * 16 + 7]));
-        }
-        wave_lds_sync();
-        // ---- substitution (luma 33 samples, chroma 2 x 17), luma [1 2 1] filter, DC
-        for (int i = lane; i < 33 + 34; i += 64) {
+        // ---- references in one pass: lane i < 33 takes luma reference i (ref_subst's search order:
+        // below-left bottom-up, left, corner, top, top-right), i >= 33 chroma; each lane fetches its
+        // substituted sample straight from the neighbours / the unit's reconstruction, the luma [1 2 1]
+        // filter takes the neighbours in search order by lane shuffles (the ends stay unfiltered; at
+        // the corner the filter is the same three-tap form), the DC sums are wave sums
+        int dcl = 0, dcc0 = 0, dcc1 = 0;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            const int i = lane + 64 * pass;
+            int v = 0;
             if (i < 33) {
-                const int v = ref_subst(i, 8, avl, S.lp[0], S.tp[0], S.tr[0], S.corner[0]);
-                if (i < 16) S.L[0][16 - i] = v;
-                else if (i == 16) S.L[0][0] = S.T[0][0] = v;
-                else S.T[0][i - 16] = v;
-            } else {
+                const int j = ref_subst_idx(i, 8, avl);
+                if (j < 0) {
+                    v = 128;
+                } else if (j < 16) {  // left (q < 8) / below-left (TU 0 only) sample q
+                    const int q = 15 - j;
+                    v = q < 8 ? (bx == 0 ? R.lpx[by + q] : t.pred[(by + q) * 16 + bx - 1]) : R.lpx[q];
+                } else if (j == 16) {
+                    v = k == 0 ? R.corner : (k == 1 ? R.tpx[7] : (k == 2 ? R.lpx[7] : t.pred[7 * 16 + 7]));
+                } else if (j <= 24) {
+                    const int c = j - 17;
+                    v = by == 0 ? R.tpx[bx + c] : t.pred[7 * 16 + bx + c];
+                } else {
+                    const int c = j - 25;
+                    v = k == 0 ? R.tpx[8 + c] : (k == 1 ? R.trx[c] : t.pred[7 * 16 + 8 + c]);
+                }
+            } else if (i < 33 + 34) {
                 const int c = (i - 33) / 17, q = (i - 33) - c * 17;
-                const int v = ref_subst(q, 4, avl, S.lp[1 + c], S.tp[1 + c], S.tr[1 + c], S.corner[1 + c]);
+                const int j = ref_subst_idx(q, 4, avl);
+                const uint8_t* up = t.pred + 256 + c * 64;
+                if (j < 0) {
+                    v = 128;
+                } else if (j < 8) {
+                    const int r = 7 - j;
+                    v = r < 4 ? (cbx == 0 ? R.lc[c][cby + r] : up[(cby + r) * 8 + cbx - 1]) : R.lc[c][r];
+                } else if (j == 8) {
+                    v = k == 0 ? R.corner_c[c] : (k == 1 ? R.tc[c][3] : (k == 2 ? R.lc[c][3] : up[3 * 8 + 3]));
+                } else if (j <= 12) {
+                    const int d = j - 9;
+                    v = cby == 0 ? R.tc[c][cbx + d] : up[3 * 8 + cbx + d];
+                } else {
+                    const int d = j - 13;
+                    v = k == 0 ? R.tc[c][4 + d] : (k == 1 ? R.trc[c][d] : up[3 * 8 + 4 + d]);
+                }
                 if (q < 8) S.L[1 + c][8 - q] = v;
                 else if (q == 8) S.L[1 + c][0] = S.T[1 + c][0] = v;
                 else S.T[1 + c][q - 8] = v;
             }
-        }
-        wave_lds_sync();
-        if (lane < 17) {
-            const int q = lane;
-            if (q == 0) {
-                S.LF[0][0] = S.TF[0][0] = (S.L[0][1] + 2 * S.L[0][0] + S.T[0][1] + 2) >> 2;
-            } else if (q == 16) {
-                S.LF[0][16] = S.L[0][16];
-                S.TF[0][16] = S.T[0][16];
-            } else {
-                S.LF[0][q] = (S.L[0][q + 1] + 2 * S.L[0][q] + S.L[0][q - 1] + 2) >> 2;
-                S.TF[0][q] = (S.T[0][q + 1] + 2 * S.T[0][q] + S.T[0][q - 1] + 2) >> 2;
+            if (pass == 0) {
+                const int vm = __shfl_up(v, 1, 64), vp = __shfl_down(v, 1, 64);
+                if (i < 33) {
+                    const int f = (i == 0 || i == 32) ? v : (vm + 2 * v + vp + 2) >> 2;
+                    if (i < 16) {
+                        S.L[0][16 - i] = v;
+                        S.LF[0][16 - i] = f;
+                    } else if (i == 16) {
+                        S.L[0][0] = S.T[0][0] = v;
+                        S.LF[0][0] = S.TF[0][0] = f;
+                    } else {
+                        S.T[0][i - 16] = v;
+                        S.TF[0][i - 16] = f;
+                    }
+                }
+                // DC: luma L[1..8] (i 8..15) + T[1..8] (i 17..24); chroma c: L[1..4] (q 4..7), T[1..4] (q 9..12)
+                dcl = wsum((i >= 8 && i <= 15) || (i >= 17 && i <= 24) ? v : 0);
+                const int qc = i - 33, qq = qc - 17;
+                dcc0 = wsum(i >= 33 && ((qc >= 4 && qc <= 7) || (qc >= 9 && qc <= 12)) ? v : 0);
+                dcc1 = wsum(i >= 50 && ((qq >= 4 && qq <= 7) || (qq >= 9 && qq <= 12)) ? v : 0);
             }
         }
-        {  // DC sums: lanes 0..15 luma, 16..23 Cb, 24..31 Cr
-            const int v = lane < 16 ? (lane < 8 ? S.L[0][1 + lane] : S.T[0][1 + lane - 8])
-                                    : (lane < 32 ? ((lane & 7) < 4 ? S.L[1 + ((lane >> 3) & 1)][1 + (lane & 3)]
-                                                                   : S.T[1 + ((lane >> 3) & 1)][1 + (lane & 3)])
-                                                 : 0);
-            const int g8 = gsum<8>(v);
-            const int g16 = gsum<16>(v);
-            if (lane == 0) S.dc[0] = (g16 + 8) >> 4;
-            if (lane == 16) S.dc[1] = (g8 + 4) >> 3;
-            if (lane == 24) S.dc[2] = (g8 + 4) >> 3;
-        }
+        dcl = (dcl + 8) >> 4;
+        dcc0 = (dcc0 + 4) >> 3;
+        dcc1 = (dcc1 + 4) >> 3;
         wave_lds_sync();
         // ---- prediction and residual
-        const int pl = pred_sample(mode, 3, true, S.L[0], S.T[0], S.LF[0], S.TF[0], S.dc[0], lx, ly);
+        const int pl = pred_sample(mode, 3, true, S.L[0], S.T[0], S.LF[0], S.TF[0], dcl, lx, ly);
         const int ol = (by + ly) * 16 + bx + lx;
         t.res[lane] = (int16_t)((int)src[ol] - pl);
         int pc = 0, oc = 0;
         if (cl) {
-            pc = pred_sample(mode, 2, false, S.L[1 + comp], S.T[1 + comp], S.L[1 + comp], S.T[1 + comp], S.dc[1 + comp],
-                             cx, cy);
+            pc = pred_sample(mode, 2, false, S.L[1 + comp], S.T[1 + comp], S.L[1 + comp], S.T[1 + comp],
+                             comp ? dcc1 : dcc0, cx, cy);
             oc = 256 + comp * 64 + (cby + cy) * 8 + cbx + cx;
             t.res[64 + comp * 16 + cy * 4 + cx] = (int16_t)((int)src[oc] - pc);
         }
