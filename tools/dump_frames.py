@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bitrate-kbps", type=int, default=8000)
     ap.add_argument("--out", default="gpurun_out/frames_1080p.npz")
+    ap.add_argument("--content", default="desktop", choices=["desktop", "motion", "subpel"])
     a = ap.parse_args()
     import mxdesk
 
@@ -31,6 +32,9 @@ def main():
     cfg = N.SessionConfig()
     cfg.width, cfg.height, cfg.fps = a.width, a.height, 60
     cfg.fake_clock = 1
+    cfg.content = {"desktop": 0, "motion": 1, "subpel": 2}[a.content]
+    if a.content != "desktop":
+        cfg.noise = 0  # as bench.py: the moving contents carry a video panel instead of the noise panel
     cfg.enc.bitrate_kbps = a.bitrate_kbps
     ow, oh = a.width, a.height
     cfg.mask_x0, cfg.mask_y0 = int(ow * 0.04), int(oh * 0.55)
