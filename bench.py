@@ -350,6 +350,9 @@ def main() -> None:
     ap.add_argument("--deblock", type=int, default=None,
                     help="in-loop deblocking filter 0 off / 1 on / 2 adaptive per picture (H.264: "
                          "from the picture's temporal classes; default: the encoder's)")
+    ap.add_argument("--hevc-intra-split", type=int, default=None,
+                    help="HEVC I pictures: 16x16 intra units may split into four 8x8 luma / 4x4 chroma TUs "
+                         "(1, the encoder's default) or not (0)")
     ap.add_argument("--hevc-chroma-keep", type=int, default=None,
                     help="HEVC: changing content keeps its chroma residual (1) instead of dropping it (0)")
     ap.add_argument("--chroma-qp-offset", type=int, default=None,
@@ -458,6 +461,8 @@ def main() -> None:
         cfg.enc.hevc_wpp_rows = args.hevc_wpp_rows
     if args.hevc_chroma_keep is not None:
         cfg.enc.hevc_chroma_keep = args.hevc_chroma_keep
+    if args.hevc_intra_split is not None:
+        cfg.enc.hevc_intra_split = args.hevc_intra_split
     if args.chroma_qp_offset is not None:
         cfg.enc.chroma_qp_offset = args.chroma_qp_offset
     if args.intra_in_p is not None:
@@ -620,6 +625,7 @@ def main() -> None:
                 int(cfg.enc.deblock), "off" if args.codec == "vp8" else "adaptive"),
             "intra_in_p": int(cfg.enc.intra_in_p),
             "vp8_tools": {"bpred": int(cfg.enc.vp8_bpred), "intra": int(cfg.enc.vp8_intra)} if args.codec == "vp8" else None,
+            "hevc_intra_split": int(cfg.enc.hevc_intra_split) if args.codec == "hevc" else None,
             "deblocked_frames_pct": round(100.0 * sum(dbk) / max(1, len(dbk)), 1),
             # the adaptive filter's inputs (h264_deblock.h db_auto_decide): mean coherent / moving
             # macroblocks per picture
