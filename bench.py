@@ -308,6 +308,32 @@ class CpuSession:
                                      t_encoded_us=t1 * 1e6)
 
 
+def serving_probe(args, dev_index: int) -> dict | None:
+    """The density probes in the serving path's configuration: a child process of this one (never an
+    exec) with GPU_MAX_HW_QUEUES=16, as `mxdesk serve --sessions K` runs its sessions (mxdesk/cli.py),
+    on this rank's GPU, outside any process group.  More hardware queues let the sessions' IDR
+    wavefronts -- long serial chains on few workgroups -- run side by side instead of queueing
+    (profiles/r06_density/NOTES.md); the in-process probes keep HIP's default."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["GPU_MAX_HW_QUEUES"] = "16"
+    cmd = [sys.executable, str(Path(__file__).resolve()), *sys.argv[1:], "--gpus", "1", "--density-only", "1",
+           "--device-index", str(dev_index), "--quality-probe", "0"]
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    except subprocess.TimeoutExpired:
+        print("bench.py: serving probe timed out", file=sys.stderr)
+        return None
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        print(f"bench.py: serving probe failed (rc {p.returncode}): {p.stderr[-500:]}", file=sys.stderr)
+        return None
+    return json.loads(lines[-1])
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -379,6 +405,12 @@ def main() -> None:
                     help="after the timed run, measure how many paced 1080p60 sessions this GPU sustains in this "
                          "process (doubling K until a 60 fps slot is missed, then bisecting); reported, never part "
                          "of `value`")
+    ap.add_argument("--serving-probe", type=int, default=1,
+                    help="GPU: also run the paced and IDR-storm density probes in the serving path's configuration "
+                         "(a child process with the 16 hardware queues `mxdesk serve --sessions K` sets, "
+                         "mxdesk/cli.py); reported beside the in-process probes, never part of `value`")
+    ap.add_argument("--density-only", type=int, default=0, help=argparse.SUPPRESS)  # the serving-probe child
+    ap.add_argument("--device-index", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL on ROCm; gloo only to rehearse the "
                          "multi-rank plumbing with several ranks on one GPU)")
@@ -423,7 +455,7 @@ def main() -> None:
 
     # one rank per GPU; the modulo only matters when rehearsing several ranks on fewer GPUs
     ndev = max(1, torch.cuda.device_count()) if gpu else 1
-    dev_index = local_rank % ndev
+    dev_index = args.device_index if args.device_index >= 0 else local_rank % ndev
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
@@ -491,6 +523,11 @@ def main() -> None:
         # renderer's desktop_px(), csrc/kernels/pixel.hip, in encoded-picture coordinates)
         cfg.mask_x0, cfg.mask_y0 = int(ow * 0.04), int(oh * 0.55)
         cfg.mask_x1, cfg.mask_y1 = cfg.mask_x0 + int(ow * 0.16) + 1, cfg.mask_y0 + int(oh * 0.22) + 1
+    if args.density_only:  # the serving-probe child: the two density probes, one JSON line
+        d = density_probe(N, cfg, args.fps)
+        st = density_probe(N, cfg, args.fps, k0=max(4, (d["sustained"] or 16) // 4), idr_storm=True)
+        print(json.dumps({"density": d, "storm": st, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}), flush=True)
+        return
     K = max(1, args.sessions_per_gpu)
     sessions = [N.Session(cfg) if gpu else CpuSession(N, cfg, args.noise) for _ in range(K)]
 
@@ -565,6 +602,7 @@ def main() -> None:
     # the same probe with every session's IDR in one slot, from a quarter of the steady-state K
     storm = (density_probe(N, cfg, args.fps, k0=max(4, (density["sustained"] or 16) // 4), idr_storm=True)
              if args.density_probe and gpu else None)
+    serving = serving_probe(args, dev_index) if args.density_probe and args.serving_probe and gpu else None
 
     if dist is not None:
         t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
@@ -578,12 +616,17 @@ def main() -> None:
         all_sizes = [x for g in gsz for x in g]
         # every rank probed its own GPU: the node's figure is the sum over ranks
         gd = [None] * world
-        dist.all_gather_object(gd, [density["sustained"] if density else None, storm["sustained"] if storm else None])
+        dist.all_gather_object(gd, [density["sustained"] if density else None, storm["sustained"] if storm else None,
+                                    serving["density"]["sustained"] if serving else None,
+                                    serving["storm"]["sustained"] if serving else None])
         rank_density, rank_storm = [d[0] for d in gd], [d[1] for d in gd]
+        rank_sdensity, rank_sstorm = [d[2] for d in gd], [d[3] for d in gd]
     else:
         elapsed_max, all_lat, all_sizes = elapsed, lat_ms, sizes
         rank_density = [density["sustained"] if density else None]
         rank_storm = [storm["sustained"] if storm else None]
+        rank_sdensity = [serving["density"]["sustained"] if serving else None]
+        rank_sstorm = [serving["storm"]["sustained"] if serving else None]
 
     def node_sum(v):
         return None if any(x is None for x in v) else sum(v)
@@ -657,6 +700,13 @@ def main() -> None:
             # measured: the sustained K when every session codes a forced IDR in the same slot
             "sessions_per_gpu_idr_storm_measured": storm["sustained"] if storm else None,
             "density_probe_idr_storm": storm,
+            # the same two probes in the serving path's configuration (serving_probe: a child process
+            # with the 16 hardware queues `mxdesk serve --sessions K` uses)
+            "serving_config": {"hw_queues": 16,
+                               "sessions_per_node_measured": node_sum(rank_sdensity),
+                               "sessions_per_node_idr_storm_measured": node_sum(rank_sstorm),
+                               "sessions_per_gpu_measured_by_rank": rank_sdensity,
+                               "sessions_per_gpu_idr_storm_by_rank": rank_sstorm} if serving else None,
             "dtype": "uint8 video (8-bit 4:2:0), " + CODEC_LABEL[args.codec][2],
             "data": "synthetic (HIP-rendered animated-noise/gears desktop, random-free deterministic)" if gpu
             else "synthetic (numpy-rendered desktop, mxdesk.models.synthetic.CpuSyntheticDesktop)",
