@@ -7,9 +7,10 @@
 //                  matrix products (4 luma + 2 chroma outputs per lane per stage),
 //                  quantisation, normative inverse transform and reconstruction, coded
 //                  sub-block / last-position summaries by wave reductions.
-//  * k_hevc_intra  one workgroup per slice, one wave per CTU row; the rows of a slice run
-//                  as a wavefront (row r two CTUs behind row r-1) with the left column
-//                  and the bottom rows of the row above exchanged through LDS.
+//  * k_hevc_intra  one workgroup per slice, one wave per unit row; the rows of a slice run
+//                  as a wavefront (a unit waits until the row above finished the units
+//                  above and above-right: per-row progress counters in LDS, no workgroup
+//                  barriers) with the left column and the bottom rows exchanged through LDS.
 //  * k_hevc_bins / k_hevc_tokscan / k_hevc_tokgather / k_hevc_arith  CABAC in two phases:
 //                  every CTU binarised at once (one wave per CTU, one lane per syntax part,
 //                  hevc_core.h binarise_part) into bin tokens laid out densely in decoding order, then
@@ -108,15 +109,11 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// Stage separator of the TU helpers: a workgroup barrier when the waves of the workgroup run in
-// lockstep (the intra wavefront), else a wave-local one (inter CUs: every wave has its own LDS
-// scratch and may skip work the others do).
+// Stage separator of the TU helpers: wave-local (every wave has its own LDS scratch; the intra
+// wavefront's rows synchronise through progress counters, not workgroup barriers).
 template <bool kWaveLocal>
 __device__ __forceinline__ void tu_sync() {
-    if (kWaveLocal)
-        wave_lds_sync();
-    else
-        __syncthreads();
+    wave_lds_sync();  // both users run their waves alone (the intra wavefront through progress counters)
 }
 
 // Transform matrices in LDS (filled once per workgroup).
@@ -171,10 +168,9 @@ struct alignas(16) TuBuf {
 
 // One wave transforms, quantises and reconstructs its CU's three TUs.  Lane mapping per
 // stage: luma outputs lane*4 .. lane*4+3, chroma outputs (lane&31)*2 .. +1 of component
-// lane>>5.  tu_sync<kInterCu>() separates the stages: intra CUs (kInterCu false) run in lockstep
-// with workgroup barriers, so every wave of the workgroup calls this the same number of times
-// (idle waves with valid == false), and keep their reconstruction in t.pred for the neighbours;
-// inter CUs sync per wave and leave t.pred (the prediction) intact for the split tree after it.
+// lane>>5.  tu_sync<kInterCu>() (wave-local) separates the stages; intra CUs (kInterCu false)
+// keep their reconstruction in t.pred for the neighbours, inter CUs leave t.pred (the prediction)
+// intact for the split tree after it.
 struct TuResult {
     int last[3];
     uint32_t csbf[3];
@@ -1492,19 +1488,19 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     __shared__ uint8_t leftc[kMaxSliceRows][32];  // right column of the wave's previous CU: 16 Y, 8 Cb, 8 Cr
     __shared__ SplitRefs srf[kMaxSliceRows];          // split units: TU references (split_intra_code)
     __shared__ alignas(16) uint8_t srcs[kMaxSliceRows][384];  // split units: the unit's source (t.pred layout)
+    // units of each row finished: its bottom lines are in LDS up to there (the row below waits on it)
+    __shared__ int prog[kMaxSliceRows];
     fill_mats(M);
-    __syncthreads();
+    if (threadIdx.x < kMaxSliceRows) prog[threadIdx.x] = 0;
+    __syncthreads();  // the only workgroup barrier: from here every wave runs its row alone
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int sr = fs->slice_rows;
-    // one wave per unit row (the launch may add idle helper waves: H per row)
-    const int H = max(1, ((int)blockDim.x >> 6) / sr);
-    const int row = wave / H, sub = wave - row * H, mw = row * H;
-    const bool main_w = sub == 0;
+    const int row = wave;  // one wave per unit row of the slice
     // slice blockIdx.x: segment seg of CTB row band blockIdx.x / split (unit columns [xb, xe))
     const int seg_w = fs->i_seg_w, split = (g.mb_w + seg_w - 1) / seg_w;
     const int seg = (int)blockIdx.x % split, xb = seg * seg_w, xe = min(g.mb_w, xb + seg_w);
     const int y = ((int)blockIdx.x / split) * sr + row;  // CTU row of this wave
-    const bool row_ok = row < sr && y < g.mb_h;
+    if (row >= sr || y >= g.mb_h) return;  // wave-uniform; no workgroup barrier below, nobody waits on it
     const int qp = fs->qp;
     const int qpc = chroma_qp(qp, fs->chroma_qp_offset);
     const int cw = g.coded_w;
@@ -1515,20 +1511,20 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
     TuBuf& t = tb[wave];
     IntraRefs& R = rf[wave];
     unsigned long long acc[3] = {0, 0, 0};
-    const int steps = (xe - xb) + 2 * (sr - 1);
-    // this lane's source samples of the CTU, loaded a step ahead (off the critical path):
+    // this lane's source samples of the CTU, loaded a unit ahead (off the critical path):
     // luma row lane / 4, columns 4 (lane % 4) .. +3; chroma row lane / 8, Cb/Cr pair lane % 8
     auto load_src = [&](int xx, uint32_t& ly, uint32_t& lc) {
-        if (!row_ok || xx < xb || xx >= xe) return;
+        if (xx >= xe) return;
         const int r = lane >> 2, cb = (lane & 3) * 4, rc = lane >> 3, cc = lane & 7;
         ly = *reinterpret_cast<const uint32_t*>(src_y + (size_t)(y * 16 + r) * g.pitch + xx * 16 + cb);
         lc = *reinterpret_cast<const uint16_t*>(src_uv + (size_t)(y * 8 + rc) * g.pitch + xx * 16 + 2 * cc);
     };
     uint32_t nsy = 0, nsc = 0;
-    load_src(xb - 2 * row, nsy, nsc);
-    for (int step = 0; step < steps; ++step) {
-        const int x = xb + step - 2 * row;
-        const bool valid = row_ok && x >= xb && x < xe;
+    load_src(xb, nsy, nsc);
+    // The rows of a slice form a wavefront through the progress counters alone (as k_intra_wave):
+    // unit x of row r needs units x - 1 .. x + 1 of row r - 1 (corner, top, top-right), so a split
+    // unit (four serial TU chains) delays only the rows below it, and only when they catch up.
+    for (int x = xb; x < xe; ++x) {
         const int x0 = x * 16, y0 = y * 16;
         const uint32_t sy4 = nsy, sc2 = nsc;
         load_src(x + 1, nsy, nsc);
@@ -1537,99 +1533,35 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
         // by this raster wavefront: k_hevc_intra_modes gave that unit a mode that never reads it
         const int z = ((y & 1) << 1) | (x & 1);
         const bool al = x > xb, at = row > 0, atr = at && x + 1 < xe && z != 3, ac = at && x > xb;
+        if (at) {
+            const int need = (atr ? x + 2 : x + 1) - xb;
+            while (__hip_atomic_load(&prog[row - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+                __builtin_amdgcn_s_sleep(1);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        }
         // ---- gather neighbour samples (left from LDS, above from the upper wave's bottom row)
-        if (valid) {
-            if (lane < 16) {
-                R.lpx[lane] = al ? leftc[mw][lane] : 0;
-                R.tpx[lane] = at ? up_y[x0 + lane] : 0;
-                R.trx[lane] = atr ? up_y[x0 + 16 + lane] : 0;
-            } else if (lane < 32) {
-                const int k = lane - 16, comp = k >> 3, q = k & 7;
-                R.lc[comp][q] = al ? leftc[mw][16 + comp * 8 + q] : 0;
-                R.tc[comp][q] = at ? up_c[x0 + 2 * q + comp] : 0;
-                R.trc[comp][q] = atr ? up_c[x0 + 16 + 2 * q + comp] : 0;
-            } else if (lane == 32) {
-                R.corner = ac ? up_y[x0 - 1] : 0;
-                R.corner_c[0] = ac ? up_c[x0 - 2] : 0;
-                R.corner_c[1] = ac ? up_c[x0 - 1] : 0;
-            }
+        if (lane < 16) {
+            R.lpx[lane] = al ? leftc[wave][lane] : 0;
+            R.tpx[lane] = at ? up_y[x0 + lane] : 0;
+            R.trx[lane] = atr ? up_y[x0 + 16 + lane] : 0;
+        } else if (lane < 32) {
+            const int k = lane - 16, comp = k >> 3, q = k & 7;
+            R.lc[comp][q] = al ? leftc[wave][16 + comp * 8 + q] : 0;
+            R.tc[comp][q] = at ? up_c[x0 + 2 * q + comp] : 0;
+            R.trc[comp][q] = atr ? up_c[x0 + 16 + 2 * q + comp] : 0;
+        } else if (lane == 32) {
+            R.corner = ac ? up_y[x0 - 1] : 0;
+            R.corner_c[0] = ac ? up_c[x0 - 2] : 0;
+            R.corner_c[1] = ac ? up_c[x0 - 1] : 0;
         }
-        __syncthreads();
-        // ---- reference substitution (8.4.4.2.2) for every sample at once, then the planar
-        // filter and DC sums; the same values as intra_refs() + the lane-serial loops this
-        // replaced (their availability/pointer lambdas lived in scratch: two dependent memory
-        // round trips per reference sample on the wavefront's critical path)
-        if (valid) {
-            const int avl = (al ? 2 : 0) | (ac ? 4 : 0) | (at ? 8 : 0) | (atr ? 16 : 0);  // no bottom-left
-            for (int i = lane; i <= 64; i += 64) {
-                const int v = ref_subst(i, 16, avl, R.lpx, R.tpx, R.trx, R.corner);
-                if (i < 32) R.L[32 - i] = v;
-                else if (i == 32) R.L[0] = R.T[0] = v;
-                else R.T[i - 32] = v;
-            }
-            for (int k = lane; k < 66; k += 64) {
-                const int comp = k >= 33 ? 1 : 0, i = k - 33 * comp;
-                const int v = ref_subst(i, 8, avl, R.lc[comp], R.tc[comp], R.trc[comp], R.corner_c[comp]);
-                if (i < 16) R.Lc[comp][16 - i] = v;
-                else if (i == 16) R.Lc[comp][0] = R.Tc[comp][0] = v;
-                else R.Tc[comp][i - 16] = v;
-            }
-        }
-        __syncthreads();
-        if (valid) {
-            if (lane <= 32) {
-                const int k = lane;
-                if (k == 0) {
-                    R.LF[0] = R.TF[0] = (R.L[1] + 2 * R.L[0] + R.T[1] + 2) >> 2;
-                } else if (k == 32) {
-                    R.LF[32] = R.L[32];
-                    R.TF[32] = R.T[32];
-                } else {
-                    R.LF[k] = (R.L[k + 1] + 2 * R.L[k] + R.L[k - 1] + 2) >> 2;
-                    R.TF[k] = (R.T[k + 1] + 2 * R.T[k] + R.T[k - 1] + 2) >> 2;
-                }
-            }
-            const int sl = lane < 16 ? R.L[1 + lane] + R.T[1 + lane] : 0;
-            const int c0 = (lane >= 16 && lane < 24) ? R.Lc[0][lane - 15] + R.Tc[0][lane - 15] : 0;
-            const int c1 = (lane >= 24 && lane < 32) ? R.Lc[1][lane - 23] + R.Tc[1][lane - 23] : 0;
-            const int s_l = wsum(sl), s_c0 = wsum(c0), s_c1 = wsum(c1);
-            if (lane == 0) {
-                R.dc = (s_l + 16) >> 5;
-                R.dcc[0] = (s_c0 + 8) >> 4;
-                R.dcc[1] = (s_c1 + 8) >> 4;
-            }
-        }
-        __syncthreads();
+        wave_lds_sync();
         // ---- the mode (and the split) decided open-loop by k_hevc_intra_modes
-        int mode = 1;
-        bool split = false;
-        if (valid && main_w) {
-            const int im = (int)imode[y * g.mb_w + x];  // (wave-uniform)
-            mode = im & (kIntraSplitFlag - 1);
-            split = (im & kIntraSplitFlag) != 0;
-        }
-        if (valid && main_w && !split) {
-            const int r = lane >> 2, cb = (lane & 3) * 4;
-            for (int j = 0; j < 4; ++j) {
-                const int p = pred_sample(mode, 4, true, R.L, R.T, R.LF, R.TF, R.dc, cb + j, r);
-                t.pred[r * 16 + cb + j] = (uint8_t)p;
-                t.res[r * 16 + cb + j] = (int16_t)((int)((sy4 >> (8 * j)) & 0xff) - p);
-            }
-            const int rc = lane >> 3, cc = lane & 7;
-            for (int comp = 0; comp < 2; ++comp) {
-                const int p = pred_sample(mode, 3, false, R.Lc[comp], R.Tc[comp], R.Lc[comp], R.Tc[comp], R.dcc[comp],
-                                          cc, rc);
-                t.pred[256 + comp * 64 + rc * 8 + cc] = (uint8_t)p;
-                t.res[256 + comp * 64 + rc * 8 + cc] = (int16_t)((int)((sc2 >> (8 * comp)) & 0xff) - p);
-            }
-        }
-        __syncthreads();
-        const int i = valid ? y * g.mb_w + x : 0;
-        const TuResult res = code_tus<false>(t, M, qp, qpc, true, valid && main_w && !split,
-                                             coef + (size_t)i * kCoefPerCu, fs->rec_y, g.pitch, fs->rec_uv, x0, y0,
-                                             g.width, g.height);
-        if (valid && main_w && split) {
-            // four 8x8 TUs, wave-local (the other waves wait at the step's next barrier)
+        const int im = (int)imode[y * g.mb_w + x];  // (wave-uniform)
+        const int mode = im & (kIntraSplitFlag - 1);
+        const bool split = (im & kIntraSplitFlag) != 0;
+        const int i = y * g.mb_w + x;
+        if (split) {
+            // four 8x8 TUs, each predicted from the reconstruction of the TUs before it
             uint8_t* sb = srcs[wave];
             {
                 const int r = lane >> 2, cb = (lane & 3) * 4, rc = lane >> 3, cc = lane & 7;
@@ -1658,7 +1590,59 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 cus[i] = c;
                 qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
             }
-        } else if (valid && main_w) {
+        } else {
+            // ---- reference substitution (8.4.4.2.2) for every sample at once, then the planar
+            // filter and DC sums; the same values as intra_refs() + the lane-serial loops this
+            // replaced (their availability/pointer lambdas lived in scratch: two dependent memory
+            // round trips per reference sample on the wavefront's critical path)
+            const int avl = (al ? 2 : 0) | (ac ? 4 : 0) | (at ? 8 : 0) | (atr ? 16 : 0);  // no bottom-left
+            for (int q = lane; q <= 64; q += 64) {
+                const int v = ref_subst(q, 16, avl, R.lpx, R.tpx, R.trx, R.corner);
+                if (q < 32) R.L[32 - q] = v;
+                else if (q == 32) R.L[0] = R.T[0] = v;
+                else R.T[q - 32] = v;
+            }
+            for (int k = lane; k < 66; k += 64) {
+                const int comp = k >= 33 ? 1 : 0, q = k - 33 * comp;
+                const int v = ref_subst(q, 8, avl, R.lc[comp], R.tc[comp], R.trc[comp], R.corner_c[comp]);
+                if (q < 16) R.Lc[comp][16 - q] = v;
+                else if (q == 16) R.Lc[comp][0] = R.Tc[comp][0] = v;
+                else R.Tc[comp][q - 16] = v;
+            }
+            wave_lds_sync();
+            if (lane <= 32) {
+                const int k = lane;
+                if (k == 0) {
+                    R.LF[0] = R.TF[0] = (R.L[1] + 2 * R.L[0] + R.T[1] + 2) >> 2;
+                } else if (k == 32) {
+                    R.LF[32] = R.L[32];
+                    R.TF[32] = R.T[32];
+                } else {
+                    R.LF[k] = (R.L[k + 1] + 2 * R.L[k] + R.L[k - 1] + 2) >> 2;
+                    R.TF[k] = (R.T[k + 1] + 2 * R.T[k] + R.T[k - 1] + 2) >> 2;
+                }
+            }
+            const int sl = lane < 16 ? R.L[1 + lane] + R.T[1 + lane] : 0;
+            const int c0 = (lane >= 16 && lane < 24) ? R.Lc[0][lane - 15] + R.Tc[0][lane - 15] : 0;
+            const int c1 = (lane >= 24 && lane < 32) ? R.Lc[1][lane - 23] + R.Tc[1][lane - 23] : 0;
+            const int dcl = (wsum(sl) + 16) >> 5, dc0 = (wsum(c0) + 8) >> 4, dc1 = (wsum(c1) + 8) >> 4;
+            wave_lds_sync();
+            const int r = lane >> 2, cb = (lane & 3) * 4;
+            for (int j = 0; j < 4; ++j) {
+                const int p = pred_sample(mode, 4, true, R.L, R.T, R.LF, R.TF, dcl, cb + j, r);
+                t.pred[r * 16 + cb + j] = (uint8_t)p;
+                t.res[r * 16 + cb + j] = (int16_t)((int)((sy4 >> (8 * j)) & 0xff) - p);
+            }
+            const int rc = lane >> 3, cc = lane & 7;
+            for (int comp = 0; comp < 2; ++comp) {
+                const int p = pred_sample(mode, 3, false, R.Lc[comp], R.Tc[comp], R.Lc[comp], R.Tc[comp],
+                                          comp ? dc1 : dc0, cc, rc);
+                t.pred[256 + comp * 64 + rc * 8 + cc] = (uint8_t)p;
+                t.res[256 + comp * 64 + rc * 8 + cc] = (int16_t)((int)((sc2 >> (8 * comp)) & 0xff) - p);
+            }
+            wave_lds_sync();
+            const TuResult res = code_tus<false>(t, M, qp, qpc, true, true, coef + (size_t)i * kCoefPerCu, fs->rec_y,
+                                                 g.pitch, fs->rec_uv, x0, y0, g.width, g.height);
             acc[0] += (unsigned)res.sse[0];
             acc[1] += (unsigned)res.sse[1];
             acc[2] += (unsigned)res.sse[2];
@@ -1677,22 +1661,22 @@ __global__ __launch_bounds__(64 * kMaxSliceRows) void k_hevc_intra(Geometry g, c
                 qp_coded[i] = c.cbf ? c.qp : (uint8_t)255;
             }
         }
-        __syncthreads();
-        if (valid && main_w) {
-            // reconstruction edges (kept in t.pred by code_tus): right column -> left
-            // neighbour of this row's next CU, bottom rows -> the waves of the row below
-            if (lane < 16) {
-                leftc[mw][lane] = t.pred[lane * 16 + 15];
-                bot_y[x0 + lane] = t.pred[15 * 16 + lane];
-                bot_c[x0 + lane] = t.pred[256 + (lane & 1) * 64 + 7 * 8 + (lane >> 1)];
-            } else if (lane < 32) {
-                const int k = lane - 16, comp = k >> 3, q = k & 7;
-                leftc[mw][16 + comp * 8 + q] = t.pred[256 + comp * 64 + q * 8 + 7];
-            }
+        wave_lds_sync();
+        // reconstruction edges (kept in t.pred): right column -> left neighbour of this row's next
+        // unit, bottom rows -> the row below, then publish the unit
+        if (lane < 16) {
+            leftc[wave][lane] = t.pred[lane * 16 + 15];
+            bot_y[x0 + lane] = t.pred[15 * 16 + lane];
+            bot_c[x0 + lane] = t.pred[256 + (lane & 1) * 64 + 7 * 8 + (lane >> 1)];
+        } else if (lane < 32) {
+            const int k = lane - 16, comp = k >> 3, q = k & 7;
+            leftc[wave][16 + comp * 8 + q] = t.pred[256 + comp * 64 + q * 8 + 7];
         }
-        __syncthreads();
+        wave_lds_sync();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // LDS completes the line stores before the counter
+        if (lane == 0) __hip_atomic_store(&prog[row], x - xb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (row_ok && main_w && lane < 3)  // wave sums (identical in every lane)
+    if (lane < 3)  // wave sums (identical in every lane)
         fs->sse_part[lane * h264::kSsePartStride + y * split + seg] = lane == 0 ? acc[0] : (lane == 1 ? acc[1] : acc[2]);
 }
 
