@@ -2015,6 +2015,9 @@ inline uint64_t bl_safe_split() { return bl_safe_modes(3, 0) & bl_safe_modes(2, 
 constexpr int kIntraSplitBits = 10;
 constexpr int kIntraSplitFlag = 64;
 MXHD bool intra_split_wins(int cost16, int cost8, int lambda) { return cost8 + lambda * kIntraSplitBits < cost16; }
+// a split cost is at least lambda * 2 (the cheapest mode signalling): below this unsplit cost the split
+// search cannot win and is skipped (flat content; the decision is unchanged)
+MXHD bool intra_split_possible(int cost16, int lambda) { return cost16 > lambda * (kIntraSplitBits + 2); }
 
 constexpr int kIntraCoarse[11] = {0, 1, 2, 6, 10, 14, 18, 22, 26, 30, 34};
 constexpr int kIntraNoMode = 0x7fffffff;

@@ -480,7 +480,7 @@ int intra_decide_mode(const uint8_t* sy, int pitch, int mb_w, int mb_h, int x, i
         return satd16(sy, pitch, x0, y0, pred) + lambda * intra_mode_bits(m, 1, 1);
     };
     const int best = intra_mode_search(cost);
-    if (!split) return best;
+    if (!split || !intra_split_possible(cost(best), lambda)) return best;
     int Lk[4][17], Tk[4][17];
     for (int k = 0; k < 4; ++k)
         block_refs(sy, pitch, 1, x0 + (k & 1) * 8, y0 + (k >> 1) * 8, 8, split_tu_avl(k, al, ac, at, atr), Lk[k], Tk[k]);

@@ -1250,7 +1250,8 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
     };
     const int best = intra_mode_search(cost);  // coarse-to-fine: at most 15 of the 35 modes
     int out = best;
-    if (fs->depth_intra > 0) {  // the split tree: its own mode search over the four TUs' predictions
+    const int cost16 = cost(best);
+    if (fs->depth_intra > 0 && intra_split_possible(cost16, lambda)) {  // the split tree's own mode search (wave-uniform)
         SplitRefs& S = srf[wave];
         for (int i = lane; i < 4 * 33; i += 64) {  // raw references of the four TUs, from the source
             const int k = i / 33, q = i - k * 33;
@@ -1287,7 +1288,7 @@ __global__ __launch_bounds__(256) void k_hevc_intra_modes(Geometry g, const Hevc
             return wsum(sad) + lambda * intra_mode_bits(m, 1, 1);
         };
         const int best_s = intra_mode_search(cost_split);
-        if (intra_split_wins(cost(best), cost_split(best_s), lambda)) out = best_s | kIntraSplitFlag;
+        if (intra_split_wins(cost16, cost_split(best_s), lambda)) out = best_s | kIntraSplitFlag;
     }
     if (lane == 0) imode[y * g.mb_w + x] = (uint8_t)out;
 }
