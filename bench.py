@@ -395,7 +395,7 @@ def main() -> None:
                          "default 3, VP8 4: its host bitstream writers run one per frame in flight)")
     ap.add_argument("--capture-stream", type=int, default=-1,
                     help="depth > 1: render + convert on a capture stream, one NV12 buffer per frame in flight "
-                         "(frame n+1's capture overlaps frame n's analysis); -1 = H.264 only (measured gain), "
+                         "(frame n+1's capture overlaps frame n's analysis); -1 = H.264 and HEVC (measured gains), "
                          "1 = every codec, 0 = one analysis stream")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay the per-frame chain as a hipGraph (eager launches measured faster: profiles/r01_graph)")

@@ -112,7 +112,8 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
         HIP_CHECK(hipMalloc(&nv12_y_[k], (size_t)g.pitch * g.coded_h));
         HIP_CHECK(hipMalloc(&nv12_uv_[k], (size_t)g.pitch * g.coded_h / 2));
     }
-    const bool cap = cfg_.capture_stream > 0 || (cfg_.capture_stream < 0 && std::string(enc_->codec()) == "h264");
+    const std::string codec = enc_->codec();
+    const bool cap = cfg_.capture_stream > 0 || (cfg_.capture_stream < 0 && (codec == "h264" || codec == "hevc"));
     if (depth_ > 1 && cap && !cfg_.use_graph) {
         // MXDESK_CAPTURE_PRIORITY=low: the capture stream at the lowest priority, so its render /
         // conversion kernels yield compute units to the previous frame's analysis (4K H.264

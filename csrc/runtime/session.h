@@ -67,9 +67,11 @@ struct SessionConfig {
     int mask_x0 = 0, mask_y0 = 0, mask_x1 = 0, mask_y1 = 0;
     int scale_valu = 0;     // 1: the LDS/VALU Lanczos kernel instead of the matrix-core one
     // pipeline depth > 1: render + convert each frame on a capture stream into its own NV12
-    // buffer, so frame n+1's capture overlaps frame n's analysis.  -1 = H.264 only (1080p: 9,040
-    // -> 10,125 fps; HEVC 4K: 2,272 -> 1,633 fps, its 4K render then contends with the analysis
-    // kernels -- profiles/r04_capture), 1 = every codec, 0 = one analysis stream
+    // buffer, so frame n+1's capture overlaps frame n's analysis.  -1 = H.264 and HEVC (1080p H.264:
+    // 9,040 -> 10,125 fps, profiles/r04_capture; 4K HEVC: 2,176 -> 2,277 fps once its entropy
+    // streams leave the capture stream a hardware queue of its own -- sharing the analysis queue it
+    // had cost 2,272 -> 1,633 in round 4, profiles/r06_streams), 1 = every codec (VP8 too), 0 = one
+    // analysis stream
     int capture_stream = -1;
     h264::EncoderConfig enc;  // width/height overwritten from out size
 };
