@@ -193,7 +193,7 @@ def test_decoder_rejects_truncated_stream(native):
 
 # ---------------------------------------------------------------------------- GPU tier
 def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, aq=1, desktop=False, sao=1,
-                wpp=0, wpp_rows=8):
+                wpp=0, wpp_rows=8, intra_split=None, idr_at=()):
     import torch
 
     from .gpu_util import pitched
@@ -201,6 +201,8 @@ def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, 
     cfg = _cfg(gpu, w, h, fps, qp, sr=sr, tu_split=tu_split, aq=aq)
     cfg.sao = sao
     cfg.hevc_wpp, cfg.hevc_wpp_rows = wpp, wpp_rows
+    if intra_split is not None:
+        cfg.hevc_intra_split = intra_split
     desk = None
     if desktop:
         from mxdesk.models.synthetic import CpuSyntheticDesktop, bgrx_to_nv12
@@ -219,8 +221,8 @@ def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, 
         dy = pitched(y, genc.pitch, ch)
         duv = pitched(uv, genc.pitch, ch // 2, uv=True)
         torch.cuda.synchronize()
-        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), False)
-        cau = cenc.encode(y, uv, False)
+        gau = genc.encode(dy.data_ptr(), duv.data_ptr(), t in idr_at)
+        cau = cenc.encode(y, uv, t in idr_at)
         assert bool(gau == cau), f"frame {t}: GPU HEVC bitstream differs from the CPU encoder ({len(gau)} vs {len(cau)})"
         gs += gau
         grec.append(genc.recon())
@@ -241,6 +243,15 @@ def _gpu_vs_cpu(gpu, w, h, frames, fps=60, qp=26, fresh=True, sr=8, tu_split=0, 
                                         (128, 96, 60, 4)])
 def test_gpu_hevc_bit_exact_vs_cpu(gpu, w, h, fps, qp):
     _gpu_vs_cpu(gpu, w, h, 3, fps=fps, qp=qp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("intra_split", [0, 1])
+@pytest.mark.parametrize("w,h,qp", [(320, 192, 22), (352, 288, 34), (1920, 1080, 40)])
+def test_gpu_hevc_intra_split_bit_exact_vs_cpu(gpu, w, h, qp, intra_split):
+    """IDR pictures with and without the intra transform-tree split (the second one forced, into
+    reconstruction buffers that hold a previous picture): GPU == CPU == decoder, on the desktop."""
+    _gpu_vs_cpu(gpu, w, h, 3, qp=qp, desktop=True, intra_split=intra_split, idr_at=(2,))
 
 
 @pytest.mark.gpu
