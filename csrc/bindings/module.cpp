@@ -748,6 +748,19 @@ PYBIND11_MODULE(_native, m) {
             py::arg("addr"), py::arg("pitch"), py::arg("nbytes"), py::arg("force_idr") = false,
             "BGRx frame at a host address with `nbytes` readable (zero-copy inside a registered buffer; "
             "ValueError if the frame does not fit)")
+        .def(
+            "submit_bgrx_damage",
+            [](Session& s, uintptr_t addr, int pitch, size_t nbytes, std::vector<std::pair<int, int>> bands,
+               bool force_idr) {
+                py::gil_scoped_release rel;
+                s.submit_bgrx_damage(as_ptr<const uint8_t>(addr), pitch, nbytes, bands, force_idr);
+            },
+            py::arg("addr"), py::arg("pitch"), py::arg("nbytes"), py::arg("bands"), py::arg("force_idr") = false,
+            "damage-driven capture: DMA only the changed row bands [(y0, y1), ...] into the session's "
+            "device-resident screen (the first call uploads everything); ValueError for a band outside the frame")
+        .def("invalidate_screen", &Session::invalidate_screen,
+             "the next submit_bgrx_damage uploads the whole frame (e.g. after the capture lost damage events)")
+        .def_property_readonly("damage_bytes_uploaded", &Session::damage_bytes_uploaded)
         .def("collect",
              [](Session& s) {
                  py::gil_scoped_release rel;

@@ -232,6 +232,7 @@ Session::~Session() {
     if (lt_mem_) hipFree(lt_mem_);
     if (lt_mf_mem_) hipFree(lt_mf_mem_);
     for (const auto& r : host_regs_) (void)hipHostUnregister(const_cast<uint8_t*>(r.first));
+    if (screen_) (void)hipFree(screen_);
     if (ev_upload_) (void)hipEventDestroy(ev_upload_);
     if (upload_stream_) {
         (void)hipStreamSynchronize(upload_stream_);
@@ -432,8 +433,67 @@ void Session::register_host_buffer(const void* p, size_t bytes) {
         if (r.first == b && r.second == bytes) return;
     HIP_CHECK(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault));
     host_regs_.emplace_back(b, bytes);
+    ensure_upload_stream();
+}
+
+void Session::ensure_upload_stream() {
     if (!ev_upload_) HIP_CHECK(hipEventCreateWithFlags(&ev_upload_, hipEventDisableTiming));
     if (!upload_stream_) HIP_CHECK(hipStreamCreateWithFlags(&upload_stream_, hipStreamNonBlocking));
+}
+
+void Session::encode_uploaded(int slot, int k, bool force_idr) {
+    HIP_CHECK(hipEventRecord(ev_upload_, upload_stream_));
+    if (cap_stream_) {  // the conversion follows the DMA on its stream (overlaps earlier frames' analysis)
+        convert(slot, upload_stream_, devclk_ ? ts_ + slot : nullptr);
+        HIP_CHECK(hipEventRecord(ev_conv_[k], upload_stream_));
+        HIP_CHECK(hipStreamWaitEvent(stream_, ev_conv_[k], 0));
+        encode_converted(force_idr);
+    } else {
+        HIP_CHECK(hipStreamWaitEvent(stream_, ev_upload_, 0));
+        convert_and_encode(slot, force_idr, true);  // GPU time from the conversion (DMA excluded)
+    }
+    HIP_CHECK(hipEventSynchronize(ev_upload_));  // the caller may overwrite the buffer now
+}
+
+void Session::submit_bgrx_damage(const uint8_t* host_bgrx, int host_pitch, size_t bytes,
+                                 const std::vector<std::pair<int, int>>& bands, bool force_idr) {
+    TraceRange tr("mxdesk.submit_bgrx_damage(upload)");
+    if (host_pitch < cfg_.width * 4) throw std::invalid_argument("pitch < width * 4");
+    const int row = cfg_.width * 4;
+    const size_t span = (size_t)host_pitch * (cfg_.height - 1) + (size_t)row;
+    if (host_bgrx == nullptr || bytes < span)
+        throw std::invalid_argument("frame span (" + std::to_string(span) + " B) exceeds the buffer (" +
+                                    std::to_string(bytes) + " B)");
+    for (const auto& b : bands)
+        if (b.first < 0 || b.second > cfg_.height || b.first > b.second)
+            throw std::invalid_argument("damage band [" + std::to_string(b.first) + ", " + std::to_string(b.second) +
+                                        ") outside the frame");
+    ensure_upload_stream();
+    const size_t pitch = pool_->pitch();
+    if (!screen_) {
+        HIP_CHECK(hipMalloc(&screen_, pitch * cfg_.height));
+        screen_valid_ = false;
+    }
+    std::vector<std::pair<int, int>> todo;
+    if (!screen_valid_) todo.emplace_back(0, cfg_.height);
+    else
+        for (const auto& b : bands)
+            if (b.second > b.first) todo.push_back(b);
+    const int slot = pool_->acquire();
+    const int k = begin_frame(slot);
+    ++frame_id_;
+    if (!devclk_) HIP_CHECK(hipEventRecord(ev_start_[k], stream_));
+    // Bands and the screen -> slot copy are ordered on the upload stream; the slot's previous
+    // reader finished before its frame was collected (as in submit_bgrx's zero-copy path).
+    for (const auto& b : todo) {
+        HIP_CHECK(hipMemcpy2DAsync(screen_ + (size_t)b.first * pitch, pitch, host_bgrx + (size_t)b.first * host_pitch,
+                                   host_pitch, row, b.second - b.first, hipMemcpyHostToDevice, upload_stream_));
+        damage_bytes_ += (uint64_t)row * (b.second - b.first);
+    }
+    HIP_CHECK(hipMemcpyAsync(pool_->data(slot), screen_, pitch * cfg_.height, hipMemcpyDeviceToDevice,
+                             upload_stream_));
+    screen_valid_ = true;
+    encode_uploaded(slot, k, force_idr);
 }
 
 void Session::submit_bgrx_span(const uint8_t* host_bgrx, int host_pitch, size_t bytes, bool force_idr) {
@@ -463,17 +523,7 @@ void Session::submit_bgrx(const uint8_t* host_bgrx, int host_pitch, bool force_i
         // collected only after its whole chain completed.
         HIP_CHECK(hipMemcpy2DAsync(pool_->data(slot), pool_->pitch(), host_bgrx, host_pitch, row, cfg_.height,
                                    hipMemcpyHostToDevice, upload_stream_));
-        HIP_CHECK(hipEventRecord(ev_upload_, upload_stream_));
-        if (cap_stream_) {  // the conversion follows the DMA on its stream (overlaps earlier frames' analysis)
-            convert(slot, upload_stream_, devclk_ ? ts_ + slot : nullptr);
-            HIP_CHECK(hipEventRecord(ev_conv_[k], upload_stream_));
-            HIP_CHECK(hipStreamWaitEvent(stream_, ev_conv_[k], 0));
-            encode_converted(force_idr);
-        } else {
-            HIP_CHECK(hipStreamWaitEvent(stream_, ev_upload_, 0));
-            convert_and_encode(slot, force_idr, true);  // GPU time from the conversion (DMA excluded)
-        }
-        HIP_CHECK(hipEventSynchronize(ev_upload_));  // the caller may overwrite the buffer now
+        encode_uploaded(slot, k, force_idr);
         return;
     }
     const int slot = pool_->acquire();

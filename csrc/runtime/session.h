@@ -132,6 +132,17 @@ class Session {
     // submit_bgrx from a raw host address whose readable extent is `bytes`: throws
     // std::invalid_argument unless the frame span (pitch * (height - 1) + width * 4) fits.
     void submit_bgrx_span(const uint8_t* host_bgrx, int host_pitch, size_t bytes, bool force_idr = false);
+    // Damage-driven capture (XDamage): only the row bands [y0, y1) that changed since the last
+    // submit are DMA'd from the host frame into a device-resident copy of the screen, which is
+    // then copied into the frame-pool slot on the device.  The first call (and any call after
+    // invalidate_screen()) uploads the whole frame.  An empty band list re-encodes the resident
+    // screen without reading host memory.  A static desktop costs no PCIe traffic (at 1080p60 a
+    // full-frame upload is 0.5 GB/s per session, so 200 sessions would exceed a x16 link).
+    void submit_bgrx_damage(const uint8_t* host_bgrx, int host_pitch, size_t bytes,
+                            const std::vector<std::pair<int, int>>& bands, bool force_idr = false);
+    void invalidate_screen() { screen_valid_ = false; }
+    // host bytes DMA'd by submit_bgrx_damage so far (bands + first full frames)
+    uint64_t damage_bytes_uploaded() const { return damage_bytes_; }
     FrameResult collect();
     FrameResult step(bool force_idr = false) {
         submit_synthetic(force_idr);
@@ -189,6 +200,11 @@ class Session {
     std::vector<std::pair<const uint8_t*, size_t>> host_regs_;  // register_host_buffer ranges
     hipEvent_t ev_upload_ = nullptr;
     hipStream_t upload_stream_ = nullptr;  // zero-copy DMA from registered capture buffers
+    uint8_t* screen_ = nullptr;  // device-resident screen (submit_bgrx_damage), pool pitch
+    bool screen_valid_ = false;
+    uint64_t damage_bytes_ = 0;
+    void ensure_upload_stream();
+    void encode_uploaded(int slot, int k, bool force_idr);  // tail of the upload-stream paths
     // frames in flight (pipeline depth 1..kMaxDepth): per-frame start event / staging buffer
     struct Inflight {
         uint32_t frame_id;

@@ -55,6 +55,8 @@ def build_pipeline(cfg: C.Config, device: int = 0, session_name: str = "0", capt
         from .models.x11 import X11Capture
 
         capture = X11Capture(cfg.display, cfg.sizew, cfg.sizeh)
+        if cfg.capture_damage and not capture.enable_damage():
+            logging.getLogger("mxdesk").info("XDamage unavailable: full-frame capture")
     return StreamPipeline(cfg.sizew, cfg.sizeh, cfg.stream_fps, backend=backend, device=device,
                           bitrate_kbps=cfg.video_bitrate, keyint=cfg.keyint_frames, search_range=cfg.search_range,
                           subpel=cfg.subpel, noise=cfg.noise, out_width=cfg.out_width, out_height=cfg.out_height,

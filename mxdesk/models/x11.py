@@ -6,6 +6,15 @@ the frame is grabbed with ``XShmGetImage`` into a SysV shared-memory segment -- 
 inside this process -- and returned as an (H, W, 4) BGRx numpy view that the GPU session
 uploads from pinned memory (``Session.submit_bgrx``).  Falls back to ``XGetImage`` when the
 MIT-SHM extension is unavailable (e.g. remote displays).
+
+Damage-driven capture (``enable_damage``): the reference's ``ximagesrc`` runs with
+``use-damage=0`` and copies the whole screen every frame (selkies pipeline,
+``/root/reference/entrypoint.sh:110-131`` starts the X server it grabs from).  Here an XDamage
+object on the root window accumulates the changed region; each tick subtracts it (before the
+grab, so a change racing the grab is reported again next tick), turns its rectangles into a few
+row bands, and ``XShmGetImage`` copies only those bands into the SHM segment.  The GPU session
+DMAs the same bands into its device-resident screen (``Session.submit_bgrx_damage``), so a
+static desktop costs neither X-server copies nor PCIe traffic.
 """
 from __future__ import annotations
 
@@ -33,11 +42,128 @@ class XImage(ctypes.Structure):  # leading fields of Xlib's XImage (x86_64 layou
                 ("depth", ctypes.c_int), ("bytes_per_line", ctypes.c_int), ("bits_per_pixel", ctypes.c_int)]
 
 
+class XRectangle(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_short), ("y", ctypes.c_short), ("width", ctypes.c_ushort),
+                ("height", ctypes.c_ushort)]
+
+
+XDamageReportNonEmpty = 3  # one event when the damage goes from empty to non-empty
+
+
+def rects_to_bands(rects, height: int, align: int = 16, max_gap: int = 32, max_bands: int = 16
+                   ) -> list[tuple[int, int]]:
+    """Damaged rectangles ``(x, y, w, h)`` -> sorted, disjoint row bands ``(y0, y1)``.
+
+    Bands are widened to ``align``-row boundaries (macroblock rows: one DMA per band, and the
+    encoder's rows change whole), bands closer than ``max_gap`` rows merge (a DMA costs more
+    than a few extra rows), and while more than ``max_bands`` remain the closest pair merges."""
+    iv = []
+    for x, y, w, h in rects:
+        if w <= 0 or h <= 0:
+            continue
+        y0 = max(0, int(y)) // align * align
+        y1 = min(height, -(-(int(y) + int(h)) // align) * align)
+        if y1 > y0:
+            iv.append((y0, y1))
+    iv.sort()
+    out: list[list[int]] = []
+    for y0, y1 in iv:
+        if out and y0 - out[-1][1] < max_gap:
+            out[-1][1] = max(out[-1][1], y1)
+        else:
+            out.append([y0, y1])
+    while len(out) > max(1, max_bands):
+        i = min(range(len(out) - 1), key=lambda j: out[j + 1][0] - out[j][1])
+        out[i][1] = out[i + 1][1]
+        del out[i + 1]
+    return [(a, b) for a, b in out]
+
+
+class DamageTracker:
+    """XDamage on the root window (libXdamage + libXfixes through ctypes).  ``poll()`` returns
+    the row bands changed since the previous poll; the first poll (and the one after
+    ``invalidate()``) returns the whole screen."""
+
+    def __init__(self, x11, dpy, root: int, height: int, xdamage=None, xfixes=None):
+        self.x11, self.dpy, self.h = x11, dpy, int(height)
+        xd = xdamage or ctypes.CDLL(ctypes.util.find_library("Xdamage") or "libXdamage.so.1")
+        xf = xfixes or ctypes.CDLL(ctypes.util.find_library("Xfixes") or "libXfixes.so.3")
+        ev, err = ctypes.c_int(0), ctypes.c_int(0)
+        xd.XDamageQueryExtension.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_int)]
+        if not xd.XDamageQueryExtension(dpy, ctypes.byref(ev), ctypes.byref(err)):
+            raise OSError("no DAMAGE extension")
+        xd.XDamageCreate.restype = ctypes.c_ulong
+        xd.XDamageCreate.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+        xd.XDamageSubtract.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
+        xd.XDamageDestroy.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
+        xf.XFixesCreateRegion.restype = ctypes.c_ulong
+        xf.XFixesCreateRegion.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        xf.XFixesFetchRegion.restype = ctypes.POINTER(XRectangle)
+        xf.XFixesFetchRegion.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.POINTER(ctypes.c_int)]
+        xf.XFixesDestroyRegion.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
+        x11.XPending.argtypes = [ctypes.c_void_p]
+        x11.XNextEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        x11.XFree.argtypes = [ctypes.c_void_p]
+        self.xd, self.xf = xd, xf
+        self.damage = xd.XDamageCreate(dpy, root, XDamageReportNonEmpty)
+        self.region = xf.XFixesCreateRegion(dpy, None, 0)
+        self._event = ctypes.create_string_buffer(192)  # sizeof(XEvent)
+        self.full = True
+        self.polls = 0
+        self.rows_grabbed = 0
+
+    def invalidate(self) -> None:
+        self.full = True
+
+    def resize(self, height: int) -> None:
+        self.h = int(height)
+        self.full = True
+
+    def poll(self) -> list[tuple[int, int]]:
+        while self.x11.XPending(self.dpy):  # the notify events only say "non-empty": drop them
+            self.x11.XNextEvent(self.dpy, self._event)
+        self.xd.XDamageSubtract(self.dpy, self.damage, 0, self.region)  # clear; region <- damage
+        n = ctypes.c_int(0)
+        r = self.xf.XFixesFetchRegion(self.dpy, self.region, ctypes.byref(n))
+        rects = [(r[i].x, r[i].y, r[i].width, r[i].height) for i in range(n.value)] if r else []
+        if r:
+            self.x11.XFree(r)
+        self.polls += 1
+        if self.full:
+            self.full = False
+            bands = [(0, self.h)]
+        else:
+            bands = rects_to_bands(rects, self.h)
+        self.rows_grabbed += sum(b - a for a, b in bands)
+        return bands
+
+    def close(self) -> None:
+        self.xf.XFixesDestroyRegion(self.dpy, self.region)
+        self.xd.XDamageDestroy(self.dpy, self.damage)
+
+
 class XFixesCursorImage(ctypes.Structure):
     _fields_ = [("x", ctypes.c_short), ("y", ctypes.c_short), ("width", ctypes.c_ushort),
                 ("height", ctypes.c_ushort), ("xhot", ctypes.c_ushort), ("yhot", ctypes.c_ushort),
                 ("cursor_serial", ctypes.c_ulong), ("pixels", ctypes.POINTER(ctypes.c_ulong)),
                 ("atom", ctypes.c_ulong), ("name", ctypes.c_char_p)]
+
+
+def grab_bands(xext, dpy, root: int, img, shmaddr: int, pitch: int, bands) -> None:
+    """``XShmGetImage`` of row bands into one full-frame SHM image: the image's height and
+    data pointer are narrowed to the band (Xlib sends ``data - shmaddr`` as the segment
+    offset), then restored."""
+    c = img.contents
+    full_h, full_data = c.height, c.data
+    try:
+        for y0, y1 in bands:
+            c.height = int(y1 - y0)
+            c.data = shmaddr + int(y0) * pitch
+            if not xext.XShmGetImage(dpy, root, img, 0, int(y0), AllPlanes):
+                raise OSError(f"XShmGetImage failed for rows [{y0}, {y1})")
+    finally:
+        c.height, c.data = full_h, full_data
 
 
 def argb_longs_to_rgba(pixels: np.ndarray, width: int, height: int) -> np.ndarray:
@@ -80,10 +206,22 @@ class X11Capture:
         self.w = width or x.XDisplayWidth(self.dpy, scr)
         self.h = height or x.XDisplayHeight(self.dpy, scr)
         self.shm = None
+        self.damage: DamageTracker | None = None
         try:
             self._init_shm(scr)
         except OSError:
             self.shm = None
+
+    def enable_damage(self) -> bool:
+        """Track XDamage on the root window so ``grab_shm_damage`` grabs only changed row
+        bands; False (full-frame capture stays) without the DAMAGE extension or MIT-SHM."""
+        if self.shm is None:
+            return False
+        try:
+            self.damage = DamageTracker(self.x11, self.dpy, self.root, self.h)
+        except (OSError, AttributeError):
+            self.damage = None
+        return self.damage is not None
 
     def _init_shm(self, scr: int) -> None:
         xext = ctypes.CDLL(ctypes.util.find_library("Xext") or "libXext.so.6")
@@ -140,6 +278,8 @@ class X11Capture:
             self._init_shm(self.x11.XDefaultScreen(self.dpy))
         except OSError:
             self.shm = None
+        if self.damage is not None:
+            self.damage.resize(self.h)
 
     def cursor_image(self):
         """Current cursor as ``(serial, xhot, yhot, rgba)`` via XFixesGetCursorImage, or None
@@ -186,6 +326,17 @@ class X11Capture:
         if not self.xext.XShmGetImage(self.dpy, self.root, img, 0, 0, AllPlanes):
             raise OSError("XShmGetImage failed")
         return int(info.shmaddr), int(self.pitch)
+
+    def grab_shm_damage(self) -> tuple[int, int, list[tuple[int, int]]] | None:
+        """Damage-driven grab into the SHM segment: ``(address, pitch, bands)`` where only the
+        row bands ``[y0, y1)`` were copied by the X server (the rest of the segment still holds
+        the previous frame's pixels); None without SHM or damage tracking."""
+        if self.shm is None or self.damage is None:
+            return None
+        info, img, _ = self.shm
+        bands = self.damage.poll()  # subtract before grabbing: a racing change is re-reported
+        grab_bands(self.xext, self.dpy, self.root, img, int(info.shmaddr), self.pitch, bands)
+        return int(info.shmaddr), int(self.pitch), bands
 
     def grab(self) -> np.ndarray:
         """One frame as an (H, W, 4) uint8 BGRx array."""

@@ -313,7 +313,17 @@ class StreamPipeline:
                         log.warning("register_host_buffer failed (%s); using the staging copy", e)
                         shm = None
                         self.capture_zero_copy = False
-                if shm is not None and getattr(self, "capture_zero_copy", True):
+                dmg = getattr(self.capture, "damage", None) if shm is not None else None
+                if dmg is not None:
+                    # damage-driven: the X server copies and the GPU DMAs only the changed bands
+                    # (into the session's device-resident screen; its first frame is whole)
+                    if getattr(self, "_damage_sess", None) is not s:
+                        self._damage_sess = s  # new session (resize / restart): whole frame
+                        dmg.invalidate()
+                        s.invalidate_screen()
+                    addr, pitch, bands = self.capture.grab_shm_damage()
+                    s.submit_bgrx_damage(addr, pitch, shm[1] - (addr - shm[0]), bands, force_idr)
+                elif shm is not None and getattr(self, "capture_zero_copy", True):
                     addr, pitch = self.capture.grab_shm()
                     s.submit_bgrx_ptr(addr, pitch, shm[1] - (addr - shm[0]), force_idr)
                 else:

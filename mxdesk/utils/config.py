@@ -146,6 +146,8 @@ SCHEMA: list[Var] = [
     # ---- mxdesk options
     Var("gpu", ["MXDESK_GPU", "GPU_SELECT"], None, str, "GPU index / PCI bus id / unique id to use"),
     Var("source", ["MXDESK_SOURCE"], "auto", str, "frame source: synthetic | x11 | auto"),
+    Var("capture_damage", ["MXDESK_CAPTURE_DAMAGE"], True, bool,
+        "X11 capture driven by XDamage: grab and upload only the changed row bands"),
     Var("out_width", ["MXDESK_OUT_WIDTH"], 0, int, "encoded width (0 = SIZEW; else Lanczos scale)"),
     Var("out_height", ["MXDESK_OUT_HEIGHT"], 0, int, "encoded height (0 = SIZEH)"),
     Var("search_range", ["MXDESK_SEARCH_RANGE"], 16, int, "motion search radius (integer pels, <= 32)"),

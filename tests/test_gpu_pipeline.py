@@ -479,6 +479,56 @@ def test_zero_copy_registered_capture_matches_staged_upload(gpu):
         zc.submit_bgrx_ptr(buf.ctypes.data, pitch, pitch * (h - 1) + w * 4 - 1, False)
 
 
+@pytest.mark.parametrize("registered", [True, False])
+def test_damage_driven_capture_matches_full_upload(gpu, registered):
+    """Damage-driven capture (XDamage bands -> Session.submit_bgrx_damage): only the changed
+    row bands are read from host memory into the session's device-resident screen.  Rows
+    outside the bands are zeroed in the host buffer to prove they are never read; the access
+    units equal a session fed every whole frame."""
+    w, h, pitch = 320, 192, 320 * 4 + 256
+    rng = np.random.default_rng(11)
+    f0 = rng.integers(0, 256, (h, pitch), dtype=np.uint8)
+    f1 = f0.copy()
+    f1[48:96] = rng.integers(0, 256, (48, pitch), dtype=np.uint8)
+    f2 = f1.copy()
+    f2[0:16] = 7
+    f2[160:176] = 200
+    # (frame, damage bands): whole first frame, one band, nothing changed, two bands
+    seq = [(f0, [(0, h)]), (f1, [(48, 96)]), (f1, []), (f2, [(0, 16), (160, 176)])]
+
+    def session():
+        cfg = gpu.SessionConfig()
+        cfg.width, cfg.height, cfg.fps = w, h, 60
+        cfg.enc.bitrate_kbps = 0
+        cfg.enc.qp = 26
+        return gpu.Session(cfg)
+
+    full, dmg = session(), session()
+    buf = np.zeros((h, pitch), np.uint8)
+    if registered:
+        dmg.register_host_buffer(buf.ctypes.data, buf.nbytes)
+    for i, (f, bands) in enumerate(seq):
+        full.submit_bgrx(np.ascontiguousarray(f[:, : w * 4]).reshape(h, w, 4), False)
+        a = full.collect().au
+        buf[:] = 0
+        for y0, y1 in bands:
+            buf[y0:y1] = f[y0:y1]
+        dmg.submit_bgrx_damage(buf.ctypes.data, pitch, buf.nbytes, bands, False)
+        b = dmg.collect().au
+        assert a == b, f"frame {i}"
+    assert dmg.damage_bytes_uploaded == w * 4 * (h + 48 + 32)
+    # after invalidate_screen the next submit reads the whole frame again
+    dmg.invalidate_screen()
+    buf[:] = f2
+    dmg.submit_bgrx_damage(buf.ctypes.data, pitch, buf.nbytes, [], False)
+    dmg.collect()
+    assert dmg.damage_bytes_uploaded == w * 4 * (2 * h + 48 + 32)
+    with pytest.raises(ValueError):
+        dmg.submit_bgrx_damage(buf.ctypes.data, pitch, buf.nbytes, [(0, h + 16)], False)
+    with pytest.raises(ValueError):
+        dmg.submit_bgrx_damage(buf.ctypes.data, pitch, pitch * (h - 1), [], False)
+
+
 @pytest.mark.parametrize("codec", ["h264", "hevc"])
 def test_depth3_hevc_h264_match_depth1(gpu, codec):
     """Three frames in flight == one, constant QP, both codecs (eager and graph replay)."""

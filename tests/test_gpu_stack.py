@@ -282,3 +282,66 @@ def test_gpu_wall_two_processes_one_gpu():
     mask = np.ones_like(ref, bool)
     mask[8 + 8: 8 + 16, :] = False  # timestamp cells (capture time)
     assert np.array_equal(wall_y[mask], ref[mask])
+
+
+class _FakeCapture:
+    """A capture whose "SHM segment" is a numpy buffer; with ``damage`` it follows
+    X11Capture's damage-driven protocol (the segment's undamaged rows keep stale data)."""
+
+    def __init__(self, frames, w, h, damage):
+        self.frames, self.w, self.h, self.i = frames, w, h, 0
+        self.buf = np.zeros((h, w * 4), np.uint8)
+        if damage:
+            self.damage = self
+            self.full = True
+            self.bands_log = []
+
+    def invalidate(self):
+        self.full = True
+
+    def shm_buffer(self):
+        return (self.buf.ctypes.data, self.buf.nbytes) if hasattr(self, "damage") else None
+
+    def grab(self):
+        f = self.frames[self.i]
+        self.i += 1
+        return f.reshape(self.h, self.w, 4)
+
+    def grab_shm_damage(self):
+        f = self.frames[self.i]
+        prev = self.frames[self.i - 1] if self.i else None
+        self.i += 1
+        if self.full or prev is None:
+            bands, self.full = [(0, self.h)], False
+        else:
+            rows = np.nonzero((f != prev).any(axis=1))[0]
+            bands = [(int(rows.min()) // 16 * 16, min(self.h, (int(rows.max()) // 16 + 1) * 16))] if len(rows) else []
+        self.buf[:] = 0
+        for y0, y1 in bands:
+            self.buf[y0:y1] = f[y0:y1]
+        self.bands_log.append(bands)
+        return self.buf.ctypes.data, self.w * 4, bands
+
+
+def test_gpu_pipeline_damage_capture_matches_full_grab(gpu):
+    """StreamPipeline's damage-driven capture path (XDamage bands -> submit_bgrx_damage)
+    produces the same access units as full-frame grabs of the same screens."""
+    from mxdesk.pipeline.stream import StreamPipeline
+
+    w, h = 320, 192
+    rng = np.random.default_rng(5)
+    frames = [rng.integers(0, 256, (h, w * 4), dtype=np.uint8)]
+    for i in range(4):
+        f = frames[-1].copy()
+        if i != 1:  # frame 2 is unchanged (no bands)
+            f[20 * i + 10: 20 * i + 40, 40:200] = rng.integers(0, 256, (30, 160), dtype=np.uint8)
+        frames.append(f)
+    full = _FakeCapture(frames, w, h, damage=False)
+    dmg = _FakeCapture(frames, w, h, damage=True)
+    pa = StreamPipeline(w, h, 60, backend="gpu", bitrate_kbps=0, capture=full)
+    pb = StreamPipeline(w, h, 60, backend="gpu", bitrate_kbps=0, capture=dmg)
+    for i in range(len(frames)):
+        a, b = pa.step(), pb.step()
+        assert a.au == b.au, f"frame {i}"
+    assert dmg.bands_log[0] == [(0, h)] and dmg.bands_log[2] == []
+    assert pb._sess.damage_bytes_uploaded < len(frames) * w * h * 4 // 2
