@@ -240,6 +240,14 @@ class StreamPipeline:
         self.restarts = 0
         self.last_error: str | None = None
         self._fault = self._parse_fault(os.environ.get("MXDESK_FAULT", ""))
+        # damage-driven frame rate (captures with XDamage only): frames without damage after which
+        # production pauses (0: never), and the longest pause (MXDESK_IDLE_AFTER / _HEARTBEAT_S)
+        self.idle_after = int(os.environ.get("MXDESK_IDLE_AFTER", "") or 30)
+        self.idle_heartbeat_s = float(os.environ.get("MXDESK_IDLE_HEARTBEAT_S", "") or 1.0)
+        self.frames_idle = 0
+        self._static_frames = 0
+        self._idle_cursor = self._cursor
+        self._last_produced_t = 0.0
         self._make_session()
 
     # ------------------------------------------------------------------ session backends
@@ -289,7 +297,26 @@ class StreamPipeline:
         else:
             raise ValueError(f"unknown backend {self.backend}")
 
-    def _produce(self, force_idr: bool) -> EncodedFrame:
+    def _idle_skip(self, bands, force_idr: bool) -> bool:
+        """Damage-driven frame rate: after ``idle_after`` consecutive frames without damage
+        (the encoder has refined the still picture by then) no frame is produced until the
+        screen or the cursor changes, a key frame is asked for, or ``idle_heartbeat_s`` passed
+        since the last frame (receivers keep statistics and liveness).  An idle desktop then
+        costs no GPU work and no link bandwidth; receivers keep showing the last picture."""
+        cursor = self._cursor
+        if bands or force_idr or cursor != self._idle_cursor:
+            self._static_frames = 0
+            self._idle_cursor = cursor
+            return False
+        self._static_frames += 1
+        now = time.monotonic()
+        if (self.idle_after > 0 and self._static_frames > self.idle_after
+                and now - self._last_produced_t < self.idle_heartbeat_s):
+            self.frames_idle += 1
+            return True
+        return False
+
+    def _produce(self, force_idr: bool) -> EncodedFrame | None:
         from .. import native
 
         if self._pending_bitrate is not None:
@@ -322,6 +349,8 @@ class StreamPipeline:
                         dmg.invalidate()
                         s.invalidate_screen()
                     addr, pitch, bands = self.capture.grab_shm_damage()
+                    if self._idle_skip(bands, force_idr):
+                        return None
                     s.submit_bgrx_damage(addr, pitch, shm[1] - (addr - shm[0]), bands, force_idr)
                 elif shm is not None and getattr(self, "capture_zero_copy", True):
                     addr, pitch = self.capture.grab_shm()
@@ -405,8 +434,9 @@ class StreamPipeline:
             return len(self._subs)
 
     # ------------------------------------------------------------------ loop
-    def step(self) -> EncodedFrame:
-        """Produce one frame synchronously (no pacing); publishes to subscribers."""
+    def step(self) -> EncodedFrame | None:
+        """Produce one frame synchronously (no pacing); publishes to subscribers.  None when the
+        damage-driven capture reports an idle screen (``_idle_skip``)."""
         pending, self._pending_resize = self._pending_resize, None
         if pending is not None:
             self._apply_resize(*pending)
@@ -418,10 +448,13 @@ class StreamPipeline:
         if "stall" in self._fault and n == 3:
             time.sleep(self._fault.pop("stall"))
         fr = self._produce(force)
+        self.last_frame_t = time.monotonic()  # the loop is alive (also while idle)
+        if fr is None:  # idle: nothing changed on screen (damage-driven frame rate)
+            return None
+        self._last_produced_t = self.last_frame_t
         if fr.idr:
             self.keyframes.on_idr()
         self.frames_out += 1
-        self.last_frame_t = time.monotonic()
         self.metrics.on_frame(len(fr.au), (fr.t_encoded_us - fr.t_capture_us) / 1000.0, fr.gpu_ms, fr.qp, fr.idr)
         if "drop" in self._fault and self.frames_out % int(self._fault["drop"]) == 0:
             self.metrics.on_drop()
@@ -505,6 +538,7 @@ class StreamPipeline:
         return {"backend": self.backend, "device": self.device, "width": self.out_w, "height": self.out_h,
                 "fps": self.fps, "frames": self.frames_out, "clients": self.subscribers, "restarts": self.restarts,
                 "last_error": self.last_error, "resizes": self.resizes, "keyframes": self.keyframes.snapshot(),
+                "frames_idle": self.frames_idle,
                 **self.metrics.summary()}
 
 

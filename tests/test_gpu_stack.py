@@ -345,3 +345,31 @@ def test_gpu_pipeline_damage_capture_matches_full_grab(gpu):
         assert a.au == b.au, f"frame {i}"
     assert dmg.bands_log[0] == [(0, h)] and dmg.bands_log[2] == []
     assert pb._sess.damage_bytes_uploaded < len(frames) * w * h * 4 // 2
+
+
+def test_gpu_pipeline_damage_idle_screen_pauses_production(gpu, monkeypatch):
+    """Damage-driven frame rate: after MXDESK_IDLE_AFTER frames without damage the pipeline
+    produces nothing until the screen changes; the frames it does produce form one decodable
+    stream whose last picture is the changed screen."""
+    from mxdesk.models.synthetic import bgrx_to_nv12
+    from mxdesk.pipeline.stream import StreamPipeline
+
+    monkeypatch.setenv("MXDESK_IDLE_AFTER", "3")
+    w, h = 320, 192
+    rng = np.random.default_rng(8)
+    f0 = rng.integers(0, 256, (h, w * 4), dtype=np.uint8)
+    f1 = f0.copy()
+    f1[64:128, 64:256] = 30
+    frames = [f0] * 8 + [f1, f1]
+    cap = _FakeCapture(frames, w, h, damage=True)
+    pipe = StreamPipeline(w, h, 60, backend="gpu", bitrate_kbps=0, capture=cap)
+    out = [pipe.step() for _ in frames]
+    produced = [fr is not None for fr in out]
+    assert produced == [True, True, True, True, False, False, False, False, True, True], produced
+    assert pipe.frames_idle == 4 and pipe.status()["frames_idle"] == 4
+    stream = b"".join(fr.au for fr in out if fr is not None)
+    dec = Decoder().decode(stream)
+    assert len(dec) == 6
+    y_src, _ = bgrx_to_nv12(f1.reshape(h, w, 4))
+    err = dec[-1][0].astype(np.float64) - y_src.astype(np.float64)
+    assert 10 * np.log10(255 ** 2 / max(1e-9, float((err ** 2).mean()))) > 30

@@ -141,3 +141,31 @@ def test_capture_damage_grab_and_pipeline_fallbacks():
     fx.region_rects = [(3, 70, 2, 2)]
     assert cap.grab_shm_damage() == (0x20000, pitch, [(64, 80)])
     assert grabbed == [(0, 96), (64, 16)]
+
+
+def test_idle_skip_policy(monkeypatch):
+    """Damage-driven frame rate: production pauses after `idle_after` frames without damage and
+    resumes on damage, a cursor move, a key-frame request or the heartbeat."""
+    from mxdesk.pipeline import stream as S
+
+    now = [100.0]
+    monkeypatch.setattr(S.time, "monotonic", lambda: now[0])
+    p = S.StreamPipeline.__new__(S.StreamPipeline)
+    p.idle_after, p.idle_heartbeat_s, p.frames_idle = 3, 1.0, 0
+    p._static_frames, p._cursor, p._last_produced_t = 0, (-1, -1), 100.0
+    p._idle_cursor = p._cursor
+    assert [p._idle_skip([], False) for _ in range(5)] == [False, False, False, True, True]
+    assert p.frames_idle == 2
+    assert p._idle_skip([(0, 16)], False) is False  # damage resumes at once
+    assert [p._idle_skip([], False) for _ in range(4)] == [False, False, False, True]
+    assert p._idle_skip([], True) is False  # a key frame is always produced
+    p._static_frames = 10
+    p._cursor = (5, 5)
+    assert p._idle_skip([], False) is False  # the cursor moved (it is drawn into the picture)
+    p._static_frames = 10
+    now[0] = 101.5  # heartbeat: one frame per idle_heartbeat_s
+    assert p._idle_skip([], False) is False
+    p.idle_after = 0  # disabled
+    now[0] = 100.2
+    p._static_frames = 50
+    assert p._idle_skip([], False) is False
