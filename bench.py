@@ -663,9 +663,8 @@ def main() -> None:
             "device": args.device,
             "pipeline_depth": args.depth,
             "deblock": int(cfg.enc.deblock),
-            # -1 resolves per codec: H.264 / HEVC adaptive, VP8 off (csrc/codec/h264_encoder.h deblock)
-            "deblock_mode": {0: "off", 1: "on", 2: "adaptive"}.get(
-                int(cfg.enc.deblock), "off" if args.codec == "vp8" else "adaptive"),
+            # -1 resolves to adaptive for every codec (csrc/codec/h264_encoder.h deblock)
+            "deblock_mode": {0: "off", 1: "on", 2: "adaptive"}.get(int(cfg.enc.deblock), "adaptive"),
             "intra_in_p": int(cfg.enc.intra_in_p),
             "vp8_tools": {"bpred": int(cfg.enc.vp8_bpred), "intra": int(cfg.enc.vp8_intra)} if args.codec == "vp8" else None,
             "hevc_intra_split": int(cfg.enc.hevc_intra_split) if args.codec == "hevc" else None,

@@ -58,9 +58,10 @@ struct EncoderConfig {
     // HEVC adaptive (8.7.2 is fully parallel), H.264 adaptive (8.7 is a picture-wide wavefront,
     // k_deblock: on when at least a tenth of the picture moves coherently, where it gains 1.3 dB,
     // off on a mostly static desktop, where it gains 0.2 dB for -64 % single-session throughput;
-    // paced density is 200 sessions either way, profiles/r06_defaults/NOTES.md), VP8
-    // off (section 15 is the same raster-order chain, k_vp8_lf: +1.4 dB on motion content for
-    // -77 % throughput, profiles/r05_vp8/NOTES.md; 2 = adaptive, vp8_encoder.h LfDecision)
+    // paced density is 200 sessions either way, profiles/r06_defaults/NOTES.md), VP8 adaptive
+    // too (section 15 is the same raster-order chain, k_vp8_lf: the desktop stays unfiltered at
+    // the same rate, full-screen motion +0.8 dB for -15 % paced density / -74 % single-session
+    // throughput, profiles/r06_vp8db/NOTES.md; vp8_encoder.h LfDecision)
     int deblock = -1;
     // P pictures: also search 16x8 / 8x16 partitionings (two vectors per macroblock) and take one
     // when its SAD + lambda * vector rate beats the 16x16 vector's
@@ -78,7 +79,7 @@ struct EncoderConfig {
     // HEVC's default is adaptive: deblocking costs the still desktop 0.3 dB (its text regions
     // 4.5 dB) and gains 0.2 dB on motion content at 4K 18 Mbps (profiles/r05_hevc/NOTES.md)
     bool hevc_deblock_auto() const { return deblock == 2 || deblock < 0; }
-    int vp8_deblock_mode() const { return deblock == 1 || deblock == 2 ? deblock : 0; }  // off / on / adaptive
+    int vp8_deblock_mode() const { return deblock == 1 || deblock == 2 ? deblock : (deblock < 0 ? 2 : 0); }
     int intra_in_p = 0;       // H.264: P-slice macroblocks may be coded intra (open-loop cost decision); off by
                               // default: it costs -35 % fps on the 1080p desktop (k_intra_analyze + k_intra_p on
                               // the analysis queue, profiles/r04_toolset/NOTES.md)

@@ -159,7 +159,7 @@ MXV8 bool vp8_drop_residual(uint32_t lsad, long long d_pred, long long d_coded, 
 }
 MXV8 uint32_t vp8_block_bits(int nz) { return nz ? 2u + 6u * (uint32_t)nz : 0u; }
 
-// Loop-filter decision per frame (EncoderConfig::deblock: 0 or -1 (the VP8 default) off, 1 on, 2
+// Loop-filter decision per frame (EncoderConfig::deblock: 0 off, 1 on, 2 or -1 (the VP8 default)
 // adaptive).  Adaptive is the H.264 encoder's rule (h264_deblock.h db_auto_decide: filter when the
 // moving macroblocks move coherently -- pans, scrolls, video -- not for a still desktop, whose text
 // the filter only blurs) on the vectors of the inter frame kStatsLag frames back: the newest frame

@@ -230,14 +230,14 @@ def test_loop_filtered_inter_frames_decode_to_reconstruction(native, aq):
 
 def test_adaptive_loop_filter_follows_coherent_motion(native):
     """deblock 2 (adaptive): a still picture is never filtered; a pan switches the filter on
-    kStatsLag (4) frames after the first panned frame, and the bitstream says so.  (The default,
-    -1, is off: no frame filtered.)"""
+    kStatsLag (4) frames after the first panned frame, and the bitstream says so.  The default,
+    -1, is the same adaptive rule."""
     w, h = 192, 128
     base, uv0 = _picture(w + 64, h, 9)
 
-    def run(pan):
+    def run(pan, mode=2):
         c = native.EncoderConfig()
-        c.width, c.height, c.qp, c.bitrate_kbps, c.search_range, c.deblock = w, h, 32, 0, 16, 2
+        c.width, c.height, c.qp, c.bitrate_kbps, c.search_range, c.deblock = w, h, 32, 0, 16, mode
         enc = native.CpuVp8Encoder(c)
         frames = []
         for t in range(9):
@@ -259,6 +259,7 @@ def test_adaptive_loop_filter_follows_coherent_motion(native):
             assert filtered[:5] == [0] * 5 and filtered[5:] == [1] * 4, filtered
         else:
             assert sum(filtered) == want, filtered
+        assert run(pan, -1) == frames  # the default
 
 
 @pytest.mark.parametrize("qp", [20, 34, 46])
