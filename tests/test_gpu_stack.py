@@ -373,3 +373,43 @@ def test_gpu_pipeline_damage_idle_screen_pauses_production(gpu, monkeypatch):
     y_src, _ = bgrx_to_nv12(f1.reshape(h, w, 4))
     err = dec[-1][0].astype(np.float64) - y_src.astype(np.float64)
     assert 10 * np.log10(255 ** 2 / max(1e-9, float((err ** 2).mean()))) > 30
+
+
+def test_gpu_x11_capture_through_fake_server(gpu, monkeypatch):
+    """Real libX11 / libXext / libXdamage / libXfixes against tests/fake_xserver.py: MIT-SHM
+    capture registered for zero-copy DMA, XDamage bands, GPU encode; the decoded pictures are
+    the X framebuffer's, and a small change uploads only its band."""
+    import ctypes.util
+
+    if not all(ctypes.util.find_library(n) for n in ("X11", "Xext", "Xdamage", "Xfixes")):
+        pytest.skip("X client libraries not installed")
+    from mxdesk.models.synthetic import bgrx_to_nv12
+    from mxdesk.models.x11 import X11Capture
+    from mxdesk.pipeline.stream import StreamPipeline
+    from tests.fake_xserver import FakeXServer
+
+    monkeypatch.setenv("MXDESK_IDLE_AFTER", "2")
+    w, h = 320, 192
+    srv = FakeXServer(w, h)
+    try:
+        yy, xx = np.mgrid[0:h, 0:w]
+        srv.fb[..., 0] = (xx * 255 // w).astype(np.uint8)
+        srv.fb[..., 1] = (yy * 255 // h).astype(np.uint8)
+        srv.fb[..., 2] = 128
+        cap = X11Capture(srv.display)
+        assert cap.enable_damage()
+        pipe = StreamPipeline(w, h, 60, backend="gpu", bitrate_kbps=0, capture=cap)
+        out = [pipe.step() for _ in range(4)]  # IDR, 2 static frames, then idle
+        assert [f is not None for f in out] == [True, True, True, False]
+        srv.draw(40, 70, 100, 20, 240)
+        out.append(pipe.step())
+        assert out[-1] is not None
+        up = pipe._sess.damage_bytes_uploaded
+        assert up == w * 4 * (h + 32)  # the first frame + one 32-row band (rows 64..96)
+        frames = Decoder().decode(b"".join(f.au for f in out if f is not None))
+        assert len(frames) == 4
+        y_src, _ = bgrx_to_nv12(srv.fb)
+        err = frames[-1][0].astype(np.float64) - y_src.astype(np.float64)
+        assert 10 * np.log10(255 ** 2 / max(1e-9, float((err ** 2).mean()))) > 35
+    finally:
+        srv.close()
