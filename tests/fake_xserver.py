@@ -19,11 +19,14 @@ import threading
 
 import numpy as np
 
-SHM_OP, DAMAGE_OP, XFIXES_OP = 130, 131, 132
+SHM_OP, DAMAGE_OP, XFIXES_OP, XTEST_OP = 130, 131, 132, 133
 DAMAGE_EVENT = 90
 ROOT, VISUAL, COLORMAP = 0x100, 0x21, 0x20
 EXTENSIONS = {b"MIT-SHM": (SHM_OP, 0, 128), b"DAMAGE": (DAMAGE_OP, DAMAGE_EVENT, 140),
-              b"XFIXES": (XFIXES_OP, 100, 150)}
+              b"XFIXES": (XFIXES_OP, 100, 150), b"XTEST": (XTEST_OP, 0, 0)}
+# core keyboard map: keycode -> (unshifted, shifted) keysyms
+KEYMAP = {38: (0x61, 0x41), 36: (0xFF0D, 0), 50: (0xFFE1, 0), 9: (0xFF1B, 0)}
+MIN_KEYCODE, MAX_KEYCODE = 8, 255
 
 
 def _pad(n: int) -> int:
@@ -41,6 +44,8 @@ class FakeXServer:
         self.segments: dict[int, int] = {}  # shmseg -> attached address in this process
         self.requests: list[tuple[int, int]] = []  # (major, minor) of every request
         self.getimage_rows = 0
+        self.fake_inputs: list[tuple[int, int, int, int]] = []  # XTestFakeInput (type, detail, x, y)
+        self.cursor = None  # (xhot, yhot, serial, (h, w) uint32 ARGB) for XFixesGetCursorImage
         self.seq: dict[socket.socket, int] = {}  # last request sequence per connection (events carry it)
         self.libc = ctypes.CDLL("libc.so.6", use_errno=True)
         self.libc.shmat.restype = ctypes.c_void_p
@@ -120,7 +125,7 @@ class FakeXServer:
         screen = struct.pack("<IIIIIHHHHHHIBBBB", ROOT, COLORMAP, 0xFFFFFF, 0, 0, self.w, self.h, 300, 200, 1, 1,
                              VISUAL, 0, 0, 24, 1) + depth
         body = struct.pack("<IIIIHHBBBBBBBB4x", 1, 0x00400000, 0x001FFFFF, 0, len(vendor), 65535, 1, 2, 0, 0, 32, 32,
-                           8, 255)
+                           MIN_KEYCODE, MAX_KEYCODE)
         body += vendor + b"\0" * _pad(len(vendor)) + formats + screen
         return struct.pack("<BxHHH", 1, 11, 0, len(body) // 4) + body
 
@@ -167,6 +172,20 @@ class FakeXServer:
             return self._damage(c, data, body, seq)
         if op == XFIXES_OP:
             return self._xfixes(data, body, seq)
+        if op == XTEST_OP:
+            if data == 0:  # XTestGetVersion
+                return self._reply(seq, 2, struct.pack("<H", 2))
+            if data == 2:  # XTestFakeInput
+                typ, detail = body[0], body[1]
+                rx, ry = struct.unpack_from("<hh", body, 20) if typ == 6 else (0, 0)  # root x/y: motion only
+                self.fake_inputs.append((typ, detail, rx, ry))
+            return None
+        if op == 101:  # GetKeyboardMapping(first, count)
+            first, count = body[0], body[1]
+            syms = b"".join(struct.pack("<II", *KEYMAP.get(k, (0, 0))) for k in range(first, first + count))
+            return self._reply(seq, 2, b"", syms)
+        if op == 119:  # GetModifierMapping: one keycode per modifier, shift = 50
+            return self._reply(seq, 1, b"", struct.pack("<8B", 50, 0, 0, 0, 0, 0, 0, 0))
         return None  # requests without replies (or not modelled) are accepted silently
 
     def _shm(self, minor: int, body: bytes, seq: int) -> bytes | None:
@@ -225,6 +244,16 @@ class FakeXServer:
         if minor == 10:  # DestroyRegion
             self.regions.pop(struct.unpack_from("<I", body, 0)[0], None)
             return None
+        if minor in (4, 25) and self.cursor is not None:  # GetCursorImage (AndName)
+            xhot, yhot, serial, px = self.cursor
+            hh, ww = px.shape
+            head = struct.pack("<hhHHHHI", 10, 20, ww, hh, xhot, yhot, serial)
+            pixels = np.ascontiguousarray(px, np.uint32).tobytes()
+            if minor == 4:
+                return self._reply(seq, 0, head, pixels)
+            name = b"left_ptr"
+            head += struct.pack("<IHH", 0, len(name), 0)
+            return self._reply(seq, 0, head, pixels + name + b"\0" * _pad(len(name)))
         if minor == 19:  # FetchRegion -> extents + rectangles
             rects = self.regions.get(struct.unpack_from("<I", body, 0)[0], [])
             if rects:

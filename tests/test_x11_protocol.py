@@ -66,3 +66,39 @@ def test_damage_capture_grabs_only_changed_bands(xserver):
     assert np.array_equal(view[96:112], xserver.fb[96:112])
     assert not view[0:16].any()
     cap.damage.close()
+
+
+def test_xtest_injection_reaches_the_server(xserver):
+    """Browser input -> XTestInjector -> XTestFakeInput requests: absolute motion, button
+    press / release, wheel clicks and a key looked up through the core keyboard map."""
+    if not ctypes.util.find_library("Xtst"):
+        pytest.skip("libXtst not installed")
+    from mxdesk.server.input import InputEvent, XTestInjector
+
+    inj = XTestInjector(xserver.display)
+    inj.apply(InputEvent("mouse", x=100, y=50, buttons=1))
+    inj.apply(InputEvent("mouse", x=101, y=52, buttons=0, scroll=1))
+    inj.apply(InputEvent("key", keysym=0x61, down=True))
+    inj.apply(InputEvent("key", keysym=0x61, down=False))
+    inj.apply(InputEvent("key", keysym=0xFF0D, down=True))
+    inj.x11.XSync.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    inj.x11.XSync(inj.dpy, 0)
+    MOTION, BPRESS, BRELEASE, KPRESS, KRELEASE = 6, 4, 5, 2, 3
+    assert xserver.fake_inputs == [
+        (MOTION, 0, 100, 50), (BPRESS, 1, 0, 0),
+        (MOTION, 0, 101, 52), (BRELEASE, 1, 0, 0), (BPRESS, 4, 0, 0), (BRELEASE, 4, 0, 0),
+        (KPRESS, 38, 0, 0), (KRELEASE, 38, 0, 0), (KPRESS, 36, 0, 0)]
+
+
+def test_cursor_image_through_xfixes(xserver):
+    """X11Capture.cursor_image (remote cursors): XFixesGetCursorImage's premultiplied ARGB
+    through libXfixes -> straight RGBA."""
+    px = np.array([[0xFF102030, 0x80400000], [0x00000000, 0xFFFFFFFF]], np.uint32)
+    xserver.cursor = (1, 0, 7, px)
+    cap = X.X11Capture(xserver.display)
+    serial, xhot, yhot, rgba = cap.cursor_image()
+    assert (serial, xhot, yhot) == (7, 1, 0)
+    assert rgba.shape == (2, 2, 4)
+    assert rgba[0, 0].tolist() == [0x10, 0x20, 0x30, 255]
+    assert rgba[0, 1].tolist() == [0x80, 0, 0, 0x80]  # un-premultiplied
+    assert rgba[1, 0, 3] == 0 and rgba[1, 1].tolist() == [255, 255, 255, 255]
