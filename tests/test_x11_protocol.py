@@ -102,3 +102,28 @@ def test_cursor_image_through_xfixes(xserver):
     assert rgba[0, 0].tolist() == [0x10, 0x20, 0x30, 255]
     assert rgba[0, 1].tolist() == [0x80, 0, 0, 0x80]  # un-premultiplied
     assert rgba[1, 0, 3] == 0 and rgba[1, 1].tolist() == [255, 255, 255, 255]
+
+
+def test_serve_pipeline_captures_the_x_display(xserver):
+    """`mxdesk serve` wiring with MXDESK_SOURCE=x11: build_pipeline opens the display, turns on
+    XDamage (MXDESK_CAPTURE_DAMAGE) and the CPU encoder (x264enc) streams the X framebuffer."""
+    from mxdesk.cli import build_pipeline
+    from mxdesk.codec.h264_decoder import Decoder
+    from mxdesk.models.synthetic import bgrx_to_nv12
+    from mxdesk.utils import config as C
+
+    yy, xx = np.mgrid[0:192, 0:320]
+    xserver.fb[..., 0] = (xx * 255 // 320).astype(np.uint8)
+    xserver.fb[..., 1] = (yy * 255 // 192).astype(np.uint8)
+    xserver.fb[..., 2] = 90
+    cfg = C.load(env={"ENABLE_BASIC_AUTH": "false", "SIZEW": "320", "SIZEH": "192", "DISPLAY": xserver.display,
+                      "MXDESK_SOURCE": "x11", "WEBRTC_ENCODER": "x264enc"}, argv=[])
+    pipe = build_pipeline(cfg)
+    assert pipe.capture is not None and pipe.capture.damage is not None
+    xserver.draw(0, 0, 64, 64, 250)
+    stream = b"".join(pipe.step().au for _ in range(2))
+    frames = Decoder().decode(stream)
+    assert len(frames) == 2
+    y_src, _ = bgrx_to_nv12(xserver.fb)
+    err = frames[-1][0].astype(np.float64) - y_src.astype(np.float64)
+    assert 10 * np.log10(255 ** 2 / max(1e-9, float((err ** 2).mean()))) > 30
