@@ -47,6 +47,7 @@ class FakeXServer:
         self.fake_inputs: list[tuple[int, int, int, int]] = []  # XTestFakeInput (type, detail, x, y)
         self.cursor = None  # (xhot, yhot, serial, (h, w) uint32 ARGB) for XFixesGetCursorImage
         self.seq: dict[socket.socket, int] = {}  # last request sequence per connection (events carry it)
+        self.send_lock = threading.Lock()  # replies (server threads) and events (draw) never interleave
         self.libc = ctypes.CDLL("libc.so.6", use_errno=True)
         self.libc.shmat.restype = ctypes.c_void_p
         self.libc.shmat.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
@@ -81,7 +82,8 @@ class FakeXServer:
             ev = struct.pack("<BBHIIIhhHHhhHH", DAMAGE_EVENT, 3, self.seq.get(conn, 0), ROOT, did, 0, x, y, w, h, 0, 0,
                              self.w, self.h)
             try:
-                conn.sendall(ev)
+                with self.send_lock:
+                    conn.sendall(ev)
             except OSError:
                 pass
 
@@ -136,7 +138,8 @@ class FakeXServer:
                 return  # little-endian clients only
             n_name, n_data = struct.unpack_from("<HH", hdr, 6)
             self._recv(c, n_name + _pad(n_name) + n_data + _pad(n_data))
-            c.sendall(self._setup_reply())
+            with self.send_lock:
+                c.sendall(self._setup_reply())
             seq = 0
             while True:
                 h = self._recv(c, 4)
@@ -147,7 +150,8 @@ class FakeXServer:
                 self.requests.append((op, data))
                 reply = self._handle(c, op, data, body, seq)
                 if reply:
-                    c.sendall(reply)
+                    with self.send_lock:
+                        c.sendall(reply)
         except (EOFError, OSError):
             pass
 
