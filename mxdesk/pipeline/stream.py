@@ -313,6 +313,7 @@ class StreamPipeline:
         if (self.idle_after > 0 and self._static_frames > self.idle_after
                 and now - self._last_produced_t < self.idle_heartbeat_s):
             self.frames_idle += 1
+            self.metrics.on_idle()
             return True
         return False
 
@@ -349,6 +350,7 @@ class StreamPipeline:
                         dmg.invalidate()
                         s.invalidate_screen()
                     addr, pitch, bands = self.capture.grab_shm_damage()
+                    self.metrics.on_capture_rows(sum(y1 - y0 for y0, y1 in bands))
                     if self._idle_skip(bands, force_idr):
                         return None
                     s.submit_bgrx_damage(addr, pitch, shm[1] - (addr - shm[0]), bands, force_idr)

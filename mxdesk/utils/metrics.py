@@ -60,6 +60,10 @@ class SessionMetrics:
         self.kf_coalesced = Counter("mxdesk_keyframe_requests_coalesced", "Keyframe requests that joined a pending "
                                     "or just-coded IDR (or waited out a viewer's backoff)", lab,
                                     registry=self.registry)
+        self.idle = Counter("mxdesk_idle_frames", "Frame ticks not encoded because the screen did not change "
+                            "(damage-driven capture)", lab, registry=self.registry)
+        self.capture_rows = Counter("mxdesk_capture_rows", "Screen rows grabbed and uploaded by the damage-driven "
+                                    "capture", lab, registry=self.registry)
         self.qp = Gauge("mxdesk_qp", "Current QP", lab, registry=self.registry)
         self.bitrate = Gauge("mxdesk_bitrate_kbps", "Measured bitrate (kbps, 1 s window)", lab,
                              registry=self.registry)
@@ -101,6 +105,12 @@ class SessionMetrics:
         self.kf_requests.labels(self.session, reason).inc()
         if coalesced:
             self.kf_coalesced.labels(self.session).inc()
+
+    def on_idle(self) -> None:
+        self.idle.labels(self.session).inc()
+
+    def on_capture_rows(self, n: int) -> None:
+        self.capture_rows.labels(self.session).inc(n)
 
     def on_drop(self, n: int = 1) -> None:
         self.dropped.labels(self.session).inc(n)

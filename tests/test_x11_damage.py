@@ -150,12 +150,16 @@ def test_idle_skip_policy(monkeypatch):
 
     now = [100.0]
     monkeypatch.setattr(S.time, "monotonic", lambda: now[0])
+    from mxdesk.utils.metrics import SessionMetrics
+
     p = S.StreamPipeline.__new__(S.StreamPipeline)
+    p.metrics = SessionMetrics("t")
     p.idle_after, p.idle_heartbeat_s, p.frames_idle = 3, 1.0, 0
     p._static_frames, p._cursor, p._last_produced_t = 0, (-1, -1), 100.0
     p._idle_cursor = p._cursor
     assert [p._idle_skip([], False) for _ in range(5)] == [False, False, False, True, True]
     assert p.frames_idle == 2
+    assert p.metrics.idle.labels("t")._value.get() == 2  # /metrics mxdesk_idle_frames_total
     assert p._idle_skip([(0, 16)], False) is False  # damage resumes at once
     assert [p._idle_skip([], False) for _ in range(4)] == [False, False, False, True]
     assert p._idle_skip([], True) is False  # a key frame is always produced
