@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import ctypes.util
+import threading
 
 import numpy as np
 
@@ -198,6 +199,9 @@ class X11Capture:
                                 ctypes.c_uint, ctypes.c_ulong, ctypes.c_int]
         x.XDestroyImage = getattr(x, "XDestroyImage", None)
         self.display_name = display
+        # one connection shared by the pipeline thread and the RFB server's executor thread: Xlib
+        # is not thread-safe (no XInitThreads), so every request sequence holds this lock
+        self._lock = threading.RLock()
         self.dpy = x.XOpenDisplay(display.encode())
         if not self.dpy:
             raise OSError(f"cannot open X display {display}")
@@ -218,7 +222,8 @@ class X11Capture:
         if self.shm is None:
             return False
         try:
-            self.damage = DamageTracker(self.x11, self.dpy, self.root, self.h)
+            with self._lock:
+                self.damage = DamageTracker(self.x11, self.dpy, self.root, self.h)
         except (OSError, AttributeError):
             self.damage = None
         return self.damage is not None
@@ -272,6 +277,10 @@ class X11Capture:
 
     def resize(self, width: int, height: int) -> None:
         """Re-create the capture image after the screen changed size (RandR resize)."""
+        with self._lock:
+            self._resize_locked(width, height)
+
+    def _resize_locked(self, width: int, height: int) -> None:
         self._release_shm()
         self.w, self.h = int(width), int(height)
         try:
@@ -323,8 +332,9 @@ class X11Capture:
         if self.shm is None:
             return None
         info, img, _ = self.shm
-        if not self.xext.XShmGetImage(self.dpy, self.root, img, 0, 0, AllPlanes):
-            raise OSError("XShmGetImage failed")
+        with self._lock:
+            if not self.xext.XShmGetImage(self.dpy, self.root, img, 0, 0, AllPlanes):
+                raise OSError("XShmGetImage failed")
         return int(info.shmaddr), int(self.pitch)
 
     def grab_shm_damage(self) -> tuple[int, int, list[tuple[int, int]]] | None:
@@ -334,18 +344,23 @@ class X11Capture:
         if self.shm is None or self.damage is None:
             return None
         info, img, _ = self.shm
-        bands = self.damage.poll()  # subtract before grabbing: a racing change is re-reported
-        grab_bands(self.xext, self.dpy, self.root, img, int(info.shmaddr), self.pitch, bands)
+        with self._lock:
+            bands = self.damage.poll()  # subtract before grabbing: a racing change is re-reported
+            grab_bands(self.xext, self.dpy, self.root, img, int(info.shmaddr), self.pitch, bands)
         return int(info.shmaddr), int(self.pitch), bands
 
     def grab(self) -> np.ndarray:
-        """One frame as an (H, W, 4) uint8 BGRx array."""
+        """One frame as an (H, W, 4) uint8 BGRx array (a copy: the SHM segment is rewritten by
+        the next grab, possibly from another thread).  It does not consume XDamage: a full grab
+        only makes the segment newer, and the damage stays pending for ``grab_shm_damage``."""
         if self.shm is not None:
             info, img, size = self.shm
-            if not self.xext.XShmGetImage(self.dpy, self.root, img, 0, 0, AllPlanes):
-                raise OSError("XShmGetImage failed")
-            return self.view.reshape(self.h, self.pitch)[:, : self.w * 4].reshape(self.h, self.w, 4)
-        img = self.x11.XGetImage(self.dpy, self.root, 0, 0, self.w, self.h, AllPlanes, ZPixmap)
+            with self._lock:
+                if not self.xext.XShmGetImage(self.dpy, self.root, img, 0, 0, AllPlanes):
+                    raise OSError("XShmGetImage failed")
+                return self.view.reshape(self.h, self.pitch)[:, : self.w * 4].reshape(self.h, self.w, 4).copy()
+        with self._lock:
+            img = self.x11.XGetImage(self.dpy, self.root, 0, 0, self.w, self.h, AllPlanes, ZPixmap)
         if not img:
             raise OSError("XGetImage failed")
         bpl = img.contents.bytes_per_line

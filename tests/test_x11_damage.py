@@ -126,8 +126,10 @@ def test_grab_bands_narrows_and_restores_the_image():
 def test_capture_damage_grab_and_pipeline_fallbacks():
     """X11Capture.grab_shm_damage returns (addr, pitch, bands); without SHM enable_damage is
     False and the pipeline keeps the full-frame path."""
+    import threading
+
     cap = X.X11Capture.__new__(X.X11Capture)
-    cap.shm, cap.damage = None, None
+    cap.shm, cap.damage, cap._lock = None, None, threading.RLock()
     assert cap.enable_damage() is False and cap.grab_shm_damage() is None
     fx = FakeX()
     cap.damage = fx.tracker(96)

@@ -127,3 +127,40 @@ def test_serve_pipeline_captures_the_x_display(xserver):
     y_src, _ = bgrx_to_nv12(xserver.fb)
     err = frames[-1][0].astype(np.float64) - y_src.astype(np.float64)
     assert 10 * np.log10(255 ** 2 / max(1e-9, float((err ** 2).mean()))) > 30
+
+
+def test_full_grab_from_another_thread_keeps_damage_pending(xserver):
+    """The RFB server grabs whole frames from its executor thread on the same connection as
+    the pipeline's damage polls: those grabs are serialised with the polls, return copies and
+    never consume damage, so the video path still uploads every changed band."""
+    import threading
+
+    cap = X.X11Capture(xserver.display)
+    assert cap.enable_damage()
+    cap.grab_shm_damage()
+    xserver.draw(0, 40, 50, 10, 123)
+    stop = threading.Event()
+    errors = []
+
+    def rfb_like():
+        try:
+            while not stop.is_set():
+                f = cap.grab()
+                assert f.shape == (192, 320, 4)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    t = threading.Thread(target=rfb_like)
+    t.start()
+    try:
+        f = cap.grab()
+        assert np.array_equal(f, xserver.fb)
+        assert not np.shares_memory(f, cap.view)  # a copy, not the live segment
+        bands = []
+        for _ in range(20):
+            bands += cap.grab_shm_damage()[2]
+    finally:
+        stop.set()
+        t.join()
+    assert not errors
+    assert bands == [(32, 64)]  # reported exactly once, to the damage path
