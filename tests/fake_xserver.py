@@ -53,11 +53,13 @@ class FakeXServer:
         self.libc.shmat.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         self.libc.shmdt.argtypes = [ctypes.c_void_p]
         self.sock = None
-        for n in range(40, 90):
+        for n in range(40, 140):
+            # no SO_REUSEADDR: with it two processes (pytest-xdist workers) could both bind a port
+            # before either listens, and the second listen() would fail; busy ports are skipped
             s = socket.socket()
-            s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             try:
                 s.bind(("127.0.0.1", 6000 + n))
+                s.listen(4)
             except OSError:
                 s.close()
                 continue
@@ -65,7 +67,6 @@ class FakeXServer:
             break
         if self.sock is None:
             raise OSError("no free X display port")
-        self.sock.listen(4)
         self.conns: list[socket.socket] = []
         self._stop = False
         self.thread = threading.Thread(target=self._accept, daemon=True)
